@@ -1,0 +1,57 @@
+// C ABI of the gfx950 kernel launchers (implemented in *.hip, used by binding.cpp).
+// Every launcher is asynchronous on the given stream, allocates nothing and never
+// synchronises, so callers may capture it into a hipGraph.
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+extern "C" {
+// sampling.hip
+hipError_t eh_rng_advance(int64_t* state, int64_t inc, hipStream_t s);
+hipError_t eh_sample_neighbor(const int64_t* indptr, const int32_t* nbr, const float* cumw, int64_t num_rows,
+                              int num_types, uint32_t type_mask, const void* nodes, int nodes_is64, int64_t n,
+                              int count, int32_t default_row, const int64_t* rng, uint64_t stream_id, int32_t* out,
+                              float* out_w, int32_t* out_t, hipStream_t s);
+hipError_t eh_alias_sample(const float* prob, const int32_t* alias, const int32_t* rows, int64_t pop, int64_t count,
+                           const int64_t* rng, uint64_t stream_id, int32_t* out, hipStream_t s);
+hipError_t eh_random_walk(const int64_t* indptr, const int32_t* nbr, const float* cumw, int64_t num_rows,
+                          int num_types, const uint32_t* step_masks, const int32_t* starts, int64_t n, int walk_len,
+                          int32_t default_row, const int64_t* rng, uint64_t stream_id, int32_t* out, hipStream_t s);
+hipError_t eh_synth_degree(int64_t n, float avg_deg, int max_deg, uint64_t seed, int64_t* deg, hipStream_t s);
+hipError_t eh_synth_fill(int64_t n, const int64_t* indptr, uint64_t seed, int32_t* nbr, float* cumw, hipStream_t s);
+
+// sage.hip
+hipError_t eh_sage_fwd(const void* x, int D, const int32_t* self_idx, const int32_t* nbr_idx, int F,
+                       int include_self, float inv_cnt, const void* W, const float* bias, int H, int64_t M, void* out,
+                       void* a_save, int relu, hipStream_t s);
+hipError_t eh_linear_fwd(const void* A, int K, const void* W, const float* bias, int H, int64_t M, void* out,
+                         int relu, hipStream_t s);
+hipError_t eh_sage_bwd_scatter(const void* dA, int D, const int32_t* self_idx, const int32_t* nbr_idx, int F,
+                               int include_self, float inv_cnt, int64_t M, int disjoint, float* dx, hipStream_t s);
+hipError_t eh_relu_bwd(void* g, const void* y, int64_t n, hipStream_t s);
+
+// mp.hip
+hipError_t eh_gather_rows(const void* x, int64_t n_rows, int64_t row_bytes, const void* idx, int idx_is64, int64_t n,
+                          void* out, hipStream_t s);
+hipError_t eh_segment_reduce(const void* src, int is_bf16, int D, const int64_t* indptr, const int64_t* perm,
+                             int64_t S, int op, float empty_val, void* out, int64_t* argmax, hipStream_t s);
+hipError_t eh_index_add_rows(const void* src, int is_bf16, int D, const int64_t* idx, int64_t n, float* out,
+                             int64_t n_out, hipStream_t s);
+hipError_t eh_max_bwd(const void* gout, int is_bf16, const int64_t* argmax, int64_t S, int D, void* gsrc,
+                      hipStream_t s);
+hipError_t eh_edge_softmax(const void* logits, int is_bf16, int H, const int64_t* indptr, const int64_t* perm,
+                           int64_t S, void* out, hipStream_t s);
+hipError_t eh_edge_softmax_bwd(const void* p, const void* g, int is_bf16, int H, const int64_t* indptr,
+                               const int64_t* perm, int64_t S, void* gin, hipStream_t s);
+hipError_t eh_spmm_csr(const int64_t* indptr, const int64_t* col, const float* w, const void* x, int is_bf16, int D,
+                       int64_t S, void* out, hipStream_t s);
+}
+
+extern "C" {
+// optim.hip
+hipError_t eh_flat_optim(float* p, const float* g, float* m, float* v, int64_t n, int64_t* step, float lr, float b1,
+                         float b2, float eps, float wd, float grad_scale, int kind, hipStream_t s);
+hipError_t eh_sparse_optim(float* table, float* m, float* v, const int64_t* rows, const float* grads, int64_t n, int D,
+                           int64_t n_rows, int64_t* step, float lr, float b1, float b2, float eps, int kind,
+                           hipStream_t s);
+}

@@ -1,0 +1,321 @@
+// Message-passing primitives:
+//   gather_rows      out[e]  = x[idx[e]]                         (K1; idx < 0 -> zero row)
+//   segment_reduce   out[s]  = reduce_{e in seg s} src[perm[e]]  (K2; sum | mean | max + argmax)
+//   index_add_rows   out[idx[e]] += src[e]                       (atomic fp32, gather backward)
+//   scatter_rows     out[idx[e]]  = src[e]                       (max backward, unique positions)
+//   edge_softmax     per-destination online softmax over [E, H] logits (K5)
+//
+// Segments come from a CSR over *destination* indices built once per block
+// (sorted by destination), so sum/mean/max are deterministic and atomic-free
+// (reference used tf.tensor_scatter_add / a serial loop: mp_ops.py:27-79,
+// tf_euler/kernels/scatter_op.cc:27-105).
+#include "hip/common.h"
+
+namespace euler_hip {
+
+// rows are moved in 16-byte vectors when possible, else 4-byte words
+template <int VB>  // vector bytes: 16 or 4
+struct Vec;
+template <>
+struct Vec<16> { using T = uint4_t; };
+template <>
+struct Vec<4> { using T = uint32_t; };
+
+template <int VB, typename IdxT>
+__global__ __launch_bounds__(256) void gather_rows_kernel(const uint8_t* __restrict__ x, int64_t n_rows,
+                                                          int64_t row_bytes, const IdxT* __restrict__ idx,
+                                                          int64_t n, uint8_t* __restrict__ out) {
+  using V = typename Vec<VB>::T;
+  const int64_t vpr = row_bytes / VB;
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= n * vpr) return;
+  const int64_t e = t / vpr, c = t - e * vpr;
+  const int64_t r = static_cast<int64_t>(idx[e]);
+  V v{};
+  if (r >= 0 && r < n_rows) v = reinterpret_cast<const V*>(x + r * row_bytes)[c];
+  reinterpret_cast<V*>(out + e * row_bytes)[c] = v;
+}
+
+template <typename T>
+__device__ __forceinline__ float ld(const T* p);
+template <>
+__device__ __forceinline__ float ld<float>(const float* p) { return *p; }
+template <>
+__device__ __forceinline__ float ld<bf16_t>(const bf16_t* p) { return bf2f(*p); }
+template <typename T>
+__device__ __forceinline__ void st(T* p, float v);
+template <>
+__device__ __forceinline__ void st<float>(float* p, float v) { *p = v; }
+template <>
+__device__ __forceinline__ void st<bf16_t>(bf16_t* p, float v) { *p = f2bf(v); }
+
+// op: 0 sum, 1 mean, 2 max.  One thread per (segment, 4-column group).
+template <typename T>
+__global__ __launch_bounds__(256) void segment_reduce_kernel(const T* __restrict__ src, int D,
+                                                             const int64_t* __restrict__ indptr,
+                                                             const int64_t* __restrict__ perm, int64_t S, int op,
+                                                             float empty_val, T* __restrict__ out,
+                                                             int64_t* __restrict__ argmax) {
+  const int groups = (D + 3) / 4;
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= S * groups) return;
+  const int64_t s = t / groups;
+  const int d0 = static_cast<int>(t - s * groups) * 4;
+  const int nd = min(4, D - d0);
+  const int64_t a = indptr[s], b = indptr[s + 1];
+  float acc[4];
+  int64_t am[4] = {-1, -1, -1, -1};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = op == 2 ? -INFINITY : 0.f;
+  for (int64_t e = a; e < b; ++e) {
+    const int64_t row = perm ? perm[e] : e;
+    const T* p = src + row * D + d0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i < nd) {
+        const float v = ld<T>(p + i);
+        if (op == 2) {
+          if (v > acc[i]) { acc[i] = v; am[i] = row; }
+        } else {
+          acc[i] += v;
+        }
+      }
+    }
+  }
+  const float inv = (op == 1 && b > a) ? 1.f / static_cast<float>(b - a) : 1.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (i < nd) {
+      float v = acc[i] * inv;
+      if (b == a) v = (op == 2) ? empty_val : 0.f;
+      st<T>(out + s * D + d0 + i, v);
+      if (argmax) argmax[s * D + d0 + i] = am[i];
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void index_add_rows_kernel(const T* __restrict__ src, int D,
+                                                             const int64_t* __restrict__ idx, int64_t n,
+                                                             float* __restrict__ out, int64_t n_out) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= n * D) return;
+  const int64_t e = t / D;
+  const int d = static_cast<int>(t - e * D);
+  const int64_t r = idx[e];
+  if (r < 0 || r >= n_out) return;
+  atomicAdd(out + r * D + d, ld<T>(src + t));
+}
+
+// max backward: grad_src[argmax[s,d], d] = grad_out[s,d]  (argmax positions are unique)
+template <typename T>
+__global__ __launch_bounds__(256) void max_bwd_kernel(const T* __restrict__ gout, const int64_t* __restrict__ argmax,
+                                                      int64_t S, int D, T* __restrict__ gsrc) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= S * D) return;
+  const int64_t r = argmax[t];
+  if (r < 0) return;
+  const int d = static_cast<int>(t % D);
+  gsrc[r * D + d] = gout[t];
+}
+
+// ---------------------------------------------------------------------------
+// K5: edge softmax over destination segments, H heads packed per edge.
+//   logits [E, H] (edge order = perm over destination CSR), out [E, H]
+// One thread per (segment, head): online max / sum-exp in a single pass, then
+// a normalising pass (two reads of the segment's logits, one write).
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void edge_softmax_kernel(const T* __restrict__ logits, int H,
+                                                           const int64_t* __restrict__ indptr,
+                                                           const int64_t* __restrict__ perm, int64_t S,
+                                                           T* __restrict__ out) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= S * H) return;
+  const int64_t s = t / H;
+  const int h = static_cast<int>(t - s * H);
+  const int64_t a = indptr[s], b = indptr[s + 1];
+  float m = -INFINITY, l = 0.f;
+  for (int64_t e = a; e < b; ++e) {
+    const int64_t row = perm ? perm[e] : e;
+    const float v = ld<T>(logits + row * H + h);
+    const float nm = fmaxf(m, v);
+    l = l * __expf(m - nm) + __expf(v - nm);
+    m = nm;
+  }
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  for (int64_t e = a; e < b; ++e) {
+    const int64_t row = perm ? perm[e] : e;
+    st<T>(out + row * H + h, __expf(ld<T>(logits + row * H + h) - m) * inv);
+  }
+}
+
+// softmax backward: g_in = p * (g - sum_seg(p * g))
+template <typename T>
+__global__ __launch_bounds__(256) void edge_softmax_bwd_kernel(const T* __restrict__ p, const T* __restrict__ g,
+                                                               int H, const int64_t* __restrict__ indptr,
+                                                               const int64_t* __restrict__ perm, int64_t S,
+                                                               T* __restrict__ gin) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= S * H) return;
+  const int64_t s = t / H;
+  const int h = static_cast<int>(t - s * H);
+  const int64_t a = indptr[s], b = indptr[s + 1];
+  float dot = 0.f;
+  for (int64_t e = a; e < b; ++e) {
+    const int64_t row = perm ? perm[e] : e;
+    dot += ld<T>(p + row * H + h) * ld<T>(g + row * H + h);
+  }
+  for (int64_t e = a; e < b; ++e) {
+    const int64_t row = perm ? perm[e] : e;
+    const float pv = ld<T>(p + row * H + h);
+    st<T>(gin + row * H + h, pv * (ld<T>(g + row * H + h) - dot));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K4: CSR SpMM  out[s, :] = sum_{e in seg s} w[e] * x[col[e], :]  (row-split, one
+// thread per (row, 4-column group), fp32 accumulation).  x may be bf16 or fp32.
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void spmm_csr_kernel(const int64_t* __restrict__ indptr,
+                                                       const int64_t* __restrict__ col,
+                                                       const float* __restrict__ w, const T* __restrict__ x, int D,
+                                                       int64_t S, T* __restrict__ out) {
+  const int groups = (D + 3) / 4;
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= S * groups) return;
+  const int64_t s = t / groups;
+  const int d0 = static_cast<int>(t - s * groups) * 4;
+  const int nd = min(4, D - d0);
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t e = indptr[s]; e < indptr[s + 1]; ++e) {
+    const int64_t c = col[e];
+    if (c < 0) continue;
+    const float we = w ? w[e] : 1.f;
+    const T* p = x + c * D + d0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (i < nd) acc[i] += we * ld<T>(p + i);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (i < nd) st<T>(out + s * D + d0 + i, acc[i]);
+}
+
+}  // namespace euler_hip
+
+using namespace euler_hip;
+
+extern "C" {
+
+hipError_t eh_gather_rows(const void* x, int64_t n_rows, int64_t row_bytes, const void* idx, int idx_is64, int64_t n,
+                          void* out, hipStream_t s) {
+  if (n == 0 || row_bytes == 0) return hipSuccess;
+  const bool v16 = (row_bytes % 16 == 0) && (reinterpret_cast<uintptr_t>(x) % 16 == 0) &&
+                   (reinterpret_cast<uintptr_t>(out) % 16 == 0);
+  if (!v16 && row_bytes % 4 != 0) return hipErrorInvalidValue;
+  const int vb = v16 ? 16 : 4;
+  const int64_t total = n * (row_bytes / vb);
+  const dim3 grid(static_cast<uint32_t>(ceil_div(total, 256)));
+  const uint8_t* xb = static_cast<const uint8_t*>(x);
+  uint8_t* ob = static_cast<uint8_t*>(out);
+  if (v16) {
+    if (idx_is64)
+      hipLaunchKernelGGL((gather_rows_kernel<16, int64_t>), grid, dim3(256), 0, s, xb, n_rows, row_bytes,
+                         static_cast<const int64_t*>(idx), n, ob);
+    else
+      hipLaunchKernelGGL((gather_rows_kernel<16, int32_t>), grid, dim3(256), 0, s, xb, n_rows, row_bytes,
+                         static_cast<const int32_t*>(idx), n, ob);
+  } else {
+    if (idx_is64)
+      hipLaunchKernelGGL((gather_rows_kernel<4, int64_t>), grid, dim3(256), 0, s, xb, n_rows, row_bytes,
+                         static_cast<const int64_t*>(idx), n, ob);
+    else
+      hipLaunchKernelGGL((gather_rows_kernel<4, int32_t>), grid, dim3(256), 0, s, xb, n_rows, row_bytes,
+                         static_cast<const int32_t*>(idx), n, ob);
+  }
+  return hipGetLastError();
+}
+
+
+hipError_t eh_segment_reduce(const void* src, int is_bf16, int D, const int64_t* indptr, const int64_t* perm,
+                             int64_t S, int op, float empty_val, void* out, int64_t* argmax, hipStream_t s) {
+  if (S == 0 || D == 0) return hipSuccess;
+  const int64_t total = S * ((D + 3) / 4);
+  const dim3 grid(static_cast<uint32_t>(ceil_div(total, 256)));
+  if (is_bf16)
+    hipLaunchKernelGGL(segment_reduce_kernel<bf16_t>, grid, dim3(256), 0, s, static_cast<const bf16_t*>(src), D,
+                       indptr, perm, S, op, empty_val, static_cast<bf16_t*>(out), argmax);
+  else
+    hipLaunchKernelGGL(segment_reduce_kernel<float>, grid, dim3(256), 0, s, static_cast<const float*>(src), D,
+                       indptr, perm, S, op, empty_val, static_cast<float*>(out), argmax);
+  return hipGetLastError();
+}
+
+hipError_t eh_index_add_rows(const void* src, int is_bf16, int D, const int64_t* idx, int64_t n, float* out,
+                             int64_t n_out, hipStream_t s) {
+  if (n == 0 || D == 0) return hipSuccess;
+  const dim3 grid(static_cast<uint32_t>(ceil_div(n * D, 256)));
+  if (is_bf16)
+    hipLaunchKernelGGL(index_add_rows_kernel<bf16_t>, grid, dim3(256), 0, s, static_cast<const bf16_t*>(src), D, idx,
+                       n, out, n_out);
+  else
+    hipLaunchKernelGGL(index_add_rows_kernel<float>, grid, dim3(256), 0, s, static_cast<const float*>(src), D, idx, n,
+                       out, n_out);
+  return hipGetLastError();
+}
+
+hipError_t eh_max_bwd(const void* gout, int is_bf16, const int64_t* argmax, int64_t S, int D, void* gsrc,
+                      hipStream_t s) {
+  if (S == 0 || D == 0) return hipSuccess;
+  const dim3 grid(static_cast<uint32_t>(ceil_div(S * D, 256)));
+  if (is_bf16)
+    hipLaunchKernelGGL(max_bwd_kernel<bf16_t>, grid, dim3(256), 0, s, static_cast<const bf16_t*>(gout), argmax, S, D,
+                       static_cast<bf16_t*>(gsrc));
+  else
+    hipLaunchKernelGGL(max_bwd_kernel<float>, grid, dim3(256), 0, s, static_cast<const float*>(gout), argmax, S, D,
+                       static_cast<float*>(gsrc));
+  return hipGetLastError();
+}
+
+hipError_t eh_edge_softmax(const void* logits, int is_bf16, int H, const int64_t* indptr, const int64_t* perm,
+                           int64_t S, void* out, hipStream_t s) {
+  if (S == 0 || H == 0) return hipSuccess;
+  const dim3 grid(static_cast<uint32_t>(ceil_div(S * H, 256)));
+  if (is_bf16)
+    hipLaunchKernelGGL(edge_softmax_kernel<bf16_t>, grid, dim3(256), 0, s, static_cast<const bf16_t*>(logits), H,
+                       indptr, perm, S, static_cast<bf16_t*>(out));
+  else
+    hipLaunchKernelGGL(edge_softmax_kernel<float>, grid, dim3(256), 0, s, static_cast<const float*>(logits), H,
+                       indptr, perm, S, static_cast<float*>(out));
+  return hipGetLastError();
+}
+
+hipError_t eh_edge_softmax_bwd(const void* p, const void* g, int is_bf16, int H, const int64_t* indptr,
+                               const int64_t* perm, int64_t S, void* gin, hipStream_t s) {
+  if (S == 0 || H == 0) return hipSuccess;
+  const dim3 grid(static_cast<uint32_t>(ceil_div(S * H, 256)));
+  if (is_bf16)
+    hipLaunchKernelGGL(edge_softmax_bwd_kernel<bf16_t>, grid, dim3(256), 0, s, static_cast<const bf16_t*>(p),
+                       static_cast<const bf16_t*>(g), H, indptr, perm, S, static_cast<bf16_t*>(gin));
+  else
+    hipLaunchKernelGGL(edge_softmax_bwd_kernel<float>, grid, dim3(256), 0, s, static_cast<const float*>(p),
+                       static_cast<const float*>(g), H, indptr, perm, S, static_cast<float*>(gin));
+  return hipGetLastError();
+}
+
+hipError_t eh_spmm_csr(const int64_t* indptr, const int64_t* col, const float* w, const void* x, int is_bf16, int D,
+                       int64_t S, void* out, hipStream_t s) {
+  if (S == 0 || D == 0) return hipSuccess;
+  const dim3 grid(static_cast<uint32_t>(ceil_div(S * ((D + 3) / 4), 256)));
+  if (is_bf16)
+    hipLaunchKernelGGL(spmm_csr_kernel<bf16_t>, grid, dim3(256), 0, s, indptr, col, w,
+                       static_cast<const bf16_t*>(x), D, S, static_cast<bf16_t*>(out));
+  else
+    hipLaunchKernelGGL(spmm_csr_kernel<float>, grid, dim3(256), 0, s, indptr, col, w, static_cast<const float*>(x), D,
+                       S, static_cast<float*>(out));
+  return hipGetLastError();
+}
+
+}  // extern "C"

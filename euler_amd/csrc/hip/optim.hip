@@ -1,0 +1,100 @@
+// Optimizer kernels.
+//   flat_adam   : one launch updates every dense parameter of a model whose params
+//                 live in one flat fp32 buffer (FlatParams); the step count is a
+//                 device scalar so the update is hipGraph-replay safe.
+//   sparse_adam : row-sparse Adam/Adagrad on the rows of an embedding shard that
+//                 received gradients (ids already de-duplicated by the caller).
+// Reference optimizers: tf_euler/python/utils/optimizers.py:22-31 (sgd, momentum,
+// adagrad, adam); embedding stores: utils/embedding.py:24-68.
+#include "hip/common.h"
+
+namespace euler_hip {
+
+// kind: 0 adam, 1 adagrad, 2 sgd, 3 momentum
+__global__ __launch_bounds__(256) void flat_optim_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                         float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                         const int64_t* __restrict__ step, float lr, float b1,
+                                                         float b2, float eps, float wd, float grad_scale, int kind) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float gi = g[i] * grad_scale + wd * p[i];
+  if (kind == 0) {
+    const float t = static_cast<float>(step[0]);
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float bc1 = 1.f - __powf(b1, t), bc2 = 1.f - __powf(b2, t);
+    p[i] -= lr * (mi / bc1) / (sqrtf(vi / bc2) + eps);
+  } else if (kind == 1) {
+    const float acc = v[i] + gi * gi;
+    v[i] = acc;
+    p[i] -= lr * gi / (sqrtf(acc) + eps);
+  } else if (kind == 2) {
+    p[i] -= lr * gi;
+  } else {
+    const float mi = b1 * m[i] + gi;
+    m[i] = mi;
+    p[i] -= lr * mi;
+  }
+}
+
+__global__ void step_inc_kernel(int64_t* step) { step[0] += 1; }
+
+// rows: unique row ids (int64) into the table, grads [n, D] fp32
+__global__ __launch_bounds__(256) void sparse_optim_kernel(float* __restrict__ table, float* __restrict__ m,
+                                                           float* __restrict__ v, const int64_t* __restrict__ rows,
+                                                           const float* __restrict__ grads, int64_t n, int D,
+                                                           int64_t n_rows, const int64_t* __restrict__ step, float lr,
+                                                           float b1, float b2, float eps, int kind) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= n * D) return;
+  const int64_t e = t / D;
+  const int d = static_cast<int>(t - e * D);
+  const int64_t r = rows[e];
+  if (r < 0 || r >= n_rows) return;
+  const int64_t o = r * D + d;
+  const float gi = grads[t];
+  if (kind == 0) {
+    const float st = static_cast<float>(step[0]);
+    const float mi = b1 * m[o] + (1.f - b1) * gi;
+    const float vi = b2 * v[o] + (1.f - b2) * gi * gi;
+    m[o] = mi;
+    v[o] = vi;
+    const float bc1 = 1.f - __powf(b1, st), bc2 = 1.f - __powf(b2, st);
+    table[o] -= lr * (mi / bc1) / (sqrtf(vi / bc2) + eps);
+  } else if (kind == 1) {
+    const float acc = v[o] + gi * gi;
+    v[o] = acc;
+    table[o] -= lr * gi / (sqrtf(acc) + eps);
+  } else {
+    table[o] -= lr * gi;
+  }
+}
+
+}  // namespace euler_hip
+
+using namespace euler_hip;
+
+extern "C" {
+
+hipError_t eh_flat_optim(float* p, const float* g, float* m, float* v, int64_t n, int64_t* step, float lr, float b1,
+                         float b2, float eps, float wd, float grad_scale, int kind, hipStream_t s) {
+  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, s, step);
+  if (n == 0) return hipGetLastError();
+  hipLaunchKernelGGL(flat_optim_kernel, dim3(static_cast<uint32_t>(ceil_div(n, 256))), dim3(256), 0, s, p, g, m, v, n,
+                     step, lr, b1, b2, eps, wd, grad_scale, kind);
+  return hipGetLastError();
+}
+
+hipError_t eh_sparse_optim(float* table, float* m, float* v, const int64_t* rows, const float* grads, int64_t n, int D,
+                           int64_t n_rows, int64_t* step, float lr, float b1, float b2, float eps, int kind,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, s, step);
+  if (n == 0 || D == 0) return hipGetLastError();
+  hipLaunchKernelGGL(sparse_optim_kernel, dim3(static_cast<uint32_t>(ceil_div(n * D, 256))), dim3(256), 0, s, table,
+                     m, v, rows, grads, n, D, n_rows, step, lr, b1, b2, eps, kind);
+  return hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,247 @@
+"""HBM-resident graph shard with GPU-side sampling.
+
+An MI355X has 288 GB of HBM: a 100M-node / 1B-edge weighted graph (CSR with int32
+neighbor rows + fp32 cumulative weights ~ 8.8 GB) plus 100M x 128 bf16 features
+(25.6 GB) fits on every GPU with room to spare.  Keeping the shard resident lets
+neighbor sampling run as gfx950 kernels next to the model instead of streaming
+sampled ids over PCIe each step (SURVEY §7.4 "possibly GPU-side sampling from an
+HBM-resident CSR ... decide by measurement").
+
+Semantics are the engine's (``csrc/graph``): per (row, edge type) segments with
+inclusive prefix-sum weights; a neighbor draw picks an edge-type group by its
+weight sum, then binary-searches the group (reference ``node.cc:98-161``); empty
+rows yield ``default`` (reference ``sample_neighbor_op.cc:37-145``).  Rows are
+dense 0..N-1; ``ids`` (optional) maps rows back to raw uint64 node ids.
+
+Randomness: Philox counter-based, keyed by a device-resident ``(seed, counter)``
+pair.  Each call site passes a distinct ``stream_id`` and ``advance()`` bumps the
+counter on the GPU, so a captured hipGraph replays with fresh samples.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from euler_amd.ops._native import hip, use_hip
+
+__all__ = ["DeviceGraph", "build_alias_table"]
+
+
+def build_alias_table(weights: np.ndarray):
+    """Vose alias table (reference ``euler/common/alias_method.cc:23-70``), vectorised."""
+    w = np.asarray(weights, dtype=np.float64)
+    n = w.shape[0]
+    if n == 0:
+        return np.zeros(0, np.float32), np.zeros(0, np.int32)
+    total = w.sum()
+    if total <= 0:
+        w = np.ones(n)
+        total = float(n)
+    p = w * (n / total)
+    prob = np.ones(n, dtype=np.float64)
+    alias = np.arange(n, dtype=np.int64)
+    if np.allclose(p, 1.0):
+        return prob.astype(np.float32), alias.astype(np.int32)
+    small = list(np.nonzero(p < 1.0)[0])
+    large = list(np.nonzero(p >= 1.0)[0])
+    p = p.copy()
+    while small and large:
+        s = small.pop()
+        l = large[-1]
+        prob[s] = p[s]
+        alias[s] = l
+        p[l] = p[l] - (1.0 - p[s])
+        if p[l] < 1.0:
+            large.pop()
+            small.append(l)
+    for i in small + large:
+        prob[i] = 1.0
+    return prob.astype(np.float32), alias.astype(np.int32)
+
+
+class DeviceGraph:
+    def __init__(self, indptr, nbr, cumw, num_types=1, node_prob=None, node_alias=None, ids=None,
+                 seed: int = 0, device=None):
+        device = torch.device(device) if device is not None else indptr.device
+        self.device = device
+        self.indptr = indptr.to(device=device, dtype=torch.int64).contiguous()
+        self.nbr = nbr.to(device=device, dtype=torch.int32).contiguous()
+        self.cumw = cumw.to(device=device, dtype=torch.float32).contiguous()
+        self.num_types = int(num_types)
+        self.num_rows = (self.indptr.numel() - 1) // self.num_types
+        assert self.indptr.numel() == self.num_rows * self.num_types + 1, "indptr must be [N*T+1]"
+        if node_prob is None:
+            node_prob = torch.ones(self.num_rows, dtype=torch.float32)
+            node_alias = torch.arange(self.num_rows, dtype=torch.int32)
+        self.node_prob = torch.as_tensor(node_prob, dtype=torch.float32).to(device).contiguous()
+        self.node_alias = torch.as_tensor(node_alias, dtype=torch.int32).to(device).contiguous()
+        self.ids = ids
+        self.rng = torch.tensor([int(seed), 0], dtype=torch.int64, device=device)
+        self._cpu_gen = torch.Generator(device="cpu")
+        self._cpu_gen.manual_seed(int(seed))
+
+    # ------------------------------------------------------------------ construction
+    @classmethod
+    def synthetic(cls, num_nodes: int, avg_degree: float = 10.0, max_degree: int = 2048, seed: int = 0,
+                  device="cuda"):
+        """Power-law random graph generated directly in HBM (GPU) or with torch (CPU)."""
+        device = torch.device(device)
+        if device.type == "cuda":
+            indptr, nbr, cumw = hip().synth_csr(int(num_nodes), float(avg_degree), int(max_degree), int(seed),
+                                               device.index if device.index is not None else
+                                               torch.cuda.current_device())
+        else:
+            indptr, nbr, cumw = _synth_cpu(int(num_nodes), float(avg_degree), int(max_degree), int(seed))
+        return cls(indptr, nbr, cumw, 1, seed=seed, device=device)
+
+    @classmethod
+    def from_csr(cls, indptr, nbr, weights, num_types=1, node_weights=None, ids=None, seed=0, device="cuda"):
+        """From host CSR arrays with *raw* edge weights (prefix sums computed here per segment)."""
+        indptr_t = torch.as_tensor(np.asarray(indptr), dtype=torch.int64)
+        w = torch.as_tensor(np.asarray(weights), dtype=torch.float64)
+        cs = torch.cumsum(w, 0)
+        seg_start = torch.repeat_interleave(indptr_t[:-1], torch.diff(indptr_t))
+        base = torch.cat([torch.zeros(1, dtype=torch.float64), cs])[seg_start]
+        cumw = (cs - base).float()
+        prob = alias = None
+        if node_weights is not None:
+            prob, alias = build_alias_table(np.asarray(node_weights))
+            prob, alias = torch.from_numpy(prob), torch.from_numpy(alias)
+        return cls(indptr_t, torch.as_tensor(np.asarray(nbr), dtype=torch.int32), cumw, num_types, prob, alias,
+                   ids, seed, device)
+
+    # ------------------------------------------------------------------ randomness
+    def advance(self, inc: int = 1):
+        """Bump the device-side Philox counter (once per training step)."""
+        if use_hip(self.rng):
+            hip().rng_advance(self.rng, int(inc))
+        else:
+            self.rng[1] += inc
+
+    def manual_seed(self, seed: int):
+        self.rng.fill_(0)
+        self.rng[0] = int(seed)
+        self._cpu_gen.manual_seed(int(seed))
+
+    def _mask(self, edge_types) -> int:
+        if edge_types is None:
+            return (1 << self.num_types) - 1
+        m = 0
+        for t in ([edge_types] if isinstance(edge_types, int) else edge_types):
+            m |= 1 << int(t)
+        return m
+
+    # ------------------------------------------------------------------ sampling
+    def sample_node(self, count: int, stream_id: int = 1) -> torch.Tensor:
+        if use_hip(self.node_prob):
+            return hip().alias_sample(self.node_prob, self.node_alias, None, int(count), self.rng, int(stream_id))
+        n = self.num_rows
+        k = torch.randint(0, n, (count,), generator=self._cpu_gen)
+        u = torch.rand(count, generator=self._cpu_gen)
+        pick = torch.where(u < self.node_prob[k], k, self.node_alias[k].long())
+        return pick.int()
+
+    def sample_neighbor(self, rows: torch.Tensor, count: int, edge_types=None, default: int = -1,
+                        stream_id: int = 2, with_weights: bool = False):
+        rows = rows.reshape(-1)
+        if use_hip(self.indptr, rows):
+            res = hip().sample_neighbor(self.indptr, self.nbr, self.cumw, self.num_rows, self.num_types,
+                                        self._mask(edge_types), rows.contiguous(), int(count), int(default),
+                                        self.rng, int(stream_id), bool(with_weights))
+            return tuple(res) if with_weights else res[0]
+        return self._sample_neighbor_cpu(rows, count, self._mask(edge_types), default, with_weights)
+
+    def _sample_neighbor_cpu(self, rows, count, mask, default, with_weights):
+        n = rows.numel()
+        T = self.num_types
+        r = rows.long()
+        valid = (r >= 0) & (r < self.num_rows)
+        rc = torch.where(valid, r, torch.zeros_like(r))
+        base = rc * T
+        starts = torch.stack([self.indptr[base + t] for t in range(T)], 1)
+        ends = torch.stack([self.indptr[base + t + 1] for t in range(T)], 1)
+        tot = torch.where(ends > starts, self.cumw[(ends - 1).clamp(min=0)], torch.zeros(()))
+        sel = torch.tensor([(mask >> t) & 1 for t in range(T)], dtype=torch.bool)
+        tot = tot * sel.unsqueeze(0)
+        out = torch.full((n, count), default, dtype=torch.int32)
+        wout = torch.zeros((n, count), dtype=torch.float32)
+        tout = torch.full((n, count), -1, dtype=torch.int32)
+        cum_t = torch.cumsum(tot, 1)
+        ttot = cum_t[:, -1]
+        ok = valid & (ttot > 0)
+        if count > 0 and bool(ok.any()):
+            u1 = torch.rand((n, count), generator=self._cpu_gen) * ttot.unsqueeze(1)
+            t = torch.searchsorted(cum_t.contiguous(), u1.contiguous(), right=True).clamp(max=T - 1)
+            s = torch.gather(starts, 1, t)
+            e = torch.gather(ends, 1, t)
+            g = torch.gather(tot, 1, t)
+            u2 = torch.rand((n, count), generator=self._cpu_gen) * g
+            # binary search per draw inside [s, e)
+            lo, hi = s.clone(), (e - 1).clamp(min=0)
+            for _ in range(64):
+                act = lo < hi
+                if not bool(act.any()):
+                    break
+                mid = (lo + hi) // 2
+                go_left = self.cumw[mid] > u2
+                hi = torch.where(act & go_left, mid, hi)
+                lo = torch.where(act & ~go_left, mid + 1, lo)
+            pos = lo
+            okm = ok.unsqueeze(1).expand(n, count)
+            out = torch.where(okm, self.nbr[pos], out)
+            prev = torch.where(pos > s, self.cumw[(pos - 1).clamp(min=0)], torch.zeros(()))
+            wout = torch.where(okm, self.cumw[pos] - prev, wout)
+            tout = torch.where(okm, t.int(), tout)
+        if with_weights:
+            return out, wout, tout
+        return out
+
+    def random_walk(self, starts: torch.Tensor, walk_len: int, edge_types=None, default: int = -1,
+                    stream_id: int = 3) -> torch.Tensor:
+        starts = starts.reshape(-1).int()
+        masks = torch.tensor([self._mask(edge_types)] * int(walk_len), dtype=torch.int64)
+        masks = ((masks + 2 ** 31) % 2 ** 32 - 2 ** 31).int()
+        if use_hip(self.indptr, starts):
+            return hip().random_walk(self.indptr, self.nbr, self.cumw, self.num_rows, self.num_types,
+                                     masks.to(self.device), starts.contiguous(), int(default), self.rng,
+                                     int(stream_id))
+        cols = [starts]
+        cur = starts
+        for _ in range(int(walk_len)):
+            cur = self._sample_neighbor_cpu(cur, 1, self._mask(edge_types), default, False).reshape(-1)
+            cols.append(cur)
+        return torch.stack(cols, 1)
+
+    def degree(self, rows: torch.Tensor) -> torch.Tensor:
+        r = rows.long()
+        return self.indptr[(r + 1) * self.num_types] - self.indptr[r * self.num_types]
+
+    @property
+    def num_edges(self) -> int:
+        return int(self.nbr.numel())
+
+    def nbytes(self) -> int:
+        return sum(t.numel() * t.element_size() for t in (self.indptr, self.nbr, self.cumw, self.node_prob,
+                                                           self.node_alias))
+
+
+def _synth_cpu(n: int, avg_deg: float, max_deg: int, seed: int):
+    """CPU twin of the device generator (same distribution family, not bitwise)."""
+    g = torch.Generator().manual_seed(seed)
+    u = torch.rand(n, generator=g).clamp(min=1e-7)
+    deg = (avg_deg * 0.5 / torch.sqrt(u)).long().clamp(1, max_deg)
+    indptr = torch.zeros(n + 1, dtype=torch.int64)
+    torch.cumsum(deg, 0, out=indptr[1:])
+    e = int(indptr[-1])
+    src = torch.repeat_interleave(torch.arange(n), deg)
+    nbr = torch.randint(0, n, (e,), generator=g)
+    nbr = torch.where(nbr == src, (nbr + 1) % n, nbr)
+    # sort neighbors inside each row
+    key = src * n + nbr
+    order = torch.argsort(key)
+    nbr = nbr[order]
+    w = 0.5 + torch.rand(e, generator=g)
+    cs = torch.cumsum(w.double(), 0)
+    base = torch.cat([torch.zeros(1, dtype=torch.float64), cs])[indptr[:-1]]
+    cumw = (cs - torch.repeat_interleave(base, deg)).float()
+    return indptr, nbr.int(), cumw

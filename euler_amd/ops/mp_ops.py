@@ -1,0 +1,226 @@
+"""Message-passing ops: ``gather`` and ``scatter_{add,mean,max,softmax}``.
+
+Same names and semantics as the reference's ``tf_euler.python.euler_ops.mp_ops``
+(``/root/reference/tf_euler/python/euler_ops/mp_ops.py:27-79``):
+
+* ``gather(params, indices)``                 -> ``params[indices]``
+* ``scatter_add(updates, indices, size)``     -> segment sum into ``size`` rows
+* ``scatter_mean``                            -> segment mean (empty rows = 0)
+* ``scatter_max``                             -> segment max (empty rows = 0; reference
+  initialises with -1e9 and the TF op keeps that for empty rows, we clamp to 0 to
+  match ``scatter_`` usage in convs)
+* ``scatter_softmax(logits, indices, size)``  -> per-destination softmax
+
+On GPU tensors every op runs a hand-written gfx950 kernel (``csrc/hip/mp.hip``):
+destinations are turned into a CSR once (``SegmentIndex``, cached on the dataflow
+block) and reduced deterministically without atomics; gradients are exact
+(argmax routing for max, p*(g - <p,g>) for softmax).  CPU tensors use the
+pure-torch reference path, which is also the numerics oracle in tests.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from euler_amd.ops._native import hip, use_hip
+
+__all__ = ["SegmentIndex", "gather", "scatter_add", "scatter_mean", "scatter_max", "scatter_softmax",
+           "scatter_", "segment_index"]
+
+
+class SegmentIndex:
+    """Destination CSR for a fixed ``(indices, size)`` pair.
+
+    ``perm`` orders edges by destination (stable), ``indptr[s]:indptr[s+1]``
+    delimits the edges of destination ``s``.  Built lazily on first use and
+    reused by every scatter over the same edges (forward and backward).
+    """
+
+    __slots__ = ("indices", "size", "_perm", "_indptr", "_counts")
+
+    def __init__(self, indices: torch.Tensor, size: int):
+        self.indices = indices.reshape(-1).long()
+        self.size = int(size)
+        self._perm = None
+        self._indptr = None
+        self._counts = None
+
+    def _build(self):
+        # padding destinations (< 0) go to a sentinel segment past the end
+        idx = torch.where(self.indices < 0, torch.full_like(self.indices, self.size), self.indices)
+        self._perm = torch.argsort(idx, stable=True)
+        counts = torch.bincount(idx, minlength=self.size + 1)[: self.size]
+        self._counts = counts
+        indptr = torch.zeros(self.size + 1, dtype=torch.long, device=idx.device)
+        torch.cumsum(counts, 0, out=indptr[1:])
+        self._indptr = indptr
+
+    @property
+    def perm(self):
+        if self._perm is None:
+            self._build()
+        return self._perm
+
+    @property
+    def indptr(self):
+        if self._indptr is None:
+            self._build()
+        return self._indptr
+
+    @property
+    def counts(self):
+        if self._counts is None:
+            self._build()
+        return self._counts
+
+
+def segment_index(indices, size) -> SegmentIndex:
+    if isinstance(indices, SegmentIndex):
+        return indices
+    return SegmentIndex(indices, size)
+
+
+def _deterministic() -> bool:
+    return os.environ.get("EULER_AMD_DETERMINISTIC", "0") == "1" or torch.are_deterministic_algorithms_enabled()
+
+
+# ----------------------------------------------------------------------------- gather
+class _Gather(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, params, indices):
+        ctx.n = params.shape[0]
+        ctx.save_for_backward(indices)
+        return hip().gather_rows(params.contiguous(), indices.contiguous())
+
+    @staticmethod
+    def backward(ctx, g):
+        (indices,) = ctx.saved_tensors
+        g = g.contiguous()
+        g2 = g.reshape(g.shape[0], -1)
+        idx = indices.reshape(-1).long()
+        if _deterministic():
+            seg = SegmentIndex(idx, ctx.n)
+            out = hip().segment_reduce(g2, seg.indptr, seg.perm, 0, 0.0)[0]
+        else:
+            acc = torch.zeros((ctx.n, g2.shape[1]), dtype=torch.float32, device=g.device)
+            hip().index_add_rows_(acc, idx, g2)
+            out = acc.to(g.dtype)
+        return out.reshape((ctx.n,) + tuple(g.shape[1:])), None
+
+
+def gather(params: torch.Tensor, indices: torch.Tensor) -> torch.Tensor:
+    """``params[indices]`` along dim 0 (reference ``mp_ops.gather``)."""
+    if use_hip(params, indices) and params.dim() >= 1 and params.is_floating_point():
+        idx = indices.reshape(-1)
+        if idx.dtype not in (torch.int32, torch.int64):
+            idx = idx.long()
+        out = _Gather.apply(params, idx)
+        return out.reshape(tuple(indices.shape) + tuple(params.shape[1:]))
+    return params[indices.long()]
+
+
+# ----------------------------------------------------------------------------- scatter
+class _SegmentReduce(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, src, seg, op):
+        shape = src.shape
+        s2 = src.contiguous().reshape(shape[0], -1)
+        res = hip().segment_reduce(s2, seg.indptr, seg.perm, op, 0.0)
+        ctx.op, ctx.seg, ctx.shape = op, seg, shape
+        if op == 2:
+            ctx.save_for_backward(res[1])
+        return res[0].reshape((seg.size,) + tuple(shape[1:]))
+
+    @staticmethod
+    def backward(ctx, g):
+        seg, op, shape = ctx.seg, ctx.op, ctx.shape
+        g2 = g.contiguous().reshape(seg.size, -1)
+        if op == 2:
+            (am,) = ctx.saved_tensors
+            gs = hip().max_bwd(g2, am, shape[0])
+        else:
+            if op == 1:
+                cnt = seg.counts.clamp(min=1).to(g2.dtype).unsqueeze(1)
+                g2 = g2 / cnt
+            # gather_rows yields zero rows for negative (padding) destinations
+            gs = hip().gather_rows(g2.contiguous(), seg.indices)
+        return gs.reshape(shape), None, None
+
+
+def _cpu_scatter(src, idx, size, reduce):
+    idx = idx.reshape(-1).long()
+    out_shape = (size,) + tuple(src.shape[1:])
+    if reduce == "max":
+        out = torch.full(out_shape, float("-inf"), dtype=src.dtype, device=src.device)
+        ex = idx.view(-1, *([1] * (src.dim() - 1))).expand_as(src)
+        out = out.scatter_reduce(0, ex, src, reduce="amax", include_self=True)
+        return torch.where(torch.isinf(out), torch.zeros_like(out), out)
+    out = torch.zeros(out_shape, dtype=src.dtype, device=src.device)
+    out = out.index_add(0, idx, src)
+    if reduce == "mean":
+        cnt = torch.bincount(idx, minlength=size)[:size].clamp(min=1).to(src.dtype)
+        out = out / cnt.view(-1, *([1] * (src.dim() - 1)))
+    return out
+
+
+def _scatter(src, indices, size, reduce):
+    if size is None:
+        size = int(indices.max().item()) + 1 if indices.numel() else 0
+    if isinstance(size, torch.Tensor):
+        size = int(size.item())
+    if use_hip(src) and src.is_floating_point() and src.dtype in (torch.float32, torch.bfloat16):
+        seg = segment_index(indices, size)
+        op = {"add": 0, "sum": 0, "mean": 1, "max": 2}[reduce]
+        return _SegmentReduce.apply(src, seg, op)
+    idx = indices.indices if isinstance(indices, SegmentIndex) else indices
+    return _cpu_scatter(src, idx, size, reduce)
+
+
+def scatter_add(updates, indices, size=None):
+    return _scatter(updates, indices, size, "add")
+
+
+def scatter_mean(updates, indices, size=None):
+    return _scatter(updates, indices, size, "mean")
+
+
+def scatter_max(updates, indices, size=None):
+    return _scatter(updates, indices, size, "max")
+
+
+def scatter_(op, updates, indices, size=None):
+    """Dispatch by name, like the reference's ``mp_ops.scatter_`` (``add|mean|max``)."""
+    assert op in ("add", "mean", "max")
+    return _scatter(updates, indices, size, op)
+
+
+class _EdgeSoftmax(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, seg):
+        shape = logits.shape
+        l2 = logits.contiguous().reshape(shape[0], -1)
+        p = hip().edge_softmax(l2, seg.indptr, seg.perm)
+        ctx.seg, ctx.shape = seg, shape
+        ctx.save_for_backward(p)
+        return p.reshape(shape)
+
+    @staticmethod
+    def backward(ctx, g):
+        (p,) = ctx.saved_tensors
+        g2 = g.contiguous().reshape(p.shape).to(p.dtype)
+        gin = hip().edge_softmax_bwd(p, g2, ctx.seg.indptr, ctx.seg.perm)
+        return gin.reshape(ctx.shape), None
+
+
+def scatter_softmax(logits, indices, size=None):
+    """Softmax of ``logits`` grouped by destination ``indices`` (reference mp_ops.py:76-79)."""
+    if size is None:
+        size = int(indices.max().item()) + 1 if indices.numel() else 0
+    if use_hip(logits) and logits.dtype in (torch.float32, torch.bfloat16):
+        return _EdgeSoftmax.apply(logits, segment_index(indices, size))
+    idx = indices.indices if isinstance(indices, SegmentIndex) else indices.reshape(-1).long()
+    mx = _cpu_scatter(logits.detach(), idx, size, "max")
+    z = torch.exp(logits - mx[idx])
+    den = _cpu_scatter(z, idx, size, "add")
+    return z / den[idx]
