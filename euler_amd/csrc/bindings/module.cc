@@ -1,0 +1,461 @@
+// pybind11 module `euler_amd._engine`: the C++ graph engine as seen from Python.
+// Plays the role of the reference's C ABI + TF custom ops (SURVEY §2.1 N25,
+// tf_euler/utils/init_query_proxy.cc, euler/service/python_api.cc): numpy in,
+// numpy out, the GIL released around every engine call.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "framework/framework.h"
+#include "gql/gql.h"
+#include "graph/graph.h"
+#include "index/index.h"
+#include "rpc/rpc.h"
+
+namespace py = pybind11;
+using namespace euler;
+
+namespace {
+
+void Throw(const Status& st) {
+  if (!st.ok()) throw std::runtime_error(st.message());
+}
+
+// ------------------------------------------------------------------ numpy <-> Tensor
+Tensor FromPy(const py::handle& obj) {
+  if (py::isinstance<py::str>(obj) || py::isinstance<py::bytes>(obj))
+    return Tensor::Strings({obj.cast<std::string>()});
+  if (py::isinstance<py::list>(obj) || py::isinstance<py::tuple>(obj)) {
+    py::sequence seq = obj.cast<py::sequence>();
+    bool all_str = seq.size() > 0;
+    for (auto it : seq) all_str = all_str && (py::isinstance<py::str>(it) || py::isinstance<py::bytes>(it));
+    if (all_str) {
+      std::vector<std::string> v;
+      for (auto it : seq) v.push_back(it.cast<std::string>());
+      return Tensor::Strings(v);
+    }
+  }
+  py::array arr = py::array::ensure(obj);
+  if (!arr) throw std::runtime_error("cannot convert input to an array");
+  if (arr.dtype().kind() == 'U' || arr.dtype().kind() == 'S' || arr.dtype().kind() == 'O') {
+    std::vector<std::string> v;
+    for (auto it : arr.attr("reshape")(-1)) v.push_back(py::str(it).cast<std::string>());
+    std::vector<int64_t> shape(arr.shape(), arr.shape() + arr.ndim());
+    return Tensor::Strings(v, shape.empty() ? std::vector<int64_t>{1} : shape);
+  }
+  arr = py::array::ensure(arr, py::array::c_style);
+  std::vector<int64_t> shape(arr.shape(), arr.shape() + arr.ndim());
+  if (shape.empty()) shape = {1};
+  DType dt;
+  const char k = arr.dtype().kind();
+  const int sz = static_cast<int>(arr.dtype().itemsize());
+  if (k == 'f') dt = sz == 4 ? DType::kFloat : DType::kDouble;
+  else if (k == 'i') dt = sz == 1 ? DType::kInt8 : sz == 2 ? DType::kInt16 : sz == 4 ? DType::kInt32 : DType::kInt64;
+  else if (k == 'u') dt = sz == 1 ? DType::kUInt8 : sz == 2 ? DType::kUInt16 : sz == 4 ? DType::kUInt32 : DType::kUInt64;
+  else if (k == 'b') dt = DType::kBool;
+  else throw std::runtime_error("unsupported numpy dtype");
+  Tensor t(dt, shape);
+  if (t.nbytes()) memcpy(t.raw(), arr.data(), t.nbytes());
+  return t;
+}
+
+py::object ToPy(const Tensor& t) {
+  std::vector<py::ssize_t> shape(t.shape().begin(), t.shape().end());
+  if (t.dtype() == DType::kString) {
+    py::list l;
+    for (auto& s : t.strings()) l.append(py::bytes(s));
+    return std::move(l);
+  }
+  auto mk = [&](auto tag) -> py::object {
+    using T = decltype(tag);
+    py::array_t<T> a(shape);
+    if (t.nbytes()) memcpy(a.mutable_data(), t.raw(), t.nbytes());
+    return std::move(a);
+  };
+  switch (t.dtype()) {
+    case DType::kInt8: return mk(int8_t());
+    case DType::kInt16: return mk(int16_t());
+    case DType::kInt32: return mk(int32_t());
+    case DType::kInt64: return mk(int64_t());
+    case DType::kUInt8: case DType::kBool: return mk(uint8_t());
+    case DType::kUInt16: return mk(uint16_t());
+    case DType::kUInt32: return mk(uint32_t());
+    case DType::kUInt64: return mk(uint64_t());
+    case DType::kFloat: return mk(float());
+    case DType::kDouble: return mk(double());
+    default: break;
+  }
+  throw std::runtime_error("unsupported tensor dtype");
+}
+
+// ------------------------------------------------------------------ Engine (QueryProxy)
+class Engine {
+ public:
+  Engine() : proxy_(new QueryProxy) {}
+  explicit Engine(std::unique_ptr<QueryProxy> p) : proxy_(std::move(p)) {}
+
+  static std::shared_ptr<Engine> FromConfig(const std::map<std::string, std::string>& cfg) {
+    auto e = std::make_shared<Engine>();
+    Status st;
+    {
+      py::gil_scoped_release nogil;
+      st = e->proxy_->Init(cfg);
+    }
+    Throw(st);
+    return e;
+  }
+
+  py::list Run(const std::string& gql, py::dict inputs, const std::vector<std::string>& outputs) {
+    std::vector<std::pair<std::string, Tensor>> in;
+    for (auto kv : inputs) in.emplace_back(kv.first.cast<std::string>(), FromPy(kv.second));
+    std::vector<Tensor> res;
+    Status st;
+    {
+      py::gil_scoped_release nogil;
+      st = proxy_->Run(gql, in, outputs, &res);
+    }
+    Throw(st);
+    py::list out;
+    for (auto& t : res) out.append(ToPy(t));
+    return out;
+  }
+
+  std::string Explain(const std::string& gql) {
+    std::string s;
+    Throw(proxy_->Explain(gql, &s));
+    return s;
+  }
+
+  py::dict Meta() const {
+    const GraphMeta& m = proxy_->meta();
+    py::dict d;
+    d["name"] = m.name;
+    d["version"] = m.version;
+    d["node_count"] = m.node_count;
+    d["edge_count"] = m.edge_count;
+    d["partitions_num"] = m.partitions_num;
+    auto feats = [](const std::vector<FeatureInfo>& v) {
+      py::dict f;
+      for (auto& fi : v) f[py::str(fi.name)] = py::make_tuple(static_cast<int>(fi.type), fi.idx, fi.dim);
+      return f;
+    };
+    d["node_features"] = feats(m.node_features);
+    d["edge_features"] = feats(m.edge_features);
+    py::dict nt, et;
+    for (auto& kv : m.node_types) nt[py::str(kv.first)] = kv.second;
+    for (auto& kv : m.edge_types) et[py::str(kv.first)] = kv.second;
+    d["node_types"] = nt;
+    d["edge_types"] = et;
+    d["mode"] = proxy_->mode();
+    d["shard_num"] = proxy_->shard_num();
+    d["graph_labels"] = proxy_->env()->graph_labels;
+    d["index_info"] = proxy_->env()->index_info;
+    return d;
+  }
+
+  Graph& LocalGraph() const {
+    Graph* g = proxy_->local_graph();
+    if (!g) throw std::runtime_error("this engine has no in-process graph (remote mode)");
+    return *g;
+  }
+
+  // ---- fast local paths for the training input pipeline (no GQL, numpy in/out)
+  py::array_t<uint64_t> SampleNode(int type, int64_t count) {
+    Graph& g = LocalGraph();
+    std::vector<uint64_t> out;
+    {
+      py::gil_scoped_release nogil;
+      Rng rng(GlobalSeed() ^ 0x77ULL, static_cast<uint64_t>(NowMicros()));
+      g.SampleNode(type, count, rng, &out);
+    }
+    py::array_t<uint64_t> a(out.size());
+    if (!out.empty()) memcpy(a.mutable_data(), out.data(), out.size() * 8);
+    return a;
+  }
+
+  py::tuple SampleNeighbor(py::array_t<uint64_t, py::array::c_style | py::array::forcecast> ids,
+                           std::vector<int32_t> etypes, int count, uint64_t def) {
+    Graph& g = LocalGraph();
+    const int64_t n = ids.size();
+    py::array_t<uint64_t> oid({n, static_cast<int64_t>(count)});
+    py::array_t<float> ow({n, static_cast<int64_t>(count)});
+    py::array_t<int32_t> ot({n, static_cast<int64_t>(count)});
+    const uint64_t* pid = ids.data();
+    uint64_t* po = oid.mutable_data();
+    float* pw = ow.mutable_data();
+    int32_t* pt = ot.mutable_data();
+    {
+      py::gil_scoped_release nogil;
+      const uint64_t seed = GlobalSeed() * 0x9E3779B97F4A7C15ULL + NowMicros();
+      const int64_t chunk = 512, nchunks = (n + chunk - 1) / chunk;
+      ThreadPool::Default()->ParallelFor(nchunks, 1, [&](int64_t cb, int64_t ce) {
+        std::vector<IdWeightType> tmp;
+        for (int64_t c = cb; c < ce; ++c) {
+          Rng rng(seed, static_cast<uint64_t>(c));
+          for (int64_t i = c * chunk; i < std::min(n, (c + 1) * chunk); ++i) {
+            g.SampleNeighbor(g.Row(pid[i]), etypes, count, true, rng, &tmp);
+            for (int k = 0; k < count; ++k) {
+              const bool ok = k < static_cast<int>(tmp.size());
+              po[i * count + k] = ok ? tmp[k].id : def;
+              pw[i * count + k] = ok ? tmp[k].weight : 0.f;
+              pt[i * count + k] = ok ? tmp[k].type : -1;
+            }
+          }
+        }
+      });
+    }
+    return py::make_tuple(oid, ow, ot);
+  }
+
+  // dense node feature rows (missing ids / shorter rows -> zeros), [n, dim] float32
+  py::array_t<float> DenseFeature(py::array_t<uint64_t, py::array::c_style | py::array::forcecast> ids,
+                                  const std::string& name, int64_t dim) {
+    Graph& g = LocalGraph();
+    const FeatureInfo* fi = g.meta().NodeFeature(name);
+    if (!fi || fi->type != kDense) throw std::runtime_error("no dense node feature named " + name);
+    const Column<float>* c = g.NodeDense(fi->idx);
+    const int64_t n = ids.size();
+    py::array_t<float> out({n, dim});
+    float* po = out.mutable_data();
+    const uint64_t* pid = ids.data();
+    {
+      py::gil_scoped_release nogil;
+      ThreadPool::Default()->ParallelFor(n, 1024, [&](int64_t b, int64_t e) {
+        for (int64_t i = b; i < e; ++i) {
+          const int64_t r = g.Row(pid[i]);
+          const float* p = nullptr;
+          int64_t k = 0;
+          if (c && r >= 0) c->Get(r, &p, &k);
+          const int64_t m = std::min(k, dim);
+          if (m > 0) memcpy(po + i * dim, p, m * 4);
+          if (m < dim) memset(po + i * dim + m, 0, (dim - m) * 4);
+        }
+      });
+    }
+    return out;
+  }
+
+  // whole CSR (out direction) for moving the shard into HBM: indptr, nbr rows (int32), raw weights
+  py::tuple ExportCsr() {
+    Graph& g = LocalGraph();
+    const Adjacency& A = g.adj(true);
+    py::array_t<int64_t> indptr(A.indptr.size());
+    memcpy(indptr.mutable_data(), A.indptr.data(), A.indptr.size() * 8);
+    py::array_t<int64_t> nbr(A.nbr.size());
+    py::array_t<float> w(A.nbr.size());
+    int64_t* pn = nbr.mutable_data();
+    float* pw = w.mutable_data();
+    {
+      py::gil_scoped_release nogil;
+      ThreadPool::Default()->ParallelFor(static_cast<int64_t>(g.num_nodes()) * g.num_edge_types(), 4096,
+                                         [&](int64_t b, int64_t e) {
+                                           for (int64_t s = b; s < e; ++s)
+                                             for (uint64_t k = A.indptr[s]; k < A.indptr[s + 1]; ++k) {
+                                               pn[k] = g.Row(A.nbr[k]);
+                                               pw[k] = A.EdgeWeight(k, A.indptr[s]);
+                                             }
+                                         });
+    }
+    py::array_t<uint64_t> ids(g.num_nodes());
+    memcpy(ids.mutable_data(), g.node_ids().data(), g.num_nodes() * 8);
+    py::array_t<float> nw(g.num_nodes());
+    for (int64_t r = 0; r < g.num_nodes(); ++r) nw.mutable_data()[r] = g.NodeWeight(r);
+    return py::make_tuple(indptr, nbr, w, g.num_edge_types(), ids, nw);
+  }
+
+  std::string Summary() const {
+    Graph* g = proxy_->local_graph();
+    return g ? g->Summary() : std::string("remote engine (") + proxy_->mode() + ")";
+  }
+
+  QueryProxy* proxy() { return proxy_.get(); }
+
+ private:
+  std::unique_ptr<QueryProxy> proxy_;
+};
+
+// ------------------------------------------------------------------ builder
+class PyBuilder {
+ public:
+  void SetMeta(const std::string& serialized) { Throw(b_.meta().Parse(serialized.data(), serialized.size())); }
+  void AddNodes(py::array_t<uint64_t, py::array::c_style | py::array::forcecast> ids,
+                py::array_t<int32_t, py::array::c_style | py::array::forcecast> types,
+                py::array_t<float, py::array::c_style | py::array::forcecast> weights) {
+    for (py::ssize_t i = 0; i < ids.size(); ++i) b_.AddNode(ids.at(i), types.at(i), weights.at(i));
+  }
+  void AddEdges(py::array_t<uint64_t, py::array::c_style | py::array::forcecast> src,
+                py::array_t<uint64_t, py::array::c_style | py::array::forcecast> dst,
+                py::array_t<int32_t, py::array::c_style | py::array::forcecast> types,
+                py::array_t<float, py::array::c_style | py::array::forcecast> weights) {
+    for (py::ssize_t i = 0; i < src.size(); ++i) b_.AddEdge(src.at(i), dst.at(i), types.at(i), weights.at(i));
+  }
+  void NodeDense(uint64_t id, int idx, py::array_t<float, py::array::c_style | py::array::forcecast> v) {
+    b_.AddNodeDense(id, idx, v.data(), v.size());
+  }
+  void NodeDenseMatrix(py::array_t<uint64_t, py::array::c_style | py::array::forcecast> ids, int idx,
+                       py::array_t<float, py::array::c_style | py::array::forcecast> m) {
+    const int64_t d = m.ndim() == 2 ? m.shape(1) : 1;
+    for (py::ssize_t i = 0; i < ids.size(); ++i) b_.AddNodeDense(ids.at(i), idx, m.data() + i * d, d);
+  }
+  void NodeSparse(uint64_t id, int idx, py::array_t<uint64_t, py::array::c_style | py::array::forcecast> v) {
+    b_.AddNodeSparse(id, idx, v.data(), v.size());
+  }
+  void NodeBinary(uint64_t id, int idx, const std::string& v) { b_.AddNodeBinary(id, idx, v.data(), v.size()); }
+  void EdgeDense(uint64_t s, uint64_t d, int32_t t, int idx, py::array_t<float, py::array::c_style | py::array::forcecast> v) {
+    b_.AddEdgeDense(s, d, t, idx, v.data(), v.size());
+  }
+  void EdgeSparse(uint64_t s, uint64_t d, int32_t t, int idx, py::array_t<uint64_t, py::array::c_style | py::array::forcecast> v) {
+    b_.AddEdgeSparse(s, d, t, idx, v.data(), v.size());
+  }
+  void EdgeBinary(uint64_t s, uint64_t d, int32_t t, int idx, const std::string& v) {
+    b_.AddEdgeBinary(s, d, t, idx, v.data(), v.size());
+  }
+  void DeriveIn(bool v) { b_.SetDeriveInFromEdges(v); }
+  std::shared_ptr<Engine> Finish() {
+    std::unique_ptr<Graph> g;
+    {
+      py::gil_scoped_release nogil;
+      g = b_.Finish();
+    }
+    std::unique_ptr<QueryProxy> p(new QueryProxy);
+    Throw(p->InitWithGraph(std::move(g), nullptr));
+    return std::make_shared<Engine>(std::move(p));
+  }
+
+ private:
+  GraphBuilder b_;
+};
+
+// ------------------------------------------------------------------ server
+class PyServer {
+ public:
+  PyServer(const std::string& data_path, int shard_idx, int shard_num, const std::string& registry, int port,
+           int threads, const std::string& host) {
+    Status st;
+    {
+      py::gil_scoped_release nogil;
+      st = LoadShard(data_path, shard_idx, shard_num, &g_, &idx_);
+    }
+    Throw(st);
+    env_ = QueryProxy::MakeEnv(g_.get(), idx_.get(), shard_num);
+    ServerOptions opt;
+    opt.port = port;
+    opt.num_threads = threads;
+    opt.registry = registry;
+    opt.host = host;
+    server_.reset(new GraphServer(env_.get(), shard_idx, shard_num, opt));
+    Throw(server_->Start());
+  }
+  int port() const { return server_->port(); }
+  int64_t requests() const { return server_->requests(); }
+  void Stop() {
+    py::gil_scoped_release nogil;
+    server_->Stop();
+  }
+
+ private:
+  std::unique_ptr<Graph> g_;
+  std::unique_ptr<IndexManager> idx_;
+  std::unique_ptr<EngineEnv> env_;
+  std::unique_ptr<GraphServer> server_;
+};
+
+}  // namespace
+
+PYBIND11_MODULE(_engine, m) {
+  m.doc() = "euler_amd C++ graph engine";
+  LinkGraphOps();
+  LinkDistOps();
+  LinkRemoteOp();
+
+  py::class_<Engine, std::shared_ptr<Engine>>(m, "Engine")
+      .def_static("from_config", &Engine::FromConfig)
+      .def("run", &Engine::Run, py::arg("gql"), py::arg("inputs"), py::arg("outputs"))
+      .def("explain", &Engine::Explain)
+      .def("meta", &Engine::Meta)
+      .def("summary", &Engine::Summary)
+      .def("sample_node", &Engine::SampleNode)
+      .def("sample_neighbor", &Engine::SampleNeighbor)
+      .def("dense_feature", &Engine::DenseFeature)
+      .def("export_csr", &Engine::ExportCsr);
+
+  py::class_<PyBuilder>(m, "GraphBuilder")
+      .def(py::init<>())
+      .def("set_meta", &PyBuilder::SetMeta)
+      .def("add_nodes", &PyBuilder::AddNodes)
+      .def("add_edges", &PyBuilder::AddEdges)
+      .def("node_dense", &PyBuilder::NodeDense)
+      .def("node_dense_matrix", &PyBuilder::NodeDenseMatrix)
+      .def("node_sparse", &PyBuilder::NodeSparse)
+      .def("node_binary", &PyBuilder::NodeBinary)
+      .def("edge_dense", &PyBuilder::EdgeDense)
+      .def("edge_sparse", &PyBuilder::EdgeSparse)
+      .def("edge_binary", &PyBuilder::EdgeBinary)
+      .def("derive_in_from_edges", &PyBuilder::DeriveIn)
+      .def("finish", &PyBuilder::Finish);
+
+  py::class_<PyServer>(m, "GraphServer")
+      .def(py::init<const std::string&, int, int, const std::string&, int, int, const std::string&>(),
+           py::arg("data_path"), py::arg("shard_idx"), py::arg("shard_num"), py::arg("registry") = "",
+           py::arg("port") = 0, py::arg("threads") = 32, py::arg("host") = "127.0.0.1")
+      .def_property_readonly("port", &PyServer::port)
+      .def_property_readonly("requests", &PyServer::requests)
+      .def("stop", &PyServer::Stop);
+
+  m.def("synthetic", [](int64_t n, double avg_deg, int64_t max_deg, int node_types, int edge_types, int feature_dim,
+                        int label_dim, uint64_t seed) {
+    std::unique_ptr<Graph> g;
+    {
+      py::gil_scoped_release nogil;
+      g = SyntheticGraph(n, avg_deg, max_deg, node_types, edge_types, feature_dim, label_dim, seed, 0);
+    }
+    std::unique_ptr<QueryProxy> p(new QueryProxy);
+    Throw(p->InitWithGraph(std::move(g), nullptr));
+    return std::make_shared<Engine>(std::move(p));
+  });
+  m.def("parse_gql", [](const std::string& q) {
+    std::vector<GqlStep> steps;
+    Throw(ParseGql(q, &steps));
+    py::list out;
+    for (auto& s : steps) {
+      py::dict d;
+      d["op"] = s.op;
+      d["params"] = s.params;
+      d["dnf"] = s.dnf;
+      d["post"] = s.post;
+      d["alias"] = s.alias;
+      out.append(d);
+    }
+    return out;
+  });
+  m.def("compile_gql", [](const std::string& q, const std::string& mode, int shards, std::vector<std::string> nbr_idx) {
+    CompileOptions o;
+    o.mode = mode == "local" ? CompileMode::kLocal : CompileMode::kDistribute;
+    o.shard_num = shards;
+    o.neighbor_indexes = nbr_idx;
+    std::shared_ptr<const DAGDef> d;
+    Throw(Compiler::Get().Compile(q, o, &d));
+    py::list nodes;
+    for (auto& n : d->nodes) {
+      py::dict x;
+      x["name"] = n.name();
+      x["op"] = n.op;
+      x["inputs"] = n.inputs;
+      x["attrs"] = n.attrs;
+      x["shard"] = n.shard_idx;
+      std::vector<std::string> inner;
+      for (auto& c : n.inner) inner.push_back(c.op);
+      x["inner"] = inner;
+      nodes.append(x);
+    }
+    return nodes;
+  }, py::arg("query"), py::arg("mode") = "local", py::arg("shard_num") = 1,
+     py::arg("neighbor_indexes") = std::vector<std::string>{});
+  m.def("set_seed", [](uint64_t s) { SetGlobalSeed(s); });
+  m.def("hash64", [](py::bytes b) {
+    std::string s = b;
+    return Hash64(s.data(), static_cast<int>(s.size()));
+  });
+  m.def("edge_id_hash", &EdgeIdHash);
+  m.def("registered_ops", [] { return KernelRegistry::Get().Ops(); });
+}

@@ -1,0 +1,791 @@
+#include "rpc/rpc.h"
+
+#include <arpa/inet.h>
+#include <errno.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <set>
+
+namespace euler {
+
+namespace {
+constexpr uint32_t kMagic = 0x524C5545;  // "EULR"
+enum : uint32_t { kPing = 1, kExecute = 2, kMeta = 3, kReply = 100 };
+
+double NowSec() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+bool WriteAll(int fd, const void* p, size_t n) {
+  const char* c = static_cast<const char*>(p);
+  while (n > 0) {
+    ssize_t k = ::send(fd, c, n, MSG_NOSIGNAL);
+    if (k < 0 && errno == EINTR) continue;
+    if (k <= 0) return false;
+    c += k;
+    n -= static_cast<size_t>(k);
+  }
+  return true;
+}
+
+bool ReadAll(int fd, void* p, size_t n) {
+  char* c = static_cast<char*>(p);
+  while (n > 0) {
+    ssize_t k = ::recv(fd, c, n, 0);
+    if (k < 0 && errno == EINTR) continue;
+    if (k <= 0) return false;
+    c += k;
+    n -= static_cast<size_t>(k);
+  }
+  return true;
+}
+
+bool SendFrame(int fd, uint32_t kind, const std::string& payload) {
+  char hdr[16];
+  const uint64_t len = payload.size();
+  memcpy(hdr, &kMagic, 4);
+  memcpy(hdr + 4, &kind, 4);
+  memcpy(hdr + 8, &len, 8);
+  return WriteAll(fd, hdr, 16) && WriteAll(fd, payload.data(), payload.size());
+}
+
+bool RecvFrame(int fd, uint32_t* kind, std::string* payload) {
+  char hdr[16];
+  if (!ReadAll(fd, hdr, 16)) return false;
+  uint32_t magic;
+  uint64_t len;
+  memcpy(&magic, hdr, 4);
+  memcpy(kind, hdr + 4, 4);
+  memcpy(&len, hdr + 8, 8);
+  if (magic != kMagic || len > (1ULL << 36)) return false;
+  payload->resize(len);
+  return len == 0 || ReadAll(fd, &(*payload)[0], len);
+}
+
+int Connect(const Endpoint& ep, int timeout_ms) {
+  struct addrinfo hints, *res = nullptr;
+  memset(&hints, 0, sizeof(hints));
+  hints.ai_family = AF_INET;
+  hints.ai_socktype = SOCK_STREAM;
+  if (getaddrinfo(ep.host.c_str(), std::to_string(ep.port).c_str(), &hints, &res) != 0 || !res) return -1;
+  int fd = socket(res->ai_family, res->ai_socktype, res->ai_protocol);
+  if (fd < 0) {
+    freeaddrinfo(res);
+    return -1;
+  }
+  int one = 1;
+  setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  struct timeval tv;
+  tv.tv_sec = timeout_ms / 1000;
+  tv.tv_usec = (timeout_ms % 1000) * 1000;
+  setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+  setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
+  if (connect(fd, res->ai_addr, res->ai_addrlen) != 0) {
+    close(fd);
+    freeaddrinfo(res);
+    return -1;
+  }
+  freeaddrinfo(res);
+  return fd;
+}
+
+std::string EncodeExecute(const DAGDef& dag, const std::vector<std::pair<std::string, Tensor>>& inputs,
+                          const std::vector<std::string>& outputs) {
+  BytesWriter w;
+  w.Write(dag.Serialize());
+  w.Write<uint32_t>(static_cast<uint32_t>(inputs.size()));
+  for (auto& kv : inputs) {
+    w.Write(kv.first);
+    kv.second.Encode(&w);
+  }
+  w.Write<uint32_t>(static_cast<uint32_t>(outputs.size()));
+  for (auto& o : outputs) w.Write(o);
+  return w.str();
+}
+
+bool DecodeExecute(const std::string& p, DAGDef* dag, std::vector<std::pair<std::string, Tensor>>* inputs,
+                   std::vector<std::string>* outputs) {
+  BytesReader r(p.data(), p.size());
+  std::string d;
+  uint32_t n;
+  if (!r.Read(&d) || !DAGDef::Parse(d.data(), d.size(), dag) || !r.Read(&n)) return false;
+  inputs->resize(n);
+  for (auto& kv : *inputs)
+    if (!r.Read(&kv.first) || !Tensor::Decode(&r, &kv.second)) return false;
+  if (!r.Read(&n)) return false;
+  outputs->resize(n);
+  for (auto& o : *outputs)
+    if (!r.Read(&o)) return false;
+  return true;
+}
+
+std::string EncodeReply(const Status& st, const std::vector<Tensor>& ts) {
+  BytesWriter w;
+  w.Write<int32_t>(static_cast<int32_t>(st.code()));
+  w.Write(st.message());
+  w.Write<uint32_t>(static_cast<uint32_t>(ts.size()));
+  for (auto& t : ts) t.Encode(&w);
+  return w.str();
+}
+
+Status DecodeReply(const std::string& p, std::vector<Tensor>* ts) {
+  BytesReader r(p.data(), p.size());
+  int32_t code;
+  std::string msg;
+  uint32_t n;
+  if (!r.Read(&code) || !r.Read(&msg) || !r.Read(&n)) return Status::RpcError("malformed reply");
+  if (code != 0) return Status(static_cast<Code>(code), msg);
+  ts->resize(n);
+  for (auto& t : *ts)
+    if (!Tensor::Decode(&r, &t)) return Status::RpcError("malformed reply tensor");
+  return Status::OK();
+}
+
+double FaultRate() {
+  static double r = [] {
+    const char* e = getenv("EULER_RPC_FAULT_RATE");
+    return e ? atof(e) : 0.0;
+  }();
+  return r;
+}
+int FaultDelayMs() {
+  static int d = [] {
+    const char* e = getenv("EULER_RPC_FAULT_DELAY_MS");
+    return e ? atoi(e) : 0;
+  }();
+  return d;
+}
+}  // namespace
+
+// ============================================================================ execution
+Status ExecuteDag(EngineEnv* env, const DAGDef& dag, const std::vector<std::pair<std::string, Tensor>>& inputs,
+                  const std::vector<std::string>& outputs, std::vector<Tensor>* results) {
+  OpContext ctx(env);
+  for (auto& kv : inputs) ctx.Set(kv.first, kv.second);
+  Executor ex(dag, &ctx, ThreadPool::Default());
+  EULER_RETURN_IF_ERROR(ex.Run());
+  results->clear();
+  for (auto& o : outputs) {
+    Tensor t;
+    if (!ctx.TryGet(o, &t)) return Status::NotFound("output '" + o + "' was not produced");
+    results->push_back(t);
+  }
+  return Status::OK();
+}
+
+void InProcessShards::Execute(int shard, const DAGDef& dag, std::vector<std::pair<std::string, Tensor>> inputs,
+                              std::vector<std::string> outputs, Done done) {
+  if (shard < 0 || shard >= num_shards()) {
+    done(Status::InvalidArgument("bad shard index"), {});
+    return;
+  }
+  // shards run concurrently on their own pool, like separate servers would
+  static ThreadPool* pool = new ThreadPool(16, "euler-inproc-shards");
+  EngineEnv* env = envs_[shard];
+  auto dagp = std::make_shared<DAGDef>(dag);
+  pool->Schedule([env, dagp, inputs, outputs, done] {
+    std::vector<Tensor> res;
+    Status st;
+    try {
+      st = ExecuteDag(env, *dagp, inputs, outputs, &res);
+    } catch (const std::exception& e) {
+      st = Status::Internal(e.what());
+    }
+    done(st, std::move(res));
+  });
+}
+
+// ============================================================================ REMOTE kernel
+namespace {
+class RemoteOp : public OpKernel {
+ public:
+  bool is_async() const override { return true; }
+  void Compute(const NodeDef&, OpContext*) override { EULER_THROW("REMOTE is asynchronous"); }
+  void ComputeAsync(const NodeDef& nd, OpContext* ctx, std::function<void(Status)> done) override {
+    RemoteClients* rc = ctx->env() ? ctx->env()->clients : nullptr;
+    if (!rc) {
+      done(Status::Unavailable("REMOTE node but no remote clients configured"));
+      return;
+    }
+    // ship every client tensor the sub-DAG references (inputs, attrs, DNF values)
+    std::set<std::string> produced;
+    for (auto& n : nd.inner)
+      for (int k = 0; k < std::max(1, n.output_num); ++k) produced.insert(n.Output(k));
+    std::set<std::string> names;
+    auto consider = [&](const std::string& s) {
+      if (!produced.count(s) && ctx->Has(s)) names.insert(s);
+    };
+    for (auto& n : nd.inner) {
+      for (auto& s : n.inputs) consider(s);
+      for (auto& s : n.attrs) consider(s);
+      for (auto& conj : n.dnf)
+        for (auto& term : Split(conj, ","))
+          for (auto& tok : Split(term, " ")) consider(Trim(tok));
+    }
+    std::vector<std::pair<std::string, Tensor>> inputs;
+    for (auto& s : names) inputs.emplace_back(s, ctx->Get(s));
+    DAGDef sub;
+    sub.nodes = nd.inner;
+    const std::string me = nd.name();
+    const int on = nd.output_num;
+    rc->Execute(nd.shard_idx, sub, std::move(inputs), nd.output_list,
+                [ctx, me, on, done](Status st, std::vector<Tensor> res) {
+                  if (st.ok()) {
+                    for (int k = 0; k < on && k < static_cast<int>(res.size()); ++k)
+                      ctx->Set(me + ":" + std::to_string(k), std::move(res[k]));
+                  }
+                  done(st);
+                });
+  }
+};
+}  // namespace
+REGISTER_OP_KERNEL("REMOTE", RemoteOp);
+void LinkRemoteOp() {}
+
+// ============================================================================ ShardMeta
+static std::string HexEncode(const std::string& s) {
+  static const char* d = "0123456789abcdef";
+  std::string o;
+  o.reserve(s.size() * 2);
+  for (unsigned char c : s) {
+    o.push_back(d[c >> 4]);
+    o.push_back(d[c & 15]);
+  }
+  return o;
+}
+static std::string HexDecode(const std::string& s) {
+  std::string o;
+  auto v = [](char c) { return c <= '9' ? c - '0' : c - 'a' + 10; };
+  for (size_t i = 0; i + 1 < s.size(); i += 2) o.push_back(static_cast<char>((v(s[i]) << 4) | v(s[i + 1])));
+  return o;
+}
+static std::string JoinD(const std::vector<double>& v) {
+  std::vector<std::string> s;
+  for (double x : v) {
+    std::ostringstream os;
+    os.precision(17);
+    os << x;
+    s.push_back(os.str());
+  }
+  return Join(s, ",");
+}
+static std::vector<double> SplitD(const std::string& s) {
+  std::vector<double> v;
+  for (auto& p : Split(s, ",")) {
+    double x = 0;
+    ParseDouble(p, &x);
+    v.push_back(x);
+  }
+  return v;
+}
+
+std::string ShardMeta::ToString() const {
+  std::ostringstream os;
+  os << "shard_idx=" << shard_idx << "\nshard_num=" << shard_num << "\nnum_partitions=" << num_partitions
+     << "\nnode_sum_weight=" << JoinD(node_weight_sums) << "\nedge_sum_weight=" << JoinD(edge_weight_sums)
+     << "\ngraph_label=" << HexEncode(Join(graph_labels, "\x1f")) << "\nindex_info=" << index_info
+     << "\ngraph_meta=" << HexEncode(graph_meta) << "\n";
+  return os.str();
+}
+
+bool ShardMeta::Parse(const std::string& s, ShardMeta* m) {
+  for (auto& line : Split(s, "\n")) {
+    const size_t eq = line.find('=');
+    if (eq == std::string::npos) continue;
+    const std::string k = line.substr(0, eq), v = line.substr(eq + 1);
+    int64_t x;
+    if (k == "shard_idx" && ParseInt64(v, &x)) m->shard_idx = static_cast<int>(x);
+    else if (k == "shard_num" && ParseInt64(v, &x)) m->shard_num = static_cast<int>(x);
+    else if (k == "num_partitions" && ParseInt64(v, &x)) m->num_partitions = static_cast<uint32_t>(x);
+    else if (k == "node_sum_weight") m->node_weight_sums = SplitD(v);
+    else if (k == "edge_sum_weight") m->edge_weight_sums = SplitD(v);
+    else if (k == "graph_label") m->graph_labels = Split(HexDecode(v), "\x1f");
+    else if (k == "index_info") m->index_info = v;
+    else if (k == "graph_meta") m->graph_meta = HexDecode(v);
+  }
+  return true;
+}
+
+ShardMeta ShardMeta::FromEnv(const EngineEnv& env, int shard_idx, int shard_num) {
+  ShardMeta m;
+  m.shard_idx = shard_idx;
+  m.shard_num = shard_num;
+  if (env.graph) {
+    const Graph& g = *env.graph;
+    m.num_partitions = std::max<uint32_t>(1, g.meta().partitions_num);
+    for (int t = 0; t < g.num_node_types(); ++t) m.node_weight_sums.push_back(g.NodeWeightSum(t));
+    for (int t = 0; t < g.num_edge_types(); ++t) m.edge_weight_sums.push_back(g.EdgeWeightSum(t));
+    m.graph_labels = g.graph_labels();
+    m.graph_meta = g.meta().Serialize();
+  }
+  if (env.index) m.index_info = env.index->IndexInfo();
+  return m;
+}
+
+// ============================================================================ Registry
+namespace {
+class FileRegistry : public Registry {
+ public:
+  explicit FileRegistry(std::string dir) : dir_(std::move(dir)) { MakeDirs(dir_); }
+  Status Register(int shard, const Endpoint& ep, const ShardMeta& meta) override {
+    const std::string tmp = JoinPath(dir_, ".tmp." + std::to_string(shard) + "#" + ep.ToString());
+    EULER_RETURN_IF_ERROR(WriteFile(tmp, meta.ToString()));
+    if (rename(tmp.c_str(), JoinPath(dir_, std::to_string(shard) + "#" + ep.ToString()).c_str()) != 0)
+      return Status::Internal("registry rename failed");
+    return Status::OK();
+  }
+  Status Deregister(int shard, const Endpoint& ep) override {
+    unlink(JoinPath(dir_, std::to_string(shard) + "#" + ep.ToString()).c_str());
+    return Status::OK();
+  }
+  Status List(std::map<int, std::vector<std::pair<Endpoint, ShardMeta>>>* out) override {
+    out->clear();
+    std::vector<std::string> names;
+    EULER_RETURN_IF_ERROR(ListDir(dir_, &names));
+    for (auto& n : names) {
+      if (n.empty() || n[0] == '.') continue;
+      const size_t h = n.find('#'), c = n.rfind(':');
+      int64_t shard, port;
+      if (h == std::string::npos || c == std::string::npos || !ParseInt64(n.substr(0, h), &shard) ||
+          !ParseInt64(n.substr(c + 1), &port))
+        continue;
+      std::unique_ptr<FileView> f;
+      if (!FileView::Open(JoinPath(dir_, n), &f).ok()) continue;
+      ShardMeta m;
+      ShardMeta::Parse(std::string(f->data(), f->size()), &m);
+      (*out)[static_cast<int>(shard)].push_back({Endpoint{n.substr(h + 1, c - h - 1), static_cast<int>(port)}, m});
+    }
+    return Status::OK();
+  }
+
+ private:
+  std::string dir_;
+};
+
+class MemoryRegistry : public Registry {
+ public:
+  explicit MemoryRegistry(std::string name) : name_(std::move(name)) {}
+  static std::mutex& mu() {
+    static std::mutex m;
+    return m;
+  }
+  static std::map<std::string, std::map<std::string, std::tuple<int, Endpoint, ShardMeta>>>& store() {
+    static std::map<std::string, std::map<std::string, std::tuple<int, Endpoint, ShardMeta>>> s;
+    return s;
+  }
+  Status Register(int shard, const Endpoint& ep, const ShardMeta& meta) override {
+    std::lock_guard<std::mutex> l(mu());
+    store()[name_][std::to_string(shard) + "#" + ep.ToString()] = std::make_tuple(shard, ep, meta);
+    return Status::OK();
+  }
+  Status Deregister(int shard, const Endpoint& ep) override {
+    std::lock_guard<std::mutex> l(mu());
+    store()[name_].erase(std::to_string(shard) + "#" + ep.ToString());
+    return Status::OK();
+  }
+  Status List(std::map<int, std::vector<std::pair<Endpoint, ShardMeta>>>* out) override {
+    std::lock_guard<std::mutex> l(mu());
+    out->clear();
+    for (auto& kv : store()[name_]) (*out)[std::get<0>(kv.second)].push_back({std::get<1>(kv.second), std::get<2>(kv.second)});
+    return Status::OK();
+  }
+
+ private:
+  std::string name_;
+};
+}  // namespace
+
+std::unique_ptr<Registry> Registry::Open(const std::string& spec) {
+  if (StartsWith(spec, "memory:")) return std::unique_ptr<Registry>(new MemoryRegistry(spec.substr(7)));
+  if (StartsWith(spec, "file:")) return std::unique_ptr<Registry>(new FileRegistry(spec.substr(5)));
+  if (StartsWith(spec, "zk:") || spec.find("2181") != std::string::npos)
+    EULER_THROW("ZooKeeper registries are not built into euler_amd; use a shared directory (file:<dir>)");
+  return std::unique_ptr<Registry>(new FileRegistry(spec));
+}
+
+// ============================================================================ GraphServer
+GraphServer::GraphServer(EngineEnv* env, int shard_idx, int shard_num, const ServerOptions& opt)
+    : env_(env), shard_idx_(shard_idx), shard_num_(shard_num), opt_(opt) {
+  host_ = opt.host.empty() ? "127.0.0.1" : opt.host;
+}
+
+GraphServer::~GraphServer() { Stop(); }
+
+Status GraphServer::Start() {
+  listen_fd_ = socket(AF_INET, SOCK_STREAM, 0);
+  if (listen_fd_ < 0) return Status::Internal("socket failed");
+  int one = 1;
+  setsockopt(listen_fd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+  struct sockaddr_in addr;
+  memset(&addr, 0, sizeof(addr));
+  addr.sin_family = AF_INET;
+  addr.sin_addr.s_addr = htonl(INADDR_ANY);
+  addr.sin_port = htons(static_cast<uint16_t>(opt_.port));
+  if (bind(listen_fd_, reinterpret_cast<sockaddr*>(&addr), sizeof(addr)) != 0)
+    return Status::Internal("bind failed on port " + std::to_string(opt_.port) + ": " + strerror(errno));
+  if (listen(listen_fd_, 128) != 0) return Status::Internal("listen failed");
+  socklen_t len = sizeof(addr);
+  getsockname(listen_fd_, reinterpret_cast<sockaddr*>(&addr), &len);
+  port_ = ntohs(addr.sin_port);
+  pool_.reset(new ThreadPool(std::max(1, opt_.num_threads), "euler-server"));
+  running_ = true;
+  accept_thread_ = std::thread([this] { AcceptLoop(); });
+  if (!opt_.registry.empty()) {
+    registry_ = Registry::Open(opt_.registry);
+    EULER_RETURN_IF_ERROR(registry_->Register(shard_idx_, endpoint(), ShardMeta::FromEnv(*env_, shard_idx_, shard_num_)));
+  }
+  EULER_LOG(Info) << "graph server shard " << shard_idx_ << "/" << shard_num_ << " listening on " << port_;
+  return Status::OK();
+}
+
+void GraphServer::Stop() {
+  if (!running_.exchange(false)) return;
+  if (registry_) registry_->Deregister(shard_idx_, endpoint());
+  shutdown(listen_fd_, SHUT_RDWR);
+  close(listen_fd_);
+  if (accept_thread_.joinable()) accept_thread_.join();
+  std::vector<std::thread> ts;
+  {
+    std::lock_guard<std::mutex> l(conn_mu_);
+    for (int fd : conn_fds_) shutdown(fd, SHUT_RDWR);
+    ts.swap(conn_threads_);
+  }
+  for (auto& t : ts)
+    if (t.joinable()) t.join();
+  pool_.reset();
+}
+
+void GraphServer::AcceptLoop() {
+  while (running_) {
+    int fd = accept(listen_fd_, nullptr, nullptr);
+    if (fd < 0) {
+      if (!running_) break;
+      continue;
+    }
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+    std::lock_guard<std::mutex> l(conn_mu_);
+    conn_fds_.push_back(fd);
+    conn_threads_.emplace_back([this, fd] { Serve(fd); });
+  }
+}
+
+void GraphServer::Serve(int fd) {
+  uint32_t kind;
+  std::string payload;
+  while (running_ && RecvFrame(fd, &kind, &payload)) {
+    requests_++;
+    std::string reply;
+    if (kind == kPing) {
+      reply = EncodeReply(Status::OK(), {});
+    } else if (kind == kMeta) {
+      reply = EncodeReply(Status::OK(), {Tensor::Strings({ShardMeta::FromEnv(*env_, shard_idx_, shard_num_).ToString()})});
+    } else if (kind == kExecute) {
+      DAGDef dag;
+      std::vector<std::pair<std::string, Tensor>> inputs;
+      std::vector<std::string> outputs;
+      if (!DecodeExecute(payload, &dag, &inputs, &outputs)) {
+        reply = EncodeReply(Status::RpcError("malformed execute request"), {});
+      } else {
+        std::vector<Tensor> res;
+        Status st;
+        Latch latch(1);
+        pool_->Schedule([&] {
+          try {
+            st = ExecuteDag(env_, dag, inputs, outputs, &res);
+          } catch (const std::exception& e) {
+            st = Status::Internal(e.what());
+          }
+          latch.CountDown();
+        });
+        latch.Wait();
+        reply = EncodeReply(st, res);
+      }
+    } else {
+      reply = EncodeReply(Status::Unimplemented("unknown request kind"), {});
+    }
+    if (!SendFrame(fd, kReply, reply)) break;
+  }
+  close(fd);
+}
+
+// ============================================================================ RpcClients
+RpcClients::RpcClients(std::map<int, std::vector<Endpoint>> shards, const ClientOptions& opt) : opt_(opt) {
+  int n = 0;
+  for (auto& kv : shards) n = std::max(n, kv.first + 1);
+  shards_.resize(n);
+  rr_ = std::vector<std::atomic<uint64_t>>(n);
+  for (auto& kv : shards)
+    for (auto& ep : kv.second) {
+      std::unique_ptr<Host> h(new Host);
+      h->ep = ep;
+      shards_[kv.first].push_back(std::move(h));
+    }
+  pool_.reset(new ThreadPool(std::max(8, 2 * n), "euler-client"));
+}
+
+RpcClients::~RpcClients() {
+  pool_.reset();
+  for (auto& s : shards_)
+    for (auto& h : s)
+      for (int fd : h->idle) close(fd);
+}
+
+Status RpcClients::CallHost(Host* h, uint32_t kind, const std::string& payload, std::string* reply) {
+  int fd = -1;
+  {
+    std::lock_guard<std::mutex> l(h->mu);
+    if (!h->idle.empty()) {
+      fd = h->idle.back();
+      h->idle.pop_back();
+    }
+  }
+  if (fd < 0) fd = Connect(h->ep, opt_.timeout_ms);
+  if (fd < 0) return Status::Unavailable("connect failed: " + h->ep.ToString());
+  uint32_t rk;
+  if (!SendFrame(fd, kind, payload) || !RecvFrame(fd, &rk, reply) || rk != kReply) {
+    close(fd);
+    return Status::RpcError("rpc to " + h->ep.ToString() + " failed");
+  }
+  std::lock_guard<std::mutex> l(h->mu);
+  if (static_cast<int>(h->idle.size()) < opt_.num_channels_per_host) h->idle.push_back(fd);
+  else close(fd);
+  return Status::OK();
+}
+
+Status RpcClients::Call(int shard, uint32_t kind, const std::string& payload, std::string* reply) {
+  if (shard < 0 || shard >= static_cast<int>(shards_.size()) || shards_[shard].empty())
+    return Status::Unavailable("no server for shard " + std::to_string(shard));
+  auto& hosts = shards_[shard];
+  Status last;
+  for (int attempt = 0; attempt <= opt_.num_retries; ++attempt) {
+    if (FaultDelayMs() > 0) std::this_thread::sleep_for(std::chrono::milliseconds(FaultDelayMs()));
+    // round-robin over replicas that are not quarantined
+    Host* h = nullptr;
+    const double now = NowSec();
+    for (size_t k = 0; k < hosts.size(); ++k) {
+      Host* c = hosts[(rr_[shard].fetch_add(1)) % hosts.size()].get();
+      if (c->bad_until <= now) {
+        h = c;
+        break;
+      }
+    }
+    if (!h) h = hosts[rr_[shard].fetch_add(1) % hosts.size()].get();  // all bad: try anyway
+    if (FaultRate() > 0 && ThreadRng().Uniform() < FaultRate()) {
+      last = Status::RpcError("injected fault");
+    } else {
+      last = CallHost(h, kind, payload, reply);
+      if (last.ok()) return last;
+    }
+    failures_++;
+    h->bad_until = NowSec() + opt_.bad_host_timeout;  // move to bad host list
+    EULER_LOG(Warning) << "rpc shard " << shard << " attempt " << attempt << " failed: " << last.message();
+  }
+  return last;
+}
+
+void RpcClients::Execute(int shard, const DAGDef& dag, std::vector<std::pair<std::string, Tensor>> inputs,
+                         std::vector<std::string> outputs, Done done) {
+  auto payload = std::make_shared<std::string>(EncodeExecute(dag, inputs, outputs));
+  pool_->Schedule([this, shard, payload, done] {
+    std::string reply;
+    Status st = Call(shard, kExecute, *payload, &reply);
+    std::vector<Tensor> res;
+    if (st.ok()) st = DecodeReply(reply, &res);
+    done(st, std::move(res));
+  });
+}
+
+Status RpcClients::Ping(int shard) {
+  std::string reply;
+  EULER_RETURN_IF_ERROR(Call(shard, kPing, "", &reply));
+  std::vector<Tensor> r;
+  return DecodeReply(reply, &r);
+}
+
+Status RpcClients::FetchMeta(int shard, ShardMeta* meta) {
+  std::string reply;
+  EULER_RETURN_IF_ERROR(Call(shard, kMeta, "", &reply));
+  std::vector<Tensor> r;
+  EULER_RETURN_IF_ERROR(DecodeReply(reply, &r));
+  if (r.empty()) return Status::RpcError("empty meta reply");
+  ShardMeta::Parse(r[0].strings()[0], meta);
+  return Status::OK();
+}
+
+// ============================================================================ QueryProxy
+Status LoadShard(const std::string& data_path, int shard_idx, int shard_num, std::unique_ptr<Graph>* g,
+                 std::unique_ptr<IndexManager>* idx, int threads) {
+  GraphBuilder b;
+  EULER_RETURN_IF_ERROR(b.LoadReferenceFormat(data_path, shard_idx, shard_num, true, true, threads));
+  *g = b.Finish();
+  idx->reset(new IndexManager);
+  EULER_RETURN_IF_ERROR((*idx)->Load(JoinPath(data_path, "Index"), shard_idx, shard_num));
+  return Status::OK();
+}
+
+std::unique_ptr<EngineEnv> QueryProxy::MakeEnv(Graph* g, IndexManager* idx, int shard_num) {
+  std::unique_ptr<EngineEnv> e(new EngineEnv);
+  e->graph = g;
+  e->index = idx;
+  e->shard_num = shard_num;
+  e->num_partitions = g ? std::max<uint32_t>(1, g->meta().partitions_num) : 1;
+  if (g) e->graph_labels = g->graph_labels();
+  if (idx) e->index_info = idx->IndexInfo();
+  return e;
+}
+
+Status QueryProxy::FillWeightTables(const std::vector<ShardMeta>& metas) {
+  const int S = static_cast<int>(metas.size());
+  size_t nt = 0, et = 0;
+  for (auto& m : metas) {
+    nt = std::max(nt, m.node_weight_sums.size());
+    et = std::max(et, m.edge_weight_sums.size());
+  }
+  // [type + 1][shard + 1]; last row = all types, last column = all shards
+  auto fill = [&](bool node, size_t T, std::vector<std::vector<double>>* tab) {
+    tab->assign(T + 1, std::vector<double>(S + 1, 0.0));
+    for (int s = 0; s < S; ++s) {
+      const auto& v = node ? metas[s].node_weight_sums : metas[s].edge_weight_sums;
+      for (size_t t = 0; t < v.size(); ++t) {
+        (*tab)[t][s] += v[t];
+        (*tab)[t][S] += v[t];
+        (*tab)[T][s] += v[t];
+        (*tab)[T][S] += v[t];
+      }
+    }
+  };
+  fill(true, nt, &env_.node_weight_sums);
+  fill(false, et, &env_.edge_weight_sums);
+  std::set<std::string> labels;
+  for (auto& m : metas)
+    for (auto& l : m.graph_labels)
+      if (!l.empty()) labels.insert(l);
+  env_.graph_labels.assign(labels.begin(), labels.end());
+  return Status::OK();
+}
+
+static std::string Cfg(const std::map<std::string, std::string>& c, const std::string& k, const std::string& d) {
+  auto it = c.find(k);
+  return it == c.end() ? d : it->second;
+}
+
+Status QueryProxy::Init(const std::map<std::string, std::string>& config) {
+  mode_ = Cfg(config, "mode", "local");
+  int64_t seed;
+  if (ParseInt64(Cfg(config, "seed", ""), &seed)) SetGlobalSeed(static_cast<uint64_t>(seed));
+  pool_.reset(new ThreadPool(8, "euler-proxy"));
+  if (mode_ == "local") {
+    std::unique_ptr<Graph> g;
+    std::unique_ptr<IndexManager> idx;
+    EULER_RETURN_IF_ERROR(LoadShard(Cfg(config, "data_path", ""), 0, 1, &g, &idx));
+    return InitWithGraph(std::move(g), std::move(idx));
+  }
+  int64_t shards = 1;
+  if (mode_ == "local_sharded") {
+    // S shards of one dataset inside this process, queried through the distribute compiler
+    ParseInt64(Cfg(config, "shard_num", "2"), &shards);
+    const std::string path = Cfg(config, "data_path", "");
+    std::vector<EngineEnv*> envs;
+    std::vector<ShardMeta> metas;
+    for (int s = 0; s < shards; ++s) {
+      std::unique_ptr<Graph> g;
+      std::unique_ptr<IndexManager> idx;
+      EULER_RETURN_IF_ERROR(LoadShard(path, s, static_cast<int>(shards), &g, &idx));
+      shard_envs_.push_back(MakeEnv(g.get(), idx.get(), static_cast<int>(shards)));
+      envs.push_back(shard_envs_.back().get());
+      metas.push_back(ShardMeta::FromEnv(*envs.back(), s, static_cast<int>(shards)));
+      shard_graphs_.push_back(std::move(g));
+      shard_indexes_.push_back(std::move(idx));
+    }
+    meta_ = shard_graphs_[0]->meta();
+    clients_.reset(new InProcessShards(envs));
+    env_.shard_num = static_cast<int>(shards);
+    env_.num_partitions = std::max<uint32_t>(1, meta_.partitions_num);
+    env_.index_info = metas[0].index_info;
+    FillWeightTables(metas);
+  } else if (mode_ == "remote" || mode_ == "graph_partition") {
+    std::string reg = Cfg(config, "registry", Cfg(config, "zk_path", ""));
+    if (reg.empty()) return Status::InvalidArgument("remote mode needs registry=<dir|memory:name>");
+    auto r = Registry::Open(reg);
+    std::map<int, std::vector<std::pair<Endpoint, ShardMeta>>> listing;
+    int64_t want = 0;
+    ParseInt64(Cfg(config, "shard_num", "0"), &want);
+    double wait = 30;
+    ParseDouble(Cfg(config, "wait_seconds", "30"), &wait);
+    const double deadline = NowSec() + wait;
+    for (;;) {
+      EULER_RETURN_IF_ERROR(r->List(&listing));
+      int expect = static_cast<int>(want);
+      if (!listing.empty() && expect == 0) expect = listing.begin()->second.front().second.shard_num;
+      if (expect > 0 && static_cast<int>(listing.size()) >= expect) break;
+      if (NowSec() > deadline) return Status::Unavailable("timed out waiting for graph servers in " + reg);
+      std::this_thread::sleep_for(std::chrono::milliseconds(100));
+    }
+    ClientOptions co;
+    int64_t x;
+    if (ParseInt64(Cfg(config, "num_retries", "10"), &x)) co.num_retries = static_cast<int>(x);
+    if (ParseInt64(Cfg(config, "num_channels_per_host", "4"), &x)) co.num_channels_per_host = static_cast<int>(x);
+    ParseDouble(Cfg(config, "bad_host_timeout", "10"), &co.bad_host_timeout);
+    std::map<int, std::vector<Endpoint>> eps;
+    std::vector<ShardMeta> metas;
+    for (auto& kv : listing) {
+      for (auto& e : kv.second) eps[kv.first].push_back(e.first);
+      metas.push_back(kv.second.front().second);
+    }
+    clients_.reset(new RpcClients(eps, co));
+    shards = static_cast<int64_t>(listing.size());
+    env_.shard_num = static_cast<int>(shards);
+    env_.num_partitions = std::max<uint32_t>(1, metas[0].num_partitions);
+    env_.index_info = metas[0].index_info;
+    meta_.Parse(metas[0].graph_meta.data(), metas[0].graph_meta.size());
+    FillWeightTables(metas);
+  } else {
+    return Status::InvalidArgument("unknown mode " + mode_);
+  }
+  env_.clients = clients_.get();
+  copt_.mode = CompileMode::kDistribute;
+  copt_.shard_num = env_.shard_num;
+  copt_.neighbor_indexes.clear();
+  for (auto& item : Split(env_.index_info, ",")) {
+    auto p = Split(item, ":");
+    if (p.size() == 2 && p[1] == "hash_range_index") copt_.neighbor_indexes.push_back(p[0]);
+  }
+  return Status::OK();
+}
+
+Status QueryProxy::InitWithGraph(std::unique_ptr<Graph> g, std::unique_ptr<IndexManager> idx) {
+  mode_ = "local";
+  graph_ = std::move(g);
+  index_ = idx ? std::move(idx) : std::unique_ptr<IndexManager>(new IndexManager);
+  auto e = MakeEnv(graph_.get(), index_.get(), 1);
+  env_ = *e;
+  meta_ = graph_->meta();
+  ShardMeta m = ShardMeta::FromEnv(env_, 0, 1);
+  FillWeightTables({m});
+  copt_.mode = CompileMode::kLocal;
+  copt_.shard_num = 1;
+  return Status::OK();
+}
+
+Status QueryProxy::Run(const std::string& gql, const std::vector<std::pair<std::string, Tensor>>& inputs,
+                       const std::vector<std::string>& outputs, std::vector<Tensor>* results) {
+  std::shared_ptr<const DAGDef> dag;
+  EULER_RETURN_IF_ERROR(Compiler::Get().Compile(gql, copt_, &dag));
+  return ExecuteDag(&env_, *dag, inputs, outputs, results);
+}
+
+Status QueryProxy::Explain(const std::string& gql, std::string* out) {
+  std::shared_ptr<const DAGDef> dag;
+  EULER_RETURN_IF_ERROR(Compiler::Get().Compile(gql, copt_, &dag));
+  *out = dag->DebugString();
+  return Status::OK();
+}
+
+}  // namespace euler
