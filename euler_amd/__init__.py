@@ -1,5 +1,23 @@
 """euler_amd — an MI355X-native large-scale graph-learning framework with the
-capabilities of Euler-2.0 (renyi533/euler): C++ sharded graph engine + GQL,
-tf_euler-shaped Python API on PyTorch-ROCm, gfx950 HIP message-passing kernels and
-RCCL data/embedding parallelism."""
+capabilities of Euler-2.0 (renyi533/euler).
+
+Layers:
+  * C++ engine (``euler_amd._engine``): sharded columnar graph store, attribute
+    indexes, GQL compiler + dataflow executor, RPC graph servers;
+  * graph-query API with the reference's ``tf_euler`` names (this module's top level);
+  * message passing on hand-written gfx950 HIP kernels (``euler_amd.ops``), the
+    convolution / dataflow / encoder / solution libraries, estimators and the
+    model zoo, data parallelism and sharded embeddings over RCCL (``euler_amd.parallel``).
+"""
 __version__ = "0.1.0"
+
+from euler_amd.ops.base import (  # noqa: F401
+    GraphBuilder, get_engine, initialize_embedded_graph, initialize_graph, initialize_shared_graph, set_seed,
+    start_service, synthetic_graph, use_graph)
+from euler_amd.ops.graph_api import *  # noqa: F401,F403
+from euler_amd.ops.graph_api import __all__ as _graph_all
+
+start = start_service  # reference `euler.start(...)`
+
+__all__ = ["initialize_graph", "initialize_embedded_graph", "initialize_shared_graph", "use_graph", "get_engine",
+           "set_seed", "synthetic_graph", "GraphBuilder", "start_service", "start"] + list(_graph_all)

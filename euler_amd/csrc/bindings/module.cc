@@ -120,6 +120,22 @@ class Engine {
     return out;
   }
 
+  py::list RunOp(const std::string& op, py::dict inputs, const std::vector<std::string>& input_names,
+                 const std::vector<std::string>& attrs, int output_num) {
+    std::vector<std::pair<std::string, Tensor>> in;
+    for (auto kv : inputs) in.emplace_back(kv.first.cast<std::string>(), FromPy(kv.second));
+    std::vector<Tensor> res;
+    Status st;
+    {
+      py::gil_scoped_release nogil;
+      st = proxy_->RunOp(op, input_names, attrs, output_num, in, &res);
+    }
+    Throw(st);
+    py::list out;
+    for (auto& t : res) out.append(ToPy(t));
+    return out;
+  }
+
   std::string Explain(const std::string& gql) {
     std::string s;
     Throw(proxy_->Explain(gql, &s));
@@ -372,6 +388,8 @@ PYBIND11_MODULE(_engine, m) {
       .def_static("from_config", &Engine::FromConfig)
       .def("run", &Engine::Run, py::arg("gql"), py::arg("inputs"), py::arg("outputs"))
       .def("explain", &Engine::Explain)
+      .def("run_op", &Engine::RunOp, py::arg("op"), py::arg("inputs"), py::arg("input_names"), py::arg("attrs"),
+           py::arg("output_num"))
       .def("meta", &Engine::Meta)
       .def("summary", &Engine::Summary)
       .def("sample_node", &Engine::SampleNode)

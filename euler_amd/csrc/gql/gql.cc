@@ -162,6 +162,7 @@ struct Cursor {
 
 class Translator {
  public:
+  // nodes are referenced while later ones are appended: keep the storage stable
   Translator(const CompileOptions& opt, DAGDef* dag) : opt_(opt), dag_(dag) {}
 
   NodeDef& Add(const std::string& op) {
@@ -194,6 +195,8 @@ class Translator {
   }
 
   Status Run(const std::vector<GqlStep>& steps) {
+    // node references are held while later nodes are appended: keep storage stable
+    dag_->nodes.reserve(steps.size() * 8 + 8);
     Cursor c;
     for (size_t si = 0; si < steps.size(); ++si) {
       const GqlStep& s = steps[si];
@@ -409,6 +412,8 @@ class Optimizer {
   }
 
   void Run(const DAGDef& logical) {
+    // node references are held while more nodes are appended: reserve an upper bound
+    out_->nodes.reserve(logical.nodes.size() * (16 + 8 * static_cast<size_t>(std::max(1, opt_.shard_num))) + 16);
     for (auto& n : logical.nodes) next_id_ = std::max(next_id_, n.id + 1);
     for (const NodeDef& orig : logical.nodes) {
       NodeDef nd = orig;

@@ -781,6 +781,29 @@ Status QueryProxy::Run(const std::string& gql, const std::vector<std::pair<std::
   return ExecuteDag(&env_, *dag, inputs, outputs, results);
 }
 
+Status QueryProxy::RunOp(const std::string& op, const std::vector<std::string>& input_names,
+                         const std::vector<std::string>& attrs, int output_num,
+                         const std::vector<std::pair<std::string, Tensor>>& inputs, std::vector<Tensor>* results) {
+  DAGDef logical;
+  NodeDef nd;
+  nd.op = op;
+  nd.id = 1;
+  nd.inputs = input_names;
+  nd.attrs = attrs;
+  nd.output_num = output_num;
+  NodeDef as;
+  as.op = "AS";
+  as.id = 2;
+  as.attrs = {"__result"};
+  for (int k = 0; k < output_num; ++k) as.inputs.push_back(nd.Output(k));
+  logical.nodes = {nd, as};
+  DAGDef phys;
+  EULER_RETURN_IF_ERROR(Compiler::Get().Optimize(logical, copt_, &phys));
+  std::vector<std::string> outs;
+  for (int k = 0; k < output_num; ++k) outs.push_back("__result:" + std::to_string(k));
+  return ExecuteDag(&env_, phys, inputs, outs, results);
+}
+
 Status QueryProxy::Explain(const std::string& gql, std::string* out) {
   std::shared_ptr<const DAGDef> dag;
   EULER_RETURN_IF_ERROR(Compiler::Get().Compile(gql, copt_, &dag));

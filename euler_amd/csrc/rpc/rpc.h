@@ -173,6 +173,10 @@ class QueryProxy {
   Status Run(const std::string& gql, const std::vector<std::pair<std::string, Tensor>>& inputs,
              const std::vector<std::string>& outputs, std::vector<Tensor>* results);
   Status Explain(const std::string& gql, std::string* out);
+  // single-op query (reference Query(op, alias, n_out, inputs, attrs)), sharded like a GQL step
+  Status RunOp(const std::string& op, const std::vector<std::string>& input_names,
+               const std::vector<std::string>& attrs, int output_num,
+               const std::vector<std::pair<std::string, Tensor>>& inputs, std::vector<Tensor>* results);
   const GraphMeta& meta() const { return meta_; }
   Graph* local_graph() const { return graph_.get(); }
   IndexManager* index() const { return index_.get(); }

@@ -1,0 +1,98 @@
+"""Graph-engine session for the Python API (reference ``tf_euler/python/euler_ops/base.py``).
+
+``initialize_graph(config)`` takes a dict or a ``"k=v;k=v"`` string, exactly like the
+reference (``base.py:37-60``); keys: ``mode`` (local | remote | local_sharded),
+``data_path``, ``shard_num``, ``registry`` (shared directory or ``memory:<name>``; the
+reference's ``zk_server``/``zk_path`` are accepted and mapped to it), ``num_retries``,
+``bad_host_timeout``, ``num_channels_per_host``, ``seed``.
+
+Besides reference-format directories an engine can also adopt an in-process graph
+(``use_graph``): a ``GraphBuilder`` result or the native synthetic generator.
+"""
+from __future__ import annotations
+
+import threading
+
+from euler_amd.ops._native import engine as _engine_mod
+
+__all__ = ["initialize_graph", "initialize_embedded_graph", "initialize_shared_graph", "get_engine",
+           "use_graph", "set_seed", "synthetic_graph", "GraphBuilder", "start_service"]
+
+_ENGINE = None
+_LOCK = threading.Lock()
+
+
+def _parse(config):
+    if isinstance(config, dict):
+        return {str(k): str(v) for k, v in config.items()}
+    if isinstance(config, bytes):
+        config = config.decode()
+    if not isinstance(config, str):
+        raise TypeError("Expect str or dict for graph config, got {}.".format(type(config).__name__))
+    out = {}
+    for kv in config.split(";"):
+        if "=" in kv:
+            k, v = kv.split("=", 1)
+            out[k.strip()] = v.strip()
+    return out
+
+
+def initialize_graph(config) -> bool:
+    global _ENGINE
+    cfg = _parse(config)
+    if "registry" not in cfg and "zk_path" in cfg:
+        cfg["registry"] = cfg["zk_path"]
+    eng = _engine_mod().Engine.from_config(cfg)
+    with _LOCK:
+        _ENGINE = eng
+    return True
+
+
+def initialize_embedded_graph(data_dir, sampler_type="all", data_type="all") -> bool:
+    return initialize_graph({"mode": "local", "data_path": data_dir, "data_type": data_type,
+                             "sampler_type": sampler_type})
+
+
+def initialize_shared_graph(data_dir_or_registry, zk_addr=None, zk_path=None, shard_num=0, **kw) -> bool:
+    """Remote mode.  ``zk_path`` / the first argument name the shared registry directory."""
+    reg = zk_path or data_dir_or_registry
+    cfg = {"mode": "remote", "registry": reg, "shard_num": shard_num, "num_retries": kw.get("num_retries", 1)}
+    cfg.update({k: v for k, v in kw.items() if k != "num_retries"})
+    return initialize_graph(cfg)
+
+
+def use_graph(engine_obj):
+    """Make an already-built engine (builder / synthetic) the current graph."""
+    global _ENGINE
+    with _LOCK:
+        _ENGINE = engine_obj
+    return engine_obj
+
+
+def get_engine():
+    if _ENGINE is None:
+        raise RuntimeError("graph not initialized: call euler_amd.initialize_graph(...) first")
+    return _ENGINE
+
+
+def set_seed(seed: int):
+    _engine_mod().set_seed(int(seed))
+
+
+def synthetic_graph(num_nodes, avg_degree=10.0, max_degree=1024, node_types=1, edge_types=1, feature_dim=0,
+                    label_dim=0, seed=0, make_current=True):
+    e = _engine_mod().synthetic(int(num_nodes), float(avg_degree), int(max_degree), int(node_types),
+                                int(edge_types), int(feature_dim), int(label_dim), int(seed))
+    if make_current:
+        use_graph(e)
+    return e
+
+
+def GraphBuilder():
+    return _engine_mod().GraphBuilder()
+
+
+def start_service(data_path, shard_idx, shard_num, registry="", port=0, threads=32, host="127.0.0.1"):
+    """Start a graph shard server in this process (reference ``euler.start``)."""
+    return _engine_mod().GraphServer(data_path, int(shard_idx), int(shard_num), registry, int(port), int(threads),
+                                     host)
