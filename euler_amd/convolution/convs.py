@@ -1,0 +1,375 @@
+"""Message-passing convolutions (reference ``tf_euler/python/convolution/*.py``).
+
+Contract (unchanged from the reference ``conv.py:27-53``)::
+
+    out = conv(x, edge_index, size, edge_attr=None)
+
+* ``x = (x_target, x_source)``: rows of the smaller (target, ``size[0]``) and larger
+  (source, ``size[1]``) node sets of a dataflow block;
+* ``edge_index`` [2, E]: row 0 indexes targets, row 1 indexes sources;
+* every gather / scatter goes through :mod:`euler_amd.ops.mp_ops`, i.e. the gfx950
+  segment-reduce / edge-softmax kernels on GPU tensors.
+
+Destination CSRs are built once per ``edge_index`` and cached on the block
+(``SegmentIndex``), so the degree normalisations, softmax and aggregation of one
+layer all reuse one sort.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from euler_amd.ops import mp_ops
+from euler_amd.ops.mp_ops import SegmentIndex
+from euler_amd.utils.layers import Dense
+
+__all__ = ["Conv", "GCNConv", "SAGEConv", "GATConv", "TAGConv", "AGNNConv", "SGCNConv", "GINConv", "GraphConv",
+           "APPNPConv", "ARMAConv", "DNAConv", "RelationConv", "GatedConv", "restricted_softmax"]
+
+
+def _seg(edge_index, i, size):
+    """destination CSR of edge_index[i] (cached on the tensor object)."""
+    key = "_euler_seg%d_%d" % (i, int(size))
+    cache = getattr(edge_index, "_euler_cache", None)
+    if cache is None:
+        cache = {}
+        try:
+            edge_index._euler_cache = cache
+        except AttributeError:
+            pass
+    if key not in cache:
+        cache[key] = SegmentIndex(edge_index[i], int(size))
+    return cache[key]
+
+
+class Conv(nn.Module):
+    def __init__(self, aggr="add"):
+        super().__init__()
+        assert aggr in ("add", "mean", "max")
+        self.aggr = aggr
+
+    @staticmethod
+    def gather_feature(features, edge_index):
+        out = []
+        for feature in features:
+            assert isinstance(feature, (tuple, list)) and len(feature) == 2
+            feature = list(feature)
+            if feature[1] is None:
+                feature[1] = feature[0]
+            out.append([None if t is None else mp_ops.gather(t, edge_index[i]) for i, t in enumerate(feature)])
+        return out
+
+    def scatter(self, values, edge_index, size, aggr=None):
+        return mp_ops.scatter_(aggr or self.aggr, values, _seg(edge_index, 0, size[0]), size[0])
+
+    @staticmethod
+    def norm(edge_index, size):
+        """deg^-1/2 on both ends (reference gcn_conv.py:32-40)."""
+        ones = torch.ones(edge_index.shape[1], 1, device=edge_index.device)
+
+        def dis(i):
+            deg = mp_ops.scatter_add(ones, _seg(edge_index, i, size[i]), size[i])
+            return deg.clamp(min=1e-12).pow(-0.5)
+
+        return dis(0), dis(1)
+
+    def apply_edge(self, x_j):
+        return x_j
+
+    def apply_node(self, aggr_out):
+        return aggr_out
+
+
+def _pair(x):
+    return list(x) if isinstance(x, (list, tuple)) else [x, None]
+
+
+class GCNConv(Conv):
+    def __init__(self, dim, **kwargs):
+        super().__init__("add")
+        self.fc = Dense(dim, use_bias=False)
+
+    def forward(self, x, edge_index, size=None, **kwargs):
+        x = _pair(x)
+        n0, n1 = self.norm(edge_index, size)
+        src = x[1] if x[1] is not None else x[0]
+        out = mp_ops.gather(n0, edge_index[0]) * mp_ops.gather(n1, edge_index[1]) * mp_ops.gather(src, edge_index[1])
+        return self.fc(self.scatter(out, edge_index, size))
+
+
+class SAGEConv(Conv):
+    """self_fc(x) + neigh_fc(mean_j x_j) (reference sage_conv.py:26-44)."""
+
+    def __init__(self, dim, **kwargs):
+        super().__init__("mean")
+        self.self_fc = Dense(dim, use_bias=False)
+        self.neigh_fc = Dense(dim, use_bias=False)
+
+    def forward(self, x, edge_index, size=None, **kwargs):
+        x = _pair(x)
+        xs = x[1] if x[1] is not None else x[0]
+        agg = self.scatter(mp_ops.gather(xs, edge_index[1]), edge_index, size)
+        return self.self_fc(x[0]) + self.neigh_fc(agg)
+
+
+class GATConv(Conv):
+    """Single-head GAT (reference gat_conv.py:41-78); the logits softmax per destination
+    runs in the edge_softmax kernel."""
+
+    def __init__(self, dim, improved=False, aggr="add", **kwargs):
+        super().__init__(aggr)
+        self.dim = dim
+        self.improved = improved
+        self.fc = Dense(dim, use_bias=False)
+        self.att_i = Dense(1, use_bias=False)
+        self.att_j = Dense(1, use_bias=False)
+
+    def forward(self, x, edge_index, size=None, **kwargs):
+        x = _pair(x)
+        x = [None if t is None else self.fc(t) for t in x]
+        gx = self.gather_feature([x], edge_index)[0]
+        x_i, x_j = gx
+        alpha = F.leaky_relu(self.att_i(x_i) + self.att_j(x_j), 0.2)
+        alpha = mp_ops.scatter_softmax(alpha, _seg(edge_index, 0, size[0]), size[0])
+        out = self.scatter(x_j * alpha.reshape(-1, 1), edge_index, size)
+        if self.improved:
+            out = x[0] + out
+        return out
+
+
+class TAGConv(Conv):
+    def __init__(self, dim, K=3, **kwargs):
+        super().__init__("add")
+        self.K = K
+        self.fc = Dense(dim, use_bias=False)
+
+    def forward(self, x, edge_index, size=None, **kwargs):
+        x = _pair(x)
+        n0, n1 = self.norm(edge_index, size)
+        gi, gj = mp_ops.gather(n0, edge_index[0]), mp_ops.gather(n1, edge_index[1])
+        xs = [x[0]]
+        src = x[1] if x[1] is not None else x[0]
+        for _ in range(self.K):
+            xj = mp_ops.gather(src, edge_index[1])
+            xs.append(self.scatter(gi * gj * xj, edge_index, size))
+        return self.fc(torch.cat(xs, -1))
+
+
+class AGNNConv(Conv):
+    def __init__(self, dim=None, **kwargs):
+        super().__init__("add")
+        self.beta = nn.Parameter(torch.ones(1))
+
+    def forward(self, x, edge_index, size=None, **kwargs):
+        x = _pair(x)
+        norm = [None if t is None else F.normalize(t, dim=-1) for t in x]
+        gx, gn = self.gather_feature([x, norm], edge_index)
+        alpha = (self.beta * gn[0] * gn[1]).sum(-1, keepdim=True)
+        alpha = mp_ops.scatter_softmax(alpha, _seg(edge_index, 0, size[0]), size[0])
+        return self.scatter(gx[1] * alpha.reshape(-1, 1), edge_index, size)
+
+
+class SGCNConv(Conv):
+    def __init__(self, dim, K=1, **kwargs):
+        super().__init__("add")
+        self.K = K
+        self.fc = Dense(dim, use_bias=False)
+
+    def forward(self, x, edge_index, size=None, **kwargs):
+        x = _pair(x)
+        n0, n1 = self.norm(edge_index, size)
+        gi, gj = mp_ops.gather(n0, edge_index[0]), mp_ops.gather(n1, edge_index[1])
+        out = x[0]
+        src = x[1] if x[1] is not None else x[0]
+        for _ in range(self.K):
+            out = self.scatter(gi * gj * mp_ops.gather(src, edge_index[1]), edge_index, size)
+        return self.fc(out)
+
+
+class GINConv(Conv):
+    def __init__(self, dim, mlp=None, eps=0.0, train_eps=True, **kwargs):
+        super().__init__("add")
+        self.mlp = mlp if mlp is not None else Dense(dim, use_bias=False)
+        if train_eps:
+            self.eps = nn.Parameter(torch.tensor([float(eps)]))
+        else:
+            self.register_buffer("eps", torch.tensor([float(eps)]))
+
+    def forward(self, x, edge_index, size=None, **kwargs):
+        x = _pair(x)
+        src = x[1] if x[1] is not None else x[0]
+        agg = self.scatter(mp_ops.gather(src, edge_index[1]), edge_index, size)
+        return self.mlp((1 + self.eps) * x[0] + agg)
+
+
+class GraphConv(Conv):
+    def __init__(self, dim, **kwargs):
+        super().__init__("mean")
+        self.fc = Dense(dim, use_bias=False)
+        self.liner = Dense(dim, use_bias=True)
+
+    def forward(self, x, edge_index, size=None, **kwargs):
+        x = _pair(x)
+        src = x[1] if x[1] is not None else x[0]
+        agg = self.scatter(mp_ops.gather(self.fc(src), edge_index[1]), edge_index, size)
+        return self.liner(x[0]) + agg
+
+
+class APPNPConv(Conv):
+    def __init__(self, dim, K=10, alpha=0.1, **kwargs):
+        super().__init__("add")
+        self.K = K
+        self.alpha = alpha
+
+    def forward(self, x, edge_index, size=None, **kwargs):
+        x = _pair(x)
+        hidden = list(x)
+        n0, n1 = self.norm(edge_index, size)
+        gi, gj = mp_ops.gather(n0, edge_index[0]), mp_ops.gather(n1, edge_index[1])
+        cur = x
+        out = x[0]
+        for _ in range(self.K):
+            src = cur[1] if cur[1] is not None else cur[0]
+            out = self.scatter(gi * gj * mp_ops.gather(src, edge_index[1]), edge_index, size)
+            out = out * (1 - self.alpha) + self.alpha * hidden[0]
+            cur = [out, hidden[1]]
+        return out
+
+
+class ARMAConv(Conv):
+    def __init__(self, dim, K=1, num_layers=1, shared_weights=False, act=F.relu, **kwargs):
+        super().__init__("add")
+        self.K, self.T, self.dim = K, num_layers, dim
+        self.shared_weights = shared_weights
+        self.act = act
+        n = 1 if shared_weights else num_layers
+        self.ws = nn.ModuleList([Dense(K * dim, use_bias=False) for _ in range(n)])
+        self.vs = nn.ModuleList([Dense(K * dim, use_bias=False) for _ in range(n)])
+
+    def forward(self, x, edge_index, size=None, **kwargs):
+        x = _pair(x)
+        origin = list(x)
+        n0, n1 = self.norm(edge_index, size)
+        gi, gj = mp_ops.gather(n0, edge_index[0]), mp_ops.gather(n1, edge_index[1])
+        cur = x
+        out = None
+        for t in range(self.T):
+            k = 0 if self.shared_weights else t
+            src = cur[1] if cur[1] is not None else cur[0]
+            xj = self.ws[k](mp_ops.gather(src, edge_index[1]))
+            out = self.scatter(gi * gj * xj, edge_index, size) + self.vs[k](origin[0])
+            if self.act is not None:
+                out = self.act(out)
+            cur = [out, origin[1]]
+        return out.reshape(-1, self.K, self.dim).mean(1)
+
+
+class GroupDense(nn.Module):
+    """Grouped linear (reference dna_conv.py GroupDense)."""
+
+    def __init__(self, dim, groups=1, use_bias=True):
+        super().__init__()
+        self.dim, self.groups = dim, groups
+        self.kernel = nn.UninitializedParameter()
+        self.bias = nn.Parameter(torch.zeros(dim)) if use_bias else None
+
+    def forward(self, x):
+        if isinstance(self.kernel, nn.UninitializedParameter):
+            self.kernel.materialize((self.groups, x.shape[-1] // self.groups, self.dim // self.groups),
+                                    device=x.device)
+            with torch.no_grad():
+                nn.init.xavier_uniform_(self.kernel.view(-1, self.dim // self.groups))
+        shp = x.shape
+        xg = x.reshape(-1, self.groups, shp[-1] // self.groups).transpose(0, 1)
+        out = torch.bmm(xg, self.kernel).transpose(0, 1).reshape(*shp[:-1], self.dim)
+        return out + self.bias if self.bias is not None else out
+
+
+def restricted_softmax(inputs, dim=-1, margin=0.0):
+    m = inputs.max(dim=dim, keepdim=True).values.clamp(min=0)
+    out = torch.exp(inputs - m)
+    return out / (out.sum(dim=dim, keepdim=True) + torch.exp(margin - m))
+
+
+class DNAConv(Conv):
+    def __init__(self, dim, heads=1, groups=1, use_bias=True, **kwargs):
+        super().__init__("mean")
+        assert dim % heads == 0 and dim % groups == 0
+        self.dim, self.heads, self.groups = dim, heads, groups
+        self.in_fc = Dense(dim, use_bias=False)
+        self.lin_q = GroupDense(dim, groups, use_bias)
+        self.lin_k = GroupDense(dim, groups, use_bias)
+        self.lin_v = GroupDense(dim, groups, use_bias)
+
+    def multi_head(self, q, k, v):  # [E, 1, D]
+        q, k, v = self.lin_q(q), self.lin_k(k), self.lin_v(v)
+        E = q.shape[0]
+        ch = self.dim // self.heads
+        q = q.reshape(E, -1, self.heads, ch).transpose(1, 2)
+        k = k.reshape(E, -1, self.heads, ch).transpose(1, 2)
+        v = v.reshape(E, -1, self.heads, ch).transpose(1, 2)
+        s = restricted_softmax(q @ k.transpose(-1, -2) / math.sqrt(ch), dim=-1)
+        return (s @ v).transpose(1, 2).reshape(E, -1, self.dim)
+
+    def forward(self, x, edge_index, size=None, **kwargs):
+        x = _pair(x)
+        x = [None if t is None else self.in_fc(t) for t in x]
+        n0, n1 = self.norm(edge_index, size)
+        gx, gn = self.gather_feature([x, [n0, n1]], edge_index)
+        out = self.multi_head(gx[0].unsqueeze(1), gx[1].unsqueeze(1), gx[1].unsqueeze(1)).squeeze(1)
+        return self.scatter(gn[0] * gn[1] * out, edge_index, size)
+
+
+class RelationConv(Conv):
+    """R-GCN relation transform (reference relation_conv.py:33-73).  Instead of gathering
+    an [E, dim, fea_dim] matrix per edge, edges are grouped by relation and each group
+    does one GEMM."""
+
+    def __init__(self, fea_dim, dim, metapath=None, total_relation_num=1, **kwargs):
+        super().__init__("mean")
+        self.fea_dim, self.dim, self.relation_num = fea_dim, dim, total_relation_num
+        self.matrix = nn.Parameter(torch.empty(total_relation_num, dim, fea_dim))
+        nn.init.kaiming_uniform_(self.matrix.view(total_relation_num * dim, fea_dim), a=math.sqrt(5))
+        self.fc = Dense(dim, use_bias=False)
+
+    def forward(self, x, edge_index, size=None, edge_attr=None, **kwargs):
+        assert edge_attr is not None
+        x = _pair(x)
+        src = x[1] if x[1] is not None else x[0]
+        xj = mp_ops.gather(src, edge_index[1])
+        rel = edge_attr.reshape(-1).long()
+        out = torch.zeros(xj.shape[0], self.dim, dtype=xj.dtype, device=xj.device)
+        for r in torch.unique(rel).tolist():
+            sel = (rel == r).nonzero(as_tuple=True)[0]
+            out[sel] = xj[sel] @ self.matrix[int(r)].t().to(xj.dtype)
+        return self.fc(x[0]) + self.scatter(out, edge_index, size)
+
+
+class GatedConv(Conv):
+    """Gated graph conv with a stacked GRU (reference gated_graph_conv.py:26-60)."""
+
+    def __init__(self, dim, processing_steps=2, lstm_layers=2, **kwargs):
+        super().__init__("add")
+        self.dim = dim
+        self.steps = processing_steps
+        self.layers = lstm_layers
+        self.fc = nn.ModuleList([Dense(dim, use_bias=False) for _ in range(processing_steps)])
+        self.cells = nn.ModuleList([nn.GRUCell(dim, dim) for _ in range(lstm_layers)])
+
+    def forward(self, x, edge_index, size=None, **kwargs):
+        h = _pair(x)
+        out = None
+        for i in range(self.steps):
+            src = h[1] if h[1] is not None else h[0]
+            m = mp_ops.gather(self.fc[i](src), edge_index[1])
+            out = self.scatter(m, edge_index, size)
+            state = h[0]
+            inp = out
+            for cell in self.cells:
+                inp = cell(inp, state)
+            out = inp
+            h = [out, h[1]]
+        return out

