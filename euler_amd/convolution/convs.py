@@ -27,7 +27,7 @@ from euler_amd.ops.mp_ops import SegmentIndex
 from euler_amd.utils.layers import Dense
 
 __all__ = ["Conv", "GCNConv", "SAGEConv", "GATConv", "TAGConv", "AGNNConv", "SGCNConv", "GINConv", "GraphConv",
-           "APPNPConv", "ARMAConv", "DNAConv", "RelationConv", "GatedConv", "restricted_softmax"]
+           "APPNPConv", "ARMAConv", "DNAConv", "RelationConv", "GatedConv", "MultiHeadGATConv", "restricted_softmax"]
 
 
 def _seg(edge_index, i, size):
@@ -373,3 +373,45 @@ class GatedConv(Conv):
             out = inp
             h = [out, h[1]]
         return out
+
+
+class MultiHeadGATConv(Conv):
+    """All GAT heads in one pass (the reference builds ``head_num`` separate GATConv
+    objects and concatenates, examples/gat/gat.py:56-70).
+
+    One GEMM projects to ``[N, H*C]``; the ``[E, H]`` logits go through ONE
+    edge-softmax launch (the kernel treats the H columns as independent softmaxes);
+    one gather + one segment-sum aggregate every head.  ``concat=False`` averages the
+    heads (the reference's reshape-then-mean over the feature axis is a bug, §2.10).
+    """
+
+    def __init__(self, dim, heads=1, concat=True, improved=False, negative_slope=0.2, **kwargs):
+        super().__init__("add")
+        if concat:
+            assert dim % heads == 0, "dim must be divisible by heads when concat=True"
+        self.heads, self.concat, self.improved = heads, concat, improved
+        self.ch = dim // heads if concat else dim
+        self.slope = negative_slope
+        self.fc = Dense(heads * self.ch, use_bias=False)
+        self.att_i = nn.Parameter(torch.empty(heads, self.ch))
+        self.att_j = nn.Parameter(torch.empty(heads, self.ch))
+        nn.init.xavier_uniform_(self.att_i)
+        nn.init.xavier_uniform_(self.att_j)
+
+    def forward(self, x, edge_index, size=None, **kwargs):
+        x = _pair(x)
+        H, Ch = self.heads, self.ch
+        h_dst = self.fc(x[0])
+        h_src = self.fc(x[1]) if x[1] is not None else h_dst
+        a_i = (h_dst.view(-1, H, Ch) * self.att_i.to(h_dst.dtype)).sum(-1)
+        a_j = (h_src.view(-1, H, Ch) * self.att_j.to(h_src.dtype)).sum(-1)
+        logit = F.leaky_relu(mp_ops.gather(a_i, edge_index[0]) + mp_ops.gather(a_j, edge_index[1]), self.slope)
+        seg = _seg(edge_index, 0, size[0])
+        alpha = mp_ops.scatter_softmax(logit, seg, size[0])  # [E, H]
+        msg = mp_ops.gather(h_src, edge_index[1]).view(-1, H, Ch) * alpha.unsqueeze(-1)
+        out = mp_ops.scatter_add(msg.reshape(-1, H * Ch), seg, size[0])
+        if self.improved:
+            out = out + h_dst
+        if self.concat:
+            return out
+        return out.view(-1, H, Ch).mean(1)

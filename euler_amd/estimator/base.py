@@ -1,0 +1,333 @@
+"""Training loop (reference ``euler_estimator/python/base_estimator.py:28-188``).
+
+``tf.estimator`` gave the reference: a model_fn per mode, a global step, optimizer
+``minimize``, ``LoggingTensorHook`` every ``log_steps``, checkpoints under
+``model_dir`` with auto-resume, and ``predict`` writing ``embedding_<worker>.npy`` /
+``ids_<worker>.npy``.  This module provides the same contract on PyTorch-ROCm:
+
+* ``train()``  — sample -> model -> loss -> backward -> (RCCL bucketed gradient
+  all-reduce, overlapped with backward) -> optimizer; logs ``step/loss/<metric>`` and
+  samples/s every ``log_steps``; checkpoints every ``save_checkpoints_steps`` and at
+  the end (``model_dir/model.ckpt-<step>.pt`` + a ``checkpoint`` index file naming
+  the latest, pruned to ``keep_checkpoint_max``); resumes from the latest checkpoint.
+* ``evaluate()`` — streams the id file, logs loss + running metric per batch,
+  returns the final values.
+* ``infer()``  — streams the id file, writes ``embedding_<rank>.npy`` and
+  ``ids_<rank>.npy`` into ``infer_dir``.
+
+Parameters (``params`` dict, reference names): ``model_dir``, ``batch_size``,
+``total_step``, ``optimizer``, ``learning_rate``, ``log_steps``, ``id_file``,
+``infer_dir``; extras: ``device``, ``amp`` ("bf16" runs the model under bf16
+autocast), ``save_checkpoints_steps``, ``keep_checkpoint_max``, ``seed``.
+"""
+from __future__ import annotations
+
+import glob
+import logging
+import os
+import re
+import time
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from euler_amd.parallel import dp
+from euler_amd.parallel.embedding import is_sharded
+from euler_amd.utils.misc import get_optimizer
+
+__all__ = ["BaseEstimator", "latest_checkpoint", "id_file_batches"]
+
+log = logging.getLogger("euler_amd.estimator")
+
+
+def latest_checkpoint(model_dir):
+    idx = os.path.join(model_dir, "checkpoint")
+    if os.path.exists(idx):
+        with open(idx) as f:
+            for line in f:
+                m = re.match(r'model_checkpoint_path:\s*"?([^"\n]+)"?', line.strip())
+                if m:
+                    p = m.group(1)
+                    p = p if os.path.isabs(p) else os.path.join(model_dir, p)
+                    if os.path.exists(p):
+                        return p
+    cks = glob.glob(os.path.join(model_dir, "model.ckpt-*.pt"))
+    if not cks:
+        return None
+    return max(cks, key=lambda p: int(re.search(r"model\.ckpt-(\d+)\.pt$", p).group(1)))
+
+
+def id_file_batches(path, batch_size, parse=int, shard=(0, 1)):
+    """Batches of parsed lines of a text file (reference ``TextLineDataset.batch``).
+
+    ``shard=(rank, world)`` gives each data-parallel worker every world-th batch.
+    """
+    rk, ws = shard
+    batch, bi = [], 0
+    with open(path) as f:
+        for line in f:
+            line = line.strip()
+            if not line:
+                continue
+            batch.append(parse(line))
+            if len(batch) == batch_size:
+                if bi % ws == rk:
+                    yield batch
+                batch, bi = [], bi + 1
+    if batch and bi % ws == rk:
+        yield batch
+
+
+class BaseEstimator:
+    def __init__(self, model_fn, params, run_config=None, profiling=False):
+        self.model = model_fn
+        self.params = dict(params)
+        self.run_config = dict(run_config or {})
+        self.profiling = profiling
+        self.evaluate_stop_onetime = False
+        dev = self.params.get("device")
+        if dev is None:
+            dev = "cuda" if torch.cuda.is_available() else "cpu"
+        self.device = torch.device(dev)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", 0)))
+        self.rank, self.world = dp.rank(), dp.world_size()
+        self.global_step = 0
+        self.optimizer = None
+        self._sync = None
+
+    # ------------------------------------------------------------------ hooks (reference names)
+    def get_train_from_input(self, inputs, params):
+        return inputs
+
+    def get_evaluate_from_input(self, inputs, params):
+        return inputs
+
+    def get_infer_from_input(self, inputs, params):
+        return inputs
+
+    def transfer_embedding(self, source, emb):
+        return source, emb
+
+    def train_input_fn(self):
+        raise NotImplementedError
+
+    def evaluate_input_fn(self):
+        raise NotImplementedError
+
+    def infer_input_fn(self):
+        return self.evaluate_input_fn()
+
+    # ------------------------------------------------------------------ helpers
+    @property
+    def model_dir(self):
+        return self.params.get("model_dir", "ckpt")
+
+    def _autocast(self):
+        amp = self.params.get("amp")
+        if amp in ("bf16", "bfloat16") and self.device.type == "cuda":
+            return torch.autocast("cuda", dtype=torch.bfloat16)
+        return torch.autocast("cpu", enabled=False)
+
+    def _run_model(self, source):
+        with self._autocast():
+            return self.model(source)
+
+    def _extra_losses(self):
+        total = None
+        for m in self.model.modules():
+            sl = getattr(m, "store_loss", None)
+            if isinstance(sl, torch.Tensor):
+                total = sl if total is None else total + sl
+        return total
+
+    def _after_backward(self):
+        for m in self.model.modules():
+            fn = getattr(m, "after_backward", None)
+            if callable(fn) and m is not self.model:
+                fn()
+
+    def _prepare(self, source):
+        """Move the model, materialise lazy parameters with one no-grad pass,
+        broadcast rank 0's initial weights, build the optimizer and gradient sync."""
+        self.model.to(self.device)
+        if any(isinstance(p, nn.parameter.UninitializedParameter) for p in self.model.parameters()):
+            was = self.model.training
+            with torch.no_grad():
+                self._run_model(source)
+            self.model.train(was)
+            for m in self.model.modules():
+                if hasattr(m, "_pending"):
+                    m._pending = None
+            self.model.to(self.device)
+        dp.broadcast_module(self.model)
+        params = [p for p in self.model.parameters() if p.requires_grad]
+        name = self.params.get("optimizer", "adam")
+        self.optimizer = get_optimizer(name)(params, self.params.get("learning_rate", 0.001))
+        dense = [p for p in params if not is_sharded(p)]
+        self._sync = dp.GradSync(dense, bucket_bytes=int(self.params.get("bucket_bytes", 32 << 20)))
+
+    def save(self, step=None):
+        step = self.global_step if step is None else step
+        if self.rank != 0 and not any(is_sharded(p) for p in self.model.parameters()):
+            return None
+        os.makedirs(self.model_dir, exist_ok=True)
+        suffix = "" if self.world == 1 or self.rank == 0 else "-rank%d" % self.rank
+        path = os.path.join(self.model_dir, "model.ckpt-%d%s.pt" % (step, suffix))
+        model_state = {k: v for k, v in self.model.state_dict().items()
+                       if not isinstance(v, nn.parameter.UninitializedParameter)}  # never-called lazy layers
+        state = {"step": step, "model": model_state,
+                 "optimizer": self.optimizer.state_dict() if self.optimizer is not None else None,
+                 "world": self.world}
+        tmp = path + ".tmp"
+        torch.save(state, tmp)
+        os.replace(tmp, path)
+        if self.rank == 0:
+            with open(os.path.join(self.model_dir, "checkpoint"), "w") as f:
+                f.write('model_checkpoint_path: "%s"\n' % os.path.basename(path))
+            keep = int(self.run_config.get("keep_checkpoint_max", self.params.get("keep_checkpoint_max", 5)))
+            cks = sorted(glob.glob(os.path.join(self.model_dir, "model.ckpt-*.pt")),
+                         key=lambda p: int(re.search(r"model\.ckpt-(\d+)", p).group(1)))
+            for old in cks[:-keep] if keep > 0 else []:
+                if not old.endswith(os.path.basename(path)):
+                    os.remove(old)
+        return path
+
+    def restore(self, path=None, strict=True):
+        path = path or latest_checkpoint(self.model_dir)
+        if path is None:
+            return False
+        if self.world > 1 and self.rank != 0:
+            own = path.replace(".pt", "-rank%d.pt" % self.rank)
+            if os.path.exists(own):
+                path = own
+        state = torch.load(path, map_location=self.device, weights_only=True)
+        self.model.load_state_dict(state["model"], strict=strict)
+        if self.optimizer is not None and state.get("optimizer") is not None:
+            self.optimizer.load_state_dict(state["optimizer"])
+        self.global_step = int(state["step"])
+        log.info("restored %s at step %d", path, self.global_step)
+        return True
+
+    # ------------------------------------------------------------------ modes
+    def train(self):
+        seed = self.params.get("seed")
+        if seed is not None:
+            torch.manual_seed(int(seed) + self.rank)
+        total = self.params.get("total_step")
+        total = int(total) if total is not None else 1
+        log_steps = int(self.params.get("log_steps", 100))
+        save_steps = int(self.run_config.get("save_checkpoints_steps", self.params.get("save_checkpoints_steps", 0))
+                         or 0)
+        inputs = self.train_input_fn()
+        first = self.get_train_from_input(inputs, self.params)
+        self.model.train()
+        self._prepare(first)
+        self.restore()
+        if self.global_step >= total:
+            log.info("already trained to step %d", self.global_step)
+            return {}
+        pending = first
+        t0, n0 = time.time(), self.global_step
+        last = {}
+        prof = None
+        if self.profiling:
+            prof = torch.profiler.profile(schedule=torch.profiler.schedule(wait=5, warmup=5, active=20),
+                                          on_trace_ready=torch.profiler.tensorboard_trace_handler("prof_dir"))
+            prof.start()
+        while self.global_step < total:
+            source = pending if pending is not None else self.get_train_from_input(inputs, self.params)
+            pending = None
+            _, loss, metric_name, metric = self._run_model(source)
+            extra = self._extra_losses()
+            obj = loss if extra is None else loss + extra
+            self.optimizer.zero_grad(set_to_none=False)
+            obj.backward()
+            self._after_backward()
+            self._sync.finish()
+            self.optimizer.step()
+            self.global_step += 1
+            if prof is not None:
+                prof.step()
+            if self.global_step % log_steps == 0 or self.global_step == total:
+                dt = max(time.time() - t0, 1e-9)
+                rate = (self.global_step - n0) * int(self.params.get("batch_size", 1)) / dt
+                last = {"step": self.global_step, "loss": float(loss.detach()), metric_name: float(metric),
+                        "samples_per_sec": rate}
+                if self.rank == 0:
+                    log.info("step = %d, loss = %.6f, %s = %.6f (%.1f samples/s)", self.global_step, last["loss"],
+                             metric_name, last[metric_name], rate)
+                t0, n0 = time.time(), self.global_step
+            if save_steps and self.global_step % save_steps == 0:
+                self.save()
+        if prof is not None:
+            prof.stop()
+        self.save()
+        dp.barrier()
+        return last
+
+    def _eval_batches(self):
+        return self.evaluate_input_fn()
+
+    @torch.no_grad()
+    def evaluate(self):
+        self.model.to(self.device)
+        batches = iter(self._eval_batches())
+        first = next(batches, None)
+        if first is None:
+            return {}
+        src = self.get_evaluate_from_input(first, self.params)
+        self.model.eval()
+        if any(isinstance(p, nn.parameter.UninitializedParameter) for p in self.model.parameters()):
+            self._run_model(src)
+        self.restore(strict=False)
+        for m in self.model.modules():
+            met = getattr(m, "metric", None)
+            if met is not None and hasattr(met, "reset"):
+                met.reset()
+        res = {}
+        steps = 0
+        losses = []
+        while src is not None:
+            _, loss, name, metric = self._run_model(src)
+            losses.append(float(loss))
+            res = {"loss": float(np.mean(losses)), name: float(metric)}
+            steps += 1
+            if self.evaluate_stop_onetime:
+                break
+            nxt = next(batches, None)
+            src = None if nxt is None else self.get_evaluate_from_input(nxt, self.params)
+        if self.rank == 0:
+            log.info("evaluate: %s over %d batches", res, steps)
+        return res
+
+    @torch.no_grad()
+    def infer(self):
+        self.model.to(self.device)
+        self.model.eval()
+        ids_out, emb_out = [], []
+        restored = False
+        for batch in self.infer_input_fn():
+            src = self.get_infer_from_input(batch, self.params)
+            if not restored:
+                if any(isinstance(p, nn.parameter.UninitializedParameter) for p in self.model.parameters()):
+                    self._run_model(src)
+                self.restore(strict=False)
+                restored = True
+            emb, _, _, _ = self._run_model(src)
+            s, e = self.transfer_embedding(src, emb)
+            ids_out.append(np.asarray(torch.as_tensor(s).detach().cpu()))
+            emb_out.append(torch.as_tensor(e).detach().float().cpu().numpy())
+        out_dir = self.params.get("infer_dir", self.model_dir)
+        os.makedirs(out_dir, exist_ok=True)
+        ids = np.concatenate(ids_out, 0) if ids_out else np.zeros((0,), np.int64)
+        embs = np.concatenate(emb_out, 0) if emb_out else np.zeros((0, 0), np.float32)
+        np.save(os.path.join(out_dir, "embedding_%d.npy" % self.rank), embs)
+        np.save(os.path.join(out_dir, "ids_%d.npy" % self.rank), ids)
+        return ids, embs
+
+    def train_and_evaluate(self):
+        res = self.train()
+        ev = self.evaluate()
+        return res, ev

@@ -30,11 +30,17 @@ __all__ = ["ShallowEncoder", "GCNEncoder", "GenieEncoder", "ScalableGCNEncoder",
 
 
 def module_device(m: nn.Module) -> torch.device:
-    for p in m.parameters():
-        return p.device
     for b in m.buffers():
         return b.device
+    for p in m.parameters():
+        return p.device
     return getattr(m, "_device_hint", torch.device("cpu"))
+
+
+def _shaped(inputs, out):
+    """reshape [n, d] -> inputs.shape + [d] (the reference's output_shape idiom)."""
+    shape = tuple(torch.as_tensor(inputs).shape)
+    return out.reshape(*shape, out.shape[-1])
 
 
 def _as_list(x, n=None):
@@ -83,7 +89,9 @@ class ShallowEncoder(nn.Module):
         self.feature_idx, self.feature_dim = feature_idx, feature_dim
         self.sparse_feature_idx, self.sparse_feature_max_id = sparse_feature_idx, sparse_feature_max_id
         self.embedding_dim = embedding_dim
-        if dim:
+        # follows .to(device) even when the encoder has no parameters (features only)
+        self.register_buffer("_device_anchor", torch.empty(0), persistent=False)
+        if dim and (combiner == "concat" or use_feature):  # only when forward() uses it
             self.dense = Dense(dim, use_bias=False)
         ed, uh = (list(embedding_dim), list(use_hash_embedding)) if n_emb else ([], [])
         if use_id:
@@ -175,7 +183,7 @@ class GCNEncoder(nn.Module):
     def forward(self, inputs):
         nodes, adjs = G.get_multi_hop_neighbor(inputs, self.metapath)
         hidden = self._propagate([self.node_encoder(n) for n in nodes], adjs)
-        return hidden[0]
+        return _shaped(inputs, hidden[0])
 
 
 class GenieEncoder(GCNEncoder):
@@ -202,7 +210,7 @@ class GenieEncoder(GCNEncoder):
             h_t.append(self.depth_fc[layer + 1](hidden[0]))
         seq = torch.stack(h_t, 1)  # [B, L+1, dim]
         out, _ = self.lstm(seq)
-        return out[:, 0, :]
+        return _shaped(inputs, out[:, 0, :])
 
 
 class _StoreMixin:
@@ -285,7 +293,7 @@ class ScalableGCNEncoder(_StoreMixin, GCNEncoder):
                 neigh_emb = self._lookup_neighbors(layer, neighbor)
                 leaves.append(neigh_emb)
         self._finish_training_forward(node, node_embs, neighbor, leaves)
-        return node_emb
+        return _shaped(inputs, node_emb)
 
 
 class SageEncoder(nn.Module):
@@ -336,7 +344,7 @@ class SageEncoder(nn.Module):
         return hidden[0]
 
     def forward(self, inputs):
-        return self._aggregate([self.node_encoder(s) for s in self._sample(inputs)])
+        return _shaped(inputs, self._aggregate([self.node_encoder(s) for s in self._sample(inputs)]))
 
 
 class ShuffleSageEncoder(SageEncoder):
@@ -367,7 +375,7 @@ class ShuffleSageEncoder(SageEncoder):
 
     def forward(self, inputs):
         samples = self._sample(inputs)
-        return [self.agg(samples, False), self.agg(samples, True)]
+        return [_shaped(inputs, self.agg(samples, False)), _shaped(inputs, self.agg(samples, True))]
 
 
 class SageEncoderNew(SageEncoder):
@@ -397,7 +405,7 @@ class SageEncoderNew(SageEncoder):
         for layer in range(self.num_layers + 1):
             embs = [e(sp) for e, sp in zip(self.sparse_embeddings, feats[layer * f:(layer + 1) * f])]
             hidden.append(torch.cat(embs, -1).reshape(-1, self.embedding_dim * f))
-        return self._aggregate(hidden)
+        return _shaped(inputs, self._aggregate(hidden))
 
 
 class ScalableSageEncoder(_StoreMixin, SageEncoder):
@@ -430,7 +438,7 @@ class ScalableSageEncoder(_StoreMixin, SageEncoder):
                 neigh_emb = self._lookup_neighbors(layer, neighbor)
                 leaves.append(neigh_emb)
         self._finish_training_forward(node, node_embs, neighbor, leaves)
-        return node_emb
+        return _shaped(inputs, node_emb)
 
 
 class LayerEncoder(SageEncoder):
@@ -461,7 +469,7 @@ class LayerEncoder(SageEncoder):
 
     def forward(self, inputs):
         hidden = [self.node_encoder(s) for s in self._sample(inputs)]
-        return self.fm(self.layerwise_embed(hidden))
+        return _shaped(inputs, self.fm(self.layerwise_embed(hidden)))
 
 
 class SparseSageEncoder(SageEncoder):
