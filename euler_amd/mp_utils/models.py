@@ -58,9 +58,8 @@ def get_flow_class(flow):
 
 
 def model_device(m: nn.Module):
-    for p in m.parameters():
-        if not isinstance(p, nn.parameter.UninitializedParameter):
-            return p.device
+    for p in m.parameters():  # lazy (uninitialized) parameters carry their device too
+        return p.device
     for b in m.buffers():
         return b.device
     return getattr(m, "_euler_device", torch.device("cpu"))

@@ -26,7 +26,7 @@ python -c "import torch; print(torch.__version__, torch.cuda.get_device_name(0))
 python -m euler_amd._build >"$OUT/build.log" 2>&1 || { cat "$OUT/build.log"; exit 4; }
 
 if [[ "$STEPS" == *tests* || "$STEPS" == all ]]; then
-  run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
+  run pytest_gpu 900 python -m pytest tests -m gpu --maxfail=20 -q -p no:cacheprovider -rf
 fi
 if [[ "$STEPS" == *bench* || "$STEPS" == all ]]; then
   run bench_small 400 python bench.py --num-nodes 2000000 --steps 50 --warmup 10 --log
