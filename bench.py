@@ -49,6 +49,9 @@ def parse_args(argv=None):
     p.add_argument("--lr", type=float, default=0.01)
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--no-graph", action="store_true", help="eager steps instead of hipGraph replay")
+    p.add_argument("--impl", choices=["fused", "autograd"], default="fused",
+                   help="fused = the 10-kernel gfx950 training step (models/sage_step.py); "
+                        "autograd = fused SAGE layers under torch autograd (models/fused_sage.py)")
     p.add_argument("--log", action="store_true")
     return p.parse_args(argv)
 
@@ -89,29 +92,47 @@ def main(argv=None):
 
     torch.manual_seed(args.seed)
     model = FusedSupervisedGraphSage(args.feature_dim, args.hidden_dim, args.label_dim, fanouts).to(dev)
-    flat = FlatParams(model.parameters(), dev)
-    if world > 1:
-        dist.broadcast(flat.flat, 0)
-    opt = FlatOptimizer(flat, "adam", args.lr)
     grad_scale = 1.0 / world
-    loss_buf = torch.zeros((), device=dev)
+    if args.impl == "fused":
+        from euler_amd.models.sage_step import FusedSageTrainer
 
-    def fwd_bwd():
-        graph.advance()
-        roots = graph.sample_node(B, stream_id=1)
-        levels, nbrs = model.sample(graph, roots)
-        logits = model(feats, levels, nbrs)
-        loss = model.loss(logits, labels[roots.long()])
-        flat.zero_grad()
-        loss.backward()
-        loss_buf.copy_(loss.detach())
+        trainer = FusedSageTrainer(graph, feats, labels, B, fanouts, args.hidden_dim, args.label_dim, lr=args.lr,
+                                   init_model=model)
+        if world > 1:
+            dist.broadcast(trainer.flat, 0)
+            trainer.refresh_shadows()
+        loss_buf = trainer.loss_out
+        grad_buf = trainer.grad
+
+        def fwd_bwd():
+            trainer.forward_backward()
+
+        def opt_step():
+            trainer.optimizer_step(grad_scale=grad_scale)
+    else:
+        flat = FlatParams(model.parameters(), dev)
+        if world > 1:
+            dist.broadcast(flat.flat, 0)
+        opt = FlatOptimizer(flat, "adam", args.lr)
+        loss_buf = torch.zeros((), device=dev)
+        grad_buf = flat.grad
+
+        def fwd_bwd():
+            graph.advance()
+            roots = graph.sample_node(B, stream_id=1)
+            levels, nbrs = model.sample(graph, roots)
+            logits = model(feats, levels, nbrs)
+            loss = model.loss(logits, labels[roots.long()])
+            flat.zero_grad()
+            loss.backward()
+            loss_buf.copy_(loss.detach())
+
+        def opt_step():
+            opt.step(grad_scale=grad_scale)
 
     def allreduce():
         if world > 1:
-            dist.all_reduce(flat.grad)
-
-    def opt_step():
-        opt.step(grad_scale=grad_scale)
+            dist.all_reduce(grad_buf)
 
     use_graph = not args.no_graph
     if use_graph:
@@ -124,7 +145,8 @@ def main(argv=None):
                 opt_step()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        flat.rebind_grads()
+        if args.impl == "autograd":
+            flat.rebind_grads()
         if world == 1:
             g_all = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g_all):
@@ -203,6 +225,7 @@ def main(argv=None):
                 "hidden_dim": args.hidden_dim,
                 "label_dim": args.label_dim,
                 "hipgraph": use_graph,
+                "impl": args.impl,
                 "loss_first_last": [round(first_loss, 4), round(last_loss, 4)],
             },
         }

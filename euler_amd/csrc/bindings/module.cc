@@ -476,4 +476,21 @@ PYBIND11_MODULE(_engine, m) {
   });
   m.def("edge_id_hash", &EdgeIdHash);
   m.def("registered_ops", [] { return KernelRegistry::Get().Ops(); });
+  m.def("stats", [] {
+    auto& c = EngineCounters::Get();
+    py::dict d;
+    d["queries"] = c.queries.load();
+    d["compile_us"] = c.compile_us.load();
+    d["exec_us"] = c.exec_us.load();
+    d["dag_nodes"] = c.dag_nodes.load();
+    d["remote_calls"] = c.remote_calls.load();
+    d["rpc_attempts"] = c.rpc_attempts.load();
+    d["rpc_failures"] = c.rpc_failures.load();
+    d["rpc_bytes_out"] = c.rpc_bytes_out.load();
+    d["rpc_bytes_in"] = c.rpc_bytes_in.load();
+    d["server_requests"] = c.server_requests.load();
+    d["server_us"] = c.server_us.load();
+    return d;
+  }, "per-stage engine counters (process-wide)");
+  m.def("reset_stats", [] { EngineCounters::Get().Reset(); });
 }

@@ -302,3 +302,18 @@ Status MakeDirs(const std::string& path) {
 }
 
 }  // namespace euler
+
+namespace euler {
+
+EngineCounters& EngineCounters::Get() {
+  static EngineCounters c;
+  return c;
+}
+
+void EngineCounters::Reset() {
+  for (auto* a : {&queries, &compile_us, &exec_us, &dag_nodes, &remote_calls, &rpc_attempts, &rpc_failures,
+                  &rpc_bytes_out, &rpc_bytes_in, &server_requests, &server_us})
+    a->store(0);
+}
+
+}  // namespace euler

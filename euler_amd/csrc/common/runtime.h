@@ -146,4 +146,27 @@ bool FileExists(const std::string& path);
 Status WriteFile(const std::string& path, const std::string& content);
 Status MakeDirs(const std::string& path);
 
+// ============================================================================ observability
+// Process-wide per-stage counters of the engine (query compile / execute, DAG nodes,
+// remote fan-out, RPC attempts / failures / bytes, server requests), exported to
+// Python as _engine.stats().  Relaxed atomics: cheap enough to stay always on.
+struct EngineCounters {
+  std::atomic<int64_t> queries{0}, compile_us{0}, exec_us{0}, dag_nodes{0};
+  std::atomic<int64_t> remote_calls{0}, rpc_attempts{0}, rpc_failures{0}, rpc_bytes_out{0}, rpc_bytes_in{0};
+  std::atomic<int64_t> server_requests{0}, server_us{0};
+  static EngineCounters& Get();
+  void Reset();
+};
+
+// adds the elapsed microseconds to a counter when it goes out of scope
+class ScopedMicros {
+ public:
+  explicit ScopedMicros(std::atomic<int64_t>* c) : c_(c), t0_(NowMicros()) {}
+  ~ScopedMicros() { c_->fetch_add(static_cast<int64_t>(NowMicros() - t0_), std::memory_order_relaxed); }
+
+ private:
+  std::atomic<int64_t>* c_;
+  uint64_t t0_;
+};
+
 }  // namespace euler

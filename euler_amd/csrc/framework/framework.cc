@@ -365,6 +365,7 @@ void Executor::Schedule(size_t i) {
     NodeDone(i, Status::NotFound("no kernel registered for op " + nd.op));
     return;
   }
+  EngineCounters::Get().dag_nodes.fetch_add(1, std::memory_order_relaxed);
   auto run = [this, i, k, &nd] {
     if (k->is_async()) {
       k->ComputeAsync(nd, ctx_, [this, i](Status st) { NodeDone(i, st); });

@@ -213,6 +213,7 @@ class RemoteOp : public OpKernel {
       done(Status::Unavailable("REMOTE node but no remote clients configured"));
       return;
     }
+    EngineCounters::Get().remote_calls.fetch_add(1, std::memory_order_relaxed);
     // ship every client tensor the sub-DAG references (inputs, attrs, DNF values)
     std::set<std::string> produced;
     for (auto& n : nd.inner)
@@ -481,6 +482,8 @@ void GraphServer::Serve(int fd) {
   std::string payload;
   while (running_ && RecvFrame(fd, &kind, &payload)) {
     requests_++;
+    EngineCounters::Get().server_requests.fetch_add(1, std::memory_order_relaxed);
+    ScopedMicros timing(&EngineCounters::Get().server_us);
     std::string reply;
     if (kind == kPing) {
       reply = EncodeReply(Status::OK(), {});
@@ -564,7 +567,9 @@ Status RpcClients::Call(int shard, uint32_t kind, const std::string& payload, st
     return Status::Unavailable("no server for shard " + std::to_string(shard));
   auto& hosts = shards_[shard];
   Status last;
+  auto& ctr = EngineCounters::Get();
   for (int attempt = 0; attempt <= opt_.num_retries; ++attempt) {
+    ctr.rpc_attempts.fetch_add(1, std::memory_order_relaxed);
     if (FaultDelayMs() > 0) std::this_thread::sleep_for(std::chrono::milliseconds(FaultDelayMs()));
     // round-robin over replicas that are not quarantined
     Host* h = nullptr;
@@ -581,8 +586,13 @@ Status RpcClients::Call(int shard, uint32_t kind, const std::string& payload, st
       last = Status::RpcError("injected fault");
     } else {
       last = CallHost(h, kind, payload, reply);
-      if (last.ok()) return last;
+      if (last.ok()) {
+        ctr.rpc_bytes_out.fetch_add(static_cast<int64_t>(payload.size()), std::memory_order_relaxed);
+        ctr.rpc_bytes_in.fetch_add(static_cast<int64_t>(reply->size()), std::memory_order_relaxed);
+        return last;
+      }
     }
+    ctr.rpc_failures.fetch_add(1, std::memory_order_relaxed);
     failures_++;
     h->bad_until = NowSec() + opt_.bad_host_timeout;  // move to bad host list
     EULER_LOG(Warning) << "rpc shard " << shard << " attempt " << attempt << " failed: " << last.message();
@@ -776,8 +786,14 @@ Status QueryProxy::InitWithGraph(std::unique_ptr<Graph> g, std::unique_ptr<Index
 
 Status QueryProxy::Run(const std::string& gql, const std::vector<std::pair<std::string, Tensor>>& inputs,
                        const std::vector<std::string>& outputs, std::vector<Tensor>* results) {
+  auto& ctr = EngineCounters::Get();
+  ctr.queries.fetch_add(1, std::memory_order_relaxed);
   std::shared_ptr<const DAGDef> dag;
-  EULER_RETURN_IF_ERROR(Compiler::Get().Compile(gql, copt_, &dag));
+  {
+    ScopedMicros t(&ctr.compile_us);
+    EULER_RETURN_IF_ERROR(Compiler::Get().Compile(gql, copt_, &dag));
+  }
+  ScopedMicros t(&ctr.exec_us);
   return ExecuteDag(&env_, *dag, inputs, outputs, results);
 }
 
@@ -797,10 +813,16 @@ Status QueryProxy::RunOp(const std::string& op, const std::vector<std::string>& 
   as.attrs = {"__result"};
   for (int k = 0; k < output_num; ++k) as.inputs.push_back(nd.Output(k));
   logical.nodes = {nd, as};
+  auto& ctr = EngineCounters::Get();
+  ctr.queries.fetch_add(1, std::memory_order_relaxed);
   DAGDef phys;
-  EULER_RETURN_IF_ERROR(Compiler::Get().Optimize(logical, copt_, &phys));
+  {
+    ScopedMicros t(&ctr.compile_us);
+    EULER_RETURN_IF_ERROR(Compiler::Get().Optimize(logical, copt_, &phys));
+  }
   std::vector<std::string> outs;
   for (int k = 0; k < output_num; ++k) outs.push_back("__result:" + std::to_string(k));
+  ScopedMicros t(&ctr.exec_us);
   return ExecuteDag(&env_, phys, inputs, outs, results);
 }
 

@@ -22,6 +22,7 @@ autocast), ``save_checkpoints_steps``, ``keep_checkpoint_max``, ``seed``.
 """
 from __future__ import annotations
 
+import contextlib
 import glob
 import logging
 import os
@@ -34,6 +35,7 @@ import torch.nn as nn
 
 from euler_amd.parallel import dp
 from euler_amd.parallel.embedding import is_sharded
+from euler_amd.utils import trace
 from euler_amd.utils.misc import get_optimizer
 
 __all__ = ["BaseEstimator", "latest_checkpoint", "id_file_batches"]
@@ -179,7 +181,7 @@ class BaseEstimator:
                        if not isinstance(v, nn.parameter.UninitializedParameter)}  # never-called lazy layers
         state = {"step": step, "model": model_state,
                  "optimizer": self.optimizer.state_dict() if self.optimizer is not None else None,
-                 "world": self.world}
+                 "world": self.world, "torch_rng": torch.get_rng_state()}
         tmp = path + ".tmp"
         torch.save(state, tmp)
         os.replace(tmp, path)
@@ -207,6 +209,8 @@ class BaseEstimator:
         if self.optimizer is not None and state.get("optimizer") is not None:
             self.optimizer.load_state_dict(state["optimizer"])
         self.global_step = int(state["step"])
+        if state.get("torch_rng") is not None:
+            torch.set_rng_state(state["torch_rng"].cpu())
         log.info("restored %s at step %d", path, self.global_step)
         return True
 
@@ -236,17 +240,24 @@ class BaseEstimator:
             prof = torch.profiler.profile(schedule=torch.profiler.schedule(wait=5, warmup=5, active=20),
                                           on_trace_ready=torch.profiler.tensorboard_trace_handler("prof_dir"))
             prof.start()
+        tracing = bool(self.params.get("trace")) or trace.enabled()
+        rng = (lambda name: trace.trace_range(name)) if tracing else (lambda name: contextlib.nullcontext())
         while self.global_step < total:
-            source = pending if pending is not None else self.get_train_from_input(inputs, self.params)
+            with rng("sample"):
+                source = pending if pending is not None else self.get_train_from_input(inputs, self.params)
             pending = None
-            _, loss, metric_name, metric = self._run_model(source)
-            extra = self._extra_losses()
-            obj = loss if extra is None else loss + extra
-            self.optimizer.zero_grad(set_to_none=False)
-            obj.backward()
-            self._after_backward()
-            self._sync.finish()
-            self.optimizer.step()
+            with rng("forward"):
+                _, loss, metric_name, metric = self._run_model(source)
+                extra = self._extra_losses()
+                obj = loss if extra is None else loss + extra
+            with rng("backward"):
+                self.optimizer.zero_grad(set_to_none=False)
+                obj.backward()
+                self._after_backward()
+            with rng("grad_sync"):
+                self._sync.finish()
+            with rng("optimizer"):
+                self.optimizer.step()
             self.global_step += 1
             if prof is not None:
                 prof.step()
@@ -258,6 +269,9 @@ class BaseEstimator:
                 if self.rank == 0:
                     log.info("step = %d, loss = %.6f, %s = %.6f (%.1f samples/s)", self.global_step, last["loss"],
                              metric_name, last[metric_name], rate)
+                    if tracing:
+                        log.info("stage timings:\n%s\nengine: %s", trace.default_timer.report(),
+                                 trace.engine_stats())
                 t0, n0 = time.time(), self.global_step
             if save_steps and self.global_step % save_steps == 0:
                 self.save()
