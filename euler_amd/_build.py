@@ -126,6 +126,40 @@ def build_engine(max_workers: int = 8, extra_flags=None) -> str:
     return out
 
 
+_SANITIZERS = {
+    "thread": ["-fsanitize=thread"],
+    "address": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"],
+    "none": [],
+}
+
+
+def build_selftest(sanitize: str = "thread", max_workers: int = 8) -> str:
+    """Engine self-test binary (csrc/tests/engine_selftest.cc) under a sanitizer:
+    ``thread`` (TSAN) or ``address`` (ASAN + UBSan).  Host code only; the pybind
+    module is not part of it.  Returns the binary path (mtime-cached under build/)."""
+    if sanitize not in _SANITIZERS:
+        raise ValueError("sanitize must be one of %s" % sorted(_SANITIZERS))
+    objdir = os.path.join(BUILD, "selftest_" + sanitize)
+    os.makedirs(objdir, exist_ok=True)
+    out = os.path.join(objdir, "engine_selftest")
+    san = _SANITIZERS[sanitize]
+    flags = ["-O1", "-g", "-std=c++17", "-pthread", "-fno-omit-frame-pointer", "-Wno-sign-compare"] + san
+    srcs = [s for s in engine_sources() if os.sep + "bindings" + os.sep not in s]
+    srcs.append(os.path.join(CSRC, "tests", "engine_selftest.cc"))
+    hdr_m = _newest(engine_headers() + [__file__])
+    jobs, objs = [], []
+    for s in srcs:
+        rel = os.path.relpath(s, CSRC).replace(os.sep, "_")
+        o = os.path.join(objdir, rel + ".o")
+        objs.append(o)
+        jobs.append((["g++"] + flags + ["-I" + CSRC, "-c", s, "-o", o], o, hdr_m, s))
+    changed = _compile_all(jobs, max_workers)
+    if changed or not os.path.exists(out) or os.path.getmtime(out) < _newest(objs):
+        _run(["g++"] + san + ["-pthread", "-o", out] + objs + ["-ldl"])
+        _log("linked " + os.path.relpath(out, REPO))
+    return out
+
+
 # ----------------------------------------------------------------------------
 # HIP kernels (gfx950) + torch binding
 # ----------------------------------------------------------------------------

@@ -270,7 +270,7 @@ __device__ __forceinline__ void st_kt4(bf16_t* kt, int64_t row, int col, int N, 
   *reinterpret_cast<st_uint2*>(kt + kt_off(row, col, N)) = v;
 }
 
-constexpr int HB = 64;   // head rows per block: every block streams all head weights from L2, so
+constexpr int HB = 32;   // head rows per block: every block streams all head weights from L2, so
                          // fewer, taller blocks cut that traffic (the head FLOPs are tiny)
 constexpr int HFM = HB / 16;
 constexpr int HNW = 16;  // head waves per block (1024 threads): short per-wave instruction chains

@@ -50,8 +50,8 @@ class FusedSageTrainer:
             raise ValueError("labels must be int16 class ids")
         B, (F1, F2) = int(batch_size), (int(fanouts[0]), int(fanouts[1]))
         D, H, C = features.shape[1], int(hidden_dim), int(label_dim)
-        if B % 64 or D % 16 or H % 64 or C % 32:
-            raise ValueError("need batch%64 == 0, feature_dim%16 == 0, hidden%64 == 0, label_dim%32 == 0")
+        if B % 32 or D % 16 or H % 64 or C % 32:
+            raise ValueError("need batch%32 == 0, feature_dim%16 == 0, hidden%64 == 0, label_dim%32 == 0")
         self.B, self.F1, self.F2, self.D, self.H, self.C = B, F1, F2, D, H, C
         self.M1 = B * (F1 + 1)
         self.include_self = bool(add_self_loops)
