@@ -26,7 +26,8 @@ import sysconfig
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(ROOT)
-BUILD = os.path.join(REPO, "build")
+# object files live outside the tree (only the linked .so files travel with a snapshot)
+BUILD = os.environ.get("EULER_AMD_BUILD_DIR", os.path.join(os.path.expanduser("~"), ".cache", "euler_amd_build"))
 CSRC = os.path.join(ROOT, "csrc")
 ARCH = os.environ.get("EULER_AMD_ARCH", "gfx950")
 
