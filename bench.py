@@ -56,6 +56,21 @@ def parse_args(argv=None):
     return p.parse_args(argv)
 
 
+def _cpu_baseline():
+    """BASELINE.md publishes no reference number; its prescribed comparison point is the
+    reference-equivalent CPU path measured on the MI355X host (euler_amd/tools/cpu_baseline.py,
+    result committed in profiles/cpu_baseline.json)."""
+    path = os.path.join(ROOT, "profiles", "cpu_baseline.json")
+    try:
+        with open(path) as f:
+            b = json.loads(f.readline())
+        note = (f"profiles/cpu_baseline.json: reference-equivalent CPU path, {b['value']} samples/s "
+                f"({b.get('threads')} host threads, {b['config']['num_nodes']} nodes)")
+        return float(b["value"]), note
+    except (OSError, ValueError, KeyError):
+        return None, None
+
+
 def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
@@ -198,6 +213,7 @@ def main(argv=None):
     last_loss = float(loss_buf.item())
     ms = elapsed * 1000.0 / max(args.steps, 1)
     value = world * B * args.steps / elapsed
+    base_value, base_note = _cpu_baseline()
     if rank == 0:
         log(f"loss after warmup {first_loss:.4f} -> after timed steps {last_loss:.4f}")
         out = {
@@ -210,7 +226,7 @@ def main(argv=None):
             "ms_per_step": round(ms, 4),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": None,
+            "vs_baseline": round(value / base_value, 2) if base_value else None,
             "dtype": "bf16",
             "data": "synthetic (power-law random graph + random-normal features, random-init weights)",
             "config": {
@@ -227,6 +243,7 @@ def main(argv=None):
                 "hipgraph": use_graph,
                 "impl": args.impl,
                 "loss_first_last": [round(first_loss, 4), round(last_loss, 4)],
+                "baseline": base_note,
             },
         }
         print(json.dumps(out), flush=True)

@@ -420,17 +420,22 @@ PYBIND11_MODULE(_engine, m) {
       .def_property_readonly("requests", &PyServer::requests)
       .def("stop", &PyServer::Stop);
 
-  m.def("synthetic", [](int64_t n, double avg_deg, int64_t max_deg, int node_types, int edge_types, int feature_dim,
-                        int label_dim, uint64_t seed) {
-    std::unique_ptr<Graph> g;
-    {
-      py::gil_scoped_release nogil;
-      g = SyntheticGraph(n, avg_deg, max_deg, node_types, edge_types, feature_dim, label_dim, seed, 0);
-    }
-    std::unique_ptr<QueryProxy> p(new QueryProxy);
-    Throw(p->InitWithGraph(std::move(g), nullptr));
-    return std::make_shared<Engine>(std::move(p));
-  });
+  m.def(
+      "synthetic",
+      [](int64_t n, double avg_deg, int64_t max_deg, int node_types, int edge_types, int feature_dim, int label_dim,
+         uint64_t seed, bool out_only) {
+        std::unique_ptr<Graph> g;
+        {
+          py::gil_scoped_release nogil;
+          g = SyntheticGraph(n, avg_deg, max_deg, node_types, edge_types, feature_dim, label_dim, seed, out_only);
+        }
+        std::unique_ptr<QueryProxy> p(new QueryProxy);
+        Throw(p->InitWithGraph(std::move(g), nullptr));
+        return std::make_shared<Engine>(std::move(p));
+      },
+      py::arg("num_nodes"), py::arg("avg_degree"), py::arg("max_degree"), py::arg("node_types"),
+      py::arg("edge_types"), py::arg("feature_dim"), py::arg("label_dim"), py::arg("seed"),
+      py::arg("out_only") = false);
   m.def("parse_gql", [](const std::string& q) {
     std::vector<GqlStep> steps;
     Throw(ParseGql(q, &steps));

@@ -803,8 +803,7 @@ std::unique_ptr<Graph> GraphBuilder::Finish() {
 // ============================================================================ synthetic
 std::unique_ptr<Graph> SyntheticGraph(int64_t N, double avg_degree, int64_t max_degree, int num_node_types,
                                       int num_edge_types, int feature_dim, int label_dim, uint64_t seed,
-                                      int threads) {
-  (void)threads;
+                                      bool out_only) {
   std::unique_ptr<Graph> g(new Graph);
   const int T = std::max(1, num_edge_types);
   const int NT = std::max(1, num_node_types);
@@ -854,43 +853,48 @@ std::unique_ptr<Graph> SyntheticGraph(int64_t N, double avg_degree, int64_t max_
       }
     }
   });
-  // in-adjacency and the edge table from the out CSR
-  g->edge_src_.resize(E);
-  g->edge_dst_.resize(E);
-  g->edge_type_.resize(E);
-  g->edge_weight_.resize(E);
-  std::vector<uint64_t> in_cnt(static_cast<size_t>(N) * T + 1, 0);
-  for (int64_t i = 0; i < N; ++i)
-    for (int t = 0; t < T; ++t)
-      for (uint64_t k = ip[i * T + t]; k < ip[i * T + t + 1]; ++k) {
-        g->edge_src_[k] = i;
-        g->edge_dst_[k] = g->out_.nbr[k];
-        g->edge_type_[k] = t;
-        g->edge_weight_[k] = g->out_.EdgeWeight(k, ip[i * T + t]);
-        in_cnt[g->out_.nbr[k] * T + t + 1]++;
+  // in-adjacency and the edge table from the out CSR (skipped for out_only graphs: a
+  // sampling-only benchmark graph keeps just the out CSR, ~12 bytes per edge)
+  if (out_only) {
+    g->in_.indptr.assign(static_cast<size_t>(N) * T + 1, 0);
+  } else {
+    g->edge_src_.resize(E);
+    g->edge_dst_.resize(E);
+    g->edge_type_.resize(E);
+    g->edge_weight_.resize(E);
+    std::vector<uint64_t> in_cnt(static_cast<size_t>(N) * T + 1, 0);
+    for (int64_t i = 0; i < N; ++i)
+      for (int t = 0; t < T; ++t)
+        for (uint64_t k = ip[i * T + t]; k < ip[i * T + t + 1]; ++k) {
+          g->edge_src_[k] = i;
+          g->edge_dst_[k] = g->out_.nbr[k];
+          g->edge_type_[k] = t;
+          g->edge_weight_[k] = g->out_.EdgeWeight(k, ip[i * T + t]);
+          in_cnt[g->out_.nbr[k] * T + t + 1]++;
+        }
+    for (size_t i = 1; i < in_cnt.size(); ++i) in_cnt[i] += in_cnt[i - 1];
+    g->in_.indptr = in_cnt;
+    g->in_.nbr.resize(E);
+    g->in_.cumw.resize(E);
+    {
+      std::vector<uint64_t> pos(in_cnt.begin(), in_cnt.end() - 1);
+      std::vector<float> w(E);
+      for (uint64_t k = 0; k < E; ++k) {
+        const uint64_t seg = g->edge_dst_[k] * T + g->edge_type_[k];
+        const uint64_t p = pos[seg]++;
+        g->in_.nbr[p] = g->edge_src_[k];  // sources visited in ascending order: segments stay sorted
+        w[p] = g->edge_weight_[k];
       }
-  for (size_t i = 1; i < in_cnt.size(); ++i) in_cnt[i] += in_cnt[i - 1];
-  g->in_.indptr = in_cnt;
-  g->in_.nbr.resize(E);
-  g->in_.cumw.resize(E);
-  {
-    std::vector<uint64_t> pos(in_cnt.begin(), in_cnt.end() - 1);
-    std::vector<float> w(E);
-    for (uint64_t k = 0; k < E; ++k) {
-      const uint64_t seg = g->edge_dst_[k] * T + g->edge_type_[k];
-      const uint64_t p = pos[seg]++;
-      g->in_.nbr[p] = g->edge_src_[k];  // sources visited in ascending order: segments stay sorted
-      w[p] = g->edge_weight_[k];
-    }
-    for (size_t s = 0; s + 1 < in_cnt.size(); ++s) {
-      float acc = 0.f;
-      for (uint64_t k = in_cnt[s]; k < in_cnt[s + 1]; ++k) {
-        acc += w[k];
-        g->in_.cumw[k] = acc;
+      for (size_t s = 0; s + 1 < in_cnt.size(); ++s) {
+        float acc = 0.f;
+        for (uint64_t k = in_cnt[s]; k < in_cnt[s + 1]; ++k) {
+          acc += w[k];
+          g->in_.cumw[k] = acc;
+        }
       }
     }
+    g->BuildEdgeIndex();
   }
-  g->BuildEdgeIndex();
   // meta + features
   GraphMeta& m = g->meta_;
   m.name = "synthetic";

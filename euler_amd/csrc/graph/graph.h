@@ -128,7 +128,7 @@ class IdMap {
 class Graph;
 std::unique_ptr<Graph> SyntheticGraph(int64_t num_nodes, double avg_degree, int64_t max_degree, int num_node_types,
                                       int num_edge_types, int feature_dim, int label_dim, uint64_t seed,
-                                      int threads);
+                                      bool out_only);
 
 struct IdWeightType {
   uint64_t id;
@@ -196,7 +196,7 @@ class Graph {
 
  private:
   friend class GraphBuilder;
-  friend std::unique_ptr<Graph> SyntheticGraph(int64_t, double, int64_t, int, int, int, int, uint64_t, int);
+  friend std::unique_ptr<Graph> SyntheticGraph(int64_t, double, int64_t, int, int, int, int, uint64_t, bool);
   template <typename T>
   static const Column<T>* ColAt(const std::vector<Column<T>>& v, int idx) {
     return (idx >= 0 && idx < static_cast<int>(v.size())) ? &v[idx] : nullptr;

@@ -510,7 +510,8 @@ void st_tree_mean(torch::Tensor h0, int64_t B, int64_t F1, bool include_self, to
 void st_head(torch::Tensor A1, torch::Tensor W1b, torch::Tensor Wfc, torch::Tensor WfcT, torch::Tensor bfc,
              torch::Tensor Wout, torch::Tensor WoutT, torch::Tensor W1T, torch::Tensor label_idx, torch::Tensor A1_kt,
              torch::Tensor h1_kt, torch::Tensor emb_kt, torch::Tensor dlog_kt, torch::Tensor demb_kt,
-             torch::Tensor g1_kt, torch::Tensor dA1, torch::Tensor dbfc, torch::Tensor loss_acc) {
+             torch::Tensor g1_kt, torch::Tensor dA1, torch::Tensor dbfc, torch::Tensor loss_acc,
+             c10::optional<torch::Tensor> prof) {
   for (auto* p : {&A1, &W1b, &Wfc, &WfcT, &Wout, &WoutT, &W1T, &A1_kt, &h1_kt, &emb_kt, &dlog_kt, &demb_kt, &g1_kt})
     need_bf16(*p, "st_head bf16 operand");
   need_f32(bfc, "bfc");
@@ -535,27 +536,37 @@ void st_head(torch::Tensor A1, torch::Tensor W1b, torch::Tensor Wfc, torch::Tens
   need_numel(demb_kt, B * H, "demb_kt");
   need_numel(g1_kt, B * H, "g1_kt");
   need_numel(dA1, B * 2 * H, "dA1");
+  long long* prof_p = nullptr;
+  if (prof.has_value()) {
+    TORCH_CHECK(prof->scalar_type() == torch::kInt64 && prof->is_contiguous() && prof->is_cuda(),
+                "prof must be a contiguous int64 device tensor");
+    TORCH_CHECK(B % kStHeadRows == 0, "B must be a multiple of the head block");
+    need_numel(*prof, (B / kStHeadRows) * 8, "prof");
+    prof_p = reinterpret_cast<long long*>(prof->data_ptr<int64_t>());
+  }
   const c10::DeviceGuard g(A1.device());
   check(eh_st_head(A1.data_ptr(), static_cast<int>(B), static_cast<int>(H), static_cast<int>(C), W1b.data_ptr(),
                    Wfc.data_ptr(), WfcT.data_ptr(), bfc.data_ptr<float>(), Wout.data_ptr(), WoutT.data_ptr(),
                    W1T.data_ptr(), label_idx.data_ptr<int32_t>(), 1.f / static_cast<float>(B * C), A1_kt.data_ptr(),
                    h1_kt.data_ptr(), emb_kt.data_ptr(), dlog_kt.data_ptr(), demb_kt.data_ptr(), g1_kt.data_ptr(),
-                   dA1.data_ptr<float>(), dbfc.data_ptr<float>(), loss_acc.data_ptr<float>(), cur_stream()),
+                   dA1.data_ptr<float>(), dbfc.data_ptr<float>(), loss_acc.data_ptr<float>(), prof_p, cur_stream()),
         "st_head");
 }
 
-void st_route(torch::Tensor dA1, int64_t F1, bool include_self, torch::Tensor h0, torch::Tensor g0_kt) {
+void st_route(torch::Tensor dA1, int64_t F1, bool include_self, torch::Tensor mask, torch::Tensor g0_kt) {
   need_f32(dA1, "dA1");
-  need_bf16(h0, "h0");
+  TORCH_CHECK(mask.scalar_type() == torch::kInt32 && mask.is_contiguous(), "mask must be contiguous int32");
   need_bf16(g0_kt, "g0_kt");
-  const int64_t B = dA1.size(0), H = h0.size(1), M1 = h0.size(0);
-  TORCH_CHECK(dA1.size(1) == 2 * H, "dA1 must be [B, 2H]");
-  TORCH_CHECK(M1 == B * (F1 + 1), "h0 rows must be B*(F1+1)");
+  const int64_t B = dA1.size(0), H = dA1.size(1) / 2, M1 = B * (F1 + 1);
+  TORCH_CHECK(dA1.size(1) == 2 * H && H % 8 == 0, "dA1 must be [B, 2H] with H % 8 == 0");
+  TORCH_CHECK(M1 % 32 == 0, "B*(F1+1) must be a multiple of 32");
+  need_numel(mask, (M1 / 32) * H, "mask");
   need_numel(g0_kt, M1 * H, "g0_kt");
   const float inv = 1.f / static_cast<float>(F1 + (include_self ? 1 : 0));
-  const c10::DeviceGuard g(h0.device());
+  const c10::DeviceGuard g(dA1.device());
   check(eh_st_route(dA1.data_ptr<float>(), static_cast<int>(H), B * F1, static_cast<int>(F1), include_self ? 1 : 0,
-                    inv, h0.data_ptr(), M1, g0_kt.data_ptr(), cur_stream()),
+                    inv, reinterpret_cast<const uint32_t*>(mask.data_ptr<int32_t>()), M1, g0_kt.data_ptr(),
+                    cur_stream()),
         "st_route");
 }
 
@@ -724,7 +735,11 @@ PYBIND11_MODULE(_hip_ops, m) {
   m.def("sample_neighbor_into", &sample_neighbor_into);
   m.def("st_roots", &st_roots);
   m.def("st_sage_fwd", &st_sage_fwd);
-  m.def("st_head", &st_head);
+  m.attr("st_head_rows") = kStHeadRows;
+  m.def("st_head", &st_head, "fused head fwd+bwd", py::arg("A1"), py::arg("W1b"), py::arg("Wfc"), py::arg("WfcT"),
+        py::arg("bfc"), py::arg("Wout"), py::arg("WoutT"), py::arg("W1T"), py::arg("label_idx"), py::arg("A1_kt"),
+        py::arg("h1_kt"), py::arg("emb_kt"), py::arg("dlog_kt"), py::arg("demb_kt"), py::arg("g1_kt"), py::arg("dA1"),
+        py::arg("dbfc"), py::arg("loss_acc"), py::arg("prof") = py::none());
   m.def("st_tree_mean", &st_tree_mean);
   m.def("st_route", &st_route);
   m.def("st_dw", &st_dw);

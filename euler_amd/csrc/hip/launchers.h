@@ -57,12 +57,14 @@ hipError_t eh_st_sage_fwd(const void* x, int D, const int32_t* self_idx, const i
                           uint32_t* relu_mask, int bm, hipStream_t s);
 hipError_t eh_st_tree_mean(const void* h0, int H, int64_t B, int F1, int include_self, float inv_cnt, void* A1,
                            hipStream_t s);
+// rows per block of the fused head kernel (sage_train.hip)
+constexpr int kStHeadRows = 32;
 hipError_t eh_st_head(const void* A1, int B, int H, int C, const void* W1b, const void* Wfc, const void* WfcT,
                       const float* bfc, const void* Wout, const void* WoutT, const void* W1T, const int32_t* label_idx,
                       float inv_scale, void* A1_kt, void* h1_kt, void* emb_kt, void* dlog_kt, void* demb_kt,
-                      void* g1_kt, float* dA1, float* dbfc, float* loss_acc, hipStream_t s);
+                      void* g1_kt, float* dA1, float* dbfc, float* loss_acc, long long* prof, hipStream_t s);
 hipError_t eh_st_route(const float* dA1, int H, int64_t nb_rows, int F1, int include_self, float inv_cnt,
-                       const void* h0, int64_t M1, void* g0_kt, hipStream_t s);
+                       const uint32_t* mask, int64_t M1, void* g0_kt, hipStream_t s);
 hipError_t eh_st_dw(int n, const void* const* G, const void* const* X, float* const* part, const int* P,
                     const int* Q, const int64_t* M, const int* kps, const uint32_t* route_mask,
                     const float* route_dA1, int64_t nb_rows, int F1, int include_self, float inv_cnt, hipStream_t s);

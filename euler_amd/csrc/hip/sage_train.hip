@@ -18,6 +18,7 @@
 // both MFMA fragments of dW = G^T X are single 16-byte loads
 // (lane l: 8 consecutive m at column l&15), no LDS transpose in the dW kernel.
 #include "hip/common.h"
+#include "hip/launchers.h"
 
 namespace euler_hip {
 
@@ -32,6 +33,20 @@ __device__ __forceinline__ float4_t st_mfma(uint4_t a, uint4_t b, float4_t c) {
 // offset of element (m, n) of an [M][N] matrix stored k-tiled ([M/32][N][32])
 __device__ __forceinline__ int64_t kt_off(int64_t m, int64_t n, int64_t N) {
   return ((m >> 5) * N + n) * 32 + (m & 31);
+}
+
+// "fm" (fragment-major) layout of the bf16 weight shadows W[N][K] used as MFMA B operands:
+// Wf[N/16][K/32][64 lanes][8].  The B fragment of (16-column slab, 32-deep k-step) is one
+// contiguous 1 KB (lane l: W[n0 + (l&15)][k0 + 8*(l>>4) .. +8]), so each wave load is
+// fully coalesced instead of 16 rows x 64 B (which the texture path serves at a quarter
+// of the rate and made the head kernel load-issue bound).
+__device__ __forceinline__ int64_t fm_off(int64_t n, int64_t k, int64_t K) {
+  return (((n >> 4) * (K >> 5) + (k >> 5)) * 64 + ((k & 31) >> 3) * 16 + (n & 15)) * 8 + (k & 7);
+}
+// the B fragment of slab n0 (multiple of 16), k-step k0 (multiple of 32) for this lane
+__device__ __forceinline__ uint4_t fm_frag(const bf16_t* __restrict__ Wf, int n0, int k0, int K, int lane) {
+  return *reinterpret_cast<const uint4_t*>(
+      Wf + ((static_cast<int64_t>(n0 >> 4) * (K >> 5) + (k0 >> 5)) * 64 + lane) * 8);
 }
 
 __device__ __forceinline__ bool bf_pos(bf16_t v) { return (v & 0x8000u) == 0 && (v & 0x7fffu) != 0; }
@@ -71,7 +86,7 @@ __global__ __launch_bounds__(256) void st_roots_kernel(const float* __restrict__
 //    Emits out (row-major bf16, LDS-staged 16-byte stores) and the A tile in kt layout.
 // ----------------------------------------------------------------------------
 template <int BM, int BN>
-__global__ __launch_bounds__(256) void st_sage_fwd_kernel(
+__global__ __launch_bounds__(256, BM <= 32 ? 4 : 2) void st_sage_fwd_kernel(
     const bf16_t* __restrict__ x, int D, const int32_t* __restrict__ self_idx, const int32_t* __restrict__ nbr_idx,
     int F, int include_self, float inv_cnt, const bf16_t* __restrict__ W, int H, int64_t M,
     bf16_t* __restrict__ out, bf16_t* __restrict__ a_kt, uint32_t* __restrict__ relu_mask) {
@@ -98,7 +113,7 @@ __global__ __launch_bounds__(256) void st_sage_fwd_kernel(
       // (no index loads, the addresses are known up front)
       const bool contig = nbr_idx == nullptr;
       const int32_t* nb = contig ? nullptr : nbr_idx + grow * F;
-      constexpr int G = 16;  // neighbour rows in flight per item
+      constexpr int G = 12;  // neighbour rows in flight per item (fits 4 waves/SIMD)
       for (int k = 0; k < F; k += G) {
         int32_t j[G];
         uint4_t v[G];
@@ -144,7 +159,10 @@ __global__ __launch_bounds__(256) void st_sage_fwd_kernel(
   const int lane = threadIdx.x & 63;
   const int wm = wave / WN, wn = wave % WN;
   const int lr = lane & 15, lk = (lane >> 4) * 8;
-  bf16_t* otile = lds + BM * ldsw;  // [BM][BN + 8] staging tile after the A tile
+  // [BM][BN + 8] output staging tile: aliases the (then dead) A tile when one column chunk
+  // covers H, which halves the LDS footprint and doubles the resident blocks per CU
+  const bool alias_out = H <= BN && BN <= K2;
+  bf16_t* otile = alias_out ? lds : lds + BM * ldsw;
   const int ldo = BN + 8;
   for (int cchunk = 0; cchunk < H; cchunk += BN) {
     const int cb = cchunk + wn * 64;
@@ -154,18 +172,15 @@ __global__ __launch_bounds__(256) void st_sage_fwd_kernel(
 #pragma unroll
       for (int n = 0; n < FN; ++n) acc[m][n] = float4_t{0.f, 0.f, 0.f, 0.f};
     if (cb < H) {
-      const bf16_t* wrow[FN];
-#pragma unroll
-      for (int n = 0; n < FN; ++n) wrow[n] = W + static_cast<int64_t>(cb + n * 16 + lr) * K2 + lk;
       uint4_t bcur[FN];
 #pragma unroll
-      for (int n = 0; n < FN; ++n) bcur[n] = *reinterpret_cast<const uint4_t*>(wrow[n]);
+      for (int n = 0; n < FN; ++n) bcur[n] = fm_frag(W, cb + n * 16, 0, K2, lane);
       for (int k0 = 0; k0 < K2; k0 += 32) {
         uint4_t bnext[FN];
         const bool more = k0 + 32 < K2;
 #pragma unroll
         for (int n = 0; n < FN; ++n)
-          bnext[n] = more ? *reinterpret_cast<const uint4_t*>(wrow[n] + k0 + 32) : uint4_t{0u, 0u, 0u, 0u};
+          bnext[n] = more ? fm_frag(W, cb + n * 16, k0 + 32, K2, lane) : uint4_t{0u, 0u, 0u, 0u};
         uint4_t a[FM];
 #pragma unroll
         for (int m = 0; m < FM; ++m)
@@ -177,6 +192,9 @@ __global__ __launch_bounds__(256) void st_sage_fwd_kernel(
 #pragma unroll
         for (int n = 0; n < FN; ++n) bcur[n] = bnext[n];
       }
+    }
+    if (alias_out) __syncthreads();  // every wave is done reading the A tile
+    if (cb < H) {
       // ReLU + bf16 into the staging tile (C map: col = lane&15, row = (lane>>4)*4 + j)
 #pragma unroll
       for (int m = 0; m < FM; ++m)
@@ -221,35 +239,48 @@ __global__ __launch_bounds__(256) void st_sage_fwd_kernel(
 // 3. head: fc + out_fc + sigmoid-CE + backward down to dA1 = g1 @ W1, 32 rows / block.
 // ----------------------------------------------------------------------------
 // acc[FM][FN] += A_lds[row0 + m*16 + r][k] * Bg[col0 + n*16 + r][k]  (Bg row-major [N][K])
-template <int FM, int FN>
-__device__ __forceinline__ void st_gemm_lds_glb(const bf16_t* A, int lda, const bf16_t* __restrict__ Bg, int ldb,
-                                                int col0, int K, float4_t (&acc)[FM][FN], int lane) {
-  // The head runs one block per CU, so it is latency-bound, not occupancy-bound: issue
-  // every B-fragment load of a 256-deep K chunk before the first MFMA (one exposed L2
-  // latency per chunk instead of one per k-step).
-  constexpr int KC = 8;
+constexpr int ST_KC = 8;  // k-steps (x32) per B chunk of the head GEMMs
+
+// issue the first B chunk of a head GEMM (slab col0 of fm weight Bf[N][K]) ahead of time
+__device__ __forceinline__ void st_prefetch(const bf16_t* __restrict__ Bf, int col0, int N, int K, int lane,
+                                            uint4_t (&b)[ST_KC]) {
+  // branch-free (clamped addresses; out-of-range fragments are loaded but never used) so
+  // all ST_KC loads stay in flight together
+  const int c = col0 < N ? col0 : 0;
+#pragma unroll
+  for (int s = 0; s < ST_KC; ++s) b[s] = fm_frag(Bf, c, s * 32 < K ? s * 32 : 0, K, lane);
+}
+
+template <int FM>
+__device__ __forceinline__ void st_mfma_chunk(const bf16_t* A, int lda, int kc, int K, const uint4_t (&b)[ST_KC],
+                                              float4_t (&acc)[FM][1], int lane) {
   const int lr = lane & 15, lk = (lane >> 4) * 8;
-  for (int kc = 0; kc < K; kc += 32 * KC) {
-    uint4_t b[KC][FN];
 #pragma unroll
-    for (int s = 0; s < KC; ++s)
-#pragma unroll
-      for (int n = 0; n < FN; ++n)
-        b[s][n] = (kc + s * 32 < K) ? *reinterpret_cast<const uint4_t*>(
-                                          Bg + static_cast<int64_t>(col0 + n * 16 + lr) * ldb + kc + s * 32 + lk)
-                                    : uint4_t{0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int s = 0; s < KC; ++s) {
-      if (kc + s * 32 >= K) break;
+  for (int s = 0; s < ST_KC; ++s) {
+    if (kc + s * 32 < K) {  // uniform guard, no early exit: keeps the chunk's loads batched
       uint4_t a[FM];
 #pragma unroll
       for (int m = 0; m < FM; ++m)
         a[m] = *reinterpret_cast<const uint4_t*>(A + (m * 16 + lr) * lda + kc + s * 32 + lk);
 #pragma unroll
-      for (int m = 0; m < FM; ++m)
-#pragma unroll
-        for (int n = 0; n < FN; ++n) acc[m][n] = st_mfma(a[m], b[s][n], acc[m][n]);
+      for (int m = 0; m < FM; ++m) acc[m][0] = st_mfma(a[m], b[s], acc[m][0]);
     }
+  }
+}
+
+template <int FM>
+__device__ __forceinline__ void st_gemm_lds_glb(const bf16_t* A, int lda, const bf16_t* __restrict__ Bf, int col0,
+                                                int K, float4_t (&acc)[FM][1], int lane, const uint4_t (&pre)[ST_KC]) {
+  // B = fm-layout weight shadow [N][K]; its first 256-deep chunk was issued by
+  // st_prefetch before the preceding barrier (weights do not depend on the previous
+  // phase), later chunks issue all their loads before the first MFMA.  The head runs one
+  // block per CU, so it is latency-bound: this leaves ~one exposed L2 latency per phase.
+  st_mfma_chunk<FM>(A, lda, 0, K, pre, acc, lane);
+  for (int kc = 32 * ST_KC; kc < K; kc += 32 * ST_KC) {
+    uint4_t b[ST_KC];
+#pragma unroll
+    for (int s = 0; s < ST_KC; ++s) b[s] = fm_frag(Bf, col0, kc + s * 32 < K ? kc + s * 32 : 0, K, lane);
+    st_mfma_chunk<FM>(A, lda, kc, K, b, acc, lane);
   }
 }
 
@@ -270,7 +301,7 @@ __device__ __forceinline__ void st_kt4(bf16_t* kt, int64_t row, int col, int N, 
   *reinterpret_cast<st_uint2*>(kt + kt_off(row, col, N)) = v;
 }
 
-constexpr int HB = 32;   // head rows per block: every block streams all head weights from L2, so
+constexpr int HB = kStHeadRows;  // head rows per block: every block streams all head weights from L2, so
                          // fewer, taller blocks cut that traffic (the head FLOPs are tiny)
 constexpr int HFM = HB / 16;
 constexpr int HNW = 16;  // head waves per block (1024 threads): short per-wave instruction chains
@@ -333,8 +364,12 @@ __global__ __launch_bounds__(HNW * 64) void st_head_kernel(
     const bf16_t* __restrict__ WoutT, const bf16_t* __restrict__ W1T, const int32_t* __restrict__ label_idx,
     float inv_scale, bf16_t* __restrict__ A1_kt, bf16_t* __restrict__ h1_kt, bf16_t* __restrict__ emb_kt,
     bf16_t* __restrict__ dlog_kt, bf16_t* __restrict__ demb_kt, bf16_t* __restrict__ g1_kt, float* __restrict__ dA1,
-    float* __restrict__ dbfc, float* __restrict__ loss_acc) {
+    float* __restrict__ dbfc, float* __restrict__ loss_acc, long long* __restrict__ prof) {
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  // optional phase timestamps (100 MHz wall clock) of every block: prof[block][8]
+#define ST_STAMP(k) \
+  if (prof && threadIdx.x == 0) prof[blockIdx.x * 8 + (k)] = static_cast<long long>(wall_clock64())
+  ST_STAMP(0);
   const int H2 = 2 * H;
   const int lda = H2 + 8, ldh = H + 8, ldc = C + 8;
   bf16_t* Aa = lds;              // [HB][2H+8] A1 tile
@@ -347,31 +382,42 @@ __global__ __launch_bounds__(HNW * 64) void st_head_kernel(
   const int lr = lane & 15, lg = lane >> 4;
   constexpr int NT = HNW * 64;
 
+  // the block's labels, staged in LDS up front (used in S3's epilogue)
+  __shared__ int lab_s[HB];
+  if (threadIdx.x < HB) lab_s[threadIdx.x] = label_idx[r0 + threadIdx.x];
+
   // S0: A1 tile -> LDS (+ A1_kt); h1 = relu(A1 @ W1^T) -> Ah
+  uint4_t pre[ST_KC];
+  st_prefetch(W1b, wave * 16, H, H2, lane, pre);
   const int cpa = H2 >> 3;
   for (int it = threadIdx.x; it < HB * cpa; it += NT) {
     const int r = it / cpa, c = it - r * cpa;
     *reinterpret_cast<uint4_t*>(Aa + r * lda + c * 8) = *reinterpret_cast<const uint4_t*>(A1g + (r0 + r) * H2 + c * 8);
   }
   __syncthreads();
+  ST_STAMP(1);
   st_lds_to_kt(Aa, lda, H2, r0, A1_kt);
   for (int cc = wave * 16; cc < H; cc += HNW * 16) {
     float4_t acc[HFM][1];
     st_zero(acc);
-    st_gemm_lds_glb<HFM, 1>(Aa, lda, W1b, H2, cc, H2, acc, lane);
+    st_gemm_lds_glb<HFM>(Aa, lda, W1b, cc, H2, acc, lane, pre);
+    if (cc + HNW * 16 < H) st_prefetch(W1b, cc + HNW * 16, H, H2, lane, pre);
 #pragma unroll
     for (int m = 0; m < HFM; ++m)
 #pragma unroll
       for (int j = 0; j < 4; ++j) Ah[(m * 16 + lg * 4 + j) * ldh + cc + lr] = f2bf(fmaxf(acc[m][0][j], 0.f));
   }
+  st_prefetch(Wfc, wave * 16, H, H, lane, pre);  // next phase's first chunk, ahead of the barrier
   __syncthreads();
+  ST_STAMP(2);
   st_lds_to_kt(Ah, ldh, H, r0, h1_kt);
 
   // S2: emb = h1 @ Wfc^T + bfc
   for (int cc = wave * 16; cc < H; cc += HNW * 16) {
     float4_t acc[HFM][1];
     st_zero(acc);
-    st_gemm_lds_glb<HFM, 1>(Ah, ldh, Wfc, H, cc, H, acc, lane);
+    st_gemm_lds_glb<HFM>(Ah, ldh, Wfc, cc, H, acc, lane, pre);
+    if (cc + HNW * 16 < H) st_prefetch(Wfc, cc + HNW * 16, H, H, lane, pre);
     const int col = cc + lr;
     const float b = bfc[col];
 #pragma unroll
@@ -385,14 +431,17 @@ __global__ __launch_bounds__(HNW * 64) void st_head_kernel(
       st_kt4(emb_kt, r0 + m * 16 + lg * 4, col, H, e[0], e[1], e[2], e[3]);
     }
   }
+  st_prefetch(Wout, wave * 16, C, H, lane, pre);  // next phase's first chunk, ahead of the barrier
   __syncthreads();
+  ST_STAMP(3);
 
   // S3: logits = emb @ Wout^T ; dlogits, loss
   float lsum = 0.f;
   for (int cc = wave * 16; cc < C; cc += HNW * 16) {
     float4_t acc[HFM][1];
     st_zero(acc);
-    st_gemm_lds_glb<HFM, 1>(Eb, ldh, Wout, H, cc, H, acc, lane);
+    st_gemm_lds_glb<HFM>(Eb, ldh, Wout, cc, H, acc, lane, pre);
+    if (cc + HNW * 16 < C) st_prefetch(Wout, cc + HNW * 16, C, H, lane, pre);
     const int col = cc + lr;
 #pragma unroll
     for (int m = 0; m < HFM; ++m) {
@@ -401,7 +450,7 @@ __global__ __launch_bounds__(HNW * 64) void st_head_kernel(
       for (int j = 0; j < 4; ++j) {
         const int row = m * 16 + lg * 4 + j;
         const float xv = acc[m][0][j];
-        const float y = (label_idx[r0 + row] == col) ? 1.f : 0.f;
+        const float y = (lab_s[row] == col) ? 1.f : 0.f;
         const float p = 1.f / (1.f + __expf(-xv));
         lsum += fmaxf(xv, 0.f) - xv * y + log1pf(__expf(-fabsf(xv)));
         d[j] = bf2f(f2bf((p - y) * inv_scale));
@@ -414,13 +463,16 @@ __global__ __launch_bounds__(HNW * 64) void st_head_kernel(
     lsum = wave_sum(lsum);
     if (lane == 0) atomicAdd(loss_acc, lsum * inv_scale);
   }
+  st_prefetch(WoutT, wave * 16, H, C, lane, pre);  // next phase's first chunk, ahead of the barrier
   __syncthreads();
+  ST_STAMP(4);
 
   // S4: demb = dlogits @ Wout (B operand from WoutT [H][C]); dbfc = column sums
   for (int cc = wave * 16; cc < H; cc += HNW * 16) {
     float4_t acc[HFM][1];
     st_zero(acc);
-    st_gemm_lds_glb<HFM, 1>(Dl, ldc, WoutT, C, cc, C, acc, lane);
+    st_gemm_lds_glb<HFM>(Dl, ldc, WoutT, cc, C, acc, lane, pre);
+    if (cc + HNW * 16 < H) st_prefetch(WoutT, cc + HNW * 16, H, C, lane, pre);
     const int col = cc + lr;
     float cs = 0.f;
 #pragma unroll
@@ -438,13 +490,16 @@ __global__ __launch_bounds__(HNW * 64) void st_head_kernel(
     cs += __shfl_xor(cs, 32, 64);
     if (lg == 0) atomicAdd(dbfc + col, cs);
   }
+  st_prefetch(WfcT, wave * 16, H, H, lane, pre);  // next phase's first chunk, ahead of the barrier
   __syncthreads();
+  ST_STAMP(5);
 
   // S5: dh1 = demb @ Wfc (B operand from WfcT); g1 = dh1 * (h1 > 0) -> Eb, g1_kt
   for (int cc = wave * 16; cc < H; cc += HNW * 16) {
     float4_t acc[HFM][1];
     st_zero(acc);
-    st_gemm_lds_glb<HFM, 1>(Db, ldh, WfcT, H, cc, H, acc, lane);
+    st_gemm_lds_glb<HFM>(Db, ldh, WfcT, cc, H, acc, lane, pre);
+    if (cc + HNW * 16 < H) st_prefetch(WfcT, cc + HNW * 16, H, H, lane, pre);
     const int col = cc + lr;
 #pragma unroll
     for (int m = 0; m < HFM; ++m) {
@@ -458,18 +513,23 @@ __global__ __launch_bounds__(HNW * 64) void st_head_kernel(
       st_kt4(g1_kt, r0 + m * 16 + lg * 4, col, H, e[0], e[1], e[2], e[3]);
     }
   }
+  st_prefetch(W1T, wave * 16, H2, H, lane, pre);  // next phase's first chunk, ahead of the barrier
   __syncthreads();
+  ST_STAMP(6);
 
   // S6: dA1 = g1 @ W1 (B operand from W1T [2H][H]) -> fp32 row-major [B][2H]
   for (int cc = wave * 16; cc < H2; cc += HNW * 16) {
     float4_t acc[HFM][1];
     st_zero(acc);
-    st_gemm_lds_glb<HFM, 1>(Eb, ldh, W1T, H, cc, H, acc, lane);
+    st_gemm_lds_glb<HFM>(Eb, ldh, W1T, cc, H, acc, lane, pre);
+    if (cc + HNW * 16 < H2) st_prefetch(W1T, cc + HNW * 16, H2, H, lane, pre);
 #pragma unroll
     for (int m = 0; m < HFM; ++m)
 #pragma unroll
       for (int j = 0; j < 4; ++j) dA1[(r0 + m * 16 + lg * 4 + j) * H2 + cc + lr] = acc[m][0][j];
   }
+  ST_STAMP(7);
+#undef ST_STAMP
 }
 
 // ----------------------------------------------------------------------------
@@ -477,40 +537,51 @@ __global__ __launch_bounds__(HNW * 64) void st_head_kernel(
 //    mask and emit g0 in kt layout.
 //    rows [0, B*F1): neighbour slot k of target r / F1 ; rows [B*F1, M1): self of r - B*F1
 // ----------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void st_route_kernel(const float* __restrict__ dA1, int H, int64_t nb_rows, int F1,
-                                                       int include_self, float inv_cnt,
-                                                       const bf16_t* __restrict__ h0, bf16_t* __restrict__ g0_kt) {
-  // one block = one 32-row k-block.  (1) h0 rows -> LDS with coalesced 16-byte loads;
-  // (2) item = (column n, 8-row chunk q): 4 lanes cover a column's 32 rows, so a wave
-  // stores 16 columns x 64 B = 1 KB contiguous of the kt output.
-  extern __shared__ __attribute__((aligned(16))) bf16_t tile[];
-  const int ld = H + 8;
-  const int64_t kb = blockIdx.x;
-  const int64_t rbase = kb * 32;
-  const int cpr = H >> 3;
-  for (int it = threadIdx.x; it < 32 * cpr; it += 256) {
-    const int i = it / cpr, c = it - i * cpr;
-    *reinterpret_cast<uint4_t*>(tile + i * ld + c * 8) = *reinterpret_cast<const uint4_t*>(h0 + (rbase + i) * H + c * 8);
-  }
-  __syncthreads();
-  const int H2 = 2 * H;
-  for (int it = threadIdx.x; it < H * 4; it += 256) {
-    const int q = it & 3, n = it >> 2;
-    float v[8];
+__global__ __launch_bounds__(256) void st_route_kernel(const float* __restrict__ dA1, int H, int nb_rows,
+                                                       uint32_t magic, int shift, int include_self, float inv_cnt,
+                                                       const uint32_t* __restrict__ mask, bf16_t* __restrict__ g0_kt) {
+  // one block = one 32-row k-block; item = (column n, 8-row chunk q): 4 lanes cover a
+  // column's 32 rows, so a wave stores 16 columns x 64 B = 1 KB contiguous of the kt
+  // output.  The L0 ReLU mask comes from the forward's bit mask ([M/32][H], bit = row&31),
+  // so h0 is never re-read; row -> target is a 32-bit magic division.  A thread's U items
+  // issue all their loads before any use (one exposed latency per thread, not 2U).
+  constexpr int U = 4;
+  const int kb = blockIdx.x;
+  const uint32_t H2 = 2u * static_cast<uint32_t>(H);  // dA1 holds < 2^31 elements: 32-bit offsets
+  const float inv_self = include_self ? inv_cnt : 0.f;
+  const int items = H * 4;
+  for (int base = 0; base < items; base += 256 * U) {
+    uint32_t bits[U];
+    float v[U][8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int64_t r = rbase + q * 8 + i;
-      float val;
-      if (r < nb_rows) {
-        val = dA1[(r / F1) * H2 + H + n] * inv_cnt;
-      } else {
-        const int64_t t = r - nb_rows;
-        val = dA1[t * H2 + n];
-        if (include_self) val += dA1[t * H2 + H + n] * inv_cnt;
+    for (int u = 0; u < U; ++u) {
+      // branch-free: every load is unconditional (clamped item, selected address), so the
+      // compiler issues all 2*8*U of them before the first wait
+      const int it = min(base + u * 256 + static_cast<int>(threadIdx.x), items - 1);
+      const uint32_t q = it & 3, n = it >> 2;
+      bits[u] = (mask[static_cast<int64_t>(kb) * H + n] >> (q * 8)) & 0xffu;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t r = static_cast<uint32_t>(kb) * 32u + q * 8u + static_cast<uint32_t>(i);
+        const bool nb = static_cast<int>(r) < nb_rows;
+        const uint32_t tn = shift < 0 ? r : (__umulhi(r, magic) >> shift);
+        const uint32_t ts = nb ? 0u : r - static_cast<uint32_t>(nb_rows);
+        const float x1 = dA1[nb ? tn * H2 + H + n : ts * H2 + n];
+        const float x2 = dA1[ts * H2 + H + n];
+        // arithmetic blend (not a select) so neither load can be sunk into a branch
+        const float w1 = nb ? inv_cnt : 1.f, w2 = nb ? 0.f : inv_self;
+        v[u][i] = x1 * w1 + x2 * w2;
       }
-      v[i] = bf_pos(tile[(q * 8 + i) * ld + n]) ? val : 0.f;
     }
-    *reinterpret_cast<uint4_t*>(g0_kt + (kb * H + n) * 32 + q * 8) = pack_bf16x8(v);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int it = base + u * 256 + threadIdx.x;
+      if (it >= items) continue;
+      const int q = it & 3, n = it >> 2;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[u][i] = ((bits[u] >> i) & 1u) ? v[u][i] : 0.f;
+      *reinterpret_cast<uint4_t*>(g0_kt + (static_cast<int64_t>(kb) * H + n) * 32 + q * 8) = pack_bf16x8(v[u]);
+    }
   }
 }
 
@@ -693,13 +764,12 @@ __device__ __forceinline__ void st_write_shadow(const StShadow& sh, int64_t i, f
     if (s >= sh.count) break;
     const int64_t l = i - sh.off[s];
     if (l >= 0 && l < sh.n[s]) {
+      // both shadows in fm layout: W [rows][cols] and W^T [cols][rows]
       const bf16_t b = f2bf(val);
-      sh.sh[s][l] = b;
-      if (sh.shT[s]) {
-        const int64_t rows = sh.n[s] / sh.cols[s];
-        const int64_t r = l / sh.cols[s], c = l - r * sh.cols[s];
-        sh.shT[s][c * rows + r] = b;
-      }
+      const int64_t rows = sh.n[s] / sh.cols[s];
+      const int64_t r = l / sh.cols[s], c = l - r * sh.cols[s];
+      sh.sh[s][fm_off(r, c, sh.cols[s])] = b;
+      if (sh.shT[s]) sh.shT[s][fm_off(c, r, rows)] = b;
     }
   }
 }
@@ -758,7 +828,9 @@ hipError_t eh_st_sage_fwd(const void* x, int D, const int32_t* self_idx, const i
   if (D % 16 != 0 || D > 512 || H % 64 != 0 || M % 32 != 0) return hipErrorInvalidValue;
   if (relu_mask && bm % 32 != 0) return hipErrorInvalidValue;
   const int BN = 256;
-  const size_t lds = (static_cast<size_t>(bm) * (2 * D + 8) + static_cast<size_t>(bm) * (BN + 8)) * sizeof(bf16_t);
+  const bool alias_out = H <= BN && BN <= 2 * D;  // must match the kernel's choice
+  const size_t lds = (static_cast<size_t>(bm) * (2 * D + 8) + (alias_out ? 0 : static_cast<size_t>(bm) * (BN + 8))) *
+                     sizeof(bf16_t);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   const dim3 grid(static_cast<uint32_t>(ceil_div(M, bm)));
 #define ST_LAUNCH(BMV)                                                                                         \
@@ -789,7 +861,7 @@ hipError_t eh_st_tree_mean(const void* h0, int H, int64_t B, int F1, int include
 hipError_t eh_st_head(const void* A1, int B, int H, int C, const void* W1b, const void* Wfc, const void* WfcT,
                       const float* bfc, const void* Wout, const void* WoutT, const void* W1T, const int32_t* label_idx,
                       float inv_scale, void* A1_kt, void* h1_kt, void* emb_kt, void* dlog_kt, void* demb_kt,
-                      void* g1_kt, float* dA1, float* dbfc, float* loss_acc, hipStream_t s) {
+                      void* g1_kt, float* dA1, float* dbfc, float* loss_acc, long long* prof, hipStream_t s) {
   if (B % HB != 0 || H % 64 != 0 || C % 32 != 0 || C > 256) return hipErrorInvalidValue;
   const size_t lds = (static_cast<size_t>(HB) * (2 * H + 8) + 3 * static_cast<size_t>(HB) * (H + 8) +
                       static_cast<size_t>(HB) * (C + 8)) * sizeof(bf16_t);
@@ -802,17 +874,29 @@ hipError_t eh_st_head(const void* A1, int B, int H, int C, const void* W1b, cons
                      static_cast<const bf16_t*>(WoutT), static_cast<const bf16_t*>(W1T), label_idx, inv_scale,
                      static_cast<bf16_t*>(A1_kt), static_cast<bf16_t*>(h1_kt), static_cast<bf16_t*>(emb_kt),
                      static_cast<bf16_t*>(dlog_kt), static_cast<bf16_t*>(demb_kt), static_cast<bf16_t*>(g1_kt), dA1,
-                     dbfc, loss_acc);
+                     dbfc, loss_acc, prof);
   return hipGetLastError();
 }
 
+// round-up magic division, exact for 31-bit numerators and F1 >= 2: l = ceil(log2 F1),
+// magic = ceil(2^(31+l) / F1), m / F1 == mulhi(m, magic) >> (l - 1)
+static void st_magic(int F1, uint32_t* magic, int* shift) {
+  int l = 0;
+  while ((int64_t(1) << l) < F1) ++l;
+  const uint64_t num = uint64_t(1) << (31 + l);
+  *magic = static_cast<uint32_t>((num + static_cast<uint64_t>(F1) - 1) / static_cast<uint64_t>(F1));
+  *shift = l - 1;
+}
+
 hipError_t eh_st_route(const float* dA1, int H, int64_t nb_rows, int F1, int include_self, float inv_cnt,
-                       const void* h0, int64_t M1, void* g0_kt, hipStream_t s) {
-  if (M1 % 32 != 0 || H % 8 != 0) return hipErrorInvalidValue;
-  const size_t lds = 32 * static_cast<size_t>(H + 8) * sizeof(bf16_t);
-  if (lds > 65536) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(st_route_kernel, dim3(static_cast<uint32_t>(M1 / 32)), dim3(256), lds, s, dA1, H, nb_rows, F1,
-                     include_self, inv_cnt, static_cast<const bf16_t*>(h0), static_cast<bf16_t*>(g0_kt));
+                       const uint32_t* mask, int64_t M1, void* g0_kt, hipStream_t s) {
+  if (M1 % 32 != 0 || H % 8 != 0 || F1 < 1 || M1 >= (int64_t(1) << 31)) return hipErrorInvalidValue;
+  uint32_t magic = 0;
+  int shift = -1;  // F1 == 1: identity
+  if (F1 >= 2) st_magic(F1, &magic, &shift);
+  hipLaunchKernelGGL(st_route_kernel, dim3(static_cast<uint32_t>(M1 / 32)), dim3(256), 0, s, dA1, H,
+                     static_cast<int>(nb_rows), magic, shift, include_self, inv_cnt, mask,
+                     static_cast<bf16_t*>(g0_kt));
   return hipGetLastError();
 }
 
@@ -837,11 +921,7 @@ hipError_t eh_st_dw(int n, const void* const* G, const void* const* X, float* co
       p.inv_cnt = inv_cnt;
       // round-up magic division, exact for 31-bit numerators: l = ceil(log2 F1),
       // magic = ceil(2^(31+l) / F1), m / F1 == mulhi(m, magic) >> (l - 1)
-      int l = 0;
-      while ((int64_t(1) << l) < F1) ++l;
-      const uint64_t num = uint64_t(1) << (31 + l);
-      p.magic = static_cast<uint32_t>((num + static_cast<uint64_t>(F1) - 1) / static_cast<uint64_t>(F1));
-      p.shift = l - 1;
+      st_magic(F1, &p.magic, &p.shift);
     }
     p.G = static_cast<const bf16_t*>(G[i]);
     p.X = static_cast<const bf16_t*>(X[i]);
@@ -883,6 +963,11 @@ static hipError_t st_fill_shadow(StShadow& sh, int count, const int64_t* off, co
   if (count > 6) return hipErrorInvalidValue;
   sh.count = count;
   for (int i = 0; i < count; ++i) {
+    // fm layout needs rows % 16 == 0 and cols % 32 == 0 (and the transpose the converse)
+    if (cols[i] <= 0 || n[i] % cols[i] != 0) return hipErrorInvalidValue;
+    const int64_t rows = n[i] / cols[i];
+    if (rows % 16 != 0 || cols[i] % 32 != 0) return hipErrorInvalidValue;
+    if (shadowT[i] && (rows % 32 != 0 || cols[i] % 16 != 0)) return hipErrorInvalidValue;
     sh.off[i] = off[i];
     sh.n[i] = n[i];
     sh.cols[i] = cols[i];

@@ -83,10 +83,10 @@ int main(int argc, char** argv) {
 
   // local engine over a synthetic graph
   QueryProxy local;
-  Expect(local.InitWithGraph(SyntheticGraph(5000, 6.0, 64, 1, 1, 8, 0, 7, 4), nullptr).ok(), "local init");
+  Expect(local.InitWithGraph(SyntheticGraph(5000, 6.0, 64, 1, 1, 8, 0, 7, false), nullptr).ok(), "local init");
 
   // one graph server (shard 0 of 1) + a remote client through the in-memory registry
-  std::unique_ptr<Graph> served = SyntheticGraph(5000, 6.0, 64, 1, 1, 8, 0, 7, 4);
+  std::unique_ptr<Graph> served = SyntheticGraph(5000, 6.0, 64, 1, 1, 8, 0, 7, false);
   std::unique_ptr<EngineEnv> env = QueryProxy::MakeEnv(served.get(), nullptr, 1);
   ServerOptions so;
   so.num_threads = 8;

@@ -34,6 +34,13 @@ __all__ = ["FusedSageTrainer"]
 _S_ROOTS, _S_HOP = 1, 16
 
 
+def fm_to_dense(t: torch.Tensor) -> torch.Tensor:
+    """Row-major view of a weight shadow stored in the kernels' fragment-major layout
+    Wf[N/16][K/32][4][16][8] (sage_train.hip fm_off); ``t`` has the logical shape [N, K]."""
+    N, K = t.shape
+    return t.reshape(N // 16, K // 32, 4, 16, 8).permute(0, 3, 1, 2, 4).reshape(N, K)
+
+
 class FusedSageTrainer:
     def __init__(self, graph, features: torch.Tensor, labels: torch.Tensor, batch_size: int, fanouts,
                  hidden_dim: int, label_dim: int, lr: float = 0.01, betas=(0.9, 0.999), eps: float = 1e-8,
@@ -85,6 +92,7 @@ class FusedSageTrainer:
         self.gbfc = self.grad[o[3]:o[4]]
         self.gWout = self.grad[o[4]:o[5]]
 
+        # bf16 shadows in the kernels' fragment-major layout (see fm_to_dense); same shapes
         bf = dict(dtype=torch.bfloat16, device=dev)
         self.W0b = torch.empty(H, 2 * D, **bf)
         self.W1b = torch.empty(H, 2 * H, **bf)
@@ -116,10 +124,11 @@ class FusedSageTrainer:
         self.demb_kt = torch.empty(B * H, **bf)
         self.g1_kt = torch.empty(B * H, **bf)
         self.dA1 = torch.empty(B, 2 * H, dtype=torch.float32, device=dev)
-        # outer-layer gradient: with F1 >= 2 the dW kernel rebuilds g0 on the fly from dA1,
-        # the tree layout and the forward's ReLU mask bits (no 2 x 13.6 MB g0 round trip);
-        # otherwise a separate route kernel materialises g0 in kt layout
-        self.fuse_route = F1 >= 2 and os.environ.get("EULER_AMD_FUSE_ROUTE", "1") == "1"
+        # outer-layer gradient g0: the route kernel materialises it in kt layout from dA1, the
+        # tree layout and the forward's ReLU mask bits.  EULER_AMD_FUSE_ROUTE=1 instead rebuilds
+        # g0 fragments inside the dW kernel (no g0 round trip, but 8 scalar loads per MFMA
+        # operand: measured 105 us vs 19 + 19 us for route + dW on MI355X, so off by default)
+        self.fuse_route = F1 >= 2 and os.environ.get("EULER_AMD_FUSE_ROUTE", "0") == "1"
         self.mask0 = torch.empty((M1 // 32) * H, **i32)
         self.g0_kt = None if self.fuse_route else torch.empty(M1 * H, **bf)
         self.loss_acc = torch.zeros(1, dtype=torch.float32, device=dev)
@@ -137,7 +146,7 @@ class FusedSageTrainer:
         self.parts = [torch.empty(s * p * q, dtype=torch.float32, device=dev)
                       for s, (_, _, p, q, _) in zip(self._splits, self._dw)]
         self._grad_views = [self.gW0, self.gW1, self.gWfc, self.gWout]
-        self.bm0 = int(os.environ.get("EULER_AMD_BM0", "64"))  # rows per block of the outer layer
+        self.bm0 = int(os.environ.get("EULER_AMD_BM0", "32"))  # rows per block of the outer layer
 
     # ------------------------------------------------------------------ kernels
     def refresh_shadows(self):
@@ -158,7 +167,7 @@ class FusedSageTrainer:
         h = hip()
         self.sample()
         h.st_sage_fwd(self.features, self.level1, self.nb2, self.F2, self.include_self, self.W0b, self.h0,
-                      self.A0_kt, self.mask0 if self.fuse_route else None, self.bm0)
+                      self.A0_kt, self.mask0, self.bm0)
         # inner hop: tree layout, neighbours of root t are level-1 rows t*F1 .. t*F1+F1-1; its
         # GEMM (h1 = relu(A1 W1^T)) runs inside the head kernel
         h.st_tree_mean(self.h0, self.B, self.F1, self.include_self, self.A1)
@@ -170,7 +179,7 @@ class FusedSageTrainer:
                     [d[3] for d in self._dw], [d[4] for d in self._dw], [self._kps] * 4, self.mask0, self.dA1,
                     self.F1, self.include_self)
         else:
-            h.st_route(self.dA1, self.F1, self.include_self, self.h0, self.g0_kt)
+            h.st_route(self.dA1, self.F1, self.include_self, self.mask0, self.g0_kt)
             h.st_dw([d[0] for d in self._dw], [d[1] for d in self._dw], self.parts, [d[2] for d in self._dw],
                     [d[3] for d in self._dw], [d[4] for d in self._dw], [self._kps] * 4, None, None, 0, False)
         h.st_reduce(self.parts, self._grad_views, self._splits)

@@ -80,9 +80,11 @@ def set_seed(seed: int):
 
 
 def synthetic_graph(num_nodes, avg_degree=10.0, max_degree=1024, node_types=1, edge_types=1, feature_dim=0,
-                    label_dim=0, seed=0, make_current=True):
+                    label_dim=0, seed=0, make_current=True, out_only=False):
+    """Power-law synthetic graph inside the C++ engine.  ``out_only`` keeps only the out
+    CSR (no in-adjacency / edge table): enough for neighbour sampling at 100M-node scale."""
     e = _engine_mod().synthetic(int(num_nodes), float(avg_degree), int(max_degree), int(node_types),
-                                int(edge_types), int(feature_dim), int(label_dim), int(seed))
+                                int(edge_types), int(feature_dim), int(label_dim), int(seed), bool(out_only))
     if make_current:
         use_graph(e)
     return e

@@ -46,11 +46,13 @@ def test_fused_step_grads_match_autograd(cuda, cfg):
         assert cos > 0.995 and rel < 0.06, (name, cos, rel)
 
 
-def test_unfused_route_path_matches_autograd(cuda, monkeypatch):
-    """the materialised-g0 path (route kernel + kt dW) used when the route is not fused"""
-    monkeypatch.setenv("EULER_AMD_FUSE_ROUTE", "0")
-    tr = _setup(cuda, B=64, fanouts=(5, 3), D=64, H=64, C=32)
-    assert not tr.fuse_route
+@pytest.mark.parametrize("fuse,fanouts", [("1", (5, 3)), ("0", (1, 3))])
+def test_route_variants_match_autograd(cuda, monkeypatch, fuse, fanouts):
+    """g0 rebuilt inside the dW kernel (EULER_AMD_FUSE_ROUTE=1), and the route kernel's
+    F1 == 1 identity-division case"""
+    monkeypatch.setenv("EULER_AMD_FUSE_ROUTE", fuse)
+    tr = _setup(cuda, B=64, fanouts=fanouts, D=64, H=64, C=32)
+    assert tr.fuse_route == (fuse == "1")
     tr.forward_backward()
     torch.cuda.synchronize()
     g0 = tr.gW0.clone()
@@ -75,10 +77,14 @@ def test_fused_adam_and_shadows(cuda):
     # bias grad (atomically accumulated) is re-zeroed; loss handed off; shadows refreshed
     assert float(tr.gbfc.abs().sum()) == 0.0
     assert float(tr.loss_acc.item()) == 0.0 and float(tr.loss_out.item()) > 0
-    assert torch.equal(tr.W1b, tr.W1.to(torch.bfloat16))
-    assert torch.equal(tr.W1T, tr.W1.to(torch.bfloat16).t().contiguous())
-    assert torch.equal(tr.WoutT, tr.Wout.to(torch.bfloat16).t().contiguous())
-    assert torch.equal(tr.WfcT, tr.Wfc.to(torch.bfloat16).t().contiguous())
+    from euler_amd.models.sage_step import fm_to_dense
+
+    assert torch.equal(fm_to_dense(tr.W1b), tr.W1.to(torch.bfloat16))
+    assert torch.equal(fm_to_dense(tr.W0b), tr.W0.to(torch.bfloat16))
+    assert torch.equal(fm_to_dense(tr.Woutb), tr.Wout.to(torch.bfloat16))
+    assert torch.equal(fm_to_dense(tr.W1T), tr.W1.to(torch.bfloat16).t())
+    assert torch.equal(fm_to_dense(tr.WoutT), tr.Wout.to(torch.bfloat16).t())
+    assert torch.equal(fm_to_dense(tr.WfcT), tr.Wfc.to(torch.bfloat16).t())
 
 
 def test_fused_step_hipgraph_trains(cuda):
@@ -106,3 +112,4 @@ def test_fused_step_hipgraph_trains(cuda):
     assert losses[-1] < losses[0]
     assert len(roots_seen) > 1  # replays draw fresh samples
     assert int(tr.step_count.item()) == 62  # 2 eager + 60 replays (capture does not execute)
+

@@ -72,3 +72,32 @@ def test_console_commands(fixture_graph):
     assert "nb: 2 4" in text
     assert "feature: 11 12" in text
     assert "unknown command" in text
+
+
+def test_cpu_baseline_runs(tmp_path):
+    """reference-equivalent CPU path on a small graph: loss drops"""
+    import json
+
+    from euler_amd.tools import cpu_baseline
+
+    out = tmp_path / "b.json"
+    res = cpu_baseline.main(["--num-nodes", "20000", "--batch-size", "64", "--fanouts", "5,3", "--feature-dim", "32",
+                             "--hidden-dim", "32", "--label-dim", "8", "--steps", "30", "--warmup", "1",
+                             "--threads", "2", "--out", str(out)])
+    assert res["value"] > 0
+    first, last = res["config"]["loss_first_last"]
+    assert last < first
+    assert json.loads(out.read_text())["value"] == res["value"]
+
+
+def test_engine_out_only_synthetic():
+    import numpy as np
+
+    from euler_amd.ops import base
+
+    e = base.synthetic_graph(5000, 6.0, 64, 1, 1, 8, 4, 3, make_current=False, out_only=True)
+    nb, w, t = e.sample_neighbor(np.arange(10, dtype=np.uint64), [], 4, np.uint64(5000))
+    assert nb.shape == (10, 4) and (nb < 5000).all()
+    f = e.dense_feature(np.arange(3, dtype=np.uint64), "dense_feature", 8)
+    lab = e.dense_feature(np.arange(3, dtype=np.uint64), "dense_label", 4)
+    assert (lab.argmax(1) == f[:, :4].argmax(1)).all()
