@@ -22,7 +22,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from euler_amd.ops import mp_ops
+from euler_amd.ops import gnn_ops, mp_ops
 from euler_amd.ops.mp_ops import SegmentIndex
 from euler_amd.utils.layers import Dense
 
@@ -130,6 +130,12 @@ class GATConv(Conv):
     def forward(self, x, edge_index, size=None, **kwargs):
         x = _pair(x)
         x = [None if t is None else self.fc(t) for t in x]
+        if self.aggr == "add":
+            # fused logits + edge softmax + weighted aggregation (gat.hip)
+            xs = x[1] if x[1] is not None else x[0]
+            out = gnn_ops.gat_aggregate(xs.unsqueeze(1), self.att_j(xs).float(), self.att_i(x[0]).float(),
+                                        edge_index, size, 0.2).squeeze(1)
+            return x[0] + out if self.improved else out
         gx = self.gather_feature([x], edge_index)[0]
         x_i, x_j = gx
         alpha = F.leaky_relu(self.att_i(x_i) + self.att_j(x_j), 0.2)
@@ -339,13 +345,9 @@ class RelationConv(Conv):
         assert edge_attr is not None
         x = _pair(x)
         src = x[1] if x[1] is not None else x[0]
-        xj = mp_ops.gather(src, edge_index[1])
-        rel = edge_attr.reshape(-1).long()
-        out = torch.zeros(xj.shape[0], self.dim, dtype=xj.dtype, device=xj.device)
-        for r in torch.unique(rel).tolist():
-            sel = (rel == r).nonzero(as_tuple=True)[0]
-            out[sel] = xj[sel] @ self.matrix[int(r)].t().to(xj.dtype)
-        return self.fc(x[0]) + self.scatter(out, edge_index, size)
+        # relation-grouped MFMA GEMM with the gather and the mean aggregation fused (rgcn.hip)
+        agg = gnn_ops.relation_transform(src, edge_attr, self.matrix, edge_index, size, "mean")
+        return self.fc(x[0]) + agg.to(src.dtype)
 
 
 class GatedConv(Conv):
@@ -403,13 +405,11 @@ class MultiHeadGATConv(Conv):
         H, Ch = self.heads, self.ch
         h_dst = self.fc(x[0])
         h_src = self.fc(x[1]) if x[1] is not None else h_dst
-        a_i = (h_dst.view(-1, H, Ch) * self.att_i.to(h_dst.dtype)).sum(-1)
-        a_j = (h_src.view(-1, H, Ch) * self.att_j.to(h_src.dtype)).sum(-1)
-        logit = F.leaky_relu(mp_ops.gather(a_i, edge_index[0]) + mp_ops.gather(a_j, edge_index[1]), self.slope)
-        seg = _seg(edge_index, 0, size[0])
-        alpha = mp_ops.scatter_softmax(logit, seg, size[0])  # [E, H]
-        msg = mp_ops.gather(h_src, edge_index[1]).view(-1, H, Ch) * alpha.unsqueeze(-1)
-        out = mp_ops.scatter_add(msg.reshape(-1, H * Ch), seg, size[0])
+        a_i = (h_dst.view(-1, H, Ch).float() * self.att_i.float()).sum(-1)
+        a_j = (h_src.view(-1, H, Ch).float() * self.att_j.float()).sum(-1)
+        # one fused kernel: logits, per-head edge softmax and weighted aggregation (gat.hip)
+        out = gnn_ops.gat_aggregate(h_src.view(-1, H, Ch), a_j, a_i, edge_index, size, self.slope)
+        out = out.reshape(-1, H * Ch)
         if self.improved:
             out = out + h_dst
         if self.concat:

@@ -1,0 +1,298 @@
+// torch binding for the GAT / R-GCN / embedding / unique kernels (gat.hip, rgcn.hip,
+// embed.hip, unique.hip).  Host-only, same rules as binding.cpp: every operand is
+// validated (dtype, device, contiguity, shape) before a launch, launches go to torch's
+// current HIP stream, outputs are allocated by torch's caching allocator.
+#include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime_api.h>
+#include <torch/extension.h>
+
+#include "hip/launchers.h"
+
+namespace {
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void ok(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, "euler_amd HIP kernel '", what, "' failed: ", hipGetErrorString(e));
+}
+
+void dev(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+void typed(const torch::Tensor& t, c10::ScalarType st, const char* name) {
+  dev(t, name);
+  TORCH_CHECK(t.scalar_type() == st, name, " has dtype ", t.scalar_type(), ", expected ", st);
+}
+
+bool bf16_or_f32(const torch::Tensor& t, const char* name) {
+  dev(t, name);
+  TORCH_CHECK(t.scalar_type() == torch::kBFloat16 || t.scalar_type() == torch::kFloat32, name,
+              " must be bfloat16 or float32");
+  return t.scalar_type() == torch::kBFloat16;
+}
+
+// ----------------------------------------------------------------------------- GAT
+bool gat_supported(int64_t H, int64_t C, bool is_bf16) {
+  return eh_gat_supported(static_cast<int>(H), static_cast<int>(C), is_bf16 ? 1 : 0) != 0;
+}
+
+void gat_common(const torch::Tensor& indptr, const torch::Tensor& col, const torch::Tensor& h,
+                const torch::Tensor& al, const torch::Tensor& ar, int64_t H, int64_t C) {
+  typed(indptr, torch::kInt64, "indptr");
+  typed(col, torch::kInt32, "col");
+  bf16_or_f32(h, "h");
+  typed(al, torch::kFloat32, "al");
+  typed(ar, torch::kFloat32, "ar");
+  TORCH_CHECK(h.dim() == 2 && h.size(1) == H * C, "h must be [N, H*C]");
+  TORCH_CHECK(al.dim() == 2 && al.size(0) == h.size(0) && al.size(1) == H, "al must be [N, H]");
+  TORCH_CHECK(ar.dim() == 2 && ar.size(1) == H && ar.size(0) == indptr.numel() - 1, "ar must be [S, H]");
+  TORCH_CHECK(gat_supported(H, C, h.scalar_type() == torch::kBFloat16), "GAT shape H=", H, " C=", C,
+              " is not supported by the fused kernel");
+}
+
+std::vector<torch::Tensor> gat_fwd(torch::Tensor indptr, torch::Tensor col, torch::Tensor h, torch::Tensor al,
+                                   torch::Tensor ar, int64_t H, int64_t C, double slope) {
+  gat_common(indptr, col, h, al, ar, H, C);
+  const c10::DeviceGuard g(h.device());
+  const int64_t S = indptr.numel() - 1;
+  auto out = torch::empty({S, H * C}, h.options());
+  auto lse = torch::empty({S, H}, al.options());
+  ok(eh_gat_fwd(indptr.data_ptr<int64_t>(), col.data_ptr<int32_t>(), S, h.data_ptr(),
+                h.scalar_type() == torch::kBFloat16, al.data_ptr<float>(), ar.data_ptr<float>(), static_cast<int>(H),
+                static_cast<int>(C), static_cast<float>(slope), out.data_ptr(), lse.data_ptr<float>(), stream()),
+     "gat_fwd");
+  return {out, lse};
+}
+
+std::vector<torch::Tensor> gat_bwd(torch::Tensor indptr, torch::Tensor col, torch::Tensor cindptr, torch::Tensor crow,
+                                   torch::Tensor h, torch::Tensor al, torch::Tensor ar, int64_t H, int64_t C,
+                                   double slope, torch::Tensor out, torch::Tensor dout, torch::Tensor lse) {
+  gat_common(indptr, col, h, al, ar, H, C);
+  typed(cindptr, torch::kInt64, "cindptr");
+  typed(crow, torch::kInt32, "crow");
+  TORCH_CHECK(cindptr.numel() == h.size(0) + 1, "cindptr must have N+1 entries");
+  TORCH_CHECK(crow.numel() == col.numel(), "CSC and CSR must hold the same edges");
+  const int64_t S = indptr.numel() - 1, N = h.size(0);
+  TORCH_CHECK(out.sizes() == dout.sizes() && out.size(0) == S && out.size(1) == H * C, "out/dout must be [S, H*C]");
+  typed(out, h.scalar_type(), "out");
+  typed(dout, h.scalar_type(), "dout");
+  typed(lse, torch::kFloat32, "lse");
+  TORCH_CHECK(lse.numel() == S * H, "lse must be [S, H]");
+  const c10::DeviceGuard g(h.device());
+  auto dh = torch::empty_like(h);
+  auto dal = torch::empty_like(al);
+  auto dar = torch::empty_like(ar);
+  auto dv = torch::empty({S, H}, al.options());
+  ok(eh_gat_bwd(indptr.data_ptr<int64_t>(), col.data_ptr<int32_t>(), S, cindptr.data_ptr<int64_t>(),
+                crow.data_ptr<int32_t>(), N, h.data_ptr(), h.scalar_type() == torch::kBFloat16, al.data_ptr<float>(),
+                ar.data_ptr<float>(), static_cast<int>(H), static_cast<int>(C), static_cast<float>(slope),
+                out.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(), dv.data_ptr<float>(), dh.data_ptr(),
+                dal.data_ptr<float>(), dar.data_ptr<float>(), stream()),
+     "gat_bwd");
+  return {dh, dal, dar};
+}
+
+// ----------------------------------------------------------------------------- R-GCN
+void tiles_check(const torch::Tensor& trel, const torch::Tensor& tstart, const torch::Tensor& tlen) {
+  typed(trel, torch::kInt32, "tile_rel");
+  typed(tstart, torch::kInt32, "tile_start");
+  typed(tlen, torch::kInt32, "tile_len");
+  TORCH_CHECK(trel.numel() == tstart.numel() && trel.numel() == tlen.numel(), "tile arrays must match");
+}
+
+void rel_gemm(torch::Tensor A, torch::Tensor a_idx, torch::Tensor trel, torch::Tensor tstart, torch::Tensor tlen,
+              torch::Tensor B, c10::optional<torch::Tensor> scale, torch::Tensor o_idx, int64_t mode, torch::Tensor Y) {
+  typed(A, torch::kBFloat16, "A");
+  typed(B, torch::kBFloat16, "B");
+  typed(a_idx, torch::kInt32, "a_idx");
+  typed(o_idx, torch::kInt32, "o_idx");
+  tiles_check(trel, tstart, tlen);
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 3 && B.size(2) == A.size(1), "A [*, K], B [R, N, K]");
+  const int64_t K = A.size(1), N = B.size(1);
+  TORCH_CHECK(K % 32 == 0 && K <= 1024 && N % 16 == 0, "rel_gemm needs K % 32 == 0, K <= 1024, N % 16 == 0");
+  TORCH_CHECK(a_idx.numel() == o_idx.numel(), "a_idx / o_idx must cover the same edges");
+  if (scale.has_value()) {
+    typed(*scale, torch::kFloat32, "scale");
+    TORCH_CHECK(scale->numel() == a_idx.numel(), "scale must be per edge");
+  }
+  TORCH_CHECK(mode == 0 || mode == 1, "mode: 0 store bf16, 1 atomic-add fp32");
+  typed(Y, mode == 0 ? torch::kBFloat16 : torch::kFloat32, "Y");
+  TORCH_CHECK(Y.dim() == 2 && Y.size(1) == N, "Y must be [rows, N]");
+  const c10::DeviceGuard g(A.device());
+  ok(eh_rel_gemm(A.data_ptr(), static_cast<int>(K), a_idx.data_ptr<int32_t>(), trel.data_ptr<int32_t>(),
+                 tstart.data_ptr<int32_t>(), tlen.data_ptr<int32_t>(), static_cast<int>(trel.numel()), B.data_ptr(),
+                 static_cast<int>(N), scale.has_value() ? scale->data_ptr<float>() : nullptr,
+                 o_idx.data_ptr<int32_t>(), static_cast<int>(mode), Y.data_ptr(), stream()),
+     "rel_gemm");
+}
+
+void rel_gemm_dw(torch::Tensor G, torch::Tensor g_idx, torch::Tensor X, torch::Tensor x_idx,
+                 c10::optional<torch::Tensor> scale, torch::Tensor trel, torch::Tensor tstart, torch::Tensor tlen,
+                 torch::Tensor dW) {
+  typed(G, torch::kBFloat16, "G");
+  typed(X, torch::kBFloat16, "X");
+  typed(g_idx, torch::kInt32, "g_idx");
+  typed(x_idx, torch::kInt32, "x_idx");
+  typed(dW, torch::kFloat32, "dW");
+  tiles_check(trel, tstart, tlen);
+  TORCH_CHECK(G.dim() == 2 && X.dim() == 2 && dW.dim() == 3, "G [*, N], X [*, K], dW [R, N, K]");
+  const int64_t N = G.size(1), K = X.size(1);
+  TORCH_CHECK(dW.size(1) == N && dW.size(2) == K, "dW must be [R, N, K]");
+  TORCH_CHECK(N % 16 == 0 && K % 16 == 0, "rel_gemm_dw needs N, K multiples of 16");
+  TORCH_CHECK(eh_rel_gemm_dw_lds(static_cast<int>(N), static_cast<int>(K)) <= 160 * 1024, "N + K too large");
+  TORCH_CHECK(g_idx.numel() == x_idx.numel(), "g_idx / x_idx must cover the same edges");
+  if (scale.has_value()) {
+    typed(*scale, torch::kFloat32, "scale");
+    TORCH_CHECK(scale->numel() == g_idx.numel(), "scale must be per edge");
+  }
+  const c10::DeviceGuard g(G.device());
+  ok(eh_rel_gemm_dw(G.data_ptr(), static_cast<int>(N), g_idx.data_ptr<int32_t>(), X.data_ptr(), static_cast<int>(K),
+                    x_idx.data_ptr<int32_t>(), scale.has_value() ? scale->data_ptr<float>() : nullptr,
+                    trel.data_ptr<int32_t>(), tstart.data_ptr<int32_t>(), tlen.data_ptr<int32_t>(),
+                    static_cast<int>(trel.numel()), dW.data_ptr<float>(), stream()),
+     "rel_gemm_dw");
+}
+
+// ----------------------------------------------------------------------------- skip-gram loss
+void sgns_check(const torch::Tensor& emb, const torch::Tensor& pos, const torch::Tensor& neg) {
+  const bool bf = bf16_or_f32(emb, "emb");
+  typed(pos, emb.scalar_type(), "pos");
+  typed(neg, emb.scalar_type(), "neg");
+  TORCH_CHECK(emb.dim() == 2 && pos.dim() == 3 && neg.dim() == 3, "emb [B, D], pos [B, P, D], neg [B, K, D]");
+  const int64_t B = emb.size(0), D = emb.size(1);
+  TORCH_CHECK(pos.size(0) == B && neg.size(0) == B && pos.size(2) == D && neg.size(2) == D, "sgns shape mismatch");
+  const int V = bf ? 8 : 4;
+  TORCH_CHECK(D % V == 0 && D / V <= 64, "sgns needs D % ", V, " == 0 and D <= ", 64 * V);
+}
+
+std::vector<torch::Tensor> sgns_fwd(torch::Tensor emb, torch::Tensor pos, torch::Tensor neg) {
+  sgns_check(emb, pos, neg);
+  const c10::DeviceGuard g(emb.device());
+  const int64_t B = emb.size(0), P = pos.size(1), K = neg.size(1);
+  auto fopt = emb.options().dtype(torch::kFloat32);
+  auto logits = torch::empty({B, P + K}, fopt);
+  auto loss_rows = torch::empty({B}, fopt);
+  ok(eh_sgns_fwd(emb.data_ptr(), pos.data_ptr(), neg.data_ptr(), emb.scalar_type() == torch::kBFloat16, B,
+                 static_cast<int>(P), static_cast<int>(K), static_cast<int>(emb.size(1)), logits.data_ptr<float>(),
+                 loss_rows.data_ptr<float>(), stream()),
+     "sgns_fwd");
+  return {logits, loss_rows};
+}
+
+std::vector<torch::Tensor> sgns_bwd(torch::Tensor emb, torch::Tensor pos, torch::Tensor neg, torch::Tensor logits,
+                                    double gscale) {
+  sgns_check(emb, pos, neg);
+  typed(logits, torch::kFloat32, "logits");
+  const int64_t B = emb.size(0), P = pos.size(1), K = neg.size(1);
+  TORCH_CHECK(logits.numel() == B * (P + K), "logits must be [B, P+K]");
+  const c10::DeviceGuard g(emb.device());
+  auto demb = torch::empty_like(emb);
+  auto dpos = torch::empty_like(pos);
+  auto dneg = torch::empty_like(neg);
+  ok(eh_sgns_bwd(emb.data_ptr(), pos.data_ptr(), neg.data_ptr(), emb.scalar_type() == torch::kBFloat16, B,
+                 static_cast<int>(P), static_cast<int>(K), static_cast<int>(emb.size(1)), logits.data_ptr<float>(),
+                 static_cast<float>(gscale), demb.data_ptr(), dpos.data_ptr(), dneg.data_ptr(), stream()),
+     "sgns_bwd");
+  return {demb, dpos, dneg};
+}
+
+// ----------------------------------------------------------------------------- KG scores
+struct KgIn {
+  int64_t B, K, D, nneg;
+};
+
+KgIn kg_check(const torch::Tensor& ent, const torch::Tensor& rel, const torch::Tensor& src, const torch::Tensor& dst,
+              const torch::Tensor& ridx, const torch::Tensor& neg, int64_t kind, int64_t corrupt) {
+  typed(ent, torch::kFloat32, "ent");
+  typed(rel, torch::kFloat32, "rel");
+  for (const auto* t : {&src, &dst, &ridx, &neg}) typed(*t, torch::kInt64, "kg index");
+  TORCH_CHECK(ent.dim() == 2 && rel.dim() == 2 && ent.size(1) == rel.size(1), "ent [Ne, D], rel [Nr, D]");
+  const int64_t B = src.numel(), D = ent.size(1);
+  TORCH_CHECK(dst.numel() == B && ridx.numel() == B, "src/dst/rel index must have B entries");
+  TORCH_CHECK(B == 0 || neg.numel() % B == 0, "neg must be [B, K]");
+  TORCH_CHECK(D % 4 == 0 && D <= 256, "kg kernels need D % 4 == 0 and D <= 256");
+  TORCH_CHECK(kind >= 0 && kind <= 2 && corrupt >= 0 && corrupt <= 2, "bad kind / corrupt");
+  const int64_t K = B ? neg.numel() / B : 0;
+  return KgIn{B, K, D, corrupt == 2 ? 2 * K : K};
+}
+
+std::vector<torch::Tensor> kg_fwd(torch::Tensor ent, torch::Tensor rel, torch::Tensor src, torch::Tensor dst,
+                                  torch::Tensor ridx, torch::Tensor neg, int64_t kind, int64_t corrupt,
+                                  bool normalize) {
+  const KgIn k = kg_check(ent, rel, src, dst, ridx, neg, kind, corrupt);
+  const c10::DeviceGuard g(ent.device());
+  auto pos_s = torch::empty({k.B}, ent.options());
+  auto neg_s = torch::empty({k.B, k.nneg}, ent.options());
+  ok(eh_kg_fwd(ent.data_ptr<float>(), rel.data_ptr<float>(), src.data_ptr<int64_t>(), dst.data_ptr<int64_t>(),
+               ridx.data_ptr<int64_t>(), neg.data_ptr<int64_t>(), k.B, static_cast<int>(k.K), static_cast<int>(k.D),
+               static_cast<int>(kind), static_cast<int>(corrupt), normalize ? 1 : 0, pos_s.data_ptr<float>(),
+               neg_s.data_ptr<float>(), stream()),
+     "kg_fwd");
+  return {pos_s, neg_s};
+}
+
+void kg_bwd(torch::Tensor ent, torch::Tensor rel, torch::Tensor src, torch::Tensor dst, torch::Tensor ridx,
+            torch::Tensor neg, int64_t kind, int64_t corrupt, bool normalize, torch::Tensor gpos, torch::Tensor gneg,
+            torch::Tensor dent, torch::Tensor drel) {
+  const KgIn k = kg_check(ent, rel, src, dst, ridx, neg, kind, corrupt);
+  typed(gpos, torch::kFloat32, "gpos");
+  typed(gneg, torch::kFloat32, "gneg");
+  typed(dent, torch::kFloat32, "dent");
+  typed(drel, torch::kFloat32, "drel");
+  TORCH_CHECK(gpos.numel() == k.B && gneg.numel() == k.B * k.nneg, "score grads must match the scores");
+  TORCH_CHECK(dent.sizes() == ent.sizes() && drel.sizes() == rel.sizes(), "table grads must match the tables");
+  const c10::DeviceGuard g(ent.device());
+  ok(eh_kg_bwd(ent.data_ptr<float>(), rel.data_ptr<float>(), src.data_ptr<int64_t>(), dst.data_ptr<int64_t>(),
+               ridx.data_ptr<int64_t>(), neg.data_ptr<int64_t>(), k.B, static_cast<int>(k.K), static_cast<int>(k.D),
+               static_cast<int>(kind), static_cast<int>(corrupt), normalize ? 1 : 0, gpos.data_ptr<float>(),
+               gneg.data_ptr<float>(), dent.data_ptr<float>(), drel.data_ptr<float>(), stream()),
+     "kg_bwd");
+}
+
+// ----------------------------------------------------------------------------- unique
+std::vector<torch::Tensor> unique_first(torch::Tensor x) {
+  typed(x, torch::kInt64, "x");
+  const int64_t n = x.numel();
+  TORCH_CHECK(n < (1ll << 30), "unique_first supports < 2^30 elements");
+  const c10::DeviceGuard g(x.device());
+  auto opts = x.options();
+  if (n == 0) return {torch::empty({0}, opts), torch::empty({0}, opts)};
+  int64_t cap = 1;
+  while (cap < 2 * n) cap <<= 1;
+  auto keys = torch::full({cap}, std::numeric_limits<int64_t>::min(), opts);
+  auto minpos = torch::full({cap}, std::numeric_limits<int32_t>::max(), opts.dtype(torch::kInt32));
+  auto slot = torch::empty({n}, opts.dtype(torch::kInt32));
+  auto flag = torch::empty({n}, opts.dtype(torch::kInt32));
+  ok(eh_unique_insert(x.data_ptr<int64_t>(), n, keys.data_ptr(), minpos.data_ptr<int32_t>(), cap,
+                      slot.data_ptr<int32_t>(), stream()),
+     "unique_insert");
+  ok(eh_unique_mark(n, slot.data_ptr<int32_t>(), minpos.data_ptr<int32_t>(), flag.data_ptr<int32_t>(), stream()),
+     "unique_mark");
+  auto pos = torch::cumsum(flag, 0, torch::kInt32);
+  const int64_t u = pos[n - 1].item<int32_t>();
+  auto uniq = torch::empty({u}, opts);
+  auto inv = torch::empty({n}, opts);
+  ok(eh_unique_finalize(x.data_ptr<int64_t>(), n, slot.data_ptr<int32_t>(), minpos.data_ptr<int32_t>(),
+                        flag.data_ptr<int32_t>(), pos.data_ptr<int32_t>(), inv.data_ptr<int64_t>(),
+                        uniq.data_ptr<int64_t>(), stream()),
+     "unique_finalize");
+  return {uniq, inv};
+}
+
+}  // namespace
+
+void register_gnn_ops(pybind11::module& m) {
+  m.def("gat_supported", &gat_supported);
+  m.def("gat_fwd", &gat_fwd);
+  m.def("gat_bwd", &gat_bwd);
+  m.def("rel_gemm", &rel_gemm);
+  m.def("rel_gemm_dw", &rel_gemm_dw);
+  m.def("sgns_fwd", &sgns_fwd);
+  m.def("sgns_bwd", &sgns_bwd);
+  m.def("kg_fwd", &kg_fwd);
+  m.def("kg_bwd", &kg_bwd);
+  m.def("unique_first", &unique_first);
+}

@@ -1,0 +1,381 @@
+// Embedding-training kernels:
+//
+//   sgns_fwd / sgns_bwd  (K11) skip-gram / unsupervised sigmoid-CE over
+//       logits[b, k] = <emb[b], ctx[b, k]>, label 1 for the P positives, 0 for the K negatives
+//       (reference mp_utils/base.py:80-91, solution/logits.py:30-34: a batched matmul, two
+//       sigmoid-CE ops, a concat and a mean; and the same again in the backward)
+//   kg_fwd / kg_bwd      (K10) TransE (L1 / L2) and DistMult scores that gather the entity /
+//       relation rows straight from the tables, L2-normalise them in registers and, in the
+//       backward, push the row gradients through the normalisation and atomically into the
+//       fp32 table gradients (reference examples/TransX/transX.py:72-145,
+//       distmult.py:74-77: 4 embedding lookups, 4 normalisations, tile copies per negative).
+//
+// Both map one row b to a group of lanes (4 fp32 / 8 bf16 columns per lane) like gat.hip,
+// so a wave covers several short rows and the row reductions are group shuffles.
+#include "hip/common.h"
+#include "hip/launchers.h"
+
+namespace euler_hip {
+
+template <typename T>
+struct EV;
+template <>
+struct EV<bf16_t> {
+  static constexpr int N = 8;
+  __device__ __forceinline__ static void load(const bf16_t* p, float* f) {
+    const uint4_t u = *reinterpret_cast<const uint4_t*>(p);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f[2 * i] = __uint_as_float(u[i] << 16);
+      f[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u);
+    }
+  }
+  __device__ __forceinline__ static void store(bf16_t* p, const float* f) {
+    *reinterpret_cast<uint4_t*>(p) = pack_bf16x8(f);
+  }
+};
+template <>
+struct EV<float> {
+  static constexpr int N = 4;
+  __device__ __forceinline__ static void load(const float* p, float* f) {
+    const float4_t u = *reinterpret_cast<const float4_t*>(p);
+    f[0] = u[0];
+    f[1] = u[1];
+    f[2] = u[2];
+    f[3] = u[3];
+  }
+  __device__ __forceinline__ static void store(float* p, const float* f) {
+    *reinterpret_cast<float4_t*>(p) = float4_t{f[0], f[1], f[2], f[3]};
+  }
+};
+
+// sum over aligned groups of g lanes; all lanes of a group follow the same path
+__device__ __forceinline__ float emb_group_sum(float v, int g) {
+  for (int o = g >> 1; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+struct RowLane {
+  int64_t row;
+  int sub;
+  bool ok;
+};
+__device__ __forceinline__ RowLane row_lane(int lp, int64_t rows) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  RowLane r;
+  r.row = wave * (64 / lp) + lane / lp;
+  r.sub = lane & (lp - 1);
+  r.ok = r.row < rows;
+  return r;
+}
+
+// numerically stable sigmoid cross-entropy with logits
+__device__ __forceinline__ float sigmoid_ce(float x, float y) {
+  return fmaxf(x, 0.f) - x * y + __logf(1.f + __expf(-fabsf(x)));
+}
+__device__ __forceinline__ float sigmoidf(float x) { return 1.f / (1.f + __expf(-x)); }
+
+// ----------------------------------------------------------------------------- K11
+// emb [B, D], pos [B, P, D], neg [B, K, D]; a row is D/V chunks, one per lane of its group
+template <typename T>
+__global__ __launch_bounds__(256) void sgns_fwd_kernel(const T* __restrict__ emb, const T* __restrict__ pos,
+                                                       const T* __restrict__ neg, int64_t B, int P, int K, int D,
+                                                       int lp, float* __restrict__ logits,
+                                                       float* __restrict__ loss_rows) {
+  constexpr int V = EV<T>::N;
+  const RowLane L = row_lane(lp, B);
+  const bool ok = L.ok && L.sub * V < D;
+  float e[V], c[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) e[v] = 0.f;
+  if (ok) EV<T>::load(emb + L.row * D + L.sub * V, e);
+  float loss = 0.f;
+  const int KK = P + K;
+  for (int k = 0; k < KK; ++k) {
+    const bool is_pos = k < P;
+    float part = 0.f;
+    if (ok) {
+      const T* src = is_pos ? pos + (L.row * P + k) * D : neg + (L.row * K + (k - P)) * D;
+      EV<T>::load(src + L.sub * V, c);
+#pragma unroll
+      for (int v = 0; v < V; ++v) part += e[v] * c[v];
+    }
+    const float x = emb_group_sum(part, lp);
+    loss += sigmoid_ce(x, is_pos ? 1.f : 0.f);
+    if (L.ok && L.sub == 0) logits[L.row * KK + k] = x;
+  }
+  if (L.ok && L.sub == 0) loss_rows[L.row] = loss;
+}
+
+// g_bk = (sigmoid(x) - y) * gscale ; demb = sum_k g ctx ; dctx = g emb
+template <typename T>
+__global__ __launch_bounds__(256) void sgns_bwd_kernel(const T* __restrict__ emb, const T* __restrict__ pos,
+                                                       const T* __restrict__ neg, int64_t B, int P, int K, int D,
+                                                       int lp, const float* __restrict__ logits, float gscale,
+                                                       T* __restrict__ demb, T* __restrict__ dpos,
+                                                       T* __restrict__ dneg) {
+  constexpr int V = EV<T>::N;
+  const RowLane L = row_lane(lp, B);
+  if (!L.ok || L.sub * V >= D) return;  // no cross-lane exchange in the backward
+  float e[V], c[V], de[V], dc[V];
+  EV<T>::load(emb + L.row * D + L.sub * V, e);
+#pragma unroll
+  for (int v = 0; v < V; ++v) de[v] = 0.f;
+  const int KK = P + K;
+  for (int k = 0; k < KK; ++k) {
+    const bool is_pos = k < P;
+    const int64_t off = is_pos ? (L.row * P + k) * D : (L.row * K + (k - P)) * D;
+    const float g = (sigmoidf(logits[L.row * KK + k]) - (is_pos ? 1.f : 0.f)) * gscale;
+    EV<T>::load((is_pos ? pos : neg) + off + L.sub * V, c);
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      de[v] += g * c[v];
+      dc[v] = g * e[v];
+    }
+    EV<T>::store((is_pos ? dpos : dneg) + off + L.sub * V, dc);
+  }
+  EV<T>::store(demb + L.row * D + L.sub * V, de);
+}
+
+// ----------------------------------------------------------------------------- K10
+// score kinds: 0 TransE-L1, 1 TransE-L2, 2 DistMult.  corrupt: 0 front (neg replaces src),
+// 1 tail (neg replaces dst), 2 both (front scores then tail scores).  Tables fp32 [*, D].
+struct KgArgs {
+  const float* ent;
+  const float* rel;
+  const int64_t* src;
+  const int64_t* dst;
+  const int64_t* ridx;
+  const int64_t* neg;
+  int64_t B;
+  int K, D, kind, corrupt, normalize, lp;
+};
+
+__device__ __forceinline__ void kg_load_norm(const float* tab, int64_t row, int sub, int D, int lp, bool normalize,
+                                             float* x, float& nrm) {
+  float part = 0.f;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) x[v] = 0.f;
+  if (sub * 4 < D && row >= 0) {
+    EV<float>::load(tab + row * D + sub * 4, x);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) part += x[v] * x[v];
+  }
+  nrm = 1.f;
+  if (normalize) {
+    nrm = fmaxf(sqrtf(emb_group_sum(part, lp)), 1e-12f);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) x[v] /= nrm;
+  }
+}
+
+// this lane's part of a score; the caller reduces over the group
+__device__ __forceinline__ float kg_part(int kind, const float* h, const float* r, const float* t) {
+  float p = 0.f;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    if (kind == 2) {
+      p += h[v] * r[v] * t[v];
+    } else {
+      const float d = h[v] + r[v] - t[v];
+      p += kind == 0 ? fabsf(d) : d * d;
+    }
+  }
+  return p;
+}
+
+__device__ __forceinline__ float kg_finish(int kind, float s) {
+  return kind == 0 ? -s : (kind == 1 ? -sqrtf(s) : s);
+}
+
+__global__ __launch_bounds__(256) void kg_fwd_kernel(KgArgs a, float* __restrict__ pos_score,
+                                                     float* __restrict__ neg_score) {
+  const RowLane L = row_lane(a.lp, a.B);
+  if (!L.ok) return;  // whole lane groups exit together
+  float h[4], r[4], t[4], n[4], nh, nr, nt, nn;
+  kg_load_norm(a.ent, a.src[L.row], L.sub, a.D, a.lp, a.normalize, h, nh);
+  kg_load_norm(a.rel, a.ridx[L.row], L.sub, a.D, a.lp, a.normalize, r, nr);
+  kg_load_norm(a.ent, a.dst[L.row], L.sub, a.D, a.lp, a.normalize, t, nt);
+  const float ps = kg_finish(a.kind, emb_group_sum(kg_part(a.kind, h, r, t), a.lp));
+  if (L.sub == 0) pos_score[L.row] = ps;
+  const int nneg = a.corrupt == 2 ? 2 * a.K : a.K;
+  for (int k = 0; k < a.K; ++k) {
+    kg_load_norm(a.ent, a.neg[L.row * a.K + k], L.sub, a.D, a.lp, a.normalize, n, nn);
+    if (a.corrupt != 1) {  // front
+      const float s = kg_finish(a.kind, emb_group_sum(kg_part(a.kind, n, r, t), a.lp));
+      if (L.sub == 0) neg_score[L.row * nneg + k] = s;
+    }
+    if (a.corrupt != 0) {  // tail
+      const float s = kg_finish(a.kind, emb_group_sum(kg_part(a.kind, h, r, n), a.lp));
+      if (L.sub == 0) neg_score[L.row * nneg + (a.corrupt == 2 ? a.K : 0) + k] = s;
+    }
+  }
+}
+
+// d score / d (h, r, t) of one score with upstream g, accumulated into dh, dr, dt
+__device__ __forceinline__ void kg_grad(int kind, int lp, float g, const float* h, const float* r, const float* t,
+                                        float* dh, float* dr, float* dt) {
+  float coef = 1.f;
+  if (kind == 1) {
+    float p = 0.f;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const float d = h[v] + r[v] - t[v];
+      p += d * d;
+    }
+    const float nrm = sqrtf(emb_group_sum(p, lp));
+    coef = nrm > 0.f ? 1.f / nrm : 0.f;
+  }
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    if (kind == 2) {
+      dh[v] += g * r[v] * t[v];
+      dr[v] += g * h[v] * t[v];
+      dt[v] += g * h[v] * r[v];
+    } else {
+      const float d = h[v] + r[v] - t[v];
+      // score = -|d|_1  or  -|d|_2
+      const float gd = -g * (kind == 0 ? (d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f)) : d * coef);
+      dh[v] += gd;
+      dr[v] += gd;
+      dt[v] -= gd;
+    }
+  }
+}
+
+// push the gradient w.r.t. a normalised row through x / |x| and add it to the table grad
+__device__ __forceinline__ void kg_scatter(float* __restrict__ dtab, int64_t row, int sub, int D, int lp,
+                                           bool normalize, const float* xhat, float nrm, float* dx) {
+  if (normalize) {
+    float p = 0.f;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) p += xhat[v] * dx[v];
+    const float dot = emb_group_sum(p, lp);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) dx[v] = (dx[v] - xhat[v] * dot) / nrm;
+  }
+  if (sub * 4 < D && row >= 0) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) atomicAdd(dtab + row * D + sub * 4 + v, dx[v]);
+  }
+}
+
+__global__ __launch_bounds__(256) void kg_bwd_kernel(KgArgs a, const float* __restrict__ gpos,
+                                                     const float* __restrict__ gneg, float* __restrict__ dent,
+                                                     float* __restrict__ drel) {
+  const RowLane L = row_lane(a.lp, a.B);
+  if (!L.ok) return;
+  float h[4], r[4], t[4], n[4], nh, nr, nt, nn;
+  float dh[4] = {0.f, 0.f, 0.f, 0.f}, dr[4] = {0.f, 0.f, 0.f, 0.f}, dt[4] = {0.f, 0.f, 0.f, 0.f};
+  const int64_t hs = a.src[L.row], rs = a.ridx[L.row], ts = a.dst[L.row];
+  kg_load_norm(a.ent, hs, L.sub, a.D, a.lp, a.normalize, h, nh);
+  kg_load_norm(a.rel, rs, L.sub, a.D, a.lp, a.normalize, r, nr);
+  kg_load_norm(a.ent, ts, L.sub, a.D, a.lp, a.normalize, t, nt);
+  kg_grad(a.kind, a.lp, gpos[L.row], h, r, t, dh, dr, dt);
+  const int nneg = a.corrupt == 2 ? 2 * a.K : a.K;
+  for (int k = 0; k < a.K; ++k) {
+    const int64_t ns = a.neg[L.row * a.K + k];
+    kg_load_norm(a.ent, ns, L.sub, a.D, a.lp, a.normalize, n, nn);
+    float dn[4] = {0.f, 0.f, 0.f, 0.f};
+    if (a.corrupt != 1) kg_grad(a.kind, a.lp, gneg[L.row * nneg + k], n, r, t, dn, dr, dt);
+    if (a.corrupt != 0)
+      kg_grad(a.kind, a.lp, gneg[L.row * nneg + (a.corrupt == 2 ? a.K : 0) + k], h, r, n, dh, dr, dn);
+    kg_scatter(dent, ns, L.sub, a.D, a.lp, a.normalize, n, nn, dn);
+  }
+  kg_scatter(dent, hs, L.sub, a.D, a.lp, a.normalize, h, nh, dh);
+  kg_scatter(drel, rs, L.sub, a.D, a.lp, a.normalize, r, nr, dr);
+  kg_scatter(dent, ts, L.sub, a.D, a.lp, a.normalize, t, nt, dt);
+}
+
+inline int row_lanes(int chunks) {
+  int lp = 1;
+  while (lp < chunks && lp < 64) lp <<= 1;
+  return lp;
+}
+inline dim3 row_grid(int64_t rows, int lp) {
+  const int64_t rpw = 64 / lp;
+  const int64_t waves = (rows + rpw - 1) / rpw;
+  return dim3(static_cast<uint32_t>((waves + 3) / 4));
+}
+
+}  // namespace euler_hip
+
+using namespace euler_hip;
+
+extern "C" {
+
+hipError_t eh_sgns_fwd(const void* emb, const void* pos, const void* neg, int is_bf16, int64_t B, int P, int K, int D,
+                       float* logits, float* loss_rows, hipStream_t s) {
+  if (B == 0) return hipSuccess;
+  const int V = is_bf16 ? 8 : 4;
+  if (D % V != 0 || D / V > 64) return hipErrorInvalidValue;
+  const int lp = row_lanes(D / V);
+  if (is_bf16)
+    hipLaunchKernelGGL(sgns_fwd_kernel<bf16_t>, row_grid(B, lp), dim3(256), 0, s, static_cast<const bf16_t*>(emb),
+                       static_cast<const bf16_t*>(pos), static_cast<const bf16_t*>(neg), B, P, K, D, lp, logits,
+                       loss_rows);
+  else
+    hipLaunchKernelGGL(sgns_fwd_kernel<float>, row_grid(B, lp), dim3(256), 0, s, static_cast<const float*>(emb),
+                       static_cast<const float*>(pos), static_cast<const float*>(neg), B, P, K, D, lp, logits,
+                       loss_rows);
+  return hipGetLastError();
+}
+
+hipError_t eh_sgns_bwd(const void* emb, const void* pos, const void* neg, int is_bf16, int64_t B, int P, int K, int D,
+                       const float* logits, float gscale, void* demb, void* dpos, void* dneg, hipStream_t s) {
+  if (B == 0) return hipSuccess;
+  const int V = is_bf16 ? 8 : 4;
+  if (D % V != 0 || D / V > 64) return hipErrorInvalidValue;
+  const int lp = row_lanes(D / V);
+  if (is_bf16)
+    hipLaunchKernelGGL(sgns_bwd_kernel<bf16_t>, row_grid(B, lp), dim3(256), 0, s, static_cast<const bf16_t*>(emb),
+                       static_cast<const bf16_t*>(pos), static_cast<const bf16_t*>(neg), B, P, K, D, lp, logits,
+                       gscale, static_cast<bf16_t*>(demb), static_cast<bf16_t*>(dpos), static_cast<bf16_t*>(dneg));
+  else
+    hipLaunchKernelGGL(sgns_bwd_kernel<float>, row_grid(B, lp), dim3(256), 0, s, static_cast<const float*>(emb),
+                       static_cast<const float*>(pos), static_cast<const float*>(neg), B, P, K, D, lp, logits, gscale,
+                       static_cast<float*>(demb), static_cast<float*>(dpos), static_cast<float*>(dneg));
+  return hipGetLastError();
+}
+
+static KgArgs kg_args(const float* ent, const float* rel, const int64_t* src, const int64_t* dst, const int64_t* ridx,
+                      const int64_t* neg, int64_t B, int K, int D, int kind, int corrupt, int normalize) {
+  KgArgs a;
+  a.ent = ent;
+  a.rel = rel;
+  a.src = src;
+  a.dst = dst;
+  a.ridx = ridx;
+  a.neg = neg;
+  a.B = B;
+  a.K = K;
+  a.D = D;
+  a.kind = kind;
+  a.corrupt = corrupt;
+  a.normalize = normalize;
+  a.lp = row_lanes((D + 3) / 4);
+  return a;
+}
+
+hipError_t eh_kg_fwd(const float* ent, const float* rel, const int64_t* src, const int64_t* dst, const int64_t* ridx,
+                     const int64_t* neg, int64_t B, int K, int D, int kind, int corrupt, int normalize,
+                     float* pos_score, float* neg_score, hipStream_t s) {
+  if (B == 0) return hipSuccess;
+  if (D % 4 != 0 || D > 256 || kind < 0 || kind > 2 || corrupt < 0 || corrupt > 2) return hipErrorInvalidValue;
+  const KgArgs a = kg_args(ent, rel, src, dst, ridx, neg, B, K, D, kind, corrupt, normalize);
+  hipLaunchKernelGGL(kg_fwd_kernel, row_grid(B, a.lp), dim3(256), 0, s, a, pos_score, neg_score);
+  return hipGetLastError();
+}
+
+hipError_t eh_kg_bwd(const float* ent, const float* rel, const int64_t* src, const int64_t* dst, const int64_t* ridx,
+                     const int64_t* neg, int64_t B, int K, int D, int kind, int corrupt, int normalize,
+                     const float* gpos, const float* gneg, float* dent, float* drel, hipStream_t s) {
+  if (B == 0) return hipSuccess;
+  if (D % 4 != 0 || D > 256 || kind < 0 || kind > 2 || corrupt < 0 || corrupt > 2) return hipErrorInvalidValue;
+  const KgArgs a = kg_args(ent, rel, src, dst, ridx, neg, B, K, D, kind, corrupt, normalize);
+  hipLaunchKernelGGL(kg_bwd_kernel, row_grid(B, a.lp), dim3(256), 0, s, a, gpos, gneg, dent, drel);
+  return hipGetLastError();
+}
+
+}  // extern "C"

@@ -78,6 +78,45 @@ hipError_t eh_st_adam(float* p, float* g, float* m, float* v, int64_t n, const i
 hipError_t eh_st_shadow(const float* p, int64_t n, int sh_count, const int64_t* sh_off, const int64_t* sh_n,
                         const int* sh_cols, void* const* sh_ptr, void* const* shT_ptr, hipStream_t s);
 
+// gat.hip (K5: fused multi-head GAT edge-softmax + aggregation)
+int eh_gat_supported(int H, int C, int is_bf16);
+hipError_t eh_gat_fwd(const int64_t* indptr, const int32_t* col, int64_t S, const void* h, int is_bf16,
+                      const float* al, const float* ar, int H, int C, float slope, void* out, float* lse,
+                      hipStream_t s);
+hipError_t eh_gat_bwd(const int64_t* indptr, const int32_t* col, int64_t S, const int64_t* cindptr,
+                      const int32_t* crow, int64_t N, const void* h, int is_bf16, const float* al, const float* ar,
+                      int H, int C, float slope, const void* out, const void* dout, const float* lse, float* dv,
+                      void* dh, float* dal, float* dar, hipStream_t s);
+
+// rgcn.hip (K6: relation-grouped MFMA GEMM)
+size_t eh_rel_gemm_lds(int K);
+size_t eh_rel_gemm_dw_lds(int N, int K);
+hipError_t eh_rel_gemm(const void* A, int K, const int32_t* a_idx, const int32_t* trel, const int32_t* tstart,
+                       const int32_t* tlen, int n_tiles, const void* B, int N, const float* scale,
+                       const int32_t* o_idx, int mode, void* Y, hipStream_t s);
+hipError_t eh_rel_gemm_dw(const void* G, int N, const int32_t* g_idx, const void* X, int K, const int32_t* x_idx,
+                          const float* scale, const int32_t* trel, const int32_t* tstart, const int32_t* tlen,
+                          int n_tiles, float* dW, hipStream_t s);
+
+// embed.hip (K10 knowledge-graph scores, K11 skip-gram sigmoid-CE)
+hipError_t eh_sgns_fwd(const void* emb, const void* pos, const void* neg, int is_bf16, int64_t B, int P, int K, int D,
+                       float* logits, float* loss_rows, hipStream_t s);
+hipError_t eh_sgns_bwd(const void* emb, const void* pos, const void* neg, int is_bf16, int64_t B, int P, int K, int D,
+                       const float* logits, float gscale, void* demb, void* dpos, void* dneg, hipStream_t s);
+hipError_t eh_kg_fwd(const float* ent, const float* rel, const int64_t* src, const int64_t* dst, const int64_t* ridx,
+                     const int64_t* neg, int64_t B, int K, int D, int kind, int corrupt, int normalize,
+                     float* pos_score, float* neg_score, hipStream_t s);
+hipError_t eh_kg_bwd(const float* ent, const float* rel, const int64_t* src, const int64_t* dst, const int64_t* ridx,
+                     const int64_t* neg, int64_t B, int K, int D, int kind, int corrupt, int normalize,
+                     const float* gpos, const float* gneg, float* dent, float* drel, hipStream_t s);
+
+// unique.hip (K8: hash unique, first-occurrence order)
+hipError_t eh_unique_insert(const int64_t* x, int64_t n, void* keys, int32_t* minpos, int64_t cap, int32_t* slot,
+                            hipStream_t s);
+hipError_t eh_unique_mark(int64_t n, const int32_t* slot, const int32_t* minpos, int32_t* flag, hipStream_t s);
+hipError_t eh_unique_finalize(const int64_t* x, int64_t n, const int32_t* slot, const int32_t* minpos,
+                              const int32_t* flag, const int32_t* pos, int64_t* inv, int64_t* uniq, hipStream_t s);
+
 // optim.hip
 hipError_t eh_flat_optim(float* p, const float* g, float* m, float* v, int64_t n, int64_t* step, float lr, float b1,
                          float b2, float eps, float wd, float grad_scale, int kind, hipStream_t s);

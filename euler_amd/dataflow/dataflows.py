@@ -17,6 +17,7 @@ from __future__ import annotations
 import torch
 
 import euler_amd.ops.graph_api as ge
+from euler_amd.ops.gnn_ops import unique_first
 
 __all__ = ["Block", "DataFlow", "NeighborDataFlow", "UniqueDataFlow", "SageDataFlow", "GCNDataFlow",
            "FastGCNDataFlow", "LayerwiseDataFlow", "LayerwiseEachDataFlow", "WholeDataFlow", "RelationDataFlow",
@@ -24,9 +25,10 @@ __all__ = ["Block", "DataFlow", "NeighborDataFlow", "UniqueDataFlow", "SageDataF
 
 
 def unique_with_inverse(x: torch.Tensor):
-    """(unique values, inverse) — the role of ``tf.unique`` (order: sorted)."""
-    u, inv = torch.unique(x.reshape(-1), sorted=True, return_inverse=True)
-    return u, inv
+    """(unique values, inverse) — ``tf.unique`` semantics: first-occurrence order, so
+    the previous hop's nodes keep their positions (GPU tensors: hash-table kernel
+    ``unique.hip``; CPU: sort-based, same result)."""
+    return unique_first(x)
 
 
 class Block:

@@ -18,6 +18,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 import euler_amd.ops.graph_api as ge
+from euler_amd.ops import gnn_ops
 from euler_amd.parallel.embedding import ShardedEmbedding
 from euler_amd.utils import metrics as M
 from euler_amd.utils.layers import Embedding
@@ -82,10 +83,29 @@ class TransX(nn.Module):
     def generate_embedding(self, src, dst, neg, rel):
         raise NotImplementedError
 
+    # score kind of the fused gfx950 kernel (embed.hip kg_fwd / kg_bwd), None = unfused
+    fused_kind = None
+
+    def _fused_forward(self, src, dst, neg, rel):
+        """gather + l2-normalise + score of the positive and every corrupted triple, and
+        the whole backward into the two tables, in two kernels."""
+        ent, rtab = self.entity_encoder, self.relation_encoder
+        pos_s, neg_s = gnn_ops.kg_score(ent.weight, rtab.weight, ent._rows(src), ent._rows(dst),
+                                        rtab._rows(rel), ent._rows(neg), self.fused_kind, self.corrupt, True)
+        pos, neg_s = pos_s.view(-1, 1, 1), neg_s.view(pos_s.shape[0], 1, -1)
+        loss = self.loss_fn(pos, neg_s)
+        metric = self.metric(pos.detach().float().cpu(), neg_s.detach().float().cpu())
+        with torch.no_grad():
+            s, d, r = self.norm_emb(ent(src)), self.norm_emb(ent(dst)), self.norm_emb(rtab(rel))
+        return [s.reshape(-1, s.shape[-1]), r.reshape(-1, r.shape[-1]), d.reshape(-1, d.shape[-1])], loss, \
+            self.metric_name, metric
+
     def forward(self, inputs):
         src, dst, neg, rel = self.generate_triplets(inputs)
         dev = self._dev()
         src, dst, neg, rel = src.to(dev), dst.to(dev), neg.to(dev), rel.to(dev)
+        if self.fused_kind is not None and dev.type == "cuda" and isinstance(self.entity_encoder, Embedding):
+            return self._fused_forward(src, dst, neg, rel)
         s, d, n, r = self.generate_embedding(src, dst, neg, rel)
         loss, metric = self.calculate_energy(s, d, n, r)
         return [s.reshape(-1, s.shape[-1]), r.reshape(-1, r.shape[-1]), d.reshape(-1, d.shape[-1])], loss, \
@@ -100,6 +120,10 @@ class TransE(TransX):
         if ent_dim != rel_dim:
             raise ValueError("Entity dim and Relation dim should be equal in TransE")
         self.margin = margin
+        # subclasses with projections (TransH / TransD) override generate_embedding and
+        # keep the unfused path
+        if type(self).generate_embedding is TransE.generate_embedding:
+            self.fused_kind = "l1" if l1 else "l2"
 
     def generate_embedding(self, src, dst, neg, rel):
         e = self.entity_encoder
@@ -168,6 +192,7 @@ class DistMult(TransX):
         super().__init__(node_type, edge_type, node_max_id, edge_max_id, ent_dim, rel_dim, num_negs, True,
                          metric_name, corrupt, sharded)
         self.margin, self.l2_regular, self.regular_param = margin, l2_regular, regular_param
+        self.fused_kind = "distmult"
 
     def calculate_scores(self, src, rel, dst):
         return (src * rel * dst).sum(-1)

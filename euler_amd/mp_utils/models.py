@@ -18,7 +18,7 @@ import euler_amd.ops.graph_api as ge
 from euler_amd.convolution import convs as C
 from euler_amd.dataflow import dataflows as D
 from euler_amd.graph_pool.pools import Pooling
-from euler_amd.ops import mp_ops
+from euler_amd.ops import gnn_ops, mp_ops
 from euler_amd.utils import metrics as M
 from euler_amd.utils.layers import Dense
 
@@ -282,12 +282,11 @@ class UnsuperviseModel(nn.Module):
         emb = self.embed(src)
         emb_pos = self.embed_context(pos)
         emb_neg = self.embed_context(negs)
-        logits = torch.matmul(emb, emb_pos.transpose(1, 2)).float()
-        neg_logits = torch.matmul(emb, emb_neg.transpose(1, 2)).float()
-        metric = self.metric(logits.detach().cpu(), neg_logits.detach().cpu())
-        true_x = F.binary_cross_entropy_with_logits(logits, torch.ones_like(logits), reduction="none")
-        neg_x = F.binary_cross_entropy_with_logits(neg_logits, torch.zeros_like(neg_logits), reduction="none")
-        loss = torch.cat([true_x.reshape(-1), neg_x.reshape(-1)]).mean()
+        # one fused kernel for the dot products, both sigmoid-CEs and the mean (embed.hip K11)
+        b = emb.shape[0]
+        loss, logits, neg_logits = gnn_ops.sgns_loss(emb.reshape(b, -1), emb_pos, emb_neg)
+        logits, neg_logits = logits.float().view(b, 1, -1), neg_logits.float().view(b, 1, -1)
+        metric = self.metric(logits.cpu(), neg_logits.cpu())
         embedding = self.embed(torch.as_tensor(inputs).reshape(-1))
         return embedding, loss, self.metric_name, metric
 

@@ -1,0 +1,390 @@
+"""Fused GNN / embedding ops on the gfx950 kernels.
+
+=====================  ==========================================  =================================
+op                     replaces (reference)                        kernel
+=====================  ==========================================  =================================
+``gat_aggregate``      GATConv logits + scatter_softmax + gather   ``gat.hip`` (online softmax, one
+                       + scatter_add (gat_conv.py:41-78,            pass per destination; backward:
+                       mp_ops.py:76-79), one conv per head          destination + source passes)
+``relation_transform`` RelationConv per-edge [dim, fea] matmul      ``rgcn.hip`` (relation-grouped
+                       (relation_conv.py:63-70)                     MFMA GEMM, gather in prologue)
+``sgns_loss``          matmul + 2x sigmoid-CE + concat + mean       ``embed.hip`` sgns_fwd / sgns_bwd
+                       (mp_utils/base.py:80-91)
+``kg_score``           4 lookups + 4 l2-normalise + TransE/         ``embed.hip`` kg_fwd / kg_bwd
+                       DistMult score (transX.py:72-145)
+``unique_first``       tf.unique (first-occurrence order)           ``unique.hip`` (hash table)
+=====================  ==========================================  =================================
+
+GPU tensors always take the kernel path (``use_hip``); CPU tensors take a plain torch
+composition of the same math, which is also the numerics oracle in the tests.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from euler_amd.ops._native import hip, use_hip
+from euler_amd.ops.mp_ops import SegmentIndex
+
+__all__ = ["EdgeCSR", "gat_aggregate", "gat_aggregate_reference", "RelationTiles", "relation_transform",
+           "relation_transform_reference", "sgns_loss", "sgns_loss_reference", "kg_score", "kg_score_reference",
+           "unique_first", "KG_KINDS", "KG_CORRUPT"]
+
+
+# ----------------------------------------------------------------------------- edge structures
+class EdgeCSR:
+    """Destination CSR + source CSC of an ``edge_index`` ([2, E]: row 0 = destination,
+    row 1 = source), with int32 neighbour columns, built once and reused by forward and
+    backward.  Edges with a negative endpoint (padding) are dropped."""
+
+    def __init__(self, edge_index: torch.Tensor, size):
+        self.edge_index = edge_index
+        self.n_dst, self.n_src = int(size[0]), int(size[1])
+        self._csr = None
+        self._csc = None
+
+    @classmethod
+    def from_csr(cls, indptr: torch.Tensor, col: torch.Tensor, n_src: int) -> "EdgeCSR":
+        """From an existing destination CSR (e.g. a resident full graph): no sort for the
+        forward; the source CSC is built on first backward."""
+        n_dst = indptr.numel() - 1
+        dst = torch.repeat_interleave(torch.arange(n_dst, device=indptr.device, dtype=torch.int32),
+                                      torch.diff(indptr))
+        obj = cls(torch.stack([dst, col.to(torch.int32)]), (n_dst, n_src))
+        obj._csr = (indptr.to(torch.int64).contiguous(), col.to(torch.int32).contiguous())
+        return obj
+
+    def csr(self):
+        if self._csr is None:
+            dst, src = self.edge_index[0].long(), self.edge_index[1].long()
+            seg = SegmentIndex(dst, self.n_dst)
+            col = src[seg.perm].to(torch.int32)
+            self._csr = (seg.indptr, col.contiguous())
+        return self._csr
+
+    def csc(self):
+        if self._csc is None:
+            dst, src = self.edge_index[0].long(), self.edge_index[1].long()
+            seg = SegmentIndex(src, self.n_src)
+            row = dst[seg.perm].to(torch.int32)
+            self._csc = (seg.indptr, row.contiguous())
+        return self._csc
+
+
+def _cached(edge_index, key, build):
+    cache = getattr(edge_index, "_euler_cache", None)
+    if cache is None:
+        cache = {}
+        try:
+            edge_index._euler_cache = cache
+        except AttributeError:
+            return build()
+    if key not in cache:
+        cache[key] = build()
+    return cache[key]
+
+
+def edge_csr(edge_index, size) -> EdgeCSR:
+    return _cached(edge_index, "_euler_csr_%d_%d" % (int(size[0]), int(size[1])), lambda: EdgeCSR(edge_index, size))
+
+
+# ----------------------------------------------------------------------------- K5 GAT
+def gat_aggregate_reference(h, al, ar, edge_index, size, slope=0.2):
+    """Plain torch: per-head softmax over each destination's in-edges, weighted sum of
+    the source rows.  h [N_src, H, C], al [N_src, H], ar [N_dst, H] -> [N_dst, H, C]."""
+    dst, src = edge_index[0].long(), edge_index[1].long()
+    keep = (dst >= 0) & (src >= 0)
+    dst, src = dst[keep], src[keep]
+    S, H = int(size[0]), al.shape[1]
+    z = F.leaky_relu(al.float()[src] + ar.float()[dst], slope)  # [E, H]
+    mx = torch.full((S, H), float("-inf"), device=z.device).scatter_reduce(
+        0, dst.view(-1, 1).expand_as(z), z, reduce="amax", include_self=True)
+    p = torch.exp(z - mx[dst])
+    den = torch.zeros(S, H, device=z.device).index_add(0, dst, p)
+    p = p / den[dst]
+    msg = h.float()[src] * p.unsqueeze(-1)
+    return torch.zeros((S,) + tuple(h.shape[1:]), device=z.device).index_add(0, dst, msg)
+
+
+class _GatAggregate(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h2, al, ar, csr, H, C, slope):
+        indptr, col = csr.csr()
+        out, lse = hip().gat_fwd(indptr, col, h2, al, ar, H, C, slope)
+        ctx.csr, ctx.H, ctx.C, ctx.slope = csr, H, C, slope
+        ctx.save_for_backward(h2, al, ar, out, lse)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        h2, al, ar, out, lse = ctx.saved_tensors
+        indptr, col = ctx.csr.csr()
+        cindptr, crow = ctx.csr.csc()
+        dout = dout.to(h2.dtype).contiguous()
+        dh, dal, dar = hip().gat_bwd(indptr, col, cindptr, crow, h2, al, ar, ctx.H, ctx.C, ctx.slope, out, dout, lse)
+        return dh, dal, dar, None, None, None, None
+
+
+def gat_aggregate(h, al, ar, edge_index, size, slope=0.2, csr=None):
+    """Fused multi-head GAT aggregation.
+
+    h [N_src, H, C] (bf16 or fp32) projected source features, al [N_src, H] and
+    ar [N_dst, H] the per-node attention terms; returns [N_dst, H, C] with
+    ``out[i, h] = sum_j softmax_j(leaky_relu(al[j, h] + ar[i, h])) * h[j, h]``.
+    Differentiable in h, al and ar.  ``csr`` (an :class:`EdgeCSR`) may be passed
+    instead of ``edge_index`` for a resident graph.
+    """
+    N, H, C = h.shape
+    if csr is not None:
+        edge_index, size = csr.edge_index, (csr.n_dst, csr.n_src)
+    if use_hip(h, al, ar) and h.dtype in (torch.bfloat16, torch.float32) and \
+            hip().gat_supported(H, C, h.dtype == torch.bfloat16):
+        csr = csr if csr is not None else edge_csr(edge_index, size)
+        out = _GatAggregate.apply(h.reshape(N, H * C).contiguous(), al.float().contiguous(),
+                                  ar.float().contiguous(), csr, H, C, float(slope))
+        return out.view(-1, H, C)
+    return gat_aggregate_reference(h, al, ar, edge_index, size, slope).to(h.dtype)
+
+
+# ----------------------------------------------------------------------------- K6 relation transform
+_TILE = 64
+
+
+def _round_up(x, m):
+    return (x + m - 1) // m * m
+
+
+class RelationTiles:
+    """Edges grouped by relation and cut into tiles of <= 64 edges of one relation.
+
+    Arrays are over the relation-sorted edge order: ``src``/``dst`` (int32), ``scale``
+    (1 / in-degree of the destination for mean aggregation, else 1), tiles
+    ``(rel, start, len)`` (int32).  Built once per (edge_index, relation ids)."""
+
+    def __init__(self, edge_index, rel, size, num_rel, aggr="mean"):
+        dst, src = edge_index[0].long(), edge_index[1].long()
+        rel = rel.reshape(-1).long()
+        valid = (dst >= 0) & (src >= 0) & (rel >= 0) & (rel < num_rel)
+        idx = valid.nonzero(as_tuple=True)[0]
+        order = idx[torch.argsort(rel[idx], stable=True)]
+        r_sorted = rel[order]
+        dev = edge_index.device
+        self.src = src[order].to(torch.int32).contiguous()
+        self.dst = dst[order].to(torch.int32).contiguous()
+        n_dst = int(size[0])
+        if aggr == "mean":
+            deg = torch.bincount(dst[idx], minlength=n_dst)[:n_dst].clamp(min=1).float()
+            self.scale = (1.0 / deg)[self.dst.long()].contiguous()
+        else:
+            self.scale = torch.ones(order.numel(), device=dev)
+        counts = torch.bincount(r_sorted, minlength=num_rel)[:num_rel]
+        ntile = (counts + _TILE - 1) // _TILE
+        T = int(ntile.sum().item())
+        tile_rel = torch.repeat_interleave(torch.arange(num_rel, device=dev), ntile)
+        first_tile = torch.cumsum(ntile, 0) - ntile
+        k_in_rel = torch.arange(T, device=dev) - first_tile[tile_rel]
+        rel_start = torch.cumsum(counts, 0) - counts
+        self.tile_rel = tile_rel.to(torch.int32).contiguous()
+        self.tile_start = (rel_start[tile_rel] + _TILE * k_in_rel).to(torch.int32).contiguous()
+        self.tile_len = torch.clamp(counts[tile_rel] - _TILE * k_in_rel, max=_TILE).to(torch.int32).contiguous()
+        self.num_tiles = T
+
+    def tiles(self):
+        return self.tile_rel, self.tile_start, self.tile_len
+
+
+def relation_transform_reference(x, rel, weight, edge_index, size, aggr="mean"):
+    """out[i] = aggr_{e: dst(e) = i} weight[rel(e)] @ x[src(e)]  (weight [R, N, K])."""
+    dst, src = edge_index[0].long(), edge_index[1].long()
+    rel = rel.reshape(-1).long()
+    valid = (dst >= 0) & (src >= 0) & (rel >= 0) & (rel < weight.shape[0])
+    dst, src, rel = dst[valid], src[valid], rel[valid]
+    msg = torch.einsum("enk,ek->en", weight.float()[rel], x.float()[src])
+    S = int(size[0])
+    out = torch.zeros(S, weight.shape[1], device=x.device).index_add(0, dst, msg)
+    if aggr == "mean":
+        cnt = torch.bincount(dst, minlength=S)[:S].clamp(min=1).float()
+        out = out / cnt.unsqueeze(1)
+    return out
+
+
+class _RelationTransform(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, tiles, n_dst):
+        R, N, K = weight.shape
+        Kp, Np = _round_up(K, 32), _round_up(N, 32)
+        xb = F.pad(x.to(torch.bfloat16), (0, Kp - K)).contiguous()
+        wb = F.pad(weight.to(torch.bfloat16), (0, Kp - K, 0, Np - N)).contiguous()
+        out = torch.zeros(n_dst, Np, device=x.device, dtype=torch.float32)
+        tr, ts, tl = tiles.tiles()
+        hip().rel_gemm(xb, tiles.src, tr, ts, tl, wb, tiles.scale, tiles.dst, 1, out)
+        ctx.tiles, ctx.dims = tiles, (R, N, K, Kp, Np, x.shape[0])
+        ctx.x_dtype, ctx.w_dtype = x.dtype, weight.dtype
+        ctx.save_for_backward(xb, wb)
+        return out[:, :N].to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, dout):
+        xb, wb = ctx.saved_tensors
+        R, N, K, Kp, Np, n_src = ctx.dims
+        tiles = ctx.tiles
+        tr, ts, tl = tiles.tiles()
+        gb = F.pad(dout.to(torch.bfloat16), (0, Np - N)).contiguous()
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            wt = wb.transpose(1, 2).contiguous()  # [R, Kp, Np]
+            dxp = torch.zeros(n_src, Kp, device=dout.device, dtype=torch.float32)
+            hip().rel_gemm(gb, tiles.dst, tr, ts, tl, wt, tiles.scale, tiles.src, 1, dxp)
+            dx = dxp[:, :K].to(ctx.x_dtype)
+        if ctx.needs_input_grad[1]:
+            dwp = torch.zeros(R, Np, Kp, device=dout.device, dtype=torch.float32)
+            hip().rel_gemm_dw(gb, tiles.dst, xb, tiles.src, tiles.scale, tr, ts, tl, dwp)
+            dw = dwp[:, :N, :K].to(ctx.w_dtype)
+        return dx, dw, None, None
+
+
+def relation_transform(x, rel, weight, edge_index, size, aggr="mean", tiles=None):
+    """R-GCN message + aggregation: ``out[i] = aggr_e weight[rel_e] @ x[src_e]`` over the
+    in-edges of ``i`` (aggr ``mean`` or ``add``).  x [N_src, K], weight [R, N, K]."""
+    R, N, K = weight.shape
+    if use_hip(x, weight) and _round_up(K, 32) <= 1024 and _round_up(N, 32) <= 1024 and \
+            _round_up(N, 32) + _round_up(K, 32) <= 1120:
+        if tiles is None:
+            key = "_euler_reltiles_%d_%d_%s" % (int(size[0]), R, aggr)
+            tiles = _cached(edge_index, key, lambda: RelationTiles(edge_index, rel, size, R, aggr))
+        return _RelationTransform.apply(x, weight, tiles, int(size[0]))
+    return relation_transform_reference(x, rel, weight, edge_index, size, aggr).to(x.dtype)
+
+
+# ----------------------------------------------------------------------------- K11 skip-gram loss
+def sgns_loss_reference(emb, pos, neg):
+    emb = emb.reshape(emb.shape[0], -1).float()
+    lp = torch.einsum("bd,bpd->bp", emb, pos.float())
+    ln = torch.einsum("bd,bkd->bk", emb, neg.float())
+    lt = F.binary_cross_entropy_with_logits(lp, torch.ones_like(lp), reduction="none")
+    lf = F.binary_cross_entropy_with_logits(ln, torch.zeros_like(ln), reduction="none")
+    return torch.cat([lt.reshape(-1), lf.reshape(-1)]).mean(), lp, ln
+
+
+class _Sgns(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, emb, pos, neg):
+        logits, loss_rows = hip().sgns_fwd(emb, pos, neg)
+        count = emb.shape[0] * (pos.shape[1] + neg.shape[1])
+        ctx.save_for_backward(emb, pos, neg, logits)
+        ctx.count = count
+        ctx.mark_non_differentiable(logits)
+        return loss_rows.sum() / max(count, 1), logits
+
+    @staticmethod
+    def backward(ctx, g, _g_logits):
+        emb, pos, neg, logits = ctx.saved_tensors
+        demb, dpos, dneg = hip().sgns_bwd(emb, pos, neg, logits, 1.0 / max(ctx.count, 1))
+        g = g.to(demb.dtype)
+        return demb * g, dpos * g, dneg * g
+
+
+def sgns_loss(emb, pos, neg):
+    """Mean sigmoid cross-entropy of ``<emb, pos>`` (label 1) and ``<emb, neg>`` (label 0).
+
+    emb [B, D] or [B, 1, D]; pos [B, P, D]; neg [B, K, D].  Returns
+    ``(loss, pos_logits [B, P], neg_logits [B, K])`` (logits detached)."""
+    B = emb.shape[0]
+    e2 = emb.reshape(B, -1)
+    D = e2.shape[1]
+    V = 8 if e2.dtype == torch.bfloat16 else 4
+    if use_hip(e2, pos, neg) and e2.dtype in (torch.bfloat16, torch.float32) and pos.dtype == e2.dtype and \
+            neg.dtype == e2.dtype and D % V == 0 and D // V <= 64:
+        loss, logits = _Sgns.apply(e2.contiguous(), pos.contiguous(), neg.contiguous())
+        P = pos.shape[1]
+        return loss, logits[:, :P], logits[:, P:]
+    loss, lp, ln = sgns_loss_reference(e2, pos, neg)
+    return loss, lp.detach(), ln.detach()
+
+
+# ----------------------------------------------------------------------------- K10 KG scores
+KG_KINDS = {"l1": 0, "l2": 1, "distmult": 2}
+KG_CORRUPT = {"front": 0, "tail": 1, "both": 2}
+
+
+def kg_score_reference(ent, rel, src, dst, ridx, neg, kind="l1", corrupt="both", normalize=True):
+    def row(t, i):
+        x = t[i.long()]
+        return F.normalize(x, dim=-1) if normalize else x
+
+    h, t, r = row(ent, src.reshape(-1)), row(ent, dst.reshape(-1)), row(rel, ridx.reshape(-1))
+    n = row(ent, neg.reshape(src.numel(), -1))
+
+    def score(a, b, c):
+        if kind == "distmult":
+            return (a * b * c).sum(-1)
+        d = a + b - c
+        return -(d.abs().sum(-1) if kind == "l1" else d.norm(dim=-1))
+
+    pos = score(h, r, t)
+    r1, h1, t1 = r.unsqueeze(1), h.unsqueeze(1), t.unsqueeze(1)
+    if corrupt == "front":
+        ns = score(n, r1, t1)
+    elif corrupt == "tail":
+        ns = score(h1, r1, n)
+    else:
+        ns = torch.cat([score(n, r1, t1), score(h1, r1, n)], -1)
+    return pos, ns
+
+
+class _KgScore(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ent, rel, src, dst, ridx, neg, kind, corrupt, normalize):
+        pos_s, neg_s = hip().kg_fwd(ent, rel, src, dst, ridx, neg, kind, corrupt, normalize)
+        ctx.save_for_backward(ent, rel, src, dst, ridx, neg)
+        ctx.args = (kind, corrupt, normalize)
+        return pos_s, neg_s
+
+    @staticmethod
+    def backward(ctx, gpos, gneg):
+        ent, rel, src, dst, ridx, neg = ctx.saved_tensors
+        dent = torch.zeros_like(ent)
+        drel = torch.zeros_like(rel)
+        B = src.numel()
+        nneg = (2 if ctx.args[1] == 2 else 1) * (neg.numel() // max(B, 1))
+        gpos = torch.zeros(B, device=ent.device) if gpos is None else gpos.float().contiguous()
+        gneg = torch.zeros(B, nneg, device=ent.device) if gneg is None else gneg.float().contiguous()
+        hip().kg_bwd(ent, rel, src, dst, ridx, neg, *ctx.args, gpos, gneg, dent, drel)
+        return dent, drel, None, None, None, None, None, None, None
+
+
+def kg_score(ent, rel, src, dst, ridx, neg, kind="l1", corrupt="both", normalize=True):
+    """Scores of the positive triples ``(src, ridx, dst)`` [B] and of the corrupted ones
+    [B, K] (front or tail) or [B, 2K] (both: front scores first), with rows gathered from
+    the entity / relation tables and optionally l2-normalised.  ``kind``: ``l1`` /
+    ``l2`` (TransE, score = -|h + r - t|) or ``distmult`` (score = sum h r t).
+    Differentiable in both tables."""
+    B = src.numel()
+    D = ent.shape[1]
+    if use_hip(ent, rel) and ent.dtype == torch.float32 and rel.dtype == torch.float32 and D % 4 == 0 and D <= 256:
+        def ids(t, n_rows):
+            return t.reshape(-1).long().clamp(0, n_rows - 1).contiguous()
+
+        return _KgScore.apply(ent, rel, ids(src, ent.shape[0]), ids(dst, ent.shape[0]), ids(ridx, rel.shape[0]),
+                              ids(neg, ent.shape[0]).view(B, -1), KG_KINDS[kind], KG_CORRUPT[corrupt],
+                              bool(normalize))
+    return kg_score_reference(ent, rel, src, dst, ridx, neg, kind, corrupt, normalize)
+
+
+# ----------------------------------------------------------------------------- K8 unique
+def unique_first(x: torch.Tensor):
+    """``(unique values, inverse)`` of a 1-D id tensor in first-occurrence order — the
+    semantics of ``tf.unique`` (reference dataflows rely on the previous hop's nodes
+    keeping their leading positions).  GPU: hash-table kernel; CPU: sort-based."""
+    x = x.reshape(-1)
+    if use_hip(x):
+        return tuple(hip().unique_first(x.long().contiguous()))
+    u, inv = torch.unique(x, sorted=True, return_inverse=True)
+    if u.numel() == 0:
+        return u, inv
+    first = torch.full((u.numel(),), x.numel(), dtype=torch.long, device=x.device)
+    first = first.scatter_reduce(0, inv, torch.arange(x.numel(), device=x.device), reduce="amin")
+    order = torch.argsort(first)
+    rank = torch.empty_like(order)
+    rank[order] = torch.arange(order.numel(), device=x.device)
+    return u[order], rank[inv]

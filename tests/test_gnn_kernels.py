@@ -1,0 +1,185 @@
+"""Numerics of the fused GAT / R-GCN / skip-gram / KG-score / unique kernels against plain
+PyTorch fp32 references of the same ops (euler_amd/ops/gnn_ops.py)."""
+import pytest
+import torch
+
+from euler_amd.ops import gnn_ops as G
+
+
+def _graph(n_dst, n_src, E, device, seed=0, pad=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    dst = torch.randint(0, n_dst, (E,), generator=g)
+    src = torch.randint(0, n_src, (E,), generator=g)
+    if pad:
+        dst[:pad] = -1
+        src[pad:2 * pad] = -1
+    return torch.stack([dst, src]).to(device)
+
+
+# ----------------------------------------------------------------------------- CPU (reference semantics)
+def test_unique_first_cpu_order():
+    x = torch.tensor([5, 3, 5, 9, 3, 1, 9, 7])
+    u, inv = G.unique_first(x)
+    assert u.tolist() == [5, 3, 9, 1, 7]
+    assert torch.equal(u[inv], x)
+
+
+def test_gat_reference_matches_composed_convs():
+    from euler_amd.ops import mp_ops
+
+    torch.manual_seed(0)
+    ei = _graph(30, 50, 400, "cpu")
+    H, C = 4, 8
+    h = torch.randn(50, H, C)
+    al, ar = torch.randn(50, H), torch.randn(30, H)
+    out = G.gat_aggregate(h, al, ar, ei, (30, 50), 0.2)
+    logit = torch.nn.functional.leaky_relu(al[ei[1]] + ar[ei[0]], 0.2)
+    alpha = mp_ops.scatter_softmax(logit, ei[0], 30)
+    ref = mp_ops.scatter_add((h[ei[1]] * alpha.unsqueeze(-1)).reshape(-1, H * C), ei[0], 30).view(30, H, C)
+    torch.testing.assert_close(out, ref, atol=1e-5, rtol=1e-5)
+
+
+def test_relation_reference_matches_loop():
+    torch.manual_seed(1)
+    ei = _graph(20, 40, 300, "cpu")
+    rel = torch.randint(0, 5, (300,))
+    x, W = torch.randn(40, 12), torch.randn(5, 6, 12)
+    out = G.relation_transform(x, rel, W, ei, (20, 40), "mean")
+    ref = torch.zeros(20, 6)
+    cnt = torch.zeros(20)
+    for e in range(300):
+        ref[ei[0, e]] += W[rel[e]] @ x[ei[1, e]]
+        cnt[ei[0, e]] += 1
+    torch.testing.assert_close(out, ref / cnt.clamp(min=1).unsqueeze(1), atol=1e-4, rtol=1e-4)
+
+
+def test_kg_reference_shapes():
+    ent, rel = torch.randn(50, 16), torch.randn(7, 16)
+    src, dst, r = torch.randint(0, 50, (8,)), torch.randint(0, 50, (8,)), torch.randint(0, 7, (8,))
+    neg = torch.randint(0, 50, (8, 3))
+    p, n = G.kg_score(ent, rel, src, dst, r, neg, "l1", "both")
+    assert p.shape == (8,) and n.shape == (8, 6)
+    p, n = G.kg_score(ent, rel, src, dst, r, neg, "distmult", "tail")
+    assert n.shape == (8, 3)
+
+
+# ----------------------------------------------------------------------------- GPU kernels
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,C,dtype", [(8, 16, torch.bfloat16), (1, 32, torch.float32), (4, 64, torch.bfloat16),
+                                       (8, 8, torch.float32), (2, 256, torch.bfloat16)])
+def test_gat_fused_matches_reference(cuda, H, C, dtype):
+    torch.manual_seed(2)
+    n_dst, n_src, E = 700, 1500, 9000
+    ei = _graph(n_dst, n_src, E, cuda, seed=3, pad=20)
+    h = torch.randn(n_src, H, C, device=cuda).to(dtype).requires_grad_(True)
+    al = torch.randn(n_src, H, device=cuda).requires_grad_(True)
+    ar = torch.randn(n_dst, H, device=cuda).requires_grad_(True)
+    out = G.gat_aggregate(h, al, ar, ei, (n_dst, n_src), 0.2)
+    g = torch.randn(out.shape, device=cuda)
+    (out.float() * g).sum().backward()
+    h2 = h.detach().float().requires_grad_(True)
+    al2, ar2 = al.detach().clone().requires_grad_(True), ar.detach().clone().requires_grad_(True)
+    ref = G.gat_aggregate_reference(h2, al2, ar2, ei, (n_dst, n_src), 0.2)
+    (ref * g).sum().backward()
+    tol = dict(atol=3e-2, rtol=3e-2) if dtype == torch.bfloat16 else dict(atol=2e-4, rtol=2e-4)
+    torch.testing.assert_close(out.float(), ref, **tol)
+    torch.testing.assert_close(h.grad.float(), h2.grad, **tol)
+    if dtype == torch.bfloat16:
+        # the upstream gradient is rounded to bf16 before the <dout, h_j> dot products:
+        # its error grows like sqrt(C)
+        tol = dict(atol=3e-2 * max(1.0, (C / 64) ** 0.5), rtol=3e-2)
+    torch.testing.assert_close(al.grad, al2.grad, **tol)
+    torch.testing.assert_close(ar.grad, ar2.grad, **tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K,N,aggr", [(100, 100, "mean"), (128, 64, "add"), (32, 200, "mean")])
+def test_relation_transform_matches_reference(cuda, K, N, aggr):
+    torch.manual_seed(4)
+    n_dst, n_src, E, R = 400, 900, 7000, 13
+    ei = _graph(n_dst, n_src, E, cuda, seed=5, pad=10)
+    rel = torch.randint(0, R, (E,), device=cuda)
+    x = (torch.randn(n_src, K, device=cuda) * 0.5).requires_grad_(True)
+    W = (torch.randn(R, N, K, device=cuda) * 0.1).requires_grad_(True)
+    out = G.relation_transform(x, rel, W, ei, (n_dst, n_src), aggr)
+    g = torch.randn(out.shape, device=cuda)
+    (out * g).sum().backward()
+    x2 = x.detach().to(torch.bfloat16).float().requires_grad_(True)
+    W2 = W.detach().to(torch.bfloat16).float().requires_grad_(True)
+    ref = G.relation_transform_reference(x2, rel, W2, ei, (n_dst, n_src), aggr)
+    (ref * g).sum().backward()
+    torch.testing.assert_close(out, ref, atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(x.grad, x2.grad, atol=3e-2, rtol=3e-2)
+    # dW sums ~E/R bf16-rounded products: bound the error relative to its magnitude
+    torch.testing.assert_close(W.grad, W2.grad, atol=1e-2 * float(W2.grad.abs().max()), rtol=3e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D,dtype", [(128, torch.bfloat16), (32, torch.float32), (100, torch.float32)])
+def test_sgns_matches_reference(cuda, D, dtype):
+    torch.manual_seed(6)
+    B, P, K = 333, 2, 5
+    emb = (torch.randn(B, D, device=cuda) * 0.3).to(dtype).requires_grad_(True)
+    pos = (torch.randn(B, P, D, device=cuda) * 0.3).to(dtype).requires_grad_(True)
+    neg = (torch.randn(B, K, D, device=cuda) * 0.3).to(dtype).requires_grad_(True)
+    loss, lp, ln = G.sgns_loss(emb, pos, neg)
+    (loss * 3.0).backward()
+    e2, p2, n2 = (t.detach().float().requires_grad_(True) for t in (emb, pos, neg))
+    ref, rlp, rln = G.sgns_loss_reference(e2, p2, n2)
+    (ref * 3.0).backward()
+    tol = dict(atol=2e-2, rtol=2e-2) if dtype == torch.bfloat16 else dict(atol=1e-5, rtol=1e-4)
+    torch.testing.assert_close(loss, ref, **tol)
+    torch.testing.assert_close(lp, rlp.detach(), **tol)
+    torch.testing.assert_close(ln, rln.detach(), **tol)
+    for a, b in ((emb, e2), (pos, p2), (neg, n2)):
+        torch.testing.assert_close(a.grad.float(), b.grad, **tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,corrupt,normalize", [("l1", "both", True), ("l2", "front", True),
+                                                    ("distmult", "tail", True), ("l2", "both", False)])
+def test_kg_score_matches_reference(cuda, kind, corrupt, normalize):
+    torch.manual_seed(7)
+    Ne, Nr, D, B, K = 500, 20, 100, 128, 4
+    ent = torch.randn(Ne, D, device=cuda).requires_grad_(True)
+    rel = torch.randn(Nr, D, device=cuda).requires_grad_(True)
+    src, dst = torch.randint(0, Ne, (B,), device=cuda), torch.randint(0, Ne, (B,), device=cuda)
+    r = torch.randint(0, Nr, (B,), device=cuda)
+    neg = torch.randint(0, Ne, (B, K), device=cuda)
+    ps, ns = G.kg_score(ent, rel, src, dst, r, neg, kind, corrupt, normalize)
+    gp, gn = torch.randn_like(ps), torch.randn_like(ns)
+    ((ps * gp).sum() + (ns * gn).sum()).backward()
+    ent2, rel2 = ent.detach().clone().requires_grad_(True), rel.detach().clone().requires_grad_(True)
+    rp, rn = G.kg_score_reference(ent2, rel2, src, dst, r, neg, kind, corrupt, normalize)
+    ((rp * gp).sum() + (rn * gn).sum()).backward()
+    torch.testing.assert_close(ps, rp, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(ns, rn, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(ent.grad, ent2.grad, atol=1e-4, rtol=1e-3)
+    torch.testing.assert_close(rel.grad, rel2.grad, atol=1e-4, rtol=1e-3)
+
+
+@pytest.mark.gpu
+def test_unique_first_gpu_matches_cpu(cuda):
+    torch.manual_seed(8)
+    x = torch.randint(0, 5000, (20000,))
+    u_c, inv_c = G.unique_first(x)
+    u_g, inv_g = G.unique_first(x.to(cuda))
+    assert torch.equal(u_g.cpu(), u_c)
+    assert torch.equal(inv_g.cpu(), inv_c)
+    e_u, _ = G.unique_first(torch.empty(0, dtype=torch.long, device=cuda))
+    assert e_u.numel() == 0
+
+
+@pytest.mark.gpu
+def test_gat_conv_uses_fused_kernel(cuda):
+    from euler_amd.convolution import MultiHeadGATConv
+
+    torch.manual_seed(9)
+    conv = MultiHeadGATConv(64, heads=8).to(cuda)
+    x = torch.randn(300, 32, device=cuda)
+    ei = _graph(100, 300, 2000, cuda, seed=10)
+    out = conv([x[:100], x], ei, (100, 300))
+    out.sum().backward()
+    assert out.shape == (100, 64)
+    cache = ei._euler_cache
+    assert any(k.startswith("_euler_csr") for k in cache), "fused GAT path not taken"
