@@ -53,21 +53,30 @@ void gat_common(const torch::Tensor& indptr, const torch::Tensor& col, const tor
               " is not supported by the fused kernel");
 }
 
-std::vector<torch::Tensor> gat_fwd(torch::Tensor indptr, torch::Tensor col, torch::Tensor h, torch::Tensor al,
-                                   torch::Tensor ar, int64_t H, int64_t C, double slope) {
+const int32_t* order_ptr(const c10::optional<torch::Tensor>& order, int64_t rows, const char* name) {
+  if (!order.has_value()) return nullptr;
+  typed(*order, torch::kInt32, name);
+  TORCH_CHECK(order->numel() == rows, name, " must be a permutation of the ", rows, " rows");
+  return order->data_ptr<int32_t>();
+}
+
+std::vector<torch::Tensor> gat_fwd(torch::Tensor indptr, torch::Tensor col, c10::optional<torch::Tensor> order,
+                                   torch::Tensor h, torch::Tensor al, torch::Tensor ar, int64_t H, int64_t C,
+                                   double slope) {
   gat_common(indptr, col, h, al, ar, H, C);
   const c10::DeviceGuard g(h.device());
   const int64_t S = indptr.numel() - 1;
   auto out = torch::empty({S, H * C}, h.options());
   auto lse = torch::empty({S, H}, al.options());
-  ok(eh_gat_fwd(indptr.data_ptr<int64_t>(), col.data_ptr<int32_t>(), S, h.data_ptr(),
+  ok(eh_gat_fwd(indptr.data_ptr<int64_t>(), col.data_ptr<int32_t>(), order_ptr(order, S, "order"), S, h.data_ptr(),
                 h.scalar_type() == torch::kBFloat16, al.data_ptr<float>(), ar.data_ptr<float>(), static_cast<int>(H),
                 static_cast<int>(C), static_cast<float>(slope), out.data_ptr(), lse.data_ptr<float>(), stream()),
      "gat_fwd");
   return {out, lse};
 }
 
-std::vector<torch::Tensor> gat_bwd(torch::Tensor indptr, torch::Tensor col, torch::Tensor cindptr, torch::Tensor crow,
+std::vector<torch::Tensor> gat_bwd(torch::Tensor indptr, torch::Tensor col, c10::optional<torch::Tensor> order,
+                                   torch::Tensor cindptr, torch::Tensor crow, c10::optional<torch::Tensor> corder,
                                    torch::Tensor h, torch::Tensor al, torch::Tensor ar, int64_t H, int64_t C,
                                    double slope, torch::Tensor out, torch::Tensor dout, torch::Tensor lse) {
   gat_common(indptr, col, h, al, ar, H, C);
@@ -85,14 +94,60 @@ std::vector<torch::Tensor> gat_bwd(torch::Tensor indptr, torch::Tensor col, torc
   auto dh = torch::empty_like(h);
   auto dal = torch::empty_like(al);
   auto dar = torch::empty_like(ar);
-  auto dv = torch::empty({S, H}, al.options());
-  ok(eh_gat_bwd(indptr.data_ptr<int64_t>(), col.data_ptr<int32_t>(), S, cindptr.data_ptr<int64_t>(),
-                crow.data_ptr<int32_t>(), N, h.data_ptr(), h.scalar_type() == torch::kBFloat16, al.data_ptr<float>(),
-                ar.data_ptr<float>(), static_cast<int>(H), static_cast<int>(C), static_cast<float>(slope),
-                out.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(), dv.data_ptr<float>(), dh.data_ptr(),
-                dal.data_ptr<float>(), dar.data_ptr<float>(), stream()),
+  auto stat = torch::empty({S, H, 4}, al.options());
+  ok(eh_gat_bwd(indptr.data_ptr<int64_t>(), col.data_ptr<int32_t>(), order_ptr(order, S, "order"), S,
+                cindptr.data_ptr<int64_t>(), crow.data_ptr<int32_t>(), order_ptr(corder, N, "corder"), N,
+                h.data_ptr(), h.scalar_type() == torch::kBFloat16, al.data_ptr<float>(), ar.data_ptr<float>(),
+                static_cast<int>(H), static_cast<int>(C), static_cast<float>(slope), out.data_ptr(), dout.data_ptr(),
+                lse.data_ptr<float>(), stat.data_ptr<float>(), dh.data_ptr(), dal.data_ptr<float>(),
+                dar.data_ptr<float>(), stream()),
      "gat_bwd");
   return {dh, dal, dar};
+}
+
+void att_check(const torch::Tensor& z, const torch::Tensor& a_src, const torch::Tensor& a_dst, int64_t H,
+               int64_t C) {
+  bf16_or_f32(z, "z");
+  typed(a_src, torch::kFloat32, "a_src");
+  typed(a_dst, torch::kFloat32, "a_dst");
+  TORCH_CHECK(z.dim() == 2 && z.size(1) == H * C, "z must be [N, H*C]");
+  TORCH_CHECK(a_src.numel() == H * C && a_dst.numel() == H * C, "attention vectors must be [H, C]");
+  TORCH_CHECK(gat_supported(H, C, z.scalar_type() == torch::kBFloat16), "unsupported GAT shape");
+}
+
+std::vector<torch::Tensor> gat_att_fwd(torch::Tensor z, torch::Tensor a_src, torch::Tensor a_dst, int64_t H,
+                                       int64_t C) {
+  att_check(z, a_src, a_dst, H, C);
+  const c10::DeviceGuard g(z.device());
+  auto fopt = z.options().dtype(torch::kFloat32);
+  auto al = torch::empty({z.size(0), H}, fopt);
+  auto ar = torch::empty({z.size(0), H}, fopt);
+  ok(eh_gat_att_fwd(z.data_ptr(), z.scalar_type() == torch::kBFloat16, z.size(0), static_cast<int>(H),
+                    static_cast<int>(C), a_src.data_ptr<float>(), a_dst.data_ptr<float>(), al.data_ptr<float>(),
+                    ar.data_ptr<float>(), stream()),
+     "gat_att_fwd");
+  return {al, ar};
+}
+
+// dz is updated in place; returns (da_src, da_dst)
+std::vector<torch::Tensor> gat_att_bwd_(torch::Tensor z, torch::Tensor a_src, torch::Tensor a_dst, int64_t H,
+                                        int64_t C, torch::Tensor dal, torch::Tensor dar, torch::Tensor dz) {
+  att_check(z, a_src, a_dst, H, C);
+  typed(dal, torch::kFloat32, "dal");
+  typed(dar, torch::kFloat32, "dar");
+  typed(dz, z.scalar_type(), "dz");
+  TORCH_CHECK(dz.sizes() == z.sizes() && dal.numel() == z.size(0) * H && dar.numel() == z.size(0) * H,
+              "gat_att_bwd shape mismatch");
+  const c10::DeviceGuard g(z.device());
+  const bool bf = z.scalar_type() == torch::kBFloat16;
+  const int64_t nb = eh_gat_att_bwd_blocks(z.size(0), static_cast<int>(H), static_cast<int>(C), bf);
+  auto ps = torch::zeros({nb, H, C}, a_src.options());
+  auto pd = torch::zeros({nb, H, C}, a_dst.options());
+  ok(eh_gat_att_bwd(z.data_ptr(), bf, z.size(0), static_cast<int>(H), static_cast<int>(C), a_src.data_ptr<float>(),
+                    a_dst.data_ptr<float>(), dal.data_ptr<float>(), dar.data_ptr<float>(), dz.data_ptr(),
+                    ps.data_ptr<float>(), pd.data_ptr<float>(), stream()),
+     "gat_att_bwd");
+  return {ps.sum(0), pd.sum(0)};
 }
 
 // ----------------------------------------------------------------------------- R-GCN
@@ -288,6 +343,8 @@ void register_gnn_ops(pybind11::module& m) {
   m.def("gat_supported", &gat_supported);
   m.def("gat_fwd", &gat_fwd);
   m.def("gat_bwd", &gat_bwd);
+  m.def("gat_att_fwd", &gat_att_fwd);
+  m.def("gat_att_bwd_", &gat_att_bwd_);
   m.def("rel_gemm", &rel_gemm);
   m.def("rel_gemm_dw", &rel_gemm_dw);
   m.def("sgns_fwd", &sgns_fwd);

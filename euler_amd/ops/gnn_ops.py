@@ -20,6 +20,8 @@ composition of the same math, which is also the numerics oracle in the tests.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -70,6 +72,24 @@ class EdgeCSR:
             self._csc = (seg.indptr, row.contiguous())
         return self._csc
 
+    @staticmethod
+    def _by_degree(indptr):
+        # longest rows first: the rows sharing a wave have similar lengths and the
+        # heaviest work starts first (cdna_hip_programming.md App. B, skewed gathers)
+        if os.environ.get("EULER_AMD_GAT_ORDER", "1") == "0":
+            return None
+        return torch.argsort(torch.diff(indptr), descending=True).to(torch.int32).contiguous()
+
+    def csr_order(self):
+        if getattr(self, "_csr_order", None) is None:
+            self._csr_order = self._by_degree(self.csr()[0])
+        return self._csr_order
+
+    def csc_order(self):
+        if getattr(self, "_csc_order", None) is None:
+            self._csc_order = self._by_degree(self.csc()[0])
+        return self._csc_order
+
 
 def _cached(edge_index, key, build):
     cache = getattr(edge_index, "_euler_cache", None)
@@ -110,7 +130,7 @@ class _GatAggregate(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h2, al, ar, csr, H, C, slope):
         indptr, col = csr.csr()
-        out, lse = hip().gat_fwd(indptr, col, h2, al, ar, H, C, slope)
+        out, lse = hip().gat_fwd(indptr, col, csr.csr_order(), h2, al, ar, H, C, slope)
         ctx.csr, ctx.H, ctx.C, ctx.slope = csr, H, C, slope
         ctx.save_for_backward(h2, al, ar, out, lse)
         return out
@@ -121,7 +141,8 @@ class _GatAggregate(torch.autograd.Function):
         indptr, col = ctx.csr.csr()
         cindptr, crow = ctx.csr.csc()
         dout = dout.to(h2.dtype).contiguous()
-        dh, dal, dar = hip().gat_bwd(indptr, col, cindptr, crow, h2, al, ar, ctx.H, ctx.C, ctx.slope, out, dout, lse)
+        dh, dal, dar = hip().gat_bwd(indptr, col, ctx.csr.csr_order(), cindptr, crow, ctx.csr.csc_order(), h2, al,
+                                     ar, ctx.H, ctx.C, ctx.slope, out, dout, lse)
         return dh, dal, dar, None, None, None, None
 
 
@@ -144,6 +165,82 @@ def gat_aggregate(h, al, ar, edge_index, size, slope=0.2, csr=None):
                                   ar.float().contiguous(), csr, H, C, float(slope))
         return out.view(-1, H, C)
     return gat_aggregate_reference(h, al, ar, edge_index, size, slope).to(h.dtype)
+
+
+def gat_conv_reference(z, a_src, a_dst, edge_index, size, slope=0.2):
+    al = (z.float() * a_src.float()).sum(-1)
+    ar = (z.float() * a_dst.float()).sum(-1)
+    return gat_aggregate_reference(z, al, ar, edge_index, size, slope)
+
+
+class _GatConv(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z2, a_src, a_dst, csr, H, C, slope):
+        al, ar = hip().gat_att_fwd(z2, a_src, a_dst, H, C)
+        indptr, col = csr.csr()
+        out, lse = hip().gat_fwd(indptr, col, csr.csr_order(), z2, al, ar, H, C, slope)
+        ctx.csr, ctx.H, ctx.C, ctx.slope = csr, H, C, slope
+        ctx.save_for_backward(z2, a_src, a_dst, al, ar, out, lse)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        z2, a_src, a_dst, al, ar, out, lse = ctx.saved_tensors
+        csr = ctx.csr
+        indptr, col = csr.csr()
+        cindptr, crow = csr.csc()
+        dout = dout.to(z2.dtype).contiguous()
+        dz, dal, dar = hip().gat_bwd(indptr, col, csr.csr_order(), cindptr, crow, csr.csc_order(), z2, al, ar,
+                                     ctx.H, ctx.C, ctx.slope, out, dout, lse)
+        # dz += dal (x) a_src + dar (x) a_dst in place; attention-vector grads in the same pass
+        da_src, da_dst = hip().gat_att_bwd_(z2, a_src, a_dst, ctx.H, ctx.C, dal, dar, dz)
+        return dz, da_src, da_dst, None, None, None, None
+
+
+def gat_conv(z, a_src, a_dst, csr: EdgeCSR, slope=0.2):
+    """Whole GAT convolution over ONE node set (full-graph training: sources and
+    destinations are the same N nodes): attention terms, per-head edge softmax and the
+    weighted aggregation, forward and backward, in 2 + 3 kernels.  z [N, H, C] projected
+    features, a_src / a_dst [H, C] attention vectors; returns [N, H, C]."""
+    N, H, C = z.shape
+    assert csr.n_dst == csr.n_src == N, "gat_conv needs one node set (use gat_aggregate for blocks)"
+    if use_hip(z, a_src, a_dst) and z.dtype in (torch.bfloat16, torch.float32) and \
+            hip().gat_supported(H, C, z.dtype == torch.bfloat16):
+        out = _GatConv.apply(z.reshape(N, H * C).contiguous(), a_src.float().contiguous(),
+                             a_dst.float().contiguous(), csr, H, C, float(slope))
+        return out.view(N, H, C)
+    return gat_conv_reference(z, a_src, a_dst, csr.edge_index, (N, N), slope).to(z.dtype)
+
+
+class _TallLinear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, chunk):
+        ctx.save_for_backward(x, w)
+        ctx.chunk = chunk
+        return x @ w.t().to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = dy.to(x.dtype)
+        dx = dy @ w.to(x.dtype)
+        n = x.shape[0]
+        p = max(1, n // ctx.chunk)
+        n0 = (n // p) * p
+        # dW = dy^T x split over row chunks: P batched GEMMs fill the chip where a single
+        # [M x N] x [N x K] reduction GEMM over millions of rows runs on a few workgroups
+        dw = torch.bmm(dy[:n0].view(p, n0 // p, -1).transpose(1, 2), x[:n0].view(p, n0 // p, -1)).float().sum(0)
+        if n0 < n:
+            dw += (dy[n0:].t() @ x[n0:]).float()
+        return dx, dw.to(w.dtype), None
+
+
+def tall_linear(x, weight, chunk=8192):
+    """``x @ weight^T`` for x with millions of rows (full-graph layers): the weight
+    gradient is computed as a split-K batched GEMM instead of one skinny reduction."""
+    if x.is_cuda and x.dim() == 2 and x.shape[0] >= 4 * chunk:
+        return _TallLinear.apply(x, weight, chunk)
+    return x @ weight.t().to(x.dtype)
 
 
 # ----------------------------------------------------------------------------- K6 relation transform

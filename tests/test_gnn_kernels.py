@@ -93,6 +93,45 @@ def test_gat_fused_matches_reference(cuda, H, C, dtype):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("H,C,dtype", [(8, 16, torch.bfloat16), (4, 8, torch.float32)])
+def test_gat_conv_full_graph(cuda, H, C, dtype):
+    torch.manual_seed(12)
+    N, E = 2000, 30000
+    ei = _graph(N, N, E, cuda, seed=13)
+    csr = G.EdgeCSR(ei, (N, N))
+    z = torch.randn(N, H, C, device=cuda).to(dtype).requires_grad_(True)
+    a_s = (torch.randn(H, C, device=cuda) * 0.3).requires_grad_(True)
+    a_d = (torch.randn(H, C, device=cuda) * 0.3).requires_grad_(True)
+    out = G.gat_conv(z, a_s, a_d, csr, 0.2)
+    g = torch.randn(out.shape, device=cuda)
+    (out.float() * g).sum().backward()
+    z2 = z.detach().float().requires_grad_(True)
+    as2, ad2 = a_s.detach().clone().requires_grad_(True), a_d.detach().clone().requires_grad_(True)
+    ref = G.gat_conv_reference(z2, as2, ad2, ei, (N, N), 0.2)
+    (ref * g).sum().backward()
+    tol = dict(atol=4e-2, rtol=4e-2) if dtype == torch.bfloat16 else dict(atol=3e-4, rtol=3e-4)
+    torch.testing.assert_close(out.float(), ref, **tol)
+    torch.testing.assert_close(z.grad.float(), z2.grad, **tol)
+    scale = float(as2.grad.abs().max())
+    torch.testing.assert_close(a_s.grad, as2.grad, atol=2e-2 * scale, rtol=3e-2)
+    torch.testing.assert_close(a_d.grad, ad2.grad, atol=2e-2 * float(ad2.grad.abs().max()), rtol=3e-2)
+
+
+@pytest.mark.gpu
+def test_tall_linear_grads(cuda):
+    torch.manual_seed(14)
+    x = torch.randn(70000, 96, device=cuda).requires_grad_(True)
+    w = torch.randn(64, 96, device=cuda).requires_grad_(True)
+    y = G.tall_linear(x, w, chunk=4096)
+    g = torch.randn_like(y)
+    (y * g).sum().backward()
+    x2, w2 = x.detach().clone().requires_grad_(True), w.detach().clone().requires_grad_(True)
+    ((x2 @ w2.t()) * g).sum().backward()
+    torch.testing.assert_close(w.grad, w2.grad, atol=5e-2, rtol=1e-3)
+    torch.testing.assert_close(x.grad, x2.grad, atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("K,N,aggr", [(100, 100, "mean"), (128, 64, "add"), (32, 200, "mean")])
 def test_relation_transform_matches_reference(cuda, K, N, aggr):
     torch.manual_seed(4)
