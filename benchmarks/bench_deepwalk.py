@@ -1,0 +1,125 @@
+#!/usr/bin/env python3
+"""BASELINE config 4: DeepWalk 128-d embeddings on a 100M-node graph, data parallel over
+N GPUs with the embedding tables row-sharded across the ranks (RCCL all-to-all over
+xGMI for ids, rows and row gradients).
+
+Per rank and step: ``--batch`` random walks (walk_len 3, p = q = 1) on the GPU-resident
+graph, skip-gram pairs with window 1/1 (6 per walk), 5 negatives per pair, fused
+sigmoid-CE forward/backward, row-sparse Adam on the owners' shards (reference
+examples/deepwalk: walk_len 3, window 1/1, 5 negatives, Adam; embedding_dim 128 per
+BASELINE config 4).  Nothing is skipped inside the timed region.
+
+Usage:  python benchmarks/bench_deepwalk.py [--steps K] [--warmup W]
+        torchrun --nproc-per-node N benchmarks/bench_deepwalk.py   (one rank per GPU)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def main(argv=None):
+    p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--num-nodes", type=int, default=100_000_000)
+    p.add_argument("--avg-degree", type=float, default=10.0)
+    p.add_argument("--max-degree", type=int, default=1024)
+    p.add_argument("--dim", type=int, default=128)
+    p.add_argument("--batch", type=int, default=16384, help="walks per GPU per step")
+    p.add_argument("--walk-len", type=int, default=3)
+    p.add_argument("--num-negs", type=int, default=5)
+    p.add_argument("--optimizer", choices=["auto", "adam", "adagrad", "sgd"], default="auto")
+    p.add_argument("--lr", type=float, default=0.01)
+    p.add_argument("--seed", type=int, default=1234)
+    args = p.parse_args(argv)
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if not torch.cuda.is_available():
+        raise SystemExit("bench_deepwalk.py needs a GPU")
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    from euler_amd.graph.device_graph import DeviceGraph
+    from euler_amd.models.deepwalk_step import DeepWalkTrainer
+    from euler_amd.parallel.sparse_table import ShardedTable
+
+    if args.optimizer == "auto":
+        # Adam keeps 2 slots per row: two 100M x 128 fp32 tables + slots need 286 GiB, more
+        # than one GPU holds next to the graph; there (world 1) Adagrad's single slot fits
+        rows_per_rank = (args.num_nodes + 1 + world - 1) // world
+        need = 2 * rows_per_rank * ShardedTable.bytes_per_row(args.dim, "adam")
+        free = torch.cuda.mem_get_info(dev)[0]
+        args.optimizer = "adam" if need < 0.8 * free else "adagrad"
+    t0 = time.time()
+    g = DeviceGraph.synthetic(args.num_nodes, args.avg_degree, args.max_degree, seed=args.seed, device=dev)
+    g.manual_seed(args.seed * 7919 + rank)
+    tr = DeepWalkTrainer(g, args.num_nodes, args.dim, args.walk_len, 1, 1, args.num_negs, args.batch, args.lr,
+                         args.optimizer, seed=args.seed)
+    torch.cuda.synchronize()
+    if rank == 0:
+        gib = (tr.target.nbytes() + tr.context.nbytes()) / 2 ** 30
+        print(f"[bench_deepwalk] {args.num_nodes} nodes, {g.num_edges} edges, tables+slots {gib:.1f} GiB/rank, "
+              f"setup {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
+
+    for _ in range(args.warmup):
+        tr.step()
+    torch.cuda.synchronize()
+    first = float(tr.loss)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        tr.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t1
+    elt = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elt, op=dist.ReduceOp.MAX)
+    el = float(elt.item())
+    pairs = tr.pairs_per_step() * world * args.steps
+    if rank == 0:
+        print(json.dumps({
+            "metric": "train pairs/sec (whole node), DeepWalk 128-d skip-gram on 100M-node synthetic graph",
+            "value": round(pairs / el, 1),
+            "unit": "pairs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el * 1e3 / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (power-law random graph, random-init tables)",
+            "config": {"model": f"DeepWalk (walk_len 3, window 1/1, 5 negs, row-sparse {args.optimizer})",
+                       "num_nodes": args.num_nodes, "dim": args.dim, "walks_per_gpu": args.batch,
+                       "pairs_per_gpu_step": tr.pairs_per_step(), "parallelism": f"dp{world}+sharded-emb",
+                       "loss_first_last": [round(first, 4), round(float(tr.loss), 4)],
+                       "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1)},
+        }), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -168,6 +168,8 @@ void rel_gemm(torch::Tensor A, torch::Tensor a_idx, torch::Tensor trel, torch::T
   TORCH_CHECK(A.dim() == 2 && B.dim() == 3 && B.size(2) == A.size(1), "A [*, K], B [R, N, K]");
   const int64_t K = A.size(1), N = B.size(1);
   TORCH_CHECK(K % 32 == 0 && K <= 1024 && N % 16 == 0, "rel_gemm needs K % 32 == 0, K <= 1024, N % 16 == 0");
+  TORCH_CHECK(eh_rel_gemm_lds(static_cast<int>(K), static_cast<int>(N), static_cast<int>(mode)) <= 160 * 1024,
+              "rel_gemm: K + N too large for the LDS tiles");
   TORCH_CHECK(a_idx.numel() == o_idx.numel(), "a_idx / o_idx must cover the same edges");
   if (scale.has_value()) {
     typed(*scale, torch::kFloat32, "scale");
@@ -196,8 +198,7 @@ void rel_gemm_dw(torch::Tensor G, torch::Tensor g_idx, torch::Tensor X, torch::T
   TORCH_CHECK(G.dim() == 2 && X.dim() == 2 && dW.dim() == 3, "G [*, N], X [*, K], dW [R, N, K]");
   const int64_t N = G.size(1), K = X.size(1);
   TORCH_CHECK(dW.size(1) == N && dW.size(2) == K, "dW must be [R, N, K]");
-  TORCH_CHECK(N % 16 == 0 && K % 16 == 0, "rel_gemm_dw needs N, K multiples of 16");
-  TORCH_CHECK(eh_rel_gemm_dw_lds(static_cast<int>(N), static_cast<int>(K)) <= 160 * 1024, "N + K too large");
+  TORCH_CHECK(N % 64 == 0 && K % 64 == 0, "rel_gemm_dw needs N, K multiples of 64");
   TORCH_CHECK(g_idx.numel() == x_idx.numel(), "g_idx / x_idx must cover the same edges");
   if (scale.has_value()) {
     typed(*scale, torch::kFloat32, "scale");
@@ -347,6 +348,7 @@ void register_gnn_ops(pybind11::module& m) {
   m.def("gat_att_bwd_", &gat_att_bwd_);
   m.def("rel_gemm", &rel_gemm);
   m.def("rel_gemm_dw", &rel_gemm_dw);
+  m.attr("rel_gemm_dw_chunk") = eh_rel_gemm_dw_chunk();
   m.def("sgns_fwd", &sgns_fwd);
   m.def("sgns_bwd", &sgns_bwd);
   m.def("kg_fwd", &kg_fwd);

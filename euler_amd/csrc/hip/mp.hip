@@ -67,17 +67,29 @@ __global__ __launch_bounds__(256) void segment_reduce_kernel(const T* __restrict
   int64_t am[4] = {-1, -1, -1, -1};
 #pragma unroll
   for (int i = 0; i < 4; ++i) acc[i] = op == 2 ? -INFINITY : 0.f;
-  for (int64_t e = a; e < b; ++e) {
-    const int64_t row = perm ? perm[e] : e;
-    const T* p = src + row * D + d0;
+  // 4 source rows in flight per thread: the perm loads, then the row loads, are issued
+  // back to back instead of one dependent pair per edge
+  constexpr int U = 4;
+  for (int64_t e0 = a; e0 < b; e0 += U) {
+    int64_t row[U];
+    float v[U][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (i < nd) {
-        const float v = ld<T>(p + i);
-        if (op == 2) {
-          if (v > acc[i]) { acc[i] = v; am[i] = row; }
-        } else {
-          acc[i] += v;
+    for (int u = 0; u < U; ++u) row[u] = (e0 + u < b) ? (perm ? perm[e0 + u] : e0 + u) : -1;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[u][i] = (row[u] >= 0 && i < nd) ? ld<T>(src + row[u] * D + d0 + i) : 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (row[u] < 0) continue;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (i < nd) {
+          if (op == 2) {
+            if (v[u][i] > acc[i]) { acc[i] = v[u][i]; am[i] = row[u]; }
+          } else {
+            acc[i] += v[u][i];
+          }
         }
       }
     }

@@ -41,6 +41,50 @@ __global__ __launch_bounds__(256) void flat_optim_kernel(float* __restrict__ p, 
 
 __global__ void step_inc_kernel(int64_t* step) { step[0] += 1; }
 
+// float4 form of sparse_optim_kernel for D % 4 == 0: 16-byte loads/stores of the table,
+// slots and grads (a quarter of the threads, 4x the bytes in flight per thread)
+__global__ __launch_bounds__(256) void sparse_optim4_kernel(float* __restrict__ table, float* __restrict__ m,
+                                                            float* __restrict__ v, const int64_t* __restrict__ rows,
+                                                            const float* __restrict__ grads, int64_t n, int D,
+                                                            int64_t n_rows, const int64_t* __restrict__ step, float lr,
+                                                            float b1, float b2, float eps, int kind) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int D4 = D >> 2;
+  if (t >= n * D4) return;
+  const int64_t e = t / D4;
+  const int d = static_cast<int>(t - e * D4) * 4;
+  const int64_t r = rows[e];
+  if (r < 0 || r >= n_rows) return;
+  const int64_t o = r * D + d;
+  const float4_t gi = *reinterpret_cast<const float4_t*>(grads + e * D + d);
+  float4_t p = *reinterpret_cast<float4_t*>(table + o);
+  if (kind == 0) {
+    const float st = static_cast<float>(step[0]);
+    const float bc1 = 1.f - __powf(b1, st), bc2 = 1.f - __powf(b2, st);
+    float4_t mi = *reinterpret_cast<float4_t*>(m + o), vi = *reinterpret_cast<float4_t*>(v + o);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      mi[k] = b1 * mi[k] + (1.f - b1) * gi[k];
+      vi[k] = b2 * vi[k] + (1.f - b2) * gi[k] * gi[k];
+      p[k] -= lr * (mi[k] / bc1) / (sqrtf(vi[k] / bc2) + eps);
+    }
+    *reinterpret_cast<float4_t*>(m + o) = mi;
+    *reinterpret_cast<float4_t*>(v + o) = vi;
+  } else if (kind == 1) {
+    float4_t acc = *reinterpret_cast<float4_t*>(v + o);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      acc[k] += gi[k] * gi[k];
+      p[k] -= lr * gi[k] / (sqrtf(acc[k]) + eps);
+    }
+    *reinterpret_cast<float4_t*>(v + o) = acc;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) p[k] -= lr * gi[k];
+  }
+  *reinterpret_cast<float4_t*>(table + o) = p;
+}
+
 // rows: unique row ids (int64) into the table, grads [n, D] fp32
 __global__ __launch_bounds__(256) void sparse_optim_kernel(float* __restrict__ table, float* __restrict__ m,
                                                            float* __restrict__ v, const int64_t* __restrict__ rows,
@@ -92,6 +136,11 @@ hipError_t eh_sparse_optim(float* table, float* m, float* v, const int64_t* rows
                            hipStream_t s) {
   hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, s, step);
   if (n == 0 || D == 0) return hipGetLastError();
+  if (D % 4 == 0) {
+    hipLaunchKernelGGL(sparse_optim4_kernel, dim3(static_cast<uint32_t>(ceil_div(n * (D / 4), 256))), dim3(256), 0,
+                       s, table, m, v, rows, grads, n, D, n_rows, step, lr, b1, b2, eps, kind);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(sparse_optim_kernel, dim3(static_cast<uint32_t>(ceil_div(n * D, 256))), dim3(256), 0, s, table,
                      m, v, rows, grads, n, D, n_rows, step, lr, b1, b2, eps, kind);
   return hipGetLastError();

@@ -252,11 +252,15 @@ def _round_up(x, m):
 
 
 class RelationTiles:
-    """Edges grouped by relation and cut into tiles of <= 64 edges of one relation.
+    """Edges grouped by relation, for the relation-grouped MFMA GEMM (rgcn.hip).
 
-    Arrays are over the relation-sorted edge order: ``src``/``dst`` (int32), ``scale``
-    (1 / in-degree of the destination for mean aggregation, else 1), tiles
-    ``(rel, start, len)`` (int32).  Built once per (edge_index, relation ids)."""
+    Arrays are over the relation-sorted order of the valid edges: ``src``/``dst``
+    (int32), ``scale`` (1 / in-degree for mean aggregation, else 1), ``eid`` (arange:
+    the message row of each edge), tiles ``(rel, start, len)`` of <= 64 edges of one
+    relation for the message GEMMs, chunks ``(rel, start, len)`` of <= 1024 edges of one
+    relation for the weight gradient, and the destination / source CSRs over the
+    messages (``SegmentIndex``) for the deterministic per-node sums.  Built once per
+    (edge_index, relation ids)."""
 
     def __init__(self, edge_index, rel, size, num_rel, aggr="mean"):
         dst, src = edge_index[0].long(), edge_index[1].long()
@@ -266,28 +270,41 @@ class RelationTiles:
         order = idx[torch.argsort(rel[idx], stable=True)]
         r_sorted = rel[order]
         dev = edge_index.device
+        n_dst, n_src = int(size[0]), int(size[1])
+        self.aggr = aggr
+        self.num_edges = int(order.numel())
         self.src = src[order].to(torch.int32).contiguous()
         self.dst = dst[order].to(torch.int32).contiguous()
-        n_dst = int(size[0])
+        self.eid = torch.arange(self.num_edges, device=dev, dtype=torch.int32)
         if aggr == "mean":
             deg = torch.bincount(dst[idx], minlength=n_dst)[:n_dst].clamp(min=1).float()
             self.scale = (1.0 / deg)[self.dst.long()].contiguous()
         else:
             self.scale = torch.ones(order.numel(), device=dev)
         counts = torch.bincount(r_sorted, minlength=num_rel)[:num_rel]
-        ntile = (counts + _TILE - 1) // _TILE
-        T = int(ntile.sum().item())
-        tile_rel = torch.repeat_interleave(torch.arange(num_rel, device=dev), ntile)
-        first_tile = torch.cumsum(ntile, 0) - ntile
-        k_in_rel = torch.arange(T, device=dev) - first_tile[tile_rel]
-        rel_start = torch.cumsum(counts, 0) - counts
-        self.tile_rel = tile_rel.to(torch.int32).contiguous()
-        self.tile_start = (rel_start[tile_rel] + _TILE * k_in_rel).to(torch.int32).contiguous()
-        self.tile_len = torch.clamp(counts[tile_rel] - _TILE * k_in_rel, max=_TILE).to(torch.int32).contiguous()
-        self.num_tiles = T
+        self.tile_rel, self.tile_start, self.tile_len, self.num_tiles = self._cut(counts, _TILE, dev)
+        chunk = hip().rel_gemm_dw_chunk if dev.type == "cuda" else 1024
+        self.chunk_rel, self.chunk_start, self.chunk_len, self.num_chunks = self._cut(counts, chunk, dev)
+        self.dst_seg = SegmentIndex(self.dst.long(), n_dst)
+        self.src_seg = SegmentIndex(self.src.long(), n_src)
+
+    @staticmethod
+    def _cut(counts, size, dev):
+        R = counts.numel()
+        n = (counts + size - 1) // size
+        T = int(n.sum().item())
+        t_rel = torch.repeat_interleave(torch.arange(R, device=dev), n)
+        first = torch.cumsum(n, 0) - n
+        k = torch.arange(T, device=dev) - first[t_rel]
+        start = torch.cumsum(counts, 0) - counts
+        return (t_rel.to(torch.int32).contiguous(), (start[t_rel] + size * k).to(torch.int32).contiguous(),
+                torch.clamp(counts[t_rel] - size * k, max=size).to(torch.int32).contiguous(), T)
 
     def tiles(self):
         return self.tile_rel, self.tile_start, self.tile_len
+
+    def chunks(self):
+        return self.chunk_rel, self.chunk_start, self.chunk_len
 
 
 def relation_transform_reference(x, rel, weight, edge_index, size, aggr="mean"):
@@ -306,15 +323,22 @@ def relation_transform_reference(x, rel, weight, edge_index, size, aggr="mean"):
 
 
 class _RelationTransform(torch.autograd.Function):
+    """Messages W_rel x_src are stored once per edge (bf16, 16-byte rows) by the grouped
+    GEMM and summed per destination by the segment kernel: plain stores + one
+    deterministic read-back instead of fp32 atomics into the destination rows."""
+
     @staticmethod
     def forward(ctx, x, weight, tiles, n_dst):
         R, N, K = weight.shape
-        Kp, Np = _round_up(K, 32), _round_up(N, 32)
+        Kp, Np = _round_up(K, 64), _round_up(N, 64)
         xb = F.pad(x.to(torch.bfloat16), (0, Kp - K)).contiguous()
         wb = F.pad(weight.to(torch.bfloat16), (0, Kp - K, 0, Np - N)).contiguous()
-        out = torch.zeros(n_dst, Np, device=x.device, dtype=torch.float32)
+        msg = torch.empty(tiles.num_edges, Np, device=x.device, dtype=torch.bfloat16)
         tr, ts, tl = tiles.tiles()
-        hip().rel_gemm(xb, tiles.src, tr, ts, tl, wb, tiles.scale, tiles.dst, 1, out)
+        hip().rel_gemm(xb, tiles.src, tr, ts, tl, wb, None, tiles.eid, 0, msg)
+        op = 1 if tiles.aggr == "mean" else 0
+        seg = tiles.dst_seg
+        out = hip().segment_reduce(msg, seg.indptr, seg.perm, op, 0.0)[0]
         ctx.tiles, ctx.dims = tiles, (R, N, K, Kp, Np, x.shape[0])
         ctx.x_dtype, ctx.w_dtype = x.dtype, weight.dtype
         ctx.save_for_backward(xb, wb)
@@ -325,17 +349,20 @@ class _RelationTransform(torch.autograd.Function):
         xb, wb = ctx.saved_tensors
         R, N, K, Kp, Np, n_src = ctx.dims
         tiles = ctx.tiles
-        tr, ts, tl = tiles.tiles()
         gb = F.pad(dout.to(torch.bfloat16), (0, Np - N)).contiguous()
         dx = dw = None
         if ctx.needs_input_grad[0]:
             wt = wb.transpose(1, 2).contiguous()  # [R, Kp, Np]
-            dxp = torch.zeros(n_src, Kp, device=dout.device, dtype=torch.float32)
-            hip().rel_gemm(gb, tiles.dst, tr, ts, tl, wt, tiles.scale, tiles.src, 1, dxp)
+            msgx = torch.empty(tiles.num_edges, Kp, device=dout.device, dtype=torch.bfloat16)
+            tr, ts, tl = tiles.tiles()
+            hip().rel_gemm(gb, tiles.dst, tr, ts, tl, wt, tiles.scale, tiles.eid, 0, msgx)
+            seg = tiles.src_seg
+            dxp = hip().segment_reduce(msgx, seg.indptr, seg.perm, 0, 0.0)[0]
             dx = dxp[:, :K].to(ctx.x_dtype)
         if ctx.needs_input_grad[1]:
             dwp = torch.zeros(R, Np, Kp, device=dout.device, dtype=torch.float32)
-            hip().rel_gemm_dw(gb, tiles.dst, xb, tiles.src, tiles.scale, tr, ts, tl, dwp)
+            cr, cs, cl = tiles.chunks()
+            hip().rel_gemm_dw(gb, tiles.dst, xb, tiles.src, tiles.scale, cr, cs, cl, dwp)
             dw = dwp[:, :N, :K].to(ctx.w_dtype)
         return dx, dw, None, None
 
@@ -344,8 +371,7 @@ def relation_transform(x, rel, weight, edge_index, size, aggr="mean", tiles=None
     """R-GCN message + aggregation: ``out[i] = aggr_e weight[rel_e] @ x[src_e]`` over the
     in-edges of ``i`` (aggr ``mean`` or ``add``).  x [N_src, K], weight [R, N, K]."""
     R, N, K = weight.shape
-    if use_hip(x, weight) and _round_up(K, 32) <= 1024 and _round_up(N, 32) <= 1024 and \
-            _round_up(N, 32) + _round_up(K, 32) <= 1120:
+    if use_hip(x, weight) and _round_up(N, 64) + _round_up(K, 64) <= 1024:
         if tiles is None:
             key = "_euler_reltiles_%d_%d_%s" % (int(size[0]), R, aggr)
             tiles = _cached(edge_index, key, lambda: RelationTiles(edge_index, rel, size, R, aggr))

@@ -1,0 +1,147 @@
+"""Row-sharded embedding tables with row-sparse training — the MI355X replacement for
+the reference's parameter-server ``mod``-partitioned embedding variables and their
+sparse ``scatter_update`` / optimizer slots (``tf_euler/python/utils/embedding.py:24-68``,
+``layers.py:135-149``; SURVEY §2.7 C2/K12, §2.8 "Embedding / model parallelism").
+
+Row ``r`` lives on rank ``r % world`` at local row ``r // world``.  One training step of
+a table is explicit (no autograd, no dense gradient of the table):
+
+  lookup(ids)                 ids de-duplicated on the GPU (hash kernel, unique.hip),
+                              routed to their owners with one RCCL all-to-all of ids and
+                              one of rows (fwd) — only the touched rows move over xGMI
+  apply(handle, grad_rows)    per-unique-row gradients go back to the owners with one
+                              all-to-all; the owner merges rows requested by several
+                              ranks and applies a row-sparse Adam / Adagrad / SGD update
+                              (optim.hip sparse_optim) to its shard in place
+
+With world == 1 the same code runs without collectives.  With 288 GB of HBM a rank
+holds ~100M x 128 fp32 rows plus Adam slots, so DeepWalk/LINE tables of billions of
+rows fit across one node.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.distributed as dist
+
+from euler_amd.ops import mp_ops
+from euler_amd.ops._native import hip, use_hip
+from euler_amd.ops.gnn_ops import unique_first
+
+__all__ = ["ShardedTable", "LookupHandle"]
+
+_KINDS = {"adam": 0, "adagrad": 1, "sgd": 2}
+
+
+class LookupHandle:
+    __slots__ = ("order", "send", "recv", "local_rows", "n")
+
+    def __init__(self, order, send, recv, local_rows, n):
+        self.order, self.send, self.recv, self.local_rows, self.n = order, send, recv, local_rows, n
+
+
+class ShardedTable:
+    def __init__(self, num_rows, dim, device, group=None, optimizer="adam", lr=0.01, init_std=0.1, seed=0,
+                 beta1=0.9, beta2=0.999, eps=1e-8):
+        self.num_rows, self.dim = int(num_rows), int(dim)
+        self.group = group
+        dist_on = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+        self.world = dist.get_world_size(group) if dist_on else 1
+        self.rank = dist.get_rank(group) if dist_on else 0
+        self.device = torch.device(device)
+        local = max(0, math.ceil((self.num_rows - self.rank) / self.world))
+        g = torch.Generator(device=self.device).manual_seed(int(seed) * 131 + self.rank)
+        self.weight = torch.empty(local, self.dim, device=self.device)
+        self.weight.normal_(0.0, init_std, generator=g)
+        self.kind = _KINDS[optimizer]
+        # optimizer slots: Adam keeps m and v, Adagrad only the accumulator v, SGD none
+        # (the kernel never touches an unused slot, so it aliases a used one or the weight)
+        self.v = torch.zeros_like(self.weight) if self.kind in (0, 1) else self.weight
+        self.m = torch.zeros_like(self.weight) if self.kind == 0 else self.v
+        self.step = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self.lr, self.b1, self.b2, self.eps = float(lr), float(beta1), float(beta2), float(eps)
+
+    # ------------------------------------------------------------------ forward
+    def lookup(self, ids: torch.Tensor):
+        """rows [n, D] (fp32) of the DISTINCT global ids ``ids`` (callers de-duplicate
+        with :func:`unique_first`), plus the handle needed by :meth:`apply`."""
+        ids = ids.reshape(-1).long()
+        if self.world == 1:
+            return self._gather(ids), LookupHandle(None, None, None, ids, ids.numel())
+        W = self.world
+        owner = torch.remainder(ids, W)
+        order = torch.argsort(owner, stable=True)
+        send_counts = torch.bincount(owner, minlength=W)
+        recv_counts = torch.empty_like(send_counts)
+        dist.all_to_all_single(recv_counts, send_counts, group=self.group)
+        counts = torch.stack([send_counts, recv_counts]).cpu()  # one host sync for both
+        send, recv = counts[0].tolist(), counts[1].tolist()
+        recv_ids = torch.empty(sum(recv), dtype=ids.dtype, device=ids.device)
+        dist.all_to_all_single(recv_ids, ids[order].contiguous(), recv, send, group=self.group)
+        local = torch.div(recv_ids, W, rounding_mode="floor")
+        rows = self._gather(local)
+        out_sorted = torch.empty(ids.numel(), self.dim, dtype=rows.dtype, device=rows.device)
+        dist.all_to_all_single(out_sorted, rows, send, recv, group=self.group)
+        out = torch.empty_like(out_sorted)
+        out[order] = out_sorted
+        return out, LookupHandle(order, send, recv, local, ids.numel())
+
+    def _gather(self, local):
+        if use_hip(self.weight, local):
+            return mp_ops.gather(self.weight, local)
+        return self.weight[local]
+
+    # ------------------------------------------------------------------ backward + update
+    def apply(self, handle: LookupHandle, grad_rows: torch.Tensor):
+        """Row-sparse optimizer step with ``grad_rows`` [n, D] = gradient of the rows
+        returned by :meth:`lookup` (same order)."""
+        g = grad_rows.float().contiguous()
+        if self.world > 1:
+            g_sorted = g[handle.order].contiguous()
+            recv_g = torch.empty(sum(handle.recv), self.dim, dtype=g.dtype, device=g.device)
+            dist.all_to_all_single(recv_g, g_sorted, handle.recv, handle.send, group=self.group)
+            rows, g = handle.local_rows, recv_g
+            # several ranks may have asked for the same row: merge before the update
+            rows_u, inv = unique_first(rows)
+            if rows_u.numel() != rows.numel():
+                acc = torch.zeros(rows_u.numel(), self.dim, dtype=g.dtype, device=g.device)
+                if use_hip(acc, inv):
+                    hip().index_add_rows_(acc, inv.contiguous(), g)
+                else:
+                    acc.index_add_(0, inv, g)
+                rows, g = rows_u, acc
+        else:
+            rows = handle.local_rows
+        self._update(rows.contiguous(), g)
+
+    def _update(self, rows, g):
+        if use_hip(self.weight, rows, g):
+            hip().sparse_optim_(self.weight, self.m, self.v, rows, g, self.step, self.lr, self.b1, self.b2,
+                                self.eps, self.kind)
+            return
+        self.step += 1
+        if self.kind == 0:
+            t = float(self.step.item())
+            m = self.b1 * self.m[rows] + (1 - self.b1) * g
+            v = self.b2 * self.v[rows] + (1 - self.b2) * g * g
+            self.m[rows], self.v[rows] = m, v
+            upd = (m / (1 - self.b1 ** t)) / ((v / (1 - self.b2 ** t)).sqrt() + self.eps)
+            self.weight[rows] -= self.lr * upd
+        elif self.kind == 1:
+            acc = self.v[rows] + g * g
+            self.v[rows] = acc
+            self.weight[rows] -= self.lr * g / (acc.sqrt() + self.eps)
+        else:
+            self.weight[rows] -= self.lr * g
+
+    def global_ids(self):
+        return torch.arange(self.weight.shape[0], device=self.device) * self.world + self.rank
+
+    def nbytes(self):
+        ts = {id(t): t for t in (self.weight, self.m, self.v)}.values()
+        return sum(t.numel() * t.element_size() for t in ts)
+
+    @staticmethod
+    def bytes_per_row(dim, optimizer):
+        return dim * 4 * {"adam": 3, "adagrad": 2, "sgd": 1}[optimizer]

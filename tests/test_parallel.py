@@ -151,3 +151,61 @@ def test_data_parallel_estimator(tmp_path):
     res = _run(_worker_estimator, str(tmp_path / "data"), str(tmp_path / "ckpt"))
     assert not [r for r in res if r[1] == "error"], res
     assert len(res) == 2 and all(r[2] for r in res), res
+
+
+def _worker_sparse_table(rank, world, port, q):
+    try:
+        _init(rank, world, port)
+        from euler_amd.ops.gnn_ops import unique_first
+        from euler_amd.parallel.sparse_table import ShardedTable
+
+        torch.manual_seed(0)
+        full = torch.randn(31, 4)
+        tab = ShardedTable(31, 4, "cpu", optimizer="sgd", lr=0.5)
+        tab.weight.copy_(full[tab.global_ids()])
+        # overlapping ids across ranks: the owner must merge the two ranks' grads
+        ids = torch.tensor([3, 29, 7, 12, 3, 0]) + rank
+        u, inv = unique_first(ids)
+        rows, h = tab.lookup(u)
+        ok_fwd = torch.allclose(rows, full[u])
+        g = torch.arange(u.numel() * 4, dtype=torch.float32).view(-1, 4) + 100 * rank
+        tab.apply(h, g)
+        # expected: full - lr * (sum of every rank's grad rows for that id)
+        exp = full.clone()
+        for r in range(world):
+            ur, _ = unique_first(torch.tensor([3, 29, 7, 12, 3, 0]) + r)
+            gr = torch.arange(ur.numel() * 4, dtype=torch.float32).view(-1, 4) + 100 * r
+            exp.index_add_(0, ur, -0.5 * gr)
+        ok_upd = torch.allclose(tab.weight, exp[tab.global_ids()])
+        q.put((rank, "sparse_table", bool(ok_fwd and ok_upd)))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, "error", repr(e)))
+
+
+def _worker_deepwalk(rank, world, port, q):
+    try:
+        _init(rank, world, port)
+        from euler_amd.graph.device_graph import DeviceGraph
+        from euler_amd.models.deepwalk_step import DeepWalkTrainer
+
+        g = DeviceGraph.synthetic(400, 6.0, 40, seed=3, device="cpu")
+        g.manual_seed(11 + rank)
+        tr = DeepWalkTrainer(g, 400, dim=16, batch_size=64, lr=0.05, optimizer="adagrad", seed=5)
+        losses = [float(tr.step()) for _ in range(30)]
+        q.put((rank, "deepwalk", bool(sum(losses[-5:]) < sum(losses[:5]))))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, "error", repr(e)))
+
+
+def test_sharded_table_row_sparse_update():
+    res = _run(_worker_sparse_table)
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == 2 and all(r[2] for r in res), res
+
+
+def test_deepwalk_sharded_two_ranks():
+    res = _run(_worker_deepwalk)
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == 2 and all(r[2] for r in res), res
