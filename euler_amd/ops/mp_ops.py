@@ -26,7 +26,7 @@ import torch
 from euler_amd.ops._native import hip, use_hip
 
 __all__ = ["SegmentIndex", "gather", "scatter_add", "scatter_mean", "scatter_max", "scatter_softmax",
-           "scatter_", "segment_index"]
+           "scatter_", "segment_index", "embedding_bag"]
 
 
 class SegmentIndex:
@@ -214,6 +214,45 @@ class _EdgeSoftmax(torch.autograd.Function):
         g2 = g.contiguous().reshape(p.shape).to(p.dtype)
         gin = hip().edge_softmax_bwd(p, g2, ctx.seg.indptr, ctx.seg.perm)
         return gin.reshape(ctx.shape), None
+
+
+class _EmbeddingBag(torch.autograd.Function):
+    """K9: out[b] = sum_{j in bag b} w_j table[ids_j] as ONE CSR SpMM launch (no [nnz, D]
+    intermediate); backward = per-id rows w_j dout[bag(j)] added into the table grad."""
+
+    @staticmethod
+    def forward(ctx, table, indptr, ids, w, bag_of):
+        ctx.save_for_backward(ids, w, bag_of)
+        ctx.n = table.shape[0]
+        return hip().spmm_csr(indptr, ids, w, table.contiguous())
+
+    @staticmethod
+    def backward(ctx, g):
+        ids, w, bag_of = ctx.saved_tensors
+        rows = hip().gather_rows(g.contiguous(), bag_of) * w.unsqueeze(1).to(g.dtype)
+        acc = torch.zeros((ctx.n, g.shape[1]), dtype=torch.float32, device=g.device)
+        hip().index_add_rows_(acc, ids, rows.contiguous())
+        return acc.to(g.dtype), None, None, None, None
+
+
+def embedding_bag(table, ids, bag_of, num_bags, combiner="sum", weights=None):
+    """Embedding-bag (``tf.nn.embedding_lookup_sparse``, reference layers.py:152-169):
+    ``out[b] = combine_{j: bag_of[j] == b} weights_j * table[ids_j]`` with combiner
+    ``sum`` or ``mean``; ``bag_of`` must be sorted (SparseTensor row order)."""
+    ids = ids.reshape(-1).long()
+    bag_of = bag_of.reshape(-1).long()
+    num_bags = int(num_bags)
+    w = torch.ones(ids.numel(), dtype=torch.float32, device=ids.device) if weights is None else \
+        weights.reshape(-1).float()
+    cnt = torch.bincount(bag_of, minlength=num_bags)[:num_bags]
+    if combiner == "mean":
+        w = w / cnt.clamp(min=1).to(w.dtype)[bag_of]
+    if use_hip(table, ids) and table.dtype in (torch.float32, torch.bfloat16) and table.dim() == 2:
+        indptr = torch.zeros(num_bags + 1, dtype=torch.long, device=ids.device)
+        torch.cumsum(cnt, 0, out=indptr[1:])
+        return _EmbeddingBag.apply(table, indptr, ids.contiguous(), w.contiguous(), bag_of.contiguous())
+    vals = table[ids] * w.unsqueeze(1).to(table.dtype)
+    return torch.zeros((num_bags, table.shape[1]), dtype=table.dtype, device=table.device).index_add(0, bag_of, vals)
 
 
 def scatter_softmax(logits, indices, size=None):

@@ -102,8 +102,11 @@ class SparseEmbedding(Embedding):
     def forward(self, sp):
         rows = torch.as_tensor(sp.indices)[:, 0].to(self.weight.device).long()
         n = int(sp.dense_shape[0])
-        vals = super().forward(torch.as_tensor(sp.values).to(torch.int64))
-        return mp_ops.scatter_("mean" if self.combiner == "mean" else "add", vals, rows, n)
+        ids = self._rows(torch.as_tensor(sp.values).to(torch.int64))
+        # one fused embedding-bag (CSR SpMM over the table) instead of gather + scatter
+        order = torch.argsort(rows, stable=True)
+        return mp_ops.embedding_bag(self.weight, ids.reshape(-1)[order], rows[order], n,
+                                    "mean" if self.combiner == "mean" else "sum")
 
 
 class HashSparseEmbedding(SparseEmbedding):

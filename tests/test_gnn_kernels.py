@@ -222,3 +222,36 @@ def test_gat_conv_uses_fused_kernel(cuda):
     assert out.shape == (100, 64)
     cache = ei._euler_cache
     assert any(k.startswith("_euler_csr") for k in cache), "fused GAT path not taken"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("combiner", ["sum", "mean"])
+def test_embedding_bag_matches_reference(cuda, combiner):
+    from euler_amd.ops import mp_ops
+
+    torch.manual_seed(15)
+    table = torch.randn(1000, 64, device=cuda).requires_grad_(True)
+    bag_of = torch.sort(torch.randint(0, 300, (5000,), device=cuda))[0]
+    ids = torch.randint(0, 1000, (5000,), device=cuda)
+    w = torch.rand(5000, device=cuda)
+    out = mp_ops.embedding_bag(table, ids, bag_of, 310, combiner, w)
+    g = torch.randn_like(out)
+    (out * g).sum().backward()
+    t2 = table.detach().clone().requires_grad_(True)
+    ww = w / torch.bincount(bag_of, minlength=310).clamp(min=1)[bag_of] if combiner == "mean" else w
+    ref = torch.zeros(310, 64, device=cuda).index_add(0, bag_of, t2[ids] * ww.unsqueeze(1))
+    (ref * g).sum().backward()
+    torch.testing.assert_close(out, ref, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(table.grad, t2.grad, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.gpu
+def test_deepwalk_step_gpu(cuda):
+    from euler_amd.graph.device_graph import DeviceGraph
+    from euler_amd.models.deepwalk_step import DeepWalkTrainer
+
+    g = DeviceGraph.synthetic(20000, 8.0, 64, seed=2, device=cuda)
+    tr = DeepWalkTrainer(g, 20000, dim=64, batch_size=512, lr=0.05, optimizer="adam", seed=1)
+    losses = [float(tr.step()) for _ in range(40)]
+    assert all(l == l for l in losses)
+    assert sum(losses[-5:]) < sum(losses[:5])
