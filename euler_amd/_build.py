@@ -127,6 +127,37 @@ def build_engine(max_workers: int = 8, extra_flags=None) -> str:
     return out
 
 
+def console_target():
+    return os.path.join(ROOT, "bin", "remote_console")
+
+
+def build_console(max_workers: int = 8) -> str:
+    """Native remote console (csrc/tools/remote_console.cc; reference
+    euler/tools/remote_console): the engine objects (minus the pybind module) + main()."""
+    build_engine(max_workers)
+    out = console_target()
+    objdir = os.path.join(BUILD, "engine")
+    src = os.path.join(CSRC, "tools", "remote_console.cc")
+    flags = ["-O2", "-std=c++17", "-pthread", "-Wall", "-Wno-sign-compare", "-I" + CSRC]
+    obj = os.path.join(objdir, "tools_remote_console.cc.o")
+    hdr_m = _newest(engine_headers() + [__file__])
+    _compile_all([(["g++"] + flags + ["-c", src, "-o", obj], obj, hdr_m, src)], 1)
+    objs = []
+    for s in engine_sources():
+        if os.sep + "bindings" + os.sep in s:
+            continue
+        o = os.path.join(objdir, os.path.relpath(s, CSRC).replace(os.sep, "_") + ".o")
+        if not os.path.exists(o):  # engine .so was up to date but objects are gone: rebuild them
+            _compile_all([(["g++", "-O3", "-std=c++17", "-fPIC", "-pthread", "-I" + CSRC] +
+                           ["-I" + p for p in _pybind_includes()] + ["-c", s, "-o", o], o, hdr_m, s)], 1)
+        objs.append(o)
+    if not os.path.exists(out) or os.path.getmtime(out) < _newest(objs + [obj]):
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        _run(["g++", "-pthread", "-o", out, obj] + objs + ["-ldl"])
+        _log("linked " + os.path.relpath(out, REPO))
+    return out
+
+
 _SANITIZERS = {
     "thread": ["-fsanitize=thread"],
     "address": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"],
@@ -219,6 +250,7 @@ def build_hip(max_workers: int = 8) -> str:
 def build_all(max_workers: int = 8) -> None:
     if engine_sources():
         build_engine(max_workers)
+        build_console(max_workers)
     build_hip(max_workers)
 
 
@@ -231,3 +263,5 @@ if __name__ == "__main__":
             build_engine()
         if "hip" in what:
             build_hip()
+        if "console" in what:
+            build_console()

@@ -81,3 +81,25 @@ def test_failover_and_fault_injection(cluster):
     env = dict(os.environ, PYTHONPATH=ROOT, EULER_RPC_FAULT_RATE="0.3", EULER_LOG_LEVEL="error")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_native_remote_console(cluster):
+    """The C++ remote console (reference euler/tools/remote_console) against the live
+    2-shard cluster: neighbours of node 1 span both shards' edge types."""
+    from euler_amd import _build
+
+    data, reg = cluster
+    exe = _build.build_console()
+    cmds = "query_nb 1 0\nquery_dense_fea 3 f3\nsample_nb 5 1 4\nmeta\nquit\n"
+    r = subprocess.run([exe, "--registry", reg, "--shard_num", "2"], input=cmds, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    assert "nb: 2 4" in lines
+    assert any(l.startswith("feature: 3.1") for l in lines)
+    nb = [l for l in lines if l.startswith("nb:")][1].split()[1:]
+    assert len(nb) == 4
+    # embedded mode over the same data
+    r = subprocess.run([exe, "--data_path", data], input="query_nb 1 0\nquit\n", capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0 and "nb: 2 4" in r.stdout.splitlines()
