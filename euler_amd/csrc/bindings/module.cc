@@ -489,6 +489,8 @@ PYBIND11_MODULE(_engine, m) {
     d["exec_us"] = c.exec_us.load();
     d["dag_nodes"] = c.dag_nodes.load();
     d["remote_calls"] = c.remote_calls.load();
+    d["local_connections"] = c.local_connections.load();
+    d["tcp_connections"] = c.tcp_connections.load();
     d["rpc_attempts"] = c.rpc_attempts.load();
     d["rpc_failures"] = c.rpc_failures.load();
     d["rpc_bytes_out"] = c.rpc_bytes_out.load();

@@ -154,6 +154,7 @@ struct EngineCounters {
   std::atomic<int64_t> queries{0}, compile_us{0}, exec_us{0}, dag_nodes{0};
   std::atomic<int64_t> remote_calls{0}, rpc_attempts{0}, rpc_failures{0}, rpc_bytes_out{0}, rpc_bytes_in{0};
   std::atomic<int64_t> server_requests{0}, server_us{0};
+  std::atomic<int64_t> local_connections{0}, tcp_connections{0};  // client transports
   static EngineCounters& Get();
   void Reset();
 };

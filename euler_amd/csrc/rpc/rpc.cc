@@ -6,6 +6,7 @@
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <sys/socket.h>
+#include <sys/un.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -68,7 +69,60 @@ bool RecvFrame(int fd, uint32_t* kind, std::string* payload) {
   return len == 0 || ReadAll(fd, &(*payload)[0], len);
 }
 
+// Same-host transport: servers also listen on an abstract-namespace Unix socket named after
+// their TCP port, so a client on the same host skips the TCP/IP stack ("a
+// shared-memory / local transport when client and shards are on one host").  Disabled
+// with EULER_RPC_TRANSPORT=tcp.
+std::string LocalSocketName(int port) { return std::string("euler_amd_rpc_") + std::to_string(port); }
+
+bool LocalTransportEnabled() {
+  const char* t = std::getenv("EULER_RPC_TRANSPORT");
+  return t == nullptr || std::string(t) != "tcp";
+}
+
+bool IsLocalHost(const std::string& host) {
+  if (host == "127.0.0.1" || host == "localhost" || host == "::1") return true;
+  char name[256] = {0};
+  return gethostname(name, sizeof(name) - 1) == 0 && host == name;
+}
+
+socklen_t AbstractAddr(int port, struct sockaddr_un* addr) {
+  memset(addr, 0, sizeof(*addr));
+  addr->sun_family = AF_UNIX;
+  const std::string name = LocalSocketName(port);
+  memcpy(addr->sun_path + 1, name.data(), name.size());  // sun_path[0] = 0: abstract namespace
+  return static_cast<socklen_t>(offsetof(struct sockaddr_un, sun_path) + 1 + name.size());
+}
+
+void SetTimeouts(int fd, int timeout_ms) {
+  struct timeval tv;
+  tv.tv_sec = timeout_ms / 1000;
+  tv.tv_usec = (timeout_ms % 1000) * 1000;
+  setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+  setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
+}
+
+int ConnectLocal(const Endpoint& ep, int timeout_ms) {
+  int fd = socket(AF_UNIX, SOCK_STREAM, 0);
+  if (fd < 0) return -1;
+  struct sockaddr_un addr;
+  const socklen_t len = AbstractAddr(ep.port, &addr);
+  SetTimeouts(fd, timeout_ms);
+  if (connect(fd, reinterpret_cast<sockaddr*>(&addr), len) != 0) {
+    close(fd);
+    return -1;
+  }
+  return fd;
+}
+
 int Connect(const Endpoint& ep, int timeout_ms) {
+  if (LocalTransportEnabled() && IsLocalHost(ep.host)) {
+    const int fd = ConnectLocal(ep, timeout_ms);
+    if (fd >= 0) {
+      EngineCounters::Get().local_connections.fetch_add(1, std::memory_order_relaxed);
+      return fd;
+    }
+  }
   struct addrinfo hints, *res = nullptr;
   memset(&hints, 0, sizeof(hints));
   hints.ai_family = AF_INET;
@@ -81,17 +135,14 @@ int Connect(const Endpoint& ep, int timeout_ms) {
   }
   int one = 1;
   setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
-  struct timeval tv;
-  tv.tv_sec = timeout_ms / 1000;
-  tv.tv_usec = (timeout_ms % 1000) * 1000;
-  setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
-  setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
+  SetTimeouts(fd, timeout_ms);
   if (connect(fd, res->ai_addr, res->ai_addrlen) != 0) {
     close(fd);
     freeaddrinfo(res);
     return -1;
   }
   freeaddrinfo(res);
+  EngineCounters::Get().tcp_connections.fetch_add(1, std::memory_order_relaxed);
   return fd;
 }
 
@@ -436,7 +487,19 @@ Status GraphServer::Start() {
   port_ = ntohs(addr.sin_port);
   pool_.reset(new ThreadPool(std::max(1, opt_.num_threads), "euler-server"));
   running_ = true;
-  accept_thread_ = std::thread([this] { AcceptLoop(); });
+  accept_thread_ = std::thread([this] { AcceptLoop(listen_fd_); });
+  // same-host listener (abstract Unix socket keyed by the TCP port); best effort
+  local_fd_ = socket(AF_UNIX, SOCK_STREAM, 0);
+  if (local_fd_ >= 0) {
+    struct sockaddr_un ua;
+    const socklen_t ulen = AbstractAddr(port_, &ua);
+    if (bind(local_fd_, reinterpret_cast<sockaddr*>(&ua), ulen) == 0 && listen(local_fd_, 128) == 0) {
+      local_accept_thread_ = std::thread([this] { AcceptLoop(local_fd_); });
+    } else {
+      close(local_fd_);
+      local_fd_ = -1;
+    }
+  }
   if (!opt_.registry.empty()) {
     registry_ = Registry::Open(opt_.registry);
     EULER_RETURN_IF_ERROR(registry_->Register(shard_idx_, endpoint(), ShardMeta::FromEnv(*env_, shard_idx_, shard_num_)));
@@ -450,7 +513,12 @@ void GraphServer::Stop() {
   if (registry_) registry_->Deregister(shard_idx_, endpoint());
   shutdown(listen_fd_, SHUT_RDWR);
   close(listen_fd_);
+  if (local_fd_ >= 0) {
+    shutdown(local_fd_, SHUT_RDWR);
+    close(local_fd_);
+  }
   if (accept_thread_.joinable()) accept_thread_.join();
+  if (local_accept_thread_.joinable()) local_accept_thread_.join();
   std::vector<std::thread> ts;
   {
     std::lock_guard<std::mutex> l(conn_mu_);
@@ -462,9 +530,9 @@ void GraphServer::Stop() {
   pool_.reset();
 }
 
-void GraphServer::AcceptLoop() {
+void GraphServer::AcceptLoop(int lfd) {
   while (running_) {
-    int fd = accept(listen_fd_, nullptr, nullptr);
+    int fd = accept(lfd, nullptr, nullptr);
     if (fd < 0) {
       if (!running_) break;
       continue;

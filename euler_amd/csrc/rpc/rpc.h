@@ -110,15 +110,16 @@ class GraphServer {
   int64_t requests() const { return requests_.load(); }
 
  private:
-  void AcceptLoop();
+  void AcceptLoop(int listen_fd);
   void Serve(int fd);
   EngineEnv* env_;
   int shard_idx_, shard_num_;
   ServerOptions opt_;
   std::string host_;
   int listen_fd_ = -1, port_ = 0;
+  int local_fd_ = -1;  // Unix-domain (abstract namespace) listener for same-host clients
   std::atomic<bool> running_{false};
-  std::thread accept_thread_;
+  std::thread accept_thread_, local_accept_thread_;
   std::mutex conn_mu_;
   std::vector<std::thread> conn_threads_;
   std::vector<int> conn_fds_;

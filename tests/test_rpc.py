@@ -103,3 +103,25 @@ def test_native_remote_console(cluster):
     r = subprocess.run([exe, "--data_path", data], input="query_nb 1 0\nquit\n", capture_output=True, text=True,
                        timeout=120)
     assert r.returncode == 0 and "nb: 2 4" in r.stdout.splitlines()
+
+
+def test_same_host_local_transport(cluster):
+    """Same-host clients reach the shard servers over the abstract Unix socket; with
+    EULER_RPC_TRANSPORT=tcp they use TCP (the fallback for remote hosts)."""
+    data, reg = cluster
+    code = ("import euler_amd as ea, json;ea.initialize_graph({'mode':'remote','registry':%r,'shard_num':2});"
+            "ids,_,_=ea.get_full_neighbor([1],['0']);from euler_amd.utils import trace;s=trace.engine_stats();"
+            "print(json.dumps([ids.values.tolist(), s['local_connections'], s['tcp_connections']]))" % reg)
+    import json
+
+    out = {}
+    for mode in ("local", "tcp"):
+        env = dict(os.environ, PYTHONPATH=ROOT)
+        if mode == "tcp":
+            env["EULER_RPC_TRANSPORT"] = "tcp"
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        out[mode] = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["local"][0] == out["tcp"][0] == [2, 4]
+    assert out["local"][1] > 0 and out["local"][2] == 0
+    assert out["tcp"][1] == 0 and out["tcp"][2] > 0
