@@ -45,6 +45,10 @@ class Block:
         mv = lambda t: None if t is None else t.to(device, non_blocking=non_blocking)  # noqa: E731
         return Block(mv(self.n_id), mv(self.res_n_id), mv(self.e_id), mv(self.edge_index), self.size)
 
+    def pin_memory(self):
+        pm = lambda t: None if t is None else t.pin_memory()  # noqa: E731
+        return Block(pm(self.n_id), pm(self.res_n_id), pm(self.e_id), pm(self.edge_index), self.size)
+
 
 class DataFlow:
     def __init__(self, n_id):
@@ -69,6 +73,12 @@ class DataFlow:
     def to(self, device, non_blocking=True):
         out = DataFlow(self.n_id.to(device, non_blocking=non_blocking))
         out.blocks = [b.to(device, non_blocking) for b in self.blocks]
+        out._last = self._last
+        return out
+
+    def pin_memory(self):
+        out = DataFlow(self.n_id.pin_memory())
+        out.blocks = [b.pin_memory() for b in self.blocks]
         out._last = self._last
         return out
 

@@ -35,6 +35,7 @@ import torch.nn as nn
 
 from euler_amd.parallel import dp
 from euler_amd.parallel.embedding import is_sharded
+from euler_amd.utils.prefetch import Prefetcher
 from euler_amd.utils import trace
 from euler_amd.utils.misc import get_optimizer
 
@@ -233,6 +234,15 @@ class BaseEstimator:
             log.info("already trained to step %d", self.global_step)
             return {}
         pending = first
+        # asynchronous input pipeline: the next batches are sampled by the engine (which
+        # releases the GIL) on a worker thread and copied to HBM on a side stream while
+        # this thread runs the current step (utils/prefetch.py); params["prefetch"] = 0
+        # turns it off
+        prefetcher = None
+        depth = int(self.params.get("prefetch", 2 if self.device.type == "cuda" else 0))
+        if depth > 0 and callable(getattr(self.model, "prepare", None)):
+            prefetcher = Prefetcher(lambda: self.model.prepare(self.get_train_from_input(inputs, self.params)),
+                                    self.device, depth=depth)
         t0, n0 = time.time(), self.global_step
         last = {}
         prof = None
@@ -244,7 +254,12 @@ class BaseEstimator:
         rng = (lambda name: trace.trace_range(name)) if tracing else (lambda name: contextlib.nullcontext())
         while self.global_step < total:
             with rng("sample"):
-                source = pending if pending is not None else self.get_train_from_input(inputs, self.params)
+                if pending is not None:
+                    source = pending
+                elif prefetcher is not None:
+                    source = prefetcher.get()
+                else:
+                    source = self.get_train_from_input(inputs, self.params)
             pending = None
             with rng("forward"):
                 _, loss, metric_name, metric = self._run_model(source)
@@ -275,6 +290,8 @@ class BaseEstimator:
                 t0, n0 = time.time(), self.global_step
             if save_steps and self.global_step % save_steps == 0:
                 self.save()
+        if prefetcher is not None:
+            prefetcher.close()
         if prof is not None:
             prof.stop()
         self.save()

@@ -67,6 +67,9 @@ class SupervisedGNN(SuperviseModel):
     def embed(self, n_id):
         return self.gnn(n_id)
 
+    def prepare_embed(self, n_id):
+        return self.gnn.sample_inputs(n_id)
+
 
 class SupervisedGraphSage(SupervisedGNN):
     def __init__(self, dims, fanouts, metapath, feature_idx, feature_dim, label_idx, label_dim, max_id=-1,

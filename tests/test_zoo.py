@@ -282,3 +282,41 @@ def test_kg_zoo_gpu(fb, tmp_path):
     p = _params(fb, tmp_path, train_edge_type="train", batch_size=64, total_step=5, device="cuda", amp="bf16")
     res = EdgeEstimator(model, p).train()
     assert np.isfinite(res["loss"])
+
+
+def test_prefetcher_order_and_errors():
+    from euler_amd.utils.prefetch import Prefetcher
+
+    it = iter(range(5))
+    pf = Prefetcher(lambda: next(it, None), "cpu", depth=2)
+    assert [pf.get() for _ in range(5)] == [0, 1, 2, 3, 4]
+    with pytest.raises(StopIteration):
+        pf.get()
+    pf.close()
+
+    def boom():
+        raise ValueError("sampler failed")
+
+    pf = Prefetcher(boom, "cpu")
+    with pytest.raises(ValueError):
+        pf.get()
+    pf.close()
+
+
+@pytest.mark.parametrize("name", ["graphsage", "gat"])
+def test_estimator_async_input_pipeline(cora, tmp_path, name):
+    """prefetch > 0: engine sampling of the next batches runs on a worker thread"""
+    torch.manual_seed(0)
+    est = NodeEstimator(_node_models(cora)[name](), _params(cora, tmp_path, total_step=6, prefetch=2))
+    res = est.train()
+    assert np.isfinite(res["loss"]) and est.global_step == 6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["graphsage", "gcn", "gat"])
+def test_estimator_gpu_prefetch(cora, tmp_path, name):
+    """CPU engine sampling -> pinned -> side-stream H2D -> gfx950 kernels, through the estimator"""
+    torch.manual_seed(0)
+    est = NodeEstimator(_node_models(cora)[name](), _params(cora, tmp_path, total_step=8, device="cuda"))
+    res = est.train()
+    assert np.isfinite(res["loss"]) and est.global_step == 8
