@@ -162,24 +162,45 @@ def main(argv=None):
         torch.cuda.synchronize()
         if args.impl == "autograd":
             flat.rebind_grads()
+        # the fused trainer double-buffers its samples (next step's roots/hops are drawn on a
+        # side stream during this step): one captured graph per sample-set parity
+        pipelined = args.impl == "fused" and trainer.pipelined
+        parities = (0, 1) if pipelined else (0,)
+
+        def parity():
+            return trainer.parity if pipelined else 0
+
+        def next_parity():
+            if pipelined:
+                trainer.advance_parity()
+
         if world == 1:
-            g_all = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g_all):
-                fwd_bwd()
-                opt_step()
+            g_all = {}
+            for _ in parities:
+                p_ = parity()
+                g_all[p_] = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g_all[p_]):
+                    fwd_bwd()
+                    opt_step()
+            # capture toggled the parity once per graph: back where the eager warmup left it
 
             def step():
-                g_all.replay()
+                g_all[parity()].replay()
+                next_parity()
         else:
-            g_fb = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g_fb):
-                fwd_bwd()
+            g_fb = {}
+            for _ in parities:
+                p_ = parity()
+                g_fb[p_] = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g_fb[p_]):
+                    fwd_bwd()
             g_opt = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g_opt):
                 opt_step()
 
             def step():
-                g_fb.replay()
+                g_fb[parity()].replay()
+                next_parity()
                 allreduce()
                 g_opt.replay()
     else:

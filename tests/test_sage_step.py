@@ -113,3 +113,38 @@ def test_fused_step_hipgraph_trains(cuda):
     assert len(roots_seen) > 1  # replays draw fresh samples
     assert int(tr.step_count.item()) == 62  # 2 eager + 60 replays (capture does not execute)
 
+
+
+def test_fused_step_pipelined_sampling_hipgraph(cuda, monkeypatch):
+    """EULER_AMD_PIPELINE_SAMPLING=1: next step's samples drawn on a side stream; one
+    captured graph per sample-set parity, replayed alternately, keeps training on fresh
+    samples and counts Adam steps like the serial order."""
+    monkeypatch.setenv("EULER_AMD_PIPELINE_SAMPLING", "1")
+    tr = _setup(cuda, B=128, fanouts=(5, 3), D=64, H=64, C=32)
+    assert tr.pipelined
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            tr.step()
+    torch.cuda.current_stream().wait_stream(s)
+    graphs = {}
+    for _ in range(2):
+        p = tr.parity
+        graphs[p] = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graphs[p]):
+            tr.step()
+    losses, roots_seen = [], set()
+    for i in range(60):
+        graphs[tr.parity].replay()
+        tr.advance_parity()
+        if i % 10 == 0:
+            torch.cuda.synchronize()
+            losses.append(float(tr.loss.item()))
+            roots_seen.add(tuple(tr.roots[:8].tolist()))
+    torch.cuda.synchronize()
+    losses.append(float(tr.loss.item()))
+    assert all(l == l for l in losses)
+    assert losses[-1] < losses[0]
+    assert len(roots_seen) > 1
+    assert int(tr.step_count.item()) == 63  # 3 eager + 60 replays
