@@ -53,6 +53,13 @@ def parse_args(argv=None):
                    help="fused = the 10-kernel gfx950 training step (models/sage_step.py); "
                         "autograd = fused SAGE layers under torch autograd (models/fused_sage.py)")
     p.add_argument("--log", action="store_true")
+    p.add_argument("--force-dist", action="store_true",
+                   help="take the multi-GPU code path (process group, graph segments around the gradient "
+                        "all-reduce) even with one rank: validates that path on a single GPU")
+    p.add_argument("--grad-sync", choices=["graph", "single", "overlap"], default="graph",
+                   help="N>1: graph = the RCCL all-reduce is captured into the step's hipGraph (one replay per "
+                        "step, no host launches in between); single = eager all-reduce between two graph "
+                        "segments; overlap = fused impl, all-reduce W1/fc/out grads while dW0 is computed")
     return p.parse_args(argv)
 
 
@@ -80,7 +87,8 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    dist_on = world > 1 or args.force_dist
+    if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
@@ -113,7 +121,7 @@ def main(argv=None):
 
         trainer = FusedSageTrainer(graph, feats, labels, B, fanouts, args.hidden_dim, args.label_dim, lr=args.lr,
                                    init_model=model)
-        if world > 1:
+        if dist_on:
             dist.broadcast(trainer.flat, 0)
             trainer.refresh_shadows()
         loss_buf = trainer.loss_out
@@ -126,7 +134,7 @@ def main(argv=None):
             trainer.optimizer_step(grad_scale=grad_scale)
     else:
         flat = FlatParams(model.parameters(), dev)
-        if world > 1:
+        if dist_on:
             dist.broadcast(flat.flat, 0)
         opt = FlatOptimizer(flat, "adam", args.lr)
         loss_buf = torch.zeros((), device=dev)
@@ -146,8 +154,29 @@ def main(argv=None):
             opt.step(grad_scale=grad_scale)
 
     def allreduce():
-        if world > 1:
+        if dist_on:
             dist.all_reduce(grad_buf)
+
+    # fused impl, N > 1: all-reduce the W1/fc/out_fc gradients (77 % of the bytes) on RCCL's
+    # stream while the outer layer's dW0 is still being computed, then W0's
+    overlap = (args.impl == "fused" and dist_on and args.grad_sync == "overlap" and not trainer.pipelined)
+
+    def synced_step(head, outer, opt):
+        head()
+        w1 = dist.all_reduce(trainer.grad_bucket_head, async_op=True)
+        outer()
+        w2 = dist.all_reduce(trainer.grad_bucket_outer, async_op=True)
+        w1.wait()  # stream-ordered: the optimizer kernels wait for both reductions
+        w2.wait()
+        opt()
+
+    def eager_step():
+        if overlap:
+            synced_step(lambda: trainer.forward_backward("head"), lambda: trainer.forward_backward("outer"), opt_step)
+        else:
+            fwd_bwd()
+            allreduce()
+            opt_step()
 
     use_graph = not args.no_graph
     if use_graph:
@@ -155,9 +184,7 @@ def main(argv=None):
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(3):
-                fwd_bwd()
-                allreduce()
-                opt_step()
+                eager_step()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         if args.impl == "autograd":
@@ -174,19 +201,45 @@ def main(argv=None):
             if pipelined:
                 trainer.advance_parity()
 
-        if world == 1:
-            g_all = {}
-            for _ in parities:
-                p_ = parity()
-                g_all[p_] = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g_all[p_]):
-                    fwd_bwd()
-                    opt_step()
-            # capture toggled the parity once per graph: back where the eager warmup left it
+        captured = False
+        if not dist_on or args.grad_sync == "graph":
+            # one graph per step; with N > 1 the flat-gradient all-reduce is captured too
+            # (RCCL kernels inside the hipGraph)
+            try:
+                g_all = {}
+                for _ in parities:
+                    p_ = parity()
+                    g_all[p_] = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g_all[p_]):
+                        fwd_bwd()
+                        allreduce()
+                        opt_step()
+                # capture toggled the parity once per graph: back where the eager warmup left it
+                captured = True
+            except Exception as e:  # pragma: no cover - RCCL capture unsupported: graph segments
+                if not dist_on:
+                    raise
+                log(f"all-reduce capture failed ({e!r}); falling back to --grad-sync single")
+                args.grad_sync = "single"
+                torch.cuda.synchronize()
+                if pipelined:  # the failed capture toggled the parity
+                    trainer.advance_parity()
 
+        if captured:
             def step():
                 g_all[parity()].replay()
                 next_parity()
+        elif overlap:
+            g_head, g_outer, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g_head):
+                trainer.forward_backward("head")
+            with torch.cuda.graph(g_outer):
+                trainer.forward_backward("outer")
+            with torch.cuda.graph(g_opt):
+                opt_step()
+
+            def step():
+                synced_step(g_head.replay, g_outer.replay, g_opt.replay)
         else:
             g_fb = {}
             for _ in parities:
@@ -204,17 +257,14 @@ def main(argv=None):
                 allreduce()
                 g_opt.replay()
     else:
-        def step():
-            fwd_bwd()
-            allreduce()
-            opt_step()
+        step = eager_step
 
     for i in range(args.warmup):
         step()
     torch.cuda.synchronize()
     first_loss = float(loss_buf.item())
 
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
@@ -224,11 +274,11 @@ def main(argv=None):
             torch.cuda.synchronize()
             log(f"step {i+1} loss {float(loss_buf.item()):.4f}")
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
+    if dist_on:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
     last_loss = float(loss_buf.item())
@@ -262,13 +312,14 @@ def main(argv=None):
                 "hidden_dim": args.hidden_dim,
                 "label_dim": args.label_dim,
                 "hipgraph": use_graph,
+                "grad_sync": ("overlap" if overlap else args.grad_sync) if dist_on else None,
                 "impl": args.impl,
                 "loss_first_last": [round(first_loss, 4), round(last_loss, 4)],
                 "baseline": base_note,
             },
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
 

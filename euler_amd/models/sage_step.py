@@ -127,6 +127,7 @@ class FusedSageTrainer:
         self._cur = 0          # set holding the samples of the next forward_backward
         self._primed = False   # pipelined: set _cur has been sampled
         self._side = torch.cuda.Stream(device=dev) if self.pipelined else None
+        self._join = None
         self._bind(0)
         self.h0 = torch.empty(M1, H, **bf)
         self.A0_kt = torch.empty(M1 * 2 * D, **bf)
@@ -184,11 +185,34 @@ class FusedSageTrainer:
         h.sample_neighbor_into(g.indptr, g.nbr, g.cumw, g.num_rows, g.num_types, -1, st["level1"], self.F2, -1,
                                g.rng, _S_HOP + 1, st["nb2"])
 
-    def forward_backward(self):
+    def forward_backward(self, phase: str = "all"):
+        """One step's sampling, forward and backward into :attr:`grad`.
+
+        ``phase`` splits the step for data parallelism with overlapped gradient sync:
+        ``"head"`` ends once the gradients of W1 / fc / out_fc (:attr:`grad_bucket_head`,
+        77 % of the bytes) are final, ``"outer"`` then computes the outer layer's dW0
+        (:attr:`grad_bucket_outer`), so the all-reduce of the first bucket runs while the
+        second is computed.  ``"all"`` = both, with one grouped dW launch."""
+        if phase in ("all", "head"):
+            self._forward_and_head()
+        if phase == "all":
+            self._dw_reduce([0, 1, 2, 3])
+        elif phase == "head":
+            self._dw_reduce([1, 2, 3])
+        elif phase == "outer":
+            self._dw_reduce([0])
+        else:
+            raise ValueError("phase must be all | head | outer")
+        if phase in ("all", "outer") and self._join is not None:
+            # the optimizer advances the RNG counter: the next step's draws must precede it
+            torch.cuda.current_stream(self.device).wait_event(self._join)
+            self._join = None
+
+    def _forward_and_head(self):
         h = hip()
         use = self._cur
         self._bind(use)
-        join = None
+        self._join = None
         if not self.pipelined:
             self.sample(use)
         else:
@@ -204,8 +228,8 @@ class FusedSageTrainer:
             self._side.wait_event(fork)
             with torch.cuda.stream(self._side):
                 self.sample(1 - use, self._dummy_step)
-                join = torch.cuda.Event()
-                join.record(self._side)
+                self._join = torch.cuda.Event()
+                self._join.record(self._side)
             self._cur = 1 - use
         h.st_sage_fwd(self.features, self.level1, self.nb2, self.F2, self.include_self, self.W0b, self.h0,
                       self.A0_kt, self.mask0, self.bm0)
@@ -215,18 +239,31 @@ class FusedSageTrainer:
         h.st_head(self.A1, self.W1b, self.Wfcb, self.WfcT, self.bfc, self.Woutb, self.WoutT, self.W1T,
                   self.label_idx, self.A1_kt, self.h1_kt, self.emb_kt, self.dlog_kt, self.demb_kt, self.g1_kt,
                   self.dA1, self.gbfc, self.loss_acc)
-        if self.fuse_route:
-            h.st_dw([d[0] for d in self._dw], [d[1] for d in self._dw], self.parts, [d[2] for d in self._dw],
-                    [d[3] for d in self._dw], [d[4] for d in self._dw], [self._kps] * 4, self.mask0, self.dA1,
-                    self.F1, self.include_self)
-        else:
+
+    def _dw_reduce(self, probs):
+        """grouped split-K dW of the listed problems (0 = outer layer W0, routed from dA1)
+        and their split-K reduction into the flat gradient"""
+        h = hip()
+        dw = [self._dw[i] for i in probs]
+        route = 0 in probs
+        if route and not self.fuse_route:
             h.st_route(self.dA1, self.F1, self.include_self, self.mask0, self.g0_kt)
-            h.st_dw([d[0] for d in self._dw], [d[1] for d in self._dw], self.parts, [d[2] for d in self._dw],
-                    [d[3] for d in self._dw], [d[4] for d in self._dw], [self._kps] * 4, None, None, 0, False)
-        h.st_reduce(self.parts, self._grad_views, self._splits)
-        if join is not None:
-            # the optimizer advances the RNG counter: the next step's draws must precede it
-            torch.cuda.current_stream(self.device).wait_event(join)
+        fused = route and self.fuse_route
+        h.st_dw([d[0] for d in dw], [d[1] for d in dw], [self.parts[i] for i in probs], [d[2] for d in dw],
+                [d[3] for d in dw], [d[4] for d in dw], [self._kps] * len(probs), self.mask0 if fused else None,
+                self.dA1 if fused else None, self.F1 if fused else 0, self.include_self if fused else False)
+        h.st_reduce([self.parts[i] for i in probs], [self._grad_views[i] for i in probs],
+                    [self._splits[i] for i in probs])
+
+    @property
+    def grad_bucket_head(self) -> torch.Tensor:
+        """W1, fc (weight + bias) and out_fc gradients: final after phase "head"."""
+        return self.grad[self.offsets[1]:self.offsets[5]]
+
+    @property
+    def grad_bucket_outer(self) -> torch.Tensor:
+        """W0 gradient: final after phase "outer"."""
+        return self.grad[self.offsets[0]:self.offsets[1]]
 
     def optimizer_step(self, grad_scale: float = 1.0):
         o = self.offsets
