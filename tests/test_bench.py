@@ -1,0 +1,52 @@
+"""bench.py contract: one JSON line with the driver's fields, on the single-GPU path and on
+the multi-GPU path (RCCL process group + all-reduce captured in the hipGraph) run with one
+rank under torch.distributed.run."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(cmd):
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    out = json.loads(line)
+    assert KEYS <= set(out), set(KEYS) - set(out)
+    return out
+
+
+SMALL = ["--num-nodes", "200000", "--steps", "20", "--warmup", "5"]
+
+
+@pytest.mark.gpu
+def test_bench_single_gpu_json():
+    out = _run([sys.executable, "bench.py"] + SMALL)
+    assert out["n_gpus"] == 1 and out["value"] > 0 and out["config"]["parallelism"] == "dp1"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["graph", "single"])
+def test_bench_distributed_path_one_rank(mode):
+    out = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--force-dist",
+                "--grad-sync", mode] + SMALL)
+    assert out["config"]["grad_sync"] == mode and out["value"] > 0
+    first, last = out["config"]["loss_first_last"]
+    assert last == last and first == first
