@@ -42,6 +42,8 @@ def main(argv=None):
     p.add_argument("--optimizer", choices=["auto", "adam", "adagrad", "sgd"], default="auto")
     p.add_argument("--lr", type=float, default=0.01)
     p.add_argument("--seed", type=int, default=1234)
+    p.add_argument("--force-dist", action="store_true",
+                   help="process group + all-to-all path even with one rank (validates the N>1 path)")
     args = p.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -51,7 +53,8 @@ def main(argv=None):
         raise SystemExit("bench_deepwalk.py needs a GPU")
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
-    if world > 1:
+    dist_on = world > 1 or args.force_dist
+    if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=dev)
 
@@ -70,7 +73,7 @@ def main(argv=None):
     g = DeviceGraph.synthetic(args.num_nodes, args.avg_degree, args.max_degree, seed=args.seed, device=dev)
     g.manual_seed(args.seed * 7919 + rank)
     tr = DeepWalkTrainer(g, args.num_nodes, args.dim, args.walk_len, 1, 1, args.num_negs, args.batch, args.lr,
-                         args.optimizer, seed=args.seed)
+                         args.optimizer, seed=args.seed, force_comm=args.force_dist)
     torch.cuda.synchronize()
     if rank == 0:
         gib = (tr.target.nbytes() + tr.context.nbytes()) / 2 ** 30
@@ -81,18 +84,18 @@ def main(argv=None):
         tr.step()
     torch.cuda.synchronize()
     first = float(tr.loss)
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     for _ in range(args.steps):
         tr.step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     el = time.perf_counter() - t1
     elt = torch.tensor([el], dtype=torch.float64, device=dev)
-    if world > 1:
+    if dist_on:
         dist.all_reduce(elt, op=dist.ReduceOp.MAX)
     el = float(elt.item())
     pairs = tr.pairs_per_step() * world * args.steps
@@ -112,11 +115,11 @@ def main(argv=None):
             "data": "synthetic (power-law random graph, random-init tables)",
             "config": {"model": f"DeepWalk (walk_len 3, window 1/1, 5 negs, row-sparse {args.optimizer})",
                        "num_nodes": args.num_nodes, "dim": args.dim, "walks_per_gpu": args.batch,
-                       "pairs_per_gpu_step": tr.pairs_per_step(), "parallelism": f"dp{world}+sharded-emb",
+                       "pairs_per_gpu_step": tr.pairs_per_step(), "parallelism": f"dp{world}+sharded-emb", "all_to_all": bool(tr.target.comm),
                        "loss_first_last": [round(first, 4), round(float(tr.loss), 4)],
                        "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1)},
         }), flush=True)
-    if world > 1:
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
 

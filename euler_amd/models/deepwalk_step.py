@@ -40,15 +40,18 @@ def _pair_positions(walk_len, left, right):
 
 class DeepWalkTrainer:
     def __init__(self, graph, num_nodes, dim=128, walk_len=3, left_win_size=1, right_win_size=1, num_negs=5,
-                 batch_size=1024, lr=0.01, optimizer="adam", group=None, seed=0, emb_dtype=torch.float32):
+                 batch_size=1024, lr=0.01, optimizer="adam", group=None, seed=0, emb_dtype=torch.float32,
+                 force_comm=False):
         self.graph = graph
         self.num_nodes = int(num_nodes)
         self.pad = self.num_nodes  # rows: num_nodes + 1 (pad row like the reference's max_id + 1)
         self.dim, self.walk_len, self.num_negs, self.batch = int(dim), int(walk_len), int(num_negs), int(batch_size)
         dev = graph.device
         self.device = dev
-        self.target = ShardedTable(self.num_nodes + 1, dim, dev, group, optimizer, lr, seed=seed)
-        self.context = ShardedTable(self.num_nodes + 1, dim, dev, group, optimizer, lr, seed=seed + 1)
+        self.target = ShardedTable(self.num_nodes + 1, dim, dev, group, optimizer, lr, seed=seed,
+                                   force_comm=force_comm)
+        self.context = ShardedTable(self.num_nodes + 1, dim, dev, group, optimizer, lr, seed=seed + 1,
+                                    force_comm=force_comm)
         pi, pj = _pair_positions(walk_len, left_win_size, right_win_size)
         self.pi, self.pj = pi.to(dev), pj.to(dev)
         self.pairs_per_walk = int(pi.numel())

@@ -43,12 +43,15 @@ class LookupHandle:
 
 class ShardedTable:
     def __init__(self, num_rows, dim, device, group=None, optimizer="adam", lr=0.01, init_std=0.1, seed=0,
-                 beta1=0.9, beta2=0.999, eps=1e-8):
+                 beta1=0.9, beta2=0.999, eps=1e-8, force_comm=False):
         self.num_rows, self.dim = int(num_rows), int(dim)
         self.group = group
-        dist_on = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+        init = dist.is_available() and dist.is_initialized()
+        dist_on = init and dist.get_world_size(group) > 1
         self.world = dist.get_world_size(group) if dist_on else 1
         self.rank = dist.get_rank(group) if dist_on else 0
+        # collectives on (force_comm: also with one rank, to exercise the all-to-all path)
+        self.comm = dist_on or (init and force_comm)
         self.device = torch.device(device)
         local = max(0, math.ceil((self.num_rows - self.rank) / self.world))
         g = torch.Generator(device=self.device).manual_seed(int(seed) * 131 + self.rank)
@@ -67,7 +70,7 @@ class ShardedTable:
         """rows [n, D] (fp32) of the DISTINCT global ids ``ids`` (callers de-duplicate
         with :func:`unique_first`), plus the handle needed by :meth:`apply`."""
         ids = ids.reshape(-1).long()
-        if self.world == 1:
+        if not self.comm:
             return self._gather(ids), LookupHandle(None, None, None, ids, ids.numel())
         W = self.world
         owner = torch.remainder(ids, W)
@@ -97,7 +100,7 @@ class ShardedTable:
         """Row-sparse optimizer step with ``grad_rows`` [n, D] = gradient of the rows
         returned by :meth:`lookup` (same order)."""
         g = grad_rows.float().contiguous()
-        if self.world > 1:
+        if self.comm:
             g_sorted = g[handle.order].contiguous()
             recv_g = torch.empty(sum(handle.recv), self.dim, dtype=g.dtype, device=g.device)
             dist.all_to_all_single(recv_g, g_sorted, handle.recv, handle.send, group=self.group)
