@@ -76,6 +76,11 @@ class Conv(nn.Module):
 
         return dis(0), dis(1)
 
+    def edge_weight(self, edge_index, size):
+        """n0[dst] * n1[src] per edge (the symmetric GCN normalisation)."""
+        n0, n1 = self.norm(edge_index, size)
+        return (mp_ops.gather(n0, edge_index[0]) * mp_ops.gather(n1, edge_index[1])).reshape(-1)
+
     def apply_edge(self, x_j):
         return x_j
 
@@ -94,10 +99,10 @@ class GCNConv(Conv):
 
     def forward(self, x, edge_index, size=None, **kwargs):
         x = _pair(x)
-        n0, n1 = self.norm(edge_index, size)
         src = x[1] if x[1] is not None else x[0]
-        out = mp_ops.gather(n0, edge_index[0]) * mp_ops.gather(n1, edge_index[1]) * mp_ops.gather(src, edge_index[1])
-        return self.fc(self.scatter(out, edge_index, size))
+        # deg^-1/2 on both ends folded into per-edge weights: one SpMM instead of three
+        # gathers, a product and a scatter
+        return self.fc(mp_ops.weighted_aggregate(src, edge_index, size, self.edge_weight(edge_index, size)))
 
 
 class SAGEConv(Conv):
@@ -154,13 +159,11 @@ class TAGConv(Conv):
 
     def forward(self, x, edge_index, size=None, **kwargs):
         x = _pair(x)
-        n0, n1 = self.norm(edge_index, size)
-        gi, gj = mp_ops.gather(n0, edge_index[0]), mp_ops.gather(n1, edge_index[1])
+        w = self.edge_weight(edge_index, size)
         xs = [x[0]]
         src = x[1] if x[1] is not None else x[0]
         for _ in range(self.K):
-            xj = mp_ops.gather(src, edge_index[1])
-            xs.append(self.scatter(gi * gj * xj, edge_index, size))
+            xs.append(mp_ops.weighted_aggregate(src, edge_index, size, w))
         return self.fc(torch.cat(xs, -1))
 
 
@@ -186,12 +189,11 @@ class SGCNConv(Conv):
 
     def forward(self, x, edge_index, size=None, **kwargs):
         x = _pair(x)
-        n0, n1 = self.norm(edge_index, size)
-        gi, gj = mp_ops.gather(n0, edge_index[0]), mp_ops.gather(n1, edge_index[1])
+        w = self.edge_weight(edge_index, size)
         out = x[0]
         src = x[1] if x[1] is not None else x[0]
         for _ in range(self.K):
-            out = self.scatter(gi * gj * mp_ops.gather(src, edge_index[1]), edge_index, size)
+            out = mp_ops.weighted_aggregate(src, edge_index, size, w)
         return self.fc(out)
 
 
@@ -233,13 +235,12 @@ class APPNPConv(Conv):
     def forward(self, x, edge_index, size=None, **kwargs):
         x = _pair(x)
         hidden = list(x)
-        n0, n1 = self.norm(edge_index, size)
-        gi, gj = mp_ops.gather(n0, edge_index[0]), mp_ops.gather(n1, edge_index[1])
+        w = self.edge_weight(edge_index, size)
         cur = x
         out = x[0]
         for _ in range(self.K):
             src = cur[1] if cur[1] is not None else cur[0]
-            out = self.scatter(gi * gj * mp_ops.gather(src, edge_index[1]), edge_index, size)
+            out = mp_ops.weighted_aggregate(src, edge_index, size, w)
             out = out * (1 - self.alpha) + self.alpha * hidden[0]
             cur = [out, hidden[1]]
         return out
@@ -258,15 +259,14 @@ class ARMAConv(Conv):
     def forward(self, x, edge_index, size=None, **kwargs):
         x = _pair(x)
         origin = list(x)
-        n0, n1 = self.norm(edge_index, size)
-        gi, gj = mp_ops.gather(n0, edge_index[0]), mp_ops.gather(n1, edge_index[1])
+        w = self.edge_weight(edge_index, size)
         cur = x
         out = None
         for t in range(self.T):
             k = 0 if self.shared_weights else t
             src = cur[1] if cur[1] is not None else cur[0]
-            xj = self.ws[k](mp_ops.gather(src, edge_index[1]))
-            out = self.scatter(gi * gj * xj, edge_index, size) + self.vs[k](origin[0])
+            # W (A x) == A (W x): the linear runs on the source rows, not on every edge
+            out = mp_ops.weighted_aggregate(self.ws[k](src), edge_index, size, w) + self.vs[k](origin[0])
             if self.act is not None:
                 out = self.act(out)
             cur = [out, origin[1]]

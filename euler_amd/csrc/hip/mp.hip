@@ -201,14 +201,25 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(const int64_t* __restrict
   const int d0 = static_cast<int>(t - s * groups) * 4;
   const int nd = min(4, D - d0);
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int64_t e = indptr[s]; e < indptr[s + 1]; ++e) {
-    const int64_t c = col[e];
-    if (c < 0) continue;
-    const float we = w ? w[e] : 1.f;
-    const T* p = x + c * D + d0;
+  const int64_t a = indptr[s], b = indptr[s + 1];
+  // 4 neighbour rows in flight per thread (index + weight loads, then the row loads)
+  constexpr int U = 4;
+  for (int64_t e0 = a; e0 < b; e0 += U) {
+    int64_t c[U];
+    float we[U], v[U][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (i < nd) acc[i] += we * ld<T>(p + i);
+    for (int u = 0; u < U; ++u) {
+      c[u] = (e0 + u < b) ? col[e0 + u] : -1;
+      we[u] = (e0 + u < b && w) ? w[e0 + u] : 1.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[u][i] = (c[u] >= 0 && i < nd) ? ld<T>(x + c[u] * D + d0 + i) : 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] += we[u] * v[u][i];
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i)

@@ -26,7 +26,7 @@ import torch
 from euler_amd.ops._native import hip, use_hip
 
 __all__ = ["SegmentIndex", "gather", "scatter_add", "scatter_mean", "scatter_max", "scatter_softmax",
-           "scatter_", "segment_index", "embedding_bag"]
+           "scatter_", "segment_index", "embedding_bag", "weighted_aggregate"]
 
 
 class SegmentIndex:
@@ -214,6 +214,65 @@ class _EdgeSoftmax(torch.autograd.Function):
         g2 = g.contiguous().reshape(p.shape).to(p.dtype)
         gin = hip().edge_softmax_bwd(p, g2, ctx.seg.indptr, ctx.seg.perm)
         return gin.reshape(ctx.shape), None
+
+
+class _SpmmIndex:
+    """Destination CSR and source CSC of one ``edge_index`` for weighted aggregation."""
+
+    def __init__(self, edge_index, size):
+        self.dst = SegmentIndex(edge_index[0], size[0])
+        self.src = SegmentIndex(edge_index[1], size[1])
+        self.col = edge_index[1].reshape(-1).long()[self.dst.perm].contiguous()   # sources, CSR order
+        self.row = edge_index[0].reshape(-1).long()[self.src.perm].contiguous()   # destinations, CSC order
+
+
+def _spmm_index(edge_index, size):
+    key = "_euler_spmm_%d_%d" % (int(size[0]), int(size[1]))
+    cache = getattr(edge_index, "_euler_cache", None)
+    if cache is None:
+        cache = {}
+        try:
+            edge_index._euler_cache = cache
+        except AttributeError:
+            return _SpmmIndex(edge_index, size)
+    if key not in cache:
+        cache[key] = _SpmmIndex(edge_index, size)
+    return cache[key]
+
+
+class _WeightedAggregate(torch.autograd.Function):
+    """K4: out = A x with A[dst, src] = w_e (CSR SpMM); backward dx = A^T dout over the
+    CSC, both one launch of ``spmm_csr`` with fp32 accumulation."""
+
+    @staticmethod
+    def forward(ctx, x, w, idx):
+        wd = None if w is None else w[idx.dst.perm].contiguous()
+        ctx.idx, ctx.w, ctx.dtype = idx, w, x.dtype
+        return hip().spmm_csr(idx.dst.indptr, idx.col, wd, x.contiguous())
+
+    @staticmethod
+    def backward(ctx, g):
+        idx, w = ctx.idx, ctx.w
+        ws = None if w is None else w[idx.src.perm].contiguous()
+        dx = hip().spmm_csr(idx.src.indptr, idx.row, ws, g.to(ctx.dtype).contiguous())
+        return dx, None, None
+
+
+def weighted_aggregate(x, edge_index, size, weight=None):
+    """``out[i] = sum_{e: dst(e) = i} weight_e * x[src(e)]`` (``edge_index`` row 0 =
+    destination, row 1 = source) — the GCN-family normalised aggregation
+    (gcn_conv.py:42-54: gather, gather, gather, multiply, scatter_add) as one SpMM.
+    ``weight`` (per edge) is treated as a constant (no gradient)."""
+    size = (int(size[0]), int(size[1]))
+    w = None if weight is None else weight.reshape(-1).float().detach()
+    if use_hip(x) and x.dim() == 2 and x.dtype in (torch.float32, torch.bfloat16):
+        return _WeightedAggregate.apply(x, w, _spmm_index(edge_index, size))
+    dst, src = edge_index[0].reshape(-1).long(), edge_index[1].reshape(-1).long()
+    keep = (dst >= 0) & (src >= 0)
+    vals = x[src[keep]]
+    if w is not None:
+        vals = vals * w[keep].to(x.dtype).view(-1, *([1] * (x.dim() - 1)))
+    return torch.zeros((size[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device).index_add(0, dst[keep], vals)
 
 
 class _EmbeddingBag(torch.autograd.Function):

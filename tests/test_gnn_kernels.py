@@ -255,3 +255,25 @@ def test_deepwalk_step_gpu(cuda):
     losses = [float(tr.step()) for _ in range(40)]
     assert all(l == l for l in losses)
     assert sum(losses[-5:]) < sum(losses[:5])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,D", [(torch.float32, 48), (torch.bfloat16, 64), (torch.float32, 7)])
+def test_weighted_aggregate_spmm(cuda, dtype, D):
+    from euler_amd.ops import mp_ops
+
+    torch.manual_seed(16)
+    n_dst, n_src, E = 300, 800, 6000
+    ei = _graph(n_dst, n_src, E, cuda, seed=17, pad=15)
+    x = torch.randn(n_src, D, device=cuda).to(dtype).requires_grad_(True)
+    w = torch.rand(E, device=cuda)
+    out = mp_ops.weighted_aggregate(x, ei, (n_dst, n_src), w)
+    g = torch.randn(out.shape, device=cuda)
+    (out.float() * g).sum().backward()
+    x2 = x.detach().float().requires_grad_(True)
+    keep = (ei[0] >= 0) & (ei[1] >= 0)
+    ref = torch.zeros(n_dst, D, device=cuda).index_add(0, ei[0][keep], x2[ei[1][keep]] * w[keep].unsqueeze(1))
+    (ref * g).sum().backward()
+    tol = dict(atol=3e-2, rtol=3e-2) if dtype == torch.bfloat16 else dict(atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(out.float(), ref, **tol)
+    torch.testing.assert_close(x.grad.float(), x2.grad, **tol)
