@@ -76,6 +76,19 @@ class Conv(nn.Module):
 
         return dis(0), dis(1)
 
+    def aggregate(self, src, edge_index, size, aggr=None):
+        """aggr (add | mean) of the source rows over each destination's in-edges as one SpMM
+        (mean: weight 1 / in-degree); max keeps the gather + segment-max kernels."""
+        aggr = aggr or self.aggr
+        if aggr == "max":
+            return self.scatter(mp_ops.gather(src, edge_index[1]), edge_index, size, "max")
+        w = None
+        if aggr == "mean":
+            seg = _seg(edge_index, 0, size[0])
+            inv = 1.0 / seg.counts.clamp(min=1).float()
+            w = inv[edge_index[0].long().clamp(min=0)]
+        return mp_ops.weighted_aggregate(src, edge_index, size, w)
+
     def edge_weight(self, edge_index, size):
         """n0[dst] * n1[src] per edge (the symmetric GCN normalisation)."""
         n0, n1 = self.norm(edge_index, size)
@@ -116,7 +129,7 @@ class SAGEConv(Conv):
     def forward(self, x, edge_index, size=None, **kwargs):
         x = _pair(x)
         xs = x[1] if x[1] is not None else x[0]
-        agg = self.scatter(mp_ops.gather(xs, edge_index[1]), edge_index, size)
+        agg = self.aggregate(xs, edge_index, size)
         return self.self_fc(x[0]) + self.neigh_fc(agg)
 
 
@@ -209,7 +222,7 @@ class GINConv(Conv):
     def forward(self, x, edge_index, size=None, **kwargs):
         x = _pair(x)
         src = x[1] if x[1] is not None else x[0]
-        agg = self.scatter(mp_ops.gather(src, edge_index[1]), edge_index, size)
+        agg = self.aggregate(src, edge_index, size)
         return self.mlp((1 + self.eps) * x[0] + agg)
 
 
@@ -222,7 +235,7 @@ class GraphConv(Conv):
     def forward(self, x, edge_index, size=None, **kwargs):
         x = _pair(x)
         src = x[1] if x[1] is not None else x[0]
-        agg = self.scatter(mp_ops.gather(self.fc(src), edge_index[1]), edge_index, size)
+        agg = self.aggregate(self.fc(src), edge_index, size)
         return self.liner(x[0]) + agg
 
 
