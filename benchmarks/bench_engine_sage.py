@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""GraphSAGE through the C++ graph engine (the reference's architecture: CPU-side graph
+store + sampler, tensors streamed to the GPU) with the estimator loop, with and without
+the asynchronous input pipeline (utils/prefetch.py: engine sampling + feature/label
+fetch of the next batches on a worker thread, pinned side-stream H2D).
+
+Data: PPI-schema synthetic graph (``get_dataset("ppi")``: 56,944 nodes, 50-d features,
+121 multi-hot labels; reference examples/graphsage default dataset family), converted
+to the reference on-disk format and loaded by the engine.  Model: SupervisedGraphSage
+[128, 128, 121], fanouts [10, 10], sigmoid CE, Adam.
+
+Usage: python benchmarks/bench_engine_sage.py [--steps K] [--scale S] [--batch B]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def run(ds, args, prefetch, device, workers=2):
+    import euler_amd as ea
+    from euler_amd import models as Z
+    from euler_amd.estimator import NodeEstimator
+
+    ea.set_seed(1)
+    torch.manual_seed(1)
+    model = Z.SupervisedGraphSage([128, 128, ds.label_dim], [10, 10], [["train"], ["train"]], "feature",
+                                  ds.feature_dim, "label", ds.label_dim, max_id=ds.max_node_id)
+    tnt = ds.train_node_type[0] if isinstance(ds.train_node_type, list) else ds.train_node_type
+
+    def params(total):
+        return {"model_dir": tempfile.mkdtemp(prefix="euler_amd_ckpt_"), "batch_size": args.batch,
+                "total_step": total, "optimizer": "adam", "learning_rate": 0.01, "log_steps": 10 ** 9,
+                "train_node_type": tnt, "device": device, "prefetch": prefetch,
+                "prefetch_workers": workers}
+
+    NodeEstimator(model, params(args.warmup)).train()
+    est = NodeEstimator(model, params(args.steps))
+    if device == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = est.train()
+    if device == "cuda":
+        torch.cuda.synchronize()
+    return time.perf_counter() - t0, res
+
+
+def main(argv=None):
+    p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    p.add_argument("--steps", type=int, default=60)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=512)
+    p.add_argument("--scale", type=float, default=1.0)
+    args = p.parse_args(argv)
+    from euler_amd.dataset import get_dataset
+
+    dev = "cuda" if torch.cuda.is_available() else "cpu"
+    t0 = time.time()
+    ds = get_dataset("ppi", data_dir=tempfile.mkdtemp(prefix="euler_amd_ppi_"), scale=args.scale)
+    ds.load_graph()
+    print(f"[bench_engine_sage] ppi-schema graph scale {args.scale} ready in {time.time() - t0:.1f}s",
+          file=sys.stderr, flush=True)
+    out = {}
+    for name, pf, wk in (("serial", 0, 1), ("prefetch_1worker", 2, 1), ("prefetch", 4, 4)):
+        el, res = run(ds, args, pf, dev, wk)
+        out[name] = {"samples_per_s": round(args.batch * args.steps / el, 1), "ms_per_step": round(el * 1e3 / args.steps, 2),
+                     "loss": round(float(res.get("loss", float("nan"))), 4)}
+    print(json.dumps({
+        "metric": "train samples/sec, GraphSAGE via the C++ graph engine + estimator (reference architecture)",
+        "value": out["prefetch"]["samples_per_s"],
+        "unit": "samples/s",
+        "n_gpus": 1 if dev == "cuda" else 0,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": out["prefetch"]["ms_per_step"],
+        "higher_is_better": True,
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic PPI-schema graph (56,944 nodes, 50-d features, 121 labels)",
+        "config": {"model": "SupervisedGraphSage [128, 128, 121], fanouts [10, 10], Adam", "batch": args.batch,
+                   "scale": args.scale, **out},
+    }), flush=True)
+
+
+if __name__ == "__main__":
+    main()

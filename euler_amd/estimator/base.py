@@ -242,7 +242,7 @@ class BaseEstimator:
         depth = int(self.params.get("prefetch", 2 if self.device.type == "cuda" else 0))
         if depth > 0 and callable(getattr(self.model, "prepare", None)):
             prefetcher = Prefetcher(lambda: self.model.prepare(self.get_train_from_input(inputs, self.params)),
-                                    self.device, depth=depth)
+                                    self.device, depth=depth, workers=int(self.params.get("prefetch_workers", 1)))
         t0, n0 = time.time(), self.global_step
         last = {}
         prof = None
