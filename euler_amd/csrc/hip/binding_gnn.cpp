@@ -255,6 +255,128 @@ std::vector<torch::Tensor> sgns_bwd(torch::Tensor emb, torch::Tensor pos, torch:
   return {demb, dpos, dneg};
 }
 
+// ----------------------------------------------------------------------------- index-driven SGNS
+const int64_t* map_ptr(const c10::optional<torch::Tensor>& map, int64_t& n, const char* name) {
+  n = 0;
+  if (!map.has_value()) return nullptr;
+  typed(*map, torch::kInt64, name);
+  n = map->numel();
+  return map->data_ptr<int64_t>();
+}
+
+// T / C fp32 row tables; tinv [P], cinv [P*(1+K)] (positives then negatives) index the
+// unique ids, tmap / cmap map those to table rows (absent: the ids are rows)
+std::vector<torch::Tensor> sgns_fwd_idx(torch::Tensor T, c10::optional<torch::Tensor> tmap, torch::Tensor tinv,
+                                        torch::Tensor C, c10::optional<torch::Tensor> cmap, torch::Tensor cinv,
+                                        int64_t K, double gscale) {
+  typed(T, torch::kFloat32, "T");
+  typed(C, torch::kFloat32, "C");
+  typed(tinv, torch::kInt64, "tinv");
+  typed(cinv, torch::kInt64, "cinv");
+  TORCH_CHECK(T.dim() == 2 && C.dim() == 2 && T.size(1) == C.size(1), "T [*, D], C [*, D]");
+  const int64_t P = tinv.numel(), D = T.size(1);
+  TORCH_CHECK(K >= 0 && cinv.numel() == P * (1 + K), "cinv must hold P*(1+K) entries");
+  TORCH_CHECK(D % 4 == 0 && D <= 256, "sgns_fwd_idx needs D % 4 == 0 and D <= 256");
+  int64_t nTm, nCm;
+  const int64_t* tm = map_ptr(tmap, nTm, "tmap");
+  const int64_t* cm = map_ptr(cmap, nCm, "cmap");
+  const c10::DeviceGuard g(T.device());
+  auto fopt = T.options();
+  auto coef = torch::empty({P, 1 + K}, fopt);
+  auto loss_rows = torch::empty({P}, fopt);
+  ok(eh_sgns_fwd_idx(T.data_ptr<float>(), tm, nTm, tinv.data_ptr<int64_t>(), T.size(0), C.data_ptr<float>(), cm, nCm,
+                     cinv.data_ptr<int64_t>(), C.size(0), P, static_cast<int>(K), static_cast<int>(D),
+                     static_cast<float>(gscale), coef.data_ptr<float>(), loss_rows.data_ptr<float>(), stream()),
+     "sgns_fwd_idx");
+  return {coef, loss_rows};
+}
+
+// occurrence lists of inv (values in [0, n_u)): ptr [n_u + 1] int64, list [n] int32
+std::vector<torch::Tensor> occ_csr(torch::Tensor inv, int64_t n_u) {
+  typed(inv, torch::kInt64, "inv");
+  TORCH_CHECK(inv.numel() < (int64_t{1} << 31), "occ_csr: too many occurrences");
+  const c10::DeviceGuard g(inv.device());
+  auto iopt = inv.options();
+  auto ptr = torch::zeros({n_u + 1}, iopt);
+  if (inv.numel() > 0) {
+    auto cnt = torch::bincount(inv, {}, n_u);
+    TORCH_CHECK(cnt.numel() == n_u, "occ_csr: inv values must lie in [0, n_u)");
+    ptr.narrow(0, 1, n_u).copy_(torch::cumsum(cnt, 0));
+  }
+  auto cursor = torch::zeros({n_u}, iopt.dtype(torch::kInt32));
+  auto list = torch::empty({inv.numel()}, iopt.dtype(torch::kInt32));
+  ok(eh_occ_fill(inv.data_ptr<int64_t>(), inv.numel(), ptr.data_ptr<int64_t>(), cursor.data_ptr<int32_t>(),
+                 list.data_ptr<int32_t>(), stream()),
+     "occ_fill");
+  return {ptr, list};
+}
+
+struct UpdIn {
+  int64_t n_u, P, n_smap;
+  const int64_t* smap;
+};
+
+UpdIn upd_check(int64_t side, const torch::Tensor& ptr, const torch::Tensor& list, const torch::Tensor& coef, int64_t K,
+                const torch::Tensor& src, const c10::optional<torch::Tensor>& smap, const torch::Tensor& sinv) {
+  TORCH_CHECK(side == 0 || side == 1, "side: 0 target, 1 context");
+  typed(ptr, torch::kInt64, "ptr");
+  typed(list, torch::kInt32, "list");
+  typed(coef, torch::kFloat32, "coef");
+  typed(src, torch::kFloat32, "src");
+  typed(sinv, torch::kInt64, "sinv");
+  TORCH_CHECK(coef.dim() == 2 && coef.size(1) == K + 1 && K >= (side == 1 ? 1 : 0), "coef must be [P, 1+K]");
+  TORCH_CHECK(src.dim() == 2 && src.size(1) % 4 == 0 && src.size(1) <= 256, "src [*, D], D % 4 == 0, D <= 256");
+  const int64_t P = coef.size(0);
+  TORCH_CHECK(sinv.numel() == (side == 0 ? P * (1 + K) : P), "sinv: context occurrences (side 0) or targets (side 1)");
+  TORCH_CHECK(list.numel() == (side == 0 ? P : P * (1 + K)), "list must cover every occurrence of this side");
+  UpdIn r;
+  r.n_u = ptr.numel() - 1;
+  r.P = P;
+  r.smap = map_ptr(smap, r.n_smap, "smap");
+  return r;
+}
+
+torch::Tensor sgns_grad(int64_t side, torch::Tensor ptr, torch::Tensor list, torch::Tensor coef, int64_t K,
+                        torch::Tensor src, c10::optional<torch::Tensor> smap, torch::Tensor sinv) {
+  const UpdIn u = upd_check(side, ptr, list, coef, K, src, smap, sinv);
+  const c10::DeviceGuard g(src.device());
+  const int64_t D = src.size(1);
+  auto gout = torch::empty({u.n_u, D}, src.options());
+  ok(eh_sgns_update(static_cast<int>(side), u.n_u, ptr.data_ptr<int64_t>(), list.data_ptr<int32_t>(),
+                    coef.data_ptr<float>(), u.P, static_cast<int>(K), static_cast<int>(D), src.data_ptr<float>(),
+                    src.size(0), u.smap, u.n_smap, sinv.data_ptr<int64_t>(), gout.data_ptr<float>(), nullptr, nullptr,
+                    nullptr, nullptr, 0, nullptr, 0.f, 0.f, 0.f, 0.f, 2, stream()),
+     "sgns_grad");
+  return gout;
+}
+
+void sgns_apply_(int64_t side, torch::Tensor ptr, torch::Tensor list, torch::Tensor coef, int64_t K, torch::Tensor src,
+                 c10::optional<torch::Tensor> smap, torch::Tensor sinv, torch::Tensor table, torch::Tensor m,
+                 torch::Tensor v, c10::optional<torch::Tensor> rows, torch::Tensor step, double lr, double b1, double b2,
+                 double eps, int64_t kind) {
+  const UpdIn u = upd_check(side, ptr, list, coef, K, src, smap, sinv);
+  typed(table, torch::kFloat32, "table");
+  typed(m, torch::kFloat32, "m");
+  typed(v, torch::kFloat32, "v");
+  typed(step, torch::kInt64, "step");
+  TORCH_CHECK(kind >= 0 && kind <= 2, "kind: 0 adam, 1 adagrad, 2 sgd");
+  TORCH_CHECK(table.dim() == 2 && table.size(1) == src.size(1) && m.sizes() == table.sizes() &&
+                  v.sizes() == table.sizes(),
+              "table / m / v must be [rows, D]");
+  int64_t n_rows_map = 0;
+  const int64_t* rp = map_ptr(rows, n_rows_map, "rows");
+  TORCH_CHECK(!rp || n_rows_map == u.n_u, "rows must hold one table row per unique id");
+  TORCH_CHECK(rp || u.n_u <= table.size(0), "without rows, unique ids are table rows");
+  const c10::DeviceGuard g(src.device());
+  ok(eh_sgns_update(static_cast<int>(side), u.n_u, ptr.data_ptr<int64_t>(), list.data_ptr<int32_t>(),
+                    coef.data_ptr<float>(), u.P, static_cast<int>(K), static_cast<int>(src.size(1)),
+                    src.data_ptr<float>(), src.size(0), u.smap, u.n_smap, sinv.data_ptr<int64_t>(), nullptr,
+                    table.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), rp, table.size(0),
+                    step.data_ptr<int64_t>(), static_cast<float>(lr), static_cast<float>(b1), static_cast<float>(b2),
+                    static_cast<float>(eps), static_cast<int>(kind), stream()),
+     "sgns_apply");
+}
+
 // ----------------------------------------------------------------------------- KG scores
 struct KgIn {
   int64_t B, K, D, nneg;
@@ -351,6 +473,10 @@ void register_gnn_ops(pybind11::module& m) {
   m.attr("rel_gemm_dw_chunk") = eh_rel_gemm_dw_chunk();
   m.def("sgns_fwd", &sgns_fwd);
   m.def("sgns_bwd", &sgns_bwd);
+  m.def("sgns_fwd_idx", &sgns_fwd_idx);
+  m.def("occ_csr", &occ_csr);
+  m.def("sgns_grad", &sgns_grad);
+  m.def("sgns_apply_", &sgns_apply_);
   m.def("kg_fwd", &kg_fwd);
   m.def("kg_bwd", &kg_bwd);
   m.def("unique_first", &unique_first);

@@ -138,6 +138,176 @@ __global__ __launch_bounds__(256) void sgns_bwd_kernel(const T* __restrict__ emb
   EV<T>::store(demb + L.row * D + L.sub * V, de);
 }
 
+// ----------------------------------------------------------------------------- K11b
+// Index-driven skip-gram step with no per-pair gradient rows (DeepWalk / LINE tables).
+// A step has P pairs, each with one positive and K negatives.  Rows are addressed through
+// two levels: inv (per occurrence, into the de-duplicated ids) and map (unique id -> table
+// row; null = identity).  Context occurrences are ordered [P positives | P*K negatives].
+//
+//   sgns_fwd_idx : logits straight from the tables, writes coef[p, s] = (sigmoid(x) - y) * gscale
+//   sgns_update  : per UNIQUE row u, its gradient is rebuilt from the occurrence list of u
+//                  (CSR over inv: occ_fill) instead of being scattered from per-pair rows:
+//                    side 0 (target):  g_u = sum_{p in occ(u)} sum_s coef[p, s] * C[ctx(p, s)]
+//                    side 1 (context): g_u = sum_{(p,s) in occ(u)} coef[p, s] * E[tgt(p)]
+//                  then either written out (sharded tables: sent to the owners) or applied in
+//                  place with row-sparse Adam / Adagrad / SGD (one rank owns every row).
+// Compared with sgns_bwd + index_add_rows + sparse_optim this drops the per-pair gradient
+// rows (P*(1+K)*D*4 bytes written and read back), the zero fill of the accumulator, every
+// float atomic, and the accumulator round trip.
+
+// table row of occurrence i, or -1 when the row is outside [0, n) (the load is skipped)
+// (map holds n_map entries; inv values outside it are dropped as well)
+__device__ __forceinline__ int64_t occ_row(const int64_t* __restrict__ map, int64_t n_map,
+                                           const int64_t* __restrict__ inv, int64_t i, int64_t n) {
+  const int64_t u = inv[i];
+  if (map && (u < 0 || u >= n_map)) return -1;
+  const int64_t r = map ? map[u] : u;
+  return r >= 0 && r < n ? r : -1;
+}
+__device__ __forceinline__ void load_row4(const float* __restrict__ base, int64_t r, int D, int d, float* x) {
+  if (r >= 0) {
+    EV<float>::load(base + r * D + d, x);
+  } else {
+    x[0] = x[1] = x[2] = x[3] = 0.f;
+  }
+}
+
+// context occurrence index of slot s (0 = positive) of pair p
+__device__ __forceinline__ int64_t ctx_occ(int64_t p, int s, int64_t P, int K) {
+  return s == 0 ? p : P + p * K + (s - 1);
+}
+
+__global__ __launch_bounds__(256) void sgns_fwd_idx_kernel(const float* __restrict__ T, const int64_t* __restrict__ tmap,
+                                                           int64_t nTm, const int64_t* __restrict__ tinv, int64_t nT,
+                                                           const float* __restrict__ C,
+                                                           const int64_t* __restrict__ cmap, int64_t nCm,
+                                                           const int64_t* __restrict__ cinv, int64_t nC, int64_t P,
+                                                           int K, int D,
+                                                           int lp, float gscale, float* __restrict__ coef,
+                                                           float* __restrict__ loss_rows) {
+  const RowLane L = row_lane(lp, P);
+  const bool ok = L.ok && L.sub * 4 < D;
+  float e[4] = {0.f, 0.f, 0.f, 0.f};
+  if (ok) load_row4(T, occ_row(tmap, nTm, tinv, L.row, nT), D, L.sub * 4, e);
+  float loss = 0.f;
+  for (int s = 0; s <= K; ++s) {
+    float part = 0.f;
+    if (ok) {
+      float c[4];
+      load_row4(C, occ_row(cmap, nCm, cinv, ctx_occ(L.row, s, P, K), nC), D, L.sub * 4, c);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) part += e[v] * c[v];
+    }
+    const float x = emb_group_sum(part, lp);
+    const float y = s == 0 ? 1.f : 0.f;
+    loss += sigmoid_ce(x, y);
+    if (L.ok && L.sub == 0) coef[L.row * (K + 1) + s] = (sigmoidf(x) - y) * gscale;
+  }
+  if (L.ok && L.sub == 0) loss_rows[L.row] = loss;
+}
+
+// occurrence lists: list[ptr[inv[o]] + k] = o (order inside a list follows the atomics)
+__global__ __launch_bounds__(256) void occ_fill_kernel(const int64_t* __restrict__ inv, int64_t n,
+                                                       const int64_t* __restrict__ ptr, int* __restrict__ cursor,
+                                                       int* __restrict__ list) {
+  const int64_t o = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (o >= n) return;
+  const int64_t u = inv[o];
+  list[ptr[u] + atomicAdd(cursor + u, 1)] = static_cast<int>(o);
+}
+
+struct SgnsUpd {
+  const int64_t* ptr;   // [n_u + 1]
+  const int* list;      // occurrence ids
+  const float* coef;    // [P, K + 1]
+  const float* src;     // rows the gradient is built from
+  const int64_t* smap;  // unique id -> src row (null = identity)
+  const int64_t* sinv;  // occurrence -> unique id of the OTHER table (side 0: context occ, side 1: target occ)
+  float* gout;          // [n_u, D] or null (apply the optimizer instead)
+  float* table;
+  float* m;
+  float* v;
+  const int64_t* rows;  // unique id -> row of `table` (null = identity)
+  const int64_t* step;
+  int64_t n_u, P, n_rows, n_src, n_smap;
+  int K, D, lp, side, kind;
+  float lr, b1, b2, eps;
+};
+
+__global__ __launch_bounds__(256) void sgns_update_kernel(SgnsUpd a) {
+  const RowLane L = row_lane(a.lp, a.n_u);
+  if (!L.ok || L.sub * 4 >= a.D) return;  // no cross-lane exchange
+  const int d = L.sub * 4;
+  float g[4] = {0.f, 0.f, 0.f, 0.f};
+  const int64_t beg = a.ptr[L.row], end = a.ptr[L.row + 1];
+  const int KK = a.K + 1;
+  for (int64_t i = beg; i < end; ++i) {
+    const int64_t o = a.list[i];
+    if (a.side == 0) {
+      // target occurrence o is pair o: all of its context rows
+      for (int s = 0; s < KK; ++s) {
+        float c[4];
+        const float w = a.coef[o * KK + s];
+        load_row4(a.src, occ_row(a.smap, a.n_smap, a.sinv, ctx_occ(o, s, a.P, a.K), a.n_src), a.D, d, c);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) g[k] += w * c[k];
+      }
+    } else {
+      // context occurrence o -> (pair, slot)
+      int64_t p;
+      int s;
+      if (o < a.P) {
+        p = o;
+        s = 0;
+      } else {
+        const int64_t q = o - a.P;
+        p = q / a.K;
+        s = 1 + static_cast<int>(q - p * a.K);
+      }
+      float e[4];
+      const float w = a.coef[p * KK + s];
+      load_row4(a.src, occ_row(a.smap, a.n_smap, a.sinv, p, a.n_src), a.D, d, e);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) g[k] += w * e[k];
+    }
+  }
+  if (a.gout) {
+    EV<float>::store(a.gout + L.row * a.D + d, g);
+    return;
+  }
+  const int64_t r = a.rows ? a.rows[L.row] : L.row;
+  if (r < 0 || r >= a.n_rows) return;
+  const int64_t off = r * a.D + d;
+  float4_t p = *reinterpret_cast<float4_t*>(a.table + off);
+  if (a.kind == 0) {
+    const float st = static_cast<float>(a.step[0]);
+    const float bc1 = 1.f - __powf(a.b1, st), bc2 = 1.f - __powf(a.b2, st);
+    float4_t mi = *reinterpret_cast<float4_t*>(a.m + off), vi = *reinterpret_cast<float4_t*>(a.v + off);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      mi[k] = a.b1 * mi[k] + (1.f - a.b1) * g[k];
+      vi[k] = a.b2 * vi[k] + (1.f - a.b2) * g[k] * g[k];
+      p[k] -= a.lr * (mi[k] / bc1) / (sqrtf(vi[k] / bc2) + a.eps);
+    }
+    *reinterpret_cast<float4_t*>(a.m + off) = mi;
+    *reinterpret_cast<float4_t*>(a.v + off) = vi;
+  } else if (a.kind == 1) {
+    float4_t acc = *reinterpret_cast<float4_t*>(a.v + off);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      acc[k] += g[k] * g[k];
+      p[k] -= a.lr * g[k] / (sqrtf(acc[k]) + a.eps);
+    }
+    *reinterpret_cast<float4_t*>(a.v + off) = acc;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) p[k] -= a.lr * g[k];
+  }
+  *reinterpret_cast<float4_t*>(a.table + off) = p;
+}
+
+__global__ void sgns_step_inc_kernel(int64_t* step) { step[0] += 1; }
+
 // ----------------------------------------------------------------------------- K10
 // score kinds: 0 TransE-L1, 1 TransE-L2, 2 DistMult.  corrupt: 0 front (neg replaces src),
 // 1 tail (neg replaces dst), 2 both (front scores then tail scores).  Tables fp32 [*, D].
@@ -375,6 +545,65 @@ hipError_t eh_kg_bwd(const float* ent, const float* rel, const int64_t* src, con
   if (D % 4 != 0 || D > 256 || kind < 0 || kind > 2 || corrupt < 0 || corrupt > 2) return hipErrorInvalidValue;
   const KgArgs a = kg_args(ent, rel, src, dst, ridx, neg, B, K, D, kind, corrupt, normalize);
   hipLaunchKernelGGL(kg_bwd_kernel, row_grid(B, a.lp), dim3(256), 0, s, a, gpos, gneg, dent, drel);
+  return hipGetLastError();
+}
+
+hipError_t eh_sgns_fwd_idx(const float* T, const int64_t* tmap, int64_t nTm, const int64_t* tinv, int64_t nT,
+                           const float* C, const int64_t* cmap, int64_t nCm, const int64_t* cinv, int64_t nC,
+                           int64_t P, int K, int D,
+                           float gscale, float* coef, float* loss_rows, hipStream_t s) {
+  if (P == 0) return hipSuccess;
+  if (D % 4 != 0 || D / 4 > 64 || K < 0) return hipErrorInvalidValue;
+  const int lp = row_lanes(D / 4);
+  hipLaunchKernelGGL(sgns_fwd_idx_kernel, row_grid(P, lp), dim3(256), 0, s, T, tmap, nTm, tinv, nT, C, cmap, nCm, cinv, nC,
+                     P, K,
+                     D, lp, gscale, coef, loss_rows);
+  return hipGetLastError();
+}
+
+hipError_t eh_occ_fill(const int64_t* inv, int64_t n, const int64_t* ptr, int* cursor, int* list, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(occ_fill_kernel, dim3(static_cast<uint32_t>(ceil_div(n, 256))), dim3(256), 0, s, inv, n, ptr,
+                     cursor, list);
+  return hipGetLastError();
+}
+
+hipError_t eh_sgns_update(int side, int64_t n_u, const int64_t* ptr, const int* list, const float* coef, int64_t P,
+                          int K, int D, const float* src, int64_t n_src, const int64_t* smap, int64_t n_smap,
+                          const int64_t* sinv, float* gout, float* table, float* m, float* v, const int64_t* rows, int64_t n_rows,
+                          int64_t* step, float lr, float b1, float b2, float eps, int kind, hipStream_t s) {
+  if (D % 4 != 0 || D / 4 > 64 || (side != 0 && side != 1) || (side == 1 && K < 0) || kind < 0 || kind > 2)
+    return hipErrorInvalidValue;
+  if (!gout) hipLaunchKernelGGL(sgns_step_inc_kernel, dim3(1), dim3(1), 0, s, step);
+  if (n_u == 0) return hipGetLastError();
+  SgnsUpd a;
+  a.ptr = ptr;
+  a.list = list;
+  a.coef = coef;
+  a.src = src;
+  a.smap = smap;
+  a.sinv = sinv;
+  a.gout = gout;
+  a.table = table;
+  a.m = m;
+  a.v = v;
+  a.rows = rows;
+  a.step = step;
+  a.n_u = n_u;
+  a.P = P;
+  a.n_rows = n_rows;
+  a.n_src = n_src;
+  a.n_smap = n_smap;
+  a.K = K;
+  a.D = D;
+  a.lp = row_lanes(D / 4);
+  a.side = side;
+  a.kind = kind;
+  a.lr = lr;
+  a.b1 = b1;
+  a.b2 = b2;
+  a.eps = eps;
+  hipLaunchKernelGGL(sgns_update_kernel, row_grid(n_u, a.lp), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

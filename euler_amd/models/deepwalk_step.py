@@ -11,12 +11,18 @@ One step here, per rank (no autograd, no dense table gradient):
 
   1. walks    : ``random_walk_kernel`` from ``batch`` alias-sampled start nodes
   2. pairs    : skip-gram (centre, context) pairs of every walk; negatives per pair
-  3. unique   : hash-table unique of the centre ids and of the context+negative ids
-  4. lookup   : ShardedTable.lookup — RCCL all-to-all of ids and rows (world > 1)
-  5. loss     : gather rows per pair, fused dot + sigmoid-CE fwd/bwd (embed.hip K11)
-  6. grads    : per-unique-row gradient sums (index_add_rows kernel)
-  7. update   : ShardedTable.apply — all-to-all of row grads to the owners, merge,
-                row-sparse Adam (optim.hip) on the owner's shard
+  3. unique   : hash-table unique of the centre ids and of the context+negative ids,
+                plus the occurrence lists of every unique id (occ_csr)
+  4. loss     : ``sgns_fwd_idx`` — logits straight from the table rows through the two-level
+                (occurrence -> unique id -> row) index; emits only coef = dloss/dlogit
+  5. update   : per unique row, the gradient is rebuilt from its occurrence list and
+                applied in place (``sgns_update``: row-sparse Adam/Adagrad/SGD) — no
+                per-pair gradient rows, no zero-filled accumulator, no float atomics.
+                Target rows are updated first from the (not yet updated) context table;
+                the context update reads a copy of the pre-update target rows.
+     world > 1: rows come from ShardedTable.lookup (RCCL all-to-all), ``sgns_grad`` builds
+                the per-unique-row gradients from the looked-up rows and
+                ShardedTable.apply sends them to the owners.
 
 Padding: a walk that hits a node without out-edges continues with the pad row
 ``num_nodes`` (the reference's ``max_id + 1`` default node).
@@ -40,8 +46,7 @@ def _pair_positions(walk_len, left, right):
 
 class DeepWalkTrainer:
     def __init__(self, graph, num_nodes, dim=128, walk_len=3, left_win_size=1, right_win_size=1, num_negs=5,
-                 batch_size=1024, lr=0.01, optimizer="adam", group=None, seed=0, emb_dtype=torch.float32,
-                 force_comm=False):
+                 batch_size=1024, lr=0.01, optimizer="adam", group=None, seed=0, force_comm=False):
         self.graph = graph
         self.num_nodes = int(num_nodes)
         self.pad = self.num_nodes  # rows: num_nodes + 1 (pad row like the reference's max_id + 1)
@@ -55,22 +60,12 @@ class DeepWalkTrainer:
         pi, pj = _pair_positions(walk_len, left_win_size, right_win_size)
         self.pi, self.pj = pi.to(dev), pj.to(dev)
         self.pairs_per_walk = int(pi.numel())
-        self.emb_dtype = emb_dtype
         self.loss = torch.zeros((), device=dev)
 
     def _gather(self, rows, inv):
         if use_hip(rows, inv):
             return hip().gather_rows(rows, inv.contiguous())
         return rows[inv]
-
-    def _grad_rows(self, n, inv, g):
-        acc = torch.zeros(n, self.dim, dtype=torch.float32, device=g.device)
-        g2 = g.reshape(-1, self.dim).float().contiguous()
-        if use_hip(acc, inv, g2):
-            hip().index_add_rows_(acc, inv.reshape(-1).contiguous(), g2)
-        else:
-            acc.index_add_(0, inv.reshape(-1), g2)
-        return acc
 
     def sample(self):
         """(centre [P], positive [P], negatives [P, K]) global ids of one step."""
@@ -87,32 +82,28 @@ class DeepWalkTrainer:
     def step(self):
         src, pos, negs = self.sample()
         P, K = src.numel(), self.num_negs
+        gscale = 1.0 / (P * (1 + K))
         # unique ids per table (first-occurrence order; hash kernel on the GPU)
         u_t, inv_t = gnn_ops.unique_first(src)
         u_c, inv_c = gnn_ops.unique_first(torch.cat([pos, negs.reshape(-1)]))
-        rows_t, h_t = self.target.lookup(u_t)
-        rows_c, h_c = self.context.lookup(u_c)
-        rt, rc = rows_t.to(self.emb_dtype), rows_c.to(self.emb_dtype)
-        emb = self._gather(rt, inv_t)                                       # [P, D]
-        pos_rows = self._gather(rc, inv_c[:P]).view(P, 1, self.dim)         # [P, 1, D]
-        neg_rows = self._gather(rc, inv_c[P:]).view(P, K, self.dim)         # [P, K, D]
-        if use_hip(emb, pos_rows, neg_rows):
-            logits, loss_rows = hip().sgns_fwd(emb, pos_rows, neg_rows)
-            demb, dpos, dneg = hip().sgns_bwd(emb, pos_rows, neg_rows, logits, 1.0 / (P * (1 + K)))
-            self.loss = loss_rows.sum() / (P * (1 + K))
+        ptr_t, lst_t = gnn_ops.occ_csr(inv_t, u_t.numel())
+        ptr_c, lst_c = gnn_ops.occ_csr(inv_c, u_c.numel())
+        T, C = self.target, self.context
+        if T.fused_sgns_ok(u_t) and C.fused_sgns_ok(u_c):
+            # one rank owns every row: local row == global id
+            coef, loss_rows = gnn_ops.sgns_fwd_idx(T.weight, u_t, inv_t, C.weight, u_c, inv_c, K, gscale)
+            rt = self._gather(T.weight, u_t)                # pre-update target rows
+            T.apply_sgns(0, ptr_t, lst_t, coef, K, C.weight, u_c, inv_c, u_t)
+            C.apply_sgns(1, ptr_c, lst_c, coef, K, rt, None, inv_t, u_c)
         else:
-            e = emb.float().requires_grad_(True)
-            p_ = pos_rows.float().requires_grad_(True)
-            n_ = neg_rows.float().requires_grad_(True)
-            loss, _, _ = gnn_ops.sgns_loss_reference(e, p_, n_)
-            demb, dpos, dneg = torch.autograd.grad(loss, (e, p_, n_))
-            self.loss = loss.detach()
-        g_t = self._grad_rows(u_t.numel(), inv_t, demb)
-        # inv_c is ordered [positives (P), negatives (P*K)]: stack the grads the same way
-        g_c = self._grad_rows(u_c.numel(), inv_c,
-                              torch.cat([dpos.reshape(P, self.dim), dneg.reshape(P * K, self.dim)], 0))
-        self.target.apply(h_t, g_t)
-        self.context.apply(h_c, g_c)
+            rows_t, h_t = T.lookup(u_t)
+            rows_c, h_c = C.lookup(u_c)
+            coef, loss_rows = gnn_ops.sgns_fwd_idx(rows_t, None, inv_t, rows_c, None, inv_c, K, gscale)
+            g_t = gnn_ops.sgns_grad(0, ptr_t, lst_t, coef, K, rows_c, None, inv_c, inv_self=inv_t)
+            g_c = gnn_ops.sgns_grad(1, ptr_c, lst_c, coef, K, rows_t, None, inv_t, inv_self=inv_c)
+            T.apply(h_t, g_t)
+            C.apply(h_c, g_c)
+        self.loss = loss_rows.sum() * gscale
         return self.loss
 
     def pairs_per_step(self):

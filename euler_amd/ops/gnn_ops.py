@@ -30,7 +30,7 @@ from euler_amd.ops.mp_ops import SegmentIndex
 
 __all__ = ["EdgeCSR", "gat_aggregate", "gat_aggregate_reference", "RelationTiles", "relation_transform",
            "relation_transform_reference", "sgns_loss", "sgns_loss_reference", "kg_score", "kg_score_reference",
-           "unique_first", "KG_KINDS", "KG_CORRUPT"]
+           "unique_first", "KG_KINDS", "KG_CORRUPT", "sgns_fwd_idx", "occ_csr", "sgns_grad"]
 
 
 # ----------------------------------------------------------------------------- edge structures
@@ -423,6 +423,77 @@ def sgns_loss(emb, pos, neg):
         return loss, logits[:, :P], logits[:, P:]
     loss, lp, ln = sgns_loss_reference(e2, pos, neg)
     return loss, lp.detach(), ln.detach()
+
+
+# ----------------------------------------------------------------------------- K11b index-driven SGNS
+# One skip-gram step over de-duplicated ids without per-pair gradient rows (DeepWalk /
+# LINE; embed.hip sgns_fwd_idx / sgns_update).  P pairs, each one positive and K
+# negatives; ``tinv`` [P] / ``cinv`` [P*(1+K)] (positives then negatives) index the unique
+# target / context ids, ``tmap`` / ``cmap`` map unique ids to table rows (None: identity).
+
+def _rows(table, map_, inv):
+    idx = inv if map_ is None else map_[inv]
+    return table[idx]
+
+
+def sgns_fwd_idx(T, tmap, tinv, C, cmap, cinv, K, gscale):
+    """``(coef [P, 1+K], loss_rows [P])``: coef = (sigmoid(logit) - label) * gscale, the
+    loss gradient of each logit; loss_rows the per-pair sigmoid-CE sums."""
+    if use_hip(T, tinv, C, cinv):
+        return tuple(hip().sgns_fwd_idx(T.contiguous(), tmap, tinv.contiguous(), C.contiguous(), cmap,
+                                        cinv.contiguous(), int(K), float(gscale)))
+    P = tinv.numel()
+    e = _rows(T, tmap, tinv).float()
+    c = _rows(C, cmap, cinv).float()
+    ctx = torch.cat([c[:P].view(P, 1, -1), c[P:].view(P, K, -1)], 1)
+    x = torch.einsum("pd,psd->ps", e, ctx)
+    y = torch.zeros_like(x)
+    y[:, 0] = 1.0
+    loss = F.binary_cross_entropy_with_logits(x, y, reduction="none").sum(1)
+    return (torch.sigmoid(x) - y) * gscale, loss
+
+
+def occ_csr(inv, n_u):
+    """occurrence lists of ``inv`` (values in [0, n_u)): ``(ptr [n_u+1] int64, list int32)``."""
+    inv = inv.reshape(-1).long()
+    if use_hip(inv):
+        return tuple(hip().occ_csr(inv.contiguous(), int(n_u)))
+    cnt = torch.bincount(inv, minlength=n_u)
+    ptr = torch.zeros(n_u + 1, dtype=torch.long, device=inv.device)
+    ptr[1:] = torch.cumsum(cnt, 0)
+    return ptr, torch.argsort(inv, stable=True).int()
+
+
+def _ctx_occ_pairs(P, K, device):
+    """(pair, slot) of every context occurrence, in cinv order."""
+    pos = torch.arange(P, device=device)
+    q = torch.arange(P * K, device=device)
+    return torch.cat([pos, q // max(K, 1)]), torch.cat([torch.zeros_like(pos), 1 + q % max(K, 1)])
+
+
+def sgns_grad_reference(side, coef, K, src, smap, sinv, n_u, inv_self):
+    P = coef.shape[0]
+    D = src.shape[1]
+    if side == 0:   # target u: sum over its pairs of sum_s coef[p, s] * C[ctx(p, s)]
+        c = _rows(src, smap, sinv).float()
+        ctx = torch.cat([c[:P].view(P, 1, D), c[P:].view(P, K, D)], 1)
+        per = torch.einsum("ps,psd->pd", coef, ctx)
+    else:           # context occurrence (p, s): coef[p, s] * E[tgt(p)]
+        e = _rows(src, smap, sinv).float()
+        pp, ss = _ctx_occ_pairs(P, K, coef.device)
+        per = coef[pp, ss].unsqueeze(1) * e[pp]
+    return torch.zeros(n_u, D, dtype=torch.float32, device=src.device).index_add_(0, inv_self.reshape(-1), per)
+
+
+def sgns_grad(side, ptr, lst, coef, K, src, smap, sinv, inv_self=None):
+    """per-unique-row gradient ``[n_u, D]`` of one table (side 0 target, 1 context),
+    rebuilt from the occurrence lists (no per-pair rows, no atomics).  ``inv_self`` (this
+    side's inverse) is only read by the CPU composition."""
+    n_u = ptr.numel() - 1
+    if use_hip(coef, src):
+        return hip().sgns_grad(int(side), ptr, lst, coef.contiguous(), int(K), src.contiguous(), smap,
+                               sinv.contiguous())
+    return sgns_grad_reference(side, coef, K, src, smap, sinv, n_u, inv_self)
 
 
 # ----------------------------------------------------------------------------- K10 KG scores

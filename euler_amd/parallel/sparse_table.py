@@ -138,6 +138,18 @@ class ShardedTable:
         else:
             self.weight[rows] -= self.lr * g
 
+    def fused_sgns_ok(self, *tensors):
+        """True when a skip-gram update can be applied in place by the fused kernel
+        (one rank owns every row, GPU tensors, D % 4 == 0)."""
+        return not self.comm and use_hip(self.weight, *tensors) and self.dim % 4 == 0 and self.dim <= 256
+
+    def apply_sgns(self, side, ptr, lst, coef, K, src, smap, sinv, ids):
+        """fused row-sparse update from occurrence lists (embed.hip sgns_update, see
+        gnn_ops.sgns_grad): gradients of the unique ids ``ids`` are rebuilt and applied
+        in one pass, no gradient rows are materialised.  Requires :meth:`fused_sgns_ok`."""
+        hip().sgns_apply_(int(side), ptr, lst, coef, int(K), src, smap, sinv, self.weight, self.m, self.v,
+                          ids.contiguous(), self.step, self.lr, self.b1, self.b2, self.eps, self.kind)
+
     def global_ids(self):
         return torch.arange(self.weight.shape[0], device=self.device) * self.world + self.rank
 

@@ -277,3 +277,88 @@ def test_weighted_aggregate_spmm(cuda, dtype, D):
     tol = dict(atol=3e-2, rtol=3e-2) if dtype == torch.bfloat16 else dict(atol=1e-4, rtol=1e-4)
     torch.testing.assert_close(out.float(), ref, **tol)
     torch.testing.assert_close(x.grad.float(), x2.grad, **tol)
+
+
+# ----------------------------------------------------------------------------- index-driven SGNS
+def _sgns_case(device, P=300, K=5, D=32, n_t=40, n_c=120, seed=21):
+    g = torch.Generator().manual_seed(seed)
+    T = torch.randn(n_t + 7, D, generator=g).to(device)
+    C = torch.randn(n_c + 9, D, generator=g).to(device)
+    src = torch.randint(0, n_t, (P,), generator=g).to(device)
+    ctx = torch.randint(0, n_c, (P * (1 + K),), generator=g).to(device)
+    return T, C, src, ctx
+
+
+def _sgns_autograd(T, C, src, ctx, K):
+    P = src.numel()
+    Tg = T.detach().clone().requires_grad_(True)
+    Cg = C.detach().clone().requires_grad_(True)
+    c = Cg[ctx]
+    loss, _, _ = G.sgns_loss_reference(Tg[src], c[:P].view(P, 1, -1), c[P:].view(P, K, -1))
+    loss.backward()
+    return loss.detach(), Tg.grad, Cg.grad
+
+
+def test_sgns_idx_reference_matches_autograd():
+    K = 5
+    T, C, src, ctx = _sgns_case("cpu", K=K)
+    P = src.numel()
+    u_t, inv_t = G.unique_first(src)
+    u_c, inv_c = G.unique_first(ctx)
+    gscale = 1.0 / (P * (1 + K))
+    coef, loss_rows = G.sgns_fwd_idx(T, u_t, inv_t, C, u_c, inv_c, K, gscale)
+    ptr_t, lst_t = G.occ_csr(inv_t, u_t.numel())
+    ptr_c, lst_c = G.occ_csr(inv_c, u_c.numel())
+    g_t = G.sgns_grad(0, ptr_t, lst_t, coef, K, C, u_c, inv_c, inv_self=inv_t)
+    g_c = G.sgns_grad(1, ptr_c, lst_c, coef, K, T, u_t, inv_t, inv_self=inv_c)
+    loss, dT, dC = _sgns_autograd(T, C, src, ctx, K)
+    torch.testing.assert_close(loss_rows.sum() * gscale, loss, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(g_t, dT[u_t], atol=1e-6, rtol=1e-5)
+    torch.testing.assert_close(g_c, dC[u_c], atol=1e-6, rtol=1e-5)
+    # occurrence lists: every occurrence once, grouped by its unique id
+    assert torch.equal(torch.sort(lst_c.long())[0], torch.arange(ctx.numel()))
+    assert torch.equal(inv_c[lst_c.long()], torch.repeat_interleave(torch.arange(u_c.numel()), ptr_c.diff()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["adam", "adagrad", "sgd"])
+def test_sgns_idx_kernels_match_cpu(cuda, kind):
+    from euler_amd.parallel.sparse_table import ShardedTable
+
+    K, D = 5, 64
+    T, C, src, ctx = _sgns_case("cpu", P=2000, K=K, D=D, n_t=300, n_c=900, seed=22)
+    P = src.numel()
+    gscale = 1.0 / (P * (1 + K))
+    u_t, inv_t = G.unique_first(src)
+    u_c, inv_c = G.unique_first(ctx)
+    coef, loss_rows = G.sgns_fwd_idx(T, u_t, inv_t, C, u_c, inv_c, K, gscale)
+    _, dT, dC = _sgns_autograd(T, C, src, ctx, K)
+    dv = [t.to(cuda) for t in (T, C, src, ctx)]
+    Tg, Cg, srcg, ctxg = dv
+    ug_t, ig_t = G.unique_first(srcg)
+    ug_c, ig_c = G.unique_first(ctxg)
+    assert torch.equal(ug_t.cpu(), u_t) and torch.equal(ig_c.cpu(), inv_c)
+    coef_g, loss_g = G.sgns_fwd_idx(Tg, ug_t, ig_t, Cg, ug_c, ig_c, K, gscale)
+    torch.testing.assert_close(coef_g.cpu(), coef, atol=1e-7, rtol=1e-4)
+    torch.testing.assert_close(loss_g.cpu(), loss_rows, atol=1e-4, rtol=1e-5)
+    ptr_t, lst_t = G.occ_csr(ig_t, ug_t.numel())
+    ptr_c, lst_c = G.occ_csr(ig_c, ug_c.numel())
+    assert torch.equal(torch.sort(lst_c.long())[0].cpu(), torch.arange(ctx.numel()))
+    g_t = G.sgns_grad(0, ptr_t, lst_t, coef_g, K, Cg, ug_c, ig_c)
+    g_c = G.sgns_grad(1, ptr_c, lst_c, coef_g, K, Tg, ug_t, ig_t)
+    torch.testing.assert_close(g_t.cpu(), dT[u_t], atol=1e-7, rtol=1e-4)
+    torch.testing.assert_close(g_c.cpu(), dC[u_c], atol=1e-7, rtol=1e-4)
+    # fused in-place optimizer == plain optimizer on the reference gradients
+    n_rows = C.shape[0]
+    fused = ShardedTable(n_rows, D, cuda, optimizer=kind, lr=0.05, seed=3)
+    plain = ShardedTable(n_rows, D, "cpu", optimizer=kind, lr=0.05, seed=3)
+    plain.weight.copy_(fused.weight.cpu())
+    for _ in range(2):
+        fused.apply_sgns(1, ptr_c, lst_c, coef_g, K, Tg, ug_t, ig_t, ug_c)
+        plain._update(u_c, dC[u_c])
+    # Adam / Adagrad normalise each gradient element (g / (|g| + eps) on the first step), so
+    # elements whose gradient cancels to ~eps amplify the 1e-4 relative gradient differences
+    torch.testing.assert_close(fused.weight.cpu(), plain.weight, atol=1e-3 if kind != "sgd" else 1e-5, rtol=1e-4)
+    if kind != "sgd":
+        torch.testing.assert_close(fused.v.cpu(), plain.v, atol=1e-9, rtol=1e-3)
+    assert int(fused.step.item()) == 2
