@@ -187,21 +187,32 @@ __global__ __launch_bounds__(256) void sgns_fwd_idx_kernel(const float* __restri
                                                            float* __restrict__ loss_rows) {
   const RowLane L = row_lane(lp, P);
   const bool ok = L.ok && L.sub * 4 < D;
+  const int d = L.sub * 4;
   float e[4] = {0.f, 0.f, 0.f, 0.f};
-  if (ok) load_row4(T, occ_row(tmap, nTm, tinv, L.row, nT), D, L.sub * 4, e);
+  if (ok) load_row4(T, occ_row(tmap, nTm, tinv, L.row, nT), D, d, e);
   float loss = 0.f;
-  for (int s = 0; s <= K; ++s) {
-    float part = 0.f;
-    if (ok) {
-      float c[4];
-      load_row4(C, occ_row(cmap, nCm, cinv, ctx_occ(L.row, s, P, K), nC), D, L.sub * 4, c);
+  // SG context rows per round: their index chains and row loads are all in flight together
+  constexpr int SG = 4;
+  for (int s0 = 0; s0 <= K; s0 += SG) {
+    int64_t r[SG];
+    float c[SG][4];
 #pragma unroll
-      for (int v = 0; v < 4; ++v) part += e[v] * c[v];
+    for (int j = 0; j < SG; ++j)
+      r[j] = ok && s0 + j <= K ? occ_row(cmap, nCm, cinv, ctx_occ(L.row, s0 + j, P, K), nC) : -1;
+#pragma unroll
+    for (int j = 0; j < SG; ++j) load_row4(C, r[j], D, d, c[j]);
+#pragma unroll
+    for (int j = 0; j < SG; ++j) {
+      const int s = s0 + j;
+      if (s > K) break;  // uniform across the group
+      float part = 0.f;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) part += e[v] * c[j][v];
+      const float x = emb_group_sum(part, lp);
+      const float y = s == 0 ? 1.f : 0.f;
+      loss += sigmoid_ce(x, y);
+      if (L.ok && L.sub == 0) coef[L.row * (K + 1) + s] = (sigmoidf(x) - y) * gscale;
     }
-    const float x = emb_group_sum(part, lp);
-    const float y = s == 0 ? 1.f : 0.f;
-    loss += sigmoid_ce(x, y);
-    if (L.ok && L.sub == 0) coef[L.row * (K + 1) + s] = (sigmoidf(x) - y) * gscale;
   }
   if (L.ok && L.sub == 0) loss_rows[L.row] = loss;
 }
@@ -238,51 +249,69 @@ __global__ __launch_bounds__(256) void sgns_update_kernel(SgnsUpd a) {
   const RowLane L = row_lane(a.lp, a.n_u);
   if (!L.ok || L.sub * 4 >= a.D) return;  // no cross-lane exchange
   const int d = L.sub * 4;
+  // the table row, its slots and the occurrence range are loaded first, so their latency
+  // overlaps the dependent index chain of the gradient below
+  const bool apply = a.gout == nullptr;
+  int64_t r = -1;
+  float4_t p{}, mi{}, vi{};
+  if (apply) {
+    r = a.rows ? a.rows[L.row] : L.row;
+    if (r < 0 || r >= a.n_rows) return;
+    const int64_t off = r * a.D + d;
+    p = *reinterpret_cast<const float4_t*>(a.table + off);
+    if (a.kind != 2) vi = *reinterpret_cast<const float4_t*>(a.v + off);
+    if (a.kind == 0) mi = *reinterpret_cast<const float4_t*>(a.m + off);
+  }
   float g[4] = {0.f, 0.f, 0.f, 0.f};
   const int64_t beg = a.ptr[L.row], end = a.ptr[L.row + 1];
   const int KK = a.K + 1;
+  constexpr int SG = 4;
   for (int64_t i = beg; i < end; ++i) {
     const int64_t o = a.list[i];
     if (a.side == 0) {
-      // target occurrence o is pair o: all of its context rows
-      for (int s = 0; s < KK; ++s) {
-        float c[4];
-        const float w = a.coef[o * KK + s];
-        load_row4(a.src, occ_row(a.smap, a.n_smap, a.sinv, ctx_occ(o, s, a.P, a.K), a.n_src), a.D, d, c);
+      // target occurrence o is pair o: all of its context rows, SG at a time
+      for (int s0 = 0; s0 < KK; s0 += SG) {
+        int64_t rr[SG];
+        float c[SG][4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) g[k] += w * c[k];
+        for (int j = 0; j < SG; ++j)
+          rr[j] = s0 + j < KK ? occ_row(a.smap, a.n_smap, a.sinv, ctx_occ(o, s0 + j, a.P, a.K), a.n_src) : -1;
+#pragma unroll
+        for (int j = 0; j < SG; ++j) load_row4(a.src, rr[j], a.D, d, c[j]);
+#pragma unroll
+        for (int j = 0; j < SG; ++j) {
+          const float w = s0 + j < KK ? a.coef[o * KK + s0 + j] : 0.f;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) g[k] += w * c[j][k];
+        }
       }
     } else {
       // context occurrence o -> (pair, slot)
-      int64_t p;
+      int64_t pp;
       int s;
       if (o < a.P) {
-        p = o;
+        pp = o;
         s = 0;
       } else {
         const int64_t q = o - a.P;
-        p = q / a.K;
-        s = 1 + static_cast<int>(q - p * a.K);
+        pp = q / a.K;
+        s = 1 + static_cast<int>(q - pp * a.K);
       }
       float e[4];
-      const float w = a.coef[p * KK + s];
-      load_row4(a.src, occ_row(a.smap, a.n_smap, a.sinv, p, a.n_src), a.D, d, e);
+      const float w = a.coef[pp * KK + s];
+      load_row4(a.src, occ_row(a.smap, a.n_smap, a.sinv, pp, a.n_src), a.D, d, e);
 #pragma unroll
       for (int k = 0; k < 4; ++k) g[k] += w * e[k];
     }
   }
-  if (a.gout) {
+  if (!apply) {
     EV<float>::store(a.gout + L.row * a.D + d, g);
     return;
   }
-  const int64_t r = a.rows ? a.rows[L.row] : L.row;
-  if (r < 0 || r >= a.n_rows) return;
   const int64_t off = r * a.D + d;
-  float4_t p = *reinterpret_cast<float4_t*>(a.table + off);
   if (a.kind == 0) {
     const float st = static_cast<float>(a.step[0]);
     const float bc1 = 1.f - __powf(a.b1, st), bc2 = 1.f - __powf(a.b2, st);
-    float4_t mi = *reinterpret_cast<float4_t*>(a.m + off), vi = *reinterpret_cast<float4_t*>(a.v + off);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       mi[k] = a.b1 * mi[k] + (1.f - a.b1) * g[k];
@@ -292,13 +321,12 @@ __global__ __launch_bounds__(256) void sgns_update_kernel(SgnsUpd a) {
     *reinterpret_cast<float4_t*>(a.m + off) = mi;
     *reinterpret_cast<float4_t*>(a.v + off) = vi;
   } else if (a.kind == 1) {
-    float4_t acc = *reinterpret_cast<float4_t*>(a.v + off);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      acc[k] += g[k] * g[k];
-      p[k] -= a.lr * g[k] / (sqrtf(acc[k]) + a.eps);
+      vi[k] += g[k] * g[k];
+      p[k] -= a.lr * g[k] / (sqrtf(vi[k]) + a.eps);
     }
-    *reinterpret_cast<float4_t*>(a.v + off) = acc;
+    *reinterpret_cast<float4_t*>(a.v + off) = vi;
   } else {
 #pragma unroll
     for (int k = 0; k < 4; ++k) p[k] -= a.lr * g[k];
