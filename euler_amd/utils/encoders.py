@@ -20,6 +20,7 @@ import torch
 import torch.nn as nn
 
 from euler_amd.ops import graph_api as G
+from euler_amd.parallel.replicated import apply_replicated, sync_group
 from euler_amd.utils import aggregators as dense_aggs
 from euler_amd.utils import sparse_aggregators
 from euler_amd.utils.layers import (AttLayer, Dense, Embedding, HashEmbedding, HashSparseEmbedding, SparseEmbedding)
@@ -247,7 +248,7 @@ class _StoreMixin:
         for i in range(self._num_stores):
             gs = self.gradient_stores(i)
             g = gs[rows].clone()
-            gs.index_fill_(0, rows, 0.0)
+            gs.index_fill_(0, rows, 0.0)  # the other ranks zero these rows in after_backward
             losses.append((node_embeddings[i] * g.to(node_embeddings[i].dtype)).sum())
         self.store_loss = sum(losses) if losses else torch.zeros((), device=rows.device)
         self._pending = (rows, [e.detach() for e in node_embeddings[:self._num_stores]], self._rows(neighbor),
@@ -259,11 +260,19 @@ class _StoreMixin:
         if self._pending is None:
             return
         rows, embs, nrows, leaves = self._pending
+        # data parallel: every rank applies every rank's writes (parallel/replicated.py), so
+        # the replicas behave like the reference's shared PS stores
+        group = getattr(self, "store_group", None)
+        synced = sync_group(group) is not None
         for i in range(self._num_stores):
-            self.stores(i).index_copy_(0, rows, embs[i].to(self.stores(i).dtype))
+            if synced:
+                apply_replicated(self.gradient_stores(i), rows, None, "zero", group)
+            apply_replicated(self.stores(i), rows, embs[i], "copy", group)
         for i, leaf in enumerate(leaves):
-            if leaf.grad is not None:
-                self.gradient_stores(i).index_add_(0, nrows, leaf.grad.reshape(nrows.numel(), -1).float())
+            grad = leaf.grad if leaf.grad is not None else torch.zeros_like(leaf)
+            if leaf.grad is not None or synced:  # ranks must join the same collectives
+                apply_replicated(self.gradient_stores(i), nrows, grad.reshape(nrows.numel(), -1).float(), "add",
+                                 group)
         self._pending = None
 
 

@@ -209,3 +209,38 @@ def test_deepwalk_sharded_two_ranks():
     res = _run(_worker_deepwalk)
     assert not [r for r in res if r[1] == "error"], res
     assert len(res) == 2 and all(r[2] for r in res), res
+
+
+def _worker_replicated_store(rank, world, port, q):
+    try:
+        _init(rank, world, port)
+        from euler_amd.parallel.replicated import apply_replicated
+
+        store = torch.zeros(10, 3)
+        grads = torch.zeros(10, 3)
+        # rank r writes rows {r, 5} (row 5 shared: the higher rank wins) and adds to rows {7, 8 + r}
+        rows = torch.tensor([rank, 5])
+        vals = torch.full((2, 3), float(rank + 1))
+        apply_replicated(store, rows, vals, "copy")
+        apply_replicated(grads, torch.tensor([7, 8 + rank]), torch.ones(2, 3), "add")
+        exp = torch.zeros(10, 3)
+        for r in range(world):
+            exp[r] = r + 1
+        exp[5] = world
+        eg = torch.zeros(10, 3)
+        eg[7] = world
+        for r in range(world):
+            eg[min(8 + r, 9)] += 1
+        apply_replicated(grads, torch.tensor([9]), None, "zero") if rank == 0 else \
+            apply_replicated(grads, torch.empty(0, dtype=torch.long), None, "zero")
+        eg[9] = 0
+        q.put((rank, "replicated", bool(torch.equal(store, exp) and torch.equal(grads, eg))))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, "error", repr(e)))
+
+
+def test_replicated_store_writes_reach_every_rank():
+    res = _run(_worker_replicated_store)
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == 2 and all(r[2] for r in res), res
