@@ -188,7 +188,7 @@ void rel_gemm(torch::Tensor A, torch::Tensor a_idx, torch::Tensor trel, torch::T
 
 void rel_gemm_dw(torch::Tensor G, torch::Tensor g_idx, torch::Tensor X, torch::Tensor x_idx,
                  c10::optional<torch::Tensor> scale, torch::Tensor trel, torch::Tensor tstart, torch::Tensor tlen,
-                 torch::Tensor dW) {
+                 c10::optional<torch::Tensor> solo, torch::Tensor dW) {
   typed(G, torch::kBFloat16, "G");
   typed(X, torch::kBFloat16, "X");
   typed(g_idx, torch::kInt32, "g_idx");
@@ -204,11 +204,16 @@ void rel_gemm_dw(torch::Tensor G, torch::Tensor g_idx, torch::Tensor X, torch::T
     typed(*scale, torch::kFloat32, "scale");
     TORCH_CHECK(scale->numel() == g_idx.numel(), "scale must be per edge");
   }
+  if (solo.has_value()) {
+    typed(*solo, torch::kInt32, "solo");
+    TORCH_CHECK(solo->numel() == trel.numel(), "solo must hold one flag per chunk");
+  }
   const c10::DeviceGuard g(G.device());
   ok(eh_rel_gemm_dw(G.data_ptr(), static_cast<int>(N), g_idx.data_ptr<int32_t>(), X.data_ptr(), static_cast<int>(K),
                     x_idx.data_ptr<int32_t>(), scale.has_value() ? scale->data_ptr<float>() : nullptr,
                     trel.data_ptr<int32_t>(), tstart.data_ptr<int32_t>(), tlen.data_ptr<int32_t>(),
-                    static_cast<int>(trel.numel()), dW.data_ptr<float>(), stream()),
+                    solo.has_value() ? solo->data_ptr<int32_t>() : nullptr, static_cast<int>(trel.numel()),
+                    dW.data_ptr<float>(), stream()),
      "rel_gemm_dw");
 }
 

@@ -106,7 +106,7 @@ hipError_t eh_rel_gemm(const void* A, int K, const int32_t* a_idx, const int32_t
                        const int32_t* o_idx, int mode, void* Y, hipStream_t s);
 hipError_t eh_rel_gemm_dw(const void* G, int N, const int32_t* g_idx, const void* X, int K, const int32_t* x_idx,
                           const float* scale, const int32_t* crel, const int32_t* cstart, const int32_t* clen,
-                          int n_chunks, float* dW, hipStream_t s);
+                          const int32_t* csolo, int n_chunks, float* dW, hipStream_t s);
 
 // embed.hip (K10 knowledge-graph scores, K11 skip-gram sigmoid-CE)
 hipError_t eh_sgns_fwd(const void* emb, const void* pos, const void* neg, int is_bf16, int64_t B, int P, int K, int D,

@@ -12,8 +12,9 @@
 //   rel_gemm    : Y[o_idx[e]] (+)= scale[e] * A[a_idx[e]] @ B[rel]^T
 //                 forward  (A = x,    B = W  [R][N][K], o = dst)
 //                 backward (A = dout, B = W^T [R][K][N], o = src)  -> dx
-//   rel_gemm_dw : dW[rel] += sum_e (scale[e] * G[g_idx[e]])^T X[x_idx[e]]  (per-tile
-//                 outer-product GEMM over the 64 edges, fp32 atomics into [R][N][K])
+//   rel_gemm_dw : dW[rel] += sum_e (scale[e] * G[g_idx[e]])^T X[x_idx[e]]  (per-chunk
+//                 outer-product GEMM, fragments by transposing LDS reads; a relation's
+//                 only chunk stores its slab, longer relations add with fp32 atomics)
 #include "hip/common.h"
 #include "hip/launchers.h"
 
@@ -116,12 +117,38 @@ __global__ __launch_bounds__(256) void rel_gemm_kernel(const bf16_t* __restrict_
   }
 }
 
-// dW for one (chunk of <= RG_CH edges of ONE relation, 64 x 64 slab of dW[rel]) per workgroup:
-// the chunk's 64-edge sub-tiles are staged transposed in LDS and accumulated in registers
-// (wave w: slab rows w*16..+16, four 16-column fragments), so each dW element receives one
-// atomic per chunk instead of one per 64-edge tile (the atomics were the dW kernel's floor).
+// dW for one (chunk of <= RG_CH edges of ONE relation, T x T slab of dW[rel]) per workgroup:
+// the chunk's 64-edge sub-tiles are staged in LDS and accumulated in registers, so each dW
+// element receives one write per chunk instead of one atomic per 64-edge tile.
 constexpr int RG_CH = 1024;  // edges per dW chunk
 
+// MFMA fragments of dW = Gs^T X straight from edge-major LDS images with the gfx950
+// transposing read ds_read_b64_tr_b16: a 16-lane group reads a 4-edge x 16-column block and
+// lane i receives column i (4 edges).  Two reads give the 8 reduction elements of a lane:
+// group g takes edges e0 + 4g .. +3 and e0 + 16 + 4g .. +3 (A and B use the same edge map,
+// which is all the MFMA needs).  Images are [64 edges][T + 16] bf16: with a row stride of
+// 40 (T = 64) or 72 (T = 128) dwords the 8 rows a 32-lane half reads land on 8 disjoint
+// 8-bank sets (conflict-free), and the 16-byte row-segment stores of 8 consecutive lanes
+// cover the 32 banks once.
+typedef short rg_v4i16 __attribute__((ext_vector_type(4)));
+typedef uint32_t rg_u2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) rg_v4i16 rg_lds_v4i16;
+
+template <int LD>
+__device__ __forceinline__ uint4_t rg_tr_frag(const bf16_t* img, int e0, int c0, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const bf16_t* a = img + (e0 + 4 * g + (i >> 2)) * LD + c0 + 4 * (i & 3);
+  const rg_v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((rg_lds_v4i16*)(a));
+  const rg_v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((rg_lds_v4i16*)(a + 16 * LD));
+  const rg_u2 l2 = __builtin_bit_cast(rg_u2, lo), h2 = __builtin_bit_cast(rg_u2, hi);
+  return uint4_t{l2[0], l2[1], h2[0], h2[1]};
+}
+
+// one workgroup = one (chunk of <= RG_CH edges of one relation) x (T x T slab of dW[rel]);
+// T = 128 covers a 128 x 128 weight in one slab, so every edge row is read once.  Wave w
+// owns rows w*T/4 .. of the slab (T/64 MFMA row tiles) x all T columns (T/16 tiles).
+// A chunk that is its relation's only one (csolo) stores its slab; otherwise fp32 atomics.
+template <int T>
 __global__ __launch_bounds__(256) void rel_gemm_dw_kernel(const bf16_t* __restrict__ G, int N,
                                                           const int32_t* __restrict__ g_idx,
                                                           const bf16_t* __restrict__ X, int K,
@@ -129,32 +156,36 @@ __global__ __launch_bounds__(256) void rel_gemm_dw_kernel(const bf16_t* __restri
                                                           const float* __restrict__ scale,
                                                           const int32_t* __restrict__ crel,
                                                           const int32_t* __restrict__ cstart,
-                                                          const int32_t* __restrict__ clen, float* __restrict__ dW) {
-  constexpr int LDT = RG_BM + 8;  // transposed tiles: [col][edge], 144-byte rows
-  __shared__ __attribute__((aligned(16))) bf16_t gT[64 * LDT];
-  __shared__ __attribute__((aligned(16))) bf16_t xT[64 * LDT];
-  const int SN = N >> 6, SK = K >> 6;
+                                                          const int32_t* __restrict__ clen,
+                                                          const int32_t* __restrict__ csolo, float* __restrict__ dW) {
+  constexpr int LD = T + 16;
+  constexpr int FM = T / 64, FN = T / 16;
+  constexpr int CPR = T / 8;               // 16-byte chunks per row segment
+  constexpr int IT = RG_BM * CPR / 256;    // items per thread and operand
+  __shared__ __attribute__((aligned(16))) bf16_t gS[RG_BM * LD];
+  __shared__ __attribute__((aligned(16))) bf16_t xS[RG_BM * LD];
+  const int SN = N / T, SK = K / T;
   const int b = xcd_remap(blockIdx.x, gridDim.x);
   const int chunk = b / (SN * SK), s = b - chunk * (SN * SK);
   const int sn = s / SK, sk = s - sn * SK;
   const int r = crel[chunk], c0 = cstart[chunk], clen_ = clen[chunk];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int lr = lane & 15, lk = (lane >> 4) * 8;
-  float4_t acc[4];
+  float4_t acc[FM][FN];
 #pragma unroll
-  for (int f = 0; f < 4; ++f) acc[f] = float4_t{0.f, 0.f, 0.f, 0.f};
-  // item = (edge e = it & 63, 8-column chunk c = it >> 6): the 64 lanes of a wave take 64
-  // consecutive edges of one chunk, so the transposed LDS writes hit consecutive bytes
-  // (no bank conflicts); 2 items per thread and operand.  The next sub-tile's rows are
-  // loaded into registers while the MFMAs of the current one run.
-  uint4_t gv[2], xv[2];
-  float gs[2];
+  for (int m = 0; m < FM; ++m)
+#pragma unroll
+    for (int f = 0; f < FN; ++f) acc[m][f] = float4_t{0.f, 0.f, 0.f, 0.f};
+  // item = (edge e = it / CPR, 16-byte column chunk c = it % CPR): consecutive lanes move
+  // one row segment (coalesced loads, conflict-free LDS stores).  The next sub-tile's rows
+  // are loaded into registers while the current one's MFMAs run.
+  uint4_t gv[IT], xv[IT];
+  float gs[IT];
   auto prefetch = [&](int sub) {
     const int ne = min(RG_BM, clen_ - sub);
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < IT; ++h) {
       const int it = threadIdx.x + h * 256;
-      const int e = it & 63, c = it >> 6;
+      const int e = it / CPR, c = it % CPR;
       gv[h] = uint4_t{0u, 0u, 0u, 0u};
       xv[h] = uint4_t{0u, 0u, 0u, 0u};
       gs[h] = 0.f;
@@ -162,50 +193,55 @@ __global__ __launch_bounds__(256) void rel_gemm_dw_kernel(const bf16_t* __restri
         const int64_t gi = g_idx[c0 + sub + e];
         const int64_t xi = x_idx[c0 + sub + e];
         if (gi >= 0) {
-          gv[h] = *reinterpret_cast<const uint4_t*>(G + gi * N + sn * 64 + c * 8);
+          gv[h] = *reinterpret_cast<const uint4_t*>(G + gi * N + sn * T + c * 8);
           gs[h] = scale ? scale[c0 + sub + e] : 1.f;
         }
-        if (xi >= 0) xv[h] = *reinterpret_cast<const uint4_t*>(X + xi * K + sk * 64 + c * 8);
+        if (xi >= 0) xv[h] = *reinterpret_cast<const uint4_t*>(X + xi * K + sk * T + c * 8);
       }
     }
   };
   prefetch(0);
   for (int sub = 0; sub < clen_; sub += RG_BM) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < IT; ++h) {
       const int it = threadIdx.x + h * 256;
-      const int e = it & 63, c = it >> 6;
+      const int e = it / CPR, c = it % CPR;
       float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       acc_bf16x8(v, gv[h], gs[h]);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) gT[(c * 8 + q) * LDT + e] = f2bf(v[q]);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        xT[(c * 8 + 2 * q) * LDT + e] = static_cast<bf16_t>(xv[h][q] & 0xffffu);
-        xT[(c * 8 + 2 * q + 1) * LDT + e] = static_cast<bf16_t>(xv[h][q] >> 16);
-      }
+      *reinterpret_cast<uint4_t*>(gS + e * LD + c * 8) = pack_bf16x8(v);
+      *reinterpret_cast<uint4_t*>(xS + e * LD + c * 8) = xv[h];
     }
     __syncthreads();
     if (sub + RG_BM < clen_) prefetch(sub + RG_BM);
 #pragma unroll
     for (int k0 = 0; k0 < RG_BM; k0 += 32) {
-      const uint4_t a = *reinterpret_cast<const uint4_t*>(gT + (wave * 16 + lr) * LDT + k0 + lk);
+      uint4_t a[FM];
 #pragma unroll
-      for (int f = 0; f < 4; ++f) {
-        const uint4_t bb = *reinterpret_cast<const uint4_t*>(xT + (f * 16 + lr) * LDT + k0 + lk);
-        acc[f] = rg_mfma(a, bb, acc[f]);
+      for (int m = 0; m < FM; ++m) a[m] = rg_tr_frag<LD>(gS, k0, wave * (T / 4) + m * 16, lane);
+#pragma unroll
+      for (int f = 0; f < FN; ++f) {
+        const uint4_t bb = rg_tr_frag<LD>(xS, k0, f * 16, lane);
+#pragma unroll
+        for (int m = 0; m < FM; ++m) acc[m][f] = rg_mfma(a[m], bb, acc[m][f]);
       }
     }
     __syncthreads();
   }
   float* __restrict__ dWr = dW + static_cast<int64_t>(r) * N * K;
+  const bool solo = csolo && csolo[chunk];
 #pragma unroll
-  for (int f = 0; f < 4; ++f)
+  for (int m = 0; m < FM; ++m)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = sn * 64 + wave * 16 + (lane >> 4) * 4 + j;
-      atomicAdd(dWr + static_cast<int64_t>(n) * K + sk * 64 + f * 16 + lr, acc[f][j]);
-    }
+    for (int f = 0; f < FN; ++f)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = sn * T + wave * (T / 4) + m * 16 + (lane >> 4) * 4 + j;
+        float* dst = dWr + static_cast<int64_t>(n) * K + sk * T + f * 16 + (lane & 15);
+        if (solo)
+          *dst = acc[m][f][j];
+        else
+          atomicAdd(dst, acc[m][f][j]);
+      }
 }
 
 }  // namespace euler_hip
@@ -232,14 +268,20 @@ hipError_t eh_rel_gemm(const void* A, int K, const int32_t* a_idx, const int32_t
 
 hipError_t eh_rel_gemm_dw(const void* G, int N, const int32_t* g_idx, const void* X, int K, const int32_t* x_idx,
                           const float* scale, const int32_t* crel, const int32_t* cstart, const int32_t* clen,
-                          int n_chunks, float* dW, hipStream_t s) {
+                          const int32_t* csolo, int n_chunks, float* dW, hipStream_t s) {
   if (n_chunks == 0) return hipSuccess;
   if (N % 64 != 0 || K % 64 != 0) return hipErrorInvalidValue;
-  const int64_t blocks = static_cast<int64_t>(n_chunks) * (N / 64) * (K / 64);
+  const int T = (N % 128 == 0 && K % 128 == 0) ? 128 : 64;
+  const int64_t blocks = static_cast<int64_t>(n_chunks) * (N / T) * (K / T);
   if (blocks >= (1ll << 31)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(rel_gemm_dw_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s,
-                     static_cast<const bf16_t*>(G), N, g_idx, static_cast<const bf16_t*>(X), K, x_idx, scale, crel,
-                     cstart, clen, dW);
+  if (T == 128)
+    hipLaunchKernelGGL(rel_gemm_dw_kernel<128>, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s,
+                       static_cast<const bf16_t*>(G), N, g_idx, static_cast<const bf16_t*>(X), K, x_idx, scale, crel,
+                       cstart, clen, csolo, dW);
+  else
+    hipLaunchKernelGGL(rel_gemm_dw_kernel<64>, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s,
+                       static_cast<const bf16_t*>(G), N, g_idx, static_cast<const bf16_t*>(X), K, x_idx, scale, crel,
+                       cstart, clen, csolo, dW);
   return hipGetLastError();
 }
 

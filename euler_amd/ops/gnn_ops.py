@@ -285,6 +285,8 @@ class RelationTiles:
         self.tile_rel, self.tile_start, self.tile_len, self.num_tiles = self._cut(counts, _TILE, dev)
         chunk = hip().rel_gemm_dw_chunk if dev.type == "cuda" else 1024
         self.chunk_rel, self.chunk_start, self.chunk_len, self.num_chunks = self._cut(counts, chunk, dev)
+        # a relation's only chunk stores its dW slab instead of adding atomically
+        self.chunk_solo = (counts[self.chunk_rel.long()] <= chunk).to(torch.int32).contiguous()
         self.dst_seg = SegmentIndex(self.dst.long(), n_dst)
         self.src_seg = SegmentIndex(self.src.long(), n_src)
 
@@ -362,7 +364,7 @@ class _RelationTransform(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             dwp = torch.zeros(R, Np, Kp, device=dout.device, dtype=torch.float32)
             cr, cs, cl = tiles.chunks()
-            hip().rel_gemm_dw(gb, tiles.dst, xb, tiles.src, tiles.scale, cr, cs, cl, dwp)
+            hip().rel_gemm_dw(gb, tiles.dst, xb, tiles.src, tiles.scale, cr, cs, cl, tiles.chunk_solo, dwp)
             dw = dwp[:, :N, :K].to(ctx.w_dtype)
         return dx, dw, None, None
 

@@ -132,10 +132,11 @@ def test_tall_linear_grads(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("K,N,aggr", [(100, 100, "mean"), (128, 64, "add"), (32, 200, "mean")])
-def test_relation_transform_matches_reference(cuda, K, N, aggr):
+@pytest.mark.parametrize("K,N,aggr,R", [(100, 100, "mean", 13), (128, 64, "add", 13), (32, 200, "mean", 13),
+                                         (128, 128, "mean", 3)])  # R = 3: multi-chunk relations (atomic dW)
+def test_relation_transform_matches_reference(cuda, K, N, aggr, R):
     torch.manual_seed(4)
-    n_dst, n_src, E, R = 400, 900, 7000, 13
+    n_dst, n_src, E = 400, 900, 7000
     ei = _graph(n_dst, n_src, E, cuda, seed=5, pad=10)
     rel = torch.randint(0, R, (E,), device=cuda)
     x = (torch.randn(n_src, K, device=cuda) * 0.5).requires_grad_(True)
