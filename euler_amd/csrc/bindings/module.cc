@@ -2,6 +2,9 @@
 // Plays the role of the reference's C ABI + TF custom ops (SURVEY §2.1 N25,
 // tf_euler/utils/init_query_proxy.cc, euler/service/python_api.cc): numpy in,
 // numpy out, the GIL released around every engine call.
+#include <cstring>
+#include <vector>
+
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -419,6 +422,53 @@ PYBIND11_MODULE(_engine, m) {
       .def_property_readonly("port", &PyServer::port)
       .def_property_readonly("requests", &PyServer::requests)
       .def("stop", &PyServer::Stop);
+
+  // (unique values in first-occurrence order, inverse) of an int64 array: tf.unique
+  // semantics for the CPU dataflows (every hop of SageDataFlow / NeighborDataFlow).  One
+  // pass over an open-addressing table (multiplicative hash, linear probing), GIL released:
+  // O(n) instead of the sort + scatter-min + argsort composition.
+  m.def(
+      "unique_first",
+      [](py::array_t<int64_t, py::array::c_style | py::array::forcecast> x) {
+        const int64_t n = static_cast<int64_t>(x.size());
+        py::array_t<int64_t> inv(n);
+        std::vector<int64_t> uniq;
+        {
+          py::gil_scoped_release nogil;
+          const int64_t* xs = x.data();
+          int64_t* iv = inv.mutable_data();
+          uint64_t cap = 16;
+          while (cap < static_cast<uint64_t>(2 * n)) cap <<= 1;
+          const uint64_t mask = cap - 1;
+          struct Cell {
+            int64_t key;
+            int64_t slot;
+          };
+          std::vector<Cell> table(cap, Cell{0, -1});  // key and slot on one cache line
+          uniq.reserve(static_cast<size_t>(n));
+          for (int64_t i = 0; i < n; ++i) {
+            const int64_t v = xs[i];
+            uint64_t z = static_cast<uint64_t>(v) * 0x9e3779b97f4a7c15ull;
+            uint64_t h = (z ^ (z >> 29)) & mask;
+            while (true) {
+              Cell& c = table[h];
+              if (c.slot < 0) {
+                c.slot = static_cast<int64_t>(uniq.size());
+                c.key = v;
+                uniq.push_back(v);
+                break;
+              }
+              if (c.key == v) break;
+              h = (h + 1) & mask;
+            }
+            iv[i] = table[h].slot;
+          }
+        }
+        py::array_t<int64_t> u(static_cast<py::ssize_t>(uniq.size()));
+        if (!uniq.empty()) std::memcpy(u.mutable_data(), uniq.data(), uniq.size() * sizeof(int64_t));
+        return py::make_tuple(u, inv);
+      },
+      py::arg("x"));
 
   m.def(
       "synthetic",

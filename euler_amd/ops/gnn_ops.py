@@ -25,7 +25,7 @@ import os
 import torch
 import torch.nn.functional as F
 
-from euler_amd.ops._native import hip, use_hip
+from euler_amd.ops._native import engine, hip, use_hip
 from euler_amd.ops.mp_ops import SegmentIndex
 
 __all__ = ["EdgeCSR", "gat_aggregate", "gat_aggregate_reference", "RelationTiles", "relation_transform",
@@ -571,10 +571,15 @@ def kg_score(ent, rel, src, dst, ridx, neg, kind="l1", corrupt="both", normalize
 def unique_first(x: torch.Tensor):
     """``(unique values, inverse)`` of a 1-D id tensor in first-occurrence order — the
     semantics of ``tf.unique`` (reference dataflows rely on the previous hop's nodes
-    keeping their leading positions).  GPU: hash-table kernel; CPU: sort-based."""
+    keeping their leading positions).  GPU: hash-table kernel; CPU: the engine's O(n)
+    hash pass (``_engine.unique_first``)."""
     x = x.reshape(-1)
     if use_hip(x):
         return tuple(hip().unique_first(x.long().contiguous()))
+    if x.device.type == "cpu" and x.numel() > 0:
+        # O(n) hash pass in the C++ engine (GIL released) — the CPU dataflows call this per hop
+        u, inv = engine().unique_first(x.long().contiguous().numpy())
+        return torch.from_numpy(u), torch.from_numpy(inv)
     u, inv = torch.unique(x, sorted=True, return_inverse=True)
     if u.numel() == 0:
         return u, inv
