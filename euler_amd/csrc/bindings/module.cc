@@ -91,6 +91,45 @@ py::object ToPy(const Tensor& t) {
   throw std::runtime_error("unsupported tensor dtype");
 }
 
+// ------------------------------------------------------------------ dataflow helpers
+// tf.unique (first-occurrence order) in one pass over an open-addressing table
+// (multiplicative hash, linear probing, key and slot on one cache line)
+void UniqueFirst(const int64_t* xs, int64_t n, std::vector<int64_t>* uniq, int64_t* inv) {
+  uint64_t cap = 16;
+  while (cap < static_cast<uint64_t>(2 * n)) cap <<= 1;
+  const uint64_t mask = cap - 1;
+  struct Cell {
+    int64_t key;
+    int64_t slot;
+  };
+  std::vector<Cell> table(cap, Cell{0, -1});
+  uniq->clear();
+  uniq->reserve(static_cast<size_t>(n));
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t v = xs[i];
+    const uint64_t z = static_cast<uint64_t>(v) * 0x9e3779b97f4a7c15ull;
+    uint64_t h = (z ^ (z >> 29)) & mask;
+    while (true) {
+      Cell& c = table[h];
+      if (c.slot < 0) {
+        c.slot = static_cast<int64_t>(uniq->size());
+        c.key = v;
+        uniq->push_back(v);
+        break;
+      }
+      if (c.key == v) break;
+      h = (h + 1) & mask;
+    }
+    inv[i] = table[h].slot;
+  }
+}
+
+py::array_t<int64_t> I64(const std::vector<int64_t>& v) {
+  py::array_t<int64_t> a(static_cast<py::ssize_t>(v.size()));
+  if (!v.empty()) memcpy(a.mutable_data(), v.data(), v.size() * sizeof(int64_t));
+  return a;
+}
+
 // ------------------------------------------------------------------ Engine (QueryProxy)
 class Engine {
  public:
@@ -224,6 +263,66 @@ class Engine {
       });
     }
     return py::make_tuple(oid, ow, ot);
+  }
+
+  // SageDataFlow (dataflow/dataflows.py) in one call with the GIL released: per hop,
+  // fixed-fanout sampling of the current node set, tf.unique of [neighbours | nodes], the
+  // previous set's positions and the [2, E] edge index (+ self loops).  Returns a list of
+  // (n_id, res_n_id, edge_index) int64 arrays, innermost hop first.
+  py::list SageFlow(py::array_t<int64_t, py::array::c_style | py::array::forcecast> roots,
+                    std::vector<std::vector<int32_t>> etypes, std::vector<int> counts, int64_t def,
+                    bool self_loops) {
+    Graph& g = LocalGraph();
+    if (etypes.size() != counts.size()) throw std::runtime_error("one fanout per hop");
+    struct Hop {
+      std::vector<int64_t> n_id, res, src, dst;
+    };
+    std::vector<Hop> hops(etypes.size());
+    std::vector<int64_t> cur(roots.data(), roots.data() + roots.size());
+    {
+      py::gil_scoped_release nogil;
+      const uint64_t seed = GlobalSeed() * 0x9E3779B97F4A7C15ULL + NowMicros();
+      for (size_t h = 0; h < etypes.size(); ++h) {
+        const int64_t n = static_cast<int64_t>(cur.size());
+        const int k = counts[h];
+        std::vector<int64_t> cat(static_cast<size_t>(n * k + n));
+        const int64_t chunk = 512, nchunks = (n + chunk - 1) / chunk;
+        ThreadPool::Default()->ParallelFor(nchunks, 1, [&](int64_t cb, int64_t ce) {
+          std::vector<IdWeightType> tmp;
+          for (int64_t c = cb; c < ce; ++c) {
+            Rng rng(seed + h * 0x51ED27ULL, static_cast<uint64_t>(c));
+            for (int64_t i = c * chunk; i < std::min(n, (c + 1) * chunk); ++i) {
+              g.SampleNeighbor(g.Row(static_cast<uint64_t>(cur[i])), etypes[h], k, true, rng, &tmp);
+              for (int j = 0; j < k; ++j)
+                cat[i * k + j] = j < static_cast<int>(tmp.size()) ? static_cast<int64_t>(tmp[j].id) : def;
+            }
+          }
+        });
+        std::copy(cur.begin(), cur.end(), cat.begin() + n * k);
+        Hop& o = hops[h];
+        std::vector<int64_t> inv(cat.size());
+        UniqueFirst(cat.data(), static_cast<int64_t>(cat.size()), &o.n_id, inv.data());
+        o.res.assign(inv.end() - n, inv.end());
+        const int64_t e = self_loops ? n * k + n : n * k;
+        o.src.resize(static_cast<size_t>(e));
+        for (int64_t i = 0; i < n * k; ++i) o.src[i] = i / k;
+        if (self_loops)
+          for (int64_t i = 0; i < n; ++i) o.src[n * k + i] = i;
+        o.dst.assign(inv.begin(), inv.begin() + e);
+        cur = o.n_id;
+      }
+    }
+    py::list out;
+    for (auto& o : hops) {
+      const py::ssize_t e = static_cast<py::ssize_t>(o.src.size());
+      py::array_t<int64_t> ei({static_cast<py::ssize_t>(2), e});
+      if (e) {
+        memcpy(ei.mutable_data(), o.src.data(), e * sizeof(int64_t));
+        memcpy(ei.mutable_data() + e, o.dst.data(), e * sizeof(int64_t));
+      }
+      out.append(py::make_tuple(I64(o.n_id), I64(o.res), ei));
+    }
+    return out;
   }
 
   // dense node feature rows (missing ids / shorter rows -> zeros), [n, dim] float32
@@ -397,6 +496,8 @@ PYBIND11_MODULE(_engine, m) {
       .def("summary", &Engine::Summary)
       .def("sample_node", &Engine::SampleNode)
       .def("sample_neighbor", &Engine::SampleNeighbor)
+      .def("sage_flow", &Engine::SageFlow, py::arg("roots"), py::arg("edge_types"), py::arg("counts"),
+           py::arg("default_node"), py::arg("self_loops") = true)
       .def("dense_feature", &Engine::DenseFeature)
       .def("export_csr", &Engine::ExportCsr);
 
@@ -424,9 +525,8 @@ PYBIND11_MODULE(_engine, m) {
       .def("stop", &PyServer::Stop);
 
   // (unique values in first-occurrence order, inverse) of an int64 array: tf.unique
-  // semantics for the CPU dataflows (every hop of SageDataFlow / NeighborDataFlow).  One
-  // pass over an open-addressing table (multiplicative hash, linear probing), GIL released:
-  // O(n) instead of the sort + scatter-min + argsort composition.
+  // semantics for the CPU dataflows (every hop of SageDataFlow / NeighborDataFlow), GIL
+  // released.
   m.def(
       "unique_first",
       [](py::array_t<int64_t, py::array::c_style | py::array::forcecast> x) {
@@ -435,38 +535,9 @@ PYBIND11_MODULE(_engine, m) {
         std::vector<int64_t> uniq;
         {
           py::gil_scoped_release nogil;
-          const int64_t* xs = x.data();
-          int64_t* iv = inv.mutable_data();
-          uint64_t cap = 16;
-          while (cap < static_cast<uint64_t>(2 * n)) cap <<= 1;
-          const uint64_t mask = cap - 1;
-          struct Cell {
-            int64_t key;
-            int64_t slot;
-          };
-          std::vector<Cell> table(cap, Cell{0, -1});  // key and slot on one cache line
-          uniq.reserve(static_cast<size_t>(n));
-          for (int64_t i = 0; i < n; ++i) {
-            const int64_t v = xs[i];
-            uint64_t z = static_cast<uint64_t>(v) * 0x9e3779b97f4a7c15ull;
-            uint64_t h = (z ^ (z >> 29)) & mask;
-            while (true) {
-              Cell& c = table[h];
-              if (c.slot < 0) {
-                c.slot = static_cast<int64_t>(uniq.size());
-                c.key = v;
-                uniq.push_back(v);
-                break;
-              }
-              if (c.key == v) break;
-              h = (h + 1) & mask;
-            }
-            iv[i] = table[h].slot;
-          }
+          UniqueFirst(x.data(), n, &uniq, inv.mutable_data());
         }
-        py::array_t<int64_t> u(static_cast<py::ssize_t>(uniq.size()));
-        if (!uniq.empty()) std::memcpy(u.mutable_data(), uniq.data(), uniq.size() * sizeof(int64_t));
-        return py::make_tuple(u, inv);
+        return py::make_tuple(I64(uniq), inv);
       },
       py::arg("x"));
 

@@ -27,7 +27,7 @@ __all__ = ["Block", "DataFlow", "NeighborDataFlow", "UniqueDataFlow", "SageDataF
 def unique_with_inverse(x: torch.Tensor):
     """(unique values, inverse) — ``tf.unique`` semantics: first-occurrence order, so
     the previous hop's nodes keep their positions (GPU tensors: hash-table kernel
-    ``unique.hip``; CPU: sort-based, same result)."""
+    ``unique.hip``; CPU: the engine's hash pass, same result)."""
     return unique_first(x)
 
 
@@ -149,6 +149,17 @@ class SageDataFlow(UniqueDataFlow):
         self.fanouts = fanouts
         self.metapath = metapath
         self.max_id = max_id
+
+    def produce_subgraph(self, n_id):
+        n_id = torch.as_tensor(n_id).reshape(-1).long()
+        hops = ge.sage_flow(n_id, self.metapath, self.fanouts, self.max_id + 1, self.add_self_loops)
+        if hops is None:  # remote graph: per-hop GQL sampling + unique below
+            return super().produce_subgraph(n_id)
+        # the engine built every hop in one native call (sampling, unique, edge index)
+        df = DataFlow(n_id)
+        for new_n_id, res_n_id, edge_index in hops:
+            df.append(new_n_id, res_n_id, None, edge_index)
+        return df
 
     def get_neighbors(self, n_id):
         neighbors, srcs = [], []

@@ -22,7 +22,7 @@ from euler_amd.ops.base import get_engine
 __all__ = [
     "SparseTensor", "ALL_NODE_TYPE", "get_node_type_id", "get_edge_type_id", "get_node_type",
     "sample_node", "sample_edge", "sample_node_with_src", "sample_n_with_types", "sample_graph_label",
-    "get_graph_by_label", "sample_neighbor", "get_top_k_neighbor", "get_full_neighbor",
+    "get_graph_by_label", "sample_neighbor", "sage_flow", "get_top_k_neighbor", "get_full_neighbor",
     "get_sorted_full_neighbor", "get_in_neighbor", "sample_fanout", "sample_fanout_with_feature",
     "sample_neighbor_layerwise", "sample_fanout_layerwise", "sample_fanout_layerwise_each_node",
     "get_multi_hop_neighbor", "sparse_get_adj", "get_dense_feature", "get_sparse_feature",
@@ -234,6 +234,19 @@ def sample_neighbor(nodes, edge_types, count, default_node=-1, condition=""):
                 {"nodes": ids, "edge_types": et, "nb_count": np.asarray([int(count)])},
                 ["nb:0", "nb:1", "nb:2", "nb:3"])
     return _dense_rows(r[0], r[1], r[2], r[3], len(ids), int(count), int(default_node))
+
+
+def sage_flow(roots, metapath, fanouts, default_node=-1, self_loops=True):
+    """Native SageDataFlow (``_engine.sage_flow``, GIL released): per hop fixed-fanout
+    sampling + first-occurrence unique + edge index, innermost hop first, as
+    ``[(n_id, res_n_id, edge_index [2, E])]`` int64 tensors.  Returns None when the graph
+    is not in-process (remote / sharded mode: the GQL path is used instead)."""
+    if _meta()["mode"] != "local":
+        return None
+    ets = [[int(x) for x in _et(et) if x >= 0] for et in metapath]
+    hops = get_engine().sage_flow(np.ascontiguousarray(_u64(roots).view(np.int64)), ets,
+                                  [int(c) for c in fanouts], int(default_node), bool(self_loops))
+    return [(torch.from_numpy(a), torch.from_numpy(b), torch.from_numpy(c)) for a, b, c in hops]
 
 
 def get_top_k_neighbor(nodes, edge_types, k, default_node=-1, condition=""):

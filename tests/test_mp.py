@@ -149,6 +149,42 @@ def test_sage_dataflow_shapes(syn):
     assert torch.equal(inner.n_id[inner.res_n_id], torch.arange(8))
 
 
+@pytest.mark.parametrize("self_loops", [True, False])
+def test_native_sage_flow_matches_python_semantics(syn, self_loops):
+    """_engine.sage_flow (one GIL-free call) builds the same structure as the per-hop
+    Python dataflow: node sets deduplicated in first-occurrence order, res_n_id, edge
+    rows = [target position repeated fanout times | self loops], sampled ids are real
+    neighbours (or the default node)."""
+    import euler_amd.ops.graph_api as ge
+
+    roots = torch.tensor([3, 8, 3, 11, 0])
+    flow = D.SageDataFlow([4, 2], ["0", "0"], add_self_loops=self_loops, max_id=399)
+    df = flow(roots)
+    last = roots
+    for blk, k in zip(df.blocks, [4, 2]):
+        n = last.numel()
+        assert blk.size == [n, blk.n_id.numel()]
+        assert torch.equal(blk.n_id[blk.res_n_id], last)
+        assert blk.edge_index.shape == (2, n * k + (n if self_loops else 0))
+        src, dst = blk.edge_index
+        assert torch.equal(src[:n * k], torch.arange(n).repeat_interleave(k))
+        if self_loops:
+            assert torch.equal(blk.n_id[dst[n * k:]], last)
+        assert len(set(blk.n_id.tolist())) == blk.n_id.numel()
+        # first-occurrence order of [neighbours | previous nodes]
+        cat = torch.cat([blk.n_id[dst[:n * k]], last])
+        seen = []
+        for v in cat.tolist():
+            if v not in seen:
+                seen.append(v)
+        assert blk.n_id.tolist() == seen
+        full = ge.get_full_neighbor(last, ["0"])[0]
+        for e in range(n * k):
+            s_, d_ = int(src[e]), int(blk.n_id[dst[e]])
+            assert d_ == 400 or d_ in full.values[full.indices[:, 0] == s_].tolist()
+        last = blk.n_id
+
+
 @pytest.mark.parametrize("flow", ["sage", "full", "whole", "fast", "adapt"])
 def test_supervised_gnn_trains(syn, flow):
     torch.manual_seed(0)
