@@ -261,8 +261,10 @@ def _ragged_to_sparse(idx, vals, values_cast=None):
     n = idx.shape[0]
     lens = (idx[:, 1] - idx[:, 0]).astype(np.int64)
     rows = np.repeat(np.arange(n, dtype=np.int64), lens)
-    cols = np.concatenate([np.arange(l, dtype=np.int64) for l in lens]) if n else np.zeros(0, np.int64)
-    sel = np.concatenate([np.arange(b, e) for b, e in idx]) if n else np.zeros(0, np.int64)
+    # position inside each row and source index, vectorised (no per-row Python loop)
+    out_off = np.cumsum(lens) - lens
+    cols = np.arange(int(lens.sum()), dtype=np.int64) - np.repeat(out_off, lens)
+    sel = np.repeat(idx[:, 0].astype(np.int64), lens) + cols
     v = np.asarray(vals)[sel.astype(np.int64)] if len(sel) else np.asarray(vals)[:0]
     if values_cast is not None:
         v = v.astype(values_cast)
