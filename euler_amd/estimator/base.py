@@ -34,7 +34,7 @@ import torch
 import torch.nn as nn
 
 from euler_amd.parallel import dp
-from euler_amd.parallel.embedding import is_sharded
+from euler_amd.parallel.embedding import is_sharded, reshard_rows, sharded_param_names
 from euler_amd.utils.prefetch import Prefetcher
 from euler_amd.utils import trace
 from euler_amd.utils.misc import get_optimizer
@@ -206,6 +206,10 @@ class BaseEstimator:
             if os.path.exists(own):
                 path = own
         state = torch.load(path, map_location=self.device, weights_only=True)
+        saved_world = int(state.get("world", 1))
+        names = sharded_param_names(self.model)
+        if names and saved_world != self.world:
+            self._reshard(state, path, saved_world, names)
         self.model.load_state_dict(state["model"], strict=strict)
         if self.optimizer is not None and state.get("optimizer") is not None:
             self.optimizer.load_state_dict(state["optimizer"])
@@ -214,6 +218,30 @@ class BaseEstimator:
             torch.set_rng_state(state["torch_rng"].cpu())
         log.info("restored %s at step %d", path, self.global_step)
         return True
+
+    def _reshard(self, state, path, saved_world, names):
+        """Sharded embedding tables (and their optimizer slots) saved by ``saved_world``
+        ranks, re-sharded for this run's world size: every rank reads all the shard files
+        and keeps its ``mod`` rows."""
+        base = re.sub(r"-rank\d+\.pt$", ".pt", path)
+        files = [base if r == 0 else base.replace(".pt", "-rank%d.pt" % r) for r in range(saved_world)]
+        states = [torch.load(f, map_location="cpu", weights_only=True) for f in files]
+        dev = self.device
+        for n in names:
+            state["model"][n] = reshard_rows([st["model"][n] for st in states], self.rank, self.world).to(dev)
+        # optimizer slots of the sharded tables follow their rows (param order = optimizer order)
+        opt = state.get("optimizer")
+        if opt is None:
+            return
+        pnames = [n for n, p in self.model.named_parameters() if p.requires_grad]
+        for i, n in enumerate(pnames):
+            if n not in names or i not in opt["state"]:
+                continue
+            rows = [st["model"][n].shape[0] for st in states]
+            for k, v in list(opt["state"][i].items()):
+                if torch.is_tensor(v) and v.dim() > 0 and v.shape[0] == rows[0]:
+                    parts = [st["optimizer"]["state"][i][k] for st in states]
+                    opt["state"][i][k] = reshard_rows(parts, self.rank, self.world).to(dev)
 
     # ------------------------------------------------------------------ modes
     def train(self):

@@ -22,7 +22,7 @@ import torch.nn as nn
 
 from euler_amd.ops import mp_ops
 
-__all__ = ["ShardedEmbedding", "sharded_lookup", "is_sharded"]
+__all__ = ["ShardedEmbedding", "sharded_lookup", "is_sharded", "sharded_param_names", "reshard_rows"]
 
 
 def is_sharded(p) -> bool:
@@ -106,3 +106,22 @@ class ShardedEmbedding(nn.Module):
     def global_ids(self):
         """ids of the rows this rank owns, in local order."""
         return torch.arange(self.weight.shape[0], device=self.weight.device) * self.world + self.rank
+
+
+def sharded_param_names(model: nn.Module):
+    """state_dict names of every ShardedEmbedding table of ``model`` (sharded or not in
+    the current run: a one-process run holds the whole table)."""
+    return {(name + "." if name else "") + "weight" for name, m in model.named_modules()
+            if isinstance(m, ShardedEmbedding)}
+
+
+def reshard_rows(parts, new_rank: int, new_world: int) -> torch.Tensor:
+    """Re-shard a ``mod``-sharded table saved by ``len(parts)`` ranks (part r holds global
+    rows r, r + W, r + 2W, ...) for rank ``new_rank`` of ``new_world``: the checkpoint
+    restores with a different world size."""
+    W = len(parts)
+    n = sum(int(p.shape[0]) for p in parts)
+    full = torch.empty((n,) + tuple(parts[0].shape[1:]), dtype=parts[0].dtype)
+    for r, part in enumerate(parts):
+        full[r::W] = part.to(full.device)
+    return full[new_rank::new_world].clone()

@@ -244,3 +244,59 @@ def test_replicated_store_writes_reach_every_rank():
     res = _run(_worker_replicated_store)
     assert not [r for r in res if r[1] == "error"], res
     assert len(res) == 2 and all(r[2] for r in res), res
+
+
+class _EmbModel(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        from euler_amd.parallel.embedding import ShardedEmbedding
+
+        self.emb = ShardedEmbedding(9, 3)   # 10 rows, sharded mod world
+        self.lin = torch.nn.Linear(3, 1)
+
+
+def _worker_ckpt_save(rank, world, port, q, model_dir):
+    try:
+        _init(rank, world, port)
+        from euler_amd.estimator.base import BaseEstimator
+
+        torch.manual_seed(0)
+        m = _EmbModel()
+        with torch.no_grad():  # row value = its global id
+            m.emb.weight.copy_(m.emb.global_ids().float().unsqueeze(1).repeat(1, 3))
+        est = BaseEstimator(m, {"model_dir": model_dir, "device": "cpu"})
+        est.optimizer = torch.optim.Adagrad(m.parameters(), lr=0.1)
+        for p in m.parameters():
+            p.grad = torch.ones_like(p)
+        est.optimizer.step()
+        est.global_step = 7
+        est.save()
+        dist.barrier()
+        q.put((rank, "saved", True))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, "error", repr(e)))
+
+
+def test_checkpoint_reshards_on_world_size_change(tmp_path):
+    """2 ranks save their ShardedEmbedding shards; a 1-process run restores the whole
+    table (rows re-interleaved) and its Adagrad slots."""
+    from euler_amd.estimator.base import BaseEstimator
+    from euler_amd.parallel.embedding import reshard_rows
+
+    res = _run(_worker_ckpt_save, str(tmp_path))
+    assert not [r for r in res if r[1] == "error"], res
+    m = _EmbModel()
+    est = BaseEstimator(m, {"model_dir": str(tmp_path), "device": "cpu"})
+    est.optimizer = torch.optim.Adagrad(m.parameters(), lr=0.1)
+    assert est.restore()
+    w = m.emb.weight.detach()
+    assert w.shape == (10, 3) and est.global_step == 7
+    # every row took the same Adagrad step, so rows differ by their global ids
+    torch.testing.assert_close(w[:, 0] - w[0, 0], torch.arange(10).float())
+    st = est.optimizer.state_dict()["state"]
+    emb_idx = [n for n, _ in m.named_parameters()].index("emb.weight")
+    assert st[emb_idx]["sum"].shape == (10, 3)
+    # 3-way re-shard of a 2-way sharded table
+    full = torch.arange(10).float().unsqueeze(1)
+    assert torch.equal(reshard_rows([full[0::2], full[1::2]], 1, 3), full[1::3])
