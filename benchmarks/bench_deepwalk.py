@@ -76,7 +76,7 @@ def main(argv=None):
                          args.optimizer, seed=args.seed, force_comm=args.force_dist)
     torch.cuda.synchronize()
     if rank == 0:
-        gib = (tr.target.nbytes() + tr.context.nbytes()) / 2 ** 30
+        gib = tr.table.nbytes() / 2 ** 30
         print(f"[bench_deepwalk] {args.num_nodes} nodes, {g.num_edges} edges, tables+slots {gib:.1f} GiB/rank, "
               f"setup {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
 
@@ -115,7 +115,7 @@ def main(argv=None):
             "data": "synthetic (power-law random graph, random-init tables)",
             "config": {"model": f"DeepWalk (walk_len 3, window 1/1, 5 negs, row-sparse {args.optimizer})",
                        "num_nodes": args.num_nodes, "dim": args.dim, "walks_per_gpu": args.batch,
-                       "pairs_per_gpu_step": tr.pairs_per_step(), "parallelism": f"dp{world}+sharded-emb", "all_to_all": bool(tr.target.comm),
+                       "pairs_per_gpu_step": tr.pairs_per_step(), "parallelism": f"dp{world}+sharded-emb", "all_to_all": bool(tr.table.comm),
                        "loss_first_last": [round(first, 4), round(float(tr.loss), 4)],
                        "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1)},
         }), flush=True)

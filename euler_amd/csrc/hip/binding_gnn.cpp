@@ -341,24 +341,34 @@ UpdIn upd_check(int64_t side, const torch::Tensor& ptr, const torch::Tensor& lis
   return r;
 }
 
+// per-unique-row gradients of one side; rows with no occurrence on this side are written
+// only when the buffer is allocated here (zeros) — with ``out`` they are left untouched
 torch::Tensor sgns_grad(int64_t side, torch::Tensor ptr, torch::Tensor list, torch::Tensor coef, int64_t K,
-                        torch::Tensor src, c10::optional<torch::Tensor> smap, torch::Tensor sinv) {
+                        torch::Tensor src, c10::optional<torch::Tensor> smap, torch::Tensor sinv,
+                        c10::optional<torch::Tensor> out) {
   const UpdIn u = upd_check(side, ptr, list, coef, K, src, smap, sinv);
   const c10::DeviceGuard g(src.device());
   const int64_t D = src.size(1);
-  auto gout = torch::empty({u.n_u, D}, src.options());
+  torch::Tensor gout;
+  if (out.has_value()) {
+    typed(*out, torch::kFloat32, "out");
+    TORCH_CHECK(out->dim() == 2 && out->size(0) == u.n_u && out->size(1) == D, "out must be [n_u, D]");
+    gout = *out;
+  } else {
+    gout = torch::zeros({u.n_u, D}, src.options());
+  }
   ok(eh_sgns_update(static_cast<int>(side), u.n_u, ptr.data_ptr<int64_t>(), list.data_ptr<int32_t>(),
                     coef.data_ptr<float>(), u.P, static_cast<int>(K), static_cast<int>(D), src.data_ptr<float>(),
                     src.size(0), u.smap, u.n_smap, sinv.data_ptr<int64_t>(), gout.data_ptr<float>(), nullptr, nullptr,
-                    nullptr, nullptr, 0, nullptr, 0.f, 0.f, 0.f, 0.f, 2, stream()),
+                    nullptr, nullptr, 0, nullptr, 0, 0.f, 0.f, 0.f, 0.f, 2, stream()),
      "sgns_grad");
   return gout;
 }
 
 void sgns_apply_(int64_t side, torch::Tensor ptr, torch::Tensor list, torch::Tensor coef, int64_t K, torch::Tensor src,
                  c10::optional<torch::Tensor> smap, torch::Tensor sinv, torch::Tensor table, torch::Tensor m,
-                 torch::Tensor v, c10::optional<torch::Tensor> rows, torch::Tensor step, double lr, double b1, double b2,
-                 double eps, int64_t kind) {
+                 torch::Tensor v, c10::optional<torch::Tensor> rows, torch::Tensor step, bool inc_step, double lr,
+                 double b1, double b2, double eps, int64_t kind) {
   const UpdIn u = upd_check(side, ptr, list, coef, K, src, smap, sinv);
   typed(table, torch::kFloat32, "table");
   typed(m, torch::kFloat32, "m");
@@ -377,7 +387,8 @@ void sgns_apply_(int64_t side, torch::Tensor ptr, torch::Tensor list, torch::Ten
                     coef.data_ptr<float>(), u.P, static_cast<int>(K), static_cast<int>(src.size(1)),
                     src.data_ptr<float>(), src.size(0), u.smap, u.n_smap, sinv.data_ptr<int64_t>(), nullptr,
                     table.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), rp, table.size(0),
-                    step.data_ptr<int64_t>(), static_cast<float>(lr), static_cast<float>(b1), static_cast<float>(b2),
+                    step.data_ptr<int64_t>(), inc_step ? 1 : 0, static_cast<float>(lr), static_cast<float>(b1),
+                    static_cast<float>(b2),
                     static_cast<float>(eps), static_cast<int>(kind), stream()),
      "sgns_apply");
 }

@@ -305,7 +305,9 @@ __global__ __launch_bounds__(256) void sgns_update_kernel(SgnsUpd a) {
     }
   }
   if (!apply) {
-    EV<float>::store(a.gout + L.row * a.D + d, g);
+    // rows without occurrences on this side are left untouched: two launches (target and
+    // context side) can fill one buffer whose rows each belong to exactly one side
+    if (end > beg) EV<float>::store(a.gout + L.row * a.D + d, g);
     return;
   }
   const int64_t off = r * a.D + d;
@@ -598,11 +600,12 @@ hipError_t eh_occ_fill(const int64_t* inv, int64_t n, const int64_t* ptr, int* c
 
 hipError_t eh_sgns_update(int side, int64_t n_u, const int64_t* ptr, const int* list, const float* coef, int64_t P,
                           int K, int D, const float* src, int64_t n_src, const int64_t* smap, int64_t n_smap,
-                          const int64_t* sinv, float* gout, float* table, float* m, float* v, const int64_t* rows, int64_t n_rows,
-                          int64_t* step, float lr, float b1, float b2, float eps, int kind, hipStream_t s) {
+                          const int64_t* sinv, float* gout, float* table, float* m, float* v, const int64_t* rows,
+                          int64_t n_rows, int64_t* step, int inc_step, float lr, float b1, float b2, float eps,
+                          int kind, hipStream_t s) {
   if (D % 4 != 0 || D / 4 > 64 || (side != 0 && side != 1) || (side == 1 && K < 0) || kind < 0 || kind > 2)
     return hipErrorInvalidValue;
-  if (!gout) hipLaunchKernelGGL(sgns_step_inc_kernel, dim3(1), dim3(1), 0, s, step);
+  if (!gout && inc_step) hipLaunchKernelGGL(sgns_step_inc_kernel, dim3(1), dim3(1), 0, s, step);
   if (n_u == 0) return hipGetLastError();
   SgnsUpd a;
   a.ptr = ptr;

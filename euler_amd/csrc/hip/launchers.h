@@ -120,8 +120,9 @@ hipError_t eh_sgns_fwd_idx(const float* T, const int64_t* tmap, int64_t nTm, con
 hipError_t eh_occ_fill(const int64_t* inv, int64_t n, const int64_t* ptr, int* cursor, int* list, hipStream_t s);
 hipError_t eh_sgns_update(int side, int64_t n_u, const int64_t* ptr, const int* list, const float* coef, int64_t P,
                           int K, int D, const float* src, int64_t n_src, const int64_t* smap, int64_t n_smap,
-                          const int64_t* sinv, float* gout, float* table, float* m, float* v, const int64_t* rows, int64_t n_rows,
-                          int64_t* step, float lr, float b1, float b2, float eps, int kind, hipStream_t s);
+                          const int64_t* sinv, float* gout, float* table, float* m, float* v, const int64_t* rows,
+                          int64_t n_rows, int64_t* step, int inc_step, float lr, float b1, float b2, float eps,
+                          int kind, hipStream_t s);
 hipError_t eh_kg_fwd(const float* ent, const float* rel, const int64_t* src, const int64_t* dst, const int64_t* ridx,
                      const int64_t* neg, int64_t B, int K, int D, int kind, int corrupt, int normalize,
                      float* pos_score, float* neg_score, hipStream_t s);

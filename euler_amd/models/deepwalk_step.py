@@ -13,6 +13,7 @@ One step here, per rank (no autograd, no dense table gradient):
   2. pairs    : skip-gram (centre, context) pairs of every walk; negatives per pair
   3. unique   : hash-table unique of the centre ids and of the context+negative ids,
                 plus the occurrence lists of every unique id (occ_csr)
+     (one row-sharded table holds target rows [0, N] and context rows [N+1, 2N+1])
   4. loss     : ``sgns_fwd_idx`` — logits straight from the table rows through the two-level
                 (occurrence -> unique id -> row) index; emits only coef = dloss/dlogit
   5. update   : per unique row, the gradient is rebuilt from its occurrence list and
@@ -53,10 +54,11 @@ class DeepWalkTrainer:
         self.dim, self.walk_len, self.num_negs, self.batch = int(dim), int(walk_len), int(num_negs), int(batch_size)
         dev = graph.device
         self.device = dev
-        self.target = ShardedTable(self.num_nodes + 1, dim, dev, group, optimizer, lr, seed=seed,
-                                   force_comm=force_comm)
-        self.context = ShardedTable(self.num_nodes + 1, dim, dev, group, optimizer, lr, seed=seed + 1,
-                                    force_comm=force_comm)
+        # ONE row-sharded table holds both embeddings: target row of node i is row i, its
+        # context row is row off + i.  A step then needs one id exchange, one row exchange,
+        # one gradient exchange and one host sync (world > 1) instead of two of each.
+        self.off = self.num_nodes + 1
+        self.table = ShardedTable(2 * self.off, dim, dev, group, optimizer, lr, seed=seed, force_comm=force_comm)
         pi, pj = _pair_positions(walk_len, left_win_size, right_win_size)
         self.pi, self.pj = pi.to(dev), pj.to(dev)
         self.pairs_per_walk = int(pi.numel())
@@ -83,26 +85,36 @@ class DeepWalkTrainer:
         src, pos, negs = self.sample()
         P, K = src.numel(), self.num_negs
         gscale = 1.0 / (P * (1 + K))
-        # unique ids per table (first-occurrence order; hash kernel on the GPU)
+        # unique ids per role (first-occurrence order; hash kernel on the GPU)
         u_t, inv_t = gnn_ops.unique_first(src)
         u_c, inv_c = gnn_ops.unique_first(torch.cat([pos, negs.reshape(-1)]))
-        ptr_t, lst_t = gnn_ops.occ_csr(inv_t, u_t.numel())
-        ptr_c, lst_c = gnn_ops.occ_csr(inv_c, u_c.numel())
-        T, C = self.target, self.context
-        if T.fused_sgns_ok(u_t) and C.fused_sgns_ok(u_c):
-            # one rank owns every row: local row == global id
-            coef, loss_rows = gnn_ops.sgns_fwd_idx(T.weight, u_t, inv_t, C.weight, u_c, inv_c, K, gscale)
-            rt = self._gather(T.weight, u_t)                # pre-update target rows
-            T.apply_sgns(0, ptr_t, lst_t, coef, K, C.weight, u_c, inv_c, u_t)
-            C.apply_sgns(1, ptr_c, lst_c, coef, K, rt, None, inv_t, u_c)
+        n_t = u_t.numel()
+        tab = self.table
+        rows_c_id = u_c + self.off
+        if tab.fused_sgns_ok(u_t):
+            # one rank owns every row: local row == table row
+            ptr_t, lst_t = gnn_ops.occ_csr(inv_t, n_t)
+            ptr_c, lst_c = gnn_ops.occ_csr(inv_c, u_c.numel())
+            W = tab.weight
+            coef, loss_rows = gnn_ops.sgns_fwd_idx(W, u_t, inv_t, W, rows_c_id, inv_c, K, gscale)
+            rt = self._gather(W, u_t)                       # pre-update target rows
+            tab.apply_sgns(0, ptr_t, lst_t, coef, K, W, rows_c_id, inv_c, u_t)
+            tab.apply_sgns(1, ptr_c, lst_c, coef, K, rt, None, inv_t, rows_c_id, inc_step=False)
         else:
-            rows_t, h_t = T.lookup(u_t)
-            rows_c, h_c = C.lookup(u_c)
-            coef, loss_rows = gnn_ops.sgns_fwd_idx(rows_t, None, inv_t, rows_c, None, inv_c, K, gscale)
-            g_t = gnn_ops.sgns_grad(0, ptr_t, lst_t, coef, K, rows_c, None, inv_c, inv_self=inv_t)
-            g_c = gnn_ops.sgns_grad(1, ptr_c, lst_c, coef, K, rows_t, None, inv_t, inv_self=inv_c)
-            T.apply(h_t, g_t)
-            C.apply(h_c, g_c)
+            # target and context rows in one exchange (the id sets are disjoint); rows stay
+            # in the owner-sorted order they arrive in and the index arrays are remapped, so
+            # the gradients come out in send order (no [n, D] permutations)
+            rows, h = tab.lookup(torch.cat([u_t, rows_c_id]), sorted_out=True)
+            n = rows.shape[0]
+            tinv = h.rank[inv_t]
+            cinv = h.rank[n_t + inv_c]
+            coef, loss_rows = gnn_ops.sgns_fwd_idx(rows, None, tinv, rows, None, cinv, K, gscale)
+            ptr_t, lst_t = gnn_ops.occ_csr(tinv, n)
+            ptr_c, lst_c = gnn_ops.occ_csr(cinv, n)
+            g = torch.empty_like(rows)   # every row is a target row or a context row
+            gnn_ops.sgns_grad(0, ptr_t, lst_t, coef, K, rows, None, cinv, inv_self=tinv, out=g)
+            gnn_ops.sgns_grad(1, ptr_c, lst_c, coef, K, rows, None, tinv, inv_self=cinv, out=g)
+            tab.apply(h, g, sorted_in=True)
         self.loss = loss_rows.sum() * gscale
         return self.loss
 
@@ -112,5 +124,10 @@ class DeepWalkTrainer:
     def embedding(self, ids):
         """target embeddings of global ids (inference)."""
         u, inv = gnn_ops.unique_first(ids.reshape(-1).long())
-        rows, _ = self.target.lookup(u)
+        rows, _ = self.table.lookup(u)
+        return rows[inv].view(*ids.shape, self.dim)
+
+    def context_embedding(self, ids):
+        u, inv = gnn_ops.unique_first(ids.reshape(-1).long())
+        rows, _ = self.table.lookup(u + self.off)
         return rows[inv].view(*ids.shape, self.dim)

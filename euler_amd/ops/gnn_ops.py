@@ -487,15 +487,22 @@ def sgns_grad_reference(side, coef, K, src, smap, sinv, n_u, inv_self):
     return torch.zeros(n_u, D, dtype=torch.float32, device=src.device).index_add_(0, inv_self.reshape(-1), per)
 
 
-def sgns_grad(side, ptr, lst, coef, K, src, smap, sinv, inv_self=None):
+def sgns_grad(side, ptr, lst, coef, K, src, smap, sinv, inv_self=None, out=None):
     """per-unique-row gradient ``[n_u, D]`` of one table (side 0 target, 1 context),
     rebuilt from the occurrence lists (no per-pair rows, no atomics).  ``inv_self`` (this
-    side's inverse) is only read by the CPU composition."""
+    side's inverse) is only read by the CPU composition.  With ``out`` the rows that have
+    occurrences on this side are written into it and the others left untouched, so the
+    two sides can fill one buffer."""
     n_u = ptr.numel() - 1
     if use_hip(coef, src):
         return hip().sgns_grad(int(side), ptr, lst, coef.contiguous(), int(K), src.contiguous(), smap,
-                               sinv.contiguous())
-    return sgns_grad_reference(side, coef, K, src, smap, sinv, n_u, inv_self)
+                               sinv.contiguous(), out)
+    g = sgns_grad_reference(side, coef, K, src, smap, sinv, n_u, inv_self)
+    if out is None:
+        return g
+    has = ptr[1:] > ptr[:-1]
+    out[has] = g[has]
+    return out
 
 
 # ----------------------------------------------------------------------------- K10 KG scores

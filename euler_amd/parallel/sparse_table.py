@@ -35,10 +35,12 @@ _KINDS = {"adam": 0, "adagrad": 1, "sgd": 2}
 
 
 class LookupHandle:
-    __slots__ = ("order", "send", "recv", "local_rows", "n")
+    __slots__ = ("order", "send", "recv", "local_rows", "n", "rank")
 
-    def __init__(self, order, send, recv, local_rows, n):
+    def __init__(self, order, send, recv, local_rows, n, rank=None):
         self.order, self.send, self.recv, self.local_rows, self.n = order, send, recv, local_rows, n
+        # sorted_out lookups: position of ids[k] in the returned (owner-sorted) rows
+        self.rank = rank
 
 
 class ShardedTable:
@@ -66,15 +68,22 @@ class ShardedTable:
         self.lr, self.b1, self.b2, self.eps = float(lr), float(beta1), float(beta2), float(eps)
 
     # ------------------------------------------------------------------ forward
-    def lookup(self, ids: torch.Tensor):
+    def lookup(self, ids: torch.Tensor, sorted_out: bool = False):
         """rows [n, D] (fp32) of the DISTINCT global ids ``ids`` (callers de-duplicate
-        with :func:`unique_first`), plus the handle needed by :meth:`apply`."""
+        with :func:`unique_first`), plus the handle needed by :meth:`apply`.
+
+        ``sorted_out``: with collectives the rows are returned in the owner-sorted order
+        they arrive in and ``handle.rank[k]`` is the row of ``ids[k]`` — callers remap
+        their (small) index arrays instead of permuting [n, D] rows twice per step."""
         ids = ids.reshape(-1).long()
         if not self.comm:
-            return self._gather(ids), LookupHandle(None, None, None, ids, ids.numel())
+            rank = torch.arange(ids.numel(), device=ids.device) if sorted_out else None
+            return self._gather(ids), LookupHandle(None, None, None, ids, ids.numel(), rank)
         W = self.world
         owner = torch.remainder(ids, W)
-        order = torch.argsort(owner, stable=True)
+        # stable bucket order by owner: radix sort on a small key
+        key = owner.to(torch.uint8) if W <= 256 else owner
+        order = torch.sort(key, stable=True)[1]
         send_counts = torch.bincount(owner, minlength=W)
         recv_counts = torch.empty_like(send_counts)
         dist.all_to_all_single(recv_counts, send_counts, group=self.group)
@@ -86,6 +95,10 @@ class ShardedTable:
         rows = self._gather(local)
         out_sorted = torch.empty(ids.numel(), self.dim, dtype=rows.dtype, device=rows.device)
         dist.all_to_all_single(out_sorted, rows, send, recv, group=self.group)
+        if sorted_out:
+            rank = torch.empty_like(order)
+            rank[order] = torch.arange(order.numel(), device=order.device)
+            return out_sorted, LookupHandle(order, send, recv, local, ids.numel(), rank)
         out = torch.empty_like(out_sorted)
         out[order] = out_sorted
         return out, LookupHandle(order, send, recv, local, ids.numel())
@@ -96,17 +109,19 @@ class ShardedTable:
         return self.weight[local]
 
     # ------------------------------------------------------------------ backward + update
-    def apply(self, handle: LookupHandle, grad_rows: torch.Tensor):
+    def apply(self, handle: LookupHandle, grad_rows: torch.Tensor, sorted_in: bool = False):
         """Row-sparse optimizer step with ``grad_rows`` [n, D] = gradient of the rows
-        returned by :meth:`lookup` (same order)."""
+        returned by :meth:`lookup` (same order; ``sorted_in``: in the owner-sorted order
+        of a ``sorted_out`` lookup)."""
         g = grad_rows.float().contiguous()
         if self.comm:
-            g_sorted = g[handle.order].contiguous()
+            g_sorted = g if sorted_in else g[handle.order].contiguous()
             recv_g = torch.empty(sum(handle.recv), self.dim, dtype=g.dtype, device=g.device)
             dist.all_to_all_single(recv_g, g_sorted, handle.recv, handle.send, group=self.group)
             rows, g = handle.local_rows, recv_g
             # several ranks may have asked for the same row: merge before the update
-            rows_u, inv = unique_first(rows)
+            # (one rank's ids are distinct already)
+            rows_u, inv = unique_first(rows) if self.world > 1 else (rows, None)
             if rows_u.numel() != rows.numel():
                 acc = torch.zeros(rows_u.numel(), self.dim, dtype=g.dtype, device=g.device)
                 if use_hip(acc, inv):
@@ -143,12 +158,15 @@ class ShardedTable:
         (one rank owns every row, GPU tensors, D % 4 == 0)."""
         return not self.comm and use_hip(self.weight, *tensors) and self.dim % 4 == 0 and self.dim <= 256
 
-    def apply_sgns(self, side, ptr, lst, coef, K, src, smap, sinv, ids):
+    def apply_sgns(self, side, ptr, lst, coef, K, src, smap, sinv, ids, inc_step=True):
         """fused row-sparse update from occurrence lists (embed.hip sgns_update, see
         gnn_ops.sgns_grad): gradients of the unique ids ``ids`` are rebuilt and applied
-        in one pass, no gradient rows are materialised.  Requires :meth:`fused_sgns_ok`."""
+        in one pass, no gradient rows are materialised.  ``inc_step`` advances the
+        optimizer step (once per training step when several updates hit one table).
+        Requires :meth:`fused_sgns_ok`."""
         hip().sgns_apply_(int(side), ptr, lst, coef, int(K), src, smap, sinv, self.weight, self.m, self.v,
-                          ids.contiguous(), self.step, self.lr, self.b1, self.b2, self.eps, self.kind)
+                          ids.contiguous(), self.step, bool(inc_step), self.lr, self.b1, self.b2, self.eps,
+                          self.kind)
 
     def global_ids(self):
         return torch.arange(self.weight.shape[0], device=self.device) * self.world + self.rank

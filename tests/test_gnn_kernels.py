@@ -256,6 +256,7 @@ def test_deepwalk_step_gpu(cuda):
     losses = [float(tr.step()) for _ in range(40)]
     assert all(l == l for l in losses)
     assert sum(losses[-5:]) < sum(losses[:5])
+    assert int(tr.table.step.item()) == 40  # one optimizer step per training step (Adam bias correction)
 
 
 @pytest.mark.gpu
