@@ -398,36 +398,40 @@ __global__ __launch_bounds__(256) void gat_att_bwd_kernel(const T* __restrict__ 
     }
   }
   const int64_t stride = nwaves * rpw;
-  // two rows per lane group per iteration: both rows' loads are in flight together
-  for (int64_t r0 = wave * rpw + lane / lp; r0 < N; r0 += 2 * stride) {
-    const int64_t r1 = r0 + stride;
-    const bool has1 = r1 < N;
+  // RR rows per lane group per iteration: all of their loads are issued before any use
+  constexpr int RR = 4;
+  for (int64_t r0 = wave * rpw + lane / lp; r0 < N; r0 += RR * stride) {
 #pragma unroll
     for (int k = 0; k < MAXCH; ++k) {
       const int c = sub + k * lp;
       if (c >= nch) continue;
       const int h = (c * V) / C;
-      float x0[V], d0[V], x1[V], d1[V];
-      const float gs0 = dal[r0 * H + h], gd0 = dar[r0 * H + h];
-      const float gs1 = has1 ? dal[r1 * H + h] : 0.f, gd1 = has1 ? dar[r1 * H + h] : 0.f;
-      GV<T>::load(z + r0 * HC + c * V, x0);
-      GV<T>::load(dz + r0 * HC + c * V, d0);
-      if (has1) {
-        GV<T>::load(z + r1 * HC + c * V, x1);
-        GV<T>::load(dz + r1 * HC + c * V, d1);
-      } else {
+      float x[RR][V], d[RR][V], gs[RR], gd[RR];
 #pragma unroll
-        for (int v = 0; v < V; ++v) x1[v] = d1[v] = 0.f;
+      for (int q = 0; q < RR; ++q) {
+        const int64_t r = r0 + q * stride;
+        if (r < N) {
+          gs[q] = dal[r * H + h];
+          gd[q] = dar[r * H + h];
+          GV<T>::load(z + r * HC + c * V, x[q]);
+          GV<T>::load(dz + r * HC + c * V, d[q]);
+        } else {
+          gs[q] = gd[q] = 0.f;
+#pragma unroll
+          for (int v = 0; v < V; ++v) x[q][v] = d[q][v] = 0.f;
+        }
       }
 #pragma unroll
-      for (int v = 0; v < V; ++v) {
-        d0[v] += gs0 * as[k][v] + gd0 * ad[k][v];
-        d1[v] += gs1 * as[k][v] + gd1 * ad[k][v];
-        ps[k][v] += gs0 * x0[v] + gs1 * x1[v];
-        pd[k][v] += gd0 * x0[v] + gd1 * x1[v];
+      for (int q = 0; q < RR; ++q) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          d[q][v] += gs[q] * as[k][v] + gd[q] * ad[k][v];
+          ps[k][v] += gs[q] * x[q][v];
+          pd[k][v] += gd[q] * x[q][v];
+        }
+        const int64_t r = r0 + q * stride;
+        if (r < N) GV<T>::store(dz + r * HC + c * V, d[q]);
       }
-      GV<T>::store(dz + r0 * HC + c * V, d0);
-      if (has1) GV<T>::store(dz + r1 * HC + c * V, d1);
     }
   }
   // the rpw row groups of the wave hold partials of the same columns: fold them
@@ -541,10 +545,11 @@ hipError_t eh_gat_att_fwd(const void* z, int is_bf16, int64_t N, int H, int C, c
 }
 
 int eh_gat_att_bwd_blocks(int64_t N, int H, int C, int is_bf16) {
-  // grid-stride: partials stay in registers across rows; <= 1024 block partials
+  // grid-stride: partials stay in registers across rows; <= 2048 block partials (8 waves
+  // per CU of row streams)
   const GatShape sh = gat_shape(H * C, is_bf16 ? 8 : 4);
   const dim3 grid = gat_grid(N > 0 ? N : 1, sh.lp);
-  return static_cast<int>(grid.x > 1024 ? 1024 : grid.x);
+  return static_cast<int>(grid.x > 2048 ? 2048 : grid.x);
 }
 
 hipError_t eh_gat_att_bwd(const void* z, int is_bf16, int64_t N, int H, int C, const float* a_src, const float* a_dst,
