@@ -87,7 +87,8 @@ class GATNet(nn.Module):
             h = F.elu(agg.reshape(-1, H * C))
         # the classifier only runs on the rows the loss reads (same loss and gradients
         # as classifying every node; avoids a 2.4M-row logits tensor and its bias reduce)
-        return self.out(h if rows is None else h[rows])
+        hr = h if rows is None else h[rows]
+        return gnn_ops.tall_linear(hr, self.out.weight, self.out.bias)
 
 
 def csr_seg(csr):
@@ -136,7 +137,7 @@ def main(argv=None):
     def step():
         with torch.autocast("cuda", dtype=torch.bfloat16):
             logits = model(x, csr, train_idx)
-        loss = F.cross_entropy(logits.float(), y_train)
+        loss = gnn_ops.xent(logits, y_train)
         opt.zero_grad(set_to_none=True)
         loss.backward()
         opt.step()

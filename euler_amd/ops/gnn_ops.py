@@ -30,7 +30,7 @@ from euler_amd.ops.mp_ops import SegmentIndex
 
 __all__ = ["EdgeCSR", "gat_aggregate", "gat_aggregate_reference", "RelationTiles", "relation_transform",
            "relation_transform_reference", "sgns_loss", "sgns_loss_reference", "kg_score", "kg_score_reference",
-           "unique_first", "KG_KINDS", "KG_CORRUPT", "sgns_fwd_idx", "occ_csr", "sgns_grad"]
+           "unique_first", "KG_KINDS", "KG_CORRUPT", "sgns_fwd_idx", "occ_csr", "sgns_grad", "tall_linear", "xent"]
 
 
 # ----------------------------------------------------------------------------- edge structures
@@ -214,10 +214,12 @@ def gat_conv(z, a_src, a_dst, csr: EdgeCSR, slope=0.2):
 
 class _TallLinear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, chunk):
+    def forward(ctx, x, w, b, chunk):
         ctx.save_for_backward(x, w)
         ctx.chunk = chunk
-        return x @ w.t().to(x.dtype)
+        ctx.has_bias = b is not None
+        y = x @ w.t().to(x.dtype)
+        return y if b is None else y + b.to(y.dtype)
 
     @staticmethod
     def backward(ctx, dy):
@@ -229,18 +231,38 @@ class _TallLinear(torch.autograd.Function):
         n0 = (n // p) * p
         # dW = dy^T x split over row chunks: P batched GEMMs fill the chip where a single
         # [M x N] x [N x K] reduction GEMM over millions of rows runs on a few workgroups
-        dw = torch.bmm(dy[:n0].view(p, n0 // p, -1).transpose(1, 2), x[:n0].view(p, n0 // p, -1)).float().sum(0)
+        dyv = dy[:n0].view(p, n0 // p, -1)
+        dw = torch.bmm(dyv.transpose(1, 2), x[:n0].view(p, n0 // p, -1)).float().sum(0)
         if n0 < n:
             dw += (dy[n0:].t() @ x[n0:]).float()
-        return dx, dw.to(w.dtype), None
+        db = None
+        if ctx.has_bias:
+            # column sums as the same split-K GEMM (ones^T dy): a plain dim-0 reduction of a
+            # [millions, C] tensor with a few dozen columns runs on a few workgroups
+            ones = torch.ones(p, 1, n0 // p, device=dy.device, dtype=dy.dtype)
+            db = torch.bmm(ones, dyv).float().sum((0, 1))
+            if n0 < n:
+                db += dy[n0:].float().sum(0)
+        return dx, dw.to(w.dtype), db, None
 
 
-def tall_linear(x, weight, chunk=8192):
-    """``x @ weight^T`` for x with millions of rows (full-graph layers): the weight
-    gradient is computed as a split-K batched GEMM instead of one skinny reduction."""
+def tall_linear(x, weight, bias=None, chunk=8192):
+    """``x @ weight^T (+ bias)`` for x with millions of rows (full-graph layers): the
+    weight (and bias) gradients are computed as split-K batched GEMMs instead of one
+    skinny reduction."""
     if x.is_cuda and x.dim() == 2 and x.shape[0] >= 4 * chunk:
-        return _TallLinear.apply(x, weight, chunk)
-    return x @ weight.t().to(x.dtype)
+        return _TallLinear.apply(x, weight, bias, chunk)
+    y = x @ weight.t().to(x.dtype)
+    return y if bias is None else y + bias.to(y.dtype)
+
+
+def xent(logits, labels):
+    """Mean softmax cross-entropy with row-parallel kernels (logsumexp + gather + mean):
+    on ROCm the mean-reduced ``F.cross_entropy`` runs its NLL reduction on one
+    workgroup (~0.5 ms fwd + bwd at 200K rows)."""
+    logits = logits.float()
+    lse = torch.logsumexp(logits, dim=1)
+    return (lse - logits.gather(1, labels.long().view(-1, 1)).squeeze(1)).mean()
 
 
 # ----------------------------------------------------------------------------- K6 relation transform

@@ -53,6 +53,20 @@ def test_relation_reference_matches_loop():
     torch.testing.assert_close(out, ref / cnt.clamp(min=1).unsqueeze(1), atol=1e-4, rtol=1e-4)
 
 
+def test_xent_matches_cross_entropy():
+    torch.manual_seed(3)
+    logits = torch.randn(500, 47, requires_grad=True)
+    y = torch.randint(0, 47, (500,))
+    l1 = G.xent(logits, y)
+    l1.backward()
+    g1 = logits.grad.clone()
+    logits.grad = None
+    l2 = torch.nn.functional.cross_entropy(logits, y)
+    l2.backward()
+    torch.testing.assert_close(l1, l2)
+    torch.testing.assert_close(g1, logits.grad)
+
+
 def test_kg_reference_shapes():
     ent, rel = torch.randn(50, 16), torch.randn(7, 16)
     src, dst, r = torch.randint(0, 50, (8,)), torch.randint(0, 50, (8,)), torch.randint(0, 7, (8,))
@@ -118,17 +132,24 @@ def test_gat_conv_full_graph(cuda, H, C, dtype):
 
 
 @pytest.mark.gpu
-def test_tall_linear_grads(cuda):
+@pytest.mark.parametrize("bias", [False, True])
+def test_tall_linear_grads(cuda, bias):
     torch.manual_seed(14)
-    x = torch.randn(70000, 96, device=cuda).requires_grad_(True)
-    w = torch.randn(64, 96, device=cuda).requires_grad_(True)
-    y = G.tall_linear(x, w, chunk=4096)
+    x = torch.randn(70001, 96, device=cuda).requires_grad_(True)   # 70001: a remainder chunk
+    w = torch.randn(47, 96, device=cuda).requires_grad_(True)
+    b = torch.randn(47, device=cuda).requires_grad_(True) if bias else None
+    y = G.tall_linear(x, w, b, chunk=4096)
     g = torch.randn_like(y)
     (y * g).sum().backward()
     x2, w2 = x.detach().clone().requires_grad_(True), w.detach().clone().requires_grad_(True)
-    ((x2 @ w2.t()) * g).sum().backward()
+    b2 = b.detach().clone().requires_grad_(True) if bias else None
+    y2 = x2 @ w2.t() + (b2 if bias else 0)
+    (y2 * g).sum().backward()
+    torch.testing.assert_close(y, y2, atol=1e-3, rtol=1e-3)
     torch.testing.assert_close(w.grad, w2.grad, atol=5e-2, rtol=1e-3)
     torch.testing.assert_close(x.grad, x2.grad, atol=1e-3, rtol=1e-3)
+    if bias:
+        torch.testing.assert_close(b.grad, b2.grad, atol=5e-2, rtol=1e-3)
 
 
 @pytest.mark.gpu
