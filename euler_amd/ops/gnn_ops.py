@@ -346,6 +346,15 @@ def relation_transform_reference(x, rel, weight, edge_index, size, aggr="mean"):
     return out
 
 
+def _pad_bf16(t, pad):
+    """bf16, contiguous, zero-padded copy — one conversion kernel and no pad copy when the
+    shape is already aligned"""
+    t = t.to(torch.bfloat16)
+    if any(pad):
+        t = F.pad(t, pad)
+    return t.contiguous()
+
+
 class _RelationTransform(torch.autograd.Function):
     """Messages W_rel x_src are stored once per edge (bf16, 16-byte rows) by the grouped
     GEMM and summed per destination by the segment kernel: plain stores + one
@@ -355,8 +364,8 @@ class _RelationTransform(torch.autograd.Function):
     def forward(ctx, x, weight, tiles, n_dst):
         R, N, K = weight.shape
         Kp, Np = _round_up(K, 64), _round_up(N, 64)
-        xb = F.pad(x.to(torch.bfloat16), (0, Kp - K)).contiguous()
-        wb = F.pad(weight.to(torch.bfloat16), (0, Kp - K, 0, Np - N)).contiguous()
+        xb = _pad_bf16(x, (0, Kp - K))
+        wb = _pad_bf16(weight, (0, Kp - K, 0, Np - N))
         msg = torch.empty(tiles.num_edges, Np, device=x.device, dtype=torch.bfloat16)
         tr, ts, tl = tiles.tiles()
         hip().rel_gemm(xb, tiles.src, tr, ts, tl, wb, None, tiles.eid, 0, msg)
@@ -373,7 +382,7 @@ class _RelationTransform(torch.autograd.Function):
         xb, wb = ctx.saved_tensors
         R, N, K, Kp, Np, n_src = ctx.dims
         tiles = ctx.tiles
-        gb = F.pad(dout.to(torch.bfloat16), (0, Np - N)).contiguous()
+        gb = _pad_bf16(dout, (0, Np - N))
         dx = dw = None
         if ctx.needs_input_grad[0]:
             wt = wb.transpose(1, 2).contiguous()  # [R, Kp, Np]
