@@ -22,6 +22,10 @@
 //   API_SAMPLE_ROOT            in [roots, weights] attrs [n, m, default] -> m roots per batch of n
 //   API_LOCAL_SAMPLE_L         in [idx, ids, w, t] attrs [n, m, weight_func, default]
 //   API_SAMPLE_GRAPH_LABEL     attrs [count]                -> labels (strings)
+//   GP_*_MERGE                 graph-partition names of the merges; GP_UNIQUE_MERGE row unique
+//   API_SPARSE_GEN_ADJ         in [roots, l_nb, n]          -> (root, batch) rows, l_nb
+//   API_GATHER_RESULT          in [x_i...]                  -> aliases
+//   API_RESHAPE                in [x] attrs ["d0,?,..."]    -> x with that shape
 #include <cmath>
 #include <unordered_map>
 #include <unordered_set>
@@ -422,6 +426,118 @@ class AsOp : public OpKernel {
   }
 };
 
+// GP_UNIQUE_MERGE: in [d_0, m_0, d_1, m_1, ...] (uint64 rows of equal width; the m_s are
+// ignored) -> 0 the distinct rows over all shards in first-seen order, s+1 for each shard
+// the int32 position of each of its rows in output 0.  Graph-partition mode: the same
+// node can come back from several shards.  Rows are keyed by their full uint64 content
+// (the reference keys by concatenated decimal text, so rows {1, 23} and {12, 3} collide).
+struct RowKey {
+  std::vector<uint64_t> v;
+  bool operator==(const RowKey& o) const { return v == o.v; }
+};
+struct RowKeyHash {
+  size_t operator()(const RowKey& k) const {
+    uint64_t h = 0x9e3779b97f4a7c15ull;
+    for (uint64_t x : k.v) h = (h ^ x) * 0xbf58476d1ce4e5b9ull + (h >> 31);
+    return static_cast<size_t>(h);
+  }
+};
+
+class GpUniqueMergeOp : public OpKernel {
+ public:
+  void Compute(const NodeDef& nd, OpContext* ctx) override {
+    std::vector<Tensor> parts;
+    for (size_t i = 0; i < nd.inputs.size(); i += 2) parts.push_back(ctx->Get(nd.inputs[i]));
+    if (parts.empty()) EULER_THROW("GP_UNIQUE_MERGE needs at least one shard input");
+    const int64_t width = RowWidth(parts[0]);
+    std::unordered_map<RowKey, int32_t, RowKeyHash> pos;
+    std::vector<uint64_t> uniq;
+    std::vector<std::vector<int32_t>> where(parts.size());
+    for (size_t s = 0; s < parts.size(); ++s) {
+      if (RowWidth(parts[s]) != width && Rows(parts[s]) > 0) EULER_THROW("GP_UNIQUE_MERGE: row widths differ");
+      const auto vals = parts[s].ToUInt64();
+      const int64_t n = Rows(parts[s]);
+      where[s].resize(n);
+      for (int64_t r = 0; r < n; ++r) {
+        RowKey k{std::vector<uint64_t>(vals.begin() + r * width, vals.begin() + (r + 1) * width)};
+        auto it = pos.find(k);
+        if (it == pos.end()) {
+          it = pos.emplace(k, static_cast<int32_t>(uniq.size() / std::max<int64_t>(width, 1))).first;
+          uniq.insert(uniq.end(), k.v.begin(), k.v.end());
+        }
+        where[s][r] = it->second;
+      }
+    }
+    std::vector<int64_t> shape = parts[0].shape();
+    if (shape.empty()) shape = {0};
+    shape[0] = static_cast<int64_t>(pos.size());
+    ctx->Set(nd.Output(0), Tensor::FromVector(uniq, shape));
+    for (size_t s = 0; s < parts.size(); ++s) ctx->Set(nd.Output(static_cast<int>(s) + 1), Tensor::FromVector(where[s]));
+  }
+};
+
+// API_SPARSE_GEN_ADJ: in [roots (b*n ids), l_nb, n] -> 0 (root id, batch number) uint64
+// rows [b*n, 2], 1 l_nb passed through (the two inputs of API_SPARSE_GET_ADJ's split)
+class SparseGenAdjOp : public OpKernel {
+ public:
+  void Compute(const NodeDef& nd, OpContext* ctx) override {
+    const Tensor& roots = ctx->Get(nd.inputs.at(0));
+    const int64_t n = nd.inputs.size() > 2 ? ctx->AttrInt(nd.inputs[2]) : ctx->AttrInt(nd.attrs.at(0));
+    if (n <= 0) EULER_THROW("API_SPARSE_GEN_ADJ: n must be positive");
+    const auto ids = roots.ToUInt64();
+    const int64_t total = static_cast<int64_t>(ids.size());
+    if (total % n != 0) EULER_THROW("API_SPARSE_GEN_ADJ: " << total << " roots are not batches of " << n);
+    std::vector<uint64_t> rb(2 * total);
+    for (int64_t c = 0; c < total; ++c) {
+      rb[2 * c] = ids[c];
+      rb[2 * c + 1] = static_cast<uint64_t>(c / n);
+    }
+    ctx->Set(nd.Output(0), Tensor::FromVector(rb, {total, 2}));
+    ctx->Set(nd.Output(1), ctx->Get(nd.inputs.at(1)));
+  }
+};
+
+// API_GATHER_RESULT: outputs i alias inputs i (collects a sub-DAG's results under one node)
+class GatherResultOp : public OpKernel {
+ public:
+  void Compute(const NodeDef& nd, OpContext* ctx) override {
+    for (size_t i = 0; i < nd.inputs.size(); ++i) ctx->Set(nd.Output(static_cast<int>(i)), ctx->Get(nd.inputs[i]));
+  }
+};
+
+// API_RESHAPE: in [x] attrs ["d0,d1,..."] (one "?" inferred) -> x viewed with that shape
+class ReshapeOp : public OpKernel {
+ public:
+  void Compute(const NodeDef& nd, OpContext* ctx) override {
+    Tensor x = ctx->Get(nd.inputs.at(0));
+    const std::string spec = nd.inputs.size() > 1 ? ctx->AttrStr(nd.inputs[1]) : nd.attrs.at(0);
+    std::vector<int64_t> shape;
+    int unknown = -1;
+    int64_t known = 1;
+    for (auto& tok : Split(spec, ",")) {
+      const std::string t = Trim(tok);
+      if (t == "?" || t == "-1") {
+        if (unknown >= 0) EULER_THROW("API_RESHAPE: more than one unknown dimension in '" << spec << "'");
+        unknown = static_cast<int>(shape.size());
+        shape.push_back(0);
+      } else {
+        int64_t d;
+        if (!ParseInt64(t, &d) || d < 0) EULER_THROW("API_RESHAPE: bad dimension '" << t << "'");
+        shape.push_back(d);
+        known *= d;
+      }
+    }
+    if (unknown >= 0) {
+      if (known == 0 || x.numel() % known != 0) EULER_THROW("API_RESHAPE: " << x.numel() << " elements vs '" << spec << "'");
+      shape[unknown] = x.numel() / known;
+    } else if (known != x.numel()) {
+      EULER_THROW("API_RESHAPE: " << x.numel() << " elements vs '" << spec << "'");
+    }
+    x.Reshape(shape);  // shares the (immutable) storage
+    ctx->Set(nd.Output(0), x);
+  }
+};
+
 void ReadNeighbors(OpContext* ctx, const NodeDef& nd, std::vector<std::vector<IdWeightType>>* rows) {
   const Tensor& idx = ctx->Get(nd.inputs.at(0));
   const Tensor& ids = ctx->Get(nd.inputs.at(1));
@@ -567,6 +683,16 @@ REGISTER_OP_KERNEL("API_GET_NB_FILTER", NbFilterOp);
 REGISTER_OP_KERNEL("API_SAMPLE_ROOT", SampleRootOp);
 REGISTER_OP_KERNEL("API_LOCAL_SAMPLE_L", LocalSampleLayerOp);
 REGISTER_OP_KERNEL("API_SAMPLE_GRAPH_LABEL", SampleGraphLabelOp);
+// graph-partition variants: same merges (ids may repeat across partitions; the merges
+// never assume disjoint shards), plus the row-level unique merge
+REGISTER_OP_KERNEL("GP_APPEND_MERGE", AppendMergeOp);
+REGISTER_OP_KERNEL("GP_IDX_MERGE", IdxMergeOp);
+REGISTER_OP_KERNEL("GP_DATA_MERGE", DataMergeOp);
+REGISTER_OP_KERNEL("GP_REGULAR_DATA_MERGE", RegularDataMergeOp);
+REGISTER_OP_KERNEL("GP_UNIQUE_MERGE", GpUniqueMergeOp);
+REGISTER_OP_KERNEL("API_SPARSE_GEN_ADJ", SparseGenAdjOp);
+REGISTER_OP_KERNEL("API_GATHER_RESULT", GatherResultOp);
+REGISTER_OP_KERNEL("API_RESHAPE", ReshapeOp);
 
 void LinkDistOps() {}
 

@@ -257,3 +257,33 @@ def test_builder_and_synthetic():
     assert "nodes=2000" in s.summary()
     f = ea.get_dense_feature([0, 1], ["feature"], [8])[0]
     assert f.shape == (2, 8)
+
+
+def test_plumbing_ops_via_run_op(graph):
+    """Engine ops of the graph-partition / adjacency plumbing: GP_* merges,
+    GP_UNIQUE_MERGE (row-level, no text-key collisions), API_SPARSE_GEN_ADJ,
+    API_GATHER_RESULT, API_RESHAPE."""
+    eng = ea.get_engine()
+    u64 = lambda *v: np.asarray(v, dtype=np.uint64)  # noqa: E731
+    # rows {1, 23} and {12, 3} are distinct (decimal-concatenation keys would merge them)
+    a = u64(1, 23, 5, 6).reshape(2, 2)
+    b = u64(12, 3, 1, 23).reshape(2, 2)
+    out = eng.run_op("GP_UNIQUE_MERGE", {"a": a, "m0": np.zeros(2, np.int32), "b": b, "m1": np.zeros(2, np.int32)},
+                     ["a", "m0", "b", "m1"], [], 3)
+    assert out[0].reshape(-1, 2).tolist() == [[1, 23], [5, 6], [12, 3]]
+    assert out[1].tolist() == [0, 1] and out[2].tolist() == [2, 0]
+    # GP_APPEND_MERGE = APPEND_MERGE
+    out = eng.run_op("GP_APPEND_MERGE", {"a": u64(1, 2), "b": u64(3)}, ["a", "b"], [], 1)
+    assert out[0].tolist() == [1, 2, 3]
+    # (root, batch) pairs; l_nb passed through
+    out = eng.run_op("API_SPARSE_GEN_ADJ", {"r": u64(10, 11, 12, 13), "l": u64(7, 8), "n": np.asarray([2], np.int32)},
+                     ["r", "l", "n"], [], 2)
+    assert out[0].reshape(-1, 2).tolist() == [[10, 0], [11, 0], [12, 1], [13, 1]]
+    assert out[1].tolist() == [7, 8]
+    out = eng.run_op("API_GATHER_RESULT", {"x": u64(1), "y": np.asarray([2.5], np.float32), "z": u64(3)},
+                     ["x", "y", "z"], [], 3)
+    assert [o.tolist() for o in out] == [[1], [2.5], [3]]
+    out = eng.run_op("API_RESHAPE", {"x": np.arange(6, dtype=np.int32)}, ["x"], ["?,3"], 1)
+    assert out[0].shape == (2, 3) and out[0].tolist() == [[0, 1, 2], [3, 4, 5]]
+    with pytest.raises(Exception):
+        eng.run_op("API_RESHAPE", {"x": np.arange(6, dtype=np.int32)}, ["x"], ["4,?"], 1)
