@@ -120,7 +120,7 @@ __global__ __launch_bounds__(256) void rel_gemm_kernel(const bf16_t* __restrict_
 // dW for one (chunk of <= RG_CH edges of ONE relation, T x T slab of dW[rel]) per workgroup:
 // the chunk's 64-edge sub-tiles are staged in LDS and accumulated in registers, so each dW
 // element receives one write per chunk instead of one atomic per 64-edge tile.
-constexpr int RG_CH = 1024;  // edges per dW chunk
+constexpr int RG_CH = 512;  // edges per dW chunk (256: same time, more atomics; 1024: long serial chunks)
 
 // MFMA fragments of dW = Gs^T X straight from edge-major LDS images with the gfx950
 // transposing read ds_read_b64_tr_b16: a 16-lane group reads a 4-edge x 16-column block and
