@@ -95,16 +95,19 @@ def test_gather_rows(cuda, dtype, idx_dtype):
 
 
 @pytest.mark.parametrize("reduce", ["add", "mean", "max"])
-def test_scatter_ops_match_cpu(cuda, reduce):
+@pytest.mark.parametrize("D,dtype", [(19, torch.float32), (64, torch.float32), (64, torch.bfloat16)])
+def test_scatter_ops_match_cpu(cuda, reduce, D, dtype):
+    """scalar path (D = 19) and the 16-byte-vector path (D % 4 fp32, D % 8 bf16)"""
     from euler_amd.ops import mp_ops
 
     torch.manual_seed(4)
-    E, S, D = 3000, 200, 19
-    src = torch.randn(E, D)
-    idx = torch.randint(0, S, (E,))
-    ref = mp_ops._cpu_scatter(src, idx, S, reduce)
+    E, S = 3000, 230   # some segments stay empty
+    src = torch.randn(E, D).to(dtype)
+    idx = torch.randint(0, S - 20, (E,))
+    ref = mp_ops._cpu_scatter(src.float(), idx, S, reduce)
     out = mp_ops.scatter_(reduce, src.to(cuda), idx.to(cuda), S)
-    torch.testing.assert_close(out.cpu(), ref, atol=1e-5, rtol=1e-5)
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    torch.testing.assert_close(out.float().cpu(), ref, atol=tol, rtol=tol)
 
 
 @pytest.mark.parametrize("reduce", ["add", "mean", "max"])
