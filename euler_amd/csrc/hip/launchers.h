@@ -58,7 +58,7 @@ hipError_t eh_st_sage_fwd(const void* x, int D, const int32_t* self_idx, const i
 hipError_t eh_st_tree_mean(const void* h0, int H, int64_t B, int F1, int include_self, float inv_cnt, void* A1,
                            hipStream_t s);
 // rows per block of the fused head kernel (sage_train.hip)
-constexpr int kStHeadRows = 32;
+constexpr int kStHeadRows = 16;
 hipError_t eh_st_head(const void* A1, int B, int H, int C, const void* W1b, const void* Wfc, const void* WfcT,
                       const float* bfc, const void* Wout, const void* WoutT, const void* W1T, const int32_t* label_idx,
                       float inv_scale, void* A1_kt, void* h1_kt, void* emb_kt, void* dlog_kt, void* demb_kt,
