@@ -7,13 +7,13 @@ synthetic graph".  Config (defaults): 100M-node power-law synthetic graph (avg d
 (reference examples/graphsage: SAGEConv x2 + fc + out_fc, sigmoid CE, Adam), fanouts
 [25, 10], 1024 roots per GPU per step (weak scaling), hidden 256.
 
-One process per GPU (torchrun); every rank holds the whole graph + feature table
-resident in its own HBM and samples on the GPU; dense gradients are synchronised
-with one flat RCCL all-reduce per step.  One "step" = sample roots + 2 hops of
-neighbor sampling + forward + backward + all-reduce + optimizer update; nothing is
-skipped inside the timed region.  On one GPU the whole step is a single hipGraph
-replay; with N>1 the forward/backward and the optimizer are two graphs around an
-eager all-reduce.
+The step is the framework's training path, euler_amd.models.sage_trainer.SageTrainer
+(the same class NodeEstimator(device_graph=True) drives on loaded datasets): roots +
+2 hops of neighbour sampling on the GPU, forward, backward, optimizer — four gfx950
+launches captured in one hipGraph.  One process per GPU (torchrun): every rank holds
+the whole graph + feature table in its own HBM with its own sample stream; the flat
+fp32 gradient is all-reduced over RCCL inside the captured step.  Nothing is skipped
+inside the timed region.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [...]
 """
@@ -44,22 +44,16 @@ def parse_args(argv=None):
     p.add_argument("--batch-size", type=int, default=1024, help="roots per GPU per step")
     p.add_argument("--fanouts", type=str, default="25,10")
     p.add_argument("--feature-dim", type=int, default=128)
+    p.add_argument("--feature-dtype", choices=["bf16", "fp32"], default="bf16",
+                   help="storage dtype of the HBM feature table (GEMMs are bf16 MFMA either way)")
     p.add_argument("--hidden-dim", type=int, default=256)
     p.add_argument("--label-dim", type=int, default=64)
     p.add_argument("--lr", type=float, default=0.01)
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--no-graph", action="store_true", help="eager steps instead of hipGraph replay")
-    p.add_argument("--impl", choices=["fused", "autograd"], default="fused",
-                   help="fused = the 10-kernel gfx950 training step (models/sage_step.py); "
-                        "autograd = fused SAGE layers under torch autograd (models/fused_sage.py)")
     p.add_argument("--log", action="store_true")
     p.add_argument("--force-dist", action="store_true",
-                   help="take the multi-GPU code path (process group, graph segments around the gradient "
-                        "all-reduce) even with one rank: validates that path on a single GPU")
-    p.add_argument("--grad-sync", choices=["graph", "single", "overlap"], default="graph",
-                   help="N>1: graph = the RCCL all-reduce is captured into the step's hipGraph (one replay per "
-                        "step, no host launches in between); single = eager all-reduce between two graph "
-                        "segments; overlap = fused impl, all-reduce W1/fc/out grads while dW0 is computed")
+                   help="take the multi-GPU code path (process group, all-reduce in the step) even with one rank")
     return p.parse_args(argv)
 
 
@@ -98,171 +92,49 @@ def main(argv=None):
     torch.cuda.set_device(dev)
 
     from euler_amd.graph.device_graph import DeviceGraph
-    from euler_amd.models.fused_sage import FusedSupervisedGraphSage, synthetic_features, synthetic_labels
-    from euler_amd.parallel.flat import FlatOptimizer, FlatParams
+    from euler_amd.models.fused_sage import synthetic_features, synthetic_labels
+    from euler_amd.models.sage_trainer import SageTrainer
 
     fanouts = [int(x) for x in args.fanouts.split(",")]
     B = args.batch_size
     t0 = time.time()
     graph = DeviceGraph.synthetic(args.num_nodes, args.avg_degree, args.max_degree, seed=args.seed, device=dev)
     graph.manual_seed(args.seed * 7919 + rank)  # different root/neighbor draws per rank
-    feats = synthetic_features(args.num_nodes, args.feature_dim, args.seed + 1, dev)
+    fdt = torch.bfloat16 if args.feature_dtype == "bf16" else torch.float32
+    feats = synthetic_features(args.num_nodes, args.feature_dim, args.seed + 1, dev, dtype=fdt)
     labels = synthetic_labels(feats, args.label_dim)
     torch.cuda.synchronize()
     if rank == 0:
         log(f"graph: {graph.num_rows} nodes, {graph.num_edges} edges, csr {graph.nbytes()/2**30:.2f} GiB, "
-            f"features {feats.numel()*2/2**30:.2f} GiB, build {time.time()-t0:.1f}s")
+            f"features {feats.numel()*feats.element_size()/2**30:.2f} GiB ({args.feature_dtype}), "
+            f"build {time.time()-t0:.1f}s")
 
-    torch.manual_seed(args.seed)
-    model = FusedSupervisedGraphSage(args.feature_dim, args.hidden_dim, args.label_dim, fanouts).to(dev)
-    grad_scale = 1.0 / world
-    if args.impl == "fused":
-        from euler_amd.models.sage_step import FusedSageTrainer
+    dims = [args.hidden_dim] * (len(fanouts) + 1)  # reference run_graphsage: [hidden] * (layers + 1)
+    tr = SageTrainer(graph, B, fanouts, dims, args.label_dim, features=feats, labels=labels, learning_rate=args.lr,
+                     init_seed=args.seed, keep_samples=False)
+    grad_sync = None
+    if dist_on:
+        dist.broadcast(tr.flat, 0)
+        tr.refresh_shadows()
 
-        trainer = FusedSageTrainer(graph, feats, labels, B, fanouts, args.hidden_dim, args.label_dim, lr=args.lr,
-                                   init_model=model)
-        if dist_on:
-            dist.broadcast(trainer.flat, 0)
-            trainer.refresh_shadows()
-        loss_buf = trainer.loss_out
-        grad_buf = trainer.grad
-
-        def fwd_bwd():
-            trainer.forward_backward()
-
-        def opt_step():
-            trainer.optimizer_step(grad_scale=grad_scale)
-    else:
-        flat = FlatParams(model.parameters(), dev)
-        if dist_on:
-            dist.broadcast(flat.flat, 0)
-        opt = FlatOptimizer(flat, "adam", args.lr)
-        loss_buf = torch.zeros((), device=dev)
-        grad_buf = flat.grad
-
-        def fwd_bwd():
-            graph.advance()
-            roots = graph.sample_node(B, stream_id=1)
-            levels, nbrs = model.sample(graph, roots)
-            logits = model(feats, levels, nbrs)
-            loss = model.loss(logits, labels[roots.long()])
-            flat.zero_grad()
-            loss.backward()
-            loss_buf.copy_(loss.detach())
-
-        def opt_step():
-            opt.step(grad_scale=grad_scale)
-
-    def allreduce():
-        if dist_on:
-            dist.all_reduce(grad_buf)
-
-    # fused impl, N > 1: all-reduce the W1/fc/out_fc gradients (77 % of the bytes) on RCCL's
-    # stream while the outer layer's dW0 is still being computed, then W0's
-    overlap = (args.impl == "fused" and dist_on and args.grad_sync == "overlap" and not trainer.pipelined)
-
-    def synced_step(head, outer, opt):
-        head()
-        w1 = dist.all_reduce(trainer.grad_bucket_head, async_op=True)
-        outer()
-        w2 = dist.all_reduce(trainer.grad_bucket_outer, async_op=True)
-        w1.wait()  # stream-ordered: the optimizer kernels wait for both reductions
-        w2.wait()
-        opt()
-
-    def eager_step():
-        if overlap:
-            synced_step(lambda: trainer.forward_backward("head"), lambda: trainer.forward_backward("outer"), opt_step)
-        else:
-            fwd_bwd()
-            allreduce()
-            opt_step()
+        def grad_sync(g):
+            dist.all_reduce(g)
+            return 1.0 / world
 
     use_graph = not args.no_graph
     if use_graph:
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(3):
-                eager_step()
-        torch.cuda.current_stream().wait_stream(s)
-        torch.cuda.synchronize()
-        if args.impl == "autograd":
-            flat.rebind_grads()
-        # the fused trainer double-buffers its samples (next step's roots/hops are drawn on a
-        # side stream during this step): one captured graph per sample-set parity
-        pipelined = args.impl == "fused" and trainer.pipelined
-        parities = (0, 1) if pipelined else (0,)
+        tr.capture(grad_sync)
 
-        def parity():
-            return trainer.parity if pipelined else 0
-
-        def next_parity():
-            if pipelined:
-                trainer.advance_parity()
-
-        captured = False
-        if not dist_on or args.grad_sync == "graph":
-            # one graph per step; with N > 1 the flat-gradient all-reduce is captured too
-            # (RCCL kernels inside the hipGraph)
-            try:
-                g_all = {}
-                for _ in parities:
-                    p_ = parity()
-                    g_all[p_] = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g_all[p_]):
-                        fwd_bwd()
-                        allreduce()
-                        opt_step()
-                # capture toggled the parity once per graph: back where the eager warmup left it
-                captured = True
-            except Exception as e:  # pragma: no cover - RCCL capture unsupported: graph segments
-                if not dist_on:
-                    raise
-                log(f"all-reduce capture failed ({e!r}); falling back to --grad-sync single")
-                args.grad_sync = "single"
-                torch.cuda.synchronize()
-                if pipelined:  # the failed capture toggled the parity
-                    trainer.advance_parity()
-
-        if captured:
-            def step():
-                g_all[parity()].replay()
-                next_parity()
-        elif overlap:
-            g_head, g_outer, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g_head):
-                trainer.forward_backward("head")
-            with torch.cuda.graph(g_outer):
-                trainer.forward_backward("outer")
-            with torch.cuda.graph(g_opt):
-                opt_step()
-
-            def step():
-                synced_step(g_head.replay, g_outer.replay, g_opt.replay)
-        else:
-            g_fb = {}
-            for _ in parities:
-                p_ = parity()
-                g_fb[p_] = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g_fb[p_]):
-                    fwd_bwd()
-            g_opt = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g_opt):
-                opt_step()
-
-            def step():
-                g_fb[parity()].replay()
-                next_parity()
-                allreduce()
-                g_opt.replay()
+        def step():
+            tr.replay()
     else:
-        step = eager_step
+        def step():
+            tr.step(grad_sync)
 
-    for i in range(args.warmup):
+    for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    first_loss = float(loss_buf.item())
+    first_loss = float(tr.loss.item())
 
     if dist_on:
         dist.barrier()
@@ -272,7 +144,7 @@ def main(argv=None):
         step()
         if args.log and rank == 0 and (i + 1) % 50 == 0:
             torch.cuda.synchronize()
-            log(f"step {i+1} loss {float(loss_buf.item()):.4f}")
+            log(f"step {i+1} loss {float(tr.loss.item()):.4f}")
     torch.cuda.synchronize()
     if dist_on:
         dist.barrier()
@@ -281,7 +153,7 @@ def main(argv=None):
     if dist_on:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
-    last_loss = float(loss_buf.item())
+    last_loss = float(tr.loss.item())
     ms = elapsed * 1000.0 / max(args.steps, 1)
     value = world * B * args.steps / elapsed
     base_value, base_note = _cpu_baseline()
@@ -309,11 +181,12 @@ def main(argv=None):
                 "num_edges": graph.num_edges,
                 "fanouts": fanouts,
                 "feature_dim": args.feature_dim,
+                "feature_dtype": args.feature_dtype,
                 "hidden_dim": args.hidden_dim,
                 "label_dim": args.label_dim,
                 "hipgraph": use_graph,
-                "grad_sync": ("overlap" if overlap else args.grad_sync) if dist_on else None,
-                "impl": args.impl,
+                "grad_sync": "rccl all-reduce in the captured step" if dist_on else None,
+                "impl": "euler_amd.models.sage_trainer.SageTrainer (4 fused gfx950 launches per step)",
                 "loss_first_last": [round(first_loss, 4), round(last_loss, 4)],
                 "baseline": base_note,
             },

@@ -381,6 +381,23 @@ class Engine {
     return py::make_tuple(indptr, nbr, w, g.num_edge_types(), ids, nw);
   }
 
+  // per-row node ids, types and weights (row order of ExportCsr), for HBM upload
+  py::tuple ExportNodes() {
+    Graph& g = LocalGraph();
+    const int64_t n = g.num_nodes();
+    py::array_t<uint64_t> ids(n);
+    py::array_t<int32_t> types(n);
+    py::array_t<float> w(n);
+    memcpy(ids.mutable_data(), g.node_ids().data(), n * 8);
+    int32_t* pt = types.mutable_data();
+    float* pw = w.mutable_data();
+    for (int64_t r = 0; r < n; ++r) {
+      pt[r] = g.NodeType(r);
+      pw[r] = g.NodeWeight(r);
+    }
+    return py::make_tuple(ids, types, w);
+  }
+
   std::string Summary() const {
     Graph* g = proxy_->local_graph();
     return g ? g->Summary() : std::string("remote engine (") + proxy_->mode() + ")";
@@ -499,7 +516,8 @@ PYBIND11_MODULE(_engine, m) {
       .def("sage_flow", &Engine::SageFlow, py::arg("roots"), py::arg("edge_types"), py::arg("counts"),
            py::arg("default_node"), py::arg("self_loops") = true)
       .def("dense_feature", &Engine::DenseFeature)
-      .def("export_csr", &Engine::ExportCsr);
+      .def("export_csr", &Engine::ExportCsr)
+      .def("export_nodes", &Engine::ExportNodes);
 
   py::class_<PyBuilder>(m, "GraphBuilder")
       .def(py::init<>())

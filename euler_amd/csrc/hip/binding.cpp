@@ -713,9 +713,12 @@ void st_shadow(torch::Tensor p, std::vector<int64_t> sh_off, std::vector<int64_t
 
 // binding_gnn.cpp: GAT / R-GCN / embedding-loss / unique kernels
 void register_gnn_ops(pybind11::module& m);
+// binding_tree.cpp: fused GraphSAGE tree-step plan
+void register_tree_ops(pybind11::module& m);
 
 PYBIND11_MODULE(_hip_ops, m) {
   register_gnn_ops(m);
+  register_tree_ops(m);
   m.doc() = "euler_amd hand-written CDNA4 (gfx950) HIP kernels";
   m.attr("arch") = "gfx950";
   m.def("rng_advance", &rng_advance);

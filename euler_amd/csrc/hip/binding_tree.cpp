@@ -1,0 +1,473 @@
+// torch binding of the fused GraphSAGE tree step (sage_tree.hip).
+//
+// A TreePlan is built once per trainer from a dict of device tensors and sizes: every
+// operand is validated here (dtype, device, contiguity and the exact element count the
+// kernels' grids assume), the kernel argument blocks are filled once, and the per-step
+// methods only launch on torch's current stream (hipGraph-capturable, no allocation,
+// no host sync, no per-call Python marshalling).
+#include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime_api.h>
+#include <torch/extension.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "hip/tree_args.h"
+
+namespace py = pybind11;
+using namespace euler_hip;
+
+namespace {
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+// EULER_AMD_TREE_SYNC=1: synchronise after every launch and name the kernel that failed
+// (debugging aid; never set it for timing or graph capture)
+bool sync_debug() {
+  static const bool on = [] {
+    const char* e = std::getenv("EULER_AMD_TREE_SYNC");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+void ok(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, "euler_amd tree kernel '", what, "' failed: ", hipGetErrorString(e));
+  if (sync_debug()) {
+    const hipError_t s = hipStreamSynchronize(c10::hip::getCurrentHIPStream().stream());
+    TORCH_CHECK(s == hipSuccess, "euler_amd tree kernel '", what, "' faulted: ", hipGetErrorString(s));
+    fprintf(stderr, "[tree-sync] %s ok\n", what);
+  }
+}
+
+class TreePlan {
+ public:
+  explicit TreePlan(py::dict d) : d_(d) {
+    L_ = geti("L");
+    B_ = geti("B");
+    TORCH_CHECK(L_ >= 1 && L_ <= 3, "TreePlan: 1..3 hops");
+    TORCH_CHECK(B_ > 0 && B_ % 32 == 0, "TreePlan: batch must be a positive multiple of 32");
+    F_ = getv("F");
+    logP_ = getv("logP");  // logP[k] for levels k = 1..L-1 (index 0 unused)
+    masks_ = getv("masks");
+    dims_ = getv("H");     // padded conv widths H_0..H_{L-1}
+    TORCH_CHECK((int)F_.size() == L_ + 1 && (int)masks_.size() == L_ + 1 && (int)logP_.size() >= L_ &&
+                    (int)dims_.size() == L_,
+                "TreePlan: F/masks need L+1 entries (index 0 unused), logP L, H L");
+    D_ = geti("D");
+    E_ = geti("E");
+    C_ = geti("C");
+    C_real_ = geti("C_real");
+    self_ = geti("include_self");
+    dev_ = T("rng").device();
+    TORCH_CHECK(dev_.is_cuda(), "TreePlan: tensors must be on the GPU");
+    for (int k = 1; k < L_; ++k) TORCH_CHECK(logP_[k] >= 4 && (1 << logP_[k]) > F_[k], "TreePlan: slot group too small");
+    for (int k = 0; k < L_; ++k) TORCH_CHECK(dims_[k] % 64 == 0, "TreePlan: conv widths must be padded to 64");
+    TORCH_CHECK(D_ % 16 == 0 && E_ % 32 == 0 && C_ % 32 == 0 && C_real_ <= C_, "TreePlan: padded dims");
+    // level sizes M[k] = B * P1 * ... * Pk
+    M_.assign(L_, 0);
+    M_[0] = B_;
+    for (int k = 1; k < L_; ++k) M_[k] = M_[k - 1] << logP_[k];
+    build_graph();
+    build_fwd();
+    build_head();
+    build_dw();
+    build_opt();
+  }
+
+  void fwd() {
+    const c10::DeviceGuard g(dev_);
+    ok(eh_tr_fwd(&fwd0_, L_ == 1 ? 1 : 0, feat_fp32_, bm0_, stream()), "tr_fwd");
+    if (L_ == 3) ok(eh_tr_fwd(&fwd1_, 2, 0, bm1_, stream()), "tr_fwd(inner)");
+  }
+
+  void head(c10::optional<torch::Tensor> prof) {
+    const c10::DeviceGuard g(dev_);
+    TrHeadArgs a = head_;
+    if (prof.has_value()) {
+      need(*prof, torch::kInt64, (B_ / kTrHeadRows) * 8, "prof");
+      a.prof = reinterpret_cast<long long*>(prof->data_ptr<int64_t>());
+    }
+    ok(eh_tr_head(&a, B_, stream()), "tr_head");
+  }
+
+  void bwd() {
+    if (L_ != 3) return;
+    const c10::DeviceGuard g(dev_);
+    ok(eh_tr_bwd(&bwd1_, stream()), "tr_bwd");
+  }
+
+  void dw(std::vector<int64_t> which) {
+    const c10::DeviceGuard g(dev_);
+    TrDwProbs p{};
+    for (int64_t i : which) {
+      TORCH_CHECK(i >= 0 && i < (int64_t)probs_.size(), "dw: problem index out of range");
+      p.p[p.n++] = probs_[i];
+    }
+    if (p.n == 0) return;
+    ok(eh_tr_dw(&p, stream()), "tr_dw");
+  }
+
+  // mode 0 reduce, 1 optimizer, 2 fused, 3 shadows only
+  void opt(int64_t mode, double grad_scale) {
+    const c10::DeviceGuard g(dev_);
+    TrOptArgs a = opt_;
+    a.grad_scale = static_cast<float>(grad_scale);
+    ok(eh_tr_opt(&a, static_cast<int>(mode), stream()), "tr_opt");
+  }
+
+  void set_lr(double lr) { opt_.lr = static_cast<float>(lr); }
+  int64_t num_problems() const { return (int64_t)probs_.size(); }
+  std::vector<int64_t> splits() const {
+    std::vector<int64_t> s;
+    for (const auto& p : probs_) s.push_back((p.MB + p.kps - 1) / p.kps);
+    return s;
+  }
+
+ private:
+  py::dict d_;
+  int L_, B_, D_, E_, C_, C_real_, self_;
+  int feat_fp32_ = 0, bm0_ = 32, bm1_ = 32;
+  std::vector<int64_t> F_, logP_, masks_, dims_, M_;
+  c10::Device dev_{c10::kCPU};
+  TrGraph graph_{};
+  TrTree tree_{};
+  TrFwdArgs fwd0_{}, fwd1_{};
+  TrHeadArgs head_{};
+  TrBwdArgs bwd1_{};
+  std::vector<TrDwProb> probs_;
+  std::vector<torch::Tensor> owned_;
+  TrOptArgs opt_{};
+
+  bool has(const char* k) const { return d_.contains(k) && !d_[k].is_none(); }
+  int64_t geti(const char* k) const {
+    TORCH_CHECK(d_.contains(k), "TreePlan: missing '", k, "'");
+    return d_[k].cast<int64_t>();
+  }
+  double getf(const char* k) const { return d_[k].cast<double>(); }
+  std::vector<int64_t> getv(const char* k) const {
+    TORCH_CHECK(d_.contains(k), "TreePlan: missing '", k, "'");
+    return d_[k].cast<std::vector<int64_t>>();
+  }
+  torch::Tensor T(const char* k) const {
+    TORCH_CHECK(has(k), "TreePlan: missing tensor '", k, "'");
+    return d_[k].cast<torch::Tensor>();
+  }
+  torch::Tensor Tk(const std::string& k) const { return T(k.c_str()); }
+  void need(const torch::Tensor& t, c10::ScalarType st, int64_t numel, const std::string& name) const {
+    TORCH_CHECK(t.is_cuda() && t.device() == dev_, name, " must be on the trainer's GPU");
+    TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+    TORCH_CHECK(t.scalar_type() == st, name, " has the wrong dtype");
+    if (numel >= 0) TORCH_CHECK(t.numel() == numel, name, " has ", t.numel(), " elements, expected ", numel);
+  }
+  template <typename P>
+  P* ptr(const std::string& k, c10::ScalarType st, int64_t numel) {
+    torch::Tensor t = Tk(k);
+    need(t, st, numel, k);
+    return reinterpret_cast<P*>(t.data_ptr());
+  }
+  uint16_t* bf(const std::string& k, int64_t numel) { return ptr<uint16_t>(k, torch::kBFloat16, numel); }
+  float* f32(const std::string& k, int64_t numel) { return ptr<float>(k, torch::kFloat32, numel); }
+  int32_t* i32(const std::string& k, int64_t numel) { return ptr<int32_t>(k, torch::kInt32, numel); }
+
+  int64_t Hin(int k) const { return k == 0 ? D_ : dims_[k - 1]; }
+
+  void build_graph() {
+    torch::Tensor indptr = T("indptr"), rng = T("rng");
+    need(indptr, torch::kInt64, -1, "indptr");
+    need(rng, torch::kInt64, 2, "rng");
+    const int64_t T_ = geti("num_types");
+    TORCH_CHECK(T_ >= 1 && T_ <= 32 && (indptr.numel() - 1) % T_ == 0, "TreePlan: indptr must be [N*T+1]");
+    graph_.indptr = indptr.data_ptr<int64_t>();
+    graph_.num_types = static_cast<int32_t>(T_);
+    graph_.num_rows = (indptr.numel() - 1) / T_;
+    torch::Tensor nbr = T("nbr"), cumw = T("cumw");
+    need(nbr, torch::kInt32, -1, "nbr");
+    need(cumw, torch::kFloat32, nbr.numel(), "cumw");
+    graph_.nbr = nbr.data_ptr<int32_t>();
+    graph_.cumw = cumw.data_ptr<float>();
+    torch::Tensor prob = T("node_prob");
+    need(prob, torch::kFloat32, -1, "node_prob");
+    graph_.pop = prob.numel();
+    TORCH_CHECK(graph_.pop > 0, "TreePlan: empty root population");
+    graph_.prob = prob.data_ptr<float>();
+    graph_.alias = i32("node_alias", graph_.pop);
+    graph_.root_rows = has("root_rows") ? i32("root_rows", graph_.pop) : nullptr;
+    tree_.rng = rng.data_ptr<int64_t>();
+    tree_.F1 = L_ > 1 ? static_cast<int32_t>(F_[1]) : 0;
+    tree_.F2 = L_ > 2 ? static_cast<int32_t>(F_[2]) : 0;
+    tree_.logP1 = L_ > 1 ? static_cast<int32_t>(logP_[1]) : 0;
+    tree_.logP2 = L_ > 2 ? static_cast<int32_t>(logP_[2]) : 0;
+    tree_.m1 = static_cast<uint32_t>(masks_[1]);
+    tree_.m2 = L_ > 2 ? static_cast<uint32_t>(masks_[2]) : 0u;
+  }
+
+  void build_fwd() {
+    torch::Tensor x = T("features");
+    TORCH_CHECK(x.dim() == 2 && x.size(1) == D_, "features must be [N, D] with D padded to 16");
+    TORCH_CHECK(x.size(0) == graph_.num_rows, "features must have one row per graph row");
+    TORCH_CHECK(x.scalar_type() == torch::kBFloat16 || x.scalar_type() == torch::kFloat32,
+                "features must be bf16 or fp32");
+    need(x, x.scalar_type(), -1, "features");
+    feat_fp32_ = x.scalar_type() == torch::kFloat32;
+    const int lv = L_ - 1;           // level of layer 0's target rows
+    const int64_t M = M_[lv];
+    TrFwdArgs& a = fwd0_;
+    a.g = graph_;
+    a.tr = tree_;
+    a.x = x.data_ptr();
+    a.D = D_;
+    a.M = M;
+    a.lv = lv;
+    a.FL = static_cast<int32_t>(F_[L_]);
+    a.mL = static_cast<uint32_t>(masks_[L_]);
+    a.hopL = L_;
+    a.include_self = self_;
+    a.inv_leaf = 1.f / static_cast<float>(a.FL + self_);
+    a.roots = i32("roots", B_);
+    a.nodes = has("nodes") ? i32("nodes", M) : nullptr;
+    a.leaf = has("leaf") ? i32("leaf", M * a.FL) : nullptr;
+    a.step = ptr<int64_t>("step", torch::kInt64, 1);
+    if (L_ == 1) {
+      a.a_next = bf("A0", B_ * 2 * D_);  // the head's input rows [B][2D]
+      bm0_ = 32;
+      return;
+    }
+    a.W = bf("W0_sh", dims_[0] * 2 * D_);
+    a.H = static_cast<int32_t>(dims_[0]);
+    a.a_kt = bf("A0_kt", M * 2 * D_);
+    a.mask = i32_as_u32("mask0", (M / 32) * dims_[0]);
+    a.logPg = static_cast<int32_t>(logP_[lv]);
+    a.Fg = static_cast<int32_t>(F_[lv]);
+    a.inv_grp = 1.f / static_cast<float>(a.Fg + self_);
+    a.a_next = bf("A1", M_[lv - 1] * 2 * dims_[0]);
+    bm0_ = (1 << a.logPg) > 32 ? (1 << a.logPg) : 32;
+    TORCH_CHECK(bm0_ <= 128, "TreePlan: slot groups above 128 rows are not supported");
+    if (L_ == 3) {
+      TrFwdArgs& b = fwd1_;
+      b.g = graph_;
+      b.tr = tree_;
+      b.x = Tk("A1").data_ptr();
+      b.D = static_cast<int32_t>(dims_[0]);
+      b.M = M_[1];
+      b.include_self = self_;
+      b.W = bf("W1_sh", dims_[1] * 2 * dims_[0]);
+      b.H = static_cast<int32_t>(dims_[1]);
+      b.a_kt = bf("A1_kt", M_[1] * 2 * dims_[0]);
+      b.mask = i32_as_u32("mask1", (M_[1] / 32) * dims_[1]);
+      b.logPg = static_cast<int32_t>(logP_[1]);
+      b.Fg = static_cast<int32_t>(F_[1]);
+      b.inv_grp = 1.f / static_cast<float>(b.Fg + self_);
+      b.a_next = bf("A2", B_ * 2 * dims_[1]);
+      bm1_ = (1 << b.logPg) > 32 ? (1 << b.logPg) : 32;
+    }
+  }
+
+  uint32_t* i32_as_u32(const std::string& k, int64_t numel) { return reinterpret_cast<uint32_t*>(i32(k, numel)); }
+
+  void build_head() {
+    const int last = L_ - 1;
+    const int64_t Hin2 = 2 * Hin(last), H = dims_[last];
+    TrHeadArgs& a = head_;
+    a.A = bf("A" + std::to_string(last), B_ * Hin2);
+    a.Hin2 = static_cast<int32_t>(Hin2);
+    a.H = static_cast<int32_t>(H);
+    a.E = E_;
+    a.C = C_;
+    a.C_real = C_real_;
+    a.W = bf("W" + std::to_string(last) + "_sh", H * Hin2);
+    a.WT = L_ > 1 ? bf("W" + std::to_string(last) + "_shT", H * Hin2) : nullptr;
+    a.Wfc = bf("Wfc_sh", (int64_t)E_ * H);
+    a.WfcT = bf("Wfc_shT", (int64_t)E_ * H);
+    a.Wout = bf("Wout_sh", (int64_t)C_ * E_);
+    a.WoutT = bf("Wout_shT", (int64_t)C_ * E_);
+    a.bfc = f32("bfc", E_);
+    a.roots = i32("roots", B_);
+    const int mode = static_cast<int>(geti("label_mode"));
+    torch::Tensor lab = T("labels");
+    TORCH_CHECK(lab.is_cuda() && lab.is_contiguous() && lab.device() == dev_, "labels must be contiguous on the GPU");
+    TORCH_CHECK(mode >= 0 && mode <= 2, "label_mode must be 0, 1 or 2");
+    if (mode == 0) {
+      TORCH_CHECK(lab.scalar_type() == torch::kInt16 && lab.numel() == graph_.num_rows, "labels int16 [N]");
+    } else if (mode == 1) {
+      TORCH_CHECK(lab.scalar_type() == torch::kInt32 && lab.numel() == graph_.num_rows, "labels int32 [N]");
+    } else {
+      TORCH_CHECK(lab.scalar_type() == torch::kBFloat16 && lab.numel() == graph_.num_rows * C_, "labels bf16 [N, C]");
+    }
+    a.labels = lab.data_ptr();
+    a.label_mode = mode;
+    a.inv_scale = 1.f / static_cast<float>(B_ * C_real_);
+    a.A_kt = bf("A" + std::to_string(last) + "_kt", B_ * Hin2);
+    a.h_kt = bf("h_kt", B_ * H);
+    a.emb_kt = bf("emb_kt", (int64_t)B_ * E_);
+    a.dlog_kt = bf("dlog_kt", (int64_t)B_ * C_);
+    a.demb_kt = bf("demb_kt", (int64_t)B_ * E_);
+    a.g_kt = bf("g_kt", B_ * H);
+    a.dA = L_ > 1 ? f32("dA" + std::to_string(last), B_ * Hin2) : nullptr;
+    a.loss_acc = f32("loss_acc", 1);
+    a.counts = i32_as_u32("counts", 3);
+    a.prof = nullptr;
+    const size_t lds = eh_tr_head_lds(a.Hin2, a.H, a.E, a.C, mode);
+    TORCH_CHECK(lds <= 160 * 1024 - 64, "TreePlan: head tile does not fit in LDS (", lds, " bytes)");
+    if (L_ == 3) {
+      TrBwdArgs& b = bwd1_;
+      b.dA = f32("dA2", B_ * 2 * dims_[1]);
+      b.mask = i32_as_u32("mask1", (M_[1] / 32) * dims_[1]);
+      b.WT = bf("W1_shT", dims_[1] * 2 * dims_[0]);
+      b.Hk = static_cast<int32_t>(dims_[1]);
+      b.K2out = static_cast<int32_t>(2 * dims_[0]);
+      b.M = M_[1];
+      b.logPg = static_cast<int32_t>(logP_[1]);
+      b.Fg = static_cast<int32_t>(F_[1]);
+      b.include_self = self_;
+      b.inv = 1.f / static_cast<float>(b.Fg + self_);
+      b.dA_out = f32("dA1", M_[1] * 2 * dims_[0]);
+    }
+  }
+
+  // split-K plan: ~target workgroups per problem, at least min_kps 32-row k-blocks per split
+  int kps_for(int64_t MB, int64_t tiles) const {
+    const int64_t target = has("dw_target_wg") ? geti("dw_target_wg") : 512;
+    const int64_t minkps = has("dw_min_kps") ? geti("dw_min_kps") : 4;
+    int64_t kps = (MB * tiles + target - 1) / target;
+    if (kps < minkps) kps = minkps;
+    if (kps > MB) kps = MB;
+    return static_cast<int>(kps);
+  }
+
+  void add_prob(const std::string& /*name*/, int64_t P, int64_t Q, int64_t M, const uint16_t* G, const uint16_t* X,
+                const float* dA, const uint32_t* mask, int logPg, int Fg) {
+    TrDwProb p{};
+    p.P = static_cast<int32_t>(P);
+    p.Q = static_cast<int32_t>(Q);
+    p.MB = static_cast<int32_t>(M / 32);
+    const int64_t tiles = ((P + 63) / 64) * ((Q + 63) / 64);
+    p.kps = kps_for(p.MB, tiles);
+    const int64_t S = (p.MB + p.kps - 1) / p.kps;
+    // split-K partials are owned by the plan (their size follows its split plan)
+    torch::Tensor t = torch::empty({S * P * Q}, torch::TensorOptions().dtype(torch::kFloat32).device(dev_));
+    owned_.push_back(t);
+    p.part = t.data_ptr<float>();
+    p.G = G;
+    p.X = X;
+    if (dA) {
+      p.route = 1;
+      p.dA = dA;
+      p.mask = mask;
+      p.logPg = logPg;
+      p.Fg = Fg;
+      p.include_self = self_;
+      p.inv = 1.f / static_cast<float>(Fg + self_);
+    }
+    probs_.push_back(p);
+  }
+
+  void build_dw() {
+    // conv layers 0..L-1, then fc and out_fc
+    for (int k = 0; k < L_; ++k) {
+      const int64_t P = dims_[k], Q = 2 * Hin(k);
+      const std::string ks = std::to_string(k);
+      if (k < L_ - 1) {
+        const int lvl = L_ - 1 - k;  // target level of layer k
+        add_prob("part" + ks, P, Q, M_[lvl], nullptr, bf("A" + ks + "_kt", M_[lvl] * Q),
+                 f32("dA" + std::to_string(k + 1), M_[lvl - 1] * 2 * P), i32_as_u32("mask" + ks, (M_[lvl] / 32) * P),
+                 static_cast<int>(logP_[lvl]), static_cast<int>(F_[lvl]));
+      } else {
+        add_prob("part" + ks, P, Q, B_, bf("g_kt", B_ * P), bf("A" + ks + "_kt", B_ * Q), nullptr, nullptr, 0, 0);
+      }
+    }
+    const int64_t H = dims_[L_ - 1];
+    add_prob("part_fc", E_, H, B_, bf("demb_kt", (int64_t)B_ * E_), bf("h_kt", B_ * H), nullptr, nullptr, 0, 0);
+    add_prob("part_out", C_, E_, B_, bf("dlog_kt", (int64_t)B_ * C_), bf("emb_kt", (int64_t)B_ * E_), nullptr,
+             nullptr, 0, 0);
+  }
+
+  void build_opt() {
+    torch::Tensor flat = T("flat");
+    const int64_t n = flat.numel();
+    TrOptArgs& a = opt_;
+    a.p = f32("flat", n);
+    a.g = f32("grad", n);
+    a.m = f32("m", n);
+    a.v = f32("v", n);
+    a.n = n;
+    std::vector<int64_t> off = getv("offsets");  // L convs, fc W, fc b, out W, end
+    TORCH_CHECK((int)off.size() == L_ + 4 && off.back() == n, "TreePlan: offsets must cover the flat buffer");
+    int seg = 0;
+    for (int k = 0; k < L_ + 3; ++k) {
+      TrSeg& s = a.seg[seg++];
+      s.off = off[k];
+      s.n = off[k + 1] - off[k];
+      const bool bias = k == L_ + 1;
+      if (bias) {
+        s.part = nullptr;
+        s.S = 0;
+      } else {
+        const int pi = k < L_ ? k : (k == L_ ? L_ : L_ + 1);
+        const TrDwProb& p = probs_[pi];
+        TORCH_CHECK(s.n == (int64_t)p.P * p.Q, "TreePlan: flat segment ", k, " does not match its dW problem");
+        s.part = p.part;
+        s.S = (p.MB + p.kps - 1) / p.kps;
+      }
+    }
+    a.nseg = seg;
+    // the head accumulates the fc-bias gradient atomically into its flat-gradient segment
+    head_.dbfc = a.g + off[L_ + 1];
+    // bf16 shadows: conv weights (+ transposes where a backward GEMM uses them), fc, out
+    int ns = 0;
+    for (int k = 0; k < L_; ++k) {
+      const std::string ks = std::to_string(k);
+      const int64_t rows = dims_[k], cols = 2 * Hin(k);
+      TrShadow& s = a.sh[ns++];
+      s.off = off[k];
+      s.n = rows * cols;
+      s.cols = static_cast<int32_t>(cols);
+      s.sh = bf("W" + ks + "_sh", rows * cols);
+      s.shT = k >= 1 ? bf("W" + ks + "_shT", rows * cols) : nullptr;
+    }
+    const int64_t H = dims_[L_ - 1];
+    TrShadow& f = a.sh[ns++];
+    f.off = off[L_];
+    f.n = (int64_t)E_ * H;
+    f.cols = static_cast<int32_t>(H);
+    f.sh = bf("Wfc_sh", f.n);
+    f.shT = bf("Wfc_shT", f.n);
+    TrShadow& o = a.sh[ns++];
+    o.off = off[L_ + 2];
+    o.n = (int64_t)C_ * E_;
+    o.cols = E_;
+    o.sh = bf("Wout_sh", o.n);
+    o.shT = bf("Wout_shT", o.n);
+    a.nsh = ns;
+    a.step = ptr<int64_t>("step", torch::kInt64, 1);
+    a.lr = static_cast<float>(getf("lr"));
+    a.b1 = static_cast<float>(getf("beta1"));
+    a.b2 = static_cast<float>(getf("beta2"));
+    a.eps = static_cast<float>(getf("eps"));
+    a.wd = static_cast<float>(getf("weight_decay"));
+    a.grad_scale = 1.f;
+    a.kind = static_cast<int32_t>(geti("opt_kind"));
+    a.loss_acc = f32("loss_acc", 1);
+    a.loss_out = f32("loss_out", 1);
+    a.rng = ptr<int64_t>("rng", torch::kInt64, 2);
+  }
+};
+
+}  // namespace
+
+void register_tree_ops(py::module& m) {
+  py::class_<TreePlan>(m, "TreePlan")
+      .def(py::init<py::dict>())
+      .def("fwd", &TreePlan::fwd)
+      .def("head", &TreePlan::head, py::arg("prof") = py::none())
+      .def("bwd", &TreePlan::bwd)
+      .def("dw", &TreePlan::dw)
+      .def("opt", &TreePlan::opt, py::arg("mode"), py::arg("grad_scale") = 1.0)
+      .def("set_lr", &TreePlan::set_lr)
+      .def("num_problems", &TreePlan::num_problems)
+      .def("splits", &TreePlan::splits);
+  m.attr("tree_head_rows") = kTrHeadRows;
+}

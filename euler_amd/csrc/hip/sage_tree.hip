@@ -1,0 +1,1010 @@
+// Fused GraphSAGE training step on gfx950 for 1-3 hop models (SURVEY §2.7 K1/K2/K3/K11/
+// K12/K13, §7.3) — the kernels behind euler_amd.models.sage_trainer.SageTrainer, which
+// NodeEstimator(device_graph=True) and bench.py run.
+//
+// Model (reference examples/graphsage/graphsage.py:56-67, mp_utils/base_gnn.py:75-92,
+// mp_utils/base.py:24-47, convolution/sage_conv.py:33-44):
+//   h_k   = relu([h_{k-1}[self] | mean_nbr h_{k-1}] @ W_k^T)     k = 0 .. L-1
+//   emb   = h_{L-1} @ Wfc^T + bfc ;  logits = emb @ Wout^T
+//   loss  = mean(sigmoid_ce(logits, label))
+// Mini-batch = the reference SageDataFlow (sample every node of the previous hops again,
+// sage_dataflow.py:35-50) without dedup, in the slotted tree layout of tree_args.h.
+//
+// A 2-hop step is four launches:
+//   tr_fwd  (mode 0)  roots + hop 1 + hop 2 sampling (Philox, on the HBM CSR), gather of
+//                     the leaf feature rows, mean, MFMA GEMM + ReLU, and the tree mean of
+//                     the next layer as the epilogue -> A1 rows, A0 (kt), ReLU bits
+//   tr_head           last conv + fc + out_fc + loss + backward to dA1
+//   tr_dw             grouped split-K dW of every weight; the outer layer's G operand is
+//                     routed from dA1 through the tree inside the kernel (never stored)
+//   tr_opt   (mode 2) split-K reduce + Adam/Adagrad/SGD/momentum + bf16 weight shadows
+// (3 hops add one tr_fwd mode 2 and one tr_bwd; 1 hop uses tr_fwd mode 1).
+#include "hip/tile.h"
+#include "hip/tree_args.h"
+
+namespace euler_hip {
+
+constexpr uint64_t kTrStreamRoot = 1, kTrStreamHop = 16;
+constexpr int kTrBN = 256;  // output columns per GEMM chunk (4 waves x 64)
+
+__device__ __forceinline__ uint4_t tr_rand(const int64_t* rng, uint64_t stream, uint64_t idx) {
+  return Philox::gen(static_cast<uint64_t>(rng[0]), (static_cast<uint64_t>(rng[1]) << 8) ^ stream, idx);
+}
+
+// Walker alias draw of root t (reference sample_node: weighted, per node type)
+__device__ __forceinline__ int32_t tr_root(const TrGraph& g, const int64_t* rng, int64_t t) {
+  const uint4_t r = tr_rand(rng, kTrStreamRoot, static_cast<uint64_t>(t));
+  const uint64_t x = (static_cast<uint64_t>(r[0]) << 32) | r[1];
+  int64_t k = static_cast<int64_t>(__umul64hi(x, static_cast<uint64_t>(g.pop)));
+  if (k >= g.pop) k = g.pop - 1;
+  const int64_t pick = (u01(r[2]) < g.prob[k]) ? k : static_cast<int64_t>(g.alias[k]);
+  return g.root_rows ? g.root_rows[pick] : static_cast<int32_t>(pick);
+}
+
+// one weighted with-replacement neighbour draw (reference node.cc:98-161: pick an edge
+// type group by its weight sum, then binary-search the group); -1 when there is none
+__device__ int32_t tr_neighbor(const TrGraph& g, int32_t row, uint32_t mask, uint4_t r) {
+  if (row < 0 || row >= g.num_rows) return -1;
+  const int64_t base = static_cast<int64_t>(row) * g.num_types;
+  int64_t lo = 0, hi = 0;
+  float total = 0.f;
+  if (g.num_types == 1) {
+    if (!(mask & 1u)) return -1;
+    lo = g.indptr[base];
+    hi = g.indptr[base + 1];
+    total = hi > lo ? g.cumw[hi - 1] : 0.f;
+  } else {
+    float tot = 0.f;
+    for (int t = 0; t < g.num_types; ++t) {
+      if (!((mask >> t) & 1u)) continue;
+      const int64_t a = g.indptr[base + t], b = g.indptr[base + t + 1];
+      if (b > a) tot += g.cumw[b - 1];
+    }
+    if (!(tot > 0.f)) return -1;
+    float u = u01(r[0]) * tot;
+    for (int t = 0; t < g.num_types; ++t) {
+      if (!((mask >> t) & 1u)) continue;
+      const int64_t a = g.indptr[base + t], b = g.indptr[base + t + 1];
+      if (b <= a) continue;
+      const float gw = g.cumw[b - 1];
+      lo = a;
+      hi = b;
+      total = gw;
+      if (u < gw) break;
+      u -= gw;
+    }
+  }
+  if (hi <= lo || !(total > 0.f)) return -1;
+  const float u = u01(r[1]) * total;
+  int64_t a = lo, b = hi - 1;
+  while (a < b) {
+    const int64_t m = (a + b) >> 1;
+    if (g.cumw[m] > u) b = m;
+    else a = m + 1;
+  }
+  return g.nbr[a];
+}
+
+// slot j of the group of `parent` (whose own slot index is parent_slot) at hop `hop`
+__device__ __forceinline__ int32_t tr_hop(const TrGraph& g, const int64_t* rng, int32_t parent, int j, int F,
+                                          uint32_t mask, int hop, int64_t parent_slot) {
+  if (j < F)
+    return parent >= 0 ? tr_neighbor(g, parent, mask,
+                                     tr_rand(rng, kTrStreamHop + hop, static_cast<uint64_t>(parent_slot * F + j)))
+                       : -1;
+  return j == F ? parent : -1;
+}
+
+// node of slot s at level lv (0..2); *root = index of its root, *self_chain = the slot is
+// the root itself (every digit is the self slot)
+__device__ int32_t tr_slot_node(const TrGraph& g, const TrTree& tr, int64_t s, int lv, int64_t* root,
+                                bool* self_chain) {
+  int64_t i0 = s, i1 = 0, i2 = 0;
+  if (lv == 1) {
+    i1 = s;
+    i0 = s >> tr.logP1;
+  } else if (lv == 2) {
+    i2 = s;
+    i1 = s >> tr.logP2;
+    i0 = i1 >> tr.logP1;
+  }
+  int32_t node = tr_root(g, tr.rng, i0);
+  bool sc = true;
+  if (lv >= 1) {
+    const int j = static_cast<int>(i1 & ((int64_t(1) << tr.logP1) - 1));
+    sc = j == tr.F1;
+    node = tr_hop(g, tr.rng, node, j, tr.F1, tr.m1, 1, i0);
+  }
+  if (lv >= 2) {
+    const int j = static_cast<int>(i2 & ((int64_t(1) << tr.logP2) - 1));
+    sc = sc && j == tr.F2;
+    node = tr_hop(g, tr.rng, node, j, tr.F2, tr.m2, 2, i1);
+  }
+  *root = i0;
+  *self_chain = sc;
+  return node;
+}
+
+// 8 consecutive feature columns of one row, bf16 or fp32 storage
+template <typename FT>
+struct Feat8;
+template <>
+struct Feat8<bf16_t> {
+  static constexpr int kInFlight = 12;  // rows in flight per thread
+  uint4_t v;
+  __device__ __forceinline__ void load(const bf16_t* p) { v = *reinterpret_cast<const uint4_t*>(p); }
+  __device__ __forceinline__ void zero() { v = uint4_t{0u, 0u, 0u, 0u}; }
+  __device__ __forceinline__ void add_to(float* acc) const { acc_bf16x8(acc, v); }
+  __device__ __forceinline__ uint4_t bf16() const { return v; }
+};
+template <>
+struct Feat8<float> {
+  static constexpr int kInFlight = 6;
+  float4_t a, b;
+  __device__ __forceinline__ void load(const float* p) {
+    a = *reinterpret_cast<const float4_t*>(p);
+    b = *reinterpret_cast<const float4_t*>(p + 4);
+  }
+  __device__ __forceinline__ void zero() { a = b = float4_t{0.f, 0.f, 0.f, 0.f}; }
+  __device__ __forceinline__ void add_to(float* acc) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      acc[i] += a[i];
+      acc[4 + i] += b[i];
+    }
+  }
+  __device__ __forceinline__ uint4_t bf16() const {
+    float t[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    return pack_bf16x8(t);
+  }
+};
+
+__device__ __forceinline__ float bf_lo(uint32_t v) { return __uint_as_float(v << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t v) { return __uint_as_float(v & 0xffff0000u); }
+
+// ----------------------------------------------------------------------------
+// tr_fwd: one SAGE layer over BM target rows per block (see TrFwdArgs)
+// ----------------------------------------------------------------------------
+template <typename FT, int BM, int MODE>
+__global__ __launch_bounds__(256, 2) void tr_fwd_kernel(TrFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  constexpr bool kGather = MODE != 2;
+  const int D = a.D;
+  const int K2 = 2 * D;
+  const int ldsw = K2 + 8;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t row0 = static_cast<int64_t>(tile) * BM;
+  const int H = a.H;
+  const bool alias_out = H <= kTrBN && kTrBN <= K2;
+  // LDS: [BM][ldsw] A tile | [BM][kTrBN + 8] output tile (modes 0/2, unless it aliases the
+  // A tile) | node ids [BM] + leaf ids [BM][FL] (modes 0/1); must match eh_tr_fwd_lds
+  const bool own_otile = MODE != 1 && !alias_out;
+  bf16_t* otile = own_otile ? lds + BM * ldsw : lds;
+  int32_t* node_s = reinterpret_cast<int32_t*>(lds + BM * ldsw + (own_otile ? BM * (kTrBN + 8) : 0));
+  int32_t* leaf_s = node_s + BM;
+
+  if constexpr (kGather) {
+    // ---- sampling: the target rows' nodes (root -> hop chain), then their leaf draws
+    if (a.step && blockIdx.x == 0 && threadIdx.x == 0) a.step[0] += 1;
+    if (threadIdx.x < BM) {
+      const int64_t s = row0 + threadIdx.x;
+      int32_t node = -1;
+      if (s < a.M) {
+        int64_t root;
+        bool sc;
+        node = tr_slot_node(a.g, a.tr, s, a.lv, &root, &sc);
+        if (sc) a.roots[root] = node;
+        if (a.nodes) a.nodes[s] = node;
+      }
+      node_s[threadIdx.x] = node;
+    }
+    __syncthreads();
+    for (int it = threadIdx.x; it < BM * a.FL; it += 256) {
+      const int r = it / a.FL, k = it - r * a.FL;
+      const int64_t s = row0 + r;
+      const int32_t node = node_s[r];
+      const int32_t nb = node >= 0 ? tr_neighbor(a.g, node, a.mL,
+                                                 tr_rand(a.tr.rng, kTrStreamHop + a.hopL,
+                                                         static_cast<uint64_t>(s * a.FL + k)))
+                                   : -1;
+      leaf_s[it] = nb;
+      if (a.leaf && s < a.M) a.leaf[s * a.FL + k] = nb;
+    }
+    __syncthreads();
+    // ---- gather + mean: item = (row, 8-column chunk); all leaf loads of a chunk in flight
+    const FT* x = static_cast<const FT*>(a.x);
+    const int cpr = D >> 3;
+    constexpr int G = Feat8<FT>::kInFlight;
+    for (int it = threadIdx.x; it < BM * cpr; it += 256) {
+      const int r = it / cpr;
+      const int c = it - r * cpr;
+      const int64_t grow = row0 + r;
+      const int32_t node = node_s[r];
+      Feat8<FT> sv;
+      sv.zero();
+      float acc[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+      if (node >= 0) sv.load(x + static_cast<int64_t>(node) * D + c * 8);
+      if (a.include_self) sv.add_to(acc);
+      for (int k = 0; k < a.FL; k += G) {
+        int32_t j[G];
+        Feat8<FT> v[G];
+#pragma unroll
+        for (int u = 0; u < G; ++u) j[u] = (k + u < a.FL) ? leaf_s[r * a.FL + k + u] : -1;
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+          if (j[u] >= 0) v[u].load(x + static_cast<int64_t>(j[u]) * D + c * 8);
+          else v[u].zero();
+        }
+#pragma unroll
+        for (int u = 0; u < G; ++u) v[u].add_to(acc);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] *= a.inv_leaf;
+      const uint4_t selfv = sv.bf16(), meanv = pack_bf16x8(acc);
+      if constexpr (MODE == 1) {
+        if (grow < a.M) {
+          *reinterpret_cast<uint4_t*>(a.a_next + grow * K2 + c * 8) = selfv;
+          *reinterpret_cast<uint4_t*>(a.a_next + grow * K2 + D + c * 8) = meanv;
+        }
+      } else {
+        *reinterpret_cast<uint4_t*>(lds + r * ldsw + c * 8) = selfv;
+        *reinterpret_cast<uint4_t*>(lds + r * ldsw + D + c * 8) = meanv;
+      }
+    }
+    if constexpr (MODE == 1) return;
+  } else {
+    // ---- rows: BM rows of A [M][K2] (bf16) into the tile
+    const bf16_t* A = static_cast<const bf16_t*>(a.x);
+    const int cpr = K2 >> 3;
+    for (int it = threadIdx.x; it < BM * cpr; it += 256) {
+      const int r = it / cpr, c = it - r * cpr;
+      const int64_t grow = row0 + r;
+      const uint4_t v = grow < a.M ? *reinterpret_cast<const uint4_t*>(A + grow * K2 + c * 8) : uint4_t{0u, 0u, 0u, 0u};
+      *reinterpret_cast<uint4_t*>(lds + r * ldsw + c * 8) = v;
+    }
+  }
+  __syncthreads();
+
+  // ---- A tile -> kt layout (dW operand): item = (column n, 8-row chunk q)
+  if (a.a_kt) {
+    constexpr int CH = BM / 8;
+    for (int it = threadIdx.x; it < K2 * CH; it += 256) {
+      const int q = it % CH;
+      const int n = it / CH;
+      const int64_t gr = row0 + q * 8;
+      if (gr >= a.M) continue;
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = bf2f(lds[(q * 8 + i) * ldsw + n]);
+      *reinterpret_cast<uint4_t*>(a.a_kt + kt_off(gr, n, K2)) = pack_bf16x8(v);
+    }
+  }
+
+  // ---- MFMA GEMM out of LDS; wave w owns 64-column slab w of each 256-column chunk
+  constexpr int FM = BM / 16;
+  constexpr int FN = 4;
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int lr = lane & 15, lk = (lane >> 4) * 8;
+  const int ldo = kTrBN + 8;
+  const bf16_t* W = a.W;
+  for (int cchunk = 0; cchunk < H; cchunk += kTrBN) {
+    const int cb = cchunk + wave * 64;
+    float4_t acc[FM][FN];
+    tl_zero(acc);
+    if (cb < H) {
+      uint4_t bcur[FN];
+#pragma unroll
+      for (int n = 0; n < FN; ++n) bcur[n] = fm_frag(W, cb + n * 16, 0, K2, lane);
+      for (int k0 = 0; k0 < K2; k0 += 32) {
+        uint4_t bnext[FN];
+        const bool more = k0 + 32 < K2;
+#pragma unroll
+        for (int n = 0; n < FN; ++n)
+          bnext[n] = more ? fm_frag(W, cb + n * 16, k0 + 32, K2, lane) : uint4_t{0u, 0u, 0u, 0u};
+        uint4_t av[FM];
+#pragma unroll
+        for (int m = 0; m < FM; ++m)
+          av[m] = *reinterpret_cast<const uint4_t*>(lds + (m * 16 + lr) * ldsw + k0 + lk);
+#pragma unroll
+        for (int m = 0; m < FM; ++m)
+#pragma unroll
+          for (int n = 0; n < FN; ++n) acc[m][n] = mfma16(av[m], bcur[n], acc[m][n]);
+#pragma unroll
+        for (int n = 0; n < FN; ++n) bcur[n] = bnext[n];
+      }
+    }
+    if (alias_out) __syncthreads();  // every wave is done reading the A tile
+    if (cb < H) {
+#pragma unroll
+      for (int m = 0; m < FM; ++m)
+#pragma unroll
+        for (int n = 0; n < FN; ++n)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int row = m * 16 + (lane >> 4) * 4 + j;
+            otile[row * ldo + wave * 64 + n * 16 + lr] = f2bf(fmaxf(acc[m][n][j], 0.f));
+          }
+    }
+    __syncthreads();
+    const int ncols = (H - cchunk) < kTrBN ? (H - cchunk) : kTrBN;
+    // tree-mean epilogue: A_next[parent] = [h[self slot] | mean_{j < Fg} h[j]] for every
+    // sibling group of the block (item = (group, column pair), 4-byte stores)
+    {
+      const int groups = BM >> a.logPg;
+      const int pairs = ncols >> 1;
+      for (int it = threadIdx.x; it < groups * pairs; it += 256) {
+        const int gi = it / pairs;
+        const int c = (it - gi * pairs) * 2;
+        const int base = gi << a.logPg;
+        if (row0 + base >= a.M) continue;
+        const uint32_t selfp = *reinterpret_cast<const uint32_t*>(otile + (base + a.Fg) * ldo + c);
+        float s0 = 0.f, s1 = 0.f;
+        for (int j = 0; j < a.Fg; ++j) {
+          const uint32_t v = *reinterpret_cast<const uint32_t*>(otile + (base + j) * ldo + c);
+          s0 += bf_lo(v);
+          s1 += bf_hi(v);
+        }
+        if (a.include_self) {
+          s0 += bf_lo(selfp);
+          s1 += bf_hi(selfp);
+        }
+        const int64_t parent = (row0 >> a.logPg) + gi;
+        bf16_t* dst = a.a_next + parent * 2 * H + cchunk + c;
+        *reinterpret_cast<uint32_t*>(dst) = selfp;
+        *reinterpret_cast<uint32_t*>(dst + H) = pack_bf16x2(s0 * a.inv_grp, s1 * a.inv_grp);
+      }
+    }
+    // ReLU bits for the backward: word (32-row block, column) has bit i set iff row i > 0
+    if (a.mask) {
+      constexpr int KBB = BM / 32;
+      for (int it = threadIdx.x; it < KBB * ncols; it += 256) {
+        const int kbl = it / ncols, n = it - kbl * ncols;
+        const int64_t gr = row0 + kbl * 32;
+        if (gr >= a.M) continue;
+        uint32_t bits = 0;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) bits |= (bf_pos(otile[(kbl * 32 + i) * ldo + n]) ? 1u : 0u) << i;
+        a.mask[(gr >> 5) * H + cchunk + n] = bits;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ----------------------------------------------------------------------------
+// tr_bwd (3-hop inner layer): G rows routed from the parent gradient through the tree
+// and the ReLU bits, then dA_out = G @ W (fp32 rows)
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void tr_bwd_kernel(TrBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  constexpr int BM = 32;
+  const int Hk = a.Hk, K2 = a.K2out;
+  const int ldg = Hk + 8;
+  const int64_t row0 = static_cast<int64_t>(xcd_remap(blockIdx.x, gridDim.x)) * BM;
+  const int Pm = (1 << a.logPg) - 1;
+  for (int it = threadIdx.x; it < BM * Hk; it += 256) {
+    const int r = it / Hk, n = it - r * Hk;
+    const int64_t row = row0 + r;
+    float v = 0.f;
+    if (row < a.M && ((a.mask[(row >> 5) * Hk + n] >> (row & 31)) & 1u)) {
+      const int64_t t = row >> a.logPg;
+      const int j = static_cast<int>(row & Pm);
+      const float dn = a.dA[t * 2 * Hk + Hk + n] * a.inv;
+      if (j < a.Fg) v = dn;
+      else if (j == a.Fg) v = a.dA[t * 2 * Hk + n] + (a.include_self ? dn : 0.f);
+    }
+    lds[r * ldg + n] = f2bf(v);
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int lr = lane & 15, lk = (lane >> 4) * 8;
+  constexpr int FM = BM / 16, FN = 4;
+  for (int cchunk = 0; cchunk < K2; cchunk += kTrBN) {
+    const int cb = cchunk + wave * 64;
+    if (cb >= K2) continue;
+    float4_t acc[FM][FN];
+    tl_zero(acc);
+    for (int k0 = 0; k0 < Hk; k0 += 32) {
+      uint4_t b[FN], av[FM];
+#pragma unroll
+      for (int n = 0; n < FN; ++n) b[n] = fm_frag(a.WT, cb + n * 16, k0, Hk, lane);
+#pragma unroll
+      for (int m = 0; m < FM; ++m) av[m] = *reinterpret_cast<const uint4_t*>(lds + (m * 16 + lr) * ldg + k0 + lk);
+#pragma unroll
+      for (int m = 0; m < FM; ++m)
+#pragma unroll
+        for (int n = 0; n < FN; ++n) acc[m][n] = mfma16(av[m], b[n], acc[m][n]);
+    }
+#pragma unroll
+    for (int m = 0; m < FM; ++m)
+#pragma unroll
+      for (int n = 0; n < FN; ++n)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int64_t row = row0 + m * 16 + (lane >> 4) * 4 + j;
+          if (row < a.M) a.dA_out[row * K2 + cb + n * 16 + lr] = acc[m][n][j];
+        }
+  }
+}
+
+// ----------------------------------------------------------------------------
+// tr_head: kTrHeadRows roots per block, 16 waves; wave w owns 16-column slabs w, w+16, ...
+// ----------------------------------------------------------------------------
+constexpr int HB = kTrHeadRows;
+constexpr int HFM = HB / 16;
+constexpr int HNW = 16;
+constexpr int TR_KC = 8;  // k steps (x32) per B chunk
+
+__device__ __forceinline__ void tr_prefetch(const bf16_t* __restrict__ Bf, int col0, int N, int K, int lane,
+                                            uint4_t (&b)[TR_KC]) {
+  const int c = col0 < N ? col0 : 0;  // branch-free: out-of-range fragments are loaded but unused
+#pragma unroll
+  for (int s = 0; s < TR_KC; ++s) b[s] = fm_frag(Bf, c, s * 32 < K ? s * 32 : 0, K, lane);
+}
+
+__device__ __forceinline__ void tr_mfma_chunk(const bf16_t* A, int lda, int kc, int K, const uint4_t (&b)[TR_KC],
+                                              float4_t (&acc)[HFM][1], int lane) {
+  const int lr = lane & 15, lk = (lane >> 4) * 8;
+#pragma unroll
+  for (int s = 0; s < TR_KC; ++s) {
+    if (kc + s * 32 < K) {
+      uint4_t av[HFM];
+#pragma unroll
+      for (int m = 0; m < HFM; ++m) av[m] = *reinterpret_cast<const uint4_t*>(A + (m * 16 + lr) * lda + kc + s * 32 + lk);
+#pragma unroll
+      for (int m = 0; m < HFM; ++m) acc[m][0] = mfma16(av[m], b[s], acc[m][0]);
+    }
+  }
+}
+
+// acc += A_lds[rows][0:K] @ Bf[col0 .. col0+15][0:K]^T; the first chunk was prefetched
+__device__ __forceinline__ void tr_gemm(const bf16_t* A, int lda, const bf16_t* __restrict__ Bf, int col0, int K,
+                                        float4_t (&acc)[HFM][1], int lane, const uint4_t (&pre)[TR_KC]) {
+  tr_mfma_chunk(A, lda, 0, K, pre, acc, lane);
+  for (int kc = 32 * TR_KC; kc < K; kc += 32 * TR_KC) {
+    uint4_t b[TR_KC];
+#pragma unroll
+    for (int s = 0; s < TR_KC; ++s) b[s] = fm_frag(Bf, col0, kc + s * 32 < K ? kc + s * 32 : 0, K, lane);
+    tr_mfma_chunk(A, lda, kc, K, b, acc, lane);
+  }
+}
+
+__device__ __forceinline__ void tr_lds_to_kt(const bf16_t* tile, int ld, int N, int64_t r0, bf16_t* kt) {
+  for (int it = threadIdx.x; it < N * (HB / 8); it += HNW * 64) {
+    const int q = it % (HB / 8), n = it / (HB / 8);
+    float v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = bf2f(tile[(q * 8 + i) * ld + n]);
+    *reinterpret_cast<uint4_t*>(kt + kt_off(r0 + q * 8, n, N)) = pack_bf16x8(v);
+  }
+}
+
+__device__ __forceinline__ int tr_head_ld(int w) { return w + 8; }
+
+__global__ __launch_bounds__(HNW * 64) void tr_head_kernel(TrHeadArgs a) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+#define TR_STAMP(k) \
+  if (a.prof && threadIdx.x == 0) a.prof[blockIdx.x * 8 + (k)] = static_cast<long long>(wall_clock64())
+  TR_STAMP(0);
+  const int Hin2 = a.Hin2, H = a.H, E = a.E, C = a.C;
+  const int lda = tr_head_ld(Hin2), ldh = tr_head_ld(H), lde = tr_head_ld(E > H ? E : H), ldd = tr_head_ld(E),
+            ldc = tr_head_ld(C);
+  bf16_t* Aa = lds;            // [HB][lda]  A rows
+  bf16_t* Ah = Aa + HB * lda;  // [HB][ldh]  h (post-ReLU)
+  bf16_t* Eb = Ah + HB * ldh;  // [HB][lde]  emb, later g
+  bf16_t* Db = Eb + HB * lde;  // [HB][ldd]  demb
+  bf16_t* Dl = Db + HB * ldd;  // [HB][ldc]  dlogits
+  bf16_t* Ly = Dl + HB * ldc;  // [HB][C]    dense labels (label_mode 2)
+  __shared__ int lab_s[HB];
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * HB;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int lr = lane & 15, lg = lane >> 4;
+  constexpr int NT = HNW * 64;
+
+  if (a.label_mode < 2) {
+    if (threadIdx.x < HB) {
+      const int32_t root = a.roots[r0 + threadIdx.x];
+      lab_s[threadIdx.x] = a.label_mode == 0 ? static_cast<int>(static_cast<const int16_t*>(a.labels)[root])
+                                             : static_cast<const int32_t*>(a.labels)[root];
+    }
+  } else {
+    const bf16_t* L = static_cast<const bf16_t*>(a.labels);
+    const int cpl = C >> 3;
+    for (int it = threadIdx.x; it < HB * cpl; it += NT) {
+      const int r = it / cpl, c = it - r * cpl;
+      const int64_t root = a.roots[r0 + r];
+      *reinterpret_cast<uint4_t*>(Ly + r * C + c * 8) = *reinterpret_cast<const uint4_t*>(L + root * C + c * 8);
+    }
+  }
+
+  // S0: A tile -> LDS (+ A_kt); h = relu(A @ W^T)
+  uint4_t pre[TR_KC];
+  tr_prefetch(a.W, wave * 16, H, Hin2, lane, pre);
+  const int cpa = Hin2 >> 3;
+  for (int it = threadIdx.x; it < HB * cpa; it += NT) {
+    const int r = it / cpa, c = it - r * cpa;
+    *reinterpret_cast<uint4_t*>(Aa + r * lda + c * 8) =
+        *reinterpret_cast<const uint4_t*>(a.A + (r0 + r) * Hin2 + c * 8);
+  }
+  __syncthreads();
+  TR_STAMP(1);
+  tr_lds_to_kt(Aa, lda, Hin2, r0, a.A_kt);
+  for (int cc = wave * 16; cc < H; cc += HNW * 16) {
+    float4_t acc[HFM][1];
+    tl_zero(acc);
+    tr_gemm(Aa, lda, a.W, cc, Hin2, acc, lane, pre);
+    if (cc + HNW * 16 < H) tr_prefetch(a.W, cc + HNW * 16, H, Hin2, lane, pre);
+#pragma unroll
+    for (int m = 0; m < HFM; ++m)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) Ah[(m * 16 + lg * 4 + j) * ldh + cc + lr] = f2bf(fmaxf(acc[m][0][j], 0.f));
+  }
+  tr_prefetch(a.Wfc, wave * 16, E, H, lane, pre);
+  __syncthreads();
+  TR_STAMP(2);
+  tr_lds_to_kt(Ah, ldh, H, r0, a.h_kt);
+
+  // S2: emb = h @ Wfc^T + bfc
+  for (int cc = wave * 16; cc < E; cc += HNW * 16) {
+    float4_t acc[HFM][1];
+    tl_zero(acc);
+    tr_gemm(Ah, ldh, a.Wfc, cc, H, acc, lane, pre);
+    if (cc + HNW * 16 < E) tr_prefetch(a.Wfc, cc + HNW * 16, E, H, lane, pre);
+    const int col = cc + lr;
+    const float b = a.bfc[col];
+#pragma unroll
+    for (int m = 0; m < HFM; ++m) {
+      float e[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        e[j] = bf2f(f2bf(acc[m][0][j] + b));
+        Eb[(m * 16 + lg * 4 + j) * lde + col] = f2bf(e[j]);
+      }
+      kt_store4(a.emb_kt, r0 + m * 16 + lg * 4, col, E, e[0], e[1], e[2], e[3]);
+    }
+  }
+  tr_prefetch(a.Wout, wave * 16, C, E, lane, pre);
+  __syncthreads();
+  TR_STAMP(3);
+
+  // S3: logits = emb @ Wout^T ; dlogits, loss, F1 counts (padded label columns excluded)
+  float lsum = 0.f;
+  int tp = 0, fp = 0, fn = 0;
+  for (int cc = wave * 16; cc < C; cc += HNW * 16) {
+    float4_t acc[HFM][1];
+    tl_zero(acc);
+    tr_gemm(Eb, lde, a.Wout, cc, E, acc, lane, pre);
+    if (cc + HNW * 16 < C) tr_prefetch(a.Wout, cc + HNW * 16, C, E, lane, pre);
+    const int col = cc + lr;
+    const bool valid = col < a.C_real;
+#pragma unroll
+    for (int m = 0; m < HFM; ++m) {
+      float d[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = m * 16 + lg * 4 + j;
+        const float xv = acc[m][0][j];
+        const float y = a.label_mode < 2 ? ((lab_s[row] == col) ? 1.f : 0.f) : bf2f(Ly[row * C + col]);
+        const float p = 1.f / (1.f + __expf(-xv));
+        if (valid) {
+          lsum += fmaxf(xv, 0.f) - xv * y + log1pf(__expf(-fabsf(xv)));
+          const bool pred = xv >= 0.f, pos = y > 0.5f;
+          tp += pred && pos;
+          fp += pred && !pos;
+          fn += !pred && pos;
+        }
+        d[j] = valid ? bf2f(f2bf((p - y) * a.inv_scale)) : 0.f;
+        Dl[row * ldc + col] = f2bf(d[j]);
+      }
+      kt_store4(a.dlog_kt, r0 + m * 16 + lg * 4, col, C, d[0], d[1], d[2], d[3]);
+    }
+  }
+  if (wave * 16 < C) {
+    lsum = wave_sum(lsum);
+    tp = wave_sum_i(tp);
+    fp = wave_sum_i(fp);
+    fn = wave_sum_i(fn);
+    if (lane == 0) {
+      atomicAdd(a.loss_acc, lsum * a.inv_scale);
+      if (a.counts) {
+        atomicAdd(a.counts + 0, static_cast<uint32_t>(tp));
+        atomicAdd(a.counts + 1, static_cast<uint32_t>(fp));
+        atomicAdd(a.counts + 2, static_cast<uint32_t>(fn));
+      }
+    }
+  }
+  tr_prefetch(a.WoutT, wave * 16, E, C, lane, pre);
+  __syncthreads();
+  TR_STAMP(4);
+
+  // S4: demb = dlogits @ Wout ; dbfc = column sums
+  for (int cc = wave * 16; cc < E; cc += HNW * 16) {
+    float4_t acc[HFM][1];
+    tl_zero(acc);
+    tr_gemm(Dl, ldc, a.WoutT, cc, C, acc, lane, pre);
+    if (cc + HNW * 16 < E) tr_prefetch(a.WoutT, cc + HNW * 16, E, C, lane, pre);
+    const int col = cc + lr;
+    float cs = 0.f;
+#pragma unroll
+    for (int m = 0; m < HFM; ++m) {
+      float e[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        cs += acc[m][0][j];
+        e[j] = bf2f(f2bf(acc[m][0][j]));
+        Db[(m * 16 + lg * 4 + j) * ldd + col] = f2bf(e[j]);
+      }
+      kt_store4(a.demb_kt, r0 + m * 16 + lg * 4, col, E, e[0], e[1], e[2], e[3]);
+    }
+    cs += __shfl_xor(cs, 16, 64);
+    cs += __shfl_xor(cs, 32, 64);
+    if (lg == 0) atomicAdd(a.dbfc + col, cs);
+  }
+  tr_prefetch(a.WfcT, wave * 16, H, E, lane, pre);
+  __syncthreads();
+  TR_STAMP(5);
+
+  // S5: g = (demb @ Wfc) * (h > 0) -> Eb, g_kt
+  for (int cc = wave * 16; cc < H; cc += HNW * 16) {
+    float4_t acc[HFM][1];
+    tl_zero(acc);
+    tr_gemm(Db, ldd, a.WfcT, cc, E, acc, lane, pre);
+    if (cc + HNW * 16 < H) tr_prefetch(a.WfcT, cc + HNW * 16, H, E, lane, pre);
+    const int col = cc + lr;
+#pragma unroll
+    for (int m = 0; m < HFM; ++m) {
+      float e[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = m * 16 + lg * 4 + j;
+        e[j] = bf2f(f2bf(bf_pos(Ah[row * ldh + col]) ? acc[m][0][j] : 0.f));
+        Eb[row * lde + col] = f2bf(e[j]);
+      }
+      kt_store4(a.g_kt, r0 + m * 16 + lg * 4, col, H, e[0], e[1], e[2], e[3]);
+    }
+  }
+  if (a.dA) tr_prefetch(a.WT, wave * 16, Hin2, H, lane, pre);
+  __syncthreads();
+  TR_STAMP(6);
+
+  // S6: dA = g @ W (fp32 rows) for the layer below
+  if (a.dA) {
+    for (int cc = wave * 16; cc < Hin2; cc += HNW * 16) {
+      float4_t acc[HFM][1];
+      tl_zero(acc);
+      tr_gemm(Eb, lde, a.WT, cc, H, acc, lane, pre);
+      if (cc + HNW * 16 < Hin2) tr_prefetch(a.WT, cc + HNW * 16, Hin2, H, lane, pre);
+#pragma unroll
+      for (int m = 0; m < HFM; ++m)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a.dA[(r0 + m * 16 + lg * 4 + j) * Hin2 + cc + lr] = acc[m][0][j];
+    }
+  }
+  TR_STAMP(7);
+#undef TR_STAMP
+}
+
+// ----------------------------------------------------------------------------
+// tr_dw: grouped split-K weight gradients, part[s][p][q] = sum_{m in split s} G[m][p] X[m][q];
+// 64x64 tiles, 4 waves of 32x32
+// ----------------------------------------------------------------------------
+// G^T fragment of a route problem: rows mb*32 + lk .. +7 (inside one sibling group) at column p
+__device__ __forceinline__ uint4_t tr_route_frag(const TrDwProb& pr, int mb, int p, int lk) {
+  const int64_t m0 = static_cast<int64_t>(mb) * 32 + lk;
+  const int64_t t = m0 >> pr.logPg;
+  const int j0 = static_cast<int>(m0 & ((int64_t(1) << pr.logPg) - 1));
+  const uint32_t bits = pr.mask[static_cast<int64_t>(mb) * pr.P + p] >> lk;
+  const float* row = pr.dA + t * 2 * pr.P;
+  const float dn = row[pr.P + p] * pr.inv;
+  const float ds = row[p] + (pr.include_self ? dn : 0.f);
+  float v[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int j = j0 + i;
+    const float val = j < pr.Fg ? dn : (j == pr.Fg ? ds : 0.f);
+    v[i] = ((bits >> i) & 1u) ? val : 0.f;
+  }
+  return pack_bf16x8(v);
+}
+
+__global__ __launch_bounds__(256) void tr_dw_kernel(TrDwProbs probs) {
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  // constant indices only (no dynamic indexing of kernel arguments)
+  TrDwProb pr = probs.p[0];
+#pragma unroll
+  for (int i = 1; i < kTrMaxProbs; ++i)
+    if (probs.n > i && id >= probs.p[i].wg0) pr = probs.p[i];
+  const int local = id - pr.wg0;
+  const int s = local / pr.ntiles;
+  const int tile = local - s * pr.ntiles;
+  const int tp = tile / pr.tiles_q, tq = tile - (tile / pr.tiles_q) * pr.tiles_q;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int lr = lane & 15, lk = (lane >> 4) * 8;
+  const int p0 = tp * 64 + (wave >> 1) * 32;
+  const int q0 = tq * 64 + (wave & 1) * 32;
+  const int mb0 = s * pr.kps;
+  const int mb1 = (mb0 + pr.kps) < pr.MB ? (mb0 + pr.kps) : pr.MB;
+  const int64_t P = pr.P, Q = pr.Q;
+  if (p0 >= P || q0 >= Q) return;  // 32-wide edge of a 64-wide tile; no barriers in this kernel
+  float4_t acc[2][2];
+  tl_zero(acc);
+  if (pr.route) {
+    constexpr int KR = 4;
+    for (int mbc = mb0; mbc < mb1; mbc += KR) {
+      uint4_t av[KR][2], bv[KR][2];
+#pragma unroll
+      for (int u = 0; u < KR; ++u)
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          const int mb = mbc + u;
+          const bool ok = mb < mb1;
+          bv[u][f] = ok ? *reinterpret_cast<const uint4_t*>(pr.X + ((static_cast<int64_t>(mb) * Q + q0 + f * 16 + lr) * 32 + lk))
+                        : uint4_t{0u, 0u, 0u, 0u};
+          av[u][f] = ok ? tr_route_frag(pr, mb, p0 + f * 16 + lr, lk) : uint4_t{0u, 0u, 0u, 0u};
+        }
+#pragma unroll
+      for (int u = 0; u < KR; ++u)
+#pragma unroll
+        for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+          for (int fn = 0; fn < 2; ++fn) acc[fm][fn] = mfma16(av[u][fm], bv[u][fn], acc[fm][fn]);
+    }
+  } else {
+    constexpr int KB = 8;  // k-blocks of fragments in flight per wave
+    for (int mbc = mb0; mbc < mb1; mbc += KB) {
+      uint4_t av[KB][2], bv[KB][2];
+#pragma unroll
+      for (int u = 0; u < KB; ++u)
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          const int64_t mb = mbc + u;
+          const bool ok = mb < mb1;
+          av[u][f] = ok ? *reinterpret_cast<const uint4_t*>(pr.G + ((mb * P + p0 + f * 16 + lr) * 32 + lk))
+                        : uint4_t{0u, 0u, 0u, 0u};
+          bv[u][f] = ok ? *reinterpret_cast<const uint4_t*>(pr.X + ((mb * Q + q0 + f * 16 + lr) * 32 + lk))
+                        : uint4_t{0u, 0u, 0u, 0u};
+        }
+#pragma unroll
+      for (int u = 0; u < KB; ++u)
+#pragma unroll
+        for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+          for (int fn = 0; fn < 2; ++fn) acc[fm][fn] = mfma16(av[u][fm], bv[u][fn], acc[fm][fn]);
+    }
+  }
+  float* out = pr.part + static_cast<int64_t>(s) * P * Q;
+#pragma unroll
+  for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+    for (int fn = 0; fn < 2; ++fn)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        out[(p0 + fm * 16 + (lane >> 4) * 4 + j) * Q + q0 + fn * 16 + lr] = acc[fm][fn][j];
+}
+
+// ----------------------------------------------------------------------------
+// tr_opt: split-K reduce and/or the optimizer over the flat fp32 parameters, the bf16
+// weight shadows, loss hand-off and the RNG counter advance (hipGraph-replay safe)
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ void tr_shadow_write(const TrOptArgs& a, int64_t i, float val) {
+#pragma unroll
+  for (int s = 0; s < kTrMaxShadows; ++s) {
+    if (s >= a.nsh) break;
+    const TrShadow& sh = a.sh[s];
+    const int64_t l = i - sh.off;
+    if (l >= 0 && l < sh.n) {
+      const bf16_t b = f2bf(val);
+      const int64_t rows = sh.n / sh.cols;
+      const int64_t r = l / sh.cols, c = l - r * sh.cols;
+      sh.sh[fm_off(r, c, sh.cols)] = b;
+      if (sh.shT) sh.shT[fm_off(c, r, rows)] = b;
+    }
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void tr_opt_kernel(TrOptArgs a) {
+  const int64_t i4 = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (MODE != 0 && i4 == 0) {
+    a.loss_out[0] = a.loss_acc[0];
+    a.loss_acc[0] = 0.f;
+    a.rng[1] += 1;
+  }
+  const int64_t i = i4 * 4;
+  if (i >= a.n) return;
+  TrSeg sg = a.seg[0];
+#pragma unroll
+  for (int s = 1; s < kTrMaxSegs; ++s)
+    if (s < a.nseg && i >= a.seg[s].off) sg = a.seg[s];
+  float4_t g;
+  if (MODE != 1 && sg.part) {
+    const float4_t* src = reinterpret_cast<const float4_t*>(sg.part + (i - sg.off));
+    const int64_t stride = sg.n >> 2;
+    g = float4_t{0.f, 0.f, 0.f, 0.f};
+    for (int s0 = 0; s0 < sg.S; s0 += 8) {
+      float4_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = (s0 + u < sg.S) ? src[(s0 + u) * stride] : float4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 8; ++u) g += v[u];
+    }
+    if (MODE == 0) {
+      *reinterpret_cast<float4_t*>(a.g + i) = g;
+      return;
+    }
+  } else {
+    if (MODE == 0) return;
+    g = *reinterpret_cast<const float4_t*>(a.g + i);
+  }
+  if (!sg.part) *reinterpret_cast<float4_t*>(a.g + i) = float4_t{0.f, 0.f, 0.f, 0.f};  // atomics restart at 0
+  float4_t p = *reinterpret_cast<const float4_t*>(a.p + i);
+  float4_t m = *reinterpret_cast<const float4_t*>(a.m + i);
+  float4_t v = *reinterpret_cast<const float4_t*>(a.v + i);
+  const float t = static_cast<float>(a.step[0]);
+  const float bc1 = 1.f - __powf(a.b1, t), bc2 = 1.f - __powf(a.b2, t);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float gi = g[k] * a.grad_scale + a.wd * p[k];
+    if (a.kind == 0) {
+      m[k] = a.b1 * m[k] + (1.f - a.b1) * gi;
+      v[k] = a.b2 * v[k] + (1.f - a.b2) * gi * gi;
+      p[k] -= a.lr * (m[k] / bc1) / (sqrtf(v[k] / bc2) + a.eps);
+    } else if (a.kind == 1) {
+      v[k] += gi * gi;
+      p[k] -= a.lr * gi / (sqrtf(v[k]) + a.eps);
+    } else if (a.kind == 2) {
+      p[k] -= a.lr * gi;
+    } else {
+      m[k] = a.b1 * m[k] + gi;
+      p[k] -= a.lr * m[k];
+    }
+  }
+  *reinterpret_cast<float4_t*>(a.p + i) = p;
+  *reinterpret_cast<float4_t*>(a.m + i) = m;
+  *reinterpret_cast<float4_t*>(a.v + i) = v;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) tr_shadow_write(a, i + k, p[k]);
+}
+
+// shadows only (initialisation / after an external parameter write)
+__global__ __launch_bounds__(256) void tr_shadow_kernel(TrOptArgs a) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= a.n) return;
+  tr_shadow_write(a, i, a.p[i]);
+}
+
+}  // namespace euler_hip
+
+using namespace euler_hip;
+
+extern "C" {
+
+size_t eh_tr_fwd_lds(int D, int H, int bm, int FL, int mode) {
+  const int K2 = 2 * D;
+  const bool alias_out = H <= kTrBN && kTrBN <= K2;
+  size_t b = static_cast<size_t>(bm) * (K2 + 8) * sizeof(bf16_t);
+  if (mode != 1 && !alias_out) b += static_cast<size_t>(bm) * (kTrBN + 8) * sizeof(bf16_t);
+  if (mode != 2) b += static_cast<size_t>(bm) * (1 + FL) * sizeof(int32_t);
+  return b;
+}
+
+hipError_t eh_tr_fwd(const TrFwdArgs* a, int mode, int feat_fp32, int bm, hipStream_t s) {
+  if (a->M <= 0) return hipSuccess;
+  // every pointer the chosen mode dereferences must be set
+  if (!a->x || !a->a_next) return hipErrorInvalidValue;
+  if (mode != 2 && (!a->g.indptr || !a->g.nbr || !a->g.cumw || !a->g.prob || !a->g.alias || !a->tr.rng ||
+                    !a->roots || a->FL < 1))
+    return hipErrorInvalidValue;
+  if (mode != 1 && !a->W) return hipErrorInvalidValue;
+  if (a->D % 16 != 0 || a->D <= 0 || a->M % bm != 0) return hipErrorInvalidValue;
+  if (mode != 1 && (a->H % 64 != 0 || a->H <= 0 || (bm >> a->logPg) < 1 || (bm & ((1 << a->logPg) - 1)) != 0 ||
+                    a->Fg >= (1 << a->logPg)))
+    return hipErrorInvalidValue;
+  if (mode == 2 && feat_fp32) return hipErrorInvalidValue;
+  const size_t lds = eh_tr_fwd_lds(a->D, a->H, bm, a->FL, mode);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  const dim3 grid(static_cast<uint32_t>(a->M / bm));
+#define TR_FWD(FT, BMV, MODEV)                                                                               \
+  do {                                                                                                       \
+    EULER_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(tr_fwd_kernel<FT, BMV, MODEV>),         \
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds))); \
+    hipLaunchKernelGGL((tr_fwd_kernel<FT, BMV, MODEV>), grid, dim3(256), lds, s, *a);                       \
+    return hipGetLastError();                                                                                \
+  } while (0)
+#define TR_FWD_BM(FT, MODEV)                 \
+  do {                                       \
+    if (bm == 32) TR_FWD(FT, 32, MODEV);     \
+    if (bm == 64) TR_FWD(FT, 64, MODEV);     \
+    if (bm == 128) TR_FWD(FT, 128, MODEV);   \
+  } while (0)
+  if (mode == 0) {
+    if (feat_fp32) TR_FWD_BM(float, 0);
+    else TR_FWD_BM(bf16_t, 0);
+  } else if (mode == 1) {
+    if (feat_fp32) TR_FWD_BM(float, 1);
+    else TR_FWD_BM(bf16_t, 1);
+  } else if (mode == 2) {
+    TR_FWD_BM(bf16_t, 2);
+  }
+#undef TR_FWD_BM
+#undef TR_FWD
+  return hipErrorInvalidValue;
+}
+
+size_t eh_tr_head_lds(int Hin2, int H, int E, int C, int label_mode) {
+  const int ldmax = (E > H ? E : H);
+  size_t el = static_cast<size_t>(HB) * ((Hin2 + 8) + (H + 8) + (ldmax + 8) + (E + 8) + (C + 8));
+  if (label_mode == 2) el += static_cast<size_t>(HB) * C;
+  return el * sizeof(bf16_t);
+}
+
+hipError_t eh_tr_head(const TrHeadArgs* a, int64_t B, hipStream_t s) {
+  if (!a->A || !a->W || !a->Wfc || !a->WfcT || !a->Wout || !a->WoutT || !a->bfc || !a->roots || !a->labels ||
+      !a->A_kt || !a->h_kt || !a->emb_kt || !a->dlog_kt || !a->demb_kt || !a->g_kt || !a->dbfc || !a->loss_acc ||
+      (a->dA && !a->WT))
+    return hipErrorInvalidValue;
+  if (B % 32 != 0 || a->H % 16 != 0 || a->E % 32 != 0 || a->C % 32 != 0 || a->Hin2 % 32 != 0 ||
+      a->C_real > a->C || a->C_real <= 0)
+    return hipErrorInvalidValue;
+  const size_t lds = eh_tr_head_lds(a->Hin2, a->H, a->E, a->C, a->label_mode);
+  if (lds > 160 * 1024 - 64) return hipErrorInvalidValue;
+  EULER_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(tr_head_kernel),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+  hipLaunchKernelGGL(tr_head_kernel, dim3(static_cast<uint32_t>(B / HB)), dim3(HNW * 64), lds, s, *a);
+  return hipGetLastError();
+}
+
+hipError_t eh_tr_bwd(const TrBwdArgs* a, hipStream_t s) {
+  if (!a->dA || !a->mask || !a->WT || !a->dA_out) return hipErrorInvalidValue;
+  if (a->M % 32 != 0 || a->Hk % 32 != 0 || a->K2out % 64 != 0 || a->logPg < 4) return hipErrorInvalidValue;
+  const size_t lds = static_cast<size_t>(32) * (a->Hk + 8) * sizeof(bf16_t);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  EULER_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(tr_bwd_kernel),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+  hipLaunchKernelGGL(tr_bwd_kernel, dim3(static_cast<uint32_t>(a->M / 32)), dim3(256), lds, s, *a);
+  return hipGetLastError();
+}
+
+hipError_t eh_tr_dw(TrDwProbs* pr, hipStream_t s) {
+  if (pr->n < 1 || pr->n > kTrMaxProbs) return hipErrorInvalidValue;
+  int wg = 0;
+  for (int i = 0; i < pr->n; ++i) {
+    TrDwProb& p = pr->p[i];
+    if (p.P % 32 != 0 || p.Q % 32 != 0 || p.MB < 1 || p.kps < 1) return hipErrorInvalidValue;
+    if (p.route && (p.logPg < 3 || !p.dA || !p.mask)) return hipErrorInvalidValue;
+    if (!p.route && !p.G) return hipErrorInvalidValue;
+    if (!p.X || !p.part) return hipErrorInvalidValue;
+    p.S = static_cast<int>(ceil_div(p.MB, p.kps));
+    p.tiles_q = (p.Q + 63) / 64;
+    p.ntiles = ((p.P + 63) / 64) * p.tiles_q;
+    p.wg0 = wg;
+    wg += p.ntiles * p.S;
+  }
+  hipLaunchKernelGGL(tr_dw_kernel, dim3(static_cast<uint32_t>(wg)), dim3(256), 0, s, *pr);
+  return hipGetLastError();
+}
+
+hipError_t eh_tr_opt(const TrOptArgs* a, int mode, hipStream_t s) {
+  if (a->n % 4 != 0 || a->nseg < 1 || a->nseg > kTrMaxSegs || a->nsh > kTrMaxShadows) return hipErrorInvalidValue;
+  if (!a->p || !a->g || !a->m || !a->v || !a->step || !a->loss_acc || !a->loss_out || !a->rng)
+    return hipErrorInvalidValue;
+  for (int i = 0; i < a->nsh; ++i)
+    if (!a->sh[i].sh || a->sh[i].cols <= 0) return hipErrorInvalidValue;
+  for (int i = 0; i < a->nseg; ++i)
+    if (a->seg[i].off % 4 != 0 || a->seg[i].n % 4 != 0) return hipErrorInvalidValue;
+  if (mode == 3) {
+    hipLaunchKernelGGL(tr_shadow_kernel, dim3(static_cast<uint32_t>(ceil_div(a->n, 256))), dim3(256), 0, s, *a);
+    return hipGetLastError();
+  }
+  const dim3 grid(static_cast<uint32_t>(ceil_div(a->n / 4, 256)));
+  if (mode == 0) hipLaunchKernelGGL(tr_opt_kernel<0>, grid, dim3(256), 0, s, *a);
+  else if (mode == 1) hipLaunchKernelGGL(tr_opt_kernel<1>, grid, dim3(256), 0, s, *a);
+  else if (mode == 2) hipLaunchKernelGGL(tr_opt_kernel<2>, grid, dim3(256), 0, s, *a);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,157 @@
+// Argument blocks of the fused GraphSAGE tree-step kernels (sage_tree.hip), shared by
+// the kernels and the host binding (binding_tree.cpp).  Plain C++ (no device code):
+// the binding TU is compiled by g++.
+//
+// Mini-batch layout ("slotted tree"): level 0 = B roots; every row of level k-1 owns a
+// group of P_k = 2^logP_k slots at level k: slots 0..F_k-1 are its F_k sampled
+// neighbours, slot F_k is the row itself, the rest are padding (node -1, zero rows).
+// The rows of a sibling group are contiguous and power-of-two aligned, so the tree
+// mean of a layer is a block-local epilogue and the backward routing of a row is
+// row >> logP (no index tensors, no atomics).
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+namespace euler_hip {
+
+constexpr int kTrMaxProbs = 6;
+constexpr int kTrMaxSegs = 8;
+constexpr int kTrMaxShadows = 8;
+constexpr int kTrHeadRows = 16;  // roots per block of the head kernel
+
+struct TrGraph {
+  const int64_t* indptr;    // [N*T + 1]
+  const int32_t* nbr;       // [E] neighbour rows
+  const float* cumw;        // [E] per-segment inclusive prefix sums of edge weights
+  int64_t num_rows;
+  int32_t num_types;
+  const float* prob;        // root alias table over `pop` candidates
+  const int32_t* alias;
+  const int32_t* root_rows;  // optional candidate -> row map (node-type subsets)
+  int64_t pop;
+};
+
+// sampling chain above the target rows of layer 0 (levels 1 and 2 at most)
+struct TrTree {
+  const int64_t* rng;  // device (seed, counter)
+  int32_t F1, F2;      // fanouts of hops 1 and 2
+  int32_t logP1, logP2;
+  uint32_t m1, m2;     // edge-type masks of hops 1 and 2
+};
+
+// one fused SAGE layer: mode 0 = sample + gather + GEMM + tree-mean epilogue (layer 0),
+// mode 1 = sample + gather only, writing [x_self | mean x_nbr] rows (1-hop models),
+// mode 2 = rows + GEMM + tree-mean epilogue (inner layers of 3-hop models)
+struct TrFwdArgs {
+  TrGraph g;
+  TrTree tr;
+  const void* x;         // modes 0/1: feature table [N][D] (bf16 or fp32); mode 2: A rows bf16 [M][2D]
+  int32_t D;             // input width (padded, % 16 == 0)
+  int64_t M;             // target rows
+  int32_t lv;            // level of the target rows (modes 0/1)
+  int32_t FL;            // leaf fanout (hop lv + 1)
+  uint32_t mL;           // leaf edge-type mask
+  int32_t hopL;          // leaf hop number (Philox stream)
+  int32_t include_self;
+  float inv_leaf;        // 1 / (FL + include_self)
+  const uint16_t* W;     // fm bf16 [H][2D]
+  int32_t H;             // output width (% 64 == 0)
+  uint16_t* a_kt;        // [M/32][2D][32] A operand of dW (optional)
+  uint32_t* mask;        // [M/32][H] ReLU bits (optional)
+  uint16_t* a_next;      // modes 0/2: [M >> logPg][2H] parent A rows; mode 1: [M][2D]
+  int32_t logPg, Fg;     // sibling groups of the target rows: size 2^logPg, Fg neighbour slots
+  float inv_grp;         // 1 / (Fg + include_self)
+  int32_t* roots;        // [B] sampled roots (written by the root's self-chain row)
+  int32_t* nodes;        // [M] node of every target row (optional)
+  int32_t* leaf;         // [M][FL] leaf samples (optional)
+  int64_t* step;         // optimizer step counter (block 0 increments it)
+};
+
+// head: last SAGE conv + fc + out_fc + sigmoid-CE + backward down to dA, kTrHeadRows roots / block
+struct TrHeadArgs {
+  const uint16_t* A;     // [B][Hin2] bf16 rows [self | mean]
+  int32_t Hin2, H, E, C, C_real;
+  const uint16_t *W, *WT, *Wfc, *WfcT, *Wout, *WoutT;  // fm shadows
+  const float* bfc;      // [E]
+  const int32_t* roots;  // [B]
+  const void* labels;    // mode 0: int16 [N] class ids, 1: int32 [N], 2: bf16 [N][C] dense
+  int32_t label_mode;
+  float inv_scale;       // 1 / (B * C_real)
+  uint16_t *A_kt, *h_kt, *emb_kt, *dlog_kt, *demb_kt, *g_kt;
+  float* dA;             // [B][Hin2] fp32 (nullptr: no lower layer)
+  float* dbfc;           // [E] (atomically accumulated)
+  float* loss_acc;
+  uint32_t* counts;      // tp, fp, fn (threshold 0.5), accumulated
+  long long* prof;       // optional per-block phase stamps [B/16][8]
+};
+
+// inner-layer backward (3-hop): dA_out = route(dA_parent, mask) @ W  (fp32 rows)
+struct TrBwdArgs {
+  const float* dA;       // parent gradient [M >> logPg][2Hk]
+  const uint32_t* mask;  // [M/32][Hk]
+  const uint16_t* WT;    // fm [K2out][Hk]
+  int32_t Hk, K2out;
+  int64_t M;
+  int32_t logPg, Fg, include_self;
+  float inv;
+  float* dA_out;         // [M][K2out]
+};
+
+// split-K dW = G^T X for one weight; route problems build G from the parent gradient
+struct TrDwProb {
+  const uint16_t* G;     // kt [M/32][P][32] (non-route)
+  const uint16_t* X;     // kt [M/32][Q][32]
+  float* part;           // [S][P][Q]
+  int32_t P, Q, MB, kps, S, tiles_q, ntiles, wg0;
+  const float* dA;       // route: [M >> logPg][2P]
+  const uint32_t* mask;  // route: [M/32][P]
+  int32_t route, logPg, Fg, include_self;
+  float inv;
+};
+struct TrDwProbs {
+  TrDwProb p[kTrMaxProbs];
+  int32_t n;
+};
+
+// flat parameter buffer segments: part != nullptr -> gradient = sum of S split-K partials;
+// else it is accumulated in g (atomically, e.g. the fc bias) and zeroed after use
+struct TrSeg {
+  int64_t off, n;
+  const float* part;
+  int32_t S;
+};
+struct TrShadow {
+  int64_t off, n;
+  int32_t cols;
+  uint16_t* sh;   // fm [rows][cols]
+  uint16_t* shT;  // fm [cols][rows] (optional)
+};
+struct TrOptArgs {
+  float *p, *g, *m, *v;
+  int64_t n;
+  TrSeg seg[kTrMaxSegs];
+  int32_t nseg;
+  TrShadow sh[kTrMaxShadows];
+  int32_t nsh;
+  const int64_t* step;
+  float lr, b1, b2, eps, wd, grad_scale;
+  int32_t kind;  // 0 adam, 1 adagrad, 2 sgd, 3 momentum
+  float* loss_acc;
+  float* loss_out;
+  int64_t* rng;
+};
+
+}  // namespace euler_hip
+
+extern "C" {
+// feat_fp32: feature table dtype (modes 0/1); bm: rows per block (32, 64 or 128)
+hipError_t eh_tr_fwd(const euler_hip::TrFwdArgs* a, int mode, int feat_fp32, int bm, hipStream_t s);
+hipError_t eh_tr_head(const euler_hip::TrHeadArgs* a, int64_t B, hipStream_t s);
+hipError_t eh_tr_bwd(const euler_hip::TrBwdArgs* a, hipStream_t s);
+// fills S / tiles / wg0 of every problem from P, Q, MB, kps before launching
+hipError_t eh_tr_dw(euler_hip::TrDwProbs* p, hipStream_t s);
+// mode 0: split-K reduce into g; 1: optimizer from g; 2: both fused (single process)
+hipError_t eh_tr_opt(const euler_hip::TrOptArgs* a, int mode, hipStream_t s);
+size_t eh_tr_fwd_lds(int D, int H, int bm, int FL, int mode);
+size_t eh_tr_head_lds(int Hin2, int H, int E, int C, int label_mode);
+}

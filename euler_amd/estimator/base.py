@@ -171,7 +171,7 @@ class BaseEstimator:
         dense = [p for p in params if not is_sharded(p)]
         self._sync = dp.GradSync(dense, bucket_bytes=int(self.params.get("bucket_bytes", 32 << 20)))
 
-    def save(self, step=None):
+    def save(self, step=None, extra=None):
         step = self.global_step if step is None else step
         if self.rank != 0 and not any(is_sharded(p) for p in self.model.parameters()):
             return None
@@ -183,6 +183,7 @@ class BaseEstimator:
         state = {"step": step, "model": model_state,
                  "optimizer": self.optimizer.state_dict() if self.optimizer is not None else None,
                  "world": self.world, "torch_rng": torch.get_rng_state()}
+        state.update(extra or {})
         tmp = path + ".tmp"
         torch.save(state, tmp)
         os.replace(tmp, path)
@@ -245,6 +246,8 @@ class BaseEstimator:
 
     # ------------------------------------------------------------------ modes
     def train(self):
+        if self.params.get("device_graph"):
+            return self._train_device_graph()
         seed = self.params.get("seed")
         if seed is not None:
             torch.manual_seed(int(seed) + self.rank)
@@ -323,6 +326,101 @@ class BaseEstimator:
         if prof is not None:
             prof.stop()
         self.save()
+        dp.barrier()
+        return last
+
+    def _device_graph_trainer(self, first):
+        """Upload the engine's graph (structure, the model's feature and label columns) to
+        HBM and build the fused device trainer for ``self.model`` (SupervisedGraphSage)."""
+        import euler_amd.ops.graph_api as ge
+        from euler_amd.graph.device_graph import DeviceGraph
+        from euler_amd.models.sage_trainer import SageTrainer
+
+        model = self.model
+        gnn = getattr(model, "gnn", None)
+        if gnn is None or not hasattr(gnn, "feature_idx") or not hasattr(model, "label_idx"):
+            raise ValueError("device_graph=True trains SupervisedGraphSage-style models (gnn.feature_idx, label_idx)")
+        self._prepare(first)  # materialise the lazy layers, broadcast rank 0's weights
+        nt = self.params.get("train_node_type", -1)
+        node_type = -1 if nt in (None, -1, "-1") else int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
+        fdt = torch.float32 if self.params.get("device_feature_dtype", "bf16") == "fp32" else torch.bfloat16
+        seed = int(self.params.get("seed") or 0)
+        graph = DeviceGraph.from_engine(node_type=node_type, features=gnn.feature_idx, feature_dims=gnn.feature_dim,
+                                        label=model.label_idx, label_dim=model.label_dim, feature_dtype=fdt,
+                                        seed=seed * 7919 + self.rank, device=self.device)
+        return SageTrainer.from_model(model, graph, int(self.params["batch_size"]),
+                                      optimizer=self.params.get("optimizer", "adam"),
+                                      learning_rate=float(self.params.get("learning_rate", 0.001)),
+                                      keep_samples=False)
+
+    def _train_device_graph(self):
+        """NodeEstimator.train() on the device path: the whole mini-batch pipeline
+        (sample_node roots, SageDataFlow hops, feature / label lookup) and the model step
+        run as captured gfx950 kernels on an HBM copy of the graph (models/sage_trainer.py);
+        same params, logging, checkpoints (reference names + the device optimizer state
+        and Philox counter under "device_trainer") and resume as :meth:`train`."""
+        total = int(self.params.get("total_step") or 1)
+        log_steps = int(self.params.get("log_steps", 100))
+        save_steps = int(self.run_config.get("save_checkpoints_steps", self.params.get("save_checkpoints_steps", 0))
+                         or 0)
+        first = self.get_train_from_input(self.train_input_fn(), self.params)
+        self.model.train()
+        tr = self._device_graph_trainer(first)
+        self.device_trainer = tr
+        path = latest_checkpoint(self.model_dir)
+        if path is not None:
+            state = torch.load(path, map_location="cpu", weights_only=True)
+            tr.load_logical({k: v for k, v in state["model"].items() if k in tr.state_dict()})
+            if state.get("device_trainer") is not None:
+                tr.load_trainer_state(state["device_trainer"])
+            self.global_step = int(state["step"])
+            tr.write_to_model(self.model)
+            log.info("restored %s at step %d (device path)", path, self.global_step)
+        if self.global_step >= total:
+            log.info("already trained to step %d", self.global_step)
+            return {}
+        grad_sync = None
+        if self.world > 1:
+            import torch.distributed as tdist
+
+            def grad_sync(g):
+                tdist.all_reduce(g)
+                return 1.0 / self.world
+
+        use_graph = self.device.type == "cuda" and bool(self.params.get("hipgraph", True))
+        if use_graph:
+            warm = min(2, total - self.global_step)
+            tr.capture(grad_sync, warmup=warm)
+            self.global_step += warm
+
+        def one():
+            if use_graph:
+                tr.replay()
+            else:
+                tr.step(grad_sync)
+
+        bs = int(self.params["batch_size"])
+        t0, n0 = time.time(), self.global_step
+        tr.reset_metric()
+        last = {}
+        while self.global_step < total:
+            one()
+            self.global_step += 1
+            if self.global_step % log_steps == 0 or self.global_step == total:
+                loss = float(tr.loss.item())  # syncs the stream
+                dt = max(time.time() - t0, 1e-9)
+                rate = (self.global_step - n0) * bs * self.world / dt
+                last = {"step": self.global_step, "loss": loss, "f1": tr.metric(), "samples_per_sec": rate}
+                tr.reset_metric()
+                if self.rank == 0:
+                    log.info("step = %d, loss = %.6f, f1 = %.6f (%.1f samples/s, device path)", self.global_step,
+                             loss, last["f1"], rate)
+                t0, n0 = time.time(), self.global_step
+            if save_steps and self.global_step % save_steps == 0:
+                tr.write_to_model(self.model)
+                self.save(extra={"device_trainer": tr.trainer_state(), "optimizer": None})
+        tr.write_to_model(self.model)
+        self.save(extra={"device_trainer": tr.trainer_state(), "optimizer": None})
         dp.barrier()
         return last
 

@@ -76,6 +76,9 @@ class DeviceGraph:
         self.node_prob = torch.as_tensor(node_prob, dtype=torch.float32).to(device).contiguous()
         self.node_alias = torch.as_tensor(node_alias, dtype=torch.int32).to(device).contiguous()
         self.ids = ids
+        self.root_rows = None  # optional candidate -> row map of the root sampler (node-type subset)
+        self.features = None   # optional dense node feature table [N, D] (from_engine)
+        self.labels = None     # optional label table (from_engine)
         self.rng = torch.tensor([int(seed), 0], dtype=torch.int64, device=device)
         self._cpu_gen = torch.Generator(device="cpu")
         self._cpu_gen.manual_seed(int(seed))
@@ -110,6 +113,72 @@ class DeviceGraph:
         return cls(indptr_t, torch.as_tensor(np.asarray(nbr), dtype=torch.int32), cumw, num_types, prob, alias,
                    ids, seed, device)
 
+    @classmethod
+    def from_engine(cls, engine=None, node_type=-1, features=(), feature_dims=(), label=None, label_dim=None,
+                    feature_dtype=torch.bfloat16, seed=0, device="cuda"):
+        """Upload the engine's local graph shard to HBM.
+
+        The C++ engine's columnar store (``csrc/graph``) is already a per-(row, edge type)
+        CSR with raw uint64 ids; this copies it once as ``indptr`` / int32 neighbour rows /
+        per-segment prefix-sum weights, builds the root sampler of ``node_type`` (reference
+        ``sample_node(count, node_type)``: node-weighted, -1 = every type, as
+        ``graph.cc:333-403``) and, optionally, the dense ``features`` columns (concatenated,
+        ``feature_dtype``) and the dense ``label`` column as device tables.  Rows are the
+        engine's rows (sorted by node id); :meth:`rows_of` maps raw ids to rows.  Requires
+        the embedded (local) graph: the MI355X design keeps a whole shard per GPU."""
+        from euler_amd.ops import base
+
+        eng = engine if engine is not None else base.get_engine()
+        indptr, nbr, w, T, ids, _ = eng.export_csr()
+        _, types, nw = eng.export_nodes()
+        g = cls.from_csr(indptr, nbr, w, int(T), ids=np.asarray(ids), seed=seed, device=device)
+        g.node_types = np.asarray(types)
+        g.set_root_type(node_type, node_weights=np.asarray(nw))
+        if features:
+            names = [features] if isinstance(features, (str, int)) else list(features)
+            dims = [feature_dims] if isinstance(feature_dims, int) else list(feature_dims)
+            cols = [np.asarray(eng.dense_feature(g.ids, "dense_" + str(n), int(d)), np.float32)
+                    for n, d in zip(names, dims)]
+            g.features = torch.from_numpy(np.concatenate(cols, 1)).to(device=device, dtype=feature_dtype)
+        if label is not None:
+            lab = np.asarray(eng.dense_feature(g.ids, "dense_" + str(label), int(label_dim)), np.float32)
+            g.labels = torch.from_numpy(lab).to(device)
+        return g
+
+    def set_root_type(self, node_type=-1, node_weights=None):
+        """Root sampler over the rows of ``node_type`` (-1: all rows), weighted by
+        ``node_weights`` (default 1)."""
+        n = self.num_rows
+        w = np.ones(n, np.float64) if node_weights is None else np.asarray(node_weights, np.float64)
+        if node_type is None or int(node_type) < 0:
+            rows = None
+            ww = w
+        else:
+            types = getattr(self, "node_types", None)
+            if types is None:
+                raise ValueError("node types unknown: build the graph with from_engine")
+            rows = np.flatnonzero(np.asarray(types) == int(node_type)).astype(np.int32)
+            if rows.size == 0:
+                raise ValueError(f"no node of type {node_type}")
+            ww = w[rows]
+        prob, alias = build_alias_table(ww)
+        self.node_prob = torch.from_numpy(prob).to(self.device)
+        self.node_alias = torch.from_numpy(alias).to(self.device)
+        self.root_rows = None if rows is None else torch.from_numpy(rows).to(self.device)
+
+    def rows_of(self, ids) -> torch.Tensor:
+        """Rows of raw node ids (-1 when absent)."""
+        q = np.asarray(ids, dtype=np.uint64).reshape(-1)
+        if self.ids is None:
+            r = q.astype(np.int64)
+            r[(r < 0) | (r >= self.num_rows)] = -1
+            return torch.from_numpy(r)
+        srt = np.asarray(self.ids, dtype=np.uint64)
+        pos = np.searchsorted(srt, q)
+        pos_c = np.minimum(pos, max(len(srt) - 1, 0))
+        hit = (pos < len(srt)) & (srt[pos_c] == q) if len(srt) else np.zeros(q.shape, bool)
+        return torch.from_numpy(np.where(hit, pos_c, -1).astype(np.int64))
+
     # ------------------------------------------------------------------ randomness
     def advance(self, inc: int = 1):
         """Bump the device-side Philox counter (once per training step)."""
@@ -134,11 +203,14 @@ class DeviceGraph:
     # ------------------------------------------------------------------ sampling
     def sample_node(self, count: int, stream_id: int = 1) -> torch.Tensor:
         if use_hip(self.node_prob):
-            return hip().alias_sample(self.node_prob, self.node_alias, None, int(count), self.rng, int(stream_id))
-        n = self.num_rows
+            return hip().alias_sample(self.node_prob, self.node_alias, self.root_rows, int(count), self.rng,
+                                      int(stream_id))
+        n = self.node_prob.numel()
         k = torch.randint(0, n, (count,), generator=self._cpu_gen)
         u = torch.rand(count, generator=self._cpu_gen)
         pick = torch.where(u < self.node_prob[k], k, self.node_alias[k].long())
+        if self.root_rows is not None:
+            pick = self.root_rows.long()[pick]
         return pick.int()
 
     def sample_neighbor(self, rows: torch.Tensor, count: int, edge_types=None, default: int = -1,

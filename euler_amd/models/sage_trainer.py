@@ -1,0 +1,584 @@
+"""Supervised GraphSAGE training on an HBM-resident graph: the framework's device path.
+
+Model = the reference ``SupervisedGraphSage`` (``examples/graphsage/graphsage.py:56-67``):
+``dims[:-1]`` SAGEConv layers (``self_fc(x) + neigh_fc(mean_j x_j)``, no bias, ReLU;
+``convolution/sage_conv.py:33-44``), ``fc`` = Dense(dims[-1]) with bias, ``out_fc`` =
+Dense(label_dim) without, sigmoid cross-entropy averaged over ``[batch, label_dim]``
+(``mp_utils/base.py:24-47``), roots drawn by ``sample_node(batch, train_node_type)``
+(``euler_estimator/python/node_estimator.py``) and neighbours by the reference
+``SageDataFlow`` (``sage_dataflow.py:35-50``: every hop re-samples all nodes of the
+previous hops), trained with adam / adagrad / sgd / momentum (``utils/optimizers.py``).
+
+Execution (MI355X): the graph (CSR + prefix-sum weights), the feature table and the
+labels live in HBM (:meth:`DeviceGraph.from_engine` uploads a loaded dataset;
+:meth:`DeviceGraph.synthetic` builds one on the GPU).  A training step is 4 gfx950
+launches for 2 hops (``csrc/hip/sage_tree.hip``): sampling + gather + GEMM + tree mean,
+the fused head (last conv, fc, out_fc, loss, backward), the grouped split-K dW with the
+tree routing of the outer layer's gradient built in, and the reduce + optimizer + bf16
+weight shadows.  All state (RNG counter, optimizer step) is on the device, so the step
+is captured once into a hipGraph and replayed; with data parallelism the flat gradient
+is all-reduced (RCCL) between the split-K reduce and the optimizer.
+
+Layout: dims are padded (features to 16, conv widths to 64, fc / labels to 32) with
+zero rows / columns that provably stay zero (their gradients are exactly zero), and the
+mini-batch is the "slotted tree" of ``csrc/hip/tree_args.h`` (power-of-two sibling
+groups of F + 1 used slots).  Without dedup every occurrence draws its own neighbours:
+the same estimator as the reference flow, in static shapes.
+
+On a CPU device the same model, sampling layout and optimizer run in fp32 torch
+(:meth:`_cpu_step`); that implementation is also the numerics oracle of the kernels
+(:meth:`reference_loss_and_grads`).  Checkpoints hold the weights in the reference
+``SupervisedGraphSage`` parameter names (unpadded), the optimizer slots in the same
+names, the step and the Philox ``(seed, counter)``, so training resumes bit-for-bit
+on the same sample stream and a checkpoint loads into the torch model for evaluate /
+infer.
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from euler_amd.ops._native import hip
+
+__all__ = ["SageTrainer", "sage_param_names"]
+
+_OPT_KIND = {"adam": 0, "adagrad": 1, "sgd": 2, "momentum": 3}
+
+
+def _ceil(x: int, m: int) -> int:
+    return -(-int(x) // m) * m
+
+
+def _slot(f: int) -> int:
+    """log2 of the sibling-group size of a hop with fanout f (>= 16 rows, >= f + 1 slots)."""
+    p = 4
+    while (1 << p) < f + 1:
+        p += 1
+    return p
+
+
+def sage_param_names(num_layers: int):
+    """Parameter names of the reference model (euler_amd.models.SupervisedGraphSage)."""
+    names = []
+    for k in range(num_layers):
+        names += [f"gnn.convs.{k}.self_fc.weight", f"gnn.convs.{k}.neigh_fc.weight"]
+    return names + ["gnn.fc.weight", "gnn.fc.bias", "out_fc.weight"]
+
+
+def _xavier(shape, gen):
+    fan_out, fan_in = shape
+    a = math.sqrt(6.0 / (fan_in + fan_out))
+    return (torch.rand(shape, generator=gen, dtype=torch.float64) * 2 - 1).mul_(a).float()
+
+
+class SageTrainer:
+    def __init__(self, graph, batch_size, fanouts, dims, label_dim, features=None, labels=None, metapath=None,
+                 add_self_loops=False, optimizer="adam", learning_rate=0.01, betas=(0.9, 0.999), eps=1e-8,
+                 weight_decay=0.0, init=None, init_seed=0, keep_samples=True):
+        self.graph = graph
+        self.device = graph.device
+        self.B = int(batch_size)
+        self.fanouts = [int(f) for f in fanouts]
+        self.L = len(self.fanouts)
+        if not 1 <= self.L <= 3:
+            raise ValueError("1 to 3 hops are supported")
+        dims = [int(d) for d in dims]
+        if len(dims) != self.L + 1:
+            raise ValueError("dims = conv widths (one per hop) + the fc width (reference dims[:-1] / dims[-1])")
+        if self.B % 32:
+            raise ValueError("batch_size must be a multiple of 32")
+        self.conv_dims, self.E = dims[:-1], dims[-1]
+        self.C = int(label_dim)
+        self.include_self = bool(add_self_loops)
+        self.opt_name = optimizer
+        if optimizer not in _OPT_KIND:
+            raise ValueError(f"optimizer must be one of {sorted(_OPT_KIND)}")
+        self.lr, self.betas, self.eps, self.wd = float(learning_rate), tuple(betas), float(eps), float(weight_decay)
+        if optimizer == "momentum" and betas == (0.9, 0.999):
+            self.betas = (0.9, 0.0)  # momentum coefficient (reference MomentumOptimizer(lr, 0.9))
+        if optimizer == "adagrad" and eps == 1e-8:
+            self.eps = 1e-10
+        feats = features if features is not None else graph.features
+        labs = labels if labels is not None else graph.labels
+        if feats is None or labs is None:
+            raise ValueError("features and labels are required (or a graph built with from_engine)")
+        self.D = int(feats.shape[1])
+        masks = metapath if metapath is not None else [None] * self.L
+        if len(masks) != self.L:
+            raise ValueError("one metapath entry (edge types) per hop")
+        self.masks = [graph._mask(m) for m in masks]
+
+        # padded widths and the slotted tree
+        self.Dp = _ceil(self.D, 16)
+        self.Hp = [_ceil(h, 64) for h in self.conv_dims]
+        self.Ep, self.Cp = _ceil(self.E, 32), _ceil(self.C, 32)
+        self.logP = [0] + [_slot(self.fanouts[k - 1]) for k in range(1, self.L)]
+        self.M = [self.B]
+        for k in range(1, self.L):
+            self.M.append(self.M[-1] << self.logP[k])
+        self.on_gpu = self.device.type == "cuda"
+
+        # feature / label tables in the kernels' layout (padded copies only when needed)
+        self.features = self._pad_cols(feats, self.Dp, feats.dtype if feats.dtype in (torch.bfloat16,
+                                                                                  torch.float32) else torch.float32)
+        self.label_mode, self.labels = self._label_table(labs)
+
+        # logical parameters -> padded flat layout
+        self._shapes = self._logical_shapes()
+        logical = self._init_logical(init, init_seed)
+        self._build_flat()
+        self.keep_samples = keep_samples
+        self.step_count = 0  # host mirror (the device counter is authoritative on the GPU)
+        if self.on_gpu:
+            self._alloc_gpu()
+            self.load_logical(logical)
+        else:
+            self._cpu_params = {k: v.clone().to(self.device).requires_grad_(True) for k, v in logical.items()}
+            self._cpu_m = {k: torch.zeros_like(v) for k, v in logical.items()}
+            self._cpu_v = {k: torch.full_like(v, 0.1 if optimizer == "adagrad" else 0.0) for k, v in
+                           logical.items()}
+            self._cpu_loss = torch.zeros(())
+            self._cpu_counts = [0, 0, 0]
+            self._cpu_samples = None
+        self._graph_exec = None
+
+    # ------------------------------------------------------------------ construction helpers
+    @classmethod
+    def from_model(cls, model, graph, batch_size, optimizer="adam", learning_rate=0.01, **kw):
+        """Trainer for a (materialised) ``SupervisedGraphSage``: dims, fanouts, metapath,
+        self loops, feature / label names come from the model, weights are copied."""
+        from euler_amd.convolution.convs import SAGEConv
+        from euler_amd.dataflow.dataflows import SageDataFlow
+        import euler_amd.ops.graph_api as ge
+
+        gnn = model.gnn
+        if not all(isinstance(c, SAGEConv) for c in gnn.convs) or not isinstance(gnn.sampler, SageDataFlow):
+            raise ValueError("the device path trains SAGEConv + SageDataFlow models (SupervisedGraphSage)")
+        dims = [c.self_fc.out_features for c in gnn.convs] + [gnn.fc.out_features]
+        metapath = []
+        for m in gnn.sampler.metapath:
+            ids = None if m is None else [int(t) for t in np.asarray(ge.get_edge_type_id(m)).reshape(-1)]
+            metapath.append(None if ids is None or any(t < 0 for t in ids) else ids)  # -1 = every type
+        return cls(graph, batch_size, gnn.sampler.fanouts, dims, model.label_dim, metapath=metapath,
+                   add_self_loops=bool(getattr(gnn.sampler, "add_self_loops", False)), optimizer=optimizer,
+                   learning_rate=learning_rate, init=model, **kw)
+
+    def _pad_cols(self, t, width, dtype):
+        t = t.to(self.device)
+        if t.shape[1] == width and t.dtype == dtype and t.is_contiguous():
+            return t
+        out = torch.zeros((t.shape[0], width), dtype=dtype, device=self.device)
+        out[:, : t.shape[1]] = t.to(dtype)
+        return out
+
+    def _label_table(self, labs):
+        labs = labs.to(self.device)
+        if labs.dim() == 1 or (labs.dim() == 2 and labs.shape[1] == 1 and not labs.is_floating_point()):
+            labs = labs.reshape(-1)
+            if labs.dtype == torch.int16:
+                return 0, labs.contiguous()
+            return 1, labs.to(torch.int32).contiguous()
+        if labs.shape[1] != self.C:
+            raise ValueError(f"label table has {labs.shape[1]} columns, label_dim is {self.C}")
+        self._labels_dense = labs.float()
+        return 2, self._pad_cols(labs, self.Cp, torch.bfloat16)
+
+    def _logical_shapes(self):
+        shapes = {}
+        hin = self.D
+        for k, h in enumerate(self.conv_dims):
+            shapes[f"gnn.convs.{k}.self_fc.weight"] = (h, hin)
+            shapes[f"gnn.convs.{k}.neigh_fc.weight"] = (h, hin)
+            hin = h
+        shapes["gnn.fc.weight"] = (self.E, hin)
+        shapes["gnn.fc.bias"] = (self.E,)
+        shapes["out_fc.weight"] = (self.C, self.E)
+        return shapes
+
+    def _init_logical(self, init, seed):
+        if init is not None and not isinstance(init, dict):
+            sd = init.state_dict()
+            init = {k: sd[k] for k in self._shapes if k in sd}
+        gen = torch.Generator().manual_seed(int(seed))
+        out = {}
+        for k, shp in self._shapes.items():
+            if init is not None and k in init:
+                v = torch.as_tensor(init[k]).detach().float().cpu()
+                if tuple(v.shape) != tuple(shp):
+                    raise ValueError(f"{k}: shape {tuple(v.shape)} != {shp}")
+                out[k] = v.clone()
+            elif k.endswith("bias"):
+                out[k] = torch.zeros(shp)
+            else:
+                out[k] = _xavier(shp, gen)
+        return out
+
+    def _build_flat(self):
+        """offsets of the padded flat parameter buffer: convs, fc W, fc b, out W"""
+        sizes = []
+        hin = self.Dp
+        for h in self.Hp:
+            sizes.append(h * 2 * hin)
+            hin = h
+        sizes += [self.Ep * hin, self.Ep, self.Cp * self.Ep]
+        self.offsets = [0]
+        for s in sizes:
+            self.offsets.append(self.offsets[-1] + s)
+
+    def _flat_views(self, flat):
+        """padded views of a flat buffer: [conv_0 .. conv_{L-1}, fc_w, fc_b, out_w]"""
+        o = self.offsets
+        views = []
+        hin = self.Dp
+        for k, h in enumerate(self.Hp):
+            views.append(flat[o[k]:o[k + 1]].view(h, 2 * hin))
+            hin = h
+        L = self.L
+        views.append(flat[o[L]:o[L + 1]].view(self.Ep, hin))
+        views.append(flat[o[L + 1]:o[L + 2]])
+        views.append(flat[o[L + 2]:o[L + 3]].view(self.Cp, self.Ep))
+        return views
+
+    def _pack(self, logical, flat):
+        """logical (unpadded) tensors -> padded flat buffer (padding zero)"""
+        flat.zero_()
+        v = self._flat_views(flat)
+        hin, hinp = self.D, self.Dp
+        for k, h in enumerate(self.conv_dims):
+            v[k][:h, :hin] = logical[f"gnn.convs.{k}.self_fc.weight"].to(flat)
+            v[k][:h, hinp:hinp + hin] = logical[f"gnn.convs.{k}.neigh_fc.weight"].to(flat)
+            hin, hinp = h, self.Hp[k]
+        L = self.L
+        v[L][: self.E, :hin] = logical["gnn.fc.weight"].to(flat)
+        v[L + 1][: self.E] = logical["gnn.fc.bias"].to(flat)
+        v[L + 2][: self.C, : self.E] = logical["out_fc.weight"].to(flat)
+
+    def _unpack(self, flat):
+        v = self._flat_views(flat)
+        out = {}
+        hin, hinp = self.D, self.Dp
+        for k, h in enumerate(self.conv_dims):
+            out[f"gnn.convs.{k}.self_fc.weight"] = v[k][:h, :hin].clone()
+            out[f"gnn.convs.{k}.neigh_fc.weight"] = v[k][:h, hinp:hinp + hin].clone()
+            hin, hinp = h, self.Hp[k]
+        L = self.L
+        out["gnn.fc.weight"] = v[L][: self.E, :hin].clone()
+        out["gnn.fc.bias"] = v[L + 1][: self.E].clone()
+        out["out_fc.weight"] = v[L + 2][: self.C, : self.E].clone()
+        return out
+
+    # ------------------------------------------------------------------ GPU buffers + plan
+    def _alloc_gpu(self):
+        dev, B, L = self.device, self.B, self.L
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        f32 = dict(dtype=torch.float32, device=dev)
+        i32 = dict(dtype=torch.int32, device=dev)
+        n = self.offsets[-1]
+        self.flat = torch.zeros(n, **f32)
+        self.grad = torch.zeros(n, **f32)
+        self.m = torch.zeros(n, **f32)
+        self.v = torch.zeros(n, **f32)
+        self._step = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.loss_acc = torch.zeros(1, **f32)
+        self.loss_out = torch.zeros(1, **f32)
+        self.counts = torch.zeros(3, **i32)
+        if self.opt_name == "adagrad":
+            self.v.fill_(0.1)  # reference AdagradOptimizer initial_accumulator_value
+        g = self.graph
+        d = {"L": L, "B": B, "F": [0] + self.fanouts, "logP": self.logP[:L] if L > 1 else [0],
+             "masks": [0] + [int(m) & 0xFFFFFFFF for m in self.masks], "H": self.Hp, "D": self.Dp,
+             "E": self.Ep, "C": self.Cp, "C_real": self.C, "include_self": int(self.include_self),
+             "indptr": g.indptr, "nbr": g.nbr, "cumw": g.cumw, "num_types": g.num_types, "node_prob": g.node_prob,
+             "node_alias": g.node_alias, "root_rows": g.root_rows, "rng": g.rng,
+             "features": self.features, "labels": self.labels, "label_mode": self.label_mode,
+             "step": self._step, "flat": self.flat, "grad": self.grad, "m": self.m, "v": self.v,
+             "offsets": self.offsets, "loss_acc": self.loss_acc, "loss_out": self.loss_out, "counts": self.counts,
+             "lr": self.lr, "beta1": self.betas[0], "beta2": self.betas[1], "eps": self.eps,
+             "weight_decay": self.wd, "opt_kind": _OPT_KIND[self.opt_name]}
+        for key in ("EULER_AMD_DW_TARGET_WG", "EULER_AMD_DW_MIN_KPS"):
+            if os.environ.get(key):
+                d[key[len("EULER_AMD_"):].lower()] = int(os.environ[key])
+        M_last = self.M[L - 1]
+        FL = self.fanouts[-1]
+        self.roots = torch.zeros(B, **i32)
+        d["roots"] = self.roots
+        if self.keep_samples:
+            self.nodes = torch.zeros(M_last, **i32)
+            self.leaf = torch.zeros(M_last * FL, **i32)
+            d["nodes"], d["leaf"] = self.nodes, self.leaf
+        # layer inputs: A rows (row-major) feed the next layer / head, A_kt the dW GEMMs
+        hin = [self.Dp] + self.Hp[:-1]
+        for k in range(L):
+            rows = self.M[L - 1 - k]
+            d[f"A{k}_kt"] = torch.empty(rows * 2 * hin[k], **bf)
+            if k >= 1 or L == 1:
+                d[f"A{k}"] = torch.empty(rows * 2 * hin[k], **bf)
+            if k < L - 1:
+                d[f"mask{k}"] = torch.zeros((rows // 32) * self.Hp[k], **i32)
+                d[f"dA{k + 1}"] = torch.empty(self.M[L - 2 - k] * 2 * self.Hp[k], **f32)
+        H = self.Hp[-1]
+        for name, cols in (("h_kt", H), ("emb_kt", self.Ep), ("dlog_kt", self.Cp), ("demb_kt", self.Ep),
+                           ("g_kt", H)):
+            d[name] = torch.empty(B * cols, **bf)
+        views = self._flat_views(self.flat)
+        for k in range(L):
+            d[f"W{k}_sh"] = torch.empty(views[k].numel(), **bf)
+            if k >= 1:
+                d[f"W{k}_shT"] = torch.empty(views[k].numel(), **bf)
+        for name, t in (("Wfc", views[L]), ("Wout", views[L + 2])):
+            d[f"{name}_sh"] = torch.empty(t.numel(), **bf)
+            d[f"{name}_shT"] = torch.empty(t.numel(), **bf)
+        d["bfc"] = views[L + 1]
+        self._buf = d
+        self.plan = hip().TreePlan(d)
+
+    # ------------------------------------------------------------------ parameters / state
+    def load_logical(self, logical):
+        """Set the weights from logical (unpadded, reference-named) tensors."""
+        if self.on_gpu:
+            self._pack({k: torch.as_tensor(v) for k, v in logical.items()}, self.flat)
+            self.refresh_shadows()
+        else:
+            with torch.no_grad():
+                for k, v in logical.items():
+                    self._cpu_params[k].copy_(torch.as_tensor(v).to(self._cpu_params[k]))
+
+    def refresh_shadows(self):
+        """Rebuild the bf16 weight shadows from the fp32 parameters (after an external
+        write such as a load or the data-parallel broadcast)."""
+        if self.on_gpu:
+            self.plan.opt(3)
+
+    def logical_params(self):
+        if self.on_gpu:
+            return self._unpack(self.flat.detach())
+        return {k: v.detach().clone() for k, v in self._cpu_params.items()}
+
+    def state_dict(self):
+        """Weights in the reference model's names (unpadded)."""
+        return {k: v.cpu() for k, v in self.logical_params().items()}
+
+    def write_to_model(self, model):
+        """Copy the trained weights into a (materialised) SupervisedGraphSage."""
+        sd = model.state_dict()
+        with torch.no_grad():
+            for k, v in self.logical_params().items():
+                sd[k].copy_(v.to(sd[k]))
+
+    def trainer_state(self):
+        """Optimizer slots (reference names), step and the device RNG (seed, counter)."""
+        if self.on_gpu:
+            m, v = self._unpack(self.m), self._unpack(self.v)
+            step = int(self._step.item())
+        else:
+            m = {k: t.clone() for k, t in self._cpu_m.items()}
+            v = {k: t.clone() for k, t in self._cpu_v.items()}
+            step = self.step_count
+        return {"m": {k: t.cpu() for k, t in m.items()}, "v": {k: t.cpu() for k, t in v.items()}, "step": step,
+                "rng": self.graph.rng.detach().cpu().clone(), "optimizer": self.opt_name}
+
+    def load_trainer_state(self, st):
+        self.graph.rng.copy_(torch.as_tensor(st["rng"]).to(self.graph.rng))
+        self.step_count = int(st["step"])
+        if self.on_gpu:
+            self._pack({k: torch.as_tensor(t) for k, t in st["m"].items()}, self.m)
+            self._pack({k: torch.as_tensor(t) for k, t in st["v"].items()}, self.v)
+            self._step.fill_(int(st["step"]))
+        else:
+            for k in self._cpu_m:
+                self._cpu_m[k].copy_(torch.as_tensor(st["m"][k]))
+                self._cpu_v[k].copy_(torch.as_tensor(st["v"][k]))
+
+    # ------------------------------------------------------------------ training step
+    def forward_backward(self):
+        """Sampling, forward and backward of one step; the split-K partials are reduced
+        into :attr:`grad` (the all-reduce point of data parallelism)."""
+        p = self.plan
+        p.fwd()
+        p.head()
+        p.bwd()
+        p.dw(list(range(p.num_problems())))
+        p.opt(0)
+
+    def optimizer_step(self, grad_scale: float = 1.0):
+        self.plan.opt(1, float(grad_scale))
+
+    def step(self, grad_sync=None):
+        """One training step.  ``grad_sync(grad)`` (e.g. an RCCL all-reduce) runs between
+        the gradient reduce and the optimizer; None = single process (fused reduce +
+        optimizer launch)."""
+        self.step_count += 1
+        if not self.on_gpu:
+            return self._cpu_step()
+        if grad_sync is None:
+            p = self.plan
+            p.fwd()
+            p.head()
+            p.bwd()
+            p.dw(list(range(p.num_problems())))
+            p.opt(2)
+        else:
+            self.forward_backward()
+            scale = grad_sync(self.grad)
+            self.optimizer_step(1.0 if scale is None else scale)
+
+    def capture(self, grad_sync=None, warmup: int = 2):
+        """Record one step into a hipGraph (after ``warmup`` eager steps on a side
+        stream); :meth:`replay` then runs it.  ``grad_sync`` is captured too (RCCL
+        collectives are capturable)."""
+        if not self.on_gpu:
+            return None
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self.step(grad_sync)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.step(grad_sync)
+        self.step_count -= 1  # the captured step did not run
+        self._graph_exec = g
+        return g
+
+    def replay(self, n: int = 1):
+        for _ in range(int(n)):
+            self._graph_exec.replay()
+        self.step_count += int(n)
+
+    def set_learning_rate(self, lr: float):
+        self.lr = float(lr)
+        if self.on_gpu:
+            self.plan.set_lr(self.lr)
+
+    @property
+    def loss(self) -> torch.Tensor:
+        """loss of the last completed step (device scalar)"""
+        return self.loss_out if self.on_gpu else self._cpu_loss
+
+    def metric(self) -> float:
+        """streaming micro-F1 (threshold 0.5) since the last :meth:`reset_metric`
+        (reference metrics.f1_score)"""
+        tp, fp, fn = (self.counts.tolist() if self.on_gpu else self._cpu_counts)
+        return 2.0 * tp / max(2.0 * tp + fp + fn, 1e-12)
+
+    def reset_metric(self):
+        if self.on_gpu:
+            self.counts.zero_()
+        else:
+            self._cpu_counts = [0, 0, 0]
+
+    # ------------------------------------------------------------------ samples + fp32 model
+    def samples(self):
+        """(roots [B], nodes of the outer layer's target slots [M], leaf draws [M, F_L]) of
+        the last step, as int64"""
+        if self.on_gpu:
+            if not self.keep_samples:
+                raise RuntimeError("keep_samples=False")
+            return (self.roots.long(), self.nodes.long(), self.leaf.view(-1, self.fanouts[-1]).long())
+        return self._cpu_samples
+
+    def _cpu_sample(self):
+        g, B = self.graph, self.B
+        roots = g.sample_node(B).long()
+        level = roots
+        for k in range(1, self.L):
+            f, P = self.fanouts[k - 1], 1 << self.logP[k]
+            nb = g._sample_neighbor_cpu(level.int(), f, self.masks[k - 1], -1, False).long()
+            slots = torch.full((level.numel(), P), -1, dtype=torch.int64)
+            slots[:, :f] = nb
+            slots[:, f] = level
+            level = slots.reshape(-1)
+        leaf = g._sample_neighbor_cpu(level.int(), self.fanouts[-1], self.masks[-1], -1, False).long()
+        return roots, level, leaf
+
+    def _labels_of(self, roots):
+        if self.label_mode == 2:
+            return self._labels_dense[roots.to(self._labels_dense.device)].float()
+        y = torch.zeros((roots.numel(), self.C), dtype=torch.float32, device=self.labels.device)
+        y.scatter_(1, self.labels[roots.to(self.labels.device)].long().view(-1, 1), 1.0)
+        return y
+
+    def logical_forward(self, params, roots, nodes, leaf):
+        """fp32 logits of the model for one sampled slotted tree"""
+        dev = params["gnn.fc.weight"].device
+        x = self.features[:, : self.D].float().to(dev)
+        x = torch.cat([x, torch.zeros(1, self.D, device=dev)], 0)
+        n = x.shape[0] - 1
+        nodes, leaf = nodes.to(dev), leaf.to(dev)
+        xs = x[torch.where(nodes < 0, torch.full_like(nodes, n), nodes)]
+        agg = x[torch.where(leaf < 0, torch.full_like(leaf, n), leaf)].sum(1)
+        cnt = self.fanouts[-1]
+        if self.include_self:
+            agg, cnt = agg + xs, cnt + 1
+        w0 = torch.cat([params["gnn.convs.0.self_fc.weight"], params["gnn.convs.0.neigh_fc.weight"]], 1)
+        h = torch.relu(torch.cat([xs, agg / cnt], 1) @ w0.t())
+        for k in range(1, self.L):
+            lvl = self.L - 1 - k
+            P, f = 1 << self.logP[lvl + 1], self.fanouts[lvl]
+            hg = h.view(-1, P, h.shape[1])
+            s, a = hg[:, f], hg[:, :f].sum(1)
+            c = f
+            if self.include_self:
+                a, c = a + s, c + 1
+            wk = torch.cat([params[f"gnn.convs.{k}.self_fc.weight"], params[f"gnn.convs.{k}.neigh_fc.weight"]], 1)
+            h = torch.relu(torch.cat([s, a / c], 1) @ wk.t())
+        emb = h @ params["gnn.fc.weight"].t() + params["gnn.fc.bias"]
+        return emb @ params["out_fc.weight"].t()
+
+    def reference_loss_and_grads(self, params=None, samples=None):
+        """fp32 torch autograd loss and parameter gradients on the last step's samples
+        (before its optimizer update: call after :meth:`forward_backward`)"""
+        params = {k: v.detach().float().clone().requires_grad_(True)
+                  for k, v in (params or self.logical_params()).items()}
+        roots, nodes, leaf = samples if samples is not None else self.samples()
+        logits = self.logical_forward(params, roots, nodes, leaf)
+        y = self._labels_of(roots).to(logits.device)
+        loss = F.binary_cross_entropy_with_logits(logits, y)
+        loss.backward()
+        return float(loss), {k: v.grad.detach() for k, v in params.items()}
+
+    def gradients(self):
+        """logical view of :attr:`grad` after :meth:`forward_backward` (GPU)"""
+        return self._unpack(self.grad)
+
+    def _cpu_step(self):
+        roots, nodes, leaf = self._cpu_sample()
+        self._cpu_samples = (roots, nodes, leaf)
+        P = self._cpu_params
+        for t in P.values():
+            t.grad = None
+        logits = self.logical_forward(P, roots, nodes, leaf)
+        y = self._labels_of(roots).to(logits.device)
+        loss = F.binary_cross_entropy_with_logits(logits, y)
+        loss.backward()
+        with torch.no_grad():
+            pred, pos = logits >= 0, y > 0.5
+            self._cpu_counts[0] += int((pred & pos).sum())
+            self._cpu_counts[1] += int((pred & ~pos).sum())
+            self._cpu_counts[2] += int((~pred & pos).sum())
+            t = float(self.step_count)
+            b1, b2 = self.betas
+            for k, p in P.items():
+                g = p.grad + self.wd * p
+                m, v = self._cpu_m[k], self._cpu_v[k]
+                if self.opt_name == "adam":
+                    m.mul_(b1).add_(g, alpha=1 - b1)
+                    v.mul_(b2).addcmul_(g, g, value=1 - b2)
+                    p -= self.lr * (m / (1 - b1 ** t)) / (torch.sqrt(v / (1 - b2 ** t)) + self.eps)
+                elif self.opt_name == "adagrad":
+                    v.addcmul_(g, g)
+                    p -= self.lr * g / (torch.sqrt(v) + self.eps)
+                elif self.opt_name == "sgd":
+                    p -= self.lr * g
+                else:
+                    m.mul_(b1).add_(g)
+                    p -= self.lr * m
+        self._cpu_loss = loss.detach()
+        self.graph.rng[1] += 1
+        return self._cpu_loss

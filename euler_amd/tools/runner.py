@@ -42,8 +42,9 @@ def _models():
 
     F = lambda ds: ds.feature_dim  # noqa: E731
     return {
+        # reference run_graphsage.py:48: dims = [hidden_dim] * (layers + 1)
         "graphsage": ("cora", "node", lambda a, ds: Z.SupervisedGraphSage(
-            _hidden(a, ds.label_dim), a.fanouts, _mp(a), ds.feature_idx, F(ds), ds.label_idx, ds.label_dim,
+            _hidden(a, a.hidden_dim), a.fanouts, _mp(a), ds.feature_idx, F(ds), ds.label_idx, ds.label_dim,
             max_id=ds.max_node_id)),
         "graphsage_unsup": ("cora", "node", lambda a, ds: Z.UnsupervisedGraphSage(
             _hidden(a, a.dim), a.fanouts, _mp(a), ds.feature_idx, F(ds), _first(ds.train_node_type),
@@ -176,6 +177,11 @@ def parse_args(argv=None, model=None):
     p.add_argument("--sharded", action="store_true", help="row-shard id embeddings over the process group")
     p.add_argument("--device", default=None)
     p.add_argument("--amp", default=None, help="bf16 for bf16 autocast on the GPU")
+    p.add_argument("--device_graph", action="store_true",
+                   help="graphsage: train on an HBM copy of the graph with the fused gfx950 step "
+                        "(models/sage_trainer.py) instead of the CPU-engine input pipeline")
+    p.add_argument("--device_feature_dtype", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--seed", type=int, default=None)
     return p.parse_args(argv)
 
 
@@ -198,7 +204,8 @@ def build(a):
     total = a.total_step or max(1, int(a.num_epochs * ds.total_size / max(a.batch_size, 1)))
     params = {"model_dir": a.model_dir, "infer_dir": a.infer_dir, "batch_size": a.batch_size, "total_step": total,
               "log_steps": a.log_steps, "optimizer": a.optimizer, "learning_rate": a.learning_rate,
-              "device": a.device, "amp": a.amp}
+              "device": a.device, "amp": a.amp, "device_graph": a.device_graph,
+              "device_feature_dtype": a.device_feature_dtype, "seed": a.seed}
     if kind == "node":
         params.update(train_node_type=_first(ds.train_node_type), id_file=a.id_file or ds.id_file)
         est = NodeEstimator(model, params)

@@ -1,13 +1,16 @@
 #!/usr/bin/env bash
-# One GPU session on a gpurun box: GPU tests, a short bench, a rocprofv3 kernel profile.
-# Every GPU step has its own time limit; a crash/abort/timeout (exit >= 124 or signal)
-# ends the script immediately.  Plain test failures (exit 1) let the bench still run.
+# One GPU session on a gpurun box.  STEPS selects comma-separated steps:
+#   tests=<pytest args>   (default tests: the whole -m gpu suite)
+#   bench_small, bench_full, bench_fp32, prof, sweep_batch
+# Every GPU step has its own time limit; a crash/abort/timeout (exit >= 124 or a signal)
+# ends the script immediately.  Plain test failures (exit 1) let later steps still run.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 OUT=gpurun_out
-STEPS="${STEPS:-all}"
+STEPS="${STEPS:-tests,bench_small,bench_full,prof}"
+TESTS="${TESTS:-tests -m gpu}"
 
 run() {  # run <name> <timeout> cmd...
   local name=$1 to=$2; shift 2
@@ -15,25 +18,43 @@ run() {  # run <name> <timeout> cmd...
   timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "=== $name rc=$rc"
-  tail -n 25 "$OUT/$name.log"
+  tail -n 30 "$OUT/$name.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
     echo "fatal rc=$rc in $name: stopping the session"; exit $rc
+  fi
+  if grep -qE "illegal memory access|Memory access fault|hipErrorIllegalAddress|HSA_STATUS_ERROR|faulted:" "$OUT/$name.log"; then
+    echo "GPU fault in $name: stopping the session"; exit 70
   fi
   return $rc
 }
 
-python -c "import torch; print(torch.__version__, torch.cuda.get_device_name(0))" || exit 3
 python -m euler_amd._build >"$OUT/build.log" 2>&1 || { cat "$OUT/build.log"; exit 4; }
 
-if [[ "$STEPS" == *tests* || "$STEPS" == all ]]; then
-  run pytest_gpu 900 python -m pytest tests -m gpu --maxfail=20 -q -p no:cacheprovider -rf
-fi
-if [[ "$STEPS" == *bench* || "$STEPS" == all ]]; then
-  run bench_small 400 python bench.py --num-nodes 2000000 --steps 50 --warmup 10 --log
-  run bench_full 900 python bench.py --steps 200 --warmup 20 --log
-fi
-if [[ "$STEPS" == *prof* || "$STEPS" == all ]]; then
-  run rocprof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-      python3 bench.py --num-nodes 10000000 --steps 50 --warmup 5
-fi
+IFS=',' read -ra S <<< "$STEPS"
+for st in "${S[@]}"; do
+  case "$st" in
+    debug)
+      EULER_AMD_TREE_SYNC=1 run tree_debug 300 python -u tools/tree_debug.py 0 1 2 3 4 5 6 7 8 9 || exit 71 ;;
+    tests)
+      run pytest_gpu 900 python -u -m pytest $TESTS -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -rf ;;
+    bench_small)
+      run bench_small 300 python bench.py --num-nodes 2000000 --steps 100 --warmup 10 --log ;;
+    bench_full)
+      run bench_full 600 python bench.py --steps 200 --warmup 20 --log ;;
+    bench_fp32)
+      run bench_fp32 600 python bench.py --steps 200 --warmup 20 --feature-dtype fp32 ;;
+    sweep_batch)
+      for b in 1024 2048 4096 8192 16384; do
+        run "bench_b$b" 600 python bench.py --steps 100 --warmup 10 --batch-size "$b"
+      done ;;
+    prof)
+      run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+          python3 bench.py --num-nodes 10000000 --steps 100 --warmup 5 ;;
+    prof_full)
+      run rocprof_full 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof_full" -o run --output-format csv -- \
+          python3 bench.py --steps 100 --warmup 5 ;;
+    *)
+      echo "unknown step $st"; exit 2 ;;
+  esac
+done
 echo "=== done"
