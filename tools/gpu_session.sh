@@ -37,6 +37,8 @@ for st in "${S[@]}"; do
       EULER_AMD_TREE_SYNC=1 run tree_debug 300 python -u tools/tree_debug.py 0 1 2 3 4 5 6 7 8 9 || exit 71 ;;
     tests)
       run pytest_gpu 900 python -u -m pytest $TESTS -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -rf ;;
+    smoke)
+      run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench_small)
       run bench_small 300 python bench.py --num-nodes 2000000 --steps 100 --warmup 10 --log ;;
     bench_full)
