@@ -78,9 +78,19 @@ class TreePlan {
     build_opt();
   }
 
-  void fwd() {
+  void sample() {
     const c10::DeviceGuard g(dev_);
-    ok(eh_tr_fwd(&fwd0_, L_ == 1 ? 1 : 0, feat_fp32_, bm0_, stream()), "tr_fwd");
+    ok(eh_tr_sample(&sample_, stream()), "tr_sample");
+  }
+
+  void fwd(c10::optional<torch::Tensor> prof) {
+    const c10::DeviceGuard g(dev_);
+    TrFwdArgs a0 = fwd0_;
+    if (prof.has_value()) {
+      need(*prof, torch::kInt64, (fwd0_.M / bm0_) * 8, "prof");
+      a0.prof = reinterpret_cast<long long*>(prof->data_ptr<int64_t>());
+    }
+    ok(eh_tr_fwd(&a0, L_ == 1 ? 1 : 0, feat_fp32_, bm0_, stream()), "tr_fwd");
     if (L_ == 3) ok(eh_tr_fwd(&fwd1_, 2, 0, bm1_, stream()), "tr_fwd(inner)");
   }
 
@@ -100,15 +110,29 @@ class TreePlan {
     ok(eh_tr_bwd(&bwd1_, stream()), "tr_bwd");
   }
 
+  // dW of the given problems: routed problems one launch each, the others grouped
   void dw(std::vector<int64_t> which) {
     const c10::DeviceGuard g(dev_);
     TrDwProbs p{};
     for (int64_t i : which) {
       TORCH_CHECK(i >= 0 && i < (int64_t)probs_.size(), "dw: problem index out of range");
-      p.p[p.n++] = probs_[i];
+      if (probs_[i].route) {
+        TrDwProb r = probs_[i];
+        ok(eh_tr_dw_route(&r, stream()), "tr_dw_route");
+      } else {
+        TORCH_CHECK(p.n < kTrMaxProbs, "dw: too many problems");
+        p.p[p.n++] = probs_[i];
+      }
     }
     if (p.n == 0) return;
     ok(eh_tr_dw(&p, stream()), "tr_dw");
+  }
+
+  std::vector<int64_t> problems(bool route) const {
+    std::vector<int64_t> out;
+    for (size_t i = 0; i < probs_.size(); ++i)
+      if (static_cast<bool>(probs_[i].route) == route) out.push_back(static_cast<int64_t>(i));
+    return out;
   }
 
   // mode 0 reduce, 1 optimizer, 2 fused, 3 shadows only
@@ -119,11 +143,12 @@ class TreePlan {
     ok(eh_tr_opt(&a, static_cast<int>(mode), stream()), "tr_opt");
   }
 
+  int64_t fwd_blocks() const { return fwd0_.M / bm0_; }
   void set_lr(double lr) { opt_.lr = static_cast<float>(lr); }
   int64_t num_problems() const { return (int64_t)probs_.size(); }
   std::vector<int64_t> splits() const {
     std::vector<int64_t> s;
-    for (const auto& p : probs_) s.push_back((p.MB + p.kps - 1) / p.kps);
+    for (const auto& p : probs_) s.push_back(p.S);
     return s;
   }
 
@@ -135,6 +160,7 @@ class TreePlan {
   c10::Device dev_{c10::kCPU};
   TrGraph graph_{};
   TrTree tree_{};
+  TrSampleArgs sample_{};
   TrFwdArgs fwd0_{}, fwd1_{};
   TrHeadArgs head_{};
   TrBwdArgs bwd1_{};
@@ -215,22 +241,28 @@ class TreePlan {
     feat_fp32_ = x.scalar_type() == torch::kFloat32;
     const int lv = L_ - 1;           // level of layer 0's target rows
     const int64_t M = M_[lv];
+    TrSampleArgs& sm = sample_;
+    sm.g = graph_;
+    sm.tr = tree_;
+    sm.M = M;
+    sm.lv = lv;
+    sm.FL = static_cast<int32_t>(F_[L_]);
+    sm.mL = static_cast<uint32_t>(masks_[L_]);
+    sm.hopL = L_;
+    sm.roots = i32("roots", B_);
+    sm.nodes = i32("nodes", M);
+    sm.leaf = i32("leaf", M * sm.FL);
     TrFwdArgs& a = fwd0_;
-    a.g = graph_;
-    a.tr = tree_;
     a.x = x.data_ptr();
     a.D = D_;
     a.M = M;
-    a.lv = lv;
-    a.FL = static_cast<int32_t>(F_[L_]);
-    a.mL = static_cast<uint32_t>(masks_[L_]);
-    a.hopL = L_;
+    a.FL = sm.FL;
     a.include_self = self_;
     a.inv_leaf = 1.f / static_cast<float>(a.FL + self_);
-    a.roots = i32("roots", B_);
-    a.nodes = has("nodes") ? i32("nodes", M) : nullptr;
-    a.leaf = has("leaf") ? i32("leaf", M * a.FL) : nullptr;
+    a.nodes = sm.nodes;
+    a.leaf = sm.leaf;
     a.step = ptr<int64_t>("step", torch::kInt64, 1);
+    a.rng = ptr<int64_t>("rng", torch::kInt64, 2);
     if (L_ == 1) {
       a.a_next = bf("A0", B_ * 2 * D_);  // the head's input rows [B][2D]
       bm0_ = 32;
@@ -248,8 +280,6 @@ class TreePlan {
     TORCH_CHECK(bm0_ <= 128, "TreePlan: slot groups above 128 rows are not supported");
     if (L_ == 3) {
       TrFwdArgs& b = fwd1_;
-      b.g = graph_;
-      b.tr = tree_;
       b.x = Tk("A1").data_ptr();
       b.D = static_cast<int32_t>(dims_[0]);
       b.M = M_[1];
@@ -264,6 +294,12 @@ class TreePlan {
       b.a_next = bf("A2", B_ * 2 * dims_[1]);
       bm1_ = (1 << b.logPg) > 32 ? (1 << b.logPg) : 32;
     }
+  }
+
+  float* owned(int64_t n) {  // plan-owned fp32 scratch
+    torch::Tensor t = torch::zeros({n}, torch::TensorOptions().dtype(torch::kFloat32).device(dev_));
+    owned_.push_back(t);
+    return t.data_ptr<float>();
   }
 
   uint32_t* i32_as_u32(const std::string& k, int64_t numel) { return reinterpret_cast<uint32_t*>(i32(k, numel)); }
@@ -307,8 +343,9 @@ class TreePlan {
     a.demb_kt = bf("demb_kt", (int64_t)B_ * E_);
     a.g_kt = bf("g_kt", B_ * H);
     a.dA = L_ > 1 ? f32("dA" + std::to_string(last), B_ * Hin2) : nullptr;
-    a.loss_acc = f32("loss_acc", 1);
-    a.counts = i32_as_u32("counts", 3);
+    const int64_t nblk = B_ / kTrHeadRows;
+    a.dbfc_part = owned(nblk * E_);
+    a.head_part = owned(nblk * 4);
     a.prof = nullptr;
     const size_t lds = eh_tr_head_lds(a.Hin2, a.H, a.E, a.C, mode);
     TORCH_CHECK(lds <= 160 * 1024 - 64, "TreePlan: head tile does not fit in LDS (", lds, " bytes)");
@@ -328,14 +365,29 @@ class TreePlan {
     }
   }
 
-  // split-K plan: ~target workgroups per problem, at least min_kps 32-row k-blocks per split
-  int kps_for(int64_t MB, int64_t tiles) const {
+  // split-K plan.  Stored-G problems: ~target workgroups of 64x64 tiles, at least min_kps
+  // 32-row k-blocks per split.  Routed problems: 64x128 tiles, S a multiple of 8 (XCD
+  // mapping) near route_target workgroups.
+  void plan_splits(TrDwProb& p, bool route) const {
+    const int64_t MB = p.MB;
+    if (route) {
+      const int64_t tiles = (p.P / 64) * ((p.Q + 127) / 128);
+      const int64_t target = has("dw_route_wg") ? geti("dw_route_wg") : 256;
+      int64_t S = (target + tiles - 1) / tiles;
+      S = (S + 7) / 8 * 8;
+      if (S > (MB + 7) / 8 * 8) S = (MB + 7) / 8 * 8;
+      p.kps = static_cast<int32_t>((MB + S - 1) / S);
+      p.S = static_cast<int32_t>(S);  // >= ceil(MB / kps); trailing splits may be empty
+      return;
+    }
+    const int64_t tiles = ((p.P + 63) / 64) * ((p.Q + 63) / 64);
     const int64_t target = has("dw_target_wg") ? geti("dw_target_wg") : 512;
     const int64_t minkps = has("dw_min_kps") ? geti("dw_min_kps") : 4;
     int64_t kps = (MB * tiles + target - 1) / target;
     if (kps < minkps) kps = minkps;
     if (kps > MB) kps = MB;
-    return static_cast<int>(kps);
+    p.kps = static_cast<int32_t>(kps);
+    p.S = static_cast<int32_t>((MB + kps - 1) / kps);
   }
 
   void add_prob(const std::string& /*name*/, int64_t P, int64_t Q, int64_t M, const uint16_t* G, const uint16_t* X,
@@ -344,9 +396,8 @@ class TreePlan {
     p.P = static_cast<int32_t>(P);
     p.Q = static_cast<int32_t>(Q);
     p.MB = static_cast<int32_t>(M / 32);
-    const int64_t tiles = ((P + 63) / 64) * ((Q + 63) / 64);
-    p.kps = kps_for(p.MB, tiles);
-    const int64_t S = (p.MB + p.kps - 1) / p.kps;
+    plan_splits(p, dA != nullptr);
+    const int64_t S = p.S;
     // split-K partials are owned by the plan (their size follows its split plan)
     torch::Tensor t = torch::empty({S * P * Q}, torch::TensorOptions().dtype(torch::kFloat32).device(dev_));
     owned_.push_back(t);
@@ -354,6 +405,7 @@ class TreePlan {
     p.G = G;
     p.X = X;
     if (dA) {
+      TORCH_CHECK(P % 64 == 0, "TreePlan: routed dW needs P % 64 == 0");
       p.route = 1;
       p.dA = dA;
       p.mask = mask;
@@ -402,20 +454,18 @@ class TreePlan {
       s.off = off[k];
       s.n = off[k + 1] - off[k];
       const bool bias = k == L_ + 1;
-      if (bias) {
-        s.part = nullptr;
-        s.S = 0;
+      if (bias) {  // the head's per-block fc-bias sums
+        s.part = head_.dbfc_part;
+        s.S = static_cast<int32_t>(B_ / kTrHeadRows);
       } else {
         const int pi = k < L_ ? k : (k == L_ ? L_ : L_ + 1);
         const TrDwProb& p = probs_[pi];
         TORCH_CHECK(s.n == (int64_t)p.P * p.Q, "TreePlan: flat segment ", k, " does not match its dW problem");
         s.part = p.part;
-        s.S = (p.MB + p.kps - 1) / p.kps;
+        s.S = p.S;
       }
     }
     a.nseg = seg;
-    // the head accumulates the fc-bias gradient atomically into its flat-gradient segment
-    head_.dbfc = a.g + off[L_ + 1];
     // bf16 shadows: conv weights (+ transposes where a backward GEMM uses them), fc, out
     int ns = 0;
     for (int k = 0; k < L_; ++k) {
@@ -450,9 +500,11 @@ class TreePlan {
     a.wd = static_cast<float>(getf("weight_decay"));
     a.grad_scale = 1.f;
     a.kind = static_cast<int32_t>(geti("opt_kind"));
+    a.head_part = head_.head_part;
+    a.nhead = static_cast<int32_t>(B_ / kTrHeadRows);
     a.loss_acc = f32("loss_acc", 1);
+    a.counts = i32_as_u32("counts", 3);
     a.loss_out = f32("loss_out", 1);
-    a.rng = ptr<int64_t>("rng", torch::kInt64, 2);
   }
 };
 
@@ -461,13 +513,16 @@ class TreePlan {
 void register_tree_ops(py::module& m) {
   py::class_<TreePlan>(m, "TreePlan")
       .def(py::init<py::dict>())
-      .def("fwd", &TreePlan::fwd)
+      .def("sample", &TreePlan::sample)
+      .def("fwd", &TreePlan::fwd, py::arg("prof") = py::none())
+      .def("fwd_blocks", [](const TreePlan& t) { return t.fwd_blocks(); })
       .def("head", &TreePlan::head, py::arg("prof") = py::none())
       .def("bwd", &TreePlan::bwd)
       .def("dw", &TreePlan::dw)
       .def("opt", &TreePlan::opt, py::arg("mode"), py::arg("grad_scale") = 1.0)
       .def("set_lr", &TreePlan::set_lr)
       .def("num_problems", &TreePlan::num_problems)
-      .def("splits", &TreePlan::splits);
+      .def("splits", &TreePlan::splits)
+      .def("problems", &TreePlan::problems, py::arg("route"));
   m.attr("tree_head_rows") = kTrHeadRows;
 }

@@ -21,17 +21,15 @@ __device__ __forceinline__ float bf2f(bf16_t v) {
   return __uint_as_float(static_cast<uint32_t>(v) << 16);
 }
 
-// round-to-nearest-even fp32 -> bf16 (NaN-preserving)
-__device__ __forceinline__ bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<bf16_t>((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return static_cast<bf16_t>(u >> 16);
+typedef float cm_float2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 cm_bf16x2_t __attribute__((ext_vector_type(2)));
+
+// round-to-nearest-even fp32 pair -> packed bf16 (one v_cvt_pk_bf16_f32 on gfx950)
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(cm_float2_t{a, b}, cm_bf16x2_t));
 }
 
-__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
-  return static_cast<uint32_t>(f2bf(a)) | (static_cast<uint32_t>(f2bf(b)) << 16);
-}
+__device__ __forceinline__ bf16_t f2bf(float f) { return static_cast<bf16_t>(pack_bf16x2(f, 0.f)); }
 
 // unpack 8 bf16 held in a 16-byte vector into fp32 and add to acc[8]
 __device__ __forceinline__ void acc_bf16x8(float* acc, uint4_t v, float scale = 1.f) {

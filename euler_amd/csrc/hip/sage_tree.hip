@@ -163,6 +163,39 @@ __device__ __forceinline__ float bf_lo(uint32_t v) { return __uint_as_float(v <<
 __device__ __forceinline__ float bf_hi(uint32_t v) { return __uint_as_float(v & 0xffff0000u); }
 
 // ----------------------------------------------------------------------------
+// tr_sample: target-row nodes (root -> hop chain) and their leaf draws, BM rows per block
+// ----------------------------------------------------------------------------
+constexpr int kTrSampleRows = 64;
+
+__global__ __launch_bounds__(256) void tr_sample_kernel(TrSampleArgs a) {
+  __shared__ int32_t node_s[kTrSampleRows];
+  const int64_t row0 = static_cast<int64_t>(blockIdx.x) * kTrSampleRows;
+  if (threadIdx.x < kTrSampleRows) {
+    const int64_t s = row0 + threadIdx.x;
+    int32_t node = -1;
+    if (s < a.M) {
+      int64_t root;
+      bool sc;
+      node = tr_slot_node(a.g, a.tr, s, a.lv, &root, &sc);
+      if (sc) a.roots[root] = node;
+      a.nodes[s] = node;
+    }
+    node_s[threadIdx.x] = node;
+  }
+  __syncthreads();
+  for (int it = threadIdx.x; it < kTrSampleRows * a.FL; it += 256) {
+    const int r = it / a.FL, k = it - r * a.FL;
+    const int64_t s = row0 + r;
+    if (s >= a.M) break;
+    const int32_t node = node_s[r];
+    a.leaf[s * a.FL + k] =
+        node >= 0 ? tr_neighbor(a.g, node, a.mL,
+                                tr_rand(a.tr.rng, kTrStreamHop + a.hopL, static_cast<uint64_t>(s * a.FL + k)))
+                  : -1;
+  }
+}
+
+// ----------------------------------------------------------------------------
 // tr_fwd: one SAGE layer over BM target rows per block (see TrFwdArgs)
 // ----------------------------------------------------------------------------
 template <typename FT, int BM, int MODE>
@@ -183,74 +216,85 @@ __global__ __launch_bounds__(256, 2) void tr_fwd_kernel(TrFwdArgs a) {
   int32_t* node_s = reinterpret_cast<int32_t*>(lds + BM * ldsw + (own_otile ? BM * (kTrBN + 8) : 0));
   int32_t* leaf_s = node_s + BM;
 
+#define TF_STAMP(k) \
+  if (a.prof && threadIdx.x == 0) a.prof[blockIdx.x * 8 + (k)] = static_cast<long long>(wall_clock64())
+  TF_STAMP(0);
   if constexpr (kGather) {
-    // ---- sampling: the target rows' nodes (root -> hop chain), then their leaf draws
-    if (a.step && blockIdx.x == 0 && threadIdx.x == 0) a.step[0] += 1;
-    if (threadIdx.x < BM) {
-      const int64_t s = row0 + threadIdx.x;
-      int32_t node = -1;
-      if (s < a.M) {
-        int64_t root;
-        bool sc;
-        node = tr_slot_node(a.g, a.tr, s, a.lv, &root, &sc);
-        if (sc) a.roots[root] = node;
-        if (a.nodes) a.nodes[s] = node;
-      }
-      node_s[threadIdx.x] = node;
+    // ---- the sampled ids of the block (sampler output, one step ahead): coalesced
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      if (a.step) a.step[0] += 1;
+      a.rng[1] += 1;  // this batch is consumed: the sampler draws the next counter
     }
+    if (threadIdx.x < BM) node_s[threadIdx.x] = row0 + threadIdx.x < a.M ? a.nodes[row0 + threadIdx.x] : -1;
+    for (int it = threadIdx.x; it < BM * a.FL; it += 256)
+      leaf_s[it] = row0 * a.FL + it < a.M * a.FL ? a.leaf[row0 * a.FL + it] : -1;
     __syncthreads();
-    for (int it = threadIdx.x; it < BM * a.FL; it += 256) {
-      const int r = it / a.FL, k = it - r * a.FL;
-      const int64_t s = row0 + r;
-      const int32_t node = node_s[r];
-      const int32_t nb = node >= 0 ? tr_neighbor(a.g, node, a.mL,
-                                                 tr_rand(a.tr.rng, kTrStreamHop + a.hopL,
-                                                         static_cast<uint64_t>(s * a.FL + k)))
-                                   : -1;
-      leaf_s[it] = nb;
-      if (a.leaf && s < a.M) a.leaf[s * a.FL + k] = nb;
-    }
-    __syncthreads();
-    // ---- gather + mean: item = (row, 8-column chunk); all leaf loads of a chunk in flight
+    TF_STAMP(1);
+    // ---- gather + mean: item = (row, 8-column chunk); two items per thread with every
+    // leaf load of both in flight
     const FT* x = static_cast<const FT*>(a.x);
     const int cpr = D >> 3;
+    const int nitems = BM * cpr;
     constexpr int G = Feat8<FT>::kInFlight;
-    for (int it = threadIdx.x; it < BM * cpr; it += 256) {
-      const int r = it / cpr;
-      const int c = it - r * cpr;
-      const int64_t grow = row0 + r;
-      const int32_t node = node_s[r];
-      Feat8<FT> sv;
-      sv.zero();
-      float acc[8];
+    for (int it = threadIdx.x; it < nitems; it += 512) {
+      const int itb = it + 256;
+      const bool hb = itb < nitems;
+      const int ra = it / cpr, ca = it - ra * cpr;
+      const int rb = hb ? itb / cpr : ra, cb = hb ? itb - rb * cpr : ca;
+      const int32_t na = node_s[ra], nb = hb ? node_s[rb] : -1;
+      Feat8<FT> sa, sb;
+      sa.zero();
+      sb.zero();
+      float acc_a[8], acc_b[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i] = 0.f;
-      if (node >= 0) sv.load(x + static_cast<int64_t>(node) * D + c * 8);
-      if (a.include_self) sv.add_to(acc);
+      for (int i = 0; i < 8; ++i) acc_a[i] = acc_b[i] = 0.f;
+      if (na >= 0) sa.load(x + static_cast<int64_t>(na) * D + ca * 8);
+      if (nb >= 0) sb.load(x + static_cast<int64_t>(nb) * D + cb * 8);
       for (int k = 0; k < a.FL; k += G) {
-        int32_t j[G];
-        Feat8<FT> v[G];
-#pragma unroll
-        for (int u = 0; u < G; ++u) j[u] = (k + u < a.FL) ? leaf_s[r * a.FL + k + u] : -1;
+        int32_t ja[G], jb[G];
+        Feat8<FT> va[G], vb[G];
 #pragma unroll
         for (int u = 0; u < G; ++u) {
-          if (j[u] >= 0) v[u].load(x + static_cast<int64_t>(j[u]) * D + c * 8);
-          else v[u].zero();
+          ja[u] = (k + u < a.FL) ? leaf_s[ra * a.FL + k + u] : -1;
+          jb[u] = (hb && k + u < a.FL) ? leaf_s[rb * a.FL + k + u] : -1;
         }
 #pragma unroll
-        for (int u = 0; u < G; ++u) v[u].add_to(acc);
+        for (int u = 0; u < G; ++u) {
+          if (ja[u] >= 0) va[u].load(x + static_cast<int64_t>(ja[u]) * D + ca * 8);
+          else va[u].zero();
+          if (jb[u] >= 0) vb[u].load(x + static_cast<int64_t>(jb[u]) * D + cb * 8);
+          else vb[u].zero();
+        }
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+          va[u].add_to(acc_a);
+          vb[u].add_to(acc_b);
+        }
+      }
+      if (a.include_self) {
+        sa.add_to(acc_a);
+        sb.add_to(acc_b);
       }
 #pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i] *= a.inv_leaf;
-      const uint4_t selfv = sv.bf16(), meanv = pack_bf16x8(acc);
-      if constexpr (MODE == 1) {
-        if (grow < a.M) {
-          *reinterpret_cast<uint4_t*>(a.a_next + grow * K2 + c * 8) = selfv;
-          *reinterpret_cast<uint4_t*>(a.a_next + grow * K2 + D + c * 8) = meanv;
+      for (int i = 0; i < 8; ++i) {
+        acc_a[i] *= a.inv_leaf;
+        acc_b[i] *= a.inv_leaf;
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (h == 1 && !hb) break;
+        const int r = h ? rb : ra, c = h ? cb : ca;
+        const uint4_t selfv = h ? sb.bf16() : sa.bf16(), meanv = pack_bf16x8(h ? acc_b : acc_a);
+        const int64_t grow = row0 + r;
+        if constexpr (MODE == 1) {
+          if (grow < a.M) {
+            *reinterpret_cast<uint4_t*>(a.a_next + grow * K2 + c * 8) = selfv;
+            *reinterpret_cast<uint4_t*>(a.a_next + grow * K2 + D + c * 8) = meanv;
+          }
+        } else {
+          *reinterpret_cast<uint4_t*>(lds + r * ldsw + c * 8) = selfv;
+          *reinterpret_cast<uint4_t*>(lds + r * ldsw + D + c * 8) = meanv;
         }
-      } else {
-        *reinterpret_cast<uint4_t*>(lds + r * ldsw + c * 8) = selfv;
-        *reinterpret_cast<uint4_t*>(lds + r * ldsw + D + c * 8) = meanv;
       }
     }
     if constexpr (MODE == 1) return;
@@ -266,6 +310,7 @@ __global__ __launch_bounds__(256, 2) void tr_fwd_kernel(TrFwdArgs a) {
     }
   }
   __syncthreads();
+  TF_STAMP(2);
 
   // ---- A tile -> kt layout (dW operand): item = (column n, 8-row chunk q)
   if (a.a_kt) {
@@ -282,6 +327,7 @@ __global__ __launch_bounds__(256, 2) void tr_fwd_kernel(TrFwdArgs a) {
     }
   }
 
+  TF_STAMP(3);
   // ---- MFMA GEMM out of LDS; wave w owns 64-column slab w of each 256-column chunk
   constexpr int FM = BM / 16;
   constexpr int FN = 4;
@@ -329,6 +375,7 @@ __global__ __launch_bounds__(256, 2) void tr_fwd_kernel(TrFwdArgs a) {
           }
     }
     __syncthreads();
+    TF_STAMP(4);
     const int ncols = (H - cchunk) < kTrBN ? (H - cchunk) : kTrBN;
     // tree-mean epilogue: A_next[parent] = [h[self slot] | mean_{j < Fg} h[j]] for every
     // sibling group of the block (item = (group, column pair), 4-byte stores)
@@ -372,6 +419,8 @@ __global__ __launch_bounds__(256, 2) void tr_fwd_kernel(TrFwdArgs a) {
     }
     __syncthreads();
   }
+  TF_STAMP(5);
+#undef TF_STAMP
 }
 
 // ----------------------------------------------------------------------------
@@ -499,6 +548,7 @@ __global__ __launch_bounds__(HNW * 64) void tr_head_kernel(TrHeadArgs a) {
   bf16_t* Dl = Db + HB * ldd;  // [HB][ldc]  dlogits
   bf16_t* Ly = Dl + HB * ldc;  // [HB][C]    dense labels (label_mode 2)
   __shared__ int lab_s[HB];
+  __shared__ float red_s[HNW][4];
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * HB;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int lr = lane & 15, lg = lane >> 4;
@@ -602,23 +652,27 @@ __global__ __launch_bounds__(HNW * 64) void tr_head_kernel(TrHeadArgs a) {
       kt_store4(a.dlog_kt, r0 + m * 16 + lg * 4, col, C, d[0], d[1], d[2], d[3]);
     }
   }
-  if (wave * 16 < C) {
+  {
     lsum = wave_sum(lsum);
     tp = wave_sum_i(tp);
     fp = wave_sum_i(fp);
     fn = wave_sum_i(fn);
     if (lane == 0) {
-      atomicAdd(a.loss_acc, lsum * a.inv_scale);
-      if (a.counts) {
-        atomicAdd(a.counts + 0, static_cast<uint32_t>(tp));
-        atomicAdd(a.counts + 1, static_cast<uint32_t>(fp));
-        atomicAdd(a.counts + 2, static_cast<uint32_t>(fn));
-      }
+      red_s[wave][0] = lsum;
+      red_s[wave][1] = static_cast<float>(tp);
+      red_s[wave][2] = static_cast<float>(fp);
+      red_s[wave][3] = static_cast<float>(fn);
     }
   }
   tr_prefetch(a.WoutT, wave * 16, E, C, lane, pre);
   __syncthreads();
   TR_STAMP(4);
+  if (threadIdx.x < 4) {  // per-block sums, plain stores (no contended atomics)
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < HNW; ++w) v += red_s[w][threadIdx.x];
+    a.head_part[blockIdx.x * 4 + threadIdx.x] = threadIdx.x == 0 ? v * a.inv_scale : v;
+  }
 
   // S4: demb = dlogits @ Wout ; dbfc = column sums
   for (int cc = wave * 16; cc < E; cc += HNW * 16) {
@@ -641,7 +695,7 @@ __global__ __launch_bounds__(HNW * 64) void tr_head_kernel(TrHeadArgs a) {
     }
     cs += __shfl_xor(cs, 16, 64);
     cs += __shfl_xor(cs, 32, 64);
-    if (lg == 0) atomicAdd(a.dbfc + col, cs);
+    if (lg == 0) a.dbfc_part[static_cast<int64_t>(blockIdx.x) * E + col] = cs;
   }
   tr_prefetch(a.WfcT, wave * 16, H, E, lane, pre);
   __syncthreads();
@@ -691,25 +745,140 @@ __global__ __launch_bounds__(HNW * 64) void tr_head_kernel(TrHeadArgs a) {
 // tr_dw: grouped split-K weight gradients, part[s][p][q] = sum_{m in split s} G[m][p] X[m][q];
 // 64x64 tiles, 4 waves of 32x32
 // ----------------------------------------------------------------------------
-// G^T fragment of a route problem: rows mb*32 + lk .. +7 (inside one sibling group) at column p
-__device__ __forceinline__ uint4_t tr_route_frag(const TrDwProb& pr, int mb, int p, int lk) {
+// raw operands of a route problem's G^T fragment (rows mb*32 + lk .. +7, column p): the
+// ReLU bits and the parent's self / neighbour gradients
+struct RouteRaw {
+  uint32_t bits;
+  float ds, dn;
+};
+
+__device__ __forceinline__ RouteRaw tr_route_load(const TrDwProb& pr, int mb, int p, int lk) {
   const int64_t m0 = static_cast<int64_t>(mb) * 32 + lk;
-  const int64_t t = m0 >> pr.logPg;
-  const int j0 = static_cast<int>(m0 & ((int64_t(1) << pr.logPg) - 1));
-  const uint32_t bits = pr.mask[static_cast<int64_t>(mb) * pr.P + p] >> lk;
-  const float* row = pr.dA + t * 2 * pr.P;
-  const float dn = row[pr.P + p] * pr.inv;
-  const float ds = row[p] + (pr.include_self ? dn : 0.f);
+  const float* row = pr.dA + (m0 >> pr.logPg) * 2 * pr.P;
+  RouteRaw r;
+  r.bits = pr.mask[static_cast<int64_t>(mb) * pr.P + p] >> lk;
+  r.ds = row[p];
+  r.dn = row[pr.P + p];
+  return r;
+}
+
+// G[m][p] for the 8 rows: neighbour slots (j < Fg) get dn / (Fg + self), the self slot
+// ds (+ the neighbour share with self loops), padding 0, all masked by the ReLU bits
+__device__ __forceinline__ uint4_t tr_route_frag(const TrDwProb& pr, const RouteRaw& r, int mb, int lk) {
+  const int j0 = static_cast<int>((static_cast<int64_t>(mb) * 32 + lk) & ((int64_t(1) << pr.logPg) - 1));
+  const float dn = r.dn * pr.inv;
+  const float ds = r.ds + (pr.include_self ? dn : 0.f);
   float v[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int j = j0 + i;
     const float val = j < pr.Fg ? dn : (j == pr.Fg ? ds : 0.f);
-    v[i] = ((bits >> i) & 1u) ? val : 0.f;
+    v[i] = ((r.bits >> i) & 1u) ? val : 0.f;
   }
   return pack_bf16x8(v);
 }
 
+// ----------------------------------------------------------------------------
+// tr_dw_route: split-K dW of a layer whose output gradient is routed from the parent
+// rows (the tree mean's backward). Workgroup tile 64 p x 128 q; per stage of kRKB
+// k-blocks every thread builds ONE G^T fragment lane (p = tid & 63, 8 rows) into LDS, so
+// each routed element is built once per q tile; wave w multiplies 32 p x 64 q of it with
+// X fragments loaded straight from the kt layout, one stage ahead.
+// ----------------------------------------------------------------------------
+constexpr int kRP = 64, kRQ = 128, kRKB = 2, kRLd = 40;
+
+struct RouteStage {
+  RouteRaw r[kRKB];
+  uint4_t x[kRKB][4];
+};
+
+__global__ __launch_bounds__(256, 2) void tr_dw_route_kernel(TrDwProb pr) {
+  __shared__ __attribute__((aligned(16))) bf16_t gs[2][kRKB][kRP * kRLd];
+  // XCD-aware: the tiles of one split (which read the same X rows) share blockIdx % 8
+  const int b = blockIdx.x;
+  const int j = b >> 3;
+  const int tile = j % pr.ntiles;
+  const int s = (j / pr.ntiles) * 8 + (b & 7);
+  const int tp = tile / pr.tiles_q, tq = tile - tp * pr.tiles_q;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int lr = lane & 15, lk = (lane >> 4) * 8;
+  const int bp = tp * kRP + (tid & 63), blk = (tid >> 6) * 8;  // builder: column p, rows blk..+7
+  const int wp = (wave >> 1) * 32;                              // MFMA: tile rows wp..+31
+  const int wq = tq * kRQ + (wave & 1) * 64;                     //       columns wq..+63
+  const int64_t Q = pr.Q;
+  const int mb0 = s * pr.kps;
+  const int mb1 = (mb0 + pr.kps) < pr.MB ? (mb0 + pr.kps) : pr.MB;
+  float4_t acc[2][4];
+  tl_zero(acc);
+  if (mb0 < mb1) {
+    auto load = [&](RouteStage& st, int mbs) {
+#pragma unroll
+      for (int u = 0; u < kRKB; ++u) {
+        const int mb = (mbs + u) < mb1 ? (mbs + u) : (mb1 - 1);  // clamped: always a valid row
+        st.r[u] = tr_route_load(pr, mb, bp, blk);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          const int q = wq + f * 16 < Q ? wq + f * 16 + lr : lr;
+          st.x[u][f] = *reinterpret_cast<const uint4_t*>(pr.X + ((static_cast<int64_t>(mb) * Q + q) * 32 + lk));
+        }
+      }
+    };
+    auto build = [&](const RouteStage& st, int buf, int mbs) {
+#pragma unroll
+      for (int u = 0; u < kRKB; ++u) {
+        const uint4_t fr = (mbs + u) < mb1 ? tr_route_frag(pr, st.r[u], mbs + u, blk) : uint4_t{0u, 0u, 0u, 0u};
+        *reinterpret_cast<uint4_t*>(&gs[buf][u][(tid & 63) * kRLd + blk]) = fr;
+      }
+    };
+    auto compute = [&](const RouteStage& st, int buf, int mbs) {
+#pragma unroll
+      for (int u = 0; u < kRKB; ++u) {
+        if (mbs + u >= mb1) break;  // uniform
+        uint4_t a[2];
+#pragma unroll
+        for (int fm = 0; fm < 2; ++fm)
+          a[fm] = *reinterpret_cast<const uint4_t*>(&gs[buf][u][(wp + fm * 16 + lr) * kRLd + lk]);
+#pragma unroll
+        for (int fn = 0; fn < 4; ++fn) {
+          if (wq + fn * 16 >= Q) break;  // uniform
+#pragma unroll
+          for (int fm = 0; fm < 2; ++fm) acc[fm][fn] = mfma16(a[fm], st.x[u][fn], acc[fm][fn]);
+        }
+      }
+    };
+    RouteStage A, B;
+    load(A, mb0);
+    for (int mbs = mb0; mbs < mb1; mbs += 2 * kRKB) {
+      build(A, 0, mbs);
+      load(B, mbs + kRKB);
+      __syncthreads();
+      compute(A, 0, mbs);
+      if (mbs + kRKB < mb1) {
+        build(B, 1, mbs + kRKB);
+        load(A, mbs + 2 * kRKB);
+        __syncthreads();
+        compute(B, 1, mbs + kRKB);
+      }
+    }
+  }
+  float* out = pr.part + static_cast<int64_t>(s) * pr.P * Q;
+  const int p0 = tp * kRP + wp;
+#pragma unroll
+  for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+    for (int fn = 0; fn < 4; ++fn) {
+      if (wq + fn * 16 >= Q) break;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+        out[(p0 + fm * 16 + (lane >> 4) * 4 + jj) * Q + wq + fn * 16 + lr] = acc[fm][fn][jj];
+    }
+}
+
+// ----------------------------------------------------------------------------
+// tr_dw: grouped split-K dW of the problems with stored G operands (kt layout),
+// part[s][p][q] = sum_{m in split s} G[m][p] X[m][q]; 64x64 tiles, 4 waves of 32x32,
+// k-block groups double-buffered in registers (unrolled ping-pong: no register copies)
+// ----------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void tr_dw_kernel(TrDwProbs probs) {
   const int id = xcd_remap(blockIdx.x, gridDim.x);
   // constant indices only (no dynamic indexing of kernel arguments)
@@ -731,48 +900,40 @@ __global__ __launch_bounds__(256) void tr_dw_kernel(TrDwProbs probs) {
   if (p0 >= P || q0 >= Q) return;  // 32-wide edge of a 64-wide tile; no barriers in this kernel
   float4_t acc[2][2];
   tl_zero(acc);
-  if (pr.route) {
-    constexpr int KR = 4;
-    for (int mbc = mb0; mbc < mb1; mbc += KR) {
-      uint4_t av[KR][2], bv[KR][2];
+  constexpr int KB = 4;
+  struct Grp {
+    uint4_t a[KB][2], b[KB][2];
+  };
+  auto load = [&](Grp& g, int mbs) {
 #pragma unroll
-      for (int u = 0; u < KR; ++u)
+    for (int u = 0; u < KB; ++u) {
+      const int64_t mb = (mbs + u) < mb1 ? (mbs + u) : (mb1 - 1);
 #pragma unroll
-        for (int f = 0; f < 2; ++f) {
-          const int mb = mbc + u;
-          const bool ok = mb < mb1;
-          bv[u][f] = ok ? *reinterpret_cast<const uint4_t*>(pr.X + ((static_cast<int64_t>(mb) * Q + q0 + f * 16 + lr) * 32 + lk))
-                        : uint4_t{0u, 0u, 0u, 0u};
-          av[u][f] = ok ? tr_route_frag(pr, mb, p0 + f * 16 + lr, lk) : uint4_t{0u, 0u, 0u, 0u};
-        }
-#pragma unroll
-      for (int u = 0; u < KR; ++u)
-#pragma unroll
-        for (int fm = 0; fm < 2; ++fm)
-#pragma unroll
-          for (int fn = 0; fn < 2; ++fn) acc[fm][fn] = mfma16(av[u][fm], bv[u][fn], acc[fm][fn]);
+      for (int f = 0; f < 2; ++f) {
+        g.a[u][f] = *reinterpret_cast<const uint4_t*>(pr.G + ((mb * P + p0 + f * 16 + lr) * 32 + lk));
+        g.b[u][f] = *reinterpret_cast<const uint4_t*>(pr.X + ((mb * Q + q0 + f * 16 + lr) * 32 + lk));
+      }
     }
-  } else {
-    constexpr int KB = 8;  // k-blocks of fragments in flight per wave
-    for (int mbc = mb0; mbc < mb1; mbc += KB) {
-      uint4_t av[KB][2], bv[KB][2];
+  };
+  auto compute = [&](const Grp& g, int mbs) {
 #pragma unroll
-      for (int u = 0; u < KB; ++u)
+    for (int u = 0; u < KB; ++u) {
+      if (mbs + u >= mb1) break;  // uniform
 #pragma unroll
-        for (int f = 0; f < 2; ++f) {
-          const int64_t mb = mbc + u;
-          const bool ok = mb < mb1;
-          av[u][f] = ok ? *reinterpret_cast<const uint4_t*>(pr.G + ((mb * P + p0 + f * 16 + lr) * 32 + lk))
-                        : uint4_t{0u, 0u, 0u, 0u};
-          bv[u][f] = ok ? *reinterpret_cast<const uint4_t*>(pr.X + ((mb * Q + q0 + f * 16 + lr) * 32 + lk))
-                        : uint4_t{0u, 0u, 0u, 0u};
-        }
+      for (int fm = 0; fm < 2; ++fm)
 #pragma unroll
-      for (int u = 0; u < KB; ++u)
-#pragma unroll
-        for (int fm = 0; fm < 2; ++fm)
-#pragma unroll
-          for (int fn = 0; fn < 2; ++fn) acc[fm][fn] = mfma16(av[u][fm], bv[u][fn], acc[fm][fn]);
+        for (int fn = 0; fn < 2; ++fn) acc[fm][fn] = mfma16(g.a[u][fm], g.b[u][fn], acc[fm][fn]);
+    }
+  };
+  if (mb0 < mb1) {
+    Grp A, B;
+    load(A, mb0);
+    for (int mbs = mb0; mbs < mb1; mbs += 2 * KB) {
+      load(B, mbs + KB);
+      compute(A, mbs);
+      if (mbs + KB >= mb1) break;
+      load(A, mbs + 2 * KB);
+      compute(B, mbs + KB);
     }
   }
   float* out = pr.part + static_cast<int64_t>(s) * P * Q;
@@ -808,65 +969,76 @@ __device__ __forceinline__ void tr_shadow_write(const TrOptArgs& a, int64_t i, f
 template <int MODE>
 __global__ __launch_bounds__(256) void tr_opt_kernel(TrOptArgs a) {
   const int64_t i4 = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (MODE != 0 && i4 == 0) {
-    a.loss_out[0] = a.loss_acc[0];
-    a.loss_acc[0] = 0.f;
-    a.rng[1] += 1;
+  if (blockIdx.x == 0 && threadIdx.x < 64) {
+    // head statistics: reduce (modes 0/2) the per-block partials; hand the loss over (1/2)
+    const int lane = threadIdx.x;
+    if (MODE != 1) {
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int b = lane; b < a.nhead; b += 64)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] += a.head_part[b * 4 + k];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = wave_sum(v[k]);
+      if (lane == 0) {
+        a.loss_acc[0] = v[0];
+        if (a.counts) {
+          a.counts[0] += static_cast<uint32_t>(v[1]);
+          a.counts[1] += static_cast<uint32_t>(v[2]);
+          a.counts[2] += static_cast<uint32_t>(v[3]);
+        }
+        if (MODE == 2) a.loss_out[0] = v[0];
+      }
+    } else if (lane == 0) {
+      a.loss_out[0] = a.loss_acc[0];
+    }
   }
-  const int64_t i = i4 * 4;
+  // one parameter per thread: the split-K slabs of a segment are read with 8 loads in
+  // flight per thread, 256 B per wave instruction
+  const int64_t i = i4;
   if (i >= a.n) return;
   TrSeg sg = a.seg[0];
 #pragma unroll
   for (int s = 1; s < kTrMaxSegs; ++s)
     if (s < a.nseg && i >= a.seg[s].off) sg = a.seg[s];
-  float4_t g;
-  if (MODE != 1 && sg.part) {
-    const float4_t* src = reinterpret_cast<const float4_t*>(sg.part + (i - sg.off));
-    const int64_t stride = sg.n >> 2;
-    g = float4_t{0.f, 0.f, 0.f, 0.f};
+  float g;
+  if (MODE != 1) {
+    const float* src = sg.part + (i - sg.off);
+    g = 0.f;
     for (int s0 = 0; s0 < sg.S; s0 += 8) {
-      float4_t v[8];
+      float v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = (s0 + u < sg.S) ? src[(s0 + u) * stride] : float4_t{0.f, 0.f, 0.f, 0.f};
+      for (int u = 0; u < 8; ++u) v[u] = (s0 + u < sg.S) ? src[(s0 + u) * sg.n] : 0.f;
 #pragma unroll
       for (int u = 0; u < 8; ++u) g += v[u];
     }
     if (MODE == 0) {
-      *reinterpret_cast<float4_t*>(a.g + i) = g;
+      a.g[i] = g;
       return;
     }
   } else {
-    if (MODE == 0) return;
-    g = *reinterpret_cast<const float4_t*>(a.g + i);
+    g = a.g[i];
   }
-  if (!sg.part) *reinterpret_cast<float4_t*>(a.g + i) = float4_t{0.f, 0.f, 0.f, 0.f};  // atomics restart at 0
-  float4_t p = *reinterpret_cast<const float4_t*>(a.p + i);
-  float4_t m = *reinterpret_cast<const float4_t*>(a.m + i);
-  float4_t v = *reinterpret_cast<const float4_t*>(a.v + i);
+  float p = a.p[i], m = a.m[i], v = a.v[i];
   const float t = static_cast<float>(a.step[0]);
-  const float bc1 = 1.f - __powf(a.b1, t), bc2 = 1.f - __powf(a.b2, t);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float gi = g[k] * a.grad_scale + a.wd * p[k];
-    if (a.kind == 0) {
-      m[k] = a.b1 * m[k] + (1.f - a.b1) * gi;
-      v[k] = a.b2 * v[k] + (1.f - a.b2) * gi * gi;
-      p[k] -= a.lr * (m[k] / bc1) / (sqrtf(v[k] / bc2) + a.eps);
-    } else if (a.kind == 1) {
-      v[k] += gi * gi;
-      p[k] -= a.lr * gi / (sqrtf(v[k]) + a.eps);
-    } else if (a.kind == 2) {
-      p[k] -= a.lr * gi;
-    } else {
-      m[k] = a.b1 * m[k] + gi;
-      p[k] -= a.lr * m[k];
-    }
+  const float gi = g * a.grad_scale + a.wd * p;
+  if (a.kind == 0) {
+    const float bc1 = 1.f - __powf(a.b1, t), bc2 = 1.f - __powf(a.b2, t);
+    m = a.b1 * m + (1.f - a.b1) * gi;
+    v = a.b2 * v + (1.f - a.b2) * gi * gi;
+    p -= a.lr * (m / bc1) / (sqrtf(v / bc2) + a.eps);
+  } else if (a.kind == 1) {
+    v += gi * gi;
+    p -= a.lr * gi / (sqrtf(v) + a.eps);
+  } else if (a.kind == 2) {
+    p -= a.lr * gi;
+  } else {
+    m = a.b1 * m + gi;
+    p -= a.lr * m;
   }
-  *reinterpret_cast<float4_t*>(a.p + i) = p;
-  *reinterpret_cast<float4_t*>(a.m + i) = m;
-  *reinterpret_cast<float4_t*>(a.v + i) = v;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) tr_shadow_write(a, i + k, p[k]);
+  a.p[i] = p;
+  a.m[i] = m;
+  a.v[i] = v;
+  tr_shadow_write(a, i, p);
 }
 
 // shadows only (initialisation / after an external parameter write)
@@ -891,13 +1063,21 @@ size_t eh_tr_fwd_lds(int D, int H, int bm, int FL, int mode) {
   return b;
 }
 
+hipError_t eh_tr_sample(const TrSampleArgs* a, hipStream_t s) {
+  if (a->M <= 0) return hipSuccess;
+  if (!a->g.indptr || !a->g.nbr || !a->g.cumw || !a->g.prob || !a->g.alias || !a->tr.rng || !a->roots ||
+      !a->nodes || !a->leaf || a->FL < 1 || a->lv < 0 || a->lv > 2)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(tr_sample_kernel, dim3(static_cast<uint32_t>(ceil_div(a->M, kTrSampleRows))), dim3(256), 0, s,
+                     *a);
+  return hipGetLastError();
+}
+
 hipError_t eh_tr_fwd(const TrFwdArgs* a, int mode, int feat_fp32, int bm, hipStream_t s) {
   if (a->M <= 0) return hipSuccess;
   // every pointer the chosen mode dereferences must be set
   if (!a->x || !a->a_next) return hipErrorInvalidValue;
-  if (mode != 2 && (!a->g.indptr || !a->g.nbr || !a->g.cumw || !a->g.prob || !a->g.alias || !a->tr.rng ||
-                    !a->roots || a->FL < 1))
-    return hipErrorInvalidValue;
+  if (mode != 2 && (!a->nodes || !a->leaf || !a->rng || a->FL < 1)) return hipErrorInvalidValue;
   if (mode != 1 && !a->W) return hipErrorInvalidValue;
   if (a->D % 16 != 0 || a->D <= 0 || a->M % bm != 0) return hipErrorInvalidValue;
   if (mode != 1 && (a->H % 64 != 0 || a->H <= 0 || (bm >> a->logPg) < 1 || (bm & ((1 << a->logPg) - 1)) != 0 ||
@@ -943,7 +1123,7 @@ size_t eh_tr_head_lds(int Hin2, int H, int E, int C, int label_mode) {
 
 hipError_t eh_tr_head(const TrHeadArgs* a, int64_t B, hipStream_t s) {
   if (!a->A || !a->W || !a->Wfc || !a->WfcT || !a->Wout || !a->WoutT || !a->bfc || !a->roots || !a->labels ||
-      !a->A_kt || !a->h_kt || !a->emb_kt || !a->dlog_kt || !a->demb_kt || !a->g_kt || !a->dbfc || !a->loss_acc ||
+      !a->A_kt || !a->h_kt || !a->emb_kt || !a->dlog_kt || !a->demb_kt || !a->g_kt || !a->dbfc_part || !a->head_part ||
       (a->dA && !a->WT))
     return hipErrorInvalidValue;
   if (B % 32 != 0 || a->H % 16 != 0 || a->E % 32 != 0 || a->C % 32 != 0 || a->Hin2 % 32 != 0 ||
@@ -974,10 +1154,8 @@ hipError_t eh_tr_dw(TrDwProbs* pr, hipStream_t s) {
   for (int i = 0; i < pr->n; ++i) {
     TrDwProb& p = pr->p[i];
     if (p.P % 32 != 0 || p.Q % 32 != 0 || p.MB < 1 || p.kps < 1) return hipErrorInvalidValue;
-    if (p.route && (p.logPg < 3 || !p.dA || !p.mask)) return hipErrorInvalidValue;
-    if (!p.route && !p.G) return hipErrorInvalidValue;
-    if (!p.X || !p.part) return hipErrorInvalidValue;
-    p.S = static_cast<int>(ceil_div(p.MB, p.kps));
+    if (p.route || !p.G || !p.X || !p.part) return hipErrorInvalidValue;
+    if (static_cast<int64_t>(p.S) * p.kps < p.MB) return hipErrorInvalidValue;
     p.tiles_q = (p.Q + 63) / 64;
     p.ntiles = ((p.P + 63) / 64) * p.tiles_q;
     p.wg0 = wg;
@@ -987,19 +1165,33 @@ hipError_t eh_tr_dw(TrDwProbs* pr, hipStream_t s) {
   return hipGetLastError();
 }
 
+hipError_t eh_tr_dw_route(TrDwProb* p, hipStream_t s) {
+  if (!p->route || !p->dA || !p->mask || !p->X || !p->part) return hipErrorInvalidValue;
+  if (p->P % kRP != 0 || p->Q % 32 != 0 || p->MB < 1 || p->kps < 1 || p->logPg < 3) return hipErrorInvalidValue;
+  // the XCD-aware block mapping needs S % 8 == 0 (splits past MB write zero slabs)
+  if (p->S % 8 != 0 || static_cast<int64_t>(p->S) * p->kps < p->MB) return hipErrorInvalidValue;
+  p->tiles_q = static_cast<int>(ceil_div(p->Q, kRQ));
+  p->ntiles = (p->P / kRP) * p->tiles_q;
+  p->wg0 = 0;
+  hipLaunchKernelGGL(tr_dw_route_kernel, dim3(static_cast<uint32_t>(p->ntiles * p->S)), dim3(256), 0, s, *p);
+  return hipGetLastError();
+}
+
 hipError_t eh_tr_opt(const TrOptArgs* a, int mode, hipStream_t s) {
   if (a->n % 4 != 0 || a->nseg < 1 || a->nseg > kTrMaxSegs || a->nsh > kTrMaxShadows) return hipErrorInvalidValue;
-  if (!a->p || !a->g || !a->m || !a->v || !a->step || !a->loss_acc || !a->loss_out || !a->rng)
+  if (!a->p || !a->g || !a->m || !a->v || !a->step || !a->loss_acc || !a->loss_out || !a->head_part ||
+      a->nhead < 1)
     return hipErrorInvalidValue;
   for (int i = 0; i < a->nsh; ++i)
     if (!a->sh[i].sh || a->sh[i].cols <= 0) return hipErrorInvalidValue;
   for (int i = 0; i < a->nseg; ++i)
-    if (a->seg[i].off % 4 != 0 || a->seg[i].n % 4 != 0) return hipErrorInvalidValue;
+    if (a->seg[i].off % 4 != 0 || a->seg[i].n % 4 != 0 || !a->seg[i].part || a->seg[i].S < 1)
+      return hipErrorInvalidValue;
   if (mode == 3) {
     hipLaunchKernelGGL(tr_shadow_kernel, dim3(static_cast<uint32_t>(ceil_div(a->n, 256))), dim3(256), 0, s, *a);
     return hipGetLastError();
   }
-  const dim3 grid(static_cast<uint32_t>(ceil_div(a->n / 4, 256)));
+  const dim3 grid(static_cast<uint32_t>(ceil_div(a->n, 256)));
   if (mode == 0) hipLaunchKernelGGL(tr_opt_kernel<0>, grid, dim3(256), 0, s, *a);
   else if (mode == 1) hipLaunchKernelGGL(tr_opt_kernel<1>, grid, dim3(256), 0, s, *a);
   else if (mode == 2) hipLaunchKernelGGL(tr_opt_kernel<2>, grid, dim3(256), 0, s, *a);

@@ -39,21 +39,34 @@ struct TrTree {
   uint32_t m1, m2;     // edge-type masks of hops 1 and 2
 };
 
-// one fused SAGE layer: mode 0 = sample + gather + GEMM + tree-mean epilogue (layer 0),
-// mode 1 = sample + gather only, writing [x_self | mean x_nbr] rows (1-hop models),
-// mode 2 = rows + GEMM + tree-mean epilogue (inner layers of 3-hop models)
-struct TrFwdArgs {
+// mini-batch sampler: the node of every target row of layer 0 (level lv of the tree,
+// root -> hop chain) and its FL leaf draws; run one step ahead of the forward on a
+// forked stream (sampling depends on nothing the step computes)
+struct TrSampleArgs {
   TrGraph g;
   TrTree tr;
-  const void* x;         // modes 0/1: feature table [N][D] (bf16 or fp32); mode 2: A rows bf16 [M][2D]
-  int32_t D;             // input width (padded, % 16 == 0)
-  int64_t M;             // target rows
-  int32_t lv;            // level of the target rows (modes 0/1)
+  int64_t M;             // target rows (slots of level lv)
+  int32_t lv;            // level of the target rows
   int32_t FL;            // leaf fanout (hop lv + 1)
   uint32_t mL;           // leaf edge-type mask
   int32_t hopL;          // leaf hop number (Philox stream)
+  int32_t* roots;        // [B] sampled roots (written by the root's self-chain row)
+  int32_t* nodes;        // [M] node of every target row
+  int32_t* leaf;         // [M][FL] leaf samples
+};
+
+// one fused SAGE layer: mode 0 = gather (sampled ids) + GEMM + tree-mean epilogue (layer 0),
+// mode 1 = gather only, writing [x_self | mean x_nbr] rows (1-hop models),
+// mode 2 = rows + GEMM + tree-mean epilogue (inner layers of 3-hop models)
+struct TrFwdArgs {
+  const void* x;         // modes 0/1: feature table [N][D] (bf16 or fp32); mode 2: A rows bf16 [M][2D]
+  int32_t D;             // input width (padded, % 16 == 0)
+  int64_t M;             // target rows
+  int32_t FL;            // leaf fanout (hop lv + 1)
   int32_t include_self;
   float inv_leaf;        // 1 / (FL + include_self)
+  const int32_t* nodes;  // modes 0/1: [M] node of every target row (sampler output)
+  const int32_t* leaf;   // modes 0/1: [M][FL] leaf samples
   const uint16_t* W;     // fm bf16 [H][2D]
   int32_t H;             // output width (% 64 == 0)
   uint16_t* a_kt;        // [M/32][2D][32] A operand of dW (optional)
@@ -61,10 +74,9 @@ struct TrFwdArgs {
   uint16_t* a_next;      // modes 0/2: [M >> logPg][2H] parent A rows; mode 1: [M][2D]
   int32_t logPg, Fg;     // sibling groups of the target rows: size 2^logPg, Fg neighbour slots
   float inv_grp;         // 1 / (Fg + include_self)
-  int32_t* roots;        // [B] sampled roots (written by the root's self-chain row)
-  int32_t* nodes;        // [M] node of every target row (optional)
-  int32_t* leaf;         // [M][FL] leaf samples (optional)
   int64_t* step;         // optimizer step counter (block 0 increments it)
+  int64_t* rng;          // (seed, counter): block 0 advances the counter (the batch is consumed)
+  long long* prof;       // optional per-block phase stamps [grid][8]
 };
 
 // head: last SAGE conv + fc + out_fc + sigmoid-CE + backward down to dA, kTrHeadRows roots / block
@@ -79,9 +91,8 @@ struct TrHeadArgs {
   float inv_scale;       // 1 / (B * C_real)
   uint16_t *A_kt, *h_kt, *emb_kt, *dlog_kt, *demb_kt, *g_kt;
   float* dA;             // [B][Hin2] fp32 (nullptr: no lower layer)
-  float* dbfc;           // [E] (atomically accumulated)
-  float* loss_acc;
-  uint32_t* counts;      // tp, fp, fn (threshold 0.5), accumulated
+  float* dbfc_part;      // [B/kTrHeadRows][E] per-block fc-bias gradient (reduced by tr_opt)
+  float* head_part;      // [B/kTrHeadRows][4] per-block loss, tp, fp, fn (reduced by tr_opt)
   long long* prof;       // optional per-block phase stamps [B/16][8]
 };
 
@@ -113,8 +124,8 @@ struct TrDwProbs {
   int32_t n;
 };
 
-// flat parameter buffer segments: part != nullptr -> gradient = sum of S split-K partials;
-// else it is accumulated in g (atomically, e.g. the fc bias) and zeroed after use
+// flat parameter buffer segments: gradient = sum of S partials [S][n] (split-K slabs of a
+// dW problem, or the head's per-block fc-bias sums)
 struct TrSeg {
   int64_t off, n;
   const float* part;
@@ -136,20 +147,24 @@ struct TrOptArgs {
   const int64_t* step;
   float lr, b1, b2, eps, wd, grad_scale;
   int32_t kind;  // 0 adam, 1 adagrad, 2 sgd, 3 momentum
-  float* loss_acc;
-  float* loss_out;
-  int64_t* rng;
+  const float* head_part;  // [nhead][4] per-block loss / tp / fp / fn of the head
+  int32_t nhead;
+  float* loss_acc;         // loss of the last forward (written by the reduce)
+  uint32_t* counts;        // tp, fp, fn since the last reset (accumulated by the reduce)
+  float* loss_out;         // loss of the last optimizer step
 };
 
 }  // namespace euler_hip
 
 extern "C" {
 // feat_fp32: feature table dtype (modes 0/1); bm: rows per block (32, 64 or 128)
+hipError_t eh_tr_sample(const euler_hip::TrSampleArgs* a, hipStream_t s);
 hipError_t eh_tr_fwd(const euler_hip::TrFwdArgs* a, int mode, int feat_fp32, int bm, hipStream_t s);
 hipError_t eh_tr_head(const euler_hip::TrHeadArgs* a, int64_t B, hipStream_t s);
 hipError_t eh_tr_bwd(const euler_hip::TrBwdArgs* a, hipStream_t s);
 // fills S / tiles / wg0 of every problem from P, Q, MB, kps before launching
-hipError_t eh_tr_dw(euler_hip::TrDwProbs* p, hipStream_t s);
+hipError_t eh_tr_dw(euler_hip::TrDwProbs* p, hipStream_t s);        // stored-G problems, one launch
+hipError_t eh_tr_dw_route(euler_hip::TrDwProb* p, hipStream_t s);   // one routed problem (S % 8 == 0)
 // mode 0: split-K reduce into g; 1: optimizer from g; 2: both fused (single process)
 hipError_t eh_tr_opt(const euler_hip::TrOptArgs* a, int mode, hipStream_t s);
 size_t eh_tr_fwd_lds(int D, int H, int bm, int FL, int mode);

@@ -131,7 +131,7 @@ class SageTrainer:
         self._shapes = self._logical_shapes()
         logical = self._init_logical(init, init_seed)
         self._build_flat()
-        self.keep_samples = keep_samples
+        self.keep_samples = keep_samples  # accepted for compatibility: the sample buffers always exist
         self.step_count = 0  # host mirror (the device counter is authoritative on the GPU)
         if self.on_gpu:
             self._alloc_gpu()
@@ -306,10 +306,10 @@ class SageTrainer:
         FL = self.fanouts[-1]
         self.roots = torch.zeros(B, **i32)
         d["roots"] = self.roots
-        if self.keep_samples:
-            self.nodes = torch.zeros(M_last, **i32)
-            self.leaf = torch.zeros(M_last * FL, **i32)
-            d["nodes"], d["leaf"] = self.nodes, self.leaf
+        # the sampler's output (the batch of the next forward)
+        self.nodes = torch.zeros(M_last, **i32)
+        self.leaf = torch.zeros(M_last * FL, **i32)
+        d["nodes"], d["leaf"] = self.nodes, self.leaf
         # layer inputs: A rows (row-major) feed the next layer / head, A_kt the dW GEMMs
         hin = [self.Dp] + self.Hp[:-1]
         for k in range(L):
@@ -335,6 +335,10 @@ class SageTrainer:
         d["bfc"] = views[L + 1]
         self._buf = d
         self.plan = hip().TreePlan(d)
+        self._side = torch.cuda.Stream(device=dev)
+        self._dw_route = list(self.plan.problems(True))
+        self._dw_plain = list(self.plan.problems(False))
+        self._primed = False  # the sample buffers hold the batch of counter graph.rng[1]
 
     # ------------------------------------------------------------------ parameters / state
     def load_logical(self, logical):
@@ -384,6 +388,7 @@ class SageTrainer:
     def load_trainer_state(self, st):
         self.graph.rng.copy_(torch.as_tensor(st["rng"]).to(self.graph.rng))
         self.step_count = int(st["step"])
+        self._primed = False
         if self.on_gpu:
             self._pack({k: torch.as_tensor(t) for k, t in st["m"].items()}, self.m)
             self._pack({k: torch.as_tensor(t) for k, t in st["v"].items()}, self.v)
@@ -394,12 +399,20 @@ class SageTrainer:
                 self._cpu_v[k].copy_(torch.as_tensor(st["v"][k]))
 
     # ------------------------------------------------------------------ training step
+    def _prime(self):
+        if not self._primed:
+            self.plan.sample()
+            self._primed = True
+
     def forward_backward(self):
         """Sampling, forward and backward of one step; the split-K partials are reduced
-        into :attr:`grad` (the all-reduce point of data parallelism)."""
+        into :attr:`grad` (the all-reduce point of data parallelism).  The sample buffers
+        keep this step's batch (:meth:`samples`); the next call samples again."""
         p = self.plan
+        self._prime()
         p.fwd()
         p.head()
+        self._primed = False
         p.bwd()
         p.dw(list(range(p.num_problems())))
         p.opt(0)
@@ -410,21 +423,45 @@ class SageTrainer:
     def step(self, grad_sync=None):
         """One training step.  ``grad_sync(grad)`` (e.g. an RCCL all-reduce) runs between
         the gradient reduce and the optimizer; None = single process (fused reduce +
-        optimizer launch)."""
+        optimizer launch).
+
+        The next step's batch is sampled on a forked stream as soon as the head has read
+        this step's roots, concurrently with the backward (sampling reads only the graph
+        and the RNG counter the forward advanced), so the sampling latency chain is off
+        the critical path."""
         self.step_count += 1
         if not self.on_gpu:
             return self._cpu_step()
+        p = self.plan
+        self._prime()
+        cur = torch.cuda.current_stream(self.device)
+        p.fwd()
+        p.head()
+        # fork: the next batch's sampling and the stored-operand dW GEMMs (fc, out, last
+        # conv) beside the routed dW of the lower layers on the main stream
+        self._side.wait_stream(cur)
+        with torch.cuda.stream(self._side):
+            p.sample()
+            p.dw(self._dw_plain)
+        p.bwd()
+        p.dw(self._dw_route)
+        cur.wait_stream(self._side)
         if grad_sync is None:
-            p = self.plan
-            p.fwd()
-            p.head()
-            p.bwd()
-            p.dw(list(range(p.num_problems())))
             p.opt(2)
         else:
-            self.forward_backward()
+            p.opt(0)
             scale = grad_sync(self.grad)
             self.optimizer_step(1.0 if scale is None else scale)
+
+    def plan_launches(self):
+        """(name, callable) of every launch of one pipelined step, for per-kernel timing"""
+        p = self.plan
+        out = [("sample", p.sample), ("fwd", p.fwd), ("head", p.head)]
+        if self.L == 3:
+            out.append(("bwd", p.bwd))
+        out += [("dw_route", lambda: p.dw(self._dw_route)), ("dw_plain", lambda: p.dw(self._dw_plain)),
+                ("opt", lambda: p.opt(2))]
+        return out
 
     def capture(self, grad_sync=None, warmup: int = 2):
         """Record one step into a hipGraph (after ``warmup`` eager steps on a side
@@ -478,8 +515,9 @@ class SageTrainer:
         """(roots [B], nodes of the outer layer's target slots [M], leaf draws [M, F_L]) of
         the last step, as int64"""
         if self.on_gpu:
-            if not self.keep_samples:
-                raise RuntimeError("keep_samples=False")
+            if self._primed:
+                raise RuntimeError("samples() describes the batch of the last forward_backward(); step() has "
+                                   "already drawn the next batch into the sample buffers")
             return (self.roots.long(), self.nodes.long(), self.leaf.view(-1, self.fanouts[-1]).long())
         return self._cpu_samples
 

@@ -37,6 +37,10 @@ for st in "${S[@]}"; do
       EULER_AMD_TREE_SYNC=1 run tree_debug 300 python -u tools/tree_debug.py 0 1 2 3 4 5 6 7 8 9 || exit 71 ;;
     tests)
       run pytest_gpu 900 python -u -m pytest $TESTS -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -rf ;;
+    kernels)
+      run tree_kernels 300 python -u tools/tree_kernels.py ;;
+    kernels_full)
+      run tree_kernels_full 300 python -u tools/tree_kernels.py --num-nodes 100000000 ;;
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench_small)
