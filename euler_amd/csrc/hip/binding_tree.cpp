@@ -94,9 +94,14 @@ class TreePlan {
     if (L_ == 3) ok(eh_tr_fwd(&fwd1_, 2, 0, bm1_, stream()), "tr_fwd(inner)");
   }
 
-  void head(c10::optional<torch::Tensor> prof) {
+  // with_sample: extra blocks of the launch draw the next step's batch
+  void head(c10::optional<torch::Tensor> prof, bool with_sample) {
     const c10::DeviceGuard g(dev_);
     TrHeadArgs a = head_;
+    if (with_sample) {
+      a.smp = sample_;
+      a.nsample = static_cast<int32_t>((sample_.M + kTrHeadSampleRows - 1) / kTrHeadSampleRows);
+    }
     if (prof.has_value()) {
       need(*prof, torch::kInt64, (B_ / kTrHeadRows) * 8, "prof");
       a.prof = reinterpret_cast<long long*>(prof->data_ptr<int64_t>());
@@ -110,22 +115,22 @@ class TreePlan {
     ok(eh_tr_bwd(&bwd1_, stream()), "tr_bwd");
   }
 
-  // dW of the given problems: routed problems one launch each, the others grouped
+  // dW of the given problems, one launch: routed problems first, the others grouped
   void dw(std::vector<int64_t> which) {
     const c10::DeviceGuard g(dev_);
-    TrDwProbs p{};
+    TrDwLaunch L{};
     for (int64_t i : which) {
       TORCH_CHECK(i >= 0 && i < (int64_t)probs_.size(), "dw: problem index out of range");
       if (probs_[i].route) {
-        TrDwProb r = probs_[i];
-        ok(eh_tr_dw_route(&r, stream()), "tr_dw_route");
+        TORCH_CHECK(L.nroute < 2, "dw: at most two routed problems per launch");
+        L.route[L.nroute++] = probs_[i];
       } else {
-        TORCH_CHECK(p.n < kTrMaxProbs, "dw: too many problems");
-        p.p[p.n++] = probs_[i];
+        TORCH_CHECK(L.plain.n < kTrMaxProbs, "dw: too many problems");
+        L.plain.p[L.plain.n++] = probs_[i];
       }
     }
-    if (p.n == 0) return;
-    ok(eh_tr_dw(&p, stream()), "tr_dw");
+    if (L.nroute == 0 && L.plain.n == 0) return;
+    ok(eh_tr_dw(&L, stream()), "tr_dw");
   }
 
   std::vector<int64_t> problems(bool route) const {
@@ -136,10 +141,12 @@ class TreePlan {
   }
 
   // mode 0 reduce, 1 optimizer, 2 fused, 3 shadows only
-  void opt(int64_t mode, double grad_scale) {
+  // with_sample: modes 1/2 also draw the next step's batch (extra blocks of the launch)
+  void opt(int64_t mode, double grad_scale, bool with_sample) {
     const c10::DeviceGuard g(dev_);
     TrOptArgs a = opt_;
     a.grad_scale = static_cast<float>(grad_scale);
+    if (!with_sample) a.nsample = 0;
     ok(eh_tr_opt(&a, static_cast<int>(mode), stream()), "tr_opt");
   }
 
@@ -166,6 +173,7 @@ class TreePlan {
   TrBwdArgs bwd1_{};
   std::vector<TrDwProb> probs_;
   std::vector<torch::Tensor> owned_;
+  torch::Tensor roots_cur_;  // the forward's copy of the batch's roots (read by the head)
   TrOptArgs opt_{};
 
   bool has(const char* k) const { return d_.contains(k) && !d_[k].is_none(); }
@@ -261,6 +269,10 @@ class TreePlan {
     a.inv_leaf = 1.f / static_cast<float>(a.FL + self_);
     a.nodes = sm.nodes;
     a.leaf = sm.leaf;
+    a.roots_in = sm.roots;
+    roots_cur_ = torch::zeros({B_}, torch::TensorOptions().dtype(torch::kInt32).device(dev_));
+    a.roots_cur = roots_cur_.data_ptr<int32_t>();
+    a.B = B_;
     a.step = ptr<int64_t>("step", torch::kInt64, 1);
     a.rng = ptr<int64_t>("rng", torch::kInt64, 2);
     if (L_ == 1) {
@@ -277,7 +289,9 @@ class TreePlan {
     a.inv_grp = 1.f / static_cast<float>(a.Fg + self_);
     a.a_next = bf("A1", M_[lv - 1] * 2 * dims_[0]);
     bm0_ = (1 << a.logPg) > 32 ? (1 << a.logPg) : 32;
-    TORCH_CHECK(bm0_ <= 128, "TreePlan: slot groups above 128 rows are not supported");
+    if (has("fwd_bm")) bm0_ = std::max<int>(bm0_, static_cast<int>(geti("fwd_bm")));
+    TORCH_CHECK(bm0_ == 32 || bm0_ == 64 || bm0_ == 128, "TreePlan: fwd rows per block must be 32, 64 or 128");
+    TORCH_CHECK(M % bm0_ == 0, "TreePlan: target rows must be a multiple of the fwd block rows");
     if (L_ == 3) {
       TrFwdArgs& b = fwd1_;
       b.x = Tk("A1").data_ptr();
@@ -321,7 +335,7 @@ class TreePlan {
     a.Wout = bf("Wout_sh", (int64_t)C_ * E_);
     a.WoutT = bf("Wout_shT", (int64_t)C_ * E_);
     a.bfc = f32("bfc", E_);
-    a.roots = i32("roots", B_);
+    a.roots = fwd0_.roots_cur;
     const int mode = static_cast<int>(geti("label_mode"));
     torch::Tensor lab = T("labels");
     TORCH_CHECK(lab.is_cuda() && lab.is_contiguous() && lab.device() == dev_, "labels must be contiguous on the GPU");
@@ -448,50 +462,49 @@ class TreePlan {
     a.n = n;
     std::vector<int64_t> off = getv("offsets");  // L convs, fc W, fc b, out W, end
     TORCH_CHECK((int)off.size() == L_ + 4 && off.back() == n, "TreePlan: offsets must cover the flat buffer");
-    int seg = 0;
+    // segments: conv weights [H_k][2 Hin_k] (+ transposed shadows where a backward GEMM
+    // reads them), fc W [E][H], fc bias [E] (vector), out W [C][E]
+    const int64_t H = dims_[L_ - 1];
+    int seg = 0, blk = 0;
     for (int k = 0; k < L_ + 3; ++k) {
       TrSeg& s = a.seg[seg++];
       s.off = off[k];
       s.n = off[k + 1] - off[k];
+      s.blk0 = blk;
       const bool bias = k == L_ + 1;
       if (bias) {  // the head's per-block fc-bias sums
         s.part = head_.dbfc_part;
         s.S = static_cast<int32_t>(B_ / kTrHeadRows);
-      } else {
-        const int pi = k < L_ ? k : (k == L_ ? L_ : L_ + 1);
-        const TrDwProb& p = probs_[pi];
-        TORCH_CHECK(s.n == (int64_t)p.P * p.Q, "TreePlan: flat segment ", k, " does not match its dW problem");
-        s.part = p.part;
-        s.S = p.S;
+        s.rows = 1;
+        s.cols = 0;
+        blk += static_cast<int>((s.n + 255) / 256);
+        continue;
       }
+      const int pi = k < L_ ? k : (k == L_ ? L_ : L_ + 1);
+      const TrDwProb& p = probs_[pi];
+      TORCH_CHECK(s.n == (int64_t)p.P * p.Q, "TreePlan: flat segment ", k, " does not match its dW problem");
+      s.part = p.part;
+      s.S = p.S;
+      s.rows = p.P;
+      s.cols = p.Q;
+      TORCH_CHECK(s.rows % 8 == 0 && s.cols % 32 == 0, "TreePlan: weight segments need rows % 8, cols % 32");
+      if (k < L_) {
+        const std::string ks = std::to_string(k);
+        s.sh = bf("W" + ks + "_sh", s.n);
+        s.shT = k >= 1 ? bf("W" + ks + "_shT", s.n) : nullptr;
+      } else if (k == L_) {
+        s.sh = bf("Wfc_sh", (int64_t)E_ * H);
+        s.shT = bf("Wfc_shT", (int64_t)E_ * H);
+      } else {
+        s.sh = bf("Wout_sh", (int64_t)C_ * E_);
+        s.shT = bf("Wout_shT", (int64_t)C_ * E_);
+      }
+      blk += (s.rows / 8) * (s.cols / 32);
     }
     a.nseg = seg;
-    // bf16 shadows: conv weights (+ transposes where a backward GEMM uses them), fc, out
-    int ns = 0;
-    for (int k = 0; k < L_; ++k) {
-      const std::string ks = std::to_string(k);
-      const int64_t rows = dims_[k], cols = 2 * Hin(k);
-      TrShadow& s = a.sh[ns++];
-      s.off = off[k];
-      s.n = rows * cols;
-      s.cols = static_cast<int32_t>(cols);
-      s.sh = bf("W" + ks + "_sh", rows * cols);
-      s.shT = k >= 1 ? bf("W" + ks + "_shT", rows * cols) : nullptr;
-    }
-    const int64_t H = dims_[L_ - 1];
-    TrShadow& f = a.sh[ns++];
-    f.off = off[L_];
-    f.n = (int64_t)E_ * H;
-    f.cols = static_cast<int32_t>(H);
-    f.sh = bf("Wfc_sh", f.n);
-    f.shT = bf("Wfc_shT", f.n);
-    TrShadow& o = a.sh[ns++];
-    o.off = off[L_ + 2];
-    o.n = (int64_t)C_ * E_;
-    o.cols = E_;
-    o.sh = bf("Wout_sh", o.n);
-    o.shT = bf("Wout_shT", o.n);
-    a.nsh = ns;
+    a.nblk = blk;
+    a.smp = sample_;
+    a.nsample = static_cast<int32_t>((sample_.M + 63) / 64);
     a.step = ptr<int64_t>("step", torch::kInt64, 1);
     a.lr = static_cast<float>(getf("lr"));
     a.b1 = static_cast<float>(getf("beta1"));
@@ -511,15 +524,16 @@ class TreePlan {
 }  // namespace
 
 void register_tree_ops(py::module& m) {
+  static_assert(kTrHeadSampleRows == 256, "head sampler blocks: 1024 threads, 256 rows");
   py::class_<TreePlan>(m, "TreePlan")
       .def(py::init<py::dict>())
       .def("sample", &TreePlan::sample)
       .def("fwd", &TreePlan::fwd, py::arg("prof") = py::none())
       .def("fwd_blocks", [](const TreePlan& t) { return t.fwd_blocks(); })
-      .def("head", &TreePlan::head, py::arg("prof") = py::none())
+      .def("head", &TreePlan::head, py::arg("prof") = py::none(), py::arg("with_sample") = false)
       .def("bwd", &TreePlan::bwd)
       .def("dw", &TreePlan::dw)
-      .def("opt", &TreePlan::opt, py::arg("mode"), py::arg("grad_scale") = 1.0)
+      .def("opt", &TreePlan::opt, py::arg("mode"), py::arg("grad_scale") = 1.0, py::arg("with_sample") = false)
       .def("set_lr", &TreePlan::set_lr)
       .def("num_problems", &TreePlan::num_problems)
       .def("splits", &TreePlan::splits)

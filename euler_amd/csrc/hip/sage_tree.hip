@@ -19,6 +19,8 @@
 //                     routed from dA1 through the tree inside the kernel (never stored)
 //   tr_opt   (mode 2) split-K reduce + Adam/Adagrad/SGD/momentum + bf16 weight shadows
 // (3 hops add one tr_fwd mode 2 and one tr_bwd; 1 hop uses tr_fwd mode 1).
+#include <cstdlib>
+
 #include "hip/tile.h"
 #include "hip/tree_args.h"
 
@@ -130,16 +132,21 @@ template <typename FT>
 struct Feat8;
 template <>
 struct Feat8<bf16_t> {
-  static constexpr int kInFlight = 12;  // rows in flight per thread
+  static constexpr int kInFlight = 10;  // rows in flight per thread and item
   uint4_t v;
   __device__ __forceinline__ void load(const bf16_t* p) { v = *reinterpret_cast<const uint4_t*>(p); }
   __device__ __forceinline__ void zero() { v = uint4_t{0u, 0u, 0u, 0u}; }
   __device__ __forceinline__ void add_to(float* acc) const { acc_bf16x8(acc, v); }
+  // keep = false: the row was a padding id (-1) loaded from row 0; contributes zero
+  __device__ __forceinline__ void keep(bool k) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = k ? v[i] : 0u;
+  }
   __device__ __forceinline__ uint4_t bf16() const { return v; }
 };
 template <>
 struct Feat8<float> {
-  static constexpr int kInFlight = 6;
+  static constexpr int kInFlight = 5;
   float4_t a, b;
   __device__ __forceinline__ void load(const float* p) {
     a = *reinterpret_cast<const float4_t*>(p);
@@ -151,6 +158,13 @@ struct Feat8<float> {
     for (int i = 0; i < 4; ++i) {
       acc[i] += a[i];
       acc[4 + i] += b[i];
+    }
+  }
+  __device__ __forceinline__ void keep(bool k) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      a[i] = k ? a[i] : 0.f;
+      b[i] = k ? b[i] : 0.f;
     }
   }
   __device__ __forceinline__ uint4_t bf16() const {
@@ -167,10 +181,13 @@ __device__ __forceinline__ float bf_hi(uint32_t v) { return __uint_as_float(v & 
 // ----------------------------------------------------------------------------
 constexpr int kTrSampleRows = 64;
 
-__global__ __launch_bounds__(256) void tr_sample_kernel(TrSampleArgs a) {
-  __shared__ int32_t node_s[kTrSampleRows];
-  const int64_t row0 = static_cast<int64_t>(blockIdx.x) * kTrSampleRows;
-  if (threadIdx.x < kTrSampleRows) {
+// one sampler block of NT threads: NT / 4 target rows (root -> hop chain by the first
+// NT / 4 threads, then every thread draws leaves)
+template <int NT>
+__device__ __forceinline__ void tr_sample_block(const TrSampleArgs& a, int blk, int32_t* node_s) {
+  constexpr int R = NT / 4;
+  const int64_t row0 = static_cast<int64_t>(blk) * R;
+  if (threadIdx.x < R) {
     const int64_t s = row0 + threadIdx.x;
     int32_t node = -1;
     if (s < a.M) {
@@ -183,7 +200,7 @@ __global__ __launch_bounds__(256) void tr_sample_kernel(TrSampleArgs a) {
     node_s[threadIdx.x] = node;
   }
   __syncthreads();
-  for (int it = threadIdx.x; it < kTrSampleRows * a.FL; it += 256) {
+  for (int it = threadIdx.x; it < R * a.FL; it += NT) {
     const int r = it / a.FL, k = it - r * a.FL;
     const int64_t s = row0 + r;
     if (s >= a.M) break;
@@ -195,11 +212,19 @@ __global__ __launch_bounds__(256) void tr_sample_kernel(TrSampleArgs a) {
   }
 }
 
+__global__ __launch_bounds__(256) void tr_sample_kernel(TrSampleArgs a) {
+  __shared__ int32_t node_s[kTrSampleRows];
+  tr_sample_block<256>(a, blockIdx.x, node_s);
+}
+
 // ----------------------------------------------------------------------------
 // tr_fwd: one SAGE layer over BM target rows per block (see TrFwdArgs)
 // ----------------------------------------------------------------------------
+#ifndef TR_FWD_WAVES
+#define TR_FWD_WAVES 4
+#endif
 template <typename FT, int BM, int MODE>
-__global__ __launch_bounds__(256, 2) void tr_fwd_kernel(TrFwdArgs a) {
+__global__ __launch_bounds__(256, (BM == 32 ? TR_FWD_WAVES : 2)) void tr_fwd_kernel(TrFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   constexpr bool kGather = MODE != 2;
   const int D = a.D;
@@ -219,12 +244,18 @@ __global__ __launch_bounds__(256, 2) void tr_fwd_kernel(TrFwdArgs a) {
 #define TF_STAMP(k) \
   if (a.prof && threadIdx.x == 0) a.prof[blockIdx.x * 8 + (k)] = static_cast<long long>(wall_clock64())
   TF_STAMP(0);
+  constexpr int FN = 4;
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const bf16_t* W = a.W;
+  uint4_t bcur[FN];
   if constexpr (kGather) {
     // ---- the sampled ids of the block (sampler output, one step ahead): coalesced
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       if (a.step) a.step[0] += 1;
       a.rng[1] += 1;  // this batch is consumed: the sampler draws the next counter
     }
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < a.B; i += gridDim.x * 256) a.roots_cur[i] = a.roots_in[i];
     if (threadIdx.x < BM) node_s[threadIdx.x] = row0 + threadIdx.x < a.M ? a.nodes[row0 + threadIdx.x] : -1;
     for (int it = threadIdx.x; it < BM * a.FL; it += 256)
       leaf_s[it] = row0 * a.FL + it < a.M * a.FL ? a.leaf[row0 * a.FL + it] : -1;
@@ -242,14 +273,14 @@ __global__ __launch_bounds__(256, 2) void tr_fwd_kernel(TrFwdArgs a) {
       const int ra = it / cpr, ca = it - ra * cpr;
       const int rb = hb ? itb / cpr : ra, cb = hb ? itb - rb * cpr : ca;
       const int32_t na = node_s[ra], nb = hb ? node_s[rb] : -1;
+      // branch-free loads: a padding id (-1) reads row 0 and is zeroed at use, so no
+      // divergent branch forces the compiler to wait on each load (vmcnt(0))
       Feat8<FT> sa, sb;
-      sa.zero();
-      sb.zero();
       float acc_a[8], acc_b[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) acc_a[i] = acc_b[i] = 0.f;
-      if (na >= 0) sa.load(x + static_cast<int64_t>(na) * D + ca * 8);
-      if (nb >= 0) sb.load(x + static_cast<int64_t>(nb) * D + cb * 8);
+      sa.load(x + static_cast<int64_t>(na > 0 ? na : 0) * D + ca * 8);
+      sb.load(x + static_cast<int64_t>(nb > 0 ? nb : 0) * D + cb * 8);
       for (int k = 0; k < a.FL; k += G) {
         int32_t ja[G], jb[G];
         Feat8<FT> va[G], vb[G];
@@ -258,19 +289,22 @@ __global__ __launch_bounds__(256, 2) void tr_fwd_kernel(TrFwdArgs a) {
           ja[u] = (k + u < a.FL) ? leaf_s[ra * a.FL + k + u] : -1;
           jb[u] = (hb && k + u < a.FL) ? leaf_s[rb * a.FL + k + u] : -1;
         }
+        // unconditional: slots past FL (ids -1) re-read the L2-resident row 0
 #pragma unroll
         for (int u = 0; u < G; ++u) {
-          if (ja[u] >= 0) va[u].load(x + static_cast<int64_t>(ja[u]) * D + ca * 8);
-          else va[u].zero();
-          if (jb[u] >= 0) vb[u].load(x + static_cast<int64_t>(jb[u]) * D + cb * 8);
-          else vb[u].zero();
+          va[u].load(x + static_cast<int64_t>(ja[u] > 0 ? ja[u] : 0) * D + ca * 8);
+          vb[u].load(x + static_cast<int64_t>(jb[u] > 0 ? jb[u] : 0) * D + cb * 8);
         }
 #pragma unroll
         for (int u = 0; u < G; ++u) {
+          va[u].keep(ja[u] >= 0);
+          vb[u].keep(jb[u] >= 0);
           va[u].add_to(acc_a);
           vb[u].add_to(acc_b);
         }
       }
+      sa.keep(na >= 0);
+      sb.keep(nb >= 0);
       if (a.include_self) {
         sa.add_to(acc_a);
         sb.add_to(acc_b);
@@ -309,6 +343,13 @@ __global__ __launch_bounds__(256, 2) void tr_fwd_kernel(TrFwdArgs a) {
       *reinterpret_cast<uint4_t*>(lds + r * ldsw + c * 8) = v;
     }
   }
+  // the GEMM's first B fragments (weights: L2-resident) load behind the kt pass
+  if constexpr (MODE != 1) {
+    if (wave * 64 < a.H) {
+#pragma unroll
+      for (int n = 0; n < FN; ++n) bcur[n] = fm_frag(W, wave * 64 + n * 16, 0, K2, lane);
+    }
+  }
   __syncthreads();
   TF_STAMP(2);
 
@@ -330,20 +371,17 @@ __global__ __launch_bounds__(256, 2) void tr_fwd_kernel(TrFwdArgs a) {
   TF_STAMP(3);
   // ---- MFMA GEMM out of LDS; wave w owns 64-column slab w of each 256-column chunk
   constexpr int FM = BM / 16;
-  constexpr int FN = 4;
-  const int wave = threadIdx.x >> 6;
-  const int lane = threadIdx.x & 63;
   const int lr = lane & 15, lk = (lane >> 4) * 8;
   const int ldo = kTrBN + 8;
-  const bf16_t* W = a.W;
   for (int cchunk = 0; cchunk < H; cchunk += kTrBN) {
     const int cb = cchunk + wave * 64;
     float4_t acc[FM][FN];
     tl_zero(acc);
     if (cb < H) {
-      uint4_t bcur[FN];
+      if (cchunk > 0) {
 #pragma unroll
-      for (int n = 0; n < FN; ++n) bcur[n] = fm_frag(W, cb + n * 16, 0, K2, lane);
+        for (int n = 0; n < FN; ++n) bcur[n] = fm_frag(W, cb + n * 16, 0, K2, lane);
+      }
       for (int k0 = 0; k0 < K2; k0 += 32) {
         uint4_t bnext[FN];
         const bool more = k0 + 32 < K2;
@@ -421,6 +459,164 @@ __global__ __launch_bounds__(256, 2) void tr_fwd_kernel(TrFwdArgs a) {
   }
   TF_STAMP(5);
 #undef TF_STAMP
+}
+
+// ----------------------------------------------------------------------------
+// tr_fwd_pk: layer 0 as a persistent kernel, one 512-thread block per CU.  The weight
+// (fm layout, <= 128 KB) is loaded into LDS once; the block then walks its 32-row tiles
+// and software-pipelines them: the feature rows of tile t + grid are in flight (in
+// registers) while tile t's A tile is multiplied out of LDS and its tree-mean epilogue
+// runs.  Requirements (else tr_fwd_kernel): 32-row tiles cover whole sibling groups,
+// H <= 256, H <= 2D, D <= 128, FL <= NF.
+// ----------------------------------------------------------------------------
+constexpr int kPkThreads = 512;
+
+template <typename FT, int NF>
+__global__ __launch_bounds__(kPkThreads, 1) void tr_fwd_pk_kernel(TrFwdArgs a, int ntiles) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  const int D = a.D, K2 = 2 * D, H = a.H;
+  const int ldsw = K2 + 8, ldo = H + 8;
+  bf16_t* Ws = lds;                                    // [H * K2] fm weight
+  bf16_t* At = lds + static_cast<int64_t>(H) * K2;     // [32][ldsw] A tile, then [32][ldo] h tile
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int lr = lane & 15, lk = (lane >> 4) * 8;
+  if (blockIdx.x == 0 && tid == 0) {
+    if (a.step) a.step[0] += 1;
+    a.rng[1] += 1;  // this batch is consumed: the sampler draws the next counter
+  }
+  for (int i = blockIdx.x * kPkThreads + tid; i < a.B; i += gridDim.x * kPkThreads) a.roots_cur[i] = a.roots_in[i];
+  for (int it = tid; it < (H * K2) >> 3; it += kPkThreads)
+    reinterpret_cast<uint4_t*>(Ws)[it] = reinterpret_cast<const uint4_t*>(a.W)[it];
+  // gather role: row gr (0..31), 8-column chunk gc; spare threads duplicate a valid item
+  const int cpr = D >> 3;
+  const bool gth = tid < 32 * cpr;
+  const int gi = gth ? tid : tid % (32 * cpr);
+  const int gr = gi / cpr, gc = gi - gr * cpr;
+  const FT* x = static_cast<const FT*>(a.x);
+  const int G = gridDim.x;
+  const int FL = a.FL;
+  auto load_ids = [&](int tt, int32_t& nd, int32_t (&lf)[NF]) {
+    const int64_t row = static_cast<int64_t>(tt < ntiles ? tt : ntiles - 1) * 32 + gr;
+    nd = a.nodes[row];
+#pragma unroll
+    for (int u = 0; u < NF; ++u) lf[u] = a.leaf[row * FL + (u < FL ? u : FL - 1)];
+  };
+  auto issue = [&](int32_t nd, const int32_t (&lf)[NF], Feat8<FT>& sv, Feat8<FT> (&lv)[NF]) {
+    sv.load(x + static_cast<int64_t>(nd > 0 ? nd : 0) * D + gc * 8);
+#pragma unroll
+    for (int u = 0; u < NF; ++u) lv[u].load(x + static_cast<int64_t>(lf[u] > 0 ? lf[u] : 0) * D + gc * 8);
+  };
+  // ids run two tiles ahead of the feature rows, so a tile's only dependent chain
+  // inside the loop is one feature-row load
+  int t = blockIdx.x;
+  int32_t nd, lf[NF], nd2, lf2[NF];
+  Feat8<FT> sv, lv[NF];
+  load_ids(t, nd, lf);
+  load_ids(t + G, nd2, lf2);
+  issue(nd, lf, sv, lv);
+  __syncthreads();  // weight in LDS
+  for (; t < ntiles; t += G) {
+    const int64_t row0 = static_cast<int64_t>(t) * 32;
+    int32_t nd3, lf3[NF];
+    load_ids(t + 2 * G, nd3, lf3);
+    // ---- finish the gather of tile t -> A tile [x_self | mean x_leaf]
+    {
+      float acc[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+#pragma unroll
+      for (int u = 0; u < NF; ++u) {
+        lv[u].keep(u < FL && lf[u] >= 0);
+        lv[u].add_to(acc);
+      }
+      sv.keep(nd >= 0);
+      if (a.include_self) sv.add_to(acc);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] *= a.inv_leaf;
+      if (gth) {
+        *reinterpret_cast<uint4_t*>(At + gr * ldsw + gc * 8) = sv.bf16();
+        *reinterpret_cast<uint4_t*>(At + gr * ldsw + D + gc * 8) = pack_bf16x8(acc);
+      }
+    }
+    __syncthreads();
+    // ---- the next tile's rows go in flight behind this tile's GEMM and epilogue
+    nd = nd2;
+    nd2 = nd3;
+#pragma unroll
+    for (int u = 0; u < NF; ++u) {
+      lf[u] = lf2[u];
+      lf2[u] = lf3[u];
+    }
+    issue(nd, lf, sv, lv);
+    // ---- A tile -> kt layout (dW operand): item = (column n, 8-row chunk q)
+    for (int it = tid; it < K2 * 4; it += kPkThreads) {
+      const int q = it & 3, n = it >> 2;
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = bf2f(At[(q * 8 + i) * ldsw + n]);
+      *reinterpret_cast<uint4_t*>(a.a_kt + kt_off(row0 + q * 8, n, K2)) = pack_bf16x8(v);
+    }
+    // ---- GEMM: wave w owns columns w*32 .. +31 (and +256 if H were larger: H <= 256)
+    const int cb = wave * 32;
+    float4_t acc[2][2];
+    tl_zero(acc);
+    if (cb < H) {
+      for (int k0 = 0; k0 < K2; k0 += 32) {
+        uint4_t av[2], bv[2];
+#pragma unroll
+        for (int m = 0; m < 2; ++m) av[m] = *reinterpret_cast<const uint4_t*>(At + (m * 16 + lr) * ldsw + k0 + lk);
+#pragma unroll
+        for (int n = 0; n < 2; ++n) bv[n] = fm_frag(Ws, cb + n * 16, k0, K2, lane);
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int n = 0; n < 2; ++n) acc[m][n] = mfma16(av[m], bv[n], acc[m][n]);
+      }
+    }
+    __syncthreads();  // A tile fully read: the h tile overwrites it
+    if (cb < H) {
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            At[(m * 16 + (lane >> 4) * 4 + j) * ldo + cb + n * 16 + lr] = f2bf(fmaxf(acc[m][n][j], 0.f));
+    }
+    __syncthreads();
+    // ---- tree mean of every sibling group -> parent A rows; ReLU bits
+    {
+      const int groups = 32 >> a.logPg;
+      const int pairs = H >> 1;
+      for (int it = tid; it < groups * pairs; it += kPkThreads) {
+        const int gg = it / pairs;
+        const int c = (it - gg * pairs) * 2;
+        const int base = gg << a.logPg;
+        const uint32_t selfp = *reinterpret_cast<const uint32_t*>(At + (base + a.Fg) * ldo + c);
+        float s0 = 0.f, s1 = 0.f;
+        for (int j = 0; j < a.Fg; ++j) {
+          const uint32_t v = *reinterpret_cast<const uint32_t*>(At + (base + j) * ldo + c);
+          s0 += bf_lo(v);
+          s1 += bf_hi(v);
+        }
+        if (a.include_self) {
+          s0 += bf_lo(selfp);
+          s1 += bf_hi(selfp);
+        }
+        const int64_t parent = (row0 >> a.logPg) + gg;
+        bf16_t* dst = a.a_next + parent * 2 * H + c;
+        *reinterpret_cast<uint32_t*>(dst) = selfp;
+        *reinterpret_cast<uint32_t*>(dst + H) = pack_bf16x2(s0 * a.inv_grp, s1 * a.inv_grp);
+      }
+      for (int n = tid - (kPkThreads - H); n >= 0 && n < H; n += H) {  // the last H threads
+        uint32_t bits = 0;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) bits |= (bf_pos(At[i * ldo + n]) ? 1u : 0u) << i;
+        a.mask[(row0 >> 5) * H + n] = bits;
+      }
+    }
+    __syncthreads();
+  }
 }
 
 // ----------------------------------------------------------------------------
@@ -535,6 +731,11 @@ __device__ __forceinline__ int tr_head_ld(int w) { return w + 8; }
 
 __global__ __launch_bounds__(HNW * 64) void tr_head_kernel(TrHeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  const int nhb = static_cast<int>(gridDim.x) - a.nsample;
+  if (static_cast<int>(blockIdx.x) >= nhb) {  // the next step's sampler on the CUs the head leaves idle
+    tr_sample_block<HNW * 64>(a.smp, blockIdx.x - nhb, reinterpret_cast<int32_t*>(lds));
+    return;
+  }
 #define TR_STAMP(k) \
   if (a.prof && threadIdx.x == 0) a.prof[blockIdx.x * 8 + (k)] = static_cast<long long>(wall_clock64())
   TR_STAMP(0);
@@ -792,10 +993,10 @@ struct RouteStage {
   uint4_t x[kRKB][4];
 };
 
-__global__ __launch_bounds__(256, 2) void tr_dw_route_kernel(TrDwProb pr) {
-  __shared__ __attribute__((aligned(16))) bf16_t gs[2][kRKB][kRP * kRLd];
-  // XCD-aware: the tiles of one split (which read the same X rows) share blockIdx % 8
-  const int b = blockIdx.x;
+typedef bf16_t RouteLds[2][kRKB][kRP * kRLd];
+
+__device__ __forceinline__ void tr_dw_route_body(const TrDwProb& pr, int b, RouteLds& gs) {
+  // XCD-aware: the tiles of one split (which read the same X rows) share b % 8
   const int j = b >> 3;
   const int tile = j % pr.ntiles;
   const int s = (j / pr.ntiles) * 8 + (b & 7);
@@ -879,8 +1080,8 @@ __global__ __launch_bounds__(256, 2) void tr_dw_route_kernel(TrDwProb pr) {
 // part[s][p][q] = sum_{m in split s} G[m][p] X[m][q]; 64x64 tiles, 4 waves of 32x32,
 // k-block groups double-buffered in registers (unrolled ping-pong: no register copies)
 // ----------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void tr_dw_kernel(TrDwProbs probs) {
-  const int id = xcd_remap(blockIdx.x, gridDim.x);
+__device__ __forceinline__ void tr_dw_plain_body(const TrDwProbs& probs, int b, int nwg) {
+  const int id = xcd_remap(b, nwg);
   // constant indices only (no dynamic indexing of kernel arguments)
   TrDwProb pr = probs.p[0];
 #pragma unroll
@@ -946,40 +1147,42 @@ __global__ __launch_bounds__(256) void tr_dw_kernel(TrDwProbs probs) {
         out[(p0 + fm * 16 + (lane >> 4) * 4 + j) * Q + q0 + fn * 16 + lr] = acc[fm][fn][j];
 }
 
+__global__ __launch_bounds__(256, 2) void tr_dw_all_kernel(TrDwLaunch a) {
+  __shared__ __attribute__((aligned(16))) RouteLds gs;
+  const int b = blockIdx.x;
+  if (a.nroute > 0 && b < a.rwg[1]) {
+    tr_dw_route_body(a.route[0], b, gs);
+  } else if (a.nroute > 1 && b < a.rwg[2]) {
+    tr_dw_route_body(a.route[1], b - a.rwg[1], gs);
+  } else {
+    const int r = a.rwg[a.nroute];
+    tr_dw_plain_body(a.plain, b - r, static_cast<int>(gridDim.x) - r);
+  }
+}
+
 // ----------------------------------------------------------------------------
 // tr_opt: split-K reduce and/or the optimizer over the flat fp32 parameters, the bf16
 // weight shadows, loss hand-off and the RNG counter advance (hipGraph-replay safe)
 // ----------------------------------------------------------------------------
-__device__ __forceinline__ void tr_shadow_write(const TrOptArgs& a, int64_t i, float val) {
-#pragma unroll
-  for (int s = 0; s < kTrMaxShadows; ++s) {
-    if (s >= a.nsh) break;
-    const TrShadow& sh = a.sh[s];
-    const int64_t l = i - sh.off;
-    if (l >= 0 && l < sh.n) {
-      const bf16_t b = f2bf(val);
-      const int64_t rows = sh.n / sh.cols;
-      const int64_t r = l / sh.cols, c = l - r * sh.cols;
-      sh.sh[fm_off(r, c, sh.cols)] = b;
-      if (sh.shT) sh.shT[fm_off(c, r, rows)] = b;
-    }
-  }
-}
-
 template <int MODE>
 __global__ __launch_bounds__(256) void tr_opt_kernel(TrOptArgs a) {
-  const int64_t i4 = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (blockIdx.x == 0 && threadIdx.x < 64) {
+  __shared__ float tile_s[8][33];
+  __shared__ int32_t node_s[kTrSampleRows];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  if (b >= a.nblk) {  // the next step's sampler (modes 1/2)
+    tr_sample_block<256>(a.smp, b - a.nblk, node_s);
+    return;
+  }
+  if (b == 0 && tid < 64 && MODE != 3) {
     // head statistics: reduce (modes 0/2) the per-block partials; hand the loss over (1/2)
-    const int lane = threadIdx.x;
     if (MODE != 1) {
       float v[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int b = lane; b < a.nhead; b += 64)
+      for (int k = tid; k < a.nhead; k += 64)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] += a.head_part[b * 4 + k];
+        for (int c = 0; c < 4; ++c) v[c] += a.head_part[k * 4 + c];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = wave_sum(v[k]);
-      if (lane == 0) {
+      for (int c = 0; c < 4; ++c) v[c] = wave_sum(v[c]);
+      if (tid == 0) {
         a.loss_acc[0] = v[0];
         if (a.counts) {
           a.counts[0] += static_cast<uint32_t>(v[1]);
@@ -988,64 +1191,93 @@ __global__ __launch_bounds__(256) void tr_opt_kernel(TrOptArgs a) {
         }
         if (MODE == 2) a.loss_out[0] = v[0];
       }
-    } else if (lane == 0) {
+    } else if (tid == 0) {
       a.loss_out[0] = a.loss_acc[0];
     }
   }
-  // one parameter per thread: the split-K slabs of a segment are read with 8 loads in
-  // flight per thread, 256 B per wave instruction
-  const int64_t i = i4;
-  if (i >= a.n) return;
   TrSeg sg = a.seg[0];
 #pragma unroll
-  for (int s = 1; s < kTrMaxSegs; ++s)
-    if (s < a.nseg && i >= a.seg[s].off) sg = a.seg[s];
-  float g;
-  if (MODE != 1) {
-    const float* src = sg.part + (i - sg.off);
-    g = 0.f;
-    for (int s0 = 0; s0 < sg.S; s0 += 8) {
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = (s0 + u < sg.S) ? src[(s0 + u) * sg.n] : 0.f;
-#pragma unroll
-      for (int u = 0; u < 8; ++u) g += v[u];
-    }
-    if (MODE == 0) {
-      a.g[i] = g;
-      return;
-    }
+  for (int k = 1; k < kTrMaxSegs; ++k)
+    if (k < a.nseg && b >= a.seg[k].blk0) sg = a.seg[k];
+  const int local = b - sg.blk0;
+  int64_t i;
+  int r = 0, c = 0;
+  bool valid = true;
+  if (sg.cols > 0) {  // 8 x 32 tile of a weight matrix
+    const int tiles_c = sg.cols >> 5;
+    const int tr = local / tiles_c, tc = local - tr * tiles_c;
+    r = tr * 8 + (tid >> 5);
+    c = tc * 32 + (tid & 31);
+    i = sg.off + static_cast<int64_t>(r) * sg.cols + c;
   } else {
-    g = a.g[i];
+    i = sg.off + static_cast<int64_t>(local) * 256 + tid;
+    valid = i < sg.off + sg.n;
+    if (!valid) i = sg.off;  // clamped: no early return before the tile barrier
   }
-  float p = a.p[i], m = a.m[i], v = a.v[i];
-  const float t = static_cast<float>(a.step[0]);
-  const float gi = g * a.grad_scale + a.wd * p;
-  if (a.kind == 0) {
-    const float bc1 = 1.f - __powf(a.b1, t), bc2 = 1.f - __powf(a.b2, t);
-    m = a.b1 * m + (1.f - a.b1) * gi;
-    v = a.b2 * v + (1.f - a.b2) * gi * gi;
-    p -= a.lr * (m / bc1) / (sqrtf(v / bc2) + a.eps);
-  } else if (a.kind == 1) {
-    v += gi * gi;
-    p -= a.lr * gi / (sqrtf(v) + a.eps);
-  } else if (a.kind == 2) {
-    p -= a.lr * gi;
-  } else {
-    m = a.b1 * m + gi;
-    p -= a.lr * m;
+  float p = a.p[i];
+  if (MODE != 3) {
+    float g;
+    if (MODE != 1) {
+      // split-K slabs: 16 loads in flight, indices clamped (no branch around a load)
+      const float* src = sg.part + (i - sg.off);
+      g = 0.f;
+      for (int s0 = 0; s0 < sg.S; s0 += 16) {
+        float v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = src[static_cast<int64_t>(s0 + u < sg.S ? s0 + u : sg.S - 1) * sg.n];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) g += (s0 + u < sg.S) ? v[u] : 0.f;
+      }
+      if (MODE == 0) {
+        if (valid) a.g[i] = g;
+        return;
+      }
+    } else {
+      g = a.g[i];
+    }
+    float m = a.m[i], v = a.v[i];
+    const float t = static_cast<float>(a.step[0]);
+    const float gi = g * a.grad_scale + a.wd * p;
+    if (a.kind == 0) {
+      const float bc1 = 1.f - __powf(a.b1, t), bc2 = 1.f - __powf(a.b2, t);
+      m = a.b1 * m + (1.f - a.b1) * gi;
+      v = a.b2 * v + (1.f - a.b2) * gi * gi;
+      p -= a.lr * (m / bc1) / (sqrtf(v / bc2) + a.eps);
+    } else if (a.kind == 1) {
+      v += gi * gi;
+      p -= a.lr * gi / (sqrtf(v) + a.eps);
+    } else if (a.kind == 2) {
+      p -= a.lr * gi;
+    } else {
+      m = a.b1 * m + gi;
+      p -= a.lr * m;
+    }
+    if (valid) {
+      a.p[i] = p;
+      a.m[i] = m;
+      a.v[i] = v;
+    }
   }
-  a.p[i] = p;
-  a.m[i] = m;
-  a.v[i] = v;
-  tr_shadow_write(a, i, p);
-}
-
-// shadows only (initialisation / after an external parameter write)
-__global__ __launch_bounds__(256) void tr_shadow_kernel(TrOptArgs a) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= a.n) return;
-  tr_shadow_write(a, i, a.p[i]);
+  // bf16 shadows of a weight tile: rows as 16-B fm chunks (threads 0-31), columns of the
+  // transpose (threads 32-63)
+  if (sg.cols > 0 && sg.sh) {
+    tile_s[tid >> 5][tid & 31] = p;
+    __syncthreads();
+    const int r0 = r - (tid >> 5), c0 = c - (tid & 31);
+    if (tid < 32) {
+      const int row = tid >> 2, kc = (tid & 3) * 8;
+      float t8[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t8[k] = tile_s[row][kc + k];
+      *reinterpret_cast<uint4_t*>(sg.sh + fm_off(r0 + row, c0 + kc, sg.cols)) = pack_bf16x8(t8);
+    } else if (tid < 64 && sg.shT) {
+      const int col = tid - 32;
+      float t8[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t8[k] = tile_s[k][col];
+      *reinterpret_cast<uint4_t*>(sg.shT + fm_off(c0 + col, r0, sg.rows)) = pack_bf16x8(t8);
+    }
+  }
 }
 
 }  // namespace euler_hip
@@ -1063,6 +1295,26 @@ size_t eh_tr_fwd_lds(int D, int H, int bm, int FL, int mode) {
   return b;
 }
 
+static size_t pk_lds(int D, int H) {
+  const int K2 = 2 * D;
+  const int w = (K2 > H ? K2 : H) + 8;
+  return (static_cast<size_t>(H) * K2 + 32 * static_cast<size_t>(w)) * sizeof(bf16_t);
+}
+
+// the persistent layer-0 kernel applies (see tr_fwd_pk_kernel)
+static bool pk_fits(const TrFwdArgs& a, int feat_fp32) {
+  static const bool on = [] {
+    const char* e = std::getenv("EULER_AMD_PK");  // opt-in: measured slower than tr_fwd_kernel so far
+    return e && e[0] == '1';
+  }();
+  if (!on) return false;
+  if (!a.a_kt || !a.mask || !a.nodes || !a.leaf) return false;
+  if ((1 << a.logPg) > 32 || a.M % 32 != 0) return false;
+  if (a.H > 256 || a.H > 2 * a.D || a.H % 64 != 0 || a.D > 128 || a.D % 16 != 0) return false;
+  if (a.FL > (feat_fp32 ? 10 : 25)) return false;
+  return pk_lds(a.D, a.H) <= 160 * 1024;
+}
+
 hipError_t eh_tr_sample(const TrSampleArgs* a, hipStream_t s) {
   if (a->M <= 0) return hipSuccess;
   if (!a->g.indptr || !a->g.nbr || !a->g.cumw || !a->g.prob || !a->g.alias || !a->tr.rng || !a->roots ||
@@ -1077,13 +1329,40 @@ hipError_t eh_tr_fwd(const TrFwdArgs* a, int mode, int feat_fp32, int bm, hipStr
   if (a->M <= 0) return hipSuccess;
   // every pointer the chosen mode dereferences must be set
   if (!a->x || !a->a_next) return hipErrorInvalidValue;
-  if (mode != 2 && (!a->nodes || !a->leaf || !a->rng || a->FL < 1)) return hipErrorInvalidValue;
+  if (mode != 2 && (!a->nodes || !a->leaf || !a->rng || a->FL < 1 || !a->roots_in || !a->roots_cur || a->B < 1))
+    return hipErrorInvalidValue;
   if (mode != 1 && !a->W) return hipErrorInvalidValue;
   if (a->D % 16 != 0 || a->D <= 0 || a->M % bm != 0) return hipErrorInvalidValue;
   if (mode != 1 && (a->H % 64 != 0 || a->H <= 0 || (bm >> a->logPg) < 1 || (bm & ((1 << a->logPg) - 1)) != 0 ||
                     a->Fg >= (1 << a->logPg)))
     return hipErrorInvalidValue;
   if (mode == 2 && feat_fp32) return hipErrorInvalidValue;
+  if (mode == 0 && pk_fits(*a, feat_fp32)) {
+    static int ncu = 0;
+    if (ncu == 0) {
+      int dev = 0;
+      EULER_HIP_CHECK(hipGetDevice(&dev));
+      EULER_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    const int ntiles = static_cast<int>(a->M / 32);
+    const int grid = ntiles < ncu ? ntiles : ncu;
+    const size_t plds = pk_lds(a->D, a->H);
+#define TR_PK(FT, NFV)                                                                                        \
+  do {                                                                                                        \
+    EULER_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(tr_fwd_pk_kernel<FT, NFV>),             \
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(plds))); \
+    hipLaunchKernelGGL((tr_fwd_pk_kernel<FT, NFV>), dim3(grid), dim3(kPkThreads), plds, s, *a, ntiles);      \
+    return hipGetLastError();                                                                                 \
+  } while (0)
+    if (feat_fp32) {
+      TR_PK(float, 10);
+    } else {
+      if (a->FL <= 10) TR_PK(bf16_t, 10);
+      if (a->FL <= 16) TR_PK(bf16_t, 16);
+      TR_PK(bf16_t, 25);
+    }
+#undef TR_PK
+  }
   const size_t lds = eh_tr_fwd_lds(a->D, a->H, bm, a->FL, mode);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   const dim3 grid(static_cast<uint32_t>(a->M / bm));
@@ -1133,7 +1412,14 @@ hipError_t eh_tr_head(const TrHeadArgs* a, int64_t B, hipStream_t s) {
   if (lds > 160 * 1024 - 64) return hipErrorInvalidValue;
   EULER_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(tr_head_kernel),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
-  hipLaunchKernelGGL(tr_head_kernel, dim3(static_cast<uint32_t>(B / HB)), dim3(HNW * 64), lds, s, *a);
+  if (a->nsample > 0) {
+    const TrSampleArgs& m = a->smp;
+    if (!m.g.indptr || !m.g.nbr || !m.g.cumw || !m.g.prob || !m.g.alias || !m.tr.rng || !m.roots || !m.nodes ||
+        !m.leaf || m.FL < 1 || m.lv < 0 || m.lv > 2 || a->nsample != ceil_div(m.M, kTrHeadSampleRows) ||
+        m.roots == a->roots)
+      return hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL(tr_head_kernel, dim3(static_cast<uint32_t>(B / HB + a->nsample)), dim3(HNW * 64), lds, s, *a);
   return hipGetLastError();
 }
 
@@ -1148,8 +1434,21 @@ hipError_t eh_tr_bwd(const TrBwdArgs* a, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t eh_tr_dw(TrDwProbs* pr, hipStream_t s) {
-  if (pr->n < 1 || pr->n > kTrMaxProbs) return hipErrorInvalidValue;
+hipError_t eh_tr_dw(TrDwLaunch* L, hipStream_t s) {
+  TrDwProbs* pr = &L->plain;
+  if (pr->n < 0 || pr->n > kTrMaxProbs || L->nroute < 0 || L->nroute > 2) return hipErrorInvalidValue;
+  L->rwg[0] = 0;
+  for (int r = 0; r < L->nroute; ++r) {
+    TrDwProb* p = &L->route[r];
+    if (!p->route || !p->dA || !p->mask || !p->X || !p->part) return hipErrorInvalidValue;
+    if (p->P % kRP != 0 || p->Q % 32 != 0 || p->MB < 1 || p->kps < 1 || p->logPg < 3) return hipErrorInvalidValue;
+    // the XCD-aware block mapping needs S % 8 == 0 (splits past MB write zero slabs)
+    if (p->S % 8 != 0 || static_cast<int64_t>(p->S) * p->kps < p->MB) return hipErrorInvalidValue;
+    p->tiles_q = static_cast<int>(ceil_div(p->Q, kRQ));
+    p->ntiles = (p->P / kRP) * p->tiles_q;
+    p->wg0 = 0;
+    L->rwg[r + 1] = L->rwg[r] + p->ntiles * p->S;
+  }
   int wg = 0;
   for (int i = 0; i < pr->n; ++i) {
     TrDwProb& p = pr->p[i];
@@ -1161,40 +1460,44 @@ hipError_t eh_tr_dw(TrDwProbs* pr, hipStream_t s) {
     p.wg0 = wg;
     wg += p.ntiles * p.S;
   }
-  hipLaunchKernelGGL(tr_dw_kernel, dim3(static_cast<uint32_t>(wg)), dim3(256), 0, s, *pr);
-  return hipGetLastError();
-}
-
-hipError_t eh_tr_dw_route(TrDwProb* p, hipStream_t s) {
-  if (!p->route || !p->dA || !p->mask || !p->X || !p->part) return hipErrorInvalidValue;
-  if (p->P % kRP != 0 || p->Q % 32 != 0 || p->MB < 1 || p->kps < 1 || p->logPg < 3) return hipErrorInvalidValue;
-  // the XCD-aware block mapping needs S % 8 == 0 (splits past MB write zero slabs)
-  if (p->S % 8 != 0 || static_cast<int64_t>(p->S) * p->kps < p->MB) return hipErrorInvalidValue;
-  p->tiles_q = static_cast<int>(ceil_div(p->Q, kRQ));
-  p->ntiles = (p->P / kRP) * p->tiles_q;
-  p->wg0 = 0;
-  hipLaunchKernelGGL(tr_dw_route_kernel, dim3(static_cast<uint32_t>(p->ntiles * p->S)), dim3(256), 0, s, *p);
+  const int total = L->rwg[L->nroute] + wg;
+  if (total == 0) return hipSuccess;
+  hipLaunchKernelGGL(tr_dw_all_kernel, dim3(static_cast<uint32_t>(total)), dim3(256), 0, s, *L);
   return hipGetLastError();
 }
 
 hipError_t eh_tr_opt(const TrOptArgs* a, int mode, hipStream_t s) {
-  if (a->n % 4 != 0 || a->nseg < 1 || a->nseg > kTrMaxSegs || a->nsh > kTrMaxShadows) return hipErrorInvalidValue;
+  if (a->nseg < 1 || a->nseg > kTrMaxSegs || a->nblk < 1) return hipErrorInvalidValue;
   if (!a->p || !a->g || !a->m || !a->v || !a->step || !a->loss_acc || !a->loss_out || !a->head_part ||
       a->nhead < 1)
     return hipErrorInvalidValue;
-  for (int i = 0; i < a->nsh; ++i)
-    if (!a->sh[i].sh || a->sh[i].cols <= 0) return hipErrorInvalidValue;
-  for (int i = 0; i < a->nseg; ++i)
-    if (a->seg[i].off % 4 != 0 || a->seg[i].n % 4 != 0 || !a->seg[i].part || a->seg[i].S < 1)
-      return hipErrorInvalidValue;
-  if (mode == 3) {
-    hipLaunchKernelGGL(tr_shadow_kernel, dim3(static_cast<uint32_t>(ceil_div(a->n, 256))), dim3(256), 0, s, *a);
-    return hipGetLastError();
+  int blk = 0;
+  for (int i = 0; i < a->nseg; ++i) {
+    const TrSeg& g = a->seg[i];
+    if (!g.part || g.S < 1 || g.blk0 != blk) return hipErrorInvalidValue;
+    if (g.cols > 0) {
+      if (g.rows % 8 != 0 || g.cols % 32 != 0 || static_cast<int64_t>(g.rows) * g.cols != g.n)
+        return hipErrorInvalidValue;
+      blk += (g.rows / 8) * (g.cols / 32);
+    } else {
+      if (g.sh || g.shT) return hipErrorInvalidValue;
+      blk += static_cast<int>(ceil_div(g.n, 256));
+    }
   }
-  const dim3 grid(static_cast<uint32_t>(ceil_div(a->n, 256)));
+  if (blk != a->nblk) return hipErrorInvalidValue;
+  int extra = 0;
+  if ((mode == 1 || mode == 2) && a->nsample > 0) {
+    const TrSampleArgs& m = a->smp;
+    if (!m.g.indptr || !m.g.nbr || !m.g.cumw || !m.g.prob || !m.g.alias || !m.tr.rng || !m.roots || !m.nodes ||
+        !m.leaf || m.FL < 1 || m.lv < 0 || m.lv > 2 || a->nsample != ceil_div(m.M, kTrSampleRows))
+      return hipErrorInvalidValue;
+    extra = a->nsample;
+  }
+  const dim3 grid(static_cast<uint32_t>(a->nblk + extra));
   if (mode == 0) hipLaunchKernelGGL(tr_opt_kernel<0>, grid, dim3(256), 0, s, *a);
   else if (mode == 1) hipLaunchKernelGGL(tr_opt_kernel<1>, grid, dim3(256), 0, s, *a);
   else if (mode == 2) hipLaunchKernelGGL(tr_opt_kernel<2>, grid, dim3(256), 0, s, *a);
+  else if (mode == 3) hipLaunchKernelGGL(tr_opt_kernel<3>, grid, dim3(256), 0, s, *a);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }

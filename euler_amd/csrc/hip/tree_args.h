@@ -16,8 +16,8 @@ namespace euler_hip {
 
 constexpr int kTrMaxProbs = 6;
 constexpr int kTrMaxSegs = 8;
-constexpr int kTrMaxShadows = 8;
 constexpr int kTrHeadRows = 16;  // roots per block of the head kernel
+constexpr int kTrHeadSampleRows = 256;  // target rows per sampler block of the head launch
 
 struct TrGraph {
   const int64_t* indptr;    // [N*T + 1]
@@ -76,6 +76,9 @@ struct TrFwdArgs {
   float inv_grp;         // 1 / (Fg + include_self)
   int64_t* step;         // optimizer step counter (block 0 increments it)
   int64_t* rng;          // (seed, counter): block 0 advances the counter (the batch is consumed)
+  const int32_t* roots_in;  // modes 0/1: [B] the batch's roots (sampler output) ...
+  int32_t* roots_cur;       // ... copied here for the head (the sampler may refill roots_in)
+  int32_t B;
   long long* prof;       // optional per-block phase stamps [grid][8]
 };
 
@@ -85,7 +88,7 @@ struct TrHeadArgs {
   int32_t Hin2, H, E, C, C_real;
   const uint16_t *W, *WT, *Wfc, *WfcT, *Wout, *WoutT;  // fm shadows
   const float* bfc;      // [E]
-  const int32_t* roots;  // [B]
+  const int32_t* roots;  // [B] (the forward's copy of the batch's roots)
   const void* labels;    // mode 0: int16 [N] class ids, 1: int32 [N], 2: bf16 [N][C] dense
   int32_t label_mode;
   float inv_scale;       // 1 / (B * C_real)
@@ -94,6 +97,8 @@ struct TrHeadArgs {
   float* dbfc_part;      // [B/kTrHeadRows][E] per-block fc-bias gradient (reduced by tr_opt)
   float* head_part;      // [B/kTrHeadRows][4] per-block loss, tp, fp, fn (reduced by tr_opt)
   long long* prof;       // optional per-block phase stamps [B/16][8]
+  TrSampleArgs smp;      // the next step's sampler, run by extra blocks of the launch on the
+  int32_t nsample;       // CUs the head leaves idle (0: none)
 };
 
 // inner-layer backward (3-hop): dA_out = route(dA_parent, mask) @ W  (fp32 rows)
@@ -125,25 +130,25 @@ struct TrDwProbs {
 };
 
 // flat parameter buffer segments: gradient = sum of S partials [S][n] (split-K slabs of a
-// dW problem, or the head's per-block fc-bias sums)
+// dW problem, or the head's per-block fc-bias sums).  Weight matrices (cols > 0, rows % 8
+// == 0, cols % 32 == 0) are processed in 8 x 32 tiles, one per block, so their bf16
+// shadows (fm [rows][cols] and the transpose fm [cols][rows]) are written as 16-B rows;
+// vectors (cols == 0) in 256-element blocks.
 struct TrSeg {
   int64_t off, n;
   const float* part;
   int32_t S;
-};
-struct TrShadow {
-  int64_t off, n;
-  int32_t cols;
-  uint16_t* sh;   // fm [rows][cols]
-  uint16_t* shT;  // fm [cols][rows] (optional)
+  int32_t rows, cols;  // cols == 0: vector segment
+  int32_t blk0;        // first block of the segment
+  uint16_t* sh;        // optional fm [rows][cols]
+  uint16_t* shT;       // optional fm [cols][rows]
 };
 struct TrOptArgs {
   float *p, *g, *m, *v;
   int64_t n;
   TrSeg seg[kTrMaxSegs];
   int32_t nseg;
-  TrShadow sh[kTrMaxShadows];
-  int32_t nsh;
+  int32_t nblk;  // blocks of the parameter part of the grid
   const int64_t* step;
   float lr, b1, b2, eps, wd, grad_scale;
   int32_t kind;  // 0 adam, 1 adagrad, 2 sgd, 3 momentum
@@ -152,6 +157,17 @@ struct TrOptArgs {
   float* loss_acc;         // loss of the last forward (written by the reduce)
   uint32_t* counts;        // tp, fp, fn since the last reset (accumulated by the reduce)
   float* loss_out;         // loss of the last optimizer step
+  TrSampleArgs smp;        // the next step's sampler, run by extra blocks (modes 1/2)
+  int32_t nsample;         // sampler blocks (0: none)
+};
+
+// one launch for every dW of the step: routed problems first (their blocks, S % 8 == 0),
+// then the stored-G problems grouped
+struct TrDwLaunch {
+  TrDwProbs plain;
+  TrDwProb route[2];
+  int32_t nroute;
+  int32_t rwg[3];  // block prefix of the routed problems
 };
 
 }  // namespace euler_hip
@@ -163,9 +179,10 @@ hipError_t eh_tr_fwd(const euler_hip::TrFwdArgs* a, int mode, int feat_fp32, int
 hipError_t eh_tr_head(const euler_hip::TrHeadArgs* a, int64_t B, hipStream_t s);
 hipError_t eh_tr_bwd(const euler_hip::TrBwdArgs* a, hipStream_t s);
 // fills S / tiles / wg0 of every problem from P, Q, MB, kps before launching
-hipError_t eh_tr_dw(euler_hip::TrDwProbs* p, hipStream_t s);        // stored-G problems, one launch
-hipError_t eh_tr_dw_route(euler_hip::TrDwProb* p, hipStream_t s);   // one routed problem (S % 8 == 0)
-// mode 0: split-K reduce into g; 1: optimizer from g; 2: both fused (single process)
+hipError_t eh_tr_dw(euler_hip::TrDwLaunch* p, hipStream_t s);
+// mode 0: split-K reduce into g; 1: optimizer from g; 2: both fused (single process);
+// 3: shadows only (after an external parameter write).  Modes 1/2 also run a->nsample
+// sampler blocks.
 hipError_t eh_tr_opt(const euler_hip::TrOptArgs* a, int mode, hipStream_t s);
 size_t eh_tr_fwd_lds(int D, int H, int bm, int FL, int mode);
 size_t eh_tr_head_lds(int Hin2, int H, int E, int C, int label_mode);

@@ -299,7 +299,7 @@ class SageTrainer:
              "offsets": self.offsets, "loss_acc": self.loss_acc, "loss_out": self.loss_out, "counts": self.counts,
              "lr": self.lr, "beta1": self.betas[0], "beta2": self.betas[1], "eps": self.eps,
              "weight_decay": self.wd, "opt_kind": _OPT_KIND[self.opt_name]}
-        for key in ("EULER_AMD_DW_TARGET_WG", "EULER_AMD_DW_MIN_KPS"):
+        for key in ("EULER_AMD_DW_TARGET_WG", "EULER_AMD_DW_MIN_KPS", "EULER_AMD_DW_ROUTE_WG", "EULER_AMD_FWD_BM"):
             if os.environ.get(key):
                 d[key[len("EULER_AMD_"):].lower()] = int(os.environ[key])
         M_last = self.M[L - 1]
@@ -335,9 +335,7 @@ class SageTrainer:
         d["bfc"] = views[L + 1]
         self._buf = d
         self.plan = hip().TreePlan(d)
-        self._side = torch.cuda.Stream(device=dev)
-        self._dw_route = list(self.plan.problems(True))
-        self._dw_plain = list(self.plan.problems(False))
+        self._dw_all = list(range(self.plan.num_problems()))
         self._primed = False  # the sample buffers hold the batch of counter graph.rng[1]
 
     # ------------------------------------------------------------------ parameters / state
@@ -414,7 +412,7 @@ class SageTrainer:
         p.head()
         self._primed = False
         p.bwd()
-        p.dw(list(range(p.num_problems())))
+        p.dw(self._dw_all)
         p.opt(0)
 
     def optimizer_step(self, grad_scale: float = 1.0):
@@ -425,42 +423,37 @@ class SageTrainer:
         the gradient reduce and the optimizer; None = single process (fused reduce +
         optimizer launch).
 
-        The next step's batch is sampled on a forked stream as soon as the head has read
-        this step's roots, concurrently with the backward (sampling reads only the graph
-        and the RNG counter the forward advanced), so the sampling latency chain is off
-        the critical path."""
+        One stream, no forks (a hipGraph branch join costs more than the work it would
+        overlap): fwd -> head -> [bwd] -> every dW in one launch -> optimizer.  The head
+        launch also carries the sampler of the NEXT step's batch in extra blocks, on the
+        CUs the head's B/16 blocks leave idle (sampling reads only the graph and the RNG
+        counter the forward advanced; the head reads the forward's copy of the roots), so
+        the sampler's dependent-load chain is off the critical path."""
         self.step_count += 1
         if not self.on_gpu:
             return self._cpu_step()
         p = self.plan
         self._prime()
-        cur = torch.cuda.current_stream(self.device)
         p.fwd()
-        p.head()
-        # fork: the next batch's sampling and the stored-operand dW GEMMs (fc, out, last
-        # conv) beside the routed dW of the lower layers on the main stream
-        self._side.wait_stream(cur)
-        with torch.cuda.stream(self._side):
-            p.sample()
-            p.dw(self._dw_plain)
+        p.head(None, True)
         p.bwd()
-        p.dw(self._dw_route)
-        cur.wait_stream(self._side)
+        p.dw(self._dw_all)
         if grad_sync is None:
             p.opt(2)
         else:
             p.opt(0)
             scale = grad_sync(self.grad)
-            self.optimizer_step(1.0 if scale is None else scale)
+            p.opt(1, 1.0 if scale is None else float(scale))
+        self._primed = True
 
     def plan_launches(self):
         """(name, callable) of every launch of one pipelined step, for per-kernel timing"""
         p = self.plan
-        out = [("sample", p.sample), ("fwd", p.fwd), ("head", p.head)]
+        out = [("sample", p.sample), ("fwd", p.fwd), ("head", p.head),
+               ("head+sample", lambda: p.head(None, True))]
         if self.L == 3:
             out.append(("bwd", p.bwd))
-        out += [("dw_route", lambda: p.dw(self._dw_route)), ("dw_plain", lambda: p.dw(self._dw_plain)),
-                ("opt", lambda: p.opt(2))]
+        out += [("dw", lambda: p.dw(self._dw_all)), ("opt", lambda: p.opt(2))]
         return out
 
     def capture(self, grad_sync=None, warmup: int = 2):

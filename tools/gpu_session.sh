@@ -39,8 +39,27 @@ for st in "${S[@]}"; do
       run pytest_gpu 900 python -u -m pytest $TESTS -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -rf ;;
     kernels)
       run tree_kernels 300 python -u tools/tree_kernels.py ;;
+    sweep_dw)
+      for wg in 256 512 768; do
+        EULER_AMD_DW_ROUTE_WG=$wg run "tree_kernels_rwg$wg" 300 python -u tools/tree_kernels.py
+      done
+      EULER_AMD_TREE_FORK=0 run tree_kernels_nofork 300 python -u tools/tree_kernels.py ;;
+    sweep_fwd)
+      for bm in 32 64 128; do
+        EULER_AMD_FWD_BM=$bm run "tree_kernels_fbm$bm" 300 python -u tools/tree_kernels.py
+      done ;;
+    trace)
+      run trace 300 rocprofv3 --kernel-trace -d "$OUT/trace" -o run --output-format csv -- \
+          python3 -u tools/tree_kernels.py --reps 20 && \
+      python tools/trace_gaps.py "$OUT/trace/run_kernel_trace.csv" --last 3 > "$OUT/trace_gaps.txt" 2>&1; \
+      cat "$OUT/trace_gaps.txt" ;;
     kernels_full)
       run tree_kernels_full 300 python -u tools/tree_kernels.py --num-nodes 100000000 ;;
+    kernels_sizes)
+      for nn in 2000000 100000000; do
+        run "tree_kernels_n$nn" 300 python -u tools/tree_kernels.py --num-nodes $nn
+      done
+      EULER_AMD_NO_PK=1 run tree_kernels_nopk 300 python -u tools/tree_kernels.py ;;
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench_small)

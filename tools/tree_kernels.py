@@ -55,7 +55,7 @@ def main():
     res = {}
     for name, fn in tr.plan_launches():
         res[name] = round(timeit(fn, args.reps), 2)
-    res["sum"] = round(sum(res.values()), 2)
+    res["sum"] = round(sum(v for k, v in res.items() if k not in ("sample", "head")), 2)
     for i in range(p.num_problems()):
         res[f"dw[{i}]"] = round(timeit(lambda: p.dw([i]), args.reps), 2)
     res["dw_splits"] = p.splits()
