@@ -353,18 +353,27 @@ __global__ __launch_bounds__(256, (BM == 32 ? TR_FWD_WAVES : 2)) void tr_fwd_ker
   __syncthreads();
   TF_STAMP(2);
 
-  // ---- A tile -> kt layout (dW operand): item = (column n, 8-row chunk q)
+  // ---- A tile -> kt layout (dW operand): item = (column pair, 8-row chunk q), column
+  // pairs fastest so a wave's 4-byte LDS reads cover consecutive banks
   if (a.a_kt) {
     constexpr int CH = BM / 8;
-    for (int it = threadIdx.x; it < K2 * CH; it += 256) {
-      const int q = it % CH;
-      const int n = it / CH;
+    const int np = K2 >> 1;
+    for (int it = threadIdx.x; it < np * CH; it += 256) {
+      const int q = it / np;
+      const int n = (it - q * np) * 2;
       const int64_t gr = row0 + q * 8;
       if (gr >= a.M) continue;
-      float v[8];
+      uint32_t w[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = bf2f(lds[(q * 8 + i) * ldsw + n]);
-      *reinterpret_cast<uint4_t*>(a.a_kt + kt_off(gr, n, K2)) = pack_bf16x8(v);
+      for (int i = 0; i < 8; ++i) w[i] = *reinterpret_cast<const uint32_t*>(lds + (q * 8 + i) * ldsw + n);
+      uint4_t lo, hi;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        lo[i] = (w[2 * i] & 0xffffu) | (w[2 * i + 1] << 16);
+        hi[i] = (w[2 * i] >> 16) | (w[2 * i + 1] & 0xffff0000u);
+      }
+      *reinterpret_cast<uint4_t*>(a.a_kt + kt_off(gr, n, K2)) = lo;
+      *reinterpret_cast<uint4_t*>(a.a_kt + kt_off(gr, n + 1, K2)) = hi;
     }
   }
 
@@ -717,13 +726,23 @@ __device__ __forceinline__ void tr_gemm(const bf16_t* A, int lda, const bf16_t* 
   }
 }
 
+// tile rows -> kt layout: item = (column pair, 8-row chunk), column pairs fastest (4-byte
+// LDS reads over consecutive banks), two 16-byte kt chunks per item
 __device__ __forceinline__ void tr_lds_to_kt(const bf16_t* tile, int ld, int N, int64_t r0, bf16_t* kt) {
-  for (int it = threadIdx.x; it < N * (HB / 8); it += HNW * 64) {
-    const int q = it % (HB / 8), n = it / (HB / 8);
-    float v[8];
+  const int np = N >> 1;
+  for (int it = threadIdx.x; it < np * (HB / 8); it += HNW * 64) {
+    const int q = it / np, n = (it - q * np) * 2;
+    uint32_t w[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = bf2f(tile[(q * 8 + i) * ld + n]);
-    *reinterpret_cast<uint4_t*>(kt + kt_off(r0 + q * 8, n, N)) = pack_bf16x8(v);
+    for (int i = 0; i < 8; ++i) w[i] = *reinterpret_cast<const uint32_t*>(tile + (q * 8 + i) * ld + n);
+    uint4_t lo, hi;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      lo[i] = (w[2 * i] & 0xffffu) | (w[2 * i + 1] << 16);
+      hi[i] = (w[2 * i] >> 16) | (w[2 * i + 1] & 0xffff0000u);
+    }
+    *reinterpret_cast<uint4_t*>(kt + kt_off(r0 + q * 8, n, N)) = lo;
+    *reinterpret_cast<uint4_t*>(kt + kt_off(r0 + q * 8, n + 1, N)) = hi;
   }
 }
 
@@ -982,15 +1001,16 @@ __device__ __forceinline__ uint4_t tr_route_frag(const TrDwProb& pr, const Route
 // ----------------------------------------------------------------------------
 // tr_dw_route: split-K dW of a layer whose output gradient is routed from the parent
 // rows (the tree mean's backward). Workgroup tile 64 p x 128 q; per stage of kRKB
-// k-blocks every thread builds ONE G^T fragment lane (p = tid & 63, 8 rows) into LDS, so
-// each routed element is built once per q tile; wave w multiplies 32 p x 64 q of it with
-// X fragments loaded straight from the kt layout, one stage ahead.
+// k-blocks every thread builds one G^T fragment lane per k-block (p = tid & 63, 8 rows)
+// into LDS, so each routed element is built once per q tile; wave w multiplies all 64 p
+// rows by its 32 q columns with X fragments loaded straight from the kt layout, one
+// stage (kRKB k-blocks) ahead.
 // ----------------------------------------------------------------------------
-constexpr int kRP = 64, kRQ = 128, kRKB = 2, kRLd = 40;
+constexpr int kRP = 64, kRQ = 128, kRKB = 8, kRLd = 40;
 
 struct RouteStage {
   RouteRaw r[kRKB];
-  uint4_t x[kRKB][4];
+  uint4_t x[kRKB][2];
 };
 
 typedef bf16_t RouteLds[2][kRKB][kRP * kRLd];
@@ -1004,12 +1024,12 @@ __device__ __forceinline__ void tr_dw_route_body(const TrDwProb& pr, int b, Rout
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int lr = lane & 15, lk = (lane >> 4) * 8;
   const int bp = tp * kRP + (tid & 63), blk = (tid >> 6) * 8;  // builder: column p, rows blk..+7
-  const int wp = (wave >> 1) * 32;                              // MFMA: tile rows wp..+31
-  const int wq = tq * kRQ + (wave & 1) * 64;                     //       columns wq..+63
+  const int wq = tq * kRQ + wave * 32;                           // MFMA: columns wq..+31, all 64 rows
   const int64_t Q = pr.Q;
+  const bool qok = wq < Q;  // uniform
   const int mb0 = s * pr.kps;
   const int mb1 = (mb0 + pr.kps) < pr.MB ? (mb0 + pr.kps) : pr.MB;
-  float4_t acc[2][4];
+  float4_t acc[4][2];
   tl_zero(acc);
   if (mb0 < mb1) {
     auto load = [&](RouteStage& st, int mbs) {
@@ -1018,8 +1038,8 @@ __device__ __forceinline__ void tr_dw_route_body(const TrDwProb& pr, int b, Rout
         const int mb = (mbs + u) < mb1 ? (mbs + u) : (mb1 - 1);  // clamped: always a valid row
         st.r[u] = tr_route_load(pr, mb, bp, blk);
 #pragma unroll
-        for (int f = 0; f < 4; ++f) {
-          const int q = wq + f * 16 < Q ? wq + f * 16 + lr : lr;
+        for (int f = 0; f < 2; ++f) {
+          const int q = qok ? wq + f * 16 + lr : lr;
           st.x[u][f] = *reinterpret_cast<const uint4_t*>(pr.X + ((static_cast<int64_t>(mb) * Q + q) * 32 + lk));
         }
       }
@@ -1032,19 +1052,18 @@ __device__ __forceinline__ void tr_dw_route_body(const TrDwProb& pr, int b, Rout
       }
     };
     auto compute = [&](const RouteStage& st, int buf, int mbs) {
+      if (!qok) return;
 #pragma unroll
       for (int u = 0; u < kRKB; ++u) {
         if (mbs + u >= mb1) break;  // uniform
-        uint4_t a[2];
+        uint4_t a[4];
 #pragma unroll
-        for (int fm = 0; fm < 2; ++fm)
-          a[fm] = *reinterpret_cast<const uint4_t*>(&gs[buf][u][(wp + fm * 16 + lr) * kRLd + lk]);
+        for (int fm = 0; fm < 4; ++fm)
+          a[fm] = *reinterpret_cast<const uint4_t*>(&gs[buf][u][(fm * 16 + lr) * kRLd + lk]);
 #pragma unroll
-        for (int fn = 0; fn < 4; ++fn) {
-          if (wq + fn * 16 >= Q) break;  // uniform
+        for (int fn = 0; fn < 2; ++fn)
 #pragma unroll
-          for (int fm = 0; fm < 2; ++fm) acc[fm][fn] = mfma16(a[fm], st.x[u][fn], acc[fm][fn]);
-        }
+          for (int fm = 0; fm < 4; ++fm) acc[fm][fn] = mfma16(a[fm], st.x[u][fn], acc[fm][fn]);
       }
     };
     RouteStage A, B;
@@ -1062,17 +1081,16 @@ __device__ __forceinline__ void tr_dw_route_body(const TrDwProb& pr, int b, Rout
       }
     }
   }
+  if (!qok) return;
   float* out = pr.part + static_cast<int64_t>(s) * pr.P * Q;
-  const int p0 = tp * kRP + wp;
+  const int p0 = tp * kRP;
 #pragma unroll
-  for (int fm = 0; fm < 2; ++fm)
+  for (int fm = 0; fm < 4; ++fm)
 #pragma unroll
-    for (int fn = 0; fn < 4; ++fn) {
-      if (wq + fn * 16 >= Q) break;
+    for (int fn = 0; fn < 2; ++fn)
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj)
         out[(p0 + fm * 16 + (lane >> 4) * 4 + jj) * Q + wq + fn * 16 + lr] = acc[fm][fn][jj];
-    }
 }
 
 // ----------------------------------------------------------------------------

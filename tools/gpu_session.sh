@@ -53,6 +53,9 @@ for st in "${S[@]}"; do
           python3 -u tools/tree_kernels.py --reps 20 && \
       python tools/trace_gaps.py "$OUT/trace/run_kernel_trace.csv" --last 3 > "$OUT/trace_gaps.txt" 2>&1; \
       cat "$OUT/trace_gaps.txt" ;;
+    pmc)
+      PASSES="FETCH_SIZE|TCC_HIT_sum TCC_MISS_sum|SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD|SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE|SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS" \
+        run pmc 600 bash tools/pmc_passes.sh tree "$PWD/tools/tree_kernels.py" --reps 10 ;;
     kernels_full)
       run tree_kernels_full 300 python -u tools/tree_kernels.py --num-nodes 100000000 ;;
     kernels_sizes)

@@ -10,7 +10,9 @@ NAME=$1; shift
 OUT=$REPO/gpurun_out/pmc_$NAME
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-for pass in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" "SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS"; do
+PASSES=${PASSES:-"FETCH_SIZE|WRITE_SIZE|SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE|SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS"}
+IFS='|' read -ra PL <<< "$PASSES"
+for pass in "${PL[@]}"; do
   tag=$(echo "$pass" | tr ' ' '+')
   timeout -s KILL 180 rocprofv3 --pmc $pass --output-format csv -d "$OUT/$tag" -o run -- python3 "$@" \
     > "$OUT/$tag.log" 2>&1 || { echo "pass $pass failed rc=$?"; tail -5 "$OUT/$tag.log"; exit 1; }
