@@ -227,7 +227,9 @@ class _SpmmIndex:
 
 
 def _spmm_index(edge_index, size):
-    key = "_euler_spmm_%d_%d" % (int(size[0]), int(size[1]))
+    # keyed on the tensor's version counter too: an in-place write to a caller's
+    # edge_index (copy_, index_put_) invalidates the cached CSR / CSC
+    key = "_euler_spmm_%d_%d_v%d" % (int(size[0]), int(size[1]), int(edge_index._version))
     cache = getattr(edge_index, "_euler_cache", None)
     if cache is None:
         cache = {}

@@ -1,7 +1,7 @@
 """contrib back ends (reference tf_euler/python/contrib) against plain fp32 PyTorch, and
 the sample-solution example end to end."""
+import math
 import os
-import sys
 
 import pytest
 import torch
@@ -43,23 +43,89 @@ def _check_scatter(device):
         torch.testing.assert_close(mx[r], want)
 
 
+def _check_grads(device):
+    """backward of spmm_add / spmm_mean (CSC SpMM) and of scatter_add / scatter_mean /
+    scatter_max against torch autograd on the dense reference"""
+    ei, x = _case(device)
+    a = _ref_adj(ei.cpu(), (9, 11)).to(device)
+    g = torch.randn(9, 5, generator=torch.Generator().manual_seed(3)).to(device)
+    for fn, dense in ((spmm.spmm_add, lambda t: a @ t),
+                      (spmm.spmm_mean, lambda t: (a @ t) / a.sum(1, keepdim=True).clamp(min=1))):
+        x1 = x.clone().requires_grad_(True)
+        (fn(x1, ei, (9, 11)) * g).sum().backward()
+        x2 = x.clone().requires_grad_(True)
+        (dense(x2) * g).sum().backward()
+        torch.testing.assert_close(x1.grad, x2.grad, atol=1e-5, rtol=1e-5)
+    idx = ei[0][:11]
+    for op in ("add", "mean", "max"):
+        x1 = x.clone().requires_grad_(True)
+        out = py_scatter.scatter_(op, x1, idx, 9, fill_value=-3.0 if op == "max" else 0.0)
+        (out * g).sum().backward()
+        x2 = x.clone().requires_grad_(True)
+        if op == "add":
+            ref = torch.zeros(9, 5, device=device).index_add(0, idx, x2)
+        elif op == "mean":
+            cnt = torch.zeros(9, device=device).index_add(0, idx, torch.ones(11, device=device)).clamp(min=1)
+            ref = torch.zeros(9, 5, device=device).index_add(0, idx, x2) / cnt[:, None]
+        else:
+            ref = torch.full((9, 5), -3.0, device=device).scatter_reduce(0, idx[:, None].expand(-1, 5), x2, "amax",
+                                                                         include_self=False)
+        (ref * g).sum().backward()
+        torch.testing.assert_close(x1.grad, x2.grad, atol=1e-5, rtol=1e-5)
+    # scatter_mean with a fill value: empty rows take it, the others are plain means
+    m = py_scatter.scatter_("mean", x, idx, 9, fill_value=4.0).cpu()
+    for r in range(9):
+        rows = x.cpu()[idx.cpu() == r]
+        want = rows.mean(0) if len(rows) else torch.full((5,), 4.0)
+        torch.testing.assert_close(m[r], want, atol=1e-5, rtol=1e-5)
+
+
+def _check_errors(device):
+    ei, x = _case(device)
+    with pytest.raises(ValueError):
+        spmm.spmm_add(x, ei, (9, 12))          # size[1] != src rows
+    with pytest.raises(ValueError):
+        spmm.spmm_add(x, ei, (3, 11))          # output index past size[0]
+    bad = ei.clone()
+    bad[1, 0] = 11
+    with pytest.raises(ValueError):
+        spmm.spmm_add(x, bad, (9, 11))         # source index past src
+    bad[1, 0] = -1
+    with pytest.raises(ValueError):
+        spmm.spmm_mean(x, bad, (9, 11))        # negative index
+
+
 def test_contrib_cpu():
     _check_spmm("cpu")
     _check_scatter("cpu")
+    _check_grads("cpu")
+    _check_errors("cpu")
     with pytest.raises(ValueError):
         spmm.spmm_("min", *_case()[::-1], (9, 11))
+
+
+def test_spmm_cache_follows_in_place_writes():
+    ei, x = _case()
+    spmm.spmm_add(x, ei, (9, 11))  # caches the CSR of the old contents
+    ei[0].copy_(torch.flip(ei[0], [0]))  # same tensor object, new contents
+    a = _ref_adj(ei, (9, 11))
+    torch.testing.assert_close(spmm.spmm_add(x, ei, (9, 11)), a @ x, atol=1e-5, rtol=1e-5)
 
 
 @pytest.mark.gpu
 def test_contrib_gpu():
     _check_spmm("cuda")
     _check_scatter("cuda")
+    _check_grads("cuda")
+    _check_errors("cuda")
 
 
-def test_run_sample_solution(tmp_path):
-    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples"))
+def test_run_sample_solution(tmp_path, monkeypatch):
+    monkeypatch.syspath_prepend(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples"))
     import run_sample_solution
 
     res = run_sample_solution.main(["--scale", "0.05", "--data_dir", str(tmp_path / "cora"), "--num_samples", "64",
                                     "--batch_size", "16", "--epoch", "1", "--model_dir", str(tmp_path / "ckpt")])
-    assert res["loss"] == res["loss"]
+    assert math.isfinite(res["loss"])
+    ckpt = tmp_path / "ckpt"
+    assert ckpt.exists() and any(ckpt.iterdir()), "the sample solution wrote no checkpoint"
