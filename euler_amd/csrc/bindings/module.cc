@@ -325,6 +325,23 @@ class Engine {
     return out;
   }
 
+  // random walks [n, L + 1] (node2vec-biased unless p = q = 1), GIL released
+  py::array_t<int64_t> RandomWalkPy(py::array_t<uint64_t, py::array::c_style | py::array::forcecast> starts,
+                                    std::vector<std::vector<int32_t>> etypes, double p, double q,
+                                    int64_t default_node, uint64_t seed) {
+    Graph& g = LocalGraph();
+    const int64_t n = starts.size();
+    const int64_t L = static_cast<int64_t>(etypes.size());
+    if (p <= 0.0 || q <= 0.0) throw std::invalid_argument("random_walk: p and q must be positive");
+    py::array_t<int64_t> out({n, L + 1});
+    {
+      py::gil_scoped_release nogil;
+      RandomWalk(g, starts.data(), n, etypes, static_cast<float>(p), static_cast<float>(q), default_node, seed,
+                 out.mutable_data());
+    }
+    return out;
+  }
+
   // dense node feature rows (missing ids / shorter rows -> zeros), [n, dim] float32
   py::array_t<float> DenseFeature(py::array_t<uint64_t, py::array::c_style | py::array::forcecast> ids,
                                   const std::string& name, int64_t dim) {
@@ -515,6 +532,8 @@ PYBIND11_MODULE(_engine, m) {
       .def("sample_neighbor", &Engine::SampleNeighbor)
       .def("sage_flow", &Engine::SageFlow, py::arg("roots"), py::arg("edge_types"), py::arg("counts"),
            py::arg("default_node"), py::arg("self_loops") = true)
+      .def("random_walk", &Engine::RandomWalkPy, py::arg("starts"), py::arg("edge_types"), py::arg("p"),
+           py::arg("q"), py::arg("default_node"), py::arg("seed"))
       .def("dense_feature", &Engine::DenseFeature)
       .def("export_csr", &Engine::ExportCsr)
       .def("export_nodes", &Engine::ExportNodes);

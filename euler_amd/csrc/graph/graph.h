@@ -236,6 +236,12 @@ class Graph {
 // source (reference-format .dat files, numpy arrays, JSON via Python, synthetic
 // generator), then Finish() sorts into the columnar layout.
 // ---------------------------------------------------------------------------
+// Random walks [n][L + 1] over out edges (walk.cc): p = q = 1 plain weighted walks,
+// otherwise node2vec-biased; etypes[s] = edge types of step s (empty = all); walk i uses
+// the Philox stream (seed, i).
+void RandomWalk(const Graph& g, const uint64_t* starts, int64_t n, const std::vector<std::vector<int32_t>>& etypes,
+                float p, float q, int64_t default_node, uint64_t seed, int64_t* out);
+
 class GraphBuilder {
  public:
   GraphBuilder() = default;

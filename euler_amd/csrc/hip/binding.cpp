@@ -109,7 +109,8 @@ torch::Tensor alias_sample(torch::Tensor prob, torch::Tensor alias, c10::optiona
 
 torch::Tensor random_walk(torch::Tensor indptr, torch::Tensor nbr, torch::Tensor cumw, int64_t num_rows,
                           int64_t num_types, torch::Tensor step_masks, torch::Tensor starts, int64_t default_row,
-                          torch::Tensor rng, int64_t stream_id) {
+                          torch::Tensor rng, int64_t stream_id, double p, double q) {
+  TORCH_CHECK(p > 0.0 && q > 0.0, "random_walk: p and q must be positive");
   need_i64(indptr, "indptr");
   need_i32(nbr, "nbr");
   need_cuda(cumw, "cumw");
@@ -124,7 +125,7 @@ torch::Tensor random_walk(torch::Tensor indptr, torch::Tensor nbr, torch::Tensor
                        static_cast<int>(num_types), reinterpret_cast<const uint32_t*>(step_masks.data_ptr<int32_t>()),
                        starts.data_ptr<int32_t>(), starts.numel(), static_cast<int>(walk_len),
                        static_cast<int32_t>(default_row), rng.data_ptr<int64_t>(), static_cast<uint64_t>(stream_id),
-                       out.data_ptr<int32_t>(), cur_stream()),
+                       static_cast<float>(p), static_cast<float>(q), out.data_ptr<int32_t>(), cur_stream()),
         "random_walk");
   return out;
 }
@@ -724,7 +725,9 @@ PYBIND11_MODULE(_hip_ops, m) {
   m.def("rng_advance", &rng_advance);
   m.def("sample_neighbor", &sample_neighbor);
   m.def("alias_sample", &alias_sample);
-  m.def("random_walk", &random_walk);
+  m.def("random_walk", &random_walk, py::arg("indptr"), py::arg("nbr"), py::arg("cumw"), py::arg("num_rows"),
+        py::arg("num_types"), py::arg("step_masks"), py::arg("starts"), py::arg("default_row"), py::arg("rng"),
+        py::arg("stream_id"), py::arg("p") = 1.0, py::arg("q") = 1.0);
   m.def("synth_csr", &synth_csr);
   m.def("sage_fwd", &sage_fwd);
   m.def("linear_fwd", &linear_fwd);

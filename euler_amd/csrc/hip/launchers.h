@@ -16,7 +16,8 @@ hipError_t eh_alias_sample(const float* prob, const int32_t* alias, const int32_
                            const int64_t* rng, uint64_t stream_id, int32_t* out, hipStream_t s);
 hipError_t eh_random_walk(const int64_t* indptr, const int32_t* nbr, const float* cumw, int64_t num_rows,
                           int num_types, const uint32_t* step_masks, const int32_t* starts, int64_t n, int walk_len,
-                          int32_t default_row, const int64_t* rng, uint64_t stream_id, int32_t* out, hipStream_t s);
+                          int32_t default_row, const int64_t* rng, uint64_t stream_id, float p, float q, int32_t* out,
+                          hipStream_t s);
 hipError_t eh_synth_degree(int64_t n, float avg_deg, int max_deg, uint64_t seed, int64_t* deg, hipStream_t s);
 hipError_t eh_synth_fill(int64_t n, const int64_t* indptr, uint64_t seed, int32_t* nbr, float* cumw, hipStream_t s);
 

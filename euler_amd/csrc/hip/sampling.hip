@@ -98,54 +98,111 @@ __global__ __launch_bounds__(256) void alias_sample_kernel(const float* __restri
   out[tid] = rows ? rows[pick] : static_cast<int32_t>(pick);
 }
 
-// Random walk (p = q = 1 path: chained weighted neighbor sampling;
-// reference random_walk_op.cc:179-188).  out [n, walk_len + 1].
+// Random walks, out [n, walk_len + 1] (reference random_walk_op.cc:70-188).
+// p = q = 1: chained weighted neighbour sampling (type group by weight, then a binary
+// search of its prefix sums).  Otherwise node2vec: candidate weights of the current row
+// times 1/p for the previous row, 1 for rows in the previous row's neighbour segments
+// (previous step's edge types; binary search, segments are sorted by row), 1/q for the
+// rest; two passes over the candidates (total, then the draw).  As in the reference the
+// first step's "previous" row is the start itself with no neighbour set.
+__device__ __forceinline__ bool rw_in_row(const int64_t* __restrict__ indptr, const int32_t* __restrict__ nbr,
+                                          int num_types, uint32_t mask, int64_t row, int32_t v) {
+  for (int t = 0; t < num_types; ++t) {
+    if (!((mask >> t) & 1u)) continue;
+    int64_t a = indptr[row * num_types + t], b = indptr[row * num_types + t + 1];
+    while (a < b) {
+      const int64_t m = (a + b) >> 1;
+      const int32_t x = nbr[m];
+      if (x == v) return true;
+      if (x < v) a = m + 1;
+      else b = m;
+    }
+  }
+  return false;
+}
+
 __global__ __launch_bounds__(256) void random_walk_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ nbr, const float* __restrict__ cumw,
     int64_t num_rows, int num_types, const uint32_t* __restrict__ step_masks, const int32_t* __restrict__ starts,
     int64_t n, int walk_len, int32_t default_row, const int64_t* __restrict__ rng, uint64_t stream_id,
-    int32_t* __restrict__ out) {
+    float inv_p, float inv_q, int biased, int32_t* __restrict__ out) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= n) return;
   int64_t cur = starts[i];
+  int64_t prev = cur;
+  uint32_t prev_mask = 0u;  // no neighbour set before the first step
   out[i * (walk_len + 1)] = static_cast<int32_t>(cur);
   for (int s = 0; s < walk_len; ++s) {
     int32_t nxt = default_row;
+    const uint32_t mask = step_masks[s];
     if (cur >= 0 && cur < num_rows) {
       const uint4_t r = Philox::gen(static_cast<uint64_t>(rng[0]),
                                     (static_cast<uint64_t>(rng[1]) << 8) ^ stream_id,
                                     static_cast<uint64_t>(i) * 1024u + s);
-      const uint32_t mask = step_masks[s];
       const int64_t base = cur * num_types;
-      float tot = 0.f;
-      for (int t = 0; t < num_types; ++t) {
-        if (!((mask >> t) & 1u)) continue;
-        const int64_t a = indptr[base + t], b = indptr[base + t + 1];
-        if (b > a) tot += cumw[b - 1];
-      }
-      if (tot > 0.f) {
-        float u = u01(r[0]) * tot;
-        int64_t lo = 0, hi = 0;
-        float g = 0.f;
+      if (biased) {
+        const bool has_prev = prev >= 0 && prev < num_rows;
+        float tot = 0.f;
+        for (int pass = 0; pass < 2 && nxt == default_row; ++pass) {
+          const float target = pass == 0 ? 0.f : u01(r[0]) * tot;
+          float acc = 0.f;
+          int32_t last = default_row;
+          for (int t = 0; t < num_types; ++t) {
+            if (!((mask >> t) & 1u)) continue;
+            const int64_t a = indptr[base + t], b = indptr[base + t + 1];
+            for (int64_t e = a; e < b; ++e) {
+              const int32_t c = nbr[e];
+              float w = e > a ? cumw[e] - cumw[e - 1] : cumw[e];
+              if (c == prev) w *= inv_p;
+              else if (!(has_prev && prev_mask && rw_in_row(indptr, nbr, num_types, prev_mask, prev, c))) w *= inv_q;
+              acc += w;
+              if (w > 0.f) last = c;
+              if (pass == 1 && acc > target) {
+                nxt = c;
+                break;
+              }
+            }
+            if (nxt != default_row) break;
+          }
+          if (pass == 0) tot = acc;
+          if (pass == 1 && nxt == default_row) nxt = last;  // rounding at the top end
+          if (pass == 0 && !(tot > 0.f)) break;
+        }
+      } else {
+        float tot = 0.f;
         for (int t = 0; t < num_types; ++t) {
           if (!((mask >> t) & 1u)) continue;
           const int64_t a = indptr[base + t], b = indptr[base + t + 1];
-          if (b <= a) continue;
-          g = cumw[b - 1];
-          lo = a; hi = b;
-          if (u < g) break;
-          u -= g;
+          if (b > a) tot += cumw[b - 1];
         }
-        const float v = u01(r[1]) * g;
-        int64_t a = lo, b = hi - 1;
-        while (a < b) {
-          const int64_t m = (a + b) >> 1;
-          if (cumw[m] > v) b = m; else a = m + 1;
+        if (tot > 0.f) {
+          float u = u01(r[0]) * tot;
+          int64_t lo = 0, hi = 0;
+          float g = 0.f;
+          for (int t = 0; t < num_types; ++t) {
+            if (!((mask >> t) & 1u)) continue;
+            const int64_t a = indptr[base + t], b = indptr[base + t + 1];
+            if (b <= a) continue;
+            g = cumw[b - 1];
+            lo = a;
+            hi = b;
+            if (u < g) break;
+            u -= g;
+          }
+          const float v = u01(r[1]) * g;
+          int64_t a = lo, b = hi - 1;
+          while (a < b) {
+            const int64_t m = (a + b) >> 1;
+            if (cumw[m] > v) b = m;
+            else a = m + 1;
+          }
+          nxt = nbr[a];
         }
-        nxt = nbr[a];
       }
     }
     out[i * (walk_len + 1) + s + 1] = nxt;
+    prev = cur;
+    prev_mask = mask;
     cur = nxt;
   }
 }
@@ -239,10 +296,14 @@ hipError_t eh_alias_sample(const float* prob, const int32_t* alias, const int32_
 
 hipError_t eh_random_walk(const int64_t* indptr, const int32_t* nbr, const float* cumw, int64_t num_rows,
                           int num_types, const uint32_t* step_masks, const int32_t* starts, int64_t n, int walk_len,
-                          int32_t default_row, const int64_t* rng, uint64_t stream_id, int32_t* out, hipStream_t s) {
+                          int32_t default_row, const int64_t* rng, uint64_t stream_id, float p, float q, int32_t* out,
+                          hipStream_t s) {
   if (n == 0) return hipSuccess;
+  if (!(p > 0.f) || !(q > 0.f)) return hipErrorInvalidValue;
+  const int biased = (p != 1.f || q != 1.f) ? 1 : 0;
   hipLaunchKernelGGL(random_walk_kernel, dim3(static_cast<uint32_t>(ceil_div(n, 256))), dim3(256), 0, s, indptr, nbr,
-                     cumw, num_rows, num_types, step_masks, starts, n, walk_len, default_row, rng, stream_id, out);
+                     cumw, num_rows, num_types, step_masks, starts, n, walk_len, default_row, rng, stream_id, 1.f / p,
+                     1.f / q, biased, out);
   return hipGetLastError();
 }
 

@@ -269,20 +269,85 @@ class DeviceGraph:
         return out
 
     def random_walk(self, starts: torch.Tensor, walk_len: int, edge_types=None, default: int = -1,
-                    stream_id: int = 3) -> torch.Tensor:
+                    stream_id: int = 3, p: float = 1.0, q: float = 1.0) -> torch.Tensor:
+        """Walks [n, walk_len + 1] of rows; node2vec-biased when p or q != 1 (see
+        ``random_walk_kernel`` in csrc/hip/sampling.hip; neighbour segments must be sorted
+        by row, as from_engine / synthetic build them)."""
+        if float(p) <= 0.0 or float(q) <= 0.0:
+            raise ValueError("random_walk: p and q must be positive")
         starts = starts.reshape(-1).int()
         masks = torch.tensor([self._mask(edge_types)] * int(walk_len), dtype=torch.int64)
         masks = ((masks + 2 ** 31) % 2 ** 32 - 2 ** 31).int()
         if use_hip(self.indptr, starts):
             return hip().random_walk(self.indptr, self.nbr, self.cumw, self.num_rows, self.num_types,
                                      masks.to(self.device), starts.contiguous(), int(default), self.rng,
-                                     int(stream_id))
-        cols = [starts]
-        cur = starts
-        for _ in range(int(walk_len)):
-            cur = self._sample_neighbor_cpu(cur, 1, self._mask(edge_types), default, False).reshape(-1)
-            cols.append(cur)
-        return torch.stack(cols, 1)
+                                     int(stream_id), float(p), float(q))
+        if float(p) == 1.0 and float(q) == 1.0:
+            cols = [starts]
+            cur = starts
+            for _ in range(int(walk_len)):
+                cur = self._sample_neighbor_cpu(cur, 1, self._mask(edge_types), default, False).reshape(-1)
+                cols.append(cur)
+            return torch.stack(cols, 1)
+        return self._node2vec_cpu(starts, int(walk_len), self._mask(edge_types), int(default), float(p), float(q))
+
+    def _candidates_cpu(self, rows: torch.Tensor, mask: int):
+        """(walk index, edge index) of every out edge of rows[i] under the type mask"""
+        T = self.num_types
+        ok = rows >= 0
+        walk, seg = [], []
+        for t in range(T):
+            if not (mask >> t) & 1:
+                continue
+            w = torch.nonzero(ok).reshape(-1)
+            walk.append(w)
+            seg.append(rows[w].long() * T + t)
+        if not walk:
+            return torch.zeros(0, dtype=torch.long), torch.zeros(0, dtype=torch.long)
+        walk, seg = torch.cat(walk), torch.cat(seg)
+        order = torch.argsort(walk, stable=True)  # walk-major (candidates of a walk contiguous)
+        walk, seg = walk[order], seg[order]
+        a, b = self.indptr[seg].cpu(), self.indptr[seg + 1].cpu()
+        ln = (b - a).clamp(min=0)
+        wi = torch.repeat_interleave(walk, ln)
+        off = torch.arange(int(ln.sum())) - torch.repeat_interleave(torch.cumsum(ln, 0) - ln, ln)
+        return wi, torch.repeat_interleave(a, ln) + off
+
+    def _node2vec_cpu(self, starts, walk_len, mask, default, p, q):
+        gen = torch.Generator().manual_seed(int(self.rng[0]) * 1000003 + int(self.rng[1]))
+        n, N = starts.numel(), self.num_rows
+        nbr, cumw, indptr = self.nbr.cpu().long(), self.cumw.cpu().double(), self.indptr.cpu()
+        seg_first = torch.zeros_like(cumw, dtype=torch.bool)
+        seg_first[indptr[:-1][indptr[:-1] < indptr[1:]]] = True
+        ew = torch.where(seg_first, cumw, cumw - torch.roll(cumw, 1))  # per-edge weights
+        cur = starts.long().cpu()
+        prev, prev_keys = cur.clone(), None
+        cols = [cur.clone()]
+        for _ in range(walk_len):
+            wi, e = self._candidates_cpu(cur, mask)
+            c = nbr[e]
+            w = ew[e] * torch.where(c == prev[wi], 1.0 / p, 1.0 / q)
+            keys = wi * N + c
+            if prev_keys is not None:
+                common = torch.isin(keys, prev_keys) & (c != prev[wi])
+                w = torch.where(common, ew[e], w)
+            nxt = torch.full((n,), default, dtype=torch.long)
+            if wi.numel():
+                cum = torch.cumsum(w, 0)
+                ar = torch.arange(n)
+                st = torch.searchsorted(wi, ar, right=False)
+                en = torch.searchsorted(wi, ar, right=True)
+                has = en > st
+                base = torch.where(st > 0, cum[(st - 1).clamp(min=0)], torch.zeros(n, dtype=cum.dtype))
+                tot = torch.where(has, cum[(en - 1).clamp(min=0)] - base, torch.zeros(n, dtype=cum.dtype))
+                u = base + torch.rand(n, generator=gen, dtype=torch.float64) * tot
+                pick = torch.minimum(torch.searchsorted(cum, u, right=True), (en - 1).clamp(min=0))
+                okw = has & (tot > 0)
+                nxt[okw] = c[pick[okw]]
+            prev_keys = keys
+            prev, cur = cur, nxt
+            cols.append(cur.clone())
+        return torch.stack(cols, 1).int()
 
     def degree(self, rows: torch.Tensor) -> torch.Tensor:
         r = rows.long()

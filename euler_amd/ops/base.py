@@ -75,8 +75,22 @@ def get_engine():
     return _ENGINE
 
 
+_WALK_SEED = [0x9E3779B97F4A7C15, 0]  # (global seed, calls): per-call walk seeds
+
+
 def set_seed(seed: int):
+    """Seed the engine's samplers and the per-call seeds of the walk ops."""
     _engine_mod().set_seed(int(seed))
+    _WALK_SEED[0], _WALK_SEED[1] = int(seed), 0
+
+
+def next_walk_seed() -> int:
+    """A fresh, reproducible seed for one walk call (a function of the global seed and the
+    number of calls since it was set)."""
+    _WALK_SEED[1] += 1
+    x = (_WALK_SEED[0] * 0x9E3779B97F4A7C15 + _WALK_SEED[1] * 0xBF58476D1CE4E5B9) & (2 ** 64 - 1)
+    x ^= x >> 31
+    return x & (2 ** 63 - 1)
 
 
 def synthetic_graph(num_nodes, avg_degree=10.0, max_degree=1024, node_types=1, edge_types=1, feature_dim=0,

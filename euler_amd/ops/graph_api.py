@@ -494,38 +494,72 @@ def get_edge_binary_feature(edges, feature_names, thread_num=1):
 
 
 # ----------------------------------------------------------------------------- walks
-def random_walk(nodes, edge_types, p=1.0, q=1.0, default_node=-1):
-    """Random walk [n, len(edge_types) + 1]; node2vec bias when p or q != 1
-    (reference random_walk_op.cc:70-188: 1/p back to the previous node, 1 to common
-    neighbors of the previous node, 1/q otherwise)."""
-    cur = torch.as_tensor(_u64(nodes).view(np.int64))
-    cols = [cur]
-    prev = None
-    for step, et in enumerate(edge_types):
-        if (p == 1.0 and q == 1.0) or prev is None:
-            nxt, _, _ = sample_neighbor(cur, et, 1, default_node)
-            nxt = nxt.reshape(-1)
-        else:
-            nb, w, _ = get_full_neighbor(cur, et)
-            prev_nb, _, _ = get_full_neighbor(prev, et)
-            nxt = torch.full((cur.numel(),), int(default_node), dtype=torch.int64)
-            rng = np.random.default_rng()
-            ind = nb.indices.numpy()
-            vals, wts = nb.values.numpy(), w.values.numpy()
-            pind, pvals = prev_nb.indices.numpy(), prev_nb.values.numpy()
-            for i in range(cur.numel()):
-                sel = ind[:, 0] == i
-                if not sel.any():
-                    continue
-                cand, cw = vals[sel], wts[sel].astype(np.float64)
-                pset = set(pvals[pind[:, 0] == i].tolist())
-                pv = int(prev[i])
-                bias = np.where(cand == pv, 1.0 / p, np.where(np.isin(cand, list(pset)), 1.0, 1.0 / q))
-                pw = cw * bias
-                nxt[i] = int(cand[rng.choice(len(cand), p=pw / pw.sum())])
-        cols.append(nxt)
-        prev, cur = cur, nxt
-    return torch.stack(cols, 1)
+def random_walk(nodes, edge_types, p=1.0, q=1.0, default_node=-1, seed=None):
+    """Random walks [n, len(edge_types) + 1] (``edge_types[s]`` = the edge types of step
+    s); node2vec bias when p or q != 1 (reference random_walk_op.cc:70-188: 1/p back to
+    the previous node, 1 to common neighbours of the previous node, 1/q otherwise).
+
+    Local graph: one GIL-free native call (``Engine.random_walk``, csrc/graph/walk.cc),
+    each walk on its own Philox stream.  ``seed`` None draws the next seed of
+    :func:`euler_amd.set_seed`'s sequence, so results are reproducible per global seed.
+    Remote shards: one full-neighbour query per step and a vectorised numpy draw with the
+    same bias, seeded the same way."""
+    from euler_amd.ops import base as _base
+
+    if float(p) <= 0.0 or float(q) <= 0.0:
+        raise ValueError("random_walk: p and q must be positive")
+    seed = _base.next_walk_seed() if seed is None else int(seed)
+    ids = _u64(nodes)
+    steps = [[int(x) for x in _et(et) if x >= 0] for et in edge_types]
+    eng = get_engine()
+    if _meta()["mode"] == "local":
+        return torch.as_tensor(eng.random_walk(ids, steps, float(p), float(q), int(default_node), seed))
+    return _random_walk_remote(ids, edge_types, float(p), float(q), int(default_node), seed)
+
+
+def _pair_keys(rows, ids):
+    """(row, id) pairs as 16-byte void scalars, for exact vectorised set membership"""
+    a = np.ascontiguousarray(np.stack([np.asarray(rows, np.uint64), np.asarray(ids, np.uint64)], 1))
+    return a.view(np.dtype((np.void, 16))).reshape(-1)
+
+
+def _random_walk_remote(ids, edge_types, p, q, default_node, seed):
+    rng = np.random.default_rng(seed)
+    n = len(ids)
+    cur = ids.astype(np.int64)
+    prev, prev_keys = cur.copy(), None  # step 0: the previous node is the start, no neighbour set
+    cols = [cur.copy()]
+    biased = p != 1.0 or q != 1.0
+    for et in edge_types:
+        nb, w, _ = get_full_neighbor(cur, et)
+        ind = nb.indices.numpy()
+        r, c = ind[:, 0], nb.values.numpy().astype(np.int64)
+        wt = w.values.numpy().astype(np.float64)
+        if biased and len(r):
+            bias = np.full(len(r), 1.0 / q)
+            if prev_keys is not None:
+                bias[np.isin(_pair_keys(r, c.view(np.uint64)), prev_keys)] = 1.0
+            bias[c == prev[r]] = 1.0 / p
+            wt = wt * bias
+        nxt = np.full(n, int(default_node), dtype=np.int64)
+        if len(r):
+            order = np.argsort(r, kind="stable")
+            r, c, wt = r[order], c[order], wt[order]
+            cum = np.cumsum(wt)
+            starts = np.searchsorted(r, np.arange(n), "left")
+            ends = np.searchsorted(r, np.arange(n), "right")
+            has = ends > starts
+            base = np.where(starts > 0, cum[np.maximum(starts - 1, 0)], 0.0)
+            tot = np.where(has, cum[np.maximum(ends - 1, 0)] - base, 0.0)
+            u = base + rng.random(n) * tot
+            pick = np.minimum(np.searchsorted(cum, u, "right"), np.maximum(ends - 1, 0))
+            ok = has & (tot > 0)
+            nxt[ok] = c[pick[ok]]
+        prev_keys = _pair_keys(r, c.view(np.uint64)) if biased else None
+        prev = cur
+        cur = nxt
+        cols.append(cur.copy())
+    return torch.as_tensor(np.stack(cols, 1))
 
 
 def gen_pair(paths, left_win_size, right_win_size):
