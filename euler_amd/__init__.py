@@ -12,15 +12,14 @@ Layers:
 __version__ = "0.1.0"
 
 from euler_amd.ops.base import (  # noqa: F401
-    GraphBuilder, get_engine, initialize_embedded_graph, initialize_graph, initialize_shared_graph, set_seed,
-    start_service, synthetic_graph, use_graph)
+    GraphBuilder, Module, get_engine, initialize_embedded_graph, initialize_graph, initialize_shared_graph, set_seed,
+    start, start_service, synthetic_graph, use_graph)
 from euler_amd.ops.graph_api import *  # noqa: F401,F403
 from euler_amd.ops.graph_api import __all__ as _graph_all
 # message-passing ops (reference tf_euler euler_ops/mp_ops.py re-exported at top level)
 from euler_amd.ops.mp_ops import gather, scatter_, scatter_add, scatter_max, scatter_mean, scatter_softmax  # noqa: F401
 
-start = start_service  # reference `euler.start(...)`
 
 __all__ = ["initialize_graph", "initialize_embedded_graph", "initialize_shared_graph", "use_graph", "get_engine",
-           "set_seed", "synthetic_graph", "GraphBuilder", "start_service", "start", "gather", "scatter_",
+           "set_seed", "synthetic_graph", "GraphBuilder", "Module", "start_service", "start", "gather", "scatter_",
            "scatter_add", "scatter_max", "scatter_mean", "scatter_softmax"] + list(_graph_all)

@@ -325,6 +325,8 @@ class Engine {
     return out;
   }
 
+  std::map<int, std::vector<std::string>> Endpoints() const { return proxy_->Endpoints(); }
+
   // random walks [n, L + 1] (node2vec-biased unless p = q = 1), GIL released
   py::array_t<int64_t> RandomWalkPy(py::array_t<uint64_t, py::array::c_style | py::array::forcecast> starts,
                                     std::vector<std::vector<int32_t>> etypes, double p, double q,
@@ -482,11 +484,14 @@ class PyBuilder {
 class PyServer {
  public:
   PyServer(const std::string& data_path, int shard_idx, int shard_num, const std::string& registry, int port,
-           int threads, const std::string& host) {
+           int threads, const std::string& host, const std::string& load_data_type,
+           const std::string& global_sampler_type, int heartbeat_ms) {
+    LoadOptions lopt;
+    Throw(LoadOptions::Parse(load_data_type, global_sampler_type, &lopt));
     Status st;
     {
       py::gil_scoped_release nogil;
-      st = LoadShard(data_path, shard_idx, shard_num, &g_, &idx_);
+      st = LoadShard(data_path, shard_idx, shard_num, &g_, &idx_, 8, lopt);
     }
     Throw(st);
     env_ = QueryProxy::MakeEnv(g_.get(), idx_.get(), shard_num);
@@ -495,6 +500,7 @@ class PyServer {
     opt.num_threads = threads;
     opt.registry = registry;
     opt.host = host;
+    opt.heartbeat_ms = heartbeat_ms;
     server_.reset(new GraphServer(env_.get(), shard_idx, shard_num, opt));
     Throw(server_->Start());
   }
@@ -536,6 +542,7 @@ PYBIND11_MODULE(_engine, m) {
            py::arg("q"), py::arg("default_node"), py::arg("seed"))
       .def("dense_feature", &Engine::DenseFeature)
       .def("export_csr", &Engine::ExportCsr)
+      .def("endpoints", [](Engine& e) { return e.Endpoints(); })
       .def("export_nodes", &Engine::ExportNodes);
 
   py::class_<PyBuilder>(m, "GraphBuilder")
@@ -554,9 +561,11 @@ PYBIND11_MODULE(_engine, m) {
       .def("finish", &PyBuilder::Finish);
 
   py::class_<PyServer>(m, "GraphServer")
-      .def(py::init<const std::string&, int, int, const std::string&, int, int, const std::string&>(),
+      .def(py::init<const std::string&, int, int, const std::string&, int, int, const std::string&, const std::string&,
+                    const std::string&, int>(),
            py::arg("data_path"), py::arg("shard_idx"), py::arg("shard_num"), py::arg("registry") = "",
-           py::arg("port") = 0, py::arg("threads") = 32, py::arg("host") = "127.0.0.1")
+           py::arg("port") = 0, py::arg("threads") = 32, py::arg("host") = "127.0.0.1",
+           py::arg("load_data_type") = "all", py::arg("global_sampler_type") = "all", py::arg("heartbeat_ms") = 1000)
       .def_property_readonly("port", &PyServer::port)
       .def_property_readonly("requests", &PyServer::requests)
       .def("stop", &PyServer::Stop);
@@ -632,6 +641,17 @@ PYBIND11_MODULE(_engine, m) {
     return nodes;
   }, py::arg("query"), py::arg("mode") = "local", py::arg("shard_num") = 1,
      py::arg("neighbor_indexes") = std::vector<std::string>{});
+  m.def(
+      "registry_list",
+      [](const std::string& spec, double ttl) {
+        std::map<int, std::vector<std::pair<Endpoint, ShardMeta>>> listing;
+        Throw(Registry::Open(spec)->List(&listing, ttl));
+        std::map<int, std::vector<std::string>> out;
+        for (auto& kv : listing)
+          for (auto& e : kv.second) out[kv.first].push_back(e.first.ToString());
+        return out;
+      },
+      py::arg("spec"), py::arg("ttl") = 0.0);
   m.def("set_seed", [](uint64_t s) { SetGlobalSeed(s); });
   m.def("hash64", [](py::bytes b) {
     std::string s = b;

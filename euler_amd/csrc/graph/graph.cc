@@ -321,7 +321,26 @@ void Graph::BuildEdgeIndex() {
   }
 }
 
-void Graph::BuildSamplers() {
+Status LoadOptions::Parse(const std::string& data, const std::string& sampler, LoadOptions* o) {
+  auto two = [](const std::string& v, const char* what, bool* a, bool* b) -> Status {
+    if (v == "none") *a = false, *b = false;
+    else if (v == "node") *a = true, *b = false;
+    else if (v == "edge") *a = false, *b = true;
+    else if (v == "all" || v.empty()) *a = true, *b = true;
+    else return Status::InvalidArgument(std::string("invalid ") + what + ": '" + v + "' (none, node, edge or all)");
+    return Status::OK();
+  };
+  EULER_RETURN_IF_ERROR(two(data, "load_data_type", &o->load_nodes, &o->load_edges));
+  return two(sampler, "global_sampler_type", &o->node_sampler, &o->edge_sampler);
+}
+
+std::string LoadOptions::ToString() const {
+  auto s = [](bool a, bool b) { return a ? (b ? "all" : "node") : (b ? "edge" : "none"); };
+  return std::string("load_data_type=") + s(load_nodes, load_edges) + " global_sampler_type=" +
+         s(node_sampler, edge_sampler);
+}
+
+void Graph::BuildSamplers(bool node_on, bool edge_on) {
   const int NT = num_node_types_;
   node_rows_by_type_.assign(NT, {});
   for (int64_t r = 0; r < num_nodes(); ++r) {
@@ -330,15 +349,17 @@ void Graph::BuildSamplers() {
   }
   node_sampler_.assign(NT + 1, AliasTable());
   node_wsum_.assign(NT + 1, 0.0);
-  for (int t = 0; t < NT; ++t) {
+  for (int t = 0; t < NT && node_on; ++t) {
     std::vector<float> w;
     w.reserve(node_rows_by_type_[t].size());
     for (int64_t r : node_rows_by_type_[t]) w.push_back(node_weight_[r]);
     node_sampler_[t].Init(w.data(), w.size());
     node_wsum_[t] = node_sampler_[t].total();
   }
-  node_sampler_[NT].Init(node_weight_.data(), node_weight_.size());
-  node_wsum_[NT] = node_sampler_[NT].total();
+  if (node_on) {
+    node_sampler_[NT].Init(node_weight_.data(), node_weight_.size());
+    node_wsum_[NT] = node_sampler_[NT].total();
+  }
 
   const int ET = num_edge_types_;
   edge_rows_by_type_.assign(ET, {});
@@ -348,14 +369,16 @@ void Graph::BuildSamplers() {
   }
   edge_sampler_.assign(ET + 1, AliasTable());
   edge_wsum_.assign(ET + 1, 0.0);
-  for (int t = 0; t < ET; ++t) {
+  for (int t = 0; t < ET && edge_on; ++t) {
     std::vector<float> w;
     for (int64_t e : edge_rows_by_type_[t]) w.push_back(edge_weight_[e]);
     edge_sampler_[t].Init(w.data(), w.size());
     edge_wsum_[t] = edge_sampler_[t].total();
   }
-  edge_sampler_[ET].Init(edge_weight_.data(), edge_weight_.size());
-  edge_wsum_[ET] = edge_sampler_[ET].total();
+  if (edge_on) {
+    edge_sampler_[ET].Init(edge_weight_.data(), edge_weight_.size());
+    edge_wsum_[ET] = edge_sampler_[ET].total();
+  }
 
   graph_labels_.clear();
   const FeatureInfo* fi = meta_.NodeFeature("binary_graph_label");
@@ -789,7 +812,7 @@ std::unique_ptr<Graph> GraphBuilder::Finish() {
   }
   g->meta_.node_count = N;
   g->meta_.edge_count = E;
-  g->BuildSamplers();
+  g->BuildSamplers(node_sampler_on_, edge_sampler_on_);
   // release builder memory
   nodes_.clear();
   adj_out_.clear();

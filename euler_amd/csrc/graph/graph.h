@@ -201,7 +201,7 @@ class Graph {
   static const Column<T>* ColAt(const std::vector<Column<T>>& v, int idx) {
     return (idx >= 0 && idx < static_cast<int>(v.size())) ? &v[idx] : nullptr;
   }
-  void BuildSamplers();
+  void BuildSamplers(bool node = true, bool edge = true);
   void BuildEdgeIndex();
 
   GraphMeta meta_;
@@ -236,6 +236,16 @@ class Graph {
 // source (reference-format .dat files, numpy arrays, JSON via Python, synthetic
 // generator), then Finish() sorts into the columnar layout.
 // ---------------------------------------------------------------------------
+// What a shard loads and which global samplers it builds (reference start_service.py:33-80
+// Module NODE / EDGE / NODE_SAMPLER / EDGE_SAMPLER and graph.cc:39-70): load_data_type
+// and global_sampler_type are each "none", "node", "edge" or "all".
+struct LoadOptions {
+  bool load_nodes = true, load_edges = true;
+  bool node_sampler = true, edge_sampler = true;
+  static Status Parse(const std::string& load_data_type, const std::string& global_sampler_type, LoadOptions* o);
+  std::string ToString() const;
+};
+
 // Random walks [n][L + 1] over out edges (walk.cc): p = q = 1 plain weighted walks,
 // otherwise node2vec-biased; etypes[s] = edge types of step s (empty = all); walk i uses
 // the Philox stream (seed, i).
@@ -273,10 +283,16 @@ class GraphBuilder {
                              bool load_edges = true, int threads = 8);
 
   std::unique_ptr<Graph> Finish();
+  // which global samplers Finish() builds (reference global_sampler_type, graph.cc:39-53)
+  void SetSamplers(bool node, bool edge) {
+    node_sampler_on_ = node;
+    edge_sampler_on_ = edge;
+  }
 
   int64_t pending_nodes() const { return static_cast<int64_t>(nodes_.size()); }
 
  private:
+  bool node_sampler_on_ = true, edge_sampler_on_ = true;
   struct NodeRec {
     uint64_t id;
     int32_t type;

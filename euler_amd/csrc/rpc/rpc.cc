@@ -6,6 +6,8 @@
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <sys/socket.h>
+#include <fcntl.h>
+#include <sys/stat.h>
 #include <sys/un.h>
 #include <unistd.h>
 
@@ -18,6 +20,11 @@ namespace euler {
 namespace {
 constexpr uint32_t kMagic = 0x524C5545;  // "EULR"
 enum : uint32_t { kPing = 1, kExecute = 2, kMeta = 3, kReply = 100 };
+
+// wall clock (file mtimes of the registry are wall-clock stamps)
+double WallSec() {
+  return std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
+}
 
 double NowSec() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -396,12 +403,26 @@ class FileRegistry : public Registry {
     unlink(JoinPath(dir_, std::to_string(shard) + "#" + ep.ToString()).c_str());
     return Status::OK();
   }
-  Status List(std::map<int, std::vector<std::pair<Endpoint, ShardMeta>>>* out) override {
+  Status Heartbeat(int shard, const Endpoint& ep) override {
+    const std::string path = JoinPath(dir_, std::to_string(shard) + "#" + ep.ToString());
+    if (utimensat(AT_FDCWD, path.c_str(), nullptr, 0) != 0)
+      return errno == ENOENT ? Status::NotFound("registry entry gone: " + path)
+                             : Status::Internal("registry heartbeat failed: " + path);
+    return Status::OK();
+  }
+  Status List(std::map<int, std::vector<std::pair<Endpoint, ShardMeta>>>* out, double ttl) override {
     out->clear();
     std::vector<std::string> names;
     EULER_RETURN_IF_ERROR(ListDir(dir_, &names));
+    const double now = WallSec();
     for (auto& n : names) {
       if (n.empty() || n[0] == '.') continue;
+      if (ttl > 0) {
+        struct stat st;
+        if (stat(JoinPath(dir_, n).c_str(), &st) != 0) continue;
+        const double mt = st.st_mtim.tv_sec + 1e-9 * st.st_mtim.tv_nsec;
+        if (now - mt > ttl) continue;  // no heartbeat within ttl: the server is gone
+      }
       const size_t h = n.find('#'), c = n.rfind(':');
       int64_t shard, port;
       if (h == std::string::npos || c == std::string::npos || !ParseInt64(n.substr(0, h), &shard) ||
@@ -441,7 +462,12 @@ class MemoryRegistry : public Registry {
     store()[name_].erase(std::to_string(shard) + "#" + ep.ToString());
     return Status::OK();
   }
-  Status List(std::map<int, std::vector<std::pair<Endpoint, ShardMeta>>>* out) override {
+  Status Heartbeat(int shard, const Endpoint& ep) override {  // in-process: lives with the server
+    std::lock_guard<std::mutex> l(mu());
+    return store()[name_].count(std::to_string(shard) + "#" + ep.ToString()) ? Status::OK()
+                                                                             : Status::NotFound("gone");
+  }
+  Status List(std::map<int, std::vector<std::pair<Endpoint, ShardMeta>>>* out, double) override {
     std::lock_guard<std::mutex> l(mu());
     out->clear();
     for (auto& kv : store()[name_]) (*out)[std::get<0>(kv.second)].push_back({std::get<1>(kv.second), std::get<2>(kv.second)});
@@ -502,7 +528,19 @@ Status GraphServer::Start() {
   }
   if (!opt_.registry.empty()) {
     registry_ = Registry::Open(opt_.registry);
-    EULER_RETURN_IF_ERROR(registry_->Register(shard_idx_, endpoint(), ShardMeta::FromEnv(*env_, shard_idx_, shard_num_)));
+    const ShardMeta meta = ShardMeta::FromEnv(*env_, shard_idx_, shard_num_);
+    EULER_RETURN_IF_ERROR(registry_->Register(shard_idx_, endpoint(), meta));
+    if (opt_.heartbeat_ms > 0) {
+      heartbeat_thread_ = std::thread([this, meta] {
+        std::unique_lock<std::mutex> l(hb_mu_);
+        while (running_.load()) {
+          hb_cv_.wait_for(l, std::chrono::milliseconds(opt_.heartbeat_ms));
+          if (!running_.load()) break;
+          const Status st = registry_->Heartbeat(shard_idx_, endpoint());
+          if (st.code() == Code::NOT_FOUND) registry_->Register(shard_idx_, endpoint(), meta);  // re-register
+        }
+      });
+    }
   }
   EULER_LOG(Info) << "graph server shard " << shard_idx_ << "/" << shard_num_ << " listening on " << port_;
   return Status::OK();
@@ -510,6 +548,11 @@ Status GraphServer::Start() {
 
 void GraphServer::Stop() {
   if (!running_.exchange(false)) return;
+  {
+    std::lock_guard<std::mutex> l(hb_mu_);
+    hb_cv_.notify_all();
+  }
+  if (heartbeat_thread_.joinable()) heartbeat_thread_.join();
   if (registry_) registry_->Deregister(shard_idx_, endpoint());
   shutdown(listen_fd_, SHUT_RDWR);
   close(listen_fd_);
@@ -592,20 +635,49 @@ RpcClients::RpcClients(std::map<int, std::vector<Endpoint>> shards, const Client
   for (auto& kv : shards) n = std::max(n, kv.first + 1);
   shards_.resize(n);
   rr_ = std::vector<std::atomic<uint64_t>>(n);
-  for (auto& kv : shards)
+  for (auto& kv : shards) {
+    auto hl = std::make_shared<HostList>();
     for (auto& ep : kv.second) {
-      std::unique_ptr<Host> h(new Host);
+      auto h = std::make_shared<Host>();
       h->ep = ep;
-      shards_[kv.first].push_back(std::move(h));
+      hl->push_back(std::move(h));
     }
+    shards_[kv.first] = std::move(hl);
+  }
+  for (auto& sp : shards_)
+    if (!sp) sp = std::make_shared<HostList>();
   pool_.reset(new ThreadPool(std::max(8, 2 * n), "euler-client"));
 }
 
 RpcClients::~RpcClients() {
   pool_.reset();
   for (auto& s : shards_)
-    for (auto& h : s)
+    for (auto& h : *std::atomic_load(&s))
       for (int fd : h->idle) close(fd);
+}
+
+void RpcClients::UpdateShard(int shard, const std::vector<Endpoint>& eps) {
+  if (shard < 0 || shard >= static_cast<int>(shards_.size()) || eps.empty()) return;
+  auto cur = std::atomic_load(&shards_[shard]);
+  auto next = std::make_shared<HostList>();
+  for (const auto& ep : eps) {
+    std::shared_ptr<Host> keep;
+    for (const auto& h : *cur)
+      if (h->ep.host == ep.host && h->ep.port == ep.port) keep = h;
+    if (!keep) {
+      keep = std::make_shared<Host>();
+      keep->ep = ep;
+    }
+    next->push_back(std::move(keep));
+  }
+  std::atomic_store(&shards_[shard], std::shared_ptr<const HostList>(std::move(next)));
+}
+
+std::map<int, std::vector<std::string>> RpcClients::Endpoints() const {
+  std::map<int, std::vector<std::string>> out;
+  for (size_t s = 0; s < shards_.size(); ++s)
+    for (const auto& h : *std::atomic_load(&shards_[s])) out[static_cast<int>(s)].push_back(h->ep.ToString());
+  return out;
 }
 
 Status RpcClients::CallHost(Host* h, uint32_t kind, const std::string& payload, std::string* reply) {
@@ -631,9 +703,11 @@ Status RpcClients::CallHost(Host* h, uint32_t kind, const std::string& payload, 
 }
 
 Status RpcClients::Call(int shard, uint32_t kind, const std::string& payload, std::string* reply) {
-  if (shard < 0 || shard >= static_cast<int>(shards_.size()) || shards_[shard].empty())
+  if (shard < 0 || shard >= static_cast<int>(shards_.size()))
     return Status::Unavailable("no server for shard " + std::to_string(shard));
-  auto& hosts = shards_[shard];
+  const std::shared_ptr<const HostList> snap = std::atomic_load(&shards_[shard]);  // registry watch may swap it
+  const HostList& hosts = *snap;
+  if (hosts.empty()) return Status::Unavailable("no server for shard " + std::to_string(shard));
   Status last;
   auto& ctr = EngineCounters::Get();
   for (int attempt = 0; attempt <= opt_.num_retries; ++attempt) {
@@ -699,9 +773,11 @@ Status RpcClients::FetchMeta(int shard, ShardMeta* meta) {
 
 // ============================================================================ QueryProxy
 Status LoadShard(const std::string& data_path, int shard_idx, int shard_num, std::unique_ptr<Graph>* g,
-                 std::unique_ptr<IndexManager>* idx, int threads) {
+                 std::unique_ptr<IndexManager>* idx, int threads, const LoadOptions& opt) {
   GraphBuilder b;
-  EULER_RETURN_IF_ERROR(b.LoadReferenceFormat(data_path, shard_idx, shard_num, true, true, threads));
+  b.SetSamplers(opt.node_sampler, opt.edge_sampler);
+  EULER_RETURN_IF_ERROR(
+      b.LoadReferenceFormat(data_path, shard_idx, shard_num, opt.load_nodes, opt.load_edges, threads));
   *g = b.Finish();
   idx->reset(new IndexManager);
   EULER_RETURN_IF_ERROR((*idx)->Load(JoinPath(data_path, "Index"), shard_idx, shard_num));
@@ -754,15 +830,57 @@ static std::string Cfg(const std::map<std::string, std::string>& c, const std::s
   return it == c.end() ? d : it->second;
 }
 
+Status LoadOptionsFromConfig(const std::map<std::string, std::string>& config, LoadOptions* opt) {
+  const std::string data = Cfg(config, "load_data_type", Cfg(config, "data_type", "all"));
+  const std::string smp = Cfg(config, "global_sampler_type", Cfg(config, "sampler_type", "all"));
+  return LoadOptions::Parse(data, smp, opt);
+}
+
+// registry watch (reference ZkServerMonitor child watch, zk_server_monitor.cc:186-200):
+// re-list live entries every `period` seconds and swap each shard's replica set, so a
+// server that stopped heartbeating is no longer routed to and a new replica is picked up
+void QueryProxy::WatchRegistry(std::string spec, double ttl, double period) {
+  std::unique_ptr<Registry> r = Registry::Open(spec);
+  std::unique_lock<std::mutex> l(watch_mu_);
+  while (!watch_stop_) {
+    watch_cv_.wait_for(l, std::chrono::milliseconds(static_cast<int64_t>(period * 1000)));
+    if (watch_stop_) break;
+    std::map<int, std::vector<std::pair<Endpoint, ShardMeta>>> listing;
+    if (!r->List(&listing, ttl).ok()) continue;
+    auto* rc = static_cast<RpcClients*>(clients_.get());
+    for (auto& kv : listing) {
+      std::vector<Endpoint> eps;
+      for (auto& e : kv.second) eps.push_back(e.first);
+      rc->UpdateShard(kv.first, eps);  // a shard with no live entry keeps its last replicas
+    }
+  }
+}
+
+std::map<int, std::vector<std::string>> QueryProxy::Endpoints() const {
+  if (mode_ != "remote" && mode_ != "graph_partition") return {};
+  return static_cast<RpcClients*>(clients_.get())->Endpoints();
+}
+
+QueryProxy::~QueryProxy() {
+  {
+    std::lock_guard<std::mutex> l(watch_mu_);
+    watch_stop_ = true;
+    watch_cv_.notify_all();
+  }
+  if (watch_thread_.joinable()) watch_thread_.join();
+}
+
 Status QueryProxy::Init(const std::map<std::string, std::string>& config) {
   mode_ = Cfg(config, "mode", "local");
   int64_t seed;
   if (ParseInt64(Cfg(config, "seed", ""), &seed)) SetGlobalSeed(static_cast<uint64_t>(seed));
   pool_.reset(new ThreadPool(8, "euler-proxy"));
+  LoadOptions lopt;
+  EULER_RETURN_IF_ERROR(LoadOptionsFromConfig(config, &lopt));
   if (mode_ == "local") {
     std::unique_ptr<Graph> g;
     std::unique_ptr<IndexManager> idx;
-    EULER_RETURN_IF_ERROR(LoadShard(Cfg(config, "data_path", ""), 0, 1, &g, &idx));
+    EULER_RETURN_IF_ERROR(LoadShard(Cfg(config, "data_path", ""), 0, 1, &g, &idx, 8, lopt));
     return InitWithGraph(std::move(g), std::move(idx));
   }
   int64_t shards = 1;
@@ -775,7 +893,7 @@ Status QueryProxy::Init(const std::map<std::string, std::string>& config) {
     for (int s = 0; s < shards; ++s) {
       std::unique_ptr<Graph> g;
       std::unique_ptr<IndexManager> idx;
-      EULER_RETURN_IF_ERROR(LoadShard(path, s, static_cast<int>(shards), &g, &idx));
+      EULER_RETURN_IF_ERROR(LoadShard(path, s, static_cast<int>(shards), &g, &idx, 8, lopt));
       shard_envs_.push_back(MakeEnv(g.get(), idx.get(), static_cast<int>(shards)));
       envs.push_back(shard_envs_.back().get());
       metas.push_back(ShardMeta::FromEnv(*envs.back(), s, static_cast<int>(shards)));
@@ -795,11 +913,13 @@ Status QueryProxy::Init(const std::map<std::string, std::string>& config) {
     std::map<int, std::vector<std::pair<Endpoint, ShardMeta>>> listing;
     int64_t want = 0;
     ParseInt64(Cfg(config, "shard_num", "0"), &want);
-    double wait = 30;
+    double wait = 30, ttl = 10, refresh = 2;
     ParseDouble(Cfg(config, "wait_seconds", "30"), &wait);
+    ParseDouble(Cfg(config, "registry_ttl", "10"), &ttl);        // entries not refreshed within ttl are dead
+    ParseDouble(Cfg(config, "registry_refresh", "2"), &refresh);  // client re-list period (0: never)
     const double deadline = NowSec() + wait;
     for (;;) {
-      EULER_RETURN_IF_ERROR(r->List(&listing));
+      EULER_RETURN_IF_ERROR(r->List(&listing, ttl));
       int expect = static_cast<int>(want);
       if (!listing.empty() && expect == 0) expect = listing.begin()->second.front().second.shard_num;
       if (expect > 0 && static_cast<int>(listing.size()) >= expect) break;
@@ -818,6 +938,7 @@ Status QueryProxy::Init(const std::map<std::string, std::string>& config) {
       metas.push_back(kv.second.front().second);
     }
     clients_.reset(new RpcClients(eps, co));
+    if (refresh > 0) watch_thread_ = std::thread([this, reg, ttl, refresh] { WatchRegistry(reg, ttl, refresh); });
     shards = static_cast<int64_t>(listing.size());
     env_.shard_num = static_cast<int>(shards);
     env_.num_partitions = std::max<uint32_t>(1, metas[0].num_partitions);

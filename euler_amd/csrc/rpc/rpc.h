@@ -80,13 +80,19 @@ struct Endpoint {
   std::string ToString() const { return host + ":" + std::to_string(port); }
 };
 
+// Service discovery (reference ZK registry: zk_server_register.cc / zk_server_monitor.cc).
+// Liveness replaces ZooKeeper's ephemeral nodes: a server refreshes its entry every
+// heartbeat (Heartbeat; NOT_FOUND -> the server registers again, the analog of
+// re-registering after a session expiry) and List(ttl) skips entries not refreshed within
+// ttl seconds, so a SIGKILLed server drops out of every client's view.
 class Registry {
  public:
   virtual ~Registry() = default;
   virtual Status Register(int shard, const Endpoint& ep, const ShardMeta& meta) = 0;
   virtual Status Deregister(int shard, const Endpoint& ep) = 0;
-  // shard -> replicas
-  virtual Status List(std::map<int, std::vector<std::pair<Endpoint, ShardMeta>>>* out) = 0;
+  virtual Status Heartbeat(int shard, const Endpoint& ep) = 0;
+  // shard -> live replicas (ttl <= 0: every entry)
+  virtual Status List(std::map<int, std::vector<std::pair<Endpoint, ShardMeta>>>* out, double ttl = 0) = 0;
   // "file:<dir>" | "<dir>" | "memory:<name>"
   static std::unique_ptr<Registry> Open(const std::string& spec);
 };
@@ -97,6 +103,7 @@ struct ServerOptions {
   std::string host;  // advertised host (default: 127.0.0.1)
   int num_threads = 32;
   std::string registry;  // optional
+  int heartbeat_ms = 1000;  // registry entry refresh period
 };
 
 class GraphServer {
@@ -125,6 +132,9 @@ class GraphServer {
   std::vector<int> conn_fds_;
   std::unique_ptr<ThreadPool> pool_;
   std::unique_ptr<Registry> registry_;
+  std::thread heartbeat_thread_;
+  std::mutex hb_mu_;
+  std::condition_variable hb_cv_;
   std::atomic<int64_t> requests_{0};
 };
 
@@ -141,6 +151,9 @@ class RpcClients : public RemoteClients {
   RpcClients(std::map<int, std::vector<Endpoint>> shards, const ClientOptions& opt);
   ~RpcClients() override;
   int num_shards() const override { return static_cast<int>(shards_.size()); }
+  // replace the replicas of a shard (registry watch); hosts still present keep their pools
+  void UpdateShard(int shard, const std::vector<Endpoint>& eps);
+  std::map<int, std::vector<std::string>> Endpoints() const;
   void Execute(int shard, const DAGDef& dag, std::vector<std::pair<std::string, Tensor>> inputs,
                std::vector<std::string> outputs, Done done) override;
   Status Ping(int shard);
@@ -154,9 +167,11 @@ class RpcClients : public RemoteClients {
     std::vector<int> idle;  // pooled connected sockets
     double bad_until = 0;
   };
+  typedef std::vector<std::shared_ptr<Host>> HostList;
   Status Call(int shard, uint32_t kind, const std::string& payload, std::string* reply);
   Status CallHost(Host* h, uint32_t kind, const std::string& payload, std::string* reply);
-  std::vector<std::vector<std::unique_ptr<Host>>> shards_;
+  // per shard, swapped atomically by UpdateShard (callers work on a snapshot)
+  std::vector<std::shared_ptr<const HostList>> shards_;
   std::vector<std::atomic<uint64_t>> rr_;
   ClientOptions opt_;
   std::unique_ptr<ThreadPool> pool_;
@@ -186,9 +201,17 @@ class QueryProxy {
   int shard_num() const { return env_.shard_num; }
   // run a DAG in-process against a shard env (used by the local fast paths)
   static std::unique_ptr<EngineEnv> MakeEnv(Graph* g, IndexManager* idx, int shard_num);
+  // remote mode: current replicas per shard as the client routes to them
+  std::map<int, std::vector<std::string>> Endpoints() const;
+  ~QueryProxy();
 
  private:
   Status FillWeightTables(const std::vector<ShardMeta>& metas);
+  void WatchRegistry(std::string spec, double ttl, double period);
+  std::thread watch_thread_;
+  std::mutex watch_mu_;
+  std::condition_variable watch_cv_;
+  bool watch_stop_ = false;
   std::string mode_ = "local";
   CompileOptions copt_;
   EngineEnv env_;
@@ -203,8 +226,12 @@ class QueryProxy {
   std::unique_ptr<ThreadPool> pool_;
 };
 
-// Load one shard (graph + indexes) from a reference-format directory.
+// Load one shard (graph + indexes) from a reference-format directory; opt selects the
+// node / edge tables and the global samplers (load_data_type / global_sampler_type).
 Status LoadShard(const std::string& data_path, int shard_idx, int shard_num, std::unique_ptr<Graph>* g,
-                 std::unique_ptr<IndexManager>* idx, int threads = 8);
+                 std::unique_ptr<IndexManager>* idx, int threads = 8, const LoadOptions& opt = LoadOptions());
+// LoadOptions from config keys load_data_type / global_sampler_type (aliases data_type /
+// sampler_type, the names initialize_embedded_graph uses)
+Status LoadOptionsFromConfig(const std::map<std::string, std::string>& config, LoadOptions* opt);
 
 }  // namespace euler

@@ -108,7 +108,50 @@ def GraphBuilder():
     return _engine_mod().GraphBuilder()
 
 
-def start_service(data_path, shard_idx, shard_num, registry="", port=0, threads=32, host="127.0.0.1"):
-    """Start a graph shard server in this process (reference ``euler.start``)."""
+class Module:
+    """What a shard server loads and which global samplers it builds (reference
+    ``euler/python/start_service.py:33-67``): data tables NODE / EDGE, samplers
+    NODE_SAMPLER / EDGE_SAMPLER, OR-ed together."""
+    NODE = 1
+    EDGE = 2
+    NODE_SAMPLER = 4
+    EDGE_SAMPLER = 8
+    DEFAULT_MODULE = NODE | NODE_SAMPLER
+
+    @staticmethod
+    def _two(module, a, b):
+        m = module & (a | b)
+        return {0: "none", a: "node", b: "edge", a | b: "all"}[m]
+
+    @classmethod
+    def to_load_data_type_string(cls, module):
+        return cls._two(int(module), cls.NODE, cls.EDGE)
+
+    @classmethod
+    def to_global_sampler_type_string(cls, module):
+        return cls._two(int(module), cls.NODE_SAMPLER, cls.EDGE_SAMPLER)
+
+
+def start_service(data_path, shard_idx, shard_num, registry="", port=0, threads=32, host="127.0.0.1",
+                  module=None, load_data_type=None, global_sampler_type=None, heartbeat_ms=1000):
+    """Start a graph shard server in this process.  ``module`` (Module flags) or the
+    explicit ``load_data_type`` / ``global_sampler_type`` strings ("none" / "node" /
+    "edge" / "all") select the loaded tables and global samplers (default: everything);
+    the registry entry is refreshed every ``heartbeat_ms`` (clients drop entries older
+    than their ``registry_ttl``)."""
+    if module is not None:
+        load_data_type = load_data_type or Module.to_load_data_type_string(module)
+        global_sampler_type = global_sampler_type or Module.to_global_sampler_type_string(module)
     return _engine_mod().GraphServer(data_path, int(shard_idx), int(shard_num), registry, int(port), int(threads),
-                                     host)
+                                     host, load_data_type or "all", global_sampler_type or "all", int(heartbeat_ms))
+
+
+def start(directory="", shard_idx=0, shard_num=1, zk_addr="", zk_path="", module=Module.DEFAULT_MODULE,
+          server_thread_num=None):
+    """Reference ``euler.start`` signature (``euler/python/start_service.py:70-80``): the
+    ZooKeeper path names the shared registry directory here."""
+    import multiprocessing
+
+    reg = zk_path or zk_addr
+    return start_service(directory, shard_idx, shard_num, reg, 0, int(server_thread_num or multiprocessing.cpu_count()),
+                         module=module)

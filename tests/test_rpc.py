@@ -125,3 +125,90 @@ def test_same_host_local_transport(cluster):
     assert out["local"][0] == out["tcp"][0] == [2, 4]
     assert out["local"][1] > 0 and out["local"][2] == 0
     assert out["tcp"][1] == 0 and out["tcp"][2] > 0
+
+
+def _serve(data, reg, shard, num, *extra):
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    return subprocess.Popen([sys.executable, "-m", "euler_amd.tools.service", "--data_path", data, "--shard_idx",
+                             str(shard), "--shard_num", str(num), "--registry", reg, "--threads", "2"] + list(extra),
+                            env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+
+
+def test_registry_liveness_sigkill():
+    """A SIGKILLed replica stops heartbeating: after registry_ttl its entry is ignored by
+    the registry listing and the client's registry watch removes it from the routing set,
+    so later queries never touch it (no RPC failures), with no Stop() / deregistration
+    (reference ZK ephemeral nodes + child watch, zk_server_monitor.cc:186-200)."""
+    import euler_amd._engine as E
+
+    data = tempfile.mkdtemp(prefix="euler_amd_live_data_")
+    convert_json(os.path.join(HERE, "data", "graph.json"), data, 1)
+    reg = tempfile.mkdtemp(prefix="euler_amd_live_reg_")
+    procs = [_serve(data, reg, 0, 1, "--heartbeat_ms", "150") for _ in range(2)]
+    try:
+        deadline = time.time() + 60
+        while time.time() < deadline and len(E.registry_list(reg, 1.0).get(0, [])) < 2:
+            time.sleep(0.1)
+        assert len(E.registry_list(reg, 1.0).get(0, [])) == 2
+        eng = ea.initialize_graph({"mode": "remote", "registry": reg, "shard_num": 1, "registry_ttl": 1.0,
+                                   "registry_refresh": 0.2, "num_retries": 3})
+        eng = ea.get_engine()
+        assert len(eng.endpoints()[0]) == 2
+        procs[0].kill()  # SIGKILL: no deregistration, the entry file stays
+        procs[0].wait(timeout=30)
+        time.sleep(2.0)
+        assert len([f for f in os.listdir(reg) if f.startswith("0#")]) == 2  # stale file still there
+        assert len(E.registry_list(reg, 1.0)[0]) == 1
+        assert len(E.registry_list(reg, 0.0)[0]) == 2  # ttl 0: every entry
+        assert len(eng.endpoints()[0]) == 1
+        before = E.stats()["rpc_failures"]
+        for _ in range(20):
+            ids, _, _ = ea.get_full_neighbor([1, 2], ["0", "1"])
+            assert ids.to_dense().tolist() == [[2, 4, 3], [3, 5, 0]]
+        assert E.stats()["rpc_failures"] == before, "queries were routed to the dead replica"
+        # a new replica joins and is picked up by the watch
+        procs.append(_serve(data, reg, 0, 1, "--heartbeat_ms", "150"))
+        deadline = time.time() + 60
+        while time.time() < deadline and len(eng.endpoints()[0]) < 2:
+            time.sleep(0.1)
+        assert len(eng.endpoints()[0]) == 2
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+                p.wait(timeout=30)
+
+
+def test_load_and_sampler_options(tmp_path):
+    """load_data_type / global_sampler_type (reference Module NODE / EDGE / NODE_SAMPLER /
+    EDGE_SAMPLER, start_service.py:33-80, graph.cc:39-70)."""
+    from euler_amd.ops.base import Module
+
+    data = str(tmp_path / "g")
+    convert_json(os.path.join(HERE, "data", "graph.json"), data, 1)
+    assert Module.to_load_data_type_string(Module.DEFAULT_MODULE) == "node"
+    assert Module.to_global_sampler_type_string(Module.DEFAULT_MODULE) == "node"
+    assert Module.to_load_data_type_string(Module.NODE | Module.EDGE) == "all"
+    assert Module.to_global_sampler_type_string(Module.EDGE_SAMPLER) == "edge"
+    ea.initialize_graph({"mode": "local", "data_path": data, "global_sampler_type": "edge"})
+    assert ea.sample_node(16, "-1").numel() == 0  # no node sampler built
+    assert ea.sample_edge(16, "-1").shape[0] == 16
+    ea.initialize_graph({"mode": "local", "data_path": data, "global_sampler_type": "node"})
+    assert ea.sample_node(16, "-1").numel() == 16
+    assert ea.sample_edge(16, "-1").numel() == 0
+    ea.initialize_graph({"mode": "local", "data_path": data, "load_data_type": "node"})
+    ids, _, _ = ea.get_full_neighbor([1], ["0"])
+    assert ids.to_dense().tolist() == [[2, 4]]  # adjacency lives with the nodes
+    with pytest.raises(Exception):
+        ea.initialize_graph({"mode": "local", "data_path": data, "load_data_type": "everything"})
+    # the server side: a NODE-only shard answers neighbour queries
+    reg = str(tmp_path / "reg")
+    os.makedirs(reg)
+    p = _serve(data, reg, 0, 1, "--module", str(Module.NODE | Module.NODE_SAMPLER))
+    try:
+        ea.initialize_shared_graph(reg, shard_num=1)
+        ids, _, _ = ea.get_full_neighbor([1], ["0"])
+        assert ids.to_dense().tolist() == [[2, 4]]
+    finally:
+        p.terminate()
+        p.wait(timeout=30)
