@@ -618,11 +618,13 @@ PYBIND11_MODULE(_engine, m) {
     }
     return out;
   });
-  m.def("compile_gql", [](const std::string& q, const std::string& mode, int shards, std::vector<std::string> nbr_idx) {
+  m.def("compile_gql", [](const std::string& q, const std::string& mode, int shards, std::vector<std::string> nbr_idx,
+                          bool fuse) {
     CompileOptions o;
     o.mode = mode == "local" ? CompileMode::kLocal : CompileMode::kDistribute;
     o.shard_num = shards;
     o.neighbor_indexes = nbr_idx;
+    o.fuse = fuse;
     std::shared_ptr<const DAGDef> d;
     Throw(Compiler::Get().Compile(q, o, &d));
     py::list nodes;
@@ -640,7 +642,7 @@ PYBIND11_MODULE(_engine, m) {
     }
     return nodes;
   }, py::arg("query"), py::arg("mode") = "local", py::arg("shard_num") = 1,
-     py::arg("neighbor_indexes") = std::vector<std::string>{});
+     py::arg("neighbor_indexes") = std::vector<std::string>{}, py::arg("fuse") = true);
   m.def(
       "registry_list",
       [](const std::string& spec, double ttl) {

@@ -42,6 +42,9 @@ struct CompileOptions {
   int shard_num = 1;
   // names of neighbor (hash_range) indexes: conditions on them stay on the shard
   std::vector<std::string> neighbor_indexes;
+  // fuse independent REMOTE nodes of a shard into one RPC (reference FusionAndShardRule,
+  // compiler.cc:92-162 / DAGDef::FusionNodes, dag_def.cc:128-203); EULER_GQL_FUSE=0 disables
+  bool fuse = true;
 };
 
 class Compiler {

@@ -12,6 +12,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <chrono>
 #include <set>
 
@@ -906,7 +907,17 @@ Status QueryProxy::Init(const std::map<std::string, std::string>& config) {
     env_.num_partitions = std::max<uint32_t>(1, meta_.partitions_num);
     env_.index_info = metas[0].index_info;
     FillWeightTables(metas);
-  } else if (mode_ == "remote" || mode_ == "graph_partition") {
+  } else if (mode_ == "graph_partition") {
+    // The reference's graph_partition mode (query_proxy.cc:35-60, optimizer.cc:235-454)
+    // macro-fuses every shard-executable op of a query into one sub-DAG that each shard
+    // runs on its own partition, with GP_* merges chaining the per-hop row orders.  Its
+    // multi-hop results are partition-local approximations; euler_amd serves sharded
+    // graphs with exact distribute mode, whose REMOTE fusion already costs one RPC per
+    // shard per hop.  Refuse instead of silently running distribute semantics.
+    return Status::Unimplemented(
+        "graph_partition mode is not supported: use mode=remote (distribute compiler with per-hop REMOTE "
+        "fusion; GP_* merge kernels are available as single ops via run_op)");
+  } else if (mode_ == "remote") {
     std::string reg = Cfg(config, "registry", Cfg(config, "zk_path", ""));
     if (reg.empty()) return Status::InvalidArgument("remote mode needs registry=<dir|memory:name>");
     auto r = Registry::Open(reg);
@@ -951,6 +962,10 @@ Status QueryProxy::Init(const std::map<std::string, std::string>& config) {
   env_.clients = clients_.get();
   copt_.mode = CompileMode::kDistribute;
   copt_.shard_num = env_.shard_num;
+  {
+    const char* f = std::getenv("EULER_GQL_FUSE");
+    copt_.fuse = !(f && f[0] == '0');
+  }
   copt_.neighbor_indexes.clear();
   for (auto& item : Split(env_.index_info, ",")) {
     auto p = Split(item, ":");

@@ -208,16 +208,24 @@ def get_node_type(nodes):
 
 
 # ----------------------------------------------------------------------------- neighbors
+def _ragged_slots(idx, k):
+    """(row, slot, source position) of the first k entries of every ragged row"""
+    idx = np.asarray(idx).reshape(-1, 2)
+    b = idx[:, 0].astype(np.int64)
+    m = np.clip(idx[:, 1].astype(np.int64) - b, 0, int(k))
+    rows = np.repeat(np.arange(len(b)), m)
+    slot = np.arange(int(m.sum())) - np.repeat(np.cumsum(m) - m, m)
+    return rows, slot, np.repeat(b, m) + slot
+
+
 def _dense_rows(idx, ids, w, t, n, k, default_node):
     out_id = np.full((n, k), np.uint64(default_node & 0xFFFFFFFFFFFFFFFF), dtype=np.uint64)
     out_w = np.zeros((n, k), np.float32)
     out_t = np.full((n, k), -1, np.int32)
-    for i in range(n):
-        b, e = idx[i]
-        m = min(k, e - b)
-        out_id[i, :m] = ids[b:b + m]
-        out_w[i, :m] = w[b:b + m]
-        out_t[i, :m] = t[b:b + m]
+    rows, slot, src = _ragged_slots(idx[:n], k)
+    out_id[rows, slot] = np.asarray(ids)[src]
+    out_w[rows, slot] = np.asarray(w)[src]
+    out_t[rows, slot] = np.asarray(t)[src]
     return _i64(out_id), _t(out_w), _t(out_t)
 
 
@@ -307,14 +315,51 @@ def sample_fanout(nodes, edge_types, counts, default_node=-1):
 
 def sample_fanout_with_feature(nodes, edge_types, count, default_node, dense_feature_names, dense_dimensions,
                                sparse_feature_names, sparse_default_values):
-    neighbors, weights, types = sample_fanout(nodes, edge_types, count, default_node)
-    dense = []
-    sparse = []
-    for hop in neighbors:
-        if dense_feature_names:
-            dense.extend(get_dense_feature(hop, dense_feature_names, dense_dimensions))
+    """Multi-hop sampling plus the features of every hop's nodes as ONE GQL query (the
+    reference's ``v(nodes).as(nb_0).sampleNB(...).as(nb_1)... .v_select(nb_i).values(...)``,
+    sample_fanout_with_feature_op.cc:43-69).  In remote mode the compiler fuses each hop's
+    sampleNB with the values() of the same frontier into one REMOTE per shard, so the
+    query costs one RPC per shard per hop (+1 for the leaf features)."""
+    dense_feature_names = list(dense_feature_names or [])
+    sparse_feature_names = list(sparse_feature_names or [])
+    names = ["dense_" + str(n) for n in dense_feature_names] + ["sparse_" + str(n) for n in sparse_feature_names]
+    ids = _u64(nodes)
+    L = len(count)
+    q = "v(nodes).as(nb_0)"
+    inputs = {"nodes": ids}
+    outs = []
+    for i in range(1, L + 1):
+        q += ".sampleNB(et_%d, c_%d, %d).as(nb_%d)" % (i, i, int(default_node), i)
+        inputs["et_%d" % i] = _et(edge_types[i - 1])
+        inputs["c_%d" % i] = np.asarray([int(count[i - 1])])
+        outs += ["nb_%d:%d" % (i, k) for k in range(4)]
+    if names:
+        keys = ["__f%d" % j for j in range(len(names))]
+        for k, nm in zip(keys, names):
+            inputs[k] = nm
+        for i in range(L + 1):
+            q += ".v_select(nb_%d).values(%s).as(fea_%d)" % (i, ", ".join(keys), i)
+            outs += ["fea_%d:%d" % (i, k) for k in range(2 * len(names))]
+    r = run_gql(q, inputs, outs)
+    neighbors = [torch.as_tensor(ids.view(np.int64))]
+    weights, types = [], []
+    n = len(ids)
+    for i in range(L):
+        c = int(count[i])
+        nb, w, t = _dense_rows(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3], n, c, int(default_node))
+        neighbors.append(nb.reshape(-1))
+        weights.append(w.reshape(-1))
+        types.append(t.reshape(-1))
+        n *= c
+    dense, sparse = [], []
+    base = 4 * L
+    nd = len(dense_feature_names)
+    for i in range(L + 1 if names else 0):
+        res = [(r[base + 2 * j], r[base + 2 * j + 1]) for j in range(len(names))]
+        base += 2 * len(names)
+        dense.extend(_dense_from_ragged(idx, vals, d) for (idx, vals), d in zip(res[:nd], dense_dimensions))
         if sparse_feature_names:
-            sparse.extend(get_sparse_feature(hop, sparse_feature_names, sparse_default_values))
+            sparse.extend(_sparse_list(res[nd:], sparse_default_values))
     return neighbors, weights, types, dense, sparse
 
 
@@ -429,10 +474,8 @@ def _feature_query(root, ids_key, ids, prefix, names):
 def _dense_from_ragged(idx, vals, dim):
     n = idx.shape[0]
     out = np.zeros((n, int(dim)), np.float32)
-    for i in range(n):
-        b, e = idx[i]
-        m = min(int(dim), e - b)
-        out[i, :m] = vals[b:b + m]
+    rows, slot, src = _ragged_slots(idx, dim)
+    out[rows, slot] = np.asarray(vals)[src]
     return _t(out)
 
 

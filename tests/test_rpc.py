@@ -212,3 +212,34 @@ def test_load_and_sampler_options(tmp_path):
     finally:
         p.terminate()
         p.wait(timeout=30)
+
+
+def test_fused_fanout_with_feature_one_rpc_per_shard_per_hop(cluster):
+    """sample_fanout_with_feature is one GQL query; the distribute compiler fuses each
+    hop's sampleNB with the frontier's values() into one REMOTE per shard (reference
+    FusionAndShardRule, compiler.cc:92-162), so 2 hops on 2 shards cost (2 + 1) x 2 = 6
+    RPCs (10 unfused).  Features returned for every hop match get_dense_feature."""
+    import json
+
+    data, reg = cluster
+    code = ("import euler_amd as ea, json, numpy as np, euler_amd._engine as E;"
+            "ea.initialize_graph({'mode':'remote','registry':%r,'shard_num':2});"
+            "E.reset_stats();"
+            "nb,w,t,dense,sp=ea.sample_fanout_with_feature([1,2,3],[['0','1'],['0','1']],[2,2],-1,['f3'],[2],[],[]);"
+            "calls=E.stats()['remote_calls'];"
+            "ok=all(np.allclose(d.numpy(), ea.get_dense_feature(h,['f3'],[2])[0].numpy()) for h,d in zip(nb,dense));"
+            "print(json.dumps([calls, [len(h) for h in nb], ok]))") % reg
+    out = {}
+    for fuse in ("1", "0"):
+        env = dict(os.environ, PYTHONPATH=ROOT, EULER_GQL_FUSE=fuse)
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        out[fuse] = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["1"][0] == 6 and out["0"][0] == 10, out
+    assert out["1"][1] == [3, 6, 12] and out["1"][2] and out["0"][2]
+
+
+def test_graph_partition_mode_rejected(cluster):
+    data, reg = cluster
+    with pytest.raises(Exception, match="graph_partition mode is not supported"):
+        ea.initialize_graph({"mode": "graph_partition", "registry": reg, "shard_num": 2})
