@@ -119,7 +119,15 @@ class GCNConv(Conv):
 
 
 class SAGEConv(Conv):
-    """self_fc(x) + neigh_fc(mean_j x_j) (reference sage_conv.py:26-44)."""
+    """self_fc(x) + neigh_fc(mean_j x_j) (reference sage_conv.py:26-44).
+
+    :meth:`fused_relu` is the fixed-fanout GPU form the GNN loops dispatch to when a block
+    carries a dense neighbour matrix (SageDataFlow): gather + mean + both linears + ReLU
+    in the K3 kernel (``sage_fwd``, csrc/hip/sage.hip: LDS-staged gather, bf16 MFMA,
+    fp32 accumulation), backward through ``sage_bwd_scatter`` — no edge list, no
+    segment reduce, no separate GEMMs."""
+
+    fused_calls = 0  # class-wide counter of fused dispatches (tests / tracing)
 
     def __init__(self, dim, **kwargs):
         super().__init__("mean")
@@ -131,6 +139,26 @@ class SAGEConv(Conv):
         xs = x[1] if x[1] is not None else x[0]
         agg = self.aggregate(xs, edge_index, size)
         return self.self_fc(x[0]) + self.neigh_fc(agg)
+
+    def can_fuse(self, x_all, block) -> bool:
+        import os
+
+        if block.nbr is None or not x_all.is_cuda or os.environ.get("EULER_AMD_FUSED_CONV", "1") == "0":
+            return False
+        if self.self_fc.has_uninitialized_params() or self.neigh_fc.has_uninitialized_params():
+            return False  # the first (materialising) call takes the generic path
+        d = x_all.shape[1]
+        return d % 16 == 0 and d <= 512
+
+    def fused_relu(self, x_all, block):
+        """relu(self_fc(x_all[res_n_id]) + neigh_fc(mean_j x_all[nbr[:, j]])) in one kernel."""
+        from euler_amd.ops.sage_ops import sage_layer
+
+        SAGEConv.fused_calls += 1
+        w = torch.cat([self.self_fc.weight, self.neigh_fc.weight], 1)
+        out = sage_layer(x_all.to(torch.bfloat16), block.res_n_id.to(torch.int32), block.nbr, w, None,
+                         include_self=False, relu=True, disjoint=False)
+        return out.to(x_all.dtype)
 
 
 class GATConv(Conv):

@@ -32,22 +32,26 @@ def unique_with_inverse(x: torch.Tensor):
 
 
 class Block:
-    __slots__ = ("n_id", "res_n_id", "e_id", "edge_index", "size", "_euler_cache")
+    """One hop of a DataFlow.  ``nbr`` (fixed-fanout flows only): int32 [n_target, F (+1)]
+    positions of every target's sampled neighbours (and its self loop) in ``n_id`` —
+    the edge list in the dense form the fused SAGE kernel consumes (K3, sage_ops)."""
+    __slots__ = ("n_id", "res_n_id", "e_id", "edge_index", "size", "nbr", "_euler_cache")
 
-    def __init__(self, n_id, res_n_id, e_id, edge_index, size):
+    def __init__(self, n_id, res_n_id, e_id, edge_index, size, nbr=None):
         self.n_id = n_id
         self.res_n_id = res_n_id
         self.e_id = e_id
         self.edge_index = edge_index
         self.size = size
+        self.nbr = nbr
 
     def to(self, device, non_blocking=True):
         mv = lambda t: None if t is None else t.to(device, non_blocking=non_blocking)  # noqa: E731
-        return Block(mv(self.n_id), mv(self.res_n_id), mv(self.e_id), mv(self.edge_index), self.size)
+        return Block(mv(self.n_id), mv(self.res_n_id), mv(self.e_id), mv(self.edge_index), self.size, mv(self.nbr))
 
     def pin_memory(self):
         pm = lambda t: None if t is None else t.pin_memory()  # noqa: E731
-        return Block(pm(self.n_id), pm(self.res_n_id), pm(self.e_id), pm(self.edge_index), self.size)
+        return Block(pm(self.n_id), pm(self.res_n_id), pm(self.e_id), pm(self.edge_index), self.size, pm(self.nbr))
 
 
 class DataFlow:
@@ -154,12 +158,28 @@ class SageDataFlow(UniqueDataFlow):
         n_id = torch.as_tensor(n_id).reshape(-1).long()
         hops = ge.sage_flow(n_id, self.metapath, self.fanouts, self.max_id + 1, self.add_self_loops)
         if hops is None:  # remote graph: per-hop GQL sampling + unique below
-            return super().produce_subgraph(n_id)
-        # the engine built every hop in one native call (sampling, unique, edge index)
-        df = DataFlow(n_id)
-        for new_n_id, res_n_id, edge_index in hops:
-            df.append(new_n_id, res_n_id, None, edge_index)
+            df = super().produce_subgraph(n_id)
+        else:
+            # the engine built every hop in one native call (sampling, unique, edge index)
+            df = DataFlow(n_id)
+            for new_n_id, res_n_id, edge_index in hops:
+                df.append(new_n_id, res_n_id, None, edge_index)
+        self._attach_nbr(df)
         return df
+
+    def _attach_nbr(self, df):
+        """Both flows emit each hop's edges target-major (F sampled edges per target, then
+        the n self loops): that is the dense [n, F (+1)] neighbour matrix, row-major."""
+        for b, f in zip(df.blocks, self.fanouts):
+            n, f = int(b.size[0]), int(f)
+            e = int(b.edge_index.shape[1])
+            if e != n * f + (n if self.add_self_loops else 0):
+                continue
+            src = b.edge_index[1]
+            nbr = src[: n * f].view(n, f)
+            if self.add_self_loops:
+                nbr = torch.cat([nbr, src[n * f:].view(n, 1)], 1)
+            b.nbr = nbr.to(torch.int32).contiguous()
 
     def get_neighbors(self, n_id):
         neighbors, srcs = [], []

@@ -146,6 +146,10 @@ class BaseGNNNet(_GNNBase):
     def forward(self, n_id):
         data_flow, x = self._inputs(n_id)
         for conv, block in zip(self.convs, data_flow):
+            if not self.whole_graph and block.e_id is None and getattr(conv, "can_fuse", None) and \
+                    conv.can_fuse(x, block):
+                x = conv.fused_relu(x, block)  # fixed-fanout block: fused K3 kernel on the GPU
+                continue
             edge_attr = None if block.e_id is None else self.get_edge_attr(block)
             x_src = mp_ops.gather(x, block.res_n_id)
             x_dst = None if self.whole_graph else x

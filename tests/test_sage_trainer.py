@@ -287,3 +287,19 @@ def test_estimator_device_graph_gpu(tmp_path, monkeypatch):
     assert r1["step"] == 40 and math.isfinite(r1["loss"])
     r2 = _run_graphsage(tmp_path, "cuda", 60)
     assert r2["step"] == 60 and r2["loss"] < 0.7
+
+
+@pytest.mark.gpu
+def test_device_path_tracks_engine_path(tmp_path, monkeypatch):
+    """The same SupervisedGraphSage / PPI-schema run through the estimator on the engine
+    path (CPU sampling + autograd on the GPU) and on the device path (fused kernels on an
+    HBM copy of the graph): after 150 steps both reach the same loss level."""
+    monkeypatch.chdir(tmp_path)
+    from euler_amd.tools.runner import main
+
+    base = ["--dataset", "ppi", "--scale", "0.05", "--batch_size", "256", "--total_step", "150", "--log_steps",
+            "150", "--device", "cuda", "--seed", "3", "--fanouts", "5", "3", "--learning_rate", "0.01"]
+    eng = main(base + ["--model_dir", str(tmp_path / "eng")], model="graphsage")
+    dev = main(base + ["--model_dir", str(tmp_path / "dev"), "--device_graph"], model="graphsage")
+    assert math.isfinite(eng["loss"]) and math.isfinite(dev["loss"])
+    assert abs(dev["loss"] - eng["loss"]) < 0.12 * eng["loss"], (eng["loss"], dev["loss"])

@@ -56,6 +56,14 @@ for st in "${S[@]}"; do
     pmc)
       PASSES="FETCH_SIZE|TCC_HIT_sum TCC_MISS_sum|SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD|SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE|SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS" \
         run pmc 600 bash tools/pmc_passes.sh tree "$PWD/tools/tree_kernels.py" --reps 10 ;;
+    ppi_device)
+      run ppi_device 600 python -u examples/run_graphsage.py --dataset ppi --device_graph --device cuda \
+          --batch_size 512 --total_step 3000 --log_steps 500 --model_dir /tmp/ppi_dev --fanouts 10 10 \
+          --learning_rate 0.01 ;;
+    ppi_device_b32)
+      run ppi_device_b32 600 python -u examples/run_graphsage.py --dataset ppi --device_graph --device cuda \
+          --batch_size 32 --total_step 3000 --log_steps 500 --model_dir /tmp/ppi_dev32 --fanouts 10 10 \
+          --learning_rate 0.01 ;;
     kernels_full)
       run tree_kernels_full 300 python -u tools/tree_kernels.py --num-nodes 100000000 ;;
     kernels_sizes)
