@@ -82,7 +82,7 @@ def _pybind_includes():
 # ----------------------------------------------------------------------------
 # C++ engine (CPU)
 # ----------------------------------------------------------------------------
-ENGINE_DIRS = ["common", "graph", "index", "framework", "gql", "ops", "rpc", "bindings"]
+ENGINE_DIRS = ["common", "graph", "index", "framework", "gql", "ops", "rpc", "pipeline", "bindings"]
 
 
 def engine_sources():

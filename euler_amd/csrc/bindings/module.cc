@@ -13,6 +13,7 @@
 #include "gql/gql.h"
 #include "graph/graph.h"
 #include "index/index.h"
+#include "pipeline/pipeline.h"
 #include "rpc/rpc.h"
 
 namespace py = pybind11;
@@ -518,6 +519,66 @@ class PyServer {
   std::unique_ptr<GraphServer> server_;
 };
 
+// Native batch pipeline (pipeline/pipeline.h) over an engine's in-process graph; the
+// slot buffers are caller-owned (pinned torch tensors), passed as raw addresses.
+SageBatchSpec MakeSpec(const Graph& g, int batch, int node_type, const std::vector<std::vector<int32_t>>& etypes,
+                       const std::vector<int>& fanouts, int64_t def, bool self_loops,
+                       const std::vector<std::string>& dense, const std::vector<int>& dims, const std::string& label,
+                       int label_dim) {
+  SageBatchSpec s;
+  s.batch = batch;
+  s.node_type = node_type;
+  s.etypes = etypes;
+  s.fanouts = fanouts;
+  s.default_node = def;
+  s.self_loops = self_loops;
+  auto dense_idx = [&](const std::string& n) {
+    const FeatureInfo* fi = g.meta().NodeFeature(n);
+    if (!fi || fi->type != kDense) throw std::runtime_error("no dense node feature named " + n);
+    return fi->idx;
+  };
+  for (auto& n : dense) s.dense_idx.push_back(dense_idx(n));
+  s.dense_dims = dims;
+  if (!label.empty()) s.label_idx = dense_idx(label);
+  s.label_dim = label.empty() ? 0 : label_dim;
+  return s;
+}
+
+class PySagePipeline {
+ public:
+  PySagePipeline(std::shared_ptr<Engine> e, int batch, int node_type, std::vector<std::vector<int32_t>> etypes,
+                 std::vector<int> fanouts, int64_t def, bool self_loops, std::vector<std::string> dense,
+                 std::vector<int> dims, std::string label, int label_dim, std::vector<uintptr_t> ints,
+                 std::vector<uintptr_t> floats, int workers, uint64_t seed)
+      : e_(std::move(e)) {
+    const Graph& g = e_->LocalGraph();
+    SageBatchSpec spec = MakeSpec(g, batch, node_type, etypes, fanouts, def, self_loops, dense, dims, label, label_dim);
+    std::vector<int64_t*> ip;
+    std::vector<float*> fp;
+    for (auto a : ints) ip.push_back(reinterpret_cast<int64_t*>(a));
+    for (auto a : floats) fp.push_back(reinterpret_cast<float*>(a));
+    p_.reset(new SagePipeline(&g, spec, ip, fp, workers, seed));
+  }
+  ~PySagePipeline() {
+    py::gil_scoped_release nogil;
+    p_.reset();
+  }
+  int Next() {
+    py::gil_scoped_release nogil;
+    return p_->Next();
+  }
+  void Release(int slot) { p_->Release(slot); }
+  void Stop() {
+    py::gil_scoped_release nogil;
+    p_->Stop();
+  }
+  int64_t batches() const { return p_->batches(); }
+
+ private:
+  std::shared_ptr<Engine> e_;
+  std::unique_ptr<SagePipeline> p_;
+};
+
 }  // namespace
 
 PYBIND11_MODULE(_engine, m) {
@@ -544,6 +605,43 @@ PYBIND11_MODULE(_engine, m) {
       .def("export_csr", &Engine::ExportCsr)
       .def("endpoints", [](Engine& e) { return e.Endpoints(); })
       .def("export_nodes", &Engine::ExportNodes);
+
+  py::class_<PySagePipeline>(m, "SagePipeline")
+      .def(py::init<std::shared_ptr<Engine>, int, int, std::vector<std::vector<int32_t>>, std::vector<int>, int64_t,
+                    bool, std::vector<std::string>, std::vector<int>, std::string, int, std::vector<uintptr_t>,
+                    std::vector<uintptr_t>, int, uint64_t>(),
+           py::arg("engine"), py::arg("batch"), py::arg("node_type"), py::arg("edge_types"), py::arg("fanouts"),
+           py::arg("default_node"), py::arg("self_loops"), py::arg("dense_features"), py::arg("dense_dims"),
+           py::arg("label"), py::arg("label_dim"), py::arg("ints"), py::arg("floats"), py::arg("workers"),
+           py::arg("seed"))
+      .def("next", &PySagePipeline::Next)
+      .def("release", &PySagePipeline::Release)
+      .def("stop", &PySagePipeline::Stop)
+      .def_property_readonly("batches", &PySagePipeline::batches);
+  m.def(
+      "sage_pipeline_layout",
+      [](int batch, std::vector<int> fanouts, bool self_loops, std::vector<int> dims, int label_dim) {
+        SageBatchSpec s;
+        s.batch = batch;
+        s.fanouts = fanouts;
+        s.self_loops = self_loops;
+        s.dense_dims = dims;
+        s.label_dim = label_dim;
+        SageSlotLayout l = SageSlotLayout::Make(s);
+        py::dict d;
+        d["ints"] = l.ints;
+        d["floats"] = l.floats;
+        d["feat_dim"] = l.feat_dim;
+        d["off_labels"] = l.off_labels;
+        d["cap"] = l.cap;
+        d["ecap"] = l.ecap;
+        d["off_nid"] = l.off_nid;
+        d["off_res"] = l.off_res;
+        d["off_src"] = l.off_src;
+        d["off_nbr"] = l.off_nbr;
+        return d;
+      },
+      py::arg("batch"), py::arg("fanouts"), py::arg("self_loops"), py::arg("dense_dims"), py::arg("label_dim"));
 
   py::class_<PyBuilder>(m, "GraphBuilder")
       .def(py::init<>())

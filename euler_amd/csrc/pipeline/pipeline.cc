@@ -1,0 +1,233 @@
+// Native SageDataFlow + feature batch pipeline (see pipeline.h).
+#include "pipeline/pipeline.h"
+
+#include <string.h>
+
+#include <algorithm>
+
+namespace euler {
+
+namespace {
+
+// tf.unique (first-occurrence order): open addressing, linear probing
+void UniqueInto(const int64_t* xs, int64_t n, int64_t* uniq, int64_t* nu, int64_t* inv,
+                std::vector<std::pair<int64_t, int64_t>>* table) {
+  uint64_t cap = 16;
+  while (cap < static_cast<uint64_t>(2 * n)) cap <<= 1;
+  const uint64_t mask = cap - 1;
+  table->assign(cap, {0, -1});
+  int64_t k = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t v = xs[i];
+    const uint64_t z = static_cast<uint64_t>(v) * 0x9e3779b97f4a7c15ull;
+    uint64_t h = (z ^ (z >> 29)) & mask;
+    for (;;) {
+      auto& c = (*table)[h];
+      if (c.second < 0) {
+        c = {v, k};
+        uniq[k++] = v;
+        break;
+      }
+      if (c.first == v) break;
+      h = (h + 1) & mask;
+    }
+    inv[i] = (*table)[h].second;
+  }
+  *nu = k;
+}
+
+}  // namespace
+
+SageSlotLayout SageSlotLayout::Make(const SageBatchSpec& s) {
+  SageSlotLayout l;
+  const int L = static_cast<int>(s.fanouts.size());
+  l.cap.assign(L + 1, 0);
+  l.ecap.assign(L + 1, 0);
+  l.off_nid.assign(L + 1, 0);
+  l.off_res.assign(L + 1, 0);
+  l.off_src.assign(L + 1, 0);
+  l.off_nbr.assign(L + 1, 0);
+  l.cap[0] = s.batch;
+  int64_t off = 16 + s.batch;
+  for (int h = 1; h <= L; ++h) {
+    const int64_t f = s.fanouts[h - 1];
+    l.cap[h] = l.cap[h - 1] * (f + 1);
+    l.ecap[h] = l.cap[h - 1] * f + (s.self_loops ? l.cap[h - 1] : 0);
+    l.off_nid[h] = off;
+    off += l.cap[h];
+    l.off_res[h] = off;
+    off += l.cap[h - 1];
+    l.off_src[h] = off;
+    off += 2 * l.ecap[h];
+    l.off_nbr[h] = off;
+    off += (l.cap[h - 1] * (f + (s.self_loops ? 1 : 0)) + 1) / 2;
+  }
+  l.ints = off;
+  for (int d : s.dense_dims) l.feat_dim += d;
+  l.off_labels = l.cap[L] * l.feat_dim;
+  l.floats = l.off_labels + static_cast<int64_t>(s.batch) * s.label_dim;
+  return l;
+}
+
+SagePipeline::SagePipeline(const Graph* g, SageBatchSpec spec, std::vector<int64_t*> ints, std::vector<float*> floats,
+                           int workers, uint64_t seed)
+    : g_(g), spec_(std::move(spec)), ints_(std::move(ints)), floats_(std::move(floats)), seed_(seed) {
+  lay_ = SageSlotLayout::Make(spec_);
+  if (ints_.size() != floats_.size() || ints_.empty()) EULER_THROW("SagePipeline: one int and one float buffer per slot");
+  if (spec_.etypes.size() != spec_.fanouts.size() || spec_.fanouts.empty() || spec_.fanouts.size() > 7)
+    EULER_THROW("SagePipeline: 1..7 hops, one edge-type list per fanout");
+  if (spec_.dense_idx.size() != spec_.dense_dims.size()) EULER_THROW("SagePipeline: one dimension per feature");
+  for (int i = 0; i < static_cast<int>(ints_.size()); ++i) free_.push_back(i);
+  const int nw = std::max(1, workers);
+  for (int w = 0; w < nw; ++w) threads_.emplace_back([this] { Worker(); });
+}
+
+SagePipeline::~SagePipeline() { Stop(); }
+
+void SagePipeline::Stop() {
+  {
+    std::lock_guard<std::mutex> l(mu_);
+    if (stop_ && threads_.empty()) return;
+    stop_ = true;
+  }
+  cv_free_.notify_all();
+  cv_ready_.notify_all();
+  for (auto& t : threads_)
+    if (t.joinable()) t.join();
+  threads_.clear();
+}
+
+void SagePipeline::Worker() {
+  for (;;) {
+    int slot;
+    uint64_t seq;
+    {
+      std::unique_lock<std::mutex> l(mu_);
+      cv_free_.wait(l, [&] { return stop_ || !free_.empty(); });
+      if (stop_) return;
+      slot = free_.back();
+      free_.pop_back();
+      seq = issue_seq_++;
+    }
+    Fill(slot, seq);
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      ready_[seq] = slot;
+    }
+    cv_ready_.notify_all();
+  }
+}
+
+int SagePipeline::Next() {
+  std::unique_lock<std::mutex> l(mu_);
+  cv_ready_.wait(l, [&] { return stop_ || ready_.count(next_seq_); });
+  if (stop_) return -1;
+  auto it = ready_.find(next_seq_);
+  const int slot = it->second;
+  ready_.erase(it);
+  ++next_seq_;
+  return slot;
+}
+
+void SagePipeline::Release(int slot) {
+  {
+    std::lock_guard<std::mutex> l(mu_);
+    free_.push_back(slot);
+  }
+  cv_free_.notify_one();
+}
+
+void SagePipeline::Fill(int slot, uint64_t seq) {
+  const Graph& g = *g_;
+  const SageBatchSpec& s = spec_;
+  const SageSlotLayout& lay = lay_;
+  int64_t* I = ints_[slot];
+  float* Fp = floats_[slot];
+  const int L = static_cast<int>(s.fanouts.size());
+  Rng rng(seed_, seq);
+  // roots
+  std::vector<uint64_t> roots;
+  g.SampleNode(s.node_type, s.batch, rng, &roots);
+  int64_t* lvl0 = I + 16;
+  for (int i = 0; i < s.batch; ++i)
+    lvl0[i] = i < static_cast<int>(roots.size()) ? static_cast<int64_t>(roots[i]) : s.default_node;
+  I[0] = L;
+  I[1] = s.batch;
+  // hops
+  std::vector<int64_t> cat, inv;
+  std::vector<IdWeightType> tmp;
+  std::vector<std::pair<int64_t, int64_t>> table;
+  const int64_t* cur = lvl0;
+  int64_t n = s.batch;
+  for (int h = 1; h <= L; ++h) {
+    const int k = s.fanouts[h - 1];
+    cat.resize(static_cast<size_t>(n * k + n));
+    inv.resize(cat.size());
+    for (int64_t i = 0; i < n; ++i) {
+      g.SampleNeighbor(g.Row(static_cast<uint64_t>(cur[i])), s.etypes[h - 1], k, true, rng, &tmp);
+      for (int j = 0; j < k; ++j)
+        cat[i * k + j] = j < static_cast<int>(tmp.size()) ? static_cast<int64_t>(tmp[j].id) : s.default_node;
+    }
+    std::copy(cur, cur + n, cat.begin() + n * k);
+    int64_t* nid = I + lay.off_nid[h];
+    int64_t nu = 0;
+    UniqueInto(cat.data(), static_cast<int64_t>(cat.size()), nid, &nu, inv.data(), &table);
+    int64_t* res = I + lay.off_res[h];
+    std::copy(inv.end() - n, inv.end(), res);
+    const int64_t e = s.self_loops ? n * k + n : n * k;
+    int64_t* src = I + lay.off_src[h];
+    int64_t* dst = src + e;  // packed behind src: [2, e] is contiguous
+    for (int64_t i = 0; i < n * k; ++i) src[i] = i / k;
+    if (s.self_loops)
+      for (int64_t i = 0; i < n; ++i) src[n * k + i] = i;
+    std::copy(inv.begin(), inv.begin() + e, dst);
+    // dense neighbour matrix (int32, self loop last) for the fused SAGE kernel
+    int32_t* nb = reinterpret_cast<int32_t*>(I + lay.off_nbr[h]);
+    const int w = k + (s.self_loops ? 1 : 0);
+    for (int64_t i = 0; i < n; ++i) {
+      for (int j = 0; j < k; ++j) nb[i * w + j] = static_cast<int32_t>(inv[i * k + j]);
+      if (s.self_loops) nb[i * w + k] = static_cast<int32_t>(inv[n * k + i]);
+    }
+    I[1 + h] = nu;
+    I[8 + h] = e;
+    cur = nid;
+    n = nu;
+  }
+  // dense input features of the outermost node set, row-major [n][feat_dim]
+  const int64_t fd = lay.feat_dim;
+  if (fd > 0) {
+    std::vector<const Column<float>*> cols;
+    for (int idx : s.dense_idx) cols.push_back(g.NodeDense(idx));
+    for (int64_t i = 0; i < n; ++i) {
+      const int64_t r = g.Row(static_cast<uint64_t>(cur[i]));
+      float* o = Fp + i * fd;
+      int64_t c0 = 0;
+      for (size_t f = 0; f < cols.size(); ++f) {
+        const int64_t dim = s.dense_dims[f];
+        const float* p = nullptr;
+        int64_t m = 0;
+        if (cols[f] && r >= 0) cols[f]->Get(r, &p, &m);
+        m = std::min(m, dim);
+        if (m > 0) memcpy(o + c0, p, m * sizeof(float));
+        if (m < dim) memset(o + c0 + m, 0, (dim - m) * sizeof(float));
+        c0 += dim;
+      }
+    }
+  }
+  // labels of the roots
+  if (s.label_dim > 0) {
+    const Column<float>* lc = s.label_idx >= 0 ? g.NodeDense(s.label_idx) : nullptr;
+    float* o = Fp + lay.off_labels;
+    for (int i = 0; i < s.batch; ++i) {
+      const int64_t r = g.Row(static_cast<uint64_t>(lvl0[i]));
+      const float* p = nullptr;
+      int64_t m = 0;
+      if (lc && r >= 0) lc->Get(r, &p, &m);
+      m = std::min<int64_t>(m, s.label_dim);
+      if (m > 0) memcpy(o + i * s.label_dim, p, m * sizeof(float));
+      if (m < s.label_dim) memset(o + i * s.label_dim + m, 0, (s.label_dim - m) * sizeof(float));
+    }
+  }
+}
+
+}  // namespace euler

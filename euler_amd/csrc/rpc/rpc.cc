@@ -533,10 +533,16 @@ Status GraphServer::Start() {
     EULER_RETURN_IF_ERROR(registry_->Register(shard_idx_, endpoint(), meta));
     if (opt_.heartbeat_ms > 0) {
       heartbeat_thread_ = std::thread([this, meta] {
-        std::unique_lock<std::mutex> l(hb_mu_);
-        while (running_.load()) {
-          hb_cv_.wait_for(l, std::chrono::milliseconds(opt_.heartbeat_ms));
-          if (!running_.load()) break;
+        for (;;) {
+          {
+            std::unique_lock<std::mutex> l(hb_mu_);
+            // system_clock deadline: pthread_cond_timedwait (steady-clock waits use
+            // pthread_cond_clockwait, which gcc-11's TSAN does not intercept)
+            hb_cv_.wait_until(l, std::chrono::system_clock::now() + std::chrono::milliseconds(opt_.heartbeat_ms),
+                              [this] { return !running_.load(); });
+            if (!running_.load()) return;
+          }
+          // registry I/O outside the lock
           const Status st = registry_->Heartbeat(shard_idx_, endpoint());
           if (st.code() == Code::NOT_FOUND) registry_->Register(shard_idx_, endpoint(), meta);  // re-register
         }
@@ -549,10 +555,8 @@ Status GraphServer::Start() {
 
 void GraphServer::Stop() {
   if (!running_.exchange(false)) return;
-  {
-    std::lock_guard<std::mutex> l(hb_mu_);
-    hb_cv_.notify_all();
-  }
+  { std::lock_guard<std::mutex> l(hb_mu_); }  // the heartbeat thread sees running_ == false
+  hb_cv_.notify_all();
   if (heartbeat_thread_.joinable()) heartbeat_thread_.join();
   if (registry_) registry_->Deregister(shard_idx_, endpoint());
   shutdown(listen_fd_, SHUT_RDWR);
@@ -842,10 +846,14 @@ Status LoadOptionsFromConfig(const std::map<std::string, std::string>& config, L
 // server that stopped heartbeating is no longer routed to and a new replica is picked up
 void QueryProxy::WatchRegistry(std::string spec, double ttl, double period) {
   std::unique_ptr<Registry> r = Registry::Open(spec);
-  std::unique_lock<std::mutex> l(watch_mu_);
-  while (!watch_stop_) {
-    watch_cv_.wait_for(l, std::chrono::milliseconds(static_cast<int64_t>(period * 1000)));
-    if (watch_stop_) break;
+  for (;;) {
+    {
+      std::unique_lock<std::mutex> l(watch_mu_);
+      watch_cv_.wait_until(l, std::chrono::system_clock::now() +
+                                  std::chrono::milliseconds(static_cast<int64_t>(period * 1000)),
+                           [this] { return watch_stop_; });
+      if (watch_stop_) return;
+    }
     std::map<int, std::vector<std::pair<Endpoint, ShardMeta>>> listing;
     if (!r->List(&listing, ttl).ok()) continue;
     auto* rc = static_cast<RpcClients*>(clients_.get());
@@ -866,8 +874,8 @@ QueryProxy::~QueryProxy() {
   {
     std::lock_guard<std::mutex> l(watch_mu_);
     watch_stop_ = true;
-    watch_cv_.notify_all();
   }
+  watch_cv_.notify_all();
   if (watch_thread_.joinable()) watch_thread_.join();
 }
 

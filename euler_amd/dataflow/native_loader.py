@@ -1,0 +1,160 @@
+"""Native mini-batch pipeline for the engine (CPU-sampling) GraphSAGE path.
+
+C++ worker threads (``_engine.SagePipeline``, csrc/pipeline/pipeline.cc; no GIL) build
+complete batches — roots, every SageDataFlow hop (sampling, unique, edge list), the
+outermost node set's dense input features and the roots' labels — into pinned slot
+buffers that are allocated once and reused.  The consumer side here only wraps a ready
+slot in tensor views, issues the H2D copies on a side stream (``non_blocking``), makes
+the compute stream wait on that copy's event, and returns the slot to the workers once
+the copy has completed (event polled, never a host sync on the compute stream).  Slots:
+``workers + 3`` by default (every worker filling one, two copies in flight, one being
+handed out).
+
+Reference mechanics replaced: the reference builds the same batch inside the TF graph
+with one GQL op per hop plus one per feature (tf_euler/kernels/
+sample_fanout_with_feature_op.cc:43-69, get_dense_feature_op.cc:89-116) serially with
+the step; the round-1 Python prefetcher called ``pin_memory()`` on every batch.
+
+Batch b is drawn from the Philox stream (seed, b) and delivered in order, so the batch
+stream is reproducible for any worker count.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from euler_amd.dataflow.dataflows import Block, DataFlow
+from euler_amd.mp_utils.models import Prepared
+from euler_amd.ops.base import get_engine
+
+__all__ = ["NativeSageLoader", "native_spec"]
+
+
+def _names(x):
+    if x is None:
+        return []
+    return [x] if isinstance(x, str) else list(x)
+
+
+def native_spec(model, params):
+    """(flow, dense names, dims, label, label_dim, node_type) for models the native
+    pipeline serves (SupervisedGNN with a SageDataFlow); None otherwise."""
+    from euler_amd.dataflow.dataflows import SageDataFlow
+
+    gnn = getattr(model, "gnn", None)
+    flow = getattr(gnn, "sampler", None)
+    if not isinstance(flow, SageDataFlow) or not hasattr(model, "label_idx"):
+        return None
+    names, dims = _names(getattr(gnn, "feature_idx", None)), getattr(gnn, "feature_dim", None)
+    dims = [int(dims)] * len(names) if isinstance(dims, int) else [int(d) for d in (dims or [])]
+    if not names or len(names) != len(dims):
+        return None
+    return flow, names, dims, model.label_idx, int(model.label_dim), params.get("train_node_type", -1)
+
+
+class NativeSageLoader:
+    def __init__(self, flow, dense_names, dense_dims, label, label_dim, batch_size, node_type, device, workers=8,
+                 slots=None, seed=0):
+        import euler_amd._engine as E
+        import euler_amd.ops.graph_api as ge
+
+        eng = get_engine()
+        if eng.meta()["mode"] != "local":
+            raise ValueError("the native pipeline needs the graph in this process (local mode)")
+        self.device = torch.device(device)
+        self.cuda = self.device.type == "cuda"
+        self.B = int(batch_size)
+        self.fanouts = [int(f) for f in flow.fanouts]
+        self.self_loops = bool(flow.add_self_loops)
+        self.label_dim = int(label_dim)
+        ets = [[int(x) for x in np.asarray(ge.get_edge_type_id(m)).reshape(-1) if int(x) >= 0] if m is not None else []
+               for m in flow.metapath]
+        nt = -1 if node_type in (None, -1, "-1") else int(np.asarray(ge.get_node_type_id(node_type)).reshape(-1)[0])
+        self.lay = E.sage_pipeline_layout(self.B, self.fanouts, self.self_loops, [int(d) for d in dense_dims],
+                                          self.label_dim)
+        n_slots = int(slots or (int(workers) + 3))
+        pin = self.cuda
+        self.ints = [torch.zeros(self.lay["ints"], dtype=torch.int64, pin_memory=pin) for _ in range(n_slots)]
+        self.floats = [torch.zeros(max(1, self.lay["floats"]), dtype=torch.float32, pin_memory=pin)
+                       for _ in range(n_slots)]
+        self.pipe = E.SagePipeline(eng, self.B, nt, ets, self.fanouts, int(flow.max_id) + 1, self.self_loops,
+                                   ["dense_" + str(nm) for nm in dense_names], [int(d) for d in dense_dims],
+                                   ("dense_" + str(label)) if label else "",
+                                   self.label_dim, [t.data_ptr() for t in self.ints],
+                                   [t.data_ptr() for t in self.floats], int(workers), int(seed))
+        self.stream = torch.cuda.Stream(device=self.device) if self.cuda else None
+        self._inflight = []  # (slot, event) copies not yet known complete
+
+    # ------------------------------------------------------------------ consumer
+    def _recycle(self, block=False):
+        keep = []
+        for slot, ev in self._inflight:
+            if ev is None or ev.query() or block:
+                if ev is not None and block:
+                    ev.synchronize()
+                self.pipe.release(slot)
+            else:
+                keep.append((slot, ev))
+        self._inflight = keep
+
+    def _extent(self, slot):
+        """(header sizes, used int64 prefix length) of a filled slot"""
+        I, lay = self.ints[slot], self.lay
+        hdr = I[:16].tolist()
+        L = int(hdr[0])
+        n = [int(hdr[1 + h]) for h in range(L + 1)]
+        e = [0] + [int(hdr[8 + h]) for h in range(1, L + 1)]
+        f = self.fanouts[L - 1] + (1 if self.self_loops else 0)
+        return L, n, e, int(lay["off_nbr"][L]) + (n[L - 1] * f + 1) // 2
+
+    def get(self):
+        """Prepared(inputs=roots, label, embed_in=Prepared(flow, x)) on the device.  Three
+        H2D copies per batch (used int prefix, feature rows, labels), device-side views."""
+        self._recycle()
+        slot = self.pipe.next()
+        if slot < 0:
+            raise StopIteration
+        L, n, e, used = self._extent(slot)
+        I, Fl, lay = self.ints[slot], self.floats[slot], self.lay
+        fd = int(lay["feat_dim"])
+        src = (I[:used], Fl[:n[L] * fd], Fl[lay["off_labels"]:lay["off_labels"] + self.B * self.label_dim])
+        if self.cuda:
+            cur = torch.cuda.current_stream(self.device)
+            with torch.cuda.stream(self.stream):
+                ints_d, x_d, lab_d = (t.to(self.device, non_blocking=True) for t in src)
+                ev = torch.cuda.Event()
+                ev.record(self.stream)
+            cur.wait_event(ev)
+            for t in (ints_d, x_d, lab_d):
+                t.record_stream(cur)
+            self._inflight.append((slot, ev))
+        else:
+            ints_d, x_d, lab_d = (t.clone() for t in src)
+            self._inflight.append((slot, None))
+        # views (compute stream, after the copy event)
+        roots = ints_d[16:16 + self.B]
+        df = DataFlow(roots)
+        for h in range(1, L + 1):
+            nid = ints_d[lay["off_nid"][h]:lay["off_nid"][h] + n[h]]
+            res = ints_d[lay["off_res"][h]:lay["off_res"][h] + n[h - 1]]
+            ei = ints_d[lay["off_src"][h]:lay["off_src"][h] + 2 * e[h]].view(2, e[h])
+            t, w = n[h - 1], self.fanouts[h - 1] + (1 if self.self_loops else 0)
+            o = lay["off_nbr"][h]
+            nbr = ints_d[o:o + (t * w + 1) // 2].view(torch.int32)[: t * w].view(t, w)
+            df.blocks.append(Block(nid, res, None, ei, [t, n[h]], nbr))
+            df._last = nid
+        x = x_d.view(n[L], fd)
+        lab = lab_d.view(self.B, self.label_dim)
+        return Prepared(inputs=roots, label=lab, embed_in=Prepared(flow=df, x=x))
+
+    def close(self):
+        if self.pipe is not None:
+            self.pipe.stop()
+            self._recycle(block=True)
+            self.pipe = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

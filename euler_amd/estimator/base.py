@@ -269,9 +269,9 @@ class BaseEstimator:
         # releases the GIL) on a worker thread and copied to HBM on a side stream while
         # this thread runs the current step (utils/prefetch.py); params["prefetch"] = 0
         # turns it off
-        prefetcher = None
+        prefetcher = self._native_pipeline()
         depth = int(self.params.get("prefetch", 2 if self.device.type == "cuda" else 0))
-        if depth > 0 and callable(getattr(self.model, "prepare", None)):
+        if prefetcher is None and depth > 0 and callable(getattr(self.model, "prepare", None)):
             prefetcher = Prefetcher(lambda: self.model.prepare(self.get_train_from_input(inputs, self.params)),
                                     self.device, depth=depth, workers=int(self.params.get("prefetch_workers", 1)))
         t0, n0 = time.time(), self.global_step
@@ -297,7 +297,7 @@ class BaseEstimator:
                 extra = self._extra_losses()
                 obj = loss if extra is None else loss + extra
             with rng("backward"):
-                self.optimizer.zero_grad(set_to_none=False)
+                self.optimizer.zero_grad(set_to_none=True)
                 obj.backward()
                 self._after_backward()
             with rng("grad_sync"):
@@ -328,6 +328,26 @@ class BaseEstimator:
         self.save()
         dp.barrier()
         return last
+
+    def _native_pipeline(self):
+        """The C++ batch pipeline (dataflow/native_loader.py) for SupervisedGNN + SageDataFlow
+        models on an in-process graph: params["native_pipeline"] = True / False / "auto"
+        (default: on for GPU training), "pipeline_workers" worker threads."""
+        mode = self.params.get("native_pipeline", "auto")
+        if mode in (False, "0", "false", "off") or (mode == "auto" and self.device.type != "cuda"):
+            return None
+        from euler_amd.dataflow.native_loader import NativeSageLoader, native_spec
+        from euler_amd.ops.base import get_engine
+
+        spec = native_spec(self.model, self.params)
+        if spec is None or get_engine().meta()["mode"] != "local":
+            return None
+        flow, names, dims, label, label_dim, node_type = spec
+        seed = int(self.params.get("seed") or 0) * 1000003 + self.rank
+        workers = int(self.params.get("pipeline_workers", 8))
+        log.info("native batch pipeline: %d workers", workers)
+        return NativeSageLoader(flow, names, dims, label, label_dim, int(self.params["batch_size"]), node_type,
+                                self.device, workers=workers, seed=seed)
 
     def _device_graph_trainer(self, first):
         """Upload the engine's graph (structure, the model's feature and label columns) to

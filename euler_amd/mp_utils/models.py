@@ -304,7 +304,8 @@ class SuperviseModel(nn.Module):
         label = label.to(embedding.device)
         logit = self.out_fc(embedding).float()
         loss = F.binary_cross_entropy_with_logits(logit, label.float())
-        metric = self.metric(label.detach().cpu(), torch.sigmoid(logit).detach().cpu())
+        # streaming metric on the device (no per-step host sync; read at log steps)
+        metric = self.metric(label.detach(), torch.sigmoid(logit).detach())
         return embedding, loss, self.metric_name, metric
 
 

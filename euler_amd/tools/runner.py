@@ -181,6 +181,10 @@ def parse_args(argv=None, model=None):
                    help="graphsage: train on an HBM copy of the graph with the fused gfx950 step "
                         "(models/sage_trainer.py) instead of the CPU-engine input pipeline")
     p.add_argument("--device_feature_dtype", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--native_pipeline", default="auto", choices=["auto", "on", "off"],
+                   help="engine path: C++ batch pipeline (sampling + features into pinned slots) for "
+                        "SupervisedGNN + SageDataFlow models; auto = on for GPU training")
+    p.add_argument("--pipeline_workers", type=int, default=8)
     p.add_argument("--seed", type=int, default=None)
     return p.parse_args(argv)
 
@@ -205,7 +209,9 @@ def build(a):
     params = {"model_dir": a.model_dir, "infer_dir": a.infer_dir, "batch_size": a.batch_size, "total_step": total,
               "log_steps": a.log_steps, "optimizer": a.optimizer, "learning_rate": a.learning_rate,
               "device": a.device, "amp": a.amp, "device_graph": a.device_graph,
-              "device_feature_dtype": a.device_feature_dtype, "seed": a.seed}
+              "device_feature_dtype": a.device_feature_dtype, "seed": a.seed,
+              "native_pipeline": {"auto": "auto", "on": True, "off": False}[a.native_pipeline],
+              "pipeline_workers": a.pipeline_workers}
     if kind == "node":
         params.update(train_node_type=_first(ds.train_node_type), id_file=a.id_file or ds.id_file)
         est = NodeEstimator(model, params)

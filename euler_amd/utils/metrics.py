@@ -12,6 +12,68 @@ import torch
 __all__ = ["Metric", "AccScore", "AucScore", "F1Score", "MrrScore", "HitKScore", "MrScore", "get", "metrics"]
 
 
+class Lazy:
+    """A metric value that stays on the device until read (``float(m)``): updates from
+    GPU tensors never synchronise the stream."""
+
+    __slots__ = ("fn",)
+
+    def __init__(self, fn):
+        self.fn = fn
+
+    def __float__(self):
+        return float(self.fn())
+
+    def __repr__(self):
+        return repr(float(self))
+
+    def __format__(self, spec):
+        return format(float(self), spec)
+
+    # numeric protocol through the value (comparisons, arithmetic in user code / tests)
+    def __eq__(self, o):
+        return float(self) == o
+
+    def __lt__(self, o):
+        return float(self) < o
+
+    def __le__(self, o):
+        return float(self) <= o
+
+    def __gt__(self, o):
+        return float(self) > o
+
+    def __ge__(self, o):
+        return float(self) >= o
+
+    def __add__(self, o):
+        return float(self) + o
+
+    __radd__ = __add__
+
+    def __sub__(self, o):
+        return float(self) - o
+
+    def __rsub__(self, o):
+        return o - float(self)
+
+    def __mul__(self, o):
+        return float(self) * o
+
+    __rmul__ = __mul__
+
+    def __truediv__(self, o):
+        return float(self) / o
+
+    def __abs__(self):
+        return abs(float(self))
+
+    def __round__(self, n=None):
+        return round(float(self), n)
+
+    __hash__ = None
+
+
 class Metric:
     def __init__(self):
         self.reset()
@@ -35,9 +97,9 @@ class AccScore(Metric):
     def update(self, labels, predict):
         labels = torch.as_tensor(labels).float()
         pred = torch.floor(torch.as_tensor(predict).float() + 0.5)
-        self.correct += float((pred == labels).float().sum())
+        self.correct = self.correct + (pred == labels).float().sum()  # device-resident accumulator
         self.total += float(labels.numel())
-        return self.correct / max(self.total, 1.0)
+        return Lazy(lambda: float(self.correct) / max(self.total, 1.0))
 
 
 class AucScore(Metric):
@@ -74,14 +136,20 @@ class F1Score(Metric):
 
     def update(self, labels, predict):
         y = torch.as_tensor(labels).float()
-        p = torch.floor(torch.as_tensor(predict).float() + 0.5)
-        self.tp += float((p * y).sum())
-        self.fp += float((p * (1 - y)).sum())
-        self.fn += float(((1 - p) * y).sum())
-        eps = 1e-7
-        prec = self.tp / (eps + self.tp + self.fp)
-        rec = self.tp / (eps + self.tp + self.fn)
-        return 2.0 * prec * rec / (prec + rec + eps)
+        p = torch.floor(torch.as_tensor(predict).float().to(y.device) + 0.5)
+        # device-resident accumulators: no host sync per step (read through Lazy)
+        self.tp = self.tp + (p * y).sum()
+        self.fp = self.fp + (p * (1 - y)).sum()
+        self.fn = self.fn + ((1 - p) * y).sum()
+        tp, fp, fn = self.tp, self.fp, self.fn
+
+        def value():
+            eps = 1e-7
+            prec = float(tp) / (eps + float(tp) + float(fp))
+            rec = float(tp) / (eps + float(tp) + float(fn))
+            return 2.0 * prec * rec / (prec + rec + eps)
+
+        return Lazy(value)
 
 
 def _ranks(pos, neg):

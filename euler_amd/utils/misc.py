@@ -11,11 +11,30 @@ __all__ = ["get_optimizer", "optimizers", "embedding_update", "embedding_add", "
 
 
 # ----------------------------------------------------------------------------- optimizers
+def _fused_ok(params):
+    """GPU parameters: the single-kernel (fused) multi-tensor optimizer step"""
+    params = list(params)
+    return bool(params) and all(p.is_cuda and p.is_floating_point() for p in params), params
+
+
+def _adam(params, lr):
+    ok, params = _fused_ok(params)
+    return torch.optim.Adam(params, lr=lr, fused=True) if ok else torch.optim.Adam(params, lr=lr)
+
+
+def _sgd(momentum):
+    def make(params, lr):
+        ok, params = _fused_ok(params)
+        return torch.optim.SGD(params, lr=lr, momentum=momentum, fused=True) if ok else \
+            torch.optim.SGD(params, lr=lr, momentum=momentum)
+    return make
+
+
 optimizers = {
-    "sgd": lambda params, lr: torch.optim.SGD(params, lr=lr, momentum=0.0),
-    "momentum": lambda params, lr: torch.optim.SGD(params, lr=lr, momentum=0.9),
+    "sgd": _sgd(0.0),
+    "momentum": _sgd(0.9),
     "adagrad": lambda params, lr: torch.optim.Adagrad(params, lr=lr, initial_accumulator_value=0.1),
-    "adam": lambda params, lr: torch.optim.Adam(params, lr=lr),
+    "adam": _adam,
 }
 
 

@@ -64,6 +64,8 @@ for st in "${S[@]}"; do
       run ppi_device_b32 600 python -u examples/run_graphsage.py --dataset ppi --device_graph --device cuda \
           --batch_size 32 --total_step 3000 --log_steps 500 --model_dir /tmp/ppi_dev32 --fanouts 10 10 \
           --learning_rate 0.01 ;;
+    engine_sage)
+      run engine_sage 900 python -u benchmarks/bench_engine_sage.py --steps 300 --warmup 20 ;;
     kernels_full)
       run tree_kernels_full 300 python -u tools/tree_kernels.py --num-nodes 100000000 ;;
     kernels_sizes)
