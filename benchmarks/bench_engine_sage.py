@@ -31,7 +31,7 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
-def run(ds, args, prefetch, device, workers=2, native=False):
+def run(ds, args, prefetch, device, workers=2, native=False, graph="auto"):
     import euler_amd as ea
     from euler_amd import models as Z
     from euler_amd.estimator import NodeEstimator
@@ -46,7 +46,8 @@ def run(ds, args, prefetch, device, workers=2, native=False):
         return {"model_dir": tempfile.mkdtemp(prefix="euler_amd_ckpt_"), "batch_size": args.batch,
                 "total_step": total, "optimizer": "adam", "learning_rate": 0.01, "log_steps": 10 ** 9,
                 "train_node_type": tnt, "device": device, "prefetch": prefetch,
-                "prefetch_workers": workers, "native_pipeline": native, "pipeline_workers": workers}
+                "prefetch_workers": workers, "native_pipeline": native, "pipeline_workers": workers,
+                "cuda_graph": graph}
 
     NodeEstimator(model, params(args.warmup)).train()
     est = NodeEstimator(model, params(args.steps))
@@ -66,6 +67,8 @@ def main(argv=None):
     p.add_argument("--batch", type=int, default=512)
     p.add_argument("--scale", type=float, default=1.0)
     p.add_argument("--native_workers", type=int, nargs="+", default=[4, 8, 16])
+    p.add_argument("--only", default="", help="comma list of variant names to run (default: all)")
+    p.add_argument("--cprofile", default="", help="write the consumer's cProfile top-40 (cumulative) here")
     args = p.parse_args(argv)
     from euler_amd.dataset import get_dataset
 
@@ -76,14 +79,33 @@ def main(argv=None):
     print(f"[bench_engine_sage] ppi-schema graph scale {args.scale} ready in {time.time() - t0:.1f}s",
           file=sys.stderr, flush=True)
     out = {}
-    variants = [("serial", 0, 1, False), ("py_prefetch_1worker", 2, 1, False)]
-    variants += [("native_%dworkers" % w, 0, w, True) for w in args.native_workers]
-    for name, pf, wk, nat in variants:
-        el, res = run(ds, args, pf, dev, wk, nat)
+    variants = [("serial", 0, 1, False, False), ("py_prefetch_1worker", 2, 1, False, False)]
+    variants += [("native_%dworkers_eager" % w, 0, w, True, False) for w in args.native_workers[:1]]
+    # native pipeline + graph-captured step (the estimator default on a GPU)
+    variants += [("native_%dworkers" % w, 0, w, True, "auto") for w in args.native_workers]
+    if args.only:
+        keep = set(args.only.split(","))
+        variants = [v for v in variants if v[0] in keep]
+    for name, pf, wk, nat, gr in variants:
+        if args.cprofile:
+            import cProfile
+            import io
+            import pstats
+
+            pr = cProfile.Profile()
+            pr.enable()
+            el, res = run(ds, args, pf, dev, wk, nat, gr)
+            pr.disable()
+            buf = io.StringIO()
+            pstats.Stats(pr, stream=buf).sort_stats("tottime").print_stats(40)
+            with open(args.cprofile, "a") as f:
+                f.write(f"==== {name}\n{buf.getvalue()}\n")
+        else:
+            el, res = run(ds, args, pf, dev, wk, nat, gr)
         out[name] = {"samples_per_s": round(args.batch * args.steps / el, 1), "ms_per_step": round(el * 1e3 / args.steps, 2),
                      "loss": round(float(res.get("loss", float("nan"))), 4)}
         print(f"[bench_engine_sage] {name}: {out[name]}", file=sys.stderr, flush=True)
-    best = max((k for k in out if k.startswith("native")), key=lambda k: out[k]["samples_per_s"])
+    best = max((k for k in out if k.startswith("native") and not k.endswith("eager")) or out, key=lambda k: out[k]["samples_per_s"])
     print(json.dumps({
         "metric": "train samples/sec, GraphSAGE via the C++ graph engine + estimator (reference architecture)",
         "value": out[best]["samples_per_s"],   # the estimator default on a GPU: the native pipeline

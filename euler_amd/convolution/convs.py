@@ -147,16 +147,21 @@ class SAGEConv(Conv):
             return False
         if self.self_fc.has_uninitialized_params() or self.neigh_fc.has_uninitialized_params():
             return False  # the first (materialising) call takes the generic path
-        d = x_all.shape[1]
-        return d % 16 == 0 and d <= 512
+        return x_all.shape[1] <= 512
 
     def fused_relu(self, x_all, block):
-        """relu(self_fc(x_all[res_n_id]) + neigh_fc(mean_j x_all[nbr[:, j]])) in one kernel."""
+        """relu(self_fc(x_all[res_n_id]) + neigh_fc(mean_j x_all[nbr[:, j]])) in one kernel.
+        Widths that are not a multiple of the kernel's 16-column K step (e.g. 50-d input
+        features) are zero-padded on x and on both weights' input columns."""
         from euler_amd.ops.sage_ops import sage_layer
 
         SAGEConv.fused_calls += 1
-        w = torch.cat([self.self_fc.weight, self.neigh_fc.weight], 1)
-        out = sage_layer(x_all.to(torch.bfloat16), block.res_n_id.to(torch.int32), block.nbr, w, None,
+        xb, ws, wn = x_all.to(torch.bfloat16), self.self_fc.weight, self.neigh_fc.weight
+        pad = -x_all.shape[1] % 16
+        if pad:
+            xb, ws, wn = F.pad(xb, (0, pad)), F.pad(ws, (0, pad)), F.pad(wn, (0, pad))
+        w = torch.cat([ws, wn], 1)
+        out = sage_layer(xb, block.res_n_id.to(torch.int32), block.nbr, w, None,
                          include_self=False, relu=True, disjoint=False)
         return out.to(x_all.dtype)
 

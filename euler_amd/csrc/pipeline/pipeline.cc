@@ -188,6 +188,10 @@ void SagePipeline::Fill(int slot, uint64_t seq) {
       for (int j = 0; j < k; ++j) nb[i * w + j] = static_cast<int32_t>(inv[i * k + j]);
       if (s.self_loops) nb[i * w + k] = static_cast<int32_t>(inv[n * k + i]);
     }
+    // capacity padding: rows past n read the zero row (-1), so fixed-capacity consumers
+    // (the graph-captured step) compute exact results for the valid rows
+    std::fill(res + n, res + lay.cap[h - 1], int64_t{-1});
+    std::fill(nb + n * w, nb + lay.cap[h - 1] * w, int32_t{-1});
     I[1 + h] = nu;
     I[8 + h] = e;
     cur = nid;

@@ -41,7 +41,8 @@ struct SageBatchSpec {
 //   level 0 ids        [batch]
 //   per hop h = 1..L:  n_id [cap_h] | res [cap_{h-1}] | edges [2 * ecap_h] (src[e] then dst[e]
 //                      packed: the [2, e] edge index is one contiguous view) | nbr: int32
-//                      [cap_{h-1}][F_h (+1)] dense neighbour positions (self loop last)
+//                      [cap_{h-1}][F_h (+1)] dense neighbour positions (self loop last);
+//                      res and nbr are padded with -1 up to cap_{h-1} rows
 // float words: features [cap_L][sum dense_dims] | labels [batch][label_dim]
 struct SageSlotLayout {
   std::vector<int64_t> cap, ecap;   // per level / hop

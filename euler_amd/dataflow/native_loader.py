@@ -17,6 +17,14 @@ the step; the round-1 Python prefetcher called ``pin_memory()`` on every batch.
 
 Batch b is drawn from the Philox stream (seed, b) and delivered in order, so the batch
 stream is reproducible for any worker count.
+
+Static mode (``static=True``, GPU only) serves every batch through ONE set of
+fixed-capacity device tensors, the inputs of a graph-captured training step
+(estimator/graph_step.py): the slot's ``res`` / ``nbr`` are padded with -1 up to the
+level capacities by the C++ writer, the H2D copy lands in one of two device staging
+sets on the side stream, and a device-to-device copy on the compute stream moves it into
+the static set right before the replay (the staging set is reused only after that copy
+has run, tracked by an event).  ``get()`` then returns the same ``Prepared`` every time.
 """
 from __future__ import annotations
 
@@ -54,7 +62,7 @@ def native_spec(model, params):
 
 class NativeSageLoader:
     def __init__(self, flow, dense_names, dense_dims, label, label_dim, batch_size, node_type, device, workers=8,
-                 slots=None, seed=0):
+                 slots=None, seed=0, static=False):
         import euler_amd._engine as E
         import euler_amd.ops.graph_api as ge
 
@@ -84,6 +92,66 @@ class NativeSageLoader:
                                    [t.data_ptr() for t in self.floats], int(workers), int(seed))
         self.stream = torch.cuda.Stream(device=self.device) if self.cuda else None
         self._inflight = []  # (slot, event) copies not yet known complete
+        self.static = bool(static) and self.cuda
+        if self.static:
+            self._setup_static(dense_dims)
+
+    # ------------------------------------------------------------------ static mode
+    def _setup_static(self, dense_dims):
+        lay, L = self.lay, len(self.fanouts)
+        self.cap = [int(c) for c in lay["cap"]]
+        self.w = [f + (1 if self.self_loops else 0) for f in self.fanouts]
+        self.fd = int(lay["feat_dim"])
+        # every int word any static view reads lies below the end of hop L's nbr block
+        self.static_ints = int(lay["off_nbr"][L]) + (self.cap[L - 1] * self.w[L - 1] + 1) // 2
+        dev = self.device
+
+        def bufs():
+            return (torch.zeros(self.static_ints, dtype=torch.int64, device=dev),
+                    torch.zeros(self.cap[L] * self.fd, dtype=torch.float32, device=dev),
+                    torch.zeros(self.B * self.label_dim, dtype=torch.float32, device=dev))
+
+        self._stage = [bufs(), bufs()]
+        self._stage_free = [None, None]  # compute-stream event after the D2D out of stage j
+        self._j = 0
+        ints, x, lab = self._static_bufs = bufs()
+        df = DataFlow(ints[16:16 + self.B])
+        for h in range(1, L + 1):
+            nid = ints[lay["off_nid"][h]:lay["off_nid"][h] + self.cap[h]]
+            res = ints[lay["off_res"][h]:lay["off_res"][h] + self.cap[h - 1]]
+            t, w, o = self.cap[h - 1], self.w[h - 1], int(lay["off_nbr"][h])
+            nbr = ints[o:o + (t * w + 1) // 2].view(torch.int32)[: t * w].view(t, w)
+            df.blocks.append(Block(nid, res, None, None, [t, self.cap[h]], nbr))
+            df._last = nid
+        self.static_prepared = Prepared(inputs=ints[16:16 + self.B], label=lab.view(self.B, self.label_dim),
+                                        embed_in=Prepared(flow=df, x=x.view(self.cap[L], self.fd)))
+
+    def _get_static(self, slot, n):
+        L = len(self.fanouts)
+        I, Fl, lay = self.ints[slot], self.floats[slot], self.lay
+        nx = n[L] * self.fd
+        j = self._j
+        self._j ^= 1
+        st = self._stage[j]
+        cur = torch.cuda.current_stream(self.device)
+        with torch.cuda.stream(self.stream):
+            if self._stage_free[j] is not None:
+                self.stream.wait_event(self._stage_free[j])
+            st[0].copy_(I[:self.static_ints], non_blocking=True)
+            st[1][:nx].copy_(Fl[:nx], non_blocking=True)
+            st[2].copy_(Fl[lay["off_labels"]:lay["off_labels"] + self.B * self.label_dim], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        self._inflight.append((slot, ev))
+        cur.wait_event(ev)
+        ints, x, lab = self._static_bufs
+        ints.copy_(st[0])
+        x[:nx].copy_(st[1][:nx])
+        lab.copy_(st[2])
+        free = torch.cuda.Event()
+        free.record(cur)
+        self._stage_free[j] = free
+        return self.static_prepared
 
     # ------------------------------------------------------------------ consumer
     def _recycle(self, block=False):
@@ -115,6 +183,8 @@ class NativeSageLoader:
         if slot < 0:
             raise StopIteration
         L, n, e, used = self._extent(slot)
+        if self.static:
+            return self._get_static(slot, n)
         I, Fl, lay = self.ints[slot], self.floats[slot], self.lay
         fd = int(lay["feat_dim"])
         src = (I[:used], Fl[:n[L] * fd], Fl[lay["off_labels"]:lay["off_labels"] + self.B * self.label_dim])

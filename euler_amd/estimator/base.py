@@ -274,6 +274,11 @@ class BaseEstimator:
         if prefetcher is None and depth > 0 and callable(getattr(self.model, "prepare", None)):
             prefetcher = Prefetcher(lambda: self.model.prepare(self.get_train_from_input(inputs, self.params)),
                                     self.device, depth=depth, workers=int(self.params.get("prefetch_workers", 1)))
+        graphed = None
+        if getattr(prefetcher, "static", False):
+            from euler_amd.estimator.graph_step import GraphedTrainStep
+
+            graphed = GraphedTrainStep(self, prefetcher)
         t0, n0 = time.time(), self.global_step
         last = {}
         prof = None
@@ -291,6 +296,17 @@ class BaseEstimator:
                     source = prefetcher.get()
                 else:
                     source = self.get_train_from_input(inputs, self.params)
+            if graphed is not None and source is not first:
+                # graph-captured step over the pipeline's static inputs (estimator/graph_step.py)
+                with rng("graph_step"):
+                    loss, metric_name, metric = graphed.step(source)
+                self.global_step += 1
+                if prof is not None:
+                    prof.step()
+                last, t0, n0 = self._log_step(total, log_steps, loss, metric_name, metric, t0, n0, tracing, last)
+                if save_steps and self.global_step % save_steps == 0:
+                    self.save()
+                continue
             pending = None
             with rng("forward"):
                 _, loss, metric_name, metric = self._run_model(source)
@@ -307,18 +323,7 @@ class BaseEstimator:
             self.global_step += 1
             if prof is not None:
                 prof.step()
-            if self.global_step % log_steps == 0 or self.global_step == total:
-                dt = max(time.time() - t0, 1e-9)
-                rate = (self.global_step - n0) * int(self.params.get("batch_size", 1)) / dt
-                last = {"step": self.global_step, "loss": float(loss.detach()), metric_name: float(metric),
-                        "samples_per_sec": rate}
-                if self.rank == 0:
-                    log.info("step = %d, loss = %.6f, %s = %.6f (%.1f samples/s)", self.global_step, last["loss"],
-                             metric_name, last[metric_name], rate)
-                    if tracing:
-                        log.info("stage timings:\n%s\nengine: %s", trace.default_timer.report(),
-                                 trace.engine_stats())
-                t0, n0 = time.time(), self.global_step
+            last, t0, n0 = self._log_step(total, log_steps, loss, metric_name, metric, t0, n0, tracing, last)
             if save_steps and self.global_step % save_steps == 0:
                 self.save()
         if prefetcher is not None:
@@ -328,6 +333,20 @@ class BaseEstimator:
         self.save()
         dp.barrier()
         return last
+
+    def _log_step(self, total, log_steps, loss, metric_name, metric, t0, n0, tracing, last):
+        if not (self.global_step % log_steps == 0 or self.global_step == total):
+            return last, t0, n0
+        dt = max(time.time() - t0, 1e-9)
+        rate = (self.global_step - n0) * int(self.params.get("batch_size", 1)) / dt
+        last = {"step": self.global_step, "loss": float(loss.detach()), metric_name: float(metric),
+                "samples_per_sec": rate}
+        if self.rank == 0:
+            log.info("step = %d, loss = %.6f, %s = %.6f (%.1f samples/s)", self.global_step, last["loss"],
+                     metric_name, last[metric_name], rate)
+            if tracing:
+                log.info("stage timings:\n%s\nengine: %s", trace.default_timer.report(), trace.engine_stats())
+        return last, time.time(), self.global_step
 
     def _native_pipeline(self):
         """The C++ batch pipeline (dataflow/native_loader.py) for SupervisedGNN + SageDataFlow
@@ -345,9 +364,13 @@ class BaseEstimator:
         flow, names, dims, label, label_dim, node_type = spec
         seed = int(self.params.get("seed") or 0) * 1000003 + self.rank
         workers = int(self.params.get("pipeline_workers", 8))
-        log.info("native batch pipeline: %d workers", workers)
+        from euler_amd.estimator.graph_step import graph_step_blocker
+
+        why = graph_step_blocker(self, sum(dims))
+        log.info("native batch pipeline: %d workers; graph-captured step: %s", workers,
+                 "yes" if why is None else "no (%s)" % why)
         return NativeSageLoader(flow, names, dims, label, label_dim, int(self.params["batch_size"]), node_type,
-                                self.device, workers=workers, seed=seed)
+                                self.device, workers=workers, seed=seed, static=why is None)
 
     def _device_graph_trainer(self, first):
         """Upload the engine's graph (structure, the model's feature and label columns) to

@@ -88,18 +88,39 @@ class Metric:
         return self.update(*args)
 
 
+def _accumulate(metric, parts):
+    """Add the stacked per-batch counts into the metric's device accumulator IN PLACE, so
+    a graph-captured step keeps accumulating on every replay (a rebinding ``a = a + v``
+    would freeze the captured tensor)."""
+    v = torch.stack([t.float() for t in parts])
+    if metric.acc is None or metric.acc.device != v.device:
+        metric.acc = torch.zeros_like(v)
+    metric.acc.add_(v)
+    return metric.acc
+
+
 class AccScore(Metric):
     """accuracy of floor(p + 0.5) against labels (predict = probabilities)."""
 
     def reset(self):
-        self.correct, self.total = 0.0, 0.0
+        if getattr(self, "acc", None) is not None:
+            self.acc.zero_()
+        else:
+            self.acc = None
 
     def update(self, labels, predict):
         labels = torch.as_tensor(labels).float()
-        pred = torch.floor(torch.as_tensor(predict).float() + 0.5)
-        self.correct = self.correct + (pred == labels).float().sum()  # device-resident accumulator
-        self.total += float(labels.numel())
-        return Lazy(lambda: float(self.correct) / max(self.total, 1.0))
+        pred = torch.floor(torch.as_tensor(predict).float().to(labels.device) + 0.5)
+        acc = _accumulate(self, [(pred == labels).float().sum(), labels.new_full((), float(labels.numel()))])
+        return Lazy(lambda: float(acc[0]) / max(float(acc[1]), 1.0))
+
+    @property
+    def correct(self):
+        return 0.0 if self.acc is None else float(self.acc[0])
+
+    @property
+    def total(self):
+        return 0.0 if self.acc is None else float(self.acc[1])
 
 
 class AucScore(Metric):
@@ -132,21 +153,22 @@ class AucScore(Metric):
 
 class F1Score(Metric):
     def reset(self):
-        self.tp = self.fp = self.fn = 0.0
+        if getattr(self, "acc", None) is not None:
+            self.acc.zero_()
+        else:
+            self.acc = None
 
     def update(self, labels, predict):
         y = torch.as_tensor(labels).float()
         p = torch.floor(torch.as_tensor(predict).float().to(y.device) + 0.5)
-        # device-resident accumulators: no host sync per step (read through Lazy)
-        self.tp = self.tp + (p * y).sum()
-        self.fp = self.fp + (p * (1 - y)).sum()
-        self.fn = self.fn + ((1 - p) * y).sum()
-        tp, fp, fn = self.tp, self.fp, self.fn
+        # device-resident accumulators [tp, fp, fn]: no host sync per step (read through Lazy)
+        acc = _accumulate(self, [(p * y).sum(), (p * (1 - y)).sum(), ((1 - p) * y).sum()])
 
         def value():
+            tp, fp, fn = (float(v) for v in acc.tolist())
             eps = 1e-7
-            prec = float(tp) / (eps + float(tp) + float(fp))
-            rec = float(tp) / (eps + float(tp) + float(fn))
+            prec = tp / (eps + tp + fp)
+            rec = tp / (eps + tp + fn)
             return 2.0 * prec * rec / (prec + rec + eps)
 
         return Lazy(value)

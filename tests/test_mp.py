@@ -348,12 +348,14 @@ def test_sage_flow_blocks_carry_neighbour_matrix(syn):
 
 
 @pytest.mark.gpu
-def test_gnn_dispatches_fused_sage_kernel(syn, cuda, monkeypatch):
+@pytest.mark.parametrize("din", [32, 50])
+def test_gnn_dispatches_fused_sage_kernel(syn, cuda, monkeypatch, din):
     """BaseGNNNet with SAGEConv on fixed-fanout blocks runs the fused gather + mean +
-    linear + ReLU kernel on the GPU; outputs and gradients match the generic path."""
+    linear + ReLU kernel on the GPU; outputs and gradients match the generic path
+    (din=50: input width zero-padded to the kernel's 16-column step)."""
     torch.manual_seed(0)
     net = BaseGNNNet("sage", "sage", [32, 32, 32], [5, 3], [["0"], ["0"]], max_id=399)
-    feats = torch.randn(400, 32)
+    feats = torch.randn(400, din)
     ids = torch.arange(16)
     flow = net.sampler(ids)
     x0 = feats[flow[0].n_id]
