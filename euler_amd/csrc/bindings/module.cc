@@ -224,7 +224,7 @@ class Engine {
     std::vector<uint64_t> out;
     {
       py::gil_scoped_release nogil;
-      Rng rng(GlobalSeed() ^ 0x77ULL, static_cast<uint64_t>(NowMicros()));
+      Rng rng(GlobalSeed() ^ 0x77ULL, NextOpEpoch());
       g.SampleNode(type, count, rng, &out);
     }
     py::array_t<uint64_t> a(out.size());
@@ -245,7 +245,7 @@ class Engine {
     int32_t* pt = ot.mutable_data();
     {
       py::gil_scoped_release nogil;
-      const uint64_t seed = GlobalSeed() * 0x9E3779B97F4A7C15ULL + NowMicros();
+      const uint64_t seed = GlobalSeed() * 0x9E3779B97F4A7C15ULL + NextOpEpoch();
       const int64_t chunk = 512, nchunks = (n + chunk - 1) / chunk;
       ThreadPool::Default()->ParallelFor(nchunks, 1, [&](int64_t cb, int64_t ce) {
         std::vector<IdWeightType> tmp;
@@ -282,7 +282,7 @@ class Engine {
     std::vector<int64_t> cur(roots.data(), roots.data() + roots.size());
     {
       py::gil_scoped_release nogil;
-      const uint64_t seed = GlobalSeed() * 0x9E3779B97F4A7C15ULL + NowMicros();
+      const uint64_t seed = GlobalSeed() * 0x9E3779B97F4A7C15ULL + NextOpEpoch();
       for (size_t h = 0; h < etypes.size(); ++h) {
         const int64_t n = static_cast<int64_t>(cur.size());
         const int k = counts[h];

@@ -129,12 +129,15 @@ uint64_t Rng::Below(uint64_t n) {
 
 static std::atomic<uint64_t> g_seed{0x5eed5eedULL};
 static std::atomic<uint64_t> g_epoch{1};
+static std::atomic<uint64_t> g_op_epoch{1};
 static std::atomic<uint64_t> g_thread_ordinal{0};
 
 void SetGlobalSeed(uint64_t seed) {
   g_seed.store(seed);
+  g_op_epoch.store(1);
   g_epoch.fetch_add(1);
 }
+uint64_t NextOpEpoch() { return g_op_epoch.fetch_add(1); }
 uint64_t GlobalSeed() { return g_seed.load(); }
 
 Rng& ThreadRng() {

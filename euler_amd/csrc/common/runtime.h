@@ -90,6 +90,9 @@ class Rng {
 
 void SetGlobalSeed(uint64_t seed);
 uint64_t GlobalSeed();
+// Per-call RNG stream counter of the sampling ops; SetGlobalSeed restarts it, so a
+// sequence of calls after set_seed(s) draws the same streams in every process.
+uint64_t NextOpEpoch();
 // thread-local Rng keyed by (global seed, thread ordinal); re-keyed when the seed changes
 Rng& ThreadRng();
 

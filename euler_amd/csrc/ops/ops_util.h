@@ -38,10 +38,7 @@ inline Tensor MakeUniformIdx(int64_t n, int64_t per) {
 
 // Reproducible parallel loop: fixed-size chunks, chunk c draws from
 // Rng(global seed + epoch, c) whatever thread runs it.
-inline uint64_t NextEpoch() {
-  static std::atomic<uint64_t> e{1};
-  return e.fetch_add(1);
-}
+inline uint64_t NextEpoch() { return NextOpEpoch(); }
 
 template <typename Fn>
 void ParallelChunks(int64_t n, int64_t chunk, Fn fn) {

@@ -297,7 +297,9 @@ class BaseEstimator:
                 else:
                     source = self.get_train_from_input(inputs, self.params)
             if graphed is not None and source is not first:
-                # graph-captured step over the pipeline's static inputs (estimator/graph_step.py)
+                # graph-captured step over the pipeline's static inputs (estimator/graph_step.py);
+                # drop the eager step's autograd graph first
+                _ = loss = obj = extra = metric = None
                 with rng("graph_step"):
                     loss, metric_name, metric = graphed.step(source)
                 self.global_step += 1

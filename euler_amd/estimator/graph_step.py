@@ -86,11 +86,14 @@ class GraphedTrainStep:
         est.optimizer.zero_grad(set_to_none=True)
         loss.backward()
         est.optimizer.step()
-        return loss, name, metric
+        # detached: a live autograd graph keeps its AccumulateGrad nodes (bound to the
+        # stream they were created on) alive into the capture, which then breaks
+        return loss.detach(), name, metric
 
     def step(self, source):
         """One training step over the static inputs ``source`` (already filled for this
-        step on the current stream); returns (loss tensor, metric name, metric)."""
+        step on the current stream); returns (loss tensor, metric name, metric).  The
+        caller must not hold any autograd graph of an earlier step."""
         cur = torch.cuda.current_stream()
         if self.graph is None and self.warm > 0:
             self.warm -= 1

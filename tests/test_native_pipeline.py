@@ -148,19 +148,28 @@ def test_static_loader_serves_one_prepared(graph, cuda):
 @pytest.mark.gpu
 def test_graph_captured_step_tracks_eager_step(graph, cuda, tmp_path):
     """Same seeds -> same batch stream; the hipGraph-replayed step (capacity-padded
-    inputs) must follow the eager step's trajectory."""
+    inputs) must follow the eager step's trajectory as closely as a second eager run does.
+    (Eager runs are not bitwise reproducible themselves: the fused layer's input-gradient
+    scatter accumulates with fp32 atomics, and Adam's per-coordinate normalisation turns
+    that rounding into sign noise on near-zero gradients.)"""
     from euler_amd.convolution.convs import SAGEConv
 
     ea.use_graph(graph)
-    steps = 40
+    steps = 12
     m_e, r_e = _train(tmp_path / "eager", cuda, steps, cuda_graph=False)
+    m_e2, r_e2 = _train(tmp_path / "eager2", cuda, steps, cuda_graph=False)
     before = SAGEConv.fused_calls
     m_g, r_g = _train(tmp_path / "graph", cuda, steps, cuda_graph=True)
     # 1 first (raw-input) step + 3 warm eager steps + 1 capture: 5 Python dispatches per conv
     assert SAGEConv.fused_calls - before == 2 * 5
     assert r_g["step"] == steps
-    assert abs(r_g["loss"] - r_e["loss"]) < 0.02 * r_e["loss"] + 1e-3, (r_g["loss"], r_e["loss"])
-    for (k, a), b in zip(m_e.state_dict().items(), m_g.state_dict().values()):
+    tol = max(0.01 * r_e["loss"], 3 * abs(r_e2["loss"] - r_e["loss"]))
+    assert abs(r_g["loss"] - r_e["loss"]) < tol, (r_g["loss"], r_e["loss"], r_e2["loss"])
+    cos = torch.nn.functional.cosine_similarity
+    sd_e, sd_e2 = m_e.state_dict(), m_e2.state_dict()
+    for k, b in m_g.state_dict().items():
+        a = sd_e[k]
         if a.is_floating_point() and a.numel() > 1:
-            c = torch.nn.functional.cosine_similarity(a.float().reshape(-1), b.float().reshape(-1), dim=0)
-            assert c > 0.99, (k, float(c))
+            c = float(cos(a.float().reshape(-1), b.float().reshape(-1), dim=0))
+            c_ee = float(cos(a.float().reshape(-1), sd_e2[k].float().reshape(-1), dim=0))
+            assert c > min(0.999, c_ee - 0.005), (k, c, c_ee)
