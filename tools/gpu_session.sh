@@ -65,13 +65,14 @@ for st in "${S[@]}"; do
           --batch_size 32 --total_step 3000 --log_steps 500 --model_dir /tmp/ppi_dev32 --fanouts 10 10 \
           --learning_rate 0.01 ;;
     engine_sage)
-      run engine_sage 900 python -u benchmarks/bench_engine_sage.py --steps 300 --warmup 20 ;;
+      run engine_sage 900 python -u benchmarks/bench_engine_sage.py --steps 300 --warmup 20 \
+        --native_workers ${ENGINE_WORKERS:-4 8 16} ;;
     engine_prof)
       run engine_sage_cprofile 600 python -u benchmarks/bench_engine_sage.py --steps 200 --warmup 20 \
         --only native_8workers --cprofile gpurun_out/engine_sage_cprofile.txt ;;
     engine_rocprof)
       run engine_rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/engine_prof" -o run --output-format csv -- \
-          python3 benchmarks/bench_engine_sage.py --steps 200 --warmup 20 --only native_8workers ;;
+          python3 benchmarks/bench_engine_sage.py --steps 300 --warmup 20 --native_workers 16 --only native_16workers ;;
     kernels_full)
       run tree_kernels_full 300 python -u tools/tree_kernels.py --num-nodes 100000000 ;;
     kernels_sizes)
