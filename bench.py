@@ -65,6 +65,13 @@ def _cpu_baseline():
     try:
         with open(path) as f:
             b = json.loads(f.readline())
+        if "value_node_linear" in b:
+            # whole node: the measured per-GPU host share scaled linearly to every core (an
+            # upper bound for the CPU path, so vs_baseline is conservative)
+            note = (f"profiles/cpu_baseline.json: reference-equivalent CPU path, {b['value']} samples/s on "
+                    f"{b.get('threads')} host threads, linearly scaled to all {b['node_cores']} node cores: "
+                    f"{b['value_node_linear']} samples/s ({b['config']['num_nodes']} nodes)")
+            return float(b["value_node_linear"]), note
         note = (f"profiles/cpu_baseline.json: reference-equivalent CPU path, {b['value']} samples/s "
                 f"({b.get('threads')} host threads, {b['config']['num_nodes']} nodes)")
         return float(b["value"]), note

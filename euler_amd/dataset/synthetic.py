@@ -1,0 +1,120 @@
+"""Synthetic graphs WITH learnable structure, for benchmark learning evidence.
+
+The throughput benchmarks run on synthetic data of the reference configs' shapes (no
+network, no dataset downloads).  Uniformly random edges carry nothing to learn, so a
+held-out metric on them stays at chance; the generators here plant structure a model of
+the benchmarked family can recover, so the committed bench JSONs can report a held-out
+metric that must beat chance:
+
+* :func:`lattice_kg` — entities on a 3-D integer lattice, every relation a fixed lattice
+  translation: (h, r, t) holds iff pos(t) = pos(h) + off(r).  Exactly the TransE
+  hypothesis (h + r = t); the FB15k-shaped config-5 bench trains R-GCN + TransE on it and
+  reports tail-ranking MRR / hit@10 on held-out triples.
+* :func:`community_graph` — a planted-partition graph (dense inside communities, sparse
+  across): a node's walk neighbours share its community, so skip-gram embeddings
+  (DeepWalk / LINE, config 4) separate held-out intra-community pairs from random pairs
+  (link-prediction AUC).
+* :func:`community_labels` — class = community (+ label noise): node classification on
+  the same structure (GAT, config 3).
+
+Reference counterparts: the datasets the reference examples train on (examples/TransX,
+examples/deepwalk, examples/gat: FB15k, PPI/Cora, ...); these keep their shapes.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+__all__ = ["lattice_kg", "community_graph", "community_labels", "tail_ranks", "rank_metrics", "auc"]
+
+
+def lattice_kg(num_ent, num_rel, num_triples, num_test, seed=0, max_off=5):
+    """(train (src, rel, dst), test (src, rel, dst)) int64 CPU tensors.  Relation
+    frequencies follow a power law (few relations dominate, like FB15k)."""
+    g = torch.Generator().manual_seed(int(seed))
+    side = int(math.ceil(num_ent ** (1.0 / 3.0)))
+    idx = torch.arange(num_ent)
+    pos = torch.stack([idx // (side * side), (idx // side) % side, idx % side], 1)
+    off = torch.randint(-max_off, max_off + 1, (num_rel, 3), generator=g)
+    off[(off == 0).all(1)] = 1
+    w = 1.0 / torch.arange(1, num_rel + 1, dtype=torch.float64) ** 1.1
+    want = num_triples + num_test
+    src_l, rel_l, dst_l, have = [], [], [], 0
+    while have < want:
+        m = 2 * (want - have) + 1024
+        h = torch.randint(0, num_ent, (m,), generator=g)
+        r = torch.multinomial(w, m, replacement=True, generator=g)
+        p = pos[h] + off[r]
+        ok = ((p >= 0) & (p < side)).all(1)
+        t = p[:, 0] * side * side + p[:, 1] * side + p[:, 2]
+        ok &= t < num_ent
+        src_l.append(h[ok])
+        rel_l.append(r[ok])
+        dst_l.append(t[ok])
+        have += int(ok.sum())
+    src, rel, dst = (torch.cat(x)[:want] for x in (src_l, rel_l, dst_l))
+    return (src[:num_triples], rel[:num_triples], dst[:num_triples]), (src[num_triples:], rel[num_triples:],
+                                                                       dst[num_triples:])
+
+
+def community_graph(num_nodes, num_comm, avg_degree, p_in=0.9, seed=0):
+    """(src, dst, comm): ``num_nodes * avg_degree`` directed edges, a fraction ``p_in``
+    inside the source's community (community of node i = i % num_comm)."""
+    g = torch.Generator().manual_seed(int(seed))
+    m = int(num_nodes * avg_degree)
+    src = torch.randint(0, num_nodes, (m,), generator=g)
+    inside = torch.rand(m, generator=g) < p_in
+    per = num_nodes // num_comm
+    k = torch.randint(0, per, (m,), generator=g)
+    dst_in = (k * num_comm + src % num_comm).clamp_max(num_nodes - 1)
+    dst_out = torch.randint(0, num_nodes, (m,), generator=g)
+    dst = torch.where(inside, dst_in, dst_out)
+    return src, dst, torch.arange(num_nodes) % num_comm
+
+
+def community_labels(comm, num_classes, noise=0.1, seed=0):
+    g = torch.Generator().manual_seed(int(seed) + 1)
+    y = comm % num_classes
+    flip = torch.rand(comm.numel(), generator=g) < noise
+    return torch.where(flip, torch.randint(0, num_classes, (comm.numel(),), generator=g), y)
+
+
+@torch.no_grad()
+def tail_ranks(ent, rel, src, ridx, dst, normalize=True, kind="l2", chunk=1024):
+    """Raw rank (1 = best) of the true tail among ALL entities for each test triple,
+    TransE score -|h + r - t| (l1 / l2) on (optionally) l2-normalised rows; ties count
+    against the true tail."""
+    E = torch.nn.functional.normalize(ent.float(), dim=-1) if normalize else ent.float()
+    R = torch.nn.functional.normalize(rel.float(), dim=-1) if normalize else rel.float()
+    out = []
+    for a in range(0, src.numel(), chunk):
+        s, r, t = src[a:a + chunk], ridx[a:a + chunk], dst[a:a + chunk]
+        q = E[s] + R[r]                                        # [c, D]
+        d = torch.cdist(q, E, p=1.0 if kind == "l1" else 2.0)  # [c, Ne]
+        true = d.gather(1, t.view(-1, 1))
+        out.append((d <= true).sum(1))
+    return torch.cat(out)
+
+
+def rank_metrics(ranks, ks=(1, 3, 10)):
+    r = ranks.double()
+    res = {"mrr": float((1.0 / r).mean())}
+    for k in ks:
+        res["hit@%d" % k] = float((r <= k).double().mean())
+    return res
+
+
+def auc(pos_scores, neg_scores):
+    """ROC AUC = P(score(pos) > score(neg)) (ties count half), exact via ranks."""
+    s = torch.cat([pos_scores.reshape(-1), neg_scores.reshape(-1)]).double()
+    y = torch.cat([torch.ones(pos_scores.numel()), torch.zeros(neg_scores.numel())]).double()
+    order = torch.argsort(s)
+    ranks = torch.empty_like(s)
+    ranks[order] = torch.arange(1, s.numel() + 1, dtype=torch.float64)
+    # average ranks of ties
+    su, inv, cnt = torch.unique(s, return_inverse=True, return_counts=True)
+    rsum = torch.zeros(su.numel(), dtype=torch.float64).index_add_(0, inv, ranks)
+    ranks = (rsum / cnt.double())[inv]
+    n_pos, n_neg = pos_scores.numel(), neg_scores.numel()
+    return float((ranks[y == 1].sum() - n_pos * (n_pos + 1) / 2) / (n_pos * n_neg))

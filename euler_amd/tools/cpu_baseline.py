@@ -25,6 +25,13 @@ feature columns, fanouts [25, 10], 1024 roots per step, hidden 256, 64 classes.
 ``python -m euler_amd.tools.cpu_baseline --num-nodes 100000000 --threads 16`` prints one
 JSON line; ``--out profiles/cpu_baseline.json`` stores it for ``bench.py``'s
 ``vs_baseline``.
+
+Whole-node figure: a GPU box grants one GPU's share of the host (16 threads), so the run
+measures that share and ``--sweep 4,8,16`` records how the path scales with threads.  The
+reference would fill a whole node with independent data-parallel CPU workers, so
+``value_node_linear`` = value x node_cores / threads (perfect linear scaling to every core
+of the node — an upper bound for the CPU) is the denominator ``bench.py`` uses: the
+reported ``vs_baseline`` is conservative.
 """
 from __future__ import annotations
 
@@ -51,6 +58,8 @@ def parse_args(argv=None):
     p.add_argument("--threads", type=int, default=16, help="CPU threads for the engine and torch")
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--out", type=str, default="", help="also write the JSON result to this file")
+    p.add_argument("--node-cores", type=int, default=0, help="cores of the whole node (default os.cpu_count())")
+    p.add_argument("--sweep", type=str, default="", help="also time these thread counts, e.g. 4,8,16")
     return p.parse_args(argv)
 
 
@@ -160,7 +169,35 @@ def run(args) -> dict:
 
 def main(argv=None):
     args = parse_args(argv)
+    sweep = {}
+    if args.sweep:
+        import subprocess
+
+        given = sys.argv[1:] if argv is None else list(argv)
+        keep, skip = [], False
+        for x in given:  # the child gets every flag but --sweep / --out / --threads
+            if skip:
+                skip = False
+                continue
+            name = x.split("=", 1)[0]
+            if name in ("--sweep", "--out", "--threads"):
+                skip = "=" not in x
+                continue
+            keep.append(x)
+        for t in [int(x) for x in args.sweep.split(",") if x]:
+            if t == args.threads:
+                continue
+            # a fresh process per thread count (torch's intra-op pool is fixed at first use)
+            a = keep
+            out = subprocess.run([sys.executable, "-m", "euler_amd.tools.cpu_baseline", *a, "--threads", str(t)],
+                                 capture_output=True, text=True, check=True).stdout.strip().splitlines()[-1]
+            sweep[t] = json.loads(out)["value"]
     res = run(args)
+    sweep[args.threads] = res["value"]
+    cores = int(args.node_cores or os.cpu_count() or args.threads)
+    res["node_cores"] = cores
+    res["value_node_linear"] = round(res["value"] * cores / args.threads, 1)
+    res["thread_sweep"] = {str(k): sweep[k] for k in sorted(sweep)}
     line = json.dumps(res)
     print(line, flush=True)
     if args.out:

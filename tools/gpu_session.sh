@@ -73,6 +73,9 @@ for st in "${S[@]}"; do
     engine_rocprof)
       run engine_rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/engine_prof" -o run --output-format csv -- \
           python3 benchmarks/bench_engine_sage.py --steps 300 --warmup 20 --native_workers 16 --only native_16workers ;;
+    cpu_baseline)
+      run cpu_baseline 900 python -u -m euler_amd.tools.cpu_baseline --num-nodes 100000000 --threads 16 \
+        --sweep 4,8,16 --out "$OUT/cpu_baseline.json" ;;
     kernels_full)
       run tree_kernels_full 300 python -u tools/tree_kernels.py --num-nodes 100000000 ;;
     kernels_sizes)
