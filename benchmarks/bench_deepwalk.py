@@ -9,6 +9,12 @@ sigmoid-CE forward/backward, row-sparse Adam on the owners' shards (reference
 examples/deepwalk: walk_len 3, window 1/1, 5 negatives, Adam; embedding_dim 128 per
 BASELINE config 4).  Nothing is skipped inside the timed region.
 
+Learning evidence (after the timed run, untimed, tables of the timed run freed): the same
+trainer on a 1M-node planted-community graph (dataset/synthetic.py community_graph: 90 %
+of a node's edges stay in its community) with 100K edges held out; link-prediction AUC
+of held-out edges vs random pairs (cosine of target embeddings) at init and during
+training goes into the JSON.
+
 Usage:  python benchmarks/bench_deepwalk.py [--steps K] [--warmup W]
         torchrun --nproc-per-node N benchmarks/bench_deepwalk.py   (one rank per GPU)
 """
@@ -28,6 +34,46 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+def link_prediction_eval(args, dev):
+    """DeepWalk on a planted-community graph; AUC of held-out edges vs random pairs."""
+    import numpy as np
+
+    from euler_amd.dataset.synthetic import auc, community_graph
+    from euler_amd.graph.device_graph import DeviceGraph
+    from euler_amd.models.deepwalk_step import DeepWalkTrainer
+
+    N = args.eval_nodes
+    src, dst, _ = community_graph(N, max(2, N // 1000), args.avg_degree, 0.9, seed=args.seed)
+    gen = torch.Generator().manual_seed(args.seed + 5)
+    perm = torch.randperm(src.numel(), generator=gen)
+    n_hold = min(100_000, src.numel() // 10)
+    hold, keep = perm[:n_hold], perm[n_hold:]
+    s, d = src[keep], dst[keep]
+    o = torch.argsort(s, stable=True)
+    s, d = s[o], d[o]
+    indptr = torch.zeros(N + 1, dtype=torch.int64)
+    indptr[1:] = torch.cumsum(torch.bincount(s, minlength=N), 0)
+    g = DeviceGraph.from_csr(indptr.numpy(), d.int().numpy(), np.ones(d.numel(), np.float32), seed=args.seed,
+                             device=dev)
+    tr = DeepWalkTrainer(g, N, args.dim, args.walk_len, 1, 1, args.num_negs, args.batch, args.eval_lr, "adam",
+                         seed=args.seed)
+    pu, pv = src[hold].to(dev), dst[hold].to(dev)
+    nu = torch.randint(0, N, (n_hold,), generator=gen).to(dev)
+    nv = torch.randint(0, N, (n_hold,), generator=gen).to(dev)
+
+    def score():
+        e = torch.nn.functional.normalize(tr.embedding(torch.arange(N, device=dev)), dim=-1)
+        return round(auc((e[pu] * e[pv]).sum(-1).cpu(), (e[nu] * e[nv]).sum(-1).cpu()), 4)
+
+    curve = {0: score()}
+    for i in range(1, args.eval_steps + 1):
+        tr.step()
+        if i % max(1, args.eval_steps // 4) == 0 or i == args.eval_steps:
+            curve[i] = score()
+    return {"nodes": N, "edges_train": int(keep.numel()), "heldout_edges": n_hold, "lr": args.eval_lr,
+            "optimizer": "adam", "auc_by_step": curve, "chance_auc": 0.5, "final_loss": round(float(tr.loss), 4)}
+
+
 def main(argv=None):
     p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     p.add_argument("--steps", type=int, default=50)
@@ -44,6 +90,9 @@ def main(argv=None):
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--force-dist", action="store_true",
                    help="process group + all-to-all path even with one rank (validates the N>1 path)")
+    p.add_argument("--eval-nodes", type=int, default=1_000_000, help="0: skip the learning-evidence run")
+    p.add_argument("--eval-steps", type=int, default=3000)
+    p.add_argument("--eval-lr", type=float, default=0.05)
     args = p.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -99,6 +148,11 @@ def main(argv=None):
         dist.all_reduce(elt, op=dist.ReduceOp.MAX)
     el = float(elt.item())
     pairs = tr.pairs_per_step() * world * args.steps
+    pairs_per_step, table_comm, loss_last = tr.pairs_per_step(), bool(tr.table.comm), float(tr.loss)
+    peak = torch.cuda.max_memory_allocated() / 2 ** 30
+    del tr, g
+    torch.cuda.empty_cache()
+    heldout = link_prediction_eval(args, dev) if args.eval_nodes > 0 else None
     if rank == 0:
         print(json.dumps({
             "metric": "train pairs/sec (whole node), DeepWalk 128-d skip-gram on 100M-node synthetic graph",
@@ -115,9 +169,9 @@ def main(argv=None):
             "data": "synthetic (power-law random graph, random-init tables)",
             "config": {"model": f"DeepWalk (walk_len 3, window 1/1, 5 negs, row-sparse {args.optimizer})",
                        "num_nodes": args.num_nodes, "dim": args.dim, "walks_per_gpu": args.batch,
-                       "pairs_per_gpu_step": tr.pairs_per_step(), "parallelism": f"dp{world}+sharded-emb", "all_to_all": bool(tr.table.comm),
-                       "loss_first_last": [round(first, 4), round(float(tr.loss), 4)],
-                       "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1)},
+                       "pairs_per_gpu_step": pairs_per_step, "parallelism": f"dp{world}+sharded-emb",
+                       "all_to_all": table_comm, "loss_first_last": [round(first, 4), round(loss_last, 4)],
+                       "peak_mem_gib": round(peak, 1), "heldout_link_prediction": heldout},
         }), flush=True)
     if dist_on:
         dist.barrier()

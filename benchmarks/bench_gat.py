@@ -6,8 +6,12 @@ the training nodes, backward and an Adam step (nothing skipped in the timed regi
 
 Graph: ogbn-products shape — 2,449,029 nodes, ~124M directed edges (avg in-degree ~50,
 power-law), 100-d bf16 features, 47 classes, 8 % training nodes; self-loops added like
-the reference's full flow.  Random graph / random-normal features / labels from a
-random projection (no dataset download is possible), random-init weights.
+the reference's full flow.  Random graph / random-normal features, random-init weights;
+labels are PLANTED in the graph: class = argmax of a random projection of the node's
+neighbourhood-mean features (one SpMM), so they are learnable only through message
+passing.  After the timed epochs training continues (untimed) to --eval-epochs and the
+accuracy on 50K held-out nodes (init / after the timed run / final, vs the majority-class
+rate) goes into the JSON as learning evidence.
 
 Model (reference examples/gat/gat.py:27-86, all heads of a layer in ONE conv here):
   layer l: z = h W_l  ->  [N, 8, 16];  al = <z, a_src>, ar = <z, a_dst> per head
@@ -91,6 +95,19 @@ class GATNet(nn.Module):
         return gnn_ops.tall_linear(hr, self.out.weight, self.out.bias)
 
 
+def planted_labels(indptr, col, x, n_cls, seed=11):
+    """class = argmax of a random projection of the neighbourhood-mean features (self-loop
+    included): a function of the graph, learnable only by aggregating neighbours."""
+    from euler_amd.ops._native import hip
+
+    deg = torch.diff(indptr)
+    w = torch.repeat_interleave(1.0 / deg.clamp(min=1).float(), deg)
+    agg = hip().spmm_csr(indptr, col.long(), w, x.float().contiguous())
+    g = torch.Generator(device=x.device).manual_seed(seed)
+    proj = torch.randn(x.shape[1], n_cls, device=x.device, generator=g)
+    return (agg @ proj).argmax(1)
+
+
 def csr_seg(csr):
     if not hasattr(csr, "_seg"):
         csr._seg = mp_ops.SegmentIndex(csr.edge_index[0].long(), csr.n_dst)
@@ -111,6 +128,7 @@ def main(argv=None):
     p.add_argument("--train-frac", type=float, default=0.08)
     p.add_argument("--impl", choices=["fused", "composed"], default="fused")
     p.add_argument("--seed", type=int, default=7)
+    p.add_argument("--eval-epochs", type=int, default=400)
     args = p.parse_args(argv)
     if not torch.cuda.is_available():
         raise SystemExit("bench_gat.py needs a GPU")
@@ -124,9 +142,10 @@ def main(argv=None):
     csr = gnn_ops.EdgeCSR.from_csr(indptr, col, args.num_nodes)
     N, E = args.num_nodes, int(col.numel())
     x = torch.randn(N, args.feature_dim, device=dev).to(torch.bfloat16)
-    proj = torch.randn(args.feature_dim, args.classes, device=dev)
-    y = (x.float() @ proj).argmax(1)
-    train_idx = torch.randperm(N, device=dev)[: int(N * args.train_frac)]
+    y = planted_labels(indptr, col, x, args.classes)
+    perm = torch.randperm(N, device=dev)
+    train_idx = perm[: int(N * args.train_frac)]
+    test_idx = perm[int(N * args.train_frac):][:50_000]
     y_train = y[train_idx]
     model = GATNet(args.feature_dim, args.heads, args.head_dim, args.classes, 2, args.impl).to(dev)
     opt = torch.optim.Adam(model.parameters(), lr=5e-3, fused=True)
@@ -143,6 +162,13 @@ def main(argv=None):
         opt.step()
         return loss.detach()
 
+    @torch.no_grad()
+    def accuracy():
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            logits = model(x, csr, test_idx)
+        return round(float((logits.float().argmax(1) == y[test_idx]).float().mean()), 4)
+
+    acc_init = accuracy()
     for _ in range(args.warmup):
         loss0 = step()
     torch.cuda.synchronize()
@@ -153,6 +179,12 @@ def main(argv=None):
     torch.cuda.synchronize()
     el = time.perf_counter() - t1
     ms = el * 1e3 / args.epochs
+    acc_timed = accuracy()
+    done = args.warmup + args.epochs
+    while done < args.eval_epochs:  # untimed: learning evidence only
+        step()
+        done += 1
+    acc_final = accuracy()
     out = {
         "metric": "GAT 8-head full-graph training throughput on ogbn-products-shaped synthetic graph",
         "value": round(N * args.epochs / el, 1),
@@ -170,7 +202,11 @@ def main(argv=None):
                    "num_nodes": N, "num_edges": E, "edges_per_s": round(E * 2 * args.epochs / el, 1),
                    "feature_dim": args.feature_dim, "classes": args.classes, "impl": args.impl,
                    "train_nodes": int(train_idx.numel()), "loss_first_last": [round(first, 4), round(float(loss), 4)],
-                   "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2)},
+                   "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2),
+                   "heldout_accuracy": {"nodes": int(test_idx.numel()), "init": acc_init,
+                                        "after_timed_epochs": acc_timed, "final": acc_final, "final_epochs": done,
+                                        "majority_class_rate": round(float(torch.bincount(y, minlength=args.classes)
+                                                                           .max()) / N, 4)}},
     }
     print(json.dumps(out), flush=True)
 

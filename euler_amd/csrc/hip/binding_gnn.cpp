@@ -303,9 +303,10 @@ std::vector<torch::Tensor> occ_csr(torch::Tensor inv, int64_t n_u) {
   const c10::DeviceGuard g(inv.device());
   auto iopt = inv.options();
   auto ptr = torch::zeros({n_u + 1}, iopt);
-  if (inv.numel() > 0) {
-    auto cnt = torch::bincount(inv, {}, n_u);
-    TORCH_CHECK(cnt.numel() == n_u, "occ_csr: inv values must lie in [0, n_u)");
+  if (inv.numel() > 0 && n_u > 0) {
+    // counts by index_add (bincount would read max(inv) back to the host: a sync that
+    // also breaks hipGraph capture); inv values must lie in [0, n_u)
+    auto cnt = torch::zeros({n_u}, iopt).index_add_(0, inv, torch::ones({inv.numel()}, iopt));
     ptr.narrow(0, 1, n_u).copy_(torch::cumsum(cnt, 0));
   }
   auto cursor = torch::zeros({n_u}, iopt.dtype(torch::kInt32));
@@ -476,6 +477,37 @@ std::vector<torch::Tensor> unique_first(torch::Tensor x) {
   return {uniq, inv};
 }
 
+// Fixed-capacity form for graph-captured steps: no host read of the unique count.
+// uniq [n] holds the distinct values in first-occurrence order followed by `fill`,
+// count [1] (device) the number of distinct values.
+std::vector<torch::Tensor> unique_first_padded(torch::Tensor x, int64_t fill) {
+  typed(x, torch::kInt64, "x");
+  const int64_t n = x.numel();
+  TORCH_CHECK(n < (1ll << 30), "unique_first_padded supports < 2^30 elements");
+  const c10::DeviceGuard g(x.device());
+  auto opts = x.options();
+  if (n == 0) return {torch::empty({0}, opts), torch::empty({0}, opts), torch::zeros({1}, opts)};
+  int64_t cap = 1;
+  while (cap < 2 * n) cap <<= 1;
+  auto keys = torch::full({cap}, std::numeric_limits<int64_t>::min(), opts);
+  auto minpos = torch::full({cap}, std::numeric_limits<int32_t>::max(), opts.dtype(torch::kInt32));
+  auto slot = torch::empty({n}, opts.dtype(torch::kInt32));
+  auto flag = torch::empty({n}, opts.dtype(torch::kInt32));
+  ok(eh_unique_insert(x.data_ptr<int64_t>(), n, keys.data_ptr(), minpos.data_ptr<int32_t>(), cap,
+                      slot.data_ptr<int32_t>(), stream()),
+     "unique_insert");
+  ok(eh_unique_mark(n, slot.data_ptr<int32_t>(), minpos.data_ptr<int32_t>(), flag.data_ptr<int32_t>(), stream()),
+     "unique_mark");
+  auto pos = torch::cumsum(flag, 0, torch::kInt32);
+  auto uniq = torch::full({n}, fill, opts);
+  auto inv = torch::empty({n}, opts);
+  ok(eh_unique_finalize(x.data_ptr<int64_t>(), n, slot.data_ptr<int32_t>(), minpos.data_ptr<int32_t>(),
+                        flag.data_ptr<int32_t>(), pos.data_ptr<int32_t>(), inv.data_ptr<int64_t>(),
+                        uniq.data_ptr<int64_t>(), stream()),
+     "unique_finalize");
+  return {uniq, inv, pos.narrow(0, n - 1, 1).to(torch::kInt64)};
+}
+
 }  // namespace
 
 void register_gnn_ops(pybind11::module& m) {
@@ -496,4 +528,5 @@ void register_gnn_ops(pybind11::module& m) {
   m.def("kg_fwd", &kg_fwd);
   m.def("kg_bwd", &kg_bwd);
   m.def("unique_first", &unique_first);
+  m.def("unique_first_padded", &unique_first_padded);
 }

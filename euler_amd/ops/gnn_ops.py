@@ -30,7 +30,7 @@ from euler_amd.ops.mp_ops import SegmentIndex
 
 __all__ = ["EdgeCSR", "gat_aggregate", "gat_aggregate_reference", "RelationTiles", "relation_transform",
            "relation_transform_reference", "sgns_loss", "sgns_loss_reference", "kg_score", "kg_score_reference",
-           "unique_first", "KG_KINDS", "KG_CORRUPT", "sgns_fwd_idx", "occ_csr", "sgns_grad", "tall_linear", "xent"]
+           "unique_first", "unique_first_padded", "KG_KINDS", "KG_CORRUPT", "sgns_fwd_idx", "occ_csr", "sgns_grad", "tall_linear", "xent"]
 
 
 # ----------------------------------------------------------------------------- edge structures
@@ -486,12 +486,25 @@ def sgns_fwd_idx(T, tmap, tinv, C, cmap, cinv, K, gscale):
     return (torch.sigmoid(x) - y) * gscale, loss
 
 
+def unique_first_padded(x: torch.Tensor, fill: int = -1):
+    """Fixed-capacity :func:`unique_first` for graph-captured steps: ``(uniq [n], inverse
+    [n], count [1])`` with the distinct values in first-occurrence order followed by
+    ``fill``; the count stays on the device (GPU: no host sync)."""
+    x = x.reshape(-1)
+    if use_hip(x):
+        return tuple(hip().unique_first_padded(x.long().contiguous(), int(fill)))
+    u, inv = unique_first(x)
+    out = torch.full((x.numel(),), int(fill), dtype=torch.long, device=x.device)
+    out[: u.numel()] = u
+    return out, inv.long(), torch.tensor([u.numel()], dtype=torch.long, device=x.device)
+
+
 def occ_csr(inv, n_u):
     """occurrence lists of ``inv`` (values in [0, n_u)): ``(ptr [n_u+1] int64, list int32)``."""
     inv = inv.reshape(-1).long()
     if use_hip(inv):
         return tuple(hip().occ_csr(inv.contiguous(), int(n_u)))
-    cnt = torch.bincount(inv, minlength=n_u)
+    cnt = torch.zeros(n_u, dtype=torch.long, device=inv.device).index_add_(0, inv, torch.ones_like(inv))
     ptr = torch.zeros(n_u + 1, dtype=torch.long, device=inv.device)
     ptr[1:] = torch.cumsum(cnt, 0)
     return ptr, torch.argsort(inv, stable=True).int()

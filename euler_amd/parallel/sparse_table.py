@@ -17,6 +17,16 @@ a table is explicit (no autograd, no dense gradient of the table):
 With world == 1 the same code runs without collectives.  With 288 GB of HBM a rank
 holds ~100M x 128 fp32 rows plus Adam slots, so DeepWalk/LINE tables of billions of
 rows fit across one node.
+
+Fixed-capacity form (``lookup_static`` / ``apply_static``): for hipGraph-captured steps
+nothing may depend on a host-read size.  Ids arrive padded (-1 = no id, from
+``unique_first_padded``), each owner gets a fixed ``C`` slots per peer, and every
+exchange is an equal-split ``all_to_all_single`` of ``W * C`` entries — no count
+exchange, no ``.cpu()``.  ``C`` = mean + 6 sigma + 64 of the per-owner load of ``n``
+hashed ids (``capacity``); an id that would not fit raises the device-side ``overflow``
+flag (``check_overflow`` reads it, e.g. once per log interval) instead of being silently
+dropped unnoticed.  Expected traffic per step and rank with n ids of D fp32: ids
+8 W C bytes, rows and gradients 2 x 4 D W C bytes, ~3 x n / W of it leaving the rank.
 """
 from __future__ import annotations
 
@@ -29,7 +39,7 @@ from euler_amd.ops import mp_ops
 from euler_amd.ops._native import hip, use_hip
 from euler_amd.ops.gnn_ops import unique_first
 
-__all__ = ["ShardedTable", "LookupHandle"]
+__all__ = ["ShardedTable", "LookupHandle", "StaticHandle"]
 
 _KINDS = {"adam": 0, "adagrad": 1, "sgd": 2}
 
@@ -41,6 +51,15 @@ class LookupHandle:
         self.order, self.send, self.recv, self.local_rows, self.n = order, send, recv, local_rows, n
         # sorted_out lookups: position of ids[k] in the returned (owner-sorted) rows
         self.rank = rank
+
+
+class StaticHandle:
+    """``pos[k]``: slot (in the W*C exchange space) of padded id k (W*C = none);
+    ``local``: the owner-local rows this rank serves per slot (-1 = empty slot)."""
+    __slots__ = ("pos", "local")
+
+    def __init__(self, pos, local):
+        self.pos, self.local = pos, local
 
 
 class ShardedTable:
@@ -66,6 +85,78 @@ class ShardedTable:
         self.m = torch.zeros_like(self.weight) if self.kind == 0 else self.v
         self.step = torch.zeros(1, dtype=torch.int64, device=self.device)
         self.lr, self.b1, self.b2, self.eps = float(lr), float(beta1), float(beta2), float(eps)
+        self.overflow = torch.zeros(1, dtype=torch.int32, device=self.device)
+
+    # ------------------------------------------------------------------ fixed capacity
+    def capacity(self, n: int) -> int:
+        """slots per peer for ``n`` (padded) ids per rank"""
+        if self.world == 1:
+            return int(n)
+        mean = n / self.world
+        return min(int(n), int(math.ceil((mean + 6.0 * math.sqrt(mean) + 64) / 64.0)) * 64)
+
+    def lookup_static(self, ids: torch.Tensor):
+        """rows [W*C, D] in slot order for padded DISTINCT ids [n] (-1 = none) and the
+        :class:`StaticHandle`; row ``handle.pos[k]`` is the row of ``ids[k]``.  Shapes
+        depend on n only: safe inside a hipGraph capture."""
+        ids = ids.reshape(-1).long()
+        n = ids.numel()
+        if not self.comm:
+            pos = torch.arange(n, device=ids.device)
+            return self._gather(ids), StaticHandle(pos, ids)
+        W, C = self.world, self.capacity(n)
+        valid = ids >= 0
+        owner = torch.where(valid, torch.remainder(ids, W), torch.full_like(ids, W))
+        order = torch.sort(owner, stable=True)[1]
+        cnt = torch.zeros(W + 1, dtype=torch.long, device=ids.device).index_add_(0, owner, torch.ones_like(owner))
+        start = torch.cumsum(cnt, 0) - cnt
+        so = owner[order]
+        slot = torch.arange(n, device=ids.device) - start[so]
+        real = so < W
+        fits = real & (slot < C)
+        torch.maximum(self.overflow, (real & ~fits).any().int().view(1), out=self.overflow)
+        trash = W * C
+        dest = torch.where(fits, so * C + slot, torch.full_like(slot, trash))
+        send = torch.full((trash + 1,), -1, dtype=torch.long, device=ids.device)
+        send.scatter_(0, dest, torch.where(fits, ids[order], torch.full_like(slot, -1)))
+        pos = torch.empty_like(dest)
+        pos[order] = dest
+        recv = torch.empty(trash, dtype=torch.long, device=ids.device)
+        dist.all_to_all_single(recv, send[:trash], group=self.group)
+        local = torch.where(recv >= 0, torch.div(recv, W, rounding_mode="floor"), torch.full_like(recv, -1))
+        rows = self._gather(local)
+        out = torch.empty_like(rows)
+        dist.all_to_all_single(out, rows, group=self.group)
+        return out, StaticHandle(pos, local)
+
+    def apply_static(self, handle: StaticHandle, grad_rows: torch.Tensor):
+        """row-sparse update from gradients [W*C, D] in slot order (rows of empty slots
+        are ignored)."""
+        g = grad_rows.float().contiguous()
+        rows = handle.local
+        if self.comm:
+            recv_g = torch.empty_like(g)
+            dist.all_to_all_single(recv_g, g, group=self.group)
+            g = recv_g
+            if self.world > 1:
+                # several ranks may have asked for the same row: merge (the -1 bucket of
+                # empty slots collects their rows and is skipped by the update)
+                from euler_amd.ops.gnn_ops import unique_first_padded
+
+                rows_u, inv, _ = unique_first_padded(rows)
+                acc = torch.zeros_like(g)
+                if use_hip(acc, inv):
+                    hip().index_add_rows_(acc, inv.contiguous(), g)
+                else:
+                    acc.index_add_(0, inv, g)
+                rows, g = rows_u, acc
+        self._update(rows.contiguous(), g)
+
+    def check_overflow(self):
+        """host read of the overflow flag of the fixed-capacity exchanges (a sync)"""
+        if int(self.overflow.item()):
+            raise RuntimeError("ShardedTable: a fixed-capacity exchange overflowed its per-peer slots; "
+                               "ids were dropped (raise the capacity or use lookup/apply)")
 
     # ------------------------------------------------------------------ forward
     def lookup(self, ids: torch.Tensor, sorted_out: bool = False):

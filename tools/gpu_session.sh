@@ -76,6 +76,12 @@ for st in "${S[@]}"; do
     cpu_baseline)
       run cpu_baseline 900 python -u -m euler_amd.tools.cpu_baseline --num-nodes 100000000 --threads 16 \
         --sweep 4,8,16 --out "$OUT/cpu_baseline.json" ;;
+    learn_kg)
+      run bench_kg 600 python -u benchmarks/bench_kg.py ;;
+    learn_gat)
+      run bench_gat 900 python -u benchmarks/bench_gat.py ;;
+    learn_deepwalk)
+      run bench_deepwalk 900 python -u benchmarks/bench_deepwalk.py ;;
     kernels_full)
       run tree_kernels_full 300 python -u tools/tree_kernels.py --num-nodes 100000000 ;;
     kernels_sizes)
