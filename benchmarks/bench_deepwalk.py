@@ -90,6 +90,9 @@ def main(argv=None):
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--force-dist", action="store_true",
                    help="process group + all-to-all path even with one rank (validates the N>1 path)")
+    p.add_argument("--mode", choices=["graph", "static", "dynamic"], default="graph",
+                   help="graph: fixed-capacity step captured in one hipGraph and replayed; static: the same "
+                        "step eager; dynamic: exact-size step (host-read unique counts / all-to-all splits)")
     p.add_argument("--eval-nodes", type=int, default=1_000_000, help="0: skip the learning-evidence run")
     p.add_argument("--eval-steps", type=int, default=3000)
     p.add_argument("--eval-lr", type=float, default=0.05)
@@ -122,17 +125,20 @@ def main(argv=None):
     g = DeviceGraph.synthetic(args.num_nodes, args.avg_degree, args.max_degree, seed=args.seed, device=dev)
     g.manual_seed(args.seed * 7919 + rank)
     tr = DeepWalkTrainer(g, args.num_nodes, args.dim, args.walk_len, 1, 1, args.num_negs, args.batch, args.lr,
-                         args.optimizer, seed=args.seed, force_comm=args.force_dist)
+                         args.optimizer, seed=args.seed, force_comm=args.force_dist, static=args.mode != "dynamic")
     torch.cuda.synchronize()
     if rank == 0:
         gib = tr.table.nbytes() / 2 ** 30
         print(f"[bench_deepwalk] {args.num_nodes} nodes, {g.num_edges} edges, tables+slots {gib:.1f} GiB/rank, "
               f"setup {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
 
-    for _ in range(args.warmup):
-        tr.step()
+    if args.mode == "graph":
+        tr.capture(warm=max(1, args.warmup))  # warm-up steps run inside, then one step is captured
+    else:
+        for _ in range(args.warmup):
+            tr.step()
     torch.cuda.synchronize()
-    first = float(tr.loss)
+    first = float(tr.warm_loss if args.mode == "graph" else tr.loss)
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
@@ -148,8 +154,10 @@ def main(argv=None):
         dist.all_reduce(elt, op=dist.ReduceOp.MAX)
     el = float(elt.item())
     pairs = tr.pairs_per_step() * world * args.steps
+    tr.table.check_overflow()
     pairs_per_step, table_comm, loss_last = tr.pairs_per_step(), bool(tr.table.comm), float(tr.loss)
     peak = torch.cuda.max_memory_allocated() / 2 ** 30
+    tr.release()
     del tr, g
     torch.cuda.empty_cache()
     heldout = link_prediction_eval(args, dev) if args.eval_nodes > 0 else None
@@ -170,7 +178,8 @@ def main(argv=None):
             "config": {"model": f"DeepWalk (walk_len 3, window 1/1, 5 negs, row-sparse {args.optimizer})",
                        "num_nodes": args.num_nodes, "dim": args.dim, "walks_per_gpu": args.batch,
                        "pairs_per_gpu_step": pairs_per_step, "parallelism": f"dp{world}+sharded-emb",
-                       "all_to_all": table_comm, "loss_first_last": [round(first, 4), round(loss_last, 4)],
+                       "all_to_all": table_comm, "step_mode": args.mode,
+                       "loss_first_last": [round(first, 4), round(loss_last, 4)],
                        "peak_mem_gib": round(peak, 1), "heldout_link_prediction": heldout},
         }), flush=True)
     if dist_on:

@@ -276,11 +276,16 @@ class DeviceGraph:
         if float(p) <= 0.0 or float(q) <= 0.0:
             raise ValueError("random_walk: p and q must be positive")
         starts = starts.reshape(-1).int()
-        masks = torch.tensor([self._mask(edge_types)] * int(walk_len), dtype=torch.int64)
-        masks = ((masks + 2 ** 31) % 2 ** 32 - 2 ** 31).int()
         if use_hip(self.indptr, starts):
+            # per-step type masks: built once per (mask, length) and kept on the device, so a
+            # walk inside a hipGraph capture issues no host->device copy
+            key = (self._mask(edge_types), int(walk_len))
+            cache = self.__dict__.setdefault("_walk_masks", {})
+            if key not in cache:
+                m = torch.tensor([key[0]] * key[1], dtype=torch.int64)
+                cache[key] = ((m + 2 ** 31) % 2 ** 32 - 2 ** 31).int().to(self.device)
             return hip().random_walk(self.indptr, self.nbr, self.cumw, self.num_rows, self.num_types,
-                                     masks.to(self.device), starts.contiguous(), int(default), self.rng,
+                                     cache[key], starts.contiguous(), int(default), self.rng,
                                      int(stream_id), float(p), float(q))
         if float(p) == 1.0 and float(q) == 1.0:
             cols = [starts]

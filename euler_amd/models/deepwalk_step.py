@@ -27,6 +27,13 @@ One step here, per rank (no autograd, no dense table gradient):
 
 Padding: a walk that hits a node without out-edges continues with the pad row
 ``num_nodes`` (the reference's ``max_id + 1`` default node).
+
+Static mode (``static=True``): the unique id sets are fixed-capacity (padded with -1 by
+``unique_first_padded``, count kept on the device), occurrence lists are built over the
+capacities, and with collectives the table exchange is ShardedTable.lookup_static /
+apply_static (equal-split all-to-alls of W x C slots).  No step size is read back to the
+host, so :meth:`capture` records the whole step — sampling, unique, (all-to-all), loss,
+row-sparse update — into one hipGraph that :meth:`step` replays.
 """
 from __future__ import annotations
 
@@ -47,7 +54,7 @@ def _pair_positions(walk_len, left, right):
 
 class DeepWalkTrainer:
     def __init__(self, graph, num_nodes, dim=128, walk_len=3, left_win_size=1, right_win_size=1, num_negs=5,
-                 batch_size=1024, lr=0.01, optimizer="adam", group=None, seed=0, force_comm=False):
+                 batch_size=1024, lr=0.01, optimizer="adam", group=None, seed=0, force_comm=False, static=False):
         self.graph = graph
         self.num_nodes = int(num_nodes)
         self.pad = self.num_nodes  # rows: num_nodes + 1 (pad row like the reference's max_id + 1)
@@ -63,6 +70,8 @@ class DeepWalkTrainer:
         self.pi, self.pj = pi.to(dev), pj.to(dev)
         self.pairs_per_walk = int(pi.numel())
         self.loss = torch.zeros((), device=dev)
+        self.static = bool(static)
+        self.hip_graph = None
 
     def _gather(self, rows, inv):
         if use_hip(rows, inv):
@@ -82,6 +91,74 @@ class DeepWalkTrainer:
         return src, pos, negs
 
     def step(self):
+        if self.hip_graph is not None:
+            self.hip_graph.replay()
+            return self.loss
+        return self._step_static() if self.static else self._step_dynamic()
+
+    def capture(self, warm=2):
+        """Record one static step into a hipGraph (after ``warm`` real eager steps on a side
+        stream, which allocate the kernels' workspaces; ``warm_loss`` is the last one's
+        loss); later :meth:`step` calls replay it.  Capturing executes nothing, so
+        ``self.loss`` (the graph's output) is valid after the first replay."""
+        if not (self.static and self.device.type == "cuda"):
+            raise ValueError("capture needs static=True on a GPU")
+        cur = torch.cuda.current_stream()
+        side = torch.cuda.Stream()
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            for _ in range(int(warm)):
+                self.warm_loss = self._step_static()
+        cur.wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._step_static()
+        self.hip_graph = g
+        return g
+
+    def release(self):
+        """Drop the captured graph (do this before destroying a process group whose
+        collectives it recorded: a live graph keeps the communicator's work pending)."""
+        if self.hip_graph is not None:
+            torch.cuda.synchronize()
+            self.hip_graph.reset()
+            self.hip_graph = None
+
+    def _step_static(self):
+        src, pos, negs = self.sample()
+        P, K = src.numel(), self.num_negs
+        gscale = 1.0 / (P * (1 + K))
+        u_t, inv_t, _ = gnn_ops.unique_first_padded(src)
+        u_c, inv_c, _ = gnn_ops.unique_first_padded(torch.cat([pos, negs.reshape(-1)]))
+        rows_c_id = torch.where(u_c >= 0, u_c + self.off, u_c)
+        tab = self.table
+        if tab.fused_sgns_ok(u_t):
+            ptr_t, lst_t = gnn_ops.occ_csr(inv_t, u_t.numel())
+            ptr_c, lst_c = gnn_ops.occ_csr(inv_c, u_c.numel())
+            W = tab.weight
+            coef, loss_rows = gnn_ops.sgns_fwd_idx(W, u_t, inv_t, W, rows_c_id, inv_c, K, gscale)
+            rt = self._gather(W, u_t)                       # pre-update target rows (pad: zero)
+            tab.apply_sgns(0, ptr_t, lst_t, coef, K, W, rows_c_id, inv_c, u_t)
+            tab.apply_sgns(1, ptr_c, lst_c, coef, K, rt, None, inv_t, rows_c_id, inc_step=False)
+        else:
+            ids = torch.cat([u_t, rows_c_id])
+            rows, h = tab.lookup_static(ids)
+            n = rows.shape[0]
+            # a dropped id (overflow flag raised) points at the last slot: wrong but in bounds
+            slot = h.pos.clamp(max=n - 1)
+            tinv = slot[inv_t]
+            cinv = slot[u_t.numel() + inv_c]
+            coef, loss_rows = gnn_ops.sgns_fwd_idx(rows, None, tinv, rows, None, cinv, K, gscale)
+            ptr_t, lst_t = gnn_ops.occ_csr(tinv, n)
+            ptr_c, lst_c = gnn_ops.occ_csr(cinv, n)
+            g = torch.zeros_like(rows)
+            gnn_ops.sgns_grad(0, ptr_t, lst_t, coef, K, rows, None, cinv, inv_self=tinv, out=g)
+            gnn_ops.sgns_grad(1, ptr_c, lst_c, coef, K, rows, None, tinv, inv_self=cinv, out=g)
+            tab.apply_static(h, g)
+        self.loss = loss_rows.sum() * gscale
+        return self.loss
+
+    def _step_dynamic(self):
         src, pos, negs = self.sample()
         P, K = src.numel(), self.num_negs
         gscale = 1.0 / (P * (1 + K))

@@ -86,10 +86,13 @@ class ShardedTable:
         self.step = torch.zeros(1, dtype=torch.int64, device=self.device)
         self.lr, self.b1, self.b2, self.eps = float(lr), float(beta1), float(beta2), float(eps)
         self.overflow = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.cap_override = None  # fixed per-peer slot count (tests / tuning)
 
     # ------------------------------------------------------------------ fixed capacity
     def capacity(self, n: int) -> int:
         """slots per peer for ``n`` (padded) ids per rank"""
+        if self.cap_override is not None:
+            return int(self.cap_override)
         if self.world == 1:
             return int(n)
         mean = n / self.world
@@ -229,6 +232,9 @@ class ShardedTable:
             hip().sparse_optim_(self.weight, self.m, self.v, rows, g, self.step, self.lr, self.b1, self.b2,
                                 self.eps, self.kind)
             return
+        keep = (rows >= 0) & (rows < self.weight.shape[0])  # -1: empty slot (fixed-capacity path)
+        if not bool(keep.all()):
+            rows, g = rows[keep], g[keep]
         self.step += 1
         if self.kind == 0:
             t = float(self.step.item())

@@ -199,6 +199,76 @@ def _worker_deepwalk(rank, world, port, q):
         q.put((rank, "error", repr(e)))
 
 
+def _worker_sparse_table_static(rank, world, port, q):
+    try:
+        _init(rank, world, port)
+        from euler_amd.ops.gnn_ops import unique_first_padded
+        from euler_amd.parallel.sparse_table import ShardedTable
+
+        torch.manual_seed(0)
+        full = torch.randn(31, 4)
+        tab = ShardedTable(31, 4, "cpu", optimizer="sgd", lr=0.5)
+        tab.weight.copy_(full[tab.global_ids()])
+        raw = torch.tensor([3, 29, 7, 12, 3, 0, 7]) + rank
+        u, inv, cnt = unique_first_padded(raw)          # 5 distinct + two -1 pads
+        ok_pad = int(cnt) == 5 and u[5:].tolist() == [-1, -1] and torch.equal(u[inv], raw)
+        rows, h = tab.lookup_static(u)
+        assert rows.shape[0] == world * tab.capacity(u.numel())
+        ok_fwd = torch.allclose(rows[h.pos[:5]], full[u[:5]])
+        g_slot = torch.zeros_like(rows)
+        g_id = torch.arange(5 * 4, dtype=torch.float32).view(5, 4) + 100 * rank
+        g_slot[h.pos[:5]] = g_id
+        tab.apply_static(h, g_slot)
+        exp = full.clone()
+        for r in range(world):
+            ur, _, _ = unique_first_padded(torch.tensor([3, 29, 7, 12, 3, 0, 7]) + r)
+            gr = torch.arange(5 * 4, dtype=torch.float32).view(5, 4) + 100 * r
+            exp.index_add_(0, ur[:5], -0.5 * gr)
+        ok_upd = torch.allclose(tab.weight, exp[tab.global_ids()])
+        tab.check_overflow()
+        # a too-small capacity raises the device flag instead of silently dropping ids
+        tab.cap_override = 1
+        tab.lookup_static(u)
+        try:
+            tab.check_overflow()
+            ok_flag = False
+        except RuntimeError:
+            ok_flag = True
+        q.put((rank, "sparse_table_static", bool(ok_pad and ok_fwd and ok_upd and ok_flag)))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, "error", repr(e)))
+
+
+def _worker_deepwalk_static(rank, world, port, q):
+    try:
+        _init(rank, world, port)
+        from euler_amd.graph.device_graph import DeviceGraph
+        from euler_amd.models.deepwalk_step import DeepWalkTrainer
+
+        g = DeviceGraph.synthetic(400, 6.0, 40, seed=3, device="cpu")
+        g.manual_seed(11 + rank)
+        tr = DeepWalkTrainer(g, 400, dim=16, batch_size=64, lr=0.05, optimizer="adagrad", seed=5, static=True)
+        losses = [float(tr.step()) for _ in range(30)]
+        tr.table.check_overflow()
+        q.put((rank, "deepwalk_static", bool(sum(losses[-5:]) < sum(losses[:5]))))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, "error", repr(e)))
+
+
+def test_sharded_table_fixed_capacity_exchange():
+    res = _run(_worker_sparse_table_static)
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == 2 and all(r[2] for r in res), res
+
+
+def test_deepwalk_static_two_ranks():
+    res = _run(_worker_deepwalk_static)
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == 2 and all(r[2] for r in res), res
+
+
 def test_sharded_table_row_sparse_update():
     res = _run(_worker_sparse_table)
     assert not [r for r in res if r[1] == "error"], res

@@ -36,7 +36,7 @@ for st in "${S[@]}"; do
     debug)
       EULER_AMD_TREE_SYNC=1 run tree_debug 300 python -u tools/tree_debug.py 0 1 2 3 4 5 6 7 8 9 || exit 71 ;;
     tests)
-      run pytest_gpu 900 python -u -m pytest $TESTS -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -rf ;;
+      run pytest_gpu 900 python -u -m pytest $TESTS -x -v --timeout 120 --timeout-method thread -p no:cacheprovider -rf ;;
     kernels)
       run tree_kernels 300 python -u tools/tree_kernels.py ;;
     sweep_dw)
@@ -82,6 +82,19 @@ for st in "${S[@]}"; do
       run bench_gat 900 python -u benchmarks/bench_gat.py ;;
     learn_deepwalk)
       run bench_deepwalk 900 python -u benchmarks/bench_deepwalk.py ;;
+    deepwalk_modes)
+      for m in dynamic static graph; do
+        run "deepwalk_$m" 600 python -u benchmarks/bench_deepwalk.py --eval-nodes 0 --mode $m || exit $?
+        run "deepwalk_${m}_dist" 600 python -u -m torch.distributed.run --nnodes 1 --nproc-per-node 1 \
+          --master-addr 127.0.0.1 --master-port 29531 benchmarks/bench_deepwalk.py --eval-nodes 0 --mode $m \
+          --force-dist || exit $?
+      done ;;
+    deepwalk_prof)
+      run deepwalk_prof_local 600 rocprofv3 --kernel-trace --stats -d "$OUT/dw_prof_local" -o run --output-format csv -- \
+          python3 benchmarks/bench_deepwalk.py --eval-nodes 0 --mode static --steps 20 || exit $?
+      RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29533 \
+        run deepwalk_prof_dist 600 rocprofv3 --kernel-trace --stats -d "$OUT/dw_prof_dist" -o run --output-format csv -- \
+          python3 benchmarks/bench_deepwalk.py --eval-nodes 0 --mode static --steps 20 --force-dist ;;
     kernels_full)
       run tree_kernels_full 300 python -u tools/tree_kernels.py --num-nodes 100000000 ;;
     kernels_sizes)
