@@ -502,6 +502,7 @@ class PyServer {
     opt.registry = registry;
     opt.host = host;
     opt.heartbeat_ms = heartbeat_ms;
+    if (const char* e = std::getenv("EULER_RPC_IO_THREADS")) opt.io_threads = std::max(1, std::atoi(e));
     server_.reset(new GraphServer(env_.get(), shard_idx, shard_num, opt));
     Throw(server_->Start());
   }

@@ -5,6 +5,8 @@
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
 #include <sys/socket.h>
 #include <fcntl.h>
 #include <sys/stat.h>
@@ -14,7 +16,9 @@
 #include <algorithm>
 #include <cstdlib>
 #include <chrono>
+#include <deque>
 #include <set>
+#include <unordered_map>
 
 namespace euler {
 
@@ -489,6 +493,39 @@ std::unique_ptr<Registry> Registry::Open(const std::string& spec) {
 }
 
 // ============================================================================ GraphServer
+// Event-driven server: accept threads hand each connection to one of `io_threads` epoll
+// loops (non-blocking sockets, level-triggered).  A loop reassembles frames from its
+// connections' byte streams, answers ping / meta inline and schedules DAG executions on
+// the worker pool; a finished execution is posted back to the connection's loop
+// (mutex-protected completion queue + eventfd wake-up), which writes the reply without
+// blocking (EPOLLOUT while a reply is partially sent).  Threads do not grow with the
+// number of client connections (8 ranks x many workers x S shards), unlike the
+// thread-per-connection design it replaces.
+struct GraphServer::Conn {
+  int fd = -1;
+  std::string in;       // received bytes not yet consumed
+  size_t in_off = 0;
+  std::string out;      // reply bytes not yet written
+  size_t out_off = 0;
+  bool busy = false;    // an execution of this connection is in flight (one at a time)
+  bool closed = false;
+  bool want_out = false;
+};
+
+struct GraphServer::Loop {
+  int ep = -1, wake = -1;
+  std::thread th;
+  std::unordered_map<int, std::shared_ptr<Conn>> conns;  // loop thread only
+  std::mutex mu;                                           // guards the queues below
+  std::vector<int> incoming;                                // accepted fds to adopt
+  std::vector<std::pair<std::shared_ptr<Conn>, std::string>> done;  // finished replies
+  void Wake() {
+    const uint64_t one = 1;
+    ssize_t r = ::write(wake, &one, sizeof(one));
+    (void)r;
+  }
+};
+
 GraphServer::GraphServer(EngineEnv* env, int shard_idx, int shard_num, const ServerOptions& opt)
     : env_(env), shard_idx_(shard_idx), shard_num_(shard_num), opt_(opt) {
   host_ = opt.host.empty() ? "127.0.0.1" : opt.host;
@@ -508,19 +545,33 @@ Status GraphServer::Start() {
   addr.sin_port = htons(static_cast<uint16_t>(opt_.port));
   if (bind(listen_fd_, reinterpret_cast<sockaddr*>(&addr), sizeof(addr)) != 0)
     return Status::Internal("bind failed on port " + std::to_string(opt_.port) + ": " + strerror(errno));
-  if (listen(listen_fd_, 128) != 0) return Status::Internal("listen failed");
+  if (listen(listen_fd_, 1024) != 0) return Status::Internal("listen failed");
   socklen_t len = sizeof(addr);
   getsockname(listen_fd_, reinterpret_cast<sockaddr*>(&addr), &len);
   port_ = ntohs(addr.sin_port);
   pool_.reset(new ThreadPool(std::max(1, opt_.num_threads), "euler-server"));
   running_ = true;
+  for (int i = 0; i < std::max(1, opt_.io_threads); ++i) {
+    std::unique_ptr<Loop> lp(new Loop);
+    lp->ep = epoll_create1(EPOLL_CLOEXEC);
+    lp->wake = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    if (lp->ep < 0 || lp->wake < 0) return Status::Internal("epoll/eventfd failed");
+    struct epoll_event ev;
+    memset(&ev, 0, sizeof(ev));
+    ev.events = EPOLLIN;
+    ev.data.fd = lp->wake;
+    epoll_ctl(lp->ep, EPOLL_CTL_ADD, lp->wake, &ev);
+    Loop* raw = lp.get();
+    lp->th = std::thread([this, raw] { RunLoop(raw); });
+    loops_.push_back(std::move(lp));
+  }
   accept_thread_ = std::thread([this] { AcceptLoop(listen_fd_); });
   // same-host listener (abstract Unix socket keyed by the TCP port); best effort
   local_fd_ = socket(AF_UNIX, SOCK_STREAM, 0);
   if (local_fd_ >= 0) {
     struct sockaddr_un ua;
     const socklen_t ulen = AbstractAddr(port_, &ua);
-    if (bind(local_fd_, reinterpret_cast<sockaddr*>(&ua), ulen) == 0 && listen(local_fd_, 128) == 0) {
+    if (bind(local_fd_, reinterpret_cast<sockaddr*>(&ua), ulen) == 0 && listen(local_fd_, 1024) == 0) {
       local_accept_thread_ = std::thread([this] { AcceptLoop(local_fd_); });
     } else {
       close(local_fd_);
@@ -549,7 +600,8 @@ Status GraphServer::Start() {
       });
     }
   }
-  EULER_LOG(Info) << "graph server shard " << shard_idx_ << "/" << shard_num_ << " listening on " << port_;
+  EULER_LOG(Info) << "graph server shard " << shard_idx_ << "/" << shard_num_ << " listening on " << port_
+                  << " (" << loops_.size() << " epoll loops, " << opt_.num_threads << " workers)";
   return Status::OK();
 }
 
@@ -567,71 +619,235 @@ void GraphServer::Stop() {
   }
   if (accept_thread_.joinable()) accept_thread_.join();
   if (local_accept_thread_.joinable()) local_accept_thread_.join();
-  std::vector<std::thread> ts;
-  {
-    std::lock_guard<std::mutex> l(conn_mu_);
-    for (int fd : conn_fds_) shutdown(fd, SHUT_RDWR);
-    ts.swap(conn_threads_);
-  }
-  for (auto& t : ts)
-    if (t.joinable()) t.join();
+  // running executions finish first (their completions are then discarded)
   pool_.reset();
+  for (auto& lp : loops_) lp->Wake();
+  for (auto& lp : loops_) {
+    if (lp->th.joinable()) lp->th.join();
+    for (auto& kv : lp->conns) close(kv.first);
+    {
+      std::lock_guard<std::mutex> l(lp->mu);
+      for (int fd : lp->incoming) close(fd);
+      lp->incoming.clear();
+      lp->done.clear();
+    }
+    close(lp->ep);
+    close(lp->wake);
+  }
+  loops_.clear();
 }
 
 void GraphServer::AcceptLoop(int lfd) {
   while (running_) {
-    int fd = accept(lfd, nullptr, nullptr);
+    int fd = accept4(lfd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
     if (fd < 0) {
       if (!running_) break;
       continue;
     }
     int one = 1;
-    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
-    std::lock_guard<std::mutex> l(conn_mu_);
-    conn_fds_.push_back(fd);
-    conn_threads_.emplace_back([this, fd] { Serve(fd); });
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));  // fails harmlessly on Unix sockets
+    Loop* lp = loops_[next_loop_.fetch_add(1) % loops_.size()].get();
+    {
+      std::lock_guard<std::mutex> l(lp->mu);
+      lp->incoming.push_back(fd);
+    }
+    lp->Wake();
   }
 }
 
-void GraphServer::Serve(int fd) {
-  uint32_t kind;
-  std::string payload;
-  while (running_ && RecvFrame(fd, &kind, &payload)) {
+void GraphServer::RunLoop(Loop* lp) {
+  std::vector<struct epoll_event> evs(256);
+  while (running_) {
+    const int n = epoll_wait(lp->ep, evs.data(), static_cast<int>(evs.size()), 200);
+    if (n < 0 && errno != EINTR) break;
+    for (int i = 0; i < std::max(n, 0); ++i) {
+      const int fd = evs[i].data.fd;
+      if (fd == lp->wake) {
+        uint64_t v;
+        while (::read(lp->wake, &v, sizeof(v)) > 0) {
+        }
+        continue;
+      }
+      auto it = lp->conns.find(fd);
+      if (it == lp->conns.end()) continue;
+      std::shared_ptr<Conn> c = it->second;
+      if (evs[i].events & (EPOLLERR | EPOLLHUP)) {
+        if (!(evs[i].events & EPOLLIN)) {
+          Drop(lp, c);
+          continue;
+        }
+      }
+      if (evs[i].events & EPOLLOUT) Flush(lp, c);
+      if (!c->closed && (evs[i].events & EPOLLIN)) OnReadable(lp, c);
+    }
+    // adopt new connections, deliver finished executions
+    std::vector<int> inc;
+    std::vector<std::pair<std::shared_ptr<Conn>, std::string>> done;
+    {
+      std::lock_guard<std::mutex> l(lp->mu);
+      inc.swap(lp->incoming);
+      done.swap(lp->done);
+    }
+    for (int fd : inc) {
+      auto c = std::make_shared<Conn>();
+      c->fd = fd;
+      struct epoll_event ev;
+      memset(&ev, 0, sizeof(ev));
+      ev.events = EPOLLIN;
+      ev.data.fd = fd;
+      if (epoll_ctl(lp->ep, EPOLL_CTL_ADD, fd, &ev) != 0) {
+        close(fd);
+        continue;
+      }
+      lp->conns[fd] = c;
+    }
+    for (auto& d : done) {
+      std::shared_ptr<Conn> c = d.first;
+      c->busy = false;
+      if (c->closed) continue;
+      c->out.append(d.second);
+      Flush(lp, c);
+      if (!c->closed) Dispatch(lp, c);  // a pipelined next request may already be buffered
+    }
+  }
+}
+
+void GraphServer::OnReadable(Loop* lp, const std::shared_ptr<Conn>& c) {
+  char buf[1 << 16];
+  for (;;) {
+    const ssize_t k = ::recv(c->fd, buf, sizeof(buf), 0);
+    if (k > 0) {
+      c->in.append(buf, static_cast<size_t>(k));
+      continue;
+    }
+    if (k < 0 && errno == EINTR) continue;
+    if (k < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) break;
+    Drop(lp, c);  // orderly shutdown or error
+    return;
+  }
+  Dispatch(lp, c);
+}
+
+void GraphServer::Dispatch(Loop* lp, const std::shared_ptr<Conn>& c) {
+  while (!c->busy && !c->closed) {
+    const size_t avail = c->in.size() - c->in_off;
+    if (avail < 16) break;
+    const char* h = c->in.data() + c->in_off;
+    uint32_t magic, kind;
+    uint64_t len;
+    memcpy(&magic, h, 4);
+    memcpy(&kind, h + 4, 4);
+    memcpy(&len, h + 8, 8);
+    if (magic != kMagic || len > (1ULL << 36)) {
+      Drop(lp, c);
+      return;
+    }
+    if (avail < 16 + len) break;
+    std::string payload(h + 16, static_cast<size_t>(len));
+    c->in_off += 16 + len;
+    if (c->in_off == c->in.size()) {
+      c->in.clear();
+      c->in_off = 0;
+    } else if (c->in_off > (1u << 20)) {
+      c->in.erase(0, c->in_off);
+      c->in_off = 0;
+    }
     requests_++;
     EngineCounters::Get().server_requests.fetch_add(1, std::memory_order_relaxed);
-    ScopedMicros timing(&EngineCounters::Get().server_us);
-    std::string reply;
-    if (kind == kPing) {
-      reply = EncodeReply(Status::OK(), {});
-    } else if (kind == kMeta) {
-      reply = EncodeReply(Status::OK(), {Tensor::Strings({ShardMeta::FromEnv(*env_, shard_idx_, shard_num_).ToString()})});
-    } else if (kind == kExecute) {
-      DAGDef dag;
-      std::vector<std::pair<std::string, Tensor>> inputs;
-      std::vector<std::string> outputs;
-      if (!DecodeExecute(payload, &dag, &inputs, &outputs)) {
-        reply = EncodeReply(Status::RpcError("malformed execute request"), {});
-      } else {
-        std::vector<Tensor> res;
-        Status st;
-        Latch latch(1);
-        pool_->Schedule([&] {
-          try {
-            st = ExecuteDag(env_, dag, inputs, outputs, &res);
-          } catch (const std::exception& e) {
-            st = Status::Internal(e.what());
-          }
-          latch.CountDown();
-        });
-        latch.Wait();
-        reply = EncodeReply(st, res);
-      }
-    } else {
-      reply = EncodeReply(Status::Unimplemented("unknown request kind"), {});
+    if (kind != kExecute) {
+      std::string reply = Handle(kind, payload);
+      char hdr[16];
+      const uint64_t rl = reply.size();
+      const uint32_t rk = kReply;
+      memcpy(hdr, &kMagic, 4);
+      memcpy(hdr + 4, &rk, 4);
+      memcpy(hdr + 8, &rl, 8);
+      c->out.append(hdr, 16);
+      c->out.append(reply);
+      Flush(lp, c);
+      continue;
     }
-    if (!SendFrame(fd, kReply, reply)) break;
+    c->busy = true;
+    std::shared_ptr<Conn> keep = c;
+    pool_->Schedule([this, lp, keep, payload = std::move(payload)] {
+      std::string reply = Handle(kExecute, payload);
+      char hdr[16];
+      const uint64_t rl = reply.size();
+      const uint32_t rk = kReply;
+      memcpy(hdr, &kMagic, 4);
+      memcpy(hdr + 4, &rk, 4);
+      memcpy(hdr + 8, &rl, 8);
+      std::string frame(hdr, 16);
+      frame.append(reply);
+      {
+        std::lock_guard<std::mutex> l(lp->mu);
+        lp->done.emplace_back(keep, std::move(frame));
+      }
+      lp->Wake();
+    });
   }
-  close(fd);
+}
+
+void GraphServer::Flush(Loop* lp, const std::shared_ptr<Conn>& c) {
+  while (c->out_off < c->out.size()) {
+    const ssize_t k = ::send(c->fd, c->out.data() + c->out_off, c->out.size() - c->out_off, MSG_NOSIGNAL);
+    if (k > 0) {
+      c->out_off += static_cast<size_t>(k);
+      continue;
+    }
+    if (k < 0 && errno == EINTR) continue;
+    if (k < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+      if (!c->want_out) {
+        struct epoll_event ev;
+        memset(&ev, 0, sizeof(ev));
+        ev.events = EPOLLIN | EPOLLOUT;
+        ev.data.fd = c->fd;
+        epoll_ctl(lp->ep, EPOLL_CTL_MOD, c->fd, &ev);
+        c->want_out = true;
+      }
+      return;
+    }
+    Drop(lp, c);
+    return;
+  }
+  c->out.clear();
+  c->out_off = 0;
+  if (c->want_out) {
+    struct epoll_event ev;
+    memset(&ev, 0, sizeof(ev));
+    ev.events = EPOLLIN;
+    ev.data.fd = c->fd;
+    epoll_ctl(lp->ep, EPOLL_CTL_MOD, c->fd, &ev);
+    c->want_out = false;
+  }
+}
+
+void GraphServer::Drop(Loop* lp, const std::shared_ptr<Conn>& c) {
+  if (c->closed) return;
+  c->closed = true;
+  epoll_ctl(lp->ep, EPOLL_CTL_DEL, c->fd, nullptr);
+  close(c->fd);
+  lp->conns.erase(c->fd);
+}
+
+std::string GraphServer::Handle(uint32_t kind, const std::string& payload) {
+  ScopedMicros timing(&EngineCounters::Get().server_us);
+  if (kind == kPing) return EncodeReply(Status::OK(), {});
+  if (kind == kMeta)
+    return EncodeReply(Status::OK(), {Tensor::Strings({ShardMeta::FromEnv(*env_, shard_idx_, shard_num_).ToString()})});
+  if (kind != kExecute) return EncodeReply(Status::Unimplemented("unknown request kind"), {});
+  DAGDef dag;
+  std::vector<std::pair<std::string, Tensor>> inputs;
+  std::vector<std::string> outputs;
+  if (!DecodeExecute(payload, &dag, &inputs, &outputs)) return EncodeReply(Status::RpcError("malformed execute request"), {});
+  std::vector<Tensor> res;
+  Status st;
+  try {
+    st = ExecuteDag(env_, dag, inputs, outputs, &res);
+  } catch (const std::exception& e) {
+    st = Status::Internal(e.what());
+  }
+  return EncodeReply(st, res);
 }
 
 // ============================================================================ RpcClients

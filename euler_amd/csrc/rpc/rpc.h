@@ -101,7 +101,8 @@ class Registry {
 struct ServerOptions {
   int port = 0;  // 0: ephemeral
   std::string host;  // advertised host (default: 127.0.0.1)
-  int num_threads = 32;
+  int num_threads = 32;   // DAG execution workers
+  int io_threads = 2;     // epoll event loops (connections are spread over them)
   std::string registry;  // optional
   int heartbeat_ms = 1000;  // registry entry refresh period
 };
@@ -117,8 +118,15 @@ class GraphServer {
   int64_t requests() const { return requests_.load(); }
 
  private:
+  struct Conn;
+  struct Loop;
   void AcceptLoop(int listen_fd);
-  void Serve(int fd);
+  void RunLoop(Loop* lp);
+  void OnReadable(Loop* lp, const std::shared_ptr<Conn>& c);
+  void Dispatch(Loop* lp, const std::shared_ptr<Conn>& c);
+  void Flush(Loop* lp, const std::shared_ptr<Conn>& c);
+  void Drop(Loop* lp, const std::shared_ptr<Conn>& c);
+  std::string Handle(uint32_t kind, const std::string& payload);
   EngineEnv* env_;
   int shard_idx_, shard_num_;
   ServerOptions opt_;
@@ -127,9 +135,8 @@ class GraphServer {
   int local_fd_ = -1;  // Unix-domain (abstract namespace) listener for same-host clients
   std::atomic<bool> running_{false};
   std::thread accept_thread_, local_accept_thread_;
-  std::mutex conn_mu_;
-  std::vector<std::thread> conn_threads_;
-  std::vector<int> conn_fds_;
+  std::vector<std::unique_ptr<Loop>> loops_;
+  std::atomic<uint64_t> next_loop_{0};
   std::unique_ptr<ThreadPool> pool_;
   std::unique_ptr<Registry> registry_;
   std::thread heartbeat_thread_;

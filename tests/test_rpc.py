@@ -17,6 +17,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 
 
+_PROCS = []
+
+
 @pytest.fixture(scope="module")
 def cluster():
     data = tempfile.mkdtemp(prefix="euler_amd_rpc_data_")
@@ -30,6 +33,7 @@ def cluster():
     while time.time() < deadline and len([f for f in os.listdir(reg) if "#" in f]) < 2:
         time.sleep(0.1)
     assert len([f for f in os.listdir(reg) if "#" in f]) == 2, "servers did not register"
+    _PROCS[:] = procs
     yield data, reg
     for p in procs:
         p.terminate()
@@ -243,3 +247,47 @@ def test_graph_partition_mode_rejected(cluster):
     data, reg = cluster
     with pytest.raises(Exception, match="graph_partition mode is not supported"):
         ea.initialize_graph({"mode": "graph_partition", "registry": reg, "shard_num": 2})
+
+
+def test_event_loop_server_threads_do_not_grow_with_connections(cluster):
+    """The shard server multiplexes connections over epoll loops (rpc.cc GraphServer):
+    300 concurrent client connections, each with a ping in flight, are served without
+    the server's thread count growing (thread-per-connection would add 300 threads)."""
+    import socket
+    import struct
+
+    import psutil
+
+    from euler_amd import _engine
+
+    data, reg = cluster
+    eps = _engine.registry_list(reg)
+    host, port = next(iter(eps.values()))[0].rsplit(":", 1)
+    procs = [psutil.Process(p.pid) for p in _PROCS]
+    before = {p.pid: p.num_threads() for p in procs}
+    ping = struct.pack("<IIQ", 0x524C5545, 1, 0)
+    socks = []
+    try:
+        for _ in range(300):
+            s = socket.create_connection((host, int(port)), timeout=10)
+            s.sendall(ping)
+            socks.append(s)
+        for s in socks:
+            hdr = b""
+            while len(hdr) < 16:
+                chunk = s.recv(16 - len(hdr))
+                assert chunk, "server closed the connection"
+                hdr += chunk
+            magic, kind, n = struct.unpack("<IIQ", hdr)
+            assert magic == 0x524C5545 and kind == 100
+            body = b""
+            while len(body) < n:
+                body += s.recv(n - len(body))
+        after = {p.pid: p.num_threads() for p in procs}
+        assert all(after[pid] <= before[pid] + 2 for pid in before), (before, after)
+    finally:
+        for s in socks:
+            s.close()
+    # and the cluster still answers queries
+    ea.initialize_shared_graph(reg, shard_num=2)
+    assert ea.sample_node(10, "-1").numel() == 10
