@@ -1233,6 +1233,13 @@ __global__ __launch_bounds__(256) void tr_opt_kernel(TrOptArgs a) {
     if (!valid) i = sg.off;  // clamped: no early return before the tile barrier
   }
   float p = a.p[i];
+  // optimizer slots loaded up front: independent of the split-K sum, so their latency
+  // overlaps the partial-slab loads instead of adding a round trip after them
+  float m = 0.f, v = 0.f;
+  if (MODE == 1 || MODE == 2) {
+    m = a.m[i];
+    v = a.v[i];
+  }
   if (MODE != 3) {
     float g;
     if (MODE != 1) {
@@ -1253,7 +1260,6 @@ __global__ __launch_bounds__(256) void tr_opt_kernel(TrOptArgs a) {
     } else {
       g = a.g[i];
     }
-    float m = a.m[i], v = a.v[i];
     const float t = static_cast<float>(a.step[0]);
     const float gi = g * a.grad_scale + a.wd * p;
     if (a.kind == 0) {

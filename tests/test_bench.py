@@ -42,11 +42,11 @@ def test_bench_single_gpu_json():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["graph", "single"])
-def test_bench_distributed_path_one_rank(mode):
+@pytest.mark.parametrize("extra", [[], ["--no-graph"]], ids=["captured", "eager"])
+def test_bench_distributed_path_one_rank(extra):
     out = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
-                "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--force-dist",
-                "--grad-sync", mode] + SMALL)
-    assert out["config"]["grad_sync"] == mode and out["value"] > 0
+                "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--force-dist"]
+               + extra + SMALL)
+    assert "all-reduce" in out["config"]["grad_sync"] and out["value"] > 0
     first, last = out["config"]["loss_first_last"]
     assert last == last and first == first

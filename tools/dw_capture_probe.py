@@ -50,6 +50,7 @@ def main():
         tr.step()
         torch.cuda.synchronize()
         say("replay", i, float(tr.loss))
+    tr.table.check_overflow()
     tr.release()
     say("released")
     dist.destroy_process_group()
