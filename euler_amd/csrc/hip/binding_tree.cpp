@@ -152,6 +152,19 @@ class TreePlan {
 
   int64_t fwd_blocks() const { return fwd0_.M / bm0_; }
   void set_lr(double lr) { opt_.lr = static_cast<float>(lr); }
+  // bf16 gradient buffer for the data-parallel hand-off (None: fp32 grad)
+  void set_grad16(c10::optional<torch::Tensor> g16) {
+    if (!g16.has_value()) {
+      opt_.g16 = nullptr;
+      g16_ = torch::Tensor();
+      return;
+    }
+    TORCH_CHECK(g16->is_cuda() && g16->scalar_type() == torch::kBFloat16 && g16->is_contiguous() &&
+                    g16->numel() == opt_.n,
+                "grad16 must be a contiguous bf16 GPU tensor of the flat parameter size");
+    g16_ = *g16;
+    opt_.g16 = reinterpret_cast<uint16_t*>(g16_.data_ptr());
+  }
   int64_t num_problems() const { return (int64_t)probs_.size(); }
   std::vector<int64_t> splits() const {
     std::vector<int64_t> s;
@@ -175,6 +188,7 @@ class TreePlan {
   std::vector<torch::Tensor> owned_;
   torch::Tensor roots_cur_;  // the forward's copy of the batch's roots (read by the head)
   TrOptArgs opt_{};
+  torch::Tensor g16_;
 
   bool has(const char* k) const { return d_.contains(k) && !d_[k].is_none(); }
   int64_t geti(const char* k) const {
@@ -535,6 +549,7 @@ void register_tree_ops(py::module& m) {
       .def("dw", &TreePlan::dw)
       .def("opt", &TreePlan::opt, py::arg("mode"), py::arg("grad_scale") = 1.0, py::arg("with_sample") = false)
       .def("set_lr", &TreePlan::set_lr)
+      .def("set_grad16", &TreePlan::set_grad16, py::arg("g16"))
       .def("num_problems", &TreePlan::num_problems)
       .def("splits", &TreePlan::splits)
       .def("problems", &TreePlan::problems, py::arg("route"));

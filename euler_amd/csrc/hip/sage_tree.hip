@@ -1254,11 +1254,14 @@ __global__ __launch_bounds__(256) void tr_opt_kernel(TrOptArgs a) {
         for (int u = 0; u < 16; ++u) g += (s0 + u < sg.S) ? v[u] : 0.f;
       }
       if (MODE == 0) {
-        if (valid) a.g[i] = g;
+        if (valid) {
+          if (a.g16) a.g16[i] = f2bf(g);
+          else a.g[i] = g;
+        }
         return;
       }
     } else {
-      g = a.g[i];
+      g = a.g16 ? bf2f(a.g16[i]) : a.g[i];
     }
     const float t = static_cast<float>(a.step[0]);
     const float gi = g * a.grad_scale + a.wd * p;

@@ -145,6 +145,8 @@ struct TrSeg {
 };
 struct TrOptArgs {
   float *p, *g, *m, *v;
+  uint16_t* g16;  // optional bf16 gradient (data parallel: the all-reduce moves half the bytes);
+                  // mode 0 writes it instead of g, mode 1 reads it
   int64_t n;
   TrSeg seg[kTrMaxSegs];
   int32_t nseg;

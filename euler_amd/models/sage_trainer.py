@@ -442,7 +442,8 @@ class SageTrainer:
             p.opt(2)
         else:
             p.opt(0)
-            scale = grad_sync(self.grad)
+            g16 = getattr(self, "grad16", None)
+            scale = grad_sync(self.grad if g16 is None else g16)
             p.opt(1, 1.0 if scale is None else float(scale))
         self._primed = True
 
@@ -480,6 +481,20 @@ class SageTrainer:
         for _ in range(int(n)):
             self._graph_exec.replay()
         self.step_count += int(n)
+
+    def set_grad_sync_dtype(self, dtype):
+        """Data parallel: the gradient handed to ``grad_sync`` as fp32 (default) or bf16
+        (the reduce launch writes bf16, the optimizer reads it back: the all-reduce moves
+        half the bytes; an 8-rank all-reduce of this ~1 MB gradient is latency/bandwidth
+        bound on the critical path of an ~80 us step)."""
+        if not self.on_gpu:
+            return
+        if dtype in (torch.bfloat16, "bf16", "bfloat16"):
+            self.grad16 = torch.zeros(self.grad.numel(), dtype=torch.bfloat16, device=self.device)
+            self.plan.set_grad16(self.grad16)
+        else:
+            self.grad16 = None
+            self.plan.set_grad16(None)
 
     def set_learning_rate(self, lr: float):
         self.lr = float(lr)

@@ -197,6 +197,34 @@ def test_graph_replay_matches_eager(cuda):
 
 
 @pytest.mark.gpu
+def test_grad_sync_handoff_fp32_and_bf16(cuda):
+    """Data-parallel path: reduce -> grad_sync(grad) -> optimizer.  With an identity sync
+    the fp32 hand-off reproduces the fused single-process step exactly; the bf16 hand-off
+    (half the all-reduce bytes) tracks it within bf16 rounding."""
+    ref = _trainer(cuda, [5, 3], [64, 64, 32], 32)
+    f32 = _trainer(cuda, [5, 3], [64, 64, 32], 32)
+    b16 = _trainer(cuda, [5, 3], [64, 64, 32], 32)
+    b16.set_grad_sync_dtype(torch.bfloat16)
+    seen = []
+
+    def sync(g):
+        seen.append(g.dtype)
+        return 1.0
+
+    lr, lf, lb = [], [], []
+    for _ in range(30):
+        ref.step()
+        f32.step(sync)
+        b16.step(sync)
+        lr.append(float(ref.loss.item()))
+        lf.append(float(f32.loss.item()))
+        lb.append(float(b16.loss.item()))
+    assert seen[0] == torch.float32 and seen[1] == torch.bfloat16
+    np.testing.assert_allclose(lf, lr, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(lb, lr, rtol=0.03, atol=1e-3)
+
+
+@pytest.mark.gpu
 def test_gpu_resume_continues_trajectory(cuda):
     a = _trainer(cuda, [5, 3], [64, 64, 32], 10, mode="dense")
     for _ in range(6):
