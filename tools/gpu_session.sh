@@ -56,6 +56,12 @@ for st in "${S[@]}"; do
     pmc)
       PASSES="FETCH_SIZE|TCC_HIT_sum TCC_MISS_sum|SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD|SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE|SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS" \
         run pmc 600 bash tools/pmc_passes.sh tree "$PWD/tools/tree_kernels.py" --reps 10 ;;
+    pmc_calib)
+      PASSES="FETCH_SIZE|WRITE_SIZE|TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" \
+        run pmc_calib 300 bash tools/pmc_passes.sh calib "$PWD/tools/pmc_calibrate.py" ;;
+    pmc_fwd)
+      run pmc_fwd_plain 300 python -u tools/pmc_fwd_check.py || exit $?
+      PASSES="FETCH_SIZE|TCC_HIT_sum TCC_MISS_sum" run pmc_fwd 300 bash tools/pmc_passes.sh fwd "$PWD/tools/pmc_fwd_check.py" ;;
     ppi_device)
       run ppi_device 600 python -u examples/run_graphsage.py --dataset ppi --device_graph --device cuda \
           --batch_size 512 --total_step 3000 --log_steps 500 --model_dir /tmp/ppi_dev --fanouts 10 10 \
