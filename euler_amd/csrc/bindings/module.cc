@@ -669,6 +669,20 @@ PYBIND11_MODULE(_engine, m) {
       .def_property_readonly("requests", &PyServer::requests)
       .def("stop", &PyServer::Stop);
 
+  py::class_<RegistryServer>(m, "RegistryServer")
+      .def(py::init([](int port) {
+             auto r = std::make_unique<RegistryServer>(port);
+             Throw(r->Start());
+             return r;
+           }),
+           py::arg("port") = 0)
+      .def_property_readonly("port", &RegistryServer::port)
+      .def("size", &RegistryServer::size)
+      .def("stop", [](RegistryServer& r) {
+        py::gil_scoped_release nogil;
+        r.Stop();
+      });
+
   // (unique values in first-occurrence order, inverse) of an int64 array: tf.unique
   // semantics for the CPU dataflows (every hop of SageDataFlow / NeighborDataFlow), GIL
   // released.

@@ -24,7 +24,8 @@ namespace euler {
 
 namespace {
 constexpr uint32_t kMagic = 0x524C5545;  // "EULR"
-enum : uint32_t { kPing = 1, kExecute = 2, kMeta = 3, kReply = 100 };
+enum : uint32_t { kPing = 1, kExecute = 2, kMeta = 3, kRegPut = 10, kRegBeat = 11, kRegDel = 12, kRegList = 13,
+                  kReply = 100 };
 
 // wall clock (file mtimes of the registry are wall-clock stamps)
 double WallSec() {
@@ -482,13 +483,170 @@ class MemoryRegistry : public Registry {
  private:
   std::string name_;
 };
+
+// ---------------------------------------------------------------- TCP registry (client side)
+// record separators of the list reply: metas are "k=v\n" text with hex-encoded free-form
+// fields, so they never contain these bytes
+constexpr char kRecSep = '\x1d', kFieldSep = '\x1e';
+
+class TcpRegistry : public Registry {
+ public:
+  explicit TcpRegistry(Endpoint ep) : ep_(std::move(ep)) {}
+  Status Register(int shard, const Endpoint& ep, const ShardMeta& meta) override {
+    return Call(kRegPut, std::to_string(shard) + kFieldSep + ep.ToString() + kFieldSep + meta.ToString(), nullptr);
+  }
+  Status Deregister(int shard, const Endpoint& ep) override {
+    return Call(kRegDel, std::to_string(shard) + kFieldSep + ep.ToString(), nullptr);
+  }
+  Status Heartbeat(int shard, const Endpoint& ep) override {
+    return Call(kRegBeat, std::to_string(shard) + kFieldSep + ep.ToString(), nullptr);
+  }
+  Status List(std::map<int, std::vector<std::pair<Endpoint, ShardMeta>>>* out, double ttl) override {
+    out->clear();
+    std::string body;
+    EULER_RETURN_IF_ERROR(Call(kRegList, std::to_string(ttl), &body));
+    for (auto& rec : Split(body, std::string(1, kRecSep))) {
+      auto f = Split(rec, std::string(1, kFieldSep));
+      if (f.size() != 3) continue;
+      int64_t shard, port;
+      const size_t c = f[1].rfind(':');
+      if (c == std::string::npos || !ParseInt64(f[0], &shard) || !ParseInt64(f[1].substr(c + 1), &port)) continue;
+      ShardMeta m;
+      ShardMeta::Parse(f[2], &m);
+      (*out)[static_cast<int>(shard)].push_back({Endpoint{f[1].substr(0, c), static_cast<int>(port)}, m});
+    }
+    return Status::OK();
+  }
+
+ private:
+  // one request per short connection: "OK" / "NF" (not found) / "ER<msg>" + body
+  Status Call(uint32_t kind, const std::string& payload, std::string* body) {
+    const int fd = Connect(ep_, 5000);
+    if (fd < 0) return Status::Unavailable("registry " + ep_.ToString() + " unreachable");
+    uint32_t rk = 0;
+    std::string reply;
+    const bool ok = SendFrame(fd, kind, payload) && RecvFrame(fd, &rk, &reply) && rk == kReply && reply.size() >= 2;
+    close(fd);
+    if (!ok) return Status::Unavailable("registry " + ep_.ToString() + " request failed");
+    if (StartsWith(reply, "NF")) return Status::NotFound("registry entry gone");
+    if (!StartsWith(reply, "OK")) return Status::Internal("registry: " + reply.substr(2));
+    if (body) *body = reply.substr(2);
+    return Status::OK();
+  }
+  Endpoint ep_;
+};
 }  // namespace
 
+// ---------------------------------------------------------------- RegistryServer
+RegistryServer::RegistryServer(int port) : port_req_(port) {}
+RegistryServer::~RegistryServer() { Stop(); }
+
+Status RegistryServer::Start() {
+  fd_ = socket(AF_INET, SOCK_STREAM, 0);
+  if (fd_ < 0) return Status::Internal("socket failed");
+  int one = 1;
+  setsockopt(fd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+  struct sockaddr_in addr;
+  memset(&addr, 0, sizeof(addr));
+  addr.sin_family = AF_INET;
+  addr.sin_addr.s_addr = htonl(INADDR_ANY);
+  addr.sin_port = htons(static_cast<uint16_t>(port_req_));
+  if (bind(fd_, reinterpret_cast<sockaddr*>(&addr), sizeof(addr)) != 0)
+    return Status::Internal("registry bind failed: " + std::string(strerror(errno)));
+  if (listen(fd_, 256) != 0) return Status::Internal("registry listen failed");
+  socklen_t len = sizeof(addr);
+  getsockname(fd_, reinterpret_cast<sockaddr*>(&addr), &len);
+  port_ = ntohs(addr.sin_port);
+  running_ = true;
+  th_ = std::thread([this] { Loop(); });
+  EULER_LOG(Info) << "registry server listening on " << port_;
+  return Status::OK();
+}
+
+void RegistryServer::Stop() {
+  if (!running_.exchange(false)) return;
+  shutdown(fd_, SHUT_RDWR);
+  close(fd_);
+  if (th_.joinable()) th_.join();
+}
+
+size_t RegistryServer::size() {
+  std::lock_guard<std::mutex> l(mu_);
+  return entries_.size();
+}
+
+void RegistryServer::Loop() {
+  // requests are tiny and connections short: served one at a time on this thread, each
+  // socket with a receive timeout so a stalled client cannot block the registry
+  while (running_) {
+    const int c = accept(fd_, nullptr, nullptr);
+    if (c < 0) {
+      if (!running_) break;
+      continue;
+    }
+    SetTimeouts(c, 2000);
+    uint32_t kind;
+    std::string payload;
+    if (RecvFrame(c, &kind, &payload)) SendFrame(c, kReply, Handle(kind, payload));
+    close(c);
+  }
+}
+
+std::string RegistryServer::Handle(uint32_t kind, const std::string& payload) {
+  auto f = Split(payload, std::string(1, kFieldSep));
+  std::lock_guard<std::mutex> l(mu_);
+  const double now = WallSec();
+  if (kind == kRegList) {
+    double ttl = 0;
+    ParseDouble(payload, &ttl);
+    std::string out = "OK";
+    bool first = true;
+    for (auto& kv : entries_) {
+      if (ttl > 0 && now - kv.second.seen > ttl) continue;
+      if (!first) out += kRecSep;
+      first = false;
+      out += std::to_string(kv.second.shard) + kFieldSep + kv.second.ep.ToString() + kFieldSep + kv.second.meta;
+    }
+    return out;
+  }
+  if (f.size() < 2) return "ERmalformed request";
+  int64_t shard, port;
+  const size_t c = f[1].rfind(':');
+  if (!ParseInt64(f[0], &shard) || c == std::string::npos || !ParseInt64(f[1].substr(c + 1), &port))
+    return "ERmalformed endpoint";
+  const std::string key = f[0] + "#" + f[1];
+  if (kind == kRegPut) {
+    if (f.size() != 3) return "ERmalformed put";
+    entries_[key] = Entry{static_cast<int>(shard), Endpoint{f[1].substr(0, c), static_cast<int>(port)}, f[2], now};
+    return "OK";
+  }
+  if (kind == kRegBeat) {
+    auto it = entries_.find(key);
+    if (it == entries_.end()) return "NF";
+    it->second.seen = now;
+    return "OK";
+  }
+  if (kind == kRegDel) {
+    entries_.erase(key);
+    return "OK";
+  }
+  return "ERunknown request";
+}
+
 std::unique_ptr<Registry> Registry::Open(const std::string& spec) {
+  if (StartsWith(spec, "tcp://")) {
+    const std::string hp = spec.substr(6);
+    const size_t c = hp.rfind(':');
+    int64_t port = 0;
+    if (c == std::string::npos || !ParseInt64(hp.substr(c + 1), &port))
+      EULER_THROW("registry spec tcp://<host>:<port> expected, got " + spec);
+    return std::unique_ptr<Registry>(new TcpRegistry(Endpoint{hp.substr(0, c), static_cast<int>(port)}));
+  }
   if (StartsWith(spec, "memory:")) return std::unique_ptr<Registry>(new MemoryRegistry(spec.substr(7)));
   if (StartsWith(spec, "file:")) return std::unique_ptr<Registry>(new FileRegistry(spec.substr(5)));
   if (StartsWith(spec, "zk:") || spec.find("2181") != std::string::npos)
-    EULER_THROW("ZooKeeper registries are not built into euler_amd; use a shared directory (file:<dir>)");
+    EULER_THROW("ZooKeeper registries are not built into euler_amd; run euler_amd.tools.registry and use "
+                "tcp://<host>:<port>, or a shared directory (file:<dir>)");
   return std::unique_ptr<Registry>(new FileRegistry(spec));
 }
 

@@ -93,8 +93,38 @@ class Registry {
   virtual Status Heartbeat(int shard, const Endpoint& ep) = 0;
   // shard -> live replicas (ttl <= 0: every entry)
   virtual Status List(std::map<int, std::vector<std::pair<Endpoint, ShardMeta>>>* out, double ttl = 0) = 0;
-  // "file:<dir>" | "<dir>" | "memory:<name>"
+  // "file:<dir>" | "<dir>" | "memory:<name>" | "tcp://<host>:<port>" (RegistryServer)
   static std::unique_ptr<Registry> Open(const std::string& spec);
+};
+
+// Network registry service (the reference's ZooKeeper ensemble role, zk_server_register.cc /
+// zk_server_monitor.cc) for deployments without a shared filesystem: one small process
+// holds the shard -> replica table; servers register and heartbeat over TCP
+// (Registry::Open("tcp://host:port")), clients list with a TTL exactly like the file
+// registry.  Requests are single frames of the RPC wire format on short connections.
+class RegistryServer {
+ public:
+  explicit RegistryServer(int port = 0);
+  ~RegistryServer();
+  Status Start();
+  void Stop();
+  int port() const { return port_; }
+  size_t size();
+
+ private:
+  void Loop();
+  std::string Handle(uint32_t kind, const std::string& payload);
+  struct Entry {
+    int shard;
+    Endpoint ep;
+    std::string meta;
+    double seen;
+  };
+  int port_req_, port_ = 0, fd_ = -1;
+  std::atomic<bool> running_{false};
+  std::thread th_;
+  std::mutex mu_;
+  std::map<std::string, Entry> entries_;
 };
 
 // ============================================================================ server

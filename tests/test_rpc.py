@@ -183,6 +183,54 @@ def test_registry_liveness_sigkill():
                 p.wait(timeout=30)
 
 
+def test_tcp_registry_service_liveness():
+    """Network registry (tools/registry.py, rpc.cc RegistryServer): shard servers register
+    and heartbeat over TCP, the client discovers them through tcp://host:port, a SIGKILLed
+    replica drops out after the TTL and queries keep succeeding — no shared filesystem."""
+    import euler_amd._engine as E
+
+    rs = E.RegistryServer(0)
+    spec = "tcp://127.0.0.1:%d" % rs.port
+    data = tempfile.mkdtemp(prefix="euler_amd_tcpreg_data_")
+    convert_json(os.path.join(HERE, "data", "graph.json"), data, 1)
+    procs = [_serve(data, spec, 0, 1, "--heartbeat_ms", "150") for _ in range(2)]
+    try:
+        deadline = time.time() + 60
+        while time.time() < deadline and len(E.registry_list(spec, 1.0).get(0, [])) < 2:
+            time.sleep(0.1)
+        assert len(E.registry_list(spec, 1.0).get(0, [])) == 2 and rs.size() == 2
+        ea.initialize_graph({"mode": "remote", "registry": spec, "shard_num": 1, "registry_ttl": 1.0,
+                             "registry_refresh": 0.2, "num_retries": 3})
+        eng = ea.get_engine()
+        assert len(eng.endpoints()[0]) == 2
+        ids, _, _ = ea.get_full_neighbor([1, 2], ["0", "1"])
+        assert ids.to_dense().tolist() == [[2, 4, 3], [3, 5, 0]]
+        procs[0].kill()
+        procs[0].wait(timeout=30)
+        time.sleep(2.0)
+        assert len(E.registry_list(spec, 1.0)[0]) == 1
+        assert len(E.registry_list(spec, 0.0)[0]) == 2  # the stale entry is still held
+        assert len(eng.endpoints()[0]) == 1
+        before = E.stats()["rpc_failures"]
+        for _ in range(10):
+            ids, _, _ = ea.get_full_neighbor([1, 2], ["0", "1"])
+            assert ids.to_dense().tolist() == [[2, 4, 3], [3, 5, 0]]
+        assert E.stats()["rpc_failures"] == before
+        # a graceful stop deregisters
+        procs[1].terminate()
+        procs[1].wait(timeout=30)
+        deadline = time.time() + 10
+        while time.time() < deadline and rs.size() != 1:
+            time.sleep(0.1)
+        assert rs.size() == 1  # only the SIGKILLed (never deregistered) entry remains
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+                p.wait(timeout=30)
+        rs.stop()
+
+
 def test_load_and_sampler_options(tmp_path):
     """load_data_type / global_sampler_type (reference Module NODE / EDGE / NODE_SAMPLER /
     EDGE_SAMPLER, start_service.py:33-80, graph.cc:39-70)."""
