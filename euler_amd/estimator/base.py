@@ -165,6 +165,11 @@ class BaseEstimator:
                     m._pending = None
             self.model.to(self.device)
         dp.broadcast_module(self.model)
+        if self.params.get("historical_store", "replicated") == "sharded":
+            # Scalable* encoders: row-sharded stale-embedding / gradient stores (parallel/sharded_store.py)
+            for m in self.model.modules():
+                if callable(getattr(m, "use_sharded_stores", None)) and not getattr(m, "_sharded", None):
+                    m.use_sharded_stores()
         params = [p for p in self.model.parameters() if p.requires_grad]
         name = self.params.get("optimizer", "adam")
         self.optimizer = get_optimizer(name)(params, self.params.get("learning_rate", 0.001))

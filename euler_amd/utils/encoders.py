@@ -215,7 +215,12 @@ class GenieEncoder(GCNEncoder):
 
 
 class _StoreMixin:
-    """Stale-embedding stores + gradient stores (reference encoders.py:313-408, 657-748)."""
+    """Stale-embedding stores + gradient stores (reference encoders.py:313-408, 657-748).
+
+    Data parallel: by default every rank keeps a full replica and applies every rank's
+    writes (parallel/replicated.py); :meth:`use_sharded_stores` switches to row-sharded
+    stores (parallel/sharded_store.py: row r on rank r % world, reads and writes over
+    all-to-all) when a replica per rank is too large."""
 
     def _build_stores(self, dims, max_id, init_maxval):
         g = torch.Generator().manual_seed(1)
@@ -224,6 +229,8 @@ class _StoreMixin:
                                  persistent=False)
             self.register_buffer("gradient_store_layer_%d" % i, torch.zeros(max_id + 2, d), persistent=False)
         self._num_stores = len(dims)
+        self._n_store_rows = max_id + 2
+        self._sharded = None  # [(store, gradient store)] when row-sharded
         self._pending = None
         self.store_loss = None
 
@@ -233,22 +240,52 @@ class _StoreMixin:
     def gradient_stores(self, i):
         return getattr(self, "gradient_store_layer_%d" % (i + 1))
 
+    def use_sharded_stores(self, group=None):
+        """Replace the replicated stores by row-sharded ones (every rank must call this;
+        the initial rows are taken from this rank's replica, which starts identical on
+        every rank)."""
+        from euler_amd.parallel.sharded_store import ShardedRowStore
+
+        shards = []
+        for i in range(self._num_stores):
+            full, gfull = self.stores(i), self.gradient_stores(i)
+            n, d = full.shape
+            st = ShardedRowStore(n, d, full.device, group, init=lambda ids, f=full: f[ids])
+            gs = ShardedRowStore(n, d, full.device, group, init=lambda ids, f=gfull: f[ids])
+            shards.append((st, gs))
+            # drop the replicas (keep empty placeholders so .to() / state handling still work)
+            setattr(self, "store_layer_%d" % (i + 1), torch.empty(0, d, device=full.device))
+            setattr(self, "gradient_store_layer_%d" % (i + 1), torch.empty(0, d, device=full.device))
+        self._sharded = shards
+        self.store_group = group
+        return self
+
+    def _store_device(self):
+        return self._sharded[0][0].device if self._sharded else self.stores(0).device
+
     def _rows(self, ids):
-        ids = torch.as_tensor(ids).to(self.stores(0).device).long()
-        n = self.stores(0).shape[0]
+        ids = torch.as_tensor(ids).to(self._store_device()).long()
+        n = self._n_store_rows
         return torch.where((ids < 0) | (ids >= n), torch.full_like(ids, n - 1), ids)
 
+    def _read(self, i, rows, grad=False):
+        if self._sharded:
+            return self._sharded[i][1 if grad else 0].read(rows)
+        return (self.gradient_stores(i) if grad else self.stores(i))[rows]
+
     def _lookup_neighbors(self, layer, neighbor):
-        leaf = self.stores(layer)[self._rows(neighbor)].detach().requires_grad_(self.training)
-        return leaf
+        rows = self._rows(neighbor)
+        leaf = self._read(layer, rows.reshape(-1)).reshape(tuple(rows.shape) + (-1,))
+        return leaf.detach().requires_grad_(self.training)
 
     def _finish_training_forward(self, node, node_embeddings, neighbor, neigh_leaves):
         rows = self._rows(node)
         losses = []
         for i in range(self._num_stores):
-            gs = self.gradient_stores(i)
-            g = gs[rows].clone()
-            gs.index_fill_(0, rows, 0.0)  # the other ranks zero these rows in after_backward
+            g = self._read(i, rows.reshape(-1), grad=True).reshape(tuple(rows.shape) + (-1,)).clone()
+            if not self._sharded:
+                # the other ranks zero these rows in after_backward (sharded: the owner does)
+                self.gradient_stores(i).index_fill_(0, rows.reshape(-1), 0.0)
             losses.append((node_embeddings[i] * g.to(node_embeddings[i].dtype)).sum())
         self.store_loss = sum(losses) if losses else torch.zeros((), device=rows.device)
         self._pending = (rows, [e.detach() for e in node_embeddings[:self._num_stores]], self._rows(neighbor),
@@ -260,6 +297,15 @@ class _StoreMixin:
         if self._pending is None:
             return
         rows, embs, nrows, leaves = self._pending
+        if self._sharded:
+            for i, (st, gs) in enumerate(self._sharded):
+                gs.write(rows, None, "zero")
+                st.write(rows, embs[i], "copy")
+            for i, leaf in enumerate(leaves):
+                grad = leaf.grad if leaf.grad is not None else torch.zeros_like(leaf)
+                self._sharded[i][1].write(nrows, grad.reshape(nrows.numel(), -1).float(), "add")
+            self._pending = None
+            return
         # data parallel: every rank applies every rank's writes (parallel/replicated.py), so
         # the replicas behave like the reference's shared PS stores
         group = getattr(self, "store_group", None)

@@ -310,6 +310,70 @@ def _worker_replicated_store(rank, world, port, q):
         q.put((rank, "error", repr(e)))
 
 
+def _worker_sharded_store(rank, world, port, q):
+    try:
+        _init(rank, world, port)
+        import euler_amd as ea
+        from euler_amd.parallel.sharded_store import ShardedRowStore
+        from euler_amd.utils import encoders as E
+
+        # 1) store semantics: copy (later source rank wins), add, zero, read
+        st = ShardedRowStore(11, 3, "cpu", init=lambda ids: ids.float().view(-1, 1).expand(-1, 3))
+        flags = []
+        ok = torch.equal(st.read(torch.tensor([10, 3, 3])), torch.tensor([[10.0] * 3, [3.0] * 3, [3.0] * 3]))
+        st.write(torch.tensor([5, rank]), torch.full((2, 3), float(rank + 100)), "copy")
+        st.write(torch.tensor([7]), torch.ones(1, 3), "add")
+        st.write(torch.tensor([9]) if rank == 0 else torch.empty(0, dtype=torch.long), None, "zero")
+        full = st.read(torch.arange(11))
+        exp = torch.arange(11).float().view(-1, 1).expand(-1, 3).clone()
+        for r in range(world):
+            exp[r] = r + 100
+        exp[5] = world - 1 + 100
+        exp[7] += world
+        exp[9] = 0
+        ok = ok and torch.equal(full, exp)
+        flags.append(("store", bool(ok)))
+        # 2) Scalable encoder: sharded stores reproduce the replicated stores step by step
+        ea.synthetic_graph(200, avg_degree=5, max_degree=16, feature_dim=6, label_dim=2, seed=3)
+        encs = []
+        for sharded in (False, True):
+            torch.manual_seed(0)
+            e = E.ScalableSageEncoder("0", 2, 2, 4, feature_idx="feature", feature_dim=6, max_id=199)
+            e.train()
+            e.store_group = None
+            if sharded:
+                e.use_sharded_stores()
+            encs.append(e)
+        for step in range(3):
+            ids = torch.arange(6) + 10 * rank + step
+            outs = []
+            for e in encs:
+                ea.set_seed(100 + step * 7 + rank)
+                torch.manual_seed(step)  # the lazy layers materialise identically
+                out = e(ids)
+                (out.sum() + e.store_loss).backward()
+                e.after_backward()
+                outs.append(out.detach())
+            ok = ok and torch.allclose(outs[0], outs[1], atol=1e-6)
+            flags.append(("out", step, float((outs[0] - outs[1]).abs().max())))
+        rep, shd = encs
+        allids = torch.arange(rep.stores(0).shape[0])
+        ok = ok and torch.allclose(rep.stores(0), shd._sharded[0][0].read(allids), atol=1e-6)
+        flags.append(("st", float((rep.stores(0) - shd._sharded[0][0].read(allids)).abs().max())))
+        ok = ok and torch.allclose(rep.gradient_stores(0), shd._sharded[0][1].read(allids), atol=1e-6)
+        q.put((rank, "sharded_store", bool(ok), flags))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_sharded_historical_store_matches_replicated():
+    res = _run(_worker_sharded_store)
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == 2 and all(r[2] for r in res), res
+
+
 def test_replicated_store_writes_reach_every_rank():
     res = _run(_worker_replicated_store)
     assert not [r for r in res if r[1] == "error"], res
