@@ -30,7 +30,8 @@ from euler_amd.ops.mp_ops import SegmentIndex
 
 __all__ = ["EdgeCSR", "gat_aggregate", "gat_aggregate_reference", "RelationTiles", "relation_transform",
            "relation_transform_reference", "sgns_loss", "sgns_loss_reference", "kg_score", "kg_score_reference",
-           "unique_first", "unique_first_padded", "KG_KINDS", "KG_CORRUPT", "sgns_fwd_idx", "occ_csr", "sgns_grad", "tall_linear", "xent"]
+           "unique_first", "unique_first_padded", "KG_KINDS", "KG_CORRUPT", "sgns_fwd_idx", "occ_csr", "sgns_grad", "tall_linear", "xent",
+           "splitk_mm_t", "splitk_linear"]
 
 
 # ----------------------------------------------------------------------------- edge structures
@@ -244,6 +245,55 @@ class _TallLinear(torch.autograd.Function):
             if n0 < n:
                 db += dy[n0:].float().sum(0)
         return dx, dw.to(w.dtype), db, None
+
+
+def splitk_mm_t(a, b, parts=None):
+    """``a^T @ b`` (fp32 result) for tall a [M, P], b [M, Q] as ``parts`` batched row chunks +
+    a sum: dW-shaped products with few output tiles otherwise run on one or two workgroups
+    (hipBLASLt picks one 128x128 tile over all M rows)."""
+    M = a.shape[0]
+    p = parts or max(1, min(32, M // 128))
+    if not (a.is_cuda and p > 1):
+        return torch.mm(a.t().float(), b.float()) if not a.is_cuda else torch.mm(a.t(), b, out_dtype=torch.float32)
+    n0 = (M // p) * p
+    av, bv = a[:n0].reshape(p, n0 // p, -1), b[:n0].reshape(p, n0 // p, -1)
+    if a.dtype == torch.float32:
+        out = torch.bmm(av.transpose(1, 2), bv).sum(0)
+    else:
+        try:
+            out = torch.bmm(av.transpose(1, 2), bv, out_dtype=torch.float32).sum(0)
+        except (RuntimeError, TypeError, NotImplementedError):
+            out = torch.bmm(av.transpose(1, 2).float(), bv.float()).sum(0)
+    if n0 < M:
+        out = out + (torch.mm(a[n0:].t(), b[n0:], out_dtype=torch.float32) if a.dtype != torch.float32
+                     else a[n0:].t() @ b[n0:])
+    return out
+
+
+class _SplitKLinear(torch.autograd.Function):
+    """``x @ w^T + b`` whose weight / bias gradients use :func:`splitk_mm_t` (GPU)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_bias = b is not None
+        return torch.nn.functional.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = dy @ w if ctx.needs_input_grad[0] else None
+        dw = splitk_mm_t(dy, x).to(w.dtype) if ctx.needs_input_grad[1] else None
+        db = dy.float().sum(0).to(w.dtype) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        return dx, dw, db
+
+
+def splitk_linear(x, weight, bias=None):
+    """Linear layer for GPU batches of >= 512 rows with split-K weight gradients."""
+    if x.is_cuda and x.dim() == 2 and x.shape[0] >= 512 and x.dtype == weight.dtype:
+        return _SplitKLinear.apply(x, weight, bias)
+    return torch.nn.functional.linear(x, weight, bias)
 
 
 def tall_linear(x, weight, bias=None, chunk=8192):

@@ -71,7 +71,9 @@ class _SageFused(torch.autograd.Function):
         if ctx.relu:
             g = g.clone()
             hip().relu_bwd_(g, out)
-        dw = torch.mm(g.t(), a, out_dtype=torch.float32).to(ctx.wdtype)
+        from euler_amd.ops.gnn_ops import splitk_mm_t
+
+        dw = splitk_mm_t(g, a).to(ctx.wdtype)  # split-K: M rows over many workgroups
         db = g.float().sum(0) if ctx.has_bias else None
         dx = None
         if ctx.needs_input_grad[0]:

@@ -47,7 +47,12 @@ class Dense(nn.LazyLinear):
             return super().forward(x) if self.activation is None else self.activation(super().forward(x))
         w = self.weight if self.weight.dtype == x.dtype else self.weight.to(x.dtype)
         b = None if self.bias is None else (self.bias if self.bias.dtype == x.dtype else self.bias.to(x.dtype))
-        y = F.linear(x, w, b)
+        if x.is_cuda and x.dim() == 2 and x.shape[0] >= 512:
+            from euler_amd.ops.gnn_ops import splitk_linear
+
+            y = splitk_linear(x, w, b)  # split-K weight gradient (GPU, tall batches)
+        else:
+            y = F.linear(x, w, b)
         return y if self.activation is None else self.activation(y)
 
 

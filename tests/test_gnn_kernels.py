@@ -385,3 +385,28 @@ def test_sgns_idx_kernels_match_cpu(cuda, kind):
     if kind != "sgd":
         torch.testing.assert_close(fused.v.cpu(), plain.v, atol=1e-9, rtol=1e-3)
     assert int(fused.step.item()) == 2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_splitk_linear_grads_match(cuda, dtype):
+    """Dense / fused-SAGE weight gradients as split-K batched GEMMs (gnn_ops.splitk_*)
+    equal the plain linear backward (fp32 reference)."""
+    from euler_amd.ops.gnn_ops import splitk_linear, splitk_mm_t
+
+    g = torch.Generator(device="cpu").manual_seed(0)
+    x = torch.randn(5632 + 37, 256, generator=g).to(cuda, dtype).requires_grad_(True)
+    w = torch.randn(121, 256, generator=g).to(cuda, dtype).requires_grad_(True)
+    b = torch.randn(121, generator=g).to(cuda, dtype).requires_grad_(True)
+    y = splitk_linear(x, w, b)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, w, b))
+    torch.nn.functional.linear(xr, wr, br).backward(dy.float())
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    for got, ref in ((x.grad, xr.grad), (w.grad, wr.grad), (b.grad, br.grad)):
+        rel = (got.float() - ref).norm() / ref.norm()
+        assert rel < tol, rel
+    m = splitk_mm_t(dy, x.detach())
+    assert m.dtype == torch.float32 and m.shape == (121, 256)
+    assert ((m - dy.float().t() @ x.detach().float()).norm() / m.norm()) < tol
