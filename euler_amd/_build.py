@@ -222,6 +222,7 @@ def build_hip(max_workers: int = 8) -> str:
         return out
     kflags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
               "-D__HIP_PLATFORM_AMD__=1", "-I" + CSRC, "-Wno-unused-result"]
+    kflags += os.environ.get("EULER_AMD_HIP_FLAGS", "").split()  # tuning experiments (-DNAME=value)
     bflags = ["-O2", "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
               f"-D_GLIBCXX_USE_CXX11_ABI={int(abi)}", "-DTORCH_API_INCLUDE_EXTENSION_H",
               "-DTORCH_EXTENSION_NAME=_hip_ops", "-I" + CSRC, "-I/opt/rocm/include",

@@ -1006,7 +1006,11 @@ __device__ __forceinline__ uint4_t tr_route_frag(const TrDwProb& pr, const Route
 // rows by its 32 q columns with X fragments loaded straight from the kt layout, one
 // stage (kRKB k-blocks) ahead.
 // ----------------------------------------------------------------------------
-constexpr int kRP = 64, kRQ = 128, kRKB = 8, kRLd = 40;
+#ifndef TR_RKB
+#define TR_RKB 8
+#endif
+// kRKB k-blocks per stage; the double-buffered G tile takes 2 * kRKB * 5 KiB of LDS
+constexpr int kRP = 64, kRQ = 128, kRKB = TR_RKB, kRLd = 40;
 
 struct RouteStage {
   RouteRaw r[kRKB];

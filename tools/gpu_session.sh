@@ -101,6 +101,12 @@ for st in "${S[@]}"; do
       RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29533 \
         run deepwalk_prof_dist 600 rocprofv3 --kernel-trace --stats -d "$OUT/dw_prof_dist" -o run --output-format csv -- \
           python3 benchmarks/bench_deepwalk.py --eval-nodes 0 --mode static --steps 20 --force-dist ;;
+    rkb_sweep)
+      for v in ${RKB_VALUES:-6 4}; do
+        touch euler_amd/csrc/hip/sage_tree.hip
+        EULER_AMD_HIP_FLAGS="-DTR_RKB=$v" python -m euler_amd._build > "$OUT/build_rkb$v.log" 2>&1 || exit 4
+        run "tree_kernels_rkb$v" 300 python -u tools/tree_kernels.py || exit $?
+      done ;;
     kernels_full)
       run tree_kernels_full 300 python -u tools/tree_kernels.py --num-nodes 100000000 ;;
     kernels_sizes)
