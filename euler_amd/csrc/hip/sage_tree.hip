@@ -223,6 +223,9 @@ __global__ __launch_bounds__(256) void tr_sample_kernel(TrSampleArgs a) {
 #ifndef TR_FWD_WAVES
 #define TR_FWD_WAVES 4
 #endif
+#ifndef TR_FWD_BPF
+#define TR_FWD_BPF 2
+#endif
 template <typename FT, int BM, int MODE>
 __global__ __launch_bounds__(256, (BM == 32 ? TR_FWD_WAVES : 2)) void tr_fwd_kernel(TrFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
@@ -245,10 +248,11 @@ __global__ __launch_bounds__(256, (BM == 32 ? TR_FWD_WAVES : 2)) void tr_fwd_ker
   if (a.prof && threadIdx.x == 0) a.prof[blockIdx.x * 8 + (k)] = static_cast<long long>(wall_clock64())
   TF_STAMP(0);
   constexpr int FN = 4;
+  constexpr int kBP = TR_FWD_BPF;  // k-steps of weight fragments in flight
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const bf16_t* W = a.W;
-  uint4_t bcur[FN];
+  uint4_t bq[kBP][FN];
   if constexpr (kGather) {
     // ---- the sampled ids of the block (sampler output, one step ahead): coalesced
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -343,11 +347,15 @@ __global__ __launch_bounds__(256, (BM == 32 ? TR_FWD_WAVES : 2)) void tr_fwd_ker
       *reinterpret_cast<uint4_t*>(lds + r * ldsw + c * 8) = v;
     }
   }
-  // the GEMM's first B fragments (weights: L2-resident) load behind the kt pass
+  // the GEMM's first kBP k-steps of B fragments (weights: L2-resident) load behind the kt
+  // pass; the loop below keeps kBP steps in flight (a weight-fragment load from L2 takes
+  // longer than one step's MFMAs, so one step ahead leaves the chain latency-bound)
   if constexpr (MODE != 1) {
     if (wave * 64 < a.H) {
 #pragma unroll
-      for (int n = 0; n < FN; ++n) bcur[n] = fm_frag(W, wave * 64 + n * 16, 0, K2, lane);
+      for (int q = 0; q < kBP; ++q)
+#pragma unroll
+        for (int n = 0; n < FN; ++n) bq[q][n] = fm_frag(W, wave * 64 + n * 16, q * 32 < K2 ? q * 32 : 0, K2, lane);
     }
   }
   __syncthreads();
@@ -389,24 +397,29 @@ __global__ __launch_bounds__(256, (BM == 32 ? TR_FWD_WAVES : 2)) void tr_fwd_ker
     if (cb < H) {
       if (cchunk > 0) {
 #pragma unroll
-        for (int n = 0; n < FN; ++n) bcur[n] = fm_frag(W, cb + n * 16, 0, K2, lane);
+        for (int q = 0; q < kBP; ++q)
+#pragma unroll
+          for (int n = 0; n < FN; ++n) bq[q][n] = fm_frag(W, cb + n * 16, q * 32 < K2 ? q * 32 : 0, K2, lane);
       }
-      for (int k0 = 0; k0 < K2; k0 += 32) {
-        uint4_t bnext[FN];
-        const bool more = k0 + 32 < K2;
+      // kBP steps per iteration, ring slot q holds step k0 + 32 q; after its MFMAs the slot
+      // is refilled with step k0 + 32 (q + kBP) (clamped to a valid fragment past the end)
+      for (int k0 = 0; k0 < K2; k0 += 32 * kBP) {
 #pragma unroll
-        for (int n = 0; n < FN; ++n)
-          bnext[n] = more ? fm_frag(W, cb + n * 16, k0 + 32, K2, lane) : uint4_t{0u, 0u, 0u, 0u};
-        uint4_t av[FM];
+        for (int q = 0; q < kBP; ++q) {
+          const int ks = k0 + 32 * q;
+          if (ks >= K2) break;  // uniform
+          uint4_t av[FM];
 #pragma unroll
-        for (int m = 0; m < FM; ++m)
-          av[m] = *reinterpret_cast<const uint4_t*>(lds + (m * 16 + lr) * ldsw + k0 + lk);
+          for (int m = 0; m < FM; ++m)
+            av[m] = *reinterpret_cast<const uint4_t*>(lds + (m * 16 + lr) * ldsw + ks + lk);
 #pragma unroll
-        for (int m = 0; m < FM; ++m)
+          for (int m = 0; m < FM; ++m)
 #pragma unroll
-          for (int n = 0; n < FN; ++n) acc[m][n] = mfma16(av[m], bcur[n], acc[m][n]);
+            for (int n = 0; n < FN; ++n) acc[m][n] = mfma16(av[m], bq[q][n], acc[m][n]);
+          const int kn = ks + 32 * kBP;
 #pragma unroll
-        for (int n = 0; n < FN; ++n) bcur[n] = bnext[n];
+          for (int n = 0; n < FN; ++n) bq[q][n] = fm_frag(W, cb + n * 16, kn < K2 ? kn : 0, K2, lane);
+        }
       }
     }
     if (alias_out) __syncthreads();  // every wave is done reading the A tile

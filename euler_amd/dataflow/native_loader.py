@@ -81,6 +81,8 @@ class NativeSageLoader:
         self.lay = E.sage_pipeline_layout(self.B, self.fanouts, self.self_loops, [int(d) for d in dense_dims],
                                           self.label_dim)
         n_slots = int(slots or (int(workers) + 3))
+        self.n_slots = n_slots
+        self.workers = int(workers)
         pin = self.cuda
         self.ints = [torch.zeros(self.lay["ints"], dtype=torch.int64, pin_memory=pin) for _ in range(n_slots)]
         self.floats = [torch.zeros(max(1, self.lay["floats"]), dtype=torch.float32, pin_memory=pin)
@@ -175,10 +177,23 @@ class NativeSageLoader:
         f = self.fanouts[L - 1] + (1 if self.self_loops else 0)
         return L, n, e, int(lay["off_nbr"][L]) + (n[L - 1] * f + 1) // 2
 
+    def _backpressure(self):
+        """Slots held by copies still in flight must leave the workers something to fill:
+        ``next()`` blocks in C++ and nothing releases a slot meanwhile, so if the host ran
+        far ahead of the GPU (asynchronous graph replays) and every slot waited on a copy,
+        ``next()`` would wait forever.  Wait on the oldest copies instead (bounded: the GPU
+        completes them), keeping at least ``workers`` slots free or filled."""
+        while self._inflight and len(self._inflight) > self.n_slots - self.workers - 1:
+            slot, ev = self._inflight.pop(0)
+            if ev is not None:
+                ev.synchronize()
+            self.pipe.release(slot)
+
     def get(self):
         """Prepared(inputs=roots, label, embed_in=Prepared(flow, x)) on the device.  Three
         H2D copies per batch (used int prefix, feature rows, labels), device-side views."""
         self._recycle()
+        self._backpressure()
         slot = self.pipe.next()
         if slot < 0:
             raise StopIteration

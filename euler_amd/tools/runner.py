@@ -181,6 +181,8 @@ def parse_args(argv=None, model=None):
                    help="graphsage: train on an HBM copy of the graph with the fused gfx950 step "
                         "(models/sage_trainer.py) instead of the CPU-engine input pipeline")
     p.add_argument("--device_feature_dtype", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--cuda_graph", default="auto", choices=["auto", "off"],
+                   help="capture the engine-path training step in a hipGraph when eligible")
     p.add_argument("--native_pipeline", default="auto", choices=["auto", "on", "off"],
                    help="engine path: C++ batch pipeline (sampling + features into pinned slots) for "
                         "SupervisedGNN + SageDataFlow models; auto = on for GPU training")
@@ -211,6 +213,7 @@ def build(a):
               "device": a.device, "amp": a.amp, "device_graph": a.device_graph,
               "device_feature_dtype": a.device_feature_dtype, "seed": a.seed,
               "native_pipeline": {"auto": "auto", "on": True, "off": False}[a.native_pipeline],
+              "cuda_graph": a.cuda_graph if a.cuda_graph == "auto" else False,
               "pipeline_workers": a.pipeline_workers}
     if kind == "node":
         params.update(train_node_type=_first(ds.train_node_type), id_file=a.id_file or ds.id_file)

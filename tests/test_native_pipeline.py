@@ -94,6 +94,31 @@ def test_batch_stream_reproducible_across_worker_counts(graph):
         assert torch.equal(a, b)
 
 
+def test_slots_never_all_held_by_inflight_copies(graph):
+    """Back-pressure: with copies that never report completion on their own (events that
+    only finish on synchronize), get() must still make progress: the loader waits on its
+    oldest in-flight copy instead of blocking forever in next()."""
+    ea.use_graph(graph)
+    flow = SageDataFlow([4, 3], [["0"], ["0"]], max_id=N - 1)
+    ld = _loader(flow, workers=2)
+
+    class SlowEvent:
+        def query(self):
+            return False
+
+        def synchronize(self):
+            pass
+
+    try:
+        for _ in range(3 * ld.n_slots):
+            ld.get()
+            # pretend the copy of the batch just handed out is still in flight
+            ld._inflight[-1] = (ld._inflight[-1][0], SlowEvent())
+            assert len(ld._inflight) <= ld.n_slots - ld.workers
+    finally:
+        ld.close()
+
+
 def _model():
     from euler_amd import models as Z
 

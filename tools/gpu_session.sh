@@ -107,6 +107,12 @@ for st in "${S[@]}"; do
         EULER_AMD_HIP_FLAGS="-DTR_RKB=$v" python -m euler_amd._build > "$OUT/build_rkb$v.log" 2>&1 || exit 4
         run "tree_kernels_rkb$v" 300 python -u tools/tree_kernels.py || exit $?
       done ;;
+    bpf_sweep)
+      for v in ${BPF_VALUES:-2 4}; do
+        touch euler_amd/csrc/hip/sage_tree.hip
+        EULER_AMD_HIP_FLAGS="-DTR_FWD_BPF=$v" python -m euler_amd._build > "$OUT/build_bpf$v.log" 2>&1 || exit 4
+        run "tree_kernels_bpf$v" 300 python -u tools/tree_kernels.py || exit $?
+      done ;;
     kernels_full)
       run tree_kernels_full 300 python -u tools/tree_kernels.py --num-nodes 100000000 ;;
     kernels_sizes)
