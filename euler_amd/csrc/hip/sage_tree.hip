@@ -127,6 +127,9 @@ __device__ int32_t tr_slot_node(const TrGraph& g, const TrTree& tr, int64_t s, i
   return node;
 }
 
+__device__ __forceinline__ float bf_lo(uint32_t v) { return __uint_as_float(v << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t v) { return __uint_as_float(v & 0xffff0000u); }
+
 // 8 consecutive feature columns of one row, bf16 or fp32 storage
 template <typename FT>
 struct Feat8;
@@ -137,6 +140,13 @@ struct Feat8<bf16_t> {
   __device__ __forceinline__ void load(const bf16_t* p) { v = *reinterpret_cast<const uint4_t*>(p); }
   __device__ __forceinline__ void zero() { v = uint4_t{0u, 0u, 0u, 0u}; }
   __device__ __forceinline__ void add_to(float* acc) const { acc_bf16x8(acc, v); }
+  __device__ __forceinline__ void add_scaled_to(float* acc, float w) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      acc[2 * i] += w * bf_lo(v[i]);
+      acc[2 * i + 1] += w * bf_hi(v[i]);
+    }
+  }
   // keep = false: the row was a padding id (-1) loaded from row 0; contributes zero
   __device__ __forceinline__ void keep(bool k) {
 #pragma unroll
@@ -160,6 +170,13 @@ struct Feat8<float> {
       acc[4 + i] += b[i];
     }
   }
+  __device__ __forceinline__ void add_scaled_to(float* acc, float w) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      acc[i] += w * a[i];
+      acc[4 + i] += w * b[i];
+    }
+  }
   __device__ __forceinline__ void keep(bool k) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -172,9 +189,6 @@ struct Feat8<float> {
     return pack_bf16x8(t);
   }
 };
-
-__device__ __forceinline__ float bf_lo(uint32_t v) { return __uint_as_float(v << 16); }
-__device__ __forceinline__ float bf_hi(uint32_t v) { return __uint_as_float(v & 0xffff0000u); }
 
 // ----------------------------------------------------------------------------
 // tr_sample: target-row nodes (root -> hop chain) and their leaf draws, BM rows per block
@@ -226,6 +240,13 @@ __global__ __launch_bounds__(256) void tr_sample_kernel(TrSampleArgs a) {
 #ifndef TR_FWD_BPF
 #define TR_FWD_BPF 2
 #endif
+// TR_FWD_DEDUP=1: fetch each distinct leaf of a row once (weighted by its draw count).
+// Correct (oracle tests pass) but measured 1.9x slower: the serial per-row compaction and
+// the exec-masked, variable-count loads stall the gather (profiles/r2_mid/sweeps/
+// dedup_variant.log); the repeats are cheap L2 hits with branch-free loads.
+#ifndef TR_FWD_DEDUP
+#define TR_FWD_DEDUP 0
+#endif
 template <typename FT, int BM, int MODE>
 __global__ __launch_bounds__(256, (BM == 32 ? TR_FWD_WAVES : 2)) void tr_fwd_kernel(TrFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
@@ -243,6 +264,10 @@ __global__ __launch_bounds__(256, (BM == 32 ? TR_FWD_WAVES : 2)) void tr_fwd_ker
   bf16_t* otile = own_otile ? lds + BM * ldsw : lds;
   int32_t* node_s = reinterpret_cast<int32_t*>(lds + BM * ldsw + (own_otile ? BM * (kTrBN + 8) : 0));
   int32_t* leaf_s = node_s + BM;
+  // leaf dedup (TR_FWD_DEDUP): per row, the distinct leaf ids move to the front of the
+  // row's leaf_s segment, mult_s holds their draw counts and cnt_s the distinct count
+  int32_t* mult_s = leaf_s + BM * a.FL;
+  int32_t* cnt_s = mult_s + BM * a.FL;
 
 #define TF_STAMP(k) \
   if (a.prof && threadIdx.x == 0) a.prof[blockIdx.x * 8 + (k)] = static_cast<long long>(wall_clock64())
@@ -264,6 +289,30 @@ __global__ __launch_bounds__(256, (BM == 32 ? TR_FWD_WAVES : 2)) void tr_fwd_ker
     for (int it = threadIdx.x; it < BM * a.FL; it += 256)
       leaf_s[it] = row0 * a.FL + it < a.M * a.FL ? a.leaf[row0 * a.FL + it] : -1;
     __syncthreads();
+#if TR_FWD_DEDUP
+    // with-replacement draws repeat rows (a node with fewer out-edges than FL draws the
+    // same neighbours again): fetch each distinct leaf row once, weighted by its count
+    if (threadIdx.x < BM) {
+      int32_t* ids = leaf_s + threadIdx.x * a.FL;
+      int32_t* mul = mult_s + threadIdx.x * a.FL;
+      int n = 0;
+      for (int k = 0; k < a.FL; ++k) {
+        const int32_t v = ids[k];
+        if (v < 0) continue;
+        int j = 0;
+        while (j < n && ids[j] != v) ++j;
+        if (j < n) {
+          mul[j] += 1;
+        } else {
+          ids[n] = v;
+          mul[n] = 1;
+          ++n;
+        }
+      }
+      cnt_s[threadIdx.x] = n;
+    }
+    __syncthreads();
+#endif
     TF_STAMP(1);
     // ---- gather + mean: item = (row, 8-column chunk); two items per thread with every
     // leaf load of both in flight
@@ -285,6 +334,36 @@ __global__ __launch_bounds__(256, (BM == 32 ? TR_FWD_WAVES : 2)) void tr_fwd_ker
       for (int i = 0; i < 8; ++i) acc_a[i] = acc_b[i] = 0.f;
       sa.load(x + static_cast<int64_t>(na > 0 ? na : 0) * D + ca * 8);
       sb.load(x + static_cast<int64_t>(nb > 0 ? nb : 0) * D + cb * 8);
+#if TR_FWD_DEDUP
+      const int na_cnt = cnt_s[ra], nb_cnt = hb ? cnt_s[rb] : 0;
+      const int kmax = na_cnt > nb_cnt ? na_cnt : nb_cnt;
+      for (int k = 0; k < kmax; k += G) {
+        int32_t ja[G], jb[G];
+        float wa[G], wb[G];
+        Feat8<FT> va[G], vb[G];
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+          const bool oa = k + u < na_cnt, ob = k + u < nb_cnt;
+          ja[u] = oa ? leaf_s[ra * a.FL + k + u] : -1;
+          jb[u] = ob ? leaf_s[rb * a.FL + k + u] : -1;
+          wa[u] = oa ? static_cast<float>(mult_s[ra * a.FL + k + u]) : 0.f;
+          wb[u] = ob ? static_cast<float>(mult_s[rb * a.FL + k + u]) : 0.f;
+        }
+        // lanes past their row's distinct count are masked off: no memory request
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+          if (ja[u] >= 0) va[u].load(x + static_cast<int64_t>(ja[u]) * D + ca * 8);
+          else va[u].zero();
+          if (jb[u] >= 0) vb[u].load(x + static_cast<int64_t>(jb[u]) * D + cb * 8);
+          else vb[u].zero();
+        }
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+          va[u].add_scaled_to(acc_a, wa[u]);
+          vb[u].add_scaled_to(acc_b, wb[u]);
+        }
+      }
+#else
       for (int k = 0; k < a.FL; k += G) {
         int32_t ja[G], jb[G];
         Feat8<FT> va[G], vb[G];
@@ -307,6 +386,7 @@ __global__ __launch_bounds__(256, (BM == 32 ? TR_FWD_WAVES : 2)) void tr_fwd_ker
           vb[u].add_to(acc_b);
         }
       }
+#endif
       sa.keep(na >= 0);
       sb.keep(nb >= 0);
       if (a.include_self) {
@@ -1336,6 +1416,7 @@ size_t eh_tr_fwd_lds(int D, int H, int bm, int FL, int mode) {
   size_t b = static_cast<size_t>(bm) * (K2 + 8) * sizeof(bf16_t);
   if (mode != 1 && !alias_out) b += static_cast<size_t>(bm) * (kTrBN + 8) * sizeof(bf16_t);
   if (mode != 2) b += static_cast<size_t>(bm) * (1 + FL) * sizeof(int32_t);
+  if (mode != 2) b += static_cast<size_t>(bm) * (1 + FL) * sizeof(int32_t);  // dedup counts
   return b;
 }
 

@@ -113,6 +113,22 @@ for st in "${S[@]}"; do
         EULER_AMD_HIP_FLAGS="-DTR_FWD_BPF=$v" python -m euler_amd._build > "$OUT/build_bpf$v.log" 2>&1 || exit 4
         run "tree_kernels_bpf$v" 300 python -u tools/tree_kernels.py || exit $?
       done ;;
+    variants)
+      # VARIANTS="-DA=1|-DB=2": rebuild the HIP extension with each flag set, time the
+      # step launches, and (VARIANT_TESTS=1) run the tree-step oracle tests on that build
+      IFS='|' read -ra VL <<< "${VARIANTS:-}"
+      i=0
+      for v in "${VL[@]}"; do
+        i=$((i+1))
+        touch euler_amd/csrc/hip/sage_tree.hip
+        EULER_AMD_HIP_FLAGS="$v" python -m euler_amd._build > "$OUT/build_variant$i.log" 2>&1 || exit 4
+        echo "variant $i: $v" > "$OUT/variant$i.txt"
+        if [ "${VARIANT_TESTS:-0}" = 1 ]; then
+          run "variant${i}_tests" 300 python -u -m pytest tests/test_sage_trainer.py -m gpu -x -q --timeout 120 \
+            --timeout-method thread -p no:cacheprovider -k "oracle or replay or trajectory" || exit $?
+        fi
+        run "tree_kernels_variant$i" 300 python -u tools/tree_kernels.py || exit $?
+      done ;;
     kernels_full)
       run tree_kernels_full 300 python -u tools/tree_kernels.py --num-nodes 100000000 ;;
     kernels_sizes)
