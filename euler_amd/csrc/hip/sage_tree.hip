@@ -1416,7 +1416,7 @@ size_t eh_tr_fwd_lds(int D, int H, int bm, int FL, int mode) {
   size_t b = static_cast<size_t>(bm) * (K2 + 8) * sizeof(bf16_t);
   if (mode != 1 && !alias_out) b += static_cast<size_t>(bm) * (kTrBN + 8) * sizeof(bf16_t);
   if (mode != 2) b += static_cast<size_t>(bm) * (1 + FL) * sizeof(int32_t);
-  if (mode != 2) b += static_cast<size_t>(bm) * (1 + FL) * sizeof(int32_t);  // dedup counts
+  if (TR_FWD_DEDUP && mode != 2) b += static_cast<size_t>(bm) * (1 + FL) * sizeof(int32_t);  // dedup counts
   return b;
 }
 
