@@ -784,6 +784,8 @@ PYBIND11_MODULE(_engine, m) {
     d["remote_calls"] = c.remote_calls.load();
     d["local_connections"] = c.local_connections.load();
     d["tcp_connections"] = c.tcp_connections.load();
+    d["shm_channels"] = c.shm_channels.load();
+    d["shm_bytes"] = c.shm_bytes.load();
     d["rpc_attempts"] = c.rpc_attempts.load();
     d["rpc_failures"] = c.rpc_failures.load();
     d["rpc_bytes_out"] = c.rpc_bytes_out.load();

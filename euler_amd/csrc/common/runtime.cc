@@ -315,7 +315,8 @@ EngineCounters& EngineCounters::Get() {
 
 void EngineCounters::Reset() {
   for (auto* a : {&queries, &compile_us, &exec_us, &dag_nodes, &remote_calls, &rpc_attempts, &rpc_failures,
-                  &rpc_bytes_out, &rpc_bytes_in, &server_requests, &server_us, &local_connections, &tcp_connections})
+                  &rpc_bytes_out, &rpc_bytes_in, &server_requests, &server_us, &local_connections, &tcp_connections,
+                  &shm_channels, &shm_bytes})
     a->store(0);
 }
 

@@ -158,6 +158,7 @@ struct EngineCounters {
   std::atomic<int64_t> remote_calls{0}, rpc_attempts{0}, rpc_failures{0}, rpc_bytes_out{0}, rpc_bytes_in{0};
   std::atomic<int64_t> server_requests{0}, server_us{0};
   std::atomic<int64_t> local_connections{0}, tcp_connections{0};  // client transports
+  std::atomic<int64_t> shm_channels{0}, shm_bytes{0};  // same-host shared-memory payloads (both sides)
   static EngineCounters& Get();
   void Reset();
 };

@@ -7,6 +7,8 @@
 #include <netinet/tcp.h>
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
+#include <sys/mman.h>
+#include <sys/syscall.h>
 #include <sys/socket.h>
 #include <fcntl.h>
 #include <sys/stat.h>
@@ -25,7 +27,26 @@ namespace euler {
 namespace {
 constexpr uint32_t kMagic = 0x524C5545;  // "EULR"
 enum : uint32_t { kPing = 1, kExecute = 2, kMeta = 3, kRegPut = 10, kRegBeat = 11, kRegDel = 12, kRegList = 13,
-                  kReply = 100 };
+                  kShmAttach = 20, kReply = 100 };
+// Same-host shared-memory payloads: a frame whose kind carries kShmFlag has an 8-byte
+// payload = the length of the real payload, which sits at offset 0 of the connection's
+// shared region (one request per connection is in flight, so request and reply take turns).
+constexpr uint32_t kShmFlag = 0x1000;
+constexpr size_t kShmMin = 64 << 10;  // smaller payloads stay in-band
+constexpr unsigned int MFD_CLOEXEC_FLAG = 1U;  // MFD_CLOEXEC
+
+size_t ShmCapacity() {
+  const char* e = std::getenv("EULER_RPC_SHM_MB");
+  const long mb = e ? std::atol(e) : 64;
+  return static_cast<size_t>(mb > 0 ? mb : 0) << 20;
+}
+
+std::string EncodeLen(uint64_t n) { return std::string(reinterpret_cast<const char*>(&n), 8); }
+uint64_t DecodeLen(const std::string& s) {
+  uint64_t n = 0;
+  if (s.size() == 8) memcpy(&n, s.data(), 8);
+  return n;
+}
 
 // wall clock (file mtimes of the registry are wall-clock stamps)
 double WallSec() {
@@ -80,6 +101,39 @@ bool RecvFrame(int fd, uint32_t* kind, std::string* payload) {
   if (magic != kMagic || len > (1ULL << 36)) return false;
   payload->resize(len);
   return len == 0 || ReadAll(fd, &(*payload)[0], len);
+}
+
+// attach frame: kShmAttach with payload = region size; the memfd travels as SCM_RIGHTS
+bool SendAttach(int fd, int memfd, uint64_t size) {
+  char hdr[16 + 8];
+  const uint32_t kind = kShmAttach;
+  const uint64_t len = 8;
+  memcpy(hdr, &kMagic, 4);
+  memcpy(hdr + 4, &kind, 4);
+  memcpy(hdr + 8, &len, 8);
+  memcpy(hdr + 16, &size, 8);
+  struct iovec iov;
+  iov.iov_base = hdr;
+  iov.iov_len = sizeof(hdr);
+  char ctrl[CMSG_SPACE(sizeof(int))];
+  memset(ctrl, 0, sizeof(ctrl));
+  struct msghdr msg;
+  memset(&msg, 0, sizeof(msg));
+  msg.msg_iov = &iov;
+  msg.msg_iovlen = 1;
+  msg.msg_control = ctrl;
+  msg.msg_controllen = sizeof(ctrl);
+  struct cmsghdr* cm = CMSG_FIRSTHDR(&msg);
+  cm->cmsg_level = SOL_SOCKET;
+  cm->cmsg_type = SCM_RIGHTS;
+  cm->cmsg_len = CMSG_LEN(sizeof(int));
+  memcpy(CMSG_DATA(cm), &memfd, sizeof(int));
+  for (;;) {
+    const ssize_t k = ::sendmsg(fd, &msg, MSG_NOSIGNAL);
+    if (k == static_cast<ssize_t>(sizeof(hdr))) return true;
+    if (k < 0 && errno == EINTR) continue;
+    return false;  // a short write of 24 bytes on a fresh Unix socket does not happen
+  }
 }
 
 // Same-host transport: servers also listen on an abstract-namespace Unix socket named after
@@ -668,6 +722,13 @@ struct GraphServer::Conn {
   bool busy = false;    // an execution of this connection is in flight (one at a time)
   bool closed = false;
   bool want_out = false;
+  int pending_fd = -1;  // memfd received with the attach frame
+  char* shm = nullptr;  // the client's shared region (same-host connections)
+  size_t shm_cap = 0;
+  ~Conn() {
+    if (shm) munmap(shm, shm_cap);
+    if (pending_fd >= 0) close(pending_fd);
+  }
 };
 
 struct GraphServer::Loop {
@@ -873,7 +934,27 @@ void GraphServer::RunLoop(Loop* lp) {
 void GraphServer::OnReadable(Loop* lp, const std::shared_ptr<Conn>& c) {
   char buf[1 << 16];
   for (;;) {
-    const ssize_t k = ::recv(c->fd, buf, sizeof(buf), 0);
+    struct iovec iov;
+    iov.iov_base = buf;
+    iov.iov_len = sizeof(buf);
+    char ctrl[CMSG_SPACE(sizeof(int))];
+    struct msghdr msg;
+    memset(&msg, 0, sizeof(msg));
+    msg.msg_iov = &iov;
+    msg.msg_iovlen = 1;
+    msg.msg_control = ctrl;
+    msg.msg_controllen = sizeof(ctrl);
+    const ssize_t k = ::recvmsg(c->fd, &msg, MSG_CMSG_CLOEXEC);
+    if (k > 0) {
+      for (struct cmsghdr* cm = CMSG_FIRSTHDR(&msg); cm; cm = CMSG_NXTHDR(&msg, cm)) {
+        if (cm->cmsg_level == SOL_SOCKET && cm->cmsg_type == SCM_RIGHTS) {
+          int got;
+          memcpy(&got, CMSG_DATA(cm), sizeof(int));
+          if (c->pending_fd >= 0) close(c->pending_fd);
+          c->pending_fd = got;
+        }
+      }
+    }
     if (k > 0) {
       c->in.append(buf, static_cast<size_t>(k));
       continue;
@@ -910,6 +991,34 @@ void GraphServer::Dispatch(Loop* lp, const std::shared_ptr<Conn>& c) {
       c->in.erase(0, c->in_off);
       c->in_off = 0;
     }
+    if (kind == kShmAttach) {  // map the client's region (fd arrived with these bytes)
+      const uint64_t size = DecodeLen(payload);
+      if (c->pending_fd >= 0 && size > 0) {
+        void* p = mmap(nullptr, size, PROT_READ | PROT_WRITE, MAP_SHARED, c->pending_fd, 0);
+        if (p != MAP_FAILED) {
+          if (c->shm) munmap(c->shm, c->shm_cap);
+          c->shm = static_cast<char*>(p);
+          c->shm_cap = size;
+          EngineCounters::Get().shm_channels.fetch_add(1, std::memory_order_relaxed);
+        }
+        close(c->pending_fd);
+        c->pending_fd = -1;
+      }
+      continue;  // no reply
+    }
+    bool via_shm = false;
+    if (kind & kShmFlag) {  // the request payload is in the shared region
+      const uint64_t n = DecodeLen(payload);
+      if (!c->shm || n > c->shm_cap) {
+        Drop(lp, c);
+        return;
+      }
+      payload.assign(c->shm, n);
+      EngineCounters::Get().shm_bytes.fetch_add(static_cast<int64_t>(n), std::memory_order_relaxed);
+      kind &= ~kShmFlag;
+      via_shm = true;
+    }
+    (void)via_shm;
     requests_++;
     EngineCounters::Get().server_requests.fetch_add(1, std::memory_order_relaxed);
     if (kind != kExecute) {
@@ -929,9 +1038,16 @@ void GraphServer::Dispatch(Loop* lp, const std::shared_ptr<Conn>& c) {
     std::shared_ptr<Conn> keep = c;
     pool_->Schedule([this, lp, keep, payload = std::move(payload)] {
       std::string reply = Handle(kExecute, payload);
+      uint32_t rk = kReply;
+      if (keep->shm && reply.size() >= kShmMin && reply.size() <= keep->shm_cap) {
+        // the request was consumed (copied out) before this task ran: the region is free
+        memcpy(keep->shm, reply.data(), reply.size());
+        EngineCounters::Get().shm_bytes.fetch_add(static_cast<int64_t>(reply.size()), std::memory_order_relaxed);
+        reply = EncodeLen(reply.size());
+        rk = kReply | kShmFlag;
+      }
       char hdr[16];
       const uint64_t rl = reply.size();
-      const uint32_t rk = kReply;
       memcpy(hdr, &kMagic, 4);
       memcpy(hdr + 4, &rk, 4);
       memcpy(hdr + 8, &rl, 8);
@@ -1032,7 +1148,7 @@ RpcClients::~RpcClients() {
   pool_.reset();
   for (auto& s : shards_)
     for (auto& h : *std::atomic_load(&s))
-      for (int fd : h->idle) close(fd);
+      for (auto& c : h->idle) CloseChan(&c);
 }
 
 void RpcClients::UpdateShard(int shard, const std::vector<Endpoint>& eps) {
@@ -1059,25 +1175,81 @@ std::map<int, std::vector<std::string>> RpcClients::Endpoints() const {
   return out;
 }
 
+RpcClients::Chan RpcClients::OpenChan(const Endpoint& ep, int timeout_ms) {
+  Chan c;
+  c.fd = Connect(ep, timeout_ms);
+  if (c.fd < 0) return c;
+  struct sockaddr_storage ss;
+  socklen_t sl = sizeof(ss);
+  const size_t cap = ShmCapacity();
+  const char* off = std::getenv("EULER_RPC_SHM");
+  if (cap == 0 || (off && std::string(off) == "0") || getsockname(c.fd, reinterpret_cast<sockaddr*>(&ss), &sl) != 0 ||
+      ss.ss_family != AF_UNIX)
+    return c;
+  // same host: a shared region for large payloads, handed to the server with the attach frame
+  const int mfd = static_cast<int>(syscall(SYS_memfd_create, "euler_amd_rpc", MFD_CLOEXEC_FLAG));
+  if (mfd < 0) return c;
+  if (ftruncate(mfd, static_cast<off_t>(cap)) == 0) {
+    void* p = mmap(nullptr, cap, PROT_READ | PROT_WRITE, MAP_SHARED, mfd, 0);
+    if (p != MAP_FAILED) {
+      if (SendAttach(c.fd, mfd, cap)) {
+        c.shm = static_cast<char*>(p);
+        c.cap = cap;
+        EngineCounters::Get().shm_channels.fetch_add(1, std::memory_order_relaxed);
+      } else {
+        munmap(p, cap);
+      }
+    }
+  }
+  close(mfd);  // the mappings keep the region alive
+  return c;
+}
+
+void RpcClients::CloseChan(Chan* c) {
+  if (c->shm) munmap(c->shm, c->cap);
+  if (c->fd >= 0) close(c->fd);
+  c->shm = nullptr;
+  c->fd = -1;
+}
+
 Status RpcClients::CallHost(Host* h, uint32_t kind, const std::string& payload, std::string* reply) {
-  int fd = -1;
+  Chan c;
   {
     std::lock_guard<std::mutex> l(h->mu);
     if (!h->idle.empty()) {
-      fd = h->idle.back();
+      c = h->idle.back();
       h->idle.pop_back();
     }
   }
-  if (fd < 0) fd = Connect(h->ep, opt_.timeout_ms);
-  if (fd < 0) return Status::Unavailable("connect failed: " + h->ep.ToString());
+  if (c.fd < 0) c = OpenChan(h->ep, opt_.timeout_ms);
+  if (c.fd < 0) return Status::Unavailable("connect failed: " + h->ep.ToString());
   uint32_t rk;
-  if (!SendFrame(fd, kind, payload) || !RecvFrame(fd, &rk, reply) || rk != kReply) {
-    close(fd);
+  bool ok;
+  if (c.shm && payload.size() >= kShmMin && payload.size() <= c.cap) {
+    memcpy(c.shm, payload.data(), payload.size());
+    EngineCounters::Get().shm_bytes.fetch_add(static_cast<int64_t>(payload.size()), std::memory_order_relaxed);
+    ok = SendFrame(c.fd, kind | kShmFlag, EncodeLen(payload.size()));
+  } else {
+    ok = SendFrame(c.fd, kind, payload);
+  }
+  ok = ok && RecvFrame(c.fd, &rk, reply);
+  if (ok && rk == (kReply | kShmFlag) && c.shm) {
+    const uint64_t n = DecodeLen(*reply);
+    ok = n <= c.cap;
+    if (ok) {
+      reply->assign(c.shm, n);
+      EngineCounters::Get().shm_bytes.fetch_add(static_cast<int64_t>(n), std::memory_order_relaxed);
+    }
+  } else {
+    ok = ok && rk == kReply;
+  }
+  if (!ok) {
+    CloseChan(&c);
     return Status::RpcError("rpc to " + h->ep.ToString() + " failed");
   }
   std::lock_guard<std::mutex> l(h->mu);
-  if (static_cast<int>(h->idle.size()) < opt_.num_channels_per_host) h->idle.push_back(fd);
-  else close(fd);
+  if (static_cast<int>(h->idle.size()) < opt_.num_channels_per_host) h->idle.push_back(c);
+  else CloseChan(&c);
   return Status::OK();
 }
 

@@ -198,12 +198,21 @@ class RpcClients : public RemoteClients {
   int64_t failures() const { return failures_.load(); }
 
  private:
+  // a pooled connection; same-host (Unix socket) channels also carry a shared-memory
+  // region for large payloads
+  struct Chan {
+    int fd = -1;
+    char* shm = nullptr;
+    size_t cap = 0;
+  };
   struct Host {
     Endpoint ep;
     std::mutex mu;
-    std::vector<int> idle;  // pooled connected sockets
+    std::vector<Chan> idle;  // pooled connected sockets
     double bad_until = 0;
   };
+  static Chan OpenChan(const Endpoint& ep, int timeout_ms);
+  static void CloseChan(Chan* c);
   typedef std::vector<std::shared_ptr<Host>> HostList;
   Status Call(int shard, uint32_t kind, const std::string& payload, std::string* reply);
   Status CallHost(Host* h, uint32_t kind, const std::string& payload, std::string* reply);

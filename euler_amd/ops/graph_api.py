@@ -219,6 +219,10 @@ def _ragged_slots(idx, k):
 
 
 def _dense_rows(idx, ids, w, t, n, k, default_node):
+    if _uniform_rows(np.asarray(idx).reshape(-1, 2)[:n], k) and len(ids) >= n * k:
+        return (_i64(np.asarray(ids, dtype=np.uint64)[: n * k].reshape(n, k)),
+                _t(np.asarray(w, dtype=np.float32)[: n * k].reshape(n, k)),
+                _t(np.asarray(t, dtype=np.int32)[: n * k].reshape(n, k)))
     out_id = np.full((n, k), np.uint64(default_node & 0xFFFFFFFFFFFFFFFF), dtype=np.uint64)
     out_w = np.zeros((n, k), np.float32)
     out_t = np.full((n, k), -1, np.int32)
@@ -471,8 +475,20 @@ def _feature_query(root, ids_key, ids, prefix, names):
     return [(r[2 * i], r[2 * i + 1]) for i in range(len(names))]
 
 
+def _uniform_rows(idx, k):
+    """True when ragged row i is exactly [i*k, (i+1)*k) (the common full-row case)"""
+    idx = np.asarray(idx).reshape(-1, 2)
+    n = idx.shape[0]
+    if n == 0:
+        return True
+    b, e = idx[:, 0].astype(np.int64), idx[:, 1].astype(np.int64)
+    return bool(b[0] == 0 and (e - b == k).all() and (n == 1 or (b[1:] == e[:-1]).all()))
+
+
 def _dense_from_ragged(idx, vals, dim):
     n = idx.shape[0]
+    if _uniform_rows(idx, int(dim)):  # every row present and full: a reshape
+        return _t(np.asarray(vals, dtype=np.float32)[: n * int(dim)].reshape(n, int(dim)))
     out = np.zeros((n, int(dim)), np.float32)
     rows, slot, src = _ragged_slots(idx, dim)
     out[rows, slot] = np.asarray(vals)[src]
