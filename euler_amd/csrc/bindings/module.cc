@@ -795,4 +795,11 @@ PYBIND11_MODULE(_engine, m) {
     return d;
   }, "per-stage engine counters (process-wide)");
   m.def("reset_stats", [] { EngineCounters::Get().Reset(); });
+  m.def("set_op_profile", [](bool on) { SetOpProfile(on); }, py::arg("on") = true);
+  m.def("op_profile", [] {
+    py::dict d;
+    for (auto& kv : OpProfileSnapshot()) d[py::str(kv.first)] = py::make_tuple(kv.second.first, kv.second.second);
+    return d;
+  });
+  m.def("reset_op_profile", [] { OpProfileReset(); });
 }

@@ -148,24 +148,41 @@ class BytesReader {
 
 class BytesWriter {
  public:
+  BytesWriter() = default;
+  // write into caller memory of `cap` bytes instead of the owned string (size() counts
+  // every byte offered; overflowed() when that exceeds cap and the tail was dropped)
+  BytesWriter(char* ext, size_t cap) : ext_(ext), cap_(cap) {}
   template <typename T>
   void Write(const T& v) {
-    buf_.append(reinterpret_cast<const char*>(&v), sizeof(T));
+    WriteRaw(&v, sizeof(T));
   }
   template <typename T>
   void Write(const std::vector<T>& v) {
     Write<uint32_t>(static_cast<uint32_t>(v.size()));
-    if (!v.empty()) buf_.append(reinterpret_cast<const char*>(v.data()), v.size() * sizeof(T));
+    if (!v.empty()) WriteRaw(v.data(), v.size() * sizeof(T));
   }
   void Write(const std::string& s) {
     Write<uint32_t>(static_cast<uint32_t>(s.size()));
-    buf_.append(s);
+    WriteRaw(s.data(), s.size());
   }
-  void WriteRaw(const void* p, size_t n) { buf_.append(static_cast<const char*>(p), n); }
+  void WriteRaw(const void* p, size_t n) {
+    if (!ext_) {
+      buf_.append(static_cast<const char*>(p), n);
+      return;
+    }
+    if (len_ + n <= cap_) memcpy(ext_ + len_, p, n);
+    else overflow_ = true;
+    len_ += n;
+  }
   std::string& str() { return buf_; }
+  size_t size() const { return ext_ ? len_ : buf_.size(); }
+  bool overflowed() const { return overflow_; }
 
  private:
   std::string buf_;
+  char* ext_ = nullptr;
+  size_t cap_ = 0, len_ = 0;
+  bool overflow_ = false;
 };
 
 // ---------------------------------------------------------------- hash

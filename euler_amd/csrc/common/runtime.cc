@@ -320,4 +320,35 @@ void EngineCounters::Reset() {
     a->store(0);
 }
 
+namespace {
+std::atomic<int> g_op_profile{-1};
+std::mutex g_op_prof_mu;
+std::map<std::string, std::pair<int64_t, int64_t>> g_op_prof;
+}  // namespace
+
+bool OpProfileEnabled() {
+  int v = g_op_profile.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = getenv("EULER_OP_PROFILE");
+    v = (e && atoi(e) != 0) ? 1 : 0;
+    g_op_profile.store(v, std::memory_order_relaxed);
+  }
+  return v == 1;
+}
+void SetOpProfile(bool on) { g_op_profile.store(on ? 1 : 0, std::memory_order_relaxed); }
+void OpProfileAdd(const std::string& op, int64_t us) {
+  std::lock_guard<std::mutex> l(g_op_prof_mu);
+  auto& e = g_op_prof[op];
+  e.first += us;
+  e.second += 1;
+}
+std::map<std::string, std::pair<int64_t, int64_t>> OpProfileSnapshot() {
+  std::lock_guard<std::mutex> l(g_op_prof_mu);
+  return g_op_prof;
+}
+void OpProfileReset() {
+  std::lock_guard<std::mutex> l(g_op_prof_mu);
+  g_op_prof.clear();
+}
+
 }  // namespace euler

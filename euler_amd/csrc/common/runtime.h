@@ -15,6 +15,7 @@
 #include <stdint.h>
 
 #include <atomic>
+#include <map>
 #include <condition_variable>
 #include <deque>
 #include <functional>
@@ -162,6 +163,15 @@ struct EngineCounters {
   static EngineCounters& Get();
   void Reset();
 };
+
+// Opt-in per-op kernel profile (EULER_OP_PROFILE=1 or SetOpProfile(true)): wall
+// microseconds and calls by op name, both sides of the RPC (server DAGs included).
+// Async kernels (REMOTE) are timed from launch to completion callback.
+bool OpProfileEnabled();
+void SetOpProfile(bool on);
+void OpProfileAdd(const std::string& op, int64_t us);
+std::map<std::string, std::pair<int64_t, int64_t>> OpProfileSnapshot();  // op -> (us, calls)
+void OpProfileReset();
 
 // adds the elapsed microseconds to a counter when it goes out of scope
 class ScopedMicros {

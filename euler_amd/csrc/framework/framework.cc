@@ -1,9 +1,80 @@
 #include "framework/framework.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 namespace euler {
+
+// ============================================================================ buffer cache
+namespace {
+constexpr size_t kBlockMin = size_t(1) << 20;
+struct BlockCache {
+  std::mutex mu;
+  std::vector<std::vector<void*>> free;  // by log2 size class
+  size_t cached = 0, cap = 0;
+  BlockCache() : free(64) {
+    const char* e = getenv("EULER_TENSOR_CACHE_MB");
+    cap = static_cast<size_t>(e ? std::max(0L, atol(e)) : 512) << 20;
+  }
+  ~BlockCache() = delete;  // process lifetime (buffers may be freed during static teardown)
+};
+BlockCache& Cache() {
+  static BlockCache* c = new BlockCache();
+  return *c;
+}
+int SizeClass(size_t n) {
+  int k = 20;
+  while ((size_t(1) << k) < n) ++k;
+  return k;
+}
+}  // namespace
+
+void* TensorBlockAlloc(size_t n) {
+  if (n < kBlockMin) {
+    void* p = std::malloc(n ? n : 1);
+    if (!p) throw std::bad_alloc();
+    return p;
+  }
+  const int k = SizeClass(n);
+  BlockCache& c = Cache();
+  {
+    std::lock_guard<std::mutex> l(c.mu);
+    if (!c.free[k].empty()) {
+      void* p = c.free[k].back();
+      c.free[k].pop_back();
+      c.cached -= size_t(1) << k;
+      return p;
+    }
+  }
+  void* p = std::malloc(size_t(1) << k);
+  if (!p) throw std::bad_alloc();
+  return p;
+}
+
+void TensorBlockFree(void* p, size_t n) {
+  if (!p) return;
+  if (n < kBlockMin) {
+    std::free(p);
+    return;
+  }
+  const int k = SizeClass(n);
+  BlockCache& c = Cache();
+  {
+    std::lock_guard<std::mutex> l(c.mu);
+    if (c.cached + (size_t(1) << k) <= c.cap) {
+      c.free[k].push_back(p);
+      c.cached += size_t(1) << k;
+      return;
+    }
+  }
+  std::free(p);
+}
+
+size_t TensorBlockCached() {
+  std::lock_guard<std::mutex> l(Cache().mu);
+  return Cache().cached;
+}
 
 // ============================================================================ Tensor
 size_t DTypeSize(DType t) {
@@ -26,7 +97,19 @@ const char* DTypeName(DType t) {
 Tensor::Tensor(DType t, std::vector<int64_t> shape) : dtype_(t), shape_(std::move(shape)) {
   const int64_t n = numel();
   if (t == DType::kString) strs_ = std::make_shared<std::vector<std::string>>(n);
-  else bytes_ = std::make_shared<std::vector<char>>(static_cast<size_t>(n) * DTypeSize(t));
+  else {
+    bytes_ = std::make_shared<ByteBuf>(static_cast<size_t>(n) * DTypeSize(t));
+    if (!bytes_->empty()) memset(bytes_->data(), 0, bytes_->size());
+  }
+}
+
+Tensor Tensor::Uninit(DType t, std::vector<int64_t> shape) {
+  if (t == DType::kString) return Tensor(t, std::move(shape));
+  Tensor r;
+  r.dtype_ = t;
+  r.shape_ = std::move(shape);
+  r.bytes_ = std::make_shared<ByteBuf>(static_cast<size_t>(r.numel()) * DTypeSize(t));
+  return r;
 }
 
 Tensor Tensor::Strings(const std::vector<std::string>& v, std::vector<int64_t> shape) {
@@ -125,6 +208,16 @@ void Tensor::Encode(BytesWriter* w) const {
   }
 }
 
+size_t Tensor::EncodedSize() const {
+  size_t n = 4 + 4 + 8 * shape_.size();
+  if (dtype_ == DType::kString) {
+    for (const auto& x : *strs_) n += 4 + x.size();
+  } else {
+    n += 8 + nbytes();
+  }
+  return n;
+}
+
 bool Tensor::Decode(BytesReader* r, Tensor* t) {
   int32_t dt;
   uint32_t rank;
@@ -132,7 +225,7 @@ bool Tensor::Decode(BytesReader* r, Tensor* t) {
   std::vector<int64_t> shape(rank);
   for (auto& d : shape)
     if (!r->Read(&d)) return false;
-  *t = Tensor(static_cast<DType>(dt), shape);
+  *t = Tensor::Uninit(static_cast<DType>(dt), shape);
   if (t->dtype() == DType::kString) {
     for (auto& s : t->strings())
       if (!r->Read(&s)) return false;
@@ -367,8 +460,13 @@ void Executor::Schedule(size_t i) {
   }
   EngineCounters::Get().dag_nodes.fetch_add(1, std::memory_order_relaxed);
   auto run = [this, i, k, &nd] {
+    const bool prof = OpProfileEnabled();
+    const uint64_t t0 = prof ? NowMicros() : 0;
     if (k->is_async()) {
-      k->ComputeAsync(nd, ctx_, [this, i](Status st) { NodeDone(i, st); });
+      k->ComputeAsync(nd, ctx_, [this, i, prof, t0, &nd](Status st) {
+        if (prof) OpProfileAdd(nd.op, static_cast<int64_t>(NowMicros() - t0));
+        NodeDone(i, st);
+      });
       return;
     }
     Status st;
@@ -377,6 +475,7 @@ void Executor::Schedule(size_t i) {
     } catch (const std::exception& e) {
       st = Status::Internal(nd.name() + ": " + e.what());
     }
+    if (prof) OpProfileAdd(nd.op, static_cast<int64_t>(NowMicros() - t0));
     NodeDone(i, st);
   };
   run();

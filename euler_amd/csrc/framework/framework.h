@@ -47,13 +47,48 @@ template <> struct DTypeOf<uint64_t> { static constexpr DType v = DType::kUInt64
 template <> struct DTypeOf<float> { static constexpr DType v = DType::kFloat; };
 template <> struct DTypeOf<double> { static constexpr DType v = DType::kDouble; };
 
+// Large tensor buffers (>= 1 MiB) are recycled through a process-wide cache of
+// power-of-two blocks instead of going back to the OS: a fresh multi-MB malloc is an
+// mmap whose first touch page-faults every 4 KiB, which dominated the remote feature
+// path (13 MB replies).  Capped by EULER_TENSOR_CACHE_MB (default 512; 0 disables).
+void* TensorBlockAlloc(size_t n);
+void TensorBlockFree(void* p, size_t n);
+size_t TensorBlockCached();
+
+// byte storage whose resize leaves the bytes uninitialised: Tensor's constructor zeroes
+// them explicitly, Tensor::Uninit skips that for buffers the caller overwrites whole
+template <typename T>
+struct NoInitAlloc : std::allocator<T> {
+  using value_type = T;
+  T* allocate(size_t n) { return static_cast<T*>(TensorBlockAlloc(n * sizeof(T))); }
+  void deallocate(T* p, size_t n) { TensorBlockFree(p, n * sizeof(T)); }
+  template <typename U>
+  struct rebind {
+    using other = NoInitAlloc<U>;
+  };
+  NoInitAlloc() = default;
+  template <typename U>
+  NoInitAlloc(const NoInitAlloc<U>&) {}
+  template <typename U>
+  void construct(U* p) {
+    ::new (static_cast<void*>(p)) U;
+  }
+  template <typename U, typename... A>
+  void construct(U* p, A&&... a) {
+    ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+  }
+};
+using ByteBuf = std::vector<char, NoInitAlloc<char>>;
+
 class Tensor {
  public:
   Tensor() = default;
-  Tensor(DType t, std::vector<int64_t> shape);
+  Tensor(DType t, std::vector<int64_t> shape);  // zero-filled
+  static Tensor Uninit(DType t, std::vector<int64_t> shape);  // numeric only, bytes undefined
   template <typename T>
   static Tensor FromVector(const std::vector<T>& v, std::vector<int64_t> shape = {}) {
-    Tensor t(DTypeOf<T>::v, shape.empty() ? std::vector<int64_t>{static_cast<int64_t>(v.size())} : shape);
+    Tensor t = Uninit(DTypeOf<T>::v, shape.empty() ? std::vector<int64_t>{static_cast<int64_t>(v.size())} : shape);
+    if (t.nbytes() > v.size() * sizeof(T)) memset(t.raw(), 0, t.nbytes());
     if (!v.empty()) memcpy(t.raw(), v.data(), v.size() * sizeof(T));
     return t;
   }
@@ -93,12 +128,13 @@ class Tensor {
   void Reshape(std::vector<int64_t> s) { shape_ = std::move(s); }
 
   void Encode(BytesWriter* w) const;
+  size_t EncodedSize() const;  // bytes Encode writes
   static bool Decode(BytesReader* r, Tensor* t);
 
  private:
   DType dtype_ = DType::kInt64;
   std::vector<int64_t> shape_;
-  std::shared_ptr<std::vector<char>> bytes_;
+  std::shared_ptr<ByteBuf> bytes_;
   std::shared_ptr<std::vector<std::string>> strs_;
 };
 
@@ -122,6 +158,7 @@ struct NodeDef {
   std::string name() const { return op + "," + std::to_string(id); }
   std::string Output(int slot) const { return name() + ":" + std::to_string(slot); }
   void Encode(BytesWriter* w) const;
+  size_t EncodedSize() const;  // bytes Encode writes
   static bool Decode(BytesReader* r, NodeDef* n);
   std::string DebugString(int indent = 0) const;
 };

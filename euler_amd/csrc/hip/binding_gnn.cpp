@@ -60,9 +60,16 @@ const int32_t* order_ptr(const c10::optional<torch::Tensor>& order, int64_t rows
   return order->data_ptr<int32_t>();
 }
 
+const float* asrc_ptr(const c10::optional<torch::Tensor>& a_src, int64_t H, int64_t C) {
+  if (!a_src.has_value()) return nullptr;
+  typed(*a_src, torch::kFloat32, "a_src");
+  TORCH_CHECK(a_src->numel() == H * C && a_src->is_contiguous(), "a_src must be a contiguous [H, C] fp32 tensor");
+  return a_src->data_ptr<float>();
+}
+
 std::vector<torch::Tensor> gat_fwd(torch::Tensor indptr, torch::Tensor col, c10::optional<torch::Tensor> order,
                                    torch::Tensor h, torch::Tensor al, torch::Tensor ar, int64_t H, int64_t C,
-                                   double slope) {
+                                   double slope, c10::optional<torch::Tensor> a_src) {
   gat_common(indptr, col, h, al, ar, H, C);
   const c10::DeviceGuard g(h.device());
   const int64_t S = indptr.numel() - 1;
@@ -70,7 +77,8 @@ std::vector<torch::Tensor> gat_fwd(torch::Tensor indptr, torch::Tensor col, c10:
   auto lse = torch::empty({S, H}, al.options());
   ok(eh_gat_fwd(indptr.data_ptr<int64_t>(), col.data_ptr<int32_t>(), order_ptr(order, S, "order"), S, h.data_ptr(),
                 h.scalar_type() == torch::kBFloat16, al.data_ptr<float>(), ar.data_ptr<float>(), static_cast<int>(H),
-                static_cast<int>(C), static_cast<float>(slope), out.data_ptr(), lse.data_ptr<float>(), stream()),
+                static_cast<int>(C), static_cast<float>(slope), out.data_ptr(), lse.data_ptr<float>(),
+                asrc_ptr(a_src, H, C), stream()),
      "gat_fwd");
   return {out, lse};
 }
@@ -78,7 +86,8 @@ std::vector<torch::Tensor> gat_fwd(torch::Tensor indptr, torch::Tensor col, c10:
 std::vector<torch::Tensor> gat_bwd(torch::Tensor indptr, torch::Tensor col, c10::optional<torch::Tensor> order,
                                    torch::Tensor cindptr, torch::Tensor crow, c10::optional<torch::Tensor> corder,
                                    torch::Tensor h, torch::Tensor al, torch::Tensor ar, int64_t H, int64_t C,
-                                   double slope, torch::Tensor out, torch::Tensor dout, torch::Tensor lse) {
+                                   double slope, torch::Tensor out, torch::Tensor dout, torch::Tensor lse,
+                                   c10::optional<torch::Tensor> a_src) {
   gat_common(indptr, col, h, al, ar, H, C);
   typed(cindptr, torch::kInt64, "cindptr");
   typed(crow, torch::kInt32, "crow");
@@ -100,7 +109,7 @@ std::vector<torch::Tensor> gat_bwd(torch::Tensor indptr, torch::Tensor col, c10:
                 h.data_ptr(), h.scalar_type() == torch::kBFloat16, al.data_ptr<float>(), ar.data_ptr<float>(),
                 static_cast<int>(H), static_cast<int>(C), static_cast<float>(slope), out.data_ptr(), dout.data_ptr(),
                 lse.data_ptr<float>(), stat.data_ptr<float>(), dh.data_ptr(), dal.data_ptr<float>(),
-                dar.data_ptr<float>(), stream()),
+                dar.data_ptr<float>(), asrc_ptr(a_src, H, C), stream()),
      "gat_bwd");
   return {dh, dal, dar};
 }
@@ -512,8 +521,11 @@ std::vector<torch::Tensor> unique_first_padded(torch::Tensor x, int64_t fill) {
 
 void register_gnn_ops(pybind11::module& m) {
   m.def("gat_supported", &gat_supported);
-  m.def("gat_fwd", &gat_fwd);
-  m.def("gat_bwd", &gat_bwd);
+  m.def("gat_fwd", &gat_fwd, py::arg("indptr"), py::arg("col"), py::arg("order"), py::arg("h"), py::arg("al"),
+        py::arg("ar"), py::arg("H"), py::arg("C"), py::arg("slope"), py::arg("a_src") = py::none());
+  m.def("gat_bwd", &gat_bwd, py::arg("indptr"), py::arg("col"), py::arg("order"), py::arg("cindptr"), py::arg("crow"),
+        py::arg("corder"), py::arg("h"), py::arg("al"), py::arg("ar"), py::arg("H"), py::arg("C"), py::arg("slope"),
+        py::arg("out"), py::arg("dout"), py::arg("lse"), py::arg("a_src") = py::none());
   m.def("gat_att_fwd", &gat_att_fwd);
   m.def("gat_att_bwd_", &gat_att_bwd_);
   m.def("rel_gemm", &rel_gemm);

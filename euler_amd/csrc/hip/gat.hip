@@ -106,14 +106,19 @@ __global__ __launch_bounds__(256) void gat_fwd_kernel(const int64_t* __restrict_
                                                       const int32_t* __restrict__ order, int64_t S,
                                                       const T* __restrict__ h, const float* __restrict__ al,
                                                       const float* __restrict__ ar, int H, int C, float slope, int lp,
-                                                      T* __restrict__ out, float* __restrict__ lse) {
+                                                      T* __restrict__ out, float* __restrict__ lse,
+                                                      const float* __restrict__ a_src) {
   constexpr int V = GV<T>::N;
   constexpr int U = GAT_UF;
-  const int HC = H * C, nch = HC / V;
+  const int HC = H * C, nch = HC / V, g = C / V;
   const GatLane L = gat_lane(lp, S, order);
+  // a_src given: al[j, h] = <h_j, a_src[h]> is recomputed from the neighbour row already in
+  // registers (same per-lane partial + group sum as gat_att_fwd) instead of gathered, so an
+  // edge costs one row fetch, not a row plus a 32-byte al line
+  const bool rc = a_src != nullptr;
   bool ok[MAXCH];
   int hd[MAXCH];
-  float ari[MAXCH], m[MAXCH], l[MAXCH], acc[MAXCH][V];
+  float ari[MAXCH], m[MAXCH], l[MAXCH], acc[MAXCH][V], asv[MAXCH][V];
 #pragma unroll
   for (int k = 0; k < MAXCH; ++k) {
     const int c = L.sub + k * lp;
@@ -123,7 +128,10 @@ __global__ __launch_bounds__(256) void gat_fwd_kernel(const int64_t* __restrict_
     m[k] = -INFINITY;
     l[k] = 0.f;
 #pragma unroll
-    for (int v = 0; v < V; ++v) acc[k][v] = 0.f;
+    for (int v = 0; v < V; ++v) {
+      acc[k][v] = 0.f;
+      asv[k][v] = (rc && c < nch) ? a_src[c * V + v] : 0.f;
+    }
   }
   const int64_t a = L.ok ? indptr[L.row] : 0, b = L.ok ? indptr[L.row + 1] : 0;
   int32_t jn[U];
@@ -142,11 +150,21 @@ __global__ __launch_bounds__(256) void gat_fwd_kernel(const int64_t* __restrict_
       for (int u = 0; u < U; ++u) {
         s[u] = -INFINITY;
         if (j[u] >= 0) {
-          s[u] = al[static_cast<int64_t>(j[u]) * H + hd[k]];
+          if (!rc) s[u] = al[static_cast<int64_t>(j[u]) * H + hd[k]];
           GV<T>::load(h + static_cast<int64_t>(j[u]) * HC + c0, x[u]);
         } else {
 #pragma unroll
           for (int v = 0; v < V; ++v) x[u][v] = 0.f;
+        }
+      }
+      if (rc) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          float d = 0.f;
+#pragma unroll
+          for (int v = 0; v < V; ++v) d += x[u][v] * asv[k][v];
+          d = gat_group_sum(d, g);
+          if (j[u] >= 0) s[u] = d;
         }
       }
       // one rescale per batch: nm = max(m, max_u s_u)
@@ -189,17 +207,20 @@ __global__ __launch_bounds__(256) void gat_bwd_dst_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ col, const int32_t* __restrict__ order,
     int64_t S, const T* __restrict__ h, const float* __restrict__ al, const float* __restrict__ ar, int H, int C,
     float slope, int lp, const T* __restrict__ out, const T* __restrict__ dout, const float* __restrict__ lse,
-    float* __restrict__ dar, float4_t* __restrict__ stat) {
+    float* __restrict__ dar, float4_t* __restrict__ stat, const float* __restrict__ a_src) {
   constexpr int V = GV<T>::N;
   constexpr int U = GAT_UB;
   const int HC = H * C, nch = HC / V, g = C / V;
   const GatLane L = gat_lane(lp, S, order);
+  const bool rc = a_src != nullptr;  // recompute al from the gathered row (see the forward)
   bool ok[MAXCH];
   int hd[MAXCH];
-  float ari[MAXCH], lsei[MAXCH], Dv[MAXCH], dacc[MAXCH], dO[MAXCH][V];
+  float ari[MAXCH], lsei[MAXCH], Dv[MAXCH], dacc[MAXCH], dO[MAXCH][V], asv[MAXCH][V];
 #pragma unroll
   for (int k = 0; k < MAXCH; ++k) {
     const int c = L.sub + k * lp;
+#pragma unroll
+    for (int v = 0; v < V; ++v) asv[k][v] = (rc && c < nch) ? a_src[c * V + v] : 0.f;
     ok[k] = L.ok && c < nch;
     hd[k] = ok[k] ? (c * V) / C : 0;
     dacc[k] = 0.f;
@@ -230,22 +251,27 @@ __global__ __launch_bounds__(256) void gat_bwd_dst_kernel(
     for (int k = 0; k < MAXCH; ++k) {
       if (!ok[k]) continue;
       const int c0 = (L.sub + k * lp) * V;
-      float z[U], part[U];
+      float z[U], part[U], alp[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         part[u] = 0.f;
+        alp[u] = 0.f;
         z[u] = 0.f;
         if (j[u] >= 0) {
           float x[V];
-          z[u] = al[static_cast<int64_t>(j[u]) * H + hd[k]] + ari[k];
+          if (!rc) z[u] = al[static_cast<int64_t>(j[u]) * H + hd[k]] + ari[k];
           GV<T>::load(h + static_cast<int64_t>(j[u]) * HC + c0, x);
 #pragma unroll
-          for (int v = 0; v < V; ++v) part[u] += dO[k][v] * x[v];
+          for (int v = 0; v < V; ++v) {
+            part[u] += dO[k][v] * x[v];
+            alp[u] += x[v] * asv[k][v];
+          }
         }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (j[u] < 0) continue;
+        if (rc) z[u] = gat_group_sum(alp[u], g) + ari[k];
         const float dp = gat_group_sum(part[u], g);
         const float p = __expf(lrelu(z[u], slope) - lsei[k]);
         const float ds = p * (dp - Dv[k]);
@@ -513,17 +539,17 @@ int eh_gat_supported(int H, int C, int is_bf16) {
 
 hipError_t eh_gat_fwd(const int64_t* indptr, const int32_t* col, const int32_t* order, int64_t S, const void* h,
                       int is_bf16, const float* al, const float* ar, int H, int C, float slope, void* out, float* lse,
-                      hipStream_t s) {
+                      const float* a_src, hipStream_t s) {
   if (S == 0) return hipSuccess;
   if (!eh_gat_supported(H, C, is_bf16)) return hipErrorInvalidValue;
   const GatShape sh = gat_shape(H * C, is_bf16 ? 8 : 4);
   const dim3 grid = gat_grid(S, sh.lp);
   if (is_bf16) {
     GAT_DISPATCH(bf16_t, sh.maxch, gat_fwd_kernel, grid, dim3(256), 0, s, indptr, col, order, S,
-                 static_cast<const bf16_t*>(h), al, ar, H, C, slope, sh.lp, static_cast<bf16_t*>(out), lse)
+                 static_cast<const bf16_t*>(h), al, ar, H, C, slope, sh.lp, static_cast<bf16_t*>(out), lse, a_src)
   } else {
     GAT_DISPATCH(float, sh.maxch, gat_fwd_kernel, grid, dim3(256), 0, s, indptr, col, order, S,
-                 static_cast<const float*>(h), al, ar, H, C, slope, sh.lp, static_cast<float*>(out), lse)
+                 static_cast<const float*>(h), al, ar, H, C, slope, sh.lp, static_cast<float*>(out), lse, a_src)
   }
   return hipGetLastError();
 }
@@ -573,7 +599,7 @@ hipError_t eh_gat_bwd(const int64_t* indptr, const int32_t* col, const int32_t* 
                       const int64_t* cindptr, const int32_t* crow, const int32_t* corder, int64_t N, const void* h,
                       int is_bf16, const float* al, const float* ar, int H, int C, float slope, const void* out,
                       const void* dout, const float* lse, float* stat, void* dh, float* dal, float* dar,
-                      hipStream_t s) {
+                      const float* a_src, hipStream_t s) {
   if (!eh_gat_supported(H, C, is_bf16)) return hipErrorInvalidValue;
   const GatShape sh = gat_shape(H * C, is_bf16 ? 8 : 4);
   float4_t* st = reinterpret_cast<float4_t*>(stat);
@@ -582,11 +608,11 @@ hipError_t eh_gat_bwd(const int64_t* indptr, const int32_t* col, const int32_t* 
     if (is_bf16) {
       GAT_DISPATCH(bf16_t, sh.maxch, gat_bwd_dst_kernel, grid, dim3(256), 0, s, indptr, col, order, S,
                    static_cast<const bf16_t*>(h), al, ar, H, C, slope, sh.lp, static_cast<const bf16_t*>(out),
-                   static_cast<const bf16_t*>(dout), lse, dar, st)
+                   static_cast<const bf16_t*>(dout), lse, dar, st, a_src)
     } else {
       GAT_DISPATCH(float, sh.maxch, gat_bwd_dst_kernel, grid, dim3(256), 0, s, indptr, col, order, S,
                    static_cast<const float*>(h), al, ar, H, C, slope, sh.lp, static_cast<const float*>(out),
-                   static_cast<const float*>(dout), lse, dar, st)
+                   static_cast<const float*>(dout), lse, dar, st, a_src)
     }
     EULER_HIP_CHECK(hipGetLastError());
   }

@@ -81,10 +81,12 @@ hipError_t eh_st_shadow(const float* p, int64_t n, int sh_count, const int64_t* 
 
 // gat.hip (K5: fused multi-head GAT edge-softmax + aggregation)
 int eh_gat_supported(int H, int C, int is_bf16);
-// order / corder: optional visiting order of the CSR / CSC rows (nullptr = identity)
+// order / corder: optional visiting order of the CSR / CSC rows (nullptr = identity);
+// a_src (optional, [H*C]): al = <h, a_src> per head, recomputed from each gathered row
+// instead of read from al (h must then be the same rows al was computed from)
 hipError_t eh_gat_fwd(const int64_t* indptr, const int32_t* col, const int32_t* order, int64_t S, const void* h,
                       int is_bf16, const float* al, const float* ar, int H, int C, float slope, void* out, float* lse,
-                      hipStream_t s);
+                      const float* a_src, hipStream_t s);
 // attention terms al/ar = <z, a_src/a_dst> per head, and their backward (dz += ..., da += ...)
 hipError_t eh_gat_att_fwd(const void* z, int is_bf16, int64_t N, int H, int C, const float* a_src,
                           const float* a_dst, float* al, float* ar, hipStream_t s);
@@ -97,7 +99,7 @@ hipError_t eh_gat_bwd(const int64_t* indptr, const int32_t* col, const int32_t* 
                       const int64_t* cindptr, const int32_t* crow, const int32_t* corder, int64_t N, const void* h,
                       int is_bf16, const float* al, const float* ar, int H, int C, float slope, const void* out,
                       const void* dout, const float* lse, float* stat, void* dh, float* dal, float* dar,
-                      hipStream_t s);
+                      const float* a_src, hipStream_t s);
 
 // rgcn.hip (K6: relation-grouped MFMA GEMM)
 size_t eh_rel_gemm_lds(int K, int N, int mode);

@@ -44,7 +44,7 @@ int64_t RowWidth(const Tensor& t) {
   return r > 0 ? t.numel() / r : (t.shape().size() > 1 ? t.dim(1) : 1);
 }
 
-// gather rows of t (any dtype) into a new tensor
+// gather rows of t (any dtype) into a new tensor; runs of consecutive rows are one memcpy
 Tensor TakeRows(const Tensor& t, const std::vector<int64_t>& rows, int64_t width) {
   std::vector<int64_t> shape = t.shape();
   if (shape.empty()) shape = {static_cast<int64_t>(rows.size())};
@@ -57,10 +57,53 @@ Tensor TakeRows(const Tensor& t, const std::vector<int64_t>& rows, int64_t width
     const size_t es = DTypeSize(t.dtype()) * width;
     const char* src = static_cast<const char*>(t.raw());
     char* dst = static_cast<char*>(out.raw());
-    for (size_t i = 0; i < rows.size(); ++i) memcpy(dst + i * es, src + rows[i] * es, es);
+    for (size_t i = 0; i < rows.size();) {
+      size_t j = i + 1;
+      while (j < rows.size() && rows[j] == rows[j - 1] + 1) ++j;
+      memcpy(dst + i * es, src + rows[i] * es, (j - i) * es);
+      i = j;
+    }
   }
   return out;
 }
+
+// g == 0, 1, ..., rows-1 (a gather that keeps every row in place)
+bool IsIdentity(const Tensor& g, int64_t rows) {
+  if (g.numel() != rows) return false;
+  for (int64_t i = 0; i < rows; ++i)
+    if (g.AsInt(i) != i) return false;
+  return true;
+}
+
+// open-addressing id -> first position map (linear probing, power-of-two capacity)
+class IdPosMap {
+ public:
+  explicit IdPosMap(size_t n) {
+    size_t cap = 16;
+    while (cap < 2 * n) cap <<= 1;
+    mask_ = cap - 1;
+    keys_.resize(cap);
+    pos_.assign(cap, -1);
+  }
+  // position of `id`, inserting `next` when absent (returns next then)
+  int32_t FindOrInsert(uint64_t id, int32_t next) {
+    size_t h = static_cast<size_t>((id * 0x9E3779B97F4A7C15ull) >> 17) & mask_;
+    for (;;) {
+      if (pos_[h] < 0) {
+        keys_[h] = id;
+        pos_[h] = next;
+        return next;
+      }
+      if (keys_[h] == id) return pos_[h];
+      h = (h + 1) & mask_;
+    }
+  }
+
+ private:
+  size_t mask_;
+  std::vector<uint64_t> keys_;
+  std::vector<int32_t> pos_;
+};
 
 Tensor Concat(const std::vector<const Tensor*>& parts, DType fallback, int64_t width_hint) {
   int64_t rows = 0, width = width_hint > 0 ? width_hint : 1;
@@ -104,6 +147,15 @@ class IdSplitOp : public OpKernel {
     const bool edges = in.shape().size() == 2 && in.dim(1) == 3;
     const int64_t n = edges ? in.dim(0) : in.numel();
     const int64_t width = edges ? 3 : 1;
+    if (S == 1) {  // one shard: the ids as they are, identity merge index
+      Tensor part = in;
+      if (!edges) part.Reshape({n});
+      ctx->Set(nd.Output(0), part);
+      std::vector<int32_t> mi(n);
+      for (int64_t i = 0; i < n; ++i) mi[i] = static_cast<int32_t>(i);
+      ctx->Set(nd.Output(1), Tensor::FromVector(mi));
+      return;
+    }
     std::vector<std::vector<int64_t>> rows(S);
     for (int64_t i = 0; i < n; ++i) {
       // edges are split by their source (reference id_split_op.cc:46-49)
@@ -247,6 +299,14 @@ class DataMergeOp : public OpKernel {
       }
       total_rows += Rows(d[s]);
     }
+    if (S == 1) {  // single shard in original order: the data is already merged
+      bool identity = true;
+      for (int64_t i = 0; i < mi[0].numel() && identity; ++i) identity = mi[0].AsInt(i) == i;
+      if (identity) {
+        ctx->Set(nd.Output(0), d[0]);
+        return;
+      }
+    }
     // destination offsets in original order
     std::vector<int64_t> counts(n, 0);
     std::vector<std::pair<int, int64_t>> where(n);  // (shard, local row)
@@ -373,17 +433,14 @@ class IdUniqueOp : public OpKernel {
       return;
     }
     auto ids = in.ToUInt64();
-    std::unordered_map<uint64_t, int32_t> pos;
-    pos.reserve(ids.size() * 2);
+    IdPosMap pos(ids.size());
     std::vector<uint64_t> uniq;
+    uniq.reserve(ids.size());
     std::vector<int32_t> gidx(ids.size());
     for (size_t i = 0; i < ids.size(); ++i) {
-      auto it = pos.find(ids[i]);
-      if (it == pos.end()) {
-        it = pos.emplace(ids[i], static_cast<int32_t>(uniq.size())).first;
-        uniq.push_back(ids[i]);
-      }
-      gidx[i] = it->second;
+      const int32_t next = static_cast<int32_t>(uniq.size());
+      gidx[i] = pos.FindOrInsert(ids[i], next);
+      if (gidx[i] == next) uniq.push_back(ids[i]);
     }
     ctx->Set(nd.Output(0), Tensor::FromVector(uniq));
     ctx->Set(nd.Output(1), Tensor::FromVector(gidx));
@@ -394,6 +451,10 @@ class IdxGatherOp : public OpKernel {
  public:
   void Compute(const NodeDef& nd, OpContext* ctx) override {
     const Tensor& idx = ctx->Get(nd.inputs.at(0));
+    if (IsIdentity(ctx->Get(nd.inputs.at(1)), Rows(idx))) {  // ids were already distinct
+      ctx->Set(nd.Output(0), idx);
+      return;
+    }
     auto g = ctx->Get(nd.inputs.at(1)).ToInt64();
     const int32_t* p = idx.data<int32_t>();
     std::vector<int64_t> counts(g.size());
@@ -407,13 +468,35 @@ class DataGatherOp : public OpKernel {
   void Compute(const NodeDef& nd, OpContext* ctx) override {
     const Tensor& d = ctx->Get(nd.inputs.at(0));
     const Tensor& idx = ctx->Get(nd.inputs.at(1));
+    if (IsIdentity(ctx->Get(nd.inputs.at(2)), Rows(idx))) {
+      ctx->Set(nd.Output(0), d);
+      return;
+    }
     auto g = ctx->Get(nd.inputs.at(2)).ToInt64();
     const int32_t* p = idx.data<int32_t>();
     const int64_t w = RowWidth(d);
-    std::vector<int64_t> rows;
-    for (int64_t u : g)
-      for (int32_t k = p[2 * u]; k < p[2 * u + 1]; ++k) rows.push_back(k);
-    ctx->Set(nd.Output(0), TakeRows(d, rows, w));
+    int64_t total = 0;
+    for (int64_t u : g) total += p[2 * u + 1] - p[2 * u];
+    std::vector<int64_t> shape = d.shape();
+    if (shape.empty()) shape = {0};
+    shape[0] = total;
+    Tensor out = Tensor::Uninit(d.dtype(), shape);
+    int64_t off = 0;
+    if (d.dtype() == DType::kString) {
+      for (int64_t u : g)
+        for (int64_t k = p[2 * u] * w; k < p[2 * u + 1] * w; ++k) out.strings()[off++] = d.strings()[k];
+    } else {
+      // one memcpy per gathered ragged row
+      const size_t es = DTypeSize(d.dtype()) * w;
+      const char* src = static_cast<const char*>(d.raw());
+      char* dst = static_cast<char*>(out.raw());
+      for (int64_t u : g) {
+        const int64_t k = p[2 * u + 1] - p[2 * u];
+        if (k) memcpy(dst + off * es, src + p[2 * u] * es, k * es);
+        off += k;
+      }
+    }
+    ctx->Set(nd.Output(0), out);
   }
 };
 

@@ -253,6 +253,26 @@ class GetFeatureOp : public OpKernel {
                              (udf_feats.empty() || udf_feats.count(fname) || udf_feats.count(nd.attrs[f]));
       if (fi->type == kDense) {
         const Column<float>* c = edges ? g.EdgeDense(fi->idx) : g.NodeDense(fi->idx);
+        if (!apply_udf) {
+          // size pass, then one memcpy per row straight into the output tensor
+          std::vector<const float*> src(n, nullptr);
+          int64_t total = 0;
+          for (int64_t i = 0; i < n; ++i) {
+            int64_t k = 0;
+            if (c && rows[i] >= 0) c->Get(rows[i], &src[i], &k);
+            counts[i] = k;
+            total += k;
+          }
+          Tensor out = Tensor::Uninit(DType::kFloat, {total});
+          float* dst = out.data<float>();
+          for (int64_t i = 0; i < n; ++i) {
+            if (counts[i]) memcpy(dst, src[i], counts[i] * sizeof(float));
+            dst += counts[i];
+          }
+          ctx->Set(nd.Output(2 * f), MakeIdx(counts));
+          ctx->Set(nd.Output(2 * f + 1), out);
+          continue;
+        }
         std::vector<float> vals;
         for (int64_t i = 0; i < n; ++i) {
           const float* p = nullptr;

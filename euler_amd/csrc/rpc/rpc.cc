@@ -243,27 +243,47 @@ bool DecodeExecute(const std::string& p, DAGDef* dag, std::vector<std::pair<std:
   return true;
 }
 
-std::string EncodeReply(const Status& st, const std::vector<Tensor>& ts) {
-  BytesWriter w;
-  w.Write<int32_t>(static_cast<int32_t>(st.code()));
-  w.Write(st.message());
-  w.Write<uint32_t>(static_cast<uint32_t>(ts.size()));
-  for (auto& t : ts) t.Encode(&w);
-  return w.str();
+size_t ReplySize(const Status& st, const std::vector<Tensor>& ts) {
+  size_t n = 4 + 4 + st.message().size() + 4;
+  for (auto& t : ts) n += t.EncodedSize();
+  return n;
 }
 
-Status DecodeReply(const std::string& p, std::vector<Tensor>* ts) {
-  BytesReader r(p.data(), p.size());
+void EncodeReplyTo(BytesWriter* w, const Status& st, const std::vector<Tensor>& ts) {
+  w->Write<int32_t>(static_cast<int32_t>(st.code()));
+  w->Write(st.message());
+  w->Write<uint32_t>(static_cast<uint32_t>(ts.size()));
+  for (auto& t : ts) t.Encode(w);
+}
+
+std::string EncodeReply(const Status& st, const std::vector<Tensor>& ts) {
+  BytesWriter w;
+  w.str().reserve(ReplySize(st, ts));
+  EncodeReplyTo(&w, st, ts);
+  return std::move(w.str());
+}
+
+// false = malformed bytes (a transport failure); *app = the server's own status
+bool ParseReply(const char* data, size_t size, Status* app, std::vector<Tensor>* ts) {
+  BytesReader r(data, size);
   int32_t code;
   std::string msg;
   uint32_t n;
-  if (!r.Read(&code) || !r.Read(&msg) || !r.Read(&n)) return Status::RpcError("malformed reply");
-  if (code != 0) return Status(static_cast<Code>(code), msg);
+  if (!r.Read(&code) || !r.Read(&msg) || !r.Read(&n)) return false;
+  *app = code != 0 ? Status(static_cast<Code>(code), msg) : Status::OK();
+  if (code != 0) return true;
   ts->resize(n);
   for (auto& t : *ts)
-    if (!Tensor::Decode(&r, &t)) return Status::RpcError("malformed reply tensor");
-  return Status::OK();
+    if (!Tensor::Decode(&r, &t)) return false;
+  return true;
 }
+
+Status DecodeReply(const char* data, size_t size, std::vector<Tensor>* ts) {
+  Status app;
+  if (!ParseReply(data, size, &app, ts)) return Status::RpcError("malformed reply");
+  return app;
+}
+Status DecodeReply(const std::string& p, std::vector<Tensor>* ts) { return DecodeReply(p.data(), p.size(), ts); }
 
 double FaultRate() {
   static double r = [] {
@@ -1037,14 +1057,25 @@ void GraphServer::Dispatch(Loop* lp, const std::shared_ptr<Conn>& c) {
     c->busy = true;
     std::shared_ptr<Conn> keep = c;
     pool_->Schedule([this, lp, keep, payload = std::move(payload)] {
-      std::string reply = Handle(kExecute, payload);
+      Status st;
+      std::vector<Tensor> res;
+      std::string reply;
       uint32_t rk = kReply;
-      if (keep->shm && reply.size() >= kShmMin && reply.size() <= keep->shm_cap) {
-        // the request was consumed (copied out) before this task ran: the region is free
-        memcpy(keep->shm, reply.data(), reply.size());
-        EngineCounters::Get().shm_bytes.fetch_add(static_cast<int64_t>(reply.size()), std::memory_order_relaxed);
-        reply = EncodeLen(reply.size());
-        rk = kReply | kShmFlag;
+      {
+        ScopedMicros timing(&EngineCounters::Get().server_us);
+        HandleExecute(payload, &st, &res);
+        const size_t n = ReplySize(st, res);
+        if (keep->shm && n >= kShmMin && n <= keep->shm_cap) {
+          // the request was consumed (copied out) before this task ran: the region is
+          // free, and the reply is encoded straight into it
+          BytesWriter w(keep->shm, keep->shm_cap);
+          EncodeReplyTo(&w, st, res);
+          EngineCounters::Get().shm_bytes.fetch_add(static_cast<int64_t>(n), std::memory_order_relaxed);
+          reply = EncodeLen(n);
+          rk = kReply | kShmFlag;
+        } else {
+          reply = EncodeReply(st, res);
+        }
       }
       char hdr[16];
       const uint64_t rl = reply.size();
@@ -1110,18 +1141,26 @@ std::string GraphServer::Handle(uint32_t kind, const std::string& payload) {
   if (kind == kMeta)
     return EncodeReply(Status::OK(), {Tensor::Strings({ShardMeta::FromEnv(*env_, shard_idx_, shard_num_).ToString()})});
   if (kind != kExecute) return EncodeReply(Status::Unimplemented("unknown request kind"), {});
+  Status st;
+  std::vector<Tensor> res;
+  HandleExecute(payload, &st, &res);
+  return EncodeReply(st, res);
+}
+
+void GraphServer::HandleExecute(const std::string& payload, Status* st, std::vector<Tensor>* res) {
   DAGDef dag;
   std::vector<std::pair<std::string, Tensor>> inputs;
   std::vector<std::string> outputs;
-  if (!DecodeExecute(payload, &dag, &inputs, &outputs)) return EncodeReply(Status::RpcError("malformed execute request"), {});
-  std::vector<Tensor> res;
-  Status st;
-  try {
-    st = ExecuteDag(env_, dag, inputs, outputs, &res);
-  } catch (const std::exception& e) {
-    st = Status::Internal(e.what());
+  res->clear();
+  if (!DecodeExecute(payload, &dag, &inputs, &outputs)) {
+    *st = Status::RpcError("malformed execute request");
+    return;
   }
-  return EncodeReply(st, res);
+  try {
+    *st = ExecuteDag(env_, dag, inputs, outputs, res);
+  } catch (const std::exception& e) {
+    *st = Status::Internal(e.what());
+  }
 }
 
 // ============================================================================ RpcClients
@@ -1212,7 +1251,8 @@ void RpcClients::CloseChan(Chan* c) {
   c->fd = -1;
 }
 
-Status RpcClients::CallHost(Host* h, uint32_t kind, const std::string& payload, std::string* reply) {
+Status RpcClients::CallHost(Host* h, uint32_t kind, const std::string& payload, std::string* reply, size_t* in_bytes,
+                            std::vector<Tensor>* decoded, Status* app) {
   Chan c;
   {
     std::lock_guard<std::mutex> l(h->mu);
@@ -1233,15 +1273,24 @@ Status RpcClients::CallHost(Host* h, uint32_t kind, const std::string& payload, 
     ok = SendFrame(c.fd, kind, payload);
   }
   ok = ok && RecvFrame(c.fd, &rk, reply);
+  // a malformed reply is a transport failure; the server's own status goes to *app
   if (ok && rk == (kReply | kShmFlag) && c.shm) {
     const uint64_t n = DecodeLen(*reply);
     ok = n <= c.cap;
     if (ok) {
-      reply->assign(c.shm, n);
       EngineCounters::Get().shm_bytes.fetch_add(static_cast<int64_t>(n), std::memory_order_relaxed);
+      *in_bytes = n;
+      if (decoded) {  // decode straight out of the region: no staging copy
+        reply->clear();
+        ok = ParseReply(c.shm, n, app, decoded);
+      } else {
+        reply->assign(c.shm, n);
+      }
     }
   } else {
     ok = ok && rk == kReply;
+    *in_bytes = reply->size();
+    if (ok && decoded) ok = ParseReply(reply->data(), reply->size(), app, decoded);
   }
   if (!ok) {
     CloseChan(&c);
@@ -1253,7 +1302,8 @@ Status RpcClients::CallHost(Host* h, uint32_t kind, const std::string& payload, 
   return Status::OK();
 }
 
-Status RpcClients::Call(int shard, uint32_t kind, const std::string& payload, std::string* reply) {
+Status RpcClients::Call(int shard, uint32_t kind, const std::string& payload, std::string* reply,
+                        std::vector<Tensor>* decoded, Status* app) {
   if (shard < 0 || shard >= static_cast<int>(shards_.size()))
     return Status::Unavailable("no server for shard " + std::to_string(shard));
   const std::shared_ptr<const HostList> snap = std::atomic_load(&shards_[shard]);  // registry watch may swap it
@@ -1278,10 +1328,11 @@ Status RpcClients::Call(int shard, uint32_t kind, const std::string& payload, st
     if (FaultRate() > 0 && ThreadRng().Uniform() < FaultRate()) {
       last = Status::RpcError("injected fault");
     } else {
-      last = CallHost(h, kind, payload, reply);
+      size_t in_bytes = 0;
+      last = CallHost(h, kind, payload, reply, &in_bytes, decoded, app);
       if (last.ok()) {
         ctr.rpc_bytes_out.fetch_add(static_cast<int64_t>(payload.size()), std::memory_order_relaxed);
-        ctr.rpc_bytes_in.fetch_add(static_cast<int64_t>(reply->size()), std::memory_order_relaxed);
+        ctr.rpc_bytes_in.fetch_add(static_cast<int64_t>(in_bytes), std::memory_order_relaxed);
         return last;
       }
     }
@@ -1298,9 +1349,10 @@ void RpcClients::Execute(int shard, const DAGDef& dag, std::vector<std::pair<std
   auto payload = std::make_shared<std::string>(EncodeExecute(dag, inputs, outputs));
   pool_->Schedule([this, shard, payload, done] {
     std::string reply;
-    Status st = Call(shard, kExecute, *payload, &reply);
     std::vector<Tensor> res;
-    if (st.ok()) st = DecodeReply(reply, &res);
+    Status app;
+    Status st = Call(shard, kExecute, *payload, &reply, &res, &app);
+    if (st.ok()) st = app;
     done(st, std::move(res));
   });
 }

@@ -157,6 +157,7 @@ class GraphServer {
   void Flush(Loop* lp, const std::shared_ptr<Conn>& c);
   void Drop(Loop* lp, const std::shared_ptr<Conn>& c);
   std::string Handle(uint32_t kind, const std::string& payload);
+  void HandleExecute(const std::string& payload, Status* st, std::vector<Tensor>* res);
   EngineEnv* env_;
   int shard_idx_, shard_num_;
   ServerOptions opt_;
@@ -214,8 +215,12 @@ class RpcClients : public RemoteClients {
   static Chan OpenChan(const Endpoint& ep, int timeout_ms);
   static void CloseChan(Chan* c);
   typedef std::vector<std::shared_ptr<Host>> HostList;
-  Status Call(int shard, uint32_t kind, const std::string& payload, std::string* reply);
-  Status CallHost(Host* h, uint32_t kind, const std::string& payload, std::string* reply);
+  // transport status; with `decoded`, the reply is decoded in place (straight out of the
+  // shared region when it came that way) and the server's status lands in *app
+  Status Call(int shard, uint32_t kind, const std::string& payload, std::string* reply,
+              std::vector<Tensor>* decoded = nullptr, Status* app = nullptr);
+  Status CallHost(Host* h, uint32_t kind, const std::string& payload, std::string* reply, size_t* in_bytes,
+                  std::vector<Tensor>* decoded, Status* app);
   // per shard, swapped atomically by UpdateShard (callers work on a snapshot)
   std::vector<std::shared_ptr<const HostList>> shards_;
   std::vector<std::atomic<uint64_t>> rr_;

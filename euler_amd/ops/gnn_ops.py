@@ -179,7 +179,9 @@ class _GatConv(torch.autograd.Function):
     def forward(ctx, z2, a_src, a_dst, csr, H, C, slope):
         al, ar = hip().gat_att_fwd(z2, a_src, a_dst, H, C)
         indptr, col = csr.csr()
-        out, lse = hip().gat_fwd(indptr, col, csr.csr_order(), z2, al, ar, H, C, slope)
+        # al is recomputed from each gathered z row inside the edge kernels (a_src passed):
+        # one row fetch per edge instead of a row plus an al line
+        out, lse = hip().gat_fwd(indptr, col, csr.csr_order(), z2, al, ar, H, C, slope, a_src)
         ctx.csr, ctx.H, ctx.C, ctx.slope = csr, H, C, slope
         ctx.save_for_backward(z2, a_src, a_dst, al, ar, out, lse)
         return out
@@ -192,7 +194,7 @@ class _GatConv(torch.autograd.Function):
         cindptr, crow = csr.csc()
         dout = dout.to(z2.dtype).contiguous()
         dz, dal, dar = hip().gat_bwd(indptr, col, csr.csr_order(), cindptr, crow, csr.csc_order(), z2, al, ar,
-                                     ctx.H, ctx.C, ctx.slope, out, dout, lse)
+                                     ctx.H, ctx.C, ctx.slope, out, dout, lse, a_src)
         # dz += dal (x) a_src + dar (x) a_dst in place; attention-vector grads in the same pass
         da_src, da_dst = hip().gat_att_bwd_(z2, a_src, a_dst, ctx.H, ctx.C, dal, dar, dz)
         return dz, da_src, da_dst, None, None, None, None

@@ -132,6 +132,36 @@ def test_gat_conv_full_graph(cuda, H, C, dtype):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("H,C,dtype", [(8, 16, torch.bfloat16), (4, 8, torch.float32), (2, 64, torch.bfloat16)])
+def test_gat_recomputed_al_matches_gathered(cuda, H, C, dtype):
+    """The edge kernels given a_src recompute al = <z_j, a_src> from the gathered row; the
+    result must match the path that gathers the precomputed al (same partial order)."""
+    from euler_amd.ops._native import hip
+
+    torch.manual_seed(15)
+    N, E = 3000, 40000
+    ei = _graph(N, N, E, cuda, seed=16)
+    csr = G.EdgeCSR(ei, (N, N))
+    z = torch.randn(N, H * C, device=cuda).to(dtype)
+    a_s = torch.randn(H, C, device=cuda) * 0.3
+    a_d = torch.randn(H, C, device=cuda) * 0.3
+    al, ar = hip().gat_att_fwd(z, a_s, a_d, H, C)
+    indptr, col = csr.csr()
+    cindptr, crow = csr.csc()
+    o1, l1 = hip().gat_fwd(indptr, col, csr.csr_order(), z, al, ar, H, C, 0.2)
+    o2, l2 = hip().gat_fwd(indptr, col, csr.csr_order(), z, al, ar, H, C, 0.2, a_s)
+    torch.testing.assert_close(o2.float(), o1.float(), atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(l2, l1, atol=1e-5, rtol=1e-5)
+    dout = torch.randn_like(o1)
+    r1 = hip().gat_bwd(indptr, col, csr.csr_order(), cindptr, crow, csr.csc_order(), z, al, ar, H, C, 0.2, o1,
+                       dout, l1)
+    r2 = hip().gat_bwd(indptr, col, csr.csr_order(), cindptr, crow, csr.csc_order(), z, al, ar, H, C, 0.2, o1,
+                       dout, l1, a_s)
+    for a, b in zip(r2, r1):
+        torch.testing.assert_close(a.float(), b.float(), atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("bias", [False, True])
 def test_tall_linear_grads(cuda, bias):
     torch.manual_seed(14)

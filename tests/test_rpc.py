@@ -58,6 +58,19 @@ def test_remote_queries(cluster):
     ids, _, _ = ea.get_full_neighbor([1, 2, 3], ["0", "1"], "att gt 4")
     assert ids.to_dense().tolist() == [[4], [5], [4]]
     assert ea.get_graph_by_label(["3"]).to_dense().tolist() == [[3]]
+    # repeated, shuffled ids: the unique -> split -> merge -> gather chain is not the identity
+    import euler_amd._engine as E
+    E.set_op_profile(True)
+    E.reset_op_profile()
+    try:
+        f3 = ea.get_dense_feature([6, 1, 6, 3, 1, 2], ["f3"], [2])[0]
+        assert np.allclose(f3.numpy()[:, 0], [6.1, 1.1, 6.1, 3.1, 1.1, 2.1])
+        prof = E.op_profile()
+    finally:
+        E.set_op_profile(False)
+    for op in ("ID_UNIQUE", "ID_SPLIT", "REMOTE", "DATA_MERGE", "DATA_GATHER"):
+        assert prof[op][1] >= 1, (op, prof)
+    assert prof["REMOTE"][1] == 2  # one call per shard
 
 
 def test_same_host_shared_memory_payloads(tmp_path):
