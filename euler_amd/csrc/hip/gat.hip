@@ -26,7 +26,8 @@
 // degree, longest first), so the 64/lp rows sharing a wave have similar lengths (a wave
 // runs as long as its longest row) and the heaviest rows start first.  The next batch's
 // column indices are loaded before the current batch's rows are consumed, so each batch
-// costs one memory round trip instead of two.
+// costs one memory round trip instead of two.  al of a neighbour is recomputed from its
+// gathered row when a_src is given (one row fetch per edge instead of row + al line).
 #include "hip/common.h"
 #include "hip/launchers.h"
 
@@ -73,8 +74,18 @@ __device__ __forceinline__ float gat_group_sum(float v, int g) {
 
 __device__ __forceinline__ float lrelu(float z, float slope) { return z > 0.f ? z : z * slope; }
 
-constexpr int GAT_UF = 8;  // neighbour rows in flight per lane, forward
-constexpr int GAT_UB = 4;  // backward (more live registers per row)
+#ifndef GAT_FWD_U
+#define GAT_FWD_U 2
+#endif
+#ifndef GAT_BWD_U
+#define GAT_BWD_U 2
+#endif
+// neighbour rows in flight per lane group.  Measured on the ogbn-products-shaped graph
+// (tools/gat_kernels.py, profiles/r2_gat/): 2 beats 4/8/16 — the gathers are latency-bound
+// and fewer live rows per lane buys more resident waves than the unroll buys in-flight loads
+// (fwd 5.3 ms at U=2 vs 8.4 ms at U=8; bwd 13.1 vs 15.9 ms).
+constexpr int GAT_UF = GAT_FWD_U;
+constexpr int GAT_UB = GAT_BWD_U;
 
 // row of this lane group, its lane-in-row and whether the row exists
 struct GatLane {

@@ -86,6 +86,21 @@ for st in "${S[@]}"; do
       run bench_kg 600 python -u benchmarks/bench_kg.py ;;
     learn_gat)
       run bench_gat 900 python -u benchmarks/bench_gat.py ;;
+    gat_variants)
+      # GAT_VARIANTS="-DGAT_FWD_U=4|-DGAT_FWD_U=8": rebuild gat.hip per flag set, time the edge kernels
+      IFS='|' read -ra VL <<< "${GAT_VARIANTS:-}"
+      i=0
+      for v in "${VL[@]}"; do
+        i=$((i+1))
+        touch euler_amd/csrc/hip/gat.hip
+        EULER_AMD_HIP_FLAGS="$v" python -m euler_amd._build > "$OUT/build_gat_variant$i.log" 2>&1 || exit 4
+        EULER_AMD_HIP_FLAGS="$v" run "gat_kernels_variant$i" 300 python -u tools/gat_kernels.py || exit $?
+      done ;;
+    gat_time)
+      run bench_gat_time 600 python -u benchmarks/bench_gat.py --eval-epochs 0 ;;
+    gat_prof)
+      run gat_prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/gat_prof" -o run --output-format csv -- \
+          python3 benchmarks/bench_gat.py --epochs 5 --warmup 2 --eval-epochs 0 ;;
     learn_deepwalk)
       run bench_deepwalk 900 python -u benchmarks/bench_deepwalk.py ;;
     deepwalk_modes)
