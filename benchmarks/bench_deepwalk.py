@@ -90,6 +90,8 @@ def main(argv=None):
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--force-dist", action="store_true",
                    help="process group + all-to-all path even with one rank (validates the N>1 path)")
+    p.add_argument("--wire-dtype", choices=["bf16", "fp32"], default="bf16",
+                   help="dtype of the row / gradient all-to-alls (the table and its update stay fp32)")
     p.add_argument("--mode", choices=["graph", "static", "dynamic"], default="graph",
                    help="graph: fixed-capacity step captured in one hipGraph and replayed; static: the same "
                         "step eager; dynamic: exact-size step (host-read unique counts / all-to-all splits)")
@@ -125,7 +127,8 @@ def main(argv=None):
     g = DeviceGraph.synthetic(args.num_nodes, args.avg_degree, args.max_degree, seed=args.seed, device=dev)
     g.manual_seed(args.seed * 7919 + rank)
     tr = DeepWalkTrainer(g, args.num_nodes, args.dim, args.walk_len, 1, 1, args.num_negs, args.batch, args.lr,
-                         args.optimizer, seed=args.seed, force_comm=args.force_dist, static=args.mode != "dynamic")
+                         args.optimizer, seed=args.seed, force_comm=args.force_dist, static=args.mode != "dynamic",
+                         wire_dtype=args.wire_dtype)
     torch.cuda.synchronize()
     if rank == 0:
         gib = tr.table.nbytes() / 2 ** 30
@@ -176,6 +179,7 @@ def main(argv=None):
             "dtype": "fp32",
             "data": "synthetic (power-law random graph, random-init tables)",
             "config": {"model": f"DeepWalk (walk_len 3, window 1/1, 5 negs, row-sparse {args.optimizer})",
+                       "exchange_dtype": args.wire_dtype,
                        "num_nodes": args.num_nodes, "dim": args.dim, "walks_per_gpu": args.batch,
                        "pairs_per_gpu_step": pairs_per_step, "parallelism": f"dp{world}+sharded-emb",
                        "all_to_all": table_comm, "step_mode": args.mode,

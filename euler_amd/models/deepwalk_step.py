@@ -54,7 +54,8 @@ def _pair_positions(walk_len, left, right):
 
 class DeepWalkTrainer:
     def __init__(self, graph, num_nodes, dim=128, walk_len=3, left_win_size=1, right_win_size=1, num_negs=5,
-                 batch_size=1024, lr=0.01, optimizer="adam", group=None, seed=0, force_comm=False, static=False):
+                 batch_size=1024, lr=0.01, optimizer="adam", group=None, seed=0, force_comm=False, static=False,
+                 wire_dtype="bf16"):
         self.graph = graph
         self.num_nodes = int(num_nodes)
         self.pad = self.num_nodes  # rows: num_nodes + 1 (pad row like the reference's max_id + 1)
@@ -65,7 +66,8 @@ class DeepWalkTrainer:
         # context row is row off + i.  A step then needs one id exchange, one row exchange,
         # one gradient exchange and one host sync (world > 1) instead of two of each.
         self.off = self.num_nodes + 1
-        self.table = ShardedTable(2 * self.off, dim, dev, group, optimizer, lr, seed=seed, force_comm=force_comm)
+        self.table = ShardedTable(2 * self.off, dim, dev, group, optimizer, lr, seed=seed, force_comm=force_comm,
+                                  wire_dtype=wire_dtype)
         pi, pj = _pair_positions(walk_len, left_win_size, right_win_size)
         self.pi, self.pj = pi.to(dev), pj.to(dev)
         self.pairs_per_walk = int(pi.numel())

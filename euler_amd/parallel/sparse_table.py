@@ -27,6 +27,10 @@ hashed ids (``capacity``); an id that would not fit raises the device-side ``ove
 flag (``check_overflow`` reads it, e.g. once per log interval) instead of being silently
 dropped unnoticed.  Expected traffic per step and rank with n ids of D fp32: ids
 8 W C bytes, rows and gradients 2 x 4 D W C bytes, ~3 x n / W of it leaving the rank.
+
+``wire_dtype="bf16"`` moves the row and gradient exchanges (both forms) as bf16: half the
+bytes on xGMI for the two large all-to-alls; the table, its optimizer slots and the
+update stay fp32 (rows are widened on arrival, gradients rounded once before sending).
 """
 from __future__ import annotations
 
@@ -64,8 +68,11 @@ class StaticHandle:
 
 class ShardedTable:
     def __init__(self, num_rows, dim, device, group=None, optimizer="adam", lr=0.01, init_std=0.1, seed=0,
-                 beta1=0.9, beta2=0.999, eps=1e-8, force_comm=False):
+                 beta1=0.9, beta2=0.999, eps=1e-8, force_comm=False, wire_dtype="fp32"):
         self.num_rows, self.dim = int(num_rows), int(dim)
+        if wire_dtype not in ("fp32", "bf16"):
+            raise ValueError("wire_dtype must be fp32 or bf16")
+        self.wire = torch.bfloat16 if wire_dtype == "bf16" else torch.float32
         self.group = group
         init = dist.is_available() and dist.is_initialized()
         dist_on = init and dist.get_world_size(group) > 1
@@ -127,9 +134,7 @@ class ShardedTable:
         recv = torch.empty(trash, dtype=torch.long, device=ids.device)
         dist.all_to_all_single(recv, send[:trash], group=self.group)
         local = torch.where(recv >= 0, torch.div(recv, W, rounding_mode="floor"), torch.full_like(recv, -1))
-        rows = self._gather(local)
-        out = torch.empty_like(rows)
-        dist.all_to_all_single(out, rows, group=self.group)
+        out = self._a2a_rows(self._gather(local))
         return out, StaticHandle(pos, local)
 
     def apply_static(self, handle: StaticHandle, grad_rows: torch.Tensor):
@@ -138,9 +143,7 @@ class ShardedTable:
         g = grad_rows.float().contiguous()
         rows = handle.local
         if self.comm:
-            recv_g = torch.empty_like(g)
-            dist.all_to_all_single(recv_g, g, group=self.group)
-            g = recv_g
+            g = self._a2a_rows(g)
             if self.world > 1:
                 # several ranks may have asked for the same row: merge (the -1 bucket of
                 # empty slots collects their rows and is skipped by the update)
@@ -186,9 +189,7 @@ class ShardedTable:
         recv_ids = torch.empty(sum(recv), dtype=ids.dtype, device=ids.device)
         dist.all_to_all_single(recv_ids, ids[order].contiguous(), recv, send, group=self.group)
         local = torch.div(recv_ids, W, rounding_mode="floor")
-        rows = self._gather(local)
-        out_sorted = torch.empty(ids.numel(), self.dim, dtype=rows.dtype, device=rows.device)
-        dist.all_to_all_single(out_sorted, rows, send, recv, group=self.group)
+        out_sorted = self._a2a_rows(self._gather(local), send, recv)
         if sorted_out:
             rank = torch.empty_like(order)
             rank[order] = torch.arange(order.numel(), device=order.device)
@@ -196,6 +197,14 @@ class ShardedTable:
         out = torch.empty_like(out_sorted)
         out[order] = out_sorted
         return out, LookupHandle(order, send, recv, local, ids.numel())
+
+    def _a2a_rows(self, x, out_splits=None, in_splits=None):
+        """all-to-all of [*, D] rows in the wire dtype; returns fp32 rows"""
+        xw = x.to(self.wire).contiguous()
+        n = xw.shape[0] if out_splits is None else sum(out_splits)
+        out = torch.empty(n, self.dim, dtype=self.wire, device=xw.device)
+        dist.all_to_all_single(out, xw, out_splits, in_splits, group=self.group)
+        return out.float()
 
     def _gather(self, local):
         if use_hip(self.weight, local):
@@ -210,9 +219,7 @@ class ShardedTable:
         g = grad_rows.float().contiguous()
         if self.comm:
             g_sorted = g if sorted_in else g[handle.order].contiguous()
-            recv_g = torch.empty(sum(handle.recv), self.dim, dtype=g.dtype, device=g.device)
-            dist.all_to_all_single(recv_g, g_sorted, handle.recv, handle.send, group=self.group)
-            rows, g = handle.local_rows, recv_g
+            rows, g = handle.local_rows, self._a2a_rows(g_sorted, handle.recv, handle.send)
             # several ranks may have asked for the same row: merge before the update
             # (one rank's ids are distinct already)
             rows_u, inv = unique_first(rows) if self.world > 1 else (rows, None)
