@@ -84,8 +84,12 @@ __device__ __forceinline__ float lrelu(float z, float slope) { return z > 0.f ? 
 // (tools/gat_kernels.py, profiles/r2_gat/): 2 beats 4/8/16 — the gathers are latency-bound
 // and fewer live rows per lane buys more resident waves than the unroll buys in-flight loads
 // (fwd 5.3 ms at U=2 vs 8.4 ms at U=8; bwd 13.1 vs 15.9 ms).
+#ifndef GAT_BWD_SRC_U
+#define GAT_BWD_SRC_U GAT_BWD_U
+#endif
 constexpr int GAT_UF = GAT_FWD_U;
 constexpr int GAT_UB = GAT_BWD_U;
+constexpr int GAT_UBS = GAT_BWD_SRC_U;  // source (CSC) pass of the backward
 
 // row of this lane group, its lane-in-row and whether the row exists
 struct GatLane {
@@ -308,7 +312,7 @@ __global__ __launch_bounds__(256) void gat_bwd_src_kernel(
     int64_t N, const T* __restrict__ h, const float* __restrict__ al, int H, int C, float slope, int lp,
     const T* __restrict__ dout, const float4_t* __restrict__ stat, T* __restrict__ dh, float* __restrict__ dal) {
   constexpr int V = GV<T>::N;
-  constexpr int U = GAT_UB;
+  constexpr int U = GAT_UBS;
   const int HC = H * C, nch = HC / V, g = C / V;
   const GatLane L = gat_lane(lp, N, order);
   bool ok[MAXCH];
