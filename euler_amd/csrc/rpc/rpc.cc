@@ -1519,7 +1519,10 @@ Status QueryProxy::Init(const std::map<std::string, std::string>& config) {
     // runs on its own partition, with GP_* merges chaining the per-hop row orders.  Its
     // multi-hop results are partition-local approximations; euler_amd serves sharded
     // graphs with exact distribute mode, whose REMOTE fusion already costs one RPC per
-    // shard per hop.  Refuse instead of silently running distribute semantics.
+    // shard per hop.  Refuse instead of silently running distribute semantics.  (The
+    // reference's own rule table routes API_GET_NODE / API_SAMPLE_NB / API_GET_P ids
+    // through GP_BROAD_CAST_SPLIT, optimizer.h:56-61, a kernel nothing in
+    // euler/core/kernels registers, so those plans cannot execute there either.)
     return Status::Unimplemented(
         "graph_partition mode is not supported: use mode=remote (distribute compiler with per-hop REMOTE "
         "fusion; GP_* merge kernels are available as single ops via run_op)");
