@@ -55,8 +55,10 @@ def link_prediction_eval(args, dev):
     indptr[1:] = torch.cumsum(torch.bincount(s, minlength=N), 0)
     g = DeviceGraph.from_csr(indptr.numpy(), d.int().numpy(), np.ones(d.numel(), np.float32), seed=args.seed,
                              device=dev)
+    # same exchange path as the timed run (--force-dist / --mode / --wire-dtype)
     tr = DeepWalkTrainer(g, N, args.dim, args.walk_len, 1, 1, args.num_negs, args.batch, args.eval_lr, "adam",
-                         seed=args.seed)
+                         seed=args.seed, force_comm=args.force_dist, static=args.mode != "dynamic",
+                         wire_dtype=args.wire_dtype)
     pu, pv = src[hold].to(dev), dst[hold].to(dev)
     nu = torch.randint(0, N, (n_hold,), generator=gen).to(dev)
     nv = torch.randint(0, N, (n_hold,), generator=gen).to(dev)

@@ -96,11 +96,18 @@ for st in "${S[@]}"; do
         EULER_AMD_HIP_FLAGS="$v" python -m euler_amd._build > "$OUT/build_gat_variant$i.log" 2>&1 || exit 4
         EULER_AMD_HIP_FLAGS="$v" run "gat_kernels_variant$i" 300 python -u tools/gat_kernels.py || exit $?
       done ;;
+    kg_prof)
+      run kg_prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/kg_prof" -o run --output-format csv -- \
+          python3 benchmarks/bench_kg.py --steps 50 --warmup 5 --eval-after 0 ;;
     gat_time)
       run bench_gat_time 600 python -u benchmarks/bench_gat.py --eval-epochs 0 ;;
     gat_prof)
       run gat_prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/gat_prof" -o run --output-format csv -- \
           python3 benchmarks/bench_gat.py --epochs 5 --warmup 2 --eval-epochs 0 ;;
+    learn_deepwalk_dist)
+      # learning evidence through the sharded exchange (bf16 rows/grads on the wire)
+      run bench_deepwalk_dist 900 python -u -m torch.distributed.run --nnodes 1 --nproc-per-node 1 \
+        --master-addr 127.0.0.1 --master-port 29535 benchmarks/bench_deepwalk.py --mode static --force-dist ;;
     learn_deepwalk)
       run bench_deepwalk 900 python -u benchmarks/bench_deepwalk.py ;;
     deepwalk_modes)
