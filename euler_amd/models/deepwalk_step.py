@@ -153,7 +153,10 @@ class DeepWalkTrainer:
             coef, loss_rows = gnn_ops.sgns_fwd_idx(rows, None, tinv, rows, None, cinv, K, gscale)
             ptr_t, lst_t = gnn_ops.occ_csr(tinv, n)
             ptr_c, lst_c = gnn_ops.occ_csr(cinv, n)
-            g = torch.zeros_like(rows)
+            # every occupied slot is written by exactly one side (target and context ids
+            # live in different table halves); empty slots (local row -1) are skipped by the
+            # update, so no 4*D*W*C-byte zero fill per step
+            g = torch.empty_like(rows)
             gnn_ops.sgns_grad(0, ptr_t, lst_t, coef, K, rows, None, cinv, inv_self=tinv, out=g)
             gnn_ops.sgns_grad(1, ptr_c, lst_c, coef, K, rows, None, tinv, inv_self=cinv, out=g)
             tab.apply_static(h, g)
