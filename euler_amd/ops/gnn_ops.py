@@ -329,8 +329,9 @@ class RelationTiles:
     """Edges grouped by relation, for the relation-grouped MFMA GEMM (rgcn.hip).
 
     Arrays are over the relation-sorted order of the valid edges: ``src``/``dst``
-    (int32), ``scale`` (1 / in-degree for mean aggregation, else 1), ``eid`` (arange:
-    the message row of each edge), tiles ``(rel, start, len)`` of <= 64 edges of one
+    (int32), ``scale`` (1 / in-degree for mean aggregation, else 1), ``eid`` (arange),
+    ``slot_dst`` / ``slot_src`` (the message row of each edge in the forward / backward
+    GEMM: its position in the destination / source CSR), tiles ``(rel, start, len)`` of <= 64 edges of one
     relation for the message GEMMs, chunks ``(rel, start, len)`` of <= 1024 edges of one
     relation for the weight gradient, and the destination / source CSRs over the
     messages (``SegmentIndex``) for the deterministic per-node sums.  Built once per
@@ -363,6 +364,18 @@ class RelationTiles:
         self.chunk_solo = (counts[self.chunk_rel.long()] <= chunk).to(torch.int32).contiguous()
         self.dst_seg = SegmentIndex(self.dst.long(), n_dst)
         self.src_seg = SegmentIndex(self.src.long(), n_src)
+        # message rows in destination-CSR order (forward) / source-CSR order (backward):
+        # the GEMM epilogue scatters each 16-byte-vector message row to its edge's slot, so
+        # the per-node sums stream the messages sequentially (no perm indirection, no
+        # random row reads)
+        self.slot_dst = self._slots(self.dst_seg.perm, dev)
+        self.slot_src = self._slots(self.src_seg.perm, dev)
+
+    @staticmethod
+    def _slots(perm, dev):
+        slot = torch.empty(perm.numel(), dtype=torch.int32, device=dev)
+        slot[perm] = torch.arange(perm.numel(), dtype=torch.int32, device=dev)
+        return slot
 
     @staticmethod
     def _cut(counts, size, dev):
@@ -420,10 +433,9 @@ class _RelationTransform(torch.autograd.Function):
         wb = _pad_bf16(weight, (0, Kp - K, 0, Np - N))
         msg = torch.empty(tiles.num_edges, Np, device=x.device, dtype=torch.bfloat16)
         tr, ts, tl = tiles.tiles()
-        hip().rel_gemm(xb, tiles.src, tr, ts, tl, wb, None, tiles.eid, 0, msg)
+        hip().rel_gemm(xb, tiles.src, tr, ts, tl, wb, None, tiles.slot_dst, 0, msg)
         op = 1 if tiles.aggr == "mean" else 0
-        seg = tiles.dst_seg
-        out = hip().segment_reduce(msg, seg.indptr, seg.perm, op, 0.0)[0]
+        out = hip().segment_reduce(msg, tiles.dst_seg.indptr, None, op, 0.0)[0]
         ctx.tiles, ctx.dims = tiles, (R, N, K, Kp, Np, x.shape[0])
         ctx.x_dtype, ctx.w_dtype = x.dtype, weight.dtype
         ctx.save_for_backward(xb, wb)
@@ -440,9 +452,8 @@ class _RelationTransform(torch.autograd.Function):
             wt = wb.transpose(1, 2).contiguous()  # [R, Kp, Np]
             msgx = torch.empty(tiles.num_edges, Kp, device=dout.device, dtype=torch.bfloat16)
             tr, ts, tl = tiles.tiles()
-            hip().rel_gemm(gb, tiles.dst, tr, ts, tl, wt, tiles.scale, tiles.eid, 0, msgx)
-            seg = tiles.src_seg
-            dxp = hip().segment_reduce(msgx, seg.indptr, seg.perm, 0, 0.0)[0]
+            hip().rel_gemm(gb, tiles.dst, tr, ts, tl, wt, tiles.scale, tiles.slot_src, 0, msgx)
+            dxp = hip().segment_reduce(msgx, tiles.src_seg.indptr, None, 0, 0.0)[0]
             dx = dxp[:, :K].to(ctx.x_dtype)
         if ctx.needs_input_grad[1]:
             dwp = torch.zeros(R, Np, Kp, device=dout.device, dtype=torch.float32)
