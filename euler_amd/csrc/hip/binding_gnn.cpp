@@ -168,7 +168,7 @@ void tiles_check(const torch::Tensor& trel, const torch::Tensor& tstart, const t
 }
 
 void rel_gemm(torch::Tensor A, torch::Tensor a_idx, torch::Tensor trel, torch::Tensor tstart, torch::Tensor tlen,
-              torch::Tensor B, c10::optional<torch::Tensor> scale, torch::Tensor o_idx, int64_t mode, torch::Tensor Y) {
+              torch::Tensor B, c10::optional<torch::Tensor> scale, torch::Tensor o_idx, int64_t mode, int64_t tm, torch::Tensor Y) {
   typed(A, torch::kBFloat16, "A");
   typed(B, torch::kBFloat16, "B");
   typed(a_idx, torch::kInt32, "a_idx");
@@ -177,9 +177,10 @@ void rel_gemm(torch::Tensor A, torch::Tensor a_idx, torch::Tensor trel, torch::T
   TORCH_CHECK(A.dim() == 2 && B.dim() == 3 && B.size(2) == A.size(1), "A [*, K], B [R, N, K]");
   const int64_t K = A.size(1), N = B.size(1);
   TORCH_CHECK(K % 32 == 0 && K <= 1024 && N % 16 == 0, "rel_gemm needs K % 32 == 0, K <= 1024, N % 16 == 0");
-  TORCH_CHECK(eh_rel_gemm_lds(static_cast<int>(K), static_cast<int>(N), static_cast<int>(mode)) <= 160 * 1024,
+  TORCH_CHECK(eh_rel_gemm_lds(static_cast<int>(K), static_cast<int>(N), static_cast<int>(mode), static_cast<int>(tm)) <= 160 * 1024 - 2048,
               "rel_gemm: K + N too large for the LDS tiles");
   TORCH_CHECK(a_idx.numel() == o_idx.numel(), "a_idx / o_idx must cover the same edges");
+  TORCH_CHECK(tm % 16 == 0 && tm >= 16 && tm <= eh_rel_gemm_tile(), "rel_gemm: tile rows tm must be a multiple of 16 in [16, rel_gemm_tile]");
   if (scale.has_value()) {
     typed(*scale, torch::kFloat32, "scale");
     TORCH_CHECK(scale->numel() == a_idx.numel(), "scale must be per edge");
@@ -191,7 +192,7 @@ void rel_gemm(torch::Tensor A, torch::Tensor a_idx, torch::Tensor trel, torch::T
   ok(eh_rel_gemm(A.data_ptr(), static_cast<int>(K), a_idx.data_ptr<int32_t>(), trel.data_ptr<int32_t>(),
                  tstart.data_ptr<int32_t>(), tlen.data_ptr<int32_t>(), static_cast<int>(trel.numel()), B.data_ptr(),
                  static_cast<int>(N), scale.has_value() ? scale->data_ptr<float>() : nullptr,
-                 o_idx.data_ptr<int32_t>(), static_cast<int>(mode), Y.data_ptr(), stream()),
+                 o_idx.data_ptr<int32_t>(), static_cast<int>(mode), static_cast<int>(tm), Y.data_ptr(), stream()),
      "rel_gemm");
 }
 
@@ -531,6 +532,7 @@ void register_gnn_ops(pybind11::module& m) {
   m.def("rel_gemm", &rel_gemm);
   m.def("rel_gemm_dw", &rel_gemm_dw);
   m.attr("rel_gemm_dw_chunk") = eh_rel_gemm_dw_chunk();
+  m.attr("rel_gemm_tile") = eh_rel_gemm_tile();
   m.def("sgns_fwd", &sgns_fwd);
   m.def("sgns_bwd", &sgns_bwd);
   m.def("sgns_fwd_idx", &sgns_fwd_idx);

@@ -102,11 +102,12 @@ hipError_t eh_gat_bwd(const int64_t* indptr, const int32_t* col, const int32_t* 
                       const float* a_src, hipStream_t s);
 
 // rgcn.hip (K6: relation-grouped MFMA GEMM)
-size_t eh_rel_gemm_lds(int K, int N, int mode);
+size_t eh_rel_gemm_lds(int K, int N, int mode, int tm);
+int eh_rel_gemm_tile();      // edges per message-GEMM tile (tiles: <= this many edges of one relation)
 int eh_rel_gemm_dw_chunk();  // edges per dW chunk (chunks: <= this many edges of one relation)
 hipError_t eh_rel_gemm(const void* A, int K, const int32_t* a_idx, const int32_t* trel, const int32_t* tstart,
                        const int32_t* tlen, int n_tiles, const void* B, int N, const float* scale,
-                       const int32_t* o_idx, int mode, void* Y, hipStream_t s);
+                       const int32_t* o_idx, int mode, int tm, void* Y, hipStream_t s);
 hipError_t eh_rel_gemm_dw(const void* G, int N, const int32_t* g_idx, const void* X, int K, const int32_t* x_idx,
                           const float* scale, const int32_t* crel, const int32_t* cstart, const int32_t* clen,
                           const int32_t* csolo, int n_chunks, float* dW, hipStream_t s);

@@ -29,20 +29,33 @@ __device__ __forceinline__ float4_t rg_mfma(uint4_t a, uint4_t b, float4_t c) {
 
 constexpr int RG_BM = 64;  // edges per tile
 
+#ifndef RG_TM
+#define RG_TM 128  // max edges per message-GEMM tile (tm): one W_rel read serves up to tm edges;
+                   // gnn_ops picks tm = 64 (sweep: profiles/r2_final/sweeps/rel_gemm_tile.txt)
+#endif
+constexpr int RG_TMF = RG_TM / 16;
+
 __global__ __launch_bounds__(256) void rel_gemm_kernel(const bf16_t* __restrict__ A, int K,
                                                        const int32_t* __restrict__ a_idx,
                                                        const int32_t* __restrict__ trel,
                                                        const int32_t* __restrict__ tstart,
                                                        const int32_t* __restrict__ tlen, const bf16_t* __restrict__ B,
                                                        int N, const float* __restrict__ scale,
-                                                       const int32_t* __restrict__ o_idx, int mode, void* Y) {
+                                                       const int32_t* __restrict__ o_idx, int mode, int tm, void* Y) {
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  __shared__ int32_t orow_s[RG_TM];
+  __shared__ float osc_s[RG_TM];
   const int t = xcd_remap(blockIdx.x, gridDim.x);
-  const int r = trel[t], e0 = tstart[t], ne = tlen[t];
+  const int r = trel[t], e0 = tstart[t], ne = min(tlen[t], tm);  // tm bounds the LDS rows
   const int ldk = K + 8;
   const int cpr = K >> 3;
+  // epilogue bookkeeping per tile row: output row and scale
+  for (int row = threadIdx.x; row < RG_TM; row += 256) {
+    orow_s[row] = row < ne ? o_idx[e0 + row] : -1;
+    osc_s[row] = (row < ne && scale) ? scale[e0 + row] : 1.f;
+  }
   // prologue: gather the tile's A rows (zero rows past the tile / for padding ids)
-  for (int it = threadIdx.x; it < RG_BM * cpr; it += 256) {
+  for (int it = threadIdx.x; it < tm * cpr; it += 256) {
     const int row = it / cpr, c = it - row * cpr;
     uint4_t v = {0u, 0u, 0u, 0u};
     if (row < ne) {
@@ -56,51 +69,46 @@ __global__ __launch_bounds__(256) void rel_gemm_kernel(const bf16_t* __restrict_
   const int lr = lane & 15, lk = (lane >> 4) * 8;
   const bf16_t* __restrict__ Br = B + static_cast<int64_t>(r) * N * K;
   const int ldn = N + 8;
-  bf16_t* otile = lds + RG_BM * ldk;  // mode 0 output tile [64][N + 8]
-  // epilogue bookkeeping for the 16 rows this lane owns in C (row = m*16 + (lane>>4)*4 + j)
-  int64_t orow[4][4];
-  float osc[4][4];
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int row = m * 16 + (lane >> 4) * 4 + j;
-      orow[m][j] = row < ne ? static_cast<int64_t>(o_idx[e0 + row]) : -1;
-      osc[m][j] = (row < ne && scale) ? scale[e0 + row] : 1.f;
-    }
+  bf16_t* otile = lds + tm * ldk;  // mode 0 output tile [tm][N + 8]
+  // fragments past the tile's last edge multiply zero rows: skip them (uniform per block)
+  const int mf = (ne + 15) >> 4;
   for (int n0 = wave * 16; n0 < N; n0 += 64) {
-    float4_t acc[4];
+    float4_t acc[RG_TMF];
 #pragma unroll
-    for (int m = 0; m < 4; ++m) acc[m] = float4_t{0.f, 0.f, 0.f, 0.f};
+    for (int m = 0; m < RG_TMF; ++m) acc[m] = float4_t{0.f, 0.f, 0.f, 0.f};
     uint4_t b = *reinterpret_cast<const uint4_t*>(Br + static_cast<int64_t>(n0 + lr) * K + lk);
     for (int k0 = 0; k0 < K; k0 += 32) {
       const bool more = k0 + 32 < K;
       const uint4_t bn = more ? *reinterpret_cast<const uint4_t*>(Br + static_cast<int64_t>(n0 + lr) * K + k0 + 32 + lk)
                               : uint4_t{0u, 0u, 0u, 0u};
-      uint4_t a[4];
 #pragma unroll
-      for (int m = 0; m < 4; ++m) a[m] = *reinterpret_cast<const uint4_t*>(lds + (m * 16 + lr) * ldk + k0 + lk);
-#pragma unroll
-      for (int m = 0; m < 4; ++m) acc[m] = rg_mfma(a[m], b, acc[m]);
+      for (int m = 0; m < RG_TMF; ++m) {
+        if (m < mf) {
+          const uint4_t a = *reinterpret_cast<const uint4_t*>(lds + (m * 16 + lr) * ldk + k0 + lk);
+          acc[m] = rg_mfma(a, b, acc[m]);
+        }
+      }
       b = bn;
     }
     const int col = n0 + lr;
     if (mode == 0) {
       // stage the bf16 tile in LDS; rows leave as 16-byte stores below
 #pragma unroll
-      for (int m = 0; m < 4; ++m)
+      for (int m = 0; m < RG_TMF; ++m)
+        if (m < mf)  // rows < tm: inside the tile's LDS rows
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int row = m * 16 + (lane >> 4) * 4 + j;
+            otile[row * ldn + col] = f2bf(acc[m][j] * osc_s[row]);
+          }
+    } else {
+#pragma unroll
+      for (int m = 0; m < RG_TMF; ++m)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int row = m * 16 + (lane >> 4) * 4 + j;
-          otile[row * ldn + col] = f2bf(acc[m][j] * osc[m][j]);
-        }
-    } else {
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int64_t o = orow[m][j];
-          if (o >= 0) atomicAdd(static_cast<float*>(Y) + o * N + col, acc[m][j] * osc[m][j]);
+          const int64_t o = orow_s[row];
+          if (o >= 0) atomicAdd(static_cast<float*>(Y) + o * N + col, acc[m][j] * osc_s[row]);
         }
     }
   }
@@ -109,7 +117,7 @@ __global__ __launch_bounds__(256) void rel_gemm_kernel(const bf16_t* __restrict_
     const int cpn = N >> 3;
     for (int it = threadIdx.x; it < ne * cpn; it += 256) {
       const int row = it / cpn, c = it - row * cpn;
-      const int64_t o = o_idx[e0 + row];
+      const int64_t o = orow_s[row];
       if (o >= 0)
         *reinterpret_cast<uint4_t*>(static_cast<bf16_t*>(Y) + o * N + c * 8) =
             *reinterpret_cast<const uint4_t*>(otile + row * ldn + c * 8);
@@ -250,19 +258,24 @@ using namespace euler_hip;
 
 extern "C" {
 
-size_t eh_rel_gemm_lds(int K, int N, int mode) {
-  return static_cast<size_t>(RG_BM) * ((K + 8) + (mode == 0 ? N + 8 : 0)) * sizeof(bf16_t);
+size_t eh_rel_gemm_lds(int K, int N, int mode, int tm) {
+  return static_cast<size_t>(tm) * ((K + 8) + (mode == 0 ? N + 8 : 0)) * sizeof(bf16_t);
 }
+
+int eh_rel_gemm_tile() { return RG_TM; }
 
 hipError_t eh_rel_gemm(const void* A, int K, const int32_t* a_idx, const int32_t* trel, const int32_t* tstart,
                        const int32_t* tlen, int n_tiles, const void* B, int N, const float* scale,
-                       const int32_t* o_idx, int mode, void* Y, hipStream_t s) {
+                       const int32_t* o_idx, int mode, int tm, void* Y, hipStream_t s) {
   if (n_tiles == 0) return hipSuccess;
-  if (K % 32 != 0 || N % 16 != 0 || K > 1024 || N <= 0) return hipErrorInvalidValue;
-  const size_t lds = eh_rel_gemm_lds(K, N, mode);
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (K % 32 != 0 || N % 16 != 0 || K > 1024 || N <= 0 || tm % 16 != 0 || tm < 16 || tm > RG_TM)
+    return hipErrorInvalidValue;
+  const size_t lds = eh_rel_gemm_lds(K, N, mode, tm);
+  if (lds > 160 * 1024 - 2048) return hipErrorInvalidValue;
+  EULER_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(rel_gemm_kernel),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
   hipLaunchKernelGGL(rel_gemm_kernel, dim3(n_tiles), dim3(256), lds, s, static_cast<const bf16_t*>(A), K, a_idx, trel,
-                     tstart, tlen, static_cast<const bf16_t*>(B), N, scale, o_idx, mode, Y);
+                     tstart, tlen, static_cast<const bf16_t*>(B), N, scale, o_idx, mode, tm, Y);
   return hipGetLastError();
 }
 

@@ -337,7 +337,7 @@ class RelationTiles:
     messages (``SegmentIndex``) for the deterministic per-node sums.  Built once per
     (edge_index, relation ids)."""
 
-    def __init__(self, edge_index, rel, size, num_rel, aggr="mean"):
+    def __init__(self, edge_index, rel, size, num_rel, aggr="mean", tile=_TILE):
         dst, src = edge_index[0].long(), edge_index[1].long()
         rel = rel.reshape(-1).long()
         valid = (dst >= 0) & (src >= 0) & (rel >= 0) & (rel < num_rel)
@@ -357,7 +357,8 @@ class RelationTiles:
         else:
             self.scale = torch.ones(order.numel(), device=dev)
         counts = torch.bincount(r_sorted, minlength=num_rel)[:num_rel]
-        self.tile_rel, self.tile_start, self.tile_len, self.num_tiles = self._cut(counts, _TILE, dev)
+        self.tile = int(tile)
+        self.tile_rel, self.tile_start, self.tile_len, self.num_tiles = self._cut(counts, tile, dev)
         chunk = hip().rel_gemm_dw_chunk if dev.type == "cuda" else 1024
         self.chunk_rel, self.chunk_start, self.chunk_len, self.num_chunks = self._cut(counts, chunk, dev)
         # a relation's only chunk stores its dW slab instead of adding atomically
@@ -433,7 +434,7 @@ class _RelationTransform(torch.autograd.Function):
         wb = _pad_bf16(weight, (0, Kp - K, 0, Np - N))
         msg = torch.empty(tiles.num_edges, Np, device=x.device, dtype=torch.bfloat16)
         tr, ts, tl = tiles.tiles()
-        hip().rel_gemm(xb, tiles.src, tr, ts, tl, wb, None, tiles.slot_dst, 0, msg)
+        hip().rel_gemm(xb, tiles.src, tr, ts, tl, wb, None, tiles.slot_dst, 0, tiles.tile, msg)
         op = 1 if tiles.aggr == "mean" else 0
         out = hip().segment_reduce(msg, tiles.dst_seg.indptr, None, op, 0.0)[0]
         ctx.tiles, ctx.dims = tiles, (R, N, K, Kp, Np, x.shape[0])
@@ -452,7 +453,7 @@ class _RelationTransform(torch.autograd.Function):
             wt = wb.transpose(1, 2).contiguous()  # [R, Kp, Np]
             msgx = torch.empty(tiles.num_edges, Kp, device=dout.device, dtype=torch.bfloat16)
             tr, ts, tl = tiles.tiles()
-            hip().rel_gemm(gb, tiles.dst, tr, ts, tl, wt, tiles.scale, tiles.slot_src, 0, msgx)
+            hip().rel_gemm(gb, tiles.dst, tr, ts, tl, wt, tiles.scale, tiles.slot_src, 0, tiles.tile, msgx)
             dxp = hip().segment_reduce(msgx, tiles.src_seg.indptr, None, 0, 0.0)[0]
             dx = dxp[:, :K].to(ctx.x_dtype)
         if ctx.needs_input_grad[1]:
@@ -467,10 +468,15 @@ def relation_transform(x, rel, weight, edge_index, size, aggr="mean", tiles=None
     """R-GCN message + aggregation: ``out[i] = aggr_e weight[rel_e] @ x[src_e]`` over the
     in-edges of ``i`` (aggr ``mean`` or ``add``).  x [N_src, K], weight [R, N, K]."""
     R, N, K = weight.shape
-    if use_hip(x, weight) and _round_up(N, 64) + _round_up(K, 64) <= 1024:
+    lds_row = (_round_up(N, 64) + _round_up(K, 64) + 16) * 2  # bytes per tile row (A + output)
+    if use_hip(x, weight) and lds_row * 16 <= 158 * 1024:
         if tiles is None:
-            key = "_euler_reltiles_%d_%d_%s" % (int(size[0]), R, aggr)
-            tiles = _cached(edge_index, key, lambda: RelationTiles(edge_index, rel, size, R, aggr))
+            # the largest tile (edges of one relation per W_rel read) whose LDS rows fit
+            tm = min(hip().rel_gemm_tile, int(os.environ.get("EULER_AMD_RG_TILE", "64")))
+            while tm > 16 and lds_row * tm > 158 * 1024:
+                tm //= 2
+            key = "_euler_reltiles_%d_%d_%s_%d" % (int(size[0]), R, aggr, tm)
+            tiles = _cached(edge_index, key, lambda: RelationTiles(edge_index, rel, size, R, aggr, tile=tm))
         return _RelationTransform.apply(x, weight, tiles, int(size[0]))
     return relation_transform_reference(x, rel, weight, edge_index, size, aggr).to(x.dtype)
 

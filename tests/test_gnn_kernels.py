@@ -184,7 +184,7 @@ def test_tall_linear_grads(cuda, bias):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("K,N,aggr,R", [(100, 100, "mean", 13), (128, 64, "add", 13), (32, 200, "mean", 13),
-                                         (128, 128, "mean", 3), (128, 96, "mean", 13)])  # R = 3: multi-chunk relations (atomic dW)
+                                         (128, 128, "mean", 3), (128, 96, "mean", 13), (320, 320, "mean", 13)])  # R = 3: multi-chunk relations (atomic dW)
 def test_relation_transform_matches_reference(cuda, K, N, aggr, R):
     torch.manual_seed(4)
     n_dst, n_src, E = 400, 900, 7000
