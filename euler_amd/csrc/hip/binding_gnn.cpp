@@ -196,6 +196,20 @@ void rel_gemm(torch::Tensor A, torch::Tensor a_idx, torch::Tensor trel, torch::T
      "rel_gemm");
 }
 
+std::vector<torch::Tensor> rel_weight_bf16(torch::Tensor W) {
+  typed(W, torch::kFloat32, "W");
+  TORCH_CHECK(W.dim() == 3 && W.is_contiguous(), "W must be a contiguous [R, N, K] tensor");
+  const int64_t R = W.size(0), N = W.size(1), K = W.size(2);
+  TORCH_CHECK(N % 64 == 0 && K % 64 == 0, "rel_weight_bf16 needs N, K multiples of 64");
+  auto opt = W.options().dtype(torch::kBFloat16);
+  torch::Tensor wb = torch::empty({R, N, K}, opt), wt = torch::empty({R, K, N}, opt);
+  const c10::DeviceGuard g(W.device());
+  ok(eh_rel_weight_bf16(W.data_ptr<float>(), R, static_cast<int>(N), static_cast<int>(K), wb.data_ptr(), wt.data_ptr(),
+                        stream()),
+     "rel_weight_bf16");
+  return {wb, wt};
+}
+
 void rel_gemm_dw(torch::Tensor G, torch::Tensor g_idx, torch::Tensor X, torch::Tensor x_idx,
                  c10::optional<torch::Tensor> scale, torch::Tensor trel, torch::Tensor tstart, torch::Tensor tlen,
                  c10::optional<torch::Tensor> solo, torch::Tensor dW) {
@@ -531,6 +545,7 @@ void register_gnn_ops(pybind11::module& m) {
   m.def("gat_att_bwd_", &gat_att_bwd_);
   m.def("rel_gemm", &rel_gemm);
   m.def("rel_gemm_dw", &rel_gemm_dw);
+  m.def("rel_weight_bf16", &rel_weight_bf16);
   m.attr("rel_gemm_dw_chunk") = eh_rel_gemm_dw_chunk();
   m.attr("rel_gemm_tile") = eh_rel_gemm_tile();
   m.def("sgns_fwd", &sgns_fwd);

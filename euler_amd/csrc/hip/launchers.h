@@ -104,7 +104,8 @@ hipError_t eh_gat_bwd(const int64_t* indptr, const int32_t* col, const int32_t* 
 // rgcn.hip (K6: relation-grouped MFMA GEMM)
 size_t eh_rel_gemm_lds(int K, int N, int mode, int tm);
 int eh_rel_gemm_tile();      // edges per message-GEMM tile (tiles: <= this many edges of one relation)
-int eh_rel_gemm_dw_chunk();  // edges per dW chunk (chunks: <= this many edges of one relation)
+int eh_rel_gemm_dw_chunk();
+hipError_t eh_rel_weight_bf16(const float* W, int64_t R, int N, int K, void* wb, void* wt, hipStream_t s);  // edges per dW chunk (chunks: <= this many edges of one relation)
 hipError_t eh_rel_gemm(const void* A, int K, const int32_t* a_idx, const int32_t* trel, const int32_t* tstart,
                        const int32_t* tlen, int n_tiles, const void* B, int N, const float* scale,
                        const int32_t* o_idx, int mode, int tm, void* Y, hipStream_t s);

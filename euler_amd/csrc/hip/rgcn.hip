@@ -252,6 +252,42 @@ __global__ __launch_bounds__(256) void rel_gemm_dw_kernel(const bf16_t* __restri
       }
 }
 
+// bf16 operands of the relation weights for one step: wb[r] = bf16(W[r]) ([N][K], the
+// forward B) and wt[r] = bf16(W[r])^T ([K][N], the backward B) from one read of the fp32
+// weights; 64 x 64 tiles, the transpose through LDS (padded rows: conflict-free columns)
+__global__ __launch_bounds__(256) void rel_weight_bf16_kernel(const float* __restrict__ W, int N, int K,
+                                                              bf16_t* __restrict__ wb, bf16_t* __restrict__ wt) {
+  __shared__ bf16_t t_s[64][66];
+  const int tk = K >> 6, tn = N >> 6;
+  const int64_t b = blockIdx.x;
+  const int64_t r = b / (static_cast<int64_t>(tn) * tk);
+  const int rem = static_cast<int>(b - r * tn * tk);
+  const int n0 = (rem / tk) * 64, k0 = (rem % tk) * 64;
+  const int tid = threadIdx.x, row = tid >> 2, c0 = (tid & 3) * 16;
+  const int64_t base = r * static_cast<int64_t>(N) * K;
+  const float* src = W + base + static_cast<int64_t>(n0 + row) * K + k0 + c0;
+  float v[16];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4_t f = *reinterpret_cast<const float4_t*>(src + q * 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[q * 4 + j] = f[j];
+  }
+  bf16_t* dst = wb + base + static_cast<int64_t>(n0 + row) * K + k0 + c0;
+  *reinterpret_cast<uint4_t*>(dst) = pack_bf16x8(v);
+  *reinterpret_cast<uint4_t*>(dst + 8) = pack_bf16x8(v + 8);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) t_s[row][c0 + j] = f2bf(v[j]);
+  __syncthreads();
+  // transposed: output row k0 + row (an input column), columns n0 + c0 .. + 15
+  float u[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) u[j] = bf2f(t_s[c0 + j][row]);
+  bf16_t* dT = wt + base + static_cast<int64_t>(k0 + row) * N + n0 + c0;
+  *reinterpret_cast<uint4_t*>(dT) = pack_bf16x8(u);
+  *reinterpret_cast<uint4_t*>(dT + 8) = pack_bf16x8(u + 8);
+}
+
 }  // namespace euler_hip
 
 using namespace euler_hip;
@@ -299,5 +335,15 @@ hipError_t eh_rel_gemm_dw(const void* G, int N, const int32_t* g_idx, const void
 }
 
 int eh_rel_gemm_dw_chunk() { return RG_CH; }
+
+hipError_t eh_rel_weight_bf16(const float* W, int64_t R, int N, int K, void* wb, void* wt, hipStream_t s) {
+  if (R <= 0) return hipSuccess;
+  if (N % 64 != 0 || K % 64 != 0) return hipErrorInvalidValue;
+  const int64_t blocks = R * (N / 64) * (K / 64);
+  if (blocks >= (1ll << 31)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(rel_weight_bf16_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, W, N, K,
+                     static_cast<bf16_t*>(wb), static_cast<bf16_t*>(wt));
+  return hipGetLastError();
+}
 
 }  // extern "C"

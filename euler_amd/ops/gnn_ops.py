@@ -431,7 +431,12 @@ class _RelationTransform(torch.autograd.Function):
         R, N, K = weight.shape
         Kp, Np = _round_up(K, 64), _round_up(N, 64)
         xb = _pad_bf16(x, (0, Kp - K))
-        wb = _pad_bf16(weight, (0, Kp - K, 0, Np - N))
+        wt = None
+        if Kp == K and Np == N and weight.dtype == torch.float32:
+            # both bf16 operands (forward W, backward W^T) from one pass over the fp32 weights
+            wb, wt = hip().rel_weight_bf16(weight.contiguous())
+        else:
+            wb = _pad_bf16(weight, (0, Kp - K, 0, Np - N))
         msg = torch.empty(tiles.num_edges, Np, device=x.device, dtype=torch.bfloat16)
         tr, ts, tl = tiles.tiles()
         hip().rel_gemm(xb, tiles.src, tr, ts, tl, wb, None, tiles.slot_dst, 0, tiles.tile, msg)
@@ -439,6 +444,7 @@ class _RelationTransform(torch.autograd.Function):
         out = hip().segment_reduce(msg, tiles.dst_seg.indptr, None, op, 0.0)[0]
         ctx.tiles, ctx.dims = tiles, (R, N, K, Kp, Np, x.shape[0])
         ctx.x_dtype, ctx.w_dtype = x.dtype, weight.dtype
+        ctx.wt = wt
         ctx.save_for_backward(xb, wb)
         return out[:, :N].to(x.dtype)
 
@@ -450,7 +456,7 @@ class _RelationTransform(torch.autograd.Function):
         gb = _pad_bf16(dout, (0, Np - N))
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            wt = wb.transpose(1, 2).contiguous()  # [R, Kp, Np]
+            wt = ctx.wt if ctx.wt is not None else wb.transpose(1, 2).contiguous()  # [R, Kp, Np]
             msgx = torch.empty(tiles.num_edges, Kp, device=dout.device, dtype=torch.bfloat16)
             tr, ts, tl = tiles.tiles()
             hip().rel_gemm(gb, tiles.dst, tr, ts, tl, wt, tiles.scale, tiles.slot_src, 0, tiles.tile, msgx)

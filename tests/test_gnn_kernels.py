@@ -440,3 +440,13 @@ def test_splitk_linear_grads_match(cuda, dtype):
     m = splitk_mm_t(dy, x.detach())
     assert m.dtype == torch.float32 and m.shape == (121, 256)
     assert ((m - dy.float().t() @ x.detach().float()).norm() / m.norm()) < tol
+
+
+@pytest.mark.gpu
+def test_rel_weight_bf16_shadows(cuda):
+    from euler_amd.ops._native import hip
+    W = torch.randn(5, 128, 192, device=cuda)
+    wb, wt = hip().rel_weight_bf16(W)
+    ref = W.to(torch.bfloat16)
+    assert torch.equal(wb, ref)
+    assert torch.equal(wt, ref.transpose(1, 2).contiguous())
