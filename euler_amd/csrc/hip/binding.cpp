@@ -277,6 +277,30 @@ std::vector<torch::Tensor> segment_reduce(torch::Tensor src, torch::Tensor indpt
   return {out};
 }
 
+// wave-per-segment sum / mean (skewed segment lengths); D / (8 bf16 | 4 fp32) a power of two <= 64
+torch::Tensor segment_reduce_wave(torch::Tensor src, torch::Tensor indptr, c10::optional<torch::Tensor> perm,
+                                  int64_t op) {
+  need_cuda(src, "src");
+  need_i64(indptr, "indptr");
+  const bool bf = is_bf16(src, "src");
+  TORCH_CHECK(src.dim() == 2 && src.is_contiguous(), "src must be a contiguous 2-D tensor");
+  if (perm.has_value()) {
+    need_i64(*perm, "perm");
+    TORCH_CHECK(perm->numel() == src.size(0), "perm must cover src rows");
+  }
+  TORCH_CHECK(op == 0 || op == 1, "op must be 0(sum) 1(mean)");
+  const int64_t S = indptr.numel() - 1, D = src.size(1), LP = D / (bf ? 8 : 4);
+  TORCH_CHECK(D % (bf ? 8 : 4) == 0 && LP <= 64 && (LP & (LP - 1)) == 0,
+              "segment_reduce_wave needs D / (8 bf16 | 4 fp32) to be a power of two <= 64");
+  const c10::DeviceGuard g(src.device());
+  auto out = torch::empty({S, D}, src.options());
+  check(eh_segment_reduce_wave(src.data_ptr(), bf, static_cast<int>(D), indptr.data_ptr<int64_t>(),
+                               perm.has_value() ? perm->data_ptr<int64_t>() : nullptr, S, static_cast<int>(op),
+                               out.data_ptr(), cur_stream()),
+        "segment_reduce_wave");
+  return out;
+}
+
 void index_add_rows_(torch::Tensor out, torch::Tensor idx, torch::Tensor src) {
   need_cuda(out, "out");
   need_i64(idx, "idx");
@@ -735,6 +759,7 @@ PYBIND11_MODULE(_hip_ops, m) {
   m.def("relu_bwd_", &relu_bwd_);
   m.def("gather_rows", &gather_rows);
   m.def("segment_reduce", &segment_reduce);
+  m.def("segment_reduce_wave", &segment_reduce_wave);
   m.def("index_add_rows_", &index_add_rows_);
   m.def("max_bwd", &max_bwd);
   m.def("edge_softmax", &edge_softmax);

@@ -34,6 +34,8 @@ hipError_t eh_relu_bwd(void* g, const void* y, int64_t n, hipStream_t s);
 // mp.hip
 hipError_t eh_gather_rows(const void* x, int64_t n_rows, int64_t row_bytes, const void* idx, int idx_is64, int64_t n,
                           void* out, hipStream_t s);
+hipError_t eh_segment_reduce_wave(const void* src, int is_bf16, int D, const int64_t* indptr, const int64_t* perm,
+                                  int64_t S, int op, void* out, hipStream_t s);
 hipError_t eh_segment_reduce(const void* src, int is_bf16, int D, const int64_t* indptr, const int64_t* perm,
                              int64_t S, int op, float empty_val, void* out, int64_t* argmax, hipStream_t s);
 hipError_t eh_index_add_rows(const void* src, int is_bf16, int D, const int64_t* idx, int64_t n, float* out,

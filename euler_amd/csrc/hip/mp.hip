@@ -201,6 +201,58 @@ __global__ __launch_bounds__(256) void segment_reduce_vec_kernel(const T* __rest
   }
 }
 
+// wave-per-segment sum / mean for skewed segment lengths (power-law in-degrees: a hot
+// destination's long segment is no longer one lane group's serial chain).  A wave covers one
+// segment: LP = D / V lanes per row, 64 / LP rows side by side, U row steps in flight, then
+// a butterfly over the row slots.  op 0 sum, 1 mean; D / V a power of two <= 64.
+template <typename T>
+__global__ __launch_bounds__(256) void segment_reduce_wave_kernel(const T* __restrict__ src, int D,
+                                                                  const int64_t* __restrict__ indptr,
+                                                                  const int64_t* __restrict__ perm, int64_t S, int op,
+                                                                  T* __restrict__ out) {
+  constexpr int V = SegVec<T>::V;
+  const int64_t s = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (s >= S) return;  // uniform per wave
+  const int LP = D / V, R = 64 / LP;
+  const int lane = threadIdx.x & 63, slot = lane / LP, d0 = (lane - slot * LP) * V;
+  const int64_t a = indptr[s], b = indptr[s + 1];
+  float acc[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) acc[i] = 0.f;
+  constexpr int U = 4;
+  for (int64_t e0 = a + slot; e0 < b; e0 += static_cast<int64_t>(R) * U) {
+    int64_t row[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t e = e0 + static_cast<int64_t>(u) * R;
+      row[u] = e < b ? (perm ? perm[e] : e) : -1;
+    }
+    float v[U][V];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (row[u] >= 0) {
+        SegVec<T>::load(src + row[u] * D + d0, v[u]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < V; ++i) v[u][i] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int i = 0; i < V; ++i) acc[i] += v[u][i];
+  }
+  for (int off = LP; off < 64; off <<= 1)
+#pragma unroll
+    for (int i = 0; i < V; ++i) acc[i] += __shfl_xor(acc[i], off, 64);
+  if (slot == 0) {
+    const float inv = (op == 1 && b > a) ? 1.f / static_cast<float>(b - a) : 1.f;
+#pragma unroll
+    for (int i = 0; i < V; ++i) acc[i] *= inv;
+    SegVec<T>::store(out + s * D + d0, acc);
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void index_add_rows_kernel(const T* __restrict__ src, int D,
                                                              const int64_t* __restrict__ idx, int64_t n,
@@ -399,6 +451,24 @@ hipError_t eh_gather_rows(const void* x, int64_t n_rows, int64_t row_bytes, cons
   return hipGetLastError();
 }
 
+
+hipError_t eh_segment_reduce_wave(const void* src, int is_bf16, int D, const int64_t* indptr, const int64_t* perm,
+                                  int64_t S, int op, void* out, hipStream_t s) {
+  if (S == 0 || D == 0) return hipSuccess;
+  const int V = is_bf16 ? 8 : 4;
+  const int LP = D / V;
+  if (D % V != 0 || LP > 64 || (LP & (LP - 1)) != 0 || op < 0 || op > 1) return hipErrorInvalidValue;
+  if (reinterpret_cast<uintptr_t>(src) % 16 != 0 || reinterpret_cast<uintptr_t>(out) % 16 != 0)
+    return hipErrorInvalidValue;
+  const dim3 grid(static_cast<uint32_t>(ceil_div(S, 4)));
+  if (is_bf16)
+    hipLaunchKernelGGL(segment_reduce_wave_kernel<bf16_t>, grid, dim3(256), 0, s, static_cast<const bf16_t*>(src), D,
+                       indptr, perm, S, op, static_cast<bf16_t*>(out));
+  else
+    hipLaunchKernelGGL(segment_reduce_wave_kernel<float>, grid, dim3(256), 0, s, static_cast<const float*>(src), D,
+                       indptr, perm, S, op, static_cast<float*>(out));
+  return hipGetLastError();
+}
 
 hipError_t eh_segment_reduce(const void* src, int is_bf16, int D, const int64_t* indptr, const int64_t* perm,
                              int64_t S, int op, float empty_val, void* out, int64_t* argmax, hipStream_t s) {

@@ -421,6 +421,18 @@ def _pad_bf16(t, pad):
     return t.contiguous()
 
 
+def _seg_sum(msg, indptr, op):
+    """per-node sum (op 0) / mean (1) of CSR-ordered message rows: one wave per node
+    (relation graphs have power-law in-degrees) when the row width allows it"""
+    lp = msg.shape[1] // (8 if msg.dtype == torch.bfloat16 else 4)
+    if _SEG_WAVE and 0 < lp <= 64 and lp & (lp - 1) == 0:
+        return hip().segment_reduce_wave(msg, indptr, None, op)
+    return hip().segment_reduce(msg, indptr, None, op, 0.0)[0]
+
+
+_SEG_WAVE = os.environ.get("EULER_AMD_SEG_WAVE", "1") == "1"
+
+
 class _RelationTransform(torch.autograd.Function):
     """Messages W_rel x_src are stored once per edge (bf16, 16-byte rows) by the grouped
     GEMM and summed per destination by the segment kernel: plain stores + one
@@ -441,7 +453,7 @@ class _RelationTransform(torch.autograd.Function):
         tr, ts, tl = tiles.tiles()
         hip().rel_gemm(xb, tiles.src, tr, ts, tl, wb, None, tiles.slot_dst, 0, tiles.tile, msg)
         op = 1 if tiles.aggr == "mean" else 0
-        out = hip().segment_reduce(msg, tiles.dst_seg.indptr, None, op, 0.0)[0]
+        out = _seg_sum(msg, tiles.dst_seg.indptr, op)
         ctx.tiles, ctx.dims = tiles, (R, N, K, Kp, Np, x.shape[0])
         ctx.x_dtype, ctx.w_dtype = x.dtype, weight.dtype
         ctx.wt = wt
@@ -460,7 +472,7 @@ class _RelationTransform(torch.autograd.Function):
             msgx = torch.empty(tiles.num_edges, Kp, device=dout.device, dtype=torch.bfloat16)
             tr, ts, tl = tiles.tiles()
             hip().rel_gemm(gb, tiles.dst, tr, ts, tl, wt, tiles.scale, tiles.slot_src, 0, tiles.tile, msgx)
-            dxp = hip().segment_reduce(msgx, tiles.src_seg.indptr, None, 0, 0.0)[0]
+            dxp = _seg_sum(msgx, tiles.src_seg.indptr, 0)
             dx = dxp[:, :K].to(ctx.x_dtype)
         if ctx.needs_input_grad[1]:
             dwp = torch.zeros(R, Np, Kp, device=dout.device, dtype=torch.float32)

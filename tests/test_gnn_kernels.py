@@ -450,3 +450,28 @@ def test_rel_weight_bf16_shadows(cuda):
     ref = W.to(torch.bfloat16)
     assert torch.equal(wb, ref)
     assert torch.equal(wt, ref.transpose(1, 2).contiguous())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,D,op,use_perm", [(torch.bfloat16, 128, 1, False), (torch.float32, 128, 0, True),
+                                                 (torch.bfloat16, 64, 0, True), (torch.float32, 16, 1, False)])
+def test_segment_reduce_wave_matches_reference(cuda, dtype, D, op, use_perm):
+    from euler_amd.ops._native import hip
+    torch.manual_seed(7)
+    S = 300
+    lens = (torch.rand(S) ** 6 * 900).long()  # skewed: a few long segments, many short / empty
+    lens[::37] = 0
+    indptr = torch.zeros(S + 1, dtype=torch.long)
+    indptr[1:] = torch.cumsum(lens, 0)
+    n = int(indptr[-1])
+    x = torch.randn(n, D, device=cuda).to(dtype)
+    perm = torch.randperm(n, device=cuda) if use_perm else None
+    out = hip().segment_reduce_wave(x, indptr.to(cuda), perm, op)
+    xs = (x[perm] if use_perm else x).float().cpu()
+    ref = torch.zeros(S, D)
+    for s in range(S):
+        a, b = int(indptr[s]), int(indptr[s + 1])
+        if b > a:
+            ref[s] = xs[a:b].sum(0) / (b - a if op == 1 else 1)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(out.float().cpu(), ref, atol=tol * 10, rtol=tol)
