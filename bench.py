@@ -133,8 +133,21 @@ def main(argv=None):
 
     use_graph = not args.no_graph
     if use_graph:
-        tr.capture(grad_sync)
+        ok = True
+        try:
+            tr.capture(grad_sync)
+        except RuntimeError as e:  # e.g. a collective the runtime cannot capture
+            ok = False
+            log(f"rank {rank}: step capture failed ({e}); running eager steps")
+        if dist_on:  # every rank takes the same path (captured collectives never ran)
+            flag = torch.tensor([0 if ok else 1], dtype=torch.int32, device=dev)
+            dist.all_reduce(flag)
+            ok = int(flag.item()) == 0
+        if not ok:
+            tr._graph_exec = None
+            use_graph = False
 
+    if use_graph:
         def step():
             tr.replay()
     else:
