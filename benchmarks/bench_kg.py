@@ -84,6 +84,7 @@ def main(argv=None):
     p.add_argument("--num-negs", type=int, default=8)
     p.add_argument("--lr", type=float, default=1e-3)
     p.add_argument("--seed", type=int, default=3)
+    p.add_argument("--layers", type=int, default=2, help="R-GCN layers before the TransE decoder (0: TransE alone)")
     p.add_argument("--eval-after", type=int, default=2000,
                    help="keep training (untimed) to this many steps, then rank the held-out triples")
     args = p.parse_args(argv)
@@ -105,7 +106,7 @@ def main(argv=None):
     # message direction src -> dst (row 0 = destination, row 1 = source)
     edge_index = torch.stack([dst, src])
     torch.manual_seed(args.seed)
-    model = RGCNTransE(args.num_ent, args.num_rel, args.dim).to(dev)
+    model = RGCNTransE(args.num_ent, args.num_rel, args.dim, layers=args.layers).to(dev)
     gen = torch.Generator(device=dev).manual_seed(args.seed * 101 + rank)
 
     def batch():
@@ -176,7 +177,7 @@ def main(argv=None):
             "vs_baseline": None,
             "dtype": "bf16 relation GEMMs (fp32 accumulate), fp32 scores",
             "data": "synthetic (FB15k-shaped random KG, power-law relations)",
-            "config": {"model": "R-GCN 2x RelationConv(mean, self-loop) + TransE-l2 margin, Adam",
+            "config": {"model": f"R-GCN {args.layers}x RelationConv(mean, self-loop) + TransE-l2 margin, Adam",
                        "num_ent": args.num_ent, "num_rel": args.num_rel, "num_triples": args.num_triples,
                        "dim": args.dim, "batch_per_gpu": args.batch, "num_negs": args.num_negs,
                        "parallelism": f"dp{world}", "loss_first_last": [round(first, 4), round(float(last), 4)],
