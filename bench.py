@@ -12,8 +12,9 @@ The step is the framework's training path, euler_amd.models.sage_trainer.SageTra
 2 hops of neighbour sampling on the GPU, forward, backward, optimizer — four gfx950
 launches captured in one hipGraph.  One process per GPU (torchrun): every rank holds
 the whole graph + feature table in its own HBM with its own sample stream; the flat
-fp32 gradient is all-reduced over RCCL inside the captured step.  Nothing is skipped
-inside the timed region.
+gradient is all-reduced over RCCL inside the captured step (fp32 by default, as the
+reference's synchronous gradient sync; --grad-reduce-dtype bf16 halves the bytes and the
+JSON config records which one ran).  Nothing is skipped inside the timed region.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [...]
 """
@@ -52,8 +53,9 @@ def parse_args(argv=None):
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--no-graph", action="store_true", help="eager steps instead of hipGraph replay")
     p.add_argument("--log", action="store_true")
-    p.add_argument("--grad-reduce-dtype", choices=["bf16", "fp32"], default="bf16",
-                   help="dtype of the data-parallel gradient all-reduce (bf16: half the bytes on xGMI)")
+    p.add_argument("--grad-reduce-dtype", choices=["bf16", "fp32"], default="fp32",
+                   help="dtype of the data-parallel gradient all-reduce (bf16: half the bytes on xGMI, "
+                        "summed in bf16 by RCCL)")
     p.add_argument("--force-dist", action="store_true",
                    help="take the multi-GPU code path (process group, all-reduce in the step) even with one rank")
     return p.parse_args(argv)

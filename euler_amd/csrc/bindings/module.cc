@@ -327,6 +327,7 @@ class Engine {
   }
 
   std::map<int, std::vector<std::string>> Endpoints() const { return proxy_->Endpoints(); }
+  void SetReplicas(int shard, const std::vector<std::string>& eps) { Throw(proxy_->SetReplicas(shard, eps)); }
 
   // random walks [n, L + 1] (node2vec-biased unless p = q = 1), GIL released
   py::array_t<int64_t> RandomWalkPy(py::array_t<uint64_t, py::array::c_style | py::array::forcecast> starts,
@@ -605,6 +606,7 @@ PYBIND11_MODULE(_engine, m) {
       .def("dense_feature", &Engine::DenseFeature)
       .def("export_csr", &Engine::ExportCsr)
       .def("endpoints", [](Engine& e) { return e.Endpoints(); })
+      .def("set_replicas", &Engine::SetReplicas, py::arg("shard"), py::arg("endpoints"))
       .def("export_nodes", &Engine::ExportNodes);
 
   py::class_<PySagePipeline>(m, "SagePipeline")
@@ -756,6 +758,34 @@ PYBIND11_MODULE(_engine, m) {
     return nodes;
   }, py::arg("query"), py::arg("mode") = "local", py::arg("shard_num") = 1,
      py::arg("neighbor_indexes") = std::vector<std::string>{}, py::arg("fuse") = true);
+  // the REMOTE fusion pass on a hand-built DAG: nodes = [(op, id, inputs, shard)] in
+  // topological order; returns [(name, op, shard, inputs, [inner op names])]
+  m.def("fuse_remote_nodes", [](std::vector<std::tuple<std::string, int, std::vector<std::string>, int>> spec) {
+    DAGDef d;
+    for (auto& t : spec) {
+      NodeDef n;
+      n.op = std::get<0>(t);
+      n.id = std::get<1>(t);
+      n.inputs = std::get<2>(t);
+      n.shard_idx = std::get<3>(t);
+      if (n.op == "REMOTE") {
+        NodeDef inner;
+        inner.op = "INNER_" + std::to_string(n.id);
+        inner.id = n.id;
+        n.inner.push_back(inner);
+        n.output_list.push_back(inner.Output(0));
+      }
+      d.nodes.push_back(n);
+    }
+    FuseRemoteNodes(&d);
+    py::list out;
+    for (auto& n : d.nodes) {
+      std::vector<std::string> inner;
+      for (auto& c : n.inner) inner.push_back(c.op);
+      out.append(py::make_tuple(n.name(), n.op, n.shard_idx, n.inputs, inner));
+    }
+    return out;
+  });
   m.def(
       "registry_list",
       [](const std::string& spec, double ttl) {

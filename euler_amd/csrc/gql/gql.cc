@@ -428,7 +428,7 @@ class Optimizer {
       EmitSharded(orig, nd, it->second);
     }
     Cse();
-    if (opt_.fuse) FuseRemotes();
+    if (opt_.fuse) FuseRemoteNodes(out_);
   }
 
  private:
@@ -596,121 +596,6 @@ class Optimizer {
     out_->nodes.swap(kept);
   }
 
-  // Fuse the REMOTE nodes of each shard that do not depend on each other into one REMOTE
-  // with a multi-node inner sub-DAG: one RPC per shard per dependency level instead of one
-  // per op (e.g. a hop's sampleNB and the frontier's values()).  Greedy in topological
-  // order: a REMOTE joins the first group of its shard that is not among its (transitive)
-  // ancestors — group ancestry is tracked through fused groups, so no cycle can form.
-  // Output slots of a fused member are renumbered behind the group's first node.
-  void FuseRemotes() {
-    std::vector<NodeDef>& nodes = out_->nodes;
-    const size_t N = nodes.size();
-    std::unordered_map<std::string, size_t> by_name;
-    for (size_t i = 0; i < N; ++i) by_name[nodes[i].name()] = i;
-    std::vector<int> group(N, -1);
-    std::vector<std::set<int>> anc(N);       // ancestor groups of each node
-    std::vector<std::set<int>> ganc;          // ancestor groups of each group
-    std::vector<std::vector<size_t>> members;
-    std::vector<int> gshard;
-    auto refs = [](const NodeDef& n) {
-      std::vector<std::string> r = n.inputs;
-      for (auto& a : n.attrs)
-        if (a.find(':') != std::string::npos) r.push_back(a);
-      return r;
-    };
-    for (size_t i = 0; i < N; ++i) {
-      std::set<int> a;
-      for (auto& ref : refs(nodes[i])) {
-        auto it = by_name.find(InputNode(ref));
-        if (it == by_name.end() || it->second >= i) continue;
-        const size_t p = it->second;
-        if (group[p] >= 0) {
-          a.insert(group[p]);
-          a.insert(ganc[group[p]].begin(), ganc[group[p]].end());
-        } else {
-          a.insert(anc[p].begin(), anc[p].end());
-        }
-      }
-      anc[i] = a;
-      if (nodes[i].op != "REMOTE") continue;
-      int g = -1;
-      for (size_t k = 0; k < members.size(); ++k)
-        if (gshard[k] == nodes[i].shard_idx && !a.count(static_cast<int>(k))) {
-          g = static_cast<int>(k);
-          break;
-        }
-      if (g < 0) {
-        g = static_cast<int>(members.size());
-        members.push_back({});
-        ganc.push_back({});
-        gshard.push_back(nodes[i].shard_idx);
-      }
-      members[g].push_back(i);
-      ganc[g].insert(a.begin(), a.end());
-      group[i] = g;
-    }
-    // merge: the first member absorbs the others' inner nodes, inputs and output slots
-    std::unordered_map<std::string, std::string> ren;  // "REMOTE,<b>:<k>" -> "REMOTE,<a>:<off + k>"
-    std::vector<bool> drop(N, false);
-    for (auto& mem : members) {
-      if (mem.size() < 2) continue;
-      NodeDef& head = nodes[mem[0]];
-      const std::string hn = head.name();
-      std::set<std::string> ins(head.inputs.begin(), head.inputs.end());
-      for (size_t k = 1; k < mem.size(); ++k) {
-        NodeDef& m = nodes[mem[k]];
-        for (int o = 0; o < m.output_num; ++o)
-          ren[m.Output(o)] = hn + ":" + std::to_string(head.output_num + o);
-        head.output_num += m.output_num;
-        head.output_list.insert(head.output_list.end(), m.output_list.begin(), m.output_list.end());
-        head.inner.insert(head.inner.end(), m.inner.begin(), m.inner.end());
-        for (auto& x : m.inputs)
-          if (ins.insert(x).second) head.inputs.push_back(x);
-        drop[mem[k]] = true;
-      }
-    }
-    if (ren.empty()) return;
-    std::vector<NodeDef> kept;
-    kept.reserve(N);
-    for (size_t i = 0; i < N; ++i) {
-      if (drop[i]) continue;
-      NodeDef m = nodes[i];
-      for (auto& x : m.inputs) {
-        auto it = ren.find(x);
-        if (it != ren.end()) x = it->second;
-      }
-      for (auto& x : m.attrs) {
-        auto it = ren.find(x);
-        if (it != ren.end()) x = it->second;
-      }
-      kept.push_back(std::move(m));
-    }
-    // the fused node sits where its first member was: restore a topological order
-    std::unordered_map<std::string, size_t> pos;
-    for (size_t i = 0; i < kept.size(); ++i) pos[kept[i].name()] = i;
-    std::vector<int> indeg(kept.size(), 0);
-    std::vector<std::vector<size_t>> succ(kept.size());
-    for (size_t i = 0; i < kept.size(); ++i)
-      for (auto& ref : refs(kept[i])) {
-        auto it = pos.find(InputNode(ref));
-        if (it == pos.end() || it->second == i) continue;
-        succ[it->second].push_back(i);
-        ++indeg[i];
-      }
-    std::vector<NodeDef> order;
-    order.reserve(kept.size());
-    std::vector<size_t> ready;
-    for (size_t i = 0; i < kept.size(); ++i)
-      if (indeg[i] == 0) ready.push_back(i);
-    for (size_t r = 0; r < ready.size(); ++r) {
-      order.push_back(kept[ready[r]]);
-      for (size_t j : succ[ready[r]])
-        if (--indeg[j] == 0) ready.push_back(j);
-    }
-    if (order.size() == kept.size()) nodes.swap(order);
-    else nodes.swap(kept);  // unreachable (fusion never forms a cycle); keep a valid DAG list anyway
-  }
-
   const CompileOptions& opt_;
   DAGDef* out_;
   int next_id_ = 1;
@@ -718,6 +603,137 @@ class Optimizer {
 };
 
 }  // namespace
+
+// Fuse the REMOTE nodes of each shard that do not depend on each other into one REMOTE
+// with a multi-node inner sub-DAG: one RPC per shard per dependency level instead of one
+// per op (e.g. a hop's sampleNB and the frontier's values()).  Greedy in topological
+// order: a REMOTE joins the first group of its shard that is not among its ancestor
+// groups.  Ancestry is evaluated at join time as the transitive closure through the
+// groups' CURRENT dependencies (a group gains dependencies as members join, and every
+// node downstream of it inherits them), so a join can never close a cycle.  Output slots
+// of a fused member are renumbered behind the group's first node.  If the fused list
+// cannot be ordered topologically (a bug), the unfused DAG is kept.
+void FuseRemoteNodes(DAGDef* dag) {
+  std::vector<NodeDef>& nodes = dag->nodes;
+  const size_t N = nodes.size();
+  std::unordered_map<std::string, size_t> by_name;
+  for (size_t i = 0; i < N; ++i) by_name[nodes[i].name()] = i;
+  std::vector<int> group(N, -1);
+  std::vector<std::set<int>> dep(N);   // nearest groups each node depends on (direct or via non-REMOTE nodes)
+  std::vector<std::set<int>> gdep;     // union of the members' dep sets, per group (grows as members join)
+  std::vector<std::vector<size_t>> members;
+  std::vector<int> gshard;
+  auto refs = [](const NodeDef& n) {
+    std::vector<std::string> r = n.inputs;
+    for (auto& a : n.attrs)
+      if (a.find(':') != std::string::npos) r.push_back(a);
+    return r;
+  };
+  auto closure = [&](const std::set<int>& seed) {
+    std::set<int> out(seed);
+    std::vector<int> stack(seed.begin(), seed.end());
+    while (!stack.empty()) {
+      const int g = stack.back();
+      stack.pop_back();
+      for (int h : gdep[g])
+        if (out.insert(h).second) stack.push_back(h);
+    }
+    return out;
+  };
+  for (size_t i = 0; i < N; ++i) {
+    std::set<int> d;
+    for (auto& ref : refs(nodes[i])) {
+      auto it = by_name.find(InputNode(ref));
+      if (it == by_name.end() || it->second >= i) continue;
+      const size_t p = it->second;
+      if (group[p] >= 0) d.insert(group[p]);
+      else d.insert(dep[p].begin(), dep[p].end());
+    }
+    dep[i] = d;
+    if (nodes[i].op != "REMOTE") continue;
+    const std::set<int> anc = closure(d);
+    int g = -1;
+    for (size_t k = 0; k < members.size(); ++k)
+      if (gshard[k] == nodes[i].shard_idx && !anc.count(static_cast<int>(k))) {
+        g = static_cast<int>(k);
+        break;
+      }
+    if (g < 0) {
+      g = static_cast<int>(members.size());
+      members.push_back({});
+      gdep.push_back({});
+      gshard.push_back(nodes[i].shard_idx);
+    }
+    members[g].push_back(i);
+    gdep[g].insert(d.begin(), d.end());
+    group[i] = g;
+  }
+  // merge: the first member absorbs the others' inner nodes, inputs and output slots
+  std::unordered_map<std::string, std::string> ren;  // "REMOTE,<b>:<k>" -> "REMOTE,<a>:<off + k>"
+  std::vector<bool> drop(N, false);
+  std::vector<NodeDef> original;
+  for (auto& mem : members) {
+    if (mem.size() < 2) continue;
+    if (original.empty()) original = nodes;
+    NodeDef& head = nodes[mem[0]];
+    const std::string hn = head.name();
+    std::set<std::string> ins(head.inputs.begin(), head.inputs.end());
+    for (size_t k = 1; k < mem.size(); ++k) {
+      NodeDef& m = nodes[mem[k]];
+      for (int o = 0; o < m.output_num; ++o) ren[m.Output(o)] = hn + ":" + std::to_string(head.output_num + o);
+      head.output_num += m.output_num;
+      head.output_list.insert(head.output_list.end(), m.output_list.begin(), m.output_list.end());
+      head.inner.insert(head.inner.end(), m.inner.begin(), m.inner.end());
+      for (auto& x : m.inputs)
+        if (ins.insert(x).second) head.inputs.push_back(x);
+      drop[mem[k]] = true;
+    }
+  }
+  if (ren.empty()) return;
+  std::vector<NodeDef> kept;
+  kept.reserve(N);
+  for (size_t i = 0; i < N; ++i) {
+    if (drop[i]) continue;
+    NodeDef m = nodes[i];
+    for (auto& x : m.inputs) {
+      auto it = ren.find(x);
+      if (it != ren.end()) x = it->second;
+    }
+    for (auto& x : m.attrs) {
+      auto it = ren.find(x);
+      if (it != ren.end()) x = it->second;
+    }
+    kept.push_back(std::move(m));
+  }
+  // the fused node sits where its first member was: restore a topological order
+  std::unordered_map<std::string, size_t> pos;
+  for (size_t i = 0; i < kept.size(); ++i) pos[kept[i].name()] = i;
+  std::vector<int> indeg(kept.size(), 0);
+  std::vector<std::vector<size_t>> succ(kept.size());
+  for (size_t i = 0; i < kept.size(); ++i)
+    for (auto& ref : refs(kept[i])) {
+      auto it = pos.find(InputNode(ref));
+      if (it == pos.end() || it->second == i) continue;
+      succ[it->second].push_back(i);
+      ++indeg[i];
+    }
+  std::vector<NodeDef> order;
+  order.reserve(kept.size());
+  std::vector<size_t> ready;
+  for (size_t i = 0; i < kept.size(); ++i)
+    if (indeg[i] == 0) ready.push_back(i);
+  for (size_t r = 0; r < ready.size(); ++r) {
+    order.push_back(kept[ready[r]]);
+    for (size_t j : succ[ready[r]])
+      if (--indeg[j] == 0) ready.push_back(j);
+  }
+  if (order.size() == kept.size()) {
+    nodes.swap(order);
+  } else {
+    EULER_LOG(Error) << "FuseRemoteNodes: fused DAG is cyclic; keeping the unfused plan";
+    nodes.swap(original);
+  }
+}
 
 Compiler& Compiler::Get() {
   static Compiler c;

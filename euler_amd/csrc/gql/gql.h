@@ -47,6 +47,9 @@ struct CompileOptions {
   bool fuse = true;
 };
 
+// REMOTE fusion pass of the distribute-mode optimizer (exposed for tests)
+void FuseRemoteNodes(DAGDef* dag);
+
 class Compiler {
  public:
   static Compiler& Get();

@@ -430,10 +430,6 @@ void need_f32(const torch::Tensor& t, const char* name) {
   TORCH_CHECK(t.scalar_type() == torch::kFloat32, name, " must be float32");
 }
 
-void need_numel(const torch::Tensor& t, int64_t n, const char* name) {
-  TORCH_CHECK(t.numel() == n, name, " must have ", n, " elements, got ", t.numel());
-}
-
 // sample_neighbor writing into a caller-provided int32 buffer (no allocation)
 void sample_neighbor_into(torch::Tensor indptr, torch::Tensor nbr, torch::Tensor cumw, int64_t num_rows,
                           int64_t num_types, int64_t type_mask, torch::Tensor nodes, int64_t count,
@@ -455,283 +451,6 @@ void sample_neighbor_into(torch::Tensor indptr, torch::Tensor nbr, torch::Tensor
                            rng.data_ptr<int64_t>(), static_cast<uint64_t>(stream_id), out.data_ptr<int32_t>(),
                            nullptr, nullptr, cur_stream()),
         "sample_neighbor_into");
-}
-
-void st_roots(torch::Tensor prob, torch::Tensor alias, torch::Tensor rng, int64_t stream_id, torch::Tensor labels,
-              torch::Tensor roots, torch::Tensor level1, torch::Tensor label_idx, torch::Tensor step) {
-  need_f32(prob, "prob");
-  need_i32(alias, "alias");
-  need_i64(rng, "rng");
-  need_cuda(labels, "labels");
-  TORCH_CHECK(labels.scalar_type() == torch::kInt16, "labels must be int16");
-  need_i32(roots, "roots");
-  need_i32(level1, "level1");
-  need_i32(label_idx, "label_idx");
-  need_i64(step, "step");
-  TORCH_CHECK(prob.numel() == alias.numel() && prob.numel() == labels.numel(), "population size mismatch");
-  const int64_t B = roots.numel();
-  need_numel(label_idx, B, "label_idx");
-  TORCH_CHECK(level1.numel() >= B, "level1 too small");
-  const c10::DeviceGuard g(roots.device());
-  check(eh_st_roots(prob.data_ptr<float>(), alias.data_ptr<int32_t>(), prob.numel(), static_cast<int>(B),
-                    rng.data_ptr<int64_t>(), static_cast<uint64_t>(stream_id),
-                    reinterpret_cast<const int16_t*>(labels.data_ptr()), roots.data_ptr<int32_t>(),
-                    level1.data_ptr<int32_t>() + (level1.numel() - B), label_idx.data_ptr<int32_t>(),
-                    step.data_ptr<int64_t>(), cur_stream()),
-        "st_roots");
-}
-
-// nbr_idx None: tree layout, the neighbours of output row m are input rows m*F .. m*F+F-1
-void st_sage_fwd(torch::Tensor x, torch::Tensor self_idx, c10::optional<torch::Tensor> nbr_idx, int64_t F,
-                 bool include_self, torch::Tensor W, torch::Tensor out, torch::Tensor a_kt,
-                 c10::optional<torch::Tensor> relu_mask, int64_t bm) {
-  need_bf16(x, "x");
-  need_i32(self_idx, "self_idx");
-  need_bf16(W, "W");
-  need_bf16(out, "out");
-  need_bf16(a_kt, "a_kt");
-  TORCH_CHECK(x.dim() == 2 && W.dim() == 2, "bad ranks");
-  const int64_t D = x.size(1), M = self_idx.numel(), H = W.size(0);
-  if (nbr_idx.has_value()) {
-    need_i32(*nbr_idx, "nbr_idx");
-    TORCH_CHECK(nbr_idx->dim() == 2 && nbr_idx->size(0) == M && nbr_idx->size(1) == F,
-                "nbr_idx must be [M, F]");
-  } else {
-    TORCH_CHECK(M * F <= x.size(0), "tree layout needs M*F input rows");
-  }
-  TORCH_CHECK(W.size(1) == 2 * D, "W must be [H, 2D]");
-  need_numel(out, M * H, "out");
-  need_numel(a_kt, M * 2 * D, "a_kt");
-  if (relu_mask.has_value()) {
-    need_cuda(*relu_mask, "relu_mask");
-    TORCH_CHECK(relu_mask->scalar_type() == torch::kInt32, "relu_mask must be int32 (bit words)");
-    need_numel(*relu_mask, (M / 32) * H, "relu_mask");
-  }
-  TORCH_CHECK(M % 32 == 0 && D % 16 == 0 && H % 64 == 0, "st_sage_fwd needs M%32, D%16, H%64 == 0");
-  const float inv = 1.f / static_cast<float>(std::max<int64_t>(F + (include_self ? 1 : 0), 1));
-  const c10::DeviceGuard g(x.device());
-  check(eh_st_sage_fwd(x.data_ptr(), static_cast<int>(D), self_idx.data_ptr<int32_t>(),
-                       nbr_idx.has_value() ? nbr_idx->data_ptr<int32_t>() : nullptr, static_cast<int>(F),
-                       include_self ? 1 : 0, inv, W.data_ptr(),
-                       static_cast<int>(H), M, out.data_ptr(), a_kt.data_ptr(),
-                       relu_mask.has_value() ? reinterpret_cast<uint32_t*>(relu_mask->data_ptr()) : nullptr,
-                       static_cast<int>(bm), cur_stream()),
-        "st_sage_fwd");
-}
-
-void st_tree_mean(torch::Tensor h0, int64_t B, int64_t F1, bool include_self, torch::Tensor A1) {
-  need_bf16(h0, "h0");
-  need_bf16(A1, "A1");
-  const int64_t H = h0.size(1);
-  TORCH_CHECK(h0.size(0) == B * (F1 + 1), "h0 rows must be B*(F1+1)");
-  need_numel(A1, B * 2 * H, "A1");
-  const float inv = 1.f / static_cast<float>(F1 + (include_self ? 1 : 0));
-  const c10::DeviceGuard g(h0.device());
-  check(eh_st_tree_mean(h0.data_ptr(), static_cast<int>(H), B, static_cast<int>(F1), include_self ? 1 : 0, inv,
-                        A1.data_ptr(), cur_stream()),
-        "st_tree_mean");
-}
-
-void st_head(torch::Tensor A1, torch::Tensor W1b, torch::Tensor Wfc, torch::Tensor WfcT, torch::Tensor bfc,
-             torch::Tensor Wout, torch::Tensor WoutT, torch::Tensor W1T, torch::Tensor label_idx, torch::Tensor A1_kt,
-             torch::Tensor h1_kt, torch::Tensor emb_kt, torch::Tensor dlog_kt, torch::Tensor demb_kt,
-             torch::Tensor g1_kt, torch::Tensor dA1, torch::Tensor dbfc, torch::Tensor loss_acc,
-             c10::optional<torch::Tensor> prof) {
-  for (auto* p : {&A1, &W1b, &Wfc, &WfcT, &Wout, &WoutT, &W1T, &A1_kt, &h1_kt, &emb_kt, &dlog_kt, &demb_kt, &g1_kt})
-    need_bf16(*p, "st_head bf16 operand");
-  need_f32(bfc, "bfc");
-  need_f32(dA1, "dA1");
-  need_f32(dbfc, "dbfc");
-  need_f32(loss_acc, "loss_acc");
-  need_i32(label_idx, "label_idx");
-  const int64_t B = A1.size(0), H = A1.size(1) / 2, C = Wout.size(0);
-  need_numel(W1b, H * 2 * H, "W1b");
-  need_numel(A1_kt, B * 2 * H, "A1_kt");
-  need_numel(Wfc, H * H, "Wfc");
-  need_numel(WfcT, H * H, "WfcT");
-  need_numel(bfc, H, "bfc");
-  need_numel(dbfc, H, "dbfc");
-  TORCH_CHECK(Wout.size(1) == H, "Wout must be [C, H]");
-  need_numel(WoutT, C * H, "WoutT");
-  need_numel(W1T, 2 * H * H, "W1T");
-  need_numel(label_idx, B, "label_idx");
-  need_numel(h1_kt, B * H, "h1_kt");
-  need_numel(emb_kt, B * H, "emb_kt");
-  need_numel(dlog_kt, B * C, "dlog_kt");
-  need_numel(demb_kt, B * H, "demb_kt");
-  need_numel(g1_kt, B * H, "g1_kt");
-  need_numel(dA1, B * 2 * H, "dA1");
-  long long* prof_p = nullptr;
-  if (prof.has_value()) {
-    TORCH_CHECK(prof->scalar_type() == torch::kInt64 && prof->is_contiguous() && prof->is_cuda(),
-                "prof must be a contiguous int64 device tensor");
-    TORCH_CHECK(B % kStHeadRows == 0, "B must be a multiple of the head block");
-    need_numel(*prof, (B / kStHeadRows) * 8, "prof");
-    prof_p = reinterpret_cast<long long*>(prof->data_ptr<int64_t>());
-  }
-  const c10::DeviceGuard g(A1.device());
-  check(eh_st_head(A1.data_ptr(), static_cast<int>(B), static_cast<int>(H), static_cast<int>(C), W1b.data_ptr(),
-                   Wfc.data_ptr(), WfcT.data_ptr(), bfc.data_ptr<float>(), Wout.data_ptr(), WoutT.data_ptr(),
-                   W1T.data_ptr(), label_idx.data_ptr<int32_t>(), 1.f / static_cast<float>(B * C), A1_kt.data_ptr(),
-                   h1_kt.data_ptr(), emb_kt.data_ptr(), dlog_kt.data_ptr(), demb_kt.data_ptr(), g1_kt.data_ptr(),
-                   dA1.data_ptr<float>(), dbfc.data_ptr<float>(), loss_acc.data_ptr<float>(), prof_p, cur_stream()),
-        "st_head");
-}
-
-void st_route(torch::Tensor dA1, int64_t F1, bool include_self, torch::Tensor mask, torch::Tensor g0_kt) {
-  need_f32(dA1, "dA1");
-  TORCH_CHECK(mask.scalar_type() == torch::kInt32 && mask.is_contiguous(), "mask must be contiguous int32");
-  need_bf16(g0_kt, "g0_kt");
-  const int64_t B = dA1.size(0), H = dA1.size(1) / 2, M1 = B * (F1 + 1);
-  TORCH_CHECK(dA1.size(1) == 2 * H && H % 8 == 0, "dA1 must be [B, 2H] with H % 8 == 0");
-  TORCH_CHECK(M1 % 32 == 0, "B*(F1+1) must be a multiple of 32");
-  need_numel(mask, (M1 / 32) * H, "mask");
-  need_numel(g0_kt, M1 * H, "g0_kt");
-  const float inv = 1.f / static_cast<float>(F1 + (include_self ? 1 : 0));
-  const c10::DeviceGuard g(dA1.device());
-  check(eh_st_route(dA1.data_ptr<float>(), static_cast<int>(H), B * F1, static_cast<int>(F1), include_self ? 1 : 0,
-                    inv, reinterpret_cast<const uint32_t*>(mask.data_ptr<int32_t>()), M1, g0_kt.data_ptr(),
-                    cur_stream()),
-        "st_route");
-}
-
-// problems: (G_kt [M*P], X_kt [M*Q], part fp32 [S*P*Q], P, Q, M, kps)
-// route_* (optional): problem 0 is the outer SAGE layer in route mode; its G (= g0) is
-// built in-kernel from route_dA1 [B][2P], the ReLU mask bits [M/32][P] and the tree layout
-void st_dw(std::vector<c10::optional<torch::Tensor>> G, std::vector<torch::Tensor> X,
-           std::vector<torch::Tensor> part, std::vector<int64_t> P, std::vector<int64_t> Q, std::vector<int64_t> M,
-           std::vector<int64_t> kps, c10::optional<torch::Tensor> route_mask,
-           c10::optional<torch::Tensor> route_dA1, int64_t route_F1, bool route_include_self) {
-  const size_t n = G.size();
-  TORCH_CHECK(n >= 1 && n <= 4 && X.size() == n && part.size() == n && P.size() == n && Q.size() == n &&
-                  M.size() == n && kps.size() == n,
-              "st_dw: 1..4 problems with matching argument lists");
-  const bool route = route_mask.has_value();
-  int64_t nb_rows = 0;
-  if (route) {
-    TORCH_CHECK(route_dA1.has_value(), "route mode needs route_dA1");
-    need_cuda(*route_mask, "route_mask");
-    TORCH_CHECK(route_mask->scalar_type() == torch::kInt32, "route_mask must be int32 bit words");
-    need_f32(*route_dA1, "route_dA1");
-    need_numel(*route_mask, (M[0] / 32) * P[0], "route_mask");
-    TORCH_CHECK(route_dA1->dim() == 2 && route_dA1->size(1) == 2 * P[0], "route_dA1 must be [B, 2P]");
-    TORCH_CHECK(route_F1 >= 2, "route mode needs F1 >= 2");
-    TORCH_CHECK(M[0] == route_dA1->size(0) * (route_F1 + 1), "M must be B*(F1+1) in route mode");
-    nb_rows = route_dA1->size(0) * route_F1;
-  }
-  const void* gp[4];
-  const void* xp[4];
-  float* pp[4];
-  int pi[4], qi[4], ki[4];
-  int64_t mi[4];
-  for (size_t i = 0; i < n; ++i) {
-    const bool routed = route && i == 0;
-    if (!routed) {
-      TORCH_CHECK(G[i].has_value(), "G_kt missing");
-      need_bf16(*G[i], "G_kt");
-      need_numel(*G[i], M[i] * P[i], "G_kt");
-    }
-    need_bf16(X[i], "X_kt");
-    need_f32(part[i], "part");
-    need_numel(X[i], M[i] * Q[i], "X_kt");
-    const int64_t S = (M[i] / 32 + kps[i] - 1) / kps[i];
-    TORCH_CHECK(part[i].numel() >= S * P[i] * Q[i], "part buffer too small");
-    gp[i] = routed ? nullptr : G[i]->data_ptr();
-    xp[i] = X[i].data_ptr();
-    pp[i] = part[i].data_ptr<float>();
-    pi[i] = static_cast<int>(P[i]);
-    qi[i] = static_cast<int>(Q[i]);
-    mi[i] = M[i];
-    ki[i] = static_cast<int>(kps[i]);
-  }
-  const float inv = 1.f / static_cast<float>(route_F1 + (route_include_self ? 1 : 0));
-  const c10::DeviceGuard g(X[0].device());
-  check(eh_st_dw(static_cast<int>(n), gp, xp, pp, pi, qi, mi, ki,
-                 route ? reinterpret_cast<const uint32_t*>(route_mask->data_ptr()) : nullptr,
-                 route ? route_dA1->data_ptr<float>() : nullptr, nb_rows, static_cast<int>(route_F1),
-                 route_include_self ? 1 : 0, inv, cur_stream()),
-        "st_dw");
-}
-
-void st_reduce(std::vector<torch::Tensor> part, std::vector<torch::Tensor> out, std::vector<int64_t> S) {
-  const size_t n = part.size();
-  TORCH_CHECK(n >= 1 && n <= 4 && out.size() == n && S.size() == n, "st_reduce: 1..4 problems");
-  const float* pp[4];
-  float* op[4];
-  int64_t ne[4];
-  int si[4];
-  for (size_t i = 0; i < n; ++i) {
-    need_f32(part[i], "part");
-    need_f32(out[i], "out");
-    TORCH_CHECK(part[i].numel() >= S[i] * out[i].numel(), "part buffer too small");
-    pp[i] = part[i].data_ptr<float>();
-    op[i] = out[i].data_ptr<float>();
-    ne[i] = out[i].numel();
-    si[i] = static_cast<int>(S[i]);
-  }
-  const c10::DeviceGuard g(out[0].device());
-  check(eh_st_reduce(static_cast<int>(n), pp, op, ne, si, cur_stream()), "st_reduce");
-}
-
-struct ShadowArgs {
-  int count = 0;
-  int64_t off[6], n[6];
-  int cols[6];
-  void* sh[6];
-  void* shT[6];
-};
-
-ShadowArgs make_shadows(const torch::Tensor& p, const std::vector<int64_t>& off, const std::vector<int64_t>& cols,
-                        const std::vector<torch::Tensor>& sh, const std::vector<c10::optional<torch::Tensor>>& shT) {
-  ShadowArgs a;
-  TORCH_CHECK(off.size() <= 6 && off.size() == cols.size() && off.size() == sh.size() && off.size() == shT.size(),
-              "shadow lists must match, <= 6 segments");
-  a.count = static_cast<int>(off.size());
-  for (size_t i = 0; i < off.size(); ++i) {
-    need_bf16(sh[i], "shadow");
-    TORCH_CHECK(off[i] >= 0 && off[i] + sh[i].numel() <= p.numel(), "shadow segment out of range");
-    TORCH_CHECK(cols[i] > 0 && sh[i].numel() % cols[i] == 0, "shadow cols must divide the segment");
-    a.off[i] = off[i];
-    a.n[i] = sh[i].numel();
-    a.cols[i] = static_cast<int>(cols[i]);
-    a.sh[i] = sh[i].data_ptr();
-    a.shT[i] = nullptr;
-    if (shT[i].has_value()) {
-      need_bf16(*shT[i], "shadowT");
-      need_numel(*shT[i], sh[i].numel(), "shadowT");
-      a.shT[i] = shT[i]->data_ptr();
-    }
-  }
-  return a;
-}
-
-void st_adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, torch::Tensor step, double lr,
-             double b1, double b2, double eps, double wd, double grad_scale, std::vector<int64_t> sh_off,
-             std::vector<int64_t> sh_cols, std::vector<torch::Tensor> sh, std::vector<c10::optional<torch::Tensor>> shT,
-             int64_t zero_off, int64_t zero_n, torch::Tensor loss_acc, torch::Tensor loss_out, torch::Tensor rng) {
-  for (auto* t : {&p, &g, &m, &v, &loss_acc, &loss_out}) need_f32(*t, "st_adam fp32 operand");
-  need_i64(step, "step");
-  need_i64(rng, "rng");
-  const int64_t n = p.numel();
-  TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "flat buffers must match");
-  TORCH_CHECK(zero_off >= 0 && zero_off + zero_n <= n, "zero range out of bounds");
-  ShadowArgs a = make_shadows(p, sh_off, sh_cols, sh, shT);
-  const c10::DeviceGuard gd(p.device());
-  check(eh_st_adam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), n,
-                   step.data_ptr<int64_t>(), static_cast<float>(lr), static_cast<float>(b1), static_cast<float>(b2),
-                   static_cast<float>(eps), static_cast<float>(wd), static_cast<float>(grad_scale), a.count, a.off,
-                   a.n, a.cols, a.sh, a.shT, zero_off, zero_n, loss_acc.data_ptr<float>(),
-                   loss_out.data_ptr<float>(), rng.data_ptr<int64_t>(), cur_stream()),
-        "st_adam");
-}
-
-void st_shadow(torch::Tensor p, std::vector<int64_t> sh_off, std::vector<int64_t> sh_cols,
-               std::vector<torch::Tensor> sh, std::vector<c10::optional<torch::Tensor>> shT) {
-  need_f32(p, "p");
-  ShadowArgs a = make_shadows(p, sh_off, sh_cols, sh, shT);
-  const c10::DeviceGuard gd(p.device());
-  check(eh_st_shadow(p.data_ptr<float>(), p.numel(), a.count, a.off, a.n, a.cols, a.sh, a.shT, cur_stream()),
-        "st_shadow");
 }
 
 }  // namespace
@@ -768,17 +487,4 @@ PYBIND11_MODULE(_hip_ops, m) {
   m.def("flat_optim_", &flat_optim_);
   m.def("sparse_optim_", &sparse_optim_);
   m.def("sample_neighbor_into", &sample_neighbor_into);
-  m.def("st_roots", &st_roots);
-  m.def("st_sage_fwd", &st_sage_fwd);
-  m.attr("st_head_rows") = kStHeadRows;
-  m.def("st_head", &st_head, "fused head fwd+bwd", py::arg("A1"), py::arg("W1b"), py::arg("Wfc"), py::arg("WfcT"),
-        py::arg("bfc"), py::arg("Wout"), py::arg("WoutT"), py::arg("W1T"), py::arg("label_idx"), py::arg("A1_kt"),
-        py::arg("h1_kt"), py::arg("emb_kt"), py::arg("dlog_kt"), py::arg("demb_kt"), py::arg("g1_kt"), py::arg("dA1"),
-        py::arg("dbfc"), py::arg("loss_acc"), py::arg("prof") = py::none());
-  m.def("st_tree_mean", &st_tree_mean);
-  m.def("st_route", &st_route);
-  m.def("st_dw", &st_dw);
-  m.def("st_reduce", &st_reduce);
-  m.def("st_adam", &st_adam);
-  m.def("st_shadow", &st_shadow);
 }

@@ -150,6 +150,28 @@ class TreePlan {
     ok(eh_tr_opt(&a, static_cast<int>(mode), stream()), "tr_opt");
   }
 
+  // split-K reduce (mode 0) of a subset of the flat segments (data-parallel buckets);
+  // head_stats: this launch also reduces the head's loss / F1 partials
+  void opt_segments(int64_t mode, std::vector<int64_t> segs, bool head_stats) {
+    TORCH_CHECK(mode == 0, "opt_segments: only the reduce (mode 0) runs on a segment subset");
+    TORCH_CHECK(!segs.empty() && (int64_t)segs.size() <= opt_.nseg, "opt_segments: bad segment list");
+    const c10::DeviceGuard g(dev_);
+    TrOptArgs a = opt_;
+    int blk = 0, n = 0;
+    for (int64_t k : segs) {
+      TORCH_CHECK(k >= 0 && k < opt_.nseg, "opt_segments: segment index out of range");
+      TrSeg s = opt_.seg[k];
+      s.blk0 = blk;
+      blk += s.cols > 0 ? (s.rows / 8) * (s.cols / 32) : static_cast<int>((s.n + 255) / 256);
+      a.seg[n++] = s;
+    }
+    a.nseg = n;
+    a.nblk = blk;
+    a.nsample = 0;
+    if (!head_stats) a.nhead = 0;
+    ok(eh_tr_opt(&a, 0, stream()), "tr_opt(segments)");
+  }
+
   int64_t fwd_blocks() const { return fwd0_.M / bm0_; }
   void set_lr(double lr) { opt_.lr = static_cast<float>(lr); }
   // bf16 gradient buffer for the data-parallel hand-off (None: fp32 grad)
@@ -548,6 +570,7 @@ void register_tree_ops(py::module& m) {
       .def("bwd", &TreePlan::bwd)
       .def("dw", &TreePlan::dw)
       .def("opt", &TreePlan::opt, py::arg("mode"), py::arg("grad_scale") = 1.0, py::arg("with_sample") = false)
+      .def("opt_segments", &TreePlan::opt_segments, py::arg("mode"), py::arg("segs"), py::arg("head_stats"))
       .def("set_lr", &TreePlan::set_lr)
       .def("set_grad16", &TreePlan::set_grad16, py::arg("g16"))
       .def("num_problems", &TreePlan::num_problems)

@@ -51,36 +51,6 @@ hipError_t eh_spmm_csr(const int64_t* indptr, const int64_t* col, const float* w
 }
 
 extern "C" {
-// sage_train.hip (fused GraphSAGE training step)
-hipError_t eh_st_roots(const float* prob, const int32_t* alias, int64_t pop, int B, const int64_t* rng,
-                       uint64_t stream_id, const int16_t* labels, int32_t* roots, int32_t* level1_tail,
-                       int32_t* label_idx, int64_t* step, hipStream_t s);
-hipError_t eh_st_sage_fwd(const void* x, int D, const int32_t* self_idx, const int32_t* nbr_idx, int F,
-                          int include_self, float inv_cnt, const void* W, int H, int64_t M, void* out, void* a_kt,
-                          uint32_t* relu_mask, int bm, hipStream_t s);
-hipError_t eh_st_tree_mean(const void* h0, int H, int64_t B, int F1, int include_self, float inv_cnt, void* A1,
-                           hipStream_t s);
-// rows per block of the fused head kernel (sage_train.hip)
-constexpr int kStHeadRows = 16;
-hipError_t eh_st_head(const void* A1, int B, int H, int C, const void* W1b, const void* Wfc, const void* WfcT,
-                      const float* bfc, const void* Wout, const void* WoutT, const void* W1T, const int32_t* label_idx,
-                      float inv_scale, void* A1_kt, void* h1_kt, void* emb_kt, void* dlog_kt, void* demb_kt,
-                      void* g1_kt, float* dA1, float* dbfc, float* loss_acc, long long* prof, hipStream_t s);
-hipError_t eh_st_route(const float* dA1, int H, int64_t nb_rows, int F1, int include_self, float inv_cnt,
-                       const uint32_t* mask, int64_t M1, void* g0_kt, hipStream_t s);
-hipError_t eh_st_dw(int n, const void* const* G, const void* const* X, float* const* part, const int* P,
-                    const int* Q, const int64_t* M, const int* kps, const uint32_t* route_mask,
-                    const float* route_dA1, int64_t nb_rows, int F1, int include_self, float inv_cnt, hipStream_t s);
-hipError_t eh_st_reduce(int n, const float* const* part, float* const* out, const int64_t* numel, const int* S,
-                        hipStream_t s);
-hipError_t eh_st_adam(float* p, float* g, float* m, float* v, int64_t n, const int64_t* step, float lr, float b1,
-                      float b2, float eps, float wd, float grad_scale, int sh_count, const int64_t* sh_off,
-                      const int64_t* sh_n, const int* sh_cols, void* const* sh_ptr, void* const* shT_ptr,
-                      int64_t zero_off, int64_t zero_n, float* loss_acc, float* loss_out, int64_t* rng,
-                      hipStream_t s);
-hipError_t eh_st_shadow(const float* p, int64_t n, int sh_count, const int64_t* sh_off, const int64_t* sh_n,
-                        const int* sh_cols, void* const* sh_ptr, void* const* shT_ptr, hipStream_t s);
-
 // gat.hip (K5: fused multi-head GAT edge-softmax + aggregation)
 int eh_gat_supported(int H, int C, int is_bf16);
 // order / corder: optional visiting order of the CSR / CSC rows (nullptr = identity);

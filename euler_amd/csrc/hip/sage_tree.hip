@@ -1288,8 +1288,9 @@ __global__ __launch_bounds__(256) void tr_opt_kernel(TrOptArgs a) {
     tr_sample_block<256>(a.smp, b - a.nblk, node_s);
     return;
   }
-  if (b == 0 && tid < 64 && MODE != 3) {
-    // head statistics: reduce (modes 0/2) the per-block partials; hand the loss over (1/2)
+  if (b == 0 && tid < 64 && MODE != 3 && a.nhead > 0) {
+    // head statistics: reduce (modes 0/2) the per-block partials; hand the loss over (1/2);
+    // nhead == 0: a segment-subset reduce launch that leaves them to another launch
     if (MODE != 1) {
       float v[4] = {0.f, 0.f, 0.f, 0.f};
       for (int k = tid; k < a.nhead; k += 64)
@@ -1594,7 +1595,7 @@ hipError_t eh_tr_dw(TrDwLaunch* L, hipStream_t s) {
 hipError_t eh_tr_opt(const TrOptArgs* a, int mode, hipStream_t s) {
   if (a->nseg < 1 || a->nseg > kTrMaxSegs || a->nblk < 1) return hipErrorInvalidValue;
   if (!a->p || !a->g || !a->m || !a->v || !a->step || !a->loss_acc || !a->loss_out || !a->head_part ||
-      a->nhead < 1)
+      a->nhead < 0 || (a->nhead == 0 && mode != 0))
     return hipErrorInvalidValue;
   int blk = 0;
   for (int i = 0; i < a->nseg; ++i) {

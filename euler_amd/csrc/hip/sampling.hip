@@ -143,11 +143,14 @@ __global__ __launch_bounds__(256) void random_walk_kernel(
       if (biased) {
         const bool has_prev = prev >= 0 && prev < num_rows;
         float tot = 0.f;
-        for (int pass = 0; pass < 2 && nxt == default_row; ++pass) {
+        // `picked` (not nxt == default_row) marks a draw: the default may be a valid row
+        bool picked = false;
+        for (int pass = 0; pass < 2 && !picked; ++pass) {
           const float target = pass == 0 ? 0.f : u01(r[0]) * tot;
           float acc = 0.f;
           int32_t last = default_row;
-          for (int t = 0; t < num_types; ++t) {
+          bool have_last = false;
+          for (int t = 0; t < num_types && !picked; ++t) {
             if (!((mask >> t) & 1u)) continue;
             const int64_t a = indptr[base + t], b = indptr[base + t + 1];
             for (int64_t e = a; e < b; ++e) {
@@ -156,16 +159,22 @@ __global__ __launch_bounds__(256) void random_walk_kernel(
               if (c == prev) w *= inv_p;
               else if (!(has_prev && prev_mask && rw_in_row(indptr, nbr, num_types, prev_mask, prev, c))) w *= inv_q;
               acc += w;
-              if (w > 0.f) last = c;
+              if (w > 0.f) {
+                last = c;
+                have_last = true;
+              }
               if (pass == 1 && acc > target) {
                 nxt = c;
+                picked = true;
                 break;
               }
             }
-            if (nxt != default_row) break;
           }
           if (pass == 0) tot = acc;
-          if (pass == 1 && nxt == default_row) nxt = last;  // rounding at the top end
+          if (pass == 1 && !picked && have_last) {  // rounding at the top end
+            nxt = last;
+            picked = true;
+          }
           if (pass == 0 && !(tot > 0.f)) break;
         }
       } else {

@@ -1184,10 +1184,7 @@ RpcClients::RpcClients(std::map<int, std::vector<Endpoint>> shards, const Client
 }
 
 RpcClients::~RpcClients() {
-  pool_.reset();
-  for (auto& s : shards_)
-    for (auto& h : *std::atomic_load(&s))
-      for (auto& c : h->idle) CloseChan(&c);
+  pool_.reset();  // in-flight calls finish first; the Host destructors close the pooled channels
 }
 
 void RpcClients::UpdateShard(int shard, const std::vector<Endpoint>& eps) {
@@ -1461,6 +1458,21 @@ void QueryProxy::WatchRegistry(std::string spec, double ttl, double period) {
       rc->UpdateShard(kv.first, eps);  // a shard with no live entry keeps its last replicas
     }
   }
+}
+
+Status QueryProxy::SetReplicas(int shard, const std::vector<std::string>& endpoints) {
+  if (mode_ != "remote" && mode_ != "graph_partition") return Status::InvalidArgument("not a remote session");
+  std::vector<Endpoint> eps;
+  for (const auto& e : endpoints) {
+    const size_t c = e.rfind(':');
+    if (c == std::string::npos) return Status::InvalidArgument("endpoint must be host:port: " + e);
+    Endpoint ep;
+    ep.host = e.substr(0, c);
+    ep.port = std::atoi(e.c_str() + c + 1);
+    eps.push_back(ep);
+  }
+  static_cast<RpcClients*>(clients_.get())->UpdateShard(shard, eps);
+  return Status::OK();
 }
 
 std::map<int, std::vector<std::string>> QueryProxy::Endpoints() const {

@@ -206,11 +206,17 @@ class RpcClients : public RemoteClients {
     char* shm = nullptr;
     size_t cap = 0;
   };
+  // A replica.  Dropped from the routing set by UpdateShard, it lives on while a call
+  // holds a snapshot of the old list (that call still returns its channel here), and
+  // its destructor closes every pooled channel (socket + shared region).
   struct Host {
     Endpoint ep;
     std::mutex mu;
     std::vector<Chan> idle;  // pooled connected sockets
     double bad_until = 0;
+    ~Host() {
+      for (auto& c : idle) CloseChan(&c);
+    }
   };
   static Chan OpenChan(const Endpoint& ep, int timeout_ms);
   static void CloseChan(Chan* c);
@@ -253,6 +259,8 @@ class QueryProxy {
   // run a DAG in-process against a shard env (used by the local fast paths)
   static std::unique_ptr<EngineEnv> MakeEnv(Graph* g, IndexManager* idx, int shard_num);
   // remote mode: current replicas per shard as the client routes to them
+  // replace a shard's replica set (what the registry watch does; remote mode only)
+  Status SetReplicas(int shard, const std::vector<std::string>& endpoints);
   std::map<int, std::vector<std::string>> Endpoints() const;
   ~QueryProxy();
 

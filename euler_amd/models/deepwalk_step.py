@@ -55,7 +55,7 @@ def _pair_positions(walk_len, left, right):
 class DeepWalkTrainer:
     def __init__(self, graph, num_nodes, dim=128, walk_len=3, left_win_size=1, right_win_size=1, num_negs=5,
                  batch_size=1024, lr=0.01, optimizer="adam", group=None, seed=0, force_comm=False, static=False,
-                 wire_dtype="bf16"):
+                 wire_dtype="bf16", overflow_check_every=200):
         self.graph = graph
         self.num_nodes = int(num_nodes)
         self.pad = self.num_nodes  # rows: num_nodes + 1 (pad row like the reference's max_id + 1)
@@ -74,6 +74,10 @@ class DeepWalkTrainer:
         self.loss = torch.zeros((), device=dev)
         self.static = bool(static)
         self.hip_graph = None
+        # static mode: read the exchange's device overflow flag every N steps (one host
+        # sync) so a dropped id fails loudly instead of silently training less
+        self.overflow_check_every = int(overflow_check_every)
+        self.steps_done = 0
 
     def _gather(self, rows, inv):
         if use_hip(rows, inv):
@@ -93,6 +97,9 @@ class DeepWalkTrainer:
         return src, pos, negs
 
     def step(self):
+        self.steps_done += 1
+        if self.static and self.overflow_check_every > 0 and self.steps_done % self.overflow_check_every == 0:
+            self.table.check_overflow()
         if self.hip_graph is not None:
             self.hip_graph.replay()
             return self.loss
@@ -144,22 +151,22 @@ class DeepWalkTrainer:
             tab.apply_sgns(1, ptr_c, lst_c, coef, K, rt, None, inv_t, rows_c_id, inc_step=False)
         else:
             ids = torch.cat([u_t, rows_c_id])
-            rows, h = tab.lookup_static(ids)
+            # rows [W*C + 1, D]: the extra zero row is the trash slot of ids dropped by a
+            # capacity overflow (pos = W*C), so they never alias a live slot
+            rows, h = tab.lookup_static(ids, trash_row=True)
             n = rows.shape[0]
-            # a dropped id (overflow flag raised) points at the last slot: wrong but in bounds
-            slot = h.pos.clamp(max=n - 1)
-            tinv = slot[inv_t]
-            cinv = slot[u_t.numel() + inv_c]
+            tinv = h.pos[inv_t]
+            cinv = h.pos[u_t.numel() + inv_c]
             coef, loss_rows = gnn_ops.sgns_fwd_idx(rows, None, tinv, rows, None, cinv, K, gscale)
             ptr_t, lst_t = gnn_ops.occ_csr(tinv, n)
             ptr_c, lst_c = gnn_ops.occ_csr(cinv, n)
-            # every occupied slot is written by exactly one side (target and context ids
+            # every occupied live slot is written by exactly one side (target and context ids
             # live in different table halves); empty slots (local row -1) are skipped by the
-            # update, so no 4*D*W*C-byte zero fill per step
+            # update, so no 4*D*W*C-byte zero fill per step; the trash row is not applied
             g = torch.empty_like(rows)
             gnn_ops.sgns_grad(0, ptr_t, lst_t, coef, K, rows, None, cinv, inv_self=tinv, out=g)
             gnn_ops.sgns_grad(1, ptr_c, lst_c, coef, K, rows, None, tinv, inv_self=cinv, out=g)
-            tab.apply_static(h, g)
+            tab.apply_static(h, g[: n - 1])
         self.loss = loss_rows.sum() * gscale
         return self.loss
 

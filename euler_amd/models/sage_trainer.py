@@ -418,34 +418,70 @@ class SageTrainer:
     def optimizer_step(self, grad_scale: float = 1.0):
         self.plan.opt(1, float(grad_scale))
 
-    def step(self, grad_sync=None):
-        """One training step.  ``grad_sync(grad)`` (e.g. an RCCL all-reduce) runs between
-        the gradient reduce and the optimizer; None = single process (fused reduce +
-        optimizer launch).
+    def grad_buckets(self):
+        """(name, start, end) of the data-parallel gradient buckets in the flat layout, in
+        the order ``grad_sync`` receives them: "head" = the last conv, fc and out_fc (their
+        dW needs only the head's outputs), then "routed" = the inner convs, whose dW (the
+        tree-routed split-K problems, the longest launch of the backward) it overlaps."""
+        o = self.offsets
+        return [("head", o[self.L - 1], o[-1]), ("routed", 0, o[self.L - 1])]
 
-        One stream, no forks (a hipGraph branch join costs more than the work it would
-        overlap): fwd -> head -> [bwd] -> every dW in one launch -> optimizer.  The head
-        launch also carries the sampler of the NEXT step's batch in extra blocks, on the
-        CUs the head's B/16 blocks leave idle (sampling reads only the graph and the RNG
-        counter the forward advanced; the head reads the forward's copy of the roots), so
-        the sampler's dependent-load chain is off the critical path."""
+    def step(self, grad_sync=None):
+        """One training step.  ``grad_sync(bucket)`` (e.g. an in-place RCCL all-reduce)
+        is called once per gradient bucket (:meth:`grad_buckets`, in that order) and
+        returns the scale applied to the summed gradient (1 / world); None = single
+        process (fused reduce + optimizer launch).
+
+        Single process: one stream, no forks (a hipGraph branch join costs more than the
+        work it would overlap): fwd -> head -> [bwd] -> every dW in one launch ->
+        optimizer.  The head launch also carries the sampler of the NEXT step's batch in
+        extra blocks, on the CUs the head's B/16 blocks leave idle (sampling reads only the
+        graph and the RNG counter the forward advanced; the head reads the forward's copy
+        of the roots), so the sampler's dependent-load chain is off the critical path.
+
+        Data parallel: the dW of the "head" bucket (last conv, fc, out_fc) runs on a side
+        stream next to the routed inner-layer dW; its split-K reduce and all-reduce then
+        overlap the routed dW, and only the routed bucket's (smaller) all-reduce is on the
+        critical path.  Both collectives are issued on the side stream in bucket order, so
+        every rank enqueues them identically."""
         self.step_count += 1
         if not self.on_gpu:
-            return self._cpu_step()
+            return self._cpu_step(grad_sync)
         p = self.plan
         self._prime()
         p.fwd()
         p.head(None, True)
         p.bwd()
-        p.dw(self._dw_all)
         if grad_sync is None:
+            p.dw(self._dw_all)
             p.opt(2)
         else:
-            p.opt(0)
-            g16 = getattr(self, "grad16", None)
-            scale = grad_sync(self.grad if g16 is None else g16)
-            p.opt(1, 1.0 if scale is None else float(scale))
+            self._dist_backward(grad_sync)
         self._primed = True
+
+    def _dist_backward(self, grad_sync):
+        p = self.plan
+        if not hasattr(self, "_comm_stream"):
+            self._comm_stream = torch.cuda.Stream(device=self.device)
+            nseg = self.L + 3
+            self._segs_head = list(range(self.L - 1, nseg))
+            self._segs_routed = list(range(0, self.L - 1))
+        g = self.grad if getattr(self, "grad16", None) is None else self.grad16
+        (_, a0, a1), (_, b0, b1) = self.grad_buckets()
+        main, side = torch.cuda.current_stream(self.device), self._comm_stream
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            p.dw(p.problems(False))
+            p.opt_segments(0, self._segs_head, True)
+            scale = grad_sync(g[a0:a1])
+        if self._segs_routed:
+            p.dw(p.problems(True))
+            p.opt_segments(0, self._segs_routed, False)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                grad_sync(g[b0:b1])
+        main.wait_stream(side)
+        p.opt(1, 1.0 if scale is None else float(scale))
 
     def plan_launches(self):
         """(name, callable) of every launch of one pipelined step, for per-kernel timing"""
@@ -488,6 +524,7 @@ class SageTrainer:
         half the bytes; an 8-rank all-reduce of this ~1 MB gradient is latency/bandwidth
         bound on the critical path of an ~80 us step)."""
         if not self.on_gpu:
+            self.set_grad_sync_dtype_cpu(dtype)
             return
         if dtype in (torch.bfloat16, "bf16", "bfloat16"):
             self.grad16 = torch.zeros(self.grad.numel(), dtype=torch.bfloat16, device=self.device)
@@ -593,7 +630,11 @@ class SageTrainer:
         """logical view of :attr:`grad` after :meth:`forward_backward` (GPU)"""
         return self._unpack(self.grad)
 
-    def _cpu_step(self):
+    def set_grad_sync_dtype_cpu(self, dtype):
+        self._cpu_sync_bf16 = dtype in (torch.bfloat16, "bf16", "bfloat16")
+
+    def _cpu_forward_backward(self):
+        """fp32 autograd forward + backward of a fresh batch: p.grad of every parameter"""
         roots, nodes, leaf = self._cpu_sample()
         self._cpu_samples = (roots, nodes, leaf)
         P = self._cpu_params
@@ -608,10 +649,35 @@ class SageTrainer:
             self._cpu_counts[0] += int((pred & pos).sum())
             self._cpu_counts[1] += int((pred & ~pos).sum())
             self._cpu_counts[2] += int((~pred & pos).sum())
+        self.graph.rng[1] += 1
+        return loss.detach()
+
+    def _cpu_grad_sync(self, grad_sync):
+        """the GPU path's data-parallel hand-off on the CPU twin: the gradients in the flat
+        (logical) parameter order, the same buckets in the same order, fp32 or bf16"""
+        names = list(self._shapes)
+        flat = torch.cat([self._cpu_params[k].grad.reshape(-1) for k in names])
+        cut = sum(self._cpu_params[k].numel() for k in names[: 2 * (self.L - 1)])  # routed convs first
+        buf = flat.to(torch.bfloat16) if getattr(self, "_cpu_sync_bf16", False) else flat
+        scale = grad_sync(buf[cut:])
+        if cut:
+            grad_sync(buf[:cut])
+        flat = buf.float()
+        o = 0
+        for k in names:
+            n = self._cpu_params[k].numel()
+            self._cpu_params[k].grad = flat[o:o + n].view_as(self._cpu_params[k]).clone()
+            o += n
+        return 1.0 if scale is None else float(scale)
+
+    def _cpu_apply(self, grad_scale=1.0):
+        """optimizer step from p.grad (scaled by grad_scale), same update rule as tr_opt"""
+        P = self._cpu_params
+        with torch.no_grad():
             t = float(self.step_count)
             b1, b2 = self.betas
             for k, p in P.items():
-                g = p.grad + self.wd * p
+                g = p.grad * grad_scale + self.wd * p
                 m, v = self._cpu_m[k], self._cpu_v[k]
                 if self.opt_name == "adam":
                     m.mul_(b1).add_(g, alpha=1 - b1)
@@ -625,6 +691,10 @@ class SageTrainer:
                 else:
                     m.mul_(b1).add_(g)
                     p -= self.lr * m
-        self._cpu_loss = loss.detach()
-        self.graph.rng[1] += 1
+
+    def _cpu_step(self, grad_sync=None):
+        loss = self._cpu_forward_backward()
+        scale = self._cpu_grad_sync(grad_sync) if grad_sync is not None else 1.0
+        self._cpu_apply(scale)
+        self._cpu_loss = loss
         return self._cpu_loss

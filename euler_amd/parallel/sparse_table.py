@@ -105,15 +105,24 @@ class ShardedTable:
         mean = n / self.world
         return min(int(n), int(math.ceil((mean + 6.0 * math.sqrt(mean) + 64) / 64.0)) * 64)
 
-    def lookup_static(self, ids: torch.Tensor):
+    def lookup_static(self, ids: torch.Tensor, trash_row: bool = False):
         """rows [W*C, D] in slot order for padded DISTINCT ids [n] (-1 = none) and the
         :class:`StaticHandle`; row ``handle.pos[k]`` is the row of ``ids[k]``.  Shapes
-        depend on n only: safe inside a hipGraph capture."""
+        depend on n only: safe inside a hipGraph capture.
+
+        An id dropped by a capacity overflow gets ``pos = W*C``.  With ``trash_row`` the
+        returned rows have one extra zero row at index W*C, so a dropped id reads zeros
+        and a caller's gradient for it lands in that row (never in a live slot); pass only
+        the first W*C gradient rows to :meth:`apply_static`."""
         ids = ids.reshape(-1).long()
         n = ids.numel()
+        extra = 1 if trash_row else 0
         if not self.comm:
             pos = torch.arange(n, device=ids.device)
-            return self._gather(ids), StaticHandle(pos, ids)
+            rows = self._gather(ids)
+            if extra:
+                rows = torch.cat([rows, rows.new_zeros(1, self.dim)])
+            return rows, StaticHandle(pos, ids)
         W, C = self.world, self.capacity(n)
         valid = ids >= 0
         owner = torch.where(valid, torch.remainder(ids, W), torch.full_like(ids, W))
@@ -134,7 +143,7 @@ class ShardedTable:
         recv = torch.empty(trash, dtype=torch.long, device=ids.device)
         dist.all_to_all_single(recv, send[:trash], group=self.group)
         local = torch.where(recv >= 0, torch.div(recv, W, rounding_mode="floor"), torch.full_like(recv, -1))
-        out = self._a2a_rows(self._gather(local))
+        out = self._a2a_rows(self._gather(local), extra=extra)
         return out, StaticHandle(pos, local)
 
     def apply_static(self, handle: StaticHandle, grad_rows: torch.Tensor):
@@ -198,12 +207,15 @@ class ShardedTable:
         out[order] = out_sorted
         return out, LookupHandle(order, send, recv, local, ids.numel())
 
-    def _a2a_rows(self, x, out_splits=None, in_splits=None):
-        """all-to-all of [*, D] rows in the wire dtype; returns fp32 rows"""
+    def _a2a_rows(self, x, out_splits=None, in_splits=None, extra=0):
+        """all-to-all of [*, D] rows in the wire dtype; returns fp32 rows (plus ``extra``
+        zero rows at the end)"""
         xw = x.to(self.wire).contiguous()
         n = xw.shape[0] if out_splits is None else sum(out_splits)
-        out = torch.empty(n, self.dim, dtype=self.wire, device=xw.device)
-        dist.all_to_all_single(out, xw, out_splits, in_splits, group=self.group)
+        out = torch.empty(n + extra, self.dim, dtype=self.wire, device=xw.device)
+        if extra:
+            out[n:].zero_()
+        dist.all_to_all_single(out[:n], xw, out_splits, in_splits, group=self.group)
         return out.float()
 
     def _gather(self, local):

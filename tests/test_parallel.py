@@ -238,7 +238,22 @@ def _worker_sparse_table_static(rank, world, port, q, wire="fp32"):
             ok_flag = False
         except RuntimeError:
             ok_flag = True
-        q.put((rank, "sparse_table_static", bool(ok_pad and ok_fwd and ok_upd and ok_flag)))
+        # dropped ids go to the trash row (index W*C), never onto a live slot: every live
+        # row is updated by exactly its own id's gradient
+        tab.weight.copy_(full[tab.global_ids()])
+        rows, h = tab.lookup_static(u, trash_row=True)
+        WC = world * 1
+        ok_trash = rows.shape[0] == WC + 1 and float(rows[WC].abs().sum()) == 0.0
+        g_slot = torch.zeros_like(rows)
+        g_slot[h.pos[:5]] = g_id                         # dropped ids write the trash row
+        live = h.pos[:5] < WC
+        ok_trash = ok_trash and bool((~live).any()) and torch.allclose(rows[h.pos[:5]][live], full[u[:5]][live], **tol)
+        tab.apply_static(h, g_slot[:WC])
+        got = torch.zeros(world, dtype=torch.int64)
+        dist.all_gather_into_tensor(got, live.sum().view(1))
+        changed = (tab.weight - full[tab.global_ids()]).abs().sum(1) > 0
+        ok_trash = ok_trash and int(changed.sum()) <= int(got.sum())
+        q.put((rank, "sparse_table_static", bool(ok_pad and ok_fwd and ok_upd and ok_flag and ok_trash)))
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover
         q.put((rank, "error", repr(e)))
@@ -439,3 +454,68 @@ def test_checkpoint_reshards_on_world_size_change(tmp_path):
     # 3-way re-shard of a 2-way sharded table
     full = torch.arange(10).float().unsqueeze(1)
     assert torch.equal(reshard_rows([full[0::2], full[1::2]], 1, 3), full[1::3])
+
+
+def _worker_sage_dp(rank, world, port, q, dtype):
+    """SageTrainer.step(grad_sync) on 2 gloo ranks with different sample streams: the
+    parameters stay bit-identical across ranks and equal a single-process update on the
+    summed gradients of the two ranks' batches, for 10 steps (fp32 or bf16 hand-off)."""
+    try:
+        import sys
+
+        _init(rank, world, port)
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from test_sage_trainer import _trainer
+
+        def make(r):
+            tr = _trainer("cpu", [5, 3], [32, 32, 16], 5, seed=3)
+            tr.graph.manual_seed(1000 + r)  # per-rank sample stream
+            tr.set_grad_sync_dtype(dtype)
+            return tr
+
+        calls = []
+
+        def sync(g):
+            calls.append(g.numel())
+            dist.all_reduce(g)
+            return 1.0 / world
+
+        tr = make(rank)
+        for _ in range(10):
+            tr.step(sync)
+        mine = tr.logical_params()
+        names = list(mine)
+        flat = torch.cat([mine[k].reshape(-1) for k in names])
+        allp = [torch.zeros_like(flat) for _ in range(world)]
+        dist.all_gather(allp, flat)
+        lockstep = all(torch.equal(a, allp[0]) for a in allp)
+        # single-process oracle: both ranks' batches, summed gradients, one update rule
+        ref = [make(r) for r in range(world)]
+        for _ in range(10):
+            for t in ref:
+                t.step_count += 1
+                t._cpu_forward_backward()
+            for k in names:
+                gs = [t._cpu_params[k].grad for t in ref]
+                s = gs[0].bfloat16() + gs[1].bfloat16() if dtype == "bf16" else gs[0] + gs[1]
+                for t in ref:
+                    t._cpu_params[k].grad = s.float().clone()
+            for t in ref:
+                t._cpu_apply(1.0 / world)
+        rp = ref[0].logical_params()
+        oracle = all(torch.equal(mine[k], rp[k]) for k in names)
+        moved = any(not torch.equal(mine[k], make(rank).logical_params()[k]) for k in names)
+        two_buckets = len(calls) == 20 and len(set(calls)) == 2
+        q.put((rank, f"sage_dp_{dtype}", bool(lockstep and oracle and moved and two_buckets)))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_sage_trainer_data_parallel_lockstep(dtype):
+    res = _run(_worker_sage_dp, dtype)
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == 2 and all(r[2] for r in res), res

@@ -390,3 +390,30 @@ def test_event_loop_server_threads_do_not_grow_with_connections(cluster):
     # and the cluster still answers queries
     ea.initialize_shared_graph(reg, shard_num=2)
     assert ea.sample_node(10, "-1").numel() == 10
+
+
+def test_replica_swaps_do_not_leak_channels(cluster):
+    """UpdateShard (the registry watch) drops Host objects; their pooled channels (socket +
+    64 MB shared region each) must be closed, so repeated replica-set swaps keep the
+    process's fd count flat."""
+    data, reg = cluster
+    ea.initialize_shared_graph(reg, shard_num=2)
+    eng = ea.get_engine()
+    eps = eng.endpoints()
+    port0 = int(eps[0][0].rsplit(":", 1)[1])
+
+    def nfd():
+        return len(os.listdir("/proc/self/fd"))
+
+    def query():
+        ids, _, _ = ea.get_full_neighbor([1, 2], ["0", "1"])
+        assert ids.to_dense().tolist() == [[2, 4, 3], [3, 5, 0]]
+
+    for host in ("127.0.0.1", "localhost"):  # warm both pools once
+        eng.set_replicas(0, [f"{host}:{port0}"])
+        query()
+    base = nfd()
+    for i in range(40):
+        eng.set_replicas(0, [f"{'localhost' if i % 2 else '127.0.0.1'}:{port0}"])
+        query()
+    assert nfd() <= base + 2, (base, nfd())
