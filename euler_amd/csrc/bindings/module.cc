@@ -10,6 +10,7 @@
 #include <pybind11/stl.h>
 
 #include "framework/framework.h"
+#include "framework/udf.h"
 #include "gql/gql.h"
 #include "graph/graph.h"
 #include "index/index.h"
@@ -804,6 +805,7 @@ PYBIND11_MODULE(_engine, m) {
   });
   m.def("edge_id_hash", &EdgeIdHash);
   m.def("registered_ops", [] { return KernelRegistry::Get().Ops(); });
+  m.def("registered_udfs", [] { return RegisteredUdfs(); });
   m.def("stats", [] {
     auto& c = EngineCounters::Get();
     py::dict d;

@@ -19,6 +19,7 @@
 #include <cmath>
 #include <unordered_set>
 
+#include "framework/udf.h"
 #include "ops/ops_util.h"
 
 namespace euler {
@@ -207,21 +208,12 @@ class GetNodeTypeOp : public OpKernel {
 };
 
 // ---------------------------------------------------------------- features
-// UDFs over dense feature values (reference euler/core/kernels/udf: mean / min / max)
-bool ApplyUdf(const std::string& udf, const std::vector<float>& in, float* out) {
-  if (in.empty()) return false;
-  if (udf == "udf_mean" || udf == "mean") {
-    double s = 0;
-    for (float x : in) s += x;
-    *out = static_cast<float>(s / in.size());
-  } else if (udf == "udf_min" || udf == "min") {
-    *out = *std::min_element(in.begin(), in.end());
-  } else if (udf == "udf_max" || udf == "max") {
-    *out = *std::max_element(in.begin(), in.end());
-  } else {
-    EULER_THROW("unknown udf " << udf);
-  }
-  return true;
+// values() UDFs come from the registry (framework/udf.h; built-ins in ops/udfs.cc)
+std::shared_ptr<const ValuesUdf> UdfOf(const NodeDef& nd) {
+  const std::string name = StartsWith(nd.udf_name, "udf_") ? nd.udf_name : "udf_" + nd.udf_name;
+  auto u = FindUdf(name);
+  if (!u) EULER_THROW("unknown udf " << nd.udf_name << " (registered: " << Join(RegisteredUdfs(), ", ") << ")");
+  return u;
 }
 
 class GetFeatureOp : public OpKernel {
@@ -273,24 +265,22 @@ class GetFeatureOp : public OpKernel {
           ctx->Set(nd.Output(2 * f + 1), out);
           continue;
         }
-        std::vector<float> vals;
+        UdfColumn col;
+        col.kind = UdfColumn::kDense;
+        col.counts.assign(n, 0);
         for (int64_t i = 0; i < n; ++i) {
           const float* p = nullptr;
           int64_t k = 0;
           if (c && rows[i] >= 0) c->Get(rows[i], &p, &k);
-          if (apply_udf) {
-            float r;
-            if (ApplyUdf(nd.udf_name, std::vector<float>(p, p + k), &r)) {
-              vals.push_back(r);
-              counts[i] = 1;
-            }
-          } else {
-            vals.insert(vals.end(), p, p + k);
-            counts[i] = k;
-          }
+          col.f.insert(col.f.end(), p, p + k);
+          col.counts[i] = k;
         }
-        ctx->Set(nd.Output(2 * f), MakeIdx(counts));
-        ctx->Set(nd.Output(2 * f + 1), Tensor::FromVector(vals));
+        UdfColumn res;
+        UdfOf(nd)->Compute(col, nd.udf_num_params, &res);
+        if (static_cast<int64_t>(res.counts.size()) != n || res.kind != UdfColumn::kDense)
+          EULER_THROW("udf " << nd.udf_name << " returned a malformed column");
+        ctx->Set(nd.Output(2 * f), MakeIdx(res.counts));
+        ctx->Set(nd.Output(2 * f + 1), Tensor::FromVector(res.f));
       } else if (fi->type == kSparse) {
         const Column<uint64_t>* c = edges ? g.EdgeSparse(fi->idx) : g.NodeSparse(fi->idx);
         std::vector<uint64_t> vals;
@@ -300,6 +290,17 @@ class GetFeatureOp : public OpKernel {
           if (c && rows[i] >= 0) c->Get(rows[i], &p, &k);
           vals.insert(vals.end(), p, p + k);
           counts[i] = k;
+        }
+        if (apply_udf) {
+          UdfColumn col, res;
+          col.kind = UdfColumn::kSparse;
+          col.counts = counts;
+          col.u.swap(vals);
+          UdfOf(nd)->Compute(col, nd.udf_num_params, &res);
+          if (static_cast<int64_t>(res.counts.size()) != n || res.kind != UdfColumn::kSparse)
+            EULER_THROW("udf " << nd.udf_name << " returned a malformed column");
+          counts.swap(res.counts);
+          vals.swap(res.u);
         }
         ctx->Set(nd.Output(2 * f), MakeIdx(counts));
         ctx->Set(nd.Output(2 * f + 1), Tensor::FromVector(vals));

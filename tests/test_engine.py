@@ -287,3 +287,36 @@ def test_plumbing_ops_via_run_op(graph):
     assert out[0].shape == (2, 3) and out[0].tolist() == [[0, 1, 2], [3, 4, 5]]
     with pytest.raises(Exception):
         eng.run_op("API_RESHAPE", {"x": np.arange(6, dtype=np.int32)}, ["x"], ["4,?"], 1)
+
+
+def _udf_queries():
+    n = {"nodes": np.array([1, 2, 3], dtype=np.uint64)}
+    top2 = ea.run_gql("v(nodes).values(dense_f3, dense_f4).udf_topk(dense_f4)[2].as(x)", n,
+                      ["x:0", "x:1", "x:2", "x:3"])
+    smax = ea.run_gql("v(nodes).values(sparse_f1, dense_f4).max(sparse_f1).as(x)", n, ["x:0", "x:1", "x:2", "x:3"])
+    mean = ea.run_gql("v(nodes).values(dense_f4).mean(dense_f4).as(x)", n, ["x:0", "x:1"])
+    return top2, smax, mean
+
+
+def check_udfs(top2, smax, mean):
+    # f3 untouched, topk(f4)[2] = the two largest values per node, descending
+    assert top2[0].tolist() == [[0, 2], [2, 4], [4, 6]]
+    np.testing.assert_allclose(top2[1], [1.1, 1.2, 2.1, 2.2, 3.1, 3.2], rtol=1e-6)
+    assert top2[2].tolist() == [[0, 2], [2, 4], [4, 6]]
+    np.testing.assert_allclose(top2[3], [1.5, 1.4, 2.5, 2.4, 3.5, 3.4], rtol=1e-6)
+    # sparse max (reference end2end_local_test.cc:146-174 style), dense column passes through
+    assert smax[0].tolist() == [[0, 1], [1, 2], [2, 3]] and smax[1].tolist() == [12, 22, 32]
+    assert smax[2].tolist() == [[0, 3], [3, 6], [6, 9]]
+    np.testing.assert_allclose(mean[1], [1.4, 2.4, 3.4], rtol=1e-6)
+
+
+def test_udf_registry(graph):
+    """REGISTER_UDF registry (framework/udf.h): built-ins and a numeric-parameter UDF
+    (udf_topk [k]) through local and local-sharded mode; remote mode: test_rpc.py."""
+    import euler_amd._engine as E
+
+    assert {"udf_mean", "udf_min", "udf_max", "udf_sum", "udf_topk"} <= set(E.registered_udfs())
+    check_udfs(*_udf_queries())
+    with pytest.raises(RuntimeError, match="unknown udf"):
+        ea.run_gql("v(nodes).values(dense_f4).udf_nope(dense_f4).as(x)", {"nodes": np.array([1], np.uint64)},
+                   ["x:0"])

@@ -417,3 +417,13 @@ def test_replica_swaps_do_not_leak_channels(cluster):
         eng.set_replicas(0, [f"{'localhost' if i % 2 else '127.0.0.1'}:{port0}"])
         query()
     assert nfd() <= base + 2, (base, nfd())
+
+
+def test_udf_with_parameters_on_shard_servers(cluster):
+    """the UDF name and its numeric [..] parameters travel inside the REMOTE sub-DAG and
+    run on the shard that holds the feature (same answers as local mode)."""
+    from test_engine import _udf_queries, check_udfs
+
+    data, reg = cluster
+    ea.initialize_shared_graph(reg, shard_num=2)
+    check_udfs(*_udf_queries())

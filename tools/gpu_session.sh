@@ -164,6 +164,16 @@ for st in "${S[@]}"; do
       run bench_small 300 python bench.py --num-nodes 2000000 --steps 100 --warmup 10 --log ;;
     bench_full)
       run bench_full 600 python bench.py --steps 200 --warmup 20 --log ;;
+    dist_bench)
+      # the multi-GPU code path (process group, bucketed all-reduce captured in the step) on one rank
+      for dt in ${DIST_DTYPES:-fp32 bf16}; do
+        run "bench_dist_$dt" 600 python -u -m torch.distributed.run --nnodes 1 --nproc-per-node 1 \
+          --master-addr 127.0.0.1 --master-port 29541 bench.py --force-dist --grad-reduce-dtype $dt \
+          --steps 200 --warmup 20 || exit $?
+      done ;;
+    pmc_lds)
+      PASSES="SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE" \
+        run pmc_lds 300 bash tools/pmc_passes.sh lds "$PWD/tools/tree_kernels.py" --reps 10 ;;
     bench_fp32)
       run bench_fp32 600 python bench.py --steps 200 --warmup 20 --feature-dtype fp32 ;;
     sweep_batch)
