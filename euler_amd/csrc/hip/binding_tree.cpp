@@ -73,6 +73,7 @@ class TreePlan {
     for (int k = 1; k < L_; ++k) M_[k] = M_[k - 1] << logP_[k];
     build_graph();
     build_fwd();
+    build_comb();
     build_head();
     build_dw();
     build_opt();
@@ -346,6 +347,37 @@ class TreePlan {
     }
   }
 
+  // fc and out_fc combined for the head (TrCombArgs): rebuilt every step by extra blocks
+  // of the first forward launch from the fp32 masters in the flat buffer
+  void build_comb() {
+    torch::Tensor flat = T("flat");
+    need(flat, torch::kFloat32, -1, "flat");
+    std::vector<int64_t> off = getv("offsets");  // L convs, fc W, fc b, out W, end
+    TORCH_CHECK((int)off.size() == L_ + 4 && off.back() == flat.numel(), "TreePlan: offsets must cover the flat buffer");
+    const int64_t H = dims_[L_ - 1];
+    TORCH_CHECK(off[L_ + 1] - off[L_] == (int64_t)E_ * H && off[L_ + 3] - off[L_ + 2] == (int64_t)C_ * E_,
+                "TreePlan: fc / out_fc segments do not match E, H, C");
+    TORCH_CHECK(C_ % kTrCombRows == 0, "TreePlan: label width must be a multiple of the combination rows");
+    float* base = flat.data_ptr<float>();
+    TrCombArgs& c = fwd0_.comb;
+    c.wfc = base + off[L_];
+    c.bfc = base + off[L_ + 1];
+    c.wout = base + off[L_ + 2];
+    c.C = C_;
+    c.E = E_;
+    c.H = static_cast<int32_t>(H);
+    c.Wc = owned_bf16((int64_t)C_ * H);
+    c.WcT = owned_bf16((int64_t)C_ * H);
+    c.bc = owned(C_);
+    fwd0_.ncomb = C_ / kTrCombRows;
+  }
+
+  uint16_t* owned_bf16(int64_t n) {
+    torch::Tensor t = torch::zeros({n}, torch::TensorOptions().dtype(torch::kBFloat16).device(dev_));
+    owned_.push_back(t);
+    return reinterpret_cast<uint16_t*>(t.data_ptr());
+  }
+
   float* owned(int64_t n) {  // plan-owned fp32 scratch
     torch::Tensor t = torch::zeros({n}, torch::TensorOptions().dtype(torch::kFloat32).device(dev_));
     owned_.push_back(t);
@@ -371,6 +403,9 @@ class TreePlan {
     a.Wout = bf("Wout_sh", (int64_t)C_ * E_);
     a.WoutT = bf("Wout_shT", (int64_t)C_ * E_);
     a.bfc = f32("bfc", E_);
+    a.Wc = fwd0_.comb.Wc;
+    a.WcT = fwd0_.comb.WcT;
+    a.bc = fwd0_.comb.bc;
     a.roots = fwd0_.roots_cur;
     const int mode = static_cast<int>(geti("label_mode"));
     torch::Tensor lab = T("labels");

@@ -191,6 +191,38 @@ struct Feat8<float> {
 };
 
 // ----------------------------------------------------------------------------
+// combination block of a forward launch: kTrCombRows rows of Wc = Wout Wfc (fp32 FMA from
+// the fp32 masters, the thread of column h runs down E), their bf16 fm images Wc / WcT,
+// and bc = Wout bfc
+// ----------------------------------------------------------------------------
+template <int NT>
+__device__ void tr_comb_block(const TrCombArgs& c, int blk) {
+  const int c0 = blk * kTrCombRows;
+  for (int h = threadIdx.x; h < c.H; h += NT) {
+    float acc[kTrCombRows];
+#pragma unroll
+    for (int r = 0; r < kTrCombRows; ++r) acc[r] = 0.f;
+#pragma unroll 8
+    for (int e = 0; e < c.E; ++e) {
+      const float w = c.wfc[static_cast<int64_t>(e) * c.H + h];
+#pragma unroll
+      for (int r = 0; r < kTrCombRows; ++r) acc[r] += c.wout[static_cast<int64_t>(c0 + r) * c.E + e] * w;
+    }
+#pragma unroll
+    for (int r = 0; r < kTrCombRows; ++r) {
+      c.Wc[fm_off(c0 + r, h, c.H)] = f2bf(acc[r]);
+      c.WcT[fm_off(h, c0 + r, c.C)] = f2bf(acc[r]);
+    }
+  }
+  if (threadIdx.x < kTrCombRows) {
+    const float* w = c.wout + static_cast<int64_t>(c0 + threadIdx.x) * c.E;
+    float b = 0.f;
+    for (int e = 0; e < c.E; ++e) b += w[e] * c.bfc[e];
+    c.bc[c0 + threadIdx.x] = b;
+  }
+}
+
+// ----------------------------------------------------------------------------
 // tr_sample: target-row nodes (root -> hop chain) and their leaf draws, BM rows per block
 // ----------------------------------------------------------------------------
 constexpr int kTrSampleRows = 64;
@@ -240,21 +272,19 @@ __global__ __launch_bounds__(256) void tr_sample_kernel(TrSampleArgs a) {
 #ifndef TR_FWD_BPF
 #define TR_FWD_BPF 2
 #endif
-// TR_FWD_DEDUP=1: fetch each distinct leaf of a row once (weighted by its draw count).
-// Correct (oracle tests pass) but measured 1.9x slower: the serial per-row compaction and
-// the exec-masked, variable-count loads stall the gather (profiles/r2_mid/sweeps/
-// dedup_variant.log); the repeats are cheap L2 hits with branch-free loads.
-#ifndef TR_FWD_DEDUP
-#define TR_FWD_DEDUP 0
-#endif
 template <typename FT, int BM, int MODE>
 __global__ __launch_bounds__(256, (BM == 32 ? TR_FWD_WAVES : 2)) void tr_fwd_kernel(TrFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   constexpr bool kGather = MODE != 2;
+  if (static_cast<int>(blockIdx.x) < a.ncomb) {  // the head's Wc (first forward launch)
+    tr_comb_block<256>(a.comb, blockIdx.x);
+    return;
+  }
+  const int tb = static_cast<int>(blockIdx.x) - a.ncomb, ntb = static_cast<int>(gridDim.x) - a.ncomb;
   const int D = a.D;
   const int K2 = 2 * D;
   const int ldsw = K2 + 8;
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = xcd_remap(tb, ntb);
   const int64_t row0 = static_cast<int64_t>(tile) * BM;
   const int H = a.H;
   const bool alias_out = H <= kTrBN && kTrBN <= K2;
@@ -264,13 +294,9 @@ __global__ __launch_bounds__(256, (BM == 32 ? TR_FWD_WAVES : 2)) void tr_fwd_ker
   bf16_t* otile = own_otile ? lds + BM * ldsw : lds;
   int32_t* node_s = reinterpret_cast<int32_t*>(lds + BM * ldsw + (own_otile ? BM * (kTrBN + 8) : 0));
   int32_t* leaf_s = node_s + BM;
-  // leaf dedup (TR_FWD_DEDUP): per row, the distinct leaf ids move to the front of the
-  // row's leaf_s segment, mult_s holds their draw counts and cnt_s the distinct count
-  int32_t* mult_s = leaf_s + BM * a.FL;
-  int32_t* cnt_s = mult_s + BM * a.FL;
 
 #define TF_STAMP(k) \
-  if (a.prof && threadIdx.x == 0) a.prof[blockIdx.x * 8 + (k)] = static_cast<long long>(wall_clock64())
+  if (a.prof && threadIdx.x == 0) a.prof[tb * 8 + (k)] = static_cast<long long>(wall_clock64())
   TF_STAMP(0);
   constexpr int FN = 4;
   constexpr int kBP = TR_FWD_BPF;  // k-steps of weight fragments in flight
@@ -280,39 +306,15 @@ __global__ __launch_bounds__(256, (BM == 32 ? TR_FWD_WAVES : 2)) void tr_fwd_ker
   uint4_t bq[kBP][FN];
   if constexpr (kGather) {
     // ---- the sampled ids of the block (sampler output, one step ahead): coalesced
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (tb == 0 && threadIdx.x == 0) {
       if (a.step) a.step[0] += 1;
       a.rng[1] += 1;  // this batch is consumed: the sampler draws the next counter
     }
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < a.B; i += gridDim.x * 256) a.roots_cur[i] = a.roots_in[i];
+    for (int i = tb * 256 + threadIdx.x; i < a.B; i += ntb * 256) a.roots_cur[i] = a.roots_in[i];
     if (threadIdx.x < BM) node_s[threadIdx.x] = row0 + threadIdx.x < a.M ? a.nodes[row0 + threadIdx.x] : -1;
     for (int it = threadIdx.x; it < BM * a.FL; it += 256)
       leaf_s[it] = row0 * a.FL + it < a.M * a.FL ? a.leaf[row0 * a.FL + it] : -1;
     __syncthreads();
-#if TR_FWD_DEDUP
-    // with-replacement draws repeat rows (a node with fewer out-edges than FL draws the
-    // same neighbours again): fetch each distinct leaf row once, weighted by its count
-    if (threadIdx.x < BM) {
-      int32_t* ids = leaf_s + threadIdx.x * a.FL;
-      int32_t* mul = mult_s + threadIdx.x * a.FL;
-      int n = 0;
-      for (int k = 0; k < a.FL; ++k) {
-        const int32_t v = ids[k];
-        if (v < 0) continue;
-        int j = 0;
-        while (j < n && ids[j] != v) ++j;
-        if (j < n) {
-          mul[j] += 1;
-        } else {
-          ids[n] = v;
-          mul[n] = 1;
-          ++n;
-        }
-      }
-      cnt_s[threadIdx.x] = n;
-    }
-    __syncthreads();
-#endif
     TF_STAMP(1);
     // ---- gather + mean: item = (row, 8-column chunk); two items per thread with every
     // leaf load of both in flight
@@ -334,36 +336,6 @@ __global__ __launch_bounds__(256, (BM == 32 ? TR_FWD_WAVES : 2)) void tr_fwd_ker
       for (int i = 0; i < 8; ++i) acc_a[i] = acc_b[i] = 0.f;
       sa.load(x + static_cast<int64_t>(na > 0 ? na : 0) * D + ca * 8);
       sb.load(x + static_cast<int64_t>(nb > 0 ? nb : 0) * D + cb * 8);
-#if TR_FWD_DEDUP
-      const int na_cnt = cnt_s[ra], nb_cnt = hb ? cnt_s[rb] : 0;
-      const int kmax = na_cnt > nb_cnt ? na_cnt : nb_cnt;
-      for (int k = 0; k < kmax; k += G) {
-        int32_t ja[G], jb[G];
-        float wa[G], wb[G];
-        Feat8<FT> va[G], vb[G];
-#pragma unroll
-        for (int u = 0; u < G; ++u) {
-          const bool oa = k + u < na_cnt, ob = k + u < nb_cnt;
-          ja[u] = oa ? leaf_s[ra * a.FL + k + u] : -1;
-          jb[u] = ob ? leaf_s[rb * a.FL + k + u] : -1;
-          wa[u] = oa ? static_cast<float>(mult_s[ra * a.FL + k + u]) : 0.f;
-          wb[u] = ob ? static_cast<float>(mult_s[rb * a.FL + k + u]) : 0.f;
-        }
-        // lanes past their row's distinct count are masked off: no memory request
-#pragma unroll
-        for (int u = 0; u < G; ++u) {
-          if (ja[u] >= 0) va[u].load(x + static_cast<int64_t>(ja[u]) * D + ca * 8);
-          else va[u].zero();
-          if (jb[u] >= 0) vb[u].load(x + static_cast<int64_t>(jb[u]) * D + cb * 8);
-          else vb[u].zero();
-        }
-#pragma unroll
-        for (int u = 0; u < G; ++u) {
-          va[u].add_scaled_to(acc_a, wa[u]);
-          vb[u].add_scaled_to(acc_b, wb[u]);
-        }
-      }
-#else
       for (int k = 0; k < a.FL; k += G) {
         int32_t ja[G], jb[G];
         Feat8<FT> va[G], vb[G];
@@ -386,7 +358,6 @@ __global__ __launch_bounds__(256, (BM == 32 ? TR_FWD_WAVES : 2)) void tr_fwd_ker
           vb[u].add_to(acc_b);
         }
       }
-#endif
       sa.keep(na >= 0);
       sb.keep(nb >= 0);
       if (a.include_self) {
@@ -564,161 +535,246 @@ __global__ __launch_bounds__(256, (BM == 32 ? TR_FWD_WAVES : 2)) void tr_fwd_ker
 }
 
 // ----------------------------------------------------------------------------
-// tr_fwd_pk: layer 0 as a persistent kernel, one 512-thread block per CU.  The weight
-// (fm layout, <= 128 KB) is loaded into LDS once; the block then walks its 32-row tiles
-// and software-pipelines them: the feature rows of tile t + grid are in flight (in
-// registers) while tile t's A tile is multiplied out of LDS and its tree-mean epilogue
-// runs.  Requirements (else tr_fwd_kernel): 32-row tiles cover whole sibling groups,
-// H <= 256, H <= 2D, D <= 128, FL <= NF.
+// tr_fwd2: layer 0 (mode 0) with 64 target rows and 8 waves per block.  Versus
+// tr_fwd_kernel<BM=32> (4 waves, each 64 columns x 32 rows):
+//   * every wave multiplies all 64 rows by its 32 columns, so a weight fragment fetched
+//     from L2 serves 64 rows instead of 32 (the GEMM phase was bound by re-fetching W
+//     per 32 rows: 800 blocks x 128 KB);
+//   * the A tile has no padding; 16-B chunk c of row r lives at chunk c ^ (r & 15), so
+//     each ds_read_b128 lane group ({0-3,12-15,20-27}, ...: rows 0-15 x k-quarters 0/1
+//     or 2/3) touches 16 distinct 16-B bank slots (the padded layout put two lanes of a
+//     group on one slot: a 2-way conflict on every fragment read);
+//   * the ReLU'd output goes to LDS transposed ([column][row], row stride 68 bf16 =
+//     34 dwords): one 8-byte store per lane per MFMA tile instead of four 2-byte ones,
+//     and the tree-mean / ReLU-bit epilogue reads whole 4-row words (ds_read_b64), all
+//     bank-conflict-free (34c mod 64 is distinct for the 32 lanes of a half-wave).
+// Needs D % 64 == 0 (A rows of a multiple of 16 chunks), M % 64 == 0 and sibling groups
+// of at most 64 rows (else tr_fwd_kernel).
 // ----------------------------------------------------------------------------
-constexpr int kPkThreads = 512;
+constexpr int kF2Rows = 64, kF2Threads = 512, kF2Ldt = kF2Rows + 4;
 
-template <typename FT, int NF>
-__global__ __launch_bounds__(kPkThreads, 1) void tr_fwd_pk_kernel(TrFwdArgs a, int ntiles) {
+__device__ __forceinline__ int f2_chunk(int r, int c) { return c ^ (r & 15); }
+
+template <typename FT>
+__global__ __launch_bounds__(kF2Threads, 4) void tr_fwd2_kernel(TrFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  constexpr int BM = kF2Rows, NT = kF2Threads;
+  if (static_cast<int>(blockIdx.x) < a.ncomb) {  // the head's Wc
+    tr_comb_block<NT>(a.comb, blockIdx.x);
+    return;
+  }
+  const int tb = static_cast<int>(blockIdx.x) - a.ncomb, ntb = static_cast<int>(gridDim.x) - a.ncomb;
   const int D = a.D, K2 = 2 * D, H = a.H;
-  const int ldsw = K2 + 8, ldo = H + 8;
-  bf16_t* Ws = lds;                                    // [H * K2] fm weight
-  bf16_t* At = lds + static_cast<int64_t>(H) * K2;     // [32][ldsw] A tile, then [32][ldo] h tile
+  const int tile = xcd_remap(tb, ntb);
+  const int64_t row0 = static_cast<int64_t>(tile) * BM;
+  // LDS: A tile [BM][K2] (swizzled) | output tile [kTrBN][kF2Ldt] (transposed) | ids
+  bf16_t* At = lds;
+  bf16_t* Ot = lds + BM * K2;
+  int32_t* node_s = reinterpret_cast<int32_t*>(Ot + kTrBN * kF2Ldt);
+  int32_t* leaf_s = node_s + BM;
+#define F2_STAMP(k) \
+  if (a.prof && threadIdx.x == 0) a.prof[tb * 8 + (k)] = static_cast<long long>(wall_clock64())
+  F2_STAMP(0);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int lr = lane & 15, lk = (lane >> 4) * 8;
-  if (blockIdx.x == 0 && tid == 0) {
+  const int lr = lane & 15, lg = lane >> 4;
+  if (tb == 0 && tid == 0) {
     if (a.step) a.step[0] += 1;
     a.rng[1] += 1;  // this batch is consumed: the sampler draws the next counter
   }
-  for (int i = blockIdx.x * kPkThreads + tid; i < a.B; i += gridDim.x * kPkThreads) a.roots_cur[i] = a.roots_in[i];
-  for (int it = tid; it < (H * K2) >> 3; it += kPkThreads)
-    reinterpret_cast<uint4_t*>(Ws)[it] = reinterpret_cast<const uint4_t*>(a.W)[it];
-  // gather role: row gr (0..31), 8-column chunk gc; spare threads duplicate a valid item
-  const int cpr = D >> 3;
-  const bool gth = tid < 32 * cpr;
-  const int gi = gth ? tid : tid % (32 * cpr);
-  const int gr = gi / cpr, gc = gi - gr * cpr;
-  const FT* x = static_cast<const FT*>(a.x);
-  const int G = gridDim.x;
-  const int FL = a.FL;
-  auto load_ids = [&](int tt, int32_t& nd, int32_t (&lf)[NF]) {
-    const int64_t row = static_cast<int64_t>(tt < ntiles ? tt : ntiles - 1) * 32 + gr;
-    nd = a.nodes[row];
+  for (int i = tb * NT + tid; i < a.B; i += ntb * NT) a.roots_cur[i] = a.roots_in[i];
+  if (tid < BM) node_s[tid] = a.nodes[row0 + tid];
+  for (int it = tid; it < BM * a.FL; it += NT) leaf_s[it] = a.leaf[row0 * a.FL + it];
+  __syncthreads();
+  F2_STAMP(1);
+  // ---- gather + mean: item = (row, 8-column chunk); two items per thread, every leaf
+  // load of both in flight; padding ids (-1) read row 0 and are zeroed at use
+  {
+    const FT* x = static_cast<const FT*>(a.x);
+    const int cpr = D >> 3;
+    const int nitems = BM * cpr;
+    constexpr int G = Feat8<FT>::kInFlight;
+    for (int it = tid; it < nitems; it += 2 * NT) {
+      const int itb = it + NT;
+      const bool hb = itb < nitems;
+      const int ra = it / cpr, ca = it - ra * cpr;
+      const int rb = hb ? itb / cpr : ra, cb = hb ? itb - rb * cpr : ca;
+      const int32_t na = node_s[ra], nb = hb ? node_s[rb] : -1;
+      Feat8<FT> sa, sb;
+      float acc_a[8], acc_b[8];
 #pragma unroll
-    for (int u = 0; u < NF; ++u) lf[u] = a.leaf[row * FL + (u < FL ? u : FL - 1)];
-  };
-  auto issue = [&](int32_t nd, const int32_t (&lf)[NF], Feat8<FT>& sv, Feat8<FT> (&lv)[NF]) {
-    sv.load(x + static_cast<int64_t>(nd > 0 ? nd : 0) * D + gc * 8);
+      for (int i = 0; i < 8; ++i) acc_a[i] = acc_b[i] = 0.f;
+      sa.load(x + static_cast<int64_t>(na > 0 ? na : 0) * D + ca * 8);
+      sb.load(x + static_cast<int64_t>(nb > 0 ? nb : 0) * D + cb * 8);
+      for (int k = 0; k < a.FL; k += G) {
+        int32_t ja[G], jb[G];
+        Feat8<FT> va[G], vb[G];
 #pragma unroll
-    for (int u = 0; u < NF; ++u) lv[u].load(x + static_cast<int64_t>(lf[u] > 0 ? lf[u] : 0) * D + gc * 8);
-  };
-  // ids run two tiles ahead of the feature rows, so a tile's only dependent chain
-  // inside the loop is one feature-row load
-  int t = blockIdx.x;
-  int32_t nd, lf[NF], nd2, lf2[NF];
-  Feat8<FT> sv, lv[NF];
-  load_ids(t, nd, lf);
-  load_ids(t + G, nd2, lf2);
-  issue(nd, lf, sv, lv);
-  __syncthreads();  // weight in LDS
-  for (; t < ntiles; t += G) {
-    const int64_t row0 = static_cast<int64_t>(t) * 32;
-    int32_t nd3, lf3[NF];
-    load_ids(t + 2 * G, nd3, lf3);
-    // ---- finish the gather of tile t -> A tile [x_self | mean x_leaf]
-    {
-      float acc[8];
+        for (int u = 0; u < G; ++u) {
+          ja[u] = (k + u < a.FL) ? leaf_s[ra * a.FL + k + u] : -1;
+          jb[u] = (hb && k + u < a.FL) ? leaf_s[rb * a.FL + k + u] : -1;
+        }
 #pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+        for (int u = 0; u < G; ++u) {
+          va[u].load(x + static_cast<int64_t>(ja[u] > 0 ? ja[u] : 0) * D + ca * 8);
+          vb[u].load(x + static_cast<int64_t>(jb[u] > 0 ? jb[u] : 0) * D + cb * 8);
+        }
 #pragma unroll
-      for (int u = 0; u < NF; ++u) {
-        lv[u].keep(u < FL && lf[u] >= 0);
-        lv[u].add_to(acc);
+        for (int u = 0; u < G; ++u) {
+          va[u].keep(ja[u] >= 0);
+          vb[u].keep(jb[u] >= 0);
+          va[u].add_to(acc_a);
+          vb[u].add_to(acc_b);
+        }
       }
-      sv.keep(nd >= 0);
-      if (a.include_self) sv.add_to(acc);
+      sa.keep(na >= 0);
+      sb.keep(nb >= 0);
+      if (a.include_self) {
+        sa.add_to(acc_a);
+        sb.add_to(acc_b);
+      }
 #pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i] *= a.inv_leaf;
-      if (gth) {
-        *reinterpret_cast<uint4_t*>(At + gr * ldsw + gc * 8) = sv.bf16();
-        *reinterpret_cast<uint4_t*>(At + gr * ldsw + D + gc * 8) = pack_bf16x8(acc);
+      for (int i = 0; i < 8; ++i) {
+        acc_a[i] *= a.inv_leaf;
+        acc_b[i] *= a.inv_leaf;
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (h == 1 && !hb) break;
+        const int r = h ? rb : ra, c = h ? cb : ca;
+        *reinterpret_cast<uint4_t*>(At + r * K2 + f2_chunk(r, c) * 8) = h ? sb.bf16() : sa.bf16();
+        *reinterpret_cast<uint4_t*>(At + r * K2 + f2_chunk(r, cpr + c) * 8) = pack_bf16x8(h ? acc_b : acc_a);
       }
     }
-    __syncthreads();
-    // ---- the next tile's rows go in flight behind this tile's GEMM and epilogue
-    nd = nd2;
-    nd2 = nd3;
+  }
+  // the first two k-steps of this wave's weight fragments load behind the kt pass (not
+  // earlier: held through the gather they would push its 20 row loads in flight to spill)
+  const bf16_t* W = a.W;
+  uint4_t bq[2][2];
+  if (wave * 32 < H) {
 #pragma unroll
-    for (int u = 0; u < NF; ++u) {
-      lf[u] = lf2[u];
-      lf2[u] = lf3[u];
-    }
-    issue(nd, lf, sv, lv);
-    // ---- A tile -> kt layout (dW operand): item = (column n, 8-row chunk q)
-    for (int it = tid; it < K2 * 4; it += kPkThreads) {
-      const int q = it & 3, n = it >> 2;
-      float v[8];
+    for (int q = 0; q < 2; ++q)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = bf2f(At[(q * 8 + i) * ldsw + n]);
-      *reinterpret_cast<uint4_t*>(a.a_kt + kt_off(row0 + q * 8, n, K2)) = pack_bf16x8(v);
+      for (int n = 0; n < 2; ++n) bq[q][n] = fm_frag(W, wave * 32 + n * 16, q * 32 < K2 ? q * 32 : 0, K2, lane);
+  }
+  __syncthreads();
+  F2_STAMP(2);
+  // ---- A tile -> kt layout (dW operand): item = (column pair, 8-row chunk), column pairs
+  // fastest: a half-wave's 4-byte reads cover 128 contiguous (permuted) bytes of a row
+  {
+    const int np = K2 >> 1;
+    for (int it = tid; it < np * (BM / 8); it += NT) {
+      const int q = it / np;
+      const int n = (it - q * np) * 2;
+      uint32_t w[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int r = q * 8 + i;
+        w[i] = *reinterpret_cast<const uint32_t*>(At + r * K2 + f2_chunk(r, n >> 3) * 8 + (n & 7));
+      }
+      uint4_t lo, hi;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        lo[i] = (w[2 * i] & 0xffffu) | (w[2 * i + 1] << 16);
+        hi[i] = (w[2 * i] >> 16) | (w[2 * i + 1] & 0xffff0000u);
+      }
+      *reinterpret_cast<uint4_t*>(a.a_kt + kt_off(row0 + q * 8, n, K2)) = lo;
+      *reinterpret_cast<uint4_t*>(a.a_kt + kt_off(row0 + q * 8, n + 1, K2)) = hi;
     }
-    // ---- GEMM: wave w owns columns w*32 .. +31 (and +256 if H were larger: H <= 256)
-    const int cb = wave * 32;
-    float4_t acc[2][2];
+  }
+  F2_STAMP(3);
+  // ---- MFMA GEMM out of LDS: wave w owns columns w*32..+31 of each 256-column chunk, all
+  // 64 rows; two k-steps of weight fragments in flight
+  constexpr int FM = BM / 16, FN = 2;
+  for (int cchunk = 0; cchunk < H; cchunk += kTrBN) {
+    const int cb = cchunk + wave * 32;
+    float4_t acc[FM][FN];
     tl_zero(acc);
     if (cb < H) {
-      for (int k0 = 0; k0 < K2; k0 += 32) {
-        uint4_t av[2], bv[2];
+      if (cchunk > 0) {
 #pragma unroll
-        for (int m = 0; m < 2; ++m) av[m] = *reinterpret_cast<const uint4_t*>(At + (m * 16 + lr) * ldsw + k0 + lk);
+        for (int q = 0; q < 2; ++q)
 #pragma unroll
-        for (int n = 0; n < 2; ++n) bv[n] = fm_frag(Ws, cb + n * 16, k0, K2, lane);
-#pragma unroll
-        for (int m = 0; m < 2; ++m)
-#pragma unroll
-          for (int n = 0; n < 2; ++n) acc[m][n] = mfma16(av[m], bv[n], acc[m][n]);
+          for (int n = 0; n < FN; ++n) bq[q][n] = fm_frag(W, cb + n * 16, q * 32 < K2 ? q * 32 : 0, K2, lane);
       }
-    }
-    __syncthreads();  // A tile fully read: the h tile overwrites it
-    if (cb < H) {
+      for (int k0 = 0; k0 < K2; k0 += 64) {
 #pragma unroll
-      for (int m = 0; m < 2; ++m)
+        for (int q = 0; q < 2; ++q) {
+          const int ks = k0 + 32 * q;
+          if (ks >= K2) break;  // uniform
+          uint4_t av[FM];
+          const int phys = f2_chunk(lr, (ks >> 3) + lg) * 8;
 #pragma unroll
-        for (int n = 0; n < 2; ++n)
+          for (int m = 0; m < FM; ++m) av[m] = *reinterpret_cast<const uint4_t*>(At + (m * 16 + lr) * K2 + phys);
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
-            At[(m * 16 + (lane >> 4) * 4 + j) * ldo + cb + n * 16 + lr] = f2bf(fmaxf(acc[m][n][j], 0.f));
+          for (int m = 0; m < FM; ++m)
+#pragma unroll
+            for (int n = 0; n < FN; ++n) acc[m][n] = mfma16(av[m], bq[q][n], acc[m][n]);
+          const int kn = ks + 64;
+#pragma unroll
+          for (int n = 0; n < FN; ++n) bq[q][n] = fm_frag(W, cb + n * 16, kn < K2 ? kn : 0, K2, lane);
+        }
+      }
+      // ReLU -> transposed output tile: 4 consecutive rows of one column per 8-byte store
+#pragma unroll
+      for (int m = 0; m < FM; ++m)
+#pragma unroll
+        for (int n = 0; n < FN; ++n) {
+          tl_uint2 v;
+          v[0] = pack_bf16x2(fmaxf(acc[m][n][0], 0.f), fmaxf(acc[m][n][1], 0.f));
+          v[1] = pack_bf16x2(fmaxf(acc[m][n][2], 0.f), fmaxf(acc[m][n][3], 0.f));
+          *reinterpret_cast<tl_uint2*>(Ot + (wave * 32 + n * 16 + lr) * kF2Ldt + m * 16 + lg * 4) = v;
+        }
     }
     __syncthreads();
-    // ---- tree mean of every sibling group -> parent A rows; ReLU bits
+    F2_STAMP(4);
+    const int ncols = (H - cchunk) < kTrBN ? (H - cchunk) : kTrBN;
+    // tree-mean epilogue: item = (sibling group, column); the group's rows are contiguous
+    // in the column's LDS row: 8-byte reads of 4 rows
     {
-      const int groups = 32 >> a.logPg;
-      const int pairs = H >> 1;
-      for (int it = tid; it < groups * pairs; it += kPkThreads) {
-        const int gg = it / pairs;
-        const int c = (it - gg * pairs) * 2;
-        const int base = gg << a.logPg;
-        const uint32_t selfp = *reinterpret_cast<const uint32_t*>(At + (base + a.Fg) * ldo + c);
-        float s0 = 0.f, s1 = 0.f;
-        for (int j = 0; j < a.Fg; ++j) {
-          const uint32_t v = *reinterpret_cast<const uint32_t*>(At + (base + j) * ldo + c);
-          s0 += bf_lo(v);
-          s1 += bf_hi(v);
+      const int P = 1 << a.logPg;
+      const int groups = BM >> a.logPg;
+      for (int it = tid; it < groups * ncols; it += NT) {
+        const int gi = it / ncols, c = it - gi * ncols;
+        const bf16_t* col = Ot + c * kF2Ldt + (gi << a.logPg);
+        float s = 0.f, self = 0.f;
+        for (int r4 = 0; r4 < P; r4 += 4) {
+          const tl_uint2 v = *reinterpret_cast<const tl_uint2*>(col + r4);
+          const float e[4] = {bf_lo(v[0]), bf_hi(v[0]), bf_lo(v[1]), bf_hi(v[1])};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int r = r4 + j;
+            s += r < a.Fg ? e[j] : 0.f;
+            self = r == a.Fg ? e[j] : self;
+          }
         }
-        if (a.include_self) {
-          s0 += bf_lo(selfp);
-          s1 += bf_hi(selfp);
-        }
-        const int64_t parent = (row0 >> a.logPg) + gg;
-        bf16_t* dst = a.a_next + parent * 2 * H + c;
-        *reinterpret_cast<uint32_t*>(dst) = selfp;
-        *reinterpret_cast<uint32_t*>(dst + H) = pack_bf16x2(s0 * a.inv_grp, s1 * a.inv_grp);
+        if (a.include_self) s += self;
+        const int64_t parent = (row0 >> a.logPg) + gi;
+        bf16_t* dst = a.a_next + parent * 2 * H + cchunk + c;
+        dst[0] = f2bf(self);
+        dst[H] = f2bf(s * a.inv_grp);
       }
-      for (int n = tid - (kPkThreads - H); n >= 0 && n < H; n += H) {  // the last H threads
+    }
+    // ReLU bits for the backward: word (32-row block, column) has bit i set iff row i > 0
+    if (a.mask) {
+      for (int it = tid; it < (BM / 32) * ncols; it += NT) {
+        const int kbl = it / ncols, c = it - kbl * ncols;
+        const bf16_t* col = Ot + c * kF2Ldt + kbl * 32;
         uint32_t bits = 0;
 #pragma unroll
-        for (int i = 0; i < 32; ++i) bits |= (bf_pos(At[i * ldo + n]) ? 1u : 0u) << i;
-        a.mask[(row0 >> 5) * H + n] = bits;
+        for (int r4 = 0; r4 < 32; r4 += 4) {
+          const tl_uint2 v = *reinterpret_cast<const tl_uint2*>(col + r4);
+          bits |= (bf_pos(static_cast<bf16_t>(v[0] & 0xffffu)) ? 1u : 0u) << r4;
+          bits |= (bf_pos(static_cast<bf16_t>(v[0] >> 16)) ? 1u : 0u) << (r4 + 1);
+          bits |= (bf_pos(static_cast<bf16_t>(v[1] & 0xffffu)) ? 1u : 0u) << (r4 + 2);
+          bits |= (bf_pos(static_cast<bf16_t>(v[1] >> 16)) ? 1u : 0u) << (r4 + 3);
+        }
+        a.mask[((row0 >> 5) + kbl) * H + cchunk + c] = bits;
       }
     }
     __syncthreads();
   }
+  F2_STAMP(5);
+#undef F2_STAMP
 }
 
 // ----------------------------------------------------------------------------
@@ -785,6 +841,18 @@ constexpr int HFM = HB / 16;
 constexpr int HNW = 16;
 constexpr int TR_KC = 8;  // k steps (x32) per B chunk
 
+// Head LDS tiles: rows padded by 16 bf16 (stride = 2 mod 4 16-B slots), so every
+// ds_read_b128 lane group of an MFMA A-fragment read (rows 0-15 of two k-quarters:
+// {0-3,12-15,20-27}, ...) lands on 16 distinct bank slots (2r + kq mod 16); the old
+// +8 padding (stride 1 mod 16) put two lanes of every group on one slot.  Per-lane
+// addresses stay base + constant, so the k loop folds them into the load offsets.
+__device__ __forceinline__ int sw_off(int r, int col, int ld) { return r * ld + col; }
+
+// the routed dW's G^T tile [64 p][32 k] (4 chunks per row, no padding): chunk c of row r
+// at c ^ ((r >> 2) & 2) — conflict-free for the fragment reads and for 8-lane store groups
+// that cover two whole rows (rows sharing a slot quad get distinct masks)
+__device__ __forceinline__ int rt_off(int r, int col) { return r * 32 + ((((col >> 3) ^ ((r >> 2) & 2))) << 3) + (col & 7); }
+
 __device__ __forceinline__ void tr_prefetch(const bf16_t* __restrict__ Bf, int col0, int N, int K, int lane,
                                             uint4_t (&b)[TR_KC]) {
   const int c = col0 < N ? col0 : 0;  // branch-free: out-of-range fragments are loaded but unused
@@ -800,7 +868,7 @@ __device__ __forceinline__ void tr_mfma_chunk(const bf16_t* A, int lda, int kc, 
     if (kc + s * 32 < K) {
       uint4_t av[HFM];
 #pragma unroll
-      for (int m = 0; m < HFM; ++m) av[m] = *reinterpret_cast<const uint4_t*>(A + (m * 16 + lr) * lda + kc + s * 32 + lk);
+      for (int m = 0; m < HFM; ++m) av[m] = *reinterpret_cast<const uint4_t*>(A + sw_off(m * 16 + lr, kc + s * 32 + lk, lda));
 #pragma unroll
       for (int m = 0; m < HFM; ++m) acc[m][0] = mfma16(av[m], b[s], acc[m][0]);
     }
@@ -827,7 +895,7 @@ __device__ __forceinline__ void tr_lds_to_kt(const bf16_t* tile, int ld, int N, 
     const int q = it / np, n = (it - q * np) * 2;
     uint32_t w[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) w[i] = *reinterpret_cast<const uint32_t*>(tile + (q * 8 + i) * ld + n);
+    for (int i = 0; i < 8; ++i) w[i] = *reinterpret_cast<const uint32_t*>(tile + sw_off(q * 8 + i, n, ld));
     uint4_t lo, hi;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -839,8 +907,19 @@ __device__ __forceinline__ void tr_lds_to_kt(const bf16_t* tile, int ld, int N, 
   }
 }
 
-__device__ __forceinline__ int tr_head_ld(int w) { return w + 8; }
+__device__ __forceinline__ int tr_head_ld(int w) { return w + 16; }  // see sw_off
 
+// Phases (a barrier between each; every wave takes tile jobs j = wave, wave + 16, ...):
+//   P0  h = relu(A W^T)                                  [A tile + A_kt, h_kt]
+//   P1  logits = h Wc^T + bc -> loss, F1 counts, dlogits   (C/16 jobs, critical path)
+//       emb = h Wfc^T + bfc -> emb_kt                      (fills the idle waves)
+//   P2  g = (dlogits Wc) * relu'(h) -> g_kt                (H/16 jobs, critical path)
+//       demb = dlogits Wout -> demb_kt, fc-bias partials   (E/16 jobs)
+//       remaining emb jobs
+//   P3  dA = g W (fp32 rows for the layer below)
+// fc and out_fc enter the critical path only through Wc = Wout Wfc (TrCombArgs): the
+// reference model has no nonlinearity between them, so logits and their gradient to h are
+// the same products with two dependent GEMM phases fewer.
 __global__ __launch_bounds__(HNW * 64) void tr_head_kernel(TrHeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   const int nhb = static_cast<int>(gridDim.x) - a.nsample;
@@ -852,13 +931,11 @@ __global__ __launch_bounds__(HNW * 64) void tr_head_kernel(TrHeadArgs a) {
   if (a.prof && threadIdx.x == 0) a.prof[blockIdx.x * 8 + (k)] = static_cast<long long>(wall_clock64())
   TR_STAMP(0);
   const int Hin2 = a.Hin2, H = a.H, E = a.E, C = a.C;
-  const int lda = tr_head_ld(Hin2), ldh = tr_head_ld(H), lde = tr_head_ld(E > H ? E : H), ldd = tr_head_ld(E),
-            ldc = tr_head_ld(C);
+  const int lda = tr_head_ld(Hin2), ldh = tr_head_ld(H), ldc = tr_head_ld(C);
   bf16_t* Aa = lds;            // [HB][lda]  A rows
   bf16_t* Ah = Aa + HB * lda;  // [HB][ldh]  h (post-ReLU)
-  bf16_t* Eb = Ah + HB * ldh;  // [HB][lde]  emb, later g
-  bf16_t* Db = Eb + HB * lde;  // [HB][ldd]  demb
-  bf16_t* Dl = Db + HB * ldd;  // [HB][ldc]  dlogits
+  bf16_t* Gb = Ah + HB * ldh;  // [HB][ldh]  g
+  bf16_t* Dl = Gb + HB * ldh;  // [HB][ldc]  dlogits
   bf16_t* Ly = Dl + HB * ldc;  // [HB][C]    dense labels (label_mode 2)
   __shared__ int lab_s[HB];
   __shared__ float red_s[HNW][4];
@@ -882,14 +959,42 @@ __global__ __launch_bounds__(HNW * 64) void tr_head_kernel(TrHeadArgs a) {
       *reinterpret_cast<uint4_t*>(Ly + r * C + c * 8) = *reinterpret_cast<const uint4_t*>(L + root * C + c * 8);
     }
   }
+  // job lists of P1 / P2: (B operand, its K, output column)
+  const int nl = C >> 4, ne = E >> 4, nh = H >> 4;
+  const int ne1 = (HNW - nl) > 0 ? ((HNW - nl) < ne ? (HNW - nl) : ne) : 0;  // emb jobs beside the logits
+  const int n1 = nl + ne1, n2 = nh + ne + (ne - ne1);
+  auto job1 = [&](int j, const bf16_t*& Bf, int& cc) {
+    if (j < nl) {
+      Bf = a.Wc;
+      cc = j * 16;
+    } else {
+      Bf = a.Wfc;
+      cc = (j - nl) * 16;
+    }
+  };
+  auto job2 = [&](int j, const bf16_t*& Bf, int& cc, int& K) {
+    if (j < nh) {
+      Bf = a.WcT;
+      cc = j * 16;
+      K = C;
+    } else if (j < nh + ne) {
+      Bf = a.WoutT;
+      cc = (j - nh) * 16;
+      K = C;
+    } else {
+      Bf = a.Wfc;
+      cc = (ne1 + j - nh - ne) * 16;
+      K = H;
+    }
+  };
 
-  // S0: A tile -> LDS (+ A_kt); h = relu(A @ W^T)
+  // P0: A tile -> LDS (+ A_kt); h = relu(A @ W^T)
   uint4_t pre[TR_KC];
   tr_prefetch(a.W, wave * 16, H, Hin2, lane, pre);
   const int cpa = Hin2 >> 3;
   for (int it = threadIdx.x; it < HB * cpa; it += NT) {
     const int r = it / cpa, c = it - r * cpa;
-    *reinterpret_cast<uint4_t*>(Aa + r * lda + c * 8) =
+    *reinterpret_cast<uint4_t*>(Aa + sw_off(r, c * 8, lda)) =
         *reinterpret_cast<const uint4_t*>(a.A + (r0 + r) * Hin2 + c * 8);
   }
   __syncthreads();
@@ -903,66 +1008,65 @@ __global__ __launch_bounds__(HNW * 64) void tr_head_kernel(TrHeadArgs a) {
 #pragma unroll
     for (int m = 0; m < HFM; ++m)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) Ah[(m * 16 + lg * 4 + j) * ldh + cc + lr] = f2bf(fmaxf(acc[m][0][j], 0.f));
+      for (int j = 0; j < 4; ++j) Ah[sw_off(m * 16 + lg * 4 + j, cc + lr, ldh)] = f2bf(fmaxf(acc[m][0][j], 0.f));
   }
-  tr_prefetch(a.Wfc, wave * 16, E, H, lane, pre);
+  if (wave < n1) {
+    const bf16_t* Bf;
+    int cc;
+    job1(wave, Bf, cc);
+    tr_prefetch(Bf, cc, 1 << 30, H, lane, pre);
+  }
   __syncthreads();
   TR_STAMP(2);
   tr_lds_to_kt(Ah, ldh, H, r0, a.h_kt);
 
-  // S2: emb = h @ Wfc^T + bfc
-  for (int cc = wave * 16; cc < E; cc += HNW * 16) {
-    float4_t acc[HFM][1];
-    tl_zero(acc);
-    tr_gemm(Ah, ldh, a.Wfc, cc, H, acc, lane, pre);
-    if (cc + HNW * 16 < E) tr_prefetch(a.Wfc, cc + HNW * 16, E, H, lane, pre);
-    const int col = cc + lr;
-    const float b = a.bfc[col];
-#pragma unroll
-    for (int m = 0; m < HFM; ++m) {
-      float e[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        e[j] = bf2f(f2bf(acc[m][0][j] + b));
-        Eb[(m * 16 + lg * 4 + j) * lde + col] = f2bf(e[j]);
-      }
-      kt_store4(a.emb_kt, r0 + m * 16 + lg * 4, col, E, e[0], e[1], e[2], e[3]);
-    }
-  }
-  tr_prefetch(a.Wout, wave * 16, C, E, lane, pre);
-  __syncthreads();
-  TR_STAMP(3);
-
-  // S3: logits = emb @ Wout^T ; dlogits, loss, F1 counts (padded label columns excluded)
+  // P1: logits (+ loss, dlogits, F1 counts; padded label columns excluded) and emb
   float lsum = 0.f;
   int tp = 0, fp = 0, fn = 0;
-  for (int cc = wave * 16; cc < C; cc += HNW * 16) {
+  for (int j = wave; j < n1; j += HNW) {
+    const bf16_t* Bf;
+    int cc;
+    job1(j, Bf, cc);
     float4_t acc[HFM][1];
     tl_zero(acc);
-    tr_gemm(Eb, lde, a.Wout, cc, E, acc, lane, pre);
-    if (cc + HNW * 16 < C) tr_prefetch(a.Wout, cc + HNW * 16, C, E, lane, pre);
+    tr_gemm(Ah, ldh, Bf, cc, H, acc, lane, pre);
     const int col = cc + lr;
-    const bool valid = col < a.C_real;
+    if (j < nl) {
+      const bool valid = col < a.C_real;
+      const float bias = a.bc[col];
 #pragma unroll
-    for (int m = 0; m < HFM; ++m) {
-      float d[4];
+      for (int m = 0; m < HFM; ++m) {
+        float d[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = m * 16 + lg * 4 + j;
-        const float xv = acc[m][0][j];
-        const float y = a.label_mode < 2 ? ((lab_s[row] == col) ? 1.f : 0.f) : bf2f(Ly[row * C + col]);
-        const float p = 1.f / (1.f + __expf(-xv));
-        if (valid) {
-          lsum += fmaxf(xv, 0.f) - xv * y + log1pf(__expf(-fabsf(xv)));
-          const bool pred = xv >= 0.f, pos = y > 0.5f;
-          tp += pred && pos;
-          fp += pred && !pos;
-          fn += !pred && pos;
+        for (int jj = 0; jj < 4; ++jj) {
+          const int row = m * 16 + lg * 4 + jj;
+          const float xv = acc[m][0][jj] + bias;
+          const float y = a.label_mode < 2 ? ((lab_s[row] == col) ? 1.f : 0.f) : bf2f(Ly[row * C + col]);
+          const float p = 1.f / (1.f + __expf(-xv));
+          if (valid) {
+            lsum += fmaxf(xv, 0.f) - xv * y + log1pf(__expf(-fabsf(xv)));
+            const bool pred = xv >= 0.f, pos = y > 0.5f;
+            tp += pred && pos;
+            fp += pred && !pos;
+            fn += !pred && pos;
+          }
+          d[jj] = valid ? bf2f(f2bf((p - y) * a.inv_scale)) : 0.f;
+          Dl[sw_off(row, col, ldc)] = f2bf(d[jj]);
         }
-        d[j] = valid ? bf2f(f2bf((p - y) * a.inv_scale)) : 0.f;
-        Dl[row * ldc + col] = f2bf(d[j]);
+        kt_store4(a.dlog_kt, r0 + m * 16 + lg * 4, col, C, d[0], d[1], d[2], d[3]);
       }
-      kt_store4(a.dlog_kt, r0 + m * 16 + lg * 4, col, C, d[0], d[1], d[2], d[3]);
+    } else {
+      const float b = a.bfc[col];
+#pragma unroll
+      for (int m = 0; m < HFM; ++m)
+        kt_store4(a.emb_kt, r0 + m * 16 + lg * 4, col, E, acc[m][0][0] + b, acc[m][0][1] + b, acc[m][0][2] + b,
+                  acc[m][0][3] + b);
+    }
+    if (j + HNW < n1) {  // (after the epilogue: the loss math keeps no prefetch registers live)
+      const bf16_t* Bn;
+      int cn;
+      job1(j + HNW, Bn, cn);
+      tr_prefetch(Bn, cn, 1 << 30, H, lane, pre);
     }
   }
   {
@@ -977,9 +1081,14 @@ __global__ __launch_bounds__(HNW * 64) void tr_head_kernel(TrHeadArgs a) {
       red_s[wave][3] = static_cast<float>(fn);
     }
   }
-  tr_prefetch(a.WoutT, wave * 16, E, C, lane, pre);
+  if (wave < n2) {
+    const bf16_t* Bf;
+    int cc, K;
+    job2(wave, Bf, cc, K);
+    tr_prefetch(Bf, cc, 1 << 30, K, lane, pre);
+  }
   __syncthreads();
-  TR_STAMP(4);
+  TR_STAMP(3);
   if (threadIdx.x < 4) {  // per-block sums, plain stores (no contended atomics)
     float v = 0.f;
 #pragma unroll
@@ -987,62 +1096,62 @@ __global__ __launch_bounds__(HNW * 64) void tr_head_kernel(TrHeadArgs a) {
     a.head_part[blockIdx.x * 4 + threadIdx.x] = threadIdx.x == 0 ? v * a.inv_scale : v;
   }
 
-  // S4: demb = dlogits @ Wout ; dbfc = column sums
-  for (int cc = wave * 16; cc < E; cc += HNW * 16) {
+  // P2: g = (dlogits Wc) * relu'(h); demb = dlogits Wout (+ fc-bias column sums); emb rest
+  for (int j = wave; j < n2; j += HNW) {
+    const bf16_t* Bf;
+    int cc, K;
+    job2(j, Bf, cc, K);
     float4_t acc[HFM][1];
     tl_zero(acc);
-    tr_gemm(Dl, ldc, a.WoutT, cc, C, acc, lane, pre);
-    if (cc + HNW * 16 < E) tr_prefetch(a.WoutT, cc + HNW * 16, E, C, lane, pre);
+    tr_gemm(j < nh + ne ? Dl : Ah, j < nh + ne ? ldc : ldh, Bf, cc, K, acc, lane, pre);
     const int col = cc + lr;
-    float cs = 0.f;
+    if (j < nh) {
 #pragma unroll
-    for (int m = 0; m < HFM; ++m) {
-      float e[4];
+      for (int m = 0; m < HFM; ++m) {
+        float e[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        cs += acc[m][0][j];
-        e[j] = bf2f(f2bf(acc[m][0][j]));
-        Db[(m * 16 + lg * 4 + j) * ldd + col] = f2bf(e[j]);
+        for (int jj = 0; jj < 4; ++jj) {
+          const int row = m * 16 + lg * 4 + jj;
+          e[jj] = bf2f(f2bf(bf_pos(Ah[sw_off(row, col, ldh)]) ? acc[m][0][jj] : 0.f));
+          Gb[sw_off(row, col, ldh)] = f2bf(e[jj]);
+        }
+        kt_store4(a.g_kt, r0 + m * 16 + lg * 4, col, H, e[0], e[1], e[2], e[3]);
       }
-      kt_store4(a.demb_kt, r0 + m * 16 + lg * 4, col, E, e[0], e[1], e[2], e[3]);
+    } else if (j < nh + ne) {
+      float cs = 0.f;
+#pragma unroll
+      for (int m = 0; m < HFM; ++m) {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) cs += acc[m][0][jj];
+        kt_store4(a.demb_kt, r0 + m * 16 + lg * 4, col, E, acc[m][0][0], acc[m][0][1], acc[m][0][2], acc[m][0][3]);
+      }
+      cs += __shfl_xor(cs, 16, 64);
+      cs += __shfl_xor(cs, 32, 64);
+      if (lg == 0) a.dbfc_part[static_cast<int64_t>(blockIdx.x) * E + col] = cs;
+    } else {
+      const float b = a.bfc[col];
+#pragma unroll
+      for (int m = 0; m < HFM; ++m)
+        kt_store4(a.emb_kt, r0 + m * 16 + lg * 4, col, E, acc[m][0][0] + b, acc[m][0][1] + b, acc[m][0][2] + b,
+                  acc[m][0][3] + b);
     }
-    cs += __shfl_xor(cs, 16, 64);
-    cs += __shfl_xor(cs, 32, 64);
-    if (lg == 0) a.dbfc_part[static_cast<int64_t>(blockIdx.x) * E + col] = cs;
-  }
-  tr_prefetch(a.WfcT, wave * 16, H, E, lane, pre);
-  __syncthreads();
-  TR_STAMP(5);
-
-  // S5: g = (demb @ Wfc) * (h > 0) -> Eb, g_kt
-  for (int cc = wave * 16; cc < H; cc += HNW * 16) {
-    float4_t acc[HFM][1];
-    tl_zero(acc);
-    tr_gemm(Db, ldd, a.WfcT, cc, E, acc, lane, pre);
-    if (cc + HNW * 16 < H) tr_prefetch(a.WfcT, cc + HNW * 16, H, E, lane, pre);
-    const int col = cc + lr;
-#pragma unroll
-    for (int m = 0; m < HFM; ++m) {
-      float e[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = m * 16 + lg * 4 + j;
-        e[j] = bf2f(f2bf(bf_pos(Ah[row * ldh + col]) ? acc[m][0][j] : 0.f));
-        Eb[row * lde + col] = f2bf(e[j]);
-      }
-      kt_store4(a.g_kt, r0 + m * 16 + lg * 4, col, H, e[0], e[1], e[2], e[3]);
+    if (j + HNW < n2) {
+      const bf16_t* Bn;
+      int cn, Kn;
+      job2(j + HNW, Bn, cn, Kn);
+      tr_prefetch(Bn, cn, 1 << 30, Kn, lane, pre);
     }
   }
   if (a.dA) tr_prefetch(a.WT, wave * 16, Hin2, H, lane, pre);
   __syncthreads();
-  TR_STAMP(6);
+  TR_STAMP(4);
 
-  // S6: dA = g @ W (fp32 rows) for the layer below
+  // P3: dA = g @ W (fp32 rows) for the layer below
   if (a.dA) {
     for (int cc = wave * 16; cc < Hin2; cc += HNW * 16) {
       float4_t acc[HFM][1];
       tl_zero(acc);
-      tr_gemm(Eb, lde, a.WT, cc, H, acc, lane, pre);
+      tr_gemm(Gb, ldh, a.WT, cc, H, acc, lane, pre);
       if (cc + HNW * 16 < Hin2) tr_prefetch(a.WT, cc + HNW * 16, Hin2, H, lane, pre);
 #pragma unroll
       for (int m = 0; m < HFM; ++m)
@@ -1050,7 +1159,7 @@ __global__ __launch_bounds__(HNW * 64) void tr_head_kernel(TrHeadArgs a) {
         for (int j = 0; j < 4; ++j) a.dA[(r0 + m * 16 + lg * 4 + j) * Hin2 + cc + lr] = acc[m][0][j];
     }
   }
-  TR_STAMP(7);
+  TR_STAMP(5);
 #undef TR_STAMP
 }
 
@@ -1102,8 +1211,11 @@ __device__ __forceinline__ uint4_t tr_route_frag(const TrDwProb& pr, const Route
 #ifndef TR_RKB
 #define TR_RKB 8
 #endif
-// kRKB k-blocks per stage; the double-buffered G tile takes 2 * kRKB * 5 KiB of LDS
-constexpr int kRP = 64, kRQ = 128, kRKB = TR_RKB, kRLd = 40;
+// kRKB k-blocks per stage; the double-buffered G tile takes 2 * kRKB * 4 KiB of LDS.
+// G^T tile [64 p][32 rows], 16-B chunks swizzled (rt_off, 4 chunks per row): the MFMA
+// fragment reads and the builder's stores (lanes 4i..4i+3 = the 4 chunks of p-row i, so
+// an 8-lane store group covers two whole rows) are bank-conflict-free
+constexpr int kRP = 64, kRQ = 128, kRKB = TR_RKB, kRLd = 32;
 
 struct RouteStage {
   RouteRaw r[kRKB];
@@ -1120,7 +1232,8 @@ __device__ __forceinline__ void tr_dw_route_body(const TrDwProb& pr, int b, Rout
   const int tp = tile / pr.tiles_q, tq = tile - tp * pr.tiles_q;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int lr = lane & 15, lk = (lane >> 4) * 8;
-  const int bp = tp * kRP + (tid & 63), blk = (tid >> 6) * 8;  // builder: column p, rows blk..+7
+  const int bpl = tid >> 2, blk = (tid & 3) * 8;  // builder: column p = bpl, rows blk..+7
+  const int bp = tp * kRP + bpl;
   const int wq = tq * kRQ + wave * 32;                           // MFMA: columns wq..+31, all 64 rows
   const int64_t Q = pr.Q;
   const bool qok = wq < Q;  // uniform
@@ -1145,7 +1258,7 @@ __device__ __forceinline__ void tr_dw_route_body(const TrDwProb& pr, int b, Rout
 #pragma unroll
       for (int u = 0; u < kRKB; ++u) {
         const uint4_t fr = (mbs + u) < mb1 ? tr_route_frag(pr, st.r[u], mbs + u, blk) : uint4_t{0u, 0u, 0u, 0u};
-        *reinterpret_cast<uint4_t*>(&gs[buf][u][(tid & 63) * kRLd + blk]) = fr;
+        *reinterpret_cast<uint4_t*>(&gs[buf][u][rt_off(bpl, blk)]) = fr;
       }
     };
     auto compute = [&](const RouteStage& st, int buf, int mbs) {
@@ -1156,7 +1269,7 @@ __device__ __forceinline__ void tr_dw_route_body(const TrDwProb& pr, int b, Rout
         uint4_t a[4];
 #pragma unroll
         for (int fm = 0; fm < 4; ++fm)
-          a[fm] = *reinterpret_cast<const uint4_t*>(&gs[buf][u][(fm * 16 + lr) * kRLd + lk]);
+          a[fm] = *reinterpret_cast<const uint4_t*>(&gs[buf][u][rt_off(fm * 16 + lr, lk)]);
 #pragma unroll
         for (int fn = 0; fn < 2; ++fn)
 #pragma unroll
@@ -1417,28 +1530,23 @@ size_t eh_tr_fwd_lds(int D, int H, int bm, int FL, int mode) {
   size_t b = static_cast<size_t>(bm) * (K2 + 8) * sizeof(bf16_t);
   if (mode != 1 && !alias_out) b += static_cast<size_t>(bm) * (kTrBN + 8) * sizeof(bf16_t);
   if (mode != 2) b += static_cast<size_t>(bm) * (1 + FL) * sizeof(int32_t);
-  if (TR_FWD_DEDUP && mode != 2) b += static_cast<size_t>(bm) * (1 + FL) * sizeof(int32_t);  // dedup counts
   return b;
 }
 
-static size_t pk_lds(int D, int H) {
-  const int K2 = 2 * D;
-  const int w = (K2 > H ? K2 : H) + 8;
-  return (static_cast<size_t>(H) * K2 + 32 * static_cast<size_t>(w)) * sizeof(bf16_t);
+size_t eh_tr_fwd2_lds(int D, int FL) {
+  return static_cast<size_t>(kF2Rows) * 2 * D * sizeof(bf16_t) +
+         static_cast<size_t>(kTrBN) * kF2Ldt * sizeof(bf16_t) + static_cast<size_t>(kF2Rows) * (1 + FL) * sizeof(int32_t);
 }
 
-// the persistent layer-0 kernel applies (see tr_fwd_pk_kernel)
-static bool pk_fits(const TrFwdArgs& a, int feat_fp32) {
-  static const bool on = [] {
-    const char* e = std::getenv("EULER_AMD_PK");  // opt-in: measured slower than tr_fwd_kernel so far
-    return e && e[0] == '1';
+// the 64-row / 8-wave layer-0 kernel applies (EULER_AMD_FWD2=0 disables it)
+static bool fwd2_fits(const TrFwdArgs& a) {
+  static const bool off = [] {
+    const char* e = std::getenv("EULER_AMD_FWD2");
+    return e && e[0] == '0';
   }();
-  if (!on) return false;
-  if (!a.a_kt || !a.mask || !a.nodes || !a.leaf) return false;
-  if ((1 << a.logPg) > 32 || a.M % 32 != 0) return false;
-  if (a.H > 256 || a.H > 2 * a.D || a.H % 64 != 0 || a.D > 128 || a.D % 16 != 0) return false;
-  if (a.FL > (feat_fp32 ? 10 : 25)) return false;
-  return pk_lds(a.D, a.H) <= 160 * 1024;
+  if (off || !a.a_kt) return false;
+  if (a.D % 64 != 0 || a.M % kF2Rows != 0 || a.logPg < 2 || (1 << a.logPg) > kF2Rows) return false;
+  return eh_tr_fwd2_lds(a.D, a.FL) <= 80 * 1024;  // two blocks per CU
 }
 
 hipError_t eh_tr_sample(const TrSampleArgs* a, hipStream_t s) {
@@ -1463,35 +1571,27 @@ hipError_t eh_tr_fwd(const TrFwdArgs* a, int mode, int feat_fp32, int bm, hipStr
                     a->Fg >= (1 << a->logPg)))
     return hipErrorInvalidValue;
   if (mode == 2 && feat_fp32) return hipErrorInvalidValue;
-  if (mode == 0 && pk_fits(*a, feat_fp32)) {
-    static int ncu = 0;
-    if (ncu == 0) {
-      int dev = 0;
-      EULER_HIP_CHECK(hipGetDevice(&dev));
-      EULER_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    }
-    const int ntiles = static_cast<int>(a->M / 32);
-    const int grid = ntiles < ncu ? ntiles : ncu;
-    const size_t plds = pk_lds(a->D, a->H);
-#define TR_PK(FT, NFV)                                                                                        \
-  do {                                                                                                        \
-    EULER_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(tr_fwd_pk_kernel<FT, NFV>),             \
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(plds))); \
-    hipLaunchKernelGGL((tr_fwd_pk_kernel<FT, NFV>), dim3(grid), dim3(kPkThreads), plds, s, *a, ntiles);      \
-    return hipGetLastError();                                                                                 \
+  if (a->ncomb < 0 || (a->ncomb > 0 && (mode == 2 || !a->comb.wout || !a->comb.wfc || !a->comb.bfc || !a->comb.Wc ||
+                                        !a->comb.WcT || !a->comb.bc || a->comb.C != a->ncomb * kTrCombRows ||
+                                        a->comb.H % 32 != 0 || a->comb.C % 32 != 0)))
+    return hipErrorInvalidValue;
+  if (mode == 0 && fwd2_fits(*a)) {
+    const size_t l2 = eh_tr_fwd2_lds(a->D, a->FL);
+    const dim3 g2(static_cast<uint32_t>(a->M / kF2Rows + a->ncomb));
+#define TR_FWD2(FT)                                                                                        \
+  do {                                                                                                     \
+    EULER_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(tr_fwd2_kernel<FT>),                \
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(l2))); \
+    hipLaunchKernelGGL((tr_fwd2_kernel<FT>), g2, dim3(kF2Threads), l2, s, *a);                             \
+    return hipGetLastError();                                                                              \
   } while (0)
-    if (feat_fp32) {
-      TR_PK(float, 10);
-    } else {
-      if (a->FL <= 10) TR_PK(bf16_t, 10);
-      if (a->FL <= 16) TR_PK(bf16_t, 16);
-      TR_PK(bf16_t, 25);
-    }
-#undef TR_PK
+    if (feat_fp32) TR_FWD2(float);
+    TR_FWD2(bf16_t);
+#undef TR_FWD2
   }
   const size_t lds = eh_tr_fwd_lds(a->D, a->H, bm, a->FL, mode);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  const dim3 grid(static_cast<uint32_t>(a->M / bm));
+  const dim3 grid(static_cast<uint32_t>(a->M / bm + a->ncomb));
 #define TR_FWD(FT, BMV, MODEV)                                                                               \
   do {                                                                                                       \
     EULER_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(tr_fwd_kernel<FT, BMV, MODEV>),         \
@@ -1520,14 +1620,15 @@ hipError_t eh_tr_fwd(const TrFwdArgs* a, int mode, int feat_fp32, int bm, hipStr
 }
 
 size_t eh_tr_head_lds(int Hin2, int H, int E, int C, int label_mode) {
-  const int ldmax = (E > H ? E : H);
-  size_t el = static_cast<size_t>(HB) * ((Hin2 + 8) + (H + 8) + (ldmax + 8) + (E + 8) + (C + 8));
+  (void)E;
+  size_t el = static_cast<size_t>(HB) * ((Hin2 + 16) + 2 * (H + 16) + (C + 16));
   if (label_mode == 2) el += static_cast<size_t>(HB) * C;
   return el * sizeof(bf16_t);
 }
 
 hipError_t eh_tr_head(const TrHeadArgs* a, int64_t B, hipStream_t s) {
-  if (!a->A || !a->W || !a->Wfc || !a->WfcT || !a->Wout || !a->WoutT || !a->bfc || !a->roots || !a->labels ||
+  if (!a->A || !a->W || !a->Wfc || !a->WfcT || !a->Wout || !a->WoutT || !a->Wc || !a->WcT || !a->bc || !a->bfc ||
+      !a->roots || !a->labels ||
       !a->A_kt || !a->h_kt || !a->emb_kt || !a->dlog_kt || !a->demb_kt || !a->g_kt || !a->dbfc_part || !a->head_part ||
       (a->dA && !a->WT))
     return hipErrorInvalidValue;

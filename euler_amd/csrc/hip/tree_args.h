@@ -55,6 +55,22 @@ struct TrSampleArgs {
   int32_t* leaf;         // [M][FL] leaf samples
 };
 
+// fc and out_fc combined: there is no nonlinearity between them, so the head computes
+// logits = h Wc^T + bc and the logits' gradient to h as dlog Wc with Wc = Wout Wfc [C][H]
+// and bc = Wout bfc [C] (two dependent GEMM phases fewer on the head's critical path; emb
+// and demb, needed only by the fc / out_fc weight gradients, are computed off it).  Wc is
+// rebuilt every step from the fp32 masters by extra blocks of the first forward launch.
+struct TrCombArgs {
+  const float* wout;  // [C][E] fp32 (flat parameters)
+  const float* wfc;   // [E][H] fp32
+  const float* bfc;   // [E]
+  int32_t C, E, H;
+  uint16_t* Wc;       // fm [C][H] bf16
+  uint16_t* WcT;      // fm [H][C] bf16
+  float* bc;          // [C]
+};
+constexpr int kTrCombRows = 4;  // rows of Wc per combination block
+
 // one fused SAGE layer: mode 0 = gather (sampled ids) + GEMM + tree-mean epilogue (layer 0),
 // mode 1 = gather only, writing [x_self | mean x_nbr] rows (1-hop models),
 // mode 2 = rows + GEMM + tree-mean epilogue (inner layers of 3-hop models)
@@ -80,6 +96,8 @@ struct TrFwdArgs {
   int32_t* roots_cur;       // ... copied here for the head (the sampler may refill roots_in)
   int32_t B;
   long long* prof;       // optional per-block phase stamps [grid][8]
+  TrCombArgs comb;       // modes 0/1: blocks [0, ncomb) build the head's Wc / WcT / bc
+  int32_t ncomb;
 };
 
 // head: last SAGE conv + fc + out_fc + sigmoid-CE + backward down to dA, kTrHeadRows roots / block
@@ -87,7 +105,9 @@ struct TrHeadArgs {
   const uint16_t* A;     // [B][Hin2] bf16 rows [self | mean]
   int32_t Hin2, H, E, C, C_real;
   const uint16_t *W, *WT, *Wfc, *WfcT, *Wout, *WoutT;  // fm shadows
+  const uint16_t *Wc, *WcT;  // fm Wout Wfc and its transpose (TrCombArgs)
   const float* bfc;      // [E]
+  const float* bc;       // [C] Wout bfc
   const int32_t* roots;  // [B] (the forward's copy of the batch's roots)
   const void* labels;    // mode 0: int16 [N] class ids, 1: int32 [N], 2: bf16 [N][C] dense
   int32_t label_mode;
@@ -187,5 +207,6 @@ hipError_t eh_tr_dw(euler_hip::TrDwLaunch* p, hipStream_t s);
 // sampler blocks.
 hipError_t eh_tr_opt(const euler_hip::TrOptArgs* a, int mode, hipStream_t s);
 size_t eh_tr_fwd_lds(int D, int H, int bm, int FL, int mode);
+size_t eh_tr_fwd2_lds(int D, int FL);
 size_t eh_tr_head_lds(int Hin2, int H, int E, int C, int label_mode);
 }

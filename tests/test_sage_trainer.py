@@ -198,9 +198,10 @@ def test_graph_replay_matches_eager(cuda):
 
 @pytest.mark.gpu
 def test_grad_sync_handoff_fp32_and_bf16(cuda):
-    """Data-parallel path: reduce -> grad_sync(grad) -> optimizer.  With an identity sync
-    the fp32 hand-off reproduces the fused single-process step exactly; the bf16 hand-off
-    (half the all-reduce bytes) tracks it within bf16 rounding."""
+    """Data-parallel path: per bucket reduce -> grad_sync(bucket) (two buckets, the head
+    bucket first, overlapped with the routed dW) -> optimizer.  With an identity sync the
+    fp32 hand-off reproduces the fused single-process step exactly; the bf16 hand-off (half
+    the all-reduce bytes) tracks it within bf16 rounding."""
     ref = _trainer(cuda, [5, 3], [64, 64, 32], 32)
     f32 = _trainer(cuda, [5, 3], [64, 64, 32], 32)
     b16 = _trainer(cuda, [5, 3], [64, 64, 32], 32)
@@ -208,7 +209,7 @@ def test_grad_sync_handoff_fp32_and_bf16(cuda):
     seen = []
 
     def sync(g):
-        seen.append(g.dtype)
+        seen.append((g.dtype, g.numel()))
         return 1.0
 
     lr, lf, lb = [], [], []
@@ -219,7 +220,10 @@ def test_grad_sync_handoff_fp32_and_bf16(cuda):
         lr.append(float(ref.loss.item()))
         lf.append(float(f32.loss.item()))
         lb.append(float(b16.loss.item()))
-    assert seen[0] == torch.float32 and seen[1] == torch.bfloat16
+    (_, a0, a1), (_, b0, b1) = f32.grad_buckets()
+    assert seen[:4] == [(torch.float32, a1 - a0), (torch.float32, b1 - b0), (torch.bfloat16, a1 - a0),
+                        (torch.bfloat16, b1 - b0)]
+    assert a1 - a0 + b1 - b0 == f32.grad.numel()
     np.testing.assert_allclose(lf, lr, rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(lb, lr, rtol=0.03, atol=1e-3)
 

@@ -156,8 +156,7 @@ for st in "${S[@]}"; do
     kernels_sizes)
       for nn in 2000000 100000000; do
         run "tree_kernels_n$nn" 300 python -u tools/tree_kernels.py --num-nodes $nn
-      done
-      EULER_AMD_NO_PK=1 run tree_kernels_nopk 300 python -u tools/tree_kernels.py ;;
+      done ;;
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench_small)
@@ -171,6 +170,16 @@ for st in "${S[@]}"; do
           --master-addr 127.0.0.1 --master-port 29541 bench.py --force-dist --grad-reduce-dtype $dt \
           --steps 200 --warmup 20 || exit $?
       done ;;
+    trace_bench)
+      # whole-step timeline of the bench (dp1, then the one-rank process-group path)
+      run trace_bench 300 rocprofv3 --kernel-trace -d "$OUT/trace_bench" -o run --output-format csv -- \
+          python3 bench.py --num-nodes 10000000 --steps 30 --warmup 5 && \
+      python tools/trace_gaps.py "$OUT/trace_bench/run_kernel_trace.csv" --last 2 > "$OUT/trace_bench_gaps.txt" 2>&1
+      RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29561 \
+        run trace_dist 300 rocprofv3 --kernel-trace -d "$OUT/trace_dist" -o run --output-format csv -- \
+          python3 bench.py --num-nodes 10000000 --steps 30 --warmup 5 --force-dist && \
+      python tools/trace_gaps.py "$OUT/trace_dist/run_kernel_trace.csv" --last 2 > "$OUT/trace_dist_gaps.txt" 2>&1
+      cat "$OUT/trace_bench_gaps.txt" "$OUT/trace_dist_gaps.txt" ;;
     pmc_lds)
       PASSES="SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE" \
         run pmc_lds 300 bash tools/pmc_passes.sh lds "$PWD/tools/tree_kernels.py" --reps 10 ;;
