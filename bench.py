@@ -56,6 +56,9 @@ def parse_args(argv=None):
     p.add_argument("--grad-reduce-dtype", choices=["bf16", "fp32"], default="fp32",
                    help="dtype of the data-parallel gradient all-reduce (bf16: half the bytes on xGMI, "
                         "summed in bf16 by RCCL)")
+    p.add_argument("--grad-buckets", type=int, choices=[1, 2], default=1,
+                   help="data-parallel gradient buckets: 1 = one all-reduce after the reduce (one stream); "
+                        "2 = the head-layer bucket's reduce + all-reduce overlap the routed dW on a side stream")
     p.add_argument("--force-dist", action="store_true",
                    help="take the multi-GPU code path (process group, all-reduce in the step) even with one rank")
     return p.parse_args(argv)
@@ -122,7 +125,7 @@ def main(argv=None):
 
     dims = [args.hidden_dim] * (len(fanouts) + 1)  # reference run_graphsage: [hidden] * (layers + 1)
     tr = SageTrainer(graph, B, fanouts, dims, args.label_dim, features=feats, labels=labels, learning_rate=args.lr,
-                     init_seed=args.seed, keep_samples=False)
+                     init_seed=args.seed, keep_samples=False, grad_buckets=args.grad_buckets)
     grad_sync = None
     if dist_on:
         dist.broadcast(tr.flat, 0)
@@ -210,8 +213,8 @@ def main(argv=None):
                 "hidden_dim": args.hidden_dim,
                 "label_dim": args.label_dim,
                 "hipgraph": use_graph,
-                "grad_sync": f"rccl all-reduce ({args.grad_reduce_dtype} gradient) in the captured step"
-                if dist_on else None,
+                "grad_sync": f"rccl all-reduce ({args.grad_reduce_dtype} gradient, {args.grad_buckets} bucket(s)) "
+                             f"in the captured step" if dist_on else None,
                 "impl": "euler_amd.models.sage_trainer.SageTrainer (4 fused gfx950 launches per step)",
                 "loss_first_last": [round(first_loss, 4), round(last_loss, 4)],
                 "baseline": base_note,

@@ -357,7 +357,7 @@ class TreePlan {
     const int64_t H = dims_[L_ - 1];
     TORCH_CHECK(off[L_ + 1] - off[L_] == (int64_t)E_ * H && off[L_ + 3] - off[L_ + 2] == (int64_t)C_ * E_,
                 "TreePlan: fc / out_fc segments do not match E, H, C");
-    TORCH_CHECK(C_ % kTrCombRows == 0, "TreePlan: label width must be a multiple of the combination rows");
+    TORCH_CHECK(C_ % 16 == 0 && H % 64 == 0 && E_ % 32 == 0, "TreePlan: combination tiles need C % 16, H % 64, E % 32");
     float* base = flat.data_ptr<float>();
     TrCombArgs& c = fwd0_.comb;
     c.wfc = base + off[L_];
@@ -369,7 +369,7 @@ class TreePlan {
     c.Wc = owned_bf16((int64_t)C_ * H);
     c.WcT = owned_bf16((int64_t)C_ * H);
     c.bc = owned(C_);
-    fwd0_.ncomb = C_ / kTrCombRows;
+    fwd0_.ncomb = tr_comb_blocks(C_, static_cast<int>(H));
   }
 
   uint16_t* owned_bf16(int64_t n) {

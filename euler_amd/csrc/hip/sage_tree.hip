@@ -191,35 +191,71 @@ struct Feat8<float> {
 };
 
 // ----------------------------------------------------------------------------
-// combination block of a forward launch: kTrCombRows rows of Wc = Wout Wfc (fp32 FMA from
-// the fp32 masters, the thread of column h runs down E), their bf16 fm images Wc / WcT,
-// and bc = Wout bfc
+// combination blocks of a forward launch: Wc = Wout Wfc (fp32 FMA from the fp32 masters)
+// in [16 rows x 64 columns] tiles, one per block, plus bc = Wout bfc.  E is streamed
+// through LDS in chunks of 32 with the next chunk's loads in flight, so a block is a few
+// load latencies long and finishes well inside the forward's span (a per-thread serial
+// E loop made the whole launch wait on its dependent loads).
 // ----------------------------------------------------------------------------
+constexpr int kCbRows = 16, kCbCols = 64, kCbE = 32;
+constexpr size_t kCbLds = (kCbRows * kCbE + kCbE * kCbCols + kCbE) * sizeof(float);
+
 template <int NT>
-__device__ void tr_comb_block(const TrCombArgs& c, int blk) {
-  const int c0 = blk * kTrCombRows;
-  for (int h = threadIdx.x; h < c.H; h += NT) {
-    float acc[kTrCombRows];
+__device__ void tr_comb_block(const TrCombArgs& c, int blk, float* sm) {
+  static_assert((kCbRows * kCbE) % NT == 0 || NT % (kCbRows * kCbE) == 0, "comb tiling");
+  static_assert((kCbE * kCbCols) % NT == 0 && (kCbRows * kCbCols) % NT == 0, "comb tiling");
+  constexpr int WO = (kCbRows * kCbE + NT - 1) / NT, WF = kCbE * kCbCols / NT, OUT = kCbRows * kCbCols / NT;
+  float* wo_s = sm;                           // [16][32]
+  float* wf_s = wo_s + kCbRows * kCbE;        // [32][64]
+  float* bf_s = wf_s + kCbE * kCbCols;        // [32]
+  const int nhc = c.H / kCbCols;
+  const int c0 = (blk / nhc) * kCbRows, h0 = (blk % nhc) * kCbCols;
+  const int tid = threadIdx.x;
+  float acc[OUT];
 #pragma unroll
-    for (int r = 0; r < kTrCombRows; ++r) acc[r] = 0.f;
+  for (int k = 0; k < OUT; ++k) acc[k] = 0.f;
+  float bsum = 0.f;
+  float rwo[WO], rbf = 0.f, rwf[WF];
+  auto load = [&](int e0) {
+#pragma unroll
+    for (int k = 0; k < WO; ++k) {
+      const int i = tid + k * NT;
+      if (i < kCbRows * kCbE) rwo[k] = c.wout[static_cast<int64_t>(c0 + i / kCbE) * c.E + e0 + i % kCbE];
+    }
+    if (tid < kCbE) rbf = c.bfc[e0 + tid];
+#pragma unroll
+    for (int k = 0; k < WF; ++k) {
+      const int i = tid + k * NT;
+      rwf[k] = c.wfc[static_cast<int64_t>(e0 + i / kCbCols) * c.H + h0 + i % kCbCols];
+    }
+  };
+  load(0);
+  for (int e0 = 0; e0 < c.E; e0 += kCbE) {
+    __syncthreads();  // the previous chunk is consumed
+#pragma unroll
+    for (int k = 0; k < WO; ++k)
+      if (tid + k * NT < kCbRows * kCbE) wo_s[tid + k * NT] = rwo[k];
+    if (tid < kCbE) bf_s[tid] = rbf;
+#pragma unroll
+    for (int k = 0; k < WF; ++k) wf_s[tid + k * NT] = rwf[k];
+    __syncthreads();
+    if (e0 + kCbE < c.E) load(e0 + kCbE);
+#pragma unroll
+    for (int k = 0; k < OUT; ++k) {
+      const int o = tid + k * NT, r = o / kCbCols, h = o % kCbCols;
 #pragma unroll 8
-    for (int e = 0; e < c.E; ++e) {
-      const float w = c.wfc[static_cast<int64_t>(e) * c.H + h];
-#pragma unroll
-      for (int r = 0; r < kTrCombRows; ++r) acc[r] += c.wout[static_cast<int64_t>(c0 + r) * c.E + e] * w;
+      for (int e = 0; e < kCbE; ++e) acc[k] += wo_s[r * kCbE + e] * wf_s[e * kCbCols + h];
     }
+    if (h0 == 0 && tid < kCbRows)
+      for (int e = 0; e < kCbE; ++e) bsum += wo_s[tid * kCbE + e] * bf_s[e];
+  }
 #pragma unroll
-    for (int r = 0; r < kTrCombRows; ++r) {
-      c.Wc[fm_off(c0 + r, h, c.H)] = f2bf(acc[r]);
-      c.WcT[fm_off(h, c0 + r, c.C)] = f2bf(acc[r]);
-    }
+  for (int k = 0; k < OUT; ++k) {
+    const int o = tid + k * NT, r = c0 + o / kCbCols, h = h0 + o % kCbCols;
+    c.Wc[fm_off(r, h, c.H)] = f2bf(acc[k]);
+    c.WcT[fm_off(h, r, c.C)] = f2bf(acc[k]);
   }
-  if (threadIdx.x < kTrCombRows) {
-    const float* w = c.wout + static_cast<int64_t>(c0 + threadIdx.x) * c.E;
-    float b = 0.f;
-    for (int e = 0; e < c.E; ++e) b += w[e] * c.bfc[e];
-    c.bc[c0 + threadIdx.x] = b;
-  }
+  if (h0 == 0 && tid < kCbRows) c.bc[c0 + tid] = bsum;
 }
 
 // ----------------------------------------------------------------------------
@@ -277,7 +313,7 @@ __global__ __launch_bounds__(256, (BM == 32 ? TR_FWD_WAVES : 2)) void tr_fwd_ker
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   constexpr bool kGather = MODE != 2;
   if (static_cast<int>(blockIdx.x) < a.ncomb) {  // the head's Wc (first forward launch)
-    tr_comb_block<256>(a.comb, blockIdx.x);
+    tr_comb_block<256>(a.comb, blockIdx.x, reinterpret_cast<float*>(lds));
     return;
   }
   const int tb = static_cast<int>(blockIdx.x) - a.ncomb, ntb = static_cast<int>(gridDim.x) - a.ncomb;
@@ -560,7 +596,7 @@ __global__ __launch_bounds__(kF2Threads, 4) void tr_fwd2_kernel(TrFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   constexpr int BM = kF2Rows, NT = kF2Threads;
   if (static_cast<int>(blockIdx.x) < a.ncomb) {  // the head's Wc
-    tr_comb_block<NT>(a.comb, blockIdx.x);
+    tr_comb_block<NT>(a.comb, blockIdx.x, reinterpret_cast<float*>(lds));
     return;
   }
   const int tb = static_cast<int>(blockIdx.x) - a.ncomb, ntb = static_cast<int>(gridDim.x) - a.ncomb;
@@ -1572,11 +1608,13 @@ hipError_t eh_tr_fwd(const TrFwdArgs* a, int mode, int feat_fp32, int bm, hipStr
     return hipErrorInvalidValue;
   if (mode == 2 && feat_fp32) return hipErrorInvalidValue;
   if (a->ncomb < 0 || (a->ncomb > 0 && (mode == 2 || !a->comb.wout || !a->comb.wfc || !a->comb.bfc || !a->comb.Wc ||
-                                        !a->comb.WcT || !a->comb.bc || a->comb.C != a->ncomb * kTrCombRows ||
-                                        a->comb.H % 32 != 0 || a->comb.C % 32 != 0)))
+                                        !a->comb.WcT || !a->comb.bc || a->comb.C % kCbRows != 0 ||
+                                        a->comb.H % kCbCols != 0 || a->comb.E % kCbE != 0 ||
+                                        a->ncomb != (a->comb.C / kCbRows) * (a->comb.H / kCbCols))))
     return hipErrorInvalidValue;
   if (mode == 0 && fwd2_fits(*a)) {
-    const size_t l2 = eh_tr_fwd2_lds(a->D, a->FL);
+    size_t l2 = eh_tr_fwd2_lds(a->D, a->FL);
+    if (a->ncomb > 0 && l2 < kCbLds) l2 = kCbLds;
     const dim3 g2(static_cast<uint32_t>(a->M / kF2Rows + a->ncomb));
 #define TR_FWD2(FT)                                                                                        \
   do {                                                                                                     \
@@ -1589,7 +1627,8 @@ hipError_t eh_tr_fwd(const TrFwdArgs* a, int mode, int feat_fp32, int bm, hipStr
     TR_FWD2(bf16_t);
 #undef TR_FWD2
   }
-  const size_t lds = eh_tr_fwd_lds(a->D, a->H, bm, a->FL, mode);
+  size_t lds = eh_tr_fwd_lds(a->D, a->H, bm, a->FL, mode);
+  if (a->ncomb > 0 && lds < kCbLds) lds = kCbLds;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   const dim3 grid(static_cast<uint32_t>(a->M / bm + a->ncomb));
 #define TR_FWD(FT, BMV, MODEV)                                                                               \

@@ -69,7 +69,8 @@ struct TrCombArgs {
   uint16_t* WcT;      // fm [H][C] bf16
   float* bc;          // [C]
 };
-constexpr int kTrCombRows = 4;  // rows of Wc per combination block
+// combination tiles: 16 rows x 64 columns of Wc per block (C % 16, H % 64, E % 32 == 0)
+inline int tr_comb_blocks(int C, int H) { return (C / 16) * (H / 64); }
 
 // one fused SAGE layer: mode 0 = gather (sampled ids) + GEMM + tree-mean epilogue (layer 0),
 // mode 1 = gather only, writing [x_self | mean x_nbr] rows (1-hop models),

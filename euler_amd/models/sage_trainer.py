@@ -78,7 +78,7 @@ def _xavier(shape, gen):
 class SageTrainer:
     def __init__(self, graph, batch_size, fanouts, dims, label_dim, features=None, labels=None, metapath=None,
                  add_self_loops=False, optimizer="adam", learning_rate=0.01, betas=(0.9, 0.999), eps=1e-8,
-                 weight_decay=0.0, init=None, init_seed=0, keep_samples=True):
+                 weight_decay=0.0, init=None, init_seed=0, keep_samples=True, grad_buckets=1):
         self.graph = graph
         self.device = graph.device
         self.B = int(batch_size)
@@ -92,6 +92,9 @@ class SageTrainer:
         if self.B % 32:
             raise ValueError("batch_size must be a multiple of 32")
         self.conv_dims, self.E = dims[:-1], dims[-1]
+        if grad_buckets not in (1, 2):
+            raise ValueError("grad_buckets must be 1 or 2")
+        self.n_buckets = int(grad_buckets)
         self.C = int(label_dim)
         self.include_self = bool(add_self_loops)
         self.opt_name = optimizer
@@ -420,10 +423,14 @@ class SageTrainer:
 
     def grad_buckets(self):
         """(name, start, end) of the data-parallel gradient buckets in the flat layout, in
-        the order ``grad_sync`` receives them: "head" = the last conv, fc and out_fc (their
-        dW needs only the head's outputs), then "routed" = the inner convs, whose dW (the
-        tree-routed split-K problems, the longest launch of the backward) it overlaps."""
+        the order ``grad_sync`` receives them.  One bucket (default): the whole flat
+        gradient.  Two (``grad_buckets=2``): "head" = the last conv, fc and out_fc (their dW
+        needs only the head's outputs), then "routed" = the inner convs, whose dW (the
+        tree-routed split-K problems, the longest launch of the backward) the head
+        bucket's reduce and all-reduce overlap on a side stream."""
         o = self.offsets
+        if self.n_buckets == 1 or self.L == 1:
+            return [("all", 0, o[-1])]
         return [("head", o[self.L - 1], o[-1]), ("routed", 0, o[self.L - 1])]
 
     def step(self, grad_sync=None):
@@ -432,6 +439,11 @@ class SageTrainer:
         returns the scale applied to the summed gradient (1 / world); None = single
         process (fused reduce + optimizer launch).
 
+        One bucket (default): fwd -> head -> [bwd] -> dW -> reduce -> grad_sync -> optimizer
+        on one stream — four graph nodes plus the collective.  Inside a hipGraph a
+        side-stream fork / join costs ~5 us per edge on MI355X (measured:
+        profiles/r3_dist/), as much as the all-reduce it would hide at one rank.
+
         Single process: one stream, no forks (a hipGraph branch join costs more than the
         work it would overlap): fwd -> head -> [bwd] -> every dW in one launch ->
         optimizer.  The head launch also carries the sampler of the NEXT step's batch in
@@ -439,7 +451,7 @@ class SageTrainer:
         graph and the RNG counter the forward advanced; the head reads the forward's copy
         of the roots), so the sampler's dependent-load chain is off the critical path.
 
-        Data parallel: the dW of the "head" bucket (last conv, fc, out_fc) runs on a side
+        Two buckets: the dW of the "head" bucket (last conv, fc, out_fc) runs on a side
         stream next to the routed inner-layer dW; its split-K reduce and all-reduce then
         overlap the routed dW, and only the routed bucket's (smaller) all-reduce is on the
         critical path.  Both collectives are issued on the side stream in bucket order, so
@@ -455,6 +467,12 @@ class SageTrainer:
         if grad_sync is None:
             p.dw(self._dw_all)
             p.opt(2)
+        elif len(self.grad_buckets()) == 1:
+            p.dw(self._dw_all)
+            p.opt(0)
+            g = self.grad if getattr(self, "grad16", None) is None else self.grad16
+            scale = grad_sync(g)
+            p.opt(1, 1.0 if scale is None else float(scale))
         else:
             self._dist_backward(grad_sync)
         self._primed = True
@@ -657,10 +675,12 @@ class SageTrainer:
         (logical) parameter order, the same buckets in the same order, fp32 or bf16"""
         names = list(self._shapes)
         flat = torch.cat([self._cpu_params[k].grad.reshape(-1) for k in names])
-        cut = sum(self._cpu_params[k].numel() for k in names[: 2 * (self.L - 1)])  # routed convs first
         buf = flat.to(torch.bfloat16) if getattr(self, "_cpu_sync_bf16", False) else flat
-        scale = grad_sync(buf[cut:])
-        if cut:
+        if len(self.grad_buckets()) == 1:
+            scale = grad_sync(buf)
+        else:
+            cut = sum(self._cpu_params[k].numel() for k in names[: 2 * (self.L - 1)])  # routed convs first
+            scale = grad_sync(buf[cut:])
             grad_sync(buf[:cut])
         flat = buf.float()
         o = 0

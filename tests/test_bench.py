@@ -42,8 +42,8 @@ def test_bench_single_gpu_json():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("extra", [[], ["--no-graph"], ["--grad-reduce-dtype", "fp32"]],
-                         ids=["captured", "eager", "fp32_allreduce"])
+@pytest.mark.parametrize("extra", [[], ["--no-graph"], ["--grad-reduce-dtype", "bf16"], ["--grad-buckets", "2"]],
+                         ids=["captured", "eager", "bf16_allreduce", "two_buckets"])
 def test_bench_distributed_path_one_rank(extra):
     out = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
                 "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--force-dist"]

@@ -456,7 +456,7 @@ def test_checkpoint_reshards_on_world_size_change(tmp_path):
     assert torch.equal(reshard_rows([full[0::2], full[1::2]], 1, 3), full[1::3])
 
 
-def _worker_sage_dp(rank, world, port, q, dtype):
+def _worker_sage_dp(rank, world, port, q, dtype, buckets):
     """SageTrainer.step(grad_sync) on 2 gloo ranks with different sample streams: the
     parameters stay bit-identical across ranks and equal a single-process update on the
     summed gradients of the two ranks' batches, for 10 steps (fp32 or bf16 hand-off)."""
@@ -469,6 +469,7 @@ def _worker_sage_dp(rank, world, port, q, dtype):
 
         def make(r):
             tr = _trainer("cpu", [5, 3], [32, 32, 16], 5, seed=3)
+            tr.n_buckets = buckets
             tr.graph.manual_seed(1000 + r)  # per-rank sample stream
             tr.set_grad_sync_dtype(dtype)
             return tr
@@ -505,8 +506,8 @@ def _worker_sage_dp(rank, world, port, q, dtype):
         rp = ref[0].logical_params()
         oracle = all(torch.equal(mine[k], rp[k]) for k in names)
         moved = any(not torch.equal(mine[k], make(rank).logical_params()[k]) for k in names)
-        two_buckets = len(calls) == 20 and len(set(calls)) == 2
-        q.put((rank, f"sage_dp_{dtype}", bool(lockstep and oracle and moved and two_buckets)))
+        ncalls = len(calls) == 10 * buckets and len(set(calls)) == buckets
+        q.put((rank, f"sage_dp_{dtype}_{buckets}", bool(lockstep and oracle and moved and ncalls)))
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover
         import traceback
@@ -514,8 +515,8 @@ def _worker_sage_dp(rank, world, port, q, dtype):
         q.put((rank, "error", traceback.format_exc()))
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-def test_sage_trainer_data_parallel_lockstep(dtype):
-    res = _run(_worker_sage_dp, dtype)
+@pytest.mark.parametrize("dtype,buckets", [("fp32", 1), ("bf16", 1), ("fp32", 2), ("bf16", 2)])
+def test_sage_trainer_data_parallel_lockstep(dtype, buckets):
+    res = _run(_worker_sage_dp, dtype, buckets)
     assert not [r for r in res if r[1] == "error"], res
     assert len(res) == 2 and all(r[2] for r in res), res

@@ -205,6 +205,7 @@ def test_grad_sync_handoff_fp32_and_bf16(cuda):
     ref = _trainer(cuda, [5, 3], [64, 64, 32], 32)
     f32 = _trainer(cuda, [5, 3], [64, 64, 32], 32)
     b16 = _trainer(cuda, [5, 3], [64, 64, 32], 32)
+    f32.n_buckets = b16.n_buckets = 2  # the overlapped two-bucket path (one bucket: test_bench)
     b16.set_grad_sync_dtype(torch.bfloat16)
     seen = []
 

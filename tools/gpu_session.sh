@@ -165,10 +165,11 @@ for st in "${S[@]}"; do
       run bench_full 600 python bench.py --steps 200 --warmup 20 --log ;;
     dist_bench)
       # the multi-GPU code path (process group, bucketed all-reduce captured in the step) on one rank
-      for dt in ${DIST_DTYPES:-fp32 bf16}; do
-        run "bench_dist_$dt" 600 python -u -m torch.distributed.run --nnodes 1 --nproc-per-node 1 \
+      for cfg in ${DIST_CFGS:-fp32:1 fp32:2}; do
+        dt=${cfg%%:*}; nb=${cfg##*:}
+        run "bench_dist_${dt}_b$nb" 600 python -u -m torch.distributed.run --nnodes 1 --nproc-per-node 1 \
           --master-addr 127.0.0.1 --master-port 29541 bench.py --force-dist --grad-reduce-dtype $dt \
-          --steps 200 --warmup 20 || exit $?
+          --grad-buckets $nb --steps 200 --warmup 20 || exit $?
       done ;;
     trace_bench)
       # whole-step timeline of the bench (dp1, then the one-rank process-group path)
