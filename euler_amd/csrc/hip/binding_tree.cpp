@@ -357,19 +357,20 @@ class TreePlan {
     const int64_t H = dims_[L_ - 1];
     TORCH_CHECK(off[L_ + 1] - off[L_] == (int64_t)E_ * H && off[L_ + 3] - off[L_ + 2] == (int64_t)C_ * E_,
                 "TreePlan: fc / out_fc segments do not match E, H, C");
-    TORCH_CHECK(C_ % 16 == 0 && H % 64 == 0 && E_ % 32 == 0, "TreePlan: combination tiles need C % 16, H % 64, E % 32");
+    TORCH_CHECK(C_ % 16 == 0 && H % 16 == 0 && E_ % 32 == 0, "TreePlan: combination tiles need C % 16, H % 16, E % 32");
     float* base = flat.data_ptr<float>();
     TrCombArgs& c = fwd0_.comb;
-    c.wfc = base + off[L_];
     c.bfc = base + off[L_ + 1];
     c.wout = base + off[L_ + 2];
+    c.wout_sh = bf("Wout_sh", (int64_t)C_ * E_);
+    c.wfcT_sh = bf("Wfc_shT", (int64_t)E_ * H);
     c.C = C_;
     c.E = E_;
     c.H = static_cast<int32_t>(H);
     c.Wc = owned_bf16((int64_t)C_ * H);
     c.WcT = owned_bf16((int64_t)C_ * H);
     c.bc = owned(C_);
-    fwd0_.ncomb = tr_comb_blocks(C_, static_cast<int>(H));
+    fwd0_.ncomb = 1;  // requested; the launcher sizes it to the chosen kernel's waves per block
   }
 
   uint16_t* owned_bf16(int64_t n) {
@@ -592,6 +593,214 @@ class TreePlan {
   }
 };
 
+// Layer 0 of a 2-hop SAGE tower over GIVEN roots (pair / unsupervised models, where the
+// roots are a node's sampled positive and negatives): the tree sampler draws hop 1 and the
+// leaves from the roots in `roots_in`, tr_fwd (mode 0) gathers the leaf rows, runs the
+// layer-0 GEMM + ReLU and the tree mean of hop 1, producing the last conv's input rows
+// A1 = [h0(root) | mean h0(hop-1 nbrs)] [R][2H0] bf16.  The backward takes dA1 (fp32),
+// routes it through the tree and the ReLU bits inside the split-K dW kernel and reduces
+// the partials into the fp32 gradient of W0.  The rest of the tower (last conv, fc, loss)
+// is ordinary torch on [R][2H0] rows (euler_amd/models/sage_tower.py).
+class TowerPlan {
+ public:
+  explicit TowerPlan(py::dict d) : d_(d) {
+    R_ = geti("R");
+    F1_ = geti("F1");
+    F2_ = geti("F2");
+    logP_ = geti("logP");
+    D_ = geti("D");
+    H_ = geti("H");
+    self_ = geti("include_self");
+    dev_ = T("rng").device();
+    TORCH_CHECK(dev_.is_cuda(), "TowerPlan: tensors must be on the GPU");
+    TORCH_CHECK(R_ > 0 && R_ % 32 == 0, "TowerPlan: roots must be a positive multiple of 32");
+    TORCH_CHECK(logP_ >= 4 && (1 << logP_) > F1_ && F1_ >= 1 && F2_ >= 1, "TowerPlan: slot group too small");
+    TORCH_CHECK(D_ % 16 == 0 && H_ % 64 == 0, "TowerPlan: padded dims (D % 16, H % 64)");
+    M_ = R_ << logP_;
+    // graph + tree
+    torch::Tensor indptr = T("indptr"), rng = T("rng"), nbr = T("nbr"), cumw = T("cumw"), prob = T("node_prob");
+    need(indptr, torch::kInt64, -1, "indptr");
+    need(rng, torch::kInt64, 2, "rng");
+    const int64_t nt = geti("num_types");
+    TORCH_CHECK(nt >= 1 && nt <= 32 && (indptr.numel() - 1) % nt == 0, "TowerPlan: indptr must be [N*T+1]");
+    g_.indptr = indptr.data_ptr<int64_t>();
+    g_.num_types = static_cast<int32_t>(nt);
+    g_.num_rows = (indptr.numel() - 1) / nt;
+    need(nbr, torch::kInt32, -1, "nbr");
+    need(cumw, torch::kFloat32, nbr.numel(), "cumw");
+    g_.nbr = nbr.data_ptr<int32_t>();
+    g_.cumw = cumw.data_ptr<float>();
+    need(prob, torch::kFloat32, -1, "node_prob");
+    g_.pop = prob.numel();
+    g_.prob = prob.data_ptr<float>();
+    g_.alias = ptr<int32_t>("node_alias", torch::kInt32, g_.pop);
+    g_.root_rows = nullptr;
+    tree_.rng = rng.data_ptr<int64_t>();
+    tree_.root_in = ptr<int32_t>("roots_in", torch::kInt32, R_);
+    tree_.F1 = static_cast<int32_t>(F1_);
+    tree_.F2 = 0;
+    tree_.logP1 = static_cast<int32_t>(logP_);
+    tree_.logP2 = 0;
+    tree_.m1 = static_cast<uint32_t>(geti("mask1"));
+    tree_.m2 = 0u;
+    // sampler: level-1 slots (hop 1 of each root) and their F2 leaves
+    sample_.g = g_;
+    sample_.tr = tree_;
+    sample_.M = M_;
+    sample_.lv = 1;
+    sample_.FL = static_cast<int32_t>(F2_);
+    sample_.mL = static_cast<uint32_t>(geti("mask2"));
+    sample_.hopL = 2;
+    sample_.roots = owned_i32(R_);
+    sample_.nodes = ptr<int32_t>("nodes", torch::kInt32, M_);
+    sample_.leaf = ptr<int32_t>("leaf", torch::kInt32, M_ * F2_);
+    // layer 0 (mode 0)
+    torch::Tensor x = T("features");
+    TORCH_CHECK(x.dim() == 2 && x.size(1) == D_ && x.size(0) == g_.num_rows, "features must be [N, D]");
+    TORCH_CHECK(x.scalar_type() == torch::kBFloat16 || x.scalar_type() == torch::kFloat32, "features bf16 / fp32");
+    need(x, x.scalar_type(), -1, "features");
+    feat_fp32_ = x.scalar_type() == torch::kFloat32;
+    TrFwdArgs& a = fwd_;
+    a.x = x.data_ptr();
+    a.D = static_cast<int32_t>(D_);
+    a.M = M_;
+    a.FL = static_cast<int32_t>(F2_);
+    a.include_self = static_cast<int32_t>(self_);
+    a.inv_leaf = 1.f / static_cast<float>(F2_ + self_);
+    a.nodes = sample_.nodes;
+    a.leaf = sample_.leaf;
+    a.roots_in = sample_.roots;
+    a.roots_cur = owned_i32(R_);
+    a.B = static_cast<int32_t>(R_);
+    a.step = nullptr;
+    a.rng = rng.data_ptr<int64_t>();
+    a.W = ptr<uint16_t>("W0_sh", torch::kBFloat16, H_ * 2 * D_);
+    a.H = static_cast<int32_t>(H_);
+    a.a_kt = ptr<uint16_t>("A0_kt", torch::kBFloat16, M_ * 2 * D_);
+    a.mask = reinterpret_cast<uint32_t*>(ptr<int32_t>("mask0", torch::kInt32, (M_ / 32) * H_));
+    a.logPg = static_cast<int32_t>(logP_);
+    a.Fg = static_cast<int32_t>(F1_);
+    a.inv_grp = 1.f / static_cast<float>(F1_ + self_);
+    a.a_next = ptr<uint16_t>("A1", torch::kBFloat16, R_ * 2 * H_);
+    a.ncomb = 0;
+    bm_ = (1 << logP_) > 32 ? (1 << logP_) : 32;
+    TORCH_CHECK(bm_ <= 128 && M_ % bm_ == 0, "TowerPlan: sibling groups of at most 128 rows");
+    // routed dW of W0 (G routed from dA1 through the tree and the ReLU bits)
+    TrDwProb& p = prob_;
+    p.P = static_cast<int32_t>(H_);
+    p.Q = static_cast<int32_t>(2 * D_);
+    p.MB = static_cast<int32_t>(M_ / 32);
+    const int64_t tiles = (p.P / 64) * ((p.Q + 127) / 128);
+    const int64_t target = has("dw_route_wg") ? geti("dw_route_wg") : 256;
+    int64_t S = (target + tiles - 1) / tiles;
+    S = (S + 7) / 8 * 8;
+    if (S > (p.MB + 7) / 8 * 8) S = (p.MB + 7) / 8 * 8;
+    p.kps = static_cast<int32_t>((p.MB + S - 1) / S);
+    p.S = static_cast<int32_t>(S);
+    part_ = torch::empty({S * p.P * p.Q}, torch::TensorOptions().dtype(torch::kFloat32).device(dev_));
+    p.part = part_.data_ptr<float>();
+    p.G = nullptr;
+    p.X = a.a_kt;
+    p.route = 1;
+    p.dA = ptr<float>("dA1", torch::kFloat32, R_ * 2 * H_);
+    p.mask = a.mask;
+    p.logPg = static_cast<int32_t>(logP_);
+    p.Fg = static_cast<int32_t>(F1_);
+    p.include_self = static_cast<int32_t>(self_);
+    p.inv = 1.f / static_cast<float>(F1_ + self_);
+    // reduce into the fp32 gradient / bf16 shadow of the fp32 master (one weight segment)
+    TrOptArgs& o = opt_;
+    float* w = ptr<float>("W0", torch::kFloat32, H_ * 2 * D_);
+    o.p = o.m = o.v = w;
+    o.g = ptr<float>("gW0", torch::kFloat32, H_ * 2 * D_);
+    o.n = H_ * 2 * D_;
+    TrSeg& sg = o.seg[0];
+    sg.off = 0;
+    sg.n = o.n;
+    sg.part = p.part;
+    sg.S = p.S;
+    sg.rows = static_cast<int32_t>(H_);
+    sg.cols = static_cast<int32_t>(2 * D_);
+    sg.blk0 = 0;
+    sg.sh = const_cast<uint16_t*>(a.W);
+    sg.shT = nullptr;
+    o.nseg = 1;
+    o.nblk = static_cast<int32_t>((H_ / 8) * (2 * D_ / 32));
+    dummy_ = torch::zeros({8}, torch::TensorOptions().dtype(torch::kFloat32).device(dev_));
+    step_ = torch::zeros({1}, torch::TensorOptions().dtype(torch::kInt64).device(dev_));
+    o.step = step_.data_ptr<int64_t>();
+    o.head_part = o.loss_acc = o.loss_out = dummy_.data_ptr<float>();
+    o.nhead = 0;
+    o.counts = nullptr;
+    o.nsample = 0;
+    o.kind = 2;
+  }
+
+  // refresh the bf16 fm shadow of W0 from the fp32 master (call after each update)
+  void shadow() {
+    const c10::DeviceGuard g(dev_);
+    ok(eh_tr_opt(&opt_, 3, stream()), "tower shadow");
+  }
+  void sample() {
+    const c10::DeviceGuard g(dev_);
+    ok(eh_tr_sample(&sample_, stream()), "tower sample");
+  }
+  void fwd() {
+    const c10::DeviceGuard g(dev_);
+    ok(eh_tr_fwd(&fwd_, 0, feat_fp32_, bm_, stream()), "tower fwd");
+  }
+  // dA1 (the plan's buffer) -> gW0 (the plan's buffer)
+  void bwd() {
+    const c10::DeviceGuard g(dev_);
+    TrDwLaunch L{};
+    L.route[0] = prob_;
+    L.nroute = 1;
+    ok(eh_tr_dw(&L, stream()), "tower dw");
+    ok(eh_tr_opt(&opt_, 0, stream()), "tower reduce");
+  }
+
+ private:
+  py::dict d_;
+  int64_t R_, F1_, F2_, logP_, D_, H_, self_, M_;
+  int feat_fp32_ = 0, bm_ = 32;
+  c10::Device dev_{c10::kCPU};
+  TrGraph g_{};
+  TrTree tree_{};
+  TrSampleArgs sample_{};
+  TrFwdArgs fwd_{};
+  TrDwProb prob_{};
+  TrOptArgs opt_{};
+  torch::Tensor part_, dummy_, step_;
+  std::vector<torch::Tensor> owned_;
+
+  bool has(const char* k) const { return d_.contains(k) && !d_[k].is_none(); }
+  int64_t geti(const char* k) const {
+    TORCH_CHECK(d_.contains(k), "TowerPlan: missing '", k, "'");
+    return d_[k].cast<int64_t>();
+  }
+  torch::Tensor T(const char* k) const {
+    TORCH_CHECK(has(k), "TowerPlan: missing tensor '", k, "'");
+    return d_[k].cast<torch::Tensor>();
+  }
+  void need(const torch::Tensor& t, c10::ScalarType st, int64_t numel, const std::string& name) const {
+    TORCH_CHECK(t.is_cuda() && t.device() == dev_, name, " must be on the tower's GPU");
+    TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+    TORCH_CHECK(t.scalar_type() == st, name, " has the wrong dtype");
+    if (numel >= 0) TORCH_CHECK(t.numel() == numel, name, " has ", t.numel(), " elements, expected ", numel);
+  }
+  template <typename P>
+  P* ptr(const char* k, c10::ScalarType st, int64_t numel) {
+    torch::Tensor t = T(k);
+    need(t, st, numel, k);
+    return reinterpret_cast<P*>(t.data_ptr());
+  }
+  int32_t* owned_i32(int64_t n) {
+    torch::Tensor t = torch::full({n}, -1, torch::TensorOptions().dtype(torch::kInt32).device(dev_));
+    owned_.push_back(t);
+    return t.data_ptr<int32_t>();
+  }
+};
+
 }  // namespace
 
 void register_tree_ops(py::module& m) {
@@ -612,4 +821,10 @@ void register_tree_ops(py::module& m) {
       .def("splits", &TreePlan::splits)
       .def("problems", &TreePlan::problems, py::arg("route"));
   m.attr("tree_head_rows") = kTrHeadRows;
+  py::class_<TowerPlan>(m, "TowerPlan")
+      .def(py::init<py::dict>())
+      .def("shadow", &TowerPlan::shadow)
+      .def("sample", &TowerPlan::sample)
+      .def("fwd", &TowerPlan::fwd)
+      .def("bwd", &TowerPlan::bwd);
 }

@@ -110,7 +110,7 @@ __device__ int32_t tr_slot_node(const TrGraph& g, const TrTree& tr, int64_t s, i
     i1 = s >> tr.logP2;
     i0 = i1 >> tr.logP1;
   }
-  int32_t node = tr_root(g, tr.rng, i0);
+  int32_t node = tr.root_in ? tr.root_in[i0] : tr_root(g, tr.rng, i0);
   bool sc = true;
   if (lv >= 1) {
     const int j = static_cast<int>(i1 & ((int64_t(1) << tr.logP1) - 1));
@@ -191,71 +191,50 @@ struct Feat8<float> {
 };
 
 // ----------------------------------------------------------------------------
-// combination blocks of a forward launch: Wc = Wout Wfc (fp32 FMA from the fp32 masters)
-// in [16 rows x 64 columns] tiles, one per block, plus bc = Wout bfc.  E is streamed
-// through LDS in chunks of 32 with the next chunk's loads in flight, so a block is a few
-// load latencies long and finishes well inside the forward's span (a per-thread serial
-// E loop made the whole launch wait on its dependent loads).
+// combination blocks of a forward launch: Wc = Wout Wfc as MFMA tiles of the bf16 fm
+// shadows (an fm fragment of Wout [C][E] is also a valid A fragment: lane l holds row
+// l & 15, k 8(l >> 4)..+7), one 16 x 16 tile per wave, all E/32 fragment pairs in flight;
+// bc = Wout bfc in fp32 from the masters by block 0.  A block is ~one load latency long.
 // ----------------------------------------------------------------------------
-constexpr int kCbRows = 16, kCbCols = 64, kCbE = 32;
-constexpr size_t kCbLds = (kCbRows * kCbE + kCbE * kCbCols + kCbE) * sizeof(float);
-
 template <int NT>
-__device__ void tr_comb_block(const TrCombArgs& c, int blk, float* sm) {
-  static_assert((kCbRows * kCbE) % NT == 0 || NT % (kCbRows * kCbE) == 0, "comb tiling");
-  static_assert((kCbE * kCbCols) % NT == 0 && (kCbRows * kCbCols) % NT == 0, "comb tiling");
-  constexpr int WO = (kCbRows * kCbE + NT - 1) / NT, WF = kCbE * kCbCols / NT, OUT = kCbRows * kCbCols / NT;
-  float* wo_s = sm;                           // [16][32]
-  float* wf_s = wo_s + kCbRows * kCbE;        // [32][64]
-  float* bf_s = wf_s + kCbE * kCbCols;        // [32]
-  const int nhc = c.H / kCbCols;
-  const int c0 = (blk / nhc) * kCbRows, h0 = (blk % nhc) * kCbCols;
-  const int tid = threadIdx.x;
-  float acc[OUT];
+__device__ void tr_comb_block(const TrCombArgs& c, int blk) {
+  constexpr int NW = NT / 64;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int tcols = c.H >> 4, ntiles = (c.C >> 4) * tcols;
+  const int t = blk * NW + wave;
+  if (t < ntiles) {
+    const int c0 = (t / tcols) * 16, h0 = (t % tcols) * 16;
+    float4_t acc = float4_t{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < c.E; k0 += 256) {
+      uint4_t av[8], bv[8];
 #pragma unroll
-  for (int k = 0; k < OUT; ++k) acc[k] = 0.f;
-  float bsum = 0.f;
-  float rwo[WO], rbf = 0.f, rwf[WF];
-  auto load = [&](int e0) {
+      for (int s = 0; s < 8; ++s) {
+        const int k = k0 + s * 32 < c.E ? k0 + s * 32 : 0;
+        av[s] = fm_frag(c.wout_sh, c0, k, c.E, lane);
+        bv[s] = fm_frag(c.wfcT_sh, h0, k, c.E, lane);
+      }
 #pragma unroll
-    for (int k = 0; k < WO; ++k) {
-      const int i = tid + k * NT;
-      if (i < kCbRows * kCbE) rwo[k] = c.wout[static_cast<int64_t>(c0 + i / kCbE) * c.E + e0 + i % kCbE];
+      for (int s = 0; s < 8; ++s)
+        if (k0 + s * 32 < c.E) acc = mfma16(av[s], bv[s], acc);
     }
-    if (tid < kCbE) rbf = c.bfc[e0 + tid];
+    const int h = h0 + (lane & 15);
 #pragma unroll
-    for (int k = 0; k < WF; ++k) {
-      const int i = tid + k * NT;
-      rwf[k] = c.wfc[static_cast<int64_t>(e0 + i / kCbCols) * c.H + h0 + i % kCbCols];
+    for (int j = 0; j < 4; ++j) {
+      const int r = c0 + (lane >> 4) * 4 + j;
+      c.Wc[fm_off(r, h, c.H)] = f2bf(acc[j]);
+      c.WcT[fm_off(h, r, c.C)] = f2bf(acc[j]);
     }
-  };
-  load(0);
-  for (int e0 = 0; e0 < c.E; e0 += kCbE) {
-    __syncthreads();  // the previous chunk is consumed
-#pragma unroll
-    for (int k = 0; k < WO; ++k)
-      if (tid + k * NT < kCbRows * kCbE) wo_s[tid + k * NT] = rwo[k];
-    if (tid < kCbE) bf_s[tid] = rbf;
-#pragma unroll
-    for (int k = 0; k < WF; ++k) wf_s[tid + k * NT] = rwf[k];
-    __syncthreads();
-    if (e0 + kCbE < c.E) load(e0 + kCbE);
-#pragma unroll
-    for (int k = 0; k < OUT; ++k) {
-      const int o = tid + k * NT, r = o / kCbCols, h = o % kCbCols;
-#pragma unroll 8
-      for (int e = 0; e < kCbE; ++e) acc[k] += wo_s[r * kCbE + e] * wf_s[e * kCbCols + h];
-    }
-    if (h0 == 0 && tid < kCbRows)
-      for (int e = 0; e < kCbE; ++e) bsum += wo_s[tid * kCbE + e] * bf_s[e];
   }
-#pragma unroll
-  for (int k = 0; k < OUT; ++k) {
-    const int o = tid + k * NT, r = c0 + o / kCbCols, h = h0 + o % kCbCols;
-    c.Wc[fm_off(r, h, c.H)] = f2bf(acc[k]);
-    c.WcT[fm_off(h, r, c.C)] = f2bf(acc[k]);
+  if (blk == 0) {  // bc = Wout bfc: 4 threads per row, fp32
+    for (int r = threadIdx.x >> 2; r < c.C; r += NT >> 2) {
+      const float* w = c.wout + static_cast<int64_t>(r) * c.E;
+      float b = 0.f;
+      for (int e = threadIdx.x & 3; e < c.E; e += 4) b += w[e] * c.bfc[e];
+      b += __shfl_xor(b, 1, 64);
+      b += __shfl_xor(b, 2, 64);
+      if ((threadIdx.x & 3) == 0) c.bc[r] = b;
+    }
   }
-  if (h0 == 0 && tid < kCbRows) c.bc[c0 + tid] = bsum;
 }
 
 // ----------------------------------------------------------------------------
@@ -313,7 +292,7 @@ __global__ __launch_bounds__(256, (BM == 32 ? TR_FWD_WAVES : 2)) void tr_fwd_ker
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   constexpr bool kGather = MODE != 2;
   if (static_cast<int>(blockIdx.x) < a.ncomb) {  // the head's Wc (first forward launch)
-    tr_comb_block<256>(a.comb, blockIdx.x, reinterpret_cast<float*>(lds));
+    tr_comb_block<256>(a.comb, blockIdx.x);
     return;
   }
   const int tb = static_cast<int>(blockIdx.x) - a.ncomb, ntb = static_cast<int>(gridDim.x) - a.ncomb;
@@ -596,7 +575,7 @@ __global__ __launch_bounds__(kF2Threads, 4) void tr_fwd2_kernel(TrFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   constexpr int BM = kF2Rows, NT = kF2Threads;
   if (static_cast<int>(blockIdx.x) < a.ncomb) {  // the head's Wc
-    tr_comb_block<NT>(a.comb, blockIdx.x, reinterpret_cast<float*>(lds));
+    tr_comb_block<NT>(a.comb, blockIdx.x);
     return;
   }
   const int tb = static_cast<int>(blockIdx.x) - a.ncomb, ntb = static_cast<int>(gridDim.x) - a.ncomb;
@@ -1607,14 +1586,16 @@ hipError_t eh_tr_fwd(const TrFwdArgs* a, int mode, int feat_fp32, int bm, hipStr
                     a->Fg >= (1 << a->logPg)))
     return hipErrorInvalidValue;
   if (mode == 2 && feat_fp32) return hipErrorInvalidValue;
-  if (a->ncomb < 0 || (a->ncomb > 0 && (mode == 2 || !a->comb.wout || !a->comb.wfc || !a->comb.bfc || !a->comb.Wc ||
-                                        !a->comb.WcT || !a->comb.bc || a->comb.C % kCbRows != 0 ||
-                                        a->comb.H % kCbCols != 0 || a->comb.E % kCbE != 0 ||
-                                        a->ncomb != (a->comb.C / kCbRows) * (a->comb.H / kCbCols))))
+  if (a->ncomb < 0 || (a->ncomb > 0 && (mode == 2 || !a->comb.wout || !a->comb.bfc || !a->comb.Wc ||
+                                        !a->comb.WcT || !a->comb.bc || !a->comb.wout_sh || !a->comb.wfcT_sh ||
+                                        a->comb.C % 16 != 0 || a->comb.H % 16 != 0 || a->comb.E % 32 != 0)))
     return hipErrorInvalidValue;
+  // ncomb > 0 requests the combination blocks; their count follows the chosen kernel's block size
+  TrFwdArgs ac = *a;
+  if (ac.ncomb > 0) ac.ncomb = tr_comb_blocks(ac.comb.C, ac.comb.H, (mode == 0 && fwd2_fits(ac)) ? kF2Threads / 64 : 4);
+  a = &ac;
   if (mode == 0 && fwd2_fits(*a)) {
-    size_t l2 = eh_tr_fwd2_lds(a->D, a->FL);
-    if (a->ncomb > 0 && l2 < kCbLds) l2 = kCbLds;
+    const size_t l2 = eh_tr_fwd2_lds(a->D, a->FL);
     const dim3 g2(static_cast<uint32_t>(a->M / kF2Rows + a->ncomb));
 #define TR_FWD2(FT)                                                                                        \
   do {                                                                                                     \
@@ -1627,8 +1608,7 @@ hipError_t eh_tr_fwd(const TrFwdArgs* a, int mode, int feat_fp32, int bm, hipStr
     TR_FWD2(bf16_t);
 #undef TR_FWD2
   }
-  size_t lds = eh_tr_fwd_lds(a->D, a->H, bm, a->FL, mode);
-  if (a->ncomb > 0 && lds < kCbLds) lds = kCbLds;
+  const size_t lds = eh_tr_fwd_lds(a->D, a->H, bm, a->FL, mode);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   const dim3 grid(static_cast<uint32_t>(a->M / bm + a->ncomb));
 #define TR_FWD(FT, BMV, MODEV)                                                                               \
@@ -1735,7 +1715,7 @@ hipError_t eh_tr_dw(TrDwLaunch* L, hipStream_t s) {
 hipError_t eh_tr_opt(const TrOptArgs* a, int mode, hipStream_t s) {
   if (a->nseg < 1 || a->nseg > kTrMaxSegs || a->nblk < 1) return hipErrorInvalidValue;
   if (!a->p || !a->g || !a->m || !a->v || !a->step || !a->loss_acc || !a->loss_out || !a->head_part ||
-      a->nhead < 0 || (a->nhead == 0 && mode != 0))
+      a->nhead < 0 || (a->nhead == 0 && mode != 0 && mode != 3))
     return hipErrorInvalidValue;
   int blk = 0;
   for (int i = 0; i < a->nseg; ++i) {

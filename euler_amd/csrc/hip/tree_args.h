@@ -34,6 +34,8 @@ struct TrGraph {
 // sampling chain above the target rows of layer 0 (levels 1 and 2 at most)
 struct TrTree {
   const int64_t* rng;  // device (seed, counter)
+  const int32_t* root_in;  // optional: the roots are given (root t = root_in[t], -1 = padding)
+                           // instead of drawn from the alias table (towers of pair models)
   int32_t F1, F2;      // fanouts of hops 1 and 2
   int32_t logP1, logP2;
   uint32_t m1, m2;     // edge-type masks of hops 1 and 2
@@ -61,16 +63,20 @@ struct TrSampleArgs {
 // and demb, needed only by the fc / out_fc weight gradients, are computed off it).  Wc is
 // rebuilt every step from the fp32 masters by extra blocks of the first forward launch.
 struct TrCombArgs {
-  const float* wout;  // [C][E] fp32 (flat parameters)
-  const float* wfc;   // [E][H] fp32
+  const float* wout;  // [C][E] fp32 (flat parameters), for bc
   const float* bfc;   // [E]
+  const uint16_t* wout_sh;  // fm [C][E] bf16 shadow (the optimizer's)
+  const uint16_t* wfcT_sh;  // fm [H][E] bf16 shadow of Wfc^T
   int32_t C, E, H;
   uint16_t* Wc;       // fm [C][H] bf16
   uint16_t* WcT;      // fm [H][C] bf16
   float* bc;          // [C]
 };
-// combination tiles: 16 rows x 64 columns of Wc per block (C % 16, H % 64, E % 32 == 0)
-inline int tr_comb_blocks(int C, int H) { return (C / 16) * (H / 64); }
+// combination blocks: one 16 x 16 tile of Wc per wave (C % 16, H % 16, E % 32 == 0)
+inline int tr_comb_blocks(int C, int H, int waves_per_block) {
+  const int t = (C / 16) * (H / 16);
+  return (t + waves_per_block - 1) / waves_per_block;
+}
 
 // one fused SAGE layer: mode 0 = gather (sampled ids) + GEMM + tree-mean epilogue (layer 0),
 // mode 1 = gather only, writing [x_self | mean x_nbr] rows (1-hop models),
