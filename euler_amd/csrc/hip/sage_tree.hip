@@ -567,6 +567,11 @@ __global__ __launch_bounds__(256, (BM == 32 ? TR_FWD_WAVES : 2)) void tr_fwd_ker
 // of at most 64 rows (else tr_fwd_kernel).
 // ----------------------------------------------------------------------------
 constexpr int kF2Rows = 64, kF2Threads = 512, kF2Ldt = kF2Rows + 4;
+// F2_ALIAS=1: the output tile aliases the A tile (one region of max(A, O) bytes, a barrier
+// between the last A read and the first O write): ~38 KB of LDS per block instead of ~70 KB
+#ifndef F2_ALIAS
+#define F2_ALIAS 1
+#endif
 
 __device__ __forceinline__ int f2_chunk(int r, int c) { return c ^ (r & 15); }
 
@@ -584,8 +589,13 @@ __global__ __launch_bounds__(kF2Threads, 4) void tr_fwd2_kernel(TrFwdArgs a) {
   const int64_t row0 = static_cast<int64_t>(tile) * BM;
   // LDS: A tile [BM][K2] (swizzled) | output tile [kTrBN][kF2Ldt] (transposed) | ids
   bf16_t* At = lds;
+#if F2_ALIAS
+  bf16_t* Ot = lds;
+  int32_t* node_s = reinterpret_cast<int32_t*>(lds + (BM * K2 > kTrBN * kF2Ldt ? BM * K2 : kTrBN * kF2Ldt));
+#else
   bf16_t* Ot = lds + BM * K2;
   int32_t* node_s = reinterpret_cast<int32_t*>(Ot + kTrBN * kF2Ldt);
+#endif
   int32_t* leaf_s = node_s + BM;
 #define F2_STAMP(k) \
   if (a.prof && threadIdx.x == 0) a.prof[tb * 8 + (k)] = static_cast<long long>(wall_clock64())
@@ -729,6 +739,11 @@ __global__ __launch_bounds__(kF2Threads, 4) void tr_fwd2_kernel(TrFwdArgs a) {
           for (int n = 0; n < FN; ++n) bq[q][n] = fm_frag(W, cb + n * 16, kn < K2 ? kn : 0, K2, lane);
         }
       }
+    }
+#if F2_ALIAS
+    __syncthreads();  // every wave is done reading the A tile the output tile overwrites
+#endif
+    if (cb < H) {
       // ReLU -> transposed output tile: 4 consecutive rows of one column per 8-byte store
 #pragma unroll
       for (int m = 0; m < FM; ++m)
@@ -1549,8 +1564,8 @@ size_t eh_tr_fwd_lds(int D, int H, int bm, int FL, int mode) {
 }
 
 size_t eh_tr_fwd2_lds(int D, int FL) {
-  return static_cast<size_t>(kF2Rows) * 2 * D * sizeof(bf16_t) +
-         static_cast<size_t>(kTrBN) * kF2Ldt * sizeof(bf16_t) + static_cast<size_t>(kF2Rows) * (1 + FL) * sizeof(int32_t);
+  const size_t a = static_cast<size_t>(kF2Rows) * 2 * D, o = static_cast<size_t>(kTrBN) * kF2Ldt;
+  return (F2_ALIAS ? (a > o ? a : o) : a + o) * sizeof(bf16_t) + static_cast<size_t>(kF2Rows) * (1 + FL) * sizeof(int32_t);
 }
 
 // the 64-row / 8-wave layer-0 kernel applies (EULER_AMD_FWD2=0 disables it)
@@ -1561,6 +1576,7 @@ static bool fwd2_fits(const TrFwdArgs& a) {
   }();
   if (off || !a.a_kt) return false;
   if (a.D % 64 != 0 || a.M % kF2Rows != 0 || a.logPg < 2 || (1 << a.logPg) > kF2Rows) return false;
+  if (F2_ALIAS && a.H > kTrBN) return false;  // the aliased A tile must outlive every column chunk
   return eh_tr_fwd2_lds(a.D, a.FL) <= 80 * 1024;  // two blocks per CU
 }
 

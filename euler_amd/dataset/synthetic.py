@@ -26,7 +26,8 @@ import math
 
 import torch
 
-__all__ = ["lattice_kg", "community_graph", "community_labels", "tail_ranks", "rank_metrics", "auc"]
+__all__ = ["lattice_kg", "community_graph", "community_labels", "community_features", "tail_ranks", "rank_metrics",
+           "auc"]
 
 
 def lattice_kg(num_ent, num_rel, num_triples, num_test, seed=0, max_off=5):
@@ -71,6 +72,17 @@ def community_graph(num_nodes, num_comm, avg_degree, p_in=0.9, seed=0):
     dst_out = torch.randint(0, num_nodes, (m,), generator=g)
     dst = torch.where(inside, dst_in, dst_out)
     return src, dst, torch.arange(num_nodes) % num_comm
+
+
+def community_features(comm, dim, signal=0.5, seed=0):
+    """[n, dim] node features = signal * (unit centroid of the node's community) + N(0, 1)
+    noise / sqrt(dim): one node's own row is a weak community cue, the mean over its
+    (mostly same-community) neighbours a strong one — the regime where aggregating the
+    neighbourhood (GraphSAGE) beats the node's features alone."""
+    g = torch.Generator().manual_seed(int(seed) + 7)
+    k = int(comm.max()) + 1
+    cent = torch.nn.functional.normalize(torch.randn(k, dim, generator=g), dim=1)
+    return signal * cent[comm] + torch.randn(comm.numel(), dim, generator=g) / math.sqrt(dim)
 
 
 def community_labels(comm, num_classes, noise=0.1, seed=0):

@@ -388,13 +388,24 @@ class BaseEstimator:
 
         model = self.model
         gnn = getattr(model, "gnn", None)
-        if gnn is None or not hasattr(gnn, "feature_idx") or not hasattr(model, "label_idx"):
-            raise ValueError("device_graph=True trains SupervisedGraphSage-style models (gnn.feature_idx, label_idx)")
+        unsup = hasattr(model, "context_gnn")
+        if gnn is None or not hasattr(gnn, "feature_idx") or not (unsup or hasattr(model, "label_idx")):
+            raise ValueError("device_graph=True trains SupervisedGraphSage / UnsupervisedGraphSage-style models "
+                             "(gnn.feature_idx + label_idx, or a context_gnn)")
         self._prepare(first)  # materialise the lazy layers, broadcast rank 0's weights
         nt = self.params.get("train_node_type", -1)
         node_type = -1 if nt in (None, -1, "-1") else int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
         fdt = torch.float32 if self.params.get("device_feature_dtype", "bf16") == "fp32" else torch.bfloat16
         seed = int(self.params.get("seed") or 0)
+        if unsup:
+            from euler_amd.models.sage_tower import UnsupSageTrainer
+
+            graph = DeviceGraph.from_engine(node_type=node_type, features=gnn.feature_idx,
+                                            feature_dims=gnn.feature_dim, feature_dtype=fdt,
+                                            seed=seed * 7919 + self.rank, device=self.device)
+            return UnsupSageTrainer.from_model(model, graph, int(self.params["batch_size"]),
+                                               optimizer=self.params.get("optimizer", "adam"),
+                                               learning_rate=float(self.params.get("learning_rate", 0.001)))
         graph = DeviceGraph.from_engine(node_type=node_type, features=gnn.feature_idx, feature_dims=gnn.feature_dim,
                                         label=model.label_idx, label_dim=model.label_dim, feature_dtype=fdt,
                                         seed=seed * 7919 + self.rank, device=self.device)
@@ -460,11 +471,12 @@ class BaseEstimator:
                 loss = float(tr.loss.item())  # syncs the stream
                 dt = max(time.time() - t0, 1e-9)
                 rate = (self.global_step - n0) * bs * self.world / dt
-                last = {"step": self.global_step, "loss": loss, "f1": tr.metric(), "samples_per_sec": rate}
+                mname = getattr(tr, "metric_name", "f1")
+                last = {"step": self.global_step, "loss": loss, mname: tr.metric(), "samples_per_sec": rate}
                 tr.reset_metric()
                 if self.rank == 0:
-                    log.info("step = %d, loss = %.6f, f1 = %.6f (%.1f samples/s, device path)", self.global_step,
-                             loss, last["f1"], rate)
+                    log.info("step = %d, loss = %.6f, %s = %.6f (%.1f samples/s, device path)", self.global_step,
+                             loss, mname, last[mname], rate)
                 t0, n0 = time.time(), self.global_step
             if save_steps and self.global_step % save_steps == 0:
                 tr.write_to_model(self.model)

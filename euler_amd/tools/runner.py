@@ -178,8 +178,9 @@ def parse_args(argv=None, model=None):
     p.add_argument("--device", default=None)
     p.add_argument("--amp", default=None, help="bf16 for bf16 autocast on the GPU")
     p.add_argument("--device_graph", action="store_true",
-                   help="graphsage: train on an HBM copy of the graph with the fused gfx950 step "
-                        "(models/sage_trainer.py) instead of the CPU-engine input pipeline")
+                   help="graphsage / graphsage_unsup: train on an HBM copy of the graph with the fused "
+                        "gfx950 step (models/sage_trainer.py, models/sage_tower.py) instead of the "
+                        "CPU-engine input pipeline")
     p.add_argument("--device_feature_dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--cuda_graph", default="auto", choices=["auto", "off"],
                    help="capture the engine-path training step in a hipGraph when eligible")

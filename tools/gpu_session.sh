@@ -181,6 +181,11 @@ for st in "${S[@]}"; do
           python3 bench.py --num-nodes 10000000 --steps 30 --warmup 5 --force-dist && \
       python tools/trace_gaps.py "$OUT/trace_dist/run_kernel_trace.csv" --last 2 > "$OUT/trace_dist_gaps.txt" 2>&1
       cat "$OUT/trace_bench_gaps.txt" "$OUT/trace_dist_gaps.txt" ;;
+    unsup)
+      run bench_unsup 900 python -u benchmarks/bench_unsup_sage.py ${UNSUP_ARGS:-} ;;
+    unsup_prof)
+      run unsup_prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/unsup_prof" -o run --output-format csv -- \
+          python3 benchmarks/bench_unsup_sage.py --steps 100 --eval-pairs 2000 ;;
     pmc_lds)
       PASSES="SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE" \
         run pmc_lds 300 bash tools/pmc_passes.sh lds "$PWD/tools/tree_kernels.py" --reps 10 ;;
