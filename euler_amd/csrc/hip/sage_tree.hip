@@ -600,6 +600,7 @@ __global__ __launch_bounds__(kF2Threads, 4) void tr_fwd2_kernel(TrFwdArgs a) {
 #define F2_STAMP(k) \
   if (a.prof && threadIdx.x == 0) a.prof[tb * 8 + (k)] = static_cast<long long>(wall_clock64())
   F2_STAMP(0);
+  if (a.prof && threadIdx.x == 0) a.prof[tb * 8 + 6] = static_cast<long long>(__smid());  // XCC / SE / CU
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int lr = lane & 15, lg = lane >> 4;
   if (tb == 0 && tid == 0) {

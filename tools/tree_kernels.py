@@ -76,7 +76,16 @@ def main():
         p.fwd(fprof)
         torch.cuda.synchronize()
         f = fprof.view(-1, 8).cpu().double() / 100.0
-        f = f[f[:, 0] > 0]  # blocks of the launched kernel (64-row tiles: half the 32-row count)
+        raw = fprof.view(-1, 8).cpu()
+        live = raw[:, 0] > 0
+        f = f[live]  # blocks of the launched kernel (64-row tiles: half the 32-row count)
+        cu = raw[live, 6]
+        st = (f[:, 0] - f[:, 0].min())
+        uniq, cnt = torch.unique(cu, return_counts=True)
+        print("fwd blocks", int(live.sum()), "distinct CUs", int(uniq.numel()), "max blocks per CU", int(cnt.max()),
+              "start-time percentiles (us) 50/90/99/max",
+              [round(float(torch.quantile(st, q)), 2) for q in (0.5, 0.9, 0.99)], round(float(st.max()), 2),
+              "end-time spread (us)", round(float((f[:, 5] - f[:, 5].min()).max()), 2))
         f0 = f[:, 0].min()
         fph = [(f[:, k] - f[:, k - 1]).mean().item() for k in range(1, 6)]
         print("fwd phases (us, mean over blocks: ids, gather, kt, gemm, epilogue):", [round(v, 2) for v in fph],
