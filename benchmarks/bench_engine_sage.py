@@ -31,6 +31,25 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+def start_cluster(data_dir, shards, threads=8):
+    """``shards`` same-host shard servers over the reference-format ``data_dir``, found
+    through a file registry; returns (registry, processes)."""
+    import subprocess
+
+    reg = tempfile.mkdtemp(prefix="euler_amd_bench_reg_")
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    procs = [subprocess.Popen([sys.executable, "-m", "euler_amd.tools.service", "--data_path", data_dir,
+                               "--shard_idx", str(s), "--shard_num", str(shards), "--registry", reg,
+                               "--threads", str(threads)], env=env, stdout=subprocess.DEVNULL,
+                              stderr=subprocess.STDOUT) for s in range(shards)]
+    deadline = time.time() + 120
+    while time.time() < deadline and len([f for f in os.listdir(reg) if "#" in f]) < shards:
+        time.sleep(0.2)
+    if len([f for f in os.listdir(reg) if "#" in f]) < shards:
+        raise RuntimeError("shard servers did not register")
+    return reg, procs
+
+
 def run(ds, args, prefetch, device, workers=2, native=False, graph="auto"):
     import euler_amd as ea
     from euler_amd import models as Z
@@ -69,15 +88,28 @@ def main(argv=None):
     p.add_argument("--native_workers", type=int, nargs="+", default=[4, 8, 16])
     p.add_argument("--only", default="", help="comma list of variant names to run (default: all)")
     p.add_argument("--cprofile", default="", help="write the consumer's cProfile top-40 (cumulative) here")
+    p.add_argument("--mode", choices=["local", "remote"], default="local",
+                   help="remote: the graph on --shards same-host shard servers (initialize_shared_graph)")
+    p.add_argument("--shards", type=int, default=2)
+    p.add_argument("--server_threads", type=int, default=8)
+    p.add_argument("--device", default=None)
     args = p.parse_args(argv)
     from euler_amd.dataset import get_dataset
 
-    dev = "cuda" if torch.cuda.is_available() else "cpu"
+    dev = args.device or ("cuda" if torch.cuda.is_available() else "cpu")
     t0 = time.time()
     ds = get_dataset("ppi", data_dir=tempfile.mkdtemp(prefix="euler_amd_ppi_"), scale=args.scale)
-    ds.load_graph()
-    print(f"[bench_engine_sage] ppi-schema graph scale {args.scale} ready in {time.time() - t0:.1f}s",
-          file=sys.stderr, flush=True)
+    if args.mode == "remote":
+        ds.partition_num = args.shards  # partition p is served by shard p % shards
+    data_dir = ds.load_graph()
+    procs = []
+    if args.mode == "remote":
+        import euler_amd as ea
+
+        reg, procs = start_cluster(data_dir, args.shards, args.server_threads)
+        ea.initialize_shared_graph(reg, shard_num=args.shards)
+    print(f"[bench_engine_sage] ppi-schema graph scale {args.scale} ready in {time.time() - t0:.1f}s "
+          f"({args.mode})", file=sys.stderr, flush=True)
     out = {}
     variants = [("serial", 0, 1, False, False), ("py_prefetch_1worker", 2, 1, False, False)]
     variants += [("native_%dworkers_eager" % w, 0, w, True, False) for w in args.native_workers[:1]]
@@ -105,9 +137,13 @@ def main(argv=None):
         out[name] = {"samples_per_s": round(args.batch * args.steps / el, 1), "ms_per_step": round(el * 1e3 / args.steps, 2),
                      "loss": round(float(res.get("loss", float("nan"))), 4)}
         print(f"[bench_engine_sage] {name}: {out[name]}", file=sys.stderr, flush=True)
+    for pr in procs:
+        pr.terminate()
+        pr.wait(timeout=30)
     best = max((k for k in out if k.startswith("native") and not k.endswith("eager")) or out, key=lambda k: out[k]["samples_per_s"])
     print(json.dumps({
-        "metric": "train samples/sec, GraphSAGE via the C++ graph engine + estimator (reference architecture)",
+        "metric": "train samples/sec, GraphSAGE via the C++ graph engine + estimator (reference architecture)"
+                  + (", graph on %d shard servers" % args.shards if args.mode == "remote" else ""),
         "value": out[best]["samples_per_s"],   # the estimator default on a GPU: the native pipeline
         "unit": "samples/s",
         "n_gpus": 1 if dev == "cuda" else 0,
@@ -119,7 +155,8 @@ def main(argv=None):
         "dtype": "fp32",
         "data": "synthetic PPI-schema graph (56,944 nodes, 50-d features, 121 labels)",
         "config": {"model": "SupervisedGraphSage [128, 128, 121], fanouts [10, 10], Adam", "batch": args.batch,
-                   "scale": args.scale, **out},
+                   "scale": args.scale, "mode": args.mode, "shards": args.shards if args.mode == "remote" else 0,
+                   **out},
     }), flush=True)
 
 

@@ -213,6 +213,7 @@ class Engine {
     return d;
   }
 
+  QueryProxy* Proxy() const { return proxy_.get(); }
   Graph& LocalGraph() const {
     Graph* g = proxy_->local_graph();
     if (!g) throw std::runtime_error("this engine has no in-process graph (remote mode)");
@@ -554,12 +555,30 @@ class PySagePipeline {
                  std::vector<int> dims, std::string label, int label_dim, std::vector<uintptr_t> ints,
                  std::vector<uintptr_t> floats, int workers, uint64_t seed)
       : e_(std::move(e)) {
-    const Graph& g = e_->LocalGraph();
-    SageBatchSpec spec = MakeSpec(g, batch, node_type, etypes, fanouts, def, self_loops, dense, dims, label, label_dim);
     std::vector<int64_t*> ip;
     std::vector<float*> fp;
     for (auto a : ints) ip.push_back(reinterpret_cast<int64_t*>(a));
     for (auto a : floats) fp.push_back(reinterpret_cast<float*>(a));
+    QueryProxy* q = e_->Proxy();
+    if (q->mode() == "remote" || q->mode() == "local_sharded") {
+      // the graph lives on shard servers (or in-process shards): batches through the
+      // distribute-mode GQL plans (pipeline.h RemoteSource)
+      SageBatchSpec spec;
+      spec.batch = batch;
+      spec.node_type = node_type;
+      spec.etypes = etypes;
+      spec.fanouts = fanouts;
+      spec.default_node = def;
+      spec.self_loops = self_loops;
+      spec.dense_names = dense;
+      spec.dense_dims = dims;
+      spec.label_name = label;
+      spec.label_dim = label.empty() ? 0 : label_dim;
+      p_.reset(new SagePipeline(MakeRemoteSource(q), spec, ip, fp, workers, seed));
+      return;
+    }
+    const Graph& g = e_->LocalGraph();
+    SageBatchSpec spec = MakeSpec(g, batch, node_type, etypes, fanouts, def, self_loops, dense, dims, label, label_dim);
     p_.reset(new SagePipeline(&g, spec, ip, fp, workers, seed));
   }
   ~PySagePipeline() {

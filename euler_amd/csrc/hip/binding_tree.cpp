@@ -370,7 +370,7 @@ class TreePlan {
     c.Wc = owned_bf16((int64_t)C_ * H);
     c.WcT = owned_bf16((int64_t)C_ * H);
     c.bc = owned(C_);
-    fwd0_.ncomb = 1;  // requested; the launcher sizes it to the chosen kernel's waves per block
+    fwd0_.ncomb = 1;
   }
 
   uint16_t* owned_bf16(int64_t n) {

@@ -191,30 +191,28 @@ struct Feat8<float> {
 };
 
 // ----------------------------------------------------------------------------
-// combination blocks of a forward launch: Wc = Wout Wfc as MFMA tiles of the bf16 fm
-// shadows (an fm fragment of Wout [C][E] is also a valid A fragment: lane l holds row
-// l & 15, k 8(l >> 4)..+7), one 16 x 16 tile per wave, all E/32 fragment pairs in flight;
-// bc = Wout bfc in fp32 from the masters by block 0.  A block is ~one load latency long.
+// combination tiles, computed by wave 0 of the forward launch's tile blocks before their
+// own work (the MFMA units are idle during the gather): Wc = Wout Wfc as 16 x 16 MFMA
+// tiles of the bf16 fm shadows (an fm fragment of Wout [C][E] is also a valid A fragment:
+// lane l holds row l & 15, k 8(l >> 4)..+7), all E/32 fragment pairs of a tile in
+// flight; bc = Wout bfc in fp32 from the masters (block 0's wave 0).  No extra blocks:
+// extra blocks would push tile blocks past the resident slots into a second round.
 // ----------------------------------------------------------------------------
-template <int NT>
-__device__ void tr_comb_block(const TrCombArgs& c, int blk) {
-  constexpr int NW = NT / 64;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+__device__ __forceinline__ void tr_comb_wave(const TrCombArgs& c, int first, int stride, int lane) {
   const int tcols = c.H >> 4, ntiles = (c.C >> 4) * tcols;
-  const int t = blk * NW + wave;
-  if (t < ntiles) {
+  for (int t = first; t < ntiles; t += stride) {
     const int c0 = (t / tcols) * 16, h0 = (t % tcols) * 16;
     float4_t acc = float4_t{0.f, 0.f, 0.f, 0.f};
-    for (int k0 = 0; k0 < c.E; k0 += 256) {
-      uint4_t av[8], bv[8];
+    for (int k0 = 0; k0 < c.E; k0 += 128) {  // 4 fragment pairs in flight (register budget of the host kernel)
+      uint4_t av[4], bv[4];
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
+      for (int s = 0; s < 4; ++s) {
         const int k = k0 + s * 32 < c.E ? k0 + s * 32 : 0;
         av[s] = fm_frag(c.wout_sh, c0, k, c.E, lane);
         bv[s] = fm_frag(c.wfcT_sh, h0, k, c.E, lane);
       }
 #pragma unroll
-      for (int s = 0; s < 8; ++s)
+      for (int s = 0; s < 4; ++s)
         if (k0 + s * 32 < c.E) acc = mfma16(av[s], bv[s], acc);
     }
     const int h = h0 + (lane & 15);
@@ -225,14 +223,12 @@ __device__ void tr_comb_block(const TrCombArgs& c, int blk) {
       c.WcT[fm_off(h, r, c.C)] = f2bf(acc[j]);
     }
   }
-  if (blk == 0) {  // bc = Wout bfc: 4 threads per row, fp32
-    for (int r = threadIdx.x >> 2; r < c.C; r += NT >> 2) {
+  if (first == 0) {  // bc = Wout bfc: one row per lane, fp32
+    for (int r = lane; r < c.C; r += 64) {
       const float* w = c.wout + static_cast<int64_t>(r) * c.E;
       float b = 0.f;
-      for (int e = threadIdx.x & 3; e < c.E; e += 4) b += w[e] * c.bfc[e];
-      b += __shfl_xor(b, 1, 64);
-      b += __shfl_xor(b, 2, 64);
-      if ((threadIdx.x & 3) == 0) c.bc[r] = b;
+      for (int e = 0; e < c.E; ++e) b += w[e] * c.bfc[e];
+      c.bc[r] = b;
     }
   }
 }
@@ -291,11 +287,8 @@ template <typename FT, int BM, int MODE>
 __global__ __launch_bounds__(256, (BM == 32 ? TR_FWD_WAVES : 2)) void tr_fwd_kernel(TrFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   constexpr bool kGather = MODE != 2;
-  if (static_cast<int>(blockIdx.x) < a.ncomb) {  // the head's Wc (first forward launch)
-    tr_comb_block<256>(a.comb, blockIdx.x);
-    return;
-  }
-  const int tb = static_cast<int>(blockIdx.x) - a.ncomb, ntb = static_cast<int>(gridDim.x) - a.ncomb;
+  const int tb = static_cast<int>(blockIdx.x), ntb = static_cast<int>(gridDim.x);
+  if (a.ncomb && threadIdx.x < 64) tr_comb_wave(a.comb, tb, ntb, threadIdx.x);  // the head's Wc
   const int D = a.D;
   const int K2 = 2 * D;
   const int ldsw = K2 + 8;
@@ -572,6 +565,9 @@ constexpr int kF2Rows = 64, kF2Threads = 512, kF2Ldt = kF2Rows + 4;
 #ifndef F2_ALIAS
 #define F2_ALIAS 1
 #endif
+#ifndef F2_SKIP_PAD
+#define F2_SKIP_PAD 1
+#endif
 
 __device__ __forceinline__ int f2_chunk(int r, int c) { return c ^ (r & 15); }
 
@@ -579,11 +575,7 @@ template <typename FT>
 __global__ __launch_bounds__(kF2Threads, 4) void tr_fwd2_kernel(TrFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   constexpr int BM = kF2Rows, NT = kF2Threads;
-  if (static_cast<int>(blockIdx.x) < a.ncomb) {  // the head's Wc
-    tr_comb_block<NT>(a.comb, blockIdx.x);
-    return;
-  }
-  const int tb = static_cast<int>(blockIdx.x) - a.ncomb, ntb = static_cast<int>(gridDim.x) - a.ncomb;
+  const int tb = static_cast<int>(blockIdx.x), ntb = static_cast<int>(gridDim.x);
   const int D = a.D, K2 = 2 * D, H = a.H;
   const int tile = xcd_remap(tb, ntb);
   const int64_t row0 = static_cast<int64_t>(tile) * BM;
@@ -612,18 +604,30 @@ __global__ __launch_bounds__(kF2Threads, 4) void tr_fwd2_kernel(TrFwdArgs a) {
   for (int it = tid; it < BM * a.FL; it += NT) leaf_s[it] = a.leaf[row0 * a.FL + it];
   __syncthreads();
   F2_STAMP(1);
-  // ---- gather + mean: item = (row, 8-column chunk); two items per thread, every leaf
-  // load of both in flight; padding ids (-1) read row 0 and are zeroed at use
+  // ---- gather + mean: item = (used row, 8-column chunk); two items per thread, every leaf
+  // load of both in flight; padding ids (-1) read row 0 and are zeroed at use.  Only the
+  // Fg + 1 used slots of each sibling group are items (F2_SKIP_PAD; at fanout 25, 26 of
+  // every 32 rows): the unused slots' A rows are zero-filled instead of gathered.
   {
     const FT* x = static_cast<const FT*>(a.x);
     const int cpr = D >> 3;
-    const int nitems = BM * cpr;
+    const int P = 1 << a.logPg, U = F2_SKIP_PAD ? a.Fg + 1 : P;
+    const int nitems = (BM >> a.logPg) * U * cpr;
     constexpr int G = Feat8<FT>::kInFlight;
+    if (F2_SKIP_PAD && U < P) {
+      const int pad = P - U, nch = K2 >> 3;
+      for (int it = tid; it < (BM >> a.logPg) * pad * nch; it += NT) {
+        const int q = it / nch, c = it - q * nch;
+        const int r = (q / pad) * P + U + q % pad;
+        *reinterpret_cast<uint4_t*>(At + r * K2 + f2_chunk(r, c) * 8) = uint4_t{0u, 0u, 0u, 0u};
+      }
+    }
     for (int it = tid; it < nitems; it += 2 * NT) {
       const int itb = it + NT;
       const bool hb = itb < nitems;
-      const int ra = it / cpr, ca = it - ra * cpr;
-      const int rb = hb ? itb / cpr : ra, cb = hb ? itb - rb * cpr : ca;
+      const int qa = it / cpr, ca = it - qa * cpr;
+      const int qb = hb ? itb / cpr : qa, cb = hb ? itb - qb * cpr : ca;
+      const int ra = (qa / U) * P + qa % U, rb = (qb / U) * P + qb % U;
       const int32_t na = node_s[ra], nb = hb ? node_s[rb] : -1;
       Feat8<FT> sa, sb;
       float acc_a[8], acc_b[8];
@@ -672,6 +676,8 @@ __global__ __launch_bounds__(kF2Threads, 4) void tr_fwd2_kernel(TrFwdArgs a) {
       }
     }
   }
+  // the head's Wc tiles (wave 0, after the gather: its registers are free again)
+  if (a.ncomb && wave == 0) tr_comb_wave(a.comb, tb, ntb, lane);
   // the first two k-steps of this wave's weight fragments load behind the kt pass (not
   // earlier: held through the gather they would push its 20 row loads in flight to spill)
   const bf16_t* W = a.W;
@@ -1607,13 +1613,9 @@ hipError_t eh_tr_fwd(const TrFwdArgs* a, int mode, int feat_fp32, int bm, hipStr
                                         !a->comb.WcT || !a->comb.bc || !a->comb.wout_sh || !a->comb.wfcT_sh ||
                                         a->comb.C % 16 != 0 || a->comb.H % 16 != 0 || a->comb.E % 32 != 0)))
     return hipErrorInvalidValue;
-  // ncomb > 0 requests the combination blocks; their count follows the chosen kernel's block size
-  TrFwdArgs ac = *a;
-  if (ac.ncomb > 0) ac.ncomb = tr_comb_blocks(ac.comb.C, ac.comb.H, (mode == 0 && fwd2_fits(ac)) ? kF2Threads / 64 : 4);
-  a = &ac;
   if (mode == 0 && fwd2_fits(*a)) {
     const size_t l2 = eh_tr_fwd2_lds(a->D, a->FL);
-    const dim3 g2(static_cast<uint32_t>(a->M / kF2Rows + a->ncomb));
+    const dim3 g2(static_cast<uint32_t>(a->M / kF2Rows));
 #define TR_FWD2(FT)                                                                                        \
   do {                                                                                                     \
     EULER_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(tr_fwd2_kernel<FT>),                \
@@ -1627,7 +1629,7 @@ hipError_t eh_tr_fwd(const TrFwdArgs* a, int mode, int feat_fp32, int bm, hipStr
   }
   const size_t lds = eh_tr_fwd_lds(a->D, a->H, bm, a->FL, mode);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  const dim3 grid(static_cast<uint32_t>(a->M / bm + a->ncomb));
+  const dim3 grid(static_cast<uint32_t>(a->M / bm));
 #define TR_FWD(FT, BMV, MODEV)                                                                               \
   do {                                                                                                       \
     EULER_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(tr_fwd_kernel<FT, BMV, MODEV>),         \

@@ -72,11 +72,6 @@ struct TrCombArgs {
   uint16_t* WcT;      // fm [H][C] bf16
   float* bc;          // [C]
 };
-// combination blocks: one 16 x 16 tile of Wc per wave (C % 16, H % 16, E % 32 == 0)
-inline int tr_comb_blocks(int C, int H, int waves_per_block) {
-  const int t = (C / 16) * (H / 16);
-  return (t + waves_per_block - 1) / waves_per_block;
-}
 
 // one fused SAGE layer: mode 0 = gather (sampled ids) + GEMM + tree-mean epilogue (layer 0),
 // mode 1 = gather only, writing [x_self | mean x_nbr] rows (1-hop models),
@@ -103,7 +98,7 @@ struct TrFwdArgs {
   int32_t* roots_cur;       // ... copied here for the head (the sampler may refill roots_in)
   int32_t B;
   long long* prof;       // optional per-block phase stamps [grid][8]
-  TrCombArgs comb;       // modes 0/1: blocks [0, ncomb) build the head's Wc / WcT / bc
+  TrCombArgs comb;       // modes 0/1, ncomb != 0: wave 0 of every block builds tiles of the head's Wc
   int32_t ncomb;
 };
 

@@ -5,6 +5,8 @@
 
 #include <algorithm>
 
+#include "rpc/rpc.h"
+
 namespace euler {
 
 namespace {
@@ -69,15 +71,177 @@ SageSlotLayout SageSlotLayout::Make(const SageBatchSpec& s) {
   return l;
 }
 
+namespace {
+
+// the in-process shard: direct column / CSR reads, sampling from the batch's stream
+class LocalSource : public SageSource {
+ public:
+  explicit LocalSource(const Graph* g) : g_(*g) {}
+
+  void Roots(const SageBatchSpec& s, Rng& rng, int64_t* roots, float* labels) override {
+    std::vector<uint64_t> r;
+    g_.SampleNode(s.node_type, s.batch, rng, &r);
+    for (int i = 0; i < s.batch; ++i)
+      roots[i] = i < static_cast<int>(r.size()) ? static_cast<int64_t>(r[i]) : s.default_node;
+    if (s.label_dim <= 0) return;
+    const Column<float>* lc = s.label_idx >= 0 ? g_.NodeDense(s.label_idx) : nullptr;
+    for (int i = 0; i < s.batch; ++i) {
+      const int64_t row = g_.Row(static_cast<uint64_t>(roots[i]));
+      const float* p = nullptr;
+      int64_t m = 0;
+      if (lc && row >= 0) lc->Get(row, &p, &m);
+      m = std::min<int64_t>(m, s.label_dim);
+      if (m > 0) memcpy(labels + i * s.label_dim, p, m * sizeof(float));
+      if (m < s.label_dim) memset(labels + i * s.label_dim + m, 0, (s.label_dim - m) * sizeof(float));
+    }
+  }
+
+  void Hop(const SageBatchSpec& s, int hop, const int64_t* ids, int64_t n, Rng& rng, int64_t* out) override {
+    const int k = s.fanouts[hop - 1];
+    std::vector<IdWeightType> tmp;
+    for (int64_t i = 0; i < n; ++i) {
+      g_.SampleNeighbor(g_.Row(static_cast<uint64_t>(ids[i])), s.etypes[hop - 1], k, true, rng, &tmp);
+      for (int j = 0; j < k; ++j)
+        out[i * k + j] = j < static_cast<int>(tmp.size()) ? static_cast<int64_t>(tmp[j].id) : s.default_node;
+    }
+  }
+
+  void Features(const SageBatchSpec& s, const int64_t* ids, int64_t n, int64_t fd, float* out) override {
+    std::vector<const Column<float>*> cols;
+    for (int idx : s.dense_idx) cols.push_back(g_.NodeDense(idx));
+    for (int64_t i = 0; i < n; ++i) {
+      const int64_t r = g_.Row(static_cast<uint64_t>(ids[i]));
+      float* o = out + i * fd;
+      int64_t c0 = 0;
+      for (size_t f = 0; f < cols.size(); ++f) {
+        const int64_t dim = s.dense_dims[f];
+        const float* p = nullptr;
+        int64_t m = 0;
+        if (cols[f] && r >= 0) cols[f]->Get(r, &p, &m);
+        m = std::min(m, dim);
+        if (m > 0) memcpy(o + c0, p, m * sizeof(float));
+        if (m < dim) memset(o + c0 + m, 0, (dim - m) * sizeof(float));
+        c0 += dim;
+      }
+    }
+  }
+
+ private:
+  const Graph& g_;
+};
+
+// ragged (idx [n][2], flat data) -> dense rows [n][w], zero / default padded
+template <typename T>
+void DenseFromRagged(const Tensor& idx, const T* data, int64_t n, int64_t w, T pad, T* out) {
+  const std::vector<int64_t> ix = idx.ToInt64();
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t b = 2 * i + 1 < static_cast<int64_t>(ix.size()) ? ix[2 * i] : 0;
+    const int64_t e = 2 * i + 1 < static_cast<int64_t>(ix.size()) ? ix[2 * i + 1] : 0;
+    const int64_t m = std::min(e - b, w);
+    for (int64_t j = 0; j < w; ++j) out[i * w + j] = j < m ? data[b + j] : pad;
+  }
+}
+
+// the shard servers, through the session's distribute-mode plans (see pipeline.h)
+class RemoteSource : public SageSource {
+ public:
+  explicit RemoteSource(QueryProxy* q) : q_(q) {}
+
+  void Roots(const SageBatchSpec& s, Rng&, int64_t* roots, float* labels) override {
+    std::vector<std::pair<std::string, Tensor>> in = {
+        {"node_type", Tensor::FromVector(std::vector<int32_t>{s.node_type})},
+        {"count", Tensor::FromVector(std::vector<int64_t>{s.batch})}};
+    std::string gql = "sampleN(node_type, count).as(r)";
+    std::vector<std::string> outs = {"r:0"};
+    const bool lab = s.label_dim > 0 && !s.label_name.empty();
+    if (lab) {
+      gql += ".values(__lab).as(lb)";
+      in.push_back({"__lab", Tensor::Strings({s.label_name})});
+      outs.push_back("lb:0");
+      outs.push_back("lb:1");
+    }
+    std::vector<Tensor> res;
+    Check(q_->Run(gql, in, outs, &res), "roots");
+    const std::vector<int64_t> r = res[0].ToInt64();
+    for (int i = 0; i < s.batch; ++i) roots[i] = i < static_cast<int>(r.size()) ? r[i] : s.default_node;
+    if (s.label_dim > 0) {
+      if (lab) DenseFromRagged<float>(res[1], res[2].data<float>(), s.batch, s.label_dim, 0.f, labels);
+      else memset(labels, 0, sizeof(float) * s.batch * s.label_dim);
+    }
+  }
+
+  void Hop(const SageBatchSpec& s, int hop, const int64_t* ids, int64_t n, Rng&, int64_t* out) override {
+    const int k = s.fanouts[hop - 1];
+    std::vector<uint64_t> u(ids, ids + n);
+    std::vector<int32_t> et = s.etypes[hop - 1];
+    if (et.empty()) et.push_back(-1);
+    std::vector<std::pair<std::string, Tensor>> in = {{"nodes", Tensor::FromVector(u)},
+                                                       {"edge_types", Tensor::FromVector(et)},
+                                                       {"nb_count", Tensor::FromVector(std::vector<int64_t>{k})}};
+    std::vector<Tensor> res;
+    const std::string gql = "v(nodes).sampleNB(edge_types, nb_count, " + std::to_string(s.default_node) + ").as(nb)";
+    Check(q_->Run(gql, in, {"nb:0", "nb:1"}, &res), "sampleNB");
+    const std::vector<int64_t> flat = res[1].ToInt64();
+    DenseFromRagged<int64_t>(res[0], flat.data(), n, k, s.default_node, out);
+  }
+
+  void Features(const SageBatchSpec& s, const int64_t* ids, int64_t n, int64_t fd, float* out) override {
+    std::vector<uint64_t> u(ids, ids + n);
+    std::vector<std::pair<std::string, Tensor>> in = {{"nodes", Tensor::FromVector(u)}};
+    std::string keys;
+    std::vector<std::string> outs;
+    for (size_t f = 0; f < s.dense_names.size(); ++f) {
+      const std::string k = "__f" + std::to_string(f);
+      in.push_back({k, Tensor::Strings({s.dense_names[f]})});
+      keys += (f ? ", " : "") + k;
+      outs.push_back("fea:" + std::to_string(2 * f));
+      outs.push_back("fea:" + std::to_string(2 * f + 1));
+    }
+    std::vector<Tensor> res;
+    Check(q_->Run("v(nodes).values(" + keys + ").as(fea)", in, outs, &res), "values");
+    std::vector<float> col;
+    int64_t c0 = 0;
+    for (size_t f = 0; f < s.dense_names.size(); ++f) {
+      const int64_t dim = s.dense_dims[f];
+      col.assign(static_cast<size_t>(n * dim), 0.f);
+      DenseFromRagged<float>(res[2 * f], res[2 * f + 1].data<float>(), n, dim, 0.f, col.data());
+      for (int64_t i = 0; i < n; ++i) memcpy(out + i * fd + c0, col.data() + i * dim, dim * sizeof(float));
+      c0 += dim;
+    }
+  }
+
+ private:
+  static void Check(const Status& st, const char* what) {
+    if (!st.ok()) EULER_THROW("SagePipeline remote " << what << ": " << st.ToString());
+  }
+  QueryProxy* q_;
+};
+
+}  // namespace
+
+std::unique_ptr<SageSource> MakeLocalSource(const Graph* g) { return std::unique_ptr<SageSource>(new LocalSource(g)); }
+std::unique_ptr<SageSource> MakeRemoteSource(QueryProxy* q) {
+  return std::unique_ptr<SageSource>(new RemoteSource(q));
+}
+
 SagePipeline::SagePipeline(const Graph* g, SageBatchSpec spec, std::vector<int64_t*> ints, std::vector<float*> floats,
                            int workers, uint64_t seed)
-    : g_(g), spec_(std::move(spec)), ints_(std::move(ints)), floats_(std::move(floats)), seed_(seed) {
+    : SagePipeline(MakeLocalSource(g), std::move(spec), std::move(ints), std::move(floats), workers, seed) {}
+
+SagePipeline::SagePipeline(std::unique_ptr<SageSource> src, SageBatchSpec spec, std::vector<int64_t*> ints,
+                           std::vector<float*> floats, int workers, uint64_t seed)
+    : src_(std::move(src)), spec_(std::move(spec)), ints_(std::move(ints)), floats_(std::move(floats)), seed_(seed) {
   lay_ = SageSlotLayout::Make(spec_);
   if (ints_.size() != floats_.size() || ints_.empty()) EULER_THROW("SagePipeline: one int and one float buffer per slot");
   if (spec_.etypes.size() != spec_.fanouts.size() || spec_.fanouts.empty() || spec_.fanouts.size() > 7)
     EULER_THROW("SagePipeline: 1..7 hops, one edge-type list per fanout");
-  if (spec_.dense_idx.size() != spec_.dense_dims.size()) EULER_THROW("SagePipeline: one dimension per feature");
+  if (spec_.dense_dims.size() != std::max(spec_.dense_idx.size(), spec_.dense_names.size()))
+    EULER_THROW("SagePipeline: one dimension per feature");
   for (int i = 0; i < static_cast<int>(ints_.size()); ++i) free_.push_back(i);
+  Start(workers);
+}
+
+void SagePipeline::Start(int workers) {
   const int nw = std::max(1, workers);
   for (int w = 0; w < nw; ++w) threads_.emplace_back([this] { Worker(); });
 }
@@ -138,24 +302,19 @@ void SagePipeline::Release(int slot) {
 }
 
 void SagePipeline::Fill(int slot, uint64_t seq) {
-  const Graph& g = *g_;
   const SageBatchSpec& s = spec_;
   const SageSlotLayout& lay = lay_;
   int64_t* I = ints_[slot];
   float* Fp = floats_[slot];
   const int L = static_cast<int>(s.fanouts.size());
   Rng rng(seed_, seq);
-  // roots
-  std::vector<uint64_t> roots;
-  g.SampleNode(s.node_type, s.batch, rng, &roots);
+  // roots (+ labels)
   int64_t* lvl0 = I + 16;
-  for (int i = 0; i < s.batch; ++i)
-    lvl0[i] = i < static_cast<int>(roots.size()) ? static_cast<int64_t>(roots[i]) : s.default_node;
+  src_->Roots(s, rng, lvl0, s.label_dim > 0 ? Fp + lay.off_labels : nullptr);
   I[0] = L;
   I[1] = s.batch;
   // hops
   std::vector<int64_t> cat, inv;
-  std::vector<IdWeightType> tmp;
   std::vector<std::pair<int64_t, int64_t>> table;
   const int64_t* cur = lvl0;
   int64_t n = s.batch;
@@ -163,11 +322,7 @@ void SagePipeline::Fill(int slot, uint64_t seq) {
     const int k = s.fanouts[h - 1];
     cat.resize(static_cast<size_t>(n * k + n));
     inv.resize(cat.size());
-    for (int64_t i = 0; i < n; ++i) {
-      g.SampleNeighbor(g.Row(static_cast<uint64_t>(cur[i])), s.etypes[h - 1], k, true, rng, &tmp);
-      for (int j = 0; j < k; ++j)
-        cat[i * k + j] = j < static_cast<int>(tmp.size()) ? static_cast<int64_t>(tmp[j].id) : s.default_node;
-    }
+    src_->Hop(s, h, cur, n, rng, cat.data());
     std::copy(cur, cur + n, cat.begin() + n * k);
     int64_t* nid = I + lay.off_nid[h];
     int64_t nu = 0;
@@ -198,40 +353,7 @@ void SagePipeline::Fill(int slot, uint64_t seq) {
     n = nu;
   }
   // dense input features of the outermost node set, row-major [n][feat_dim]
-  const int64_t fd = lay.feat_dim;
-  if (fd > 0) {
-    std::vector<const Column<float>*> cols;
-    for (int idx : s.dense_idx) cols.push_back(g.NodeDense(idx));
-    for (int64_t i = 0; i < n; ++i) {
-      const int64_t r = g.Row(static_cast<uint64_t>(cur[i]));
-      float* o = Fp + i * fd;
-      int64_t c0 = 0;
-      for (size_t f = 0; f < cols.size(); ++f) {
-        const int64_t dim = s.dense_dims[f];
-        const float* p = nullptr;
-        int64_t m = 0;
-        if (cols[f] && r >= 0) cols[f]->Get(r, &p, &m);
-        m = std::min(m, dim);
-        if (m > 0) memcpy(o + c0, p, m * sizeof(float));
-        if (m < dim) memset(o + c0 + m, 0, (dim - m) * sizeof(float));
-        c0 += dim;
-      }
-    }
-  }
-  // labels of the roots
-  if (s.label_dim > 0) {
-    const Column<float>* lc = s.label_idx >= 0 ? g.NodeDense(s.label_idx) : nullptr;
-    float* o = Fp + lay.off_labels;
-    for (int i = 0; i < s.batch; ++i) {
-      const int64_t r = g.Row(static_cast<uint64_t>(lvl0[i]));
-      const float* p = nullptr;
-      int64_t m = 0;
-      if (lc && r >= 0) lc->Get(r, &p, &m);
-      m = std::min<int64_t>(m, s.label_dim);
-      if (m > 0) memcpy(o + i * s.label_dim, p, m * sizeof(float));
-      if (m < s.label_dim) memset(o + i * s.label_dim + m, 0, (s.label_dim - m) * sizeof(float));
-    }
-  }
+  if (lay.feat_dim > 0) src_->Features(s, cur, n, lay.feat_dim, Fp);
 }
 
 }  // namespace euler

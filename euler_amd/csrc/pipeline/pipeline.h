@@ -16,6 +16,8 @@
 
 #include <condition_variable>
 #include <map>
+#include <memory>
+#include <string>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -23,6 +25,8 @@
 #include "graph/graph.h"
 
 namespace euler {
+
+class QueryProxy;
 
 struct SageBatchSpec {
   int batch = 0;
@@ -33,7 +37,31 @@ struct SageBatchSpec {
   bool self_loops = true;
   std::vector<int> dense_idx, dense_dims;      // input features (concatenated)
   int label_idx = -1, label_dim = 0;           // dense label column of the roots
+  std::vector<std::string> dense_names;        // the same columns by name (remote source)
+  std::string label_name;
 };
+
+// Where a batch's graph lookups go.  LocalSource: the in-process shard (batch b draws from
+// the Philox stream (seed, b): reproducible for any worker count).  RemoteSource: the
+// shard servers, through the session's compiled distribute-mode plans — per batch one
+// roots (+ labels) query, one sampleNB query per hop over the hop's unique frontier and
+// one values() query for the outermost node set; each query is one RPC per shard
+// (split -> REMOTE -> merge, REMOTE fusion), issued by the worker thread that owns the
+// batch, so W workers keep W batches of RPCs in flight.  Remote sampling draws from the
+// servers' generators (not the batch's stream).
+class SageSource {
+ public:
+  virtual ~SageSource() = default;
+  // roots [batch] and, with label_dim > 0, their labels [batch][label_dim]
+  virtual void Roots(const SageBatchSpec& s, Rng& rng, int64_t* roots, float* labels) = 0;
+  // k neighbour draws per id (default_node where none), out [n * k]
+  virtual void Hop(const SageBatchSpec& s, int hop, const int64_t* ids, int64_t n, Rng& rng, int64_t* out) = 0;
+  // dense input features [n][feat_dim] (zero-filled when missing)
+  virtual void Features(const SageBatchSpec& s, const int64_t* ids, int64_t n, int64_t feat_dim, float* out) = 0;
+};
+
+std::unique_ptr<SageSource> MakeLocalSource(const Graph* g);
+std::unique_ptr<SageSource> MakeRemoteSource(QueryProxy* proxy);
 
 // Slot layout (int64 words):
 //   [0, 16)            header: hdr[0] = L, hdr[1 + h] = |n_id of level h| (h = 0..L),
@@ -55,6 +83,8 @@ class SagePipeline {
  public:
   SagePipeline(const Graph* g, SageBatchSpec spec, std::vector<int64_t*> ints, std::vector<float*> floats,
                int workers, uint64_t seed);
+  SagePipeline(std::unique_ptr<SageSource> src, SageBatchSpec spec, std::vector<int64_t*> ints,
+               std::vector<float*> floats, int workers, uint64_t seed);
   ~SagePipeline();
   // the next batch's slot, in sequence order (blocks; -1 after Stop)
   int Next();
@@ -65,9 +95,10 @@ class SagePipeline {
   int64_t batches() const { return next_seq_; }
 
  private:
+  void Start(int workers);
   void Worker();
   void Fill(int slot, uint64_t seq);
-  const Graph* g_;
+  std::unique_ptr<SageSource> src_;
   SageBatchSpec spec_;
   SageSlotLayout lay_;
   std::vector<int64_t*> ints_;

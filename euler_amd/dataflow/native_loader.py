@@ -18,6 +18,15 @@ the step; the round-1 Python prefetcher called ``pin_memory()`` on every batch.
 Batch b is drawn from the Philox stream (seed, b) and delivered in order, so the batch
 stream is reproducible for any worker count.
 
+Remote sessions (``initialize_shared_graph``; also ``local_sharded``): the same workers
+build the batch through the session's distribute-mode GQL plans — one roots (+ labels)
+query, one ``sampleNB`` query per hop over the hop's unique frontier and one ``values``
+query for the outermost nodes, each one RPC per shard (csrc/pipeline/pipeline.cc
+RemoteSource; reference tf_euler/kernels/sample_fanout_with_feature_op.cc:43-69 +
+euler/core/kernels/remote_op.cc:60-146) — so W workers keep W batches of RPCs in flight
+and the step still only consumes ready slots.  Remote draws come from the servers'
+generators.
+
 Static mode (``static=True``, GPU only) serves every batch through ONE set of
 fixed-capacity device tensors, the inputs of a graph-captured training step
 (estimator/graph_step.py): the slot's ``res`` / ``nbr`` are padded with -1 up to the
@@ -67,8 +76,9 @@ class NativeSageLoader:
         import euler_amd.ops.graph_api as ge
 
         eng = get_engine()
-        if eng.meta()["mode"] != "local":
-            raise ValueError("the native pipeline needs the graph in this process (local mode)")
+        self.mode = eng.meta()["mode"]
+        if self.mode not in ("local", "remote", "local_sharded"):
+            raise ValueError("the native pipeline serves local, local_sharded and remote sessions")
         self.device = torch.device(device)
         self.cuda = self.device.type == "cuda"
         self.B = int(batch_size)

@@ -366,7 +366,7 @@ class BaseEstimator:
         from euler_amd.ops.base import get_engine
 
         spec = native_spec(self.model, self.params)
-        if spec is None or get_engine().meta()["mode"] != "local":
+        if spec is None or get_engine().meta()["mode"] not in ("local", "remote", "local_sharded"):
             return None
         flow, names, dims, label, label_dim, node_type = spec
         seed = int(self.params.get("seed") or 0) * 1000003 + self.rank

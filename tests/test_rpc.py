@@ -427,3 +427,82 @@ def test_udf_with_parameters_on_shard_servers(cluster):
     data, reg = cluster
     ea.initialize_shared_graph(reg, shard_num=2)
     check_udfs(*_udf_queries())
+
+
+def test_native_pipeline_over_shard_servers(cluster):
+    """The native batch pipeline on a remote session (csrc/pipeline/pipeline.cc
+    RemoteSource): the SageDataFlow contract holds, every sampled neighbour is a real
+    out-neighbour, and features / labels equal the engine's own lookups."""
+    import torch
+
+    from euler_amd.dataflow.dataflows import SageDataFlow
+    from euler_amd.dataflow.native_loader import NativeSageLoader
+
+    data, reg = cluster
+    ea.initialize_shared_graph(reg, shard_num=2)
+    flow = SageDataFlow([3, 2], [["0", "1"], ["0", "1"]], add_self_loops=True, max_id=6)
+    ld = NativeSageLoader(flow, ["f3"], [2], "f4", 3, 8, -1, "cpu", workers=2, seed=1)
+    full = {n: set(ea.get_full_neighbor([n], ["0", "1"])[0].to_dense().reshape(-1).tolist()) - {0}
+            for n in range(1, 7)}
+    try:
+        for _ in range(3):
+            p = ld.get()
+            df = p.fields["embed_in"].fields["flow"]
+            prev = p.fields["inputs"]
+            assert set(prev.tolist()) <= set(range(1, 7))
+            for b in df.blocks:
+                assert torch.equal(b.n_id[b.res_n_id], prev)
+                for i, row in enumerate(b.nbr[:, :-1].tolist()):
+                    src = int(prev[i])
+                    for j in row:
+                        nb = int(b.n_id[j])
+                        assert nb in full[src] or (nb == 7 and not full[src]), (src, nb)
+                prev = b.n_id
+            x = p.fields["embed_in"].fields["x"]
+            want = ea.get_dense_feature(df.blocks[-1].n_id, ["f3"], [2])[0]
+            assert torch.allclose(x, torch.as_tensor(want).float())
+            lab = ea.get_dense_feature(p.fields["inputs"], ["f4"], [3])[0]
+            assert torch.allclose(p.fields["label"], torch.as_tensor(lab).float())
+    finally:
+        ld.close()
+
+
+def test_remote_native_pipeline_trains_like_local(tmp_path):
+    """SupervisedGraphSage through the estimator + native pipeline: graph on 2 shard
+    servers vs the same graph in-process.  Remote draws come from the servers' own
+    generators, so the trajectories agree statistically (final loss within 10 %)."""
+    sys.path.insert(0, os.path.join(ROOT, "benchmarks"))
+    from bench_engine_sage import start_cluster
+
+    from euler_amd import models as Z
+    from euler_amd.dataset import get_dataset
+    from euler_amd.estimator import NodeEstimator
+
+    ds = get_dataset("ppi", data_dir=str(tmp_path / "ppi"), scale=0.03)
+    ds.partition_num = 2
+    d = ds.load_graph()
+    tnt = ds.train_node_type[0] if isinstance(ds.train_node_type, list) else ds.train_node_type
+
+    def train(tag):
+        ea.set_seed(3)
+        import torch
+
+        torch.manual_seed(0)
+        m = Z.SupervisedGraphSage([32, 32, ds.label_dim], [5, 5], [["train"], ["train"]], "feature", ds.feature_dim,
+                                  "label", ds.label_dim, max_id=ds.max_node_id)
+        params = {"model_dir": str(tmp_path / tag), "batch_size": 128, "total_step": 60, "optimizer": "adam",
+                  "learning_rate": 0.01, "log_steps": 60, "train_node_type": tnt, "device": "cpu", "seed": 4,
+                  "native_pipeline": True, "pipeline_workers": 3}
+        return NodeEstimator(m, params).train()
+
+    local = train("local")
+    reg, procs = start_cluster(d, 2, 4)
+    try:
+        ea.initialize_shared_graph(reg, shard_num=2)
+        remote = train("remote")
+    finally:
+        for p in procs:
+            p.terminate()
+            p.wait(timeout=30)
+    assert remote["step"] == local["step"] == 60
+    assert abs(remote["loss"] - local["loss"]) < 0.1 * local["loss"], (local, remote)
