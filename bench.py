@@ -59,6 +59,10 @@ def parse_args(argv=None):
     p.add_argument("--grad-buckets", type=int, choices=[1, 2], default=1,
                    help="data-parallel gradient buckets: 1 = one all-reduce after the reduce (one stream); "
                         "2 = the head-layer bucket's reduce + all-reduce overlap the routed dW on a side stream")
+    p.add_argument("--shard-features", action="store_true",
+                   help="row-shard the feature table over the ranks (row r on rank r %% world); every step's "
+                        "sampled rows come over an all-to-all (graph/sharded_features.py). Needs the process "
+                        "group: torchrun, or --force-dist with one rank")
     p.add_argument("--force-dist", action="store_true",
                    help="take the multi-GPU code path (process group, all-reduce in the step) even with one rank")
     return p.parse_args(argv)
@@ -124,8 +128,17 @@ def main(argv=None):
             f"build {time.time()-t0:.1f}s")
 
     dims = [args.hidden_dim] * (len(fanouts) + 1)  # reference run_graphsage: [hidden] * (layers + 1)
+    fshard = None
+    if args.shard_features:
+        if not dist_on:
+            raise SystemExit("--shard-features needs the process group (torchrun, or --force-dist with one rank)")
+        from euler_amd.graph.sharded_features import ShardedFeatures
+
+        fshard = ShardedFeatures(feats[rank::world].contiguous(), args.num_nodes, force_comm=True)
+        feats = None  # this rank keeps its shard only
+        torch.cuda.empty_cache()
     tr = SageTrainer(graph, B, fanouts, dims, args.label_dim, features=feats, labels=labels, learning_rate=args.lr,
-                     init_seed=args.seed, keep_samples=False, grad_buckets=args.grad_buckets)
+                     init_seed=args.seed, keep_samples=False, grad_buckets=args.grad_buckets, feature_shard=fshard)
     grad_sync = None
     if dist_on:
         dist.broadcast(tr.flat, 0)
@@ -182,6 +195,8 @@ def main(argv=None):
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
     last_loss = float(tr.loss.item())
+    if fshard is not None:
+        fshard.check_overflow()
     ms = elapsed * 1000.0 / max(args.steps, 1)
     value = world * B * args.steps / elapsed
     base_value, base_note = _cpu_baseline()
@@ -213,6 +228,8 @@ def main(argv=None):
                 "hidden_dim": args.hidden_dim,
                 "label_dim": args.label_dim,
                 "hipgraph": use_graph,
+                "feature_sharding": (f"row-sharded over {world} rank(s), per-step all-to-all of the sampled rows"
+                                     if fshard is not None else None),
                 "grad_sync": f"rccl all-reduce ({args.grad_reduce_dtype} gradient, {args.grad_buckets} bucket(s)) "
                              f"in the captured step" if dist_on else None,
                 "impl": "euler_amd.models.sage_trainer.SageTrainer (4 fused gfx950 launches per step)",

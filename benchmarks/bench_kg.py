@@ -66,9 +66,11 @@ class RGCNTransE(nn.Module):
                 h = F.relu(h)
         return h
 
+    norm = True
+
     def forward(self, edge_index, edge_rel, src, rel, dst, negs):
         h = self.encode(edge_index, edge_rel).float()
-        pos, neg = gnn_ops.kg_score(h, self.rel, src, dst, rel, negs, "l2", "both", True)
+        pos, neg = gnn_ops.kg_score(h, self.rel, src, dst, rel, negs, "l2", "both", self.norm)
         return F.relu(self.margin + neg.mean(-1) - pos).mean()
 
 
@@ -85,6 +87,13 @@ def main(argv=None):
     p.add_argument("--lr", type=float, default=1e-3)
     p.add_argument("--seed", type=int, default=3)
     p.add_argument("--layers", type=int, default=2, help="R-GCN layers before the TransE decoder (0: TransE alone)")
+    p.add_argument("--normalize", type=int, default=1,
+                   help="1: l2-normalised rows in the score (reference transX.py:63-66); 0: raw rows")
+    p.add_argument("--task", choices=["lattice", "cold"], default="lattice",
+                   help="cold: a fraction of the entities never appears in a loss triple (their edges stay in "
+                        "the encoder graph); held-out triples with a cold head are ranked")
+    p.add_argument("--cold-frac", type=float, default=0.1)
+    p.add_argument("--no-graph", action="store_true", help="eager steps (default: one hipGraph per step)")
     p.add_argument("--eval-after", type=int, default=2000,
                    help="keep training (untimed) to this many steps, then rank the held-out triples")
     args = p.parse_args(argv)
@@ -99,58 +108,97 @@ def main(argv=None):
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=dev)
-    from euler_amd.parallel.dp import GradSync, broadcast_module
+    from euler_amd.parallel.flat import FlatOptimizer, FlatParams
 
+    norm = bool(args.normalize)
     (src, rel, dst), (te_src, te_rel, te_dst) = synthetic_kg(args.num_ent, args.num_rel, args.num_triples,
                                                              args.seed, dev)
-    # message direction src -> dst (row 0 = destination, row 1 = source)
+    # message direction src -> dst (row 0 = destination, row 1 = source); every training
+    # triple is an encoder edge, also in the cold task
     edge_index = torch.stack([dst, src])
-    torch.manual_seed(args.seed)
+    pool = torch.arange(src.numel(), device=dev)
+    if args.task == "cold":
+        g = torch.Generator().manual_seed(args.seed + 5)
+        cold = torch.zeros(args.num_ent, dtype=torch.bool)
+        cold[torch.randperm(args.num_ent, generator=g)[: int(args.cold_frac * args.num_ent)]] = True
+        cold = cold.to(dev)
+        pool = pool[~(cold[src] | cold[dst])]            # loss triples: warm head and tail
+        keep = cold[te_src] & ~cold[te_dst]               # test: cold head, warm tail
+        te_src, te_rel, te_dst = te_src[keep], te_rel[keep], te_dst[keep]
+    torch.manual_seed(args.seed * 101 + rank)
     model = RGCNTransE(args.num_ent, args.num_rel, args.dim, layers=args.layers).to(dev)
-    gen = torch.Generator(device=dev).manual_seed(args.seed * 101 + rank)
+    model.norm = norm
 
     def batch():
-        idx = torch.randint(0, args.num_triples, (args.batch,), device=dev, generator=gen)
-        negs = torch.randint(0, args.num_ent, (args.batch, args.num_negs), device=dev, generator=gen)
+        idx = pool[torch.randint(0, pool.numel(), (args.batch,), device=dev)]
+        negs = torch.randint(0, args.num_ent, (args.batch, args.num_negs), device=dev)
         return src[idx], rel[idx], dst[idx], negs
 
     model(edge_index, rel, *batch()).backward()  # materialise lazy layers before the optimizer
-    model.zero_grad(set_to_none=True)
+    if world > 1:
+        from euler_amd.parallel.dp import broadcast_module
+
+        broadcast_module(model)
+    # every parameter (entity / relation tables, relation weights, self-loop fc) in ONE flat
+    # fp32 buffer: one flat Adam launch (optim.hip), one all-reduce with data parallelism
+    flat = FlatParams(model.parameters(), dev)
+    opt = FlatOptimizer(flat, "adam", args.lr)
+    loss_buf = torch.zeros((), device=dev)
 
     def evaluate():
         from euler_amd.dataset.synthetic import rank_metrics, tail_ranks
 
         with torch.no_grad():
             h = model.encode(edge_index, rel).float()
-        m = rank_metrics(tail_ranks(h, model.rel, te_src, te_rel, te_dst))
+        m = rank_metrics(tail_ranks(h, model.rel, te_src, te_rel, te_dst, normalize=norm))
         return {k: round(v, 4) for k, v in m.items()}
 
     eval_init = evaluate()
-    if world > 1:
-        broadcast_module(model)
-    sync = GradSync(model.parameters()) if world > 1 else None
-    opt = torch.optim.Adam(model.parameters(), lr=args.lr, fused=True)
 
-    def step():
-        opt.zero_grad(set_to_none=True)
+    def step_body():
+        opt.zero_grad()
         loss = model(edge_index, rel, *batch())
         loss.backward()
-        if sync is not None:
-            sync.finish()
-        opt.step()
-        return loss.detach()
+        scale = 1.0
+        if world > 1:
+            dist.all_reduce(flat.grad)
+            scale = 1.0 / world
+        opt.step(scale)
+        loss_buf.copy_(loss.detach())
+
+    graph = None
+    if not args.no_graph:
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                step_body()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        flat.rebind_grads()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step_body()
+
+    def step():
+        if graph is not None:
+            graph.replay()
+        else:
+            step_body()
+        return loss_buf
 
     for _ in range(args.warmup):
-        first = step()
+        step()
     torch.cuda.synchronize()
-    first = float(first)
+    first = float(loss_buf)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        last = step()
+        step()
     torch.cuda.synchronize()
+    last = float(loss_buf)
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
@@ -158,7 +206,7 @@ def main(argv=None):
     if world > 1:
         dist.all_reduce(elt, op=dist.ReduceOp.MAX)
     el = float(elt.item())
-    done = args.warmup + args.steps
+    done = args.warmup + args.steps + (0 if args.no_graph else 2)
     while done < args.eval_after:  # untimed: learning evidence only
         step()
         done += 1
@@ -176,11 +224,12 @@ def main(argv=None):
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16 relation GEMMs (fp32 accumulate), fp32 scores",
-            "data": "synthetic (FB15k-shaped random KG, power-law relations)",
-            "config": {"model": f"R-GCN {args.layers}x RelationConv(mean, self-loop) + TransE-l2 margin, Adam",
+            "data": "synthetic (FB15k-shaped lattice KG, power-law relations)",
+            "config": {"model": f"R-GCN {args.layers}x RelationConv(mean, self-loop) + TransE-l2 margin, flat Adam",
                        "num_ent": args.num_ent, "num_rel": args.num_rel, "num_triples": args.num_triples,
                        "dim": args.dim, "batch_per_gpu": args.batch, "num_negs": args.num_negs,
-                       "parallelism": f"dp{world}", "loss_first_last": [round(first, 4), round(float(last), 4)],
+                       "normalize": norm, "task": args.task, "hipgraph": graph is not None,
+                       "parallelism": f"dp{world}", "loss_first_last": [round(first, 4), round(last, 4)],
                        "heldout_tail_ranking": {"triples": int(te_src.numel()), "entities": args.num_ent,
                                                 "after_steps": done, "init": eval_init, "trained": eval_final,
                                                 "chance_mrr": round(sum(1.0 / k for k in range(1, args.num_ent + 1))

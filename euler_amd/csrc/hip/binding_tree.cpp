@@ -277,9 +277,12 @@ class TreePlan {
   }
 
   void build_fwd() {
-    torch::Tensor x = T("features");
+    // "fwd_features" (+ "fwd_nodes" / "fwd_leaf" cache positions): the forward gathers from
+    // a feature cache filled by the sharded-feature exchange instead of the whole table
+    const bool cached = has("fwd_features");
+    torch::Tensor x = cached ? T("fwd_features") : T("features");
     TORCH_CHECK(x.dim() == 2 && x.size(1) == D_, "features must be [N, D] with D padded to 16");
-    TORCH_CHECK(x.size(0) == graph_.num_rows, "features must have one row per graph row");
+    TORCH_CHECK(cached || x.size(0) == graph_.num_rows, "features must have one row per graph row");
     TORCH_CHECK(x.scalar_type() == torch::kBFloat16 || x.scalar_type() == torch::kFloat32,
                 "features must be bf16 or fp32");
     need(x, x.scalar_type(), -1, "features");
@@ -304,8 +307,8 @@ class TreePlan {
     a.FL = sm.FL;
     a.include_self = self_;
     a.inv_leaf = 1.f / static_cast<float>(a.FL + self_);
-    a.nodes = sm.nodes;
-    a.leaf = sm.leaf;
+    a.nodes = cached ? i32("fwd_nodes", M) : sm.nodes;
+    a.leaf = cached ? i32("fwd_leaf", M * sm.FL) : sm.leaf;
     a.roots_in = sm.roots;
     roots_cur_ = torch::zeros({B_}, torch::TensorOptions().dtype(torch::kInt32).device(dev_));
     a.roots_cur = roots_cur_.data_ptr<int32_t>();

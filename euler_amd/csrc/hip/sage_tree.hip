@@ -195,7 +195,7 @@ struct Feat8<float> {
 // own work (the MFMA units are idle during the gather): Wc = Wout Wfc as 16 x 16 MFMA
 // tiles of the bf16 fm shadows (an fm fragment of Wout [C][E] is also a valid A fragment:
 // lane l holds row l & 15, k 8(l >> 4)..+7), all E/32 fragment pairs of a tile in
-// flight; bc = Wout bfc in fp32 from the masters (block 0's wave 0).  No extra blocks:
+// flight; bc = Wout bfc in fp32 from the masters (one row per block).  No extra blocks:
 // extra blocks would push tile blocks past the resident slots into a second round.
 // ----------------------------------------------------------------------------
 __device__ __forceinline__ void tr_comb_wave(const TrCombArgs& c, int first, int stride, int lane) {
@@ -223,13 +223,16 @@ __device__ __forceinline__ void tr_comb_wave(const TrCombArgs& c, int first, int
       c.WcT[fm_off(h, r, c.C)] = f2bf(acc[j]);
     }
   }
-  if (first == 0) {  // bc = Wout bfc: one row per lane, fp32
-    for (int r = lane; r < c.C; r += 64) {
-      const float* w = c.wout + static_cast<int64_t>(r) * c.E;
-      float b = 0.f;
-      for (int e = 0; e < c.E; ++e) b += w[e] * c.bfc[e];
-      c.bc[r] = b;
-    }
+  // bc = Wout bfc in fp32: one row per block (rows strided over the blocks like the tiles),
+  // the wave's lanes split E and reduce by shuffles.  (One row per lane with a serial loop
+  // over E made block 0 a 25 us straggler: 256 dependent-issue global loads per lane.)
+  for (int r = first; r < c.C; r += stride) {
+    const float* w = c.wout + static_cast<int64_t>(r) * c.E;
+    float b = 0.f;
+    for (int e = lane; e < c.E; e += 64) b += w[e] * c.bfc[e];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) b += __shfl_xor(b, o, 64);
+    if (lane == 0) c.bc[r] = b;
   }
 }
 

@@ -10,7 +10,7 @@ import shutil
 import numpy as np
 
 __all__ = ["DataSet", "get_dataset", "dataset_names", "Cora", "Citeseer", "Pubmed", "PPI", "Reddit", "FB15K",
-           "FB15K237", "WN18", "Mutag", "MovieLens1M", "TestData"]
+           "FB15K237", "WN18", "Mutag", "MovieLens1M", "TestData", "Community"]
 
 _HOME = os.environ.get("EULER_AMD_DATA", os.path.join(os.path.expanduser("~"), ".euler_amd", "data"))
 
@@ -173,6 +173,43 @@ class _Citation(DataSet):
         by_cls = [np.flatnonzero(cls == c) for c in range(max(L, 1))]
         dst = np.where(same, [rng.choice(by_cls[cls[s]]) if len(by_cls[cls[s]]) else s for s in src],
                        rng.integers(0, n, m))
+        edges = []
+        for s, d in zip(src.tolist(), dst.tolist()):
+            if s == d:
+                continue
+            t = "train" if s < start and d < start else "train_removed"
+            edges.append(_edge(s, d, t))
+            edges.append(_edge(d, s, t))
+        self._write_ids(range(start, n))
+        return {"nodes": nodes, "edges": edges}
+
+
+class Community(_Citation):
+    """Planted-community node classification (no reference counterpart: a learnable
+    synthetic task for the supervised GraphSAGE paths).  Node i is in community i % 64
+    (dataset/synthetic.py community_graph: 90 % of edges inside the community, both
+    directions stored), its label is its community mod 16 (10 % flipped,
+    community_labels, one-hot), its features a weak noisy community cue
+    (community_features) — the neighbourhood mean carries the signal, so aggregation
+    must beat a feature-only classifier.  Test nodes are the last 20 %."""
+
+    name, num_nodes, feature_dim, label_dim, test_start_num = "community", 20000, 64, 16, 16000
+    num_comm = 64
+    avg_degree = 10.0
+
+    def synthesize(self, rng):
+        from euler_amd.dataset.synthetic import community_features, community_graph, community_labels
+
+        n, L = self.total_size, self.label_dim
+        seed = int(rng.integers(0, 2 ** 31))
+        src, dst, comm = community_graph(n, self.num_comm, self.avg_degree / 2, seed=seed)
+        x = community_features(comm, self.feature_dim, signal=0.5, seed=seed).numpy()
+        y = community_labels(comm, L, noise=0.1, seed=seed).numpy()
+        start = self._split_start(n)
+        eye = np.eye(L)
+        nodes = [_node(i, "train" if i < start else "test",
+                       [{"name": "label", "type": "dense", "value": eye[y[i]].tolist()},
+                        {"name": "feature", "type": "dense", "value": x[i].tolist()}]) for i in range(n)]
         edges = []
         for s, d in zip(src.tolist(), dst.tolist()):
             if s == d:
@@ -588,6 +625,7 @@ class TestData(DataSet):
 _REGISTRY = {
     "cora": Cora, "citeseer": Citeseer, "pubmed": Pubmed, "ppi": PPI, "reddit": Reddit, "fb15k": FB15K,
     "fb15k-237": FB15K237, "wn18": WN18, "mutag": Mutag, "movielens-1m": MovieLens1M, "test_data": TestData,
+    "community": Community,
 }
 
 

@@ -78,8 +78,11 @@ def _xavier(shape, gen):
 class SageTrainer:
     def __init__(self, graph, batch_size, fanouts, dims, label_dim, features=None, labels=None, metapath=None,
                  add_self_loops=False, optimizer="adam", learning_rate=0.01, betas=(0.9, 0.999), eps=1e-8,
-                 weight_decay=0.0, init=None, init_seed=0, keep_samples=True, grad_buckets=1):
+                 weight_decay=0.0, init=None, init_seed=0, keep_samples=True, grad_buckets=1, feature_shard=None):
         self.graph = graph
+        # row-sharded features (graph/sharded_features.py): this rank holds rows r % W; each
+        # step's sampled rows come over the all-to-all into a fixed cache the forward reads
+        self.fshard = feature_shard
         self.device = graph.device
         self.B = int(batch_size)
         self.fanouts = [int(f) for f in fanouts]
@@ -106,6 +109,10 @@ class SageTrainer:
         if optimizer == "adagrad" and eps == 1e-8:
             self.eps = 1e-10
         feats = features if features is not None else graph.features
+        if feature_shard is not None:
+            feats = feature_shard.shard
+            if feats.shape[1] % 16 or feats.dtype not in (torch.bfloat16, torch.float32):
+                raise ValueError("sharded features must be bf16 / fp32 with a width padded to 16")
         labs = labels if labels is not None else graph.labels
         if feats is None or labs is None:
             raise ValueError("features and labels are required (or a graph built with from_engine)")
@@ -297,7 +304,7 @@ class SageTrainer:
              "E": self.Ep, "C": self.Cp, "C_real": self.C, "include_self": int(self.include_self),
              "indptr": g.indptr, "nbr": g.nbr, "cumw": g.cumw, "num_types": g.num_types, "node_prob": g.node_prob,
              "node_alias": g.node_alias, "root_rows": g.root_rows, "rng": g.rng,
-             "features": self.features, "labels": self.labels, "label_mode": self.label_mode,
+             "labels": self.labels, "label_mode": self.label_mode,
              "step": self._step, "flat": self.flat, "grad": self.grad, "m": self.m, "v": self.v,
              "offsets": self.offsets, "loss_acc": self.loss_acc, "loss_out": self.loss_out, "counts": self.counts,
              "lr": self.lr, "beta1": self.betas[0], "beta2": self.betas[1], "eps": self.eps,
@@ -313,6 +320,15 @@ class SageTrainer:
         self.nodes = torch.zeros(M_last, **i32)
         self.leaf = torch.zeros(M_last * FL, **i32)
         d["nodes"], d["leaf"] = self.nodes, self.leaf
+        if self.fshard is None:
+            d["features"] = self.features
+        else:
+            # the forward gathers from the exchange's cache through cache positions
+            n = M_last * (1 + FL)
+            self.fshard.alloc_cache(n)
+            self._fpos = torch.full((n,), -1, **i32)
+            d["fwd_features"] = self.fshard.cache
+            d["fwd_nodes"], d["fwd_leaf"] = self._fpos[:M_last], self._fpos[M_last:]
         # layer inputs: A rows (row-major) feed the next layer / head, A_kt the dW GEMMs
         hin = [self.Dp] + self.Hp[:-1]
         for k in range(L):
@@ -405,13 +421,18 @@ class SageTrainer:
             self.plan.sample()
             self._primed = True
 
+    def _fwd(self):
+        if self.fshard is not None:
+            self.fshard.exchange(torch.cat([self.nodes, self.leaf]), pos_out=self._fpos)
+        self.plan.fwd()
+
     def forward_backward(self):
         """Sampling, forward and backward of one step; the split-K partials are reduced
         into :attr:`grad` (the all-reduce point of data parallelism).  The sample buffers
         keep this step's batch (:meth:`samples`); the next call samples again."""
         p = self.plan
         self._prime()
-        p.fwd()
+        self._fwd()
         p.head()
         self._primed = False
         p.bwd()
@@ -461,7 +482,7 @@ class SageTrainer:
             return self._cpu_step(grad_sync)
         p = self.plan
         self._prime()
-        p.fwd()
+        self._fwd()
         p.head(None, True)
         p.bwd()
         if grad_sync is None:
@@ -504,7 +525,7 @@ class SageTrainer:
     def plan_launches(self):
         """(name, callable) of every launch of one pipelined step, for per-kernel timing"""
         p = self.plan
-        out = [("sample", p.sample), ("fwd", p.fwd), ("head", p.head),
+        out = [("sample", p.sample), ("fwd", self._fwd), ("head", p.head),
                ("head+sample", lambda: p.head(None, True))]
         if self.L == 3:
             out.append(("bwd", p.bwd))
@@ -605,10 +626,11 @@ class SageTrainer:
         y.scatter_(1, self.labels[roots.to(self.labels.device)].long().view(-1, 1), 1.0)
         return y
 
-    def logical_forward(self, params, roots, nodes, leaf):
-        """fp32 logits of the model for one sampled slotted tree"""
+    def logical_forward(self, params, roots, nodes, leaf, table=None):
+        """fp32 logits of the model for one sampled slotted tree (``table``: the feature rows
+        ``nodes`` / ``leaf`` index; default the whole feature table)"""
         dev = params["gnn.fc.weight"].device
-        x = self.features[:, : self.D].float().to(dev)
+        x = (self.features if table is None else table)[:, : self.D].float().to(dev)
         x = torch.cat([x, torch.zeros(1, self.D, device=dev)], 0)
         n = x.shape[0] - 1
         nodes, leaf = nodes.to(dev), leaf.to(dev)
@@ -658,7 +680,12 @@ class SageTrainer:
         P = self._cpu_params
         for t in P.values():
             t.grad = None
-        logits = self.logical_forward(P, roots, nodes, leaf)
+        table = None
+        if self.fshard is not None:
+            pos = self.fshard.exchange(torch.cat([nodes, leaf.reshape(-1)])).long()
+            nodes, leaf = pos[: nodes.numel()], pos[nodes.numel():].view_as(leaf)
+            table = self.fshard.cache
+        logits = self.logical_forward(P, roots, nodes, leaf, table)
         y = self._labels_of(roots).to(logits.device)
         loss = F.binary_cross_entropy_with_logits(logits, y)
         loss.backward()

@@ -32,8 +32,15 @@ def _hidden(a, out):
 
 
 def _mp(a, n=None):
-    et = _first(a._ds.train_edge_type)
-    return [[et]] * (n or a.layers)
+    """metapath: the training edges for run_mode train, every edge type otherwise (the
+    reference's run_graphsage.py:53-57 — evaluation reaches the held-out nodes, whose
+    edges are not training edges)"""
+    ds = a._ds
+    et = ds.train_edge_type
+    if a.run_mode != "train" and getattr(ds, "all_edge_type", None) not in (None, -1):
+        et = ds.all_edge_type
+    et = list(et) if isinstance(et, (list, tuple)) else [et]
+    return [et] * (n or a.layers)
 
 
 # name -> (default dataset, estimator kind, builder(args, ds))

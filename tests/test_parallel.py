@@ -520,3 +520,55 @@ def test_sage_trainer_data_parallel_lockstep(dtype, buckets):
     res = _run(_worker_sage_dp, dtype, buckets)
     assert not [r for r in res if r[1] == "error"], res
     assert len(res) == 2 and all(r[2] for r in res), res
+
+
+def _worker_sharded_features(rank, world, port, q, dedup):
+    """SageTrainer over a row-sharded feature table (graph/sharded_features.py): each
+    rank holds rows r % 2 and every step's sampled rows come over the all-to-all.  Both
+    ranks sample the same batches, so the data-parallel run must reproduce a single
+    process on the whole table step by step (losses and parameters)."""
+    try:
+        import sys
+
+        _init(rank, world, port)
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from test_sage_trainer import _graph, _tables
+        from euler_amd.graph.sharded_features import ShardedFeatures
+        from euler_amd.models.sage_trainer import SageTrainer
+
+        def make(shard):
+            g = _graph("cpu", seed=3)
+            g.manual_seed(20)
+            x, lab = _tables("cpu", g.num_rows, 32, 5, "class", torch.float32)
+            fs = ShardedFeatures.from_full(x, force_comm=True, dedup=dedup) if shard else None
+            tr = SageTrainer(g, 64, [5, 3], [32, 32, 16], 5, features=None if shard else x, labels=lab,
+                             feature_shard=fs, init_seed=3)
+            return tr, fs
+
+        tr, fs = make(True)
+        ref, _ = make(False)
+        assert fs.shard.shape[0] == (ref.features.shape[0] - rank + 1) // 2
+
+        def sync(g):
+            dist.all_reduce(g)
+            return 1.0 / world
+
+        diffs = []
+        for _ in range(5):
+            diffs.append(abs(float(tr.step(sync)) - float(ref.step())))
+        a, b = tr.logical_params(), ref.logical_params()
+        pdiff = max(float((a[k] - b[k]).abs().max()) for k in a)
+        fs.check_overflow()
+        q.put((rank, f"sharded_features_{dedup}", bool(max(diffs) < 1e-6 and pdiff < 1e-6), max(diffs), pdiff))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+
+
+@pytest.mark.parametrize("dedup", [True, False])
+def test_sage_trainer_sharded_features_matches_whole_table(dedup):
+    res = _run(_worker_sharded_features, dedup)
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == 2 and all(r[2] for r in res), res

@@ -197,6 +197,41 @@ def test_graph_replay_matches_eager(cuda):
 
 
 @pytest.mark.gpu
+def test_sharded_feature_cache_matches_whole_table(cuda):
+    """The forward reading a feature cache through cache positions (the sharded-feature
+    exchange, here one rank without collectives: unique + gather into the cache) trains
+    exactly like the forward reading the whole table, eager and graph-replayed."""
+    from euler_amd.graph.sharded_features import ShardedFeatures
+    from euler_amd.models.sage_trainer import SageTrainer
+
+    def make(shard):
+        g = _graph(cuda, seed=3)
+        g.manual_seed(20)
+        x, lab = _tables(cuda, g.num_rows, 32, 32, "class", torch.bfloat16)
+        fs = ShardedFeatures.from_full(x) if shard else None
+        return SageTrainer(g, 64, [5, 3], [64, 64, 32], 32, features=None if shard else x, labels=lab,
+                           feature_shard=fs, init_seed=3)
+
+    a, b = make(False), make(True)
+    la, lb = [], []
+    for _ in range(4):
+        a.step()
+        b.step()
+        la.append(float(a.loss.item()))
+        lb.append(float(b.loss.item()))
+    a.capture(warmup=1)
+    b.capture(warmup=1)
+    for _ in range(6):
+        a.replay()
+        b.replay()
+        la.append(float(a.loss.item()))
+        lb.append(float(b.loss.item()))
+    assert la == lb, (la, lb)
+    pa, pb = a.logical_params(), b.logical_params()
+    assert all(torch.equal(pa[k], pb[k]) for k in pa)
+
+
+@pytest.mark.gpu
 def test_grad_sync_handoff_fp32_and_bf16(cuda):
     """Data-parallel path: per bucket reduce -> grad_sync(bucket) (two buckets, the head
     bucket first, overlapped with the routed dW) -> optimizer.  With an identity sync the

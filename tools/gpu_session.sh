@@ -86,6 +86,21 @@ for st in "${S[@]}"; do
       run bench_kg 600 python -u benchmarks/bench_kg.py ;;
     learn_gat)
       run bench_gat 900 python -u benchmarks/bench_gat.py ;;
+    shard_bench)
+      # bench.py with the feature table row-sharded: one rank through the all-to-all path
+      run bench_shard 600 python -u -m torch.distributed.run --nnodes 1 --nproc-per-node 1 \
+        --master-addr 127.0.0.1 --master-port 29541 bench.py --force-dist --shard-features --steps 200 \
+        --warmup 20 || exit $?
+      run bench_force_dist 600 python -u -m torch.distributed.run --nnodes 1 --nproc-per-node 1 \
+        --master-addr 127.0.0.1 --master-port 29542 bench.py --force-dist --steps 200 --warmup 20 ;;
+    community_f1)
+      run community_f1 900 python -u benchmarks/bench_community_f1.py --steps "${F1_STEPS:-1000}" ;;
+    gat_compare)
+      # same task, same seed, same epochs: fused gat.hip vs the composed autograd reference
+      for impl in fused composed; do
+        run "bench_gat_$impl" 900 python -u benchmarks/bench_gat.py --impl $impl \
+          --eval-epochs "${GAT_EPOCHS:-400}" || exit $?
+      done ;;
     gat_variants)
       # GAT_VARIANTS="-DGAT_FWD_U=4|-DGAT_FWD_U=8": rebuild gat.hip per flag set, time the edge kernels
       IFS='|' read -ra VL <<< "${GAT_VARIANTS:-}"
@@ -95,6 +110,15 @@ for st in "${S[@]}"; do
         touch euler_amd/csrc/hip/gat.hip
         EULER_AMD_HIP_FLAGS="$v" python -m euler_amd._build > "$OUT/build_gat_variant$i.log" 2>&1 || exit 4
         EULER_AMD_HIP_FLAGS="$v" run "gat_kernels_variant$i" 300 python -u tools/gat_kernels.py || exit $?
+      done ;;
+    kg_tasks)
+      # learning evidence: unnormalised TransE alone vs R-GCN + TransE on the lattice and on
+      # the cold-entity task (KG_STEPS untimed training steps before the ranking)
+      for t in lattice cold; do
+        for l in 0 2; do
+          run "kg_${t}_l$l" 600 python -u benchmarks/bench_kg.py --task $t --layers $l --normalize 0 \
+            --eval-after "${KG_STEPS:-3000}" || exit $?
+        done
       done ;;
     kg_prof)
       run kg_prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/kg_prof" -o run --output-format csv -- \
