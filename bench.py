@@ -239,6 +239,11 @@ def main(argv=None):
         }
         print(json.dumps(out), flush=True)
     if dist_on:
+        # a live graph holding captured collectives keeps the communicator busy: drop it first
+        torch.cuda.synchronize()
+        if tr._graph_exec is not None:
+            tr._graph_exec.reset()
+            tr._graph_exec = None
         dist.barrier()
         dist.destroy_process_group()
 

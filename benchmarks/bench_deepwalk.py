@@ -58,7 +58,7 @@ def link_prediction_eval(args, dev):
     # same exchange path as the timed run (--force-dist / --mode / --wire-dtype)
     tr = DeepWalkTrainer(g, N, args.dim, args.walk_len, 1, 1, args.num_negs, args.batch, args.eval_lr, "adam",
                          seed=args.seed, force_comm=args.force_dist, static=args.mode != "dynamic",
-                         wire_dtype=args.wire_dtype)
+                         wire_dtype=args.wire_dtype, micro_batches=args.micro_batches)
     pu, pv = src[hold].to(dev), dst[hold].to(dev)
     nu = torch.randint(0, N, (n_hold,), generator=gen).to(dev)
     nv = torch.randint(0, N, (n_hold,), generator=gen).to(dev)
@@ -94,6 +94,9 @@ def main(argv=None):
                    help="process group + all-to-all path even with one rank (validates the N>1 path)")
     p.add_argument("--wire-dtype", choices=["bf16", "fp32"], default="bf16",
                    help="dtype of the row / gradient all-to-alls (the table and its update stay fp32)")
+    p.add_argument("--micro-batches", type=int, choices=[1, 2], default=1,
+                   help="static/graph modes with collectives: 2 = two micro-batches per step, each one's "
+                        "all-to-alls on a comm stream under the other's compute")
     p.add_argument("--mode", choices=["graph", "static", "dynamic"], default="graph",
                    help="graph: fixed-capacity step captured in one hipGraph and replayed; static: the same "
                         "step eager; dynamic: exact-size step (host-read unique counts / all-to-all splits)")
@@ -130,7 +133,7 @@ def main(argv=None):
     g.manual_seed(args.seed * 7919 + rank)
     tr = DeepWalkTrainer(g, args.num_nodes, args.dim, args.walk_len, 1, 1, args.num_negs, args.batch, args.lr,
                          args.optimizer, seed=args.seed, force_comm=args.force_dist, static=args.mode != "dynamic",
-                         wire_dtype=args.wire_dtype)
+                         wire_dtype=args.wire_dtype, micro_batches=args.micro_batches)
     torch.cuda.synchronize()
     if rank == 0:
         gib = tr.table.nbytes() / 2 ** 30
@@ -184,7 +187,7 @@ def main(argv=None):
                        "exchange_dtype": args.wire_dtype,
                        "num_nodes": args.num_nodes, "dim": args.dim, "walks_per_gpu": args.batch,
                        "pairs_per_gpu_step": pairs_per_step, "parallelism": f"dp{world}+sharded-emb",
-                       "all_to_all": table_comm, "step_mode": args.mode,
+                       "all_to_all": table_comm, "step_mode": args.mode, "micro_batches": args.micro_batches,
                        "loss_first_last": [round(first, 4), round(loss_last, 4)],
                        "peak_mem_gib": round(peak, 1), "heldout_link_prediction": heldout},
         }), flush=True)

@@ -79,6 +79,34 @@ def run(ds, args, prefetch, device, workers=2, native=False, graph="auto"):
     return time.perf_counter() - t0, res
 
 
+def run_pipeline(ds, args, device, workers):
+    """input pipeline alone: batches/s of the native C++ pipeline (sampling, unique, feature
+    and label fetch — local engine or per-shard RPCs — into pinned slots, + H2D on a GPU),
+    drained without a model step"""
+    import euler_amd as ea
+    from euler_amd import models as Z
+    from euler_amd.dataflow.native_loader import NativeSageLoader, native_spec
+
+    ea.set_seed(1)
+    model = Z.SupervisedGraphSage([128, 128, ds.label_dim], [10, 10], [["train"], ["train"]], "feature",
+                                  ds.feature_dim, "label", ds.label_dim, max_id=ds.max_node_id)
+    tnt = ds.train_node_type[0] if isinstance(ds.train_node_type, list) else ds.train_node_type
+    flow, names, dims, label, label_dim, node_type = native_spec(model, {"train_node_type": tnt})
+    ld = NativeSageLoader(flow, names, dims, label, label_dim, args.batch, node_type, torch.device(device),
+                          workers=workers, seed=1)
+    sync = torch.cuda.synchronize if device == "cuda" else (lambda: None)
+    for _ in range(args.warmup):
+        ld.get()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ld.get()
+    sync()
+    el = time.perf_counter() - t0
+    ld.close()
+    return el
+
+
 def main(argv=None):
     p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     p.add_argument("--steps", type=int, default=60)
@@ -93,6 +121,8 @@ def main(argv=None):
     p.add_argument("--shards", type=int, default=2)
     p.add_argument("--server_threads", type=int, default=8)
     p.add_argument("--device", default=None)
+    p.add_argument("--pipeline_only", action="store_true",
+                   help="time the native pipeline alone (no model step) for each --native_workers count")
     args = p.parse_args(argv)
     from euler_amd.dataset import get_dataset
 
@@ -111,6 +141,23 @@ def main(argv=None):
     print(f"[bench_engine_sage] ppi-schema graph scale {args.scale} ready in {time.time() - t0:.1f}s "
           f"({args.mode})", file=sys.stderr, flush=True)
     out = {}
+    if args.pipeline_only:
+        for w in args.native_workers:
+            el = run_pipeline(ds, args, dev, w)
+            out[f"pipeline_{w}workers"] = {"samples_per_s": round(args.batch * args.steps / el, 1),
+                                           "ms_per_batch": round(el * 1e3 / args.steps, 2)}
+            print(f"[bench_engine_sage] pipeline {w} workers: {out[f'pipeline_{w}workers']}", file=sys.stderr,
+                  flush=True)
+        for pr in procs:
+            pr.terminate()
+            pr.wait(timeout=30)
+        best = max(out, key=lambda k: out[k]["samples_per_s"])
+        print(json.dumps({"metric": "native input pipeline samples/sec (no model step)" + (
+            ", graph on %d shard servers" % args.shards if args.mode == "remote" else ""),
+            "value": out[best]["samples_per_s"], "unit": "samples/s", "steps": args.steps,
+            "config": {"batch": args.batch, "fanouts": [10, 10], "mode": args.mode, "device": dev,
+                       "shards": args.shards if args.mode == "remote" else 0, **out}}), flush=True)
+        return
     variants = [("serial", 0, 1, False, False), ("py_prefetch_1worker", 2, 1, False, False)]
     variants += [("native_%dworkers_eager" % w, 0, w, True, False) for w in args.native_workers[:1]]
     # native pipeline + graph-captured step (the estimator default on a GPU)

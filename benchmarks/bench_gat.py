@@ -184,16 +184,20 @@ def main(argv=None):
     torch.cuda.synchronize()
     first = float(loss0)
     t1 = time.perf_counter()
-    for _ in range(args.epochs):
+    for i in range(args.epochs):
         loss = step()
+        if (i + 1) % 10 == 0:
+            print(f"[bench_gat] timed epoch {i + 1}", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     el = time.perf_counter() - t1
     ms = el * 1e3 / args.epochs
     acc_timed = accuracy()
     done = args.warmup + args.epochs
     while done < args.eval_epochs:  # untimed: learning evidence only
-        step()
+        loss = step()
         done += 1
+        if done % 25 == 0:
+            print(f"[bench_gat] epoch {done} loss {float(loss):.4f}", file=sys.stderr, flush=True)
     acc_final = accuracy()
     out = {
         "metric": "GAT 8-head full-graph training throughput on ogbn-products-shaped synthetic graph",

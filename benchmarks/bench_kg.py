@@ -85,6 +85,7 @@ def main(argv=None):
     p.add_argument("--batch", type=int, default=4096, help="training triples per GPU per step")
     p.add_argument("--num-negs", type=int, default=8)
     p.add_argument("--lr", type=float, default=1e-3)
+    p.add_argument("--margin", type=float, default=1.0, help="TransE margin (reference run_transX --margin)")
     p.add_argument("--seed", type=int, default=3)
     p.add_argument("--layers", type=int, default=2, help="R-GCN layers before the TransE decoder (0: TransE alone)")
     p.add_argument("--normalize", type=int, default=1,
@@ -94,6 +95,7 @@ def main(argv=None):
                         "the encoder graph); held-out triples with a cold head are ranked")
     p.add_argument("--cold-frac", type=float, default=0.1)
     p.add_argument("--no-graph", action="store_true", help="eager steps (default: one hipGraph per step)")
+    p.add_argument("--device", default="cuda", help="cpu: torch reference ops (exploration only, eager)")
     p.add_argument("--eval-after", type=int, default=2000,
                    help="keep training (untimed) to this many steps, then rank the held-out triples")
     args = p.parse_args(argv)
@@ -101,16 +103,21 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if not torch.cuda.is_available():
-        raise SystemExit("bench_kg.py needs a GPU")
-    dev = torch.device("cuda", local_rank)
-    torch.cuda.set_device(dev)
+    if args.device == "cpu":
+        dev = torch.device("cpu")
+        args.no_graph = True
+    else:
+        if not torch.cuda.is_available():
+            raise SystemExit("bench_kg.py needs a GPU (or --device cpu)")
+        dev = torch.device("cuda", local_rank)
+        torch.cuda.set_device(dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=dev)
     from euler_amd.parallel.flat import FlatOptimizer, FlatParams
 
     norm = bool(args.normalize)
+    sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
     (src, rel, dst), (te_src, te_rel, te_dst) = synthetic_kg(args.num_ent, args.num_rel, args.num_triples,
                                                              args.seed, dev)
     # message direction src -> dst (row 0 = destination, row 1 = source); every training
@@ -126,7 +133,7 @@ def main(argv=None):
         keep = cold[te_src] & ~cold[te_dst]               # test: cold head, warm tail
         te_src, te_rel, te_dst = te_src[keep], te_rel[keep], te_dst[keep]
     torch.manual_seed(args.seed * 101 + rank)
-    model = RGCNTransE(args.num_ent, args.num_rel, args.dim, layers=args.layers).to(dev)
+    model = RGCNTransE(args.num_ent, args.num_rel, args.dim, layers=args.layers, margin=args.margin).to(dev)
     model.norm = norm
 
     def batch():
@@ -142,6 +149,10 @@ def main(argv=None):
     # every parameter (entity / relation tables, relation weights, self-loop fc) in ONE flat
     # fp32 buffer: one flat Adam launch (optim.hip), one all-reduce with data parallelism
     flat = FlatParams(model.parameters(), dev)
+    for conv in model.convs:
+        # the relation dW accumulates straight into its flat-grad view (no [R, D, D] temporary
+        # + AccumulateGrad pass per layer; the flat grad is all-reduced as one buffer)
+        gnn_ops.enable_grad_sink(conv.matrix)
     opt = FlatOptimizer(flat, "adam", args.lr)
     loss_buf = torch.zeros((), device=dev)
 
@@ -174,7 +185,7 @@ def main(argv=None):
             for _ in range(2):
                 step_body()
         torch.cuda.current_stream().wait_stream(s)
-        torch.cuda.synchronize()
+        sync()
         flat.rebind_grads()
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
@@ -189,15 +200,15 @@ def main(argv=None):
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    sync()
     first = float(loss_buf)
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize()
+    sync()
     last = float(loss_buf)
     if world > 1:
         dist.barrier()

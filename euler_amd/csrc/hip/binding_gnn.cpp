@@ -212,7 +212,7 @@ std::vector<torch::Tensor> rel_weight_bf16(torch::Tensor W) {
 
 void rel_gemm_dw(torch::Tensor G, torch::Tensor g_idx, torch::Tensor X, torch::Tensor x_idx,
                  c10::optional<torch::Tensor> scale, torch::Tensor trel, torch::Tensor tstart, torch::Tensor tlen,
-                 c10::optional<torch::Tensor> solo, torch::Tensor dW) {
+                 c10::optional<torch::Tensor> solo, torch::Tensor dW, bool accumulate) {
   typed(G, torch::kBFloat16, "G");
   typed(X, torch::kBFloat16, "X");
   typed(g_idx, torch::kInt32, "g_idx");
@@ -237,7 +237,7 @@ void rel_gemm_dw(torch::Tensor G, torch::Tensor g_idx, torch::Tensor X, torch::T
                     x_idx.data_ptr<int32_t>(), scale.has_value() ? scale->data_ptr<float>() : nullptr,
                     trel.data_ptr<int32_t>(), tstart.data_ptr<int32_t>(), tlen.data_ptr<int32_t>(),
                     solo.has_value() ? solo->data_ptr<int32_t>() : nullptr, static_cast<int>(trel.numel()),
-                    dW.data_ptr<float>(), stream()),
+                    dW.data_ptr<float>(), accumulate ? 1 : 0, stream()),
      "rel_gemm_dw");
 }
 
@@ -532,9 +532,30 @@ std::vector<torch::Tensor> unique_first_padded(torch::Tensor x, int64_t fill) {
   return {uniq, inv, pos.narrow(0, n - 1, 1).to(torch::kInt64)};
 }
 
+// (pos [n] slot of every id in the W*C exchange space, W*C = none / did not fit; send
+// [W*C + 1] the id of every slot, -1 = empty); overflow [1] int32 is set to 1 when an id
+// did not fit its owner's C slots
+std::vector<torch::Tensor> route_by_owner(torch::Tensor ids, int64_t W, int64_t C, torch::Tensor overflow) {
+  typed(ids, torch::kInt64, "ids");
+  typed(overflow, torch::kInt32, "overflow");
+  TORCH_CHECK(overflow.numel() >= 1 && overflow.device() == ids.device(), "overflow must be [1] int32 on the ids' device");
+  TORCH_CHECK(W >= 1 && W <= 63 && C >= 1, "route_by_owner: 1 <= W <= 63, C >= 1");
+  const int64_t n = ids.numel();
+  const c10::DeviceGuard g(ids.device());
+  auto opts = ids.options();
+  auto pos = torch::empty({n}, opts);
+  auto send = torch::full({W * C + 1}, -1, opts);
+  auto cnt = torch::empty({std::max<int64_t>(eh_route_chunks(n), 1) * (W + 1)}, opts.dtype(torch::kInt32));
+  ok(eh_route_by_owner(ids.data_ptr<int64_t>(), n, static_cast<int>(W), C, cnt.data_ptr<int32_t>(),
+                       pos.data_ptr<int64_t>(), send.data_ptr<int64_t>(), overflow.data_ptr<int32_t>(), stream()),
+     "route_by_owner");
+  return {pos, send};
+}
+
 }  // namespace
 
 void register_gnn_ops(pybind11::module& m) {
+  m.def("route_by_owner", &route_by_owner);
   m.def("gat_supported", &gat_supported);
   m.def("gat_fwd", &gat_fwd, py::arg("indptr"), py::arg("col"), py::arg("order"), py::arg("h"), py::arg("al"),
         py::arg("ar"), py::arg("H"), py::arg("C"), py::arg("slope"), py::arg("a_src") = py::none());
@@ -544,7 +565,9 @@ void register_gnn_ops(pybind11::module& m) {
   m.def("gat_att_fwd", &gat_att_fwd);
   m.def("gat_att_bwd_", &gat_att_bwd_);
   m.def("rel_gemm", &rel_gemm);
-  m.def("rel_gemm_dw", &rel_gemm_dw);
+  m.def("rel_gemm_dw", &rel_gemm_dw, py::arg("G"), py::arg("g_idx"), py::arg("X"), py::arg("x_idx"), py::arg("scale"),
+        py::arg("trel"), py::arg("tstart"), py::arg("tlen"), py::arg("solo"), py::arg("dW"),
+        py::arg("accumulate") = false);
   m.def("rel_weight_bf16", &rel_weight_bf16);
   m.attr("rel_gemm_dw_chunk") = eh_rel_gemm_dw_chunk();
   m.attr("rel_gemm_tile") = eh_rel_gemm_tile();

@@ -83,7 +83,7 @@ hipError_t eh_rel_gemm(const void* A, int K, const int32_t* a_idx, const int32_t
                        const int32_t* o_idx, int mode, int tm, void* Y, hipStream_t s);
 hipError_t eh_rel_gemm_dw(const void* G, int N, const int32_t* g_idx, const void* X, int K, const int32_t* x_idx,
                           const float* scale, const int32_t* crel, const int32_t* cstart, const int32_t* clen,
-                          const int32_t* csolo, int n_chunks, float* dW, hipStream_t s);
+                          const int32_t* csolo, int n_chunks, float* dW, int accum, hipStream_t s);
 
 // embed.hip (K10 knowledge-graph scores, K11 skip-gram sigmoid-CE)
 hipError_t eh_sgns_fwd(const void* emb, const void* pos, const void* neg, int is_bf16, int64_t B, int P, int K, int D,
@@ -106,6 +106,11 @@ hipError_t eh_kg_fwd(const float* ent, const float* rel, const int64_t* src, con
 hipError_t eh_kg_bwd(const float* ent, const float* rel, const int64_t* src, const int64_t* dst, const int64_t* ridx,
                      const int64_t* neg, int64_t B, int K, int D, int kind, int corrupt, int normalize,
                      const float* gpos, const float* gneg, float* dent, float* drel, hipStream_t s);
+
+// route.hip (owner routing of the fixed-capacity all-to-all exchanges)
+int64_t eh_route_chunks(int64_t n);
+hipError_t eh_route_by_owner(const int64_t* ids, int64_t n, int W, int64_t C, int32_t* cnt, int64_t* pos,
+                             int64_t* send, int32_t* overflow, hipStream_t s);
 
 // unique.hip (K8: hash unique, first-occurrence order)
 hipError_t eh_unique_insert(const int64_t* x, int64_t n, void* keys, int32_t* minpos, int64_t cap, int32_t* slot,

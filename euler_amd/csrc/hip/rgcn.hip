@@ -155,7 +155,8 @@ __device__ __forceinline__ uint4_t rg_tr_frag(const bf16_t* img, int e0, int c0,
 // one workgroup = one (chunk of <= RG_CH edges of one relation) x (T x T slab of dW[rel]);
 // T = 128 covers a 128 x 128 weight in one slab, so every edge row is read once.  Wave w
 // owns rows w*T/4 .. of the slab (T/64 MFMA row tiles) x all T columns (T/16 tiles).
-// A chunk that is its relation's only one (csolo) stores its slab; otherwise fp32 atomics.
+// A chunk that is its relation's only one (csolo) stores its slab (accum: adds it to the
+// slab's current contents, no other workgroup touches that slab); otherwise fp32 atomics.
 template <int T>
 __global__ __launch_bounds__(256) void rel_gemm_dw_kernel(const bf16_t* __restrict__ G, int N,
                                                           const int32_t* __restrict__ g_idx,
@@ -165,7 +166,8 @@ __global__ __launch_bounds__(256) void rel_gemm_dw_kernel(const bf16_t* __restri
                                                           const int32_t* __restrict__ crel,
                                                           const int32_t* __restrict__ cstart,
                                                           const int32_t* __restrict__ clen,
-                                                          const int32_t* __restrict__ csolo, float* __restrict__ dW) {
+                                                          const int32_t* __restrict__ csolo, float* __restrict__ dW,
+                                                          int accum) {
   constexpr int LD = T + 16;
   constexpr int FM = T / 64, FN = T / 16;
   constexpr int CPR = T / 8;               // 16-byte chunks per row segment
@@ -246,7 +248,7 @@ __global__ __launch_bounds__(256) void rel_gemm_dw_kernel(const bf16_t* __restri
         const int n = sn * T + wave * (T / 4) + m * 16 + (lane >> 4) * 4 + j;
         float* dst = dWr + static_cast<int64_t>(n) * K + sk * T + f * 16 + (lane & 15);
         if (solo)
-          *dst = acc[m][f][j];
+          *dst = accum ? *dst + acc[m][f][j] : acc[m][f][j];
         else
           atomicAdd(dst, acc[m][f][j]);
       }
@@ -317,7 +319,7 @@ hipError_t eh_rel_gemm(const void* A, int K, const int32_t* a_idx, const int32_t
 
 hipError_t eh_rel_gemm_dw(const void* G, int N, const int32_t* g_idx, const void* X, int K, const int32_t* x_idx,
                           const float* scale, const int32_t* crel, const int32_t* cstart, const int32_t* clen,
-                          const int32_t* csolo, int n_chunks, float* dW, hipStream_t s) {
+                          const int32_t* csolo, int n_chunks, float* dW, int accum, hipStream_t s) {
   if (n_chunks == 0) return hipSuccess;
   if (N % 64 != 0 || K % 64 != 0) return hipErrorInvalidValue;
   const int T = (N % 128 == 0 && K % 128 == 0) ? 128 : 64;
@@ -326,11 +328,11 @@ hipError_t eh_rel_gemm_dw(const void* G, int N, const int32_t* g_idx, const void
   if (T == 128)
     hipLaunchKernelGGL(rel_gemm_dw_kernel<128>, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s,
                        static_cast<const bf16_t*>(G), N, g_idx, static_cast<const bf16_t*>(X), K, x_idx, scale, crel,
-                       cstart, clen, csolo, dW);
+                       cstart, clen, csolo, dW, accum);
   else
     hipLaunchKernelGGL(rel_gemm_dw_kernel<64>, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s,
                        static_cast<const bf16_t*>(G), N, g_idx, static_cast<const bf16_t*>(X), K, x_idx, scale, crel,
-                       cstart, clen, csolo, dW);
+                       cstart, clen, csolo, dW, accum);
   return hipGetLastError();
 }
 

@@ -12,8 +12,8 @@ hipGraph-capturable: fixed shapes, no host-read sizes):
 
   ids [n]           every sampled tree row and leaf of this rank's batch (-1 = none)
   unique            ``unique_first_padded`` (hash kernel): each distinct id once
-  route             owner = id % W, stable sort by owner, C slots per peer (fixed
-                    capacity, the ShardedTable.lookup_static scheme); an id that does
+  route             owner = id % W, stable rank per owner (route.hip), C slots per peer
+                    (fixed capacity, the ShardedTable.lookup_static scheme); an id that does
                     not fit raises the device ``overflow`` flag and reads the zero trash row
   all-to-all ids    W*C int64 per rank
   gather + all-to-all rows   the owners gather their local rows (bf16) and send them back
@@ -34,7 +34,7 @@ import torch.distributed as dist
 
 from euler_amd.ops import mp_ops
 from euler_amd.ops._native import use_hip
-from euler_amd.ops.gnn_ops import unique_first_padded
+from euler_amd.ops.gnn_ops import route_by_owner, unique_first_padded
 
 __all__ = ["ShardedFeatures"]
 
@@ -116,22 +116,7 @@ class ShardedFeatures:
             self.cache[:n].copy_(self._gather(local))
             pu = torch.arange(n, device=ids.device)
         else:
-            valid = u >= 0
-            owner = torch.where(valid, torch.remainder(u, W), torch.full_like(u, W))
-            order = torch.sort(owner, stable=True)[1]
-            cnt = torch.zeros(W + 1, dtype=torch.long, device=ids.device).index_add_(0, owner,
-                                                                                   torch.ones_like(owner))
-            start = torch.cumsum(cnt, 0) - cnt
-            so = owner[order]
-            slot = torch.arange(n, device=ids.device) - start[so]
-            real = so < W
-            fits = real & (slot < C)
-            torch.maximum(self.overflow, (real & ~fits).any().int().view(1), out=self.overflow)
-            dest = torch.where(fits, so * C + slot, torch.full_like(slot, trash))
-            send = torch.full((trash + 1,), -1, dtype=torch.long, device=ids.device)
-            send.scatter_(0, dest, torch.where(fits, u[order], torch.full_like(slot, -1)))
-            pu = torch.empty_like(dest)
-            pu[order] = dest
+            pu, send = route_by_owner(u, W, C, self.overflow)
             recv = torch.empty(trash, dtype=torch.long, device=ids.device)
             dist.all_to_all_single(recv, send[:trash], group=self.group)
             local = torch.where(recv >= 0, torch.div(recv, W, rounding_mode="floor"), torch.full_like(recv, -1))

@@ -55,7 +55,7 @@ def _pair_positions(walk_len, left, right):
 class DeepWalkTrainer:
     def __init__(self, graph, num_nodes, dim=128, walk_len=3, left_win_size=1, right_win_size=1, num_negs=5,
                  batch_size=1024, lr=0.01, optimizer="adam", group=None, seed=0, force_comm=False, static=False,
-                 wire_dtype="bf16", overflow_check_every=200):
+                 wire_dtype="bf16", overflow_check_every=200, micro_batches=1):
         self.graph = graph
         self.num_nodes = int(num_nodes)
         self.pad = self.num_nodes  # rows: num_nodes + 1 (pad row like the reference's max_id + 1)
@@ -78,17 +78,24 @@ class DeepWalkTrainer:
         # sync) so a dropped id fails loudly instead of silently training less
         self.overflow_check_every = int(overflow_check_every)
         self.steps_done = 0
+        # static mode with collectives: 2 = two micro-batches per step whose exchanges run
+        # on a comm stream under the other micro-batch's sampling / SGNS compute
+        if micro_batches not in (1, 2) or (micro_batches == 2 and self.batch % 2):
+            raise ValueError("micro_batches must be 1 or 2 (2 needs an even batch)")
+        self.micro_batches = int(micro_batches)
+        self._xstream = None
+        self._keep = None
 
     def _gather(self, rows, inv):
         if use_hip(rows, inv):
             return hip().gather_rows(rows, inv.contiguous())
         return rows[inv]
 
-    def sample(self):
+    def sample(self, batch=None):
         """(centre [P], positive [P], negatives [P, K]) global ids of one step."""
         g = self.graph
         g.advance()
-        starts = g.sample_node(self.batch, stream_id=1)
+        starts = g.sample_node(self.batch if batch is None else int(batch), stream_id=1)
         walks = g.random_walk(starts, self.walk_len, default=-1, stream_id=3).long()
         walks = torch.where(walks < 0, torch.full_like(walks, self.pad), walks)
         src = walks[:, self.pi].reshape(-1)
@@ -134,6 +141,8 @@ class DeepWalkTrainer:
             self.hip_graph = None
 
     def _step_static(self):
+        if self.micro_batches == 2 and self.table.comm:
+            return self._step_static_overlapped()
         src, pos, negs = self.sample()
         P, K = src.numel(), self.num_negs
         gscale = 1.0 / (P * (1 + K))
@@ -168,6 +177,87 @@ class DeepWalkTrainer:
             gnn_ops.sgns_grad(1, ptr_c, lst_c, coef, K, rows, None, tinv, inv_self=cinv, out=g)
             tab.apply_static(h, g[: n - 1])
         self.loss = loss_rows.sum() * gscale
+        return self.loss
+
+    # ------------------------------------------------------------------ overlapped static step
+    def _mb_front(self, nb):
+        """sample + unique + owner routing of one micro-batch (no collective)"""
+        src, pos, negs = self.sample(nb)
+        u_t, inv_t, _ = gnn_ops.unique_first_padded(src)
+        u_c, inv_c, _ = gnn_ops.unique_first_padded(torch.cat([pos, negs.reshape(-1)]))
+        rows_c_id = torch.where(u_c >= 0, u_c + self.off, u_c)
+        routed = self.table.route_static(torch.cat([u_t, rows_c_id]))
+        return {"P": src.numel(), "inv_t": inv_t, "inv_c": inv_c, "nt": u_t.numel(), "routed": routed}
+
+    def _mb_compute(self, mb, rows, h):
+        """SGNS loss + per-slot gradients of one micro-batch from its exchanged rows"""
+        K = self.num_negs
+        gscale = 1.0 / (mb["P"] * (1 + K))
+        n = rows.shape[0]
+        tinv = h.pos[mb["inv_t"]]
+        cinv = h.pos[mb["nt"] + mb["inv_c"]]
+        coef, loss_rows = gnn_ops.sgns_fwd_idx(rows, None, tinv, rows, None, cinv, K, gscale)
+        ptr_t, lst_t = gnn_ops.occ_csr(tinv, n)
+        ptr_c, lst_c = gnn_ops.occ_csr(cinv, n)
+        g = torch.empty_like(rows)
+        gnn_ops.sgns_grad(0, ptr_t, lst_t, coef, K, rows, None, cinv, inv_self=tinv, out=g)
+        gnn_ops.sgns_grad(1, ptr_c, lst_c, coef, K, rows, None, tinv, inv_self=cinv, out=g)
+        return g[: n - 1], loss_rows.sum() * gscale, (coef, ptr_t, lst_t, ptr_c, lst_c, g)
+
+    def _step_static_overlapped(self):
+        """Two micro-batches of batch/2 walks.  Compute stream S: front0, front1, compute0,
+        compute1; comm stream X: exchange0 (after front0), exchange1 (after front1), apply0
+        (after compute0), apply1 (after compute1).  So exchange0 runs under front1,
+        exchange1 under compute0 and apply0 under compute1; every table read (the owners'
+        row gathers) and write (the updates) is on X in that order, micro-batch 1 reads its
+        rows before micro-batch 0's update lands (the full-batch step reads every row
+        before its single update), and every rank issues the collectives in the same
+        order on X.  Each micro-batch applies its own row-sparse optimizer update."""
+        tab = self.table
+        S = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
+        if S is None:  # CPU (gloo): the same phases in order on one stream
+            m0 = self._mb_front(self.batch // 2)
+            r0 = tab.exchange_static(m0["routed"], trash_row=True)
+            m1 = self._mb_front(self.batch // 2)
+            r1 = tab.exchange_static(m1["routed"], trash_row=True)
+            g0, l0, _ = self._mb_compute(m0, *r0)
+            tab.apply_static(r0[1], g0)
+            g1, l1, _ = self._mb_compute(m1, *r1)
+            tab.apply_static(r1[1], g1)
+            self.loss = 0.5 * (l0 + l1)
+            return self.loss
+        if self._xstream is None:
+            self._xstream = torch.cuda.Stream(device=self.device)
+        X = self._xstream
+        ev = [torch.cuda.Event() for _ in range(6)]
+        m0 = self._mb_front(self.batch // 2)
+        ev[0].record(S)
+        m1 = self._mb_front(self.batch // 2)
+        ev[1].record(S)
+        with torch.cuda.stream(X):
+            X.wait_event(ev[0])
+            r0 = tab.exchange_static(m0["routed"], trash_row=True)
+            ev[2].record(X)
+            X.wait_event(ev[1])
+            r1 = tab.exchange_static(m1["routed"], trash_row=True)
+            ev[3].record(X)
+        S.wait_event(ev[2])
+        g0, l0, k0 = self._mb_compute(m0, *r0)
+        ev[4].record(S)
+        with torch.cuda.stream(X):
+            X.wait_event(ev[4])
+            tab.apply_static(r0[1], g0)
+        S.wait_event(ev[3])
+        g1, l1, k1 = self._mb_compute(m1, *r1)
+        ev[5].record(S)
+        with torch.cuda.stream(X):
+            X.wait_event(ev[5])
+            tab.apply_static(r1[1], g1)
+        S.wait_stream(X)
+        # every intermediate stays referenced until the next step: tensors made on one
+        # stream and read on the other are never handed back to the allocator mid-step
+        self._keep = (m0, m1, r0, r1, g0, g1, k0, k1)
+        self.loss = 0.5 * (l0 + l1)
         return self.loss
 
     def _step_dynamic(self):

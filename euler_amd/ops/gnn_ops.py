@@ -456,6 +456,7 @@ class _RelationTransform(torch.autograd.Function):
         out = _seg_sum(msg, tiles.dst_seg.indptr, op)
         ctx.tiles, ctx.dims = tiles, (R, N, K, Kp, Np, x.shape[0])
         ctx.x_dtype, ctx.w_dtype = x.dtype, weight.dtype
+        ctx.weight = weight
         ctx.wt = wt
         ctx.save_for_backward(xb, wb)
         return out[:, :N].to(x.dtype)
@@ -475,11 +476,29 @@ class _RelationTransform(torch.autograd.Function):
             dxp = _seg_sum(msgx, tiles.src_seg.indptr, 0)
             dx = dxp[:, :K].to(ctx.x_dtype)
         if ctx.needs_input_grad[1]:
-            dwp = torch.zeros(R, Np, Kp, device=dout.device, dtype=torch.float32)
             cr, cs, cl = tiles.chunks()
-            hip().rel_gemm_dw(gb, tiles.dst, xb, tiles.src, tiles.scale, cr, cs, cl, tiles.chunk_solo, dwp)
-            dw = dwp[:, :N, :K].to(ctx.w_dtype)
+            sink = ctx.weight.grad if getattr(ctx.weight, "_grad_sink", False) else None
+            if (sink is not None and sink.dtype == torch.float32 and sink.is_contiguous()
+                    and tuple(sink.shape) == (R, Np, Kp)):
+                # grad sink (enable_grad_sink): dW accumulates straight into the weight's
+                # persistent .grad buffer (e.g. a FlatParams view the optimizer zeroes) — no
+                # zero-filled [R, N, K] temporary and no AccumulateGrad add pass over it
+                hip().rel_gemm_dw(gb, tiles.dst, xb, tiles.src, tiles.scale, cr, cs, cl, tiles.chunk_solo, sink,
+                                  accumulate=True)
+            else:
+                dwp = torch.zeros(R, Np, Kp, device=dout.device, dtype=torch.float32)
+                hip().rel_gemm_dw(gb, tiles.dst, xb, tiles.src, tiles.scale, cr, cs, cl, tiles.chunk_solo, dwp)
+                dw = dwp[:, :N, :K].to(ctx.w_dtype)
         return dx, dw, None, None
+
+
+def enable_grad_sink(weight, on: bool = True):
+    """Let :func:`relation_transform`'s backward accumulate dW straight into
+    ``weight.grad`` (which must then exist and persist, zeroed by its owner between steps,
+    as FlatParams grads do).  Autograd never sees that gradient: gradient hooks on the
+    weight (e.g. dp.GradSync buckets) do not fire for it — sync the owner's flat grad."""
+    weight._grad_sink = bool(on)
+    return weight
 
 
 def relation_transform(x, rel, weight, edge_index, size, aggr="mean", tiles=None):
@@ -584,6 +603,35 @@ def unique_first_padded(x: torch.Tensor, fill: int = -1):
     out = torch.full((x.numel(),), int(fill), dtype=torch.long, device=x.device)
     out[: u.numel()] = u
     return out, inv.long(), torch.tensor([u.numel()], dtype=torch.long, device=x.device)
+
+
+def route_by_owner(ids, W: int, C: int, overflow):
+    """Slots of the fixed-capacity all-to-all exchange (csrc/hip/route.hip): id k (>= 0)
+    goes to owner ``ids[k] % W`` at slot ``owner * C + r``, r = its stable rank among the
+    ids of that owner; ids < 0 or past an owner's C slots get ``W * C`` (the latter set
+    ``overflow[0] = 1``).  Returns ``(pos [n] int64, send [W*C + 1] int64)``: the slot of
+    every id and the id in every slot (-1 = empty)."""
+    ids = ids.reshape(-1).long()
+    if use_hip(ids):
+        return tuple(hip().route_by_owner(ids.contiguous(), int(W), int(C), overflow))
+    n = ids.numel()
+    trash = W * C
+    owner = torch.where(ids >= 0, torch.remainder(ids, W), torch.full_like(ids, W))
+    order = torch.sort(owner, stable=True)[1]
+    cnt = torch.zeros(W + 1, dtype=torch.long, device=ids.device).index_add_(0, owner, torch.ones_like(owner))
+    start = torch.cumsum(cnt, 0) - cnt
+    so = owner[order]
+    slot = torch.arange(n, device=ids.device) - start[so]
+    real = so < W
+    fits = real & (slot < C)
+    torch.maximum(overflow, (real & ~fits).any().int().view(1), out=overflow)
+    dest = torch.where(fits, so * C + slot, torch.full_like(slot, trash))
+    send = torch.full((trash + 1,), -1, dtype=torch.long, device=ids.device)
+    send.scatter_(0, dest, torch.where(fits, ids[order], torch.full_like(slot, -1)))
+    send[trash] = -1
+    pos = torch.empty_like(dest)
+    pos[order] = dest
+    return pos, send
 
 
 def occ_csr(inv, n_u):

@@ -41,7 +41,7 @@ import torch.distributed as dist
 
 from euler_amd.ops import mp_ops
 from euler_amd.ops._native import hip, use_hip
-from euler_amd.ops.gnn_ops import unique_first
+from euler_amd.ops.gnn_ops import route_by_owner, unique_first
 
 __all__ = ["ShardedTable", "LookupHandle", "StaticHandle"]
 
@@ -123,27 +123,23 @@ class ShardedTable:
             if extra:
                 rows = torch.cat([rows, rows.new_zeros(1, self.dim)])
             return rows, StaticHandle(pos, ids)
-        W, C = self.world, self.capacity(n)
-        valid = ids >= 0
-        owner = torch.where(valid, torch.remainder(ids, W), torch.full_like(ids, W))
-        order = torch.sort(owner, stable=True)[1]
-        cnt = torch.zeros(W + 1, dtype=torch.long, device=ids.device).index_add_(0, owner, torch.ones_like(owner))
-        start = torch.cumsum(cnt, 0) - cnt
-        so = owner[order]
-        slot = torch.arange(n, device=ids.device) - start[so]
-        real = so < W
-        fits = real & (slot < C)
-        torch.maximum(self.overflow, (real & ~fits).any().int().view(1), out=self.overflow)
-        trash = W * C
-        dest = torch.where(fits, so * C + slot, torch.full_like(slot, trash))
-        send = torch.full((trash + 1,), -1, dtype=torch.long, device=ids.device)
-        send.scatter_(0, dest, torch.where(fits, ids[order], torch.full_like(slot, -1)))
-        pos = torch.empty_like(dest)
-        pos[order] = dest
-        recv = torch.empty(trash, dtype=torch.long, device=ids.device)
+        return self.exchange_static(self.route_static(ids), trash_row)
+
+    def route_static(self, ids: torch.Tensor):
+        """first half of :meth:`lookup_static` (no collective): the exchange slots of the
+        padded distinct ids -> ``(pos, send)``, for a caller that overlaps the exchange"""
+        ids = ids.reshape(-1).long()
+        return route_by_owner(ids, self.world, self.capacity(ids.numel()), self.overflow)
+
+    def exchange_static(self, routed, trash_row: bool = False):
+        """second half of :meth:`lookup_static`: the id and row all-to-alls of routed ids"""
+        pos, send = routed
+        W = self.world
+        trash = send.numel() - 1
+        recv = torch.empty(trash, dtype=torch.long, device=send.device)
         dist.all_to_all_single(recv, send[:trash], group=self.group)
         local = torch.where(recv >= 0, torch.div(recv, W, rounding_mode="floor"), torch.full_like(recv, -1))
-        out = self._a2a_rows(self._gather(local), extra=extra)
+        out = self._a2a_rows(self._gather(local), extra=1 if trash_row else 0)
         return out, StaticHandle(pos, local)
 
     def apply_static(self, handle: StaticHandle, grad_rows: torch.Tensor):

@@ -206,6 +206,27 @@ def test_relation_transform_matches_reference(cuda, K, N, aggr, R):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("R", [13, 3])  # 3: multi-chunk relations (atomic partials)
+def test_relation_dw_grad_sink_accumulates(cuda, R):
+    """enable_grad_sink: dW accumulates into the weight's existing .grad (solo chunks add
+    to their slab, shared ones use atomics) and equals grad + the autograd dW."""
+    torch.manual_seed(5)
+    n_dst, n_src, E, K, N = 300, 700, 6000, 128, 128
+    ei = _graph(n_dst, n_src, E, cuda, seed=6, pad=10)
+    rel = torch.randint(0, R, (E,), device=cuda)
+    x = torch.randn(n_src, K, device=cuda) * 0.5
+    W = torch.nn.Parameter(torch.randn(R, N, K, device=cuda) * 0.1)
+    g = torch.randn(n_dst, N, device=cuda)
+    (G.relation_transform(x, rel, W, ei, (n_dst, n_src), "mean") * g).sum().backward()
+    plain = W.grad.clone()
+    base = torch.randn_like(W) * 0.01
+    W.grad = base.clone()
+    G.enable_grad_sink(W)
+    (G.relation_transform(x, rel, W, ei, (n_dst, n_src), "mean") * g).sum().backward()
+    torch.testing.assert_close(W.grad, base + plain, atol=1e-4 * float(plain.abs().max()), rtol=1e-4)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("D,dtype", [(128, torch.bfloat16), (32, torch.float32), (100, torch.float32)])
 def test_sgns_matches_reference(cuda, D, dtype):
     torch.manual_seed(6)

@@ -259,7 +259,7 @@ def _worker_sparse_table_static(rank, world, port, q, wire="fp32"):
         q.put((rank, "error", repr(e)))
 
 
-def _worker_deepwalk_static(rank, world, port, q):
+def _worker_deepwalk_static(rank, world, port, q, mbs=1):
     try:
         _init(rank, world, port)
         from euler_amd.graph.device_graph import DeviceGraph
@@ -267,10 +267,17 @@ def _worker_deepwalk_static(rank, world, port, q):
 
         g = DeviceGraph.synthetic(400, 6.0, 40, seed=3, device="cpu")
         g.manual_seed(11 + rank)
-        tr = DeepWalkTrainer(g, 400, dim=16, batch_size=64, lr=0.05, optimizer="adagrad", seed=5, static=True)
+        tr = DeepWalkTrainer(g, 400, dim=16, batch_size=64, lr=0.05, optimizer="adagrad", seed=5, static=True,
+                             micro_batches=mbs)
         losses = [float(tr.step()) for _ in range(30)]
         tr.table.check_overflow()
-        q.put((rank, "deepwalk_static", bool(sum(losses[-5:]) < sum(losses[:5]))))
+        # the shards together still hold one consistent table: every rank's lookups agree
+        ids = torch.arange(0, 2 * tr.off, 7)
+        rows, _ = tr.table.lookup(ids)
+        allr = [torch.zeros_like(rows) for _ in range(world)]
+        dist.all_gather(allr, rows)
+        same = all(torch.equal(a, allr[0]) for a in allr)
+        q.put((rank, f"deepwalk_static_mb{mbs}", bool(sum(losses[-5:]) < sum(losses[:5]) and same)))
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover
         q.put((rank, "error", repr(e)))
@@ -283,8 +290,9 @@ def test_sharded_table_fixed_capacity_exchange(wire):
     assert len(res) == 2 and all(r[2] for r in res), res
 
 
-def test_deepwalk_static_two_ranks():
-    res = _run(_worker_deepwalk_static)
+@pytest.mark.parametrize("mbs", [1, 2])
+def test_deepwalk_static_two_ranks(mbs):
+    res = _run(_worker_deepwalk_static, mbs)
     assert not [r for r in res if r[1] == "error"], res
     assert len(res) == 2 and all(r[2] for r in res), res
 

@@ -73,6 +73,12 @@ for st in "${S[@]}"; do
     engine_sage)
       run engine_sage 900 python -u benchmarks/bench_engine_sage.py --steps 300 --warmup 20 \
         --native_workers ${ENGINE_WORKERS:-4 8 16} ;;
+    engine_remote)
+      # native pipeline over 2 same-host shard servers: input alone, then with the model step
+      run engine_remote_pipeline 600 python -u benchmarks/bench_engine_sage.py --mode remote --pipeline_only \
+        --native_workers 4 8 16 --steps 200 || exit $?
+      run engine_remote 900 python -u benchmarks/bench_engine_sage.py --mode remote --native_workers 8 16 \
+        --only native_8workers,native_16workers --steps 200 ;;
     engine_prof)
       run engine_sage_cprofile 600 python -u benchmarks/bench_engine_sage.py --steps 200 --warmup 20 \
         --only native_8workers --cprofile gpurun_out/engine_sage_cprofile.txt ;;
@@ -86,6 +92,10 @@ for st in "${S[@]}"; do
       run bench_kg 600 python -u benchmarks/bench_kg.py ;;
     learn_gat)
       run bench_gat 900 python -u benchmarks/bench_gat.py ;;
+    shard_prof)
+      RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29552 \
+        run shard_prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/shard_prof" -o run --output-format csv -- \
+          python3 bench.py --force-dist --shard-features --steps 50 --warmup 5 ;;
     shard_bench)
       # bench.py with the feature table row-sharded: one rank through the all-to-all path
       run bench_shard 600 python -u -m torch.distributed.run --nnodes 1 --nproc-per-node 1 \
@@ -120,6 +130,13 @@ for st in "${S[@]}"; do
             --eval-after "${KG_STEPS:-3000}" || exit $?
         done
       done ;;
+    kg_sweep)
+      # KG_SWEEP="task:layers:lr:margin ..." (3000 training steps each, unnormalised TransE)
+      for c in ${KG_SWEEP:-lattice:0:0.01:10}; do
+        IFS=':' read -r t l lr mg <<< "$c"
+        run "kgs_${t}_l${l}_lr${lr}_m${mg}" 600 python -u benchmarks/bench_kg.py --task $t --layers $l --normalize 0 \
+          --lr $lr --margin $mg --eval-after "${KG_STEPS:-3000}" || exit $?
+      done ;;
     kg_prof)
       run kg_prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/kg_prof" -o run --output-format csv -- \
           python3 benchmarks/bench_kg.py --steps 50 --warmup 5 --eval-after 0 ;;
@@ -140,6 +157,14 @@ for st in "${S[@]}"; do
         run "deepwalk_${m}_dist" 600 python -u -m torch.distributed.run --nnodes 1 --nproc-per-node 1 \
           --master-addr 127.0.0.1 --master-port 29531 benchmarks/bench_deepwalk.py --eval-nodes 0 --mode $m \
           --force-dist || exit $?
+      done ;;
+    deepwalk_overlap)
+      # graph mode: no-comm step vs one-rank all-to-all path with 1 and 2 micro-batches
+      run deepwalk_graph 600 python -u benchmarks/bench_deepwalk.py --eval-nodes 0 --mode graph || exit $?
+      for mb in 1 2; do
+        run "deepwalk_graph_dist_mb$mb" 600 python -u -m torch.distributed.run --nnodes 1 --nproc-per-node 1 \
+          --master-addr 127.0.0.1 --master-port 2953$mb benchmarks/bench_deepwalk.py --eval-nodes 0 --mode graph \
+          --force-dist --micro-batches $mb || exit $?
       done ;;
     deepwalk_prof)
       run deepwalk_prof_local 600 rocprofv3 --kernel-trace --stats -d "$OUT/dw_prof_local" -o run --output-format csv -- \
