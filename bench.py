@@ -63,6 +63,9 @@ def parse_args(argv=None):
                    help="row-shard the feature table over the ranks (row r on rank r %% world); every step's "
                         "sampled rows come over an all-to-all (graph/sharded_features.py). Needs the process "
                         "group: torchrun, or --force-dist with one rank")
+    p.add_argument("--steps-per-graph", type=int, default=4,
+                   help="complete training steps captured per hipGraph (replays amortise the per-launch gap; "
+                        "the timed region still runs exactly --steps steps)")
     p.add_argument("--force-dist", action="store_true",
                    help="take the multi-GPU code path (process group, all-reduce in the step) even with one rank")
     return p.parse_args(argv)
@@ -153,7 +156,7 @@ def main(argv=None):
     if use_graph:
         ok = True
         try:
-            tr.capture(grad_sync)
+            tr.capture(grad_sync, steps=max(1, args.steps_per_graph))
         except RuntimeError as e:  # e.g. a collective the runtime cannot capture
             ok = False
             log(f"rank {rank}: step capture failed ({e}); running eager steps")
@@ -166,14 +169,14 @@ def main(argv=None):
             use_graph = False
 
     if use_graph:
-        def step():
-            tr.replay()
+        def run_steps(n):
+            tr.replay_steps(n)
     else:
-        def step():
-            tr.step(grad_sync)
+        def run_steps(n):
+            for _ in range(n):
+                tr.step(grad_sync)
 
-    for _ in range(args.warmup):
-        step()
+    run_steps(args.warmup)
     torch.cuda.synchronize()
     first_loss = float(tr.loss.item())
 
@@ -181,11 +184,14 @@ def main(argv=None):
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
-    for i in range(args.steps):
-        step()
-        if args.log and rank == 0 and (i + 1) % 50 == 0:
+    done = 0
+    while done < args.steps:
+        n = min(args.steps - done, 48 if args.log else args.steps)
+        run_steps(n)
+        done += n
+        if args.log and rank == 0:
             torch.cuda.synchronize()
-            log(f"step {i+1} loss {float(tr.loss.item()):.4f}")
+            log(f"step {done} loss {float(tr.loss.item()):.4f}")
     torch.cuda.synchronize()
     if dist_on:
         dist.barrier()
@@ -228,6 +234,7 @@ def main(argv=None):
                 "hidden_dim": args.hidden_dim,
                 "label_dim": args.label_dim,
                 "hipgraph": use_graph,
+                "steps_per_graph": args.steps_per_graph if use_graph else None,
                 "feature_sharding": (f"row-sharded over {world} rank(s), per-step all-to-all of the sampled rows"
                                      if fshard is not None else None),
                 "grad_sync": f"rccl all-reduce ({args.grad_reduce_dtype} gradient, {args.grad_buckets} bucket(s)) "
@@ -241,9 +248,7 @@ def main(argv=None):
     if dist_on:
         # a live graph holding captured collectives keeps the communicator busy: drop it first
         torch.cuda.synchronize()
-        if tr._graph_exec is not None:
-            tr._graph_exec.reset()
-            tr._graph_exec = None
+        tr.release_graphs()
         dist.barrier()
         dist.destroy_process_group()
 

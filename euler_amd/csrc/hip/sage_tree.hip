@@ -571,6 +571,10 @@ constexpr int kF2Rows = 64, kF2Threads = 512, kF2Ldt = kF2Rows + 4;
 #ifndef F2_SKIP_PAD
 #define F2_SKIP_PAD 1
 #endif
+// k-steps of weight fragments in flight in the GEMM (2 per wave = 16 VGPRs, 4 = 32)
+#ifndef F2_WPF
+#define F2_WPF 4
+#endif
 
 __device__ __forceinline__ int f2_chunk(int r, int c) { return c ^ (r & 15); }
 
@@ -681,13 +685,14 @@ __global__ __launch_bounds__(kF2Threads, 4) void tr_fwd2_kernel(TrFwdArgs a) {
   }
   // the head's Wc tiles (wave 0, after the gather: its registers are free again)
   if (a.ncomb && wave == 0) tr_comb_wave(a.comb, tb, ntb, lane);
-  // the first two k-steps of this wave's weight fragments load behind the kt pass (not
+  // the first WPF k-steps of this wave's weight fragments load behind the kt pass (not
   // earlier: held through the gather they would push its 20 row loads in flight to spill)
   const bf16_t* W = a.W;
-  uint4_t bq[2][2];
+  constexpr int WPF = F2_WPF;
+  uint4_t bq[WPF][2];
   if (wave * 32 < H) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
+    for (int q = 0; q < WPF; ++q)
 #pragma unroll
       for (int n = 0; n < 2; ++n) bq[q][n] = fm_frag(W, wave * 32 + n * 16, q * 32 < K2 ? q * 32 : 0, K2, lane);
   }
@@ -727,13 +732,13 @@ __global__ __launch_bounds__(kF2Threads, 4) void tr_fwd2_kernel(TrFwdArgs a) {
     if (cb < H) {
       if (cchunk > 0) {
 #pragma unroll
-        for (int q = 0; q < 2; ++q)
+        for (int q = 0; q < WPF; ++q)
 #pragma unroll
           for (int n = 0; n < FN; ++n) bq[q][n] = fm_frag(W, cb + n * 16, q * 32 < K2 ? q * 32 : 0, K2, lane);
       }
-      for (int k0 = 0; k0 < K2; k0 += 64) {
+      for (int k0 = 0; k0 < K2; k0 += 32 * WPF) {
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
+        for (int q = 0; q < WPF; ++q) {
           const int ks = k0 + 32 * q;
           if (ks >= K2) break;  // uniform
           uint4_t av[FM];
@@ -744,7 +749,7 @@ __global__ __launch_bounds__(kF2Threads, 4) void tr_fwd2_kernel(TrFwdArgs a) {
           for (int m = 0; m < FM; ++m)
 #pragma unroll
             for (int n = 0; n < FN; ++n) acc[m][n] = mfma16(av[m], bq[q][n], acc[m][n]);
-          const int kn = ks + 64;
+          const int kn = ks + 32 * WPF;
 #pragma unroll
           for (int n = 0; n < FN; ++n) bq[q][n] = fm_frag(W, cb + n * 16, kn < K2 ? kn : 0, K2, lane);
         }

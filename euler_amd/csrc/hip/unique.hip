@@ -34,11 +34,22 @@ __global__ __launch_bounds__(256) void unique_insert_kernel(const int64_t* __res
   if (i >= n) return;
   const unsigned long long k = static_cast<unsigned long long>(x[i]);
   uint64_t h = fmix64(k) & static_cast<uint64_t>(cap - 1);
-  // cap >= 2n guarantees a free slot; the probe count is bounded by cap
+  // cap >= 2n guarantees a free slot; the probe count is bounded by cap.  Repeated keys
+  // (padding ids, hub nodes: 67K copies of -1 in a sharded-feature exchange) must not
+  // serialise on one address: a plain load finds a present key without a CAS, and the
+  // position atomic is skipped once an earlier occurrence holds the slot (1175 -> ~10 us,
+  // profiles/r3_headline/shard_prof)
+  const volatile unsigned long long* vkeys = keys;
+  const volatile int32_t* vmin = minpos;
   for (int64_t probe = 0; probe < cap; ++probe) {
-    const unsigned long long prev = atomicCAS(keys + h, kUniqEmpty, k);
-    if (prev == kUniqEmpty || prev == k) {
-      atomicMin(minpos + h, static_cast<int32_t>(i));
+    const unsigned long long cur = vkeys[h];
+    bool mine = cur == k;
+    if (!mine && cur == kUniqEmpty) {
+      const unsigned long long prev = atomicCAS(keys + h, kUniqEmpty, k);
+      mine = prev == kUniqEmpty || prev == k;
+    }
+    if (mine) {
+      if (vmin[h] > static_cast<int32_t>(i)) atomicMin(minpos + h, static_cast<int32_t>(i));
       slot[i] = static_cast<int32_t>(h);
       return;
     }

@@ -228,6 +228,10 @@ class DeepWalkTrainer:
             return self.loss
         if self._xstream is None:
             self._xstream = torch.cuda.Stream(device=self.device)
+            # per micro-batch exchange buffers: allocated by the first (eager) step, reused
+            # by every later step and by the capture (collective operands on the comm stream
+            # must not be allocated inside the capture)
+            self._bufs = ({}, {})
         X = self._xstream
         ev = [torch.cuda.Event() for _ in range(6)]
         m0 = self._mb_front(self.batch // 2)
@@ -236,23 +240,23 @@ class DeepWalkTrainer:
         ev[1].record(S)
         with torch.cuda.stream(X):
             X.wait_event(ev[0])
-            r0 = tab.exchange_static(m0["routed"], trash_row=True)
+            r0 = tab.exchange_static(m0["routed"], trash_row=True, bufs=self._bufs[0])
             ev[2].record(X)
             X.wait_event(ev[1])
-            r1 = tab.exchange_static(m1["routed"], trash_row=True)
+            r1 = tab.exchange_static(m1["routed"], trash_row=True, bufs=self._bufs[1])
             ev[3].record(X)
         S.wait_event(ev[2])
         g0, l0, k0 = self._mb_compute(m0, *r0)
         ev[4].record(S)
         with torch.cuda.stream(X):
             X.wait_event(ev[4])
-            tab.apply_static(r0[1], g0)
+            tab.apply_static(r0[1], g0, bufs=self._bufs[0])
         S.wait_event(ev[3])
         g1, l1, k1 = self._mb_compute(m1, *r1)
         ev[5].record(S)
         with torch.cuda.stream(X):
             X.wait_event(ev[5])
-            tab.apply_static(r1[1], g1)
+            tab.apply_static(r1[1], g1, bufs=self._bufs[1])
         S.wait_stream(X)
         # every intermediate stays referenced until the next step: tensors made on one
         # stream and read on the other are never handed back to the allocator mid-step

@@ -75,6 +75,10 @@ def _xavier(shape, gen):
     return (torch.rand(shape, generator=gen, dtype=torch.float64) * 2 - 1).mul_(a).float()
 
 
+# which launch carries the next step's sampler blocks: the head (default) or the optimizer
+_SAMPLE_IN_OPT = os.environ.get("EULER_AMD_SAMPLE_IN", "head") == "opt"
+
+
 class SageTrainer:
     def __init__(self, graph, batch_size, fanouts, dims, label_dim, features=None, labels=None, metapath=None,
                  add_self_loops=False, optimizer="adam", learning_rate=0.01, betas=(0.9, 0.999), eps=1e-8,
@@ -483,11 +487,12 @@ class SageTrainer:
         p = self.plan
         self._prime()
         self._fwd()
-        p.head(None, True)
+        smp_opt = _SAMPLE_IN_OPT and grad_sync is None
+        p.head(None, not smp_opt)
         p.bwd()
         if grad_sync is None:
             p.dw(self._dw_all)
-            p.opt(2)
+            p.opt(2, 1.0, smp_opt)
         elif len(self.grad_buckets()) == 1:
             p.dw(self._dw_all)
             p.opt(0)
@@ -532,10 +537,13 @@ class SageTrainer:
         out += [("dw", lambda: p.dw(self._dw_all)), ("opt", lambda: p.opt(2))]
         return out
 
-    def capture(self, grad_sync=None, warmup: int = 2):
-        """Record one step into a hipGraph (after ``warmup`` eager steps on a side
-        stream); :meth:`replay` then runs it.  ``grad_sync`` is captured too (RCCL
-        collectives are capturable)."""
+    def capture(self, grad_sync=None, warmup: int = 2, steps: int = 1):
+        """Record ``steps`` consecutive training steps into one hipGraph (after ``warmup``
+        eager steps on a side stream); :meth:`replay` then runs it.  ``grad_sync`` is
+        captured too (RCCL collectives are capturable).  ``steps > 1`` amortises the
+        per-replay launch gap (~5 us between back-to-back replays of a ~74 us graph,
+        profiles/r3_headline/) over several complete steps; a 1-step graph is kept as well
+        for step counts that are not a multiple (:meth:`replay_steps`)."""
         if not self.on_gpu:
             return None
         s = torch.cuda.Stream(device=self.device)
@@ -545,17 +553,42 @@ class SageTrainer:
                 self.step(grad_sync)
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self.step(grad_sync)
-        self.step_count -= 1  # the captured step did not run
-        self._graph_exec = g
-        return g
+        self._graphs = {}
+        for k in sorted({1, int(steps)}, reverse=True):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(k):
+                    self.step(grad_sync)
+            self.step_count -= k  # the captured steps did not run
+            self._graphs[k] = g
+        self._graph_steps = int(steps)
+        self._graph_exec = self._graphs[1]
+        return self._graphs[int(steps)]
 
     def replay(self, n: int = 1):
+        """n replays of the 1-step graph"""
         for _ in range(int(n)):
             self._graph_exec.replay()
         self.step_count += int(n)
+
+    def replay_steps(self, n: int):
+        """exactly n training steps: the multi-step graph as often as it fits, then the
+        1-step graph for the rest"""
+        k = getattr(self, "_graph_steps", 1)
+        big, rest = divmod(int(n), k)
+        for _ in range(big):
+            self._graphs[k].replay()
+        for _ in range(rest):
+            self._graph_exec.replay()
+        self.step_count += int(n)
+
+    def release_graphs(self):
+        """drop the captured graphs (before destroying a process group whose collectives
+        they recorded)"""
+        for g in getattr(self, "_graphs", {}).values():
+            g.reset()
+        self._graphs = {}
+        self._graph_exec = None
 
     def set_grad_sync_dtype(self, dtype):
         """Data parallel: the gradient handed to ``grad_sync`` as fp32 (default) or bf16

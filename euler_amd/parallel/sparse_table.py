@@ -131,24 +131,27 @@ class ShardedTable:
         ids = ids.reshape(-1).long()
         return route_by_owner(ids, self.world, self.capacity(ids.numel()), self.overflow)
 
-    def exchange_static(self, routed, trash_row: bool = False):
-        """second half of :meth:`lookup_static`: the id and row all-to-alls of routed ids"""
+    def exchange_static(self, routed, trash_row: bool = False, bufs=None):
+        """second half of :meth:`lookup_static`: the id and row all-to-alls of routed ids
+        (``bufs``: persistent buffers for the collectives, see :meth:`_buf`)"""
         pos, send = routed
         W = self.world
         trash = send.numel() - 1
-        recv = torch.empty(trash, dtype=torch.long, device=send.device)
-        dist.all_to_all_single(recv, send[:trash], group=self.group)
+        sd = self._buf(bufs, "send", (trash,), torch.long, send.device)
+        sd.copy_(send[:trash])
+        recv = self._buf(bufs, "recv", (trash,), torch.long, send.device)
+        dist.all_to_all_single(recv, sd, group=self.group)
         local = torch.where(recv >= 0, torch.div(recv, W, rounding_mode="floor"), torch.full_like(recv, -1))
-        out = self._a2a_rows(self._gather(local), extra=1 if trash_row else 0)
+        out = self._a2a_rows(self._gather(local), extra=1 if trash_row else 0, bufs=bufs, tag="rows_")
         return out, StaticHandle(pos, local)
 
-    def apply_static(self, handle: StaticHandle, grad_rows: torch.Tensor):
+    def apply_static(self, handle: StaticHandle, grad_rows: torch.Tensor, bufs=None):
         """row-sparse update from gradients [W*C, D] in slot order (rows of empty slots
         are ignored)."""
         g = grad_rows.float().contiguous()
         rows = handle.local
         if self.comm:
-            g = self._a2a_rows(g)
+            g = self._a2a_rows(g, bufs=bufs, tag="grad_")
             if self.world > 1:
                 # several ranks may have asked for the same row: merge (the -1 bucket of
                 # empty slots collects their rows and is skipped by the update)
@@ -203,12 +206,25 @@ class ShardedTable:
         out[order] = out_sorted
         return out, LookupHandle(order, send, recv, local, ids.numel())
 
-    def _a2a_rows(self, x, out_splits=None, in_splits=None, extra=0):
+    @staticmethod
+    def _buf(bufs, name, shape, dtype, device):
+        """persistent exchange buffer ``name`` of ``bufs`` (None: a fresh tensor).  Buffers
+        that collectives read or write on a side stream of a captured graph must outlive
+        the capture (allocated by the first eager step, reused by the capture)."""
+        if bufs is None:
+            return torch.empty(shape, dtype=dtype, device=device)
+        t = bufs.get(name)
+        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
+            t = bufs[name] = torch.empty(shape, dtype=dtype, device=device)
+        return t
+
+    def _a2a_rows(self, x, out_splits=None, in_splits=None, extra=0, bufs=None, tag=""):
         """all-to-all of [*, D] rows in the wire dtype; returns fp32 rows (plus ``extra``
         zero rows at the end)"""
-        xw = x.to(self.wire).contiguous()
+        xw = self._buf(bufs, tag + "in", (x.shape[0], self.dim), self.wire, x.device)
+        xw.copy_(x)
         n = xw.shape[0] if out_splits is None else sum(out_splits)
-        out = torch.empty(n + extra, self.dim, dtype=self.wire, device=xw.device)
+        out = self._buf(bufs, tag + "out", (n + extra, self.dim), self.wire, xw.device)
         if extra:
             out[n:].zero_()
         dist.all_to_all_single(out[:n], xw, out_splits, in_splits, group=self.group)

@@ -44,6 +44,8 @@ for st in "${S[@]}"; do
         EULER_AMD_DW_ROUTE_WG=$wg run "tree_kernels_rwg$wg" 300 python -u tools/tree_kernels.py
       done
       EULER_AMD_TREE_FORK=0 run tree_kernels_nofork 300 python -u tools/tree_kernels.py ;;
+    sweep_sample)
+      EULER_AMD_SAMPLE_IN=opt run tree_kernels_sample_opt 300 python -u tools/tree_kernels.py ;;
     sweep_fwd)
       for bm in 32 64 128; do
         EULER_AMD_FWD_BM=$bm run "tree_kernels_fbm$bm" 300 python -u tools/tree_kernels.py
@@ -158,6 +160,11 @@ for st in "${S[@]}"; do
           --master-addr 127.0.0.1 --master-port 29531 benchmarks/bench_deepwalk.py --eval-nodes 0 --mode $m \
           --force-dist || exit $?
       done ;;
+    dw_probe)
+      RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29561 \
+        run dw_probe_eager 120 python -u -X faulthandler tools/dw_overlap_probe.py eager || exit $?
+      RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29562 \
+        run dw_probe_graph 120 python -u -X faulthandler tools/dw_overlap_probe.py graph ;;
     deepwalk_overlap)
       # graph mode: no-comm step vs one-rank all-to-all path with 1 and 2 micro-batches
       run deepwalk_graph 600 python -u benchmarks/bench_deepwalk.py --eval-nodes 0 --mode graph || exit $?

@@ -59,8 +59,9 @@ def main():
     for i in range(p.num_problems()):
         res[f"dw[{i}]"] = round(timeit(lambda: p.dw([i]), args.reps), 2)
     res["dw_splits"] = p.splits()
-    tr.capture()
+    tr.capture(steps=4)
     res["graph_step"] = round(timeit(lambda: tr.replay(1), args.reps), 2)
+    res["graph_step_x4"] = round(timeit(lambda: tr.replay_steps(4), args.reps) / 4, 2)  # per step
     print(json.dumps(res))
     if hasattr(p, "head"):
         rows = torch.ops  # noqa: F841
