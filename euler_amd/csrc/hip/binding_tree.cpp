@@ -84,14 +84,17 @@ class TreePlan {
     ok(eh_tr_sample(&sample_, stream()), "tr_sample");
   }
 
-  void fwd(c10::optional<torch::Tensor> prof) {
+  // gemm_only (pipelined step): layer 0 from the A rows the previous optimizer launch's
+  // gather blocks wrote (opt(..., with_gather=True))
+  void fwd(c10::optional<torch::Tensor> prof, bool gemm_only) {
     const c10::DeviceGuard g(dev_);
+    TORCH_CHECK(!gemm_only || pipeline_ok(), "TreePlan: no pipelined forward for this plan");
     TrFwdArgs a0 = fwd0_;
     if (prof.has_value()) {
-      need(*prof, torch::kInt64, (fwd0_.M / bm0_) * 8, "prof");
+      need(*prof, torch::kInt64, (fwd0_.M / (gemm_only ? 64 : bm0_)) * 8, "prof");
       a0.prof = reinterpret_cast<long long*>(prof->data_ptr<int64_t>());
     }
-    ok(eh_tr_fwd(&a0, L_ == 1 ? 1 : 0, feat_fp32_, bm0_, stream()), "tr_fwd");
+    ok(eh_tr_fwd(&a0, gemm_only ? 3 : (L_ == 1 ? 1 : 0), feat_fp32_, bm0_, stream()), "tr_fwd");
     if (L_ == 3) ok(eh_tr_fwd(&fwd1_, 2, 0, bm1_, stream()), "tr_fwd(inner)");
   }
 
@@ -143,12 +146,38 @@ class TreePlan {
 
   // mode 0 reduce, 1 optimizer, 2 fused, 3 shadows only
   // with_sample: modes 1/2 also draw the next step's batch (extra blocks of the launch)
-  void opt(int64_t mode, double grad_scale, bool with_sample) {
+  // with_gather: extra blocks gather the NEXT step's layer-0 inputs (the tree the head's
+  // sampler drew) into A0_kt and A0_rows, so that step's forward is GEMM-only
+  void opt(int64_t mode, double grad_scale, bool with_sample, bool with_gather) {
     const c10::DeviceGuard g(dev_);
+    TORCH_CHECK(!with_gather || pipeline_ok(), "TreePlan: no pipelined gather for this plan");
     TrOptArgs a = opt_;
     a.grad_scale = static_cast<float>(grad_scale);
     if (!with_sample) a.nsample = 0;
+    if (with_gather) {
+      a.gat = fwd0_;
+      a.ngather = static_cast<int32_t>(fwd0_.M / 32);
+      a.gat_fp32 = feat_fp32_;
+      static const int first = [] {
+        const char* e = std::getenv("EULER_AMD_GATHER_FIRST");
+        return e ? std::atoi(e) : 1;
+      }();
+      a.gather_first = first;
+      static const int tpb = [] {
+        const char* e = std::getenv("EULER_AMD_OPT_TPB");
+        return e ? std::atoi(e) : 4;
+      }();
+      a.opt_tpb = tpb;
+    }
     ok(eh_tr_opt(&a, static_cast<int>(mode), stream()), "tr_opt");
+  }
+
+  // the pipelined step applies: 2 hops, the 64-row layer-0 kernel, A0_rows given, sibling
+  // groups of at most 32 rows (one gather tile)
+  bool pipeline_ok() const {
+    return L_ == 2 && fwd0_.a_rows != nullptr && !cached_ && bm0_ <= 64 && logP_[1] <= 5 && D_ % 64 == 0 &&
+           fwd0_.M % 64 == 0 && dims_[0] <= 256 &&
+           eh_tr_gather32_lds(static_cast<int>(D_), static_cast<int>(fwd0_.FL)) <= 64 * 1024;
   }
 
   // split-K reduce (mode 0) of a subset of the flat segments (data-parallel buckets);
@@ -199,6 +228,7 @@ class TreePlan {
   py::dict d_;
   int L_, B_, D_, E_, C_, C_real_, self_;
   int feat_fp32_ = 0, bm0_ = 32, bm1_ = 32;
+  bool cached_ = false;
   std::vector<int64_t> F_, logP_, masks_, dims_, M_;
   c10::Device dev_{c10::kCPU};
   TrGraph graph_{};
@@ -307,6 +337,7 @@ class TreePlan {
     a.FL = sm.FL;
     a.include_self = self_;
     a.inv_leaf = 1.f / static_cast<float>(a.FL + self_);
+    cached_ = cached;
     a.nodes = cached ? i32("fwd_nodes", M) : sm.nodes;
     a.leaf = cached ? i32("fwd_leaf", M * sm.FL) : sm.leaf;
     a.roots_in = sm.roots;
@@ -328,6 +359,7 @@ class TreePlan {
     a.Fg = static_cast<int32_t>(F_[lv]);
     a.inv_grp = 1.f / static_cast<float>(a.Fg + self_);
     a.a_next = bf("A1", M_[lv - 1] * 2 * dims_[0]);
+    a.a_rows = has("A0_rows") ? bf("A0_rows", M * 2 * D_) : nullptr;
     bm0_ = (1 << a.logPg) > 32 ? (1 << a.logPg) : 32;
     if (has("fwd_bm")) bm0_ = std::max<int>(bm0_, static_cast<int>(geti("fwd_bm")));
     TORCH_CHECK(bm0_ == 32 || bm0_ == 64 || bm0_ == 128, "TreePlan: fwd rows per block must be 32, 64 or 128");
@@ -811,12 +843,14 @@ void register_tree_ops(py::module& m) {
   py::class_<TreePlan>(m, "TreePlan")
       .def(py::init<py::dict>())
       .def("sample", &TreePlan::sample)
-      .def("fwd", &TreePlan::fwd, py::arg("prof") = py::none())
+      .def("fwd", &TreePlan::fwd, py::arg("prof") = py::none(), py::arg("gemm_only") = false)
       .def("fwd_blocks", [](const TreePlan& t) { return t.fwd_blocks(); })
       .def("head", &TreePlan::head, py::arg("prof") = py::none(), py::arg("with_sample") = false)
       .def("bwd", &TreePlan::bwd)
       .def("dw", &TreePlan::dw)
-      .def("opt", &TreePlan::opt, py::arg("mode"), py::arg("grad_scale") = 1.0, py::arg("with_sample") = false)
+      .def("opt", &TreePlan::opt, py::arg("mode"), py::arg("grad_scale") = 1.0, py::arg("with_sample") = false,
+           py::arg("with_gather") = false)
+      .def("pipeline_ok", &TreePlan::pipeline_ok)
       .def("opt_segments", &TreePlan::opt_segments, py::arg("mode"), py::arg("segs"), py::arg("head_stats"))
       .def("set_lr", &TreePlan::set_lr)
       .def("set_grad16", &TreePlan::set_grad16, py::arg("g16"))

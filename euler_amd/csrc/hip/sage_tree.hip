@@ -578,7 +578,139 @@ constexpr int kF2Rows = 64, kF2Threads = 512, kF2Ldt = kF2Rows + 4;
 
 __device__ __forceinline__ int f2_chunk(int r, int c) { return c ^ (r & 15); }
 
+// gather + mean of BM target rows into the swizzled LDS tile At [BM][2D] (see tr_fwd2):
+// item = (used row, 8-column chunk), two items per thread, every leaf load of both in
+// flight; padding ids (-1) read row 0 and are zeroed at use; only the Fg + 1 used slots of
+// each sibling group are gathered (F2_SKIP_PAD), the unused slots' rows are zero-filled.
+template <typename FT, int BM, int NT>
+__device__ __forceinline__ void f2_gather(const TrFwdArgs& a, bf16_t* At, const int32_t* node_s,
+                                          const int32_t* leaf_s, int tid) {
+  const int D = a.D, K2 = 2 * D;
+  const FT* x = static_cast<const FT*>(a.x);
+  const int cpr = D >> 3;
+  const int P = 1 << a.logPg, U = F2_SKIP_PAD ? a.Fg + 1 : P;
+  const int nitems = (BM >> a.logPg) * U * cpr;
+  constexpr int G = Feat8<FT>::kInFlight;
+  if (F2_SKIP_PAD && U < P) {
+    const int pad = P - U, nch = K2 >> 3;
+    for (int it = tid; it < (BM >> a.logPg) * pad * nch; it += NT) {
+      const int q = it / nch, c = it - q * nch;
+      const int r = (q / pad) * P + U + q % pad;
+      *reinterpret_cast<uint4_t*>(At + r * K2 + f2_chunk(r, c) * 8) = uint4_t{0u, 0u, 0u, 0u};
+    }
+  }
+  for (int it = tid; it < nitems; it += 2 * NT) {
+    const int itb = it + NT;
+    const bool hb = itb < nitems;
+    const int qa = it / cpr, ca = it - qa * cpr;
+    const int qb = hb ? itb / cpr : qa, cb = hb ? itb - qb * cpr : ca;
+    const int ra = (qa / U) * P + qa % U, rb = (qb / U) * P + qb % U;
+    const int32_t na = node_s[ra], nb = hb ? node_s[rb] : -1;
+    Feat8<FT> sa, sb;
+    float acc_a[8], acc_b[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc_a[i] = acc_b[i] = 0.f;
+    sa.load(x + static_cast<int64_t>(na > 0 ? na : 0) * D + ca * 8);
+    sb.load(x + static_cast<int64_t>(nb > 0 ? nb : 0) * D + cb * 8);
+    for (int k = 0; k < a.FL; k += G) {
+      int32_t ja[G], jb[G];
+      Feat8<FT> va[G], vb[G];
+#pragma unroll
+      for (int u = 0; u < G; ++u) {
+        ja[u] = (k + u < a.FL) ? leaf_s[ra * a.FL + k + u] : -1;
+        jb[u] = (hb && k + u < a.FL) ? leaf_s[rb * a.FL + k + u] : -1;
+      }
+#pragma unroll
+      for (int u = 0; u < G; ++u) {
+        va[u].load(x + static_cast<int64_t>(ja[u] > 0 ? ja[u] : 0) * D + ca * 8);
+        vb[u].load(x + static_cast<int64_t>(jb[u] > 0 ? jb[u] : 0) * D + cb * 8);
+      }
+#pragma unroll
+      for (int u = 0; u < G; ++u) {
+        va[u].keep(ja[u] >= 0);
+        vb[u].keep(jb[u] >= 0);
+        va[u].add_to(acc_a);
+        vb[u].add_to(acc_b);
+      }
+    }
+    sa.keep(na >= 0);
+    sb.keep(nb >= 0);
+    if (a.include_self) {
+      sa.add_to(acc_a);
+      sb.add_to(acc_b);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      acc_a[i] *= a.inv_leaf;
+      acc_b[i] *= a.inv_leaf;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1 && !hb) break;
+      const int r = h ? rb : ra, c = h ? cb : ca;
+      *reinterpret_cast<uint4_t*>(At + r * K2 + f2_chunk(r, c) * 8) = h ? sb.bf16() : sa.bf16();
+      *reinterpret_cast<uint4_t*>(At + r * K2 + f2_chunk(r, cpr + c) * 8) = pack_bf16x8(h ? acc_b : acc_a);
+    }
+  }
+}
+
+// the A tile -> kt layout (dW operand): item = (column pair, 8-row chunk), column pairs
+// fastest: a half-wave's 4-byte reads cover 128 contiguous (permuted) bytes of a row
+template <int BM, int NT>
+__device__ __forceinline__ void f2_kt(const TrFwdArgs& a, int64_t row0, const bf16_t* At, int tid) {
+  const int K2 = 2 * a.D;
+  const int np = K2 >> 1;
+  for (int it = tid; it < np * (BM / 8); it += NT) {
+    const int q = it / np;
+    const int n = (it - q * np) * 2;
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = q * 8 + i;
+      w[i] = *reinterpret_cast<const uint32_t*>(At + r * K2 + f2_chunk(r, n >> 3) * 8 + (n & 7));
+    }
+    uint4_t lo, hi;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      lo[i] = (w[2 * i] & 0xffffu) | (w[2 * i + 1] << 16);
+      hi[i] = (w[2 * i] >> 16) | (w[2 * i + 1] & 0xffff0000u);
+    }
+    *reinterpret_cast<uint4_t*>(a.a_kt + kt_off(row0 + q * 8, n, K2)) = lo;
+    *reinterpret_cast<uint4_t*>(a.a_kt + kt_off(row0 + q * 8, n + 1, K2)) = hi;
+  }
+}
+
+// one 32-row gather tile of the pipelined step (extra blocks of the optimizer launch, 256
+// threads): ids -> gather + mean -> LDS -> kt copy (dW operand) + row-major A rows (the
+// GEMM-only forward's input).  LDS: A tile [32][2D] + ids (eh_tr_gather32_lds).
+constexpr int kG32Rows = 32, kG32Threads = 256;
+
 template <typename FT>
+__device__ __forceinline__ void tr_gather32_tile(const TrFwdArgs& a, int tile, bf16_t* lds) {
+  constexpr int BM = kG32Rows, NT = kG32Threads;
+  const int K2 = 2 * a.D, tid = threadIdx.x;
+  const int64_t row0 = static_cast<int64_t>(tile) * BM;
+  bf16_t* At = lds;
+  int32_t* node_s = reinterpret_cast<int32_t*>(lds + BM * K2);
+  int32_t* leaf_s = node_s + BM;
+  if (tid < BM) node_s[tid] = a.nodes[row0 + tid];
+  for (int it = tid; it < BM * a.FL; it += NT) leaf_s[it] = a.leaf[row0 * a.FL + it];
+  __syncthreads();
+  f2_gather<FT, BM, NT>(a, At, node_s, leaf_s, tid);
+  __syncthreads();
+  f2_kt<BM, NT>(a, row0, At, tid);
+  const int cpr2 = K2 >> 3;
+  for (int it = tid; it < BM * cpr2; it += NT) {
+    const int r = it / cpr2, c = it - r * cpr2;
+    *reinterpret_cast<uint4_t*>(a.a_rows + (row0 + r) * K2 + c * 8) =
+        *reinterpret_cast<const uint4_t*>(At + r * K2 + f2_chunk(r, c) * 8);
+  }
+}
+
+// GO = 1 (pipelined step, mode 3): the gather already ran in the previous launch (gather
+// blocks of tr_opt, tr_gather32_tile): the A tile is loaded from a.a_rows and the kt copy
+// for dW exists; only the GEMM, the tree mean, the ReLU bits and the head's Wc remain.
+template <typename FT, int GO>
 __global__ __launch_bounds__(kF2Threads, 4) void tr_fwd2_kernel(TrFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   constexpr int BM = kF2Rows, NT = kF2Threads;
@@ -607,82 +739,25 @@ __global__ __launch_bounds__(kF2Threads, 4) void tr_fwd2_kernel(TrFwdArgs a) {
     a.rng[1] += 1;  // this batch is consumed: the sampler draws the next counter
   }
   for (int i = tb * NT + tid; i < a.B; i += ntb * NT) a.roots_cur[i] = a.roots_in[i];
-  if (tid < BM) node_s[tid] = a.nodes[row0 + tid];
-  for (int it = tid; it < BM * a.FL; it += NT) leaf_s[it] = a.leaf[row0 * a.FL + it];
-  __syncthreads();
+  if constexpr (GO) {
+    // A rows [64][K2] (row-major, 16-byte chunks) -> the swizzled LDS tile
+    const int cpr2 = K2 >> 3;
+    for (int it = tid; it < BM * cpr2; it += NT) {
+      const int r = it / cpr2, c = it - r * cpr2;
+      *reinterpret_cast<uint4_t*>(At + r * K2 + f2_chunk(r, c) * 8) =
+          *reinterpret_cast<const uint4_t*>(a.a_rows + (row0 + r) * K2 + c * 8);
+    }
+  } else {
+    if (tid < BM) node_s[tid] = a.nodes[row0 + tid];
+    for (int it = tid; it < BM * a.FL; it += NT) leaf_s[it] = a.leaf[row0 * a.FL + it];
+    __syncthreads();
+  }
   F2_STAMP(1);
   // ---- gather + mean: item = (used row, 8-column chunk); two items per thread, every leaf
   // load of both in flight; padding ids (-1) read row 0 and are zeroed at use.  Only the
   // Fg + 1 used slots of each sibling group are items (F2_SKIP_PAD; at fanout 25, 26 of
   // every 32 rows): the unused slots' A rows are zero-filled instead of gathered.
-  {
-    const FT* x = static_cast<const FT*>(a.x);
-    const int cpr = D >> 3;
-    const int P = 1 << a.logPg, U = F2_SKIP_PAD ? a.Fg + 1 : P;
-    const int nitems = (BM >> a.logPg) * U * cpr;
-    constexpr int G = Feat8<FT>::kInFlight;
-    if (F2_SKIP_PAD && U < P) {
-      const int pad = P - U, nch = K2 >> 3;
-      for (int it = tid; it < (BM >> a.logPg) * pad * nch; it += NT) {
-        const int q = it / nch, c = it - q * nch;
-        const int r = (q / pad) * P + U + q % pad;
-        *reinterpret_cast<uint4_t*>(At + r * K2 + f2_chunk(r, c) * 8) = uint4_t{0u, 0u, 0u, 0u};
-      }
-    }
-    for (int it = tid; it < nitems; it += 2 * NT) {
-      const int itb = it + NT;
-      const bool hb = itb < nitems;
-      const int qa = it / cpr, ca = it - qa * cpr;
-      const int qb = hb ? itb / cpr : qa, cb = hb ? itb - qb * cpr : ca;
-      const int ra = (qa / U) * P + qa % U, rb = (qb / U) * P + qb % U;
-      const int32_t na = node_s[ra], nb = hb ? node_s[rb] : -1;
-      Feat8<FT> sa, sb;
-      float acc_a[8], acc_b[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) acc_a[i] = acc_b[i] = 0.f;
-      sa.load(x + static_cast<int64_t>(na > 0 ? na : 0) * D + ca * 8);
-      sb.load(x + static_cast<int64_t>(nb > 0 ? nb : 0) * D + cb * 8);
-      for (int k = 0; k < a.FL; k += G) {
-        int32_t ja[G], jb[G];
-        Feat8<FT> va[G], vb[G];
-#pragma unroll
-        for (int u = 0; u < G; ++u) {
-          ja[u] = (k + u < a.FL) ? leaf_s[ra * a.FL + k + u] : -1;
-          jb[u] = (hb && k + u < a.FL) ? leaf_s[rb * a.FL + k + u] : -1;
-        }
-#pragma unroll
-        for (int u = 0; u < G; ++u) {
-          va[u].load(x + static_cast<int64_t>(ja[u] > 0 ? ja[u] : 0) * D + ca * 8);
-          vb[u].load(x + static_cast<int64_t>(jb[u] > 0 ? jb[u] : 0) * D + cb * 8);
-        }
-#pragma unroll
-        for (int u = 0; u < G; ++u) {
-          va[u].keep(ja[u] >= 0);
-          vb[u].keep(jb[u] >= 0);
-          va[u].add_to(acc_a);
-          vb[u].add_to(acc_b);
-        }
-      }
-      sa.keep(na >= 0);
-      sb.keep(nb >= 0);
-      if (a.include_self) {
-        sa.add_to(acc_a);
-        sb.add_to(acc_b);
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        acc_a[i] *= a.inv_leaf;
-        acc_b[i] *= a.inv_leaf;
-      }
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if (h == 1 && !hb) break;
-        const int r = h ? rb : ra, c = h ? cb : ca;
-        *reinterpret_cast<uint4_t*>(At + r * K2 + f2_chunk(r, c) * 8) = h ? sb.bf16() : sa.bf16();
-        *reinterpret_cast<uint4_t*>(At + r * K2 + f2_chunk(r, cpr + c) * 8) = pack_bf16x8(h ? acc_b : acc_a);
-      }
-    }
-  }
+  if constexpr (!GO) f2_gather<FT, BM, NT>(a, At, node_s, leaf_s, tid);
   // the head's Wc tiles (wave 0, after the gather: its registers are free again)
   if (a.ncomb && wave == 0) tr_comb_wave(a.comb, tb, ntb, lane);
   // the first WPF k-steps of this wave's weight fragments load behind the kt pass (not
@@ -700,27 +775,7 @@ __global__ __launch_bounds__(kF2Threads, 4) void tr_fwd2_kernel(TrFwdArgs a) {
   F2_STAMP(2);
   // ---- A tile -> kt layout (dW operand): item = (column pair, 8-row chunk), column pairs
   // fastest: a half-wave's 4-byte reads cover 128 contiguous (permuted) bytes of a row
-  {
-    const int np = K2 >> 1;
-    for (int it = tid; it < np * (BM / 8); it += NT) {
-      const int q = it / np;
-      const int n = (it - q * np) * 2;
-      uint32_t w[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int r = q * 8 + i;
-        w[i] = *reinterpret_cast<const uint32_t*>(At + r * K2 + f2_chunk(r, n >> 3) * 8 + (n & 7));
-      }
-      uint4_t lo, hi;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        lo[i] = (w[2 * i] & 0xffffu) | (w[2 * i + 1] << 16);
-        hi[i] = (w[2 * i] >> 16) | (w[2 * i + 1] & 0xffff0000u);
-      }
-      *reinterpret_cast<uint4_t*>(a.a_kt + kt_off(row0 + q * 8, n, K2)) = lo;
-      *reinterpret_cast<uint4_t*>(a.a_kt + kt_off(row0 + q * 8, n + 1, K2)) = hi;
-    }
-  }
+  if constexpr (!GO) f2_kt<BM, NT>(a, row0, At, tid);
   F2_STAMP(3);
   // ---- MFMA GEMM out of LDS: wave w owns columns w*32..+31 of each 256-column chunk, all
   // 64 rows; two k-steps of weight fragments in flight
@@ -1437,15 +1492,13 @@ __global__ __launch_bounds__(256, 2) void tr_dw_all_kernel(TrDwLaunch a) {
 // tr_opt: split-K reduce and/or the optimizer over the flat fp32 parameters, the bf16
 // weight shadows, loss hand-off and the RNG counter advance (hipGraph-replay safe)
 // ----------------------------------------------------------------------------
+// GATHER: the launch also carries the next step's layer-0 gather tiles (pipelined step);
+// a separate instantiation so the plain optimizer keeps its small register footprint
+// one 8 x 32 (or 256-element) tile of the optimizer launch: split-K reduce and / or the
+// update, the bf16 shadows of weight tiles; block 0 also reduces the head statistics
 template <int MODE>
-__global__ __launch_bounds__(256) void tr_opt_kernel(TrOptArgs a) {
-  __shared__ float tile_s[8][33];
-  __shared__ int32_t node_s[kTrSampleRows];
-  const int b = blockIdx.x, tid = threadIdx.x;
-  if (b >= a.nblk) {  // the next step's sampler (modes 1/2)
-    tr_sample_block<256>(a.smp, b - a.nblk, node_s);
-    return;
-  }
+__device__ __forceinline__ void tr_opt_tile(const TrOptArgs& a, int b, float (*tile_s)[33]) {
+  const int tid = threadIdx.x;
   if (b == 0 && tid < 64 && MODE != 3 && a.nhead > 0) {
     // head statistics: reduce (modes 0/2) the per-block partials; hand the loss over (1/2);
     // nhead == 0: a segment-subset reduce launch that leaves them to another launch
@@ -1564,6 +1617,42 @@ __global__ __launch_bounds__(256) void tr_opt_kernel(TrOptArgs a) {
   }
 }
 
+template <int MODE, typename FT, int GATHER>
+__global__ __launch_bounds__(256, GATHER ? 4 : 1) void tr_opt_kernel(TrOptArgs a) {
+  __shared__ float tile_s[8][33];
+  __shared__ int32_t node_s[kTrSampleRows];
+  extern __shared__ __attribute__((aligned(16))) bf16_t glds[];  // gather tiles only
+  int b = blockIdx.x;
+  // GATHER launches: opt_tpb parameter tiles per block, so the parameter blocks take few of
+  // the slots the gather tiles need
+  const int tpb = GATHER && a.opt_tpb > 1 ? a.opt_tpb : 1;
+  const int nopt = (a.nblk + tpb - 1) / tpb;
+  if constexpr (GATHER) {
+    // the next step's layer-0 gather (pipelined step): first in the grid unless
+    // gather_first == 0
+    if (a.gather_first) {
+      if (b < a.ngather) {
+        tr_gather32_tile<FT>(a.gat, b, glds);
+        return;
+      }
+      b -= a.ngather;
+    } else if (b >= nopt + a.nsample) {
+      tr_gather32_tile<FT>(a.gat, b - nopt - a.nsample, glds);
+      return;
+    }
+  }
+  if (b >= nopt) {  // the next step's sampler (modes 1/2)
+    tr_sample_block<256>(a.smp, b - nopt, node_s);
+    return;
+  }
+  for (int r = 0; r < tpb; ++r) {
+    const int bt = b * tpb + r;
+    if (bt >= a.nblk) break;  // uniform across the block
+    tr_opt_tile<MODE>(a, bt, tile_s);
+    if (tpb > 1) __syncthreads();  // tile_s is reused by the next tile
+  }
+}
+
 }  // namespace euler_hip
 
 using namespace euler_hip;
@@ -1622,15 +1711,24 @@ hipError_t eh_tr_fwd(const TrFwdArgs* a, int mode, int feat_fp32, int bm, hipStr
                                         !a->comb.WcT || !a->comb.bc || !a->comb.wout_sh || !a->comb.wfcT_sh ||
                                         a->comb.C % 16 != 0 || a->comb.H % 16 != 0 || a->comb.E % 32 != 0)))
     return hipErrorInvalidValue;
+  if (mode == 3) {  // GEMM-only (pipelined step): the A rows come from the gather blocks
+    if (!fwd2_fits(*a) || !a->a_rows) return hipErrorInvalidValue;
+    const size_t l2 = eh_tr_fwd2_lds(a->D, a->FL);
+    EULER_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(tr_fwd2_kernel<bf16_t, 1>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(l2)));
+    hipLaunchKernelGGL((tr_fwd2_kernel<bf16_t, 1>), dim3(static_cast<uint32_t>(a->M / kF2Rows)), dim3(kF2Threads), l2,
+                       s, *a);
+    return hipGetLastError();
+  }
   if (mode == 0 && fwd2_fits(*a)) {
     const size_t l2 = eh_tr_fwd2_lds(a->D, a->FL);
     const dim3 g2(static_cast<uint32_t>(a->M / kF2Rows));
-#define TR_FWD2(FT)                                                                                        \
-  do {                                                                                                     \
-    EULER_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(tr_fwd2_kernel<FT>),                \
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(l2))); \
-    hipLaunchKernelGGL((tr_fwd2_kernel<FT>), g2, dim3(kF2Threads), l2, s, *a);                             \
-    return hipGetLastError();                                                                              \
+#define TR_FWD2(FT)                                                                                          \
+  do {                                                                                                       \
+    EULER_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(tr_fwd2_kernel<FT, 0>),               \
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(l2)));   \
+    hipLaunchKernelGGL((tr_fwd2_kernel<FT, 0>), g2, dim3(kF2Threads), l2, s, *a);                            \
+    return hipGetLastError();                                                                                \
   } while (0)
     if (feat_fp32) TR_FWD2(float);
     TR_FWD2(bf16_t);
@@ -1740,7 +1838,15 @@ hipError_t eh_tr_dw(TrDwLaunch* L, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t eh_tr_opt(const TrOptArgs* a, int mode, hipStream_t s) {
+size_t eh_tr_gather32_lds(int D, int FL) {
+  return static_cast<size_t>(kG32Rows) * 2 * D * sizeof(bf16_t) + static_cast<size_t>(kG32Rows) * (1 + FL) * sizeof(int32_t);
+}
+
+hipError_t eh_tr_opt(const TrOptArgs* ain, int mode, hipStream_t s) {
+  TrOptArgs A = *ain;
+  const TrOptArgs* a = &A;
+  if (!(mode == 1 || mode == 2)) A.nsample = 0;  // the sampler runs in modes 1/2 only
+  if (mode == 3) A.ngather = 0;
   if (a->nseg < 1 || a->nseg > kTrMaxSegs || a->nblk < 1) return hipErrorInvalidValue;
   if (!a->p || !a->g || !a->m || !a->v || !a->step || !a->loss_acc || !a->loss_out || !a->head_part ||
       a->nhead < 0 || (a->nhead == 0 && mode != 0 && mode != 3))
@@ -1760,19 +1866,48 @@ hipError_t eh_tr_opt(const TrOptArgs* a, int mode, hipStream_t s) {
   }
   if (blk != a->nblk) return hipErrorInvalidValue;
   int extra = 0;
-  if ((mode == 1 || mode == 2) && a->nsample > 0) {
+  if (a->nsample > 0) {
     const TrSampleArgs& m = a->smp;
     if (!m.g.indptr || !m.g.nbr || !m.g.cumw || !m.g.prob || !m.g.alias || !m.tr.rng || !m.roots || !m.nodes ||
         !m.leaf || m.FL < 1 || m.lv < 0 || m.lv > 2 || a->nsample != ceil_div(m.M, kTrSampleRows))
       return hipErrorInvalidValue;
     extra = a->nsample;
   }
-  const dim3 grid(static_cast<uint32_t>(a->nblk + extra));
-  if (mode == 0) hipLaunchKernelGGL(tr_opt_kernel<0>, grid, dim3(256), 0, s, *a);
-  else if (mode == 1) hipLaunchKernelGGL(tr_opt_kernel<1>, grid, dim3(256), 0, s, *a);
-  else if (mode == 2) hipLaunchKernelGGL(tr_opt_kernel<2>, grid, dim3(256), 0, s, *a);
-  else if (mode == 3) hipLaunchKernelGGL(tr_opt_kernel<3>, grid, dim3(256), 0, s, *a);
-  else return hipErrorInvalidValue;
+  size_t lds = 0;
+  if (a->ngather > 0) {
+    // every gather tile reads ids and features and writes both A copies of its 32 rows;
+    // sibling groups must fit a tile (P <= 32) and rows be whole 16-byte chunks
+    const TrFwdArgs& g = a->gat;
+    if (!g.x || !g.nodes || !g.leaf || !g.a_kt || !g.a_rows || g.FL < 1 || g.D % 8 != 0 || g.D <= 0 ||
+        g.M % kG32Rows != 0 || a->ngather != g.M / kG32Rows || g.logPg < 2 || (1 << g.logPg) > kG32Rows ||
+        g.Fg >= (1 << g.logPg))
+      return hipErrorInvalidValue;
+    lds = eh_tr_gather32_lds(g.D, g.FL);
+    if (lds > 64 * 1024) return hipErrorInvalidValue;
+    extra += a->ngather;
+  }
+  const int tpb = a->ngather > 0 && a->opt_tpb > 1 ? a->opt_tpb : 1;
+  const int nopt = (a->nblk + tpb - 1) / tpb;
+  const dim3 grid(static_cast<uint32_t>(nopt + extra));
+#define TR_OPT(MODEV, FT, G) hipLaunchKernelGGL((tr_opt_kernel<MODEV, FT, G>), grid, dim3(256), lds, s, A)
+  if (a->ngather > 0 && a->gat_fp32) {
+    if (mode == 0) TR_OPT(0, float, 1);
+    else if (mode == 1) TR_OPT(1, float, 1);
+    else if (mode == 2) TR_OPT(2, float, 1);
+    else return hipErrorInvalidValue;
+  } else if (a->ngather > 0) {
+    if (mode == 0) TR_OPT(0, bf16_t, 1);
+    else if (mode == 1) TR_OPT(1, bf16_t, 1);
+    else if (mode == 2) TR_OPT(2, bf16_t, 1);
+    else return hipErrorInvalidValue;
+  } else {
+    if (mode == 0) TR_OPT(0, bf16_t, 0);
+    else if (mode == 1) TR_OPT(1, bf16_t, 0);
+    else if (mode == 2) TR_OPT(2, bf16_t, 0);
+    else if (mode == 3) TR_OPT(3, bf16_t, 0);
+    else return hipErrorInvalidValue;
+  }
+#undef TR_OPT
   return hipGetLastError();
 }
 

@@ -100,6 +100,9 @@ struct TrFwdArgs {
   long long* prof;       // optional per-block phase stamps [grid][8]
   TrCombArgs comb;       // modes 0/1, ncomb != 0: wave 0 of every block builds tiles of the head's Wc
   int32_t ncomb;
+  uint16_t* a_rows;      // pipelined step: [M][2D] row-major A rows ([self | mean]) written by the
+                         // gather blocks of the previous optimizer launch, read by the GEMM-only
+                         // forward (mode 3)
 };
 
 // head: last SAGE conv + fc + out_fc + sigmoid-CE + backward down to dA, kTrHeadRows roots / block
@@ -183,6 +186,11 @@ struct TrOptArgs {
   float* loss_out;         // loss of the last optimizer step
   TrSampleArgs smp;        // the next step's sampler, run by extra blocks (modes 1/2)
   int32_t nsample;         // sampler blocks (0: none)
+  TrFwdArgs gat;           // the next step's layer-0 gather (pipelined step), run by extra blocks:
+  int32_t ngather;         //   32-row tiles -> gat.a_kt (dW operand) and gat.a_rows (0: none)
+  int32_t gat_fp32;        //   feature table dtype
+  int32_t gather_first;    //   gather tiles before the parameter / sampler blocks in the grid
+  int32_t opt_tpb;         //   with gather tiles: parameter tiles per block (fewer, longer blocks)
 };
 
 // one launch for every dW of the step: routed problems first (their blocks, S % 8 == 0),
@@ -199,7 +207,10 @@ struct TrDwLaunch {
 extern "C" {
 // feat_fp32: feature table dtype (modes 0/1); bm: rows per block (32, 64 or 128)
 hipError_t eh_tr_sample(const euler_hip::TrSampleArgs* a, hipStream_t s);
+// mode 3: GEMM-only layer 0 of the pipelined step (a->a_rows from the gather blocks of the
+// previous tr_opt launch; fwd2 shapes only)
 hipError_t eh_tr_fwd(const euler_hip::TrFwdArgs* a, int mode, int feat_fp32, int bm, hipStream_t s);
+size_t eh_tr_gather32_lds(int D, int FL);
 hipError_t eh_tr_head(const euler_hip::TrHeadArgs* a, int64_t B, hipStream_t s);
 hipError_t eh_tr_bwd(const euler_hip::TrBwdArgs* a, hipStream_t s);
 // fills S / tiles / wg0 of every problem from P, Q, MB, kps before launching

@@ -205,14 +205,13 @@ class DeepWalkTrainer:
         return g[: n - 1], loss_rows.sum() * gscale, (coef, ptr_t, lst_t, ptr_c, lst_c, g)
 
     def _step_static_overlapped(self):
-        """Two micro-batches of batch/2 walks.  Compute stream S: front0, front1, compute0,
-        compute1; comm stream X: exchange0 (after front0), exchange1 (after front1), apply0
-        (after compute0), apply1 (after compute1).  So exchange0 runs under front1,
-        exchange1 under compute0 and apply0 under compute1; every table read (the owners'
-        row gathers) and write (the updates) is on X in that order, micro-batch 1 reads its
-        rows before micro-batch 0's update lands (the full-batch step reads every row
-        before its single update), and every rank issues the collectives in the same
-        order on X.  Each micro-batch applies its own row-sparse optimizer update."""
+        """Two micro-batches of batch/2 walks.  The calling stream S runs every collective
+        and table access in order: front0, exchange0, exchange1, apply0, apply1; a forked
+        compute stream X runs front1 (under exchange0), compute0 (under exchange1) and
+        compute1 (under apply0).  Micro-batch 1 reads its rows before micro-batch 0's
+        update lands (the full-batch step reads every row before its single update); every
+        rank issues the collectives in the same order.  Each micro-batch applies its own
+        row-sparse optimizer update."""
         tab = self.table
         S = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
         if S is None:  # CPU (gloo): the same phases in order on one stream
@@ -229,35 +228,35 @@ class DeepWalkTrainer:
         if self._xstream is None:
             self._xstream = torch.cuda.Stream(device=self.device)
             # per micro-batch exchange buffers: allocated by the first (eager) step, reused
-            # by every later step and by the capture (collective operands on the comm stream
-            # must not be allocated inside the capture)
+            # by every later step and by the capture
             self._bufs = ({}, {})
+        # collectives stay on the calling (capture-origin) stream S; the micro-batches'
+        # sampling / SGNS compute forks onto X (a capture with RCCL all-to-alls issued on a
+        # side stream crashed in capture_end on this ROCm: profiles/r3_deepwalk/)
         X = self._xstream
-        ev = [torch.cuda.Event() for _ in range(6)]
-        m0 = self._mb_front(self.batch // 2)
+        ev = [torch.cuda.Event() for _ in range(5)]
+        m0 = self._mb_front(self.batch // 2)                                   # S
         ev[0].record(S)
-        m1 = self._mb_front(self.batch // 2)
-        ev[1].record(S)
         with torch.cuda.stream(X):
             X.wait_event(ev[0])
-            r0 = tab.exchange_static(m0["routed"], trash_row=True, bufs=self._bufs[0])
-            ev[2].record(X)
-            X.wait_event(ev[1])
-            r1 = tab.exchange_static(m1["routed"], trash_row=True, bufs=self._bufs[1])
+            m1 = self._mb_front(self.batch // 2)                               # X, under exchange 0
+            ev[1].record(X)
+        r0 = tab.exchange_static(m0["routed"], trash_row=True, bufs=self._bufs[0])  # S
+        ev[2].record(S)
+        with torch.cuda.stream(X):
+            X.wait_event(ev[2])
+            g0, l0, k0 = self._mb_compute(m0, *r0)                            # X, under exchange 1
             ev[3].record(X)
-        S.wait_event(ev[2])
-        g0, l0, k0 = self._mb_compute(m0, *r0)
+        S.wait_event(ev[1])
+        r1 = tab.exchange_static(m1["routed"], trash_row=True, bufs=self._bufs[1])  # S
+        S.wait_event(ev[3])
         ev[4].record(S)
         with torch.cuda.stream(X):
             X.wait_event(ev[4])
-            tab.apply_static(r0[1], g0, bufs=self._bufs[0])
-        S.wait_event(ev[3])
-        g1, l1, k1 = self._mb_compute(m1, *r1)
-        ev[5].record(S)
-        with torch.cuda.stream(X):
-            X.wait_event(ev[5])
-            tab.apply_static(r1[1], g1, bufs=self._bufs[1])
+            g1, l1, k1 = self._mb_compute(m1, *r1)                            # X, under apply 0
+        tab.apply_static(r0[1], g0, bufs=self._bufs[0])                        # S
         S.wait_stream(X)
+        tab.apply_static(r1[1], g1, bufs=self._bufs[1])                        # S
         # every intermediate stays referenced until the next step: tensors made on one
         # stream and read on the other are never handed back to the allocator mid-step
         self._keep = (m0, m1, r0, r1, g0, g1, k0, k1)

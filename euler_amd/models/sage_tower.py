@@ -18,8 +18,11 @@ Execution (MI355X), per step, one hipGraph:
     layer-0 MFMA GEMM + ReLU and the tree mean of hop 1 in one launch, producing the last
     conv's input rows [R][2H0]; its backward routes dA1 through the tree and the ReLU bits
     inside the split-K dW kernel (no per-row gradient tensor is materialised);
-  * the last conv, fc, the pair logits and the loss are [R]-row torch ops (hipBLASLt GEMMs)
-    under autograd; one flat Adam launch (``csrc/hip/optim.hip``) updates both towers.
+  * the last conv and fc of a tower form ONE autograd node with its layer 0
+    (``models/_tower_ops.py`` tower_head: split-K head dW, every gradient written into its
+    flat-gradient view, no zero fill, no accumulation pass); the pair logits + sigmoid CE are
+    one more node (pair_loss); one flat Adam launch (``csrc/hip/optim.hip``) updates both
+    towers.
 
 Widths are padded (features to 16, conv widths to 64, fc to 32) with zero rows / columns
 that stay zero.  On a CPU device the same model, sampling layout and optimizer run in fp32
@@ -32,6 +35,7 @@ import math
 import torch
 import torch.nn.functional as F
 
+from euler_amd.models._tower_ops import pair_loss, tower_head
 from euler_amd.ops._native import hip
 from euler_amd.parallel.flat import FlatOptimizer, FlatParams
 
@@ -79,7 +83,11 @@ class _Tower:
         self.leaf = torch.zeros(self.M * self.F2, **i32)
         self.A1 = torch.zeros(self.R * 2 * self.H0, dtype=torch.bfloat16, device=device)
         self.dA1 = torch.zeros(self.R * 2 * self.H0, dtype=torch.float32, device=device)
-        self.gW0 = torch.zeros(W0.numel(), dtype=torch.float32, device=device)
+        # the routed layer-0 dW is reduced straight into W0's flat-gradient view when there
+        # is one (FlatParams), else into a buffer of its own
+        g = W0.grad
+        self.gW0 = (g.view(-1) if g is not None and g.is_contiguous() and g.dtype == torch.float32
+                    else torch.zeros(W0.numel(), dtype=torch.float32, device=device))
         self.plan = None
         if device.type == "cuda":
             g = graph
@@ -94,27 +102,6 @@ class _Tower:
                  "gW0": self.gW0}
             self._keep = d
             self.plan = hip().TowerPlan(d)
-
-
-class _TowerL0(torch.autograd.Function):
-    """A1 = layer 0 of a tower (fused sample + gather + GEMM + tree mean); backward: the
-    routed split-K dW of W0."""
-
-    @staticmethod
-    def forward(ctx, W0, tower):
-        p = tower.plan
-        p.shadow()
-        p.sample()
-        p.fwd()
-        ctx.tower = tower
-        return tower.A1.view(tower.R, 2 * tower.H0).float()
-
-    @staticmethod
-    def backward(ctx, dA1):
-        t = ctx.tower
-        t.dA1.view(t.R, 2 * t.H0).copy_(dA1)
-        t.plan.bwd()
-        return t.gW0.view(t.H0, -1), None
 
 
 class UnsupSageTrainer:
@@ -352,8 +339,17 @@ class UnsupSageTrainer:
             ts.roots_in.copy_(src)
             tc.roots_in[: self.B].copy_(pos)
             tc.roots_in[self.B:].copy_(negs)
-            A1s = _TowerL0.apply(self.params["gnn.W0"], ts)
-            A1c = _TowerL0.apply(self.params["context_gnn.W0"], tc)
+            P = self.params
+            # fused towers (one autograd node each: layer 0 + last conv + fc, gradients
+            # written into the flat-gradient views) and the fused pair loss
+            es = tower_head(P["gnn.W0"], P["gnn.W1"], P["gnn.Wfc"], P["gnn.bfc"], ts)
+            ec = tower_head(P["context_gnn.W0"], P["context_gnn.W1"], P["context_gnn.Wfc"], P["context_gnn.bfc"],
+                            tc)
+            loss, logits = pair_loss(es, ec, self.B, self.K)
+            with torch.no_grad():
+                rank = 1 + (logits[:, 1:] >= logits[:, :1]).sum(1).float()
+                mrr = (1.0 / rank).sum()
+            return loss, mrr
         else:
             ctx = torch.cat([pos, negs]).long()
             ns, ls = self._cpu_tree(src.long())
@@ -379,7 +375,8 @@ class UnsupSageTrainer:
 
     def _step(self, grad_sync=None):
         loss, mrr = self._forward_loss()
-        self.opt.zero_grad()
+        if self.device.type != "cuda":
+            self.opt.zero_grad()  # the GPU towers overwrite every gradient view instead
         loss.backward()
         scale = 1.0
         if grad_sync is not None:
@@ -485,7 +482,8 @@ class UnsupSageTrainer:
     def forward_backward(self):
         """sampling, forward, backward of one step (no optimizer): :meth:`gradients`"""
         loss, _ = self._forward_loss()
-        self.opt.zero_grad()
+        if self.device.type != "cuda":
+            self.opt.zero_grad()
         loss.backward()
         return float(loss)
 

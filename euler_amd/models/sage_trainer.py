@@ -77,6 +77,9 @@ def _xavier(shape, gen):
 
 # which launch carries the next step's sampler blocks: the head (default) or the optimizer
 _SAMPLE_IN_OPT = os.environ.get("EULER_AMD_SAMPLE_IN", "head") == "opt"
+# pipelined step (2 hops): the optimizer launch gathers the next step's layer-0 inputs on
+# the CUs its parameter blocks leave idle, the forward is then GEMM-only
+_PIPELINE = os.environ.get("EULER_AMD_PIPELINE", "1") != "0"
 
 
 class SageTrainer:
@@ -156,6 +159,7 @@ class SageTrainer:
             self._cpu_v = {k: torch.full_like(v, 0.1 if optimizer == "adagrad" else 0.0) for k, v in
                            logical.items()}
             self._cpu_loss = torch.zeros(())
+            self.pipelined, self._gathered = False, False
             self._cpu_counts = [0, 0, 0]
             self._cpu_samples = None
         self._graph_exec = None
@@ -326,6 +330,8 @@ class SageTrainer:
         d["nodes"], d["leaf"] = self.nodes, self.leaf
         if self.fshard is None:
             d["features"] = self.features
+            if _PIPELINE and L == 2:
+                d["A0_rows"] = torch.empty(M_last * 2 * self.Dp, **bf)
         else:
             # the forward gathers from the exchange's cache through cache positions
             n = M_last * (1 + FL)
@@ -360,6 +366,8 @@ class SageTrainer:
         self.plan = hip().TreePlan(d)
         self._dw_all = list(range(self.plan.num_problems()))
         self._primed = False  # the sample buffers hold the batch of counter graph.rng[1]
+        self.pipelined = bool(self.plan.pipeline_ok())
+        self._gathered = False  # A0_rows / A0_kt hold the layer-0 inputs of the sampled batch
 
     # ------------------------------------------------------------------ parameters / state
     def load_logical(self, logical):
@@ -410,6 +418,7 @@ class SageTrainer:
         self.graph.rng.copy_(torch.as_tensor(st["rng"]).to(self.graph.rng))
         self.step_count = int(st["step"])
         self._primed = False
+        self._gathered = False
         if self.on_gpu:
             self._pack({k: torch.as_tensor(t) for k, t in st["m"].items()}, self.m)
             self._pack({k: torch.as_tensor(t) for k, t in st["v"].items()}, self.v)
@@ -424,6 +433,7 @@ class SageTrainer:
         if not self._primed:
             self.plan.sample()
             self._primed = True
+            self._gathered = False
 
     def _fwd(self):
         if self.fshard is not None:
@@ -439,6 +449,7 @@ class SageTrainer:
         self._fwd()
         p.head()
         self._primed = False
+        self._gathered = False
         p.bwd()
         p.dw(self._dw_all)
         p.opt(0)
@@ -486,24 +497,29 @@ class SageTrainer:
             return self._cpu_step(grad_sync)
         p = self.plan
         self._prime()
-        self._fwd()
+        if self.pipelined and self._gathered:
+            p.fwd(None, True)  # layer-0 inputs gathered by the previous optimizer launch
+        else:
+            self._fwd()
         smp_opt = _SAMPLE_IN_OPT and grad_sync is None
         p.head(None, not smp_opt)
         p.bwd()
+        gat = self.pipelined  # this launch gathers the batch the head just sampled
         if grad_sync is None:
             p.dw(self._dw_all)
-            p.opt(2, 1.0, smp_opt)
+            p.opt(2, 1.0, smp_opt, gat)
         elif len(self.grad_buckets()) == 1:
             p.dw(self._dw_all)
-            p.opt(0)
+            p.opt(0, 1.0, False, gat)  # independent of the all-reduce that follows
             g = self.grad if getattr(self, "grad16", None) is None else self.grad16
             scale = grad_sync(g)
             p.opt(1, 1.0 if scale is None else float(scale))
         else:
-            self._dist_backward(grad_sync)
+            self._dist_backward(grad_sync, gat)
         self._primed = True
+        self._gathered = gat
 
-    def _dist_backward(self, grad_sync):
+    def _dist_backward(self, grad_sync, gather=False):
         p = self.plan
         if not hasattr(self, "_comm_stream"):
             self._comm_stream = torch.cuda.Stream(device=self.device)
@@ -525,7 +541,7 @@ class SageTrainer:
             with torch.cuda.stream(side):
                 grad_sync(g[b0:b1])
         main.wait_stream(side)
-        p.opt(1, 1.0 if scale is None else float(scale))
+        p.opt(1, 1.0 if scale is None else float(scale), False, gather)
 
     def plan_launches(self):
         """(name, callable) of every launch of one pipelined step, for per-kernel timing"""
@@ -535,6 +551,8 @@ class SageTrainer:
         if self.L == 3:
             out.append(("bwd", p.bwd))
         out += [("dw", lambda: p.dw(self._dw_all)), ("opt", lambda: p.opt(2))]
+        if self.pipelined:
+            out += [("opt+gather", lambda: p.opt(2, 1.0, False, True)), ("fwd_gemm", lambda: p.fwd(None, True))]
         return out
 
     def capture(self, grad_sync=None, warmup: int = 2, steps: int = 1):

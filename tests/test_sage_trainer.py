@@ -197,6 +197,34 @@ def test_graph_replay_matches_eager(cuda):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fdt", [torch.bfloat16, torch.float32])
+def test_pipelined_step_matches_unpipelined(cuda, fdt):
+    """The pipelined step (the optimizer launch gathers the next batch's layer-0 inputs,
+    the forward is GEMM-only) computes exactly what the fused gather+GEMM forward does:
+    bit-identical losses and parameters, eager and graph-replayed."""
+    a = _trainer(cuda, [25, 10], [64, 64, 32], 32, fdt=fdt, D=64)
+    b = _trainer(cuda, [25, 10], [64, 64, 32], 32, fdt=fdt, D=64)
+    assert a.pipelined
+    b.pipelined = False
+    la, lb = [], []
+    for _ in range(5):
+        a.step()
+        b.step()
+        la.append(float(a.loss.item()))
+        lb.append(float(b.loss.item()))
+    a.capture(warmup=1, steps=2)
+    b.capture(warmup=1, steps=2)
+    a.replay_steps(5)
+    b.replay_steps(5)
+    la.append(float(a.loss.item()))
+    lb.append(float(b.loss.item()))
+    assert la == lb, (la, lb)
+    pa, pb = a.logical_params(), b.logical_params()
+    assert all(torch.equal(pa[k], pb[k]) for k in pa)
+    assert la[-1] < la[0]
+
+
+@pytest.mark.gpu
 def test_sharded_feature_cache_matches_whole_table(cuda):
     """The forward reading a feature cache through cache positions (the sharded-feature
     exchange, here one rank without collectives: unique + gather into the cache) trains

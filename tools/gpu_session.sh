@@ -46,6 +46,14 @@ for st in "${S[@]}"; do
       EULER_AMD_TREE_FORK=0 run tree_kernels_nofork 300 python -u tools/tree_kernels.py ;;
     sweep_sample)
       EULER_AMD_SAMPLE_IN=opt run tree_kernels_sample_opt 300 python -u tools/tree_kernels.py ;;
+    sweep_pipe)
+      # pipelined step: gather tiles first / last in the optimizer grid, parameter tiles per block
+      for cfg in "1:4" "1:1" "0:4" "0:8" "1:8"; do
+        IFS=':' read -r gf tpb <<< "$cfg"
+        EULER_AMD_GATHER_FIRST=$gf EULER_AMD_OPT_TPB=$tpb run "tree_kernels_pipe_gf${gf}_tpb${tpb}" 300 \
+          python -u tools/tree_kernels.py || exit $?
+      done
+      EULER_AMD_PIPELINE=0 run tree_kernels_nopipe 300 python -u tools/tree_kernels.py ;;
     sweep_fwd)
       for bm in 32 64 128; do
         EULER_AMD_FWD_BM=$bm run "tree_kernels_fbm$bm" 300 python -u tools/tree_kernels.py
