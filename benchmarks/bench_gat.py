@@ -22,6 +22,7 @@ Labels: class = argmax of a random projection of the 2-hop neighbourhood mean (-
 --impl fused    : gat.hip (one pass per destination, online softmax; bwd: CSR + CSC passes)
 --impl composed : the reference's op sequence on our segment kernels (gather logits,
                   scatter_softmax, gather messages, scatter_add) — materialises [E, H*C]
+                  (fp32 messages: the same accumulation precision as the fused kernel)
 
 Prints one JSON line (rank 0).  Usage: python benchmarks/bench_gat.py [--epochs K] [--warmup W]
 """
@@ -87,8 +88,11 @@ class GATNet(nn.Module):
                 seg = csr_seg(csr)
                 logit = F.leaky_relu(mp_ops.gather(ar, ei[0]) + mp_ops.gather(al, ei[1]), 0.2)
                 alpha = mp_ops.scatter_softmax(logit, seg, csr.n_dst)
-                msg = mp_ops.gather(z.reshape(-1, H * C), ei[1]).view(-1, H, C) * alpha.unsqueeze(-1).to(z.dtype)
-                agg = mp_ops.scatter_add(msg.reshape(-1, H * C), seg, csr.n_dst).view(-1, H, C)
+                # messages and their sums in fp32 like the fused kernel's accumulators (bf16
+                # messages summed over ~50 in-edges cost this variant ~13 points of held-out
+                # accuracy at 400 epochs: profiles/r3_learning/bench_gat_composed_bf16msg.log)
+                msg = mp_ops.gather(z.reshape(-1, H * C), ei[1]).view(-1, H, C).float() * alpha.unsqueeze(-1).float()
+                agg = mp_ops.scatter_add(msg.reshape(-1, H * C), seg, csr.n_dst).view(-1, H, C).to(z.dtype)
             h = F.elu(agg.reshape(-1, H * C))
         # the classifier only runs on the rows the loss reads (same loss and gradients
         # as classifying every node; avoids a 2.4M-row logits tensor and its bias reduce)

@@ -393,7 +393,13 @@ class RelationConv(Conv):
         src = x[1] if x[1] is not None else x[0]
         # relation-grouped MFMA GEMM with the gather and the mean aggregation fused (rgcn.hip)
         agg = gnn_ops.relation_transform(src, edge_attr, self.matrix, edge_index, size, "mean")
-        return self.fc(x[0]) + agg.to(src.dtype)
+        fc, x0 = self.fc, x[0]
+        if x0.is_cuda and x0.dim() == 2 and not fc.has_uninitialized_params() and fc.bias is None \
+                and fc.activation is None:
+            # self-loop transform on the tiled MFMA GEMM, bf16 operands like the relation
+            # GEMMs (hipBLASLt ran it on a few 128 x 128 tiles)
+            return gnn_ops.linear(x0, fc.weight) + agg.to(src.dtype)
+        return fc(x0) + agg.to(src.dtype)
 
 
 class GatedConv(Conv):

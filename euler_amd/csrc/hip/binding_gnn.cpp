@@ -532,6 +532,53 @@ std::vector<torch::Tensor> unique_first_padded(torch::Tensor x, int64_t fill) {
   return {uniq, inv, pos.narrow(0, n - 1, 1).to(torch::kInt64)};
 }
 
+// C = op(A) op(B) (+ bias) (relu) (* relu'(rmask)) with the tiled MFMA GEMM (gemm.hip):
+// trans_a: A is [K][M]; trans_b: B is [N][K] (else [K][N]); A, B fp32 or bf16 row-major
+// (unit inner stride); C fp32 or bf16 [M][N] (row stride >= N) is written in place.
+// splits > 1: split-K over the reduction dimension (deterministic slabs + one reduce).
+void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool trans_a, bool trans_b,
+          c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> rmask, bool relu, int64_t splits,
+          double alpha) {
+  auto fp = [](const torch::Tensor& t, const char* n) {
+    TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.stride(1) == 1 &&
+                    (t.scalar_type() == torch::kFloat32 || t.scalar_type() == torch::kBFloat16),
+                n, " must be a 2-D fp32/bf16 GPU matrix with unit inner stride");
+  };
+  fp(A, "A");
+  fp(B, "B");
+  fp(C, "C");
+  const int64_t M = trans_a ? A.size(1) : A.size(0), K = trans_a ? A.size(0) : A.size(1);
+  const int64_t N = trans_b ? B.size(0) : B.size(1), KB = trans_b ? B.size(1) : B.size(0);
+  TORCH_CHECK(K == KB, "gemm: inner dimensions differ (", K, " vs ", KB, ")");
+  TORCH_CHECK(C.size(0) == M && C.size(1) == N, "gemm: C must be [", M, ", ", N, "]");
+  TORCH_CHECK(splits >= 1 && splits <= 1024, "gemm: 1 <= splits <= 1024");
+  const float* bp = nullptr;
+  if (bias.has_value()) {
+    typed(*bias, torch::kFloat32, "bias");
+    TORCH_CHECK(bias->numel() == N, "gemm: bias must have N elements");
+    bp = bias->data_ptr<float>();
+  }
+  const void* rp = nullptr;
+  int64_t ldr = 0;
+  int r_bf16 = 0;
+  if (rmask.has_value()) {
+    fp(*rmask, "rmask");
+    TORCH_CHECK(rmask->size(0) == M && rmask->size(1) == N, "gemm: rmask must be [M, N]");
+    rp = rmask->data_ptr();
+    ldr = rmask->stride(0);
+    r_bf16 = rmask->scalar_type() == torch::kBFloat16;
+  }
+  const c10::DeviceGuard g(A.device());
+  torch::Tensor part;
+  if (splits > 1) part = torch::empty({splits * M * N}, A.options().dtype(torch::kFloat32));
+  ok(eh_gemm(A.data_ptr(), B.data_ptr(), C.data_ptr(), bp, rp, splits > 1 ? part.data_ptr<float>() : nullptr, M, N, K,
+             A.stride(0), B.stride(0), C.stride(0), ldr, trans_a ? 1 : 0, trans_b ? 0 : 1,
+             A.scalar_type() == torch::kBFloat16, B.scalar_type() == torch::kBFloat16,
+             C.scalar_type() == torch::kBFloat16, r_bf16, relu ? 1 : 0, static_cast<int>(splits),
+             static_cast<float>(alpha), stream()),
+     "gemm");
+}
+
 // (pos [n] slot of every id in the W*C exchange space, W*C = none / did not fit; send
 // [W*C + 1] the id of every slot, -1 = empty); overflow [1] int32 is set to 1 when an id
 // did not fit its owner's C slots
@@ -556,6 +603,9 @@ std::vector<torch::Tensor> route_by_owner(torch::Tensor ids, int64_t W, int64_t 
 
 void register_gnn_ops(pybind11::module& m) {
   m.def("route_by_owner", &route_by_owner);
+  m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("trans_a") = false,
+        py::arg("trans_b") = false, py::arg("bias") = py::none(), py::arg("rmask") = py::none(),
+        py::arg("relu") = false, py::arg("splits") = 1, py::arg("alpha") = 1.0);
   m.def("gat_supported", &gat_supported);
   m.def("gat_fwd", &gat_fwd, py::arg("indptr"), py::arg("col"), py::arg("order"), py::arg("h"), py::arg("al"),
         py::arg("ar"), py::arg("H"), py::arg("C"), py::arg("slope"), py::arg("a_src") = py::none());

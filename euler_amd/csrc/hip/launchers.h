@@ -107,6 +107,12 @@ hipError_t eh_kg_bwd(const float* ent, const float* rel, const int64_t* src, con
                      const int64_t* neg, int64_t B, int K, int D, int kind, int corrupt, int normalize,
                      const float* gpos, const float* gneg, float* dent, float* drel, hipStream_t s);
 
+// gemm.hip (tiled MFMA GEMM with fused epilogues and split-K)
+hipError_t eh_gemm(const void* A, const void* B, void* C, const float* bias, const void* rmask, float* part,
+                   int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int a_t,
+                   int b_t, int a_bf16, int b_bf16, int c_bf16, int r_bf16, int relu, int splits, float alpha,
+                   hipStream_t s);
+
 // route.hip (owner routing of the fixed-capacity all-to-all exchanges)
 int64_t eh_route_chunks(int64_t n);
 hipError_t eh_route_by_owner(const int64_t* ids, int64_t n, int W, int64_t C, int32_t* cnt, int64_t* pos,

@@ -1,12 +1,13 @@
 """Fused autograd pieces of the unsupervised GraphSAGE device step (models/sage_tower.py).
 
 ``tower_head``: layer 0 of a tower (TowerPlan: sample + gather + MFMA GEMM + tree mean)
-followed by the last SAGE conv and the fc layer, as ONE autograd node whose backward writes
-every parameter gradient straight into its flat-gradient view (``out=``): the head dW
-products as split-K batched GEMMs (a [R]-row reduction as one GEMM runs on a handful of
-workgroups: 38 us per call in ``profiles/r3_unsup/``), dA1 into the plan's buffer and
-the routed layer-0 dW by the plan.  Nothing is accumulated, so the trainer never zeroes
-the flat gradient (each step overwrites all of it).
+followed by the last SAGE conv and the fc layer, as ONE autograd node on the tiled MFMA
+GEMM (csrc/hip/gemm.hip: ReLU, bias and the ReLU-mask product fused as epilogues; the
+[R]-row weight-gradient products split-K — hipBLASLt ran them on a handful of 256 x 128
+tiles, 20-38 us per call in ``profiles/r3_unsup/``), whose backward writes every parameter
+gradient straight into its flat-gradient view (``out=``), dA1 into the plan's buffer and
+the routed layer-0 dW through the plan.  Nothing is accumulated, so the trainer never
+zeroes the flat gradient (each step overwrites all of it).
 
 ``pair_loss``: the source / context dot products of the B positives and B*K negatives,
 sigmoid cross-entropy (mean over the B + B*K logits, the reference's
@@ -18,31 +19,18 @@ import torch
 import torch.nn.functional as F
 
 
-def mm_t_into(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, parts: int = 0):
-    """``out = a^T @ b`` (fp32) for tall a [M, P], b [M, Q], as row-chunk batched GEMMs
-    summed into ``out`` (overwritten)."""
-    M = a.shape[0]
-    p = parts or max(1, min(32, M // 256))
-    while p > 1 and M % p:
-        p -= 1
-    if p == 1:
-        torch.mm(a.t(), b, out=out)
-        return out
-    part = torch.bmm(a.view(p, M // p, -1).transpose(1, 2), b.view(p, M // p, -1))
-    torch.sum(part, 0, out=out)
-    return out
-
-
 class _TowerHead(torch.autograd.Function):
     @staticmethod
     def forward(ctx, W0, W1, Wfc, bfc, tower):
+        from euler_amd.ops.gnn_ops import gemm
+
         p = tower.plan
         p.shadow()
         p.sample()
         p.fwd()
-        A1 = tower.A1.view(tower.R, 2 * tower.H0).float()
-        h1 = torch.relu(A1 @ W1.t())
-        e = torch.addmm(bfc, h1, Wfc.t())
+        A1 = tower.A1.view(tower.R, 2 * tower.H0)  # bf16 rows [self | mean] from layer 0
+        h1 = gemm(A1, W1, trans_b=True, relu=True)
+        e = gemm(h1, Wfc, trans_b=True, bias=bfc)
         ctx.tower = tower
         ctx.params = (W1, Wfc, bfc)
         ctx.save_for_backward(A1, h1)
@@ -50,17 +38,25 @@ class _TowerHead(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, de):
+        from euler_amd.ops.gnn_ops import _gemm_splits, gemm
+
         A1, h1 = ctx.saved_tensors
         W1, Wfc, bfc = ctx.params
         t = ctx.tower
         de = de.contiguous()
-        mm_t_into(de, h1, Wfc.grad)
+        R = de.shape[0]
+        # weight gradients: split-K over the R rows, written into the flat-gradient views
+        gemm(de, h1, out=Wfc.grad, trans_a=True, splits=_gemm_splits(R, _tiles(Wfc)))
         torch.sum(de, 0, out=bfc.grad)
-        dh1 = torch.ops.aten.threshold_backward(de @ Wfc, h1, 0.0)
-        mm_t_into(dh1, A1, W1.grad)
-        torch.mm(dh1, W1, out=t.dA1.view(t.R, 2 * t.H0))
+        dh1 = gemm(de, Wfc, rmask=h1)  # (de Wfc) * relu'(h1)
+        gemm(dh1, A1, out=W1.grad, trans_a=True, splits=_gemm_splits(R, _tiles(W1)))
+        gemm(dh1, W1, out=t.dA1.view(R, 2 * t.H0))
         t.plan.bwd()  # routed layer-0 dW, reduced into the W0 gradient view
         return None, None, None, None, None
+
+
+def _tiles(w):
+    return -(-w.shape[0] // 64) * -(-w.shape[1] // 64)
 
 
 def tower_head(W0, W1, Wfc, bfc, tower):

@@ -79,7 +79,7 @@ def _xavier(shape, gen):
 _SAMPLE_IN_OPT = os.environ.get("EULER_AMD_SAMPLE_IN", "head") == "opt"
 # pipelined step (2 hops): the optimizer launch gathers the next step's layer-0 inputs on
 # the CUs its parameter blocks leave idle, the forward is then GEMM-only
-_PIPELINE = os.environ.get("EULER_AMD_PIPELINE", "1") != "0"
+_PIPELINE = os.environ.get("EULER_AMD_PIPELINE", "0") == "1"
 
 
 class SageTrainer:

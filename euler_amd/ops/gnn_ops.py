@@ -215,6 +215,71 @@ def gat_conv(z, a_src, a_dst, csr: EdgeCSR, slope=0.2):
     return gat_conv_reference(z, a_src, a_dst, csr.edge_index, (N, N), slope).to(z.dtype)
 
 
+def gemm(a, b, out=None, trans_a=False, trans_b=False, bias=None, relu=False, rmask=None, splits=1, alpha=1.0,
+         out_dtype=torch.float32):
+    """``out = alpha * op(a) @ op(b) (+ bias) (relu) (* (rmask > 0))`` with op(x) = x^T when
+    trans_x (BLAS convention).  GPU: the tiled MFMA kernel of csrc/hip/gemm.hip (bf16
+    operands, fp32 accumulation; ``splits`` > 1 splits the reduction dimension into
+    deterministic partial slabs + one reduce, for [R]-row weight-gradient products) —
+    hipBLASLt runs these skinny shapes on a few large tiles.  CPU: the torch composition."""
+    A = a.t() if trans_a else a
+    Bm = b.t() if trans_b else b
+    M, N = A.shape[0], Bm.shape[1]
+    if use_hip(a, b):
+        if out is None:
+            out = torch.empty(M, N, device=a.device, dtype=out_dtype)
+        aa = a if a.stride(-1) == 1 else a.contiguous()
+        bb = b if b.stride(-1) == 1 else b.contiguous()
+        hip().gemm(aa, bb, out, bool(trans_a), bool(trans_b), bias, rmask, bool(relu), int(splits), float(alpha))
+        return out
+    y = (A.float() @ Bm.float()) * alpha
+    if bias is not None:
+        y = y + bias.float()
+    if relu:
+        y = torch.relu(y)
+    if rmask is not None:
+        y = y * (rmask > 0).to(y.dtype)
+    if out is None:
+        return y.to(out_dtype)
+    out.copy_(y)
+    return out
+
+
+def _gemm_splits(k_rows, tiles):
+    """split-K count for a weight-gradient product over k_rows rows with `tiles` 64x64
+    output tiles: about 256 workgroups, at least 256 rows per split"""
+    return int(max(1, min(64, k_rows // 256, -(-256 // max(tiles, 1)))))
+
+
+class _Linear(torch.autograd.Function):
+    """``x @ w^T`` on the tiled MFMA GEMM (forward, dx, split-K dW)"""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return gemm(x, w, trans_b=True, out_dtype=x.dtype if x.dtype in (torch.float32, torch.bfloat16)
+                    else torch.float32)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = gemm(g, w, out_dtype=x.dtype)
+        if ctx.needs_input_grad[1]:
+            tiles = -(-w.shape[0] // 64) * -(-w.shape[1] // 64)
+            dw = gemm(g, x, trans_a=True, splits=_gemm_splits(x.shape[0], tiles), out_dtype=w.dtype)
+        return dx, dw
+
+
+def linear(x, w):
+    """``x @ w^T`` (no bias) for 2-D x: the tiled MFMA GEMM on the GPU (self-loop transforms
+    of full-graph layers), torch elsewhere"""
+    if use_hip(x, w) and x.dim() == 2 and w.dtype == torch.float32:
+        return _Linear.apply(x, w)
+    return x @ w.t().to(x.dtype)
+
+
 class _TallLinear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, chunk):
