@@ -90,9 +90,11 @@ def main(argv=None):
     p.add_argument("--layers", type=int, default=2, help="R-GCN layers before the TransE decoder (0: TransE alone)")
     p.add_argument("--normalize", type=int, default=1,
                    help="1: l2-normalised rows in the score (reference transX.py:63-66); 0: raw rows")
-    p.add_argument("--task", choices=["lattice", "cold"], default="lattice",
+    p.add_argument("--task", choices=["lattice", "cold", "types"], default="lattice",
                    help="cold: a fraction of the entities never appears in a loss triple (their edges stay in "
-                        "the encoder graph); held-out triples with a cold head are ranked")
+                        "the encoder graph); held-out triples with a cold head are ranked.  types: "
+                        "dataset/synthetic.py typed_kg — rank the type hub of cold entities, whose type only "
+                        "their neighbourhood carries")
     p.add_argument("--cold-frac", type=float, default=0.1)
     p.add_argument("--no-graph", action="store_true", help="eager steps (default: one hipGraph per step)")
     p.add_argument("--device", default="cuda", help="cpu: torch reference ops (exploration only, eager)")
@@ -118,11 +120,22 @@ def main(argv=None):
 
     norm = bool(args.normalize)
     sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
-    (src, rel, dst), (te_src, te_rel, te_dst) = synthetic_kg(args.num_ent, args.num_rel, args.num_triples,
-                                                             args.seed, dev)
-    # message direction src -> dst (row 0 = destination, row 1 = source); every training
-    # triple is an encoder edge, also in the cold task
-    edge_index = torch.stack([dst, src])
+    if args.task == "types":
+        from euler_amd.dataset.synthetic import typed_kg
+
+        tr_, gr_, te_ = typed_kg(args.num_ent, args.num_rel, args.num_triples, cold_frac=args.cold_frac,
+                                 seed=args.seed)
+        (src, rel, dst), (gsrc, grel, gdst), (te_src, te_rel, te_dst) = (tuple(x.to(dev) for x in t)
+                                                                         for t in (tr_, gr_, te_))
+        # encoder graph: every link triple (cold ones too) + the warm type triples; the loss
+        # samples the training triples only
+        edge_index, edge_rel = torch.stack([gdst, gsrc]), grel
+    else:
+        (src, rel, dst), (te_src, te_rel, te_dst) = synthetic_kg(args.num_ent, args.num_rel, args.num_triples,
+                                                                 args.seed, dev)
+        # message direction src -> dst (row 0 = destination, row 1 = source); every training
+        # triple is an encoder edge, also in the cold task
+        edge_index, edge_rel = torch.stack([dst, src]), rel
     pool = torch.arange(src.numel(), device=dev)
     if args.task == "cold":
         g = torch.Generator().manual_seed(args.seed + 5)
@@ -141,7 +154,7 @@ def main(argv=None):
         negs = torch.randint(0, args.num_ent, (args.batch, args.num_negs), device=dev)
         return src[idx], rel[idx], dst[idx], negs
 
-    model(edge_index, rel, *batch()).backward()  # materialise lazy layers before the optimizer
+    model(edge_index, edge_rel, *batch()).backward()  # materialise lazy layers before the optimizer
     if world > 1:
         from euler_amd.parallel.dp import broadcast_module
 
@@ -152,7 +165,7 @@ def main(argv=None):
     for conv in model.convs:
         # the relation dW accumulates straight into its flat-grad view (no [R, D, D] temporary
         # + AccumulateGrad pass per layer; the flat grad is all-reduced as one buffer)
-        gnn_ops.enable_grad_sink(conv.matrix)
+        gnn_ops.enable_grad_sink(conv.matrix, zeroed=True)  # opt.zero_grad() runs before every backward
     opt = FlatOptimizer(flat, "adam", args.lr)
     loss_buf = torch.zeros((), device=dev)
 
@@ -160,7 +173,7 @@ def main(argv=None):
         from euler_amd.dataset.synthetic import rank_metrics, tail_ranks
 
         with torch.no_grad():
-            h = model.encode(edge_index, rel).float()
+            h = model.encode(edge_index, edge_rel).float()
         m = rank_metrics(tail_ranks(h, model.rel, te_src, te_rel, te_dst, normalize=norm))
         return {k: round(v, 4) for k, v in m.items()}
 
@@ -168,7 +181,7 @@ def main(argv=None):
 
     def step_body():
         opt.zero_grad()
-        loss = model(edge_index, rel, *batch())
+        loss = model(edge_index, edge_rel, *batch())
         loss.backward()
         scale = 1.0
         if world > 1:

@@ -59,6 +59,49 @@ def lattice_kg(num_ent, num_rel, num_triples, num_test, seed=0, max_off=5):
                                                                        dst[num_triples:])
 
 
+def typed_kg(num_ent, num_rel, num_triples, num_types=50, p_in=0.9, cold_frac=0.1, seed=0):
+    """Planted typed KG where an entity's type is carried by its neighbourhood.
+
+    Entities 0..num_types-1 are type hubs; every other entity e has a type c(e) and one
+    triple (e, rel 0 = "has_type", hub c(e)).  The other num_triples triples link entities
+    through relations 1..num_rel-1 (power-law frequencies), the tail drawn from the head's
+    type with probability p_in.  A cold_frac of the non-hub entities are *cold*: none of
+    their triples is a training (loss) triple, but their link triples stay in the encoder
+    graph; the test set is the cold entities' has_type triples — ranking the right hub
+    needs the type inferred from the neighbours (message passing), a cold entity's own
+    embedding never being trained.
+
+    Returns (train (src, rel, dst), graph (src, rel, dst), test (src, rel, dst)) int64 CPU
+    tensors: graph = every link triple (training + cold) + the warm has_type triples."""
+    g = torch.Generator().manual_seed(int(seed))
+    T = int(num_types)
+    ent = torch.arange(T, num_ent)
+    ctype = torch.randint(0, T, (num_ent,), generator=g)
+    ctype[:T] = torch.arange(T)
+    by_type = [ent[ctype[T:] == c] for c in range(T)]
+    cold = torch.zeros(num_ent, dtype=torch.bool)
+    cold[ent[torch.randperm(ent.numel(), generator=g)[: int(cold_frac * ent.numel())]]] = True
+    w = 1.0 / torch.arange(1, num_rel, dtype=torch.float64) ** 1.1
+    h = ent[torch.randint(0, ent.numel(), (num_triples,), generator=g)]
+    r = 1 + torch.multinomial(w, num_triples, replacement=True, generator=g)
+    inside = torch.rand(num_triples, generator=g) < p_in
+    t = ent[torch.randint(0, ent.numel(), (num_triples,), generator=g)]
+    for c in range(T):  # same-type tails
+        sel = inside & (ctype[h] == c)
+        k = int(sel.sum())
+        if k:
+            t[sel] = by_type[c][torch.randint(0, by_type[c].numel(), (k,), generator=g)]
+    types = (ent, torch.zeros_like(ent), ctype[ent])
+    link_cold = cold[h] | cold[t]
+    warm_types = ~cold[ent]
+    train = (torch.cat([h[~link_cold], types[0][warm_types]]), torch.cat([r[~link_cold], types[1][warm_types]]),
+             torch.cat([t[~link_cold], types[2][warm_types]]))
+    graph = (torch.cat([h, types[0][warm_types]]), torch.cat([r, types[1][warm_types]]),
+             torch.cat([t, types[2][warm_types]]))
+    test = (types[0][~warm_types], types[1][~warm_types], types[2][~warm_types])
+    return train, graph, test
+
+
 def community_graph(num_nodes, num_comm, avg_degree, p_in=0.9, seed=0):
     """(src, dst, comm): ``num_nodes * avg_degree`` directed edges, a fraction ``p_in``
     inside the source's community (community of node i = i % num_comm)."""

@@ -549,7 +549,7 @@ class _RelationTransform(torch.autograd.Function):
                 # persistent .grad buffer (e.g. a FlatParams view the optimizer zeroes) — no
                 # zero-filled [R, N, K] temporary and no AccumulateGrad add pass over it
                 hip().rel_gemm_dw(gb, tiles.dst, xb, tiles.src, tiles.scale, cr, cs, cl, tiles.chunk_solo, sink,
-                                  accumulate=True)
+                                  accumulate=ctx.weight._grad_sink != "zeroed")
             else:
                 dwp = torch.zeros(R, Np, Kp, device=dout.device, dtype=torch.float32)
                 hip().rel_gemm_dw(gb, tiles.dst, xb, tiles.src, tiles.scale, cr, cs, cl, tiles.chunk_solo, dwp)
@@ -557,12 +557,14 @@ class _RelationTransform(torch.autograd.Function):
         return dx, dw, None, None
 
 
-def enable_grad_sink(weight, on: bool = True):
-    """Let :func:`relation_transform`'s backward accumulate dW straight into
-    ``weight.grad`` (which must then exist and persist, zeroed by its owner between steps,
-    as FlatParams grads do).  Autograd never sees that gradient: gradient hooks on the
-    weight (e.g. dp.GradSync buckets) do not fire for it — sync the owner's flat grad."""
-    weight._grad_sink = bool(on)
+def enable_grad_sink(weight, on: bool = True, zeroed: bool = False):
+    """Let :func:`relation_transform`'s backward write dW straight into ``weight.grad``
+    (which must then exist and persist, as FlatParams grads do).  ``zeroed``: the owner
+    zeroes the gradient before every backward (FlatOptimizer.zero_grad), so relations with
+    a single edge chunk store their slab instead of read-modify-writing it; otherwise dW is
+    accumulated.  Autograd never sees that gradient: gradient hooks on the weight (e.g.
+    dp.GradSync buckets) do not fire for it — sync the owner's flat grad."""
+    weight._grad_sink = ("zeroed" if zeroed else "accumulate") if on else False
     return weight
 
 
