@@ -407,13 +407,16 @@ void sparse_optim_(torch::Tensor table, torch::Tensor m, torch::Tensor v, torch:
   need_i64(rows, "rows");
   need_cuda(grads, "grads");
   need_i64(step, "step");
-  TORCH_CHECK(table.scalar_type() == torch::kFloat32 && grads.scalar_type() == torch::kFloat32, "fp32 table/grads");
+  const bool gbf = grads.scalar_type() == torch::kBFloat16;
+  TORCH_CHECK(table.scalar_type() == torch::kFloat32 && (gbf || grads.scalar_type() == torch::kFloat32),
+              "fp32 table, fp32 or bf16 grads");
+  TORCH_CHECK(grads.is_contiguous() && (!gbf || table.size(1) % 4 == 0), "contiguous grads (bf16: D % 4 == 0)");
   TORCH_CHECK(table.dim() == 2 && grads.dim() == 2 && grads.size(1) == table.size(1) && grads.size(0) == rows.numel(),
               "sparse_optim shape mismatch");
   TORCH_CHECK(m.sizes() == table.sizes() && v.sizes() == table.sizes(), "optimizer state shape mismatch");
   const c10::DeviceGuard gd(table.device());
   check(eh_sparse_optim(table.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), rows.data_ptr<int64_t>(),
-                        grads.data_ptr<float>(), rows.numel(), static_cast<int>(table.size(1)), table.size(0),
+                        grads.data_ptr(), gbf ? 1 : 0, rows.numel(), static_cast<int>(table.size(1)), table.size(0),
                         step.data_ptr<int64_t>(), static_cast<float>(lr), static_cast<float>(b1),
                         static_cast<float>(b2), static_cast<float>(eps), static_cast<int>(kind), cur_stream()),
         "sparse_optim");

@@ -298,8 +298,9 @@ const int64_t* map_ptr(const c10::optional<torch::Tensor>& map, int64_t& n, cons
 std::vector<torch::Tensor> sgns_fwd_idx(torch::Tensor T, c10::optional<torch::Tensor> tmap, torch::Tensor tinv,
                                         torch::Tensor C, c10::optional<torch::Tensor> cmap, torch::Tensor cinv,
                                         int64_t K, double gscale) {
-  typed(T, torch::kFloat32, "T");
-  typed(C, torch::kFloat32, "C");
+  const bool bf = T.scalar_type() == torch::kBFloat16;
+  typed(T, bf ? torch::kBFloat16 : torch::kFloat32, "T");
+  typed(C, bf ? torch::kBFloat16 : torch::kFloat32, "C");
   typed(tinv, torch::kInt64, "tinv");
   typed(cinv, torch::kInt64, "cinv");
   TORCH_CHECK(T.dim() == 2 && C.dim() == 2 && T.size(1) == C.size(1), "T [*, D], C [*, D]");
@@ -310,14 +311,36 @@ std::vector<torch::Tensor> sgns_fwd_idx(torch::Tensor T, c10::optional<torch::Te
   const int64_t* tm = map_ptr(tmap, nTm, "tmap");
   const int64_t* cm = map_ptr(cmap, nCm, "cmap");
   const c10::DeviceGuard g(T.device());
-  auto fopt = T.options();
+  auto fopt = T.options().dtype(torch::kFloat32);
   auto coef = torch::empty({P, 1 + K}, fopt);
   auto loss_rows = torch::empty({P}, fopt);
-  ok(eh_sgns_fwd_idx(T.data_ptr<float>(), tm, nTm, tinv.data_ptr<int64_t>(), T.size(0), C.data_ptr<float>(), cm, nCm,
+  ok(eh_sgns_fwd_idx(T.data_ptr(), tm, nTm, tinv.data_ptr<int64_t>(), T.size(0), C.data_ptr(), cm, nCm,
                      cinv.data_ptr<int64_t>(), C.size(0), P, static_cast<int>(K), static_cast<int>(D),
-                     static_cast<float>(gscale), coef.data_ptr<float>(), loss_rows.data_ptr<float>(), stream()),
+                     static_cast<float>(gscale), coef.data_ptr<float>(), loss_rows.data_ptr<float>(), bf ? 1 : 0,
+                     stream()),
      "sgns_fwd_idx");
   return {coef, loss_rows};
+}
+
+// rows idx [n] (int64; < 0: zero row) of an fp32 table, packed as bf16 [n, D]
+torch::Tensor gather_f32_bf16(torch::Tensor x, torch::Tensor idx, c10::optional<torch::Tensor> out) {
+  typed(x, torch::kFloat32, "x");
+  typed(idx, torch::kInt64, "idx");
+  TORCH_CHECK(x.dim() == 2 && x.size(1) % 4 == 0, "x [rows, D], D % 4 == 0");
+  const int64_t n = idx.numel(), D = x.size(1);
+  torch::Tensor o;
+  if (out.has_value()) {
+    typed(*out, torch::kBFloat16, "out");
+    TORCH_CHECK(out->dim() == 2 && out->size(0) == n && out->size(1) == D, "out must be [n, D]");
+    o = *out;
+  } else {
+    o = torch::empty({n, D}, x.options().dtype(torch::kBFloat16));
+  }
+  const c10::DeviceGuard g(x.device());
+  ok(eh_gather_f32_bf16(x.data_ptr<float>(), x.size(0), static_cast<int>(D), idx.data_ptr<int64_t>(), n, o.data_ptr(),
+                        stream()),
+     "gather_f32_bf16");
+  return o;
 }
 
 // occurrence lists of inv (values in [0, n_u)): ptr [n_u + 1] int64, list [n] int32
@@ -352,7 +375,7 @@ UpdIn upd_check(int64_t side, const torch::Tensor& ptr, const torch::Tensor& lis
   typed(ptr, torch::kInt64, "ptr");
   typed(list, torch::kInt32, "list");
   typed(coef, torch::kFloat32, "coef");
-  typed(src, torch::kFloat32, "src");
+  typed(src, src.scalar_type() == torch::kBFloat16 ? torch::kBFloat16 : torch::kFloat32, "src");
   typed(sinv, torch::kInt64, "sinv");
   TORCH_CHECK(coef.dim() == 2 && coef.size(1) == K + 1 && K >= (side == 1 ? 1 : 0), "coef must be [P, 1+K]");
   TORCH_CHECK(src.dim() == 2 && src.size(1) % 4 == 0 && src.size(1) <= 256, "src [*, D], D % 4 == 0, D <= 256");
@@ -376,15 +399,16 @@ torch::Tensor sgns_grad(int64_t side, torch::Tensor ptr, torch::Tensor list, tor
   const int64_t D = src.size(1);
   torch::Tensor gout;
   if (out.has_value()) {
-    typed(*out, torch::kFloat32, "out");
+    typed(*out, out->scalar_type() == torch::kBFloat16 ? torch::kBFloat16 : torch::kFloat32, "out");
     TORCH_CHECK(out->dim() == 2 && out->size(0) == u.n_u && out->size(1) == D, "out must be [n_u, D]");
     gout = *out;
   } else {
-    gout = torch::zeros({u.n_u, D}, src.options());
+    gout = torch::zeros({u.n_u, D}, src.options().dtype(torch::kFloat32));
   }
+  const int sbf = src.scalar_type() == torch::kBFloat16, gbf = gout.scalar_type() == torch::kBFloat16;
   ok(eh_sgns_update(static_cast<int>(side), u.n_u, ptr.data_ptr<int64_t>(), list.data_ptr<int32_t>(),
-                    coef.data_ptr<float>(), u.P, static_cast<int>(K), static_cast<int>(D), src.data_ptr<float>(),
-                    src.size(0), u.smap, u.n_smap, sinv.data_ptr<int64_t>(), gout.data_ptr<float>(), nullptr, nullptr,
+                    coef.data_ptr<float>(), u.P, static_cast<int>(K), static_cast<int>(D), src.data_ptr(), sbf,
+                    src.size(0), u.smap, u.n_smap, sinv.data_ptr<int64_t>(), gout.data_ptr(), gbf, nullptr, nullptr,
                     nullptr, nullptr, 0, nullptr, 0, 0.f, 0.f, 0.f, 0.f, 2, stream()),
      "sgns_grad");
   return gout;
@@ -410,8 +434,8 @@ void sgns_apply_(int64_t side, torch::Tensor ptr, torch::Tensor list, torch::Ten
   const c10::DeviceGuard g(src.device());
   ok(eh_sgns_update(static_cast<int>(side), u.n_u, ptr.data_ptr<int64_t>(), list.data_ptr<int32_t>(),
                     coef.data_ptr<float>(), u.P, static_cast<int>(K), static_cast<int>(src.size(1)),
-                    src.data_ptr<float>(), src.size(0), u.smap, u.n_smap, sinv.data_ptr<int64_t>(), nullptr,
-                    table.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), rp, table.size(0),
+                    src.data_ptr(), src.scalar_type() == torch::kBFloat16 ? 1 : 0, src.size(0), u.smap, u.n_smap,
+                    sinv.data_ptr<int64_t>(), nullptr, 0, table.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), rp, table.size(0),
                     step.data_ptr<int64_t>(), inc_step ? 1 : 0, static_cast<float>(lr), static_cast<float>(b1),
                     static_cast<float>(b2),
                     static_cast<float>(eps), static_cast<int>(kind), stream()),
@@ -626,6 +650,7 @@ void register_gnn_ops(pybind11::module& m) {
   m.def("sgns_fwd_idx", &sgns_fwd_idx);
   m.def("occ_csr", &occ_csr);
   m.def("sgns_grad", &sgns_grad);
+  m.def("gather_f32_bf16", &gather_f32_bf16, py::arg("x"), py::arg("idx"), py::arg("out") = py::none());
   m.def("sgns_apply_", &sgns_apply_);
   m.def("kg_fwd", &kg_fwd);
   m.def("kg_bwd", &kg_bwd);

@@ -171,15 +171,33 @@ __device__ __forceinline__ void load_row4(const float* __restrict__ base, int64_
     x[0] = x[1] = x[2] = x[3] = 0.f;
   }
 }
+typedef uint32_t tl2u __attribute__((ext_vector_type(2)));  // 4 bf16 = one 8-byte load
+
+// fp32 or bf16 rows (bf: the exchanged rows of a sharded table stay in the bf16 wire dtype)
+__device__ __forceinline__ void load_row4v(const void* __restrict__ base, int bf, int64_t r, int D, int d, float* x) {
+  if (!bf) {
+    load_row4(static_cast<const float*>(base), r, D, d, x);
+    return;
+  }
+  if (r >= 0) {
+    const tl2u v = *reinterpret_cast<const tl2u*>(static_cast<const bf16_t*>(base) + r * D + d);
+    x[0] = bf2f(static_cast<bf16_t>(v[0] & 0xffffu));
+    x[1] = bf2f(static_cast<bf16_t>(v[0] >> 16));
+    x[2] = bf2f(static_cast<bf16_t>(v[1] & 0xffffu));
+    x[3] = bf2f(static_cast<bf16_t>(v[1] >> 16));
+  } else {
+    x[0] = x[1] = x[2] = x[3] = 0.f;
+  }
+}
 
 // context occurrence index of slot s (0 = positive) of pair p
 __device__ __forceinline__ int64_t ctx_occ(int64_t p, int s, int64_t P, int K) {
   return s == 0 ? p : P + p * K + (s - 1);
 }
 
-__global__ __launch_bounds__(256) void sgns_fwd_idx_kernel(const float* __restrict__ T, const int64_t* __restrict__ tmap,
+__global__ __launch_bounds__(256) void sgns_fwd_idx_kernel(const void* __restrict__ T, const int64_t* __restrict__ tmap,
                                                            int64_t nTm, const int64_t* __restrict__ tinv, int64_t nT,
-                                                           const float* __restrict__ C,
+                                                           const void* __restrict__ C, int bf,
                                                            const int64_t* __restrict__ cmap, int64_t nCm,
                                                            const int64_t* __restrict__ cinv, int64_t nC, int64_t P,
                                                            int K, int D,
@@ -189,7 +207,7 @@ __global__ __launch_bounds__(256) void sgns_fwd_idx_kernel(const float* __restri
   const bool ok = L.ok && L.sub * 4 < D;
   const int d = L.sub * 4;
   float e[4] = {0.f, 0.f, 0.f, 0.f};
-  if (ok) load_row4(T, occ_row(tmap, nTm, tinv, L.row, nT), D, d, e);
+  if (ok) load_row4v(T, bf, occ_row(tmap, nTm, tinv, L.row, nT), D, d, e);
   float loss = 0.f;
   // SG context rows per round: their index chains and row loads are all in flight together
   constexpr int SG = 4;
@@ -200,7 +218,7 @@ __global__ __launch_bounds__(256) void sgns_fwd_idx_kernel(const float* __restri
     for (int j = 0; j < SG; ++j)
       r[j] = ok && s0 + j <= K ? occ_row(cmap, nCm, cinv, ctx_occ(L.row, s0 + j, P, K), nC) : -1;
 #pragma unroll
-    for (int j = 0; j < SG; ++j) load_row4(C, r[j], D, d, c[j]);
+    for (int j = 0; j < SG; ++j) load_row4v(C, bf, r[j], D, d, c[j]);
 #pragma unroll
     for (int j = 0; j < SG; ++j) {
       const int s = s0 + j;
@@ -231,10 +249,10 @@ struct SgnsUpd {
   const int64_t* ptr;   // [n_u + 1]
   const int* list;      // occurrence ids
   const float* coef;    // [P, K + 1]
-  const float* src;     // rows the gradient is built from
+  const void* src;      // rows the gradient is built from (fp32, or bf16 when src_bf16)
   const int64_t* smap;  // unique id -> src row (null = identity)
   const int64_t* sinv;  // occurrence -> unique id of the OTHER table (side 0: context occ, side 1: target occ)
-  float* gout;          // [n_u, D] or null (apply the optimizer instead)
+  void* gout;           // [n_u, D] (fp32, or bf16 when gout_bf16) or null (apply the optimizer instead)
   float* table;
   float* m;
   float* v;
@@ -243,6 +261,7 @@ struct SgnsUpd {
   int64_t n_u, P, n_rows, n_src, n_smap;
   int K, D, lp, side, kind;
   float lr, b1, b2, eps;
+  int src_bf16, gout_bf16;
 };
 
 __global__ __launch_bounds__(256) void sgns_update_kernel(SgnsUpd a) {
@@ -277,7 +296,7 @@ __global__ __launch_bounds__(256) void sgns_update_kernel(SgnsUpd a) {
         for (int j = 0; j < SG; ++j)
           rr[j] = s0 + j < KK ? occ_row(a.smap, a.n_smap, a.sinv, ctx_occ(o, s0 + j, a.P, a.K), a.n_src) : -1;
 #pragma unroll
-        for (int j = 0; j < SG; ++j) load_row4(a.src, rr[j], a.D, d, c[j]);
+        for (int j = 0; j < SG; ++j) load_row4v(a.src, a.src_bf16, rr[j], a.D, d, c[j]);
 #pragma unroll
         for (int j = 0; j < SG; ++j) {
           const float w = s0 + j < KK ? a.coef[o * KK + s0 + j] : 0.f;
@@ -299,7 +318,7 @@ __global__ __launch_bounds__(256) void sgns_update_kernel(SgnsUpd a) {
       }
       float e[4];
       const float w = a.coef[pp * KK + s];
-      load_row4(a.src, occ_row(a.smap, a.n_smap, a.sinv, pp, a.n_src), a.D, d, e);
+      load_row4v(a.src, a.src_bf16, occ_row(a.smap, a.n_smap, a.sinv, pp, a.n_src), a.D, d, e);
 #pragma unroll
       for (int k = 0; k < 4; ++k) g[k] += w * e[k];
     }
@@ -307,7 +326,16 @@ __global__ __launch_bounds__(256) void sgns_update_kernel(SgnsUpd a) {
   if (!apply) {
     // rows without occurrences on this side are left untouched: two launches (target and
     // context side) can fill one buffer whose rows each belong to exactly one side
-    if (end > beg) EV<float>::store(a.gout + L.row * a.D + d, g);
+    if (end > beg) {
+      if (a.gout_bf16) {
+        tl2u v;
+        v[0] = pack_bf16x2(g[0], g[1]);
+        v[1] = pack_bf16x2(g[2], g[3]);
+        *reinterpret_cast<tl2u*>(static_cast<bf16_t*>(a.gout) + L.row * a.D + d) = v;
+      } else {
+        EV<float>::store(static_cast<float*>(a.gout) + L.row * a.D + d, g);
+      }
+    }
     return;
   }
   const int64_t off = r * a.D + d;
@@ -499,6 +527,23 @@ inline dim3 row_grid(int64_t rows, int lp) {
   return dim3(static_cast<uint32_t>((waves + 3) / 4));
 }
 
+__global__ __launch_bounds__(256) void gather_f32_bf16_kernel(const float* __restrict__ x, int64_t n_rows, int D,
+                                                              const int64_t* __restrict__ idx, int64_t n,
+                                                              bf16_t* __restrict__ out) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int D4 = D >> 2;
+  if (t >= n * D4) return;
+  const int64_t e = t / D4;
+  const int d = static_cast<int>(t - e * D4) * 4;
+  const int64_t r = idx[e];
+  float4_t v = {0.f, 0.f, 0.f, 0.f};
+  if (r >= 0 && r < n_rows) v = *reinterpret_cast<const float4_t*>(x + r * D + d);
+  tl2u w;
+  w[0] = pack_bf16x2(v[0], v[1]);
+  w[1] = pack_bf16x2(v[2], v[3]);
+  *reinterpret_cast<tl2u*>(out + e * D + d) = w;
+}
+
 }  // namespace euler_hip
 
 using namespace euler_hip;
@@ -578,14 +623,15 @@ hipError_t eh_kg_bwd(const float* ent, const float* rel, const int64_t* src, con
   return hipGetLastError();
 }
 
-hipError_t eh_sgns_fwd_idx(const float* T, const int64_t* tmap, int64_t nTm, const int64_t* tinv, int64_t nT,
-                           const float* C, const int64_t* cmap, int64_t nCm, const int64_t* cinv, int64_t nC,
+hipError_t eh_sgns_fwd_idx(const void* T, const int64_t* tmap, int64_t nTm, const int64_t* tinv, int64_t nT,
+                           const void* C, const int64_t* cmap, int64_t nCm, const int64_t* cinv, int64_t nC,
                            int64_t P, int K, int D,
-                           float gscale, float* coef, float* loss_rows, hipStream_t s) {
+                           float gscale, float* coef, float* loss_rows, int rows_bf16, hipStream_t s) {
   if (P == 0) return hipSuccess;
   if (D % 4 != 0 || D / 4 > 64 || K < 0) return hipErrorInvalidValue;
   const int lp = row_lanes(D / 4);
-  hipLaunchKernelGGL(sgns_fwd_idx_kernel, row_grid(P, lp), dim3(256), 0, s, T, tmap, nTm, tinv, nT, C, cmap, nCm, cinv, nC,
+  hipLaunchKernelGGL(sgns_fwd_idx_kernel, row_grid(P, lp), dim3(256), 0, s, T, tmap, nTm, tinv, nT, C, rows_bf16, cmap,
+                     nCm, cinv, nC,
                      P, K,
                      D, lp, gscale, coef, loss_rows);
   return hipGetLastError();
@@ -599,10 +645,10 @@ hipError_t eh_occ_fill(const int64_t* inv, int64_t n, const int64_t* ptr, int* c
 }
 
 hipError_t eh_sgns_update(int side, int64_t n_u, const int64_t* ptr, const int* list, const float* coef, int64_t P,
-                          int K, int D, const float* src, int64_t n_src, const int64_t* smap, int64_t n_smap,
-                          const int64_t* sinv, float* gout, float* table, float* m, float* v, const int64_t* rows,
-                          int64_t n_rows, int64_t* step, int inc_step, float lr, float b1, float b2, float eps,
-                          int kind, hipStream_t s) {
+                          int K, int D, const void* src, int src_bf16, int64_t n_src, const int64_t* smap,
+                          int64_t n_smap, const int64_t* sinv, void* gout, int gout_bf16, float* table, float* m,
+                          float* v, const int64_t* rows, int64_t n_rows, int64_t* step, int inc_step, float lr,
+                          float b1, float b2, float eps, int kind, hipStream_t s) {
   if (D % 4 != 0 || D / 4 > 64 || (side != 0 && side != 1) || (side == 1 && K < 0) || kind < 0 || kind > 2)
     return hipErrorInvalidValue;
   if (!gout && inc_step) hipLaunchKernelGGL(sgns_step_inc_kernel, dim3(1), dim3(1), 0, s, step);
@@ -634,7 +680,21 @@ hipError_t eh_sgns_update(int side, int64_t n_u, const int64_t* ptr, const int* 
   a.b1 = b1;
   a.b2 = b2;
   a.eps = eps;
+  a.src_bf16 = src_bf16;
+  a.gout_bf16 = gout_bf16;
   hipLaunchKernelGGL(sgns_update_kernel, row_grid(n_u, a.lp), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+// rows idx of an fp32 table as bf16 (idx < 0: a zero row): the sharded-table exchange
+// packs its send buffer in the wire dtype in the gather itself
+hipError_t eh_gather_f32_bf16(const float* x, int64_t n_rows, int D, const int64_t* idx, int64_t n, void* out,
+                              hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (D % 4 != 0) return hipErrorInvalidValue;
+  const int64_t tot = n * (D / 4);
+  hipLaunchKernelGGL(gather_f32_bf16_kernel, dim3(static_cast<uint32_t>(ceil_div(tot, 256))), dim3(256), 0, s, x,
+                     n_rows, D, idx, n, static_cast<bf16_t*>(out));
   return hipGetLastError();
 }
 

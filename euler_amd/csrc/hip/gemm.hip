@@ -18,7 +18,7 @@
 
 namespace euler_hip {
 
-constexpr int kGmT = 64, kGmK = 32, kGmLd = kGmK + 8;  // tile, k step, LDS row (bf16, +16 B pad)
+constexpr int kGmT = 64, kGmK = 64, kGmLd = kGmK + 8;  // tile, k step, LDS row (bf16, +16 B pad)
 
 struct GemmArgs {
   const void* A;
@@ -72,8 +72,9 @@ __device__ __forceinline__ void gm_load8(const void* X, int bf, int t, int64_t l
 }
 
 // one 64 x 64 output tile (a K range for split-K); 4 waves, wave w: rows (w >> 1) * 32,
-// columns (w & 1) * 32 as 2 x 2 MFMA tiles.  Operand staging: thread t owns row t >> 2,
-// k chunk (t & 3) * 8 of both the A and the B tile.
+// columns (w & 1) * 32 as 2 x 2 MFMA tiles, two 32-deep MFMA k-steps per 64-deep stage.
+// Operand staging: thread t owns row t >> 2, k chunk (t & 3) * 16 of both the A and the B
+// tile (4 x 8 values in flight per thread and stage).
 __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t As[2][kGmT * kGmLd];
   __shared__ __attribute__((aligned(16))) bf16_t Bs[2][kGmT * kGmLd];
@@ -82,15 +83,19 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
   const int split = blockIdx.z;
   const int64_t kb = static_cast<int64_t>(split) * a.kps;
   const int64_t ke = kb + a.kps < a.K ? kb + a.kps : a.K;
-  const int sr = tid >> 2, sk = (tid & 3) * 8;
-  float va[8], vb[8];
+  const int sr = tid >> 2, sk = (tid & 3) * 16;
+  float va[16], vb[16];
   auto fetch = [&](int64_t k0) {
     gm_load8(a.A, a.a_bf16, a.a_t, a.lda, a.M, ke, m0 + sr, k0 + sk, va);
+    gm_load8(a.A, a.a_bf16, a.a_t, a.lda, a.M, ke, m0 + sr, k0 + sk + 8, va + 8);
     gm_load8(a.B, a.b_bf16, a.b_t, a.ldb, a.N, ke, n0 + sr, k0 + sk, vb);
+    gm_load8(a.B, a.b_bf16, a.b_t, a.ldb, a.N, ke, n0 + sr, k0 + sk + 8, vb + 8);
   };
   auto stage = [&](int buf) {
     *reinterpret_cast<uint4_t*>(&As[buf][sr * kGmLd + sk]) = pack_bf16x8(va);
+    *reinterpret_cast<uint4_t*>(&As[buf][sr * kGmLd + sk + 8]) = pack_bf16x8(va + 8);
     *reinterpret_cast<uint4_t*>(&Bs[buf][sr * kGmLd + sk]) = pack_bf16x8(vb);
+    *reinterpret_cast<uint4_t*>(&Bs[buf][sr * kGmLd + sk + 8]) = pack_bf16x8(vb + 8);
   };
   float4_t acc[2][2];
   tl_zero(acc);
@@ -104,16 +109,19 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
     for (int64_t k0 = kb; k0 < ke; k0 += kGmK) {
       const bool more = k0 + kGmK < ke;
       if (more) fetch(k0 + kGmK);  // next k step in flight during this one's MFMAs
-      uint4_t fa[2], fb[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        fa[i] = *reinterpret_cast<const uint4_t*>(&As[buf][(wr + i * 16 + lr) * kGmLd + lk]);
-        fb[i] = *reinterpret_cast<const uint4_t*>(&Bs[buf][(wc + i * 16 + lr) * kGmLd + lk]);
+      for (int ks = 0; ks < kGmK; ks += 32) {
+        uint4_t fa[2], fb[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          fa[i] = *reinterpret_cast<const uint4_t*>(&As[buf][(wr + i * 16 + lr) * kGmLd + ks + lk]);
+          fb[i] = *reinterpret_cast<const uint4_t*>(&Bs[buf][(wc + i * 16 + lr) * kGmLd + ks + lk]);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(fa[i], fb[j], acc[i][j]);
       }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(fa[i], fb[j], acc[i][j]);
       if (more) {
         stage(buf ^ 1);
         __syncthreads();
@@ -156,7 +164,16 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(GemmArgs a) {
   if (i >= a.M * a.N) return;
   const int64_t row = i / a.N, col = i - row * a.N;
   float v = 0.f;
-  for (int s = 0; s < a.splits; ++s) v += a.part[static_cast<int64_t>(s) * a.M * a.N + i];
+  const int64_t MN = a.M * a.N;
+  int s = 0;
+  for (; s + 8 <= a.splits; s += 8) {  // 8 slab loads in flight
+    float t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = a.part[(s + u) * MN + i];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v += t[u];
+  }
+  for (; s < a.splits; ++s) v += a.part[s * MN + i];
   if (a.bias) v += a.bias[col];
   if (a.relu) v = fmaxf(v, 0.f);
   if (a.rmask) {

@@ -90,16 +90,18 @@ hipError_t eh_sgns_fwd(const void* emb, const void* pos, const void* neg, int is
                        float* logits, float* loss_rows, hipStream_t s);
 hipError_t eh_sgns_bwd(const void* emb, const void* pos, const void* neg, int is_bf16, int64_t B, int P, int K, int D,
                        const float* logits, float gscale, void* demb, void* dpos, void* dneg, hipStream_t s);
-hipError_t eh_sgns_fwd_idx(const float* T, const int64_t* tmap, int64_t nTm, const int64_t* tinv, int64_t nT,
-                           const float* C, const int64_t* cmap, int64_t nCm, const int64_t* cinv, int64_t nC,
+hipError_t eh_sgns_fwd_idx(const void* T, const int64_t* tmap, int64_t nTm, const int64_t* tinv, int64_t nT,
+                           const void* C, const int64_t* cmap, int64_t nCm, const int64_t* cinv, int64_t nC,
                            int64_t P, int K, int D,
-                           float gscale, float* coef, float* loss_rows, hipStream_t s);
+                           float gscale, float* coef, float* loss_rows, int rows_bf16, hipStream_t s);
+hipError_t eh_gather_f32_bf16(const float* x, int64_t n_rows, int D, const int64_t* idx, int64_t n, void* out,
+                              hipStream_t s);
 hipError_t eh_occ_fill(const int64_t* inv, int64_t n, const int64_t* ptr, int* cursor, int* list, hipStream_t s);
 hipError_t eh_sgns_update(int side, int64_t n_u, const int64_t* ptr, const int* list, const float* coef, int64_t P,
-                          int K, int D, const float* src, int64_t n_src, const int64_t* smap, int64_t n_smap,
-                          const int64_t* sinv, float* gout, float* table, float* m, float* v, const int64_t* rows,
-                          int64_t n_rows, int64_t* step, int inc_step, float lr, float b1, float b2, float eps,
-                          int kind, hipStream_t s);
+                          int K, int D, const void* src, int src_bf16, int64_t n_src, const int64_t* smap,
+                          int64_t n_smap, const int64_t* sinv, void* gout, int gout_bf16, float* table, float* m,
+                          float* v, const int64_t* rows, int64_t n_rows, int64_t* step, int inc_step, float lr,
+                          float b1, float b2, float eps, int kind, hipStream_t s);
 hipError_t eh_kg_fwd(const float* ent, const float* rel, const int64_t* src, const int64_t* dst, const int64_t* ridx,
                      const int64_t* neg, int64_t B, int K, int D, int kind, int corrupt, int normalize,
                      float* pos_score, float* neg_score, hipStream_t s);
@@ -128,7 +130,7 @@ hipError_t eh_unique_finalize(const int64_t* x, int64_t n, const int32_t* slot, 
 // optim.hip
 hipError_t eh_flat_optim(float* p, const float* g, float* m, float* v, int64_t n, int64_t* step, float lr, float b1,
                          float b2, float eps, float wd, float grad_scale, int kind, hipStream_t s);
-hipError_t eh_sparse_optim(float* table, float* m, float* v, const int64_t* rows, const float* grads, int64_t n, int D,
-                           int64_t n_rows, int64_t* step, float lr, float b1, float b2, float eps, int kind,
-                           hipStream_t s);
+hipError_t eh_sparse_optim(float* table, float* m, float* v, const int64_t* rows, const void* grads, int grads_bf16,
+                           int64_t n, int D, int64_t n_rows, int64_t* step, float lr, float b1, float b2, float eps,
+                           int kind, hipStream_t s);
 }

@@ -87,11 +87,21 @@ __global__ __launch_bounds__(256) void flat_optim4_kernel(float* __restrict__ p,
 
 __global__ void step_inc_kernel(int64_t* step) { step[0] += 1; }
 
+__device__ __forceinline__ float4_t load_grad4(const float* g) { return *reinterpret_cast<const float4_t*>(g); }
+__device__ __forceinline__ float4_t load_grad4(const bf16_t* g) {
+  const uint32_t* u = reinterpret_cast<const uint32_t*>(g);
+  const uint32_t a = u[0], b = u[1];
+  return float4_t{bf2f(static_cast<bf16_t>(a & 0xffffu)), bf2f(static_cast<bf16_t>(a >> 16)),
+                  bf2f(static_cast<bf16_t>(b & 0xffffu)), bf2f(static_cast<bf16_t>(b >> 16))};
+}
+
 // float4 form of sparse_optim_kernel for D % 4 == 0: 16-byte loads/stores of the table,
-// slots and grads (a quarter of the threads, 4x the bytes in flight per thread)
+// slots and grads (a quarter of the threads, 4x the bytes in flight per thread); GT =
+// bf16 takes the gradients straight from a bf16 exchange buffer
+template <typename GT>
 __global__ __launch_bounds__(256) void sparse_optim4_kernel(float* __restrict__ table, float* __restrict__ m,
                                                             float* __restrict__ v, const int64_t* __restrict__ rows,
-                                                            const float* __restrict__ grads, int64_t n, int D,
+                                                            const GT* __restrict__ grads, int64_t n, int D,
                                                             int64_t n_rows, const int64_t* __restrict__ step, float lr,
                                                             float b1, float b2, float eps, int kind) {
   const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -102,7 +112,7 @@ __global__ __launch_bounds__(256) void sparse_optim4_kernel(float* __restrict__ 
   const int64_t r = rows[e];
   if (r < 0 || r >= n_rows) return;
   const int64_t o = r * D + d;
-  const float4_t gi = *reinterpret_cast<const float4_t*>(grads + e * D + d);
+  const float4_t gi = load_grad4(grads + e * D + d);
   float4_t p = *reinterpret_cast<float4_t*>(table + o);
   if (kind == 0) {
     const float st = static_cast<float>(step[0]);
@@ -187,18 +197,24 @@ hipError_t eh_flat_optim(float* p, const float* g, float* m, float* v, int64_t n
   return hipGetLastError();
 }
 
-hipError_t eh_sparse_optim(float* table, float* m, float* v, const int64_t* rows, const float* grads, int64_t n, int D,
-                           int64_t n_rows, int64_t* step, float lr, float b1, float b2, float eps, int kind,
-                           hipStream_t s) {
+hipError_t eh_sparse_optim(float* table, float* m, float* v, const int64_t* rows, const void* grads, int grads_bf16,
+                           int64_t n, int D, int64_t n_rows, int64_t* step, float lr, float b1, float b2, float eps,
+                           int kind, hipStream_t s) {
   hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, s, step);
   if (n == 0 || D == 0) return hipGetLastError();
+  if (grads_bf16 && D % 4 != 0) return hipErrorInvalidValue;
   if (D % 4 == 0) {
-    hipLaunchKernelGGL(sparse_optim4_kernel, dim3(static_cast<uint32_t>(ceil_div(n * (D / 4), 256))), dim3(256), 0,
-                       s, table, m, v, rows, grads, n, D, n_rows, step, lr, b1, b2, eps, kind);
+    const dim3 grid(static_cast<uint32_t>(ceil_div(n * (D / 4), 256)));
+    if (grads_bf16)
+      hipLaunchKernelGGL(sparse_optim4_kernel<bf16_t>, grid, dim3(256), 0, s, table, m, v, rows,
+                         static_cast<const bf16_t*>(grads), n, D, n_rows, step, lr, b1, b2, eps, kind);
+    else
+      hipLaunchKernelGGL(sparse_optim4_kernel<float>, grid, dim3(256), 0, s, table, m, v, rows,
+                         static_cast<const float*>(grads), n, D, n_rows, step, lr, b1, b2, eps, kind);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(sparse_optim_kernel, dim3(static_cast<uint32_t>(ceil_div(n * D, 256))), dim3(256), 0, s, table,
-                     m, v, rows, grads, n, D, n_rows, step, lr, b1, b2, eps, kind);
+                     m, v, rows, static_cast<const float*>(grads), n, D, n_rows, step, lr, b1, b2, eps, kind);
   return hipGetLastError();
 }
 

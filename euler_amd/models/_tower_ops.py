@@ -15,22 +15,52 @@ sigmoid cross-entropy (mean over the B + B*K logits, the reference's
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
+
+
+# products of the tower heads: "gemm" = the tiled MFMA kernel (gemm.hip), "torch" = torch
+# matmuls (hipBLASLt; fp32 A1); "mixed" = the kernel for the row-parallel products, torch
+# for the [R]-row weight-gradient reductions
+_HEAD_GEMM = os.environ.get("EULER_AMD_TOWER_GEMM", "mixed")
+
+
+def _mm(a, b, out=None, trans_a=False, trans_b=False, relu=False, bias=None, rmask=None, wgrad=False):
+    from euler_amd.ops.gnn_ops import _gemm_splits, gemm
+
+    use = _HEAD_GEMM == "gemm" or (_HEAD_GEMM == "mixed" and not wgrad)
+    if use:
+        splits = 1
+        if wgrad:
+            M, N = (a.shape[1] if trans_a else a.shape[0]), (b.shape[0] if trans_b else b.shape[1])
+            splits = _gemm_splits(a.shape[0], -(-M // 64) * -(-N // 64))
+        return gemm(a, b, out=out, trans_a=trans_a, trans_b=trans_b, relu=relu, bias=bias, rmask=rmask,
+                    splits=splits)
+    A = (a.t() if trans_a else a).float()
+    B = (b.t() if trans_b else b).float()
+    y = torch.addmm(bias, A, B) if bias is not None else A @ B
+    if relu:
+        y = torch.relu_(y)
+    if rmask is not None:
+        y = torch.ops.aten.threshold_backward(y, rmask, 0.0)
+    if out is None:
+        return y
+    out.copy_(y)
+    return out
 
 
 class _TowerHead(torch.autograd.Function):
     @staticmethod
     def forward(ctx, W0, W1, Wfc, bfc, tower):
-        from euler_amd.ops.gnn_ops import gemm
-
         p = tower.plan
         p.shadow()
         p.sample()
         p.fwd()
         A1 = tower.A1.view(tower.R, 2 * tower.H0)  # bf16 rows [self | mean] from layer 0
-        h1 = gemm(A1, W1, trans_b=True, relu=True)
-        e = gemm(h1, Wfc, trans_b=True, bias=bfc)
+        h1 = _mm(A1, W1, trans_b=True, relu=True)
+        e = _mm(h1, Wfc, trans_b=True, bias=bfc)
         ctx.tower = tower
         ctx.params = (W1, Wfc, bfc)
         ctx.save_for_backward(A1, h1)
@@ -38,25 +68,19 @@ class _TowerHead(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, de):
-        from euler_amd.ops.gnn_ops import _gemm_splits, gemm
-
         A1, h1 = ctx.saved_tensors
         W1, Wfc, bfc = ctx.params
         t = ctx.tower
         de = de.contiguous()
         R = de.shape[0]
-        # weight gradients: split-K over the R rows, written into the flat-gradient views
-        gemm(de, h1, out=Wfc.grad, trans_a=True, splits=_gemm_splits(R, _tiles(Wfc)))
+        # weight gradients (reductions over the R rows) written into the flat-gradient views
+        _mm(de, h1, out=Wfc.grad, trans_a=True, wgrad=True)
         torch.sum(de, 0, out=bfc.grad)
-        dh1 = gemm(de, Wfc, rmask=h1)  # (de Wfc) * relu'(h1)
-        gemm(dh1, A1, out=W1.grad, trans_a=True, splits=_gemm_splits(R, _tiles(W1)))
-        gemm(dh1, W1, out=t.dA1.view(R, 2 * t.H0))
+        dh1 = _mm(de, Wfc, rmask=h1)  # (de Wfc) * relu'(h1)
+        _mm(dh1, A1, out=W1.grad, trans_a=True, wgrad=True)
+        _mm(dh1, W1, out=t.dA1.view(R, 2 * t.H0))
         t.plan.bwd()  # routed layer-0 dW, reduced into the W0 gradient view
         return None, None, None, None, None
-
-
-def _tiles(w):
-    return -(-w.shape[0] // 64) * -(-w.shape[1] // 64)
 
 
 def tower_head(W0, W1, Wfc, bfc, tower):

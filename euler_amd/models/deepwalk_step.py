@@ -162,7 +162,7 @@ class DeepWalkTrainer:
             ids = torch.cat([u_t, rows_c_id])
             # rows [W*C + 1, D]: the extra zero row is the trash slot of ids dropped by a
             # capacity overflow (pos = W*C), so they never alias a live slot
-            rows, h = tab.lookup_static(ids, trash_row=True)
+            rows, h = tab.lookup_static(ids, trash_row=True, keep_wire=True)
             n = rows.shape[0]
             tinv = h.pos[inv_t]
             cinv = h.pos[u_t.numel() + inv_c]
@@ -216,9 +216,9 @@ class DeepWalkTrainer:
         S = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
         if S is None:  # CPU (gloo): the same phases in order on one stream
             m0 = self._mb_front(self.batch // 2)
-            r0 = tab.exchange_static(m0["routed"], trash_row=True)
+            r0 = tab.exchange_static(m0["routed"], trash_row=True, keep_wire=True)
             m1 = self._mb_front(self.batch // 2)
-            r1 = tab.exchange_static(m1["routed"], trash_row=True)
+            r1 = tab.exchange_static(m1["routed"], trash_row=True, keep_wire=True)
             g0, l0, _ = self._mb_compute(m0, *r0)
             tab.apply_static(r0[1], g0)
             g1, l1, _ = self._mb_compute(m1, *r1)
@@ -241,14 +241,16 @@ class DeepWalkTrainer:
             X.wait_event(ev[0])
             m1 = self._mb_front(self.batch // 2)                               # X, under exchange 0
             ev[1].record(X)
-        r0 = tab.exchange_static(m0["routed"], trash_row=True, bufs=self._bufs[0])  # S
+        r0 = tab.exchange_static(m0["routed"], trash_row=True, bufs=self._bufs[0],
+                                keep_wire=True)  # S
         ev[2].record(S)
         with torch.cuda.stream(X):
             X.wait_event(ev[2])
             g0, l0, k0 = self._mb_compute(m0, *r0)                            # X, under exchange 1
             ev[3].record(X)
         S.wait_event(ev[1])
-        r1 = tab.exchange_static(m1["routed"], trash_row=True, bufs=self._bufs[1])  # S
+        r1 = tab.exchange_static(m1["routed"], trash_row=True, bufs=self._bufs[1],
+                                keep_wire=True)  # S
         S.wait_event(ev[3])
         ev[4].record(S)
         with torch.cuda.stream(X):

@@ -247,8 +247,9 @@ def gemm(a, b, out=None, trans_a=False, trans_b=False, bias=None, relu=False, rm
 
 def _gemm_splits(k_rows, tiles):
     """split-K count for a weight-gradient product over k_rows rows with `tiles` 64x64
-    output tiles: about 256 workgroups, at least 256 rows per split"""
-    return int(max(1, min(64, k_rows // 256, -(-256 // max(tiles, 1)))))
+    output tiles: about 256 workgroups, at least 512 rows (8 k-stages) per split, at most 32
+    slabs for the reduce"""
+    return int(max(1, min(32, k_rows // 512, -(-256 // max(tiles, 1)))))
 
 
 class _Linear(torch.autograd.Function):
@@ -747,7 +748,7 @@ def sgns_grad(side, ptr, lst, coef, K, src, smap, sinv, inv_self=None, out=None)
     if out is None:
         return g
     has = ptr[1:] > ptr[:-1]
-    out[has] = g[has]
+    out[has] = g[has].to(out.dtype)
     return out
 
 

@@ -31,6 +31,11 @@ dropped unnoticed.  Expected traffic per step and rank with n ids of D fp32: ids
 ``wire_dtype="bf16"`` moves the row and gradient exchanges (both forms) as bf16: half the
 bytes on xGMI for the two large all-to-alls; the table, its optimizer slots and the
 update stay fp32 (rows are widened on arrival, gradients rounded once before sending).
+The fixed-capacity form can keep the wire dtype end to end (``keep_wire``): the owner
+gathers its fp32 rows straight into the bf16 send buffer (one converting gather kernel),
+the caller's kernels read the received bf16 rows and write bf16 gradients, and the
+row-sparse optimizer reads those gradients from the receive buffer — no fp32 copies of
+the W*C exchanged rows on either side (DeepWalk, models/deepwalk_step.py).
 """
 from __future__ import annotations
 
@@ -105,7 +110,7 @@ class ShardedTable:
         mean = n / self.world
         return min(int(n), int(math.ceil((mean + 6.0 * math.sqrt(mean) + 64) / 64.0)) * 64)
 
-    def lookup_static(self, ids: torch.Tensor, trash_row: bool = False):
+    def lookup_static(self, ids: torch.Tensor, trash_row: bool = False, keep_wire: bool = False):
         """rows [W*C, D] in slot order for padded DISTINCT ids [n] (-1 = none) and the
         :class:`StaticHandle`; row ``handle.pos[k]`` is the row of ``ids[k]``.  Shapes
         depend on n only: safe inside a hipGraph capture.
@@ -113,7 +118,8 @@ class ShardedTable:
         An id dropped by a capacity overflow gets ``pos = W*C``.  With ``trash_row`` the
         returned rows have one extra zero row at index W*C, so a dropped id reads zeros
         and a caller's gradient for it lands in that row (never in a live slot); pass only
-        the first W*C gradient rows to :meth:`apply_static`."""
+        the first W*C gradient rows to :meth:`apply_static`.  ``keep_wire``: rows in the
+        wire dtype (bf16 wire: no fp32 copy) when they went through a collective."""
         ids = ids.reshape(-1).long()
         n = ids.numel()
         extra = 1 if trash_row else 0
@@ -123,7 +129,7 @@ class ShardedTable:
             if extra:
                 rows = torch.cat([rows, rows.new_zeros(1, self.dim)])
             return rows, StaticHandle(pos, ids)
-        return self.exchange_static(self.route_static(ids), trash_row)
+        return self.exchange_static(self.route_static(ids), trash_row, keep_wire=keep_wire)
 
     def route_static(self, ids: torch.Tensor):
         """first half of :meth:`lookup_static` (no collective): the exchange slots of the
@@ -131,9 +137,10 @@ class ShardedTable:
         ids = ids.reshape(-1).long()
         return route_by_owner(ids, self.world, self.capacity(ids.numel()), self.overflow)
 
-    def exchange_static(self, routed, trash_row: bool = False, bufs=None):
+    def exchange_static(self, routed, trash_row: bool = False, bufs=None, keep_wire: bool = False):
         """second half of :meth:`lookup_static`: the id and row all-to-alls of routed ids
-        (``bufs``: persistent buffers for the collectives, see :meth:`_buf`)"""
+        (``bufs``: persistent buffers for the collectives, see :meth:`_buf`; ``keep_wire``:
+        return the received rows in the wire dtype)"""
         pos, send = routed
         W = self.world
         trash = send.numel() - 1
@@ -142,27 +149,32 @@ class ShardedTable:
         recv = self._buf(bufs, "recv", (trash,), torch.long, send.device)
         dist.all_to_all_single(recv, sd, group=self.group)
         local = torch.where(recv >= 0, torch.div(recv, W, rounding_mode="floor"), torch.full_like(recv, -1))
-        out = self._a2a_rows(self._gather(local), extra=1 if trash_row else 0, bufs=bufs, tag="rows_")
+        xw = self._buf(bufs, "rows_in", (trash, self.dim), self.wire, send.device)
+        self._gather_into(local, xw)
+        out = self._a2a_rows(xw, extra=1 if trash_row else 0, bufs=bufs, tag="rows_", keep_wire=keep_wire)
         return out, StaticHandle(pos, local)
 
     def apply_static(self, handle: StaticHandle, grad_rows: torch.Tensor, bufs=None):
         """row-sparse update from gradients [W*C, D] in slot order (rows of empty slots
-        are ignored)."""
-        g = grad_rows.float().contiguous()
+        are ignored).  fp32 or wire-dtype gradients; a bf16 wire sends them as they are
+        and the optimizer reads them from the receive buffer."""
+        g = grad_rows.contiguous()
+        if g.dtype not in (torch.float32, self.wire):
+            g = g.float()
         rows = handle.local
         if self.comm:
-            g = self._a2a_rows(g, bufs=bufs, tag="grad_")
+            g = self._a2a_rows(g, bufs=bufs, tag="grad_", keep_wire=True)
             if self.world > 1:
                 # several ranks may have asked for the same row: merge (the -1 bucket of
                 # empty slots collects their rows and is skipped by the update)
                 from euler_amd.ops.gnn_ops import unique_first_padded
 
                 rows_u, inv, _ = unique_first_padded(rows)
-                acc = torch.zeros_like(g)
+                acc = torch.zeros(g.shape, dtype=torch.float32, device=g.device)
                 if use_hip(acc, inv):
                     hip().index_add_rows_(acc, inv.contiguous(), g)
                 else:
-                    acc.index_add_(0, inv, g)
+                    acc.index_add_(0, inv, g.float())
                 rows, g = rows_u, acc
         self._update(rows.contiguous(), g)
 
@@ -218,17 +230,28 @@ class ShardedTable:
             t = bufs[name] = torch.empty(shape, dtype=dtype, device=device)
         return t
 
-    def _a2a_rows(self, x, out_splits=None, in_splits=None, extra=0, bufs=None, tag=""):
-        """all-to-all of [*, D] rows in the wire dtype; returns fp32 rows (plus ``extra``
-        zero rows at the end)"""
-        xw = self._buf(bufs, tag + "in", (x.shape[0], self.dim), self.wire, x.device)
-        xw.copy_(x)
+    def _a2a_rows(self, x, out_splits=None, in_splits=None, extra=0, bufs=None, tag="", keep_wire=False):
+        """all-to-all of [*, D] rows in the wire dtype; returns fp32 rows (``keep_wire``:
+        the wire-dtype receive buffer) plus ``extra`` zero rows at the end.  Rows already
+        in the wire dtype are sent as they are."""
+        if x.dtype == self.wire and x.is_contiguous():
+            xw = x
+        else:
+            xw = self._buf(bufs, tag + "in", (x.shape[0], self.dim), self.wire, x.device)
+            xw.copy_(x)
         n = xw.shape[0] if out_splits is None else sum(out_splits)
         out = self._buf(bufs, tag + "out", (n + extra, self.dim), self.wire, xw.device)
         if extra:
             out[n:].zero_()
         dist.all_to_all_single(out[:n], xw, out_splits, in_splits, group=self.group)
-        return out.float()
+        return out if keep_wire else out.float()
+
+    def _gather_into(self, local, out):
+        """``out[k] = weight[local[k]]`` in out's dtype (local < 0: a zero row)"""
+        if out.dtype == torch.bfloat16 and use_hip(self.weight, local) and self.dim % 4 == 0:
+            hip().gather_f32_bf16(self.weight, local.contiguous(), out)
+            return
+        out.copy_(self._gather(local))
 
     def _gather(self, local):
         if use_hip(self.weight, local):
@@ -259,6 +282,9 @@ class ShardedTable:
         self._update(rows.contiguous(), g)
 
     def _update(self, rows, g):
+        if g.dtype != torch.float32 and not (g.dtype == torch.bfloat16 and use_hip(self.weight, rows, g)
+                                             and self.dim % 4 == 0):
+            g = g.float()
         if use_hip(self.weight, rows, g):
             hip().sparse_optim_(self.weight, self.m, self.v, rows, g, self.step, self.lr, self.b1, self.b2,
                                 self.eps, self.kind)

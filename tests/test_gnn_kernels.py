@@ -439,6 +439,54 @@ def test_sgns_idx_kernels_match_cpu(cuda, kind):
 
 
 @pytest.mark.gpu
+def test_sgns_idx_bf16_rows_match_fp32(cuda):
+    """bf16 exchanged rows (sharded-table keep_wire path): the index-driven SGNS kernels
+    read bf16 rows and write bf16 gradients, the converting gather packs fp32 rows as bf16
+    and the row-sparse optimizer reads bf16 gradients — each against the fp32 composition
+    of the same (bf16-rounded) inputs."""
+    from euler_amd.ops._native import hip
+
+    K, D = 5, 64
+    T, C, src, ctx = _sgns_case("cpu", P=2000, K=K, D=D, n_t=300, n_c=900, seed=23)
+    Tb, Cb = T.bfloat16(), C.bfloat16()
+    P = src.numel()
+    gscale = 1.0 / (P * (1 + K))
+    u_t, inv_t = G.unique_first(src)
+    u_c, inv_c = G.unique_first(ctx)
+    coef, loss_rows = G.sgns_fwd_idx(Tb.float(), u_t, inv_t, Cb.float(), u_c, inv_c, K, gscale)
+    ptr_t, lst_t = G.occ_csr(inv_t, u_t.numel())
+    g_t = G.sgns_grad(0, ptr_t, lst_t, coef, K, Cb.float(), u_c, inv_c, inv_self=inv_t)
+    d = lambda *ts: [t.to(cuda) for t in ts]  # noqa: E731
+    Tg, Cg, ug_t, ig_t, ug_c, ig_c = d(Tb, Cb, u_t, inv_t, u_c, inv_c)
+    coef_g, loss_g = G.sgns_fwd_idx(Tg, ug_t, ig_t, Cg, ug_c, ig_c, K, gscale)
+    torch.testing.assert_close(coef_g.cpu(), coef, atol=1e-7, rtol=1e-4)
+    torch.testing.assert_close(loss_g.cpu(), loss_rows, atol=1e-4, rtol=1e-5)
+    pg, lg = G.occ_csr(ig_t, ug_t.numel())
+    out = torch.zeros(ug_t.numel(), D, dtype=torch.bfloat16, device=cuda)
+    G.sgns_grad(0, pg, lg, coef_g, K, Cg, ug_c, ig_c, out=out)
+    torch.testing.assert_close(out.float().cpu(), g_t, atol=1e-6, rtol=1e-2)
+    # converting gather: rows (and -1 -> zeros) of an fp32 table as bf16
+    x = torch.randn(500, D, device=cuda)
+    idx = torch.randint(-1, 500, (777,), device=cuda)
+    got = hip().gather_f32_bf16(x, idx)
+    want = torch.where((idx >= 0).unsqueeze(1), x[idx.clamp(min=0)], torch.zeros_like(x[:1])).bfloat16()
+    assert torch.equal(got, want)
+    # row-sparse Adam from bf16 gradients == from their fp32 widening
+    rows = torch.randperm(500, device=cuda)[:300]
+    rows[::7] = -1  # empty exchange slots are skipped
+    gb = torch.randn(300, D, device=cuda).bfloat16()
+    w0 = torch.randn(500, D, device=cuda)
+    res = []
+    for g in (gb, gb.float()):
+        w, m, v, st = w0.clone(), torch.zeros_like(w0), torch.zeros_like(w0), torch.zeros(1, dtype=torch.long,
+                                                                                             device=cuda)
+        hip().sparse_optim_(w, m, v, rows, g.contiguous(), st, 0.01, 0.9, 0.999, 1e-8, 0)
+        res.append((w, m, v))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_splitk_linear_grads_match(cuda, dtype):
     """Dense / fused-SAGE weight gradients as split-K batched GEMMs (gnn_ops.splitk_*)

@@ -54,6 +54,8 @@ for st in "${S[@]}"; do
           python -u tools/tree_kernels.py || exit $?
       done
       EULER_AMD_PIPELINE=0 run tree_kernels_nopipe 300 python -u tools/tree_kernels.py ;;
+    gemm_bench)
+      run gemm_bench 300 python -u tools/gemm_bench.py ;;
     sweep_fwd)
       for bm in 32 64 128; do
         EULER_AMD_FWD_BM=$bm run "tree_kernels_fbm$bm" 300 python -u tools/tree_kernels.py
@@ -247,6 +249,10 @@ for st in "${S[@]}"; do
       cat "$OUT/trace_bench_gaps.txt" "$OUT/trace_dist_gaps.txt" ;;
     unsup)
       run bench_unsup 900 python -u benchmarks/bench_unsup_sage.py ${UNSUP_ARGS:-} ;;
+    unsup_ab)
+      for m in mixed torch gemm; do
+        EULER_AMD_TOWER_GEMM=$m run "bench_unsup_$m" 600 python -u benchmarks/bench_unsup_sage.py --steps 1000 || exit $?
+      done ;;
     unsup_prof)
       run unsup_prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/unsup_prof" -o run --output-format csv -- \
           python3 benchmarks/bench_unsup_sage.py --steps 100 --eval-pairs 2000 ;;
