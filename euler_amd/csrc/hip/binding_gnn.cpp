@@ -343,6 +343,51 @@ torch::Tensor gather_f32_bf16(torch::Tensor x, torch::Tensor idx, c10::optional<
   return o;
 }
 
+// unsupervised pair objective: es [B, E] sources, ec [B + B K, E] contexts (B positives,
+// then the B x K negatives source-major) -> (logits [B, 1 + K], loss_part [B]); the
+// reciprocal ranks of the positives are added to mrr[0] when given
+std::vector<torch::Tensor> pair_fwd(torch::Tensor es, torch::Tensor ec, int64_t B, int64_t K,
+                                    c10::optional<torch::Tensor> mrr) {
+  typed(es, torch::kFloat32, "es");
+  typed(ec, torch::kFloat32, "ec");
+  TORCH_CHECK(es.dim() == 2 && ec.dim() == 2 && es.size(0) == B && ec.size(0) == B * (1 + K) &&
+                  es.size(1) == ec.size(1) && es.is_contiguous() && ec.is_contiguous(),
+              "pair_fwd: es [B, E], ec [B (1 + K), E], contiguous");
+  const int64_t E = es.size(1);
+  TORCH_CHECK(E % 4 == 0 && E <= 256 && K >= 0 && K <= 15, "pair_fwd: E % 4 == 0, E <= 256, K <= 15");
+  float* mp = nullptr;
+  if (mrr.has_value()) {
+    typed(*mrr, torch::kFloat32, "mrr");
+    TORCH_CHECK(mrr->numel() == 1, "mrr must hold one value");
+    mp = mrr->data_ptr<float>();
+  }
+  const c10::DeviceGuard g(es.device());
+  auto logits = torch::empty({B, 1 + K}, es.options());
+  auto loss_part = torch::empty({B}, es.options());
+  ok(eh_pair_fwd(es.data_ptr<float>(), ec.data_ptr<float>(), static_cast<int>(B), static_cast<int>(K),
+                 static_cast<int>(E), 1.f / static_cast<float>(B * (1 + K)), logits.data_ptr<float>(),
+                 loss_part.data_ptr<float>(), mp, stream()),
+     "pair_fwd");
+  return {logits, loss_part};
+}
+
+void pair_bwd(torch::Tensor es, torch::Tensor ec, int64_t B, int64_t K, torch::Tensor logits, torch::Tensor dloss,
+              torch::Tensor des, torch::Tensor dec) {
+  typed(logits, torch::kFloat32, "logits");
+  typed(dloss, torch::kFloat32, "dloss");
+  typed(des, torch::kFloat32, "des");
+  typed(dec, torch::kFloat32, "dec");
+  TORCH_CHECK(logits.numel() == B * (1 + K) && dloss.numel() == 1 && des.sizes() == es.sizes() &&
+                  dec.sizes() == ec.sizes() && des.is_contiguous() && dec.is_contiguous() && es.is_contiguous() &&
+                  ec.is_contiguous(),
+              "pair_bwd shapes");
+  const c10::DeviceGuard g(es.device());
+  ok(eh_pair_bwd(es.data_ptr<float>(), ec.data_ptr<float>(), static_cast<int>(B), static_cast<int>(K),
+                 static_cast<int>(es.size(1)), 1.f / static_cast<float>(B * (1 + K)), logits.data_ptr<float>(),
+                 dloss.data_ptr<float>(), des.data_ptr<float>(), dec.data_ptr<float>(), stream()),
+     "pair_bwd");
+}
+
 // occurrence lists of inv (values in [0, n_u)): ptr [n_u + 1] int64, list [n] int32
 std::vector<torch::Tensor> occ_csr(torch::Tensor inv, int64_t n_u) {
   typed(inv, torch::kInt64, "inv");
@@ -479,19 +524,25 @@ std::vector<torch::Tensor> kg_fwd(torch::Tensor ent, torch::Tensor rel, torch::T
 
 void kg_bwd(torch::Tensor ent, torch::Tensor rel, torch::Tensor src, torch::Tensor dst, torch::Tensor ridx,
             torch::Tensor neg, int64_t kind, int64_t corrupt, bool normalize, torch::Tensor gpos, torch::Tensor gneg,
-            torch::Tensor dent, torch::Tensor drel) {
+            torch::Tensor dent, torch::Tensor drel, bool occ) {
   const KgIn k = kg_check(ent, rel, src, dst, ridx, neg, kind, corrupt);
   typed(gpos, torch::kFloat32, "gpos");
   typed(gneg, torch::kFloat32, "gneg");
   typed(dent, torch::kFloat32, "dent");
   typed(drel, torch::kFloat32, "drel");
   TORCH_CHECK(gpos.numel() == k.B && gneg.numel() == k.B * k.nneg, "score grads must match the scores");
-  TORCH_CHECK(dent.sizes() == ent.sizes() && drel.sizes() == rel.sizes(), "table grads must match the tables");
+  if (occ) {  // per-occurrence rows: [B * (2 + K), D] entities (h, t, negatives), [B, D] relations
+    TORCH_CHECK(dent.dim() == 2 && dent.size(0) == k.B * (2 + k.K) && dent.size(1) == k.D && drel.dim() == 2 &&
+                    drel.size(0) == k.B && drel.size(1) == k.D,
+                "occurrence grads must be [B*(2+K), D] and [B, D]");
+  } else {
+    TORCH_CHECK(dent.sizes() == ent.sizes() && drel.sizes() == rel.sizes(), "table grads must match the tables");
+  }
   const c10::DeviceGuard g(ent.device());
   ok(eh_kg_bwd(ent.data_ptr<float>(), rel.data_ptr<float>(), src.data_ptr<int64_t>(), dst.data_ptr<int64_t>(),
                ridx.data_ptr<int64_t>(), neg.data_ptr<int64_t>(), k.B, static_cast<int>(k.K), static_cast<int>(k.D),
                static_cast<int>(kind), static_cast<int>(corrupt), normalize ? 1 : 0, gpos.data_ptr<float>(),
-               gneg.data_ptr<float>(), dent.data_ptr<float>(), drel.data_ptr<float>(), stream()),
+               gneg.data_ptr<float>(), dent.data_ptr<float>(), drel.data_ptr<float>(), occ ? 1 : 0, stream()),
      "kg_bwd");
 }
 
@@ -653,7 +704,11 @@ void register_gnn_ops(pybind11::module& m) {
   m.def("gather_f32_bf16", &gather_f32_bf16, py::arg("x"), py::arg("idx"), py::arg("out") = py::none());
   m.def("sgns_apply_", &sgns_apply_);
   m.def("kg_fwd", &kg_fwd);
-  m.def("kg_bwd", &kg_bwd);
+  m.def("pair_fwd", &pair_fwd, py::arg("es"), py::arg("ec"), py::arg("B"), py::arg("K"), py::arg("mrr") = py::none());
+  m.def("pair_bwd", &pair_bwd);
+  m.def("kg_bwd", &kg_bwd, py::arg("ent"), py::arg("rel"), py::arg("src"), py::arg("dst"), py::arg("ridx"),
+        py::arg("neg"), py::arg("kind"), py::arg("corrupt"), py::arg("normalize"), py::arg("gpos"), py::arg("gneg"),
+        py::arg("dent"), py::arg("drel"), py::arg("occ") = false);
   m.def("unique_first", &unique_first);
   m.def("unique_first_padded", &unique_first_padded);
 }

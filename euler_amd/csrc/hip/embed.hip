@@ -473,8 +473,10 @@ __device__ __forceinline__ void kg_grad(int kind, int lp, float g, const float* 
 }
 
 // push the gradient w.r.t. a normalised row through x / |x| and add it to the table grad
+// (occ: store it as occurrence row ``row`` instead — summed per table row afterwards by a
+// segment reduction, no atomics on hot rows)
 __device__ __forceinline__ void kg_scatter(float* __restrict__ dtab, int64_t row, int sub, int D, int lp,
-                                           bool normalize, const float* xhat, float nrm, float* dx) {
+                                           bool normalize, const float* xhat, float nrm, float* dx, bool occ = false) {
   if (normalize) {
     float p = 0.f;
 #pragma unroll
@@ -484,6 +486,10 @@ __device__ __forceinline__ void kg_scatter(float* __restrict__ dtab, int64_t row
     for (int v = 0; v < 4; ++v) dx[v] = (dx[v] - xhat[v] * dot) / nrm;
   }
   if (sub * 4 < D && row >= 0) {
+    if (occ) {
+      EV<float>::store(dtab + row * D + sub * 4, dx);
+      return;
+    }
 #pragma unroll
     for (int v = 0; v < 4; ++v) atomicAdd(dtab + row * D + sub * 4 + v, dx[v]);
   }
@@ -491,7 +497,7 @@ __device__ __forceinline__ void kg_scatter(float* __restrict__ dtab, int64_t row
 
 __global__ __launch_bounds__(256) void kg_bwd_kernel(KgArgs a, const float* __restrict__ gpos,
                                                      const float* __restrict__ gneg, float* __restrict__ dent,
-                                                     float* __restrict__ drel) {
+                                                     float* __restrict__ drel, int occ) {
   const RowLane L = row_lane(a.lp, a.B);
   if (!L.ok) return;
   float h[4], r[4], t[4], n[4], nh, nr, nt, nn;
@@ -509,11 +515,12 @@ __global__ __launch_bounds__(256) void kg_bwd_kernel(KgArgs a, const float* __re
     if (a.corrupt != 1) kg_grad(a.kind, a.lp, gneg[L.row * nneg + k], n, r, t, dn, dr, dt);
     if (a.corrupt != 0)
       kg_grad(a.kind, a.lp, gneg[L.row * nneg + (a.corrupt == 2 ? a.K : 0) + k], h, r, n, dh, dr, dn);
-    kg_scatter(dent, ns, L.sub, a.D, a.lp, a.normalize, n, nn, dn);
+    // occurrence rows of triple i: [h, t, neg_0 .. neg_{K-1}] (entities), i (relation)
+    kg_scatter(dent, occ ? L.row * (2 + a.K) + 2 + k : ns, L.sub, a.D, a.lp, a.normalize, n, nn, dn, occ);
   }
-  kg_scatter(dent, hs, L.sub, a.D, a.lp, a.normalize, h, nh, dh);
-  kg_scatter(drel, rs, L.sub, a.D, a.lp, a.normalize, r, nr, dr);
-  kg_scatter(dent, ts, L.sub, a.D, a.lp, a.normalize, t, nt, dt);
+  kg_scatter(dent, occ ? L.row * (2 + a.K) : hs, L.sub, a.D, a.lp, a.normalize, h, nh, dh, occ);
+  kg_scatter(drel, occ ? L.row : rs, L.sub, a.D, a.lp, a.normalize, r, nr, dr, occ);
+  kg_scatter(dent, occ ? L.row * (2 + a.K) + 1 : ts, L.sub, a.D, a.lp, a.normalize, t, nt, dt, occ);
 }
 
 inline int row_lanes(int chunks) {
@@ -615,11 +622,11 @@ hipError_t eh_kg_fwd(const float* ent, const float* rel, const int64_t* src, con
 
 hipError_t eh_kg_bwd(const float* ent, const float* rel, const int64_t* src, const int64_t* dst, const int64_t* ridx,
                      const int64_t* neg, int64_t B, int K, int D, int kind, int corrupt, int normalize,
-                     const float* gpos, const float* gneg, float* dent, float* drel, hipStream_t s) {
+                     const float* gpos, const float* gneg, float* dent, float* drel, int occ, hipStream_t s) {
   if (B == 0) return hipSuccess;
   if (D % 4 != 0 || D > 256 || kind < 0 || kind > 2 || corrupt < 0 || corrupt > 2) return hipErrorInvalidValue;
   const KgArgs a = kg_args(ent, rel, src, dst, ridx, neg, B, K, D, kind, corrupt, normalize);
-  hipLaunchKernelGGL(kg_bwd_kernel, row_grid(B, a.lp), dim3(256), 0, s, a, gpos, gneg, dent, drel);
+  hipLaunchKernelGGL(kg_bwd_kernel, row_grid(B, a.lp), dim3(256), 0, s, a, gpos, gneg, dent, drel, occ);
   return hipGetLastError();
 }
 

@@ -107,7 +107,13 @@ hipError_t eh_kg_fwd(const float* ent, const float* rel, const int64_t* src, con
                      float* pos_score, float* neg_score, hipStream_t s);
 hipError_t eh_kg_bwd(const float* ent, const float* rel, const int64_t* src, const int64_t* dst, const int64_t* ridx,
                      const int64_t* neg, int64_t B, int K, int D, int kind, int corrupt, int normalize,
-                     const float* gpos, const float* gneg, float* dent, float* drel, hipStream_t s);
+                     const float* gpos, const float* gneg, float* dent, float* drel, int occ, hipStream_t s);
+
+// pair.hip (fused sigmoid cross-entropy of the unsupervised pair objective)
+hipError_t eh_pair_fwd(const float* es, const float* ec, int B, int K, int E, float inv_n, float* logits,
+                       float* loss_part, float* mrr, hipStream_t s);
+hipError_t eh_pair_bwd(const float* es, const float* ec, int B, int K, int E, float inv_n, const float* logits,
+                       const float* dloss, float* des, float* dec, hipStream_t s);
 
 // gemm.hip (tiled MFMA GEMM with fused epilogues and split-K)
 hipError_t eh_gemm(const void* A, const void* B, void* C, const float* bias, const void* rmask, float* part,

@@ -90,6 +90,31 @@ def tower_head(W0, W1, Wfc, bfc, tower):
     return _TowerHead.apply(W0, W1, Wfc, bfc, tower)
 
 
+class _PairLossFused(torch.autograd.Function):
+    """csrc/hip/pair.hip: logits + softplus CE + reciprocal ranks in one launch, the
+    closed-form gradient in another (the torch composition below is ~20 launches)"""
+
+    @staticmethod
+    def forward(ctx, es, ec, B, K, mrr):
+        from euler_amd.ops._native import hip
+
+        es, ec = es.contiguous(), ec.contiguous()
+        logits, part = hip().pair_fwd(es, ec, B, K, mrr)
+        ctx.save_for_backward(es, ec, logits)
+        ctx.B, ctx.K = B, K
+        ctx.mark_non_differentiable(logits)
+        return part.sum(), logits
+
+    @staticmethod
+    def backward(ctx, dloss, _dlogits):
+        from euler_amd.ops._native import hip
+
+        es, ec, logits = ctx.saved_tensors
+        des, dec = torch.empty_like(es), torch.empty_like(ec)
+        hip().pair_bwd(es, ec, ctx.B, ctx.K, logits, dloss.float().reshape(1).contiguous(), des, dec)
+        return des, dec, None, None, None
+
+
 class _PairLoss(torch.autograd.Function):
     @staticmethod
     def forward(ctx, es, ec, B, K):
@@ -118,6 +143,17 @@ class _PairLoss(torch.autograd.Function):
         return des, dec, None, None
 
 
-def pair_loss(es, ec, B, K):
-    """(loss, logits [B, 1 + K] with the positive first) of the unsupervised objective"""
-    return _PairLoss.apply(es, ec, B, K)
+def pair_loss(es, ec, B, K, mrr_out=None):
+    """(loss, logits [B, 1 + K] with the positive first) of the unsupervised objective.
+    ``mrr_out`` (fp32 [1]): the fused kernel adds the batch's reciprocal ranks of the
+    positives to it; returns ``(loss, logits, True)`` when it did (else False)."""
+    D = es.shape[1]
+    if (_PAIR_FUSED and es.is_cuda and es.dtype == torch.float32 and ec.dtype == torch.float32 and D % 4 == 0
+            and D <= 256 and 0 <= K <= 15):
+        loss, logits = _PairLossFused.apply(es, ec, B, K, mrr_out)
+        return loss, logits, mrr_out is not None
+    loss, logits = _PairLoss.apply(es, ec, B, K)
+    return loss, logits, False
+
+
+_PAIR_FUSED = os.environ.get("EULER_AMD_PAIR_FUSED", "1") == "1"

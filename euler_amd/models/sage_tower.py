@@ -345,7 +345,9 @@ class UnsupSageTrainer:
             es = tower_head(P["gnn.W0"], P["gnn.W1"], P["gnn.Wfc"], P["gnn.bfc"], ts)
             ec = tower_head(P["context_gnn.W0"], P["context_gnn.W1"], P["context_gnn.Wfc"], P["context_gnn.bfc"],
                             tc)
-            loss, logits = pair_loss(es, ec, self.B, self.K)
+            loss, logits, counted = pair_loss(es, ec, self.B, self.K, self.mrr_sum)
+            if counted:
+                return loss, None  # the kernel added the batch's reciprocal ranks to mrr_sum
             with torch.no_grad():
                 rank = 1 + (logits[:, 1:] >= logits[:, :1]).sum(1).float()
                 mrr = (1.0 / rank).sum()
@@ -384,7 +386,8 @@ class UnsupSageTrainer:
             scale = 1.0 if s is None else float(s)
         self.opt.step(scale)
         self.loss_out.copy_(loss.detach())
-        self.mrr_sum.add_(mrr)
+        if mrr is not None:
+            self.mrr_sum.add_(mrr)
         return self.loss_out
 
     def capture(self, grad_sync=None, warmup: int = 2):

@@ -108,3 +108,28 @@ def test_estimator_unsup_device_graph_train_resume_cpu(tmp_path, monkeypatch):
     assert r2["step"] == 30
     st = torch.load(str(tmp_path / "ckpt" / "model.ckpt-30.pt"), weights_only=True)
     assert "context_gnn.convs.1.neigh_fc.weight" in st["model"] and st["device_trainer"]["step"] >= 20
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("E,K", [(128, 5), (64, 1), (40, 15)])
+def test_fused_pair_loss_matches_torch(cuda, E, K):
+    """pair.hip (loss, logits, reciprocal ranks, gradients) against the torch composition"""
+    from euler_amd.models import _tower_ops as T
+
+    torch.manual_seed(3)
+    B = 300
+    es = (torch.randn(B, E, device=cuda) * 0.3).requires_grad_(True)
+    ec = (torch.randn(B * (1 + K), E, device=cuda) * 0.3).requires_grad_(True)
+    mrr = torch.zeros(1, device=cuda)
+    loss, logits, counted = T.pair_loss(es, ec, B, K, mrr)
+    assert counted
+    (loss * 1.7).backward()
+    es2, ec2 = es.detach().clone().requires_grad_(True), ec.detach().clone().requires_grad_(True)
+    loss2, logits2 = T._PairLoss.apply(es2, ec2, B, K)
+    (loss2 * 1.7).backward()
+    torch.testing.assert_close(loss, loss2, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(logits, logits2, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(es.grad, es2.grad, atol=1e-7, rtol=1e-4)
+    torch.testing.assert_close(ec.grad, ec2.grad, atol=1e-7, rtol=1e-4)
+    rank = 1 + (logits2[:, 1:] >= logits2[:, :1]).sum(1).float()
+    torch.testing.assert_close(mrr[0], (1.0 / rank).sum(), atol=1e-3, rtol=1e-5)

@@ -120,8 +120,10 @@ for st in "${S[@]}"; do
     gat_compare)
       # same task, same seed, same epochs: fused gat.hip vs the composed autograd reference
       for impl in fused composed; do
+        # 1M nodes: the composed variant's fp32 per-edge messages of the full 124M-edge
+        # graph do not fit next to its autograd buffers
         run "bench_gat_$impl" 900 python -u benchmarks/bench_gat.py --impl $impl \
-          --eval-epochs "${GAT_EPOCHS:-400}" || exit $?
+          --num-nodes "${GAT_NODES:-1000000}" --eval-epochs "${GAT_EPOCHS:-400}" || exit $?
       done ;;
     gat_variants)
       # GAT_VARIANTS="-DGAT_FWD_U=4|-DGAT_FWD_U=8": rebuild gat.hip per flag set, time the edge kernels
