@@ -2,6 +2,8 @@
 // embed.hip, unique.hip).  Host-only, same rules as binding.cpp: every operand is
 // validated (dtype, device, contiguity, shape) before a launch, launches go to torch's
 // current HIP stream, outputs are allocated by torch's caching allocator.
+#include <cstdlib>
+
 #include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime_api.h>
@@ -344,8 +346,8 @@ torch::Tensor gather_f32_bf16(torch::Tensor x, torch::Tensor idx, c10::optional<
 }
 
 // unsupervised pair objective: es [B, E] sources, ec [B + B K, E] contexts (B positives,
-// then the B x K negatives source-major) -> (logits [B, 1 + K], loss_part [B]); the
-// reciprocal ranks of the positives are added to mrr[0] when given
+// then the B x K negatives source-major) -> (logits [B, 1 + K], loss [] = mean sigmoid CE);
+// the batch's summed reciprocal ranks of the positives are added to mrr[0] when given
 std::vector<torch::Tensor> pair_fwd(torch::Tensor es, torch::Tensor ec, int64_t B, int64_t K,
                                     c10::optional<torch::Tensor> mrr) {
   typed(es, torch::kFloat32, "es");
@@ -363,12 +365,13 @@ std::vector<torch::Tensor> pair_fwd(torch::Tensor es, torch::Tensor ec, int64_t 
   }
   const c10::DeviceGuard g(es.device());
   auto logits = torch::empty({B, 1 + K}, es.options());
-  auto loss_part = torch::empty({B}, es.options());
+  auto part = torch::empty({2 * B}, es.options());
+  auto loss = torch::empty({}, es.options());
   ok(eh_pair_fwd(es.data_ptr<float>(), ec.data_ptr<float>(), static_cast<int>(B), static_cast<int>(K),
                  static_cast<int>(E), 1.f / static_cast<float>(B * (1 + K)), logits.data_ptr<float>(),
-                 loss_part.data_ptr<float>(), mp, stream()),
+                 part.data_ptr<float>(), loss.data_ptr<float>(), mp, stream()),
      "pair_fwd");
-  return {logits, loss_part};
+  return {logits, loss};
 }
 
 void pair_bwd(torch::Tensor es, torch::Tensor ec, int64_t B, int64_t K, torch::Tensor logits, torch::Tensor dloss,
@@ -561,7 +564,7 @@ std::vector<torch::Tensor> unique_first(torch::Tensor x) {
   auto slot = torch::empty({n}, opts.dtype(torch::kInt32));
   auto flag = torch::empty({n}, opts.dtype(torch::kInt32));
   ok(eh_unique_insert(x.data_ptr<int64_t>(), n, keys.data_ptr(), minpos.data_ptr<int32_t>(), cap,
-                      slot.data_ptr<int32_t>(), stream()),
+                      slot.data_ptr<int32_t>(), 0, stream()),
      "unique_insert");
   ok(eh_unique_mark(n, slot.data_ptr<int32_t>(), minpos.data_ptr<int32_t>(), flag.data_ptr<int32_t>(), stream()),
      "unique_mark");
@@ -593,7 +596,7 @@ std::vector<torch::Tensor> unique_first_padded(torch::Tensor x, int64_t fill) {
   auto slot = torch::empty({n}, opts.dtype(torch::kInt32));
   auto flag = torch::empty({n}, opts.dtype(torch::kInt32));
   ok(eh_unique_insert(x.data_ptr<int64_t>(), n, keys.data_ptr(), minpos.data_ptr<int32_t>(), cap,
-                      slot.data_ptr<int32_t>(), stream()),
+                      slot.data_ptr<int32_t>(), 1, stream()),
      "unique_insert");
   ok(eh_unique_mark(n, slot.data_ptr<int32_t>(), minpos.data_ptr<int32_t>(), flag.data_ptr<int32_t>(), stream()),
      "unique_mark");
@@ -646,6 +649,19 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool trans_a, bool 
   const c10::DeviceGuard g(A.device());
   torch::Tensor part;
   if (splits > 1) part = torch::empty({splits * M * N}, A.options().dtype(torch::kFloat32));
+  static const bool tn_on = [] {  // EULER_AMD_GEMM_TN=0: the generic kernel's strided path
+    const char* e = std::getenv("EULER_AMD_GEMM_TN");
+    return !(e && e[0] == '0');
+  }();
+  if (tn_on && trans_a && !trans_b && !bp && !rp && !relu) {
+    // both operands k-major: the transposing-read kernel
+    ok(eh_gemm_tn(A.data_ptr(), B.data_ptr(), C.data_ptr(), splits > 1 ? part.data_ptr<float>() : nullptr, M, N, K,
+                  A.stride(0), B.stride(0), C.stride(0), A.scalar_type() == torch::kBFloat16,
+                  B.scalar_type() == torch::kBFloat16, C.scalar_type() == torch::kBFloat16, static_cast<int>(splits),
+                  static_cast<float>(alpha), stream()),
+       "gemm_tn");
+    return;
+  }
   ok(eh_gemm(A.data_ptr(), B.data_ptr(), C.data_ptr(), bp, rp, splits > 1 ? part.data_ptr<float>() : nullptr, M, N, K,
              A.stride(0), B.stride(0), C.stride(0), ldr, trans_a ? 1 : 0, trans_b ? 0 : 1,
              A.scalar_type() == torch::kBFloat16, B.scalar_type() == torch::kBFloat16,

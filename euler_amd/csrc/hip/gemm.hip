@@ -158,6 +158,117 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
     }
 }
 
+// C = alpha A^T B for k-major operands (A [K][M], B [K][N], row-major: the weight gradients
+// dW = dY^T X of row-batched layers): 64-row k sub-tiles of both operands are staged in LDS
+// as they lie in memory ([k][64 columns], contiguous 16-value row segments per thread, fp32
+// rounded to bf16 on the way) and the MFMA fragments come out of the gfx950 transposing
+// read (tl_tr_frag) — the generic kernel's transposed path loads every operand element
+// with its own strided scalar load.  Split-K over grid.z (kps rows per split) into the
+// partial slabs, summed by gemm_reduce_kernel.
+constexpr int kTnLd = kGmT + 16;  // LDS row (halfwords): 40 dwords, conflict-free tr reads
+
+__device__ __forceinline__ void tn_load16(const void* X, int bf, int64_t ld, int64_t rows, int64_t cols, int64_t k,
+                                          int64_t c, float* v) {
+#pragma unroll
+  for (int j = 0; j < 16; ++j) v[j] = 0.f;
+  if (k >= rows) return;
+  if (c + 16 <= cols && (ld & 7) == 0 && (c & 7) == 0 && (reinterpret_cast<uintptr_t>(X) & 31) == 0) {
+    if (bf) {
+      const bf16_t* p = static_cast<const bf16_t*>(X) + k * ld + c;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint4_t q = *reinterpret_cast<const uint4_t*>(p + 8 * h);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[8 * h + 2 * j] = bf2f(static_cast<bf16_t>(q[j] & 0xffffu));
+          v[8 * h + 2 * j + 1] = bf2f(static_cast<bf16_t>(q[j] >> 16));
+        }
+      }
+    } else {
+      const float* p = static_cast<const float*>(X) + k * ld + c;
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const float4_t f = *reinterpret_cast<const float4_t*>(p + 4 * h);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[4 * h + j] = f[j];
+      }
+    }
+    return;
+  }
+  for (int j = 0; j < 16; ++j)
+    if (c + j < cols)
+      v[j] = bf ? bf2f(static_cast<const bf16_t*>(X)[k * ld + c + j]) : static_cast<const float*>(X)[k * ld + c + j];
+}
+
+__global__ __launch_bounds__(256) void gemm_tn_kernel(GemmArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16_t As[2][kGmK * kTnLd];
+  __shared__ __attribute__((aligned(16))) bf16_t Bs[2][kGmK * kTnLd];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int64_t m0 = static_cast<int64_t>(blockIdx.x) * kGmT, n0 = static_cast<int64_t>(blockIdx.y) * kGmT;
+  const int split = blockIdx.z;
+  const int64_t kb = static_cast<int64_t>(split) * a.kps;
+  const int64_t ke = kb + a.kps < a.K ? kb + a.kps : a.K;
+  const int sr = tid >> 2, sc = (tid & 3) * 16;  // staged k row, 16-column segment
+  float va[16], vb[16];
+  auto fetch = [&](int64_t k0) {
+    tn_load16(a.A, a.a_bf16, a.lda, ke, a.M, k0 + sr, m0 + sc, va);
+    tn_load16(a.B, a.b_bf16, a.ldb, ke, a.N, k0 + sr, n0 + sc, vb);
+  };
+  auto stage = [&](int buf) {
+    *reinterpret_cast<uint4_t*>(&As[buf][sr * kTnLd + sc]) = pack_bf16x8(va);
+    *reinterpret_cast<uint4_t*>(&As[buf][sr * kTnLd + sc + 8]) = pack_bf16x8(va + 8);
+    *reinterpret_cast<uint4_t*>(&Bs[buf][sr * kTnLd + sc]) = pack_bf16x8(vb);
+    *reinterpret_cast<uint4_t*>(&Bs[buf][sr * kTnLd + sc + 8]) = pack_bf16x8(vb + 8);
+  };
+  float4_t acc[2][2];
+  tl_zero(acc);
+  const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
+  if (kb < ke) {
+    fetch(kb);
+    stage(0);
+    __syncthreads();
+    int buf = 0;
+    for (int64_t k0 = kb; k0 < ke; k0 += kGmK) {
+      const bool more = k0 + kGmK < ke;
+      if (more) fetch(k0 + kGmK);
+#pragma unroll
+      for (int ks = 0; ks < kGmK; ks += 32) {
+        uint4_t fa[2], fb[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          fa[i] = tl_tr_frag<kTnLd>(As[buf], ks, wr + i * 16, lane);
+          fb[i] = tl_tr_frag<kTnLd>(Bs[buf], ks, wc + i * 16, lane);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(fa[i], fb[j], acc[i][j]);
+      }
+      if (more) {
+        stage(buf ^ 1);  // buf ^ 1 was last read before the previous step's barrier
+        __syncthreads();
+        buf ^= 1;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t col = n0 + wc + j * 16 + (lane & 15);
+      if (col >= a.N) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t row = m0 + wr + i * 16 + (lane >> 4) * 4 + q;
+        if (row >= a.M) continue;
+        const float v = acc[i][j][q] * a.alpha;
+        if (a.splits > 1) a.part[(static_cast<int64_t>(split) * a.M + row) * a.N + col] = v;
+        else if (a.c_bf16) static_cast<bf16_t*>(a.C)[row * a.ldc + col] = f2bf(v);
+        else static_cast<float*>(a.C)[row * a.ldc + col] = v;
+      }
+    }
+}
+
 // sum of the split-K slabs + the epilogue
 __global__ __launch_bounds__(256) void gemm_reduce_kernel(GemmArgs a) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -203,6 +314,23 @@ hipError_t eh_gemm(const void* A, const void* B, void* C, const float* bias, con
   const dim3 grid(static_cast<uint32_t>(ceil_div(M, kGmT)), static_cast<uint32_t>(ceil_div(N, kGmT)),
                   static_cast<uint32_t>(splits));
   hipLaunchKernelGGL(gemm_kernel, grid, dim3(256), 0, s, g);
+  if (splits > 1)
+    hipLaunchKernelGGL(gemm_reduce_kernel, dim3(static_cast<uint32_t>(ceil_div(M * N, 256))), dim3(256), 0, s, g);
+  return hipGetLastError();
+}
+
+// C [M][N] = alpha A^T B, A [K][M] (lda), B [K][N] (ldb), split over K in `splits` slabs
+hipError_t eh_gemm_tn(const void* A, const void* B, void* C, float* part, int64_t M, int64_t N, int64_t K, int64_t lda,
+                      int64_t ldb, int64_t ldc, int a_bf16, int b_bf16, int c_bf16, int splits, float alpha,
+                      hipStream_t s) {
+  if (M <= 0 || N <= 0 || K <= 0 || splits < 1 || (splits > 1 && !part)) return hipErrorInvalidValue;
+  GemmArgs g{A, B, C, nullptr, nullptr, part, M, N, K, lda, ldb, ldc, 0, 1, 1, a_bf16, b_bf16, c_bf16, 0,
+             0, splits, 0, alpha};
+  const int64_t ksteps = ceil_div(K, kGmK);
+  g.kps = static_cast<int32_t>(ceil_div(ksteps, splits) * kGmK);
+  const dim3 grid(static_cast<uint32_t>(ceil_div(M, kGmT)), static_cast<uint32_t>(ceil_div(N, kGmT)),
+                  static_cast<uint32_t>(splits));
+  hipLaunchKernelGGL(gemm_tn_kernel, grid, dim3(256), 0, s, g);
   if (splits > 1)
     hipLaunchKernelGGL(gemm_reduce_kernel, dim3(static_cast<uint32_t>(ceil_div(M * N, 256))), dim3(256), 0, s, g);
   return hipGetLastError();

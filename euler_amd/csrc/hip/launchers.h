@@ -110,8 +110,8 @@ hipError_t eh_kg_bwd(const float* ent, const float* rel, const int64_t* src, con
                      const float* gpos, const float* gneg, float* dent, float* drel, int occ, hipStream_t s);
 
 // pair.hip (fused sigmoid cross-entropy of the unsupervised pair objective)
-hipError_t eh_pair_fwd(const float* es, const float* ec, int B, int K, int E, float inv_n, float* logits,
-                       float* loss_part, float* mrr, hipStream_t s);
+hipError_t eh_pair_fwd(const float* es, const float* ec, int B, int K, int E, float inv_n, float* logits, float* part,
+                       float* loss, float* mrr, hipStream_t s);
 hipError_t eh_pair_bwd(const float* es, const float* ec, int B, int K, int E, float inv_n, const float* logits,
                        const float* dloss, float* des, float* dec, hipStream_t s);
 
@@ -121,6 +121,10 @@ hipError_t eh_gemm(const void* A, const void* B, void* C, const float* bias, con
                    int b_t, int a_bf16, int b_bf16, int c_bf16, int r_bf16, int relu, int splits, float alpha,
                    hipStream_t s);
 
+hipError_t eh_gemm_tn(const void* A, const void* B, void* C, float* part, int64_t M, int64_t N, int64_t K, int64_t lda,
+                      int64_t ldb, int64_t ldc, int a_bf16, int b_bf16, int c_bf16, int splits, float alpha,
+                      hipStream_t s);
+
 // route.hip (owner routing of the fixed-capacity all-to-all exchanges)
 int64_t eh_route_chunks(int64_t n);
 hipError_t eh_route_by_owner(const int64_t* ids, int64_t n, int W, int64_t C, int32_t* cnt, int64_t* pos,
@@ -128,7 +132,7 @@ hipError_t eh_route_by_owner(const int64_t* ids, int64_t n, int W, int64_t C, in
 
 // unique.hip (K8: hash unique, first-occurrence order)
 hipError_t eh_unique_insert(const int64_t* x, int64_t n, void* keys, int32_t* minpos, int64_t cap, int32_t* slot,
-                            hipStream_t s);
+                            int skip_neg, hipStream_t s);
 hipError_t eh_unique_mark(int64_t n, const int32_t* slot, const int32_t* minpos, int32_t* flag, hipStream_t s);
 hipError_t eh_unique_finalize(const int64_t* x, int64_t n, const int32_t* slot, const int32_t* minpos,
                               const int32_t* flag, const int32_t* pos, int64_t* inv, int64_t* uniq, hipStream_t s);

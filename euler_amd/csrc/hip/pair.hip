@@ -4,29 +4,26 @@
 // elementwise / reduction kernels (profiles/r3_unsup/).
 //
 //   pair_fwd : one wave per source b: x_s = <es[b], ec[row(b, s)]> for s = 0 (positive,
-//              row b) and s = 1..K (negatives, rows B + b K + s - 1); loss_part[b] =
-//              (sum_s softplus(x_s) - x_0) * inv_n; logits [B, 1 + K]; the reciprocal rank of
-//              the positive is added to mrr[0] (metric only)
+//              row b) and s = 1..K (negatives, rows B + b K + s - 1); part[b] =
+//              (sum_s softplus(x_s) - x_0) * inv_n, part[B + b] = reciprocal rank of the
+//              positive; logits [B, 1 + K]
+//   pair_sum : one workgroup: loss[0] = sum_b part[b]; mrr[0] += sum_b part[B + b] (a
+//              fixed-order tree sum: deterministic, no same-address atomics)
 //   pair_bwd : g_s = (sigmoid(x_s) - [s == 0]) * dloss[0] * inv_n; des[b] = sum_s g_s ec_s,
 //              dec[row(b, s)] = g_s es[b]
 #include "hip/common.h"
 #include "hip/launchers.h"
+#include "hip/tile.h"
 
 namespace euler_hip {
 
 constexpr int PL_MAXK = 15;  // negatives per source (larger K: the torch composition)
 
-__device__ __forceinline__ float pl_wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
 __device__ __forceinline__ float pl_softplus(float x) { return x > 20.f ? x : log1pf(__expf(x)); }
 
 __global__ __launch_bounds__(256) void pair_fwd_kernel(const float* __restrict__ es, const float* __restrict__ ec,
                                                        int B, int K, int E, float inv_n, float* __restrict__ logits,
-                                                       float* __restrict__ loss_part, float* __restrict__ mrr) {
+                                                       float* __restrict__ part) {
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (b >= B) return;
   const int d = lane * 4;
@@ -42,7 +39,7 @@ __global__ __launch_bounds__(256) void pair_fwd_kernel(const float* __restrict__
       const float4_t c = *reinterpret_cast<const float4_t*>(ec + row * E + d);
       p = s[0] * c[0] + s[1] * c[1] + s[2] * c[2] + s[3] * c[3];
     }
-    x[k] = pl_wave_sum(p);
+    x[k] = wave_sum(p);
   }
   if (lane == 0) {
     float l = -x[0];
@@ -54,8 +51,35 @@ __global__ __launch_bounds__(256) void pair_fwd_kernel(const float* __restrict__
       logits[static_cast<int64_t>(b) * (K + 1) + k] = x[k];
       if (k > 0 && x[k] >= x[0]) ++rank;
     }
-    loss_part[b] = l * inv_n;
-    if (mrr) atomicAdd(mrr, 1.f / static_cast<float>(rank));
+    part[b] = l * inv_n;
+    part[B + b] = 1.f / static_cast<float>(rank);
+  }
+}
+
+__global__ __launch_bounds__(1024) void pair_sum_kernel(const float* __restrict__ part, int B, float* __restrict__ loss,
+                                                        float* __restrict__ mrr) {
+  __shared__ float red[2][16];
+  float l = 0.f, r = 0.f;
+  for (int b = threadIdx.x; b < B; b += 1024) {
+    l += part[b];
+    r += part[B + b];
+  }
+  l = wave_sum(l);
+  r = wave_sum(r);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][w] = l;
+    red[1][w] = r;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float sl = 0.f, sr = 0.f;
+    for (int i = 0; i < 16; ++i) {
+      sl += red[0][i];
+      sr += red[1][i];
+    }
+    loss[0] = sl;
+    if (mrr) mrr[0] += sr;
   }
 }
 
@@ -87,12 +111,14 @@ using namespace euler_hip;
 
 extern "C" {
 
-hipError_t eh_pair_fwd(const float* es, const float* ec, int B, int K, int E, float inv_n, float* logits,
-                       float* loss_part, float* mrr, hipStream_t s) {
+// part: [2 B] scratch; loss [1] is written, mrr [1] (optional) accumulated
+hipError_t eh_pair_fwd(const float* es, const float* ec, int B, int K, int E, float inv_n, float* logits, float* part,
+                       float* loss, float* mrr, hipStream_t s) {
   if (B == 0) return hipSuccess;
   if (E % 4 != 0 || E > 256 || K < 0 || K > PL_MAXK) return hipErrorInvalidValue;
   hipLaunchKernelGGL(pair_fwd_kernel, dim3(static_cast<uint32_t>(ceil_div(B, 4))), dim3(256), 0, s, es, ec, B, K, E,
-                     inv_n, logits, loss_part, mrr);
+                     inv_n, logits, part);
+  hipLaunchKernelGGL(pair_sum_kernel, dim3(1), dim3(1024), 0, s, part, B, loss, mrr);
   return hipGetLastError();
 }
 

@@ -15,8 +15,11 @@
 //   rel_gemm_dw : dW[rel] += sum_e (scale[e] * G[g_idx[e]])^T X[x_idx[e]]  (per-chunk
 //                 outer-product GEMM, fragments by transposing LDS reads; a relation's
 //                 only chunk stores its slab, longer relations add with fp32 atomics)
+#include <cstdlib>
+
 #include "hip/common.h"
 #include "hip/launchers.h"
+#include "hip/tile.h"
 
 namespace euler_hip {
 
@@ -138,20 +141,6 @@ constexpr int RG_CH = 512;  // edges per dW chunk (256: same time, more atomics;
 // 40 (T = 64) or 72 (T = 128) dwords the 8 rows a 32-lane half reads land on 8 disjoint
 // 8-bank sets (conflict-free), and the 16-byte row-segment stores of 8 consecutive lanes
 // cover the 32 banks once.
-typedef short rg_v4i16 __attribute__((ext_vector_type(4)));
-typedef uint32_t rg_u2 __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(3))) rg_v4i16 rg_lds_v4i16;
-
-template <int LD>
-__device__ __forceinline__ uint4_t rg_tr_frag(const bf16_t* img, int e0, int c0, int lane) {
-  const int g = lane >> 4, i = lane & 15;
-  const bf16_t* a = img + (e0 + 4 * g + (i >> 2)) * LD + c0 + 4 * (i & 3);
-  const rg_v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((rg_lds_v4i16*)(a));
-  const rg_v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((rg_lds_v4i16*)(a + 16 * LD));
-  const rg_u2 l2 = __builtin_bit_cast(rg_u2, lo), h2 = __builtin_bit_cast(rg_u2, hi);
-  return uint4_t{l2[0], l2[1], h2[0], h2[1]};
-}
-
 // one workgroup = one (chunk of <= RG_CH edges of one relation) x (T x T slab of dW[rel]);
 // T = 128 covers a 128 x 128 weight in one slab, so every edge row is read once.  Wave w
 // owns rows w*T/4 .. of the slab (T/64 MFMA row tiles) x all T columns (T/16 tiles).
@@ -227,10 +216,10 @@ __global__ __launch_bounds__(256) void rel_gemm_dw_kernel(const bf16_t* __restri
     for (int k0 = 0; k0 < RG_BM; k0 += 32) {
       uint4_t a[FM];
 #pragma unroll
-      for (int m = 0; m < FM; ++m) a[m] = rg_tr_frag<LD>(gS, k0, wave * (T / 4) + m * 16, lane);
+      for (int m = 0; m < FM; ++m) a[m] = tl_tr_frag<LD>(gS, k0, wave * (T / 4) + m * 16, lane);
 #pragma unroll
       for (int f = 0; f < FN; ++f) {
-        const uint4_t bb = rg_tr_frag<LD>(xS, k0, f * 16, lane);
+        const uint4_t bb = tl_tr_frag<LD>(xS, k0, f * 16, lane);
 #pragma unroll
         for (int m = 0; m < FM; ++m) acc[m][f] = rg_mfma(a[m], bb, acc[m][f]);
       }
@@ -322,7 +311,11 @@ hipError_t eh_rel_gemm_dw(const void* G, int N, const int32_t* g_idx, const void
                           const int32_t* csolo, int n_chunks, float* dW, int accum, hipStream_t s) {
   if (n_chunks == 0) return hipSuccess;
   if (N % 64 != 0 || K % 64 != 0) return hipErrorInvalidValue;
-  const int T = (N % 128 == 0 && K % 128 == 0) ? 128 : 64;
+  static const int t_max = [] {  // EULER_AMD_RG_DW_T=64: 64 x 64 slabs only (tuning knob)
+    const char* e = std::getenv("EULER_AMD_RG_DW_T");
+    return e ? std::atoi(e) : 128;
+  }();
+  const int T = (t_max >= 128 && N % 128 == 0 && K % 128 == 0) ? 128 : 64;
   const int64_t blocks = static_cast<int64_t>(n_chunks) * (N / T) * (K / T);
   if (blocks >= (1ll << 31)) return hipErrorInvalidValue;
   if (T == 128)

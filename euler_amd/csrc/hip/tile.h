@@ -38,6 +38,25 @@ __device__ __forceinline__ uint4_t fm_frag(const bf16_t* __restrict__ Wf, int n0
                                            ((static_cast<int64_t>(n0 >> 4) * (K >> 5) + (k0 >> 5)) * 64 + lane) * 8);
 }
 
+// MFMA fragment of 16 columns c0.. of a row-major bf16 LDS image [rows][LD] whose rows are
+// the reduction index (k-major operands: dW = G^T X, C = A^T B), via the gfx950 transposing
+// read ds_read_b64_tr_b16: a 16-lane group reads a 4-row x 16-column block and lane i gets
+// column i.  Lane group g holds rows e0 + 4g .. +3 and e0 + 16 + 4g .. +3 (the same row map
+// for both operands, which is all the MFMA needs).  LD = 80 or 144 halfwords keeps the 8
+// rows a 32-lane half reads on disjoint bank sets.
+typedef short tl_v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) tl_v4i16 tl_lds_v4i16;
+
+template <int LD>
+__device__ __forceinline__ uint4_t tl_tr_frag(const bf16_t* img, int e0, int c0, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const bf16_t* a = img + (e0 + 4 * g + (i >> 2)) * LD + c0 + 4 * (i & 3);
+  const tl_v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tl_lds_v4i16*)(a));
+  const tl_v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tl_lds_v4i16*)(a + 16 * LD));
+  const tl_uint2 l2 = __builtin_bit_cast(tl_uint2, lo), h2 = __builtin_bit_cast(tl_uint2, hi);
+  return uint4_t{l2[0], l2[1], h2[0], h2[1]};
+}
+
 __device__ __forceinline__ bool bf_pos(bf16_t v) { return (v & 0x8000u) == 0 && (v & 0x7fffu) != 0; }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -29,16 +29,21 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
 __global__ __launch_bounds__(256) void unique_insert_kernel(const int64_t* __restrict__ x, int64_t n,
                                                             unsigned long long* __restrict__ keys,
                                                             int32_t* __restrict__ minpos, int64_t cap,
-                                                            int32_t* __restrict__ slot) {
+                                                            int32_t* __restrict__ slot, int skip_neg) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  if (skip_neg && x[i] < 0) {  // padding ("no id"): not a key, inverse -1
+    slot[i] = -1;
+    return;
+  }
   const unsigned long long k = static_cast<unsigned long long>(x[i]);
   uint64_t h = fmix64(k) & static_cast<uint64_t>(cap - 1);
   // cap >= 2n guarantees a free slot; the probe count is bounded by cap.  Repeated keys
-  // (padding ids, hub nodes: 67K copies of -1 in a sharded-feature exchange) must not
-  // serialise on one address: a plain load finds a present key without a CAS, and the
-  // position atomic is skipped once an earlier occurrence holds the slot (1175 -> ~10 us,
-  // profiles/r3_headline/shard_prof)
+  // (hub nodes) must not serialise on one address: a plain load finds a present key
+  // without a CAS, and the position atomic is skipped once an earlier occurrence holds the
+  // slot.  Padding ids (skip_neg: 67K copies of -1 in a sharded-feature exchange, all
+  // inserted at once, 434 us of same-address CAS: profiles/r3_headline/shard_prof) never
+  // reach the table.
   const volatile unsigned long long* vkeys = keys;
   const volatile int32_t* vmin = minpos;
   for (int64_t probe = 0; probe < cap; ++probe) {
@@ -87,11 +92,11 @@ using namespace euler_hip;
 extern "C" {
 
 hipError_t eh_unique_insert(const int64_t* x, int64_t n, void* keys, int32_t* minpos, int64_t cap, int32_t* slot,
-                            hipStream_t s) {
+                            int skip_neg, hipStream_t s) {
   if (n == 0) return hipSuccess;
   if (cap < 2 * n || (cap & (cap - 1)) != 0 || n >= (1ll << 31)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(unique_insert_kernel, dim3(static_cast<uint32_t>(ceil_div(n, 256))), dim3(256), 0, s, x, n,
-                     static_cast<unsigned long long*>(keys), minpos, cap, slot);
+                     static_cast<unsigned long long*>(keys), minpos, cap, slot, skip_neg);
   return hipGetLastError();
 }
 

@@ -99,11 +99,11 @@ class _PairLossFused(torch.autograd.Function):
         from euler_amd.ops._native import hip
 
         es, ec = es.contiguous(), ec.contiguous()
-        logits, part = hip().pair_fwd(es, ec, B, K, mrr)
+        logits, loss = hip().pair_fwd(es, ec, B, K, mrr)
         ctx.save_for_backward(es, ec, logits)
         ctx.B, ctx.K = B, K
         ctx.mark_non_differentiable(logits)
-        return part.sum(), logits
+        return loss, logits
 
     @staticmethod
     def backward(ctx, dloss, _dlogits):

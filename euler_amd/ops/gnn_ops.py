@@ -247,9 +247,9 @@ def gemm(a, b, out=None, trans_a=False, trans_b=False, bias=None, relu=False, rm
 
 def _gemm_splits(k_rows, tiles):
     """split-K count for a weight-gradient product over k_rows rows with `tiles` 64x64
-    output tiles: about 256 workgroups, at least 512 rows (8 k-stages) per split, at most 32
-    slabs for the reduce"""
-    return int(max(1, min(32, k_rows // 512, -(-256 // max(tiles, 1)))))
+    output tiles: about 512 workgroups (two per CU: the k loop is a dependent load chain),
+    at least 128 rows (2 k-stages) per split, at most 64 slabs for the reduce"""
+    return int(max(1, min(64, k_rows // 128, -(-512 // max(tiles, 1)))))
 
 
 class _Linear(torch.autograd.Function):
@@ -426,6 +426,7 @@ class RelationTiles:
         self.tile = int(tile)
         self.tile_rel, self.tile_start, self.tile_len, self.num_tiles = self._cut(counts, tile, dev)
         chunk = hip().rel_gemm_dw_chunk if dev.type == "cuda" else 1024
+        chunk = int(os.environ.get("EULER_AMD_RG_CH", chunk))  # tuning knob (tools/gpu_session.sh kg_dw_sweep)
         self.chunk_rel, self.chunk_start, self.chunk_len, self.num_chunks = self._cut(counts, chunk, dev)
         # a relation's only chunk stores its dW slab instead of adding atomically
         self.chunk_solo = (counts[self.chunk_rel.long()] <= chunk).to(torch.int32).contiguous()
@@ -662,15 +663,19 @@ def sgns_fwd_idx(T, tmap, tinv, C, cmap, cinv, K, gscale):
 
 def unique_first_padded(x: torch.Tensor, fill: int = -1):
     """Fixed-capacity :func:`unique_first` for graph-captured steps: ``(uniq [n], inverse
-    [n], count [1])`` with the distinct values in first-occurrence order followed by
-    ``fill``; the count stays on the device (GPU: no host sync)."""
+    [n], count [1])`` with the distinct non-negative values in first-occurrence order
+    followed by ``fill``; negative values are padding ("no id": not counted, inverse -1);
+    the count stays on the device (GPU: no host sync)."""
     x = x.reshape(-1)
     if use_hip(x):
         return tuple(hip().unique_first_padded(x.long().contiguous(), int(fill)))
-    u, inv = unique_first(x)
+    valid = x >= 0
+    u, inv_v = unique_first(x[valid])
+    inv = torch.full((x.numel(),), -1, dtype=torch.long, device=x.device)
+    inv[valid] = inv_v.long()
     out = torch.full((x.numel(),), int(fill), dtype=torch.long, device=x.device)
     out[: u.numel()] = u
-    return out, inv.long(), torch.tensor([u.numel()], dtype=torch.long, device=x.device)
+    return out, inv, torch.tensor([u.numel()], dtype=torch.long, device=x.device)
 
 
 def route_by_owner(ids, W: int, C: int, overflow):

@@ -165,8 +165,9 @@ class ShardedTable:
         if self.comm:
             g = self._a2a_rows(g, bufs=bufs, tag="grad_", keep_wire=True)
             if self.world > 1:
-                # several ranks may have asked for the same row: merge (the -1 bucket of
-                # empty slots collects their rows and is skipped by the update)
+                # several ranks may have asked for the same row: merge (empty slots, local
+                # row -1, have inverse -1: the merge skips them and the -1 fill of rows_u
+                # past the distinct rows is skipped by the update)
                 from euler_amd.ops.gnn_ops import unique_first_padded
 
                 rows_u, inv, _ = unique_first_padded(rows)
@@ -174,7 +175,8 @@ class ShardedTable:
                 if use_hip(acc, inv):
                     hip().index_add_rows_(acc, inv.contiguous(), g)
                 else:
-                    acc.index_add_(0, inv, g.float())
+                    keep = inv >= 0
+                    acc.index_add_(0, inv[keep], g[keep].float())
                 rows, g = rows_u, acc
         self._update(rows.contiguous(), g)
 

@@ -107,6 +107,51 @@ def test_gat_fused_matches_reference(cuda, H, C, dtype):
 
 
 @pytest.mark.gpu
+def test_gat_composed_mp_ops_grads_match_torch(cuda):
+    """The composed GAT of benchmarks/bench_gat.py (--impl composed: mp_ops gather,
+    scatter_softmax and scatter_add kernels under autograd) against index ops + a
+    per-destination softmax in plain fp32 torch: forward and every input gradient."""
+    from euler_amd.ops import mp_ops
+
+    torch.manual_seed(14)
+    N, E, H, C = 900, 12000, 4, 8
+    ei = _graph(N, N, E, cuda, seed=15)
+    ei = ei[:, torch.argsort(ei[0])]  # destination-sorted like EdgeCSR.edge_index
+    z = torch.randn(N, H, C, device=cuda, requires_grad=True)
+    a_s = (torch.randn(H, C, device=cuda) * 0.3).requires_grad_(True)
+    a_d = (torch.randn(H, C, device=cuda) * 0.3).requires_grad_(True)
+    seg = mp_ops.SegmentIndex(ei[0].long(), N)
+
+    def composed(z, a_s, a_d):
+        al, ar = (z * a_s).sum(-1), (z * a_d).sum(-1)
+        logit = torch.nn.functional.leaky_relu(mp_ops.gather(ar, ei[0]) + mp_ops.gather(al, ei[1]), 0.2)
+        alpha = mp_ops.scatter_softmax(logit, seg, N)
+        msg = mp_ops.gather(z.reshape(-1, H * C), ei[1]).view(-1, H, C) * alpha.unsqueeze(-1)
+        return mp_ops.scatter_add(msg.reshape(-1, H * C), seg, N).view(-1, H, C)
+
+    def plain(z, a_s, a_d):
+        al, ar = (z * a_s).sum(-1), (z * a_d).sum(-1)
+        d, s = ei[0].long(), ei[1].long()
+        logit = torch.nn.functional.leaky_relu(ar[d] + al[s], 0.2)
+        mx = torch.full((N, H), -1e30, device=cuda).scatter_reduce(0, d.unsqueeze(1).expand(-1, H), logit, "amax")
+        ex = torch.exp(logit - mx[d])
+        den = torch.zeros(N, H, device=cuda).index_add(0, d, ex)
+        alpha = ex / den[d]
+        return torch.zeros(N, H, C, device=cuda).index_add(0, d, z[s] * alpha.unsqueeze(-1))
+
+    g = torch.randn(N, H, C, device=cuda)
+    out = composed(z, a_s, a_d)
+    (out * g).sum().backward()
+    grads = [t.grad.clone() for t in (z, a_s, a_d)]
+    z2, s2, d2 = (t.detach().clone().requires_grad_(True) for t in (z, a_s, a_d))
+    ref = plain(z2, s2, d2)
+    (ref * g).sum().backward()
+    torch.testing.assert_close(out, ref, atol=1e-4, rtol=1e-4)
+    for a, b in zip(grads, (z2.grad, s2.grad, d2.grad)):
+        torch.testing.assert_close(a, b, atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("H,C,dtype", [(8, 16, torch.bfloat16), (4, 8, torch.float32)])
 def test_gat_conv_full_graph(cuda, H, C, dtype):
     torch.manual_seed(12)
@@ -272,6 +317,25 @@ def test_kg_score_matches_reference(cuda, kind, corrupt, normalize, D, Ne):
     torch.testing.assert_close(ns, rn, atol=1e-4, rtol=1e-4)
     torch.testing.assert_close(ent.grad, ent2.grad, atol=1e-4, rtol=1e-3)
     torch.testing.assert_close(rel.grad, rel2.grad, atol=1e-4, rtol=1e-3)
+
+
+def test_unique_first_padded_skips_padding_cpu():
+    x = torch.tensor([5, -1, 3, 5, -1, -1, 9, 3])
+    u, inv, cnt = G.unique_first_padded(x)
+    assert u.tolist() == [5, 3, 9, -1, -1, -1, -1, -1] and int(cnt) == 3
+    assert inv.tolist() == [0, -1, 1, 0, -1, -1, 2, 1]
+
+
+@pytest.mark.gpu
+def test_unique_first_padded_gpu_matches_cpu(cuda):
+    """padding ids (< 0, many copies) are not keys on the GPU either: same uniq / inverse /
+    count as the CPU composition"""
+    torch.manual_seed(9)
+    x = torch.randint(0, 3000, (50000,))
+    x[torch.rand(50000) < 0.3] = -1
+    u_c, i_c, n_c = G.unique_first_padded(x)
+    u_g, i_g, n_g = G.unique_first_padded(x.to(cuda))
+    assert torch.equal(u_g.cpu(), u_c) and torch.equal(i_g.cpu(), i_c) and int(n_g) == int(n_c)
 
 
 @pytest.mark.gpu

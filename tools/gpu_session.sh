@@ -151,6 +151,12 @@ for st in "${S[@]}"; do
         run "kgs_${t}_l${l}_lr${lr}_m${mg}" 600 python -u benchmarks/bench_kg.py --task $t --layers $l --normalize 0 \
           --lr $lr --margin $mg --eval-after "${KG_STEPS:-3000}" || exit $?
       done ;;
+    kg_dw_sweep)
+      # KG_DW="chunk:slab ..." (rel_gemm_dw edges per chunk, slab width)
+      for c in ${KG_DW:-512:128 256:128 1024:128 512:64 256:64}; do
+        EULER_AMD_RG_CH=${c%%:*} EULER_AMD_RG_DW_T=${c##*:} run "kg_dw_${c%%:*}_${c##*:}" 300 \
+          python -u benchmarks/bench_kg.py --steps 100 --warmup 10 --eval-after 0 || exit $?
+      done ;;
     kg_prof)
       run kg_prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/kg_prof" -o run --output-format csv -- \
           python3 benchmarks/bench_kg.py --steps 50 --warmup 5 --eval-after 0 ;;
