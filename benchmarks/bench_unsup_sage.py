@@ -120,7 +120,7 @@ def main(argv=None):
            "heldout_link_auc_init": round(auc0, 4), "heldout_link_auc": round(auc1, 4),
            "config": {k: getattr(args, k) for k in ("num_nodes", "num_comm", "avg_degree", "feature_dim", "signal",
                                                      "batch_size", "fanouts", "dims", "num_negs", "lr")},
-           "impl": "euler_amd.models.sage_tower.UnsupSageTrainer (fused layer-0 tower kernels + torch head)",
+           "impl": "euler_amd.models.sage_tower.UnsupSageTrainer (fused layer-0 tower kernels; tower heads, weight gradients and pair loss on the hand-written GEMM / pair kernels)",
            "data": "synthetic planted communities, features = weak community cue + noise"}
     print(json.dumps(out), flush=True)
     return out

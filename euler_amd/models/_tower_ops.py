@@ -24,7 +24,7 @@ import torch.nn.functional as F
 # products of the tower heads: "gemm" = the tiled MFMA kernel (gemm.hip), "torch" = torch
 # matmuls (hipBLASLt; fp32 A1); "mixed" = the kernel for the row-parallel products, torch
 # for the [R]-row weight-gradient reductions
-_HEAD_GEMM = os.environ.get("EULER_AMD_TOWER_GEMM", "mixed")
+_HEAD_GEMM = os.environ.get("EULER_AMD_TOWER_GEMM", "gemm")
 
 
 def _mm(a, b, out=None, trans_a=False, trans_b=False, relu=False, bias=None, rmask=None, wgrad=False):

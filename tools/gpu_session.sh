@@ -125,6 +125,8 @@ for st in "${S[@]}"; do
         run "bench_gat_$impl" 900 python -u benchmarks/bench_gat.py --impl $impl \
           --num-nodes "${GAT_NODES:-1000000}" --eval-epochs "${GAT_EPOCHS:-400}" || exit $?
       done ;;
+    gat_ab)
+      run gat_ab 600 python -u tools/gat_ab.py ;;
     gat_variants)
       # GAT_VARIANTS="-DGAT_FWD_U=4|-DGAT_FWD_U=8": rebuild gat.hip per flag set, time the edge kernels
       IFS='|' read -ra VL <<< "${GAT_VARIANTS:-}"
