@@ -84,6 +84,21 @@ __device__ __forceinline__ float u01(uint32_t x) { return (x >> 8) * (1.0f / 167
 
 __host__ __device__ __forceinline__ int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// One-thread-per-item kernels over possibly more than 2^32 items (an [E, 128] message
+// tensor of a 50M-edge graph has 6.4e9 elements): a dispatch counts its work-items in 32
+// bits, so a grid of ceil(n / 256) blocks would wrap and silently drop most of the items.
+// Launch grid_for(n) (capped) and loop with grid_stride inside the kernel.
+constexpr int64_t kMaxGridBlocks = int64_t{1} << 22;  // 2^30 work-items per dispatch
+inline dim3 grid_for(int64_t n, int threads = 256) {
+  const int64_t b = ceil_div(n, threads);
+  return dim3(static_cast<uint32_t>(b < kMaxGridBlocks ? (b > 0 ? b : 1) : kMaxGridBlocks));
+}
+template <typename F>
+__device__ __forceinline__ void grid_stride(int64_t n, F&& f) {
+  const int64_t step = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < n; t += step) f(t);
+}
+
 // XCD-aware bijective block remap (cdna_hip_programming.md §5 "XCD swizzle must
 // be bijective"): consecutive logical tiles land on the same XCD / L2.
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {

@@ -537,18 +537,18 @@ inline dim3 row_grid(int64_t rows, int lp) {
 __global__ __launch_bounds__(256) void gather_f32_bf16_kernel(const float* __restrict__ x, int64_t n_rows, int D,
                                                               const int64_t* __restrict__ idx, int64_t n,
                                                               bf16_t* __restrict__ out) {
-  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const int D4 = D >> 2;
-  if (t >= n * D4) return;
-  const int64_t e = t / D4;
-  const int d = static_cast<int>(t - e * D4) * 4;
-  const int64_t r = idx[e];
-  float4_t v = {0.f, 0.f, 0.f, 0.f};
-  if (r >= 0 && r < n_rows) v = *reinterpret_cast<const float4_t*>(x + r * D + d);
-  tl2u w;
-  w[0] = pack_bf16x2(v[0], v[1]);
-  w[1] = pack_bf16x2(v[2], v[3]);
-  *reinterpret_cast<tl2u*>(out + e * D + d) = w;
+  grid_stride(n * D4, [&](int64_t t) {
+    const int64_t e = t / D4;
+    const int d = static_cast<int>(t - e * D4) * 4;
+    const int64_t r = idx[e];
+    float4_t v = {0.f, 0.f, 0.f, 0.f};
+    if (r >= 0 && r < n_rows) v = *reinterpret_cast<const float4_t*>(x + r * D + d);
+    tl2u w;
+    w[0] = pack_bf16x2(v[0], v[1]);
+    w[1] = pack_bf16x2(v[2], v[3]);
+    *reinterpret_cast<tl2u*>(out + e * D + d) = w;
+  });
 }
 
 }  // namespace euler_hip
@@ -700,7 +700,7 @@ hipError_t eh_gather_f32_bf16(const float* x, int64_t n_rows, int D, const int64
   if (n == 0) return hipSuccess;
   if (D % 4 != 0) return hipErrorInvalidValue;
   const int64_t tot = n * (D / 4);
-  hipLaunchKernelGGL(gather_f32_bf16_kernel, dim3(static_cast<uint32_t>(ceil_div(tot, 256))), dim3(256), 0, s, x,
+  hipLaunchKernelGGL(gather_f32_bf16_kernel, grid_for(tot), dim3(256), 0, s, x,
                      n_rows, D, idx, n, static_cast<bf16_t*>(out));
   return hipGetLastError();
 }

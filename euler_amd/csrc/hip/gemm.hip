@@ -271,29 +271,30 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmArgs a) {
 
 // sum of the split-K slabs + the epilogue
 __global__ __launch_bounds__(256) void gemm_reduce_kernel(GemmArgs a) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= a.M * a.N) return;
-  const int64_t row = i / a.N, col = i - row * a.N;
-  float v = 0.f;
-  const int64_t MN = a.M * a.N;
-  int s = 0;
-  for (; s + 8 <= a.splits; s += 8) {  // 8 slab loads in flight
-    float t[8];
+
+  grid_stride(a.M * a.N, [&](int64_t i) {
+    const int64_t row = i / a.N, col = i - row * a.N;
+    float v = 0.f;
+    const int64_t MN = a.M * a.N;
+    int s = 0;
+    for (; s + 8 <= a.splits; s += 8) {  // 8 slab loads in flight
+      float t[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) t[u] = a.part[(s + u) * MN + i];
+      for (int u = 0; u < 8; ++u) t[u] = a.part[(s + u) * MN + i];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v += t[u];
-  }
-  for (; s < a.splits; ++s) v += a.part[s * MN + i];
-  if (a.bias) v += a.bias[col];
-  if (a.relu) v = fmaxf(v, 0.f);
-  if (a.rmask) {
-    const float rv = a.r_bf16 ? bf2f(static_cast<const bf16_t*>(a.rmask)[row * a.ldr + col])
-                              : static_cast<const float*>(a.rmask)[row * a.ldr + col];
-    if (!(rv > 0.f)) v = 0.f;
-  }
-  if (a.c_bf16) static_cast<bf16_t*>(a.C)[row * a.ldc + col] = f2bf(v);
-  else static_cast<float*>(a.C)[row * a.ldc + col] = v;
+      for (int u = 0; u < 8; ++u) v += t[u];
+    }
+    for (; s < a.splits; ++s) v += a.part[s * MN + i];
+    if (a.bias) v += a.bias[col];
+    if (a.relu) v = fmaxf(v, 0.f);
+    if (a.rmask) {
+      const float rv = a.r_bf16 ? bf2f(static_cast<const bf16_t*>(a.rmask)[row * a.ldr + col])
+                                : static_cast<const float*>(a.rmask)[row * a.ldr + col];
+      if (!(rv > 0.f)) v = 0.f;
+    }
+    if (a.c_bf16) static_cast<bf16_t*>(a.C)[row * a.ldc + col] = f2bf(v);
+    else static_cast<float*>(a.C)[row * a.ldc + col] = v;
+  });
 }
 
 }  // namespace euler_hip
@@ -315,7 +316,7 @@ hipError_t eh_gemm(const void* A, const void* B, void* C, const float* bias, con
                   static_cast<uint32_t>(splits));
   hipLaunchKernelGGL(gemm_kernel, grid, dim3(256), 0, s, g);
   if (splits > 1)
-    hipLaunchKernelGGL(gemm_reduce_kernel, dim3(static_cast<uint32_t>(ceil_div(M * N, 256))), dim3(256), 0, s, g);
+    hipLaunchKernelGGL(gemm_reduce_kernel, grid_for(M * N), dim3(256), 0, s, g);
   return hipGetLastError();
 }
 
@@ -332,7 +333,7 @@ hipError_t eh_gemm_tn(const void* A, const void* B, void* C, float* part, int64_
                   static_cast<uint32_t>(splits));
   hipLaunchKernelGGL(gemm_tn_kernel, grid, dim3(256), 0, s, g);
   if (splits > 1)
-    hipLaunchKernelGGL(gemm_reduce_kernel, dim3(static_cast<uint32_t>(ceil_div(M * N, 256))), dim3(256), 0, s, g);
+    hipLaunchKernelGGL(gemm_reduce_kernel, grid_for(M * N), dim3(256), 0, s, g);
   return hipGetLastError();
 }
 

@@ -27,13 +27,13 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const uint8_t* __restr
                                                           int64_t n, uint8_t* __restrict__ out) {
   using V = typename Vec<VB>::T;
   const int64_t vpr = row_bytes / VB;
-  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (t >= n * vpr) return;
-  const int64_t e = t / vpr, c = t - e * vpr;
-  const int64_t r = static_cast<int64_t>(idx[e]);
-  V v{};
-  if (r >= 0 && r < n_rows) v = reinterpret_cast<const V*>(x + r * row_bytes)[c];
-  reinterpret_cast<V*>(out + e * row_bytes)[c] = v;
+  grid_stride(n * vpr, [&](int64_t t) {
+    const int64_t e = t / vpr, c = t - e * vpr;
+    const int64_t r = static_cast<int64_t>(idx[e]);
+    V v{};
+    if (r >= 0 && r < n_rows) v = reinterpret_cast<const V*>(x + r * row_bytes)[c];
+    reinterpret_cast<V*>(out + e * row_bytes)[c] = v;
+  });
 }
 
 template <typename T>
@@ -57,53 +57,53 @@ __global__ __launch_bounds__(256) void segment_reduce_kernel(const T* __restrict
                                                              float empty_val, T* __restrict__ out,
                                                              int64_t* __restrict__ argmax) {
   const int groups = (D + 3) / 4;
-  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (t >= S * groups) return;
-  const int64_t s = t / groups;
-  const int d0 = static_cast<int>(t - s * groups) * 4;
-  const int nd = min(4, D - d0);
-  const int64_t a = indptr[s], b = indptr[s + 1];
-  float acc[4];
-  int64_t am[4] = {-1, -1, -1, -1};
+  grid_stride(S * groups, [&](int64_t t) {
+    const int64_t s = t / groups;
+    const int d0 = static_cast<int>(t - s * groups) * 4;
+    const int nd = min(4, D - d0);
+    const int64_t a = indptr[s], b = indptr[s + 1];
+    float acc[4];
+    int64_t am[4] = {-1, -1, -1, -1};
 #pragma unroll
-  for (int i = 0; i < 4; ++i) acc[i] = op == 2 ? -INFINITY : 0.f;
-  // 4 source rows in flight per thread: the perm loads, then the row loads, are issued
-  // back to back instead of one dependent pair per edge
-  constexpr int U = 4;
-  for (int64_t e0 = a; e0 < b; e0 += U) {
-    int64_t row[U];
-    float v[U][4];
+    for (int i = 0; i < 4; ++i) acc[i] = op == 2 ? -INFINITY : 0.f;
+    // 4 source rows in flight per thread: the perm loads, then the row loads, are issued
+    // back to back instead of one dependent pair per edge
+    constexpr int U = 4;
+    for (int64_t e0 = a; e0 < b; e0 += U) {
+      int64_t row[U];
+      float v[U][4];
 #pragma unroll
-    for (int u = 0; u < U; ++u) row[u] = (e0 + u < b) ? (perm ? perm[e0 + u] : e0 + u) : -1;
+      for (int u = 0; u < U; ++u) row[u] = (e0 + u < b) ? (perm ? perm[e0 + u] : e0 + u) : -1;
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+      for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[u][i] = (row[u] >= 0 && i < nd) ? ld<T>(src + row[u] * D + d0 + i) : 0.f;
+        for (int i = 0; i < 4; ++i) v[u][i] = (row[u] >= 0 && i < nd) ? ld<T>(src + row[u] * D + d0 + i) : 0.f;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (row[u] < 0) continue;
+      for (int u = 0; u < U; ++u) {
+        if (row[u] < 0) continue;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if (i < nd) {
-          if (op == 2) {
-            if (v[u][i] > acc[i]) { acc[i] = v[u][i]; am[i] = row[u]; }
-          } else {
-            acc[i] += v[u][i];
+        for (int i = 0; i < 4; ++i) {
+          if (i < nd) {
+            if (op == 2) {
+              if (v[u][i] > acc[i]) { acc[i] = v[u][i]; am[i] = row[u]; }
+            } else {
+              acc[i] += v[u][i];
+            }
           }
         }
       }
     }
-  }
-  const float inv = (op == 1 && b > a) ? 1.f / static_cast<float>(b - a) : 1.f;
+    const float inv = (op == 1 && b > a) ? 1.f / static_cast<float>(b - a) : 1.f;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if (i < nd) {
-      float v = acc[i] * inv;
-      if (b == a) v = (op == 2) ? empty_val : 0.f;
-      st<T>(out + s * D + d0 + i, v);
-      if (argmax) argmax[s * D + d0 + i] = am[i];
+    for (int i = 0; i < 4; ++i) {
+      if (i < nd) {
+        float v = acc[i] * inv;
+        if (b == a) v = (op == 2) ? empty_val : 0.f;
+        st<T>(out + s * D + d0 + i, v);
+        if (argmax) argmax[s * D + d0 + i] = am[i];
+      }
     }
-  }
+  });
 }
 
 // 16-byte-vector form of segment_reduce for D % V == 0 (V = 8 bf16 / 4 fp32 columns per
@@ -148,57 +148,57 @@ __global__ __launch_bounds__(256) void segment_reduce_vec_kernel(const T* __rest
                                                                  int64_t* __restrict__ argmax) {
   constexpr int V = SegVec<T>::V;
   const int groups = D / V;
-  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (t >= S * groups) return;
-  const int64_t s = t / groups;
-  const int d0 = static_cast<int>(t - s * groups) * V;
-  const int64_t a = indptr[s], b = indptr[s + 1];
-  float acc[V];
-  int64_t am[V];
+  grid_stride(S * groups, [&](int64_t t) {
+    const int64_t s = t / groups;
+    const int d0 = static_cast<int>(t - s * groups) * V;
+    const int64_t a = indptr[s], b = indptr[s + 1];
+    float acc[V];
+    int64_t am[V];
 #pragma unroll
-  for (int i = 0; i < V; ++i) {
-    acc[i] = op == 2 ? -INFINITY : 0.f;
-    am[i] = -1;
-  }
-  constexpr int U = 8;
-  for (int64_t e0 = a; e0 < b; e0 += U) {
-    int64_t row[U];
-    float v[U][V];
-#pragma unroll
-    for (int u = 0; u < U; ++u) row[u] = (e0 + u < b) ? (perm ? perm[e0 + u] : e0 + u) : -1;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (row[u] >= 0) {
-        SegVec<T>::load(src + row[u] * D + d0, v[u]);
-      } else {
-#pragma unroll
-        for (int i = 0; i < V; ++i) v[u][i] = 0.f;
-      }
+    for (int i = 0; i < V; ++i) {
+      acc[i] = op == 2 ? -INFINITY : 0.f;
+      am[i] = -1;
     }
+    constexpr int U = 8;
+    for (int64_t e0 = a; e0 < b; e0 += U) {
+      int64_t row[U];
+      float v[U][V];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (row[u] < 0) continue;
+      for (int u = 0; u < U; ++u) row[u] = (e0 + u < b) ? (perm ? perm[e0 + u] : e0 + u) : -1;
 #pragma unroll
-      for (int i = 0; i < V; ++i) {
-        if (op == 2) {
-          if (v[u][i] > acc[i]) {
-            acc[i] = v[u][i];
-            am[i] = row[u];
-          }
+      for (int u = 0; u < U; ++u) {
+        if (row[u] >= 0) {
+          SegVec<T>::load(src + row[u] * D + d0, v[u]);
         } else {
-          acc[i] += v[u][i];
+#pragma unroll
+          for (int i = 0; i < V; ++i) v[u][i] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (row[u] < 0) continue;
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+          if (op == 2) {
+            if (v[u][i] > acc[i]) {
+              acc[i] = v[u][i];
+              am[i] = row[u];
+            }
+          } else {
+            acc[i] += v[u][i];
+          }
         }
       }
     }
-  }
-  const float inv = (op == 1 && b > a) ? 1.f / static_cast<float>(b - a) : 1.f;
+    const float inv = (op == 1 && b > a) ? 1.f / static_cast<float>(b - a) : 1.f;
 #pragma unroll
-  for (int i = 0; i < V; ++i) acc[i] = b == a ? (op == 2 ? empty_val : 0.f) : acc[i] * inv;
-  SegVec<T>::store(out + s * D + d0, acc);
-  if (argmax) {
+    for (int i = 0; i < V; ++i) acc[i] = b == a ? (op == 2 ? empty_val : 0.f) : acc[i] * inv;
+    SegVec<T>::store(out + s * D + d0, acc);
+    if (argmax) {
 #pragma unroll
-    for (int i = 0; i < V; ++i) argmax[s * D + d0 + i] = am[i];
-  }
+      for (int i = 0; i < V; ++i) argmax[s * D + d0 + i] = am[i];
+    }
+  });
 }
 
 // wave-per-segment sum / mean for skewed segment lengths (power-law in-degrees: a hot
@@ -211,45 +211,47 @@ __global__ __launch_bounds__(256) void segment_reduce_wave_kernel(const T* __res
                                                                   const int64_t* __restrict__ perm, int64_t S, int op,
                                                                   T* __restrict__ out) {
   constexpr int V = SegVec<T>::V;
-  const int64_t s = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
-  if (s >= S) return;  // uniform per wave
   const int LP = D / V, R = 64 / LP;
   const int lane = threadIdx.x & 63, slot = lane / LP, d0 = (lane - slot * LP) * V;
-  const int64_t a = indptr[s], b = indptr[s + 1];
-  float acc[V];
+  // one segment per wave and iteration (uniform per wave); capped grid, see grid_for
+  for (int64_t s = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6); s < S;
+       s += static_cast<int64_t>(gridDim.x) * 4) {
+    const int64_t a = indptr[s], b = indptr[s + 1];
+    float acc[V];
 #pragma unroll
-  for (int i = 0; i < V; ++i) acc[i] = 0.f;
-  constexpr int U = 4;
-  for (int64_t e0 = a + slot; e0 < b; e0 += static_cast<int64_t>(R) * U) {
-    int64_t row[U];
+    for (int i = 0; i < V; ++i) acc[i] = 0.f;
+    constexpr int U = 4;
+    for (int64_t e0 = a + slot; e0 < b; e0 += static_cast<int64_t>(R) * U) {
+      int64_t row[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t e = e0 + static_cast<int64_t>(u) * R;
-      row[u] = e < b ? (perm ? perm[e] : e) : -1;
-    }
-    float v[U][V];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (row[u] >= 0) {
-        SegVec<T>::load(src + row[u] * D + d0, v[u]);
-      } else {
-#pragma unroll
-        for (int i = 0; i < V; ++i) v[u][i] = 0.f;
+      for (int u = 0; u < U; ++u) {
+        const int64_t e = e0 + static_cast<int64_t>(u) * R;
+        row[u] = e < b ? (perm ? perm[e] : e) : -1;
       }
+      float v[U][V];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (row[u] >= 0) {
+          SegVec<T>::load(src + row[u] * D + d0, v[u]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < V; ++i) v[u][i] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int i = 0; i < V; ++i) acc[i] += v[u][i];
     }
+    for (int off = LP; off < 64; off <<= 1)
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+      for (int i = 0; i < V; ++i) acc[i] += __shfl_xor(acc[i], off, 64);
+    if (slot == 0) {
+      const float inv = (op == 1 && b > a) ? 1.f / static_cast<float>(b - a) : 1.f;
 #pragma unroll
-      for (int i = 0; i < V; ++i) acc[i] += v[u][i];
-  }
-  for (int off = LP; off < 64; off <<= 1)
-#pragma unroll
-    for (int i = 0; i < V; ++i) acc[i] += __shfl_xor(acc[i], off, 64);
-  if (slot == 0) {
-    const float inv = (op == 1 && b > a) ? 1.f / static_cast<float>(b - a) : 1.f;
-#pragma unroll
-    for (int i = 0; i < V; ++i) acc[i] *= inv;
-    SegVec<T>::store(out + s * D + d0, acc);
+      for (int i = 0; i < V; ++i) acc[i] *= inv;
+      SegVec<T>::store(out + s * D + d0, acc);
+    }
   }
 }
 
@@ -257,25 +259,25 @@ template <typename T>
 __global__ __launch_bounds__(256) void index_add_rows_kernel(const T* __restrict__ src, int D,
                                                              const int64_t* __restrict__ idx, int64_t n,
                                                              float* __restrict__ out, int64_t n_out) {
-  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (t >= n * D) return;
-  const int64_t e = t / D;
-  const int d = static_cast<int>(t - e * D);
-  const int64_t r = idx[e];
-  if (r < 0 || r >= n_out) return;
-  atomicAdd(out + r * D + d, ld<T>(src + t));
+  grid_stride(n * D, [&](int64_t t) {
+    const int64_t e = t / D;
+    const int d = static_cast<int>(t - e * D);
+    const int64_t r = idx[e];
+    if (r < 0 || r >= n_out) return;
+    atomicAdd(out + r * D + d, ld<T>(src + t));
+  });
 }
 
 // max backward: grad_src[argmax[s,d], d] = grad_out[s,d]  (argmax positions are unique)
 template <typename T>
 __global__ __launch_bounds__(256) void max_bwd_kernel(const T* __restrict__ gout, const int64_t* __restrict__ argmax,
                                                       int64_t S, int D, T* __restrict__ gsrc) {
-  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (t >= S * D) return;
-  const int64_t r = argmax[t];
-  if (r < 0) return;
-  const int d = static_cast<int>(t % D);
-  gsrc[r * D + d] = gout[t];
+  grid_stride(S * D, [&](int64_t t) {
+    const int64_t r = argmax[t];
+    if (r < 0) return;
+    const int d = static_cast<int>(t % D);
+    gsrc[r * D + d] = gout[t];
+  });
 }
 
 // ---------------------------------------------------------------------------
@@ -289,24 +291,24 @@ __global__ __launch_bounds__(256) void edge_softmax_kernel(const T* __restrict__
                                                            const int64_t* __restrict__ indptr,
                                                            const int64_t* __restrict__ perm, int64_t S,
                                                            T* __restrict__ out) {
-  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (t >= S * H) return;
-  const int64_t s = t / H;
-  const int h = static_cast<int>(t - s * H);
-  const int64_t a = indptr[s], b = indptr[s + 1];
-  float m = -INFINITY, l = 0.f;
-  for (int64_t e = a; e < b; ++e) {
-    const int64_t row = perm ? perm[e] : e;
-    const float v = ld<T>(logits + row * H + h);
-    const float nm = fmaxf(m, v);
-    l = l * __expf(m - nm) + __expf(v - nm);
-    m = nm;
-  }
-  const float inv = l > 0.f ? 1.f / l : 0.f;
-  for (int64_t e = a; e < b; ++e) {
-    const int64_t row = perm ? perm[e] : e;
-    st<T>(out + row * H + h, __expf(ld<T>(logits + row * H + h) - m) * inv);
-  }
+  grid_stride(S * H, [&](int64_t t) {
+    const int64_t s = t / H;
+    const int h = static_cast<int>(t - s * H);
+    const int64_t a = indptr[s], b = indptr[s + 1];
+    float m = -INFINITY, l = 0.f;
+    for (int64_t e = a; e < b; ++e) {
+      const int64_t row = perm ? perm[e] : e;
+      const float v = ld<T>(logits + row * H + h);
+      const float nm = fmaxf(m, v);
+      l = l * __expf(m - nm) + __expf(v - nm);
+      m = nm;
+    }
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    for (int64_t e = a; e < b; ++e) {
+      const int64_t row = perm ? perm[e] : e;
+      st<T>(out + row * H + h, __expf(ld<T>(logits + row * H + h) - m) * inv);
+    }
+  });
 }
 
 // softmax backward: g_in = p * (g - sum_seg(p * g))
@@ -315,21 +317,21 @@ __global__ __launch_bounds__(256) void edge_softmax_bwd_kernel(const T* __restri
                                                                int H, const int64_t* __restrict__ indptr,
                                                                const int64_t* __restrict__ perm, int64_t S,
                                                                T* __restrict__ gin) {
-  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (t >= S * H) return;
-  const int64_t s = t / H;
-  const int h = static_cast<int>(t - s * H);
-  const int64_t a = indptr[s], b = indptr[s + 1];
-  float dot = 0.f;
-  for (int64_t e = a; e < b; ++e) {
-    const int64_t row = perm ? perm[e] : e;
-    dot += ld<T>(p + row * H + h) * ld<T>(g + row * H + h);
-  }
-  for (int64_t e = a; e < b; ++e) {
-    const int64_t row = perm ? perm[e] : e;
-    const float pv = ld<T>(p + row * H + h);
-    st<T>(gin + row * H + h, pv * (ld<T>(g + row * H + h) - dot));
-  }
+  grid_stride(S * H, [&](int64_t t) {
+    const int64_t s = t / H;
+    const int h = static_cast<int>(t - s * H);
+    const int64_t a = indptr[s], b = indptr[s + 1];
+    float dot = 0.f;
+    for (int64_t e = a; e < b; ++e) {
+      const int64_t row = perm ? perm[e] : e;
+      dot += ld<T>(p + row * H + h) * ld<T>(g + row * H + h);
+    }
+    for (int64_t e = a; e < b; ++e) {
+      const int64_t row = perm ? perm[e] : e;
+      const float pv = ld<T>(p + row * H + h);
+      st<T>(gin + row * H + h, pv * (ld<T>(g + row * H + h) - dot));
+    }
+  });
 }
 
 // ---------------------------------------------------------------------------
@@ -342,35 +344,35 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(const int64_t* __restrict
                                                        const float* __restrict__ w, const T* __restrict__ x, int D,
                                                        int64_t S, T* __restrict__ out) {
   const int groups = (D + 3) / 4;
-  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (t >= S * groups) return;
-  const int64_t s = t / groups;
-  const int d0 = static_cast<int>(t - s * groups) * 4;
-  const int nd = min(4, D - d0);
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  const int64_t a = indptr[s], b = indptr[s + 1];
-  // 4 neighbour rows in flight per thread (index + weight loads, then the row loads)
-  constexpr int U = 4;
-  for (int64_t e0 = a; e0 < b; e0 += U) {
-    int64_t c[U];
-    float we[U], v[U][4];
+  grid_stride(S * groups, [&](int64_t t) {
+    const int64_t s = t / groups;
+    const int d0 = static_cast<int>(t - s * groups) * 4;
+    const int nd = min(4, D - d0);
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    const int64_t a = indptr[s], b = indptr[s + 1];
+    // 4 neighbour rows in flight per thread (index + weight loads, then the row loads)
+    constexpr int U = 4;
+    for (int64_t e0 = a; e0 < b; e0 += U) {
+      int64_t c[U];
+      float we[U], v[U][4];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      c[u] = (e0 + u < b) ? col[e0 + u] : -1;
-      we[u] = (e0 + u < b && w) ? w[e0 + u] : 1.f;
+      for (int u = 0; u < U; ++u) {
+        c[u] = (e0 + u < b) ? col[e0 + u] : -1;
+        we[u] = (e0 + u < b && w) ? w[e0 + u] : 1.f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[u][i] = (c[u] >= 0 && i < nd) ? ld<T>(x + c[u] * D + d0 + i) : 0.f;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i] += we[u] * v[u][i];
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[u][i] = (c[u] >= 0 && i < nd) ? ld<T>(x + c[u] * D + d0 + i) : 0.f;
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i] += we[u] * v[u][i];
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    if (i < nd) st<T>(out + s * D + d0 + i, acc[i]);
+    for (int i = 0; i < 4; ++i)
+      if (i < nd) st<T>(out + s * D + d0 + i, acc[i]);
+  });
 }
 
 // 16-byte-vector form of spmm_csr for D % V == 0 (SegVec: 8 bf16 / 4 fp32 columns per
@@ -382,38 +384,38 @@ __global__ __launch_bounds__(256) void spmm_csr_vec_kernel(const int64_t* __rest
                                                            int D, int64_t S, T* __restrict__ out) {
   constexpr int V = SegVec<T>::V;
   const int groups = D / V;
-  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (t >= S * groups) return;
-  const int64_t s = t / groups;
-  const int d0 = static_cast<int>(t - s * groups) * V;
-  float acc[V];
+  grid_stride(S * groups, [&](int64_t t) {
+    const int64_t s = t / groups;
+    const int d0 = static_cast<int>(t - s * groups) * V;
+    float acc[V];
 #pragma unroll
-  for (int i = 0; i < V; ++i) acc[i] = 0.f;
-  const int64_t a = indptr[s], b = indptr[s + 1];
-  constexpr int U = 8;
-  for (int64_t e0 = a; e0 < b; e0 += U) {
-    int64_t c[U];
-    float we[U], v[U][V];
+    for (int i = 0; i < V; ++i) acc[i] = 0.f;
+    const int64_t a = indptr[s], b = indptr[s + 1];
+    constexpr int U = 8;
+    for (int64_t e0 = a; e0 < b; e0 += U) {
+      int64_t c[U];
+      float we[U], v[U][V];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      c[u] = (e0 + u < b) ? col[e0 + u] : -1;
-      we[u] = (e0 + u < b && w) ? w[e0 + u] : 1.f;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (c[u] >= 0) {
-        SegVec<T>::load(x + c[u] * D + d0, v[u]);
-      } else {
-#pragma unroll
-        for (int i = 0; i < V; ++i) v[u][i] = 0.f;
+      for (int u = 0; u < U; ++u) {
+        c[u] = (e0 + u < b) ? col[e0 + u] : -1;
+        we[u] = (e0 + u < b && w) ? w[e0 + u] : 1.f;
       }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (c[u] >= 0) {
+          SegVec<T>::load(x + c[u] * D + d0, v[u]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < V; ++i) v[u][i] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int i = 0; i < V; ++i) acc[i] += we[u] * v[u][i];
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int i = 0; i < V; ++i) acc[i] += we[u] * v[u][i];
-  }
-  SegVec<T>::store(out + s * D + d0, acc);
+    SegVec<T>::store(out + s * D + d0, acc);
+  });
 }
 
 }  // namespace euler_hip
@@ -430,7 +432,7 @@ hipError_t eh_gather_rows(const void* x, int64_t n_rows, int64_t row_bytes, cons
   if (!v16 && row_bytes % 4 != 0) return hipErrorInvalidValue;
   const int vb = v16 ? 16 : 4;
   const int64_t total = n * (row_bytes / vb);
-  const dim3 grid(static_cast<uint32_t>(ceil_div(total, 256)));
+  const dim3 grid = grid_for(total);
   const uint8_t* xb = static_cast<const uint8_t*>(x);
   uint8_t* ob = static_cast<uint8_t*>(out);
   if (v16) {
@@ -460,7 +462,7 @@ hipError_t eh_segment_reduce_wave(const void* src, int is_bf16, int D, const int
   if (D % V != 0 || LP > 64 || (LP & (LP - 1)) != 0 || op < 0 || op > 1) return hipErrorInvalidValue;
   if (reinterpret_cast<uintptr_t>(src) % 16 != 0 || reinterpret_cast<uintptr_t>(out) % 16 != 0)
     return hipErrorInvalidValue;
-  const dim3 grid(static_cast<uint32_t>(ceil_div(S, 4)));
+  const dim3 grid = grid_for(S, 4);
   if (is_bf16)
     hipLaunchKernelGGL(segment_reduce_wave_kernel<bf16_t>, grid, dim3(256), 0, s, static_cast<const bf16_t*>(src), D,
                        indptr, perm, S, op, static_cast<bf16_t*>(out));
@@ -475,7 +477,7 @@ hipError_t eh_segment_reduce(const void* src, int is_bf16, int D, const int64_t*
   if (S == 0 || D == 0) return hipSuccess;
   const int V = is_bf16 ? 8 : 4;
   if (D % V == 0 && reinterpret_cast<uintptr_t>(src) % 16 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0) {
-    const dim3 vgrid(static_cast<uint32_t>(ceil_div(S * (D / V), 256)));
+    const dim3 vgrid = grid_for(S * (D / V));
     if (is_bf16)
       hipLaunchKernelGGL(segment_reduce_vec_kernel<bf16_t>, vgrid, dim3(256), 0, s, static_cast<const bf16_t*>(src),
                          D, indptr, perm, S, op, empty_val, static_cast<bf16_t*>(out), argmax);
@@ -484,8 +486,7 @@ hipError_t eh_segment_reduce(const void* src, int is_bf16, int D, const int64_t*
                          indptr, perm, S, op, empty_val, static_cast<float*>(out), argmax);
     return hipGetLastError();
   }
-  const int64_t total = S * ((D + 3) / 4);
-  const dim3 grid(static_cast<uint32_t>(ceil_div(total, 256)));
+  const dim3 grid = grid_for(S * ((D + 3) / 4));
   if (is_bf16)
     hipLaunchKernelGGL(segment_reduce_kernel<bf16_t>, grid, dim3(256), 0, s, static_cast<const bf16_t*>(src), D,
                        indptr, perm, S, op, empty_val, static_cast<bf16_t*>(out), argmax);
@@ -498,7 +499,7 @@ hipError_t eh_segment_reduce(const void* src, int is_bf16, int D, const int64_t*
 hipError_t eh_index_add_rows(const void* src, int is_bf16, int D, const int64_t* idx, int64_t n, float* out,
                              int64_t n_out, hipStream_t s) {
   if (n == 0 || D == 0) return hipSuccess;
-  const dim3 grid(static_cast<uint32_t>(ceil_div(n * D, 256)));
+  const dim3 grid = grid_for(n * D);
   if (is_bf16)
     hipLaunchKernelGGL(index_add_rows_kernel<bf16_t>, grid, dim3(256), 0, s, static_cast<const bf16_t*>(src), D, idx,
                        n, out, n_out);
@@ -511,7 +512,7 @@ hipError_t eh_index_add_rows(const void* src, int is_bf16, int D, const int64_t*
 hipError_t eh_max_bwd(const void* gout, int is_bf16, const int64_t* argmax, int64_t S, int D, void* gsrc,
                       hipStream_t s) {
   if (S == 0 || D == 0) return hipSuccess;
-  const dim3 grid(static_cast<uint32_t>(ceil_div(S * D, 256)));
+  const dim3 grid = grid_for(S * D);
   if (is_bf16)
     hipLaunchKernelGGL(max_bwd_kernel<bf16_t>, grid, dim3(256), 0, s, static_cast<const bf16_t*>(gout), argmax, S, D,
                        static_cast<bf16_t*>(gsrc));
@@ -524,7 +525,7 @@ hipError_t eh_max_bwd(const void* gout, int is_bf16, const int64_t* argmax, int6
 hipError_t eh_edge_softmax(const void* logits, int is_bf16, int H, const int64_t* indptr, const int64_t* perm,
                            int64_t S, void* out, hipStream_t s) {
   if (S == 0 || H == 0) return hipSuccess;
-  const dim3 grid(static_cast<uint32_t>(ceil_div(S * H, 256)));
+  const dim3 grid = grid_for(S * H);
   if (is_bf16)
     hipLaunchKernelGGL(edge_softmax_kernel<bf16_t>, grid, dim3(256), 0, s, static_cast<const bf16_t*>(logits), H,
                        indptr, perm, S, static_cast<bf16_t*>(out));
@@ -537,7 +538,7 @@ hipError_t eh_edge_softmax(const void* logits, int is_bf16, int H, const int64_t
 hipError_t eh_edge_softmax_bwd(const void* p, const void* g, int is_bf16, int H, const int64_t* indptr,
                                const int64_t* perm, int64_t S, void* gin, hipStream_t s) {
   if (S == 0 || H == 0) return hipSuccess;
-  const dim3 grid(static_cast<uint32_t>(ceil_div(S * H, 256)));
+  const dim3 grid = grid_for(S * H);
   if (is_bf16)
     hipLaunchKernelGGL(edge_softmax_bwd_kernel<bf16_t>, grid, dim3(256), 0, s, static_cast<const bf16_t*>(p),
                        static_cast<const bf16_t*>(g), H, indptr, perm, S, static_cast<bf16_t*>(gin));
@@ -552,7 +553,7 @@ hipError_t eh_spmm_csr(const int64_t* indptr, const int64_t* col, const float* w
   if (S == 0 || D == 0) return hipSuccess;
   const int V = is_bf16 ? 8 : 4;
   if (D % V == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0) {
-    const dim3 vgrid(static_cast<uint32_t>(ceil_div(S * (D / V), 256)));
+    const dim3 vgrid = grid_for(S * (D / V));
     if (is_bf16)
       hipLaunchKernelGGL(spmm_csr_vec_kernel<bf16_t>, vgrid, dim3(256), 0, s, indptr, col, w,
                          static_cast<const bf16_t*>(x), D, S, static_cast<bf16_t*>(out));
@@ -561,7 +562,7 @@ hipError_t eh_spmm_csr(const int64_t* indptr, const int64_t* col, const float* w
                          static_cast<const float*>(x), D, S, static_cast<float*>(out));
     return hipGetLastError();
   }
-  const dim3 grid(static_cast<uint32_t>(ceil_div(S * ((D + 3) / 4), 256)));
+  const dim3 grid = grid_for(S * ((D + 3) / 4));
   if (is_bf16)
     hipLaunchKernelGGL(spmm_csr_kernel<bf16_t>, grid, dim3(256), 0, s, indptr, col, w,
                        static_cast<const bf16_t*>(x), D, S, static_cast<bf16_t*>(out));

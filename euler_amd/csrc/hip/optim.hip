@@ -104,41 +104,41 @@ __global__ __launch_bounds__(256) void sparse_optim4_kernel(float* __restrict__ 
                                                             const GT* __restrict__ grads, int64_t n, int D,
                                                             int64_t n_rows, const int64_t* __restrict__ step, float lr,
                                                             float b1, float b2, float eps, int kind) {
-  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const int D4 = D >> 2;
-  if (t >= n * D4) return;
-  const int64_t e = t / D4;
-  const int d = static_cast<int>(t - e * D4) * 4;
-  const int64_t r = rows[e];
-  if (r < 0 || r >= n_rows) return;
-  const int64_t o = r * D + d;
-  const float4_t gi = load_grad4(grads + e * D + d);
-  float4_t p = *reinterpret_cast<float4_t*>(table + o);
-  if (kind == 0) {
-    const float st = static_cast<float>(step[0]);
-    const float bc1 = 1.f - __powf(b1, st), bc2 = 1.f - __powf(b2, st);
-    float4_t mi = *reinterpret_cast<float4_t*>(m + o), vi = *reinterpret_cast<float4_t*>(v + o);
+  grid_stride(n * D4, [&](int64_t t) {
+    const int64_t e = t / D4;
+    const int d = static_cast<int>(t - e * D4) * 4;
+    const int64_t r = rows[e];
+    if (r < 0 || r >= n_rows) return;
+    const int64_t o = r * D + d;
+    const float4_t gi = load_grad4(grads + e * D + d);
+    float4_t p = *reinterpret_cast<float4_t*>(table + o);
+    if (kind == 0) {
+      const float st = static_cast<float>(step[0]);
+      const float bc1 = 1.f - __powf(b1, st), bc2 = 1.f - __powf(b2, st);
+      float4_t mi = *reinterpret_cast<float4_t*>(m + o), vi = *reinterpret_cast<float4_t*>(v + o);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      mi[k] = b1 * mi[k] + (1.f - b1) * gi[k];
-      vi[k] = b2 * vi[k] + (1.f - b2) * gi[k] * gi[k];
-      p[k] -= lr * (mi[k] / bc1) / (sqrtf(vi[k] / bc2) + eps);
+      for (int k = 0; k < 4; ++k) {
+        mi[k] = b1 * mi[k] + (1.f - b1) * gi[k];
+        vi[k] = b2 * vi[k] + (1.f - b2) * gi[k] * gi[k];
+        p[k] -= lr * (mi[k] / bc1) / (sqrtf(vi[k] / bc2) + eps);
+      }
+      *reinterpret_cast<float4_t*>(m + o) = mi;
+      *reinterpret_cast<float4_t*>(v + o) = vi;
+    } else if (kind == 1) {
+      float4_t acc = *reinterpret_cast<float4_t*>(v + o);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        acc[k] += gi[k] * gi[k];
+        p[k] -= lr * gi[k] / (sqrtf(acc[k]) + eps);
+      }
+      *reinterpret_cast<float4_t*>(v + o) = acc;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) p[k] -= lr * gi[k];
     }
-    *reinterpret_cast<float4_t*>(m + o) = mi;
-    *reinterpret_cast<float4_t*>(v + o) = vi;
-  } else if (kind == 1) {
-    float4_t acc = *reinterpret_cast<float4_t*>(v + o);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      acc[k] += gi[k] * gi[k];
-      p[k] -= lr * gi[k] / (sqrtf(acc[k]) + eps);
-    }
-    *reinterpret_cast<float4_t*>(v + o) = acc;
-  } else {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) p[k] -= lr * gi[k];
-  }
-  *reinterpret_cast<float4_t*>(table + o) = p;
+    *reinterpret_cast<float4_t*>(table + o) = p;
+  });
 }
 
 // rows: unique row ids (int64) into the table, grads [n, D] fp32
@@ -147,29 +147,30 @@ __global__ __launch_bounds__(256) void sparse_optim_kernel(float* __restrict__ t
                                                            const float* __restrict__ grads, int64_t n, int D,
                                                            int64_t n_rows, const int64_t* __restrict__ step, float lr,
                                                            float b1, float b2, float eps, int kind) {
-  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (t >= n * D) return;
-  const int64_t e = t / D;
-  const int d = static_cast<int>(t - e * D);
-  const int64_t r = rows[e];
-  if (r < 0 || r >= n_rows) return;
-  const int64_t o = r * D + d;
-  const float gi = grads[t];
-  if (kind == 0) {
-    const float st = static_cast<float>(step[0]);
-    const float mi = b1 * m[o] + (1.f - b1) * gi;
-    const float vi = b2 * v[o] + (1.f - b2) * gi * gi;
-    m[o] = mi;
-    v[o] = vi;
-    const float bc1 = 1.f - __powf(b1, st), bc2 = 1.f - __powf(b2, st);
-    table[o] -= lr * (mi / bc1) / (sqrtf(vi / bc2) + eps);
-  } else if (kind == 1) {
-    const float acc = v[o] + gi * gi;
-    v[o] = acc;
-    table[o] -= lr * gi / (sqrtf(acc) + eps);
-  } else {
-    table[o] -= lr * gi;
-  }
+
+  grid_stride(n * D, [&](int64_t t) {
+    const int64_t e = t / D;
+    const int d = static_cast<int>(t - e * D);
+    const int64_t r = rows[e];
+    if (r < 0 || r >= n_rows) return;
+    const int64_t o = r * D + d;
+    const float gi = grads[t];
+    if (kind == 0) {
+      const float st = static_cast<float>(step[0]);
+      const float mi = b1 * m[o] + (1.f - b1) * gi;
+      const float vi = b2 * v[o] + (1.f - b2) * gi * gi;
+      m[o] = mi;
+      v[o] = vi;
+      const float bc1 = 1.f - __powf(b1, st), bc2 = 1.f - __powf(b2, st);
+      table[o] -= lr * (mi / bc1) / (sqrtf(vi / bc2) + eps);
+    } else if (kind == 1) {
+      const float acc = v[o] + gi * gi;
+      v[o] = acc;
+      table[o] -= lr * gi / (sqrtf(acc) + eps);
+    } else {
+      table[o] -= lr * gi;
+    }
+  });
 }
 
 }  // namespace euler_hip
@@ -204,7 +205,7 @@ hipError_t eh_sparse_optim(float* table, float* m, float* v, const int64_t* rows
   if (n == 0 || D == 0) return hipGetLastError();
   if (grads_bf16 && D % 4 != 0) return hipErrorInvalidValue;
   if (D % 4 == 0) {
-    const dim3 grid(static_cast<uint32_t>(ceil_div(n * (D / 4), 256)));
+    const dim3 grid = grid_for(n * (D / 4));
     if (grads_bf16)
       hipLaunchKernelGGL(sparse_optim4_kernel<bf16_t>, grid, dim3(256), 0, s, table, m, v, rows,
                          static_cast<const bf16_t*>(grads), n, D, n_rows, step, lr, b1, b2, eps, kind);
@@ -213,7 +214,7 @@ hipError_t eh_sparse_optim(float* table, float* m, float* v, const int64_t* rows
                          static_cast<const float*>(grads), n, D, n_rows, step, lr, b1, b2, eps, kind);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(sparse_optim_kernel, dim3(static_cast<uint32_t>(ceil_div(n * D, 256))), dim3(256), 0, s, table,
+  hipLaunchKernelGGL(sparse_optim_kernel, grid_for(n * D), dim3(256), 0, s, table,
                      m, v, rows, static_cast<const float*>(grads), n, D, n_rows, step, lr, b1, b2, eps, kind);
   return hipGetLastError();
 }

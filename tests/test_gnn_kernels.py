@@ -612,3 +612,20 @@ def test_segment_reduce_wave_matches_reference(cuda, dtype, D, op, use_perm):
             ref[s] = xs[a:b].sum(0) / (b - a if op == 1 else 1)
     tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
     torch.testing.assert_close(out.float().cpu(), ref, atol=tol * 10, rtol=tol)
+
+
+@pytest.mark.gpu
+def test_per_item_kernels_cover_more_than_2pow32_items(cuda):
+    """A dispatch counts work-items in 32 bits: one-thread-per-item kernels over > 2^32
+    items (an [E, 128] message tensor of a 50M-edge graph) run on a capped grid with a
+    grid-stride loop (common.h grid_for / grid_stride) instead of silently wrapping — the
+    bug behind the composed GAT's wrong gradients at 1M nodes (profiles/r3_learning/gat_ab/)."""
+    from euler_amd.ops._native import hip
+
+    E, D = (1 << 25) + (1 << 20), 128          # 4.43e9 elements (8.9 GB of bf16 ones)
+    src = torch.ones(E, D, dtype=torch.bfloat16, device=cuda)
+    idx = torch.div(torch.arange(E, device=cuda), 64, rounding_mode="floor")
+    out = torch.zeros(E // 64, D, device=cuda)
+    hip().index_add_rows_(out, idx, src)
+    del src
+    assert float(out.min()) == 64.0 and float(out.max()) == 64.0

@@ -126,7 +126,7 @@ for st in "${S[@]}"; do
           --num-nodes "${GAT_NODES:-1000000}" --eval-epochs "${GAT_EPOCHS:-400}" || exit $?
       done ;;
     gat_ab)
-      run gat_ab 600 python -u tools/gat_ab.py ;;
+      run gat_ab 600 python -u tools/gat_ab.py --num-nodes "${GAT_AB_NODES:-1000000}" ;;
     gat_variants)
       # GAT_VARIANTS="-DGAT_FWD_U=4|-DGAT_FWD_U=8": rebuild gat.hip per flag set, time the edge kernels
       IFS='|' read -ra VL <<< "${GAT_VARIANTS:-}"
