@@ -299,7 +299,10 @@ def test_sgns_matches_reference(cuda, D, dtype):
                                                           # D / 4 a power of two: occurrence rows + segment sums
                                                           # (Ne = 40: hot rows shared by many triples)
                                                           ("l1", "both", True, 128, 40), ("l2", "tail", True, 64, 500)])
-def test_kg_score_matches_reference(cuda, kind, corrupt, normalize, D, Ne):
+@pytest.mark.parametrize("occ", [False, True])
+def test_kg_score_matches_reference(cuda, kind, corrupt, normalize, D, Ne, occ, monkeypatch):
+    # occ: per-occurrence gradient rows + segment sums instead of atomics (EULER_AMD_KG_OCC)
+    monkeypatch.setattr(G, "_KG_OCC", occ)
     torch.manual_seed(7)
     Nr, B, K = 20, 128, 4
     ent = torch.randn(Ne, D, device=cuda).requires_grad_(True)

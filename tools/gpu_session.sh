@@ -153,6 +153,19 @@ for st in "${S[@]}"; do
         run "kgs_${t}_l${l}_lr${lr}_m${mg}" 600 python -u benchmarks/bench_kg.py --task $t --layers $l --normalize 0 \
           --lr $lr --margin $mg --eval-after "${KG_STEPS:-3000}" || exit $?
       done ;;
+    final_benches)
+      # BASELINE.md protocol for the secondary configs: 3 runs of >= 200 timed steps each
+      # (tools/median_summary.py takes the medians)
+      for r in 1 2 3; do
+        run "fb_unsup_$r" 300 python -u benchmarks/bench_unsup_sage.py --steps 1000 || exit $?
+        run "fb_kg_$r" 300 python -u benchmarks/bench_kg.py --steps 200 --warmup 10 --eval-after 0 || exit $?
+        run "fb_dw_$r" 300 python -u benchmarks/bench_deepwalk.py --eval-nodes 0 --mode graph --steps 200 || exit $?
+        run "fb_dw_dist_$r" 300 python -u -m torch.distributed.run --nnodes 1 --nproc-per-node 1 \
+          --master-addr 127.0.0.1 --master-port 2956$r benchmarks/bench_deepwalk.py --eval-nodes 0 --mode graph \
+          --steps 200 --force-dist || exit $?
+        run "fb_gat_$r" 600 python -u benchmarks/bench_gat.py --epochs 200 --eval-epochs 0 || exit $?
+        run "fb_headline_$r" 300 python -u bench.py --steps 1000 --warmup 20 || exit $?
+      done ;;
     kg_dw_sweep)
       # KG_DW="chunk:slab ..." (rel_gemm_dw edges per chunk, slab width)
       for c in ${KG_DW:-512:128 256:128 1024:128 512:64 256:64}; do
