@@ -12,9 +12,13 @@ The step is the framework's training path, euler_amd.models.sage_trainer.SageTra
 2 hops of neighbour sampling on the GPU, forward, backward, optimizer — four gfx950
 launches captured in one hipGraph.  One process per GPU (torchrun): every rank holds
 the whole graph + feature table in its own HBM with its own sample stream; the flat
-gradient is all-reduced over RCCL inside the captured step (fp32 by default, as the
-reference's synchronous gradient sync; --grad-reduce-dtype bf16 halves the bytes and the
-JSON config records which one ran).  Nothing is skipped inside the timed region.
+gradient (fp32 by default, as the reference's synchronous gradient sync; --grad-reduce-dtype
+bf16 halves the bytes) is all-reduced inside the captured step by the two-shot xGMI
+peer-memory all-reduce (parallel/xgmi.py: every rank reads its peers' staged gradients
+directly over the point-to-point links, two cross-GPU barriers instead of a ring's 2 (W-1)
+hops) when its start-up self-test passes on every rank, else by RCCL (--grad-sync rccl
+forces RCCL; the JSON config records which one ran).  Nothing is skipped inside the timed
+region.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [...]
 """
@@ -68,6 +72,12 @@ def parse_args(argv=None):
                         "the timed region still runs exactly --steps steps)")
     p.add_argument("--force-dist", action="store_true",
                    help="take the multi-GPU code path (process group, all-reduce in the step) even with one rank")
+    p.add_argument("--grad-sync", choices=["auto", "xgmi", "rccl"], default="auto",
+                   help="data-parallel gradient all-reduce: auto = the xGMI two-shot kernel with 2+ ranks when its "
+                        "self-test passes on every rank, else RCCL")
+    p.add_argument("--shared-gpu", action="store_true",
+                   help="rehearsal: every rank on cuda:0 with a gloo process group (xGMI all-reduce only; "
+                        "checks the multi-rank step on a one-GPU box)")
     return p.parse_args(argv)
 
 
@@ -102,11 +112,16 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist_on = world > 1 or args.force_dist
+    dist_on = world > 1 or args.force_dist or args.shared_gpu
+    if args.shared_gpu:
+        local_rank = 0
     if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.shared_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (run through gpurun on an MI355X)")
     dev = torch.device("cuda", local_rank)
@@ -142,64 +157,102 @@ def main(argv=None):
         torch.cuda.empty_cache()
     tr = SageTrainer(graph, B, fanouts, dims, args.label_dim, features=feats, labels=labels, learning_rate=args.lr,
                      init_seed=args.seed, keep_samples=False, grad_buckets=args.grad_buckets, feature_shard=fshard)
-    grad_sync = None
+    xar = None
+    sync_name = None
     if dist_on:
         dist.broadcast(tr.flat, 0)
         tr.refresh_shadows()
         tr.set_grad_sync_dtype(args.grad_reduce_dtype)
+        gbuf = tr.grad if getattr(tr, "grad16", None) is None else tr.grad16
+        if args.grad_sync == "xgmi" or (args.grad_sync == "auto" and world > 1) or args.shared_gpu:
+            from euler_amd.parallel.xgmi import XgmiAllReduce
 
-        def grad_sync(g):
-            dist.all_reduce(g)
-            return 1.0 / world
+            xar = XgmiAllReduce(gbuf.numel() * gbuf.element_size())
+            if not xar.self_test(numel=gbuf.numel(), dtype=gbuf.dtype):
+                if args.shared_gpu:
+                    raise SystemExit("--shared-gpu needs the xGMI all-reduce, whose self-test failed")
+                log(f"rank {rank}: xGMI all-reduce self-test failed on some rank; using RCCL")
+                xar = None
 
-    use_graph = not args.no_graph
-    if use_graph:
-        ok = True
-        try:
-            tr.capture(grad_sync, steps=max(1, args.steps_per_graph))
-        except RuntimeError as e:  # e.g. a collective the runtime cannot capture
-            ok = False
-            log(f"rank {rank}: step capture failed ({e}); running eager steps")
-        if dist_on:  # every rank takes the same path (captured collectives never ran)
-            flag = torch.tensor([0 if ok else 1], dtype=torch.int32, device=dev)
-            dist.all_reduce(flag)
-            ok = int(flag.item()) == 0
-        if not ok:
-            tr._graph_exec = None
-            use_graph = False
+    def make_sync(kind):
+        if kind == "xgmi":
+            def grad_sync(g):
+                xar(g)
+                return 1.0 / world
+        else:
+            def grad_sync(g):
+                dist.all_reduce(g)
+                return 1.0 / world
+        return grad_sync
 
-    if use_graph:
-        def run_steps(n):
-            tr.replay_steps(n)
-    else:
-        def run_steps(n):
-            for _ in range(n):
-                tr.step(grad_sync)
+    def timed_run(grad_sync):
+        use_graph = not args.no_graph
+        if use_graph:
+            ok = True
+            try:
+                tr.capture(grad_sync, steps=max(1, args.steps_per_graph))
+            except RuntimeError as e:  # e.g. a collective the runtime cannot capture
+                ok = False
+                log(f"rank {rank}: step capture failed ({e}); running eager steps")
+            if dist_on:  # every rank takes the same path (captured collectives never ran)
+                flag = torch.tensor([0 if ok else 1], dtype=torch.int32, device=dev)
+                dist.all_reduce(flag)
+                ok = int(flag.item()) == 0
+            if not ok:
+                tr._graph_exec = None
+                use_graph = False
 
-    run_steps(args.warmup)
-    torch.cuda.synchronize()
-    first_loss = float(tr.loss.item())
+        if use_graph:
+            def run_steps(n):
+                tr.replay_steps(n)
+        else:
+            def run_steps(n):
+                for _ in range(n):
+                    tr.step(grad_sync)
 
+        run_steps(args.warmup)
+        torch.cuda.synchronize()
+        first_loss = float(tr.loss.item())
+
+        if dist_on:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t_start = time.perf_counter()
+        done = 0
+        while done < args.steps:
+            n = min(args.steps - done, 48 if args.log else args.steps)
+            run_steps(n)
+            done += n
+            if args.log and rank == 0:
+                torch.cuda.synchronize()
+                log(f"step {done} loss {float(tr.loss.item()):.4f}")
+        torch.cuda.synchronize()
+        if dist_on:
+            dist.barrier()
+        elapsed = time.perf_counter() - t_start
+        el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        if dist_on:
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        return float(el.item()), first_loss, use_graph
+
+    grad_sync = None
     if dist_on:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    done = 0
-    while done < args.steps:
-        n = min(args.steps - done, 48 if args.log else args.steps)
-        run_steps(n)
-        done += n
-        if args.log and rank == 0:
+        sync_name = "xgmi" if xar is not None else "rccl"
+        grad_sync = make_sync(sync_name)
+    elapsed, first_loss, use_graph = timed_run(grad_sync)
+    if xar is not None:
+        # a cross-GPU wait that timed out (lost peer) leaves a wrong sum behind, never a hang:
+        # every rank agrees and the measurement is repeated over RCCL
+        flag = torch.tensor([xar.error()], dtype=torch.int32, device=dev if not args.shared_gpu else "cpu")
+        dist.all_reduce(flag)
+        if int(flag.item()) != 0 and not args.shared_gpu:
+            log("xGMI all-reduce timed out on some rank during the run; re-measuring over RCCL")
             torch.cuda.synchronize()
-            log(f"step {done} loss {float(tr.loss.item()):.4f}")
-    torch.cuda.synchronize()
-    if dist_on:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if dist_on:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
+            tr.release_graphs()
+            sync_name = "rccl (xgmi timed out)"
+            elapsed, first_loss, use_graph = timed_run(make_sync("rccl"))
+        elif int(flag.item()) != 0:
+            raise SystemExit("xGMI all-reduce timed out")
     last_loss = float(tr.loss.item())
     if fshard is not None:
         fshard.check_overflow()
@@ -237,8 +290,9 @@ def main(argv=None):
                 "steps_per_graph": args.steps_per_graph if use_graph else None,
                 "feature_sharding": (f"row-sharded over {world} rank(s), per-step all-to-all of the sampled rows"
                                      if fshard is not None else None),
-                "grad_sync": f"rccl all-reduce ({args.grad_reduce_dtype} gradient, {args.grad_buckets} bucket(s)) "
-                             f"in the captured step" if dist_on else None,
+                "grad_sync": (f"{sync_name} all-reduce ({args.grad_reduce_dtype} gradient, {args.grad_buckets} "
+                              f"bucket(s)) in the captured step" if dist_on else None),
+                "shared_gpu_rehearsal": bool(args.shared_gpu) or None,
                 "impl": "euler_amd.models.sage_trainer.SageTrainer (4 fused gfx950 launches per step)",
                 "loss_first_last": [round(first_loss, 4), round(last_loss, 4)],
                 "baseline": base_note,

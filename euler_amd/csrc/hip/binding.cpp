@@ -4,6 +4,9 @@
 // assumes — and launches on torch's current HIP stream so the ops compose with
 // torch streams and hipGraph capture.
 #include <c10/hip/HIPStream.h>
+#include <cstring>
+#include <string>
+#include <vector>
 #include <c10/hip/HIPGuard.h>
 #include <hip/hip_runtime_api.h>
 #include <torch/extension.h>
@@ -456,6 +459,82 @@ void sample_neighbor_into(torch::Tensor indptr, torch::Tensor nbr, torch::Tensor
         "sample_neighbor_into");
 }
 
+
+// ----------------------------------------------------------------------------- xGMI all-reduce
+// One rank's side of the two-shot peer-memory all-reduce (xgmi_ar.hip): owns the rank's
+// uncached IPC buffer, maps the peers' buffers from their IPC handles, launches the kernel on
+// the current stream (hipGraph-capturable: no allocation, no sync).
+class XgmiAr {
+ public:
+  XgmiAr(int64_t cap, double timeout_s) : cap_(cap) {
+    TORCH_CHECK(cap > 0 && cap % 16 == 0, "xgmi all-reduce capacity must be a positive multiple of 16 bytes");
+    check(hipGetDevice(&dev_), "xar get device");
+    check(eh_xar_alloc(cap, &own_), "xar alloc");
+    check(hipMalloc(reinterpret_cast<void**>(&epoch_), eh_xar_max_blocks() * sizeof(uint32_t)), "xar epoch");
+    check(hipMalloc(reinterpret_cast<void**>(&err_), sizeof(int)), "xar err");
+    check(hipMemset(epoch_, 0, eh_xar_max_blocks() * sizeof(uint32_t)), "xar epoch zero");
+    check(hipMemset(err_, 0, sizeof(int)), "xar err zero");
+    int khz = 0;
+    check(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev_), "xar wall clock rate");
+    timeout_ = static_cast<long long>(timeout_s * 1000.0 * (khz > 0 ? khz : 100000));
+    check(hipDeviceSynchronize(), "xar init sync");
+  }
+  ~XgmiAr() {
+    hipSetDevice(dev_);
+    for (size_t r = 0; r < bufs_.size(); ++r)
+      if (static_cast<int>(r) != rank_ && bufs_[r]) hipIpcCloseMemHandle(bufs_[r]);
+    if (own_) hipFree(own_);
+    if (epoch_) hipFree(epoch_);
+    if (err_) hipFree(err_);
+  }
+  py::bytes handle() const {
+    hipIpcMemHandle_t h;
+    check(hipIpcGetMemHandle(&h, own_), "xar ipc handle");
+    return py::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
+  }
+  void open(const std::vector<std::string>& handles, int rank) {
+    const int world = static_cast<int>(handles.size());
+    TORCH_CHECK(world >= 1 && world <= eh_xar_max_ranks() && rank >= 0 && rank < world, "xar: bad world/rank");
+    TORCH_CHECK(bufs_.empty(), "xar: peers already opened");
+    bufs_.assign(world, nullptr);
+    rank_ = rank;
+    for (int r = 0; r < world; ++r) {
+      if (r == rank) {
+        bufs_[r] = own_;
+        continue;
+      }
+      TORCH_CHECK(handles[r].size() == sizeof(hipIpcMemHandle_t), "xar: bad ipc handle size");
+      hipIpcMemHandle_t h;
+      std::memcpy(&h, handles[r].data(), sizeof(h));
+      check(hipIpcOpenMemHandle(&bufs_[r], h, hipIpcMemLazyEnablePeerAccess), "xar ipc open");
+    }
+  }
+  void run(torch::Tensor t, int64_t blocks) {
+    need_cuda(t, "xgmi all-reduce tensor");
+    TORCH_CHECK(!bufs_.empty(), "xar: open() the peers first");
+    TORCH_CHECK(t.get_device() == dev_, "xar: tensor on another device");
+    const bool bf = is_bf16(t, "xgmi all-reduce tensor");
+    check(eh_xar_run(bufs_.data(), static_cast<int>(bufs_.size()), rank_, t.data_ptr(), bf ? 1 : 0, t.numel(), cap_,
+                     static_cast<int>(blocks), epoch_, err_, timeout_, cur_stream()),
+          "xgmi_allreduce");
+  }
+  int error() const {
+    int v = 0;
+    check(hipMemcpy(&v, err_, sizeof(int), hipMemcpyDeviceToHost), "xar read error");
+    return v;
+  }
+  int64_t capacity() const { return cap_; }
+
+ private:
+  int64_t cap_;
+  int dev_ = 0, rank_ = -1;
+  void* own_ = nullptr;
+  uint32_t* epoch_ = nullptr;
+  int* err_ = nullptr;
+  long long timeout_ = 0;
+  std::vector<void*> bufs_;
+};
+
 }  // namespace
 
 // binding_gnn.cpp: GAT / R-GCN / embedding-loss / unique kernels
@@ -490,4 +569,13 @@ PYBIND11_MODULE(_hip_ops, m) {
   m.def("flat_optim_", &flat_optim_);
   m.def("sparse_optim_", &sparse_optim_);
   m.def("sample_neighbor_into", &sample_neighbor_into);
+  py::class_<XgmiAr>(m, "XgmiAr")
+      .def(py::init<int64_t, double>(), py::arg("capacity_bytes"), py::arg("timeout_s") = 2.0)
+      .def("handle", &XgmiAr::handle)
+      .def("open", &XgmiAr::open)
+      .def("run", &XgmiAr::run)
+      .def("error", &XgmiAr::error)
+      .def("capacity", &XgmiAr::capacity);
+  m.attr("xar_max_ranks") = eh_xar_max_ranks();
+  m.attr("xar_max_blocks") = eh_xar_max_blocks();
 }

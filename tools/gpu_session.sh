@@ -246,6 +246,19 @@ for st in "${S[@]}"; do
       for nn in 2000000 100000000; do
         run "tree_kernels_n$nn" 300 python -u tools/tree_kernels.py --num-nodes $nn
       done ;;
+    xgmi)
+      # two-shot xGMI all-reduce: 2 ranks sharing the box's GPU (protocol + capture), the
+      # headline step through it on 2 ranks (rehearsal), and its one-rank cost next to RCCL's
+      run xgmi_test 300 python -u -m pytest tests/test_xgmi.py -x -v --timeout 120 --timeout-method thread \
+        -p no:cacheprovider || exit $?
+      run bench_shared_gpu_2r 600 python -u -m torch.distributed.run --nnodes 1 --nproc-per-node 2 \
+        --master-addr 127.0.0.1 --master-port 29571 bench.py --shared-gpu --num-nodes 2000000 --steps 100 \
+        --warmup 10 || exit $?
+      for gs in xgmi rccl; do
+        run "bench_force_dist_$gs" 600 python -u -m torch.distributed.run --nnodes 1 --nproc-per-node 1 \
+          --master-addr 127.0.0.1 --master-port 29572 bench.py --force-dist --grad-sync $gs --steps 200 \
+          --warmup 20 || exit $?
+      done ;;
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench_small)
