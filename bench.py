@@ -16,8 +16,9 @@ gradient (fp32 by default, as the reference's synchronous gradient sync; --grad-
 bf16 halves the bytes) is all-reduced inside the captured step by the two-shot xGMI
 peer-memory all-reduce (parallel/xgmi.py: every rank reads its peers' staged gradients
 directly over the point-to-point links, two cross-GPU barriers instead of a ring's 2 (W-1)
-hops) when its start-up self-test passes on every rank, else by RCCL (--grad-sync rccl
-forces RCCL; the JSON config records which one ran).  Nothing is skipped inside the timed
+hops) or by RCCL: with 2+ ranks the xGMI kernel's self-test runs on every rank, then both
+are timed on the gradient buffer at start-up and the faster one is used (--grad-sync
+xgmi / rccl forces one; the JSON config records the timings and the choice).  Nothing is skipped inside the timed
 region.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [...]
@@ -159,31 +160,20 @@ def main(argv=None):
                      init_seed=args.seed, keep_samples=False, grad_buckets=args.grad_buckets, feature_shard=fshard)
     xar = None
     sync_name = None
+    sync_info = {}
+    grad_sync = None
     if dist_on:
+        from euler_amd.parallel.xgmi import make_grad_sync
+
         dist.broadcast(tr.flat, 0)
         tr.refresh_shadows()
         tr.set_grad_sync_dtype(args.grad_reduce_dtype)
         gbuf = tr.grad if getattr(tr, "grad16", None) is None else tr.grad16
-        if args.grad_sync == "xgmi" or (args.grad_sync == "auto" and world > 1) or args.shared_gpu:
-            from euler_amd.parallel.xgmi import XgmiAllReduce
-
-            xar = XgmiAllReduce(gbuf.numel() * gbuf.element_size())
-            if not xar.self_test(numel=gbuf.numel(), dtype=gbuf.dtype):
-                if args.shared_gpu:
-                    raise SystemExit("--shared-gpu needs the xGMI all-reduce, whose self-test failed")
-                log(f"rank {rank}: xGMI all-reduce self-test failed on some rank; using RCCL")
-                xar = None
-
-    def make_sync(kind):
-        if kind == "xgmi":
-            def grad_sync(g):
-                xar(g)
-                return 1.0 / world
-        else:
-            def grad_sync(g):
-                dist.all_reduce(g)
-                return 1.0 / world
-        return grad_sync
+        kind = "xgmi" if args.shared_gpu else args.grad_sync
+        grad_sync, sync_name, sync_info = make_grad_sync(gbuf, kind)
+        xar = sync_info.pop("xar")
+        if rank == 0 and sync_info:
+            log(f"gradient all-reduce: {sync_name} ({sync_info})")
 
     def timed_run(grad_sync):
         use_graph = not args.no_graph
@@ -235,10 +225,6 @@ def main(argv=None):
             dist.all_reduce(el, op=dist.ReduceOp.MAX)
         return float(el.item()), first_loss, use_graph
 
-    grad_sync = None
-    if dist_on:
-        sync_name = "xgmi" if xar is not None else "rccl"
-        grad_sync = make_sync(sync_name)
     elapsed, first_loss, use_graph = timed_run(grad_sync)
     if xar is not None:
         # a cross-GPU wait that timed out (lost peer) leaves a wrong sum behind, never a hang:
@@ -250,7 +236,7 @@ def main(argv=None):
             torch.cuda.synchronize()
             tr.release_graphs()
             sync_name = "rccl (xgmi timed out)"
-            elapsed, first_loss, use_graph = timed_run(make_sync("rccl"))
+            elapsed, first_loss, use_graph = timed_run(make_grad_sync(gbuf, "rccl")[0])
         elif int(flag.item()) != 0:
             raise SystemExit("xGMI all-reduce timed out")
     last_loss = float(tr.loss.item())
@@ -292,6 +278,7 @@ def main(argv=None):
                                      if fshard is not None else None),
                 "grad_sync": (f"{sync_name} all-reduce ({args.grad_reduce_dtype} gradient, {args.grad_buckets} "
                               f"bucket(s)) in the captured step" if dist_on else None),
+                "grad_sync_choice": sync_info or None,
                 "shared_gpu_rehearsal": bool(args.shared_gpu) or None,
                 "impl": "euler_amd.models.sage_trainer.SageTrainer (4 fused gfx950 launches per step)",
                 "loss_first_last": [round(first_loss, 4), round(last_loss, 4)],

@@ -179,14 +179,21 @@ def main(argv=None):
 
     eval_init = evaluate()
 
+    grad_sync, sync_name, sync_info = None, None, {}
+    if world > 1:
+        # xGMI two-shot peer-memory all-reduce or RCCL, whichever times faster on this node
+        from euler_amd.parallel.xgmi import make_grad_sync
+
+        grad_sync, sync_name, sync_info = make_grad_sync(flat.grad)
+        sync_info.pop("xar", None)
+
     def step_body():
         opt.zero_grad()
         loss = model(edge_index, edge_rel, *batch())
         loss.backward()
         scale = 1.0
-        if world > 1:
-            dist.all_reduce(flat.grad)
-            scale = 1.0 / world
+        if grad_sync is not None:
+            scale = grad_sync(flat.grad)
         opt.step(scale)
         loss_buf.copy_(loss.detach())
 
@@ -254,6 +261,7 @@ def main(argv=None):
                        "dim": args.dim, "batch_per_gpu": args.batch, "num_negs": args.num_negs,
                        "normalize": norm, "task": args.task, "hipgraph": graph is not None,
                        "parallelism": f"dp{world}", "loss_first_last": [round(first, 4), round(last, 4)],
+                       "grad_sync": sync_name, "grad_sync_choice": sync_info or None,
                        "heldout_tail_ranking": {"triples": int(te_src.numel()), "entities": args.num_ent,
                                                 "after_steps": done, "init": eval_init, "trained": eval_final,
                                                 "chance_mrr": round(sum(1.0 / k for k in range(1, args.num_ent + 1))

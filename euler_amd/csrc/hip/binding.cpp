@@ -469,7 +469,7 @@ class XgmiAr {
   XgmiAr(int64_t cap, double timeout_s) : cap_(cap) {
     TORCH_CHECK(cap > 0 && cap % 16 == 0, "xgmi all-reduce capacity must be a positive multiple of 16 bytes");
     check(hipGetDevice(&dev_), "xar get device");
-    check(eh_xar_alloc(cap, &own_), "xar alloc");
+    check(eh_xar_alloc(cap, &own_sig_, &own_buf_), "xar alloc");
     check(hipMalloc(reinterpret_cast<void**>(&epoch_), eh_xar_max_blocks() * sizeof(uint32_t)), "xar epoch");
     check(hipMalloc(reinterpret_cast<void**>(&err_), sizeof(int)), "xar err");
     check(hipMemset(epoch_, 0, eh_xar_max_blocks() * sizeof(uint32_t)), "xar epoch zero");
@@ -481,32 +481,41 @@ class XgmiAr {
   }
   ~XgmiAr() {
     hipSetDevice(dev_);
-    for (size_t r = 0; r < bufs_.size(); ++r)
-      if (static_cast<int>(r) != rank_ && bufs_[r]) hipIpcCloseMemHandle(bufs_[r]);
-    if (own_) hipFree(own_);
+    for (size_t r = 0; r < bufs_.size(); ++r) {
+      if (static_cast<int>(r) == rank_) continue;
+      if (sigs_[r]) hipIpcCloseMemHandle(sigs_[r]);
+      if (bufs_[r]) hipIpcCloseMemHandle(bufs_[r]);
+    }
+    if (own_sig_) hipFree(own_sig_);
+    if (own_buf_) hipFree(own_buf_);
     if (epoch_) hipFree(epoch_);
     if (err_) hipFree(err_);
   }
+  // the flag area's handle followed by the data area's
   py::bytes handle() const {
-    hipIpcMemHandle_t h;
-    check(hipIpcGetMemHandle(&h, own_), "xar ipc handle");
-    return py::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
+    hipIpcMemHandle_t h[2];
+    check(hipIpcGetMemHandle(&h[0], own_sig_), "xar ipc handle (flags)");
+    check(hipIpcGetMemHandle(&h[1], own_buf_), "xar ipc handle (data)");
+    return py::bytes(reinterpret_cast<const char*>(h), sizeof(h));
   }
   void open(const std::vector<std::string>& handles, int rank) {
     const int world = static_cast<int>(handles.size());
     TORCH_CHECK(world >= 1 && world <= eh_xar_max_ranks() && rank >= 0 && rank < world, "xar: bad world/rank");
     TORCH_CHECK(bufs_.empty(), "xar: peers already opened");
+    sigs_.assign(world, nullptr);
     bufs_.assign(world, nullptr);
     rank_ = rank;
     for (int r = 0; r < world; ++r) {
       if (r == rank) {
-        bufs_[r] = own_;
+        sigs_[r] = own_sig_;
+        bufs_[r] = own_buf_;
         continue;
       }
-      TORCH_CHECK(handles[r].size() == sizeof(hipIpcMemHandle_t), "xar: bad ipc handle size");
-      hipIpcMemHandle_t h;
-      std::memcpy(&h, handles[r].data(), sizeof(h));
-      check(hipIpcOpenMemHandle(&bufs_[r], h, hipIpcMemLazyEnablePeerAccess), "xar ipc open");
+      TORCH_CHECK(handles[r].size() == 2 * sizeof(hipIpcMemHandle_t), "xar: bad ipc handle size");
+      hipIpcMemHandle_t h[2];
+      std::memcpy(h, handles[r].data(), sizeof(h));
+      check(hipIpcOpenMemHandle(&sigs_[r], h[0], hipIpcMemLazyEnablePeerAccess), "xar ipc open (flags)");
+      check(hipIpcOpenMemHandle(&bufs_[r], h[1], hipIpcMemLazyEnablePeerAccess), "xar ipc open (data)");
     }
   }
   void run(torch::Tensor t, int64_t blocks) {
@@ -514,8 +523,8 @@ class XgmiAr {
     TORCH_CHECK(!bufs_.empty(), "xar: open() the peers first");
     TORCH_CHECK(t.get_device() == dev_, "xar: tensor on another device");
     const bool bf = is_bf16(t, "xgmi all-reduce tensor");
-    check(eh_xar_run(bufs_.data(), static_cast<int>(bufs_.size()), rank_, t.data_ptr(), bf ? 1 : 0, t.numel(), cap_,
-                     static_cast<int>(blocks), epoch_, err_, timeout_, cur_stream()),
+    check(eh_xar_run(sigs_.data(), bufs_.data(), static_cast<int>(bufs_.size()), rank_, t.data_ptr(), bf ? 1 : 0,
+                     t.numel(), cap_, static_cast<int>(blocks), epoch_, err_, timeout_, cur_stream()),
           "xgmi_allreduce");
   }
   int error() const {
@@ -528,11 +537,12 @@ class XgmiAr {
  private:
   int64_t cap_;
   int dev_ = 0, rank_ = -1;
-  void* own_ = nullptr;
+  void* own_sig_ = nullptr;
+  void* own_buf_ = nullptr;
   uint32_t* epoch_ = nullptr;
   int* err_ = nullptr;
   long long timeout_ = 0;
-  std::vector<void*> bufs_;
+  std::vector<void*> sigs_, bufs_;
 };
 
 }  // namespace
@@ -578,4 +588,5 @@ PYBIND11_MODULE(_hip_ops, m) {
       .def("capacity", &XgmiAr::capacity);
   m.attr("xar_max_ranks") = eh_xar_max_ranks();
   m.attr("xar_max_blocks") = eh_xar_max_blocks();
+  m.attr("xar_vec_per_thread") = eh_xar_vec_per_thread();
 }

@@ -147,10 +147,10 @@ hipError_t eh_sparse_optim(float* table, float* m, float* v, const int64_t* rows
 
 extern "C" {
 // xgmi_ar.hip: two-shot all-reduce over xGMI peer memory (IPC-mapped uncached buffers)
-int64_t eh_xar_header_bytes();
 int eh_xar_max_ranks();
 int eh_xar_max_blocks();
-hipError_t eh_xar_alloc(int64_t cap, void** out);
-hipError_t eh_xar_run(void* const* bufs, int world, int rank, void* data, int is_bf16, int64_t n, int64_t cap,
-                      int blocks, uint32_t* epoch, int* err, long long timeout, hipStream_t s);
+int eh_xar_vec_per_thread();
+hipError_t eh_xar_alloc(int64_t cap, void** sig, void** data);
+hipError_t eh_xar_run(void* const* sigs, void* const* bufs, int world, int rank, void* data, int is_bf16, int64_t n,
+                      int64_t cap, int blocks, uint32_t* epoch, int* err, long long timeout, hipStream_t s);
 }

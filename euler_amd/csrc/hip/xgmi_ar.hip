@@ -6,7 +6,7 @@
 // peers), so a rank can read every peer's memory directly and the whole reduction takes two
 // phases with one cross-GPU barrier each:
 //
-//   A  stage: copy the local gradient into this rank's IPC buffer `in` (uncached HBM);
+//   A  stage: copy the local gradient into this rank's IPC buffer `in`;
 //      barrier 1 (every block b signals block b of every peer, waits for all of them)
 //   B  reduce-scatter: rank r sums shard r of every peer's `in` (7 remote reads in flight per
 //      thread, one per link, fp32 accumulation) and writes it to `out` (and the local result);
@@ -18,10 +18,14 @@
 // Block b of every rank touches the same element chunks in every phase, so the barriers are
 // per block (no grid-wide sync) and every block's waits depend only on block b of the peers.
 //
-// Memory model: `in`, `out` and the flags live in one hipDeviceMallocUncached allocation per
-// rank, exported with hipIpcGetMemHandle and mapped by the peers; data stores are followed by
-// a system-scope fence in every thread before the block barrier, flags are written with
-// system-scope release stores and polled with system-scope acquire loads.  Every wait is
+// Memory model: per rank, the flags live in a small hipDeviceMallocUncached allocation and
+// `in` / `out` in ordinary HBM (XAR_UNCACHED_DATA=1 puts them in uncached memory too, which
+// measured ~25 us per one-rank call: profiles/r3_xgmi/); both are exported with
+// hipIpcGetMemHandle and mapped by the peers.  Data stores are followed by a system-scope
+// drain (vmcnt) in every wave and a block barrier, then one system-scope release store per
+// peer from wave 0 (its L2 write-back makes the block's data visible over xGMI); flags are
+// polled with system-scope loads and wave 0's system-scope acquire invalidates stale lines
+// before the block reads the peers' data.  Every wait is
 // bounded (wall clock); a timeout sets the error word and lets the grid drain, so a lost peer
 // can never hang the GPU — the caller checks error() and falls back to RCCL.
 //
@@ -43,11 +47,14 @@ constexpr int kArMaxRanks = 8;
 constexpr int kArMaxBlocks = 64;
 constexpr int kArThreads = 256;
 constexpr int64_t kArSigBytes = 2 * kArMaxBlocks * kArMaxRanks * sizeof(uint32_t);
-constexpr int64_t kArHeader = 4096;  // flags, padded so `in` starts 4 KiB aligned
-static_assert(kArSigBytes <= kArHeader, "flag area exceeds the header");
+constexpr int kArVecPerThread = 4;  // 16-byte vectors per thread per shard sweep
+#ifndef XAR_UNCACHED_DATA
+#define XAR_UNCACHED_DATA 0
+#endif
 
 struct ArArgs {
-  char* buf[kArMaxRanks];  // every rank's buffer (own included), identical layout
+  char* sig[kArMaxRanks];  // every rank's flag area (own included)
+  char* buf[kArMaxRanks];  // every rank's data area: in [cap] then out [cap]
   void* data;              // local tensor: input and output, n elements
   int64_t n;               // elements; a multiple of the 16-byte vector width
   int64_t shard;           // elements per rank's shard (multiple of the vector width)
@@ -58,19 +65,26 @@ struct ArArgs {
   long long timeout;       // wall_clock64 ticks per wait
 };
 
-__device__ __forceinline__ uint32_t* ar_sig(char* buf, int which, int b, int r) {
-  return reinterpret_cast<uint32_t*>(buf) + (which * kArMaxBlocks + b) * kArMaxRanks + r;
+__device__ __forceinline__ uint32_t* ar_sig(char* sig, int which, int b, int r) {
+  return reinterpret_cast<uint32_t*>(sig) + (which * kArMaxBlocks + b) * kArMaxRanks + r;
 }
 
-// thread t < world signals peer t; then thread t < world waits for peer t's signal
+// thread t < world (lanes of wave 0) signals peer t, then waits for peer t's signal.  The
+// other waves only drain their own stores (vmcnt(0)) before the block barrier: wave 0's
+// system-scope release (one L2 write-back) then covers the whole block's stores, and its
+// system-scope acquire (one cache invalidation) covers the whole block's later loads.
+// XAR_FENCE_ALL=1: every thread fences at system scope on both sides instead (measured).
+#ifndef XAR_FENCE_ALL
+#define XAR_FENCE_ALL 0
+#endif
 __device__ __forceinline__ void ar_barrier(const ArArgs& a, int which, uint32_t e) {
   const int t = threadIdx.x, b = blockIdx.x;
-  // every thread's stores of this phase are visible at system scope before any signal leaves
-  __threadfence_system();
+  if (XAR_FENCE_ALL) __threadfence_system();
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (t < a.world) {
-    __hip_atomic_store(ar_sig(a.buf[t], which, b, a.rank), e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    const uint32_t* f = ar_sig(a.buf[a.rank], which, b, t);
+    __hip_atomic_store(ar_sig(a.sig[t], which, b, a.rank), e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint32_t* f = ar_sig(a.sig[a.rank], which, b, t);
     const long long t0 = wall_clock64();
     while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
       if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
@@ -83,7 +97,7 @@ __device__ __forceinline__ void ar_barrier(const ArArgs& a, int which, uint32_t 
     __atomic_thread_fence(__ATOMIC_ACQUIRE);  // system scope: the peers' data after their flags
   }
   __syncthreads();
-  __threadfence_system();
+  if (XAR_FENCE_ALL) __threadfence_system();
 }
 
 template <typename T>
@@ -117,6 +131,7 @@ __global__ __launch_bounds__(kArThreads) void xgmi_allreduce_kernel(ArArgs a) {
   if (t == 0) e_s = a.epoch[b] + 1;
   __syncthreads();
   const uint32_t e = e_s;
+  // block b owns vectors [b * kArThreads + t] + k * G * kArThreads of every shard
   const int64_t step = static_cast<int64_t>(G) * kArThreads * V;  // elements per grid sweep of a shard
   const int64_t first = (static_cast<int64_t>(b) * kArThreads + t) * V;
   auto shard_len = [&](int s) {
@@ -124,15 +139,24 @@ __global__ __launch_bounds__(kArThreads) void xgmi_allreduce_kernel(ArArgs a) {
     const int64_t hi = lo + a.shard < a.n ? lo + a.shard : a.n;
     return hi > lo ? hi - lo : int64_t{0};
   };
-  uint4_t* data = reinterpret_cast<uint4_t*>(a.data);
-  auto in_of = [&](int r) { return reinterpret_cast<uint4_t*>(a.buf[r] + kArHeader); };
-  auto out_of = [&](int r) { return reinterpret_cast<uint4_t*>(a.buf[r] + kArHeader + a.cap); };
+  uint4_t* __restrict__ data = reinterpret_cast<uint4_t*>(a.data);
+  auto in_of = [&](int r) { return reinterpret_cast<uint4_t*>(a.buf[r]); };
+  auto out_of = [&](int r) { return reinterpret_cast<uint4_t*>(a.buf[r] + a.cap); };
 
-  // A: stage this rank's input (the chunks block b owns in every shard)
-  uint4_t* my_in = in_of(a.rank);
+  // A: stage this rank's input (the chunks block b owns in every shard); every load of a
+  // sweep is issued before its stores
+  uint4_t* __restrict__ my_in = in_of(a.rank);
   for (int s = 0; s < a.world; ++s) {
     const int64_t len = shard_len(s), base = s * a.shard;
-    for (int64_t o = first; o < len; o += step) my_in[(base + o) / V] = data[(base + o) / V];
+    for (int64_t o0 = first; o0 < len; o0 += kArVecPerThread * step) {
+      uint4_t v[kArVecPerThread];
+#pragma unroll
+      for (int k = 0; k < kArVecPerThread; ++k)
+        if (o0 + k * step < len) v[k] = data[(base + o0 + k * step) / V];
+#pragma unroll
+      for (int k = 0; k < kArVecPerThread; ++k)
+        if (o0 + k * step < len) my_in[(base + o0 + k * step) / V] = v[k];
+    }
   }
   ar_barrier(a, 0, e);
 
@@ -159,12 +183,21 @@ __global__ __launch_bounds__(kArThreads) void xgmi_allreduce_kernel(ArArgs a) {
   }
   ar_barrier(a, 1, e);
 
-  // D: gather every other rank's reduced shard
-  for (int s = 0; s < a.world; ++s) {
-    if (s == a.rank) continue;
-    const int64_t len = shard_len(s), base = s * a.shard;
-    const uint4_t* src = out_of(s);
-    for (int64_t o = first; o < len; o += step) data[(base + o) / V] = src[(base + o) / V];
+  // D: gather every other rank's reduced shard (all loads of a sweep in flight)
+  for (int64_t o0 = first; o0 < a.shard; o0 += kArVecPerThread * step) {
+    uint4_t v[kArVecPerThread][kArMaxRanks];
+#pragma unroll
+    for (int k = 0; k < kArVecPerThread; ++k)
+#pragma unroll
+      for (int s = 0; s < kArMaxRanks; ++s)
+        if (s < a.world && s != a.rank && o0 + k * step < shard_len(s))
+          v[k][s] = out_of(s)[(s * a.shard + o0 + k * step) / V];
+#pragma unroll
+    for (int k = 0; k < kArVecPerThread; ++k)
+#pragma unroll
+      for (int s = 0; s < kArMaxRanks; ++s)
+        if (s < a.world && s != a.rank && o0 + k * step < shard_len(s))
+          data[(s * a.shard + o0 + k * step) / V] = v[k][s];
   }
   if (t == 0) a.epoch[b] = e;
 }
@@ -175,23 +208,26 @@ using namespace euler_hip;
 
 extern "C" {
 
-int64_t eh_xar_header_bytes() { return kArHeader; }
 int eh_xar_max_ranks() { return kArMaxRanks; }
 int eh_xar_max_blocks() { return kArMaxBlocks; }
+int eh_xar_vec_per_thread() { return kArVecPerThread; }
 
-// one rank's buffer: flags + in + out, uncached (coherent across the xGMI peers), zeroed
-hipError_t eh_xar_alloc(int64_t cap, void** out) {
-  const size_t bytes = static_cast<size_t>(kArHeader + 2 * cap);
-  hipError_t e = hipExtMallocWithFlags(out, bytes, hipDeviceMallocUncached);
+// one rank's flag area (uncached: polled across the xGMI peers) and data area (in + out,
+// ordinary HBM unless XAR_UNCACHED_DATA), both zeroed
+hipError_t eh_xar_alloc(int64_t cap, void** sig, void** data) {
+  hipError_t e = hipExtMallocWithFlags(sig, static_cast<size_t>(kArSigBytes), hipDeviceMallocUncached);
   if (e != hipSuccess) return e;
-  e = hipMemset(*out, 0, bytes);
+  if ((e = hipMemset(*sig, 0, static_cast<size_t>(kArSigBytes))) != hipSuccess) return e;
+  const size_t bytes = static_cast<size_t>(2 * cap);
+  e = XAR_UNCACHED_DATA ? hipExtMallocWithFlags(data, bytes, hipDeviceMallocUncached) : hipMalloc(data, bytes);
   if (e != hipSuccess) return e;
+  if ((e = hipMemset(*data, 0, bytes)) != hipSuccess) return e;
   return hipDeviceSynchronize();
 }
 
-// bufs: world pointers (this rank's own and the mapped peers'); blocks <= kArMaxBlocks
-hipError_t eh_xar_run(void* const* bufs, int world, int rank, void* data, int is_bf16, int64_t n, int64_t cap,
-                      int blocks, uint32_t* epoch, int* err, long long timeout, hipStream_t s) {
+// sigs / bufs: world pointers (this rank's own and the mapped peers'); blocks <= kArMaxBlocks
+hipError_t eh_xar_run(void* const* sigs, void* const* bufs, int world, int rank, void* data, int is_bf16, int64_t n,
+                      int64_t cap, int blocks, uint32_t* epoch, int* err, long long timeout, hipStream_t s) {
   if (world < 1 || world > kArMaxRanks || rank < 0 || rank >= world || blocks < 1 || blocks > kArMaxBlocks ||
       !data || !epoch || !err || n < 0)
     return hipErrorInvalidValue;
@@ -201,8 +237,9 @@ hipError_t eh_xar_run(void* const* bufs, int world, int rank, void* data, int is
   if (reinterpret_cast<uintptr_t>(data) % 16 != 0) return hipErrorInvalidValue;
   ArArgs a{};
   for (int r = 0; r < world; ++r) {
-    if (!bufs[r]) return hipErrorInvalidValue;
+    if (!bufs[r] || !sigs[r]) return hipErrorInvalidValue;
     a.buf[r] = static_cast<char*>(bufs[r]);
+    a.sig[r] = static_cast<char*>(sigs[r]);
   }
   a.data = data;
   a.n = n;

@@ -442,11 +442,16 @@ class BaseEstimator:
             return {}
         grad_sync = None
         if self.world > 1:
-            import torch.distributed as tdist
+            # xGMI two-shot peer-memory all-reduce or RCCL on GPUs, whichever the start-up
+            # timing on this node finds faster (parallel/xgmi.py); gloo on CPUs
+            from ..parallel.xgmi import make_grad_sync
 
-            def grad_sync(g):
-                tdist.all_reduce(g)
-                return 1.0 / self.world
+            kind = "auto" if self.device.type == "cuda" else "rccl"
+            gbuf = getattr(tr, "grad16", None)
+            if gbuf is None:
+                gbuf = getattr(tr, "grad", None)
+            grad_sync, name, _ = make_grad_sync(gbuf, str(self.params.get("grad_sync", kind)))
+            log.info("device path gradient sync: %s all-reduce", name)
 
         use_graph = self.device.type == "cuda" and bool(self.params.get("hipgraph", True))
         if use_graph:

@@ -21,6 +21,8 @@ euler_estimator/python/base_estimator.py:164).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -28,10 +30,15 @@ from ..ops._native import hip
 
 
 def _blocks_for(numel: int, world: int, elem_bytes: int) -> int:
-    # one 16-byte vector per thread per shard sweep, 256 threads per block
+    # xar_vec_per_thread 16-byte vectors per thread per shard sweep, 256 threads per block
+    # (EULER_AMD_XAR_BLOCKS overrides, for tuning)
+    env = os.environ.get("EULER_AMD_XAR_BLOCKS")
+    if env:
+        return max(1, min(int(hip().xar_max_blocks), int(env)))
     vec = 16 // elem_bytes
     shard_vecs = -(-numel // (vec * world))
-    return max(1, min(int(hip().xar_max_blocks), -(-shard_vecs // 256)))
+    per_block = 256 * int(hip().xar_vec_per_thread)
+    return max(1, min(int(hip().xar_max_blocks), -(-shard_vecs // per_block)))
 
 
 class XgmiAllReduce:
@@ -90,3 +97,78 @@ class XgmiAllReduce:
             flag = flag.to(dev)
         dist.all_reduce(flag, group=self.group)
         return int(flag.item()) == 0
+
+
+def _graph_call_us(fn, calls: int = 20, reps: int = 3, group=None) -> float:
+    """Per-call time of ``fn`` replayed from a hipGraph of ``calls`` calls (best of ``reps``
+    replays), the MAX over the ranks of ``group`` (every rank gets the same number)."""
+    import time
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(calls):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    best = float("inf")
+    for _ in range(reps):
+        dist.barrier(group=group)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        g.replay()
+        torch.cuda.synchronize()
+        best = min(best, (time.perf_counter() - t0) / calls * 1e6)
+    del g
+    t = torch.tensor([best], dtype=torch.float64)
+    if dist.get_backend(group) == "nccl":
+        t = t.cuda()
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
+
+
+def make_grad_sync(buf: torch.Tensor, kind: str = "auto", group=None):
+    """``grad_sync(g)`` for a data-parallel trainer step (SageTrainer / UnsupSageTrainer
+    ``step(grad_sync)``): an in-place sum all-reduce of (slices of) ``buf`` returning the
+    1 / world scale.  ``kind``: "xgmi" (this module's kernel), "rccl" (torch.distributed
+    all_reduce) or "auto": with 2+ ranks on GPUs, the xGMI kernel's self-test runs on every
+    rank, then both all-reduces are timed on ``buf`` itself (hipGraph-replayed, max over
+    ranks) and the faster one is kept — measured on the node the job runs on, not assumed.
+    Returns ``(grad_sync, name, info)``; ``info`` holds the XgmiAllReduce (``xar``, None for
+    RCCL, whose :meth:`~XgmiAllReduce.error` the caller checks after a run) and the timings."""
+    world = dist.get_world_size(group)
+    info = {"xar": None}
+    xar = None
+    if kind == "xgmi" or (kind == "auto" and world > 1 and buf is not None and buf.is_cuda):
+        xar = XgmiAllReduce(buf.numel() * buf.element_size(), group=group)
+        if not xar.self_test(numel=buf.numel(), dtype=buf.dtype):
+            if kind == "xgmi":
+                raise RuntimeError("xGMI all-reduce self-test failed")
+            info["xgmi_self_test"] = "failed"
+            xar = None
+    if xar is not None and kind == "auto" and dist.get_backend(group) == "nccl":
+        scratch = torch.zeros_like(buf)
+        t_x = _graph_call_us(lambda: xar(scratch), group=group)
+        t_r = _graph_call_us(lambda: dist.all_reduce(scratch, group=group), group=group)
+        info["us_per_call"] = {"xgmi": round(t_x, 2), "rccl": round(t_r, 2)}
+        if xar.error() != 0 or t_r < t_x:
+            xar = None
+    if xar is not None:
+        info["xar"] = xar
+
+        def grad_sync(g):
+            xar(g)
+            return 1.0 / world
+
+        return grad_sync, "xgmi", info
+
+    def grad_sync(g):
+        dist.all_reduce(g, group=group)
+        return 1.0 / world
+
+    return grad_sync, "rccl", info

@@ -117,8 +117,8 @@ def test_xgmi_block_count():
     pytest.importorskip("euler_amd._hip_ops")
     from euler_amd.parallel import xgmi
 
-    # one 16-byte vector per thread and shard sweep, 256 threads per block, capped
-    assert xgmi._blocks_for(278784, 8, 4) == 35
-    assert xgmi._blocks_for(278784, 8, 2) == 18
+    # 4 16-byte vectors per thread and shard sweep, 256 threads per block, capped
+    assert xgmi._blocks_for(278784, 8, 4) == 9
+    assert xgmi._blocks_for(278784, 8, 2) == 5
     assert xgmi._blocks_for(8, 2, 2) == 1
     assert xgmi._blocks_for(1 << 30, 2, 4) == 64

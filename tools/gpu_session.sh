@@ -259,6 +259,35 @@ for st in "${S[@]}"; do
           --master-addr 127.0.0.1 --master-port 29572 bench.py --force-dist --grad-sync $gs --steps 200 \
           --warmup 20 || exit $?
       done ;;
+    xgmi_bench)
+      run xgmi_test 300 python -u -m pytest tests/test_xgmi.py -x -v --timeout 120 --timeout-method thread \
+        -p no:cacheprovider || exit $?
+      for nb in "" 4 16 32 64; do
+        EULER_AMD_XAR_BLOCKS=$nb RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=2958${#nb} \
+          run "xgmi_bench_1r_b${nb:-auto}" 120 python -u tools/xgmi_bench.py --numel 278784 1048576 || exit $?
+      done
+      run xgmi_bench_2r_shared 120 python -u -m torch.distributed.run --nnodes 1 --nproc-per-node 2 \
+        --master-addr 127.0.0.1 --master-port 29589 tools/xgmi_bench.py --shared-gpu || exit $?
+      run "bench_force_dist_xgmi" 600 python -u -m torch.distributed.run --nnodes 1 --nproc-per-node 1 \
+        --master-addr 127.0.0.1 --master-port 29572 bench.py --force-dist --grad-sync xgmi --steps 200 \
+        --warmup 20 ;;
+    xgmi_variants)
+      # XAR_VARIANTS="|-DXAR_FENCE_ALL=1|-DXAR_UNCACHED_DATA=1": rebuild xgmi_ar.hip per flag set,
+      # one-rank call times + the 2-ranks-on-one-GPU test
+      IFS='|' read -ra VL <<< "${XAR_VARIANTS:-}"
+      i=0
+      for v in "${VL[@]}"; do
+        i=$((i+1))
+        touch euler_amd/csrc/hip/xgmi_ar.hip
+        EULER_AMD_HIP_FLAGS="$v" python -m euler_amd._build > "$OUT/build_xar_variant$i.log" 2>&1 || exit 4
+        echo "variant $i: $v" > "$OUT/xar_variant$i.txt"
+        RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=2959$i \
+          run "xgmi_bench_1r_variant$i" 120 python -u tools/xgmi_bench.py --numel 278784 1048576 || exit $?
+        run "xgmi_test_variant$i" 300 python -u -m pytest tests/test_xgmi.py -x -q --timeout 120 \
+          --timeout-method thread -p no:cacheprovider || exit $?
+      done
+      touch euler_amd/csrc/hip/xgmi_ar.hip
+      python -m euler_amd._build > "$OUT/build_xar_default.log" 2>&1 || exit 4 ;;
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench_small)
