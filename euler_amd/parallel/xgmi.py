@@ -35,10 +35,13 @@ def _blocks_for(numel: int, world: int, elem_bytes: int) -> int:
     env = os.environ.get("EULER_AMD_XAR_BLOCKS")
     if env:
         return max(1, min(int(hip().xar_max_blocks), int(env)))
+    # at least 16 blocks (two per XCD): the staging copy moves the WHOLE local tensor, not
+    # one shard, and a few blocks cannot pull ~1 MB out of HBM quickly
     vec = 16 // elem_bytes
     shard_vecs = -(-numel // (vec * world))
     per_block = 256 * int(hip().xar_vec_per_thread)
-    return max(1, min(int(hip().xar_max_blocks), -(-shard_vecs // per_block)))
+    need = -(-shard_vecs // per_block)
+    return max(1, min(int(hip().xar_max_blocks), max(need, min(16, -(-numel // (vec * 256))))))
 
 
 class XgmiAllReduce:

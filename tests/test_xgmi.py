@@ -117,8 +117,11 @@ def test_xgmi_block_count():
     pytest.importorskip("euler_amd._hip_ops")
     from euler_amd.parallel import xgmi
 
-    # 4 16-byte vectors per thread and shard sweep, 256 threads per block, capped
-    assert xgmi._blocks_for(278784, 8, 4) == 9
-    assert xgmi._blocks_for(278784, 8, 2) == 5
+    # 4 16-byte vectors per thread and shard sweep, 256 threads per block, at least 16
+    # blocks when the tensor has that many 256-vector chunks, at most 64
+    assert xgmi._blocks_for(278784, 8, 4) == 16
+    assert xgmi._blocks_for(278784, 8, 2) == 16
+    assert xgmi._blocks_for(278784, 1, 4) == 64
+    assert xgmi._blocks_for(4096, 2, 4) == 4
     assert xgmi._blocks_for(8, 2, 2) == 1
     assert xgmi._blocks_for(1 << 30, 2, 4) == 64
