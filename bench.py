@@ -73,9 +73,10 @@ def parse_args(argv=None):
                         "the timed region still runs exactly --steps steps)")
     p.add_argument("--force-dist", action="store_true",
                    help="take the multi-GPU code path (process group, all-reduce in the step) even with one rank")
-    p.add_argument("--grad-sync", choices=["auto", "xgmi", "rccl"], default="auto",
-                   help="data-parallel gradient all-reduce: auto = the xGMI two-shot kernel with 2+ ranks when its "
-                        "self-test passes on every rank, else RCCL")
+    p.add_argument("--grad-sync", choices=["auto", "xgmi", "rccl", "tune"], default="auto",
+                   help="data-parallel gradient all-reduce: auto = with 2+ ranks, the xGMI two-shot kernel's "
+                        "self-test, then xGMI and RCCL timed on the gradient buffer and the faster kept; tune = "
+                        "the same with one rank too")
     p.add_argument("--shared-gpu", action="store_true",
                    help="rehearsal: every rank on cuda:0 with a gloo process group (xGMI all-reduce only; "
                         "checks the multi-rank step on a one-GPU box)")

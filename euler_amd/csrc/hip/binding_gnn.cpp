@@ -673,18 +673,20 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool trans_a, bool 
 // (pos [n] slot of every id in the W*C exchange space, W*C = none / did not fit; send
 // [W*C + 1] the id of every slot, -1 = empty); overflow [1] int32 is set to 1 when an id
 // did not fit its owner's C slots
-std::vector<torch::Tensor> route_by_owner(torch::Tensor ids, int64_t W, int64_t C, torch::Tensor overflow) {
+std::vector<torch::Tensor> route_by_owner(torch::Tensor ids, int64_t W, int64_t C, torch::Tensor overflow,
+                                          int64_t self_rank) {
   typed(ids, torch::kInt64, "ids");
   typed(overflow, torch::kInt32, "overflow");
   TORCH_CHECK(overflow.numel() >= 1 && overflow.device() == ids.device(), "overflow must be [1] int32 on the ids' device");
-  TORCH_CHECK(W >= 1 && W <= 63 && C >= 1, "route_by_owner: 1 <= W <= 63, C >= 1");
+  TORCH_CHECK(W >= 1 && W <= 63 && C >= 1 && self_rank < W, "route_by_owner: 1 <= W <= 63, C >= 1, self_rank < W");
   const int64_t n = ids.numel();
   const c10::DeviceGuard g(ids.device());
   auto opts = ids.options();
   auto pos = torch::empty({n}, opts);
   auto send = torch::full({W * C + 1}, -1, opts);
   auto cnt = torch::empty({std::max<int64_t>(eh_route_chunks(n), 1) * (W + 1)}, opts.dtype(torch::kInt32));
-  ok(eh_route_by_owner(ids.data_ptr<int64_t>(), n, static_cast<int>(W), C, cnt.data_ptr<int32_t>(),
+  ok(eh_route_by_owner(ids.data_ptr<int64_t>(), n, static_cast<int>(W), C, static_cast<int>(self_rank),
+                       cnt.data_ptr<int32_t>(),
                        pos.data_ptr<int64_t>(), send.data_ptr<int64_t>(), overflow.data_ptr<int32_t>(), stream()),
      "route_by_owner");
   return {pos, send};
@@ -693,7 +695,8 @@ std::vector<torch::Tensor> route_by_owner(torch::Tensor ids, int64_t W, int64_t 
 }  // namespace
 
 void register_gnn_ops(pybind11::module& m) {
-  m.def("route_by_owner", &route_by_owner);
+  m.def("route_by_owner", &route_by_owner, py::arg("ids"), py::arg("W"), py::arg("C"), py::arg("overflow"),
+        py::arg("self_rank") = -1);
   m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("trans_a") = false,
         py::arg("trans_b") = false, py::arg("bias") = py::none(), py::arg("rmask") = py::none(),
         py::arg("relu") = false, py::arg("splits") = 1, py::arg("alpha") = 1.0);

@@ -127,8 +127,8 @@ hipError_t eh_gemm_tn(const void* A, const void* B, void* C, float* part, int64_
 
 // route.hip (owner routing of the fixed-capacity all-to-all exchanges)
 int64_t eh_route_chunks(int64_t n);
-hipError_t eh_route_by_owner(const int64_t* ids, int64_t n, int W, int64_t C, int32_t* cnt, int64_t* pos,
-                             int64_t* send, int32_t* overflow, hipStream_t s);
+hipError_t eh_route_by_owner(const int64_t* ids, int64_t n, int W, int64_t C, int self_rank, int32_t* cnt,
+                             int64_t* pos, int64_t* send, int32_t* overflow, hipStream_t s);
 
 // unique.hip (K8: hash unique, first-occurrence order)
 hipError_t eh_unique_insert(const int64_t* x, int64_t n, void* keys, int32_t* minpos, int64_t cap, int32_t* slot,

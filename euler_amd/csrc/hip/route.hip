@@ -9,6 +9,10 @@
 //           of 256 ids in order: per wave and owner a ballot gives the lane prefix and the
 //           wave count, waves are combined through LDS, the running count carries on.
 // Owners W <= 63 (a ballot per owner bin per round).
+// self_rank >= 0: the caller's own block goes LAST and the peers' blocks keep rank order
+// (block of owner o: o < self ? o : o > self ? o - 1 : W - 1), so the peers' slots are one
+// contiguous prefix that an uneven-split all-to-all sends as it is, and the caller's own
+// ids never travel through the collective (no self-copy); self_rank < 0: block = owner.
 #include "hip/common.h"
 #include "hip/launchers.h"
 
@@ -36,8 +40,13 @@ __global__ __launch_bounds__(kRouteThreads) void route_count_kernel(const int64_
   if (threadIdx.x < NB) cnt[static_cast<int64_t>(blockIdx.x) * NB + threadIdx.x] = c[threadIdx.x];
 }
 
+__device__ __forceinline__ int64_t route_block(int b, int W, int self_rank) {
+  if (self_rank < 0) return b;
+  return b < self_rank ? b : (b > self_rank ? b - 1 : W - 1);
+}
+
 __global__ __launch_bounds__(kRouteThreads) void route_place_kernel(const int64_t* __restrict__ ids, int64_t n,
-                                                                     int W, int64_t C,
+                                                                     int W, int64_t C, int self_rank,
                                                                      const int32_t* __restrict__ cnt,
                                                                      int64_t* __restrict__ pos,
                                                                      int64_t* __restrict__ send,
@@ -77,7 +86,7 @@ __global__ __launch_bounds__(kRouteThreads) void route_place_kernel(const int64_
       int64_t d = trash;
       if (b < W) {
         if (rank < C) {
-          d = static_cast<int64_t>(b) * C + rank;
+          d = route_block(b, W, self_rank) * C + rank;
           send[d] = id;
         } else {
           over = true;
@@ -104,14 +113,14 @@ extern "C" {
 
 int64_t eh_route_chunks(int64_t n) { return ceil_div(n, kRouteChunk); }
 
-hipError_t eh_route_by_owner(const int64_t* ids, int64_t n, int W, int64_t C, int32_t* cnt, int64_t* pos,
-                             int64_t* send, int32_t* overflow, hipStream_t s) {
+hipError_t eh_route_by_owner(const int64_t* ids, int64_t n, int W, int64_t C, int self_rank, int32_t* cnt,
+                             int64_t* pos, int64_t* send, int32_t* overflow, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  if (W < 1 || W + 1 > kRouteMaxBins || C < 1) return hipErrorInvalidValue;
+  if (W < 1 || W + 1 > kRouteMaxBins || C < 1 || self_rank >= W) return hipErrorInvalidValue;
   const uint32_t nb = static_cast<uint32_t>(ceil_div(n, kRouteChunk));
   hipLaunchKernelGGL(route_count_kernel, dim3(nb), dim3(kRouteThreads), 0, s, ids, n, W, cnt);
-  hipLaunchKernelGGL(route_place_kernel, dim3(nb), dim3(kRouteThreads), 0, s, ids, n, W, C, cnt, pos, send,
-                     overflow);
+  hipLaunchKernelGGL(route_place_kernel, dim3(nb), dim3(kRouteThreads), 0, s, ids, n, W, C, self_rank, cnt, pos,
+                     send, overflow);
   return hipGetLastError();
 }
 

@@ -678,15 +678,17 @@ def unique_first_padded(x: torch.Tensor, fill: int = -1):
     return out, inv, torch.tensor([u.numel()], dtype=torch.long, device=x.device)
 
 
-def route_by_owner(ids, W: int, C: int, overflow):
+def route_by_owner(ids, W: int, C: int, overflow, self_rank: int = -1):
     """Slots of the fixed-capacity all-to-all exchange (csrc/hip/route.hip): id k (>= 0)
-    goes to owner ``ids[k] % W`` at slot ``owner * C + r``, r = its stable rank among the
-    ids of that owner; ids < 0 or past an owner's C slots get ``W * C`` (the latter set
-    ``overflow[0] = 1``).  Returns ``(pos [n] int64, send [W*C + 1] int64)``: the slot of
-    every id and the id in every slot (-1 = empty)."""
+    goes to owner ``ids[k] % W`` at slot ``block(owner) * C + r``, r = its stable rank among
+    the ids of that owner; ids < 0 or past an owner's C slots get ``W * C`` (the latter set
+    ``overflow[0] = 1``).  ``block(o) = o`` for ``self_rank < 0``; otherwise the caller's own
+    block is last and the peers keep rank order (o < self: o, o > self: o - 1), so the
+    peers' slots form one prefix.  Returns ``(pos [n] int64, send [W*C + 1] int64)``: the
+    slot of every id and the id in every slot (-1 = empty)."""
     ids = ids.reshape(-1).long()
     if use_hip(ids):
-        return tuple(hip().route_by_owner(ids.contiguous(), int(W), int(C), overflow))
+        return tuple(hip().route_by_owner(ids.contiguous(), int(W), int(C), overflow, int(self_rank)))
     n = ids.numel()
     trash = W * C
     owner = torch.where(ids >= 0, torch.remainder(ids, W), torch.full_like(ids, W))
@@ -698,7 +700,10 @@ def route_by_owner(ids, W: int, C: int, overflow):
     real = so < W
     fits = real & (slot < C)
     torch.maximum(overflow, (real & ~fits).any().int().view(1), out=overflow)
-    dest = torch.where(fits, so * C + slot, torch.full_like(slot, trash))
+    blk = so
+    if self_rank >= 0:
+        blk = torch.where(so < self_rank, so, torch.where(so > self_rank, so - 1, torch.full_like(so, W - 1)))
+    dest = torch.where(fits, blk * C + slot, torch.full_like(slot, trash))
     send = torch.full((trash + 1,), -1, dtype=torch.long, device=ids.device)
     send.scatter_(0, dest, torch.where(fits, ids[order], torch.full_like(slot, -1)))
     send[trash] = -1

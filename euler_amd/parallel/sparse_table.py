@@ -135,49 +135,85 @@ class ShardedTable:
         """first half of :meth:`lookup_static` (no collective): the exchange slots of the
         padded distinct ids -> ``(pos, send)``, for a caller that overlaps the exchange"""
         ids = ids.reshape(-1).long()
-        return route_by_owner(ids, self.world, self.capacity(ids.numel()), self.overflow)
+        return route_by_owner(ids, self.world, self.capacity(ids.numel()), self.overflow, self.rank)
+
+    def _peer_splits(self, C):
+        """equal C-slot splits to / from every peer, none to / from this rank (its own
+        slots are the last block of the layout and never enter the collective)"""
+        return [0 if r == self.rank else int(C) for r in range(self.world)]
 
     def exchange_static(self, routed, trash_row: bool = False, bufs=None, keep_wire: bool = False):
         """second half of :meth:`lookup_static`: the id and row all-to-alls of routed ids
         (``bufs``: persistent buffers for the collectives, see :meth:`_buf`; ``keep_wire``:
-        return the received rows in the wire dtype)"""
+        return the received rows in the wire dtype).
+
+        Slot layout (``route_by_owner(..., self_rank)``): the peers' C-slot blocks in rank
+        order, then this rank's own block.  Only the peers' prefix (W-1)*C goes through the
+        uneven-split all-to-alls; the own block's ids are served here — its rows are gathered
+        straight into the output — so no rank copies its own rows through RCCL (with one
+        rank there is no collective at all)."""
         pos, send = routed
         W = self.world
         trash = send.numel() - 1
-        sd = self._buf(bufs, "send", (trash,), torch.long, send.device)
-        sd.copy_(send[:trash])
-        recv = self._buf(bufs, "recv", (trash,), torch.long, send.device)
-        dist.all_to_all_single(recv, sd, group=self.group)
+        C = trash // W
+        P = trash - C  # the peers' slots
+        dev = send.device
+        recv = self._buf(bufs, "recv", (trash,), torch.long, dev)
+        if P:
+            sd = self._buf(bufs, "send", (P,), torch.long, dev)
+            sd.copy_(send[:P])
+            sp = self._peer_splits(C)
+            dist.all_to_all_single(recv[:P], sd, sp, sp, group=self.group)
+        recv[P:].copy_(send[P:trash])  # own requests
         local = torch.where(recv >= 0, torch.div(recv, W, rounding_mode="floor"), torch.full_like(recv, -1))
-        xw = self._buf(bufs, "rows_in", (trash, self.dim), self.wire, send.device)
-        self._gather_into(local, xw)
-        out = self._a2a_rows(xw, extra=1 if trash_row else 0, bufs=bufs, tag="rows_", keep_wire=keep_wire)
-        return out, StaticHandle(pos, local)
+        extra = 1 if trash_row else 0
+        out = self._buf(bufs, "rows_out", (trash + extra, self.dim), self.wire, dev)
+        if extra:
+            out[trash:].zero_()
+        if P:
+            xw = self._buf(bufs, "rows_in", (P, self.dim), self.wire, dev)
+            self._gather_into(local[:P], xw)
+            dist.all_to_all_single(out[:P], xw, sp, sp, group=self.group)
+        self._gather_into(local[P:], out[P:trash])
+        return (out if keep_wire else out.float()), StaticHandle(pos, local)
 
     def apply_static(self, handle: StaticHandle, grad_rows: torch.Tensor, bufs=None):
         """row-sparse update from gradients [W*C, D] in slot order (rows of empty slots
         are ignored).  fp32 or wire-dtype gradients; a bf16 wire sends them as they are
-        and the optimizer reads them from the receive buffer."""
+        and the optimizer reads them from the receive buffer.  The peers' slots go back to
+        their owners over the all-to-all; the own block's gradients are applied here."""
         g = grad_rows.contiguous()
         if g.dtype not in (torch.float32, self.wire):
             g = g.float()
         rows = handle.local
-        if self.comm:
-            g = self._a2a_rows(g, bufs=bufs, tag="grad_", keep_wire=True)
-            if self.world > 1:
-                # several ranks may have asked for the same row: merge (empty slots, local
-                # row -1, have inverse -1: the merge skips them and the -1 fill of rows_u
-                # past the distinct rows is skipped by the update)
-                from euler_amd.ops.gnn_ops import unique_first_padded
+        if self.comm and self.world > 1:
+            W = self.world
+            trash = g.shape[0]
+            C = trash // W
+            P = trash - C
+            if g.dtype != self.wire:
+                gw = self._buf(bufs, "grad_in", (P, self.dim), self.wire, g.device)
+                gw.copy_(g[:P])
+            else:
+                gw = g[:P]
+            gr = self._buf(bufs, "grad_out", (trash, self.dim), self.wire, g.device)
+            sp = self._peer_splits(C)
+            dist.all_to_all_single(gr[:P], gw, sp, sp, group=self.group)
+            gr[P:].copy_(g[P:])  # own block
+            g = gr
+            # several ranks may have asked for the same row: merge (empty slots, local
+            # row -1, have inverse -1: the merge skips them and the -1 fill of rows_u
+            # past the distinct rows is skipped by the update)
+            from euler_amd.ops.gnn_ops import unique_first_padded
 
-                rows_u, inv, _ = unique_first_padded(rows)
-                acc = torch.zeros(g.shape, dtype=torch.float32, device=g.device)
-                if use_hip(acc, inv):
-                    hip().index_add_rows_(acc, inv.contiguous(), g)
-                else:
-                    keep = inv >= 0
-                    acc.index_add_(0, inv[keep], g[keep].float())
-                rows, g = rows_u, acc
+            rows_u, inv, _ = unique_first_padded(rows)
+            acc = torch.zeros(g.shape, dtype=torch.float32, device=g.device)
+            if use_hip(acc, inv):
+                hip().index_add_rows_(acc, inv.contiguous(), g)
+            else:
+                keep = inv >= 0
+                acc.index_add_(0, inv[keep], g[keep].float())
+            rows, g = rows_u, acc
         self._update(rows.contiguous(), g)
 
     def check_overflow(self):

@@ -139,15 +139,19 @@ def make_grad_sync(buf: torch.Tensor, kind: str = "auto", group=None):
     """``grad_sync(g)`` for a data-parallel trainer step (SageTrainer / UnsupSageTrainer
     ``step(grad_sync)``): an in-place sum all-reduce of (slices of) ``buf`` returning the
     1 / world scale.  ``kind``: "xgmi" (this module's kernel), "rccl" (torch.distributed
-    all_reduce) or "auto": with 2+ ranks on GPUs, the xGMI kernel's self-test runs on every
+    all_reduce), "auto": with 2+ ranks on GPUs, the xGMI kernel's self-test runs on every
     rank, then both all-reduces are timed on ``buf`` itself (hipGraph-replayed, max over
-    ranks) and the faster one is kept — measured on the node the job runs on, not assumed.
+    ranks) and the faster one is kept — measured on the node the job runs on, not assumed —
+    or "tune" (the same, also with one rank).
     Returns ``(grad_sync, name, info)``; ``info`` holds the XgmiAllReduce (``xar``, None for
     RCCL, whose :meth:`~XgmiAllReduce.error` the caller checks after a run) and the timings."""
     world = dist.get_world_size(group)
     info = {"xar": None}
     xar = None
-    if kind == "xgmi" or (kind == "auto" and world > 1 and buf is not None and buf.is_cuda):
+    world_ok = world > 1 or kind == "tune"  # "tune": "auto" also with one rank
+    if kind == "tune":
+        kind = "auto"
+    if kind == "xgmi" or (kind == "auto" and world_ok and buf is not None and buf.is_cuda):
         xar = XgmiAllReduce(buf.numel() * buf.element_size(), group=group)
         if not xar.self_test(numel=buf.numel(), dtype=buf.dtype):
             if kind == "xgmi":

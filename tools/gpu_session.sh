@@ -268,9 +268,14 @@ for st in "${S[@]}"; do
       done
       run xgmi_bench_2r_shared 120 python -u -m torch.distributed.run --nnodes 1 --nproc-per-node 2 \
         --master-addr 127.0.0.1 --master-port 29589 tools/xgmi_bench.py --shared-gpu || exit $?
-      run "bench_force_dist_xgmi" 600 python -u -m torch.distributed.run --nnodes 1 --nproc-per-node 1 \
-        --master-addr 127.0.0.1 --master-port 29572 bench.py --force-dist --grad-sync xgmi --steps 200 \
-        --warmup 20 ;;
+      for gs in xgmi tune; do
+        run "bench_force_dist_$gs" 600 python -u -m torch.distributed.run --nnodes 1 --nproc-per-node 1 \
+          --master-addr 127.0.0.1 --master-port 29572 bench.py --force-dist --grad-sync $gs --steps 200 \
+          --warmup 20 || exit $?
+      done
+      run bench_shared_gpu_2r 600 python -u -m torch.distributed.run --nnodes 1 --nproc-per-node 2 \
+        --master-addr 127.0.0.1 --master-port 29571 bench.py --shared-gpu --num-nodes 2000000 --steps 100 \
+        --warmup 10 ;;
     xgmi_variants)
       # XAR_VARIANTS="|-DXAR_FENCE_ALL=1|-DXAR_UNCACHED_DATA=1": rebuild xgmi_ar.hip per flag set,
       # one-rank call times + the 2-ranks-on-one-GPU test
