@@ -116,12 +116,22 @@ class ShardedFeatures:
             self.cache[:n].copy_(self._gather(local))
             pu = torch.arange(n, device=ids.device)
         else:
-            pu, send = route_by_owner(u, W, C, self.overflow)
-            recv = torch.empty(trash, dtype=torch.long, device=ids.device)
-            dist.all_to_all_single(recv, send[:trash], group=self.group)
-            local = torch.where(recv >= 0, torch.div(recv, W, rounding_mode="floor"), torch.full_like(recv, -1))
-            rows = self._gather(local).to(self.cache.dtype).contiguous()
-            dist.all_to_all_single(self.cache[:trash], rows, group=self.group)
+            # slot layout: the peers' C-slot blocks in rank order, then this rank's own block;
+            # only the peers' prefix goes through the (uneven-split) all-to-alls, the own
+            # block's rows are gathered straight into the cache (no RCCL self-copy; with one
+            # rank no collective at all)
+            pu, send = route_by_owner(u, W, C, self.overflow, self.rank)
+            P = trash - C
+            if P:
+                sp = [0 if r == self.rank else C for r in range(W)]
+                recv = torch.empty(P, dtype=torch.long, device=ids.device)
+                dist.all_to_all_single(recv, send[:P], sp, sp, group=self.group)
+                local = torch.where(recv >= 0, torch.div(recv, W, rounding_mode="floor"), torch.full_like(recv, -1))
+                rows = self._gather(local).to(self.cache.dtype).contiguous()
+                dist.all_to_all_single(self.cache[:P], rows, sp, sp, group=self.group)
+            own = send[P:trash]
+            local = torch.where(own >= 0, torch.div(own, W, rounding_mode="floor"), torch.full_like(own, -1))
+            self.cache[P:trash].copy_(self._gather(local))
         pos = pu if inv is None else pu[inv]
         pos = torch.where(i64 >= 0, pos, torch.full_like(pos, -1)).int()
         if pos_out is not None:

@@ -56,17 +56,31 @@ class XgmiAllReduce:
         if self.world > int(hip().xar_max_ranks):
             raise ValueError(f"xGMI all-reduce supports up to {hip().xar_max_ranks} ranks, got {self.world}")
         cap = -(-int(capacity_bytes) // 4096) * 4096
-        self._ar = hip().XgmiAr(cap, float(timeout_s))
+        # a rank that cannot allocate, export or map still takes part in every collective
+        # below (no rank may hang in the exchange); self_test() then fails on every rank
+        self.setup_error = None
+        try:
+            self._ar = hip().XgmiAr(cap, float(timeout_s))
+            mine = self._ar.handle()
+        except Exception as e:  # noqa: BLE001 - reported through self_test()
+            self._ar, mine, self.setup_error = None, b"", repr(e)
         handles = [None] * self.world
-        dist.all_gather_object(handles, self._ar.handle(), group=group)
-        self._ar.open(handles, self.rank)
+        dist.all_gather_object(handles, mine, group=group)
+        self.ok = self._ar is not None and all(len(h) > 0 for h in handles)
+        if self.ok:
+            try:
+                self._ar.open(handles, self.rank)
+            except Exception as e:  # noqa: BLE001
+                self.ok, self.setup_error = False, repr(e)
         dist.barrier(group=group)  # every buffer zeroed and mapped before any flag is written
 
     @property
     def capacity(self) -> int:
-        return int(self._ar.capacity())
+        return int(self._ar.capacity()) if self._ar is not None else 0
 
     def __call__(self, t: torch.Tensor) -> torch.Tensor:
+        if not self.ok:
+            raise RuntimeError(f"xGMI all-reduce is not set up on this rank: {self.setup_error}")
         if t.numel() * t.element_size() > self.capacity:
             raise ValueError("tensor exceeds the xGMI all-reduce buffer")
         self._ar.run(t, _blocks_for(t.numel(), self.world, t.element_size()))
@@ -74,13 +88,21 @@ class XgmiAllReduce:
 
     def error(self) -> int:
         """1 if a cross-GPU wait timed out on this rank since construction (synchronises)."""
-        return int(self._ar.error())
+        return int(self._ar.error()) if self._ar is not None else 1
 
     def self_test(self, numel: int | None = None, dtype=torch.float32, calls: int = 3) -> bool:
         """Eager check against an RCCL/gloo-free reference: rank r contributes (r + 1) * base
         with a rank-independent ``base``, so every element's sum is known in closed form.
         Returns the all-rank verdict (True only if every rank saw exact results)."""
         dev = torch.device("cuda", torch.cuda.current_device())
+        # every rank must agree that every rank mapped its peers before any kernel runs
+        # (a rank whose peers are not mapped would wait on flags nobody writes)
+        flag = torch.tensor([0 if self.ok else 1], dtype=torch.int32)
+        if dist.get_backend(self.group) == "nccl":
+            flag = flag.to(dev)
+        dist.all_reduce(flag, group=self.group)
+        if int(flag.item()) != 0:
+            return False
         esz = torch.empty((), dtype=dtype).element_size()
         vec = 16 // esz
         n = numel if numel is not None else self.capacity // esz
