@@ -206,8 +206,9 @@ def _worker_sparse_table_static(rank, world, port, q, wire="fp32"):
         from euler_amd.parallel.sparse_table import ShardedTable
 
         torch.manual_seed(0)
-        full = torch.randn(31, 4)
-        tab = ShardedTable(31, 4, "cpu", optimizer="sgd", lr=0.5, wire_dtype=wire)
+        nrows = 31 + world  # ids go up to 29 + rank
+        full = torch.randn(nrows, 4)
+        tab = ShardedTable(nrows, 4, "cpu", optimizer="sgd", lr=0.5, wire_dtype=wire)
         # bf16 on the wire: rows and gradients rounded once (8 mantissa bits)
         tol = dict(rtol=1e-2, atol=1e-2) if wire == "bf16" else {}
         tab.weight.copy_(full[tab.global_ids()])
@@ -288,6 +289,14 @@ def test_sharded_table_fixed_capacity_exchange(wire):
     res = _run(_worker_sparse_table_static, wire)
     assert not [r for r in res if r[1] == "error"], res
     assert len(res) == 2 and all(r[2] for r in res), res
+
+
+def test_sharded_table_fixed_capacity_exchange_four_ranks():
+    """4 ranks: the own-block-last slot layout with the own block in the middle of the
+    rank order (ranks 1, 2), at the front (0) and at the end (3) of the peers' prefix"""
+    res = _run(_worker_sparse_table_static, "fp32", world=4)
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == 4 and all(r[2] for r in res), res
 
 
 @pytest.mark.parametrize("mbs", [1, 2])
@@ -555,7 +564,7 @@ def _worker_sharded_features(rank, world, port, q, dedup):
 
         tr, fs = make(True)
         ref, _ = make(False)
-        assert fs.shard.shape[0] == (ref.features.shape[0] - rank + 1) // 2
+        assert fs.shard.shape[0] == (ref.features.shape[0] - rank + world - 1) // world
 
         def sync(g):
             dist.all_reduce(g)
@@ -575,8 +584,8 @@ def _worker_sharded_features(rank, world, port, q, dedup):
         q.put((rank, "error", traceback.format_exc()))
 
 
-@pytest.mark.parametrize("dedup", [True, False])
-def test_sage_trainer_sharded_features_matches_whole_table(dedup):
-    res = _run(_worker_sharded_features, dedup)
+@pytest.mark.parametrize("dedup,world", [(True, 2), (False, 2), (True, 3)])
+def test_sage_trainer_sharded_features_matches_whole_table(dedup, world):
+    res = _run(_worker_sharded_features, dedup, world=world)
     assert not [r for r in res if r[1] == "error"], res
-    assert len(res) == 2 and all(r[2] for r in res), res
+    assert len(res) == world and all(r[2] for r in res), res
