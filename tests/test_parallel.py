@@ -589,3 +589,36 @@ def test_sage_trainer_sharded_features_matches_whole_table(dedup, world):
     res = _run(_worker_sharded_features, dedup, world=world)
     assert not [r for r in res if r[1] == "error"], res
     assert len(res) == world and all(r[2] for r in res), res
+
+
+def _worker_estimator_device_dp(rank, world, port, q, tmp):
+    """NodeEstimator(device_graph=True) under 2 gloo ranks (runner flags as under torchrun):
+    per-rank sample streams, gradients summed through make_grad_sync every step, so both
+    ranks end with bit-identical trainer parameters."""
+    try:
+        _init(rank, world, port)
+        from euler_amd.tools import runner
+
+        a = runner.parse_args(["--dataset", "ppi", "--scale", "0.05", "--batch_size", "32", "--total_step", "6",
+                               "--log_steps", "3", "--model_dir", os.path.join(tmp, f"ckpt_r{rank}"),
+                               "--device_graph", "--device", "cpu", "--seed", "1", "--fanouts", "5", "3"],
+                              model="graphsage")
+        _, est = runner.build(a)
+        est.train()
+        p = est.device_trainer.logical_params()
+        flat = torch.cat([p[k].reshape(-1).float() for k in sorted(p)])
+        allp = [torch.zeros_like(flat) for _ in range(world)]
+        dist.all_gather(allp, flat)
+        same = all(torch.equal(x, allp[0]) for x in allp)
+        q.put((rank, "estimator_device_dp", bool(same and est.global_step == 6)))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_estimator_device_graph_data_parallel_lockstep(tmp_path):
+    res = _run(_worker_estimator_device_dp, str(tmp_path))
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == 2 and all(r[2] for r in res), res
