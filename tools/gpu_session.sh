@@ -293,6 +293,17 @@ for st in "${S[@]}"; do
       done
       touch euler_amd/csrc/hip/xgmi_ar.hip
       python -m euler_amd._build > "$OUT/build_xar_default.log" 2>&1 || exit 4 ;;
+    spg_sweep)
+      # complete steps per hipGraph replay (bench.py --steps-per-graph)
+      for k in ${SPG_VALUES:-4 8 16}; do
+        run "bench_spg$k" 300 python -u bench.py --steps 1000 --warmup 20 --steps-per-graph $k || exit $?
+      done ;;
+    xgmi_prof)
+      # kernel table of the xGMI all-reduce (one rank: the launch, staging, both barriers,
+      # reduce) and of RCCL's one-rank all_reduce, hipGraph-replayed
+      RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29597 \
+        run xgmi_prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/xgmi_prof" -o run --output-format csv -- \
+          python3 tools/xgmi_bench.py --numel 278784 --calls 100 --reps 3 ;;
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench_small)
