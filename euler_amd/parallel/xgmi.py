@@ -49,7 +49,7 @@ class XgmiAllReduce:
     (one process per GPU; ``group`` is only used to exchange handles at setup, so a gloo
     group works as well as an RCCL one)."""
 
-    def __init__(self, capacity_bytes: int, group=None, timeout_s: float = 2.0):
+    def __init__(self, capacity_bytes: int, group=None, timeout_s: float = 10.0):
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)

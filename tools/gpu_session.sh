@@ -166,6 +166,16 @@ for st in "${S[@]}"; do
         run "fb_gat_$r" 600 python -u benchmarks/bench_gat.py --epochs 200 --eval-epochs 0 || exit $?
         run "fb_headline_$r" 300 python -u bench.py --steps 1000 --warmup 20 || exit $?
       done ;;
+    final_benches_hd)
+      # the 3-run protocol for the benchmarks this session changed: headline, DeepWalk local
+      # and its one-rank all-to-all path
+      for r in 1 2 3; do
+        run "fb_dw_$r" 300 python -u benchmarks/bench_deepwalk.py --eval-nodes 0 --mode graph --steps 200 || exit $?
+        run "fb_dw_dist_$r" 300 python -u -m torch.distributed.run --nnodes 1 --nproc-per-node 1 \
+          --master-addr 127.0.0.1 --master-port 2956$r benchmarks/bench_deepwalk.py --eval-nodes 0 --mode graph \
+          --steps 200 --force-dist || exit $?
+        run "fb_headline_$r" 300 python -u bench.py --steps 1000 --warmup 20 || exit $?
+      done ;;
     kg_dw_sweep)
       # KG_DW="chunk:slab ..." (rel_gemm_dw edges per chunk, slab width)
       for c in ${KG_DW:-512:128 256:128 1024:128 512:64 256:64}; do
