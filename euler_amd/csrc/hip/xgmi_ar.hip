@@ -69,6 +69,39 @@ __device__ __forceinline__ uint32_t* ar_sig(char* sig, int which, int b, int r) 
   return reinterpret_cast<uint32_t*>(sig) + (which * kArMaxBlocks + b) * kArMaxRanks + r;
 }
 
+// XAR_WT=1: the exchanged data never sits in an L2 — staged / reduced vectors are written
+// with system-scope (write-through) stores and the peers' vectors read with system-scope
+// loads — so a barrier needs neither the L2 write-back before the signal nor the
+// invalidation after the wait: every wave drains its stores (vmcnt(0)), the flags are
+// relaxed system-scope atomics.
+#ifndef XAR_WT
+#define XAR_WT 0
+#endif
+__device__ __forceinline__ void st_x(uint4_t* p, uint4_t v) {
+  if (XAR_WT) {
+    uint64_t* q = reinterpret_cast<uint64_t*>(p);
+    __hip_atomic_store(q, (static_cast<uint64_t>(v[1]) << 32) | v[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(q + 1, (static_cast<uint64_t>(v[3]) << 32) | v[2], __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  } else {
+    *p = v;
+  }
+}
+__device__ __forceinline__ uint4_t ld_x(const uint4_t* p) {
+  if (XAR_WT) {
+    const uint64_t* q = reinterpret_cast<const uint64_t*>(p);
+    const uint64_t a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint64_t b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    uint4_t v;
+    v[0] = static_cast<uint32_t>(a);
+    v[1] = static_cast<uint32_t>(a >> 32);
+    v[2] = static_cast<uint32_t>(b);
+    v[3] = static_cast<uint32_t>(b >> 32);
+    return v;
+  }
+  return *p;
+}
+
 // thread t < world (lanes of wave 0) signals peer t, then waits for peer t's signal.  The
 // other waves only drain their own stores (vmcnt(0)) before the block barrier: wave 0's
 // system-scope release (one L2 write-back) then covers the whole block's stores, and its
@@ -83,7 +116,8 @@ __device__ __forceinline__ void ar_barrier(const ArArgs& a, int which, uint32_t 
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (t < a.world) {
-    __hip_atomic_store(ar_sig(a.sig[t], which, b, a.rank), e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(ar_sig(a.sig[t], which, b, a.rank), e, XAR_WT ? __ATOMIC_RELAXED : __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
     const uint32_t* f = ar_sig(a.sig[a.rank], which, b, t);
     const long long t0 = wall_clock64();
     while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
@@ -94,7 +128,7 @@ __device__ __forceinline__ void ar_barrier(const ArArgs& a, int which, uint32_t 
       }
       __builtin_amdgcn_s_sleep(1);
     }
-    __atomic_thread_fence(__ATOMIC_ACQUIRE);  // system scope: the peers' data after their flags
+    if (!XAR_WT) __atomic_thread_fence(__ATOMIC_ACQUIRE);  // system scope: the peers' data after their flags
   }
   __syncthreads();
   if (XAR_FENCE_ALL) __threadfence_system();
@@ -155,7 +189,7 @@ __global__ __launch_bounds__(kArThreads) void xgmi_allreduce_kernel(ArArgs a) {
         if (o0 + k * step < len) v[k] = data[(base + o0 + k * step) / V];
 #pragma unroll
       for (int k = 0; k < kArVecPerThread; ++k)
-        if (o0 + k * step < len) my_in[(base + o0 + k * step) / V] = v[k];
+        if (o0 + k * step < len) st_x(&my_in[(base + o0 + k * step) / V], v[k]);
     }
   }
   ar_barrier(a, 0, e);
@@ -169,7 +203,7 @@ __global__ __launch_bounds__(kArThreads) void xgmi_allreduce_kernel(ArArgs a) {
       uint4_t v[kArMaxRanks];
 #pragma unroll
       for (int r = 0; r < kArMaxRanks; ++r)
-        if (r < a.world) v[r] = in_of(r)[vi];  // one load per link in flight
+        if (r < a.world) v[r] = ld_x(&in_of(r)[vi]);  // one load per link in flight
       float acc[V];
 #pragma unroll
       for (int i = 0; i < V; ++i) acc[i] = 0.f;
@@ -177,7 +211,7 @@ __global__ __launch_bounds__(kArThreads) void xgmi_allreduce_kernel(ArArgs a) {
       for (int r = 0; r < kArMaxRanks; ++r)
         if (r < a.world) ArVec<T>::add(acc, v[r]);
       const uint4_t res = ArVec<T>::pack(acc);
-      my_out[vi] = res;
+      st_x(&my_out[vi], res);
       data[vi] = res;
     }
   }
@@ -191,7 +225,7 @@ __global__ __launch_bounds__(kArThreads) void xgmi_allreduce_kernel(ArArgs a) {
 #pragma unroll
       for (int s = 0; s < kArMaxRanks; ++s)
         if (s < a.world && s != a.rank && o0 + k * step < shard_len(s))
-          v[k][s] = out_of(s)[(s * a.shard + o0 + k * step) / V];
+          v[k][s] = ld_x(&out_of(s)[(s * a.shard + o0 + k * step) / V]);
 #pragma unroll
     for (int k = 0; k < kArVecPerThread; ++k)
 #pragma unroll

@@ -91,8 +91,9 @@ class XgmiAllReduce:
         return int(self._ar.error()) if self._ar is not None else 1
 
     def self_test(self, numel: int | None = None, dtype=torch.float32, calls: int = 3) -> bool:
-        """Eager check against an RCCL/gloo-free reference: rank r contributes (r + 1) * base
-        with a rank-independent ``base``, so every element's sum is known in closed form.
+        """Eager check against an RCCL/gloo-free reference: in call c rank r contributes
+        (r + 1) * 2^c * base with a rank-independent ``base``, so every element's sum is
+        known in closed form and differs from call to call.
         Returns the all-rank verdict (True only if every rank saw exact results)."""
         dev = torch.device("cuda", torch.cuda.current_device())
         # every rank must agree that every rank mapped its peers before any kernel runs
@@ -111,11 +112,13 @@ class XgmiAllReduce:
         base = torch.randint(-8, 9, (n,), generator=g).to(dev, torch.float32)  # exact in bf16 sums
         want = base * (self.world * (self.world + 1) // 2)
         ok = True
-        for _ in range(calls):
-            x = (base * (self.rank + 1)).to(dtype)
+        for c in range(calls):
+            # a different sum every call (x 2^c keeps bf16 exact): a stale read of the
+            # previous call's peer data cannot pass
+            x = (base * ((self.rank + 1) * 2 ** c)).to(dtype)
             self(x)
             torch.cuda.synchronize()
-            ok = ok and bool(torch.equal(x.float(), want))
+            ok = ok and bool(torch.equal(x.float(), want * 2 ** c))
         ok = ok and self.error() == 0
         flag = torch.tensor([0 if ok else 1], dtype=torch.int32)
         if dist.get_backend(self.group) == "nccl":
