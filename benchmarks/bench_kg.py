@@ -208,7 +208,7 @@ def main(argv=None):
         sync()
         flat.rebind_grads()
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             step_body()
 
     def step():

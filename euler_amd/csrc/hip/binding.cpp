@@ -533,6 +533,14 @@ class XgmiAr {
     return v;
   }
   int64_t capacity() const { return cap_; }
+  // a tensor over this rank's `in` region: a producer that writes its gradient here lets
+  // run() reduce in place (no staging copy); valid while this object lives
+  torch::Tensor input_view(int64_t numel, bool bf16) const {
+    const int64_t esz = bf16 ? 2 : 4;
+    TORCH_CHECK(numel >= 0 && numel * esz <= cap_, "xar: input view exceeds the capacity");
+    auto opts = torch::TensorOptions().dtype(bf16 ? torch::kBFloat16 : torch::kFloat32).device(torch::kCUDA, dev_);
+    return torch::from_blob(own_buf_, {numel}, opts);
+  }
 
  private:
   int64_t cap_;
@@ -585,7 +593,8 @@ PYBIND11_MODULE(_hip_ops, m) {
       .def("open", &XgmiAr::open)
       .def("run", &XgmiAr::run)
       .def("error", &XgmiAr::error)
-      .def("capacity", &XgmiAr::capacity);
+      .def("capacity", &XgmiAr::capacity)
+      .def("input_view", &XgmiAr::input_view, py::arg("numel"), py::arg("bf16"));
   m.attr("xar_max_ranks") = eh_xar_max_ranks();
   m.attr("xar_max_blocks") = eh_xar_max_blocks();
   m.attr("xar_vec_per_thread") = eh_xar_vec_per_thread();

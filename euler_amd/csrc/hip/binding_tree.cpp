@@ -205,6 +205,14 @@ class TreePlan {
   int64_t fwd_blocks() const { return fwd0_.M / bm0_; }
   void set_lr(double lr) { opt_.lr = static_cast<float>(lr); }
   // bf16 gradient buffer for the data-parallel hand-off (None: fp32 grad)
+  // the flat fp32 gradient the reduce launch writes and the optimizer reads (e.g. a view of
+  // the xGMI all-reduce's IPC input region, so the all-reduce runs in place there)
+  void set_grad(torch::Tensor g) {
+    TORCH_CHECK(g.is_cuda() && g.scalar_type() == torch::kFloat32 && g.is_contiguous() && g.numel() == opt_.n,
+                "grad must be a contiguous fp32 GPU tensor of the flat parameter size");
+    grad_ = g;
+    opt_.g = g.data_ptr<float>();
+  }
   void set_grad16(c10::optional<torch::Tensor> g16) {
     if (!g16.has_value()) {
       opt_.g16 = nullptr;
@@ -241,7 +249,7 @@ class TreePlan {
   std::vector<torch::Tensor> owned_;
   torch::Tensor roots_cur_;  // the forward's copy of the batch's roots (read by the head)
   TrOptArgs opt_{};
-  torch::Tensor g16_;
+  torch::Tensor g16_, grad_;
 
   bool has(const char* k) const { return d_.contains(k) && !d_[k].is_none(); }
   int64_t geti(const char* k) const {
@@ -854,6 +862,7 @@ void register_tree_ops(py::module& m) {
       .def("opt_segments", &TreePlan::opt_segments, py::arg("mode"), py::arg("segs"), py::arg("head_stats"))
       .def("set_lr", &TreePlan::set_lr)
       .def("set_grad16", &TreePlan::set_grad16, py::arg("g16"))
+      .def("set_grad", &TreePlan::set_grad, py::arg("g"))
       .def("num_problems", &TreePlan::num_problems)
       .def("splits", &TreePlan::splits)
       .def("problems", &TreePlan::problems, py::arg("route"));

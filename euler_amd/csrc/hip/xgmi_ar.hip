@@ -60,6 +60,8 @@ struct ArArgs {
   int64_t shard;           // elements per rank's shard (multiple of the vector width)
   int64_t cap;             // bytes of each of `in` and `out`
   int rank, world;
+  int64_t in_off;          // >= 0: data IS this rank's `in` region at this byte offset (the
+                           // producer wrote it there: no staging copy); -1: stage it
   uint32_t* epoch;         // [gridDim.x] call counters (this rank, ordinary memory)
   int* err;                // set to 1 by a wait that timed out
   long long timeout;       // wall_clock64 ticks per wait
@@ -174,13 +176,15 @@ __global__ __launch_bounds__(kArThreads) void xgmi_allreduce_kernel(ArArgs a) {
     return hi > lo ? hi - lo : int64_t{0};
   };
   uint4_t* __restrict__ data = reinterpret_cast<uint4_t*>(a.data);
-  auto in_of = [&](int r) { return reinterpret_cast<uint4_t*>(a.buf[r]); };
-  auto out_of = [&](int r) { return reinterpret_cast<uint4_t*>(a.buf[r] + a.cap); };
+  const int64_t in_off = a.in_off > 0 ? a.in_off : 0;
+  auto in_of = [&](int r) { return reinterpret_cast<uint4_t*>(a.buf[r] + in_off); };
+  auto out_of = [&](int r) { return reinterpret_cast<uint4_t*>(a.buf[r] + a.cap + in_off); };
 
   // A: stage this rank's input (the chunks block b owns in every shard); every load of a
-  // sweep is issued before its stores
+  // sweep is issued before its stores.  In place (in_off >= 0) the producer kernel already
+  // wrote it into the IPC region, and the kernel boundary wrote it back to memory.
   uint4_t* __restrict__ my_in = in_of(a.rank);
-  for (int s = 0; s < a.world; ++s) {
+  for (int s = 0; s < (a.in_off >= 0 ? 0 : a.world); ++s) {
     const int64_t len = shard_len(s), base = s * a.shard;
     for (int64_t o0 = first; o0 < len; o0 += kArVecPerThread * step) {
       uint4_t v[kArVecPerThread];
@@ -260,6 +264,8 @@ hipError_t eh_xar_alloc(int64_t cap, void** sig, void** data) {
 }
 
 // sigs / bufs: world pointers (this rank's own and the mapped peers'); blocks <= kArMaxBlocks
+// data inside this rank's `in` region (bufs[rank] .. + cap): the all-reduce runs in place
+// there, and every rank must pass the same offset (same tensor slicing on every rank)
 hipError_t eh_xar_run(void* const* sigs, void* const* bufs, int world, int rank, void* data, int is_bf16, int64_t n,
                       int64_t cap, int blocks, uint32_t* epoch, int* err, long long timeout, hipStream_t s) {
   if (world < 1 || world > kArMaxRanks || rank < 0 || rank >= world || blocks < 1 || blocks > kArMaxBlocks ||
@@ -276,6 +282,9 @@ hipError_t eh_xar_run(void* const* sigs, void* const* bufs, int world, int rank,
     a.sig[r] = static_cast<char*>(sigs[r]);
   }
   a.data = data;
+  const char* own = static_cast<const char*>(bufs[rank]);
+  const char* d = static_cast<const char*>(data);
+  a.in_off = (d >= own && d + n * esz <= own + cap) ? static_cast<int64_t>(d - own) : -1;
   a.n = n;
   a.shard = ((n / V + world - 1) / world) * V;
   a.cap = cap;

@@ -450,7 +450,8 @@ class BaseEstimator:
             gbuf = getattr(tr, "grad16", None)
             if gbuf is None:
                 gbuf = getattr(tr, "grad", None)
-            grad_sync, name, _ = make_grad_sync(gbuf, str(self.params.get("grad_sync", kind)))
+            grad_sync, name, _ = make_grad_sync(gbuf, str(self.params.get("grad_sync", kind)),
+                                                rebind=tr.use_grad_buffer if tr.on_gpu else None)
             log.info("device path gradient sync: %s all-reduce", name)
 
         use_graph = self.device.type == "cuda" and bool(self.params.get("hipgraph", True))

@@ -106,7 +106,7 @@ class GraphedTrainStep:
         if self.graph is None:
             self.est.optimizer.zero_grad(set_to_none=True)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 _, loss, name, metric = self.est._run_model(source)
                 loss.backward()
                 self.est.optimizer.step()

@@ -127,7 +127,7 @@ class DeepWalkTrainer:
                 self.warm_loss = self._step_static()
         cur.wait_stream(side)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             self._step_static()
         self.hip_graph = g
         return g

@@ -406,7 +406,7 @@ class UnsupSageTrainer:
         torch.cuda.synchronize(self.device)
         self.flat.rebind_grads()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             self._step(grad_sync)
         self._graph_exec = g
         return g

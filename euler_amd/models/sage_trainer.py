@@ -574,7 +574,11 @@ class SageTrainer:
         self._graphs = {}
         for k in sorted({1, int(steps)}, reverse=True):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            # thread-local capture: RCCL's watchdog thread keeps querying the events of
+            # collectives that just finished; under the default global mode such a query
+            # during the capture invalidates it and aborts the process (seen on a box:
+            # profiles/r3_xgmi/xgmi_bench_capture_race.log)
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 for _ in range(k):
                     self.step(grad_sync)
             self.step_count -= k  # the captured steps did not run
@@ -622,6 +626,24 @@ class SageTrainer:
         else:
             self.grad16 = None
             self.plan.set_grad16(None)
+
+    def use_grad_buffer(self, t: torch.Tensor):
+        """Data parallel: make ``t`` the gradient buffer that the reduce launch writes and
+        ``grad_sync`` receives (fp32 :attr:`grad`, or bf16 :attr:`grad16` after
+        ``set_grad_sync_dtype("bf16")``) — e.g. the xGMI all-reduce's IPC input region, so
+        the all-reduce runs in place without a staging copy (parallel/xgmi.py)."""
+        if not self.on_gpu:
+            raise RuntimeError("use_grad_buffer: GPU trainers only")
+        if t.dtype == torch.bfloat16:
+            if getattr(self, "grad16", None) is None:
+                raise ValueError("bf16 gradient buffer without set_grad_sync_dtype('bf16')")
+            t.copy_(self.grad16)
+            self.grad16 = t
+            self.plan.set_grad16(t)
+        else:
+            t.copy_(self.grad)
+            self.grad = t
+            self.plan.set_grad(t)
 
     def set_learning_rate(self, lr: float):
         self.lr = float(lr)

@@ -86,14 +86,24 @@ class XgmiAllReduce:
         self._ar.run(t, _blocks_for(t.numel(), self.world, t.element_size()))
         return t
 
+    def input_view(self, numel: int, dtype) -> torch.Tensor:
+        """A tensor over this rank's IPC input region.  A producer that writes its gradient
+        there (SageTrainer.use_grad_buffer) gets the all-reduce in place: no staging copy,
+        one dependent memory round trip less per call.  Valid while this object lives; a
+        call on any other tensor stages through the same region, so a caller that adopted
+        the view reduces only the view (or slices of it, sliced alike on every rank)."""
+        return self._ar.input_view(int(numel), dtype == torch.bfloat16)
+
     def error(self) -> int:
         """1 if a cross-GPU wait timed out on this rank since construction (synchronises)."""
         return int(self._ar.error()) if self._ar is not None else 1
 
-    def self_test(self, numel: int | None = None, dtype=torch.float32, calls: int = 3) -> bool:
+    def self_test(self, numel: int | None = None, dtype=torch.float32, calls: int = 3,
+                  in_place: bool = False) -> bool:
         """Eager check against an RCCL/gloo-free reference: in call c rank r contributes
         (r + 1) * 2^c * base with a rank-independent ``base``, so every element's sum is
-        known in closed form and differs from call to call.
+        known in closed form and differs from call to call.  ``in_place``: the input is
+        written into :meth:`input_view` first (the trainer's zero-copy mode).
         Returns the all-rank verdict (True only if every rank saw exact results)."""
         dev = torch.device("cuda", torch.cuda.current_device())
         # every rank must agree that every rank mapped its peers before any kernel runs
@@ -116,6 +126,8 @@ class XgmiAllReduce:
             # a different sum every call (x 2^c keeps bf16 exact): a stale read of the
             # previous call's peer data cannot pass
             x = (base * ((self.rank + 1) * 2 ** c)).to(dtype)
+            if in_place:  # written by a torch kernel into the IPC region, reduced there
+                x = self.input_view(n, dtype).copy_(x)
             self(x)
             torch.cuda.synchronize()
             ok = ok and bool(torch.equal(x.float(), want * 2 ** c))
@@ -139,7 +151,7 @@ def _graph_call_us(fn, calls: int = 20, reps: int = 3, group=None) -> float:
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
         for _ in range(calls):
             fn()
     g.replay()
@@ -160,7 +172,7 @@ def _graph_call_us(fn, calls: int = 20, reps: int = 3, group=None) -> float:
     return float(t.item())
 
 
-def make_grad_sync(buf: torch.Tensor, kind: str = "auto", group=None):
+def make_grad_sync(buf: torch.Tensor, kind: str = "auto", group=None, rebind=None):
     """``grad_sync(g)`` for a data-parallel trainer step (SageTrainer / UnsupSageTrainer
     ``step(grad_sync)``): an in-place sum all-reduce of (slices of) ``buf`` returning the
     1 / world scale.  ``kind``: "xgmi" (this module's kernel), "rccl" (torch.distributed
@@ -168,6 +180,8 @@ def make_grad_sync(buf: torch.Tensor, kind: str = "auto", group=None):
     rank, then both all-reduces are timed on ``buf`` itself (hipGraph-replayed, max over
     ranks) and the faster one is kept — measured on the node the job runs on, not assumed —
     or "tune" (the same, also with one rank).
+    ``rebind(view)``: with xGMI chosen, hand the producer a view of the IPC input region to
+    write its gradient into (SageTrainer.use_grad_buffer), after an in-place self-test.
     Returns ``(grad_sync, name, info)``; ``info`` holds the XgmiAllReduce (``xar``, None for
     RCCL, whose :meth:`~XgmiAllReduce.error` the caller checks after a run) and the timings."""
     world = dist.get_world_size(group)
@@ -190,6 +204,13 @@ def make_grad_sync(buf: torch.Tensor, kind: str = "auto", group=None):
         info["us_per_call"] = {"xgmi": round(t_x, 2), "rccl": round(t_r, 2)}
         if xar.error() != 0 or t_r < t_x:
             xar = None
+    if xar is not None and rebind is not None:
+        # zero copy: the producer writes its gradient straight into the IPC input region
+        if xar.self_test(numel=buf.numel(), dtype=buf.dtype, in_place=True):
+            rebind(xar.input_view(buf.numel(), buf.dtype))
+            info["in_place"] = True
+        else:
+            info["in_place"] = False
     if xar is not None:
         info["xar"] = xar
 

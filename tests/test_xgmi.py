@@ -36,6 +36,8 @@ def _worker(rank, world, port, q):
         ar = XgmiAllReduce(2 << 20, timeout_s=10.0)
         res["self_test_fp32"] = ar.self_test(dtype=torch.float32)
         res["self_test_bf16"] = ar.self_test(numel=4096, dtype=torch.bfloat16)
+        res["self_test_fp32_in_place"] = ar.self_test(numel=278784, dtype=torch.float32, in_place=True)
+        res["self_test_bf16_in_place"] = ar.self_test(numel=278784, dtype=torch.bfloat16, in_place=True)
         # random data, sizes that do not divide evenly into shards / blocks
         for n in (278784, 8, 4104, 131080):
             for dtype in (torch.float32, torch.bfloat16):
@@ -62,7 +64,7 @@ def _worker(rank, world, port, q):
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             ar(xd)
         ok = True
         for k in range(5):
@@ -73,9 +75,33 @@ def _worker(rank, world, port, q):
             want = sum(float(r + 1 + 10 * k) for r in range(world))
             ok = ok and bool(torch.all(xd == want).item())
         res["graph_replays"] = ok
+        # in place inside a captured graph: a producer kernel (copy_) writes the IPC input
+        # view, the all-reduce reduces it there; and slices of the view (2-bucket trainer)
+        xv = ar.input_view(n, torch.float32)
+        src = torch.zeros(n, device=dev)
+        graph2 = torch.cuda.CUDAGraph()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            xv.copy_(src)
+            ar(xv[: n // 2])
+            ar(xv[n // 2:])
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        with torch.cuda.graph(graph2, capture_error_mode="thread_local"):
+            xv.copy_(src)
+            ar(xv[: n // 2])
+            ar(xv[n // 2:])
+        ok = True
+        for k in range(4):
+            src.copy_(torch.arange(n, dtype=torch.float32).to(dev) * (rank + 1) + k)
+            graph2.replay()
+            torch.cuda.synchronize()
+            want = torch.arange(n, dtype=torch.float32) * (world * (world + 1) // 2) + k * world
+            ok = ok and bool(torch.equal(xv.cpu(), want))
+        res["graph_in_place_slices"] = ok
         res["error"] = ar.error()
         dist.barrier()
-        del graph
+        del graph, graph2
         q.put((rank, res))
     except Exception as e:  # reported to the parent, which fails the test
         q.put((rank, {"exception": repr(e)}))

@@ -25,7 +25,7 @@ def timed(fn, calls, reps):
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
         for _ in range(calls):
             fn()
     g.replay()
@@ -75,6 +75,8 @@ def main():
             x = torch.randn(n, device=dev).to(dt)
             key = f"{n}_{str(dt)[6:]}"
             out[f"xgmi_us_{key}"] = round(timed(lambda: ar(x), args.calls, args.reps), 2)
+            xi = ar.input_view(n, dt).copy_(x)  # in place: the producer wrote the IPC region
+            out[f"xgmi_inplace_us_{key}"] = round(timed(lambda: ar(xi), args.calls, args.reps), 2)
             out[f"xgmi_blocks_{key}"] = _blocks_for(n, world, x.element_size())
             if not args.shared_gpu:
                 out[f"rccl_us_{key}"] = round(timed(lambda: dist.all_reduce(x), args.calls, args.reps), 2)
