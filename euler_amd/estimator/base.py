@@ -447,11 +447,15 @@ class BaseEstimator:
             from ..parallel.xgmi import make_grad_sync
 
             kind = "auto" if self.device.type == "cuda" else "rccl"
+            # the buffer grad_sync receives: SageTrainer's flat grad (bf16 hand-off: grad16),
+            # UnsupSageTrainer's FlatParams grad
             gbuf = getattr(tr, "grad16", None)
             if gbuf is None:
                 gbuf = getattr(tr, "grad", None)
-            grad_sync, name, _ = make_grad_sync(gbuf, str(self.params.get("grad_sync", kind)),
-                                                rebind=tr.use_grad_buffer if tr.on_gpu else None)
+            if gbuf is None and hasattr(tr, "flat"):
+                gbuf = tr.flat.grad
+            rebind = getattr(tr, "use_grad_buffer", None) if getattr(tr, "on_gpu", False) else None
+            grad_sync, name, _ = make_grad_sync(gbuf, str(self.params.get("grad_sync", kind)), rebind=rebind)
             log.info("device path gradient sync: %s all-reduce", name)
 
         use_graph = self.device.type == "cuda" and bool(self.params.get("hipgraph", True))

@@ -622,3 +622,34 @@ def test_estimator_device_graph_data_parallel_lockstep(tmp_path):
     res = _run(_worker_estimator_device_dp, str(tmp_path))
     assert not [r for r in res if r[1] == "error"], res
     assert len(res) == 2 and all(r[2] for r in res), res
+
+
+def _worker_estimator_unsup_device_dp(rank, world, port, q, tmp):
+    """the unsupervised GraphSAGE device path (UnsupSageTrainer) under 2 gloo ranks: the
+    estimator finds its FlatParams gradient for make_grad_sync and the ranks stay in step"""
+    try:
+        _init(rank, world, port)
+        from euler_amd.tools import runner
+
+        a = runner.parse_args(["--dataset", "ppi", "--scale", "0.05", "--batch_size", "32", "--total_step", "4",
+                               "--log_steps", "2", "--model_dir", os.path.join(tmp, f"ckpt_u{rank}"),
+                               "--device_graph", "--device", "cpu", "--seed", "1", "--fanouts", "5", "3",
+                               "--dim", "32"], model="graphsage_unsup")
+        _, est = runner.build(a)
+        est.train()
+        flat = est.device_trainer.flat.flat.detach().clone()
+        allp = [torch.zeros_like(flat) for _ in range(world)]
+        dist.all_gather(allp, flat)
+        same = all(torch.equal(x, allp[0]) for x in allp)
+        q.put((rank, "estimator_unsup_device_dp", bool(same and est.global_step == 4)))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_estimator_unsup_device_graph_data_parallel_lockstep(tmp_path):
+    res = _run(_worker_estimator_unsup_device_dp, str(tmp_path))
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == 2 and all(r[2] for r in res), res
