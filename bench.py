@@ -171,7 +171,7 @@ def main(argv=None):
         tr.set_grad_sync_dtype(args.grad_reduce_dtype)
         gbuf = tr.grad if getattr(tr, "grad16", None) is None else tr.grad16
         kind = "xgmi" if args.shared_gpu else args.grad_sync
-        grad_sync, sync_name, sync_info = make_grad_sync(gbuf, kind)
+        grad_sync, sync_name, sync_info = make_grad_sync(gbuf, kind, rebind=tr.use_grad_buffer)
         xar = sync_info.pop("xar")
         if rank == 0 and sync_info:
             log(f"gradient all-reduce: {sync_name} ({sync_info})")
