@@ -314,6 +314,9 @@ for st in "${S[@]}"; do
       RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29597 \
         run xgmi_prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/xgmi_prof" -o run --output-format csv -- \
           python3 tools/xgmi_bench.py --numel 278784 --calls 100 --reps 3 ;;
+    bench_default)
+      # exactly the driver's 1-GPU bench command shape (bench.py defaults)
+      run bench_default 600 python -u bench.py --gpus 1 --steps 200 --warmup 20 ;;
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench_small)
