@@ -176,6 +176,13 @@ for st in "${S[@]}"; do
           --steps 200 --force-dist || exit $?
         run "fb_headline_$r" 300 python -u bench.py --steps 1000 --warmup 20 || exit $?
       done ;;
+    final_benches_other)
+      # the 3-run protocol for unsupervised GraphSAGE, R-GCN + TransE and GAT
+      for r in 1 2 3; do
+        run "fb_unsup_$r" 300 python -u benchmarks/bench_unsup_sage.py --steps 1000 || exit $?
+        run "fb_kg_$r" 300 python -u benchmarks/bench_kg.py --steps 200 --warmup 10 --eval-after 0 || exit $?
+        run "fb_gat_$r" 600 python -u benchmarks/bench_gat.py --epochs 200 --eval-epochs 0 || exit $?
+      done ;;
     kg_dw_sweep)
       # KG_DW="chunk:slab ..." (rel_gemm_dw edges per chunk, slab width)
       for c in ${KG_DW:-512:128 256:128 1024:128 512:64 256:64}; do
