@@ -461,22 +461,36 @@ class BaseEstimator:
         use_graph = self.device.type == "cuda" and bool(self.params.get("hipgraph", True))
         if use_graph:
             warm = min(2, total - self.global_step)
-            tr.capture(grad_sync, warmup=warm)
+            # several complete steps per hipGraph replay (SageTrainer): the ~5 us gap between
+            # replays is paid once per chunk instead of once per step
+            multi = hasattr(tr, "replay_steps")
+            if multi:
+                tr.capture(grad_sync, warmup=warm, steps=int(self.params.get("steps_per_graph", 8)))
+            else:
+                tr.capture(grad_sync, warmup=warm)
             self.global_step += warm
 
-        def one():
-            if use_graph:
-                tr.replay()
-            else:
-                tr.step(grad_sync)
+        def run(n):
+            if use_graph and multi:
+                tr.replay_steps(n)
+                return
+            for _ in range(n):
+                if use_graph:
+                    tr.replay()
+                else:
+                    tr.step(grad_sync)
 
         bs = int(self.params["batch_size"])
         t0, n0 = time.time(), self.global_step
         tr.reset_metric()
         last = {}
         while self.global_step < total:
-            one()
-            self.global_step += 1
+            # run up to the next log / checkpoint boundary in one go
+            nxt = min(total, (self.global_step // log_steps + 1) * log_steps)
+            if save_steps:
+                nxt = min(nxt, (self.global_step // save_steps + 1) * save_steps)
+            run(nxt - self.global_step)
+            self.global_step = nxt
             if self.global_step % log_steps == 0 or self.global_step == total:
                 loss = float(tr.loss.item())  # syncs the stream
                 dt = max(time.time() - t0, 1e-9)
