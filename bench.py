@@ -22,6 +22,9 @@ xgmi / rccl forces one; the JSON config records the timings and the choice).  No
 region.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [...]
+
+`--gpus N` without torchrun starts N ranks on this node itself (parallel/launch.py); under
+torchrun it must equal WORLD_SIZE.
 """
 from __future__ import annotations
 
@@ -111,6 +114,17 @@ def log(*a):
 
 def main(argv=None):
     args = parse_args(argv)
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # plain `python bench.py --gpus N`: start N ranks here (one process per GPU) before
+        # anything touches the GPU; rank 0's JSON line is this process's stdout
+        from euler_amd.parallel.launch import spawn_local
+
+        return spawn_local(args.gpus, list(sys.argv[1:] if argv is None else argv), script=os.path.abspath(__file__))
+    if env_world is not None and int(env_world) != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} disagrees with WORLD_SIZE={env_world} (torchrun --nproc-per-node)")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -130,7 +144,7 @@ def main(argv=None):
     torch.cuda.set_device(dev)
 
     from euler_amd.graph.device_graph import DeviceGraph
-    from euler_amd.models.fused_sage import synthetic_features, synthetic_labels
+    from euler_amd.dataset.synthetic import synthetic_features, synthetic_labels
     from euler_amd.models.sage_trainer import SageTrainer
 
     fanouts = [int(x) for x in args.fanouts.split(",")]
@@ -293,7 +307,8 @@ def main(argv=None):
         tr.release_graphs()
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -464,7 +464,7 @@ void sample_neighbor_into(torch::Tensor indptr, torch::Tensor nbr, torch::Tensor
 // One rank's side of the two-shot peer-memory all-reduce (xgmi_ar.hip): owns the rank's
 // uncached IPC buffer, maps the peers' buffers from their IPC handles, launches the kernel on
 // the current stream (hipGraph-capturable: no allocation, no sync).
-class XgmiAr {
+class XgmiAr : public std::enable_shared_from_this<XgmiAr> {
  public:
   XgmiAr(int64_t cap, double timeout_s) : cap_(cap) {
     TORCH_CHECK(cap > 0 && cap % 16 == 0, "xgmi all-reduce capacity must be a positive multiple of 16 bytes");
@@ -534,12 +534,15 @@ class XgmiAr {
   }
   int64_t capacity() const { return cap_; }
   // a tensor over this rank's `in` region: a producer that writes its gradient here lets
-  // run() reduce in place (no staging copy); valid while this object lives
-  torch::Tensor input_view(int64_t numel, bool bf16) const {
+  // run() reduce in place (no staging copy).  The tensor's deleter holds a reference to
+  // this object, so the IPC region outlives every view (a trainer that adopted the view as
+  // its gradient keeps it mapped after the Python all-reduce object is gone)
+  torch::Tensor input_view(int64_t numel, bool bf16) {
     const int64_t esz = bf16 ? 2 : 4;
     TORCH_CHECK(numel >= 0 && numel * esz <= cap_, "xar: input view exceeds the capacity");
     auto opts = torch::TensorOptions().dtype(bf16 ? torch::kBFloat16 : torch::kFloat32).device(torch::kCUDA, dev_);
-    return torch::from_blob(own_buf_, {numel}, opts);
+    std::shared_ptr<XgmiAr> keep = shared_from_this();
+    return torch::from_blob(own_buf_, {numel}, [keep](void*) mutable { keep.reset(); }, opts);
   }
 
  private:
@@ -587,7 +590,7 @@ PYBIND11_MODULE(_hip_ops, m) {
   m.def("flat_optim_", &flat_optim_);
   m.def("sparse_optim_", &sparse_optim_);
   m.def("sample_neighbor_into", &sample_neighbor_into);
-  py::class_<XgmiAr>(m, "XgmiAr")
+  py::class_<XgmiAr, std::shared_ptr<XgmiAr>>(m, "XgmiAr")
       .def(py::init<int64_t, double>(), py::arg("capacity_bytes"), py::arg("timeout_s") = 2.0)
       .def("handle", &XgmiAr::handle)
       .def("open", &XgmiAr::open)

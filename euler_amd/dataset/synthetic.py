@@ -26,7 +26,7 @@ import math
 
 import torch
 
-__all__ = ["lattice_kg", "community_graph", "community_labels", "community_features", "tail_ranks", "rank_metrics",
+__all__ = ["synthetic_features", "synthetic_labels", "lattice_kg", "community_graph", "community_labels", "community_features", "tail_ranks", "rank_metrics",
            "auc"]
 
 
@@ -173,3 +173,25 @@ def auc(pos_scores, neg_scores):
     ranks = (rsum / cnt.double())[inv]
     n_pos, n_neg = pos_scores.numel(), neg_scores.numel()
     return float((ranks[y == 1].sum() - n_pos * (n_pos + 1) / 2) / (n_pos * n_neg))
+
+
+def synthetic_labels(features: torch.Tensor, label_dim: int, chunk: int = 1 << 22) -> torch.Tensor:
+    """Learnable synthetic labels: argmax of the first ``label_dim`` feature columns (the
+    headline bench's node labels; int16 class ids, the device trainer's compact label mode)."""
+    n = features.shape[0]
+    out = torch.empty(n, dtype=torch.int16, device=features.device)
+    for s in range(0, n, chunk):
+        out[s:s + chunk] = features[s:s + chunk, :label_dim].float().argmax(1).to(torch.int16)
+    return out
+
+
+def synthetic_features(n: int, dim: int, seed: int, device, dtype=torch.bfloat16, chunk: int = 1 << 22):
+    """[n, dim] random-normal feature table generated on ``device`` in chunks (no host copy of
+    a 100M-row table)."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    out = torch.empty((n, dim), dtype=dtype, device=device)
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        out[s:e] = torch.randn((e - s, dim), generator=g, device=device, dtype=torch.float32).to(dtype)
+    return out

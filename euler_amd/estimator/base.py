@@ -39,7 +39,7 @@ from euler_amd.utils.prefetch import Prefetcher
 from euler_amd.utils import trace
 from euler_amd.utils.misc import get_optimizer
 
-__all__ = ["BaseEstimator", "latest_checkpoint", "id_file_batches"]
+__all__ = ["BaseEstimator", "latest_checkpoint", "rank_checkpoint", "id_file_batches"]
 
 log = logging.getLogger("euler_amd.estimator")
 
@@ -55,10 +55,17 @@ def latest_checkpoint(model_dir):
                     p = p if os.path.isabs(p) else os.path.join(model_dir, p)
                     if os.path.exists(p):
                         return p
-    cks = glob.glob(os.path.join(model_dir, "model.ckpt-*.pt"))
+    # rank 0's files only: "model.ckpt-<step>.pt" (per-rank files carry a "-rank<r>" suffix)
+    cks = [p for p in glob.glob(os.path.join(model_dir, "model.ckpt-*.pt"))
+           if re.search(r"model\.ckpt-\d+\.pt$", p)]
     if not cks:
         return None
     return max(cks, key=lambda p: int(re.search(r"model\.ckpt-(\d+)\.pt$", p).group(1)))
+
+
+def rank_checkpoint(path, rank):
+    """Rank ``rank``'s file of the checkpoint whose rank-0 file is ``path``."""
+    return path if rank == 0 else path.replace(".pt", "-rank%d.pt" % rank)
 
 
 def id_file_batches(path, batch_size, parse=int, shard=(0, 1)):
@@ -80,6 +87,12 @@ def id_file_batches(path, batch_size, parse=int, shard=(0, 1)):
                 batch, bi = [], bi + 1
     if batch and bi % ws == rk:
         yield batch
+
+
+def dist_backend():
+    import torch.distributed as dist
+
+    return dist.get_backend() if dist.is_available() and dist.is_initialized() else None
 
 
 class BaseEstimator:
@@ -176,13 +189,18 @@ class BaseEstimator:
         dense = [p for p in params if not is_sharded(p)]
         self._sync = dp.GradSync(dense, bucket_bytes=int(self.params.get("bucket_bytes", 32 << 20)))
 
-    def save(self, step=None, extra=None):
+    def save(self, step=None, extra=None, all_ranks=False):
+        """Write ``model.ckpt-<step>.pt`` (rank 0) and, when some state differs per rank
+        (sharded tables, or ``all_ranks``: e.g. the device path's per-rank sampler stream),
+        ``model.ckpt-<step>-rank<r>.pt`` on every other rank (reference per-worker outputs,
+        ``base_estimator.py:157-179``).  Rank 0 keeps the newest ``keep_checkpoint_max``
+        steps, every rank's file of a step together."""
         step = self.global_step if step is None else step
-        if self.rank != 0 and not any(is_sharded(p) for p in self.model.parameters()):
+        if self.rank != 0 and not all_ranks and not any(is_sharded(p) for p in self.model.parameters()):
             return None
         os.makedirs(self.model_dir, exist_ok=True)
-        suffix = "" if self.world == 1 or self.rank == 0 else "-rank%d" % self.rank
-        path = os.path.join(self.model_dir, "model.ckpt-%d%s.pt" % (step, suffix))
+        path = rank_checkpoint(os.path.join(self.model_dir, "model.ckpt-%d.pt" % step),
+                               0 if self.world == 1 else self.rank)
         model_state = {k: v for k, v in self.model.state_dict().items()
                        if not isinstance(v, nn.parameter.UninitializedParameter)}  # never-called lazy layers
         state = {"step": step, "model": model_state,
@@ -196,11 +214,16 @@ class BaseEstimator:
             with open(os.path.join(self.model_dir, "checkpoint"), "w") as f:
                 f.write('model_checkpoint_path: "%s"\n' % os.path.basename(path))
             keep = int(self.run_config.get("keep_checkpoint_max", self.params.get("keep_checkpoint_max", 5)))
-            cks = sorted(glob.glob(os.path.join(self.model_dir, "model.ckpt-*.pt")),
-                         key=lambda p: int(re.search(r"model\.ckpt-(\d+)", p).group(1)))
-            for old in cks[:-keep] if keep > 0 else []:
-                if not old.endswith(os.path.basename(path)):
-                    os.remove(old)
+            cks = glob.glob(os.path.join(self.model_dir, "model.ckpt-*.pt"))
+            step_of = {p: int(re.search(r"model\.ckpt-(\d+)", p).group(1)) for p in cks}
+            steps = sorted(set(step_of.values()))
+            drop = set(steps[:-keep]) - {step} if keep > 0 else set()
+            for old in cks:
+                if step_of[old] in drop:
+                    try:
+                        os.remove(old)
+                    except FileNotFoundError:
+                        pass
         return path
 
     def restore(self, path=None, strict=True):
@@ -208,7 +231,7 @@ class BaseEstimator:
         if path is None:
             return False
         if self.world > 1 and self.rank != 0:
-            own = path.replace(".pt", "-rank%d.pt" % self.rank)
+            own = rank_checkpoint(path, self.rank)
             if os.path.exists(own):
                 path = own
         state = torch.load(path, map_location=self.device, weights_only=True)
@@ -419,7 +442,14 @@ class BaseEstimator:
         (sample_node roots, SageDataFlow hops, feature / label lookup) and the model step
         run as captured gfx950 kernels on an HBM copy of the graph (models/sage_trainer.py);
         same params, logging, checkpoints (reference names + the device optimizer state
-        and Philox counter under "device_trainer") and resume as :meth:`train`."""
+        and Philox counter under "device_trainer") and resume as :meth:`train`.
+
+        Data parallel: every rank writes its own checkpoint file (same weights and
+        optimizer slots, its own sampler stream), so a resumed job continues every rank's
+        stream where it stopped; with a different world size each rank re-derives its key
+        (``seed * 7919 + rank``) and keeps the saved counter.  A timed-out xGMI wait (lost
+        peer) is checked at every log / checkpoint boundary: all ranks agree, drop the
+        captured graphs, re-synchronise rank 0's parameters and continue over RCCL."""
         total = int(self.params.get("total_step") or 1)
         log_steps = int(self.params.get("log_steps", 100))
         save_steps = int(self.run_config.get("save_checkpoints_steps", self.params.get("save_checkpoints_steps", 0))
@@ -428,47 +458,28 @@ class BaseEstimator:
         self.model.train()
         tr = self._device_graph_trainer(first)
         self.device_trainer = tr
-        path = latest_checkpoint(self.model_dir)
-        if path is not None:
-            state = torch.load(path, map_location="cpu", weights_only=True)
-            tr.load_logical({k: v for k, v in state["model"].items() if k in tr.state_dict()})
-            if state.get("device_trainer") is not None:
-                tr.load_trainer_state(state["device_trainer"])
-            self.global_step = int(state["step"])
-            tr.write_to_model(self.model)
-            log.info("restored %s at step %d (device path)", path, self.global_step)
+        self._device_restore(tr)
         if self.global_step >= total:
             log.info("already trained to step %d", self.global_step)
             return {}
-        grad_sync = None
+        grad_sync, xar, gbuf = None, None, None
         if self.world > 1:
             # xGMI two-shot peer-memory all-reduce or RCCL on GPUs, whichever the start-up
             # timing on this node finds faster (parallel/xgmi.py); gloo on CPUs
             from ..parallel.xgmi import make_grad_sync
 
             kind = "auto" if self.device.type == "cuda" else "rccl"
-            # the buffer grad_sync receives: SageTrainer's flat grad (bf16 hand-off: grad16),
-            # UnsupSageTrainer's FlatParams grad
-            gbuf = getattr(tr, "grad16", None)
-            if gbuf is None:
-                gbuf = getattr(tr, "grad", None)
-            if gbuf is None and hasattr(tr, "flat"):
-                gbuf = tr.flat.grad
+            gbuf = self._device_grad_buffer(tr)
             rebind = getattr(tr, "use_grad_buffer", None) if getattr(tr, "on_gpu", False) else None
-            grad_sync, name, _ = make_grad_sync(gbuf, str(self.params.get("grad_sync", kind)), rebind=rebind)
+            grad_sync, name, info = make_grad_sync(gbuf, str(self.params.get("grad_sync", kind)), rebind=rebind,
+                                                   timeout_s=float(self.params.get("xgmi_timeout_s", 10.0)))
+            xar = info.get("xar")
             log.info("device path gradient sync: %s all-reduce", name)
 
         use_graph = self.device.type == "cuda" and bool(self.params.get("hipgraph", True))
+        multi = hasattr(tr, "replay_steps")
         if use_graph:
-            warm = min(2, total - self.global_step)
-            # several complete steps per hipGraph replay (SageTrainer): the ~5 us gap between
-            # replays is paid once per chunk instead of once per step
-            multi = hasattr(tr, "replay_steps")
-            if multi:
-                tr.capture(grad_sync, warmup=warm, steps=int(self.params.get("steps_per_graph", 8)))
-            else:
-                tr.capture(grad_sync, warmup=warm)
-            self.global_step += warm
+            self.global_step += self._device_capture(tr, grad_sync, total)
 
         def run(n):
             if use_graph and multi:
@@ -484,13 +495,33 @@ class BaseEstimator:
         t0, n0 = time.time(), self.global_step
         tr.reset_metric()
         last = {}
+        delay = self.params.get("debug_delay_rank")  # test hook: one rank arrives late
         while self.global_step < total:
             # run up to the next log / checkpoint boundary in one go
             nxt = min(total, (self.global_step // log_steps + 1) * log_steps)
             if save_steps:
                 nxt = min(nxt, (self.global_step // save_steps + 1) * save_steps)
+            if delay is not None and int(delay) == self.rank:
+                time.sleep(float(self.params.get("debug_delay_s", 2.0)))
+                delay = None
             run(nxt - self.global_step)
             self.global_step = nxt
+            if xar is not None and self._xgmi_failed(xar):
+                # sums since the failed wait are partial: rank 0's state wins, RCCL from here
+                from ..parallel.xgmi import make_grad_sync
+
+                log.warning("rank %d: xGMI all-reduce wait timed out before step %d; re-synchronising rank 0's "
+                            "parameters and continuing over RCCL", self.rank, self.global_step)
+                self._device_release(tr)
+                self._xar_failed = xar  # keeps the IPC region alive while tensors still view it
+                xar = None
+                self._device_resync(tr)
+                grad_sync = make_grad_sync(gbuf, "rccl")[0]
+                self.grad_sync_fallback = True
+                if use_graph and dist_backend() == "gloo":
+                    use_graph = False  # gloo collectives are not capturable
+                if use_graph:
+                    self.global_step += self._device_capture(tr, grad_sync, total)
             if self.global_step % log_steps == 0 or self.global_step == total:
                 loss = float(tr.loss.item())  # syncs the stream
                 dt = max(time.time() - t0, 1e-9)
@@ -502,13 +533,109 @@ class BaseEstimator:
                     log.info("step = %d, loss = %.6f, %s = %.6f (%.1f samples/s, device path)", self.global_step,
                              loss, mname, last[mname], rate)
                 t0, n0 = time.time(), self.global_step
-            if save_steps and self.global_step % save_steps == 0:
-                tr.write_to_model(self.model)
-                self.save(extra={"device_trainer": tr.trainer_state(), "optimizer": None})
-        tr.write_to_model(self.model)
-        self.save(extra={"device_trainer": tr.trainer_state(), "optimizer": None})
+            if save_steps and self.global_step % save_steps == 0 and self.global_step < total:
+                self._device_save(tr)
+        self._device_save(tr)
+        # graphs holding captured collectives keep the communicator busy: drop them before
+        # the final barrier / process-group teardown
+        self._device_release(tr)
         dp.barrier()
         return last
+
+    @staticmethod
+    def _device_grad_buffer(tr):
+        """the buffer grad_sync receives: SageTrainer's flat grad (bf16 hand-off: grad16),
+        UnsupSageTrainer's FlatParams grad"""
+        gbuf = getattr(tr, "grad16", None)
+        if gbuf is None:
+            gbuf = getattr(tr, "grad", None)
+        if gbuf is None and hasattr(tr, "flat"):
+            gbuf = tr.flat.grad
+        return gbuf
+
+    def _device_capture(self, tr, grad_sync, total):
+        """capture the step graph(s); returns the eager warm-up steps it ran"""
+        warm = min(2, total - self.global_step)
+        if hasattr(tr, "replay_steps"):
+            # several complete steps per hipGraph replay (SageTrainer): the ~5 us gap between
+            # replays is paid once per chunk instead of once per step
+            tr.capture(grad_sync, warmup=warm, steps=int(self.params.get("steps_per_graph", 8)))
+        else:
+            tr.capture(grad_sync, warmup=warm)
+        return warm
+
+    @staticmethod
+    def _device_release(tr):
+        if callable(getattr(tr, "release_graphs", None)):
+            if getattr(tr, "on_gpu", False) or getattr(tr, "device", torch.device("cpu")).type == "cuda":
+                torch.cuda.synchronize(tr.device)
+            tr.release_graphs()
+        else:
+            tr._graph_exec = None
+
+    def _xgmi_failed(self, xar) -> bool:
+        """every rank's xGMI error word, agreed over the process group (MAX)"""
+        import torch.distributed as dist
+
+        err = int(xar.error())  # synchronises this rank's device
+        flag = torch.tensor([err], dtype=torch.int32)
+        if dist_backend() == "nccl":
+            flag = flag.to(self.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        return int(flag.item()) != 0
+
+    def _device_resync(self, tr):
+        """broadcast rank 0's parameters and optimizer state to every rank (after a
+        collective that may have left the ranks apart)"""
+        import torch.distributed as dist
+
+        for t in tr.dp_state_tensors():
+            if dist_backend() == "gloo" and t.is_cuda:
+                h = t.cpu()
+                dist.broadcast(h, 0)
+                t.copy_(h)
+            else:
+                dist.broadcast(t, 0)
+        if callable(getattr(tr, "refresh_shadows", None)):
+            tr.refresh_shadows()
+
+    def _device_restore(self, tr):
+        """resume from model_dir: weights + optimizer slots (rank 0's file, identical on every
+        rank) and this rank's own sampler stream"""
+        path = latest_checkpoint(self.model_dir)
+        if path is None:
+            return
+        state = torch.load(path, map_location="cpu", weights_only=True)
+        saved_world = int(state.get("world", 1))
+        own = rank_checkpoint(path, self.rank)
+        same_world = saved_world == self.world
+        if self.rank != 0 and same_world and os.path.exists(own):
+            state = torch.load(own, map_location="cpu", weights_only=True)
+        elif self.rank != 0:
+            same_world = False  # no file of this rank: derive its stream
+        tr.load_logical({k: v for k, v in state["model"].items() if k in tr.state_dict()})
+        st = state.get("device_trainer")
+        if st is not None:
+            st = dict(st)
+            if not same_world:
+                # a new rank layout: a per-rank key as at start-up, the saved counter (no
+                # rank replays a stream another rank already consumed)
+                rng = torch.as_tensor(st["rng"]).clone()
+                rng[0] = int(self.params.get("seed") or 0) * 7919 + self.rank
+                st["rng"] = rng
+            tr.load_trainer_state(st)
+        self.global_step = int(state["step"])
+        tr.write_to_model(self.model)
+        log.info("restored %s at step %d (device path, rank %d%s)", own if same_world else path, self.global_step,
+                 self.rank, "" if same_world else ", re-derived sampler key")
+
+    def _device_save(self, tr):
+        """every rank writes its checkpoint file (its own Philox stream); the barrier keeps
+        the other ranks out of the next chunk's collectives until rank 0 has written (a
+        rank spinning in an xGMI wait while rank 0 writes could time out)"""
+        tr.write_to_model(self.model)
+        self.save(extra={"device_trainer": tr.trainer_state(), "optimizer": None}, all_ranks=True)
+        dp.barrier()
 
     def _eval_batches(self):
         return self.evaluate_input_fn()

@@ -192,6 +192,12 @@ class DeviceGraph:
         self.rng[0] = int(seed)
         self._cpu_gen.manual_seed(int(seed))
 
+    def reseed_cpu(self):
+        """CPU twin: re-key the host generator from the (seed, counter) pair, so a CPU batch
+        is a function of the device RNG state alone (as the Philox draws are on the GPU) and
+        a checkpointed (seed, counter) reproduces it after a restart."""
+        self._cpu_gen.manual_seed((int(self.rng[0]) * 1000003 + int(self.rng[1])) % (1 << 63))
+
     def _mask(self, edge_types) -> int:
         if edge_types is None:
             return (1 << self.num_types) - 1

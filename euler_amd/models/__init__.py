@@ -1,5 +1,6 @@
-"""Model zoo (reference ``examples/*``) plus the fused GraphSAGE
-flagship used by ``bench.py``.
+"""Model zoo (reference ``examples/*``) plus the device-path trainers
+(:mod:`~euler_amd.models.sage_trainer` — the fused GraphSAGE step ``bench.py`` measures,
+:mod:`~euler_amd.models.sage_tower` — unsupervised GraphSAGE).
 
 * :mod:`~euler_amd.models.node_classification` — GraphSAGE, GCN, GAT, FastGCN,
   AdaptiveGCN, AGNN, APPNP, ARMA, DNA, SGCN, TAGCN, GeniePath, LGCN;
@@ -7,7 +8,6 @@ flagship used by ``bench.py``.
   DGI, GAE, VGAE, RGCN;
 * :mod:`~euler_amd.models.knowledge_graph` — TransE, TransH, TransR, TransD, DistMult;
 * :mod:`~euler_amd.models.graph_classification` — GIN, GatedGraph, GraphGCN, Set2Set;
-* :mod:`~euler_amd.models.fused_sage` — the device-resident fused GraphSAGE.
 """
 from euler_amd.models.graph_classification import GIN, GatedGraph, GraphGCN, Set2SetModel  # noqa: F401
 from euler_amd.models.knowledge_graph import DistMult, TransD, TransE, TransH, TransR  # noqa: F401

@@ -265,6 +265,10 @@ class UnsupSageTrainer:
         return {"m": self.opt.m.cpu().clone(), "v": self.opt.v.cpu().clone(),
                 "step": int(self.opt.step_count.item()), "rng": self.graph.rng.detach().cpu().clone()}
 
+    def dp_state_tensors(self):
+        """tensors equal on every data-parallel rank (what a re-synchronisation broadcasts)"""
+        return [self.flat.flat, self.opt.m, self.opt.v, self.opt.step_count]
+
     def load_trainer_state(self, st):
         self.opt.m.copy_(torch.as_tensor(st["m"]).to(self.opt.m))
         self.opt.v.copy_(torch.as_tensor(st["v"]).to(self.opt.v))
@@ -277,6 +281,8 @@ class UnsupSageTrainer:
         """(sources [B], positives [B], negatives [B*K]) int32 rows; -1 = no positive"""
         g = self.graph
         g.advance()
+        if self.device.type != "cuda":
+            g.reseed_cpu()
         src = g.sample_node(self.B, stream_id=5)
         pos = g.sample_neighbor(src, 1, self._types(self.pos_mask), -1, stream_id=6).reshape(-1)
         negs = g.sample_node(self.B * self.K, stream_id=7)

@@ -414,6 +414,13 @@ class SageTrainer:
         return {"m": {k: t.cpu() for k, t in m.items()}, "v": {k: t.cpu() for k, t in v.items()}, "step": step,
                 "rng": self.graph.rng.detach().cpu().clone(), "optimizer": self.opt_name}
 
+    def dp_state_tensors(self):
+        """tensors that must be equal on every data-parallel rank (parameters, optimizer
+        slots, step): what a re-synchronisation broadcasts from rank 0"""
+        if self.on_gpu:
+            return [self.flat, self.m, self.v, self._step]
+        return [t.data for t in self._cpu_params.values()] + list(self._cpu_m.values()) + list(self._cpu_v.values())
+
     def load_trainer_state(self, st):
         self.graph.rng.copy_(torch.as_tensor(st["rng"]).to(self.graph.rng))
         self.step_count = int(st["step"])
@@ -680,6 +687,7 @@ class SageTrainer:
 
     def _cpu_sample(self):
         g, B = self.graph, self.B
+        g.reseed_cpu()
         roots = g.sample_node(B).long()
         level = roots
         for k in range(1, self.L):

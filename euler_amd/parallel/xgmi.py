@@ -172,7 +172,7 @@ def _graph_call_us(fn, calls: int = 20, reps: int = 3, group=None) -> float:
     return float(t.item())
 
 
-def make_grad_sync(buf: torch.Tensor, kind: str = "auto", group=None, rebind=None):
+def make_grad_sync(buf: torch.Tensor, kind: str = "auto", group=None, rebind=None, timeout_s: float = 10.0):
     """``grad_sync(g)`` for a data-parallel trainer step (SageTrainer / UnsupSageTrainer
     ``step(grad_sync)``): an in-place sum all-reduce of (slices of) ``buf`` returning the
     1 / world scale.  ``kind``: "xgmi" (this module's kernel), "rccl" (torch.distributed
@@ -182,6 +182,7 @@ def make_grad_sync(buf: torch.Tensor, kind: str = "auto", group=None, rebind=Non
     or "tune" (the same, also with one rank).
     ``rebind(view)``: with xGMI chosen, hand the producer a view of the IPC input region to
     write its gradient into (SageTrainer.use_grad_buffer), after an in-place self-test.
+    ``timeout_s`` bounds every cross-GPU wait of the xGMI kernel.
     Returns ``(grad_sync, name, info)``; ``info`` holds the XgmiAllReduce (``xar``, None for
     RCCL, whose :meth:`~XgmiAllReduce.error` the caller checks after a run) and the timings."""
     world = dist.get_world_size(group)
@@ -191,7 +192,7 @@ def make_grad_sync(buf: torch.Tensor, kind: str = "auto", group=None, rebind=Non
     if kind == "tune":
         kind = "auto"
     if kind == "xgmi" or (kind == "auto" and world_ok and buf is not None and buf.is_cuda):
-        xar = XgmiAllReduce(buf.numel() * buf.element_size(), group=group)
+        xar = XgmiAllReduce(buf.numel() * buf.element_size(), group=group, timeout_s=timeout_s)
         if not xar.self_test(numel=buf.numel(), dtype=buf.dtype):
             if kind == "xgmi":
                 raise RuntimeError("xGMI all-reduce self-test failed")
@@ -219,6 +220,18 @@ def make_grad_sync(buf: torch.Tensor, kind: str = "auto", group=None, rebind=Non
             return 1.0 / world
 
         return grad_sync, "xgmi", info
+
+    if dist.get_backend(group) == "gloo":
+        def grad_sync(g):  # gloo: through host memory (eager only, not capturable)
+            if g.is_cuda:
+                h = g.cpu()
+                dist.all_reduce(h, group=group)
+                g.copy_(h)
+            else:
+                dist.all_reduce(g, group=group)
+            return 1.0 / world
+
+        return grad_sync, "gloo", info
 
     def grad_sync(g):
         dist.all_reduce(g, group=group)

@@ -51,3 +51,13 @@ def test_bench_distributed_path_one_rank(extra):
     assert "all-reduce" in out["config"]["grad_sync"] and out["value"] > 0
     first, last = out["config"]["loss_first_last"]
     assert last == last and first == first
+
+
+@pytest.mark.gpu
+def test_bench_gpus_flag_launches_ranks():
+    # plain `python bench.py --gpus 2` (the driver's BENCH invocation) starts 2 ranks itself;
+    # --shared-gpu puts both on the one GPU of the box (gloo group, xGMI all-reduce kernel)
+    out = _run([sys.executable, "bench.py", "--gpus", "2", "--shared-gpu"] + SMALL)
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["config"]["global_batch"] == 2 * 1024
+    assert "xgmi" in out["config"]["grad_sync"] and out["value"] > 0

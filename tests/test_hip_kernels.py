@@ -234,44 +234,3 @@ def test_flat_adam_matches_cpu(cuda):
             m(xx).pow(2).sum().backward()
             o.step()
     torch.testing.assert_close(f1.flat.cpu(), f2.flat, atol=1e-5, rtol=1e-5)
-
-
-def test_fused_sage_train_step_and_graph_capture(cuda):
-    from euler_amd.graph.device_graph import DeviceGraph
-    from euler_amd.models.fused_sage import FusedSupervisedGraphSage, synthetic_features, synthetic_labels
-    from euler_amd.parallel.flat import FlatOptimizer, FlatParams
-
-    g = DeviceGraph.synthetic(20_000, 8.0, 256, seed=1, device=cuda)
-    feats = synthetic_features(20_000, 64, 2, cuda)
-    labels = synthetic_labels(feats, 16)
-    torch.manual_seed(0)
-    model = FusedSupervisedGraphSage(64, 64, 16, [5, 3]).to(cuda)
-    flat = FlatParams(model.parameters(), cuda)
-    opt = FlatOptimizer(flat, "adam", 1e-2)
-    lb = torch.zeros((), device=cuda)
-
-    def step():
-        g.advance()
-        roots = g.sample_node(256)
-        levels, nbrs = model.sample(g, roots)
-        loss = model.loss(model(feats, levels, nbrs), labels[roots.long()])
-        flat.zero_grad()
-        loss.backward()
-        opt.step()
-        lb.copy_(loss.detach())
-
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
-        for _ in range(3):
-            step()
-    torch.cuda.current_stream().wait_stream(s)
-    flat.rebind_grads()
-    first = lb.item()
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
-        step()
-    for _ in range(200):
-        graph.replay()
-    torch.cuda.synchronize()
-    assert lb.item() < first, (first, lb.item())

@@ -653,3 +653,51 @@ def test_estimator_unsup_device_graph_data_parallel_lockstep(tmp_path):
     res = _run(_worker_estimator_unsup_device_dp, str(tmp_path))
     assert not [r for r in res if r[1] == "error"], res
     assert len(res) == 2 and all(r[2] for r in res), res
+
+
+def _worker_estimator_device_resume(rank, world, port, q, tmp):
+    """Device-path data parallelism with a SHARED model_dir (as a real job): run A trains 6
+    steps straight; run B trains 3, stops, and a fresh estimator resumes to 6.  Every rank
+    writes its own checkpoint file, so after the resume each rank continues ITS sample
+    stream: rank r's last batch and the final parameters equal run A's, and the ranks'
+    batches differ from each other (per-rank RNG state in checkpoints)."""
+    try:
+        _init(rank, world, port)
+        from euler_amd.tools import runner
+
+        def train(model_dir, total):
+            torch.manual_seed(0)  # the same initial weights in every run of this process
+            a = runner.parse_args(["--dataset", "ppi", "--scale", "0.05", "--batch_size", "32", "--total_step",
+                                   str(total), "--log_steps", "3", "--model_dir", model_dir, "--device_graph",
+                                   "--device", "cpu", "--seed", "1", "--fanouts", "5", "3"], model="graphsage")
+            _, est = runner.build(a)
+            est.train()
+            tr = est.device_trainer
+            p = tr.logical_params()
+            return est, [s.clone() for s in tr.samples()], torch.cat([p[k].reshape(-1).float() for k in sorted(p)])
+
+        est_a, smp_a, par_a = train(os.path.join(tmp, "a"), 6)
+        dist.barrier()
+        train(os.path.join(tmp, "b"), 3)
+        dist.barrier()
+        files = sorted(os.listdir(os.path.join(tmp, "b")))
+        est_b, smp_b, par_b = train(os.path.join(tmp, "b"), 6)
+        same_as_uninterrupted = all(torch.equal(x, y) for x, y in zip(smp_a, smp_b)) and torch.equal(par_a, par_b)
+        roots = smp_b[0]
+        other = [torch.zeros_like(roots) for _ in range(world)]
+        dist.all_gather(other, roots)
+        ranks_differ = not torch.equal(other[0], other[1])
+        per_rank_files = "model.ckpt-3.pt" in files and "model.ckpt-3-rank1.pt" in files
+        q.put((rank, "device_resume", bool(same_as_uninterrupted and ranks_differ and per_rank_files
+                                           and est_b.global_step == 6), files))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_estimator_device_graph_resume_keeps_per_rank_streams(tmp_path):
+    res = _run(_worker_estimator_device_resume, str(tmp_path))
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == 2 and all(r[2] for r in res), res

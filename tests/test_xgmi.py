@@ -151,3 +151,72 @@ def test_xgmi_block_count():
     assert xgmi._blocks_for(4096, 2, 4) == 4
     assert xgmi._blocks_for(8, 2, 2) == 1
     assert xgmi._blocks_for(1 << 30, 2, 4) == 64
+
+
+def _worker_estimator_timeout(rank, world, port, q, tmp):
+    """NodeEstimator(device_graph=True) on 2 ranks sharing the GPU with the xGMI all-reduce
+    forced and a 0.5 s wait bound; rank 1 arrives 3 s late at its first chunk, so rank 0's
+    waits time out.  The estimator must notice at the next boundary on BOTH ranks, drop the
+    graphs, re-synchronise rank 0's parameters and finish over the fallback all-reduce with
+    the ranks in lockstep."""
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+
+    try:
+        os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                           "WORLD_SIZE": str(world), "LOCAL_RANK": "0"})
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        from euler_amd.tools import runner
+
+        torch.manual_seed(0)
+        a = runner.parse_args(["--dataset", "ppi", "--scale", "0.05", "--batch_size", "64", "--total_step", "24",
+                               "--log_steps", "8", "--model_dir", os.path.join(tmp, f"ckpt{rank}"),
+                               "--device_graph", "--device", "cuda:0", "--seed", "1", "--fanouts", "5", "3"],
+                              model="graphsage")
+        _, est = runner.build(a)
+        est.params.update(grad_sync="xgmi", xgmi_timeout_s=0.5, debug_delay_rank=1, debug_delay_s=3.0)
+        est.train()
+        p = est.device_trainer.logical_params()
+        flat = torch.cat([p[k].reshape(-1).float().cpu() for k in sorted(p)])
+        allp = [torch.zeros_like(flat) for _ in range(world)]
+        dist.all_gather(allp, flat)
+        same = all(torch.equal(x, allp[0]) for x in allp)
+        q.put((rank, {"fallback": bool(getattr(est, "grad_sync_fallback", False)), "lockstep": same,
+                      "steps": est.global_step == 24, "finite": bool(torch.isfinite(flat).all())}))
+    except Exception:  # reported to the parent, which fails the test
+        import traceback
+
+        q.put((rank, {"exception": traceback.format_exc()}))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_estimator_falls_back_when_xgmi_wait_times_out(tmp_path):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 2
+    procs = [ctx.Process(target=_worker_estimator_timeout, args=(r, world, port, q, str(tmp_path)))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in range(world):
+            r, res = q.get(timeout=110)
+            out[r] = res
+    finally:
+        for p in procs:
+            p.join(timeout=20)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        res = out[r]
+        assert "exception" not in res, res
+        bad = [k for k, v in res.items() if not v]
+        assert not bad, (r, bad, res)

@@ -15,7 +15,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     from euler_amd.graph.device_graph import DeviceGraph
-    from euler_amd.models.fused_sage import synthetic_features, synthetic_labels
+    from euler_amd.dataset.synthetic import synthetic_features, synthetic_labels
     from euler_amd.models.sage_trainer import SageTrainer
     from euler_amd.ops._native import hip
 

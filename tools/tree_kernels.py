@@ -37,7 +37,7 @@ def main():
     ap.add_argument("--feature-dtype", default="bf16")
     args = ap.parse_args()
     from euler_amd.graph.device_graph import DeviceGraph
-    from euler_amd.models.fused_sage import synthetic_features, synthetic_labels
+    from euler_amd.dataset.synthetic import synthetic_features, synthetic_labels
     from euler_amd.models.sage_trainer import SageTrainer
 
     dev = torch.device("cuda", 0)
