@@ -195,7 +195,10 @@ def main(argv=None):
         if use_graph:
             ok = True
             try:
-                tr.capture(grad_sync, steps=max(1, args.steps_per_graph))
+                spg = max(1, args.steps_per_graph)
+                # remainder graphs for the warm-up and timed counts: every step of the timed
+                # region still runs, in as few replays as possible
+                tr.capture(grad_sync, steps=spg, extra_sizes=(args.warmup % spg, args.steps % spg))
             except RuntimeError as e:  # e.g. a collective the runtime cannot capture
                 ok = False
                 log(f"rank {rank}: step capture failed ({e}); running eager steps")

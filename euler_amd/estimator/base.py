@@ -559,7 +559,12 @@ class BaseEstimator:
         if hasattr(tr, "replay_steps"):
             # several complete steps per hipGraph replay (SageTrainer): the ~5 us gap between
             # replays is paid once per chunk instead of once per step
-            tr.capture(grad_sync, warmup=warm, steps=int(self.params.get("steps_per_graph", 8)))
+            spg = max(1, int(self.params.get("steps_per_graph", 8)))
+            log_steps = int(self.params.get("log_steps", 100))
+            save_steps = int(self.run_config.get("save_checkpoints_steps",
+                                                 self.params.get("save_checkpoints_steps", 0)) or 0)
+            # the remainders of the log / checkpoint chunks get graphs of their own
+            tr.capture(grad_sync, warmup=warm, steps=spg, extra_sizes=(log_steps % spg, save_steps % spg))
         else:
             tr.capture(grad_sync, warmup=warm)
         return warm

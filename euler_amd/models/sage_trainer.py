@@ -562,13 +562,14 @@ class SageTrainer:
             out += [("opt+gather", lambda: p.opt(2, 1.0, False, True)), ("fwd_gemm", lambda: p.fwd(None, True))]
         return out
 
-    def capture(self, grad_sync=None, warmup: int = 2, steps: int = 1):
+    def capture(self, grad_sync=None, warmup: int = 2, steps: int = 1, extra_sizes=()):
         """Record ``steps`` consecutive training steps into one hipGraph (after ``warmup``
         eager steps on a side stream); :meth:`replay` then runs it.  ``grad_sync`` is
         captured too (RCCL collectives are capturable).  ``steps > 1`` amortises the
         per-replay launch gap (~5 us between back-to-back replays of a ~74 us graph,
-        profiles/r3_headline/) over several complete steps; a 1-step graph is kept as well
-        for step counts that are not a multiple (:meth:`replay_steps`)."""
+        profiles/r3_headline/) over several complete steps; a 1-step graph is kept as well,
+        and one graph per entry of ``extra_sizes`` (e.g. the remainder of a known step
+        count), so :meth:`replay_steps` covers any count with few replays."""
         if not self.on_gpu:
             return None
         s = torch.cuda.Stream(device=self.device)
@@ -579,7 +580,7 @@ class SageTrainer:
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         self._graphs = {}
-        for k in sorted({1, int(steps)}, reverse=True):
+        for k in sorted({1, int(steps)} | {int(e) for e in extra_sizes if int(e) > 0}, reverse=True):
             g = torch.cuda.CUDAGraph()
             # thread-local capture: RCCL's watchdog thread keeps querying the events of
             # collectives that just finished; under the default global mode such a query
@@ -601,14 +602,13 @@ class SageTrainer:
         self.step_count += int(n)
 
     def replay_steps(self, n: int):
-        """exactly n training steps: the multi-step graph as often as it fits, then the
-        1-step graph for the rest"""
-        k = getattr(self, "_graph_steps", 1)
-        big, rest = divmod(int(n), k)
-        for _ in range(big):
-            self._graphs[k].replay()
-        for _ in range(rest):
-            self._graph_exec.replay()
+        """exactly n training steps, greedily from the largest captured graph down (the
+        multi-step graph as often as it fits, then the remainder graphs, 1-step last)"""
+        left = int(n)
+        for k in sorted(self._graphs, reverse=True):
+            while left >= k:
+                self._graphs[k].replay()
+                left -= k
         self.step_count += int(n)
 
     def release_graphs(self):
