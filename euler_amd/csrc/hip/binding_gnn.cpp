@@ -610,6 +610,41 @@ std::vector<torch::Tensor> unique_first_padded(torch::Tensor x, int64_t fill) {
   return {uniq, inv, pos.narrow(0, n - 1, 1).to(torch::kInt64)};
 }
 
+// Full neighbours of a capacity-padded row set (flow.hip): (nbr rows, target positions),
+// both int64 [cap], -1 past the real edge count; overflow[0] |= 1 when the edges exceed cap.
+// No allocation beyond the outputs and one scan buffer, no host sync (hipGraph-capturable).
+std::vector<torch::Tensor> full_neighbors(torch::Tensor indptr, torch::Tensor nbr, int64_t num_rows,
+                                          int64_t num_types, int64_t mask, torch::Tensor rows, int64_t cap,
+                                          torch::Tensor overflow) {
+  typed(indptr, torch::kInt64, "indptr");
+  typed(nbr, torch::kInt32, "nbr");
+  typed(rows, torch::kInt64, "rows");
+  typed(overflow, torch::kInt32, "overflow");
+  TORCH_CHECK(indptr.numel() == num_rows * num_types + 1, "full_neighbors: indptr size mismatch");
+  TORCH_CHECK(num_types >= 1 && num_types <= 32 && cap >= 0, "full_neighbors: bad arguments");
+  const c10::DeviceGuard g(rows.device());
+  const int64_t n = rows.numel();
+  auto opts = rows.options();
+  auto out_nbr = torch::empty({cap}, opts);
+  auto out_src = torch::empty({cap}, opts);
+  if (n == 0) {
+    out_nbr.fill_(-1);
+    out_src.fill_(-1);
+    return {out_nbr, out_src};
+  }
+  auto deg = torch::empty({n}, opts);
+  ok(eh_flow_degree(indptr.data_ptr<int64_t>(), num_rows, static_cast<int>(num_types), static_cast<uint32_t>(mask),
+                    rows.data_ptr<int64_t>(), n, deg.data_ptr<int64_t>(), stream()),
+     "flow_degree");
+  auto offs = torch::cumsum(deg, 0);
+  ok(eh_flow_expand(indptr.data_ptr<int64_t>(), nbr.data_ptr<int32_t>(), num_rows, static_cast<int>(num_types),
+                    static_cast<uint32_t>(mask), rows.data_ptr<int64_t>(), n, offs.data_ptr<int64_t>(), cap,
+                    out_nbr.data_ptr<int64_t>(), out_src.data_ptr<int64_t>(), overflow.data_ptr<int32_t>(),
+                    stream()),
+     "flow_expand");
+  return {out_nbr, out_src};
+}
+
 // C = op(A) op(B) (+ bias) (relu) (* relu'(rmask)) with the tiled MFMA GEMM (gemm.hip):
 // trans_a: A is [K][M]; trans_b: B is [N][K] (else [K][N]); A, B fp32 or bf16 row-major
 // (unit inner stride); C fp32 or bf16 [M][N] (row stride >= N) is written in place.
@@ -730,4 +765,5 @@ void register_gnn_ops(pybind11::module& m) {
         py::arg("dent"), py::arg("drel"), py::arg("occ") = false);
   m.def("unique_first", &unique_first);
   m.def("unique_first_padded", &unique_first_padded);
+  m.def("full_neighbors", &full_neighbors);
 }

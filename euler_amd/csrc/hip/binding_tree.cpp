@@ -71,6 +71,7 @@ class TreePlan {
     M_.assign(L_, 0);
     M_[0] = B_;
     for (int k = 1; k < L_; ++k) M_[k] = M_[k - 1] << logP_[k];
+    if (has("dw_route_impl")) route_impl_ = static_cast<int>(geti("dw_route_impl"));
     build_graph();
     build_fwd();
     build_comb();
@@ -120,9 +121,14 @@ class TreePlan {
   }
 
   // dW of the given problems, one launch: routed problems first, the others grouped
-  void dw(std::vector<int64_t> which) {
+  void dw(std::vector<int64_t> which, c10::optional<torch::Tensor> prof) {
     const c10::DeviceGuard g(dev_);
     TrDwLaunch L{};
+    L.route_impl = route_impl_;
+    if (prof.has_value()) {
+      TORCH_CHECK(prof->dtype() == torch::kInt64 && prof->is_cuda() && prof->is_contiguous(), "dw: prof");
+      L.prof = reinterpret_cast<long long*>(prof->data_ptr<int64_t>());
+    }
     for (int64_t i : which) {
       TORCH_CHECK(i >= 0 && i < (int64_t)probs_.size(), "dw: problem index out of range");
       if (probs_[i].route) {
@@ -226,6 +232,11 @@ class TreePlan {
     opt_.g16 = reinterpret_cast<uint16_t*>(g16_.data_ptr());
   }
   int64_t num_problems() const { return (int64_t)probs_.size(); }
+  // blocks of the routed problem i in a dw launch (the prof rows it stamps)
+  int64_t route_blocks(int64_t i) const {
+    const TrDwProb& p = probs_.at(i);
+    return p.route ? (int64_t)(p.P / 64) * ((p.Q + 127) / 128) * p.S : 0;
+  }
   std::vector<int64_t> splits() const {
     std::vector<int64_t> s;
     for (const auto& p : probs_) s.push_back(p.S);
@@ -236,6 +247,7 @@ class TreePlan {
   py::dict d_;
   int L_, B_, D_, E_, C_, C_real_, self_;
   int feat_fp32_ = 0, bm0_ = 32, bm1_ = 32;
+  int route_impl_ = 0;  // EULER_AMD_DW_ROUTE_IMPL / plan key dw_route_impl
   bool cached_ = false;
   std::vector<int64_t> F_, logP_, masks_, dims_, M_;
   c10::Device dev_{c10::kCPU};
@@ -855,7 +867,8 @@ void register_tree_ops(py::module& m) {
       .def("fwd_blocks", [](const TreePlan& t) { return t.fwd_blocks(); })
       .def("head", &TreePlan::head, py::arg("prof") = py::none(), py::arg("with_sample") = false)
       .def("bwd", &TreePlan::bwd)
-      .def("dw", &TreePlan::dw)
+      .def("dw", &TreePlan::dw, py::arg("which"), py::arg("prof") = py::none())
+      .def("route_blocks", &TreePlan::route_blocks)
       .def("opt", &TreePlan::opt, py::arg("mode"), py::arg("grad_scale") = 1.0, py::arg("with_sample") = false,
            py::arg("with_gather") = false)
       .def("pipeline_ok", &TreePlan::pipeline_ok)

@@ -137,6 +137,13 @@ hipError_t eh_unique_mark(int64_t n, const int32_t* slot, const int32_t* minpos,
 hipError_t eh_unique_finalize(const int64_t* x, int64_t n, const int32_t* slot, const int32_t* minpos,
                               const int32_t* flag, const int32_t* pos, int64_t* inv, int64_t* uniq, hipStream_t s);
 
+// flow.hip (device full-neighbourhood expansion, capacity-padded)
+hipError_t eh_flow_degree(const int64_t* indptr, int64_t num_rows, int num_types, uint32_t mask, const int64_t* rows,
+                          int64_t n, int64_t* deg, hipStream_t s);
+hipError_t eh_flow_expand(const int64_t* indptr, const int32_t* nbr, int64_t num_rows, int num_types, uint32_t mask,
+                          const int64_t* rows, int64_t n, const int64_t* offs, int64_t cap, int64_t* out_nbr,
+                          int64_t* out_src, int32_t* overflow, hipStream_t s);
+
 // optim.hip
 hipError_t eh_flat_optim(float* p, const float* g, float* m, float* v, int64_t n, int64_t* step, float lr, float b1,
                          float b2, float eps, float wd, float grad_scale, int kind, hipStream_t s);

@@ -1300,6 +1300,40 @@ __device__ __forceinline__ uint4_t tr_route_frag(const TrDwProb& pr, const Route
   return pack_bf16x8(v);
 }
 
+// the same fragment with a handful of instructions (the select chain above costs ~77 VALU
+// per fragment and made the routed dW issue-bound): which of the 8 rows are neighbour /
+// self slots is two 8-bit masks of j0, the ReLU bits pick rows, and `lut` (256 entries,
+// LDS) spreads an 8-bit row set into the 0xffff halves of 4 words; the values are the
+// bf16 pair of dn (resp. ds), rounded exactly like pack_bf16x8.
+__device__ __forceinline__ uint4_t tr_route_frag_lut(const TrDwProb& pr, const RouteRaw& r, int mb, int lk,
+                                                     const uint4_t* lut) {
+  const int j0 = static_cast<int>((static_cast<int64_t>(mb) * 32 + lk) & ((int64_t(1) << pr.logPg) - 1));
+  const int dF = pr.Fg - j0;
+  const uint32_t nm = dF >= 8 ? 0xffu : (dF <= 0 ? 0u : ((1u << dF) - 1u));
+  const uint32_t sm = (dF >= 0 && dF < 8) ? (1u << dF) : 0u;
+  const uint32_t b8 = r.bits & 0xffu;
+  const float dn = r.dn * pr.inv;
+  const float ds = r.ds + (pr.include_self ? dn : 0.f);
+  const uint32_t DN = pack_bf16x2(dn, dn), DS = pack_bf16x2(ds, ds);
+  const uint4_t mN = lut[b8 & nm], mS = lut[b8 & sm];
+  uint4_t out;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) out[i] = (DN & mN[i]) | (DS & mS[i]);
+  return out;
+}
+
+// lut[b] word i = (bit 2i of b ? 0x0000ffff : 0) | (bit 2i + 1 ? 0xffff0000 : 0); one entry
+// per thread of a 256-thread block (the caller synchronises before the first use)
+__device__ __forceinline__ void tr_spread_lut_init(uint4_t* lut) {
+  if (threadIdx.x < 256) {
+    const uint32_t b = threadIdx.x;
+    uint4_t w;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = (((b >> (2 * i)) & 1u) ? 0x0000ffffu : 0u) | (((b >> (2 * i + 1)) & 1u) ? 0xffff0000u : 0u);
+    lut[b] = w;
+  }
+}
+
 // ----------------------------------------------------------------------------
 // tr_dw_route: split-K dW of a layer whose output gradient is routed from the parent
 // rows (the tree mean's backward). Workgroup tile 64 p x 128 q; per stage of kRKB
@@ -1324,7 +1358,11 @@ struct RouteStage {
 
 typedef bf16_t RouteLds[2][kRKB][kRP * kRLd];
 
-__device__ __forceinline__ void tr_dw_route_body(const TrDwProb& pr, int b, RouteLds& gs) {
+#define RT_STAMP(k) \
+  if (prof && threadIdx.x == 0) prof[static_cast<int64_t>(b) * 8 + (k)] = static_cast<long long>(wall_clock64())
+__device__ __forceinline__ void tr_dw_route_body(const TrDwProb& pr, int b, RouteLds& gs, const uint4_t* lut,
+                                                 long long* prof) {
+  RT_STAMP(0);
   // XCD-aware: the tiles of one split (which read the same X rows) share b % 8
   const int j = b >> 3;
   const int tile = j % pr.ntiles;
@@ -1357,7 +1395,7 @@ __device__ __forceinline__ void tr_dw_route_body(const TrDwProb& pr, int b, Rout
     auto build = [&](const RouteStage& st, int buf, int mbs) {
 #pragma unroll
       for (int u = 0; u < kRKB; ++u) {
-        const uint4_t fr = (mbs + u) < mb1 ? tr_route_frag(pr, st.r[u], mbs + u, blk) : uint4_t{0u, 0u, 0u, 0u};
+        const uint4_t fr = (mbs + u) < mb1 ? tr_route_frag_lut(pr, st.r[u], mbs + u, blk, lut) : uint4_t{0u, 0u, 0u, 0u};
         *reinterpret_cast<uint4_t*>(&gs[buf][u][rt_off(bpl, blk)]) = fr;
       }
     };
@@ -1378,6 +1416,7 @@ __device__ __forceinline__ void tr_dw_route_body(const TrDwProb& pr, int b, Rout
     };
     RouteStage A, B;
     load(A, mb0);
+    int it = 0;
     for (int mbs = mb0; mbs < mb1; mbs += 2 * kRKB) {
       build(A, 0, mbs);
       load(B, mbs + kRKB);
@@ -1389,8 +1428,11 @@ __device__ __forceinline__ void tr_dw_route_body(const TrDwProb& pr, int b, Rout
         __syncthreads();
         compute(B, 1, mbs + kRKB);
       }
+      ++it;
+      if (it < 6) RT_STAMP(it);
     }
   }
+  RT_STAMP(7);
   if (!qok) return;
   float* out = pr.part + static_cast<int64_t>(s) * pr.P * Q;
   const int p0 = tp * kRP;
@@ -1402,6 +1444,85 @@ __device__ __forceinline__ void tr_dw_route_body(const TrDwProb& pr, int b, Rout
       for (int jj = 0; jj < 4; ++jj)
         out[(p0 + fm * 16 + (lane >> 4) * 4 + jj) * Q + wq + fn * 16 + lr] = acc[fm][fn][jj];
 }
+
+// ----------------------------------------------------------------------------
+// tr_dw_route_reg: the routed dW without the LDS G tile or any barrier.  Every wave builds
+// the G^T fragments of all 64 p rows of the tile in registers (p = p0 + 16 fm + lr, rows
+// lk..lk+7 of the k-block) from the ReLU bits and the parent's dA row (4x redundant across
+// the block's waves, served by L1) and multiplies them by its own 32 X columns; k-block
+// groups of kRG double-buffered in registers like the plain body, so the next group's
+// loads are in flight behind this group's build + MFMAs.
+// ----------------------------------------------------------------------------
+constexpr int kRG = 4;
+__device__ __forceinline__ void tr_dw_route_reg_body(const TrDwProb& pr, int b, const uint4_t* lut, long long* prof) {
+  RT_STAMP(0);
+  const int j = b >> 3;
+  const int tile = j % pr.ntiles;
+  const int s = (j / pr.ntiles) * 8 + (b & 7);
+  const int tp = tile / pr.tiles_q, tq = tile - tp * pr.tiles_q;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int lr = lane & 15, lk = (lane >> 4) * 8;
+  const int p0 = tp * kRP;
+  const int wq = tq * kRQ + wave * 32;
+  const int64_t Q = pr.Q, P = pr.P;
+  if (wq >= Q) return;  // no barriers in this body
+  const int mb0 = s * pr.kps;
+  const int mb1 = (mb0 + pr.kps) < pr.MB ? (mb0 + pr.kps) : pr.MB;
+  float4_t acc[4][2];
+  tl_zero(acc);
+  struct Grp {
+    uint4_t x[kRG][2];
+    RouteRaw r[kRG][4];
+  };
+  auto load = [&](Grp& g, int mbs) {
+#pragma unroll
+    for (int u = 0; u < kRG; ++u) {
+      const int mb = (mbs + u) < mb1 ? (mbs + u) : (mb1 - 1);
+#pragma unroll
+      for (int f = 0; f < 2; ++f)
+        g.x[u][f] = *reinterpret_cast<const uint4_t*>(pr.X + ((static_cast<int64_t>(mb) * Q + wq + f * 16 + lr) * 32 + lk));
+#pragma unroll
+      for (int fm = 0; fm < 4; ++fm) g.r[u][fm] = tr_route_load(pr, mb, p0 + fm * 16 + lr, lk);
+    }
+  };
+  auto compute = [&](const Grp& g, int mbs) {
+#pragma unroll
+    for (int u = 0; u < kRG; ++u) {
+      if (mbs + u >= mb1) break;  // uniform
+#pragma unroll
+      for (int fm = 0; fm < 4; ++fm) {
+        const uint4_t a = tr_route_frag_lut(pr, g.r[u][fm], mbs + u, lk, lut);
+#pragma unroll
+        for (int fn = 0; fn < 2; ++fn) acc[fm][fn] = mfma16(a, g.x[u][fn], acc[fm][fn]);
+      }
+    }
+  };
+  if (mb0 < mb1) {
+    Grp A, B;
+    load(A, mb0);
+    int it = 0;
+    for (int mbs = mb0; mbs < mb1; mbs += 2 * kRG) {
+      load(B, mbs + kRG);
+      compute(A, mbs);
+      if (mbs + kRG >= mb1) break;
+      load(A, mbs + 2 * kRG);
+      compute(B, mbs + kRG);
+      ++it;
+      if (it < 6 && (it & 1) == 0) RT_STAMP(it >> 1);
+    }
+  }
+  (void)P;
+  float* out = pr.part + static_cast<int64_t>(s) * pr.P * Q;
+#pragma unroll
+  for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+    for (int fn = 0; fn < 2; ++fn)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+        out[(p0 + fm * 16 + (lane >> 4) * 4 + jj) * Q + wq + fn * 16 + lr] = acc[fm][fn][jj];
+  RT_STAMP(7);
+}
+#undef RT_STAMP
 
 // ----------------------------------------------------------------------------
 // tr_dw: grouped split-K dW of the problems with stored G operands (kt layout),
@@ -1477,11 +1598,18 @@ __device__ __forceinline__ void tr_dw_plain_body(const TrDwProbs& probs, int b, 
 
 __global__ __launch_bounds__(256, 2) void tr_dw_all_kernel(TrDwLaunch a) {
   __shared__ __attribute__((aligned(16))) RouteLds gs;
+  __shared__ uint4_t lut[256];
   const int b = blockIdx.x;
+  if (a.nroute > 0 && b < a.rwg[a.nroute]) {  // routed blocks: the fragment-spread table first
+    tr_spread_lut_init(lut);
+    __syncthreads();
+  }
   if (a.nroute > 0 && b < a.rwg[1]) {
-    tr_dw_route_body(a.route[0], b, gs);
+    if (a.route_impl == 1) tr_dw_route_reg_body(a.route[0], b, lut, a.prof);
+    else tr_dw_route_body(a.route[0], b, gs, lut, a.prof);
   } else if (a.nroute > 1 && b < a.rwg[2]) {
-    tr_dw_route_body(a.route[1], b - a.rwg[1], gs);
+    if (a.route_impl == 1) tr_dw_route_reg_body(a.route[1], b - a.rwg[1], lut, nullptr);
+    else tr_dw_route_body(a.route[1], b - a.rwg[1], gs, lut, nullptr);
   } else {
     const int r = a.rwg[a.nroute];
     tr_dw_plain_body(a.plain, b - r, static_cast<int>(gridDim.x) - r);

@@ -199,7 +199,9 @@ struct TrDwLaunch {
   TrDwProbs plain;
   TrDwProb route[2];
   int32_t nroute;
-  int32_t rwg[3];  // block prefix of the routed problems
+  int32_t rwg[3];       // block prefix of the routed problems
+  int32_t route_impl;   // 0: G^T tile built once per block in LDS; 1: built per wave in registers
+  long long* prof;      // optional [route blocks][8] wall-clock stamps (diagnostics)
 };
 
 }  // namespace euler_hip

@@ -1,0 +1,180 @@
+"""Full-neighbourhood dataflow built on the device, in fixed (capacity-padded) shapes.
+
+The reference ``GCNDataFlow`` (``tf_euler/python/dataflow/gcn_dataflow.py:26-48``) expands
+every hop with ``get_full_neighbor`` over the whole current node set and dedups with
+``tf.unique`` (``neighbor_dataflow.py:84-110``), so its blocks change size every batch.  The
+engine path (``dataflows.GCNDataFlow``) reproduces that on the CPU graph engine and ships
+each block to the GPU.  Here the same blocks are built from the HBM copy of the graph
+(:class:`~euler_amd.graph.device_graph.DeviceGraph`) with every shape fixed up front:
+
+* node sets and edge lists have per-hop capacities (exact upper bounds from the graph's
+  maximum out-degree over the hop's edge types, never from a guess, so no batch can
+  overflow them); unused slots hold ``-1``;
+* ``-1`` is the padding convention every message-passing op already honours
+  (``mp_ops``: a ``-1`` destination / source edge is dropped, a ``-1`` gather row reads
+  zeros), so the unchanged model convolutions run on the padded blocks and padded rows
+  stay out of every real row;
+* the expansion is ``full_neighbors`` (``csrc/hip/flow.hip``: degree, scan, binary-search
+  expand; target-major edges in storage order, the reference's value order) and the dedup
+  ``unique_first_padded`` (``csrc/hip/unique.hip``: first-occurrence order = ``tf.unique``);
+  nothing syncs with the host, so sampling + model + backward + optimizer capture into
+  one hipGraph (``models/full_trainer.py``).
+
+Block layout equals ``UniqueDataFlow.produce_subgraph`` (``dataflows.py``): hop h's new
+set is ``unique([neighbours, previous set])``, ``res_n_id`` = the previous set's positions
+in it, edges = (target position, source position) for every neighbour occurrence and,
+with self loops, one (t, position of t) per target.
+"""
+from __future__ import annotations
+
+import torch
+
+from euler_amd.dataflow.dataflows import Block, DataFlow
+from euler_amd.ops._native import hip, use_hip
+
+__all__ = ["DeviceFullFlow", "full_neighbors_cpu", "max_out_degree"]
+
+
+def _round_up(x: int, m: int = 256) -> int:
+    return -(-int(x) // m) * m
+
+
+def max_out_degree(graph, mask: int) -> int:
+    """largest out-degree of any row over the edge types of ``mask``"""
+    T = graph.num_types
+    seg = (graph.indptr[1:] - graph.indptr[:-1]).view(graph.num_rows, T)
+    sel = torch.tensor([(mask >> t) & 1 for t in range(T)], dtype=seg.dtype, device=seg.device)
+    return int((seg * sel).sum(1).max().item()) if graph.num_rows else 0
+
+
+def masked_edges(graph, mask: int) -> int:
+    T = graph.num_types
+    seg = (graph.indptr[1:] - graph.indptr[:-1]).view(graph.num_rows, T)
+    sel = torch.tensor([(mask >> t) & 1 for t in range(T)], dtype=seg.dtype, device=seg.device)
+    return int((seg * sel).sum().item())
+
+
+def full_neighbors_cpu(graph, mask: int, rows: torch.Tensor, cap: int, overflow: torch.Tensor):
+    """torch twin of ``hip().full_neighbors`` (same order, same padding)"""
+    T = graph.num_types
+    rows = rows.reshape(-1).long()
+    ok = rows >= 0
+    r = torch.where(ok, rows, torch.zeros_like(rows))
+    nbrs, srcs = [], []
+    for i in range(rows.numel()):
+        if not bool(ok[i]):
+            continue
+        for t in range(T):
+            if not (mask >> t) & 1:
+                continue
+            a, b = int(graph.indptr[int(r[i]) * T + t]), int(graph.indptr[int(r[i]) * T + t + 1])
+            if b > a:
+                nbrs.append(graph.nbr[a:b].long())
+                srcs.append(torch.full((b - a,), i, dtype=torch.long))
+    nb = torch.cat(nbrs) if nbrs else torch.zeros(0, dtype=torch.long)
+    sc = torch.cat(srcs) if srcs else torch.zeros(0, dtype=torch.long)
+    if nb.numel() > cap:
+        overflow.fill_(1)
+        nb, sc = nb[:cap], sc[:cap]
+    out_n = torch.full((cap,), -1, dtype=torch.long)
+    out_s = torch.full((cap,), -1, dtype=torch.long)
+    out_n[: nb.numel()] = nb
+    out_s[: sc.numel()] = sc
+    return out_n, out_s
+
+
+def _unique_padded(x: torch.Tensor):
+    """(uniq padded with -1, inverse (-1 for -1 entries), count [1]) in first-occurrence order"""
+    if use_hip(x):
+        uniq, inv, cnt = hip().unique_first_padded(x.contiguous(), -1)
+        return uniq, inv, cnt
+    valid = x >= 0
+    vals = x[valid]
+    seen, order, inv_v = {}, [], []
+    for v in vals.tolist():
+        if v not in seen:
+            seen[v] = len(order)
+            order.append(v)
+        inv_v.append(seen[v])
+    uniq = torch.full_like(x, -1)
+    uniq[: len(order)] = torch.tensor(order, dtype=x.dtype)
+    inv = torch.full_like(x, -1)
+    inv[valid] = torch.tensor(inv_v, dtype=x.dtype)
+    return uniq, inv, torch.tensor([len(order)], dtype=torch.long)
+
+
+class DeviceFullFlow:
+    """``GCNDataFlow`` on the device with fixed shapes.
+
+    ``metapath``: one edge-type mask per hop (``DeviceGraph._mask``); ``batch_size``: the
+    number of roots (set 0, unpadded: the roots as drawn, repeats included, as the
+    reference).  ``caps`` (optional): per-hop (edge capacity, next-set capacity) pairs
+    overriding the exact bounds (smaller caps cost less; an overflow sets :attr:`overflow`
+    and :meth:`check` raises)."""
+
+    def __init__(self, graph, masks, batch_size: int, add_self_loops: bool = True, caps=None):
+        self.g = graph
+        self.masks = [int(m) for m in masks]
+        self.B = int(batch_size)
+        self.self_loops = bool(add_self_loops)
+        self.L = len(self.masks)
+        N = graph.num_rows
+        if caps is None:
+            caps = []
+            n = self.B
+            for m in self.masks:
+                e = min(masked_edges(graph, m), n * max_out_degree(graph, m))
+                n_next = min(N, n + e)
+                caps.append((_round_up(max(e, 1)), _round_up(n_next)))
+                n = n_next
+        self.caps = [(int(e), int(n)) for e, n in caps]
+        self.overflow = torch.zeros(1, dtype=torch.int32, device=graph.device)
+
+    def node_caps(self):
+        return [self.B] + [n for _, n in self.caps]
+
+    def produce(self, roots: torch.Tensor) -> DataFlow:
+        """the padded DataFlow of ``roots`` (int rows [B]); blocks carry fixed sizes
+        ``[cap_prev, cap_next]``; ``df.valid[h]`` = device count of real nodes of set h"""
+        g = self.g
+        n_id = roots.reshape(-1).long()
+        if n_id.numel() != self.B:
+            raise ValueError(f"expected {self.B} roots, got {n_id.numel()}")
+        dev = n_id.device
+        df = DataFlow(n_id)
+        last_idx = torch.arange(self.B, dtype=torch.long, device=dev)
+        cap_prev = self.B
+        for h, mask in enumerate(self.masks):
+            cap_e, cap_n = self.caps[h]
+            if use_hip(n_id):
+                nbr, src = hip().full_neighbors(g.indptr, g.nbr, g.num_rows, g.num_types, mask & 0xFFFFFFFF,
+                                                n_id, cap_e, self.overflow)
+            else:
+                nbr, src = full_neighbors_cpu(g, mask, n_id, cap_e, self.overflow)
+            cat = torch.cat([nbr, n_id])
+            uniq, inv, cnt = _unique_padded(cat)
+            # a set beyond its capacity: flag it and drop the excess (never index past it)
+            self.overflow.copy_(torch.maximum(self.overflow, (cnt.reshape(1) > cap_n).to(self.overflow.dtype)))
+            new_n_id = uniq[:cap_n] if uniq.numel() >= cap_n else torch.cat(
+                [uniq, torch.full((cap_n - uniq.numel(),), -1, dtype=uniq.dtype, device=dev)])
+            inv = torch.where(inv < cap_n, inv, torch.full_like(inv, -1))
+            res_n_id = inv[cap_e:]
+            if self.self_loops:
+                edge_t = torch.cat([src, last_idx])
+                edge_s = inv
+            else:
+                edge_t, edge_s = src, inv[:cap_e]
+            # an edge whose source was dropped by an overflow must not keep its target
+            edge_t = torch.where(edge_s >= 0, edge_t, torch.full_like(edge_t, -1))
+            df.blocks.append(Block(new_n_id, res_n_id, None, torch.stack([edge_t, edge_s]), [cap_prev, cap_n]))
+            df._last = new_n_id
+            ar = torch.arange(cap_n, dtype=torch.long, device=dev)
+            last_idx = torch.where(ar < cnt.reshape(()), ar, torch.full_like(ar, -1))
+            n_id = new_n_id
+            cap_prev = cap_n
+        return df
+
+    def check(self):
+        """raise if any batch so far exceeded a capacity (host sync)"""
+        if int(self.overflow.item()) != 0:
+            raise RuntimeError(f"device dataflow capacity exceeded (caps {self.caps}): raise the caps")

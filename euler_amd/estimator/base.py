@@ -409,17 +409,33 @@ class BaseEstimator:
         from euler_amd.graph.device_graph import DeviceGraph
         from euler_amd.models.sage_trainer import SageTrainer
 
+        from euler_amd.dataflow.dataflows import GCNDataFlow
+
         model = self.model
         gnn = getattr(model, "gnn", None)
         unsup = hasattr(model, "context_gnn")
         if gnn is None or not hasattr(gnn, "feature_idx") or not (unsup or hasattr(model, "label_idx")):
             raise ValueError("device_graph=True trains SupervisedGraphSage / UnsupervisedGraphSage-style models "
-                             "(gnn.feature_idx + label_idx, or a context_gnn)")
+                             "and the full-neighbourhood zoo (gnn.feature_idx + label_idx, or a context_gnn)")
         self._prepare(first)  # materialise the lazy layers, broadcast rank 0's weights
         nt = self.params.get("train_node_type", -1)
         node_type = -1 if nt in (None, -1, "-1") else int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
         fdt = torch.float32 if self.params.get("device_feature_dtype", "bf16") == "fp32" else torch.bfloat16
         seed = int(self.params.get("seed") or 0)
+        if isinstance(getattr(gnn, "sampler", None), GCNDataFlow):
+            # GCN / APPNP / SGCN / TAGCN / ... : full-neighbourhood blocks built on the device
+            from euler_amd.models.full_trainer import FullFlowTrainer
+
+            if self._sync is not None:
+                self._sync.remove()  # the trainer all-reduces its flat gradient itself
+            graph = DeviceGraph.from_engine(node_type=node_type, features=gnn.feature_idx,
+                                            feature_dims=gnn.feature_dim, label=model.label_idx,
+                                            label_dim=model.label_dim, feature_dtype=fdt,
+                                            seed=seed * 7919 + self.rank, device=self.device)
+            return FullFlowTrainer.from_model(model, graph, int(self.params["batch_size"]),
+                                              optimizer=self.params.get("optimizer", "adam"),
+                                              learning_rate=float(self.params.get("learning_rate", 0.001)),
+                                              caps=self.params.get("device_flow_caps"))
         if unsup:
             from euler_amd.models.sage_tower import UnsupSageTrainer
 

@@ -317,7 +317,8 @@ class SageTrainer:
              "offsets": self.offsets, "loss_acc": self.loss_acc, "loss_out": self.loss_out, "counts": self.counts,
              "lr": self.lr, "beta1": self.betas[0], "beta2": self.betas[1], "eps": self.eps,
              "weight_decay": self.wd, "opt_kind": _OPT_KIND[self.opt_name]}
-        for key in ("EULER_AMD_DW_TARGET_WG", "EULER_AMD_DW_MIN_KPS", "EULER_AMD_DW_ROUTE_WG", "EULER_AMD_FWD_BM"):
+        for key in ("EULER_AMD_DW_TARGET_WG", "EULER_AMD_DW_MIN_KPS", "EULER_AMD_DW_ROUTE_WG", "EULER_AMD_FWD_BM",
+                    "EULER_AMD_DW_ROUTE_IMPL"):
             if os.environ.get(key):
                 d[key[len("EULER_AMD_"):].lower()] = int(os.environ[key])
         M_last = self.M[L - 1]

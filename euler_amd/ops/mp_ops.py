@@ -47,14 +47,14 @@ class SegmentIndex:
         self._counts = None
 
     def _build(self):
-        # padding destinations (< 0) go to a sentinel segment past the end
+        # padding destinations (< 0) go to a sentinel segment past the end; the segment
+        # bounds come from a binary search of the sorted destinations (no bincount: its
+        # output size depends on the data, a host sync that a captured step cannot have)
         idx = torch.where(self.indices < 0, torch.full_like(self.indices, self.size), self.indices)
         self._perm = torch.argsort(idx, stable=True)
-        counts = torch.bincount(idx, minlength=self.size + 1)[: self.size]
-        self._counts = counts
-        indptr = torch.zeros(self.size + 1, dtype=torch.long, device=idx.device)
-        torch.cumsum(counts, 0, out=indptr[1:])
-        self._indptr = indptr
+        bounds = torch.arange(self.size + 1, dtype=torch.long, device=idx.device)
+        self._indptr = torch.searchsorted(idx[self._perm].contiguous(), bounds)
+        self._counts = self._indptr[1:] - self._indptr[:-1]
 
     @property
     def perm(self):

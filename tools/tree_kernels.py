@@ -59,6 +59,7 @@ def main():
     for i in range(p.num_problems()):
         res[f"dw[{i}]"] = round(timeit(lambda: p.dw([i]), args.reps), 2)
     res["dw_splits"] = p.splits()
+    res["route_profile"] = route_profile(tr)
     tr.capture(steps=4)
     res["graph_step"] = round(timeit(lambda: tr.replay(1), args.reps), 2)
     res["graph_step_x4"] = round(timeit(lambda: tr.replay_steps(4), args.reps) / 4, 2)  # per step
@@ -94,6 +95,37 @@ def main():
               "block time", round(float((f[:, 5] - f[:, 0]).mean()), 2))
         print("head phases (us, mean over blocks):", [round(v, 2) for v in ph],
               "span", round(float(t[:, 7].max() - t0), 2), "start skew", round(float(t[:, 0].max() - t0), 2))
+
+
+def route_profile(tr, reps=3):
+    """wall-clock stamps of the routed dW blocks (problem 0): start, progress points, end"""
+    p = tr.plan
+    nb = p.route_blocks(0)
+    if nb == 0:
+        return None
+    prof = torch.zeros(nb * 8, dtype=torch.int64, device=tr.device)
+    for _ in range(reps):
+        prof.zero_()
+        p.dw([0], prof)
+    torch.cuda.synchronize()
+    t = prof.view(-1, 8).cpu().double() / 100.0  # wall_clock64 = 100 MHz
+    t0 = t[:, 0].min()
+    out = {"blocks": nb, "start_skew_us": round(float(t[:, 0].max() - t0), 2),
+           "span_us": round(float(t[:, 7].max() - t0), 2),
+           "block_time_mean_us": round(float((t[:, 7] - t[:, 0]).mean()), 2),
+           "block_time_max_us": round(float((t[:, 7] - t[:, 0]).max()), 2)}
+    prog = []
+    prev = t[:, 0]
+    for k in range(1, 7):
+        col = t[:, k]
+        ok = col > 0
+        if not bool(ok.any()):
+            break
+        prog.append(round(float((col[ok] - prev[ok]).mean()), 2))
+        prev = torch.where(ok, col, prev)
+    out["progress_deltas_us"] = prog
+    out["tail_us"] = round(float((t[:, 7] - prev).mean()), 2)
+    return out
 
 
 if __name__ == "__main__":
