@@ -71,7 +71,7 @@ def parse_args(argv=None):
                    help="row-shard the feature table over the ranks (row r on rank r %% world); every step's "
                         "sampled rows come over an all-to-all (graph/sharded_features.py). Needs the process "
                         "group: torchrun, or --force-dist with one rank")
-    p.add_argument("--steps-per-graph", type=int, default=8,
+    p.add_argument("--steps-per-graph", type=int, default=32,
                    help="complete training steps captured per hipGraph (replays amortise the per-launch gap; "
                         "the timed region still runs exactly --steps steps)")
     p.add_argument("--force-dist", action="store_true",

@@ -32,7 +32,11 @@ def run(path, args, work):
     if path == "device":
         argv.append("--device_graph")
     t0 = time.time()
-    res, ev = main(argv, model="graphsage")
+    if args.model != "graphsage":
+        argv = [a for a in argv]
+        i = argv.index("--fanouts")
+        del argv[i:i + 3]  # full-neighbourhood models take no fanouts
+    res, ev = main(argv, model=args.model)
     return {"train_last": {k: round(float(v), 4) for k, v in res.items()}, "heldout": {k: round(float(v), 4)
                                                                                        for k, v in ev.items()},
             "wall_s": round(time.time() - t0, 1)}
@@ -45,12 +49,15 @@ def main(argv=None):
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--device", default="cuda")
+    ap.add_argument("--model", default="graphsage", help="graphsage, or a full-neighbourhood model (gcn, appnp, "
+                                                          "sgcn, tagcn)")
     args = ap.parse_args(argv)
     work = tempfile.mkdtemp(prefix="community_f1_")
     os.environ.setdefault("EULER_AMD_DATA", os.path.join(work, "data"))
-    out = {"metric": "held-out micro-F1, supervised GraphSAGE (NodeEstimator)", "dataset": "community (synthetic "
+    out = {"metric": f"held-out micro-F1, supervised {args.model} (NodeEstimator)", "dataset": "community (synthetic "
            "planted communities, 20000 nodes, 16 classes, 10% label noise)", "steps": args.steps,
-           "batch_size": args.batch_size, "fanouts": [10, 10], "device": args.device}
+           "batch_size": args.batch_size, "fanouts": [10, 10] if args.model == "graphsage" else None,
+           "device": args.device}
     for path in ("engine", "device"):
         out[path] = run(path, args, work)
         print(f"[community_f1] {path}: {out[path]}", file=sys.stderr, flush=True)
