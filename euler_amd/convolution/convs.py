@@ -23,7 +23,6 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from euler_amd.ops import gnn_ops, mp_ops
-from euler_amd.ops.mp_ops import SegmentIndex
 from euler_amd.utils.layers import Dense
 
 __all__ = ["Conv", "GCNConv", "SAGEConv", "GATConv", "TAGConv", "AGNNConv", "SGCNConv", "GINConv", "GraphConv",
@@ -31,18 +30,8 @@ __all__ = ["Conv", "GCNConv", "SAGEConv", "GATConv", "TAGConv", "AGNNConv", "SGC
 
 
 def _seg(edge_index, i, size):
-    """destination CSR of edge_index[i] (cached on the tensor object)."""
-    key = "_euler_seg%d_%d" % (i, int(size))
-    cache = getattr(edge_index, "_euler_cache", None)
-    if cache is None:
-        cache = {}
-        try:
-            edge_index._euler_cache = cache
-        except AttributeError:
-            pass
-    if key not in cache:
-        cache[key] = SegmentIndex(edge_index[i], int(size))
-    return cache[key]
+    """destination CSR of edge_index[i] (cached on the tensor object, shared with the SpMM)."""
+    return mp_ops.cached_segment(edge_index, i, size)
 
 
 class Conv(nn.Module):
@@ -71,7 +60,8 @@ class Conv(nn.Module):
         ones = torch.ones(edge_index.shape[1], 1, device=edge_index.device)
 
         def dis(i):
-            deg = mp_ops.scatter_add(ones, _seg(edge_index, i, size[i]), size[i])
+            # the in-degree of every segment is its CSR count (the reference's sum of ones)
+            deg = _seg(edge_index, i, size[i]).counts.to(ones.dtype).unsqueeze(1)
             return deg.clamp(min=1e-12).pow(-0.5)
 
         return dis(0), dis(1)

@@ -610,8 +610,9 @@ std::vector<torch::Tensor> unique_first_padded(torch::Tensor x, int64_t fill) {
   return {uniq, inv, pos.narrow(0, n - 1, 1).to(torch::kInt64)};
 }
 
-// Full neighbours of a capacity-padded row set (flow.hip): (nbr rows, target positions),
-// both int64 [cap], -1 past the real edge count; overflow[0] |= 1 when the edges exceed cap.
+// Full neighbours of a capacity-padded row set (flow.hip): (nbr rows, target positions,
+// inclusive per-target edge offsets [n]); the first two int64 [cap], -1 past the real edge
+// count; overflow[0] |= 1 when the edges exceed cap.
 // No allocation beyond the outputs and one scan buffer, no host sync (hipGraph-capturable).
 std::vector<torch::Tensor> full_neighbors(torch::Tensor indptr, torch::Tensor nbr, int64_t num_rows,
                                           int64_t num_types, int64_t mask, torch::Tensor rows, int64_t cap,
@@ -630,7 +631,7 @@ std::vector<torch::Tensor> full_neighbors(torch::Tensor indptr, torch::Tensor nb
   if (n == 0) {
     out_nbr.fill_(-1);
     out_src.fill_(-1);
-    return {out_nbr, out_src};
+    return {out_nbr, out_src, torch::zeros({0}, opts)};
   }
   auto deg = torch::empty({n}, opts);
   ok(eh_flow_degree(indptr.data_ptr<int64_t>(), num_rows, static_cast<int>(num_types), static_cast<uint32_t>(mask),
@@ -642,7 +643,7 @@ std::vector<torch::Tensor> full_neighbors(torch::Tensor indptr, torch::Tensor nb
                     out_nbr.data_ptr<int64_t>(), out_src.data_ptr<int64_t>(), overflow.data_ptr<int32_t>(),
                     stream()),
      "flow_expand");
-  return {out_nbr, out_src};
+  return {out_nbr, out_src, offs};  // offs: inclusive edge offsets per target
 }
 
 // C = op(A) op(B) (+ bias) (relu) (* relu'(rmask)) with the tiled MFMA GEMM (gemm.hip):

@@ -31,6 +31,7 @@ import torch
 
 from euler_amd.dataflow.dataflows import Block, DataFlow
 from euler_amd.ops._native import hip, use_hip
+from euler_amd.ops.mp_ops import SegmentIndex
 
 __all__ = ["DeviceFullFlow", "full_neighbors_cpu", "max_out_degree"]
 
@@ -80,7 +81,33 @@ def full_neighbors_cpu(graph, mask: int, rows: torch.Tensor, cap: int, overflow:
     out_s = torch.full((cap,), -1, dtype=torch.long)
     out_n[: nb.numel()] = nb
     out_s[: sc.numel()] = sc
-    return out_n, out_s
+    deg = torch.bincount(sc, minlength=rows.numel())[: rows.numel()] if sc.numel() else \
+        torch.zeros(rows.numel(), dtype=torch.long)
+    return out_n, out_s, torch.cumsum(deg, 0)
+
+
+def _dst_csr(src, offs, n_targets, cap_e, cap_t, self_loops):
+    """(perm, indptr) of the block's destination CSR, straight from the expansion: edges are
+    target-major already, so target t's edges are its neighbours [offs[t-1], offs[t]) then
+    (with self loops) its self edge cap_e + t — the order a stable sort of the reference
+    edge list ([neighbours..., self loops...]) gives — and no sort is needed.  Padding
+    edges fill the tail (the sentinel segment past indptr[cap_t])."""
+    dev = src.device
+    excl = torch.cat([torch.zeros(1, dtype=torch.long, device=dev), offs])  # [cap_t + 1]
+    if not self_loops:
+        return torch.arange(cap_e, dtype=torch.long, device=dev), excl
+    t_ar = torch.arange(cap_t + 1, dtype=torch.long, device=dev)
+    indptr = excl + torch.minimum(t_ar, n_targets)
+    e_ar = torch.arange(cap_e, dtype=torch.long, device=dev)
+    new_nbr = torch.where(src >= 0, e_ar + src, e_ar + n_targets)
+    t = t_ar[:-1]
+    new_self = torch.where(t < n_targets, excl[1:] + t, cap_e + t)
+    new_pos = torch.cat([new_nbr, new_self])
+    # zeros, not empty: after a capacity overflow (flagged, raised at the next check) the
+    # positions may collide, and every entry must still be a valid edge index
+    perm = torch.zeros_like(new_pos)
+    perm.scatter_(0, new_pos, torch.arange(new_pos.numel(), dtype=torch.long, device=dev))
+    return perm, indptr
 
 
 def _unique_padded(x: torch.Tensor):
@@ -143,14 +170,15 @@ class DeviceFullFlow:
         dev = n_id.device
         df = DataFlow(n_id)
         last_idx = torch.arange(self.B, dtype=torch.long, device=dev)
+        prev_cnt = torch.full((), self.B, dtype=torch.long, device=dev)
         cap_prev = self.B
         for h, mask in enumerate(self.masks):
             cap_e, cap_n = self.caps[h]
             if use_hip(n_id):
-                nbr, src = hip().full_neighbors(g.indptr, g.nbr, g.num_rows, g.num_types, mask & 0xFFFFFFFF,
-                                                n_id, cap_e, self.overflow)
+                nbr, src, offs = hip().full_neighbors(g.indptr, g.nbr, g.num_rows, g.num_types, mask & 0xFFFFFFFF,
+                                                      n_id, cap_e, self.overflow)
             else:
-                nbr, src = full_neighbors_cpu(g, mask, n_id, cap_e, self.overflow)
+                nbr, src, offs = full_neighbors_cpu(g, mask, n_id, cap_e, self.overflow)
             cat = torch.cat([nbr, n_id])
             uniq, inv, cnt = _unique_padded(cat)
             # a set beyond its capacity: flag it and drop the excess (never index past it)
@@ -166,10 +194,17 @@ class DeviceFullFlow:
                 edge_t, edge_s = src, inv[:cap_e]
             # an edge whose source was dropped by an overflow must not keep its target
             edge_t = torch.where(edge_s >= 0, edge_t, torch.full_like(edge_t, -1))
-            df.blocks.append(Block(new_n_id, res_n_id, None, torch.stack([edge_t, edge_s]), [cap_prev, cap_n]))
+            edge_index = torch.stack([edge_t, edge_s])
+            # the destination CSR is known from the expansion: the convolutions' scatters and
+            # SpMM reuse it instead of sorting (mp_ops.cached_segment)
+            perm, indptr = _dst_csr(src, offs.clamp(max=cap_e), prev_cnt, cap_e, cap_prev, self.self_loops)
+            edge_index._euler_cache = {"_euler_seg0_%d" % cap_prev: SegmentIndex.from_csr(edge_t, cap_prev, perm,
+                                                                                             indptr)}
+            df.blocks.append(Block(new_n_id, res_n_id, None, edge_index, [cap_prev, cap_n]))
             df._last = new_n_id
             ar = torch.arange(cap_n, dtype=torch.long, device=dev)
-            last_idx = torch.where(ar < cnt.reshape(()), ar, torch.full_like(ar, -1))
+            prev_cnt = torch.clamp(cnt.reshape(()), max=cap_n)
+            last_idx = torch.where(ar < prev_cnt, ar, torch.full_like(ar, -1))
             n_id = new_n_id
             cap_prev = cap_n
         return df

@@ -46,6 +46,14 @@ class SegmentIndex:
         self._indptr = None
         self._counts = None
 
+    @classmethod
+    def from_csr(cls, indices, size, perm, indptr):
+        """a SegmentIndex whose stable destination order is already known"""
+        s = cls(indices, size)
+        s._perm, s._indptr = perm, indptr
+        s._counts = indptr[1:] - indptr[:-1]
+        return s
+
     def _build(self):
         # padding destinations (< 0) go to a sentinel segment past the end; the segment
         # bounds come from a binary search of the sorted destinations (no bincount: its
@@ -73,6 +81,24 @@ class SegmentIndex:
         if self._counts is None:
             self._build()
         return self._counts
+
+
+def cached_segment(edge_index, i, size) -> SegmentIndex:
+    """The CSR of ``edge_index[i]`` (``size`` segments), built once per edge_index tensor and
+    shared by every op over it (degree normalisations, scatters, the SpMM and its
+    backward); a producer that already knows the CSR (dataflow/device_flow.py) stores it
+    here under the same key."""
+    key = "_euler_seg%d_%d" % (i, int(size))
+    cache = getattr(edge_index, "_euler_cache", None)
+    if cache is None:
+        cache = {}
+        try:
+            edge_index._euler_cache = cache
+        except AttributeError:
+            return SegmentIndex(edge_index[i], int(size))
+    if key not in cache:
+        cache[key] = SegmentIndex(edge_index[i], int(size))
+    return cache[key]
 
 
 def segment_index(indices, size) -> SegmentIndex:
@@ -220,8 +246,8 @@ class _SpmmIndex:
     """Destination CSR and source CSC of one ``edge_index`` for weighted aggregation."""
 
     def __init__(self, edge_index, size):
-        self.dst = SegmentIndex(edge_index[0], size[0])
-        self.src = SegmentIndex(edge_index[1], size[1])
+        self.dst = cached_segment(edge_index, 0, size[0])
+        self.src = cached_segment(edge_index, 1, size[1])
         self.col = edge_index[1].reshape(-1).long()[self.dst.perm].contiguous()   # sources, CSR order
         self.row = edge_index[0].reshape(-1).long()[self.src.perm].contiguous()   # destinations, CSC order
 

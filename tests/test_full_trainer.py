@@ -167,3 +167,23 @@ def test_estimator_device_graph_gcn_family_gpu(tmp_path, monkeypatch, model):
               "--seed", "1", "--model_dir", str(tmp_path / "ckpt"), "--device_graph", "--total_step", "80",
               "--learning_rate", "0.01"], model=model)
     assert r["step"] == 80 and math.isfinite(r["loss"]) and r["loss"] < 0.69
+
+
+def test_device_flow_dst_csr_equals_sorted_csr_cpu():
+    """the destination CSR handed to the convolutions equals the stable sort the engine
+    path would compute (SegmentIndex on the same edge list)"""
+    from euler_amd.dataflow.device_flow import DeviceFullFlow
+    from euler_amd.ops.mp_ops import SegmentIndex
+
+    _, m, _ = _setup("cpu")
+    g = _device_graph(m, "cpu")
+    flow = m.gnn.sampler
+    for loops in (True, False):
+        dflow = DeviceFullFlow(g, _masks(g, flow), 16, add_self_loops=loops)
+        roots = torch.randint(0, g.num_rows, (16,), generator=torch.Generator().manual_seed(9))
+        for b in dflow.produce(roots).blocks:
+            pre = b.edge_index._euler_cache["_euler_seg0_%d" % b.size[0]]
+            ref = SegmentIndex(b.edge_index[0], b.size[0])
+            n_real = int(ref.indptr[-1])
+            assert torch.equal(pre.indptr, ref.indptr)
+            assert torch.equal(pre.perm[:n_real], ref.perm[:n_real])
