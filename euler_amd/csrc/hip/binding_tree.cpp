@@ -689,7 +689,9 @@ class TowerPlan {
     g_.pop = prob.numel();
     g_.prob = prob.data_ptr<float>();
     g_.alias = ptr<int32_t>("node_alias", torch::kInt32, g_.pop);
-    g_.root_rows = nullptr;
+    // candidate -> row map of the root sampler (node-type subset); used when the roots are
+    // drawn in the sampler (PairPlan), not when they are given
+    g_.root_rows = has("root_rows") ? ptr<int32_t>("root_rows", torch::kInt32, g_.pop) : nullptr;
     tree_.rng = rng.data_ptr<int64_t>();
     tree_.root_in = ptr<int32_t>("roots_in", torch::kInt32, R_);
     tree_.F1 = static_cast<int32_t>(F1_);
@@ -706,7 +708,7 @@ class TowerPlan {
     sample_.FL = static_cast<int32_t>(F2_);
     sample_.mL = static_cast<uint32_t>(geti("mask2"));
     sample_.hopL = 2;
-    sample_.roots = owned_i32(R_);
+    sample_.roots = has("roots_out") ? ptr<int32_t>("roots_out", torch::kInt32, R_) : owned_i32(R_);
     sample_.nodes = ptr<int32_t>("nodes", torch::kInt32, M_);
     sample_.leaf = ptr<int32_t>("leaf", torch::kInt32, M_ * F2_);
     // layer 0 (mode 0)
@@ -804,6 +806,18 @@ class TowerPlan {
     const c10::DeviceGuard g(dev_);
     ok(eh_tr_fwd(&fwd_, 0, feat_fp32_, bm_, stream()), "tower fwd");
   }
+  // internals for PairPlan (the fused pair step reuses this tower's sampler / forward /
+  // routed dW description)
+  const TrSampleArgs& sample_args() const { return sample_; }
+  const TrFwdArgs& fwd_args() const { return fwd_; }
+  const TrDwProb& prob() const { return prob_; }
+  int feat_fp32() const { return feat_fp32_; }
+  int bm() const { return bm_; }
+  int64_t R() const { return R_; }
+  int64_t H() const { return H_; }
+  int64_t D() const { return D_; }
+  c10::Device device() const { return dev_; }
+
   // dA1 (the plan's buffer) -> gW0 (the plan's buffer)
   void bwd() {
     const c10::DeviceGuard g(dev_);
@@ -856,6 +870,265 @@ class TowerPlan {
   }
 };
 
+// The fused unsupervised GraphSAGE step (models/sage_tower.py, fused mode): both towers'
+// layer 0 (their TowerPlan samplers + forwards; the roots are drawn inside the samplers:
+// source roots from the alias table, the context tower's positives as one out-neighbour of
+// the recomputed source root and its negatives from a stream of their own), the pair head
+// (tr_pair_head: last conv + fc of both towers, pair loss, backward to dA1), ONE dW launch
+// (both routed W0 problems + W1 / Wfc of both towers) and ONE optimizer launch over the
+// flat parameters (split-K reduce, Adam / Adagrad / SGD / momentum, bf16 shadows, loss and
+// reciprocal-rank hand-off): 7 launches per step.
+class PairPlan {
+ public:
+  PairPlan(const TowerPlan& s, const TowerPlan& c, py::dict d) : d_(d), dev_(s.device()) {
+    B_ = geti("B");
+    K_ = geti("K");
+    H0_ = s.H();
+    H1_ = geti("H1");
+    E_ = geti("E");
+    TORCH_CHECK(c.R() == B_ * (1 + K_) && s.R() == B_, "PairPlan: tower roots must be B and B (1 + K)");
+    TORCH_CHECK(c.H() == H0_ && c.D() == s.D(), "PairPlan: towers must have the same layer-0 shape");
+    TORCH_CHECK(B_ % 32 == 0 && K_ >= 1 && K_ <= 15, "PairPlan: B % 32 == 0 and 1 <= K <= 15");
+    TORCH_CHECK(H1_ % 64 == 0 && E_ % 32 == 0, "PairPlan: padded dims (H1 % 64, E % 32)");
+    TORCH_CHECK(eh_tr_pair_head_lds(static_cast<int>(K_), static_cast<int>(2 * H0_), static_cast<int>(H1_),
+                                    static_cast<int>(E_)) <= 160 * 1024 - 256,
+                "PairPlan: the pair head does not fit in LDS (K / widths too large)");
+    fpx_ = s.feat_fp32();
+    bm_s_ = s.bm();
+    bm_c_ = c.bm();
+    // samplers: roots drawn in the kernels
+    ss_ = s.sample_args();
+    sc_ = c.sample_args();
+    ss_.tr.root_in = nullptr;
+    ss_.tr.root_mode = 0;
+    ss_.tr.stream_off = 0;
+    sc_.tr.root_in = nullptr;
+    sc_.tr.root_mode = 1;
+    sc_.tr.pair_B = static_cast<int32_t>(B_);
+    sc_.tr.pair_mask = static_cast<uint32_t>(geti("pos_mask"));
+    sc_.tr.stream_off = 8;
+    // forwards: the source tower's block 0 advances the Adam step and the RNG counter
+    step_ = T("step");
+    need(step_, torch::kInt64, 1, "step");
+    fs_ = s.fwd_args();
+    fc_ = c.fwd_args();
+    fs_.roots_in = ss_.roots;  // roots_cur: the roots the samplers drew
+    fc_.roots_in = sc_.roots;
+    fs_.step = step_.data_ptr<int64_t>();
+    fc_.step = nullptr;
+    rng_dummy_ = torch::zeros({2}, torch::TensorOptions().dtype(torch::kInt64).device(dev_));
+    fc_.rng = rng_dummy_.data_ptr<int64_t>();
+    // head
+    nblk_ = B_ / 16;
+    TrPairHeadArgs& h = head_;
+    h.B = static_cast<int32_t>(B_);
+    h.K = static_cast<int32_t>(K_);
+    h.H0x2 = static_cast<int32_t>(2 * H0_);
+    h.H1 = static_cast<int32_t>(H1_);
+    h.E = static_cast<int32_t>(E_);
+    h.inv_n = 1.f / static_cast<float>(B_ * (1 + K_));
+    h.head_part = owned(nblk_ * 4);
+    tower(h.s, s, "s");
+    tower(h.c, c, "c");
+    // dW: routed W0 of both towers + W1 / Wfc of both towers
+    L_.route[0] = s.prob();
+    L_.route[1] = c.prob();
+    L_.nroute = 2;
+    L_.plain.n = 0;
+    const char* tn[2] = {"s", "c"};
+    const int64_t R[2] = {B_, B_ * (1 + K_)};
+    const TrPairTower* tw[2] = {&h.s, &h.c};
+    for (int t = 0; t < 2; ++t) {
+      plain_[2 * t] = add_plain(H1_, 2 * H0_, R[t], tw[t]->g_kt, tw[t]->A1_kt);   // dW1 = g^T A1
+      plain_[2 * t + 1] = add_plain(E_, H1_, R[t], tw[t]->de_kt, tw[t]->h_kt);   // dWfc = de^T h1
+    }
+    (void)tn;
+    // optimizer over the flat buffer: per tower W0, W1, Wfc, bfc
+    TrOptArgs& o = opt_;
+    torch::Tensor flat = T("flat");
+    need(flat, torch::kFloat32, -1, "flat");
+    o.n = flat.numel();
+    o.p = flat.data_ptr<float>();
+    o.g = ptr<float>("grad", torch::kFloat32, o.n);
+    o.m = ptr<float>("m", torch::kFloat32, o.n);
+    o.v = ptr<float>("v", torch::kFloat32, o.n);
+    std::vector<int64_t> off = d_["offsets"].cast<std::vector<int64_t>>();
+    TORCH_CHECK(off.size() == 9 && off.back() == o.n, "PairPlan: offsets = 8 segments + end");
+    int blk = 0, seg = 0;
+    const TowerPlan* tp[2] = {&s, &c};
+    for (int t = 0; t < 2; ++t) {
+      const TrPairTower& T_ = *tw[t];
+      const TrDwProb& W0 = tp[t]->prob();
+      add_seg(seg++, blk, off[4 * t], W0.part, W0.S, W0.P, W0.Q, const_cast<uint16_t*>(tp[t]->fwd_args().W), nullptr);
+      const TrDwProb& W1 = L_.plain.p[plain_[2 * t]];
+      add_seg(seg++, blk, off[4 * t + 1], W1.part, W1.S, W1.P, W1.Q, const_cast<uint16_t*>(T_.W1),
+              const_cast<uint16_t*>(T_.W1T));
+      const TrDwProb& Wf = L_.plain.p[plain_[2 * t + 1]];
+      add_seg(seg++, blk, off[4 * t + 2], Wf.part, Wf.S, Wf.P, Wf.Q, const_cast<uint16_t*>(T_.Wfc),
+              const_cast<uint16_t*>(T_.WfcT));
+      add_seg(seg++, blk, off[4 * t + 3], T_.dbfc_part, static_cast<int32_t>(nblk_), 1, 0, nullptr, nullptr);
+      TORCH_CHECK(off[4 * t + 4] - off[4 * t + 3] == E_, "PairPlan: bias segment must be E long");
+    }
+    o.nseg = seg;
+    o.nblk = blk;
+    o.step = step_.data_ptr<int64_t>();
+    o.lr = static_cast<float>(getf("lr"));
+    o.b1 = static_cast<float>(getf("beta1"));
+    o.b2 = static_cast<float>(getf("beta2"));
+    o.eps = static_cast<float>(getf("eps"));
+    o.wd = static_cast<float>(getf("weight_decay"));
+    o.grad_scale = 1.f;
+    o.kind = static_cast<int32_t>(geti("opt_kind"));
+    o.head_part = h.head_part;
+    o.nhead = static_cast<int32_t>(nblk_);
+    o.loss_acc = ptr<float>("loss_acc", torch::kFloat32, 1);
+    o.loss_out = ptr<float>("loss_out", torch::kFloat32, 1);
+    o.stat_f = ptr<float>("mrr_sum", torch::kFloat32, 1);
+    o.counts = nullptr;
+    o.nsample = 0;
+  }
+
+  void sample() {
+    const c10::DeviceGuard g(dev_);
+    ok(eh_tr_sample(&ss_, stream()), "pair sample (source)");
+    ok(eh_tr_sample(&sc_, stream()), "pair sample (context)");
+  }
+  void fwd() {
+    const c10::DeviceGuard g(dev_);
+    ok(eh_tr_fwd(&fs_, 0, fpx_, bm_s_, stream()), "pair fwd (source)");
+    ok(eh_tr_fwd(&fc_, 0, fpx_, bm_c_, stream()), "pair fwd (context)");
+  }
+  void head() {
+    const c10::DeviceGuard g(dev_);
+    ok(eh_tr_pair_head(&head_, stream()), "pair head");
+  }
+  void dw() {
+    const c10::DeviceGuard g(dev_);
+    TrDwLaunch L = L_;
+    ok(eh_tr_dw(&L, stream()), "pair dw");
+  }
+  // 0: split-K reduce into the flat gradient; 1: optimizer from it (scaled); 2: both; 3: shadows
+  void opt(int mode, double grad_scale) {
+    const c10::DeviceGuard g(dev_);
+    TrOptArgs a = opt_;
+    a.grad_scale = static_cast<float>(grad_scale);
+    ok(eh_tr_opt(&a, mode, stream()), "pair opt");
+  }
+  void set_lr(double lr) { opt_.lr = static_cast<float>(lr); }
+  void set_grad(torch::Tensor g) {
+    need(g, torch::kFloat32, opt_.n, "grad");
+    grad_keep_ = g;
+    opt_.g = g.data_ptr<float>();
+  }
+
+ private:
+  py::dict d_;
+  c10::Device dev_;
+  int64_t B_, K_, H0_, H1_, E_, nblk_;
+  int fpx_ = 0, bm_s_ = 32, bm_c_ = 32;
+  TrSampleArgs ss_{}, sc_{};
+  TrFwdArgs fs_{}, fc_{};
+  TrPairHeadArgs head_{};
+  TrDwLaunch L_{};
+  int plain_[4] = {0, 0, 0, 0};
+  TrOptArgs opt_{};
+  torch::Tensor step_, rng_dummy_, grad_keep_;
+  std::vector<torch::Tensor> owned_;
+
+  void tower(TrPairTower& t, const TowerPlan& tp, const std::string& x) {
+    const int64_t R = tp.R();
+    t.A1 = tp.fwd_args().a_next;
+    t.W1 = bf(("W1_sh_" + x).c_str(), H1_ * 2 * H0_);
+    t.W1T = bf(("W1_shT_" + x).c_str(), H1_ * 2 * H0_);
+    t.Wfc = bf(("Wfc_sh_" + x).c_str(), E_ * H1_);
+    t.WfcT = bf(("Wfc_shT_" + x).c_str(), E_ * H1_);
+    t.bfc = ptr<float>(("bfc_" + x).c_str(), torch::kFloat32, E_);
+    t.A1_kt = owned_bf16(R * 2 * H0_);
+    t.h_kt = owned_bf16(R * H1_);
+    t.de_kt = owned_bf16(R * E_);
+    t.g_kt = owned_bf16(R * H1_);
+    t.dA1 = const_cast<float*>(tp.prob().dA);
+    t.dbfc_part = owned(nblk_ * E_);
+  }
+
+  // stored-G dW problem: ~512 workgroups of 64 x 64 tiles, >= 4 k-blocks per split
+  int add_plain(int64_t P, int64_t Q, int64_t M, const uint16_t* G, const uint16_t* X) {
+    TORCH_CHECK(M % 32 == 0 && P % 32 == 0 && Q % 32 == 0, "PairPlan: dW problem shapes");
+    TrDwProb p{};
+    p.P = static_cast<int32_t>(P);
+    p.Q = static_cast<int32_t>(Q);
+    p.MB = static_cast<int32_t>(M / 32);
+    const int64_t tiles = ((P + 63) / 64) * ((Q + 63) / 64);
+    const int64_t target = has("dw_target_wg") ? geti("dw_target_wg") : 512;
+    int64_t kps = (p.MB * tiles + target - 1) / target;
+    kps = std::max<int64_t>(kps, 4);
+    kps = std::min<int64_t>(kps, p.MB);
+    p.kps = static_cast<int32_t>(kps);
+    p.S = static_cast<int32_t>((p.MB + kps - 1) / kps);
+    p.part = owned(static_cast<int64_t>(p.S) * P * Q);
+    p.G = G;
+    p.X = X;
+    TORCH_CHECK(L_.plain.n < kTrMaxProbs, "PairPlan: too many dW problems");
+    L_.plain.p[L_.plain.n] = p;
+    return L_.plain.n++;
+  }
+
+  void add_seg(int seg, int& blk, int64_t off, const float* part, int32_t S, int64_t rows, int64_t cols, uint16_t* sh,
+               uint16_t* shT) {
+    TORCH_CHECK(seg < kTrMaxSegs, "PairPlan: too many optimizer segments");
+    TrSeg& g = opt_.seg[seg];
+    g.off = off;
+    g.n = cols > 0 ? rows * cols : E_;
+    g.part = part;
+    g.S = S;
+    g.rows = static_cast<int32_t>(rows);
+    g.cols = static_cast<int32_t>(cols);
+    g.blk0 = blk;
+    g.sh = sh;
+    g.shT = shT;
+    if (cols > 0) {
+      TORCH_CHECK(rows % 8 == 0 && cols % 32 == 0, "PairPlan: weight segments need rows % 8, cols % 32");
+      blk += static_cast<int>((rows / 8) * (cols / 32));
+    } else {
+      blk += static_cast<int>((g.n + 255) / 256);
+    }
+  }
+
+  bool has(const char* k) const { return d_.contains(k) && !d_[k].is_none(); }
+  int64_t geti(const char* k) const {
+    TORCH_CHECK(d_.contains(k), "PairPlan: missing '", k, "'");
+    return d_[k].cast<int64_t>();
+  }
+  double getf(const char* k) const { return d_[k].cast<double>(); }
+  torch::Tensor T(const char* k) const {
+    TORCH_CHECK(has(k), "PairPlan: missing tensor '", k, "'");
+    return d_[k].cast<torch::Tensor>();
+  }
+  void need(const torch::Tensor& t, c10::ScalarType st, int64_t numel, const std::string& name) const {
+    TORCH_CHECK(t.is_cuda() && t.device() == dev_, name, " must be on the plan's GPU");
+    TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+    TORCH_CHECK(t.scalar_type() == st, name, " has the wrong dtype");
+    if (numel >= 0) TORCH_CHECK(t.numel() == numel, name, " has ", t.numel(), " elements, expected ", numel);
+  }
+  template <typename P>
+  P* ptr(const char* k, c10::ScalarType st, int64_t numel) {
+    torch::Tensor t = T(k);
+    need(t, st, numel, k);
+    return reinterpret_cast<P*>(t.data_ptr());
+  }
+  uint16_t* bf(const char* k, int64_t numel) { return ptr<uint16_t>(k, torch::kBFloat16, numel); }
+  float* owned(int64_t n) {
+    torch::Tensor t = torch::zeros({n}, torch::TensorOptions().dtype(torch::kFloat32).device(dev_));
+    owned_.push_back(t);
+    return t.data_ptr<float>();
+  }
+  uint16_t* owned_bf16(int64_t n) {
+    torch::Tensor t = torch::zeros({n}, torch::TensorOptions().dtype(torch::kBFloat16).device(dev_));
+    owned_.push_back(t);
+    return reinterpret_cast<uint16_t*>(t.data_ptr());
+  }
+};
+
 }  // namespace
 
 void register_tree_ops(py::module& m) {
@@ -886,4 +1159,13 @@ void register_tree_ops(py::module& m) {
       .def("sample", &TowerPlan::sample)
       .def("fwd", &TowerPlan::fwd)
       .def("bwd", &TowerPlan::bwd);
+  py::class_<PairPlan>(m, "PairPlan")
+      .def(py::init<const TowerPlan&, const TowerPlan&, py::dict>(), py::keep_alive<1, 2>(), py::keep_alive<1, 3>())
+      .def("sample", &PairPlan::sample)
+      .def("fwd", &PairPlan::fwd)
+      .def("head", &PairPlan::head)
+      .def("dw", &PairPlan::dw)
+      .def("opt", &PairPlan::opt, py::arg("mode"), py::arg("grad_scale") = 1.0)
+      .def("set_lr", &PairPlan::set_lr)
+      .def("set_grad", &PairPlan::set_grad);
 }

@@ -19,6 +19,7 @@
 //                     routed from dA1 through the tree inside the kernel (never stored)
 //   tr_opt   (mode 2) split-K reduce + Adam/Adagrad/SGD/momentum + bf16 weight shadows
 // (3 hops add one tr_fwd mode 2 and one tr_bwd; 1 hop uses tr_fwd mode 1).
+#include <algorithm>
 #include <cstdlib>
 
 #include "hip/tile.h"
@@ -26,7 +27,7 @@
 
 namespace euler_hip {
 
-constexpr uint64_t kTrStreamRoot = 1, kTrStreamHop = 16;
+constexpr uint64_t kTrStreamRoot = 1, kTrStreamPos = 2, kTrStreamNeg = 3, kTrStreamHop = 16;
 constexpr int kTrBN = 256;  // output columns per GEMM chunk (4 waves x 64)
 
 __device__ __forceinline__ uint4_t tr_rand(const int64_t* rng, uint64_t stream, uint64_t idx) {
@@ -34,8 +35,9 @@ __device__ __forceinline__ uint4_t tr_rand(const int64_t* rng, uint64_t stream, 
 }
 
 // Walker alias draw of root t (reference sample_node: weighted, per node type)
-__device__ __forceinline__ int32_t tr_root(const TrGraph& g, const int64_t* rng, int64_t t) {
-  const uint4_t r = tr_rand(rng, kTrStreamRoot, static_cast<uint64_t>(t));
+__device__ __forceinline__ int32_t tr_root(const TrGraph& g, const int64_t* rng, int64_t t,
+                                           uint64_t stream = kTrStreamRoot) {
+  const uint4_t r = tr_rand(rng, stream, static_cast<uint64_t>(t));
   const uint64_t x = (static_cast<uint64_t>(r[0]) << 32) | r[1];
   int64_t k = static_cast<int64_t>(__umul64hi(x, static_cast<uint64_t>(g.pop)));
   if (k >= g.pop) k = g.pop - 1;
@@ -89,12 +91,26 @@ __device__ int32_t tr_neighbor(const TrGraph& g, int32_t row, uint32_t mask, uin
 
 // slot j of the group of `parent` (whose own slot index is parent_slot) at hop `hop`
 __device__ __forceinline__ int32_t tr_hop(const TrGraph& g, const int64_t* rng, int32_t parent, int j, int F,
-                                          uint32_t mask, int hop, int64_t parent_slot) {
+                                          uint32_t mask, int hop, int64_t parent_slot, int stream_off = 0) {
   if (j < F)
     return parent >= 0 ? tr_neighbor(g, parent, mask,
-                                     tr_rand(rng, kTrStreamHop + hop, static_cast<uint64_t>(parent_slot * F + j)))
+                                     tr_rand(rng, kTrStreamHop + hop + stream_off,
+                                             static_cast<uint64_t>(parent_slot * F + j)))
                        : -1;
   return j == F ? parent : -1;
+}
+
+// root t of a tree (see TrTree::root_mode): given, an alias draw, or a pair model's context
+// root (the source root's positive neighbour, or a negative draw)
+__device__ __forceinline__ int32_t tr_tree_root(const TrGraph& g, const TrTree& tr, int64_t t) {
+  if (tr.root_in) return tr.root_in[t];
+  if (tr.root_mode == 0) return tr_root(g, tr.rng, t);
+  if (t < tr.pair_B) {
+    const int32_t src = tr_root(g, tr.rng, t);
+    return src >= 0 ? tr_neighbor(g, src, tr.pair_mask, tr_rand(tr.rng, kTrStreamPos, static_cast<uint64_t>(t)))
+                    : -1;
+  }
+  return tr_root(g, tr.rng, t, kTrStreamNeg);
 }
 
 // node of slot s at level lv (0..2); *root = index of its root, *self_chain = the slot is
@@ -110,17 +126,17 @@ __device__ int32_t tr_slot_node(const TrGraph& g, const TrTree& tr, int64_t s, i
     i1 = s >> tr.logP2;
     i0 = i1 >> tr.logP1;
   }
-  int32_t node = tr.root_in ? tr.root_in[i0] : tr_root(g, tr.rng, i0);
+  int32_t node = tr_tree_root(g, tr, i0);
   bool sc = true;
   if (lv >= 1) {
     const int j = static_cast<int>(i1 & ((int64_t(1) << tr.logP1) - 1));
     sc = j == tr.F1;
-    node = tr_hop(g, tr.rng, node, j, tr.F1, tr.m1, 1, i0);
+    node = tr_hop(g, tr.rng, node, j, tr.F1, tr.m1, 1, i0, tr.stream_off);
   }
   if (lv >= 2) {
     const int j = static_cast<int>(i2 & ((int64_t(1) << tr.logP2) - 1));
     sc = sc && j == tr.F2;
-    node = tr_hop(g, tr.rng, node, j, tr.F2, tr.m2, 2, i1);
+    node = tr_hop(g, tr.rng, node, j, tr.F2, tr.m2, 2, i1, tr.stream_off);
   }
   *root = i0;
   *self_chain = sc;
@@ -267,7 +283,8 @@ __device__ __forceinline__ void tr_sample_block(const TrSampleArgs& a, int blk, 
     const int32_t node = node_s[r];
     a.leaf[s * a.FL + k] =
         node >= 0 ? tr_neighbor(a.g, node, a.mL,
-                                tr_rand(a.tr.rng, kTrStreamHop + a.hopL, static_cast<uint64_t>(s * a.FL + k)))
+                                tr_rand(a.tr.rng, kTrStreamHop + a.hopL + a.tr.stream_off,
+                                        static_cast<uint64_t>(s * a.FL + k)))
                   : -1;
   }
 }
@@ -1264,6 +1281,198 @@ __global__ __launch_bounds__(HNW * 64) void tr_head_kernel(TrHeadArgs a) {
 }
 
 // ----------------------------------------------------------------------------
+// tr_pair_head: the head of the unsupervised GraphSAGE step (see TrPairHeadArgs; reference
+// examples/graphsage/graphsage.py:70-98, tf_euler/python/mp_utils/base.py:49-91).  Block b:
+// sources 16b..16b+15 and their context rows, 2 + K row tiles of 16 in LDS (tile 0: the
+// sources, tile 1: their positives, tiles 2..: their negatives, source-major), 16 waves;
+// every phase deals its (tile, 16-column slab) jobs round-robin over the waves, each one
+// tr_gemm (A rows from LDS, the tile's tower's B fragments from L2):
+//   P1 h1 = relu(A1 W1^T)                   -> H   (+ A1_kt, h_kt for the dW GEMMs)
+//   P2 e  = h1 Wfc^T + bfc                  -> Ef  (fp32, over the dead A1 tile)
+//   P3 wave i = source i: logits <e_i, e_ctx>, softplus CE, reciprocal rank, de (fp32)
+//                                           -> D (bf16, + de_kt), bias / loss partials
+//   P4 g  = (de Wfc) * relu'(h1)            -> G   (over the dead Ef) (+ g_kt)
+//   P5 dA1 = g W1                           (fp32 rows: the routed layer-0 dW reads them)
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ const TrPairTower& pr_tower(const TrPairHeadArgs& a, int t) { return t == 0 ? a.s : a.c; }
+
+// first row of tile t in its tower
+__device__ __forceinline__ int64_t pr_row0(const TrPairHeadArgs& a, int b, int t) {
+  if (t <= 1) return static_cast<int64_t>(b) * 16;
+  return static_cast<int64_t>(a.B) + static_cast<int64_t>(b) * 16 * a.K + 16 * (t - 2);
+}
+
+__global__ __launch_bounds__(HNW * 64) void tr_pair_head_kernel(TrPairHeadArgs a) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  const int b = blockIdx.x;
+  const int NTILE = 2 + a.K, rows = 16 * NTILE;
+  const int H0x2 = a.H0x2, H1 = a.H1, E = a.E;
+  const int lda = tr_head_ld(H0x2), ldh = tr_head_ld(H1), lde = tr_head_ld(E);
+  const int abytes = rows * lda * 2, ebytes = rows * E * 4, gbytes = rows * ldh * 2;
+  const int region = ((abytes > ebytes ? abytes : ebytes) > gbytes ? (abytes > ebytes ? abytes : ebytes) : gbytes);
+  bf16_t* Aa = lds;                                                   // P1 input
+  float* Ef = reinterpret_cast<float*>(lds);                          // P2 -> P3 (over Aa)
+  bf16_t* Gg = lds;                                                   // P4 -> P5 (over Ef)
+  bf16_t* Hh = lds + region / 2;                                      // h1
+  bf16_t* Dd = Hh + rows * ldh;                                       // de
+  float* ps = reinterpret_cast<float*>(Dd + rows * lde);              // [2][16][E] bias partials
+  __shared__ float red_s[HNW][2];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int lr = lane & 15, lg = lane >> 4;
+  constexpr int NT = HNW * 64;
+
+  // A1 rows of every tile -> LDS (+ the kt copies for dW1)
+  const int cpa = H0x2 >> 3;
+  for (int it = threadIdx.x; it < rows * cpa; it += NT) {
+    const int r = it / cpa, c = it - r * cpa;
+    const int t = r >> 4;
+    const TrPairTower& tw = pr_tower(a, t);
+    *reinterpret_cast<uint4_t*>(Aa + sw_off(r, c * 8, lda)) =
+        *reinterpret_cast<const uint4_t*>(tw.A1 + (pr_row0(a, b, t) + (r & 15)) * H0x2 + c * 8);
+  }
+  __syncthreads();
+  for (int t = 0; t < NTILE; ++t) tr_lds_to_kt(Aa + 16 * t * lda, lda, H0x2, pr_row0(a, b, t), pr_tower(a, t).A1_kt);
+
+  uint4_t pre[TR_KC];
+  // P1: h1 = relu(A1 W1^T)
+  {
+    const int nc = H1 >> 4, nj = NTILE * nc;
+    if (wave < nj) tr_prefetch(pr_tower(a, wave / nc).W1, (wave % nc) * 16, H1, H0x2, lane, pre);
+    for (int j = wave; j < nj; j += HNW) {
+      const int t = j / nc, cs = (j - t * nc) * 16;
+      float4_t acc[HFM][1];
+      tl_zero(acc);
+      tr_gemm(Aa + 16 * t * lda, lda, pr_tower(a, t).W1, cs, H0x2, acc, lane, pre);
+      if (j + HNW < nj) tr_prefetch(pr_tower(a, (j + HNW) / nc).W1, ((j + HNW) % nc) * 16, H1, H0x2, lane, pre);
+      float v[4];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        v[jj] = fmaxf(acc[0][0][jj], 0.f);
+        Hh[sw_off(16 * t + lg * 4 + jj, cs + lr, ldh)] = f2bf(v[jj]);
+      }
+      kt_store4(pr_tower(a, t).h_kt, pr_row0(a, b, t) + lg * 4, cs + lr, H1, bf2f(f2bf(v[0])), bf2f(f2bf(v[1])),
+                bf2f(f2bf(v[2])), bf2f(f2bf(v[3])));
+    }
+  }
+  __syncthreads();  // A1 dead from here (Ef takes its place)
+  // P2: e = h1 Wfc^T + bfc (fp32)
+  {
+    const int nc = E >> 4, nj = NTILE * nc;
+    if (wave < nj) tr_prefetch(pr_tower(a, wave / nc).Wfc, (wave % nc) * 16, E, H1, lane, pre);
+    for (int j = wave; j < nj; j += HNW) {
+      const int t = j / nc, cs = (j - t * nc) * 16;
+      float4_t acc[HFM][1];
+      tl_zero(acc);
+      tr_gemm(Hh + 16 * t * ldh, ldh, pr_tower(a, t).Wfc, cs, H1, acc, lane, pre);
+      if (j + HNW < nj) tr_prefetch(pr_tower(a, (j + HNW) / nc).Wfc, ((j + HNW) % nc) * 16, E, H1, lane, pre);
+      const float bias = pr_tower(a, t).bfc[cs + lr];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) Ef[(16 * t + lg * 4 + jj) * E + cs + lr] = acc[0][0][jj] + bias;
+    }
+  }
+  __syncthreads();
+  // P3: wave i = source i of the block
+  {
+    // logits / gradients of the 1 + K <= 16 pairs in registers (fully unrolled: constant
+    // indices, no scratch)
+    const int i = wave;
+    const int K = a.K;
+    float l[16], g[16];
+    const float* es = Ef + i * E;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      l[k] = 0.f;
+      if (k > K) continue;
+      const int row = k == 0 ? 16 + i : 32 + i * K + (k - 1);
+      float d = 0.f;
+      for (int c = lane; c < E; c += 64) d += es[c] * Ef[row * E + c];
+      l[k] = wave_sum(d);
+    }
+    float loss = 0.f, gsum = 0.f;
+    int beat = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      g[k] = 0.f;
+      if (k > K) continue;
+      const float x = l[k];
+      loss += fmaxf(x, 0.f) + log1pf(__expf(-fabsf(x))) - (k == 0 ? x : 0.f);
+      g[k] = (1.f / (1.f + __expf(-x)) - (k == 0 ? 1.f : 0.f)) * a.inv_n;
+      gsum += g[k];
+      if (k > 0 && x >= l[0]) ++beat;
+    }
+    if (lane == 0) {
+      red_s[i][0] = loss * a.inv_n;
+      red_s[i][1] = 1.f / static_cast<float>(1 + beat);
+    }
+    for (int c = lane; c < E; c += 64) {
+      const float ev = es[c];
+      float de = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        if (k > K) continue;
+        const int row = k == 0 ? 16 + i : 32 + i * K + (k - 1);
+        de += g[k] * Ef[row * E + c];
+        Dd[sw_off(row, c, lde)] = f2bf(g[k] * ev);
+      }
+      Dd[sw_off(i, c, lde)] = f2bf(de);
+      ps[i * E + c] = de;                 // source-tower bias gradient share
+      ps[(16 + i) * E + c] = gsum * ev;   // context-tower share: sum_k g_k e_i
+    }
+  }
+  __syncthreads();  // Ef dead from here (G takes its place)
+  for (int t = 0; t < NTILE; ++t) tr_lds_to_kt(Dd + 16 * t * lde, lde, E, pr_row0(a, b, t), pr_tower(a, t).de_kt);
+  for (int c = threadIdx.x; c < 2 * E; c += NT) {  // per-block bias partials, fixed order
+    const int tw = c >= E, col = c - tw * E;
+    float v = 0.f;
+    for (int w = 0; w < 16; ++w) v += ps[(tw * 16 + w) * E + col];
+    (tw ? a.c : a.s).dbfc_part[static_cast<int64_t>(b) * E + col] = v;
+  }
+  if (threadIdx.x < 4) {
+    float v = 0.f;
+    if (threadIdx.x < 2)
+      for (int w = 0; w < 16; ++w) v += red_s[w][threadIdx.x];
+    a.head_part[b * 4 + threadIdx.x] = v;
+  }
+  // P4: g = (de Wfc) * relu'(h1)
+  {
+    const int nc = H1 >> 4, nj = NTILE * nc;
+    if (wave < nj) tr_prefetch(pr_tower(a, wave / nc).WfcT, (wave % nc) * 16, H1, E, lane, pre);
+    for (int j = wave; j < nj; j += HNW) {
+      const int t = j / nc, cs = (j - t * nc) * 16;
+      float4_t acc[HFM][1];
+      tl_zero(acc);
+      tr_gemm(Dd + 16 * t * lde, lde, pr_tower(a, t).WfcT, cs, E, acc, lane, pre);
+      if (j + HNW < nj) tr_prefetch(pr_tower(a, (j + HNW) / nc).WfcT, ((j + HNW) % nc) * 16, H1, E, lane, pre);
+      float v[4];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int row = 16 * t + lg * 4 + jj;
+        v[jj] = bf2f(f2bf(bf_pos(Hh[sw_off(row, cs + lr, ldh)]) ? acc[0][0][jj] : 0.f));
+        Gg[sw_off(row, cs + lr, ldh)] = f2bf(v[jj]);
+      }
+      kt_store4(pr_tower(a, t).g_kt, pr_row0(a, b, t) + lg * 4, cs + lr, H1, v[0], v[1], v[2], v[3]);
+    }
+  }
+  __syncthreads();
+  // P5: dA1 = g W1 (fp32 rows)
+  {
+    const int nc = H0x2 >> 4, nj = NTILE * nc;
+    if (wave < nj) tr_prefetch(pr_tower(a, wave / nc).W1T, (wave % nc) * 16, H0x2, H1, lane, pre);
+    for (int j = wave; j < nj; j += HNW) {
+      const int t = j / nc, cs = (j - t * nc) * 16;
+      float4_t acc[HFM][1];
+      tl_zero(acc);
+      tr_gemm(Gg + 16 * t * ldh, ldh, pr_tower(a, t).W1T, cs, H1, acc, lane, pre);
+      if (j + HNW < nj) tr_prefetch(pr_tower(a, (j + HNW) / nc).W1T, ((j + HNW) % nc) * 16, H0x2, H1, lane, pre);
+      float* out = pr_tower(a, t).dA1;
+      const int64_t r0 = pr_row0(a, b, t);
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) out[(r0 + lg * 4 + jj) * H0x2 + cs + lr] = acc[0][0][jj];
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------
 // tr_dw: grouped split-K weight gradients, part[s][p][q] = sum_{m in split s} G[m][p] X[m][q];
 // 64x64 tiles, 4 waves of 32x32
 // ----------------------------------------------------------------------------
@@ -1639,7 +1848,9 @@ __device__ __forceinline__ void tr_opt_tile(const TrOptArgs& a, int b, float (*t
       for (int c = 0; c < 4; ++c) v[c] = wave_sum(v[c]);
       if (tid == 0) {
         a.loss_acc[0] = v[0];
-        if (a.counts) {
+        if (a.stat_f) {
+          a.stat_f[0] += v[1];
+        } else if (a.counts) {
           a.counts[0] += static_cast<uint32_t>(v[1]);
           a.counts[1] += static_cast<uint32_t>(v[2]);
           a.counts[2] += static_cast<uint32_t>(v[3]);
@@ -1931,6 +2142,31 @@ hipError_t eh_tr_bwd(const TrBwdArgs* a, hipStream_t s) {
   EULER_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(tr_bwd_kernel),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
   hipLaunchKernelGGL(tr_bwd_kernel, dim3(static_cast<uint32_t>(a->M / 32)), dim3(256), lds, s, *a);
+  return hipGetLastError();
+}
+
+size_t eh_tr_pair_head_lds(int K, int H0x2, int H1, int E) {
+  const size_t rows = 16 * static_cast<size_t>(2 + K);
+  const size_t abytes = rows * (H0x2 + 16) * 2, ebytes = rows * E * 4, gbytes = rows * (H1 + 16) * 2;
+  const size_t region = std::max(std::max(abytes, ebytes), gbytes);
+  return region + rows * (H1 + 16) * 2 + rows * (E + 16) * 2 + 2 * 16 * static_cast<size_t>(E) * 4;
+}
+
+hipError_t eh_tr_pair_head(const TrPairHeadArgs* a, hipStream_t s) {
+  if (a->B <= 0 || a->B % 16 != 0 || a->K < 1 || a->K > 15 || a->H0x2 % 32 != 0 || a->H1 % 32 != 0 ||
+      a->E % 32 != 0 || a->E > 1024)
+    return hipErrorInvalidValue;
+  const TrPairTower* tw[2] = {&a->s, &a->c};
+  for (const TrPairTower* t : tw)
+    if (!t->A1 || !t->W1 || !t->W1T || !t->Wfc || !t->WfcT || !t->bfc || !t->A1_kt || !t->h_kt || !t->de_kt ||
+        !t->g_kt || !t->dA1 || !t->dbfc_part)
+      return hipErrorInvalidValue;
+  if (!a->head_part) return hipErrorInvalidValue;
+  const size_t lds = eh_tr_pair_head_lds(a->K, a->H0x2, a->H1, a->E);
+  if (lds > 160 * 1024 - 256) return hipErrorInvalidValue;
+  EULER_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(tr_pair_head_kernel),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+  hipLaunchKernelGGL(tr_pair_head_kernel, dim3(static_cast<uint32_t>(a->B / 16)), dim3(HNW * 64), lds, s, *a);
   return hipGetLastError();
 }
 

@@ -39,6 +39,14 @@ struct TrTree {
   int32_t F1, F2;      // fanouts of hops 1 and 2
   int32_t logP1, logP2;
   uint32_t m1, m2;     // edge-type masks of hops 1 and 2
+  // root_in == nullptr: root_mode 0 = alias draw t (stream kTrStreamRoot); 1 = the context
+  // tower of a pair model: t < pair_B -> one out-neighbour (pair_mask, stream kTrStreamPos)
+  // of the source root t (alias draw t, recomputed), -1 when it has none; t >= pair_B -> an
+  // alias draw of the negative stream (kTrStreamNeg)
+  int32_t root_mode, pair_B;
+  uint32_t pair_mask;
+  int32_t stream_off;  // added to the hop / leaf Philox streams (the two towers of a pair
+                       // model draw independent neighbourhoods)
 };
 
 // mini-batch sampler: the node of every target row of layer 0 (level lv of the tree,
@@ -126,6 +134,28 @@ struct TrHeadArgs {
   int32_t nsample;       // CUs the head leaves idle (0: none)
 };
 
+// pair head (unsupervised GraphSAGE, models/sage_tower.py): for kTrHeadRows sources per
+// block and their 1 + K context rows (positive, K negatives) the last conv + fc of both
+// towers, the pair logits + sigmoid CE + reciprocal rank, and the backward to dA1 of both
+// towers; weight-gradient operands in kt layout for tr_dw, per-block bias / loss partials
+// for tr_opt.  Tower s = source (R = B rows), c = context (R = B (1 + K): B positives, then
+// the B x K negatives source-major).
+struct TrPairTower {
+  const uint16_t* A1;        // [R][2H0] bf16 rows [self | mean] (layer 0 of the tower)
+  const uint16_t *W1, *W1T;  // fm [H1][2H0] and its transpose
+  const uint16_t *Wfc, *WfcT;  // fm [E][H1] and its transpose
+  const float* bfc;          // [E] fp32 master
+  uint16_t *A1_kt, *h_kt, *de_kt, *g_kt;  // kt [R][2H0], [R][H1], [R][E], [R][H1]
+  float* dA1;                // [R][2H0] fp32
+  float* dbfc_part;          // [nblk][E]
+};
+struct TrPairHeadArgs {
+  TrPairTower s, c;
+  int32_t B, K, H0x2, H1, E;
+  float inv_n;       // 1 / (B (1 + K))
+  float* head_part;  // [nblk][4]: loss, reciprocal-rank sum, 0, 0
+};
+
 // inner-layer backward (3-hop): dA_out = route(dA_parent, mask) @ W  (fp32 rows)
 struct TrBwdArgs {
   const float* dA;       // parent gradient [M >> logPg][2Hk]
@@ -184,6 +214,8 @@ struct TrOptArgs {
   float* loss_acc;         // loss of the last forward (written by the reduce)
   uint32_t* counts;        // tp, fp, fn since the last reset (accumulated by the reduce)
   float* loss_out;         // loss of the last optimizer step
+  float* stat_f;           // optional: += the head's second statistic (pair models: reciprocal
+                           // ranks) instead of the tp / fp / fn counts
   TrSampleArgs smp;        // the next step's sampler, run by extra blocks (modes 1/2)
   int32_t nsample;         // sampler blocks (0: none)
   TrFwdArgs gat;           // the next step's layer-0 gather (pipelined step), run by extra blocks:
@@ -224,4 +256,6 @@ hipError_t eh_tr_opt(const euler_hip::TrOptArgs* a, int mode, hipStream_t s);
 size_t eh_tr_fwd_lds(int D, int H, int bm, int FL, int mode);
 size_t eh_tr_fwd2_lds(int D, int FL);
 size_t eh_tr_head_lds(int Hin2, int H, int E, int C, int label_mode);
+size_t eh_tr_pair_head_lds(int K, int H0x2, int H1, int E);
+hipError_t eh_tr_pair_head(const euler_hip::TrPairHeadArgs* a, hipStream_t s);
 }

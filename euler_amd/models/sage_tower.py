@@ -31,6 +31,7 @@ torch (:meth:`_tower_reference` is also the GPU kernels' numerics oracle).
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -38,6 +39,10 @@ import torch.nn.functional as F
 from euler_amd.models._tower_ops import pair_loss, tower_head
 from euler_amd.ops._native import hip
 from euler_amd.parallel.flat import FlatOptimizer, FlatParams
+
+# the fused 7-launch step (PairPlan) on GPUs; EULER_AMD_PAIR_FUSED_STEP=0 keeps the
+# per-op autograd step (tower kernels + GEMM autograd nodes)
+_FUSED = os.environ.get("EULER_AMD_PAIR_FUSED_STEP", "1") == "1"
 
 __all__ = ["UnsupSageTrainer", "unsup_param_names"]
 
@@ -79,6 +84,7 @@ class _Tower:
         self.D = int(features.shape[1])
         i32 = dict(dtype=torch.int32, device=device)
         self.roots_in = torch.full((self.R,), -1, **i32)
+        self.roots_out = torch.full((self.R,), -1, **i32)  # the roots the sampler used
         self.nodes = torch.zeros(self.M, **i32)
         self.leaf = torch.zeros(self.M * self.F2, **i32)
         self.A1 = torch.zeros(self.R * 2 * self.H0, dtype=torch.bfloat16, device=device)
@@ -95,7 +101,9 @@ class _Tower:
                  "include_self": int(include_self), "mask1": int(masks[0]) & 0xFFFFFFFF,
                  "mask2": int(masks[1]) & 0xFFFFFFFF, "indptr": g.indptr, "nbr": g.nbr, "cumw": g.cumw,
                  "num_types": g.num_types, "node_prob": g.node_prob, "node_alias": g.node_alias, "rng": g.rng,
-                 "roots_in": self.roots_in, "nodes": self.nodes, "leaf": self.leaf, "features": features,
+                 "roots_in": self.roots_in, "roots_out": self.roots_out, "nodes": self.nodes, "leaf": self.leaf,
+                 "features": features,
+                 "root_rows": g.root_rows,
                  "W0": W0, "W0_sh": torch.zeros(W0.numel(), dtype=torch.bfloat16, device=device),
                  "A0_kt": torch.empty(self.M * 2 * self.D, dtype=torch.bfloat16, device=device),
                  "mask0": torch.zeros((self.M // 32) * self.H0, **i32), "A1": self.A1, "dA1": self.dA1,
@@ -106,7 +114,8 @@ class _Tower:
 
 class UnsupSageTrainer:
     def __init__(self, graph, batch_size, fanouts, dims, features=None, num_negs=5, pos_edge_types=None,
-                 metapath=None, add_self_loops=False, optimizer="adam", learning_rate=0.01, init=None, init_seed=0):
+                 metapath=None, add_self_loops=False, optimizer="adam", learning_rate=0.01, init=None, init_seed=0,
+                 fused=True):
         self.graph = graph
         self.device = graph.device
         self.B = int(batch_size)
@@ -159,9 +168,60 @@ class UnsupSageTrainer:
         self.mrr_n = 0
         self.step_count = 0
         self._graph_exec = None
+        self._graphs = {}
         self._samples = None
+        self.pair = None
+        if self.device.type == "cuda" and fused and _FUSED:
+            try:
+                self._build_pair(optimizer)
+            except RuntimeError as e:  # shapes the pair head does not take (LDS): per-op step
+                self.pair = None
+                self.fused_error = str(e)
 
     metric_name = "mrr"
+
+    # ------------------------------------------------------------------ fused step (GPU)
+    def _build_pair(self, optimizer):
+        """the 7-launch step (csrc/hip/binding_tree.cpp PairPlan): both towers' layer 0, the
+        pair head kernel, one dW launch, one optimizer launch over the flat buffer"""
+        dev = self.device
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        H0, H1 = self.Hp
+        E = self.Ep
+        names = [f"{t}.{k}" for t in ("gnn", "context_gnn") for k in ("W0", "W1", "Wfc", "bfc")]
+        where = {id(p): i for i, p in enumerate(self.flat.params)}
+        offs = [self.flat.offsets[where[id(self.params[n])]][0] for n in names] + [self.flat.numel]
+        if offs != sorted(offs):
+            raise RuntimeError("flat parameter order is not the pair plan's segment order")
+        d = {"B": self.B, "K": self.K, "H1": H1, "E": E, "pos_mask": int(self.pos_mask) & 0xFFFFFFFF,
+             "flat": self.flat.flat, "grad": self.flat.grad, "m": self.opt.m, "v": self.opt.v,
+             "step": self.opt.step_count, "offsets": offs, "loss_acc": torch.zeros(1, device=dev),
+             "loss_out": self.loss_out, "mrr_sum": self.mrr_sum, "lr": self.opt.lr, "beta1": self.opt.b1,
+             "beta2": self.opt.b2, "eps": self.opt.eps, "weight_decay": self.opt.wd,
+             "opt_kind": {"adam": 0, "adagrad": 1, "sgd": 2, "momentum": 3}[optimizer]}
+        for x, t in (("s", "gnn"), ("c", "context_gnn")):
+            d[f"W1_sh_{x}"] = torch.zeros(H1 * 2 * H0, **bf)
+            d[f"W1_shT_{x}"] = torch.zeros(H1 * 2 * H0, **bf)
+            d[f"Wfc_sh_{x}"] = torch.zeros(E * H1, **bf)
+            d[f"Wfc_shT_{x}"] = torch.zeros(E * H1, **bf)
+            d[f"bfc_{x}"] = self.params[f"{t}.bfc"]
+        self._pair_keep = d
+        self.pair = hip().PairPlan(self.towers["gnn"].plan, self.towers["context_gnn"].plan, d)
+        self.pair.opt(3)  # bf16 shadows of every weight
+
+    def _fused_step(self, grad_sync=None):
+        p = self.pair
+        p.sample()
+        p.fwd()
+        p.head()
+        p.dw()
+        if grad_sync is None:
+            p.opt(2)
+        else:
+            p.opt(0)
+            s = grad_sync(self.flat.grad)
+            p.opt(1, 1.0 if s is None else float(s))
+        return self.loss_out
 
     @classmethod
     def from_model(cls, model, graph, batch_size, optimizer="adam", learning_rate=0.01, **kw):
@@ -201,6 +261,8 @@ class UnsupSageTrainer:
 
     def set_learning_rate(self, lr):
         self.opt.lr = float(lr)
+        if self.pair is not None:
+            self.pair.set_lr(float(lr))
 
     # ------------------------------------------------------------------ parameters
     def _logical_shapes(self):
@@ -275,6 +337,12 @@ class UnsupSageTrainer:
         self.opt.step_count.fill_(int(st["step"]))
         self.graph.rng.copy_(torch.as_tensor(st["rng"]).to(self.graph.rng))
         self.step_count = int(st["step"])
+        self.refresh_shadows()
+
+    def refresh_shadows(self):
+        """rebuild the fused step's bf16 weight shadows (after a load or a broadcast)"""
+        if self.pair is not None:
+            self.pair.opt(3)
 
     # ------------------------------------------------------------------ sampling
     def sample_roots(self):
@@ -381,7 +449,24 @@ class UnsupSageTrainer:
             self._graph_exec.replay()
         self.step_count += int(n)
 
+    def replay_steps(self, n: int):
+        """exactly n steps, greedily from the largest captured graph down"""
+        left = int(n)
+        for k in sorted(self._graphs, reverse=True):
+            while left >= k:
+                self._graphs[k].replay()
+                left -= k
+        self.step_count += int(n)
+
+    def release_graphs(self):
+        for gr in self._graphs.values():
+            gr.reset()
+        self._graphs = {}
+        self._graph_exec = None
+
     def _step(self, grad_sync=None):
+        if self.pair is not None:
+            return self._fused_step(grad_sync)
         loss, mrr = self._forward_loss()
         if self.device.type != "cuda":
             self.opt.zero_grad()  # the GPU towers overwrite every gradient view instead
@@ -396,10 +481,11 @@ class UnsupSageTrainer:
             self.mrr_sum.add_(mrr)
         return self.loss_out
 
-    def capture(self, grad_sync=None, warmup: int = 2):
-        """Record one step (sampling, both towers, loss, backward, [all-reduce,] Adam) into
-        a hipGraph after ``warmup`` eager steps on a side stream; :meth:`step` / :meth:`replay`
-        then replay it."""
+    def capture(self, grad_sync=None, warmup: int = 2, steps: int = 1, extra_sizes=()):
+        """Record ``steps`` complete steps (sampling, both towers, loss, backward,
+        [all-reduce,] optimizer) into one hipGraph after ``warmup`` eager steps on a side
+        stream; graphs of 1 step and of each ``extra_sizes`` entry are kept too
+        (:meth:`replay_steps`; :meth:`step` / :meth:`replay` replay the 1-step graph)."""
         if self.device.type != "cuda":
             return None
         s = torch.cuda.Stream(device=self.device)
@@ -411,11 +497,15 @@ class UnsupSageTrainer:
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         self.flat.rebind_grads()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
-            self._step(grad_sync)
-        self._graph_exec = g
-        return g
+        self._graphs = {}
+        for k in sorted({1, int(steps)} | {int(e) for e in extra_sizes if int(e) > 0}, reverse=True):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                for _ in range(k):
+                    self._step(grad_sync)
+            self._graphs[k] = g
+        self._graph_exec = self._graphs[1]
+        return self._graphs[int(steps)]
 
     @property
     def loss(self):
@@ -474,7 +564,8 @@ class UnsupSageTrainer:
             src, ctx, ns, ls, nc, lc = self._samples
             return (src, ns, ls) if tower == "gnn" else (ctx, nc, lc)
         t = self.towers[tower]
-        return t.roots_in.long(), t.nodes.long(), t.leaf.view(-1, self.fanouts[1]).long()
+        roots = t.roots_out if self.pair is not None else t.roots_in
+        return roots.long(), t.nodes.long(), t.leaf.view(-1, self.fanouts[1]).long()
 
     def reference_loss_and_grads(self):
         """fp32 torch autograd loss and gradients (padded parameter names) on the samples
@@ -490,6 +581,14 @@ class UnsupSageTrainer:
 
     def forward_backward(self):
         """sampling, forward, backward of one step (no optimizer): :meth:`gradients`"""
+        if self.pair is not None:
+            p = self.pair
+            p.sample()
+            p.fwd()
+            p.head()
+            p.dw()
+            p.opt(0)  # split-K reduce into the flat gradient, no update
+            return float(self._pair_keep["loss_acc"].item())
         loss, _ = self._forward_loss()
         if self.device.type != "cuda":
             self.opt.zero_grad()

@@ -14,12 +14,14 @@ import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "benchmarks"))
 
 
-def _setup(device, n=6000, comm=30, dim=32, dims=(64, 64, 32), B=64, fan=(10, 5), lr=0.01, seed=7):
+def _setup(device, n=6000, comm=30, dim=32, dims=(64, 64, 32), B=64, fan=(10, 5), lr=0.01, seed=7, fused=True,
+           K=5):
     from bench_unsup_sage import build
     from euler_amd.models.sage_tower import UnsupSageTrainer
 
     graph, x, test = build(n, comm, 10, dim, 0.5, seed, torch.device(device))
-    tr = UnsupSageTrainer(graph, B, list(fan), list(dims), features=x, num_negs=5, learning_rate=lr, init_seed=seed)
+    tr = UnsupSageTrainer(graph, B, list(fan), list(dims), features=x, num_negs=K, learning_rate=lr, init_seed=seed,
+                          fused=fused)
     return tr, test
 
 
@@ -60,9 +62,15 @@ def test_unsup_param_layout_roundtrip_cpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dims,fan", [((64, 64, 32), (10, 5)), ((128, 256, 128), (25, 10)), ((40, 72, 24), (5, 3))])
-def test_unsup_kernels_match_fp32_oracle(cuda, dims, fan):
-    tr, _ = _setup(cuda, dims=dims, fan=fan, B=64)
+@pytest.mark.parametrize("fused", [True, False], ids=["pair_plan", "per_op"])
+@pytest.mark.parametrize("dims,fan,K", [((64, 64, 32), (10, 5), 5), ((128, 128, 128), (25, 10), 5),
+                                        ((40, 72, 24), (5, 3), 3), ((128, 256, 128), (10, 5), 1)])
+def test_unsup_kernels_match_fp32_oracle(cuda, dims, fan, K, fused):
+    """the fused 7-launch step (PairPlan: roots drawn in the samplers, pair head kernel, one
+    dW and one optimizer launch) and the per-op step against the fp32 torch oracle on the
+    same sampled trees: loss and every parameter gradient"""
+    tr, _ = _setup(cuda, dims=dims, fan=fan, B=64, fused=fused, K=K)
+    assert (tr.pair is not None) == fused, getattr(tr, "fused_error", None)
     loss_k = tr.forward_backward()
     torch.cuda.synchronize()
     gk = tr.gradients()
@@ -77,15 +85,15 @@ def test_unsup_kernels_match_fp32_oracle(cuda, dims, fan):
 
 
 @pytest.mark.gpu
-def test_unsup_graph_replay_trains(cuda):
+@pytest.mark.parametrize("fused", [True, False], ids=["pair_plan", "per_op"])
+def test_unsup_graph_replay_trains(cuda, fused):
     from bench_unsup_sage import link_auc
 
-    tr, test = _setup(cuda, n=8000, comm=40, B=128)
+    tr, test = _setup(cuda, n=8000, comm=40, B=128, fused=fused)
     auc0 = link_auc(tr, test, 8000, 2000, 7)
-    tr.capture()
+    tr.capture(steps=4)
     first = float(tr.loss)
-    for _ in range(300):
-        tr.step()
+    tr.replay_steps(300)
     torch.cuda.synchronize()
     last = float(tr.loss)
     assert math.isfinite(last) and last < 0.6 * first, (first, last)
