@@ -50,11 +50,12 @@ def synthetic_kg(num_ent, num_rel, num_triples, seed, device, num_test=5000):
 
 
 class RGCNTransE(nn.Module):
-    def __init__(self, num_ent, num_rel, dim, layers=2, margin=1.0):
+    def __init__(self, num_ent, num_rel, dim, layers=1, margin=1.0, num_bases=0):
         super().__init__()
         self.ent = nn.Parameter(torch.randn(num_ent, dim) * 0.1)
         self.rel = nn.Parameter(torch.randn(num_rel, dim) * 0.1)
-        self.convs = nn.ModuleList([RelationConv(dim, dim, total_relation_num=num_rel) for _ in range(layers)])
+        self.convs = nn.ModuleList([RelationConv(dim, dim, total_relation_num=num_rel, num_bases=num_bases)
+                                    for _ in range(layers)])
         self.margin = margin
 
     def encode(self, edge_index, edge_rel):
@@ -87,7 +88,14 @@ def main(argv=None):
     p.add_argument("--lr", type=float, default=1e-3)
     p.add_argument("--margin", type=float, default=1.0, help="TransE margin (reference run_transX --margin)")
     p.add_argument("--seed", type=int, default=3)
-    p.add_argument("--layers", type=int, default=2, help="R-GCN layers before the TransE decoder (0: TransE alone)")
+    p.add_argument("--layers", type=int, default=1,
+                   help="R-GCN layers before the TransE decoder (0: TransE alone; the reference "
+                        "examples/rgcn/run_rgcn.py:35 runs 1)")
+    p.add_argument("--num-bases", type=int, default=0,
+                   help="basis decomposition of the relation matrices (0: one full matrix per relation, as the "
+                        "reference)")
+    p.add_argument("--rel-wd", type=float, default=0.0,
+                   help="weight decay on the relation matrices / bases only (a flat-optimizer decay range)")
     p.add_argument("--normalize", type=int, default=1,
                    help="1: l2-normalised rows in the score (reference transX.py:63-66); 0: raw rows")
     p.add_argument("--task", choices=["lattice", "cold", "types"], default="lattice",
@@ -146,7 +154,8 @@ def main(argv=None):
         keep = cold[te_src] & ~cold[te_dst]               # test: cold head, warm tail
         te_src, te_rel, te_dst = te_src[keep], te_rel[keep], te_dst[keep]
     torch.manual_seed(args.seed * 101 + rank)
-    model = RGCNTransE(args.num_ent, args.num_rel, args.dim, layers=args.layers, margin=args.margin).to(dev)
+    model = RGCNTransE(args.num_ent, args.num_rel, args.dim, layers=args.layers, margin=args.margin,
+                       num_bases=args.num_bases).to(dev)
     model.norm = norm
 
     def batch():
@@ -163,10 +172,19 @@ def main(argv=None):
     # fp32 buffer: one flat Adam launch (optim.hip), one all-reduce with data parallelism
     flat = FlatParams(model.parameters(), dev)
     for conv in model.convs:
-        # the relation dW accumulates straight into its flat-grad view (no [R, D, D] temporary
-        # + AccumulateGrad pass per layer; the flat grad is all-reduced as one buffer)
-        gnn_ops.enable_grad_sink(conv.matrix, zeroed=True)  # opt.zero_grad() runs before every backward
+        if conv.num_bases == 0:
+            # the relation dW accumulates straight into its flat-grad view (no [R, D, D] temporary
+            # + AccumulateGrad pass per layer; the flat grad is all-reduced as one buffer)
+            gnn_ops.enable_grad_sink(conv.matrix, zeroed=True)  # opt.zero_grad() runs before every backward
     opt = FlatOptimizer(flat, "adam", args.lr)
+    if args.rel_wd > 0 and model.convs:
+        # decay on the relation transforms only: they are contiguous in the flat buffer
+        rel_params = {id(p) for c in model.convs for p in ([c.matrix] if c.num_bases == 0 else [c.bases, c.coef])}
+        spans = [(o, o + n) for p, (o, n) in zip(flat.params, flat.offsets) if id(p) in rel_params]
+        lo, hi = min(a for a, _ in spans), max(b for _, b in spans)
+        if hi - lo != sum(b - a for a, b in spans):
+            raise SystemExit("relation parameters are not contiguous in the flat buffer")
+        opt.set_decay_range(lo, hi, args.rel_wd)
     loss_buf = torch.zeros((), device=dev)
 
     def evaluate():
@@ -244,7 +262,7 @@ def main(argv=None):
     eval_final = evaluate()
     if rank == 0:
         print(json.dumps({
-            "metric": "train triples/sec (whole node), R-GCN (2 layers) + TransE on FB15k-shaped KG",
+            "metric": f"train triples/sec (whole node), R-GCN ({args.layers} layer(s)) + TransE on FB15k-shaped KG",
             "value": round(args.batch * world * args.steps / el, 1),
             "unit": "triples/s",
             "n_gpus": world,
@@ -256,10 +274,13 @@ def main(argv=None):
             "vs_baseline": None,
             "dtype": "bf16 relation GEMMs (fp32 accumulate), fp32 scores",
             "data": "synthetic (FB15k-shaped lattice KG, power-law relations)",
-            "config": {"model": f"R-GCN {args.layers}x RelationConv(mean, self-loop) + TransE-l2 margin, flat Adam",
+            "config": {"model": f"R-GCN {args.layers}x RelationConv(mean, self-loop"
+                                f"{', %d bases' % args.num_bases if args.num_bases else ''}) + TransE-l2 margin, "
+                                f"flat Adam{', relation weight decay %g' % args.rel_wd if args.rel_wd else ''}",
                        "num_ent": args.num_ent, "num_rel": args.num_rel, "num_triples": args.num_triples,
                        "dim": args.dim, "batch_per_gpu": args.batch, "num_negs": args.num_negs,
                        "normalize": norm, "task": args.task, "hipgraph": graph is not None,
+                       "lr": args.lr, "margin": args.margin, "num_bases": args.num_bases, "rel_wd": args.rel_wd,
                        "parallelism": f"dp{world}", "loss_first_last": [round(first, 4), round(last, 4)],
                        "grad_sync": sync_name, "grad_sync_choice": sync_info or None,
                        "heldout_tail_ranking": {"triples": int(te_src.numel()), "entities": args.num_ent,

@@ -365,24 +365,63 @@ class DNAConv(Conv):
         return self.scatter(gn[0] * gn[1] * out, edge_index, size)
 
 
+class _BasisCompose(torch.autograd.Function):
+    """W [R, N*K] = coef [R, B] @ bases [B, N*K] and its gradients on the tiled MFMA GEMM"""
+
+    @staticmethod
+    def forward(ctx, coef, bases):
+        ctx.save_for_backward(coef, bases)
+        return gnn_ops.gemm(coef, bases)
+
+    @staticmethod
+    def backward(ctx, dw):
+        coef, bases = ctx.saved_tensors
+        dw = dw.contiguous().float()
+        dcoef = gnn_ops.gemm(dw, bases, trans_b=True)
+        dbases = gnn_ops.gemm(coef, dw, trans_a=True,
+                              splits=gnn_ops._gemm_splits(coef.shape[0], -(-bases.shape[1] // 64)))
+        return dcoef, dbases
+
+
 class RelationConv(Conv):
     """R-GCN relation transform (reference relation_conv.py:33-73).  Instead of gathering
     an [E, dim, fea_dim] matrix per edge, edges are grouped by relation and each group
-    does one GEMM."""
+    does one GEMM.
 
-    def __init__(self, fea_dim, dim, metapath=None, total_relation_num=1, **kwargs):
+    ``num_bases`` > 0 (an extension; the reference keeps one full matrix per relation):
+    the basis decomposition of the R-GCN paper, W_r = sum_b a_rb V_b with B shared bases —
+    rare relations of a power-law KG then share what the frequent ones learn instead of
+    memorising their few triples.  :attr:`matrix` is then composed every forward (one GEMM)."""
+
+    def __init__(self, fea_dim, dim, metapath=None, total_relation_num=1, num_bases=0, **kwargs):
         super().__init__("mean")
         self.fea_dim, self.dim, self.relation_num = fea_dim, dim, total_relation_num
-        self.matrix = nn.Parameter(torch.empty(total_relation_num, dim, fea_dim))
-        nn.init.kaiming_uniform_(self.matrix.view(total_relation_num * dim, fea_dim), a=math.sqrt(5))
+        self.num_bases = int(num_bases)
+        if self.num_bases > 0:
+            self.bases = nn.Parameter(torch.empty(self.num_bases, dim, fea_dim))
+            nn.init.kaiming_uniform_(self.bases.view(self.num_bases * dim, fea_dim), a=math.sqrt(5))
+            self.coef = nn.Parameter(torch.randn(total_relation_num, self.num_bases) / math.sqrt(self.num_bases))
+        else:
+            self.matrix = nn.Parameter(torch.empty(total_relation_num, dim, fea_dim))
+            nn.init.kaiming_uniform_(self.matrix.view(total_relation_num * dim, fea_dim), a=math.sqrt(5))
         self.fc = Dense(dim, use_bias=False)
+
+    def relation_matrices(self):
+        """[R, dim, fea_dim] relation transforms"""
+        if self.num_bases == 0:
+            return self.matrix
+        if self.bases.is_cuda:
+            w = _BasisCompose.apply(self.coef, self.bases.view(self.num_bases, -1))
+        else:
+            w = self.coef @ self.bases.view(self.num_bases, -1)
+        return w.view(self.relation_num, self.dim, self.fea_dim)
 
     def forward(self, x, edge_index, size=None, edge_attr=None, **kwargs):
         assert edge_attr is not None
         x = _pair(x)
         src = x[1] if x[1] is not None else x[0]
         # relation-grouped MFMA GEMM with the gather and the mean aggregation fused (rgcn.hip)
-        agg = gnn_ops.relation_transform(src, edge_attr, self.matrix, edge_index, size, "mean")
+        agg = gnn_ops.relation_transform(src, edge_attr, self.relation_matrices(), edge_index, size, "mean")
         fc, x0 = self.fc, x[0]
         if x0.is_cuda and x0.dim() == 2 and not fc.has_uninitialized_params() and fc.bias is None \
                 and fc.activation is None:

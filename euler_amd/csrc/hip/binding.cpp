@@ -388,17 +388,25 @@ torch::Tensor spmm_csr(torch::Tensor indptr, torch::Tensor col, c10::optional<to
 
 // ----------------------------------------------------------------------------- optimizers
 void flat_optim_(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, torch::Tensor step, double lr,
-                 double b1, double b2, double eps, double wd, double grad_scale, int64_t kind) {
+                 double b1, double b2, double eps, double wd, double grad_scale, int64_t kind,
+                 c10::optional<torch::Tensor> ticket, double wd2, int64_t w0, int64_t w1) {
   for (auto* t : {&p, &g, &m, &v}) {
     need_cuda(*t, "optimizer buffer");
-    TORCH_CHECK(t->scalar_type() == torch::kFloat32 && t->numel() == p.numel(), "optimizer buffers: fp32, same size");
+    TORCH_CHECK(t->scalar_type() == torch::kFloat32 && t->numel() == p.numel() && t->is_contiguous(),
+                "optimizer buffers: fp32, same size, contiguous");
   }
   need_i64(step, "step");
+  int32_t* tk = nullptr;
+  if (ticket.has_value()) {
+    need_cuda(*ticket, "ticket");
+    TORCH_CHECK(ticket->scalar_type() == torch::kInt32 && ticket->numel() >= 1, "ticket: int32 [1]");
+    tk = ticket->data_ptr<int32_t>();
+  }
   const c10::DeviceGuard gd(p.device());
-  check(eh_flat_optim(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), p.numel(),
-                      step.data_ptr<int64_t>(), static_cast<float>(lr), static_cast<float>(b1), static_cast<float>(b2),
-                      static_cast<float>(eps), static_cast<float>(wd), static_cast<float>(grad_scale),
-                      static_cast<int>(kind), cur_stream()),
+  check(eh_flat_optim2(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), p.numel(),
+                       step.data_ptr<int64_t>(), tk, static_cast<float>(lr), static_cast<float>(b1),
+                       static_cast<float>(b2), static_cast<float>(eps), static_cast<float>(wd), static_cast<float>(wd2),
+                       w0, w1, static_cast<float>(grad_scale), static_cast<int>(kind), cur_stream()),
         "flat_optim");
 }
 
@@ -587,7 +595,9 @@ PYBIND11_MODULE(_hip_ops, m) {
   m.def("edge_softmax", &edge_softmax);
   m.def("edge_softmax_bwd", &edge_softmax_bwd);
   m.def("spmm_csr", &spmm_csr);
-  m.def("flat_optim_", &flat_optim_);
+  m.def("flat_optim_", &flat_optim_, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("step"),
+        py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("grad_scale"),
+        py::arg("kind"), py::arg("ticket") = py::none(), py::arg("wd2") = 0.0, py::arg("w0") = 0, py::arg("w1") = 0);
   m.def("sparse_optim_", &sparse_optim_);
   m.def("sample_neighbor_into", &sample_neighbor_into);
   py::class_<XgmiAr, std::shared_ptr<XgmiAr>>(m, "XgmiAr")

@@ -147,6 +147,11 @@ hipError_t eh_flow_expand(const int64_t* indptr, const int32_t* nbr, int64_t num
 // optim.hip
 hipError_t eh_flat_optim(float* p, const float* g, float* m, float* v, int64_t n, int64_t* step, float lr, float b1,
                          float b2, float eps, float wd, float grad_scale, int kind, hipStream_t s);
+// ticket (int32 [1], zero-initialised; null: a separate step-increment launch): the last block
+// advances the step; wd2 replaces wd on the elements [w0, w1)
+hipError_t eh_flat_optim2(float* p, const float* g, float* m, float* v, int64_t n, int64_t* step, int32_t* ticket,
+                          float lr, float b1, float b2, float eps, float wd, float wd2, int64_t w0, int64_t w1,
+                          float grad_scale, int kind, hipStream_t s);
 hipError_t eh_sparse_optim(float* table, float* m, float* v, const int64_t* rows, const void* grads, int grads_bf16,
                            int64_t n, int D, int64_t n_rows, int64_t* step, float lr, float b1, float b2, float eps,
                            int kind, hipStream_t s);

@@ -7,40 +7,30 @@
 // Reference optimizers: tf_euler/python/utils/optimizers.py:22-31 (sgd, momentum,
 // adagrad, adam); embedding stores: utils/embedding.py:24-68.
 #include "hip/common.h"
+#include "hip/launchers.h"
 
 namespace euler_hip {
 
-// kind: 0 adam, 1 adagrad, 2 sgd, 3 momentum
-__global__ __launch_bounds__(256) void flat_optim_kernel(float* __restrict__ p, const float* __restrict__ g,
-                                                         float* __restrict__ m, float* __restrict__ v, int64_t n,
-                                                         const int64_t* __restrict__ step, float lr, float b1,
-                                                         float b2, float eps, float wd, float grad_scale, int kind) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  float gi = g[i] * grad_scale + wd * p[i];
-  if (kind == 0) {
-    const float t = static_cast<float>(step[0]);
-    const float mi = b1 * m[i] + (1.f - b1) * gi;
-    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
-    m[i] = mi;
-    v[i] = vi;
-    const float bc1 = 1.f - __powf(b1, t), bc2 = 1.f - __powf(b2, t);
-    p[i] -= lr * (mi / bc1) / (sqrtf(vi / bc2) + eps);
-  } else if (kind == 1) {
-    const float acc = v[i] + gi * gi;
-    v[i] = acc;
-    p[i] -= lr * gi / (sqrtf(acc) + eps);
-  } else if (kind == 2) {
-    p[i] -= lr * gi;
-  } else {
-    const float mi = b1 * m[i] + gi;
-    m[i] = mi;
-    p[i] -= lr * mi;
-  }
-}
+// One optimizer launch over a flat fp32 buffer (p, g, m, v), hipGraph-replay safe.
+//   * The Adam step count lives on the device: every block uses t = step + bias (bias 1:
+//     this launch advances it), and with a ticket the LAST block to finish stores step + 1
+//     and re-arms the ticket — no separate increment launch.  Every block has read the
+//     step before it takes its ticket, so none can see the new value.
+//   * Weight decay wd, or wd2 on the elements [w0, w1) (a per-parameter-group decay, e.g.
+//     only on a model's relation matrices).
+struct FlatOptArgs {
+  float *p, *m, *v;
+  const float* g;
+  int64_t n;     // elements (the scalar kernel) / float4 groups (the vector kernel)
+  int64_t base;  // index of element 0 in the whole buffer (decay range)
+  int64_t* step;
+  int32_t* ticket;  // null: the step is advanced by step_inc_kernel before the launch
+  int32_t step_bias, advance;
+  float lr, b1, b2, eps, wd, wd2, grad_scale;
+  int64_t w0, w1;
+  int32_t kind;  // 0 adam, 1 adagrad, 2 sgd, 3 momentum
+};
 
-// float4 form for the bulk of the flat buffer: 16-byte loads / stores of p, g, m, v, all
-// four loads issued before the math (the update is bandwidth-bound: 28 B per parameter)
 __device__ __forceinline__ float optim_one(float& p, float g, float& m, float& v, float t, float lr, float b1,
                                            float b2, float eps, float wd, float grad_scale, int kind) {
   const float gi = g * grad_scale + wd * p;
@@ -61,28 +51,59 @@ __device__ __forceinline__ float optim_one(float& p, float g, float& m, float& v
   return p;
 }
 
-__global__ __launch_bounds__(256) void flat_optim4_kernel(float* __restrict__ p, const float* __restrict__ g,
-                                                          float* __restrict__ m, float* __restrict__ v, int64_t n4,
-                                                          const int64_t* __restrict__ step, float lr, float b1,
-                                                          float b2, float eps, float wd, float grad_scale, int kind) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n4) return;
-  float4_t pv = reinterpret_cast<float4_t*>(p)[i];
-  const float4_t gv = reinterpret_cast<const float4_t*>(g)[i];
-  float4_t mv = kind == 0 || kind == 3 ? reinterpret_cast<float4_t*>(m)[i] : float4_t{0.f, 0.f, 0.f, 0.f};
-  float4_t vv = kind == 0 || kind == 1 ? reinterpret_cast<float4_t*>(v)[i] : float4_t{0.f, 0.f, 0.f, 0.f};
-  const float t = static_cast<float>(step[0]);
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    float pc = pv[c], mc = mv[c], vc = vv[c];
-    optim_one(pc, gv[c], mc, vc, t, lr, b1, b2, eps, wd, grad_scale, kind);
-    pv[c] = pc;
-    mv[c] = mc;
-    vv[c] = vc;
+__device__ __forceinline__ float flat_wd(const FlatOptArgs& a, int64_t e) {
+  return (e >= a.w0 && e < a.w1) ? a.wd2 : a.wd;
+}
+
+// the last block to finish advances the step (see FlatOptArgs)
+__device__ __forceinline__ void flat_step_ticket(const FlatOptArgs& a) {
+  if (!a.ticket || !a.advance) return;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int prev = atomicAdd(a.ticket, 1);
+    if (prev == static_cast<int>(gridDim.x) - 1) {
+      a.step[0] += 1;
+      *a.ticket = 0;
+    }
   }
-  reinterpret_cast<float4_t*>(p)[i] = pv;
-  if (kind == 0 || kind == 3) reinterpret_cast<float4_t*>(m)[i] = mv;
-  if (kind == 0 || kind == 1) reinterpret_cast<float4_t*>(v)[i] = vv;
+}
+
+__global__ __launch_bounds__(256) void flat_optim_kernel(FlatOptArgs a) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const float t = static_cast<float>(a.step[0] + a.step_bias);
+  if (i < a.n) {
+    float p = a.p[i], m = a.m[i], v = a.v[i];
+    optim_one(p, a.g[i], m, v, t, a.lr, a.b1, a.b2, a.eps, flat_wd(a, a.base + i), a.grad_scale, a.kind);
+    a.p[i] = p;
+    if (a.kind == 0 || a.kind == 3) a.m[i] = m;
+    if (a.kind == 0 || a.kind == 1) a.v[i] = v;
+  }
+  flat_step_ticket(a);
+}
+
+// float4 form for the bulk of the flat buffer: 16-byte loads / stores of p, g, m, v, all
+// four loads issued before the math (the update is bandwidth-bound: 28 B per parameter)
+__global__ __launch_bounds__(256) void flat_optim4_kernel(FlatOptArgs a) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const float t = static_cast<float>(a.step[0] + a.step_bias);
+  if (i < a.n) {
+    float4_t pv = reinterpret_cast<float4_t*>(a.p)[i];
+    const float4_t gv = reinterpret_cast<const float4_t*>(a.g)[i];
+    float4_t mv = a.kind == 0 || a.kind == 3 ? reinterpret_cast<float4_t*>(a.m)[i] : float4_t{0.f, 0.f, 0.f, 0.f};
+    float4_t vv = a.kind == 0 || a.kind == 1 ? reinterpret_cast<float4_t*>(a.v)[i] : float4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float pc = pv[c], mc = mv[c], vc = vv[c];
+      optim_one(pc, gv[c], mc, vc, t, a.lr, a.b1, a.b2, a.eps, flat_wd(a, a.base + 4 * i + c), a.grad_scale, a.kind);
+      pv[c] = pc;
+      mv[c] = mc;
+      vv[c] = vc;
+    }
+    reinterpret_cast<float4_t*>(a.p)[i] = pv;
+    if (a.kind == 0 || a.kind == 3) reinterpret_cast<float4_t*>(a.m)[i] = mv;
+    if (a.kind == 0 || a.kind == 1) reinterpret_cast<float4_t*>(a.v)[i] = vv;
+  }
+  flat_step_ticket(a);
 }
 
 __global__ void step_inc_kernel(int64_t* step) { step[0] += 1; }
@@ -181,20 +202,40 @@ extern "C" {
 
 hipError_t eh_flat_optim(float* p, const float* g, float* m, float* v, int64_t n, int64_t* step, float lr, float b1,
                          float b2, float eps, float wd, float grad_scale, int kind, hipStream_t s) {
-  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, s, step);
-  if (n == 0) return hipGetLastError();
+  return eh_flat_optim2(p, g, m, v, n, step, nullptr, lr, b1, b2, eps, wd, 0.f, 0, 0, grad_scale, kind, s);
+}
+
+hipError_t eh_flat_optim2(float* p, const float* g, float* m, float* v, int64_t n, int64_t* step, int32_t* ticket,
+                          float lr, float b1, float b2, float eps, float wd, float wd2, int64_t w0, int64_t w1,
+                          float grad_scale, int kind, hipStream_t s) {
+  if (!ticket) hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, s, step);
+  if (n == 0) {
+    if (ticket) hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, s, step);
+    return hipGetLastError();
+  }
+  FlatOptArgs a{p, m, v, g, 0, 0, step, ticket, ticket ? 1 : 0, 1, lr, b1, b2, eps, wd, wd2, grad_scale, w0, w1, kind};
   // 16-byte aligned buffers (torch allocations; offset 0): the float4 kernel covers the
   // first n - n % 4 parameters, the scalar kernel the tail
   const bool al = (reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
                    reinterpret_cast<uintptr_t>(v)) % 16 == 0;
   const int64_t n4 = al ? n / 4 : 0;
-  if (n4 > 0)
-    hipLaunchKernelGGL(flat_optim4_kernel, dim3(static_cast<uint32_t>(ceil_div(n4, 256))), dim3(256), 0, s, p, g, m,
-                       v, n4, step, lr, b1, b2, eps, wd, grad_scale, kind);
   const int64_t done = n4 * 4;
-  if (done < n)
-    hipLaunchKernelGGL(flat_optim_kernel, dim3(static_cast<uint32_t>(ceil_div(n - done, 256))), dim3(256), 0, s,
-                       p + done, g + done, m + done, v + done, n - done, step, lr, b1, b2, eps, wd, grad_scale, kind);
+  if (n4 > 0) {
+    FlatOptArgs b = a;
+    b.n = n4;
+    b.advance = done == n;  // the tail kernel advances the step when there is a tail
+    hipLaunchKernelGGL(flat_optim4_kernel, dim3(static_cast<uint32_t>(ceil_div(n4, 256))), dim3(256), 0, s, b);
+  }
+  if (done < n) {
+    FlatOptArgs b = a;
+    b.p += done;
+    b.g += done;
+    b.m += done;
+    b.v += done;
+    b.n = n - done;
+    b.base = done;
+    hipLaunchKernelGGL(flat_optim_kernel, dim3(static_cast<uint32_t>(ceil_div(n - done, 256))), dim3(256), 0, s, b);
+  }
   return hipGetLastError();
 }
 

@@ -71,19 +71,28 @@ class FlatOptimizer:
         if optimizer == "adagrad":
             self.v.fill_(0.1)  # tf.train.AdagradOptimizer initial_accumulator_value
         self.step_count = torch.zeros(1, dtype=torch.int64, device=dev)
+        # the last block of the update launch advances step_count (csrc/hip/optim.hip)
+        self._ticket = torch.zeros(1, dtype=torch.int32, device=dev) if dev.type == "cuda" else None
+        # (start, end, weight decay) replacing weight_decay on one element range of the flat
+        # buffer (e.g. only an R-GCN's relation matrices): set_decay_range()
+        self.decay_range = (0, 0, 0.0)
 
     def zero_grad(self):
         self.flat.zero_grad()
 
     def step(self, grad_scale: float = 1.0):
         f = self.flat
+        w0, w1, wd2 = self.decay_range
         if use_hip(f.flat):
             hip().flat_optim_(f.flat, f.grad, self.m, self.v, self.step_count, self.lr, self.b1, self.b2,
-                              self.eps, self.wd, float(grad_scale), _KINDS[self.kind])
+                              self.eps, self.wd, float(grad_scale), _KINDS[self.kind], self._ticket, float(wd2),
+                              int(w0), int(w1))
             return
         with torch.no_grad():
             self.step_count += 1
-            g = f.grad * grad_scale + self.wd * f.flat
+            wd = torch.full_like(f.flat, self.wd)
+            wd[int(w0):int(w1)] = float(wd2)
+            g = f.grad * grad_scale + wd * f.flat
             if self.kind == "adam":
                 t = float(self.step_count.item())
                 self.m.mul_(self.b1).add_(g, alpha=1 - self.b1)
@@ -99,6 +108,11 @@ class FlatOptimizer:
             else:
                 self.m.mul_(self.b1).add_(g)
                 f.flat.sub_(self.lr * self.m)
+
+    def set_decay_range(self, start: int, end: int, weight_decay: float):
+        """weight decay ``weight_decay`` instead of the optimizer's on flat elements
+        [start, end) (one parameter group, e.g. a relation-matrix regulariser)"""
+        self.decay_range = (int(start), int(end), float(weight_decay))
 
     def state_dict(self):
         return {"kind": self.kind, "lr": self.lr, "m": self.m, "v": self.v, "step": self.step_count}
