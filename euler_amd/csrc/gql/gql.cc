@@ -42,7 +42,8 @@ static std::vector<std::string> Lex(const std::string& q) {
 
 static const std::set<std::string>& StepKeywords() {
   static const std::set<std::string> k = {"v", "e", "sampleN", "sampleNWithTypes", "sampleE", "select", "v_select",
-                                          "outV", "inV", "outE", "sampleNB", "sampleLNB", "values", "label"};
+                                          "outV", "inV", "outE", "sampleNB", "sampleLNB", "values", "label",
+                                          "sampleNodeAt"};
   return k;
 }
 
@@ -250,6 +251,7 @@ class Translator {
         if (sample) {
           if (s.params.size() < 3) return Status::InvalidArgument("sampleNB needs (edge_types, count, default)");
           nd.attrs = {s.params[0], s.params[1], s.params[2]};
+          if (s.params.size() > 3) nd.attrs.push_back(s.params[3]);  // keyed draws
         } else {
           nd.attrs = {s.params.empty() ? std::string("-1") : s.params[0]};
         }
@@ -272,6 +274,14 @@ class Translator {
         }
         c = {outs[1], false};
         Alias(s.alias, outs, c);
+      } else if (op == "sampleNodeAt") {
+        // keyed root draws (graph.h KeyedBuckets): the cursor holds codes pos * buckets + bucket
+        if (s.params.size() < 3) return Status::InvalidArgument("sampleNodeAt needs (node_type, buckets, key, [default])");
+        NodeDef& nd = Add("API_SAMPLE_NODE_AT");
+        nd.inputs = {c.ids};
+        nd.attrs = s.params;
+        c = {nd.Output(0), false};
+        Alias(s.alias, {nd.Output(0)}, c);
       } else if (op == "outE") {
         NodeDef& nd = Add("API_GET_NB_EDGE");
         nd.inputs = {c.ids};
@@ -384,6 +394,9 @@ const std::map<std::string, Rule>& Rules() {
       {"API_GET_NODE_T", {SplitKind::kId, MergeKind::kRegular, false, nullptr}},
       {"API_GET_EDGE_SUM_WEIGHT", {SplitKind::kId, MergeKind::kRegular, false, nullptr}},
       {"API_SAMPLE_L", {SplitKind::kId, MergeKind::kRegular, false, nullptr}},
+      // codes pos * buckets + bucket route like ids: buckets is a multiple of the partitions
+      {"API_SAMPLE_NODE_AT", {SplitKind::kId, MergeKind::kRegular, false, nullptr}},
+      {"API_NODE_BUCKET_WEIGHT", {SplitKind::kAllShards, MergeKind::kAppend, false, nullptr}},
       {"API_GET_NODE", {SplitKind::kId, MergeKind::kAppend, false, nullptr}},
       {"API_GET_EDGE", {SplitKind::kId, MergeKind::kAppend, false, nullptr}},
       {"API_SAMPLE_NODE", {SplitKind::kSampleNode, MergeKind::kAppend, false, nullptr}},

@@ -175,6 +175,15 @@ class Graph {
   double EdgeWeightSum(int edge_type) const;
   const std::vector<int64_t>& NodeRowsOfType(int t) const;
 
+  // ------------------------------------------------------------ keyed (shard-independent) sampling
+  // See keyed.cc.  Nodes are grouped into `buckets` virtual buckets (id % buckets, buckets a
+  // multiple of the partition count, so a bucket never spans shards); the per-bucket
+  // weight sums (sorted-id order, double) and in-bucket draws come out the same on a shard
+  // as on the whole graph.
+  std::vector<double> NodeBucketWeights(int node_type, uint64_t buckets) const;
+  // one node of `bucket` by node weight (def when the bucket is empty)
+  uint64_t SampleNodeInBucket(int node_type, uint64_t buckets, uint64_t bucket, Rng& rng, uint64_t def) const;
+
   // ------------------------------------------------------------ edges
   int64_t EdgeRow(uint64_t src, uint64_t dst, int32_t type) const;
   inline uint64_t EdgeSrc(int64_t e) const { return edge_src_[e]; }
@@ -229,7 +238,32 @@ class Graph {
   std::vector<AliasTable> edge_sampler_;
   std::vector<double> edge_wsum_;
   std::vector<std::string> graph_labels_;
+  // lazily built per-(type, buckets) samplers of SampleNodeInBucket (keyed.cc)
+  struct BucketCache;
+  static std::shared_ptr<BucketCache> NewBucketCache();
+  std::shared_ptr<BucketCache> bucket_cache_ = NewBucketCache();
+  const void* BucketSampler(int node_type, uint64_t buckets) const;
 };
+
+// Keyed sampling used by the native pipeline so that a batch is a function of
+// (seed, batch, hop) only — identical whether the graph is in-process or on shard servers
+// (the reference seeds its samplers from time(0), euler/common/random.cc:21-28):
+//   KeyedBuckets(P)        the virtual bucket count for P data partitions (multiple of P)
+//   KeyedKey(seed, b, h)   the Philox key of batch b, hop h (h = 0: roots)
+//   root i                 bucket  = alias over the bucket weights, Philox (key, 2i)
+//                          node    = SampleNodeInBucket(...), Philox (key, 2i + 1)
+//   neighbours of ids[i]   Philox (key, KeyedStream(id, occurrence of id in ids[0..i]))
+uint64_t KeyedBuckets(uint32_t partitions);
+uint64_t KeyedKey(uint64_t seed, uint64_t batch, uint64_t hop);
+uint64_t KeyedStream(uint64_t id, uint64_t occurrence);
+// occurrence index of every ids[i] among ids[0..i]
+void KeyedOccurrences(const uint64_t* ids, int64_t n, std::vector<uint32_t>* occ);
+// k keyed draws per id over etypes (out edges), occ from KeyedOccurrences (any sub-range of
+// a request may be drawn on its own); a node without edges / missing gets def (weight 0,
+// type -1); out_w / out_t may be null
+void SampleNeighborsKeyed(const Graph& g, const uint64_t* ids, const uint32_t* occ, int64_t n,
+                          const std::vector<int32_t>& etypes, int k, uint64_t key, uint64_t def, uint64_t* out_id,
+                          float* out_w, int32_t* out_t);
 
 // ---------------------------------------------------------------------------
 // GraphBuilder: accumulate nodes / adjacency entries / edges / features from any

@@ -10,7 +10,11 @@
 //   API_GET_P               in [ids | edges] attrs [feature names...] udf -> 2i idx, 2i+1 values
 //   API_GET_NB_NODE / API_GET_RNB_NODE  in [ids] attrs [etypes] dnf pp -> idx ids weights types
 //   API_GET_NB_EDGE         in [ids] attrs [etypes]             -> 0 idx 1 edges 2 weights
-//   API_SAMPLE_NB           in [ids] attrs [etypes, count, default] dnf pp -> idx ids weights types
+//   API_SAMPLE_NB           in [ids] attrs [etypes, count, default, (key)] dnf pp -> idx ids weights types
+//                           (with key: keyed draws, SampleNeighborsKeyed — shard-independent)
+//   API_SAMPLE_NODE_AT      in [codes = pos * buckets + bucket] attrs [type, buckets, key, default]
+//                           -> 0 ids (one per code: the keyed in-bucket draw of root pos)
+//   API_NODE_BUCKET_WEIGHT  attrs [type, buckets]                -> 0 double [buckets]
 //   API_GET_EDGE_SUM_WEIGHT in [ids] attrs [etypes]             -> 0 float
 //   API_SAMPLE_L            in [ids] attrs [etypes, default]    -> 0 ids (one neighbor each)
 //   API_SPARSE_GET_ADJ      in [roots, candidates] attrs [etypes, batch_n] -> 0 idx 1 col (int64)
@@ -438,6 +442,34 @@ class SampleNeighborOp : public OpKernel {
       if (!nbr_idx) global = QueryIndex(ctx, d);
     }
     const int64_t n = static_cast<int64_t>(ids.size());
+    if (nd.attrs.size() > 3 && !dnf) {
+      // keyed: the draws of ids[i] depend on (key, id, occurrence) only
+      const uint64_t key = static_cast<uint64_t>(ctx->AttrInt(nd.attrs[3]));
+      std::vector<uint32_t> occ;
+      KeyedOccurrences(ids.data(), n, &occ);
+      Tensor oid(DType::kUInt64, {n * count}), ow(DType::kFloat, {n * count}), ot(DType::kInt32, {n * count});
+      uint64_t* pid = oid.data<uint64_t>();
+      float* pw = ow.data<float>();
+      int32_t* pt = ot.data<int32_t>();
+      ParallelChunks(n, 512, [&](int64_t b, int64_t e, Rng&) {
+        SampleNeighborsKeyed(g, ids.data() + b, occ.data() + b, e - b, et, count, key, def, pid + b * count,
+                             pw + b * count, pt + b * count);
+      });
+      if (pp.empty()) {
+        ctx->Set(nd.Output(0), MakeUniformIdx(n, count));
+        ctx->Set(nd.Output(1), oid);
+        ctx->Set(nd.Output(2), ow);
+        ctx->Set(nd.Output(3), ot);
+        return;
+      }
+      std::vector<std::vector<IdWeightType>> rows(n);
+      for (int64_t i = 0; i < n; ++i) {
+        for (int k = 0; k < count; ++k) rows[i].push_back({pid[i * count + k], pw[i * count + k], pt[i * count + k]});
+        pp.Apply(&rows[i]);
+      }
+      EmitNeighbors(nd, ctx, rows);
+      return;
+    }
     if (!dnf && pp.empty()) {
       // fast path: dense [n, count] outputs written in parallel
       Tensor oid(DType::kUInt64, {n * count}), ow(DType::kFloat, {n * count}), ot(DType::kInt32, {n * count});
@@ -492,6 +524,37 @@ class SampleNeighborOp : public OpKernel {
       }
     });
     EmitNeighbors(nd, ctx, rows);
+  }
+};
+
+class SampleNodeAtOp : public OpKernel {
+ public:
+  void Compute(const NodeDef& nd, OpContext* ctx) override {
+    Graph& g = G(ctx);
+    if (nd.attrs.size() < 3) EULER_THROW("API_SAMPLE_NODE_AT needs [node_type, buckets, key, (default)]");
+    auto codes = IdsOf(ctx->Get(nd.inputs.at(0)));
+    const int type = static_cast<int>(ctx->AttrInt(nd.attrs[0]));
+    const uint64_t B = static_cast<uint64_t>(ctx->AttrInt(nd.attrs[1]));
+    const uint64_t key = static_cast<uint64_t>(ctx->AttrInt(nd.attrs[2]));
+    const uint64_t def = nd.attrs.size() > 3 ? static_cast<uint64_t>(ctx->AttrInt(nd.attrs[3])) : kDefaultNode;
+    if (B == 0) EULER_THROW("API_SAMPLE_NODE_AT: zero buckets");
+    std::vector<uint64_t> out(codes.size());
+    for (size_t i = 0; i < codes.size(); ++i) {
+      Rng rng(key, 2 * (codes[i] / B) + 1);
+      out[i] = g.SampleNodeInBucket(type, B, codes[i] % B, rng, def);
+    }
+    ctx->Set(nd.Output(0), Tensor::FromVector(out));
+  }
+};
+
+class NodeBucketWeightOp : public OpKernel {
+ public:
+  void Compute(const NodeDef& nd, OpContext* ctx) override {
+    Graph& g = G(ctx);
+    if (nd.attrs.size() < 2) EULER_THROW("API_NODE_BUCKET_WEIGHT needs [node_type, buckets]");
+    const int type = static_cast<int>(ctx->AttrInt(nd.attrs[0]));
+    const uint64_t B = static_cast<uint64_t>(ctx->AttrInt(nd.attrs[1]));
+    ctx->Set(nd.Output(0), Tensor::FromVector(g.NodeBucketWeights(type, B)));
   }
 };
 
@@ -642,6 +705,8 @@ REGISTER_OP_KERNEL("API_GET_NB_NODE", GetOutNeighborOp);
 REGISTER_OP_KERNEL("API_GET_RNB_NODE", GetInNeighborOp);
 REGISTER_OP_KERNEL("API_GET_NB_EDGE", GetNeighborEdgeOp);
 REGISTER_OP_KERNEL("API_SAMPLE_NB", SampleNeighborOp);
+REGISTER_OP_KERNEL("API_SAMPLE_NODE_AT", SampleNodeAtOp);
+REGISTER_OP_KERNEL("API_NODE_BUCKET_WEIGHT", NodeBucketWeightOp);
 REGISTER_OP_KERNEL("API_GET_EDGE_SUM_WEIGHT", EdgeSumWeightOp);
 REGISTER_OP_KERNEL("API_SAMPLE_L", SampleLayerOp);
 REGISTER_OP_KERNEL("API_SPARSE_GET_ADJ", SparseGetAdjOp);

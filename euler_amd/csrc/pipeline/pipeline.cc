@@ -4,6 +4,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
 
 #include "rpc/rpc.h"
 
@@ -73,16 +74,47 @@ SageSlotLayout SageSlotLayout::Make(const SageBatchSpec& s) {
 
 namespace {
 
-// the in-process shard: direct column / CSR reads, sampling from the batch's stream
+// the bucket half of a keyed root draw: an alias table over the global bucket weights
+// (built once, on first use, from whatever source knows them)
+class KeyedRootTable {
+ public:
+  template <typename Fn>
+  void Ensure(Fn weights) {
+    std::call_once(once_, [&] {
+      std::vector<double> w = weights();
+      double t = 0;
+      for (double x : w) t += x;
+      ok_ = t > 0;
+      if (ok_) alias_.Init(w.data(), w.size());
+    });
+  }
+  // bucket of root i, or -1 when the node type has no weight
+  int64_t Bucket(uint64_t key, int64_t i) const {
+    if (!ok_) return -1;
+    Rng rng(key, 2 * static_cast<uint64_t>(i));
+    return alias_.Sample(rng);
+  }
+
+ private:
+  std::once_flag once_;
+  bool ok_ = false;
+  AliasTable alias_;
+};
+
+// the in-process shard: direct column / CSR reads, keyed sampling
 class LocalSource : public SageSource {
  public:
-  explicit LocalSource(const Graph* g) : g_(*g) {}
+  explicit LocalSource(const Graph* g) : g_(*g), buckets_(KeyedBuckets(g->meta().partitions_num)) {}
 
-  void Roots(const SageBatchSpec& s, Rng& rng, int64_t* roots, float* labels) override {
-    std::vector<uint64_t> r;
-    g_.SampleNode(s.node_type, s.batch, rng, &r);
-    for (int i = 0; i < s.batch; ++i)
-      roots[i] = i < static_cast<int>(r.size()) ? static_cast<int64_t>(r[i]) : s.default_node;
+  void Roots(const SageBatchSpec& s, uint64_t key, int64_t* roots, float* labels) override {
+    table_.Ensure([&] { return g_.NodeBucketWeights(s.node_type, buckets_); });
+    for (int i = 0; i < s.batch; ++i) {
+      const int64_t b = table_.Bucket(key, i);
+      Rng rng(key, 2 * static_cast<uint64_t>(i) + 1);
+      roots[i] = b < 0 ? s.default_node
+                       : static_cast<int64_t>(g_.SampleNodeInBucket(s.node_type, buckets_, b, rng,
+                                                                    static_cast<uint64_t>(s.default_node)));
+    }
     if (s.label_dim <= 0) return;
     const Column<float>* lc = s.label_idx >= 0 ? g_.NodeDense(s.label_idx) : nullptr;
     for (int i = 0; i < s.batch; ++i) {
@@ -96,14 +128,15 @@ class LocalSource : public SageSource {
     }
   }
 
-  void Hop(const SageBatchSpec& s, int hop, const int64_t* ids, int64_t n, Rng& rng, int64_t* out) override {
+  void Hop(const SageBatchSpec& s, int hop, const int64_t* ids, int64_t n, uint64_t key, int64_t* out) override {
     const int k = s.fanouts[hop - 1];
-    std::vector<IdWeightType> tmp;
-    for (int64_t i = 0; i < n; ++i) {
-      g_.SampleNeighbor(g_.Row(static_cast<uint64_t>(ids[i])), s.etypes[hop - 1], k, true, rng, &tmp);
-      for (int j = 0; j < k; ++j)
-        out[i * k + j] = j < static_cast<int>(tmp.size()) ? static_cast<int64_t>(tmp[j].id) : s.default_node;
-    }
+    const uint64_t* u = reinterpret_cast<const uint64_t*>(ids);
+    std::vector<uint32_t> occ;
+    KeyedOccurrences(u, n, &occ);
+    std::vector<int32_t> et = s.etypes[hop - 1];
+    if (et.size() == 1 && et[0] < 0) et.clear();
+    SampleNeighborsKeyed(g_, u, occ.data(), n, et, k, key, static_cast<uint64_t>(s.default_node),
+                         reinterpret_cast<uint64_t*>(out), nullptr, nullptr);
   }
 
   void Features(const SageBatchSpec& s, const int64_t* ids, int64_t n, int64_t fd, float* out) override {
@@ -128,6 +161,8 @@ class LocalSource : public SageSource {
 
  private:
   const Graph& g_;
+  const uint64_t buckets_;
+  KeyedRootTable table_;
 };
 
 // ragged (idx [n][2], flat data) -> dense rows [n][w], zero / default padded
@@ -145,13 +180,37 @@ void DenseFromRagged(const Tensor& idx, const T* data, int64_t n, int64_t w, T p
 // the shard servers, through the session's distribute-mode plans (see pipeline.h)
 class RemoteSource : public SageSource {
  public:
-  explicit RemoteSource(QueryProxy* q) : q_(q) {}
+  explicit RemoteSource(QueryProxy* q) : q_(q), buckets_(KeyedBuckets(q->env()->num_partitions)) {}
 
-  void Roots(const SageBatchSpec& s, Rng&, int64_t* roots, float* labels) override {
+  void Roots(const SageBatchSpec& s, uint64_t key, int64_t* roots, float* labels) override {
+    // bucket weights once: every shard reports its buckets (zeros elsewhere), summed here
+    table_.Ensure([&] {
+      std::vector<Tensor> res;
+      Check(q_->RunOp("API_NODE_BUCKET_WEIGHT", {}, {std::to_string(s.node_type), std::to_string(buckets_)}, 1, {},
+                      &res),
+            "bucket weights");
+      std::vector<double> w(buckets_, 0.0);
+      const double* p = res[0].data<double>();
+      for (int64_t j = 0; j < res[0].numel(); ++j) w[j % buckets_] += p[j];
+      return w;
+    });
+    // codes pos * buckets + bucket: the owning shard draws the node with Philox (key, 2 pos + 1)
+    std::vector<uint64_t> codes;
+    std::vector<int> at;
+    for (int i = 0; i < s.batch; ++i) {
+      const int64_t b = table_.Bucket(key, i);
+      roots[i] = s.default_node;
+      if (b < 0) continue;
+      codes.push_back(static_cast<uint64_t>(i) * buckets_ + b);
+      at.push_back(i);
+    }
     std::vector<std::pair<std::string, Tensor>> in = {
+        {"codes", Tensor::FromVector(codes)},
         {"node_type", Tensor::FromVector(std::vector<int32_t>{s.node_type})},
-        {"count", Tensor::FromVector(std::vector<int64_t>{s.batch})}};
-    std::string gql = "sampleN(node_type, count).as(r)";
+        {"nb_buckets", Tensor::FromVector(std::vector<int64_t>{static_cast<int64_t>(buckets_)})},
+        {"nb_key", Tensor::FromVector(std::vector<int64_t>{static_cast<int64_t>(key)})}};
+    std::string gql = "v(codes).sampleNodeAt(node_type, nb_buckets, nb_key, " + std::to_string(s.default_node) +
+                      ").as(r)";
     std::vector<std::string> outs = {"r:0"};
     const bool lab = s.label_dim > 0 && !s.label_name.empty();
     if (lab) {
@@ -163,23 +222,34 @@ class RemoteSource : public SageSource {
     std::vector<Tensor> res;
     Check(q_->Run(gql, in, outs, &res), "roots");
     const std::vector<int64_t> r = res[0].ToInt64();
-    for (int i = 0; i < s.batch; ++i) roots[i] = i < static_cast<int>(r.size()) ? r[i] : s.default_node;
+    for (size_t j = 0; j < at.size() && j < r.size(); ++j) roots[at[j]] = r[j];
     if (s.label_dim > 0) {
-      if (lab) DenseFromRagged<float>(res[1], res[2].data<float>(), s.batch, s.label_dim, 0.f, labels);
-      else memset(labels, 0, sizeof(float) * s.batch * s.label_dim);
+      memset(labels, 0, sizeof(float) * s.batch * s.label_dim);
+      if (lab) {
+        std::vector<float> l(at.size() * s.label_dim);
+        DenseFromRagged<float>(res[1], res[2].data<float>(), static_cast<int64_t>(at.size()), s.label_dim, 0.f,
+                               l.data());
+        for (size_t j = 0; j < at.size(); ++j)
+          memcpy(labels + at[j] * s.label_dim, l.data() + j * s.label_dim, sizeof(float) * s.label_dim);
+      }
     }
   }
 
-  void Hop(const SageBatchSpec& s, int hop, const int64_t* ids, int64_t n, Rng&, int64_t* out) override {
+  void Hop(const SageBatchSpec& s, int hop, const int64_t* ids, int64_t n, uint64_t key, int64_t* out) override {
     const int k = s.fanouts[hop - 1];
     std::vector<uint64_t> u(ids, ids + n);
     std::vector<int32_t> et = s.etypes[hop - 1];
     if (et.empty()) et.push_back(-1);
     std::vector<std::pair<std::string, Tensor>> in = {{"nodes", Tensor::FromVector(u)},
                                                        {"edge_types", Tensor::FromVector(et)},
-                                                       {"nb_count", Tensor::FromVector(std::vector<int64_t>{k})}};
+                                                       {"nb_count", Tensor::FromVector(std::vector<int64_t>{k})},
+                                                       {"nb_key", Tensor::FromVector(std::vector<int64_t>{
+                                                                      static_cast<int64_t>(key)})}};
     std::vector<Tensor> res;
-    const std::string gql = "v(nodes).sampleNB(edge_types, nb_count, " + std::to_string(s.default_node) + ").as(nb)";
+    // keyed: the owning shard draws id's neighbours with Philox (key, KeyedStream(id, occurrence));
+    // the split keeps each shard's ids in request order, so occurrences match the full list
+    const std::string gql =
+        "v(nodes).sampleNB(edge_types, nb_count, " + std::to_string(s.default_node) + ", nb_key).as(nb)";
     Check(q_->Run(gql, in, {"nb:0", "nb:1"}, &res), "sampleNB");
     const std::vector<int64_t> flat = res[1].ToInt64();
     DenseFromRagged<int64_t>(res[0], flat.data(), n, k, s.default_node, out);
@@ -215,6 +285,8 @@ class RemoteSource : public SageSource {
     if (!st.ok()) EULER_THROW("SagePipeline remote " << what << ": " << st.ToString());
   }
   QueryProxy* q_;
+  const uint64_t buckets_;
+  KeyedRootTable table_;
 };
 
 }  // namespace
@@ -307,10 +379,9 @@ void SagePipeline::Fill(int slot, uint64_t seq) {
   int64_t* I = ints_[slot];
   float* Fp = floats_[slot];
   const int L = static_cast<int>(s.fanouts.size());
-  Rng rng(seed_, seq);
   // roots (+ labels)
   int64_t* lvl0 = I + 16;
-  src_->Roots(s, rng, lvl0, s.label_dim > 0 ? Fp + lay.off_labels : nullptr);
+  src_->Roots(s, KeyedKey(seed_, seq, 0), lvl0, s.label_dim > 0 ? Fp + lay.off_labels : nullptr);
   I[0] = L;
   I[1] = s.batch;
   // hops
@@ -322,7 +393,7 @@ void SagePipeline::Fill(int slot, uint64_t seq) {
     const int k = s.fanouts[h - 1];
     cat.resize(static_cast<size_t>(n * k + n));
     inv.resize(cat.size());
-    src_->Hop(s, h, cur, n, rng, cat.data());
+    src_->Hop(s, h, cur, n, KeyedKey(seed_, seq, h), cat.data());
     std::copy(cur, cur + n, cat.begin() + n * k);
     int64_t* nid = I + lay.off_nid[h];
     int64_t nu = 0;

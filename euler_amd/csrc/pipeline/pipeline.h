@@ -8,8 +8,8 @@
 // list + self loops), the dense input features of the outermost node set and the roots'
 // labels — straight into caller-provided (pinned) slot buffers of fixed capacity.  Slots
 // circulate free -> filling -> ready -> consumer -> free; batches are delivered in sequence
-// order and batch b draws from the Philox stream (seed, b), so the stream of batches is
-// reproducible for any worker count.
+// order and batch b draws from the Philox keys KeyedKey(seed, b, hop) (graph.h), so the
+// stream of batches is reproducible for any worker count and any graph placement.
 #pragma once
 
 #include <stdint.h>
@@ -41,21 +41,24 @@ struct SageBatchSpec {
   std::string label_name;
 };
 
-// Where a batch's graph lookups go.  LocalSource: the in-process shard (batch b draws from
-// the Philox stream (seed, b): reproducible for any worker count).  RemoteSource: the
+// Where a batch's graph lookups go.  LocalSource: the in-process shard.  RemoteSource: the
 // shard servers, through the session's compiled distribute-mode plans — per batch one
 // roots (+ labels) query, one sampleNB query per hop over the hop's unique frontier and
 // one values() query for the outermost node set; each query is one RPC per shard
 // (split -> REMOTE -> merge, REMOTE fusion), issued by the worker thread that owns the
-// batch, so W workers keep W batches of RPCs in flight.  Remote sampling draws from the
-// servers' generators (not the batch's stream).
+// batch, so W workers keep W batches of RPCs in flight.
+// Both draw with the keyed samplers of graph.h: batch b, hop h uses the Philox key
+// KeyedKey(seed, b, h), roots go through the virtual node buckets and neighbour draws are
+// keyed by (id, occurrence), so a batch is the same for any worker count and whether the
+// graph is in-process or on any number of shard servers (the remote side runs the same
+// code: API_SAMPLE_NODE_AT, keyed API_SAMPLE_NB).
 class SageSource {
  public:
   virtual ~SageSource() = default;
   // roots [batch] and, with label_dim > 0, their labels [batch][label_dim]
-  virtual void Roots(const SageBatchSpec& s, Rng& rng, int64_t* roots, float* labels) = 0;
+  virtual void Roots(const SageBatchSpec& s, uint64_t key, int64_t* roots, float* labels) = 0;
   // k neighbour draws per id (default_node where none), out [n * k]
-  virtual void Hop(const SageBatchSpec& s, int hop, const int64_t* ids, int64_t n, Rng& rng, int64_t* out) = 0;
+  virtual void Hop(const SageBatchSpec& s, int hop, const int64_t* ids, int64_t n, uint64_t key, int64_t* out) = 0;
   // dense input features [n][feat_dim] (zero-filled when missing)
   virtual void Features(const SageBatchSpec& s, const int64_t* ids, int64_t n, int64_t feat_dim, float* out) = 0;
 };

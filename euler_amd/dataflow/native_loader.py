@@ -15,8 +15,10 @@ with one GQL op per hop plus one per feature (tf_euler/kernels/
 sample_fanout_with_feature_op.cc:43-69, get_dense_feature_op.cc:89-116) serially with
 the step; the round-1 Python prefetcher called ``pin_memory()`` on every batch.
 
-Batch b is drawn from the Philox stream (seed, b) and delivered in order, so the batch
-stream is reproducible for any worker count.
+Batch b is drawn with the keyed samplers (Philox key (seed, b, hop); roots through virtual
+node buckets, neighbours keyed by (id, occurrence); csrc/graph/keyed.cc) and delivered in
+order, so the batch stream is reproducible for any worker count and identical whether the
+graph is in-process or on shard servers.
 
 Remote sessions (``initialize_shared_graph``; also ``local_sharded``): the same workers
 build the batch through the session's distribute-mode GQL plans — one roots (+ labels)
@@ -24,8 +26,8 @@ query, one ``sampleNB`` query per hop over the hop's unique frontier and one ``v
 query for the outermost nodes, each one RPC per shard (csrc/pipeline/pipeline.cc
 RemoteSource; reference tf_euler/kernels/sample_fanout_with_feature_op.cc:43-69 +
 euler/core/kernels/remote_op.cc:60-146) — so W workers keep W batches of RPCs in flight
-and the step still only consumes ready slots.  Remote draws come from the servers'
-generators.
+and the step still only consumes ready slots.  The servers draw with the batch's keys
+(``sampleNodeAt`` / keyed ``sampleNB``), so a remote batch equals the local one.
 
 Static mode (``static=True``, GPU only) serves every batch through ONE set of
 fixed-capacity device tensors, the inputs of a graph-captured training step

@@ -298,6 +298,12 @@ class BaseEstimator:
         # this thread runs the current step (utils/prefetch.py); params["prefetch"] = 0
         # turns it off
         prefetcher = self._native_pipeline()
+        if prefetcher is not None:
+            # every step's batch comes from the native pipeline (``first`` only materialised
+            # the model): its keyed draws make the batch stream identical for an in-process
+            # and a sharded remote graph
+            pending = None
+        eager_first = True
         depth = int(self.params.get("prefetch", 2 if self.device.type == "cuda" else 0))
         if prefetcher is None and depth > 0 and callable(getattr(self.model, "prepare", None)):
             prefetcher = Prefetcher(lambda: self.model.prepare(self.get_train_from_input(inputs, self.params)),
@@ -324,7 +330,7 @@ class BaseEstimator:
                     source = prefetcher.get()
                 else:
                     source = self.get_train_from_input(inputs, self.params)
-            if graphed is not None and source is not first:
+            if graphed is not None and not eager_first:
                 # graph-captured step over the pipeline's static inputs (estimator/graph_step.py);
                 # drop the eager step's autograd graph first
                 _ = loss = obj = extra = metric = None
@@ -338,6 +344,7 @@ class BaseEstimator:
                     self.save()
                 continue
             pending = None
+            eager_first = False
             with rng("forward"):
                 _, loss, metric_name, metric = self._run_model(source)
                 extra = self._extra_losses()
