@@ -198,7 +198,7 @@ class TreePlan {
       TORCH_CHECK(k >= 0 && k < opt_.nseg, "opt_segments: segment index out of range");
       TrSeg s = opt_.seg[k];
       s.blk0 = blk;
-      blk += s.cols > 0 ? (s.rows / 8) * (s.cols / 32) : static_cast<int>((s.n + 255) / 256);
+      blk += tr_seg_prepare(s);
       a.seg[n++] = s;
     }
     a.nseg = n;
@@ -604,7 +604,7 @@ class TreePlan {
         s.S = static_cast<int32_t>(B_ / kTrHeadRows);
         s.rows = 1;
         s.cols = 0;
-        blk += static_cast<int>((s.n + 255) / 256);
+        blk += tr_seg_prepare(s);
         continue;
       }
       const int pi = k < L_ ? k : (k == L_ ? L_ : L_ + 1);
@@ -626,7 +626,7 @@ class TreePlan {
         s.sh = bf("Wout_sh", (int64_t)C_ * E_);
         s.shT = bf("Wout_shT", (int64_t)C_ * E_);
       }
-      blk += (s.rows / 8) * (s.cols / 32);
+      blk += tr_seg_prepare(s);
     }
     a.nseg = seg;
     a.nblk = blk;
@@ -782,7 +782,7 @@ class TowerPlan {
     sg.sh = const_cast<uint16_t*>(a.W);
     sg.shT = nullptr;
     o.nseg = 1;
-    o.nblk = static_cast<int32_t>((H_ / 8) * (2 * D_ / 32));
+    o.nblk = tr_seg_prepare(sg);
     dummy_ = torch::zeros({8}, torch::TensorOptions().dtype(torch::kFloat32).device(dev_));
     step_ = torch::zeros({1}, torch::TensorOptions().dtype(torch::kInt64).device(dev_));
     o.step = step_.data_ptr<int64_t>();
@@ -1086,12 +1086,9 @@ class PairPlan {
     g.blk0 = blk;
     g.sh = sh;
     g.shT = shT;
-    if (cols > 0) {
+    if (cols > 0)
       TORCH_CHECK(rows % 8 == 0 && cols % 32 == 0, "PairPlan: weight segments need rows % 8, cols % 32");
-      blk += static_cast<int>((rows / 8) * (cols / 32));
-    } else {
-      blk += static_cast<int>((g.n + 255) / 256);
-    }
+    blk += tr_seg_prepare(g);
   }
 
   bool has(const char* k) const { return d_.contains(k) && !d_[k].is_none(); }

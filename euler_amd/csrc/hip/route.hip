@@ -5,9 +5,12 @@
 // slot W * C.  Replaces a sort by owner + a dozen index ops (~350 us per DeepWalk step at
 // 700K ids, profiles/r2_mid/deepwalk_modes) with two passes over the ids:
 //   count : per 2048-id chunk, ids per owner (LDS atomics)
-//   place : per chunk, the owners' bases = sums of the earlier chunks' counts; then 8 rounds
-//           of 256 ids in order: per wave and owner a ballot gives the lane prefix and the
-//           wave count, waves are combined through LDS, the running count carries on.
+//   scan  : per owner, the exclusive prefix of its counts over the chunks (in place): a
+//           chunk's base for an owner is one load, not a sum over every earlier chunk (that
+//           grew with the square of the chunk count)
+//   place : per chunk, the owners' bases from the scan; then 8 rounds of 256 ids in order:
+//           per wave and owner a ballot gives the lane prefix and the wave count, waves are
+//           combined through LDS, the running count carries on.
 // Owners W <= 63 (a ballot per owner bin per round).
 // self_rank >= 0: the caller's own block goes LAST and the peers' blocks keep rank order
 // (block of owner o: o < self ? o : o > self ? o - 1 : W - 1), so the peers' slots are one
@@ -40,6 +43,33 @@ __global__ __launch_bounds__(kRouteThreads) void route_count_kernel(const int64_
   if (threadIdx.x < NB) cnt[static_cast<int64_t>(blockIdx.x) * NB + threadIdx.x] = c[threadIdx.x];
 }
 
+// one block per owner bin: exclusive prefix of cnt[.][q] over the chunks, in place
+__global__ __launch_bounds__(kRouteThreads) void route_scan_kernel(int32_t* __restrict__ cnt, int64_t nchunks,
+                                                                    int NB) {
+  __shared__ int32_t part[kRouteThreads / 64];
+  const int q = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  int32_t running = 0;
+  for (int64_t t0 = 0; t0 < nchunks; t0 += kRouteThreads) {
+    const int64_t k = t0 + tid;
+    const int32_t v = k < nchunks ? cnt[k * NB + q] : 0;
+    int32_t x = v;  // inclusive wave scan
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int32_t y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) part[wave] = x;
+    __syncthreads();
+    int32_t before = running;
+    for (int w = 0; w < wave; ++w) before += part[w];
+    if (k < nchunks) cnt[k * NB + q] = before + x - v;
+    int32_t tile = 0;
+    for (int w = 0; w < kRouteThreads / 64; ++w) tile += part[w];
+    running += tile;
+    __syncthreads();  // part[] is rewritten by the next tile
+  }
+}
+
 __device__ __forceinline__ int64_t route_block(int b, int W, int self_rank) {
   if (self_rank < 0) return b;
   return b < self_rank ? b : (b > self_rank ? b - 1 : W - 1);
@@ -56,13 +86,8 @@ __global__ __launch_bounds__(kRouteThreads) void route_place_kernel(const int64_
   const int NB = W + 1;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int blk = static_cast<int>(blockIdx.x);
-  if (tid < NB) run[tid] = 0;
-  __syncthreads();
-  // bases: the earlier chunks' counts of every owner
-  for (int k = tid; k < blk * NB; k += kRouteThreads) {
-    const int32_t v = cnt[k];
-    if (v) atomicAdd(&run[k % NB], v);
-  }
+  // bases: the earlier chunks' counts of every owner (route_scan_kernel)
+  if (tid < NB) run[tid] = cnt[static_cast<int64_t>(blk) * NB + tid];
   const int64_t trash = static_cast<int64_t>(W) * C;
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   bool over = false;
@@ -119,6 +144,8 @@ hipError_t eh_route_by_owner(const int64_t* ids, int64_t n, int W, int64_t C, in
   if (W < 1 || W + 1 > kRouteMaxBins || C < 1 || self_rank >= W) return hipErrorInvalidValue;
   const uint32_t nb = static_cast<uint32_t>(ceil_div(n, kRouteChunk));
   hipLaunchKernelGGL(route_count_kernel, dim3(nb), dim3(kRouteThreads), 0, s, ids, n, W, cnt);
+  hipLaunchKernelGGL(route_scan_kernel, dim3(static_cast<uint32_t>(W + 1)), dim3(kRouteThreads), 0, s, cnt,
+                     static_cast<int64_t>(nb), W + 1);
   hipLaunchKernelGGL(route_place_kernel, dim3(nb), dim3(kRouteThreads), 0, s, ids, n, W, C, self_rank, cnt, pos,
                      send, overflow);
   return hipGetLastError();

@@ -1869,6 +1869,9 @@ __device__ __forceinline__ void tr_opt_tile(const TrOptArgs& a, int b, float (*t
   int64_t i;
   int r = 0, c = 0;
   bool valid = true;
+  // vector segment with slab groups (tr_seg_prepare): thread = (group, element); uniform per block
+  const int grp = sg.cols == 0 && sg.sgrp > 1 ? sg.sgrp : 1;
+  const int per = 256 / grp, sub = tid / per;
   if (sg.cols > 0) {  // 8 x 32 tile of a weight matrix
     const int tiles_c = sg.cols >> 5;
     const int tr = local / tiles_c, tc = local - tr * tiles_c;
@@ -1876,9 +1879,10 @@ __device__ __forceinline__ void tr_opt_tile(const TrOptArgs& a, int b, float (*t
     c = tc * 32 + (tid & 31);
     i = sg.off + static_cast<int64_t>(r) * sg.cols + c;
   } else {
-    i = sg.off + static_cast<int64_t>(local) * 256 + tid;
+    i = sg.off + static_cast<int64_t>(local) * per + (tid - sub * per);
     valid = i < sg.off + sg.n;
     if (!valid) i = sg.off;  // clamped: no early return before the tile barrier
+    valid = valid && sub == 0;  // groups 1.. only help with the slab sum
   }
   float p = a.p[i];
   // optimizer slots loaded up front: independent of the split-K sum, so their latency
@@ -1895,12 +1899,24 @@ __device__ __forceinline__ void tr_opt_tile(const TrOptArgs& a, int b, float (*t
       // flight measured slower: 9.38 vs 8.75 us, profiles/r3_headline/)
       const float* src = sg.part + (i - sg.off);
       g = 0.f;
-      for (int s0 = 0; s0 < sg.S; s0 += 16) {
+      // slabs sub, sub + grp, ... (grp == 1: all of them, in order)
+      for (int s0 = sub; s0 < sg.S; s0 += 16 * grp) {
         float v[16];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) v[u] = src[static_cast<int64_t>(s0 + u < sg.S ? s0 + u : sg.S - 1) * sg.n];
+        for (int u = 0; u < 16; ++u) {
+          const int sl = s0 + u * grp;
+          v[u] = src[static_cast<int64_t>(sl < sg.S ? sl : sg.S - 1) * sg.n];
+        }
 #pragma unroll
-        for (int u = 0; u < 16; ++u) g += (s0 + u < sg.S) ? v[u] : 0.f;
+        for (int u = 0; u < 16; ++u) g += (s0 + u * grp < sg.S) ? v[u] : 0.f;
+      }
+      if (grp > 1) {  // the groups' sums, in group order (deterministic)
+        float* red = &tile_s[0][0];
+        red[tid] = g;
+        __syncthreads();
+        const int e = tid - sub * per;
+        g = red[e];
+        for (int q = 1; q < grp; ++q) g += red[q * per + e];
       }
       if (MODE == 0) {
         if (valid) {
@@ -2222,11 +2238,10 @@ hipError_t eh_tr_opt(const TrOptArgs* ain, int mode, hipStream_t s) {
     if (g.cols > 0) {
       if (g.rows % 8 != 0 || g.cols % 32 != 0 || static_cast<int64_t>(g.rows) * g.cols != g.n)
         return hipErrorInvalidValue;
-      blk += (g.rows / 8) * (g.cols / 32);
     } else {
-      if (g.sh || g.shT) return hipErrorInvalidValue;
-      blk += static_cast<int>(ceil_div(g.n, 256));
+      if (g.sh || g.shT || g.sgrp != tr_seg_groups(g)) return hipErrorInvalidValue;  // tr_seg_prepare
     }
+    blk += tr_seg_blocks(g);
   }
   if (blk != a->nblk) return hipErrorInvalidValue;
   int extra = 0;

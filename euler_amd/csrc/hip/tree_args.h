@@ -197,7 +197,22 @@ struct TrSeg {
   int32_t blk0;        // first block of the segment
   uint16_t* sh;        // optional fm [rows][cols]
   uint16_t* shT;       // optional fm [cols][rows]
+  int32_t sgrp;        // vector segments: slab groups per element (1 or 4; tr_seg_prepare)
 };
+// vector segments with many split-K slabs (the fc bias: one slab per head block) spread each
+// element's slab sum over 4 threads (256 / 4 elements per block): one round of 16 loads in
+// flight per thread instead of S / 16 dependent rounds, which made the bias block the tail
+// of the optimizer launch.  Returns the segment's block count.
+inline int tr_seg_groups(const TrSeg& s) { return s.cols == 0 && s.S > 16 ? 4 : 1; }
+inline int tr_seg_blocks(const TrSeg& s) {
+  if (s.cols > 0) return (s.rows / 8) * (s.cols / 32);
+  const int64_t per = 256 / tr_seg_groups(s);
+  return static_cast<int>((s.n + per - 1) / per);
+}
+inline int tr_seg_prepare(TrSeg& s) {
+  s.sgrp = tr_seg_groups(s);
+  return tr_seg_blocks(s);
+}
 struct TrOptArgs {
   float *p, *g, *m, *v;
   uint16_t* g16;  // optional bf16 gradient (data parallel: the all-reduce moves half the bytes);

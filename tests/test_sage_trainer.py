@@ -136,6 +136,7 @@ CASES = [
     dict(fanouts=[5, 3], dims=[64, 64, 32], C=32, types=2, metapath=[[0], [0, 1]]),
     dict(fanouts=[4, 3, 2], dims=[64, 64, 64, 32], C=32),                     # 3 hops (inner layer + bwd)
     dict(fanouts=[3, 20, 2], dims=[64, 128, 64, 32], C=16, mode="dense", self_loops=True),
+    dict(fanouts=[5, 3], dims=[64, 64, 32], C=32, B=1024),                    # 64 fc-bias slabs: grouped reduce
 ]
 
 
