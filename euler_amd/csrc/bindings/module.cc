@@ -404,6 +404,45 @@ class Engine {
     return py::make_tuple(indptr, nbr, w, g.num_edge_types(), ids, nw);
   }
 
+  // every edge of `etype` (-1: all) as (src ids, dst ids, weights, dense edge feature
+  // `name` [n][dim] or an empty [n][0] when name is empty), edge-row order, for HBM upload
+  // of a triple table (knowledge-graph trainers)
+  py::tuple ExportEdges(int etype, const std::string& name, int64_t dim) {
+    Graph& g = LocalGraph();
+    const Column<float>* c = nullptr;
+    if (!name.empty()) {
+      const FeatureInfo* fi = g.meta().EdgeFeature(name);
+      if (!fi || fi->type != kDense) throw std::runtime_error("no dense edge feature named " + name);
+      c = g.EdgeDense(fi->idx);
+    } else {
+      dim = 0;
+    }
+    std::vector<int64_t> rows;
+    for (int64_t e = 0; e < g.num_edges(); ++e)
+      if (etype < 0 || g.EdgeType(e) == etype) rows.push_back(e);
+    const int64_t n = static_cast<int64_t>(rows.size());
+    py::array_t<uint64_t> src(n), dst(n);
+    py::array_t<float> w(n);
+    py::array_t<float> feat({n, dim});
+    uint64_t *ps = src.mutable_data(), *pd = dst.mutable_data();
+    float *pw = w.mutable_data(), *pf = feat.mutable_data();
+    for (int64_t i = 0; i < n; ++i) {
+      const int64_t e = rows[i];
+      ps[i] = g.EdgeSrc(e);
+      pd[i] = g.EdgeDst(e);
+      pw[i] = g.EdgeWeight(e);
+      if (dim > 0) {
+        const float* p = nullptr;
+        int64_t k = 0;
+        if (c) c->Get(e, &p, &k);
+        const int64_t m = std::min(k, dim);
+        if (m > 0) memcpy(pf + i * dim, p, m * 4);
+        if (m < dim) memset(pf + i * dim + m, 0, (dim - m) * 4);
+      }
+    }
+    return py::make_tuple(src, dst, w, feat);
+  }
+
   // per-row node ids, types and weights (row order of ExportCsr), for HBM upload
   py::tuple ExportNodes() {
     Graph& g = LocalGraph();
@@ -627,7 +666,8 @@ PYBIND11_MODULE(_engine, m) {
       .def("export_csr", &Engine::ExportCsr)
       .def("endpoints", [](Engine& e) { return e.Endpoints(); })
       .def("set_replicas", &Engine::SetReplicas, py::arg("shard"), py::arg("endpoints"))
-      .def("export_nodes", &Engine::ExportNodes);
+      .def("export_nodes", &Engine::ExportNodes)
+      .def("export_edges", &Engine::ExportEdges, py::arg("edge_type"), py::arg("name") = "", py::arg("dim") = 0);
 
   py::class_<PySagePipeline>(m, "SagePipeline")
       .def(py::init<std::shared_ptr<Engine>, int, int, std::vector<std::vector<int32_t>>, std::vector<int>, int64_t,

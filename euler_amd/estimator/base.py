@@ -411,7 +411,9 @@ class BaseEstimator:
 
     def _device_graph_trainer(self, first):
         """Upload the engine's graph (structure, the model's feature and label columns) to
-        HBM and build the fused device trainer for ``self.model`` (SupervisedGraphSage)."""
+        HBM and build the device trainer for ``self.model``: SupervisedGraphSage (fused
+        kernels), UnsupervisedGraphSage, the full-neighbourhood zoo, or a TransX-family
+        knowledge-graph model (triple table + corruption sampler)."""
         import euler_amd.ops.graph_api as ge
         from euler_amd.graph.device_graph import DeviceGraph
         from euler_amd.models.sage_trainer import SageTrainer
@@ -419,6 +421,19 @@ class BaseEstimator:
         from euler_amd.dataflow.dataflows import GCNDataFlow
 
         model = self.model
+        seed = int(self.params.get("seed") or 0)
+        if hasattr(model, "loss_scores"):
+            # TransE / TransH / TransR / TransD / DistMult (EdgeEstimator): the triple table and
+            # the corruption sampler in HBM, the model's own scores (models/kg_trainer.py)
+            from euler_amd.models.kg_trainer import KGTrainer
+
+            self._prepare(first)
+            if self._sync is not None:
+                self._sync.remove()  # the trainer all-reduces its flat gradient itself
+            edge_type = self.params.get("train_edge_type", getattr(model, "edge_type", -1))
+            return KGTrainer.from_model(model, int(self.params["batch_size"]), edge_type, seed=seed * 7919 + self.rank,
+                                        device=self.device, optimizer=self.params.get("optimizer", "adam"),
+                                        learning_rate=float(self.params.get("learning_rate", 0.001)))
         gnn = getattr(model, "gnn", None)
         unsup = hasattr(model, "context_gnn")
         if gnn is None or not hasattr(gnn, "feature_idx") or not (unsup or hasattr(model, "label_idx")):
@@ -428,7 +443,6 @@ class BaseEstimator:
         nt = self.params.get("train_node_type", -1)
         node_type = -1 if nt in (None, -1, "-1") else int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
         fdt = torch.float32 if self.params.get("device_feature_dtype", "bf16") == "fp32" else torch.bfloat16
-        seed = int(self.params.get("seed") or 0)
         if isinstance(getattr(gnn, "sampler", None), GCNDataFlow):
             # GCN / APPNP / SGCN / TAGCN / ... : full-neighbourhood blocks built on the device
             from euler_amd.models.full_trainer import FullFlowTrainer

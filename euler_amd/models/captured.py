@@ -1,0 +1,174 @@
+"""Shared machinery of the device-path trainers whose step is the user's own torch model.
+
+A subclass supplies :meth:`CapturedTrainer._forward_loss` — draw the step's batch on the
+device (Philox counters of ``self.rng_source``: no host round trip), run the model, return
+the loss and update device-resident metric accumulators.  This class adds the rest of the
+estimator's device-path contract (``estimator/base.py`` ``_train_device_graph``):
+
+* the model's parameters re-homed into one flat fp32 buffer (``parallel/flat.py``), one
+  flat optimizer launch per step (``csrc/hip/optim.hip``) and an optional gradient sync
+  (all-reduce of the flat gradient) between backward and update;
+* warm-up eagerly on a side stream, then several complete steps captured per hipGraph
+  (plus a 1-step graph and graphs of the log / checkpoint remainders), replayed greedily
+  by :meth:`replay_steps`;
+* checkpoints in the model's own parameter names, the optimizer slots and the sampler's
+  (seed, counter).
+
+``rng_source`` is any object with ``rng`` (int64 [2] device tensor: seed, counter),
+``advance()`` and ``reseed_cpu()`` (DeviceGraph has them; so does
+:class:`~euler_amd.models.kg_trainer.TripleTable`).
+"""
+from __future__ import annotations
+
+import torch
+
+from euler_amd.parallel.flat import FlatOptimizer, FlatParams
+
+__all__ = ["CapturedTrainer"]
+
+
+class CapturedTrainer:
+    metric_name = "loss"
+
+    def __init__(self, model, rng_source, device, optimizer="adam", learning_rate=0.01):
+        self.model = model
+        self.rng_source = rng_source
+        self.device = torch.device(device)
+        self.on_gpu = self.device.type == "cuda"
+        model.to(self.device)
+        self._materialize()
+        self.flat = FlatParams([p for p in model.parameters() if p.requires_grad], self.device)
+        self.opt = FlatOptimizer(self.flat, optimizer, learning_rate)
+        self.loss_out = torch.zeros((), device=self.device)
+        self.step_count = 0
+        self._graphs = {}
+        self._graph_exec = None
+        self._samples = None
+
+    # ------------------------------------------------------------------ subclass hooks
+    def _materialize(self):
+        """give lazy layers their shapes before the parameters are flattened"""
+
+    def _forward_loss(self):
+        raise NotImplementedError
+
+    def metric(self) -> float:
+        return float(self.loss_out.item())
+
+    def reset_metric(self):
+        pass
+
+    # ------------------------------------------------------------------ step
+    def _draw(self):
+        """advance the sampler's Philox counter (and re-key the CPU twin's generator)"""
+        src = self.rng_source
+        src.advance()
+        if not self.on_gpu:
+            src.reseed_cpu()
+
+    def _step(self, grad_sync=None):
+        loss = self._forward_loss()
+        self.opt.zero_grad()
+        loss.backward()
+        scale = 1.0
+        if grad_sync is not None:
+            s = grad_sync(self.flat.grad)
+            scale = 1.0 if s is None else float(s)
+        self.opt.step(scale)
+        self.loss_out.copy_(loss.detach())
+        return self.loss_out
+
+    def step(self, grad_sync=None):
+        """one training step (eager; after :meth:`capture`, a replay of the 1-step graph)"""
+        self.step_count += 1
+        if self._graph_exec is not None:
+            self._graph_exec.replay()
+            return self.loss_out
+        return self._step(grad_sync)
+
+    # ------------------------------------------------------------------ hipGraph
+    def capture(self, grad_sync=None, warmup: int = 2, steps: int = 1, extra_sizes=()):
+        """Record ``steps`` complete steps (sampling, model, backward, [all-reduce,]
+        optimizer) into one hipGraph after ``warmup`` eager steps on a side stream; graphs of
+        1 step and of each ``extra_sizes`` entry are kept too (:meth:`replay_steps`)."""
+        if not self.on_gpu:
+            return None
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self.step_count += 1
+                self._step(grad_sync)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        self.flat.rebind_grads()
+        self._graphs = {}
+        for k in sorted({1, int(steps)} | {int(e) for e in extra_sizes if int(e) > 0}, reverse=True):
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr, capture_error_mode="thread_local"):
+                for _ in range(k):
+                    self._step(grad_sync)
+            self._graphs[k] = gr
+        self._graph_exec = self._graphs[1]
+        return self._graphs[int(steps)]
+
+    def replay(self, n: int = 1):
+        for _ in range(int(n)):
+            self._graph_exec.replay()
+        self.step_count += int(n)
+
+    def replay_steps(self, n: int):
+        left = int(n)
+        for k in sorted(self._graphs, reverse=True):
+            while left >= k:
+                self._graphs[k].replay()
+                left -= k
+        self.step_count += int(n)
+
+    def release_graphs(self):
+        for gr in self._graphs.values():
+            gr.reset()
+        self._graphs = {}
+        self._graph_exec = None
+
+    # ------------------------------------------------------------------ state
+    @property
+    def loss(self):
+        return self.loss_out
+
+    def samples(self):
+        return self._samples
+
+    def state_dict(self):
+        return {k: v.detach().cpu() for k, v in self.model.state_dict().items()}
+
+    def logical_params(self):
+        return {k: v.detach().clone() for k, v in self.model.state_dict().items()}
+
+    def load_logical(self, sd):
+        with torch.no_grad():
+            own = self.model.state_dict()
+            for k, v in sd.items():
+                if k in own:
+                    own[k].copy_(torch.as_tensor(v).to(own[k]))
+
+    def write_to_model(self, model):
+        if model is not self.model:
+            model.load_state_dict(self.model.state_dict())
+
+    def trainer_state(self):
+        return {"m": self.opt.m.cpu().clone(), "v": self.opt.v.cpu().clone(),
+                "step": int(self.opt.step_count.item()), "rng": self.rng_source.rng.detach().cpu().clone()}
+
+    def load_trainer_state(self, st):
+        self.opt.m.copy_(torch.as_tensor(st["m"]).to(self.opt.m))
+        self.opt.v.copy_(torch.as_tensor(st["v"]).to(self.opt.v))
+        self.opt.step_count.fill_(int(st["step"]))
+        self.rng_source.rng.copy_(torch.as_tensor(st["rng"]).to(self.rng_source.rng))
+        self.step_count = int(st["step"])
+
+    def dp_state_tensors(self):
+        return [self.flat.flat, self.opt.m, self.opt.v, self.opt.step_count]
+
+    def set_learning_rate(self, lr):
+        self.opt.lr = float(lr)

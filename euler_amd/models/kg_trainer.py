@@ -1,0 +1,150 @@
+"""Device-path training of the knowledge-graph embedding models (TransE / TransH / TransR /
+TransD / DistMult) under ``EdgeEstimator(device_graph=True)``.
+
+Reference: ``euler_estimator/python/edge_estimator.py:27-72`` (``sample_edge(batch,
+train_edge_type)`` batches), ``examples/TransX/transX.py:63-145`` (relation id = the dense
+edge feature ``id``, ``num_negs`` corruptions from ``sample_node(node_type)``, margin loss
+against the mean corrupted score).
+
+The engine path draws every batch on the CPU engine (two GQL queries and a feature lookup
+per step) and copies it to the GPU.  Here the triple table lives in HBM and the step is
+device-only:
+
+* :class:`TripleTable` — every edge of the training edge type (src id, dst id, relation
+  id from the edge feature) plus two Walker alias tables: edges by edge weight (the
+  reference ``sample_edge``) and candidate corruptions by node weight over the model's
+  ``node_type`` (the reference ``sample_node``); draws are the ``alias_sample`` kernel on
+  Philox streams (seed, counter, stream) — stream 1 triples, stream 2 corruptions;
+* the model's own ``loss_scores`` (the fused ``kg_score`` kernels for TransE / DistMult,
+  the torch compositions for the projected variants), the metric (MRR / MR / hit@10 of the
+  positive among its corruptions) accumulated on the device;
+* one flat optimizer launch over every table and parameter (``models/captured.py``),
+  several steps per hipGraph replay.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from euler_amd.graph.device_graph import build_alias_table
+from euler_amd.models.captured import CapturedTrainer
+from euler_amd.ops._native import hip, use_hip
+
+__all__ = ["TripleTable", "KGTrainer"]
+
+
+class _Alias:
+    def __init__(self, weights, device):
+        w = np.asarray(weights, np.float64)
+        if w.size == 0 or not (w > 0).any():
+            raise ValueError("nothing to sample (empty set or all weights zero)")
+        prob, alias = build_alias_table(w)
+        self.prob = torch.from_numpy(prob).to(device)
+        self.alias = torch.from_numpy(alias).to(device)
+
+
+class TripleTable:
+    """Training triples + the edge / corruption samplers in HBM, keyed by a device
+    (seed, counter) pair."""
+
+    def __init__(self, src, dst, rel, edge_weights, cand_ids, cand_weights, seed=0, device="cuda"):
+        self.device = torch.device(device)
+        self.src = torch.as_tensor(np.asarray(src, np.int64)).to(self.device)
+        self.dst = torch.as_tensor(np.asarray(dst, np.int64)).to(self.device)
+        self.rel = torch.as_tensor(np.asarray(rel, np.int64)).to(self.device)
+        self.edges = _Alias(edge_weights, self.device)
+        self.cand = torch.as_tensor(np.asarray(cand_ids, np.int64)).to(self.device)
+        self.negs = _Alias(cand_weights, self.device)
+        self.rng = torch.tensor([int(seed), 0], dtype=torch.int64, device=self.device)
+        self._cpu_gen = torch.Generator(device="cpu")
+        self._cpu_gen.manual_seed(int(seed))
+
+    @classmethod
+    def from_engine(cls, edge_type, node_type=-1, relation_feature="id", engine=None, seed=0, device="cuda"):
+        """every edge of ``edge_type`` of the engine's local graph; relation ids from the dense
+        edge feature ``relation_feature``; corruption candidates = nodes of ``node_type``"""
+        import euler_amd.ops.graph_api as ge
+        from euler_amd.ops import base
+
+        eng = engine if engine is not None else base.get_engine()
+        et = -1 if edge_type in (None, -1, "-1") else int(np.asarray(ge.get_edge_type_id(edge_type)).reshape(-1)[0])
+        src, dst, w, feat = eng.export_edges(et, "dense_" + str(relation_feature), 1)
+        ids, types, nw = eng.export_nodes()
+        nt = -1 if node_type in (None, -1, "-1") else int(np.asarray(ge.get_node_type_id(node_type)).reshape(-1)[0])
+        keep = np.ones(len(ids), bool) if nt < 0 else np.asarray(types) == nt
+        rel = np.asarray(feat).reshape(-1).astype(np.int64)
+        return cls(np.asarray(src).astype(np.int64), np.asarray(dst).astype(np.int64), rel, np.asarray(w),
+                   np.asarray(ids)[keep].astype(np.int64), np.asarray(nw)[keep], seed=seed, device=device)
+
+    # ------------------------------------------------------------------ randomness
+    def advance(self, inc: int = 1):
+        if use_hip(self.rng):
+            hip().rng_advance(self.rng, int(inc))
+        else:
+            self.rng[1] += inc
+
+    def reseed_cpu(self):
+        self._cpu_gen.manual_seed((int(self.rng[0]) * 1000003 + int(self.rng[1])) % (1 << 63))
+
+    def _draw(self, a: _Alias, count: int, stream: int) -> torch.Tensor:
+        if use_hip(a.prob):
+            return hip().alias_sample(a.prob, a.alias, None, int(count), self.rng, int(stream)).long()
+        n = a.prob.numel()
+        k = torch.randint(0, n, (count,), generator=self._cpu_gen)
+        u = torch.rand(count, generator=self._cpu_gen)
+        return torch.where(u < a.prob[k], k, a.alias[k].long())
+
+    def sample_triples(self, count: int):
+        """(src, rel, dst) [count] by edge weight (reference sample_edge)"""
+        e = self._draw(self.edges, count, 1)
+        return self.src[e], self.rel[e], self.dst[e]
+
+    def sample_corruptions(self, count: int) -> torch.Tensor:
+        """[count] node ids of the candidate type by node weight (reference sample_node)"""
+        return self.cand[self._draw(self.negs, count, 2)]
+
+
+class KGTrainer(CapturedTrainer):
+    def __init__(self, model, table: TripleTable, batch_size, optimizer="adam", learning_rate=0.01):
+        if not hasattr(model, "loss_scores"):
+            raise ValueError("KGTrainer trains the TransX family (models/knowledge_graph.py)")
+        from euler_amd.utils.layers import Embedding
+
+        if not isinstance(model.entity_encoder, Embedding):
+            raise ValueError("device_graph=True needs the dense (non-sharded) entity table")
+        self.table = table
+        self.B = int(batch_size)
+        self.metric_name = model.metric_name
+        self.msum = torch.zeros(2, dtype=torch.float64, device=table.device)  # metric sum, count
+        super().__init__(model, table, table.device, optimizer, learning_rate)
+
+    @classmethod
+    def from_model(cls, model, batch_size, edge_type, seed=0, device="cuda", optimizer="adam", learning_rate=0.01):
+        table = TripleTable.from_engine(edge_type, node_type=model.node_type, seed=seed, device=device)
+        return cls(model, table, batch_size, optimizer=optimizer, learning_rate=learning_rate)
+
+    def _forward_loss(self):
+        self._draw()
+        t = self.table
+        src, rel, dst = t.sample_triples(self.B)
+        neg = t.sample_corruptions(self.B * self.model.num_negs).view(self.B, self.model.num_negs)
+        src, rel, dst = src.view(-1, 1), rel.view(-1, 1), dst.view(-1, 1)
+        loss, pos, neg_s = self.model.loss_scores(src, dst, neg, rel)
+        with torch.no_grad():
+            r = (neg_s >= pos).sum(-1).double()  # 0 = best (utils/metrics.py _ranks)
+            if self.metric_name == "mrr":
+                v = (1.0 / (r + 1)).sum()
+            elif self.metric_name == "mr":
+                v = (r + 1).sum()
+            else:  # hit10
+                v = (r < 10).double().sum()
+            self.msum += torch.stack([v, torch.full_like(v, float(r.numel()))])
+        self._samples = (src, rel, dst, neg)
+        return loss
+
+    def metric(self) -> float:
+        s, n = self.msum.tolist()
+        return s / max(n, 1.0)
+
+    def reset_metric(self):
+        self.msum.zero_()

@@ -67,7 +67,8 @@ class TransX(nn.Module):
         """margin ranking against the MEAN negative score (transE.py:49-65)."""
         return F.relu(self.margin + neg_scores.mean(-1, keepdim=True) - pos_scores).mean()
 
-    def calculate_energy(self, src, dst, neg, rel):
+    def energy_scores(self, src, dst, neg, rel):
+        """(positive scores [B, 1, 1], corrupted scores [B, 1, k]) of embedded triples"""
         pos = self.calculate_scores(src, rel, dst).reshape(-1, 1, 1)
         if self.corrupt == "front":
             neg_s = self.calculate_scores(neg, rel, dst)
@@ -75,10 +76,29 @@ class TransX(nn.Module):
             neg_s = self.calculate_scores(src, rel, neg)
         else:
             neg_s = torch.cat([self.calculate_scores(neg, rel, dst), self.calculate_scores(src, rel, neg)], -1)
-        neg_s = neg_s.reshape(pos.shape[0], 1, -1)
+        return pos, neg_s.reshape(pos.shape[0], 1, -1)
+
+    def calculate_energy(self, src, dst, neg, rel):
+        pos, neg_s = self.energy_scores(src, dst, neg, rel)
         loss = self.loss_fn(pos, neg_s)
         metric = self.metric(pos.detach().float().cpu(), neg_s.detach().float().cpu())
         return loss, metric
+
+    def _fused_ok(self, dev):
+        return self.fused_kind is not None and dev.type == "cuda" and isinstance(self.entity_encoder, Embedding)
+
+    def loss_scores(self, src, dst, neg, rel):
+        """(loss, positive scores [B, 1, 1], corrupted scores [B, 1, k]) of device id tensors
+        src / dst / rel [B, 1], neg [B, num_negs], with no host round trip: the step of the
+        device-path trainer (models/kg_trainer.py) is captured into a hipGraph"""
+        if self._fused_ok(src.device):
+            ent, rtab = self.entity_encoder, self.relation_encoder
+            pos_s, neg_s = gnn_ops.kg_score(ent.weight, rtab.weight, ent._rows(src), ent._rows(dst),
+                                            rtab._rows(rel), ent._rows(neg), self.fused_kind, self.corrupt, True)
+            pos, neg_s = pos_s.view(-1, 1, 1), neg_s.view(pos_s.shape[0], 1, -1)
+        else:
+            pos, neg_s = self.energy_scores(*self.generate_embedding(src, dst, neg, rel))
+        return self.loss_fn(pos, neg_s), pos, neg_s
 
     def generate_embedding(self, src, dst, neg, rel):
         raise NotImplementedError
@@ -90,10 +110,7 @@ class TransX(nn.Module):
         """gather + l2-normalise + score of the positive and every corrupted triple, and
         the whole backward into the two tables, in two kernels."""
         ent, rtab = self.entity_encoder, self.relation_encoder
-        pos_s, neg_s = gnn_ops.kg_score(ent.weight, rtab.weight, ent._rows(src), ent._rows(dst),
-                                        rtab._rows(rel), ent._rows(neg), self.fused_kind, self.corrupt, True)
-        pos, neg_s = pos_s.view(-1, 1, 1), neg_s.view(pos_s.shape[0], 1, -1)
-        loss = self.loss_fn(pos, neg_s)
+        loss, pos, neg_s = self.loss_scores(src, dst, neg, rel)
         metric = self.metric(pos.detach().float().cpu(), neg_s.detach().float().cpu())
         with torch.no_grad():
             s, d, r = self.norm_emb(ent(src)), self.norm_emb(ent(dst)), self.norm_emb(rtab(rel))
@@ -104,7 +121,7 @@ class TransX(nn.Module):
         src, dst, neg, rel = self.generate_triplets(inputs)
         dev = self._dev()
         src, dst, neg, rel = src.to(dev), dst.to(dev), neg.to(dev), rel.to(dev)
-        if self.fused_kind is not None and dev.type == "cuda" and isinstance(self.entity_encoder, Embedding):
+        if self._fused_ok(dev):
             return self._fused_forward(src, dst, neg, rel)
         s, d, n, r = self.generate_embedding(src, dst, neg, rel)
         loss, metric = self.calculate_energy(s, d, n, r)
