@@ -434,6 +434,24 @@ class BaseEstimator:
             return KGTrainer.from_model(model, int(self.params["batch_size"]), edge_type, seed=seed * 7919 + self.rank,
                                         device=self.device, optimizer=self.params.get("optimizer", "adam"),
                                         learning_rate=float(self.params.get("learning_rate", 0.001)))
+        from euler_amd.models.unsupervised import BaseNode2Vec
+
+        if isinstance(model, BaseNode2Vec):
+            # DeepWalk / Node2Vec: walks, pairs, negatives and the row-sparse SGNS update on the
+            # HBM graph (models/deepwalk_step.py)
+            from euler_amd.models.deepwalk_step import DeepWalkEstimatorTrainer
+
+            if self.world > 1:
+                raise ValueError("the DeepWalk device path of the estimator runs on one rank "
+                                 "(the row-sharded multi-rank table: benchmarks/bench_deepwalk.py)")
+            self._prepare(first)
+            nt = self.params.get("train_node_type", model.node_type)
+            node_type = -1 if nt in (None, -1, "-1") else int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
+            graph = DeviceGraph.from_engine(node_type=node_type, seed=seed * 7919 + self.rank, device=self.device)
+            return DeepWalkEstimatorTrainer(model, graph, int(self.params["batch_size"]),
+                                            optimizer=self.params.get("optimizer", "adam"),
+                                            learning_rate=float(self.params.get("learning_rate", 0.001)),
+                                            seed=seed)
         gnn = getattr(model, "gnn", None)
         unsup = hasattr(model, "context_gnn")
         if gnn is None or not hasattr(gnn, "feature_idx") or not (unsup or hasattr(model, "label_idx")):
@@ -500,7 +518,7 @@ class BaseEstimator:
             log.info("already trained to step %d", self.global_step)
             return {}
         grad_sync, xar, gbuf = None, None, None
-        if self.world > 1:
+        if self.world > 1 and not getattr(tr, "self_synced", False):
             # xGMI two-shot peer-memory all-reduce or RCCL on GPUs, whichever the start-up
             # timing on this node finds faster (parallel/xgmi.py); gloo on CPUs
             from ..parallel.xgmi import make_grad_sync

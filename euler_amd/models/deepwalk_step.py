@@ -44,7 +44,7 @@ from euler_amd.ops import gnn_ops
 from euler_amd.ops._native import hip, use_hip
 from euler_amd.parallel.sparse_table import ShardedTable
 
-__all__ = ["DeepWalkTrainer"]
+__all__ = ["DeepWalkTrainer", "DeepWalkEstimatorTrainer"]
 
 
 def _pair_positions(walk_len, left, right):
@@ -55,8 +55,9 @@ def _pair_positions(walk_len, left, right):
 class DeepWalkTrainer:
     def __init__(self, graph, num_nodes, dim=128, walk_len=3, left_win_size=1, right_win_size=1, num_negs=5,
                  batch_size=1024, lr=0.01, optimizer="adam", group=None, seed=0, force_comm=False, static=False,
-                 wire_dtype="bf16", overflow_check_every=200, micro_batches=1):
+                 wire_dtype="bf16", overflow_check_every=200, micro_batches=1, edge_types=None, p=1.0, q=1.0):
         self.graph = graph
+        self.edge_types, self.p, self.q = edge_types, float(p), float(q)
         self.num_nodes = int(num_nodes)
         self.pad = self.num_nodes  # rows: num_nodes + 1 (pad row like the reference's max_id + 1)
         self.dim, self.walk_len, self.num_negs, self.batch = int(dim), int(walk_len), int(num_negs), int(batch_size)
@@ -96,7 +97,8 @@ class DeepWalkTrainer:
         g = self.graph
         g.advance()
         starts = g.sample_node(self.batch if batch is None else int(batch), stream_id=1)
-        walks = g.random_walk(starts, self.walk_len, default=-1, stream_id=3).long()
+        walks = g.random_walk(starts, self.walk_len, edge_types=self.edge_types, default=-1, stream_id=3, p=self.p,
+                              q=self.q).long()
         walks = torch.where(walks < 0, torch.full_like(walks, self.pad), walks)
         src = walks[:, self.pi].reshape(-1)
         pos = walks[:, self.pj].reshape(-1)
@@ -315,3 +317,171 @@ class DeepWalkTrainer:
         u, inv = gnn_ops.unique_first(ids.reshape(-1).long())
         rows, _ = self.table.lookup(u + self.off)
         return rows[inv].view(*ids.shape, self.dim)
+
+
+class DeepWalkEstimatorTrainer:
+    """``NodeEstimator(device_graph=True)`` for DeepWalk / Node2Vec models with id
+    embeddings (reference examples/deepwalk/deepwalk.py:27-99 through
+    euler_estimator/python/node_estimator.py): the walks, pairs, negatives and the
+    row-sparse SGNS update of :class:`DeepWalkTrainer` on the HBM graph, several static
+    steps per hipGraph replay.  The model's two embedding tables are the trainer's table
+    halves (graph row r = node id ``graph.ids[r]``; the pad row is the model's
+    ``max_id + 1`` row); checkpoints carry the model's own parameter names.  One rank (the
+    row-sharded multi-rank table is the benchmark's, benchmarks/bench_deepwalk.py)."""
+
+    metric_name = "loss"
+    self_synced = True  # no dense gradient for the estimator to all-reduce
+
+    def __init__(self, model, graph, batch_size, optimizer="adam", learning_rate=0.01, seed=0):
+        import numpy as np
+
+        import euler_amd.ops.graph_api as ge
+
+        enc_t, enc_c = getattr(model, "_target_encoder", None), getattr(model, "_context_encoder", None)
+        for e in (enc_t, enc_c):
+            if e is None or not getattr(e, "use_id", False) or getattr(e, "use_feature", True) or \
+                    getattr(e, "use_sparse_feature", True) or e.combiner != "add":
+                raise ValueError("the DeepWalk device path trains pure id embeddings (no features, combiner 'add')")
+        if enc_t is enc_c:
+            raise ValueError("the DeepWalk device path needs separate target and context tables")
+        self.model = model
+        self.graph = graph
+        self.device = graph.device
+        self.on_gpu = self.device.type == "cuda"
+        et = model.edge_type
+        ets = None if et in (None, -1, "-1") else [int(t) for t in np.asarray(ge.get_edge_type_id(et)).reshape(-1)]
+        self.inner = DeepWalkTrainer(graph, graph.num_rows, dim=model.dim, walk_len=model.walk_len,
+                                     left_win_size=model.left_win_size, right_win_size=model.right_win_size,
+                                     num_negs=model.num_negs, batch_size=batch_size, lr=learning_rate,
+                                     optimizer=optimizer, seed=seed, static=self.on_gpu, edge_types=ets,
+                                     p=model.walk_p, q=model.walk_q)
+        self._keys = ("_target_encoder.embedding.weight", "_context_encoder.embedding.weight")
+        ids = graph.ids if graph.ids is not None else np.arange(graph.num_rows)
+        self._ids = torch.as_tensor(np.asarray(ids).astype(np.int64), device=self.device)
+        self._pad_id = int(model.max_id) + 1
+        self.load_logical(model.state_dict())
+        self.loss_sum = torch.zeros(2, dtype=torch.float64, device=self.device)
+        self._graphs, self._graph_loss, self._graph_exec = {}, {}, None
+        self._loss = torch.zeros((), device=self.device)
+        self.step_count = 0
+
+    # ------------------------------------------------------------------ table <-> model
+    def _halves(self):
+        t = self.inner
+        return t.table.weight[: t.off], t.table.weight[t.off: 2 * t.off]
+
+    def load_logical(self, sd):
+        with torch.no_grad():
+            for key, half in zip(self._keys, self._halves()):
+                if key not in sd:
+                    continue
+                w = torch.as_tensor(sd[key]).to(half)
+                half[:-1].copy_(w[self._ids])
+                half[-1].copy_(w[self._pad_id])
+
+    def write_to_model(self, model):
+        own = model.state_dict()
+        with torch.no_grad():
+            for key, half in zip(self._keys, self._halves()):
+                w = own[key]
+                w[self._ids.to(w.device)] = half[:-1].to(w)
+                w[self._pad_id] = half[-1].to(w)
+
+    def state_dict(self):
+        self.write_to_model(self.model)
+        return {k: v.detach().cpu() for k, v in self.model.state_dict().items()}
+
+    def logical_params(self):
+        return self.state_dict()
+
+    # ------------------------------------------------------------------ steps
+    def _one(self):
+        loss = self.inner._step_static() if self.inner.static else self.inner._step_dynamic()
+        self.loss_sum += torch.stack([loss.detach().double(), torch.ones((), dtype=torch.float64,
+                                                                         device=self.device)])
+        return loss
+
+    def step(self, grad_sync=None):
+        self.step_count += 1
+        if self._graph_exec is not None:
+            self._graph_exec.replay()
+            self._loss = self._graph_loss[1]
+            return self._loss
+        self._loss = self._one()
+        return self._loss
+
+    def capture(self, grad_sync=None, warmup=2, steps=1, extra_sizes=()):
+        if not self.on_gpu:
+            return None
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self.step_count += 1
+                self._loss = self._one()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        self._graphs, self._graph_loss = {}, {}
+        for k in sorted({1, int(steps)} | {int(e) for e in extra_sizes if int(e) > 0}, reverse=True):
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr, capture_error_mode="thread_local"):
+                for _ in range(k):
+                    out = self._one()
+            self._graphs[k], self._graph_loss[k] = gr, out
+        self._graph_exec = self._graphs[1]
+        return self._graphs[int(steps)]
+
+    def replay(self, n=1):
+        for _ in range(int(n)):
+            self._graph_exec.replay()
+        self._loss = self._graph_loss[1]
+        self.step_count += int(n)
+
+    def replay_steps(self, n):
+        left = int(n)
+        for k in sorted(self._graphs, reverse=True):
+            while left >= k:
+                self._graphs[k].replay()
+                self._loss = self._graph_loss[k]
+                left -= k
+        self.step_count += int(n)
+
+    def release_graphs(self):
+        for g in self._graphs.values():
+            g.reset()
+        self._graphs, self._graph_loss, self._graph_exec = {}, {}, None
+
+    # ------------------------------------------------------------------ state
+    @property
+    def loss(self):
+        return self._loss
+
+    def metric(self) -> float:
+        s, n = self.loss_sum.tolist()
+        return s / max(n, 1.0)
+
+    def reset_metric(self):
+        self.loss_sum.zero_()
+
+    def samples(self):
+        return None
+
+    def trainer_state(self):
+        t = self.inner.table
+        return {"m": t.m.cpu().clone(), "v": t.v.cpu().clone(), "step": int(t.step.item()),
+                "rng": self.graph.rng.detach().cpu().clone()}
+
+    def load_trainer_state(self, st):
+        t = self.inner.table
+        t.m.copy_(torch.as_tensor(st["m"]).to(t.m))
+        t.v.copy_(torch.as_tensor(st["v"]).to(t.v))
+        t.step.fill_(int(st["step"]))
+        self.graph.rng.copy_(torch.as_tensor(st["rng"]).to(self.graph.rng))
+        self.step_count = int(st["step"])
+
+    def dp_state_tensors(self):
+        t = self.inner.table
+        return [t.weight, t.m, t.v, t.step]
+
+    def set_learning_rate(self, lr):
+        self.inner.table.lr = float(lr)

@@ -1,0 +1,87 @@
+"""NodeEstimator(device_graph=True) for DeepWalk / Node2Vec (models/deepwalk_step.py
+DeepWalkEstimatorTrainer; reference examples/deepwalk/deepwalk.py:27-99): walks, skip-gram
+pairs, negatives and the row-sparse SGNS update on the HBM graph; the model's two id
+tables are the trainer's table halves."""
+import numpy as np
+import pytest
+import torch
+
+import euler_amd as ea
+from euler_amd import models as Z
+from euler_amd.dataset import get_dataset
+from euler_amd.estimator import NodeEstimator
+
+
+@pytest.fixture(scope="module")
+def _cora(tmp_path_factory):
+    ds = get_dataset("cora", data_dir=str(tmp_path_factory.mktemp("cora")), scale=0.08)
+    ds.get_data_dir()
+    return ds
+
+
+@pytest.fixture
+def cora(_cora):
+    _cora.load_graph()
+    ea.set_seed(3)
+    return _cora
+
+
+def _params(ds, tmp, device, **kw):
+    tnt = ds.train_node_type[0] if isinstance(ds.train_node_type, list) else ds.train_node_type
+    p = {"model_dir": str(tmp / "ckpt"), "batch_size": 32, "total_step": 30, "optimizer": "adam",
+         "learning_rate": 0.02, "log_steps": 10, "train_node_type": tnt, "device": device, "device_graph": True,
+         "seed": 11}
+    p.update(kw)
+    return p
+
+
+def _model(ds, cls=Z.DeepWalk, **kw):
+    torch.manual_seed(0)
+    return cls("train", ["train"], ds.max_node_id, 8, walk_len=3, num_negs=3, **kw)
+
+
+def test_table_round_trip(cora, tmp_path):
+    """model tables -> trainer table halves -> model tables is the identity"""
+    from euler_amd.graph.device_graph import DeviceGraph
+    from euler_amd.models.deepwalk_step import DeepWalkEstimatorTrainer
+
+    m = _model(cora)
+    est = NodeEstimator(m, _params(cora, tmp_path, "cpu"))
+    est._prepare(est.get_train_from_input(32, est.params))
+    before = {k: v.clone() for k, v in m.state_dict().items()}
+    tr = DeepWalkEstimatorTrainer(m, DeviceGraph.from_engine(device="cpu"), 32)
+    for v in m.state_dict().values():
+        v.zero_()
+    tr.write_to_model(m)
+    ids = torch.as_tensor(np.asarray(tr.graph.ids).astype(np.int64))
+    for k, v in m.state_dict().items():
+        assert torch.equal(v[ids], before[k][ids]) and torch.equal(v[-1], before[k][-1])
+
+
+@pytest.mark.parametrize("cls,kw", [(Z.DeepWalk, {}), (Z.Node2Vec, {"walk_p": 0.5, "walk_q": 2.0})])
+def test_deepwalk_device_path_cpu(cora, tmp_path, cls, kw):
+    m = _model(cora, cls, **kw)
+    before = m.state_dict()["_target_encoder.embedding.weight"].clone()
+    res = NodeEstimator(m, _params(cora, tmp_path, "cpu")).train()
+    assert res["step"] == 30 and np.isfinite(res["loss"])
+    assert not torch.equal(before, m.state_dict()["_target_encoder.embedding.weight"])
+
+
+def test_deepwalk_device_path_resumes(cora, tmp_path):
+    m = _model(cora)
+    est = NodeEstimator(m, _params(cora, tmp_path, "cpu", total_step=20))
+    est.train()
+    ctr = int(est.device_trainer.graph.rng[1])
+    m2 = _model(cora)
+    est2 = NodeEstimator(m2, _params(cora, tmp_path, "cpu", total_step=30))
+    assert est2.train()["step"] == 30
+    assert int(est2.device_trainer.graph.rng[1]) == ctr + 10
+
+
+@pytest.mark.gpu
+def test_deepwalk_device_path_gpu_captured(cora, tmp_path, cuda):
+    m = _model(cora)
+    est = NodeEstimator(m, _params(cora, tmp_path, "cuda", total_step=120, log_steps=40, steps_per_graph=8))
+    res = est.train()
+    tr = est.device_trainer
+    assert res["step"] == 120 and np.isfinite(res["loss"]) and tr._graphs
