@@ -895,6 +895,166 @@ __global__ __launch_bounds__(kF2Threads, 4) void tr_fwd2_kernel(TrFwdArgs a) {
 }
 
 // ----------------------------------------------------------------------------
+// tr_fwd3: layer 0 of tr_fwd2, wave-specialised and software-pipelined.  tr_fwd2 runs two
+// blocks per CU that both gather (HBM-bound, ~9 us of a ~17 us block) and then both run
+// the kt copy, GEMM and epilogue while HBM idles.  Here one block per CU owns several
+// 64-row tiles (tile = xcd_remap(block) + j * grid) and splits its waves by role:
+//   * 4 gather waves fill the next tile's A image ([self | mean] rows, swizzled as in
+//     tr_fwd2) and then load the ids of the tile after it;
+//   * 4 math waves run the current tile: the kt copy (dW operand), the GEMM (wave w owns
+//     64 output columns of every 256-column chunk; its weight fragments are its own loads,
+//     so waiting for them never waits for the gather's loads, which sit in other waves'
+//     counters) and the epilogue straight from the accumulators: ReLU bits and the
+//     tree-mean / self rows of the parent A rows reduced across the 4 lanes that hold a
+//     column's rows (no output tile in LDS).
+// One barrier per tile.  LDS: two A images and two id sets (~70 KB at D = 128); 8 waves
+// per CU leave each up to 256 VGPRs (the gather keeps 2 x 11 row loads in flight per lane).
+// ----------------------------------------------------------------------------
+constexpr int kF3Gather = 256, kF3Math = 256, kF3Threads = kF3Gather + kF3Math;
+
+__device__ __forceinline__ void f3_math(const TrFwdArgs& a, const bf16_t* At, int64_t row0, int cw, int lane) {
+  constexpr int BM = kF2Rows, FM = BM / 16, FN = 4, WPF = 2;
+  const int K2 = 2 * a.D, H = a.H;
+  const int lr = lane & 15, lg = lane >> 4;
+  const bf16_t* W = a.W;
+  const int logP = a.logPg, P = 1 << logP, groups = BM >> logP;
+  for (int cchunk = 0; cchunk < H; cchunk += kTrBN) {
+    const int cb = cchunk + cw * 64;
+    if (cb >= H) break;  // uniform per wave; no barriers in here
+    float4_t acc[FM][FN];
+    tl_zero(acc);
+    uint4_t bq[WPF][FN];
+#pragma unroll
+    for (int q = 0; q < WPF; ++q)
+#pragma unroll
+      for (int n = 0; n < FN; ++n) bq[q][n] = fm_frag(W, cb + n * 16, q * 32 < K2 ? q * 32 : 0, K2, lane);
+    for (int k0 = 0; k0 < K2; k0 += 32 * WPF) {
+#pragma unroll
+      for (int q = 0; q < WPF; ++q) {
+        const int ks = k0 + 32 * q;
+        if (ks >= K2) break;  // uniform
+        uint4_t av[FM];
+        const int phys = f2_chunk(lr, (ks >> 3) + lg) * 8;
+#pragma unroll
+        for (int m = 0; m < FM; ++m) av[m] = *reinterpret_cast<const uint4_t*>(At + (m * 16 + lr) * K2 + phys);
+#pragma unroll
+        for (int m = 0; m < FM; ++m)
+#pragma unroll
+          for (int n = 0; n < FN; ++n) acc[m][n] = mfma16(av[m], bq[q][n], acc[m][n]);
+        const int kn = ks + 32 * WPF;
+#pragma unroll
+        for (int n = 0; n < FN; ++n) bq[q][n] = fm_frag(W, cb + n * 16, kn < K2 ? kn : 0, K2, lane);
+      }
+    }
+    // epilogue: lane (lr, lg) holds rows m * 16 + lg * 4 + j of column cb + n * 16 + lr
+#pragma unroll
+    for (int n = 0; n < FN; ++n) {
+      const int col = cb + n * 16 + lr;
+      float v[FM][4];
+#pragma unroll
+      for (int m = 0; m < FM; ++m)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[m][j] = bf2f(f2bf(fmaxf(acc[m][n][j], 0.f)));  // the bf16 h rows
+      if (a.mask) {  // word (32-row block, column): bit i = row i > 0
+#pragma unroll
+        for (int kb = 0; kb < FM / 2; ++kb) {
+          uint32_t bits = 0;
+#pragma unroll
+          for (int mm = 0; mm < 2; ++mm)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bits |= (v[kb * 2 + mm][j] > 0.f ? 1u : 0u) << (mm * 16 + lg * 4 + j);
+          bits |= __shfl_xor(bits, 16, 64);
+          bits |= __shfl_xor(bits, 32, 64);
+          if (lg == 0) a.mask[((row0 >> 5) + kb) * H + col] = bits;
+        }
+      }
+      for (int g = 0; g < groups; ++g) {
+        float sum = 0.f, self = 0.f;
+#pragma unroll
+        for (int m = 0; m < FM; ++m)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int r = m * 16 + lg * 4 + j;
+            if ((r >> logP) == g) {
+              const int q = r & (P - 1);
+              sum += q < a.Fg ? v[m][j] : 0.f;
+              self = q == a.Fg ? v[m][j] : self;
+            }
+          }
+        if (P >= 8) {
+          sum += __shfl_xor(sum, 16, 64);
+          self += __shfl_xor(self, 16, 64);
+        }
+        if (P >= 16) {
+          sum += __shfl_xor(sum, 32, 64);
+          self += __shfl_xor(self, 32, 64);
+        }
+        if (lg == (((g << logP) >> 2) & 3)) {  // the lane group holding the group's first row
+          if (a.include_self) sum += self;
+          bf16_t* dst = a.a_next + ((row0 >> logP) + g) * 2 * H + col;
+          dst[0] = f2bf(self);
+          dst[H] = f2bf(sum * a.inv_grp);
+        }
+      }
+    }
+  }
+}
+
+template <typename FT>
+__global__ __launch_bounds__(kF3Threads, 1) void tr_fwd3_kernel(TrFwdArgs a, int ntiles) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  constexpr int BM = kF2Rows;
+  const int K2 = 2 * a.D, FL = a.FL;
+  const int blk = static_cast<int>(blockIdx.x), nblk = static_cast<int>(gridDim.x);
+  const int base = xcd_remap(blk, nblk);
+  const int nt = base < ntiles ? (ntiles - base + nblk - 1) / nblk : 0;
+  bf16_t* Ab[2] = {lds, lds + BM * K2};
+  const int ids_n = BM * (1 + FL);
+  int32_t* idb = reinterpret_cast<int32_t*>(lds + 2 * BM * K2);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+#define F3_STAMP(k) \
+  if (a.prof && tid == 0) a.prof[blk * 8 + (k)] = static_cast<long long>(wall_clock64())
+  F3_STAMP(0);
+  if (a.prof && tid == 0) a.prof[blk * 8 + 6] = static_cast<long long>(__smid());
+  if (blk == 0 && tid == 0) {
+    if (a.step) a.step[0] += 1;
+    a.rng[1] += 1;  // this batch is consumed: the sampler draws the next counter
+  }
+  for (int i = blk * kF3Threads + tid; i < a.B; i += nblk * kF3Threads) a.roots_cur[i] = a.roots_in[i];
+  auto load_ids = [&](int j, int buf, int t0, int nthr) {
+    const int64_t row0 = static_cast<int64_t>(base + j * nblk) * BM;
+    int32_t* ns = idb + buf * ids_n;
+    for (int i = t0; i < BM; i += nthr) ns[i] = a.nodes[row0 + i];
+    for (int i = t0; i < BM * FL; i += nthr) ns[BM + i] = a.leaf[row0 * FL + i];
+  };
+  if (nt > 0) load_ids(0, 0, tid, kF3Threads);
+  if (nt > 1) load_ids(1, 1, tid, kF3Threads);
+  __syncthreads();
+  F3_STAMP(1);
+  if (nt > 0) {
+    if (tid < kF3Gather) f2_gather<FT, BM, kF3Gather>(a, Ab[0], idb, idb + BM, tid);
+    else if (a.ncomb && wave == kF3Gather / 64) tr_comb_wave(a.comb, blk, nblk, lane);  // the head's Wc tiles
+  }
+  __syncthreads();
+  F3_STAMP(2);
+  for (int j = 0; j < nt; ++j) {
+    const int cur = j & 1, nxt = cur ^ 1;
+    if (tid < kF3Gather) {
+      if (j + 1 < nt) f2_gather<FT, BM, kF3Gather>(a, Ab[nxt], idb + nxt * ids_n, idb + nxt * ids_n + BM, tid);
+      if (j + 2 < nt) load_ids(j + 2, cur, tid, kF3Gather);  // tile j's ids are spent
+    } else {
+      const int64_t row0 = static_cast<int64_t>(base + j * nblk) * BM;
+      f2_kt<BM, kF3Math>(a, row0, Ab[cur], tid - kF3Gather);
+      f3_math(a, Ab[cur], row0, wave - kF3Gather / 64, lane);
+    }
+    __syncthreads();
+    if (j == 0) F3_STAMP(3);
+  }
+  F3_STAMP(4);
+#undef F3_STAMP
+}
+
+// ----------------------------------------------------------------------------
 // tr_bwd (3-hop inner layer): G rows routed from the parent gradient through the tree
 // and the ReLU bits, then dA_out = G @ W (fp32 rows)
 // ----------------------------------------------------------------------------
@@ -1833,6 +1993,99 @@ __global__ __launch_bounds__(256, 2) void tr_dw_all_kernel(TrDwLaunch a) {
 // a separate instantiation so the plain optimizer keeps its small register footprint
 // one 8 x 32 (or 256-element) tile of the optimizer launch: split-K reduce and / or the
 // update, the bf16 shadows of weight tiles; block 0 also reduces the head statistics
+// one 8 x 128 weight tile (TrSeg::vec): thread = (row, 4 consecutive columns), every load and
+// store a 16-byte vector; the split-K slabs 16 in flight; the bf16 shadows through LDS
+// (tile_s [8][132]): threads 0-127 write the rows' 8-column fm chunks, 128-255 the
+// transpose's 8-row chunks
+template <int MODE>
+__device__ __forceinline__ void tr_opt_tile4(const TrOptArgs& a, const TrSeg& sg, int local, float* tile_s) {
+  constexpr int LDT = 132;
+  const int tid = threadIdx.x;
+  const int tiles_c = sg.cols >> 7;
+  const int tr = local / tiles_c, tc = local - tr * tiles_c;
+  const int r0 = tr * 8, c0 = tc * 128;
+  const int rr = tid >> 5, cc = (tid & 31) * 4;
+  const int64_t e = static_cast<int64_t>(r0 + rr) * sg.cols + c0 + cc;  // index inside the segment
+  const int64_t i = sg.off + e;
+  float4_t p = *reinterpret_cast<const float4_t*>(a.p + i);
+  float4_t m = float4_t{0.f, 0.f, 0.f, 0.f}, v = m;
+  if (MODE == 1 || MODE == 2) {
+    m = *reinterpret_cast<const float4_t*>(a.m + i);
+    v = *reinterpret_cast<const float4_t*>(a.v + i);
+  }
+  if (MODE != 3) {
+    float4_t g = float4_t{0.f, 0.f, 0.f, 0.f};
+    if (MODE != 1) {
+      const float* src = sg.part + e;
+      for (int s0 = 0; s0 < sg.S; s0 += 16) {
+        float4_t x[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          x[u] = *reinterpret_cast<const float4_t*>(src + static_cast<int64_t>(s0 + u < sg.S ? s0 + u : sg.S - 1) *
+                                                              sg.n);
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (s0 + u < sg.S) g += x[u];
+      }
+      if (MODE == 0) {
+        if (a.g16) {
+          tl_uint2 w;
+          w[0] = pack_bf16x2(g[0], g[1]);
+          w[1] = pack_bf16x2(g[2], g[3]);
+          *reinterpret_cast<tl_uint2*>(a.g16 + i) = w;
+        } else {
+          *reinterpret_cast<float4_t*>(a.g + i) = g;
+        }
+        return;
+      }
+    } else if (a.g16) {
+      const tl_uint2 w = *reinterpret_cast<const tl_uint2*>(a.g16 + i);
+      g = float4_t{bf_lo(w[0]), bf_hi(w[0]), bf_lo(w[1]), bf_hi(w[1])};
+    } else {
+      g = *reinterpret_cast<const float4_t*>(a.g + i);
+    }
+    const float t = static_cast<float>(a.step[0]);
+    const float bc1 = a.kind == 0 ? 1.f - __powf(a.b1, t) : 1.f, bc2 = a.kind == 0 ? 1.f - __powf(a.b2, t) : 1.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float gi = g[k] * a.grad_scale + a.wd * p[k];
+      if (a.kind == 0) {
+        m[k] = a.b1 * m[k] + (1.f - a.b1) * gi;
+        v[k] = a.b2 * v[k] + (1.f - a.b2) * gi * gi;
+        p[k] -= a.lr * (m[k] / bc1) / (sqrtf(v[k] / bc2) + a.eps);
+      } else if (a.kind == 1) {
+        v[k] += gi * gi;
+        p[k] -= a.lr * gi / (sqrtf(v[k]) + a.eps);
+      } else if (a.kind == 2) {
+        p[k] -= a.lr * gi;
+      } else {
+        m[k] = a.b1 * m[k] + gi;
+        p[k] -= a.lr * m[k];
+      }
+    }
+    *reinterpret_cast<float4_t*>(a.p + i) = p;
+    *reinterpret_cast<float4_t*>(a.m + i) = m;
+    *reinterpret_cast<float4_t*>(a.v + i) = v;
+  }
+  if (sg.sh) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tile_s[rr * LDT + cc + k] = p[k];
+    __syncthreads();
+    float t8[8];
+    if (tid < 128) {
+      const int row = tid >> 4, kc = (tid & 15) * 8;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t8[k] = tile_s[row * LDT + kc + k];
+      *reinterpret_cast<uint4_t*>(sg.sh + fm_off(r0 + row, c0 + kc, sg.cols)) = pack_bf16x8(t8);
+    } else if (sg.shT) {
+      const int col = tid - 128;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t8[k] = tile_s[k * LDT + col];
+      *reinterpret_cast<uint4_t*>(sg.shT + fm_off(c0 + col, r0, sg.rows)) = pack_bf16x8(t8);
+    }
+  }
+}
+
 template <int MODE>
 __device__ __forceinline__ void tr_opt_tile(const TrOptArgs& a, int b, float (*tile_s)[33]) {
   const int tid = threadIdx.x;
@@ -1866,6 +2119,10 @@ __device__ __forceinline__ void tr_opt_tile(const TrOptArgs& a, int b, float (*t
   for (int k = 1; k < kTrMaxSegs; ++k)
     if (k < a.nseg && b >= a.seg[k].blk0) sg = a.seg[k];
   const int local = b - sg.blk0;
+  if (sg.cols > 0 && sg.vec) {  // uniform per block
+    tr_opt_tile4<MODE>(a, sg, local, &tile_s[0][0]);
+    return;
+  }
   int64_t i;
   int r = 0, c = 0;
   bool valid = true;
@@ -1974,7 +2231,8 @@ __device__ __forceinline__ void tr_opt_tile(const TrOptArgs& a, int b, float (*t
 
 template <int MODE, typename FT, int GATHER>
 __global__ __launch_bounds__(256, GATHER ? 4 : 1) void tr_opt_kernel(TrOptArgs a) {
-  __shared__ float tile_s[8][33];
+  __shared__ float tile_raw[8 * 132];  // [8][33] scalar tiles, [8][132] vector tiles
+  float (*tile_s)[33] = reinterpret_cast<float (*)[33]>(tile_raw);
   __shared__ int32_t node_s[kTrSampleRows];
   extern __shared__ __attribute__((aligned(16))) bf16_t glds[];  // gather tiles only
   int b = blockIdx.x;
@@ -2028,6 +2286,23 @@ size_t eh_tr_fwd2_lds(int D, int FL) {
   return (F2_ALIAS ? (a > o ? a : o) : a + o) * sizeof(bf16_t) + static_cast<size_t>(kF2Rows) * (1 + FL) * sizeof(int32_t);
 }
 
+size_t eh_tr_fwd3_lds(int D, int FL) {
+  return static_cast<size_t>(2) * kF2Rows * 2 * D * sizeof(bf16_t) +
+         static_cast<size_t>(2) * kF2Rows * (1 + FL) * sizeof(int32_t);
+}
+
+// the pipelined, wave-specialised layer-0 kernel applies (EULER_AMD_FWD3=1 enables it):
+// the tr_fwd2 conditions, 64-column wave slabs and its LDS within one block per CU
+static bool fwd3_fits(const TrFwdArgs& a) {
+  static const bool on = [] {  // opt-in until measured on the box
+    const char* e = std::getenv("EULER_AMD_FWD3");
+    return e && e[0] == '1';
+  }();
+  if (!on || !a.a_kt || a.H % 64 != 0) return false;
+  if (a.D % 64 != 0 || a.M % kF2Rows != 0 || a.logPg < 2 || (1 << a.logPg) > kF2Rows) return false;
+  return eh_tr_fwd3_lds(a.D, a.FL) <= 150 * 1024;
+}
+
 // the 64-row / 8-wave layer-0 kernel applies (EULER_AMD_FWD2=0 disables it)
 static bool fwd2_fits(const TrFwdArgs& a) {
   static const bool off = [] {
@@ -2074,6 +2349,24 @@ hipError_t eh_tr_fwd(const TrFwdArgs* a, int mode, int feat_fp32, int bm, hipStr
     hipLaunchKernelGGL((tr_fwd2_kernel<bf16_t, 1>), dim3(static_cast<uint32_t>(a->M / kF2Rows)), dim3(kF2Threads), l2,
                        s, *a);
     return hipGetLastError();
+  }
+  if (mode == 0 && fwd3_fits(*a)) {
+    const size_t l3 = eh_tr_fwd3_lds(a->D, a->FL);
+    const int ntiles = static_cast<int>(a->M / kF2Rows);
+    int cus = 0;
+    EULER_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    const int grid = ntiles < cus ? ntiles : (cus > 0 ? cus : 1);
+#define TR_FWD3(FT)                                                                                          \
+  do {                                                                                                       \
+    EULER_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(tr_fwd3_kernel<FT>),                  \
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(l3)));   \
+    hipLaunchKernelGGL((tr_fwd3_kernel<FT>), dim3(static_cast<uint32_t>(grid)), dim3(kF3Threads), l3, s, *a,   \
+                       ntiles);                                                                              \
+    return hipGetLastError();                                                                                \
+  } while (0)
+    if (feat_fp32) TR_FWD3(float);
+    TR_FWD3(bf16_t);
+#undef TR_FWD3
   }
   if (mode == 0 && fwd2_fits(*a)) {
     const size_t l2 = eh_tr_fwd2_lds(a->D, a->FL);
@@ -2241,6 +2534,7 @@ hipError_t eh_tr_opt(const TrOptArgs* ain, int mode, hipStream_t s) {
     } else {
       if (g.sh || g.shT || g.sgrp != tr_seg_groups(g)) return hipErrorInvalidValue;  // tr_seg_prepare
     }
+    if (g.vec != tr_seg_vec(g)) return hipErrorInvalidValue;
     blk += tr_seg_blocks(g);
   }
   if (blk != a->nblk) return hipErrorInvalidValue;

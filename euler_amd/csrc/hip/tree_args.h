@@ -12,6 +12,8 @@
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 namespace euler_hip {
 
 constexpr int kTrMaxProbs = 6;
@@ -198,19 +200,31 @@ struct TrSeg {
   uint16_t* sh;        // optional fm [rows][cols]
   uint16_t* shT;       // optional fm [cols][rows]
   int32_t sgrp;        // vector segments: slab groups per element (1 or 4; tr_seg_prepare)
+  int32_t vec;         // weight segments: 8 x 128 tiles, 4 consecutive columns per thread
+                       // (float4 loads and stores; tr_seg_prepare)
 };
 // vector segments with many split-K slabs (the fc bias: one slab per head block) spread each
 // element's slab sum over 4 threads (256 / 4 elements per block): one round of 16 loads in
 // flight per thread instead of S / 16 dependent rounds, which made the bias block the tail
 // of the optimizer launch.  Returns the segment's block count.
 inline int tr_seg_groups(const TrSeg& s) { return s.cols == 0 && s.S > 16 ? 4 : 1; }
+// weight segments whose rows are whole 128-column tiles at a 16-byte aligned offset take the
+// vectorised tiles (EULER_AMD_OPT_VEC=1; opt-in until measured on the box)
+inline int tr_seg_vec(const TrSeg& s) {
+  static const bool on = [] {
+    const char* e = std::getenv("EULER_AMD_OPT_VEC");
+    return e && e[0] == '1';
+  }();
+  return on && s.cols > 0 && s.cols % 128 == 0 && s.rows % 8 == 0 && s.off % 4 == 0 && s.n % 4 == 0 ? 1 : 0;
+}
 inline int tr_seg_blocks(const TrSeg& s) {
-  if (s.cols > 0) return (s.rows / 8) * (s.cols / 32);
+  if (s.cols > 0) return (s.rows / 8) * (s.cols / (tr_seg_vec(s) ? 128 : 32));
   const int64_t per = 256 / tr_seg_groups(s);
   return static_cast<int>((s.n + per - 1) / per);
 }
 inline int tr_seg_prepare(TrSeg& s) {
   s.sgrp = tr_seg_groups(s);
+  s.vec = tr_seg_vec(s);
   return tr_seg_blocks(s);
 }
 struct TrOptArgs {

@@ -44,6 +44,7 @@ class CapturedTrainer:
         self._graphs = {}
         self._graph_exec = None
         self._samples = None
+        self.captures = 0  # hipGraph captures so far (graphs are released at the end of a run)
 
     # ------------------------------------------------------------------ subclass hooks
     def _materialize(self):
@@ -110,6 +111,7 @@ class CapturedTrainer:
                     self._step(grad_sync)
             self._graphs[k] = gr
         self._graph_exec = self._graphs[1]
+        self.captures += 1
         return self._graphs[int(steps)]
 
     def replay(self, n: int = 1):

@@ -364,6 +364,7 @@ class DeepWalkEstimatorTrainer:
         self._graphs, self._graph_loss, self._graph_exec = {}, {}, None
         self._loss = torch.zeros((), device=self.device)
         self.step_count = 0
+        self.captures = 0
 
     # ------------------------------------------------------------------ table <-> model
     def _halves(self):
@@ -429,6 +430,7 @@ class DeepWalkEstimatorTrainer:
                     out = self._one()
             self._graphs[k], self._graph_loss[k] = gr, out
         self._graph_exec = self._graphs[1]
+        self.captures += 1
         return self._graphs[int(steps)]
 
     def replay(self, n=1):

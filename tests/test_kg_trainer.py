@@ -88,7 +88,7 @@ def test_edge_estimator_device_path_gpu(fb, tmp_path, cuda, kind):
     res = est.train()
     tr = est.device_trainer
     assert res["step"] == 200 and np.isfinite(res["loss"])
-    assert tr._graphs, "the step should have been captured"
+    assert tr.captures >= 1, "the step should have been captured"
     assert tr.table.rng.is_cuda
 
 

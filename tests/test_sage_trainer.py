@@ -137,6 +137,11 @@ CASES = [
     dict(fanouts=[4, 3, 2], dims=[64, 64, 64, 32], C=32),                     # 3 hops (inner layer + bwd)
     dict(fanouts=[3, 20, 2], dims=[64, 128, 64, 32], C=16, mode="dense", self_loops=True),
     dict(fanouts=[5, 3], dims=[64, 64, 32], C=32, B=1024),                    # 64 fc-bias slabs: grouped reduce
+    # the pipelined layer-0 kernel (tr_fwd3: D % 64, H % 64) at every sibling-group size
+    dict(fanouts=[3, 3], dims=[64, 64, 32], C=32, D=64, B=256),                # 4-row groups
+    dict(fanouts=[5, 4], dims=[128, 64, 32], C=32, D=64, B=256, self_loops=True),  # 8-row groups
+    dict(fanouts=[10, 3], dims=[64, 64, 32], C=32, D=128, B=512),              # 16-row groups
+    dict(fanouts=[40, 2], dims=[64, 64, 32], C=32, D=64, B=64, mode="dense"),  # 64-row groups
 ]
 
 
@@ -160,9 +165,20 @@ def test_tree_step_matches_fp32_oracle(cuda, cfg):
     n = tr.graph.num_rows
     assert int(roots.min()) >= 0 and int(roots.max()) < n
     assert int(nodes.max()) < n and int(leaf.max()) < n
+    # the update (vectorised 8 x 128 tiles where the widths allow, 8 x 32 otherwise) is Adam
+    # in fp32 on the reduced gradient
+    p0, m0, v0, g = tr.flat.clone(), tr.m.clone(), tr.v.clone(), tr.grad.clone()
+    t = float(tr._step.item())
     tr.optimizer_step()
     torch.cuda.synchronize()
     assert math.isfinite(float(tr.loss.item()))
+    if tr.opt_name == "adam":
+        b1, b2 = tr.betas
+        m = b1 * m0 + (1 - b1) * g
+        v = b2 * v0 + (1 - b2) * g * g
+        p = p0 - tr.lr * (m / (1 - b1 ** t)) / (torch.sqrt(v / (1 - b2 ** t)) + tr.eps)
+        assert torch.allclose(tr.flat, p, rtol=1e-5, atol=1e-6)
+        assert torch.allclose(tr.m, m, rtol=1e-5, atol=1e-7)
 
 
 @pytest.mark.gpu

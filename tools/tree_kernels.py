@@ -82,17 +82,21 @@ def main():
         live = raw[:, 0] > 0
         f = f[live]  # blocks of the launched kernel (64-row tiles: half the 32-row count)
         cu = raw[live, 6]
+        # stamps 0..5 (slot 6 holds the CU id): tr_fwd2 ids / gather / kt / gemm / epilogue,
+        # tr_fwd3 ids / first gather / tile 0 / remaining tiles (slot 5 unused)
+        last = 5 if bool((raw[live, 5] > 0).all()) else 4
         st = (f[:, 0] - f[:, 0].min())
         uniq, cnt = torch.unique(cu, return_counts=True)
         print("fwd blocks", int(live.sum()), "distinct CUs", int(uniq.numel()), "max blocks per CU", int(cnt.max()),
               "start-time percentiles (us) 50/90/99/max",
               [round(float(torch.quantile(st, q)), 2) for q in (0.5, 0.9, 0.99)], round(float(st.max()), 2),
-              "end-time spread (us)", round(float((f[:, 5] - f[:, 5].min()).max()), 2))
+              "end-time spread (us)", round(float((f[:, last] - f[:, last].min()).max()), 2))
         f0 = f[:, 0].min()
-        fph = [(f[:, k] - f[:, k - 1]).mean().item() for k in range(1, 6)]
-        print("fwd phases (us, mean over blocks: ids, gather, kt, gemm, epilogue):", [round(v, 2) for v in fph],
-              "span", round(float(f[:, 5].max() - f0), 2), "start skew", round(float(f[:, 0].max() - f0), 2),
-              "block time", round(float((f[:, 5] - f[:, 0]).mean()), 2))
+        names = "ids, gather, kt, gemm, epilogue" if last == 5 else "ids, first gather, tile 0, later tiles"
+        fph = [(f[:, k] - f[:, k - 1]).mean().item() for k in range(1, last + 1)]
+        print(f"fwd phases (us, mean over blocks: {names}):", [round(v, 2) for v in fph],
+              "span", round(float(f[:, last].max() - f0), 2), "start skew", round(float(f[:, 0].max() - f0), 2),
+              "block time", round(float((f[:, last] - f[:, 0]).mean()), 2))
         print("head phases (us, mean over blocks):", [round(v, 2) for v in ph],
               "span", round(float(t[:, 7].max() - t0), 2), "start skew", round(float(t[:, 0].max() - t0), 2))
 
