@@ -60,6 +60,8 @@ def main():
         res[f"dw[{i}]"] = round(timeit(lambda: p.dw([i]), args.reps), 2)
     res["dw_splits"] = p.splits()
     res["route_profile"] = route_profile(tr)
+    if os.environ.get("EULER_AMD_FUSE_OPT", "0") == "1":
+        res["optimizer_in_forward"] = bool(tr.set_fused(True))
     tr.capture(steps=4)
     res["graph_step"] = round(timeit(lambda: tr.replay(1), args.reps), 2)
     res["graph_step_x4"] = round(timeit(lambda: tr.replay_steps(4), args.reps) / 4, 2)  # per step
