@@ -177,9 +177,6 @@ def main(argv=None):
     sync_name = None
     sync_info = {}
     grad_sync = None
-    # one process: the optimizer launch can ride in the next step's forward launch
-    # (SageTrainer.set_fused; opt-in while it is being measured: EULER_AMD_FUSE_OPT=1)
-    fused_opt = not dist_on and os.environ.get("EULER_AMD_FUSE_OPT", "0") == "1" and tr.set_fused(True)
     if dist_on:
         from euler_amd.parallel.xgmi import make_grad_sync
 
@@ -237,9 +234,6 @@ def main(argv=None):
             if args.log and rank == 0:
                 torch.cuda.synchronize()
                 log(f"step {done} loss {float(tr.loss.item()):.4f}")
-        # fused optimizer: the last step's update is still pending — apply it inside the
-        # timed region (the region then holds K + 1 updates: conservative)
-        tr.flush()
         torch.cuda.synchronize()
         if dist_on:
             dist.barrier()
@@ -298,7 +292,6 @@ def main(argv=None):
                 "label_dim": args.label_dim,
                 "hipgraph": use_graph,
                 "steps_per_graph": args.steps_per_graph if use_graph else None,
-                "optimizer_in_forward": bool(fused_opt),
                 "feature_sharding": (f"row-sharded over {world} rank(s), per-step all-to-all of the sampled rows"
                                      if fshard is not None else None),
                 "grad_sync": (f"{sync_name} all-reduce ({args.grad_reduce_dtype} gradient, {args.grad_buckets} "

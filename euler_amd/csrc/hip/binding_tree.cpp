@@ -95,18 +95,7 @@ class TreePlan {
       need(*prof, torch::kInt64, (fwd0_.M / (gemm_only ? 64 : bm0_)) * 8, "prof");
       a0.prof = reinterpret_cast<long long*>(prof->data_ptr<int64_t>());
     }
-    if (fused_ && !gemm_only) {
-      // the previous step's optimizer rides in this launch (pending partials only)
-      a0.gbar = reinterpret_cast<uint32_t*>(gbar_.data_ptr<int32_t>());
-      TrOptArgs o = opt_;  // current lr / gradient buffers
-      TORCH_CHECK(tr_opt_wave_plan(o), "TreePlan: optimizer wave plan");
-      o.nsample = 0;
-      o.ngather = 0;
-      o.pending = pending_.data_ptr<int32_t>();
-      ok(eh_tr_fwd_fused(&a0, &o, feat_fp32_, stream()), "tr_fwd(fused optimizer)");
-    } else {
-      ok(eh_tr_fwd(&a0, gemm_only ? 3 : (L_ == 1 ? 1 : 0), feat_fp32_, bm0_, stream()), "tr_fwd");
-    }
+    ok(eh_tr_fwd(&a0, gemm_only ? 3 : (L_ == 1 ? 1 : 0), feat_fp32_, bm0_, stream()), "tr_fwd");
     if (L_ == 3) ok(eh_tr_fwd(&fwd1_, 2, 0, bm1_, stream()), "tr_fwd(inner)");
   }
 
@@ -140,7 +129,6 @@ class TreePlan {
       TORCH_CHECK(prof->dtype() == torch::kInt64 && prof->is_cuda() && prof->is_contiguous(), "dw: prof");
       L.prof = reinterpret_cast<long long*>(prof->data_ptr<int64_t>());
     }
-    if (fused_) L.pending = pending_.data_ptr<int32_t>();
     for (int64_t i : which) {
       TORCH_CHECK(i >= 0 && i < (int64_t)probs_.size(), "dw: problem index out of range");
       if (probs_[i].route) {
@@ -189,52 +177,6 @@ class TreePlan {
     }
     ok(eh_tr_opt(&a, static_cast<int>(mode), stream()), "tr_opt");
   }
-
-  // the optimizer can ride in the next step's forward launch: 2 hops, the pipelined layer-0
-  // kernel (tr_fwd3) and every weight segment in vectorised wave jobs
-  bool fuse_ok() const {
-    if (L_ != 2 || eh_tr_fwd3_ok(&fwd0_, 0) == 0) return false;
-    TrOptArgs o = opt_;
-    return tr_opt_wave_plan(o);
-  }
-
-  // on: the step is fwd (+ the previous optimizer) / head / dw; the dW launch marks its
-  // partials pending and flush() applies them with a standalone launch (before reading the
-  // parameters, the loss or switching modes).  Off: flushes first.
-  void set_fused(bool on) {
-    const c10::DeviceGuard g(dev_);
-    if (on == fused_) return;
-    if (!on) {
-      flush();
-      fused_ = false;
-      return;
-    }
-    TORCH_CHECK(fuse_ok(), "TreePlan: the fused optimizer does not apply to this plan");
-    if (!pending_.defined()) {
-      const auto o = torch::TensorOptions().dtype(torch::kInt32).device(dev_);
-      pending_ = torch::zeros({1}, o);
-      gbar_ = torch::zeros({4}, o);
-    }
-    fused_ = true;
-  }
-
-  bool fused() const { return fused_; }
-
-  // apply pending partials (fused mode): the optimizer launch skips itself when nothing is
-  // pending, then the flag is cleared
-  void flush() {
-    if (!fused_) return;
-    const c10::DeviceGuard g(dev_);
-    TrOptArgs a = opt_;
-    a.nsample = 0;
-    a.pending = pending_.data_ptr<int32_t>();
-    a.check_pending = 1;
-    ok(eh_tr_opt(&a, 2, stream()), "tr_opt(flush)");
-    ok(eh_tr_clear_flag(pending_.data_ptr<int32_t>(), stream()), "tr_clear_flag");
-  }
-
-  // grid barrier waits that gave up (a block never arrived): must stay 0
-  int64_t barrier_timeouts() const { return gbar_.defined() ? gbar_[2].item<int32_t>() : 0; }
 
   // the pipelined step applies: 2 hops, the 64-row layer-0 kernel, A0_rows given, sibling
   // groups of at most 32 rows (one gather tile)
@@ -319,8 +261,6 @@ class TreePlan {
   std::vector<torch::Tensor> owned_;
   torch::Tensor roots_cur_;  // the forward's copy of the batch's roots (read by the head)
   TrOptArgs opt_{};
-  bool fused_ = false;
-  torch::Tensor pending_, gbar_;
   torch::Tensor g16_, grad_;
 
   bool has(const char* k) const { return d_.contains(k) && !d_[k].is_none(); }
@@ -1202,11 +1142,6 @@ void register_tree_ops(py::module& m) {
       .def("opt", &TreePlan::opt, py::arg("mode"), py::arg("grad_scale") = 1.0, py::arg("with_sample") = false,
            py::arg("with_gather") = false)
       .def("pipeline_ok", &TreePlan::pipeline_ok)
-      .def("fuse_ok", &TreePlan::fuse_ok)
-      .def("set_fused", &TreePlan::set_fused, py::arg("on"))
-      .def("fused", &TreePlan::fused)
-      .def("flush", &TreePlan::flush)
-      .def("barrier_timeouts", &TreePlan::barrier_timeouts)
       .def("opt_segments", &TreePlan::opt_segments, py::arg("mode"), py::arg("segs"), py::arg("head_stats"))
       .def("set_lr", &TreePlan::set_lr)
       .def("set_grad16", &TreePlan::set_grad16, py::arg("g16"))

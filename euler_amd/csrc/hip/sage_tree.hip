@@ -895,112 +895,6 @@ __global__ __launch_bounds__(kF2Threads, 4) void tr_fwd2_kernel(TrFwdArgs a) {
 }
 
 // ----------------------------------------------------------------------------
-// tr_fwd3: layer 0 of tr_fwd2, wave-specialised and software-pipelined.  tr_fwd2 runs two
-// blocks per CU that both gather (HBM-bound, ~9 us of a ~17 us block) and then both run
-// the kt copy, GEMM and epilogue while HBM idles.  Here one block per CU owns several
-// 64-row tiles (tile = xcd_remap(block) + j * grid) and splits its waves by role:
-//   * 4 gather waves fill the next tile's A image ([self | mean] rows, swizzled as in
-//     tr_fwd2) and then load the ids of the tile after it;
-//   * 4 math waves run the current tile: the kt copy (dW operand), the GEMM (wave w owns
-//     64 output columns of every 256-column chunk; its weight fragments are its own loads,
-//     so waiting for them never waits for the gather's loads, which sit in other waves'
-//     counters) and the epilogue straight from the accumulators: ReLU bits and the
-//     tree-mean / self rows of the parent A rows reduced across the 4 lanes that hold a
-//     column's rows (no output tile in LDS).
-// One barrier per tile.  LDS: two A images and two id sets (~70 KB at D = 128); 8 waves
-// per CU leave each up to 256 VGPRs (the gather keeps 2 x 11 row loads in flight per lane).
-// ----------------------------------------------------------------------------
-constexpr int kF3Gather = 256, kF3Math = 256, kF3Threads = kF3Gather + kF3Math;
-
-__device__ __forceinline__ void f3_math(const TrFwdArgs& a, const bf16_t* At, int64_t row0, int cw, int lane) {
-  constexpr int BM = kF2Rows, FM = BM / 16, FN = 4, WPF = 2;
-  const int K2 = 2 * a.D, H = a.H;
-  const int lr = lane & 15, lg = lane >> 4;
-  const bf16_t* W = a.W;
-  const int logP = a.logPg, P = 1 << logP, groups = BM >> logP;
-  for (int cchunk = 0; cchunk < H; cchunk += kTrBN) {
-    const int cb = cchunk + cw * 64;
-    if (cb >= H) break;  // uniform per wave; no barriers in here
-    float4_t acc[FM][FN];
-    tl_zero(acc);
-    uint4_t bq[WPF][FN];
-#pragma unroll
-    for (int q = 0; q < WPF; ++q)
-#pragma unroll
-      for (int n = 0; n < FN; ++n) bq[q][n] = fm_frag(W, cb + n * 16, q * 32 < K2 ? q * 32 : 0, K2, lane);
-    for (int k0 = 0; k0 < K2; k0 += 32 * WPF) {
-#pragma unroll
-      for (int q = 0; q < WPF; ++q) {
-        const int ks = k0 + 32 * q;
-        if (ks >= K2) break;  // uniform
-        uint4_t av[FM];
-        const int phys = f2_chunk(lr, (ks >> 3) + lg) * 8;
-#pragma unroll
-        for (int m = 0; m < FM; ++m) av[m] = *reinterpret_cast<const uint4_t*>(At + (m * 16 + lr) * K2 + phys);
-#pragma unroll
-        for (int m = 0; m < FM; ++m)
-#pragma unroll
-          for (int n = 0; n < FN; ++n) acc[m][n] = mfma16(av[m], bq[q][n], acc[m][n]);
-        const int kn = ks + 32 * WPF;
-#pragma unroll
-        for (int n = 0; n < FN; ++n) bq[q][n] = fm_frag(W, cb + n * 16, kn < K2 ? kn : 0, K2, lane);
-      }
-    }
-    // epilogue: lane (lr, lg) holds rows m * 16 + lg * 4 + j of column cb + n * 16 + lr
-#pragma unroll
-    for (int n = 0; n < FN; ++n) {
-      const int col = cb + n * 16 + lr;
-      float v[FM][4];
-#pragma unroll
-      for (int m = 0; m < FM; ++m)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[m][j] = bf2f(f2bf(fmaxf(acc[m][n][j], 0.f)));  // the bf16 h rows
-      if (a.mask) {  // word (32-row block, column): bit i = row i > 0
-#pragma unroll
-        for (int kb = 0; kb < FM / 2; ++kb) {
-          uint32_t bits = 0;
-#pragma unroll
-          for (int mm = 0; mm < 2; ++mm)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) bits |= (v[kb * 2 + mm][j] > 0.f ? 1u : 0u) << (mm * 16 + lg * 4 + j);
-          bits |= __shfl_xor(bits, 16, 64);
-          bits |= __shfl_xor(bits, 32, 64);
-          if (lg == 0) a.mask[((row0 >> 5) + kb) * H + col] = bits;
-        }
-      }
-      for (int g = 0; g < groups; ++g) {
-        float sum = 0.f, self = 0.f;
-#pragma unroll
-        for (int m = 0; m < FM; ++m)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int r = m * 16 + lg * 4 + j;
-            if ((r >> logP) == g) {
-              const int q = r & (P - 1);
-              sum += q < a.Fg ? v[m][j] : 0.f;
-              self = q == a.Fg ? v[m][j] : self;
-            }
-          }
-        if (P >= 8) {
-          sum += __shfl_xor(sum, 16, 64);
-          self += __shfl_xor(self, 16, 64);
-        }
-        if (P >= 16) {
-          sum += __shfl_xor(sum, 32, 64);
-          self += __shfl_xor(self, 32, 64);
-        }
-        if (lg == (((g << logP) >> 2) & 3)) {  // the lane group holding the group's first row
-          if (a.include_self) sum += self;
-          bf16_t* dst = a.a_next + ((row0 >> logP) + g) * 2 * H + col;
-          dst[0] = f2bf(self);
-          dst[H] = f2bf(sum * a.inv_grp);
-        }
-      }
-    }
-  }
-}
-
-// ----------------------------------------------------------------------------
 // tr_bwd (3-hop inner layer): G rows routed from the parent gradient through the tree
 // and the ReLU bits, then dA_out = G @ W (fp32 rows)
 // ----------------------------------------------------------------------------
@@ -1915,7 +1809,6 @@ __global__ __launch_bounds__(256, 2) void tr_dw_all_kernel(TrDwLaunch a) {
   __shared__ __attribute__((aligned(16))) RouteLds gs;
   __shared__ uint4_t lut[256];
   const int b = blockIdx.x;
-  if (a.pending && b == 0 && threadIdx.x == 0) a.pending[0] = 1;  // partials await the fused update
   if (a.nroute > 0 && b < a.rwg[a.nroute]) {  // routed blocks: the fragment-spread table first
     tr_spread_lut_init(lut);
     __syncthreads();
@@ -1940,251 +1833,39 @@ __global__ __launch_bounds__(256, 2) void tr_dw_all_kernel(TrDwLaunch a) {
 // a separate instantiation so the plain optimizer keeps its small register footprint
 // one 8 x 32 (or 256-element) tile of the optimizer launch: split-K reduce and / or the
 // update, the bf16 shadows of weight tiles; block 0 also reduces the head statistics
-// one 8 x 32 weight sub-tile per wave (TrSeg::vec): lane = (row lane & 7, 4 consecutive
-// columns 4 (lane >> 3)), every load and store a 16-byte vector, the split-K slabs 16 in
-// flight.  Wave-local (no block barrier): the bf16 shadows come out of lane shuffles — a
-// row's 8-column fm chunk from the lane pair (l, l + 8), a column's 8-row chunk of the
-// transpose from the 8 lanes of its column group.
-template <int MODE>
-__device__ __forceinline__ void tr_opt_wave_tile(const TrOptArgs& a, const TrSeg& sg, int wt, int lane) {
-  const int tiles_c = sg.cols >> 5;
-  const int tr = wt / tiles_c, tc = wt - tr * tiles_c;
-  const int r0 = tr * 8, c0 = tc * 32;
-  const int row = lane & 7, cg = lane >> 3;
-  const int64_t e = static_cast<int64_t>(r0 + row) * sg.cols + c0 + cg * 4;  // index inside the segment
-  const int64_t i = sg.off + e;
-  float4_t p = *reinterpret_cast<const float4_t*>(a.p + i);
-  float4_t m = float4_t{0.f, 0.f, 0.f, 0.f}, v = m;
-  if (MODE == 1 || MODE == 2) {
-    m = *reinterpret_cast<const float4_t*>(a.m + i);
-    v = *reinterpret_cast<const float4_t*>(a.v + i);
-  }
-  if (MODE != 3) {
-    float4_t g = float4_t{0.f, 0.f, 0.f, 0.f};
-    if (MODE != 1) {
-      const float* src = sg.part + e;
-      for (int s0 = 0; s0 < sg.S; s0 += 16) {
-        float4_t x[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u)
-          x[u] = *reinterpret_cast<const float4_t*>(src + static_cast<int64_t>(s0 + u < sg.S ? s0 + u : sg.S - 1) *
-                                                              sg.n);
-#pragma unroll
-        for (int u = 0; u < 16; ++u)
-          if (s0 + u < sg.S) g += x[u];
-      }
-      if (MODE == 0) {
-        if (a.g16) {
-          tl_uint2 w;
-          w[0] = pack_bf16x2(g[0], g[1]);
-          w[1] = pack_bf16x2(g[2], g[3]);
-          *reinterpret_cast<tl_uint2*>(a.g16 + i) = w;
-        } else {
-          *reinterpret_cast<float4_t*>(a.g + i) = g;
-        }
-        return;
-      }
-    } else if (a.g16) {
-      const tl_uint2 w = *reinterpret_cast<const tl_uint2*>(a.g16 + i);
-      g = float4_t{bf_lo(w[0]), bf_hi(w[0]), bf_lo(w[1]), bf_hi(w[1])};
-    } else {
-      g = *reinterpret_cast<const float4_t*>(a.g + i);
-    }
-    const float t = static_cast<float>(a.step[0]);
-    const float bc1 = a.kind == 0 ? 1.f - __powf(a.b1, t) : 1.f, bc2 = a.kind == 0 ? 1.f - __powf(a.b2, t) : 1.f;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float gi = g[k] * a.grad_scale + a.wd * p[k];
-      if (a.kind == 0) {
-        m[k] = a.b1 * m[k] + (1.f - a.b1) * gi;
-        v[k] = a.b2 * v[k] + (1.f - a.b2) * gi * gi;
-        p[k] -= a.lr * (m[k] / bc1) / (sqrtf(v[k] / bc2) + a.eps);
-      } else if (a.kind == 1) {
-        v[k] += gi * gi;
-        p[k] -= a.lr * gi / (sqrtf(v[k]) + a.eps);
-      } else if (a.kind == 2) {
-        p[k] -= a.lr * gi;
-      } else {
-        m[k] = a.b1 * m[k] + gi;
-        p[k] -= a.lr * m[k];
-      }
-    }
-    *reinterpret_cast<float4_t*>(a.p + i) = p;
-    *reinterpret_cast<float4_t*>(a.m + i) = m;
-    *reinterpret_cast<float4_t*>(a.v + i) = v;
-  }
-  if (sg.sh) {
-    // row chunk (row, columns 8q .. 8q + 7) = lanes row + 16q (cg = 2q) and row + 16q + 8
-    float hi[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) hi[k] = __shfl_down(p[k], 8, 64);
-    if ((cg & 1) == 0) {
-      const float t8[8] = {p[0], p[1], p[2], p[3], hi[0], hi[1], hi[2], hi[3]};
-      *reinterpret_cast<uint4_t*>(sg.sh + fm_off(r0 + row, c0 + cg * 4, sg.cols)) = pack_bf16x8(t8);
-    }
-    if (sg.shT) {
-      // transpose chunk of column j = lane (lanes 0-31): rows 0..7 from lanes i + 8 (j >> 2),
-      // component j & 3
-      const int j = lane & 31;
-      float t8[8];
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const int sl = r + 8 * (j >> 2);
-        const float x0 = __shfl(p[0], sl, 64), x1 = __shfl(p[1], sl, 64), x2 = __shfl(p[2], sl, 64),
-                    x3 = __shfl(p[3], sl, 64);
-        const int k = j & 3;
-        t8[r] = k == 0 ? x0 : (k == 1 ? x1 : (k == 2 ? x2 : x3));
-      }
-      if (lane < 32) *reinterpret_cast<uint4_t*>(sg.shT + fm_off(c0 + j, r0, sg.rows)) = pack_bf16x8(t8);
-    }
-  }
-}
-
-// a vector segment's wave job (the optimizer inside the forward): 64 / grp elements, each
-// element's slab sum split over grp lanes (lane = group * per + element) and combined by
-// shuffles
-template <int MODE>
-__device__ __forceinline__ void tr_opt_wave_vec(const TrOptArgs& a, const TrSeg& sg, int wt, int lane) {
-  const int grp = sg.sgrp > 1 ? sg.sgrp : 1, per = 64 / grp, sub = lane / per;
-  int64_t e = static_cast<int64_t>(wt) * per + (lane - sub * per);
-  const bool valid = e < sg.n && sub == 0;
-  if (e >= sg.n) e = 0;
-  const int64_t i = sg.off + e;
-  float p = a.p[i], m = 0.f, v = 0.f;
-  if (MODE == 1 || MODE == 2) {
-    m = a.m[i];
-    v = a.v[i];
-  }
-  float g = 0.f;
-  if (MODE != 1) {
-    const float* src = sg.part + e;
-    for (int s0 = sub; s0 < sg.S; s0 += 16 * grp) {
-      float x[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int sl = s0 + u * grp;
-        x[u] = src[static_cast<int64_t>(sl < sg.S ? sl : sg.S - 1) * sg.n];
-      }
-#pragma unroll
-      for (int u = 0; u < 16; ++u) g += (s0 + u * grp < sg.S) ? x[u] : 0.f;
-    }
-    if (grp > 1) {  // grp == 4: the element's lanes are lane ^ 16, ^ 32, ^ 48
-      g += __shfl_xor(g, 16, 64);
-      g += __shfl_xor(g, 32, 64);
-    }
-    if (MODE == 0) {
-      if (valid) {
-        if (a.g16) a.g16[i] = f2bf(g);
-        else a.g[i] = g;
-      }
-      return;
-    }
-  } else {
-    g = a.g16 ? bf2f(a.g16[i]) : a.g[i];
-  }
-  const float t = static_cast<float>(a.step[0]);
-  const float gi = g * a.grad_scale + a.wd * p;
-  if (a.kind == 0) {
-    const float bc1 = 1.f - __powf(a.b1, t), bc2 = 1.f - __powf(a.b2, t);
-    m = a.b1 * m + (1.f - a.b1) * gi;
-    v = a.b2 * v + (1.f - a.b2) * gi * gi;
-    p -= a.lr * (m / bc1) / (sqrtf(v / bc2) + a.eps);
-  } else if (a.kind == 1) {
-    v += gi * gi;
-    p -= a.lr * gi / (sqrtf(v) + a.eps);
-  } else if (a.kind == 2) {
-    p -= a.lr * gi;
-  } else {
-    m = a.b1 * m + gi;
-    p -= a.lr * m;
-  }
-  if (valid) {
-    a.p[i] = p;
-    a.m[i] = m;
-    a.v[i] = v;
-  }
-}
-
-// wave job u of the fused optimizer (tr_opt_wave_plan): its segment by the wt0 prefix
-template <int MODE>
-__device__ __forceinline__ void tr_opt_wave_job(const TrOptArgs& a, int u, int lane) {
-  TrSeg sg = a.seg[0];
-#pragma unroll
-  for (int k = 1; k < kTrMaxSegs; ++k)
-    if (k < a.nseg && u >= a.seg[k].wt0) sg = a.seg[k];
-  if (sg.cols > 0) tr_opt_wave_tile<MODE>(a, sg, u - sg.wt0, lane);
-  else tr_opt_wave_vec<MODE>(a, sg, u - sg.wt0, lane);
-}
-
-// grid-wide barrier of a launch whose blocks are all resident (tr_fwd3: one block per CU):
-// generation counter, agent-scope release / acquire (the L2 of every XCD sees the writes
-// before it); a bounded wait that sets bar[2] instead of hanging if a block never arrives
-__device__ __forceinline__ void tr_grid_barrier(uint32_t* bar, int nblk) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    const uint32_t gen = __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t arrived = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (arrived == static_cast<uint32_t>(nblk) - 1) {
-      __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(bar + 1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      int spins = 0;
-      while (__hip_atomic_load(bar + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == gen) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1 << 21)) {
-          __hip_atomic_fetch_or(bar + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-    }
-    __threadfence();
-  }
-  __syncthreads();
-}
-
-// head statistics (one wave, lane = tid < 64): reduce (modes 0/2) the head's per-block
-// partials; hand the loss over (1/2)
-template <int MODE>
-__device__ __forceinline__ void tr_head_stats(const TrOptArgs& a, int tid) {
-  if (MODE != 1) {
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int k = tid; k < a.nhead; k += 64)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) v[c] += a.head_part[k * 4 + c];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) v[c] = wave_sum(v[c]);
-    if (tid == 0) {
-      a.loss_acc[0] = v[0];
-      if (a.stat_f) {
-        a.stat_f[0] += v[1];
-      } else if (a.counts) {
-        a.counts[0] += static_cast<uint32_t>(v[1]);
-        a.counts[1] += static_cast<uint32_t>(v[2]);
-        a.counts[2] += static_cast<uint32_t>(v[3]);
-      }
-      if (MODE == 2) a.loss_out[0] = v[0];
-    }
-  } else if (tid == 0) {
-    a.loss_out[0] = a.loss_acc[0];
-  }
-}
-
 template <int MODE>
 __device__ __forceinline__ void tr_opt_tile(const TrOptArgs& a, int b, float (*tile_s)[33]) {
   const int tid = threadIdx.x;
-  // nhead == 0: a segment-subset reduce launch that leaves the statistics to another launch
-  if (b == 0 && tid < 64 && MODE != 3 && a.nhead > 0) tr_head_stats<MODE>(a, tid);
+  if (b == 0 && tid < 64 && MODE != 3 && a.nhead > 0) {
+    // head statistics: reduce (modes 0/2) the per-block partials; hand the loss over (1/2);
+    // nhead == 0: a segment-subset reduce launch that leaves them to another launch
+    if (MODE != 1) {
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int k = tid; k < a.nhead; k += 64)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] += a.head_part[k * 4 + c];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] = wave_sum(v[c]);
+      if (tid == 0) {
+        a.loss_acc[0] = v[0];
+        if (a.stat_f) {
+          a.stat_f[0] += v[1];
+        } else if (a.counts) {
+          a.counts[0] += static_cast<uint32_t>(v[1]);
+          a.counts[1] += static_cast<uint32_t>(v[2]);
+          a.counts[2] += static_cast<uint32_t>(v[3]);
+        }
+        if (MODE == 2) a.loss_out[0] = v[0];
+      }
+    } else if (tid == 0) {
+      a.loss_out[0] = a.loss_acc[0];
+    }
+  }
   TrSeg sg = a.seg[0];
 #pragma unroll
   for (int k = 1; k < kTrMaxSegs; ++k)
     if (k < a.nseg && b >= a.seg[k].blk0) sg = a.seg[k];
   const int local = b - sg.blk0;
-  if (sg.cols > 0 && sg.vec) {  // uniform per block: 4 wave sub-tiles
-    const int wt = local * 4 + (tid >> 6);
-    if (wt < (sg.rows >> 3) * (sg.cols >> 5)) tr_opt_wave_tile<MODE>(a, sg, wt, tid & 63);
-    return;
-  }
   int64_t i;
   int r = 0, c = 0;
   bool valid = true;
@@ -2297,7 +1978,6 @@ __global__ __launch_bounds__(256, GATHER ? 4 : 1) void tr_opt_kernel(TrOptArgs a
   __shared__ int32_t node_s[kTrSampleRows];
   extern __shared__ __attribute__((aligned(16))) bf16_t glds[];  // gather tiles only
   int b = blockIdx.x;
-  if (a.check_pending && a.pending[0] == 0) return;  // a flush with nothing pending
   // GATHER launches: opt_tpb parameter tiles per block, so the parameter blocks take few of
   // the slots the gather tiles need
   const int tpb = GATHER && a.opt_tpb > 1 ? a.opt_tpb : 1;
@@ -2328,81 +2008,6 @@ __global__ __launch_bounds__(256, GATHER ? 4 : 1) void tr_opt_kernel(TrOptArgs a
   }
 }
 
-// FUSE = 1: the math waves also run the previous step's optimizer (tr_opt mode 2 as wave jobs)
-// while the gather waves fill the first A image — it needs no weights — then a grid barrier
-// (every block is resident: one per CU) publishes the new weights and shadows before any
-// GEMM reads them.  The optimizer launch of the step disappears; *o.pending (set by the
-// dW launch) says whether partials wait to be applied, the block-0 step increment moves
-// behind the barrier (the update reads the step of its own gradients).
-template <typename FT, int FUSE>
-__global__ __launch_bounds__(kF3Threads, 1) void tr_fwd3_kernel(TrFwdArgs a, int ntiles, TrOptArgs o) {
-  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
-  constexpr int BM = kF2Rows;
-  const int K2 = 2 * a.D, FL = a.FL;
-  const int blk = static_cast<int>(blockIdx.x), nblk = static_cast<int>(gridDim.x);
-  const int base = xcd_remap(blk, nblk);
-  const int nt = base < ntiles ? (ntiles - base + nblk - 1) / nblk : 0;
-  bf16_t* Ab[2] = {lds, lds + BM * K2};
-  const int ids_n = BM * (1 + FL);
-  int32_t* idb = reinterpret_cast<int32_t*>(lds + 2 * BM * K2);
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-#define F3_STAMP(k) \
-  if (a.prof && tid == 0) a.prof[blk * 8 + (k)] = static_cast<long long>(wall_clock64())
-  F3_STAMP(0);
-  if (a.prof && tid == 0) a.prof[blk * 8 + 6] = static_cast<long long>(__smid());
-  if (blk == 0 && tid == 0) {
-    if (a.step && !FUSE) a.step[0] += 1;
-    a.rng[1] += 1;  // this batch is consumed: the sampler draws the next counter
-  }
-  const bool do_opt = FUSE && o.pending[0] != 0;  // read before any block can clear it
-  for (int i = blk * kF3Threads + tid; i < a.B; i += nblk * kF3Threads) a.roots_cur[i] = a.roots_in[i];
-  auto load_ids = [&](int j, int buf, int t0, int nthr) {
-    const int64_t row0 = static_cast<int64_t>(base + j * nblk) * BM;
-    int32_t* ns = idb + buf * ids_n;
-    for (int i = t0; i < BM; i += nthr) ns[i] = a.nodes[row0 + i];
-    for (int i = t0; i < BM * FL; i += nthr) ns[BM + i] = a.leaf[row0 * FL + i];
-  };
-  if (nt > 0) load_ids(0, 0, tid, kF3Threads);
-  if (nt > 1) load_ids(1, 1, tid, kF3Threads);
-  __syncthreads();
-  F3_STAMP(1);
-  if (nt > 0 && tid < kF3Gather) {
-    f2_gather<FT, BM, kF3Gather>(a, Ab[0], idb, idb + BM, tid);
-  } else if (tid >= kF3Gather && do_opt) {
-    const int mw = wave - kF3Gather / 64, nmw = kF3Math / 64;
-    if (blk == 0 && mw == 0 && o.nhead > 0) tr_head_stats<2>(o, lane);
-    for (int u = blk * nmw + mw; u < o.nwt; u += nblk * nmw) tr_opt_wave_job<2>(o, u, lane);
-  } else if (tid >= kF3Gather && !FUSE && a.ncomb && wave == kF3Gather / 64) {
-    tr_comb_wave(a.comb, blk, nblk, lane);  // the head's Wc tiles
-  }
-  if (FUSE) {
-    if (do_opt) tr_grid_barrier(a.gbar, nblk);  // the new weights and shadows are visible
-    if (blk == 0 && tid == 0) {
-      if (a.step) a.step[0] += 1;
-      if (do_opt) o.pending[0] = 0;  // every block read the flag before the barrier
-    }
-    // Wc from the new Wout / Wfc shadows
-    if (a.ncomb && wave == kF3Gather / 64) tr_comb_wave(a.comb, blk, nblk, lane);
-  }
-  __syncthreads();
-  F3_STAMP(2);
-  for (int j = 0; j < nt; ++j) {
-    const int cur = j & 1, nxt = cur ^ 1;
-    if (tid < kF3Gather) {
-      if (j + 1 < nt) f2_gather<FT, BM, kF3Gather>(a, Ab[nxt], idb + nxt * ids_n, idb + nxt * ids_n + BM, tid);
-      if (j + 2 < nt) load_ids(j + 2, cur, tid, kF3Gather);  // tile j's ids are spent
-    } else {
-      const int64_t row0 = static_cast<int64_t>(base + j * nblk) * BM;
-      f2_kt<BM, kF3Math>(a, row0, Ab[cur], tid - kF3Gather);
-      f3_math(a, Ab[cur], row0, wave - kF3Gather / 64, lane);
-    }
-    __syncthreads();
-    if (j == 0) F3_STAMP(3);
-  }
-  F3_STAMP(4);
-#undef F3_STAMP
-}
-
 }  // namespace euler_hip
 
 using namespace euler_hip;
@@ -2421,32 +2026,6 @@ size_t eh_tr_fwd_lds(int D, int H, int bm, int FL, int mode) {
 size_t eh_tr_fwd2_lds(int D, int FL) {
   const size_t a = static_cast<size_t>(kF2Rows) * 2 * D, o = static_cast<size_t>(kTrBN) * kF2Ldt;
   return (F2_ALIAS ? (a > o ? a : o) : a + o) * sizeof(bf16_t) + static_cast<size_t>(kF2Rows) * (1 + FL) * sizeof(int32_t);
-}
-
-static int tr_num_cus() {
-  static const int n = [] {
-    int c = 0;
-    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) c = 0;
-    return c;
-  }();
-  return n;
-}
-
-size_t eh_tr_fwd3_lds(int D, int FL) {
-  return static_cast<size_t>(2) * kF2Rows * 2 * D * sizeof(bf16_t) +
-         static_cast<size_t>(2) * kF2Rows * (1 + FL) * sizeof(int32_t);
-}
-
-// the pipelined, wave-specialised layer-0 kernel applies (EULER_AMD_FWD3=1 enables it):
-// the tr_fwd2 conditions, 64-column wave slabs and its LDS within one block per CU
-static bool fwd3_fits(const TrFwdArgs& a) {
-  static const bool on = [] {  // opt-in until measured on the box
-    const char* e = std::getenv("EULER_AMD_FWD3");
-    return e && e[0] == '1';
-  }();
-  if (!on || !a.a_kt || a.H % 64 != 0) return false;
-  if (a.D % 64 != 0 || a.M % kF2Rows != 0 || a.logPg < 2 || (1 << a.logPg) > kF2Rows) return false;
-  return eh_tr_fwd3_lds(a.D, a.FL) <= 150 * 1024;
 }
 
 // the 64-row / 8-wave layer-0 kernel applies (EULER_AMD_FWD2=0 disables it)
@@ -2495,24 +2074,6 @@ hipError_t eh_tr_fwd(const TrFwdArgs* a, int mode, int feat_fp32, int bm, hipStr
     hipLaunchKernelGGL((tr_fwd2_kernel<bf16_t, 1>), dim3(static_cast<uint32_t>(a->M / kF2Rows)), dim3(kF2Threads), l2,
                        s, *a);
     return hipGetLastError();
-  }
-  if (mode == 0 && fwd3_fits(*a)) {
-    const size_t l3 = eh_tr_fwd3_lds(a->D, a->FL);
-    const int ntiles = static_cast<int>(a->M / kF2Rows);
-    const int cus = tr_num_cus();
-    const int grid = ntiles < cus ? ntiles : (cus > 0 ? cus : 1);
-    const TrOptArgs none{};
-#define TR_FWD3(FT)                                                                                          \
-  do {                                                                                                       \
-    EULER_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(tr_fwd3_kernel<FT, 0>),               \
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(l3)));   \
-    hipLaunchKernelGGL((tr_fwd3_kernel<FT, 0>), dim3(static_cast<uint32_t>(grid)), dim3(kF3Threads), l3, s, *a, \
-                       ntiles, none);                                                                        \
-    return hipGetLastError();                                                                                \
-  } while (0)
-    if (feat_fp32) TR_FWD3(float);
-    TR_FWD3(bf16_t);
-#undef TR_FWD3
   }
   if (mode == 0 && fwd2_fits(*a)) {
     const size_t l2 = eh_tr_fwd2_lds(a->D, a->FL);
@@ -2661,53 +2222,9 @@ size_t eh_tr_gather32_lds(int D, int FL) {
   return static_cast<size_t>(kG32Rows) * 2 * D * sizeof(bf16_t) + static_cast<size_t>(kG32Rows) * (1 + FL) * sizeof(int32_t);
 }
 
-int eh_tr_fwd3_ok(const TrFwdArgs* a, int mode) { return mode == 0 && fwd3_fits(*a) ? 1 : 0; }
-
-// layer 0 (tr_fwd3) with the previous step's optimizer (mode 2) fused in: every weight
-// segment as vectorised wave jobs (tr_opt_wave_plan), one block per CU (all resident for
-// the grid barrier), the barrier words and the pending flag given
-hipError_t eh_tr_fwd_fused(const TrFwdArgs* a, const TrOptArgs* o, int feat_fp32, hipStream_t s) {
-  if (!fwd3_fits(*a) || !a->gbar || !o->pending || o->nwt < 1 || o->nseg < 1 || o->nseg > kTrMaxSegs ||
-      !o->p || !o->m || !o->v || !o->step || !o->loss_acc || !o->loss_out || !o->head_part)
-    return hipErrorInvalidValue;
-  int wt = 0;
-  for (int i = 0; i < o->nseg; ++i) {
-    const TrSeg& g = o->seg[i];
-    if (!g.part || g.S < 1 || g.wt0 != wt || g.sgrp != tr_seg_groups(g)) return hipErrorInvalidValue;
-    if (g.cols > 0 && (g.cols % 32 != 0 || g.rows % 8 != 0 || g.off % 4 != 0 || g.n % 4 != 0 ||
-                       static_cast<int64_t>(g.rows) * g.cols != g.n))
-      return hipErrorInvalidValue;
-    if (g.cols == 0 && (g.sh || g.shT)) return hipErrorInvalidValue;
-    wt += tr_seg_wave_jobs(g);
-  }
-  if (wt != o->nwt) return hipErrorInvalidValue;
-  const size_t l3 = eh_tr_fwd3_lds(a->D, a->FL);
-  const int ntiles = static_cast<int>(a->M / kF2Rows);
-  const int cus = tr_num_cus();
-  if (cus < 1) return hipErrorInvalidValue;
-  const int grid = ntiles < cus ? ntiles : cus;
-#define TR_FWD3F(FT)                                                                                         \
-  do {                                                                                                       \
-    EULER_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(tr_fwd3_kernel<FT, 1>),               \
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(l3)));   \
-    hipLaunchKernelGGL((tr_fwd3_kernel<FT, 1>), dim3(static_cast<uint32_t>(grid)), dim3(kF3Threads), l3, s, *a, \
-                       ntiles, *o);                                                                          \
-    return hipGetLastError();                                                                                \
-  } while (0)
-  if (feat_fp32) TR_FWD3F(float);
-  TR_FWD3F(bf16_t);
-#undef TR_FWD3F
-}
-
-hipError_t eh_tr_clear_flag(int32_t* flag, hipStream_t s) {
-  if (!flag) return hipErrorInvalidValue;
-  return hipMemsetAsync(flag, 0, sizeof(int32_t), s);
-}
-
 hipError_t eh_tr_opt(const TrOptArgs* ain, int mode, hipStream_t s) {
   TrOptArgs A = *ain;
   const TrOptArgs* a = &A;
-  if (a->check_pending && !a->pending) return hipErrorInvalidValue;
   if (!(mode == 1 || mode == 2)) A.nsample = 0;  // the sampler runs in modes 1/2 only
   if (mode == 3) A.ngather = 0;
   if (a->nseg < 1 || a->nseg > kTrMaxSegs || a->nblk < 1) return hipErrorInvalidValue;
@@ -2724,7 +2241,6 @@ hipError_t eh_tr_opt(const TrOptArgs* ain, int mode, hipStream_t s) {
     } else {
       if (g.sh || g.shT || g.sgrp != tr_seg_groups(g)) return hipErrorInvalidValue;  // tr_seg_prepare
     }
-    if (g.vec != tr_seg_vec(g)) return hipErrorInvalidValue;
     blk += tr_seg_blocks(g);
   }
   if (blk != a->nblk) return hipErrorInvalidValue;

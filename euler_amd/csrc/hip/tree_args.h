@@ -12,8 +12,6 @@
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
 
-#include <cstdlib>
-
 namespace euler_hip {
 
 constexpr int kTrMaxProbs = 6;
@@ -113,8 +111,6 @@ struct TrFwdArgs {
   uint16_t* a_rows;      // pipelined step: [M][2D] row-major A rows ([self | mean]) written by the
                          // gather blocks of the previous optimizer launch, read by the GEMM-only
                          // forward (mode 3)
-  uint32_t* gbar;        // tr_fwd3 with the optimizer fused: grid barrier words [arrivals,
-                         // generation, timed-out flag, unused]
 };
 
 // head: last SAGE conv + fc + out_fc + sigmoid-CE + backward down to dA, kTrHeadRows roots / block
@@ -202,44 +198,21 @@ struct TrSeg {
   uint16_t* sh;        // optional fm [rows][cols]
   uint16_t* shT;       // optional fm [cols][rows]
   int32_t sgrp;        // vector segments: slab groups per element (1 or 4; tr_seg_prepare)
-  int32_t vec;         // weight segments: one 8 x 32 sub-tile per wave, 4 consecutive columns
-                       // per lane (float4 loads and stores), 4 per block (tr_seg_prepare)
-  int32_t wt0;         // first wave job of the segment when the optimizer runs as wave jobs
-                       // inside the forward (tr_opt_wave_plan)
 };
 // vector segments with many split-K slabs (the fc bias: one slab per head block) spread each
 // element's slab sum over 4 threads (256 / 4 elements per block): one round of 16 loads in
 // flight per thread instead of S / 16 dependent rounds, which made the bias block the tail
 // of the optimizer launch.  Returns the segment's block count.
 inline int tr_seg_groups(const TrSeg& s) { return s.cols == 0 && s.S > 16 ? 4 : 1; }
-// weight segments at a 16-byte aligned offset take the vectorised wave sub-tiles
-// (EULER_AMD_OPT_VEC=1; opt-in until measured on the box)
-inline int tr_seg_vec(const TrSeg& s) {
-  static const bool on = [] {
-    const char* e = std::getenv("EULER_AMD_OPT_VEC");
-    return e && e[0] == '1';
-  }();
-  return on && s.cols > 0 && s.cols % 32 == 0 && s.rows % 8 == 0 && s.off % 4 == 0 && s.n % 4 == 0 ? 1 : 0;
-}
 inline int tr_seg_blocks(const TrSeg& s) {
-  if (s.cols > 0) return tr_seg_vec(s) ? ((s.rows / 8) * (s.cols / 32) + 3) / 4 : (s.rows / 8) * (s.cols / 32);
+  if (s.cols > 0) return (s.rows / 8) * (s.cols / 32);
   const int64_t per = 256 / tr_seg_groups(s);
   return static_cast<int>((s.n + per - 1) / per);
 }
 inline int tr_seg_prepare(TrSeg& s) {
   s.sgrp = tr_seg_groups(s);
-  s.vec = tr_seg_vec(s);
   return tr_seg_blocks(s);
 }
-// wave jobs of a segment when the optimizer runs inside the forward launch: weight segments
-// one 8 x 32 sub-tile each (vectorised), vector segments 64 / groups elements each
-inline int tr_seg_wave_jobs(const TrSeg& s) {
-  if (s.cols > 0) return (s.rows / 8) * (s.cols / 32);
-  const int64_t per = 64 / tr_seg_groups(s);
-  return static_cast<int>((s.n + per - 1) / per);
-}
-struct TrOptArgs;
-inline bool tr_opt_wave_plan(TrOptArgs& o);
 struct TrOptArgs {
   float *p, *g, *m, *v;
   uint16_t* g16;  // optional bf16 gradient (data parallel: the all-reduce moves half the bytes);
@@ -265,23 +238,7 @@ struct TrOptArgs {
   int32_t gat_fp32;        //   feature table dtype
   int32_t gather_first;    //   gather tiles before the parameter / sampler blocks in the grid
   int32_t opt_tpb;         //   with gather tiles: parameter tiles per block (fewer, longer blocks)
-  int32_t nwt;             // wave jobs of every segment (tr_opt_wave_plan; optimizer in the forward)
-  int32_t* pending;        // device flag: the last dW's partials are not applied yet (fused optimizer)
-  int32_t check_pending;   // standalone launch: every block returns when *pending == 0 (a flush)
 };
-// the optimizer as wave jobs (inside tr_fwd3): every weight segment vectorised; false if not
-inline bool tr_opt_wave_plan(TrOptArgs& o) {
-  int wt = 0;
-  for (int k = 0; k < o.nseg; ++k) {
-    TrSeg& s = o.seg[k];
-    if (s.cols > 0 && !(s.cols % 32 == 0 && s.rows % 8 == 0 && s.off % 4 == 0 && s.n % 4 == 0)) return false;
-    s.sgrp = tr_seg_groups(s);
-    s.wt0 = wt;
-    wt += tr_seg_wave_jobs(s);
-  }
-  o.nwt = wt;
-  return true;
-}
 
 // one launch for every dW of the step: routed problems first (their blocks, S % 8 == 0),
 // then the stored-G problems grouped
@@ -292,7 +249,6 @@ struct TrDwLaunch {
   int32_t rwg[3];       // block prefix of the routed problems
   int32_t route_impl;   // 0: G^T tile built once per block in LDS; 1: built per wave in registers
   long long* prof;      // optional [route blocks][8] wall-clock stamps (diagnostics)
-  int32_t* pending;     // optional: set to 1 (the partials await the fused optimizer)
 };
 
 }  // namespace euler_hip
@@ -312,10 +268,6 @@ hipError_t eh_tr_dw(euler_hip::TrDwLaunch* p, hipStream_t s);
 // 3: shadows only (after an external parameter write).  Modes 1/2 also run a->nsample
 // sampler blocks.
 hipError_t eh_tr_opt(const euler_hip::TrOptArgs* a, int mode, hipStream_t s);
-int eh_tr_fwd3_ok(const euler_hip::TrFwdArgs* a, int mode);
-hipError_t eh_tr_fwd_fused(const euler_hip::TrFwdArgs* a, const euler_hip::TrOptArgs* o, int feat_fp32,
-                           hipStream_t s);
-hipError_t eh_tr_clear_flag(int32_t* flag, hipStream_t s);
 size_t eh_tr_fwd_lds(int D, int H, int bm, int FL, int mode);
 size_t eh_tr_fwd2_lds(int D, int FL);
 size_t eh_tr_head_lds(int Hin2, int H, int E, int C, int label_mode);

@@ -373,7 +373,6 @@ class SageTrainer:
     # ------------------------------------------------------------------ parameters / state
     def load_logical(self, logical):
         """Set the weights from logical (unpadded, reference-named) tensors."""
-        self.flush()  # a pending update belongs to the state being replaced
         if self.on_gpu:
             self._pack({k: torch.as_tensor(v) for k, v in logical.items()}, self.flat)
             self.refresh_shadows()
@@ -389,7 +388,6 @@ class SageTrainer:
             self.plan.opt(3)
 
     def logical_params(self):
-        self.flush()
         if self.on_gpu:
             return self._unpack(self.flat.detach())
         return {k: v.detach().clone() for k, v in self._cpu_params.items()}
@@ -407,7 +405,6 @@ class SageTrainer:
 
     def trainer_state(self):
         """Optimizer slots (reference names), step and the device RNG (seed, counter)."""
-        self.flush()
         if self.on_gpu:
             m, v = self._unpack(self.m), self._unpack(self.v)
             step = int(self._step.item())
@@ -421,13 +418,11 @@ class SageTrainer:
     def dp_state_tensors(self):
         """tensors that must be equal on every data-parallel rank (parameters, optimizer
         slots, step): what a re-synchronisation broadcasts from rank 0"""
-        self.flush()
         if self.on_gpu:
             return [self.flat, self.m, self.v, self._step]
         return [t.data for t in self._cpu_params.values()] + list(self._cpu_m.values()) + list(self._cpu_v.values())
 
     def load_trainer_state(self, st):
-        self.flush()  # a pending update belongs to the state being replaced
         self.graph.rng.copy_(torch.as_tensor(st["rng"]).to(self.graph.rng))
         self.step_count = int(st["step"])
         self._primed = False
@@ -453,35 +448,10 @@ class SageTrainer:
             self.fshard.exchange(torch.cat([self.nodes, self.leaf]), pos_out=self._fpos)
         self.plan.fwd()
 
-    # ------------------------------------------------------------------ fused optimizer
-    @property
-    def fused(self) -> bool:
-        plan = getattr(self, "plan", None) if self.on_gpu else None
-        return bool(plan is not None and plan.fused())
-
-    def set_fused(self, on: bool = True) -> bool:
-        """Fold the optimizer launch into the next step's forward launch (single process,
-        2 hops, tr_fwd3): the step becomes fwd (+ the previous step's update) / head / dW.
-        The last step's update stays pending until the next step or :meth:`flush`; every
-        reader of the weights, the optimizer state or the loss flushes first.  Returns
-        whether the mode is on (False where the plan does not allow it)."""
-        if not self.on_gpu:
-            return False
-        on = bool(on) and self.plan.fuse_ok()
-        self.plan.set_fused(on)
-        return on
-
-    def flush(self):
-        """apply a pending fused update (no-op otherwise)"""
-        if self.fused:
-            self.plan.flush()
-
     def forward_backward(self):
         """Sampling, forward and backward of one step; the split-K partials are reduced
         into :attr:`grad` (the all-reduce point of data parallelism).  The sample buffers
         keep this step's batch (:meth:`samples`); the next call samples again."""
-        if self.fused:
-            self.set_fused(False)
         p = self.plan
         self._prime()
         self._fwd()
@@ -533,8 +503,6 @@ class SageTrainer:
         self.step_count += 1
         if not self.on_gpu:
             return self._cpu_step(grad_sync)
-        if grad_sync is not None and self.fused:
-            self.set_fused(False)  # the fused update is single-process only
         p = self.plan
         self._prime()
         if self.pipelined and self._gathered:
@@ -545,9 +513,7 @@ class SageTrainer:
         p.head(None, not smp_opt)
         p.bwd()
         gat = self.pipelined  # this launch gathers the batch the head just sampled
-        if grad_sync is None and self.fused:
-            p.dw(self._dw_all)  # its partials are applied by the next forward launch (or flush)
-        elif grad_sync is None:
+        if grad_sync is None:
             p.dw(self._dw_all)
             p.opt(2, 1.0, smp_opt, gat)
         elif len(self.grad_buckets()) == 1:
@@ -695,13 +661,11 @@ class SageTrainer:
     @property
     def loss(self) -> torch.Tensor:
         """loss of the last completed step (device scalar)"""
-        self.flush()
         return self.loss_out if self.on_gpu else self._cpu_loss
 
     def metric(self) -> float:
         """streaming micro-F1 (threshold 0.5) since the last :meth:`reset_metric`
         (reference metrics.f1_score)"""
-        self.flush()
         tp, fp, fn = (self.counts.tolist() if self.on_gpu else self._cpu_counts)
         return 2.0 * tp / max(2.0 * tp + fp + fn, 1e-12)
 

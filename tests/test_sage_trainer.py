@@ -137,7 +137,7 @@ CASES = [
     dict(fanouts=[4, 3, 2], dims=[64, 64, 64, 32], C=32),                     # 3 hops (inner layer + bwd)
     dict(fanouts=[3, 20, 2], dims=[64, 128, 64, 32], C=16, mode="dense", self_loops=True),
     dict(fanouts=[5, 3], dims=[64, 64, 32], C=32, B=1024),                    # 64 fc-bias slabs: grouped reduce
-    # the pipelined layer-0 kernel (tr_fwd3: D % 64, H % 64) at every sibling-group size
+    # every sibling-group size of the layer-0 kernel at D % 64 == 0
     dict(fanouts=[3, 3], dims=[64, 64, 32], C=32, D=64, B=256),                # 4-row groups
     dict(fanouts=[5, 4], dims=[128, 64, 32], C=32, D=64, B=256, self_loops=True),  # 8-row groups
     dict(fanouts=[10, 3], dims=[64, 64, 32], C=32, D=128, B=512),              # 16-row groups
@@ -165,8 +165,7 @@ def test_tree_step_matches_fp32_oracle(cuda, cfg):
     n = tr.graph.num_rows
     assert int(roots.min()) >= 0 and int(roots.max()) < n
     assert int(nodes.max()) < n and int(leaf.max()) < n
-    # the update (vectorised 8 x 128 tiles where the widths allow, 8 x 32 otherwise) is Adam
-    # in fp32 on the reduced gradient
+    # the update is Adam in fp32 on the reduced gradient
     p0, m0, v0, g = tr.flat.clone(), tr.m.clone(), tr.v.clone(), tr.grad.clone()
     t = float(tr._step.item())
     tr.optimizer_step()
@@ -421,40 +420,3 @@ def test_device_path_tracks_engine_path(tmp_path, monkeypatch):
     dev = main(base + ["--model_dir", str(tmp_path / "dev"), "--device_graph"], model="graphsage")
     assert math.isfinite(eng["loss"]) and math.isfinite(dev["loss"])
     assert abs(dev["loss"] - eng["loss"]) < 0.12 * eng["loss"], (eng["loss"], dev["loss"])
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("captured", [False, True])
-def test_fused_optimizer_matches_separate_launch(cuda, captured):
-    """The optimizer riding in the next forward launch (wave jobs + grid barrier, pending
-    flag set by dW) trains like the separate optimizer launch: same weights after the same
-    steps (bias sums reduce in another order: allclose), the loss of the last step after a
-    flush, no barrier wait that gave up."""
-    cfg = dict(fanouts=[10, 3], dims=[64, 64, 32], C=32, D=128, B=512)
-    a = _trainer(cuda, **cfg)
-    b = _trainer(cuda, **cfg)
-    if not b.set_fused(True):
-        pytest.skip("the fused optimizer needs the pipelined layer-0 kernel (EULER_AMD_FWD3=1)")
-    assert b.fused
-    n = 12
-    for _ in range(n):
-        a.step()
-    if captured:
-        b.capture(warmup=2, steps=4)
-        b.replay_steps(n - 2)
-    else:
-        for _ in range(n):
-            b.step()
-    b.flush()
-    torch.cuda.synchronize()
-    pa, pb = a.logical_params(), b.logical_params()
-    for k in pa:
-        assert torch.allclose(pa[k], pb[k], rtol=1e-4, atol=1e-5), k
-    assert abs(float(a.loss.item()) - float(b.loss.item())) < 1e-4
-    assert int(b.plan.barrier_timeouts()) == 0
-    # flushing twice applies nothing twice
-    before = b.flat.clone()
-    b.flush()
-    b.flush()
-    torch.cuda.synchronize()
-    assert torch.equal(before, b.flat)

@@ -60,8 +60,6 @@ def main():
         res[f"dw[{i}]"] = round(timeit(lambda: p.dw([i]), args.reps), 2)
     res["dw_splits"] = p.splits()
     res["route_profile"] = route_profile(tr)
-    if os.environ.get("EULER_AMD_FUSE_OPT", "0") == "1":
-        res["optimizer_in_forward"] = bool(tr.set_fused(True))
     tr.capture(steps=4)
     res["graph_step"] = round(timeit(lambda: tr.replay(1), args.reps), 2)
     res["graph_step_x4"] = round(timeit(lambda: tr.replay_steps(4), args.reps) / 4, 2)  # per step
@@ -84,9 +82,7 @@ def main():
         live = raw[:, 0] > 0
         f = f[live]  # blocks of the launched kernel (64-row tiles: half the 32-row count)
         cu = raw[live, 6]
-        # stamps 0..5 (slot 6 holds the CU id): tr_fwd2 ids / gather / kt / gemm / epilogue,
-        # tr_fwd3 ids / first gather / tile 0 / remaining tiles (slot 5 unused)
-        last = 5 if bool((raw[live, 5] > 0).all()) else 4
+        last = 5  # stamps 0..5: ids / gather / kt / gemm / epilogue (slot 6: the CU id)
         st = (f[:, 0] - f[:, 0].min())
         uniq, cnt = torch.unique(cu, return_counts=True)
         print("fwd blocks", int(live.sum()), "distinct CUs", int(uniq.numel()), "max blocks per CU", int(cnt.max()),
@@ -94,7 +90,7 @@ def main():
               [round(float(torch.quantile(st, q)), 2) for q in (0.5, 0.9, 0.99)], round(float(st.max()), 2),
               "end-time spread (us)", round(float((f[:, last] - f[:, last].min()).max()), 2))
         f0 = f[:, 0].min()
-        names = "ids, gather, kt, gemm, epilogue" if last == 5 else "ids, first gather, tile 0, later tiles"
+        names = "ids, gather, kt, gemm, epilogue"
         fph = [(f[:, k] - f[:, k - 1]).mean().item() for k in range(1, last + 1)]
         print(f"fwd phases (us, mean over blocks: {names}):", [round(v, 2) for v in fph],
               "span", round(float(f[:, last].max() - f0), 2), "start skew", round(float(f[:, 0].max() - f0), 2),
