@@ -58,11 +58,22 @@ class RGCNTransE(nn.Module):
                                     for _ in range(layers)])
         self.margin = margin
 
+    self_drop = 0.0  # training: probability of dropping an entity's own (self-loop) input
+    self_keep = None  # evaluation: [Ne] bool, entities whose own embedding is used (None: all)
+
     def encode(self, edge_index, edge_rel):
         n = self.ent.shape[0]
         h = self.ent
         for i, conv in enumerate(self.convs):
-            h = conv([h, h], edge_index, (n, n), edge_attr=edge_rel)
+            x0 = h
+            if self.training and self.self_drop > 0:
+                # self-loop dropout (the R-GCN paper drops self-loop edges more than others):
+                # an entity whose own input is dropped must be placed by its neighbours, so the
+                # relation transforms learn to carry type information (inductive use)
+                x0 = h * (torch.rand(n, 1, device=h.device) >= self.self_drop).to(h.dtype)
+            elif not self.training and self.self_keep is not None:
+                x0 = h * self.self_keep.view(n, 1).to(h.dtype)
+            h = conv([x0, h], edge_index, (n, n), edge_attr=edge_rel)
             if i + 1 < len(self.convs):
                 h = F.relu(h)
         return h
@@ -104,6 +115,9 @@ def main(argv=None):
                         "dataset/synthetic.py typed_kg — rank the type hub of cold entities, whose type only "
                         "their neighbourhood carries")
     p.add_argument("--cold-frac", type=float, default=0.1)
+    p.add_argument("--self-drop", type=float, default=0.0,
+                   help="R-GCN self-loop dropout while training; cold entities (never in a loss triple) are then "
+                        "placed by their neighbours alone at evaluation (inductive)")
     p.add_argument("--no-graph", action="store_true", help="eager steps (default: one hipGraph per step)")
     p.add_argument("--device", default="cuda", help="cpu: torch reference ops (exploration only, eager)")
     p.add_argument("--eval-after", type=int, default=2000,
@@ -157,6 +171,7 @@ def main(argv=None):
     model = RGCNTransE(args.num_ent, args.num_rel, args.dim, layers=args.layers, margin=args.margin,
                        num_bases=args.num_bases).to(dev)
     model.norm = norm
+    model.self_drop = float(args.self_drop)
 
     def batch():
         idx = pool[torch.randint(0, pool.numel(), (args.batch,), device=dev)]
@@ -190,8 +205,16 @@ def main(argv=None):
     def evaluate():
         from euler_amd.dataset.synthetic import rank_metrics, tail_ranks
 
+        model.eval()
+        if args.self_drop > 0 and args.task in ("types", "cold"):
+            # inductive: the test heads' own embeddings never saw a loss triple
+            keep = torch.ones(args.num_ent, dtype=torch.bool, device=dev)
+            keep[te_src] = False
+            model.self_keep = keep
         with torch.no_grad():
             h = model.encode(edge_index, edge_rel).float()
+        model.self_keep = None
+        model.train()
         m = rank_metrics(tail_ranks(h, model.rel, te_src, te_rel, te_dst, normalize=norm))
         return {k: round(v, 4) for k, v in m.items()}
 
@@ -281,6 +304,7 @@ def main(argv=None):
                        "dim": args.dim, "batch_per_gpu": args.batch, "num_negs": args.num_negs,
                        "normalize": norm, "task": args.task, "hipgraph": graph is not None,
                        "lr": args.lr, "margin": args.margin, "num_bases": args.num_bases, "rel_wd": args.rel_wd,
+                       "self_drop": args.self_drop,
                        "parallelism": f"dp{world}", "loss_first_last": [round(first, 4), round(last, 4)],
                        "grad_sync": sync_name, "grad_sync_choice": sync_info or None,
                        "heldout_tail_ranking": {"triples": int(te_src.numel()), "entities": args.num_ent,
