@@ -188,6 +188,9 @@ def main(argv=None):
                        "num_nodes": args.num_nodes, "dim": args.dim, "walks_per_gpu": args.batch,
                        "pairs_per_gpu_step": pairs_per_step, "parallelism": f"dp{world}+sharded-emb",
                        "all_to_all": table_comm, "step_mode": args.mode, "micro_batches": args.micro_batches,
+                       "optimizer_schedule": ("one sparse update per step" if args.micro_batches == 1 else
+                                              "two half-batch sparse updates per step (each micro-batch applies its "
+                                              "own update; not the same optimizer step as one full batch)"),
                        "loss_first_last": [round(first, 4), round(loss_last, 4)],
                        "peak_mem_gib": round(peak, 1), "heldout_link_prediction": heldout},
         }), flush=True)
