@@ -977,14 +977,6 @@ __device__ __forceinline__ void tr_prefetch(const bf16_t* __restrict__ Bf, int c
   for (int s = 0; s < TR_KC; ++s) b[s] = fm_frag(Bf, c, s * 32 < K ? s * 32 : 0, K, lane);
 }
 
-// the fragments of k steps k0 .. k0 + 32 (TR_KC - 1) (out-of-range steps load step 0, unused)
-__device__ __forceinline__ void tr_prefetch_k(const bf16_t* __restrict__ Bf, int col0, int N, int K, int k0, int lane,
-                                              uint4_t (&b)[TR_KC]) {
-  const int c = col0 < N ? col0 : 0;
-#pragma unroll
-  for (int s = 0; s < TR_KC; ++s) b[s] = fm_frag(Bf, c, k0 + s * 32 < K ? k0 + s * 32 : 0, K, lane);
-}
-
 __device__ __forceinline__ void tr_mfma_chunk(const bf16_t* A, int lda, int kc, int K, const uint4_t (&b)[TR_KC],
                                               float4_t (&acc)[HFM][1], int lane) {
   const int lr = lane & 15, lk = (lane >> 4) * 8;
@@ -1113,13 +1105,9 @@ __global__ __launch_bounds__(HNW * 64) void tr_head_kernel(TrHeadArgs a) {
     }
   };
 
-  // P0: A tile -> LDS (+ A_kt); h = relu(A @ W^T).  Both k chunks of the first column job's
-  // weight fragments are in flight before the A tile lands (K = Hin2 <= 512): the GEMM then
-  // waits for no L2 round trip of its own
-  uint4_t pre[TR_KC], pre2[TR_KC];
+  // P0: A tile -> LDS (+ A_kt); h = relu(A @ W^T)
+  uint4_t pre[TR_KC];
   tr_prefetch(a.W, wave * 16, H, Hin2, lane, pre);
-  const bool two = Hin2 > 32 * TR_KC && Hin2 <= 64 * TR_KC;
-  if (two) tr_prefetch_k(a.W, wave * 16, H, Hin2, 32 * TR_KC, lane, pre2);
   const int cpa = Hin2 >> 3;
   for (int it = threadIdx.x; it < HB * cpa; it += NT) {
     const int r = it / cpa, c = it - r * cpa;
@@ -1132,12 +1120,7 @@ __global__ __launch_bounds__(HNW * 64) void tr_head_kernel(TrHeadArgs a) {
   for (int cc = wave * 16; cc < H; cc += HNW * 16) {
     float4_t acc[HFM][1];
     tl_zero(acc);
-    if (two && cc == wave * 16) {
-      tr_mfma_chunk(Aa, lda, 0, Hin2, pre, acc, lane);
-      tr_mfma_chunk(Aa, lda, 32 * TR_KC, Hin2, pre2, acc, lane);
-    } else {
-      tr_gemm(Aa, lda, a.W, cc, Hin2, acc, lane, pre);
-    }
+    tr_gemm(Aa, lda, a.W, cc, Hin2, acc, lane, pre);
     if (cc + HNW * 16 < H) tr_prefetch(a.W, cc + HNW * 16, H, Hin2, lane, pre);
 #pragma unroll
     for (int m = 0; m < HFM; ++m)
@@ -1238,12 +1221,6 @@ __global__ __launch_bounds__(HNW * 64) void tr_head_kernel(TrHeadArgs a) {
     float4_t acc[HFM][1];
     tl_zero(acc);
     tr_gemm(j < nh + ne ? Dl : Ah, j < nh + ne ? ldc : ldh, Bf, cc, K, acc, lane, pre);
-    if (j + HNW < n2) {  // the next job's fragments load under this job's epilogue
-      const bf16_t* Bn;
-      int cn, Kn;
-      job2(j + HNW, Bn, cn, Kn);
-      tr_prefetch(Bn, cn, 1 << 30, Kn, lane, pre);
-    }
     const int col = cc + lr;
     if (j < nh) {
 #pragma unroll
@@ -1274,6 +1251,12 @@ __global__ __launch_bounds__(HNW * 64) void tr_head_kernel(TrHeadArgs a) {
       for (int m = 0; m < HFM; ++m)
         kt_store4(a.emb_kt, r0 + m * 16 + lg * 4, col, E, acc[m][0][0] + b, acc[m][0][1] + b, acc[m][0][2] + b,
                   acc[m][0][3] + b);
+    }
+    if (j + HNW < n2) {
+      const bf16_t* Bn;
+      int cn, Kn;
+      job2(j + HNW, Bn, cn, Kn);
+      tr_prefetch(Bn, cn, 1 << 30, Kn, lane, pre);
     }
   }
   if (a.dA) tr_prefetch(a.WT, wave * 16, Hin2, H, lane, pre);
