@@ -115,6 +115,9 @@ def main(argv=None):
                         "dataset/synthetic.py typed_kg — rank the type hub of cold entities, whose type only "
                         "their neighbourhood carries")
     p.add_argument("--cold-frac", type=float, default=0.1)
+    p.add_argument("--num-types", type=int, default=50, help="types task: type hubs (entities 0 .. n - 1)")
+    p.add_argument("--type-negs", type=int, default=0,
+                   help="types task: corrupt has_type triples with other type hubs (type-constrained negatives)")
     p.add_argument("--self-drop", type=float, default=0.0,
                    help="R-GCN self-loop dropout while training; cold entities (never in a loss triple) are then "
                         "placed by their neighbours alone at evaluation (inductive)")
@@ -145,7 +148,8 @@ def main(argv=None):
     if args.task == "types":
         from euler_amd.dataset.synthetic import typed_kg
 
-        tr_, gr_, te_ = typed_kg(args.num_ent, args.num_rel, args.num_triples, cold_frac=args.cold_frac,
+        tr_, gr_, te_ = typed_kg(args.num_ent, args.num_rel, args.num_triples, num_types=args.num_types,
+                                 cold_frac=args.cold_frac,
                                  seed=args.seed)
         (src, rel, dst), (gsrc, grel, gdst), (te_src, te_rel, te_dst) = (tuple(x.to(dev) for x in t)
                                                                          for t in (tr_, gr_, te_))
@@ -176,6 +180,11 @@ def main(argv=None):
     def batch():
         idx = pool[torch.randint(0, pool.numel(), (args.batch,), device=dev)]
         negs = torch.randint(0, args.num_ent, (args.batch, args.num_negs), device=dev)
+        if args.type_negs and args.task == "types":
+            # type-constrained corruption of has_type triples (relation 0): the negatives are
+            # other type hubs (entities 0 .. num_types - 1), so training separates the hubs
+            hub = torch.randint(0, args.num_types, (args.batch, args.num_negs), device=dev)
+            negs = torch.where((rel[idx] == 0).view(-1, 1), hub, negs)
         return src[idx], rel[idx], dst[idx], negs
 
     model(edge_index, edge_rel, *batch()).backward()  # materialise lazy layers before the optimizer
@@ -304,7 +313,7 @@ def main(argv=None):
                        "dim": args.dim, "batch_per_gpu": args.batch, "num_negs": args.num_negs,
                        "normalize": norm, "task": args.task, "hipgraph": graph is not None,
                        "lr": args.lr, "margin": args.margin, "num_bases": args.num_bases, "rel_wd": args.rel_wd,
-                       "self_drop": args.self_drop,
+                       "self_drop": args.self_drop, "type_negs": bool(args.type_negs),
                        "parallelism": f"dp{world}", "loss_first_last": [round(first, 4), round(last, 4)],
                        "grad_sync": sync_name, "grad_sync_choice": sync_info or None,
                        "heldout_tail_ranking": {"triples": int(te_src.numel()), "entities": args.num_ent,
