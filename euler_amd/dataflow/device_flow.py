@@ -33,7 +33,7 @@ from euler_amd.dataflow.dataflows import Block, DataFlow
 from euler_amd.ops._native import hip, use_hip
 from euler_amd.ops.mp_ops import SegmentIndex
 
-__all__ = ["DeviceFullFlow", "full_neighbors_cpu", "max_out_degree"]
+__all__ = ["DeviceFullFlow", "DeviceSageFlow", "full_neighbors_cpu", "max_out_degree"]
 
 
 def _round_up(x: int, m: int = 256) -> int:
@@ -213,3 +213,71 @@ class DeviceFullFlow:
         """raise if any batch so far exceeded a capacity (host sync)"""
         if int(self.overflow.item()) != 0:
             raise RuntimeError(f"device dataflow capacity exceeded (caps {self.caps}): raise the caps")
+
+
+class DeviceSageFlow:
+    """``SageDataFlow`` on the device with fixed shapes (reference
+    ``tf_euler/python/dataflow/sage_dataflow.py:35-50``; engine twin
+    ``dataflows.SageDataFlow``): per hop ``fanouts[h]`` weighted draws with replacement per
+    node (``DeviceGraph.sample_neighbor``, Philox stream 10 + h), then
+    ``unique([neighbours, previous set])`` in first-occurrence order, the previous set's
+    positions, target-major edges (F per target, then one self loop per target).
+
+    Capacities are exact: hop h's set holds at most ``cap_{h-1} (F_h + 1)`` rows (capped by
+    the graph size), its edge list ``cap_{h-1} F_h`` (+ ``cap_{h-1}`` self loops).  A node
+    without an out-edge of the hop's types draws ``-1`` (the reference draws the padding
+    node ``max_id + 1``, whose features are zero): the message-passing ops drop ``-1``
+    edges, so such a node's mean is over nothing instead of over zero rows — the same 0."""
+
+    def __init__(self, graph, edge_types, fanouts, batch_size: int, add_self_loops: bool = True):
+        self.g = graph
+        self.edge_types = [None if e is None else [int(t) for t in e] for e in edge_types]
+        self.fanouts = [int(f) for f in fanouts]
+        if len(self.edge_types) != len(self.fanouts):
+            raise ValueError("one edge-type list per fanout")
+        self.B = int(batch_size)
+        self.self_loops = bool(add_self_loops)
+        self.caps = []
+        n = self.B
+        for f in self.fanouts:
+            e = n * f + (n if self.self_loops else 0)
+            n_next = min(graph.num_rows, n * (f + 1))
+            self.caps.append((e, n_next))
+            n = n_next
+
+    def node_caps(self):
+        return [self.B] + [n for _, n in self.caps]
+
+    def produce(self, roots: torch.Tensor) -> DataFlow:
+        g = self.g
+        n_id = roots.reshape(-1).long()
+        if n_id.numel() != self.B:
+            raise ValueError(f"expected {self.B} roots, got {n_id.numel()}")
+        dev = n_id.device
+        df = DataFlow(n_id)
+        last_idx = torch.arange(self.B, dtype=torch.long, device=dev)
+        cap_prev = self.B
+        for h, (et, f) in enumerate(zip(self.edge_types, self.fanouts)):
+            cap_e, cap_n = self.caps[h]
+            nbr = g.sample_neighbor(n_id, f, edge_types=et, default=-1, stream_id=10 + h).long().reshape(-1)
+            cat = torch.cat([nbr, n_id])
+            uniq, inv, cnt = _unique_padded(cat)
+            new_n_id = uniq[:cap_n] if uniq.numel() >= cap_n else torch.cat(
+                [uniq, torch.full((cap_n - uniq.numel(),), -1, dtype=uniq.dtype, device=dev)])
+            res_n_id = inv[nbr.numel():]
+            tgt = torch.arange(cap_prev, dtype=torch.long, device=dev).repeat_interleave(f)
+            if self.self_loops:
+                edge_t = torch.cat([tgt, last_idx])
+                edge_s = inv
+            else:
+                edge_t, edge_s = tgt, inv[: nbr.numel()]
+            # an edge of a -1 draw (or of a padding target) carries nothing
+            edge_t = torch.where(edge_s >= 0, edge_t, torch.full_like(edge_t, -1))
+            df.blocks.append(Block(new_n_id, res_n_id, None, torch.stack([edge_t, edge_s]), [cap_prev, cap_n]))
+            df._last = new_n_id
+            ar = torch.arange(cap_n, dtype=torch.long, device=dev)
+            cnt_n = torch.clamp(cnt.reshape(()), max=cap_n)
+            last_idx = torch.where(ar < cnt_n, ar, torch.full_like(ar, -1))
+            n_id = new_n_id
+            cap_prev = cap_n
+        return df

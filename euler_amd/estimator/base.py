@@ -434,8 +434,26 @@ class BaseEstimator:
             return KGTrainer.from_model(model, int(self.params["batch_size"]), edge_type, seed=seed * 7919 + self.rank,
                                         device=self.device, optimizer=self.params.get("optimizer", "adam"),
                                         learning_rate=float(self.params.get("learning_rate", 0.001)))
-        from euler_amd.models.unsupervised import BaseNode2Vec
+        from euler_amd.models.unsupervised import BaseNode2Vec, GraphAutoEncoder
 
+        if isinstance(model, GraphAutoEncoder):
+            # GAE (sage / gcn encoder): roots, positives, negatives and the encoder's blocks
+            # on the HBM graph (models/gae_trainer.py)
+            from euler_amd.models.gae_trainer import GaeTrainer
+
+            self._prepare(first)
+            if self._sync is not None:
+                self._sync.remove()
+            gnn = model.gnn
+            nt = self.params.get("train_node_type", model.node_type)
+            node_type = -1 if nt in (None, -1, "-1") else int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
+            fdt = torch.float32 if self.params.get("device_feature_dtype", "bf16") == "fp32" else torch.bfloat16
+            graph = DeviceGraph.from_engine(node_type=node_type, features=gnn.feature_idx,
+                                            feature_dims=gnn.feature_dim, feature_dtype=fdt,
+                                            seed=seed * 7919 + self.rank, device=self.device)
+            return GaeTrainer(model, graph, int(self.params["batch_size"]),
+                              optimizer=self.params.get("optimizer", "adam"),
+                              learning_rate=float(self.params.get("learning_rate", 0.001)))
         if isinstance(model, BaseNode2Vec):
             # DeepWalk / Node2Vec: walks, pairs, negatives and the row-sparse SGNS update on the
             # HBM graph (models/deepwalk_step.py)

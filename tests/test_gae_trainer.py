@@ -1,0 +1,91 @@
+"""GaeEstimator(device_graph=True) for the graph auto-encoder (models/gae_trainer.py;
+reference euler_estimator/python/gae_estimator.py:26-51, mp_utils/base_gae.py:23-70) and the
+fixed-shape device SageDataFlow it builds the encoder's blocks with."""
+import numpy as np
+import pytest
+import torch
+
+import euler_amd as ea
+from euler_amd import models as Z
+from euler_amd.dataset import get_dataset
+from euler_amd.estimator import GaeEstimator
+
+
+@pytest.fixture(scope="module")
+def _cora(tmp_path_factory):
+    ds = get_dataset("cora", data_dir=str(tmp_path_factory.mktemp("cora")), scale=0.08)
+    ds.get_data_dir()
+    return ds
+
+
+@pytest.fixture
+def cora(_cora):
+    _cora.load_graph()
+    ea.set_seed(3)
+    return _cora
+
+
+F = 1433
+
+
+def _params(ds, tmp, device, **kw):
+    tnt = ds.train_node_type[0] if isinstance(ds.train_node_type, list) else ds.train_node_type
+    p = {"model_dir": str(tmp / "ckpt"), "batch_size": 16, "total_step": 24, "optimizer": "adam",
+         "learning_rate": 0.01, "log_steps": 8, "train_node_type": tnt, "device": device, "device_graph": True,
+         "seed": 5, "device_feature_dtype": "fp32"}
+    p.update(kw)
+    return p
+
+
+def _model(enc, ds):
+    torch.manual_seed(0)
+    return Z.GraphAutoEncoder(enc, [16, 8], [3], [["train"]], "feature", F, "train", ["train"], ds.max_node_id,
+                              num_negs=3)
+
+
+def test_device_sage_flow_blocks_are_consistent(cora):
+    """each hop: the previous set sits at res_n_id inside the new set, every edge joins a
+    valid target to a valid source, F draws + one self loop per target"""
+    from euler_amd.dataflow.device_flow import DeviceSageFlow
+    from euler_amd.graph.device_graph import DeviceGraph
+
+    g = DeviceGraph.from_engine(device="cpu", seed=2)
+    flow = DeviceSageFlow(g, [None, None], [4, 3], 32, add_self_loops=True)
+    roots = g.sample_node(32).long()
+    df = flow.produce(roots)
+    prev = roots
+    for blk, (e_cap, n_cap) in zip(df.blocks, flow.caps):
+        n_id, res = blk.n_id, blk.res_n_id
+        assert n_id.numel() == n_cap and blk.edge_index.shape[1] == e_cap
+        ok = prev >= 0
+        assert torch.equal(n_id[res[ok]], prev[ok])
+        t, s = blk.edge_index
+        live = t >= 0
+        assert bool((s[live] >= 0).all()) and bool((n_id[s[live]] >= 0).all())
+        assert int(t[live].max()) < prev.numel()
+        # every target keeps its self loop (the last prev.numel() edges)
+        assert torch.equal(n_id[s[-prev.numel():][ok]], prev[ok])
+        prev = n_id
+
+
+@pytest.mark.parametrize("enc", ["sage", "gcn"])
+def test_gae_device_path_cpu(cora, tmp_path, enc):
+    m = _model(enc, cora)
+    est = GaeEstimator(m, _params(cora, tmp_path, "cpu"))
+    res = est.train()
+    assert res["step"] == 24 and np.isfinite(res["loss"]) and 0.0 < res["acc"] <= 1.0
+    # resume continues the sampler's counter
+    ctr = int(est.device_trainer.graph.rng[1])
+    est2 = GaeEstimator(_model(enc, cora), _params(cora, tmp_path, "cpu", total_step=32))
+    assert est2.train()["step"] == 32
+    assert int(est2.device_trainer.graph.rng[1]) == ctr + 8
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("enc", ["sage", "gcn"])
+def test_gae_device_path_gpu_captured(cora, tmp_path, cuda, enc):
+    m = _model(enc, cora)
+    est = GaeEstimator(m, _params(cora, tmp_path, "cuda", total_step=64, log_steps=32, steps_per_graph=8))
+    res = est.train()
+    tr = est.device_trainer
+    assert res["step"] == 64 and np.isfinite(res["loss"]) and tr.captures >= 1
