@@ -479,8 +479,14 @@ class BaseEstimator:
         nt = self.params.get("train_node_type", -1)
         node_type = -1 if nt in (None, -1, "-1") else int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
         fdt = torch.float32 if self.params.get("device_feature_dtype", "bf16") == "fp32" else torch.bfloat16
-        if isinstance(getattr(gnn, "sampler", None), GCNDataFlow):
-            # GCN / APPNP / SGCN / TAGCN / ... : full-neighbourhood blocks built on the device
+        from euler_amd.convolution.convs import SAGEConv
+        from euler_amd.dataflow.dataflows import SageDataFlow
+
+        sampled_other = isinstance(getattr(gnn, "sampler", None), SageDataFlow) and not unsup and \
+            not all(isinstance(c, SAGEConv) for c in gnn.convs)
+        if isinstance(getattr(gnn, "sampler", None), GCNDataFlow) or sampled_other:
+            # GCN / APPNP / SGCN / TAGCN / ... : full-neighbourhood blocks built on the device;
+            # other convolutions on the sampled flow: fixed-fanout blocks built on the device
             from euler_amd.models.full_trainer import FullFlowTrainer
 
             if self._sync is not None:

@@ -43,7 +43,7 @@ class FullFlowTrainer(CapturedTrainer):
     metric_name = "f1"
 
     def __init__(self, model, graph, batch_size, masks, add_self_loops=True, features=None, labels=None,
-                 optimizer="adam", learning_rate=0.01, caps=None):
+                 optimizer="adam", learning_rate=0.01, caps=None, flow=None):
         self.gnn = model.gnn
         self.graph = graph
         self.B = int(batch_size)
@@ -53,7 +53,9 @@ class FullFlowTrainer(CapturedTrainer):
             raise ValueError("the device graph needs dense features and labels (DeviceGraph.from_engine)")
         self.features = feats.to(graph.device)
         self.labels = labs.to(graph.device).float()
-        self.flow = DeviceFullFlow(graph, masks, self.B, add_self_loops, caps)
+        # the full-neighbourhood flow by default; a given flow (DeviceSageFlow for models on
+        # the sampled SageDataFlow whose convolutions are not the fused SAGE kernels)
+        self.flow = flow if flow is not None else DeviceFullFlow(graph, masks, self.B, add_self_loops, caps)
         self.counts = torch.zeros(3, dtype=torch.int64, device=graph.device)
         super().__init__(model, graph, graph.device, optimizer, learning_rate)
 
@@ -65,15 +67,22 @@ class FullFlowTrainer(CapturedTrainer):
         import euler_amd.ops.graph_api as ge
         from euler_amd.dataflow.dataflows import GCNDataFlow
 
+        from euler_amd.dataflow.dataflows import SageDataFlow
+        from euler_amd.dataflow.device_flow import DeviceSageFlow
+
         flow = getattr(model.gnn, "sampler", None)
-        if not isinstance(flow, GCNDataFlow):
-            raise ValueError("FullFlowTrainer trains models on the full-neighbourhood flow (GCNDataFlow)")
-        masks = []
+        if not isinstance(flow, (GCNDataFlow, SageDataFlow)):
+            raise ValueError("FullFlowTrainer trains models on the full-neighbourhood flow (GCNDataFlow) or the "
+                             "sampled SageDataFlow")
+        ets = []
         for m in flow.metapath:
             ids = None if m is None else [int(t) for t in np.asarray(ge.get_edge_type_id(m)).reshape(-1)]
-            masks.append(graph._mask(None if ids is None or any(t < 0 for t in ids) else ids))
-        return cls(model, graph, batch_size, masks, add_self_loops=bool(flow.add_self_loops), optimizer=optimizer,
-                   learning_rate=learning_rate, **kw)
+            ets.append(None if ids is None or any(t < 0 for t in ids) else ids)
+        dflow = None
+        if isinstance(flow, SageDataFlow):
+            dflow = DeviceSageFlow(graph, ets, flow.fanouts, batch_size, bool(flow.add_self_loops))
+        return cls(model, graph, batch_size, [graph._mask(e) for e in ets], add_self_loops=bool(flow.add_self_loops),
+                   optimizer=optimizer, learning_rate=learning_rate, flow=dflow, **kw)
 
     def _materialize(self):
         """one no-grad pass so lazy layers get their shapes (they keep the values the

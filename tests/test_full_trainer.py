@@ -89,6 +89,30 @@ def test_estimator_device_graph_gcn_trains_and_resumes_cpu(tmp_path, monkeypatch
     assert st["device_trainer"]["step"] == 15
 
 
+def test_estimator_device_graph_sampled_flow_other_conv_cpu(tmp_path):
+    """a non-SAGE convolution on the sampled SageDataFlow trains on the device path through
+    the fixed-shape DeviceSageFlow (the fused GraphSAGE kernels take SAGEConv only)"""
+    from euler_amd import models as Z
+    from euler_amd.dataflow.device_flow import DeviceSageFlow
+    from euler_amd.dataset import get_dataset
+    from euler_amd.estimator import NodeEstimator
+    from euler_amd.models.full_trainer import FullFlowTrainer
+
+    ds = get_dataset("ppi", data_dir=str(tmp_path / "ppi"), scale=0.05)
+    ds.load_graph()
+    tnt = ds.train_node_type[0] if isinstance(ds.train_node_type, list) else ds.train_node_type
+    torch.manual_seed(0)
+    m = Z.SupervisedGNN("gcn", "sage", [16, 16, ds.label_dim], [5, 3], [["train"], ["train"]], "feature",
+                        ds.feature_dim, "label", ds.label_dim, max_id=ds.max_node_id)
+    p = {"model_dir": str(tmp_path / "ckpt"), "batch_size": 32, "total_step": 12, "optimizer": "adam",
+         "learning_rate": 0.01, "log_steps": 6, "train_node_type": tnt, "device": "cpu", "device_graph": True,
+         "seed": 2, "device_feature_dtype": "fp32"}
+    est = NodeEstimator(m, p)
+    res = est.train()
+    assert res["step"] == 12 and math.isfinite(res["loss"])
+    assert isinstance(est.device_trainer, FullFlowTrainer) and isinstance(est.device_trainer.flow, DeviceSageFlow)
+
+
 # ----------------------------------------------------------------------------------------- GPU
 
 @pytest.mark.gpu
