@@ -31,14 +31,12 @@ import time
 
 import torch
 import torch.distributed as dist
-import torch.nn as nn
-import torch.nn.functional as F
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-from euler_amd.convolution import RelationConv  # noqa: E402
+from euler_amd.models.rgcn_kg_step import RgcnTransE, RgcnTransEStep  # noqa: E402
 from euler_amd.ops import gnn_ops  # noqa: E402
 
 
@@ -47,43 +45,6 @@ def synthetic_kg(num_ent, num_rel, num_triples, seed, device, num_test=5000):
 
     train, test = lattice_kg(num_ent, num_rel, num_triples, num_test, seed=seed)
     return tuple(t.to(device) for t in train), tuple(t.to(device) for t in test)
-
-
-class RGCNTransE(nn.Module):
-    def __init__(self, num_ent, num_rel, dim, layers=1, margin=1.0, num_bases=0):
-        super().__init__()
-        self.ent = nn.Parameter(torch.randn(num_ent, dim) * 0.1)
-        self.rel = nn.Parameter(torch.randn(num_rel, dim) * 0.1)
-        self.convs = nn.ModuleList([RelationConv(dim, dim, total_relation_num=num_rel, num_bases=num_bases)
-                                    for _ in range(layers)])
-        self.margin = margin
-
-    self_drop = 0.0  # training: probability of dropping an entity's own (self-loop) input
-    self_keep = None  # evaluation: [Ne] bool, entities whose own embedding is used (None: all)
-
-    def encode(self, edge_index, edge_rel):
-        n = self.ent.shape[0]
-        h = self.ent
-        for i, conv in enumerate(self.convs):
-            x0 = h
-            if self.training and self.self_drop > 0:
-                # self-loop dropout (the R-GCN paper drops self-loop edges more than others):
-                # an entity whose own input is dropped must be placed by its neighbours, so the
-                # relation transforms learn to carry type information (inductive use)
-                x0 = h * (torch.rand(n, 1, device=h.device) >= self.self_drop).to(h.dtype)
-            elif not self.training and self.self_keep is not None:
-                x0 = h * self.self_keep.view(n, 1).to(h.dtype)
-            h = conv([x0, h], edge_index, (n, n), edge_attr=edge_rel)
-            if i + 1 < len(self.convs):
-                h = F.relu(h)
-        return h
-
-    norm = True
-
-    def forward(self, edge_index, edge_rel, src, rel, dst, negs):
-        h = self.encode(edge_index, edge_rel).float()
-        pos, neg = gnn_ops.kg_score(h, self.rel, src, dst, rel, negs, "l2", "both", self.norm)
-        return F.relu(self.margin + neg.mean(-1) - pos).mean()
 
 
 def main(argv=None):
@@ -122,6 +83,9 @@ def main(argv=None):
                    help="R-GCN self-loop dropout while training; cold entities (never in a loss triple) are then "
                         "placed by their neighbours alone at evaluation (inductive)")
     p.add_argument("--no-graph", action="store_true", help="eager steps (default: one hipGraph per step)")
+    p.add_argument("--fused", type=int, default=1,
+                   help="1: the fused step (models/rgcn_kg_step.py: hand-written launches only, Philox draws in the "
+                        "scoring kernel) where it applies; 0: the autograd step (torch.randint draws)")
     p.add_argument("--device", default="cuda", help="cpu: torch reference ops (exploration only, eager)")
     p.add_argument("--eval-after", type=int, default=2000,
                    help="keep training (untimed) to this many steps, then rank the held-out triples")
@@ -172,7 +136,7 @@ def main(argv=None):
         keep = cold[te_src] & ~cold[te_dst]               # test: cold head, warm tail
         te_src, te_rel, te_dst = te_src[keep], te_rel[keep], te_dst[keep]
     torch.manual_seed(args.seed * 101 + rank)
-    model = RGCNTransE(args.num_ent, args.num_rel, args.dim, layers=args.layers, margin=args.margin,
+    model = RgcnTransE(args.num_ent, args.num_rel, args.dim, layers=args.layers, margin=args.margin,
                        num_bases=args.num_bases).to(dev)
     model.norm = norm
     model.self_drop = float(args.self_drop)
@@ -181,10 +145,12 @@ def main(argv=None):
         idx = pool[torch.randint(0, pool.numel(), (args.batch,), device=dev)]
         negs = torch.randint(0, args.num_ent, (args.batch, args.num_negs), device=dev)
         if args.type_negs and args.task == "types":
-            # type-constrained corruption of has_type triples (relation 0): the negatives are
-            # other type hubs (entities 0 .. num_types - 1), so training separates the hubs
+            # type-constrained corruption of has_type triples (relation 0): half the negatives
+            # are other type hubs (entities 0 .. num_types - 1), so training separates the hubs;
+            # half of them: uniform corruptions still teach that a non-hub is no type
             hub = torch.randint(0, args.num_types, (args.batch, args.num_negs), device=dev)
-            negs = torch.where((rel[idx] == 0).view(-1, 1), hub, negs)
+            half = (torch.arange(args.num_negs, device=dev) % 2 == 0).view(1, -1)
+            negs = torch.where((rel[idx] == 0).view(-1, 1) & half, hub, negs)
         return src[idx], rel[idx], dst[idx], negs
 
     model(edge_index, edge_rel, *batch()).backward()  # materialise lazy layers before the optimizer
@@ -225,7 +191,13 @@ def main(argv=None):
         model.self_keep = None
         model.train()
         m = rank_metrics(tail_ranks(h, model.rel, te_src, te_rel, te_dst, normalize=norm))
-        return {k: round(v, 4) for k, v in m.items()}
+        out = {k: round(v, 4) for k, v in m.items()}
+        if args.task == "types":
+            # type prediction proper: the true hub ranked among the num_types hubs
+            hubs = torch.arange(args.num_types, device=dev)
+            mt = rank_metrics(tail_ranks(h, model.rel, te_src, te_rel, te_dst, normalize=norm, cands=hubs))
+            out.update({"type_" + k: round(v, 4) for k, v in mt.items()})
+        return out
 
     eval_init = evaluate()
 
@@ -237,7 +209,17 @@ def main(argv=None):
         grad_sync, sync_name, sync_info = make_grad_sync(flat.grad)
         sync_info.pop("xar", None)
 
+    fused = None
+    if args.fused and dev.type == "cuda" and args.self_drop == 0 and args.num_bases == 0 and not (
+            args.type_negs and args.task == "types") and args.dim % 8 == 0:
+        fused = RgcnTransEStep(model, flat, opt, edge_index, edge_rel, (src, rel, dst), pool, args.batch,
+                               args.num_negs, seed=args.seed * 7919 + rank, grad_sync=grad_sync)
+        loss_buf = fused.loss
+
     def step_body():
+        if fused is not None:
+            fused.step()
+            return
         opt.zero_grad()
         loss = model(edge_index, edge_rel, *batch())
         loss.backward()
@@ -271,7 +253,7 @@ def main(argv=None):
     for _ in range(args.warmup):
         step()
     sync()
-    first = float(loss_buf)
+    first = float(loss_buf.reshape(-1)[0])
     if world > 1:
         dist.barrier()
     sync()
@@ -279,7 +261,7 @@ def main(argv=None):
     for _ in range(args.steps):
         step()
     sync()
-    last = float(loss_buf)
+    last = float(loss_buf.reshape(-1)[0])
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
@@ -314,6 +296,7 @@ def main(argv=None):
                        "normalize": norm, "task": args.task, "hipgraph": graph is not None,
                        "lr": args.lr, "margin": args.margin, "num_bases": args.num_bases, "rel_wd": args.rel_wd,
                        "self_drop": args.self_drop, "type_negs": bool(args.type_negs),
+                       "step": "fused (hand-written launches, Philox draws)" if fused is not None else "autograd",
                        "parallelism": f"dp{world}", "loss_first_last": [round(first, 4), round(last, 4)],
                        "grad_sync": sync_name, "grad_sync_choice": sync_info or None,
                        "heldout_tail_ranking": {"triples": int(te_src.numel()), "entities": args.num_ent,

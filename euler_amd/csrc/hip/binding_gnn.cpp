@@ -525,6 +525,80 @@ std::vector<torch::Tensor> kg_fwd(torch::Tensor ent, torch::Tensor rel, torch::T
   return {pos_s, neg_s};
 }
 
+// fused TransE margin step (embed.hip K10b): draws B triples from `pool` and K corruptions
+// per triple with Philox(seed, step[0], row), scores them on h (the encoder output) and rel,
+// writes the mean margin loss to loss[0] and adds its gradients into dent ([N, D], zeroed
+// by the caller) and drel ([R, D]); the drawn ids land in o_src / o_dst / o_ridx / o_neg.
+// Ids are not range-checked here: the caller validates the triple tables once.
+void kg_step(torch::Tensor h, torch::Tensor rel, torch::Tensor pool, torch::Tensor t_src, torch::Tensor t_dst,
+             torch::Tensor t_rel, torch::Tensor step, int64_t seed, int64_t kind, bool normalize, double margin,
+             torch::Tensor o_src, torch::Tensor o_dst, torch::Tensor o_ridx, torch::Tensor o_neg, torch::Tensor coef,
+             torch::Tensor part, torch::Tensor loss, torch::Tensor dent, torch::Tensor drel) {
+  for (auto* t : {&h, &rel, &coef, &part, &loss, &dent, &drel}) typed(*t, torch::kFloat32, "kg_step float buffer");
+  for (auto* t : {&pool, &t_src, &t_dst, &t_rel, &step, &o_src, &o_dst, &o_ridx, &o_neg})
+    typed(*t, torch::kInt64, "kg_step id buffer");
+  TORCH_CHECK(h.dim() == 2 && rel.dim() == 2 && h.size(1) == rel.size(1), "kg_step: h [N, D], rel [R, D]");
+  TORCH_CHECK(dent.sizes() == h.sizes() && drel.sizes() == rel.sizes(), "kg_step: grads must match h / rel");
+  TORCH_CHECK(t_src.numel() == t_dst.numel() && t_src.numel() == t_rel.numel(), "kg_step: triple tables differ");
+  const int64_t B = o_src.numel();
+  TORCH_CHECK(B > 0 && o_dst.numel() == B && o_ridx.numel() == B && coef.numel() == B && o_neg.numel() % B == 0,
+              "kg_step: per-triple buffers must have B rows");
+  const int64_t K = o_neg.numel() / B, D = h.size(1);
+  TORCH_CHECK(K >= 1 && K <= 255 && D % 4 == 0 && D <= 256, "kg_step: 1 <= K <= 255, D % 4 == 0, D <= 256");
+  int nparts = 0;
+  ok(eh_kg_step(nullptr, nullptr, nullptr, 1, nullptr, nullptr, nullptr, 1, nullptr, 0, B, static_cast<int>(K),
+                static_cast<int>(D), static_cast<int>(kind), 0, 0.f, nullptr, nullptr, nullptr, nullptr, nullptr,
+                nullptr, nullptr, nullptr, nullptr, &nparts, stream()),
+     "kg_step (grid)");
+  TORCH_CHECK(part.numel() >= nparts, "kg_step: part needs ", nparts, " entries");
+  TORCH_CHECK(pool.numel() > 0 && loss.numel() >= 1 && step.numel() >= 1, "kg_step: empty pool / loss / step");
+  const c10::DeviceGuard g(h.device());
+  ok(eh_kg_step(h.data_ptr<float>(), rel.data_ptr<float>(), pool.data_ptr<int64_t>(), pool.numel(),
+                t_src.data_ptr<int64_t>(), t_dst.data_ptr<int64_t>(), t_rel.data_ptr<int64_t>(), h.size(0),
+                step.data_ptr<int64_t>(), static_cast<uint64_t>(seed), B, static_cast<int>(K), static_cast<int>(D),
+                static_cast<int>(kind), normalize ? 1 : 0, static_cast<float>(margin), o_src.data_ptr<int64_t>(),
+                o_dst.data_ptr<int64_t>(), o_ridx.data_ptr<int64_t>(), o_neg.data_ptr<int64_t>(),
+                coef.data_ptr<float>(), part.data_ptr<float>(), loss.data_ptr<float>(), dent.data_ptr<float>(),
+                drel.data_ptr<float>(), nullptr, stream()),
+     "kg_step");
+}
+
+int64_t kg_step_parts(int64_t B, int64_t D) {
+  int nparts = 0;
+  ok(eh_kg_step(nullptr, nullptr, nullptr, 1, nullptr, nullptr, nullptr, 1, nullptr, 0, B, 1, static_cast<int>(D), 1,
+                0, 0.f, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, &nparts,
+                nullptr),
+     "kg_step_parts");
+  return nparts;
+}
+
+// fp32 -> bf16 copy (out: bf16, same number of elements, both contiguous)
+void cast_bf16(torch::Tensor x, torch::Tensor out) {
+  typed(x, torch::kFloat32, "x");
+  typed(out, torch::kBFloat16, "out");
+  TORCH_CHECK(x.numel() == out.numel() && x.numel() % 4 == 0, "cast_bf16: same size, multiple of 4");
+  const c10::DeviceGuard g(x.device());
+  ok(eh_cast_bf16(x.data_ptr<float>(), x.numel(), out.data_ptr(), stream()), "cast_bf16");
+}
+
+// t = 0 as one hipMemsetAsync (a graph memset node, no elementwise kernel)
+void zero_(torch::Tensor t) {
+  dev(t, "t");
+  const c10::DeviceGuard g(t.device());
+  ok(hipMemsetAsync(t.data_ptr(), 0, static_cast<size_t>(t.numel()) * t.element_size(), stream()), "zero_");
+}
+
+// per-segment sizes of an index vector (entries outside [0, size) skipped), int64 [size]
+torch::Tensor seg_count(torch::Tensor idx, int64_t size) {
+  typed(idx, torch::kInt64, "idx");
+  TORCH_CHECK(size >= 0, "seg_count: size >= 0");
+  const c10::DeviceGuard g(idx.device());
+  auto cnt = torch::empty({size}, idx.options());
+  if (size > 0) ok(hipMemsetAsync(cnt.data_ptr(), 0, static_cast<size_t>(size) * 8, stream()), "seg_count zero");
+  ok(eh_seg_count(idx.data_ptr<int64_t>(), idx.numel(), size, cnt.data_ptr<int64_t>(), stream()), "seg_count");
+  return cnt;
+}
+
 void kg_bwd(torch::Tensor ent, torch::Tensor rel, torch::Tensor src, torch::Tensor dst, torch::Tensor ridx,
             torch::Tensor neg, int64_t kind, int64_t corrupt, bool normalize, torch::Tensor gpos, torch::Tensor gneg,
             torch::Tensor dent, torch::Tensor drel, bool occ) {
@@ -652,7 +726,7 @@ std::vector<torch::Tensor> full_neighbors(torch::Tensor indptr, torch::Tensor nb
 // splits > 1: split-K over the reduction dimension (deterministic slabs + one reduce).
 void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool trans_a, bool trans_b,
           c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> rmask, bool relu, int64_t splits,
-          double alpha) {
+          double alpha, c10::optional<torch::Tensor> addend) {
   auto fp = [](const torch::Tensor& t, const char* n) {
     TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.stride(1) == 1 &&
                     (t.scalar_type() == torch::kFloat32 || t.scalar_type() == torch::kBFloat16),
@@ -682,6 +756,16 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool trans_a, bool 
     ldr = rmask->stride(0);
     r_bf16 = rmask->scalar_type() == torch::kBFloat16;
   }
+  const void* ap = nullptr;  // residual added in the epilogue (may be C itself)
+  int64_t lda_add = 0;
+  int add_bf16 = 0;
+  if (addend.has_value()) {
+    fp(*addend, "addend");
+    TORCH_CHECK(addend->size(0) >= M && addend->size(1) >= N, "gemm: addend must cover [M, N]");
+    ap = addend->data_ptr();
+    lda_add = addend->stride(0);
+    add_bf16 = addend->scalar_type() == torch::kBFloat16;
+  }
   const c10::DeviceGuard g(A.device());
   torch::Tensor part;
   if (splits > 1) part = torch::empty({splits * M * N}, A.options().dtype(torch::kFloat32));
@@ -694,7 +778,7 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool trans_a, bool 
     ok(eh_gemm_tn(A.data_ptr(), B.data_ptr(), C.data_ptr(), splits > 1 ? part.data_ptr<float>() : nullptr, M, N, K,
                   A.stride(0), B.stride(0), C.stride(0), A.scalar_type() == torch::kBFloat16,
                   B.scalar_type() == torch::kBFloat16, C.scalar_type() == torch::kBFloat16, static_cast<int>(splits),
-                  static_cast<float>(alpha), stream()),
+                  static_cast<float>(alpha), ap, lda_add, add_bf16, stream()),
        "gemm_tn");
     return;
   }
@@ -702,7 +786,7 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool trans_a, bool 
              A.stride(0), B.stride(0), C.stride(0), ldr, trans_a ? 1 : 0, trans_b ? 0 : 1,
              A.scalar_type() == torch::kBFloat16, B.scalar_type() == torch::kBFloat16,
              C.scalar_type() == torch::kBFloat16, r_bf16, relu ? 1 : 0, static_cast<int>(splits),
-             static_cast<float>(alpha), stream()),
+             static_cast<float>(alpha), ap, lda_add, add_bf16, stream()),
      "gemm");
 }
 
@@ -735,7 +819,7 @@ void register_gnn_ops(pybind11::module& m) {
         py::arg("self_rank") = -1);
   m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("trans_a") = false,
         py::arg("trans_b") = false, py::arg("bias") = py::none(), py::arg("rmask") = py::none(),
-        py::arg("relu") = false, py::arg("splits") = 1, py::arg("alpha") = 1.0);
+        py::arg("relu") = false, py::arg("splits") = 1, py::arg("alpha") = 1.0, py::arg("addend") = py::none());
   m.def("gat_supported", &gat_supported);
   m.def("gat_fwd", &gat_fwd, py::arg("indptr"), py::arg("col"), py::arg("order"), py::arg("h"), py::arg("al"),
         py::arg("ar"), py::arg("H"), py::arg("C"), py::arg("slope"), py::arg("a_src") = py::none());
@@ -759,6 +843,11 @@ void register_gnn_ops(pybind11::module& m) {
   m.def("gather_f32_bf16", &gather_f32_bf16, py::arg("x"), py::arg("idx"), py::arg("out") = py::none());
   m.def("sgns_apply_", &sgns_apply_);
   m.def("kg_fwd", &kg_fwd);
+  m.def("kg_step", &kg_step);
+  m.def("kg_step_parts", &kg_step_parts);
+  m.def("cast_bf16", &cast_bf16);
+  m.def("zero_", &zero_);
+  m.def("seg_count", &seg_count);
   m.def("pair_fwd", &pair_fwd, py::arg("es"), py::arg("ec"), py::arg("B"), py::arg("K"), py::arg("mrr") = py::none());
   m.def("pair_bwd", &pair_bwd);
   m.def("kg_bwd", &kg_bwd, py::arg("ent"), py::arg("rel"), py::arg("src"), py::arg("dst"), py::arg("ridx"),

@@ -523,6 +523,131 @@ __global__ __launch_bounds__(256) void kg_bwd_kernel(KgArgs a, const float* __re
   kg_scatter(dent, occ ? L.row * (2 + a.K) + 1 : ts, L.sub, a.D, a.lp, a.normalize, t, nt, dt, occ);
 }
 
+// ----------------------------------------------------------------------------- K10b
+// One TransE margin step on an encoder's output without torch glue (the R-GCN + TransE
+// training step of BASELINE config 5, models/rgcn_kg_step.py).
+//   fwd: each lane group draws its triple (uniform over `pool`) and K corruptions
+//        (uniform entities) with Philox(seed, step, row), scores the triple and its 2K
+//        front / tail corruptions, and keeps
+//          loss_i = relu(margin + mean_k neg_ik - pos_i),   c_i = [loss_i > 0] / B,
+//        plus one partial loss sum per block (no atomics: the bwd kernel's block 0 adds the
+//        partials in a fixed order);
+//   bwd: d loss / d pos_i = -c_i, d loss / d neg_ik = c_i / 2K, pushed through the scores
+//        into the encoder-output and relation-table gradients (kg_grad / kg_scatter).
+struct KgStepArgs {
+  KgArgs k;  // ent = the encoder output h; src / dst / ridx / neg = the o_* buffers below
+  int64_t *o_src, *o_dst, *o_ridx, *o_neg;
+  const int64_t* pool;  // candidate triple rows
+  const int64_t* t_src;  // training triples
+  const int64_t* t_dst;
+  const int64_t* t_rel;
+  int64_t P, num_ent;
+  const int64_t* step;  // Philox counter: the optimizer's step count (advanced by its launch)
+  uint64_t seed;
+  float margin;
+  float* coef;  // [B]
+  float* part;  // [blocks of the fwd launch]
+  float* loss;  // [1]
+  int nparts;
+};
+
+__device__ __forceinline__ uint32_t kg_word(uint64_t seed, uint64_t ctr, int64_t row, int w) {
+  const uint4_t r = Philox::gen(seed, ctr, static_cast<uint64_t>(row) * 64u + static_cast<uint64_t>(w >> 2));
+  return r[w & 3];
+}
+
+__global__ __launch_bounds__(256) void kg_step_fwd_kernel(KgStepArgs s) {
+  __shared__ float red[4];
+  const KgArgs& a = s.k;
+  const RowLane L = row_lane(a.lp, a.B);
+  float li = 0.f;
+  if (L.ok) {
+    const uint64_t ctr = static_cast<uint64_t>(s.step[0]);
+    const int64_t pi = static_cast<int64_t>((static_cast<uint64_t>(kg_word(s.seed, ctr, L.row, 0)) *
+                                             static_cast<uint64_t>(s.P)) >> 32);
+    const int64_t tri = s.pool[pi];
+    const int64_t hs = s.t_src[tri], rs = s.t_rel[tri], ts = s.t_dst[tri];
+    if (L.sub == 0) {
+      s.o_src[L.row] = hs;
+      s.o_ridx[L.row] = rs;
+      s.o_dst[L.row] = ts;
+    }
+    float h[4], r[4], t[4], n[4], nh, nr, nt, nn;
+    kg_load_norm(a.ent, hs, L.sub, a.D, a.lp, a.normalize, h, nh);
+    kg_load_norm(a.rel, rs, L.sub, a.D, a.lp, a.normalize, r, nr);
+    kg_load_norm(a.ent, ts, L.sub, a.D, a.lp, a.normalize, t, nt);
+    const float ps = kg_finish(a.kind, emb_group_sum(kg_part(a.kind, h, r, t), a.lp));
+    float nsum = 0.f;
+    for (int k = 0; k < a.K; ++k) {
+      const int64_t ns = static_cast<int64_t>((static_cast<uint64_t>(kg_word(s.seed, ctr, L.row, 1 + k)) *
+                                               static_cast<uint64_t>(s.num_ent)) >> 32);
+      if (L.sub == 0) s.o_neg[L.row * a.K + k] = ns;
+      kg_load_norm(a.ent, ns, L.sub, a.D, a.lp, a.normalize, n, nn);
+      nsum += kg_finish(a.kind, emb_group_sum(kg_part(a.kind, n, r, t), a.lp));   // front
+      nsum += kg_finish(a.kind, emb_group_sum(kg_part(a.kind, h, r, n), a.lp));   // tail
+    }
+    li = fmaxf(s.margin + nsum / static_cast<float>(2 * a.K) - ps, 0.f);
+    if (L.sub == 0) s.coef[L.row] = li > 0.f ? 1.f / static_cast<float>(a.B) : 0.f;
+    if (L.sub != 0) li = 0.f;
+  }
+  for (int o = 32; o >= 1; o >>= 1) li += __shfl_xor(li, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = li;
+  __syncthreads();
+  if (threadIdx.x == 0) s.part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(256) void kg_step_bwd_kernel(KgStepArgs s, float* __restrict__ dent,
+                                                          float* __restrict__ drel) {
+  const KgArgs& a = s.k;
+  if (blockIdx.x == 0) {  // the step's loss: partial sums in a fixed order
+    __shared__ float red[256];
+    float v = 0.f;
+    for (int i = threadIdx.x; i < s.nparts; i += 256) v += s.part[i];
+    red[threadIdx.x] = v;
+    __syncthreads();
+    for (int w = 128; w >= 1; w >>= 1) {
+      if (static_cast<int>(threadIdx.x) < w) red[threadIdx.x] += red[threadIdx.x + w];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) s.loss[0] = red[0] / static_cast<float>(a.B);
+  }
+  const RowLane L = row_lane(a.lp, a.B);
+  if (!L.ok) return;
+  const float c = s.coef[L.row];
+  if (c == 0.f) return;  // whole lane group: the margin holds, no gradient
+  const float gp = -c, gn = c / static_cast<float>(2 * a.K);
+  float h[4], r[4], t[4], n[4], nh, nr, nt, nn;
+  float dh[4] = {0.f, 0.f, 0.f, 0.f}, dr[4] = {0.f, 0.f, 0.f, 0.f}, dt[4] = {0.f, 0.f, 0.f, 0.f};
+  const int64_t hs = a.src[L.row], rs = a.ridx[L.row], ts = a.dst[L.row];
+  kg_load_norm(a.ent, hs, L.sub, a.D, a.lp, a.normalize, h, nh);
+  kg_load_norm(a.rel, rs, L.sub, a.D, a.lp, a.normalize, r, nr);
+  kg_load_norm(a.ent, ts, L.sub, a.D, a.lp, a.normalize, t, nt);
+  kg_grad(a.kind, a.lp, gp, h, r, t, dh, dr, dt);
+  for (int k = 0; k < a.K; ++k) {
+    const int64_t ns = a.neg[L.row * a.K + k];
+    kg_load_norm(a.ent, ns, L.sub, a.D, a.lp, a.normalize, n, nn);
+    float dn[4] = {0.f, 0.f, 0.f, 0.f};
+    kg_grad(a.kind, a.lp, gn, n, r, t, dn, dr, dt);
+    kg_grad(a.kind, a.lp, gn, h, r, n, dh, dr, dn);
+    kg_scatter(dent, ns, L.sub, a.D, a.lp, a.normalize, n, nn, dn);
+  }
+  kg_scatter(dent, hs, L.sub, a.D, a.lp, a.normalize, h, nh, dh);
+  kg_scatter(drel, rs, L.sub, a.D, a.lp, a.normalize, r, nr, dr);
+  kg_scatter(dent, ts, L.sub, a.D, a.lp, a.normalize, t, nt, dt);
+}
+
+// fp32 -> bf16, 4 elements per item (n4 = n / 4)
+__global__ __launch_bounds__(256) void cast_bf16_kernel(const float* __restrict__ x, int64_t n4,
+                                                        bf16_t* __restrict__ out) {
+  grid_stride(n4, [&](int64_t i) {
+    const float4_t v = reinterpret_cast<const float4_t*>(x)[i];
+    tl2u w;
+    w[0] = pack_bf16x2(v[0], v[1]);
+    w[1] = pack_bf16x2(v[2], v[3]);
+    reinterpret_cast<tl2u*>(out)[i] = w;
+  });
+}
+
 inline int row_lanes(int chunks) {
   int lp = 1;
   while (lp < chunks && lp < 64) lp <<= 1;
@@ -705,4 +830,47 @@ hipError_t eh_gather_f32_bf16(const float* x, int64_t n_rows, int D, const int64
   return hipGetLastError();
 }
 
+
+// the fused TransE margin step (KgStepArgs): returns the fwd launch's block count through
+// nparts_out so the caller can size `part`; part == null: only report it
+hipError_t eh_kg_step(const float* ent, const float* rel, const int64_t* pool, int64_t P, const int64_t* t_src,
+                      const int64_t* t_dst, const int64_t* t_rel, int64_t num_ent, const int64_t* step, uint64_t seed,
+                      int64_t B, int K, int D, int kind, int normalize, float margin, int64_t* o_src, int64_t* o_dst,
+                      int64_t* o_ridx, int64_t* o_neg, float* coef, float* part, float* loss, float* dent,
+                      float* drel, int* nparts_out, hipStream_t s) {
+  if (B <= 0 || K <= 0 || K > 255 || P <= 0 || num_ent <= 0) return hipErrorInvalidValue;
+  if (D % 4 != 0 || D > 256 || kind < 0 || kind > 2) return hipErrorInvalidValue;
+  KgStepArgs a;
+  a.k = kg_args(ent, rel, o_src, o_dst, o_ridx, o_neg, B, K, D, kind, 2, normalize);
+  const dim3 grid = row_grid(B, a.k.lp);
+  if (nparts_out) *nparts_out = static_cast<int>(grid.x);
+  if (!part) return hipSuccess;
+  a.o_src = o_src;
+  a.o_dst = o_dst;
+  a.o_ridx = o_ridx;
+  a.o_neg = o_neg;
+  a.pool = pool;
+  a.t_src = t_src;
+  a.t_dst = t_dst;
+  a.t_rel = t_rel;
+  a.P = P;
+  a.num_ent = num_ent;
+  a.step = step;
+  a.seed = seed;
+  a.margin = margin;
+  a.coef = coef;
+  a.part = part;
+  a.loss = loss;
+  a.nparts = static_cast<int>(grid.x);
+  hipLaunchKernelGGL(kg_step_fwd_kernel, grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL(kg_step_bwd_kernel, grid, dim3(256), 0, s, a, dent, drel);
+  return hipGetLastError();
+}
+
+hipError_t eh_cast_bf16(const float* x, int64_t n, void* out, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (n % 4 != 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(cast_bf16_kernel, grid_for(n / 4), dim3(256), 0, s, x, n / 4, static_cast<bf16_t*>(out));
+  return hipGetLastError();
+}
 }  // extern "C"

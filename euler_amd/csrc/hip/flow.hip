@@ -74,6 +74,16 @@ __global__ __launch_bounds__(256) void flow_expand_kernel(const int64_t* __restr
   out_src[e] = pos >= 0 ? lo : -1;
 }
 
+// cnt[v] += 1 for every 0 <= idx[i] < size (padding -1 skipped: no contended sentinel
+// bin); cnt zeroed by the caller
+__global__ __launch_bounds__(256) void seg_count_kernel(const int64_t* __restrict__ idx, int64_t n, int64_t size,
+                                                        unsigned long long* __restrict__ cnt) {
+  grid_stride(n, [&](int64_t i) {
+    const int64_t v = idx[i];
+    if (v >= 0 && v < size) atomicAdd(cnt + v, 1ull);
+  });
+}
+
 }  // namespace euler_hip
 
 using namespace euler_hip;
@@ -96,6 +106,14 @@ hipError_t eh_flow_expand(const int64_t* indptr, const int32_t* nbr, int64_t num
   if (num_types < 1 || num_types > 32) return hipErrorInvalidValue;
   hipLaunchKernelGGL(flow_expand_kernel, dim3(static_cast<uint32_t>(ceil_div(cap, 256))), dim3(256), 0, s, indptr,
                      nbr, num_rows, num_types, mask, rows, n, offs, cap, out_nbr, out_src, overflow);
+  return hipGetLastError();
+}
+
+
+hipError_t eh_seg_count(const int64_t* idx, int64_t n, int64_t size, int64_t* cnt, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(seg_count_kernel, grid_for(n), dim3(256), 0, s, idx, n, size,
+                     reinterpret_cast<unsigned long long*>(cnt));
   return hipGetLastError();
 }
 

@@ -109,6 +109,13 @@ hipError_t eh_kg_bwd(const float* ent, const float* rel, const int64_t* src, con
                      const int64_t* neg, int64_t B, int K, int D, int kind, int corrupt, int normalize,
                      const float* gpos, const float* gneg, float* dent, float* drel, int occ, hipStream_t s);
 
+hipError_t eh_kg_step(const float* ent, const float* rel, const int64_t* pool, int64_t P, const int64_t* t_src,
+                      const int64_t* t_dst, const int64_t* t_rel, int64_t num_ent, const int64_t* step, uint64_t seed,
+                      int64_t B, int K, int D, int kind, int normalize, float margin, int64_t* o_src, int64_t* o_dst,
+                      int64_t* o_ridx, int64_t* o_neg, float* coef, float* part, float* loss, float* dent,
+                      float* drel, int* nparts_out, hipStream_t s);
+hipError_t eh_cast_bf16(const float* x, int64_t n, void* out, hipStream_t s);
+
 // pair.hip (fused sigmoid cross-entropy of the unsupervised pair objective)
 hipError_t eh_pair_fwd(const float* es, const float* ec, int B, int K, int E, float inv_n, float* logits, float* part,
                        float* loss, float* mrr, hipStream_t s);
@@ -119,11 +126,11 @@ hipError_t eh_pair_bwd(const float* es, const float* ec, int B, int K, int E, fl
 hipError_t eh_gemm(const void* A, const void* B, void* C, const float* bias, const void* rmask, float* part,
                    int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int a_t,
                    int b_t, int a_bf16, int b_bf16, int c_bf16, int r_bf16, int relu, int splits, float alpha,
-                   hipStream_t s);
+                   const void* addend, int64_t ld_add, int add_bf16, hipStream_t s);
 
 hipError_t eh_gemm_tn(const void* A, const void* B, void* C, float* part, int64_t M, int64_t N, int64_t K, int64_t lda,
                       int64_t ldb, int64_t ldc, int a_bf16, int b_bf16, int c_bf16, int splits, float alpha,
-                      hipStream_t s);
+                      const void* addend, int64_t ld_add, int add_bf16, hipStream_t s);
 
 // route.hip (owner routing of the fixed-capacity all-to-all exchanges)
 int64_t eh_route_chunks(int64_t n);
@@ -143,6 +150,7 @@ hipError_t eh_flow_degree(const int64_t* indptr, int64_t num_rows, int num_types
 hipError_t eh_flow_expand(const int64_t* indptr, const int32_t* nbr, int64_t num_rows, int num_types, uint32_t mask,
                           const int64_t* rows, int64_t n, const int64_t* offs, int64_t cap, int64_t* out_nbr,
                           int64_t* out_src, int32_t* overflow, hipStream_t s);
+hipError_t eh_seg_count(const int64_t* idx, int64_t n, int64_t size, int64_t* cnt, hipStream_t s);
 
 // optim.hip
 hipError_t eh_flat_optim(float* p, const float* g, float* m, float* v, int64_t n, int64_t* step, float lr, float b1,

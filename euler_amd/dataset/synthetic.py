@@ -136,17 +136,27 @@ def community_labels(comm, num_classes, noise=0.1, seed=0):
 
 
 @torch.no_grad()
-def tail_ranks(ent, rel, src, ridx, dst, normalize=True, kind="l2", chunk=1024):
-    """Raw rank (1 = best) of the true tail among ALL entities for each test triple,
-    TransE score -|h + r - t| (l1 / l2) on (optionally) l2-normalised rows; ties count
-    against the true tail."""
+def tail_ranks(ent, rel, src, ridx, dst, normalize=True, kind="l2", chunk=1024, cands=None):
+    """Raw rank (1 = best) of the true tail among ALL entities (or among the candidate
+    entities ``cands``, which must contain every true tail) for each test triple, TransE
+    score -|h + r - t| (l1 / l2) on (optionally) l2-normalised rows; ties count against the
+    true tail."""
     E = torch.nn.functional.normalize(ent.float(), dim=-1) if normalize else ent.float()
     R = torch.nn.functional.normalize(rel.float(), dim=-1) if normalize else rel.float()
+    C = E if cands is None else E[cands]
+    col = dst
+    if cands is not None:
+        pos = torch.full((E.shape[0],), -1, dtype=torch.long, device=E.device)
+        pos[cands] = torch.arange(cands.numel(), device=E.device)
+        col = pos[dst]
+        if bool((col < 0).any()):
+            raise ValueError("a true tail is not among the candidates")
     out = []
     for a in range(0, src.numel(), chunk):
-        s, r, t = src[a:a + chunk], ridx[a:a + chunk], dst[a:a + chunk]
+        s, r, t = src[a:a + chunk], ridx[a:a + chunk], col[a:a + chunk]
         q = E[s] + R[r]                                        # [c, D]
-        d = torch.cdist(q, E, p=1.0 if kind == "l1" else 2.0)  # [c, Ne]
+        d = torch.cdist(q, C, p=1.0 if kind == "l1" else 2.0,
+                        compute_mode="donot_use_mm_for_euclid_dist")  # [c, Nc]
         true = d.gather(1, t.view(-1, 1))
         out.append((d <= true).sum(1))
     return torch.cat(out)

@@ -216,8 +216,8 @@ def gat_conv(z, a_src, a_dst, csr: EdgeCSR, slope=0.2):
 
 
 def gemm(a, b, out=None, trans_a=False, trans_b=False, bias=None, relu=False, rmask=None, splits=1, alpha=1.0,
-         out_dtype=torch.float32):
-    """``out = alpha * op(a) @ op(b) (+ bias) (relu) (* (rmask > 0))`` with op(x) = x^T when
+         out_dtype=torch.float32, addend=None):
+    """``out = alpha * op(a) @ op(b) (+ bias) (+ addend) (relu) (* (rmask > 0))`` with op(x) = x^T when
     trans_x (BLAS convention).  GPU: the tiled MFMA kernel of csrc/hip/gemm.hip (bf16
     operands, fp32 accumulation; ``splits`` > 1 splits the reduction dimension into
     deterministic partial slabs + one reduce, for [R]-row weight-gradient products) —
@@ -230,11 +230,14 @@ def gemm(a, b, out=None, trans_a=False, trans_b=False, bias=None, relu=False, rm
             out = torch.empty(M, N, device=a.device, dtype=out_dtype)
         aa = a if a.stride(-1) == 1 else a.contiguous()
         bb = b if b.stride(-1) == 1 else b.contiguous()
-        hip().gemm(aa, bb, out, bool(trans_a), bool(trans_b), bias, rmask, bool(relu), int(splits), float(alpha))
+        hip().gemm(aa, bb, out, bool(trans_a), bool(trans_b), bias, rmask, bool(relu), int(splits), float(alpha),
+                   addend)
         return out
     y = (A.float() @ Bm.float()) * alpha
     if bias is not None:
         y = y + bias.float()
+    if addend is not None:
+        y = y + addend[: y.shape[0], : y.shape[1]].float()
     if relu:
         y = torch.relu(y)
     if rmask is not None:
@@ -574,17 +577,26 @@ def relation_transform(x, rel, weight, edge_index, size, aggr="mean", tiles=None
     """R-GCN message + aggregation: ``out[i] = aggr_e weight[rel_e] @ x[src_e]`` over the
     in-edges of ``i`` (aggr ``mean`` or ``add``).  x [N_src, K], weight [R, N, K]."""
     R, N, K = weight.shape
-    lds_row = (_round_up(N, 64) + _round_up(K, 64) + 16) * 2  # bytes per tile row (A + output)
-    if use_hip(x, weight) and lds_row * 16 <= 158 * 1024:
+    if use_hip(x, weight) and _rel_lds_row(N, K) * 16 <= 158 * 1024:
         if tiles is None:
-            # the largest tile (edges of one relation per W_rel read) whose LDS rows fit
-            tm = min(hip().rel_gemm_tile, int(os.environ.get("EULER_AMD_RG_TILE", "64")))
-            while tm > 16 and lds_row * tm > 158 * 1024:
-                tm //= 2
-            key = "_euler_reltiles_%d_%d_%s_%d" % (int(size[0]), R, aggr, tm)
-            tiles = _cached(edge_index, key, lambda: RelationTiles(edge_index, rel, size, R, aggr, tile=tm))
+            tiles = relation_tiles(edge_index, rel, size, R, N, K, aggr)
         return _RelationTransform.apply(x, weight, tiles, int(size[0]))
     return relation_transform_reference(x, rel, weight, edge_index, size, aggr).to(x.dtype)
+
+
+def _rel_lds_row(N, K):
+    return (_round_up(N, 64) + _round_up(K, 64) + 16) * 2  # bytes per tile row (A + output)
+
+
+def relation_tiles(edge_index, rel, size, R, N, K, aggr="mean") -> RelationTiles:
+    """the (cached) :class:`RelationTiles` of ``edge_index`` for [R, N, K] relation weights:
+    the largest tile (edges of one relation per W_rel read) whose LDS rows fit"""
+    lds_row = _rel_lds_row(N, K)
+    tm = min(hip().rel_gemm_tile, int(os.environ.get("EULER_AMD_RG_TILE", "64")))
+    while tm > 16 and lds_row * tm > 158 * 1024:
+        tm //= 2
+    key = "_euler_reltiles_%d_%d_%s_%d" % (int(size[0]), R, aggr, tm)
+    return _cached(edge_index, key, lambda: RelationTiles(edge_index, rel, size, R, aggr, tile=tm))
 
 
 # ----------------------------------------------------------------------------- K11 skip-gram loss

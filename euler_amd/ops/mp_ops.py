@@ -79,7 +79,20 @@ class SegmentIndex:
     @property
     def counts(self):
         if self._counts is None:
-            self._build()
+            if self._perm is None:
+                # a histogram (fixed size: capturable) instead of the sort when only the
+                # segment sizes are asked for (the GCN degree of the source side)
+                if use_hip(self.indices):
+                    # one atomic per real entry; torch's int64 index_add_ took 6 ms per call
+                    # on the padding bin of a capacity-padded block (profiles/r4_gcn/)
+                    self._counts = hip().seg_count(self.indices.contiguous(), self.size)
+                else:
+                    idx = torch.where(self.indices < 0, torch.full_like(self.indices, self.size), self.indices)
+                    c = torch.zeros(self.size + 1, dtype=torch.long, device=idx.device)
+                    c.index_add_(0, idx, torch.ones_like(idx))
+                    self._counts = c[: self.size]
+            else:
+                self._build()
         return self._counts
 
 
@@ -243,13 +256,23 @@ class _EdgeSoftmax(torch.autograd.Function):
 
 
 class _SpmmIndex:
-    """Destination CSR and source CSC of one ``edge_index`` for weighted aggregation."""
+    """Destination CSR and source CSC of one ``edge_index`` for weighted aggregation.  The
+    CSC (a sort of the sources) is built on first use: only a backward into ``x`` needs it,
+    and a first layer over constant features has none."""
 
     def __init__(self, edge_index, size):
+        self.edge_index = edge_index
         self.dst = cached_segment(edge_index, 0, size[0])
         self.src = cached_segment(edge_index, 1, size[1])
         self.col = edge_index[1].reshape(-1).long()[self.dst.perm].contiguous()   # sources, CSR order
-        self.row = edge_index[0].reshape(-1).long()[self.src.perm].contiguous()   # destinations, CSC order
+        self._row = None
+
+    @property
+    def row(self):
+        """destinations in CSC order"""
+        if self._row is None:
+            self._row = self.edge_index[0].reshape(-1).long()[self.src.perm].contiguous()
+        return self._row
 
 
 def _spmm_index(edge_index, size):

@@ -45,7 +45,10 @@ class FlatParams:
             o += n
 
     def zero_grad(self):
-        self.grad.zero_()
+        if use_hip(self.grad):
+            hip().zero_(self.grad)  # a memset node in captured steps, not a fill kernel
+        else:
+            self.grad.zero_()
 
     def rebind_grads(self):
         """Re-attach the flat grad views (after something replaced ``p.grad``)."""

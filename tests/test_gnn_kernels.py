@@ -632,3 +632,44 @@ def test_per_item_kernels_cover_more_than_2pow32_items(cuda):
     hip().index_add_rows_(out, idx, src)
     del src
     assert float(out.min()) == 64.0 and float(out.max()) == 64.0
+
+
+@pytest.mark.gpu
+def test_seg_count_skips_padding(cuda):
+    """SegmentIndex.counts without the sort (csrc/hip/flow.hip seg_count) vs bincount"""
+    from euler_amd.ops.mp_ops import SegmentIndex
+
+    torch.manual_seed(0)
+    idx = torch.randint(-1, 500, (200_000,), device=cuda)
+    idx[:100_000] = -1  # a capacity-padded tail of padding entries
+    cnt = SegmentIndex(idx, 500).counts
+    ref = torch.bincount(idx[idx >= 0].cpu(), minlength=500)
+    assert cnt.dtype == torch.long and torch.equal(cnt.cpu(), ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pad", [0, 300])
+def test_gcn_conv_gpu_matches_cpu(cuda, pad):
+    """GCNConv (degree norm from the segment counts, SpMM forward, lazy CSC backward) on the
+    GPU against the CPU torch composition, with and without padding edges"""
+    import copy
+
+    from euler_amd.convolution.convs import GCNConv
+
+    torch.manual_seed(1)
+    n_dst, n_src = 200, 500
+    ei = _graph(n_dst, n_src, 3000, "cpu", seed=3, pad=pad)
+    conv = GCNConv(32)
+    x = torch.randn(n_src, 48)
+    conv((x, None), ei, (n_dst, n_src))  # materialise
+    gconv = copy.deepcopy(conv).to(cuda)
+    xc = x.clone().requires_grad_(True)
+    xg = x.to(cuda).requires_grad_(True)
+    yc = conv((xc, None), ei, (n_dst, n_src))
+    yg = gconv((xg, None), ei.to(cuda), (n_dst, n_src))
+    assert torch.allclose(yg.cpu(), yc, atol=2e-3, rtol=2e-3)
+    w = torch.randn_like(yc)
+    (yc * w).sum().backward()
+    (yg * w.to(cuda)).sum().backward()
+    assert torch.allclose(xg.grad.cpu(), xc.grad, atol=2e-3, rtol=2e-3)
+    assert torch.allclose(gconv.fc.weight.grad.cpu(), conv.fc.weight.grad, atol=2e-2, rtol=2e-3)

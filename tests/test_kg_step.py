@@ -1,0 +1,114 @@
+"""Fused R-GCN + TransE step (models/rgcn_kg_step.py; BASELINE config 5, reference
+examples/rgcn/rgcn.py:30-105 + examples/TransX/transX.py:63-145) against the plain fp32
+torch composition of the same model on the same drawn batch, and the gemm addend epilogue
+it relies on."""
+import copy
+
+import pytest
+import torch
+
+from euler_amd.dataset.synthetic import lattice_kg
+from euler_amd.models.rgcn_kg_step import RgcnTransE, RgcnTransEStep
+from euler_amd.ops import gnn_ops
+from euler_amd.parallel.flat import FlatOptimizer, FlatParams
+
+
+def test_autograd_model_cpu_trains():
+    (src, rel, dst), _ = lattice_kg(300, 12, 3000, 10, seed=1)
+    torch.manual_seed(0)
+    m = RgcnTransE(300, 12, 16, layers=1, margin=1.0)
+    opt = torch.optim.Adam(m.parameters(), lr=0.01)
+    ei = torch.stack([dst, src])
+    losses = []
+    for _ in range(20):
+        idx = torch.randint(0, src.numel(), (128,))
+        negs = torch.randint(0, 300, (128, 4))
+        loss = m(ei, rel, src[idx], rel[idx], dst[idx], negs)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        losses.append(float(loss))
+    assert losses[-1] < losses[0]
+
+
+def _setup(dev, layers, D=64, num_ent=640, num_rel=24, B=256, K=4, seed=2):
+    (src, rel, dst), _ = lattice_kg(num_ent, num_rel, 8000, 10, seed=seed)
+    src, rel, dst = src.to(dev), rel.to(dev), dst.to(dev)
+    torch.manual_seed(seed)
+    m = RgcnTransE(num_ent, num_rel, D, layers=layers, margin=1.0).to(dev)
+    ei = torch.stack([dst, src])
+    m(ei, rel, src[:8], rel[:8], dst[:8], torch.zeros(8, K, dtype=torch.long, device=dev)).backward()
+    flat = FlatParams(m.parameters(), dev)
+    opt = FlatOptimizer(flat, "adam", 1e-3)
+    pool = torch.arange(src.numel(), device=dev)
+    step = RgcnTransEStep(m, flat, opt, ei, rel, (src, rel, dst), pool, B, K, seed=11)
+    return m, flat, opt, step, ei, rel
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layers", [0, 1, 2])
+def test_fused_step_matches_fp32_torch(cuda, layers):
+    m, flat, opt, step, ei, erel = _setup(cuda, layers)
+    loss = float(step.forward_backward()[0])
+    g_fused = [p.grad.detach().float().cpu().clone() for p in flat.params]
+    s, r, d, n = (t.cpu() for t in step.batch())
+    assert int(s.min()) >= 0 and int(n.max()) < m.ent.shape[0] and int(r.max()) < m.rel.shape[0]
+    ref = copy.deepcopy(m).cpu()
+    for p in ref.parameters():
+        p.grad = None
+    ref_loss = ref(ei.cpu(), erel.cpu(), s, r, d, n)
+    ref_loss.backward()
+    assert abs(loss - float(ref_loss)) <= 2e-2 * abs(float(ref_loss)) + 1e-4
+    for (name, p), gf in zip(ref.named_parameters(), g_fused):
+        gr = p.grad.float()
+        err = float((gf - gr).norm() / gr.norm().clamp(min=1e-12))
+        assert err < 5e-2, (name, err)
+    # same optimizer step count -> same draws; after the update -> new draws
+    before = [t.clone() for t in step.batch()]
+    step.forward_backward()
+    assert all(torch.equal(a, b) for a, b in zip(before, step.batch()))
+    step.optimizer_step()
+    step.forward_backward()
+    assert not torch.equal(before[3], step.batch()[3])
+
+
+@pytest.mark.gpu
+def test_fused_step_captures_and_trains(cuda):
+    m, flat, opt, step, ei, erel = _setup(cuda, 1)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            step.step()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    first = float(step.loss[0])
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        step.step()
+    for _ in range(60):
+        g.replay()
+    torch.cuda.synchronize()
+    assert int(opt.step_count.item()) == 62  # 2 eager steps + 60 replays (capture runs nothing)
+    last = float(step.loss[0])
+    assert last == last and last < first
+
+
+@pytest.mark.gpu
+def test_gemm_addend_epilogue(cuda):
+    torch.manual_seed(0)
+    a = torch.randn(300, 96, device=cuda)
+    b = torch.randn(80, 96, device=cuda)
+    add = torch.randn(300, 80, device=cuda).to(torch.bfloat16)
+    rm = torch.randn(300, 80, device=cuda)
+    out = gnn_ops.gemm(a, b, trans_b=True, addend=add, rmask=rm)
+    ref = (a.bfloat16().float() @ b.bfloat16().float().t() + add.float()) * (rm > 0).float()
+    assert torch.allclose(out, ref, atol=2e-2, rtol=1e-2)
+    # split-K transposed product with an fp32 addend aliasing the output
+    g = torch.randn(4096, 64, device=cuda)
+    x = torch.randn(4096, 64, device=cuda)
+    c = torch.randn(64, 64, device=cuda)
+    c0 = c.clone()
+    gnn_ops.gemm(g, x, out=c, trans_a=True, splits=8, addend=c)
+    ref = g.bfloat16().float().t() @ x.bfloat16().float() + c0
+    assert torch.allclose(c, ref, atol=0.5, rtol=2e-2)
