@@ -188,6 +188,10 @@ def main(argv=None):
             model.self_keep = keep
         with torch.no_grad():
             h = model.encode(edge_index, edge_rel).float()
+            if not bool(torch.isfinite(h).all()):
+                bad = [n for n, p in model.named_parameters() if not bool(torch.isfinite(p).all())]
+                print(f"[bench_kg] non-finite encoder output; non-finite parameters: {bad}", file=sys.stderr,
+                      flush=True)
         model.self_keep = None
         model.train()
         m = rank_metrics(tail_ranks(h, model.rel, te_src, te_rel, te_dst, normalize=norm))
@@ -210,8 +214,7 @@ def main(argv=None):
         sync_info.pop("xar", None)
 
     fused = None
-    if args.fused and dev.type == "cuda" and args.self_drop == 0 and args.num_bases == 0 and not (
-            args.type_negs and args.task == "types") and args.dim % 8 == 0:
+    if args.fused and dev.type == "cuda" and not (args.type_negs and args.task == "types") and args.dim % 8 == 0:
         fused = RgcnTransEStep(model, flat, opt, edge_index, edge_rel, (src, rel, dst), pool, args.batch,
                                args.num_negs, seed=args.seed * 7919 + rank, grad_sync=grad_sync)
         loss_buf = fused.loss
@@ -270,9 +273,25 @@ def main(argv=None):
         dist.all_reduce(elt, op=dist.ReduceOp.MAX)
     el = float(elt.item())
     done = args.warmup + args.steps + (0 if args.no_graph else 2)
+    probe = os.environ.get("EULER_AMD_KG_NAN_PROBE", "0") == "1"  # debugging: stop at the first non-finite step
     while done < args.eval_after:  # untimed: learning evidence only
+        snap = (flat.flat.clone(), opt.m.clone(), opt.v.clone(), opt.step_count.clone()) if probe else None
         step()
         done += 1
+        if probe and not bool(torch.isfinite(flat.flat).all()):
+            print(f"[bench_kg] non-finite parameters after step {done}", file=sys.stderr, flush=True)
+            if fused is not None:
+                flat.flat.copy_(snap[0])
+                opt.m.copy_(snap[1])
+                opt.v.copy_(snap[2])
+                opt.step_count.copy_(snap[3])
+                RgcnTransEStep._check = True
+                try:
+                    fused.forward_backward()
+                    print("[bench_kg] eager re-run of that step: finite", file=sys.stderr, flush=True)
+                except FloatingPointError as e:
+                    print(f"[bench_kg] eager re-run: {e}", file=sys.stderr, flush=True)
+            break
     eval_final = evaluate()
     if rank == 0:
         print(json.dumps({

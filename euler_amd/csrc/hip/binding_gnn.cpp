@@ -572,6 +572,21 @@ int64_t kg_step_parts(int64_t B, int64_t D) {
   return nparts;
 }
 
+// x0 = x * keep (per-row Philox keep mask, probability 1 - p), keep [n] fp32 0 / 1
+void drop_rows(torch::Tensor x, double p, int64_t seed, torch::Tensor step, int64_t salt, torch::Tensor x0,
+               torch::Tensor keep) {
+  for (auto* t : {&x, &x0, &keep}) typed(*t, torch::kFloat32, "drop_rows buffer");
+  typed(step, torch::kInt64, "step");
+  TORCH_CHECK(x.dim() == 2 && x0.sizes() == x.sizes() && keep.numel() == x.size(0) && x.size(1) % 4 == 0,
+              "drop_rows: x [n, d] (d % 4 == 0), x0 like x, keep [n]");
+  TORCH_CHECK(salt >= 0 && salt < (1 << 24), "drop_rows: 0 <= salt < 2^24");
+  const c10::DeviceGuard g(x.device());
+  ok(eh_drop_rows(x.data_ptr<float>(), x.size(0), static_cast<int>(x.size(1)), static_cast<float>(p),
+                  static_cast<uint64_t>(seed), step.data_ptr<int64_t>(), static_cast<uint64_t>(salt),
+                  x0.data_ptr<float>(), keep.data_ptr<float>(), stream()),
+     "drop_rows");
+}
+
 // fp32 -> bf16 copy (out: bf16, same number of elements, both contiguous)
 void cast_bf16(torch::Tensor x, torch::Tensor out) {
   typed(x, torch::kFloat32, "x");
@@ -581,11 +596,21 @@ void cast_bf16(torch::Tensor x, torch::Tensor out) {
   ok(eh_cast_bf16(x.data_ptr<float>(), x.numel(), out.data_ptr(), stream()), "cast_bf16");
 }
 
-// t = 0 as one hipMemsetAsync (a graph memset node, no elementwise kernel)
+// t = 0: one vector-store kernel (zero_kernel, embed.hip); EULER_AMD_ZERO_MEMSET=1: one
+// hipMemsetAsync instead
 void zero_(torch::Tensor t) {
   dev(t, "t");
   const c10::DeviceGuard g(t.device());
-  ok(hipMemsetAsync(t.data_ptr(), 0, static_cast<size_t>(t.numel()) * t.element_size(), stream()), "zero_");
+  static const bool use_memset = [] {
+    const char* e = std::getenv("EULER_AMD_ZERO_MEMSET");
+    return e && e[0] == '1';
+  }();
+  const int64_t bytes = t.numel() * t.element_size();
+  if (use_memset) {
+    ok(hipMemsetAsync(t.data_ptr(), 0, static_cast<size_t>(bytes), stream()), "zero_ (memset)");
+    return;
+  }
+  ok(eh_zero(t.data_ptr(), bytes, stream()), "zero_");
 }
 
 // per-segment sizes of an index vector (entries outside [0, size) skipped), int64 [size]
@@ -594,7 +619,7 @@ torch::Tensor seg_count(torch::Tensor idx, int64_t size) {
   TORCH_CHECK(size >= 0, "seg_count: size >= 0");
   const c10::DeviceGuard g(idx.device());
   auto cnt = torch::empty({size}, idx.options());
-  if (size > 0) ok(hipMemsetAsync(cnt.data_ptr(), 0, static_cast<size_t>(size) * 8, stream()), "seg_count zero");
+  ok(eh_zero(cnt.data_ptr(), size * 8, stream()), "seg_count zero");
   ok(eh_seg_count(idx.data_ptr<int64_t>(), idx.numel(), size, cnt.data_ptr<int64_t>(), stream()), "seg_count");
   return cnt;
 }
@@ -726,7 +751,7 @@ std::vector<torch::Tensor> full_neighbors(torch::Tensor indptr, torch::Tensor nb
 // splits > 1: split-K over the reduction dimension (deterministic slabs + one reduce).
 void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool trans_a, bool trans_b,
           c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> rmask, bool relu, int64_t splits,
-          double alpha, c10::optional<torch::Tensor> addend) {
+          double alpha, c10::optional<torch::Tensor> addend, c10::optional<torch::Tensor> row_scale) {
   auto fp = [](const torch::Tensor& t, const char* n) {
     TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.stride(1) == 1 &&
                     (t.scalar_type() == torch::kFloat32 || t.scalar_type() == torch::kBFloat16),
@@ -766,6 +791,12 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool trans_a, bool 
     lda_add = addend->stride(0);
     add_bf16 = addend->scalar_type() == torch::kBFloat16;
   }
+  const float* rs = nullptr;  // per-row scale of the product
+  if (row_scale.has_value()) {
+    typed(*row_scale, torch::kFloat32, "row_scale");
+    TORCH_CHECK(row_scale->numel() == M, "gemm: row_scale must have M elements");
+    rs = row_scale->data_ptr<float>();
+  }
   const c10::DeviceGuard g(A.device());
   torch::Tensor part;
   if (splits > 1) part = torch::empty({splits * M * N}, A.options().dtype(torch::kFloat32));
@@ -778,7 +809,7 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool trans_a, bool 
     ok(eh_gemm_tn(A.data_ptr(), B.data_ptr(), C.data_ptr(), splits > 1 ? part.data_ptr<float>() : nullptr, M, N, K,
                   A.stride(0), B.stride(0), C.stride(0), A.scalar_type() == torch::kBFloat16,
                   B.scalar_type() == torch::kBFloat16, C.scalar_type() == torch::kBFloat16, static_cast<int>(splits),
-                  static_cast<float>(alpha), ap, lda_add, add_bf16, stream()),
+                  static_cast<float>(alpha), ap, lda_add, add_bf16, rs, stream()),
        "gemm_tn");
     return;
   }
@@ -786,7 +817,7 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool trans_a, bool 
              A.stride(0), B.stride(0), C.stride(0), ldr, trans_a ? 1 : 0, trans_b ? 0 : 1,
              A.scalar_type() == torch::kBFloat16, B.scalar_type() == torch::kBFloat16,
              C.scalar_type() == torch::kBFloat16, r_bf16, relu ? 1 : 0, static_cast<int>(splits),
-             static_cast<float>(alpha), ap, lda_add, add_bf16, stream()),
+             static_cast<float>(alpha), ap, lda_add, add_bf16, rs, stream()),
      "gemm");
 }
 
@@ -819,7 +850,8 @@ void register_gnn_ops(pybind11::module& m) {
         py::arg("self_rank") = -1);
   m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("trans_a") = false,
         py::arg("trans_b") = false, py::arg("bias") = py::none(), py::arg("rmask") = py::none(),
-        py::arg("relu") = false, py::arg("splits") = 1, py::arg("alpha") = 1.0, py::arg("addend") = py::none());
+        py::arg("relu") = false, py::arg("splits") = 1, py::arg("alpha") = 1.0, py::arg("addend") = py::none(),
+        py::arg("row_scale") = py::none());
   m.def("gat_supported", &gat_supported);
   m.def("gat_fwd", &gat_fwd, py::arg("indptr"), py::arg("col"), py::arg("order"), py::arg("h"), py::arg("al"),
         py::arg("ar"), py::arg("H"), py::arg("C"), py::arg("slope"), py::arg("a_src") = py::none());
@@ -846,6 +878,7 @@ void register_gnn_ops(pybind11::module& m) {
   m.def("kg_step", &kg_step);
   m.def("kg_step_parts", &kg_step_parts);
   m.def("cast_bf16", &cast_bf16);
+  m.def("drop_rows", &drop_rows);
   m.def("zero_", &zero_);
   m.def("seg_count", &seg_count);
   m.def("pair_fwd", &pair_fwd, py::arg("es"), py::arg("ec"), py::arg("B"), py::arg("K"), py::arg("mrr") = py::none());

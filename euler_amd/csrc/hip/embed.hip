@@ -453,7 +453,9 @@ __device__ __forceinline__ void kg_grad(int kind, int lp, float g, const float* 
       p += d * d;
     }
     const float nrm = sqrtf(emb_group_sum(p, lp));
-    coef = nrm > 0.f ? 1.f / nrm : 0.f;
+    // 0 below 1e-12 (a triple already satisfied exactly): 1 / nrm of a denormal norm is
+    // inf and 0 * inf = NaN on the components with d = 0
+    coef = nrm > 1e-12f ? 1.f / nrm : 0.f;
   }
 #pragma unroll
   for (int v = 0; v < 4; ++v) {
@@ -634,6 +636,31 @@ __global__ __launch_bounds__(256) void kg_step_bwd_kernel(KgStepArgs s, float* _
   kg_scatter(dent, hs, L.sub, a.D, a.lp, a.normalize, h, nh, dh);
   kg_scatter(drel, rs, L.sub, a.D, a.lp, a.normalize, r, nr, dr);
   kg_scatter(dent, ts, L.sub, a.D, a.lp, a.normalize, t, nt, dt);
+}
+
+// self-loop dropout of the R-GCN step: keep_i = [u01(Philox(seed, step, salt * 2^40 + i))
+// >= p] (the autograd model's torch.rand(n, 1) >= p, drawn on the device), x0 = x * keep
+__global__ __launch_bounds__(256) void drop_rows_kernel(const float* __restrict__ x, int64_t n, int d4, float p,
+                                                        uint64_t seed, const int64_t* __restrict__ step, uint64_t salt,
+                                                        float* __restrict__ x0, float* __restrict__ keep) {
+  const uint64_t ctr = static_cast<uint64_t>(step[0]);
+  grid_stride(n * d4, [&](int64_t t) {
+    const int64_t i = t / d4;
+    const int64_t d = t - i * d4;
+    const uint4_t r = Philox::gen(seed, ctr, (salt << 40) | static_cast<uint64_t>(i));
+    const float k = u01(r[0]) >= p ? 1.f : 0.f;
+    const float4_t v = reinterpret_cast<const float4_t*>(x)[t];
+    reinterpret_cast<float4_t*>(x0)[t] = v * k;
+    if (d == 0) keep[i] = k;
+  });
+}
+
+// x = 0 with vector stores on the compute queue (n16: 16-byte items; tail bytes by the
+// first thread of the grid)
+__global__ __launch_bounds__(256) void zero_kernel(uint4_t* __restrict__ x, int64_t n16, unsigned char* tail,
+                                                   int ntail) {
+  grid_stride(n16, [&](int64_t i) { x[i] = uint4_t{0u, 0u, 0u, 0u}; });
+  if (blockIdx.x == 0 && threadIdx.x < static_cast<unsigned>(ntail)) tail[threadIdx.x] = 0;
 }
 
 // fp32 -> bf16, 4 elements per item (n4 = n / 4)
@@ -864,6 +891,25 @@ hipError_t eh_kg_step(const float* ent, const float* rel, const int64_t* pool, i
   a.nparts = static_cast<int>(grid.x);
   hipLaunchKernelGGL(kg_step_fwd_kernel, grid, dim3(256), 0, s, a);
   hipLaunchKernelGGL(kg_step_bwd_kernel, grid, dim3(256), 0, s, a, dent, drel);
+  return hipGetLastError();
+}
+
+hipError_t eh_drop_rows(const float* x, int64_t n, int d, float p, uint64_t seed, const int64_t* step, uint64_t salt,
+                        float* x0, float* keep, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (d % 4 != 0 || salt >= (1ull << 24)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(drop_rows_kernel, grid_for(n * (d / 4)), dim3(256), 0, s, x, n, d / 4, p, seed, step, salt, x0,
+                     keep);
+  return hipGetLastError();
+}
+
+hipError_t eh_zero(void* x, int64_t bytes, hipStream_t s) {
+  if (bytes <= 0) return hipSuccess;
+  if (reinterpret_cast<uintptr_t>(x) % 16 != 0) return hipMemsetAsync(x, 0, static_cast<size_t>(bytes), s);
+  const int64_t n16 = bytes / 16;
+  const int ntail = static_cast<int>(bytes - n16 * 16);
+  hipLaunchKernelGGL(zero_kernel, grid_for(n16 > 0 ? n16 : 1), dim3(256), 0, s, static_cast<uint4_t*>(x), n16,
+                     static_cast<unsigned char*>(x) + n16 * 16, ntail);
   return hipGetLastError();
 }
 

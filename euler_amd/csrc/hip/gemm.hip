@@ -6,7 +6,7 @@
 // epilogues, and split-K (deterministic partial slabs + one reduce) for the [R]-row
 // reductions of weight gradients.
 //
-//   C[M][N] = op(A) op(B) (+ bias[N]) (+ Add[M][N]) (relu) (* relu'(Rm[M][N]))
+//   C[M][N] = rscale[M] * (op(A) op(B)) (+ bias[N]) (+ Add[M][N]) (relu) (* relu'(Rm[M][N]))
 //   A: a_t = 0: [M][K] row-major (lda);  a_t = 1: [K][M] (lda)  -> op(A) = A or A^T
 //   B: b_t = 0: [N][K] (ldb) (C = A B^T, "NT");  b_t = 1: [K][N] (ldb) ("NN")
 //   A, B fp32 or bf16 (staged in LDS as bf16); C fp32 or bf16 (ldc); Rm bf16 or fp32
@@ -35,6 +35,7 @@ struct GemmArgs {
   const void* addend;  // [M][N] (ld_add) added before relu / rmask, or null (may alias C)
   int64_t ld_add;
   int32_t add_bf16;
+  const float* rscale;  // [M]: the product row r is scaled by rscale[r] before bias / addend
 };
 
 __device__ __forceinline__ float gm_addend(const GemmArgs& a, int64_t row, int64_t col) {
@@ -153,6 +154,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
           a.part[(static_cast<int64_t>(split) * a.M + row) * a.N + col] = v;
           continue;
         }
+        if (a.rscale) v *= a.rscale[row];
         if (a.bias) v += a.bias[col];
         if (a.addend) v += gm_addend(a, row, col);
         if (a.relu) v = fmaxf(v, 0.f);
@@ -275,6 +277,7 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmArgs a) {
           a.part[(static_cast<int64_t>(split) * a.M + row) * a.N + col] = v;
           continue;
         }
+        if (a.rscale) v *= a.rscale[row];
         if (a.addend) v += gm_addend(a, row, col);
         if (a.c_bf16) static_cast<bf16_t*>(a.C)[row * a.ldc + col] = f2bf(v);
         else static_cast<float*>(a.C)[row * a.ldc + col] = v;
@@ -298,6 +301,7 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(GemmArgs a) {
       for (int u = 0; u < 8; ++u) v += t[u];
     }
     for (; s < a.splits; ++s) v += a.part[s * MN + i];
+    if (a.rscale) v *= a.rscale[row];
     if (a.bias) v += a.bias[col];
     if (a.addend) v += gm_addend(a, row, col);
     if (a.relu) v = fmaxf(v, 0.f);
@@ -320,10 +324,10 @@ extern "C" {
 hipError_t eh_gemm(const void* A, const void* B, void* C, const float* bias, const void* rmask, float* part,
                    int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int a_t,
                    int b_t, int a_bf16, int b_bf16, int c_bf16, int r_bf16, int relu, int splits, float alpha,
-                   const void* addend, int64_t ld_add, int add_bf16, hipStream_t s) {
+                   const void* addend, int64_t ld_add, int add_bf16, const float* rscale, hipStream_t s) {
   if (M <= 0 || N <= 0 || K <= 0 || splits < 1 || (splits > 1 && !part)) return hipErrorInvalidValue;
   GemmArgs g{A, B, C, bias, rmask, part, M, N, K, lda, ldb, ldc, ldr, a_t, b_t, a_bf16, b_bf16, c_bf16, r_bf16,
-             relu, splits, 0, alpha, addend, ld_add, add_bf16};
+             relu, splits, 0, alpha, addend, ld_add, add_bf16, rscale};
   const int64_t ksteps = ceil_div(K, kGmK);
   g.kps = static_cast<int32_t>(ceil_div(ksteps, splits) * kGmK);
   const dim3 grid(static_cast<uint32_t>(ceil_div(M, kGmT)), static_cast<uint32_t>(ceil_div(N, kGmT)),
@@ -337,10 +341,10 @@ hipError_t eh_gemm(const void* A, const void* B, void* C, const float* bias, con
 // C [M][N] = alpha A^T B, A [K][M] (lda), B [K][N] (ldb), split over K in `splits` slabs
 hipError_t eh_gemm_tn(const void* A, const void* B, void* C, float* part, int64_t M, int64_t N, int64_t K, int64_t lda,
                       int64_t ldb, int64_t ldc, int a_bf16, int b_bf16, int c_bf16, int splits, float alpha,
-                      const void* addend, int64_t ld_add, int add_bf16, hipStream_t s) {
+                      const void* addend, int64_t ld_add, int add_bf16, const float* rscale, hipStream_t s) {
   if (M <= 0 || N <= 0 || K <= 0 || splits < 1 || (splits > 1 && !part)) return hipErrorInvalidValue;
   GemmArgs g{A, B, C, nullptr, nullptr, part, M, N, K, lda, ldb, ldc, 0, 1, 1, a_bf16, b_bf16, c_bf16, 0,
-             0, splits, 0, alpha, addend, ld_add, add_bf16};
+             0, splits, 0, alpha, addend, ld_add, add_bf16, rscale};
   const int64_t ksteps = ceil_div(K, kGmK);
   g.kps = static_cast<int32_t>(ceil_div(ksteps, splits) * kGmK);
   const dim3 grid(static_cast<uint32_t>(ceil_div(M, kGmT)), static_cast<uint32_t>(ceil_div(N, kGmT)),

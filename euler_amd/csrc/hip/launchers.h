@@ -115,6 +115,9 @@ hipError_t eh_kg_step(const float* ent, const float* rel, const int64_t* pool, i
                       int64_t* o_ridx, int64_t* o_neg, float* coef, float* part, float* loss, float* dent,
                       float* drel, int* nparts_out, hipStream_t s);
 hipError_t eh_cast_bf16(const float* x, int64_t n, void* out, hipStream_t s);
+hipError_t eh_zero(void* x, int64_t bytes, hipStream_t s);
+hipError_t eh_drop_rows(const float* x, int64_t n, int d, float p, uint64_t seed, const int64_t* step, uint64_t salt,
+                        float* x0, float* keep, hipStream_t s);
 
 // pair.hip (fused sigmoid cross-entropy of the unsupervised pair objective)
 hipError_t eh_pair_fwd(const float* es, const float* ec, int B, int K, int E, float inv_n, float* logits, float* part,
@@ -126,11 +129,11 @@ hipError_t eh_pair_bwd(const float* es, const float* ec, int B, int K, int E, fl
 hipError_t eh_gemm(const void* A, const void* B, void* C, const float* bias, const void* rmask, float* part,
                    int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int a_t,
                    int b_t, int a_bf16, int b_bf16, int c_bf16, int r_bf16, int relu, int splits, float alpha,
-                   const void* addend, int64_t ld_add, int add_bf16, hipStream_t s);
+                   const void* addend, int64_t ld_add, int add_bf16, const float* rscale, hipStream_t s);
 
 hipError_t eh_gemm_tn(const void* A, const void* B, void* C, float* part, int64_t M, int64_t N, int64_t K, int64_t lda,
                       int64_t ldb, int64_t ldc, int a_bf16, int b_bf16, int c_bf16, int splits, float alpha,
-                      const void* addend, int64_t ld_add, int add_bf16, hipStream_t s);
+                      const void* addend, int64_t ld_add, int add_bf16, const float* rscale, hipStream_t s);
 
 // route.hip (owner routing of the fixed-capacity all-to-all exchanges)
 int64_t eh_route_chunks(int64_t n);

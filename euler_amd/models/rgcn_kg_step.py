@@ -26,6 +26,11 @@ backward, optimizer — as hand-written launches only, for hipGraph capture:
   ``rel_gemm_dw`` into the relation weights' flat-gradient view;
 * the flat optimizer (one launch, plus the step-count increment for large buffers).
 
+Basis-decomposed relations (``num_bases`` > 0) compose W = coef @ bases with one GEMM per
+layer and step and take d coef / d bases from the composed dW with two more; self-loop
+dropout draws its per-row keep mask with Philox(seed, step, layer) (``drop_rows``) and
+scales the self-loop product's rows with it in the backward GEMM's epilogue.
+
 No torch elementwise kernel runs in the step; gradients are zeroed with one memset.  The
 draws come from a different generator than ``torch.randint`` (Philox keyed by the
 optimizer's device step count), so the batch stream differs from the autograd path's;
@@ -36,6 +41,8 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+import os
 
 from euler_amd.convolution import RelationConv
 from euler_amd.ops import gnn_ops
@@ -93,8 +100,6 @@ class RgcnTransEStep:
 
     def __init__(self, model: RgcnTransE, flat, opt, edge_index, edge_rel, triples, pool, batch: int,
                  num_negs: int, seed: int = 0, grad_sync=None):
-        if model.self_drop > 0:
-            raise ValueError("the fused step has no self-loop dropout (use the autograd step)")
         dev = model.ent.device
         if dev.type != "cuda":
             raise ValueError("the fused KG step runs on the GPU")
@@ -120,29 +125,39 @@ class RgcnTransEStep:
                 raise ValueError(f"triple {name} ids out of range [0, {hi})")
         self.t_src, self.t_rel, self.t_dst = t_src, t_rel, t_dst
         self.layers = []
+        self.drop = float(model.self_drop)
         n = self.N
+        params = [model.ent, model.rel]
         for conv in model.convs:
-            if conv.num_bases != 0 or conv.fc.has_uninitialized_params() or conv.fc.bias is not None \
-                    or conv.fc.activation is not None:
-                raise ValueError("the fused KG step needs full relation matrices and a bias-free self-loop fc "
-                                 "(materialised)")
-            W, Wfc = conv.matrix, conv.fc.weight
-            if tuple(W.shape) != (self.R, self.D, self.D) or tuple(Wfc.shape) != (self.D, self.D):
+            if conv.fc.has_uninitialized_params() or conv.fc.bias is not None or conv.fc.activation is not None:
+                raise ValueError("the fused KG step needs a bias-free, materialised self-loop fc")
+            Wfc = conv.fc.weight
+            if tuple(Wfc.shape) != (self.D, self.D):
                 raise ValueError("the fused KG step needs square [dim, dim] layers")
             tiles = gnn_ops.relation_tiles(edge_index, edge_rel, (n, n), self.R, self.D, self.D, "mean")
-            self.layers.append((W, Wfc, tiles))
-        for p in [model.ent, model.rel] + [t for W, Wfc, _ in self.layers for t in (W, Wfc)]:
+            # the relation matrices: a parameter, or composed from bases every step (coef @ bases)
+            basis = (conv.coef, conv.bases) if conv.num_bases > 0 else None
+            self.layers.append((conv.matrix if basis is None else None, Wfc, tiles, basis))
+            params += [Wfc] + ([conv.matrix] if basis is None else list(basis))
+        for p in params:
             if p.grad is None or not p.grad.is_contiguous():
                 raise ValueError("every parameter needs its flat-gradient view (FlatParams)")
         L = len(self.layers)
         f32 = dict(device=dev, dtype=torch.float32)
+        nb = sum(1 for lay in self.layers if lay[3] is not None)
+        # composed relation matrices and their gradient (basis layers; one buffer pair, reused)
+        self.Wc = torch.empty(self.R, self.D, self.D, **f32) if nb else None
+        self.dWc = torch.empty(self.R, self.D, self.D, **f32) if nb else None
+        # self-loop dropout: the masked layer input and its per-row keep mask
+        self.x0 = [torch.empty(self.N, self.D, **f32) for _ in range(L)] if self.drop > 0 else None
+        self.keep = [torch.empty(self.N, **f32) for _ in range(L)] if self.drop > 0 else None
         bf = dict(device=dev, dtype=torch.bfloat16)
         i64 = dict(device=dev, dtype=torch.int64)
         self.xb = [torch.empty(self.N, self.D, **bf) for _ in range(L)]
         self.h = [torch.empty(self.N, self.D, **f32) for _ in range(L)]
         self.dh = [torch.empty(self.N, self.D, **f32) for _ in range(L)]
         self.gb = torch.empty(self.N, self.D, **bf)
-        E = max((tiles.num_edges for _, _, tiles in self.layers), default=0)
+        E = max((lay[2].num_edges for lay in self.layers), default=0)
         self.msg = torch.empty(max(E, 1), self.D, **bf)
         self.o_src = torch.empty(self.B, **i64)
         self.o_dst = torch.empty(self.B, **i64)
@@ -154,23 +169,45 @@ class RgcnTransEStep:
         self._fc_splits = gnn_ops._gemm_splits(self.N, -(-self.D // 64) ** 2)
 
     # ------------------------------------------------------------------ step
+    def _relation_matrices(self, li):
+        W, _, _, basis = self.layers[li]
+        if basis is None:
+            return W.detach()
+        coef, bases = basis
+        B = bases.shape[0]
+        gnn_ops.gemm(coef.detach(), bases.detach().view(B, -1), out=self.Wc.view(self.R, -1))
+        return self.Wc
+
+    _check = os.environ.get("EULER_AMD_KG_STEP_CHECK", "0") == "1"  # eager debugging: finiteness per stage
+
+    def _chk(self, stage, *ts):
+        if self._check and not all(bool(torch.isfinite(t).all()) for t in ts):
+            raise FloatingPointError(f"fused KG step {int(self.opt.step_count.item())}: non-finite after {stage}")
+
     def forward_backward(self):
         """draws, encoder, loss and every gradient into the flat gradient buffer"""
         H = hip()
         m = self.model
-        hip().zero_(self.flat.grad)
+        self._chk("previous update", self.flat.flat)
+        H.zero_(self.flat.grad)
         x = m.ent.detach()
         saved = []
         L = len(self.layers)
-        for li, (W, Wfc, tiles) in enumerate(self.layers):
+        for li, (_, Wfc, tiles, _) in enumerate(self.layers):
             H.cast_bf16(x, self.xb[li])
-            wb, wt = H.rel_weight_bf16(W.detach())
+            wb, wt = H.rel_weight_bf16(self._relation_matrices(li))
             tr, ts, tl = tiles.tiles()
             msg = self.msg[: tiles.num_edges]
             H.rel_gemm(self.xb[li], tiles.src, tr, ts, tl, wb, None, tiles.slot_dst, 0, tiles.tile, msg)
             agg = gnn_ops._seg_sum(msg, tiles.dst_seg.indptr, 1)
-            gnn_ops.gemm(x, Wfc.detach(), out=self.h[li], trans_b=True, addend=agg, relu=li + 1 < L)
-            saved.append((x, wt))
+            x0 = x
+            if self.drop > 0:
+                # self-loop dropout (RgcnTransE.encode): the self term of a dropped row is 0
+                x0 = self.x0[li]
+                H.drop_rows(x, self.drop, self.seed ^ 0x5E1F, self.opt.step_count, li, x0, self.keep[li])
+            gnn_ops.gemm(x0, Wfc.detach(), out=self.h[li], trans_b=True, addend=agg, relu=li + 1 < L)
+            self._chk("layer %d forward" % li, agg, self.h[li], wb)
+            saved.append((x, x0, wt))
             x = self.h[li]
         dtop = m.ent.grad if L == 0 else self.dh[L - 1]
         if L:
@@ -178,9 +215,10 @@ class RgcnTransEStep:
         H.kg_step(x, m.rel.detach(), self.pool, self.t_src, self.t_dst, self.t_rel, self.opt.step_count, self.seed,
                   gnn_ops.KG_KINDS["l2"], self.normalize, self.margin, self.o_src, self.o_dst, self.o_rel, self.o_neg,
                   self.coef, self.part, self.loss, dtop, m.rel.grad)
+        self._chk("scores", dtop, m.rel.grad, self.loss)
         for li in range(L - 1, -1, -1):
-            W, Wfc, tiles = self.layers[li]
-            x_l, wt = saved[li]
+            W, Wfc, tiles, basis = self.layers[li]
+            x_l, x0_l, wt = saved[li]
             g = self.dh[li]
             H.cast_bf16(g, self.gb)
             tr, ts, tl = tiles.tiles()
@@ -188,13 +226,34 @@ class RgcnTransEStep:
             H.rel_gemm(self.gb, tiles.dst, tr, ts, tl, wt, tiles.scale, tiles.slot_src, 0, tiles.tile, msg)
             dxr = gnn_ops._seg_sum(msg, tiles.src_seg.indptr, 0)
             out = m.ent.grad if li == 0 else self.dh[li - 1]
-            # d h_l = dH W_self + relation part, times relu'(h_l) below the top layer
-            gnn_ops.gemm(g, Wfc.detach(), out=out, addend=dxr, rmask=x_l if li > 0 else None)
-            gnn_ops.gemm(g, x_l, out=Wfc.grad, trans_a=True, splits=self._fc_splits)
+            # d h_l = keep * (dH W_self) + relation part, times relu'(h_l) below the top layer
+            gnn_ops.gemm(g, Wfc.detach(), out=out, addend=dxr, rmask=x_l if li > 0 else None,
+                         row_scale=self.keep[li] if self.drop > 0 else None)
+            gnn_ops.gemm(g, x0_l, out=Wfc.grad, trans_a=True, splits=self._fc_splits)
+            self._chk("layer %d input gradients" % li, dxr, out, Wfc.grad)
             cr, cs, cl = tiles.chunks()
+            if basis is None:
+                H.rel_gemm_dw(self.gb, tiles.dst, self.xb[li], tiles.src, tiles.scale, cr, cs, cl, tiles.chunk_solo,
+                              W.grad, accumulate=False)
+                continue
+            # dW of the composed matrices, then d coef = dW bases^T, d bases = coef^T dW
+            coef, bases = basis
+            nbs = bases.shape[0]
+            H.zero_(self.dWc)
             H.rel_gemm_dw(self.gb, tiles.dst, self.xb[li], tiles.src, tiles.scale, cr, cs, cl, tiles.chunk_solo,
-                          W.grad, accumulate=False)
+                          self.dWc, accumulate=False)
+            dw = self.dWc.view(self.R, -1)
+            sp = int(os.environ.get("EULER_AMD_KG_DCOEF_SPLITS", "0")) or \
+                gnn_ops._gemm_splits(dw.shape[1], -(-self.R // 64))
+            gnn_ops.gemm(dw, bases.detach().view(nbs, -1), out=coef.grad, trans_b=True, splits=sp)
+            gnn_ops.gemm(coef.detach(), dw, out=bases.grad.view(nbs, -1), trans_a=True,
+                         splits=gnn_ops._gemm_splits(self.R, -(-dw.shape[1] // 64)))
+            self._chk("layer %d basis gradients" % li, self.dWc, coef.grad, bases.grad)
         return self.loss
+
+    def keep_masks(self):
+        """per-layer [N] keep masks of the last step's self-loop dropout (None without)"""
+        return self.keep
 
     def optimizer_step(self):
         scale = 1.0

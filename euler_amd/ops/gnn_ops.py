@@ -216,8 +216,8 @@ def gat_conv(z, a_src, a_dst, csr: EdgeCSR, slope=0.2):
 
 
 def gemm(a, b, out=None, trans_a=False, trans_b=False, bias=None, relu=False, rmask=None, splits=1, alpha=1.0,
-         out_dtype=torch.float32, addend=None):
-    """``out = alpha * op(a) @ op(b) (+ bias) (+ addend) (relu) (* (rmask > 0))`` with op(x) = x^T when
+         out_dtype=torch.float32, addend=None, row_scale=None):
+    """``out = row_scale * alpha * op(a) @ op(b) (+ bias) (+ addend) (relu) (* (rmask > 0))`` with op(x) = x^T when
     trans_x (BLAS convention).  GPU: the tiled MFMA kernel of csrc/hip/gemm.hip (bf16
     operands, fp32 accumulation; ``splits`` > 1 splits the reduction dimension into
     deterministic partial slabs + one reduce, for [R]-row weight-gradient products) —
@@ -231,9 +231,11 @@ def gemm(a, b, out=None, trans_a=False, trans_b=False, bias=None, relu=False, rm
         aa = a if a.stride(-1) == 1 else a.contiguous()
         bb = b if b.stride(-1) == 1 else b.contiguous()
         hip().gemm(aa, bb, out, bool(trans_a), bool(trans_b), bias, rmask, bool(relu), int(splits), float(alpha),
-                   addend)
+                   addend, row_scale)
         return out
     y = (A.float() @ Bm.float()) * alpha
+    if row_scale is not None:
+        y = y * row_scale.float().view(-1, 1)
     if bias is not None:
         y = y + bias.float()
     if addend is not None:

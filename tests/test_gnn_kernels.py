@@ -673,3 +673,17 @@ def test_gcn_conv_gpu_matches_cpu(cuda, pad):
     (yg * w.to(cuda)).sum().backward()
     assert torch.allclose(xg.grad.cpu(), xc.grad, atol=2e-3, rtol=2e-3)
     assert torch.allclose(gconv.fc.weight.grad.cpu(), conv.fc.weight.grad, atol=2e-2, rtol=2e-3)
+
+
+@pytest.mark.gpu
+def test_zero_kernel_sizes(cuda):
+    """hip().zero_ (vector-store kernel; memset fallback for unaligned views) on odd sizes"""
+    from euler_amd.ops._native import hip
+
+    for n in (1, 3, 4, 5, 17, 1000, 100_003):
+        t = torch.full((n + 1,), 7.0, device=cuda)
+        hip().zero_(t[:n])
+        assert bool((t[:n] == 0).all()) and float(t[n]) == 7.0
+        u = torch.full((n + 2,), 7.0, device=cuda)
+        hip().zero_(u[1:n + 1])  # 4-byte-aligned view
+        assert float(u[0]) == 7.0 and bool((u[1:n + 1] == 0).all()) and float(u[n + 1]) == 7.0

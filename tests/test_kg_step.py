@@ -31,13 +31,14 @@ def test_autograd_model_cpu_trains():
     assert losses[-1] < losses[0]
 
 
-def _setup(dev, layers, D=64, num_ent=640, num_rel=24, B=256, K=4, seed=2):
+def _setup(dev, layers, D=64, num_ent=640, num_rel=24, B=256, K=4, seed=2, bases=0, drop=0.0):
     (src, rel, dst), _ = lattice_kg(num_ent, num_rel, 8000, 10, seed=seed)
     src, rel, dst = src.to(dev), rel.to(dev), dst.to(dev)
     torch.manual_seed(seed)
-    m = RgcnTransE(num_ent, num_rel, D, layers=layers, margin=1.0).to(dev)
+    m = RgcnTransE(num_ent, num_rel, D, layers=layers, margin=1.0, num_bases=bases).to(dev)
     ei = torch.stack([dst, src])
     m(ei, rel, src[:8], rel[:8], dst[:8], torch.zeros(8, K, dtype=torch.long, device=dev)).backward()
+    m.self_drop = drop
     flat = FlatParams(m.parameters(), dev)
     opt = FlatOptimizer(flat, "adam", 1e-3)
     pool = torch.arange(src.numel(), device=dev)
@@ -45,18 +46,40 @@ def _setup(dev, layers, D=64, num_ent=640, num_rel=24, B=256, K=4, seed=2):
     return m, flat, opt, step, ei, rel
 
 
+def _oracle_loss(ref, ei, erel, batch, keeps):
+    """RgcnTransE.forward with the fused step's keep masks in place of torch.rand"""
+    import torch.nn.functional as F
+
+    s, r, d, negs = batch
+    n = ref.ent.shape[0]
+    h = ref.ent
+    for i, conv in enumerate(ref.convs):
+        x0 = h if keeps is None else h * keeps[i].view(n, 1)
+        h = conv([x0, h], ei, (n, n), edge_attr=erel)
+        if i + 1 < len(ref.convs):
+            h = F.relu(h)
+    pos, neg = gnn_ops.kg_score(h.float(), ref.rel, s, d, r, negs, "l2", "both", ref.norm)
+    return F.relu(ref.margin + neg.mean(-1) - pos).mean()
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("layers", [0, 1, 2])
-def test_fused_step_matches_fp32_torch(cuda, layers):
-    m, flat, opt, step, ei, erel = _setup(cuda, layers)
+@pytest.mark.parametrize("layers,bases,drop", [(0, 0, 0.0), (1, 0, 0.0), (2, 0, 0.0), (1, 4, 0.0), (1, 0, 0.5),
+                                               (2, 4, 0.5)])
+def test_fused_step_matches_fp32_torch(cuda, layers, bases, drop):
+    m, flat, opt, step, ei, erel = _setup(cuda, layers, bases=bases, drop=drop)
     loss = float(step.forward_backward()[0])
     g_fused = [p.grad.detach().float().cpu().clone() for p in flat.params]
     s, r, d, n = (t.cpu() for t in step.batch())
     assert int(s.min()) >= 0 and int(n.max()) < m.ent.shape[0] and int(r.max()) < m.rel.shape[0]
+    keeps = None
+    if drop > 0:
+        keeps = [k.cpu().clone() for k in step.keep_masks()]
+        frac = float(torch.cat(keeps).mean())
+        assert 0.4 < frac < 0.6 and set(torch.cat(keeps).unique().tolist()) <= {0.0, 1.0}
     ref = copy.deepcopy(m).cpu()
     for p in ref.parameters():
         p.grad = None
-    ref_loss = ref(ei.cpu(), erel.cpu(), s, r, d, n)
+    ref_loss = _oracle_loss(ref, ei.cpu(), erel.cpu(), (s, r, d, n), keeps)
     ref_loss.backward()
     assert abs(loss - float(ref_loss)) <= 2e-2 * abs(float(ref_loss)) + 1e-4
     for (name, p), gf in zip(ref.named_parameters(), g_fused):
