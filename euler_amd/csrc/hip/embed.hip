@@ -663,6 +663,11 @@ __global__ __launch_bounds__(256) void zero_kernel(uint4_t* __restrict__ x, int6
   if (blockIdx.x == 0 && threadIdx.x < static_cast<unsigned>(ntail)) tail[threadIdx.x] = 0;
 }
 
+// unaligned buffers: one byte per item
+__global__ __launch_bounds__(256) void zero_bytes_kernel(unsigned char* __restrict__ x, int64_t n) {
+  grid_stride(n, [&](int64_t i) { x[i] = 0; });
+}
+
 // fp32 -> bf16, 4 elements per item (n4 = n / 4)
 __global__ __launch_bounds__(256) void cast_bf16_kernel(const float* __restrict__ x, int64_t n4,
                                                         bf16_t* __restrict__ out) {
@@ -905,7 +910,10 @@ hipError_t eh_drop_rows(const float* x, int64_t n, int d, float p, uint64_t seed
 
 hipError_t eh_zero(void* x, int64_t bytes, hipStream_t s) {
   if (bytes <= 0) return hipSuccess;
-  if (reinterpret_cast<uintptr_t>(x) % 16 != 0) return hipMemsetAsync(x, 0, static_cast<size_t>(bytes), s);
+  if (reinterpret_cast<uintptr_t>(x) % 16 != 0) {
+    hipLaunchKernelGGL(zero_bytes_kernel, grid_for(bytes), dim3(256), 0, s, static_cast<unsigned char*>(x), bytes);
+    return hipGetLastError();
+  }
   const int64_t n16 = bytes / 16;
   const int ntail = static_cast<int>(bytes - n16 * 16);
   hipLaunchKernelGGL(zero_kernel, grid_for(n16 > 0 ? n16 : 1), dim3(256), 0, s, static_cast<uint4_t*>(x), n16,

@@ -685,5 +685,5 @@ def test_zero_kernel_sizes(cuda):
         hip().zero_(t[:n])
         assert bool((t[:n] == 0).all()) and float(t[n]) == 7.0
         u = torch.full((n + 2,), 7.0, device=cuda)
-        hip().zero_(u[1:n + 1])  # 4-byte-aligned view
+        hip().zero_(u[1:n + 1])  # 4-byte-aligned view (byte kernel)
         assert float(u[0]) == 7.0 and bool((u[1:n + 1] == 0).all()) and float(u[n + 1]) == 7.0
