@@ -23,6 +23,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from euler_amd.ops import gnn_ops, mp_ops
+from euler_amd.ops._native import hip, use_hip
 from euler_amd.utils.layers import Dense
 
 __all__ = ["Conv", "GCNConv", "SAGEConv", "GATConv", "TAGConv", "AGNNConv", "SGCNConv", "GINConv", "GraphConv",
@@ -81,6 +82,12 @@ class Conv(nn.Module):
 
     def edge_weight(self, edge_index, size):
         """n0[dst] * n1[src] per edge (the symmetric GCN normalisation)."""
+        if use_hip(edge_index) and edge_index.dim() == 2 and edge_index.dtype == torch.int64 \
+                and edge_index.is_contiguous():
+            # one launch over the two (cached) segment-count vectors; padding edges get 0
+            c0 = _seg(edge_index, 0, size[0]).counts.long().contiguous()
+            c1 = _seg(edge_index, 1, size[1]).counts.long().contiguous()
+            return hip().gcn_norm_weight(edge_index, c0, c1)
         n0, n1 = self.norm(edge_index, size)
         return (mp_ops.gather(n0, edge_index[0]) * mp_ops.gather(n1, edge_index[1])).reshape(-1)
 

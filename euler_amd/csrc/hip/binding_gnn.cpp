@@ -613,6 +613,116 @@ void zero_(torch::Tensor t) {
   ok(eh_zero(t.data_ptr(), bytes, stream()), "zero_");
 }
 
+// one hop's block of the device full-neighbourhood flow (flow.hip flow_block_kernel):
+// returns (new_n_id [cap_n], res_n_id [cap_prev], edge_index [2, E], perm [E],
+// indptr [cap_prev + 1], counts [cap_prev], last_idx [cap_n], n_targets [1] of the next hop)
+std::vector<torch::Tensor> flow_block(torch::Tensor src, torch::Tensor offs, torch::Tensor uniq, torch::Tensor inv,
+                                      torch::Tensor cnt, torch::Tensor last_idx, torch::Tensor n_targets,
+                                      int64_t cap_n, bool self_loops, torch::Tensor overflow) {
+  for (auto* t : {&src, &offs, &uniq, &inv, &cnt, &last_idx, &n_targets}) typed(*t, torch::kInt64, "flow_block id");
+  typed(overflow, torch::kInt32, "overflow");
+  const int64_t cap_e = src.numel(), cap_prev = offs.numel();
+  TORCH_CHECK(cap_prev > 0 && cap_n > 0 && last_idx.numel() == cap_prev, "flow_block: last_idx [cap_prev]");
+  TORCH_CHECK(uniq.numel() == cap_e + cap_prev && inv.numel() == cap_e + cap_prev,
+              "flow_block: uniq / inv over [neighbours, previous set]");
+  TORCH_CHECK(cnt.numel() >= 1 && n_targets.numel() >= 1 && overflow.numel() >= 1, "flow_block: scalars");
+  const int64_t E = self_loops ? cap_e + cap_prev : cap_e;
+  const c10::DeviceGuard g(src.device());
+  auto o = src.options();
+  auto new_n_id = torch::empty({cap_n}, o), res = torch::empty({cap_prev}, o), ei = torch::empty({2, E}, o);
+  auto perm = torch::empty({E}, o), indptr = torch::empty({cap_prev + 1}, o), counts = torch::empty({cap_prev}, o);
+  auto last_new = torch::empty({cap_n}, o), cnt_new = torch::empty({1}, o);
+  ok(eh_flow_block(src.data_ptr<int64_t>(), offs.data_ptr<int64_t>(), uniq.data_ptr<int64_t>(),
+                   inv.data_ptr<int64_t>(), cnt.data_ptr<int64_t>(), last_idx.data_ptr<int64_t>(),
+                   n_targets.data_ptr<int64_t>(), cap_e, cap_prev, cap_n, self_loops ? 1 : 0,
+                   new_n_id.data_ptr<int64_t>(), res.data_ptr<int64_t>(), ei.data_ptr<int64_t>(),
+                   perm.data_ptr<int64_t>(), indptr.data_ptr<int64_t>(), counts.data_ptr<int64_t>(),
+                   last_new.data_ptr<int64_t>(), cnt_new.data_ptr<int64_t>(), overflow.data_ptr<int32_t>(), stream()),
+     "flow_block");
+  return {new_n_id, res, ei, perm, indptr, counts, last_new, cnt_new};
+}
+
+// one hop's block of the fixed-fanout device SageDataFlow (flow.hip sage_block / sage_place):
+// returns (new_n_id, res_n_id, edge_index [2, E], perm [E], indptr [cap_prev + 1],
+// counts [cap_prev], last_idx [cap_n], n_targets [1] of the next hop)
+std::vector<torch::Tensor> sage_block(torch::Tensor inv, torch::Tensor uniq, torch::Tensor cnt,
+                                      torch::Tensor last_idx, int64_t f, int64_t cap_n, bool self_loops) {
+  for (auto* t : {&inv, &uniq, &cnt, &last_idx}) typed(*t, torch::kInt64, "sage_block id");
+  const int64_t cap_prev = last_idx.numel();
+  TORCH_CHECK(f > 0 && cap_prev > 0 && cap_n > 0 && inv.numel() == cap_prev * (f + 1) && uniq.numel() == inv.numel(),
+              "sage_block: inv / uniq over [cap_prev * f neighbours, cap_prev previous]");
+  const int64_t E = self_loops ? cap_prev * (f + 1) : cap_prev * f;
+  const c10::DeviceGuard g(inv.device());
+  auto o = inv.options();
+  auto new_n_id = torch::empty({cap_n}, o), res = torch::empty({cap_prev}, o), ei = torch::empty({2, E}, o);
+  auto counts = torch::empty({cap_prev}, o), last_new = torch::empty({cap_n}, o), cnt_new = torch::empty({1}, o);
+  ok(eh_sage_block(inv.data_ptr<int64_t>(), uniq.data_ptr<int64_t>(), cnt.data_ptr<int64_t>(),
+                   last_idx.data_ptr<int64_t>(), cap_prev, f, cap_n, self_loops ? 1 : 0, new_n_id.data_ptr<int64_t>(),
+                   res.data_ptr<int64_t>(), ei.data_ptr<int64_t>(), counts.data_ptr<int64_t>(),
+                   last_new.data_ptr<int64_t>(), cnt_new.data_ptr<int64_t>(), stream()),
+     "sage_block");
+  auto indptr = torch::empty({cap_prev + 1}, o);
+  ok(eh_zero(indptr.data_ptr(), 8, stream()), "sage_block indptr");
+  auto tail = indptr.narrow(0, 1, cap_prev);
+  torch::cumsum_out(tail, counts, 0);
+  auto perm = torch::empty({E}, o);
+  ok(eh_sage_place(inv.data_ptr<int64_t>(), last_idx.data_ptr<int64_t>(), cap_prev, f, self_loops ? 1 : 0,
+                   indptr.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), stream()),
+     "sage_place");
+  return {new_n_id, res, ei, perm, indptr, counts, last_new, cnt_new};
+}
+
+// GCN symmetric-norm edge weights from the two endpoint degree vectors (flow.hip)
+torch::Tensor gcn_norm_weight(torch::Tensor edge_index, torch::Tensor c0, torch::Tensor c1) {
+  typed(edge_index, torch::kInt64, "edge_index");
+  typed(c0, torch::kInt64, "c0");
+  typed(c1, torch::kInt64, "c1");
+  TORCH_CHECK(edge_index.dim() == 2 && edge_index.size(0) == 2, "gcn_norm_weight: edge_index [2, E]");
+  const int64_t E = edge_index.size(1);
+  const c10::DeviceGuard g(edge_index.device());
+  auto w = torch::empty({E}, edge_index.options().dtype(torch::kFloat32));
+  ok(eh_gcn_norm_weight(edge_index.data_ptr<int64_t>(), edge_index.data_ptr<int64_t>() + E, E,
+                        c0.data_ptr<int64_t>(), c0.numel(), c1.data_ptr<int64_t>(), c1.numel(), w.data_ptr<float>(),
+                        stream()),
+     "gcn_norm_weight");
+  return w;
+}
+
+// multi-label sigmoid cross-entropy (mean) of x [B, C] against labels[rows] [N, C] and the
+// F1 counts (tp, fp, fn) added into counts [3] int64; returns the 0-d loss
+torch::Tensor bce_f1_fwd(torch::Tensor x, torch::Tensor labels, torch::Tensor rows, torch::Tensor counts) {
+  typed(x, torch::kFloat32, "x");
+  typed(labels, torch::kFloat32, "labels");
+  typed(rows, torch::kInt64, "rows");
+  typed(counts, torch::kInt64, "counts");
+  TORCH_CHECK(x.dim() == 2 && labels.dim() == 2 && labels.size(1) == x.size(1) && rows.numel() == x.size(0) &&
+                  counts.numel() >= 3,
+              "bce_f1_fwd: x [B, C], labels [N, C], rows [B], counts [3]");
+  const c10::DeviceGuard g(x.device());
+  auto part = torch::empty({eh_bce_parts(x.numel())}, x.options());
+  auto loss = torch::empty({}, x.options());
+  ok(eh_bce_f1_fwd(x.data_ptr<float>(), labels.data_ptr<float>(), rows.data_ptr<int64_t>(), x.size(0),
+                   static_cast<int>(x.size(1)), part.data_ptr<float>(), loss.data_ptr<float>(),
+                   counts.data_ptr<int64_t>(), stream()),
+     "bce_f1_fwd");
+  return loss;
+}
+
+torch::Tensor bce_bwd(torch::Tensor x, torch::Tensor labels, torch::Tensor rows, torch::Tensor g) {
+  typed(x, torch::kFloat32, "x");
+  typed(labels, torch::kFloat32, "labels");
+  typed(rows, torch::kInt64, "rows");
+  typed(g, torch::kFloat32, "g");
+  TORCH_CHECK(x.dim() == 2 && labels.size(1) == x.size(1) && rows.numel() == x.size(0) && g.numel() == 1,
+              "bce_bwd: x [B, C], labels [N, C], rows [B], g scalar");
+  const c10::DeviceGuard gd(x.device());
+  auto dx = torch::empty_like(x);
+  ok(eh_bce_bwd(x.data_ptr<float>(), labels.data_ptr<float>(), rows.data_ptr<int64_t>(), x.size(0),
+                static_cast<int>(x.size(1)), g.data_ptr<float>(), dx.data_ptr<float>(), stream()),
+     "bce_bwd");
+  return dx;
+}
+
 // per-segment sizes of an index vector (entries outside [0, size) skipped), int64 [size]
 torch::Tensor seg_count(torch::Tensor idx, int64_t size) {
   typed(idx, torch::kInt64, "idx");
@@ -881,6 +991,11 @@ void register_gnn_ops(pybind11::module& m) {
   m.def("drop_rows", &drop_rows);
   m.def("zero_", &zero_);
   m.def("seg_count", &seg_count);
+  m.def("flow_block", &flow_block);
+  m.def("gcn_norm_weight", &gcn_norm_weight);
+  m.def("sage_block", &sage_block);
+  m.def("bce_f1_fwd", &bce_f1_fwd);
+  m.def("bce_bwd", &bce_bwd);
   m.def("pair_fwd", &pair_fwd, py::arg("es"), py::arg("ec"), py::arg("B"), py::arg("K"), py::arg("mrr") = py::none());
   m.def("pair_bwd", &pair_bwd);
   m.def("kg_bwd", &kg_bwd, py::arg("ent"), py::arg("rel"), py::arg("src"), py::arg("dst"), py::arg("ridx"),

@@ -668,6 +668,77 @@ __global__ __launch_bounds__(256) void zero_bytes_kernel(unsigned char* __restri
   grid_stride(n, [&](int64_t i) { x[i] = 0; });
 }
 
+// multi-label sigmoid cross-entropy of logits x [B, C] against label rows labels[rows[b]]
+// (the full-flow trainer's loss, F.binary_cross_entropy_with_logits mean) and the F1
+// counts of the thresholded predictions: per-block partial loss sums (a second one-block
+// launch adds them in order) and tp / fp / fn added into counts
+__global__ __launch_bounds__(256) void bce_f1_fwd_kernel(const float* __restrict__ x, const float* __restrict__ labels,
+                                                         const int64_t* __restrict__ rows, int64_t B, int C,
+                                                         float* __restrict__ part,
+                                                         unsigned long long* __restrict__ counts) {
+  __shared__ float red[4];
+  __shared__ unsigned int cred[4][3];
+  float l = 0.f;
+  unsigned int tp = 0, fp = 0, fn = 0;
+  grid_stride(B * C, [&](int64_t i) {
+    const int64_t b = i / C;
+    const int c = static_cast<int>(i - b * C);
+    const float xv = x[i], y = labels[rows[b] * C + c];
+    l += fmaxf(xv, 0.f) - xv * y + log1pf(__expf(-fabsf(xv)));
+    const bool pred = xv >= 0.f, pos = y > 0.5f;
+    tp += pred && pos;
+    fp += pred && !pos;
+    fn += !pred && pos;
+  });
+  for (int o = 32; o >= 1; o >>= 1) {
+    l += __shfl_xor(l, o, 64);
+    tp += __shfl_xor(tp, o, 64);
+    fp += __shfl_xor(fp, o, 64);
+    fn += __shfl_xor(fn, o, 64);
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[w] = l;
+    cred[w][0] = tp;
+    cred[w][1] = fp;
+    cred[w][2] = fn;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+  if (threadIdx.x < 3) {
+    const unsigned int v = cred[0][threadIdx.x] + cred[1][threadIdx.x] + cred[2][threadIdx.x] + cred[3][threadIdx.x];
+    if (v) atomicAdd(counts + threadIdx.x, static_cast<unsigned long long>(v));
+  }
+}
+
+__global__ __launch_bounds__(256) void bce_sum_kernel(const float* __restrict__ part, int nparts, float inv_n,
+                                                      float* __restrict__ loss) {
+  __shared__ float red[256];
+  float v = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += 256) v += part[i];
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int w = 128; w >= 1; w >>= 1) {
+    if (static_cast<int>(threadIdx.x) < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss[0] = red[0] * inv_n;
+}
+
+// d loss / d x = (sigmoid(x) - y) * g / (B C), g = the upstream gradient (device scalar)
+__global__ __launch_bounds__(256) void bce_bwd_kernel(const float* __restrict__ x, const float* __restrict__ labels,
+                                                      const int64_t* __restrict__ rows, int64_t B, int C,
+                                                      const float* __restrict__ g, float inv_n,
+                                                      float* __restrict__ dx) {
+  const float s = g[0] * inv_n;
+  grid_stride(B * C, [&](int64_t i) {
+    const int64_t b = i / C;
+    const int c = static_cast<int>(i - b * C);
+    const float xv = x[i], y = labels[rows[b] * C + c];
+    dx[i] = (1.f / (1.f + __expf(-xv)) - y) * s;
+  });
+}
+
 // fp32 -> bf16, 4 elements per item (n4 = n / 4)
 __global__ __launch_bounds__(256) void cast_bf16_kernel(const float* __restrict__ x, int64_t n4,
                                                         bf16_t* __restrict__ out) {
@@ -918,6 +989,29 @@ hipError_t eh_zero(void* x, int64_t bytes, hipStream_t s) {
   const int ntail = static_cast<int>(bytes - n16 * 16);
   hipLaunchKernelGGL(zero_kernel, grid_for(n16 > 0 ? n16 : 1), dim3(256), 0, s, static_cast<uint4_t*>(x), n16,
                      static_cast<unsigned char*>(x) + n16 * 16, ntail);
+  return hipGetLastError();
+}
+
+int eh_bce_parts(int64_t n) {
+  const int64_t b = ceil_div(n, 256);
+  return static_cast<int>(b < 1024 ? (b > 0 ? b : 1) : 1024);
+}
+
+hipError_t eh_bce_f1_fwd(const float* x, const float* labels, const int64_t* rows, int64_t B, int C, float* part,
+                         float* loss, int64_t* counts, hipStream_t s) {
+  if (B <= 0 || C <= 0) return hipErrorInvalidValue;
+  const int np = eh_bce_parts(B * C);
+  hipLaunchKernelGGL(bce_f1_fwd_kernel, dim3(np), dim3(256), 0, s, x, labels, rows, B, C, part,
+                     reinterpret_cast<unsigned long long*>(counts));
+  hipLaunchKernelGGL(bce_sum_kernel, dim3(1), dim3(256), 0, s, part, np, 1.f / static_cast<float>(B * C), loss);
+  return hipGetLastError();
+}
+
+hipError_t eh_bce_bwd(const float* x, const float* labels, const int64_t* rows, int64_t B, int C, const float* g,
+                      float* dx, hipStream_t s) {
+  if (B <= 0 || C <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bce_bwd_kernel, grid_for(B * C), dim3(256), 0, s, x, labels, rows, B, C, g,
+                     1.f / static_cast<float>(B * C), dx);
   return hipGetLastError();
 }
 

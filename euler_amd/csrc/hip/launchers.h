@@ -116,6 +116,11 @@ hipError_t eh_kg_step(const float* ent, const float* rel, const int64_t* pool, i
                       float* drel, int* nparts_out, hipStream_t s);
 hipError_t eh_cast_bf16(const float* x, int64_t n, void* out, hipStream_t s);
 hipError_t eh_zero(void* x, int64_t bytes, hipStream_t s);
+int eh_bce_parts(int64_t n);
+hipError_t eh_bce_f1_fwd(const float* x, const float* labels, const int64_t* rows, int64_t B, int C, float* part,
+                         float* loss, int64_t* counts, hipStream_t s);
+hipError_t eh_bce_bwd(const float* x, const float* labels, const int64_t* rows, int64_t B, int C, const float* g,
+                      float* dx, hipStream_t s);
 hipError_t eh_drop_rows(const float* x, int64_t n, int d, float p, uint64_t seed, const int64_t* step, uint64_t salt,
                         float* x0, float* keep, hipStream_t s);
 
@@ -154,6 +159,19 @@ hipError_t eh_flow_expand(const int64_t* indptr, const int32_t* nbr, int64_t num
                           const int64_t* rows, int64_t n, const int64_t* offs, int64_t cap, int64_t* out_nbr,
                           int64_t* out_src, int32_t* overflow, hipStream_t s);
 hipError_t eh_seg_count(const int64_t* idx, int64_t n, int64_t size, int64_t* cnt, hipStream_t s);
+hipError_t eh_sage_block(const int64_t* inv, const int64_t* uniq, const int64_t* cnt, const int64_t* last_idx,
+                         int64_t cap_prev, int64_t f, int64_t cap_n, int self_loops, int64_t* new_n_id,
+                         int64_t* res_n_id, int64_t* edge_index, int64_t* counts, int64_t* last_new, int64_t* cnt_new,
+                         hipStream_t s);
+hipError_t eh_sage_place(const int64_t* inv, const int64_t* last_idx, int64_t cap_prev, int64_t f, int self_loops,
+                         const int64_t* indptr, int64_t* perm, hipStream_t s);
+hipError_t eh_gcn_norm_weight(const int64_t* dst, const int64_t* src, int64_t E, const int64_t* c0, int64_t n0,
+                              const int64_t* c1, int64_t n1, float* w, hipStream_t s);
+hipError_t eh_flow_block(const int64_t* src, const int64_t* offs, const int64_t* uniq, const int64_t* inv,
+                         const int64_t* cnt, const int64_t* last_idx, const int64_t* n_targets, int64_t cap_e,
+                         int64_t cap_prev, int64_t cap_n, int self_loops, int64_t* new_n_id, int64_t* res_n_id,
+                         int64_t* edge_index, int64_t* perm, int64_t* indptr, int64_t* counts, int64_t* last_new,
+                         int64_t* cnt_new, int32_t* overflow, hipStream_t s);
 
 // optim.hip
 hipError_t eh_flat_optim(float* p, const float* g, float* m, float* v, int64_t n, int64_t* step, float lr, float b1,

@@ -27,6 +27,8 @@ with self loops, one (t, position of t) per target.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from euler_amd.dataflow.dataflows import Block, DataFlow
@@ -110,6 +112,9 @@ def _dst_csr(src, offs, n_targets, cap_e, cap_t, self_loops):
     return perm, indptr
 
 
+_FUSED_BLOCK = os.environ.get("EULER_AMD_FLOW_FUSED", "1") == "1"
+
+
 def _unique_padded(x: torch.Tensor):
     """(uniq padded with -1, inverse (-1 for -1 entries), count [1]) in first-occurrence order"""
     if use_hip(x):
@@ -181,6 +186,19 @@ class DeviceFullFlow:
                 nbr, src, offs = full_neighbors_cpu(g, mask, n_id, cap_e, self.overflow)
             cat = torch.cat([nbr, n_id])
             uniq, inv, cnt = _unique_padded(cat)
+            if use_hip(n_id) and _FUSED_BLOCK:
+                # the block assembly below as one launch (flow.hip flow_block_kernel)
+                new_n_id, res_n_id, edge_index, perm, indptr, counts, last_idx, prev_cnt = hip().flow_block(
+                    src, offs, uniq, inv, cnt.reshape(1), last_idx, prev_cnt.reshape(1), cap_n, self.self_loops,
+                    self.overflow)
+                seg = SegmentIndex(edge_index[0], cap_prev)
+                seg._perm, seg._indptr, seg._counts = perm, indptr, counts
+                edge_index._euler_cache = {"_euler_seg0_%d" % cap_prev: seg}
+                df.blocks.append(Block(new_n_id, res_n_id, None, edge_index, [cap_prev, cap_n]))
+                df._last = new_n_id
+                n_id = new_n_id
+                cap_prev = cap_n
+                continue
             # a set beyond its capacity: flag it and drop the excess (never index past it)
             self.overflow.copy_(torch.maximum(self.overflow, (cnt.reshape(1) > cap_n).to(self.overflow.dtype)))
             new_n_id = uniq[:cap_n] if uniq.numel() >= cap_n else torch.cat(
@@ -262,6 +280,19 @@ class DeviceSageFlow:
             nbr = g.sample_neighbor(n_id, f, edge_types=et, default=-1, stream_id=10 + h).long().reshape(-1)
             cat = torch.cat([nbr, n_id])
             uniq, inv, cnt = _unique_padded(cat)
+            if use_hip(n_id) and _FUSED_BLOCK:
+                # the block assembly below + the destination CSR as three launches (flow.hip
+                # sage_block / sage_place): the convolutions' scatters and SpMM need no sort
+                new_n_id, res_n_id, edge_index, perm, indptr, counts, last_idx, _ = hip().sage_block(
+                    inv, uniq, cnt.reshape(1), last_idx, f, cap_n, self.self_loops)
+                seg = SegmentIndex(edge_index[0], cap_prev)
+                seg._perm, seg._indptr, seg._counts = perm, indptr, counts
+                edge_index._euler_cache = {"_euler_seg0_%d" % cap_prev: seg}
+                df.blocks.append(Block(new_n_id, res_n_id, None, edge_index, [cap_prev, cap_n]))
+                df._last = new_n_id
+                n_id = new_n_id
+                cap_prev = cap_n
+                continue
             new_n_id = uniq[:cap_n] if uniq.numel() >= cap_n else torch.cat(
                 [uniq, torch.full((cap_n - uniq.numel(),), -1, dtype=uniq.dtype, device=dev)])
             res_n_id = inv[nbr.numel():]

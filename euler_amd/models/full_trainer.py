@@ -34,7 +34,7 @@ import torch.nn.functional as F
 
 from euler_amd.dataflow.device_flow import DeviceFullFlow
 from euler_amd.models.captured import CapturedTrainer
-from euler_amd.ops import mp_ops
+from euler_amd.ops import gnn_ops, mp_ops
 
 __all__ = ["FullFlowTrainer"]
 
@@ -109,11 +109,8 @@ class FullFlowTrainer(CapturedTrainer):
         self._draw()
         roots = self.graph.sample_node(self.B, stream_id=1).long()
         logits, df = self._forward(roots)
-        y = mp_ops.gather(self.labels, roots)
-        loss = F.binary_cross_entropy_with_logits(logits, y)
-        with torch.no_grad():
-            pred, pos = logits >= 0, y > 0.5
-            self.counts += torch.stack([(pred & pos).sum(), (pred & ~pos).sum(), (~pred & pos).sum()])
+        # sigmoid cross-entropy + the F1 counts in one kernel pair (gnn_ops.bce_f1_loss)
+        loss = gnn_ops.bce_f1_loss(logits, self.labels, roots, self.counts)
         self._samples = roots
         return loss
 

@@ -601,6 +601,36 @@ def relation_tiles(edge_index, rel, size, R, N, K, aggr="mean") -> RelationTiles
     return _cached(edge_index, key, lambda: RelationTiles(edge_index, rel, size, R, aggr, tile=tm))
 
 
+# ----------------------------------------------------------------------------- multi-label loss + F1
+class _BceF1(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, rows, counts):
+        x = logits.float().contiguous()
+        ctx.save_for_backward(x, labels, rows)
+        return hip().bce_f1_fwd(x, labels, rows, counts)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, labels, rows = ctx.saved_tensors
+        return hip().bce_bwd(x, labels, rows, g.float().reshape(1).contiguous()), None, None, None
+
+
+def bce_f1_loss(logits, labels, rows, counts):
+    """``F.binary_cross_entropy_with_logits(logits, labels[rows])`` (mean) and the F1 counts
+    (tp, fp, fn of ``logits >= 0`` against ``labels > 0.5``) added into ``counts`` [3] —
+    two launches forward, one backward on the GPU (the torch composition is ~18 kernels)."""
+    rows = rows.reshape(-1).long()
+    if use_hip(logits, labels) and labels.dtype == torch.float32 and counts.dtype == torch.int64 \
+            and labels.is_contiguous():
+        return _BceF1.apply(logits, labels, rows.contiguous(), counts)
+    y = labels[rows]
+    loss = F.binary_cross_entropy_with_logits(logits.float(), y)
+    with torch.no_grad():
+        pred, pos = logits >= 0, y > 0.5
+        counts += torch.stack([(pred & pos).sum(), (pred & ~pos).sum(), (~pred & pos).sum()])
+    return loss
+
+
 # ----------------------------------------------------------------------------- K11 skip-gram loss
 def sgns_loss_reference(emb, pos, neg):
     emb = emb.reshape(emb.shape[0], -1).float()

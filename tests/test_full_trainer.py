@@ -116,7 +116,10 @@ def test_estimator_device_graph_sampled_flow_other_conv_cpu(tmp_path):
 # ----------------------------------------------------------------------------------------- GPU
 
 @pytest.mark.gpu
-def test_hip_full_neighbors_matches_cpu_twin():
+@pytest.mark.parametrize("self_loops", [True, False])
+def test_hip_full_neighbors_matches_cpu_twin(self_loops):
+    """the HIP expansion + dedup + fused block assembly (flow.hip flow_block) = the CPU
+    torch composition: node sets, positions, edges and the cached destination CSR"""
     from euler_amd.dataflow.device_flow import DeviceFullFlow
 
     _, m, _ = _setup("cuda")
@@ -125,11 +128,18 @@ def test_hip_full_neighbors_matches_cpu_twin():
     flow = m.gnn.sampler
     masks = _masks(g, flow)
     roots = torch.randint(0, g.num_rows, (64,), generator=torch.Generator().manual_seed(4))
-    d_gpu = DeviceFullFlow(g, masks, 64, add_self_loops=True).produce(roots.cuda())
-    d_cpu = DeviceFullFlow(gc, masks, 64, add_self_loops=True).produce(roots)
+    roots[5] = roots[9]
+    fg = DeviceFullFlow(g, masks, 64, add_self_loops=self_loops)
+    d_gpu = fg.produce(roots.cuda())
+    d_cpu = DeviceFullFlow(gc, masks, 64, add_self_loops=self_loops).produce(roots)
     for a, b in zip(d_gpu.blocks, d_cpu.blocks):
         assert torch.equal(a.n_id.cpu(), b.n_id) and torch.equal(a.res_n_id.cpu(), b.res_n_id)
         assert torch.equal(a.edge_index.cpu(), b.edge_index)
+        key = "_euler_seg0_%d" % a.size[0]
+        sa, sb = a.edge_index._euler_cache[key], b.edge_index._euler_cache[key]
+        assert torch.equal(sa.indptr.cpu(), sb.indptr) and torch.equal(sa.counts.cpu(), sb.counts)
+        assert torch.equal(sa.perm.cpu(), sb.perm)
+    assert int(fg.overflow.item()) == 0
 
 
 @pytest.mark.gpu

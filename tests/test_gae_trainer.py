@@ -89,3 +89,30 @@ def test_gae_device_path_gpu_captured(cora, tmp_path, cuda, enc):
     res = est.train()
     tr = est.device_trainer
     assert res["step"] == 64 and np.isfinite(res["loss"]) and tr.captures >= 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("self_loops", [True, False])
+def test_device_sage_flow_fused_block_matches_torch(cora, cuda, monkeypatch, self_loops):
+    """flow.hip sage_block / sage_place = the torch block assembly on the same draws, and
+    its destination CSR = the stable sort of the edge targets"""
+    import euler_amd.dataflow.device_flow as dfm
+    from euler_amd.graph.device_graph import DeviceGraph
+    from euler_amd.ops.mp_ops import SegmentIndex
+
+    g = DeviceGraph.from_engine(device=cuda, seed=2)
+    flow = dfm.DeviceSageFlow(g, [None, None], [4, 3], 32, add_self_loops=self_loops)
+    roots = g.sample_node(32).long()
+    state = g.rng.clone()
+    fused = flow.produce(roots)
+    g.rng.copy_(state)
+    monkeypatch.setattr(dfm, "_FUSED_BLOCK", False)
+    plain = flow.produce(roots)
+    for a, b in zip(fused.blocks, plain.blocks):
+        assert torch.equal(a.n_id, b.n_id) and torch.equal(a.res_n_id, b.res_n_id)
+        assert torch.equal(a.edge_index, b.edge_index)
+        seg = a.edge_index._euler_cache["_euler_seg0_%d" % a.size[0]]
+        ref = SegmentIndex(b.edge_index[0], a.size[0])
+        assert torch.equal(seg.indptr, ref.indptr) and torch.equal(seg.counts, ref.counts)
+        n = int(ref.indptr[-1])
+        assert torch.equal(seg.perm[:n], ref.perm[:n])

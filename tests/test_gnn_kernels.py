@@ -687,3 +687,26 @@ def test_zero_kernel_sizes(cuda):
         u = torch.full((n + 2,), 7.0, device=cuda)
         hip().zero_(u[1:n + 1])  # 4-byte-aligned view (byte kernel)
         assert float(u[0]) == 7.0 and bool((u[1:n + 1] == 0).all()) and float(u[n + 1]) == 7.0
+
+
+@pytest.mark.gpu
+def test_bce_f1_loss_matches_torch(cuda):
+    """fused multi-label sigmoid CE + F1 counts (embed.hip bce_f1_*) vs the torch composition"""
+    import torch.nn.functional as F
+
+    torch.manual_seed(0)
+    labels = (torch.rand(700, 121, device=cuda) < 0.3).float()
+    rows = torch.randint(0, 700, (512,), device=cuda)
+    x = (torch.randn(512, 121, device=cuda) * 3).requires_grad_(True)
+    counts = torch.zeros(3, dtype=torch.long, device=cuda)
+    loss = G.bce_f1_loss(x, labels, rows, counts)
+    loss.backward()
+    xr = x.detach().clone().requires_grad_(True)
+    y = labels[rows]
+    ref = F.binary_cross_entropy_with_logits(xr, y)
+    ref.backward()
+    assert abs(float(loss) - float(ref)) < 1e-5 * max(1.0, abs(float(ref)))
+    assert torch.allclose(x.grad, xr.grad, atol=1e-7, rtol=1e-4)
+    pred, pos = xr.detach() >= 0, y > 0.5
+    want = [int((pred & pos).sum()), int((pred & ~pos).sum()), int((~pred & pos).sum())]
+    assert counts.tolist() == want
