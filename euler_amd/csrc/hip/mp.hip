@@ -20,6 +20,8 @@ template <>
 struct Vec<16> { using T = uint4_t; };
 template <>
 struct Vec<4> { using T = uint32_t; };
+template <>
+struct Vec<2> { using T = uint16_t; };  // rows of an odd number of bf16 values (e.g. 1433-d)
 
 template <int VB, typename IdxT>
 __global__ __launch_bounds__(256) void gather_rows_kernel(const uint8_t* __restrict__ x, int64_t n_rows,
@@ -429,8 +431,10 @@ hipError_t eh_gather_rows(const void* x, int64_t n_rows, int64_t row_bytes, cons
   if (n == 0 || row_bytes == 0) return hipSuccess;
   const bool v16 = (row_bytes % 16 == 0) && (reinterpret_cast<uintptr_t>(x) % 16 == 0) &&
                    (reinterpret_cast<uintptr_t>(out) % 16 == 0);
-  if (!v16 && row_bytes % 4 != 0) return hipErrorInvalidValue;
-  const int vb = v16 ? 16 : 4;
+  const bool v4 = !v16 && row_bytes % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 4 == 0 &&
+                  reinterpret_cast<uintptr_t>(out) % 4 == 0;
+  if (!v16 && !v4 && row_bytes % 2 != 0) return hipErrorInvalidValue;
+  const int vb = v16 ? 16 : (v4 ? 4 : 2);
   const int64_t total = n * (row_bytes / vb);
   const dim3 grid = grid_for(total);
   const uint8_t* xb = static_cast<const uint8_t*>(x);
@@ -442,12 +446,19 @@ hipError_t eh_gather_rows(const void* x, int64_t n_rows, int64_t row_bytes, cons
     else
       hipLaunchKernelGGL((gather_rows_kernel<16, int32_t>), grid, dim3(256), 0, s, xb, n_rows, row_bytes,
                          static_cast<const int32_t*>(idx), n, ob);
-  } else {
+  } else if (v4) {
     if (idx_is64)
       hipLaunchKernelGGL((gather_rows_kernel<4, int64_t>), grid, dim3(256), 0, s, xb, n_rows, row_bytes,
                          static_cast<const int64_t*>(idx), n, ob);
     else
       hipLaunchKernelGGL((gather_rows_kernel<4, int32_t>), grid, dim3(256), 0, s, xb, n_rows, row_bytes,
+                         static_cast<const int32_t*>(idx), n, ob);
+  } else {
+    if (idx_is64)
+      hipLaunchKernelGGL((gather_rows_kernel<2, int64_t>), grid, dim3(256), 0, s, xb, n_rows, row_bytes,
+                         static_cast<const int64_t*>(idx), n, ob);
+    else
+      hipLaunchKernelGGL((gather_rows_kernel<2, int32_t>), grid, dim3(256), 0, s, xb, n_rows, row_bytes,
                          static_cast<const int32_t*>(idx), n, ob);
   }
   return hipGetLastError();

@@ -710,3 +710,16 @@ def test_bce_f1_loss_matches_torch(cuda):
     pred, pos = xr.detach() >= 0, y > 0.5
     want = [int((pred & pos).sum()), int((pred & ~pos).sum()), int((~pred & pos).sum())]
     assert counts.tolist() == want
+
+
+@pytest.mark.gpu
+def test_gather_rows_odd_bf16_width(cuda):
+    """gather of bf16 rows with an odd width (Cora's 1433 features: 2866-byte rows)"""
+    from euler_amd.ops import mp_ops
+
+    x = torch.randn(50, 1433, device=cuda).to(torch.bfloat16)
+    idx = torch.tensor([3, -1, 49, 0, 3], device=cuda)
+    out = mp_ops.gather(x, idx)
+    ref = x[idx.clamp(min=0)]
+    ref[1] = 0
+    assert torch.equal(out, ref)
