@@ -16,6 +16,7 @@ run() {  # name timeout command...
   echo "$name $(tail -1 "$R/$name.log" | cut -c1-160)"
 }
 for i in 1 2 3; do run "headline_$i" 300 python -u bench.py --steps 1000 --warmup 50; done
+for i in 1 2 3; do run "config2_$i" 300 python -u bench.py --steps 1000 --warmup 50 --num-nodes 10000000; done
 for i in 1 2 3; do run "unsup_$i" 300 python -u benchmarks/bench_unsup_sage.py --steps 2000; done
 for i in 1 2 3; do run "kg_$i" 300 python -u benchmarks/bench_kg.py --steps 300 --warmup 20 --eval-after 0; done
 for i in 1 2 3; do run "gcn_$i" 400 python -u benchmarks/bench_gcn.py --steps 400 --engine-steps 40; done
