@@ -533,7 +533,8 @@ std::vector<torch::Tensor> kg_fwd(torch::Tensor ent, torch::Tensor rel, torch::T
 void kg_step(torch::Tensor h, torch::Tensor rel, torch::Tensor pool, torch::Tensor t_src, torch::Tensor t_dst,
              torch::Tensor t_rel, torch::Tensor step, int64_t seed, int64_t kind, bool normalize, double margin,
              torch::Tensor o_src, torch::Tensor o_dst, torch::Tensor o_ridx, torch::Tensor o_neg, torch::Tensor coef,
-             torch::Tensor part, torch::Tensor loss, torch::Tensor dent, torch::Tensor drel) {
+             torch::Tensor part, torch::Tensor loss, torch::Tensor dent, torch::Tensor drel,
+             c10::optional<torch::Tensor> drel_rep) {
   for (auto* t : {&h, &rel, &coef, &part, &loss, &dent, &drel}) typed(*t, torch::kFloat32, "kg_step float buffer");
   for (auto* t : {&pool, &t_src, &t_dst, &t_rel, &step, &o_src, &o_dst, &o_ridx, &o_neg})
     typed(*t, torch::kInt64, "kg_step id buffer");
@@ -548,8 +549,17 @@ void kg_step(torch::Tensor h, torch::Tensor rel, torch::Tensor pool, torch::Tens
   int nparts = 0;
   ok(eh_kg_step(nullptr, nullptr, nullptr, 1, nullptr, nullptr, nullptr, 1, nullptr, 0, B, static_cast<int>(K),
                 static_cast<int>(D), static_cast<int>(kind), 0, 0.f, nullptr, nullptr, nullptr, nullptr, nullptr,
-                nullptr, nullptr, nullptr, nullptr, &nparts, stream()),
+                nullptr, nullptr, nullptr, nullptr, &nparts, nullptr, 0, 0, stream()),
      "kg_step (grid)");
+  float* rep_p = nullptr;
+  int rep = 0;
+  if (drel_rep.has_value()) {  // [rep, R, D] relation-gradient replicas
+    typed(*drel_rep, torch::kFloat32, "drel_rep");
+    TORCH_CHECK(drel_rep->dim() == 3 && drel_rep->size(1) == rel.size(0) && drel_rep->size(2) == rel.size(1),
+                "kg_step: drel_rep [rep, R, D]");
+    rep_p = drel_rep->data_ptr<float>();
+    rep = static_cast<int>(drel_rep->size(0));
+  }
   TORCH_CHECK(part.numel() >= nparts, "kg_step: part needs ", nparts, " entries");
   TORCH_CHECK(pool.numel() > 0 && loss.numel() >= 1 && step.numel() >= 1, "kg_step: empty pool / loss / step");
   const c10::DeviceGuard g(h.device());
@@ -559,7 +569,7 @@ void kg_step(torch::Tensor h, torch::Tensor rel, torch::Tensor pool, torch::Tens
                 static_cast<int>(kind), normalize ? 1 : 0, static_cast<float>(margin), o_src.data_ptr<int64_t>(),
                 o_dst.data_ptr<int64_t>(), o_ridx.data_ptr<int64_t>(), o_neg.data_ptr<int64_t>(),
                 coef.data_ptr<float>(), part.data_ptr<float>(), loss.data_ptr<float>(), dent.data_ptr<float>(),
-                drel.data_ptr<float>(), nullptr, stream()),
+                drel.data_ptr<float>(), nullptr, rep_p, rep, rel.size(0), stream()),
      "kg_step");
 }
 
@@ -567,7 +577,7 @@ int64_t kg_step_parts(int64_t B, int64_t D) {
   int nparts = 0;
   ok(eh_kg_step(nullptr, nullptr, nullptr, 1, nullptr, nullptr, nullptr, 1, nullptr, 0, B, 1, static_cast<int>(D), 1,
                 0, 0.f, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, &nparts,
-                nullptr),
+                nullptr, 0, 0, nullptr),
      "kg_step_parts");
   return nparts;
 }
@@ -985,7 +995,10 @@ void register_gnn_ops(pybind11::module& m) {
   m.def("gather_f32_bf16", &gather_f32_bf16, py::arg("x"), py::arg("idx"), py::arg("out") = py::none());
   m.def("sgns_apply_", &sgns_apply_);
   m.def("kg_fwd", &kg_fwd);
-  m.def("kg_step", &kg_step);
+  m.def("kg_step", &kg_step, py::arg("h"), py::arg("rel"), py::arg("pool"), py::arg("t_src"), py::arg("t_dst"),
+        py::arg("t_rel"), py::arg("step"), py::arg("seed"), py::arg("kind"), py::arg("normalize"), py::arg("margin"),
+        py::arg("o_src"), py::arg("o_dst"), py::arg("o_ridx"), py::arg("o_neg"), py::arg("coef"), py::arg("part"),
+        py::arg("loss"), py::arg("dent"), py::arg("drel"), py::arg("drel_rep") = py::none());
   m.def("kg_step_parts", &kg_step_parts);
   m.def("cast_bf16", &cast_bf16);
   m.def("drop_rows", &drop_rows);

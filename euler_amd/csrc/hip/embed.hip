@@ -551,7 +551,20 @@ struct KgStepArgs {
   float* part;  // [blocks of the fwd launch]
   float* loss;  // [1]
   int nparts;
+  float* drel_rep;     // [rep][R][D] relation-gradient replicas (rep == 0: add into drel directly)
+  int64_t rep_stride;  // R * D
+  int rep;
 };
+
+// drel += sum of the replicas (fixed order)
+__global__ __launch_bounds__(256) void kg_rep_reduce_kernel(const float* __restrict__ rep, int nrep, int64_t n,
+                                                            float* __restrict__ drel) {
+  grid_stride(n, [&](int64_t i) {
+    float v = 0.f;
+    for (int r = 0; r < nrep; ++r) v += rep[static_cast<int64_t>(r) * n + i];
+    drel[i] += v;
+  });
+}
 
 __device__ __forceinline__ uint32_t kg_word(uint64_t seed, uint64_t ctr, int64_t row, int w) {
   const uint4_t r = Philox::gen(seed, ctr, static_cast<uint64_t>(row) * 64u + static_cast<uint64_t>(w >> 2));
@@ -634,7 +647,10 @@ __global__ __launch_bounds__(256) void kg_step_bwd_kernel(KgStepArgs s, float* _
     kg_scatter(dent, ns, L.sub, a.D, a.lp, a.normalize, n, nn, dn);
   }
   kg_scatter(dent, hs, L.sub, a.D, a.lp, a.normalize, h, nh, dh);
-  kg_scatter(drel, rs, L.sub, a.D, a.lp, a.normalize, r, nr, dr);
+  // relation rows: the power-law relation table makes a few of them hot; with replicas each
+  // block adds into its own copy (blockIdx % rep), summed by kg_rep_reduce_kernel
+  kg_scatter(s.rep ? s.drel_rep + static_cast<int64_t>(blockIdx.x % s.rep) * s.rep_stride : drel, rs, L.sub, a.D,
+             a.lp, a.normalize, r, nr, dr);
   kg_scatter(dent, ts, L.sub, a.D, a.lp, a.normalize, t, nt, dt);
 }
 
@@ -940,8 +956,8 @@ hipError_t eh_kg_step(const float* ent, const float* rel, const int64_t* pool, i
                       const int64_t* t_dst, const int64_t* t_rel, int64_t num_ent, const int64_t* step, uint64_t seed,
                       int64_t B, int K, int D, int kind, int normalize, float margin, int64_t* o_src, int64_t* o_dst,
                       int64_t* o_ridx, int64_t* o_neg, float* coef, float* part, float* loss, float* dent,
-                      float* drel, int* nparts_out, hipStream_t s) {
-  if (B <= 0 || K <= 0 || K > 255 || P <= 0 || num_ent <= 0) return hipErrorInvalidValue;
+                      float* drel, int* nparts_out, float* drel_rep, int rep, int64_t num_rel, hipStream_t s) {
+  if (B <= 0 || K <= 0 || K > 255 || P <= 0 || num_ent <= 0 || rep < 0) return hipErrorInvalidValue;
   if (D % 4 != 0 || D > 256 || kind < 0 || kind > 2) return hipErrorInvalidValue;
   KgStepArgs a;
   a.k = kg_args(ent, rel, o_src, o_dst, o_ridx, o_neg, B, K, D, kind, 2, normalize);
@@ -965,8 +981,15 @@ hipError_t eh_kg_step(const float* ent, const float* rel, const int64_t* pool, i
   a.part = part;
   a.loss = loss;
   a.nparts = static_cast<int>(grid.x);
+  a.rep = drel_rep ? rep : 0;
+  a.drel_rep = drel_rep;
+  a.rep_stride = num_rel * D;
+  if (a.rep) EULER_HIP_CHECK(eh_zero(drel_rep, a.rep * a.rep_stride * 4, s));
   hipLaunchKernelGGL(kg_step_fwd_kernel, grid, dim3(256), 0, s, a);
   hipLaunchKernelGGL(kg_step_bwd_kernel, grid, dim3(256), 0, s, a, dent, drel);
+  if (a.rep)
+    hipLaunchKernelGGL(kg_rep_reduce_kernel, grid_for(a.rep_stride), dim3(256), 0, s, drel_rep, a.rep, a.rep_stride,
+                       drel);
   return hipGetLastError();
 }
 

@@ -113,7 +113,7 @@ hipError_t eh_kg_step(const float* ent, const float* rel, const int64_t* pool, i
                       const int64_t* t_dst, const int64_t* t_rel, int64_t num_ent, const int64_t* step, uint64_t seed,
                       int64_t B, int K, int D, int kind, int normalize, float margin, int64_t* o_src, int64_t* o_dst,
                       int64_t* o_ridx, int64_t* o_neg, float* coef, float* part, float* loss, float* dent,
-                      float* drel, int* nparts_out, hipStream_t s);
+                      float* drel, int* nparts_out, float* drel_rep, int rep, int64_t num_rel, hipStream_t s);
 hipError_t eh_cast_bf16(const float* x, int64_t n, void* out, hipStream_t s);
 hipError_t eh_zero(void* x, int64_t bytes, hipStream_t s);
 int eh_bce_parts(int64_t n);

@@ -166,6 +166,10 @@ class RgcnTransEStep:
         self.coef = torch.empty(self.B, **f32)
         self.part = torch.empty(int(hip().kg_step_parts(self.B, self.D)), **f32)
         self.loss = torch.zeros(1, **f32)
+        # relation-gradient replicas for the backward scoring kernel's hot relations
+        # (EULER_AMD_KG_REL_REP=0: add straight into the relation table's gradient)
+        rep = int(os.environ.get("EULER_AMD_KG_REL_REP", "16"))
+        self.drel_rep = torch.empty(rep, self.R, self.D, **f32) if rep > 0 else None
         self._fc_splits = gnn_ops._gemm_splits(self.N, -(-self.D // 64) ** 2)
 
     # ------------------------------------------------------------------ step
@@ -214,7 +218,7 @@ class RgcnTransEStep:
             H.zero_(dtop)
         H.kg_step(x, m.rel.detach(), self.pool, self.t_src, self.t_dst, self.t_rel, self.opt.step_count, self.seed,
                   gnn_ops.KG_KINDS["l2"], self.normalize, self.margin, self.o_src, self.o_dst, self.o_rel, self.o_neg,
-                  self.coef, self.part, self.loss, dtop, m.rel.grad)
+                  self.coef, self.part, self.loss, dtop, m.rel.grad, self.drel_rep)
         self._chk("scores", dtop, m.rel.grad, self.loss)
         for li in range(L - 1, -1, -1):
             W, Wfc, tiles, basis = self.layers[li]
