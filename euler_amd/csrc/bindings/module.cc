@@ -797,6 +797,7 @@ PYBIND11_MODULE(_engine, m) {
                           bool fuse) {
     CompileOptions o;
     o.mode = mode == "local" ? CompileMode::kLocal : CompileMode::kDistribute;
+    o.graph_partition = mode == "graph_partition";
     o.shard_num = shards;
     o.neighbor_indexes = nbr_idx;
     o.fuse = fuse;

@@ -482,10 +482,16 @@ class Optimizer {
     SplitKind split = rule.split;
     if (split == SplitKind::kId && !has_input) split = SplitKind::kAllShards;
     if (split == SplitKind::kId) {
-      NodeDef& sp = Add("ID_SPLIT");
-      sp.inputs = {nd.inputs[0]};
-      sp.output_num = 2 * S;
-      const std::string spn = sp.name();
+      std::string spn;
+      // bucket codes (API_SAMPLE_NODE_AT) are not ids: they keep the hash route
+      if (opt_.graph_partition && S > 1 && nd.op != "API_SAMPLE_NODE_AT") {
+        spn = GpSplit(nd.inputs[0], S);
+      } else {
+        NodeDef& sp = Add("ID_SPLIT");
+        sp.inputs = {nd.inputs[0]};
+        sp.output_num = 2 * S;
+        spn = sp.name();
+      }
       for (int s = 0; s < S; ++s) {
         std::vector<std::string> ins = nd.inputs;
         ins[0] = spn + ":" + std::to_string(2 * s);
@@ -577,6 +583,33 @@ class Optimizer {
     for (int k = 0; k < nd.output_num; ++k) rename_[orig.Output(k)] = final_out[k];
   }
 
+  // graph_partition routing of the ids (or edges, by source) in `ids`: every shard reports
+  // the type of each id (-1: not held there), GP_ID_SPLIT sends each row to its first holder;
+  // one ownership round per distinct input of the query
+  std::string GpSplit(const std::string& ids, int S) {
+    auto it = gp_split_.find(ids);
+    if (it != gp_split_.end()) return it->second;
+    NodeDef& src = Add("ID_SRC");
+    src.inputs = {ids};
+    const std::string src_out = src.Output(0);
+    std::vector<std::string> types;
+    for (int s = 0; s < S; ++s) {
+      NodeDef q;
+      q.op = "API_GET_NODE_T";
+      q.id = next_id_++;
+      q.output_num = 1;
+      std::vector<std::string> outs;
+      Remote(q, s, {src_out}, {}, &outs);
+      types.push_back(outs[0]);
+    }
+    NodeDef& sp = Add("GP_ID_SPLIT");
+    sp.inputs = {ids};
+    sp.inputs.insert(sp.inputs.end(), types.begin(), types.end());
+    sp.output_num = 2 * S;
+    gp_split_[ids] = sp.name();
+    return sp.name();
+  }
+
   // common-subexpression elimination of identical split / unique nodes (reference optimizer.cc:167-201)
   void Cse() {
     std::map<std::string, std::string> seen;  // signature -> node name
@@ -611,6 +644,7 @@ class Optimizer {
 
   const CompileOptions& opt_;
   DAGDef* out_;
+  std::map<std::string, std::string> gp_split_;  // ids input -> its GP_ID_SPLIT node
   int next_id_ = 1;
   std::unordered_map<std::string, std::string> rename_;
 };
@@ -771,7 +805,8 @@ Status Compiler::Optimize(const DAGDef& logical, const CompileOptions& opt, DAGD
 }
 
 Status Compiler::Compile(const std::string& query, const CompileOptions& opt, std::shared_ptr<const DAGDef>* dag) {
-  const std::string key = std::to_string(static_cast<int>(opt.mode)) + (opt.fuse ? "f" : "u") + "|" +
+  const std::string key = std::to_string(static_cast<int>(opt.mode)) + (opt.fuse ? "f" : "u") +
+                          (opt.graph_partition ? "g" : "h") + "|" +
                           std::to_string(opt.shard_num) + "|" +
                           Join(opt.neighbor_indexes, ",") + "|" + query;
   {

@@ -45,6 +45,10 @@ struct CompileOptions {
   // fuse independent REMOTE nodes of a shard into one RPC (reference FusionAndShardRule,
   // compiler.cc:92-162 / DAGDef::FusionNodes, dag_def.cc:128-203); EULER_GQL_FUSE=0 disables
   bool fuse = true;
+  // graph_partition mode: shards hold arbitrary partitions (e.g. a min-cut partitioner's),
+  // not id-hash ones; id-routed ops first ask every shard which ids it holds
+  // (API_GET_NODE_T != -1) and route each id to its owner (GP_ID_SPLIT)
+  bool graph_partition = false;
 };
 
 // REMOTE fusion pass of the distribute-mode optimizer (exposed for tests)

@@ -30,6 +30,7 @@
 #include <unordered_map>
 #include <unordered_set>
 
+#include <stdexcept>
 #include "ops/ops_util.h"
 
 namespace euler {
@@ -161,6 +162,57 @@ class IdSplitOp : public OpKernel {
       // edges are split by their source (reference id_split_op.cc:46-49)
       const uint64_t id = static_cast<uint64_t>(in.AsInt(i * width));
       rows[ShardOf(id, P, S)].push_back(i);
+    }
+    for (int s = 0; s < S; ++s) {
+      Tensor part = TakeRows(in, rows[s], width);
+      if (!edges) part.Reshape({static_cast<int64_t>(rows[s].size())});
+      ctx->Set(nd.Output(2 * s), part);
+      std::vector<int32_t> mi(rows[s].begin(), rows[s].end());
+      ctx->Set(nd.Output(2 * s + 1), Tensor::FromVector(mi));
+    }
+  }
+};
+
+// graph_partition mode: the node ids of an id-routed input (edges [n, 3]: their sources)
+class IdSrcOp : public OpKernel {
+ public:
+  void Compute(const NodeDef& nd, OpContext* ctx) override {
+    const Tensor& in = ctx->Get(nd.inputs.at(0));
+    const bool edges = in.shape().size() == 2 && in.dim(1) == 3;
+    const int64_t n = edges ? in.dim(0) : in.numel();
+    std::vector<int64_t> ids(n);
+    for (int64_t i = 0; i < n; ++i) ids[i] = in.AsInt(edges ? i * 3 : i);
+    ctx->Set(nd.Output(0), Tensor::FromVector(ids));
+  }
+};
+
+// graph_partition mode: inputs (x, types_0 .. types_{S-1}) with types_s[i] = the type shard
+// s reports for row i's node (-1: not held there); row i goes to the first holder, a row
+// no shard holds to its hash shard (it reads as missing there, as under hash routing).
+// Outputs as ID_SPLIT: 2s = the rows of shard s, 2s + 1 = their positions.
+class GpIdSplitOp : public OpKernel {
+ public:
+  void Compute(const NodeDef& nd, OpContext* ctx) override {
+    const Tensor& in = ctx->Get(nd.inputs.at(0));
+    const int S = static_cast<int>(nd.inputs.size()) - 1;
+    const uint32_t P = ctx->env()->num_partitions;
+    const bool edges = in.shape().size() == 2 && in.dim(1) == 3;
+    const int64_t n = edges ? in.dim(0) : in.numel();
+    const int64_t width = edges ? 3 : 1;
+    std::vector<const Tensor*> types(S);
+    for (int s = 0; s < S; ++s) {
+      types[s] = &ctx->Get(nd.inputs.at(1 + s));
+      if (types[s]->numel() != n)
+        throw std::runtime_error("GP_ID_SPLIT: shard " + std::to_string(s) + " answered " +
+                                 std::to_string(types[s]->numel()) + " types for " + std::to_string(n) + " rows");
+    }
+    std::vector<std::vector<int64_t>> rows(S);
+    for (int64_t i = 0; i < n; ++i) {
+      int owner = -1;
+      for (int s = 0; s < S && owner < 0; ++s)
+        if (types[s]->AsInt(i) >= 0) owner = s;
+      if (owner < 0) owner = ShardOf(static_cast<uint64_t>(in.AsInt(i * width)), P, S);
+      rows[owner].push_back(i);
     }
     for (int s = 0; s < S; ++s) {
       Tensor part = TakeRows(in, rows[s], width);
@@ -745,6 +797,8 @@ class SampleGraphLabelOp : public OpKernel {
 }  // namespace
 
 REGISTER_OP_KERNEL("ID_SPLIT", IdSplitOp);
+REGISTER_OP_KERNEL("ID_SRC", IdSrcOp);
+REGISTER_OP_KERNEL("GP_ID_SPLIT", GpIdSplitOp);
 REGISTER_OP_KERNEL("BROAD_CAST_SPLIT", BroadcastSplitOp);
 REGISTER_OP_KERNEL("SAMPLE_NODE_SPLIT", SampleNodeSplitOp);
 REGISTER_OP_KERNEL("SAMPLE_EDGE_SPLIT", SampleEdgeSplitOp);

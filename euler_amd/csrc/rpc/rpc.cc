@@ -1525,22 +1525,13 @@ Status QueryProxy::Init(const std::map<std::string, std::string>& config) {
     env_.num_partitions = std::max<uint32_t>(1, meta_.partitions_num);
     env_.index_info = metas[0].index_info;
     FillWeightTables(metas);
-  } else if (mode_ == "graph_partition") {
-    // The reference's graph_partition mode (query_proxy.cc:35-60, optimizer.cc:235-454)
-    // macro-fuses every shard-executable op of a query into one sub-DAG that each shard
-    // runs on its own partition, with GP_* merges chaining the per-hop row orders.  Its
-    // multi-hop results are partition-local approximations; euler_amd serves sharded
-    // graphs with exact distribute mode, whose REMOTE fusion already costs one RPC per
-    // shard per hop.  Refuse instead of silently running distribute semantics.  (The
-    // reference's own rule table routes API_GET_NODE / API_SAMPLE_NB / API_GET_P ids
-    // through GP_BROAD_CAST_SPLIT, optimizer.h:56-61, a kernel nothing in
-    // euler/core/kernels registers, so those plans cannot execute there either.)
-    return Status::Unimplemented(
-        "graph_partition mode is not supported: use mode=remote (distribute compiler with per-hop REMOTE "
-        "fusion; GP_* merge kernels are available as single ops via run_op)");
-  } else if (mode_ == "remote") {
+  } else if (mode_ == "remote" || mode_ == "graph_partition") {
+    // graph_partition: the same shard cluster, but the shards hold arbitrary partitions
+    // (reference query_proxy.cc:35-60 mode names); id-routed ops ask the shards who holds
+    // each id first (CompileOptions::graph_partition), hop by hop, so results stay exact
+    // (the reference's graph_partition plans run each query partition-locally instead)
     std::string reg = Cfg(config, "registry", Cfg(config, "zk_path", ""));
-    if (reg.empty()) return Status::InvalidArgument("remote mode needs registry=<dir|memory:name>");
+    if (reg.empty()) return Status::InvalidArgument(mode_ + " mode needs registry=<dir|memory:name>");
     auto r = Registry::Open(reg);
     std::map<int, std::vector<std::pair<Endpoint, ShardMeta>>> listing;
     int64_t want = 0;
@@ -1583,6 +1574,7 @@ Status QueryProxy::Init(const std::map<std::string, std::string>& config) {
   env_.clients = clients_.get();
   copt_.mode = CompileMode::kDistribute;
   copt_.shard_num = env_.shard_num;
+  copt_.graph_partition = mode_ == "graph_partition";
   {
     const char* f = std::getenv("EULER_GQL_FUSE");
     copt_.fuse = !(f && f[0] == '0');

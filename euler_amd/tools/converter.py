@@ -162,11 +162,16 @@ def _neighbor_block(groups, n_types) -> bytes:
 class EulerGenerator:
     """``EulerGenerator(graph_json, index_meta, out_dir, partition_num).do()`` (reference API)."""
 
-    def __init__(self, graph_json, index_meta, out_dir, partition_num=1, prefix="graph"):
+    def __init__(self, graph_json, index_meta, out_dir, partition_num=1, prefix="graph", partition_fn=None):
         self.graph_json = graph_json
         self.index_meta = index_meta
         self.out_dir = out_dir
         self.partition_num = int(partition_num)
+        # node id -> partition (edges follow their source); default id % partition_num, the
+        # layout remote mode routes by.  Any other assignment (a min-cut partitioner's) is
+        # served by mode=graph_partition.
+        P = self.partition_num
+        self.partition_fn = partition_fn if partition_fn is not None else (lambda i: int(i) % P)
         self.prefix = prefix
 
     def _load(self, x):
@@ -199,20 +204,26 @@ class EulerGenerator:
             rec += _neighbor_block(out_nb.get(n["id"], {}), n_et)
             rec += _neighbor_block(in_nb.get(n["id"], {}), n_et)
             rec += _features_block(meta.node_meta, n.get("features", []))
-            node_files[int(n["id"]) % P] += struct.pack("<I", len(rec)) + rec
+            node_files[self._part(n["id"])] += struct.pack("<I", len(rec)) + rec
         edge_files = [bytearray() for _ in range(P)]
         for e in data["edges"]:
             rec = struct.pack("<QQif", int(e["src"]), int(e["dst"]), meta.edge_types[str(e["type"])], float(e["weight"]))
             rec += _features_block(meta.edge_meta, e.get("features", []))
-            edge_files[int(e["src"]) % P] += struct.pack("<I", len(rec)) + rec
+            edge_files[self._part(e["src"])] += struct.pack("<I", len(rec)) + rec
         for p in range(P):
             with open(os.path.join(self.out_dir, "Node", "%s_%d.dat" % (self.prefix, p)), "wb") as f:
                 f.write(node_files[p])
             with open(os.path.join(self.out_dir, "Edge", "%s_%d.dat" % (self.prefix, p)), "wb") as f:
                 f.write(edge_files[p])
         if self.index_meta:
-            _write_indexes(data, self._load(self.index_meta), meta, self.out_dir, P)
+            _write_indexes(data, self._load(self.index_meta), meta, self.out_dir, P, self._part)
         return self.out_dir
+
+    def _part(self, node_id):
+        p = int(self.partition_fn(int(node_id)))
+        if not 0 <= p < self.partition_num:
+            raise ValueError(f"partition_fn({node_id}) = {p} is not in [0, {self.partition_num})")
+        return p
 
 
 def _index_keys(spec):
@@ -228,7 +239,8 @@ def _index_keys(spec):
     return out
 
 
-def _write_indexes(data, spec, meta, out_dir, P):
+def _write_indexes(data, spec, meta, out_dir, P, part_of=None):
+    part_of = part_of or (lambda i: int(i) % P)
     per_part = [defaultdict(list) for _ in range(P)]  # key -> [(value, id, weight)] or neighbor dict
     nbr_node_vals = defaultdict(dict)  # neighbor-index key -> node id -> (value, id, w)
     edge_nbr = defaultdict(lambda: defaultdict(list))  # key -> src -> [(value, dst, w)]
@@ -241,7 +253,7 @@ def _write_indexes(data, spec, meta, out_dir, P):
 
     node_spec = spec.get("node", {})
     for n in data["nodes"]:
-        part = int(n["id"]) % P
+        part = part_of(n["id"])
         fs = node_spec.get("features", {})
         for f in n.get("features", []):
             if f["name"] in fs:
@@ -256,7 +268,7 @@ def _write_indexes(data, spec, meta, out_dir, P):
                 add(key, n[k], n["id"], n["weight"], part)
     edge_spec = spec.get("edge", {})
     for e in data["edges"]:
-        part = int(e["src"]) % P
+        part = part_of(e["src"])
         etno = meta.edge_types[str(e["type"])]
         iid = edge_id_hash(e["src"], e["dst"], etno)
         fs = edge_spec.get("features", {})
@@ -280,10 +292,10 @@ def _write_indexes(data, spec, meta, out_dir, P):
     for key, vals in nbr_node_vals.items():
         for e in data["edges"]:
             if e["dst"] in vals:
-                nbr_data[int(e["src"]) % P][key][e["src"]].append(vals[e["dst"]])
+                nbr_data[part_of(e["src"])][key][e["src"]].append(vals[e["dst"]])
     for key, d in edge_nbr.items():
         for src, lst in d.items():
-            nbr_data[int(src) % P][key][src].extend(lst)
+            nbr_data[part_of(src)][key][src].extend(lst)
 
     for key in _index_keys(spec):
         name, vtype, idtype, kind = key.split(":")
@@ -321,5 +333,5 @@ def _range_blob(items, vtype, idtype):
     return out + _vec("f", cum)
 
 
-def convert_json(graph_json, out_dir, partition_num=1, index_meta=None):
-    return EulerGenerator(graph_json, index_meta, out_dir, partition_num).do()
+def convert_json(graph_json, out_dir, partition_num=1, index_meta=None, partition_fn=None):
+    return EulerGenerator(graph_json, index_meta, out_dir, partition_num, partition_fn=partition_fn).do()

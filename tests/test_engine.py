@@ -320,3 +320,20 @@ def test_udf_registry(graph):
     with pytest.raises(RuntimeError, match="unknown udf"):
         ea.run_gql("v(nodes).values(dense_f4).udf_nope(dense_f4).as(x)", {"nodes": np.array([1], np.uint64)},
                    ["x:0"])
+
+
+def test_graph_partition_plan_shape():
+    """mode graph_partition: an id-routed op's ids go through one ownership round (ID_SRC,
+    a REMOTE API_GET_NODE_T per shard) and GP_ID_SPLIT instead of the hash ID_SPLIT, once
+    per distinct routed input of the query"""
+    import euler_amd._engine as E
+
+    q = "v(nodes).as(n0).sampleNB(et, n, -1).as(nb).v_select(n0).values(fid).as(f)"
+    plan = E.compile_gql(q, "graph_partition", 2, [], False)
+    ops = [n["op"] for n in plan]
+    # two distinct routed inputs: the raw ids (sampleNB) and their unique set (values)
+    assert "ID_SPLIT" not in ops and ops.count("ID_SRC") == 2 and ops.count("GP_ID_SPLIT") == 2
+    owner = [n for n in plan if n["op"] == "REMOTE" and n["inner"] == ["API_GET_NODE_T"]]
+    assert sorted(n["shard"] for n in owner) == [0, 0, 1, 1]
+    hash_plan = [n["op"] for n in E.compile_gql(q, "distribute", 2, [], False)]
+    assert "ID_SPLIT" in hash_plan and "GP_ID_SPLIT" not in hash_plan

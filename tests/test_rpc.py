@@ -342,10 +342,13 @@ def test_fused_fanout_with_feature_one_rpc_per_shard_per_hop(cluster):
     assert out["1"][1] == [3, 6, 12] and out["1"][2] and out["0"][2]
 
 
-def test_graph_partition_mode_rejected(cluster):
+def test_graph_partition_mode_on_hash_partitions(cluster):
+    """graph_partition mode also serves the id-hash layout (ownership lookups find the same
+    shards hash routing would)"""
     data, reg = cluster
-    with pytest.raises(Exception, match="graph_partition mode is not supported"):
-        ea.initialize_graph({"mode": "graph_partition", "registry": reg, "shard_num": 2})
+    ea.initialize_graph({"mode": "graph_partition", "registry": reg, "shard_num": 2})
+    ids, _, _ = ea.get_full_neighbor([1, 2], ["0", "1"])
+    assert ids.to_dense().tolist() == [[2, 4, 3], [3, 5, 0]]
 
 
 def test_event_loop_server_threads_do_not_grow_with_connections(cluster):
@@ -556,3 +559,51 @@ def test_remote_native_pipeline_trains_like_local(tmp_path):
     assert not torch.equal(local_batches[0][1], local_batches[1][1])
     assert remote["step"] == local["step"] == 60
     assert remote["loss"] == local["loss"], (local, remote)
+
+
+def test_graph_partition_mode_routes_by_ownership():
+    """mode=graph_partition (reference query_proxy.cc:35-60): the shards hold an arbitrary
+    (here: id-range) partition instead of the id-hash one, so hash routing misses ids; the
+    graph_partition optimizer asks the shards who holds each id (API_GET_NODE_T) and sends
+    every id to its holder (GP_ID_SPLIT): the same answers as the in-process graph."""
+    import euler_amd._engine as E
+
+    data = tempfile.mkdtemp(prefix="euler_amd_gp_data_")
+    convert_json(os.path.join(HERE, "data", "graph.json"), data, 2, os.path.join(HERE, "data", "index_meta.json"),
+                 partition_fn=lambda i: 0 if i <= 3 else 1)
+    q = "v(nodes).outV(edge_types).as(n1).outV(edge_types).as(n2)"
+    q_in = {"nodes": np.array([1, 2, 5], dtype=np.int64), "edge_types": np.array([0, 1], dtype=np.int32)}
+    q_out = ["n1:0", "n1:1", "n2:0", "n2:1"]
+    ea.initialize_graph({"mode": "local", "data_path": data})
+    want = [x.tolist() for x in ea.run_gql(q, q_in, q_out)]
+    reg = tempfile.mkdtemp(prefix="euler_amd_gp_reg_")
+    procs = [_serve(data, reg, s, 2) for s in range(2)]
+    try:
+        deadline = time.time() + 60
+        while time.time() < deadline and len(E.registry_list(reg, 0.0)) < 2:
+            time.sleep(0.1)
+        assert len(E.registry_list(reg, 0.0)) == 2
+        ea.initialize_graph({"mode": "graph_partition", "registry": reg, "shard_num": 2, "num_retries": 2})
+        assert ea.get_engine().meta()["mode"] == "graph_partition"
+        ids, _, _ = ea.get_full_neighbor([1, 2], ["0", "1"])
+        assert ids.to_dense().tolist() == [[2, 4, 3], [3, 5, 0]]
+        ids, _, _ = ea.get_full_neighbor([1, 2, 3, 4], ["0", "1"], "price gt 3")
+        assert ids.to_dense().tolist() == [[4, 3], [3, 5], [4, 0], [5, 0]]
+        f3 = ea.get_dense_feature([6, 1, 6, 3, 1, 2, 5, 4], ["f3"], [2])[0]
+        assert np.allclose(f3.numpy()[:, 0], [6.1, 1.1, 6.1, 3.1, 1.1, 2.1, 5.1, 4.1])
+        nb, _, _ = ea.sample_neighbor([1, 2, 5], ["0", "1"], 6)
+        assert set(nb[0].tolist()) <= {2, 3, 4} and set(nb[2].tolist()) <= {2, 6}
+        s = ea.sample_node(2000, "-1").numpy()
+        assert set(s.tolist()) == {1, 2, 3, 4, 5, 6}
+        # a 2-hop query: every hop is routed by ownership
+        assert [x.tolist() for x in ea.run_gql(q, q_in, q_out)] == want
+        assert "GP_ID_SPLIT" in ea.explain_gql(q)
+        # the same cluster through hash routing: ids land on shards that do not hold them
+        ea.initialize_graph({"mode": "remote", "registry": reg, "shard_num": 2, "num_retries": 2})
+        f3h = ea.get_dense_feature([1, 2, 3, 4, 5, 6], ["f3"], [2])[0].numpy()[:, 0]
+        assert not np.allclose(f3h, [1.1, 2.1, 3.1, 4.1, 5.1, 6.1])
+    finally:
+        for p in procs:
+            p.terminate()
+        for p in procs:
+            p.wait(timeout=30)
