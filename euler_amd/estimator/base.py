@@ -95,6 +95,10 @@ def dist_backend():
     return dist.get_backend() if dist.is_available() and dist.is_initialized() else None
 
 
+def _first_name(x):
+    return x[0] if isinstance(x, (list, tuple)) else x
+
+
 class BaseEstimator:
     def __init__(self, model_fn, params, run_config=None, profiling=False):
         self.model = model_fn
@@ -435,7 +439,21 @@ class BaseEstimator:
                                         device=self.device, optimizer=self.params.get("optimizer", "adam"),
                                         learning_rate=float(self.params.get("learning_rate", 0.001)))
         from euler_amd.models.unsupervised import BaseNode2Vec, GraphAutoEncoder
+        from euler_amd.mp_utils.models import GraphModel
 
+        if isinstance(model, GraphModel) and hasattr(model, "pool") and hasattr(getattr(model, "gnn", None),
+                                                                                 "encoder"):
+            # graph classification (GraphEstimator): graphs' node lists, labels and sparse
+            # feature ids in HBM, the induced blocks built on the device (models/graph_trainer.py)
+            from euler_amd.models.graph_trainer import GraphTrainer
+
+            self._prepare(first)
+            if self._sync is not None:
+                self._sync.remove()
+            graph = DeviceGraph.from_engine(seed=seed * 7919 + self.rank, device=self.device)
+            return GraphTrainer(model, graph, int(self.params["batch_size"]), _first_name(self.params["label"]),
+                                int(self.params["num_classes"]), optimizer=self.params.get("optimizer", "adam"),
+                                learning_rate=float(self.params.get("learning_rate", 0.001)))
         if isinstance(model, GraphAutoEncoder):
             # GAE (sage / gcn encoder): roots, positives, negatives and the encoder's blocks
             # on the HBM graph (models/gae_trainer.py)
