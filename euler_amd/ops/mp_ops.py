@@ -372,7 +372,11 @@ def scatter_softmax(logits, indices, size=None):
     if use_hip(logits) and logits.dtype in (torch.float32, torch.bfloat16):
         return _EdgeSoftmax.apply(logits, segment_index(indices, size))
     idx = indices.indices if isinstance(indices, SegmentIndex) else indices.reshape(-1).long()
+    # padding entries (index -1) get 0, as on the GPU, and stay out of every sum (an
+    # out-of-range read here would divide by an empty segment's 0 and poison the gradients)
+    valid = (idx >= 0).view(-1, *([1] * (logits.dim() - 1)))
+    safe = idx.clamp(min=0)
     mx = _cpu_scatter(logits.detach(), idx, size, "max")
-    z = torch.exp(logits - mx[idx])
+    z = torch.exp(logits - mx[safe]) * valid.to(logits.dtype)
     den = _cpu_scatter(z, idx, size, "add")
-    return z / den[idx]
+    return z / den[safe].clamp_min(1e-30)

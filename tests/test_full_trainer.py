@@ -221,3 +221,16 @@ def test_device_flow_dst_csr_equals_sorted_csr_cpu():
             n_real = int(ref.indptr[-1])
             assert torch.equal(pre.indptr, ref.indptr)
             assert torch.equal(pre.perm[:n_real], ref.perm[:n_real])
+
+
+@pytest.mark.parametrize("model", ["agnn", "gat", "dna"])
+def test_attention_convs_on_padded_blocks_stay_finite_cpu(tmp_path, model):
+    """attention convolutions on capacity-padded device blocks: the padding edges (index -1)
+    get softmax weight 0 on the CPU path too (an out-of-range read divided by an empty
+    segment's 0 and turned AGNN's gradients into NaN)"""
+    from euler_amd.tools.runner import main
+
+    res = main(["--dataset", "ppi", "--scale", "0.05", "--batch_size", "16", "--log_steps", "3", "--device", "cpu",
+                "--seed", "1", "--model_dir", str(tmp_path / model), "--device_graph", "--learning_rate", "0.01",
+                "--total_step", "6"], model=model)
+    assert res["step"] == 6 and math.isfinite(res["loss"])
