@@ -438,7 +438,7 @@ class BaseEstimator:
             return KGTrainer.from_model(model, int(self.params["batch_size"]), edge_type, seed=seed * 7919 + self.rank,
                                         device=self.device, optimizer=self.params.get("optimizer", "adam"),
                                         learning_rate=float(self.params.get("learning_rate", 0.001)))
-        from euler_amd.models.unsupervised import BaseNode2Vec, GraphAutoEncoder
+        from euler_amd.models.unsupervised import BaseNode2Vec, GraphAutoEncoder, Line, VariationalGraphAutoEncoder
         from euler_amd.mp_utils.models import GraphModel
 
         if isinstance(model, GraphModel) and hasattr(model, "pool") and hasattr(getattr(model, "gnn", None),
@@ -454,10 +454,10 @@ class BaseEstimator:
             return GraphTrainer(model, graph, int(self.params["batch_size"]), _first_name(self.params["label"]),
                                 int(self.params["num_classes"]), optimizer=self.params.get("optimizer", "adam"),
                                 learning_rate=float(self.params.get("learning_rate", 0.001)))
-        if isinstance(model, GraphAutoEncoder):
-            # GAE (sage / gcn encoder): roots, positives, negatives and the encoder's blocks
-            # on the HBM graph (models/gae_trainer.py)
-            from euler_amd.models.gae_trainer import GaeTrainer
+        if isinstance(model, (GraphAutoEncoder, VariationalGraphAutoEncoder)):
+            # GAE / VGAE (sage / gcn encoder): roots, positives, negatives and the encoder's
+            # blocks on the HBM graph (models/gae_trainer.py)
+            from euler_amd.models.gae_trainer import GaeTrainer, VgaeTrainer
 
             self._prepare(first)
             if self._sync is not None:
@@ -469,12 +469,13 @@ class BaseEstimator:
             graph = DeviceGraph.from_engine(node_type=node_type, features=gnn.feature_idx,
                                             feature_dims=gnn.feature_dim, feature_dtype=fdt,
                                             seed=seed * 7919 + self.rank, device=self.device)
-            return GaeTrainer(model, graph, int(self.params["batch_size"]),
+            cls = VgaeTrainer if isinstance(model, VariationalGraphAutoEncoder) else GaeTrainer
+            return cls(model, graph, int(self.params["batch_size"]),
                               optimizer=self.params.get("optimizer", "adam"),
                               learning_rate=float(self.params.get("learning_rate", 0.001)))
-        if isinstance(model, BaseNode2Vec):
-            # DeepWalk / Node2Vec: walks, pairs, negatives and the row-sparse SGNS update on the
-            # HBM graph (models/deepwalk_step.py)
+        if isinstance(model, (BaseNode2Vec, Line)):
+            # DeepWalk / Node2Vec / LINE (second order): walks, pairs, negatives and the
+            # row-sparse SGNS update on the HBM graph (models/deepwalk_step.py)
             from euler_amd.models.deepwalk_step import DeepWalkEstimatorTrainer
 
             if self.world > 1:
@@ -488,6 +489,26 @@ class BaseEstimator:
                                             optimizer=self.params.get("optimizer", "adam"),
                                             learning_rate=float(self.params.get("learning_rate", 0.001)),
                                             seed=seed)
+        from euler_amd.models.unsupervised import DGI
+
+        if isinstance(model, DGI):
+            # Deep Graph Infomax: roots, the fan-out tree and its shuffled view on the HBM
+            # graph, the user's aggregators and discriminator (models/dgi_trainer.py)
+            from euler_amd.models.dgi_trainer import DgiTrainer
+
+            self._prepare(first)
+            if self._sync is not None:
+                self._sync.remove()
+            ne = model._target_encoder._node_encoder
+            nt = self.params.get("train_node_type", model.node_type)
+            node_type = -1 if nt in (None, -1, "-1") else int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
+            fdt = torch.float32 if self.params.get("device_feature_dtype", "bf16") == "fp32" else torch.bfloat16
+            graph = DeviceGraph.from_engine(node_type=node_type, features=ne.feature_idx if ne.use_feature else (),
+                                            feature_dims=ne.feature_dim if ne.use_feature else (),
+                                            feature_dtype=fdt, seed=seed * 7919 + self.rank, device=self.device)
+            return DgiTrainer(model, graph, int(self.params["batch_size"]),
+                              optimizer=self.params.get("optimizer", "adam"),
+                              learning_rate=float(self.params.get("learning_rate", 0.001)))
         gnn = getattr(model, "gnn", None)
         unsup = hasattr(model, "context_gnn")
         if gnn is None or not hasattr(gnn, "feature_idx") or not (unsup or hasattr(model, "label_idx")):

@@ -320,8 +320,9 @@ class DeepWalkTrainer:
 
 
 class DeepWalkEstimatorTrainer:
-    """``NodeEstimator(device_graph=True)`` for DeepWalk / Node2Vec models with id
-    embeddings (reference examples/deepwalk/deepwalk.py:27-99 through
+    """``NodeEstimator(device_graph=True)`` for DeepWalk / Node2Vec and second-order LINE
+    models with id embeddings (reference examples/deepwalk/deepwalk.py:27-99,
+    examples/line/line.py:27-71 through
     euler_estimator/python/node_estimator.py): the walks, pairs, negatives and the
     row-sparse SGNS update of :class:`DeepWalkTrainer` on the HBM graph, several static
     steps per hipGraph replay.  The model's two embedding tables are the trainer's table
@@ -343,18 +344,24 @@ class DeepWalkEstimatorTrainer:
                     getattr(e, "use_sparse_feature", True) or e.combiner != "add":
                 raise ValueError("the DeepWalk device path trains pure id embeddings (no features, combiner 'add')")
         if enc_t is enc_c:
-            raise ValueError("the DeepWalk device path needs separate target and context tables")
+            raise ValueError("the DeepWalk device path needs separate target and context tables "
+                             "(LINE: order='second')")
         self.model = model
         self.graph = graph
         self.device = graph.device
         self.on_gpu = self.device.type == "cuda"
         et = model.edge_type
         ets = None if et in (None, -1, "-1") else [int(t) for t in np.asarray(ge.get_edge_type_id(et)).reshape(-1)]
-        self.inner = DeepWalkTrainer(graph, graph.num_rows, dim=model.dim, walk_len=model.walk_len,
-                                     left_win_size=model.left_win_size, right_win_size=model.right_win_size,
+        # LINE (second order, examples/line/line.py:27-71): the positive of a root is one
+        # weighted neighbour sample (UnsuperviseModel.to_sample) = the second node of a
+        # one-step walk, paired (root, neighbour) only: walk_len 1, window (0, 1)
+        walk_len = getattr(model, "walk_len", 1)
+        win = (getattr(model, "left_win_size", 0), getattr(model, "right_win_size", 1))
+        self.inner = DeepWalkTrainer(graph, graph.num_rows, dim=model.dim, walk_len=walk_len,
+                                     left_win_size=win[0], right_win_size=win[1],
                                      num_negs=model.num_negs, batch_size=batch_size, lr=learning_rate,
                                      optimizer=optimizer, seed=seed, static=self.on_gpu, edge_types=ets,
-                                     p=model.walk_p, q=model.walk_q)
+                                     p=getattr(model, "walk_p", 1), q=getattr(model, "walk_q", 1))
         self._keys = ("_target_encoder.embedding.weight", "_context_encoder.embedding.weight")
         ids = graph.ids if graph.ids is not None else np.arange(graph.num_rows)
         self._ids = torch.as_tensor(np.asarray(ids).astype(np.int64), device=self.device)

@@ -24,7 +24,7 @@ from euler_amd.dataflow.device_flow import DeviceFullFlow, DeviceSageFlow
 from euler_amd.models.captured import CapturedTrainer
 from euler_amd.ops import mp_ops
 
-__all__ = ["GaeTrainer"]
+__all__ = ["GaeTrainer", "VgaeTrainer"]
 
 
 def _type_ids(edge_type):
@@ -101,3 +101,49 @@ class GaeTrainer(CapturedTrainer):
 
     def reset_metric(self):
         self.acc.zero_()
+
+
+class VgaeTrainer(GaeTrainer):
+    """``VariationalGraphAutoEncoder`` on the device path (reference examples/gae/gae.py:94-153,
+    this repo's ``models/unsupervised.py`` VariationalGraphAutoEncoder): the encoder gives
+    mu, the model's id table ``log_var_encoder`` gives log sigma^2 of every node (graph row ->
+    node id through ``graph.ids``; a ``-1`` sample is the model's out-of-range row, as on the
+    engine path), the decoder reads ``mu + radius * eps * exp(log_var / 2)``, and the loss
+    adds the mean KL over every root, positive and negative.  ``eps`` comes from torch's
+    CUDA generator, which hipGraph replays advance like eager steps (the sampler's draws
+    stay on the graph's Philox counter)."""
+
+    def __init__(self, model, graph, batch_size, optimizer="adam", learning_rate=0.01):
+        ids = graph.ids if graph.ids is not None else np.arange(graph.num_rows)
+        self._ids = torch.as_tensor(np.asarray(ids).astype(np.int64), device=graph.device)
+        self._pad_id = int(model.max_id) + 1
+        self.radius = float(model.radius)
+        super().__init__(model, graph, batch_size, optimizer, learning_rate)
+
+    def _forward_loss(self):
+        self._draw()
+        g = self.graph
+        B, K = self.B, self.K
+        src = g.sample_node(B, stream_id=1).long()
+        pos = g.sample_neighbor(src, K, edge_types=self.pos_types, default=-1, stream_id=4).long().reshape(-1)
+        neg = g.sample_node(B * K, stream_id=5).long()
+        rows = torch.cat([src, pos, neg])
+        mu = self._embed(rows)
+        node_ids = torch.where(rows >= 0, self._ids[rows.clamp(min=0)], torch.full_like(rows, self._pad_id))
+        log_var = self.model.log_var_encoder(node_ids).reshape(mu.shape).to(mu.dtype)
+        emb = mu + self.radius * torch.randn_like(log_var) * torch.exp(0.5 * log_var)
+        d = emb.shape[-1]
+        e_src = emb[:B].view(B, 1, d)
+        e_pos = emb[B:B + B * K].view(B, K, d)
+        e_neg = emb[B + B * K:].view(B, K, d)
+        logits = torch.matmul(e_src, e_pos.transpose(1, 2)).float()
+        neg_logits = torch.matmul(e_src, e_neg.transpose(1, 2)).float()
+        t = F.binary_cross_entropy_with_logits(logits, torch.ones_like(logits), reduction="none")
+        n = F.binary_cross_entropy_with_logits(neg_logits, torch.zeros_like(neg_logits), reduction="none")
+        loss = torch.cat([t.reshape(-1), n.reshape(-1)]).mean()
+        loss = loss + self.model.kl(mu, log_var).float().mean()
+        with torch.no_grad():
+            right = (logits >= 0).sum() + (neg_logits < 0).sum()
+            self.acc += torch.stack([right.double(), torch.full_like(right.double(), float(2 * B * K))])
+        self._samples = (src, pos, neg)
+        return loss

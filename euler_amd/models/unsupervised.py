@@ -142,6 +142,7 @@ class Line(UnsuperviseModel):
                                            sparse_feature_max_id=sparse_feature_max_id, embedding_dim=embedding_dim,
                                            use_hash_embedding=use_hash_embedding, combiner=combiner)
 
+        self.dim = dim
         self._target_encoder = mk()
         self._context_encoder = self._target_encoder if order == "first" else mk()
 

@@ -85,3 +85,42 @@ def test_deepwalk_device_path_gpu_captured(cora, tmp_path, cuda):
     res = est.train()
     tr = est.device_trainer
     assert res["step"] == 120 and np.isfinite(res["loss"]) and tr.captures >= 1
+
+
+def _line(ds, order=2):
+    torch.manual_seed(0)
+    return Z.Line("train", ["train"], ds.max_node_id, 8, num_negs=3, order=order)
+
+
+def test_line_device_path_cpu(cora, tmp_path):
+    """second-order LINE (examples/line/line.py:27-71) on the device path: one (root,
+    weighted neighbour) pair per root, negatives from the node sampler"""
+    m = _line(cora)
+    before = m.state_dict()["_context_encoder.embedding.weight"].clone()
+    est = NodeEstimator(m, _params(cora, tmp_path, "cpu"))
+    res = est.train()
+    assert res["step"] == 30 and np.isfinite(res["loss"])
+    assert not torch.equal(before, m.state_dict()["_context_encoder.embedding.weight"])
+    inner = est.device_trainer.inner
+    assert inner.pairs_per_walk == 1 and inner.walk_len == 1
+    src, pos, negs = inner.sample()
+    g = est.device_trainer.graph
+    assert src.numel() == 32 and negs.shape == (32, 3)
+    # every positive is an out-neighbour of its root (or the pad row of a sink)
+    indptr, nbr, T = g.indptr.cpu(), g.nbr.cpu(), g.num_types
+    for s, p in zip(src.tolist(), pos.tolist()):
+        assert p == inner.pad or p in nbr[indptr[s * T]: indptr[(s + 1) * T]].tolist()
+
+
+def test_line_first_order_is_refused_on_device(cora, tmp_path):
+    m = _line(cora, order=1)
+    with pytest.raises(ValueError, match="separate target and context"):
+        NodeEstimator(m, _params(cora, tmp_path, "cpu")).train()
+
+
+@pytest.mark.gpu
+def test_line_device_path_gpu_captured(cora, tmp_path, cuda):
+    m = _line(cora)
+    est = NodeEstimator(m, _params(cora, tmp_path, "cuda", total_step=120, log_steps=40, steps_per_graph=8))
+    res = est.train()
+    assert res["step"] == 120 and np.isfinite(res["loss"]) and est.device_trainer.captures >= 1

@@ -116,3 +116,50 @@ def test_device_sage_flow_fused_block_matches_torch(cora, cuda, monkeypatch, sel
         assert torch.equal(seg.indptr, ref.indptr) and torch.equal(seg.counts, ref.counts)
         n = int(ref.indptr[-1])
         assert torch.equal(seg.perm[:n], ref.perm[:n])
+
+
+def _vgae(enc, ds, radius=0.5):
+    torch.manual_seed(0)
+    return Z.VariationalGraphAutoEncoder(radius, enc, [16, 8], [3], [["train"]], "feature", F, "train", ["train"],
+                                         ds.max_node_id, num_negs=3)
+
+
+@pytest.mark.parametrize("enc", ["sage", "gcn"])
+def test_vgae_device_path_cpu(cora, tmp_path, enc):
+    m = _vgae(enc, cora)
+    before = m.state_dict()["log_var_encoder.embedding.weight"].clone()
+    est = GaeEstimator(m, _params(cora, tmp_path, "cpu"))
+    res = est.train()
+    assert res["step"] == 24 and np.isfinite(res["loss"]) and 0.0 < res["acc"] <= 1.0
+    assert not torch.equal(before, m.state_dict()["log_var_encoder.embedding.weight"])
+
+
+def test_vgae_loss_is_gae_loss_plus_kl_cpu(cora, tmp_path):
+    """radius 0: the VGAE step's loss = the GAE decoder loss on the same draws + the mean KL
+    of (mu, log_var) over every root / positive / negative (gae.py:94-153)"""
+    from euler_amd.graph.device_graph import DeviceGraph
+    from euler_amd.models.gae_trainer import GaeTrainer, VgaeTrainer
+
+    m = _vgae("sage", cora, radius=0.0)
+    est = GaeEstimator(m, _params(cora, tmp_path, "cpu"))
+    est._prepare(est.get_train_from_input(8, est.params))  # materialise the lazy layers
+    mk = lambda: DeviceGraph.from_engine(features=m.gnn.feature_idx, feature_dims=m.gnn.feature_dim,  # noqa
+                                         feature_dtype=torch.float32, seed=9, device="cpu")
+    vt, gt = VgaeTrainer(m, mk(), 8), GaeTrainer(m, mk(), 8)
+    lv_loss, g_loss = vt._forward_loss(), gt._forward_loss()
+    src, pos, neg = vt._samples
+    assert all(torch.equal(a, b) for a, b in zip(vt._samples, gt._samples))
+    rows = torch.cat([src, pos, neg])
+    with torch.no_grad():
+        mu = vt._embed(rows)
+        ids = torch.where(rows >= 0, vt._ids[rows.clamp(min=0)], torch.full_like(rows, vt._pad_id))
+        kl = m.kl(mu, m.log_var_encoder(ids).reshape(mu.shape)).mean()
+    assert torch.allclose(lv_loss.detach(), g_loss.detach() + kl, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_vgae_device_path_gpu_captured(cora, tmp_path, cuda):
+    m = _vgae("sage", cora)
+    est = GaeEstimator(m, _params(cora, tmp_path, "cuda", total_step=64, log_steps=32, steps_per_graph=8))
+    res = est.train()
+    assert res["step"] == 64 and np.isfinite(res["loss"]) and est.device_trainer.captures >= 1
