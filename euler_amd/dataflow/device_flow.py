@@ -35,7 +35,7 @@ from euler_amd.dataflow.dataflows import Block, DataFlow
 from euler_amd.ops._native import hip, use_hip
 from euler_amd.ops.mp_ops import SegmentIndex
 
-__all__ = ["DeviceFullFlow", "DeviceSageFlow", "full_neighbors_cpu", "max_out_degree"]
+__all__ = ["DeviceFullFlow", "DeviceLayerFlow", "DeviceSageFlow", "full_neighbors_cpu", "max_out_degree"]
 
 
 def _round_up(x: int, m: int = 256) -> int:
@@ -184,9 +184,12 @@ class DeviceFullFlow:
                                                       n_id, cap_e, self.overflow)
             else:
                 nbr, src, offs = full_neighbors_cpu(g, mask, n_id, cap_e, self.overflow)
+            kept = self._filter(h, n_id, nbr)
+            if kept is not None:
+                nbr = kept
             cat = torch.cat([nbr, n_id])
             uniq, inv, cnt = _unique_padded(cat)
-            if use_hip(n_id) and _FUSED_BLOCK:
+            if use_hip(n_id) and _FUSED_BLOCK and kept is None:
                 # the block assembly below as one launch (flow.hip flow_block_kernel)
                 new_n_id, res_n_id, edge_index, perm, indptr, counts, last_idx, prev_cnt = hip().flow_block(
                     src, offs, uniq, inv, cnt.reshape(1), last_idx, prev_cnt.reshape(1), cap_n, self.self_loops,
@@ -213,11 +216,13 @@ class DeviceFullFlow:
             # an edge whose source was dropped by an overflow must not keep its target
             edge_t = torch.where(edge_s >= 0, edge_t, torch.full_like(edge_t, -1))
             edge_index = torch.stack([edge_t, edge_s])
-            # the destination CSR is known from the expansion: the convolutions' scatters and
-            # SpMM reuse it instead of sorting (mp_ops.cached_segment)
-            perm, indptr = _dst_csr(src, offs.clamp(max=cap_e), prev_cnt, cap_e, cap_prev, self.self_loops)
-            edge_index._euler_cache = {"_euler_seg0_%d" % cap_prev: SegmentIndex.from_csr(edge_t, cap_prev, perm,
-                                                                                             indptr)}
+            if kept is None:
+                # the destination CSR is known from the expansion: the convolutions' scatters
+                # and SpMM reuse it instead of sorting (mp_ops.cached_segment); a filtered hop
+                # has holes in its segments, so its index is built from edge_t as usual
+                perm, indptr = _dst_csr(src, offs.clamp(max=cap_e), prev_cnt, cap_e, cap_prev, self.self_loops)
+                edge_index._euler_cache = {"_euler_seg0_%d" % cap_prev: SegmentIndex.from_csr(edge_t, cap_prev,
+                                                                                                 perm, indptr)}
             df.blocks.append(Block(new_n_id, res_n_id, None, edge_index, [cap_prev, cap_n]))
             df._last = new_n_id
             ar = torch.arange(cap_n, dtype=torch.long, device=dev)
@@ -231,6 +236,91 @@ class DeviceFullFlow:
         """raise if any batch so far exceeded a capacity (host sync)"""
         if int(self.overflow.item()) != 0:
             raise RuntimeError(f"device dataflow capacity exceeded (caps {self.caps}): raise the caps")
+
+    def _filter(self, h, n_id, nbr):
+        """hook: the hop's neighbour list with dropped entries set to -1 (None: keep all)"""
+        return None
+
+
+class DeviceLayerFlow(DeviceFullFlow):
+    """``FastGCNDataFlow`` / ``LayerwiseDataFlow`` (reference ``fast_dataflow.py:25-57``,
+    ``layerwise_dataflow.py:26-71``; engine twins in ``dataflows.py``) on the device with
+    fixed shapes.  Every hop but the last keeps, of the current set's out-edges, those that
+    land in a per-hop sampled layer; the last hop is the full neighbourhood:
+
+    * ``"fast"``: the layer is ``sample_node(total_fanout, metapath[h][0])`` (the
+      reference's node-type argument; ``samplers[h]``, a root sampler over that type), the
+      kept edges are ``sparse_get_adj(set, unique(layer))``;
+    * ``"layer"``: ``sampleLNB`` — ``total_fanout`` roots drawn from the current set in
+      proportion to their out-edge weight, one weighted neighbour of each (Philox stream
+      30 + h), the kept edges are the set's edges into that layer.
+
+    A layer is a membership flag over the graph's rows, so an edge is kept once even when
+    its destination was drawn several times (the engine path's adjacency repeats it per
+    draw); node sets and the kept edges' (target, source) pairs otherwise equal the
+    engine's blocks, in target-major storage order.  Capacities are the full flow's
+    (exact upper bounds)."""
+
+    def __init__(self, graph, masks, kinds, fanouts, batch_size: int, add_self_loops: bool = True, samplers=None):
+        super().__init__(graph, masks, batch_size, add_self_loops)
+        self.kinds = list(kinds)
+        totals, t = [], 0
+        for f in fanouts:
+            t += int(f)
+            totals.append(t)
+        self.totals = totals
+        self.samplers = list(samplers) if samplers is not None else [None] * len(self.kinds)
+        if len(self.kinds) != self.L or any(k not in ("fast", "layer") for k in self.kinds[:-1]) or \
+                len(self.totals) < self.L - 1:
+            raise ValueError("kinds: 'fast' | 'layer' for every hop but the last")
+        self._flag = torch.zeros(graph.num_rows + 1, dtype=torch.bool, device=graph.device)
+        self._uflat_p = torch.ones(1 << 16, dtype=torch.float32, device=graph.device)
+        self._uflat_a = torch.arange(1 << 16, dtype=torch.int32, device=graph.device)
+
+    def _out_weight(self, rows, mask):
+        g = self.g
+        T = g.num_types
+        r = rows.clamp(min=0)
+        tot = torch.zeros(rows.numel(), dtype=torch.float32, device=rows.device)
+        for t in range(T):
+            if not (mask >> t) & 1:
+                continue
+            a, b = g.indptr[r * T + t], g.indptr[r * T + t + 1]
+            tot = tot + torch.where(b > a, g.cumw[(b - 1).clamp(min=0)], torch.zeros_like(tot))
+        return torch.where(rows >= 0, tot, torch.zeros_like(tot))
+
+    def _layer(self, h, n_id):
+        g, m = self.g, self.totals[h]
+        if self.kinds[h] == "fast":
+            return self.samplers[h].sample_node(m, stream_id=20 + h).long()
+        w = self._out_weight(n_id, self.masks[h])
+        cum = torch.cumsum(w, 0)
+        total = cum[-1]
+        u = self._uniform(m, 40 + h) * total
+        pick = torch.searchsorted(cum, u.contiguous(), right=True).clamp(max=n_id.numel() - 1)
+        roots = torch.where(total > 0, n_id[pick], torch.full_like(pick, -1))
+        types = [t for t in range(g.num_types) if (self.masks[h] >> t) & 1]
+        return g.sample_neighbor(roots, 1, edge_types=types, default=-1, stream_id=30 + h).long().reshape(-1)
+
+    def _uniform(self, n, stream_id):
+        """n uniforms in [0, 1) keyed by the graph's (seed, counter) and ``stream_id``: two
+        16-bit integer draws of the alias sampler over a flat table (Philox, capturable)"""
+        g = self.g
+        if use_hip(g.rng):
+            hi = hip().alias_sample(self._uflat_p, self._uflat_a, None, int(n), g.rng, int(stream_id))
+            lo = hip().alias_sample(self._uflat_p, self._uflat_a, None, int(n), g.rng, int(stream_id) + 100)
+            return (hi.double() * 65536.0 + lo.double() + 0.5).float() / float(1 << 32)
+        return torch.rand(int(n), generator=g._cpu_gen)
+
+    def _filter(self, h, n_id, nbr):
+        if h == self.L - 1:
+            return None
+        layer = self._layer(h, n_id)
+        slot = torch.where(layer >= 0, layer, torch.full_like(layer, self.g.num_rows))
+        self._flag.index_fill_(0, slot, True)  # slot num_rows (no draw) is never read below
+        keep = self._flag[nbr.clamp(min=0)] & (nbr >= 0)
+        self._flag.index_fill_(0, slot, False)
+        return torch.where(keep, nbr, torch.full_like(nbr, -1))
 
 
 class DeviceSageFlow:
@@ -278,9 +368,12 @@ class DeviceSageFlow:
         for h, (et, f) in enumerate(zip(self.edge_types, self.fanouts)):
             cap_e, cap_n = self.caps[h]
             nbr = g.sample_neighbor(n_id, f, edge_types=et, default=-1, stream_id=10 + h).long().reshape(-1)
+            kept = self._filter(h, n_id, nbr)
+            if kept is not None:
+                nbr = kept
             cat = torch.cat([nbr, n_id])
             uniq, inv, cnt = _unique_padded(cat)
-            if use_hip(n_id) and _FUSED_BLOCK:
+            if use_hip(n_id) and _FUSED_BLOCK and kept is None:
                 # the block assembly below + the destination CSR as three launches (flow.hip
                 # sage_block / sage_place): the convolutions' scatters and SpMM need no sort
                 new_n_id, res_n_id, edge_index, perm, indptr, counts, last_idx, _ = hip().sage_block(

@@ -523,7 +523,10 @@ class BaseEstimator:
 
         sampled_other = isinstance(getattr(gnn, "sampler", None), SageDataFlow) and not unsup and \
             not all(isinstance(c, SAGEConv) for c in gnn.convs)
-        if isinstance(getattr(gnn, "sampler", None), GCNDataFlow) or sampled_other:
+        from euler_amd.dataflow.dataflows import FastGCNDataFlow, LayerwiseDataFlow
+
+        layer_sampled = isinstance(getattr(gnn, "sampler", None), (FastGCNDataFlow, LayerwiseDataFlow))
+        if isinstance(getattr(gnn, "sampler", None), GCNDataFlow) or sampled_other or layer_sampled:
             # GCN / APPNP / SGCN / TAGCN / ... : full-neighbourhood blocks built on the device;
             # other convolutions on the sampled flow: fixed-fanout blocks built on the device
             from euler_amd.models.full_trainer import FullFlowTrainer

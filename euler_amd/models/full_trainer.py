@@ -70,10 +70,13 @@ class FullFlowTrainer(CapturedTrainer):
         from euler_amd.dataflow.dataflows import SageDataFlow
         from euler_amd.dataflow.device_flow import DeviceSageFlow
 
+        from euler_amd.dataflow.dataflows import FastGCNDataFlow, LayerwiseDataFlow
+        from euler_amd.dataflow.device_flow import DeviceLayerFlow
+
         flow = getattr(model.gnn, "sampler", None)
-        if not isinstance(flow, (GCNDataFlow, SageDataFlow)):
-            raise ValueError("FullFlowTrainer trains models on the full-neighbourhood flow (GCNDataFlow) or the "
-                             "sampled SageDataFlow")
+        if not isinstance(flow, (GCNDataFlow, SageDataFlow, FastGCNDataFlow, LayerwiseDataFlow)):
+            raise ValueError("FullFlowTrainer trains models on the full-neighbourhood flow (GCNDataFlow), the "
+                             "sampled SageDataFlow or the layer-sampled FastGCN / AdaptiveGCN flows")
         ets = []
         for m in flow.metapath:
             ids = None if m is None else [int(t) for t in np.asarray(ge.get_edge_type_id(m)).reshape(-1)]
@@ -81,6 +84,22 @@ class FullFlowTrainer(CapturedTrainer):
         dflow = None
         if isinstance(flow, SageDataFlow):
             dflow = DeviceSageFlow(graph, ets, flow.fanouts, batch_size, bool(flow.add_self_loops))
+        elif isinstance(flow, (FastGCNDataFlow, LayerwiseDataFlow)):
+            fast = isinstance(flow, FastGCNDataFlow)
+            samplers = [None] * len(ets)
+            if fast:
+                # FastGCN's layer: sample_node(total, metapath[h][0]) (fast_dataflow.py:44-46)
+                import copy
+
+                _, _, nw = ge.get_engine().export_nodes()
+                for h, m in enumerate(flow.metapath[:-1]):
+                    nt = m[0] if isinstance(m, (list, tuple)) else m
+                    tid = int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
+                    samplers[h] = copy.copy(graph)
+                    samplers[h].set_root_type(tid if tid >= 0 else -1, node_weights=np.asarray(nw))
+            kinds = ["fast" if fast else "layer"] * (len(ets) - 1) + ["full"]
+            dflow = DeviceLayerFlow(graph, [graph._mask(e) for e in ets], kinds, list(flow.fanouts)[:len(ets)],
+                                    batch_size, bool(flow.add_self_loops), samplers=samplers)
         return cls(model, graph, batch_size, [graph._mask(e) for e in ets], add_self_loops=bool(flow.add_self_loops),
                    optimizer=optimizer, learning_rate=learning_rate, flow=dflow, **kw)
 

@@ -192,7 +192,8 @@ def test_device_graph_replay_matches_eager():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("model", ["gcn", "appnp", "sgcn", "tagcn", "agnn", "gat", "arma", "dna"])
+@pytest.mark.parametrize("model", ["gcn", "appnp", "sgcn", "tagcn", "agnn", "gat", "arma", "dna", "fastgcn",
+                                   "adaptivegcn"])
 def test_estimator_device_graph_gcn_family_gpu(tmp_path, monkeypatch, model):
     monkeypatch.chdir(tmp_path)
     from euler_amd.tools.runner import main
@@ -228,6 +229,56 @@ def test_attention_convs_on_padded_blocks_stay_finite_cpu(tmp_path, model):
     """attention convolutions on capacity-padded device blocks: the padding edges (index -1)
     get softmax weight 0 on the CPU path too (an out-of-range read divided by an empty
     segment's 0 and turned AGNN's gradients into NaN)"""
+    from euler_amd.tools.runner import main
+
+    res = main(["--dataset", "ppi", "--scale", "0.05", "--batch_size", "16", "--log_steps", "3", "--device", "cpu",
+                "--seed", "1", "--model_dir", str(tmp_path / model), "--device_graph", "--learning_rate", "0.01",
+                "--total_step", "6"], model=model)
+    assert res["step"] == 6 and math.isfinite(res["loss"])
+
+
+@pytest.mark.parametrize("kind", ["fast", "layer"])
+def test_device_layer_flow_keeps_exactly_the_edges_into_the_layer_cpu(kind):
+    """FastGCN / AdaptiveGCN hops on the device (DeviceLayerFlow): the first hop keeps every
+    out-edge of the roots that lands in the sampled layer and nothing else (the engine's
+    sparse_get_adj(set, layer)); the last hop is the full neighbourhood"""
+    from euler_amd.dataflow.device_flow import DeviceFullFlow, DeviceLayerFlow
+
+    _, m, _ = _setup("cpu")
+    g = _device_graph(m, "cpu")
+    masks = _masks(g, m.gnn.sampler)
+    dflow = DeviceLayerFlow(g, masks, [kind, "full"], [6, 6], 16, True, samplers=[g, None])
+    layers = []
+    orig = dflow._layer
+    dflow._layer = lambda h, n_id: layers.append(orig(h, n_id)) or layers[-1]
+    roots = torch.randint(0, g.num_rows, (16,), generator=torch.Generator().manual_seed(4))
+    g.reseed_cpu()
+    df = dflow.produce(roots)
+    assert len(layers) == 1 and layers[0].numel() == 6
+    lay = set(int(v) for v in layers[0].tolist() if v >= 0)
+    T = g.num_types
+    want = set()
+    for u in roots.tolist():
+        for t in range(T):
+            if (masks[0] >> t) & 1:
+                for v in g.nbr[g.indptr[u * T + t]: g.indptr[u * T + t + 1]].tolist():
+                    if v in lay:
+                        want.add((u, v))
+    b = df.blocks[0]
+    ei, nid = b.edge_index, b.n_id
+    n_e = ei.shape[1] - 16  # the last 16 edges are the self loops
+    got = set((int(roots[t]), int(nid[s])) for t, s in zip(ei[0, :n_e].tolist(), ei[1, :n_e].tolist()) if t >= 0)
+    assert got == want
+    assert torch.equal(nid[b.res_n_id[:16]], roots)
+    # the last hop: the full flow's expansion of the same set
+    full = DeviceFullFlow(g, masks[1:], int(nid.numel()), True)
+    ref = full.produce(nid).blocks[0]
+    e1 = df.blocks[1].edge_index
+    assert int((e1[0] >= 0).sum()) == int((ref.edge_index[0] >= 0).sum())
+
+
+@pytest.mark.parametrize("model", ["fastgcn", "adaptivegcn"])
+def test_layer_sampled_gcn_device_path_cpu(tmp_path, model):
     from euler_amd.tools.runner import main
 
     res = main(["--dataset", "ppi", "--scale", "0.05", "--batch_size", "16", "--log_steps", "3", "--device", "cpu",
