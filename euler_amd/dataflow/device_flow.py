@@ -368,12 +368,9 @@ class DeviceSageFlow:
         for h, (et, f) in enumerate(zip(self.edge_types, self.fanouts)):
             cap_e, cap_n = self.caps[h]
             nbr = g.sample_neighbor(n_id, f, edge_types=et, default=-1, stream_id=10 + h).long().reshape(-1)
-            kept = self._filter(h, n_id, nbr)
-            if kept is not None:
-                nbr = kept
             cat = torch.cat([nbr, n_id])
             uniq, inv, cnt = _unique_padded(cat)
-            if use_hip(n_id) and _FUSED_BLOCK and kept is None:
+            if use_hip(n_id) and _FUSED_BLOCK:
                 # the block assembly below + the destination CSR as three launches (flow.hip
                 # sage_block / sage_place): the convolutions' scatters and SpMM need no sort
                 new_n_id, res_n_id, edge_index, perm, indptr, counts, last_idx, _ = hip().sage_block(
