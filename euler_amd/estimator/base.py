@@ -473,6 +473,20 @@ class BaseEstimator:
             return cls(model, graph, int(self.params["batch_size"]),
                               optimizer=self.params.get("optimizer", "adam"),
                               learning_rate=float(self.params.get("learning_rate", 0.001)))
+        if isinstance(model, Line) and model._target_encoder is model._context_encoder:
+            # first-order LINE: one id table in both roles, autograd over the model's own
+            # lookups (models/line_trainer.py)
+            from euler_amd.models.line_trainer import IdPairTrainer
+
+            self._prepare(first)
+            if self._sync is not None:
+                self._sync.remove()
+            nt = self.params.get("train_node_type", model.node_type)
+            node_type = -1 if nt in (None, -1, "-1") else int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
+            graph = DeviceGraph.from_engine(node_type=node_type, seed=seed * 7919 + self.rank, device=self.device)
+            return IdPairTrainer(model, graph, int(self.params["batch_size"]),
+                                 optimizer=self.params.get("optimizer", "adam"),
+                                 learning_rate=float(self.params.get("learning_rate", 0.001)))
         if isinstance(model, (BaseNode2Vec, Line)):
             # DeepWalk / Node2Vec / LINE (second order): walks, pairs, negatives and the
             # row-sparse SGNS update on the HBM graph (models/deepwalk_step.py)

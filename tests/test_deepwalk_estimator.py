@@ -112,15 +112,34 @@ def test_line_device_path_cpu(cora, tmp_path):
         assert p == inner.pad or p in nbr[indptr[s * T]: indptr[(s + 1) * T]].tolist()
 
 
-def test_line_first_order_is_refused_on_device(cora, tmp_path):
+def test_line_first_order_device_path_cpu(cora, tmp_path):
+    """first-order LINE (one table in both roles) on the autograd device trainer; the
+    row-sparse SGNS trainer refuses a shared table"""
+    from euler_amd.graph.device_graph import DeviceGraph
+    from euler_amd.models.deepwalk_step import DeepWalkEstimatorTrainer
+
     m = _line(cora, order=1)
+    before = m.state_dict()["_target_encoder.embedding.weight"].clone()
+    est = NodeEstimator(m, _params(cora, tmp_path, "cpu"))
+    res = est.train()
+    assert res["step"] == 30 and np.isfinite(res["loss"]) and 0.0 < res["mrr"] <= 1.0
+    assert type(est.device_trainer).__name__ == "IdPairTrainer"
+    assert not torch.equal(before, m.state_dict()["_target_encoder.embedding.weight"])
     with pytest.raises(ValueError, match="separate target and context"):
-        NodeEstimator(m, _params(cora, tmp_path, "cpu")).train()
+        DeepWalkEstimatorTrainer(m, DeviceGraph.from_engine(device="cpu"), 8)
 
 
 @pytest.mark.gpu
 def test_line_device_path_gpu_captured(cora, tmp_path, cuda):
     m = _line(cora)
+    est = NodeEstimator(m, _params(cora, tmp_path, "cuda", total_step=120, log_steps=40, steps_per_graph=8))
+    res = est.train()
+    assert res["step"] == 120 and np.isfinite(res["loss"]) and est.device_trainer.captures >= 1
+
+
+@pytest.mark.gpu
+def test_line_first_order_device_path_gpu_captured(cora, tmp_path, cuda):
+    m = _line(cora, order=1)
     est = NodeEstimator(m, _params(cora, tmp_path, "cuda", total_step=120, log_steps=40, steps_per_graph=8))
     res = est.train()
     assert res["step"] == 120 and np.isfinite(res["loss"]) and est.device_trainer.captures >= 1
