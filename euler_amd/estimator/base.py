@@ -523,6 +523,27 @@ class BaseEstimator:
             return DgiTrainer(model, graph, int(self.params["batch_size"]),
                               optimizer=self.params.get("optimizer", "adam"),
                               learning_rate=float(self.params.get("learning_rate", 0.001)))
+        from euler_amd.utils.encoders import GCNEncoder
+
+        if isinstance(getattr(model, "_encoder", None), GCNEncoder) and hasattr(model, "label_idx"):
+            # GeniePath and other full-neighbour encoder models: hop sets and adjacencies
+            # built on the device, the model's own encode (models/encoder_trainer.py)
+            from euler_amd.models.encoder_trainer import EncoderFlowTrainer
+
+            self._prepare(first)
+            if self._sync is not None:
+                self._sync.remove()
+            ne = model._encoder._node_encoder
+            nt = self.params.get("train_node_type", -1)
+            node_type = -1 if nt in (None, -1, "-1") else int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
+            fdt = torch.float32 if self.params.get("device_feature_dtype", "bf16") == "fp32" else torch.bfloat16
+            graph = DeviceGraph.from_engine(node_type=node_type, features=ne.feature_idx if ne.use_feature else (),
+                                            feature_dims=ne.feature_dim if ne.use_feature else (),
+                                            label=model.label_idx, label_dim=model.label_dim, feature_dtype=fdt,
+                                            seed=seed * 7919 + self.rank, device=self.device)
+            return EncoderFlowTrainer.from_model(model, graph, int(self.params["batch_size"]),
+                                                 optimizer=self.params.get("optimizer", "adam"),
+                                                 learning_rate=float(self.params.get("learning_rate", 0.001)))
         gnn = getattr(model, "gnn", None)
         unsup = hasattr(model, "context_gnn")
         if gnn is None or not hasattr(gnn, "feature_idx") or not (unsup or hasattr(model, "label_idx")):

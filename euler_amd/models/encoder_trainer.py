@@ -1,0 +1,72 @@
+"""Device-path training of the full-neighbour *encoder* models — GeniePath
+(``GenieEncoder``) and any ``SuperviseModel`` whose ``_encoder`` is a ``GCNEncoder`` —
+under ``NodeEstimator(device_graph=True)``.
+
+Reference: ``examples/geniepath/geniepath.py:26-49``, ``tf_euler/python/utils/
+encoders.py:174-291`` (``get_multi_hop_neighbor`` node sets and sparse adjacencies, the
+sparse aggregators, GeniePath's per-depth projections and LSTM).
+
+The hop sets and adjacencies come from :class:`~euler_amd.dataflow.device_flow.
+DeviceFullFlow` (no self loops): hop h+1's set is ``unique([neighbours, set h])`` — the
+reference's neighbour set plus the previous set's nodes, which have no adjacency entry
+unless they are neighbours, so every root's aggregation is the reference's — padded with
+``-1`` in fixed capacities; the adjacency of hop h is the block's (target, source) edge
+list as a ``[cap_h, cap_h+1]`` SparseTensor whose padding entries are ``(-1, -1)``, which
+the sparse aggregators drop (``utils/sparse_aggregators.py``).  The model's own
+``encode`` (``utils/encoders.py``), ``out_fc``, loss and F1 counts then run as in
+:class:`~euler_amd.models.full_trainer.FullFlowTrainer`, several steps per hipGraph.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from euler_amd.dataflow.device_flow import DeviceFullFlow
+from euler_amd.models.full_trainer import FullFlowTrainer
+from euler_amd.ops import mp_ops
+
+__all__ = ["EncoderFlowTrainer"]
+
+
+class EncoderFlowTrainer(FullFlowTrainer):
+    @classmethod
+    def from_model(cls, model, graph, batch_size, optimizer="adam", learning_rate=0.01, **kw):
+        import euler_amd.ops.graph_api as ge
+        from euler_amd.utils.encoders import GCNEncoder
+
+        enc = getattr(model, "_encoder", None)
+        ne = getattr(enc, "_node_encoder", None)
+        if not isinstance(enc, GCNEncoder) or ne is None or ne.use_id or ne.use_sparse_feature or \
+                not ne.use_feature:
+            raise ValueError("EncoderFlowTrainer trains GCNEncoder / GenieEncoder models over dense features")
+        masks = []
+        for m in enc.metapath:
+            ids = None if m is None else [int(t) for t in np.asarray(ge.get_edge_type_id(m)).reshape(-1)]
+            masks.append(graph._mask(None if ids is None or any(t < 0 for t in ids) else ids))
+        flow = DeviceFullFlow(graph, masks, int(batch_size), add_self_loops=False)
+        tr = cls(model, graph, batch_size, masks, add_self_loops=False, optimizer=optimizer,
+                 learning_rate=learning_rate, flow=flow, **kw)
+        return tr
+
+    def _node_features(self, rows):
+        ne = self.model._encoder._node_encoder
+        x = mp_ops.gather(self.features, rows.clamp(min=0)).float()
+        x = x * (rows >= 0).unsqueeze(1).to(x.dtype)
+        return ne.dense(x) if ne.combiner == "add" else x
+
+    def _forward(self, roots):
+        from euler_amd.ops.graph_api import SparseTensor
+
+        df = self.flow.produce(roots)
+        sets = [roots.reshape(-1).long()] + [b.n_id for b in df.blocks]
+        hidden = [self._node_features(s) for s in sets]
+        adjs = []
+        for b in df.blocks:
+            ei = b.edge_index
+            adj = SparseTensor(ei.t(), torch.ones(ei.shape[1], device=ei.device), list(b.size))
+            # the block's destination CSR is known from the expansion (mp_ops.cached_segment)
+            n = int(b.size[0])
+            adj._euler_idx = (ei[0], ei[1], n, mp_ops.cached_segment(ei, 0, n))
+            adjs.append(adj)
+        emb = self.model._encoder.encode(hidden, adjs)
+        return self.model.out_fc(emb).float(), df

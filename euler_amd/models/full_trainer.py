@@ -44,7 +44,7 @@ class FullFlowTrainer(CapturedTrainer):
 
     def __init__(self, model, graph, batch_size, masks, add_self_loops=True, features=None, labels=None,
                  optimizer="adam", learning_rate=0.01, caps=None, flow=None):
-        self.gnn = model.gnn
+        self.gnn = getattr(model, "gnn", None)  # None: an encoder model (models/encoder_trainer.py)
         self.graph = graph
         self.B = int(batch_size)
         feats = features if features is not None else graph.features

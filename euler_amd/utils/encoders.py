@@ -181,10 +181,14 @@ class GCNEncoder(nn.Module):
             hidden = nxt
         return hidden
 
+    def encode(self, hidden, adjs):
+        """root embeddings from the per-hop node embeddings and the hop adjacencies (the
+        device path passes -1-padded sets and adjacencies: models/encoder_trainer.py)"""
+        return self._propagate(hidden, adjs)[0]
+
     def forward(self, inputs):
         nodes, adjs = G.get_multi_hop_neighbor(inputs, self.metapath)
-        hidden = self._propagate([self.node_encoder(n) for n in nodes], adjs)
-        return _shaped(inputs, hidden[0])
+        return _shaped(inputs, self.encode([self.node_encoder(n) for n in nodes], adjs))
 
 
 class GenieEncoder(GCNEncoder):
@@ -199,7 +203,9 @@ class GenieEncoder(GCNEncoder):
 
     def forward(self, inputs):
         nodes, adjs = G.get_multi_hop_neighbor(inputs, self.metapath)
-        hidden = [self.node_encoder(n) for n in nodes]
+        return _shaped(inputs, self.encode([self.node_encoder(n) for n in nodes], adjs))
+
+    def encode(self, hidden, adjs):
         h_t = [self.depth_fc[0](hidden[0])]
         for layer in range(self.num_layers):
             agg = self.aggregators[layer]
@@ -211,7 +217,7 @@ class GenieEncoder(GCNEncoder):
             h_t.append(self.depth_fc[layer + 1](hidden[0]))
         seq = torch.stack(h_t, 1)  # [B, L+1, dim]
         out, _ = self.lstm(seq)
-        return _shaped(inputs, out[:, 0, :])
+        return out[:, 0, :]
 
 
 class _StoreMixin:

@@ -23,16 +23,31 @@ _relu = torch.relu
 
 
 def _adj_rows_cols(adj, device):
+    """(rows, cols, n, row SegmentIndex) of ``adj``, built once per adjacency and shared by
+    every aggregator / head / layer over it (a producer that knows the CSR — the device
+    flow — stores it as ``adj._euler_idx`` up front)"""
+    idx = getattr(adj, "_euler_idx", None)
+    if idx is not None and idx[0].device == torch.device(device):
+        return idx
     ind = torch.as_tensor(adj.indices).to(device).long()
     n = int(adj.dense_shape[0])
-    return ind[:, 0], ind[:, 1], n
+    rows, cols = ind[:, 0].contiguous(), ind[:, 1].contiguous()
+    idx = (rows, cols, n, mp_ops.SegmentIndex(rows, n))
+    try:
+        adj._euler_idx = idx
+    except AttributeError:
+        pass
+    return idx
 
 
-def _sum_neighbors(neigh, rows, cols, n):
+def _sum_neighbors(neigh, rows, cols, n, seg=None):
     """ones(adj) @ neigh as gather + segment sum; returns (sum [n, d], degree [n, 1])."""
+    seg = seg if seg is not None else rows
     msg = mp_ops.gather(neigh, cols)
-    s = mp_ops.scatter_add(msg, rows, n)
-    deg = torch.bincount(rows, minlength=n).to(neigh.dtype).view(-1, 1)
+    s = mp_ops.scatter_add(msg, seg, n)
+    # a -1 row (padding entry of a device-built adjacency) is dropped, like in scatter_add
+    ones = torch.ones(rows.numel(), 1, dtype=neigh.dtype, device=neigh.device)
+    deg = mp_ops.scatter_add(ones, seg, n)
     return s, deg
 
 
@@ -44,8 +59,8 @@ class GCNAggregator(nn.Module):
 
     def forward(self, inputs):
         self_emb, neigh_emb, adj = inputs
-        rows, cols, n = _adj_rows_cols(adj, self_emb.device)
-        agg, deg = _sum_neighbors(neigh_emb, rows, cols, n)
+        rows, cols, n, seg = _adj_rows_cols(adj, self_emb.device)
+        agg, deg = _sum_neighbors(neigh_emb, rows, cols, n, seg)
         if self.renorm:
             agg = (self_emb + agg) / (1.0 + deg)
         else:
@@ -64,8 +79,8 @@ class MeanAggregator(nn.Module):
 
     def forward(self, inputs):
         self_emb, neigh_emb, adj = inputs
-        rows, cols, n = _adj_rows_cols(adj, self_emb.device)
-        agg, deg = _sum_neighbors(neigh_emb, rows, cols, n)
+        rows, cols, n, seg = _adj_rows_cols(adj, self_emb.device)
+        agg, deg = _sum_neighbors(neigh_emb, rows, cols, n, seg)
         agg = agg / deg.clamp_min(1e-7)
         a, b = self.self_layer(self_emb), self.neigh_layer(agg)
         return torch.cat([a, b], 1) if self.concat else a + b
@@ -84,22 +99,25 @@ class SingleAttentionAggregator(nn.Module):
 
     def forward(self, inputs):
         self_emb, neigh_emb, adj = inputs
-        rows, cols, n = _adj_rows_cols(adj, self_emb.device)
+        rows, cols, n, seg = _adj_rows_cols(adj, self_emb.device)
         if self.renorm:
             # [eye | adj] over the column space [self rows ; neighbour rows]
             eye = torch.arange(n, device=rows.device)
             rows = torch.cat([eye, rows])
-            cols = torch.cat([eye, cols + n])
+            cols = torch.cat([eye, torch.where(cols >= 0, cols + n, cols)])
+            seg = mp_ops.SegmentIndex(rows, n)
             from_all = self.dense(torch.cat([self_emb, neigh_emb], 0))
             from_self = from_all[:n]
         else:
             from_all = self.dense(neigh_emb)
             from_self = self.dense(self_emb)
-        self_w = self.self_layer(from_self).view(-1)
-        all_w = self.neigh_layer(from_all).view(-1)
-        logits = F.leaky_relu(self_w[rows] + all_w[cols], 0.2).unsqueeze(-1)
-        coef = mp_ops.scatter_softmax(logits, rows, n)
-        out = mp_ops.scatter_add(coef * mp_ops.gather(from_all, cols), rows, n)
+        self_w = self.self_layer(from_self).view(-1, 1)
+        all_w = self.neigh_layer(from_all).view(-1, 1)
+        # gfx950 gathers (their backward is a segment reduction; a torch index backward
+        # serialises on repeated rows, e.g. the -1 padding entries of a device adjacency)
+        logits = F.leaky_relu(mp_ops.gather(self_w, rows) + mp_ops.gather(all_w, cols), 0.2)
+        coef = mp_ops.scatter_softmax(logits, seg, n)
+        out = mp_ops.scatter_add(coef * mp_ops.gather(from_all, cols), seg, n)
         if not self.renorm:
             out = from_self + out
         if self.activation is not None:

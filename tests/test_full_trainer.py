@@ -193,7 +193,7 @@ def test_device_graph_replay_matches_eager():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("model", ["gcn", "appnp", "sgcn", "tagcn", "agnn", "gat", "arma", "dna", "fastgcn",
-                                   "adaptivegcn"])
+                                   "adaptivegcn", "geniepath"])
 def test_estimator_device_graph_gcn_family_gpu(tmp_path, monkeypatch, model):
     monkeypatch.chdir(tmp_path)
     from euler_amd.tools.runner import main
@@ -285,3 +285,36 @@ def test_layer_sampled_gcn_device_path_cpu(tmp_path, model):
                 "--seed", "1", "--model_dir", str(tmp_path / model), "--device_graph", "--learning_rate", "0.01",
                 "--total_step", "6"], model=model)
     assert res["step"] == 6 and math.isfinite(res["loss"])
+
+
+@pytest.mark.parametrize("agg", ["attention", "gcn", "mean"])
+def test_encoder_device_path_matches_engine_encoder_cpu(agg, monkeypatch):
+    """GeniePath on the device path (models/encoder_trainer.py): the padded device hop sets
+    and adjacencies give the roots the same logits as the engine's get_multi_hop_neighbor
+    path of the same model"""
+    from euler_amd.models.encoder_trainer import EncoderFlowTrainer
+    from euler_amd.utils import encoders
+
+    orig = encoders.GenieEncoder.__init__
+    monkeypatch.setattr(encoders.GenieEncoder, "__init__",
+                        lambda self, mp, dim, aggregator="attention", *a, **k: orig(self, mp, dim, agg, *a, **k))
+    _, m, est = _setup("cpu", model="geniepath", batch=8)
+    est._prepare(est.get_train_from_input(8, est.params))
+    m.eval()
+    g = _device_graph(_Feat(m), "cpu")
+    tr = EncoderFlowTrainer.from_model(m, g, 8)
+    roots = torch.randint(0, g.num_rows, (8,), generator=torch.Generator().manual_seed(2))
+    with torch.no_grad():
+        dev, _ = tr._forward(roots)
+        raw = torch.as_tensor(np.asarray(g.ids)[roots.numpy()].astype(np.int64))
+        eng = m.out_fc(m.embed(raw)).float()
+    assert torch.allclose(dev, eng, atol=1e-4, rtol=1e-4)
+
+
+class _Feat:
+    """feature / label columns of an encoder model in the shape _device_graph reads"""
+
+    def __init__(self, m):
+        ne = m._encoder._node_encoder
+        self.gnn = type("G", (), {"feature_idx": ne.feature_idx, "feature_dim": ne.feature_dim})
+        self.label_idx, self.label_dim = m.label_idx, m.label_dim
