@@ -523,8 +523,27 @@ class BaseEstimator:
             return DgiTrainer(model, graph, int(self.params["batch_size"]),
                               optimizer=self.params.get("optimizer", "adam"),
                               learning_rate=float(self.params.get("learning_rate", 0.001)))
-        from euler_amd.utils.encoders import GCNEncoder
+        from euler_amd.utils.encoders import GCNEncoder, LGCEncoder
 
+        if isinstance(getattr(model, "_encoder", None), LGCEncoder) and hasattr(model, "label_idx"):
+            # LGCN: neighbour draws and feature gathers on the HBM graph, the model's own
+            # top-k + 1-D convolutions (models/encoder_trainer.py LgcnTrainer)
+            from euler_amd.models.encoder_trainer import LgcnTrainer
+
+            self._prepare(first)
+            if self._sync is not None:
+                self._sync.remove()
+            enc = model._encoder
+            nt = self.params.get("train_node_type", -1)
+            node_type = -1 if nt in (None, -1, "-1") else int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
+            fdt = torch.float32 if self.params.get("device_feature_dtype", "bf16") == "fp32" else torch.bfloat16
+            graph = DeviceGraph.from_engine(node_type=node_type, features=[enc.feature_idx],
+                                            feature_dims=[enc.feature_dim], label=model.label_idx,
+                                            label_dim=model.label_dim, feature_dtype=fdt,
+                                            seed=seed * 7919 + self.rank, device=self.device)
+            return LgcnTrainer.from_model(model, graph, int(self.params["batch_size"]),
+                                          optimizer=self.params.get("optimizer", "adam"),
+                                          learning_rate=float(self.params.get("learning_rate", 0.001)))
         if isinstance(getattr(model, "_encoder", None), GCNEncoder) and hasattr(model, "label_idx"):
             # GeniePath and other full-neighbour encoder models: hop sets and adjacencies
             # built on the device, the model's own encode (models/encoder_trainer.py)

@@ -1,6 +1,6 @@
-"""Device-path training of the full-neighbour *encoder* models — GeniePath
-(``GenieEncoder``) and any ``SuperviseModel`` whose ``_encoder`` is a ``GCNEncoder`` —
-under ``NodeEstimator(device_graph=True)``.
+"""Device-path training of the *encoder* models — GeniePath (``GenieEncoder``), any
+``SuperviseModel`` whose ``_encoder`` is a ``GCNEncoder``, and LGCN (``LGCEncoder``,
+:class:`LgcnTrainer`) — under ``NodeEstimator(device_graph=True)``.
 
 Reference: ``examples/geniepath/geniepath.py:26-49``, ``tf_euler/python/utils/
 encoders.py:174-291`` (``get_multi_hop_neighbor`` node sets and sparse adjacencies, the
@@ -25,7 +25,7 @@ from euler_amd.dataflow.device_flow import DeviceFullFlow
 from euler_amd.models.full_trainer import FullFlowTrainer
 from euler_amd.ops import mp_ops
 
-__all__ = ["EncoderFlowTrainer"]
+__all__ = ["EncoderFlowTrainer", "LgcnTrainer"]
 
 
 class EncoderFlowTrainer(FullFlowTrainer):
@@ -70,3 +70,40 @@ class EncoderFlowTrainer(FullFlowTrainer):
             adjs.append(adj)
         emb = self.model._encoder.encode(hidden, adjs)
         return self.model.out_fc(emb).float(), df
+
+
+class LgcnTrainer(FullFlowTrainer):
+    """LGCN (reference ``examples/lgcn/lgcn.py:26-37``, ``encoders.py:872-922``): ``nb_num``
+    weighted neighbour draws per root on the HBM graph (Philox stream 6; a root without an
+    out-edge draws ``-1``, whose features are zero like the engine's default node), node
+    and neighbour features gathered in HBM, then the model's own top-k + 1-D convolutions
+    (``LGCEncoder.encode``), ``out_fc``, loss and F1 counts; several steps per hipGraph."""
+
+    @classmethod
+    def from_model(cls, model, graph, batch_size, optimizer="adam", learning_rate=0.01, **kw):
+        import euler_amd.ops.graph_api as ge
+        from euler_amd.utils.encoders import LGCEncoder
+
+        enc = getattr(model, "_encoder", None)
+        if not isinstance(enc, LGCEncoder):
+            raise ValueError("LgcnTrainer trains LGCN (LGCEncoder)")
+        ids = [int(t) for t in np.asarray(ge.get_edge_type_id(enc.edge_type)).reshape(-1)]
+        tr = cls.__new__(cls)
+        tr.types = None if any(t < 0 for t in ids) else ids
+        FullFlowTrainer.__init__(tr, model, graph, batch_size, [], add_self_loops=False, optimizer=optimizer,
+                                 learning_rate=learning_rate, **kw)
+        return tr
+
+    def _forward(self, roots):
+        enc = self.model._encoder
+        roots = roots.reshape(-1).long()
+        nbrs = self.graph.sample_neighbor(roots, enc.nb_num, edge_types=self.types, default=-1,
+                                          stream_id=6).long().reshape(-1)
+
+        def feats(rows):
+            x = mp_ops.gather(self.features, rows.clamp(min=0)).float()
+            return x * (rows >= 0).unsqueeze(1).to(x.dtype)
+
+        nb_f = feats(nbrs).view(roots.numel(), enc.nb_num, -1)
+        emb = enc.encode(feats(roots), nb_f)
+        return self.model.out_fc(emb).float(), None

@@ -576,7 +576,11 @@ class LGCEncoder(nn.Module):
         nbrs = G.sample_neighbor(ids, self.edge_type, self.nb_num)[0]
         node_f = G.get_dense_feature(ids, [self.feature_idx], [self.feature_dim])[0].to(dev)
         nb_f = G.get_dense_feature(nbrs.reshape(-1), [self.feature_idx], [self.feature_dim])[0].to(dev)
-        nb_f = nb_f.reshape(b, self.nb_num, self.feature_dim)
+        return self.encode(node_f, nb_f.reshape(b, self.nb_num, self.feature_dim))
+
+    def encode(self, node_f, nb_f):
+        """node features [b, D] and sampled-neighbour features [b, nb_num, D] -> [b, out_dim]
+        (the device path passes features gathered in HBM: models/encoder_trainer.py)"""
         topk = torch.topk(nb_f.transpose(1, 2), self.k, dim=-1).values  # [b, D, k]
         seq = torch.cat([node_f.unsqueeze(-1), topk], -1)  # [b, D, k+1] (channels-first)
         out = self.conv2(self.conv1(seq))

@@ -193,7 +193,7 @@ def test_device_graph_replay_matches_eager():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("model", ["gcn", "appnp", "sgcn", "tagcn", "agnn", "gat", "arma", "dna", "fastgcn",
-                                   "adaptivegcn", "geniepath"])
+                                   "adaptivegcn", "geniepath", "lgcn"])
 def test_estimator_device_graph_gcn_family_gpu(tmp_path, monkeypatch, model):
     monkeypatch.chdir(tmp_path)
     from euler_amd.tools.runner import main
@@ -318,3 +318,44 @@ class _Feat:
         ne = m._encoder._node_encoder
         self.gnn = type("G", (), {"feature_idx": ne.feature_idx, "feature_dim": ne.feature_dim})
         self.label_idx, self.label_dim = m.label_idx, m.label_dim
+
+
+def test_lgcn_device_path_matches_engine_features_cpu(tmp_path):
+    """LGCN on the device path: for the neighbours it drew, the logits equal the model's
+    engine-side encoder over features read from the engine (default node: zeros); the
+    estimator trains it"""
+    import euler_amd.ops.graph_api as ge
+    from euler_amd.models.encoder_trainer import LgcnTrainer
+
+    a, m, est = _setup("cpu", model="lgcn", batch=8)
+    est._prepare(est.get_train_from_input(8, est.params))
+    enc = m._encoder
+    from euler_amd.graph.device_graph import DeviceGraph
+
+    g = DeviceGraph.from_engine(features=[enc.feature_idx], feature_dims=[enc.feature_dim], label=m.label_idx,
+                                label_dim=m.label_dim, feature_dtype=torch.float32, seed=5, device="cpu")
+    tr = LgcnTrainer.from_model(m, g, 8)
+    roots = torch.randint(0, g.num_rows, (8,), generator=torch.Generator().manual_seed(2))
+    state = g.rng.clone()
+    g.reseed_cpu()
+    with torch.no_grad():
+        dev, _ = tr._forward(roots)
+    g.rng.copy_(state)
+    g.reseed_cpu()
+    nbrs = g.sample_neighbor(roots, enc.nb_num, edge_types=tr.types, default=-1, stream_id=6).long().reshape(-1)
+    ids = np.asarray(g.ids).astype(np.int64)
+
+    def eng(rows):
+        raw = np.where(rows.numpy() >= 0, ids[rows.clamp(min=0).numpy()], -1)
+        x = torch.as_tensor(np.asarray(ge.get_dense_feature(raw, [enc.feature_idx], [enc.feature_dim])[0]))
+        return x.float().reshape(rows.numel(), -1) * (rows >= 0).unsqueeze(1)
+
+    with torch.no_grad():
+        want = m.out_fc(enc.encode(eng(roots), eng(nbrs).view(8, enc.nb_num, -1))).float()
+    assert torch.allclose(dev, want, atol=1e-5)
+    from euler_amd.tools.runner import main
+
+    res = main(["--dataset", "ppi", "--scale", "0.05", "--batch_size", "16", "--log_steps", "3", "--device", "cpu",
+                "--seed", "1", "--model_dir", str(tmp_path / "lgcn"), "--device_graph", "--total_step", "6"],
+               model="lgcn")
+    assert res["step"] == 6 and math.isfinite(res["loss"])
