@@ -523,7 +523,31 @@ class BaseEstimator:
             return DgiTrainer(model, graph, int(self.params["batch_size"]),
                               optimizer=self.params.get("optimizer", "adam"),
                               learning_rate=float(self.params.get("learning_rate", 0.001)))
+        from euler_amd import solution as S
         from euler_amd.utils.encoders import GCNEncoder, LGCEncoder
+
+        if isinstance(model, S.SuperviseSolution):
+            # the solution API over a SageEncoder: tree draws, features and the encoder's
+            # aggregators on the HBM graph (models/encoder_trainer.py SolutionTrainer)
+            from euler_amd.models.encoder_trainer import SolutionTrainer
+
+            self._prepare(first)
+            if self._sync is not None:
+                self._sync.remove()
+            ne = getattr(model.encoder, "_node_encoder", None)
+            lab = model.get_label_fn
+            if ne is None or not getattr(ne, "use_feature", False) or not hasattr(lab, "label_idx"):
+                raise ValueError("device_graph=True trains SuperviseSolution over a dense-feature SageEncoder "
+                                 "with GetLabelFromFea labels")
+            nt = self.params.get("train_node_type", -1)
+            node_type = -1 if nt in (None, -1, "-1") else int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
+            fdt = torch.float32 if self.params.get("device_feature_dtype", "bf16") == "fp32" else torch.bfloat16
+            graph = DeviceGraph.from_engine(node_type=node_type, features=ne.feature_idx, feature_dims=ne.feature_dim,
+                                            label=lab.label_idx, label_dim=lab.label_dim, feature_dtype=fdt,
+                                            seed=seed * 7919 + self.rank, device=self.device)
+            return SolutionTrainer.from_model(model, graph, int(self.params["batch_size"]),
+                                              optimizer=self.params.get("optimizer", "adam"),
+                                              learning_rate=float(self.params.get("learning_rate", 0.001)))
 
         if isinstance(getattr(model, "_encoder", None), LGCEncoder) and hasattr(model, "label_idx"):
             # LGCN: neighbour draws and feature gathers on the HBM graph, the model's own

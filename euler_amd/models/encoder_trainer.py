@@ -1,6 +1,7 @@
 """Device-path training of the *encoder* models — GeniePath (``GenieEncoder``), any
-``SuperviseModel`` whose ``_encoder`` is a ``GCNEncoder``, and LGCN (``LGCEncoder``,
-:class:`LgcnTrainer`) — under ``NodeEstimator(device_graph=True)``.
+``SuperviseModel`` whose ``_encoder`` is a ``GCNEncoder``, LGCN (``LGCEncoder``,
+:class:`LgcnTrainer`) and ``SuperviseSolution`` over a ``SageEncoder``
+(:class:`SolutionTrainer`) — under ``NodeEstimator(device_graph=True)``.
 
 Reference: ``examples/geniepath/geniepath.py:26-49``, ``tf_euler/python/utils/
 encoders.py:174-291`` (``get_multi_hop_neighbor`` node sets and sparse adjacencies, the
@@ -25,7 +26,7 @@ from euler_amd.dataflow.device_flow import DeviceFullFlow
 from euler_amd.models.full_trainer import FullFlowTrainer
 from euler_amd.ops import mp_ops
 
-__all__ = ["EncoderFlowTrainer", "LgcnTrainer"]
+__all__ = ["EncoderFlowTrainer", "LgcnTrainer", "SolutionTrainer"]
 
 
 class EncoderFlowTrainer(FullFlowTrainer):
@@ -107,3 +108,48 @@ class LgcnTrainer(FullFlowTrainer):
         nb_f = feats(nbrs).view(roots.numel(), enc.nb_num, -1)
         emb = enc.encode(feats(roots), nb_f)
         return self.model.out_fc(emb).float(), None
+
+
+class SolutionTrainer(FullFlowTrainer):
+    """``solution.SuperviseSolution`` (reference ``euler_estimator`` solution API,
+    ``examples/solution/run_solution.py``) over a dense-feature ``SageEncoder``, labels from
+    a dense feature (``GetLabelFromFea``), the default sigmoid loss: the fan-out tree drawn
+    per hop on the HBM graph (Philox stream 4 + h; ``-1`` for a node without an out-edge,
+    zero features like the engine's default node), features gathered once, the encoder's own
+    aggregators (``SageEncoder._aggregate``), the solution's ``logit_fn``, the fused loss +
+    F1 counts; several steps per hipGraph."""
+
+    @classmethod
+    def from_model(cls, model, graph, batch_size, optimizer="adam", learning_rate=0.01, **kw):
+        import euler_amd.ops.graph_api as ge
+        from euler_amd import solution as S
+        from euler_amd.utils.encoders import SageEncoder
+
+        enc = getattr(model, "encoder", None)
+        ne = getattr(enc, "_node_encoder", None)
+        if not isinstance(model, S.SuperviseSolution) or type(enc) is not SageEncoder or ne is None or \
+                ne.use_id or ne.use_sparse_feature or not ne.use_feature or model.loss_fn is not S.sigmoid_loss or \
+                not isinstance(model.get_label_fn, S.GetLabelFromFea):
+            raise ValueError("SolutionTrainer trains SuperviseSolution(GetLabelFromFea, dense-feature SageEncoder, "
+                             "logit_fn) with the default sigmoid loss")
+        tr = cls.__new__(cls)
+        tr.types = []
+        for m in enc.metapath:
+            ids = [int(t) for t in np.asarray(ge.get_edge_type_id(m)).reshape(-1)]
+            tr.types.append(None if any(t < 0 for t in ids) else ids)
+        FullFlowTrainer.__init__(tr, model, graph, batch_size, [], add_self_loops=False, optimizer=optimizer,
+                                 learning_rate=learning_rate, **kw)
+        return tr
+
+    def _forward(self, roots):
+        enc = self.model.encoder
+        hops = [roots.reshape(-1).long()]
+        for i, (f, et) in enumerate(zip(enc.fanouts, self.types)):
+            hops.append(self.graph.sample_neighbor(hops[-1], int(f), edge_types=et, default=-1,
+                                                   stream_id=4 + i).long().reshape(-1))
+        hidden = []
+        for rows in hops:
+            x = mp_ops.gather(self.features, rows.clamp(min=0)).float()
+            hidden.append(x * (rows >= 0).unsqueeze(1).to(x.dtype))
+        emb = enc._aggregate(hidden)
+        return self.model.logit_fn(emb).float(), None

@@ -193,7 +193,7 @@ def test_device_graph_replay_matches_eager():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("model", ["gcn", "appnp", "sgcn", "tagcn", "agnn", "gat", "arma", "dna", "fastgcn",
-                                   "adaptivegcn", "geniepath", "lgcn"])
+                                   "adaptivegcn", "geniepath", "lgcn", "solution"])
 def test_estimator_device_graph_gcn_family_gpu(tmp_path, monkeypatch, model):
     monkeypatch.chdir(tmp_path)
     from euler_amd.tools.runner import main
@@ -359,3 +359,40 @@ def test_lgcn_device_path_matches_engine_features_cpu(tmp_path):
                 "--seed", "1", "--model_dir", str(tmp_path / "lgcn"), "--device_graph", "--total_step", "6"],
                model="lgcn")
     assert res["step"] == 6 and math.isfinite(res["loss"])
+
+
+def test_solution_device_path_matches_engine_features_cpu(tmp_path):
+    """SuperviseSolution over a SageEncoder on the device path: for the tree it drew, the
+    logits equal the encoder's aggregation over features read from the engine"""
+    import euler_amd.ops.graph_api as ge
+    from euler_amd.graph.device_graph import DeviceGraph
+    from euler_amd.models.encoder_trainer import SolutionTrainer
+
+    a, m, est = _setup("cpu", model="solution", batch=8)
+    est._prepare(est.get_train_from_input(8, est.params))
+    enc, lab = m.encoder, m.get_label_fn
+    ne = enc._node_encoder
+    g = DeviceGraph.from_engine(features=ne.feature_idx, feature_dims=ne.feature_dim, label=lab.label_idx,
+                                label_dim=lab.label_dim, feature_dtype=torch.float32, seed=5, device="cpu")
+    tr = SolutionTrainer.from_model(m, g, 8)
+    roots = torch.randint(0, g.num_rows, (8,), generator=torch.Generator().manual_seed(2))
+    state = g.rng.clone()
+    g.reseed_cpu()
+    with torch.no_grad():
+        dev, _ = tr._forward(roots)
+    g.rng.copy_(state)
+    g.reseed_cpu()
+    hops = [roots.long()]
+    for i, (f, et) in enumerate(zip(enc.fanouts, tr.types)):
+        hops.append(g.sample_neighbor(hops[-1], int(f), edge_types=et, default=-1, stream_id=4 + i).long().reshape(-1))
+    ids = np.asarray(g.ids).astype(np.int64)
+
+    def eng(rows):
+        raw = ids[rows.clamp(min=0).numpy()]
+        x = torch.cat([torch.as_tensor(np.asarray(t)).float().reshape(rows.numel(), -1)
+                       for t in ge.get_dense_feature(raw, ne.feature_idx, ne.feature_dim)], 1)
+        return x * (rows >= 0).unsqueeze(1)
+
+    with torch.no_grad():
+        want = m.logit_fn(enc._aggregate([eng(h) for h in hops])).float()
+    assert torch.allclose(dev, want, atol=1e-5)
