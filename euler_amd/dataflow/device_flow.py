@@ -35,7 +35,7 @@ from euler_amd.dataflow.dataflows import Block, DataFlow
 from euler_amd.ops._native import hip, use_hip
 from euler_amd.ops.mp_ops import SegmentIndex
 
-__all__ = ["DeviceFullFlow", "DeviceLayerFlow", "DeviceSageFlow", "full_neighbors_cpu", "max_out_degree"]
+__all__ = ["DeviceFullFlow", "DeviceLayerFlow", "DeviceRelationFlow", "DeviceSageFlow", "full_neighbors_cpu", "max_out_degree"]
 
 
 def _round_up(x: int, m: int = 256) -> int:
@@ -187,6 +187,7 @@ class DeviceFullFlow:
             kept = self._filter(h, n_id, nbr)
             if kept is not None:
                 nbr = kept
+            attr = self._hop_attr(h, n_id, src, offs)
             cat = torch.cat([nbr, n_id])
             uniq, inv, cnt = _unique_padded(cat)
             if use_hip(n_id) and _FUSED_BLOCK and kept is None:
@@ -197,7 +198,7 @@ class DeviceFullFlow:
                 seg = SegmentIndex(edge_index[0], cap_prev)
                 seg._perm, seg._indptr, seg._counts = perm, indptr, counts
                 edge_index._euler_cache = {"_euler_seg0_%d" % cap_prev: seg}
-                df.blocks.append(Block(new_n_id, res_n_id, None, edge_index, [cap_prev, cap_n]))
+                df.blocks.append(Block(new_n_id, res_n_id, attr, edge_index, [cap_prev, cap_n]))
                 df._last = new_n_id
                 n_id = new_n_id
                 cap_prev = cap_n
@@ -223,7 +224,7 @@ class DeviceFullFlow:
                 perm, indptr = _dst_csr(src, offs.clamp(max=cap_e), prev_cnt, cap_e, cap_prev, self.self_loops)
                 edge_index._euler_cache = {"_euler_seg0_%d" % cap_prev: SegmentIndex.from_csr(edge_t, cap_prev,
                                                                                                  perm, indptr)}
-            df.blocks.append(Block(new_n_id, res_n_id, None, edge_index, [cap_prev, cap_n]))
+            df.blocks.append(Block(new_n_id, res_n_id, attr, edge_index, [cap_prev, cap_n]))
             df._last = new_n_id
             ar = torch.arange(cap_n, dtype=torch.long, device=dev)
             prev_cnt = torch.clamp(cnt.reshape(()), max=cap_n)
@@ -240,6 +241,48 @@ class DeviceFullFlow:
     def _filter(self, h, n_id, nbr):
         """hook: the hop's neighbour list with dropped entries set to -1 (None: keep all)"""
         return None
+
+    def _hop_attr(self, h, n_id, src, offs):
+        """hook: a per-edge attribute of the hop (the block's ``e_id``; None: no attribute)"""
+        return None
+
+    def edge_positions(self, h, n_id, src, offs):
+        """CSR position of every expansion entry (-1 for padding): entry e of target i is
+        the k-th neighbour of i, k = e - (start of i's entries), walked through i's
+        segments of the hop's edge types in ascending type order (``full_neighbors``'
+        order)"""
+        g = self.g
+        T = g.num_types
+        cap_e = src.numel()
+        ok = src >= 0
+        i = src.clamp(min=0)
+        excl = torch.cat([torch.zeros(1, dtype=offs.dtype, device=offs.device), offs])[i]
+        k = torch.arange(cap_e, dtype=torch.long, device=src.device) - excl.long()
+        r = n_id.clamp(min=0)[i]
+        pos = torch.full_like(k, -1)
+        for t in range(T):
+            if not (self.masks[h] >> t) & 1:
+                continue
+            a, b = g.indptr[r * T + t], g.indptr[r * T + t + 1]
+            n = b - a
+            pos = torch.where((pos < 0) & (k >= 0) & (k < n), a + k, pos)
+            k = k - n
+        return torch.where(ok, pos, torch.full_like(pos, -1))
+
+
+class DeviceRelationFlow(DeviceFullFlow):
+    """``RelationDataFlow`` (reference ``relation_dataflow.py:25-75``; engine twin in
+    ``dataflows.py``) on the device: full neighbourhoods without self loops, each block's
+    ``e_id`` the per-edge attribute ``edge_attr[CSR position]`` (``-1`` on padding) — the
+    R-GCN relation of the (target, neighbour, type) edge, read once from the engine."""
+
+    def __init__(self, graph, masks, batch_size: int, edge_attr: torch.Tensor, caps=None):
+        super().__init__(graph, masks, batch_size, add_self_loops=False, caps=caps)
+        self.edge_attr = edge_attr.to(graph.device).long()
+
+    def _hop_attr(self, h, n_id, src, offs):
+        pos = self.edge_positions(h, n_id, src, offs)
+        return torch.where(pos >= 0, self.edge_attr[pos.clamp(min=0)], torch.full_like(pos, -1))
 
 
 class DeviceLayerFlow(DeviceFullFlow):

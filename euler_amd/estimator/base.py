@@ -524,7 +524,23 @@ class BaseEstimator:
                               optimizer=self.params.get("optimizer", "adam"),
                               learning_rate=float(self.params.get("learning_rate", 0.001)))
         from euler_amd import solution as S
+        from euler_amd.models.unsupervised import UnsupervisedRGCN
         from euler_amd.utils.encoders import GCNEncoder, LGCEncoder
+
+        if isinstance(model, UnsupervisedRGCN):
+            # R-GCN over id embeddings: relation blocks (relations from the edge feature, read
+            # once) and the model's own layers on the HBM graph (models/rgcn_trainer.py)
+            from euler_amd.models.rgcn_trainer import UnsupRgcnTrainer
+
+            self._prepare(first)
+            if self._sync is not None:
+                self._sync.remove()
+            nt = self.params.get("train_node_type", model.node_type)
+            node_type = -1 if nt in (None, -1, "-1") else int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
+            graph = DeviceGraph.from_engine(node_type=node_type, seed=seed * 7919 + self.rank, device=self.device)
+            return UnsupRgcnTrainer(model, graph, int(self.params["batch_size"]),
+                                    optimizer=self.params.get("optimizer", "adam"),
+                                    learning_rate=float(self.params.get("learning_rate", 0.001)))
 
         if isinstance(model, S.SuperviseSolution):
             # the solution API over a SageEncoder: tree draws, features and the encoder's
