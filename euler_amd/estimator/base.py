@@ -542,6 +542,23 @@ class BaseEstimator:
                                     optimizer=self.params.get("optimizer", "adam"),
                                     learning_rate=float(self.params.get("learning_rate", 0.001)))
 
+        if isinstance(model, S.UnsuperviseSolution):
+            from euler_amd.models.encoder_trainer import UnsupSolutionTrainer
+
+            self._prepare(first)
+            if self._sync is not None:
+                self._sync.remove()
+            ne = getattr(model.target_encoder, "_node_encoder", None)
+            if ne is None or not getattr(ne, "use_feature", False):
+                raise ValueError("device_graph=True trains UnsuperviseSolution over dense-feature SageEncoders")
+            nt = self.params.get("train_node_type", -1)
+            node_type = -1 if nt in (None, -1, "-1") else int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
+            fdt = torch.float32 if self.params.get("device_feature_dtype", "bf16") == "fp32" else torch.bfloat16
+            graph = DeviceGraph.from_engine(node_type=node_type, features=ne.feature_idx, feature_dims=ne.feature_dim,
+                                            feature_dtype=fdt, seed=seed * 7919 + self.rank, device=self.device)
+            return UnsupSolutionTrainer(model, graph, int(self.params["batch_size"]),
+                                        optimizer=self.params.get("optimizer", "adam"),
+                                        learning_rate=float(self.params.get("learning_rate", 0.001)))
         if isinstance(model, S.SuperviseSolution):
             # the solution API over a SageEncoder: tree draws, features and the encoder's
             # aggregators on the HBM graph (models/encoder_trainer.py SolutionTrainer)

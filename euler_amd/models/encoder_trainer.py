@@ -23,10 +23,11 @@ import numpy as np
 import torch
 
 from euler_amd.dataflow.device_flow import DeviceFullFlow
+from euler_amd.models.captured import CapturedTrainer
 from euler_amd.models.full_trainer import FullFlowTrainer
 from euler_amd.ops import mp_ops
 
-__all__ = ["EncoderFlowTrainer", "LgcnTrainer", "SolutionTrainer"]
+__all__ = ["EncoderFlowTrainer", "LgcnTrainer", "SolutionTrainer", "UnsupSolutionTrainer"]
 
 
 class EncoderFlowTrainer(FullFlowTrainer):
@@ -153,3 +154,107 @@ class SolutionTrainer(FullFlowTrainer):
             hidden.append(x * (rows >= 0).unsqueeze(1).to(x.dtype))
         emb = enc._aggregate(hidden)
         return self.model.logit_fn(emb).float(), None
+
+
+def _check_sage_encoder(enc):
+    from euler_amd.utils.encoders import SageEncoder
+
+    ne = getattr(enc, "_node_encoder", None)
+    if type(enc) is not SageEncoder or ne is None or ne.use_id or ne.use_sparse_feature or not ne.use_feature:
+        raise ValueError("the solution device paths take dense-feature SageEncoders")
+    return ne
+
+
+def _type_list(ge, et):
+    ids = [int(t) for t in np.asarray(ge.get_edge_type_id(et)).reshape(-1)]
+    return None if any(t < 0 for t in ids) else ids
+
+
+def _sage_tree_encode(enc, graph, features, types, roots, stream_base):
+    """SageEncoder.forward on the HBM graph: per-hop draws (Philox stream_base + h), one
+    feature gather per hop, the encoder's aggregators"""
+    hops = [roots.reshape(-1).long()]
+    for i, (f, et) in enumerate(zip(enc.fanouts, types)):
+        hops.append(graph.sample_neighbor(hops[-1], int(f), edge_types=et, default=-1,
+                                          stream_id=stream_base + i).long().reshape(-1))
+    hidden = []
+    for rows in hops:
+        x = mp_ops.gather(features, rows.clamp(min=0)).float()
+        hidden.append(x * (rows >= 0).unsqueeze(1).to(x.dtype))
+    return enc._aggregate(hidden)
+
+
+class UnsupSolutionTrainer(CapturedTrainer):
+    """``solution.UnsuperviseSolution`` (reference ``base_unsupervise.py:27-73``) with
+    dense-feature ``SageEncoder`` target / context encoders, ``SamplePosWithTypes``
+    positives and single-type ``SampleNegWithTypes`` negatives: roots, positives and
+    negatives drawn on the HBM graph, both encoders' trees built there, the solution's own
+    ``logit_fn`` and ``loss_fn``, MRR on the device; several steps per hipGraph."""
+
+    metric_name = "mrr"
+
+    def __init__(self, model, graph, batch_size, optimizer="adam", learning_rate=0.01):
+        import copy
+
+        import euler_amd.ops.graph_api as ge
+        from euler_amd import solution as S
+
+        ne = _check_sage_encoder(model.target_encoder)
+        ne_c = _check_sage_encoder(model.context_encoder)
+        pos_fn, neg_fn = model.pos_sample_fn, model.neg_sample_fn
+        if not isinstance(pos_fn, S.SamplePosWithTypes) or not isinstance(neg_fn, S.SampleNegWithTypes) or \
+                len(neg_fn.neg_type) != 1 or list(ne_c.feature_idx) != list(ne.feature_idx):
+            raise ValueError("UnsupSolutionTrainer takes SamplePosWithTypes / single-type SampleNegWithTypes "
+                             "samplers and encoders over the same dense features")
+        if graph.features is None:
+            raise ValueError("the device graph needs the encoders' dense features (DeviceGraph.from_engine)")
+        self.graph, self.B = graph, int(batch_size)
+        self.P, self.K = int(pos_fn.num_pos), int(neg_fn.num_negs)
+        self.pos_types = _type_list(ge, pos_fn.edge_type)
+        self.t_types = [_type_list(ge, m) for m in model.target_encoder.metapath]
+        self.c_types = [_type_list(ge, m) for m in model.context_encoder.metapath]
+        self.features = graph.features
+        nt = neg_fn.neg_type[0]
+        tid = -1 if nt in (None, -1, "-1") else int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
+        _, _, nw = ge.get_engine().export_nodes()
+        self.neg_sampler = copy.copy(graph)
+        self.neg_sampler.set_root_type(tid, node_weights=np.asarray(nw))
+        self.mrr = torch.zeros(2, dtype=torch.float64, device=graph.device)
+        super().__init__(model, graph, graph.device, optimizer, learning_rate)
+
+    def _materialize(self):
+        if not any(isinstance(p, torch.nn.parameter.UninitializedParameter) for p in self.model.parameters()):
+            return
+        state = self.graph.rng.clone()
+        with torch.no_grad():
+            self._logits(torch.zeros(self.B, dtype=torch.long, device=self.features.device))
+        self.graph.rng.copy_(state)
+
+    def _logits(self, src):
+        m, g, B = self.model, self.graph, self.B
+        pos = g.sample_neighbor(src, self.P, edge_types=self.pos_types, default=-1, stream_id=4).long().reshape(-1)
+        neg = self.neg_sampler.sample_node(B * self.K, stream_id=5).long()
+        emb = _sage_tree_encode(m.target_encoder, g, self.features, self.t_types, src, 10).view(B, 1, -1)
+        ctx = _sage_tree_encode(m.context_encoder, g, self.features, self.c_types, torch.cat([pos, neg]), 20)
+        d = ctx.shape[-1]
+        self._samples = (src, pos, neg)
+        return m.logit_fn(emb, ctx[: B * self.P].view(B, self.P, d), ctx[B * self.P:].view(B, self.K, d))
+
+    def _forward_loss(self):
+        self._draw()
+        B = self.B
+        logits, neg_logits = self._logits(self.graph.sample_node(B, stream_id=1).long())
+        loss = self.model.loss_fn(logits, neg_logits)
+        with torch.no_grad():
+            lp = logits.float().reshape(B, -1)[:, :1]
+            ln = neg_logits.float().reshape(B, -1)
+            rank = 1.0 + (ln >= lp).sum(-1).double()
+            self.mrr += torch.stack([(1.0 / rank).sum(), torch.full_like(rank[0], float(B))])
+        return loss
+
+    def metric(self) -> float:
+        s, n = self.mrr.tolist()
+        return s / max(n, 1.0)
+
+    def reset_metric(self):
+        self.mrr.zero_()

@@ -89,3 +89,31 @@ def test_dgi_device_path_gpu_captured(cora, tmp_path, cuda):
     est = NodeEstimator(m, _params(cora, tmp_path, "cuda", total_step=64, log_steps=32, steps_per_graph=8))
     res = est.train()
     assert res["step"] == 64 and np.isfinite(res["loss"]) and est.device_trainer.captures >= 1
+
+
+def _unsup_solution(ds):
+    from euler_amd import solution as S
+    from euler_amd.utils import encoders as E
+
+    torch.manual_seed(0)
+    mk = lambda: E.SageEncoder([["train"], ["train"]], [3, 2], 8, feature_idx="feature", feature_dim=F,  # noqa
+                               max_id=ds.max_node_id)
+    return S.UnsuperviseSolution(mk(), mk(), S.SamplePosWithTypes(["train"], 1, ds.max_node_id),
+                                 S.SampleNegWithTypes("train", 3))
+
+
+def test_unsupervise_solution_device_path_cpu(cora, tmp_path):
+    """solution.UnsuperviseSolution (base_unsupervise.py:27-73) on the device path"""
+    m = _unsup_solution(cora)
+    est = NodeEstimator(m, _params(cora, tmp_path, "cpu"))
+    res = est.train()
+    assert res["step"] == 24 and np.isfinite(res["loss"]) and 0.0 < res["mrr"] <= 1.0
+    assert type(est.device_trainer).__name__ == "UnsupSolutionTrainer"
+
+
+@pytest.mark.gpu
+def test_unsupervise_solution_device_path_gpu_captured(cora, tmp_path, cuda):
+    m = _unsup_solution(cora)
+    est = NodeEstimator(m, _params(cora, tmp_path, "cuda", total_step=64, log_steps=32, steps_per_graph=8))
+    res = est.train()
+    assert res["step"] == 64 and np.isfinite(res["loss"]) and est.device_trainer.captures >= 1
