@@ -34,8 +34,13 @@ import os
 import sys
 import time
 
-import torch
-import torch.distributed as dist
+# dmabuf IPC is the only mode the MI355X host driver supports: RCCL and the xGMI all-reduce's
+# peer mappings fail without it.  Set before anything can initialise HIP, so a torchrun launch
+# behaves like the self-spawned one (parallel/launch.py sets it for its children too).
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
@@ -272,13 +277,21 @@ def main(argv=None):
                 "100M-node" if args.num_nodes == 100_000_000 else "%gM-node" % (args.num_nodes / 1e6)),
             "value": round(value, 1),
             "unit": "samples/s",
-            "n_gpus": world,
+            # a --shared-gpu rehearsal runs every rank on one physical GPU: n_gpus counts the
+            # devices, "ranks" the processes, and the number is no whole-node result
+            "n_gpus": 1 if args.shared_gpu else world,
+            "ranks": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 4),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(value / base_value, 2) if base_value and args.num_nodes == 100_000_000 else None,
+            "vs_baseline": (round(value / base_value, 2) if base_value and args.num_nodes == 100_000_000
+                            and not args.shared_gpu else None),
+            # the CPU comparison point is measured on the 16 host threads a job may use and
+            # scaled linearly to the node's cores (profiles/cpu_baseline.json)
+            "vs_baseline_kind": ("extrapolated CPU baseline (16 measured host threads scaled linearly to all node "
+                                 "cores)" if base_note and "linearly scaled" in base_note else "measured CPU baseline"),
             "dtype": "bf16",
             "data": "synthetic (power-law random graph + random-normal features, random-init weights)",
             "config": {

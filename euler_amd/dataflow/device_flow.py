@@ -7,9 +7,14 @@ engine path (``dataflows.GCNDataFlow``) reproduces that on the CPU graph engine 
 each block to the GPU.  Here the same blocks are built from the HBM copy of the graph
 (:class:`~euler_amd.graph.device_graph.DeviceGraph`) with every shape fixed up front:
 
-* node sets and edge lists have per-hop capacities (exact upper bounds from the graph's
-  maximum out-degree over the hop's edge types, never from a guess, so no batch can
-  overflow them); unused slots hold ``-1``;
+* node sets and edge lists have per-hop capacities; unused slots hold ``-1``.  The
+  default ("exact") caps are upper bounds from the graph's maximum out-degree over the
+  hop's edge types: hop 0's targets are the roots as drawn (repeats included), so its edge
+  cap is ``B * max_out_degree``; later hops expand deduplicated sets, so theirs is also
+  bounded by the masked edge count.  ``caps="bounded"`` sizes each hop from a degree
+  quantile times a safety factor instead (:func:`bounded_caps`), which on a power-law graph
+  is orders of magnitude smaller; a batch that exceeds a cap sets :attr:`overflow`, the
+  trainer notices at its next boundary and grows the caps (``grow``) and re-captures;
 * ``-1`` is the padding convention every message-passing op already honours
   (``mp_ops``: a ``-1`` destination / source edge is dropped, a ``-1`` gather row reads
   zeros), so the unchanged model convolutions run on the padded blocks and padded rows
@@ -135,6 +140,55 @@ def _unique_padded(x: torch.Tensor):
     return uniq, inv, torch.tensor([len(order)], dtype=torch.long)
 
 
+def exact_caps(graph, masks, batch_size: int):
+    """per-hop (edge, next-set) capacities no batch can exceed"""
+    caps = []
+    n = int(batch_size)
+    N = graph.num_rows
+    for h, m in enumerate(masks):
+        e = n * max_out_degree(graph, m)
+        if h > 0:  # a deduplicated set expands each node once
+            e = min(masked_edges(graph, m), e)
+        n_next = min(N, n + e)
+        caps.append((_round_up(max(e, 1)), _round_up(n_next)))
+        n = n_next
+    return caps
+
+
+def _bounded_args(spec: str):
+    """"bounded" or "bounded:<quantile>:<safety>" -> (quantile, safety)"""
+    parts = spec.split(":")
+    q = float(parts[1]) if len(parts) > 1 else 0.99
+    f = float(parts[2]) if len(parts) > 2 else 2.0
+    return q, f
+
+
+def bounded_caps(graph, masks, batch_size: int, quantile: float = 0.99, safety: float = 2.0):
+    """Per-hop capacities from the degree distribution instead of its maximum: a hop over n
+    targets is sized for n times the mean out-degree plus the ``quantile`` tail, times
+    ``safety``, never above the exact bound (:func:`exact_caps`).  On a power-law graph one
+    hub fixes ``max_out_degree`` and makes the exact caps reach the whole edge set by hop 2;
+    these stay proportional to the work a typical batch does.  A batch over them is caught
+    by the overflow flag (:meth:`DeviceFullFlow.grow`, re-capture)."""
+    exact = exact_caps(graph, masks, batch_size)
+    T = graph.num_types
+    seg = (graph.indptr[1:] - graph.indptr[:-1]).view(graph.num_rows, T)
+    caps = []
+    n = int(batch_size)
+    N = graph.num_rows
+    for (ex_e, ex_n), m in zip(exact, masks):
+        sel = torch.tensor([(m >> t) & 1 for t in range(T)], dtype=seg.dtype, device=seg.device)
+        deg = (seg * sel).sum(1).float()
+        mean = float(deg.mean().item()) if deg.numel() else 0.0
+        k = max(1, int(deg.numel() * (1.0 - quantile)))
+        tail = float(torch.topk(deg, min(k, deg.numel())).values.min().item()) if deg.numel() else 0.0
+        e = min(ex_e, _round_up(int(safety * (n * mean + tail)) + 1))
+        n_next = min(ex_n, N, _round_up(n + e))
+        caps.append((int(e), int(n_next)))
+        n = n_next
+    return caps
+
+
 class DeviceFullFlow:
     """``GCNDataFlow`` on the device with fixed shapes.
 
@@ -151,14 +205,10 @@ class DeviceFullFlow:
         self.self_loops = bool(add_self_loops)
         self.L = len(self.masks)
         N = graph.num_rows
-        if caps is None:
-            caps = []
-            n = self.B
-            for m in self.masks:
-                e = min(masked_edges(graph, m), n * max_out_degree(graph, m))
-                n_next = min(N, n + e)
-                caps.append((_round_up(max(e, 1)), _round_up(n_next)))
-                n = n_next
+        if caps is None or caps == "exact":
+            caps = exact_caps(graph, self.masks, self.B)
+        elif isinstance(caps, str) and caps.startswith("bounded"):
+            caps = bounded_caps(graph, self.masks, self.B, *_bounded_args(caps))
         self.caps = [(int(e), int(n)) for e, n in caps]
         self.overflow = torch.zeros(1, dtype=torch.int32, device=graph.device)
 
@@ -233,10 +283,26 @@ class DeviceFullFlow:
             cap_prev = cap_n
         return df
 
+    def overflowed(self) -> bool:
+        """True if any batch since the last :meth:`clear` exceeded a capacity (host sync)"""
+        return int(self.overflow.item()) != 0
+
+    def clear(self):
+        self.overflow.zero_()
+
     def check(self):
         """raise if any batch so far exceeded a capacity (host sync)"""
-        if int(self.overflow.item()) != 0:
+        if self.overflowed():
             raise RuntimeError(f"device dataflow capacity exceeded (caps {self.caps}): raise the caps")
+
+    def grow(self, factor: float = 2.0):
+        """every capacity times ``factor`` (at most the exact bound); returns the new caps.
+        The flow's fixed shapes change, so captured graphs over it must be re-captured."""
+        exact = exact_caps(self.g, self.masks, self.B)
+        self.caps = [(min(ex_e, _round_up(int(e * factor))), min(ex_n, _round_up(int(n * factor))))
+                     for (e, n), (ex_e, ex_n) in zip(self.caps, exact)]
+        self.overflow.zero_()
+        return self.caps
 
     def _filter(self, h, n_id, nbr):
         """hook: the hop's neighbour list with dropped entries set to -1 (None: keep all)"""

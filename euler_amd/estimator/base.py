@@ -65,7 +65,10 @@ def latest_checkpoint(model_dir):
 
 def rank_checkpoint(path, rank):
     """Rank ``rank``'s file of the checkpoint whose rank-0 file is ``path``."""
-    return path if rank == 0 else path.replace(".pt", "-rank%d.pt" % rank)
+    if rank == 0:
+        return path
+    # only the file name's ".pt" suffix: a model_dir such as "/runs/x.pt_exp/" stays intact
+    return re.sub(r"\.pt$", "-rank%d.pt" % rank, path)
 
 
 def id_file_batches(path, batch_size, parse=int, shard=(0, 1)):
@@ -257,7 +260,7 @@ class BaseEstimator:
         ranks, re-sharded for this run's world size: every rank reads all the shard files
         and keeps its ``mod`` rows."""
         base = re.sub(r"-rank\d+\.pt$", ".pt", path)
-        files = [base if r == 0 else base.replace(".pt", "-rank%d.pt" % r) for r in range(saved_world)]
+        files = [rank_checkpoint(base, r) for r in range(saved_world)]
         states = [torch.load(f, map_location="cpu", weights_only=True) for f in files]
         dev = self.device
         for n in names:
@@ -651,7 +654,7 @@ class BaseEstimator:
             return FullFlowTrainer.from_model(model, graph, int(self.params["batch_size"]),
                                               optimizer=self.params.get("optimizer", "adam"),
                                               learning_rate=float(self.params.get("learning_rate", 0.001)),
-                                              caps=self.params.get("device_flow_caps"))
+                                              caps=self.params.get("device_flow_caps", "bounded"))
         if unsup:
             from euler_amd.models.sage_tower import UnsupSageTrainer
 
@@ -728,6 +731,13 @@ class BaseEstimator:
         tr.reset_metric()
         last = {}
         delay = self.params.get("debug_delay_rank")  # test hook: one rank arrives late
+        # capacity-padded device flows (dataflow/device_flow.py): a batch beyond a cap sets
+        # the flow's overflow flag; it is read at every boundary, and a chunk that overflowed
+        # on any rank is rolled back (parameters, optimizer slots, sampler counter) and re-run
+        # with grown caps and re-captured graphs, so no step trains on truncated blocks
+        flow = getattr(tr, "flow", None)
+        guard = flow is not None and callable(getattr(flow, "grow", None))
+        self.flow_regrows = 0
         while self.global_step < total:
             # run up to the next log / checkpoint boundary in one go
             nxt = min(total, (self.global_step // log_steps + 1) * log_steps)
@@ -736,7 +746,25 @@ class BaseEstimator:
             if delay is not None and int(delay) == self.rank:
                 time.sleep(float(self.params.get("debug_delay_s", 2.0)))
                 delay = None
+            snap = self._device_snapshot(tr) if guard else None
             run(nxt - self.global_step)
+            if guard and self._flow_overflowed(flow):
+                self._device_rollback(tr, snap)
+                if self.flow_regrows >= int(self.params.get("max_flow_regrows", 8)):
+                    raise RuntimeError(f"device dataflow capacity exceeded {self.flow_regrows} times "
+                                       f"(caps {flow.caps})")
+                self.flow_regrows += 1
+                old = list(flow.caps)
+                self._device_release(tr)
+                flow.grow(float(self.params.get("flow_grow_factor", 2.0)))
+                log.warning("rank %d: a batch before step %d exceeded the device flow caps %s; rolled the chunk "
+                            "back, caps now %s, re-capturing", self.rank, nxt, old, flow.caps)
+                tr.reset_metric()
+                if use_graph:
+                    self.global_step += self._device_capture(tr, grad_sync, total)
+                    if self._flow_overflowed(flow):  # the capture's own eager warm-up steps
+                        raise RuntimeError(f"device dataflow capacity exceeded during re-capture (caps {flow.caps})")
+                continue
             self.global_step = nxt
             if xar is not None and self._xgmi_failed(xar):
                 # sums since the failed wait are partial: rank 0's state wins, RCCL from here
@@ -773,6 +801,42 @@ class BaseEstimator:
         self._device_release(tr)
         dp.barrier()
         return last
+
+    def _flow_overflowed(self, flow) -> bool:
+        """the flow's overflow flag, agreed over the process group (MAX)"""
+        over = int(flow.overflowed())
+        if self.world > 1:
+            import torch.distributed as dist
+
+            flag = torch.tensor([over], dtype=torch.int32)
+            if dist_backend() == "nccl":
+                flag = flag.to(self.device)
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+            over = int(flag.item())
+        if over:
+            flow.clear()
+        return bool(over)
+
+    @staticmethod
+    def _device_snapshot(tr):
+        """device copies of everything a chunk of steps changes: parameters, optimizer slots
+        and step counter, the sampler's (seed, counter)"""
+        ts = list(tr.dp_state_tensors())
+        rng = getattr(getattr(tr, "rng_source", None), "rng", None)
+        if rng is not None:
+            ts.append(rng)
+        return [(t, t.detach().clone()) for t in ts], getattr(tr, "step_count", None)
+
+    @staticmethod
+    def _device_rollback(tr, snap):
+        pairs, step_count = snap
+        with torch.no_grad():
+            for t, saved in pairs:
+                t.copy_(saved)
+        if step_count is not None:
+            tr.step_count = step_count
+        if callable(getattr(tr, "refresh_shadows", None)):
+            tr.refresh_shadows()
 
     @staticmethod
     def _device_grad_buffer(tr):

@@ -58,6 +58,22 @@ def test_bench_gpus_flag_launches_ranks():
     # plain `python bench.py --gpus 2` (the driver's BENCH invocation) starts 2 ranks itself;
     # --shared-gpu puts both on the one GPU of the box (gloo group, xGMI all-reduce kernel)
     out = _run([sys.executable, "bench.py", "--gpus", "2", "--shared-gpu"] + SMALL)
-    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
+    # a rehearsal is one physical GPU: n_gpus counts devices, "ranks" processes, no vs_baseline
+    assert out["n_gpus"] == 1 and out["ranks"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["vs_baseline"] is None
     assert out["config"]["global_batch"] == 2 * 1024
     assert "xgmi" in out["config"]["grad_sync"] and out["value"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks", [4, 8])
+def test_bench_shared_gpu_rehearsal_many_ranks(ranks):
+    # the whole-node path at the driver's rank counts, every rank on the one GPU of the box:
+    # W-rank xGMI reduce-scatter shard math, per-block flags and epochs inside the captured
+    # step; the loss must fall and stay finite on every rank's replicas
+    out = _run([sys.executable, "bench.py", "--gpus", str(ranks), "--shared-gpu", "--num-nodes", "200000",
+                "--steps", "40", "--warmup", "5"])
+    assert out["ranks"] == ranks and out["config"]["parallelism"] == "dp%d" % ranks
+    assert out["n_gpus"] == 1 and out["vs_baseline"] is None
+    first, last = out["config"]["loss_first_last"]
+    assert last == last and last < first

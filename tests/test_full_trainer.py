@@ -396,3 +396,67 @@ def test_solution_device_path_matches_engine_features_cpu(tmp_path):
     with torch.no_grad():
         want = m.logit_fn(enc._aggregate([eng(h) for h in hops])).float()
     assert torch.allclose(dev, want, atol=1e-5)
+
+
+def test_hop0_cap_holds_a_hub_repeated_among_the_roots_cpu():
+    """hop 0 expands the roots as drawn (repeats kept): a hub drawn B times needs B times
+    its degree, which can exceed the graph's masked edge count; the exact caps cover it"""
+    from euler_amd.dataflow.device_flow import DeviceFullFlow, masked_edges
+
+    _, m, _ = _setup("cpu")
+    g = _device_graph(m, "cpu")
+    masks = _masks(g, m.gnn.sampler)
+    sel = torch.tensor([(masks[0] >> t) & 1 for t in range(g.num_types)])
+    deg = ((g.indptr[1:] - g.indptr[:-1]).view(g.num_rows, g.num_types) * sel).sum(1)
+    hub = int(deg.argmax())
+    B = 64
+    flow = DeviceFullFlow(g, masks, B, add_self_loops=True)
+    assert flow.caps[0][0] >= B * int(deg[hub])
+    flow.produce(torch.full((B,), hub, dtype=torch.long))
+    assert not flow.overflowed()
+
+
+def test_bounded_caps_are_smaller_and_overflow_regrows_cpu(tmp_path):
+    """caps="bounded" sizes hops from the degree distribution; a chunk whose batch exceeds a
+    cap is rolled back and re-run with grown caps: the job finishes with the parameters of
+    a job that never overflowed (same draws, complete blocks)"""
+    from euler_amd.dataflow.device_flow import bounded_caps, exact_caps
+    from euler_amd.tools.runner import main
+
+    _, m, _ = _setup("cpu")
+    g = _device_graph(m, "cpu")
+    masks = _masks(g, m.gnn.sampler)
+    ex, bd = exact_caps(g, masks, 32), bounded_caps(g, masks, 32)
+    assert all(b[0] <= e[0] and b[1] <= e[1] for b, e in zip(bd, ex))
+    assert sum(b[0] for b in bd) < sum(e[0] for e in ex)
+
+    def run(caps, d):
+        import euler_amd.estimator.base as eb
+
+        est_box = {}
+        orig = eb.BaseEstimator._train_device_graph
+
+        def spy(self):
+            est_box["est"] = self
+            if caps is not None:
+                self.params["device_flow_caps"] = caps
+            return orig(self)
+
+        eb.BaseEstimator._train_device_graph = spy
+        torch.manual_seed(0)  # the same initial weights in both jobs
+        try:
+            r = main(["--dataset", "ppi", "--scale", "0.05", "--batch_size", "32", "--log_steps", "4",
+                      "--device", "cpu", "--seed", "1", "--model_dir", str(tmp_path / d), "--device_graph",
+                      "--total_step", "12", "--learning_rate", "0.01"], model="gcn")
+        finally:
+            eb.BaseEstimator._train_device_graph = orig
+        est = est_box["est"]
+        p = est.device_trainer.logical_params()
+        return r, est, torch.cat([p[k].reshape(-1).float() for k in sorted(p)])
+
+    r0, e0, p0 = run("exact", "a")
+    tiny = [(256, 256)] * len(masks)  # every batch of this graph overflows these
+    r1, e1, p1 = run(tiny, "b")
+    assert r1["step"] == 12 and e1.flow_regrows >= 1 and e0.flow_regrows == 0
+    assert all(c[0] > 256 for c in e1.device_trainer.flow.caps)
+    torch.testing.assert_close(p1, p0, rtol=1e-4, atol=1e-5)

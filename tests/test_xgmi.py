@@ -1,9 +1,9 @@
 """xGMI two-shot all-reduce (csrc/hip/xgmi_ar.hip, parallel/xgmi.py).
 
-Two processes share the box's one GPU: each maps the other's IPC buffer exactly as ranks on
-different GPUs of a node do, so the protocol (staging, per-block flags, epochs across calls
-and hipGraph replays, shard arithmetic for W = 2) runs for real; only the xGMI transport is
-replaced by local HBM.  Results are compared with an fp32 sum of every rank's input
+W = 2, 4 and 8 processes share the box's one GPU: each maps the others' IPC buffers exactly
+as ranks on different GPUs of a node do, so the protocol (staging, per-block flags, epochs
+across calls and hipGraph replays, shard arithmetic for the driver's rank counts) runs for
+real; only the xGMI transport is replaced by local HBM.  Results are compared with an fp32 sum of every rank's input
 gathered over gloo.
 """
 import os
@@ -111,20 +111,20 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.gpu
-def test_xgmi_allreduce_two_ranks_one_gpu():
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_xgmi_allreduce_ranks_one_gpu(world):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    world = 2
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     out = {}
     try:
         for _ in range(world):
-            r, res = q.get(timeout=100)
+            r, res = q.get(timeout=60 + 20 * world)
             out[r] = res
     finally:
         for p in procs:
