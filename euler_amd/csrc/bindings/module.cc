@@ -599,6 +599,12 @@ class PySagePipeline {
     for (auto a : ints) ip.push_back(reinterpret_cast<int64_t*>(a));
     for (auto a : floats) fp.push_back(reinterpret_cast<float*>(a));
     QueryProxy* q = e_->Proxy();
+    if (q->mode() == "graph_partition") {
+      // keyed root draws assume bucket (id % B) lives on shard (bucket % P) % S, which only an
+      // id-hash partition guarantees; an arbitrary partition_fn would bias the roots
+      throw std::invalid_argument("the native pipeline's keyed remote sampling needs an id-hash partition; "
+                                  "graph_partition sessions train on the per-op engine path");
+    }
     if (q->mode() == "remote" || q->mode() == "local_sharded") {
       // the graph lives on shard servers (or in-process shards): batches through the
       // distribute-mode GQL plans (pipeline.h RemoteSource)

@@ -9,7 +9,9 @@
 // labels — straight into caller-provided (pinned) slot buffers of fixed capacity.  Slots
 // circulate free -> filling -> ready -> consumer -> free; batches are delivered in sequence
 // order and batch b draws from the Philox keys KeyedKey(seed, b, hop) (graph.h), so the
-// stream of batches is reproducible for any worker count and any graph placement.
+// stream of batches is reproducible for any worker count and for the in-process graph or
+// any id-hash sharding of it (keyed root draws assume bucket id % B lives on shard
+// (bucket % P) % S; graph_partition sessions with an arbitrary partition_fn are refused).
 #pragma once
 
 #include <stdint.h>

@@ -80,7 +80,10 @@ class NativeSageLoader:
         eng = get_engine()
         self.mode = eng.meta()["mode"]
         if self.mode not in ("local", "remote", "local_sharded"):
-            raise ValueError("the native pipeline serves local, local_sharded and remote sessions")
+            # graph_partition: the keyed root draw assumes bucket (id % B) lives on shard
+            # (bucket % P) % S, which holds only for id-hash partitions (csrc/graph/keyed.cc)
+            raise ValueError("the native pipeline serves local, local_sharded and remote sessions "
+                             "(id-hash partitions); %s sessions train on the per-op engine path" % self.mode)
         self.device = torch.device(device)
         self.cuda = self.device.type == "cuda"
         self.B = int(batch_size)

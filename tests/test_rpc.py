@@ -598,6 +598,12 @@ def test_graph_partition_mode_routes_by_ownership():
         # a 2-hop query: every hop is routed by ownership
         assert [x.tolist() for x in ea.run_gql(q, q_in, q_out)] == want
         assert "GP_ID_SPLIT" in ea.explain_gql(q)
+        # the native pipeline's keyed root draws assume id-hash placement: refused here
+        from euler_amd.dataflow.dataflows import SageDataFlow
+        from euler_amd.dataflow.native_loader import NativeSageLoader
+
+        with pytest.raises(ValueError, match="id-hash"):
+            NativeSageLoader(SageDataFlow([2, 2], [["0", "1"], ["0", "1"]]), ["f3"], [2], "", 0, 4, -1, "cpu")
         # the same cluster through hash routing: ids land on shards that do not hold them
         ea.initialize_graph({"mode": "remote", "registry": reg, "shard_num": 2, "num_retries": 2})
         f3h = ea.get_dense_feature([1, 2, 3, 4, 5, 6], ["f3"], [2])[0].numpy()[:, 0]

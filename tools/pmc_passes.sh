@@ -14,7 +14,7 @@ PASSES=${PASSES:-"FETCH_SIZE|WRITE_SIZE|SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE
 IFS='|' read -ra PL <<< "$PASSES"
 for pass in "${PL[@]}"; do
   tag=$(echo "$pass" | tr ' ' '+')
-  timeout -s KILL 180 rocprofv3 --pmc $pass --output-format csv -d "$OUT/$tag" -o run -- python3 "$@" \
+  timeout -s KILL 180 rocprofv3 --pmc $pass --output-format csv -d "$OUT/$tag" -o run -- python3 "$REPO/$1" "${@:2}" \
     > "$OUT/$tag.log" 2>&1 || { echo "pass $pass failed rc=$?"; tail -5 "$OUT/$tag.log"; exit 1; }
   echo "pass $pass ok"
 done
