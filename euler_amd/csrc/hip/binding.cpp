@@ -570,10 +570,13 @@ class XgmiAr : public std::enable_shared_from_this<XgmiAr> {
 void register_gnn_ops(pybind11::module& m);
 // binding_tree.cpp: fused GraphSAGE tree-step plan
 void register_tree_ops(pybind11::module& m);
+// binding_gcn.cpp: fused GCN step plan
+void register_gcn_ops(pybind11::module& m);
 
 PYBIND11_MODULE(_hip_ops, m) {
   register_gnn_ops(m);
   register_tree_ops(m);
+  register_gcn_ops(m);
   m.doc() = "euler_amd hand-written CDNA4 (gfx950) HIP kernels";
   m.attr("arch") = "gfx950";
   m.def("rng_advance", &rng_advance);

@@ -418,259 +418,13 @@ class BaseEstimator:
 
     def _device_graph_trainer(self, first):
         """Upload the engine's graph (structure, the model's feature and label columns) to
-        HBM and build the device trainer for ``self.model``: SupervisedGraphSage (fused
-        kernels), UnsupervisedGraphSage, the full-neighbourhood zoo, or a TransX-family
-        knowledge-graph model (triple table + corruption sampler)."""
-        import euler_amd.ops.graph_api as ge
-        from euler_amd.graph.device_graph import DeviceGraph
-        from euler_amd.models.sage_trainer import SageTrainer
+        HBM and build the device trainer for ``self.model``: the first entry of
+        ``estimator/device_trainers.py`` REGISTRY that accepts it (fused GraphSAGE, the
+        full-neighbourhood zoo, TransX, DeepWalk / LINE, GAE, DGI, R-GCN, the solution API,
+        graph classification, ...)."""
+        from euler_amd.estimator.device_trainers import build_device_trainer
 
-        from euler_amd.dataflow.dataflows import GCNDataFlow
-
-        model = self.model
-        seed = int(self.params.get("seed") or 0)
-        if hasattr(model, "loss_scores"):
-            # TransE / TransH / TransR / TransD / DistMult (EdgeEstimator): the triple table and
-            # the corruption sampler in HBM, the model's own scores (models/kg_trainer.py)
-            from euler_amd.models.kg_trainer import KGTrainer
-
-            self._prepare(first)
-            if self._sync is not None:
-                self._sync.remove()  # the trainer all-reduces its flat gradient itself
-            edge_type = self.params.get("train_edge_type", getattr(model, "edge_type", -1))
-            return KGTrainer.from_model(model, int(self.params["batch_size"]), edge_type, seed=seed * 7919 + self.rank,
-                                        device=self.device, optimizer=self.params.get("optimizer", "adam"),
-                                        learning_rate=float(self.params.get("learning_rate", 0.001)))
-        from euler_amd.models.unsupervised import BaseNode2Vec, GraphAutoEncoder, Line, VariationalGraphAutoEncoder
-        from euler_amd.mp_utils.models import GraphModel
-
-        if isinstance(model, GraphModel) and hasattr(model, "pool") and hasattr(getattr(model, "gnn", None),
-                                                                                 "encoder"):
-            # graph classification (GraphEstimator): graphs' node lists, labels and sparse
-            # feature ids in HBM, the induced blocks built on the device (models/graph_trainer.py)
-            from euler_amd.models.graph_trainer import GraphTrainer
-
-            self._prepare(first)
-            if self._sync is not None:
-                self._sync.remove()
-            graph = DeviceGraph.from_engine(seed=seed * 7919 + self.rank, device=self.device)
-            return GraphTrainer(model, graph, int(self.params["batch_size"]), _first_name(self.params["label"]),
-                                int(self.params["num_classes"]), optimizer=self.params.get("optimizer", "adam"),
-                                learning_rate=float(self.params.get("learning_rate", 0.001)))
-        if isinstance(model, (GraphAutoEncoder, VariationalGraphAutoEncoder)):
-            # GAE / VGAE (sage / gcn encoder): roots, positives, negatives and the encoder's
-            # blocks on the HBM graph (models/gae_trainer.py)
-            from euler_amd.models.gae_trainer import GaeTrainer, VgaeTrainer
-
-            self._prepare(first)
-            if self._sync is not None:
-                self._sync.remove()
-            gnn = model.gnn
-            nt = self.params.get("train_node_type", model.node_type)
-            node_type = -1 if nt in (None, -1, "-1") else int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
-            fdt = torch.float32 if self.params.get("device_feature_dtype", "bf16") == "fp32" else torch.bfloat16
-            graph = DeviceGraph.from_engine(node_type=node_type, features=gnn.feature_idx,
-                                            feature_dims=gnn.feature_dim, feature_dtype=fdt,
-                                            seed=seed * 7919 + self.rank, device=self.device)
-            cls = VgaeTrainer if isinstance(model, VariationalGraphAutoEncoder) else GaeTrainer
-            return cls(model, graph, int(self.params["batch_size"]),
-                              optimizer=self.params.get("optimizer", "adam"),
-                              learning_rate=float(self.params.get("learning_rate", 0.001)))
-        if isinstance(model, Line) and model._target_encoder is model._context_encoder:
-            # first-order LINE: one id table in both roles, autograd over the model's own
-            # lookups (models/line_trainer.py)
-            from euler_amd.models.line_trainer import IdPairTrainer
-
-            self._prepare(first)
-            if self._sync is not None:
-                self._sync.remove()
-            nt = self.params.get("train_node_type", model.node_type)
-            node_type = -1 if nt in (None, -1, "-1") else int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
-            graph = DeviceGraph.from_engine(node_type=node_type, seed=seed * 7919 + self.rank, device=self.device)
-            return IdPairTrainer(model, graph, int(self.params["batch_size"]),
-                                 optimizer=self.params.get("optimizer", "adam"),
-                                 learning_rate=float(self.params.get("learning_rate", 0.001)))
-        if isinstance(model, (BaseNode2Vec, Line)):
-            # DeepWalk / Node2Vec / LINE (second order): walks, pairs, negatives and the
-            # row-sparse SGNS update on the HBM graph (models/deepwalk_step.py)
-            from euler_amd.models.deepwalk_step import DeepWalkEstimatorTrainer
-
-            if self.world > 1:
-                raise ValueError("the DeepWalk device path of the estimator runs on one rank "
-                                 "(the row-sharded multi-rank table: benchmarks/bench_deepwalk.py)")
-            self._prepare(first)
-            nt = self.params.get("train_node_type", model.node_type)
-            node_type = -1 if nt in (None, -1, "-1") else int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
-            graph = DeviceGraph.from_engine(node_type=node_type, seed=seed * 7919 + self.rank, device=self.device)
-            return DeepWalkEstimatorTrainer(model, graph, int(self.params["batch_size"]),
-                                            optimizer=self.params.get("optimizer", "adam"),
-                                            learning_rate=float(self.params.get("learning_rate", 0.001)),
-                                            seed=seed)
-        from euler_amd.models.unsupervised import DGI
-
-        if isinstance(model, DGI):
-            # Deep Graph Infomax: roots, the fan-out tree and its shuffled view on the HBM
-            # graph, the user's aggregators and discriminator (models/dgi_trainer.py)
-            from euler_amd.models.dgi_trainer import DgiTrainer
-
-            self._prepare(first)
-            if self._sync is not None:
-                self._sync.remove()
-            ne = model._target_encoder._node_encoder
-            nt = self.params.get("train_node_type", model.node_type)
-            node_type = -1 if nt in (None, -1, "-1") else int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
-            fdt = torch.float32 if self.params.get("device_feature_dtype", "bf16") == "fp32" else torch.bfloat16
-            graph = DeviceGraph.from_engine(node_type=node_type, features=ne.feature_idx if ne.use_feature else (),
-                                            feature_dims=ne.feature_dim if ne.use_feature else (),
-                                            feature_dtype=fdt, seed=seed * 7919 + self.rank, device=self.device)
-            return DgiTrainer(model, graph, int(self.params["batch_size"]),
-                              optimizer=self.params.get("optimizer", "adam"),
-                              learning_rate=float(self.params.get("learning_rate", 0.001)))
-        from euler_amd import solution as S
-        from euler_amd.models.unsupervised import UnsupervisedRGCN
-        from euler_amd.utils.encoders import GCNEncoder, LGCEncoder
-
-        if isinstance(model, UnsupervisedRGCN):
-            # R-GCN over id embeddings: relation blocks (relations from the edge feature, read
-            # once) and the model's own layers on the HBM graph (models/rgcn_trainer.py)
-            from euler_amd.models.rgcn_trainer import UnsupRgcnTrainer
-
-            self._prepare(first)
-            if self._sync is not None:
-                self._sync.remove()
-            nt = self.params.get("train_node_type", model.node_type)
-            node_type = -1 if nt in (None, -1, "-1") else int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
-            graph = DeviceGraph.from_engine(node_type=node_type, seed=seed * 7919 + self.rank, device=self.device)
-            return UnsupRgcnTrainer(model, graph, int(self.params["batch_size"]),
-                                    optimizer=self.params.get("optimizer", "adam"),
-                                    learning_rate=float(self.params.get("learning_rate", 0.001)))
-
-        if isinstance(model, S.UnsuperviseSolution):
-            from euler_amd.models.encoder_trainer import UnsupSolutionTrainer
-
-            self._prepare(first)
-            if self._sync is not None:
-                self._sync.remove()
-            ne = getattr(model.target_encoder, "_node_encoder", None)
-            if ne is None or not getattr(ne, "use_feature", False):
-                raise ValueError("device_graph=True trains UnsuperviseSolution over dense-feature SageEncoders")
-            nt = self.params.get("train_node_type", -1)
-            node_type = -1 if nt in (None, -1, "-1") else int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
-            fdt = torch.float32 if self.params.get("device_feature_dtype", "bf16") == "fp32" else torch.bfloat16
-            graph = DeviceGraph.from_engine(node_type=node_type, features=ne.feature_idx, feature_dims=ne.feature_dim,
-                                            feature_dtype=fdt, seed=seed * 7919 + self.rank, device=self.device)
-            return UnsupSolutionTrainer(model, graph, int(self.params["batch_size"]),
-                                        optimizer=self.params.get("optimizer", "adam"),
-                                        learning_rate=float(self.params.get("learning_rate", 0.001)))
-        if isinstance(model, S.SuperviseSolution):
-            # the solution API over a SageEncoder: tree draws, features and the encoder's
-            # aggregators on the HBM graph (models/encoder_trainer.py SolutionTrainer)
-            from euler_amd.models.encoder_trainer import SolutionTrainer
-
-            self._prepare(first)
-            if self._sync is not None:
-                self._sync.remove()
-            ne = getattr(model.encoder, "_node_encoder", None)
-            lab = model.get_label_fn
-            if ne is None or not getattr(ne, "use_feature", False) or not hasattr(lab, "label_idx"):
-                raise ValueError("device_graph=True trains SuperviseSolution over a dense-feature SageEncoder "
-                                 "with GetLabelFromFea labels")
-            nt = self.params.get("train_node_type", -1)
-            node_type = -1 if nt in (None, -1, "-1") else int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
-            fdt = torch.float32 if self.params.get("device_feature_dtype", "bf16") == "fp32" else torch.bfloat16
-            graph = DeviceGraph.from_engine(node_type=node_type, features=ne.feature_idx, feature_dims=ne.feature_dim,
-                                            label=lab.label_idx, label_dim=lab.label_dim, feature_dtype=fdt,
-                                            seed=seed * 7919 + self.rank, device=self.device)
-            return SolutionTrainer.from_model(model, graph, int(self.params["batch_size"]),
-                                              optimizer=self.params.get("optimizer", "adam"),
-                                              learning_rate=float(self.params.get("learning_rate", 0.001)))
-
-        if isinstance(getattr(model, "_encoder", None), LGCEncoder) and hasattr(model, "label_idx"):
-            # LGCN: neighbour draws and feature gathers on the HBM graph, the model's own
-            # top-k + 1-D convolutions (models/encoder_trainer.py LgcnTrainer)
-            from euler_amd.models.encoder_trainer import LgcnTrainer
-
-            self._prepare(first)
-            if self._sync is not None:
-                self._sync.remove()
-            enc = model._encoder
-            nt = self.params.get("train_node_type", -1)
-            node_type = -1 if nt in (None, -1, "-1") else int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
-            fdt = torch.float32 if self.params.get("device_feature_dtype", "bf16") == "fp32" else torch.bfloat16
-            graph = DeviceGraph.from_engine(node_type=node_type, features=[enc.feature_idx],
-                                            feature_dims=[enc.feature_dim], label=model.label_idx,
-                                            label_dim=model.label_dim, feature_dtype=fdt,
-                                            seed=seed * 7919 + self.rank, device=self.device)
-            return LgcnTrainer.from_model(model, graph, int(self.params["batch_size"]),
-                                          optimizer=self.params.get("optimizer", "adam"),
-                                          learning_rate=float(self.params.get("learning_rate", 0.001)))
-        if isinstance(getattr(model, "_encoder", None), GCNEncoder) and hasattr(model, "label_idx"):
-            # GeniePath and other full-neighbour encoder models: hop sets and adjacencies
-            # built on the device, the model's own encode (models/encoder_trainer.py)
-            from euler_amd.models.encoder_trainer import EncoderFlowTrainer
-
-            self._prepare(first)
-            if self._sync is not None:
-                self._sync.remove()
-            ne = model._encoder._node_encoder
-            nt = self.params.get("train_node_type", -1)
-            node_type = -1 if nt in (None, -1, "-1") else int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
-            fdt = torch.float32 if self.params.get("device_feature_dtype", "bf16") == "fp32" else torch.bfloat16
-            graph = DeviceGraph.from_engine(node_type=node_type, features=ne.feature_idx if ne.use_feature else (),
-                                            feature_dims=ne.feature_dim if ne.use_feature else (),
-                                            label=model.label_idx, label_dim=model.label_dim, feature_dtype=fdt,
-                                            seed=seed * 7919 + self.rank, device=self.device)
-            return EncoderFlowTrainer.from_model(model, graph, int(self.params["batch_size"]),
-                                                 optimizer=self.params.get("optimizer", "adam"),
-                                                 learning_rate=float(self.params.get("learning_rate", 0.001)))
-        gnn = getattr(model, "gnn", None)
-        unsup = hasattr(model, "context_gnn")
-        if gnn is None or not hasattr(gnn, "feature_idx") or not (unsup or hasattr(model, "label_idx")):
-            raise ValueError("device_graph=True trains SupervisedGraphSage / UnsupervisedGraphSage-style models "
-                             "and the full-neighbourhood zoo (gnn.feature_idx + label_idx, or a context_gnn)")
-        self._prepare(first)  # materialise the lazy layers, broadcast rank 0's weights
-        nt = self.params.get("train_node_type", -1)
-        node_type = -1 if nt in (None, -1, "-1") else int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
-        fdt = torch.float32 if self.params.get("device_feature_dtype", "bf16") == "fp32" else torch.bfloat16
-        from euler_amd.convolution.convs import SAGEConv
-        from euler_amd.dataflow.dataflows import SageDataFlow
-
-        sampled_other = isinstance(getattr(gnn, "sampler", None), SageDataFlow) and not unsup and \
-            not all(isinstance(c, SAGEConv) for c in gnn.convs)
-        from euler_amd.dataflow.dataflows import FastGCNDataFlow, LayerwiseDataFlow
-
-        layer_sampled = isinstance(getattr(gnn, "sampler", None), (FastGCNDataFlow, LayerwiseDataFlow))
-        if isinstance(getattr(gnn, "sampler", None), GCNDataFlow) or sampled_other or layer_sampled:
-            # GCN / APPNP / SGCN / TAGCN / ... : full-neighbourhood blocks built on the device;
-            # other convolutions on the sampled flow: fixed-fanout blocks built on the device
-            from euler_amd.models.full_trainer import FullFlowTrainer
-
-            if self._sync is not None:
-                self._sync.remove()  # the trainer all-reduces its flat gradient itself
-            graph = DeviceGraph.from_engine(node_type=node_type, features=gnn.feature_idx,
-                                            feature_dims=gnn.feature_dim, label=model.label_idx,
-                                            label_dim=model.label_dim, feature_dtype=fdt,
-                                            seed=seed * 7919 + self.rank, device=self.device)
-            return FullFlowTrainer.from_model(model, graph, int(self.params["batch_size"]),
-                                              optimizer=self.params.get("optimizer", "adam"),
-                                              learning_rate=float(self.params.get("learning_rate", 0.001)),
-                                              caps=self.params.get("device_flow_caps", "bounded"))
-        if unsup:
-            from euler_amd.models.sage_tower import UnsupSageTrainer
-
-            graph = DeviceGraph.from_engine(node_type=node_type, features=gnn.feature_idx,
-                                            feature_dims=gnn.feature_dim, feature_dtype=fdt,
-                                            seed=seed * 7919 + self.rank, device=self.device)
-            return UnsupSageTrainer.from_model(model, graph, int(self.params["batch_size"]),
-                                               optimizer=self.params.get("optimizer", "adam"),
-                                               learning_rate=float(self.params.get("learning_rate", 0.001)))
-        graph = DeviceGraph.from_engine(node_type=node_type, features=gnn.feature_idx, feature_dims=gnn.feature_dim,
-                                        label=model.label_idx, label_dim=model.label_dim, feature_dtype=fdt,
-                                        seed=seed * 7919 + self.rank, device=self.device)
-        return SageTrainer.from_model(model, graph, int(self.params["batch_size"]),
-                                      optimizer=self.params.get("optimizer", "adam"),
-                                      learning_rate=float(self.params.get("learning_rate", 0.001)),
-                                      keep_samples=False)
+        return build_device_trainer(self, self.model, first)
 
     def _train_device_graph(self):
         """NodeEstimator.train() on the device path: the whole mini-batch pipeline
@@ -749,21 +503,24 @@ class BaseEstimator:
             snap = self._device_snapshot(tr) if guard else None
             run(nxt - self.global_step)
             if guard and self._flow_overflowed(flow):
-                self._device_rollback(tr, snap)
-                if self.flow_regrows >= int(self.params.get("max_flow_regrows", 8)):
-                    raise RuntimeError(f"device dataflow capacity exceeded {self.flow_regrows} times "
-                                       f"(caps {flow.caps})")
-                self.flow_regrows += 1
-                old = list(flow.caps)
-                self._device_release(tr)
-                flow.grow(float(self.params.get("flow_grow_factor", 2.0)))
-                log.warning("rank %d: a batch before step %d exceeded the device flow caps %s; rolled the chunk "
-                            "back, caps now %s, re-capturing", self.rank, nxt, old, flow.caps)
-                tr.reset_metric()
-                if use_graph:
-                    self.global_step += self._device_capture(tr, grad_sync, total)
-                    if self._flow_overflowed(flow):  # the capture's own eager warm-up steps
-                        raise RuntimeError(f"device dataflow capacity exceeded during re-capture (caps {flow.caps})")
+                while True:
+                    self._device_rollback(tr, snap)
+                    if self.flow_regrows >= int(self.params.get("max_flow_regrows", 8)):
+                        raise RuntimeError(f"device dataflow capacity exceeded {self.flow_regrows} times "
+                                           f"(caps {flow.caps})")
+                    self.flow_regrows += 1
+                    old = list(flow.caps)
+                    self._device_release(tr)
+                    flow.grow(float(self.params.get("flow_grow_factor", 2.0)))
+                    log.warning("rank %d: a batch before step %d exceeded the device flow caps %s; rolled the "
+                                "chunk back, caps now %s, re-capturing", self.rank, nxt, old, flow.caps)
+                    tr.reset_metric()
+                    if not use_graph:
+                        break
+                    warm = self._device_capture(tr, grad_sync, total)
+                    if not self._flow_overflowed(flow):  # the capture's own eager warm-up steps fit
+                        self.global_step += warm
+                        break
                 continue
             self.global_step = nxt
             if xar is not None and self._xgmi_failed(xar):

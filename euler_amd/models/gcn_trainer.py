@@ -1,0 +1,228 @@
+"""Fused device-path training step for SupervisedGCN-shaped models (GCN over the
+full-neighbourhood flow): one fixed sequence of hand-written gfx950 launches per step
+(``csrc/hip/gcn.hip``, plan ``csrc/hip/binding_gcn.cpp``), captured in hipGraphs like every
+other device trainer.
+
+Reference model: ``examples/gcn/gcn.py:52-58`` — ``GNN('gcn', 'full', dims)`` over
+``tf_euler/python/dataflow/gcn_dataflow.py:26-48`` (every hop's full neighbourhood, unique,
+self loops), ``convolution/gcn_conv.py:26-54`` (``fc(sum_e deg_t^-1/2 deg_s^-1/2 x_s)``),
+ReLU after each conv, ``fc`` + ``out_fc`` and the sigmoid cross-entropy of
+``mp_utils/base.py:24-47``.
+
+What one step launches (L = 2 convs; 1 + 3 L + 4 + the optimizer = 12):
+
+* the root draw (alias table, Philox stream 1 of the graph's (seed, counter));
+* per hop: expand (degrees, look-back scan, neighbour list, first-occurrence claims),
+  mark (positions of the new nodes), place (edge sources, in-block source counts);
+* the outer conv: edge-parallel aggregation + MFMA linear + ReLU;
+* the head: last conv, fc, out_fc, loss, F1 counts and the whole row-local backward, the
+  weight-gradient partials of its rows and the scatter of d(h1);
+* d(W0) partials; the reduce into the flat gradient (+ loss, counts, RNG counter);
+* the flat optimizer (``parallel/flat.py``), after the data-parallel all-reduce.
+
+The generic path (``models/full_trainer.py``) runs the user's convolution modules on
+``DeviceFullFlow`` blocks: ~100 launches per step.  Both draw the same roots from the same
+graph RNG state and build the same node sets (in a different order: here each set is the
+previous one followed by its new neighbours), so their losses agree to bf16 rounding;
+``tests/test_gcn_trainer.py`` checks that and an fp32 oracle.
+
+Capacities: the flow's edge / node-set caps come from ``dataflow/device_flow.py``
+(``"bounded"`` by default through the estimator); a batch beyond them sets the overflow
+word, and the estimator rolls the chunk back, grows the caps and re-plans.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from euler_amd.dataflow.device_flow import bounded_caps, exact_caps, _bounded_args, _round_up
+from euler_amd.models.captured import CapturedTrainer
+from euler_amd.ops._native import hip
+
+__all__ = ["GcnTrainer", "GcnFlowCaps"]
+
+
+class GcnFlowCaps:
+    """Per-hop (edge, node-set) capacities of the fused GCN flow and its overflow word
+    (the DeviceFullFlow capacity API the estimator's regrow loop uses)."""
+
+    def __init__(self, graph, masks, batch_size, caps="bounded"):
+        self.g = graph
+        self.masks = [int(m) for m in masks]
+        self.B = int(batch_size)
+        if caps is None or caps == "exact":
+            caps = exact_caps(graph, self.masks, self.B)
+        elif isinstance(caps, str) and caps.startswith("bounded"):
+            caps = bounded_caps(graph, self.masks, self.B, *_bounded_args(caps))
+        self.caps = [(int(e), int(n)) for e, n in caps]
+        self.overflow = torch.zeros(1, dtype=torch.int32, device=graph.device)
+
+    def overflowed(self) -> bool:
+        return int(self.overflow.item()) != 0
+
+    def clear(self):
+        self.overflow.zero_()
+
+    def check(self):
+        if self.overflowed():
+            raise RuntimeError(f"fused GCN flow capacity exceeded (caps {self.caps})")
+
+    def grow(self, factor: float = 2.0):
+        exact = exact_caps(self.g, self.masks, self.B)
+        self.caps = [(min(ex_e, _round_up(int(e * factor))), min(ex_n, _round_up(int(n * factor))))
+                     for (e, n), (ex_e, ex_n) in zip(self.caps, exact)]
+        self.overflow.zero_()
+        return self.caps
+
+
+def _gcn_shape(model):
+    """(convs, D, widths, E, C) of a SupervisedGCN-shaped model, or None"""
+    from euler_amd.convolution.convs import GCNConv
+    from euler_amd.dataflow.dataflows import GCNDataFlow
+
+    gnn = getattr(model, "gnn", None)
+    if gnn is None or not isinstance(getattr(gnn, "sampler", None), GCNDataFlow):
+        return None
+    convs = list(getattr(gnn, "convs", []))
+    if not 1 <= len(convs) <= 2 or not all(type(c) is GCNConv for c in convs):
+        return None
+    from euler_amd.mp_utils.models import BaseGNNNet
+
+    if type(gnn).forward is not BaseGNNNet.forward or type(gnn).calculate_conv is not BaseGNNNet.calculate_conv:
+        return None  # e.g. JKGNNNet: another layer combination
+    if any(getattr(l, "activation", None) is not None for l in [c.fc for c in convs] + [gnn.fc, model.out_fc]):
+        return None
+    if any(getattr(c.fc, "bias", None) is not None for c in convs):
+        return None
+    if getattr(model.out_fc, "bias", None) is not None or getattr(gnn.fc, "bias", None) is None:
+        return None
+    return convs
+
+
+class GcnTrainer(CapturedTrainer):
+    metric_name = "f1"
+
+    def __init__(self, model, graph, batch_size, masks, caps="bounded", optimizer="adam", learning_rate=0.01):
+        if graph.device.type != "cuda":
+            raise ValueError("the fused GCN step runs on the GPU (the generic FullFlowTrainer covers the CPU)")
+        self.gnn = model.gnn
+        self.graph = graph
+        self.B = int(batch_size)
+        if graph.features is None or graph.labels is None:
+            raise ValueError("the device graph needs dense features and labels (DeviceGraph.from_engine)")
+        feats = graph.features
+        self.D = int(feats.shape[1])
+        dp = _round_up(self.D, 32)
+        if dp != self.D or not feats.is_contiguous():  # rows padded for 16-byte loads
+            padded = torch.zeros((feats.shape[0], dp), dtype=feats.dtype, device=feats.device)
+            padded[:, : self.D] = feats
+            feats = padded
+        self.features = feats
+        self.labels = graph.labels.to(graph.device).float().contiguous()
+        self.flow = GcnFlowCaps(graph, masks, self.B, caps)
+        self.masks = list(masks)
+        self.counts = torch.zeros(3, dtype=torch.int64, device=graph.device)
+        self._stamp = torch.zeros(1, dtype=torch.int32, device=graph.device)
+        super().__init__(model, graph, graph.device, optimizer, learning_rate)
+        self.plan = None
+        self._plan_caps = None
+        self._build_plan()
+
+    # ------------------------------------------------------------------ construction
+    @staticmethod
+    def supports(model, graph=None) -> bool:
+        """SupervisedGCN-shaped: 1-2 bias-free GCNConvs on GCNDataFlow with self loops, fc with
+        bias, out_fc without; conv widths <= 64, inputs <= 128, fc / label widths <= 128"""
+        if os.environ.get("EULER_AMD_GCN_FUSED", "1") == "0":
+            return False
+        convs = _gcn_shape(model)
+        if convs is None:
+            return False
+        try:
+            widths = [int(c.fc.weight.shape[0]) for c in convs]
+            ins = [int(c.fc.weight.shape[1]) for c in convs]
+            E = int(model.gnn.fc.weight.shape[0])
+            C = int(model.out_fc.weight.shape[0])
+        except (AttributeError, ValueError, RuntimeError):
+            return False  # lazy layers not materialised
+        if graph is not None and (graph.labels is None or graph.features is None or graph.device.type != "cuda"):
+            return False
+        return (max(widths) <= 64 and max(ins) <= 128 and _round_up(E, 32) <= 128 and _round_up(C, 32) <= 128)
+
+    @classmethod
+    def from_model(cls, model, graph, batch_size, optimizer="adam", learning_rate=0.01, caps="bounded"):
+        import euler_amd.ops.graph_api as ge
+
+        ets = []
+        for m in model.gnn.sampler.metapath:
+            ids = None if m is None else [int(t) for t in np.asarray(ge.get_edge_type_id(m)).reshape(-1)]
+            ets.append(None if ids is None or any(t < 0 for t in ids) else ids)
+        return cls(model, graph, batch_size, [graph._mask(e) for e in ets], caps=caps, optimizer=optimizer,
+                   learning_rate=learning_rate)
+
+    def _build_plan(self):
+        m = self.model
+        convs = list(self.gnn.convs)
+        L = len(convs)
+        if len(self.masks) != L:
+            raise ValueError("one metapath entry per GCN layer")
+        g = self.graph
+        w = [c.fc.weight for c in convs]
+        d = {"L": L, "B": self.B, "self_loops": int(bool(self.gnn.sampler.add_self_loops)), "indptr": g.indptr, "nbr": g.nbr, "num_types": g.num_types,
+             "masks": [int(x) & 0xFFFFFFFF for x in self.masks],
+             "cap_e": [e for e, _ in self.flow.caps], "cap_n": [n for _, n in self.flow.caps],
+             "node_prob": g.node_prob, "node_alias": g.node_alias, "root_rows": g.root_rows, "rng": g.rng,
+             "stamp": self._stamp, "overflow": self.flow.overflow,
+             "features": self.features, "labels": self.labels, "D": self.D,
+             "H0": int(w[0].shape[0]), "E": int(self.gnn.fc.weight.shape[0]), "C": int(m.out_fc.weight.shape[0]),
+             "w0": w[0].detach(), "g_w0": w[0].grad,
+             "wfc": self.gnn.fc.weight.detach(), "g_wfc": self.gnn.fc.weight.grad,
+             "bfc": self.gnn.fc.bias.detach(), "g_bfc": self.gnn.fc.bias.grad,
+             "wout": m.out_fc.weight.detach(), "g_wout": m.out_fc.weight.grad,
+             "loss_out": self.loss_out, "counts": self.counts}
+        if L == 2:
+            d.update({"H1": int(w[1].shape[0]), "w1": w[1].detach(), "g_w1": w[1].grad})
+        self.plan = hip().GcnPlan(d)
+        self._plan_caps = list(self.flow.caps)
+
+    # ------------------------------------------------------------------ step
+    def _step(self, grad_sync=None):
+        if self._plan_caps != self.flow.caps:  # grown after an overflow: new fixed shapes
+            self._build_plan()
+        self.plan.step()
+        scale = 1.0
+        if grad_sync is not None:
+            s = grad_sync(self.flat.grad)
+            scale = 1.0 if s is None else float(s)
+        self.opt.step(scale)
+        return self.loss_out
+
+    def capture(self, grad_sync=None, warmup: int = 2, steps: int = 1, extra_sizes=()):
+        if self._plan_caps != self.flow.caps:
+            self._build_plan()
+        return super().capture(grad_sync, warmup, steps, extra_sizes)
+
+    @property
+    def launches_per_step(self) -> int:
+        return int(self.plan.launches) + 1  # + the flat optimizer
+
+    # ------------------------------------------------------------------ metric
+    def metric(self) -> float:
+        tp, fp, fn = self.counts.tolist()
+        return 2.0 * tp / max(2.0 * tp + fp + fn, 1e-12)
+
+    def reset_metric(self):
+        self.counts.zero_()
+
+    def samples(self):
+        return (self.plan.flow()["roots"],)
+
+    # ------------------------------------------------------------------ oracle
+    def forward_backward_only(self):
+        """plan step without the optimizer (tests): loss_out and the flat gradient"""
+        if self._plan_caps != self.flow.caps:
+            self._build_plan()
+        self.plan.step()
+        return self.loss_out

@@ -1,0 +1,175 @@
+"""Fused GCN training step (csrc/hip/gcn.hip, models/gcn_trainer.py).
+
+GPU: on the same roots, the fused step's loss and every parameter gradient equal the
+generic device path's fp32 autograd over the user's GCNConv modules (DeviceFullFlow blocks,
+fp32 feature table) — with and without self loops, 1 and 2 layers; its node sets equal the
+generic flow's; hipGraph replay equals eager; the estimator routes SupervisedGCN to it,
+trains, grows its capacities after a forced overflow and matches the generic path's F1.
+CPU: model-shape predicate (which models take the fused path)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+
+def _setup(device, layers=2, self_loops=False, batch=64, hidden=32):
+    from euler_amd import models as Z
+    from euler_amd.tools import runner
+
+    a = runner.parse_args(["--dataset", "ppi", "--scale", "0.05", "--batch_size", str(batch), "--device", device,
+                           "--seed", "1", "--layers", str(layers), "--hidden_dim", str(hidden)], model="gcn")
+    torch.manual_seed(0)
+    m, est = runner.build(a)
+    if self_loops:
+        old = m
+        m = Z.SupervisedGNN("gcn", "full", [hidden] * layers + [old.label_dim], None, old.gnn.sampler.metapath,
+                            old.gnn.feature_idx, old.gnn.feature_dim, old.label_idx, old.label_dim,
+                            add_self_loops=True)
+    return m
+
+
+def _graph(m, device, fdt=torch.float32):
+    from euler_amd.graph.device_graph import DeviceGraph
+
+    return DeviceGraph.from_engine(features=m.gnn.feature_idx, feature_dims=m.gnn.feature_dim, label=m.label_idx,
+                                   label_dim=m.label_dim, feature_dtype=fdt, seed=5, device=device)
+
+
+def _materialize(m, g, B):
+    """give the lazy layers their shapes through the generic trainer's one no-grad pass"""
+    from euler_amd.models.full_trainer import FullFlowTrainer
+
+    FullFlowTrainer.from_model(m, g, B, caps="exact")
+
+
+def test_fused_gcn_predicate_cpu():
+    from euler_amd.models.gcn_trainer import _gcn_shape
+
+    assert _gcn_shape(_setup("cpu")) is not None
+    assert _gcn_shape(_setup("cpu", layers=3)) is None  # 3 convs: the generic path
+    from euler_amd.tools import runner
+
+    a = runner.parse_args(["--dataset", "ppi", "--scale", "0.05", "--device", "cpu"], model="gat")
+    m, _ = runner.build(a)
+    assert _gcn_shape(m) is None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layers,self_loops", [(2, False), (2, True), (1, False), (1, True)])
+def test_fused_gcn_step_matches_generic_fp32(layers, self_loops):
+    import torch.nn.functional as F
+
+    from euler_amd.models.full_trainer import FullFlowTrainer
+    from euler_amd.models.gcn_trainer import GcnTrainer
+
+    B = 64
+    m = _setup("cuda", layers, self_loops, B).to("cuda")
+    g = _graph(m, "cuda")
+    _materialize(m, g, B)
+    assert GcnTrainer.supports(m, g)
+    tr = GcnTrainer.from_model(m, g, B, caps="exact")
+    assert tr.launches_per_step == 2 + 3 * layers + (2 if layers == 2 else 0) + 2
+    loss_k = float(tr.forward_backward_only())
+    torch.cuda.synchronize()
+    assert int(tr.flow.overflow.item()) == 0
+    grads_k = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+    fl = tr.plan.flow()
+    roots = fl["roots"].long().clone()
+    cnt = fl["cnt"].cpu().tolist()
+    set_ids = fl["set"][: cnt[layers]].long().cpu()
+    # the generic path on the same roots and parameters (fp32 autograd)
+    ref = FullFlowTrainer.from_model(m, g, B, caps="exact")
+    for p in m.parameters():
+        p.grad = None
+    logits, df = ref._forward(roots)
+    y = g.labels[roots].float()
+    loss = F.binary_cross_entropy_with_logits(logits, y)
+    loss.backward()
+    # node sets: the same sets (the fused flow orders each set targets-first)
+    for h in range(layers):
+        nd = df.blocks[h].n_id.cpu()
+        want = set(nd[nd >= 0].tolist())
+        assert set(set_ids[: cnt[h + 1]].tolist()) == want, h
+    assert abs(loss_k - float(loss)) <= 2e-3 * abs(float(loss)), (loss_k, float(loss))
+    errs = {}
+    for n, p in m.named_parameters():
+        r = p.grad.detach()
+        errs[n] = float((grads_k[n] - r).norm() / max(float(r.norm()), 1e-12))
+    print("loss", loss_k, float(loss), "relative gradient errors", errs)
+    # bf16 MFMA operands against fp32 autograd
+    assert max(errs.values()) < 5e-2, errs
+
+
+@pytest.mark.gpu
+def test_fused_gcn_replay_matches_eager():
+    from euler_amd.models.gcn_trainer import GcnTrainer
+
+    out = []
+    for captured in (False, True):
+        m = _setup("cuda").to("cuda")
+        g = _graph(m, "cuda", torch.bfloat16)
+        _materialize(m, g, 64)
+        tr = GcnTrainer.from_model(m, g, 64, caps="exact")
+        losses = []
+        if captured:
+            tr.capture(warmup=2, steps=4)
+            losses += [None, None]
+            for _ in range(6):
+                tr.replay(1)
+                losses.append(float(tr.loss.item()))
+        else:
+            for _ in range(8):
+                tr.step()
+                losses.append(float(tr.loss.item()))
+        out.append(losses)
+    eager, graph = out
+    # the aggregation's edge-parallel flushes add in a data-dependent order: fp32 rounding
+    np.testing.assert_allclose(graph[2:], eager[2:], rtol=2e-3, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_estimator_routes_gcn_to_fused_step_and_trains(tmp_path, monkeypatch):
+    monkeypatch.chdir(tmp_path)
+    import euler_amd.estimator.base as eb
+    from euler_amd.models.gcn_trainer import GcnTrainer
+    from euler_amd.tools.runner import main
+
+    box = {}
+    orig = eb.BaseEstimator._train_device_graph
+
+    def spy(self):
+        box["est"] = self
+        return orig(self)
+
+    monkeypatch.setattr(eb.BaseEstimator, "_train_device_graph", spy)
+    r = main(["--dataset", "ppi", "--scale", "0.05", "--batch_size", "64", "--log_steps", "40", "--device", "cuda",
+              "--seed", "1", "--model_dir", str(tmp_path / "ckpt"), "--device_graph", "--total_step", "120",
+              "--learning_rate", "0.01"], model="gcn")
+    assert isinstance(box["est"].device_trainer, GcnTrainer)
+    assert r["step"] == 120 and math.isfinite(r["loss"]) and r["loss"] < 0.6
+
+
+@pytest.mark.gpu
+def test_fused_gcn_overflow_regrows(tmp_path, monkeypatch):
+    """caps far below any batch: the estimator rolls the chunk back, grows the fused flow's
+    caps, re-plans and finishes"""
+    monkeypatch.chdir(tmp_path)
+    import euler_amd.estimator.base as eb
+    from euler_amd.tools.runner import main
+
+    box = {}
+    orig = eb.BaseEstimator._train_device_graph
+
+    def spy(self):
+        box["est"] = self
+        self.params["device_flow_caps"] = [(256, 256), (256, 256)]
+        return orig(self)
+
+    monkeypatch.setattr(eb.BaseEstimator, "_train_device_graph", spy)
+    r = main(["--dataset", "ppi", "--scale", "0.05", "--batch_size", "64", "--log_steps", "8", "--device", "cuda",
+              "--seed", "1", "--model_dir", str(tmp_path / "ckpt"), "--device_graph", "--total_step", "24"],
+             model="gcn")
+    est = box["est"]
+    assert r["step"] == 24 and math.isfinite(r["loss"]) and est.flow_regrows >= 1
+    assert all(c[0] > 256 for c in est.device_trainer.flow.caps)
