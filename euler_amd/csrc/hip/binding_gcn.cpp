@@ -77,6 +77,14 @@ class GcnPlan {
   // one training step up to the flat gradient (loss_out, counts, overflow updated on the device)
   void step() {
     const c10::DeviceGuard guard(dev_);
+    step_until_head();
+    hipStream_t s = stream();
+    ok(eh_gcn_head(&head_, s), "gcn_head");
+    if (L_ == 2) ok(eh_gcn_dw(&dw_, dw_blocks_, s), "gcn_dw");
+    ok(eh_gcn_reduce(&red_, s), "gcn_reduce");
+  }
+
+  void step_until_head() {
     hipStream_t s = stream();
     ok(eh_alias_sample(prob_.data_ptr<float>(), alias_.data_ptr<int32_t>(),
                        root_rows_.defined() ? root_rows_.data_ptr<int32_t>() : nullptr, prob_.numel(), B_,
@@ -88,9 +96,20 @@ class GcnPlan {
       ok(eh_gcn_place(&hops_[h], s), "gcn_place");
     }
     if (L_ == 2) ok(eh_gcn_layer(&layer_, s), "gcn_layer");
-    ok(eh_gcn_head(&head_, s), "gcn_head");
-    if (L_ == 2) ok(eh_gcn_dw(&dw_, dw_blocks_, s), "gcn_dw");
-    ok(eh_gcn_reduce(&red_, s), "gcn_reduce");
+  }
+
+  // per-phase wall-clock stamps of the head launch (one eager step; diagnostics)
+  torch::Tensor head_profile() {
+    const c10::DeviceGuard guard(dev_);
+    const int64_t nblk = (B_ + 15) / 16;
+    torch::Tensor prof = torch::zeros({nblk, 16}, torch::TensorOptions().dtype(torch::kInt64).device(dev_));
+    GcnHeadArgs a = head_;
+    a.prof = reinterpret_cast<long long*>(prof.data_ptr<int64_t>());
+    step_until_head();
+    ok(eh_gcn_head(&a, stream()), "gcn_head(prof)");
+    if (L_ == 2) ok(eh_gcn_dw(&dw_, dw_blocks_, stream()), "gcn_dw");
+    ok(eh_gcn_reduce(&red_, stream()), "gcn_reduce");
+    return prof;
   }
 
   // the last step's flow (for tests): roots, node set, per-hop counts, edges and offsets
@@ -130,12 +149,13 @@ class GcnPlan {
   torch::Tensor prob_, alias_, root_rows_, rng_;
   torch::Tensor roots_, set_, cnt_, rself_, first_, tag_, pos_, stamp_, overflow_, err_;
   std::vector<torch::Tensor> off_, enode_, etgt_, esrc_, degs_, scan_deg_, scan_flag_;
-  torch::Tensor h1_, agg1_, dh1_, feat_, part_w_, part_fc_, part_bfc_, part_out_, part_stat_, part_w0_;
+  torch::Tensor h1_, agg1_, feat_, part_w_, part_fc_, part_bfc_, part_out_, part_stat_, part_w0_;
   std::vector<torch::Tensor> imgs_;
   GcnHop hops_[kGcnMaxHops]{};
   GcnLayerArgs layer_{};
   GcnHeadArgs head_{};
   GcnDwArgs dw_{};
+  torch::Tensor dagg_;
   GcnReduceArgs red_{};
   int64_t dw_blocks_ = 0;
 
@@ -277,7 +297,6 @@ class GcnPlan {
       const int64_t c1 = cap_t_[1];  // rows of S_1 (the layer's targets, the head's sources)
       h1_ = zeros(c1 * first.outp, torch::kBFloat16);
       agg1_ = zeros(c1 * first.inp, torch::kBFloat16);
-      dh1_ = zeros(c1 * first.outp, torch::kFloat32);
       GcnLayerArgs& y = layer_;
       y.src = fsrc;
       y.enode = hops_[1].enode;
@@ -291,14 +310,22 @@ class GcnPlan {
       y.lin = first;
       y.h_out = reinterpret_cast<uint16_t*>(h1_.data_ptr());
       y.agg_out = reinterpret_cast<uint16_t*>(agg1_.data_ptr());
-      dw_blocks_ = round_up(c1, kGcnDwRows) / kGcnDwRows;
+      dw_blocks_ = round_up(hops_[0].cap_e + B_, kGcnDwRows) / kGcnDwRows;
       part_w0_ = zeros(dw_blocks_ * first.outp * first.inp, torch::kFloat32);
+      dagg_ = zeros(B_ * first.outp, torch::kFloat32);
       GcnDwArgs& w = dw_;
-      w.dh = dh1_.data_ptr<float>();
+      w.dagg = dagg_.data_ptr<float>();
       w.h = reinterpret_cast<uint16_t*>(h1_.data_ptr());
       w.agg = reinterpret_cast<uint16_t*>(agg1_.data_ptr());
-      w.cnt = cnt_.data_ptr<int32_t>();
-      w.cap_t = c1;
+      w.off = hops_[0].off;
+      w.etgt = hops_[0].etgt;
+      w.esrc = hops_[0].esrc;
+      w.rself = rself_.data_ptr<int32_t>();
+      w.deg_s = hops_[0].deg_s;
+      w.cap_t = hops_[0].cap_t;
+      w.cap_e = hops_[0].cap_e;
+      w.B = static_cast<int32_t>(B_);
+      w.self_loops = self_;
       w.lin = first;
       w.part = part_w0_.data_ptr<float>();
     } else {
@@ -314,10 +341,10 @@ class GcnPlan {
       hs.ld = layer_.lin.outp;
       hs.cols = layer_.lin.out;
       a.src = hs;
-      a.dh_in = dh1_.data_ptr<float>();
+      a.dagg = dagg_.data_ptr<float>();
     } else {
       a.src = fsrc;
-      a.dh_in = nullptr;
+      a.dagg = nullptr;
     }
     a.enode = hops_[0].enode;
     a.off = hops_[0].off;
@@ -418,5 +445,6 @@ void register_gcn_ops(py::module& m) {
       .def(py::init<py::dict>())
       .def("step", &GcnPlan::step)
       .def("flow", &GcnPlan::flow)
+      .def("head_profile", &GcnPlan::head_profile)
       .def_property_readonly("launches", &GcnPlan::launches);
 }

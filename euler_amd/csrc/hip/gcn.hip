@@ -23,8 +23,9 @@
 //    with the transposing ds_read_b64_tr_b16 (tile.h tl_tr_frag), the other operand with
 //    the same k permutation, so no transposed copy of any weight or activation exists;
 //  * the whole row-local part of the backward (loss, d logits, d emb, d h, d aggregate) runs
-//    in the head launch; the only cross-row step, d(h1) for the layer below, is a scatter of
-//    fp32 atomics that the dW launch reads and clears.
+//    in the head launch, which writes d(agg) of the roots; the ReLU mask of h1 is per source
+//    row, so d(W0) is linear over hop 0's edges and the dW launch runs its GEMM over those
+//    edges directly: d(h1) is never formed (no scatter, no atomics, nothing to clear).
 #include <hip/hip_runtime.h>
 
 #include "hip/gcn_args.h"
@@ -381,14 +382,17 @@ __device__ __forceinline__ void gcn_row8(const GcnAggSrc& s, int32_t row, int c,
 
 // enode: neighbour node ids of the hop (by-id sources read row = enode[e]); self_src:
 // nullable (target t's self-loop source is t) ; nt: real targets
+// per-target prelude (threads < 16, once per tile): rsqrt of the target degree, the self
+// loop's source and source row, so the self items of the main loop need no extra round
 template <int KP>
 __device__ void gcn_aggregate(const GcnAggSrc& src, const int32_t* off, const int32_t* etgt, const int32_t* esrc,
                               const int32_t* enode, const int32_t* deg_s, const int32_t* self_src, int self_loops,
-                              int64_t t0, int nt, float* acc, float* rdt) {
+                              int64_t t0, int nt, float* acc, float* rdt, int* sself) {
   using AT = AggTile<KP>;
   const int tid = threadIdx.x;
   for (int i = tid; i < kGT * AT::LDA; i += 256) acc[i] = 0.f;
   __shared__ int64_t s_e[2];
+  __shared__ int s_row[kGT];
   if (tid == 0) {
     s_e[0] = off[t0];
     s_e[1] = off[t0 + kGT];
@@ -397,6 +401,9 @@ __device__ void gcn_aggregate(const GcnAggSrc& src, const int32_t* off, const in
     const int64_t t = t0 + tid;
     const int dt = t < nt ? static_cast<int>(off[t + 1] - off[t]) + self_loops : 0;
     rdt[tid] = dt > 0 ? rsqrtf(static_cast<float>(dt)) : 0.f;
+    const int ss = t < nt ? (self_src ? self_src[t] : static_cast<int>(t)) : -1;
+    sself[tid] = ss;
+    s_row[tid] = ss < 0 ? -1 : (src.by_id ? src.set[ss] : ss);
   }
   __syncthreads();
   const int64_t e0 = s_e[0], E = s_e[1] - s_e[0];
@@ -432,14 +439,11 @@ __device__ void gcn_aggregate(const GcnAggSrc& src, const int32_t* off, const in
           row[u] = src.by_id ? enode[e] : s[u];
         } else {
           tl[u] = static_cast<int>(ii - E);
-          s[u] = self_src ? self_src[t0 + tl[u]] : static_cast<int>(t0 + tl[u]);
-          row[u] = -2;  // resolved below (by-id self rows need set[s])
+          s[u] = sself[tl[u]];
+          row[u] = s_row[tl[u]];
         }
       }
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (row[u] == -2) row[u] = s[u] < 0 ? -1 : (src.by_id ? src.set[s[u]] : s[u]);
     float x[U][8];
     float ds[U];
 #pragma unroll
@@ -534,7 +538,8 @@ __global__ __launch_bounds__(256) void gcn_layer_kernel(GcnLayerArgs a) {
   const int64_t t0 = static_cast<int64_t>(blockIdx.x) * kGT;
   if (t0 >= nt) return;  // uniform: rows past the set are never read
   copy_img(a.wimg, wimg, HP * LDK);
-  gcn_aggregate<KP>(a.src, a.off, a.etgt, a.esrc, a.enode, a.deg_s, nullptr, a.self_loops, t0, nt, acc, rdt);
+  __shared__ int sself[kGT];
+  gcn_aggregate<KP>(a.src, a.off, a.etgt, a.esrc, a.enode, a.deg_s, nullptr, a.self_loops, t0, nt, acc, rdt, sself);
   // aggregate -> bf16 image + the dW operand rows
   for (int i = tid; i < kGT * (KP / 2); i += 256) {
     const int r = i / (KP / 2), c = (i - r * (KP / 2)) * 2;
@@ -569,7 +574,7 @@ __host__ __device__ inline size_t gcn_head_lds_bytes(int KP, int HP, int EP, int
   const int LK = img_ld(KP), LH = img_ld(HP);
   const size_t bf = static_cast<size_t>(HP) * LK + static_cast<size_t>(EP) * LH + static_cast<size_t>(CP) * kWide +
                     32 * LK + 32 * LH + 32 * kWide * 3 + 32 * LH;
-  return bf * 2 + static_cast<size_t>(kGT) * (KP + 1) * 4 + kGT * 4 + 64;
+  return bf * 2 + static_cast<size_t>(kGT) * (KP + 1) * 4 + kGT * 4 + static_cast<size_t>(kGT) * CP * 4 + 64;
 }
 
 template <int KP, int HP>
@@ -594,17 +599,41 @@ __global__ __launch_bounds__(256) void gcn_head_kernel(GcnHeadArgs a) {
   const int64_t t0 = static_cast<int64_t>(blockIdx.x) * kGT;
   const int blk = blockIdx.x;
   // the weights (fp32 masters -> bf16) and cleared activation images
+  __shared__ int sself[kGT];
+  __shared__ int s_root[kGT];
+  float* lab = rdt + kGT;  // [16][CP] the tile's dense labels
+#define GH_STAMP(k) \
+  if (a.prof && threadIdx.x == 0) a.prof[static_cast<int64_t>(blockIdx.x) * 16 + (k)] = wall_clock64()
+  GH_STAMP(0);
+  if (tid < kGT) s_root[tid] = t0 + tid < a.B ? a.roots[t0 + tid] : -1;
   copy_img(a.wl_img, Wl, HP * LK);
   copy_img(a.wfc_img, Wf, EP * LH);
   copy_img(a.wout_img, Wo, CP * LE);
   zero_img(Ag, 32 * LK + 32 * LH + 32 * LE * 3 + 32 * LH);
-  gcn_aggregate<KP>(a.src, a.off, a.etgt, a.esrc, a.enode, a.deg_s, a.rself, a.self_loops, t0, a.B, acc, rdt);
+  __syncthreads();
+  GH_STAMP(1);
+  {  // every label load in flight at once (16 x CP <= 2048 values: 8 per thread)
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = tid + u * 256;
+      const int r = i / CP, c = i - r * CP;
+      const int32_t root = i < kGT * CP ? s_root[r] : -1;
+      v[u] = (root >= 0 && c < a.C) ? a.labels[static_cast<int64_t>(root) * a.C + c] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (tid + u * 256 < kGT * CP) lab[tid + u * 256] = v[u];
+  }
+  gcn_aggregate<KP>(a.src, a.off, a.etgt, a.esrc, a.enode, a.deg_s, a.rself, a.self_loops, t0, a.B, acc, rdt,
+                    sself);
   for (int i = tid; i < kGT * (KP / 2); i += 256) {
     const int r = i / (KP / 2), c = (i - r * (KP / 2)) * 2;
     *reinterpret_cast<uint32_t*>(Ag + r * LK + c) = pack_bf16x2(acc[r * AggTile<KP>::LDA + c],
                                                                 acc[r * AggTile<KP>::LDA + c + 1]);
   }
   __syncthreads();
+  GH_STAMP(2);
   // z = Ag Wl^T -> H0 = relu(z)
   for (int ct = wave; ct < HP / 16; ct += 4) {
     float4_t z = float4_t{0.f, 0.f, 0.f, 0.f};
@@ -615,6 +644,7 @@ __global__ __launch_bounds__(256) void gcn_head_kernel(GcnHeadArgs a) {
     for (int j = 0; j < 4; ++j) H0[(lg * 4 + j) * LH + ct * 16 + lr] = f2bf(fmaxf(z[j], 0.f));
   }
   __syncthreads();
+  GH_STAMP(3);
   // emb = H0 Wf^T + bfc
   for (int ct = wave; ct < EP / 16; ct += 4) {
     float4_t z = float4_t{0.f, 0.f, 0.f, 0.f};
@@ -627,6 +657,7 @@ __global__ __launch_bounds__(256) void gcn_head_kernel(GcnHeadArgs a) {
     for (int j = 0; j < 4; ++j) Em[(lg * 4 + j) * LE + col] = f2bf(col < a.E ? z[j] + b : 0.f);
   }
   __syncthreads();
+  GH_STAMP(4);
   // logits = emb Wo^T -> loss, F1 counts, d logits
   float lsum = 0.f, tp = 0.f, fp = 0.f, fn = 0.f;
   for (int ct = wave; ct < CP / 16; ct += 4) {
@@ -640,8 +671,7 @@ __global__ __launch_bounds__(256) void gcn_head_kernel(GcnHeadArgs a) {
       const int64_t t = t0 + r;
       float d = 0.f;
       if (t < a.B && col < a.C) {
-        const int32_t root = a.roots[t];
-        const float y = root >= 0 ? a.labels[static_cast<int64_t>(root) * a.C + col] : 0.f;
+        const float y = lab[r * CP + col];
         const float x = z[j];
         lsum += fmaxf(x, 0.f) - x * y + log1pf(__expf(-fabsf(x)));
         const bool pred = x >= 0.f, pos = y > 0.5f;
@@ -664,6 +694,7 @@ __global__ __launch_bounds__(256) void gcn_head_kernel(GcnHeadArgs a) {
     red[wave][3] = fn;
   }
   __syncthreads();
+  GH_STAMP(5);
   if (tid < 4) {  // the mean loss's share of this block; raw F1 counts
     const float v = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
     a.part_stat[blk * 4 + tid] = tid == 0 ? v * a.inv_scale : v;
@@ -685,6 +716,7 @@ __global__ __launch_bounds__(256) void gcn_head_kernel(GcnHeadArgs a) {
     if (lg == 0) a.part_bfc[static_cast<int64_t>(blk) * EP + col] = cs;
   }
   __syncthreads();
+  GH_STAMP(6);
   // d z = (d emb Wf) * relu'(z)   (K = E: the rows of Wf are the reduction index)
   for (int ct = wave; ct < HP / 16; ct += 4) {
     float4_t z = float4_t{0.f, 0.f, 0.f, 0.f};
@@ -698,6 +730,7 @@ __global__ __launch_bounds__(256) void gcn_head_kernel(GcnHeadArgs a) {
     }
   }
   __syncthreads();
+  GH_STAMP(7);
   // weight-gradient partials of this block's rows (k = the 32 image rows, 16..31 zero):
   // d out W = Dl^T Em [CP][EP], d fc W = De^T H0 [EP][HP], d conv W = Dz^T Ag [HP][KP]
   {
@@ -732,9 +765,13 @@ __global__ __launch_bounds__(256) void gcn_head_kernel(GcnHeadArgs a) {
       for (int q = 0; q < 4; ++q) out[static_cast<int64_t>(r0 + lg * 4 + q) * ld + c0 + lr] = z[q];
     }
   }
-  if (a.dh_in == nullptr) return;  // L = 1: no layer below
+  if (a.dagg == nullptr) {  // L = 1: no layer below
+    GH_STAMP(15);
+    return;
+  }
   // d agg = Dz Wl (K = H: the rows of Wl are the reduction index) -> the fp32 accumulator
   __syncthreads();
+  GH_STAMP(8);
   for (int ct = wave; ct < KP / 16; ct += 4) {
     float4_t z = float4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -744,32 +781,14 @@ __global__ __launch_bounds__(256) void gcn_head_kernel(GcnHeadArgs a) {
     for (int j = 0; j < 4; ++j) acc[(lg * 4 + j) * AggTile<KP>::LDA + ct * 16 + lr] = z[j];
   }
   __syncthreads();
-  // scatter: d h1[src] += w_e d agg[target] over the tile's edges and self loops
-  {
-    using AT = AggTile<KP>;
-    const int64_t e0 = a.off[t0], E = a.off[t0 + kGT] - e0;
-    const int nself = a.self_loops ? static_cast<int>(a.B - t0 < kGT ? a.B - t0 : kGT) : 0;
-    const int64_t W = E + nself;
-    const int g = tid / AT::NCH, c = tid % AT::NCH;
-    const int ldh = a.lin.inp;
-    for (int64_t i = g; i < W; i += AT::NW) {
-      int tl, s;
-      if (i < E) {
-        tl = a.etgt[e0 + i] - static_cast<int>(t0);
-        s = a.esrc[e0 + i];
-      } else {
-        tl = static_cast<int>(i - E);
-        s = a.rself[t0 + tl];
-      }
-      if (s < 0) continue;
-      const float w = rdt[tl] * rsqrtf(static_cast<float>(a.deg_s[s]));
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        const int col = c * 8 + jj;
-        if (col < a.lin.in) atomicAdd(&a.dh_in[static_cast<int64_t>(s) * ldh + col], w * acc[tl * AT::LDA + col]);
-      }
-    }
+  GH_STAMP(9);
+  // d agg rows to global: gcn_dw_kernel reads them per hop-0 edge (no d h1 scatter)
+  for (int i = tid; i < kGT * KP; i += 256) {
+    const int r = i / KP, c = i - r * KP;
+    if (t0 + r < a.B) a.dagg[(t0 + r) * KP + c] = acc[r * AggTile<KP>::LDA + c];
   }
+  GH_STAMP(15);
+#undef GH_STAMP
 }
 
 // ----------------------------------------------------------------------------
@@ -777,33 +796,83 @@ __global__ __launch_bounds__(256) void gcn_head_kernel(GcnHeadArgs a) {
 // ----------------------------------------------------------------------------
 template <int KP, int HP>
 __global__ __launch_bounds__(256) void gcn_dw_kernel(GcnDwArgs a) {
+  // the ReLU mask of h1 is per source row, so
+  //   d W0 = sum_s agg[s]^T (mask[s] . sum_{e: src s} w_e d agg[t_e])
+  //        = sum_e w_e agg[s_e]^T (mask[s_e] . d agg[t_e])
+  // and the rows of this GEMM are hop 0's edges (+ self loops): no d h1 scatter, no atomics
   constexpr int LK = img_ld(KP), LH = img_ld(HP), CH = kGcnDwRows / 32;
   __shared__ __attribute__((aligned(16))) bf16_t dz[CH][32 * LH];
   __shared__ __attribute__((aligned(16))) bf16_t ag[CH][32 * LK];
+  __shared__ int32_t s_src[kGcnDwRows], s_tgt[kGcnDwRows];
+  __shared__ float s_w[kGcnDwRows];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int n = a.cnt[1];
+  const int64_t total = a.off[a.cap_t];
+  const int64_t W = total + (a.self_loops ? a.B : 0);
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kGcnDwRows;
-  // every load of the block's 128 rows in flight at once
-  for (int i = tid; i < kGcnDwRows * (HP / 2); i += 256) {
-    const int r = i / (HP / 2), c = (i - r * (HP / 2)) * 2;
-    const int64_t row = r0 + r;
-    float d0 = 0.f, d1 = 0.f;
-    if (row < n) {
-      float* p = a.dh + row * HP + c;
-      const uint32_t hv = *reinterpret_cast<const uint32_t*>(a.h + row * HP + c);
-      d0 = bf_pos(static_cast<bf16_t>(hv & 0xffffu)) ? p[0] : 0.f;
-      d1 = bf_pos(static_cast<bf16_t>(hv >> 16)) ? p[1] : 0.f;
-      p[0] = 0.f;  // cleared for the next step's scatter
-      p[1] = 0.f;
+  if (tid < kGcnDwRows) {
+    const int64_t e = r0 + tid;
+    int32_t sv = -1, tv = 0;
+    if (e < total) {
+      tv = a.etgt[e];
+      sv = a.esrc[e];
+    } else if (e < W) {
+      tv = static_cast<int32_t>(e - total);
+      sv = a.rself[tv];
     }
-    *reinterpret_cast<uint32_t*>(&dz[r >> 5][(r & 31) * LH + c]) = pack_bf16x2(d0, d1);
+    float w = 0.f;
+    if (sv >= 0) {
+      const float dt = static_cast<float>(a.off[tv + 1] - a.off[tv] + a.self_loops);
+      w = rsqrtf(dt) * rsqrtf(static_cast<float>(a.deg_s[sv]));
+    }
+    s_src[tid] = sv;
+    s_tgt[tid] = tv;
+    s_w[tid] = w;
   }
-  for (int i = tid; i < kGcnDwRows * (KP / 8); i += 256) {
-    const int r = i / (KP / 8), c = (i - r * (KP / 8)) * 8;
-    const int64_t row = r0 + r;
-    uint4_t v = uint4_t{0u, 0u, 0u, 0u};
-    if (row < n) v = *reinterpret_cast<const uint4_t*>(a.agg + row * KP + c);
-    *reinterpret_cast<uint4_t*>(&ag[r >> 5][(r & 31) * LK + c]) = v;
+  __syncthreads();
+  // every row load of the block in flight at once: dz = w (mask . d agg[t]), ag = agg[s]
+  constexpr int NZ = kGcnDwRows * (HP / 8) / 256, NA = kGcnDwRows * (KP / 8) / 256;
+  static_assert(NZ >= 1 && NA >= 1, "dw tile");
+  uint4_t hv[NZ], av[NA];
+  float4_t dlo[NZ], dhi[NZ];
+#pragma unroll
+  for (int u = 0; u < NZ; ++u) {
+    const int i = tid + u * 256, r = i / (HP / 8), c = (i - r * (HP / 8)) * 8;
+    const int32_t sv = s_src[r];
+    hv[u] = uint4_t{0u, 0u, 0u, 0u};
+    dlo[u] = dhi[u] = float4_t{0.f, 0.f, 0.f, 0.f};
+    if (sv >= 0) {
+      const int64_t t = s_tgt[r];
+      hv[u] = *reinterpret_cast<const uint4_t*>(a.h + static_cast<int64_t>(sv) * HP + c);
+      dlo[u] = *reinterpret_cast<const float4_t*>(a.dagg + t * HP + c);
+      dhi[u] = *reinterpret_cast<const float4_t*>(a.dagg + t * HP + c + 4);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < NA; ++u) {
+    const int i = tid + u * 256, r = i / (KP / 8), c = (i - r * (KP / 8)) * 8;
+    const int32_t sv = s_src[r];
+    av[u] = sv >= 0 ? *reinterpret_cast<const uint4_t*>(a.agg + static_cast<int64_t>(sv) * KP + c)
+                    : uint4_t{0u, 0u, 0u, 0u};
+  }
+#pragma unroll
+  for (int u = 0; u < NZ; ++u) {
+    const int i = tid + u * 256, r = i / (HP / 8), c = (i - r * (HP / 8)) * 8;
+    const float w = s_w[r];
+    uint4_t o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t hw = hv[u][q];
+      const float x0 = q < 2 ? dlo[u][2 * q] : dhi[u][2 * q - 4];
+      const float x1 = q < 2 ? dlo[u][2 * q + 1] : dhi[u][2 * q - 3];
+      o[q] = pack_bf16x2(bf_pos(static_cast<bf16_t>(hw & 0xffffu)) ? w * x0 : 0.f,
+                         bf_pos(static_cast<bf16_t>(hw >> 16)) ? w * x1 : 0.f);
+    }
+    *reinterpret_cast<uint4_t*>(&dz[r >> 5][(r & 31) * LH + c]) = o;
+  }
+#pragma unroll
+  for (int u = 0; u < NA; ++u) {
+    const int i = tid + u * 256, r = i / (KP / 8), c = (i - r * (KP / 8)) * 8;
+    *reinterpret_cast<uint4_t*>(&ag[r >> 5][(r & 31) * LK + c]) = av[u];
   }
   __syncthreads();
   constexpr int nt = (HP / 16) * (KP / 16);
@@ -969,7 +1038,8 @@ hipError_t eh_gcn_head(const GcnHeadArgs* a, hipStream_t s) {
 #define GCN_DW(K, H, grid, s, A) hipLaunchKernelGGL((gcn_dw_kernel<K, H>), grid, dim3(256), 0, s, A)
 
 hipError_t eh_gcn_dw(const GcnDwArgs* a, int64_t nblk, hipStream_t s) {
-  if (!a || !a->dh || !a->h || !a->agg || !a->cnt || !a->part || nblk < 1 || nblk * kGcnDwRows < a->cap_t ||
+  if (!a || !a->dagg || !a->h || !a->agg || !a->off || !a->etgt || !a->esrc || !a->rself || !a->deg_s || !a->part ||
+      a->B < 1 || nblk < 1 || nblk * kGcnDwRows < a->cap_e + a->B ||
       !gcn_kp_ok(a->lin.inp) || !gcn_hp_ok(a->lin.outp))
     return hipErrorInvalidValue;
   const dim3 grid(static_cast<uint32_t>(nblk));

@@ -16,8 +16,9 @@
 //   layer     (L = 2) the outer conv: edge-parallel weighted aggregation into LDS, MFMA
 //             linear + ReLU -> h1, the aggregate kept for dW
 //   head      the last conv + fc + out_fc + loss + the whole row-local backward + the
-//             weight-gradient partials of its rows + the scatter of d(h1) (fp32 atomics)
-//   dw        (L = 2) d(W0) partials from d(h1), ReLU mask and the kept aggregate; clears d(h1)
+//             weight-gradient partials of its rows + d(agg) of the roots (L = 2)
+//   dw        (L = 2) d(W0) partials, one GEMM row per hop-0 edge: w_e (mask[s] . d agg[t])
+//             against the kept aggregate of s (d(h1) is never formed)
 //   reduce    the partials into the flat fp32 gradient, loss / F1 counts, epoch + 1
 // then the flat optimizer (optim.hip).
 //
@@ -139,20 +140,26 @@ struct GcnHeadArgs {  // targets: the B roots; sources: S_1
   int32_t E, Ep, C, Cp;
   const float* labels;  // [N][C] dense multi-label targets
   float inv_scale;      // 1 / (B C)
-  float* dh_in;         // L = 2: [cap_1][lin.inp] fp32 d(h1) accumulated by atomics (nullptr: L = 1)
+  float* dagg;          // L = 2: [B][lin.inp] fp32 d(agg) of the roots, gcn_dw's input (nullptr: L = 1)
   float* part_w;        // [nblk][outp][inp]   d(last conv)
   float* part_fc;       // [nblk][Ep][outp]    d(fc W)
   float* part_bfc;      // [nblk][Ep]
   float* part_out;      // [nblk][Cp][Ep]      d(out_fc W)
   float* part_stat;     // [nblk][4] loss, tp, fp, fn
+  long long* prof;      // optional [nblk][16] wall-clock stamps of the phases (diagnostics)
 };
 
-struct GcnDwArgs {  // d(W0) over the rows of S_1 (L = 2)
-  float* dh;            // [cap_t][lin.outp] fp32, cleared after reading
-  const uint16_t* h;    // [cap_t][lin.outp] bf16 relu output (its sign = the ReLU mask)
-  const uint16_t* agg;  // [cap_t][lin.inp] bf16
-  const int32_t* cnt;   // rows = cnt[1]
-  int64_t cap_t;
+struct GcnDwArgs {  // d(W0) over hop 0's edges + self loops (L = 2)
+  const float* dagg;    // [B][lin.outp] fp32 d(agg) of the roots (the head writes it)
+  const uint16_t* h;    // [cap_1][lin.outp] bf16 relu output (its sign = the ReLU mask)
+  const uint16_t* agg;  // [cap_1][lin.inp] bf16
+  const int32_t* off;   // hop 0 [cap_t + 1]
+  const int32_t* etgt;
+  const int32_t* esrc;
+  const int32_t* rself;
+  const int32_t* deg_s;
+  int64_t cap_t, cap_e;  // hop 0
+  int32_t B, self_loops;
   GcnLin lin;
   float* part;          // [nblk][outp][inp]
 };

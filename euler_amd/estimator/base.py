@@ -671,7 +671,8 @@ class BaseEstimator:
             state = torch.load(own, map_location="cpu", weights_only=True)
         elif self.rank != 0:
             same_world = False  # no file of this rank: derive its stream
-        tr.load_logical({k: v for k, v in state["model"].items() if k in tr.state_dict()})
+        keys = set(tr.state_dict())  # once: a row-sharded trainer assembles it collectively
+        tr.load_logical({k: v for k, v in state["model"].items() if k in keys})
         st = state.get("device_trainer")
         if st is not None:
             st = dict(st)

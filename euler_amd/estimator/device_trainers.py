@@ -205,9 +205,6 @@ def _walks(c: Ctx):
     # id % world) and every step's rows travel over fixed-capacity all-to-alls
     from euler_amd.models.deepwalk_step import DeepWalkEstimatorTrainer
 
-    if c.est.world > 1:
-        raise ValueError("the DeepWalk device path of the estimator runs on one rank "
-                         "(the row-sharded multi-rank table: benchmarks/bench_deepwalk.py)")
     return DeepWalkEstimatorTrainer(c.model, c.upload(c.model.node_type), c.batch, seed=c.seed, **c.opt_kw())
 
 

@@ -327,8 +327,15 @@ class DeepWalkEstimatorTrainer:
     row-sparse SGNS update of :class:`DeepWalkTrainer` on the HBM graph, several static
     steps per hipGraph replay.  The model's two embedding tables are the trainer's table
     halves (graph row r = node id ``graph.ids[r]``; the pad row is the model's
-    ``max_id + 1`` row); checkpoints carry the model's own parameter names.  One rank (the
-    row-sharded multi-rank table is the benchmark's, benchmarks/bench_deepwalk.py)."""
+    ``max_id + 1`` row); checkpoints carry the model's own parameter names.
+
+    Data parallel (the reference's ``mod``-partitioned PS embedding variables,
+    tf_euler/python/utils/embedding.py:24-68): with 2+ ranks the table is row-sharded
+    (``parallel/sparse_table.py``: trainer row r on rank r % world), every step's rows travel
+    over fixed-capacity all-to-alls and only the touched rows are updated — per-step work
+    and traffic depend on the batch, never on |V|.  Each rank draws its own walks (its own
+    Philox key); the model's full tables are assembled (all-gather of the shards) only when
+    a checkpoint or the model is written."""
 
     metric_name = "loss"
     self_synced = True  # no dense gradient for the estimator to all-reduce
@@ -374,26 +381,57 @@ class DeepWalkEstimatorTrainer:
         self.captures = 0
 
     # ------------------------------------------------------------------ table <-> model
-    def _halves(self):
-        t = self.inner
-        return t.table.weight[: t.off], t.table.weight[t.off: 2 * t.off]
+    # trainer row r (target half: r < off, context half: off + r) of graph row i is node id
+    # ids[i] (the pad row, off - 1, is the model's max_id + 1 row); with a row-sharded table
+    # this rank holds trainer rows table.global_ids() (r % world == rank)
+    def _model_rows(self):
+        """model row of every trainer row of one half (off entries)"""
+        pad = torch.tensor([self._pad_id], dtype=torch.int64, device=self.device)
+        return torch.cat([self._ids, pad])
 
     def load_logical(self, sd):
+        t = self.inner
+        g = t.table.global_ids()
+        half, r = g // t.off, g % t.off
+        mrow = self._model_rows()[r]
         with torch.no_grad():
-            for key, half in zip(self._keys, self._halves()):
+            for h, key in enumerate(self._keys):
                 if key not in sd:
                     continue
-                w = torch.as_tensor(sd[key]).to(half)
-                half[:-1].copy_(w[self._ids])
-                half[-1].copy_(w[self._pad_id])
+                w = torch.as_tensor(sd[key]).to(t.table.weight)
+                sel = half == h
+                t.table.weight[sel] = w[mrow[sel]]
+
+    def _full_table(self):
+        """every trainer row (all ranks' shards; all-gather with 2+ ranks: a collective)"""
+        t = self.inner.table
+        if t.world == 1:
+            return t.weight
+        import torch.distributed as dist
+
+        n = int(t.weight.shape[0])
+        sizes = torch.tensor([n], dtype=torch.int64, device=t.weight.device)
+        all_n = [torch.zeros_like(sizes) for _ in range(t.world)]
+        dist.all_gather(all_n, sizes, group=t.group)
+        mx = max(int(x.item()) for x in all_n)
+        buf = torch.zeros((mx, t.dim), dtype=t.weight.dtype, device=t.weight.device)
+        buf[:n] = t.weight
+        parts = [torch.zeros_like(buf) for _ in range(t.world)]
+        dist.all_gather(parts, buf, group=t.group)
+        full = torch.empty((t.num_rows, t.dim), dtype=t.weight.dtype, device=t.weight.device)
+        for r, (p, k) in enumerate(zip(parts, all_n)):
+            full[r::t.world] = p[: int(k.item())]
+        return full
 
     def write_to_model(self, model):
+        t = self.inner
+        full = self._full_table()
         own = model.state_dict()
+        mrow = self._model_rows()
         with torch.no_grad():
-            for key, half in zip(self._keys, self._halves()):
+            for h, key in enumerate(self._keys):
                 w = own[key]
-                w[self._ids.to(w.device)] = half[:-1].to(w)
-                w[self._pad_id] = half[-1].to(w)
+                w[mrow.to(w.device)] = full[h * t.off: (h + 1) * t.off].to(w)
 
     def state_dict(self):
         self.write_to_model(self.model)
@@ -482,8 +520,18 @@ class DeepWalkEstimatorTrainer:
 
     def load_trainer_state(self, st):
         t = self.inner.table
-        t.m.copy_(torch.as_tensor(st["m"]).to(t.m))
-        t.v.copy_(torch.as_tensor(st["v"]).to(t.v))
+        m, v = torch.as_tensor(st["m"]), torch.as_tensor(st["v"])
+        if m.shape == t.m.shape and v.shape == t.v.shape:
+            t.m.copy_(m.to(t.m))
+            t.v.copy_(v.to(t.v))
+        else:
+            # another rank layout (the weights came from the model's full tables): the
+            # optimizer slots of the new shard start fresh
+            import logging
+
+            logging.getLogger("euler_amd.estimator").warning(
+                "DeepWalk device path: the checkpoint's optimizer slots are sharded for another world size; "
+                "restarting them")
         t.step.fill_(int(st["step"]))
         self.graph.rng.copy_(torch.as_tensor(st["rng"]).to(self.graph.rng))
         self.step_count = int(st["step"])

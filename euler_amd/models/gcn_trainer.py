@@ -16,8 +16,10 @@ What one step launches (L = 2 convs; 1 + 3 L + 4 + the optimizer = 12):
   mark (positions of the new nodes), place (edge sources, in-block source counts);
 * the outer conv: edge-parallel aggregation + MFMA linear + ReLU;
 * the head: last conv, fc, out_fc, loss, F1 counts and the whole row-local backward, the
-  weight-gradient partials of its rows and the scatter of d(h1);
-* d(W0) partials; the reduce into the flat gradient (+ loss, counts, RNG counter);
+  weight-gradient partials of its rows and d(agg) of the roots;
+* d(W0) partials as one GEMM over hop 0's edges (the ReLU mask is per source row, so
+  d(h1) is never formed: no scatter); the reduce into the flat gradient (+ loss, counts,
+  RNG counter);
 * the flat optimizer (``parallel/flat.py``), after the data-parallel all-reduce.
 
 The generic path (``models/full_trainer.py``) runs the user's convolution modules on

@@ -4,6 +4,7 @@ import os
 import socket
 import tempfile
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -699,5 +700,53 @@ def _worker_estimator_device_resume(rank, world, port, q, tmp):
 
 def test_estimator_device_graph_resume_keeps_per_rank_streams(tmp_path):
     res = _run(_worker_estimator_device_resume, str(tmp_path))
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == 2 and all(r[2] for r in res), res
+
+
+def _worker_deepwalk_estimator(rank, world, port, q, data_dir, model_dir):
+    """NodeEstimator(device_graph=True) DeepWalk on 2 ranks: row-sharded tables (rank r
+    holds trainer rows r % 2), per-rank walks, fixed-size all-to-alls; after training (and
+    after a resume) every rank assembles the same full tables, and they moved"""
+    try:
+        _init(rank, world, port)
+        import euler_amd as ea
+        from euler_amd import models as Z
+        from euler_amd.dataset import get_dataset
+        from euler_amd.estimator import NodeEstimator
+
+        ds = get_dataset("cora", data_dir=data_dir, scale=0.08)
+        ds.load_graph()
+        ea.set_seed(3)
+        tnt = ds.train_node_type[0] if isinstance(ds.train_node_type, list) else ds.train_node_type
+        res = {}
+        for total in (20, 30):  # 30: resumes the 20-step checkpoint (per-rank shards + streams)
+            torch.manual_seed(0)
+            m = Z.DeepWalk("train", ["train"], ds.max_node_id, 8, walk_len=3, num_negs=3)
+            before = m.state_dict()["_target_encoder.embedding.weight"].clone()
+            est = NodeEstimator(m, {"model_dir": model_dir, "batch_size": 32, "total_step": total,
+                                    "optimizer": "adam", "learning_rate": 0.02, "log_steps": 10,
+                                    "train_node_type": tnt, "device": "cpu", "device_graph": True, "seed": 11})
+            out = est.train()
+            tr = est.device_trainer
+            res[f"sharded_{total}"] = tr.inner.table.world == 2 and tr.inner.table.weight.shape[0] < tr.inner.table.num_rows
+            res[f"finite_{total}"] = bool(np.isfinite(out["loss"])) and out["step"] == total
+            w = m.state_dict()["_target_encoder.embedding.weight"]
+            allw = [torch.zeros_like(w) for _ in range(world)]
+            dist.all_gather(allw, w.contiguous())
+            res[f"same_tables_{total}"] = all(torch.equal(x, allw[0]) for x in allw)
+            res[f"moved_{total}"] = not torch.equal(before, w)
+        q.put((rank, "deepwalk_est", all(res.values()), res))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_deepwalk_estimator_device_path_two_ranks(tmp_path):
+    import numpy  # noqa: F401  (the worker uses np through the module import below)
+
+    res = _run(_worker_deepwalk_estimator, str(tmp_path / "cora"), str(tmp_path / "ckpt"))
     assert not [r for r in res if r[1] == "error"], res
     assert len(res) == 2 and all(r[2] for r in res), res
