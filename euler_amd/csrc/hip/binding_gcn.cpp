@@ -112,6 +112,13 @@ class GcnPlan {
     return prof;
   }
 
+  // after a discarded step (overflow / look-back timeout) a node counter may be left
+  // non-zero: the trainer clears them with the overflow word
+  void reset_counters() {
+    const c10::DeviceGuard guard(dev_);
+    cntw_.zero_();
+  }
+
   // the last step's flow (for tests): roots, node set, per-hop counts, edges and offsets
   py::dict flow() const {
     py::dict o;
@@ -147,8 +154,8 @@ class GcnPlan {
   GcnGraph g_{};
   std::vector<int64_t> masks_, cap_e_, cap_n_, cap_t_;
   torch::Tensor prob_, alias_, root_rows_, rng_;
-  torch::Tensor roots_, set_, cnt_, rself_, first_, tag_, pos_, stamp_, overflow_, err_;
-  std::vector<torch::Tensor> off_, enode_, etgt_, esrc_, degs_, scan_deg_, scan_flag_;
+  torch::Tensor roots_, set_, cnt_, rself_, first_, cntw_, tag_, pos_, stamp_, overflow_, err_;
+  std::vector<torch::Tensor> off_, enode_, etgt_, esrc_, eflag_, degs_, scan_deg_, scan_flag_;
   torch::Tensor h1_, agg1_, feat_, part_w_, part_fc_, part_bfc_, part_out_, part_stat_, part_w0_;
   std::vector<torch::Tensor> imgs_;
   GcnHop hops_[kGcnMaxHops]{};
@@ -189,6 +196,7 @@ class GcnPlan {
   void build_tables() {
     // per-node tables: never cleared (every entry is keyed by the step epoch)
     first_ = full(N_, -1, torch::kInt64);  // all ones = the largest 64-bit key
+    cntw_ = zeros(N_, torch::kInt32);      // zero between hops (claimers reset their node's)
     tag_ = full(N_, -1, torch::kInt32);
     pos_ = zeros(N_, torch::kInt32);
     // the plan's epoch continues across re-plans (capacity growth) of one trainer
@@ -222,6 +230,7 @@ class GcnPlan {
       enode_.push_back(full(cap_e_[h], -1, torch::kInt32));
       etgt_.push_back(zeros(cap_e_[h], torch::kInt32));
       esrc_.push_back(full(cap_e_[h], -1, torch::kInt32));
+      eflag_.push_back(zeros(cap_e_[h], torch::kUInt8));
       degs_.push_back(zeros(round_up(cap_n_[h], 256), torch::kInt32));
       GcnHop& a = hops_[h];
       a.g = g_;
@@ -242,6 +251,8 @@ class GcnPlan {
       a.deg_s = degs_[h].data_ptr<int32_t>();
       a.rself = rself_.data_ptr<int32_t>();
       a.first = reinterpret_cast<uint64_t*>(first_.data_ptr<int64_t>());
+      a.cntw = cntw_.data_ptr<int32_t>();
+      a.eflag = eflag_[h].data_ptr<uint8_t>();
       a.tag = tag_.data_ptr<int32_t>();
       a.pos = pos_.data_ptr<int32_t>();
       scan_deg_.push_back(zeros(eh_gcn_expand_blocks(cap_t_[h]), torch::kInt64));
@@ -445,6 +456,7 @@ void register_gcn_ops(py::module& m) {
       .def(py::init<py::dict>())
       .def("step", &GcnPlan::step)
       .def("flow", &GcnPlan::flow)
+      .def("reset_counters", &GcnPlan::reset_counters)
       .def("head_profile", &GcnPlan::head_profile)
       .def_property_readonly("launches", &GcnPlan::launches);
 }

@@ -8,9 +8,12 @@
 // sigmoid cross-entropy on dense labels).
 //
 // Design notes (MI355X):
-//  * node sets without sorting or clearing: a per-node first-occurrence claim (64-bit
-//    atomicMin of an epoch-keyed occurrence index) and a per-node (epoch, position) table;
-//    a new epoch per step makes every older entry stale, so nothing is reset;
+//  * node sets without sorting or clearing: one returning atomicAdd per edge on a per-node
+//    counter (random-address device atomics cost one memory-side request each, ~20-30 G/s
+//    chip-wide, so the flow spends exactly one per edge): the edge that sees 0 claims the
+//    node — its set position when unplaced, and later its final count (the GCN source
+//    degree, one atomic per distinct source) and the counter's reset; positions live in a
+//    per-node (epoch, position) table, so a new epoch per step makes older entries stale;
 //  * prefix sums inside the producing launch: a decoupled look-back over 8-byte
 //    {tag, flag, value} granules written with relaxed agent-scope atomics (the data is the
 //    flag: no fences), tagged with the step epoch so no status word is ever cleared;
@@ -189,6 +192,9 @@ __global__ __launch_bounds__(256) void gcn_expand_kernel(GcnHop a) {
   // this hop's source counts start from zero (place adds)
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + tid; i < a.cap_n; i += static_cast<int64_t>(nexp) * 256)
     a.deg_s[i] = 0;
+  // blocks past the last real target have nothing to publish: no later block reads them
+  const int lastb = (nt - 1) / TE;
+  if (static_cast<int>(blockIdx.x) > lastb) return;
   int32_t row = -1;
   int deg = 0;
   int64_t start = 0;
@@ -215,17 +221,20 @@ __global__ __launch_bounds__(256) void gcn_expand_kernel(GcnHop a) {
   if (tid < TE && t < a.cap_t) {
     const int64_t excl = prefix + incl - deg;
     a.off[t] = static_cast<int32_t>(excl < a.cap_e ? excl : a.cap_e);
-    if (t == a.cap_t - 1) {
-      const int64_t tot = excl + deg;
-      a.off[a.cap_t] = static_cast<int32_t>(tot < a.cap_e ? tot : a.cap_e);
-      if (tot > a.cap_e) atomicOr(a.overflow, 1);
-    }
+  }
+  if (static_cast<int>(blockIdx.x) == lastb && tid == 0) {
+    // the end offset: read at the end of this block's last tile and as the hop's total
+    const int64_t tot = prefix + total;
+    const int32_t v = static_cast<int32_t>(tot < a.cap_e ? tot : a.cap_e);
+    if (tb + TE < a.cap_t) a.off[tb + TE] = v;
+    a.off[a.cap_t] = v;
+    if (tot > a.cap_e) atomicOr(a.overflow, 1);
   }
   // hop 0: the roots are occurrences 0..B-1 (S_1 begins with the distinct roots)
   if (a.h == 0 && row >= 0) atomicMin(reinterpret_cast<unsigned long long*>(&a.first[row]), gcn_key(stamp, 0, t));
   // the block's edges [prefix, prefix + total): target by a binary search of the block's
-  // inclusive offsets; 8 edges per thread per pass, loads of a pass issued together
-  const int64_t base_occ = a.h == 0 ? a.B : 0;
+  // inclusive offsets; 8 edges per thread per pass, loads and counter atomics of a pass
+  // issued together
   constexpr int U = 8;
   for (int i0 = tid; i0 < total; i0 += 256 * U) {
     int32_t v[U], tl[U];
@@ -250,16 +259,22 @@ __global__ __launch_bounds__(256) void gcn_expand_kernel(GcnHop a) {
         e[u] = prefix + i;
       }
     }
-    int32_t tg[U];
+    int32_t tg[U], old[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) tg[u] = v[u] >= 0 ? a.tag[v[u]] : stamp;
+    for (int u = 0; u < U; ++u) {
+      tg[u] = stamp;
+      old[u] = 1;
+      if (v[u] >= 0) {
+        tg[u] = a.tag[v[u]];
+        old[u] = atomicAdd(&a.cntw[v[u]], 1);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (e[u] < 0) continue;
       a.enode[e[u]] = v[u];
       a.etgt[e[u]] = static_cast<int32_t>(tb + tl[u]);
-      if (v[u] >= 0 && tg[u] != stamp)
-        atomicMin(reinterpret_cast<unsigned long long*>(&a.first[v[u]]), gcn_key(stamp, a.h, base_occ + e[u]));
+      a.eflag[e[u]] = static_cast<uint8_t>(old[u] == 0 ? (tg[u] != stamp ? 3 : 1) : 0);
     }
   }
 }
@@ -274,15 +289,27 @@ __global__ __launch_bounds__(256) void gcn_mark_kernel(GcnHop a) {
   const int32_t stamp = a.stamp[0];
   const int64_t o = static_cast<int64_t>(blockIdx.x) * 256 + tid;
   const int64_t base_occ = a.h == 0 ? a.B : 0;
-  const int64_t total_e = a.off[a.cap_t];
+  const int64_t n_occ = base_occ + a.off[a.cap_t];
+  // the grid covers the capacity; blocks past the last occurrence exit (nothing reads them)
+  const int64_t lastb = n_occ > 0 ? (n_occ - 1) / 256 : 0;
+  if (static_cast<int64_t>(blockIdx.x) > lastb) return;
   int32_t v = -1;
+  bool isf = false;
   if (o < base_occ) {
     const int32_t r = a.roots[o];
     v = (r >= 0 && r < a.g.num_rows) ? r : -1;
-  } else if (o - base_occ < total_e) {
-    v = a.enode[o - base_occ];
+    isf = v >= 0 && a.first[v] == gcn_key(stamp, 0, o);
+  } else if (o < n_occ) {
+    const int64_t e = o - base_occ;
+    if (a.eflag[e] & 2) {
+      v = a.enode[e];
+      // hop 0: a root reached as a neighbour is already S_1's (the roots come first); a
+      // root's key this step is (stamp, hop 0, occurrence < B) — the all-ones initial key
+      // shares stamp 0's high word but not the occurrence
+      const uint64_t k = a.first[v];
+      isf = a.h != 0 || (k >> 32) != (gcn_key(stamp, 0, 0) >> 32) || (k & 0xFFFFFFFFu) >= static_cast<uint64_t>(a.B);
+    }
   }
-  const bool isf = v >= 0 && a.first[v] == gcn_key(stamp, a.h, o);
   int total = 0;
   const int incl = block_scan_incl(isf ? 1 : 0, lds4, &total);
   if (tid < 64) {
@@ -302,14 +329,15 @@ __global__ __launch_bounds__(256) void gcn_mark_kernel(GcnHop a) {
       atomicOr(a.overflow, 1);
     }
   }
-  if (blockIdx.x == gridDim.x - 1 && tid == 255) {
+  if (static_cast<int64_t>(blockIdx.x) == lastb && tid == 255) {
     const int64_t n = base_pos + s_prefix + incl;
     a.cnt[a.h + 1] = static_cast<int32_t>(n < a.cap_n ? n : a.cap_n);
   }
 }
 
 // ----------------------------------------------------------------------------
-// place: edge sources, self loops, per-source in-block counts
+// place: edge sources, self loops, per-source in-block counts (one atomic per distinct
+// source, from its counter claimer, + one per self loop)
 // ----------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void gcn_place_kernel(GcnHop a) {
   const int32_t stamp = a.stamp[0];
@@ -321,9 +349,14 @@ __global__ __launch_bounds__(256) void gcn_place_kernel(GcnHop a) {
     if (i < a.cap_e) {
       if (i >= total_e) continue;
       const int32_t v = a.enode[i];
+      const uint8_t f = a.eflag[i];
       const int32_t s = (v >= 0 && a.tag[v] == stamp) ? a.pos[v] : -1;
       a.esrc[i] = s;
-      if (s >= 0) atomicAdd(&a.deg_s[s], 1);
+      if (f & 1) {  // the counter claimer: the node's edges of this hop, then reset
+        const int32_t c = a.cntw[v];
+        a.cntw[v] = 0;
+        if (s >= 0) atomicAdd(&a.deg_s[s], c);
+      }
     } else {
       const int64_t t = i - a.cap_e;
       if (t >= nt || !a.self_loops) continue;
@@ -953,7 +986,7 @@ int64_t eh_gcn_mark_blocks(const GcnHop* a) { return ceil_div((a->h == 0 ? a->B 
 
 static bool gcn_hop_ok(const GcnHop* a) {
   return a && a->g.indptr && a->g.nbr && a->set && a->cnt && a->off && a->enode && a->etgt && a->esrc && a->deg_s &&
-         a->first && a->tag && a->pos && a->scan_deg && a->scan_flag && a->stamp && a->overflow && a->err &&
+         a->first && a->cntw && a->eflag && a->tag && a->pos && a->scan_deg && a->scan_flag && a->stamp && a->overflow && a->err &&
          a->cap_t > 0 && a->cap_t % 256 == 0 && a->cap_e > 0 && a->cap_n > 0 && a->g.num_types >= 1 &&
          a->g.num_types <= 32 && (a->h > 0 || (a->roots && a->rself && a->B > 0 && a->B <= a->cap_t)) &&
          a->cap_e + a->B < (1ll << 31) && a->cap_n < (1ll << 31);

@@ -9,10 +9,12 @@
 //
 //   per hop h (targets -> the next node set), three launches:
 //     expand  degree + look-back scan of the targets' edge offsets, the neighbour list,
-//             first-occurrence claims (epoch-keyed 64-bit atomicMin per node)
-//     mark    first occurrences -> look-back scan -> new set positions (node -> position
-//             table, stamped with the step's epoch: no table is ever cleared)
-//     place   every edge's source position, the per-source in-block counts (GCN norm)
+//             one returning atomicAdd per edge on its node's counter (the edge that sees 0
+//             claims the node: its count and, when unplaced, its new set position)
+//     mark    claims -> look-back scan -> new set positions (node -> position table,
+//             stamped with the step's epoch: no table is ever cleared)
+//     place   every edge's source position; each claimer adds its node's final count to
+//             the in-block source degree (GCN norm) and resets the counter
 //   layer     (L = 2) the outer conv: edge-parallel weighted aggregation into LDS, MFMA
 //             linear + ReLU -> h1, the aggregate kept for dW
 //   head      the last conv + fc + out_fc + loss + the whole row-local backward + the
@@ -23,7 +25,9 @@
 // then the flat optimizer (optim.hip).
 //
 // Node sets are nested (S_1 ⊂ S_2) and ordered targets-first: S_{h+1} = [S_h, new
-// neighbours in first-occurrence order], so a node keeps its position once placed.  Hop
+// neighbours in the edge order of their claims], so a node keeps its position once placed
+// (which of a node's edges claims it is a race: the order of the new nodes is not fixed
+// across runs; every per-target sum still runs over the same edges in edge order).  Hop
 // 0's targets are the B roots as drawn (repeats kept); S_1 starts with the distinct roots.
 // Sets are permutations of the reference's unique([neighbours, targets]) sets, and every
 // per-target sum runs over the same edges, so the loss equals the generic device path's.
@@ -73,7 +77,11 @@ struct GcnHop {
   int32_t* esrc;           // [cap_e] source position (-1: padding)
   int32_t* deg_s;          // [cap_n] in-block source counts (self loops included)
   int32_t* rself;          // hop 0: [B] the set position of each root (its self-loop source)
-  uint64_t* first;         // [N] epoch-keyed first occurrence
+  uint64_t* first;         // [N] epoch-keyed first occurrence of a root (hop 0)
+  int32_t* cntw;           // [N] per-node edge counters of the running hop (zero between hops:
+                           //     each node's counter claimer resets it in place)
+  uint8_t* eflag;          // [cap_e] bit 0: the edge took its node's counter first (the
+                           //     counter claimer), bit 1: ... and the node is not yet placed
   int32_t* tag;            // [N] epoch of a node's placement
   int32_t* pos;            // [N] position of a placed node
   uint64_t* scan_deg;      // look-back words of the degree scan [expand blocks]

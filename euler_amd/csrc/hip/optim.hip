@@ -21,7 +21,7 @@ namespace euler_hip {
 struct FlatOptArgs {
   float *p, *m, *v;
   const float* g;
-  int64_t n;     // elements (the scalar kernel) / float4 groups (the vector kernel)
+  int64_t n;     // elements
   int64_t base;  // index of element 0 in the whole buffer (decay range)
   int64_t* step;
   int32_t* ticket;  // null: the step is advanced by step_inc_kernel before the launch
@@ -81,12 +81,14 @@ __global__ __launch_bounds__(256) void flat_optim_kernel(FlatOptArgs a) {
   flat_step_ticket(a);
 }
 
-// float4 form for the bulk of the flat buffer: 16-byte loads / stores of p, g, m, v, all
-// four loads issued before the math (the update is bandwidth-bound: 28 B per parameter)
+// float4 form: 16-byte loads / stores of p, g, m, v, all four loads issued before the math
+// (the update is bandwidth-bound: 28 B per parameter).  a.n counts ELEMENTS; thread i owns
+// elements [4i, 4i + 4) and the last thread takes a ragged tail element-wise, so one launch
+// covers any length
 __global__ __launch_bounds__(256) void flat_optim4_kernel(FlatOptArgs a) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const float t = static_cast<float>(a.step[0] + a.step_bias);
-  if (i < a.n) {
+  if (4 * i + 4 <= a.n) {
     float4_t pv = reinterpret_cast<float4_t*>(a.p)[i];
     const float4_t gv = reinterpret_cast<const float4_t*>(a.g)[i];
     float4_t mv = a.kind == 0 || a.kind == 3 ? reinterpret_cast<float4_t*>(a.m)[i] : float4_t{0.f, 0.f, 0.f, 0.f};
@@ -102,6 +104,14 @@ __global__ __launch_bounds__(256) void flat_optim4_kernel(FlatOptArgs a) {
     reinterpret_cast<float4_t*>(a.p)[i] = pv;
     if (a.kind == 0 || a.kind == 3) reinterpret_cast<float4_t*>(a.m)[i] = mv;
     if (a.kind == 0 || a.kind == 1) reinterpret_cast<float4_t*>(a.v)[i] = vv;
+  } else {
+    for (int64_t e = 4 * i; e < a.n; ++e) {
+      float pc = a.p[e], mc = a.m[e], vc = a.v[e];
+      optim_one(pc, a.g[e], mc, vc, t, a.lr, a.b1, a.b2, a.eps, flat_wd(a, a.base + e), a.grad_scale, a.kind);
+      a.p[e] = pc;
+      if (a.kind == 0 || a.kind == 3) a.m[e] = mc;
+      if (a.kind == 0 || a.kind == 1) a.v[e] = vc;
+    }
   }
   flat_step_ticket(a);
 }
@@ -217,28 +227,16 @@ hipError_t eh_flat_optim2(float* p, const float* g, float* m, float* v, int64_t 
     return hipGetLastError();
   }
   FlatOptArgs a{p, m, v, g, 0, 0, step, ticket, ticket ? 1 : 0, 1, lr, b1, b2, eps, wd, wd2, grad_scale, w0, w1, kind};
-  // 16-byte aligned buffers (torch allocations; offset 0): the float4 kernel covers the
-  // first n - n % 4 parameters, the scalar kernel the tail
+  // 16-byte aligned buffers (torch allocations; offset 0): one float4 launch (ragged tail
+  // included); otherwise the scalar kernel
   const bool al = (reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
                    reinterpret_cast<uintptr_t>(v)) % 16 == 0;
-  const int64_t n4 = al ? n / 4 : 0;
-  const int64_t done = n4 * 4;
-  if (n4 > 0) {
-    FlatOptArgs b = a;
-    b.n = n4;
-    b.advance = done == n;  // the tail kernel advances the step when there is a tail
-    hipLaunchKernelGGL(flat_optim4_kernel, dim3(static_cast<uint32_t>(ceil_div(n4, 256))), dim3(256), 0, s, b);
-  }
-  if (done < n) {
-    FlatOptArgs b = a;
-    b.p += done;
-    b.g += done;
-    b.m += done;
-    b.v += done;
-    b.n = n - done;
-    b.base = done;
-    hipLaunchKernelGGL(flat_optim_kernel, dim3(static_cast<uint32_t>(ceil_div(n - done, 256))), dim3(256), 0, s, b);
-  }
+  FlatOptArgs b = a;
+  b.n = n;
+  if (al)
+    hipLaunchKernelGGL(flat_optim4_kernel, dim3(static_cast<uint32_t>(ceil_div(ceil_div(n, 4), 256))), dim3(256), 0, s, b);
+  else
+    hipLaunchKernelGGL(flat_optim_kernel, dim3(static_cast<uint32_t>(ceil_div(n, 256))), dim3(256), 0, s, b);
   return hipGetLastError();
 }
 

@@ -12,8 +12,9 @@ ReLU after each conv, ``fc`` + ``out_fc`` and the sigmoid cross-entropy of
 What one step launches (L = 2 convs; 1 + 3 L + 4 + the optimizer = 12):
 
 * the root draw (alias table, Philox stream 1 of the graph's (seed, counter));
-* per hop: expand (degrees, look-back scan, neighbour list, first-occurrence claims),
-  mark (positions of the new nodes), place (edge sources, in-block source counts);
+* per hop: expand (degrees, look-back scan, neighbour list, one counter atomic per edge
+  whose first taker claims the node), mark (positions of the new nodes), place (edge
+  sources, in-block source counts from the claimers);
 * the outer conv: edge-parallel aggregation + MFMA linear + ReLU;
 * the head: last conv, fc, out_fc, loss, F1 counts and the whole row-local backward, the
   weight-gradient partials of its rows and d(agg) of the roots;
@@ -25,7 +26,8 @@ What one step launches (L = 2 convs; 1 + 3 L + 4 + the optimizer = 12):
 The generic path (``models/full_trainer.py``) runs the user's convolution modules on
 ``DeviceFullFlow`` blocks: ~100 launches per step.  Both draw the same roots from the same
 graph RNG state and build the same node sets (in a different order: here each set is the
-previous one followed by its new neighbours), so their losses agree to bf16 rounding;
+previous one followed by its new neighbours in claim order), so their losses agree to bf16
+rounding;
 ``tests/test_gcn_trainer.py`` checks that and an fp32 oracle.
 
 Capacities: the flow's edge / node-set caps come from ``dataflow/device_flow.py``
@@ -60,12 +62,15 @@ class GcnFlowCaps:
             caps = bounded_caps(graph, self.masks, self.B, *_bounded_args(caps))
         self.caps = [(int(e), int(n)) for e, n in caps]
         self.overflow = torch.zeros(1, dtype=torch.int32, device=graph.device)
+        self.on_clear = None  # the plan's node-counter reset (a discarded step may leave some set)
 
     def overflowed(self) -> bool:
         return int(self.overflow.item()) != 0
 
     def clear(self):
         self.overflow.zero_()
+        if self.on_clear is not None:
+            self.on_clear()
 
     def check(self):
         if self.overflowed():
@@ -75,7 +80,7 @@ class GcnFlowCaps:
         exact = exact_caps(self.g, self.masks, self.B)
         self.caps = [(min(ex_e, _round_up(int(e * factor))), min(ex_n, _round_up(int(n * factor))))
                      for (e, n), (ex_e, ex_n) in zip(self.caps, exact)]
-        self.overflow.zero_()
+        self.clear()
         return self.caps
 
 
@@ -187,6 +192,7 @@ class GcnTrainer(CapturedTrainer):
         if L == 2:
             d.update({"H1": int(w[1].shape[0]), "w1": w[1].detach(), "g_w1": w[1].grad})
         self.plan = hip().GcnPlan(d)
+        self.flow.on_clear = self.plan.reset_counters
         self._plan_caps = list(self.flow.caps)
 
     # ------------------------------------------------------------------ step
