@@ -154,7 +154,9 @@ __device__ __forceinline__ int32_t masked_nbr(const GcnGraph& g, int32_t row, ui
 
 // ----------------------------------------------------------------------------
 // expand: targets' degrees -> offsets (look-back) -> edge list + first-occurrence claims.
-// kGcnExpandT targets per block; the block's edges are spread over all 256 threads, 8 per
+// te = gcn_expand_tile(cap_t) <= kGcnExpandT targets per block (small hops get small tiles,
+// so a hop of a few hundred targets still spreads over ~128 blocks and its hubs' edge
+// lists over many CUs); the block's edges are spread over all 256 threads, 8 per
 // thread per pass with every load of a pass in flight.  Hop 0's launch also carries the
 // weight-staging blocks (GcnHop.st: fp32 masters -> padded bf16 images for the layer and
 // head launches, which then copy them to LDS with 16-byte loads).
@@ -173,16 +175,16 @@ __device__ void gcn_stage_blocks(const GcnHop& a, int sb, int nsb) {
 }
 
 __global__ __launch_bounds__(256) void gcn_expand_kernel(GcnHop a) {
-  constexpr int TE = kGcnExpandT;
+  const int TE = gcn_expand_tile(a.cap_t);
   const int nexp = static_cast<int>(ceil_div(a.cap_t, TE));
   if (static_cast<int>(blockIdx.x) >= nexp) {  // weight staging (hop 0 only)
     gcn_stage_blocks(a, blockIdx.x - nexp, gridDim.x - nexp);
     return;
   }
   __shared__ int lds4[4];
-  __shared__ int s_incl[TE];
-  __shared__ int32_t s_row[TE];
-  __shared__ int64_t s_start[TE];
+  __shared__ int s_incl[kGcnExpandT];
+  __shared__ int32_t s_row[kGcnExpandT];
+  __shared__ int64_t s_start[kGcnExpandT];
   __shared__ int64_t s_prefix;
   const int tid = threadIdx.x;
   const int32_t stamp = a.stamp[0];
@@ -222,13 +224,18 @@ __global__ __launch_bounds__(256) void gcn_expand_kernel(GcnHop a) {
     const int64_t excl = prefix + incl - deg;
     a.off[t] = static_cast<int32_t>(excl < a.cap_e ? excl : a.cap_e);
   }
-  if (static_cast<int>(blockIdx.x) == lastb && tid == 0) {
-    // the end offset: read at the end of this block's last tile and as the hop's total
+  if (static_cast<int>(blockIdx.x) == lastb && tid < 64) {
+    // the end offset, read as the hop's total (off[cap_t]) and as the end of the last
+    // aggregation tile (16 targets, which may reach past this block when te < 16): every
+    // entry up to the next multiple of 64 beyond the block
     const int64_t tot = prefix + total;
     const int32_t v = static_cast<int32_t>(tot < a.cap_e ? tot : a.cap_e);
-    if (tb + TE < a.cap_t) a.off[tb + TE] = v;
-    a.off[a.cap_t] = v;
-    if (tot > a.cap_e) atomicOr(a.overflow, 1);
+    const int64_t te_end = tb + TE + tid;
+    if (te_end < a.cap_t && te_end <= ((tb + TE + 63) & ~int64_t{63})) a.off[te_end] = v;
+    if (tid == 0) {
+      a.off[a.cap_t] = v;
+      if (tot > a.cap_e) atomicOr(a.overflow, 1);
+    }
   }
   // hop 0: the roots are occurrences 0..B-1 (S_1 begins with the distinct roots)
   if (a.h == 0 && row >= 0) atomicMin(reinterpret_cast<unsigned long long*>(&a.first[row]), gcn_key(stamp, 0, t));
@@ -386,29 +393,47 @@ struct AggTile {
   static constexpr int LDA = KP + 1;     // fp32 accumulator row stride (bank spread)
 };
 
-__device__ __forceinline__ void gcn_row8(const GcnAggSrc& s, int32_t row, int c, float* x) {
-  const int col = c * 8;
-  if (row < 0 || col >= s.cols) {
+// one row chunk (8 columns) as loaded: bf16 rows stay packed (4 dwords) until they are
+// accumulated, so a worker keeps twice as many rows in flight in the same registers
+template <bool F32>
+struct RowRaw {
+  uint32_t w[F32 ? 8 : 4];
+};
+
+template <bool F32>
+__device__ __forceinline__ void row_load(const GcnAggSrc& s, int32_t row, int c, RowRaw<F32>& r) {
+  if (row < 0 || c * 8 >= s.cols) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) x[j] = 0.f;
+    for (int j = 0; j < (F32 ? 8 : 4); ++j) r.w[j] = 0u;
     return;
   }
-  if (s.x_fp32) {
-    const float* p = static_cast<const float*>(s.x) + static_cast<int64_t>(row) * s.ld + col;
-    const float4_t lo = *reinterpret_cast<const float4_t*>(p);
-    const float4_t hi = *reinterpret_cast<const float4_t*>(p + 4);
+  if constexpr (F32) {
+    const float* p = static_cast<const float*>(s.x) + static_cast<int64_t>(row) * s.ld + c * 8;
+    const uint4_t lo = *reinterpret_cast<const uint4_t*>(p);
+    const uint4_t hi = *reinterpret_cast<const uint4_t*>(p + 4);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      x[j] = lo[j];
-      x[4 + j] = hi[j];
+      r.w[j] = lo[j];
+      r.w[4 + j] = hi[j];
     }
   } else {
-    const uint4_t v = *reinterpret_cast<const uint4_t*>(static_cast<const bf16_t*>(s.x) +
-                                                       static_cast<int64_t>(row) * s.ld + col);
+    const uint4_t v =
+        *reinterpret_cast<const uint4_t*>(static_cast<const bf16_t*>(s.x) + static_cast<int64_t>(row) * s.ld + c * 8);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r.w[j] = v[j];
+  }
+}
+
+template <bool F32>
+__device__ __forceinline__ void row_axpy(const RowRaw<F32>& r, float w, float* run) {
+  if constexpr (F32) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) run[j] += w * __uint_as_float(r.w[j]);
+  } else {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      x[2 * j] = __uint_as_float(v[j] << 16);
-      x[2 * j + 1] = __uint_as_float(v[j] & 0xffff0000u);
+      run[2 * j] += w * __uint_as_float(r.w[j] << 16);
+      run[2 * j + 1] += w * __uint_as_float(r.w[j] & 0xffff0000u);
     }
   }
 }
@@ -416,11 +441,15 @@ __device__ __forceinline__ void gcn_row8(const GcnAggSrc& s, int32_t row, int c,
 // enode: neighbour node ids of the hop (by-id sources read row = enode[e]); self_src:
 // nullable (target t's self-loop source is t) ; nt: real targets
 // per-target prelude (threads < 16, once per tile): rsqrt of the target degree, the self
-// loop's source and source row, so the self items of the main loop need no extra round
-template <int KP>
-__device__ void gcn_aggregate(const GcnAggSrc& src, const int32_t* off, const int32_t* etgt, const int32_t* esrc,
-                              const int32_t* enode, const int32_t* deg_s, const int32_t* self_src, int self_loops,
-                              int64_t t0, int nt, float* acc, float* rdt, int* sself) {
+// loop's source and source row, so the self items of the main loop need no extra round.
+// Each worker (NCH lanes, one per 8 columns) walks a contiguous slice of the tile's edges,
+// U per batch, software-pipelined: the next batch's index loads are in flight while the
+// current batch's rows are accumulated, and its rows (+ source degrees) are issued before
+// the loop comes back — one memory round trip per batch instead of two.
+template <int KP, bool F32>
+__device__ void gcn_aggregate_t(const GcnAggSrc& src, const int32_t* off, const int32_t* etgt, const int32_t* esrc,
+                                const int32_t* enode, const int32_t* deg_s, const int32_t* self_src, int self_loops,
+                                int64_t t0, int nt, float* acc, float* rdt, int* sself) {
   using AT = AggTile<KP>;
   const int tid = threadIdx.x;
   for (int i = tid; i < kGT * AT::LDA; i += 256) acc[i] = 0.f;
@@ -445,7 +474,7 @@ __device__ void gcn_aggregate(const GcnAggSrc& src, const int32_t* off, const in
   const int g = tid / AT::NCH, c = tid % AT::NCH;
   const int64_t per = (W + AT::NW - 1) / AT::NW;
   const int64_t i0 = g * per, i1 = (i0 + per) < W ? (i0 + per) : W;
-  constexpr int U = 8;
+  constexpr int U = F32 ? 4 : 8;  // the same 32 dwords of rows in flight per batch
   float run[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   int cur = -1;
   auto flush = [&]() {
@@ -456,48 +485,74 @@ __device__ void gcn_aggregate(const GcnAggSrc& src, const int32_t* off, const in
 #pragma unroll
     for (int j = 0; j < 8; ++j) run[j] = 0.f;
   };
-  for (int64_t i = i0; i < i1; i += U) {
-    int tl[U], s[U], row[U];
+  auto load_idx = [&](int64_t i, int* tl, int* sv, int* row) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t ii = i + u;
       tl[u] = -1;
-      s[u] = -1;
+      sv[u] = -1;
       row[u] = -1;
       if (ii < i1) {
         if (ii < E) {
           const int64_t e = e0 + ii;
           tl[u] = static_cast<int>(etgt[e] - t0);
-          s[u] = esrc[e];
-          row[u] = src.by_id ? enode[e] : s[u];
+          sv[u] = esrc[e];
+          row[u] = src.by_id ? enode[e] : sv[u];
         } else {
           tl[u] = static_cast<int>(ii - E);
-          s[u] = sself[tl[u]];
+          sv[u] = sself[tl[u]];
           row[u] = s_row[tl[u]];
         }
       }
     }
-    float x[U][8];
-    float ds[U];
+  };
+  auto load_rows = [&](const int* sv, const int* row, float* ds, RowRaw<F32>* x) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      ds[u] = s[u] >= 0 ? static_cast<float>(deg_s[s[u]]) : 1.f;
-      gcn_row8(src, s[u] >= 0 ? row[u] : -1, c, x[u]);
+      ds[u] = sv[u] >= 0 ? static_cast<float>(deg_s[sv[u]]) : 1.f;
+      row_load<F32>(src, sv[u] >= 0 ? row[u] : -1, c, x[u]);
     }
+  };
+  int tl0[U], s0[U], r0[U];
+  float ds0[U];
+  RowRaw<F32> x0[U];
+  if (i0 < i1) {
+    load_idx(i0, tl0, s0, r0);
+    load_rows(s0, r0, ds0, x0);
+  }
+  for (int64_t i = i0; i < i1; i += U) {
+    int tl1[U], s1[U], r1[U];
+    const bool more = i + U < i1;
+    if (more) load_idx(i + U, tl1, s1, r1);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (tl[u] < 0 || s[u] < 0) continue;
-      if (tl[u] != cur) {
+      if (tl0[u] < 0 || s0[u] < 0) continue;
+      if (tl0[u] != cur) {
         flush();
-        cur = tl[u];
+        cur = tl0[u];
       }
-      const float w = rdt[tl[u]] * rsqrtf(ds[u]);
+      row_axpy<F32>(x0[u], rdt[tl0[u]] * rsqrtf(ds0[u]), run);
+    }
+    if (!more) break;
+    load_rows(s1, r1, ds0, x0);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) run[j] += w * x[u][j];
+    for (int u = 0; u < U; ++u) {
+      tl0[u] = tl1[u];
+      s0[u] = s1[u];
     }
   }
   flush();
   __syncthreads();
+}
+
+template <int KP>
+__device__ void gcn_aggregate(const GcnAggSrc& src, const int32_t* off, const int32_t* etgt, const int32_t* esrc,
+                              const int32_t* enode, const int32_t* deg_s, const int32_t* self_src, int self_loops,
+                              int64_t t0, int nt, float* acc, float* rdt, int* sself) {
+  if (src.x_fp32)
+    gcn_aggregate_t<KP, true>(src, off, etgt, esrc, enode, deg_s, self_src, self_loops, t0, nt, acc, rdt, sself);
+  else
+    gcn_aggregate_t<KP, false>(src, off, etgt, esrc, enode, deg_s, self_src, self_loops, t0, nt, acc, rdt, sself);
 }
 
 // ----------------------------------------------------------------------------
@@ -981,7 +1036,7 @@ using namespace euler_hip;
 
 extern "C" {
 
-int64_t eh_gcn_expand_blocks(int64_t cap_t) { return ceil_div(cap_t, kGcnExpandT); }
+int64_t eh_gcn_expand_blocks(int64_t cap_t) { return ceil_div(cap_t, gcn_expand_tile(cap_t)); }
 int64_t eh_gcn_mark_blocks(const GcnHop* a) { return ceil_div((a->h == 0 ? a->B : 0) + a->cap_e, 256); }
 
 static bool gcn_hop_ok(const GcnHop* a) {

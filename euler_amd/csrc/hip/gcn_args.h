@@ -41,7 +41,14 @@ constexpr int kGcnMaxHops = 2;
 constexpr int kGcnHeadRows = 16;   // roots per head block
 constexpr int kGcnTileRows = 64;   // targets per layer block
 constexpr int kGcnDwRows = 128;    // rows of S_1 per dw block (4 chunks of 32)
-constexpr int kGcnExpandT = 64;    // targets per expand block
+constexpr int kGcnExpandT = 64;    // most targets per expand block
+// targets per expand block for a hop of cap_t targets: a power of two in [4, 64] near
+// cap_t / 1024, so the launch has >= ~128 blocks (expand's edges spread over the chip)
+__host__ __device__ inline int gcn_expand_tile(int64_t cap_t) {
+  int te = 4;
+  while (te < kGcnExpandT && static_cast<int64_t>(te) * 2 * 1024 <= cap_t) te *= 2;
+  return te;
+}
 constexpr int kGcnMaxStage = 4;    // weight images staged per step
 constexpr int kGcnStageBlocks = 64;// extra blocks of hop 0's expand launch that stage them
 
