@@ -607,20 +607,25 @@ void cast_bf16(torch::Tensor x, torch::Tensor out) {
 }
 
 // t = 0: one vector-store kernel (zero_kernel, embed.hip); EULER_AMD_ZERO_MEMSET=1: one
-// hipMemsetAsync instead
+// hipMemsetAsync instead (read per call, so a test can switch it)
 void zero_(torch::Tensor t) {
   dev(t, "t");
   const c10::DeviceGuard g(t.device());
-  static const bool use_memset = [] {
-    const char* e = std::getenv("EULER_AMD_ZERO_MEMSET");
-    return e && e[0] == '1';
-  }();
+  const char* e = std::getenv("EULER_AMD_ZERO_MEMSET");
+  const bool use_memset = e && e[0] == '1';
   const int64_t bytes = t.numel() * t.element_size();
   if (use_memset) {
     ok(hipMemsetAsync(t.data_ptr(), 0, static_cast<size_t>(bytes), stream()), "zero_ (memset)");
     return;
   }
   ok(eh_zero(t.data_ptr(), bytes, stream()), "zero_");
+}
+
+// t = 0 through hipMemsetAsync, always (diagnostics: tests/test_graph_memset.py)
+void memset_zero(torch::Tensor t) {
+  dev(t, "t");
+  const c10::DeviceGuard g(t.device());
+  ok(hipMemsetAsync(t.data_ptr(), 0, static_cast<size_t>(t.numel() * t.element_size()), stream()), "memset_zero");
 }
 
 // one hop's block of the device full-neighbourhood flow (flow.hip flow_block_kernel):
@@ -1003,6 +1008,7 @@ void register_gnn_ops(pybind11::module& m) {
   m.def("cast_bf16", &cast_bf16);
   m.def("drop_rows", &drop_rows);
   m.def("zero_", &zero_);
+  m.def("memset_zero", &memset_zero);
   m.def("seg_count", &seg_count);
   m.def("flow_block", &flow_block);
   m.def("gcn_norm_weight", &gcn_norm_weight);

@@ -750,3 +750,53 @@ def test_deepwalk_estimator_device_path_two_ranks(tmp_path):
     res = _run(_worker_deepwalk_estimator, str(tmp_path / "cora"), str(tmp_path / "ckpt"))
     assert not [r for r in res if r[1] == "error"], res
     assert len(res) == 2 and all(r[2] for r in res), res
+
+
+def _worker_device_trainer_dp(rank, world, port, q, tmp, model, argv, want):
+    """one device-path estimator under 2 gloo ranks (runner flags as under torchrun): the
+    trainer the registry picks, per-rank sample streams, the flat gradient summed through
+    make_grad_sync every step -> bit-identical parameters on every rank"""
+    try:
+        _init(rank, world, port)
+        from euler_amd.tools import runner
+
+        a = runner.parse_args(argv + ["--model_dir", os.path.join(tmp, f"ckpt_{model}_r{rank}"), "--device_graph",
+                                      "--device", "cpu", "--seed", "1"], model=model)
+        _, est = runner.build(a)
+        est.train()
+        tr = est.device_trainer
+        p = tr.logical_params()
+        flat = torch.cat([p[k].reshape(-1).float() for k in sorted(p)])
+        allp = [torch.zeros_like(flat) for _ in range(world)]
+        dist.all_gather(allp, flat)
+        same = all(torch.equal(x, allp[0]) for x in allp)
+        # each rank drew its own batches (different sampler streams)
+        s = tr.samples()
+        drew = None
+        if s is not None:
+            mine = torch.cat([t.reshape(-1).long() for t in s])
+            got = [torch.zeros_like(mine) for _ in range(world)]
+            dist.all_gather(got, mine)
+            drew = not all(torch.equal(g, got[0]) for g in got)
+        ok = same and type(tr).__name__ == want and drew is True and bool(torch.isfinite(flat).all())
+        q.put((rank, f"{model}_dp", bool(ok), type(tr).__name__, drew))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+
+
+@pytest.mark.parametrize("model,argv,want", [
+    ("gcn", ["--dataset", "ppi", "--scale", "0.05", "--batch_size", "16", "--total_step", "4", "--log_steps", "2"],
+     "FullFlowTrainer"),
+    ("transe", ["--scale", "0.05", "--batch_size", "32", "--total_step", "4", "--log_steps", "2", "--dim", "16"],
+     "KGTrainer"),
+    ("gae", ["--scale", "0.05", "--batch_size", "16", "--total_step", "4", "--log_steps", "2", "--dim", "16",
+             "--fanouts", "4", "3"], "GaeTrainer"),
+    ("gin", ["--scale", "0.2", "--batch_size", "8", "--total_step", "4", "--log_steps", "2"], "GraphTrainer"),
+])
+def test_device_trainers_data_parallel_lockstep(tmp_path, model, argv, want):
+    res = _run(_worker_device_trainer_dp, str(tmp_path), model, argv, want)
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == 2 and all(r[2] for r in res), res
