@@ -247,6 +247,13 @@ class Pubmed(_Citation):
     name, num_nodes, feature_dim, label_dim, test_start_num = "pubmed", 19717, 500, 3, 18717
     words_per_node = 50
 
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        self.origin_files = ["data/Pubmed-Diabetes.NODE.paper.tab", "data/Pubmed-Diabetes.DIRECTED.cites.tab"]
+
+    def convert2json(self, d):
+        return _pubmed_tab(self, os.path.join(d, self.origin_files[0]), os.path.join(d, self.origin_files[1]))
+
 
 class PPI(_Citation):
     name, num_nodes, feature_dim, label_dim, test_start_num = "ppi", 56944, 50, 121, 51420
@@ -319,6 +326,59 @@ def _planetoid_like(ds, content, cites):
             t = "train" if s < start and d < start else "train_removed"
             edges += [_edge(s, d, t), _edge(d, s, t)]
     ds._write_ids(range(start, len(ids)))
+    return {"nodes": nodes, "edges": edges}
+
+
+def _pubmed_tab(ds, node_tab, cites_tab):
+    """Pubmed-Diabetes release (reference pubmed.py:38-41 + pubmed_utils.py): node ids in
+    order of first appearance in the DIRECTED citation file (papers that are never cited and
+    cite nothing follow, in node-file order); one directed edge per citation, ``train_removed``
+    when an end is past ``test_start_num``; TF-IDF features in the header's word order,
+    normalised to sum 1; one-hot labels of ``label=1..3``; ``test`` nodes past
+    ``test_start_num`` (the reference's ``id > train_num``), their ids in the id file."""
+    node_map, cites = {}, []
+    with open(cites_tab) as f:
+        for line in f:
+            a = line.strip().split("\t")
+            if len(a) != 4:
+                continue
+            s, t = a[1].split(":", 1)[1], a[3].split(":", 1)[1]
+            for p in (s, t):
+                if p not in node_map:
+                    node_map[p] = len(node_map)
+            cites.append((node_map[s], node_map[t]))
+    words, rows = None, []
+    with open(node_tab) as f:
+        for line in f:
+            a = line.rstrip("\n").split("\t")
+            if len(a) <= 2:
+                continue
+            if a[0].startswith("cat="):  # header: cat=1,2,3:label, numeric:<word>:0.0, ..., string:summary
+                words = {fld.split(":")[-2]: i for i, fld in enumerate(a[1:-1])}
+                continue
+            rows.append(a)
+    if words is None:
+        raise ValueError("%s: no feature header line" % node_tab)
+    start = ds.test_start_num
+    nodes, test_ids = [], []
+    for a in rows:
+        if a[0] not in node_map:
+            node_map[a[0]] = len(node_map)
+        i = node_map[a[0]]
+        one = np.zeros(ds.label_dim)
+        one[int(a[1].split("=")[1]) - 1] = 1.0
+        fv = np.zeros(len(words))
+        for fld in a[2:-1]:
+            k, v = fld.split("=")
+            fv[words[k]] = float(v)
+        fv = fv / (fv.sum() + 1e-7)
+        t = "test" if i > start else "train"
+        if t == "test":
+            test_ids.append(i)
+        nodes.append(_node(i, t, [{"name": "label", "type": "dense", "value": one.tolist()},
+                                  {"name": "feature", "type": "dense", "value": fv.tolist()}]))
+    edges = [_edge(s, t, "train_removed" if s > start or t > start else "train") for s, t in cites]
+    ds._write_ids(test_ids)
     return {"nodes": nodes, "edges": edges}
 
 
