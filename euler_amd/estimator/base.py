@@ -699,8 +699,89 @@ class BaseEstimator:
     def _eval_batches(self):
         return self.evaluate_input_fn()
 
+    # ------------------------------------------------------------------ device-path eval / infer
+    def _device_inference_trainer(self):
+        """the device trainer for evaluate / infer (``device_graph=True``): the live one
+        after a device-path train, else one built on the HBM graph and restored from
+        model_dir; None when its model has no device inference (``infer_logits``), which
+        leaves evaluate / infer on the engine path (reference base_estimator.py:145-179:
+        one model function for train, eval and predict)"""
+        if not self.params.get("device_graph") or self.params.get("device_infer", True) is False:
+            return None
+        tr = getattr(self, "device_trainer", None)
+        if tr is None:
+            try:
+                first = self.get_train_from_input(self.train_input_fn(), self.params)
+                tr = self._device_graph_trainer(first)
+            except (ValueError, NotImplementedError) as e:
+                log.info("no device trainer for %s (%s): engine-path evaluate / infer", type(self.model).__name__, e)
+                return None
+            self._device_restore(tr)
+            self.device_trainer = tr
+        return tr if callable(getattr(tr, "infer_logits", None)) else None
+
+    def _device_evaluate(self, tr):
+        """loss and the model's streaming metric over the eval id batches, every batch's
+        block / tree built and run on the device"""
+        import torch.nn.functional as F
+
+        met = getattr(self.model, "metric", None)
+        if met is not None and hasattr(met, "reset"):
+            met.reset()
+        name = getattr(self.model, "metric_name", getattr(tr, "metric_name", "f1"))
+        losses, res, steps, n, t0 = [], {}, 0, 0, time.time()
+        for batch in self._eval_batches():
+            src = self.get_evaluate_from_input(batch, self.params)
+            try:
+                _, logits, y = tr.infer_logits(src)
+            except NotImplementedError:
+                return None
+            losses.append(float(F.binary_cross_entropy_with_logits(logits, y.float())))
+            value = met(y.detach(), torch.sigmoid(logits).detach()) if met is not None else float("nan")
+            res = {"loss": float(np.mean(losses)), name: float(value)}
+            steps += 1
+            n += int(torch.as_tensor(src).numel())
+            if self.evaluate_stop_onetime:
+                break
+        if self.rank == 0:
+            log.info("evaluate: %s over %d batches (device path, %.1f nodes/s)", res, steps,
+                     n / max(time.time() - t0, 1e-9))
+        return res
+
+    def _device_infer(self, tr):
+        ids_out, emb_out = [], []
+        n, t0 = 0, time.time()
+        for batch in self.infer_input_fn():
+            src = self.get_infer_from_input(batch, self.params)
+            try:
+                emb = tr.infer_embed(src)
+            except NotImplementedError:
+                return None
+            s, e = self.transfer_embedding(src, emb)
+            ids_out.append(np.asarray(torch.as_tensor(s).detach().cpu()))
+            emb_out.append(torch.as_tensor(e).detach().float().cpu().numpy())
+            n += int(torch.as_tensor(src).numel())
+        self.infer_rate = n / max(time.time() - t0, 1e-9)
+        if self.rank == 0:
+            log.info("infer: %d embeddings (device path, %.1f embeddings/s)", n, self.infer_rate)
+        return self._write_infer(ids_out, emb_out)
+
+    def _write_infer(self, ids_out, emb_out):
+        out_dir = self.params.get("infer_dir", self.model_dir)
+        os.makedirs(out_dir, exist_ok=True)
+        ids = np.concatenate(ids_out, 0) if ids_out else np.zeros((0,), np.int64)
+        embs = np.concatenate(emb_out, 0) if emb_out else np.zeros((0, 0), np.float32)
+        np.save(os.path.join(out_dir, "embedding_%d.npy" % self.rank), embs)
+        np.save(os.path.join(out_dir, "ids_%d.npy" % self.rank), ids)
+        return ids, embs
+
     @torch.no_grad()
     def evaluate(self):
+        tr = self._device_inference_trainer()
+        if tr is not None:
+            res = self._device_evaluate(tr)
+            if res is not None:
+                return res
         self.model.to(self.device)
         batches = iter(self._eval_batches())
         first = next(batches, None)
@@ -733,6 +814,11 @@ class BaseEstimator:
 
     @torch.no_grad()
     def infer(self):
+        tr = self._device_inference_trainer()
+        if tr is not None:
+            out = self._device_infer(tr)
+            if out is not None:
+                return out
         self.model.to(self.device)
         self.model.eval()
         ids_out, emb_out = [], []
@@ -748,13 +834,7 @@ class BaseEstimator:
             s, e = self.transfer_embedding(src, emb)
             ids_out.append(np.asarray(torch.as_tensor(s).detach().cpu()))
             emb_out.append(torch.as_tensor(e).detach().float().cpu().numpy())
-        out_dir = self.params.get("infer_dir", self.model_dir)
-        os.makedirs(out_dir, exist_ok=True)
-        ids = np.concatenate(ids_out, 0) if ids_out else np.zeros((0,), np.int64)
-        embs = np.concatenate(emb_out, 0) if emb_out else np.zeros((0, 0), np.float32)
-        np.save(os.path.join(out_dir, "embedding_%d.npy" % self.rank), embs)
-        np.save(os.path.join(out_dir, "ids_%d.npy" % self.rank), ids)
-        return ids, embs
+        return self._write_infer(ids_out, emb_out)
 
     def train_and_evaluate(self):
         res = self.train()

@@ -36,7 +36,28 @@ from euler_amd.dataflow.device_flow import DeviceFullFlow
 from euler_amd.models.captured import CapturedTrainer
 from euler_amd.ops import gnn_ops, mp_ops
 
-__all__ = ["FullFlowTrainer"]
+__all__ = ["FullFlowTrainer", "full_flow_embed", "infer_flow"]
+
+
+def full_flow_embed(gnn, flow, features, roots):
+    """(gnn embedding [B, E], DataFlow) of ``roots`` through the model's convolutions on a
+    device flow (ReLU after every conv, then ``gnn.fc``: BaseGNNNet.forward)"""
+    df = flow.produce(roots)
+    x = mp_ops.gather(features, df[0].n_id).float()
+    for conv, block in zip(gnn.convs, df):
+        x_t = mp_ops.gather(x, block.res_n_id)
+        x = F.relu(gnn.calculate_conv(conv, (x_t, x), block.edge_index, size=block.size))
+    return gnn.fc(x), df
+
+
+def infer_flow(owner, graph, masks, self_loops, n):
+    """a cached exact-capacity DeviceFullFlow of ``n`` roots for inference batches (the
+    last id-file batch is shorter; the GCN normalisation depends on the whole block, so
+    a batch is never padded)"""
+    cache = owner.__dict__.setdefault("_infer_flows", {})
+    if n not in cache:
+        cache[n] = DeviceFullFlow(graph, masks, n, self_loops, "exact")
+    return cache[n]
 
 
 class FullFlowTrainer(CapturedTrainer):
@@ -116,13 +137,33 @@ class FullFlowTrainer(CapturedTrainer):
     # ------------------------------------------------------------------ model
     def _forward(self, roots):
         """logits [B, label_dim] of the roots through the user's convolutions"""
-        df = self.flow.produce(roots)
-        x = mp_ops.gather(self.features, df[0].n_id).float()
-        for conv, block in zip(self.gnn.convs, df):
-            x_t = mp_ops.gather(x, block.res_n_id)
-            x = F.relu(self.gnn.calculate_conv(conv, (x_t, x), block.edge_index, size=block.size))
-        emb = self.gnn.fc(x)
+        emb, df = full_flow_embed(self.gnn, self.flow, self.features, roots)
         return self.model.out_fc(emb).float(), df
+
+    # ------------------------------------------------------------------ inference
+    def _infer_flow(self, n):
+        if not isinstance(self.flow, DeviceFullFlow):
+            return None  # sampled flows: the engine path infers (their draws are the engine's)
+        return infer_flow(self, self.graph, self.flow.masks, self.flow.self_loops, n)
+
+    @torch.no_grad()
+    def infer_logits(self, ids):
+        """(embeddings [n, E], logits [n, C], labels [n, C]) of raw node ids on the device,
+        one full-neighbourhood block of exactly these roots (the engine path's batch)"""
+        flow = self._infer_flow(int(torch.as_tensor(ids).numel()))
+        if flow is None:
+            raise NotImplementedError("device inference covers the full-neighbourhood flow")
+        rows = self.graph.rows_of(ids).to(self.graph.device)
+        self.model.eval()
+        try:
+            emb, _ = full_flow_embed(self.gnn, flow, self.features, rows)
+            logits = self.model.out_fc(emb).float()
+        finally:
+            self.model.train()
+        return emb.float(), logits, self.labels[rows.clamp(min=0)]
+
+    def infer_embed(self, ids):
+        return self.infer_logits(ids)[0]
 
     def _forward_loss(self):
         self._draw()

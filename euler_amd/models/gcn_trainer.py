@@ -227,6 +227,24 @@ class GcnTrainer(CapturedTrainer):
     def samples(self):
         return (self.plan.flow()["roots"],)
 
+    # ------------------------------------------------------------------ inference
+    @torch.no_grad()
+    def infer_logits(self, ids):
+        """(embeddings, logits, labels) of raw node ids: the model's own modules (their
+        parameters are the trained flat buffer's views) on an exact full-neighbourhood block
+        of exactly these roots (models/full_trainer.py full_flow_embed)"""
+        from euler_amd.models.full_trainer import full_flow_embed, infer_flow
+
+        n = int(torch.as_tensor(ids).numel())
+        flow = infer_flow(self, self.graph, self.masks, bool(self.gnn.sampler.add_self_loops), n)
+        rows = self.graph.rows_of(ids).to(self.graph.device)
+        emb, _ = full_flow_embed(self.gnn, flow, self.graph.features, rows)
+        logits = self.model.out_fc(emb).float()
+        return emb.float(), logits, self.labels[rows.clamp(min=0)]
+
+    def infer_embed(self, ids):
+        return self.infer_logits(ids)[0]
+
     # ------------------------------------------------------------------ oracle
     def forward_backward_only(self):
         """plan step without the optimizer (tests): loss_out and the flat gradient"""

@@ -708,9 +708,48 @@ class SageTrainer:
         y.scatter_(1, self.labels[roots.to(self.labels.device)].long().view(-1, 1), 1.0)
         return y
 
+    # ------------------------------------------------------------------ inference
+    def _tree_of(self, roots):
+        """a slotted sample tree (nodes, leaf) of the given rows on the trainer's graph
+        (device sampler on the GPU; Philox streams 8.. so training's streams are untouched)"""
+        g = self.graph
+        level = roots.long()
+        types = lambda m: [t for t in range(g.num_types) if (m >> t) & 1]  # noqa: E731
+        for k in range(1, self.L):
+            f, P = self.fanouts[k - 1], 1 << self.logP[k]
+            nb = g.sample_neighbor(level.int(), f, types(self.masks[k - 1]), -1, stream_id=7 + k).view(-1, f).long()
+            slots = torch.full((level.numel(), P), -1, dtype=torch.int64, device=level.device)
+            slots[:, :f] = nb
+            slots[:, f] = level
+            level = slots.reshape(-1)
+        leaf = g.sample_neighbor(level.int(), self.fanouts[-1], types(self.masks[-1]), -1,
+                                 stream_id=7 + self.L).view(-1, self.fanouts[-1]).long()
+        g.advance()
+        return level, leaf
+
+    @torch.no_grad()
+    def infer_logits(self, ids):
+        """(embeddings [n, E], logits [n, C], labels [n, C]) of raw node ids: a fresh sample
+        tree per root (the reference's infer path samples as its train path does) and the
+        fp32 model on the trained parameters"""
+        rows = self.graph.rows_of(ids).to(self.graph.device)
+        params = self.logical_params()
+        nodes, leaf = self._tree_of(rows.clamp(min=0))
+        emb = self.logical_embed(params, nodes, leaf)
+        logits = emb @ params["out_fc.weight"].float().t().to(emb.device)
+        return emb, logits, self._labels_of(rows.clamp(min=0)).to(emb.device)
+
+    def infer_embed(self, ids):
+        return self.infer_logits(ids)[0]
+
     def logical_forward(self, params, roots, nodes, leaf, table=None):
         """fp32 logits of the model for one sampled slotted tree (``table``: the feature rows
         ``nodes`` / ``leaf`` index; default the whole feature table)"""
+        emb = self.logical_embed(params, nodes, leaf, table)
+        return emb @ params["out_fc.weight"].t()
+
+    def logical_embed(self, params, nodes, leaf, table=None):
+        """fp32 gnn embedding (``gnn.fc`` output) of one sampled slotted tree"""
         dev = params["gnn.fc.weight"].device
         x = (self.features if table is None else table)[:, : self.D].float().to(dev)
         x = torch.cat([x, torch.zeros(1, self.D, device=dev)], 0)
@@ -733,8 +772,7 @@ class SageTrainer:
                 a, c = a + s, c + 1
             wk = torch.cat([params[f"gnn.convs.{k}.self_fc.weight"], params[f"gnn.convs.{k}.neigh_fc.weight"]], 1)
             h = torch.relu(torch.cat([s, a / c], 1) @ wk.t())
-        emb = h @ params["gnn.fc.weight"].t() + params["gnn.fc.bias"]
-        return emb @ params["out_fc.weight"].t()
+        return h @ params["gnn.fc.weight"].t() + params["gnn.fc.bias"]
 
     def reference_loss_and_grads(self, params=None, samples=None):
         """fp32 torch autograd loss and parameter gradients on the last step's samples
