@@ -180,6 +180,24 @@ class Engine {
     return out;
   }
 
+  // one shard's whole graph (API_EXPORT_SHARD): ids, types, weights, indptr, neighbour ids,
+  // edge weights, then one [n][dim] table per dense feature
+  py::list ExportShard(int shard, const std::vector<std::string>& names, const std::vector<int64_t>& dims) {
+    if (names.size() != dims.size()) throw std::invalid_argument("export_shard: one width per feature");
+    std::vector<std::string> attrs(names);
+    for (int64_t d : dims) attrs.push_back(std::to_string(d));
+    std::vector<Tensor> res;
+    Status st;
+    {
+      py::gil_scoped_release nogil;
+      st = proxy_->RunOnShard(shard, "API_EXPORT_SHARD", attrs, 6 + static_cast<int>(names.size()), &res);
+    }
+    Throw(st);
+    py::list out;
+    for (auto& t : res) out.append(ToPy(t));
+    return out;
+  }
+
   std::string Explain(const std::string& gql) {
     std::string s;
     Throw(proxy_->Explain(gql, &s));
@@ -673,6 +691,10 @@ PYBIND11_MODULE(_engine, m) {
       .def("endpoints", [](Engine& e) { return e.Endpoints(); })
       .def("set_replicas", &Engine::SetReplicas, py::arg("shard"), py::arg("endpoints"))
       .def("export_nodes", &Engine::ExportNodes)
+      .def("export_shard", &Engine::ExportShard, py::arg("shard"), py::arg("names") = std::vector<std::string>(),
+           py::arg("dims") = std::vector<int64_t>())
+      .def_property_readonly("shard_num", [](Engine& e) { return e.Proxy()->shard_num(); })
+      .def_property_readonly("mode", [](Engine& e) { return e.Proxy()->mode(); })
       .def("export_edges", &Engine::ExportEdges, py::arg("edge_type"), py::arg("name") = "", py::arg("dim") = 0);
 
   py::class_<PySagePipeline>(m, "SagePipeline")

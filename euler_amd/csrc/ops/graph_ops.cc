@@ -694,6 +694,60 @@ class GetGraphByLabelOp : public OpKernel {
 
 }  // namespace
 
+// ---------------------------------------------------------------- whole-shard export
+// Every node of this shard with its out-adjacency and dense features, for assembling the
+// whole graph in HBM from a sharded / remote cluster (DeviceGraph.from_engine over
+// QueryProxy::RunOnShard).  attrs: dense node feature names followed by as many widths.
+// Outputs: 0 node ids u64 [n], 1 types i32 [n], 2 weights f32 [n], 3 indptr i64 [n*T + 1]
+// over (row, edge type) segments, 4 neighbour ids u64 [E], 5 edge weights f32 [E],
+// 6.. one f32 [n][width] table per feature (missing rows / short rows zero-filled).
+class ExportShardOp : public OpKernel {
+ public:
+  void Compute(const NodeDef& nd, OpContext* ctx) override {
+    Graph& g = G(ctx);
+    const int64_t n = g.num_nodes(), T = g.num_edge_types();
+    if (nd.attrs.size() % 2 != 0) EULER_THROW("API_EXPORT_SHARD: attrs = feature names then widths");
+    const Adjacency& A = g.adj(true);
+    std::vector<int32_t> types(n);
+    std::vector<float> nw(n);
+    for (int64_t r = 0; r < n; ++r) {
+      types[r] = g.NodeType(r);
+      nw[r] = g.NodeWeight(r);
+    }
+    std::vector<int64_t> indptr(A.indptr.begin(), A.indptr.end());
+    std::vector<float> w(A.nbr.size());
+    ThreadPool::Default()->ParallelFor(n * T, 4096, [&](int64_t b, int64_t e) {
+      for (int64_t s = b; s < e; ++s)
+        for (uint64_t k = A.indptr[s]; k < A.indptr[s + 1]; ++k) w[k] = A.EdgeWeight(k, A.indptr[s]);
+    });
+    ctx->Set(nd.Output(0), Tensor::FromVector(g.node_ids()));
+    ctx->Set(nd.Output(1), Tensor::FromVector(types));
+    ctx->Set(nd.Output(2), Tensor::FromVector(nw));
+    ctx->Set(nd.Output(3), Tensor::FromVector(indptr));
+    ctx->Set(nd.Output(4), Tensor::FromVector(A.nbr));
+    ctx->Set(nd.Output(5), Tensor::FromVector(w));
+    const size_t nf = nd.attrs.size() / 2;
+    for (size_t f = 0; f < nf; ++f) {
+      const int64_t dim = std::stoll(nd.attrs[nf + f]);
+      const FeatureInfo* fi = g.meta().NodeFeature(nd.attrs[f]);
+      if (!fi || fi->type != kDense) EULER_THROW("no dense node feature named " + nd.attrs[f]);
+      const Column<float>* c = g.NodeDense(fi->idx);
+      std::vector<float> out(static_cast<size_t>(n * dim), 0.f);
+      ThreadPool::Default()->ParallelFor(n, 1024, [&](int64_t b, int64_t e) {
+        for (int64_t r = b; r < e; ++r) {
+          const float* p = nullptr;
+          int64_t k = 0;
+          if (c) c->Get(r, &p, &k);
+          if (k > dim) k = dim;
+          if (k > 0) memcpy(out.data() + r * dim, p, k * 4);
+        }
+      });
+      ctx->Set(nd.Output(6 + static_cast<int>(f)), Tensor::FromVector(out, {n, dim}));
+    }
+  }
+};
+
+REGISTER_OP_KERNEL("API_EXPORT_SHARD", ExportShardOp);
 REGISTER_OP_KERNEL("API_GET_NODE", GetNodeOp);
 REGISTER_OP_KERNEL("API_GET_EDGE", GetEdgeOp);
 REGISTER_OP_KERNEL("API_SAMPLE_NODE", SampleNodeOp);

@@ -1,5 +1,7 @@
 #include "rpc/rpc.h"
 
+#include <future>
+
 #include <arpa/inet.h>
 #include <errno.h>
 #include <netdb.h>
@@ -1641,6 +1643,37 @@ Status QueryProxy::RunOp(const std::string& op, const std::vector<std::string>& 
   for (int k = 0; k < output_num; ++k) outs.push_back("__result:" + std::to_string(k));
   ScopedMicros t(&ctr.exec_us);
   return ExecuteDag(&env_, phys, inputs, outs, results);
+}
+
+Status QueryProxy::RunOnShard(int shard, const std::string& op, const std::vector<std::string>& attrs,
+                              int output_num, std::vector<Tensor>* results) {
+  DAGDef dag;
+  NodeDef nd;
+  nd.op = op;
+  nd.id = 1;
+  nd.attrs = attrs;
+  nd.output_num = output_num;
+  dag.nodes = {nd};
+  std::vector<std::string> outs;
+  for (int k = 0; k < output_num; ++k) outs.push_back(nd.Output(k));
+  if (mode_ == "remote") {
+    if (!clients_ || shard < 0 || shard >= clients_->num_shards()) return Status::InvalidArgument("no such shard");
+    std::promise<std::pair<Status, std::vector<Tensor>>> pr;
+    auto fut = pr.get_future();
+    clients_->Execute(shard, dag, {}, outs, [&pr](Status st, std::vector<Tensor> t) {
+      pr.set_value({st, std::move(t)});
+    });
+    auto r = fut.get();
+    if (!r.first.ok()) return r.first;
+    *results = std::move(r.second);
+    return Status::OK();
+  }
+  if (mode_ == "local_sharded") {
+    if (shard < 0 || shard >= static_cast<int>(shard_envs_.size())) return Status::InvalidArgument("no such shard");
+    return ExecuteDag(shard_envs_[shard].get(), dag, {}, outs, results);
+  }
+  if (shard != 0 || !graph_) return Status::InvalidArgument("local mode has one shard (0)");
+  return ExecuteDag(&env_, dag, {}, outs, results);
 }
 
 Status QueryProxy::Explain(const std::string& gql, std::string* out) {

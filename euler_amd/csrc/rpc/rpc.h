@@ -246,6 +246,11 @@ class QueryProxy {
   Status Run(const std::string& gql, const std::vector<std::pair<std::string, Tensor>>& inputs,
              const std::vector<std::string>& outputs, std::vector<Tensor>* results);
   Status Explain(const std::string& gql, std::string* out);
+  // one op against ONE shard's own data (no compiler rewrite, no split / merge): local mode
+  // runs it on the in-process graph (shard 0), local_sharded on that shard's env, remote
+  // mode over that shard's RPC replicas
+  Status RunOnShard(int shard, const std::string& op, const std::vector<std::string>& attrs, int output_num,
+                    std::vector<Tensor>* results);
   // single-op query (reference Query(op, alias, n_out, inputs, attrs)), sharded like a GQL step
   Status RunOp(const std::string& op, const std::vector<std::string>& input_names,
                const std::vector<std::string>& attrs, int output_num,

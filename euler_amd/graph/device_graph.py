@@ -124,25 +124,74 @@ class DeviceGraph:
         ``sample_node(count, node_type)``: node-weighted, -1 = every type, as
         ``graph.cc:333-403``) and, optionally, the dense ``features`` columns (concatenated,
         ``feature_dtype``) and the dense ``label`` column as device tables.  Rows are the
-        engine's rows (sorted by node id); :meth:`rows_of` maps raw ids to rows.  Requires
-        the embedded (local) graph: the MI355X design keeps a whole shard per GPU."""
+        engine's rows (sorted by node id); :meth:`rows_of` maps raw ids to rows.  A sharded
+        engine (remote shard servers, local_sharded) is assembled from every shard's export
+        (:meth:`_from_shards`): one GPU's 288 GB of HBM holds the whole graph."""
         from euler_amd.ops import base
 
         eng = engine if engine is not None else base.get_engine()
+        names = [] if not features else ([features] if isinstance(features, (str, int)) else list(features))
+        dims = [] if not features else ([feature_dims] if isinstance(feature_dims, int) else list(feature_dims))
+        if getattr(eng, "mode", "local") != "local":
+            return cls._from_shards(eng, node_type, names, dims, label, label_dim, feature_dtype, seed, device)
         indptr, nbr, w, T, ids, _ = eng.export_csr()
         _, types, nw = eng.export_nodes()
         g = cls.from_csr(indptr, nbr, w, int(T), ids=np.asarray(ids), seed=seed, device=device)
         g.node_types = np.asarray(types)
         g.set_root_type(node_type, node_weights=np.asarray(nw))
-        if features:
-            names = [features] if isinstance(features, (str, int)) else list(features)
-            dims = [feature_dims] if isinstance(feature_dims, int) else list(feature_dims)
+        if names:
             cols = [np.asarray(eng.dense_feature(g.ids, "dense_" + str(n), int(d)), np.float32)
                     for n, d in zip(names, dims)]
             g.features = torch.from_numpy(np.concatenate(cols, 1)).to(device=device, dtype=feature_dtype)
         if label is not None:
             lab = np.asarray(eng.dense_feature(g.ids, "dense_" + str(label), int(label_dim)), np.float32)
             g.labels = torch.from_numpy(lab).to(device)
+        return g
+
+    @classmethod
+    def _from_shards(cls, eng, node_type, names, dims, label, label_dim, feature_dtype, seed, device):
+        """The whole graph of a sharded engine (``remote``: shard servers over RPC, or
+        ``local_sharded``) assembled in HBM: every shard exports its nodes, out-adjacency
+        (neighbour ids) and dense features in one ``API_EXPORT_SHARD`` call
+        (csrc/ops/graph_ops.cc); rows are the union sorted by node id — the row order a
+        local engine over the same data has — so the device graph, its samplers and every
+        batch drawn from it are identical to the in-process job's."""
+        cols = ["dense_" + str(n) for n in names] + ([] if label is None else ["dense_" + str(label)])
+        widths = [int(d) for d in dims] + ([] if label is None else [int(label_dim)])
+        parts = [eng.export_shard(k, cols, widths) for k in range(int(eng.shard_num))]
+        ids = np.concatenate([np.asarray(p[0], np.uint64) for p in parts])
+        types = np.concatenate([np.asarray(p[1], np.int32) for p in parts])
+        nw = np.concatenate([np.asarray(p[2], np.float32) for p in parts])
+        T = max(1, (len(parts[0][3]) - 1) // max(len(parts[0][0]), 1)) if len(parts[0][0]) else 1
+        for p in parts:
+            if len(p[0]) and (len(p[3]) - 1) != len(p[0]) * T:
+                raise ValueError("shards disagree on the number of edge types")
+        # per node: its T segment lengths and its edge range in the concatenated edge arrays
+        seg = np.concatenate([np.diff(np.asarray(p[3], np.int64)).reshape(-1, T) for p in parts], 0)
+        nbr_ids = np.concatenate([np.asarray(p[4], np.uint64) for p in parts])
+        ew = np.concatenate([np.asarray(p[5], np.float32) for p in parts])
+        order = np.argsort(ids, kind="stable")
+        if len(ids) > 1 and (np.diff(ids[order].astype(np.int64)) == 0).any():
+            raise ValueError("a node id is stored on more than one shard")
+        nlen = seg.sum(1)
+        nstart = np.concatenate([[0], np.cumsum(nlen)[:-1]])
+        seg = seg[order]
+        indptr = np.concatenate([[0], np.cumsum(seg.reshape(-1))]).astype(np.int64)
+        lens = nlen[order]
+        take = np.repeat(nstart[order] - np.concatenate([[0], np.cumsum(lens)[:-1]]), lens) + np.arange(lens.sum())
+        sids = ids[order]
+        pos = np.searchsorted(sids, nbr_ids[take])
+        posc = np.minimum(pos, max(len(sids) - 1, 0))
+        rows = np.where((pos < len(sids)) & (sids[posc] == nbr_ids[take]), posc, -1).astype(np.int64)
+        g = cls.from_csr(indptr, rows, ew[take], int(T), ids=sids, seed=seed, device=device)
+        g.node_types = types[order]
+        g.set_root_type(node_type, node_weights=nw[order])
+        tabs = [np.concatenate([np.asarray(p[6 + k], np.float32).reshape(-1, widths[k]) for p in parts])[order]
+                for k in range(len(widths))]
+        if names:
+            g.features = torch.from_numpy(np.concatenate(tabs[: len(names)], 1)).to(device=device, dtype=feature_dtype)
+        if label is not None:
+            g.labels = torch.from_numpy(tabs[-1]).to(device)
         return g
 
     def set_root_type(self, node_type=-1, node_weights=None):

@@ -613,3 +613,60 @@ def test_graph_partition_mode_routes_by_ownership():
             p.terminate()
         for p in procs:
             p.wait(timeout=30)
+
+
+def test_remote_device_graph_matches_local_and_trains_alike(tmp_path):
+    """DeviceGraph.from_engine over a 2-shard remote cluster (API_EXPORT_SHARD per shard,
+    assembled in id order) equals the in-process engine's device graph tensor for tensor,
+    so a GCN device-path job over the remote cluster trains bit-identically to the
+    in-process one (reference euler_ops/base.py:70-75 remote graph)."""
+    sys.path.insert(0, os.path.join(ROOT, "benchmarks"))
+    from bench_engine_sage import start_cluster
+
+    import torch
+
+    from euler_amd import models as Z
+    from euler_amd.dataset import get_dataset
+    from euler_amd.estimator import NodeEstimator
+    from euler_amd.graph.device_graph import DeviceGraph
+
+    ds = get_dataset("ppi", data_dir=str(tmp_path / "ppi"), scale=0.03)
+    ds.partition_num = 2
+    d = ds.load_graph()
+    tnt = ds.train_node_type[0] if isinstance(ds.train_node_type, list) else ds.train_node_type
+
+    def graph():
+        return DeviceGraph.from_engine(features="feature", feature_dims=ds.feature_dim, label="label",
+                                       label_dim=ds.label_dim, feature_dtype=torch.float32, seed=3, device="cpu")
+
+    def train(tag):
+        ea.set_seed(3)
+        torch.manual_seed(0)
+        m = Z.SupervisedGCN([16, 16, ds.label_dim], [["train"], ["train"]], "feature", ds.feature_dim, "label",
+                            ds.label_dim)
+        params = {"model_dir": str(tmp_path / tag), "batch_size": 32, "total_step": 8, "optimizer": "adam",
+                  "learning_rate": 0.01, "log_steps": 4, "train_node_type": tnt, "device": "cpu", "seed": 4,
+                  "device_graph": True}
+        est = NodeEstimator(m, params)
+        res = est.train()
+        return res, type(est.device_trainer).__name__
+
+    g_local = graph()
+    local, kind = train("local")
+    assert kind == "FullFlowTrainer"
+    reg, procs = start_cluster(d, 2, 4)
+    try:
+        ea.initialize_shared_graph(reg, shard_num=2)
+        assert ea.get_engine().mode == "remote"
+        g_remote = graph()
+        remote, _ = train("remote")
+    finally:
+        for p in procs:
+            p.terminate()
+            p.wait(timeout=30)
+    for name in ("indptr", "nbr", "cumw", "node_prob", "node_alias", "features", "labels"):
+        a, b = getattr(g_local, name), getattr(g_remote, name)
+        assert a.shape == b.shape and torch.equal(a, b), name
+    assert np.array_equal(np.asarray(g_local.ids), np.asarray(g_remote.ids))
+    assert remote["step"] == local["step"] == 8
+    assert remote["loss"] == local["loss"], (local, remote)
