@@ -196,7 +196,7 @@ class BaseEstimator:
         dense = [p for p in params if not is_sharded(p)]
         self._sync = dp.GradSync(dense, bucket_bytes=int(self.params.get("bucket_bytes", 32 << 20)))
 
-    def save(self, step=None, extra=None, all_ranks=False):
+    def save(self, step=None, extra=None, all_ranks=False, model_state=None):
         """Write ``model.ckpt-<step>.pt`` (rank 0) and, when some state differs per rank
         (sharded tables, or ``all_ranks``: e.g. the device path's per-rank sampler stream),
         ``model.ckpt-<step>-rank<r>.pt`` on every other rank (reference per-worker outputs,
@@ -208,8 +208,9 @@ class BaseEstimator:
         os.makedirs(self.model_dir, exist_ok=True)
         path = rank_checkpoint(os.path.join(self.model_dir, "model.ckpt-%d.pt" % step),
                                0 if self.world == 1 else self.rank)
-        model_state = {k: v for k, v in self.model.state_dict().items()
-                       if not isinstance(v, nn.parameter.UninitializedParameter)}  # never-called lazy layers
+        if model_state is None:
+            model_state = {k: v for k, v in self.model.state_dict().items()
+                           if not isinstance(v, nn.parameter.UninitializedParameter)}  # never-called lazy layers
         state = {"step": step, "model": model_state,
                  "optimizer": self.optimizer.state_dict() if self.optimizer is not None else None,
                  "world": self.world, "torch_rng": torch.get_rng_state()}
@@ -556,6 +557,8 @@ class BaseEstimator:
         # graphs holding captured collectives keep the communicator busy: drop them before
         # the final barrier / process-group teardown
         self._device_release(tr)
+        if callable(getattr(tr, "finish", None)):
+            tr.finish()  # e.g. row-sparse tables back into the model's own modules
         dp.barrier()
         return last
 
@@ -693,7 +696,10 @@ class BaseEstimator:
         the other ranks out of the next chunk's collectives until rank 0 has written (a
         rank spinning in an xGMI wait while rank 0 writes could time out)"""
         tr.write_to_model(self.model)
-        self.save(extra={"device_trainer": tr.trainer_state(), "optimizer": None}, all_ranks=True)
+        # a trainer whose tables live outside the model's modules while it trains
+        # (row-sparse tables) gives the checkpoint its own model-named state
+        ms = tr.checkpoint_model_state() if callable(getattr(tr, "checkpoint_model_state", None)) else None
+        self.save(extra={"device_trainer": tr.trainer_state(), "optimizer": None}, all_ranks=True, model_state=ms)
         dp.barrier()
 
     def _eval_batches(self):

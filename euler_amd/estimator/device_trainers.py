@@ -158,12 +158,17 @@ def _is_unsup_gnn(model):
 def _kg(c: Ctx):
     # TransE / TransH / TransR / TransD / DistMult (EdgeEstimator): the triple table and the
     # corruption sampler in HBM, the model's own scores (models/kg_trainer.py)
-    from euler_amd.models.kg_trainer import KGTrainer
+    # row-sharded, row-sparse entity tables (RowSparseKGTrainer) for sharded models or on
+    # request (``row_sparse_tables``): per-step work independent of |V|
+    from euler_amd.models.kg_trainer import KGTrainer, RowSparseKGTrainer
+    from euler_amd.parallel.embedding import ShardedEmbedding
 
     m = c.model
     edge_type = c.params.get("train_edge_type", getattr(m, "edge_type", -1))
-    return KGTrainer.from_model(m, c.batch, edge_type, seed=c.seed * 7919 + c.est.rank, device=c.est.device,
-                                **c.opt_kw())
+    sparse = isinstance(m.entity_encoder, ShardedEmbedding) or bool(c.params.get("row_sparse_tables", False))
+    cls = RowSparseKGTrainer if sparse else KGTrainer
+    return cls.from_model(m, c.batch, edge_type, seed=c.seed * 7919 + c.est.rank, device=c.est.device,
+                          **c.opt_kw())
 
 
 @register("graph_classification", _is_graph_model)

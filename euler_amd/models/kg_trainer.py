@@ -30,7 +30,7 @@ from euler_amd.graph.device_graph import build_alias_table
 from euler_amd.models.captured import CapturedTrainer
 from euler_amd.ops._native import hip, use_hip
 
-__all__ = ["TripleTable", "KGTrainer"]
+__all__ = ["TripleTable", "KGTrainer", "RowSparseKGTrainer"]
 
 
 class _Alias:
@@ -148,3 +148,228 @@ class KGTrainer(CapturedTrainer):
 
     def reset_metric(self):
         self.msum.zero_()
+
+
+# ---------------------------------------------------------------------------- row-sparse tables
+class _RowsOf(torch.nn.Module):
+    """Stand-in for a per-entity table during a row-sparse step: ``forward(ids)`` returns
+    the rows of the step's gathered leaf tensor for the id tensors the step registered
+    (the model's ``generate_embedding`` calls its entity tables on exactly the src / dst /
+    corruption tensors the trainer passes to ``loss_scores``)."""
+
+    def __init__(self, num, dim):
+        super().__init__()
+        self.num, self.dim = int(num), int(dim)
+        self.rows = None
+        self.pos = {}
+
+    def forward(self, ids):
+        p = self.pos.get(id(ids))
+        if p is None:
+            raise RuntimeError("row-sparse KG step: the model looked up an id tensor the step did not draw")
+        return self.rows[p.reshape(-1)].reshape(*ids.shape, self.dim)
+
+
+class RowSparseKGTrainer(KGTrainer):
+    """KGTrainer with the per-entity tables (``entity_encoder``, TransD's
+    ``entity_transfer``) held as row-sharded, row-sparse :class:`ShardedTable` s instead of
+    FlatParams: per step only the touched rows (the batch's src, dst and corruptions,
+    de-duplicated on the device) are gathered — from their owner ranks over one fixed-
+    capacity all-to-all when world > 1 — and updated by the row-sparse Adam / Adagrad /
+    SGD kernel (optim.hip sparse_optim).  Per-step work is independent of |V|; the
+    relation tables and projections stay in the flat buffer (dense, all-reduced).
+
+    Reference: tf_euler/python/utils/embedding.py:24-68 (mod-partitioned embedding
+    variables, sparse updates), examples/TransX/transX.py:63-145.  Row ``r`` lives on rank
+    ``r % world`` (ShardedEmbedding's layout), so a ``sharded=True`` model's local shard is
+    the table's shard as it is; checkpoints hold the whole table under the model's name."""
+
+    TABLES = ("entity_encoder", "entity_transfer")
+
+    def __init__(self, model, table, batch_size, optimizer="adam", learning_rate=0.01, group=None):
+        from euler_amd.parallel.sparse_table import ShardedTable
+
+        if not hasattr(model, "loss_scores"):
+            raise ValueError("RowSparseKGTrainer trains the TransX family (models/knowledge_graph.py)")
+        self.table = table
+        self.B = int(batch_size)
+        self.metric_name = model.metric_name
+        self.msum = torch.zeros(2, dtype=torch.float64, device=table.device)
+        self.tables, self._orig = {}, {}
+        opt = optimizer if optimizer in ("adam", "adagrad", "sgd") else "adam"
+        for name in self.TABLES:
+            mod = getattr(model, name, None)
+            if mod is None:
+                continue
+            num, dim = int(mod.num), int(mod.dim)
+            t = ShardedTable(num, dim, table.device, group, opt, learning_rate)
+            with torch.no_grad():
+                w = mod.weight.detach().to(table.device)
+                if getattr(mod, "world", 1) > 1 or w.shape[0] == t.weight.shape[0]:
+                    t.weight.copy_(w)  # already this rank's rows (r % world == rank)
+                else:
+                    t.weight.copy_(w[t.global_ids()])
+            self.tables[name] = t
+            self._orig[name] = mod
+            setattr(model, name, _RowsOf(num, dim))
+        if "entity_encoder" not in self.tables:
+            raise ValueError("the model has no entity_encoder table")
+        CapturedTrainer.__init__(self, model, table, table.device, optimizer, learning_rate)
+        self.world = self.tables["entity_encoder"].world
+
+    @classmethod
+    def from_model(cls, model, batch_size, edge_type, seed=0, device="cuda", optimizer="adam", learning_rate=0.01):
+        table = TripleTable.from_engine(edge_type, node_type=model.node_type, seed=seed, device=device)
+        return cls(model, table, batch_size, optimizer=optimizer, learning_rate=learning_rate)
+
+    # ------------------------------------------------------------------ step
+    def _step(self, grad_sync=None):
+        from euler_amd.ops.gnn_ops import unique_first_padded
+
+        self._swap_in()
+        self._draw()
+        t = self.table
+        K = self.model.num_negs
+        src, rel, dst = t.sample_triples(self.B)
+        neg = t.sample_corruptions(self.B * K)
+        num = self.tables["entity_encoder"].num_rows
+        ids = torch.cat([src, dst, neg])
+        ids = torch.where((ids < 0) | (ids >= num), torch.full_like(ids, num - 1), ids)
+        uids, inv, _ = unique_first_padded(ids)
+        src, rel, dst = src.view(-1, 1), rel.view(-1, 1), dst.view(-1, 1)
+        neg = neg.view(self.B, K)
+        handles = {}
+        for name, tab in self.tables.items():
+            rows, h = tab.lookup_static(uids, trash_row=True)
+            leaf = rows.detach().requires_grad_(True)
+            p = h.pos[inv]
+            mod = getattr(self.model, name)
+            mod.rows = leaf
+            mod.pos = {id(src): p[: self.B], id(dst): p[self.B: 2 * self.B], id(neg): p[2 * self.B:]}
+            handles[name] = (tab, h, leaf)
+        self.opt.zero_grad()
+        loss, pos, neg_s = self.model.loss_scores(src, dst, neg, rel)
+        loss.backward()
+        with torch.no_grad():
+            r = (neg_s >= pos).sum(-1).double()
+            v = {"mrr": (1.0 / (r + 1)).sum(), "mr": (r + 1).sum()}.get(self.metric_name, (r < 10).double().sum())
+            self.msum += torch.stack([v, torch.full_like(v, float(r.numel()))])
+        scale = 1.0
+        if grad_sync is not None:
+            s = grad_sync(self.flat.grad)
+            scale = 1.0 if s is None else float(s)
+        self.opt.step(scale)
+        for tab, h, leaf in handles.values():
+            g = leaf.grad
+            if g is None:
+                g = torch.zeros_like(leaf)
+            n = g.shape[0] - 1  # the trash row (ids a capacity overflow dropped) is not applied
+            # the dense buffer's all-reduce averages over ranks; the owners sum the ranks'
+            # row gradients, so they are scaled to the same mean here
+            tab.apply_static(h, g[:n] / self.world if self.world > 1 else g[:n])
+        for name in self.tables:
+            mod = getattr(self.model, name)
+            mod.rows, mod.pos = None, {}
+        self._samples = (src, rel, dst, neg)
+        self.loss_out.copy_(loss.detach())
+        return self.loss_out
+
+    # ------------------------------------------------------------------ state
+    def _full_table(self, tab):
+        """the whole [num_rows, D] table on every rank (checkpoints: the model's names)"""
+        if tab.world == 1:
+            return tab.weight.detach().clone()
+        import torch.distributed as dist
+
+        n = tab.weight.shape[0]
+        rows = int(-(-tab.num_rows // tab.world))
+        pad = torch.zeros(rows, tab.dim, device=tab.weight.device)
+        pad[:n] = tab.weight.detach()
+        parts = [torch.zeros_like(pad) for _ in range(tab.world)]
+        dist.all_gather(parts, pad)
+        full = torch.stack(parts, 1).reshape(-1, tab.dim)  # row r = parts[r % W][r // W]
+        return full[: tab.num_rows].clone()
+
+    def _dense_names(self):
+        return {k for k in self.model.state_dict()}
+
+    def state_dict(self):
+        sd = {k: v.detach().cpu() for k, v in self.model.state_dict().items()}
+        for name, tab in self.tables.items():
+            sd[name + ".weight"] = self._full_table(tab).cpu()
+        return sd
+
+    def checkpoint_model_state(self):
+        """the model's state under its own names, the whole tables included"""
+        return self.state_dict()
+
+    def logical_params(self):
+        sd = {k: v.detach().clone() for k, v in self.model.state_dict().items()}
+        for name, tab in self.tables.items():
+            sd[name + ".weight"] = self._full_table(tab)
+        return sd
+
+    def load_logical(self, sd):
+        with torch.no_grad():
+            own = self.model.state_dict()
+            for k, v in sd.items():
+                if k in own:
+                    own[k].copy_(torch.as_tensor(v).to(own[k]))
+            for name, tab in self.tables.items():
+                v = sd.get(name + ".weight")
+                if v is None:
+                    continue
+                v = torch.as_tensor(v).to(tab.weight)
+                tab.weight.copy_(v[tab.global_ids()] if v.shape[0] == tab.num_rows else v)
+
+    def write_to_model(self, model):
+        """the trained tables back into the model's own modules (restored after training)"""
+        for name, tab in self.tables.items():
+            mod = self._orig[name]
+            with torch.no_grad():
+                if mod.weight.shape[0] == tab.weight.shape[0]:
+                    mod.weight.copy_(tab.weight.to(mod.weight))
+                else:
+                    mod.weight.copy_(self._full_table(tab).to(mod.weight))
+        if model is not self.model:
+            own = {k: v for k, v in self.model.state_dict().items()}
+            model.load_state_dict(own, strict=False)
+
+    def restore_modules(self):
+        """put the model's own table modules back (after :meth:`write_to_model`)"""
+        for name, mod in self._orig.items():
+            setattr(self.model, name, mod)
+
+    def finish(self):
+        """end of training: the trained tables into the model's own modules, which go back
+        in place (engine-path evaluate / infer and the user's model see them)"""
+        self.write_to_model(self.model)
+        self.restore_modules()
+
+    def _swap_in(self):
+        for name, tab in self.tables.items():
+            if not isinstance(getattr(self.model, name), _RowsOf):
+                setattr(self.model, name, _RowsOf(tab.num_rows, tab.dim))
+
+    def trainer_state(self):
+        st = super().trainer_state()
+        for name, tab in self.tables.items():
+            st[name] = {"m": tab.m.cpu().clone(), "v": tab.v.cpu().clone(), "step": int(tab.step.item())}
+        return st
+
+    def load_trainer_state(self, st):
+        super().load_trainer_state(st)
+        for name, tab in self.tables.items():
+            s = st.get(name)
+            if s is None or torch.as_tensor(s["m"]).shape != tab.m.shape:
+                continue  # another world size: the slots restart
+            tab.m.copy_(torch.as_tensor(s["m"]).to(tab.m))
+            tab.v.copy_(torch.as_tensor(s["v"]).to(tab.v))
+            tab.step.fill_(int(s["step"]))
+
+    def dp_state_tensors(self):
+        ts = list(super().dp_state_tensors())
+        for tab in self.tables.values():
+            ts += [tab.weight] + ([tab.m] if tab.m is not tab.weight else []) + \
+                  ([tab.v] if tab.v is not tab.weight and tab.v is not tab.m else []) + [tab.step]
+        return ts

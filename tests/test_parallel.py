@@ -792,11 +792,50 @@ def _worker_device_trainer_dp(rank, world, port, q, tmp, model, argv, want):
      "FullFlowTrainer"),
     ("transe", ["--scale", "0.05", "--batch_size", "32", "--total_step", "4", "--log_steps", "2", "--dim", "16"],
      "KGTrainer"),
+    ("transe", ["--scale", "0.05", "--batch_size", "32", "--total_step", "4", "--log_steps", "2", "--dim", "16",
+                "--sharded"], "RowSparseKGTrainer"),
     ("gae", ["--scale", "0.05", "--batch_size", "16", "--total_step", "4", "--log_steps", "2", "--dim", "16",
              "--fanouts", "4", "3"], "GaeTrainer"),
     ("gin", ["--scale", "0.2", "--batch_size", "8", "--total_step", "4", "--log_steps", "2"], "GraphTrainer"),
 ])
 def test_device_trainers_data_parallel_lockstep(tmp_path, model, argv, want):
     res = _run(_worker_device_trainer_dp, str(tmp_path), model, argv, want)
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == 2 and all(r[2] for r in res), res
+
+
+def _worker_row_sparse_vs_dense_kg(rank, world, port, q, tmp):
+    """one 2-rank step of TransE with the entity table dense in the all-reduced flat buffer
+    (KGTrainer) and row-sharded / row-sparse (RowSparseKGTrainer, fixed-capacity all-to-all
+    to the owners): Adam's first update of an untouched row is zero and the owners apply
+    the ranks' mean row gradient, so both hold the same tables after the step"""
+    try:
+        _init(rank, world, port)
+        from euler_amd.tools import runner
+
+        out = {}
+        for sparse in (False, True):
+            a = runner.parse_args(["--scale", "0.05", "--batch_size", "32", "--total_step", "1", "--log_steps", "1",
+                                   "--dim", "16", "--model_dir", os.path.join(tmp, f"ck_{int(sparse)}_r{rank}"),
+                                   "--device_graph", "--device", "cpu", "--seed", "1"], model="transe")
+            torch.manual_seed(0)
+            _, est = runner.build(a)
+            est.params["row_sparse_tables"] = sparse
+            est.train()
+            out[sparse] = (type(est.device_trainer).__name__, est.device_trainer.logical_params())
+        (k0, p0), (k1, p1) = out[False], out[True]
+        ok = k0 == "KGTrainer" and k1 == "RowSparseKGTrainer" and set(p0) == set(p1)
+        for k in p0:
+            ok = ok and torch.allclose(p0[k], p1[k], atol=1e-6)
+        q.put((rank, "row_sparse_vs_dense", bool(ok)))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_row_sparse_kg_two_ranks_matches_dense_first_step(tmp_path):
+    res = _run(_worker_row_sparse_vs_dense_kg, str(tmp_path))
     assert not [r for r in res if r[1] == "error"], res
     assert len(res) == 2 and all(r[2] for r in res), res
