@@ -197,10 +197,13 @@ def _gae(c: Ctx):
 
 @register("line_first_order", _is_line1)
 def _line1(c: Ctx):
-    # first-order LINE: one id table in both roles, autograd over the model's own lookups
-    from euler_amd.models.line_trainer import IdPairTrainer
+    # first-order LINE: one id table in both roles, autograd over the model's own lookups;
+    # row-sharded / row-sparse (RowSparseIdPairTrainer) for a sharded table or on request
+    from euler_amd.models.line_trainer import IdPairTrainer, RowSparseIdPairTrainer
 
-    return IdPairTrainer(c.model, c.upload(c.model.node_type), c.batch, **c.opt_kw())
+    sharded = getattr(c.model._target_encoder, "table", None) is not None
+    cls = RowSparseIdPairTrainer if sharded or c.params.get("row_sparse_tables", False) else IdPairTrainer
+    return cls(c.model, c.upload(c.model.node_type), c.batch, **c.opt_kw())
 
 
 @register("skipgram_walks", _cls("BaseNode2Vec", "Line"))

@@ -20,7 +20,7 @@ import torch
 from euler_amd.models.captured import CapturedTrainer
 from euler_amd.ops import gnn_ops
 
-__all__ = ["IdPairTrainer"]
+__all__ = ["IdPairTrainer", "RowSparseIdPairTrainer"]
 
 
 class IdPairTrainer(CapturedTrainer):
@@ -71,3 +71,153 @@ class IdPairTrainer(CapturedTrainer):
 
     def reset_metric(self):
         self.mrr.zero_()
+
+
+def _id_table_module(enc):
+    """the id embedding module of a pure-id encoder (ShallowEncoder with only ids, or the
+    sharded IdEncoder), else None"""
+    table = getattr(enc, "table", None)
+    if table is not None:
+        return table  # IdEncoder(sharded=True): a ShardedEmbedding
+    inner = getattr(enc, "enc", None)
+    if inner is not None:
+        enc = inner
+    if getattr(enc, "use_id", False) and not getattr(enc, "use_feature", True) and \
+            not getattr(enc, "use_sparse_feature", True) and getattr(enc, "combiner", "add") == "add" and \
+            not hasattr(enc, "dense"):
+        return getattr(enc, "embedding", None)
+    return None
+
+
+class RowSparseIdPairTrainer(IdPairTrainer):
+    """First-order LINE with its one id table row-sharded and row-sparse
+    (:class:`~euler_amd.parallel.sparse_table.ShardedTable`): per step the batch's source,
+    positive and negative ids are de-duplicated on the device, their rows gathered (from
+    the owner ranks over one fixed-capacity all-to-all when world > 1), the fused
+    ``sgns_loss`` runs on the gathered rows, and the row gradients go back to the owners'
+    row-sparse Adam / Adagrad / SGD.  Per-step work is independent of |V|; a row that is a
+    target and a context in one step gets one merged gradient (the shared-table case the
+    in-place SGNS update cannot take).  Reference: examples/line/line.py:27-71,
+    tf_euler/python/utils/embedding.py:24-68."""
+
+    def __init__(self, model, graph, batch_size, optimizer="adam", learning_rate=0.01, group=None):
+        import euler_amd.ops.graph_api as ge
+        from euler_amd.parallel.sparse_table import ShardedTable
+
+        mod = _id_table_module(getattr(model, "_target_encoder", None))
+        if mod is None or model._context_encoder is not model._target_encoder:
+            raise ValueError("RowSparseIdPairTrainer trains first-order LINE over one pure id table")
+        self.graph = graph
+        self.B, self.K = int(batch_size), int(model.num_negs)
+        et = model.edge_type
+        self.types = None if et in (None, -1, "-1") else \
+            [int(t) for t in np.asarray(ge.get_edge_type_id(et)).reshape(-1)]
+        ids = graph.ids if graph.ids is not None else np.arange(graph.num_rows)
+        self._ids = torch.as_tensor(np.asarray(ids).astype(np.int64), device=graph.device)
+        self._pad_id = int(model.max_id) + 1
+        self.mrr = torch.zeros(2, dtype=torch.float64, device=graph.device)
+        opt = optimizer if optimizer in ("adam", "adagrad", "sgd") else "adam"
+        self.id_table = ShardedTable(int(mod.num), int(mod.dim), graph.device, group, opt, learning_rate)
+        with torch.no_grad():
+            w = mod.weight.detach().to(graph.device)
+            t = self.id_table
+            t.weight.copy_(w if getattr(mod, "world", 1) > 1 or w.shape[0] == t.weight.shape[0]
+                           else w[t.global_ids()])
+        self._mod = mod
+        CapturedTrainer.__init__(self, model, graph, graph.device, optimizer, learning_rate)
+        self.world = self.id_table.world
+
+    def _step(self, grad_sync=None):
+        from euler_amd.ops.gnn_ops import unique_first_padded
+
+        self._draw()
+        g, B, K = self.graph, self.B, self.K
+        src = g.sample_node(B, stream_id=1).long()
+        pos = g.sample_neighbor(src, 1, edge_types=self.types, default=-1, stream_id=4).long().reshape(-1)
+        neg = g.sample_node(B * K, stream_id=5).long()
+        t = self.id_table
+        ids = self._node_ids(torch.cat([src, pos, neg]))
+        ids = torch.where((ids < 0) | (ids >= t.num_rows), torch.full_like(ids, t.num_rows - 1), ids)
+        uids, inv, _ = unique_first_padded(ids)
+        rows, h = t.lookup_static(uids, trash_row=True)
+        leaf = rows.detach().requires_grad_(True)
+        p = h.pos[inv]
+        emb = leaf[p[:B]]
+        emb_pos = leaf[p[B: 2 * B]].view(B, 1, -1)
+        emb_neg = leaf[p[2 * B:]].view(B, K, -1)
+        loss, logits, neg_logits = gnn_ops.sgns_loss(emb, emb_pos, emb_neg)
+        self.opt.zero_grad()
+        loss.backward()
+        with torch.no_grad():
+            lp, ln = logits.float().view(B, 1), neg_logits.float().view(B, K)
+            rank = 1.0 + (ln >= lp).sum(-1).double()
+            self.mrr += torch.stack([(1.0 / rank).sum(), torch.full_like(rank[0], float(B))])
+        scale = 1.0
+        if grad_sync is not None and self.flat.flat.numel():
+            s = grad_sync(self.flat.grad)
+            scale = 1.0 if s is None else float(s)
+        self.opt.step(scale)
+        gr = leaf.grad if leaf.grad is not None else torch.zeros_like(leaf)
+        n = gr.shape[0] - 1
+        t.apply_static(h, gr[:n] / self.world if self.world > 1 else gr[:n])
+        self._samples = (src, pos, neg)
+        self.loss_out.copy_(loss.detach())
+        return self.loss_out
+
+    # ------------------------------------------------------------------ state
+    def _full(self):
+        from euler_amd.models.kg_trainer import RowSparseKGTrainer
+
+        return RowSparseKGTrainer._full_table(self, self.id_table)
+
+    def _names(self):
+        """every state_dict key of the table (a shared table is listed under both roles)"""
+        return [k for k, v in self.model.state_dict(keep_vars=True).items() if v is self._mod.weight]
+
+    def state_dict(self):
+        sd = {k: v.detach().cpu() for k, v in self.model.state_dict().items()}
+        full = self._full().cpu()
+        for k in self._names():
+            sd[k] = full
+        return sd
+
+    checkpoint_model_state = state_dict
+
+    def logical_params(self):
+        return {k: v.to(self.device) for k, v in self.state_dict().items()}
+
+    def load_logical(self, sd):
+        t = self.id_table
+        with torch.no_grad():
+            for k in self._names():
+                v = sd.get(k)
+                if v is not None:
+                    v = torch.as_tensor(v).to(t.weight)
+                    t.weight.copy_(v[t.global_ids()] if v.shape[0] == t.num_rows else v)
+
+    def write_to_model(self, model):
+        with torch.no_grad():
+            w = self._mod.weight
+            w.copy_((self.id_table.weight if w.shape[0] == self.id_table.weight.shape[0] else self._full()).to(w))
+        if model is not self.model:
+            model.load_state_dict(self.model.state_dict(), strict=False)
+
+    def trainer_state(self):
+        st = super().trainer_state()
+        t = self.id_table
+        st["id_table"] = {"m": t.m.cpu().clone(), "v": t.v.cpu().clone(), "step": int(t.step.item())}
+        return st
+
+    def load_trainer_state(self, st):
+        super().load_trainer_state(st)
+        s, t = st.get("id_table"), self.id_table
+        if s is not None and torch.as_tensor(s["m"]).shape == t.m.shape:
+            t.m.copy_(torch.as_tensor(s["m"]).to(t.m))
+            t.v.copy_(torch.as_tensor(s["v"]).to(t.v))
+            t.step.fill_(int(s["step"]))
+
+    def dp_state_tensors(self):
+        t = self.id_table
+        extra = [t.weight] + ([t.m] if t.m is not t.weight else []) + \
+            ([t.v] if t.v is not t.weight and t.v is not t.m else []) + [t.step]
+        return list(super().dp_state_tensors()) + extra

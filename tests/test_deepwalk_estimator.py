@@ -143,3 +143,38 @@ def test_line_first_order_device_path_gpu_captured(cora, tmp_path, cuda):
     est = NodeEstimator(m, _params(cora, tmp_path, "cuda", total_step=120, log_steps=40, steps_per_graph=8))
     res = est.train()
     assert res["step"] == 120 and np.isfinite(res["loss"]) and est.device_trainer.captures >= 1
+
+
+def test_line_first_order_row_sparse_first_step_equals_dense(cora, tmp_path):
+    """RowSparseIdPairTrainer (the shared id table row-sparse: touched rows gathered,
+    merged gradients, sparse Adam) against IdPairTrainer (the table in the dense flat
+    buffer): Adam's first update of an untouched row is zero, so one step leaves both
+    tables equal; then the estimator trains it and checkpoints the table under the
+    model's own name"""
+    from euler_amd.graph.device_graph import DeviceGraph
+    from euler_amd.models.line_trainer import IdPairTrainer, RowSparseIdPairTrainer
+
+    out = {}
+    for cls in (IdPairTrainer, RowSparseIdPairTrainer):
+        torch.manual_seed(0)
+        m = _line(cora, order=1)
+        g = DeviceGraph.from_engine(node_type=0, seed=4, device="cpu")
+        tr = cls(m, g, 32, learning_rate=0.02)
+        tr.step()
+        out[cls.__name__] = (float(tr.loss), tr.logical_params())
+    (l0, p0), (l1, p1) = out["IdPairTrainer"], out["RowSparseIdPairTrainer"]
+    assert abs(l0 - l1) <= 1e-6 * abs(l0) and set(p0) == set(p1)
+    for k in p0:
+        assert torch.allclose(p0[k].cpu(), p1[k].cpu(), atol=1e-6), k
+    m = _line(cora, order=1)
+    before = m.state_dict()["_target_encoder.embedding.weight"].clone()
+    est = NodeEstimator(m, _params(cora, tmp_path, "cpu", row_sparse_tables=True))
+    res = est.train()
+    assert type(est.device_trainer).__name__ == "RowSparseIdPairTrainer"
+    assert res["step"] == 30 and np.isfinite(res["loss"]) and 0.0 < res["mrr"] <= 1.0
+    after = m.state_dict()["_target_encoder.embedding.weight"]
+    assert not torch.equal(before, after)
+    from euler_amd.estimator.base import latest_checkpoint
+
+    ck = torch.load(latest_checkpoint(str(tmp_path / "ckpt")), map_location="cpu", weights_only=True)
+    assert torch.equal(ck["model"]["_target_encoder.embedding.weight"], after)

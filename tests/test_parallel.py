@@ -794,6 +794,8 @@ def _worker_device_trainer_dp(rank, world, port, q, tmp, model, argv, want):
      "KGTrainer"),
     ("transe", ["--scale", "0.05", "--batch_size", "32", "--total_step", "4", "--log_steps", "2", "--dim", "16",
                 "--sharded"], "RowSparseKGTrainer"),
+    ("line", ["--scale", "0.1", "--batch_size", "32", "--total_step", "4", "--log_steps", "2", "--dim", "16",
+              "--order", "1", "--sharded"], "RowSparseIdPairTrainer"),
     ("gae", ["--scale", "0.05", "--batch_size", "16", "--total_step", "4", "--log_steps", "2", "--dim", "16",
              "--fanouts", "4", "3"], "GaeTrainer"),
     ("gin", ["--scale", "0.2", "--batch_size", "8", "--total_step", "4", "--log_steps", "2"], "GraphTrainer"),
