@@ -3,6 +3,7 @@
 // validated (dtype, device, contiguity, shape) before a launch, launches go to torch's
 // current HIP stream, outputs are allocated by torch's caching allocator.
 #include <cstdlib>
+#include <map>
 
 #include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
@@ -628,6 +629,65 @@ void memset_zero(torch::Tensor t) {
   ok(hipMemsetAsync(t.data_ptr(), 0, static_cast<size_t>(t.numel() * t.element_size()), stream()), "memset_zero");
 }
 
+// Nodes and dependency edges of a captured hipGraph (torch.cuda.CUDAGraph(keep_graph=True)
+// .raw_cuda_graph()), plus hipGraphDebugDotPrint into dot_path when given.  Every node:
+// (index, kind, detail) — kernel name, memset (dst, bytes, value) or memcpy; edges as
+// (from, to) index pairs (diagnostics: tests/test_graph_memset.py, tools/graph_dot.py).
+py::dict graph_summary(int64_t handle, const std::string& dot_path) {
+  hipGraph_t g = reinterpret_cast<hipGraph_t>(static_cast<uintptr_t>(handle));
+  TORCH_CHECK(g != nullptr, "graph_summary: null graph");
+  if (!dot_path.empty()) ok(hipGraphDebugDotPrint(g, dot_path.c_str(), hipGraphDebugDotFlagsVerbose), "dot print");
+  size_t n = 0;
+  ok(hipGraphGetNodes(g, nullptr, &n), "graph nodes");
+  std::vector<hipGraphNode_t> nodes(n);
+  if (n) ok(hipGraphGetNodes(g, nodes.data(), &n), "graph nodes");
+  std::map<hipGraphNode_t, int64_t> index;
+  py::list out_nodes;
+  for (size_t i = 0; i < n; ++i) {
+    index[nodes[i]] = static_cast<int64_t>(i);
+    hipGraphNodeType t;
+    ok(hipGraphNodeGetType(nodes[i], &t), "node type");
+    std::string kind, detail;
+    switch (t) {
+      case hipGraphNodeTypeKernel: {
+        kind = "kernel";
+        hipKernelNodeParams kp{};
+        if (hipGraphKernelNodeGetParams(nodes[i], &kp) == hipSuccess && kp.func) {
+          const char* nm = hipKernelNameRefByPtr(kp.func, nullptr);
+          detail = nm ? nm : "?";
+        }
+        break;
+      }
+      case hipGraphNodeTypeMemset: {
+        kind = "memset";
+        hipMemsetParams mp{};
+        if (hipGraphMemsetNodeGetParams(nodes[i], &mp) == hipSuccess)
+          detail = "dst=" + std::to_string(reinterpret_cast<uintptr_t>(mp.dst)) + " bytes=" +
+                   std::to_string(static_cast<uint64_t>(mp.width) * mp.height * mp.elementSize) +
+                   " value=" + std::to_string(mp.value);
+        break;
+      }
+      case hipGraphNodeTypeMemcpy: kind = "memcpy"; break;
+      case hipGraphNodeTypeEmpty: kind = "empty"; break;
+      case hipGraphNodeTypeWaitEvent: kind = "wait_event"; break;
+      case hipGraphNodeTypeEventRecord: kind = "event_record"; break;
+      case hipGraphNodeTypeHost: kind = "host"; break;
+      default: kind = "type" + std::to_string(static_cast<int>(t)); break;
+    }
+    out_nodes.append(py::make_tuple(static_cast<int64_t>(i), kind, detail));
+  }
+  size_t ne = 0;
+  ok(hipGraphGetEdges(g, nullptr, nullptr, &ne), "graph edges");
+  std::vector<hipGraphNode_t> from(ne), to(ne);
+  if (ne) ok(hipGraphGetEdges(g, from.data(), to.data(), &ne), "graph edges");
+  py::list edges;
+  for (size_t e = 0; e < ne; ++e) edges.append(py::make_tuple(index[from[e]], index[to[e]]));
+  py::dict d;
+  d["nodes"] = out_nodes;
+  d["edges"] = edges;
+  return d;
+}
+
 // one hop's block of the device full-neighbourhood flow (flow.hip flow_block_kernel):
 // returns (new_n_id [cap_n], res_n_id [cap_prev], edge_index [2, E], perm [E],
 // indptr [cap_prev + 1], counts [cap_prev], last_idx [cap_n], n_targets [1] of the next hop)
@@ -1009,6 +1069,7 @@ void register_gnn_ops(pybind11::module& m) {
   m.def("drop_rows", &drop_rows);
   m.def("zero_", &zero_);
   m.def("memset_zero", &memset_zero);
+  m.def("graph_summary", &graph_summary, py::arg("graph"), py::arg("dot_path") = "");
   m.def("seg_count", &seg_count);
   m.def("flow_block", &flow_block);
   m.def("gcn_norm_weight", &gcn_norm_weight);

@@ -153,6 +153,20 @@ def _is_unsup_gnn(model):
     return hasattr(model, "context_gnn") and gnn is not None and hasattr(gnn, "feature_idx")
 
 
+ROW_SPARSE_AUTO_ROWS = 1 << 20
+
+
+def row_sparse(c: Ctx, rows: int, sharded: bool = False) -> bool:
+    """an id table trained row-sparse (ShardedTable + sparse optimizer) instead of in the
+    dense flat buffer: ``row_sparse_tables`` True / False decides; "auto" (default) picks
+    row-sparse for a sharded model or a table of >= 2^20 rows (per-step work then stays
+    independent of |V|)"""
+    v = c.params.get("row_sparse_tables", "auto")
+    if isinstance(v, bool):
+        return v
+    return bool(sharded) or int(rows) >= ROW_SPARSE_AUTO_ROWS
+
+
 # ----------------------------------------------------------------------------------- builders
 @register("knowledge_graph", _is_kg)
 def _kg(c: Ctx):
@@ -165,7 +179,7 @@ def _kg(c: Ctx):
 
     m = c.model
     edge_type = c.params.get("train_edge_type", getattr(m, "edge_type", -1))
-    sparse = isinstance(m.entity_encoder, ShardedEmbedding) or bool(c.params.get("row_sparse_tables", False))
+    sparse = row_sparse(c, getattr(m.entity_encoder, "num", 0), isinstance(m.entity_encoder, ShardedEmbedding))
     cls = RowSparseKGTrainer if sparse else KGTrainer
     return cls.from_model(m, c.batch, edge_type, seed=c.seed * 7919 + c.est.rank, device=c.est.device,
                           **c.opt_kw())
@@ -201,8 +215,10 @@ def _line1(c: Ctx):
     # row-sharded / row-sparse (RowSparseIdPairTrainer) for a sharded table or on request
     from euler_amd.models.line_trainer import IdPairTrainer, RowSparseIdPairTrainer
 
-    sharded = getattr(c.model._target_encoder, "table", None) is not None
-    cls = RowSparseIdPairTrainer if sharded or c.params.get("row_sparse_tables", False) else IdPairTrainer
+    enc = c.model._target_encoder
+    sharded = getattr(enc, "table", None) is not None
+    rows = getattr(getattr(enc, "embedding", None), "num", 0)
+    cls = RowSparseIdPairTrainer if row_sparse(c, rows, sharded) else IdPairTrainer
     return cls(c.model, c.upload(c.model.node_type), c.batch, **c.opt_kw())
 
 
@@ -229,10 +245,13 @@ def _dgi(c: Ctx):
 
 @register("unsupervised_rgcn", _cls("UnsupervisedRGCN"))
 def _urgcn(c: Ctx):
-    # R-GCN over id embeddings: relation blocks and the model's own layers on the HBM graph
-    from euler_amd.models.rgcn_trainer import UnsupRgcnTrainer
+    # R-GCN over id embeddings: relation blocks and the model's own layers on the HBM graph;
+    # the id table row-sparse (RowSparseRgcnTrainer) when large or on request
+    from euler_amd.models.rgcn_trainer import RowSparseRgcnTrainer, UnsupRgcnTrainer
 
-    return UnsupRgcnTrainer(c.model, c.upload(c.model.node_type), c.batch, **c.opt_kw())
+    emb = getattr(c.model.gnn._encoder, "embedding", None)
+    cls = RowSparseRgcnTrainer if row_sparse(c, getattr(emb, "num", 0)) else UnsupRgcnTrainer
+    return cls(c.model, c.upload(c.model.node_type), c.batch, **c.opt_kw())
 
 
 @register("unsupervise_solution", _cls("UnsuperviseSolution"))

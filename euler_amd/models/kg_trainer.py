@@ -275,20 +275,9 @@ class RowSparseKGTrainer(KGTrainer):
         return self.loss_out
 
     # ------------------------------------------------------------------ state
-    def _full_table(self, tab):
-        """the whole [num_rows, D] table on every rank (checkpoints: the model's names)"""
-        if tab.world == 1:
-            return tab.weight.detach().clone()
-        import torch.distributed as dist
-
-        n = tab.weight.shape[0]
-        rows = int(-(-tab.num_rows // tab.world))
-        pad = torch.zeros(rows, tab.dim, device=tab.weight.device)
-        pad[:n] = tab.weight.detach()
-        parts = [torch.zeros_like(pad) for _ in range(tab.world)]
-        dist.all_gather(parts, pad)
-        full = torch.stack(parts, 1).reshape(-1, tab.dim)  # row r = parts[r % W][r // W]
-        return full[: tab.num_rows].clone()
+    @staticmethod
+    def _full_table(tab):
+        return tab.full()
 
     def _dense_names(self):
         return {k for k in self.model.state_dict()}
@@ -319,8 +308,7 @@ class RowSparseKGTrainer(KGTrainer):
                 v = sd.get(name + ".weight")
                 if v is None:
                     continue
-                v = torch.as_tensor(v).to(tab.weight)
-                tab.weight.copy_(v[tab.global_ids()] if v.shape[0] == tab.num_rows else v)
+                tab.load(v)
 
     def write_to_model(self, model):
         """the trained tables back into the model's own modules (restored after training)"""
@@ -354,22 +342,16 @@ class RowSparseKGTrainer(KGTrainer):
     def trainer_state(self):
         st = super().trainer_state()
         for name, tab in self.tables.items():
-            st[name] = {"m": tab.m.cpu().clone(), "v": tab.v.cpu().clone(), "step": int(tab.step.item())}
+            st[name] = tab.slot_state()
         return st
 
     def load_trainer_state(self, st):
         super().load_trainer_state(st)
         for name, tab in self.tables.items():
-            s = st.get(name)
-            if s is None or torch.as_tensor(s["m"]).shape != tab.m.shape:
-                continue  # another world size: the slots restart
-            tab.m.copy_(torch.as_tensor(s["m"]).to(tab.m))
-            tab.v.copy_(torch.as_tensor(s["v"]).to(tab.v))
-            tab.step.fill_(int(s["step"]))
+            tab.load_slot_state(st.get(name))  # another world size: the slots restart
 
     def dp_state_tensors(self):
         ts = list(super().dp_state_tensors())
         for tab in self.tables.values():
-            ts += [tab.weight] + ([tab.m] if tab.m is not tab.weight else []) + \
-                  ([tab.v] if tab.v is not tab.weight and tab.v is not tab.m else []) + [tab.step]
+            ts += tab.state_tensors()
         return ts

@@ -166,9 +166,7 @@ class RowSparseIdPairTrainer(IdPairTrainer):
 
     # ------------------------------------------------------------------ state
     def _full(self):
-        from euler_amd.models.kg_trainer import RowSparseKGTrainer
-
-        return RowSparseKGTrainer._full_table(self, self.id_table)
+        return self.id_table.full()
 
     def _names(self):
         """every state_dict key of the table (a shared table is listed under both roles)"""
@@ -192,8 +190,7 @@ class RowSparseIdPairTrainer(IdPairTrainer):
             for k in self._names():
                 v = sd.get(k)
                 if v is not None:
-                    v = torch.as_tensor(v).to(t.weight)
-                    t.weight.copy_(v[t.global_ids()] if v.shape[0] == t.num_rows else v)
+                    t.load(v)
 
     def write_to_model(self, model):
         with torch.no_grad():
@@ -204,20 +201,12 @@ class RowSparseIdPairTrainer(IdPairTrainer):
 
     def trainer_state(self):
         st = super().trainer_state()
-        t = self.id_table
-        st["id_table"] = {"m": t.m.cpu().clone(), "v": t.v.cpu().clone(), "step": int(t.step.item())}
+        st["id_table"] = self.id_table.slot_state()
         return st
 
     def load_trainer_state(self, st):
         super().load_trainer_state(st)
-        s, t = st.get("id_table"), self.id_table
-        if s is not None and torch.as_tensor(s["m"]).shape == t.m.shape:
-            t.m.copy_(torch.as_tensor(s["m"]).to(t.m))
-            t.v.copy_(torch.as_tensor(s["v"]).to(t.v))
-            t.step.fill_(int(s["step"]))
+        self.id_table.load_slot_state(st.get("id_table"))
 
     def dp_state_tensors(self):
-        t = self.id_table
-        extra = [t.weight] + ([t.m] if t.m is not t.weight else []) + \
-            ([t.v] if t.v is not t.weight and t.v is not t.m else []) + [t.step]
-        return list(super().dp_state_tensors()) + extra
+        return list(super().dp_state_tensors()) + self.id_table.state_tensors()

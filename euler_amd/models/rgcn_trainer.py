@@ -25,7 +25,7 @@ from euler_amd.dataflow.device_flow import DeviceRelationFlow
 from euler_amd.models.captured import CapturedTrainer
 from euler_amd.ops import gnn_ops, mp_ops
 
-__all__ = ["UnsupRgcnTrainer", "edge_relations"]
+__all__ = ["UnsupRgcnTrainer", "RowSparseRgcnTrainer", "edge_relations"]
 
 
 def edge_relations(graph, feature_idx, feature_dim):
@@ -124,3 +124,136 @@ class UnsupRgcnTrainer(CapturedTrainer):
 
     def reset_metric(self):
         self.mrr.zero_()
+
+
+class _RowsAt(torch.nn.Module):
+    """Stand-in for the id embedding during a row-sparse step: returns the rows of the
+    step's gathered leaf at the positions the step computed for the one id tensor the
+    encoder embeds (the block's node set)."""
+
+    def __init__(self, num, dim):
+        super().__init__()
+        self.num, self.dim = int(num), int(dim)
+        self.rows = self.p = None
+
+    def forward(self, ids):
+        if self.p is None or ids.numel() != self.p.numel():
+            raise RuntimeError("row-sparse R-GCN step: unexpected id lookup")
+        return self.rows[self.p].reshape(*ids.shape, self.dim)
+
+
+class RowSparseRgcnTrainer(UnsupRgcnTrainer):
+    """UnsupRgcnTrainer with the id embedding table row-sharded and row-sparse
+    (:class:`~euler_amd.parallel.sparse_table.ShardedTable`): per step the blocks' node set
+    (unique by construction, padding collapsed) is gathered from the table — from the
+    owner ranks over one fixed-capacity all-to-all when world > 1 — runs through the
+    encoder's own projection and the relation convolutions, and its row gradients go back
+    to the owners' row-sparse optimizer.  The relation weights and ``fc`` stay in the flat
+    buffer.  Per-step work is independent of |V| (reference examples/rgcn/rgcn.py:30-105,
+    tf_euler/python/utils/embedding.py:24-68)."""
+
+    def __init__(self, model, graph, batch_size, optimizer="adam", learning_rate=0.01, group=None):
+        from euler_amd.parallel.sparse_table import ShardedTable
+
+        enc = model.gnn._encoder
+        mod = getattr(enc, "embedding", None)
+        if mod is None or not hasattr(mod, "num"):
+            raise ValueError("RowSparseRgcnTrainer needs the encoder's id embedding")
+        opt = optimizer if optimizer in ("adam", "adagrad", "sgd") else "adam"
+        self.id_table = ShardedTable(int(mod.num), int(mod.dim), graph.device, group, opt, learning_rate)
+        self.id_table.load(mod.weight.detach())
+        self._mod, self._enc = mod, enc
+        self._names = [k for k, v in model.state_dict(keep_vars=True).items() if v is mod.weight]
+        enc.embedding = _RowsAt(mod.num, mod.dim)
+        self._pending = None
+        super().__init__(model, graph, batch_size, optimizer, learning_rate)
+        self.world = self.id_table.world
+
+    def _swap_in(self):
+        if not isinstance(self._enc.embedding, _RowsAt):
+            self._enc.embedding = _RowsAt(self._mod.num, self._mod.dim)
+
+    def _embed(self, rows):
+        from euler_amd.ops.gnn_ops import unique_first_padded
+
+        self._swap_in()
+        t = self.id_table
+        df = self.flow.produce(rows)
+        ids = self._node_ids(df[0].n_id)
+        ids = torch.where((ids < 0) | (ids >= t.num_rows), torch.full_like(ids, t.num_rows - 1), ids)
+        uids, inv, _ = unique_first_padded(ids)
+        tab_rows, h = t.lookup_static(uids, trash_row=True)
+        leaf = tab_rows.detach().requires_grad_(torch.is_grad_enabled())
+        stub = self._enc.embedding
+        stub.rows, stub.p = leaf, h.pos[inv]
+        self._pending = (h, leaf)
+        x = self.gnn.to_x(ids).float()
+        for conv, block in zip(self.gnn.convs, df):
+            x_t = mp_ops.gather(x, block.res_n_id)
+            x = F.relu(self._relation_conv(conv, x_t, x, block.edge_index, block.e_id, block.size))
+        return self.gnn.fc(x)
+
+    def _step(self, grad_sync=None):
+        loss = self._forward_loss()
+        self.opt.zero_grad()
+        loss.backward()
+        scale = 1.0
+        if grad_sync is not None:
+            s = grad_sync(self.flat.grad)
+            scale = 1.0 if s is None else float(s)
+        self.opt.step(scale)
+        h, leaf = self._pending
+        g = leaf.grad if leaf.grad is not None else torch.zeros_like(leaf)
+        n = g.shape[0] - 1
+        self.id_table.apply_static(h, g[:n] / self.world if self.world > 1 else g[:n])
+        stub = self._enc.embedding
+        stub.rows = stub.p = None
+        self._pending = None
+        self.loss_out.copy_(loss.detach())
+        return self.loss_out
+
+    # ------------------------------------------------------------------ state
+    def state_dict(self):
+        sd = {k: v.detach().cpu() for k, v in self.model.state_dict().items()}
+        full = self.id_table.full().cpu()
+        for k in self._names:
+            sd[k] = full
+        return sd
+
+    checkpoint_model_state = state_dict
+
+    def logical_params(self):
+        return {k: v.to(self.device) for k, v in self.state_dict().items()}
+
+    def load_logical(self, sd):
+        with torch.no_grad():
+            own = self.model.state_dict()
+            for k, v in sd.items():
+                if k in own:
+                    own[k].copy_(torch.as_tensor(v).to(own[k]))
+        for k in self._names:
+            if k in sd:
+                self.id_table.load(sd[k])
+
+    def write_to_model(self, model):
+        with torch.no_grad():
+            w = self._mod.weight
+            w.copy_(self.id_table.full().to(w))
+        if model is not self.model:
+            model.load_state_dict(self.state_dict(), strict=False)
+
+    def finish(self):
+        self.write_to_model(self.model)
+        self._enc.embedding = self._mod
+
+    def trainer_state(self):
+        st = super().trainer_state()
+        st["id_table"] = self.id_table.slot_state()
+        return st
+
+    def load_trainer_state(self, st):
+        super().load_trainer_state(st)
+        self.id_table.load_slot_state(st.get("id_table"))
+
+    def dp_state_tensors(self):
+        return list(super().dp_state_tensors()) + self.id_table.state_tensors()

@@ -363,6 +363,44 @@ class ShardedTable:
     def global_ids(self):
         return torch.arange(self.weight.shape[0], device=self.device) * self.world + self.rank
 
+    def full(self) -> torch.Tensor:
+        """the whole [num_rows, D] table on every rank (a collective when world > 1):
+        checkpoints keep a sharded table under the model's own parameter name"""
+        if self.world == 1:
+            return self.weight.detach().clone()
+        rows = -(-self.num_rows // self.world)
+        pad = torch.zeros(rows, self.dim, device=self.weight.device)
+        pad[: self.weight.shape[0]] = self.weight.detach()
+        parts = [torch.zeros_like(pad) for _ in range(self.world)]
+        dist.all_gather(parts, pad, group=self.group)
+        return torch.stack(parts, 1).reshape(-1, self.dim)[: self.num_rows].clone()  # row r = parts[r % W][r // W]
+
+    def load(self, w: torch.Tensor):
+        """this rank's rows from a whole table ([num_rows, D]) or from its own shard"""
+        w = torch.as_tensor(w).to(self.weight)
+        with torch.no_grad():
+            self.weight.copy_(w[self.global_ids()] if w.shape[0] == self.num_rows and self.world > 1 else
+                              w[: self.weight.shape[0]])
+
+    def slot_state(self):
+        return {"m": self.m.cpu().clone(), "v": self.v.cpu().clone(), "step": int(self.step.item())}
+
+    def load_slot_state(self, s):
+        """optimizer slots saved by :meth:`slot_state` (skipped for another shard shape)"""
+        if s is None or torch.as_tensor(s["m"]).shape != self.m.shape:
+            return
+        self.m.copy_(torch.as_tensor(s["m"]).to(self.m))
+        self.v.copy_(torch.as_tensor(s["v"]).to(self.v))
+        self.step.fill_(int(s["step"]))
+
+    def state_tensors(self):
+        """every tensor a training step changes (rollback snapshots, re-sync broadcasts)"""
+        ts = [self.weight]
+        for t in (self.m, self.v):
+            if all(t is not u for u in ts):
+                ts.append(t)
+        return ts + [self.step]
+
     def nbytes(self):
         ts = {id(t): t for t in (self.weight, self.m, self.v)}.values()
         return sum(t.numel() * t.element_size() for t in ts)

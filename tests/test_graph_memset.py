@@ -54,11 +54,33 @@ def test_captured_zero_is_ordered(cuda, nbytes, how):
 
 
 @pytest.mark.gpu
+def test_kg_step_graph_structure_with_memset(cuda):
+    """the captured KG step with memset zeroing is one linear chain of nodes: every memset
+    node has the previous kernel as its only predecessor and the next kernel as its only
+    successor (tools/graph_dot.py prints the node list)"""
+    from tools.graph_dot import analyse, capture_kg
+
+    g, _ = capture_kg("1")
+    try:
+        a = analyse(_hip().graph_summary(g.raw_cuda_graph()))
+    finally:
+        g.reset()
+    print(a)
+    assert a["kinds"].get("memset", 0) >= 1
+    assert a["linear_chain"] and len(a["roots"]) == 1
+    for m in a["memset_nodes"]:
+        assert all(k == "kernel" for k, _ in m["succs"]) and len(m["succs"]) == 1
+
+
+@pytest.mark.gpu
 def test_kg_step_memset_2000_replays_finite(cuda, monkeypatch):
+    """2,000 back-to-back replays of the captured KG step with memset zeroing stay finite;
+    its drift from the zero-kernel step is of the size of two zero-kernel runs' own drift
+    (the backward's fp32 atomics add in a data-dependent order)"""
     from tests.test_kg_step import _setup
 
-    runs = {}
-    for mode in ("0", "1"):
+    runs = []
+    for mode in ("0", "0", "1"):
         monkeypatch.setenv("EULER_AMD_ZERO_MEMSET", mode)
         m, flat, opt, step, ei, erel = _setup(cuda, 1)
         s = torch.cuda.Stream()
@@ -76,9 +98,10 @@ def test_kg_step_memset_2000_replays_finite(cuda, monkeypatch):
         torch.cuda.synchronize()
         assert int(opt.step_count.item()) == 2002
         assert bool(torch.isfinite(flat.flat).all()), mode
-        runs[mode] = (flat.flat.detach().clone(), float(step.loss[0]))
+        runs.append((flat.flat.detach().clone(), float(step.loss[0])))
         del g
-    (p0, l0), (p1, l1) = runs["0"], runs["1"]
-    # the same draws and the same arithmetic: only the zeroing differs
-    assert abs(l0 - l1) <= 1e-3 * max(abs(l0), 1e-6)
-    assert float((p0 - p1).norm() / p0.norm()) < 1e-3
+    (a, la), (b, lb), (c, lc) = runs
+    d_kk = float((a - b).norm() / a.norm())
+    d_km = max(float((a - c).norm() / a.norm()), float((b - c).norm() / b.norm()))
+    print("kernel-vs-kernel drift", d_kk, "memset-vs-kernel drift", d_km, "losses", la, lb, lc)
+    assert d_km <= 5.0 * d_kk + 1e-4

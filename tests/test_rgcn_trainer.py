@@ -70,3 +70,40 @@ def test_rgcn_device_path_gpu_captured(tmp_path, cuda):
                 "cuda", "--seed", "1", "--data_dir", str(tmp_path / "data"), "--model_dir", str(tmp_path / "ckpt"),
                 "--device_graph", "--learning_rate", "0.01"], model="rgcn")
     assert res["step"] == 80 and math.isfinite(res["loss"])
+
+
+def test_row_sparse_rgcn_matches_dense_first_step_cpu(tmp_path):
+    """RowSparseRgcnTrainer (id table row-sparse: the blocks' node set gathered, sparse Adam
+    on those rows) against UnsupRgcnTrainer (the table in the dense flat buffer): the same
+    embedding of the same blocks, and after one Adam step the same parameters (an
+    untouched row's first update is zero); the estimator trains it on request and its
+    checkpoint keeps the table under the model's name"""
+    from euler_amd.graph.device_graph import DeviceGraph
+    from euler_amd.models.rgcn_trainer import RowSparseRgcnTrainer, UnsupRgcnTrainer
+
+    out = {}
+    for cls in (UnsupRgcnTrainer, RowSparseRgcnTrainer):
+        a, m, est = _setup(tmp_path / cls.__name__)
+        est._prepare(est.get_train_from_input(8, est.params))
+        g = DeviceGraph.from_engine(seed=5, device="cpu")
+        tr = cls(m, g, 8)
+        roots = torch.randint(0, g.num_rows, (tr.flow.B,), generator=torch.Generator().manual_seed(3))
+        with torch.no_grad():
+            emb = tr._embed(roots)
+        tr.step()
+        out[cls.__name__] = (emb, float(tr.loss), tr.logical_params())
+    (e0, l0, p0), (e1, l1, p1) = out["UnsupRgcnTrainer"], out["RowSparseRgcnTrainer"]
+    assert torch.allclose(e0, e1, atol=1e-6)
+    assert abs(l0 - l1) <= 1e-5 * abs(l0) and set(p0) == set(p1)
+    for k in p0:
+        assert torch.allclose(p0[k], p1[k], atol=1e-6), k
+    a, m, est = _setup(tmp_path / "est")
+    est.params.update(device_graph=True, row_sparse_tables=True, total_step=6, log_steps=3)
+    res = est.train()
+    assert type(est.device_trainer).__name__ == "RowSparseRgcnTrainer"
+    assert res["step"] == 6 and math.isfinite(res["loss"])
+    from euler_amd.estimator.base import latest_checkpoint
+
+    ck = torch.load(latest_checkpoint(str(tmp_path / "est" / "ckpt")), map_location="cpu", weights_only=True)
+    key = "gnn._encoder.embedding.weight"
+    assert torch.equal(ck["model"][key], m.state_dict()[key])
