@@ -24,7 +24,41 @@ import torch
 
 from euler_amd.parallel.flat import FlatOptimizer, FlatParams
 
-__all__ = ["CapturedTrainer"]
+__all__ = ["CapturedTrainer", "new_graph", "graph_audit"]
+
+
+def new_graph():
+    """a torch CUDAGraph for a captured step; ``EULER_AMD_KEEP_GRAPHS=1`` keeps the
+    underlying hipGraph (``raw_cuda_graph``) for :func:`graph_audit` (instantiated on the
+    first replay)"""
+    import os
+
+    keep = os.environ.get("EULER_AMD_KEEP_GRAPHS", "0") == "1"
+    return torch.cuda.CUDAGraph(keep_graph=True) if keep else torch.cuda.CUDAGraph()
+
+
+def graph_audit(graphs):
+    """node kinds of kept captured graphs (:func:`new_graph`): {steps: {kind: count}} plus
+    the memset / memcpy / fill nodes by name — a captured step should hold kernels only
+    (tests/test_graph_memset.py)"""
+    from euler_amd.ops._native import hip
+
+    out = {}
+    for k, g in graphs.items():
+        s = hip().graph_summary(g.raw_cuda_graph())
+        kinds = {}
+        for _, kind, _ in s["nodes"]:
+            kinds[kind] = kinds.get(kind, 0) + 1
+        preds, succs = {}, {}
+        for a, b in s["edges"]:
+            succs[a] = succs.get(a, 0) + 1
+            preds[b] = preds.get(b, 0) + 1
+        chain = len(s["edges"]) == len(s["nodes"]) - 1 and all(
+            preds.get(i, 0) <= 1 and succs.get(i, 0) <= 1 for i, _, _ in s["nodes"])
+        out[k] = {"kinds": kinds, "non_kernel": [(kind, d) for _, kind, d in s["nodes"] if kind != "kernel"],
+                  "fills": [d for _, kind, d in s["nodes"] if kind == "kernel" and "rocclr" in d],
+                  "linear_chain": chain}
+    return out
 
 
 class CapturedTrainer:
@@ -105,7 +139,7 @@ class CapturedTrainer:
         self.flat.rebind_grads()
         self._graphs = {}
         for k in sorted({1, int(steps)} | {int(e) for e in extra_sizes if int(e) > 0}, reverse=True):
-            gr = torch.cuda.CUDAGraph()
+            gr = new_graph()
             with torch.cuda.graph(gr, capture_error_mode="thread_local"):
                 for _ in range(k):
                     self._step(grad_sync)

@@ -43,6 +43,7 @@ import euler_amd.ops.graph_api as ge
 from euler_amd.ops import gnn_ops
 from euler_amd.ops._native import hip, use_hip
 from euler_amd.parallel.sparse_table import ShardedTable
+from euler_amd.models.captured import new_graph
 
 __all__ = ["DeepWalkTrainer", "DeepWalkEstimatorTrainer"]
 
@@ -128,7 +129,7 @@ class DeepWalkTrainer:
             for _ in range(int(warm)):
                 self.warm_loss = self._step_static()
         cur.wait_stream(side)
-        g = torch.cuda.CUDAGraph()
+        g = new_graph()
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
             self._step_static()
         self.hip_graph = g
@@ -469,7 +470,7 @@ class DeepWalkEstimatorTrainer:
         torch.cuda.synchronize(self.device)
         self._graphs, self._graph_loss = {}, {}
         for k in sorted({1, int(steps)} | {int(e) for e in extra_sizes if int(e) > 0}, reverse=True):
-            gr = torch.cuda.CUDAGraph()
+            gr = new_graph()
             with torch.cuda.graph(gr, capture_error_mode="thread_local"):
                 for _ in range(k):
                     out = self._one()

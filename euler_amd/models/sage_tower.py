@@ -39,6 +39,7 @@ import torch.nn.functional as F
 from euler_amd.models._tower_ops import pair_loss, tower_head
 from euler_amd.ops._native import hip
 from euler_amd.parallel.flat import FlatOptimizer, FlatParams
+from euler_amd.models.captured import new_graph
 
 # the fused 7-launch step (PairPlan) on GPUs; EULER_AMD_PAIR_FUSED_STEP=0 keeps the
 # per-op autograd step (tower kernels + GEMM autograd nodes)
@@ -499,7 +500,7 @@ class UnsupSageTrainer:
         self.flat.rebind_grads()
         self._graphs = {}
         for k in sorted({1, int(steps)} | {int(e) for e in extra_sizes if int(e) > 0}, reverse=True):
-            g = torch.cuda.CUDAGraph()
+            g = new_graph()
             with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 for _ in range(k):
                     self._step(grad_sync)

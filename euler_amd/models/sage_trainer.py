@@ -43,6 +43,7 @@ import torch
 import torch.nn.functional as F
 
 from euler_amd.ops._native import hip
+from euler_amd.models.captured import new_graph
 
 __all__ = ["SageTrainer", "sage_param_names"]
 
@@ -582,7 +583,7 @@ class SageTrainer:
         torch.cuda.synchronize(self.device)
         self._graphs = {}
         for k in sorted({1, int(steps)} | {int(e) for e in extra_sizes if int(e) > 0}, reverse=True):
-            g = torch.cuda.CUDAGraph()
+            g = new_graph()
             # thread-local capture: RCCL's watchdog thread keeps querying the events of
             # collectives that just finished; under the default global mode such a query
             # during the capture invalidates it and aborts the process (seen on a box:

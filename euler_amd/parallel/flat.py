@@ -46,7 +46,9 @@ class FlatParams:
 
     def zero_grad(self):
         if use_hip(self.grad):
-            hip().zero_(self.grad)  # a memset node in captured steps, not a fill kernel
+            # one zero_kernel launch (a kernel node in captured steps; EULER_AMD_ZERO_MEMSET=1
+            # makes it a hipMemsetAsync node instead: docs/DESIGN.md §9, tests/test_graph_memset.py)
+            hip().zero_(self.grad)
         else:
             self.grad.zero_()
 

@@ -105,3 +105,49 @@ def test_kg_step_memset_2000_replays_finite(cuda, monkeypatch):
     d_km = max(float((a - c).norm() / a.norm()), float((b - c).norm() / b.norm()))
     print("kernel-vs-kernel drift", d_kk, "memset-vs-kernel drift", d_km, "losses", la, lb, lc)
     assert d_km <= 5.0 * d_kk + 1e-4
+
+
+@pytest.mark.gpu
+def test_captured_steps_hold_kernels_only(cuda, monkeypatch):
+    """VERDICT r4 item 4 audit: every captured step is one linear chain with no memset node
+    and no runtime fill / copy blit (``__amd_rocclr_*``); the headline SAGE step (4 launches)
+    and the fused GCN step (12) hold kernel nodes only, the generic full-flow step adds
+    torch's ordered device-to-device memcpy nodes (loss hand-off, overflow flags)"""
+    from euler_amd.models.captured import graph_audit
+    from tests.test_gcn_trainer import _graph as gcn_graph
+    from tests.test_gcn_trainer import _materialize, _setup as gcn_setup
+    from tests.test_sage_trainer import _trainer as sage_trainer
+
+    monkeypatch.setenv("EULER_AMD_KEEP_GRAPHS", "1")
+    report = {}
+
+    sage = sage_trainer(cuda, [10, 5], [64, 64, 32], 16)
+    sage.capture(warmup=2, steps=2)
+    sage.replay_steps(3)
+    report["SageTrainer"] = graph_audit(sage._graphs)
+
+    from euler_amd.models.full_trainer import FullFlowTrainer
+    from euler_amd.models.gcn_trainer import GcnTrainer
+
+    m = gcn_setup("cuda").to("cuda")
+    g = gcn_graph(m, "cuda", torch.bfloat16)
+    _materialize(m, g, 64)
+    gcn = GcnTrainer.from_model(m, g, 64, caps="bounded")
+    gcn.capture(warmup=2, steps=2)
+    gcn.replay_steps(3)
+    report["GcnTrainer"] = graph_audit(gcn._graphs)
+    m2 = gcn_setup("cuda").to("cuda")
+    _materialize(m2, g, 64)
+    ff = FullFlowTrainer.from_model(m2, g, 64, caps="exact")
+    ff.capture(warmup=2, steps=2)
+    ff.replay_steps(3)
+    report["FullFlowTrainer"] = graph_audit(ff._graphs)
+    torch.cuda.synchronize()
+    print(report)
+    for name, graphs in report.items():
+        for k, a in graphs.items():
+            assert a["linear_chain"] and a["fills"] == [] and "memset" not in a["kinds"], (name, k, a)
+            if name in ("SageTrainer", "GcnTrainer"):  # the hand-written steps: kernels only
+                assert a["non_kernel"] == [], (name, k, a)
+            else:  # torch's device-to-device copy_ (loss hand-off, overflow flags): ordered memcpy nodes
+                assert all(kind == "memcpy" for kind, _ in a["non_kernel"]), (name, k, a)
