@@ -142,7 +142,7 @@ class FullFlowTrainer(CapturedTrainer):
 
     # ------------------------------------------------------------------ inference
     def _infer_flow(self, n):
-        if not isinstance(self.flow, DeviceFullFlow):
+        if self.gnn is None or not isinstance(self.flow, DeviceFullFlow):
             return None  # sampled flows: the engine path infers (their draws are the engine's)
         return infer_flow(self, self.graph, self.flow.masks, self.flow.self_loops, n)
 

@@ -191,6 +191,17 @@ def test_device_graph_replay_matches_eager():
     np.testing.assert_allclose(graph[2:], eager[2:], rtol=1e-4, atol=1e-5)
 
 
+# held-out F1 floors on the planted-community graph after 200 device-path steps (measured
+# on MI355X, profiles/r5_zoo/: gcn 0.896, sgcn 0.894, tagcn 0.889, arma 0.889, solution
+# 0.842, gat 0.830, appnp 0.764, adaptivegcn 0.528; the engine path's GCN 0.894).  AGNN,
+# DNA, FastGCN, GeniePath and LGCN learn this task slowly on either path (AGNN / DNA /
+# FastGCN reach F1 0.0 on the engine path too in 200 steps): for them the held-out loss
+# must beat the best constant prediction (0.2338 for 16 one-hot labels).
+_ZOO_F1 = {"gcn": 0.8, "sgcn": 0.8, "tagcn": 0.8, "arma": 0.8, "solution": 0.7, "gat": 0.7, "appnp": 0.6,
+           "adaptivegcn": 0.3}
+_CONST_LOSS = 0.2338
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("model", ["gcn", "appnp", "sgcn", "tagcn", "agnn", "gat", "arma", "dna", "fastgcn",
                                    "adaptivegcn", "geniepath", "lgcn", "solution"])
@@ -198,10 +209,15 @@ def test_estimator_device_graph_gcn_family_gpu(tmp_path, monkeypatch, model):
     monkeypatch.chdir(tmp_path)
     from euler_amd.tools.runner import main
 
-    r = main(["--dataset", "ppi", "--scale", "0.05", "--batch_size", "64", "--log_steps", "40", "--device", "cuda",
-              "--seed", "1", "--model_dir", str(tmp_path / "ckpt"), "--device_graph", "--total_step", "80",
-              "--learning_rate", "0.01"], model=model)
-    assert r["step"] == 80 and math.isfinite(r["loss"]) and r["loss"] < 0.693
+    r, ev = main(["--dataset", "community", "--scale", "0.5", "--batch_size", "64", "--log_steps", "100",
+                  "--device", "cuda", "--seed", "1", "--model_dir", str(tmp_path / "ckpt"), "--device_graph",
+                  "--total_step", "200", "--learning_rate", "0.01", "--run_mode", "train_and_evaluate",
+                  "--data_dir", str(tmp_path / "data")], model=model)
+    assert r["step"] == 200 and math.isfinite(r["loss"]) and math.isfinite(ev["loss"])
+    if model in _ZOO_F1:
+        assert ev["f1"] >= _ZOO_F1[model], ev
+    else:
+        assert ev["loss"] < _CONST_LOSS - 0.002, ev
 
 
 def test_device_flow_dst_csr_equals_sorted_csr_cpu():

@@ -81,11 +81,23 @@ def test_fused_step_matches_fp32_torch(cuda, layers, bases, drop):
         p.grad = None
     ref_loss = _oracle_loss(ref, ei.cpu(), erel.cpu(), (s, r, d, n), keeps)
     ref_loss.backward()
-    assert abs(loss - float(ref_loss)) <= 2e-2 * abs(float(ref_loss)) + 1e-4
+    errs = {}
     for (name, p), gf in zip(ref.named_parameters(), g_fused):
         gr = p.grad.float()
-        err = float((gf - gr).norm() / gr.norm().clamp(min=1e-12))
-        assert err < 5e-2, (name, err)
+        errs[name] = float((gf - gr).norm() / gr.norm().clamp(min=1e-12))
+    print("loss", loss, float(ref_loss), "relative gradient errors", errs)
+    # bf16 operands (messages, relation-transformed rows, MFMA inputs) against fp32 torch;
+    # bounds per parameter from MI355X runs (profiles/r5_zoo/kg_step_fp32_oracle.log):
+    # <= 1 layer every gradient 0.3-0.5 % (bound 1 %); with 2 layers the first layer's
+    # and the entity table's gradients pass through two bf16 message hops, 2.8-3.6 %
+    # (bound 5 %), the rest 0.3-0.5 % (bound 1 %); the loss agrees to 3e-5 (bound 1e-4)
+    assert abs(loss - float(ref_loss)) <= 1e-4 * abs(float(ref_loss)) + 1e-5
+    deep = layers >= 2
+    for name, err in errs.items():
+        bound = 5e-2 if deep and (name == "ent" or name.startswith("convs.0.")) else 1e-2
+        if layers == 0:
+            bound = 1e-5  # no message passing: the scores are the only bf16-free path
+        assert err < bound, (name, err, bound)
     # same optimizer step count -> same draws; after the update -> new draws
     before = [t.clone() for t in step.batch()]
     step.forward_backward()
