@@ -119,6 +119,19 @@ class GcnPlan {
     cntw_.zero_();
   }
 
+  // one eager step with the head's fp32 root aggregates written out [B][KP] (diagnostics)
+  torch::Tensor head_aggregates() {
+    const c10::DeviceGuard guard(dev_);
+    torch::Tensor out = torch::zeros({B_, head_.lin.inp}, torch::TensorOptions().dtype(torch::kFloat32).device(dev_));
+    GcnHeadArgs a = head_;
+    a.dbg_agg = out.data_ptr<float>();
+    step_until_head();
+    ok(eh_gcn_head(&a, stream()), "gcn_head(dbg)");
+    if (L_ == 2) ok(eh_gcn_dw(&dw_, dw_blocks_, stream()), "gcn_dw");
+    ok(eh_gcn_reduce(&red_, stream()), "gcn_reduce");
+    return out;
+  }
+
   // the last step's flow (for tests): roots, node set, per-hop counts, edges and offsets
   py::dict flow() const {
     py::dict o;
@@ -457,6 +470,7 @@ void register_gcn_ops(py::module& m) {
       .def("step", &GcnPlan::step)
       .def("flow", &GcnPlan::flow)
       .def("reset_counters", &GcnPlan::reset_counters)
+      .def("head_aggregates", &GcnPlan::head_aggregates)
       .def("head_profile", &GcnPlan::head_profile)
       .def_property_readonly("launches", &GcnPlan::launches);
 }

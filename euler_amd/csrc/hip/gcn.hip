@@ -719,6 +719,10 @@ __global__ __launch_bounds__(256) void gcn_head_kernel(GcnHeadArgs a) {
     const int r = i / (KP / 2), c = (i - r * (KP / 2)) * 2;
     *reinterpret_cast<uint32_t*>(Ag + r * LK + c) = pack_bf16x2(acc[r * AggTile<KP>::LDA + c],
                                                                 acc[r * AggTile<KP>::LDA + c + 1]);
+    if (a.dbg_agg && t0 + r < a.B) {
+      a.dbg_agg[(t0 + r) * KP + c] = acc[r * AggTile<KP>::LDA + c];
+      a.dbg_agg[(t0 + r) * KP + c + 1] = acc[r * AggTile<KP>::LDA + c + 1];
+    }
   }
   __syncthreads();
   GH_STAMP(2);

@@ -156,6 +156,7 @@ struct GcnHeadArgs {  // targets: the B roots; sources: S_1
   const float* labels;  // [N][C] dense multi-label targets
   float inv_scale;      // 1 / (B C)
   float* dagg;          // L = 2: [B][lin.inp] fp32 d(agg) of the roots, gcn_dw's input (nullptr: L = 1)
+  float* dbg_agg;       // diagnostics (nullptr in the step): [B][KP] the roots' fp32 aggregates
   float* part_w;        // [nblk][outp][inp]   d(last conv)
   float* part_fc;       // [nblk][Ep][outp]    d(fc W)
   float* part_bfc;      // [nblk][Ep]

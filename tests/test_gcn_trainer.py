@@ -97,8 +97,16 @@ def test_fused_gcn_step_matches_generic_fp32(layers, self_loops):
         r = p.grad.detach()
         errs[n] = float((grads_k[n] - r).norm() / max(float(r.norm()), 1e-12))
     print("loss", loss_k, float(loss), "relative gradient errors", errs)
-    # bf16 MFMA operands against fp32 autograd
-    assert max(errs.values()) < 5e-2, errs
+    # bf16 MFMA operands against fp32 autograd.  Every gradient but the outer conv's agrees
+    # to 0.2-0.6 % (bound 1 %).  The conv weights get 5 %: the kernel's roots' aggregates
+    # equal the bf16-feature reference to 3e-7 (tools/gcn_oracle_probe.py,
+    # profiles/r5_gcn/oracle/), but the aggregate is rounded to bf16 before the conv GEMM,
+    # and a hidden unit whose pre-activation sits at ~0 for every root (dead in the fp32
+    # reference, a zero gradient row) can come out alive for one root — one nonzero row
+    # against a zero row moves the relative error of the whole matrix to ~4 % (L = 1
+    # without self loops), not a wrong sum
+    for n, e in errs.items():
+        assert e < (5e-2 if ".convs." in n else 1e-2), (n, e)
 
 
 @pytest.mark.gpu
