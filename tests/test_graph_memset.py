@@ -119,6 +119,7 @@ def test_captured_steps_hold_kernels_only(cuda, monkeypatch):
     from tests.test_sage_trainer import _trainer as sage_trainer
 
     monkeypatch.setenv("EULER_AMD_KEEP_GRAPHS", "1")
+    monkeypatch.delenv("EULER_AMD_ZERO_MEMSET", raising=False)
     report = {}
 
     sage = sage_trainer(cuda, [10, 5], [64, 64, 32], 16)

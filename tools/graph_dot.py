@@ -18,18 +18,25 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def capture_kg(mode):
     from tests.test_kg_step import _setup
 
+    old = os.environ.get("EULER_AMD_ZERO_MEMSET")
     os.environ["EULER_AMD_ZERO_MEMSET"] = mode
-    m, flat, opt, step, ei, erel = _setup("cuda", 1)
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
-        for _ in range(2):
+    try:
+        m, flat, opt, step, ei, erel = _setup("cuda", 1)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                step.step()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph(keep_graph=True)
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             step.step()
-    torch.cuda.current_stream().wait_stream(s)
-    torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph(keep_graph=True)
-    with torch.cuda.graph(g, capture_error_mode="thread_local"):
-        step.step()
+    finally:  # the zeroing mode is read per call: never leak it into the caller's process
+        if old is None:
+            os.environ.pop("EULER_AMD_ZERO_MEMSET", None)
+        else:
+            os.environ["EULER_AMD_ZERO_MEMSET"] = old
     return g, (m, flat, opt, step)
 
 
