@@ -75,22 +75,66 @@ class GcnPlan {
   }
 
   // one training step up to the flat gradient (loss_out, counts, overflow updated on the device)
-  void step() {
+  // fused_opt: the reduce launch also applies the flat optimizer (set_optimizer)
+  void step(bool fused_opt) {
     const c10::DeviceGuard guard(dev_);
     step_until_head();
     hipStream_t s = stream();
-    ok(eh_gcn_head(&head_, s), "gcn_head");
+    TORCH_CHECK(!fused_opt || red_opt_.fuse_opt, "GcnPlan: set_optimizer first");
+    GcnHeadArgs ha = head_;
+    if (fused_opt) ha.ostep_inc = opt_step_;  // the optimizer's step, read by the reduce below
+    ok(eh_gcn_head(&ha, s), "gcn_head");
     if (L_ == 2) ok(eh_gcn_dw(&dw_, dw_blocks_, s), "gcn_dw");
-    ok(eh_gcn_reduce(&red_, s), "gcn_reduce");
+    if (fused_opt) {
+      ok(eh_gcn_reduce(&red_opt_, s), "gcn_reduce(opt)");
+    } else {
+      ok(eh_gcn_reduce(&red_, s), "gcn_reduce");
+    }
+  }
+
+  // the flat optimizer the fused step applies: d = {flat, grad, m, v, step, kind,
+  // lr, b1, b2, eps, wd, grad_scale}; every reduce segment is a view of `grad`, and the
+  // segments must cover the whole flat buffer.  Returns False (nothing set) otherwise.
+  bool set_optimizer(py::dict d) {
+    auto t = [&](const char* k) { return d[k].cast<torch::Tensor>(); };
+    torch::Tensor flat = t("flat"), grad = t("grad"), m = t("m"), v = t("v"), stp = t("step");
+    need(flat, torch::kFloat32, -1, "flat");
+    need(grad, torch::kFloat32, flat.numel(), "grad");
+    need(m, torch::kFloat32, flat.numel(), "m");
+    need(v, torch::kFloat32, flat.numel(), "v");
+    need(stp, torch::kInt64, 1, "step");
+    GcnReduceArgs r = red_;
+    int64_t covered = 0;
+    const float* g0 = grad.data_ptr<float>();
+    for (int k = 0; k < r.nseg; ++k) {
+      GcnRedSeg& q = r.seg[k];
+      const int64_t off = q.grad - g0;
+      const int64_t n = static_cast<int64_t>(q.rows) * q.cols;
+      if (off < 0 || off + n > flat.numel()) return false;
+      q.p = flat.data_ptr<float>() + off;
+      q.m = m.data_ptr<float>() + off;
+      q.v = v.data_ptr<float>() + off;
+      covered += n;
+    }
+    if (covered != flat.numel()) return false;
+    r.fuse_opt = 1;
+    r.okind = d["kind"].cast<int>();
+    r.ostep = stp.data_ptr<int64_t>();
+    opt_step_ = stp.data_ptr<int64_t>();
+    r.lr = d["lr"].cast<float>();
+    r.b1 = d["b1"].cast<float>();
+    r.b2 = d["b2"].cast<float>();
+    r.eps = d["eps"].cast<float>();
+    r.wd = d["wd"].cast<float>();
+    r.grad_scale = d["grad_scale"].cast<float>();
+    red_opt_ = r;
+    opt_refs_ = {flat, grad, m, v, stp};
+    return true;
   }
 
   void step_until_head() {
     hipStream_t s = stream();
-    ok(eh_alias_sample(prob_.data_ptr<float>(), alias_.data_ptr<int32_t>(),
-                       root_rows_.defined() ? root_rows_.data_ptr<int32_t>() : nullptr, prob_.numel(), B_,
-                       rng_.data_ptr<int64_t>(), 1, roots_.data_ptr<int32_t>(), s),
-       "gcn roots");
-    for (int h = 0; h < L_; ++h) {
+    for (int h = 0; h < L_; ++h) {  // hop 0's expand also draws the roots
       ok(eh_gcn_expand(&hops_[h], s), "gcn_expand");
       ok(eh_gcn_mark(&hops_[h], s), "gcn_mark");
       ok(eh_gcn_place(&hops_[h], s), "gcn_place");
@@ -156,7 +200,7 @@ class GcnPlan {
     }
     return o;
   }
-  int64_t launches() const { return 2 + 3 * L_ + (L_ == 2 ? 2 : 0) + 1; }
+  int64_t launches() const { return 1 + 3 * L_ + (L_ == 2 ? 2 : 0) + 1; }
 
  private:
   py::dict d_;
@@ -175,6 +219,9 @@ class GcnPlan {
   GcnLayerArgs layer_{};
   GcnHeadArgs head_{};
   GcnDwArgs dw_{};
+  GcnReduceArgs red_opt_{};
+  int64_t* opt_step_ = nullptr;
+  std::vector<torch::Tensor> opt_refs_;
   torch::Tensor dagg_;
   GcnReduceArgs red_{};
   int64_t dw_blocks_ = 0;
@@ -251,6 +298,13 @@ class GcnPlan {
       a.h = h;
       a.self_loops = self_;
       a.roots = h == 0 ? roots_.data_ptr<int32_t>() : nullptr;
+      if (h == 0) {
+        a.prob = prob_.data_ptr<float>();
+        a.alias = alias_.data_ptr<int32_t>();
+        a.root_rows = root_rows_.defined() ? root_rows_.data_ptr<int32_t>() : nullptr;
+        a.pop = prob_.numel();
+        a.rng = rng_.data_ptr<int64_t>();
+      }
       a.B = static_cast<int32_t>(B_);
       a.set = set_.data_ptr<int32_t>();
       a.cnt = cnt_.data_ptr<int32_t>();
@@ -467,7 +521,8 @@ class GcnPlan {
 void register_gcn_ops(py::module& m) {
   py::class_<GcnPlan>(m, "GcnPlan")
       .def(py::init<py::dict>())
-      .def("step", &GcnPlan::step)
+      .def("step", &GcnPlan::step, py::arg("fused_opt") = false)
+      .def("set_optimizer", &GcnPlan::set_optimizer)
       .def("flow", &GcnPlan::flow)
       .def("reset_counters", &GcnPlan::reset_counters)
       .def("head_aggregates", &GcnPlan::head_aggregates)

@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include "hip/gcn_args.h"
+#include "hip/optim_math.h"
 #include "hip/tile.h"
 
 namespace euler_hip {
@@ -202,7 +203,18 @@ __global__ __launch_bounds__(256) void gcn_expand_kernel(GcnHop a) {
   int64_t start = 0;
   bool contig = true;
   if (tid < TE && t < nt && t < a.cap_t) {
-    row = a.h == 0 ? a.roots[t] : a.set[t];
+    if (a.h == 0) {  // this block's roots: the alias draw of sampling.hip, stream 1
+      const uint4_t r = Philox::gen(static_cast<uint64_t>(a.rng[0]), (static_cast<uint64_t>(a.rng[1]) << 8) ^ 1ull,
+                                    static_cast<uint64_t>(t));
+      const uint64_t x = (static_cast<uint64_t>(r[0]) << 32) | r[1];
+      int64_t k = static_cast<int64_t>(__umul64hi(x, static_cast<uint64_t>(a.pop)));
+      if (k >= a.pop) k = a.pop - 1;
+      const int64_t pick = (u01(r[2]) < a.prob[k]) ? k : static_cast<int64_t>(a.alias[k]);
+      row = a.root_rows ? a.root_rows[pick] : static_cast<int32_t>(pick);
+      a.roots[t] = row;
+    } else {
+      row = a.set[t];
+    }
     if (row >= 0 && row < a.g.num_rows) deg = masked_degree(a.g, row, a.mask, &start, &contig);
     else row = -1;
   }
@@ -289,36 +301,53 @@ __global__ __launch_bounds__(256) void gcn_expand_kernel(GcnHop a) {
 // ----------------------------------------------------------------------------
 // mark: first occurrences -> positions in S_{h+1}
 // ----------------------------------------------------------------------------
+constexpr int kGcnMarkPer = 4;  // occurrences per thread (1024 per block: a quarter of the look-back chain)
+
 __global__ __launch_bounds__(256) void gcn_mark_kernel(GcnHop a) {
   __shared__ int lds4[4];
   __shared__ int64_t s_prefix;
   const int tid = threadIdx.x;
   const int32_t stamp = a.stamp[0];
-  const int64_t o = static_cast<int64_t>(blockIdx.x) * 256 + tid;
+  const int64_t o0 = static_cast<int64_t>(blockIdx.x) * 256 * kGcnMarkPer + tid * kGcnMarkPer;
   const int64_t base_occ = a.h == 0 ? a.B : 0;
   const int64_t n_occ = base_occ + a.off[a.cap_t];
   // the grid covers the capacity; blocks past the last occurrence exit (nothing reads them)
-  const int64_t lastb = n_occ > 0 ? (n_occ - 1) / 256 : 0;
+  const int64_t lastb = n_occ > 0 ? (n_occ - 1) / (256 * kGcnMarkPer) : 0;
   if (static_cast<int64_t>(blockIdx.x) > lastb) return;
-  int32_t v = -1;
-  bool isf = false;
-  if (o < base_occ) {
-    const int32_t r = a.roots[o];
-    v = (r >= 0 && r < a.g.num_rows) ? r : -1;
-    isf = v >= 0 && a.first[v] == gcn_key(stamp, 0, o);
-  } else if (o < n_occ) {
-    const int64_t e = o - base_occ;
-    if (a.eflag[e] & 2) {
-      v = a.enode[e];
+  int32_t v[kGcnMarkPer];
+  bool isf[kGcnMarkPer];
+  uint8_t fl[kGcnMarkPer];
+#pragma unroll
+  for (int j = 0; j < kGcnMarkPer; ++j) {  // every flag load in flight first
+    const int64_t o = o0 + j;
+    fl[j] = (o >= base_occ && o < n_occ) ? a.eflag[o - base_occ] : 0;
+  }
+  int c = 0;
+#pragma unroll
+  for (int j = 0; j < kGcnMarkPer; ++j) {
+    const int64_t o = o0 + j;
+    v[j] = -1;
+    isf[j] = false;
+    if (o < base_occ) {
+      const int32_t r = a.roots[o];
+      v[j] = (r >= 0 && r < a.g.num_rows) ? r : -1;
+      isf[j] = v[j] >= 0 && a.first[v[j]] == gcn_key(stamp, 0, o);
+    } else if (fl[j] & 2) {
+      v[j] = a.enode[o - base_occ];
       // hop 0: a root reached as a neighbour is already S_1's (the roots come first); a
       // root's key this step is (stamp, hop 0, occurrence < B) — the all-ones initial key
       // shares stamp 0's high word but not the occurrence
-      const uint64_t k = a.first[v];
-      isf = a.h != 0 || (k >> 32) != (gcn_key(stamp, 0, 0) >> 32) || (k & 0xFFFFFFFFu) >= static_cast<uint64_t>(a.B);
+      if (a.h == 0) {
+        const uint64_t k = a.first[v[j]];
+        isf[j] = (k >> 32) != (gcn_key(stamp, 0, 0) >> 32) || (k & 0xFFFFFFFFu) >= static_cast<uint64_t>(a.B);
+      } else {
+        isf[j] = true;
+      }
     }
+    c += isf[j] ? 1 : 0;
   }
   int total = 0;
-  const int incl = block_scan_incl(isf ? 1 : 0, lds4, &total);
+  const int incl = block_scan_incl(c, lds4, &total);
   if (tid < 64) {
     const int64_t p = lb_prefix(a.scan_flag, blockIdx.x, total, static_cast<uint32_t>(stamp) * 8u + 2u * a.h + 1u,
                                 a.err);
@@ -326,15 +355,18 @@ __global__ __launch_bounds__(256) void gcn_mark_kernel(GcnHop a) {
   }
   __syncthreads();
   const int64_t base_pos = a.h == 0 ? 0 : a.cnt[a.h];
-  const int64_t p = base_pos + s_prefix + incl - 1;
-  if (isf) {
+  int64_t p = base_pos + s_prefix + incl - c;
+#pragma unroll
+  for (int j = 0; j < kGcnMarkPer; ++j) {
+    if (!isf[j]) continue;
     if (p < a.cap_n) {
-      a.set[p] = v;
-      a.pos[v] = static_cast<int32_t>(p);
-      a.tag[v] = stamp;
+      a.set[p] = v[j];
+      a.pos[v[j]] = static_cast<int32_t>(p);
+      a.tag[v[j]] = stamp;
     } else {
       atomicOr(a.overflow, 1);
     }
+    ++p;
   }
   if (static_cast<int64_t>(blockIdx.x) == lastb && tid == 255) {
     const int64_t n = base_pos + s_prefix + incl;
@@ -693,6 +725,7 @@ __global__ __launch_bounds__(256) void gcn_head_kernel(GcnHeadArgs a) {
 #define GH_STAMP(k) \
   if (a.prof && threadIdx.x == 0) a.prof[static_cast<int64_t>(blockIdx.x) * 16 + (k)] = wall_clock64()
   GH_STAMP(0);
+  if (a.ostep_inc && blk == 0 && tid == 0) a.ostep_inc[0] += 1;  // read by this step's reduce launch
   if (tid < kGT) s_root[tid] = t0 + tid < a.B ? a.roots[t0 + tid] : -1;
   copy_img(a.wl_img, Wl, HP * LK);
   copy_img(a.wfc_img, Wf, EP * LH);
@@ -1015,7 +1048,15 @@ __global__ __launch_bounds__(256) void gcn_reduce_kernel(GcnReduceArgs a) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) t += red[q][el];
     sg.grad[i] = t;
+    if (a.fuse_opt) {
+      float p = sg.p[i], m = sg.m[i], v = sg.v[i];
+      optim_one(p, t, m, v, static_cast<float>(a.ostep[0]), a.lr, a.b1, a.b2, a.eps, a.wd, a.grad_scale, a.okind);
+      sg.p[i] = p;
+      if (a.okind == 0 || a.okind == 3) sg.m[i] = m;
+      if (a.okind == 0 || a.okind == 1) sg.v[i] = v;
+    }
   }
+
   if (b == 0 && tid < 64) {
     float st[4] = {0.f, 0.f, 0.f, 0.f};
     for (int k = tid; k < a.nstat; k += 64)
@@ -1041,12 +1082,15 @@ using namespace euler_hip;
 extern "C" {
 
 int64_t eh_gcn_expand_blocks(int64_t cap_t) { return ceil_div(cap_t, gcn_expand_tile(cap_t)); }
-int64_t eh_gcn_mark_blocks(const GcnHop* a) { return ceil_div((a->h == 0 ? a->B : 0) + a->cap_e, 256); }
+int64_t eh_gcn_mark_blocks(const GcnHop* a) {
+  return ceil_div((a->h == 0 ? a->B : 0) + a->cap_e, 256 * kGcnMarkPer);
+}
 
 static bool gcn_hop_ok(const GcnHop* a) {
   return a && a->g.indptr && a->g.nbr && a->set && a->cnt && a->off && a->enode && a->etgt && a->esrc && a->deg_s &&
          a->first && a->cntw && a->eflag && a->tag && a->pos && a->scan_deg && a->scan_flag && a->stamp && a->overflow && a->err &&
          a->cap_t > 0 && a->cap_t % 256 == 0 && a->cap_e > 0 && a->cap_n > 0 && a->g.num_types >= 1 &&
+         (a->h > 0 || (a->prob && a->alias && a->rng && a->pop > 0)) &&
          a->g.num_types <= 32 && (a->h > 0 || (a->roots && a->rself && a->B > 0 && a->B <= a->cap_t)) &&
          a->cap_e + a->B < (1ll << 31) && a->cap_n < (1ll << 31);
 }
@@ -1146,7 +1190,9 @@ hipError_t eh_gcn_reduce(const GcnReduceArgs* a, hipStream_t s) {
   for (int k = 0; k < a->nseg; ++k) {
     const GcnRedSeg& g = a->seg[k];
     if (!g.grad || !g.part || g.rows < 1 || g.cols < 1 || g.S < 1 || g.prs < g.cols) return hipErrorInvalidValue;
+    if (a->fuse_opt && (!g.p || !g.m || !g.v)) return hipErrorInvalidValue;
   }
+  if (a->fuse_opt && !a->ostep) return hipErrorInvalidValue;
   hipLaunchKernelGGL(gcn_reduce_kernel, dim3(static_cast<uint32_t>(a->nblk)), dim3(256), 0, s, *a);
   return hipGetLastError();
 }

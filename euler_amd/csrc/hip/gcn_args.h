@@ -71,7 +71,7 @@ struct GcnHop {
   uint32_t mask;           // edge types of this hop
   int32_t h;               // hop index
   int32_t self_loops;      // 1: one (t, t) edge per target (counted in the source degrees)
-  const int32_t* roots;    // hop 0: [B] target rows; nullptr for h >= 1 (targets = set[0, cnt[h]))
+  int32_t* roots;          // hop 0: [B] the drawn roots (expand writes them); nullptr for h >= 1
   int32_t B;
   int32_t* set;            // cumulative node set [cap_set] (ids by position)
   int32_t* cnt;            // [kGcnMaxHops + 1] device counts (cnt[0] = B)
@@ -84,6 +84,13 @@ struct GcnHop {
   int32_t* esrc;           // [cap_e] source position (-1: padding)
   int32_t* deg_s;          // [cap_n] in-block source counts (self loops included)
   int32_t* rself;          // hop 0: [B] the set position of each root (its self-loop source)
+  // hop 0: the roots are drawn by this launch (Walker alias table over root_rows, Philox
+  // (rng[0], rng[1] << 8 ^ 1, t): the same draw as sampling.hip alias_sample_kernel)
+  const float* prob;
+  const int32_t* alias;
+  const int32_t* root_rows;  // nullable: draw rows directly
+  int64_t pop;
+  const int64_t* rng;
   uint64_t* first;         // [N] epoch-keyed first occurrence of a root (hop 0)
   int32_t* cntw;           // [N] per-node edge counters of the running hop (zero between hops:
                            //     each node's counter claimer resets it in place)
@@ -157,6 +164,8 @@ struct GcnHeadArgs {  // targets: the B roots; sources: S_1
   float inv_scale;      // 1 / (B C)
   float* dagg;          // L = 2: [B][lin.inp] fp32 d(agg) of the roots, gcn_dw's input (nullptr: L = 1)
   float* dbg_agg;       // diagnostics (nullptr in the step): [B][KP] the roots' fp32 aggregates
+  int64_t* ostep_inc;   // fused optimizer step: block 0 advances the optimizer's step count
+                        // (the reduce launch then reads it; no ticket over its ~2K blocks)
   float* part_w;        // [nblk][outp][inp]   d(last conv)
   float* part_fc;       // [nblk][Ep][outp]    d(fc W)
   float* part_bfc;      // [nblk][Ep]
@@ -189,6 +198,7 @@ struct GcnRedSeg {
   int64_t slab;         // elements per slab
   int32_t S;
   int32_t blk0;         // first block of the segment
+  float *p, *m, *v;     // fused optimizer: the parameter and its slots, laid out as grad
 };
 struct GcnReduceArgs {
   GcnRedSeg seg[kGcnMaxSegs];
@@ -199,6 +209,13 @@ struct GcnReduceArgs {
   int64_t* counts;         // [3] tp, fp, fn (accumulated)
   int32_t* stamp;          // [1] += 1 (block 0, after every read of this step)
   int64_t* rng;            // [2] (seed, counter): counter += 1 (the step's draws are consumed)
+  // the flat optimizer folded into this launch (one process: no gradient all-reduce between
+  // the reduce and the update): every element is updated where its gradient is summed, at
+  // the optimizer's step count the head launch of this step already advanced (a ticket
+  // over this launch's ~2K blocks would serialise on one word: ~18 us)
+  int32_t fuse_opt, okind;
+  const int64_t* ostep;
+  float lr, b1, b2, eps, wd, grad_scale;
 };
 
 }  // namespace euler_hip

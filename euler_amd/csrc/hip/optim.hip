@@ -8,6 +8,7 @@
 // adagrad, adam); embedding stores: utils/embedding.py:24-68.
 #include "hip/common.h"
 #include "hip/launchers.h"
+#include "hip/optim_math.h"
 
 namespace euler_hip {
 
@@ -30,26 +31,6 @@ struct FlatOptArgs {
   int64_t w0, w1;
   int32_t kind;  // 0 adam, 1 adagrad, 2 sgd, 3 momentum
 };
-
-__device__ __forceinline__ float optim_one(float& p, float g, float& m, float& v, float t, float lr, float b1,
-                                           float b2, float eps, float wd, float grad_scale, int kind) {
-  const float gi = g * grad_scale + wd * p;
-  if (kind == 0) {
-    m = b1 * m + (1.f - b1) * gi;
-    v = b2 * v + (1.f - b2) * gi * gi;
-    const float bc1 = 1.f - __powf(b1, t), bc2 = 1.f - __powf(b2, t);
-    p -= lr * (m / bc1) / (sqrtf(v / bc2) + eps);
-  } else if (kind == 1) {
-    v += gi * gi;
-    p -= lr * gi / (sqrtf(v) + eps);
-  } else if (kind == 2) {
-    p -= lr * gi;
-  } else {
-    m = b1 * m + gi;
-    p -= lr * m;
-  }
-  return p;
-}
 
 __device__ __forceinline__ float flat_wd(const FlatOptArgs& a, int64_t e) {
   return (e >= a.w0 && e < a.w1) ? a.wd2 : a.wd;

@@ -9,19 +9,22 @@ self loops), ``convolution/gcn_conv.py:26-54`` (``fc(sum_e deg_t^-1/2 deg_s^-1/2
 ReLU after each conv, ``fc`` + ``out_fc`` and the sigmoid cross-entropy of
 ``mp_utils/base.py:24-47``.
 
-What one step launches (L = 2 convs; 1 + 3 L + 4 + the optimizer = 12):
+What one step launches (L = 2 convs; 3 L + 4 = 10 on one process, the flat optimizer
+folded into the reduce; 11 with a data-parallel all-reduce between them):
 
-* the root draw (alias table, Philox stream 1 of the graph's (seed, counter));
-* per hop: expand (degrees, look-back scan, neighbour list, one counter atomic per edge
-  whose first taker claims the node), mark (positions of the new nodes), place (edge
+* per hop: expand (hop 0's also draws the roots: the alias table on Philox stream 1 of the
+  graph's (seed, counter), the same draw as ``alias_sample``; degrees, look-back scan,
+  neighbour list, one counter atomic per edge whose first taker claims the node), mark (positions of the new nodes), place (edge
   sources, in-block source counts from the claimers);
 * the outer conv: edge-parallel aggregation + MFMA linear + ReLU;
 * the head: last conv, fc, out_fc, loss, F1 counts and the whole row-local backward, the
   weight-gradient partials of its rows and d(agg) of the roots;
 * d(W0) partials as one GEMM over hop 0's edges (the ReLU mask is per source row, so
   d(h1) is never formed: no scatter); the reduce into the flat gradient (+ loss, counts,
-  RNG counter);
-* the flat optimizer (``parallel/flat.py``), after the data-parallel all-reduce.
+  RNG counter) — on one process it also applies the flat optimizer to every element it
+  sums (``optim_math.h``; the head launch advances FlatOptimizer's step count first);
+* with data parallelism: the all-reduce, then the flat optimizer launch
+  (``parallel/flat.py``).
 
 The generic path (``models/full_trainer.py``) runs the user's convolution modules on
 ``DeviceFullFlow`` blocks: ~100 launches per step.  Both draw the same roots from the same
@@ -194,11 +197,33 @@ class GcnTrainer(CapturedTrainer):
         self.plan = hip().GcnPlan(d)
         self.flow.on_clear = self.plan.reset_counters
         self._plan_caps = list(self.flow.caps)
+        self._fused_opt = self._set_fused_optimizer()
+
+    def _set_fused_optimizer(self, grad_scale: float = 1.0) -> bool:
+        """hand the flat optimizer to the plan so one process's step applies it in the
+        reduce launch (no separate optimizer launch); False when the optimizer has a
+        per-range weight decay or the reduce does not cover the flat buffer"""
+        from euler_amd.parallel.flat import _KINDS
+
+        o = self.opt
+        if o.decay_range[1] > o.decay_range[0] or o._ticket is None:
+            return False
+        return bool(self.plan.set_optimizer({
+            "flat": self.flat.flat, "grad": self.flat.grad, "m": o.m, "v": o.v, "step": o.step_count,
+            "kind": _KINDS[o.kind], "lr": o.lr, "b1": o.b1, "b2": o.b2, "eps": o.eps,
+            "wd": o.wd, "grad_scale": float(grad_scale)}))
+
+    def set_learning_rate(self, lr):
+        super().set_learning_rate(lr)
+        self._fused_opt = self._set_fused_optimizer()
 
     # ------------------------------------------------------------------ step
     def _step(self, grad_sync=None):
         if self._plan_caps != self.flow.caps:  # grown after an overflow: new fixed shapes
             self._build_plan()
+        if grad_sync is None and self._fused_opt:  # one process: the update rides the reduce launch
+            self.plan.step(True)
+            return self.loss_out
         self.plan.step()
         scale = 1.0
         if grad_sync is not None:
@@ -214,7 +239,8 @@ class GcnTrainer(CapturedTrainer):
 
     @property
     def launches_per_step(self) -> int:
-        return int(self.plan.launches) + 1  # + the flat optimizer
+        """launches of one single-process step (the optimizer folded into the reduce)"""
+        return int(self.plan.launches) + (0 if self._fused_opt else 1)
 
     # ------------------------------------------------------------------ metric
     def metric(self) -> float:

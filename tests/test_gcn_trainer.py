@@ -69,7 +69,8 @@ def test_fused_gcn_step_matches_generic_fp32(layers, self_loops):
     _materialize(m, g, B)
     assert GcnTrainer.supports(m, g)
     tr = GcnTrainer.from_model(m, g, B, caps="exact")
-    assert tr.launches_per_step == 2 + 3 * layers + (2 if layers == 2 else 0) + 2
+    # per hop 3, the outer conv + d(W0) (L = 2), head, reduce (+ Adam): 10 for L = 2
+    assert tr.launches_per_step == 3 * layers + (2 if layers == 2 else 0) + 2
     loss_k = float(tr.forward_backward_only())
     torch.cuda.synchronize()
     assert int(tr.flow.overflow.item()) == 0
@@ -181,3 +182,28 @@ def test_fused_gcn_overflow_regrows(tmp_path, monkeypatch):
     est = box["est"]
     assert r["step"] == 24 and math.isfinite(r["loss"]) and est.flow_regrows >= 1
     assert all(c[0] > 256 for c in est.device_trainer.flow.caps)
+
+
+@pytest.mark.gpu
+def test_fused_optimizer_matches_flat_optimizer():
+    """one process: the reduce launch applies Adam (FlatOptimizer semantics, its step count
+    and ticket) — the same parameters, slots and step as the separate flat optimizer launch"""
+    from euler_amd.models.gcn_trainer import GcnTrainer
+
+    out = []
+    for fused in (True, False):
+        m = _setup("cuda").to("cuda")
+        g = _graph(m, "cuda", torch.bfloat16)
+        _materialize(m, g, 64)
+        tr = GcnTrainer.from_model(m, g, 64, caps="exact")
+        assert tr._fused_opt
+        tr._fused_opt = fused
+        for _ in range(6):
+            tr.step()
+        torch.cuda.synchronize()
+        out.append((tr.flat.flat.clone(), tr.opt.m.clone(), tr.opt.v.clone(), int(tr.opt.step_count.item())))
+    (p0, m0, v0, s0), (p1, m1, v1, s1) = out
+    assert s0 == s1 == 6
+    # the aggregation's flush order is data dependent: fp32 rounding only
+    for a, b in ((p0, p1), (m0, m1), (v0, v1)):
+        assert float((a - b).norm() / b.norm().clamp(min=1e-12)) < 1e-4
