@@ -418,10 +418,10 @@ __global__ __launch_bounds__(256) void gcn_place_kernel(GcnHop a) {
 // ----------------------------------------------------------------------------
 constexpr int kGT = 16;  // targets per tile
 
-template <int KP>
+template <int KP, int NT = 256>
 struct AggTile {
   static constexpr int NCH = KP / 8;     // column chunks of 8 (one lane each)
-  static constexpr int NW = 256 / NCH;   // workers per block
+  static constexpr int NW = NT / NCH;    // workers per block of NT threads
   static constexpr int LDA = KP + 1;     // fp32 accumulator row stride (bank spread)
 };
 
@@ -478,13 +478,13 @@ __device__ __forceinline__ void row_axpy(const RowRaw<F32>& r, float w, float* r
 // U per batch, software-pipelined: the next batch's index loads are in flight while the
 // current batch's rows are accumulated, and its rows (+ source degrees) are issued before
 // the loop comes back — one memory round trip per batch instead of two.
-template <int KP, bool F32>
+template <int KP, bool F32, int NT>
 __device__ void gcn_aggregate_t(const GcnAggSrc& src, const int32_t* off, const int32_t* etgt, const int32_t* esrc,
                                 const int32_t* enode, const int32_t* deg_s, const int32_t* self_src, int self_loops,
                                 int64_t t0, int nt, float* acc, float* rdt, int* sself) {
-  using AT = AggTile<KP>;
+  using AT = AggTile<KP, NT>;
   const int tid = threadIdx.x;
-  for (int i = tid; i < kGT * AT::LDA; i += 256) acc[i] = 0.f;
+  for (int i = tid; i < kGT * AT::LDA; i += NT) acc[i] = 0.f;
   __shared__ int64_t s_e[2];
   __shared__ int s_row[kGT];
   if (tid == 0) {
@@ -577,14 +577,14 @@ __device__ void gcn_aggregate_t(const GcnAggSrc& src, const int32_t* off, const 
   __syncthreads();
 }
 
-template <int KP>
+template <int KP, int NT = 256>
 __device__ void gcn_aggregate(const GcnAggSrc& src, const int32_t* off, const int32_t* etgt, const int32_t* esrc,
                               const int32_t* enode, const int32_t* deg_s, const int32_t* self_src, int self_loops,
                               int64_t t0, int nt, float* acc, float* rdt, int* sself) {
   if (src.x_fp32)
-    gcn_aggregate_t<KP, true>(src, off, etgt, esrc, enode, deg_s, self_src, self_loops, t0, nt, acc, rdt, sself);
+    gcn_aggregate_t<KP, true, NT>(src, off, etgt, esrc, enode, deg_s, self_src, self_loops, t0, nt, acc, rdt, sself);
   else
-    gcn_aggregate_t<KP, false>(src, off, etgt, esrc, enode, deg_s, self_src, self_loops, t0, nt, acc, rdt, sself);
+    gcn_aggregate_t<KP, false, NT>(src, off, etgt, esrc, enode, deg_s, self_src, self_loops, t0, nt, acc, rdt, sself);
 }
 
 // ----------------------------------------------------------------------------
@@ -620,19 +620,20 @@ __device__ __forceinline__ void stage_w(const float* w, int rows, int cols, int 
 }
 
 // copy a staged bf16 image (global, 16-byte multiples) into LDS: every load in flight
+template <int NT = 256>
 __device__ __forceinline__ void copy_img(const uint16_t* src, bf16_t* dst, int n) {
   const uint4_t* s = reinterpret_cast<const uint4_t*>(src);
   uint4_t* d = reinterpret_cast<uint4_t*>(dst);
   const int n16 = n >> 3;
   constexpr int U = 8;
-  for (int i0 = threadIdx.x; i0 < n16; i0 += 256 * U) {
+  for (int i0 = threadIdx.x; i0 < n16; i0 += NT * U) {
     uint4_t v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (i0 + u * 256 < n16) v[u] = s[i0 + u * 256];
+      if (i0 + u * NT < n16) v[u] = s[i0 + u * NT];
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (i0 + u * 256 < n16) d[i0 + u * 256] = v[u];
+      if (i0 + u * NT < n16) d[i0 + u * NT] = v[u];
   }
 }
 
@@ -646,9 +647,15 @@ __host__ __device__ constexpr int img_ld(int w) { return w <= 64 ? 80 : 144; }
 // ----------------------------------------------------------------------------
 // layer (L = 2): targets S_1 in tiles of 16, sources S_2 (feature rows by node id)
 // ----------------------------------------------------------------------------
+// threads per 16-target tile of the layer launch (512 measured slower on PPI: 33.4 vs
+// 25.2 us, profiles/r5_gcn/fused_v3/ — the tile's LDS flushes contend and fewer tiles
+// are resident)
+constexpr int kGcnLayerThreads = 256;
+
 template <int KP, int HP>
-__global__ __launch_bounds__(256) void gcn_layer_kernel(GcnLayerArgs a) {
-  constexpr int LDK = img_ld(KP), LDAcc = AggTile<KP>::LDA;
+__global__ __launch_bounds__(kGcnLayerThreads) void gcn_layer_kernel(GcnLayerArgs a) {
+  constexpr int NT = kGcnLayerThreads;
+  constexpr int LDK = img_ld(KP), LDAcc = AggTile<KP, NT>::LDA;
   __shared__ __attribute__((aligned(16))) bf16_t wimg[HP * LDK];
   __shared__ __attribute__((aligned(16))) bf16_t aimg[kGT * LDK];
   __shared__ float acc[kGT * LDAcc];
@@ -657,19 +664,20 @@ __global__ __launch_bounds__(256) void gcn_layer_kernel(GcnLayerArgs a) {
   const int nt = a.cnt[1];
   const int64_t t0 = static_cast<int64_t>(blockIdx.x) * kGT;
   if (t0 >= nt) return;  // uniform: rows past the set are never read
-  copy_img(a.wimg, wimg, HP * LDK);
+  copy_img<NT>(a.wimg, wimg, HP * LDK);
   __shared__ int sself[kGT];
-  gcn_aggregate<KP>(a.src, a.off, a.etgt, a.esrc, a.enode, a.deg_s, nullptr, a.self_loops, t0, nt, acc, rdt, sself);
+  gcn_aggregate<KP, NT>(a.src, a.off, a.etgt, a.esrc, a.enode, a.deg_s, nullptr, a.self_loops, t0, nt, acc, rdt,
+                        sself);
   // aggregate -> bf16 image + the dW operand rows
-  for (int i = tid; i < kGT * (KP / 2); i += 256) {
+  for (int i = tid; i < kGT * (KP / 2); i += NT) {
     const int r = i / (KP / 2), c = (i - r * (KP / 2)) * 2;
     const uint32_t pk = pack_bf16x2(acc[r * LDAcc + c], acc[r * LDAcc + c + 1]);
     *reinterpret_cast<uint32_t*>(aimg + r * LDK + c) = pk;
     *reinterpret_cast<uint32_t*>(a.agg_out + (t0 + r) * KP + c) = pk;
   }
   __syncthreads();
-  // z = agg W^T, h = relu(z): wave w -> 16-column tiles w, w + 4, ...
-  for (int ct = wave; ct < HP / 16; ct += 4) {
+  // z = agg W^T, h = relu(z): wave w -> 16-column tiles w, w + NT / 64, ...
+  for (int ct = wave; ct < HP / 16; ct += NT / 64) {
     float4_t z = float4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int k0 = 0; k0 < KP; k0 += 32)
@@ -1135,7 +1143,8 @@ static bool gcn_src_ok(const GcnAggSrc& s, int kp) {
     else KERNEL(128, 64, __VA_ARGS__);                                              \
   } while (0)
 
-#define GCN_LAYER(K, H, grid, s, A) hipLaunchKernelGGL((gcn_layer_kernel<K, H>), grid, dim3(256), 0, s, A)
+#define GCN_LAYER(K, H, grid, s, A) \
+  hipLaunchKernelGGL((gcn_layer_kernel<K, H>), grid, dim3(kGcnLayerThreads), 0, s, A)
 
 hipError_t eh_gcn_layer(const GcnLayerArgs* a, hipStream_t s) {
   if (!a || !a->enode || !a->off || !a->etgt || !a->esrc || !a->deg_s || !a->cnt || !a->h_out || !a->agg_out ||
