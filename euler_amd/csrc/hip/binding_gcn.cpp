@@ -116,7 +116,8 @@ class GcnPlan {
       q.v = v.data_ptr<float>() + off;
       covered += n;
     }
-    if (covered != flat.numel()) return false;
+    const int64_t used = d.contains("used") ? d["used"].cast<int64_t>() : flat.numel();
+    if (covered != used) return false;  // every parameter element (the tail is padding)
     r.fuse_opt = 1;
     r.okind = d["kind"].cast<int>();
     r.ostep = stp.data_ptr<int64_t>();

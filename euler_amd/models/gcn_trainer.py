@@ -210,7 +210,7 @@ class GcnTrainer(CapturedTrainer):
             return False
         return bool(self.plan.set_optimizer({
             "flat": self.flat.flat, "grad": self.flat.grad, "m": o.m, "v": o.v, "step": o.step_count,
-            "kind": _KINDS[o.kind], "lr": o.lr, "b1": o.b1, "b2": o.b2, "eps": o.eps,
+            "used": int(self.flat.numel), "kind": _KINDS[o.kind], "lr": o.lr, "b1": o.b1, "b2": o.b2, "eps": o.eps,
             "wd": o.wd, "grad_scale": float(grad_scale)}))
 
     def set_learning_rate(self, lr):

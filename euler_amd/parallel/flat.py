@@ -31,9 +31,12 @@ class FlatParams:
         if device is None:
             device = self.params[0].device if self.params else torch.device("cpu")
         total = sum(p.numel() for p in self.params)
-        self.numel = total
-        self.flat = torch.zeros(total, dtype=torch.float32, device=device)
-        self.grad = torch.zeros(total, dtype=torch.float32, device=device)
+        self.numel = total  # parameter elements; the buffers are padded to a multiple of 8
+        # (zeros that never get a gradient): the xGMI all-reduce moves 16-byte vectors of
+        # fp32 or bf16 (parallel/xgmi.py), whatever the model's parameter count
+        padded = total + (-total) % 8
+        self.flat = torch.zeros(padded, dtype=torch.float32, device=device)
+        self.grad = torch.zeros(padded, dtype=torch.float32, device=device)
         self.offsets = []
         o = 0
         for p in self.params:

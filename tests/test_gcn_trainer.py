@@ -253,3 +253,71 @@ def test_fused_gcn_wide_shapes_match_generic_fp32(tmp_path, self_loops):
     print("wide shapes: relative gradient errors", errs)
     for n, e in errs.items():
         assert e < (5e-2 if ".convs." in n else 1e-2), (n, e)
+
+
+def _worker_gcn_dp(rank, world, port, q, tmp):
+    """one rank of a 2-process fused-GCN job sharing the GPU (gloo process group, the xGMI
+    peer-memory all-reduce between the plan's reduce and the flat optimizer)"""
+    import os
+
+    try:
+        os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                           "WORLD_SIZE": str(world), "LOCAL_RANK": "0"})
+        import torch.distributed as dist
+
+        from euler_amd.parallel import dp
+
+        dp.init_distributed(backend="gloo", device=torch.device("cuda", 0))
+        from euler_amd.tools import runner
+
+        a = runner.parse_args(["--dataset", "ppi", "--scale", "0.05", "--batch_size", "64", "--total_step", "6",
+                               "--log_steps", "3", "--model_dir", os.path.join(tmp, f"ck{rank}"), "--device_graph",
+                               "--device", "cuda", "--seed", "1", "--data_dir", os.path.join(tmp, "data")],
+                              model="gcn")
+        _, est = runner.build(a)
+        est.train()
+        tr = est.device_trainer
+        flat = tr.flat.flat.detach().cpu().clone()
+        allp = [torch.zeros_like(flat) for _ in range(world)]
+        dist.all_gather(allp, flat)
+        roots = tr.plan.flow()["roots"].cpu().clone()
+        allr = [torch.zeros_like(roots) for _ in range(world)]
+        dist.all_gather(allr, roots)
+        ok = (type(tr).__name__ == "GcnTrainer" and all(torch.equal(x, allp[0]) for x in allp)
+              and not torch.equal(allr[0], allr[1]) and bool(torch.isfinite(flat).all()) and est.global_step == 6)
+        q.put((rank, "gcn_dp", bool(ok), getattr(est, "grad_sync_name", None)))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+
+
+@pytest.mark.gpu
+def test_fused_gcn_two_ranks_share_the_gpu_in_lockstep(tmp_path):
+    """the data-parallel form of the fused GCN step (unfused optimizer, gradient all-reduce
+    between reduce and update): 2 ranks on one GPU end bit-identical, having drawn
+    different roots"""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker_gcn_dp, args=(r, 2, port, q, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    res = []
+    while not q.empty():
+        res.append(q.get())
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == 2 and all(r[2] for r in res), res
