@@ -947,13 +947,15 @@ class PairPlan {
     TrOptArgs& o = opt_;
     torch::Tensor flat = T("flat");
     need(flat, torch::kFloat32, -1, "flat");
-    o.n = flat.numel();
-    o.p = flat.data_ptr<float>();
-    o.g = ptr<float>("grad", torch::kFloat32, o.n);
-    o.m = ptr<float>("m", torch::kFloat32, o.n);
-    o.v = ptr<float>("v", torch::kFloat32, o.n);
     std::vector<int64_t> off = d_["offsets"].cast<std::vector<int64_t>>();
-    TORCH_CHECK(off.size() == 9 && off.back() == o.n, "PairPlan: offsets = 8 segments + end");
+    // the flat buffers may end in padding (parallel/flat.py pads to a multiple of 8)
+    TORCH_CHECK(off.size() == 9 && off.back() <= flat.numel(), "PairPlan: offsets = 8 segments + end");
+    o.n = off.back();
+    const int64_t nbuf = flat.numel();
+    o.p = flat.data_ptr<float>();
+    o.g = ptr<float>("grad", torch::kFloat32, nbuf);
+    o.m = ptr<float>("m", torch::kFloat32, nbuf);
+    o.v = ptr<float>("v", torch::kFloat32, nbuf);
     int blk = 0, seg = 0;
     const TowerPlan* tp[2] = {&s, &c};
     for (int t = 0; t < 2; ++t) {
@@ -1016,7 +1018,8 @@ class PairPlan {
   }
   void set_lr(double lr) { opt_.lr = static_cast<float>(lr); }
   void set_grad(torch::Tensor g) {
-    need(g, torch::kFloat32, opt_.n, "grad");
+    need(g, torch::kFloat32, -1, "grad");
+    TORCH_CHECK(g.numel() >= opt_.n, "grad has ", g.numel(), " elements, fewer than the ", opt_.n, " parameters");
     grad_keep_ = g;
     opt_.g = g.data_ptr<float>();
   }
