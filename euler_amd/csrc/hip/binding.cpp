@@ -572,11 +572,14 @@ void register_gnn_ops(pybind11::module& m);
 void register_tree_ops(pybind11::module& m);
 // binding_gcn.cpp: fused GCN step plan
 void register_gcn_ops(pybind11::module& m);
+// binding_graph_cls.cpp: fused graph-classification step plan
+void register_graph_cls_ops(pybind11::module& m);
 
 PYBIND11_MODULE(_hip_ops, m) {
   register_gnn_ops(m);
   register_tree_ops(m);
   register_gcn_ops(m);
+  register_graph_cls_ops(m);
   m.doc() = "euler_amd hand-written CDNA4 (gfx950) HIP kernels";
   m.attr("arch") = "gfx950";
   m.def("rng_advance", &rng_advance);

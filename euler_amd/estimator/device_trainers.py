@@ -189,11 +189,26 @@ def _kg(c: Ctx):
 def _graph(c: Ctx):
     # GraphEstimator: graphs' node lists, labels and sparse feature ids in HBM, induced
     # blocks built on the device (models/graph_trainer.py)
+    from euler_amd.models.graph_cls_trainer import GraphClsTrainer
     from euler_amd.models.graph_trainer import GraphTrainer
 
     p = c.params
     label = p["label"][0] if isinstance(p["label"], (list, tuple)) else p["label"]
-    return GraphTrainer(c.model, c.upload(node_type=-1), c.batch, label, int(p["num_classes"]), **c.opt_kw())
+    g = c.upload(node_type=-1)
+    cls = GraphTrainer
+    if p.get("graph_fused", True) and g.device.type == "cuda" and GraphClsTrainer.supports(c.model):
+        # GIN / GraphGCN: one workgroup per graph, the whole step in two launches
+        # (models/graph_cls_trainer.py); graphs beyond its limits take the generic step
+        cls = GraphClsTrainer
+    try:
+        return cls(c.model, g, c.batch, label, int(p["num_classes"]), **c.opt_kw())
+    except ValueError as e:
+        if cls is GraphTrainer:
+            raise
+        import logging
+
+        logging.getLogger(__name__).warning("fused graph-classification step not applicable (%s): generic step", e)
+        return GraphTrainer(c.model, g, c.batch, label, int(p["num_classes"]), **c.opt_kw())
 
 
 @register("graph_autoencoder", _cls("GraphAutoEncoder", "VariationalGraphAutoEncoder"))

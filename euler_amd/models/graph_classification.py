@@ -16,9 +16,10 @@ __all__ = ["SparseFeatureGNN", "GIN", "GatedGraph", "GraphGCN", "Set2SetModel"]
 
 
 class SparseFeatureGNN(BaseGNNNet):
-    def __init__(self, conv, flow, dims, fanouts, metapath, feature_idx, feature_max_id, conv_kwargs=None):
+    def __init__(self, conv, flow, dims, fanouts, metapath, feature_idx, feature_max_id, conv_kwargs=None,
+                 add_self_loops=False):
         self._conv_kwargs = dict(conv_kwargs or {})
-        super().__init__(conv, flow, dims, fanouts, metapath, add_self_loops=False)
+        super().__init__(conv, flow, dims, fanouts, metapath, add_self_loops=add_self_loops)
         self.feature_idx = feature_idx if isinstance(feature_idx, list) else [feature_idx]
         self.encoder = SparseEmbedding(feature_max_id, dims[0])
 
@@ -56,7 +57,10 @@ class GatedGraph(_PooledGraphModel):
 class GraphGCN(_PooledGraphModel):
     def __init__(self, dims, metapath, label_dim, feature_idx, feature_max_id):
         super().__init__(label_dim)
-        self.gnn = SparseFeatureGNN("graphgcn", "full", dims, None, metapath, feature_idx, feature_max_id)
+        # the reference's GraphGCN flow adds self loops (examples/graphgcn/graphgcn.py:32), the
+        # other graph models' flows do not
+        self.gnn = SparseFeatureGNN("graphgcn", "full", dims, None, metapath, feature_idx, feature_max_id,
+                                    add_self_loops=True)
         self.pool = Pooling("add")
 
 
