@@ -36,11 +36,9 @@ class GraphClsPlan {
     a.kind = static_cast<int32_t>(geti("kind"));
     a.self_loops = static_cast<int32_t>(geti("self_loops"));
     a.nmax = static_cast<int32_t>(geti("nmax"));
-    a.emax = static_cast<int32_t>(std::max<int64_t>(geti("emax"), 1));
     a.E = static_cast<int32_t>(geti("E"));
     a.C = static_cast<int32_t>(geti("C"));
     a.G = static_cast<int32_t>(geti("G"));
-    a.mean_comb = static_cast<int32_t>(geti("mean_comb"));
     a.tab_rows = static_cast<int32_t>(geti("tab_rows"));
     TORCH_CHECK(a.L >= 1 && a.L <= kGcMaxLayers, "GraphClsPlan: 1 to ", kGcMaxLayers, " convs");
     TORCH_CHECK(a.kind == 0 || a.kind == 1, "GraphClsPlan: kind 0 (GIN) or 1 (GraphConv)");
@@ -54,27 +52,22 @@ class GraphClsPlan {
       dmax = std::max(dmax, D[l]);
     }
     TORCH_CHECK(a.E >= 1 && a.E <= kGcMaxWidth && a.C >= 1 && a.C <= kGcMaxLabels, "GraphClsPlan: fc / label widths");
-    TORCH_CHECK(static_cast<int64_t>(a.tab_rows) * a.D[0] <= kGcMaxTable, "GraphClsPlan: the embedding table exceeds ",
-                kGcMaxTable, " elements");
-    // adjacency of every distinct mask
-    py::list offs = d_["adj_off"], nbrs = d_["adj_nbr"], roffs = d_["adj_roff"], rnbrs = d_["adj_rnbr"];
-    a.nadj = static_cast<int32_t>(offs.size());
-    TORCH_CHECK(a.nadj >= 1 && a.nadj <= kGcMaxAdj && nbrs.size() == offs.size() && roffs.size() == offs.size() &&
-                    rnbrs.size() == offs.size(),
-                "GraphClsPlan: 1 to ", kGcMaxAdj, " adjacencies");
-    torch::Tensor gbase = T("gbase");
-    need(gbase, torch::kInt32, a.G + 1, "gbase");
-    dev_ = gbase.device();
-    const int64_t nall = gbase[a.G].item<int32_t>();
+    TORCH_CHECK(static_cast<int64_t>(a.tab_rows) * a.D[0] <= kGcMaxTable && a.tab_rows >= 1 &&
+                    a.tab_rows <= kGcMaxTableRows,
+                "GraphClsPlan: the embedding table must have 1..", kGcMaxTableRows, " rows and at most ", kGcMaxTable,
+                " elements");
+    // graph records, edge pairs of every distinct mask, feature pairs
+    py::list pairs = d_["adj_pair"];
+    a.nadj = static_cast<int32_t>(pairs.size());
+    TORCH_CHECK(a.nadj >= 1 && a.nadj <= kGcMaxAdj, "GraphClsPlan: 1 to ", kGcMaxAdj, " adjacencies");
+    torch::Tensor rec = T("rec");
+    need(rec, torch::kInt32, static_cast<int64_t>(a.G) * kGcRec, "rec");
+    dev_ = rec.device();
     for (int j = 0; j < a.nadj; ++j) {
-      torch::Tensor o = offs[j].cast<torch::Tensor>(), n = nbrs[j].cast<torch::Tensor>();
-      torch::Tensor ro = roffs[j].cast<torch::Tensor>(), rn = rnbrs[j].cast<torch::Tensor>();
-      need(o, torch::kInt32, nall + 1, "adj_off");
-      need(ro, torch::kInt32, nall + 1, "adj_roff");
-      need(n, torch::kInt32, -1, "adj_nbr");
-      need(rn, torch::kInt32, -1, "adj_rnbr");
-      keep_.insert(keep_.end(), {o, n, ro, rn});
-      a.adj[j] = GcAdj{o.data_ptr<int32_t>(), n.data_ptr<int32_t>(), ro.data_ptr<int32_t>(), rn.data_ptr<int32_t>()};
+      torch::Tensor pr = pairs[j].cast<torch::Tensor>();
+      need(pr, torch::kInt32, -1, "adj_pair");
+      keep_.push_back(pr);
+      a.adj[j] = GcAdj{pr.data_ptr<int32_t>()};
     }
     std::vector<int64_t> adj_of = getv("adj_of");
     TORCH_CHECK(static_cast<int>(adj_of.size()) == a.L, "GraphClsPlan: one adjacency per conv");
@@ -82,22 +75,22 @@ class GraphClsPlan {
       TORCH_CHECK(adj_of[l] >= 0 && adj_of[l] < a.nadj, "GraphClsPlan: adjacency index");
       a.adj_of[l] = static_cast<int32_t>(adj_of[l]);
     }
-    torch::Tensor gprob = T("gprob"), galias = T("galias"), rng = T("rng"), fo = T("fo"), fid = T("fid"),
+    torch::Tensor gprob = T("gprob"), galias = T("galias"), rng = T("rng"), fpair = T("fpair"), fw = T("fw"),
                   onehot = T("onehot"), table = T("table");
     need(gprob, torch::kFloat32, a.G, "gprob");
     need(galias, torch::kInt32, a.G, "galias");
     need(rng, torch::kInt64, 2, "rng");
-    need(fo, torch::kInt32, nall + 1, "fo");
-    need(fid, torch::kInt32, -1, "fid");
+    need(fpair, torch::kInt32, -1, "fpair");
+    need(fw, torch::kFloat32, fpair.numel(), "fw");
     need(onehot, torch::kFloat32, static_cast<int64_t>(a.G) * a.C, "onehot");
     need(table, torch::kFloat32, static_cast<int64_t>(a.tab_rows) * a.D[0], "table");
-    keep_.insert(keep_.end(), {gprob, galias, rng, gbase, fo, fid, onehot, table});
+    keep_.insert(keep_.end(), {gprob, galias, rng, rec, fpair, fw, onehot, table});
     a.gprob = gprob.data_ptr<float>();
     a.galias = galias.data_ptr<int32_t>();
     a.rng = rng.data_ptr<int64_t>();
-    a.gbase = gbase.data_ptr<int32_t>();
-    a.fo = fo.data_ptr<int32_t>();
-    a.fid = fid.data_ptr<int32_t>();
+    a.rec = rec.data_ptr<int32_t>();
+    a.fpair = fpair.data_ptr<int32_t>();
+    a.fw = fw.data_ptr<float>();
     a.onehot = onehot.data_ptr<float>();
     a.table = table.data_ptr<float>();
     // parameters
@@ -143,6 +136,11 @@ class GraphClsPlan {
     a.o_bfc = geti("o_bfc");
     a.o_out = geti("o_out");
     a.o_tab = geti("o_tab");
+    torch::Tensor warm = T("warm");
+    need(warm, torch::kFloat32, -1, "warm");
+    keep_.push_back(warm);
+    a.warm = warm.data_ptr<float>();
+    a.warm_n = warm.numel();
     // outputs
     a.S = geti("S");
     auto opt = [&](c10::ScalarType st) { return torch::TensorOptions().dtype(st).device(dev_); };
@@ -156,6 +154,7 @@ class GraphClsPlan {
     a.gidx = gidx_.data_ptr<int32_t>();
     a.inv_scale = 1.f / static_cast<float>(static_cast<int64_t>(a.B) * a.C);
     a.ostep_inc = nullptr;
+    if (has("max_lds")) max_lds_ = geti("max_lds");
     layout(dmax);
     // reduce
     GcReduceArgs& r = r_;
@@ -215,8 +214,19 @@ class GraphClsPlan {
     return true;
   }
 
+  // one eager step (no optimizer) with per-block phase stamps [B][32] (diagnostics)
+  torch::Tensor profile() {
+    const c10::DeviceGuard guard(dev_);
+    torch::Tensor prof = torch::zeros({a_.B, 32}, torch::TensorOptions().dtype(torch::kInt64).device(dev_));
+    GcStepArgs a = a_;
+    a.prof = reinterpret_cast<long long*>(prof.data_ptr<int64_t>());
+    gc_ok(eh_gc_step(&a, gc_stream()), "gc_step(prof)");
+    gc_ok(eh_gc_reduce(&r_, gc_stream()), "gc_reduce");
+    return prof;
+  }
   torch::Tensor gidx() const { return gidx_; }
   int64_t lds_bytes() const { return a_.lds_bytes; }
+  bool z_kept() const { return a_.zst != 0; }
 
  private:
   py::dict d_;
@@ -225,6 +235,7 @@ class GraphClsPlan {
   GcReduceArgs r_{}, ro_{};
   std::vector<torch::Tensor> keep_, opt_keep_;
   torch::Tensor slab_, loss_part_, acc_part_, gidx_;
+  int64_t max_lds_ = 160 * 1024;  // "max_lds" in the dict: a smaller budget (tests of the global-weight path)
 
   void layout(int64_t dmax) {
     GcStepArgs& a = a_;
@@ -234,20 +245,32 @@ class GraphClsPlan {
       off += (bytes + 15) / 16 * 16;
       return static_cast<int32_t>(o);
     };
+    const int64_t nmax = a.nmax;
     for (int l = 0; l <= a.L; ++l) {
       a.ldx[l] = a.D[l] + 4;
-      a.lds_x[l] = take(static_cast<int64_t>(a.nmax) * a.ldx[l] * 4);
+      a.lds_x[l] = take(nmax * a.ldx[l] * 4);
     }
     const int64_t kmax = a.kind == 1 ? 2 * dmax : dmax;
     a.ldz = static_cast<int32_t>(kmax + 4);
     a.ldy = static_cast<int32_t>(dmax + 4);
-    a.lds_z = take(static_cast<int64_t>(a.nmax) * a.ldz * 4);
-    a.lds_dz = take(static_cast<int64_t>(a.nmax) * a.ldz * 4);
-    a.lds_dy = take(static_cast<int64_t>(a.nmax) * a.ldy * 4);
-    a.lds_tab = take(static_cast<int64_t>(a.tab_rows) * a.D[0] * 4);
-    a.lds_vec = take((4 * kGcMaxWidth + 3 * kGcMaxLabels) * 4);
-    a.lds_adj = take(static_cast<int64_t>(a.nadj) * (2 * (a.nmax + 1) + 2 * a.emax) * 4);
+    a.lda = static_cast<int32_t>(nmax + 4);
+    a.trp = (a.tab_rows + 15) / 16 * 16;
+    a.ldsm = a.trp + 4;
+    a.ldt = a.D[0] + 4;
+    a.lds_dz = take(nmax * a.ldz * 4);
+    a.lds_dy = take(nmax * a.ldy * 4);
+    a.lds_vec = take((5 * kGcMaxWidth + 4 * kGcMaxLabels) * 4);
+    a.lds_a = take(a.nadj * nmax * a.lda * 4);
+    a.lds_invc = take(a.nadj * nmax * 4);
+    a.lds_s = take(nmax * a.ldsm * 4);
+    a.lds_t = take(static_cast<int64_t>(a.trp) * a.ldt * 4);
+    a.lds_csum = take(static_cast<int64_t>(kGcMaxRows / 16) * kGcMaxWidth * 4);
+    const int64_t z1 = nmax * a.ldz * 4;
+    a.lds_z = take(z1);
     TORCH_CHECK(off <= 160 * 1024, "GraphClsPlan: the step needs ", off, " bytes of LDS (> 160 KB)");
+    // when it fits: every conv's Z kept for its backward (no recomputed aggregate)
+    a.zst = off + (a.L - 1) * z1 <= max_lds_ ? 1 : 0;
+    if (a.zst) off += (a.L - 1) * ((z1 + 15) / 16 * 16);
     a.lds_bytes = static_cast<int32_t>(off);
   }
 
@@ -281,5 +304,7 @@ void register_graph_cls_ops(py::module& m) {
       .def("step", &GraphClsPlan::step, py::arg("fused_opt") = false)
       .def("set_optimizer", &GraphClsPlan::set_optimizer)
       .def("gidx", &GraphClsPlan::gidx)
-      .def_property_readonly("lds_bytes", &GraphClsPlan::lds_bytes);
+      .def("profile", &GraphClsPlan::profile)
+      .def_property_readonly("lds_bytes", &GraphClsPlan::lds_bytes)
+      .def_property_readonly("z_kept", &GraphClsPlan::z_kept);
 }

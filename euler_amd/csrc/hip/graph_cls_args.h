@@ -11,13 +11,18 @@
 //
 //   gc_step    one block per drawn graph (the draw is the alias table on the graph RNG's
 //              Philox stream 3, as alias_sample): every node of the graph stays in LDS for
-//              the whole step.  Forward: the embedding bag, per conv the aggregate (LDS
-//              CSR of the graph) and an fp32 MFMA GEMM (v_mfma_f32_16x16x4_f32: exact
-//              fp32, the torch oracle's numerics) with bias / ReLU in its epilogue, fc and
-//              add pooling folded into one mat-vec of the pooled ReLU output, out_fc, loss.
-//              Backward: the pooled head's rank-1 gradients, per conv dW = G^T Z and
-//              dZ = G W as MFMA GEMMs, the transposed aggregate through the reverse CSR,
-//              the embedding-table gradient accumulated in LDS.  Every gradient element is
+//              the whole step, and every product is an fp32 MFMA GEMM on LDS operands
+//              (v_mfma_f32_16x16x4_f32: exact fp32, the torch oracle's numerics).  The
+//              graph's adjacency becomes a dense [n][n] count matrix A per edge-type mask
+//              (n <= 64), the node features a dense [n][rows] bag matrix S, so
+//                embedding     X0 = S T
+//                aggregate     GIN  Z = A X + (1 + eps + self) X
+//                              GraphConv  Z = [X | diag(1 / cnt) (A + self I) X]
+//                linear        X' = relu(Z [W | Wf]^T + b)
+//              then fc, add pooling and out_fc as mat-vecs of the pooled ReLU output, the
+//              loss; backward: the pooled head's rank-1 gradients, per conv dW = G^T Z and
+//              dZ = G W, the transposed aggregate A^T dZ (masked by the layer below's ReLU
+//              in its epilogue), the table gradient S^T dX0.  Every gradient element is
 //              written once into the block's slab row (no atomics on global memory).
 //   gc_reduce  the B slab rows summed in block order into the flat gradient, or straight
 //              into the flat optimizer's update (one process); loss, accuracy, RNG counter.
@@ -33,21 +38,22 @@ constexpr int kGcThreads = 256;
 constexpr int kGcMaxRows = 64;      // nodes per graph
 constexpr int kGcMaxWidth = 128;    // conv / fc widths
 constexpr int kGcMaxLabels = 64;
-constexpr int kGcMaxTable = 8192;   // embedding-table elements (LDS gradient accumulator)
+constexpr int kGcMaxTable = 8192;   // embedding-table elements (staged in LDS)
+constexpr int kGcMaxTableRows = 64; // rows of the dense bag matrix S
 
-// one edge-type mask's adjacency of every graph, local node indices (static, built once)
+constexpr int kGcRec = 12;          // ints per graph record: n, feature pairs [f0, f1), per mask edge pairs [e0, e1)
+
+// one edge-type mask's edges of every graph, graph by graph (static, built once): each
+// edge t <- s (the flow's full-neighbour expansion of t, repeats kept) as (t << 8) | s in
+// local node indices
 struct GcAdj {
-  const int32_t* off;   // [Nall + 1] in-neighbour offsets of every node (global positions)
-  const int32_t* nbr;   // local index of each in-neighbour (source) within its graph
-  const int32_t* roff;  // [Nall + 1] reverse: the targets each node is a source of
-  const int32_t* rnbr;
+  const int32_t* pair;
 };
 
 struct GcStepArgs {
   int32_t L, B, kind;   // kind 0: GIN, 1: GraphConv
   int32_t self_loops;
   int32_t nmax;         // LDS rows (max nodes per graph, rounded up to 16)
-  int32_t emax;         // LDS edges per adjacency (max over graphs)
   int32_t D[kGcMaxLayers + 1];  // D[0]: embedding width; D[l + 1]: conv l's width
   int32_t E, C;         // fc width, labels
   int32_t adj_of[kGcMaxLayers];
@@ -58,10 +64,9 @@ struct GcStepArgs {
   const float* gprob;   // [G] alias table of the uniform graph draw
   const int32_t* galias;
   const int64_t* rng;   // (seed, counter): this launch draws with counter + 1
-  const int32_t* gbase; // [G + 1] first node of each graph (node numbering of the adjacency)
-  const int32_t* fo;    // [Nall + 1] feature offsets of every node
-  const int32_t* fid;   // embedding-table rows
-  int32_t mean_comb;    // SparseEmbedding combiner: 0 sum, 1 mean
+  const int32_t* rec;   // [G][kGcRec] graph records
+  const int32_t* fpair; // (node << 16) | table row of every feature occurrence, graph by graph
+  const float* fw;      // its bag weight (1; 1 / features of the node for the mean combiner)
   const float* onehot;  // [G][C]
   // parameters (flat fp32 views)
   const float* table;   // [tab_rows][D0]
@@ -84,9 +89,16 @@ struct GcStepArgs {
   int32_t* gidx;        // [B] the drawn graphs
   int64_t* ostep_inc;   // block 0 advances the optimizer's step (the fused update reads it)
   float inv_scale;      // 1 / (B C)
-  // LDS layout (bytes), computed by the host
-  int32_t lds_x[kGcMaxLayers + 1], lds_z, lds_dy, lds_dz, lds_tab, lds_vec, lds_adj, lds_bytes;
-  int32_t ldx[kGcMaxLayers + 1], ldz, ldy;
+  // LDS layout (bytes), computed by the host: activations X_l [nmax][ldx], Z [nmax][ldz]
+  // (one per conv when zst, else one recomputed in the backward), dZ, d(out) / G [nmax][ldy],
+  // A [nadj][nmax][lda], 1 / cnt [nadj][nmax], S [nmax][lds], the table [trp][ldt]
+  int32_t lds_x[kGcMaxLayers + 1], lds_z, lds_dy, lds_dz, lds_vec, lds_a, lds_invc, lds_s, lds_t, lds_csum, lds_bytes;
+  int32_t ldx[kGcMaxLayers + 1], ldz, ldy, lda, ldsm, ldt, trp;
+  int32_t zst;
+  // the flat parameter buffer: each XCD's blocks touch it once at the start (L2 warm-up)
+  const float* warm;
+  int64_t warm_n;
+  long long* prof;      // [B][32] phase wall-clock stamps (diagnostics; null in training)
 };
 
 struct GcReduceArgs {

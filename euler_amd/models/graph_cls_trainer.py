@@ -12,10 +12,12 @@ The generic :class:`~euler_amd.models.graph_trainer.GraphTrainer` builds the bat
 induced blocks with :class:`~euler_amd.dataflow.device_flow.DeviceFullFlow` and runs the
 model's own modules: ~60 launches per step for 5 layers.  Graphs are small (MUTAG: 10-28
 nodes), so this trainer gives each drawn graph one workgroup that keeps all of its nodes in
-LDS for the whole step (``csrc/hip/graph_cls.hip``): 2 launches per step, fp32 MFMA GEMMs,
-every gradient written once into a per-graph slab row, and the slab reduction fused with
-the flat optimizer on one process.  The graphs' adjacency (CSR and reverse CSR with local
-node indices, per distinct edge-type mask), node feature ids and labels are uploaded once.
+LDS for the whole step (``csrc/hip/graph_cls.hip``): 2 launches per step; the graph is
+densified in LDS (adjacency count matrix, feature bag matrix) so embedding, aggregation,
+linear and their gradients are all fp32 MFMA GEMMs; every gradient is written once into a
+per-graph slab row, and the slab reduction is fused with the flat optimizer on one process.
+The graphs' adjacency (CSR with local node indices, per distinct edge-type mask), node
+feature ids and labels are uploaded once.
 
 The draw is the generic trainer's (the alias table on the graph RNG's Philox stream 3 at
 the advanced counter), so both trainers see the same graphs from the same RNG state;
@@ -34,7 +36,7 @@ from euler_amd.ops._native import hip
 
 __all__ = ["GraphClsTrainer"]
 
-_MAX_ROWS, _MAX_WIDTH, _MAX_LABELS, _MAX_TABLE, _MAX_LAYERS = 64, 128, 64, 8192, 8
+_MAX_ROWS, _MAX_WIDTH, _MAX_LABELS, _MAX_TABLE, _MAX_TABLE_ROWS, _MAX_LAYERS = 64, 128, 64, 8192, 64, 8
 
 
 def _conv_kind(model):
@@ -95,20 +97,19 @@ class GraphClsTrainer(GraphTrainer):
         self._fused_opt = self._set_fused_optimizer()
 
     # ------------------------------------------------------------------ static inputs
-    def _adjacency(self, mask, nodes, base):
-        """(off, nbr, roff, rnbr) over every graph node (numbered base[g] + local index):
-        in-neighbours = the node's full out-neighbour list under ``mask`` (the flow's
-        expansion, types in order, repeats kept) as local indices of the same graph"""
+    def _edge_pairs(self, mask, nodes):
+        """every graph's edges t <- s under ``mask`` as (t << 8) | s in local node indices,
+        graph by graph (the flow's full-neighbour expansion of t: its out-neighbour list,
+        types in order, repeats kept), and each graph's [begin, end)"""
         g = self.graph
         T = g.num_types
         indptr = g.indptr.cpu().numpy()
         nbr = g.nbr.cpu().numpy()
         types = [t for t in range(T) if (mask >> t) & 1]
-        off, lst, rev = [0], [], [[] for _ in range(int(base[-1]))]
-        emax = 0
+        pairs, spans = [], []
         for gi, rows in enumerate(nodes):
             local = {int(r): v for v, r in enumerate(rows)}
-            e_first = len(lst)
+            e0 = len(pairs)
             for v, r in enumerate(rows):
                 for t in types:
                     a, b = int(indptr[r * T + t]), int(indptr[r * T + t + 1])
@@ -116,16 +117,9 @@ class GraphClsTrainer(GraphTrainer):
                         s = int(s)
                         if s not in local:
                             raise ValueError(f"graph {gi}: node row {r} has a neighbour outside its graph")
-                        lst.append(local[s])
-                        rev[base[gi] + local[s]].append(v)
-                off.append(len(lst))
-            emax = max(emax, len(lst) - e_first)
-        roff = np.zeros(int(base[-1]) + 1, np.int64)
-        roff[1:] = np.cumsum([len(x) for x in rev])
-        rnbr = [t for x in rev for t in x]
-        dev = g.device
-        i32 = lambda a: torch.as_tensor(np.asarray(a, np.int64).astype(np.int32), device=dev)
-        return (i32(off), i32(lst if lst else [0]), i32(roff), i32(rnbr if rnbr else [0])), emax
+                        pairs.append((v << 8) | local[s])
+            spans.append((e0, len(pairs)))
+        return pairs, spans
 
     def _plan_dict(self):
         m, gnn = self.model, self.gnn
@@ -138,30 +132,35 @@ class GraphClsTrainer(GraphTrainer):
         counts = np.array([len(ns) for ns in nodes], np.int64)
         if counts.max() > _MAX_ROWS:
             raise ValueError(f"graphs of more than {_MAX_ROWS} nodes")
-        base = np.zeros(len(nodes) + 1, np.int64)
-        base[1:] = np.cumsum(counts)
-        # one adjacency per distinct mask
-        masks, adj_of, adjs, emax = [], [], [], 1
+        # edge pairs of every distinct mask
+        masks, adj_of, pairs, spans = [], [], [], []
         for mk in self._layer_masks():
             if mk not in masks:
                 masks.append(mk)
-                a, e = self._adjacency(mk, nodes, base)
-                adjs.append(a)
-                emax = max(emax, e)
+                p, sp = self._edge_pairs(mk, nodes)
+                pairs.append(p)
+                spans.append(sp)
             adj_of.append(masks.index(mk))
         if len(masks) > 4:
             raise ValueError("more than 4 distinct edge-type masks")
-        # node feature ids (embedding-table rows), the order of GraphTrainer.feat_ids
+        # feature occurrences (embedding-table rows, GraphTrainer.feat_ids) and bag weights
+        enc = gnn.encoder
         fmat = self.feat_ids.cpu().numpy()
-        fo, fid = [0], []
+        fpair, fw, fspan = [], [], []
         for ns in nodes:
-            for r in ns:
+            f0 = len(fpair)
+            for v, r in enumerate(ns):
                 f = [int(x) for x in fmat[r] if x >= 0]
-                fid += f
-                fo.append(fo[-1] + len(f))
+                fpair += [(v << 16) | x for x in f]
+                fw += [1.0 / len(f) if enc.combiner == "mean" else 1.0] * len(f)
+            fspan.append((f0, len(fpair)))
+        rec = np.zeros((len(nodes), 12), np.int64)
+        rec[:, 0] = counts
+        rec[:, 1:3] = np.asarray(fspan, np.int64).reshape(-1, 2)
+        for j, sp in enumerate(spans):
+            rec[:, 3 + 2 * j:5 + 2 * j] = np.asarray(sp, np.int64).reshape(-1, 2)
         dev = self.graph.device
         i32 = lambda a: torch.as_tensor(np.asarray(a, np.int64).astype(np.int32), device=dev)
-        enc = gnn.encoder
         D = [int(enc.weight.shape[1])]
         for c in convs:
             w = c.mlp.weight if self.kind == 0 else c.liner.weight
@@ -169,8 +168,8 @@ class GraphClsTrainer(GraphTrainer):
         E, C = int(gnn.fc.weight.shape[0]), int(m.out_fc.weight.shape[0])
         if any(d % 16 or d > _MAX_WIDTH for d in D) or E > _MAX_WIDTH or C > _MAX_LABELS:
             raise ValueError(f"widths must be multiples of 16 up to {_MAX_WIDTH} (labels <= {_MAX_LABELS})")
-        if enc.weight.numel() > _MAX_TABLE:
-            raise ValueError(f"the embedding table exceeds {_MAX_TABLE} elements")
+        if enc.weight.numel() > _MAX_TABLE or enc.weight.shape[0] > _MAX_TABLE_ROWS:
+            raise ValueError(f"the embedding table exceeds {_MAX_TABLE_ROWS} rows / {_MAX_TABLE} elements")
         if int(gnn.fc.weight.shape[1]) != D[-1] or int(m.out_fc.weight.shape[1]) != E:
             raise ValueError("fc / out_fc widths do not chain")
         # flat offsets of every parameter
@@ -204,18 +203,21 @@ class GraphClsTrainer(GraphTrainer):
                 eps.append(None)
                 oeps.append(-1)
         d = {"L": L, "B": self.B, "kind": self.kind, "self_loops": int(bool(gnn.sampler.add_self_loops)),
-             "nmax": int(-(-counts.max() // 16) * 16), "emax": int(emax), "D": D, "E": E, "C": C,
-             "G": len(nodes), "mean_comb": int(enc.combiner == "mean"), "tab_rows": int(enc.weight.shape[0]),
-             "adj_off": [a[0] for a in adjs], "adj_nbr": [a[1] for a in adjs], "adj_roff": [a[2] for a in adjs],
-             "adj_rnbr": [a[3] for a in adjs], "adj_of": adj_of,
+             "nmax": int(-(-counts.max() // 16) * 16), "D": D, "E": E, "C": C,
+             "G": len(nodes), "tab_rows": int(enc.weight.shape[0]),
+             "adj_pair": [i32(p if p else [0]) for p in pairs], "adj_of": adj_of, "rec": i32(rec),
+             "fpair": i32(fpair if fpair else [0]),
+             "fw": torch.tensor(fw if fw else [0.0], dtype=torch.float32, device=dev),
              "gprob": self.g_prob.float().contiguous(), "galias": self.g_alias.to(torch.int32).contiguous(),
-             "rng": self.graph.rng, "gbase": i32(base), "fo": i32(fo), "fid": i32(fid if fid else [0]),
+             "rng": self.graph.rng,
              "onehot": self.onehot.float().contiguous(), "table": enc.weight.detach(),
              "W": W, "Wf": Wf, "bl": bl, "eps": eps, "o_W": oW, "o_Wf": oWf, "o_bl": obl, "o_eps": oeps,
              "Wfc": gnn.fc.weight.detach(), "bfc": gnn.fc.bias.detach(), "Wout": m.out_fc.weight.detach(),
              "o_fc": off(gnn.fc.weight), "o_bfc": off(gnn.fc.bias), "o_out": off(m.out_fc.weight),
              "o_tab": off(enc.weight), "S": int(self.flat.numel), "grad": self.flat.grad,
-             "loss_out": self.loss_out, "right": self.right}
+             "loss_out": self.loss_out, "right": self.right, "warm": self.flat.flat}
+        if os.environ.get("EULER_AMD_GRAPH_MAX_LDS"):  # tests: force the recomputed-Z path
+            d["max_lds"] = int(os.environ["EULER_AMD_GRAPH_MAX_LDS"])
         # every flat parameter gets its gradient from the slab (no other trainable tensor)
         cov = sorted(covered)
         pos = 0

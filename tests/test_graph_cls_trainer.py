@@ -59,13 +59,18 @@ def test_cpu_routes_to_generic_trainer(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("model", ["gin", "graphgcn"])
-def test_fused_step_matches_cpu_autograd(tmp_path, cuda, model):
+@pytest.mark.parametrize("model,zst", [("gin", True), ("graphgcn", True), ("gin", False), ("graphgcn", False)])
+def test_fused_step_matches_cpu_autograd(tmp_path, cuda, model, zst, monkeypatch):
+    """both kernel variants: every conv's aggregate kept in LDS for the backward (default)
+    and recomputed there (the fallback when they do not fit, forced by a small LDS budget)"""
     from euler_amd.models.graph_cls_trainer import GraphClsTrainer
 
+    if not zst:
+        monkeypatch.setenv("EULER_AMD_GRAPH_MAX_LDS", "1")
     _, est = _est(tmp_path, model, "cuda")
     tr = _trainer(est)
     assert isinstance(tr, GraphClsTrainer) and tr.launches_per_step == 2
+    assert tr.plan.z_kept == zst
     _, est_c = _est(tmp_path, model, "cpu")
     trc = _trainer(est_c)
     assert len(trc.flat.params) == len(tr.flat.params)
