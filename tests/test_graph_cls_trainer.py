@@ -151,3 +151,71 @@ def test_fused_estimator_learns(tmp_path, cuda, model):
                        "--learning_rate", "0.01"], model=model)
     assert res["step"] == 400 and math.isfinite(res["loss"])
     assert res["accuracy"] > 0.7, res
+
+
+def _worker_graph_dp(rank, world, port, q, tmp, model):
+    """one rank of a 2-process fused graph-classification job sharing the GPU (gloo process
+    group; the gradient all-reduce between the slab reduce and the flat optimizer)"""
+    import os
+
+    try:
+        os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                           "WORLD_SIZE": str(world), "LOCAL_RANK": "0"})
+        import torch.distributed as dist
+
+        from euler_amd.parallel import dp
+
+        dp.init_distributed(backend="gloo", device=torch.device("cuda", 0))
+        from euler_amd.tools import runner
+
+        a = runner.parse_args(["--batch_size", "16", "--total_step", "6", "--log_steps", "3", "--model_dir",
+                               os.path.join(tmp, f"ck{rank}"), "--device_graph", "--device", "cuda", "--seed", "1",
+                               "--data_dir", os.path.join(tmp, "data")], model=model)
+        _, est = runner.build(a)
+        est.train()
+        tr = est.device_trainer
+        flat = tr.flat.flat.detach().cpu().clone()
+        allp = [torch.zeros_like(flat) for _ in range(world)]
+        dist.all_gather(allp, flat)
+        gidx = tr.plan.gidx().cpu().clone()
+        allg = [torch.zeros_like(gidx) for _ in range(world)]
+        dist.all_gather(allg, gidx)
+        ok = (type(tr).__name__ == "GraphClsTrainer" and all(torch.equal(x, allp[0]) for x in allp)
+              and not torch.equal(allg[0], allg[1]) and bool(torch.isfinite(flat).all()) and est.global_step == 6)
+        q.put((rank, "graph_dp", bool(ok), getattr(est, "grad_sync_name", None)))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model", ["gin", "graphgcn"])
+def test_fused_graph_two_ranks_share_the_gpu_in_lockstep(tmp_path, model):
+    """the data-parallel form of the fused step (slab reduce into the flat gradient, the
+    all-reduce, then the flat optimizer): 2 ranks on one GPU end bit-identical, having
+    drawn different graphs"""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker_graph_dp, args=(r, 2, port, q, str(tmp_path), model)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    res = []
+    while not q.empty():
+        res.append(q.get())
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == 2 and all(r[2] for r in res), res
