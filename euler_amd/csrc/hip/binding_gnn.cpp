@@ -629,6 +629,15 @@ void memset_zero(torch::Tensor t) {
   ok(hipMemsetAsync(t.data_ptr(), 0, static_cast<size_t>(t.numel() * t.element_size()), stream()), "memset_zero");
 }
 
+// hipGraphUpload of an instantiated graph (torch.cuda.CUDAGraph.raw_cuda_graph_exec()) on
+// torch's current stream: the executable's device-side state is prepared ahead of its first
+// launch, so the first replay starts like every later one
+void graph_upload(int64_t exec_handle) {
+  hipGraphExec_t e = reinterpret_cast<hipGraphExec_t>(static_cast<uintptr_t>(exec_handle));
+  TORCH_CHECK(e != nullptr, "graph_upload: null graph exec");
+  ok(hipGraphUpload(e, c10::hip::getCurrentHIPStream().stream()), "graph upload");
+}
+
 // Nodes and dependency edges of a captured hipGraph (torch.cuda.CUDAGraph(keep_graph=True)
 // .raw_cuda_graph()), plus hipGraphDebugDotPrint into dot_path when given.  Every node:
 // (index, kind, detail) — kernel name, memset (dst, bytes, value) or memcpy; edges as
@@ -1070,6 +1079,7 @@ void register_gnn_ops(pybind11::module& m) {
   m.def("zero_", &zero_);
   m.def("memset_zero", &memset_zero);
   m.def("graph_summary", &graph_summary, py::arg("graph"), py::arg("dot_path") = "");
+  m.def("graph_upload", &graph_upload, py::arg("exec"));
   m.def("seg_count", &seg_count);
   m.def("flow_block", &flow_block);
   m.def("gcn_norm_weight", &gcn_norm_weight);
