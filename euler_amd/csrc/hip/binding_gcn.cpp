@@ -71,6 +71,7 @@ class GcnPlan {
     need(rng_, torch::kInt64, 2, "rng");
     build_tables();
     build_hops();
+    build_layer_draws();
     build_model();
   }
 
@@ -136,6 +137,7 @@ class GcnPlan {
   void step_until_head() {
     hipStream_t s = stream();
     for (int h = 0; h < L_; ++h) {  // hop 0's expand also draws the roots
+      if (hops_[h].lflag) ok(eh_gcn_layer_draw(&draws_[h], s), "gcn_layer_draw");
       ok(eh_gcn_expand(&hops_[h], s), "gcn_expand");
       ok(eh_gcn_mark(&hops_[h], s), "gcn_mark");
       ok(eh_gcn_place(&hops_[h], s), "gcn_place");
@@ -201,7 +203,7 @@ class GcnPlan {
     }
     return o;
   }
-  int64_t launches() const { return 1 + 3 * L_ + (L_ == 2 ? 2 : 0) + 1; }
+  int64_t launches() const { return 1 + 3 * L_ + (L_ == 2 ? 2 : 0) + 1 + ndraws_; }
 
  private:
   py::dict d_;
@@ -217,6 +219,10 @@ class GcnPlan {
   torch::Tensor h1_, agg1_, feat_, part_w_, part_fc_, part_bfc_, part_out_, part_stat_, part_w0_;
   std::vector<torch::Tensor> imgs_;
   GcnHop hops_[kGcnMaxHops]{};
+  GcnLayerDraw draws_[kGcnMaxHops]{};
+  int ndraws_ = 0;
+  torch::Tensor lflag_;
+  std::vector<torch::Tensor> draw_refs_;
   GcnLayerArgs layer_{};
   GcnHeadArgs head_{};
   GcnDwArgs dw_{};
@@ -333,6 +339,43 @@ class GcnPlan {
     }
     // hop h + 1's targets are the cumulative set: its capacity bounds theirs
     for (int h = 1; h < L_; ++h) TORCH_CHECK(cap_t_[h] >= cap_n_[h - 1], "GcnPlan: target capacity");
+  }
+
+  // FastGCN: "layer_draws" = one entry per hop, None (the full neighbourhood) or a dict
+  // {prob, alias, root_rows (optional), count, stream}: the hop keeps the edges into that
+  // step's layer (GcnLayerDraw); the layer flags are epoch-stamped, never cleared
+  void build_layer_draws() {
+    if (!has("layer_draws")) return;
+    py::list ld = d_["layer_draws"];
+    TORCH_CHECK(static_cast<int>(ld.size()) == L_, "GcnPlan: one layer_draws entry per hop");
+    for (int h = 0; h < L_; ++h) {
+      if (ld[h].is_none()) continue;
+      py::dict q = ld[h].cast<py::dict>();
+      if (!lflag_.defined()) lflag_ = full(N_, -1, torch::kInt32);
+      torch::Tensor prob = q["prob"].cast<torch::Tensor>(), alias = q["alias"].cast<torch::Tensor>();
+      need(prob, torch::kFloat32, -1, "layer prob");
+      need(alias, torch::kInt32, prob.numel(), "layer alias");
+      GcnLayerDraw& w = draws_[h];
+      w.prob = prob.data_ptr<float>();
+      w.alias = alias.data_ptr<int32_t>();
+      w.root_rows = nullptr;
+      if (q.contains("root_rows") && !q["root_rows"].is_none()) {
+        torch::Tensor rr = q["root_rows"].cast<torch::Tensor>();
+        need(rr, torch::kInt32, prob.numel(), "layer root_rows");
+        w.root_rows = rr.data_ptr<int32_t>();
+        draw_refs_.push_back(rr);
+      }
+      w.pop = prob.numel();
+      w.rng = rng_.data_ptr<int64_t>();
+      w.stream = q["stream"].cast<uint64_t>();
+      w.count = q["count"].cast<int64_t>();
+      TORCH_CHECK(w.count >= 1 && w.pop >= 1, "GcnPlan: a layer draw needs a positive count and population");
+      w.lflag = lflag_.data_ptr<int32_t>();
+      w.stamp = stamp_.data_ptr<int32_t>();
+      draw_refs_.insert(draw_refs_.end(), {prob, alias});
+      hops_[h].lflag = lflag_.data_ptr<int32_t>();
+      ++ndraws_;
+    }
   }
 
   GcnLin lin(const char* wname, int64_t out, int64_t in) {

@@ -175,6 +175,20 @@ __device__ void gcn_stage_blocks(const GcnHop& a, int sb, int nsb) {
   }
 }
 
+// FastGCN: stamp this step's layer (GcnLayerDraw); a row drawn twice is stamped twice
+__global__ __launch_bounds__(256) void gcn_layer_draw_kernel(GcnLayerDraw a) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= a.count) return;
+  const uint4_t r = Philox::gen(static_cast<uint64_t>(a.rng[0]), (static_cast<uint64_t>(a.rng[1]) << 8) ^ a.stream,
+                                static_cast<uint64_t>(i));
+  const uint64_t x = (static_cast<uint64_t>(r[0]) << 32) | r[1];
+  int64_t k = static_cast<int64_t>(__umul64hi(x, static_cast<uint64_t>(a.pop)));
+  if (k >= a.pop) k = a.pop - 1;
+  const int64_t pick = (u01(r[2]) < a.prob[k]) ? k : static_cast<int64_t>(a.alias[k]);
+  const int32_t row = a.root_rows ? a.root_rows[pick] : static_cast<int32_t>(pick);
+  if (row >= 0) a.lflag[row] = a.stamp[0];
+}
+
 __global__ __launch_bounds__(256) void gcn_expand_kernel(GcnHop a) {
   const int TE = gcn_expand_tile(a.cap_t);
   const int nexp = static_cast<int>(ceil_div(a.cap_t, TE));
@@ -219,12 +233,29 @@ __global__ __launch_bounds__(256) void gcn_expand_kernel(GcnHop a) {
     else row = -1;
   }
   if (!contig) start = -1;  // per-type walk (masked_nbr) for this target
+  const int raw = deg;
+  if (a.lflag && row >= 0) {  // FastGCN layer: only the neighbours in this step's layer
+    int kept = 0;
+    for (int k0 = 0; k0 < raw; k0 += 8) {
+      int32_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + u;
+        v[u] = k < raw ? (start >= 0 ? a.g.nbr[start + k] : masked_nbr(a.g, row, a.mask, k)) : -1;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) kept += (v[u] >= 0 && a.lflag[v[u]] == stamp) ? 1 : 0;
+    }
+    deg = kept;
+  }
   int total = 0;
   const int incl = block_scan_incl(deg, lds4, &total);
+  __shared__ int s_raw[kGcnExpandT];
   if (tid < TE) {
     s_incl[tid] = incl;
     s_row[tid] = row;
     s_start[tid] = start;
+    s_raw[tid] = raw;
   }
   if (tid < 64) {
     const int64_t p = lb_prefix(a.scan_deg, blockIdx.x, total, static_cast<uint32_t>(stamp) * 8u + 2u * a.h, a.err);
@@ -251,6 +282,37 @@ __global__ __launch_bounds__(256) void gcn_expand_kernel(GcnHop a) {
   }
   // hop 0: the roots are occurrences 0..B-1 (S_1 begins with the distinct roots)
   if (a.h == 0 && row >= 0) atomicMin(reinterpret_cast<unsigned long long*>(&a.first[row]), gcn_key(stamp, 0, t));
+  if (a.lflag) {
+    // filtered: one wave per target walks its neighbour list 64 at a time; the kept ones
+    // (ballot + prefix popcount) take consecutive edge slots in neighbour order
+    const int lane = tid & 63, wave = tid >> 6;
+    const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    for (int tl = wave; tl < TE; tl += 4) {
+      const int32_t r = s_row[tl];
+      if (r < 0) continue;
+      const int n = s_raw[tl];
+      const int64_t st = s_start[tl];
+      int64_t e_at = prefix + (tl > 0 ? s_incl[tl - 1] : 0);
+      for (int c0 = 0; c0 < n; c0 += 64) {
+        const int k = c0 + lane;
+        const int32_t v = k < n ? (st >= 0 ? a.g.nbr[st + k] : masked_nbr(a.g, r, a.mask, k)) : -1;
+        const bool keep = v >= 0 && a.lflag[v] == stamp;
+        const uint64_t bal = __ballot(keep);
+        if (keep) {
+          const int64_t e = e_at + __popcll(bal & below);
+          if (e < a.cap_e) {
+            const int32_t tg = a.tag[v];
+            const int32_t old = atomicAdd(&a.cntw[v], 1);
+            a.enode[e] = v;
+            a.etgt[e] = static_cast<int32_t>(tb + tl);
+            a.eflag[e] = static_cast<uint8_t>(old == 0 ? (tg != stamp ? 3 : 1) : 0);
+          }
+        }
+        e_at += __popcll(bal);
+      }
+    }
+    return;
+  }
   // the block's edges [prefix, prefix + total): target by a binary search of the block's
   // inclusive offsets; 8 edges per thread per pass, loads and counter atomics of a pass
   // issued together
@@ -1101,6 +1163,14 @@ static bool gcn_hop_ok(const GcnHop* a) {
          (a->h > 0 || (a->prob && a->alias && a->rng && a->pop > 0)) &&
          a->g.num_types <= 32 && (a->h > 0 || (a->roots && a->rself && a->B > 0 && a->B <= a->cap_t)) &&
          a->cap_e + a->B < (1ll << 31) && a->cap_n < (1ll << 31);
+}
+
+hipError_t eh_gcn_layer_draw(const GcnLayerDraw* a, hipStream_t s) {
+  if (!a || !a->prob || !a->alias || a->pop < 1 || !a->rng || a->count < 1 || !a->lflag || !a->stamp)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gcn_layer_draw_kernel, dim3(static_cast<uint32_t>(ceil_div(a->count, 256))), dim3(256), 0, s,
+                     *a);
+  return hipGetLastError();
 }
 
 hipError_t eh_gcn_expand(const GcnHop* a, hipStream_t s) {

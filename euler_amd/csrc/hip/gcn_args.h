@@ -105,6 +105,25 @@ struct GcnHop {
   int32_t* err;            // [1] |= 2 when a look-back wait timed out
   GcnStageW st[kGcnMaxStage];  // hop 0: weight images staged by extra blocks of expand
   int32_t nst;
+  // FastGCN layer filter (nullptr: the full neighbourhood): an edge is kept iff its
+  // neighbour's lflag entry holds this step's epoch (gcn_layer_draw stamps the layer)
+  const int32_t* lflag;
+};
+
+// FastGCN's per-hop layer: count rows drawn from a node-type sampler's alias table on
+// Philox (rng[0], rng[1] << 8 ^ stream, i) — sample_node(count, stream) of the generic
+// DeviceLayerFlow — and stamped with the step's epoch in lflag (reference
+// tf_euler/python/dataflow/fast_dataflow.py:25-57)
+struct GcnLayerDraw {
+  const float* prob;
+  const int32_t* alias;
+  const int32_t* root_rows;  // nullable
+  int64_t pop;
+  const int64_t* rng;
+  uint64_t stream;
+  int64_t count;
+  int32_t* lflag;
+  const int32_t* stamp;
 };
 
 // one conv layer's weights (fp32 masters, unpadded [out][in])
@@ -222,6 +241,7 @@ struct GcnReduceArgs {
 
 extern "C" {
 hipError_t eh_gcn_expand(const euler_hip::GcnHop* a, hipStream_t s);
+hipError_t eh_gcn_layer_draw(const euler_hip::GcnLayerDraw* a, hipStream_t s);
 hipError_t eh_gcn_mark(const euler_hip::GcnHop* a, hipStream_t s);
 hipError_t eh_gcn_place(const euler_hip::GcnHop* a, hipStream_t s);
 int64_t eh_gcn_expand_blocks(int64_t cap_t);

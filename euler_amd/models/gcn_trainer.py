@@ -33,6 +33,12 @@ previous one followed by its new neighbours in claim order), so their losses agr
 rounding;
 ``tests/test_gcn_trainer.py`` checks that and an fp32 oracle.
 
+FastGCN (``examples/fastgcn``: the same convs over ``fast_dataflow.py:25-57``) takes the same
+launches plus one per sampled hop: ``gcn_layer_draw`` stamps the step's layer (the generic
+``DeviceLayerFlow``'s ``sample_node`` draw) and that hop's expand keeps only the edges into
+it (per target: the kept count for the offsets, then one wave per target compacts its
+neighbour list with a ballot).
+
 Capacities: the flow's edge / node-set caps come from ``dataflow/device_flow.py``
 (``"bounded"`` by default through the estimator); a batch beyond them sets the overflow
 word, and the estimator rolls the chunk back, grows the caps and re-plans.
@@ -88,12 +94,13 @@ class GcnFlowCaps:
 
 
 def _gcn_shape(model):
-    """(convs, D, widths, E, C) of a SupervisedGCN-shaped model, or None"""
+    """the GCNConvs of a SupervisedGCN-shaped model (the full-neighbourhood flow, or
+    FastGCN's layer-sampled one), or None"""
     from euler_amd.convolution.convs import GCNConv
-    from euler_amd.dataflow.dataflows import GCNDataFlow
+    from euler_amd.dataflow.dataflows import FastGCNDataFlow, GCNDataFlow
 
     gnn = getattr(model, "gnn", None)
-    if gnn is None or not isinstance(getattr(gnn, "sampler", None), GCNDataFlow):
+    if gnn is None or not isinstance(getattr(gnn, "sampler", None), (GCNDataFlow, FastGCNDataFlow)):
         return None
     convs = list(getattr(gnn, "convs", []))
     if not 1 <= len(convs) <= 2 or not all(type(c) is GCNConv for c in convs):
@@ -114,7 +121,8 @@ def _gcn_shape(model):
 class GcnTrainer(CapturedTrainer):
     metric_name = "f1"
 
-    def __init__(self, model, graph, batch_size, masks, caps="bounded", optimizer="adam", learning_rate=0.01):
+    def __init__(self, model, graph, batch_size, masks, caps="bounded", optimizer="adam", learning_rate=0.01,
+                 layer_draws=None):
         if graph.device.type != "cuda":
             raise ValueError("the fused GCN step runs on the GPU (the generic FullFlowTrainer covers the CPU)")
         self.gnn = model.gnn
@@ -133,6 +141,8 @@ class GcnTrainer(CapturedTrainer):
         self.labels = graph.labels.to(graph.device).float().contiguous()
         self.flow = GcnFlowCaps(graph, masks, self.B, caps)
         self.masks = list(masks)
+        # FastGCN: per hop None or the layer draw {prob, alias, root_rows, count, stream}
+        self.layer_draws = list(layer_draws) if layer_draws is not None else None
         self.counts = torch.zeros(3, dtype=torch.int64, device=graph.device)
         self._stamp = torch.zeros(1, dtype=torch.int32, device=graph.device)
         super().__init__(model, graph, graph.device, optimizer, learning_rate)
@@ -163,14 +173,36 @@ class GcnTrainer(CapturedTrainer):
 
     @classmethod
     def from_model(cls, model, graph, batch_size, optimizer="adam", learning_rate=0.01, caps="bounded"):
-        import euler_amd.ops.graph_api as ge
+        import copy
 
+        import euler_amd.ops.graph_api as ge
+        from euler_amd.dataflow.dataflows import FastGCNDataFlow
+
+        flow = model.gnn.sampler
         ets = []
-        for m in model.gnn.sampler.metapath:
+        for m in flow.metapath:
             ids = None if m is None else [int(t) for t in np.asarray(ge.get_edge_type_id(m)).reshape(-1)]
             ets.append(None if ids is None or any(t < 0 for t in ids) else ids)
+        draws = None
+        if isinstance(flow, FastGCNDataFlow):
+            # every hop but the last keeps the edges into a layer of sum(fanouts[:h + 1])
+            # rows drawn by sample_node(.., metapath[h][0]) on Philox stream 20 + h: the
+            # generic DeviceLayerFlow's "fast" hops (models/full_trainer.py)
+            _, _, nw = ge.get_engine().export_nodes()
+            draws, total = [], 0
+            for h, m in enumerate(flow.metapath):
+                total += int(flow.fanouts[h])
+                if h == len(flow.metapath) - 1:
+                    draws.append(None)
+                    continue
+                nt = m[0] if isinstance(m, (list, tuple)) else m
+                tid = int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
+                smp = copy.copy(graph)
+                smp.set_root_type(tid if tid >= 0 else -1, node_weights=np.asarray(nw))
+                draws.append({"prob": smp.node_prob, "alias": smp.node_alias, "root_rows": smp.root_rows,
+                              "count": total, "stream": 20 + h})
         return cls(model, graph, batch_size, [graph._mask(e) for e in ets], caps=caps, optimizer=optimizer,
-                   learning_rate=learning_rate)
+                   learning_rate=learning_rate, layer_draws=draws)
 
     def _build_plan(self):
         m = self.model
@@ -191,7 +223,7 @@ class GcnTrainer(CapturedTrainer):
              "wfc": self.gnn.fc.weight.detach(), "g_wfc": self.gnn.fc.weight.grad,
              "bfc": self.gnn.fc.bias.detach(), "g_bfc": self.gnn.fc.bias.grad,
              "wout": m.out_fc.weight.detach(), "g_wout": m.out_fc.weight.grad,
-             "loss_out": self.loss_out, "counts": self.counts}
+             "loss_out": self.loss_out, "counts": self.counts, "layer_draws": self.layer_draws}
         if L == 2:
             d.update({"H1": int(w[1].shape[0]), "w1": w[1].detach(), "g_w1": w[1].grad})
         self.plan = hip().GcnPlan(d)

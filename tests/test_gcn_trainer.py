@@ -43,6 +43,72 @@ def _materialize(m, g, B):
     FullFlowTrainer.from_model(m, g, B, caps="exact")
 
 
+def _setup_fast(device, batch=64, hidden=32):
+    from euler_amd.tools import runner
+
+    a = runner.parse_args(["--dataset", "ppi", "--scale", "0.05", "--batch_size", str(batch), "--device", device,
+                           "--seed", "1", "--hidden_dim", str(hidden)], model="fastgcn")
+    torch.manual_seed(0)
+    m, _ = runner.build(a)
+    return m
+
+
+def test_fused_gcn_predicate_takes_fastgcn_not_adaptivegcn_cpu():
+    from euler_amd.models.gcn_trainer import _gcn_shape
+    from euler_amd.tools import runner
+
+    assert _gcn_shape(_setup_fast("cpu")) is not None
+    a = runner.parse_args(["--dataset", "ppi", "--scale", "0.05", "--device", "cpu"], model="adaptivegcn")
+    m, _ = runner.build(a)
+    assert _gcn_shape(m) is None  # layer-wise (sampleLNB) flow: the generic path
+
+
+@pytest.mark.gpu
+def test_fused_fastgcn_step_matches_generic_fp32():
+    """FastGCN through the fused step: the layer drawn by gcn_layer_draw and the filtered
+    expand give the generic DeviceLayerFlow's node sets from the same roots and RNG state,
+    the loss to bf16 rounding and the gradients within the GCN bounds"""
+    import torch.nn.functional as F
+
+    from euler_amd.models.full_trainer import FullFlowTrainer
+    from euler_amd.models.gcn_trainer import GcnTrainer
+
+    B = 64
+    m = _setup_fast("cuda", B).to("cuda")
+    g = _graph(m, "cuda")
+    _materialize(m, g, B)
+    assert GcnTrainer.supports(m, g)
+    tr = GcnTrainer.from_model(m, g, B, caps="exact")
+    L = len(m.gnn.convs)
+    assert tr.launches_per_step == 3 * L + (2 if L == 2 else 0) + 2 + (L - 1)
+    c0 = int(g.rng[1].item())
+    loss_k = float(tr.forward_backward_only())
+    torch.cuda.synchronize()
+    assert int(tr.flow.overflow.item()) == 0
+    grads_k = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+    fl = tr.plan.flow()
+    roots = fl["roots"].long().clone()
+    cnt = fl["cnt"].cpu().tolist()
+    set_ids = fl["set"][: cnt[L]].long().cpu()
+    ref = FullFlowTrainer.from_model(m, g, B, caps="exact")
+    for p in m.parameters():
+        p.grad = None
+    g.rng[1] = c0  # the fused step drew its layer at the step's counter (the reduce advanced it)
+    logits, df = ref._forward(roots)
+    loss = F.binary_cross_entropy_with_logits(logits, g.labels[roots].float())
+    loss.backward()
+    full = sum(int(x) for x in fl["hops"][0]["off"][-1:].tolist())
+    for h in range(L):
+        nd = df.blocks[h].n_id.cpu()
+        assert set(set_ids[: cnt[h + 1]].tolist()) == set(nd[nd >= 0].tolist()), h
+    assert full > 0
+    assert abs(loss_k - float(loss)) <= 2e-3 * abs(float(loss)), (loss_k, float(loss))
+    for n, p in m.named_parameters():
+        r = p.grad.detach()
+        err = float((grads_k[n] - r).norm() / max(float(r.norm()), 1e-12))
+        assert err < (5e-2 if "conv" in n else 1e-2), (n, err)
+
+
 def test_fused_gcn_predicate_cpu():
     from euler_amd.models.gcn_trainer import _gcn_shape
 
