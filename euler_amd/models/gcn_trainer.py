@@ -191,10 +191,10 @@ class GcnTrainer(CapturedTrainer):
             _, _, nw = ge.get_engine().export_nodes()
             draws, total = [], 0
             for h, m in enumerate(flow.metapath):
-                total += int(flow.fanouts[h])
-                if h == len(flow.metapath) - 1:
+                if h == len(flow.metapath) - 1:  # the last hop: the full neighbourhood
                     draws.append(None)
                     continue
+                total += int(flow.fanouts[h])
                 nt = m[0] if isinstance(m, (list, tuple)) else m
                 tid = int(np.asarray(ge.get_node_type_id(nt)).reshape(-1)[0])
                 smp = copy.copy(graph)
