@@ -58,20 +58,35 @@ def test_cpu_routes_to_generic_trainer(tmp_path):
     assert type(tr) is GraphTrainer and not isinstance(tr, GraphClsTrainer)
 
 
+def _train_eps(est):
+    """GIN with a trainable eps per conv (reference gin_conv.py train_eps=True)"""
+    for conv in est.model.gnn.convs:
+        del conv._buffers["eps"]
+        conv.eps = torch.nn.Parameter(torch.tensor([0.25]))
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("model,zst", [("gin", True), ("graphgcn", True), ("gin", False), ("graphgcn", False)])
+@pytest.mark.parametrize("model,zst", [("gin", True), ("graphgcn", True), ("gin", False), ("graphgcn", False),
+                                       ("gin_eps", True)])
 def test_fused_step_matches_cpu_autograd(tmp_path, cuda, model, zst, monkeypatch):
     """both kernel variants: every conv's aggregate kept in LDS for the backward (default)
-    and recomputed there (the fallback when they do not fit, forced by a small LDS budget)"""
+    and recomputed there (the fallback when they do not fit, forced by a small LDS budget);
+    GIN with trainable eps (d eps = sum dZ . x)"""
     from euler_amd.models.graph_cls_trainer import GraphClsTrainer
 
     if not zst:
         monkeypatch.setenv("EULER_AMD_GRAPH_MAX_LDS", "1")
+    eps = model == "gin_eps"
+    model = "gin" if eps else model
     _, est = _est(tmp_path, model, "cuda")
+    if eps:
+        _train_eps(est)
     tr = _trainer(est)
     assert isinstance(tr, GraphClsTrainer) and tr.launches_per_step == 2
     assert tr.plan.z_kept == zst
     _, est_c = _est(tmp_path, model, "cpu")
+    if eps:
+        _train_eps(est_c)
     trc = _trainer(est_c)
     assert len(trc.flat.params) == len(tr.flat.params)
     with torch.no_grad():  # the same weights (random, not the init: every path non-trivial)
