@@ -49,6 +49,12 @@ class GcnPlan {
     TORCH_CHECK(types >= 1 && types <= 32 && (indptr.numel() - 1) % types == 0, "GcnPlan: indptr must be [N*T+1]");
     g_.indptr = indptr.data_ptr<int64_t>();
     g_.nbr = nbr.data_ptr<int32_t>();
+    g_.cumw = nullptr;
+    if (has("cumw")) {  // the layer-wise (AdaptiveGCN) draw's weighted neighbour picks
+      torch::Tensor cw = T("cumw");
+      need(cw, torch::kFloat32, nbr.numel(), "cumw");
+      g_.cumw = cw.data_ptr<float>();
+    }
     g_.num_types = static_cast<int32_t>(types);
     g_.num_rows = (indptr.numel() - 1) / types;
     N_ = g_.num_rows;
@@ -352,6 +358,36 @@ class GcnPlan {
       if (ld[h].is_none()) continue;
       py::dict q = ld[h].cast<py::dict>();
       if (!lflag_.defined()) lflag_ = full(N_, -1, torch::kInt32);
+      const std::string kind = q.contains("kind") ? q["kind"].cast<std::string>() : std::string("fast");
+      if (kind == "layer") {
+        // AdaptiveGCN: the layer depends on the hop's set; only hop 0 (the roots) is sampled
+        // in the fused step (L <= 2), and its draw launch draws the roots too
+        TORCH_CHECK(h == 0, "GcnPlan: a layer-wise draw only on hop 0");
+        TORCH_CHECK(g_.cumw != nullptr, "GcnPlan: a layer-wise draw needs cumw");
+        TORCH_CHECK(B_ <= kGcnLayerMaxRoots, "GcnPlan: a layer-wise draw takes at most ", kGcnLayerMaxRoots,
+                    " roots");
+        GcnLayerDraw& w = draws_[h];
+        w.kind = 1;
+        w.prob = prob_.data_ptr<float>();
+        w.alias = alias_.data_ptr<int32_t>();
+        w.root_rows = root_rows_.defined() ? root_rows_.data_ptr<int32_t>() : nullptr;
+        w.pop = prob_.numel();
+        w.rng = rng_.data_ptr<int64_t>();
+        w.stream = q["stream"].cast<uint64_t>();
+        w.stream_u = q["stream_u"].cast<uint64_t>();
+        w.count = q["count"].cast<int64_t>();
+        TORCH_CHECK(w.count >= 1, "GcnPlan: a layer draw needs a positive count");
+        w.lflag = lflag_.data_ptr<int32_t>();
+        w.stamp = stamp_.data_ptr<int32_t>();
+        w.g = g_;
+        w.mask = static_cast<uint32_t>(masks_[h]);
+        w.B = static_cast<int32_t>(B_);
+        w.roots = roots_.data_ptr<int32_t>();
+        hops_[h].lflag = lflag_.data_ptr<int32_t>();
+        hops_[h].roots_given = 1;
+        ++ndraws_;
+        continue;
+      }
       torch::Tensor prob = q["prob"].cast<torch::Tensor>(), alias = q["alias"].cast<torch::Tensor>();
       need(prob, torch::kFloat32, -1, "layer prob");
       need(alias, torch::kInt32, prob.numel(), "layer alias");

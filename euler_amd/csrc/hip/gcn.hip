@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include "hip/gcn_args.h"
+#include "hip/sampling_math.h"
 #include "hip/optim_math.h"
 #include "hip/tile.h"
 
@@ -175,8 +176,98 @@ __device__ void gcn_stage_blocks(const GcnHop& a, int sb, int nsb) {
   }
 }
 
-// FastGCN: stamp this step's layer (GcnLayerDraw); a row drawn twice is stamped twice
+// alias draw of sampling.hip alias_sample_kernel (Philox (rng0, rng1 << 8 ^ stream, i))
+__device__ __forceinline__ int32_t gcn_alias_draw(const float* prob, const int32_t* alias, const int32_t* rows,
+                                                  int64_t pop, const int64_t* rng, uint64_t stream, int64_t i) {
+  const uint4_t r = Philox::gen(static_cast<uint64_t>(rng[0]), (static_cast<uint64_t>(rng[1]) << 8) ^ stream,
+                                static_cast<uint64_t>(i));
+  const uint64_t x = (static_cast<uint64_t>(r[0]) << 32) | r[1];
+  int64_t k = static_cast<int64_t>(__umul64hi(x, static_cast<uint64_t>(pop)));
+  if (k >= pop) k = pop - 1;
+  const int64_t pick = (u01(r[2]) < prob[k]) ? k : static_cast<int64_t>(alias[k]);
+  return rows ? rows[pick] : static_cast<int32_t>(pick);
+}
+
+// AdaptiveGCN's layer (GcnLayerDraw kind 1): one block
+__device__ void gcn_layerwise_draw(const GcnLayerDraw& a) {
+  __shared__ double cum[kGcnLayerMaxRoots];
+  __shared__ double s_tot[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int B = a.B;
+  const int per = (B + 255) / 256;  // consecutive roots per thread (scan order = root order)
+  double run = 0.0;
+  for (int j = 0; j < per; ++j) {
+    const int i = tid * per + j;
+    if (i >= B) break;
+    const int32_t row = gcn_alias_draw(a.prob, a.alias, a.root_rows, a.pop, a.rng, 1ull, i);
+    a.roots[i] = row;
+    // out-weight under the mask: the types' segment totals in type order (float, as the
+    // generic _out_weight)
+    float w = 0.f;
+    if (row >= 0 && row < a.g.num_rows) {
+      const int64_t base = static_cast<int64_t>(row) * a.g.num_types;
+      for (int t = 0; t < a.g.num_types; ++t) {
+        if (!((a.mask >> t) & 1u)) continue;
+        const int64_t lo = a.g.indptr[base + t], hi = a.g.indptr[base + t + 1];
+        w = w + (hi > lo ? a.g.cumw[hi - 1] : 0.f);
+      }
+    }
+    run += static_cast<double>(w);
+    cum[i] = run;  // thread-local inclusive prefix, offset below
+  }
+  // exclusive offsets of the threads' runs (doubles of float weights: exact sums)
+  double incl = run;
+  for (int o = 1; o < 64; o <<= 1) {
+    const double v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) s_tot[wave] = incl;
+  __syncthreads();
+  double woff = 0.0;
+  for (int w2 = 0; w2 < wave; ++w2) woff += s_tot[w2];
+  const double off = woff + incl - run;
+  for (int j = 0; j < per; ++j) {
+    const int i = tid * per + j;
+    if (i < B) cum[i] += off;
+  }
+  __syncthreads();
+  const double total = cum[B - 1];
+  for (int64_t m = tid; m < a.count; m += 256) {
+    int32_t root = -1;
+    if (total > 0.0) {
+      // the generic _uniform: two 16-bit draws of a flat 65536-entry alias table
+      const uint4_t rh = Philox::gen(static_cast<uint64_t>(a.rng[0]),
+                                     (static_cast<uint64_t>(a.rng[1]) << 8) ^ a.stream_u, static_cast<uint64_t>(m));
+      const uint4_t rl = Philox::gen(static_cast<uint64_t>(a.rng[0]),
+                                     (static_cast<uint64_t>(a.rng[1]) << 8) ^ (a.stream_u + 100), static_cast<uint64_t>(m));
+      const uint64_t xh = (static_cast<uint64_t>(rh[0]) << 32) | rh[1];
+      const uint64_t xl = (static_cast<uint64_t>(rl[0]) << 32) | rl[1];
+      const double hi = static_cast<double>(__umul64hi(xh, 65536ull)), lo = static_cast<double>(__umul64hi(xl, 65536ull));
+      const double u = (hi * 65536.0 + lo + 0.5) / 4294967296.0 * total;
+      int a0 = 0, b0 = B;  // first index with cum > u (searchsorted right), clamped
+      while (a0 < b0) {
+        const int mid = (a0 + b0) >> 1;
+        if (cum[mid] > u) b0 = mid;
+        else a0 = mid + 1;
+      }
+      root = a.roots[a0 < B ? a0 : B - 1];
+    }
+    int32_t v = -1;
+    if (root >= 0 && root < a.g.num_rows) {
+      const uint4_t r = Philox::gen(static_cast<uint64_t>(a.rng[0]), (static_cast<uint64_t>(a.rng[1]) << 8) ^ a.stream,
+                                    static_cast<uint64_t>(m));
+      v = sample_one_neighbor(a.g.indptr, a.g.nbr, a.g.cumw, a.g.num_types, a.mask, root, r, -1, nullptr, nullptr);
+    }
+    if (v >= 0) a.lflag[v] = a.stamp[0];
+  }
+}
+
+// stamp this step's layer (GcnLayerDraw); a row drawn twice is stamped twice
 __global__ __launch_bounds__(256) void gcn_layer_draw_kernel(GcnLayerDraw a) {
+  if (a.kind == 1) {
+    gcn_layerwise_draw(a);
+    return;
+  }
   const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   if (i >= a.count) return;
   const uint4_t r = Philox::gen(static_cast<uint64_t>(a.rng[0]), (static_cast<uint64_t>(a.rng[1]) << 8) ^ a.stream,
@@ -217,7 +308,9 @@ __global__ __launch_bounds__(256) void gcn_expand_kernel(GcnHop a) {
   int64_t start = 0;
   bool contig = true;
   if (tid < TE && t < nt && t < a.cap_t) {
-    if (a.h == 0) {  // this block's roots: the alias draw of sampling.hip, stream 1
+    if (a.h == 0 && a.roots_given) {  // drawn by the layer-wise draw launch
+      row = a.roots[t];
+    } else if (a.h == 0) {  // this block's roots: the alias draw of sampling.hip, stream 1
       const uint4_t r = Philox::gen(static_cast<uint64_t>(a.rng[0]), (static_cast<uint64_t>(a.rng[1]) << 8) ^ 1ull,
                                     static_cast<uint64_t>(t));
       const uint64_t x = (static_cast<uint64_t>(r[0]) << 32) | r[1];
@@ -1168,8 +1261,10 @@ static bool gcn_hop_ok(const GcnHop* a) {
 hipError_t eh_gcn_layer_draw(const GcnLayerDraw* a, hipStream_t s) {
   if (!a || !a->prob || !a->alias || a->pop < 1 || !a->rng || a->count < 1 || !a->lflag || !a->stamp)
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(gcn_layer_draw_kernel, dim3(static_cast<uint32_t>(ceil_div(a->count, 256))), dim3(256), 0, s,
-                     *a);
+  if (a->kind == 1 && (a->B < 1 || a->B > kGcnLayerMaxRoots || !a->roots || !a->g.indptr || !a->g.nbr || !a->g.cumw))
+    return hipErrorInvalidValue;
+  const dim3 grid(a->kind == 1 ? 1u : static_cast<uint32_t>(ceil_div(a->count, 256)));
+  hipLaunchKernelGGL(gcn_layer_draw_kernel, grid, dim3(256), 0, s, *a);
   return hipGetLastError();
 }
 

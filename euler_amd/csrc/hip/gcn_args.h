@@ -62,6 +62,7 @@ struct GcnStageW {
 struct GcnGraph {
   const int64_t* indptr;  // [N*T + 1]
   const int32_t* nbr;     // [E]
+  const float* cumw;      // [E] per-(row, type) cumulative edge weights (layer-wise draws)
   int64_t num_rows;
   int32_t num_types;
 };
@@ -105,26 +106,40 @@ struct GcnHop {
   int32_t* err;            // [1] |= 2 when a look-back wait timed out
   GcnStageW st[kGcnMaxStage];  // hop 0: weight images staged by extra blocks of expand
   int32_t nst;
-  // FastGCN layer filter (nullptr: the full neighbourhood): an edge is kept iff its
-  // neighbour's lflag entry holds this step's epoch (gcn_layer_draw stamps the layer)
+  // FastGCN / AdaptiveGCN layer filter (nullptr: the full neighbourhood): an edge is kept
+  // iff its neighbour's lflag entry holds this step's epoch (gcn_layer_draw stamps the layer)
   const int32_t* lflag;
+  int32_t roots_given;     // hop 0: the roots were drawn by the layer-wise draw (read, not drawn)
 };
 
-// FastGCN's per-hop layer: count rows drawn from a node-type sampler's alias table on
-// Philox (rng[0], rng[1] << 8 ^ stream, i) — sample_node(count, stream) of the generic
-// DeviceLayerFlow — and stamped with the step's epoch in lflag (reference
-// tf_euler/python/dataflow/fast_dataflow.py:25-57)
+// The per-hop layer of the layer-sampled flows, stamped with the step's epoch in lflag:
+//   kind 0 (FastGCN, reference tf_euler/python/dataflow/fast_dataflow.py:25-57): count rows
+//     drawn from a node-type sampler's alias table on Philox (rng[0], rng[1] << 8 ^ stream,
+//     i) — sample_node(count, stream) of the generic DeviceLayerFlow;
+//   kind 1 (AdaptiveGCN, layerwise_dataflow.py:26-71, sampleLNB): one block draws the B
+//     roots (the root alias table, stream 1, written to roots: hop 0's expand reads them),
+//     their out-weights under the hop's mask, a double prefix sum, count picks of a root in
+//     proportion (uniforms from two 16-bit draws on streams 40 + h and 140 + h) and one
+//     weighted neighbour of each (stream 30 + h) — DeviceLayerFlow's "layer" hop.
 struct GcnLayerDraw {
-  const float* prob;
+  int32_t kind;
+  const float* prob;         // kind 0: the layer sampler; kind 1: the root sampler
   const int32_t* alias;
   const int32_t* root_rows;  // nullable
   int64_t pop;
   const int64_t* rng;
-  uint64_t stream;
+  uint64_t stream;           // kind 0: the draw; kind 1: the neighbour draw (30 + h)
   int64_t count;
   int32_t* lflag;
   const int32_t* stamp;
+  // kind 1
+  GcnGraph g;
+  uint32_t mask;
+  int32_t B;
+  int32_t* roots;
+  uint64_t stream_u;         // 40 + h (the second 16 bits on stream_u + 100)
 };
+constexpr int kGcnLayerMaxRoots = 4096;  // kind 1: the roots' prefix sums live in LDS
 
 // one conv layer's weights (fp32 masters, unpadded [out][in])
 struct GcnLin {

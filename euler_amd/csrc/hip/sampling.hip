@@ -10,6 +10,7 @@
 // weight sum, then binary-search the group's cumulative weights), with empty
 // rows padded by `default_row` (reference: sample_neighbor_op.cc:37-145).
 #include "hip/common.h"
+#include "hip/sampling_math.h"
 
 namespace euler_hip {
 
@@ -32,48 +33,7 @@ __global__ __launch_bounds__(256) void sample_neighbor_kernel(
     const uint4_t r = Philox::gen(static_cast<uint64_t>(rng[0]),
                                   (static_cast<uint64_t>(rng[1]) << 8) ^ stream_id,
                                   static_cast<uint64_t>(tid));
-    const int64_t base = row * num_types;
-    int64_t lo = 0, hi = 0;
-    float total = 0.f;
-    if (num_types == 1) {
-      lo = indptr[base];
-      hi = indptr[base + 1];
-      total = hi > lo ? cumw[hi - 1] : 0.f;
-      t_out = 0;
-    } else {
-      // pick an edge type group proportionally to its weight sum
-      float tot = 0.f;
-      for (int t = 0; t < num_types; ++t) {
-        if (!((type_mask >> t) & 1u)) continue;
-        const int64_t a = indptr[base + t], b = indptr[base + t + 1];
-        if (b > a) tot += cumw[b - 1];
-      }
-      if (tot > 0.f) {
-        float u = u01(r[0]) * tot;
-        for (int t = 0; t < num_types; ++t) {
-          if (!((type_mask >> t) & 1u)) continue;
-          const int64_t a = indptr[base + t], b = indptr[base + t + 1];
-          if (b <= a) continue;
-          const float g = cumw[b - 1];
-          lo = a; hi = b; total = g; t_out = t;
-          if (u < g) break;
-          u -= g;
-        }
-      }
-    }
-    if (hi > lo && total > 0.f) {
-      const float u = u01(r[1]) * total;
-      // first position with cumw > u
-      int64_t a = lo, b = hi - 1;
-      while (a < b) {
-        const int64_t m = (a + b) >> 1;
-        if (cumw[m] > u) b = m; else a = m + 1;
-      }
-      res = nbr[a];
-      w = cumw[a] - (a > lo ? cumw[a - 1] : 0.f);
-    } else {
-      t_out = -1;
-    }
+    res = sample_one_neighbor(indptr, nbr, cumw, num_types, type_mask, row, r, default_row, &w, &t_out);
   }
   out[tid] = res;
   if (out_w) out_w[tid] = w;

@@ -403,7 +403,9 @@ class DeviceLayerFlow(DeviceFullFlow):
         if self.kinds[h] == "fast":
             return self.samplers[h].sample_node(m, stream_id=20 + h).long()
         w = self._out_weight(n_id, self.masks[h])
-        cum = torch.cumsum(w, 0)
+        # double prefix sums of the float weights (exact for any association, so the fused
+        # GCN step's block scan picks the same roots: csrc/hip/gcn.hip gcn_layerwise_draw)
+        cum = torch.cumsum(w.double(), 0)
         total = cum[-1]
         u = self._uniform(m, 40 + h) * total
         pick = torch.searchsorted(cum, u.contiguous(), right=True).clamp(max=n_id.numel() - 1)
@@ -418,8 +420,8 @@ class DeviceLayerFlow(DeviceFullFlow):
         if use_hip(g.rng):
             hi = hip().alias_sample(self._uflat_p, self._uflat_a, None, int(n), g.rng, int(stream_id))
             lo = hip().alias_sample(self._uflat_p, self._uflat_a, None, int(n), g.rng, int(stream_id) + 100)
-            return (hi.double() * 65536.0 + lo.double() + 0.5).float() / float(1 << 32)
-        return torch.rand(int(n), generator=g._cpu_gen)
+            return (hi.double() * 65536.0 + lo.double() + 0.5) / float(1 << 32)
+        return torch.rand(int(n), generator=g._cpu_gen, dtype=torch.float64)
 
     def _filter(self, h, n_id, nbr):
         if h == self.L - 1:

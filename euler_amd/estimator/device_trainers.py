@@ -332,7 +332,7 @@ def _full(c: Ctx):
 
     g = _supervised_upload(c)
     caps = c.params.get("device_flow_caps", "bounded")
-    if c.params.get("gcn_fused", True) and GcnTrainer.supports(c.model, g):
+    if c.params.get("gcn_fused", True) and GcnTrainer.supports(c.model, g, c.batch):
         # SupervisedGCN-shaped: the fused hand-written step (models/gcn_trainer.py)
         return GcnTrainer.from_model(c.model, g, c.batch, caps=caps, **c.opt_kw())
     return FullFlowTrainer.from_model(c.model, g, c.batch, **c.opt_kw(), caps=caps)

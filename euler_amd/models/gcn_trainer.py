@@ -97,10 +97,10 @@ def _gcn_shape(model):
     """the GCNConvs of a SupervisedGCN-shaped model (the full-neighbourhood flow, or
     FastGCN's layer-sampled one), or None"""
     from euler_amd.convolution.convs import GCNConv
-    from euler_amd.dataflow.dataflows import FastGCNDataFlow, GCNDataFlow
+    from euler_amd.dataflow.dataflows import FastGCNDataFlow, GCNDataFlow, LayerwiseDataFlow
 
     gnn = getattr(model, "gnn", None)
-    if gnn is None or not isinstance(getattr(gnn, "sampler", None), (GCNDataFlow, FastGCNDataFlow)):
+    if gnn is None or not isinstance(getattr(gnn, "sampler", None), (GCNDataFlow, FastGCNDataFlow, LayerwiseDataFlow)):
         return None
     convs = list(getattr(gnn, "convs", []))
     if not 1 <= len(convs) <= 2 or not all(type(c) is GCNConv for c in convs):
@@ -152,7 +152,7 @@ class GcnTrainer(CapturedTrainer):
 
     # ------------------------------------------------------------------ construction
     @staticmethod
-    def supports(model, graph=None) -> bool:
+    def supports(model, graph=None, batch_size=None) -> bool:
         """SupervisedGCN-shaped: 1-2 bias-free GCNConvs on GCNDataFlow with self loops, fc with
         bias, out_fc without; conv widths <= 64, inputs <= 128, fc / label widths <= 128"""
         if os.environ.get("EULER_AMD_GCN_FUSED", "1") == "0":
@@ -169,6 +169,10 @@ class GcnTrainer(CapturedTrainer):
             return False  # lazy layers not materialised
         if graph is not None and (graph.labels is None or graph.features is None or graph.device.type != "cuda"):
             return False
+        from euler_amd.dataflow.dataflows import LayerwiseDataFlow
+
+        if isinstance(model.gnn.sampler, LayerwiseDataFlow) and batch_size is not None and int(batch_size) > 4096:
+            return False  # the layer-wise draw keeps the roots' prefix sums in one block's LDS
         return (max(widths) <= 64 and max(ins) <= 128 and _round_up(E, 32) <= 128 and _round_up(C, 32) <= 128)
 
     @classmethod
@@ -176,7 +180,7 @@ class GcnTrainer(CapturedTrainer):
         import copy
 
         import euler_amd.ops.graph_api as ge
-        from euler_amd.dataflow.dataflows import FastGCNDataFlow
+        from euler_amd.dataflow.dataflows import FastGCNDataFlow, LayerwiseDataFlow
 
         flow = model.gnn.sampler
         ets = []
@@ -201,6 +205,12 @@ class GcnTrainer(CapturedTrainer):
                 smp.set_root_type(tid if tid >= 0 else -1, node_weights=np.asarray(nw))
                 draws.append({"prob": smp.node_prob, "alias": smp.node_alias, "root_rows": smp.root_rows,
                               "count": total, "stream": 20 + h})
+        elif isinstance(flow, LayerwiseDataFlow) and len(flow.metapath) >= 2:
+            # AdaptiveGCN (sampleLNB): hop 0's layer = fanouts[0] roots picked in proportion
+            # to their out-weight, one weighted neighbour each (DeviceLayerFlow "layer"; the
+            # last hop is the full neighbourhood)
+            draws = [{"kind": "layer", "count": int(flow.fanouts[0]), "stream": 30, "stream_u": 40}] + \
+                [None] * (len(flow.metapath) - 1)
         return cls(model, graph, batch_size, [graph._mask(e) for e in ets], caps=caps, optimizer=optimizer,
                    learning_rate=learning_rate, layer_draws=draws)
 
@@ -216,6 +226,7 @@ class GcnTrainer(CapturedTrainer):
              "masks": [int(x) & 0xFFFFFFFF for x in self.masks],
              "cap_e": [e for e, _ in self.flow.caps], "cap_n": [n for _, n in self.flow.caps],
              "node_prob": g.node_prob, "node_alias": g.node_alias, "root_rows": g.root_rows, "rng": g.rng,
+             "cumw": g.cumw,
              "stamp": self._stamp, "overflow": self.flow.overflow,
              "features": self.features, "labels": self.labels, "D": self.D,
              "H0": int(w[0].shape[0]), "E": int(self.gnn.fc.weight.shape[0]), "C": int(m.out_fc.weight.shape[0]),

@@ -43,30 +43,29 @@ def _materialize(m, g, B):
     FullFlowTrainer.from_model(m, g, B, caps="exact")
 
 
-def _setup_fast(device, batch=64, hidden=32):
+def _setup_fast(device, batch=64, hidden=32, model="fastgcn"):
     from euler_amd.tools import runner
 
     a = runner.parse_args(["--dataset", "ppi", "--scale", "0.05", "--batch_size", str(batch), "--device", device,
-                           "--seed", "1", "--hidden_dim", str(hidden)], model="fastgcn")
+                           "--seed", "1", "--hidden_dim", str(hidden)], model=model)
     torch.manual_seed(0)
     m, _ = runner.build(a)
     return m
 
 
-def test_fused_gcn_predicate_takes_fastgcn_not_adaptivegcn_cpu():
+def test_fused_gcn_predicate_takes_layer_sampled_gcns_cpu():
     from euler_amd.models.gcn_trainer import _gcn_shape
-    from euler_amd.tools import runner
 
     assert _gcn_shape(_setup_fast("cpu")) is not None
-    a = runner.parse_args(["--dataset", "ppi", "--scale", "0.05", "--device", "cpu"], model="adaptivegcn")
-    m, _ = runner.build(a)
-    assert _gcn_shape(m) is None  # layer-wise (sampleLNB) flow: the generic path
+    assert _gcn_shape(_setup_fast("cpu", model="adaptivegcn")) is not None
 
 
 @pytest.mark.gpu
-def test_fused_fastgcn_step_matches_generic_fp32():
-    """FastGCN through the fused step: the layer drawn by gcn_layer_draw and the filtered
-    expand give the generic DeviceLayerFlow's node sets from the same roots and RNG state,
+@pytest.mark.parametrize("model", ["fastgcn", "adaptivegcn"])
+def test_fused_layer_sampled_gcn_step_matches_generic_fp32(model):
+    """FastGCN / AdaptiveGCN through the fused step: the layer drawn by gcn_layer_draw
+    (sample_node; or sampleLNB: roots by out-weight, one weighted neighbour each) and the
+    filtered expand give the generic DeviceLayerFlow's node sets from the same RNG state,
     the loss to bf16 rounding and the gradients within the GCN bounds"""
     import torch.nn.functional as F
 
@@ -74,7 +73,7 @@ def test_fused_fastgcn_step_matches_generic_fp32():
     from euler_amd.models.gcn_trainer import GcnTrainer
 
     B = 64
-    m = _setup_fast("cuda", B).to("cuda")
+    m = _setup_fast("cuda", B, model=model).to("cuda")
     g = _graph(m, "cuda")
     _materialize(m, g, B)
     assert GcnTrainer.supports(m, g)
