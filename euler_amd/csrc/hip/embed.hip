@@ -259,15 +259,21 @@ struct SgnsUpd {
   const int64_t* rows;  // unique id -> row of `table` (null = identity)
   const int64_t* step;
   int64_t n_u, P, n_rows, n_src, n_smap;
-  int K, D, lp, side, kind;
+  int K, D, lp, split, side, kind;
   float lr, b1, b2, eps;
   int src_bf16, gout_bf16;
 };
 
+// One row group of lp * split lanes per unique id: `split` sub-groups of lp lanes walk the
+// occurrence list with stride split and their partial gradients are summed with xor
+// shuffles at multiples of lp (lanes that exit early exit with all of their partners, since
+// the partners share the column slice).  split > 1 only when the ids alone cannot fill the
+// chip (eh_sgns_update), so small graphs with long occurrence lists shorten their chains.
 __global__ __launch_bounds__(256) void sgns_update_kernel(SgnsUpd a) {
-  const RowLane L = row_lane(a.lp, a.n_u);
-  if (!L.ok || L.sub * 4 >= a.D) return;  // no cross-lane exchange
-  const int d = L.sub * 4;
+  const RowLane L = row_lane(a.lp * a.split, a.n_u);
+  const int sub = L.sub & (a.lp - 1), part = L.sub / a.lp;
+  if (!L.ok || sub * 4 >= a.D) return;
+  const int d = sub * 4;
   // the table row, its slots and the occurrence range are loaded first, so their latency
   // overlaps the dependent index chain of the gradient below
   const bool apply = a.gout == nullptr;
@@ -275,7 +281,9 @@ __global__ __launch_bounds__(256) void sgns_update_kernel(SgnsUpd a) {
   float4_t p{}, mi{}, vi{};
   if (apply) {
     r = a.rows ? a.rows[L.row] : L.row;
-    if (r < 0 || r >= a.n_rows) return;
+    if (r < 0 || r >= a.n_rows) return;  // uniform over the row group
+  }
+  if (apply && part == 0) {
     const int64_t off = r * a.D + d;
     p = *reinterpret_cast<const float4_t*>(a.table + off);
     if (a.kind != 2) vi = *reinterpret_cast<const float4_t*>(a.v + off);
@@ -285,7 +293,7 @@ __global__ __launch_bounds__(256) void sgns_update_kernel(SgnsUpd a) {
   const int64_t beg = a.ptr[L.row], end = a.ptr[L.row + 1];
   const int KK = a.K + 1;
   constexpr int SG = 4;
-  for (int64_t i = beg; i < end; ++i) {
+  for (int64_t i = beg + part; i < end; i += a.split) {
     const int64_t o = a.list[i];
     if (a.side == 0) {
       // target occurrence o is pair o: all of its context rows, SG at a time
@@ -323,6 +331,11 @@ __global__ __launch_bounds__(256) void sgns_update_kernel(SgnsUpd a) {
       for (int k = 0; k < 4; ++k) g[k] += w * e[k];
     }
   }
+  for (int o = a.lp; o < a.lp * a.split; o <<= 1) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) g[k] += __shfl_xor(g[k], o, 64);
+  }
+  if (part != 0) return;
   if (!apply) {
     // rows without occurrences on this side are left untouched: two launches (target and
     // context side) can fill one buffer whose rows each belong to exactly one side
@@ -925,6 +938,10 @@ hipError_t eh_sgns_update(int side, int64_t n_u, const int64_t* ptr, const int* 
   a.K = K;
   a.D = D;
   a.lp = row_lanes(D / 4);
+  // widen the row groups (up to a wave) while n_u rows alone leave the chip under half full
+  constexpr int64_t kFillLanes = int64_t{1} << 18;
+  a.split = 1;
+  while (a.lp * a.split < 64 && n_u * a.lp * a.split * 2 <= kFillLanes) a.split <<= 1;
   a.side = side;
   a.kind = kind;
   a.lr = lr;
@@ -933,7 +950,7 @@ hipError_t eh_sgns_update(int side, int64_t n_u, const int64_t* ptr, const int* 
   a.eps = eps;
   a.src_bf16 = src_bf16;
   a.gout_bf16 = gout_bf16;
-  hipLaunchKernelGGL(sgns_update_kernel, row_grid(n_u, a.lp), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(sgns_update_kernel, row_grid(n_u, a.lp * a.split), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
