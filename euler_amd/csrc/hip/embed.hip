@@ -259,38 +259,50 @@ struct SgnsUpd {
   const int64_t* rows;  // unique id -> row of `table` (null = identity)
   const int64_t* step;
   int64_t n_u, P, n_rows, n_src, n_smap;
-  int K, D, lp, split, side, kind;
+  int K, D, lp, split, lsh, side, kind;  // lsh = log2(lp * split)
   float lr, b1, b2, eps;
   int src_bf16, gout_bf16;
 };
 
-// One row group of lp * split lanes per unique id: `split` sub-groups of lp lanes walk the
-// occurrence list with stride split and their partial gradients are summed with xor
-// shuffles at multiples of lp (lanes that exit early exit with all of their partners, since
-// the partners share the column slice).  split > 1 only when the ids alone cannot fill the
-// chip (eh_sgns_update), so small graphs with long occurrence lists shorten their chains.
+// One row group of lpe = lp * split lanes per unique id (lpe <= 256): `split` sub-groups of
+// lp lanes walk the occurrence list with stride split; partial gradients are summed with xor
+// shuffles at multiples of lp inside a wave and, for row groups wider than a wave, through
+// LDS in wave order.  Lanes outside the table width or the id range stay live (no work) up to
+// that exchange, so the barrier sees every wave.  split > 1 only when the ids alone cannot
+// fill the chip (eh_sgns_update): small graphs with long occurrence lists shorten their chains.
+// kWide (lpe > 64) is its own instantiation: the wave-sized one keeps early exits and no LDS.
+template <bool kWide>
 __global__ __launch_bounds__(256) void sgns_update_kernel(SgnsUpd a) {
-  const RowLane L = row_lane(a.lp * a.split, a.n_u);
-  const int sub = L.sub & (a.lp - 1), part = L.sub / a.lp;
-  if (!L.ok || sub * 4 >= a.D) return;
+  const int lpe = a.lp * a.split;
+  const int64_t gt = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t row = gt >> a.lsh;
+  const int lsub = static_cast<int>(gt) & (lpe - 1);
+  const int sub = lsub & (a.lp - 1), part = lsub / a.lp;
   const int d = sub * 4;
   // the table row, its slots and the occurrence range are loaded first, so their latency
   // overlaps the dependent index chain of the gradient below
   const bool apply = a.gout == nullptr;
+  bool live = row < a.n_u && d < a.D;
+  if constexpr (!kWide) {
+    if (!live) return;  // partners share the row and the column slice
+  }
   int64_t r = -1;
   float4_t p{}, mi{}, vi{};
-  if (apply) {
-    r = a.rows ? a.rows[L.row] : L.row;
-    if (r < 0 || r >= a.n_rows) return;  // uniform over the row group
+  if (live && apply) {
+    r = a.rows ? a.rows[row] : row;
+    live = r >= 0 && r < a.n_rows;  // uniform over the row group
+    if constexpr (!kWide) {
+      if (!live) return;
+    }
   }
-  if (apply && part == 0) {
+  if (live && apply && part == 0) {
     const int64_t off = r * a.D + d;
     p = *reinterpret_cast<const float4_t*>(a.table + off);
     if (a.kind != 2) vi = *reinterpret_cast<const float4_t*>(a.v + off);
     if (a.kind == 0) mi = *reinterpret_cast<const float4_t*>(a.m + off);
   }
   float g[4] = {0.f, 0.f, 0.f, 0.f};
-  const int64_t beg = a.ptr[L.row], end = a.ptr[L.row + 1];
+  const int64_t beg = live ? a.ptr[row] : 0, end = live ? a.ptr[row + 1] : 0;
   const int KK = a.K + 1;
   constexpr int SG = 4;
   for (int64_t i = beg + part; i < end; i += a.split) {
@@ -331,11 +343,24 @@ __global__ __launch_bounds__(256) void sgns_update_kernel(SgnsUpd a) {
       for (int k = 0; k < 4; ++k) g[k] += w * e[k];
     }
   }
-  for (int o = a.lp; o < a.lp * a.split; o <<= 1) {
+  for (int o = a.lp; o < lpe && o < 64; o <<= 1) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) g[k] += __shfl_xor(g[k], o, 64);
   }
-  if (part != 0) return;
+  if constexpr (kWide) {
+    // lpe is a multiple of 64: the row's waves are consecutive in the block
+    __shared__ float4_t red[4][64];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane < a.lp) red[w][lane] = float4_t{g[0], g[1], g[2], g[3]};
+    __syncthreads();
+    if (part != 0) return;
+    const int nw = lpe >> 6;
+    float4_t t = red[w][sub];
+    for (int j = 1; j < nw; ++j) t += red[w + j][sub];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) g[k] = t[k];
+  }
+  if (part != 0 || !live) return;
   if (!apply) {
     // rows without occurrences on this side are left untouched: two launches (target and
     // context side) can fill one buffer whose rows each belong to exactly one side
@@ -344,9 +369,9 @@ __global__ __launch_bounds__(256) void sgns_update_kernel(SgnsUpd a) {
         tl2u v;
         v[0] = pack_bf16x2(g[0], g[1]);
         v[1] = pack_bf16x2(g[2], g[3]);
-        *reinterpret_cast<tl2u*>(static_cast<bf16_t*>(a.gout) + L.row * a.D + d) = v;
+        *reinterpret_cast<tl2u*>(static_cast<bf16_t*>(a.gout) + row * a.D + d) = v;
       } else {
-        EV<float>::store(static_cast<float*>(a.gout) + L.row * a.D + d, g);
+        EV<float>::store(static_cast<float*>(a.gout) + row * a.D + d, g);
       }
     }
     return;
@@ -938,10 +963,13 @@ hipError_t eh_sgns_update(int side, int64_t n_u, const int64_t* ptr, const int* 
   a.K = K;
   a.D = D;
   a.lp = row_lanes(D / 4);
-  // widen the row groups (up to a wave) while n_u rows alone leave the chip under half full
-  constexpr int64_t kFillLanes = int64_t{1} << 18;
+  // widen the row groups (up to a block) while the widened groups still fit the chip's
+  // resident lanes (256 CUs x 2048)
+  constexpr int64_t kFillLanes = int64_t{1} << 19;
   a.split = 1;
-  while (a.lp * a.split < 64 && n_u * a.lp * a.split * 2 <= kFillLanes) a.split <<= 1;
+  while (a.lp * a.split < 256 && n_u * a.lp * a.split * 2 <= kFillLanes) a.split <<= 1;
+  a.lsh = 0;
+  while ((1 << a.lsh) < a.lp * a.split) ++a.lsh;
   a.side = side;
   a.kind = kind;
   a.lr = lr;
@@ -950,7 +978,12 @@ hipError_t eh_sgns_update(int side, int64_t n_u, const int64_t* ptr, const int* 
   a.eps = eps;
   a.src_bf16 = src_bf16;
   a.gout_bf16 = gout_bf16;
-  hipLaunchKernelGGL(sgns_update_kernel, row_grid(n_u, a.lp * a.split), dim3(256), 0, s, a);
+  const int64_t lanes = n_u * a.lp * a.split;
+  const dim3 grid(static_cast<uint32_t>((lanes + 255) / 256));
+  if (a.lp * a.split > 64)
+    hipLaunchKernelGGL(sgns_update_kernel<true>, grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(sgns_update_kernel<false>, grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -510,6 +510,32 @@ def test_sgns_idx_kernels_match_cpu(cuda, kind):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("D,n_t,n_c,P", [
+    (128, 40000, 60000, 20000),  # ids fill the chip: one lp-lane group per row (split 1)
+    (128, 5000, 5000, 8000),     # split 2 inside a wave
+    (32, 3000, 3000, 6000),      # 128-lane groups across two waves
+    (16, 100, 300, 6000),        # block-wide groups, long occurrence lists
+])
+def test_sgns_grad_split_regimes_match_cpu(cuda, D, n_t, n_c, P):
+    """sgns_update_kernel widens each row's lane group while the unique ids underfill the chip
+    (embed.hip eh_sgns_update); every regime reduces to the CPU reference gradients."""
+    K = 5
+    T, C, src, ctx = _sgns_case("cpu", P=P, K=K, D=D, n_t=n_t, n_c=n_c, seed=23)
+    gscale = 1.0 / (P * (1 + K))
+    u_t, inv_t = G.unique_first(src)
+    u_c, inv_c = G.unique_first(ctx)
+    coef, _ = G.sgns_fwd_idx(T, u_t, inv_t, C, u_c, inv_c, K, gscale)
+    ref_t = G.sgns_grad(0, *G.occ_csr(inv_t, u_t.numel()), coef, K, C, u_c, inv_c, inv_self=inv_t)
+    ref_c = G.sgns_grad(1, *G.occ_csr(inv_c, u_c.numel()), coef, K, T, u_t, inv_t, inv_self=inv_c)
+    Tg, Cg, coef_g = T.to(cuda), C.to(cuda), coef.to(cuda)
+    ug_t, ig_t, ug_c, ig_c = (x.to(cuda) for x in (u_t, inv_t, u_c, inv_c))
+    g_t = G.sgns_grad(0, *G.occ_csr(ig_t, ug_t.numel()), coef_g, K, Cg, ug_c, ig_c)
+    g_c = G.sgns_grad(1, *G.occ_csr(ig_c, ug_c.numel()), coef_g, K, Tg, ug_t, ig_t)
+    torch.testing.assert_close(g_t.cpu(), ref_t, atol=1e-7, rtol=1e-4)
+    torch.testing.assert_close(g_c.cpu(), ref_c, atol=1e-7, rtol=1e-4)
+
+
+@pytest.mark.gpu
 def test_sgns_idx_bf16_rows_match_fp32(cuda):
     """bf16 exchanged rows (sharded-table keep_wire path): the index-driven SGNS kernels
     read bf16 rows and write bf16 gradients, the converting gather packs fp32 rows as bf16
