@@ -397,16 +397,23 @@ std::vector<torch::Tensor> occ_csr(torch::Tensor inv, int64_t n_u) {
   typed(inv, torch::kInt64, "inv");
   TORCH_CHECK(inv.numel() < (int64_t{1} << 31), "occ_csr: too many occurrences");
   const c10::DeviceGuard g(inv.device());
+  TORCH_CHECK(n_u < (int64_t{1} << 31), "occ_csr: too many unique ids");
   auto iopt = inv.options();
-  auto ptr = torch::zeros({n_u + 1}, iopt);
-  if (inv.numel() > 0 && n_u > 0) {
-    // counts by index_add (bincount would read max(inv) back to the host: a sync that
-    // also breaks hipGraph capture); inv values must lie in [0, n_u)
-    auto cnt = torch::zeros({n_u}, iopt).index_add_(0, inv, torch::ones({inv.numel()}, iopt));
-    ptr.narrow(0, 1, n_u).copy_(torch::cumsum(cnt, 0));
-  }
-  auto cursor = torch::zeros({n_u}, iopt.dtype(torch::kInt32));
   auto list = torch::empty({inv.numel()}, iopt.dtype(torch::kInt32));
+  if (n_u <= 0) return {torch::zeros({1}, iopt), list};
+  // one zero fill for the counts and the fill cursors; counts by atomics (bincount would
+  // read max(inv) back to the host: a sync that also breaks hipGraph capture), then one
+  // device scan straight into ptr[1:]; inv values must lie in [0, n_u)
+  auto ptr = torch::empty({n_u + 1}, iopt);
+  auto cc = torch::zeros({2 * n_u}, iopt.dtype(torch::kInt32));
+  size_t bytes = 0;
+  ok(eh_occ_count_scan(nullptr, 0, n_u, cc.data_ptr<int32_t>(), ptr.data_ptr<int64_t>(), nullptr, &bytes, stream()),
+     "occ_count_scan(size)");
+  auto temp = torch::empty({static_cast<int64_t>(bytes) + 1}, iopt.dtype(torch::kUInt8));
+  ok(eh_occ_count_scan(inv.data_ptr<int64_t>(), inv.numel(), n_u, cc.data_ptr<int32_t>(), ptr.data_ptr<int64_t>(),
+                       temp.data_ptr(), &bytes, stream()),
+     "occ_count_scan");
+  auto cursor = cc.narrow(0, n_u, n_u);
   ok(eh_occ_fill(inv.data_ptr<int64_t>(), inv.numel(), ptr.data_ptr<int64_t>(), cursor.data_ptr<int32_t>(),
                  list.data_ptr<int32_t>(), stream()),
      "occ_fill");
@@ -852,8 +859,9 @@ std::vector<torch::Tensor> unique_first(torch::Tensor x) {
   if (n == 0) return {torch::empty({0}, opts), torch::empty({0}, opts)};
   int64_t cap = 1;
   while (cap < 2 * n) cap <<= 1;
-  auto keys = torch::full({cap}, std::numeric_limits<int64_t>::min(), opts);
-  auto minpos = torch::full({cap}, std::numeric_limits<int32_t>::max(), opts.dtype(torch::kInt32));
+  auto keys = torch::empty({cap}, opts);
+  auto minpos = torch::empty({cap}, opts.dtype(torch::kInt32));
+  ok(eh_unique_init(keys.data_ptr(), minpos.data_ptr<int32_t>(), cap, stream()), "unique_init");
   auto slot = torch::empty({n}, opts.dtype(torch::kInt32));
   auto flag = torch::empty({n}, opts.dtype(torch::kInt32));
   ok(eh_unique_insert(x.data_ptr<int64_t>(), n, keys.data_ptr(), minpos.data_ptr<int32_t>(), cap,
@@ -884,8 +892,9 @@ std::vector<torch::Tensor> unique_first_padded(torch::Tensor x, int64_t fill) {
   if (n == 0) return {torch::empty({0}, opts), torch::empty({0}, opts), torch::zeros({1}, opts)};
   int64_t cap = 1;
   while (cap < 2 * n) cap <<= 1;
-  auto keys = torch::full({cap}, std::numeric_limits<int64_t>::min(), opts);
-  auto minpos = torch::full({cap}, std::numeric_limits<int32_t>::max(), opts.dtype(torch::kInt32));
+  auto keys = torch::empty({cap}, opts);
+  auto minpos = torch::empty({cap}, opts.dtype(torch::kInt32));
+  ok(eh_unique_init(keys.data_ptr(), minpos.data_ptr<int32_t>(), cap, stream()), "unique_init");
   auto slot = torch::empty({n}, opts.dtype(torch::kInt32));
   auto flag = torch::empty({n}, opts.dtype(torch::kInt32));
   ok(eh_unique_insert(x.data_ptr<int64_t>(), n, keys.data_ptr(), minpos.data_ptr<int32_t>(), cap,

@@ -15,6 +15,8 @@
 #include "hip/common.h"
 #include "hip/launchers.h"
 
+#include <hipcub/hipcub.hpp>
+
 namespace euler_hip {
 
 template <typename T>
@@ -243,6 +245,15 @@ __global__ __launch_bounds__(256) void occ_fill_kernel(const int64_t* __restrict
   if (o >= n) return;
   const int64_t u = inv[o];
   list[ptr[u] + atomicAdd(cursor + u, 1)] = static_cast<int>(o);
+}
+
+// occurrence counts: cnt[inv[o]] += 1 (int32, exact); the first thread also zeroes ptr[0]
+__global__ __launch_bounds__(256) void occ_count_kernel(const int64_t* __restrict__ inv, int64_t n,
+                                                        int* __restrict__ cnt, int64_t* __restrict__ ptr) {
+  const int64_t o = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (o == 0) ptr[0] = 0;
+  if (o >= n) return;
+  atomicAdd(cnt + inv[o], 1);
 }
 
 struct SgnsUpd {
@@ -924,6 +935,19 @@ hipError_t eh_sgns_fwd_idx(const void* T, const int64_t* tmap, int64_t nTm, cons
                      P, K,
                      D, lp, gscale, coef, loss_rows);
   return hipGetLastError();
+}
+
+// ptr[1 + u] = inclusive prefix sum of the occurrence counts (counts of one launch < 2^31).
+// `temp` null: *temp_bytes receives the scan's scratch size and nothing runs.
+hipError_t eh_occ_count_scan(const int64_t* inv, int64_t n, int64_t n_u, int* cnt, int64_t* ptr, void* temp,
+                             size_t* temp_bytes, hipStream_t s) {
+  if (n_u <= 0) return hipErrorInvalidValue;
+  if (!temp) return hipcub::DeviceScan::InclusiveSum(nullptr, *temp_bytes, cnt, ptr + 1, static_cast<int>(n_u), s);
+  hipLaunchKernelGGL(occ_count_kernel, dim3(static_cast<uint32_t>(ceil_div(n > 0 ? n : 1, 256))), dim3(256), 0, s,
+                     inv, n, cnt, ptr);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return hipcub::DeviceScan::InclusiveSum(temp, *temp_bytes, cnt, ptr + 1, static_cast<int>(n_u), s);
 }
 
 hipError_t eh_occ_fill(const int64_t* inv, int64_t n, const int64_t* ptr, int* cursor, int* list, hipStream_t s) {

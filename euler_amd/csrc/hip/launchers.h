@@ -96,6 +96,8 @@ hipError_t eh_sgns_fwd_idx(const void* T, const int64_t* tmap, int64_t nTm, cons
                            float gscale, float* coef, float* loss_rows, int rows_bf16, hipStream_t s);
 hipError_t eh_gather_f32_bf16(const float* x, int64_t n_rows, int D, const int64_t* idx, int64_t n, void* out,
                               hipStream_t s);
+hipError_t eh_occ_count_scan(const int64_t* inv, int64_t n, int64_t n_u, int* cnt, int64_t* ptr, void* temp,
+                             size_t* temp_bytes, hipStream_t s);
 hipError_t eh_occ_fill(const int64_t* inv, int64_t n, const int64_t* ptr, int* cursor, int* list, hipStream_t s);
 hipError_t eh_sgns_update(int side, int64_t n_u, const int64_t* ptr, const int* list, const float* coef, int64_t P,
                           int K, int D, const void* src, int src_bf16, int64_t n_src, const int64_t* smap,
@@ -146,6 +148,7 @@ hipError_t eh_route_by_owner(const int64_t* ids, int64_t n, int W, int64_t C, in
                              int64_t* pos, int64_t* send, int32_t* overflow, hipStream_t s);
 
 // unique.hip (K8: hash unique, first-occurrence order)
+hipError_t eh_unique_init(void* keys, int32_t* minpos, int64_t cap, hipStream_t s);
 hipError_t eh_unique_insert(const int64_t* x, int64_t n, void* keys, int32_t* minpos, int64_t cap, int32_t* slot,
                             int skip_neg, hipStream_t s);
 hipError_t eh_unique_mark(int64_t n, const int32_t* slot, const int32_t* minpos, int32_t* flag, hipStream_t s);

@@ -26,6 +26,15 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
   return k;
 }
 
+// empty table: keys = kUniqEmpty, minpos = INT32_MAX (one launch for both arrays)
+__global__ __launch_bounds__(256) void unique_init_kernel(unsigned long long* __restrict__ keys,
+                                                          int32_t* __restrict__ minpos, int64_t cap) {
+  grid_stride(cap, [&](int64_t i) {
+    keys[i] = kUniqEmpty;
+    minpos[i] = 0x7fffffff;
+  });
+}
+
 __global__ __launch_bounds__(256) void unique_insert_kernel(const int64_t* __restrict__ x, int64_t n,
                                                             unsigned long long* __restrict__ keys,
                                                             int32_t* __restrict__ minpos, int64_t cap,
@@ -90,6 +99,13 @@ __global__ __launch_bounds__(256) void unique_finalize_kernel(const int64_t* __r
 using namespace euler_hip;
 
 extern "C" {
+
+hipError_t eh_unique_init(void* keys, int32_t* minpos, int64_t cap, hipStream_t s) {
+  if (cap <= 0) return hipSuccess;
+  hipLaunchKernelGGL(unique_init_kernel, grid_for(cap), dim3(256), 0, s, static_cast<unsigned long long*>(keys), minpos,
+                     cap);
+  return hipGetLastError();
+}
 
 hipError_t eh_unique_insert(const int64_t* x, int64_t n, void* keys, int32_t* minpos, int64_t cap, int32_t* slot,
                             int skip_neg, hipStream_t s) {
