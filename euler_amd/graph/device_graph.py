@@ -354,7 +354,7 @@ class DeviceGraph:
     def _candidates_cpu(self, rows: torch.Tensor, mask: int):
         """(walk index, edge index) of every out edge of rows[i] under the type mask"""
         T = self.num_types
-        ok = rows >= 0
+        ok = (rows >= 0) & (rows < self.num_rows)  # a default row past the table ends a walk
         walk, seg = [], []
         for t in range(T):
             if not (mask >> t) & 1:

@@ -98,9 +98,13 @@ class DeepWalkTrainer:
         g = self.graph
         g.advance()
         starts = g.sample_node(self.batch if batch is None else int(batch), stream_id=1)
-        walks = g.random_walk(starts, self.walk_len, edge_types=self.edge_types, default=-1, stream_id=3, p=self.p,
-                              q=self.q).long()
-        walks = torch.where(walks < 0, torch.full_like(walks, self.pad), walks)
+        # a pad at or past the graph's rows ends a walk like -1 does (no row to step from), so
+        # the walk kernel writes it directly: no compare / fill / where per step
+        direct = self.pad >= g.num_rows
+        walks = g.random_walk(starts, self.walk_len, edge_types=self.edge_types, default=self.pad if direct else -1,
+                              stream_id=3, p=self.p, q=self.q).long()
+        if not direct:
+            walks = torch.where(walks < 0, torch.full_like(walks, self.pad), walks)
         src = walks[:, self.pi].reshape(-1)
         pos = walks[:, self.pj].reshape(-1)
         negs = g.sample_node(src.numel() * self.num_negs, stream_id=4).long().view(-1, self.num_negs)
