@@ -53,6 +53,16 @@ def _pair_positions(walk_len, left, right):
     return pairs[:, 0].clone(), pairs[:, 1].clone()
 
 
+def _row_sum(x):
+    """Sum of a 1-D loss vector in two passes when it splits into 256-wide rows: torch's
+    one-shot reduction of the ~98 K per-pair losses runs in a single 512-lane block (27 us
+    per step on the 100M-node bench, profiles/r5_zoo/occ_csr_fused/README.txt)."""
+    n = x.numel()
+    if n >= 4096 and n % 256 == 0:
+        return x.view(-1, 256).sum(1).sum()
+    return x.sum()
+
+
 class DeepWalkTrainer:
     def __init__(self, graph, num_nodes, dim=128, walk_len=3, left_win_size=1, right_win_size=1, num_negs=5,
                  batch_size=1024, lr=0.01, optimizer="adam", group=None, seed=0, force_comm=False, static=False,
@@ -183,7 +193,7 @@ class DeepWalkTrainer:
             gnn_ops.sgns_grad(0, ptr_t, lst_t, coef, K, rows, None, cinv, inv_self=tinv, out=g)
             gnn_ops.sgns_grad(1, ptr_c, lst_c, coef, K, rows, None, tinv, inv_self=cinv, out=g)
             tab.apply_static(h, g[: n - 1])
-        self.loss = loss_rows.sum() * gscale
+        self.loss = _row_sum(loss_rows) * gscale
         return self.loss
 
     # ------------------------------------------------------------------ overlapped static step
@@ -209,7 +219,7 @@ class DeepWalkTrainer:
         g = torch.empty_like(rows)
         gnn_ops.sgns_grad(0, ptr_t, lst_t, coef, K, rows, None, cinv, inv_self=tinv, out=g)
         gnn_ops.sgns_grad(1, ptr_c, lst_c, coef, K, rows, None, tinv, inv_self=cinv, out=g)
-        return g[: n - 1], loss_rows.sum() * gscale, (coef, ptr_t, lst_t, ptr_c, lst_c, g)
+        return g[: n - 1], _row_sum(loss_rows) * gscale, (coef, ptr_t, lst_t, ptr_c, lst_c, g)
 
     def _step_static_overlapped(self):
         """Two micro-batches of batch/2 walks.  The calling stream S runs every collective
@@ -306,7 +316,7 @@ class DeepWalkTrainer:
             gnn_ops.sgns_grad(0, ptr_t, lst_t, coef, K, rows, None, cinv, inv_self=tinv, out=g)
             gnn_ops.sgns_grad(1, ptr_c, lst_c, coef, K, rows, None, tinv, inv_self=cinv, out=g)
             tab.apply(h, g, sorted_in=True)
-        self.loss = loss_rows.sum() * gscale
+        self.loss = _row_sum(loss_rows) * gscale
         return self.loss
 
     def pairs_per_step(self):
