@@ -875,7 +875,7 @@ std::vector<torch::Tensor> unique_first(torch::Tensor x) {
   auto inv = torch::empty({n}, opts);
   ok(eh_unique_finalize(x.data_ptr<int64_t>(), n, slot.data_ptr<int32_t>(), minpos.data_ptr<int32_t>(),
                         flag.data_ptr<int32_t>(), pos.data_ptr<int32_t>(), inv.data_ptr<int64_t>(),
-                        uniq.data_ptr<int64_t>(), stream()),
+                        uniq.data_ptr<int64_t>(), 0, stream()),
      "unique_finalize");
   return {uniq, inv};
 }
@@ -883,7 +883,8 @@ std::vector<torch::Tensor> unique_first(torch::Tensor x) {
 // Fixed-capacity form for graph-captured steps: no host read of the unique count.
 // uniq [n] holds the distinct values in first-occurrence order followed by `fill`,
 // count [1] (device) the number of distinct values.
-std::vector<torch::Tensor> unique_first_padded(torch::Tensor x, int64_t fill) {
+// offset: added to every distinct value (not to the fill), e.g. a table half's base row
+std::vector<torch::Tensor> unique_first_padded(torch::Tensor x, int64_t fill, int64_t offset) {
   typed(x, torch::kInt64, "x");
   const int64_t n = x.numel();
   TORCH_CHECK(n < (1ll << 30), "unique_first_padded supports < 2^30 elements");
@@ -907,7 +908,7 @@ std::vector<torch::Tensor> unique_first_padded(torch::Tensor x, int64_t fill) {
   auto inv = torch::empty({n}, opts);
   ok(eh_unique_finalize(x.data_ptr<int64_t>(), n, slot.data_ptr<int32_t>(), minpos.data_ptr<int32_t>(),
                         flag.data_ptr<int32_t>(), pos.data_ptr<int32_t>(), inv.data_ptr<int64_t>(),
-                        uniq.data_ptr<int64_t>(), stream()),
+                        uniq.data_ptr<int64_t>(), offset, stream()),
      "unique_finalize");
   return {uniq, inv, pos.narrow(0, n - 1, 1).to(torch::kInt64)};
 }
@@ -1101,6 +1102,6 @@ void register_gnn_ops(pybind11::module& m) {
         py::arg("neg"), py::arg("kind"), py::arg("corrupt"), py::arg("normalize"), py::arg("gpos"), py::arg("gneg"),
         py::arg("dent"), py::arg("drel"), py::arg("occ") = false);
   m.def("unique_first", &unique_first);
-  m.def("unique_first_padded", &unique_first_padded);
+  m.def("unique_first_padded", &unique_first_padded, py::arg("x"), py::arg("fill") = -1, py::arg("offset") = 0);
   m.def("full_neighbors", &full_neighbors);
 }

@@ -153,7 +153,7 @@ hipError_t eh_unique_insert(const int64_t* x, int64_t n, void* keys, int32_t* mi
                             int skip_neg, hipStream_t s);
 hipError_t eh_unique_mark(int64_t n, const int32_t* slot, const int32_t* minpos, int32_t* flag, hipStream_t s);
 hipError_t eh_unique_finalize(const int64_t* x, int64_t n, const int32_t* slot, const int32_t* minpos,
-                              const int32_t* flag, const int32_t* pos, int64_t* inv, int64_t* uniq, hipStream_t s);
+                              const int32_t* flag, const int32_t* pos, int64_t* inv, int64_t* uniq, int64_t offset, hipStream_t s);
 
 // flow.hip (device full-neighbourhood expansion, capacity-padded)
 hipError_t eh_flow_degree(const int64_t* indptr, int64_t num_rows, int num_types, uint32_t mask, const int64_t* rows,

@@ -86,12 +86,13 @@ __global__ __launch_bounds__(256) void unique_finalize_kernel(const int64_t* __r
                                                               const int32_t* __restrict__ minpos,
                                                               const int32_t* __restrict__ flag,
                                                               const int32_t* __restrict__ pos,
-                                                              int64_t* __restrict__ inv, int64_t* __restrict__ uniq) {
+                                                              int64_t* __restrict__ inv, int64_t* __restrict__ uniq,
+                                                              int64_t offset) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int32_t s = slot[i];
   inv[i] = s >= 0 ? static_cast<int64_t>(pos[minpos[s]]) - 1 : -1;
-  if (flag[i]) uniq[pos[i] - 1] = x[i];
+  if (flag[i]) uniq[pos[i] - 1] = x[i] + offset;
 }
 
 }  // namespace euler_hip
@@ -124,10 +125,11 @@ hipError_t eh_unique_mark(int64_t n, const int32_t* slot, const int32_t* minpos,
 }
 
 hipError_t eh_unique_finalize(const int64_t* x, int64_t n, const int32_t* slot, const int32_t* minpos,
-                              const int32_t* flag, const int32_t* pos, int64_t* inv, int64_t* uniq, hipStream_t s) {
+                              const int32_t* flag, const int32_t* pos, int64_t* inv, int64_t* uniq, int64_t offset,
+                              hipStream_t s) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(unique_finalize_kernel, dim3(static_cast<uint32_t>(ceil_div(n, 256))), dim3(256), 0, s, x, n,
-                     slot, minpos, flag, pos, inv, uniq);
+                     slot, minpos, flag, pos, inv, uniq, offset);
   return hipGetLastError();
 }
 

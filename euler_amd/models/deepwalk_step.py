@@ -164,12 +164,12 @@ class DeepWalkTrainer:
         P, K = src.numel(), self.num_negs
         gscale = 1.0 / (P * (1 + K))
         u_t, inv_t, _ = gnn_ops.unique_first_padded(src)
-        u_c, inv_c, _ = gnn_ops.unique_first_padded(torch.cat([pos, negs.reshape(-1)]))
-        rows_c_id = torch.where(u_c >= 0, u_c + self.off, u_c)
+        # context ids straight as their table rows (off + id; padding stays -1)
+        rows_c_id, inv_c, _ = gnn_ops.unique_first_padded(torch.cat([pos, negs.reshape(-1)]), offset=self.off)
         tab = self.table
         if tab.fused_sgns_ok(u_t):
             ptr_t, lst_t = gnn_ops.occ_csr(inv_t, u_t.numel())
-            ptr_c, lst_c = gnn_ops.occ_csr(inv_c, u_c.numel())
+            ptr_c, lst_c = gnn_ops.occ_csr(inv_c, rows_c_id.numel())
             W = tab.weight
             coef, loss_rows = gnn_ops.sgns_fwd_idx(W, u_t, inv_t, W, rows_c_id, inv_c, K, gscale)
             rt = self._gather(W, u_t)                       # pre-update target rows (pad: zero)
@@ -201,8 +201,8 @@ class DeepWalkTrainer:
         """sample + unique + owner routing of one micro-batch (no collective)"""
         src, pos, negs = self.sample(nb)
         u_t, inv_t, _ = gnn_ops.unique_first_padded(src)
-        u_c, inv_c, _ = gnn_ops.unique_first_padded(torch.cat([pos, negs.reshape(-1)]))
-        rows_c_id = torch.where(u_c >= 0, u_c + self.off, u_c)
+        # context ids straight as their table rows (off + id; padding stays -1)
+        rows_c_id, inv_c, _ = gnn_ops.unique_first_padded(torch.cat([pos, negs.reshape(-1)]), offset=self.off)
         routed = self.table.route_static(torch.cat([u_t, rows_c_id]))
         return {"P": src.numel(), "inv_t": inv_t, "inv_c": inv_c, "nt": u_t.numel(), "routed": routed}
 

@@ -705,20 +705,20 @@ def sgns_fwd_idx(T, tmap, tinv, C, cmap, cinv, K, gscale):
     return (torch.sigmoid(x) - y) * gscale, loss
 
 
-def unique_first_padded(x: torch.Tensor, fill: int = -1):
+def unique_first_padded(x: torch.Tensor, fill: int = -1, offset: int = 0):
     """Fixed-capacity :func:`unique_first` for graph-captured steps: ``(uniq [n], inverse
     [n], count [1])`` with the distinct non-negative values in first-occurrence order
-    followed by ``fill``; negative values are padding ("no id": not counted, inverse -1);
-    the count stays on the device (GPU: no host sync)."""
+    (plus ``offset``) followed by ``fill``; negative values are padding ("no id": not
+    counted, inverse -1); the count stays on the device (GPU: no host sync)."""
     x = x.reshape(-1)
     if use_hip(x):
-        return tuple(hip().unique_first_padded(x.long().contiguous(), int(fill)))
+        return tuple(hip().unique_first_padded(x.long().contiguous(), int(fill), int(offset)))
     valid = x >= 0
     u, inv_v = unique_first(x[valid])
     inv = torch.full((x.numel(),), -1, dtype=torch.long, device=x.device)
     inv[valid] = inv_v.long()
     out = torch.full((x.numel(),), int(fill), dtype=torch.long, device=x.device)
-    out[: u.numel()] = u
+    out[: u.numel()] = u + int(offset)
     return out, inv, torch.tensor([u.numel()], dtype=torch.long, device=x.device)
 
 

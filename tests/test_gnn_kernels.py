@@ -327,6 +327,8 @@ def test_unique_first_padded_skips_padding_cpu():
     u, inv, cnt = G.unique_first_padded(x)
     assert u.tolist() == [5, 3, 9, -1, -1, -1, -1, -1] and int(cnt) == 3
     assert inv.tolist() == [0, -1, 1, 0, -1, -1, 2, 1]
+    u, inv2, _ = G.unique_first_padded(x, offset=100)  # distinct values shifted, fill kept
+    assert u.tolist() == [105, 103, 109, -1, -1, -1, -1, -1] and torch.equal(inv2, inv)
 
 
 @pytest.mark.gpu
@@ -339,6 +341,8 @@ def test_unique_first_padded_gpu_matches_cpu(cuda):
     u_c, i_c, n_c = G.unique_first_padded(x)
     u_g, i_g, n_g = G.unique_first_padded(x.to(cuda))
     assert torch.equal(u_g.cpu(), u_c) and torch.equal(i_g.cpu(), i_c) and int(n_g) == int(n_c)
+    u_o, i_o, _ = G.unique_first_padded(x.to(cuda), offset=7001)
+    assert torch.equal(u_o.cpu(), torch.where(u_c >= 0, u_c + 7001, u_c)) and torch.equal(i_o.cpu(), i_c)
 
 
 @pytest.mark.gpu
