@@ -196,12 +196,16 @@ class BaseEstimator:
         dense = [p for p in params if not is_sharded(p)]
         self._sync = dp.GradSync(dense, bucket_bytes=int(self.params.get("bucket_bytes", 32 << 20)))
 
-    def save(self, step=None, extra=None, all_ranks=False, model_state=None):
+    def save(self, step=None, extra=None, all_ranks=False, model_state=None, shards=None, commit=True):
         """Write ``model.ckpt-<step>.pt`` (rank 0) and, when some state differs per rank
         (sharded tables, or ``all_ranks``: e.g. the device path's per-rank sampler stream),
         ``model.ckpt-<step>-rank<r>.pt`` on every other rank (reference per-worker outputs,
-        ``base_estimator.py:157-179``).  Rank 0 keeps the newest ``keep_checkpoint_max``
-        steps, every rank's file of a step together."""
+        ``base_estimator.py:157-179``).  ``shards(path)``: writes this rank's rows of the
+        row-sharded tables (and their optimizer slots) next to the file and returns their
+        metadata (parallel/shard_io.py), kept under "shards".  ``commit``: rank 0 points
+        the ``checkpoint`` index at the new step and keeps the newest
+        ``keep_checkpoint_max`` steps (every rank's files of a step together); a caller
+        whose ranks write concurrently commits after a barrier (:meth:`_commit`)."""
         step = self.global_step if step is None else step
         if self.rank != 0 and not all_ranks and not any(is_sharded(p) for p in self.model.parameters()):
             return None
@@ -213,26 +217,72 @@ class BaseEstimator:
                            if not isinstance(v, nn.parameter.UninitializedParameter)}  # never-called lazy layers
         state = {"step": step, "model": model_state,
                  "optimizer": self.optimizer.state_dict() if self.optimizer is not None else None,
-                 "world": self.world, "torch_rng": torch.get_rng_state()}
+                 "world": self.world, "rank": self.rank, "torch_rng": torch.get_rng_state()}
         state.update(extra or {})
+        if shards is not None:
+            state["shards"] = shards(path)
         tmp = path + ".tmp"
         torch.save(state, tmp)
         os.replace(tmp, path)
-        if self.rank == 0:
-            with open(os.path.join(self.model_dir, "checkpoint"), "w") as f:
-                f.write('model_checkpoint_path: "%s"\n' % os.path.basename(path))
-            keep = int(self.run_config.get("keep_checkpoint_max", self.params.get("keep_checkpoint_max", 5)))
-            cks = glob.glob(os.path.join(self.model_dir, "model.ckpt-*.pt"))
-            step_of = {p: int(re.search(r"model\.ckpt-(\d+)", p).group(1)) for p in cks}
-            steps = sorted(set(step_of.values()))
-            drop = set(steps[:-keep]) - {step} if keep > 0 else set()
-            for old in cks:
-                if step_of[old] in drop:
+        if commit and self.rank == 0:
+            self._commit(step, path)
+        return path
+
+    def _commit(self, step, path):
+        """rank 0: the ``checkpoint`` index names step ``step``; older steps beyond
+        ``keep_checkpoint_max`` are deleted (every rank's file and shard files)"""
+        from euler_amd.parallel.shard_io import sidecar_files
+
+        with open(os.path.join(self.model_dir, "checkpoint"), "w") as f:
+            f.write('model_checkpoint_path: "%s"\n' % os.path.basename(path))
+        keep = int(self.run_config.get("keep_checkpoint_max", self.params.get("keep_checkpoint_max", 5)))
+        cks = glob.glob(os.path.join(self.model_dir, "model.ckpt-*.pt"))
+        step_of = {p: int(re.search(r"model\.ckpt-(\d+)", p).group(1)) for p in cks}
+        steps = sorted(set(step_of.values()))
+        drop = set(steps[:-keep]) - {step} if keep > 0 else set()
+        for old in cks:
+            if step_of[old] in drop:
+                for f in [old] + sidecar_files(old):
                     try:
-                        os.remove(old)
+                        os.remove(f)
                     except FileNotFoundError:
                         pass
-        return path
+
+    def _shard_metas(self, path, saved_world, state=None):
+        """table -> [per-rank shard metadata] of the checkpoint whose rank-0 file is ``path``
+        (each rank's small .pt file holds its own; tables never leave the shard files)"""
+        base = re.sub(r"-rank\d+\.pt$", ".pt", path)
+        out = {}
+        for r in range(int(saved_world)):
+            f = rank_checkpoint(base, r) if saved_world > 1 else base
+            st = state if state is not None and int(state.get("rank", 0)) == r and f == path else \
+                torch.load(f, map_location="cpu", weights_only=True)
+            for key, meta in (st.get("shards") or {}).items():
+                out.setdefault(key, []).append(meta)
+        return out
+
+    def _load_model_shards(self, path, saved_world, state):
+        """engine-path restore of tables kept in per-rank shard files: this rank's rows of a
+        ShardedEmbedding, every row of a dense table; returns the keys filled"""
+        from euler_amd.parallel.embedding import ShardedEmbedding
+        from euler_amd.parallel.shard_io import read_rows
+
+        metas = self._shard_metas(path, saved_world, state)
+        mod_of = {id(p): m for m in self.model.modules() for p in m.parameters(recurse=False)}
+        params = self.model.state_dict(keep_vars=True)  # a table shared by two roles: both names
+        done, filled = set(), set()
+        for key, ms in metas.items():
+            p = params.get(key)
+            if p is None:
+                continue
+            if id(p) not in filled:
+                m = mod_of.get(id(p))
+                rows = m.global_ids().cpu() if isinstance(m, ShardedEmbedding) else torch.arange(p.shape[0])
+                with torch.no_grad():
+                    read_rows(os.path.dirname(path), ms, "weight", rows, p.data)
+                filled.add(id(p))
+            done.add(key)
+        return done
 
     def restore(self, path=None, strict=True):
         path = path or latest_checkpoint(self.model_dir)
@@ -245,9 +295,13 @@ class BaseEstimator:
         state = torch.load(path, map_location=self.device, weights_only=True)
         saved_world = int(state.get("world", 1))
         names = sharded_param_names(self.model)
-        if names and saved_world != self.world:
+        if names and saved_world != self.world and not state.get("shards"):
             self._reshard(state, path, saved_world, names)
-        self.model.load_state_dict(state["model"], strict=strict)
+        from_shards = self._load_model_shards(path, saved_world, state) if state.get("shards") else set()
+        missing, unexpected = self.model.load_state_dict(state["model"], strict=False)
+        if strict and (set(missing) - from_shards or unexpected):
+            raise RuntimeError(f"checkpoint {path}: missing keys {sorted(set(missing) - from_shards)}, "
+                               f"unexpected keys {sorted(unexpected)}")
         if self.optimizer is not None and state.get("optimizer") is not None:
             self.optimizer.load_state_dict(state["optimizer"])
         self.global_step = int(state["step"])
@@ -283,7 +337,16 @@ class BaseEstimator:
     # ------------------------------------------------------------------ modes
     def train(self):
         if self.params.get("device_graph"):
-            return self._train_device_graph()
+            from euler_amd.estimator.device_trainers import NoDeviceTrainer, has_store_encoder
+
+            try:
+                return self._train_device_graph()
+            except NoDeviceTrainer as e:
+                if not has_store_encoder(self.model):
+                    raise
+                # historical-embedding encoders keep their stores' protocol on the engine
+                # path rather than silently training as their plain parent encoder
+                log.warning("device_graph=True: %s; training on the engine path", e)
         seed = self.params.get("seed")
         if seed is not None:
             torch.manual_seed(int(seed) + self.rank)
@@ -453,7 +516,9 @@ class BaseEstimator:
             log.info("already trained to step %d", self.global_step)
             return {}
         grad_sync, xar, gbuf = None, None, None
-        if self.world > 1 and not getattr(tr, "self_synced", False):
+        gbuf0 = self._device_grad_buffer(tr)
+        empty = gbuf0 is not None and gbuf0.numel() == 0  # every parameter row-sparse: nothing dense to sum
+        if self.world > 1 and not getattr(tr, "self_synced", False) and not empty:
             # xGMI two-shot peer-memory all-reduce or RCCL on GPUs, whichever the start-up
             # timing on this node finds faster (parallel/xgmi.py); gloo on CPUs
             from ..parallel.xgmi import make_grad_sync
@@ -468,8 +533,20 @@ class BaseEstimator:
 
         use_graph = self.device.type == "cuda" and bool(self.params.get("hipgraph", True))
         multi = hasattr(tr, "replay_steps")
+        # capacity-padded device flows (dataflow/device_flow.py): a batch beyond a cap sets
+        # the flow's overflow flag; it is read at every boundary, and a chunk that overflowed
+        # on any rank is rolled back (parameters, optimizer slots, sampler counter) and re-run
+        # with grown caps and re-captured graphs, so no step trains on truncated blocks — the
+        # capture's own eager warm-up steps included
+        flow = getattr(tr, "flow", None)
+        guard = flow is not None and callable(getattr(flow, "grow", None))
+        self.flow_regrows = 0
         if use_graph:
-            self.global_step += self._device_capture(tr, grad_sync, total)
+            snap = self._device_snapshot(tr) if guard else None
+            warm = self._device_capture(tr, grad_sync, total)
+            if guard and self._flow_overflowed(flow):
+                warm = self._regrow(tr, grad_sync, total, flow, snap, self.global_step + warm, use_graph)
+            self.global_step += warm
 
         def run(n):
             if use_graph and multi:
@@ -486,13 +563,6 @@ class BaseEstimator:
         tr.reset_metric()
         last = {}
         delay = self.params.get("debug_delay_rank")  # test hook: one rank arrives late
-        # capacity-padded device flows (dataflow/device_flow.py): a batch beyond a cap sets
-        # the flow's overflow flag; it is read at every boundary, and a chunk that overflowed
-        # on any rank is rolled back (parameters, optimizer slots, sampler counter) and re-run
-        # with grown caps and re-captured graphs, so no step trains on truncated blocks
-        flow = getattr(tr, "flow", None)
-        guard = flow is not None and callable(getattr(flow, "grow", None))
-        self.flow_regrows = 0
         while self.global_step < total:
             # run up to the next log / checkpoint boundary in one go
             nxt = min(total, (self.global_step // log_steps + 1) * log_steps)
@@ -504,24 +574,7 @@ class BaseEstimator:
             snap = self._device_snapshot(tr) if guard else None
             run(nxt - self.global_step)
             if guard and self._flow_overflowed(flow):
-                while True:
-                    self._device_rollback(tr, snap)
-                    if self.flow_regrows >= int(self.params.get("max_flow_regrows", 8)):
-                        raise RuntimeError(f"device dataflow capacity exceeded {self.flow_regrows} times "
-                                           f"(caps {flow.caps})")
-                    self.flow_regrows += 1
-                    old = list(flow.caps)
-                    self._device_release(tr)
-                    flow.grow(float(self.params.get("flow_grow_factor", 2.0)))
-                    log.warning("rank %d: a batch before step %d exceeded the device flow caps %s; rolled the "
-                                "chunk back, caps now %s, re-capturing", self.rank, nxt, old, flow.caps)
-                    tr.reset_metric()
-                    if not use_graph:
-                        break
-                    warm = self._device_capture(tr, grad_sync, total)
-                    if not self._flow_overflowed(flow):  # the capture's own eager warm-up steps fit
-                        self.global_step += warm
-                        break
+                self.global_step += self._regrow(tr, grad_sync, total, flow, snap, nxt, use_graph)
                 continue
             self.global_step = nxt
             if xar is not None and self._xgmi_failed(xar):
@@ -561,6 +614,27 @@ class BaseEstimator:
             tr.finish()  # e.g. row-sparse tables back into the model's own modules
         dp.barrier()
         return last
+
+    def _regrow(self, tr, grad_sync, total, flow, snap, nxt, use_graph):
+        """roll the overflowed chunk back to ``snap``, grow the flow's caps and re-capture
+        until the capture's own eager warm-up steps fit; returns the warm-up steps run"""
+        while True:
+            self._device_rollback(tr, snap)
+            if self.flow_regrows >= int(self.params.get("max_flow_regrows", 8)):
+                raise RuntimeError(f"device dataflow capacity exceeded {self.flow_regrows} times "
+                                   f"(caps {flow.caps})")
+            self.flow_regrows += 1
+            old = list(flow.caps)
+            self._device_release(tr)
+            flow.grow(float(self.params.get("flow_grow_factor", 2.0)))
+            log.warning("rank %d: a batch before step %d exceeded the device flow caps %s; rolled the "
+                        "chunk back, caps now %s, re-capturing", self.rank, nxt, old, flow.caps)
+            tr.reset_metric()
+            if not use_graph:
+                return 0
+            warm = self._device_capture(tr, grad_sync, total)
+            if not self._flow_overflowed(flow):  # the capture's own eager warm-up steps fit
+                return warm
 
     def _flow_overflowed(self, flow) -> bool:
         """the flow's overflow flag, agreed over the process group (MAX)"""
@@ -674,8 +748,15 @@ class BaseEstimator:
             state = torch.load(own, map_location="cpu", weights_only=True)
         elif self.rank != 0:
             same_world = False  # no file of this rank: derive its stream
-        keys = set(tr.state_dict())  # once: a row-sharded trainer assembles it collectively
+        # the trainer's own parameter names (row-sharded trainers name them without assembling
+        # any table); the tables themselves come from the per-rank shard files
+        keys = tr.logical_keys() if callable(getattr(tr, "logical_keys", None)) else set(tr.state_dict())
         tr.load_logical({k: v for k, v in state["model"].items() if k in keys})
+        if state.get("shards"):
+            if not callable(getattr(tr, "load_shards", None)):
+                raise RuntimeError(f"{path} keeps tables in per-rank shard files that this trainer cannot read")
+            base = re.sub(r"-rank\d+\.pt$", ".pt", path)
+            tr.load_shards(os.path.dirname(base), self._shard_metas(base, saved_world))
         st = state.get("device_trainer")
         if st is not None:
             st = dict(st)
@@ -692,15 +773,24 @@ class BaseEstimator:
                  self.rank, "" if same_world else ", re-derived sampler key")
 
     def _device_save(self, tr):
-        """every rank writes its checkpoint file (its own Philox stream); the barrier keeps
-        the other ranks out of the next chunk's collectives until rank 0 has written (a
-        rank spinning in an xGMI wait while rank 0 writes could time out)"""
-        tr.write_to_model(self.model)
+        """every rank writes its checkpoint file (its own Philox stream) — and, for a
+        row-sharded trainer, its own rows of every table plus their optimizer slots
+        (``checkpoint_shards``: no table is ever assembled); rank 0 commits the step after
+        the barrier, once every rank's files exist.  The barrier also keeps the other ranks
+        out of the next chunk's collectives until rank 0 has written (a rank spinning in an
+        xGMI wait while rank 0 writes could time out)."""
+        shards = getattr(tr, "checkpoint_shards", None)
+        if not callable(shards):
+            tr.write_to_model(self.model)
+            shards = None
         # a trainer whose tables live outside the model's modules while it trains
         # (row-sparse tables) gives the checkpoint its own model-named state
         ms = tr.checkpoint_model_state() if callable(getattr(tr, "checkpoint_model_state", None)) else None
-        self.save(extra={"device_trainer": tr.trainer_state(), "optimizer": None}, all_ranks=True, model_state=ms)
+        path = self.save(extra={"device_trainer": tr.trainer_state(), "optimizer": None}, all_ranks=True,
+                         model_state=ms, shards=shards, commit=False)
         dp.barrier()
+        if self.rank == 0:
+            self._commit(self.global_step, path)
 
     def _eval_batches(self):
         return self.evaluate_input_fn()
@@ -716,6 +806,10 @@ class BaseEstimator:
             return None
         tr = getattr(self, "device_trainer", None)
         if tr is None:
+            from euler_amd.estimator.device_trainers import device_infers
+
+            if not device_infers(self.model):
+                return None
             try:
                 first = self.get_train_from_input(self.train_input_fn(), self.params)
                 tr = self._device_graph_trainer(first)

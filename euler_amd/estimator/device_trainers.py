@@ -21,7 +21,12 @@ from typing import Any, Callable, List, Tuple
 import numpy as np
 import torch
 
-__all__ = ["Ctx", "REGISTRY", "build_device_trainer", "register"]
+__all__ = ["Ctx", "REGISTRY", "build_device_trainer", "register", "device_infers", "has_store_encoder",
+           "NoDeviceTrainer"]
+
+
+class NoDeviceTrainer(ValueError):
+    """no device-path trainer accepts the model (the estimator may fall back to the engine path)"""
 
 
 @dataclass
@@ -79,9 +84,38 @@ def register(name: str, predicate: Callable[[Any], bool]):
     return deco
 
 
+def has_store_encoder(model) -> bool:
+    """True when ``model`` holds a historical-embedding encoder (ScalableGCNEncoder /
+    ScalableSageEncoder: stale per-layer stores + gradient stores, reference
+    tf_euler/python/utils/encoders.py:294-408, 629-748)"""
+    from euler_amd.utils.encoders import _StoreMixin
+
+    return any(isinstance(m, _StoreMixin) for m in model.modules())
+
+
+# trainers that run a store encoder's own protocol (stores read / written inside the step)
+STORE_AWARE = {"scalable"}
+
+
+def device_infers(model) -> bool:
+    """False for models whose evaluate / infer must stay on the engine path whatever the
+    trainer: layer-sampled GCNs (FastGCN / AdaptiveGCN draw their layers, reference
+    fast_dataflow.py / layerwise_dataflow.py) — building a device trainer only to learn
+    that would also consume the engine's sampler stream before the engine-path eval."""
+    from euler_amd.dataflow import dataflows as D
+
+    sampler = getattr(getattr(model, "gnn", None), "sampler", None)
+    return not isinstance(sampler, (D.FastGCNDataFlow, D.LayerwiseDataFlow))
+
+
 def build_device_trainer(est, model, first):
-    """the first registered trainer that accepts ``model`` (ValueError if none does)"""
+    """the first registered trainer that accepts ``model`` (NoDeviceTrainer if none does).
+    A model with a historical-embedding encoder is only taken by a store-aware trainer:
+    any other trainer would train it as its plain parent encoder without stores."""
+    stores = has_store_encoder(model)
     for name, pred, builder in REGISTRY:
+        if stores and name not in STORE_AWARE:
+            continue
         if pred(model):
             est._prepare(first)  # materialise lazy layers, broadcast rank 0's weights, optimizer
             if est._sync is not None:
@@ -89,8 +123,11 @@ def build_device_trainer(est, model, first):
             tr = builder(Ctx(est, model))
             tr.device_trainer_kind = name
             return tr
-    raise ValueError("device_graph=True trains: " + ", ".join(n for n, _, _ in REGISTRY) +
-                     f"; {type(model).__name__} is none of them")
+    if stores:
+        raise NoDeviceTrainer(f"{type(model).__name__} holds a historical-embedding (Scalable*) encoder that no "
+                              "device trainer accepts")
+    raise NoDeviceTrainer("device_graph=True trains: " + ", ".join(n for n, _, _ in REGISTRY) +
+                          f"; {type(model).__name__} is none of them")
 
 
 # ----------------------------------------------------------------------------------- predicates
@@ -179,7 +216,18 @@ def _kg(c: Ctx):
 
     m = c.model
     edge_type = c.params.get("train_edge_type", getattr(m, "edge_type", -1))
-    sparse = row_sparse(c, getattr(m.entity_encoder, "num", 0), isinstance(m.entity_encoder, ShardedEmbedding))
+    sharded = isinstance(m.entity_encoder, ShardedEmbedding)
+    sparse = row_sparse(c, getattr(m.entity_encoder, "num", 0), sharded)
+    if sparse and getattr(m, "l2_regular", False):
+        # DistMult(l2_regular=True) regularises every entity row each step: only the dense
+        # trainer computes that term; a sharded table or an explicit request cannot
+        if sharded or c.params.get("row_sparse_tables", "auto") is True:
+            raise ValueError("DistMult(l2_regular=True) needs the whole entity table every step: train it with "
+                             "a dense (sharded=False) table and row_sparse_tables=False")
+        import logging
+
+        logging.getLogger(__name__).info("DistMult(l2_regular=True): dense KGTrainer (the L2 term spans every row)")
+        sparse = False
     cls = RowSparseKGTrainer if sparse else KGTrainer
     return cls.from_model(m, c.batch, edge_type, seed=c.seed * 7919 + c.est.rank, device=c.est.device,
                           **c.opt_kw())

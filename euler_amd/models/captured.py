@@ -197,8 +197,16 @@ class CapturedTrainer:
                 "step": int(self.opt.step_count.item()), "rng": self.rng_source.rng.detach().cpu().clone()}
 
     def load_trainer_state(self, st):
-        self.opt.m.copy_(torch.as_tensor(st["m"]).to(self.opt.m))
-        self.opt.v.copy_(torch.as_tensor(st["v"]).to(self.opt.v))
+        # slots saved before the flat buffers were padded to a multiple of 8 (or after):
+        # the parameters' prefix is copied and the padding tail zeroed
+        for name in ("m", "v"):
+            dst, src = getattr(self.opt, name), torch.as_tensor(st[name]).reshape(-1)
+            n = min(int(src.numel()), int(dst.numel()))
+            if n < self.flat.numel:
+                raise ValueError(f"checkpoint optimizer slot '{name}' has {src.numel()} elements for "
+                                 f"{self.flat.numel} parameters")
+            dst[:n].copy_(src[:n].to(dst))
+            dst[n:].zero_()
         self.opt.step_count.fill_(int(st["step"]))
         self.rng_source.rng.copy_(torch.as_tensor(st["rng"]).to(self.rng_source.rng))
         self.step_count = int(st["step"])
@@ -208,3 +216,107 @@ class CapturedTrainer:
 
     def set_learning_rate(self, lr):
         self.opt.lr = float(lr)
+
+
+class RowSparseTableMixin:
+    """One id table of a CapturedTrainer held as a row-sharded, row-sparse
+    :class:`~euler_amd.parallel.sparse_table.ShardedTable` (``self.id_table``) instead of
+    in the flat buffer.  Row ``r`` lives on rank ``r % world`` (ShardedEmbedding's
+    layout): a ``sharded=True`` model's shard, or any model's table on one rank, IS the
+    trainer's table — the module's weight is rebound to it (no second copy) and leaves
+    autograd and the flat buffer, so per-step work stays independent of |V|.  A dense
+    model under 2+ ranks keeps its full table, written from the shards at the end.
+    Checkpoints: per-rank shard files of the rows and their optimizer slots
+    (parallel/shard_io.py), no all-gather."""
+
+    def _adopt_table(self, model, mod, device, group, optimizer, learning_rate):
+        from euler_amd.parallel.sparse_table import ShardedTable
+
+        opt = optimizer if optimizer in ("adam", "adagrad", "sgd") else "adam"
+        t = ShardedTable(int(mod.num), int(mod.dim), device, group, opt, learning_rate, init=None)
+        w = mod.weight
+        with torch.no_grad():
+            if getattr(mod, "world", 1) > 1 or w.shape[0] == t.weight.shape[0]:
+                t.weight.copy_(w.detach().to(t.weight))  # already this rank's rows
+                w.data = t.weight
+                self._table_bound = True
+            else:
+                t.weight.copy_(w.detach()[t.global_ids().to(w.device)].to(t.weight))
+                self._table_bound = False
+        w.requires_grad_(False)
+        self.id_table, self._mod = t, mod
+        # every state_dict key of the table (a table shared by two roles is listed twice)
+        self._table_keys = [k for k, v in model.state_dict(keep_vars=True).items() if v is w]
+        return t
+
+    # ------------------------------------------------------------------ state
+    def _full(self):
+        return self.id_table.full()
+
+    def logical_keys(self):
+        return set(self.model.state_dict()) | set(self._table_keys)
+
+    def state_dict(self):
+        """model-named state with the WHOLE table (tests / export; a collective under 2+
+        ranks — checkpoints use :meth:`checkpoint_shards`)"""
+        sd = {k: v.detach().cpu() for k, v in self.model.state_dict().items()}
+        full = self._full().cpu()
+        for k in self._table_keys:
+            sd[k] = full
+        return sd
+
+    def logical_params(self):
+        return {k: v.to(self.device) for k, v in self.state_dict().items()}
+
+    def checkpoint_model_state(self):
+        return {k: v.detach().cpu() for k, v in self.model.state_dict().items() if k not in self._table_keys}
+
+    def checkpoint_shards(self, ckpt_path):
+        key = self._table_keys[0]
+        meta = self.id_table.save_shard(ckpt_path, key)
+        return {k: meta for k in self._table_keys}
+
+    def load_shards(self, dirname, metas):
+        for k in self._table_keys:
+            if k in metas:
+                self.id_table.load_shard(dirname, metas[k], name=k)
+                return
+
+    def load_logical(self, sd):
+        with torch.no_grad():
+            own = self.model.state_dict()
+            for k, v in sd.items():
+                if k in own and k not in self._table_keys:
+                    own[k].copy_(torch.as_tensor(v).to(own[k]))
+        for k in self._table_keys:
+            if k in sd:
+                self.id_table.load(sd[k])
+                break
+
+    def write_to_model(self, model):
+        if not (self._table_bound and model is self.model):
+            with torch.no_grad():
+                w = self._mod.weight if model is self.model else model.state_dict()[self._table_keys[0]]
+                t = self.id_table
+                w.copy_((t.weight if w.shape[0] == t.weight.shape[0] else self._full()).to(w))
+        if model is not self.model:
+            model.load_state_dict(self.checkpoint_model_state(), strict=False)
+
+    def finish(self):
+        self.write_to_model(self.model)
+        self._mod.weight.requires_grad_(True)
+
+    def trainer_state(self):
+        st = super().trainer_state()
+        st["id_table_step"] = int(self.id_table.step.item())
+        return st
+
+    def load_trainer_state(self, st):
+        super().load_trainer_state(st)
+        if "id_table" in st:  # an older checkpoint: whole slot tensors of the same layout
+            self.id_table.load_slot_state(st.get("id_table"))
+        if "id_table_step" in st:
+            self.id_table.step.fill_(int(st["id_table_step"]))
+
+    def dp_state_tensors(self):
+        return list(super().dp_state_tensors()) + self.id_table.state_tensors()

@@ -66,7 +66,10 @@ def _row_sum(x):
 class DeepWalkTrainer:
     def __init__(self, graph, num_nodes, dim=128, walk_len=3, left_win_size=1, right_win_size=1, num_negs=5,
                  batch_size=1024, lr=0.01, optimizer="adam", group=None, seed=0, force_comm=False, static=False,
-                 wire_dtype="bf16", overflow_check_every=200, micro_batches=1, edge_types=None, p=1.0, q=1.0):
+                 wire_dtype="bf16", overflow_check_every=200, micro_batches=1, edge_types=None, p=1.0, q=1.0,
+                 row_map=None, table_init="normal"):
+        import torch.distributed as dist
+
         self.graph = graph
         self.edge_types, self.p, self.q = edge_types, float(p), float(q)
         self.num_nodes = int(num_nodes)
@@ -74,12 +77,20 @@ class DeepWalkTrainer:
         self.dim, self.walk_len, self.num_negs, self.batch = int(dim), int(walk_len), int(num_negs), int(batch_size)
         dev = graph.device
         self.device = dev
+        # row_map [graph rows + 1]: table row of every graph row (the last entry: the walk's
+        # pad, graph row num_rows) when the table rows are not the graph rows (model ids)
+        self.row_map = None if row_map is None else torch.as_tensor(row_map, dtype=torch.int64).to(dev)
         # ONE row-sharded table holds both embeddings: target row of node i is row i, its
         # context row is row off + i.  A step then needs one id exchange, one row exchange,
-        # one gradient exchange and one host sync (world > 1) instead of two of each.
-        self.off = self.num_nodes + 1
+        # one gradient exchange and one host sync (world > 1) instead of two of each.  off is
+        # a multiple of the world size, so each half is itself mod-sharded: this rank's target
+        # rows and context rows are two contiguous blocks of its shard with the same layout as
+        # a ShardedEmbedding of the half (model tables can be views of them, checkpoints
+        # write each half as the model's table)
+        world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self.off = -(-(self.num_nodes + 1) // world) * world
         self.table = ShardedTable(2 * self.off, dim, dev, group, optimizer, lr, seed=seed, force_comm=force_comm,
-                                  wire_dtype=wire_dtype)
+                                  wire_dtype=wire_dtype, init=table_init)
         pi, pj = _pair_positions(walk_len, left_win_size, right_win_size)
         self.pi, self.pj = pi.to(dev), pj.to(dev)
         self.pairs_per_walk = int(pi.numel())
@@ -110,14 +121,17 @@ class DeepWalkTrainer:
         starts = g.sample_node(self.batch if batch is None else int(batch), stream_id=1)
         # a pad at or past the graph's rows ends a walk like -1 does (no row to step from), so
         # the walk kernel writes it directly: no compare / fill / where per step
-        direct = self.pad >= g.num_rows
-        walks = g.random_walk(starts, self.walk_len, edge_types=self.edge_types, default=self.pad if direct else -1,
+        pad = g.num_rows if self.row_map is not None else self.pad
+        direct = pad >= g.num_rows
+        walks = g.random_walk(starts, self.walk_len, edge_types=self.edge_types, default=pad if direct else -1,
                               stream_id=3, p=self.p, q=self.q).long()
         if not direct:
-            walks = torch.where(walks < 0, torch.full_like(walks, self.pad), walks)
+            walks = torch.where(walks < 0, torch.full_like(walks, pad), walks)
         src = walks[:, self.pi].reshape(-1)
         pos = walks[:, self.pj].reshape(-1)
         negs = g.sample_node(src.numel() * self.num_negs, stream_id=4).long().view(-1, self.num_negs)
+        if self.row_map is not None:  # graph rows -> table rows (model ids)
+            src, pos, negs = self.row_map[src], self.row_map[pos], self.row_map[negs]
         return src, pos, negs
 
     def step(self):
@@ -334,23 +348,47 @@ class DeepWalkTrainer:
         return rows[inv].view(*ids.shape, self.dim)
 
 
+def _id_table(enc):
+    """(table module, sharded) of a pure id encoder: an IdEncoder (ShardedEmbedding when
+    sharded) or a ShallowEncoder with only an id embedding and combiner 'add'; None if the
+    encoder has features"""
+    from euler_amd.models.unsupervised import IdEncoder
+
+    if isinstance(enc, IdEncoder):
+        if enc.table is not None:
+            return enc.table, True
+        enc = enc.enc
+    if enc is None or not getattr(enc, "use_id", False) or getattr(enc, "use_feature", True) or \
+            getattr(enc, "use_sparse_feature", True) or enc.combiner != "add":
+        return None
+    return enc.embedding, False
+
+
 class DeepWalkEstimatorTrainer:
     """``NodeEstimator(device_graph=True)`` for DeepWalk / Node2Vec and second-order LINE
     models with id embeddings (reference examples/deepwalk/deepwalk.py:27-99,
     examples/line/line.py:27-71 through
     euler_estimator/python/node_estimator.py): the walks, pairs, negatives and the
     row-sparse SGNS update of :class:`DeepWalkTrainer` on the HBM graph, several static
-    steps per hipGraph replay.  The model's two embedding tables are the trainer's table
-    halves (graph row r = node id ``graph.ids[r]``; the pad row is the model's
-    ``max_id + 1`` row); checkpoints carry the model's own parameter names.
+    steps per hipGraph replay.
+
+    Table ownership: the trainer's row-sharded table holds target rows [0, off) and context
+    rows [off, 2 off) in MODEL row space (model id i; the pad row is the model's
+    ``max_id + 1``; graph rows are mapped to model ids on the device when they differ).
+    ``off`` is a multiple of the world size, so this rank's rows of each half are a
+    contiguous block laid out exactly like a ``mod``-sharded table of the half.  Whenever the
+    model's table has that layout — a ``sharded=True`` model (ShardedEmbedding, any world
+    size) or any model on one rank — the model's weight becomes a VIEW of that block: no
+    second copy of a table exists while the trainer trains it (a 100M x 128 table pair is
+    102 GB).  Only a dense (non-sharded) model under 2+ ranks keeps its own full table,
+    written from the shards when training ends.
 
     Data parallel (the reference's ``mod``-partitioned PS embedding variables,
-    tf_euler/python/utils/embedding.py:24-68): with 2+ ranks the table is row-sharded
-    (``parallel/sparse_table.py``: trainer row r on rank r % world), every step's rows travel
-    over fixed-capacity all-to-alls and only the touched rows are updated — per-step work
-    and traffic depend on the batch, never on |V|.  Each rank draws its own walks (its own
-    Philox key); the model's full tables are assembled (all-gather of the shards) only when
-    a checkpoint or the model is written."""
+    tf_euler/python/utils/embedding.py:24-68): every step's rows travel over fixed-capacity
+    all-to-alls and only the touched rows are updated; each rank draws its own walks (its
+    own Philox key).  Checkpoints are per-rank shards (parallel/shard_io.py): every rank
+    writes its rows of each table and their sparse-optimizer slots, and a restore under any
+    world size reads exactly its own rows from them — no all-gather anywhere."""
 
     metric_name = "loss"
     self_synced = True  # no dense gradient for the estimator to all-reduce
@@ -361,34 +399,65 @@ class DeepWalkEstimatorTrainer:
         import euler_amd.ops.graph_api as ge
 
         enc_t, enc_c = getattr(model, "_target_encoder", None), getattr(model, "_context_encoder", None)
-        for e in (enc_t, enc_c):
-            if e is None or not getattr(e, "use_id", False) or getattr(e, "use_feature", True) or \
-                    getattr(e, "use_sparse_feature", True) or e.combiner != "add":
-                raise ValueError("the DeepWalk device path trains pure id embeddings (no features, combiner 'add')")
-        if enc_t is enc_c:
+        tabs = [_id_table(e) for e in (enc_t, enc_c)]
+        if any(t is None for t in tabs):
+            raise ValueError("the DeepWalk device path trains pure id embeddings (no features, combiner 'add')")
+        if enc_t is enc_c or tabs[0][0] is tabs[1][0]:
             raise ValueError("the DeepWalk device path needs separate target and context tables "
                              "(LINE: order='second')")
         self.model = model
         self.graph = graph
         self.device = graph.device
         self.on_gpu = self.device.type == "cuda"
+        self._mods = [t for t, _ in tabs]
+        self._sharded = tabs[0][1]
+        self.num = int(self._mods[0].num)  # model rows per table: max_id + 2 (pad row max_id + 1)
+        if int(self._mods[1].num) != self.num or self.num != int(model.max_id) + 2:
+            raise ValueError("DeepWalk tables must have max_id + 2 rows (the pad row is max_id + 1)")
+        names = {id(p): k for k, p in model.named_parameters()}
+        self._keys = tuple(names[id(m.weight)] for m in self._mods)
         et = model.edge_type
         ets = None if et in (None, -1, "-1") else [int(t) for t in np.asarray(ge.get_edge_type_id(et)).reshape(-1)]
+        # graph row -> model row, unless graph row r is node id r for every row
+        ids = graph.ids
+        row_map = None
+        if ids is not None:
+            ids = np.asarray(ids).astype(np.int64)
+            if ids.size and (ids.max() > model.max_id or ids.min() < 0):
+                raise ValueError("graph node ids beyond the model's max_id")
+            if not np.array_equal(ids, np.arange(ids.size)):
+                row_map = np.concatenate([ids, [self.num - 1]])
+        elif graph.num_rows > self.num - 1:
+            raise ValueError("graph rows beyond the model's max_id")
         # LINE (second order, examples/line/line.py:27-71): the positive of a root is one
         # weighted neighbour sample (UnsuperviseModel.to_sample) = the second node of a
         # one-step walk, paired (root, neighbour) only: walk_len 1, window (0, 1)
         walk_len = getattr(model, "walk_len", 1)
         win = (getattr(model, "left_win_size", 0), getattr(model, "right_win_size", 1))
-        self.inner = DeepWalkTrainer(graph, graph.num_rows, dim=model.dim, walk_len=walk_len,
+        self.inner = DeepWalkTrainer(graph, self.num - 1, dim=model.dim, walk_len=walk_len,
                                      left_win_size=win[0], right_win_size=win[1],
                                      num_negs=model.num_negs, batch_size=batch_size, lr=learning_rate,
                                      optimizer=optimizer, seed=seed, static=self.on_gpu, edge_types=ets,
-                                     p=getattr(model, "walk_p", 1), q=getattr(model, "walk_q", 1))
-        self._keys = ("_target_encoder.embedding.weight", "_context_encoder.embedding.weight")
-        ids = graph.ids if graph.ids is not None else np.arange(graph.num_rows)
-        self._ids = torch.as_tensor(np.asarray(ids).astype(np.int64), device=self.device)
-        self._pad_id = int(model.max_id) + 1
-        self.load_logical(model.state_dict())
+                                     p=getattr(model, "walk_p", 1), q=getattr(model, "walk_q", 1),
+                                     row_map=row_map, table_init=None)
+        t = self.inner.table
+        self._offw = self.inner.off // t.world  # local rows per half
+        self._pad_rows()
+        # the model's tables become views of the trainer's halves (same layout) — or, for a
+        # dense model under 2+ ranks, this rank's rows are copied in
+        self._bound = self._sharded or t.world == 1
+        with torch.no_grad():
+            for h, mod in enumerate(self._mods):
+                w = mod.weight
+                if self._bound:
+                    n = int(w.shape[0])
+                    view = t.weight[h * self._offw: h * self._offw + n]
+                    view.copy_(w.detach().to(view))
+                    w.data = view
+                else:
+                    rows = self._half_rows()
+                    ok = rows < self.num
+                    t.weight[h * self._offw: (h + 1) * self._offw][ok] = w.detach()[rows[ok].to(w.device)].to(t.weight)
         self.loss_sum = torch.zeros(2, dtype=torch.float64, device=self.device)
         self._graphs, self._graph_loss, self._graph_exec = {}, {}, None
         self._loss = torch.zeros((), device=self.device)
@@ -396,57 +465,68 @@ class DeepWalkEstimatorTrainer:
         self.captures = 0
 
     # ------------------------------------------------------------------ table <-> model
-    # trainer row r (target half: r < off, context half: off + r) of graph row i is node id
-    # ids[i] (the pad row, off - 1, is the model's max_id + 1 row); with a row-sharded table
-    # this rank holds trainer rows table.global_ids() (r % world == rank)
-    def _model_rows(self):
-        """model row of every trainer row of one half (off entries)"""
-        pad = torch.tensor([self._pad_id], dtype=torch.int64, device=self.device)
-        return torch.cat([self._ids, pad])
+    def _half_rows(self):
+        """model row of each of this rank's local rows of one half"""
+        t = self.inner.table
+        return torch.arange(self._offw, device=self.device) * t.world + t.rank
+
+    def _pad_rows(self):
+        """zero the alignment rows [num, off) of both halves (never drawn, never trained)"""
+        t = self.inner.table
+        rows = self._half_rows()
+        dead = torch.nonzero(rows >= self.num).reshape(-1)
+        with torch.no_grad():
+            for h in range(2):
+                t.weight[h * self._offw + dead] = 0.0
+
+    def logical_keys(self):
+        return set(self._keys)
 
     def load_logical(self, sd):
-        t = self.inner
-        g = t.table.global_ids()
-        half, r = g // t.off, g % t.off
-        mrow = self._model_rows()[r]
+        """model-named tables: this rank's rows (a ShardedEmbedding's shard) or the whole
+        table (a dense model's, or one saved by a single rank)"""
+        t = self.inner.table
+        rows = self._half_rows()
+        ok = rows < self.num
         with torch.no_grad():
             for h, key in enumerate(self._keys):
                 if key not in sd:
                     continue
-                w = torch.as_tensor(sd[key]).to(t.table.weight)
-                sel = half == h
-                t.table.weight[sel] = w[mrow[sel]]
+                w = torch.as_tensor(sd[key])
+                dst = t.weight[h * self._offw: (h + 1) * self._offw]
+                if int(w.shape[0]) == self.num:
+                    dst[ok] = w[rows[ok].cpu()].to(dst)
+                elif int(w.shape[0]) == int(ok.sum()):
+                    dst[: w.shape[0]] = w.to(dst)
+                else:
+                    raise ValueError(f"{key}: {tuple(w.shape)} is neither the table nor this rank's shard")
 
-    def _full_table(self):
-        """every trainer row (all ranks' shards; all-gather with 2+ ranks: a collective)"""
+    def _full_table(self, h):
+        """the whole table ``h`` (dense model under 2+ ranks: an all-gather)"""
         t = self.inner.table
+        half = t.weight[h * self._offw: (h + 1) * self._offw]
         if t.world == 1:
-            return t.weight
+            return half[: self.num]
         import torch.distributed as dist
 
-        n = int(t.weight.shape[0])
-        sizes = torch.tensor([n], dtype=torch.int64, device=t.weight.device)
-        all_n = [torch.zeros_like(sizes) for _ in range(t.world)]
-        dist.all_gather(all_n, sizes, group=t.group)
-        mx = max(int(x.item()) for x in all_n)
-        buf = torch.zeros((mx, t.dim), dtype=t.weight.dtype, device=t.weight.device)
-        buf[:n] = t.weight
-        parts = [torch.zeros_like(buf) for _ in range(t.world)]
-        dist.all_gather(parts, buf, group=t.group)
-        full = torch.empty((t.num_rows, t.dim), dtype=t.weight.dtype, device=t.weight.device)
-        for r, (p, k) in enumerate(zip(parts, all_n)):
-            full[r::t.world] = p[: int(k.item())]
-        return full
+        parts = [torch.empty_like(half) for _ in range(t.world)]
+        dist.all_gather(parts, half.contiguous(), group=t.group)
+        return torch.stack(parts, 1).reshape(-1, t.dim)[: self.num]
 
     def write_to_model(self, model):
-        t = self.inner
-        full = self._full_table()
+        """views: nothing to copy; a dense model under 2+ ranks gets the gathered tables
+        (a collective — at the end of training, never per checkpoint)"""
+        if self._bound and model is self.model:
+            return
         own = model.state_dict()
-        mrow = self._model_rows()
         with torch.no_grad():
             for h, key in enumerate(self._keys):
-                w = own[key]
-                w[mrow.to(w.device)] = full[h * t.off: (h + 1) * t.off].to(w)
+                full = self._full_table(h)
+                own[key].copy_(full.to(own[key]) if own[key].shape[0] == full.shape[0] else
+                               self.inner.table.weight[h * self._offw: h * self._offw + own[key].shape[0]])
+
+    def finish(self):
+        self.write_to_model(self.model)
 
     def state_dict(self):
         self.write_to_model(self.model)
@@ -454,6 +534,26 @@ class DeepWalkEstimatorTrainer:
 
     def logical_params(self):
         return self.state_dict()
+
+    # ------------------------------------------------------------------ per-rank checkpoints
+    def checkpoint_model_state(self):
+        """the model's state without its id tables (they go to the per-rank shard files)"""
+        return {k: v.detach().cpu() for k, v in self.model.state_dict().items() if k not in self._keys}
+
+    def checkpoint_shards(self, ckpt_path):
+        """write this rank's rows of both tables and their optimizer slots next to
+        ``ckpt_path``; returns the per-table metadata for the checkpoint file"""
+        t = self.inner.table
+        return {key: t.save_shard(ckpt_path, key, num=self.num, lo=h * self._offw)
+                for h, key in enumerate(self._keys)}
+
+    def load_shards(self, dirname, metas):
+        """this rank's rows of both tables (and slots) from a checkpoint of any world size"""
+        t = self.inner.table
+        for h, key in enumerate(self._keys):
+            if key in metas:
+                t.load_shard(dirname, metas[key], lo=h * self._offw, n_local=self._offw, name=key)
+        self._pad_rows()
 
     # ------------------------------------------------------------------ steps
     def _one(self):
@@ -529,24 +629,12 @@ class DeepWalkEstimatorTrainer:
         return None
 
     def trainer_state(self):
+        """step and sampler counter (the tables and their slots are in the shard files)"""
         t = self.inner.table
-        return {"m": t.m.cpu().clone(), "v": t.v.cpu().clone(), "step": int(t.step.item()),
-                "rng": self.graph.rng.detach().cpu().clone()}
+        return {"step": int(t.step.item()), "rng": self.graph.rng.detach().cpu().clone()}
 
     def load_trainer_state(self, st):
         t = self.inner.table
-        m, v = torch.as_tensor(st["m"]), torch.as_tensor(st["v"])
-        if m.shape == t.m.shape and v.shape == t.v.shape:
-            t.m.copy_(m.to(t.m))
-            t.v.copy_(v.to(t.v))
-        else:
-            # another rank layout (the weights came from the model's full tables): the
-            # optimizer slots of the new shard start fresh
-            import logging
-
-            logging.getLogger("euler_amd.estimator").warning(
-                "DeepWalk device path: the checkpoint's optimizer slots are sharded for another world size; "
-                "restarting them")
         t.step.fill_(int(st["step"]))
         self.graph.rng.copy_(torch.as_tensor(st["rng"]).to(self.graph.rng))
         self.step_count = int(st["step"])

@@ -142,7 +142,10 @@ class FullFlowTrainer(CapturedTrainer):
 
     # ------------------------------------------------------------------ inference
     def _infer_flow(self, n):
-        if self.gnn is None or not isinstance(self.flow, DeviceFullFlow):
+        # exactly the full-neighbourhood flow: DeviceLayerFlow (FastGCN / AdaptiveGCN) subclasses
+        # it but samples its layers, so those models infer on the engine path as the reference
+        # does (fast_dataflow / LayerwiseDataFlow draws)
+        if self.gnn is None or type(self.flow) is not DeviceFullFlow:
             return None  # sampled flows: the engine path infers (their draws are the engine's)
         return infer_flow(self, self.graph, self.flow.masks, self.flow.self_loops, n)
 

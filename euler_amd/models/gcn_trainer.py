@@ -304,6 +304,10 @@ class GcnTrainer(CapturedTrainer):
         of exactly these roots (models/full_trainer.py full_flow_embed)"""
         from euler_amd.models.full_trainer import full_flow_embed, infer_flow
 
+        if self.layer_draws is not None:
+            # FastGCN / AdaptiveGCN sample their layers (reference fast_dataflow /
+            # LayerwiseDataFlow): an exact block would report other metrics than the engine path
+            raise NotImplementedError("layer-sampled GCN models infer on the engine path")
         n = int(torch.as_tensor(ids).numel())
         flow = infer_flow(self, self.graph, self.masks, bool(self.gnn.sampler.add_self_loops), n)
         rows = self.graph.rows_of(ids).to(self.graph.device)

@@ -151,25 +151,6 @@ class KGTrainer(CapturedTrainer):
 
 
 # ---------------------------------------------------------------------------- row-sparse tables
-class _RowsOf(torch.nn.Module):
-    """Stand-in for a per-entity table during a row-sparse step: ``forward(ids)`` returns
-    the rows of the step's gathered leaf tensor for the id tensors the step registered
-    (the model's ``generate_embedding`` calls its entity tables on exactly the src / dst /
-    corruption tensors the trainer passes to ``loss_scores``)."""
-
-    def __init__(self, num, dim):
-        super().__init__()
-        self.num, self.dim = int(num), int(dim)
-        self.rows = None
-        self.pos = {}
-
-    def forward(self, ids):
-        p = self.pos.get(id(ids))
-        if p is None:
-            raise RuntimeError("row-sparse KG step: the model looked up an id tensor the step did not draw")
-        return self.rows[p.reshape(-1)].reshape(*ids.shape, self.dim)
-
-
 class RowSparseKGTrainer(KGTrainer):
     """KGTrainer with the per-entity tables (``entity_encoder``, TransD's
     ``entity_transfer``) held as row-sharded, row-sparse :class:`ShardedTable` s instead of
@@ -179,10 +160,20 @@ class RowSparseKGTrainer(KGTrainer):
     SGD kernel (optim.hip sparse_optim).  Per-step work is independent of |V|; the
     relation tables and projections stay in the flat buffer (dense, all-reduced).
 
+    The model scores the step on the gathered rows: the trainer passes them with src /
+    dst / corruption POSITIONS into them (``loss_scores(..., rows=)``), so TransE /
+    DistMult run the fused kg_fwd / kg_bwd kernels straight on the gathered rows and the
+    row gradients come out per gathered row, ready for the owners' update; the projected
+    variants run their torch compositions on the same rows.
+
+    Table ownership: row ``r`` lives on rank ``r % world`` (ShardedEmbedding's layout), so
+    a ``sharded=True`` model's shard — or any model's table on one rank — IS the trainer's
+    table (the module's weight is rebound to it: no second copy).  A dense model under 2+
+    ranks keeps its full table, written from the shards when training ends.  Checkpoints
+    are per-rank shard files of the rows and their optimizer slots (parallel/shard_io.py).
+
     Reference: tf_euler/python/utils/embedding.py:24-68 (mod-partitioned embedding
-    variables, sparse updates), examples/TransX/transX.py:63-145.  Row ``r`` lives on rank
-    ``r % world`` (ShardedEmbedding's layout), so a ``sharded=True`` model's local shard is
-    the table's shard as it is; checkpoints hold the whole table under the model's name."""
+    variables, sparse updates), examples/TransX/transX.py:63-145."""
 
     TABLES = ("entity_encoder", "entity_transfer")
 
@@ -191,27 +182,38 @@ class RowSparseKGTrainer(KGTrainer):
 
         if not hasattr(model, "loss_scores"):
             raise ValueError("RowSparseKGTrainer trains the TransX family (models/knowledge_graph.py)")
+        if getattr(model, "l2_regular", False):
+            # DistMult's L2 term covers the WHOLE entity table every step (distmult.py): a
+            # row-sparse step touches only the batch's rows and cannot compute it
+            raise ValueError("row-sparse entity tables cannot train DistMult(l2_regular=True): its L2 term spans "
+                             "every entity row; use the dense KGTrainer (row_sparse_tables=False)")
         self.table = table
         self.B = int(batch_size)
         self.metric_name = model.metric_name
         self.msum = torch.zeros(2, dtype=torch.float64, device=table.device)
-        self.tables, self._orig = {}, {}
+        self.tables, self._mods, self._bound = {}, {}, {}
         opt = optimizer if optimizer in ("adam", "adagrad", "sgd") else "adam"
+        names = {id(p): k for k, p in model.named_parameters()}
+        self._keys = {}
         for name in self.TABLES:
             mod = getattr(model, name, None)
             if mod is None:
                 continue
             num, dim = int(mod.num), int(mod.dim)
-            t = ShardedTable(num, dim, table.device, group, opt, learning_rate)
+            t = ShardedTable(num, dim, table.device, group, opt, learning_rate, init=None)
+            w = mod.weight
+            self._keys[name] = names[id(w)]
             with torch.no_grad():
-                w = mod.weight.detach().to(table.device)
                 if getattr(mod, "world", 1) > 1 or w.shape[0] == t.weight.shape[0]:
-                    t.weight.copy_(w)  # already this rank's rows (r % world == rank)
+                    t.weight.copy_(w.detach().to(t.weight))  # already this rank's rows (r % world == rank)
+                    w.data = t.weight                       # the module's table IS the trainer's shard
+                    self._bound[name] = True
                 else:
-                    t.weight.copy_(w[t.global_ids()])
+                    t.weight.copy_(w.detach()[t.global_ids().to(w.device)].to(t.weight))
+                    self._bound[name] = False
+            w.requires_grad_(False)  # row-sparse: never in the flat buffer, no autograd into it
             self.tables[name] = t
-            self._orig[name] = mod
-            setattr(model, name, _RowsOf(num, dim))
+            self._mods[name] = mod
         if "entity_encoder" not in self.tables:
             raise ValueError("the model has no entity_encoder table")
         CapturedTrainer.__init__(self, model, table, table.device, optimizer, learning_rate)
@@ -226,7 +228,6 @@ class RowSparseKGTrainer(KGTrainer):
     def _step(self, grad_sync=None):
         from euler_amd.ops.gnn_ops import unique_first_padded
 
-        self._swap_in()
         self._draw()
         t = self.table
         K = self.model.num_negs
@@ -236,19 +237,17 @@ class RowSparseKGTrainer(KGTrainer):
         ids = torch.cat([src, dst, neg])
         ids = torch.where((ids < 0) | (ids >= num), torch.full_like(ids, num - 1), ids)
         uids, inv, _ = unique_first_padded(ids)
-        src, rel, dst = src.view(-1, 1), rel.view(-1, 1), dst.view(-1, 1)
-        neg = neg.view(self.B, K)
-        handles = {}
+        rows, handles = {}, {}
         for name, tab in self.tables.items():
-            rows, h = tab.lookup_static(uids, trash_row=True)
-            leaf = rows.detach().requires_grad_(True)
-            p = h.pos[inv]
-            mod = getattr(self.model, name)
-            mod.rows = leaf
-            mod.pos = {id(src): p[: self.B], id(dst): p[self.B: 2 * self.B], id(neg): p[2 * self.B:]}
+            r, h = tab.lookup_static(uids, trash_row=True)
+            leaf = r.detach().requires_grad_(True)
+            rows[name] = leaf
             handles[name] = (tab, h, leaf)
+        # every table shares one id set: the positions of the step's ids in the gathered rows
+        p = handles["entity_encoder"][1].pos[inv]
+        ps, pd, pn = p[: self.B].view(-1, 1), p[self.B: 2 * self.B].view(-1, 1), p[2 * self.B:].view(self.B, K)
         self.opt.zero_grad()
-        loss, pos, neg_s = self.model.loss_scores(src, dst, neg, rel)
+        loss, pos, neg_s = self.model.loss_scores(ps, pd, pn, rel.view(-1, 1), rows=rows)
         loss.backward()
         with torch.no_grad():
             r = (neg_s >= pos).sum(-1).double()
@@ -267,88 +266,92 @@ class RowSparseKGTrainer(KGTrainer):
             # the dense buffer's all-reduce averages over ranks; the owners sum the ranks'
             # row gradients, so they are scaled to the same mean here
             tab.apply_static(h, g[:n] / self.world if self.world > 1 else g[:n])
-        for name in self.tables:
-            mod = getattr(self.model, name)
-            mod.rows, mod.pos = None, {}
-        self._samples = (src, rel, dst, neg)
+        self._samples = (src.view(-1, 1), rel.view(-1, 1), dst.view(-1, 1), neg.view(self.B, K))
         self.loss_out.copy_(loss.detach())
         return self.loss_out
 
     # ------------------------------------------------------------------ state
-    @staticmethod
-    def _full_table(tab):
+    def _full_table(self, tab):
         return tab.full()
 
-    def _dense_names(self):
-        return {k for k in self.model.state_dict()}
+    def logical_keys(self):
+        return set(self.model.state_dict())
 
     def state_dict(self):
+        """model-named state with the WHOLE tables (tests / export; a collective under 2+
+        ranks — checkpoints use :meth:`checkpoint_shards` instead)"""
         sd = {k: v.detach().cpu() for k, v in self.model.state_dict().items()}
         for name, tab in self.tables.items():
-            sd[name + ".weight"] = self._full_table(tab).cpu()
+            sd[self._keys[name]] = self._full_table(tab).cpu()
         return sd
 
     def checkpoint_model_state(self):
-        """the model's state under its own names, the whole tables included"""
-        return self.state_dict()
+        """the model's state without the row-sharded tables (those go to the shard files)"""
+        skip = set(self._keys.values())
+        return {k: v.detach().cpu() for k, v in self.model.state_dict().items() if k not in skip}
+
+    def checkpoint_shards(self, ckpt_path):
+        return {self._keys[name]: tab.save_shard(ckpt_path, self._keys[name]) for name, tab in self.tables.items()}
+
+    def load_shards(self, dirname, metas):
+        for name, tab in self.tables.items():
+            key = self._keys[name]
+            if key in metas:
+                tab.load_shard(dirname, metas[key], name=key)
 
     def logical_params(self):
         sd = {k: v.detach().clone() for k, v in self.model.state_dict().items()}
         for name, tab in self.tables.items():
-            sd[name + ".weight"] = self._full_table(tab)
+            sd[self._keys[name]] = self._full_table(tab)
         return sd
 
     def load_logical(self, sd):
         with torch.no_grad():
             own = self.model.state_dict()
+            tab_keys = {self._keys[n]: n for n in self.tables}
             for k, v in sd.items():
-                if k in own:
+                if k in own and k not in tab_keys:
                     own[k].copy_(torch.as_tensor(v).to(own[k]))
-            for name, tab in self.tables.items():
-                v = sd.get(name + ".weight")
-                if v is None:
-                    continue
-                tab.load(v)
+            for key, name in tab_keys.items():
+                if key in sd:
+                    self.tables[name].load(sd[key])
 
     def write_to_model(self, model):
-        """the trained tables back into the model's own modules (restored after training)"""
+        """bound tables are the model's own; a dense model under 2+ ranks gets the gathered
+        tables (a collective)"""
         for name, tab in self.tables.items():
-            mod = self._orig[name]
+            if self._bound[name] and model is self.model:
+                continue
+            mod = self._mods[name]
             with torch.no_grad():
-                if mod.weight.shape[0] == tab.weight.shape[0]:
-                    mod.weight.copy_(tab.weight.to(mod.weight))
-                else:
-                    mod.weight.copy_(self._full_table(tab).to(mod.weight))
+                w = mod.weight if model is self.model else model.state_dict()[self._keys[name]]
+                w.copy_((tab.weight if w.shape[0] == tab.weight.shape[0] else self._full_table(tab)).to(w))
         if model is not self.model:
-            own = {k: v for k, v in self.model.state_dict().items()}
-            model.load_state_dict(own, strict=False)
-
-    def restore_modules(self):
-        """put the model's own table modules back (after :meth:`write_to_model`)"""
-        for name, mod in self._orig.items():
-            setattr(self.model, name, mod)
+            skip = set(self._keys.values())
+            model.load_state_dict({k: v for k, v in self.model.state_dict().items() if k not in skip}, strict=False)
 
     def finish(self):
-        """end of training: the trained tables into the model's own modules, which go back
-        in place (engine-path evaluate / infer and the user's model see them)"""
+        """end of training: every table in the model's own modules (engine-path evaluate /
+        infer and the user's model see them), trainable again"""
         self.write_to_model(self.model)
-        self.restore_modules()
-
-    def _swap_in(self):
-        for name, tab in self.tables.items():
-            if not isinstance(getattr(self.model, name), _RowsOf):
-                setattr(self.model, name, _RowsOf(tab.num_rows, tab.dim))
+        for mod in self._mods.values():
+            mod.weight.requires_grad_(True)
 
     def trainer_state(self):
+        """flat-buffer slots, step and sampler counter (the tables' rows and slots are in
+        the shard files)"""
         st = super().trainer_state()
-        for name, tab in self.tables.items():
-            st[name] = tab.slot_state()
+        st["table_steps"] = {name: int(tab.step.item()) for name, tab in self.tables.items()}
         return st
 
     def load_trainer_state(self, st):
         super().load_trainer_state(st)
         for name, tab in self.tables.items():
-            tab.load_slot_state(st.get(name))  # another world size: the slots restart
+            if name in st:  # an older checkpoint: whole slot tensors of the same layout
+                tab.load_slot_state(st.get(name))
+            stp = (st.get("table_steps") or {}).get(name)
+            if stp is not None:
+                tab.step.fill_(int(stp))
 
     def dp_state_tensors(self):
         ts = list(super().dp_state_tensors())

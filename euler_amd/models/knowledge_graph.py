@@ -84,24 +84,44 @@ class TransX(nn.Module):
         metric = self.metric(pos.detach().float().cpu(), neg_s.detach().float().cpu())
         return loss, metric
 
-    def _fused_ok(self, dev):
-        return self.fused_kind is not None and dev.type == "cuda" and isinstance(self.entity_encoder, Embedding)
+    def _fused_ok(self, dev, rows=None):
+        return self.fused_kind is not None and dev.type == "cuda" and (
+            isinstance(self.entity_encoder, Embedding) or rows is not None)
 
-    def loss_scores(self, src, dst, neg, rel):
+    def loss_scores(self, src, dst, neg, rel, rows=None):
         """(loss, positive scores [B, 1, 1], corrupted scores [B, 1, k]) of device id tensors
         src / dst / rel [B, 1], neg [B, num_negs], with no host round trip: the step of the
-        device-path trainer (models/kg_trainer.py) is captured into a hipGraph"""
-        if self._fused_ok(src.device):
+        device-path trainer (models/kg_trainer.py) is captured into a hipGraph.
+
+        ``rows``: a row-sparse step (RowSparseKGTrainer) passes its gathered entity rows
+        (``{"entity_encoder": [n, D], "entity_transfer": ...}``) and src / dst / neg are
+        POSITIONS into them; the fused kinds then score and differentiate straight on those
+        rows (the kg_fwd / kg_bwd kernels, the row gradients land on the gathered rows)."""
+        if self._fused_ok(src.device, rows):
             ent, rtab = self.entity_encoder, self.relation_encoder
-            pos_s, neg_s = gnn_ops.kg_score(ent.weight, rtab.weight, ent._rows(src), ent._rows(dst),
-                                            rtab._rows(rel), ent._rows(neg), self.fused_kind, self.corrupt, True)
+            if rows is not None:
+                table, s, d, n = rows["entity_encoder"], src, dst, neg
+            else:
+                table, s, d, n = ent.weight, ent._rows(src), ent._rows(dst), ent._rows(neg)
+            pos_s, neg_s = gnn_ops.kg_score(table, rtab.weight, s, d, rtab._rows(rel), n, self.fused_kind,
+                                            self.corrupt, True)
             pos, neg_s = pos_s.view(-1, 1, 1), neg_s.view(pos_s.shape[0], 1, -1)
         else:
-            pos, neg_s = self.energy_scores(*self.generate_embedding(src, dst, neg, rel))
+            pos, neg_s = self.energy_scores(*self.generate_embedding(src, dst, neg, rel, rows=rows))
         return self.loss_fn(pos, neg_s), pos, neg_s
 
-    def generate_embedding(self, src, dst, neg, rel):
+    def generate_embedding(self, src, dst, neg, rel, rows=None):
         raise NotImplementedError
+
+    def _lookup(self, name, rows=None):
+        """the id -> row function of table ``name``: the module itself, or — in a row-sparse
+        step (``rows[name]``: the step's gathered rows) — a gather at the positions the
+        trainer passes instead of ids"""
+        if rows is None or name not in rows:
+            return getattr(self, name)
+        r = rows[name]
+        return lambda p: r[p.reshape(-1)].reshape(*p.shape, r.shape[-1])
+
 
     # score kind of the fused gfx950 kernel (embed.hip kg_fwd / kg_bwd), None = unfused
     fused_kind = None
@@ -142,8 +162,8 @@ class TransE(TransX):
         if type(self).generate_embedding is TransE.generate_embedding:
             self.fused_kind = "l1" if l1 else "l2"
 
-    def generate_embedding(self, src, dst, neg, rel):
-        e = self.entity_encoder
+    def generate_embedding(self, src, dst, neg, rel, rows=None):
+        e = self._lookup("entity_encoder", rows)
         return (self.norm_emb(e(src)), self.norm_emb(e(dst)), self.norm_emb(e(neg)),
                 self.norm_emb(self.relation_encoder(rel)))
 
@@ -158,8 +178,8 @@ class TransH(TransE):
         h = F.normalize(hyper, dim=-1)
         return x - (x * h).sum(-1, keepdim=True) * h
 
-    def generate_embedding(self, src, dst, neg, rel):
-        e = self.entity_encoder
+    def generate_embedding(self, src, dst, neg, rel, rows=None):
+        e = self._lookup("entity_encoder", rows)
         hyper = self.hyper_vector(rel)  # [B, 1, D] broadcasts over negatives
         return (self.projection(e(src), hyper), self.projection(e(dst), hyper), self.projection(e(neg), hyper),
                 self.norm_emb(self.relation_encoder(rel)))
@@ -177,8 +197,8 @@ class TransR(TransX):
         # x [B, k, ent] @ mat [B, ent, rel] -> one batched GEMM per batch (rocBLAS strided batched)
         return F.normalize(torch.bmm(x, mat), dim=-1)
 
-    def generate_embedding(self, src, dst, neg, rel):
-        e = self.entity_encoder
+    def generate_embedding(self, src, dst, neg, rel, rows=None):
+        e = self._lookup("entity_encoder", rows)
         mat = self.transfer_matrix(rel).reshape(-1, self.ent_dim, self.rel_dim)
         return (self.projection(e(src), mat), self.projection(e(dst), mat), self.projection(e(neg), mat),
                 self.norm_emb(self.relation_encoder(rel)))
@@ -194,8 +214,8 @@ class TransD(TransE):
     def projection(x, ent_t, rel_t):
         return F.normalize(x + (x * ent_t).sum(-1, keepdim=True) * rel_t, dim=-1)
 
-    def generate_embedding(self, src, dst, neg, rel):
-        e, et = self.entity_encoder, self.entity_transfer
+    def generate_embedding(self, src, dst, neg, rel, rows=None):
+        e, et = self._lookup("entity_encoder", rows), self._lookup("entity_transfer", rows)
         rt = self.relation_transfer(rel)
         return (self.projection(e(src), et(src), rt), self.projection(e(dst), et(dst), rt),
                 self.projection(e(neg), et(neg), rt), self.norm_emb(self.relation_encoder(rel)))
@@ -221,7 +241,7 @@ class DistMult(TransX):
                                                 + self.relation_encoder.weight.pow(2).sum())
         return loss
 
-    def generate_embedding(self, src, dst, neg, rel):
-        e = self.entity_encoder
+    def generate_embedding(self, src, dst, neg, rel, rows=None):
+        e = self._lookup("entity_encoder", rows)
         return (self.norm_emb(e(src)), self.norm_emb(e(dst)), self.norm_emb(e(neg)),
                 self.norm_emb(self.relation_encoder(rel)))

@@ -17,7 +17,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from euler_amd.models.captured import CapturedTrainer
+from euler_amd.models.captured import CapturedTrainer, RowSparseTableMixin
 from euler_amd.ops import gnn_ops
 
 __all__ = ["IdPairTrainer", "RowSparseIdPairTrainer"]
@@ -89,7 +89,7 @@ def _id_table_module(enc):
     return None
 
 
-class RowSparseIdPairTrainer(IdPairTrainer):
+class RowSparseIdPairTrainer(RowSparseTableMixin, IdPairTrainer):
     """First-order LINE with its one id table row-sharded and row-sparse
     (:class:`~euler_amd.parallel.sparse_table.ShardedTable`): per step the batch's source,
     positive and negative ids are de-duplicated on the device, their rows gathered (from
@@ -97,12 +97,12 @@ class RowSparseIdPairTrainer(IdPairTrainer):
     ``sgns_loss`` runs on the gathered rows, and the row gradients go back to the owners'
     row-sparse Adam / Adagrad / SGD.  Per-step work is independent of |V|; a row that is a
     target and a context in one step gets one merged gradient (the shared-table case the
-    in-place SGNS update cannot take).  Reference: examples/line/line.py:27-71,
-    tf_euler/python/utils/embedding.py:24-68."""
+    in-place SGNS update cannot take).  Table ownership and per-rank shard checkpoints:
+    :class:`~euler_amd.models.captured.RowSparseTableMixin`.  Reference:
+    examples/line/line.py:27-71, tf_euler/python/utils/embedding.py:24-68."""
 
     def __init__(self, model, graph, batch_size, optimizer="adam", learning_rate=0.01, group=None):
         import euler_amd.ops.graph_api as ge
-        from euler_amd.parallel.sparse_table import ShardedTable
 
         mod = _id_table_module(getattr(model, "_target_encoder", None))
         if mod is None or model._context_encoder is not model._target_encoder:
@@ -116,14 +116,8 @@ class RowSparseIdPairTrainer(IdPairTrainer):
         self._ids = torch.as_tensor(np.asarray(ids).astype(np.int64), device=graph.device)
         self._pad_id = int(model.max_id) + 1
         self.mrr = torch.zeros(2, dtype=torch.float64, device=graph.device)
-        opt = optimizer if optimizer in ("adam", "adagrad", "sgd") else "adam"
-        self.id_table = ShardedTable(int(mod.num), int(mod.dim), graph.device, group, opt, learning_rate)
-        with torch.no_grad():
-            w = mod.weight.detach().to(graph.device)
-            t = self.id_table
-            t.weight.copy_(w if getattr(mod, "world", 1) > 1 or w.shape[0] == t.weight.shape[0]
-                           else w[t.global_ids()])
-        self._mod = mod
+        model.to(graph.device)
+        self._adopt_table(model, mod, graph.device, group, optimizer, learning_rate)
         CapturedTrainer.__init__(self, model, graph, graph.device, optimizer, learning_rate)
         self.world = self.id_table.world
 
@@ -164,49 +158,3 @@ class RowSparseIdPairTrainer(IdPairTrainer):
         self.loss_out.copy_(loss.detach())
         return self.loss_out
 
-    # ------------------------------------------------------------------ state
-    def _full(self):
-        return self.id_table.full()
-
-    def _names(self):
-        """every state_dict key of the table (a shared table is listed under both roles)"""
-        return [k for k, v in self.model.state_dict(keep_vars=True).items() if v is self._mod.weight]
-
-    def state_dict(self):
-        sd = {k: v.detach().cpu() for k, v in self.model.state_dict().items()}
-        full = self._full().cpu()
-        for k in self._names():
-            sd[k] = full
-        return sd
-
-    checkpoint_model_state = state_dict
-
-    def logical_params(self):
-        return {k: v.to(self.device) for k, v in self.state_dict().items()}
-
-    def load_logical(self, sd):
-        t = self.id_table
-        with torch.no_grad():
-            for k in self._names():
-                v = sd.get(k)
-                if v is not None:
-                    t.load(v)
-
-    def write_to_model(self, model):
-        with torch.no_grad():
-            w = self._mod.weight
-            w.copy_((self.id_table.weight if w.shape[0] == self.id_table.weight.shape[0] else self._full()).to(w))
-        if model is not self.model:
-            model.load_state_dict(self.model.state_dict(), strict=False)
-
-    def trainer_state(self):
-        st = super().trainer_state()
-        st["id_table"] = self.id_table.slot_state()
-        return st
-
-    def load_trainer_state(self, st):
-        super().load_trainer_state(st)
-        self.id_table.load_slot_state(st.get("id_table"))
-
-    def dp_state_tensors(self):
-        return list(super().dp_state_tensors()) + self.id_table.state_tensors()

@@ -22,7 +22,7 @@ import torch
 import torch.nn.functional as F
 
 from euler_amd.dataflow.device_flow import DeviceRelationFlow
-from euler_amd.models.captured import CapturedTrainer
+from euler_amd.models.captured import CapturedTrainer, RowSparseTableMixin
 from euler_amd.ops import gnn_ops, mp_ops
 
 __all__ = ["UnsupRgcnTrainer", "RowSparseRgcnTrainer", "edge_relations"]
@@ -142,7 +142,7 @@ class _RowsAt(torch.nn.Module):
         return self.rows[self.p].reshape(*ids.shape, self.dim)
 
 
-class RowSparseRgcnTrainer(UnsupRgcnTrainer):
+class RowSparseRgcnTrainer(RowSparseTableMixin, UnsupRgcnTrainer):
     """UnsupRgcnTrainer with the id embedding table row-sharded and row-sparse
     (:class:`~euler_amd.parallel.sparse_table.ShardedTable`): per step the blocks' node set
     (unique by construction, padding collapsed) is gathered from the table — from the
@@ -153,18 +153,15 @@ class RowSparseRgcnTrainer(UnsupRgcnTrainer):
     tf_euler/python/utils/embedding.py:24-68)."""
 
     def __init__(self, model, graph, batch_size, optimizer="adam", learning_rate=0.01, group=None):
-        from euler_amd.parallel.sparse_table import ShardedTable
 
         enc = model.gnn._encoder
         mod = getattr(enc, "embedding", None)
         if mod is None or not hasattr(mod, "num"):
             raise ValueError("RowSparseRgcnTrainer needs the encoder's id embedding")
-        opt = optimizer if optimizer in ("adam", "adagrad", "sgd") else "adam"
-        self.id_table = ShardedTable(int(mod.num), int(mod.dim), graph.device, group, opt, learning_rate)
-        self.id_table.load(mod.weight.detach())
-        self._mod, self._enc = mod, enc
-        self._names = [k for k, v in model.state_dict(keep_vars=True).items() if v is mod.weight]
-        enc.embedding = _RowsAt(mod.num, mod.dim)
+        model.to(graph.device)
+        self._adopt_table(model, mod, graph.device, group, optimizer, learning_rate)
+        self._enc = enc
+        enc.embedding = _RowsAt(mod.num, mod.dim)  # position lookups into the step's gathered rows
         self._pending = None
         super().__init__(model, graph, batch_size, optimizer, learning_rate)
         self.world = self.id_table.world
@@ -213,47 +210,7 @@ class RowSparseRgcnTrainer(UnsupRgcnTrainer):
         return self.loss_out
 
     # ------------------------------------------------------------------ state
-    def state_dict(self):
-        sd = {k: v.detach().cpu() for k, v in self.model.state_dict().items()}
-        full = self.id_table.full().cpu()
-        for k in self._names:
-            sd[k] = full
-        return sd
-
-    checkpoint_model_state = state_dict
-
-    def logical_params(self):
-        return {k: v.to(self.device) for k, v in self.state_dict().items()}
-
-    def load_logical(self, sd):
-        with torch.no_grad():
-            own = self.model.state_dict()
-            for k, v in sd.items():
-                if k in own:
-                    own[k].copy_(torch.as_tensor(v).to(own[k]))
-        for k in self._names:
-            if k in sd:
-                self.id_table.load(sd[k])
-
-    def write_to_model(self, model):
-        with torch.no_grad():
-            w = self._mod.weight
-            w.copy_(self.id_table.full().to(w))
-        if model is not self.model:
-            model.load_state_dict(self.state_dict(), strict=False)
-
     def finish(self):
-        self.write_to_model(self.model)
+        """the encoder's own id embedding back in place, holding the trained table"""
         self._enc.embedding = self._mod
-
-    def trainer_state(self):
-        st = super().trainer_state()
-        st["id_table"] = self.id_table.slot_state()
-        return st
-
-    def load_trainer_state(self, st):
-        super().load_trainer_state(st)
-        self.id_table.load_slot_state(st.get("id_table"))
-
-    def dp_state_tensors(self):
-        return list(super().dp_state_tensors()) + self.id_table.state_tensors()
+        RowSparseTableMixin.finish(self)

@@ -35,11 +35,13 @@ __all__ = ["UnsupervisedGraphSage", "BaseNode2Vec", "DeepWalk", "Node2Vec", "Lin
 
 
 class IdEncoder(nn.Module):
-    """id -> embedding, optionally row-sharded over the process group."""
+    """id -> embedding, optionally row-sharded over the process group.  Both forms hold
+    ``max_id + 2`` rows: row ``max_id + 1`` is the trainable pad row of the walks' and
+    samplers' default node (reference ``max_id + 1``), never an alias of node ``max_id``."""
 
     def __init__(self, max_id, dim, sharded=False):
         super().__init__()
-        self.table = ShardedEmbedding(max_id, dim) if sharded else None
+        self.table = ShardedEmbedding(max_id + 1, dim) if sharded else None
         self.enc = None if sharded else encoders.ShallowEncoder(dim=dim, feature_idx=-1, max_id=max_id,
                                                                  embedding_dim=dim, combiner="add")
 

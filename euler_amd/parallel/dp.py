@@ -83,8 +83,10 @@ def broadcast_module(module: torch.nn.Module, src: int = 0, group=None):
     broadcast per dtype)."""
     if not is_distributed():
         return
+    # row-sharded tables (ShardedEmbedding under 2+ ranks) hold different rows per rank
     tensors = [t for t in list(module.parameters()) + list(module.buffers())
-               if not isinstance(t, torch.nn.parameter.UninitializedParameter)]
+               if not isinstance(t, torch.nn.parameter.UninitializedParameter)
+               and not getattr(t, "_euler_sharded", False)]
     by_dtype = {}
     for t in tensors:
         by_dtype.setdefault((t.dtype, t.device), []).append(t)
@@ -212,6 +214,8 @@ class GradSync:
             st["ready"] = 0
 
     def remove(self):
+        """detach the hooks and drop the bucket buffers (a trainer that syncs itself)"""
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        self._buckets, self._state, self.enabled = [], [], False

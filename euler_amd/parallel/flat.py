@@ -48,6 +48,8 @@ class FlatParams:
             o += n
 
     def zero_grad(self):
+        if self.grad.numel() == 0:
+            return
         if use_hip(self.grad):
             # one zero_kernel launch (a kernel node in captured steps; EULER_AMD_ZERO_MEMSET=1
             # makes it a hipMemsetAsync node instead: docs/DESIGN.md §9, tests/test_graph_memset.py)
@@ -90,6 +92,8 @@ class FlatOptimizer:
 
     def step(self, grad_scale: float = 1.0):
         f = self.flat
+        if f.flat.numel() == 0:  # every parameter lives elsewhere (row-sparse tables)
+            return
         w0, w1, wd2 = self.decay_range
         if use_hip(f.flat):
             hip().flat_optim_(f.flat, f.grad, self.m, self.v, self.step_count, self.lr, self.b1, self.b2,

@@ -73,23 +73,26 @@ class StaticHandle:
 
 class ShardedTable:
     def __init__(self, num_rows, dim, device, group=None, optimizer="adam", lr=0.01, init_std=0.1, seed=0,
-                 beta1=0.9, beta2=0.999, eps=1e-8, force_comm=False, wire_dtype="fp32"):
+                 beta1=0.9, beta2=0.999, eps=1e-8, force_comm=False, wire_dtype="fp32", init="normal"):
         self.num_rows, self.dim = int(num_rows), int(dim)
         if wire_dtype not in ("fp32", "bf16"):
             raise ValueError("wire_dtype must be fp32 or bf16")
         self.wire = torch.bfloat16 if wire_dtype == "bf16" else torch.float32
         self.group = group
-        init = dist.is_available() and dist.is_initialized()
-        dist_on = init and dist.get_world_size(group) > 1
+        pg = dist.is_available() and dist.is_initialized()
+        dist_on = pg and dist.get_world_size(group) > 1
         self.world = dist.get_world_size(group) if dist_on else 1
         self.rank = dist.get_rank(group) if dist_on else 0
         # collectives on (force_comm: also with one rank, to exercise the all-to-all path)
-        self.comm = dist_on or (init and force_comm)
+        self.comm = dist_on or (pg and force_comm)
         self.device = torch.device(device)
         local = max(0, math.ceil((self.num_rows - self.rank) / self.world))
         g = torch.Generator(device=self.device).manual_seed(int(seed) * 131 + self.rank)
         self.weight = torch.empty(local, self.dim, device=self.device)
-        self.weight.normal_(0.0, init_std, generator=g)
+        if init == "normal":
+            self.weight.normal_(0.0, init_std, generator=g)
+        elif init is not None:  # None: the caller fills every row (e.g. from a model's table)
+            raise ValueError("init must be 'normal' or None")
         self.kind = _KINDS[optimizer]
         # optimizer slots: Adam keeps m and v, Adagrad only the accumulator v, SGD none
         # (the kernel never touches an unused slot, so it aliases a used one or the weight)
@@ -392,6 +395,49 @@ class ShardedTable:
         self.m.copy_(torch.as_tensor(s["m"]).to(self.m))
         self.v.copy_(torch.as_tensor(s["v"]).to(self.v))
         self.step.fill_(int(s["step"]))
+
+    # ------------------------------------------------------------------ per-rank checkpoints
+    def slot_kinds(self):
+        """the optimizer slots this table keeps (Adam: m, v; Adagrad: v; SGD: none)"""
+        return {0: ("m", "v"), 1: ("v",), 2: ()}[self.kind]
+
+    def shard_tensors(self, lo=0, hi=None):
+        """kind -> local rows [lo, hi) of the weight and of every optimizer slot"""
+        out = {"weight": self.weight[lo:hi]}
+        for k in self.slot_kinds():
+            out[k] = getattr(self, k)[lo:hi]
+        return out
+
+    def save_shard(self, ckpt_path, name, num=None, lo=0, rows_of=None):
+        """write this rank's rows (and their slots) next to ``ckpt_path``
+        (parallel/shard_io.py); ``lo``: first local row of a table slice that is itself
+        ``mod``-sharded (a half of a two-table layout whose offset is a multiple of world),
+        ``num``: global rows of that slice"""
+        from euler_amd.parallel.shard_io import save_rows
+
+        num = self.num_rows if num is None else int(num)
+        n_local = -(-num // self.world)
+        return save_rows(ckpt_path, name, self.shard_tensors(lo, lo + n_local), num, self.world, self.rank)
+
+    def load_shard(self, dirname, metas, lo=0, n_local=None, name="table"):
+        """fill local rows [lo, lo + n_local) (global slice rows ``j * world + rank``) and
+        their slots from a checkpoint written by any number of ranks; slots the checkpoint
+        does not hold (another optimizer) restart at zero"""
+        import logging
+
+        from euler_amd.parallel.shard_io import read_rows
+
+        n_local = self.weight.shape[0] - lo if n_local is None else int(n_local)
+        rows = torch.arange(n_local, dtype=torch.int64) * self.world + self.rank
+        with torch.no_grad():
+            read_rows(dirname, metas, "weight", rows, self.weight[lo:lo + n_local])
+            for k in self.slot_kinds():
+                dst = getattr(self, k)[lo:lo + n_local]
+                if not read_rows(dirname, metas, k, rows, dst):
+                    dst.zero_()
+                    logging.getLogger("euler_amd.estimator").warning(
+                        "%s: the checkpoint has no '%s' optimizer slot (another optimizer); it restarts at zero",
+                        name, k)
 
     def state_tensors(self):
         """every tensor a training step changes (rollback snapshots, re-sync broadcasts)"""

@@ -40,22 +40,42 @@ def _model(ds, cls=Z.DeepWalk, **kw):
     return cls("train", ["train"], ds.max_node_id, 8, walk_len=3, num_negs=3, **kw)
 
 
-def test_table_round_trip(cora, tmp_path):
-    """model tables -> trainer table halves -> model tables is the identity"""
+@pytest.mark.parametrize("sharded", [False, True])
+def test_model_tables_are_views_of_the_trainer_halves(cora, tmp_path, sharded):
+    """the model's two id tables keep their values and become views of the trainer's table
+    halves (no second copy of a table while the trainer owns it); per-rank shard files
+    round-trip the rows and the optimizer slots"""
     from euler_amd.graph.device_graph import DeviceGraph
     from euler_amd.models.deepwalk_step import DeepWalkEstimatorTrainer
 
-    m = _model(cora)
+    m = _model(cora, sharded=sharded)
     est = NodeEstimator(m, _params(cora, tmp_path, "cpu"))
     est._prepare(est.get_train_from_input(32, est.params))
     before = {k: v.clone() for k, v in m.state_dict().items()}
     tr = DeepWalkEstimatorTrainer(m, DeviceGraph.from_engine(device="cpu"), 32)
-    for v in m.state_dict().values():
-        v.zero_()
-    tr.write_to_model(m)
-    ids = torch.as_tensor(np.asarray(tr.graph.ids).astype(np.int64))
-    for k, v in m.state_dict().items():
-        assert torch.equal(v[ids], before[k][ids]) and torch.equal(v[-1], before[k][-1])
+    t = tr.inner.table
+    assert len(tr._keys) == 2
+    for h, key in enumerate(tr._keys):
+        w = m.state_dict()[key]
+        assert w.shape[0] == cora.max_node_id + 2  # the pad row max_id + 1 included
+        assert torch.equal(w, before[key])
+        assert w.data_ptr() == t.weight[h * tr._offw].data_ptr()
+    for _ in range(3):
+        tr.step()
+    trained = {k: v.clone() for k, v in m.state_dict().items()}
+    assert any(not torch.equal(trained[k], before[k]) for k in tr._keys)
+    slots = {k: getattr(t, k).clone() for k in t.slot_kinds()}
+    ck = str(tmp_path / "model.ckpt-3.pt")
+    metas = {k: [v] for k, v in tr.checkpoint_shards(ck).items()}
+    with torch.no_grad():
+        t.weight.zero_()
+        for k in t.slot_kinds():
+            getattr(t, k).zero_()
+    tr.load_shards(str(tmp_path), metas)
+    for k in tr._keys:
+        assert torch.equal(m.state_dict()[k], trained[k])
+    for k, v in slots.items():
+        assert torch.equal(getattr(t, k), v)
 
 
 @pytest.mark.parametrize("cls,kw", [(Z.DeepWalk, {}), (Z.Node2Vec, {"walk_p": 0.5, "walk_q": 2.0})])
@@ -177,4 +197,11 @@ def test_line_first_order_row_sparse_first_step_equals_dense(cora, tmp_path):
     from euler_amd.estimator.base import latest_checkpoint
 
     ck = torch.load(latest_checkpoint(str(tmp_path / "ckpt")), map_location="cpu", weights_only=True)
-    assert torch.equal(ck["model"]["_target_encoder.embedding.weight"], after)
+    # the table lives in this rank's shard files, listed under both role names
+    assert "_target_encoder.embedding.weight" not in ck["model"]
+    assert set(ck["shards"]) >= {"_target_encoder.embedding.weight", "_context_encoder.embedding.weight"}
+    m2 = _line(cora, order=1)
+    est2 = NodeEstimator(m2, _params(cora, tmp_path, "cpu", device_graph=False))
+    est2._prepare(est2.get_train_from_input(32, est2.params))
+    assert est2.restore()
+    assert torch.equal(m2.state_dict()["_target_encoder.embedding.weight"], after)

@@ -476,3 +476,66 @@ def test_bounded_caps_are_smaller_and_overflow_regrows_cpu(tmp_path):
     assert r1["step"] == 12 and e1.flow_regrows >= 1 and e0.flow_regrows == 0
     assert all(c[0] > 256 for c in e1.device_trainer.flow.caps)
     torch.testing.assert_close(p1, p0, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("model", ["fastgcn", "adaptivegcn"])
+def test_layer_sampled_gcn_evaluate_matches_engine_path_cpu(tmp_path, model):
+    """FastGCN / AdaptiveGCN sample their layers (reference fast_dataflow / LayerwiseDataFlow):
+    after device-path training, evaluate with device_graph=True must take the engine path's
+    sampled blocks, not an exact full-neighbourhood block, so both report the same metrics"""
+    import euler_amd as ea
+    from euler_amd.tools.runner import main
+
+    base = ["--dataset", "ppi", "--scale", "0.05", "--batch_size", "16", "--log_steps", "3", "--device", "cpu",
+            "--seed", "1", "--model_dir", str(tmp_path / model), "--learning_rate", "0.01", "--total_step", "6"]
+    main(base + ["--device_graph"], model=model)
+    res = {}
+    for dg in (True, False):
+        ea.set_seed(7)
+        torch.manual_seed(7)
+        res[dg] = main(base + ["--run_mode", "evaluate"] + (["--device_graph"] if dg else []), model=model)
+    assert res[True] and res[True] == res[False]
+
+
+def test_scalable_encoder_is_not_trained_as_plain_gcn_cpu(tmp_path, caplog):
+    """a ScalableGCNEncoder model is a GCNEncoder subclass: no device trainer without the
+    stores' protocol may take it (it would silently train a full multi-hop GCN without
+    stores); without a store-aware trainer the estimator logs and trains on the engine path"""
+    import logging
+
+    import euler_amd as ea
+    from euler_amd.dataset import get_dataset
+    from euler_amd.estimator import NodeEstimator
+    from euler_amd.estimator.device_trainers import NoDeviceTrainer, REGISTRY, STORE_AWARE
+    from euler_amd.mp_utils.models import SuperviseModel
+    from euler_amd.utils import encoders as E
+
+    ds = get_dataset("ppi", data_dir=str(tmp_path / "ppi"), scale=0.05)
+    ds.load_graph()
+    ea.set_seed(3)
+
+    class M(SuperviseModel):
+        def __init__(self):
+            super().__init__(ds.label_idx, ds.label_dim)
+            self._encoder = E.ScalableGCNEncoder(["train"], 2, 16, feature_idx=ds.feature_idx,
+                                                 feature_dim=ds.feature_dim, max_id=ds.max_node_id)
+
+        def embed(self, n_id):
+            return self._encoder(n_id)
+
+    m = M()
+    tnt = ds.train_node_type[0] if isinstance(ds.train_node_type, list) else ds.train_node_type
+    p = {"model_dir": str(tmp_path / "ck"), "batch_size": 16, "total_step": 3, "log_steps": 1, "device": "cpu",
+         "device_graph": True, "train_node_type": tnt, "seed": 1}
+    est = NodeEstimator(m, p)
+    with caplog.at_level(logging.WARNING, logger="euler_amd.estimator"):
+        res = est.train()
+    assert np.isfinite(res["loss"]) and getattr(est, "device_trainer", None) is None or \
+        getattr(est.device_trainer, "device_trainer_kind", None) in STORE_AWARE
+    if not any(n in STORE_AWARE for n, _, _ in REGISTRY):
+        assert "engine path" in caplog.text
+    assert float(m._encoder.stores(0).abs().sum()) > 0
+    from euler_amd.estimator.device_trainers import build_device_trainer
+    if not any(n in STORE_AWARE for n, _, _ in REGISTRY):
+        with pytest.raises(NoDeviceTrainer):
+            build_device_trainer(est, m, None)

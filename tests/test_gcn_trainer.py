@@ -247,6 +247,23 @@ def test_fused_gcn_overflow_regrows(tmp_path, monkeypatch):
     est = box["est"]
     assert r["step"] == 24 and math.isfinite(r["loss"]) and est.flow_regrows >= 1
     assert all(c[0] > 256 for c in est.device_trainer.flow.caps)
+    # the overflowed chunks (the capture's eager warm-up included) were rolled back: the
+    # run equals one with exact caps from the same seed (same draws, no truncated block)
+    w_small = {k: v.detach().float().cpu().clone() for k, v in est.model.state_dict().items()}
+
+    def spy_exact(self):
+        box["est"] = self
+        self.params["device_flow_caps"] = "exact"
+        return orig(self)
+
+    monkeypatch.setattr(eb.BaseEstimator, "_train_device_graph", spy_exact)
+    r2 = main(["--dataset", "ppi", "--scale", "0.05", "--batch_size", "64", "--log_steps", "8", "--device", "cuda",
+               "--seed", "1", "--model_dir", str(tmp_path / "ckpt_exact"), "--device_graph", "--total_step", "24"],
+              model="gcn")
+    assert box["est"].flow_regrows == 0
+    assert abs(r2["loss"] - r["loss"]) <= 1e-3 * max(1.0, abs(r2["loss"]))
+    for k, v in box["est"].model.state_dict().items():
+        torch.testing.assert_close(v.detach().float().cpu(), w_small[k], rtol=2e-3, atol=2e-4)
 
 
 @pytest.mark.gpu

@@ -156,9 +156,56 @@ def test_edge_estimator_row_sparse_tables_cpu(fb, tmp_path):
     # the model's own module is back, trained
     from euler_amd.utils.layers import Embedding
 
-    assert isinstance(m.entity_encoder, Embedding)
+    assert isinstance(m.entity_encoder, Embedding) and m.entity_encoder.weight.requires_grad
+    # the checkpoint keeps the table in this rank's shard files (rows + Adam slots), not in
+    # the .pt; an engine-path restore reads it back
     ck = torch.load(ea_latest(tmp_path), map_location="cpu", weights_only=True)
-    assert torch.equal(ck["model"]["entity_encoder.weight"], m.entity_encoder.weight.detach())
+    assert "entity_encoder.weight" not in ck["model"] and set(ck["shards"]["entity_encoder.weight"]["files"]) == \
+        {"weight", "m", "v"}
+    m2 = _model(fb)
+    est2 = EdgeEstimator(m2, _params(tmp_path, "cpu", device_graph=False))
+    assert est2.restore()
+    assert torch.equal(m2.entity_encoder.weight.detach(), m.entity_encoder.weight.detach())
+    assert torch.equal(m2.relation_encoder.weight.detach(), m.relation_encoder.weight.detach())
+
+
+def test_row_sparse_kg_resume_equals_continuous_run(fb, tmp_path):
+    """20 steps + resume to 40 (per-rank shard files: rows AND sparse Adam slots, the flat
+    buffer's slots, the sampler counter) ends on exactly the tables of one 40-step run"""
+    runs = {}
+    for name, legs in (("cont", (40,)), ("resumed", (20, 40))):
+        for total in legs:
+            m = _model(fb)
+            est = EdgeEstimator(m, _params(tmp_path / name, "cpu", row_sparse_tables=True, total_step=total))
+            est.train()
+        runs[name] = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    for k, v in runs["cont"].items():
+        assert torch.equal(v, runs["resumed"][k]), k
+
+
+def test_row_sparse_kg_refuses_distmult_l2(fb, tmp_path):
+    """DistMult's L2 term spans every entity row each step: a row-sparse table cannot
+    compute it (explicit request or sharded table: refused; auto: the dense trainer)"""
+    from euler_amd.models.kg_trainer import RowSparseKGTrainer, TripleTable
+
+    args = ("train", "train", fb.max_node_id, fb.max_edge_id, 16, 16)
+    t = TripleTable.from_engine("train", node_type="train", seed=3, device="cpu")
+    with pytest.raises(ValueError, match="l2_regular"):
+        RowSparseKGTrainer(Z.DistMult(*args, num_negs=4, l2_regular=True), t, 64)
+    with pytest.raises(ValueError, match="l2_regular"):
+        EdgeEstimator(Z.DistMult(*args, num_negs=4, l2_regular=True),
+                      _params(tmp_path, "cpu", row_sparse_tables=True)).train()
+    import euler_amd.estimator.device_trainers as dt
+
+    old = dt.ROW_SPARSE_AUTO_ROWS
+    dt.ROW_SPARSE_AUTO_ROWS = 1  # every table counts as large: auto would pick row-sparse
+    try:
+        est = EdgeEstimator(Z.DistMult(*args, num_negs=4, l2_regular=True), _params(tmp_path / "auto", "cpu",
+                                                                                  total_step=4))
+        assert np.isfinite(est.train()["loss"])
+        assert type(est.device_trainer).__name__ == "KGTrainer"
+    finally:
+        dt.ROW_SPARSE_AUTO_ROWS = old
 
 
 def ea_latest(tmp_path):

@@ -841,3 +841,85 @@ def test_row_sparse_kg_two_ranks_matches_dense_first_step(tmp_path):
     res = _run(_worker_row_sparse_vs_dense_kg, str(tmp_path))
     assert not [r for r in res if r[1] == "error"], res
     assert len(res) == 2 and all(r[2] for r in res), res
+
+
+def _worker_dw_shard_ckpt(rank, world, port, q, data_dir, model_dir, out_dir, total):
+    """DeepWalk sharded=True through NodeEstimator(device_graph=True) at this world size:
+    trains to ``total`` (or, already trained, only restores the per-rank shard checkpoint)
+    and dumps this rank's model rows with their weight and sparse-optimizer slots"""
+    try:
+        _init(rank, world, port)
+        import euler_amd as ea
+        from euler_amd import models as Z
+        from euler_amd.dataset import get_dataset
+        from euler_amd.estimator import NodeEstimator
+
+        ds = get_dataset("cora", data_dir=data_dir, scale=0.08)
+        ds.load_graph()
+        ea.set_seed(3)
+        tnt = ds.train_node_type[0] if isinstance(ds.train_node_type, list) else ds.train_node_type
+        torch.manual_seed(0)
+        m = Z.DeepWalk("train", ["train"], ds.max_node_id, 8, walk_len=3, num_negs=3, sharded=True)
+        est = NodeEstimator(m, {"model_dir": model_dir, "batch_size": 32, "total_step": total, "optimizer": "adam",
+                                "learning_rate": 0.02, "log_steps": 5, "train_node_type": tnt, "device": "cpu",
+                                "device_graph": True, "seed": 11})
+        est.train()
+        tr = est.device_trainer
+        t = tr.inner.table
+        rows = tr._half_rows()
+        keep = rows < tr.num
+        dump = {"step": int(t.step.item()), "global_step": est.global_step}
+        for h, key in enumerate(tr._keys):
+            sl = slice(h * tr._offw, (h + 1) * tr._offw)
+            dump[key] = {"rows": rows[keep].clone(), "weight": t.weight[sl][keep].clone(),
+                         "m": t.m[sl][keep].clone(), "v": t.v[sl][keep].clone(),
+                         "model": m.state_dict()[key].clone()}
+        torch.save(dump, os.path.join(out_dir, "w%d_r%d.pt" % (world, rank)))
+        files = sorted(f for f in os.listdir(model_dir) if ".npy" in f)
+        q.put((rank, "dw_shard", True, files))
+        if dist.is_initialized():
+            dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_deepwalk_shard_checkpoint_reshards_rows_and_slots(tmp_path):
+    """per-rank shard checkpoints (parallel/shard_io.py): saved by 2 ranks, restored by 1
+    and by 4 ranks with identical tables AND sparse-optimizer slots — every rank reads only
+    its own rows, no all-gather; the model's tables are views of the trainer's shard"""
+    out = tmp_path / "dump"
+    out.mkdir()
+    ck = str(tmp_path / "ckpt")
+    args = (str(tmp_path / "cora"), ck, str(out))
+    res = _run(_worker_dw_shard_ckpt, *args, 10, world=2)
+    assert not [r for r in res if r[1] == "error"], res
+    files = res[0][3]
+    # each rank wrote its rows and its Adam slots of both tables (3 kinds x 2 tables x 2 ranks)
+    assert len(files) == 12 and any("rank1" in f for f in files), files
+
+    def full(world):
+        parts = [torch.load(out / ("w%d_r%d.pt" % (world, r)), weights_only=True) for r in range(world)]
+        tabs = {}
+        for key in [k for k in parts[0] if isinstance(parts[0][k], dict)]:
+            n = sum(int(p[key]["rows"].numel()) for p in parts)
+            tab = {k: torch.full((n, 8), float("nan")) for k in ("weight", "m", "v")}
+            for p in parts:
+                assert torch.equal(p[key]["model"], p[key]["weight"][: p[key]["model"].shape[0]])
+                for k in tab:
+                    tab[k][p[key]["rows"]] = p[key][k]
+            tabs[key] = tab
+        return tabs, {p["step"] for p in parts}, {p["global_step"] for p in parts}
+
+    ref, steps, gsteps = full(2)
+    assert steps == {10} and gsteps == {10}
+    for world in (1, 4):
+        res = _run(_worker_dw_shard_ckpt, *args, 10, world=world)
+        assert not [r for r in res if r[1] == "error"], res
+        got, steps, gsteps = full(world)
+        assert steps == {10} and gsteps == {10}
+        for key, tab in ref.items():
+            for k in ("weight", "m", "v"):
+                assert not torch.isnan(tab[k]).any()
+                assert torch.equal(got[key][k], tab[k]), (world, key, k)
