@@ -15,8 +15,9 @@ of a node's edges stay in its community) with 100K edges held out; link-predicti
 of held-out edges vs random pairs (cosine of target embeddings) at init and during
 training goes into the JSON.
 
-Usage:  python benchmarks/bench_deepwalk.py [--steps K] [--warmup W]
+Usage:  python benchmarks/bench_deepwalk.py [--steps K] [--warmup W] [--gpus N]
         torchrun --nproc-per-node N benchmarks/bench_deepwalk.py   (one rank per GPU)
+``--gpus N`` without torchrun starts N ranks itself (parallel/launch.py maybe_spawn).
 """
 from __future__ import annotations
 
@@ -26,8 +27,12 @@ import os
 import sys
 import time
 
-import torch
-import torch.distributed as dist
+# dmabuf IPC (the only mode the host driver supports): RCCL fails without it; set before
+# torch loads HIP, here as in bench.py and parallel/launch.py's children
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
@@ -78,6 +83,7 @@ def link_prediction_eval(args, dev):
 
 def main(argv=None):
     p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    p.add_argument("--gpus", type=int, default=None, help="ranks, one per GPU (default: WORLD_SIZE or 1)")
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--num-nodes", type=int, default=100_000_000)
@@ -104,12 +110,15 @@ def main(argv=None):
     p.add_argument("--eval-steps", type=int, default=3000)
     p.add_argument("--eval-lr", type=float, default=0.05)
     args = p.parse_args(argv)
+    from euler_amd.parallel.launch import maybe_spawn, require_gpu
 
+    rc = maybe_spawn(args.gpus, sys.argv[1:] if argv is None else argv, __file__)
+    if rc is not None:
+        return rc
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if not torch.cuda.is_available():
-        raise SystemExit("bench_deepwalk.py needs a GPU")
+    require_gpu(local_rank, world, "bench_deepwalk.py")
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
     dist_on = world > 1 or args.force_dist
@@ -175,6 +184,8 @@ def main(argv=None):
             "value": round(pairs / el, 1),
             "unit": "pairs/s",
             "n_gpus": world,
+            "ranks": world,
+            "parallelism": f"dp{world}+sharded-emb",
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(el * 1e3 / args.steps, 3),
@@ -200,4 +211,4 @@ def main(argv=None):
 
 
 if __name__ == "__main__":
-    main()
+    raise SystemExit(main())

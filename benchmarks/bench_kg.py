@@ -19,7 +19,8 @@ Full-graph encoder every step (the graph is small; the relation transform over a
 483K edges is the hot op).  DP: bucketed RCCL all-reduce of the dense gradients
 overlapped with the backward (parallel/dp.py GradSync).
 
-Usage: python benchmarks/bench_kg.py [--steps K] [--warmup W];  torchrun for N GPUs.
+Usage: python benchmarks/bench_kg.py [--steps K] [--warmup W] [--gpus N];  or torchrun for N GPUs
+(``--gpus N`` without torchrun starts N ranks itself: parallel/launch.py maybe_spawn).
 """
 from __future__ import annotations
 
@@ -29,8 +30,12 @@ import os
 import sys
 import time
 
-import torch
-import torch.distributed as dist
+# dmabuf IPC (the only mode the host driver supports): RCCL fails without it; set before
+# torch loads HIP, here as in bench.py and parallel/launch.py's children
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
@@ -49,6 +54,7 @@ def synthetic_kg(num_ent, num_rel, num_triples, seed, device, num_test=5000):
 
 def main(argv=None):
     p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    p.add_argument("--gpus", type=int, default=None, help="ranks, one per GPU (default: WORLD_SIZE or 1)")
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--num-ent", type=int, default=14951)
@@ -90,7 +96,11 @@ def main(argv=None):
     p.add_argument("--eval-after", type=int, default=2000,
                    help="keep training (untimed) to this many steps, then rank the held-out triples")
     args = p.parse_args(argv)
+    from euler_amd.parallel.launch import maybe_spawn, require_gpu
 
+    rc = maybe_spawn(args.gpus, sys.argv[1:] if argv is None else argv, __file__)
+    if rc is not None:
+        return rc
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -98,13 +108,15 @@ def main(argv=None):
         dev = torch.device("cpu")
         args.no_graph = True
     else:
-        if not torch.cuda.is_available():
-            raise SystemExit("bench_kg.py needs a GPU (or --device cpu)")
+        require_gpu(local_rank, world, "bench_kg.py (or --device cpu)")
         dev = torch.device("cuda", local_rank)
         torch.cuda.set_device(dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if dev.type == "cuda":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
     from euler_amd.parallel.flat import FlatOptimizer, FlatParams
 
     norm = bool(args.normalize)
@@ -299,6 +311,8 @@ def main(argv=None):
             "value": round(args.batch * world * args.steps / el, 1),
             "unit": "triples/s",
             "n_gpus": world,
+            "ranks": world,
+            "parallelism": f"dp{world}",
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(el * 1e3 / args.steps, 3),
@@ -329,4 +343,4 @@ def main(argv=None):
 
 
 if __name__ == "__main__":
-    main()
+    raise SystemExit(main())

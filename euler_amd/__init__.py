@@ -11,6 +11,14 @@ Layers:
 """
 __version__ = "0.1.0"
 
+import os as _os
+
+# dmabuf IPC, the only mode the host driver supports: RCCL and the xGMI all-reduce's peer
+# mappings fail without it ("hipIpcGetMemHandle: invalid argument").  Set before the
+# package (or a script importing it first) loads torch / HIP, so every entry point —
+# tools/runner.py, the examples, the benchmarks under torchrun — gets it.
+_os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
 from euler_amd.ops.base import (  # noqa: F401
     GraphBuilder, Module, get_engine, initialize_embedded_graph, initialize_graph, initialize_shared_graph, set_seed,
     start, start_service, synthetic_graph, use_graph)

@@ -92,6 +92,20 @@ def id_file_batches(path, batch_size, parse=int, shard=(0, 1)):
         yield batch
 
 
+def _memory_peaks(device):
+    """peak HBM allocated by this process and its peak host resident set (VmHWM), GiB"""
+    hbm = torch.cuda.max_memory_allocated(device) / 2 ** 30 if device.type == "cuda" else 0.0
+    rss = 0.0
+    try:
+        with open("/proc/self/status") as f:
+            for line in f:
+                if line.startswith("VmHWM:"):
+                    rss = int(line.split()[1]) / 2 ** 20
+    except OSError:
+        pass
+    return {"peak_hbm_gib": round(hbm, 2), "peak_host_rss_gib": round(rss, 2)}
+
+
 def dist_backend():
     import torch.distributed as dist
 
@@ -171,9 +185,12 @@ class BaseEstimator:
             if callable(fn) and m is not self.model:
                 fn()
 
-    def _prepare(self, source):
+    def _prepare(self, source, build_optimizer=True):
         """Move the model, materialise lazy parameters with one no-grad pass,
-        broadcast rank 0's initial weights, build the optimizer and gradient sync."""
+        broadcast rank 0's initial weights, build the optimizer and gradient sync
+        (``build_optimizer=False``: a device trainer runs its own optimizer — a torch
+        Adagrad would allocate its accumulators for every parameter right here, 95 GiB for
+        a 100M-node DeepWalk)."""
         self.model.to(self.device)
         if any(isinstance(p, nn.parameter.UninitializedParameter) for p in self.model.parameters()):
             was = self.model.training
@@ -191,6 +208,9 @@ class BaseEstimator:
                 if callable(getattr(m, "use_sharded_stores", None)) and not getattr(m, "_sharded", None):
                     m.use_sharded_stores()
         params = [p for p in self.model.parameters() if p.requires_grad]
+        if not build_optimizer:
+            self.optimizer, self._sync = None, None
+            return
         name = self.params.get("optimizer", "adam")
         self.optimizer = get_optimizer(name)(params, self.params.get("learning_rate", 0.001))
         dense = [p for p in params if not is_sharded(p)]
@@ -507,7 +527,10 @@ class BaseEstimator:
         log_steps = int(self.params.get("log_steps", 100))
         save_steps = int(self.run_config.get("save_checkpoints_steps", self.params.get("save_checkpoints_steps", 0))
                          or 0)
-        first = self.get_train_from_input(self.train_input_fn(), self.params)
+        # a graph from params["device_graph_factory"] has no engine to draw a first batch from
+        # (it only materialises lazy layers, which such models must not have)
+        first = None if self.params.get("device_graph_factory") else \
+            self.get_train_from_input(self.train_input_fn(), self.params)
         self.model.train()
         tr = self._device_graph_trainer(first)
         self.device_trainer = tr
@@ -599,14 +622,17 @@ class BaseEstimator:
                 rate = (self.global_step - n0) * bs * self.world / dt
                 mname = getattr(tr, "metric_name", "f1")
                 last = {"step": self.global_step, "loss": loss, mname: tr.metric(), "samples_per_sec": rate}
+                last.update(_memory_peaks(self.device))
                 tr.reset_metric()
                 if self.rank == 0:
-                    log.info("step = %d, loss = %.6f, %s = %.6f (%.1f samples/s, device path)", self.global_step,
-                             loss, mname, last[mname], rate)
+                    log.info("step = %d, loss = %.6f, %s = %.6f (%.1f samples/s, device path; peak HBM %.1f GiB, "
+                             "peak host RSS %.1f GiB)", self.global_step, loss, mname, last[mname], rate,
+                             last["peak_hbm_gib"], last["peak_host_rss_gib"])
                 t0, n0 = time.time(), self.global_step
             if save_steps and self.global_step % save_steps == 0 and self.global_step < total:
                 self._device_save(tr)
-        self._device_save(tr)
+        if self.params.get("save_final_checkpoint", True):
+            self._device_save(tr)
         # graphs holding captured collectives keep the communicator busy: drop them before
         # the final barrier / process-group teardown
         self._device_release(tr)

@@ -61,8 +61,16 @@ class Ctx:
         return torch.float32 if self.params.get("device_feature_dtype", "bf16") == "fp32" else torch.bfloat16
 
     def upload(self, default_node_type=-1, features=(), feature_dims=(), label=None, label_dim=None, node_type=None):
-        """the engine's graph (structure + the named dense feature / label columns) in HBM"""
+        """the engine's graph (structure + the named dense feature / label columns) in HBM;
+        ``params["device_graph_factory"](rank, device)`` supplies it instead (e.g. a
+        ``DeviceGraph.synthetic`` 100M-node graph generated straight in HBM, no engine)"""
         from euler_amd.graph.device_graph import DeviceGraph
+
+        factory = self.params.get("device_graph_factory")
+        if callable(factory):
+            g = factory(self.est.rank, self.est.device)
+            g.manual_seed(self.seed * 7919 + self.est.rank)
+            return g
 
         kw = {}
         if label is not None:
@@ -117,9 +125,9 @@ def build_device_trainer(est, model, first):
         if stores and name not in STORE_AWARE:
             continue
         if pred(model):
-            est._prepare(first)  # materialise lazy layers, broadcast rank 0's weights, optimizer
-            if est._sync is not None:
-                est._sync.remove()  # the trainer synchronises its gradient itself
+            # materialise lazy layers, broadcast rank 0's weights; no torch optimizer and no
+            # autograd gradient sync: every device trainer runs its own update and sync
+            est._prepare(first, build_optimizer=False)
             tr = builder(Ctx(est, model))
             tr.device_trainer_kind = name
             return tr

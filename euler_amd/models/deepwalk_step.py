@@ -67,7 +67,7 @@ class DeepWalkTrainer:
     def __init__(self, graph, num_nodes, dim=128, walk_len=3, left_win_size=1, right_win_size=1, num_negs=5,
                  batch_size=1024, lr=0.01, optimizer="adam", group=None, seed=0, force_comm=False, static=False,
                  wire_dtype="bf16", overflow_check_every=200, micro_batches=1, edge_types=None, p=1.0, q=1.0,
-                 row_map=None, table_init="normal"):
+                 row_map=None, table_init="normal", table_slots=True):
         import torch.distributed as dist
 
         self.graph = graph
@@ -90,7 +90,7 @@ class DeepWalkTrainer:
         world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
         self.off = -(-(self.num_nodes + 1) // world) * world
         self.table = ShardedTable(2 * self.off, dim, dev, group, optimizer, lr, seed=seed, force_comm=force_comm,
-                                  wire_dtype=wire_dtype, init=table_init)
+                                  wire_dtype=wire_dtype, init=table_init, slots=table_slots)
         pi, pj = _pair_positions(walk_len, left_win_size, right_win_size)
         self.pi, self.pj = pi.to(dev), pj.to(dev)
         self.pairs_per_walk = int(pi.numel())
@@ -439,7 +439,7 @@ class DeepWalkEstimatorTrainer:
                                      num_negs=model.num_negs, batch_size=batch_size, lr=learning_rate,
                                      optimizer=optimizer, seed=seed, static=self.on_gpu, edge_types=ets,
                                      p=getattr(model, "walk_p", 1), q=getattr(model, "walk_q", 1),
-                                     row_map=row_map, table_init=None)
+                                     row_map=row_map, table_init=None, table_slots=False)
         t = self.inner.table
         self._offw = self.inner.off // t.world  # local rows per half
         self._pad_rows()
@@ -458,6 +458,8 @@ class DeepWalkEstimatorTrainer:
                     rows = self._half_rows()
                     ok = rows < self.num
                     t.weight[h * self._offw: (h + 1) * self._offw][ok] = w.detach()[rows[ok].to(w.device)].to(t.weight)
+        # slots only now: the model's own table storage is gone when the tables are views
+        t.alloc_slots()
         self.loss_sum = torch.zeros(2, dtype=torch.float64, device=self.device)
         self._graphs, self._graph_loss, self._graph_exec = {}, {}, None
         self._loss = torch.zeros((), device=self.device)

@@ -319,6 +319,96 @@ class GcnTrainer(CapturedTrainer):
         return self.infer_logits(ids)[0]
 
     # ------------------------------------------------------------------ oracle
+    def reference_loss_and_grads_bf16(self):
+        """The bf16-aware fp32 oracle of the last step, in pure CPU torch (no HIP op): the
+        model's GCN on the blocks the fused flow built (``plan.flow()``: the same roots,
+        node sets and edge lists), every operand rounded to bf16 exactly where gcn.hip
+        rounds it and everything else fp32 — so the kernels must match it to fp32
+        accumulation order, not to bf16 noise.  Rounding points:
+
+        * weights: bf16 images of the fp32 masters (conv W, fc W, out W);
+        * agg_t = bf(sum_e x_s deg_t^-1/2 deg_s^-1/2) over the target's block edges (+ the
+          self loop), deg_t = its edge count (+1), deg_s = the source's in-block count;
+          h = bf(relu(agg W^T)) (the outer conv's h1 kept bf16 for the next hop);
+        * head: emb = bf(h Wfc^T + bfc), logits = emb Wout^T (fp32),
+          d = bf((sigmoid - y) / (B C)), demb = d Wout, dz = bf(relu'(h) (bf(demb) Wfc));
+          dWout = d^T emb, dWfc = bf(demb)^T h, dbfc = sum demb, dW = dz^T agg;
+        * L = 2: dagg = dz W (fp32); per hop-0 edge e: bf(relu'(h1_s) w_e dagg_t) against
+          agg1_s (gcn_dw_kernel: d h1 is never formed).
+
+        Semantics: tf_euler/python/convolution/gcn_conv.py:42-54, mp_utils/base.py:24-47."""
+        f32 = torch.float32
+        cpu = torch.device("cpu")
+
+        def bf(t):
+            return t.to(torch.bfloat16).to(f32)
+
+        fl = self.plan.flow()
+        L = len(self.gnn.convs)
+        sl = int(bool(self.gnn.sampler.add_self_loops))
+        roots = fl["roots"].to(cpu).long()
+        B = roots.numel()
+        cnt = [int(c) for c in fl["cnt"].to(cpu).tolist()]
+        node_set = fl["set"].to(cpu).long()
+        rself = fl["rself"].to(cpu).long()
+        x = self.features[:, : self.D].to(cpu).to(f32)
+        convs = [bf(c.fc.weight.detach().to(cpu).float()) for c in self.gnn.convs]
+        Wfc = bf(self.gnn.fc.weight.detach().to(cpu).float())
+        bfc = self.gnn.fc.bias.detach().to(cpu).float()
+        Wout = bf(self.model.out_fc.weight.detach().to(cpu).float())
+
+        def block(h, nt, self_pos):
+            """(target, source position, coefficient) of hop h's edges + self loops"""
+            hop = {k: v.to(cpu).long() for k, v in fl["hops"][h].items()}
+            off = hop["off"][: nt + 1]
+            E = int(off[-1])
+            t = hop["etgt"][:E]
+            sp = hop["esrc"][:E]
+            node = hop["enode"][:E]
+            keep = sp >= 0
+            t, sp, node = t[keep], sp[keep], node[keep]
+            if sl:
+                tt = torch.arange(nt)
+                t, sp = torch.cat([t, tt]), torch.cat([sp, self_pos])
+                node = torch.cat([node, node_set[self_pos]])
+            deg_t = (off[1:] - off[:-1] + sl).to(f32)
+            deg_s = hop["deg_s"].to(f32)
+            coef = deg_t[t].rsqrt() * deg_s[sp].rsqrt()
+            return t, sp, node, coef
+
+        def aggregate(nt, t, vals, coef):
+            return torch.zeros(nt, vals.shape[1]).index_add_(0, t, vals * coef[:, None])
+
+        if L == 2:
+            n1 = cnt[1]
+            t1, sp1, node1, c1 = block(1, n1, torch.arange(n1))
+            agg1 = bf(aggregate(n1, t1, x[node1], c1))
+            h1 = bf(torch.relu(agg1 @ convs[0].t()))
+            t0, sp0, node0, c0 = block(0, B, rself)
+            agg = bf(aggregate(B, t0, h1[sp0], c0))
+        else:
+            t0, sp0, node0, c0 = block(0, B, rself)
+            agg = bf(aggregate(B, t0, x[node0], c0))
+        Wl = convs[-1]
+        H0 = bf(torch.relu(agg @ Wl.t()))
+        emb = bf(H0 @ Wfc.t() + bfc)
+        logits = emb @ Wout.t()
+        y = self.labels[roots.to(self.labels.device)].to(cpu).float()
+        loss = torch.nn.functional.binary_cross_entropy_with_logits(logits, y)
+        d = bf((torch.sigmoid(logits) - y) / float(y.numel()))
+        demb = d @ Wout
+        De = bf(demb)
+        dz = bf((H0 > 0).to(f32) * (De @ Wfc))
+        names = {id(p): n for n, p in self.model.named_parameters()}
+        g = {names[id(self.model.out_fc.weight)]: d.t() @ emb, names[id(self.gnn.fc.weight)]: De.t() @ H0,
+             names[id(self.gnn.fc.bias)]: demb.sum(0), names[id(self.gnn.convs[-1].fc.weight)]: dz.t() @ agg}
+        if L == 2:
+            dagg = dz @ Wl
+            rows = bf((h1[sp0] > 0).to(f32) * (c0[:, None] * dagg[t0]))
+            g[names[id(self.gnn.convs[0].fc.weight)]] = rows.t() @ agg1[sp0]
+        return float(loss), g
+
+
     def forward_backward_only(self):
         """plan step without the optimizer (tests): loss_out and the flat gradient"""
         if self._plan_caps != self.flow.caps:

@@ -787,6 +787,88 @@ class SageTrainer:
         loss.backward()
         return float(loss), {k: v.grad.detach() for k, v in params.items()}
 
+    def reference_loss_and_grads_bf16(self, params=None, samples=None, table=None):
+        """The bf16-aware fp32 oracle of one tree step: the same model, with every operand
+        rounded to bf16 exactly where the fused kernels round it (csrc/hip/sage_tree.hip) and
+        everything else in fp32 — so the kernels' step must match it to fp32 accumulation
+        order (~1e-6), not to bf16 noise.  Rounding points (bf = round to bf16, RNE):
+
+        * weights: bf16 shadows Wk, Wfc, Wout; Wc = bf(Wout_bf @ Wfc_bf) (tr_comb_wave);
+          bc = Wout @ bfc in fp32 (masters);
+        * layer 0: A0 = [bf(x_self) | bf(sum(x_leaf (+ x_self)) * inv_leaf)];
+          h_k = bf(relu(A_k @ W_k,bf^T)); A_k+1 = [h_self | bf(sum_{j<F} h_j (+ h_self) * inv_grp)];
+        * head: logits = h @ Wc^T + bc (fp32), loss = mean BCE (fp32),
+          d = bf((sigmoid - y) / (B C)), emb = bf(h @ Wfc_bf^T + bfc), demb = d @ Wout_bf,
+          g = bf(relu'(h) * (d @ Wc)), dA = g @ W_bf (fp32);
+        * routed gradients (tr_dw_route / tr_bwd): g_k-1 = bf(relu'(h_k-1) * route(dA_k)),
+          neighbour slots dA[:, H:] * inv_grp, the self slot dA[:, :H] (+ that share with
+          self loops);
+        * dW_k = g_k^T @ A_k, dWfc = bf(demb)^T @ h, dWout = d^T @ emb, dbfc = sum demb.
+
+        Reference model semantics: tf_euler/python/convolution/sage_conv.py:33-44,
+        mp_utils/base_gnn.py:75-92, mp_utils/base.py:24-47."""
+        f32 = torch.float32
+
+        def bf(t):
+            return t.to(torch.bfloat16).to(f32)
+
+        P = {k: v.detach().to(f32) for k, v in (params or self.logical_params()).items()}
+        roots, nodes, leaf = samples if samples is not None else self.samples()
+        dev = P["gnn.fc.weight"].device
+        x = (self.features if table is None else table)[:, : self.D].to(dev).to(f32)
+        x = torch.cat([x, torch.zeros(1, self.D, device=dev)], 0)
+        n = x.shape[0] - 1
+        nodes, leaf = nodes.to(dev), leaf.to(dev)
+        xs = x[torch.where(nodes < 0, torch.full_like(nodes, n), nodes)]
+        agg = x[torch.where(leaf < 0, torch.full_like(leaf, n), leaf)].sum(1)
+        inc = 1 if self.include_self else 0
+        if inc:
+            agg = agg + xs
+        inv_leaf = torch.tensor(1.0 / (self.fanouts[-1] + inc), dtype=f32)
+        W = [bf(torch.cat([P[f"gnn.convs.{k}.self_fc.weight"], P[f"gnn.convs.{k}.neigh_fc.weight"]], 1))
+             for k in range(self.L)]
+        A = [torch.cat([bf(xs), bf(agg * inv_leaf)], 1)]
+        h = [bf(torch.relu(A[0] @ W[0].t()))]
+        groups = []
+        for k in range(1, self.L):
+            lvl = self.L - 1 - k
+            Pg, f = 1 << self.logP[lvl + 1], self.fanouts[lvl]
+            hg = h[-1].view(-1, Pg, h[-1].shape[1])
+            sf, a = hg[:, f], hg[:, :f].sum(1)
+            if inc:
+                a = a + sf
+            inv = torch.tensor(1.0 / (f + inc), dtype=f32)
+            A.append(torch.cat([sf, bf(a * inv)], 1))
+            h.append(bf(torch.relu(A[-1] @ W[k].t())))
+            groups.append((Pg, f, inv))
+        Wfc, bfc, Wout = bf(P["gnn.fc.weight"]), P["gnn.fc.bias"], bf(P["out_fc.weight"])
+        Wc = bf(Wout @ Wfc)
+        hl = h[-1]
+        logits = hl @ Wc.t() + P["out_fc.weight"] @ bfc
+        y = self._labels_of(roots).to(dev)
+        loss = torch.nn.functional.binary_cross_entropy_with_logits(logits, y)
+        d = bf((torch.sigmoid(logits) - y) / float(y.numel()))
+        emb = bf(hl @ Wfc.t() + bfc)
+        demb = d @ Wout
+        grads = {"out_fc.weight": d.t() @ emb, "gnn.fc.weight": bf(demb).t() @ hl, "gnn.fc.bias": demb.sum(0)}
+        g = bf((hl > 0).to(f32) * (d @ Wc))
+        for k in range(self.L - 1, -1, -1):
+            dW = g.t() @ A[k]
+            hin = A[k].shape[1] // 2
+            grads[f"gnn.convs.{k}.self_fc.weight"] = dW[:, :hin]
+            grads[f"gnn.convs.{k}.neigh_fc.weight"] = dW[:, hin:]
+            if k == 0:
+                break
+            dA = g @ W[k]
+            Pg, f, inv = groups[k - 1]
+            dn = dA[:, hin:] * inv
+            ds = dA[:, :hin] + (dn if inc else 0.0)
+            route = torch.zeros(dA.shape[0], Pg, hin, device=dev)
+            route[:, :f] = dn.unsqueeze(1)
+            route[:, f] = ds
+            g = bf((h[k - 1] > 0).to(f32) * route.view(-1, hin))
+        return float(loss), grads
+
     def gradients(self):
         """logical view of :attr:`grad` after :meth:`forward_backward` (GPU)"""
         return self._unpack(self.grad)

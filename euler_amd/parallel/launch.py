@@ -21,7 +21,7 @@ import sys
 import threading
 import time
 
-__all__ = ["free_port", "rank_env", "spawn_local", "LAUNCHED_ENV"]
+__all__ = ["free_port", "rank_env", "spawn_local", "maybe_spawn", "require_gpu", "LAUNCHED_ENV"]
 
 # set in every child: a script seeing it never launches again
 LAUNCHED_ENV = "EULER_AMD_LAUNCHED"
@@ -118,3 +118,43 @@ def _stop(procs, grace_s):
         except subprocess.TimeoutExpired:
             p.kill()
             p.wait()
+
+
+_REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def maybe_spawn(gpus, argv, script):
+    """The ``--gpus N`` contract of every multi-GPU entry point (bench.py,
+    benchmarks/bench_deepwalk.py, benchmarks/bench_kg.py, tools/runner.py and the
+    examples): a plain ``python script --gpus N`` (no WORLD_SIZE) starts N ranks here and
+    returns the job's exit code; a rank (torchrun's or ours) gets None and runs.  ``gpus``
+    None: whatever WORLD_SIZE says.  A WORLD_SIZE that disagrees with an explicit --gpus
+    is an error.  Call before anything touches the GPU."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if gpus is None:
+        return None
+    gpus = int(gpus)
+    if gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if env_world is None:
+        if gpus > 1 and LAUNCHED_ENV not in os.environ:
+            env = dict(os.environ)
+            env["PYTHONPATH"] = _REPO + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+            return spawn_local(gpus, list(argv), script=os.path.abspath(script), env=env)
+        return None
+    if int(env_world) != gpus:
+        raise SystemExit(f"--gpus {gpus} disagrees with WORLD_SIZE={env_world} (torchrun --nproc-per-node)")
+    return None
+
+
+def require_gpu(local_rank: int, world: int, what: str = "this script"):
+    """Fail cleanly (SystemExit naming the shortfall) when rank ``local_rank`` has no GPU of
+    its own: one rank per GPU, no device sharing under RCCL."""
+    import torch
+
+    n = torch.cuda.device_count()
+    if n == 0:
+        raise SystemExit(f"{what} needs a GPU (run through gpurun on an MI355X)")
+    if local_rank >= n:
+        raise SystemExit(f"{what}: rank with LOCAL_RANK={local_rank} of {world} needs its own GPU, but only {n} "
+                         f"visible (one rank per GPU)")

@@ -21,11 +21,15 @@ checkpoint written by W ranks restores on any W' with no collective and no all-g
 """
 from __future__ import annotations
 
+import logging
 import os
 import re
+import time
 
 import numpy as np
 import torch
+
+log = logging.getLogger("euler_amd.checkpoint")
 
 __all__ = ["shard_meta", "save_rows", "read_rows", "sidecar_files", "CHUNK_ROWS"]
 
@@ -69,14 +73,19 @@ def save_rows(ckpt_path: str, table: str, tensors: dict, num: int, world: int, r
         fn = "%s.%s.%s.npy" % (os.path.basename(stem), _safe(table), kind)
         path = os.path.join(os.path.dirname(stem) or ".", fn)
         tmp = path + ".tmp"
-        out = np.lib.format.open_memmap(tmp, mode="w+", dtype=np.float32, shape=(n, dim))
-        for s in range(0, n, CHUNK_ROWS):
-            e = min(n, s + CHUNK_ROWS)
-            out[s:e] = t[s:e].float().cpu().numpy()
-        out.flush()
-        del out
+        # a plain .npy written sequentially: header, then CHUNK_ROWS rows per device->host
+        # copy (no mapping of the whole file: host memory stays one chunk)
+        t0 = time.time()
+        with open(tmp, "wb") as f:
+            np.lib.format.write_array_header_1_0(
+                f, {"descr": np.lib.format.dtype_to_descr(np.dtype(np.float32)), "fortran_order": False,
+                    "shape": (n, dim)})
+            for s in range(0, n, CHUNK_ROWS):
+                e = min(n, s + CHUNK_ROWS)
+                f.write(np.ascontiguousarray(t[s:e].float().cpu().numpy()).tobytes())
         os.replace(tmp, path)
         files[kind] = fn
+        log.info("wrote %s: %d rows, %.2f GiB in %.1f s", fn, n, n * dim * 4 / 2 ** 30, time.time() - t0)
     return shard_meta(num, world, rank, dim or 0, files)
 
 
@@ -101,6 +110,7 @@ def read_rows(dirname: str, metas, kind: str, rows: torch.Tensor, out: torch.Ten
     if any(a is None for a in arrays):
         return False
     rows = rows.reshape(-1).long().cpu()
+    t0 = time.time()
     for s in range(0, rows.numel(), CHUNK_ROWS):
         r = rows[s: s + CHUNK_ROWS]
         ok = (r >= 0) & (r < num)
@@ -116,4 +126,6 @@ def read_rows(dirname: str, metas, kind: str, rows: torch.Tensor, out: torch.Ten
                 data = a[local]
             idx = torch.nonzero(sel).reshape(-1) + s
             out[idx.to(out.device)] = torch.from_numpy(np.array(data, dtype=np.float32)).to(out.device, out.dtype)
+    log.info("read %d rows of %s (and its %d-rank siblings) in %.1f s", rows.numel(), metas[0]["files"][kind], W,
+             time.time() - t0)
     return True

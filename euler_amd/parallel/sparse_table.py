@@ -73,7 +73,7 @@ class StaticHandle:
 
 class ShardedTable:
     def __init__(self, num_rows, dim, device, group=None, optimizer="adam", lr=0.01, init_std=0.1, seed=0,
-                 beta1=0.9, beta2=0.999, eps=1e-8, force_comm=False, wire_dtype="fp32", init="normal"):
+                 beta1=0.9, beta2=0.999, eps=1e-8, force_comm=False, wire_dtype="fp32", init="normal", slots=True):
         self.num_rows, self.dim = int(num_rows), int(dim)
         if wire_dtype not in ("fp32", "bf16"):
             raise ValueError("wire_dtype must be fp32 or bf16")
@@ -94,14 +94,23 @@ class ShardedTable:
         elif init is not None:  # None: the caller fills every row (e.g. from a model's table)
             raise ValueError("init must be 'normal' or None")
         self.kind = _KINDS[optimizer]
-        # optimizer slots: Adam keeps m and v, Adagrad only the accumulator v, SGD none
-        # (the kernel never touches an unused slot, so it aliases a used one or the weight)
-        self.v = torch.zeros_like(self.weight) if self.kind in (0, 1) else self.weight
-        self.m = torch.zeros_like(self.weight) if self.kind == 0 else self.v
+        self.m = self.v = None
+        if slots:
+            self.alloc_slots()
         self.step = torch.zeros(1, dtype=torch.int64, device=self.device)
         self.lr, self.b1, self.b2, self.eps = float(lr), float(beta1), float(beta2), float(eps)
         self.overflow = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.cap_override = None  # fixed per-peer slot count (tests / tuning)
+
+    def alloc_slots(self):
+        """the optimizer slots: Adam keeps m and v, Adagrad only the accumulator v, SGD none
+        (the kernel never touches an unused slot, so it aliases a used one or the weight).
+        ``slots=False`` at construction defers this, e.g. until a model's table has been
+        moved into :attr:`weight` and freed (a 100M x 128 table pair is 102 GB)."""
+        if self.m is not None:
+            return
+        self.v = torch.zeros_like(self.weight) if self.kind in (0, 1) else self.weight
+        self.m = torch.zeros_like(self.weight) if self.kind == 0 else self.v
 
     # ------------------------------------------------------------------ fixed capacity
     def capacity(self, n: int) -> int:

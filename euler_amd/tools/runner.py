@@ -6,15 +6,20 @@ or the thin per-model scripts under ``examples/``.  Flags keep the reference nam
 (``dataset, hidden_dim, layers, fanouts, batch_size, num_epochs, log_steps, model_dir,
 id_file, infer_dir, optimizer, learning_rate, run_mode``); ``total_step`` defaults to
 ``num_epochs * total_size / batch_size`` like the reference runners.  Data parallelism:
-launch under torchrun (``WORLD_SIZE`` > 1 initialises RCCL/gloo automatically).
+``--gpus N`` starts N ranks on this node (parallel/launch.py maybe_spawn), or launch under
+torchrun (``WORLD_SIZE`` > 1 initialises RCCL/gloo automatically); reference launcher
+``tf_euler/scripts/dist_tf_euler.sh:1-49``.
 """
 from __future__ import annotations
 
 import argparse
 import logging
 import os
+import sys
 
-import torch
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL, before torch loads HIP
+
+import torch  # noqa: E402
 
 __all__ = ["MODELS", "build", "main", "parse_args"]
 
@@ -153,6 +158,8 @@ MODELS = None
 def parse_args(argv=None, model=None):
     p = argparse.ArgumentParser(description="euler_amd model-zoo runner")
     p.add_argument("--model", default=model, required=model is None)
+    p.add_argument("--gpus", type=int, default=None, help="data-parallel ranks on this node, one per GPU "
+                   "(self-spawned; default: WORLD_SIZE or 1)")
     p.add_argument("--dataset", default=None)
     p.add_argument("--data_dir", default=None)
     p.add_argument("--scale", type=float, default=1.0, help="synthetic-dataset scale when no raw files exist")
@@ -239,6 +246,12 @@ def build(a):
 def main(argv=None, model=None):
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(message)s")
     a = parse_args(argv, model)
+    if argv is None:  # a command line (not a library call): --gpus N starts the ranks here
+        from euler_amd.parallel.launch import maybe_spawn
+
+        rc = maybe_spawn(a.gpus, sys.argv[1:], sys.argv[0])
+        if rc is not None:
+            raise SystemExit(rc)
     _, est = build(a)
     if a.run_mode == "train":
         return est.train()

@@ -53,6 +53,17 @@ def _setup_fast(device, batch=64, hidden=32, model="fastgcn"):
     return m
 
 
+def _check_bf16_oracle(tr, loss_k, grads_k):
+    """tight: the pure-CPU bf16-aware oracle on the fused step's own blocks (rounding where
+    gcn.hip rounds; fp32 elsewhere) — loss to 1e-4, every gradient to 1e-3 relative"""
+    loss_b, grads_b = tr.reference_loss_and_grads_bf16()
+    assert abs(loss_k - loss_b) <= 1e-4 * abs(loss_b), (loss_k, loss_b)
+    assert set(grads_b) == set(grads_k)
+    for n, r in grads_b.items():
+        err = float((grads_k[n].float().cpu() - r).norm() / max(float(r.norm()), 1e-12))
+        assert err < 1e-3, (n, err)
+
+
 def test_fused_gcn_predicate_takes_layer_sampled_gcns_cpu():
     from euler_amd.models.gcn_trainer import _gcn_shape
 
@@ -85,6 +96,7 @@ def test_fused_layer_sampled_gcn_step_matches_generic_fp32(model):
     torch.cuda.synchronize()
     assert int(tr.flow.overflow.item()) == 0
     grads_k = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+    _check_bf16_oracle(tr, loss_k, grads_k)
     fl = tr.plan.flow()
     roots = fl["roots"].long().clone()
     cnt = fl["cnt"].cpu().tolist()
@@ -140,6 +152,7 @@ def test_fused_gcn_step_matches_generic_fp32(layers, self_loops):
     torch.cuda.synchronize()
     assert int(tr.flow.overflow.item()) == 0
     grads_k = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+    _check_bf16_oracle(tr, loss_k, grads_k)
     fl = tr.plan.flow()
     roots = fl["roots"].long().clone()
     cnt = fl["cnt"].cpu().tolist()

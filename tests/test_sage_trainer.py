@@ -123,6 +123,29 @@ def test_from_model_matches_supervised_graphsage_names():
     assert list(tr.state_dict()) == sage_param_names(2)
 
 
+@pytest.mark.parametrize("cfg", [dict(fanouts=[6], dims=[40, 24], C=10),
+                                 dict(fanouts=[5, 3], dims=[64, 64, 32], C=10, self_loops=True, mode="dense"),
+                                 dict(fanouts=[3, 20, 2], dims=[64, 128, 64, 32], C=16, D=64, mode="dense",
+                                      self_loops=True)])
+def test_bf16_oracle_is_the_model_without_rounding_cpu(cfg, monkeypatch):
+    """the bf16-aware oracle's hand-written forward / backward (head, tree routing, the
+    combined Wout Wfc) IS the model's autograd once the bf16 rounding is switched off"""
+    tr = _trainer("cpu", fdt=torch.float32, **cfg)
+    tr.step()
+    orig = torch.Tensor.to
+
+    def no_bf16(self, *a, **k):
+        return self if a and a[0] is torch.bfloat16 else orig(self, *a, **k)
+
+    monkeypatch.setattr(torch.Tensor, "to", no_bf16)
+    loss_o, grads_o = tr.reference_loss_and_grads_bf16()
+    monkeypatch.setattr(torch.Tensor, "to", orig)
+    loss_r, grads_r = tr.reference_loss_and_grads()
+    assert abs(loss_o - loss_r) <= 1e-6 * abs(loss_r) and set(grads_o) == set(grads_r)
+    for k in grads_r:
+        assert ((grads_o[k] - grads_r[k]).norm() / grads_r[k].norm()).item() < 1e-5, k
+
+
 # ----------------------------------------------------------------------------------------- GPU
 
 CASES = [
@@ -153,12 +176,19 @@ def test_tree_step_matches_fp32_oracle(cuda, cfg):
     torch.cuda.synchronize()
     loss_k = float(tr.loss_acc.item())
     grads_k = tr.gradients()
+    # tight: the bf16-aware fp32 oracle rounds operands exactly where the kernels do, so
+    # only fp32 accumulation order separates them
+    loss_b, grads_b = tr.reference_loss_and_grads_bf16()
+    assert abs(loss_k - loss_b) <= 1e-4 * abs(loss_b), (loss_k, loss_b)
+    for name in grads_b:
+        cos, rel = _cmp(grads_k[name], grads_b[name])
+        assert rel < 1e-3, (name, cos, rel)
+    # loose, second check: the plain fp32 model (bf16 operand noise: sums over thousands
+    # of routed rows with mixed signs reach ~8 % in the relative norm)
     loss_r, grads_r = tr.reference_loss_and_grads()
     assert abs(loss_k - loss_r) <= 2e-2 * abs(loss_r) + 1e-4, (loss_k, loss_r)
     for name in grads_r:
         cos, rel = _cmp(grads_k[name], grads_r[name])
-        # bf16 operands: sums over thousands of routed rows with mixed signs amplify the
-        # per-element rounding in the relative norm (17-neighbour groups reach ~8 %)
         assert cos > 0.995 and rel < 0.1, (name, cos, rel)
     # samples are valid rows and roots of the right node population
     roots, nodes, leaf = tr.samples()
