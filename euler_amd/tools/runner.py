@@ -189,6 +189,9 @@ def parse_args(argv=None, model=None):
     p.add_argument("--gae_encoder", default="gcn")
     p.add_argument("--infer_type", default="node_src")
     p.add_argument("--sharded", action="store_true", help="row-shard id embeddings over the process group")
+    p.add_argument("--row_sparse_tables", default="auto", choices=["auto", "on", "off"],
+                   help="device path: id tables trained row-sparse (ShardedTable + sparse optimizer); auto = "
+                        "for sharded models and tables of >= 2^20 rows")
     p.add_argument("--device", default=None)
     p.add_argument("--amp", default=None, help="bf16 for bf16 autocast on the GPU")
     p.add_argument("--device_graph", action="store_true",
@@ -229,7 +232,8 @@ def build(a):
               "device_feature_dtype": a.device_feature_dtype, "seed": a.seed,
               "native_pipeline": {"auto": "auto", "on": True, "off": False}[a.native_pipeline],
               "cuda_graph": a.cuda_graph if a.cuda_graph == "auto" else False,
-              "pipeline_workers": a.pipeline_workers}
+              "pipeline_workers": a.pipeline_workers,
+              "row_sparse_tables": {"auto": "auto", "on": True, "off": False}[a.row_sparse_tables]}
     if kind == "node":
         params.update(train_node_type=_first(ds.train_node_type), id_file=a.id_file or ds.id_file)
         est = NodeEstimator(model, params)
