@@ -361,6 +361,32 @@ def _lgcn(c: Ctx):
     return LgcnTrainer.from_model(c.model, g, c.batch, **c.opt_kw())
 
 
+def _is_scalable(model):
+    from euler_amd.models.scalable_trainer import store_encoder_of
+    from euler_amd.mp_utils.models import SuperviseModel
+
+    return isinstance(model, SuperviseModel) and store_encoder_of(model) is not None
+
+
+@register("scalable", _is_scalable)
+def _scalable(c: Ctx):
+    # ScalableSageEncoder / ScalableGCNEncoder (historical embeddings): the model's own
+    # forward and store protocol with every graph query answered from HBM
+    # (graph/device_scope.py, models/scalable_trainer.py)
+    from euler_amd.models.scalable_trainer import ScalableTrainer, store_encoder_of
+
+    m = c.model
+    ne = store_encoder_of(m)._node_encoder
+    names = [str(n) for n in ne.feature_idx] if ne.use_feature else []
+    dims = [int(d) for d in ne.feature_dim] if ne.use_feature else []
+    g = c.upload(features=names, feature_dims=dims, label=m.label_idx, label_dim=m.label_dim)
+    cols, off = {}, 0
+    for n, d in zip(names, dims):
+        cols[n] = (off, d)
+        off += d
+    return ScalableTrainer(m, g, c.batch, cols, label=(m.label_idx, m.label_dim), **c.opt_kw())
+
+
 @register("encoder_flow", _encoder("GCNEncoder"))
 def _enc(c: Ctx):
     # GeniePath and other full-neighbour encoder models: hop sets and adjacencies built on

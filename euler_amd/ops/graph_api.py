@@ -48,6 +48,23 @@ class SparseTensor(namedtuple("SparseTensor", ["indices", "values", "dense_shape
 
 
 # ----------------------------------------------------------------------------- plumbing
+_SCOPE_MOD = [None]
+
+
+def _scope():
+    """the active device-graph scope (graph/device_scope.py): queries answered from HBM"""
+    m = _SCOPE_MOD[0]
+    if m is None:
+        from euler_amd.graph import device_scope as m
+
+        _SCOPE_MOD[0] = m
+    return m.active_scope()
+
+
+def device_scope_active() -> bool:
+    return _scope() is not None
+
+
 def _u64(x) -> np.ndarray:
     if isinstance(x, torch.Tensor):
         x = x.detach().cpu().numpy()
@@ -149,6 +166,9 @@ def _has(condition: str) -> str:
 # ----------------------------------------------------------------------------- sampling
 def sample_node(count, node_type, condition=""):
     """``sampleN(node_type, count)[.has(cond)]`` (reference sample_node_op.cc:60-76)."""
+    sc = _scope()
+    if sc is not None and not condition:
+        return sc.sample_node(count, node_type)
     t = -1 if (isinstance(node_type, str) and node_type == "-1") else int(_type_ids(node_type, _meta()["node_types"], "node")[0])
     r = run_gql("sampleN(node_type, count)%s.as(id)" % _has(condition),
                 {"node_type": np.asarray([t], np.int32), "count": np.asarray([int(count)], np.int64)}, ["id:0"])
@@ -235,6 +255,9 @@ def _dense_rows(idx, ids, w, t, n, k, default_node):
 
 def sample_neighbor(nodes, edge_types, count, default_node=-1, condition=""):
     """Weighted with-replacement sampling -> (ids, weights, types), each [n, count]."""
+    sc = _scope()
+    if sc is not None and not condition:
+        return sc.sample_neighbor(nodes, edge_types, count, default_node)
     ids = _u64(nodes)
     et = _et(edge_types)
     eng = get_engine()
@@ -307,6 +330,9 @@ def get_in_neighbor(nodes, edge_types, condition=""):
 
 def sample_fanout(nodes, edge_types, counts, default_node=-1):
     """Multi-hop sampling: ([n, n*c0, n*c0*c1, ...], weights, types) (reference neighbor_ops.py)."""
+    sc = _scope()
+    if sc is not None:
+        return sc.sample_fanout(nodes, edge_types, counts, default_node)
     nb = [torch.as_tensor(_u64(nodes).view(np.int64))]
     ws, ts = [], []
     for et, c in zip(edge_types, counts):
@@ -425,6 +451,9 @@ def sample_fanout_layerwise(nodes, edge_types, counts, default_node=-1, weight_f
 
 def get_multi_hop_neighbor(nodes, edge_types):
     """Unique node set per hop + sparse adjacency between hops (reference neighbor_ops.py)."""
+    sc = _scope()
+    if sc is not None:
+        return sc.get_multi_hop_neighbor(nodes, edge_types)
     cur = torch.as_tensor(_u64(nodes).view(np.int64))
     nodes_list, adj_list = [cur], []
     for et in edge_types:
@@ -497,6 +526,9 @@ def _dense_from_ragged(idx, vals, dim):
 
 def get_dense_feature(nodes, feature_names, dimensions, thread_num=1):
     """Dense node features -> list of float32 [n, dim] (missing = 0)."""
+    sc = _scope()
+    if sc is not None:
+        return sc.get_dense_feature(nodes, feature_names, dimensions)
     ids = _u64(nodes)
     eng = get_engine()
     if _meta()["mode"] == "local":

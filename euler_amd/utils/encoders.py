@@ -122,7 +122,9 @@ class ShallowEncoder(nn.Module):
         if self.use_id:
             embs.append(self.embedding(ids))
         if self.use_feature:
-            feats = torch.cat(G.get_dense_feature(ids.cpu(), self.feature_idx, self.feature_dim), -1).to(dev)
+            # a device-graph scope answers from HBM with device ids (no host round trip)
+            q = ids if G.device_scope_active() else ids.cpu()
+            feats = torch.cat(G.get_dense_feature(q, self.feature_idx, self.feature_dim), -1).to(dev)
             if self.combiner == "add":
                 feats = self.dense(feats)
             embs.append(feats)

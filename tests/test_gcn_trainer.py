@@ -230,6 +230,7 @@ def test_estimator_routes_gcn_to_fused_step_and_trains(tmp_path, monkeypatch):
         return orig(self)
 
     monkeypatch.setattr(eb.BaseEstimator, "_train_device_graph", spy)
+    torch.manual_seed(0)  # the same initial weights in both runs
     r = main(["--dataset", "ppi", "--scale", "0.05", "--batch_size", "64", "--log_steps", "40", "--device", "cuda",
               "--seed", "1", "--model_dir", str(tmp_path / "ckpt"), "--device_graph", "--total_step", "120",
               "--learning_rate", "0.01"], model="gcn")
@@ -254,6 +255,7 @@ def test_fused_gcn_overflow_regrows(tmp_path, monkeypatch):
         return orig(self)
 
     monkeypatch.setattr(eb.BaseEstimator, "_train_device_graph", spy)
+    torch.manual_seed(0)  # the same initial weights in both runs
     r = main(["--dataset", "ppi", "--scale", "0.05", "--batch_size", "64", "--log_steps", "8", "--device", "cuda",
               "--seed", "1", "--model_dir", str(tmp_path / "ckpt"), "--device_graph", "--total_step", "24"],
              model="gcn")
@@ -270,6 +272,7 @@ def test_fused_gcn_overflow_regrows(tmp_path, monkeypatch):
         return orig(self)
 
     monkeypatch.setattr(eb.BaseEstimator, "_train_device_graph", spy_exact)
+    torch.manual_seed(0)
     r2 = main(["--dataset", "ppi", "--scale", "0.05", "--batch_size", "64", "--log_steps", "8", "--device", "cuda",
                "--seed", "1", "--model_dir", str(tmp_path / "ckpt_exact"), "--device_graph", "--total_step", "24"],
               model="gcn")

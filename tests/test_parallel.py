@@ -923,3 +923,62 @@ def test_deepwalk_shard_checkpoint_reshards_rows_and_slots(tmp_path):
             for k in ("weight", "m", "v"):
                 assert not torch.isnan(tab[k]).any()
                 assert torch.equal(got[key][k], tab[k]), (world, key, k)
+
+
+def _worker_scalable_device(rank, world, port, q, data_dir, model_dir, store):
+    """ScalableSageEncoder through NodeEstimator(device_graph=True) on 2 gloo ranks: every
+    rank draws its own roots; the flat gradient is all-reduced and the stores are kept
+    consistent (replicated: every rank applies every rank's writes; sharded: row r on rank
+    r % 2 over all-to-all) -> identical parameters (and replicas) on both ranks"""
+    try:
+        _init(rank, world, port)
+        import euler_amd as ea
+        from euler_amd.dataset import get_dataset
+        from euler_amd.estimator import NodeEstimator
+        from euler_amd.mp_utils.models import SuperviseModel
+        from euler_amd.utils import encoders as E
+
+        ds = get_dataset("ppi", data_dir=data_dir, scale=0.05)
+        ds.load_graph()
+        ea.set_seed(3)
+
+        class M(SuperviseModel):
+            def __init__(self):
+                super().__init__(ds.label_idx, ds.label_dim)
+                self.enc = E.ScalableSageEncoder(["train"], 4, 2, 16, feature_idx=ds.feature_idx,
+                                                 feature_dim=ds.feature_dim, max_id=ds.max_node_id)
+
+            def embed(self, n_id):
+                return self.enc(n_id)
+
+        torch.manual_seed(0)
+        m = M()
+        tnt = ds.train_node_type[0] if isinstance(ds.train_node_type, list) else ds.train_node_type
+        est = NodeEstimator(m, {"model_dir": model_dir, "batch_size": 16, "total_step": 5, "log_steps": 5,
+                                "device": "cpu", "device_graph": True, "train_node_type": tnt, "seed": 1,
+                                "device_feature_dtype": "fp32", "historical_store": store})
+        est.train()
+        flat = torch.cat([v.reshape(-1).float() for k, v in sorted(m.state_dict().items())])
+        allp = [torch.zeros_like(flat) for _ in range(world)]
+        dist.all_gather(allp, flat)
+        same = all(torch.equal(x, allp[0]) for x in allp)
+        moved = True
+        if store == "replicated":
+            s = m.enc.stores(0).contiguous()
+            alls = [torch.zeros_like(s) for _ in range(world)]
+            dist.all_gather(alls, s)
+            same = same and all(torch.equal(x, alls[0]) for x in alls)
+        q.put((rank, "scalable_dp", bool(same and moved and est.device_trainer.device_trainer_kind == "scalable"
+                                          and est.global_step == 5)))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+
+
+@pytest.mark.parametrize("store", ["replicated", "sharded"])
+def test_scalable_device_path_two_ranks_lockstep(tmp_path, store):
+    res = _run(_worker_scalable_device, str(tmp_path / "ppi"), str(tmp_path / "ck"), store)
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == 2 and all(r[2] for r in res), res
