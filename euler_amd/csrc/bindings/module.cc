@@ -688,6 +688,19 @@ PYBIND11_MODULE(_engine, m) {
            py::arg("q"), py::arg("default_node"), py::arg("seed"))
       .def("dense_feature", &Engine::DenseFeature)
       .def("export_csr", &Engine::ExportCsr)
+      .def(
+          "save",
+          [](Engine& e, const std::string& dir, int partitions, int threads, const std::string& prefix) {
+            Graph& g = e.LocalGraph();
+            Status st;
+            {
+              py::gil_scoped_release nogil;
+              st = SaveReferenceFormat(g, dir, partitions, threads, prefix);
+            }
+            Throw(st);
+          },
+          py::arg("dir"), py::arg("partitions") = 1, py::arg("threads") = 8, py::arg("prefix") = "graph",
+          "write the in-process graph in the Euler on-disk format (euler.meta + Node/Edge partitions)")
       .def("endpoints", [](Engine& e) { return e.Endpoints(); })
       .def("set_replicas", &Engine::SetReplicas, py::arg("shard"), py::arg("endpoints"))
       .def("export_nodes", &Engine::ExportNodes)

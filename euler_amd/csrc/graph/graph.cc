@@ -1,5 +1,7 @@
 #include "graph/graph.h"
 
+#include <cstdio>
+
 #include <algorithm>
 #include <cmath>
 #include <mutex>
@@ -824,6 +826,178 @@ std::unique_ptr<Graph> GraphBuilder::Finish() {
 }
 
 // ============================================================================ synthetic
+// ============================================================================ on-disk writer
+namespace {
+// the feature block of one row: per feature type, the cumulative end offsets (int32, one
+// per column idx) and the concatenated values (reference tools/node.py / edge.py)
+template <typename T>
+void WriteCols(BytesWriter* w, const std::vector<const Column<T>*>& cols, int64_t row) {
+  std::vector<int32_t> idx;
+  std::vector<T> vals;
+  for (const Column<T>* c : cols) {
+    const T* p = nullptr;
+    int64_t n = 0;
+    if (c) c->Get(row, &p, &n);
+    vals.insert(vals.end(), p, p + n);
+    idx.push_back(static_cast<int32_t>(vals.size()));
+  }
+  w->Write(idx);
+  w->Write(vals);
+}
+
+void WriteBinaryCols(BytesWriter* w, const std::vector<const Column<char>*>& cols, int64_t row) {
+  std::vector<int32_t> idx;
+  std::string vals;
+  for (const Column<char>* c : cols) {
+    const char* p = nullptr;
+    int64_t n = 0;
+    if (c) c->Get(row, &p, &n);
+    vals.append(p ? p : "", static_cast<size_t>(n));
+    idx.push_back(static_cast<int32_t>(vals.size()));
+  }
+  w->Write(idx);
+  w->Write(vals);
+}
+
+// one direction's neighbour block: group ids, group weight sums, cumulative group ends,
+// neighbour ids, and weights as ONE prefix sum over the node's whole list
+void WriteAdj(BytesWriter* w, const Adjacency& A, int64_t row, int T) {
+  std::vector<int32_t> gids, gidx;
+  std::vector<float> gw, nw;
+  std::vector<uint64_t> nbrs;
+  float run = 0.f;
+  if (!A.indptr.empty()) {
+    for (int t = 0; t < T; ++t) {
+      const uint64_t a = A.indptr[row * T + t], b = A.indptr[row * T + t + 1];
+      if (b <= a) continue;
+      gids.push_back(t);
+      gw.push_back(A.SegTotal(row * T + t));
+      for (uint64_t k = a; k < b; ++k) {
+        nbrs.push_back(A.nbr[k]);
+        run += A.EdgeWeight(k, a);
+        nw.push_back(run);
+      }
+      gidx.push_back(static_cast<int32_t>(nbrs.size()));
+    }
+  }
+  w->Write(gids);
+  w->Write(gw);
+  w->Write(gidx);
+  w->Write(nbrs);
+  w->Write(nw);
+}
+}  // namespace
+
+Status SaveReferenceFormat(const Graph& g, const std::string& dir, int partitions, int threads,
+                           const std::string& prefix) {
+  if (partitions < 1) return Status::InvalidArgument("partitions must be >= 1");
+  EULER_RETURN_IF_ERROR(MakeDirs(JoinPath(dir, "Node")));
+  EULER_RETURN_IF_ERROR(MakeDirs(JoinPath(dir, "Edge")));
+  GraphMeta m = g.meta();
+  m.partitions_num = static_cast<uint32_t>(partitions);
+  m.node_count = static_cast<uint64_t>(g.num_nodes());
+  m.edge_count = static_cast<uint64_t>(g.num_edges());
+  EULER_RETURN_IF_ERROR(WriteFile(JoinPath(dir, "euler.meta"), m.Serialize()));
+  const int T = std::max(1, g.num_edge_types());
+  auto cols = [&](bool node, FeatureType t) {
+    const int n = m.NumColumns(node, t);
+    std::vector<const void*> out(n, nullptr);
+    for (int i = 0; i < n; ++i) {
+      if (node) out[i] = t == kDense ? static_cast<const void*>(g.NodeDense(i))
+                                     : t == kSparse ? static_cast<const void*>(g.NodeSparse(i))
+                                                    : static_cast<const void*>(g.NodeBinary(i));
+      else out[i] = t == kDense ? static_cast<const void*>(g.EdgeDense(i))
+                                : t == kSparse ? static_cast<const void*>(g.EdgeSparse(i))
+                                               : static_cast<const void*>(g.EdgeBinary(i));
+    }
+    return out;
+  };
+  auto cast_f = [](const std::vector<const void*>& v) {
+    std::vector<const Column<float>*> o;
+    for (auto* p : v) o.push_back(static_cast<const Column<float>*>(p));
+    return o;
+  };
+  auto cast_u = [](const std::vector<const void*>& v) {
+    std::vector<const Column<uint64_t>*> o;
+    for (auto* p : v) o.push_back(static_cast<const Column<uint64_t>*>(p));
+    return o;
+  };
+  auto cast_b = [](const std::vector<const void*>& v) {
+    std::vector<const Column<char>*> o;
+    for (auto* p : v) o.push_back(static_cast<const Column<char>*>(p));
+    return o;
+  };
+  const auto nd = cast_f(cols(true, kDense)), ed = cast_f(cols(false, kDense));
+  const auto ns = cast_u(cols(true, kSparse)), es = cast_u(cols(false, kSparse));
+  const auto nb = cast_b(cols(true, kBinary)), eb = cast_b(cols(false, kBinary));
+  const int64_t N = g.num_nodes(), E = g.num_edges();
+  std::vector<Status> st(static_cast<size_t>(partitions) * 2);
+  ThreadPool pool(std::max(1, std::min(threads, 2 * partitions)));
+  Latch done(2 * partitions);
+  for (int job = 0; job < 2 * partitions; ++job) {
+    pool.Schedule([&, job] {
+      const int part = job % partitions;
+      const bool node = job < partitions;
+      const std::string path = JoinPath(JoinPath(dir, node ? "Node" : "Edge"),
+                                        prefix + "_" + std::to_string(part) + ".dat");
+      const std::string tmp = path + ".tmp";
+      FILE* f = fopen(tmp.c_str(), "wb");
+      if (!f) {
+        st[job] = Status::Internal("cannot create " + tmp);
+        done.CountDown();
+        return;
+      }
+      std::string out;
+      bool io_ok = true;
+      BytesWriter rec;
+      // records stream out in ~32 MB writes: host memory stays one buffer per worker
+      auto flush_rec = [&] {
+        const uint32_t len = static_cast<uint32_t>(rec.str().size());
+        out.append(reinterpret_cast<const char*>(&len), 4);
+        out.append(rec.str());
+        rec.str().clear();
+        if (out.size() >= (size_t{32} << 20)) {
+          io_ok = io_ok && fwrite(out.data(), 1, out.size(), f) == out.size();
+          out.clear();
+        }
+      };
+      if (node) {
+        for (int64_t r = 0; r < N; ++r) {
+          if (static_cast<int>(g.Id(r) % static_cast<uint64_t>(partitions)) != part) continue;
+          rec.Write(g.Id(r));
+          rec.Write(g.NodeType(r));
+          rec.Write(g.NodeWeight(r));
+          WriteAdj(&rec, g.adj(true), r, T);
+          WriteAdj(&rec, g.adj(false), r, T);
+          WriteCols(&rec, ns, r);
+          WriteCols(&rec, nd, r);
+          WriteBinaryCols(&rec, nb, r);
+          flush_rec();
+        }
+      } else {
+        for (int64_t e = 0; e < E; ++e) {
+          if (static_cast<int>(g.EdgeSrc(e) % static_cast<uint64_t>(partitions)) != part) continue;
+          rec.Write(g.EdgeSrc(e));
+          rec.Write(g.EdgeDst(e));
+          rec.Write(g.EdgeType(e));
+          rec.Write(g.EdgeWeight(e));
+          WriteCols(&rec, es, e);
+          WriteCols(&rec, ed, e);
+          WriteBinaryCols(&rec, eb, e);
+          flush_rec();
+        }
+      }
+      io_ok = io_ok && (out.empty() || fwrite(out.data(), 1, out.size(), f) == out.size());
+      io_ok = (fclose(f) == 0) && io_ok;
+      st[job] = io_ok && rename(tmp.c_str(), path.c_str()) == 0 ? Status::OK() : Status::Internal("writing " + path);
+      done.CountDown();
+    });
+  }
+  done.Wait();
+  for (auto& s : st) EULER_RETURN_IF_ERROR(s);
+  return Status::OK();
+}
+
 std::unique_ptr<Graph> SyntheticGraph(int64_t N, double avg_degree, int64_t max_degree, int num_node_types,
                                       int num_edge_types, int feature_dim, int label_dim, uint64_t seed,
                                       bool out_only) {

@@ -126,6 +126,13 @@ class IdMap {
 };
 
 class Graph;
+// Write a graph in the Euler on-disk format (euler.meta + Node/<prefix>_<p>.dat +
+// Edge/<prefix>_<p>.dat, partition = id % partitions, edges with their source) — the
+// byte layout GraphBuilder::LoadReferenceFormat and the reference's loader read
+// (reference euler/tools/json2partdat.py, node.py, edge.py).  Partitions are written by
+// `threads` workers straight from the columnar store (no per-node objects).
+Status SaveReferenceFormat(const Graph& g, const std::string& dir, int partitions, int threads,
+                           const std::string& prefix = "graph");
 std::unique_ptr<Graph> SyntheticGraph(int64_t num_nodes, double avg_degree, int64_t max_degree, int num_node_types,
                                       int num_edge_types, int feature_dim, int label_dim, uint64_t seed,
                                       bool out_only);

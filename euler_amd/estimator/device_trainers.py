@@ -76,9 +76,11 @@ class Ctx:
         if label is not None:
             kw.update(label=label, label_dim=label_dim)
         nt = self.node_type(default_node_type) if node_type is None else node_type
+        # every rank uploads together: with 2+ ranks on a node the export happens once
+        # (local rank 0 into /dev/shm, the others map it: graph/device_graph.py shared_export)
         return DeviceGraph.from_engine(node_type=nt, features=features, feature_dims=feature_dims,
                                        feature_dtype=self.feature_dtype(), seed=self.seed * 7919 + self.est.rank,
-                                       device=self.est.device, **kw)
+                                       device=self.est.device, share=self.est.world > 1, **kw)
 
 
 Builder = Callable[[Ctx], Any]

@@ -19,12 +19,90 @@ counter on the GPU, so a captured hipGraph replays with fresh samples.
 """
 from __future__ import annotations
 
+import time
+
 import numpy as np
 import torch
 
 from euler_amd.ops._native import hip, use_hip
 
 __all__ = ["DeviceGraph", "build_alias_table"]
+
+
+def _export_local(eng, names, dims, label, label_dim):
+    """an in-process engine's graph as host arrays (CSR in engine row order, node table,
+    the dense feature / label columns)"""
+    indptr, nbr, w, T, ids, _ = eng.export_csr()
+    _, types, nw = eng.export_nodes()
+    out = {"indptr": indptr, "nbr": nbr, "w": w, "T": np.asarray([int(T)], np.int64), "ids": ids, "types": types,
+           "nw": nw}
+    if names:
+        out["features"] = np.concatenate([np.asarray(eng.dense_feature(ids, "dense_" + str(n), int(d)), np.float32)
+                                          for n, d in zip(names, dims)], 1)
+    if label is not None:
+        out["labels"] = np.asarray(eng.dense_feature(ids, "dense_" + str(label), int(label_dim)), np.float32)
+    return out
+
+
+def shared_export(fn):
+    """``(arrays, done)``: ``fn()``'s arrays, computed ONCE per node when several data-
+    parallel ranks share it (torch.distributed initialised, LOCAL_WORLD_SIZE > 1): local
+    rank 0 writes them as .npy files under /dev/shm, every local rank maps them read-only
+    (``numpy.load(mmap_mode="r")``: one physical copy in the page cache, no per-rank host
+    copy).  ``done()`` synchronises the ranks and removes the files.  Without peers it is
+    ``fn()`` and a no-op."""
+    import os
+    import shutil
+
+    import torch.distributed as dist
+
+    on = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", dist.get_world_size() if on else 1))
+    if not on or local_world <= 1 or os.environ.get("EULER_AMD_SHARED_EXPORT", "1") == "0":
+        return fn(), (lambda: None)
+    local_rank = int(os.environ.get("LOCAL_RANK", dist.get_rank()))
+    name = ["/dev/shm/euler_amd_export_%d_%d" % (os.getpid(), int(time.time() * 1e3))] if dist.get_rank() == 0 \
+        else [None]
+    dist.broadcast_object_list(name, src=0)
+    d = name[0]
+    if local_rank == 0:
+        arrays = fn()
+        os.makedirs(d, exist_ok=True)
+        for k, v in arrays.items():
+            np.save(os.path.join(d, k + ".tmp.npy"), np.asarray(v))
+            os.replace(os.path.join(d, k + ".tmp.npy"), os.path.join(d, k + ".npy"))
+        keys = sorted(arrays)
+        del arrays
+        with open(os.path.join(d, "KEYS"), "w") as f:
+            f.write("\n".join(keys))
+    dist.barrier()
+    with open(os.path.join(d, "KEYS")) as f:
+        keys = [k for k in f.read().split("\n") if k]
+    mapped = {k: np.load(os.path.join(d, k + ".npy"), mmap_mode="r", allow_pickle=False) for k in keys}
+
+    def done():
+        dist.barrier()
+        if local_rank == 0:
+            shutil.rmtree(d, ignore_errors=True)
+
+    return mapped, done
+
+
+_UPLOAD_CHUNK = 1 << 26  # elements per host -> device chunk
+
+
+def _upload(a, dtype, device) -> torch.Tensor:
+    """``a`` (numpy, possibly a read-only memory map, or a tensor) as a ``dtype`` tensor on
+    ``device``, converted and copied ``_UPLOAD_CHUNK`` elements at a time"""
+    if isinstance(a, torch.Tensor):
+        return a.to(device=device, dtype=dtype).contiguous()
+    a = np.asarray(a).reshape(-1)
+    out = torch.empty(a.shape[0], dtype=dtype, device=device)
+    npd = {torch.int64: np.int64, torch.int32: np.int32, torch.float32: np.float32, torch.float64: np.float64}[dtype]
+    for s in range(0, a.shape[0], _UPLOAD_CHUNK):
+        chunk = np.array(a[s: s + _UPLOAD_CHUNK], dtype=npd)  # one bounded host copy (also un-maps)
+        out[s: s + chunk.shape[0]].copy_(torch.from_numpy(chunk))
+    return out
 
 
 def build_alias_table(weights: np.ndarray):
@@ -99,23 +177,28 @@ class DeviceGraph:
 
     @classmethod
     def from_csr(cls, indptr, nbr, weights, num_types=1, node_weights=None, ids=None, seed=0, device="cuda"):
-        """From host CSR arrays with *raw* edge weights (prefix sums computed here per segment)."""
-        indptr_t = torch.as_tensor(np.asarray(indptr), dtype=torch.int64)
-        w = torch.as_tensor(np.asarray(weights), dtype=torch.float64)
-        cs = torch.cumsum(w, 0)
+        """From host CSR arrays with *raw* edge weights (prefix sums computed per segment on
+        the target device).  The arrays are uploaded in bounded chunks (``_upload``): host
+        memory stays the caller's arrays — which may be memory-mapped shared exports."""
+        device = torch.device(device)
+        indptr_t = _upload(indptr, torch.int64, device)
+        w = _upload(weights, torch.float32, device)
+        cs = torch.cumsum(w.double(), 0)
+        del w
         seg_start = torch.repeat_interleave(indptr_t[:-1], torch.diff(indptr_t))
-        base = torch.cat([torch.zeros(1, dtype=torch.float64), cs])[seg_start]
+        base = torch.cat([torch.zeros(1, dtype=torch.float64, device=device), cs])[seg_start]
+        del seg_start
         cumw = (cs - base).float()
+        del cs, base
         prob = alias = None
         if node_weights is not None:
             prob, alias = build_alias_table(np.asarray(node_weights))
             prob, alias = torch.from_numpy(prob), torch.from_numpy(alias)
-        return cls(indptr_t, torch.as_tensor(np.asarray(nbr), dtype=torch.int32), cumw, num_types, prob, alias,
-                   ids, seed, device)
+        return cls(indptr_t, _upload(nbr, torch.int32, device), cumw, num_types, prob, alias, ids, seed, device)
 
     @classmethod
     def from_engine(cls, engine=None, node_type=-1, features=(), feature_dims=(), label=None, label_dim=None,
-                    feature_dtype=torch.bfloat16, seed=0, device="cuda"):
+                    feature_dtype=torch.bfloat16, seed=0, device="cuda", share=False):
         """Upload the engine's local graph shard to HBM.
 
         The C++ engine's columnar store (``csrc/graph``) is already a per-(row, edge type)
@@ -126,7 +209,11 @@ class DeviceGraph:
         ``feature_dtype``) and the dense ``label`` column as device tables.  Rows are the
         engine's rows (sorted by node id); :meth:`rows_of` maps raw ids to rows.  A sharded
         engine (remote shard servers, local_sharded) is assembled from every shard's export
-        (:meth:`_from_shards`): one GPU's 288 GB of HBM holds the whole graph."""
+        (:meth:`_from_shards`): one GPU's 288 GB of HBM holds the whole graph.
+
+        ``share=True`` (every data-parallel rank calls this together, as the estimator's
+        device path does): local rank 0 exports once into /dev/shm and every local rank
+        uploads from the shared read-only mapping (:func:`shared_export`)."""
         from euler_amd.ops import base
 
         eng = engine if engine is not None else base.get_engine()
@@ -134,18 +221,23 @@ class DeviceGraph:
         dims = [] if not features else ([feature_dims] if isinstance(feature_dims, int) else list(feature_dims))
         if getattr(eng, "mode", "local") != "local":
             return cls._from_shards(eng, node_type, names, dims, label, label_dim, feature_dtype, seed, device)
-        indptr, nbr, w, T, ids, _ = eng.export_csr()
-        _, types, nw = eng.export_nodes()
-        g = cls.from_csr(indptr, nbr, w, int(T), ids=np.asarray(ids), seed=seed, device=device)
-        g.node_types = np.asarray(types)
-        g.set_root_type(node_type, node_weights=np.asarray(nw))
-        if names:
-            cols = [np.asarray(eng.dense_feature(g.ids, "dense_" + str(n), int(d)), np.float32)
-                    for n, d in zip(names, dims)]
-            g.features = torch.from_numpy(np.concatenate(cols, 1)).to(device=device, dtype=feature_dtype)
-        if label is not None:
-            lab = np.asarray(eng.dense_feature(g.ids, "dense_" + str(label), int(label_dim)), np.float32)
-            g.labels = torch.from_numpy(lab).to(device)
+        # data-parallel ranks on one node: local rank 0 exports once into /dev/shm, every rank
+        # maps it (host memory does not grow with the number of ranks)
+        export = (lambda: _export_local(eng, names, dims, label, label_dim))
+        arrays, done = shared_export(export) if share else (export(), lambda: None)
+        try:
+            ids = np.array(arrays["ids"])
+            g = cls.from_csr(arrays["indptr"], arrays["nbr"], arrays["w"], int(np.asarray(arrays["T"])[0]), ids=ids,
+                             seed=seed, device=device)
+            g.node_types = np.array(arrays["types"])
+            g.set_root_type(node_type, node_weights=np.asarray(arrays["nw"]))
+            if names:
+                g.features = _upload(arrays["features"], torch.float32, device).view(len(ids), -1).to(feature_dtype)
+            if label is not None:
+                g.labels = _upload(arrays["labels"], torch.float32, device).view(len(ids), -1)
+        finally:
+            del arrays
+            done()
         return g
 
     @classmethod
@@ -162,7 +254,9 @@ class DeviceGraph:
         ids = np.concatenate([np.asarray(p[0], np.uint64) for p in parts])
         types = np.concatenate([np.asarray(p[1], np.int32) for p in parts])
         nw = np.concatenate([np.asarray(p[2], np.float32) for p in parts])
-        T = max(1, (len(parts[0][3]) - 1) // max(len(parts[0][0]), 1)) if len(parts[0][0]) else 1
+        # the edge-type count from the first shard that holds nodes (an empty shard says nothing)
+        first = next((p for p in parts if len(p[0])), None)
+        T = max(1, (len(first[3]) - 1) // len(first[0])) if first is not None else 1
         for p in parts:
             if len(p[0]) and (len(p[3]) - 1) != len(p[0]) * T:
                 raise ValueError("shards disagree on the number of edge types")

@@ -12,8 +12,8 @@
 from euler_amd.models.graph_classification import GIN, GatedGraph, GraphGCN, Set2SetModel  # noqa: F401
 from euler_amd.models.knowledge_graph import DistMult, TransD, TransE, TransH, TransR  # noqa: F401
 from euler_amd.models.node_classification import (  # noqa: F401
-    AGNN, APPNP, ARMA, DNA, GAT, LGCN, SGCN, TAGCN, AdaptiveGCN, FastGCN, GeniePath, SupervisedGCN,
-    SupervisedGNN, SupervisedGraphSage)
+    AGNN, APPNP, ARMA, DNA, GAT, LGCN, SGCN, TAGCN, AdaptiveGCN, FastGCN, GeniePath, ScalableGCN, ScalableSage,
+    SupervisedGCN, SupervisedGNN, SupervisedGraphSage)
 from euler_amd.models.unsupervised import (  # noqa: F401
     DGI, DeepWalk, GraphAutoEncoder, Line, Node2Vec, UnsupervisedGraphSage, UnsupervisedRGCN,
     VariationalGraphAutoEncoder)

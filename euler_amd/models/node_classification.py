@@ -32,7 +32,7 @@ from euler_amd.mp_utils.models import BaseGNNNet, SuperviseModel
 from euler_amd.utils import encoders
 
 __all__ = ["FeatureGNN", "SupervisedGraphSage", "SupervisedGCN", "GAT", "FastGCN", "AdaptiveGCN", "AGNN", "APPNP",
-           "ARMA", "DNA", "SGCN", "TAGCN", "GeniePath", "LGCN", "SupervisedGNN"]
+           "ARMA", "DNA", "SGCN", "TAGCN", "GeniePath", "LGCN", "SupervisedGNN", "ScalableSage", "ScalableGCN"]
 
 
 def _lst(x):
@@ -166,3 +166,36 @@ class LGCN(SuperviseModel):
 
     def embed(self, n_id):
         return self._encoder(n_id)
+
+
+class ScalableSage(SuperviseModel):
+    """Supervised node classification over ``ScalableSageEncoder`` (reference
+    tf_euler/python/utils/encoders.py:629-748): one sampled hop per step, deeper layers from
+    per-layer stores of stale embeddings (device path: models/scalable_trainer.py)."""
+
+    def __init__(self, edge_type, fanout, num_layers, dim, label_idx, label_dim, feature_idx, feature_dim, max_id,
+                 aggregator="mean", store_learning_rate=0.001, metric_name="f1"):
+        super().__init__(label_idx, label_dim, metric_name)
+        self._encoder = encoders.ScalableSageEncoder(edge_type, fanout, num_layers, dim, aggregator=aggregator,
+                                                     feature_idx=feature_idx, feature_dim=feature_dim, max_id=max_id,
+                                                     store_learning_rate=store_learning_rate)
+
+    def embed(self, n_id):
+        return self._encoder(n_id)
+
+
+class ScalableGCN(SuperviseModel):
+    """Supervised node classification over ``ScalableGCNEncoder`` (reference
+    tf_euler/python/utils/encoders.py:294-408): the roots' full 1-hop neighbourhood per step,
+    deeper layers from stale-embedding stores."""
+
+    def __init__(self, edge_type, num_layers, dim, label_idx, label_dim, feature_idx, feature_dim, max_id,
+                 aggregator="mean", store_learning_rate=0.001, metric_name="f1"):
+        super().__init__(label_idx, label_dim, metric_name)
+        self._encoder = encoders.ScalableGCNEncoder(edge_type, num_layers, dim, aggregator=aggregator,
+                                                    feature_idx=feature_idx, feature_dim=feature_dim, max_id=max_id,
+                                                    store_learning_rate=store_learning_rate)
+
+    def embed(self, n_id):
+        return self._encoder(n_id)
+

@@ -139,6 +139,12 @@ def _models():
                                                                    ds.num_classes, ds.sparse_fea_idx,
                                                                    ds.sparse_fea_max_id)),
         "solution": ("cora", "node", _solution),
+        "scalable_sage": ("ppi", "node", lambda a, ds: Z.ScalableSage(_mp(a, 1)[0], a.fanouts[0], a.layers,
+                                                                      a.hidden_dim, ds.label_idx, ds.label_dim,
+                                                                      ds.feature_idx, F(ds), ds.max_node_id)),
+        "scalable_gcn": ("ppi", "node", lambda a, ds: Z.ScalableGCN(_mp(a, 1)[0], a.layers, a.hidden_dim,
+                                                                    ds.label_idx, ds.label_dim, ds.feature_idx,
+                                                                    F(ds), ds.max_node_id)),
     }
 
 

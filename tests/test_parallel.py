@@ -982,3 +982,50 @@ def test_scalable_device_path_two_ranks_lockstep(tmp_path, store):
     res = _run(_worker_scalable_device, str(tmp_path / "ppi"), str(tmp_path / "ck"), store)
     assert not [r for r in res if r[1] == "error"], res
     assert len(res) == 2 and all(r[2] for r in res), res
+
+
+def _worker_shared_export(rank, world, port, q, data_dir):
+    """DeviceGraph.from_engine(share=True) on 2 ranks of one node: only local rank 0 runs
+    the engine export; both ranks build the same graph as an unshared upload; the shared
+    files are gone afterwards"""
+    try:
+        _init(rank, world, port)
+        import glob
+
+        import euler_amd as ea
+        import euler_amd.graph.device_graph as DG
+        from euler_amd.dataset import get_dataset
+
+        ds = get_dataset("cora", data_dir=data_dir, scale=0.05)
+        ds.load_graph()
+        ea.set_seed(3)
+        calls = []
+        orig = DG._export_local
+
+        def counting(*a):
+            calls.append(1)
+            return orig(*a)
+
+        DG._export_local = counting
+        kw = dict(features=["feature"], feature_dims=[1433], label="label", label_dim=ds.label_dim,
+                  feature_dtype=torch.float32, seed=1, device="cpu")
+        g = DG.DeviceGraph.from_engine(share=True, **kw)
+        n_shared = len(calls)
+        ref = DG.DeviceGraph.from_engine(**kw)
+        same = all(torch.equal(a, b) for a, b in ((g.indptr, ref.indptr), (g.nbr, ref.nbr), (g.cumw, ref.cumw),
+                                                  (g.features, ref.features), (g.labels, ref.labels)))
+        same = same and np.array_equal(g.ids, ref.ids)
+        dist.barrier()
+        left = glob.glob("/dev/shm/euler_amd_export_*")
+        q.put((rank, "shared_export", bool(same and n_shared == (1 if rank == 0 else 0)), left))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_device_graph_shared_export_once_per_node(tmp_path):
+    res = _run(_worker_shared_export, str(tmp_path / "cora"))
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == 2 and all(r[2] for r in res), res
