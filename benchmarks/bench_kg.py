@@ -88,6 +88,8 @@ def main(argv=None):
     p.add_argument("--self-drop", type=float, default=0.0,
                    help="R-GCN self-loop dropout while training; cold entities (never in a loss triple) are then "
                         "placed by their neighbours alone at evaluation (inductive)")
+    p.add_argument("--deterministic", action="store_true",
+                   help="atomic-free, bit-reproducible fused step (occurrence rows + fixed-order sums)")
     p.add_argument("--no-graph", action="store_true", help="eager steps (default: one hipGraph per step)")
     p.add_argument("--fused", type=int, default=1,
                    help="1: the fused step (models/rgcn_kg_step.py: hand-written launches only, Philox draws in the "
@@ -228,7 +230,8 @@ def main(argv=None):
     fused = None
     if args.fused and dev.type == "cuda" and not (args.type_negs and args.task == "types") and args.dim % 8 == 0:
         fused = RgcnTransEStep(model, flat, opt, edge_index, edge_rel, (src, rel, dst), pool, args.batch,
-                               args.num_negs, seed=args.seed * 7919 + rank, grad_sync=grad_sync)
+                               args.num_negs, seed=args.seed * 7919 + rank, grad_sync=grad_sync,
+                               deterministic=args.deterministic)
         loss_buf = fused.loss
 
     def step_body():
@@ -330,6 +333,7 @@ def main(argv=None):
                        "lr": args.lr, "margin": args.margin, "num_bases": args.num_bases, "rel_wd": args.rel_wd,
                        "self_drop": args.self_drop, "type_negs": bool(args.type_negs),
                        "step": "fused (hand-written launches, Philox draws)" if fused is not None else "autograd",
+                       "deterministic": bool(fused is not None and fused.deterministic),
                        "parallelism": f"dp{world}", "loss_first_last": [round(first, 4), round(last, 4)],
                        "grad_sync": sync_name, "grad_sync_choice": sync_info or None,
                        "heldout_tail_ranking": {"triples": int(te_src.numel()), "entities": args.num_ent,

@@ -282,7 +282,7 @@ std::vector<torch::Tensor> segment_reduce(torch::Tensor src, torch::Tensor indpt
 
 // wave-per-segment sum / mean (skewed segment lengths); D / (8 bf16 | 4 fp32) a power of two <= 64
 torch::Tensor segment_reduce_wave(torch::Tensor src, torch::Tensor indptr, c10::optional<torch::Tensor> perm,
-                                  int64_t op) {
+                                  int64_t op, c10::optional<torch::Tensor> out_) {
   need_cuda(src, "src");
   need_i64(indptr, "indptr");
   const bool bf = is_bf16(src, "src");
@@ -296,7 +296,15 @@ torch::Tensor segment_reduce_wave(torch::Tensor src, torch::Tensor indptr, c10::
   TORCH_CHECK(D % (bf ? 8 : 4) == 0 && LP <= 64 && (LP & (LP - 1)) == 0,
               "segment_reduce_wave needs D / (8 bf16 | 4 fp32) to be a power of two <= 64");
   const c10::DeviceGuard g(src.device());
-  auto out = torch::empty({S, D}, src.options());
+  torch::Tensor out;
+  if (out_.has_value()) {  // written in place (every row: empty segments get zeros)
+    out = *out_;
+    TORCH_CHECK(out.scalar_type() == src.scalar_type() && out.is_contiguous() && out.dim() == 2 &&
+                    out.size(0) == S && out.size(1) == D && out.device() == src.device(),
+                "segment_reduce_wave: out must be a contiguous [S, D] tensor like src");
+  } else {
+    out = torch::empty({S, D}, src.options());
+  }
   check(eh_segment_reduce_wave(src.data_ptr(), bf, static_cast<int>(D), indptr.data_ptr<int64_t>(),
                                perm.has_value() ? perm->data_ptr<int64_t>() : nullptr, S, static_cast<int>(op),
                                out.data_ptr(), cur_stream()),
@@ -595,7 +603,8 @@ PYBIND11_MODULE(_hip_ops, m) {
   m.def("relu_bwd_", &relu_bwd_);
   m.def("gather_rows", &gather_rows);
   m.def("segment_reduce", &segment_reduce);
-  m.def("segment_reduce_wave", &segment_reduce_wave);
+  m.def("segment_reduce_wave", &segment_reduce_wave, py::arg("src"), py::arg("indptr"), py::arg("perm"), py::arg("op"),
+        py::arg("out") = py::none());
   m.def("index_add_rows_", &index_add_rows_);
   m.def("max_bwd", &max_bwd);
   m.def("edge_softmax", &edge_softmax);

@@ -215,7 +215,9 @@ std::vector<torch::Tensor> rel_weight_bf16(torch::Tensor W) {
 
 void rel_gemm_dw(torch::Tensor G, torch::Tensor g_idx, torch::Tensor X, torch::Tensor x_idx,
                  c10::optional<torch::Tensor> scale, torch::Tensor trel, torch::Tensor tstart, torch::Tensor tlen,
-                 c10::optional<torch::Tensor> solo, torch::Tensor dW, bool accumulate) {
+                 c10::optional<torch::Tensor> solo, torch::Tensor dW, bool accumulate,
+                 c10::optional<torch::Tensor> slot, c10::optional<torch::Tensor> part,
+                 c10::optional<torch::Tensor> mrel, c10::optional<torch::Tensor> mrp) {
   typed(G, torch::kBFloat16, "G");
   typed(X, torch::kBFloat16, "X");
   typed(g_idx, torch::kInt32, "g_idx");
@@ -235,12 +237,32 @@ void rel_gemm_dw(torch::Tensor G, torch::Tensor g_idx, torch::Tensor X, torch::T
     typed(*solo, torch::kInt32, "solo");
     TORCH_CHECK(solo->numel() == trel.numel(), "solo must hold one flag per chunk");
   }
+  // deterministic mode: chunk -> partial slot (-1 for solo chunks), the slot buffer, and
+  // the multi-chunk relations with their slot ranges (mrp: CSR over mrel)
+  const int32_t *sl = nullptr, *mr = nullptr, *mp = nullptr;
+  float* pp = nullptr;
+  int nmulti = 0;
+  if (slot.has_value()) {
+    TORCH_CHECK(solo.has_value() && part.has_value() && mrel.has_value() && mrp.has_value(),
+                "deterministic rel_gemm_dw needs solo, slot, part, mrel and mrp");
+    typed(*slot, torch::kInt32, "slot");
+    typed(*mrel, torch::kInt32, "mrel");
+    typed(*mrp, torch::kInt32, "mrp");
+    typed(*part, torch::kFloat32, "part");
+    TORCH_CHECK(slot->numel() == trel.numel() && mrp->numel() == mrel->numel() + 1, "slot / mrp sizes");
+    TORCH_CHECK(part->dim() == 3 && part->size(1) == N && part->size(2) == K, "part must be [slots, N, K]");
+    sl = slot->data_ptr<int32_t>();
+    mr = mrel->data_ptr<int32_t>();
+    mp = mrp->data_ptr<int32_t>();
+    pp = part->data_ptr<float>();
+    nmulti = static_cast<int>(mrel->numel());
+  }
   const c10::DeviceGuard g(G.device());
   ok(eh_rel_gemm_dw(G.data_ptr(), static_cast<int>(N), g_idx.data_ptr<int32_t>(), X.data_ptr(), static_cast<int>(K),
                     x_idx.data_ptr<int32_t>(), scale.has_value() ? scale->data_ptr<float>() : nullptr,
                     trel.data_ptr<int32_t>(), tstart.data_ptr<int32_t>(), tlen.data_ptr<int32_t>(),
                     solo.has_value() ? solo->data_ptr<int32_t>() : nullptr, static_cast<int>(trel.numel()),
-                    dW.data_ptr<float>(), accumulate ? 1 : 0, stream()),
+                    dW.data_ptr<float>(), accumulate ? 1 : 0, stream(), sl, pp, mr, mp, nmulti),
      "rel_gemm_dw");
 }
 
@@ -542,7 +564,8 @@ void kg_step(torch::Tensor h, torch::Tensor rel, torch::Tensor pool, torch::Tens
              torch::Tensor t_rel, torch::Tensor step, int64_t seed, int64_t kind, bool normalize, double margin,
              torch::Tensor o_src, torch::Tensor o_dst, torch::Tensor o_ridx, torch::Tensor o_neg, torch::Tensor coef,
              torch::Tensor part, torch::Tensor loss, torch::Tensor dent, torch::Tensor drel,
-             c10::optional<torch::Tensor> drel_rep) {
+             c10::optional<torch::Tensor> drel_rep, c10::optional<torch::Tensor> occ_e,
+             c10::optional<torch::Tensor> occ_r) {
   for (auto* t : {&h, &rel, &coef, &part, &loss, &dent, &drel}) typed(*t, torch::kFloat32, "kg_step float buffer");
   for (auto* t : {&pool, &t_src, &t_dst, &t_rel, &step, &o_src, &o_dst, &o_ridx, &o_neg})
     typed(*t, torch::kInt64, "kg_step id buffer");
@@ -568,6 +591,17 @@ void kg_step(torch::Tensor h, torch::Tensor rel, torch::Tensor pool, torch::Tens
     rep_p = drel_rep->data_ptr<float>();
     rep = static_cast<int>(drel_rep->size(0));
   }
+  // deterministic mode: per-occurrence gradient rows instead of atomics (the caller sums
+  // them per entity / relation in a fixed order): occ_e [B * (2 + K), D], occ_r [B, D]
+  float *oe = nullptr, *orr = nullptr;
+  if (occ_e.has_value() || occ_r.has_value()) {
+    TORCH_CHECK(occ_e.has_value() && occ_r.has_value(), "kg_step: occ_e and occ_r go together");
+    typed(*occ_e, torch::kFloat32, "occ_e");
+    typed(*occ_r, torch::kFloat32, "occ_r");
+    TORCH_CHECK(occ_e->numel() == B * (2 + K) * D && occ_r->numel() == B * D, "kg_step: occ_e [B(2+K), D], occ_r [B, D]");
+    oe = occ_e->data_ptr<float>();
+    orr = occ_r->data_ptr<float>();
+  }
   TORCH_CHECK(part.numel() >= nparts, "kg_step: part needs ", nparts, " entries");
   TORCH_CHECK(pool.numel() > 0 && loss.numel() >= 1 && step.numel() >= 1, "kg_step: empty pool / loss / step");
   const c10::DeviceGuard g(h.device());
@@ -577,7 +611,7 @@ void kg_step(torch::Tensor h, torch::Tensor rel, torch::Tensor pool, torch::Tens
                 static_cast<int>(kind), normalize ? 1 : 0, static_cast<float>(margin), o_src.data_ptr<int64_t>(),
                 o_dst.data_ptr<int64_t>(), o_ridx.data_ptr<int64_t>(), o_neg.data_ptr<int64_t>(),
                 coef.data_ptr<float>(), part.data_ptr<float>(), loss.data_ptr<float>(), dent.data_ptr<float>(),
-                drel.data_ptr<float>(), nullptr, rep_p, rep, rel.size(0), stream()),
+                drel.data_ptr<float>(), nullptr, rep_p, rep, rel.size(0), stream(), oe, orr),
      "kg_step");
 }
 
@@ -1067,7 +1101,8 @@ void register_gnn_ops(pybind11::module& m) {
   m.def("rel_gemm", &rel_gemm);
   m.def("rel_gemm_dw", &rel_gemm_dw, py::arg("G"), py::arg("g_idx"), py::arg("X"), py::arg("x_idx"), py::arg("scale"),
         py::arg("trel"), py::arg("tstart"), py::arg("tlen"), py::arg("solo"), py::arg("dW"),
-        py::arg("accumulate") = false);
+        py::arg("accumulate") = false, py::arg("slot") = py::none(), py::arg("part") = py::none(),
+        py::arg("mrel") = py::none(), py::arg("mrp") = py::none());
   m.def("rel_weight_bf16", &rel_weight_bf16);
   m.attr("rel_gemm_dw_chunk") = eh_rel_gemm_dw_chunk();
   m.attr("rel_gemm_tile") = eh_rel_gemm_tile();
@@ -1082,7 +1117,8 @@ void register_gnn_ops(pybind11::module& m) {
   m.def("kg_step", &kg_step, py::arg("h"), py::arg("rel"), py::arg("pool"), py::arg("t_src"), py::arg("t_dst"),
         py::arg("t_rel"), py::arg("step"), py::arg("seed"), py::arg("kind"), py::arg("normalize"), py::arg("margin"),
         py::arg("o_src"), py::arg("o_dst"), py::arg("o_ridx"), py::arg("o_neg"), py::arg("coef"), py::arg("part"),
-        py::arg("loss"), py::arg("dent"), py::arg("drel"), py::arg("drel_rep") = py::none());
+        py::arg("loss"), py::arg("dent"), py::arg("drel"), py::arg("drel_rep") = py::none(),
+        py::arg("occ_e") = py::none(), py::arg("occ_r") = py::none());
   m.def("kg_step_parts", &kg_step_parts);
   m.def("cast_bf16", &cast_bf16);
   m.def("drop_rows", &drop_rows);

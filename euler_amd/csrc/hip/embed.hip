@@ -661,7 +661,7 @@ __global__ __launch_bounds__(256) void kg_step_fwd_kernel(KgStepArgs s) {
 }
 
 __global__ __launch_bounds__(256) void kg_step_bwd_kernel(KgStepArgs s, float* __restrict__ dent,
-                                                          float* __restrict__ drel) {
+                                                          float* __restrict__ drel, int occ) {
   const KgArgs& a = s.k;
   if (blockIdx.x == 0) {  // the step's loss: partial sums in a fixed order
     __shared__ float red[256];
@@ -678,7 +678,14 @@ __global__ __launch_bounds__(256) void kg_step_bwd_kernel(KgStepArgs s, float* _
   const RowLane L = row_lane(a.lp, a.B);
   if (!L.ok) return;
   const float c = s.coef[L.row];
-  if (c == 0.f) return;  // whole lane group: the margin holds, no gradient
+  if (c == 0.f) {  // whole lane group: the margin holds, no gradient
+    if (occ && L.sub * 4 < a.D) {  // deterministic mode: this triple's occurrence rows are zero
+      const float z[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < 2 + a.K; ++k) EV<float>::store(dent + (L.row * (2 + a.K) + k) * a.D + L.sub * 4, z);
+      EV<float>::store(drel + L.row * a.D + L.sub * 4, z);
+    }
+    return;
+  }
   const float gp = -c, gn = c / static_cast<float>(2 * a.K);
   float h[4], r[4], t[4], n[4], nh, nr, nt, nn;
   float dh[4] = {0.f, 0.f, 0.f, 0.f}, dr[4] = {0.f, 0.f, 0.f, 0.f}, dt[4] = {0.f, 0.f, 0.f, 0.f};
@@ -693,14 +700,19 @@ __global__ __launch_bounds__(256) void kg_step_bwd_kernel(KgStepArgs s, float* _
     float dn[4] = {0.f, 0.f, 0.f, 0.f};
     kg_grad(a.kind, a.lp, gn, n, r, t, dn, dr, dt);
     kg_grad(a.kind, a.lp, gn, h, r, n, dh, dr, dn);
-    kg_scatter(dent, ns, L.sub, a.D, a.lp, a.normalize, n, nn, dn);
+    // deterministic mode: occurrence rows [h, t, neg_0 .. neg_{K-1}] per triple (summed per
+    // entity later in a fixed order), else fp32 atomics into the table gradient
+    kg_scatter(dent, occ ? L.row * (2 + a.K) + 2 + k : ns, L.sub, a.D, a.lp, a.normalize, n, nn, dn, occ);
   }
-  kg_scatter(dent, hs, L.sub, a.D, a.lp, a.normalize, h, nh, dh);
+  kg_scatter(dent, occ ? L.row * (2 + a.K) : hs, L.sub, a.D, a.lp, a.normalize, h, nh, dh, occ);
   // relation rows: the power-law relation table makes a few of them hot; with replicas each
   // block adds into its own copy (blockIdx % rep), summed by kg_rep_reduce_kernel
-  kg_scatter(s.rep ? s.drel_rep + static_cast<int64_t>(blockIdx.x % s.rep) * s.rep_stride : drel, rs, L.sub, a.D,
-             a.lp, a.normalize, r, nr, dr);
-  kg_scatter(dent, ts, L.sub, a.D, a.lp, a.normalize, t, nt, dt);
+  if (occ)
+    kg_scatter(drel, L.row, L.sub, a.D, a.lp, a.normalize, r, nr, dr, true);
+  else
+    kg_scatter(s.rep ? s.drel_rep + static_cast<int64_t>(blockIdx.x % s.rep) * s.rep_stride : drel, rs, L.sub, a.D,
+               a.lp, a.normalize, r, nr, dr);
+  kg_scatter(dent, occ ? L.row * (2 + a.K) + 1 : ts, L.sub, a.D, a.lp, a.normalize, t, nt, dt, occ);
 }
 
 // self-loop dropout of the R-GCN step: keep_i = [u01(Philox(seed, step, salt * 2^40 + i))
@@ -1030,7 +1042,8 @@ hipError_t eh_kg_step(const float* ent, const float* rel, const int64_t* pool, i
                       const int64_t* t_dst, const int64_t* t_rel, int64_t num_ent, const int64_t* step, uint64_t seed,
                       int64_t B, int K, int D, int kind, int normalize, float margin, int64_t* o_src, int64_t* o_dst,
                       int64_t* o_ridx, int64_t* o_neg, float* coef, float* part, float* loss, float* dent,
-                      float* drel, int* nparts_out, float* drel_rep, int rep, int64_t num_rel, hipStream_t s) {
+                      float* drel, int* nparts_out, float* drel_rep, int rep, int64_t num_rel, hipStream_t s,
+                      float* occ_e, float* occ_r) {
   if (B <= 0 || K <= 0 || K > 255 || P <= 0 || num_ent <= 0 || rep < 0) return hipErrorInvalidValue;
   if (D % 4 != 0 || D > 256 || kind < 0 || kind > 2) return hipErrorInvalidValue;
   KgStepArgs a;
@@ -1055,12 +1068,15 @@ hipError_t eh_kg_step(const float* ent, const float* rel, const int64_t* pool, i
   a.part = part;
   a.loss = loss;
   a.nparts = static_cast<int>(grid.x);
-  a.rep = drel_rep ? rep : 0;
+  const bool occ = occ_e != nullptr;
+  if (occ && !occ_r) return hipErrorInvalidValue;
+  a.rep = drel_rep && !occ ? rep : 0;
   a.drel_rep = drel_rep;
   a.rep_stride = num_rel * D;
   if (a.rep) EULER_HIP_CHECK(eh_zero(drel_rep, a.rep * a.rep_stride * 4, s));
   hipLaunchKernelGGL(kg_step_fwd_kernel, grid, dim3(256), 0, s, a);
-  hipLaunchKernelGGL(kg_step_bwd_kernel, grid, dim3(256), 0, s, a, dent, drel);
+  hipLaunchKernelGGL(kg_step_bwd_kernel, grid, dim3(256), 0, s, a, occ ? occ_e : dent, occ ? occ_r : drel,
+                     occ ? 1 : 0);
   if (a.rep)
     hipLaunchKernelGGL(kg_rep_reduce_kernel, grid_for(a.rep_stride), dim3(256), 0, s, drel_rep, a.rep, a.rep_stride,
                        drel);

@@ -83,7 +83,9 @@ hipError_t eh_rel_gemm(const void* A, int K, const int32_t* a_idx, const int32_t
                        const int32_t* o_idx, int mode, int tm, void* Y, hipStream_t s);
 hipError_t eh_rel_gemm_dw(const void* G, int N, const int32_t* g_idx, const void* X, int K, const int32_t* x_idx,
                           const float* scale, const int32_t* crel, const int32_t* cstart, const int32_t* clen,
-                          const int32_t* csolo, int n_chunks, float* dW, int accum, hipStream_t s);
+                          const int32_t* csolo, int n_chunks, float* dW, int accum, hipStream_t s,
+                          const int32_t* cslot = nullptr, float* part = nullptr, const int32_t* mrel = nullptr,
+                          const int32_t* mrp = nullptr, int n_multi = 0);
 
 // embed.hip (K10 knowledge-graph scores, K11 skip-gram sigmoid-CE)
 hipError_t eh_sgns_fwd(const void* emb, const void* pos, const void* neg, int is_bf16, int64_t B, int P, int K, int D,
@@ -115,7 +117,8 @@ hipError_t eh_kg_step(const float* ent, const float* rel, const int64_t* pool, i
                       const int64_t* t_dst, const int64_t* t_rel, int64_t num_ent, const int64_t* step, uint64_t seed,
                       int64_t B, int K, int D, int kind, int normalize, float margin, int64_t* o_src, int64_t* o_dst,
                       int64_t* o_ridx, int64_t* o_neg, float* coef, float* part, float* loss, float* dent,
-                      float* drel, int* nparts_out, float* drel_rep, int rep, int64_t num_rel, hipStream_t s);
+                      float* drel, int* nparts_out, float* drel_rep, int rep, int64_t num_rel, hipStream_t s,
+                      float* occ_e = nullptr, float* occ_r = nullptr);
 hipError_t eh_cast_bf16(const float* x, int64_t n, void* out, hipStream_t s);
 hipError_t eh_zero(void* x, int64_t bytes, hipStream_t s);
 int eh_bce_parts(int64_t n);

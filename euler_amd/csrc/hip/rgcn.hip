@@ -15,6 +15,7 @@
 //   rel_gemm_dw : dW[rel] += sum_e (scale[e] * G[g_idx[e]])^T X[x_idx[e]]  (per-chunk
 //                 outer-product GEMM, fragments by transposing LDS reads; a relation's
 //                 only chunk stores its slab, longer relations add with fp32 atomics)
+#include <algorithm>
 #include <cstdlib>
 
 #include "hip/common.h"
@@ -156,7 +157,8 @@ __global__ __launch_bounds__(256) void rel_gemm_dw_kernel(const bf16_t* __restri
                                                           const int32_t* __restrict__ cstart,
                                                           const int32_t* __restrict__ clen,
                                                           const int32_t* __restrict__ csolo, float* __restrict__ dW,
-                                                          int accum) {
+                                                          int accum, const int32_t* __restrict__ cslot,
+                                                          float* __restrict__ part) {
   constexpr int LD = T + 16;
   constexpr int FM = T / 64, FN = T / 16;
   constexpr int CPR = T / 8;               // 16-byte chunks per row segment
@@ -228,6 +230,9 @@ __global__ __launch_bounds__(256) void rel_gemm_dw_kernel(const bf16_t* __restri
   }
   float* __restrict__ dWr = dW + static_cast<int64_t>(r) * N * K;
   const bool solo = csolo && csolo[chunk];
+  // deterministic mode (cslot): a chunk of a multi-chunk relation stores its slab into its
+  // own partial slot; rel_dw_reduce_kernel adds the slots of each relation in chunk order
+  if (cslot && !solo) dWr = part + static_cast<int64_t>(cslot[chunk]) * N * K;
 #pragma unroll
   for (int m = 0; m < FM; ++m)
 #pragma unroll
@@ -238,9 +243,29 @@ __global__ __launch_bounds__(256) void rel_gemm_dw_kernel(const bf16_t* __restri
         float* dst = dWr + static_cast<int64_t>(n) * K + sk * T + f * 16 + (lane & 15);
         if (solo)
           *dst = accum ? *dst + acc[m][f][j] : acc[m][f][j];
+        else if (cslot)
+          *dst = acc[m][f][j];
         else
           atomicAdd(dst, acc[m][f][j]);
       }
+}
+
+// deterministic dW of the multi-chunk relations: dW[rel] (+)= sum of its partial slots in
+// chunk order (slots rp[i] .. rp[i + 1] of the i-th multi-chunk relation mrel[i])
+__global__ __launch_bounds__(256) void rel_dw_reduce_kernel(const float* __restrict__ part,
+                                                            const int32_t* __restrict__ mrel,
+                                                            const int32_t* __restrict__ rp, int nm, int64_t NK,
+                                                            float* __restrict__ dW, int accum) {
+  const int64_t total = static_cast<int64_t>(nm) * (NK >> 2);
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < total;
+       t += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int i = static_cast<int>(t / (NK >> 2));
+    const int64_t e = (t - static_cast<int64_t>(i) * (NK >> 2)) * 4;
+    float4_t v = float4_t{0.f, 0.f, 0.f, 0.f};
+    for (int sl = rp[i]; sl < rp[i + 1]; ++sl) v += *reinterpret_cast<const float4_t*>(part + sl * NK + e);
+    float4_t* d = reinterpret_cast<float4_t*>(dW + static_cast<int64_t>(mrel[i]) * NK + e);
+    *d = accum ? *d + v : v;
+  }
 }
 
 // bf16 operands of the relation weights for one step: wb[r] = bf16(W[r]) ([N][K], the
@@ -308,7 +333,8 @@ hipError_t eh_rel_gemm(const void* A, int K, const int32_t* a_idx, const int32_t
 
 hipError_t eh_rel_gemm_dw(const void* G, int N, const int32_t* g_idx, const void* X, int K, const int32_t* x_idx,
                           const float* scale, const int32_t* crel, const int32_t* cstart, const int32_t* clen,
-                          const int32_t* csolo, int n_chunks, float* dW, int accum, hipStream_t s) {
+                          const int32_t* csolo, int n_chunks, float* dW, int accum, hipStream_t s,
+                          const int32_t* cslot, float* part, const int32_t* mrel, const int32_t* mrp, int n_multi) {
   if (n_chunks == 0) return hipSuccess;
   if (N % 64 != 0 || K % 64 != 0) return hipErrorInvalidValue;
   static const int t_max = [] {  // EULER_AMD_RG_DW_T=64: 64 x 64 slabs only (tuning knob)
@@ -318,14 +344,21 @@ hipError_t eh_rel_gemm_dw(const void* G, int N, const int32_t* g_idx, const void
   const int T = (t_max >= 128 && N % 128 == 0 && K % 128 == 0) ? 128 : 64;
   const int64_t blocks = static_cast<int64_t>(n_chunks) * (N / T) * (K / T);
   if (blocks >= (1ll << 31)) return hipErrorInvalidValue;
+  if (cslot && (!csolo || !part || !mrel || !mrp)) return hipErrorInvalidValue;
   if (T == 128)
     hipLaunchKernelGGL(rel_gemm_dw_kernel<128>, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s,
                        static_cast<const bf16_t*>(G), N, g_idx, static_cast<const bf16_t*>(X), K, x_idx, scale, crel,
-                       cstart, clen, csolo, dW, accum);
+                       cstart, clen, csolo, dW, accum, cslot, part);
   else
     hipLaunchKernelGGL(rel_gemm_dw_kernel<64>, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s,
                        static_cast<const bf16_t*>(G), N, g_idx, static_cast<const bf16_t*>(X), K, x_idx, scale, crel,
-                       cstart, clen, csolo, dW, accum);
+                       cstart, clen, csolo, dW, accum, cslot, part);
+  if (cslot && n_multi > 0) {
+    const int64_t NK = static_cast<int64_t>(N) * K;
+    const int64_t items = static_cast<int64_t>(n_multi) * (NK >> 2);
+    const uint32_t g = static_cast<uint32_t>(std::min<int64_t>((items + 255) / 256, 4096));
+    hipLaunchKernelGGL(rel_dw_reduce_kernel, dim3(g), dim3(256), 0, s, part, mrel, mrp, n_multi, NK, dW, accum);
+  }
   return hipGetLastError();
 }
 

@@ -830,6 +830,8 @@ class BaseEstimator:
         one model function for train, eval and predict)"""
         if not self.params.get("device_graph") or self.params.get("device_infer", True) is False:
             return None
+        if self.params.get("device_graph_sharded"):
+            return None  # a row-sharded graph trains on the device; evaluate / infer: engine path
         tr = getattr(self, "device_trainer", None)
         if tr is None:
             from euler_amd.estimator.device_trainers import device_infers

@@ -21,8 +21,8 @@ from typing import Any, Callable, List, Tuple
 import numpy as np
 import torch
 
-__all__ = ["Ctx", "REGISTRY", "build_device_trainer", "register", "device_infers", "has_store_encoder",
-           "NoDeviceTrainer"]
+__all__ = ["Ctx", "REGISTRY", "build_device_trainer", "build_sharded_trainer", "register", "device_infers",
+           "has_store_encoder", "NoDeviceTrainer", "sharded_supported"]
 
 
 class NoDeviceTrainer(ValueError):
@@ -121,7 +121,11 @@ def device_infers(model) -> bool:
 def build_device_trainer(est, model, first):
     """the first registered trainer that accepts ``model`` (NoDeviceTrainer if none does).
     A model with a historical-embedding encoder is only taken by a store-aware trainer:
-    any other trainer would train it as its plain parent encoder without stores."""
+    any other trainer would train it as its plain parent encoder without stores.
+    ``params["device_graph_sharded"]``: the graph is row-sharded over the ranks
+    (:func:`build_sharded_trainer`)."""
+    if est.params.get("device_graph_sharded"):
+        return build_sharded_trainer(est, model, first)
     stores = has_store_encoder(model)
     for name, pred, builder in REGISTRY:
         if stores and name not in STORE_AWARE:
@@ -138,6 +142,38 @@ def build_device_trainer(est, model, first):
                               "device trainer accepts")
     raise NoDeviceTrainer("device_graph=True trains: " + ", ".join(n for n, _, _ in REGISTRY) +
                           f"; {type(model).__name__} is none of them")
+
+
+def sharded_supported(model) -> bool:
+    """supervised models on the sampled ``SageDataFlow`` (any convolution, no stores)"""
+    from euler_amd.dataflow import dataflows as D
+
+    gnn = getattr(model, "gnn", None)
+    return (gnn is not None and hasattr(gnn, "feature_idx") and hasattr(model, "label_idx")
+            and not hasattr(model, "context_gnn") and not has_store_encoder(model)
+            and isinstance(getattr(gnn, "sampler", None), D.SageDataFlow))
+
+
+def build_sharded_trainer(est, model, first):
+    """a graph larger than one GPU's HBM: every rank uploads only its rows (r % W) of the
+    CSR, features and labels (graph/sharded_graph.py) and the neighbour draws, features and
+    labels cross the ranks over all-to-all (models/full_trainer.py ShardedFlowTrainer)"""
+    from euler_amd.graph.sharded_graph import ShardedDeviceGraph
+    from euler_amd.models.full_trainer import ShardedFlowTrainer
+
+    if not sharded_supported(model):
+        raise NoDeviceTrainer("device_graph_sharded=True trains supervised models on the sampled SageDataFlow; "
+                              f"{type(model).__name__} is not one")
+    est._prepare(first, build_optimizer=False)
+    c = Ctx(est, model)
+    gnn = model.gnn
+    g = ShardedDeviceGraph.from_engine(node_type=c.node_type(-1), features=gnn.feature_idx,
+                                       feature_dims=gnn.feature_dim, label=model.label_idx,
+                                       label_dim=model.label_dim, feature_dtype=c.feature_dtype(),
+                                       seed=c.seed * 7919 + est.rank, device=est.device)
+    tr = ShardedFlowTrainer.from_model(model, g, c.batch, **c.opt_kw())
+    tr.device_trainer_kind = "sharded_sage_flow"
+    return tr
 
 
 # ----------------------------------------------------------------------------------- predicates

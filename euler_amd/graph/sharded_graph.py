@@ -1,0 +1,312 @@
+"""A graph larger than one GPU's HBM: the CSR, the feature table and the labels row-sharded
+over the data-parallel ranks, with cross-GPU neighbour sampling.
+
+The reference scales a graph past one machine by partitioning its nodes over shard servers
+(``(id % partitions) % shards``, ``euler/core/graph/graph.cc:90-98``); a query's
+``API_SAMPLE_NEIGHBOR`` / ``API_GET_P`` is split by owner (``euler/core/kernels/
+id_split_op.cc:46-49``), sent to every owning shard (``remote_op.cc:60-146``) and merged
+back in the caller's order (``id_unique_op`` / ``merge`` kernels).  Here the node's GPUs are
+the shards and RCCL's all-to-all over xGMI is the transport:
+
+* row ``r`` (engine rows: node ids sorted) lives on rank ``r % W`` at local row ``r // W``:
+  its out-edges (neighbour values stay GLOBAL rows), its prefix-sum weights, its feature
+  row and its label row — each GPU holds ~1/W of the graph;
+* ``sample_neighbor(rows, F)``: ``route_by_owner`` gives every requested row a slot in a
+  fixed-capacity ``[W, C]`` exchange (``csrc/hip/route.hip``; a row past its owner's C
+  slots raises the ``overflow`` flag and draws ``default``), one all-to-all sends the rows
+  to their owners, each owner draws F neighbours per received row from its local CSR with
+  its Philox stream (the ordinary ``sample_neighbor`` kernel), and one all-to-all returns
+  the ``[W, C, F]`` draws (and weights / types) to the requesters' slots — every
+  occurrence draws independently, as with the whole graph;
+* ``sample_node(B)``: exact global weighted root draws (reference ``sample_node`` over a
+  sharded graph: the shards' node-weight sums pick the shard, ``graph.cc:333-403``): each
+  root picks its owner from the alias table of the W shard sums, the per-owner tickets go
+  through the same exchange, the owner draws that many local roots from its own alias table;
+* features and labels: :class:`~euler_amd.graph.sharded_features.ShardedFeatures` exchanges
+  (dedup, fixed capacity, zero row for ``-1``).
+
+Every exchange has fixed shapes (no host-read sizes).  With one rank the object is the
+ordinary local graph behind the same interface (no collective).
+
+:class:`~euler_amd.models.full_trainer.ShardedFlowTrainer` trains the reference's sampled
+``SageDataFlow`` models (any convolution) on it under ``NodeEstimator(device_graph=True,
+device_graph_sharded=True)``.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from euler_amd.graph.device_graph import DeviceGraph, _upload, build_alias_table, shared_export
+from euler_amd.graph.sharded_features import ShardedFeatures
+from euler_amd.ops import mp_ops
+from euler_amd.ops._native import hip, use_hip
+from euler_amd.ops.gnn_ops import route_by_owner
+
+__all__ = ["ShardedDeviceGraph", "shard_csr"]
+
+
+def shard_csr(indptr, nbr, w, T: int, world: int, rank: int):
+    """the rows ``r % world == rank`` of a host CSR (``indptr [N*T+1]``, raw edge weights):
+    ``(indptr, nbr, w)`` of the local rows (neighbour values unchanged: global rows)"""
+    indptr = np.asarray(indptr, np.int64)
+    N = (indptr.shape[0] - 1) // T
+    rows = np.arange(rank, N, world, dtype=np.int64)
+    seg = (rows[:, None] * T + np.arange(T)[None, :]).reshape(-1)
+    starts, lens = indptr[seg], indptr[seg + 1] - indptr[seg]
+    lip = np.zeros(seg.shape[0] + 1, np.int64)
+    np.cumsum(lens, out=lip[1:])
+    take = np.repeat(starts - lip[:-1], lens) + np.arange(int(lip[-1]), dtype=np.int64)
+    return lip, np.asarray(nbr)[take], np.asarray(w)[take]
+
+
+class ShardedDeviceGraph:
+    """``local``: the :class:`DeviceGraph` of this rank's rows (local row i = global row
+    ``i * W + rank``; neighbour values are global rows), its root sampler over the local
+    rows with ``root_weight`` their total root weight; ``num_rows`` the global row count;
+    ``ids`` the sorted raw node ids of all rows (or None: rows are ids)."""
+
+    def __init__(self, local: DeviceGraph, num_rows: int, root_weight: float = None, ids=None, group=None,
+                 force_comm: bool = False, capacity_sigmas: float = 6.0):
+        self.local = local
+        self.group = group
+        on = dist.is_available() and dist.is_initialized()
+        multi = on and dist.get_world_size(group) > 1
+        self.world = dist.get_world_size(group) if multi else 1
+        self.rank = dist.get_rank(group) if multi else 0
+        self.comm = multi or (on and force_comm)
+        self.num_rows = int(num_rows)
+        want = max(0, math.ceil((self.num_rows - self.rank) / self.world))
+        if local.num_rows != want:
+            raise ValueError(f"rank {self.rank} must hold the {want} rows r % {self.world} == {self.rank}, "
+                             f"its local graph has {local.num_rows}")
+        self.num_types = local.num_types
+        self.device = local.device
+        self.rng = local.rng
+        self.ids = ids
+        self.sigmas = float(capacity_sigmas)
+        self.overflow = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.features = ShardedFeatures(local.features, self.num_rows, group, force_comm) \
+            if local.features is not None else None
+        self.labels = ShardedFeatures(local.labels.float(), self.num_rows, group, force_comm) \
+            if local.labels is not None else None
+        self.set_root_weight(root_weight)
+
+    # ------------------------------------------------------------------ construction
+    @classmethod
+    def from_full(cls, g: DeviceGraph, group=None, force_comm: bool = False, **kw):
+        """this rank's shard of a whole :class:`DeviceGraph` (tests / small graphs): same
+        rows, same edges, same root weights (the local alias tables are rebuilt from the
+        whole graph's node weights when ``node_weights`` is given)"""
+        on = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+        W, r = (dist.get_world_size(group), dist.get_rank(group)) if on else (1, 0)
+        T = g.num_types
+        indptr = g.indptr.cpu().numpy()
+        cumw = g.cumw.cpu().numpy().astype(np.float64)
+        # raw weights back from the per-segment prefix sums
+        seg_start = np.repeat(indptr[:-1], np.diff(indptr))
+        prev = np.where(np.arange(cumw.shape[0]) > seg_start, np.concatenate([[0.0], cumw[:-1]]), 0.0)
+        w = cumw - prev
+        lip, nbr, lw = shard_csr(indptr, g.nbr.cpu().numpy(), w, T, W, r)
+        nw = kw.pop("node_weights", None)
+        if nw is None:
+            nw = _alias_weights(g)
+        nw = np.asarray(nw, np.float64)
+        local = DeviceGraph.from_csr(lip, nbr, lw, T, node_weights=nw[r::W] if nw[r::W].size else None,
+                                     seed=int(g.rng[0]) + 7919 * r, device=g.device)
+        if g.features is not None:
+            local.features = g.features[r::W].contiguous()
+        if g.labels is not None:
+            local.labels = g.labels[r::W].contiguous()
+        return cls(local, g.num_rows, float(nw[r::W].sum()), ids=g.ids, group=group, force_comm=force_comm, **kw)
+
+    @classmethod
+    def from_engine(cls, engine=None, node_type=-1, features=(), feature_dims=(), label=None, label_dim=None,
+                    feature_dtype=torch.bfloat16, seed=0, device="cuda", group=None):
+        """this rank's rows of the engine's graph: the node's ranks share ONE host export
+        (``shared_export``: local rank 0 writes /dev/shm, every rank maps it) and each uploads
+        only its rows — CSR, features, labels and root weights (HBM holds 1/W of the graph)"""
+        from euler_amd.graph.device_graph import _export_local
+        from euler_amd.ops import base
+
+        eng = engine if engine is not None else base.get_engine()
+        if getattr(eng, "mode", "local") != "local":
+            raise ValueError("the sharded device graph loads from an in-process engine")
+        names = [] if not features else ([features] if isinstance(features, (str, int)) else list(features))
+        dims = [] if not features else ([feature_dims] if isinstance(feature_dims, int) else list(feature_dims))
+        on = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+        W, r = (dist.get_world_size(group), dist.get_rank(group)) if on else (1, 0)
+        arrays, done = shared_export(lambda: _export_local(eng, names, dims, label, label_dim))
+        try:
+            T = int(np.asarray(arrays["T"])[0])
+            ids = np.array(arrays["ids"])
+            lip, nbr, lw = shard_csr(arrays["indptr"], arrays["nbr"], arrays["w"], T, W, r)
+            nw = np.asarray(arrays["nw"], np.float64)[r::W].copy()
+            types = np.asarray(arrays["types"])[r::W]
+            if node_type is not None and int(node_type) >= 0:
+                nw = np.where(types == int(node_type), nw, 0.0)
+            local = DeviceGraph.from_csr(lip, nbr, lw, T, node_weights=nw if nw.size else None,
+                                         seed=seed, device=device)
+            local.node_types = types.copy()
+            if names:
+                local.features = _upload(np.asarray(arrays["features"])[r::W], torch.float32, device).view(
+                    len(nw), -1).to(feature_dtype)
+            if label is not None:
+                local.labels = _upload(np.asarray(arrays["labels"])[r::W], torch.float32, device).view(len(nw), -1)
+        finally:
+            del arrays
+            done()
+        return cls(local, len(ids), float(nw.sum()), ids=ids, group=group)
+
+    def set_root_weight(self, root_weight=None):
+        """the owner alias table of the W shards' root-weight sums (all-gathered)"""
+        wl = float(self.local.node_prob.numel() if root_weight is None else root_weight)
+        sums = torch.tensor([wl], dtype=torch.float64)
+        if self.comm:
+            out = [torch.zeros(1, dtype=torch.float64) for _ in range(self.world)]
+            dist.all_gather(out, sums, group=self.group)
+            sums = torch.cat(out)
+        self.shard_weight = sums.numpy().copy()
+        if not (self.shard_weight > 0).any():
+            raise ValueError("no shard holds a root candidate")
+        p, a = build_alias_table(self.shard_weight)
+        self._owner_prob = torch.from_numpy(p).to(self.device)
+        self._owner_alias = torch.from_numpy(a).to(self.device)
+
+    # ------------------------------------------------------------------ DeviceGraph interface
+    def rows_of(self, ids) -> torch.Tensor:
+        return DeviceGraph.rows_of(self, ids)
+
+    def advance(self, inc: int = 1):
+        self.local.advance(inc)
+
+    def manual_seed(self, seed: int):
+        self.local.manual_seed(int(seed))
+
+    def reseed_cpu(self):
+        self.local.reseed_cpu()
+
+    def _mask(self, edge_types) -> int:
+        return self.local._mask(edge_types)
+
+    def nbytes(self) -> int:
+        g = self.local
+        return sum(t.numel() * t.element_size() for t in (g.indptr, g.nbr, g.cumw, g.node_prob, g.node_alias))
+
+    def capacity(self, n: int) -> int:
+        """exchange slots per peer for n requests (mean + sigmas * sqrt(mean) + 64, 64-aligned)"""
+        if self.world == 1:
+            return int(n)
+        mean = n / self.world
+        return min(int(n), int(math.ceil((mean + self.sigmas * math.sqrt(mean) + 64) / 64.0)) * 64)
+
+    def check_overflow(self):
+        for name, o in (("graph", self.overflow), ("features", getattr(self.features, "overflow", None)),
+                        ("labels", getattr(self.labels, "overflow", None))):
+            if o is not None and int(o.item()):
+                raise RuntimeError(f"ShardedDeviceGraph: the {name} exchange overflowed its per-peer slots "
+                                   "(those requests read -1 / zeros); raise capacity_sigmas")
+
+    def _a2a(self, send: torch.Tensor) -> torch.Tensor:
+        """equal-split all-to-all of [W * C, ...] (block o -> rank o)"""
+        if not self.comm:
+            return send.clone()
+        recv = torch.empty_like(send)
+        dist.all_to_all_single(recv, send.contiguous(), group=self.group)
+        return recv
+
+    def _route(self, keys: torch.Tensor):
+        """(slot of every key [n], this rank's received keys [W*C], C) of the owner exchange
+        (owner = key % W)"""
+        n = keys.numel()
+        C = self.capacity(n)
+        pos, send = route_by_owner(keys, self.world, C, self.overflow)
+        return pos, self._a2a(send[: self.world * C]), C
+
+    def _local_rows(self, recv):
+        return torch.where(recv >= 0, torch.div(recv, self.world, rounding_mode="floor"), torch.full_like(recv, -1))
+
+    def _back(self, vals: torch.Tensor, pos: torch.Tensor, fill):
+        """the owners' answers [W*C, ...] returned to the requesters' order (trash -> fill)"""
+        back = self._a2a(vals)
+        pad = torch.full((1,) + tuple(back.shape[1:]), fill, dtype=back.dtype, device=back.device)
+        return torch.cat([back, pad])[pos]
+
+    def sample_node(self, count: int, stream_id: int = 1) -> torch.Tensor:
+        """``count`` global rows drawn with the global root weights"""
+        if self.world == 1:
+            return self.local.sample_node(int(count), stream_id)
+        owner = self._alias(self._owner_prob, self._owner_alias, int(count), stream_id).long()
+        tickets = torch.arange(int(count), device=self.device, dtype=torch.long) * self.world + owner
+        pos, recv, C = self._route(tickets)
+        # this rank draws one local root per received ticket (the empty slots draw too and
+        # are dropped: fixed shapes)
+        if self.local.node_prob.numel():
+            loc = self.local.sample_node(self.world * C, stream_id=stream_id + 64).long()
+        else:
+            loc = torch.full((self.world * C,), -1, dtype=torch.long, device=self.device)
+        glob = torch.where((recv >= 0) & (loc >= 0), loc * self.world + self.rank, torch.full_like(loc, -1))
+        return self._back(glob, pos, -1).int()
+
+    def _alias(self, prob, alias, count, stream_id):
+        if use_hip(prob):
+            return hip().alias_sample(prob, alias, None, int(count), self.local.rng, int(stream_id))
+        g = self.local._cpu_gen
+        k = torch.randint(0, prob.numel(), (count,), generator=g)
+        u = torch.rand(count, generator=g)
+        return torch.where(u < prob[k], k, alias[k].long()).int()
+
+    def sample_neighbor(self, rows: torch.Tensor, count: int, edge_types=None, default: int = -1,
+                        stream_id: int = 2, with_weights: bool = False):
+        """``count`` weighted draws with replacement per row (``[n, count]``, global rows),
+        each drawn by the row's owner from its local CSR"""
+        rows = rows.reshape(-1).long()
+        n, F = rows.numel(), int(count)
+        if self.world == 1 and not self.comm:
+            return self.local.sample_neighbor(rows, F, edge_types, default, stream_id, with_weights)
+        ok = (rows >= 0) & (rows < self.num_rows)
+        pos, recv, C = self._route(torch.where(ok, rows, torch.full_like(rows, -1)))
+        local = self._local_rows(recv)
+        nb, w, t = self.local.sample_neighbor(local, F, edge_types, -1, stream_id, True)
+        nb = nb.view(-1, F).long()
+        out_nb = self._back(nb, pos, -1)
+        out_nb = torch.where(out_nb >= 0, out_nb, torch.full_like(out_nb, int(default))).int()
+        if not with_weights:
+            return out_nb
+        return out_nb, self._back(w.view(-1, F).float(), pos, 0.0), self._back(t.view(-1, F).int(), pos, -1)
+
+    # ------------------------------------------------------------------ features / labels
+    def gather_features(self, rows: torch.Tensor) -> torch.Tensor:
+        """feature rows [n, D] of global rows (``-1``: zeros), through the feature exchange"""
+        return self._gather(self.features, rows)
+
+    def gather_labels(self, rows: torch.Tensor) -> torch.Tensor:
+        return self._gather(self.labels, rows)
+
+    @staticmethod
+    def _gather(sf, rows):
+        if sf is None:
+            raise ValueError("the sharded graph holds no such table")
+        pos = sf.exchange(rows.reshape(-1).long())
+        if use_hip(sf.cache):
+            return mp_ops.gather(sf.cache, pos.long())
+        return torch.where((pos >= 0).unsqueeze(1), sf.cache[pos.long().clamp(min=0)], torch.zeros(
+            (), dtype=sf.cache.dtype))
+
+
+def _alias_weights(g: DeviceGraph):
+    """per-row root weights of a DeviceGraph's alias table (prob / alias -> weights)"""
+    p = g.node_prob.detach().cpu().double()
+    a = g.node_alias.detach().cpu().long()
+    n = p.numel()
+    w = p.clone()
+    w.index_add_(0, a, 1.0 - p)
+    out = torch.zeros(g.num_rows, dtype=torch.float64)
+    if g.root_rows is not None:
+        out[g.root_rows.cpu().long()] = w
+    else:
+        out[:n] = w
+    return out.numpy()

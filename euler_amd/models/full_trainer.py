@@ -36,14 +36,15 @@ from euler_amd.dataflow.device_flow import DeviceFullFlow
 from euler_amd.models.captured import CapturedTrainer
 from euler_amd.ops import gnn_ops, mp_ops
 
-__all__ = ["FullFlowTrainer", "full_flow_embed", "infer_flow"]
+__all__ = ["FullFlowTrainer", "ShardedFlowTrainer", "full_flow_embed", "infer_flow"]
 
 
 def full_flow_embed(gnn, flow, features, roots):
     """(gnn embedding [B, E], DataFlow) of ``roots`` through the model's convolutions on a
     device flow (ReLU after every conv, then ``gnn.fc``: BaseGNNNet.forward)"""
     df = flow.produce(roots)
-    x = mp_ops.gather(features, df[0].n_id).float()
+    # a callable: rows -> feature rows (a row-sharded table's exchange, graph/sharded_graph.py)
+    x = (features(df[0].n_id) if callable(features) else mp_ops.gather(features, df[0].n_id)).float()
     for conv, block in zip(gnn.convs, df):
         x_t = mp_ops.gather(x, block.res_n_id)
         x = F.relu(gnn.calculate_conv(conv, (x_t, x), block.edge_index, size=block.size))
@@ -214,3 +215,78 @@ class FullFlowTrainer(CapturedTrainer):
             p.grad = saved[n]
         self.flat.rebind_grads()
         return float(loss), grads
+
+
+class ShardedFlowTrainer(FullFlowTrainer):
+    """A sampled-``SageDataFlow`` model (any convolution) trained on a graph row-sharded over
+    the data-parallel ranks (:class:`~euler_amd.graph.sharded_graph.ShardedDeviceGraph`):
+    roots drawn with the global root weights, each hop's fixed-fanout draws answered by the
+    rows' owners over the all-to-all, the input features and the roots' labels fetched from
+    their owners; the model's own convolutions, loss, backward, gradient all-reduce and the
+    flat optimizer run as in :class:`FullFlowTrainer`.  HBM per rank holds 1/W of the CSR,
+    the features and the labels.  Steps with collectives inside run eagerly (one rank: the
+    step is captured as usual)."""
+
+    def __init__(self, model, graph, batch_size, flow, optimizer="adam", learning_rate=0.01):
+        self.gnn = model.gnn
+        self.graph = graph
+        self.B = int(batch_size)
+        if graph.features is None or graph.labels is None:
+            raise ValueError("the sharded graph needs dense features and labels")
+        self.features = graph.gather_features
+        self.labels = None
+        self.flow = flow
+        self.counts = torch.zeros(3, dtype=torch.int64, device=graph.device)
+        self._rows = torch.arange(self.B, device=graph.device)
+        CapturedTrainer.__init__(self, model, graph, graph.device, optimizer, learning_rate)
+
+    @classmethod
+    def from_model(cls, model, graph, batch_size, optimizer="adam", learning_rate=0.01, **kw):
+        import euler_amd.ops.graph_api as ge
+        from euler_amd.dataflow.dataflows import SageDataFlow
+        from euler_amd.dataflow.device_flow import DeviceSageFlow
+
+        flow = getattr(model.gnn, "sampler", None)
+        if not isinstance(flow, SageDataFlow):
+            raise ValueError("the sharded device graph trains models on the sampled SageDataFlow (fixed fanouts)")
+        ets = []
+        for m in flow.metapath:
+            ids = None if m is None else [int(t) for t in np.asarray(ge.get_edge_type_id(m)).reshape(-1)]
+            ets.append(None if ids is None or any(t < 0 for t in ids) else ids)
+        dflow = DeviceSageFlow(graph, ets, flow.fanouts, batch_size, bool(flow.add_self_loops))
+        return cls(model, graph, batch_size, dflow, optimizer=optimizer, learning_rate=learning_rate)
+
+    def _forward_loss(self):
+        self._draw()
+        roots = self.graph.sample_node(self.B, stream_id=1).long()
+        logits, df = self._forward(roots)
+        y = self.graph.gather_labels(roots).float().contiguous()
+        loss = gnn_ops.bce_f1_loss(logits, y, self._rows, self.counts)
+        self._samples = roots
+        return loss
+
+    infer_logits = None  # evaluate / infer of a sharded-graph job: the engine path
+    infer_embed = None
+
+    def capture(self, grad_sync=None, warmup: int = 2, steps: int = 1, extra_sizes=()):
+        if self.graph.world == 1 and not self.graph.comm:
+            return super().capture(grad_sync, warmup, steps, extra_sizes)
+        for _ in range(int(warmup)):  # collectives in the step: eager
+            self.step_count += 1
+            self._step(grad_sync)
+        self._grad_sync = grad_sync
+        self._graphs, self._graph_exec = {}, None
+        return None
+
+    def replay(self, n: int = 1):
+        if self._graph_exec is not None:
+            return super().replay(n)
+        self.replay_steps(n)
+
+    def replay_steps(self, n: int):
+        if self._graphs:
+            return super().replay_steps(n)
+        for _ in range(int(n)):
+            self._step(getattr(self, "_grad_sync", None))
+        self.step_count += int(n)
+        self.graph.check_overflow()

@@ -31,7 +31,13 @@ layer and step and take d coef / d bases from the composed dW with two more; sel
 dropout draws its per-row keep mask with Philox(seed, step, layer) (``drop_rows``) and
 scales the self-loop product's rows with it in the backward GEMM's epilogue.
 
-No torch elementwise kernel runs in the step; gradients are zeroed with one memset.  The
+``deterministic=True`` (or ``EULER_AMD_DETERMINISTIC=1``) makes the step atomic-free and
+bit-reproducible: the scoring backward writes one gradient row per entity / relation
+occurrence, summed per row in a fixed order (stable sort of the occurrence keys +
+``segment_reduce_wave``), and the relation-weight gradient of a relation with several
+edge chunks is added from per-chunk slabs in chunk order (``rel_gemm_dw`` slot mode).
+
+No torch elementwise kernel runs in the default step; gradients are zeroed with one memset.  The
 draws come from a different generator than ``torch.randint`` (Philox keyed by the
 optimizer's device step count), so the batch stream differs from the autograd path's;
 the step's loss and gradients on the same batch match it (tests/test_kg_step.py).
@@ -99,7 +105,7 @@ class RgcnTransEStep:
     gradient between backward and update and returns the gradient scale."""
 
     def __init__(self, model: RgcnTransE, flat, opt, edge_index, edge_rel, triples, pool, batch: int,
-                 num_negs: int, seed: int = 0, grad_sync=None):
+                 num_negs: int, seed: int = 0, grad_sync=None, deterministic=None):
         dev = model.ent.device
         if dev.type != "cuda":
             raise ValueError("the fused KG step runs on the GPU")
@@ -171,6 +177,22 @@ class RgcnTransEStep:
         rep = int(os.environ.get("EULER_AMD_KG_REL_REP", "16"))
         self.drel_rep = torch.empty(rep, self.R, self.D, **f32) if rep > 0 else None
         self._fc_splits = gnn_ops._gemm_splits(self.N, -(-self.D // 64) ** 2)
+        if deterministic is None:
+            deterministic = os.environ.get("EULER_AMD_DETERMINISTIC", "0") == "1"
+        self.deterministic = bool(deterministic)
+        if self.deterministic:
+            # atomic-free backward: the scoring kernel writes one gradient row per entity /
+            # relation occurrence, summed per row in a fixed order (occurrences stably sorted
+            # by row, wave-per-row segment sums); multi-chunk relations store per-chunk dW
+            # slabs, added in chunk order (rel_gemm_dw slot mode)
+            nocc = self.B * (2 + self.K)
+            self.occ_e = torch.empty(nocc, self.D, **f32)
+            self.occ_r = torch.empty(self.B, self.D, **f32)
+            self.keys_e = torch.empty(self.B, 2 + self.K, **i64)
+            self.bnd_e = torch.arange(self.N + 1, **i64)
+            self.bnd_r = torch.arange(self.R + 1, **i64)
+            slots = max((lay[2].det_slots()[3] for lay in self.layers), default=0)
+            self.dw_part = torch.empty(max(slots, 1), self.D, self.D, **f32)
 
     # ------------------------------------------------------------------ step
     def _relation_matrices(self, li):
@@ -216,9 +238,12 @@ class RgcnTransEStep:
         dtop = m.ent.grad if L == 0 else self.dh[L - 1]
         if L:
             H.zero_(dtop)
+        occ = (self.occ_e, self.occ_r) if self.deterministic else (None, None)
         H.kg_step(x, m.rel.detach(), self.pool, self.t_src, self.t_dst, self.t_rel, self.opt.step_count, self.seed,
                   gnn_ops.KG_KINDS["l2"], self.normalize, self.margin, self.o_src, self.o_dst, self.o_rel, self.o_neg,
-                  self.coef, self.part, self.loss, dtop, m.rel.grad, self.drel_rep)
+                  self.coef, self.part, self.loss, dtop, m.rel.grad, self.drel_rep, *occ)
+        if self.deterministic:
+            self._occurrence_sums(dtop, m.rel.grad)
         self._chk("scores", dtop, m.rel.grad, self.loss)
         for li in range(L - 1, -1, -1):
             W, Wfc, tiles, basis = self.layers[li]
@@ -236,16 +261,20 @@ class RgcnTransEStep:
             gnn_ops.gemm(g, x0_l, out=Wfc.grad, trans_a=True, splits=self._fc_splits)
             self._chk("layer %d input gradients" % li, dxr, out, Wfc.grad)
             cr, cs, cl = tiles.chunks()
+            det = {}
+            if self.deterministic:
+                slot, mrel, mrp, _ = tiles.det_slots()
+                det = dict(slot=slot, part=self.dw_part, mrel=mrel, mrp=mrp)
             if basis is None:
                 H.rel_gemm_dw(self.gb, tiles.dst, self.xb[li], tiles.src, tiles.scale, cr, cs, cl, tiles.chunk_solo,
-                              W.grad, accumulate=False)
+                              W.grad, accumulate=False, **det)
                 continue
             # dW of the composed matrices, then d coef = dW bases^T, d bases = coef^T dW
             coef, bases = basis
             nbs = bases.shape[0]
             H.zero_(self.dWc)
             H.rel_gemm_dw(self.gb, tiles.dst, self.xb[li], tiles.src, tiles.scale, cr, cs, cl, tiles.chunk_solo,
-                          self.dWc, accumulate=False)
+                          self.dWc, accumulate=False, **det)
             dw = self.dWc.view(self.R, -1)
             sp = int(os.environ.get("EULER_AMD_KG_DCOEF_SPLITS", "0")) or \
                 gnn_ops._gemm_splits(dw.shape[1], -(-self.R // 64))
@@ -254,6 +283,21 @@ class RgcnTransEStep:
                          splits=gnn_ops._gemm_splits(self.R, -(-dw.shape[1] // 64)))
             self._chk("layer %d basis gradients" % li, self.dWc, coef.grad, bases.grad)
         return self.loss
+
+    def _occurrence_sums(self, dent, drel):
+        """deterministic mode: d h and d rel as fixed-order sums of the scoring kernel's
+        occurrence rows (row-major [h, t, neg_0 .. neg_{K-1}] per triple; one row per triple
+        for the relations)"""
+        H = hip()
+        k = self.keys_e
+        k[:, 0].copy_(self.o_src)
+        k[:, 1].copy_(self.o_dst)
+        k[:, 2:].copy_(self.o_neg)
+        for keys, bnd, occ, out in ((k.view(-1), self.bnd_e, self.occ_e, dent),
+                                    (self.o_rel, self.bnd_r, self.occ_r, drel)):
+            sk, perm = torch.sort(keys, stable=True)
+            ptr = torch.searchsorted(sk, bnd)
+            H.segment_reduce_wave(occ, ptr, perm, 0, out=out)
 
     def keep_masks(self):
         """per-layer [N] keep masks of the last step's self-loop dropout (None without)"""

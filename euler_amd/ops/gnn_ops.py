@@ -468,6 +468,23 @@ class RelationTiles:
     def chunks(self):
         return self.chunk_rel, self.chunk_start, self.chunk_len
 
+    def det_slots(self):
+        """the deterministic weight-gradient layout (``rel_gemm_dw(slot=, part=, mrel=, mrp=)``):
+        (chunk -> partial slot, -1 for a relation's only chunk; the relations with several
+        chunks; their slot ranges as a CSR; the number of slots).  Chunks are in relation
+        order, so each relation's slots are consecutive and summed in chunk order."""
+        if getattr(self, "_det", None) is None:
+            solo = self.chunk_solo.long()
+            multi = 1 - solo
+            slot = torch.where(multi.bool(), torch.cumsum(multi, 0) - 1, torch.full_like(multi, -1))
+            rel = self.chunk_rel.long()[multi.bool()]
+            mrel, cnt = torch.unique_consecutive(rel, return_counts=True)
+            mrp = torch.zeros(mrel.numel() + 1, dtype=torch.long, device=rel.device)
+            mrp[1:] = torch.cumsum(cnt, 0)
+            self._det = (slot.to(torch.int32).contiguous(), mrel.to(torch.int32).contiguous(),
+                         mrp.to(torch.int32).contiguous(), int(multi.sum()))
+        return self._det
+
 
 def relation_transform_reference(x, rel, weight, edge_index, size, aggr="mean"):
     """out[i] = aggr_{e: dst(e) = i} weight[rel(e)] @ x[src(e)]  (weight [R, N, K])."""

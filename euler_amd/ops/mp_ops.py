@@ -156,7 +156,14 @@ def gather(params: torch.Tensor, indices: torch.Tensor) -> torch.Tensor:
             idx = idx.long()
         out = _Gather.apply(params, idx)
         return out.reshape(tuple(indices.shape) + tuple(params.shape[1:]))
-    return params[indices.long()]
+    idx = indices.long()
+    neg = idx < 0
+    if not bool(neg.any()):
+        return params[idx]
+    # a -1 (padding) index reads a zero row, as the HIP gather does
+    out = params[idx.clamp(min=0)]
+    return torch.where(neg.reshape(tuple(idx.shape) + (1,) * (params.dim() - 1)), torch.zeros((), dtype=out.dtype),
+                       out)
 
 
 # ----------------------------------------------------------------------------- scatter

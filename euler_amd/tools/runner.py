@@ -204,6 +204,10 @@ def parse_args(argv=None, model=None):
                    help="graphsage / graphsage_unsup: train on an HBM copy of the graph with the fused "
                         "gfx950 step (models/sage_trainer.py, models/sage_tower.py) instead of the "
                         "CPU-engine input pipeline")
+    p.add_argument("--device_graph_sharded", action="store_true",
+                   help="with --device_graph: row-shard the graph (CSR, features, labels) over the ranks, "
+                        "neighbour draws and features over all-to-all (graph/sharded_graph.py; supervised "
+                        "SageDataFlow models)")
     p.add_argument("--device_feature_dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--cuda_graph", default="auto", choices=["auto", "off"],
                    help="capture the engine-path training step in a hipGraph when eligible")
@@ -234,7 +238,8 @@ def build(a):
     total = a.total_step or max(1, int(a.num_epochs * ds.total_size / max(a.batch_size, 1)))
     params = {"model_dir": a.model_dir, "infer_dir": a.infer_dir, "batch_size": a.batch_size, "total_step": total,
               "log_steps": a.log_steps, "optimizer": a.optimizer, "learning_rate": a.learning_rate,
-              "device": a.device, "amp": a.amp, "device_graph": a.device_graph,
+              "device": a.device, "amp": a.amp, "device_graph": a.device_graph or a.device_graph_sharded,
+              "device_graph_sharded": a.device_graph_sharded,
               "device_feature_dtype": a.device_feature_dtype, "seed": a.seed,
               "native_pipeline": {"auto": "auto", "on": True, "off": False}[a.native_pipeline],
               "cuda_graph": a.cuda_graph if a.cuda_graph == "auto" else False,

@@ -31,7 +31,7 @@ def test_autograd_model_cpu_trains():
     assert losses[-1] < losses[0]
 
 
-def _setup(dev, layers, D=64, num_ent=640, num_rel=24, B=256, K=4, seed=2, bases=0, drop=0.0):
+def _setup(dev, layers, D=64, num_ent=640, num_rel=24, B=256, K=4, seed=2, bases=0, drop=0.0, det=None):
     (src, rel, dst), _ = lattice_kg(num_ent, num_rel, 8000, 10, seed=seed)
     src, rel, dst = src.to(dev), rel.to(dev), dst.to(dev)
     torch.manual_seed(seed)
@@ -42,7 +42,7 @@ def _setup(dev, layers, D=64, num_ent=640, num_rel=24, B=256, K=4, seed=2, bases
     flat = FlatParams(m.parameters(), dev)
     opt = FlatOptimizer(flat, "adam", 1e-3)
     pool = torch.arange(src.numel(), device=dev)
-    step = RgcnTransEStep(m, flat, opt, ei, rel, (src, rel, dst), pool, B, K, seed=11)
+    step = RgcnTransEStep(m, flat, opt, ei, rel, (src, rel, dst), pool, B, K, seed=11, deterministic=det)
     return m, flat, opt, step, ei, rel
 
 
@@ -105,6 +105,72 @@ def test_fused_step_matches_fp32_torch(cuda, layers, bases, drop):
     step.optimizer_step()
     step.forward_backward()
     assert not torch.equal(before[3], step.batch()[3])
+
+
+def test_deterministic_dw_slots_cpu():
+    """rel_gemm_dw slot layout: solo chunks -1, each multi-chunk relation's chunks take
+    consecutive slots (chunk order), the CSR over the multi-chunk relations covers them"""
+    g = torch.Generator().manual_seed(0)
+    E = 5000
+    rel = torch.cat([torch.zeros(3000, dtype=torch.long), torch.randint(1, 6, (E - 3000,), generator=g)])
+    ei = torch.randint(0, 300, (2, E), generator=g)
+    t = gnn_ops.RelationTiles(ei, rel, (300, 300), 6, tile=64)
+    slot, mrel, mrp, n = t.det_slots()
+    cr, solo = t.chunk_rel.long(), t.chunk_solo.bool()
+    assert n == int((~solo).sum()) and n >= 3  # relation 0: 3000 edges -> 3 chunks of 1024
+    assert (slot[solo] == -1).all() and torch.equal(slot[~solo].long(), torch.arange(n))
+    assert mrel.tolist() == sorted(set(cr[~solo].tolist())) and mrel[0] == 0
+    for i, r in enumerate(mrel.tolist()):
+        assert torch.equal(slot[cr == r].long(), torch.arange(int(mrp[i]), int(mrp[i + 1])))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layers,bases,num_rel", [(0, 0, 24), (1, 0, 24), (1, 0, 4), (2, 4, 4), (1, 4, 3)])
+def test_deterministic_step_matches_atomic_step(cuda, layers, bases, num_rel):
+    """the atomic-free step (occurrence rows + fixed-order sums, per-chunk dW slabs) computes
+    the same loss and gradients as the atomic step on the same draws, to fp32 summation order;
+    with 3-4 relations over 8000 edges every relation spans several dW chunks (slot mode)"""
+    grads, losses = {}, {}
+    for det in (False, True):
+        m, flat, opt, step, ei, erel = _setup(cuda, layers, num_rel=num_rel, bases=bases, det=det)
+        losses[det] = float(step.forward_backward()[0])
+        grads[det] = flat.grad.detach().clone()
+        if det and layers:
+            assert step.layers[0][2].det_slots()[3] > (0 if num_rel <= 4 else -1)
+    assert losses[True] == losses[False]  # the forward and its loss reduction are order-fixed
+    err = float((grads[True] - grads[False]).norm() / grads[False].norm())
+    print("deterministic vs atomic relative gradient difference", err)
+    assert err <= 1e-5
+
+
+@pytest.mark.gpu
+def test_deterministic_step_2000_replays_bit_identical(cuda):
+    """two runs of 2 eager steps + 2,000 captured replays of the deterministic step (2
+    layers, basis relations, multi-chunk relations) end with bit-identical parameters,
+    optimizer state and loss"""
+    out = []
+    for _ in range(2):
+        m, flat, opt, step, ei, erel = _setup(cuda, 2, num_rel=4, bases=2, det=True)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                step.step()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            step.step()
+        for _ in range(2000):
+            g.replay()
+        torch.cuda.synchronize()
+        assert int(opt.step_count.item()) == 2002 and bool(torch.isfinite(flat.flat).all())
+        out.append((flat.flat.detach().clone(), [opt.m.clone(), opt.v.clone()],
+                    step.loss.detach().clone()))
+        del g
+    (a, sa, la), (b, sb, lb) = out
+    assert torch.equal(a, b) and torch.equal(la, lb)
+    assert all(torch.equal(x, y) for x, y in zip(sa, sb))
 
 
 @pytest.mark.gpu

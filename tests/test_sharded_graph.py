@@ -1,0 +1,217 @@
+"""A graph row-sharded over the data-parallel ranks (graph/sharded_graph.py) with
+cross-rank neighbour sampling, and the trainer on it (models/full_trainer.py
+ShardedFlowTrainer; reference euler/core/graph/graph.cc:90-98 shard filter,
+euler/core/kernels/id_split_op.cc:46-49, remote_op.cc:60-146).
+
+CPU (gloo): the local CSRs partition the whole graph's rows exactly; with 2-3 ranks every
+draw is a real out-neighbour of the requested row (with -1 for rows without one), the
+per-neighbour frequencies follow the edge weights and the root frequencies the global node
+weights; feature / label fetches equal the whole table's rows; one rank reproduces the
+unsharded trainer step for step; NodeEstimator(device_graph_sharded=True) trains on 2 ranks
+in lockstep holding half of the graph each."""
+import math
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from test_parallel import _init, _run  # noqa: E402
+
+
+def _graph(n=300, T=2, seed=0):
+    from euler_amd.graph.device_graph import DeviceGraph
+
+    g = torch.Generator().manual_seed(seed)
+    deg = torch.randint(0, 9, (n * T,), generator=g)
+    deg[7 * T: 7 * T + T] = 0  # a row without out-edges
+    indptr = torch.zeros(n * T + 1, dtype=torch.long)
+    indptr[1:] = torch.cumsum(deg, 0)
+    E = int(indptr[-1])
+    nbr = torch.randint(0, n, (E,), generator=g)
+    w = torch.rand(E, generator=g) + 0.1
+    nw = torch.rand(n, generator=g).numpy() + 0.05
+    dg = DeviceGraph.from_csr(indptr.numpy(), nbr.numpy(), w.numpy(), T, node_weights=nw, seed=5, device="cpu")
+    dg.features = torch.randn(n, 12, generator=g)
+    dg.labels = (torch.rand(n, 3, generator=g) > 0.5).float()
+    return dg, indptr, nbr, w, nw
+
+
+def test_shard_csr_partitions_rows_cpu():
+    from euler_amd.graph.sharded_graph import shard_csr
+
+    _, indptr, nbr, w, _ = _graph()
+    T, N = 2, 300
+    for W in (1, 2, 3):
+        for r in range(W):
+            lip, ln, lw = shard_csr(indptr.numpy(), nbr.numpy(), w.numpy(), T, W, r)
+            for i, row in enumerate(range(r, N, W)):
+                for t in range(T):
+                    a, b = int(indptr[row * T + t]), int(indptr[row * T + t + 1])
+                    la, lb = int(lip[i * T + t]), int(lip[i * T + t + 1])
+                    assert np.array_equal(ln[la:lb], nbr[a:b].numpy()) and np.allclose(lw[la:lb], w[a:b].numpy())
+
+
+def _worker_sampling(rank, world, port, q):
+    try:
+        _init(rank, world, port)
+        from euler_amd.graph.sharded_graph import ShardedDeviceGraph
+
+        g, indptr, nbr, w, nw = _graph()
+        sg = ShardedDeviceGraph.from_full(g, node_weights=nw)
+        assert sg.local.num_rows == len(range(rank, g.num_rows, world))
+        T = 2
+        ok = True
+        # every draw is a real neighbour of its row over the requested types
+        rows = torch.randint(0, g.num_rows, (400,), generator=torch.Generator().manual_seed(rank))
+        rows[3] = 7
+        rows[10] = -1
+        sg.advance()
+        sg.reseed_cpu()
+        nb, ww, tt = sg.sample_neighbor(rows, 6, edge_types=[1], with_weights=True)
+        for k, r in enumerate(rows.tolist()):
+            if r < 0 or r == 7:
+                ok &= bool((nb[k] == -1).all())
+                continue
+            a, b = int(indptr[r * T + 1]), int(indptr[r * T + 2])
+            cand = set(nbr[a:b].tolist())
+            if not cand:
+                ok &= bool((nb[k] == -1).all())
+            else:
+                ok &= set(nb[k].tolist()) <= cand and bool((tt[k] == 1).all())
+        # frequencies of one row's neighbours follow the edge weights
+        hot = int(torch.argmax(indptr[2::2] - indptr[1::2]))  # the row with the most type-1 edges
+        cnt = torch.zeros(g.num_rows)
+        for s in range(100):
+            sg.advance()
+            sg.reseed_cpu()
+            d = sg.sample_neighbor(torch.full((60,), hot), 10, edge_types=[1]).reshape(-1).long()
+            cnt.index_add_(0, d[d >= 0], torch.ones(int((d >= 0).sum())))
+        a, b = int(indptr[hot * T + 1]), int(indptr[hot * T + 2])
+        exp = torch.zeros(g.num_rows).index_add_(0, nbr[a:b], w[a:b])
+        exp = exp / exp.sum() * cnt.sum()
+        tv = float((cnt - exp).abs().sum() / (2 * cnt.sum()))
+        ok &= tv < 0.03
+        # roots follow the global node weights
+        rc = torch.zeros(g.num_rows)
+        for s in range(40):
+            sg.advance()
+            sg.reseed_cpu()
+            r = sg.sample_node(1000).long()
+            ok &= bool((r >= 0).all())
+            rc.index_add_(0, r, torch.ones(r.numel()))
+        pe = torch.from_numpy(nw / nw.sum()).float()
+        tv_root = float((rc / rc.sum() - pe).abs().sum() / 2)
+        ok &= tv_root < 0.06
+        # features / labels
+        ids = torch.tensor([5, -1, 299, 0, 5, 150])
+        f = sg.gather_features(ids)
+        ref = torch.where((ids >= 0).unsqueeze(1), g.features[ids.clamp(min=0)], torch.zeros(()))
+        ok &= torch.equal(f, ref) and torch.equal(sg.gather_labels(ids[ids >= 0]), g.labels[ids[ids >= 0]])
+        sg.check_overflow()
+        q.put((rank, "sampling", bool(ok), tv, tv_root))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_sampling_exact_support_and_frequencies(world):
+    res = _run(_worker_sampling, world=world)
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == world and all(r[2] for r in res), res
+
+
+def _model(ds):
+    from euler_amd import models as Z
+
+    torch.manual_seed(0)
+    return Z.SupervisedGNN("gcn", "sage", [16, 16, ds.label_dim], [5, 3], [["train"], ["train"]], "feature",
+                           ds.feature_dim, "label", ds.label_dim, max_id=ds.max_node_id)
+
+
+def test_one_rank_sharded_trainer_equals_unsharded_cpu(tmp_path):
+    """one rank: the sharded trainer (exchanges degenerate to local gathers) = the
+    unsharded FullFlowTrainer on the same local graph, loss and parameters, 6 steps"""
+    import copy
+
+    from euler_amd.dataflow.device_flow import DeviceSageFlow
+    from euler_amd.dataset import get_dataset
+    from euler_amd.graph.device_graph import DeviceGraph
+    from euler_amd.graph.sharded_graph import ShardedDeviceGraph
+    from euler_amd.models.full_trainer import FullFlowTrainer, ShardedFlowTrainer
+
+    ds = get_dataset("ppi", data_dir=str(tmp_path / "ppi"), scale=0.05)
+    ds.load_graph()
+    g = DeviceGraph.from_engine(features=["feature"], feature_dims=[ds.feature_dim], label="label",
+                                label_dim=ds.label_dim, feature_dtype=torch.float32, seed=4, device="cpu")
+    sg = ShardedDeviceGraph.from_full(g)
+    loc = sg.local
+    m1 = _model(ds)
+    with torch.no_grad():
+        from euler_amd.ops import graph_api as G  # noqa: F401
+    tr1 = ShardedFlowTrainer.from_model(m1, sg, 32)
+    m2 = copy.deepcopy(m1)
+    flow = DeviceSageFlow(loc, tr1.flow.edge_types, [5, 3], 32, tr1.flow.self_loops)
+    tr2 = FullFlowTrainer(m2, loc, 32, None, features=loc.features, labels=loc.labels, flow=flow)
+    # same weights after materialisation (lazy layers): copy tr1's into tr2
+    tr2.model.load_state_dict(tr1.model.state_dict())
+    tr2.flat.flat.copy_(tr1.flat.flat)
+    rng0 = loc.rng.clone()
+    l1, l2 = [], []
+    for _ in range(6):
+        l1.append(float(tr1.step()))
+    p1 = tr1.flat.flat.clone()
+    loc.rng.copy_(rng0)
+    for _ in range(6):
+        l2.append(float(tr2.step()))
+    assert l1 == l2, (l1, l2)
+    assert torch.equal(p1, tr2.flat.flat)
+
+
+def _worker_estimator(rank, world, port, q, tmp):
+    try:
+        _init(rank, world, port)
+        from euler_amd.models.full_trainer import ShardedFlowTrainer
+        from euler_amd.tools import runner
+
+        a = runner.parse_args(["--dataset", "ppi", "--scale", "0.05", "--batch_size", "32", "--total_step", "8",
+                               "--log_steps", "4", "--model_dir", os.path.join(tmp, "ckpt"), "--device_graph_sharded",
+                               "--device", "cpu", "--seed", "1", "--fanouts", "5", "3",
+                               "--device_feature_dtype", "fp32"], model="graphsage")
+        _, est = runner.build(a)
+        res = est.train()
+        tr = est.device_trainer
+        n = tr.graph.num_rows
+        half = tr.graph.local.num_rows == len(range(rank, n, world)) and tr.graph.features.shard.shape[0] < n
+        flat = tr.flat.flat.detach().clone()
+        allp = [torch.zeros_like(flat) for _ in range(world)]
+        dist.all_gather(allp, flat)
+        same = all(torch.equal(x, allp[0]) for x in allp)
+        ok = (isinstance(tr, ShardedFlowTrainer) and half and same and est.global_step == 8
+              and math.isfinite(res["loss"]))
+        # resumes from the shared model_dir (rank 0 wrote the checkpoint)
+        a2 = runner.parse_args(["--dataset", "ppi", "--scale", "0.05", "--batch_size", "32", "--total_step", "12",
+                                "--log_steps", "4", "--model_dir", os.path.join(tmp, "ckpt"), "--device_graph_sharded",
+                                "--device", "cpu", "--seed", "1", "--fanouts", "5", "3",
+                                "--device_feature_dtype", "fp32"], model="graphsage")
+        _, est2 = runner.build(a2)
+        est2.train()
+        ok &= est2.global_step == 12
+        q.put((rank, "sharded_estimator", bool(ok), half, same))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_estimator_sharded_graph_two_ranks_lockstep(tmp_path):
+    res = _run(_worker_estimator, str(tmp_path))
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == 2 and all(r[2] for r in res), res
