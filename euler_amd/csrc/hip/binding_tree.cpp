@@ -467,12 +467,15 @@ class TreePlan {
     torch::Tensor lab = T("labels");
     TORCH_CHECK(lab.is_cuda() && lab.is_contiguous() && lab.device() == dev_, "labels must be contiguous on the GPU");
     TORCH_CHECK(mode >= 0 && mode <= 2, "label_mode must be 0, 1 or 2");
+    // "label_rows": a label table over other rows than the graph's (the row-sharded trainer
+    // hands the head a [B] table of the batch's labels with roots = 0 .. B-1)
+    const int64_t lrows = has("label_rows") ? geti("label_rows") : graph_.num_rows;
     if (mode == 0) {
-      TORCH_CHECK(lab.scalar_type() == torch::kInt16 && lab.numel() == graph_.num_rows, "labels int16 [N]");
+      TORCH_CHECK(lab.scalar_type() == torch::kInt16 && lab.numel() == lrows, "labels int16 [N]");
     } else if (mode == 1) {
-      TORCH_CHECK(lab.scalar_type() == torch::kInt32 && lab.numel() == graph_.num_rows, "labels int32 [N]");
+      TORCH_CHECK(lab.scalar_type() == torch::kInt32 && lab.numel() == lrows, "labels int32 [N]");
     } else {
-      TORCH_CHECK(lab.scalar_type() == torch::kBFloat16 && lab.numel() == graph_.num_rows * C_, "labels bf16 [N, C]");
+      TORCH_CHECK(lab.scalar_type() == torch::kBFloat16 && lab.numel() == lrows * C_, "labels bf16 [N, C]");
     }
     a.labels = lab.data_ptr();
     a.label_mode = mode;

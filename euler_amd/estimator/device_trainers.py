@@ -171,6 +171,15 @@ def build_sharded_trainer(est, model, first):
                                        feature_dims=gnn.feature_dim, label=model.label_idx,
                                        label_dim=model.label_dim, feature_dtype=c.feature_dtype(),
                                        seed=c.seed * 7919 + est.rank, device=est.device)
+    from euler_amd.convolution.convs import SAGEConv
+
+    if all(isinstance(cv, SAGEConv) for cv in gnn.convs) and c.params.get("sharded_fused", True):
+        # SupervisedGraphSage: the fused tree-step kernels on trees drawn across the ranks
+        from euler_amd.models.sharded_sage import ShardedSageTrainer
+
+        tr = ShardedSageTrainer.from_model(model, g, c.batch, keep_samples=False, **c.opt_kw())
+        tr.device_trainer_kind = "sharded_graphsage"
+        return tr
     tr = ShardedFlowTrainer.from_model(model, g, c.batch, **c.opt_kw())
     tr.device_trainer_kind = "sharded_sage_flow"
     return tr

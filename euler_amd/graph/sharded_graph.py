@@ -164,12 +164,13 @@ class ShardedDeviceGraph:
     def set_root_weight(self, root_weight=None):
         """the owner alias table of the W shards' root-weight sums (all-gathered)"""
         wl = float(self.local.node_prob.numel() if root_weight is None else root_weight)
-        sums = torch.tensor([wl], dtype=torch.float64)
+        # on the graph's device: the process group's backend may be nccl (RCCL)
+        sums = torch.tensor([wl], dtype=torch.float64, device=self.device)
         if self.comm:
-            out = [torch.zeros(1, dtype=torch.float64) for _ in range(self.world)]
+            out = [torch.zeros(1, dtype=torch.float64, device=self.device) for _ in range(self.world)]
             dist.all_gather(out, sums, group=self.group)
             sums = torch.cat(out)
-        self.shard_weight = sums.numpy().copy()
+        self.shard_weight = sums.cpu().numpy().copy()
         if not (self.shard_weight > 0).any():
             raise ValueError("no shard holds a root candidate")
         p, a = build_alias_table(self.shard_weight)
@@ -279,6 +280,19 @@ class ShardedDeviceGraph:
         return out_nb, self._back(w.view(-1, F).float(), pos, 0.0), self._back(t.view(-1, F).int(), pos, -1)
 
     # ------------------------------------------------------------------ features / labels
+    def padded_features(self, mult: int = 16):
+        """the feature exchange over a shard whose width is padded to ``mult`` columns
+        (zeros; the fused SAGE kernels read 16-column groups)"""
+        sf = self.features
+        if sf is None or sf.dim % mult == 0:
+            return sf
+        if getattr(self, "_padded", None) is None:
+            w = -(-sf.dim // mult) * mult
+            shard = torch.zeros(sf.shard.shape[0], w, dtype=sf.shard.dtype, device=sf.shard.device)
+            shard[:, : sf.dim] = sf.shard
+            self._padded = ShardedFeatures(shard, self.num_rows, self.group, sf.comm)
+        return self._padded
+
     def gather_features(self, rows: torch.Tensor) -> torch.Tensor:
         """feature rows [n, D] of global rows (``-1``: zeros), through the feature exchange"""
         return self._gather(self.features, rows)

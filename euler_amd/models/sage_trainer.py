@@ -86,7 +86,8 @@ _PIPELINE = os.environ.get("EULER_AMD_PIPELINE", "0") == "1"
 class SageTrainer:
     def __init__(self, graph, batch_size, fanouts, dims, label_dim, features=None, labels=None, metapath=None,
                  add_self_loops=False, optimizer="adam", learning_rate=0.01, betas=(0.9, 0.999), eps=1e-8,
-                 weight_decay=0.0, init=None, init_seed=0, keep_samples=True, grad_buckets=1, feature_shard=None):
+                 weight_decay=0.0, init=None, init_seed=0, keep_samples=True, grad_buckets=1, feature_shard=None,
+                 feature_dim=None):
         self.graph = graph
         # row-sharded features (graph/sharded_features.py): this rank holds rows r % W; each
         # step's sampled rows come over the all-to-all into a fixed cache the forward reads
@@ -121,10 +122,12 @@ class SageTrainer:
             feats = feature_shard.shard
             if feats.shape[1] % 16 or feats.dtype not in (torch.bfloat16, torch.float32):
                 raise ValueError("sharded features must be bf16 / fp32 with a width padded to 16")
+            if feature_dim is not None and _ceil(int(feature_dim), 16) != feats.shape[1]:
+                raise ValueError(f"feature_dim {feature_dim} does not pad to the shard's {feats.shape[1]} columns")
         labs = labels if labels is not None else graph.labels
         if feats is None or labs is None:
             raise ValueError("features and labels are required (or a graph built with from_engine)")
-        self.D = int(feats.shape[1])
+        self.D = int(feature_dim) if feature_dim is not None else int(feats.shape[1])  # real width (padded: Dp)
         masks = metapath if metapath is not None else [None] * self.L
         if len(masks) != self.L:
             raise ValueError("one metapath entry (edge types) per hop")
@@ -315,6 +318,7 @@ class SageTrainer:
              "node_alias": g.node_alias, "root_rows": g.root_rows, "rng": g.rng,
              "labels": self.labels, "label_mode": self.label_mode,
              "step": self._step, "flat": self.flat, "grad": self.grad, "m": self.m, "v": self.v,
+             "label_rows": getattr(self, "_label_rows", None),
              "offsets": self.offsets, "loss_acc": self.loss_acc, "loss_out": self.loss_out, "counts": self.counts,
              "lr": self.lr, "beta1": self.betas[0], "beta2": self.betas[1], "eps": self.eps,
              "weight_decay": self.wd, "opt_kind": _OPT_KIND[self.opt_name]}

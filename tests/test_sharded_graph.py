@@ -22,7 +22,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from test_parallel import _init, _run  # noqa: E402
 
 
-def _graph(n=300, T=2, seed=0):
+def _graph(n=300, T=2, seed=0, device="cpu"):
     from euler_amd.graph.device_graph import DeviceGraph
 
     g = torch.Generator().manual_seed(seed)
@@ -34,9 +34,9 @@ def _graph(n=300, T=2, seed=0):
     nbr = torch.randint(0, n, (E,), generator=g)
     w = torch.rand(E, generator=g) + 0.1
     nw = torch.rand(n, generator=g).numpy() + 0.05
-    dg = DeviceGraph.from_csr(indptr.numpy(), nbr.numpy(), w.numpy(), T, node_weights=nw, seed=5, device="cpu")
-    dg.features = torch.randn(n, 12, generator=g)
-    dg.labels = (torch.rand(n, 3, generator=g) > 0.5).float()
+    dg = DeviceGraph.from_csr(indptr.numpy(), nbr.numpy(), w.numpy(), T, node_weights=nw, seed=5, device=device)
+    dg.features = torch.randn(n, 12, generator=g).to(device)
+    dg.labels = (torch.rand(n, 3, generator=g) > 0.5).float().to(device)
     return dg, indptr, nbr, w, nw
 
 
@@ -175,35 +175,51 @@ def test_one_rank_sharded_trainer_equals_unsharded_cpu(tmp_path):
 
 
 def _worker_estimator(rank, world, port, q, tmp):
+    """runner graphsage --device_graph_sharded (the fused tree step on trees drawn across
+    the ranks) trains, stays in lockstep, resumes; a non-SAGE convolution on the sampled
+    flow (ShardedFlowTrainer) too"""
     try:
         _init(rank, world, port)
+        from euler_amd.dataset import get_dataset
+        from euler_amd.estimator import NodeEstimator
         from euler_amd.models.full_trainer import ShardedFlowTrainer
+        from euler_amd.models.sharded_sage import ShardedSageTrainer
         from euler_amd.tools import runner
 
-        a = runner.parse_args(["--dataset", "ppi", "--scale", "0.05", "--batch_size", "32", "--total_step", "8",
-                               "--log_steps", "4", "--model_dir", os.path.join(tmp, "ckpt"), "--device_graph_sharded",
-                               "--device", "cpu", "--seed", "1", "--fanouts", "5", "3",
-                               "--device_feature_dtype", "fp32"], model="graphsage")
+        def same_on_all(t):
+            allp = [torch.zeros_like(t) for _ in range(world)]
+            dist.all_gather(allp, t)
+            return all(torch.equal(x, allp[0]) for x in allp)
+
+        flags = ["--dataset", "ppi", "--scale", "0.05", "--batch_size", "32", "--log_steps", "4",
+                 "--model_dir", os.path.join(tmp, "ckpt"), "--device_graph_sharded", "--device", "cpu", "--seed", "1",
+                 "--fanouts", "5", "3", "--device_feature_dtype", "fp32"]
+        a = runner.parse_args(flags + ["--total_step", "8"], model="graphsage")
         _, est = runner.build(a)
         res = est.train()
         tr = est.device_trainer
-        n = tr.graph.num_rows
-        half = tr.graph.local.num_rows == len(range(rank, n, world)) and tr.graph.features.shard.shape[0] < n
-        flat = tr.flat.flat.detach().clone()
-        allp = [torch.zeros_like(flat) for _ in range(world)]
-        dist.all_gather(allp, flat)
-        same = all(torch.equal(x, allp[0]) for x in allp)
-        ok = (isinstance(tr, ShardedFlowTrainer) and half and same and est.global_step == 8
+        n = tr.sgraph.num_rows
+        half = tr.sgraph.local.num_rows == len(range(rank, n, world)) and tr.sgraph.features.shard.shape[0] < n
+        p = tr.logical_params()
+        flat = torch.cat([p[k].reshape(-1).float() for k in sorted(p)])
+        ok = (isinstance(tr, ShardedSageTrainer) and half and same_on_all(flat) and est.global_step == 8
               and math.isfinite(res["loss"]))
-        # resumes from the shared model_dir (rank 0 wrote the checkpoint)
-        a2 = runner.parse_args(["--dataset", "ppi", "--scale", "0.05", "--batch_size", "32", "--total_step", "12",
-                                "--log_steps", "4", "--model_dir", os.path.join(tmp, "ckpt"), "--device_graph_sharded",
-                                "--device", "cpu", "--seed", "1", "--fanouts", "5", "3",
-                                "--device_feature_dtype", "fp32"], model="graphsage")
+        a2 = runner.parse_args(flags + ["--total_step", "12"], model="graphsage")
         _, est2 = runner.build(a2)
         est2.train()
         ok &= est2.global_step == 12
-        q.put((rank, "sharded_estimator", bool(ok), half, same))
+        # another convolution on the sampled flow: the generic trainer over the sharded graph
+        ds = get_dataset("ppi", data_dir=os.path.join(tmp, "ppi2"), scale=0.05)
+        ds.load_graph()
+        m = _model(ds)
+        tnt = ds.train_node_type[0] if isinstance(ds.train_node_type, list) else ds.train_node_type
+        est3 = NodeEstimator(m, {"model_dir": os.path.join(tmp, "ckpt3"), "batch_size": 32, "total_step": 6,
+                                 "log_steps": 3, "device": "cpu", "device_graph": True, "device_graph_sharded": True,
+                                 "train_node_type": tnt, "seed": 2, "device_feature_dtype": "fp32"})
+        est3.train()
+        tr3 = est3.device_trainer
+        ok &= isinstance(tr3, ShardedFlowTrainer) and same_on_all(tr3.flat.flat.detach().clone())
+        q.put((rank, "sharded_estimator", bool(ok), half))
         dist.destroy_process_group()
     except Exception:  # pragma: no cover
         import traceback
@@ -215,3 +231,110 @@ def test_estimator_sharded_graph_two_ranks_lockstep(tmp_path):
     res = _run(_worker_estimator, str(tmp_path))
     assert not [r for r in res if r[1] == "error"], res
     assert len(res) == 2 and all(r[2] for r in res), res
+
+
+def test_one_rank_sharded_sage_trainer_equals_sage_trainer_cpu():
+    """one rank: the fused-step trainer on trees drawn through the sharded graph = the
+    whole-graph SageTrainer (its CPU twin draws the same tree), 5 steps"""
+    from euler_amd.graph.sharded_graph import ShardedDeviceGraph
+    from euler_amd.models.sage_trainer import SageTrainer
+    from euler_amd.models.sharded_sage import ShardedSageTrainer
+
+    g, _, _, _, nw = _graph()
+    g.labels = (torch.rand(g.num_rows, 5, generator=torch.Generator().manual_seed(1)) > 0.6).float()
+    sg = ShardedDeviceGraph.from_full(g, node_weights=nw)
+    loc = sg.local
+    kw = dict(metapath=[[0, 1], [1]], init_seed=3, learning_rate=0.01)
+    a = ShardedSageTrainer(sg, 32, [4, 3], [16, 16, 8], 5, **kw)
+    assert a.D == 12 and a.fshard.shard.shape[1] == 16
+    b = SageTrainer(loc, 32, [4, 3], [16, 16, 8], 5, features=loc.features, labels=loc.labels, **kw)
+    r0 = loc.rng.clone()
+    la = [float(a.step()) for _ in range(5)]
+    loc.rng.copy_(r0)
+    lb = [float(b.step()) for _ in range(5)]
+    assert la == lb, (la, lb)
+    pa, pb = a.logical_params(), b.logical_params()
+    assert all(torch.equal(pa[k], pb[k]) for k in pa)
+
+
+@pytest.mark.gpu
+def test_sharded_graph_exchanges_on_the_gpu_one_rank_rccl():
+    """the HIP route kernel + RCCL all-to-all path (force_comm on a 1-rank nccl group): every
+    draw is a real neighbour, roots are valid rows, feature rows equal the table's"""
+    from test_parallel import _free_port
+
+    from euler_amd.graph.sharded_graph import ShardedDeviceGraph
+
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
+    try:
+        g, indptr, nbr, w, nw = _graph(device="cuda")
+        sg = ShardedDeviceGraph.from_full(g, force_comm=True, node_weights=nw)
+        assert sg.comm and sg.world == 1
+        rows = torch.randint(0, g.num_rows, (4096,), device="cuda")
+        rows[3] = 7
+        sg.advance()
+        nb = sg.sample_neighbor(rows, 6, edge_types=[1]).long().cpu()
+        for k, r in enumerate(rows.cpu().tolist()):
+            a, b = int(indptr[r * 2 + 1]), int(indptr[r * 2 + 2])
+            cand = set(nbr[a:b].tolist())
+            assert (set(nb[k].tolist()) <= cand) if cand else bool((nb[k] == -1).all()), (k, r)
+        roots = sg.sample_node(2048).long()
+        assert bool(((roots >= 0) & (roots < g.num_rows)).all())
+        ids = torch.tensor([5, -1, 299, 0, 5, 150], device="cuda")
+        f = sg.gather_features(ids).float()
+        ref = torch.where((ids >= 0).unsqueeze(1), g.features[ids.clamp(min=0)], torch.zeros((), device="cuda"))
+        assert torch.equal(f, ref.float())
+        sg.check_overflow()
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_sage_trainer_gpu_matches_bf16_oracle():
+    """the fused tree step on a tree drawn through the sharded graph (HIP route kernel +
+    RCCL all-to-all on a 1-rank nccl group): loss and gradients match the bf16-aware fp32
+    oracle on the same tree and batch labels; every draw is a real edge; it trains"""
+    import math
+
+    from test_parallel import _free_port
+
+    from euler_amd.graph.sharded_graph import ShardedDeviceGraph
+    from euler_amd.models.sharded_sage import ShardedSageTrainer
+
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
+    try:
+        g, indptr, nbr, w, nw = _graph(device="cuda")
+        g.labels = (torch.rand(g.num_rows, 5, generator=torch.Generator().manual_seed(1)) > 0.6).float().cuda()
+        sg = ShardedDeviceGraph.from_full(g, force_comm=True, node_weights=nw)
+        tr = ShardedSageTrainer(sg, 64, [4, 3], [64, 64, 32], 5, metapath=[[0, 1], [1]], init_seed=3)
+        tr.forward_backward()
+        torch.cuda.synchronize()
+        loss_k = float(tr.loss_acc.item())
+        grads_k = tr.gradients()
+        loss_b, grads_b = tr.reference_loss_and_grads_bf16()
+        assert abs(loss_k - loss_b) <= 1e-4 * abs(loss_b), (loss_k, loss_b)
+        for k in grads_b:
+            rel = float((grads_k[k].float().cpu() - grads_b[k].float().cpu()).norm() /
+                        grads_b[k].float().cpu().norm().clamp(min=1e-12))
+            assert rel < 1e-3, (k, rel)
+        roots, nodes, leaf = (t.cpu() for t in tr.samples())
+        for i in range(0, nodes.numel(), 7):
+            r = int(nodes[i])
+            if r < 0:
+                continue
+            a, b = int(indptr[r * 2 + 1]), int(indptr[r * 2 + 2])
+            cand = set(nbr[a:b].tolist())
+            got = set(leaf[i].tolist())
+            assert (got <= cand) if cand else got == {-1}, (i, r)
+        tr.optimizer_step()
+        first = None
+        for _ in range(60):
+            tr.step()
+            first = first if first is not None else float(tr.loss.item())
+        torch.cuda.synchronize()
+        last = float(tr.loss.item())
+        assert math.isfinite(last) and last < first, (first, last)
+        sg.check_overflow()
+    finally:
+        dist.destroy_process_group()
