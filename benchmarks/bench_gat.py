@@ -43,61 +43,8 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 from euler_amd.graph.device_graph import DeviceGraph  # noqa: E402
-from euler_amd.ops import gnn_ops, mp_ops  # noqa: E402
-
-
-def add_self_loops(indptr, col):
-    """CSR (rows = destinations) with a self-loop prepended to every row."""
-    n = indptr.numel() - 1
-    dev = indptr.device
-    deg = torch.diff(indptr)
-    new_indptr = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-    torch.cumsum(deg + 1, 0, out=new_indptr[1:])
-    new_col = torch.empty(int(col.numel()) + n, dtype=torch.int32, device=dev)
-    new_col[new_indptr[:-1]] = torch.arange(n, dtype=torch.int32, device=dev)
-    row = torch.repeat_interleave(torch.arange(n, device=dev), deg)
-    pos = torch.arange(col.numel(), device=dev) - indptr[row] + new_indptr[row] + 1
-    new_col[pos] = col
-    return new_indptr, new_col
-
-
-class GATNet(nn.Module):
-    def __init__(self, in_dim, heads, ch, n_cls, layers=2, impl="fused"):
-        super().__init__()
-        self.heads, self.ch, self.impl = heads, ch, impl
-        dims = [in_dim] + [heads * ch] * layers
-        self.lin = nn.ModuleList([nn.Linear(dims[i], dims[i + 1], bias=False) for i in range(layers)])
-        self.att_src = nn.ParameterList([nn.Parameter(torch.randn(heads, ch) * 0.1) for _ in range(layers)])
-        self.att_dst = nn.ParameterList([nn.Parameter(torch.randn(heads, ch) * 0.1) for _ in range(layers)])
-        self.out = nn.Linear(heads * ch, n_cls)
-
-    def forward(self, x, csr, rows=None):
-        h = x
-        H, C = self.heads, self.ch
-        for lin, a_s, a_d in zip(self.lin, self.att_src, self.att_dst):
-            if self.impl == "fused":
-                # projection (hipBLASLt; split-K weight gradient), then attention terms +
-                # edge softmax + aggregation in gat.hip
-                z = gnn_ops.tall_linear(h, lin.weight).view(-1, H, C)
-                agg = gnn_ops.gat_conv(z, a_s, a_d, csr, 0.2)
-            else:
-                z = lin(h).view(-1, H, C)
-                al = (z.float() * a_s).sum(-1)
-                ar = (z.float() * a_d).sum(-1)
-                ei = csr.edge_index
-                seg = csr_seg(csr)
-                logit = F.leaky_relu(mp_ops.gather(ar, ei[0]) + mp_ops.gather(al, ei[1]), 0.2)
-                alpha = mp_ops.scatter_softmax(logit, seg, csr.n_dst)
-                # messages and their sums in fp32 like the fused kernel's accumulators (bf16
-                # messages summed over ~50 in-edges cost this variant ~13 points of held-out
-                # accuracy at 400 epochs: profiles/r3_learning/bench_gat_composed_bf16msg.log)
-                msg = mp_ops.gather(z.reshape(-1, H * C), ei[1]).view(-1, H, C).float() * alpha.unsqueeze(-1).float()
-                agg = mp_ops.scatter_add(msg.reshape(-1, H * C), seg, csr.n_dst).view(-1, H, C).to(z.dtype)
-            h = F.elu(agg.reshape(-1, H * C))
-        # the classifier only runs on the rows the loss reads (same loss and gradients
-        # as classifying every node; avoids a 2.4M-row logits tensor and its bias reduce)
-        hr = h if rows is None else h[rows]
-        return gnn_ops.tall_linear(hr, self.out.weight, self.out.bias)
+from euler_amd.models.gat_full import FullGraphGAT, FullGraphGatTrainer, add_self_loops  # noqa: E402
+from euler_amd.ops import gnn_ops  # noqa: E402
 
 
 def planted_labels(indptr, col, x, n_cls, seed=11, hops=2):
@@ -119,12 +66,6 @@ def planted_labels(indptr, col, x, n_cls, seed=11, hops=2):
     return (agg @ proj).argmax(1)
 
 
-def csr_seg(csr):
-    if not hasattr(csr, "_seg"):
-        csr._seg = mp_ops.SegmentIndex(csr.edge_index[0].long(), csr.n_dst)
-    return csr._seg
-
-
 def main(argv=None):
     p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     p.add_argument("--epochs", type=int, default=20)
@@ -143,6 +84,7 @@ def main(argv=None):
     p.add_argument("--label-hops", type=int, default=2, help="planted labels: argmax of a projection of the "
                    "label-hops-times neighbourhood mean")
     p.add_argument("--lr", type=float, default=5e-3)
+    p.add_argument("--no-graph", action="store_true", help="eager epochs (default: the epoch captured in a hipGraph)")
     args = p.parse_args(argv)
     if not torch.cuda.is_available():
         raise SystemExit("bench_gat.py needs a GPU")
@@ -161,47 +103,45 @@ def main(argv=None):
     train_idx = perm[: int(N * args.train_frac)]
     test_idx = perm[int(N * args.train_frac):][:50_000]
     y_train = y[train_idx]
-    model = GATNet(args.feature_dim, args.heads, args.head_dim, args.classes, 2, args.impl).to(dev)
-    opt = torch.optim.Adam(model.parameters(), lr=args.lr, fused=True)
+    model = FullGraphGAT(args.feature_dim, args.heads, args.head_dim, args.classes, 2, args.impl).to(dev)
+    # the product's trainer: flat Adam over one parameter buffer, the epoch captured in a
+    # hipGraph (models/gat_full.py)
+    tr = FullGraphGatTrainer(model, x, csr, y, train_idx, "adam", args.lr)
     torch.cuda.synchronize()
     print(f"[bench_gat] graph {N} nodes {E} edges (with self-loops), setup {time.time() - t0:.1f}s",
           file=sys.stderr, flush=True)
+    graph = not args.no_graph and args.impl == "fused"
 
-    def step():
-        with torch.autocast("cuda", dtype=torch.bfloat16):
-            logits = model(x, csr, train_idx)
-        loss = gnn_ops.xent(logits, y_train)
-        opt.zero_grad(set_to_none=True)
-        loss.backward()
-        opt.step()
-        return loss.detach()
-
-    @torch.no_grad()
     def accuracy():
-        with torch.autocast("cuda", dtype=torch.bfloat16):
-            logits = model(x, csr, test_idx)
-        return round(float((logits.float().argmax(1) == y[test_idx]).float().mean()), 4)
+        return round(tr.accuracy(test_idx), 4)
 
     acc_init = accuracy()
-    for _ in range(args.warmup):
-        loss0 = step()
+    if graph:
+        tr.capture(warmup=args.warmup, steps=1)  # warm-up epochs run eagerly, then the capture
+        run = tr.replay_steps
+    else:
+        for _ in range(args.warmup):
+            tr.step()
+
+        def run(n):
+            for _ in range(n):
+                tr.step()
     torch.cuda.synchronize()
-    first = float(loss0)
+    first = float(tr.loss.item())
     t1 = time.perf_counter()
-    for i in range(args.epochs):
-        loss = step()
-        if (i + 1) % 10 == 0:
-            print(f"[bench_gat] timed epoch {i + 1}", file=sys.stderr, flush=True)
+    for i in range(0, args.epochs, 10):
+        run(min(10, args.epochs - i))
+        print(f"[bench_gat] timed epoch {min(i + 10, args.epochs)}", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     el = time.perf_counter() - t1
     ms = el * 1e3 / args.epochs
+    loss = tr.loss
     acc_timed = accuracy()
     done = args.warmup + args.epochs
     while done < args.eval_epochs:  # untimed: learning evidence only
-        loss = step()
-        done += 1
-        if done % 25 == 0:
-            print(f"[bench_gat] epoch {done} loss {float(loss):.4f}", file=sys.stderr, flush=True)
+        run(min(25, args.eval_epochs - done))
+        done = min(done + 25, args.eval_epochs)
+        print(f"[bench_gat] epoch {done} loss {float(tr.loss.item()):.4f}", file=sys.stderr, flush=True)
     acc_final = accuracy()
     out = {
         "metric": "GAT 8-head full-graph training throughput on ogbn-products-shaped synthetic graph",
@@ -216,7 +156,8 @@ def main(argv=None):
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic (power-law graph of ogbn-products shape, random-normal features)",
-        "config": {"model": f"GAT 2x({args.heads} heads x {args.head_dim}) + linear, full-graph, Adam",
+        "config": {"model": f"GAT 2x({args.heads} heads x {args.head_dim}) + linear, full-graph, flat Adam",
+                   "trainer": "euler_amd.models.gat_full.FullGraphGatTrainer", "hipgraph": graph,
                    "num_nodes": N, "num_edges": E, "edges_per_s": round(E * 2 * args.epochs / el, 1),
                    "feature_dim": args.feature_dim, "classes": args.classes, "impl": args.impl,
                    "label_hops": args.label_hops, "lr": args.lr,

@@ -442,6 +442,46 @@ std::vector<torch::Tensor> occ_csr(torch::Tensor inv, int64_t n_u) {
   return {ptr, list};
 }
 
+// deterministic occurrence CSR of `keys` over S segments (keys < 0 skipped): (ptr [S + 1]
+// int64, perm [n] int32: each segment's occurrence ids ascending) — det_segment_sum's
+// inputs for a fixed-order per-row sum
+std::vector<torch::Tensor> det_occ(torch::Tensor keys, int64_t S) {
+  typed(keys, torch::kInt64, "keys");
+  TORCH_CHECK(S > 0 && S < (int64_t{1} << 30) && keys.numel() < (int64_t{1} << 31), "det_occ: sizes");
+  const c10::DeviceGuard g(keys.device());
+  auto o = keys.options();
+  const int64_t n = keys.numel();
+  auto ptr = torch::empty({S + 1}, o);
+  auto perm = torch::empty({n}, o.dtype(torch::kInt32));
+  auto cnt = torch::zeros({S}, o.dtype(torch::kInt32));
+  auto work = torch::empty({3 * n + 1}, o.dtype(torch::kInt32));
+  size_t bytes = 0;
+  ok(eh_det_occ(keys.data_ptr<int64_t>(), n, S, cnt.data_ptr<int32_t>(), ptr.data_ptr<int64_t>(),
+                work.data_ptr<int32_t>(), perm.data_ptr<int32_t>(), nullptr, &bytes, stream()),
+     "det_occ(size)");
+  auto temp = torch::empty({static_cast<int64_t>(bytes) + 1}, o.dtype(torch::kUInt8));
+  ok(eh_det_occ(keys.data_ptr<int64_t>(), n, S, cnt.data_ptr<int32_t>(), ptr.data_ptr<int64_t>(),
+                work.data_ptr<int32_t>(), perm.data_ptr<int32_t>(), temp.data_ptr(), &bytes, stream()),
+     "det_occ");
+  return {ptr, perm};
+}
+
+// out [S, D] = per-segment sums of src rows over (ptr, perm) in a fixed order (det_occ's
+// CSR): deterministic, hot segments spread over a whole block
+void det_segment_sum(torch::Tensor src, torch::Tensor ptr, torch::Tensor perm, torch::Tensor out) {
+  typed(src, torch::kFloat32, "src");
+  typed(out, torch::kFloat32, "out");
+  typed(ptr, torch::kInt64, "ptr");
+  typed(perm, torch::kInt32, "perm");
+  const int64_t S = ptr.numel() - 1, D = src.size(1);
+  TORCH_CHECK(src.dim() == 2 && out.dim() == 2 && out.size(0) == S && out.size(1) == D, "det_segment_sum: shapes");
+  TORCH_CHECK(src.is_contiguous() && out.is_contiguous(), "det_segment_sum: contiguous tensors");
+  const c10::DeviceGuard g(src.device());
+  ok(eh_det_segsum(src.data_ptr<float>(), static_cast<int>(D), ptr.data_ptr<int64_t>(), perm.data_ptr<int32_t>(), S,
+                   out.data_ptr<float>(), stream()),
+     "det_segment_sum");
+}
+
 struct UpdIn {
   int64_t n_u, P, n_smap;
   const int64_t* smap;
@@ -565,7 +605,8 @@ void kg_step(torch::Tensor h, torch::Tensor rel, torch::Tensor pool, torch::Tens
              torch::Tensor o_src, torch::Tensor o_dst, torch::Tensor o_ridx, torch::Tensor o_neg, torch::Tensor coef,
              torch::Tensor part, torch::Tensor loss, torch::Tensor dent, torch::Tensor drel,
              c10::optional<torch::Tensor> drel_rep, c10::optional<torch::Tensor> occ_e,
-             c10::optional<torch::Tensor> occ_r) {
+             c10::optional<torch::Tensor> occ_r, c10::optional<torch::Tensor> key_e,
+             c10::optional<torch::Tensor> key_r) {
   for (auto* t : {&h, &rel, &coef, &part, &loss, &dent, &drel}) typed(*t, torch::kFloat32, "kg_step float buffer");
   for (auto* t : {&pool, &t_src, &t_dst, &t_rel, &step, &o_src, &o_dst, &o_ridx, &o_neg})
     typed(*t, torch::kInt64, "kg_step id buffer");
@@ -593,14 +634,22 @@ void kg_step(torch::Tensor h, torch::Tensor rel, torch::Tensor pool, torch::Tens
   }
   // deterministic mode: per-occurrence gradient rows instead of atomics (the caller sums
   // them per entity / relation in a fixed order): occ_e [B * (2 + K), D], occ_r [B, D]
+  // and the row keys of those occurrences (-1: a triple without gradient, rows not written)
   float *oe = nullptr, *orr = nullptr;
+  int64_t *ke = nullptr, *kr = nullptr;
   if (occ_e.has_value() || occ_r.has_value()) {
-    TORCH_CHECK(occ_e.has_value() && occ_r.has_value(), "kg_step: occ_e and occ_r go together");
+    TORCH_CHECK(occ_e.has_value() && occ_r.has_value() && key_e.has_value() && key_r.has_value(),
+                "kg_step: occ_e, occ_r, key_e and key_r go together");
     typed(*occ_e, torch::kFloat32, "occ_e");
     typed(*occ_r, torch::kFloat32, "occ_r");
+    typed(*key_e, torch::kInt64, "key_e");
+    typed(*key_r, torch::kInt64, "key_r");
     TORCH_CHECK(occ_e->numel() == B * (2 + K) * D && occ_r->numel() == B * D, "kg_step: occ_e [B(2+K), D], occ_r [B, D]");
+    TORCH_CHECK(key_e->numel() == B * (2 + K) && key_r->numel() == B, "kg_step: key_e [B(2+K)], key_r [B]");
     oe = occ_e->data_ptr<float>();
     orr = occ_r->data_ptr<float>();
+    ke = key_e->data_ptr<int64_t>();
+    kr = key_r->data_ptr<int64_t>();
   }
   TORCH_CHECK(part.numel() >= nparts, "kg_step: part needs ", nparts, " entries");
   TORCH_CHECK(pool.numel() > 0 && loss.numel() >= 1 && step.numel() >= 1, "kg_step: empty pool / loss / step");
@@ -611,7 +660,7 @@ void kg_step(torch::Tensor h, torch::Tensor rel, torch::Tensor pool, torch::Tens
                 static_cast<int>(kind), normalize ? 1 : 0, static_cast<float>(margin), o_src.data_ptr<int64_t>(),
                 o_dst.data_ptr<int64_t>(), o_ridx.data_ptr<int64_t>(), o_neg.data_ptr<int64_t>(),
                 coef.data_ptr<float>(), part.data_ptr<float>(), loss.data_ptr<float>(), dent.data_ptr<float>(),
-                drel.data_ptr<float>(), nullptr, rep_p, rep, rel.size(0), stream(), oe, orr),
+                drel.data_ptr<float>(), nullptr, rep_p, rep, rel.size(0), stream(), oe, orr, ke, kr),
      "kg_step");
 }
 
@@ -1118,7 +1167,10 @@ void register_gnn_ops(pybind11::module& m) {
         py::arg("t_rel"), py::arg("step"), py::arg("seed"), py::arg("kind"), py::arg("normalize"), py::arg("margin"),
         py::arg("o_src"), py::arg("o_dst"), py::arg("o_ridx"), py::arg("o_neg"), py::arg("coef"), py::arg("part"),
         py::arg("loss"), py::arg("dent"), py::arg("drel"), py::arg("drel_rep") = py::none(),
-        py::arg("occ_e") = py::none(), py::arg("occ_r") = py::none());
+        py::arg("occ_e") = py::none(), py::arg("occ_r") = py::none(), py::arg("key_e") = py::none(),
+        py::arg("key_r") = py::none());
+  m.def("det_occ", &det_occ, py::arg("keys"), py::arg("S"));
+  m.def("det_segment_sum", &det_segment_sum, py::arg("src"), py::arg("ptr"), py::arg("perm"), py::arg("out"));
   m.def("kg_step_parts", &kg_step_parts);
   m.def("cast_bf16", &cast_bf16);
   m.def("drop_rows", &drop_rows);

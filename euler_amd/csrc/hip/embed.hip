@@ -256,6 +256,84 @@ __global__ __launch_bounds__(256) void occ_count_kernel(const int64_t* __restric
   atomicAdd(cnt + inv[o], 1);
 }
 
+// deterministic occurrence CSR (keys < 0 skipped): counts + scan for ptr, and a stable
+// radix sort of (key, occurrence id) over the key's bits only for perm, so every segment's
+// occurrences are in ascending id order and a segment sum over perm adds in that order
+__global__ __launch_bounds__(256) void det_count_kernel(const int64_t* __restrict__ keys, int64_t n, int64_t S,
+                                                        int* __restrict__ cnt, int64_t* __restrict__ ptr) {
+  const int64_t o = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (o == 0) ptr[0] = 0;
+  if (o >= n) return;
+  const int64_t k = keys[o];
+  if (k >= 0 && k < S) atomicAdd(cnt + k, 1);
+}
+
+// the radix sort's inputs: 32-bit keys (a skipped key sorts last, as S) and occurrence ids
+__global__ __launch_bounds__(256) void det_prep_kernel(const int64_t* __restrict__ keys, int64_t n, int64_t S,
+                                                       int* __restrict__ k32, int* __restrict__ iota) {
+  const int64_t o = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (o >= n) return;
+  const int64_t k = keys[o];
+  k32[o] = (k >= 0 && k < S) ? static_cast<int>(k) : static_cast<int>(S);
+  iota[o] = static_cast<int>(o);
+}
+
+// out[s] = sum of src[perm[e]] over e in [ptr[s], ptr[s + 1]), in a fixed order: one block
+// per segment, row e on row-slot (e - ptr[s]) % RB (RB = 256 / (D / 4) slots side by side,
+// U rows of each slot in flight), each slot summing its rows in order, then the slot
+// partials added in slot order through LDS.  A hot row's occurrences spread over the whole
+// block instead of one wave's serial chain.  fp32, D / 4 a power of two <= 64.
+__global__ __launch_bounds__(256) void det_segsum_kernel(const float* __restrict__ src, int D,
+                                                         const int64_t* __restrict__ ptr,
+                                                         const int* __restrict__ perm, int64_t S,
+                                                         float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) float red[256 * 4];
+  const int LP = D >> 2, RB = 256 / LP;
+  const int tid = threadIdx.x, slot = tid / LP, d0 = (tid - slot * LP) * 4;
+  constexpr int U = 4;
+  for (int64_t s = blockIdx.x; s < S; s += gridDim.x) {  // uniform per block
+    const int64_t a = ptr[s], b = ptr[s + 1];
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int64_t e0 = a + slot; e0 < b; e0 += static_cast<int64_t>(RB) * U) {
+      int64_t row[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t e = e0 + static_cast<int64_t>(u) * RB;
+        row[u] = e < b ? static_cast<int64_t>(perm[e]) : -1;
+      }
+      float v[U][4];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (row[u] >= 0) {
+          EV<float>::load(src + row[u] * D + d0, v[u]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[u][i] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i] += v[u][i];
+    }
+    if (b - a <= 1) {  // one row (or none): no combine needed, slot 0 holds it
+      if (slot == 0) EV<float>::store(out + s * D + d0, acc);
+      continue;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[slot * D + d0 + i] = acc[i];
+    __syncthreads();
+    if (tid < LP) {
+      float t[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) t[i] += red[r * D + tid * 4 + i];
+      EV<float>::store(out + s * D + tid * 4, t);
+    }
+    __syncthreads();
+  }
+}
+
 struct SgnsUpd {
   const int64_t* ptr;   // [n_u + 1]
   const int* list;      // occurrence ids
@@ -603,6 +681,8 @@ struct KgStepArgs {
   float* drel_rep;     // [rep][R][D] relation-gradient replicas (rep == 0: add into drel directly)
   int64_t rep_stride;  // R * D
   int rep;
+  int64_t* key_e;  // deterministic mode: entity of every occurrence row (-1: no gradient)
+  int64_t* key_r;  // relation of every triple's relation row (-1: no gradient)
 };
 
 // drel += sum of the replicas (fixed order)
@@ -678,18 +758,21 @@ __global__ __launch_bounds__(256) void kg_step_bwd_kernel(KgStepArgs s, float* _
   const RowLane L = row_lane(a.lp, a.B);
   if (!L.ok) return;
   const float c = s.coef[L.row];
-  if (c == 0.f) {  // whole lane group: the margin holds, no gradient
-    if (occ && L.sub * 4 < a.D) {  // deterministic mode: this triple's occurrence rows are zero
-      const float z[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int k = 0; k < 2 + a.K; ++k) EV<float>::store(dent + (L.row * (2 + a.K) + k) * a.D + L.sub * 4, z);
-      EV<float>::store(drel + L.row * a.D + L.sub * 4, z);
-    }
-    return;
+  const int64_t hs = a.src[L.row], rs = a.ridx[L.row], ts = a.dst[L.row];
+  if (occ && L.sub == 0) {
+    // deterministic mode: the row keys of this triple's occurrences; a triple whose margin
+    // holds has no gradient, its rows are skipped (key -1) instead of written as zeros
+    int64_t* ke = s.key_e + L.row * (2 + a.K);
+    const bool live = c != 0.f;
+    ke[0] = live ? hs : -1;
+    ke[1] = live ? ts : -1;
+    for (int k = 0; k < a.K; ++k) ke[2 + k] = live ? a.neg[L.row * a.K + k] : -1;
+    s.key_r[L.row] = live ? rs : -1;
   }
+  if (c == 0.f) return;  // whole lane group: the margin holds, no gradient
   const float gp = -c, gn = c / static_cast<float>(2 * a.K);
   float h[4], r[4], t[4], n[4], nh, nr, nt, nn;
   float dh[4] = {0.f, 0.f, 0.f, 0.f}, dr[4] = {0.f, 0.f, 0.f, 0.f}, dt[4] = {0.f, 0.f, 0.f, 0.f};
-  const int64_t hs = a.src[L.row], rs = a.ridx[L.row], ts = a.dst[L.row];
   kg_load_norm(a.ent, hs, L.sub, a.D, a.lp, a.normalize, h, nh);
   kg_load_norm(a.rel, rs, L.sub, a.D, a.lp, a.normalize, r, nr);
   kg_load_norm(a.ent, ts, L.sub, a.D, a.lp, a.normalize, t, nt);
@@ -962,6 +1045,47 @@ hipError_t eh_occ_count_scan(const int64_t* inv, int64_t n, int64_t n_u, int* cn
   return hipcub::DeviceScan::InclusiveSum(temp, *temp_bytes, cnt, ptr + 1, static_cast<int>(n_u), s);
 }
 
+// ptr [S + 1] and perm [n] int32 (the first ptr[S] entries used) of the keys >= 0.
+// work: 4 n int32 (32-bit keys, ids, sorted keys) + S int32 counts, zeroed by the caller
+// where noted; temp: hipcub scratch for the larger of the scan and the sort (null: size
+// query into *temp_bytes)
+hipError_t eh_det_occ(const int64_t* keys, int64_t n, int64_t S, int* cnt, int64_t* ptr, int* work, int* perm,
+                      void* temp, size_t* temp_bytes, hipStream_t s) {
+  if (S <= 0 || S >= (int64_t{1} << 30) || n >= (int64_t{1} << 31)) return hipErrorInvalidValue;
+  int bits = 1;
+  while ((int64_t{1} << bits) <= S) ++bits;  // keys 0 .. S (S = skipped)
+  if (!temp) {
+    size_t a = 0, b = 0;
+    EULER_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, a, cnt, ptr + 1, static_cast<int>(S), s));
+    EULER_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, b, work, work, work, perm, static_cast<int>(n), 0,
+                                                       bits, s));
+    *temp_bytes = a > b ? a : b;
+    return hipSuccess;
+  }
+  const dim3 g(static_cast<uint32_t>(ceil_div(n > 0 ? n : 1, 256)));
+  hipLaunchKernelGGL(det_count_kernel, g, dim3(256), 0, s, keys, n, S, cnt, ptr);
+  EULER_HIP_CHECK(hipGetLastError());
+  EULER_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(temp, *temp_bytes, cnt, ptr + 1, static_cast<int>(S), s));
+  if (n == 0) return hipSuccess;
+  int* k32 = work;
+  int* iota = work + n;
+  int* ksorted = work + 2 * n;
+  hipLaunchKernelGGL(det_prep_kernel, g, dim3(256), 0, s, keys, n, S, k32, iota);
+  EULER_HIP_CHECK(hipGetLastError());
+  return hipcub::DeviceRadixSort::SortPairs(temp, *temp_bytes, k32, ksorted, iota, perm, static_cast<int>(n), 0, bits,
+                                            s);
+}
+
+hipError_t eh_det_segsum(const float* src, int D, const int64_t* ptr, const int* perm, int64_t S, float* out,
+                         hipStream_t s) {
+  if (S <= 0) return hipSuccess;
+  const int LP = D / 4;
+  if (D % 4 != 0 || LP > 64 || LP < 1 || (LP & (LP - 1)) != 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(det_segsum_kernel, dim3(static_cast<uint32_t>(S < 16384 ? S : 16384)), dim3(256), 0, s, src, D,
+                     ptr, perm, S, out);
+  return hipGetLastError();
+}
+
 hipError_t eh_occ_fill(const int64_t* inv, int64_t n, const int64_t* ptr, int* cursor, int* list, hipStream_t s) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(occ_fill_kernel, dim3(static_cast<uint32_t>(ceil_div(n, 256))), dim3(256), 0, s, inv, n, ptr,
@@ -1043,7 +1167,7 @@ hipError_t eh_kg_step(const float* ent, const float* rel, const int64_t* pool, i
                       int64_t B, int K, int D, int kind, int normalize, float margin, int64_t* o_src, int64_t* o_dst,
                       int64_t* o_ridx, int64_t* o_neg, float* coef, float* part, float* loss, float* dent,
                       float* drel, int* nparts_out, float* drel_rep, int rep, int64_t num_rel, hipStream_t s,
-                      float* occ_e, float* occ_r) {
+                      float* occ_e, float* occ_r, int64_t* key_e, int64_t* key_r) {
   if (B <= 0 || K <= 0 || K > 255 || P <= 0 || num_ent <= 0 || rep < 0) return hipErrorInvalidValue;
   if (D % 4 != 0 || D > 256 || kind < 0 || kind > 2) return hipErrorInvalidValue;
   KgStepArgs a;
@@ -1069,7 +1193,9 @@ hipError_t eh_kg_step(const float* ent, const float* rel, const int64_t* pool, i
   a.loss = loss;
   a.nparts = static_cast<int>(grid.x);
   const bool occ = occ_e != nullptr;
-  if (occ && !occ_r) return hipErrorInvalidValue;
+  if (occ && (!occ_r || !key_e || !key_r)) return hipErrorInvalidValue;
+  a.key_e = key_e;
+  a.key_r = key_r;
   a.rep = drel_rep && !occ ? rep : 0;
   a.drel_rep = drel_rep;
   a.rep_stride = num_rel * D;

@@ -118,7 +118,12 @@ hipError_t eh_kg_step(const float* ent, const float* rel, const int64_t* pool, i
                       int64_t B, int K, int D, int kind, int normalize, float margin, int64_t* o_src, int64_t* o_dst,
                       int64_t* o_ridx, int64_t* o_neg, float* coef, float* part, float* loss, float* dent,
                       float* drel, int* nparts_out, float* drel_rep, int rep, int64_t num_rel, hipStream_t s,
-                      float* occ_e = nullptr, float* occ_r = nullptr);
+                      float* occ_e = nullptr, float* occ_r = nullptr, int64_t* key_e = nullptr,
+                      int64_t* key_r = nullptr);
+hipError_t eh_det_segsum(const float* src, int D, const int64_t* ptr, const int* perm, int64_t S, float* out,
+                         hipStream_t s);
+hipError_t eh_det_occ(const int64_t* keys, int64_t n, int64_t S, int* cnt, int64_t* ptr, int* work, int* perm,
+                      void* temp, size_t* temp_bytes, hipStream_t s);
 hipError_t eh_cast_bf16(const float* x, int64_t n, void* out, hipStream_t s);
 hipError_t eh_zero(void* x, int64_t bytes, hipStream_t s);
 int eh_bce_parts(int64_t n);

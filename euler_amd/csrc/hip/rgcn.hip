@@ -262,7 +262,16 @@ __global__ __launch_bounds__(256) void rel_dw_reduce_kernel(const float* __restr
     const int i = static_cast<int>(t / (NK >> 2));
     const int64_t e = (t - static_cast<int64_t>(i) * (NK >> 2)) * 4;
     float4_t v = float4_t{0.f, 0.f, 0.f, 0.f};
-    for (int sl = rp[i]; sl < rp[i + 1]; ++sl) v += *reinterpret_cast<const float4_t*>(part + sl * NK + e);
+    const int s0 = rp[i], s1 = rp[i + 1];
+    int sl = s0;
+    for (; sl + 8 <= s1; sl += 8) {  // 8 slab loads in flight, added in slot order
+      float4_t u[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) u[k] = *reinterpret_cast<const float4_t*>(part + (sl + k) * NK + e);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v += u[k];
+    }
+    for (; sl < s1; ++sl) v += *reinterpret_cast<const float4_t*>(part + sl * NK + e);
     float4_t* d = reinterpret_cast<float4_t*>(dW + static_cast<int64_t>(mrel[i]) * NK + e);
     *d = accum ? *d + v : v;
   }

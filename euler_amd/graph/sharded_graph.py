@@ -124,6 +124,28 @@ class ShardedDeviceGraph:
         return cls(local, g.num_rows, float(nw[r::W].sum()), ids=g.ids, group=group, force_comm=force_comm, **kw)
 
     @classmethod
+    def synthetic(cls, num_nodes: int, avg_degree: float = 10.0, max_degree: int = 1024, feature_dim: int = 128,
+                  num_classes: int = 64, multi_label: bool = False, seed: int = 0, device="cuda", group=None):
+        """this rank's rows of a synthetic power-law graph generated straight in HBM (no
+        host copy): the local CSR from the device generator with its neighbour values spread
+        over every rank's rows, bf16 features and class (or multi-label) labels"""
+        on = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+        W, r = (dist.get_world_size(group), dist.get_rank(group)) if on else (1, 0)
+        n_local = max(0, math.ceil((int(num_nodes) - r) / W))
+        loc = DeviceGraph.synthetic(n_local, avg_degree, max_degree, seed=seed * 7919 + r, device=device)
+        if W > 1:
+            v = loc.nbr.long()
+            g = v * W + (v * 40503 + 17 * r) % W  # spread over the owners
+            loc.nbr = torch.where(g < num_nodes, g, g - W).to(torch.int32)
+        gen = torch.Generator(device=loc.device).manual_seed(seed * 31 + r)
+        loc.features = torch.randn(n_local, feature_dim, generator=gen, device=loc.device).to(torch.bfloat16)
+        if multi_label:
+            loc.labels = (torch.rand(n_local, num_classes, generator=gen, device=loc.device) < 0.1).float()
+        else:
+            loc.labels = torch.randint(0, num_classes, (n_local, 1), generator=gen, device=loc.device).float()
+        return cls(loc, int(num_nodes), float(n_local), group=group)
+
+    @classmethod
     def from_engine(cls, engine=None, node_type=-1, features=(), feature_dims=(), label=None, label_dim=None,
                     feature_dtype=torch.bfloat16, seed=0, device="cuda", group=None):
         """this rank's rows of the engine's graph: the node's ranks share ONE host export

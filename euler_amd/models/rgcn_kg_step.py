@@ -33,8 +33,9 @@ scales the self-loop product's rows with it in the backward GEMM's epilogue.
 
 ``deterministic=True`` (or ``EULER_AMD_DETERMINISTIC=1``) makes the step atomic-free and
 bit-reproducible: the scoring backward writes one gradient row per entity / relation
-occurrence, summed per row in a fixed order (stable sort of the occurrence keys +
-``segment_reduce_wave``), and the relation-weight gradient of a relation with several
+occurrence (and its row key; a triple whose margin holds writes none), summed per row in
+occurrence order (``det_occ``: counted CSR whose lists one wave sorts, then
+``det_segment_sum``, one block per row), and the relation-weight gradient of a relation with several
 edge chunks is added from per-chunk slabs in chunk order (``rel_gemm_dw`` slot mode).
 
 No torch elementwise kernel runs in the default step; gradients are zeroed with one memset.  The
@@ -188,9 +189,8 @@ class RgcnTransEStep:
             nocc = self.B * (2 + self.K)
             self.occ_e = torch.empty(nocc, self.D, **f32)
             self.occ_r = torch.empty(self.B, self.D, **f32)
-            self.keys_e = torch.empty(self.B, 2 + self.K, **i64)
-            self.bnd_e = torch.arange(self.N + 1, **i64)
-            self.bnd_r = torch.arange(self.R + 1, **i64)
+            self.key_e = torch.empty(nocc, **i64)
+            self.key_r = torch.empty(self.B, **i64)
             slots = max((lay[2].det_slots()[3] for lay in self.layers), default=0)
             self.dw_part = torch.empty(max(slots, 1), self.D, self.D, **f32)
 
@@ -238,7 +238,7 @@ class RgcnTransEStep:
         dtop = m.ent.grad if L == 0 else self.dh[L - 1]
         if L:
             H.zero_(dtop)
-        occ = (self.occ_e, self.occ_r) if self.deterministic else (None, None)
+        occ = (self.occ_e, self.occ_r, self.key_e, self.key_r) if self.deterministic else (None,) * 4
         H.kg_step(x, m.rel.detach(), self.pool, self.t_src, self.t_dst, self.t_rel, self.opt.step_count, self.seed,
                   gnn_ops.KG_KINDS["l2"], self.normalize, self.margin, self.o_src, self.o_dst, self.o_rel, self.o_neg,
                   self.coef, self.part, self.loss, dtop, m.rel.grad, self.drel_rep, *occ)
@@ -286,18 +286,13 @@ class RgcnTransEStep:
 
     def _occurrence_sums(self, dent, drel):
         """deterministic mode: d h and d rel as fixed-order sums of the scoring kernel's
-        occurrence rows (row-major [h, t, neg_0 .. neg_{K-1}] per triple; one row per triple
-        for the relations)"""
+        occurrence rows (keyed by the kernel: [h, t, neg_0 .. neg_{K-1}] per triple, one
+        relation row per triple, -1 for triples without gradient); each row's occurrences
+        are summed in occurrence order (det_occ: counted CSR, lists sorted in one wave)"""
         H = hip()
-        k = self.keys_e
-        k[:, 0].copy_(self.o_src)
-        k[:, 1].copy_(self.o_dst)
-        k[:, 2:].copy_(self.o_neg)
-        for keys, bnd, occ, out in ((k.view(-1), self.bnd_e, self.occ_e, dent),
-                                    (self.o_rel, self.bnd_r, self.occ_r, drel)):
-            sk, perm = torch.sort(keys, stable=True)
-            ptr = torch.searchsorted(sk, bnd)
-            H.segment_reduce_wave(occ, ptr, perm, 0, out=out)
+        for keys, S, occ, out in ((self.key_e, self.N, self.occ_e, dent), (self.key_r, self.R, self.occ_r, drel)):
+            ptr, perm = H.det_occ(keys, S)
+            H.det_segment_sum(occ, ptr, perm, out)
 
     def keep_masks(self):
         """per-layer [N] keep masks of the last step's self-loop dropout (None without)"""

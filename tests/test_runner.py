@@ -8,8 +8,8 @@ from euler_amd.tools import runner
 MODELS = ["graphsage", "graphsage_unsup", "gcn", "gat", "fastgcn", "adaptivegcn", "agnn", "appnp", "arma", "dna",
           "sgcn", "tagcn", "geniepath", "lgcn", "deepwalk", "node2vec", "line", "dgi", "gae", "vgae", "rgcn",
           "transe", "transh", "transr", "transd", "distmult", "gin", "gated_graph", "graphgcn", "set2set",
-          "solution"]
-SCALE = {"cora": 0.04, "fb15k": 0.004, "wn18": 0.003, "mutag": 0.1}
+          "solution", "scalable_sage", "scalable_gcn"]
+SCALE = {"cora": 0.04, "fb15k": 0.004, "wn18": 0.003, "mutag": 0.1, "ppi": 0.02}
 
 
 @pytest.fixture(scope="module")

@@ -1,0 +1,6 @@
+R=$GRAFT_REPO_ROOT/gpurun_out/r44
+mkdir -p $R
+timeout -k 10 600 python -u -m pytest -v --timeout 120 --timeout-method thread -m gpu tests/test_full_trainer.py > $R/pytest.log 2>&1
+rc=$?
+grep -E "PASSED|FAILED|ERROR" $R/pytest.log | tail -25
+exit $rc

@@ -2,7 +2,7 @@ set -o pipefail
 # deterministic KG backward: tests, step time atomic vs deterministic, kernel stats
 O=gpurun_out/r6_b4; mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_kg_step.py tests/test_graph_memset.py -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1; echo "tests rc=$?" >> $O/summary.txt
+timeout -k 10 600 python -u -m pytest tests/test_kg_step.py tests/test_graph_memset.py tests/test_sharded_graph.py -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1; echo "tests rc=$?" >> $O/summary.txt
 timeout -k 10 300 python benchmarks/bench_kg.py --steps 400 --warmup 20 --eval-after 0 > $O/kg_atomic.log 2>&1; echo "kg atomic rc=$?" >> $O/summary.txt
 timeout -k 10 300 python benchmarks/bench_kg.py --steps 400 --warmup 20 --eval-after 0 --deterministic > $O/kg_det.log 2>&1; echo "kg det rc=$?" >> $O/summary.txt
 timeout -k 10 300 python benchmarks/bench_kg.py --steps 400 --warmup 20 --eval-after 0 > $O/kg_atomic2.log 2>&1; echo "kg atomic2 rc=$?" >> $O/summary.txt
