@@ -8,7 +8,22 @@
 #include <numeric>
 #include <thread>
 
+#include <chrono>
+
 namespace euler {
+
+namespace {
+// load-phase timing (EULER_LOG_LEVEL=info): where a large on-disk load spends its time
+struct LoadTimer {
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void Mark(const char* phase) {
+    const auto now = std::chrono::steady_clock::now();
+    EULER_LOG(Info) << "graph load: " << phase << " " << std::chrono::duration<double>(now - t).count() << " s";
+    t = now;
+  }
+};
+}  // namespace
+
 
 // ============================================================================ GraphMeta
 Status GraphMeta::Load(const std::string& path) {
@@ -414,11 +429,20 @@ void GraphBuilder::AddAdj(bool out, uint64_t node, int32_t etype, uint64_t nbr, 
 }
 
 void GraphBuilder::AddEdge(uint64_t src, uint64_t dst, int32_t type, float weight) {
-  edge_key_rows_[EdgeIdHash(src, dst, type)] = static_cast<int64_t>(edges_.size());
   edges_.push_back({src, dst, type, weight});
 }
 
 int64_t GraphBuilder::EdgeKeyRow(uint64_t src, uint64_t dst, int32_t t) {
+  // the (src, dst, type) -> row map is only needed when edge features arrive by key (the
+  // API builder); the on-disk loader attaches them by row and never pays for it.  Edges
+  // added since the last lookup are indexed in insertion order (a later duplicate wins).
+  if (keyed_upto_ < edges_.size()) {
+    edge_key_rows_.reserve(edges_.size());
+    for (; keyed_upto_ < edges_.size(); ++keyed_upto_) {
+      const EdgeRec& e = edges_[keyed_upto_];
+      edge_key_rows_[EdgeIdHash(e.src, e.dst, e.type)] = static_cast<int64_t>(keyed_upto_);
+    }
+  }
   auto it = edge_key_rows_.find(EdgeIdHash(src, dst, t));
   return it == edge_key_rows_.end() ? -1 : it->second;
 }
@@ -595,6 +619,7 @@ Status GraphBuilder::LoadReferenceFormat(const std::string& dir, int shard_idx, 
     Status st;
   };
   std::vector<Out> outs(tasks.size());
+  LoadTimer lt;
   {
     ThreadPool pool(std::max(1, std::min<int>(threads, static_cast<int>(tasks.size()))));
     Latch done(static_cast<int64_t>(tasks.size()));
@@ -614,6 +639,19 @@ Status GraphBuilder::LoadReferenceFormat(const std::string& dir, int shard_idx, 
     }
     done.Wait();
   }
+  lt.Mark("parse files (parallel)");
+  {  // one allocation per builder array for the merge below
+    size_t nn = 0, nao = 0, nai = 0, ne = 0, nnd = 0, nns = 0, nnb = 0, ned = 0, nes = 0, neb = 0;
+    for (const Out& o : outs) {
+      nn += o.nodes.size(), nao += o.ao.size(), nai += o.ai.size(), ne += o.edges.size();
+      nnd += o.nd.size(), nns += o.ns.size(), nnb += o.nb.size();
+      ned += o.ed.size(), nes += o.es.size(), neb += o.eb.size();
+    }
+    nodes_.reserve(nodes_.size() + nn), adj_out_.reserve(adj_out_.size() + nao), adj_in_.reserve(adj_in_.size() + nai);
+    edges_.reserve(edges_.size() + ne);
+    nd_.reserve(nd_.size() + nnd), ns_.reserve(ns_.size() + nns), nb_.reserve(nb_.size() + nnb);
+    ed_.reserve(ed_.size() + ned), es_.reserve(es_.size() + nes), eb_.reserve(eb_.size() + neb);
+  }
   for (size_t i = 0; i < outs.size(); ++i) {
     Out& o = outs[i];
     if (!o.st.ok()) return Status(o.st.code(), tasks[i].path + ": " + o.st.message());
@@ -629,7 +667,9 @@ Status GraphBuilder::LoadReferenceFormat(const std::string& dir, int shard_idx, 
     for (auto& x : o.ed) ed_.push_back({x.key + base, x.idx, std::move(x.v)});
     for (auto& x : o.es) es_.push_back({x.key + base, x.idx, std::move(x.v)});
     for (auto& x : o.eb) eb_.push_back({x.key + base, x.idx, std::move(x.v)});
+    o = Out();  // release this file's records
   }
+  lt.Mark("merge parsed records");
   return Status::OK();
 }
 
@@ -732,6 +772,7 @@ void BuildAdjacency(std::vector<std::pair<int64_t, std::pair<int32_t, std::pair<
 
 std::unique_ptr<Graph> GraphBuilder::Finish() {
   std::unique_ptr<Graph> g(new Graph);
+  LoadTimer lt;
   g->meta_ = meta_;
   g->shard_idx_ = shard_idx_;
   g->shard_num_ = shard_num_;
@@ -755,6 +796,7 @@ std::unique_ptr<Graph> GraphBuilder::Finish() {
     max_nt = std::max(max_nt, uniq[i].type + 1);
   }
   g->id_map_.Build(g->node_ids_);
+  lt.Mark("nodes sorted + id map");
   for (auto& e : edges_) max_et = std::max(max_et, e.type + 1);
   for (auto& e : adj_out_) max_et = std::max(max_et, e.type + 1);
   for (auto& e : adj_in_) max_et = std::max(max_et, e.type + 1);
@@ -765,6 +807,7 @@ std::unique_ptr<Graph> GraphBuilder::Finish() {
   using Entry = std::pair<int64_t, std::pair<int32_t, std::pair<uint64_t, float>>>;
   for (int dir = 0; dir < 2; ++dir) {
     std::vector<Entry> entries;
+    entries.reserve(have_adj_ ? (dir == 0 ? adj_out_.size() : adj_in_.size()) : edges_.size());
     if (have_adj_) {
       for (auto& a : (dir == 0 ? adj_out_ : adj_in_)) {
         const int64_t r = g->Row(a.node);
@@ -781,6 +824,7 @@ std::unique_ptr<Graph> GraphBuilder::Finish() {
       }
     }
     BuildAdjacency(entries, N, T, dir == 0 ? &g->out_ : &g->in_);
+    lt.Mark(dir == 0 ? "out adjacency" : "in adjacency");
   }
   // ---- edges (this shard owns edges whose src row is local, or all when no node filter)
   const int64_t E = static_cast<int64_t>(edges_.size());
@@ -795,6 +839,7 @@ std::unique_ptr<Graph> GraphBuilder::Finish() {
     g->edge_weight_[e] = edges_[e].w;
   }
   g->BuildEdgeIndex();
+  lt.Mark("edge table + index");
   // ---- features
   auto node_row = [&](uint64_t id) { return g->Row(id); };
   auto edge_row = [&](uint64_t key) { return static_cast<int64_t>(key) < E ? static_cast<int64_t>(key) : -1; };
@@ -812,15 +857,18 @@ std::unique_ptr<Graph> GraphBuilder::Finish() {
     c.offsets.clear();
     c.values = std::move(dense_cols_[idx].first);
   }
+  lt.Mark("feature columns");
   g->meta_.node_count = N;
   g->meta_.edge_count = E;
   g->BuildSamplers(node_sampler_on_, edge_sampler_on_);
+  lt.Mark("samplers");
   // release builder memory
   nodes_.clear();
   adj_out_.clear();
   adj_in_.clear();
   edges_.clear();
   edge_key_rows_.clear();
+  keyed_upto_ = 0;
   nd_.clear(); ns_.clear(); nb_.clear(); ed_.clear(); es_.clear(); eb_.clear();
   return g;
 }

@@ -370,6 +370,7 @@ class GraphBuilder {
   std::vector<AdjRec> adj_out_, adj_in_;
   std::vector<EdgeRec> edges_;
   std::unordered_map<uint64_t, int64_t> edge_key_rows_;  // hash -> index into edges_ (builder only)
+  size_t keyed_upto_ = 0;  // edges_[0 .. keyed_upto_) are in edge_key_rows_ (built on first lookup)
   std::vector<FeatRec<float>> nd_, ed_;
   std::vector<FeatRec<uint64_t>> ns_, es_;
   std::vector<FeatRec<char>> nb_, eb_;

@@ -338,3 +338,34 @@ def test_sharded_sage_trainer_gpu_matches_bf16_oracle():
         sg.check_overflow()
     finally:
         dist.destroy_process_group()
+
+
+def _worker_synth(rank, world, port, q):
+    try:
+        _init(rank, world, port)
+        from euler_amd.graph.sharded_graph import ShardedDeviceGraph
+
+        N = 1001
+        g = ShardedDeviceGraph.synthetic(N, 6.0, 64, feature_dim=16, num_classes=5, seed=2, device="cpu")
+        loc = g.local
+        ok = loc.num_rows == len(range(rank, N, world)) and int(loc.nbr.min()) >= 0 and int(loc.nbr.max()) < N
+        ok &= tuple(loc.features.shape) == (loc.num_rows, 16) and loc.labels.shape[0] == loc.num_rows
+        # neighbour values reach every owner
+        owners = set((loc.nbr.long() % world).unique().tolist())
+        ok &= owners == set(range(world))
+        g.advance()
+        g.reseed_cpu()
+        nb = g.sample_neighbor(g.sample_node(64).long(), 4)
+        ok &= bool((nb >= 0).all()) and int(nb.max()) < N
+        q.put((rank, "synth", bool(ok)))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_sharded_synthetic_graph_two_ranks():
+    res = _run(_worker_synth)
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == 2 and all(r[2] for r in res), res
