@@ -310,32 +310,63 @@ const std::vector<int64_t>& Graph::NodeRowsOfType(int t) const {
   return node_rows_by_type_[t];
 }
 
+// The (src, dst, type) -> row index is an open-addressing table split into 2^edge_pbits_
+// partitions by the key's top bits; each partition probes within its own slots.  Every
+// partition is built by one thread scanning the edges in order, so the build is parallel
+// and still deterministic (a duplicate key keeps the probe position it would get serially).
 int64_t Graph::EdgeRow(uint64_t src, uint64_t dst, int32_t type) const {
   if (edge_slots_.empty()) return -1;
   const uint64_t key = EdgeIdHash(src, dst, type);
-  const uint64_t cap = edge_slots_.size();
-  uint64_t h = key & (cap - 1);
+  const uint64_t capP = edge_slots_.size() >> edge_pbits_;
+  const uint64_t base = edge_pbits_ ? (key >> (64 - edge_pbits_)) * capP : 0;
+  uint64_t h = key & (capP - 1);
   for (;;) {
-    const int64_t r = edge_slots_[h];
+    const int64_t r = edge_slots_[base + h];
     if (r < 0) return -1;
-    if (edge_keys_[h] == key && edge_src_[r] == src && edge_dst_[r] == dst && edge_type_[r] == type) return r;
-    h = (h + 1) & (cap - 1);
+    if (edge_keys_[base + h] == key && edge_src_[r] == src && edge_dst_[r] == dst && edge_type_[r] == type) return r;
+    h = (h + 1) & (capP - 1);
   }
 }
 
 void Graph::BuildEdgeIndex() {
   const uint64_t n = edge_src_.size();
-  uint64_t cap = 16;
-  while (cap < n * 2) cap <<= 1;
-  edge_keys_.assign(cap, 0);
-  edge_slots_.assign(cap, -1);
-  for (uint64_t e = 0; e < n; ++e) {
-    const uint64_t key = EdgeIdHash(edge_src_[e], edge_dst_[e], edge_type_[e]);
-    uint64_t h = key & (cap - 1);
-    while (edge_slots_[h] >= 0) h = (h + 1) & (cap - 1);
-    edge_keys_[h] = key;
-    edge_slots_[h] = static_cast<int64_t>(e);
+  edge_pbits_ = n >= (uint64_t{1} << 20) ? 6 : 0;  // 64 partitions for large edge tables
+  const uint64_t P = uint64_t{1} << edge_pbits_;
+  std::vector<uint64_t> keys(n);
+  auto* pool = ThreadPool::Default();
+  pool->ParallelFor(static_cast<int64_t>(n), 1 << 16, [&](int64_t b, int64_t e) {
+    for (int64_t i = b; i < e; ++i) keys[i] = EdgeIdHash(edge_src_[i], edge_dst_[i], edge_type_[i]);
+  });
+  auto part = [&](uint64_t key) { return edge_pbits_ ? key >> (64 - edge_pbits_) : 0; };
+  std::vector<uint64_t> cnt(P, 0);
+  for (uint64_t i = 0; i < n; ++i) ++cnt[part(keys[i])];
+  uint64_t mx = 1;
+  for (uint64_t c : cnt) mx = std::max(mx, c);
+  uint64_t capP = 16;
+  while (capP < mx * 2) capP <<= 1;  // every partition at most half full
+  edge_keys_.assign(capP * P, 0);
+  edge_slots_.assign(capP * P, -1);
+  // edges bucketed by partition, in edge order (counting sort)
+  std::vector<uint64_t> off(P + 1, 0);
+  for (uint64_t p = 0; p < P; ++p) off[p + 1] = off[p] + cnt[p];
+  std::vector<uint64_t> order(n);
+  {
+    std::vector<uint64_t> cur(off.begin(), off.end() - 1);
+    for (uint64_t i = 0; i < n; ++i) order[cur[part(keys[i])]++] = i;
   }
+  pool->ParallelFor(static_cast<int64_t>(P), 1, [&](int64_t b, int64_t e) {
+    for (int64_t p = b; p < e; ++p) {
+      const uint64_t base = static_cast<uint64_t>(p) * capP;
+      for (uint64_t j = off[p]; j < off[p + 1]; ++j) {
+        const uint64_t i = order[j];
+        const uint64_t key = keys[i];
+        uint64_t h = key & (capP - 1);
+        while (edge_slots_[base + h] >= 0) h = (h + 1) & (capP - 1);
+        edge_keys_[base + h] = key;
+        edge_slots_[base + h] = static_cast<int64_t>(i);
+      }
+    }
+  });
 }
 
 Status LoadOptions::Parse(const std::string& data, const std::string& sampler, LoadOptions* o) {

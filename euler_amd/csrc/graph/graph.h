@@ -237,6 +237,7 @@ class Graph {
   // edge lookup: open addressing on EdgeIdHash
   std::vector<uint64_t> edge_keys_;
   std::vector<int64_t> edge_slots_;
+  int edge_pbits_ = 0;  // log2 of the edge index's partitions (BuildEdgeIndex)
   // samplers
   std::vector<std::vector<int64_t>> node_rows_by_type_;
   std::vector<AliasTable> node_sampler_;  // per type; index num_node_types_ = all

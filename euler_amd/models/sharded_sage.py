@@ -48,8 +48,13 @@ class ShardedSageTrainer(SageTrainer):
         kw.pop("features", None)
         kw.pop("labels", None)
         kw.pop("feature_shard", None)
-        super().__init__(loc, batch_size, fanouts, dims, label_dim, labels=dummy,
-                         feature_shard=graph.padded_features(16), feature_dim=graph.features.dim, **kw)
+        if graph.comm:
+            fs = dict(feature_shard=graph.padded_features(16), feature_dim=graph.features.dim)
+        else:
+            # one rank without collectives: global rows are local rows, the forward gathers
+            # from the table itself (no exchange, no dedup pass)
+            fs = dict(features=loc.features)
+        super().__init__(loc, batch_size, fanouts, dims, label_dim, labels=dummy, **fs, **kw)
         self.pipelined = False
         if self.on_gpu:
             self.roots.copy_(torch.arange(self.B, dtype=torch.int32, device=self.device))
@@ -156,9 +161,12 @@ class ShardedSageTrainer(SageTrainer):
         P = self._cpu_params
         for t in P.values():
             t.grad = None
-        pos = self.fshard.exchange(torch.cat([nodes, leaf.reshape(-1)])).long()
-        nodes_p, leaf_p = pos[: nodes.numel()], pos[nodes.numel():].view_as(leaf)
-        logits = self.logical_forward(P, roots, nodes_p, leaf_p, self.fshard.cache)
+        if self.fshard is not None:
+            pos = self.fshard.exchange(torch.cat([nodes, leaf.reshape(-1)])).long()
+            nodes_p, leaf_p = pos[: nodes.numel()], pos[nodes.numel():].view_as(leaf)
+            logits = self.logical_forward(P, roots, nodes_p, leaf_p, self.fshard.cache)
+        else:
+            logits = self.logical_forward(P, roots, nodes, leaf)
         if self._class_labels:
             yy = torch.zeros((roots.numel(), self.C), dtype=torch.float32)
             yy.scatter_(1, y.long().view(-1, 1), 1.0)

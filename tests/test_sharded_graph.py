@@ -246,7 +246,7 @@ def test_one_rank_sharded_sage_trainer_equals_sage_trainer_cpu():
     loc = sg.local
     kw = dict(metapath=[[0, 1], [1]], init_seed=3, learning_rate=0.01)
     a = ShardedSageTrainer(sg, 32, [4, 3], [16, 16, 8], 5, **kw)
-    assert a.D == 12 and a.fshard.shard.shape[1] == 16
+    assert a.D == 12 and a.fshard is None  # one rank: the forward reads the table itself
     b = SageTrainer(loc, 32, [4, 3], [16, 16, 8], 5, features=loc.features, labels=loc.labels, **kw)
     r0 = loc.rng.clone()
     la = [float(a.step()) for _ in range(5)]
