@@ -46,43 +46,62 @@ def _export_local(eng, names, dims, label, label_dim):
 
 def shared_export(fn):
     """``(arrays, done)``: ``fn()``'s arrays, computed ONCE per node when several data-
-    parallel ranks share it (torch.distributed initialised, LOCAL_WORLD_SIZE > 1): local
-    rank 0 writes them as .npy files under /dev/shm, every local rank maps them read-only
-    (``numpy.load(mmap_mode="r")``: one physical copy in the page cache, no per-rank host
-    copy).  ``done()`` synchronises the ranks and removes the files.  Without peers it is
-    ``fn()`` and a no-op."""
+    parallel ranks share it (torch.distributed initialised, more than one rank on this
+    host): the host's lowest global rank writes them as .npy files under /dev/shm, every
+    rank of the host maps them read-only (``numpy.load(mmap_mode="r")``: one physical copy
+    in the page cache, no per-rank host copy).  ``done()`` synchronises the ranks and
+    removes the files.  Without peers it is ``fn()`` and a no-op.  The host's ranks are
+    found by host name (not LOCAL_RANK, which launchers that share one GPU between ranks
+    may set alike); a failing export is reported to every rank instead of leaving them in
+    a barrier."""
     import os
     import shutil
+    import socket
 
     import torch.distributed as dist
 
     on = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
-    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", dist.get_world_size() if on else 1))
-    if not on or local_world <= 1 or os.environ.get("EULER_AMD_SHARED_EXPORT", "1") == "0":
+    if not on or os.environ.get("EULER_AMD_SHARED_EXPORT", "1") == "0":
         return fn(), (lambda: None)
-    local_rank = int(os.environ.get("LOCAL_RANK", dist.get_rank()))
-    name = ["/dev/shm/euler_amd_export_%d_%d" % (os.getpid(), int(time.time() * 1e3))] if dist.get_rank() == 0 \
-        else [None]
-    dist.broadcast_object_list(name, src=0)
-    d = name[0]
-    if local_rank == 0:
-        arrays = fn()
-        os.makedirs(d, exist_ok=True)
-        for k, v in arrays.items():
-            np.save(os.path.join(d, k + ".tmp.npy"), np.asarray(v))
-            os.replace(os.path.join(d, k + ".tmp.npy"), os.path.join(d, k + ".npy"))
-        keys = sorted(arrays)
-        del arrays
-        with open(os.path.join(d, "KEYS"), "w") as f:
-            f.write("\n".join(keys))
-    dist.barrier()
+    me = dist.get_rank()
+    hosts = [None] * dist.get_world_size()
+    dist.all_gather_object(hosts, socket.gethostname())
+    peers = [r for r, h in enumerate(hosts) if h == hosts[me]]
+    if len(peers) <= 1:
+        return fn(), (lambda: None)
+    leader = min(peers)
+    # one directory per host leader (every rank learns every leader's choice)
+    name = "/dev/shm/euler_amd_export_%d_%d" % (os.getpid(), int(time.time() * 1e3)) if me == leader else None
+    names = [None] * dist.get_world_size()
+    dist.all_gather_object(names, name)
+    d = names[leader]
+    err = None
+    if me == leader:
+        try:
+            arrays = fn()
+            os.makedirs(d, exist_ok=True)
+            for k, v in arrays.items():
+                np.save(os.path.join(d, k + ".tmp.npy"), np.asarray(v))
+                os.replace(os.path.join(d, k + ".tmp.npy"), os.path.join(d, k + ".npy"))
+            keys = sorted(arrays)
+            del arrays
+            with open(os.path.join(d, "KEYS"), "w") as f:
+                f.write("\n".join(keys))
+        except Exception as e:  # reported to the host's ranks below
+            err = "%s: %s" % (type(e).__name__, e)
+    errs = [None] * dist.get_world_size()
+    dist.all_gather_object(errs, err)
+    if errs[leader] is not None:
+        if me == leader:
+            shutil.rmtree(d, ignore_errors=True)
+        raise RuntimeError("shared graph export on rank %d failed: %s" % (leader, errs[leader]))
     with open(os.path.join(d, "KEYS")) as f:
         keys = [k for k in f.read().split("\n") if k]
     mapped = {k: np.load(os.path.join(d, k + ".npy"), mmap_mode="r", allow_pickle=False) for k in keys}
 
     def done():
         dist.barrier()
-        if local_rank == 0:
+        if me == leader:
             shutil.rmtree(d, ignore_errors=True)
 
     return mapped, done

@@ -984,12 +984,15 @@ def test_scalable_device_path_two_ranks_lockstep(tmp_path, store):
     assert len(res) == 2 and all(r[2] for r in res), res
 
 
-def _worker_shared_export(rank, world, port, q, data_dir):
-    """DeviceGraph.from_engine(share=True) on 2 ranks of one node: only local rank 0 runs
-    the engine export; both ranks build the same graph as an unshared upload; the shared
-    files are gone afterwards"""
+def _worker_shared_export(rank, world, port, q, data_dir, same_local=False):
+    """DeviceGraph.from_engine(share=True) on 2 ranks of one node: only the host's lowest
+    rank runs the engine export (also when a launcher gives both ranks LOCAL_RANK 0, as
+    the GPU-sharing tests do); both ranks build the same graph as an unshared upload; the
+    shared files are gone afterwards"""
     try:
         _init(rank, world, port)
+        if same_local:
+            os.environ["LOCAL_RANK"] = "0"
         import glob
 
         import euler_amd as ea
@@ -1025,7 +1028,8 @@ def _worker_shared_export(rank, world, port, q, data_dir):
         q.put((rank, "error", traceback.format_exc()))
 
 
-def test_device_graph_shared_export_once_per_node(tmp_path):
-    res = _run(_worker_shared_export, str(tmp_path / "cora"))
+@pytest.mark.parametrize("same_local", [False, True])
+def test_device_graph_shared_export_once_per_node(tmp_path, same_local):
+    res = _run(_worker_shared_export, str(tmp_path / "cora"), same_local)
     assert not [r for r in res if r[1] == "error"], res
     assert len(res) == 2 and all(r[2] for r in res), res
