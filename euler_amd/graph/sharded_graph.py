@@ -91,7 +91,8 @@ class ShardedDeviceGraph:
         self.overflow = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.features = ShardedFeatures(local.features, self.num_rows, group, force_comm) \
             if local.features is not None else None
-        self.labels = ShardedFeatures(local.labels.float(), self.num_rows, group, force_comm) \
+        # labels are fetched for a batch's roots only (few repeats): no dedup pass
+        self.labels = ShardedFeatures(local.labels.float(), self.num_rows, group, force_comm, dedup=False) \
             if local.labels is not None else None
         self.set_root_weight(root_weight)
 

@@ -69,25 +69,30 @@ class ShardedSageTrainer(SageTrainer):
         return [t for t in range(self.sgraph.num_types) if (mask >> t) & 1]
 
     def _draw_tree(self):
-        """(global roots [B], slotted hop-(L-1) rows [M], leaf draws [M, F_L]) across the ranks"""
+        """(global roots [B], slotted hop-(L-1) rows [M], leaf draws [M, F_L]) across the
+        ranks, int32 throughout (the kernels' row type: no conversion passes)"""
         g = self.sgraph
-        roots = g.sample_node(self.B, stream_id=_STREAM0).long()
+        roots = g.sample_node(self.B, stream_id=_STREAM0).int()
         level = roots
         for k in range(1, self.L):
             f, P = self.fanouts[k - 1], 1 << self.logP[k]
             nb = g.sample_neighbor(level, f, self._types(self.masks[k - 1]), -1, stream_id=_STREAM0 + k).view(-1, f)
-            slots = torch.full((level.numel(), P), -1, dtype=torch.long, device=level.device)
-            slots[:, :f] = nb.long()
+            slots = torch.full((level.numel(), P), -1, dtype=torch.int32, device=level.device)
+            slots[:, :f] = nb
             slots[:, f] = level
-            level = slots.reshape(-1)
+            level = slots.view(-1)
         leaf = g.sample_neighbor(level, self.fanouts[-1], self._types(self.masks[-1]), -1,
-                                 stream_id=_STREAM0 + self.L).view(-1, self.fanouts[-1]).long()
+                                 stream_id=_STREAM0 + self.L).view(-1, self.fanouts[-1])
         return roots, level, leaf
 
     def _batch_labels(self, roots):
-        y = self.sgraph.gather_labels(roots)  # [B, C] fp32 (or [B, 1] class ids)
+        g = self.sgraph
+        if g.comm:
+            y = g.gather_labels(roots)  # [B, C] fp32 (or [B, 1] class ids) over the exchange
+        else:
+            y = g.local.labels[roots.long()]  # one rank: global rows are local rows
         if self._class_labels:
-            return y.reshape(-1).round().to(torch.int32)
+            return y.reshape(-1).to(torch.int32)
         return y
 
     def _sample_sharded(self):
@@ -96,13 +101,13 @@ class ShardedSageTrainer(SageTrainer):
         self._global_roots = roots
         self._batch_y = y
         if not self.on_gpu:
-            return roots, level, leaf, y
-        self.nodes.copy_(level.to(torch.int32))
-        self.leaf.copy_(leaf.reshape(-1).to(torch.int32))
+            return roots.long(), level.long(), leaf.long(), y
+        self.nodes.copy_(level)
+        self.leaf.copy_(leaf.reshape(-1))
         if self.label_mode == 2:
-            self.labels[:, : self.C].copy_(y.to(self.labels.dtype))
+            self.labels[:, : self.C].copy_(y)
         else:
-            self.labels.copy_(y.to(self.labels.dtype))
+            self.labels.copy_(y)
         return None
 
     # ------------------------------------------------------------------ GPU step
@@ -150,7 +155,7 @@ class ShardedSageTrainer(SageTrainer):
     def samples(self):
         """(global roots [B], hop rows [M], leaf draws [M, F_L]) of the last step"""
         if self.on_gpu:
-            return (self._global_roots, self.nodes.long(), self.leaf.view(-1, self.fanouts[-1]).long())
+            return (self._global_roots.long(), self.nodes.long(), self.leaf.view(-1, self.fanouts[-1]).long())
         return self._cpu_samples
 
     # ------------------------------------------------------------------ CPU twin
