@@ -35,6 +35,7 @@ import torch.distributed as dist
 from euler_amd.ops import mp_ops
 from euler_amd.ops._native import use_hip
 from euler_amd.ops.gnn_ops import route_by_owner, unique_first_padded
+from euler_amd.parallel import comm
 
 __all__ = ["ShardedFeatures"]
 
@@ -125,10 +126,10 @@ class ShardedFeatures:
             if P:
                 sp = [0 if r == self.rank else C for r in range(W)]
                 recv = torch.empty(P, dtype=torch.long, device=ids.device)
-                dist.all_to_all_single(recv, send[:P], sp, sp, group=self.group)
+                comm.all_to_all_single(recv, send[:P], sp, sp, group=self.group)
                 local = torch.where(recv >= 0, torch.div(recv, W, rounding_mode="floor"), torch.full_like(recv, -1))
                 rows = self._gather(local).to(self.cache.dtype).contiguous()
-                dist.all_to_all_single(self.cache[:P], rows, sp, sp, group=self.group)
+                comm.all_to_all_single(self.cache[:P], rows, sp, sp, group=self.group)
             own = send[P:trash]
             local = torch.where(own >= 0, torch.div(own, W, rounding_mode="floor"), torch.full_like(own, -1))
             self.cache[P:trash].copy_(self._gather(local))

@@ -45,6 +45,7 @@ from euler_amd.graph.sharded_features import ShardedFeatures
 from euler_amd.ops import mp_ops
 from euler_amd.ops._native import hip, use_hip
 from euler_amd.ops.gnn_ops import route_by_owner
+from euler_amd.parallel import comm
 
 __all__ = ["ShardedDeviceGraph", "shard_csr"]
 
@@ -239,7 +240,7 @@ class ShardedDeviceGraph:
         if not self.comm:
             return send.clone()
         recv = torch.empty_like(send)
-        dist.all_to_all_single(recv, send.contiguous(), group=self.group)
+        comm.all_to_all_single(recv, send.contiguous(), group=self.group)
         return recv
 
     def _route(self, keys: torch.Tensor):

@@ -21,6 +21,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from euler_amd.ops import mp_ops
+from euler_amd.parallel import comm
 
 __all__ = ["ShardedEmbedding", "sharded_lookup", "is_sharded", "sharded_param_names", "reshard_rows"]
 
@@ -38,14 +39,14 @@ class _ShardedLookup(torch.autograd.Function):
         sorted_ids = ids[order]
         send_counts = torch.bincount(owner, minlength=W)
         recv_counts = torch.empty_like(send_counts)
-        dist.all_to_all_single(recv_counts, send_counts, group=group)
+        comm.all_to_all_single(recv_counts, send_counts, group=group)
         send_l, recv_l = send_counts.tolist(), recv_counts.tolist()
         recv_ids = torch.empty(sum(recv_l), dtype=ids.dtype, device=ids.device)
-        dist.all_to_all_single(recv_ids, sorted_ids, recv_l, send_l, group=group)
+        comm.all_to_all_single(recv_ids, sorted_ids, recv_l, send_l, group=group)
         local = torch.div(recv_ids, W, rounding_mode="floor")
         rows = mp_ops.gather(weight, local) if weight.is_cuda else weight[local]
         out_sorted = torch.empty(ids.numel(), weight.shape[1], dtype=weight.dtype, device=weight.device)
-        dist.all_to_all_single(out_sorted, rows.contiguous(), send_l, recv_l, group=group)
+        comm.all_to_all_single(out_sorted, rows.contiguous(), send_l, recv_l, group=group)
         out = torch.empty_like(out_sorted)
         out[order] = out_sorted
         ctx.save_for_backward(order, local)
@@ -60,7 +61,7 @@ class _ShardedLookup(torch.autograd.Function):
         send_l, recv_l = ctx.splits
         g_sorted = g[order].contiguous()
         recv_g = torch.empty(sum(recv_l), g.shape[1], dtype=g.dtype, device=g.device)
-        dist.all_to_all_single(recv_g, g_sorted, recv_l, send_l, group=ctx.group)
+        comm.all_to_all_single(recv_g, g_sorted, recv_l, send_l, group=ctx.group)
         gw = torch.zeros(ctx.shape, dtype=g.dtype, device=g.device)
         gw.index_add_(0, local, recv_g)
         return gw, None, None

@@ -17,6 +17,8 @@ import math
 import torch
 import torch.distributed as dist
 
+from euler_amd.parallel import comm
+
 __all__ = ["ShardedRowStore"]
 
 
@@ -46,11 +48,11 @@ class ShardedRowStore:
         order = torch.sort(owner, stable=True)[1]
         send = torch.bincount(owner, minlength=W)
         recv = torch.empty_like(send)
-        dist.all_to_all_single(recv, send, group=self.group)
+        comm.all_to_all_single(recv, send, group=self.group)
         counts = torch.stack([send, recv]).cpu()
         s, r = counts[0].tolist(), counts[1].tolist()
         rid = torch.empty(sum(r), dtype=ids.dtype, device=ids.device)
-        dist.all_to_all_single(rid, ids[order].contiguous(), r, s, group=self.group)
+        comm.all_to_all_single(rid, ids[order].contiguous(), r, s, group=self.group)
         return order, s, r, rid
 
     @torch.no_grad()
@@ -62,7 +64,7 @@ class ShardedRowStore:
         order, s, r, rid = self._route(ids)
         rows = self.local[torch.div(rid, self.world, rounding_mode="floor")]
         back = torch.empty(ids.numel(), self.dim, dtype=rows.dtype, device=rows.device)
-        dist.all_to_all_single(back, rows.contiguous(), s, r, group=self.group)
+        comm.all_to_all_single(back, rows.contiguous(), s, r, group=self.group)
         out = torch.empty_like(back)
         out[order] = back
         return out
@@ -83,7 +85,7 @@ class ShardedRowStore:
             vals = None
             if op != "zero":
                 vals = torch.empty(sum(r), self.dim, dtype=self.local.dtype, device=self.device)
-                dist.all_to_all_single(vals, values[order].contiguous(), r, s, group=self.group)
+                comm.all_to_all_single(vals, values[order].contiguous(), r, s, group=self.group)
         if op == "copy":
             self.local.index_copy_(0, rows, vals)
         elif op == "add":

@@ -47,6 +47,7 @@ import torch.distributed as dist
 from euler_amd.ops import mp_ops
 from euler_amd.ops._native import hip, use_hip
 from euler_amd.ops.gnn_ops import route_by_owner, unique_first
+from euler_amd.parallel import comm
 
 __all__ = ["ShardedTable", "LookupHandle", "StaticHandle"]
 
@@ -175,7 +176,7 @@ class ShardedTable:
             sd = self._buf(bufs, "send", (P,), torch.long, dev)
             sd.copy_(send[:P])
             sp = self._peer_splits(C)
-            dist.all_to_all_single(recv[:P], sd, sp, sp, group=self.group)
+            comm.all_to_all_single(recv[:P], sd, sp, sp, group=self.group)
         recv[P:].copy_(send[P:trash])  # own requests
         local = torch.where(recv >= 0, torch.div(recv, W, rounding_mode="floor"), torch.full_like(recv, -1))
         extra = 1 if trash_row else 0
@@ -185,7 +186,7 @@ class ShardedTable:
         if P:
             xw = self._buf(bufs, "rows_in", (P, self.dim), self.wire, dev)
             self._gather_into(local[:P], xw)
-            dist.all_to_all_single(out[:P], xw, sp, sp, group=self.group)
+            comm.all_to_all_single(out[:P], xw, sp, sp, group=self.group)
         self._gather_into(local[P:], out[P:trash])
         return (out if keep_wire else out.float()), StaticHandle(pos, local)
 
@@ -210,7 +211,7 @@ class ShardedTable:
                 gw = g[:P]
             gr = self._buf(bufs, "grad_out", (trash, self.dim), self.wire, g.device)
             sp = self._peer_splits(C)
-            dist.all_to_all_single(gr[:P], gw, sp, sp, group=self.group)
+            comm.all_to_all_single(gr[:P], gw, sp, sp, group=self.group)
             gr[P:].copy_(g[P:])  # own block
             g = gr
             # several ranks may have asked for the same row: merge (empty slots, local
@@ -253,11 +254,11 @@ class ShardedTable:
         order = torch.sort(key, stable=True)[1]
         send_counts = torch.bincount(owner, minlength=W)
         recv_counts = torch.empty_like(send_counts)
-        dist.all_to_all_single(recv_counts, send_counts, group=self.group)
+        comm.all_to_all_single(recv_counts, send_counts, group=self.group)
         counts = torch.stack([send_counts, recv_counts]).cpu()  # one host sync for both
         send, recv = counts[0].tolist(), counts[1].tolist()
         recv_ids = torch.empty(sum(recv), dtype=ids.dtype, device=ids.device)
-        dist.all_to_all_single(recv_ids, ids[order].contiguous(), recv, send, group=self.group)
+        comm.all_to_all_single(recv_ids, ids[order].contiguous(), recv, send, group=self.group)
         local = torch.div(recv_ids, W, rounding_mode="floor")
         out_sorted = self._a2a_rows(self._gather(local), send, recv)
         if sorted_out:
@@ -293,7 +294,7 @@ class ShardedTable:
         out = self._buf(bufs, tag + "out", (n + extra, self.dim), self.wire, xw.device)
         if extra:
             out[n:].zero_()
-        dist.all_to_all_single(out[:n], xw, out_splits, in_splits, group=self.group)
+        comm.all_to_all_single(out[:n], xw, out_splits, in_splits, group=self.group)
         return out if keep_wire else out.float()
 
     def _gather_into(self, local, out):

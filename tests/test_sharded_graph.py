@@ -369,3 +369,52 @@ def test_sharded_synthetic_graph_two_ranks():
     res = _run(_worker_synth)
     assert not [r for r in res if r[1] == "error"], res
     assert len(res) == 2 and all(r[2] for r in res), res
+
+
+def _worker_shared_gpu(rank, world, port, q):
+    """one rank of a 2-process sharded-graph SAGE job sharing the box's GPU (gloo; the
+    all-to-alls staged through host memory, parallel/comm.py): each rank holds half of a
+    synthetic graph in HBM, draws trees across both, trains the fused step in lockstep"""
+    try:
+        os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                           "WORLD_SIZE": str(world), "LOCAL_RANK": "0"})
+        from euler_amd.graph.sharded_graph import ShardedDeviceGraph
+        from euler_amd.models.sharded_sage import ShardedSageTrainer
+        from euler_amd.parallel import dp
+
+        dp.init_distributed(backend="gloo", device=torch.device("cuda", 0))
+        N = 200_000
+        g = ShardedDeviceGraph.synthetic(N, 10.0, 256, feature_dim=64, num_classes=16, seed=5, device="cuda")
+        tr = ShardedSageTrainer(g, 256, [10, 5], [64, 64, 32], 16, learning_rate=0.01, init_seed=0)
+
+        def sync(buf):
+            host = buf.detach().cpu()
+            dist.all_reduce(host)
+            buf.copy_(host)
+            return 1.0 / world
+
+        losses = []
+        for _ in range(30):
+            tr.step(sync)
+            losses.append(float(tr.loss.item()))
+        roots, nodes, leaf = tr.samples()
+        ok = bool(((roots >= 0) & (roots < N)).all()) and int(leaf.max()) < N
+        flat = tr.flat.detach().cpu().clone()
+        allp = [torch.zeros_like(flat) for _ in range(world)]
+        dist.all_gather(allp, flat)
+        same = all(torch.equal(x, allp[0]) for x in allp)
+        g.check_overflow()
+        ok &= same and all(math.isfinite(v) for v in losses) and g.local.num_rows == N // world
+        q.put((rank, "shared_gpu", bool(ok), losses[0], losses[-1]))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+
+
+@pytest.mark.gpu
+def test_sharded_sage_two_ranks_share_the_gpu_in_lockstep():
+    res = _run(_worker_shared_gpu)
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == 2 and all(r[2] for r in res), res
