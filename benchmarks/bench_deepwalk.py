@@ -84,6 +84,9 @@ def link_prediction_eval(args, dev):
 def main(argv=None):
     p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     p.add_argument("--gpus", type=int, default=None, help="ranks, one per GPU (default: WORLD_SIZE or 1)")
+    p.add_argument("--shared-gpu", action="store_true",
+                   help="rehearsal: every rank on GPU 0 over gloo (the all-to-alls staged through host memory, "
+                        "eager steps); RCCL needs one GPU per rank")
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--num-nodes", type=int, default=100_000_000)
@@ -118,13 +121,21 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    require_gpu(local_rank, world, "bench_deepwalk.py")
-    dev = torch.device("cuda", local_rank)
+    if args.shared_gpu:
+        dev = torch.device("cuda", 0)
+        if args.mode == "graph":
+            args.mode = "static"  # gloo collectives are not capturable: the same static step, eager
+    else:
+        require_gpu(local_rank, world, "bench_deepwalk.py (or --shared-gpu)")
+        dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
     dist_on = world > 1 or args.force_dist
     if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if args.shared_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from euler_amd.graph.device_graph import DeviceGraph
     from euler_amd.models.deepwalk_step import DeepWalkTrainer
@@ -183,8 +194,9 @@ def main(argv=None):
             "metric": "train pairs/sec (whole node), DeepWalk 128-d skip-gram on 100M-node synthetic graph",
             "value": round(pairs / el, 1),
             "unit": "pairs/s",
-            "n_gpus": world,
+            "n_gpus": 1 if args.shared_gpu else world,
             "ranks": world,
+            "shared_gpu_rehearsal": bool(args.shared_gpu) or None,
             "parallelism": f"dp{world}+sharded-emb",
             "steps": args.steps,
             "warmup": args.warmup,

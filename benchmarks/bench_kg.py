@@ -95,6 +95,9 @@ def main(argv=None):
                    help="1: the fused step (models/rgcn_kg_step.py: hand-written launches only, Philox draws in the "
                         "scoring kernel) where it applies; 0: the autograd step (torch.randint draws)")
     p.add_argument("--device", default="cuda", help="cpu: torch reference ops (exploration only, eager)")
+    p.add_argument("--shared-gpu", action="store_true",
+                   help="rehearsal: every rank on GPU 0 over gloo (gradients through host memory, eager steps); "
+                        "RCCL needs one GPU per rank")
     p.add_argument("--eval-after", type=int, default=2000,
                    help="keep training (untimed) to this many steps, then rank the held-out triples")
     args = p.parse_args(argv)
@@ -109,13 +112,17 @@ def main(argv=None):
     if args.device == "cpu":
         dev = torch.device("cpu")
         args.no_graph = True
+    elif args.shared_gpu:
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        args.no_graph = True  # gloo collectives are not capturable
     else:
-        require_gpu(local_rank, world, "bench_kg.py (or --device cpu)")
+        require_gpu(local_rank, world, "bench_kg.py (or --device cpu, or --shared-gpu)")
         dev = torch.device("cuda", local_rank)
         torch.cuda.set_device(dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if dev.type == "cuda":
+        if dev.type == "cuda" and not args.shared_gpu:
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
@@ -313,8 +320,9 @@ def main(argv=None):
             "metric": f"train triples/sec (whole node), R-GCN ({args.layers} layer(s)) + TransE on FB15k-shaped KG",
             "value": round(args.batch * world * args.steps / el, 1),
             "unit": "triples/s",
-            "n_gpus": world,
+            "n_gpus": 1 if args.shared_gpu else world,
             "ranks": world,
+            "shared_gpu_rehearsal": bool(args.shared_gpu) or None,
             "parallelism": f"dp{world}",
             "steps": args.steps,
             "warmup": args.warmup,

@@ -43,6 +43,9 @@ def main(argv=None):
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--graph", action="store_true", help="capture the step (sampling exchanges included) in a hipGraph")
+    p.add_argument("--shared-gpu", action="store_true",
+                   help="rehearsal: every rank on GPU 0 over gloo (exchanges and gradients through host memory, "
+                        "eager steps); RCCL needs one GPU per rank")
     args = p.parse_args(argv)
     from euler_amd.parallel.launch import LAUNCHED_ENV, require_gpu, spawn_local
 
@@ -57,10 +60,14 @@ def main(argv=None):
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    require_gpu(local, world, "bench_sharded_sage")
-    dev = torch.device("cuda", local)
+    if args.shared_gpu:
+        dev = torch.device("cuda", 0)
+        args.graph = False
+    else:
+        require_gpu(local, world, "bench_sharded_sage (or --shared-gpu)")
+        dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    dp.init_distributed(backend="nccl", device=dev)
+    dp.init_distributed(backend="gloo" if args.shared_gpu else "nccl", device=dev)
     rank = dp.rank()
     t0 = time.time()
     g = ShardedDeviceGraph.synthetic(args.num_nodes, args.avg_degree, feature_dim=args.feature_dim,
@@ -70,7 +77,12 @@ def main(argv=None):
     sync = None
     if world > 1:
         def sync(buf):
-            dist.all_reduce(buf)
+            if args.shared_gpu:  # gloo: through host memory
+                host = buf.cpu()
+                dist.all_reduce(host)
+                buf.copy_(host)
+            else:
+                dist.all_reduce(buf)
             return 1.0 / world
     torch.cuda.synchronize()
     build_s = time.time() - t0
@@ -101,7 +113,9 @@ def main(argv=None):
     if rank == 0:
         print(json.dumps({
             "metric": "GraphSAGE train samples/s on a row-sharded graph (whole job)",
-            "value": round(args.batch * world * args.steps / el, 1), "unit": "samples/s", "n_gpus": world,
+            "value": round(args.batch * world * args.steps / el, 1), "unit": "samples/s",
+            "n_gpus": 1 if args.shared_gpu else world, "ranks": world,
+            "shared_gpu_rehearsal": bool(args.shared_gpu) or None,
             "ms_per_step": round(el * 1e3 / args.steps, 3), "steps": args.steps, "warmup": args.warmup,
             "loss": float(tr.loss.item()), "hipgraph": bool(args.graph), "build_s": round(build_s, 1),
             "graph_gib_per_gpu": round((g.nbytes() + g.features.shard.numel() * 2) / 2 ** 30, 2),
