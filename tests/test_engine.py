@@ -368,3 +368,4 @@ def test_engine_save_round_trips_the_on_disk_format(tmp_path):
     o1, o2 = np.lexsort((d1, s1)), np.lexsort((d2, s2))
     assert np.array_equal(np.asarray(s1)[o1], np.asarray(s2)[o2]) and np.array_equal(np.asarray(d1)[o1],
                                                                                        np.asarray(d2)[o2])
+
