@@ -274,7 +274,7 @@ class ShardedDeviceGraph:
         else:
             loc = torch.full((self.world * C,), -1, dtype=torch.long, device=self.device)
         glob = torch.where((recv >= 0) & (loc >= 0), loc * self.world + self.rank, torch.full_like(loc, -1))
-        return self._back(glob, pos, -1).int()
+        return self._back(glob.int(), pos, -1)
 
     def _alias(self, prob, alias, count, stream_id):
         if use_hip(prob):
@@ -296,9 +296,10 @@ class ShardedDeviceGraph:
         pos, recv, C = self._route(torch.where(ok, rows, torch.full_like(rows, -1)))
         local = self._local_rows(recv)
         nb, w, t = self.local.sample_neighbor(local, F, edge_types, -1, stream_id, True)
-        nb = nb.view(-1, F).long()
+        nb = nb.view(-1, F).int()  # global rows < 2^31: int32 halves the return all-to-all
         out_nb = self._back(nb, pos, -1)
-        out_nb = torch.where(out_nb >= 0, out_nb, torch.full_like(out_nb, int(default))).int()
+        if int(default) != -1:
+            out_nb = torch.where(out_nb >= 0, out_nb, torch.full_like(out_nb, int(default)))
         if not with_weights:
             return out_nb
         return out_nb, self._back(w.view(-1, F).float(), pos, 0.0), self._back(t.view(-1, F).int(), pos, -1)
