@@ -89,7 +89,12 @@ def upload(args):
     dp.init_distributed(backend="gloo", device=dev)  # shared-GPU rehearsal: every rank on cuda:0
     before_load = _status()
     t0 = time.time()
-    ea.initialize_embedded_graph(args.data)
+    if args.engine_shards:  # this rank's partitions only (p % W == rank)
+        from euler_amd.ops.base import initialize_graph
+
+        initialize_graph({"mode": "local", "data_path": args.data, "shard_idx": rank, "shard_num": world})
+    else:
+        ea.initialize_embedded_graph(args.data)
     load_s = time.time() - t0
     after_load = _status()
     if world > 1:
@@ -99,9 +104,15 @@ def upload(args):
         base_hbm = torch.cuda.memory_allocated(dev)
     pk = _Peak()
     t1 = time.time()
-    g = DeviceGraph.from_engine(features=["feature"], feature_dims=[args.feature_dim], label="label",
-                                label_dim=args.label_dim, feature_dtype=torch.bfloat16, seed=1, device=dev,
-                                share=world > 1)
+    kw = dict(features=["feature"], feature_dims=[args.feature_dim], label="label", label_dim=args.label_dim,
+              feature_dtype=torch.bfloat16, seed=1, device=dev)
+    if args.engine_shards:
+        from euler_amd.graph.sharded_graph import ShardedDeviceGraph
+
+        sg = ShardedDeviceGraph.from_engine_shard(**kw)
+        g = sg.local
+    else:
+        g = DeviceGraph.from_engine(share=world > 1, **kw)
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     up_s = time.time() - t1
@@ -114,7 +125,8 @@ def upload(args):
         "upload_private_peak_gib": round(peak["RssAnon"] - after_load["RssAnon"], 2),
         "upload_shared_mapped_peak_gib": round(peak.get("RssShmem", 0.0) - after_load.get("RssShmem", 0.0), 2),
         "hbm_peak_gib": round(hbm, 2), "graph_hbm_gib": round((g.nbytes() + g.features.numel() * 2) / 2 ** 30, 2),
-        "shared_export": world > 1}), flush=True)
+        "shared_export": world > 1 and not args.engine_shards, "engine_shards": bool(args.engine_shards)}),
+        flush=True)
     dp.barrier()
 
 
@@ -123,6 +135,9 @@ def main(argv=None):
     p.add_argument("--make", default=None, help="write a synthetic graph in the on-disk format to this dir")
     p.add_argument("--data", default=None, help="upload the graph in this dir")
     p.add_argument("--ranks", type=int, default=1)
+    p.add_argument("--engine-shards", action="store_true",
+                   help="every rank's engine loads only its partitions and uploads its rows of the row-sharded "
+                        "graph (graph/sharded_graph.py from_engine_shard): host memory per rank 1/W")
     p.add_argument("--num-nodes", type=int, default=10_000_000)
     p.add_argument("--avg-degree", type=float, default=10.0)
     p.add_argument("--max-degree", type=int, default=1024)

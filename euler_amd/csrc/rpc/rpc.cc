@@ -1499,9 +1499,17 @@ Status QueryProxy::Init(const std::map<std::string, std::string>& config) {
   LoadOptions lopt;
   EULER_RETURN_IF_ERROR(LoadOptionsFromConfig(config, &lopt));
   if (mode_ == "local") {
+    // optional shard_idx / shard_num: this process loads only the partitions p with
+    // p % shard_num == shard_idx (reference graph.cc:90-98), e.g. one data-parallel rank's
+    // part of a graph row-sharded over the ranks' GPUs (graph/sharded_graph.py)
+    int64_t sidx = 0, snum = 1;
+    ParseInt64(Cfg(config, "shard_idx", "0"), &sidx);
+    ParseInt64(Cfg(config, "shard_num", "1"), &snum);
+    if (snum < 1 || sidx < 0 || sidx >= snum) return Status::InvalidArgument("local mode: bad shard_idx / shard_num");
     std::unique_ptr<Graph> g;
     std::unique_ptr<IndexManager> idx;
-    EULER_RETURN_IF_ERROR(LoadShard(Cfg(config, "data_path", ""), 0, 1, &g, &idx, 8, lopt));
+    EULER_RETURN_IF_ERROR(LoadShard(Cfg(config, "data_path", ""), static_cast<int>(sidx), static_cast<int>(snum), &g,
+                                    &idx, 8, lopt));
     return InitWithGraph(std::move(g), std::move(idx));
   }
   int64_t shards = 1;

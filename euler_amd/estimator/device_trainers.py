@@ -167,10 +167,13 @@ def build_sharded_trainer(est, model, first):
     est._prepare(first, build_optimizer=False)
     c = Ctx(est, model)
     gnn = model.gnn
-    g = ShardedDeviceGraph.from_engine(node_type=c.node_type(-1), features=gnn.feature_idx,
-                                       feature_dims=gnn.feature_dim, label=model.label_idx,
-                                       label_dim=model.label_dim, feature_dtype=c.feature_dtype(),
-                                       seed=c.seed * 7919 + est.rank, device=est.device)
+    # "engine_shards": every rank's engine holds only its partitions (initialize_graph with
+    # shard_idx = rank, shard_num = W): host memory per rank is 1/W of the graph
+    build = ShardedDeviceGraph.from_engine_shard if est.params.get("device_graph_sharded") == "engine_shards" \
+        else ShardedDeviceGraph.from_engine
+    g = build(node_type=c.node_type(-1), features=gnn.feature_idx, feature_dims=gnn.feature_dim,
+              label=model.label_idx, label_dim=model.label_dim, feature_dtype=c.feature_dtype(),
+              seed=c.seed * 7919 + est.rank, device=est.device)
     from euler_amd.convolution.convs import SAGEConv
 
     if all(isinstance(cv, SAGEConv) for cv in gnn.convs) and c.params.get("sharded_fused", True):

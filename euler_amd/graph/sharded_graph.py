@@ -185,6 +185,78 @@ class ShardedDeviceGraph:
             done()
         return cls(local, len(ids), float(nw.sum()), ids=ids, group=group)
 
+    @classmethod
+    def from_engine_shard(cls, engine=None, node_type=-1, features=(), feature_dims=(), label=None, label_dim=None,
+                          feature_dtype=torch.bfloat16, seed=0, device="cuda", group=None):
+        """the sharded graph from engines that each hold ONE shard of the on-disk graph
+        (``initialize_graph({"mode": "local", ..., "shard_idx": rank, "shard_num": W})``:
+        the partitions p % W == rank, reference graph.cc:90-98) — host memory per rank is
+        1/W of the graph, not the whole of it.  Rank r's nodes (sorted by id) become the
+        global rows i * W + r; the ranks all-gather their id lists once to map every
+        neighbour id to its row (``searchsorted`` on the device); shards with fewer nodes
+        than the largest are padded with edgeless, zero-feature, zero-weight rows."""
+        from euler_amd.ops import base
+
+        eng = engine if engine is not None else base.get_engine()
+        names = [] if not features else ([features] if isinstance(features, (str, int)) else list(features))
+        dims = [] if not features else ([feature_dims] if isinstance(feature_dims, int) else list(feature_dims))
+        on = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+        W, r = (dist.get_world_size(group), dist.get_rank(group)) if on else (1, 0)
+        device = torch.device(device)
+        cols = ["dense_" + str(n) for n in names] + ([] if label is None else ["dense_" + str(label)])
+        widths = [int(d) for d in dims] + ([] if label is None else [int(label_dim)])
+        parts = eng.export_shard(0, cols, widths)
+        ids = np.asarray(parts[0], np.uint64).astype(np.int64)
+        types = np.asarray(parts[1], np.int32)
+        nw = np.asarray(parts[2], np.float64)
+        indptr = np.asarray(parts[3], np.int64)
+        n = ids.shape[0]
+        T = max(1, (indptr.shape[0] - 1) // n) if n else 1
+        # the ranks' node counts and id lists -> global rows (i * W + rank); the collectives
+        # run on the device under RCCL and on the host under gloo
+        cdev = device if on and dist.get_backend(group) == "nccl" else torch.device("cpu")
+        cnt = torch.tensor([n], dtype=torch.int64, device=cdev)
+        counts = [torch.zeros_like(cnt) for _ in range(W)] if on else [cnt]
+        if on:
+            dist.all_gather(counts, cnt, group=group)
+        M = int(max(int(c.item()) for c in counts))
+        mine = torch.full((M,), -1, dtype=torch.int64, device=cdev)
+        mine[:n] = torch.from_numpy(ids).to(cdev)
+        every = [torch.empty_like(mine) for _ in range(W)] if on else [mine]
+        if on:
+            dist.all_gather(every, mine, group=group)
+        all_ids = torch.stack(every, 1).reshape(-1).to(device)  # row g = i * W + rank -> its id (-1: padding)
+        row_of = torch.arange(all_ids.numel(), device=device)
+        valid = all_ids >= 0
+        sid, order = torch.sort(all_ids[valid])
+        srow = row_of[valid][order]
+        del every, mine
+        nbr_ids = torch.from_numpy(np.asarray(parts[4], np.uint64).astype(np.int64)).to(device)
+        pos = torch.searchsorted(sid, nbr_ids).clamp(max=max(sid.numel() - 1, 0))
+        nbr_rows = torch.where(sid[pos] == nbr_ids, srow[pos], torch.full_like(pos, -1)).to(torch.int32)
+        del nbr_ids, pos
+        pad = (M - n) * T
+        lip = np.concatenate([indptr, np.full(pad, indptr[-1] if indptr.size else 0, np.int64)]) if pad else indptr
+        if node_type is not None and int(node_type) >= 0:
+            nw = np.where(types == int(node_type), nw, 0.0)
+        nwp = np.zeros(M, np.float64)
+        nwp[:n] = nw
+        local = DeviceGraph.from_csr(lip, nbr_rows.cpu().numpy(), np.asarray(parts[5], np.float32), T,
+                                     node_weights=nwp if M else None, seed=seed, device=device)
+        tabs = [np.asarray(t, np.float32).reshape(n, w) for t, w in zip(parts[6:], widths)]
+        if names:
+            f = torch.zeros(M, sum(widths[: len(names)]), dtype=torch.float32)
+            f[:n] = torch.from_numpy(np.concatenate(tabs[: len(names)], 1))
+            local.features = f.to(device=device, dtype=feature_dtype)
+        if label is not None:
+            lab = torch.zeros(M, int(label_dim), dtype=torch.float32)
+            lab[:n] = torch.from_numpy(tabs[-1])
+            local.labels = lab.to(device)
+        obj = cls(local, W * M, float(nw.sum()), ids=None, group=group)
+        obj._id_table = (sid, srow)
+        obj.row_ids = all_ids
+        return obj
+
     def set_root_weight(self, root_weight=None):
         """the owner alias table of the W shards' root-weight sums (all-gathered)"""
         wl = float(self.local.node_prob.numel() if root_weight is None else root_weight)
@@ -203,7 +275,13 @@ class ShardedDeviceGraph:
 
     # ------------------------------------------------------------------ DeviceGraph interface
     def rows_of(self, ids) -> torch.Tensor:
-        return DeviceGraph.rows_of(self, ids)
+        tab = getattr(self, "_id_table", None)
+        if tab is None:
+            return DeviceGraph.rows_of(self, ids)
+        sid, srow = tab  # from_engine_shard: rows are not in id order
+        q = torch.as_tensor(np.asarray(ids, dtype=np.uint64).astype(np.int64)).reshape(-1).to(sid.device)
+        pos = torch.searchsorted(sid, q).clamp(max=max(sid.numel() - 1, 0))
+        return torch.where(sid[pos] == q, srow[pos], torch.full_like(pos, -1)).cpu()
 
     def advance(self, inc: int = 1):
         self.local.advance(inc)

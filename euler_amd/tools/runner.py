@@ -208,6 +208,10 @@ def parse_args(argv=None, model=None):
                    help="with --device_graph: row-shard the graph (CSR, features, labels) over the ranks, "
                         "neighbour draws and features over all-to-all (graph/sharded_graph.py; supervised "
                         "SageDataFlow models)")
+    p.add_argument("--engine_shards", action="store_true",
+                   help="with --device_graph_sharded: every rank's engine loads only its partitions "
+                        "(shard_idx = rank): host memory per rank is 1/W of the graph (training only: "
+                        "an engine-path evaluate would see one shard)")
     p.add_argument("--device_feature_dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--cuda_graph", default="auto", choices=["auto", "off"],
                    help="capture the engine-path training step in a hipGraph when eligible")
@@ -232,14 +236,24 @@ def build(a):
         raise SystemExit("unknown model %r; choose from %s" % (a.model, sorted(MODELS)))
     ds_name, kind, builder = MODELS[a.model]
     ds = get_dataset(a.dataset or ds_name, data_dir=a.data_dir, scale=a.scale)
-    ds.load_graph()
+    if getattr(a, "engine_shards", False):
+        import torch.distributed as dist
+
+        from euler_amd.ops.base import initialize_graph
+
+        on = dist.is_available() and dist.is_initialized()
+        initialize_graph({"mode": "local", "data_path": ds.get_data_dir(), "data_type": ds.data_type,
+                          "shard_idx": dist.get_rank() if on else 0, "shard_num": dist.get_world_size() if on else 1})
+    else:
+        ds.load_graph()
     a._ds = ds
     model = builder(a, ds)
     total = a.total_step or max(1, int(a.num_epochs * ds.total_size / max(a.batch_size, 1)))
     params = {"model_dir": a.model_dir, "infer_dir": a.infer_dir, "batch_size": a.batch_size, "total_step": total,
               "log_steps": a.log_steps, "optimizer": a.optimizer, "learning_rate": a.learning_rate,
               "device": a.device, "amp": a.amp, "device_graph": a.device_graph or a.device_graph_sharded,
-              "device_graph_sharded": a.device_graph_sharded,
+              "device_graph_sharded": ("engine_shards" if a.engine_shards else True) if a.device_graph_sharded
+              else False,
               "device_feature_dtype": a.device_feature_dtype, "seed": a.seed,
               "native_pipeline": {"auto": "auto", "on": True, "off": False}[a.native_pipeline],
               "cuda_graph": a.cuda_graph if a.cuda_graph == "auto" else False,

@@ -418,3 +418,116 @@ def test_sharded_sage_two_ranks_share_the_gpu_in_lockstep():
     res = _run(_worker_shared_gpu)
     assert not [r for r in res if r[1] == "error"], res
     assert len(res) == 2 and all(r[2] for r in res), res
+
+
+def _worker_engine_shard(rank, world, port, q, data):
+    """each rank's engine loads only its partitions (shard_idx = rank); the sharded device
+    graph built from them holds the same nodes, neighbour multisets, weights, features and
+    labels as the whole graph (compared per node id)"""
+    try:
+        _init(rank, world, port)
+        from euler_amd.graph.sharded_graph import ShardedDeviceGraph
+        from euler_amd.ops import base
+
+        eng = base._engine_mod().Engine.from_config({"mode": "local", "data_path": data, "shard_idx": str(rank),
+                                                     "shard_num": str(world)})
+        full = base._engine_mod().Engine.from_config({"mode": "local", "data_path": data})
+        kw = dict(features=["feature"], feature_dims=[8], label="label", label_dim=4, feature_dtype=torch.float32,
+                  seed=1, device="cpu")
+        g = ShardedDeviceGraph.from_engine_shard(eng, **kw)
+        loc = g.local
+        ok = g.num_rows % world == 0 and loc.num_rows == g.num_rows // world
+        fp = full.export_shard(0, ["dense_feature", "dense_label"], [8, 4])
+        fids = np.asarray(fp[0], np.uint64).astype(np.int64)
+        find = {int(v): i for i, v in enumerate(fids)}
+        T = (len(fp[3]) - 1) // len(fids)
+        rid = g.row_ids
+        n_local = int((eng.export_shard(0, [], [])[0]).shape[0])
+        checked = 0
+        for i in range(0, n_local, 7):
+            gid = int(rid[i * world + rank])
+            j = find[gid]
+            for t in range(T):
+                a, b = int(fp[3][j * T + t]), int(fp[3][j * T + t + 1])
+                want = sorted(zip(np.asarray(fp[4][a:b]).astype(np.int64).tolist(),
+                                  np.round(np.asarray(fp[5][a:b], np.float64), 5).tolist()))
+                la, lb = int(loc.indptr[i * T + t]), int(loc.indptr[i * T + t + 1])
+                nb = loc.nbr[la:lb].long()
+                cw = loc.cumw[la:lb].double()
+                w = torch.cat([cw[:1], cw[1:] - cw[:-1]]) if lb > la else cw
+                got = sorted(zip(rid[nb].tolist(), np.round(w.numpy(), 5).tolist()))
+                ok &= [x for x, _ in got] == [x for x, _ in want]
+                ok &= np.allclose([y for _, y in got], [y for _, y in want], atol=1e-4)
+            ok &= np.allclose(loc.features[i].numpy(), np.asarray(fp[6]).reshape(-1, 8)[j])
+            ok &= np.allclose(loc.labels[i].numpy(), np.asarray(fp[7]).reshape(-1, 4)[j])
+            checked += 1
+        # rows_of maps ids back to rows; draws through the exchanges land on real rows
+        ok &= int(g.rows_of([int(rid[rank])])[0]) == rank
+        g.advance()
+        g.reseed_cpu()
+        nb = g.sample_neighbor(g.sample_node(64).long(), 3)
+        ok &= bool((rid[nb[nb >= 0].long()] >= 0).all())
+        q.put((rank, "engine_shard", bool(ok and checked > 10), checked))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_sharded_graph_from_per_rank_engine_shards(tmp_path):
+    import euler_amd as ea
+
+    data = str(tmp_path / "g")
+    e = ea.synthetic_graph(3000, 6.0, 64, node_types=1, edge_types=2, feature_dim=8, label_dim=4, seed=3,
+                           make_current=False)
+    e.save(data, partitions=4, threads=4)
+    res = _run(_worker_engine_shard, data)
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == 2 and all(r[2] for r in res), res
+
+
+def _worker_engine_shard_estimator(rank, world, port, q, data, tmp):
+    """NodeEstimator(device_graph_sharded="engine_shards"): each rank's engine holds half of
+    the partitions; a SupervisedGraphSage trains on the fused step in lockstep"""
+    try:
+        _init(rank, world, port)
+        from euler_amd import models as Z
+        from euler_amd.estimator import NodeEstimator
+        from euler_amd.models.sharded_sage import ShardedSageTrainer
+        from euler_amd.ops.base import initialize_graph
+
+        initialize_graph({"mode": "local", "data_path": data, "shard_idx": rank, "shard_num": world})
+        torch.manual_seed(0)
+        m = Z.SupervisedGraphSage([16, 16, 8], [4, 3], [["0", "1"], ["0", "1"]], "feature", 8, "label", 4,
+                                  max_id=2999)
+        est = NodeEstimator(m, {"model_dir": os.path.join(tmp, "ck"), "batch_size": 32, "total_step": 6,
+                                "log_steps": 3, "device": "cpu", "device_graph": True,
+                                "device_graph_sharded": "engine_shards", "seed": 3, "train_node_type": -1,
+                                "device_feature_dtype": "fp32"})
+        res = est.train()
+        tr = est.device_trainer
+        p = tr.logical_params()
+        flat = torch.cat([p[k].reshape(-1).float() for k in sorted(p)])
+        allp = [torch.zeros_like(flat) for _ in range(world)]
+        dist.all_gather(allp, flat)
+        ok = isinstance(tr, ShardedSageTrainer) and all(torch.equal(x, allp[0]) for x in allp)
+        ok &= est.global_step == 6 and math.isfinite(res["loss"]) and tr.sgraph.local.num_rows < 3000
+        q.put((rank, "engine_shard_est", bool(ok)))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_estimator_on_per_rank_engine_shards(tmp_path):
+    import euler_amd as ea
+
+    data = str(tmp_path / "g")
+    e = ea.synthetic_graph(3000, 6.0, 64, node_types=1, edge_types=2, feature_dim=8, label_dim=4, seed=3,
+                           make_current=False)
+    e.save(data, partitions=4, threads=4)
+    res = _run(_worker_engine_shard_estimator, data, str(tmp_path))
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == 2 and all(r[2] for r in res), res
