@@ -120,7 +120,7 @@ def _worker_sampling(rank, world, port, q):
         q.put((rank, "error", traceback.format_exc()))
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_sharded_sampling_exact_support_and_frequencies(world):
     res = _run(_worker_sampling, world=world)
     assert not [r for r in res if r[1] == "error"], res
