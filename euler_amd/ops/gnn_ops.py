@@ -59,17 +59,16 @@ class EdgeCSR:
 
     def csr(self):
         if self._csr is None:
-            dst, src = self.edge_index[0].long(), self.edge_index[1].long()
-            seg = SegmentIndex(dst, self.n_dst)
-            col = src[seg.perm].to(torch.int32)
+            # the block's destination CSR when its producer cached one (dataflow/device_flow.py)
+            seg = _cached_segment(self.edge_index, 0, self.n_dst)
+            col = self.edge_index[1].long()[seg.perm].to(torch.int32)
             self._csr = (seg.indptr, col.contiguous())
         return self._csr
 
     def csc(self):
         if self._csc is None:
-            dst, src = self.edge_index[0].long(), self.edge_index[1].long()
-            seg = SegmentIndex(src, self.n_src)
-            row = dst[seg.perm].to(torch.int32)
+            seg = _cached_segment(self.edge_index, 1, self.n_src)
+            row = self.edge_index[0].long()[seg.perm].to(torch.int32)
             self._csc = (seg.indptr, row.contiguous())
         return self._csc
 
@@ -90,6 +89,12 @@ class EdgeCSR:
         if getattr(self, "_csc_order", None) is None:
             self._csc_order = self._by_degree(self.csc()[0])
         return self._csc_order
+
+
+def _cached_segment(edge_index, i, size):
+    from euler_amd.ops.mp_ops import cached_segment
+
+    return cached_segment(edge_index, i, size)
 
 
 def _cached(edge_index, key, build):
