@@ -72,13 +72,18 @@ class EdgeCSR:
             self._csc = (seg.indptr, row.contiguous())
         return self._csc
 
-    @staticmethod
-    def _by_degree(indptr):
+    def _by_degree(self, indptr):
         # longest rows first: the rows sharing a wave have similar lengths and the
         # heaviest work starts first (cdna_hip_programming.md App. B, skewed gathers)
         if os.environ.get("EULER_AMD_GAT_ORDER", "1") == "0":
             return None
-        return torch.argsort(torch.diff(indptr), descending=True).to(torch.int32).contiguous()
+        deg = torch.diff(indptr)
+        E = int(self.edge_index.shape[1])
+        if use_hip(deg) and 0 < E < (1 << 30):
+            # a stable radix sort of E - degree over its bits only (det_occ), no host read
+            _, perm = hip().det_occ((E - deg).contiguous(), E + 1)
+            return perm.contiguous()
+        return torch.argsort(deg, descending=True).to(torch.int32).contiguous()
 
     def csr_order(self):
         if getattr(self, "_csr_order", None) is None:
