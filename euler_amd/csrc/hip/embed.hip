@@ -263,9 +263,18 @@ __global__ __launch_bounds__(256) void det_count_kernel(const int64_t* __restric
                                                         int* __restrict__ cnt, int64_t* __restrict__ ptr) {
   const int64_t o = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (o == 0) ptr[0] = 0;
-  if (o >= n) return;
-  const int64_t k = keys[o];
-  if (k >= 0 && k < S) atomicAdd(cnt + k, 1);
+  // runs of equal keys inside a wave (target-major edge lists, hub rows) add once per run:
+  // the run's first lane adds its length, so a hot key costs one atomic per wave, not 64
+  const int lane = threadIdx.x & 63;
+  const int64_t k = o < n ? keys[o] : -1;
+  const int64_t prev = __shfl_up(k, 1, 64);
+  const bool head = lane == 0 || prev != k;
+  const unsigned long long heads = __ballot(head);
+  if (head && k >= 0 && k < S) {
+    const unsigned long long rest = lane == 63 ? 0ull : (heads >> (lane + 1));
+    const int len = rest ? __ffsll(static_cast<long long>(rest)) : 64 - lane;
+    atomicAdd(cnt + k, len);
+  }
 }
 
 // the radix sort's inputs: 32-bit keys (a skipped key sorts last, as S) and occurrence ids

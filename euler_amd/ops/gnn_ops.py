@@ -77,13 +77,9 @@ class EdgeCSR:
         # heaviest work starts first (cdna_hip_programming.md App. B, skewed gathers)
         if os.environ.get("EULER_AMD_GAT_ORDER", "1") == "0":
             return None
-        deg = torch.diff(indptr)
-        E = int(self.edge_index.shape[1])
-        if use_hip(deg) and 0 < E < (1 << 30):
-            # a stable radix sort of E - degree over its bits only (det_occ), no host read
-            _, perm = hip().det_occ((E - deg).contiguous(), E + 1)
-            return perm.contiguous()
-        return torch.argsort(deg, descending=True).to(torch.int32).contiguous()
+        # (a bit-limited radix sort of E - degree measured slower here: its count and scan
+        # run over E + 1 key values, more than the rows an argsort orders)
+        return torch.argsort(torch.diff(indptr), descending=True).to(torch.int32).contiguous()
 
     def csr_order(self):
         if getattr(self, "_csr_order", None) is None:
