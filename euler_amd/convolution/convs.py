@@ -357,6 +357,13 @@ class DNAConv(Conv):
         q, k, v = self.lin_q(q), self.lin_k(k), self.lin_v(v)
         E = q.shape[0]
         ch = self.dim // self.heads
+        if q.shape[1] == 1 and k.shape[1] == 1:
+            # one key per query (the conv's case): the attention products are per-head dot
+            # products and a scale — elementwise over the edges instead of E tiny batched
+            # matmuls (which dominated capacity-padded device blocks)
+            qh, kh, vh = (t.reshape(E, self.heads, ch) for t in (q, k, v))
+            s = restricted_softmax((qh * kh).sum(-1, keepdim=True) / math.sqrt(ch), dim=-1)
+            return (s * vh).reshape(E, 1, self.dim)
         q = q.reshape(E, -1, self.heads, ch).transpose(1, 2)
         k = k.reshape(E, -1, self.heads, ch).transpose(1, 2)
         v = v.reshape(E, -1, self.heads, ch).transpose(1, 2)

@@ -375,3 +375,21 @@ def test_gnn_dispatches_fused_sage_kernel(syn, cuda, monkeypatch, din):
     for a, b in zip(g, gref):
         c = torch.nn.functional.cosine_similarity(a.float().reshape(-1), b.float().reshape(-1), dim=0)
         assert c > 0.99, c
+
+
+def test_dna_single_key_attention_equals_matmul_form():
+    """DNAConv's one-key attention as per-head dot products equals the batched-matmul form"""
+    import math
+
+    from euler_amd.convolution.convs import DNAConv, restricted_softmax
+
+    torch.manual_seed(0)
+    conv = DNAConv(16, heads=4, groups=2)
+    q, k = torch.randn(50, 1, 16), torch.randn(50, 1, 16)
+    got = conv.multi_head(q, k, k)
+    Q, K, V = conv.lin_q(q), conv.lin_k(k), conv.lin_v(k)
+    E, h, ch = 50, 4, 4
+    Q, K, V = (t.reshape(E, -1, h, ch).transpose(1, 2) for t in (Q, K, V))
+    s = restricted_softmax(Q @ K.transpose(-1, -2) / math.sqrt(ch), dim=-1)
+    want = (s @ V).transpose(1, 2).reshape(E, -1, 16)
+    torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-6)
