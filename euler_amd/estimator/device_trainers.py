@@ -177,8 +177,17 @@ def build_sharded_trainer(est, model, first):
     from euler_amd.convolution.convs import SAGEConv
 
     if all(isinstance(cv, SAGEConv) for cv in gnn.convs) and c.params.get("sharded_fused", True):
-        # SupervisedGraphSage: the fused tree-step kernels on trees drawn across the ranks
+        # SupervisedGraphSage: the fused tree-step kernels on trees drawn across the ranks;
+        # one rank holds the whole graph: the whole-graph trainer (its sampler runs inside
+        # the head launch)
         from euler_amd.models.sharded_sage import ShardedSageTrainer
+
+        if not g.comm:
+            from euler_amd.models.sage_trainer import SageTrainer
+
+            tr = SageTrainer.from_model(model, g.local, c.batch, keep_samples=False, **c.opt_kw())
+            tr.device_trainer_kind = "graphsage"
+            return tr
 
         tr = ShardedSageTrainer.from_model(model, g, c.batch, keep_samples=False, **c.opt_kw())
         tr.device_trainer_kind = "sharded_graphsage"
