@@ -10,6 +10,8 @@ features, hidden 256, 64 classes, Adam) on a synthetic power-law graph generated
 
     python benchmarks/bench_sharded_sage.py --gpus 1 --num-nodes 100000000
     python benchmarks/bench_sharded_sage.py --gpus 8 ...        (one rank per GPU, self-spawned)
+    python benchmarks/bench_sharded_sage.py --model gcn ...     (2-layer GCN on full-neighbourhood
+        blocks expanded by the rows' owners: ShardedDeviceGraph.full_neighbors + DeviceFullFlow)
 
 Prints one JSON line (rank 0): whole-job samples/s, ms per step, per-GPU graph bytes.
 Reference: tf_euler/python/dataflow/sage_dataflow.py:35-50 over remote_op.cc:60-146.
@@ -42,7 +44,10 @@ def main(argv=None):
     p.add_argument("--classes", type=int, default=64)
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--model", choices=["sage", "gcn"], default="sage")
     p.add_argument("--graph", action="store_true", help="capture the step (sampling exchanges included) in a hipGraph")
+    p.add_argument("--force-comm", action="store_true",
+                   help="one rank: run every exchange through a 1-rank RCCL group (the W > 1 code path)")
     p.add_argument("--shared-gpu", action="store_true",
                    help="rehearsal: every rank on GPU 0 over gloo (exchanges and gradients through host memory, "
                         "eager steps); RCCL needs one GPU per rank")
@@ -68,12 +73,35 @@ def main(argv=None):
         dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     dp.init_distributed(backend="gloo" if args.shared_gpu else "nccl", device=dev)
+    if args.force_comm and world == 1:
+        import socket
+
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
     rank = dp.rank()
     t0 = time.time()
+    gcn = args.model == "gcn"
     g = ShardedDeviceGraph.synthetic(args.num_nodes, args.avg_degree, feature_dim=args.feature_dim,
-                                     num_classes=args.classes, seed=3, device=dev)
+                                     num_classes=args.classes, multi_label=gcn, seed=3, device=dev,
+                                     force_comm=args.force_comm)
     dims = [args.hidden] * len(args.fanouts) + [args.hidden]
-    tr = ShardedSageTrainer(g, args.batch, args.fanouts, dims, args.classes, learning_rate=0.01, init_seed=0)
+    if gcn:
+        # the reference's SupervisedGCN shape: GCNConv layers on GCNDataFlow (full
+        # neighbourhoods, self loops), sigmoid cross-entropy; one layer per --fanouts entry
+        from euler_amd import models as Z
+        from euler_amd.dataflow.device_flow import DeviceFullFlow
+        from euler_amd.models.full_trainer import ShardedFlowTrainer
+
+        torch.manual_seed(0)
+        L = len(args.fanouts)
+        m = Z.SupervisedGNN("gcn", "full", [args.hidden] * L + [args.classes], [1] * L, [[0]] * L, "f",
+                            args.feature_dim, "l", args.classes, max_id=args.num_nodes).to(dev)
+        flow = DeviceFullFlow(g, [1] * L, args.batch, True, "bounded")
+        tr = ShardedFlowTrainer(m, g, args.batch, flow, learning_rate=0.01)
+    else:
+        tr = ShardedSageTrainer(g, args.batch, args.fanouts, dims, args.classes, learning_rate=0.01, init_seed=0)
     sync = None
     if world > 1:
         def sync(buf):
@@ -86,7 +114,7 @@ def main(argv=None):
             return 1.0 / world
     torch.cuda.synchronize()
     build_s = time.time() - t0
-    if args.graph:
+    if args.graph and not (gcn and g.comm):  # full-flow exchanges read split sizes on the host
         tr.capture(sync, warmup=args.warmup, steps=1)
         run = tr.replay_steps
     else:
@@ -110,21 +138,28 @@ def main(argv=None):
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     el = float(el.item())
     g.check_overflow()
+    if gcn:
+        tr.flow.check()
     if rank == 0:
         print(json.dumps({
-            "metric": "GraphSAGE train samples/s on a row-sharded graph (whole job)",
+            "metric": ("GCN" if gcn else "GraphSAGE") + " train samples/s on a row-sharded graph (whole job)",
             "value": round(args.batch * world * args.steps / el, 1), "unit": "samples/s",
             "n_gpus": 1 if args.shared_gpu else world, "ranks": world,
-            "shared_gpu_rehearsal": bool(args.shared_gpu) or None,
+            "shared_gpu_rehearsal": bool(args.shared_gpu) or None, "exchanges": bool(g.comm),
             "ms_per_step": round(el * 1e3 / args.steps, 3), "steps": args.steps, "warmup": args.warmup,
-            "loss": float(tr.loss.item()), "hipgraph": bool(args.graph), "build_s": round(build_s, 1),
+            "loss": float(tr.loss.item()), "hipgraph": bool(args.graph) and tr._graphs != {} if gcn else bool(args.graph),
+            "build_s": round(build_s, 1), "flow_caps": tr.flow.caps if gcn else None,
             "graph_gib_per_gpu": round((g.nbytes() + g.features.shard.numel() * 2) / 2 ** 30, 2),
-            "config": {"num_nodes": args.num_nodes, "batch_per_gpu": args.batch, "fanouts": args.fanouts,
+            "config": {"model": args.model, "num_nodes": args.num_nodes, "batch_per_gpu": args.batch,
+                       "fanouts": None if gcn else args.fanouts, "layers": len(args.fanouts),
                        "hidden": args.hidden, "feature_dim": args.feature_dim, "classes": args.classes},
             "data": "synthetic power-law graph generated in HBM, random features / labels"}), flush=True)
     if world > 1:
         tr.release_graphs()
         dist.barrier()
+    elif dist.is_initialized():
+        tr.release_graphs()
+        dist.destroy_process_group()
     return 0
 
 

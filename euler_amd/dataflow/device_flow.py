@@ -49,6 +49,8 @@ def _round_up(x: int, m: int = 256) -> int:
 
 def max_out_degree(graph, mask: int) -> int:
     """largest out-degree of any row over the edge types of ``mask``"""
+    if hasattr(graph, "degree_stats"):  # row-sharded: reduced over the ranks
+        return graph.degree_stats(mask)[0]
     T = graph.num_types
     seg = (graph.indptr[1:] - graph.indptr[:-1]).view(graph.num_rows, T)
     sel = torch.tensor([(mask >> t) & 1 for t in range(T)], dtype=seg.dtype, device=seg.device)
@@ -56,6 +58,8 @@ def max_out_degree(graph, mask: int) -> int:
 
 
 def masked_edges(graph, mask: int) -> int:
+    if hasattr(graph, "degree_stats"):
+        return graph.degree_stats(mask)[1]
     T = graph.num_types
     seg = (graph.indptr[1:] - graph.indptr[:-1]).view(graph.num_rows, T)
     sel = torch.tensor([(mask >> t) & 1 for t in range(T)], dtype=seg.dtype, device=seg.device)
@@ -172,16 +176,20 @@ def bounded_caps(graph, masks, batch_size: int, quantile: float = 0.99, safety: 
     by the overflow flag (:meth:`DeviceFullFlow.grow`, re-capture)."""
     exact = exact_caps(graph, masks, batch_size)
     T = graph.num_types
-    seg = (graph.indptr[1:] - graph.indptr[:-1]).view(graph.num_rows, T)
     caps = []
     n = int(batch_size)
     N = graph.num_rows
     for (ex_e, ex_n), m in zip(exact, masks):
-        sel = torch.tensor([(m >> t) & 1 for t in range(T)], dtype=seg.dtype, device=seg.device)
-        deg = (seg * sel).sum(1).float()
-        mean = float(deg.mean().item()) if deg.numel() else 0.0
-        k = max(1, int(deg.numel() * (1.0 - quantile)))
-        tail = float(torch.topk(deg, min(k, deg.numel())).values.min().item()) if deg.numel() else 0.0
+        k = max(1, int(N * (1.0 - quantile)))
+        if hasattr(graph, "degree_stats"):  # row-sharded: mean and tail over every rank's rows
+            _, total, tail = graph.degree_stats(m, k)
+            mean = total / N if N else 0.0
+        else:
+            seg = (graph.indptr[1:] - graph.indptr[:-1]).view(graph.num_rows, T)
+            sel = torch.tensor([(m >> t) & 1 for t in range(T)], dtype=seg.dtype, device=seg.device)
+            deg = (seg * sel).sum(1).float()
+            mean = float(deg.mean().item()) if deg.numel() else 0.0
+            tail = float(torch.topk(deg, min(k, deg.numel())).values.min().item()) if deg.numel() else 0.0
         e = min(ex_e, _round_up(int(safety * (n * mean + tail)) + 1))
         n_next = min(ex_n, N, _round_up(n + e))
         caps.append((int(e), int(n_next)))
@@ -229,11 +237,7 @@ class DeviceFullFlow:
         cap_prev = self.B
         for h, mask in enumerate(self.masks):
             cap_e, cap_n = self.caps[h]
-            if use_hip(n_id):
-                nbr, src, offs = hip().full_neighbors(g.indptr, g.nbr, g.num_rows, g.num_types, mask & 0xFFFFFFFF,
-                                                      n_id, cap_e, self.overflow)
-            else:
-                nbr, src, offs = full_neighbors_cpu(g, mask, n_id, cap_e, self.overflow)
+            nbr, src, offs = self._expand(n_id, mask, cap_e)
             kept = self._filter(h, n_id, nbr)
             if kept is not None:
                 nbr = kept
@@ -303,6 +307,16 @@ class DeviceFullFlow:
                      for (e, n), (ex_e, ex_n) in zip(self.caps, exact)]
         self.overflow.zero_()
         return self.caps
+
+    def _expand(self, n_id, mask, cap_e):
+        """(neighbours, target index, inclusive offsets) of the hop's full expansion"""
+        g = self.g
+        if hasattr(g, "full_neighbors"):  # a row-sharded graph: the owners expand
+            return g.full_neighbors(n_id, mask, cap_e, self.overflow)
+        if use_hip(n_id):
+            return hip().full_neighbors(g.indptr, g.nbr, g.num_rows, g.num_types, mask & 0xFFFFFFFF, n_id, cap_e,
+                                        self.overflow)
+        return full_neighbors_cpu(g, mask, n_id, cap_e, self.overflow)
 
     def _filter(self, h, n_id, nbr):
         """hook: the hop's neighbour list with dropped entries set to -1 (None: keep all)"""

@@ -145,13 +145,14 @@ def build_device_trainer(est, model, first):
 
 
 def sharded_supported(model) -> bool:
-    """supervised models on the sampled ``SageDataFlow`` (any convolution, no stores)"""
+    """supervised models on the sampled ``SageDataFlow`` or the full-neighbourhood
+    ``GCNDataFlow`` (any convolution, no stores)"""
     from euler_amd.dataflow import dataflows as D
 
     gnn = getattr(model, "gnn", None)
     return (gnn is not None and hasattr(gnn, "feature_idx") and hasattr(model, "label_idx")
             and not hasattr(model, "context_gnn") and not has_store_encoder(model)
-            and isinstance(getattr(gnn, "sampler", None), D.SageDataFlow))
+            and isinstance(getattr(gnn, "sampler", None), (D.SageDataFlow, D.GCNDataFlow)))
 
 
 def build_sharded_trainer(est, model, first):
@@ -162,7 +163,8 @@ def build_sharded_trainer(est, model, first):
     from euler_amd.models.full_trainer import ShardedFlowTrainer
 
     if not sharded_supported(model):
-        raise NoDeviceTrainer("device_graph_sharded=True trains supervised models on the sampled SageDataFlow; "
+        raise NoDeviceTrainer("device_graph_sharded=True trains supervised models on the sampled SageDataFlow or "
+                              "the full-neighbourhood GCNDataFlow; "
                               f"{type(model).__name__} is not one")
     est._prepare(first, build_optimizer=False)
     c = Ctx(est, model)
@@ -176,6 +178,25 @@ def build_sharded_trainer(est, model, first):
               seed=c.seed * 7919 + est.rank, device=est.device)
     from euler_amd.convolution.convs import SAGEConv
 
+    from euler_amd.dataflow import dataflows as D
+
+    if isinstance(gnn.sampler, D.GCNDataFlow):
+        # GCN / APPNP / TAGCN / ...: full-neighbourhood blocks expanded by the rows' owners;
+        # one rank holds the whole graph: the whole-graph trainers (fused GCN step, captured)
+        caps = c.params.get("device_flow_caps", "bounded")
+        if not g.comm:
+            from euler_amd.models.full_trainer import FullFlowTrainer
+            from euler_amd.models.gcn_trainer import GcnTrainer
+
+            if c.params.get("gcn_fused", True) and GcnTrainer.supports(model, g.local, c.batch):
+                tr = GcnTrainer.from_model(model, g.local, c.batch, caps=caps, **c.opt_kw())
+            else:
+                tr = FullFlowTrainer.from_model(model, g.local, c.batch, **c.opt_kw(), caps=caps)
+            tr.device_trainer_kind = "full_flow"
+            return tr
+        tr = ShardedFlowTrainer.from_model(model, g, c.batch, caps=caps, **c.opt_kw())
+        tr.device_trainer_kind = "sharded_full_flow"
+        return tr
     if all(isinstance(cv, SAGEConv) for cv in gnn.convs) and c.params.get("sharded_fused", True):
         # SupervisedGraphSage: the fused tree-step kernels on trees drawn across the ranks;
         # one rank holds the whole graph: the whole-graph trainer (its sampler runs inside

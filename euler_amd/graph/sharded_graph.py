@@ -127,7 +127,8 @@ class ShardedDeviceGraph:
 
     @classmethod
     def synthetic(cls, num_nodes: int, avg_degree: float = 10.0, max_degree: int = 1024, feature_dim: int = 128,
-                  num_classes: int = 64, multi_label: bool = False, seed: int = 0, device="cuda", group=None):
+                  num_classes: int = 64, multi_label: bool = False, seed: int = 0, device="cuda", group=None,
+                  force_comm: bool = False):
         """this rank's rows of a synthetic power-law graph generated straight in HBM (no
         host copy): the local CSR from the device generator with its neighbour values spread
         over every rank's rows, bf16 features and class (or multi-label) labels"""
@@ -145,7 +146,7 @@ class ShardedDeviceGraph:
             loc.labels = (torch.rand(n_local, num_classes, generator=gen, device=loc.device) < 0.1).float()
         else:
             loc.labels = torch.randint(0, num_classes, (n_local, 1), generator=gen, device=loc.device).float()
-        return cls(loc, int(num_nodes), float(n_local), group=group)
+        return cls(loc, int(num_nodes), float(n_local), group=group, force_comm=force_comm)
 
     @classmethod
     def from_engine(cls, engine=None, node_type=-1, features=(), feature_dims=(), label=None, label_dim=None,
@@ -382,6 +383,93 @@ class ShardedDeviceGraph:
             return out_nb
         return out_nb, self._back(w.view(-1, F).float(), pos, 0.0), self._back(t.view(-1, F).int(), pos, -1)
 
+    # ------------------------------------------------------------------ full neighbourhoods
+    def _masked_degree(self, local_rows: torch.Tensor, mask: int) -> torch.Tensor:
+        """out-degree over the edge types of ``mask`` of local rows (``-1``: 0)"""
+        g, T = self.local, self.num_types
+        ok = local_rows >= 0
+        r = torch.where(ok, local_rows, torch.zeros_like(local_rows)) * T
+        deg = torch.zeros(local_rows.shape, dtype=torch.long, device=local_rows.device)
+        if g.num_rows == 0:
+            return deg
+        for t in range(T):
+            if (mask >> t) & 1:
+                deg += (g.indptr[r + t + 1] - g.indptr[r + t]).long()
+        return torch.where(ok, deg, torch.zeros_like(deg))
+
+    def _reduce(self, t: torch.Tensor, op) -> torch.Tensor:
+        if self.comm:
+            comm.all_reduce(t, op, group=self.group)
+        return t
+
+    def degree_stats(self, mask: int, k: int = 1):
+        """(largest out-degree, edge count, k-th largest out-degree) over the edge types of
+        ``mask`` and every rank's rows — the inputs of the full-neighbourhood flow's
+        capacities (dataflow/device_flow.py exact_caps / bounded_caps).  The k-th largest
+        comes from the all-reduced degree histogram (exact, W-independent)."""
+        n = self.local.num_rows
+        deg = self._masked_degree(torch.arange(n, device=self.device), int(mask))
+        agg = torch.stack([deg.max() if n else torch.zeros((), dtype=torch.long, device=self.device),
+                           deg.sum()])
+        mx = int(self._reduce(agg[:1].clone(), dist.ReduceOp.MAX).item()) if self.comm else int(agg[0].item())
+        total = int(self._reduce(agg[1:].clone(), dist.ReduceOp.SUM).item())
+        hist = self._reduce(torch.bincount(deg, minlength=mx + 1)[: mx + 1], dist.ReduceOp.SUM)
+        at_least = torch.flip(torch.cumsum(torch.flip(hist, [0]), 0), [0])  # rows with degree >= d
+        hit = torch.nonzero(at_least >= max(1, int(k))).reshape(-1)
+        kth = int(hit[-1].item()) if hit.numel() else 0
+        return mx, total, kth
+
+    def full_neighbors(self, rows: torch.Tensor, mask: int, cap: int, overflow: torch.Tensor):
+        """``full_neighbors`` over the sharded rows: (neighbours [cap], target index [cap],
+        inclusive per-target offsets [n]) — every neighbour of every row of the edge types of
+        ``mask``, target-major in storage order, ``-1`` padding, exactly the whole graph's
+        expansion (dataflow/device_flow.py full_neighbors_cpu).  Each row is expanded by its
+        owner; the lists come back over one variable-size all-to-all (two host reads give the
+        split sizes: the step is eager) and are laid out target-major by a searchsorted over
+        the requesters' offsets.  More than ``cap`` entries set ``overflow``."""
+        rows = rows.reshape(-1).long()
+        n, dev = rows.numel(), self.device
+        if not self.comm:
+            g = self.local
+            if use_hip(rows):
+                return hip().full_neighbors(g.indptr, g.nbr, g.num_rows, g.num_types, int(mask) & 0xFFFFFFFF, rows,
+                                            int(cap), overflow)
+            from euler_amd.dataflow.device_flow import full_neighbors_cpu
+
+            return full_neighbors_cpu(g, int(mask), rows, int(cap), overflow)
+        W = self.world
+        ok = (rows >= 0) & (rows < self.num_rows)
+        pos, recv, C = self._route(torch.where(ok, rows, torch.full_like(rows, -1)))
+        loc = self._local_rows(recv)
+        deg_l = self._masked_degree(loc, int(mask))  # [W*C], the owner's received slots
+        send_split = deg_l.view(W, C).sum(1)
+        recv_split = self._a2a(send_split)
+        splits = torch.stack([send_split, recv_split]).cpu()  # the host sync of the exchange
+        total_l = int(splits[0].sum())
+        if total_l:
+            g = self.local
+            own = torch.zeros(1, dtype=torch.int32, device=dev)
+            if use_hip(loc):
+                nb_l, _, _ = hip().full_neighbors(g.indptr, g.nbr, g.num_rows, g.num_types, int(mask) & 0xFFFFFFFF,
+                                                  loc, total_l, own)
+            else:
+                from euler_amd.dataflow.device_flow import full_neighbors_cpu
+
+                nb_l, _, _ = full_neighbors_cpu(g, int(mask), loc, total_l, own)
+            nb_l = nb_l.int()
+        else:
+            nb_l = torch.zeros(0, dtype=torch.int32, device=dev)
+        buf = torch.empty(int(splits[1].sum()), dtype=torch.int32, device=dev)
+        comm.all_to_all_single(buf, nb_l, splits[1].tolist(), splits[0].tolist(), group=self.group)
+        # requester side: the received lists are a CSR over this rank's request slots
+        # (owner-major, slot order; a slot's degree from its owner): expanding the requests'
+        # slots through it is full_neighbors again — target-major, -1 padded, overflow flagged
+        deg_s = self._a2a(deg_l)
+        ptr_s = torch.cat([torch.zeros(1, dtype=torch.long, device=dev), torch.cumsum(deg_s, 0)])
+        slots = torch.where(pos < deg_s.numel(), pos, torch.full_like(pos, -1))  # a trashed request: none
+        return _expand_csr(ptr_s, buf, slots, int(cap), overflow)
+
+
     # ------------------------------------------------------------------ features / labels
     def padded_features(self, mult: int = 16):
         """the feature exchange over a shard whose width is padded to ``mult`` columns
@@ -412,6 +500,17 @@ class ShardedDeviceGraph:
             return mp_ops.gather(sf.cache, pos.long())
         return torch.where((pos >= 0).unsqueeze(1), sf.cache[pos.long().clamp(min=0)], torch.zeros(
             (), dtype=sf.cache.dtype))
+
+
+def _expand_csr(indptr, nbr, rows, cap, overflow):
+    """``full_neighbors`` over a one-type CSR (indptr int64 [n+1], nbr int32)"""
+    if use_hip(rows):
+        return hip().full_neighbors(indptr, nbr, indptr.numel() - 1, 1, 1, rows, int(cap), overflow)
+    from types import SimpleNamespace
+
+    from euler_amd.dataflow.device_flow import full_neighbors_cpu
+
+    return full_neighbors_cpu(SimpleNamespace(indptr=indptr, nbr=nbr, num_types=1), 1, rows, int(cap), overflow)
 
 
 def _alias_weights(g: DeviceGraph):

@@ -241,19 +241,25 @@ class ShardedFlowTrainer(FullFlowTrainer):
         CapturedTrainer.__init__(self, model, graph, graph.device, optimizer, learning_rate)
 
     @classmethod
-    def from_model(cls, model, graph, batch_size, optimizer="adam", learning_rate=0.01, **kw):
+    def from_model(cls, model, graph, batch_size, optimizer="adam", learning_rate=0.01, caps="bounded", **kw):
         import euler_amd.ops.graph_api as ge
-        from euler_amd.dataflow.dataflows import SageDataFlow
-        from euler_amd.dataflow.device_flow import DeviceSageFlow
+        from euler_amd.dataflow.dataflows import GCNDataFlow, SageDataFlow
+        from euler_amd.dataflow.device_flow import DeviceFullFlow, DeviceSageFlow
 
         flow = getattr(model.gnn, "sampler", None)
-        if not isinstance(flow, SageDataFlow):
-            raise ValueError("the sharded device graph trains models on the sampled SageDataFlow (fixed fanouts)")
+        if not isinstance(flow, (SageDataFlow, GCNDataFlow)):
+            raise ValueError("the sharded device graph trains models on the sampled SageDataFlow (fixed fanouts) "
+                             "or the full-neighbourhood GCNDataFlow")
         ets = []
         for m in flow.metapath:
             ids = None if m is None else [int(t) for t in np.asarray(ge.get_edge_type_id(m)).reshape(-1)]
             ets.append(None if ids is None or any(t < 0 for t in ids) else ids)
-        dflow = DeviceSageFlow(graph, ets, flow.fanouts, batch_size, bool(flow.add_self_loops))
+        if isinstance(flow, SageDataFlow):
+            dflow = DeviceSageFlow(graph, ets, flow.fanouts, batch_size, bool(flow.add_self_loops))
+        else:
+            # every hop expanded by the rows' owners (ShardedDeviceGraph.full_neighbors),
+            # capacities from the degree statistics reduced over the ranks
+            dflow = DeviceFullFlow(graph, [graph._mask(e) for e in ets], batch_size, bool(flow.add_self_loops), caps)
         return cls(model, graph, batch_size, dflow, optimizer=optimizer, learning_rate=learning_rate)
 
     def _forward_loss(self):

@@ -12,7 +12,7 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
-__all__ = ["all_to_all_single"]
+__all__ = ["all_reduce", "all_to_all_single"]
 
 
 def all_to_all_single(output: torch.Tensor, input: torch.Tensor, output_split_sizes=None, input_split_sizes=None,
@@ -24,3 +24,14 @@ def all_to_all_single(output: torch.Tensor, input: torch.Tensor, output_split_si
         output.copy_(host_out)
         return
     dist.all_to_all_single(output, input, output_split_sizes, input_split_sizes, group=group)
+
+
+def all_reduce(t: torch.Tensor, op=dist.ReduceOp.SUM, group=None) -> torch.Tensor:
+    """in-place ``all_reduce`` of ``t`` (device tensors staged through host on gloo)"""
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        host = t.detach().cpu()
+        dist.all_reduce(host, op=op, group=group)
+        t.copy_(host)
+        return t
+    dist.all_reduce(t, op=op, group=group)
+    return t

@@ -284,10 +284,34 @@ def test_sharded_graph_exchanges_on_the_gpu_one_rank_rccl():
         f = sg.gather_features(ids).float()
         ref = torch.where((ids >= 0).unsqueeze(1), g.features[ids.clamp(min=0)], torch.zeros((), device="cuda"))
         assert torch.equal(f, ref.float())
+        # the owners' full-neighbourhood expansion (HIP full_neighbors behind the exchange)
+        # = the whole graph's HIP expansion; the flow's blocks too
+        _full_flow_matches(g, sg, rows[:300])
         sg.check_overflow()
         torch.cuda.synchronize()
     finally:
         dist.destroy_process_group()
+
+
+def _full_flow_matches(g, sg, rows):
+    from euler_amd.dataflow.device_flow import DeviceFullFlow
+    from euler_amd.ops._native import hip
+
+    for mask in (1, 3):
+        o1 = torch.zeros(1, dtype=torch.int32, device=rows.device)
+        o2 = torch.zeros(1, dtype=torch.int32, device=rows.device)
+        a = sg.full_neighbors(rows, mask, 4096, o1)
+        b = hip().full_neighbors(g.indptr, g.nbr, g.num_rows, g.num_types, mask, rows.long(), 4096, o2)
+        for x, y in zip(a, b):
+            assert torch.equal(x.long(), y.long()), mask
+        assert int(o1) == 0 == int(o2)
+    f1 = DeviceFullFlow(sg, [3, 1], 32, True, "bounded")
+    f2 = DeviceFullFlow(g, [3, 1], 32, True, "bounded")
+    assert f1.caps == f2.caps
+    d1, d2 = f1.produce(rows[:32]), f2.produce(rows[:32])
+    for b1, b2 in zip(d1, d2):
+        assert torch.equal(b1.n_id, b2.n_id) and torch.equal(b1.edge_index, b2.edge_index)
+    assert not f1.overflowed()
 
 
 @pytest.mark.gpu
@@ -420,6 +444,36 @@ def test_sharded_sage_two_ranks_share_the_gpu_in_lockstep():
     assert len(res) == 2 and all(r[2] for r in res), res
 
 
+def _worker_shared_gpu_full(rank, world, port, q):
+    """2 ranks sharing the GPU (gloo, staged exchanges): the owners' HIP full-neighbourhood
+    expansion of each rank's rows and the flow's blocks = the whole graph's on the device"""
+    try:
+        os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                           "WORLD_SIZE": str(world), "LOCAL_RANK": "0"})
+        from euler_amd.graph.sharded_graph import ShardedDeviceGraph
+        from euler_amd.parallel import dp
+
+        dp.init_distributed(backend="gloo", device=torch.device("cuda", 0))
+        g, indptr, nbr, w, nw = _graph(device="cuda")
+        sg = ShardedDeviceGraph.from_full(g, node_weights=nw)
+        rows = torch.randint(0, g.num_rows, (300,), generator=torch.Generator().manual_seed(rank)).cuda()
+        _full_flow_matches(g, sg, rows)
+        sg.check_overflow()
+        q.put((rank, "shared_gpu_full", sg.local.num_rows < g.num_rows))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+
+
+@pytest.mark.gpu
+def test_sharded_full_flow_two_ranks_share_the_gpu():
+    res = _run(_worker_shared_gpu_full)
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == 2 and all(r[2] for r in res), res
+
+
 def _worker_engine_shard(rank, world, port, q, data):
     """each rank's engine loads only its partitions (shard_idx = rank); the sharded device
     graph built from them holds the same nodes, neighbour multisets, weights, features and
@@ -529,5 +583,103 @@ def test_estimator_on_per_rank_engine_shards(tmp_path):
                            make_current=False)
     e.save(data, partitions=4, threads=4)
     res = _run(_worker_engine_shard_estimator, data, str(tmp_path))
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == 2 and all(r[2] for r in res), res
+
+
+def _worker_full_flow(rank, world, port, q):
+    """the owners' full-neighbourhood expansion = the whole graph's, entry for entry; the
+    degree statistics and so the flow capacities = the whole graph's; a full-flow block
+    stack over the sharded rows = the whole graph's; a short cap flags the overflow"""
+    try:
+        _init(rank, world, port)
+        from euler_amd.dataflow.device_flow import DeviceFullFlow, bounded_caps, exact_caps, full_neighbors_cpu
+        from euler_amd.graph.sharded_graph import ShardedDeviceGraph
+
+        g, indptr, nbr, w, nw = _graph(seed=3)
+        sg = ShardedDeviceGraph.from_full(g, node_weights=nw)
+        ok = True
+        gen = torch.Generator().manual_seed(11 + rank)  # every rank asks for different rows
+        rows = torch.randint(0, g.num_rows, (90,), generator=gen)
+        rows[4], rows[9], rows[20] = -1, 7, rows[3]
+        for mask in (1, 2, 3):
+            o1, o2 = torch.zeros(1, dtype=torch.int32), torch.zeros(1, dtype=torch.int32)
+            a = sg.full_neighbors(rows, mask, 2048, o1)
+            b = full_neighbors_cpu(g, mask, rows, 2048, o2)
+            ok &= all(torch.equal(x.long(), y.long()) for x, y in zip(a, b)) and int(o1) == 0 == int(o2)
+            st = sg.degree_stats(mask, 17)
+            T = 2
+            seg = (indptr[1:] - indptr[:-1]).view(-1, T)
+            deg = sum(seg[:, t] for t in range(T) if (mask >> t) & 1)
+            ok &= st == (int(deg.max()), int(deg.sum()), int(torch.topk(deg, 17).values.min()))
+        # a cap below the expansion: flagged, the kept prefix equals the whole graph's
+        o1, o2 = torch.zeros(1, dtype=torch.int32), torch.zeros(1, dtype=torch.int32)
+        a = sg.full_neighbors(rows, 3, 64, o1)
+        b = full_neighbors_cpu(g, 3, rows, 64, o2)
+        ok &= int(o1) == 1 == int(o2) and all(torch.equal(x.long(), y.long()) for x, y in zip(a, b))
+        masks = [3, 1]
+        ok &= exact_caps(sg, masks, 24) == exact_caps(g, masks, 24)
+        ok &= bounded_caps(sg, masks, 24) == bounded_caps(g, masks, 24)
+        f1 = DeviceFullFlow(sg, masks, 24, True, "bounded")
+        f2 = DeviceFullFlow(g, masks, 24, True, "bounded")
+        roots = torch.randint(0, g.num_rows, (24,), generator=gen)
+        d1, d2 = f1.produce(roots), f2.produce(roots)
+        for b1, b2 in zip(d1, d2):
+            ok &= torch.equal(b1.n_id, b2.n_id) and torch.equal(b1.res_n_id, b2.res_n_id)
+            ok &= torch.equal(b1.edge_index, b2.edge_index) and b1.size == b2.size
+        ok &= not f1.overflowed()
+        sg.check_overflow()
+        q.put((rank, "full_flow", bool(ok)))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_full_neighbourhood_flow_equals_whole_graph(world):
+    res = _run(_worker_full_flow, world=world)
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == world and all(r[2] for r in res), res
+
+
+def _worker_full_flow_estimator(rank, world, port, q, tmp):
+    """NodeEstimator(device_graph_sharded=True) on a GCN (full-neighbourhood GCNDataFlow):
+    the sharded full-flow trainer trains on 2 ranks in lockstep holding half the rows"""
+    try:
+        _init(rank, world, port)
+        from euler_amd import models as Z
+        from euler_amd.dataset import get_dataset
+        from euler_amd.estimator import NodeEstimator
+        from euler_amd.models.full_trainer import ShardedFlowTrainer
+
+        ds = get_dataset("ppi", data_dir=os.path.join(tmp, "ppi"), scale=0.05)
+        ds.load_graph()
+        torch.manual_seed(0)
+        m = Z.SupervisedGNN("gcn", "full", [16, 16, ds.label_dim], [5, 3], [["train"], ["train"]], "feature",
+                            ds.feature_dim, "label", ds.label_dim, max_id=ds.max_node_id)
+        tnt = ds.train_node_type[0] if isinstance(ds.train_node_type, list) else ds.train_node_type
+        est = NodeEstimator(m, {"model_dir": os.path.join(tmp, "ckpt"), "batch_size": 16, "total_step": 6,
+                                "log_steps": 3, "device": "cpu", "device_graph": True, "device_graph_sharded": True,
+                                "train_node_type": tnt, "seed": 2, "device_feature_dtype": "fp32"})
+        res = est.train()
+        tr = est.device_trainer
+        allp = [torch.zeros_like(tr.flat.flat) for _ in range(world)]
+        dist.all_gather(allp, tr.flat.flat.detach().clone())
+        n = tr.graph.num_rows
+        ok = (isinstance(tr, ShardedFlowTrainer) and tr.device_trainer_kind == "sharded_full_flow"
+              and tr.graph.local.num_rows == len(range(rank, n, world)) and math.isfinite(res["loss"])
+              and all(torch.equal(x, allp[0]) for x in allp) and est.global_step == 6)
+        q.put((rank, "full_flow_estimator", bool(ok)))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_estimator_sharded_full_flow_two_ranks(tmp_path):
+    res = _run(_worker_full_flow_estimator, str(tmp_path))
     assert not [r for r in res if r[1] == "error"], res
     assert len(res) == 2 and all(r[2] for r in res), res
