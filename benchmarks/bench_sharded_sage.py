@@ -44,7 +44,10 @@ def main(argv=None):
     p.add_argument("--classes", type=int, default=64)
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--model", choices=["sage", "gcn"], default="sage")
+    p.add_argument("--model", choices=["sage", "gcn", "flow"], default="sage",
+                   help="sage: the fused tree step; gcn: GCNConv on full-neighbourhood blocks; flow: --conv on "
+                        "the sampled flow's blocks (ShardedFlowTrainer)")
+    p.add_argument("--conv", default="gcn", help="the convolution of --model flow")
     p.add_argument("--graph", action="store_true", help="capture the step (sampling exchanges included) in a hipGraph")
     p.add_argument("--force-comm", action="store_true",
                    help="one rank: run every exchange through a 1-rank RCCL group (the W > 1 code path)")
@@ -83,11 +86,23 @@ def main(argv=None):
     rank = dp.rank()
     t0 = time.time()
     gcn = args.model == "gcn"
+    generic = args.model != "sage"  # ShardedFlowTrainer (multi-label sigmoid loss)
     g = ShardedDeviceGraph.synthetic(args.num_nodes, args.avg_degree, feature_dim=args.feature_dim,
-                                     num_classes=args.classes, multi_label=gcn, seed=3, device=dev,
+                                     num_classes=args.classes, multi_label=generic, seed=3, device=dev,
                                      force_comm=args.force_comm)
     dims = [args.hidden] * len(args.fanouts) + [args.hidden]
-    if gcn:
+    if args.model == "flow":
+        from euler_amd import models as Z
+        from euler_amd.dataflow.device_flow import DeviceSageFlow
+        from euler_amd.models.full_trainer import ShardedFlowTrainer
+
+        torch.manual_seed(0)
+        L = len(args.fanouts)
+        m = Z.SupervisedGNN(args.conv, "sage", [args.hidden] * L + [args.classes], args.fanouts, [[0]] * L, "f",
+                            args.feature_dim, "l", args.classes, max_id=args.num_nodes).to(dev)
+        flow = DeviceSageFlow(g, [None] * L, args.fanouts, args.batch, True)
+        tr = ShardedFlowTrainer(m, g, args.batch, flow, learning_rate=0.01)
+    elif gcn:
         # the reference's SupervisedGCN shape: GCNConv layers on GCNDataFlow (full
         # neighbourhoods, self loops), sigmoid cross-entropy; one layer per --fanouts entry
         from euler_amd import models as Z
@@ -114,7 +129,7 @@ def main(argv=None):
             return 1.0 / world
     torch.cuda.synchronize()
     build_s = time.time() - t0
-    if args.graph and not (gcn and g.comm):  # full-flow exchanges read split sizes on the host
+    if args.graph and (not generic or tr.capturable()):  # full-flow exchanges read split sizes on the host
         tr.capture(sync, warmup=args.warmup, steps=1)
         run = tr.replay_steps
     else:
@@ -142,16 +157,16 @@ def main(argv=None):
         tr.flow.check()
     if rank == 0:
         print(json.dumps({
-            "metric": ("GCN" if gcn else "GraphSAGE") + " train samples/s on a row-sharded graph (whole job)",
+            "metric": {"gcn": "GCN", "sage": "GraphSAGE", "flow": f"{args.conv} (sampled flow)"}[args.model] + " train samples/s on a row-sharded graph (whole job)",
             "value": round(args.batch * world * args.steps / el, 1), "unit": "samples/s",
             "n_gpus": 1 if args.shared_gpu else world, "ranks": world,
             "shared_gpu_rehearsal": bool(args.shared_gpu) or None, "exchanges": bool(g.comm),
             "ms_per_step": round(el * 1e3 / args.steps, 3), "steps": args.steps, "warmup": args.warmup,
-            "loss": float(tr.loss.item()), "hipgraph": bool(args.graph) and tr._graphs != {} if gcn else bool(args.graph),
+            "loss": float(tr.loss.item()), "hipgraph": bool(tr._graphs) if generic else bool(args.graph),
             "build_s": round(build_s, 1), "flow_caps": tr.flow.caps if gcn else None,
             "graph_gib_per_gpu": round((g.nbytes() + g.features.shard.numel() * 2) / 2 ** 30, 2),
             "config": {"model": args.model, "num_nodes": args.num_nodes, "batch_per_gpu": args.batch,
-                       "fanouts": None if gcn else args.fanouts, "layers": len(args.fanouts),
+                       "fanouts": None if gcn else args.fanouts, "conv": args.conv if args.model == "flow" else None, "layers": len(args.fanouts),
                        "hidden": args.hidden, "feature_dim": args.feature_dim, "classes": args.classes},
             "data": "synthetic power-law graph generated in HBM, random features / labels"}), flush=True)
     if world > 1:

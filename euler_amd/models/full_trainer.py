@@ -30,6 +30,7 @@ from __future__ import annotations
 
 import numpy as np
 import torch
+import torch.distributed as dist
 import torch.nn.functional as F
 
 from euler_amd.dataflow.device_flow import DeviceFullFlow
@@ -224,8 +225,10 @@ class ShardedFlowTrainer(FullFlowTrainer):
     rows' owners over the all-to-all, the input features and the roots' labels fetched from
     their owners; the model's own convolutions, loss, backward, gradient all-reduce and the
     flat optimizer run as in :class:`FullFlowTrainer`.  HBM per rank holds 1/W of the CSR,
-    the features and the labels.  Steps with collectives inside run eagerly (one rank: the
-    step is captured as usual)."""
+    the features and the labels.  A ``GCNDataFlow`` model expands every hop through the
+    rows' owners (``ShardedDeviceGraph.full_neighbors``).  Sampled-flow steps over RCCL
+    capture into a hipGraph (fixed-size exchanges); full-flow and gloo steps run eagerly
+    (:meth:`capturable`)."""
 
     def __init__(self, model, graph, batch_size, flow, optimizer="adam", learning_rate=0.01):
         self.gnn = model.gnn
@@ -274,10 +277,22 @@ class ShardedFlowTrainer(FullFlowTrainer):
     infer_logits = None  # evaluate / infer of a sharded-graph job: the engine path
     infer_embed = None
 
+    def capturable(self) -> bool:
+        """one rank without exchanges, or RCCL exchanges of fixed sizes (the sampled flow's
+        routes, draws and feature rows capture like any kernel); the full-neighbourhood
+        flow's variable-size exchange reads its split sizes on the host, and gloo stages
+        through host memory: those steps run eagerly"""
+        from euler_amd.dataflow.device_flow import DeviceSageFlow
+
+        g = self.graph
+        if not g.comm:
+            return True
+        return isinstance(self.flow, DeviceSageFlow) and self.on_gpu and dist.get_backend(g.group) != "gloo"
+
     def capture(self, grad_sync=None, warmup: int = 2, steps: int = 1, extra_sizes=()):
-        if self.graph.world == 1 and not self.graph.comm:
+        if self.capturable():
             return super().capture(grad_sync, warmup, steps, extra_sizes)
-        for _ in range(int(warmup)):  # collectives in the step: eager
+        for _ in range(int(warmup)):  # host syncs in the step: eager
             self.step_count += 1
             self._step(grad_sync)
         self._grad_sync = grad_sync

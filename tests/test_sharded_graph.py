@@ -444,6 +444,62 @@ def test_sharded_sage_two_ranks_share_the_gpu_in_lockstep():
     assert len(res) == 2 and all(r[2] for r in res), res
 
 
+@pytest.mark.gpu
+def test_sharded_sampled_flow_captures_over_rccl():
+    """ShardedFlowTrainer on the sampled flow with its exchanges on a 1-rank RCCL group:
+    the step (routes, owner draws, feature / label exchanges, model, Adam) captures into a
+    hipGraph; the first captured replay's loss equals the eager step's from the same state
+    (fp32 scatter sums: to rounding), and replays train"""
+    import copy
+    import math
+
+    from test_parallel import _free_port
+
+    from euler_amd import models as Z
+    from euler_amd.dataflow.device_flow import DeviceSageFlow
+    from euler_amd.graph.sharded_graph import ShardedDeviceGraph
+    from euler_amd.models.full_trainer import ShardedFlowTrainer
+
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
+    tr = None
+    try:
+        g, indptr, nbr, w, nw = _graph(device="cuda")
+        g.labels = (g.features[:, :3] > 0).float()  # learnable from the root's own features
+        sg = ShardedDeviceGraph.from_full(g, force_comm=True, node_weights=nw)
+        torch.manual_seed(0)
+        m = Z.SupervisedGNN("gcn", "sage", [16, 16, 3], [4, 3], [[0], [0]], "f", 12, "l", 3, max_id=300).cuda()
+        tr = ShardedFlowTrainer(m, sg, 32, DeviceSageFlow(sg, [None, None], [4, 3], 32, True), learning_rate=0.03)
+        assert tr.capturable()
+        tr.step()
+        torch.cuda.synchronize()
+        rng, flat = sg.rng.clone(), tr.flat.flat.clone()
+        st = copy.deepcopy(tr.opt.state_dict())
+        tr.step()
+        eager_loss = float(tr.loss.item())
+        tr.capture(None, warmup=0, steps=1)
+        assert tr._graph_exec is not None
+        # back to the state before the eager step, then the same step as a replay
+        sg.rng.copy_(rng)
+        tr.flat.flat.copy_(flat)
+        tr.opt.load_state_dict(st)
+        tr.replay(1)
+        torch.cuda.synchronize()
+        first = float(tr.loss.item())
+        assert abs(first - eager_loss) <= 1e-5 * abs(eager_loss), (first, eager_loss)
+        losses = []
+        for _ in range(200):
+            tr.replay(1)
+            losses.append(tr.loss.clone())
+        losses = torch.stack(losses).float().cpu()
+        head, tail = float(losses[:20].mean()), float(losses[-20:].mean())
+        assert math.isfinite(tail) and tail < 0.97 * head, (head, tail)
+        sg.check_overflow()
+    finally:
+        if tr is not None:
+            tr.release_graphs()  # a graph holding RCCL work blocks destroy_process_group
+        dist.destroy_process_group()
+
+
 def _worker_shared_gpu_full(rank, world, port, q):
     """2 ranks sharing the GPU (gloo, staged exchanges): the owners' HIP full-neighbourhood
     expansion of each rank's rows and the flow's blocks = the whole graph's on the device"""
