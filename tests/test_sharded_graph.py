@@ -693,7 +693,7 @@ def _worker_full_flow(rank, world, port, q):
         q.put((rank, "error", traceback.format_exc()))
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_sharded_full_neighbourhood_flow_equals_whole_graph(world):
     res = _run(_worker_full_flow, world=world)
     assert not [r for r in res if r[1] == "error"], res
