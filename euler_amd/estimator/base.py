@@ -31,6 +31,7 @@ import time
 
 import numpy as np
 import torch
+import torch.distributed as dist
 import torch.nn as nn
 
 from euler_amd.parallel import dp
@@ -830,8 +831,6 @@ class BaseEstimator:
         one model function for train, eval and predict)"""
         if not self.params.get("device_graph") or self.params.get("device_infer", True) is False:
             return None
-        if self.params.get("device_graph_sharded"):
-            return None  # a row-sharded graph trains on the device; evaluate / infer: engine path
         tr = getattr(self, "device_trainer", None)
         if tr is None:
             from euler_amd.estimator.device_trainers import device_infers
@@ -848,6 +847,28 @@ class BaseEstimator:
             self.device_trainer = tr
         return tr if callable(getattr(tr, "infer_logits", None)) else None
 
+    def _lockstep_batches(self, tr, batches, extract):
+        """``(src, kwargs)`` per batch.  A trainer on a row-sharded graph answers inference
+        collectively (``collective_infer``: every batch crosses the ranks' exchanges), so all
+        ranks run the same number of batches of one padded size: the count is agreed over
+        the group (MAX) and a rank out of ids runs empty batches, whose rows are all padding
+        (``src`` None: nothing to record)."""
+        if not getattr(tr, "collective_infer", False):
+            for b in batches:
+                yield extract(b), {}
+            return
+        srcs = [extract(b) for b in batches]
+        n = torch.tensor([len(srcs)], dtype=torch.int64)
+        if dp.is_distributed():
+            n = n.to(self.device) if dist.get_backend() == "nccl" else n
+            dist.all_reduce(n, op=dist.ReduceOp.MAX)
+        pad = int(self.params["batch_size"])
+        for i in range(int(n.item())):
+            if i < len(srcs):
+                yield srcs[i], {"pad_to": pad}
+            else:
+                yield None, {"pad_to": pad}
+
     def _device_evaluate(self, tr):
         """loss and the model's streaming metric over the eval id batches, every batch's
         block / tree built and run on the device"""
@@ -858,10 +879,13 @@ class BaseEstimator:
             met.reset()
         name = getattr(self.model, "metric_name", getattr(tr, "metric_name", "f1"))
         losses, res, steps, n, t0 = [], {}, 0, 0, time.time()
-        for batch in self._eval_batches():
-            src = self.get_evaluate_from_input(batch, self.params)
+        extract = lambda b: self.get_evaluate_from_input(b, self.params)  # noqa: E731
+        for src, kw in self._lockstep_batches(tr, self._eval_batches(), extract):
+            if src is None:  # a padding batch of the collective loop
+                tr.infer_logits(torch.zeros(0, dtype=torch.int64), **kw)
+                continue
             try:
-                _, logits, y = tr.infer_logits(src)
+                _, logits, y = tr.infer_logits(src, **kw)
             except NotImplementedError:
                 return None
             losses.append(float(F.binary_cross_entropy_with_logits(logits, y.float())))
@@ -869,7 +893,7 @@ class BaseEstimator:
             res = {"loss": float(np.mean(losses)), name: float(value)}
             steps += 1
             n += int(torch.as_tensor(src).numel())
-            if self.evaluate_stop_onetime:
+            if self.evaluate_stop_onetime and not getattr(tr, "collective_infer", False):
                 break
         if self.rank == 0:
             log.info("evaluate: %s over %d batches (device path, %.1f nodes/s)", res, steps,
@@ -879,10 +903,13 @@ class BaseEstimator:
     def _device_infer(self, tr):
         ids_out, emb_out = [], []
         n, t0 = 0, time.time()
-        for batch in self.infer_input_fn():
-            src = self.get_infer_from_input(batch, self.params)
+        extract = lambda b: self.get_infer_from_input(b, self.params)  # noqa: E731
+        for src, kw in self._lockstep_batches(tr, self.infer_input_fn(), extract):
+            if src is None:  # a padding batch of the collective loop
+                tr.infer_embed(torch.zeros(0, dtype=torch.int64), **kw)
+                continue
             try:
-                emb = tr.infer_embed(src)
+                emb = tr.infer_embed(src, **kw)
             except NotImplementedError:
                 return None
             s, e = self.transfer_embedding(src, emb)

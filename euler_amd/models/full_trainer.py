@@ -274,8 +274,62 @@ class ShardedFlowTrainer(FullFlowTrainer):
         self._samples = roots
         return loss
 
-    infer_logits = None  # evaluate / infer of a sharded-graph job: the engine path
-    infer_embed = None
+    # evaluate / infer on the device, collectively: every rank calls with batches of the same
+    # padded size in lockstep (estimator/base.py _lockstep_batches)
+    collective_infer = True
+
+    def _sharded_infer_flow(self, n):
+        """the training flow's kind at ``n`` roots (cached): the sampled flow as trained, the
+        full flow on degree-statistics caps grown on overflow (exact caps at hundreds of
+        millions of rows would reach the whole edge set)"""
+        from euler_amd.dataflow.device_flow import DeviceFullFlow, DeviceSageFlow
+
+        cache = self.__dict__.setdefault("_infer_flows", {})
+        if n not in cache:
+            f = self.flow
+            if isinstance(f, DeviceSageFlow):
+                cache[n] = DeviceSageFlow(self.graph, f.edge_types, f.fanouts, n, f.self_loops)
+            else:
+                cache[n] = DeviceFullFlow(self.graph, f.masks, n, f.self_loops, "bounded")
+        return cache[n]
+
+    @torch.no_grad()
+    def infer_logits(self, ids, pad_to=None):
+        """(embeddings [n, E], logits [n, C], labels [n, C]) of raw node ids on the sharded
+        graph: the rows' blocks built through the owners (sampled as in training, or full
+        neighbourhoods), features and labels over the exchanges.  Collective: every rank
+        calls it with the same ``pad_to`` (rows padded with -1, which touch nothing)."""
+        g = self.graph
+        rows = g.rows_of(ids).to(g.device).long().reshape(-1)
+        n = rows.numel()
+        B = max(n, int(pad_to or 0), 1)
+        if B > n:
+            rows = torch.cat([rows, torch.full((B - n,), -1, dtype=torch.long, device=rows.device)])
+        flow = self._sharded_infer_flow(B)
+        self.model.eval()
+        try:
+            while True:
+                emb, _ = full_flow_embed(self.gnn, flow, g.gather_features, rows)
+                if not callable(getattr(flow, "grow", None)):
+                    break
+                over = torch.tensor([int(flow.overflowed())], dtype=torch.int64)
+                if g.comm:  # every rank regrows together
+                    from euler_amd.parallel import comm
+
+                    over = over.to(g.device)
+                    comm.all_reduce(over, dist.ReduceOp.MAX, group=g.group)
+                if not int(over.item()):
+                    break
+                flow.grow(2.0)
+            logits = self.model.out_fc(emb).float()
+        finally:
+            self.model.train()
+        g.advance()  # the next batch (and training) draw from fresh counters
+        y = g.gather_labels(rows).float()
+        return emb[:n].float(), logits[:n], y[:n]
+
+    def infer_embed(self, ids, pad_to=None):
+        return self.infer_logits(ids, pad_to)[0]
 
     def capturable(self) -> bool:
         """one rank without exchanges, or RCCL exchanges of fixed sizes (the sampled flow's

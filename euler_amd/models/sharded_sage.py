@@ -17,8 +17,9 @@ the tree is drawn across the ranks before the forward — the reference's distri
   head reads it through roots 0 .. B-1 (TreePlan ``label_rows``).
 
 Forward, head, backward, split-K dW, gradient all-reduce and the optimizer are the
-whole-graph trainer's launches unchanged.  Evaluate / infer of such a job run on the
-engine path.
+whole-graph trainer's launches unchanged.  Evaluate / infer run on the device too, with the
+ranks in lockstep (:meth:`ShardedSageTrainer.infer_logits`; the engine of an
+``engine_shards`` job holds only its own partitions, so it could not answer them).
 """
 from __future__ import annotations
 
@@ -33,8 +34,9 @@ _STREAM0 = 40  # Philox streams of the tree draws (roots 40, hop k: 41 + k)
 
 
 class ShardedSageTrainer(SageTrainer):
-    infer_logits = None  # evaluate / infer: the engine path
-    infer_embed = None
+    # evaluate / infer on the device, collectively: every rank calls with batches of the same
+    # padded size in lockstep (estimator/base.py _lockstep_batches)
+    collective_infer = True
 
     def __init__(self, graph, batch_size, fanouts, dims, label_dim, **kw):
         self.sgraph = graph
@@ -141,6 +143,48 @@ class ShardedSageTrainer(SageTrainer):
             self._dist_backward(grad_sync, False)
         self._primed = False
         self._gathered = False
+
+    # ------------------------------------------------------------------ inference
+    @torch.no_grad()
+    def infer_logits(self, ids, pad_to=None):
+        """(embeddings [n, E], logits [n, C], labels [n, C]) of raw node ids: a fresh tree
+        per root drawn through the owners (Philox streams 8.., training's untouched), the
+        features over the exchange and the fp32 model on the trained parameters (the
+        whole-graph trainer's ``infer_logits`` on the sharded graph).  Collective: every rank
+        calls it with the same ``pad_to`` (rows padded with -1, which touch nothing)."""
+        g = self.sgraph
+        rows = g.rows_of(ids).to(self.device).long().reshape(-1)
+        n = rows.numel()
+        B = max(n, int(pad_to or 0), 1)
+        if B > n:
+            rows = torch.cat([rows, torch.full((B - n,), -1, dtype=torch.long, device=rows.device)])
+        level = rows.int()
+        for k in range(1, self.L):
+            f, P = self.fanouts[k - 1], 1 << self.logP[k]
+            nb = g.sample_neighbor(level, f, self._types(self.masks[k - 1]), -1, stream_id=7 + k).view(-1, f)
+            slots = torch.full((level.numel(), P), -1, dtype=torch.int32, device=level.device)
+            slots[:, :f] = nb
+            slots[:, f] = level
+            level = slots.view(-1)
+        leaf = g.sample_neighbor(level, self.fanouts[-1], self._types(self.masks[-1]), -1,
+                                 stream_id=7 + self.L).view(-1, self.fanouts[-1])
+        g.advance()
+        params = {k: v.float() for k, v in self.logical_params().items()}
+        nodes, leaf = level.long(), leaf.long()
+        if self.fshard is not None:
+            pos = self.fshard.exchange(torch.cat([nodes, leaf.reshape(-1)])).long()
+            emb = self.logical_embed(params, pos[: nodes.numel()], pos[nodes.numel():].view_as(leaf),
+                                     self.fshard.cache)
+        else:
+            emb = self.logical_embed(params, nodes, leaf)
+        logits = emb @ params["out_fc.weight"].t().to(emb.device)
+        y = self._batch_labels(rows if g.comm else rows.clamp(min=0))  # -1 rows: zeros over the exchange
+        if self._class_labels:
+            y = torch.zeros((B, self.C), dtype=torch.float32, device=y.device).scatter_(1, y.long().view(-1, 1), 1.0)
+        return emb[:n], logits[:n], y[:n].float().to(emb.device)
+
+    def infer_embed(self, ids, pad_to=None):
+        return self.infer_logits(ids, pad_to)[0]
 
     def _labels_of(self, roots):
         """the last drawn batch's labels [B, C] (fp32; the batch's roots are rows 0 .. B-1

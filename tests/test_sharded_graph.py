@@ -208,6 +208,21 @@ def _worker_estimator(rank, world, port, q, tmp):
         _, est2 = runner.build(a2)
         est2.train()
         ok &= est2.global_step == 12
+        # evaluate / infer on the device in lockstep (batches of 32: rank 0 gets 32 + 16, rank 1 32)
+        import euler_amd.ops.graph_api as ge
+
+        ids = torch.as_tensor(ge.sample_node(80, -1)).reshape(-1)
+        dist.broadcast(ids, 0)
+        idf = os.path.join(tmp, "ids.txt")
+        if rank == 0:
+            with open(idf, "w") as f:
+                f.write("\n".join(str(int(i)) for i in ids.tolist()))
+        dist.barrier()
+        est2.params["id_file"] = idf
+        ev = est2.evaluate()
+        est2.params["infer_dir"] = os.path.join(tmp, "infer")
+        out_ids, embs = est2.infer()
+        ok &= math.isfinite(ev["loss"]) and embs.shape[0] == (48 if rank == 0 else 32) == len(out_ids)
         # another convolution on the sampled flow: the generic trainer over the sharded graph
         ds = get_dataset("ppi", data_dir=os.path.join(tmp, "ppi2"), scale=0.05)
         ds.load_graph()
@@ -255,6 +270,17 @@ def test_one_rank_sharded_sage_trainer_equals_sage_trainer_cpu():
     assert la == lb, (la, lb)
     pa, pb = a.logical_params(), b.logical_params()
     assert all(torch.equal(pa[k], pb[k]) for k in pa)
+    # device inference (the estimator's evaluate / infer): same tree draws, same model
+    ids = torch.arange(0, 300, 7)
+    r1 = loc.rng.clone()
+    loc.reseed_cpu()
+    ea, xa, ya = a.infer_logits(ids)
+    loc.rng.copy_(r1)
+    loc.reseed_cpu()
+    eb, xb, yb = b.infer_logits(ids)
+    assert torch.allclose(xa, xb, atol=1e-5) and torch.equal(ya, yb) and torch.allclose(ea, eb, atol=1e-5)
+    ep, xp, yp = a.infer_logits(ids, pad_to=64)  # padded rows touch nothing
+    assert xp.shape == xa.shape and bool(torch.isfinite(xp).all()) and torch.equal(yp, ya)
 
 
 @pytest.mark.gpu
@@ -359,6 +385,9 @@ def test_sharded_sage_trainer_gpu_matches_bf16_oracle():
         torch.cuda.synchronize()
         last = float(tr.loss.item())
         assert math.isfinite(last) and last < first, (first, last)
+        emb, logits, y = tr.infer_logits(torch.arange(0, 300, 7), pad_to=64)
+        assert logits.shape == (43, 5) and bool(torch.isfinite(logits).all())
+        assert torch.equal(y.cpu(), g.labels[torch.arange(0, 300, 7)].cpu())
         sg.check_overflow()
     finally:
         dist.destroy_process_group()
@@ -493,6 +522,11 @@ def test_sharded_sampled_flow_captures_over_rccl():
         losses = torch.stack(losses).float().cpu()
         head, tail = float(losses[:20].mean()), float(losses[-20:].mean())
         assert math.isfinite(tail) and tail < 0.97 * head, (head, tail)
+        # device inference through the RCCL exchanges (the estimator's collective evaluate)
+        tr.release_graphs()
+        emb, logits, y = tr.infer_logits(torch.arange(0, 300, 11), pad_to=64)
+        assert logits.shape == (28, 3) and bool(torch.isfinite(logits).all())
+        assert torch.equal(y.cpu(), g.labels[torch.arange(0, 300, 11)].cpu())
         sg.check_overflow()
     finally:
         if tr is not None:
@@ -623,6 +657,20 @@ def _worker_engine_shard_estimator(rank, world, port, q, data, tmp):
         dist.all_gather(allp, flat)
         ok = isinstance(tr, ShardedSageTrainer) and all(torch.equal(x, allp[0]) for x in allp)
         ok &= est.global_step == 6 and math.isfinite(res["loss"]) and tr.sgraph.local.num_rows < 3000
+        # evaluate / infer: this rank's engine holds half of the graph, the device path reaches
+        # every id through the owners (ids of both halves in every batch)
+        idf = os.path.join(tmp, "ids.txt")
+        if rank == 0:
+            with open(idf, "w") as f:
+                f.write("\n".join(str(i) for i in range(0, 3000, 37)))
+        dist.barrier()
+        est.params["id_file"] = idf
+        ev = est.evaluate()
+        est.params["infer_dir"] = os.path.join(tmp, "infer")
+        out_ids, embs = est.infer()
+        rows = tr.sgraph.rows_of(torch.as_tensor(out_ids))
+        ok &= math.isfinite(ev["loss"]) and embs.shape[0] == (50 if rank == 0 else 32) == len(out_ids)
+        ok &= bool((rows >= 0).all()) and bool(np.isfinite(embs).all()) and bool((np.abs(embs).sum(1) > 0).all())
         q.put((rank, "engine_shard_est", bool(ok)))
         dist.destroy_process_group()
     except Exception:  # pragma: no cover
@@ -727,7 +775,47 @@ def _worker_full_flow_estimator(rank, world, port, q, tmp):
         ok = (isinstance(tr, ShardedFlowTrainer) and tr.device_trainer_kind == "sharded_full_flow"
               and tr.graph.local.num_rows == len(range(rank, n, world)) and math.isfinite(res["loss"])
               and all(torch.equal(x, allp[0]) for x in allp) and est.global_step == 6)
-        q.put((rank, "full_flow_estimator", bool(ok)))
+        # device inference through the owners = the whole graph's full-neighbourhood blocks
+        # on the same parameters (each rank its own ids, padded to one size, in lockstep)
+        from euler_amd.dataflow.device_flow import DeviceFullFlow
+        from euler_amd.graph.device_graph import DeviceGraph
+        from euler_amd.models.full_trainer import full_flow_embed
+
+        import euler_amd.ops.graph_api as ge
+
+        all_ids = ge.sample_node(40, tnt)  # the engine holds the whole graph in this test
+        all_ids = torch.as_tensor(all_ids).reshape(-1)
+        dist.broadcast(all_ids, 0)
+        mine = all_ids[:13] if rank == 0 else all_ids[13:40]
+        emb, logits, y = tr.infer_logits(mine, pad_to=32)
+        whole = DeviceGraph.from_engine(features=["feature"], feature_dims=[ds.feature_dim], label="label",
+                                        label_dim=ds.label_dim, feature_dtype=torch.float32, device="cpu")
+        rows = whole.rows_of(mine)
+        tr.model.eval()
+        with torch.no_grad():
+            ref_emb, _ = full_flow_embed(tr.gnn, DeviceFullFlow(whole, tr.flow.masks, rows.numel(), tr.flow.self_loops,
+                                                                "exact"), whole.features, rows)
+            ref_logits = tr.model.out_fc(ref_emb).float()
+        tr.model.train()
+        chk = {"train": bool(ok), "shape": logits.shape == (mine.numel(), ds.label_dim),
+               "logits": float((logits - ref_logits).abs().max()) if logits.shape == ref_logits.shape else -1.0,
+               "labels": torch.equal(y, whole.labels[rows].float())}
+        ok &= chk["shape"] and chk["logits"] <= 1e-4 * max(1.0, float(ref_logits.abs().max())) and chk["labels"]
+        # estimator evaluate / infer over an id file whose batches differ in count per rank
+        idf = os.path.join(tmp, "ids.txt")
+        if rank == 0:
+            with open(idf, "w") as f:
+                f.write("\n".join(str(int(i)) for i in all_ids.tolist()))
+        dist.barrier()
+        est.params["id_file"] = idf
+        ev = est.evaluate()
+        chk["eval"] = ev
+        ok &= math.isfinite(ev["loss"])
+        est.params["infer_dir"] = os.path.join(tmp, "infer")
+        ids_out, embs = est.infer()
+        chk["infer"] = (tuple(embs.shape), len(ids_out))
+        ok &= embs.shape[0] == (24 if rank == 0 else 16) and embs.shape[0] == len(ids_out)  # batches 16+8 / 16
+        q.put((rank, "full_flow_estimator", bool(ok), chk))
         dist.destroy_process_group()
     except Exception:  # pragma: no cover
         import traceback
