@@ -845,7 +845,8 @@ class BaseEstimator:
                 return None
             self._device_restore(tr)
             self.device_trainer = tr
-        return tr if callable(getattr(tr, "infer_logits", None)) else None
+        return tr if callable(getattr(tr, "infer_logits", None)) or callable(getattr(tr, "infer_embed", None)) \
+            else None
 
     def _lockstep_batches(self, tr, batches, extract):
         """``(src, kwargs)`` per batch.  A trainer on a row-sharded graph answers inference
@@ -933,7 +934,7 @@ class BaseEstimator:
     @torch.no_grad()
     def evaluate(self):
         tr = self._device_inference_trainer()
-        if tr is not None:
+        if tr is not None and callable(getattr(tr, "infer_logits", None)):
             res = self._device_evaluate(tr)
             if res is not None:
                 return res
@@ -970,7 +971,7 @@ class BaseEstimator:
     @torch.no_grad()
     def infer(self):
         tr = self._device_inference_trainer()
-        if tr is not None:
+        if tr is not None and callable(getattr(tr, "infer_embed", None)):
             out = self._device_infer(tr)
             if out is not None:
                 return out

@@ -144,12 +144,24 @@ def build_device_trainer(est, model, first):
                           f"; {type(model).__name__} is none of them")
 
 
-def sharded_supported(model) -> bool:
-    """supervised models on the sampled ``SageDataFlow`` or the full-neighbourhood
-    ``GCNDataFlow`` (any convolution, no stores)"""
+def _sharded_unsup(model) -> bool:
+    """UnsupervisedGraphSage: two 2-hop SAGEConv towers on SageDataFlow"""
+    from euler_amd.convolution.convs import SAGEConv
     from euler_amd.dataflow import dataflows as D
 
     gnn = getattr(model, "gnn", None)
+    return (_is_unsup_gnn(model) and isinstance(getattr(gnn, "sampler", None), D.SageDataFlow)
+            and len(gnn.convs) == 2 and all(isinstance(c, SAGEConv) for c in gnn.convs))
+
+
+def sharded_supported(model) -> bool:
+    """supervised models on the sampled ``SageDataFlow`` or the full-neighbourhood
+    ``GCNDataFlow`` (any convolution, no stores), and the unsupervised 2-hop GraphSAGE"""
+    from euler_amd.dataflow import dataflows as D
+
+    gnn = getattr(model, "gnn", None)
+    if _sharded_unsup(model):
+        return True
     return (gnn is not None and hasattr(gnn, "feature_idx") and hasattr(model, "label_idx")
             and not hasattr(model, "context_gnn") and not has_store_encoder(model)
             and isinstance(getattr(gnn, "sampler", None), (D.SageDataFlow, D.GCNDataFlow)))
@@ -164,7 +176,7 @@ def build_sharded_trainer(est, model, first):
 
     if not sharded_supported(model):
         raise NoDeviceTrainer("device_graph_sharded=True trains supervised models on the sampled SageDataFlow or "
-                              "the full-neighbourhood GCNDataFlow; "
+                              "the full-neighbourhood GCNDataFlow, and the unsupervised GraphSAGE; "
                               f"{type(model).__name__} is not one")
     est._prepare(first, build_optimizer=False)
     c = Ctx(est, model)
@@ -173,6 +185,22 @@ def build_sharded_trainer(est, model, first):
     # shard_idx = rank, shard_num = W): host memory per rank is 1/W of the graph
     build = ShardedDeviceGraph.from_engine_shard if est.params.get("device_graph_sharded") == "engine_shards" \
         else ShardedDeviceGraph.from_engine
+    if _sharded_unsup(model):
+        # UnsupervisedGraphSage: both towers' trees, the positives and the negatives drawn
+        # through the owners (models/sharded_unsup.py); one rank without collectives: the
+        # whole-graph fused trainer
+        from euler_amd.models.sage_tower import UnsupSageTrainer
+        from euler_amd.models.sharded_unsup import ShardedUnsupSageTrainer
+
+        g = build(node_type=c.node_type(-1), features=gnn.feature_idx, feature_dims=gnn.feature_dim,
+                  feature_dtype=c.feature_dtype(), seed=c.seed * 7919 + est.rank, device=est.device)
+        if not g.comm:
+            tr = UnsupSageTrainer.from_model(model, g.local, c.batch, **c.opt_kw())
+            tr.device_trainer_kind = "unsupervised_graphsage"
+            return tr
+        tr = ShardedUnsupSageTrainer.from_model(model, g, c.batch, **c.opt_kw())
+        tr.device_trainer_kind = "sharded_unsupervised_graphsage"
+        return tr
     g = build(node_type=c.node_type(-1), features=gnn.feature_idx, feature_dims=gnn.feature_dim,
               label=model.label_idx, label_dim=model.label_dim, feature_dtype=c.feature_dtype(),
               seed=c.seed * 7919 + est.rank, device=est.device)

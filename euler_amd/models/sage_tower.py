@@ -114,6 +114,8 @@ class _Tower:
 
 
 class UnsupSageTrainer:
+    _device_towers = True
+
     def __init__(self, graph, batch_size, fanouts, dims, features=None, num_negs=5, pos_edge_types=None,
                  metapath=None, add_self_loops=False, optimizer="adam", learning_rate=0.01, init=None, init_seed=0,
                  fused=True):
@@ -161,9 +163,11 @@ class UnsupSageTrainer:
         self.load_logical(logical)
         self.opt = FlatOptimizer(self.flat, optimizer, learning_rate)
         R = {"gnn": self.B, "context_gnn": self.B * (1 + self.K)}
+        # the towers' in-kernel samplers read a whole CSR in HBM (a row-sharded graph's
+        # trainer draws its trees across the ranks instead: models/sharded_unsup.py)
         self.towers = {t: _Tower(graph, self.features, R[t], self.fanouts[0], self.fanouts[1], self.Hp[0],
                                  self.masks, self.include_self, self.params[f"{t}.W0"], self.device)
-                       for t in ("gnn", "context_gnn")}
+                       for t in ("gnn", "context_gnn")} if self._device_towers else {}
         self.loss_out = torch.zeros((), device=self.device)
         self.mrr_sum = torch.zeros((), device=self.device)
         self.mrr_n = 0
@@ -172,7 +176,7 @@ class UnsupSageTrainer:
         self._graphs = {}
         self._samples = None
         self.pair = None
-        if self.device.type == "cuda" and fused and _FUSED:
+        if self.device.type == "cuda" and fused and _FUSED and self.towers:
             try:
                 self._build_pair(optimizer)
             except RuntimeError as e:  # shapes the pair head does not take (LDS): per-op step
@@ -370,9 +374,10 @@ class UnsupSageTrainer:
         return nodes, leaf
 
     # ------------------------------------------------------------------ model
-    def _tower_reference(self, W0, nodes, leaf):
-        """fp32 A1 rows of a tower from its sampled tree (oracle / CPU path)"""
-        x = self.features.float()
+    def _tower_reference(self, W0, nodes, leaf, table=None):
+        """fp32 A1 rows of a tower from its sampled tree (oracle / CPU path); ``table``: the
+        feature rows ``nodes`` / ``leaf`` index (default the trainer's feature table)"""
+        x = (self.features if table is None else table).float()
         x = torch.cat([x, torch.zeros(1, x.shape[1], device=x.device)], 0)
         n = x.shape[0] - 1
         nodes, leaf = nodes.to(x.device).long(), leaf.to(x.device).long()

@@ -534,6 +534,58 @@ def test_sharded_sampled_flow_captures_over_rccl():
         dist.destroy_process_group()
 
 
+@pytest.mark.gpu
+def test_sharded_unsup_captures_over_rccl():
+    """the sharded unsupervised GraphSAGE step with its exchanges on a 1-rank RCCL group
+    captures into a hipGraph; the first replay's loss equals the eager step's from the same
+    state; replays train (mean reciprocal rank rises); collective device embeddings"""
+    import copy
+
+    from test_parallel import _free_port
+
+    from euler_amd.graph.sharded_graph import ShardedDeviceGraph
+    from euler_amd.models.sharded_unsup import ShardedUnsupSageTrainer
+
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
+    tr = None
+    try:
+        g, indptr, nbr, w, nw = _graph(device="cuda")
+        sg = ShardedDeviceGraph.from_full(g, force_comm=True, node_weights=nw)
+        tr = ShardedUnsupSageTrainer(sg, 64, [4, 3], [32, 32, 16], num_negs=3, pos_edge_types=[0],
+                                     metapath=[[0, 1], [1]], learning_rate=0.01, init_seed=3)
+        assert tr.fshard is not None and tr.capturable()
+        tr.step()
+        torch.cuda.synchronize()
+        rng, flat = sg.rng.clone(), tr.flat.flat.clone()
+        st = copy.deepcopy(tr.opt.state_dict())
+        tr.step()
+        eager_loss = float(tr.loss.item())
+        tr.capture(None, warmup=0, steps=1)
+        sg.rng.copy_(rng)
+        tr.flat.flat.copy_(flat)
+        tr.opt.load_state_dict(st)
+        tr.replay(1)
+        torch.cuda.synchronize()
+        first = float(tr.loss.item())
+        assert abs(first - eager_loss) <= 1e-5 * abs(eager_loss), (first, eager_loss)
+        tr.reset_metric()
+        tr.replay(20)
+        m0 = tr.metric()
+        tr.replay(300)
+        tr.reset_metric()
+        tr.replay(20)
+        m1 = tr.metric()
+        assert m1 > m0, (m0, m1)
+        tr.release_graphs()
+        e = tr.infer_embed(torch.arange(0, 300, 7), pad_to=64)
+        assert e.shape == (43, 16) and bool(torch.isfinite(e).all())
+        sg.check_overflow()
+    finally:
+        if tr is not None:
+            tr.release_graphs()
+        dist.destroy_process_group()
+
+
 def _worker_shared_gpu_full(rank, world, port, q):
     """2 ranks sharing the GPU (gloo, staged exchanges): the owners' HIP full-neighbourhood
     expansion of each rank's rows and the flow's blocks = the whole graph's on the device"""
@@ -825,5 +877,78 @@ def _worker_full_flow_estimator(rank, world, port, q, tmp):
 
 def test_estimator_sharded_full_flow_two_ranks(tmp_path):
     res = _run(_worker_full_flow_estimator, str(tmp_path))
+    assert not [r for r in res if r[1] == "error"], res
+    assert len(res) == 2 and all(r[2] for r in res), res
+
+
+def test_one_rank_sharded_unsup_equals_unsup_trainer_cpu():
+    """one rank: unsupervised GraphSAGE with every draw through the sharded graph = the
+    whole-graph trainer's torch twin (same draws in the same order), 5 steps"""
+    from euler_amd.graph.sharded_graph import ShardedDeviceGraph
+    from euler_amd.models.sage_tower import UnsupSageTrainer
+    from euler_amd.models.sharded_unsup import ShardedUnsupSageTrainer
+
+    g, _, _, _, nw = _graph()
+    sg = ShardedDeviceGraph.from_full(g, node_weights=nw)
+    loc = sg.local
+    kw = dict(num_negs=3, pos_edge_types=[0], metapath=[[0, 1], [1]], learning_rate=0.01, init_seed=3)
+    a = ShardedUnsupSageTrainer(sg, 32, [4, 3], [16, 16, 8], **kw)
+    assert a.fshard is None and not a.towers
+    b = UnsupSageTrainer(loc, 32, [4, 3], [16, 16, 8], features=loc.features, **kw)
+    r0 = loc.rng.clone()
+    la = [float(a.step()) for _ in range(5)]
+    loc.rng.copy_(r0)
+    lb = [float(b.step()) for _ in range(5)]
+    assert la == lb, (la, lb)
+    pa, pb = a.logical_params(), b.logical_params()
+    assert all(torch.equal(pa[k], pb[k]) for k in pa)
+    assert a.metric() == b.metric()
+    e = a.infer_embed(torch.arange(0, 300, 7), pad_to=64)
+    assert e.shape == (43, 8) and bool(torch.isfinite(e).all())
+
+
+def _worker_unsup_estimator(rank, world, port, q, tmp):
+    """runner graphsage_unsup --device_graph_sharded: the sharded unsupervised trainer on 2
+    ranks holding half the rows each, in lockstep; collective device infer"""
+    try:
+        _init(rank, world, port)
+        from euler_amd.models.sharded_unsup import ShardedUnsupSageTrainer
+        from euler_amd.tools import runner
+
+        flags = ["--dataset", "cora", "--batch_size", "32", "--log_steps", "4", "--model_dir",
+                 os.path.join(tmp, "ckpt"), "--device_graph_sharded", "--device", "cpu", "--seed", "1",
+                 "--fanouts", "5", "3", "--device_feature_dtype", "fp32", "--total_step", "8"]
+        a = runner.parse_args(flags, model="graphsage_unsup")
+        _, est = runner.build(a)
+        res = est.train()
+        tr = est.device_trainer
+        allp = [torch.zeros_like(tr.flat.flat) for _ in range(world)]
+        dist.all_gather(allp, tr.flat.flat.detach().clone())
+        n = tr.sgraph.num_rows
+        ok = (isinstance(tr, ShardedUnsupSageTrainer) and tr.sgraph.local.num_rows == len(range(rank, n, world))
+              and all(torch.equal(x, allp[0]) for x in allp) and est.global_step == 8 and math.isfinite(res["loss"]))
+        idf = os.path.join(tmp, "ids.txt")
+        if rank == 0:
+            with open(idf, "w") as f:
+                f.write("\n".join(str(i) for i in range(0, 80)))
+        dist.barrier()
+        est.params["id_file"] = idf
+        est.params["infer_dir"] = os.path.join(tmp, "infer")
+        calls = []
+        orig = tr.infer_embed
+        tr.infer_embed = lambda ids, **kw: calls.append(kw) or orig(ids, **kw)  # the device path answers
+        out_ids, embs = est.infer()
+        ok &= embs.shape[0] == (48 if rank == 0 else 32) == len(out_ids) and bool(np.isfinite(embs).all())
+        ok &= len(calls) == 2 and all(c == {"pad_to": 32} for c in calls)  # rank 1 runs a padding batch
+        q.put((rank, "unsup_estimator", bool(ok)))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_estimator_sharded_unsup_two_ranks(tmp_path):
+    res = _run(_worker_unsup_estimator, str(tmp_path))
     assert not [r for r in res if r[1] == "error"], res
     assert len(res) == 2 and all(r[2] for r in res), res
