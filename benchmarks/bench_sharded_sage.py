@@ -44,9 +44,11 @@ def main(argv=None):
     p.add_argument("--classes", type=int, default=64)
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--model", choices=["sage", "gcn", "flow"], default="sage",
+    p.add_argument("--model", choices=["sage", "gcn", "flow", "unsup"], default="sage",
                    help="sage: the fused tree step; gcn: GCNConv on full-neighbourhood blocks; flow: --conv on "
-                        "the sampled flow's blocks (ShardedFlowTrainer)")
+                        "the sampled flow's blocks (ShardedFlowTrainer); unsup: unsupervised GraphSAGE "
+                        "(ShardedUnsupSageTrainer, --negs negatives per source)")
+    p.add_argument("--negs", type=int, default=5)
     p.add_argument("--conv", default="gcn", help="the convolution of --model flow")
     p.add_argument("--graph", action="store_true", help="capture the step (sampling exchanges included) in a hipGraph")
     p.add_argument("--force-comm", action="store_true",
@@ -86,12 +88,20 @@ def main(argv=None):
     rank = dp.rank()
     t0 = time.time()
     gcn = args.model == "gcn"
-    generic = args.model != "sage"  # ShardedFlowTrainer (multi-label sigmoid loss)
+    generic = args.model in ("gcn", "flow")  # ShardedFlowTrainer (multi-label sigmoid loss)
+    unsup = args.model == "unsup"
     g = ShardedDeviceGraph.synthetic(args.num_nodes, args.avg_degree, feature_dim=args.feature_dim,
                                      num_classes=args.classes, multi_label=generic, seed=3, device=dev,
                                      force_comm=args.force_comm)
     dims = [args.hidden] * len(args.fanouts) + [args.hidden]
-    if args.model == "flow":
+    if args.model == "unsup":
+        from euler_amd.models.sharded_unsup import ShardedUnsupSageTrainer
+
+        if len(args.fanouts) != 2:
+            raise SystemExit("--model unsup trains 2-hop towers")
+        tr = ShardedUnsupSageTrainer(g, args.batch, args.fanouts, [args.hidden, args.hidden, args.classes],
+                                     num_negs=args.negs, learning_rate=0.01, init_seed=0)
+    elif args.model == "flow":
         from euler_amd import models as Z
         from euler_amd.dataflow.device_flow import DeviceSageFlow
         from euler_amd.models.full_trainer import ShardedFlowTrainer
@@ -129,7 +139,7 @@ def main(argv=None):
             return 1.0 / world
     torch.cuda.synchronize()
     build_s = time.time() - t0
-    if args.graph and (not generic or tr.capturable()):  # full-flow exchanges read split sizes on the host
+    if args.graph and (args.model == "sage" or tr.capturable()):  # full-flow exchanges read split sizes on the host
         tr.capture(sync, warmup=args.warmup, steps=1)
         run = tr.replay_steps
     else:
@@ -157,16 +167,18 @@ def main(argv=None):
         tr.flow.check()
     if rank == 0:
         print(json.dumps({
-            "metric": {"gcn": "GCN", "sage": "GraphSAGE", "flow": f"{args.conv} (sampled flow)"}[args.model] + " train samples/s on a row-sharded graph (whole job)",
+            "metric": {"gcn": "GCN", "sage": "GraphSAGE", "flow": f"{args.conv} (sampled flow)",
+                       "unsup": "unsupervised GraphSAGE (sources; 1 + negs contexts each)"}[args.model] + " train samples/s on a row-sharded graph (whole job)",
             "value": round(args.batch * world * args.steps / el, 1), "unit": "samples/s",
             "n_gpus": 1 if args.shared_gpu else world, "ranks": world,
             "shared_gpu_rehearsal": bool(args.shared_gpu) or None, "exchanges": bool(g.comm),
             "ms_per_step": round(el * 1e3 / args.steps, 3), "steps": args.steps, "warmup": args.warmup,
-            "loss": float(tr.loss.item()), "hipgraph": bool(tr._graphs) if generic else bool(args.graph),
+            "loss": float(tr.loss.item()), "hipgraph": bool(tr._graphs) if args.model != "sage" else bool(args.graph),
             "build_s": round(build_s, 1), "flow_caps": tr.flow.caps if gcn else None,
             "graph_gib_per_gpu": round((g.nbytes() + g.features.shard.numel() * 2) / 2 ** 30, 2),
             "config": {"model": args.model, "num_nodes": args.num_nodes, "batch_per_gpu": args.batch,
-                       "fanouts": None if gcn else args.fanouts, "conv": args.conv if args.model == "flow" else None, "layers": len(args.fanouts),
+                       "fanouts": None if gcn else args.fanouts, "conv": args.conv if args.model == "flow" else None,
+                       "negs": args.negs if unsup else None, "layers": len(args.fanouts),
                        "hidden": args.hidden, "feature_dim": args.feature_dim, "classes": args.classes},
             "data": "synthetic power-law graph generated in HBM, random features / labels"}), flush=True)
     if world > 1:

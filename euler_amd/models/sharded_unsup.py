@@ -25,6 +25,7 @@ import torch
 import torch.distributed as dist
 
 from euler_amd.models.sage_tower import UnsupSageTrainer
+from euler_amd.ops import mp_ops
 
 __all__ = ["ShardedUnsupSageTrainer"]
 
@@ -81,6 +82,25 @@ class ShardedUnsupSageTrainer(UnsupSageTrainer):
             out.append(pos[o:o + i.numel()].view_as(i))
             o += i.numel()
         return self.fshard.cache, out
+
+    def _tower_reference(self, W0, nodes, leaf, table=None):
+        """the towers' layer 0 + slot aggregation (UnsupSageTrainer._tower_reference) with
+        the tree's rows gathered first (``-1``: zeros) and only those converted to fp32 —
+        never the whole table (100M rows at one rank)"""
+        table = self.features if table is None else table
+        xs = mp_ops.gather(table, nodes.reshape(-1)).float()
+        agg = mp_ops.gather(table, leaf.reshape(-1)).float().view(leaf.shape[0], leaf.shape[1], -1).sum(1)
+        cnt = self.fanouts[1]
+        if self.include_self:
+            agg, cnt = agg + xs, cnt + 1
+        h0 = torch.relu(torch.cat([xs, agg / cnt], 1) @ W0.t())
+        P, f = 1 << self.logP, self.fanouts[0]
+        hg = h0.view(-1, P, h0.shape[1])
+        s, a = hg[:, f], hg[:, :f].sum(1)
+        c = f
+        if self.include_self:
+            a, c = a + s, c + 1
+        return torch.cat([s, a / c], 1)
 
     # ------------------------------------------------------------------ step
     def _forward_loss(self):
