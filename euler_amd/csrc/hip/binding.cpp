@@ -239,6 +239,22 @@ void relu_bwd_(torch::Tensor g, torch::Tensor y) {
 }
 
 // ----------------------------------------------------------------------------- message passing
+// out [n, D] fp32 = sum over f of x[idx[:, f]] (idx [n, F] int64; -1 entries skipped)
+torch::Tensor gather_sum(torch::Tensor x, torch::Tensor idx) {
+  need_cuda(x, "x");
+  need_i64(idx, "idx");
+  const bool bf = is_bf16(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && idx.dim() == 2 && idx.is_contiguous(),
+              "gather_sum: x [N, D] and idx [n, F] must be contiguous");
+  TORCH_CHECK((x.size(1) * x.element_size()) % 16 == 0, "gather_sum: rows must be a multiple of 16 bytes");
+  const c10::DeviceGuard g(x.device());
+  auto out = torch::empty({idx.size(0), x.size(1)}, x.options().dtype(torch::kFloat32));
+  check(eh_gather_sum(x.data_ptr(), bf, x.size(0), x.size(1) * x.element_size(), idx.data_ptr<int64_t>(), idx.size(0),
+                      static_cast<int>(idx.size(1)), out.data_ptr<float>(), cur_stream()),
+        "gather_sum");
+  return out;
+}
+
 torch::Tensor gather_rows(torch::Tensor x, torch::Tensor idx) {
   need_cuda(x, "x");
   need_cuda(idx, "idx");
@@ -602,6 +618,7 @@ PYBIND11_MODULE(_hip_ops, m) {
   m.def("sage_bwd_scatter", &sage_bwd_scatter);
   m.def("relu_bwd_", &relu_bwd_);
   m.def("gather_rows", &gather_rows);
+  m.def("gather_sum", &gather_sum);
   m.def("segment_reduce", &segment_reduce);
   m.def("segment_reduce_wave", &segment_reduce_wave, py::arg("src"), py::arg("indptr"), py::arg("perm"), py::arg("op"),
         py::arg("out") = py::none());

@@ -32,6 +32,8 @@ hipError_t eh_sage_bwd_scatter(const void* dA, int D, const int32_t* self_idx, c
 hipError_t eh_relu_bwd(void* g, const void* y, int64_t n, hipStream_t s);
 
 // mp.hip
+hipError_t eh_gather_sum(const void* x, int is_bf16, int64_t n_rows, int64_t row_bytes, const int64_t* idx, int64_t n,
+                         int F, float* out, hipStream_t s);
 hipError_t eh_gather_rows(const void* x, int64_t n_rows, int64_t row_bytes, const void* idx, int idx_is64, int64_t n,
                           void* out, hipStream_t s);
 hipError_t eh_segment_reduce_wave(const void* src, int is_bf16, int D, const int64_t* indptr, const int64_t* perm,

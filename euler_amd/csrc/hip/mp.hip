@@ -38,6 +38,45 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const uint8_t* __restr
   });
 }
 
+// out[e, :] = sum_f x[idx[e, f], :] in fp32 (idx < 0: skipped).  One thread per (row e,
+// 16-byte column chunk); the F row loads are issued 4 at a time before they are summed, in
+// f order (the same order as a gather followed by a sum over f).
+template <bool BF>
+__global__ __launch_bounds__(256) void gather_sum_kernel(const uint8_t* __restrict__ x, int64_t n_rows,
+                                                         int64_t row_bytes, const int64_t* __restrict__ idx,
+                                                         int64_t n, int F, float* __restrict__ out) {
+  constexpr int V = BF ? 8 : 4;  // columns per 16-byte chunk
+  const int64_t cpr = row_bytes / 16;
+  grid_stride(n * cpr, [&](int64_t t) {
+    const int64_t e = t / cpr, c = t - e * cpr;
+    const int64_t* ie = idx + e * F;
+    float acc[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) acc[v] = 0.f;
+    for (int f0 = 0; f0 < F; f0 += 4) {
+      uint4_t raw[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t r = f0 + u < F ? ie[f0 + u] : -1;
+        raw[u] = uint4_t{0u, 0u, 0u, 0u};
+        if (r >= 0 && r < n_rows) raw[u] = reinterpret_cast<const uint4_t*>(x + r * row_bytes)[c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if constexpr (BF) {
+          acc_bf16x8(acc, raw[u]);
+        } else {
+#pragma unroll
+          for (int v = 0; v < 4; ++v) acc[v] += __uint_as_float(raw[u][v]);
+        }
+      }
+    }
+    float4_t* o = reinterpret_cast<float4_t*>(out + e * (cpr * V) + c * V);
+    o[0] = float4_t{acc[0], acc[1], acc[2], acc[3]};
+    if constexpr (BF) o[1] = float4_t{acc[4], acc[5], acc[6], acc[7]};
+  });
+}
+
 template <typename T>
 __device__ __forceinline__ float ld(const T* p);
 template <>
@@ -464,6 +503,21 @@ hipError_t eh_gather_rows(const void* x, int64_t n_rows, int64_t row_bytes, cons
   return hipGetLastError();
 }
 
+
+hipError_t eh_gather_sum(const void* x, int is_bf16, int64_t n_rows, int64_t row_bytes, const int64_t* idx, int64_t n,
+                         int F, float* out, hipStream_t s) {
+  if (n == 0 || row_bytes == 0) return hipSuccess;
+  if (row_bytes % 16 != 0 || reinterpret_cast<uintptr_t>(x) % 16 != 0 || reinterpret_cast<uintptr_t>(out) % 16 != 0 ||
+      F < 0)
+    return hipErrorInvalidValue;
+  const dim3 grid = grid_for(n * (row_bytes / 16));
+  const uint8_t* xb = static_cast<const uint8_t*>(x);
+  if (is_bf16)
+    hipLaunchKernelGGL((gather_sum_kernel<true>), grid, dim3(256), 0, s, xb, n_rows, row_bytes, idx, n, F, out);
+  else
+    hipLaunchKernelGGL((gather_sum_kernel<false>), grid, dim3(256), 0, s, xb, n_rows, row_bytes, idx, n, F, out);
+  return hipGetLastError();
+}
 
 hipError_t eh_segment_reduce_wave(const void* src, int is_bf16, int D, const int64_t* indptr, const int64_t* perm,
                                   int64_t S, int op, void* out, hipStream_t s) {

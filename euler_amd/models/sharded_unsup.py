@@ -89,7 +89,7 @@ class ShardedUnsupSageTrainer(UnsupSageTrainer):
         never the whole table (100M rows at one rank)"""
         table = self.features if table is None else table
         xs = mp_ops.gather(table, nodes.reshape(-1)).float()
-        agg = mp_ops.gather(table, leaf.reshape(-1)).float().view(leaf.shape[0], leaf.shape[1], -1).sum(1)
+        agg = mp_ops.gather_sum(table, leaf.reshape(leaf.shape[0], -1))  # fp32, -1 leaves add nothing
         cnt = self.fanouts[1]
         if self.include_self:
             agg, cnt = agg + xs, cnt + 1

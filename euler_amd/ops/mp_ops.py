@@ -25,7 +25,7 @@ import torch
 
 from euler_amd.ops._native import hip, use_hip
 
-__all__ = ["SegmentIndex", "gather", "scatter_add", "scatter_mean", "scatter_max", "scatter_softmax",
+__all__ = ["SegmentIndex", "gather", "gather_sum", "scatter_add", "scatter_mean", "scatter_max", "scatter_softmax",
            "scatter_", "segment_index", "embedding_bag", "weighted_aggregate"]
 
 
@@ -173,6 +173,17 @@ def gather(params: torch.Tensor, indices: torch.Tensor) -> torch.Tensor:
     out = params[idx.clamp(min=0)]
     return torch.where(neg.reshape(tuple(idx.shape) + (1,) * (params.dim() - 1)), torch.zeros((), dtype=out.dtype),
                        out)
+
+
+def gather_sum(table: torch.Tensor, indices: torch.Tensor) -> torch.Tensor:
+    """``sum_f table[indices[:, f]]`` in fp32 [n, D] (``-1`` entries add nothing), no
+    gradient: the neighbour-sum of sampled rows without materialising the [n, F, D]
+    gather (``mp.hip gather_sum``: fp32 accumulation in f order, as a gather + sum)."""
+    idx = indices.reshape(indices.shape[0], -1)
+    if (use_hip(table, idx) and table.dim() == 2 and table.dtype in (torch.float32, torch.bfloat16)
+            and (table.shape[1] * table.element_size()) % 16 == 0):
+        return hip().gather_sum(table.contiguous(), idx.long().contiguous())
+    return gather(table, idx.long()).float().sum(1)
 
 
 # ----------------------------------------------------------------------------- scatter

@@ -393,3 +393,29 @@ def test_dna_single_key_attention_equals_matmul_form():
     s = restricted_softmax(Q @ K.transpose(-1, -2) / math.sqrt(ch), dim=-1)
     want = (s @ V).transpose(1, 2).reshape(E, -1, 16)
     torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-6)
+
+
+def test_gather_sum_cpu_matches_gather_then_sum():
+    from euler_amd.ops import mp_ops
+
+    g = torch.Generator().manual_seed(0)
+    table = torch.randn(50, 24, generator=g)
+    idx = torch.randint(-1, 50, (37, 7), generator=g)
+    ref = torch.where((idx >= 0).unsqueeze(-1), table[idx.clamp(min=0)], torch.zeros(())).sum(1)
+    assert torch.equal(mp_ops.gather_sum(table, idx), ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,D,F", [(torch.bfloat16, 128, 10), (torch.bfloat16, 64, 3), (torch.float32, 36, 25)])
+def test_gather_sum_gpu_matches_fp32_torch(cuda, dtype, D, F):
+    """mp.hip gather_sum (fp32 sums of table rows, -1 skipped) vs the fp32 torch reference"""
+    from euler_amd.ops import _native, mp_ops
+
+    assert _native.hip() is not None
+    g = torch.Generator().manual_seed(1)
+    table = torch.randn(1000, D, generator=g).to(dtype)
+    idx = torch.randint(-1, 1000, (4099, F), generator=g)
+    ref = torch.where((idx >= 0).unsqueeze(-1), table.float()[idx.clamp(min=0)], torch.zeros(())).sum(1)
+    out = mp_ops.gather_sum(table.to(cuda), idx.to(cuda))
+    assert out.dtype == torch.float32 and out.shape == (4099, D)
+    assert torch.allclose(out.cpu(), ref, atol=1e-5, rtol=1e-5)
