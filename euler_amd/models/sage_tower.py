@@ -37,6 +37,7 @@ import torch
 import torch.nn.functional as F
 
 from euler_amd.models._tower_ops import pair_loss, tower_head
+from euler_amd.ops import mp_ops
 from euler_amd.ops._native import hip
 from euler_amd.parallel.flat import FlatOptimizer, FlatParams
 from euler_amd.models.captured import new_graph
@@ -377,12 +378,11 @@ class UnsupSageTrainer:
     def _tower_reference(self, W0, nodes, leaf, table=None):
         """fp32 A1 rows of a tower from its sampled tree (oracle / CPU path); ``table``: the
         feature rows ``nodes`` / ``leaf`` index (default the trainer's feature table)"""
-        x = (self.features if table is None else table).float()
-        x = torch.cat([x, torch.zeros(1, x.shape[1], device=x.device)], 0)
-        n = x.shape[0] - 1
-        nodes, leaf = nodes.to(x.device).long(), leaf.to(x.device).long()
-        xs = x[torch.where(nodes < 0, torch.full_like(nodes, n), nodes)]
-        agg = x[torch.where(leaf < 0, torch.full_like(leaf, n), leaf)].sum(1)
+        tab = self.features if table is None else table
+        nodes, leaf = nodes.to(tab.device).long(), leaf.to(tab.device).long()
+        # the tree's rows first (-1: zero rows), then fp32: never the whole table in fp32
+        xs = mp_ops.gather(tab, nodes).float()
+        agg = mp_ops.gather(tab, leaf).float().sum(1)
         cnt = self.fanouts[1]
         if self.include_self:
             agg, cnt = agg + xs, cnt + 1

@@ -42,6 +42,7 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
+from euler_amd.ops import mp_ops
 from euler_amd.ops._native import hip
 from euler_amd.models.captured import new_graph
 
@@ -756,12 +757,11 @@ class SageTrainer:
     def logical_embed(self, params, nodes, leaf, table=None):
         """fp32 gnn embedding (``gnn.fc`` output) of one sampled slotted tree"""
         dev = params["gnn.fc.weight"].device
-        x = (self.features if table is None else table)[:, : self.D].float().to(dev)
-        x = torch.cat([x, torch.zeros(1, self.D, device=dev)], 0)
-        n = x.shape[0] - 1
-        nodes, leaf = nodes.to(dev), leaf.to(dev)
-        xs = x[torch.where(nodes < 0, torch.full_like(nodes, n), nodes)]
-        agg = x[torch.where(leaf < 0, torch.full_like(leaf, n), leaf)].sum(1)
+        tab = self.features if table is None else table
+        # the tree's rows are gathered first (-1: zero rows) and only they go to fp32: the
+        # whole table in fp32 would be 51 GB at 100M rows (device evaluate / infer)
+        xs = mp_ops.gather(tab, nodes.to(tab.device).long())[:, : self.D].float().to(dev)
+        agg = mp_ops.gather(tab, leaf.to(tab.device).long())[..., : self.D].float().to(dev).sum(1)
         cnt = self.fanouts[-1]
         if self.include_self:
             agg, cnt = agg + xs, cnt + 1
