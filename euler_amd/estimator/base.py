@@ -848,7 +848,7 @@ class BaseEstimator:
         return tr if callable(getattr(tr, "infer_logits", None)) or callable(getattr(tr, "infer_embed", None)) \
             else None
 
-    def _lockstep_batches(self, tr, batches, extract):
+    def _lockstep_batches(self, tr, batches, extract, first_only=False):
         """``(src, kwargs)`` per batch.  A trainer on a row-sharded graph answers inference
         collectively (``collective_infer``: every batch crosses the ranks' exchanges), so all
         ranks run the same number of batches of one padded size: the count is agreed over
@@ -864,7 +864,8 @@ class BaseEstimator:
             n = n.to(self.device) if dist.get_backend() == "nccl" else n
             dist.all_reduce(n, op=dist.ReduceOp.MAX)
         pad = int(self.params["batch_size"])
-        for i in range(int(n.item())):
+        count = min(int(n.item()), 1) if first_only else int(n.item())  # the same on every rank
+        for i in range(count):
             if i < len(srcs):
                 yield srcs[i], {"pad_to": pad}
             else:
@@ -881,7 +882,7 @@ class BaseEstimator:
         name = getattr(self.model, "metric_name", getattr(tr, "metric_name", "f1"))
         losses, res, steps, n, t0 = [], {}, 0, 0, time.time()
         extract = lambda b: self.get_evaluate_from_input(b, self.params)  # noqa: E731
-        for src, kw in self._lockstep_batches(tr, self._eval_batches(), extract):
+        for src, kw in self._lockstep_batches(tr, self._eval_batches(), extract, self.evaluate_stop_onetime):
             if src is None:  # a padding batch of the collective loop
                 tr.infer_logits(torch.zeros(0, dtype=torch.int64), **kw)
                 continue
