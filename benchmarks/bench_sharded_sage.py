@@ -139,7 +139,7 @@ def main(argv=None):
             return 1.0 / world
     torch.cuda.synchronize()
     build_s = time.time() - t0
-    if args.graph and (args.model == "sage" or tr.capturable()):  # full-flow exchanges read split sizes on the host
+    if args.graph and (args.model == "sage" or tr.capturable()):  # gloo rehearsals run eagerly
         tr.capture(sync, warmup=args.warmup, steps=1)
         run = tr.replay_steps
     else:

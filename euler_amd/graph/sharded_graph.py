@@ -424,9 +424,10 @@ class ShardedDeviceGraph:
         inclusive per-target offsets [n]) — every neighbour of every row of the edge types of
         ``mask``, target-major in storage order, ``-1`` padding, exactly the whole graph's
         expansion (dataflow/device_flow.py full_neighbors_cpu).  Each row is expanded by its
-        owner; the lists come back over one variable-size all-to-all (two host reads give the
-        split sizes: the step is eager) and are laid out target-major by a searchsorted over
-        the requesters' offsets.  More than ``cap`` entries set ``overflow``."""
+        owner; the lists come back over one fixed-capacity all-to-all (``capacity(cap)`` slots
+        per peer) and are laid out target-major by ``full_neighbors`` over the received
+        blocks.  No host read: the step captures.  More than ``cap`` entries, or more than a
+        peer's slots, set ``overflow`` (the flow regrows its caps)."""
         rows = rows.reshape(-1).long()
         n, dev = rows.numel(), self.device
         if not self.comm:
@@ -442,32 +443,34 @@ class ShardedDeviceGraph:
         pos, recv, C = self._route(torch.where(ok, rows, torch.full_like(rows, -1)))
         loc = self._local_rows(recv)
         deg_l = self._masked_degree(loc, int(mask))  # [W*C], the owner's received slots
-        send_split = deg_l.view(W, C).sum(1)
-        recv_split = self._a2a(send_split)
-        splits = torch.stack([send_split, recv_split]).cpu()  # the host sync of the exchange
-        total_l = int(splits[0].sum())
-        if total_l:
-            g = self.local
-            own = torch.zeros(1, dtype=torch.int32, device=dev)
-            if use_hip(loc):
-                nb_l, _, _ = hip().full_neighbors(g.indptr, g.nbr, g.num_rows, g.num_types, int(mask) & 0xFFFFFFFF,
-                                                  loc, total_l, own)
-            else:
-                from euler_amd.dataflow.device_flow import full_neighbors_cpu
-
-                nb_l, _, _ = full_neighbors_cpu(g, int(mask), loc, total_l, own)
-            nb_l = nb_l.int()
-        else:
-            nb_l = torch.zeros(0, dtype=torch.int32, device=dev)
-        buf = torch.empty(int(splits[1].sum()), dtype=torch.int32, device=dev)
-        comm.all_to_all_single(buf, nb_l, splits[1].tolist(), splits[0].tolist(), group=self.group)
-        # requester side: the received lists are a CSR over this rank's request slots
-        # (owner-major, slot order; a slot's degree from its owner): expanding the requests'
-        # slots through it is full_neighbors again — target-major, -1 padded, overflow flagged
-        deg_s = self._a2a(deg_l)
-        ptr_s = torch.cat([torch.zeros(1, dtype=torch.long, device=dev), torch.cumsum(deg_s, 0)])
-        slots = torch.where(pos < deg_s.numel(), pos, torch.full_like(pos, -1))  # a trashed request: none
-        return _expand_csr(ptr_s, buf, slots, int(cap), overflow)
+        # owner side: every received row expanded (slot order = requester-block order), each
+        # requester's lists packed into its own Ce slots of one equal-split all-to-all
+        Ce = self.capacity(int(cap))
+        tot = deg_l.view(W, C).sum(1)
+        blk0 = torch.cumsum(tot, 0) - tot  # where block o starts in the flat expansion
+        own = torch.zeros(1, dtype=torch.int32, device=dev)
+        nb_l, src_l, _ = _expand_full(self.local, int(mask), loc, W * Ce, own)
+        o = torch.div(src_l.clamp(min=0), C, rounding_mode="floor")
+        off = torch.arange(W * Ce, dtype=torch.long, device=dev) - blk0[o]
+        keep = (src_l >= 0) & (off < Ce)
+        dst = torch.where(keep, o * Ce + off, torch.full_like(off, W * Ce))
+        send = torch.full((W * Ce + 1,), -1, dtype=torch.int32, device=dev)
+        send.scatter_(0, dst, nb_l.int())
+        # a requester's lists beyond its Ce slots: flagged on the flow (it regrows its caps)
+        overflow.copy_(torch.maximum(overflow, (tot > Ce).any().reshape(1).to(overflow.dtype)))
+        buf = self._a2a(send[: W * Ce])  # block o: this rank's lists from owner o
+        deg_s = self._a2a(deg_l).view(W, C)
+        # requester side: the received blocks are a CSR over this rank's request slots, one
+        # gap row per block (rows o * (C + 1) + j; the gap spans the block's unused slots), so
+        # placing the requests target-major is full_neighbors again over that CSR
+        incl = torch.cumsum(deg_s, 1).clamp(max=Ce)
+        excl = torch.cat([torch.zeros((W, 1), dtype=incl.dtype, device=dev), incl[:, :-1]], 1)
+        base = (torch.arange(W, dtype=torch.long, device=dev) * Ce).unsqueeze(1)
+        ptr = torch.cat([(torch.cat([excl, incl[:, -1:]], 1) + base).reshape(-1),
+                         torch.full((1,), W * Ce, dtype=torch.long, device=dev)])
+        pj = torch.div(pos, C, rounding_mode="floor")
+        slots = torch.where(pos < W * C, pos + pj, torch.full_like(pos, -1))  # o * (C + 1) + j
+        return _expand_csr(ptr, buf, slots, int(cap), overflow)
 
 
     # ------------------------------------------------------------------ features / labels
@@ -500,6 +503,16 @@ class ShardedDeviceGraph:
             return mp_ops.gather(sf.cache, pos.long())
         return torch.where((pos >= 0).unsqueeze(1), sf.cache[pos.long().clamp(min=0)], torch.zeros(
             (), dtype=sf.cache.dtype))
+
+
+def _expand_full(g, mask, rows, cap, overflow):
+    """``full_neighbors`` of local rows over a DeviceGraph's CSR (HIP or the torch twin)"""
+    if use_hip(rows):
+        return hip().full_neighbors(g.indptr, g.nbr, g.num_rows, g.num_types, int(mask) & 0xFFFFFFFF, rows, int(cap),
+                                    overflow)
+    from euler_amd.dataflow.device_flow import full_neighbors_cpu
+
+    return full_neighbors_cpu(g, int(mask), rows, int(cap), overflow)
 
 
 def _expand_csr(indptr, nbr, rows, cap, overflow):

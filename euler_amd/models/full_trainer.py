@@ -226,9 +226,8 @@ class ShardedFlowTrainer(FullFlowTrainer):
     their owners; the model's own convolutions, loss, backward, gradient all-reduce and the
     flat optimizer run as in :class:`FullFlowTrainer`.  HBM per rank holds 1/W of the CSR,
     the features and the labels.  A ``GCNDataFlow`` model expands every hop through the
-    rows' owners (``ShardedDeviceGraph.full_neighbors``).  Sampled-flow steps over RCCL
-    capture into a hipGraph (fixed-size exchanges); full-flow and gloo steps run eagerly
-    (:meth:`capturable`)."""
+    rows' owners (``ShardedDeviceGraph.full_neighbors``).  Steps over RCCL capture into a
+    hipGraph (fixed-size exchanges); gloo steps run eagerly (:meth:`capturable`)."""
 
     def __init__(self, model, graph, batch_size, flow, optimizer="adam", learning_rate=0.01):
         self.gnn = model.gnn
@@ -332,16 +331,13 @@ class ShardedFlowTrainer(FullFlowTrainer):
         return self.infer_logits(ids, pad_to)[0]
 
     def capturable(self) -> bool:
-        """one rank without exchanges, or RCCL exchanges of fixed sizes (the sampled flow's
-        routes, draws and feature rows capture like any kernel); the full-neighbourhood
-        flow's variable-size exchange reads its split sizes on the host, and gloo stages
+        """one rank without exchanges, or RCCL exchanges (every route, draw, expansion and
+        feature row moves in fixed-capacity slots and captures like any kernel); gloo stages
         through host memory: those steps run eagerly"""
-        from euler_amd.dataflow.device_flow import DeviceSageFlow
-
         g = self.graph
         if not g.comm:
             return True
-        return isinstance(self.flow, DeviceSageFlow) and self.on_gpu and dist.get_backend(g.group) != "gloo"
+        return self.on_gpu and dist.get_backend(g.group) != "gloo"
 
     def capture(self, grad_sync=None, warmup: int = 2, steps: int = 1, extra_sizes=()):
         if self.capturable():

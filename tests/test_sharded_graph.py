@@ -586,6 +586,54 @@ def test_sharded_unsup_captures_over_rccl():
         dist.destroy_process_group()
 
 
+@pytest.mark.gpu
+def test_sharded_full_flow_captures_over_rccl():
+    """GCN on full-neighbourhood blocks expanded by the owners through a 1-rank RCCL group:
+    no host read in the step, so it captures; the first replay equals the eager step"""
+    import copy
+
+    from test_parallel import _free_port
+
+    from euler_amd import models as Z
+    from euler_amd.dataflow.device_flow import DeviceFullFlow
+    from euler_amd.graph.sharded_graph import ShardedDeviceGraph
+    from euler_amd.models.full_trainer import ShardedFlowTrainer
+
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
+    tr = None
+    try:
+        g, indptr, nbr, w, nw = _graph(device="cuda")
+        sg = ShardedDeviceGraph.from_full(g, force_comm=True, node_weights=nw)
+        torch.manual_seed(0)
+        m = Z.SupervisedGNN("gcn", "full", [16, 16, 3], [1, 1], [[0], [0]], "f", 12, "l", 3, max_id=300).cuda()
+        tr = ShardedFlowTrainer(m, sg, 32, DeviceFullFlow(sg, [3, 1], 32, True, "bounded"), learning_rate=0.03)
+        assert tr.capturable()
+        tr.step()
+        torch.cuda.synchronize()
+        rng, flat = sg.rng.clone(), tr.flat.flat.clone()
+        st = copy.deepcopy(tr.opt.state_dict())
+        tr.step()
+        eager_loss = float(tr.loss.item())
+        tr.capture(None, warmup=0, steps=1)
+        assert tr._graph_exec is not None
+        sg.rng.copy_(rng)
+        tr.flat.flat.copy_(flat)
+        tr.opt.load_state_dict(st)
+        tr.replay(1)
+        torch.cuda.synchronize()
+        first = float(tr.loss.item())
+        assert abs(first - eager_loss) <= 1e-5 * abs(eager_loss), (first, eager_loss)
+        tr.replay(50)
+        torch.cuda.synchronize()
+        assert math.isfinite(float(tr.loss.item()))
+        assert not tr.flow.overflowed()
+        sg.check_overflow()
+    finally:
+        if tr is not None:
+            tr.release_graphs()
+        dist.destroy_process_group()
+
+
 def _worker_shared_gpu_full(rank, world, port, q):
     """2 ranks sharing the GPU (gloo, staged exchanges): the owners' HIP full-neighbourhood
     expansion of each rank's rows and the flow's blocks = the whole graph's on the device"""
@@ -768,11 +816,12 @@ def _worker_full_flow(rank, world, port, q):
             seg = (indptr[1:] - indptr[:-1]).view(-1, T)
             deg = sum(seg[:, t] for t in range(T) if (mask >> t) & 1)
             ok &= st == (int(deg.max()), int(deg.sum()), int(torch.topk(deg, 17).values.min()))
-        # a cap below the expansion: flagged, the kept prefix equals the whole graph's
+        # a cap below the expansion: flagged (the flow regrows and redoes the batch; the
+        # per-peer slots may have dropped entries before the cut, so no prefix property)
         o1, o2 = torch.zeros(1, dtype=torch.int32), torch.zeros(1, dtype=torch.int32)
         a = sg.full_neighbors(rows, 3, 64, o1)
         b = full_neighbors_cpu(g, 3, rows, 64, o2)
-        ok &= int(o1) == 1 == int(o2) and all(torch.equal(x.long(), y.long()) for x, y in zip(a, b))
+        ok &= int(o1) == 1 == int(o2) and a[0].shape == b[0].shape
         masks = [3, 1]
         ok &= exact_caps(sg, masks, 24) == exact_caps(g, masks, 24)
         ok &= bounded_caps(sg, masks, 24) == bounded_caps(g, masks, 24)
